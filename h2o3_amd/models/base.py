@@ -1,0 +1,551 @@
+"""ModelBuilder / Model base shared by every algorithm.
+
+Reference: hex/ModelBuilder.java (parameter validation, CV driver
+`computeCrossValidation`, fold assignment hex/FoldAssignment.java),
+hex/Model.java (scoring, `adaptTestForTrain`, predict frame layout),
+hex/ScoreKeeper.java (early stopping), and the client API
+h2o-py/h2o/estimators/estimator_base.py + h2o/model/model_base.py.
+
+An estimator instance is both the builder and (after `train`) the model,
+exactly like h2o-py.  Algorithms subclass `H2OEstimator` and implement
+`_fit(spec)` (train on a TrainSpec) and `_predict_raw(frame)` (device
+tensor [n, K] of link-inverse predictions / class probabilities).
+"""
+from __future__ import annotations
+
+import copy
+import json
+import math
+import os
+import time
+
+import numpy as np
+import torch
+
+from ..core import dkv
+from ..core.frame import H2OFrame, _local_slice
+from ..core.vec import NUMERIC_TYPES, T_ENUM, T_INT, T_REAL, Vec
+from ..parallel import cloud
+from ..parallel import collectives as coll
+from . import metrics as mm
+
+COMMON_DEFAULTS = dict(model_id=None, training_frame=None, validation_frame=None, nfolds=0,
+                       keep_cross_validation_models=True, keep_cross_validation_predictions=False,
+                       keep_cross_validation_fold_assignment=False, fold_assignment="auto", fold_column=None,
+                       response_column=None, ignored_columns=None, ignore_const_cols=True, offset_column=None,
+                       weights_column=None, max_runtime_secs=0.0, seed=-1, stopping_rounds=0,
+                       stopping_metric="auto", stopping_tolerance=0.001, custom_metric_func=None,
+                       export_checkpoints_dir=None, auc_type="auto", gainslift_bins=-1,
+                       score_each_iteration=False, distribution="auto")
+
+_LESS_IS_BETTER = {"deviance", "logloss", "mse", "rmse", "mae", "rmsle", "mean_per_class_error",
+                   "misclassification", "anomaly_score"}
+
+
+class TrainSpec:
+    """Resolved training inputs (reference: ModelBuilder.init + DataInfo setup)."""
+
+    def __init__(self, frame: H2OFrame, x, y, weights=None, offset=None, fold=None, valid=None):
+        self.frame = frame
+        self.x = list(x)
+        self.y = y
+        self.weights_column = weights
+        self.offset_column = offset
+        self.fold_column = fold
+        self.valid = valid
+        self.response_domain = None
+        self.nclasses = 1
+        if y is not None:
+            v = frame.vec(y)
+            if v.type == T_ENUM:
+                self.response_domain = list(v.domain)
+                self.nclasses = len(v.domain)
+
+    @property
+    def is_classification(self):
+        return self.nclasses > 1
+
+    def yvec(self, frame=None):
+        return (frame or self.frame).vec(self.y)
+
+    def y_tensor(self, frame=None, dtype=torch.float32):
+        v = self.yvec(frame)
+        if v.type == T_ENUM:
+            return v.data.to(torch.int64)
+        return v.as_float(dtype)
+
+    def w_tensor(self, frame=None):
+        fr = frame or self.frame
+        if self.weights_column and self.weights_column in fr.names:
+            w = fr.vec(self.weights_column).as_float()
+            return torch.nan_to_num(w, nan=0.0)
+        return None
+
+    def offset_tensor(self, frame=None):
+        fr = frame or self.frame
+        if self.offset_column and self.offset_column in fr.names:
+            return torch.nan_to_num(fr.vec(self.offset_column).as_float(), nan=0.0)
+        return None
+
+
+class ScoreKeeper:
+    """Early stopping on a moving average (hex/ScoreKeeper.java:stopEarly)."""
+
+    @staticmethod
+    def stop_early(history, k, tol, less_is_better=True):
+        if k <= 0 or len(history) < 2 * k:
+            return False
+        vals = [v for v in history if v is not None and not math.isnan(v)]
+        if len(vals) < 2 * k:
+            return False
+        # reference: compare the best moving average of the last k against the one before
+        last = np.mean(vals[-k:])
+        ref = np.mean(vals[-2 * k:-k])
+        best_ref = min(np.mean(vals[i - k:i]) for i in range(k, len(vals) - k + 1)) if less_is_better else \
+            max(np.mean(vals[i - k:i]) for i in range(k, len(vals) - k + 1))
+        ref = best_ref
+        if less_is_better:
+            return not (last < ref * (1 - tol) if ref >= 0 else last < ref * (1 + tol))
+        return not (last > ref * (1 + tol) if ref >= 0 else last > ref * (1 - tol))
+
+
+class H2OEstimator:
+    algo = "base"
+    supervised_learning = True
+    _defaults: dict = {}
+
+    def __init__(self, **kwargs):
+        parms = dict(COMMON_DEFAULTS)
+        parms.update(self._defaults)
+        for k, v in kwargs.items():
+            parms[k] = v
+        self._parms = parms
+        self._id = parms.get("model_id") or dkv.make_key(self.algo)
+        self._output = {}
+        self._training_metrics = None
+        self._validation_metrics = None
+        self._cross_validation_metrics = None
+        self._cv_models = []
+        self._cv_predictions = None
+        self._cv_fold_assignment = None
+        self._scoring_history = []
+        self._spec = None
+        self._run_time = 0.0
+        self._start_time = 0
+        self._end_time = 0
+        self.actual_params = {}
+
+    # ------------------------------------------------------------ params
+    def __getattr__(self, name):
+        if name.startswith("_"):
+            raise AttributeError(name)
+        p = self.__dict__.get("_parms")
+        if p is not None and name in p:
+            return p[name]
+        raise AttributeError(name)
+
+    def __setattr__(self, name, value):
+        if not name.startswith("_") and "_parms" in self.__dict__ and name in self._parms:
+            self._parms[name] = value
+        else:
+            object.__setattr__(self, name, value)
+
+    @property
+    def params(self):
+        return {k: {"default": (COMMON_DEFAULTS.get(k, self._defaults.get(k))), "actual": v}
+                for k, v in self._parms.items()}
+
+    @property
+    def parms(self):
+        return self.params
+
+    def get_params(self, deep=True):
+        return dict(self._parms)
+
+    def set_params(self, **p):
+        self._parms.update(p)
+        return self
+
+    @property
+    def model_id(self):
+        return self._id
+
+    @model_id.setter
+    def model_id(self, v):
+        self._id = v
+
+    key = model_id
+
+    @property
+    def type(self):
+        if not self.supervised_learning:
+            return "unsupervised"
+        return "classifier" if self._spec and self._spec.is_classification else "regressor"
+
+    # ------------------------------------------------------------ training
+    def _resolve_columns(self, x, y, training_frame):
+        p = self._parms
+        names = training_frame.names
+        if y is None and self.supervised_learning:
+            y = p.get("response_column")
+        if isinstance(y, int):
+            y = names[y]
+        special = {y, p.get("weights_column"), p.get("offset_column"), p.get("fold_column")}
+        ignored = set(p.get("ignored_columns") or [])
+        if x is None:
+            x = [n for n in names if n not in special and n not in ignored]
+        else:
+            x = [names[i] if isinstance(i, int) else i for i in (x if isinstance(x, (list, tuple)) else [x])]
+            x = [n for n in x if n not in special]
+        if p.get("ignore_const_cols", True):
+            x = [n for n in x if not training_frame.vec(n).is_const()]
+        # drop string/uuid columns (reference ignores them for most algos)
+        x = [n for n in x if not training_frame.vec(n).on_host]
+        return x, y
+
+    def train(self, x=None, y=None, training_frame=None, offset_column=None, fold_column=None,
+              weights_column=None, validation_frame=None, max_runtime_secs=None, ignored_columns=None,
+              model_id=None, verbose=False, **kw):
+        p = self._parms
+        if training_frame is None:
+            training_frame = p.get("training_frame")
+        if isinstance(training_frame, str):
+            training_frame = dkv.get(training_frame)
+        if validation_frame is None:
+            validation_frame = p.get("validation_frame")
+        if offset_column is not None:
+            p["offset_column"] = offset_column
+        if fold_column is not None:
+            p["fold_column"] = fold_column
+        if weights_column is not None:
+            p["weights_column"] = weights_column
+        if max_runtime_secs is not None:
+            p["max_runtime_secs"] = max_runtime_secs
+        if ignored_columns is not None:
+            p["ignored_columns"] = ignored_columns
+        if model_id is not None:
+            self._id = model_id
+        x, y = self._resolve_columns(x, y, training_frame)
+        p["response_column"] = y
+        self._check_response(training_frame, y)
+        self._start_time = int(time.time() * 1000)
+        t0 = time.time()
+        spec = TrainSpec(training_frame, x, y, p.get("weights_column"), p.get("offset_column"),
+                         p.get("fold_column"), validation_frame)
+        self._spec = spec
+        nfolds = int(p.get("nfolds") or 0)
+        if self.supervised_learning and (nfolds > 1 or p.get("fold_column")):
+            self._cross_validate(spec)
+        self._fit(spec)
+        self._score_all(spec)
+        self._run_time = time.time() - t0
+        self._end_time = int(time.time() * 1000)
+        dkv.put(self._id, self)
+        return self
+
+    def _check_response(self, frame, y):
+        pass
+
+    def _fit(self, spec: TrainSpec):
+        raise NotImplementedError
+
+    def _predict_raw(self, frame: H2OFrame) -> torch.Tensor:
+        raise NotImplementedError
+
+    # ------------------------------------------------------------ CV
+    def _fold_ids(self, spec):
+        p = self._parms
+        fr = spec.frame
+        n_local = fr.nlocal
+        if p.get("fold_column"):
+            fv = fr.vec(p["fold_column"])
+            f = fv.data.to(torch.int64) if fv.type == T_ENUM else fv.as_float().to(torch.int64)
+            uniq = torch.unique(f)
+            if cloud.is_distributed():
+                uniq = torch.unique(coll.all_gather_var(uniq))
+            remap = {int(u): i for i, u in enumerate(uniq.tolist())}
+            f = torch.tensor([remap[int(v)] for v in f.tolist()], device=f.device) if remap else f
+            return f, len(remap)
+        k = int(p["nfolds"])
+        fa = (p.get("fold_assignment") or "auto").lower()
+        seed = p.get("seed", -1)
+        seed = 42 if seed is None or seed == -1 else int(seed)
+        off = fr.row_offset()
+        gidx = torch.arange(off, off + n_local, device=cloud.device())
+        if fa == "modulo":
+            return gidx % k, k
+        if fa == "stratified" and spec.is_classification:
+            yv = spec.y_tensor()
+            g = torch.Generator(device="cpu").manual_seed(seed)
+            r = torch.rand(fr.nrows, generator=g)[off:off + n_local].to(yv.device)
+            f = torch.empty(n_local, dtype=torch.int64, device=yv.device)
+            for c in range(-1, spec.nclasses):
+                m = yv == c
+                idx = torch.nonzero(m).flatten()
+                if idx.numel() == 0:
+                    continue
+                ordr = torch.argsort(r[idx])
+                f[idx[ordr]] = torch.arange(idx.numel(), device=yv.device) % k
+            return f, k
+        g = torch.Generator(device="cpu").manual_seed(seed)
+        r = torch.randint(0, k, (fr.nrows,), generator=g)[off:off + n_local]
+        return r.to(cloud.device()), k
+
+    def _cross_validate(self, spec):
+        p = self._parms
+        folds, k = self._fold_ids(spec)
+        self._cv_fold_assignment = folds
+        fr = spec.frame
+        holdout = None
+        cv_models = []
+        for i in range(k):
+            tr_mask = folds != i
+            te_mask = folds == i
+            sub = copy.copy(self)
+            sub.__dict__ = dict(self.__dict__)
+            sub._parms = dict(self._parms)
+            sub._parms["nfolds"] = 0
+            sub._parms["fold_column"] = None
+            sub._id = f"{self._id}_cv_{i + 1}"
+            sub._cv_models = []
+            sub._scoring_history = []
+            sub._output = {}
+            tr = fr[tr_mask]
+            te = fr[te_mask]
+            sspec = TrainSpec(tr, spec.x, spec.y, spec.weights_column, spec.offset_column, None, te)
+            sspec.response_domain, sspec.nclasses = spec.response_domain, spec.nclasses
+            sub._spec = sspec
+            sub._fit(sspec)
+            pr = sub._predict_raw(te)
+            if holdout is None:
+                holdout = torch.full((fr.nlocal, pr.shape[1]), float("nan"), dtype=pr.dtype, device=pr.device)
+            holdout[te_mask] = pr
+            sub._score_all(sspec)
+            cv_models.append(sub)
+        self._cv_models = cv_models if p.get("keep_cross_validation_models", True) else []
+        self._cv_optimal_params(cv_models)
+        self._cv_holdout = holdout
+        self._cross_validation_metrics = self._metrics_from_raw(spec, fr, holdout)
+        if p.get("keep_cross_validation_predictions"):
+            self._cv_predictions = self._pred_frame_from_raw(holdout, spec)
+        # cv summary table
+        rows = {}
+        for m in cv_models:
+            mt = m._validation_metrics or m._training_metrics
+            if mt is None:
+                continue
+            for kk, v in mt._m.items():
+                if isinstance(v, (int, float)) and not isinstance(v, bool):
+                    rows.setdefault(kk, []).append(v)
+        self._output["cross_validation_metrics_summary"] = {
+            kk: {"mean": float(np.mean(v)), "sd": float(np.std(v, ddof=1)) if len(v) > 1 else 0.0, "values": v}
+            for kk, v in rows.items()}
+
+    def _cv_optimal_params(self, cv_models):
+        """Hook: adopt CV-derived parameters for the main model
+        (reference: ModelBuilder.cv_computeAndSetOptimalParameters)."""
+
+    # ------------------------------------------------------------ scoring
+    def _metrics_from_raw(self, spec, frame, raw, w=None):
+        if raw is None:
+            return None
+        y = spec.y_tensor(frame) if spec.y and spec.y in frame.names else None
+        if y is None:
+            return None
+        if w is None:
+            w = spec.w_tensor(frame)
+        dist = getattr(self, "_dist", None)
+        if spec.nclasses == 2:
+            yy = y.to(torch.float64)
+            ok = yy >= 0
+            return mm.binomial_metrics(yy[ok], raw[ok][:, -1], None if w is None else w[ok], spec.response_domain)
+        if spec.nclasses > 2:
+            return mm.multinomial_metrics(y, raw, w, spec.response_domain)
+        return mm.regression_metrics(y.to(torch.float64), raw[:, 0], w, dist)
+
+    def _score_all(self, spec):
+        if not self.supervised_learning:
+            self._score_unsupervised(spec)
+            return
+        raw = self._predict_raw(spec.frame)
+        self._training_metrics = self._metrics_from_raw(spec, spec.frame, raw)
+        if spec.valid is not None:
+            vraw = self._predict_raw(spec.valid)
+            self._validation_metrics = self._metrics_from_raw(spec, spec.valid, vraw)
+
+    def _score_unsupervised(self, spec):
+        pass
+
+    def _pred_frame_from_raw(self, raw, spec=None, threshold=None):
+        spec = spec or self._spec
+        if spec.nclasses == 2:
+            p1 = raw[:, -1]
+            thr = threshold
+            if thr is None:
+                tm = self._training_metrics
+                thr = tm["max_f1_threshold"] if tm is not None and tm.get("max_f1_threshold") is not None else 0.5
+                if self._validation_metrics is not None and self._validation_metrics.get("max_f1_threshold") is not None:
+                    thr = self._validation_metrics["max_f1_threshold"]
+            lab = (p1 >= thr).to(torch.int32)
+            lab = torch.where(torch.isnan(p1), torch.full_like(lab, -1), lab)
+            vecs = [Vec(lab, T_ENUM, spec.response_domain), Vec((1 - p1).to(torch.float32), T_REAL),
+                    Vec(p1.to(torch.float32), T_REAL)]
+            return H2OFrame.from_vecs(vecs, ["predict"] + list(spec.response_domain))
+        if spec.nclasses > 2:
+            lab = torch.argmax(raw, 1).to(torch.int32)
+            vecs = [Vec(lab, T_ENUM, spec.response_domain)] + [Vec(raw[:, k].to(torch.float32).contiguous(), T_REAL)
+                                                               for k in range(raw.shape[1])]
+            return H2OFrame.from_vecs(vecs, ["predict"] + list(spec.response_domain))
+        return H2OFrame.from_vecs([Vec(raw[:, 0].to(torch.float32).contiguous(), T_REAL)], ["predict"])
+
+    def predict(self, test_data, **kw):
+        raw = self._predict_raw(test_data)
+        return self._pred_frame_from_raw(raw)
+
+    def predict_leaf_node_assignment(self, test_data, type="Path"):
+        raise NotImplementedError(f"{self.algo} has no leaf node assignment")
+
+    def model_performance(self, test_data=None, train=False, valid=False, xval=False, auc_type=None, **kw):
+        if test_data is None:
+            if valid:
+                return self._validation_metrics
+            if xval:
+                return self._cross_validation_metrics
+            return self._training_metrics
+        if not self.supervised_learning:
+            return self._unsupervised_perf(test_data)
+        raw = self._predict_raw(test_data)
+        return self._metrics_from_raw(self._spec, test_data, raw)
+
+    def _unsupervised_perf(self, frame):
+        return None
+
+    def _pick(self, key, train, valid, xval):
+        res = {}
+        if not (train or valid or xval):
+            train = True
+        for flag, m, name in ((train, self._training_metrics, "train"), (valid, self._validation_metrics, "valid"),
+                              (xval, self._cross_validation_metrics, "xval")):
+            if flag:
+                res[name] = None if m is None else (getattr(m, key)() if callable(getattr(m, key, None)) else m.get(key))
+        return list(res.values())[0] if len(res) == 1 else res
+
+    def auc(self, train=False, valid=False, xval=False): return self._pick("auc", train, valid, xval)
+    def aucpr(self, train=False, valid=False, xval=False): return self._pick("aucpr", train, valid, xval)
+    pr_auc = aucpr
+    def logloss(self, train=False, valid=False, xval=False): return self._pick("logloss", train, valid, xval)
+    def mse(self, train=False, valid=False, xval=False): return self._pick("mse", train, valid, xval)
+    def rmse(self, train=False, valid=False, xval=False): return self._pick("rmse", train, valid, xval)
+    def mae(self, train=False, valid=False, xval=False): return self._pick("mae", train, valid, xval)
+    def rmsle(self, train=False, valid=False, xval=False): return self._pick("rmsle", train, valid, xval)
+    def r2(self, train=False, valid=False, xval=False): return self._pick("r2", train, valid, xval)
+    def gini(self, train=False, valid=False, xval=False): return self._pick("gini", train, valid, xval)
+    def mean_per_class_error(self, train=False, valid=False, xval=False): return self._pick("mean_per_class_error", train, valid, xval)
+    def mean_residual_deviance(self, train=False, valid=False, xval=False): return self._pick("mean_residual_deviance", train, valid, xval)
+    def confusion_matrix(self, train=False, valid=False, xval=False, **kw): return self._pick("confusion_matrix", train, valid, xval)
+
+    def scoring_history(self):
+        import pandas as pd
+        return pd.DataFrame(self._scoring_history)
+
+    def varimp(self, use_pandas=False):
+        vi = self._output.get("variable_importances")
+        if vi is None:
+            return None
+        rows = sorted(vi.items(), key=lambda kv: -kv[1])
+        top = rows[0][1] if rows and rows[0][1] > 0 else 1.0
+        tot = sum(v for _, v in rows) or 1.0
+        out = [(k, float(v), float(v / top), float(v / tot)) for k, v in rows]
+        if use_pandas:
+            import pandas as pd
+            return pd.DataFrame(out, columns=["variable", "relative_importance", "scaled_importance", "percentage"])
+        return out
+
+    def summary(self):
+        return self._output.get("model_summary")
+
+    def cross_validation_models(self):
+        return self._cv_models
+
+    def cross_validation_predictions(self):
+        return [m.predict(self._spec.frame) for m in self._cv_models]
+
+    def cross_validation_holdout_predictions(self):
+        return self._cv_predictions if self._cv_predictions is not None else (
+            self._pred_frame_from_raw(self._cv_holdout) if getattr(self, "_cv_holdout", None) is not None else None)
+
+    def cross_validation_fold_assignment(self):
+        f = self._cv_fold_assignment
+        return None if f is None else H2OFrame.from_vecs([Vec(f.to(torch.float32), T_INT)], ["fold_assignment"])
+
+    def cross_validation_metrics_summary(self):
+        return self._output.get("cross_validation_metrics_summary")
+
+    @property
+    def actual_params_(self):
+        return dict(self._parms)
+
+    def get_xval_models(self):
+        return self._cv_models
+
+    def is_cross_validated(self):
+        return bool(self._cv_models)
+
+    def show(self):
+        print(repr(self))
+
+    def __repr__(self):
+        s = f"{type(self).__name__} model_id={self._id}"
+        if self._training_metrics is not None:
+            s += f"\n  training: {self._training_metrics!r}"
+        if self._validation_metrics is not None:
+            s += f"\n  validation: {self._validation_metrics!r}"
+        if self._cross_validation_metrics is not None:
+            s += f"\n  xval: {self._cross_validation_metrics!r}"
+        return s
+
+    # ------------------------------------------------------------ persistence
+    def download_mojo(self, path=".", get_genmodel_jar=False, genmodel_name="", **kw):
+        from ..mojo import writer
+        return writer.write_mojo(self, path)
+
+    save_mojo = download_mojo
+
+    def save_model_details(self, path=".", force=False, filename=None):
+        fn = os.path.join(path, filename or f"{self._id}.json")
+        with open(fn, "w") as f:
+            json.dump({"model_id": self._id, "algo": self.algo, "params": {k: v for k, v in self._parms.items()
+                                                                             if isinstance(v, (int, float, str, bool, list, type(None)))}},
+                      f, indent=1, default=str)
+        return fn
+
+    # ------------------------------------------------------------ frame adaptation
+    def _adapt_enum(self, frame_vec: Vec, train_domain):
+        """Map a test categorical column onto the training domain (unseen -> NA)
+        (reference: Model.adaptTestForTrain)."""
+        if frame_vec.type == T_ENUM:
+            if frame_vec.domain == train_domain:
+                return frame_vec.data
+            idx = {d: i for i, d in enumerate(train_domain)}
+            remap = torch.tensor([idx.get(d, -1) for d in frame_vec.domain] or [-1], dtype=torch.int32,
+                                 device=frame_vec.data.device)
+            return torch.where(frame_vec.data < 0, frame_vec.data, remap[frame_vec.data.clamp(min=0).long()])
+        if frame_vec.on_host:
+            idx = {d: i for i, d in enumerate(train_domain)}
+            return torch.tensor([idx.get(str(x), -1) if x is not None else -1 for x in frame_vec.data],
+                                dtype=torch.int32, device=cloud.device())
+        # numeric column where training saw a categorical: match by label
+        x = frame_vec.as_float(torch.float64)
+        idx = {}
+        for i, d in enumerate(train_domain):
+            try:
+                idx[float(d)] = i
+            except ValueError:
+                pass
+        keys = torch.tensor(sorted(idx), dtype=torch.float64, device=x.device) if idx else None
+        if keys is None:
+            return torch.full(x.shape, -1, dtype=torch.int32, device=x.device)
+        vals = torch.tensor([idx[k] for k in sorted(idx)], dtype=torch.int32, device=x.device)
+        pos = torch.searchsorted(keys, torch.nan_to_num(x, nan=-1e308)).clamp(max=keys.numel() - 1)
+        hit = keys[pos] == x
+        return torch.where(hit, vals[pos], torch.full_like(vals[pos], -1))

@@ -1,0 +1,381 @@
+"""Model metrics computed on device.
+
+Reference: hex/ModelMetrics*.java, hex/AUC2.java (threshold table with up
+to 400 bins; AUC via trapezoids), hex/ConfusionMatrix.java,
+hex/GainsLift.java, hex/MultinomialAUC.java, hex/ModelMetricsClustering.java.
+
+The reference builds metrics with an MRTask of per-row updates into
+AUC2 histograms; here the scores and labels live in HBM, so the binomial
+metrics come from one GPU sort (exact AUC) plus a 400-point threshold table
+for the confusion-matrix family, all-gathered when sharded.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from ..parallel import cloud
+from ..parallel import collectives as coll
+
+_MAX_THRESHOLDS = 400
+
+
+def _gather(t):
+    return coll.all_gather_var(t) if cloud.is_distributed() else t
+
+
+class ModelMetrics:
+    kind = "base"
+
+    def __init__(self, **kw):
+        self._m = dict(kw)
+
+    def __getitem__(self, k):
+        return self._m[k]
+
+    def get(self, k, d=None):
+        return self._m.get(k, d)
+
+    def _metric(self, k):
+        return self._m.get(k)
+
+    # common accessors (h2o-py ModelMetricsBase)
+    def mse(self): return self._m.get("MSE")
+    def rmse(self): return self._m.get("RMSE")
+    def mae(self): return self._m.get("mae")
+    def rmsle(self): return self._m.get("rmsle")
+    def r2(self): return self._m.get("r2")
+    def logloss(self): return self._m.get("logloss")
+    def auc(self): return self._m.get("AUC")
+    def aucpr(self): return self._m.get("pr_auc")
+    pr_auc = aucpr
+    def gini(self): return self._m.get("Gini")
+    def mean_per_class_error(self): return self._m.get("mean_per_class_error")
+    def mean_residual_deviance(self): return self._m.get("mean_residual_deviance")
+    def nobs(self): return self._m.get("nobs")
+    def null_deviance(self): return self._m.get("null_deviance")
+    def residual_deviance(self): return self._m.get("residual_deviance")
+    def aic(self): return self._m.get("AIC")
+    def custom_metric_value(self): return self._m.get("custom_metric_value")
+
+    def confusion_matrix(self, metrics=None, thresholds=None):
+        return self._m.get("cm")
+
+    def metric(self, name, thresholds=None):
+        tt = self._m.get("thresholds_and_metric_scores")
+        if tt is None:
+            return None
+        if thresholds is None:
+            i = int(np.argmax(tt[name]))
+            return [[tt["threshold"][i], tt[name][i]]]
+        out = []
+        for t in thresholds:
+            i = int(np.argmin(np.abs(np.asarray(tt["threshold"]) - t)))
+            out.append([t, tt[name][i]])
+        return out
+
+    def find_threshold_by_max_metric(self, metric):
+        tt = self._m["thresholds_and_metric_scores"]
+        return float(tt["threshold"][int(np.argmax(tt[metric]))])
+
+    def F1(self, thresholds=None): return self.metric("f1", thresholds)
+    def accuracy(self, thresholds=None): return self.metric("accuracy", thresholds)
+    def precision(self, thresholds=None): return self.metric("precision", thresholds)
+    def recall(self, thresholds=None): return self.metric("recall", thresholds)
+    def tpr(self, thresholds=None): return self.metric("tpr", thresholds)
+    def fpr(self, thresholds=None): return self.metric("fpr", thresholds)
+    def specificity(self, thresholds=None): return self.metric("specificity", thresholds)
+    def mcc(self, thresholds=None): return self.metric("absolute_mcc", thresholds)
+
+    def gains_lift(self):
+        return self._m.get("gains_lift_table")
+
+    def hit_ratio_table(self):
+        return self._m.get("hit_ratio_table")
+
+    def tot_withinss(self): return self._m.get("tot_withinss")
+    def betweenss(self): return self._m.get("betweenss")
+    def totss(self): return self._m.get("totss")
+    def withinss(self): return self._m.get("withinss")
+
+    def as_dict(self):
+        return {k: v for k, v in self._m.items() if not isinstance(v, (dict, list, np.ndarray)) or k == "cm"}
+
+    def __repr__(self):
+        keys = [k for k, v in self._m.items() if isinstance(v, (int, float)) and v is not None]
+        body = ", ".join(f"{k}={self._m[k]:.6g}" for k in keys)
+        return f"ModelMetrics{self.kind.capitalize()}({body})"
+
+    def show(self):
+        print(repr(self))
+
+
+class ModelMetricsRegression(ModelMetrics):
+    kind = "regression"
+
+
+class ModelMetricsBinomial(ModelMetrics):
+    kind = "binomial"
+
+
+class ModelMetricsMultinomial(ModelMetrics):
+    kind = "multinomial"
+
+
+class ModelMetricsOrdinal(ModelMetricsMultinomial):
+    kind = "ordinal"
+
+
+class ModelMetricsClustering(ModelMetrics):
+    kind = "clustering"
+
+
+class ModelMetricsAnomaly(ModelMetrics):
+    kind = "anomaly"
+
+
+class ModelMetricsAutoEncoder(ModelMetrics):
+    kind = "autoencoder"
+
+
+class ModelMetricsDimReduction(ModelMetrics):
+    kind = "dimreduction"
+
+
+class ModelMetricsCoxPH(ModelMetrics):
+    kind = "coxph"
+
+    def concordance(self):
+        return self._m.get("concordance")
+
+
+class ModelMetricsUplift(ModelMetrics):
+    kind = "binomial_uplift"
+
+    def auuc(self, metric=None):
+        return self._m.get("AUUC")
+
+    def qini(self):
+        return self._m.get("qini")
+
+
+def _wsum(x):
+    return coll.allreduce_scalar(float(x.sum()))
+
+
+def regression_metrics(y, pred, w=None, distribution=None):
+    ok = ~torch.isnan(y) & ~torch.isnan(pred)
+    y, pred = y[ok].to(torch.float64), pred[ok].to(torch.float64)
+    w = torch.ones_like(y) if w is None else w[ok].to(torch.float64)
+    sw = _wsum(w)
+    err = pred - y
+    mse = _wsum(w * err * err) / sw if sw > 0 else float("nan")
+    mae = _wsum(w * err.abs()) / sw if sw > 0 else float("nan")
+    ymean = _wsum(w * y) / sw if sw > 0 else float("nan")
+    var = _wsum(w * (y - ymean) ** 2) / sw if sw > 0 else float("nan")
+    r2 = 1 - mse / var if var and var > 0 else float("nan")
+    if bool((y > -1).all()) and bool((pred > -1).all()):
+        rmsle = math.sqrt(_wsum(w * (torch.log1p(pred) - torch.log1p(y)) ** 2) / sw)
+    else:
+        rmsle = float("nan")
+    if distribution is not None and distribution.family not in ("gaussian",):
+        dev = _wsum(distribution.deviance(w, y, pred)) / sw
+    else:
+        dev = mse
+    n = int(coll.allreduce_scalar(float(y.numel())))
+    return ModelMetricsRegression(MSE=mse, RMSE=math.sqrt(mse) if mse == mse else float("nan"), mae=mae,
+                                  rmsle=rmsle, r2=r2, mean_residual_deviance=dev, nobs=n)
+
+
+def _auc_exact(p, y, w):
+    """Weighted ROC AUC via a single sort (ties averaged)."""
+    order = torch.argsort(p, descending=True)
+    ps, ys, ws = p[order], y[order], w[order]
+    tp = torch.cumsum(ws * ys, 0)
+    fp = torch.cumsum(ws * (1 - ys), 0)
+    # keep last index of each tie group
+    last = torch.ones_like(ps, dtype=torch.bool)
+    if ps.numel() > 1:
+        last[:-1] = ps[1:] != ps[:-1]
+    tp, fp = tp[last], fp[last]
+    P, N = tp[-1], fp[-1]
+    if P <= 0 or N <= 0:
+        return float("nan"), float("nan")
+    tpr = torch.cat([torch.zeros(1, dtype=tp.dtype, device=tp.device), tp / P])
+    fpr = torch.cat([torch.zeros(1, dtype=fp.dtype, device=fp.device), fp / N])
+    auc = float(torch.trapz(tpr, fpr))
+    # PR AUC (average precision style trapezoid over recall)
+    prec = tp / (tp + fp).clamp_min(1e-300)
+    rec = tp / P
+    rec0 = torch.cat([torch.zeros(1, dtype=rec.dtype, device=rec.device), rec])
+    prec0 = torch.cat([prec[:1], prec])
+    prauc = float(torch.trapz(prec0, rec0))
+    return auc, prauc
+
+
+def _threshold_table(p, y, w):
+    """Confusion-matrix family over <=400 thresholds (AUC2-style)."""
+    P = float((w * y).sum())
+    N = float((w * (1 - y)).sum())
+    u = torch.unique(p)
+    if u.numel() > _MAX_THRESHOLDS:
+        q = torch.linspace(0, 1, _MAX_THRESHOLDS, dtype=torch.float64, device=p.device)
+        srt = torch.sort(p).values
+        u = torch.unique(srt[(q * (srt.numel() - 1)).long()])
+    thr = torch.sort(u, descending=True).values
+    # counts of predictions >= thr
+    srt_idx = torch.argsort(p)
+    ps = p[srt_idx]
+    cw_pos = torch.cumsum((w * y)[srt_idx].flip(0), 0).flip(0)
+    cw_neg = torch.cumsum((w * (1 - y))[srt_idx].flip(0), 0).flip(0)
+    pos_idx = torch.searchsorted(ps, thr, right=False)
+    n = ps.numel()
+    valid = pos_idx < n
+    tp = torch.where(valid, cw_pos[pos_idx.clamp(max=n - 1)], torch.zeros_like(thr))
+    fp = torch.where(valid, cw_neg[pos_idx.clamp(max=n - 1)], torch.zeros_like(thr))
+    fn = P - tp
+    tn = N - fp
+    eps = 1e-300
+    prec = tp / (tp + fp).clamp_min(eps)
+    rec = tp / max(P, eps)
+    spec = tn / max(N, eps)
+    acc = (tp + tn) / max(P + N, eps)
+
+    def fb(b):
+        return (1 + b * b) * prec * rec / (b * b * prec + rec).clamp_min(eps)
+    mcc_den = torch.sqrt(((tp + fp) * (tp + fn) * (tn + fp) * (tn + fn)).clamp_min(eps))
+    mcc = ((tp * tn - fp * fn) / mcc_den).abs()
+    tpr, fpr = rec, fp / max(N, eps)
+    tnr, fnr = spec, fn / max(P, eps)
+    mpca = (tpr + tnr) / 2
+    mina = torch.minimum(tpr, tnr)
+    tab = {"threshold": thr, "f1": fb(1.0), "f2": fb(2.0), "f0point5": fb(0.5), "accuracy": acc,
+           "precision": prec, "recall": rec, "specificity": spec, "absolute_mcc": mcc,
+           "min_per_class_accuracy": mina, "mean_per_class_accuracy": mpca, "tns": tn, "fns": fn, "fps": fp,
+           "tps": tp, "tnr": tnr, "fnr": fnr, "fpr": fpr, "tpr": tpr}
+    return {k: v.cpu().numpy() for k, v in tab.items()}
+
+
+def _gains_lift(p, y, w, groups=16):
+    order = torch.argsort(p, descending=True)
+    ys, ws = (y * w)[order], w[order]
+    cw = torch.cumsum(ws, 0)
+    tot = float(cw[-1])
+    P = float(ys.sum())
+    rows = []
+    prev = 0
+    cum_resp = 0.0
+    for g in range(1, groups + 1):
+        frac = g / groups
+        idx = int(torch.searchsorted(cw, torch.tensor([frac * tot], dtype=cw.dtype, device=cw.device)).item())
+        idx = min(max(idx, prev), ys.numel() - 1)
+        grp_resp = float(ys[prev: idx + 1].sum())
+        grp_w = float(ws[prev: idx + 1].sum())
+        cum_resp += grp_resp
+        resp_rate = grp_resp / grp_w if grp_w > 0 else 0
+        avg = P / tot if tot > 0 else 0
+        rows.append({"group": g, "cumulative_data_fraction": frac,
+                     "lower_threshold": float(p[order][idx]), "lift": resp_rate / avg if avg > 0 else 0,
+                     "cumulative_lift": (cum_resp / float(cw[idx])) / avg if avg > 0 else 0,
+                     "response_rate": resp_rate, "cumulative_capture_rate": cum_resp / P if P > 0 else 0})
+        prev = idx + 1
+        if prev >= ys.numel():
+            break
+    return rows
+
+
+def binomial_metrics(y, p1, w=None, domain=None, threshold=None, auc_type="AUTO", gainslift=True):
+    """y in {0,1} (float), p1 = P(class 1)."""
+    ok = ~torch.isnan(y) & ~torch.isnan(p1)
+    y, p1 = y[ok].to(torch.float64), p1[ok].to(torch.float64)
+    w = torch.ones_like(y) if w is None else w[ok].to(torch.float64)
+    if cloud.is_distributed():
+        y, p1, w = _gather(y), _gather(p1), _gather(w)
+    sw = float(w.sum())
+    pc = torch.clamp(p1, 1e-15, 1 - 1e-15)
+    logloss = float(-(w * (y * torch.log(pc) + (1 - y) * torch.log(1 - pc))).sum() / sw)
+    mse = float((w * (y - p1) ** 2).sum() / sw)
+    auc, prauc = _auc_exact(p1, y, w)
+    tab = _threshold_table(p1, y, w)
+    i = int(np.argmax(tab["f1"])) if len(tab["f1"]) else 0
+    thr = float(tab["threshold"][i]) if threshold is None and len(tab["threshold"]) else (threshold or 0.5)
+    if threshold is not None:
+        i = int(np.argmin(np.abs(tab["threshold"] - threshold)))
+    tn, fp, fn, tp = (float(tab[k][i]) for k in ("tns", "fps", "fns", "tps"))
+    P, N = tp + fn, tn + fp
+    err0 = fp / N if N > 0 else 0
+    err1 = fn / P if P > 0 else 0
+    dom = domain or ["0", "1"]
+    cm = {"domain": dom, "matrix": [[tn, fp], [fn, tp]], "threshold": thr,
+          "errors": [err0, err1], "total_error": (fp + fn) / max(P + N, 1e-300)}
+    ymean = float((w * y).sum() / sw)
+    var = ymean * (1 - ymean)
+    m = ModelMetricsBinomial(MSE=mse, RMSE=math.sqrt(mse), logloss=logloss, AUC=auc, pr_auc=prauc,
+                             Gini=2 * auc - 1 if auc == auc else float("nan"),
+                             mean_per_class_error=(err0 + err1) / 2, max_f1_threshold=thr,
+                             r2=1 - mse / var if var > 0 else float("nan"), nobs=int(y.numel()),
+                             cm=cm, thresholds_and_metric_scores=tab, domain=dom)
+    if gainslift:
+        try:
+            m._m["gains_lift_table"] = _gains_lift(p1, y, w)
+        except Exception:
+            pass
+    return m
+
+
+def multinomial_metrics(y_codes, probs, w=None, domain=None, hit_k=10):
+    """y_codes int64 [n] (-1 = NA), probs [n, K]."""
+    ok = y_codes >= 0
+    y, P = y_codes[ok].long(), probs[ok].to(torch.float64)
+    w = torch.ones(y.numel(), dtype=torch.float64, device=y.device) if w is None else w[ok].to(torch.float64)
+    if cloud.is_distributed():
+        y, P, w = _gather(y), _gather(P), _gather(w)
+    K = P.shape[1]
+    sw = float(w.sum())
+    py = P[torch.arange(y.numel(), device=y.device), y].clamp(1e-15, 1)
+    logloss = float(-(w * torch.log(py)).sum() / sw)
+    onehot = torch.nn.functional.one_hot(y, K).to(torch.float64)
+    mse = float((w * ((onehot - P) ** 2).sum(1)).sum() / sw)
+    pred = torch.argmax(P, 1)
+    cmat = torch.zeros((K, K), dtype=torch.float64, device=y.device)
+    cmat.index_put_((y, pred), w, accumulate=True)
+    cm = cmat.cpu().numpy()
+    rows = cm.sum(1)
+    errs = [1 - cm[i, i] / rows[i] if rows[i] > 0 else 0.0 for i in range(K)]
+    present = [i for i in range(K) if rows[i] > 0]
+    mpce = float(np.mean([errs[i] for i in present])) if present else float("nan")
+    # hit ratios
+    kk = min(hit_k, K)
+    topk = torch.topk(P, kk, dim=1).indices
+    hits = (topk == y.view(-1, 1)).to(torch.float64)
+    hr = (torch.cumsum(hits, 1) * w.view(-1, 1)).sum(0) / sw
+    dom = domain or [str(i) for i in range(K)]
+    return ModelMetricsMultinomial(MSE=mse, RMSE=math.sqrt(mse), logloss=logloss, mean_per_class_error=mpce,
+                                   nobs=int(y.numel()),
+                                   cm={"domain": dom, "matrix": cm.tolist(), "errors": errs,
+                                       "total_error": 1 - float(np.trace(cm)) / max(cm.sum(), 1e-300)},
+                                   hit_ratio_table=[{"k": i + 1, "hit_ratio": float(hr[i])} for i in range(kk)],
+                                   domain=dom)
+
+
+def clustering_metrics(X, centers, assign, w=None):
+    X = X.to(torch.float64)
+    C = centers.to(torch.float64)
+    w = torch.ones(X.shape[0], dtype=torch.float64, device=X.device) if w is None else w.to(torch.float64)
+    d = ((X - C[assign]) ** 2).sum(1) * w
+    k = C.shape[0]
+    within = torch.zeros(k, dtype=torch.float64, device=X.device).index_add_(0, assign, d)
+    sizes = torch.zeros(k, dtype=torch.float64, device=X.device).index_add_(0, assign, w)
+    sw = w.sum()
+    mean = (X * w.view(-1, 1)).sum(0)
+    stats = torch.cat([within, sizes, sw.view(1), mean])
+    coll.allreduce_(stats)
+    within, sizes, sw, mean = stats[:k], stats[k:2 * k], stats[2 * k], stats[2 * k + 1:] / stats[2 * k]
+    tot = ((X - mean) ** 2).sum(1) * w
+    totss = coll.allreduce_scalar(float(tot.sum()))
+    tw = float(within.sum())
+    return ModelMetricsClustering(tot_withinss=tw, totss=totss, betweenss=totss - tw,
+                                  withinss=within.cpu().tolist(), size=sizes.cpu().tolist(),
+                                  nobs=int(float(sw)))

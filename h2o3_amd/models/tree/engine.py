@@ -1,0 +1,468 @@
+"""Level-wise GPU tree growth shared by GBM, DRF, XGBoost and Uplift.
+
+Reference: hex/tree/SharedTree.java (scoreAndBuildTrees / buildLayer),
+hex/tree/DTree.java (UndecidedNode/DecidedNode, findBestSplitPoint at
+DTree.java:984), hex/tree/ScoreBuildHistogram2.java.
+
+Per tree, per level:
+  1. histograms for the *smaller* child of every split (HIP LDS kernel,
+     ops/csrc/tree_hist.hip); the larger sibling is parent - smaller
+     (histogram subtraction — the reference builds every node from rows);
+  2. multi-GPU: reduce_scatter over the feature dim, each rank scores the
+     splits of its feature slice, candidates are all_gathered (small);
+  3. vectorized split search over [node, feature, threshold, NA-direction]
+     (squared-error criterion of the reference, or the second-order gain of
+     XGBoost), categorical levels sorted by mean response -> bitset;
+  4. stable GPU partition of each split node's row segment.
+Leaves end up as contiguous segments of the row permutation, giving the
+per-row leaf id for the leaf-value pass without any tree traversal.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from ...ops import tree_ops
+from ...parallel import cloud
+from ...parallel import collectives as coll
+
+NEG_INF = float("-inf")
+
+
+@dataclass
+class GrowParams:
+    criterion: str = "se"          # "se" (H2O GBM/DRF) | "xgb" (second order)
+    max_depth: int = 5
+    min_rows: float = 10.0         # se: min weighted rows per child; xgb: min_child_weight
+    min_split_improvement: float = 1e-5
+    reg_lambda: float = 1.0
+    reg_alpha: float = 0.0
+    gamma: float = 0.0             # xgb min_split_loss
+    max_leaves: int = 0            # 0 = unlimited
+    monotone: np.ndarray | None = None  # [F] in {-1,0,1}
+    col_sample_rate: float = 1.0   # per split (GBM) / mtries fraction
+    mtries: int = -1               # DRF: features per node (-1 = all)
+    col_sample_rate_change_per_level: float = 1.0
+    tree_col_mask: np.ndarray | None = None  # [F] bool, per-tree sampling
+    seed: int = 0
+    hist_mem_budget: int = 8 << 30
+    interaction_sets: list | None = None  # list of sets of feature ids
+
+
+@dataclass
+class Tree:
+    """Host-side tree in BFS order (the per-node arrays feed scoring kernels,
+    MOJO writer, SHAP and varimp)."""
+    feat: list = field(default_factory=list)
+    left: list = field(default_factory=list)
+    right: list = field(default_factory=list)
+    thr: list = field(default_factory=list)        # numeric: x < thr goes left
+    na_left: list = field(default_factory=list)
+    is_cat: list = field(default_factory=list)
+    cat_left: list = field(default_factory=list)   # list of np.uint8 level masks (len = cardinality) or None
+    value: list = field(default_factory=list)
+    weight: list = field(default_factory=list)     # training cover (sum w or sum h)
+    gain: list = field(default_factory=list)
+    depth: list = field(default_factory=list)
+    split_code: list = field(default_factory=list) # code threshold (numeric) for debugging
+
+    def add_node(self, depth, weight):
+        self.feat.append(-1); self.left.append(-1); self.right.append(-1); self.thr.append(0.0)
+        self.na_left.append(False); self.is_cat.append(False); self.cat_left.append(None)
+        self.value.append(0.0); self.weight.append(float(weight)); self.gain.append(0.0)
+        self.depth.append(depth); self.split_code.append(-1)
+        return len(self.feat) - 1
+
+    @property
+    def n_nodes(self):
+        return len(self.feat)
+
+    def is_leaf(self, i):
+        return self.left[i] < 0
+
+    def leaves(self):
+        return [i for i in range(self.n_nodes) if self.left[i] < 0]
+
+    def max_depth(self):
+        return max(self.depth) if self.depth else 0
+
+    def to_arrays(self):
+        return {k: np.asarray(getattr(self, k)) for k in ("feat", "left", "right", "thr", "na_left", "is_cat",
+                                                          "value", "weight", "gain", "depth")}
+
+    def predict_host(self, X: np.ndarray) -> np.ndarray:
+        """Reference traversal on host (X: [n, F] float64, cats as codes)."""
+        out = np.empty(X.shape[0])
+        for r in range(X.shape[0]):
+            i = 0
+            while self.left[i] >= 0:
+                x = X[r, self.feat[i]]
+                if self.is_cat[i]:
+                    m = self.cat_left[i]
+                    if np.isnan(x) or int(x) >= len(m) or int(x) < 0:
+                        go_left = self.na_left[i]
+                    else:
+                        go_left = bool(m[int(x)])
+                elif np.isnan(x):
+                    go_left = self.na_left[i]
+                else:
+                    go_left = x < self.thr[i]
+                i = self.left[i] if go_left else self.right[i]
+            out[r] = self.value[i]
+        return out
+
+
+class TreeGrower:
+    """Grows one tree over a BinnedData with a given channel mode."""
+
+    def __init__(self, bd, params: GrowParams):
+        self.bd = bd
+        self.p = params
+        self.dev = bd.codes.device
+        n = bd.nrows_local
+        self.ridx = torch.empty(n, dtype=torch.int32, device=self.dev)
+        self.ridx2 = torch.empty(n, dtype=torch.int32, device=self.dev)
+        self.W = cloud.world()
+        self.rank = cloud.rank()
+        F = bd.F
+        self.Fpad = ((F + self.W - 1) // self.W) * self.W
+        self.Fl = self.Fpad // self.W
+        self.f0 = self.rank * self.Fl
+        self.is_cat_t = torch.tensor(bd.is_cat + [False] * (self.Fpad - F), dtype=torch.bool, device=self.dev)
+        self.nbins_t = torch.tensor(bd.nbins + [0] * (self.Fpad - F), dtype=torch.int64, device=self.dev)
+        mono = params.monotone if params.monotone is not None else np.zeros(F)
+        self.mono_t = torch.tensor(list(mono) + [0] * (self.Fpad - F), dtype=torch.float64, device=self.dev)
+        self.rng = np.random.RandomState(params.seed & 0x7FFFFFFF)
+
+    # ------------------------------------------------------------------ hist
+    def _build_hist(self, ridx, va, vb, mode, starts, counts):
+        H = tree_ops.hist_build(self.bd, ridx, va, vb, mode, starts, counts, len(starts))
+        if self.W > 1:
+            if self.Fpad > self.bd.F:
+                H = torch.cat([H, torch.zeros((self.Fpad - self.bd.F,) + tuple(H.shape[1:]), dtype=H.dtype,
+                                              device=H.device)], 0)
+            H = coll.reduce_scatter_dim0(H)
+        return H  # [Fl, n, Bs, C]
+
+    # ------------------------------------------------------------------ splits
+    def _col_mask(self, n_nodes, depth):
+        """[n, Fpad] bool mask of features eligible per node."""
+        p = self.p
+        F = self.bd.F
+        base = np.ones(F, dtype=bool) if p.tree_col_mask is None else p.tree_col_mask.astype(bool)
+        m = np.tile(base, (n_nodes, 1))
+        rate = p.col_sample_rate * (p.col_sample_rate_change_per_level ** depth)
+        k = None
+        if p.mtries is not None and p.mtries > 0:
+            k = p.mtries
+        elif rate < 1.0:
+            k = max(1, int(math.floor(rate * base.sum() + 0.5)))
+        if k is not None and k < base.sum():
+            elig = np.nonzero(base)[0]
+            for i in range(n_nodes):
+                sel = self.rng.choice(elig, size=k, replace=False)
+                row = np.zeros(F, dtype=bool)
+                row[sel] = True
+                m[i] = row
+        if self.Fpad > F:
+            m = np.concatenate([m, np.zeros((n_nodes, self.Fpad - F), dtype=bool)], 1)
+        return torch.from_numpy(m)
+
+    def _find_splits(self, H, col_mask, allowed_sets=None):
+        """H: [Fl, n, Bs, C] (local feature slice).  Returns dict of per-node
+        tensors on device: gain, feat, na_left, mask[n, Bs], stats L/R [n,C],
+        tot [n,C]."""
+        p = self.p
+        Fl, n, Bs, C = H.shape
+        B = Bs - 1
+        h = H.permute(1, 0, 2, 3).to(torch.float64)       # [n, Fl, Bs, C]
+        bins = h[:, :, :B]
+        na = h[:, :, B]                                    # [n, Fl, C]
+        fsl = slice(self.f0, self.f0 + Fl)
+        is_cat = self.is_cat_t[fsl]
+        order = None
+        if bool(is_cat.any()):
+            if p.criterion == "xgb":
+                key = torch.where(bins[..., 1] > 0, bins[..., 0] / bins[..., 1].clamp_min(1e-300),
+                                  torch.full_like(bins[..., 0], float("inf")))
+            else:
+                key = torch.where(bins[..., 0] > 0, bins[..., 1] / bins[..., 0].clamp_min(1e-300),
+                                  torch.full_like(bins[..., 0], float("inf")))
+            ar = torch.arange(B, device=h.device).view(1, 1, B).expand(n, Fl, B)
+            key = torch.where(is_cat.view(1, Fl, 1), key, ar.to(key.dtype))
+            order = torch.argsort(key, dim=2, stable=True)             # [n, Fl, B]
+            bins = torch.gather(bins, 2, order.unsqueeze(-1).expand(-1, -1, -1, C))
+        cum = torch.cumsum(bins, 2)
+        totnn = cum[:, :, -1]                              # [n, Fl, C] non-NA totals
+        L = cum[:, :, :-1]                                 # [n, Fl, B-1, C]
+        R = totnn.unsqueeze(2) - L
+        T = totnn + na                                     # [n, Fl, C] all rows
+        naE = na.unsqueeze(2)
+        # option 0: NA right, option 1: NA left, option 2: NA vs rest
+        LA, RA = L, R + naE
+        LB, RB = L + naE, R
+        LC, RC = totnn.unsqueeze(2), naE
+
+        def score(S):
+            if p.criterion == "xgb":
+                g, hh = S[..., 0], S[..., 1]
+                if p.reg_alpha > 0:
+                    g = torch.sign(g) * torch.clamp(g.abs() - p.reg_alpha, min=0)
+                return g * g / (hh + p.reg_lambda)
+            w, wy = S[..., 0], S[..., 1]
+            return torch.where(w > 0, wy * wy / w.clamp_min(1e-300), torch.zeros_like(w))
+
+        sT = score(T).unsqueeze(2)                         # [n, Fl, 1]
+
+        def gain_of(LL, RR):
+            g = score(LL) + score(RR) - sT
+            if p.criterion == "xgb":
+                g = 0.5 * g - p.gamma
+                wl, wr = LL[..., 1], RR[..., 1]
+                ok = (wl >= max(p.min_rows, 1e-12)) & (wr >= max(p.min_rows, 1e-12))
+                predl = -LL[..., 0] / (wl + p.reg_lambda)
+                predr = -RR[..., 0] / (wr + p.reg_lambda)
+            else:
+                wl, wr = LL[..., 0], RR[..., 0]
+                ok = (wl >= p.min_rows) & (wr >= p.min_rows) & (wl > 0) & (wr > 0)
+                predl = LL[..., 1] / wl.clamp_min(1e-300)
+                predr = RR[..., 1] / wr.clamp_min(1e-300)
+                ok &= predl.to(torch.float32) != predr.to(torch.float32)
+            mono = self.mono_t[fsl].view(1, Fl, 1)
+            ok &= ~((mono > 0) & (predl > predr)) & ~((mono < 0) & (predl < predr))
+            return torch.where(ok, g, torch.full_like(g, NEG_INF))
+
+        gA = gain_of(LA, RA)
+        gB = gain_of(LB, RB)
+        has_na = (na[..., 0] > 0) if p.criterion != "xgb" else ((na[..., 1] > 0) | (na[..., 0] != 0))
+        gB = torch.where(has_na.unsqueeze(2), gB, torch.full_like(gB, NEG_INF))
+        gC = gain_of(LC, RC)
+        gC = torch.where(has_na.unsqueeze(2), gC, torch.full_like(gC, NEG_INF))
+        # feature eligibility (column sampling, padding, interaction constraints)
+        cm = col_mask[:, fsl].to(h.device)
+        if self.f0 + Fl > self.bd.F:
+            cm = cm.clone()
+            cm[:, max(0, self.bd.F - self.f0):] = False
+        allg = torch.cat([gA, gB, gC], 2)                  # [n, Fl, 2(B-1)+1]
+        allg = torch.where(cm.unsqueeze(2), allg, torch.full_like(allg, NEG_INF))
+        # min split improvement (relative to the node's squared error)
+        if p.criterion != "xgb":
+            wyy_tot = T[..., 2] if C > 2 else torch.zeros_like(T[..., 0])
+            se_before = (wyy_tot - score(T)).clamp_min(0).unsqueeze(2)
+            allg = torch.where(allg > se_before * p.min_split_improvement, allg, torch.full_like(allg, NEG_INF))
+            allg = torch.where(se_before > 0, allg, torch.full_like(allg, NEG_INF))
+        else:
+            allg = torch.where(allg > 0, allg, torch.full_like(allg, NEG_INF))
+        K = allg.shape[2]
+        flat = allg.reshape(n, Fl * K)
+        best, arg = flat.max(1)
+        fl = arg // K
+        k = arg % K
+        nt = B - 1
+        opt = torch.where(k < nt, torch.zeros_like(k), torch.where(k < 2 * nt, torch.ones_like(k), torch.full_like(k, 2)))
+        t = torch.where(opt == 0, k, torch.where(opt == 1, k - nt, torch.zeros_like(k)))
+        na_left = opt == 1
+        ar_n = torch.arange(n, device=h.device)
+        # stats of the winning split
+        Lw = torch.where((opt == 2).view(n, 1), totnn[ar_n, fl],
+                         L[ar_n, fl, t.clamp(max=nt - 1)] + torch.where(na_left.view(n, 1), na[ar_n, fl], torch.zeros_like(na[ar_n, fl])))
+        Tw = T[ar_n, fl]
+        Rw = Tw - Lw
+        # go-left masks over codes
+        codes = torch.arange(Bs, device=h.device).view(1, Bs)
+        cat_best = is_cat[fl]
+        mask_num = (codes <= t.view(n, 1)) & (codes < B)
+        mask_num = torch.where((opt == 2).view(n, 1), codes < B, mask_num)
+        if order is not None:
+            ordw = order[ar_n, fl]                                     # [n, B]
+            rank = torch.empty_like(ordw)
+            rank.scatter_(1, ordw, torch.arange(B, device=h.device).view(1, B).expand(n, B))
+            in_left = rank <= t.view(n, 1)
+            bins_w = h[ar_n, fl, :B, 0] if p.criterion != "xgb" else h[ar_n, fl, :B, 1]
+            empty = bins_w <= 0
+            in_left = torch.where(empty, na_left.view(n, 1).expand(n, B), in_left)
+            in_left = torch.where((opt == 2).view(n, 1), ~empty | na_left.view(n, 1), in_left)
+            mask_cat = torch.cat([in_left, torch.zeros((n, Bs - B), dtype=torch.bool, device=h.device)], 1)
+            mask = torch.where(cat_best.view(n, 1), mask_cat, mask_num)
+        else:
+            mask = mask_num
+        mask = mask.clone()
+        mask[:, Bs - 1] = na_left
+        res = {"gain": best, "feat": fl + self.f0, "t": t, "opt": opt, "na_left": na_left,
+               "mask": mask.to(torch.uint8), "L": Lw, "R": Rw, "tot": T[:, 0] if Fl > 0 else None}
+        if self.W > 1:
+            res = self._merge_candidates(res, n, Bs, C)
+        return res
+
+    def _merge_candidates(self, res, n, Bs, C):
+        W = self.W
+        packed = torch.cat([res["gain"].view(n, 1), res["feat"].to(torch.float64).view(n, 1),
+                            res["t"].to(torch.float64).view(n, 1), res["opt"].to(torch.float64).view(n, 1),
+                            res["L"], res["R"], res["tot"], res["mask"].to(torch.float64)], 1)
+        g = coll.all_gather_dim0(packed.contiguous()).view(W, n, -1)
+        gains = g[:, :, 0]
+        # deterministic tie-break: lowest rank (= lowest feature) wins
+        best_r = torch.argmax(gains, 0)
+        sel = g[best_r, torch.arange(n, device=g.device)]
+        off = 4
+        out = {"gain": sel[:, 0], "feat": sel[:, 1].long(), "t": sel[:, 2].long(), "opt": sel[:, 3].long()}
+        out["na_left"] = out["opt"] == 1
+        out["L"] = sel[:, off:off + C]
+        out["R"] = sel[:, off + C:off + 2 * C]
+        out["tot"] = g[0, :, off + 2 * C:off + 3 * C]   # rank 0 holds feature 0
+        out["mask"] = sel[:, off + 3 * C:].to(torch.uint8)
+        return out
+
+    # ------------------------------------------------------------------ grow
+    def grow(self, va, vb, mode, tree_node_hook=None):
+        """Grow one tree.  Returns (Tree, nid[N] leaf index per local row,
+        leaf_nodes list (tree node ids, indexed by nid), leaf_tot [n_leaves, C])."""
+        bd, p = self.bd, self.p
+        N = bd.nrows_local
+        C = tree_ops.channels(mode)
+        torch.arange(N, dtype=torch.int32, device=self.dev, out=self.ridx)
+        ridx, ridx2 = self.ridx, self.ridx2
+        tree = Tree()
+        root = tree.add_node(0, 0.0)
+        # frontier entries: [node_id, start, count_local, depth]
+        frontier = [[root, 0, N, 0]]
+        H_prev, prev_slot = None, {}
+        pair_info = []     # for level>0: (left_id, right_id, parent_slot, build_left)
+        leaves, leaf_tot = [], []
+        level = 0
+        while frontier:
+            n_front = len(frontier)
+            slot_of = {nd[0]: i for i, nd in enumerate(frontier)}
+            if level == 0 or H_prev is None:
+                build = list(range(n_front))
+                Hb = self._build_hist(ridx, va, vb, mode, [f[1] for f in frontier], [f[2] for f in frontier])
+                H = Hb
+            else:
+                build_slots, der_slots, par_slots, sib_idx = [], [], [], []
+                for (lid, rid, pslot, build_left) in pair_info:
+                    b, d = (lid, rid) if build_left else (rid, lid)
+                    build_slots.append(slot_of[b])
+                    der_slots.append(slot_of[d])
+                    par_slots.append(pslot)
+                Hb = self._build_hist(ridx, va, vb, mode, [frontier[s][1] for s in build_slots],
+                                      [frontier[s][2] for s in build_slots])
+                H = torch.empty((Hb.shape[0], n_front) + tuple(Hb.shape[2:]), dtype=Hb.dtype, device=Hb.device)
+                bs = torch.tensor(build_slots, device=Hb.device)
+                ds = torch.tensor(der_slots, device=Hb.device)
+                ps = torch.tensor(par_slots, device=Hb.device)
+                H[:, bs] = Hb
+                H[:, ds] = (H_prev[:, ps] - Hb).clamp_min_(0) if mode != 1 else (H_prev[:, ps] - Hb)
+                if mode == 0:
+                    # only w / wyy are non-negative; wy may be negative
+                    H[:, ds, :, 1] = H_prev[:, ps, :, 1] - Hb[:, :, :, 1]
+            del Hb
+            depth = frontier[0][3]
+            can_split = depth < p.max_depth
+            if can_split:
+                cm = self._col_mask(n_front, depth)
+                sp = self._find_splits(H, cm)
+                gains = sp["gain"].cpu()
+                feats = sp["feat"].cpu()
+                Ls = sp["L"].cpu()
+                Rs = sp["R"].cpu()
+                tots = sp["tot"].cpu()
+            else:
+                # totals only
+                tots = self._totals(H)
+                gains = None
+            split_ids, split_slots = [], []
+            for i, (nid_, st, ct, d) in enumerate(frontier):
+                tot_i = tots[i]
+                tree.weight[nid_] = float(tot_i[0] if mode != 1 else tot_i[1])
+                ok = can_split and gains is not None and math.isfinite(float(gains[i]))
+                if ok and p.criterion != "xgb" and float(tot_i[0]) < 2 * p.min_rows:
+                    ok = False
+                if ok and p.max_leaves and (len(leaves) + n_front + len(split_ids) + 1) > p.max_leaves:
+                    ok = False
+                if ok:
+                    split_ids.append(i)
+                else:
+                    leaves.append(nid_)
+                    leaf_tot.append(tot_i)
+                    # keep the segment for the nid pass
+                    frontier[i].append("leaf")
+            if not split_ids:
+                self._leaf_segments = [(f[0], f[1], f[2]) for f in frontier]
+                break
+            # record splits in the tree
+            masks = sp["mask"][torch.tensor(split_ids, device=sp["mask"].device)]
+            masks_h = masks.cpu().numpy()
+            t_h = sp["t"].cpu()
+            opt_h = sp["opt"].cpu()
+            nal_h = sp["na_left"].cpu()
+            new_front, new_pairs = [], []
+            part_starts, part_counts, part_feats = [], [], []
+            for j, i in enumerate(split_ids):
+                nid_, st, ct, d = frontier[i][:4]
+                f = int(feats[i])
+                tree.feat[nid_] = f
+                tree.gain[nid_] = float(gains[i])
+                tree.na_left[nid_] = bool(nal_h[i])
+                if bd.is_cat[f]:
+                    tree.is_cat[nid_] = True
+                    card = bd.cat_card[f]
+                    g = bd.cat_group[f]
+                    lv = np.arange(card) // g
+                    tree.cat_left[nid_] = masks_h[j][np.minimum(lv, bd.Bs - 2)].astype(np.uint8)
+                    tree.thr[nid_] = float("nan")
+                else:
+                    if int(opt_h[i]) == 2:
+                        tree.thr[nid_] = float("inf")     # NA vs rest: every number goes left
+                    else:
+                        tree.thr[nid_] = bd.split_value(f, int(t_h[i]))
+                    tree.split_code[nid_] = int(t_h[i])
+                lid = tree.add_node(d + 1, float(Ls[i][0]))
+                rid = tree.add_node(d + 1, float(Rs[i][0]))
+                tree.left[nid_], tree.right[nid_] = lid, rid
+                part_starts.append(st)
+                part_counts.append(ct)
+                part_feats.append(f)
+                wl = float(Ls[i][0] if mode != 1 else Ls[i][1])
+                wr = float(Rs[i][0] if mode != 1 else Rs[i][1])
+                new_pairs.append((lid, rid, j, wl <= wr))
+            # partition
+            ridx2.copy_(ridx)
+            nleft = tree_ops.partition(bd, ridx, ridx2, part_feats, masks, part_starts, part_counts)
+            ridx, ridx2 = ridx2, ridx
+            for j, i in enumerate(split_ids):
+                nid_, st, ct, d = frontier[i][:4]
+                lid, rid = tree.left[nid_], tree.right[nid_]
+                nl = nleft[j]
+                new_front.append([lid, st, nl, d + 1])
+                new_front.append([rid, st + nl, ct - nl, d + 1])
+            # keep leaf segments of this level
+            self._pending_leaf_segs = getattr(self, "_pending_leaf_segs", [])
+            for f in frontier:
+                if len(f) > 4:
+                    self._pending_leaf_segs.append((f[0], f[1], f[2]))
+            # parent hists for the next level (only split nodes)
+            H_prev = H[:, torch.tensor(split_ids, device=H.device)]
+            pair_info = new_pairs
+            frontier = new_front
+            level += 1
+        segs = getattr(self, "_pending_leaf_segs", []) + getattr(self, "_leaf_segments", [])
+        self._pending_leaf_segs = []
+        self._leaf_segments = []
+        leaf_index = {nid_: k for k, nid_ in enumerate(leaves)}
+        lids = [leaf_index[s[0]] for s in segs]
+        nid = tree_ops.fill_nid(ridx, lids, [s[1] for s in segs], [s[2] for s in segs], N)
+        self.ridx, self.ridx2 = ridx, ridx2
+        leaf_tot_t = torch.stack([torch.as_tensor(x, dtype=torch.float64) for x in leaf_tot]) if leaf_tot else \
+            torch.zeros((0, C), dtype=torch.float64)
+        return tree, nid, leaves, leaf_tot_t
+
+    def _totals(self, H):
+        """Per-node channel totals [n, C] (global), from feature 0."""
+        Fl, n, Bs, C = H.shape
+        t = H[0].to(torch.float64).sum(1) if Fl > 0 else torch.zeros((n, C), dtype=torch.float64, device=H.device)
+        if self.W > 1:
+            t = coll.all_gather_dim0(t.contiguous()).view(self.W, n, C)[0]
+        return t.cpu()

@@ -1,0 +1,469 @@
+"""Gradient Boosting Machine.
+
+Reference: hex/tree/gbm/GBM.java — per iteration: compute the negative
+half-gradient residuals (GBM.ComputePredAndRes / Distribution.negHalfGradient),
+grow K regression trees on them with the squared-error histogram
+criterion (SharedTree + DTree.findBestSplitPoint), then set terminal node
+values with the distribution-specific Newton step (GBM.GammaPass,
+gbm/GBM.java:1286: gamma = sum(w*num)/sum(w*denom)) and add
+learn_rate * gamma to the predictions.
+
+MI355X design: residuals, weights and predictions are device tensors; the
+tree is grown by TreeGrower (LDS histogram kernel + GPU partition) and the
+leaf rows are contiguous segments, so the gamma pass is two index_add
+reductions over the per-row leaf ids and the prediction update one gather.
+"""
+from __future__ import annotations
+
+import math
+import time
+
+import numpy as np
+import torch
+
+from ...core.frame import H2OFrame
+from ...parallel import cloud
+from ...parallel import collectives as coll
+from ..base import ScoreKeeper, _LESS_IS_BETTER
+from ..distributions import get_distribution
+from .engine import GrowParams, TreeGrower
+from .shared import Forest, SharedTreeEstimator
+
+GBM_DEFAULTS = dict(ntrees=50, max_depth=5, min_rows=10.0, nbins=20, nbins_top_level=1024, nbins_cats=1024,
+                    r2_stopping=1.79e308, stopping_rounds=0, stopping_metric="auto", stopping_tolerance=0.001,
+                    seed=-1, build_tree_one_node=False, learn_rate=0.1, learn_rate_annealing=1.0,
+                    distribution="auto", quantile_alpha=0.5, tweedie_power=1.5, huber_alpha=0.9,
+                    checkpoint=None, sample_rate=1.0, sample_rate_per_class=None, col_sample_rate=1.0,
+                    col_sample_rate_change_per_level=1.0, col_sample_rate_per_tree=1.0,
+                    min_split_improvement=1e-5, histogram_type="auto", max_abs_leafnode_pred=1.79e308,
+                    pred_noise_bandwidth=0.0, categorical_encoding="auto", calibrate_model=False,
+                    calibration_frame=None, calibration_method="auto", custom_distribution_func=None,
+                    monotone_constraints=None, check_constant_response=True, interaction_constraints=None,
+                    score_tree_interval=0, balance_classes=False, class_sampling_factors=None,
+                    max_after_balance_size=5.0, max_confusion_matrix_size=20, in_training_checkpoints_dir=None,
+                    in_training_checkpoints_tree_interval=1, auto_rebalance=True)
+
+
+class GBMDriver:
+    """Stateful boosting loop (one `step()` = one boosting iteration = K trees)."""
+
+    def __init__(self, est, spec, bd=None):
+        self.est = est
+        p = est._parms
+        self.spec = spec
+        self.K = spec.nclasses if spec.nclasses > 2 else 1
+        dist_name = p.get("distribution", "auto")
+        if spec.nclasses == 2 and dist_name in ("auto", "AUTO"):
+            dist_name = "bernoulli"
+        self.dist = get_distribution(dist_name, spec.nclasses, tweedie_power=p.get("tweedie_power", 1.5),
+                                     quantile_alpha=p.get("quantile_alpha", 0.5),
+                                     huber_alpha=p.get("huber_alpha", 0.9))
+        est._dist = self.dist
+        dev = cloud.device()
+        self.dev = dev
+        self.bd = bd if bd is not None else est._bin(spec)
+        N = self.bd.nrows_local
+        y = spec.y_tensor()
+        w = spec.w_tensor()
+        self.w_user = w
+        if spec.is_classification:
+            self.ycode = y.to(torch.int64)
+            valid = self.ycode >= 0
+        else:
+            self.yf = y.to(torch.float32)
+            valid = ~torch.isnan(self.yf)
+        base_w = torch.ones(N, dtype=torch.float32, device=dev) if w is None else w.to(torch.float32)
+        self.base_w = torch.where(valid, base_w, torch.zeros_like(base_w))
+        self.offset = spec.offset_tensor()
+        # init prediction (reference: GBM.init -> initial value by distribution)
+        if self.K == 1:
+            if spec.nclasses == 2:
+                yv = (self.ycode == 1).to(torch.float32)
+                self.yb = yv
+            else:
+                yv = torch.nan_to_num(self.yf)
+            sw = coll.allreduce_scalar(float(self.base_w.sum()))
+            sy = coll.allreduce_scalar(float((self.base_w * yv).sum()))
+            mu = sy / sw if sw > 0 else 0.0
+            if self.dist.family in ("laplace", "quantile", "huber"):
+                f0 = _weighted_quantile(yv[self.base_w > 0], self.base_w[self.base_w > 0],
+                                        0.5 if self.dist.family != "quantile" else self.dist.quantile_alpha)
+            elif self.dist.link == "logit":
+                mu = min(max(mu, 1e-10), 1 - 1e-10)
+                f0 = math.log(mu / (1 - mu))
+            elif self.dist.link == "log":
+                f0 = math.log(max(mu, 1e-10))
+            else:
+                f0 = mu
+            if self.offset is not None and self.dist.link != "identity":
+                f0 = self._newton_init(f0, yv)
+            self.init_f = [f0]
+        else:
+            # multinomial: reference initialises f_k = log(prior_k) - mean
+            cnt = torch.zeros(self.K, dtype=torch.float64, device=dev)
+            ok = self.ycode >= 0
+            cnt.index_add_(0, self.ycode[ok], self.base_w[ok].to(torch.float64))
+            coll.allreduce_(cnt)
+            pri = (cnt / cnt.sum()).clamp_min(1e-10)
+            lp = torch.log(pri)
+            self.init_f = (lp - lp.mean()).cpu().tolist()
+            self.Y = torch.nn.functional.one_hot(self.ycode.clamp(min=0), self.K).to(torch.float32)
+        self.f = torch.tensor(self.init_f, dtype=torch.float32, device=dev).view(1, -1).repeat(N, 1)
+        if self.offset is not None:
+            self.f += self.offset.view(-1, 1)
+        gp = GrowParams(criterion="se", max_depth=int(p["max_depth"]) if p["max_depth"] > 0 else 64,
+                        min_rows=float(p["min_rows"]), min_split_improvement=float(p["min_split_improvement"]),
+                        col_sample_rate=float(p["col_sample_rate"]),
+                        col_sample_rate_change_per_level=float(p["col_sample_rate_change_per_level"]),
+                        seed=self._seed())
+        mc = p.get("monotone_constraints")
+        if mc:
+            gp.monotone = np.array([float(mc.get(n, 0)) for n in spec.x])
+        self.gp = gp
+        self.grower = TreeGrower(self.bd, gp)
+        self.forest = Forest()
+        self.lr = float(p["learn_rate"])
+        self.iter = 0
+        self.rng = np.random.RandomState(self._seed())
+        self.gen = torch.Generator(device=dev)
+        self.gen.manual_seed(self._seed() + cloud.rank())
+        if self.dist.family == "huber":
+            self.dist.huber_delta = None
+
+    def _seed(self):
+        s = self.est._parms.get("seed", -1)
+        return 1234 if s is None or s == -1 else int(s) & 0x7FFFFFFF
+
+    def _newton_init(self, f0, yv):
+        for _ in range(20):
+            ff = f0 + self.offset
+            z = self.dist.neg_half_gradient(yv, ff)
+            num = coll.allreduce_scalar(float(self.dist.gamma_num(self.base_w, yv, z, ff).sum()))
+            den = coll.allreduce_scalar(float(self.dist.gamma_denom(self.base_w, yv, z, ff).sum()))
+            if self.dist.link == "logit":
+                step = num / den if den != 0 else 0.0
+                f0 += step
+                if abs(step) < 1e-8:
+                    break
+            else:
+                g = self.dist.gamma(num, den)
+                f0 += g
+                if abs(g) < 1e-8:
+                    break
+        return f0
+
+    def _row_weights(self):
+        p = self.est._parms
+        w = self.base_w
+        sr = float(p.get("sample_rate", 1.0))
+        srpc = p.get("sample_rate_per_class")
+        if srpc is not None and self.spec.is_classification:
+            rates = torch.tensor(srpc, dtype=torch.float32, device=self.dev)[self.ycode.clamp(min=0)]
+            keep = torch.rand(w.shape, generator=self.gen, device=self.dev) < rates
+            return w * keep
+        if sr < 1.0:
+            keep = torch.rand(w.shape, generator=self.gen, device=self.dev) < sr
+            return w * keep
+        return w
+
+    def _tree_col_mask(self):
+        r = float(self.est._parms.get("col_sample_rate_per_tree", 1.0))
+        F = self.bd.F
+        if r >= 1.0:
+            return None
+        k = max(1, int(math.floor(r * F + 0.5)))
+        m = np.zeros(F, dtype=bool)
+        m[self.rng.choice(F, size=k, replace=False)] = True
+        return m
+
+    def step(self):
+        """One boosting iteration."""
+        p = self.est._parms
+        w = self._row_weights()
+        self.gp.tree_col_mask = self._tree_col_mask()
+        lr = self.lr * (float(p.get("learn_rate_annealing", 1.0)) ** self.iter)
+        maxabs = float(p.get("max_abs_leafnode_pred", 1.79e308))
+        if self.K == 1:
+            f = self.f[:, 0]
+            y = self.yb if self.spec.nclasses == 2 else torch.nan_to_num(self.yf)
+            z = self.dist.neg_half_gradient(y, f).to(torch.float32)
+            if self.dist.family == "huber":
+                self._update_huber_delta(y, f, w)
+                z = self.dist.neg_half_gradient(y, f).to(torch.float32)
+            tree, nid, leaves, tot = self.grower.grow(z.contiguous(), w.contiguous(), 0)
+            vals = self._gamma(tree, nid, leaves, w, y, z, f, 0)
+            vals = np.clip(vals, -maxabs, maxabs)
+            for li, node in enumerate(leaves):
+                tree.value[node] = float(lr * vals[li])
+            vt = torch.tensor(lr * vals, dtype=torch.float32, device=self.dev)
+            self.f[:, 0] += vt[nid.long()]
+            self.forest.add(tree, 0)
+        else:
+            P = torch.softmax(self.f, 1)
+            new = []
+            for k in range(self.K):
+                z = (self.Y[:, k] - P[:, k]).contiguous()
+                tree, nid, leaves, tot = self.grower.grow(z, w.contiguous(), 0)
+                vals = self._gamma_multi(nid, len(leaves), w, z)
+                vals = np.clip(vals, -maxabs, maxabs)
+                for li, node in enumerate(leaves):
+                    tree.value[node] = float(lr * vals[li])
+                vt = torch.tensor(lr * vals, dtype=torch.float32, device=self.dev)
+                new.append(vt[nid.long()])
+                self.forest.add(tree, k)
+            for k in range(self.K):
+                self.f[:, k] += new[k]
+        self.iter += 1
+
+    def _update_huber_delta(self, y, f, w):
+        r = (y - f).abs()
+        m = w > 0
+        self.dist.huber_delta = _weighted_quantile(r[m], w[m], self.dist.huber_alpha)
+
+    def _gamma(self, tree, nid, leaves, w, y, z, f, k):
+        L = len(leaves)
+        idx = nid.long()
+        fam = self.dist.family
+        if fam in ("laplace", "quantile"):
+            alpha = 0.5 if fam == "laplace" else self.dist.quantile_alpha
+            return _segmented_wquantile(idx, (y - f).to(torch.float64), w.to(torch.float64), L, alpha)
+        if fam == "huber":
+            res = (y - f).to(torch.float64)
+            med = _segmented_wquantile(idx, res, w.to(torch.float64), L, 0.5)
+            mt = torch.tensor(med, dtype=torch.float64, device=self.dev)
+            d = res - mt[idx]
+            delta = self.dist.huber_delta
+            corr = torch.sign(d) * torch.minimum(d.abs(), torch.full_like(d, delta))
+            num = torch.zeros(L, dtype=torch.float64, device=self.dev).index_add_(0, idx, w.to(torch.float64) * corr)
+            den = torch.zeros(L, dtype=torch.float64, device=self.dev).index_add_(0, idx, w.to(torch.float64))
+            s = torch.cat([num, den])
+            coll.allreduce_(s)
+            num, den = s[:L], s[L:]
+            return (mt + torch.where(den > 0, num / den.clamp_min(1e-300), torch.zeros_like(num))).cpu().numpy()
+        num_r = self.dist.gamma_num(w, y, z, f).to(torch.float64)
+        den_r = self.dist.gamma_denom(w, y, z, f).to(torch.float64)
+        s = torch.zeros(2 * L, dtype=torch.float64, device=self.dev)
+        s[:L].index_add_(0, idx, num_r)
+        s[L:].index_add_(0, idx, den_r)
+        coll.allreduce_(s)
+        sh = s.cpu().numpy()
+        num, den = sh[:L], sh[L:]
+        if self.dist.link == "log" or self.dist.family in ("poisson", "gamma", "tweedie"):
+            return np.array([self.dist.gamma(float(a), float(b)) for a, b in zip(num, den)])
+        out = np.where(den != 0, num / np.where(den == 0, 1, den), 0.0)
+        return out
+
+    def _gamma_multi(self, nid, L, w, z):
+        idx = nid.long()
+        K = self.K
+        w64, z64 = w.to(torch.float64), z.to(torch.float64)
+        s = torch.zeros(2 * L, dtype=torch.float64, device=self.dev)
+        s[:L].index_add_(0, idx, w64 * z64)
+        s[L:].index_add_(0, idx, w64 * z64.abs() * (1 - z64.abs()))
+        coll.allreduce_(s)
+        sh = s.cpu().numpy()
+        num, den = sh[:L], sh[L:]
+        return (K - 1.0) / K * np.where(den > 1e-300, num / np.where(den > 1e-300, den, 1), 0.0)
+
+    def predictions(self):
+        if self.K == 1:
+            return self.dist.linkinv(self.f[:, 0])
+        return torch.softmax(self.f, 1)
+
+
+class H2OGradientBoostingEstimator(SharedTreeEstimator):
+    algo = "gbm"
+    _defaults = GBM_DEFAULTS
+
+    def _n_tree_classes(self):
+        return self._K
+
+    def _fit(self, spec):
+        p = self._parms
+        t0 = time.time()
+        drv = GBMDriver(self, spec)
+        self._K = drv.K
+        self._driver = drv
+        ntrees = int(p["ntrees"])
+        if p.get("checkpoint") is not None:
+            self._resume_from(drv, p["checkpoint"])
+        interval = int(p.get("score_tree_interval") or 0)
+        stop_rounds = int(p.get("stopping_rounds") or 0)
+        metric_name = self._stopping_metric(spec)
+        history = []
+        max_rt = float(p.get("max_runtime_secs") or 0)
+        self._scoring_history = []
+        while drv.iter < ntrees:
+            drv.step()
+            score_now = (interval > 0 and drv.iter % interval == 0) or (stop_rounds > 0 and interval == 0) or \
+                p.get("score_each_iteration") or drv.iter == ntrees
+            if score_now:
+                entry = self._score_iteration(drv, spec)
+                self._scoring_history.append(entry)
+                if stop_rounds > 0:
+                    key = "validation_" + metric_name if spec.valid is not None else "training_" + metric_name
+                    history.append(entry.get(key))
+                    if ScoreKeeper.stop_early(history, stop_rounds, float(p["stopping_tolerance"]),
+                                              metric_name in _LESS_IS_BETTER):
+                        break
+            if max_rt > 0 and time.time() - t0 > max_rt:
+                break
+        self._forest = drv.forest
+        self._init_f = drv.init_f
+        self._output["variable_importances"] = self._varimp_from_forest(drv.forest, spec.x)
+        self._output["model_summary"] = {"number_of_trees": len(drv.forest),
+                                         "number_of_internal_trees": len(drv.forest),
+                                         "min_depth": min((t.max_depth() for t in drv.forest.trees), default=0),
+                                         "max_depth": max((t.max_depth() for t in drv.forest.trees), default=0),
+                                         "mean_leaves": float(np.mean([len(t.leaves()) for t in drv.forest.trees]))
+                                         if len(drv.forest) else 0.0}
+        self._output["init_f"] = drv.init_f
+        self._train_f = drv.f
+        del drv.grower
+        self._driver = None
+        if p.get("calibrate_model") and p.get("calibration_frame") is not None:
+            from .calibration import fit_calibration
+            fit_calibration(self, p["calibration_frame"], p.get("calibration_method", "auto"))
+
+    def _cv_optimal_params(self, cv_models):
+        if int(self._parms.get("stopping_rounds") or 0) > 0 and cv_models:
+            nt = [len(m._forest) // max(1, m._K) for m in cv_models]
+            self._parms["ntrees"] = int(math.ceil(np.mean(nt)))
+            self._parms["stopping_rounds"] = 0
+
+    def _stopping_metric(self, spec):
+        m = (self._parms.get("stopping_metric") or "auto").lower()
+        if m == "auto":
+            return "logloss" if spec.is_classification else "deviance"
+        return m
+
+    def _score_iteration(self, drv, spec):
+        entry = {"number_of_trees": drv.iter}
+        pred = drv.predictions()
+        raw = pred.view(-1, 1) if pred.dim() == 1 else pred
+        if spec.nclasses == 2:
+            raw = torch.stack([1 - raw[:, 0], raw[:, 0]], 1)
+        m = self._metrics_from_raw(spec, spec.frame, raw, w=drv.w_user)
+        self._add_metrics(entry, "training", m)
+        if spec.valid is not None:
+            self._forest = drv.forest
+            self._init_f = drv.init_f
+            vm = self._metrics_from_raw(spec, spec.valid, self._predict_raw(spec.valid))
+            self._add_metrics(entry, "validation", vm)
+        return entry
+
+    @staticmethod
+    def _add_metrics(entry, prefix, m):
+        if m is None:
+            return
+        for k, name in (("RMSE", "rmse"), ("logloss", "logloss"), ("AUC", "auc"), ("mae", "mae"),
+                        ("mean_residual_deviance", "deviance"), ("MSE", "mse"), ("pr_auc", "aucpr"),
+                        ("mean_per_class_error", "mean_per_class_error"), ("r2", "r2")):
+            v = m.get(k)
+            if v is not None:
+                entry[f"{prefix}_{name}"] = v
+        if m.get("cm") is not None and m.kind in ("binomial", "multinomial"):
+            entry[f"{prefix}_classification_error"] = m["cm"]["total_error"]
+            entry[f"{prefix}_misclassification"] = m["cm"]["total_error"]
+
+    def _resume_from(self, drv, ck):
+        from ...core import dkv
+        prev = dkv.get(ck) if isinstance(ck, str) else ck
+        if prev is None:
+            raise ValueError(f"checkpoint {ck} not found")
+        drv.forest = Forest()
+        for t, k in zip(prev._forest.trees, prev._forest.tclass):
+            drv.forest.add(t, k)
+        drv.init_f = list(prev._init_f)
+        X = self._score_matrix(drv.spec.frame)
+        drv.f = torch.tensor(drv.init_f, dtype=torch.float32, device=drv.dev).view(1, -1).repeat(X.shape[1], 1)
+        drv.f += drv.forest.predict(X, drv.K)
+        drv.iter = len(drv.forest) // drv.K
+
+    def _predict_link(self, frame, ntrees=None):
+        X = self._score_matrix(frame)
+        K = self._K
+        upto = None if ntrees is None else ntrees * K
+        f = self._forest.predict(X, K, upto=upto)
+        f = f + torch.tensor(self._init_f, dtype=torch.float32, device=f.device).view(1, -1)
+        off = self._spec.offset_column
+        if off and off in frame.names:
+            f = f + torch.nan_to_num(frame.vec(off).as_float()).view(-1, 1)
+        return f
+
+    def _predict_raw(self, frame):
+        f = self._predict_link(frame)
+        if self._K > 1:
+            return torch.softmax(f, 1)
+        mu = self._dist.linkinv(f[:, 0])
+        if self._spec.nclasses == 2:
+            cal = getattr(self, "_calibrator", None)
+            if cal is not None:
+                mu = cal(mu)
+            return torch.stack([1 - mu, mu], 1)
+        return mu.view(-1, 1)
+
+    def staged_predict_proba(self, test_data):
+        out = []
+        K = self._K
+        for t in range(1, len(self._forest) // K + 1):
+            f = self._predict_link(test_data, ntrees=t)
+            if K > 1:
+                pr = torch.softmax(f, 1)
+            else:
+                pr = self._dist.linkinv(f[:, 0]).view(-1, 1)
+            out.append(pr)
+        from ...core.vec import Vec, T_REAL
+        vecs, names = [], []
+        for t, pr in enumerate(out):
+            for k in range(pr.shape[1]):
+                vecs.append(Vec(pr[:, k].contiguous(), T_REAL))
+                names.append(f"T{t + 1}.C{k + 1}")
+        return H2OFrame.from_vecs(vecs, names)
+
+    def predict_contributions(self, test_data, output_format="Original", top_n=None, bottom_n=None,
+                              compare_abs=False, background_frame=None):
+        from .shap import tree_contributions
+        return tree_contributions(self, test_data)
+
+
+def _weighted_quantile(x, w, q):
+    if x.numel() == 0:
+        return 0.0
+    if cloud.is_distributed():
+        x = coll.all_gather_var(x)
+        w = coll.all_gather_var(w)
+    o = torch.argsort(x)
+    xs, ws = x[o].to(torch.float64), w[o].to(torch.float64)
+    cw = torch.cumsum(ws, 0)
+    t = q * float(cw[-1])
+    i = int(torch.searchsorted(cw, torch.tensor([t], dtype=cw.dtype, device=cw.device)).clamp(max=xs.numel() - 1))
+    return float(xs[i])
+
+
+def _segmented_wquantile(idx, x, w, L, q):
+    """Weighted q-quantile of x within each segment id (host loop over leaves
+    after one device sort by (segment, value))."""
+    if cloud.is_distributed():
+        idx = coll.all_gather_var(idx)
+        x = coll.all_gather_var(x)
+        w = coll.all_gather_var(w)
+    m = w > 0
+    idx, x, w = idx[m], x[m], w[m]
+    key = idx.to(torch.float64) * 0 + x
+    o = torch.argsort(x)
+    idx, x, w = idx[o], x[o], w[o]
+    o2 = torch.argsort(idx, stable=True)
+    idx, x, w = idx[o2], x[o2], w[o2]
+    out = np.zeros(L)
+    counts = torch.bincount(idx, minlength=L).cpu().numpy()
+    starts = np.concatenate([[0], np.cumsum(counts)[:-1]])
+    xh, wh = x.cpu().numpy(), w.cpu().numpy()
+    for l in range(L):
+        s, c = starts[l], counts[l]
+        if c == 0:
+            continue
+        cw = np.cumsum(wh[s:s + c])
+        j = int(np.searchsorted(cw, q * cw[-1]))
+        out[l] = xh[s + min(j, c - 1)]
+    return out

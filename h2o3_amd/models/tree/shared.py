@@ -1,0 +1,263 @@
+"""Shared tree model machinery: feature prep, binning, forest packing and
+GPU scoring, variable importance, leaf-node assignment.
+
+Reference: hex/tree/SharedTree.java (driver skeleton),
+hex/tree/SharedTreeModel.java (score0, varimp, predictLeafNodeAssignment),
+hex/tree/CompressedForest.java.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import numpy as np
+import torch
+
+from ...core.frame import H2OFrame
+from ...core.vec import T_ENUM, T_INT, T_REAL, Vec
+from ...ops import _native
+from ...parallel import cloud
+from ..base import H2OEstimator
+from .binning import bin_frame_tensors
+from .engine import Tree
+
+_c_void = ctypes.c_void_p
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+class Forest:
+    """Flattened struct-of-arrays forest for the scoring kernel."""
+
+    def __init__(self):
+        self.trees: list[Tree] = []
+        self.tclass: list[int] = []
+        self._packed = None
+
+    def add(self, tree: Tree, k: int = 0):
+        self.trees.append(tree)
+        self.tclass.append(k)
+        self._packed = None
+
+    def __len__(self):
+        return len(self.trees)
+
+    def pack(self, device, upto=None):
+        trees = self.trees if upto is None else self.trees[:upto]
+        key = (str(device), len(trees))
+        if self._packed is not None and self._packed[0] == key:
+            return self._packed[1]
+        feat, thr, left, right, nal, coff, clen, val, roots, bits = [], [], [], [], [], [], [], [], [], []
+        base = 0
+        nb = 0
+        for t in trees:
+            roots.append(base)
+            for i in range(t.n_nodes):
+                feat.append(max(t.feat[i], 0))
+                thr.append(t.thr[i] if not math.isnan(t.thr[i]) else 0.0)
+                left.append(t.left[i] + base if t.left[i] >= 0 else -1)
+                right.append(t.right[i] + base if t.right[i] >= 0 else -1)
+                nal.append(1 if t.na_left[i] else 0)
+                if t.is_cat[i] and t.cat_left[i] is not None:
+                    coff.append(nb)
+                    clen.append(len(t.cat_left[i]))
+                    bits.extend(int(b) for b in t.cat_left[i])
+                    nb += len(t.cat_left[i])
+                else:
+                    coff.append(-1)
+                    clen.append(0)
+                val.append(t.value[i])
+            base += t.n_nodes
+        d = device
+        P = {"feat": torch.tensor(feat, dtype=torch.int32, device=d),
+             "thr": torch.tensor(thr, dtype=torch.float32, device=d),
+             "left": torch.tensor(left, dtype=torch.int32, device=d),
+             "right": torch.tensor(right, dtype=torch.int32, device=d),
+             "na_left": torch.tensor(nal, dtype=torch.uint8, device=d),
+             "cat_off": torch.tensor(coff, dtype=torch.int32, device=d),
+             "cat_len": torch.tensor(clen, dtype=torch.int32, device=d),
+             "cat_bits": torch.tensor(bits or [0], dtype=torch.uint8, device=d),
+             "value": torch.tensor(val, dtype=torch.float32, device=d),
+             "roots": torch.tensor(roots, dtype=torch.int32, device=d),
+             "tclass": torch.tensor(self.tclass[: len(trees)], dtype=torch.int32, device=d),
+             "T": len(trees)}
+        self._packed = (key, P)
+        return P
+
+    def predict(self, X: torch.Tensor, K: int, upto=None, leaf=False):
+        """X: [F, N] float32 column-major.  Returns [N, K] sums (or leaf ids)."""
+        N = X.shape[1]
+        P = self.pack(X.device, upto)
+        T = P["T"]
+        out = torch.zeros((N, K), dtype=torch.float32, device=X.device)
+        leaf_out = torch.empty((N, T), dtype=torch.int32, device=X.device) if leaf else None
+        if T == 0:
+            return leaf_out if leaf else out
+        if X.device.type == "cuda":
+            lib = _native.get_lib("tree_predict")
+            if not getattr(lib, "_typed", False):
+                lib.h2o_forest_predict.argtypes = [_c_void, ctypes.c_longlong] + [_c_void] * 12 + \
+                    [ctypes.c_int, ctypes.c_int, _c_void, _c_void, _c_void]
+                lib._typed = True
+            X = X.contiguous().to(torch.float32)
+            rc = lib.h2o_forest_predict(_ptr(X), N, _ptr(P["feat"]), _ptr(P["thr"]), _ptr(P["left"]),
+                                        _ptr(P["right"]), _ptr(P["na_left"]), _ptr(P["cat_off"]),
+                                        _ptr(P["cat_len"]), _ptr(P["cat_bits"]), _ptr(P["value"]),
+                                        _ptr(P["roots"]), _ptr(P["tclass"]), T, K,
+                                        _ptr(out) if not leaf else ctypes.c_void_p(0),
+                                        _ptr(leaf_out) if leaf else ctypes.c_void_p(0),
+                                        ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+            if rc != 0:
+                raise RuntimeError(f"h2o_forest_predict failed: {rc}")
+            return leaf_out if leaf else out
+        return self._predict_torch(X, K, P, leaf)
+
+    @staticmethod
+    def _predict_torch(X, K, P, leaf=False):
+        N = X.shape[1]
+        T = P["T"]
+        out = torch.zeros((N, K), dtype=torch.float32, device=X.device)
+        leaf_out = torch.empty((N, T), dtype=torch.int32, device=X.device) if leaf else None
+        ar = torch.arange(N, device=X.device)
+        for t in range(T):
+            nd = torch.full((N,), int(P["roots"][t]), dtype=torch.int64, device=X.device)
+            while True:
+                l = P["left"][nd].long()
+                active = l >= 0
+                if not bool(active.any()):
+                    break
+                f = P["feat"][nd].long()
+                x = X[f, ar]
+                isnan = torch.isnan(x)
+                co = P["cat_off"][nd].long()
+                cl = P["cat_len"][nd].long()
+                code = torch.nan_to_num(x, nan=-1).long()
+                in_rng = (code >= 0) & (code < cl)
+                bit = P["cat_bits"][(co + code.clamp(min=0)).clamp(min=0, max=P["cat_bits"].numel() - 1)] != 0
+                nal = P["na_left"][nd] != 0
+                go_cat = torch.where(isnan | ~in_rng, nal, bit)
+                go_num = torch.where(isnan, nal, x < P["thr"][nd])
+                go = torch.where(co >= 0, go_cat, go_num)
+                nxt = torch.where(go, l, P["right"][nd].long())
+                nd = torch.where(active, nxt, nd)
+            if leaf:
+                leaf_out[:, t] = (nd - int(P["roots"][t])).to(torch.int32)
+            else:
+                out[ar, int(P["tclass"][t])] += P["value"][nd]
+        return leaf_out if leaf else out
+
+
+class SharedTreeEstimator(H2OEstimator):
+    """Base of GBM / DRF / XGBoost / IsolationForest / UpliftDRF."""
+
+    def _feature_inputs(self, frame: H2OFrame, x):
+        feats, is_cat, cards = [], [], []
+        domains = {}
+        for n in x:
+            v = frame.vec(n)
+            if v.type == T_ENUM:
+                feats.append(v.data)
+                is_cat.append(True)
+                cards.append(len(v.domain))
+                domains[n] = list(v.domain)
+            else:
+                feats.append(v.as_float(torch.float32) if v.data.dtype != torch.float64 else v.data.to(torch.float32))
+                is_cat.append(False)
+                cards.append(0)
+        return feats, is_cat, cards, domains
+
+    def _bin(self, spec, hist_type=None, nbins=None, want_col_major=True):
+        p = self._parms
+        feats, is_cat, cards, domains = self._feature_inputs(spec.frame, spec.x)
+        self._x_domains = domains
+        self._x_is_cat = is_cat
+        bd = bin_frame_tensors(feats, is_cat, cards, spec.x,
+                               hist_type=hist_type or p.get("histogram_type", "AUTO"),
+                               nbins=nbins or p.get("nbins", 20), nbins_top_level=p.get("nbins_top_level", 1024),
+                               nbins_cats=p.get("nbins_cats", 1024),
+                               seed=(p.get("seed") if p.get("seed") not in (None, -1) else 1234),
+                               want_col_major=want_col_major)
+        return bd
+
+    def _score_matrix(self, frame: H2OFrame) -> torch.Tensor:
+        """[F, N] float32 column-major scoring matrix adapted to training."""
+        x = self._spec.x
+        cols = []
+        for n in x:
+            if n not in frame.names:
+                cols.append(torch.full((frame.nlocal,), float("nan"), device=cloud.device()))
+                continue
+            v = frame.vec(n)
+            if n in self._x_domains:
+                codes = self._adapt_enum(v, self._x_domains[n])
+                c = codes.to(torch.float32)
+                cols.append(torch.where(codes < 0, torch.full_like(c, float("nan")), c))
+            else:
+                cols.append(v.as_float(torch.float32) if not v.on_host else
+                            torch.full((frame.nlocal,), float("nan"), device=cloud.device()))
+        if not cols:
+            return torch.zeros((0, frame.nlocal), device=cloud.device())
+        return torch.stack(cols, 0).contiguous()
+
+    def _varimp_from_forest(self, forest: Forest, names):
+        vi = {n: 0.0 for n in names}
+        for t in forest.trees:
+            for i in range(t.n_nodes):
+                if t.left[i] >= 0:
+                    vi[names[t.feat[i]]] += max(t.gain[i], 0.0)
+        return vi
+
+    def predict_leaf_node_assignment(self, test_data, type="Path"):
+        X = self._score_matrix(test_data)
+        K = self._n_tree_classes()
+        leaf = self._forest.predict(X, K, leaf=True)
+        names = []
+        ntrees_iter = len(self._forest) // max(K, 1)
+        for t in range(len(self._forest)):
+            k = self._forest.tclass[t]
+            it = t // max(K, 1)
+            cls = "" if K == 1 else f".C{k + 1}"
+            names.append(f"T{it + 1}{cls}")
+        if type == "Node_ID":
+            vecs = [Vec(leaf[:, t].to(torch.float32).contiguous(), T_INT) for t in range(leaf.shape[1])]
+            return H2OFrame.from_vecs(vecs, names)
+        # Path: string of L/R decisions
+        paths = []
+        lh = leaf.cpu().numpy()
+        for t, tree in enumerate(self._forest.trees):
+            pmap = _paths(tree)
+            paths.append([pmap.get(int(n), "") for n in lh[:, t]])
+        from ...core.vec import make_enum_from_strings
+        vecs = [make_enum_from_strings(p) for p in paths]
+        return H2OFrame.from_vecs(vecs, names)
+
+    def _n_tree_classes(self):
+        return 1
+
+    def staged_predict_proba(self, test_data):
+        raise NotImplementedError
+
+    @property
+    def ntrees_built(self):
+        return len(self._forest) // max(1, self._n_tree_classes())
+
+    def get_tree(self, tree_number=0, tree_class=None):
+        K = self._n_tree_classes()
+        idx = tree_number * K + (0 if tree_class is None else (tree_class if isinstance(tree_class, int) else
+                                                               self._spec.response_domain.index(tree_class)))
+        return self._forest.trees[idx]
+
+
+def _paths(tree: Tree):
+    out = {}
+    stack = [(0, "")]
+    while stack:
+        i, p = stack.pop()
+        if tree.left[i] < 0:
+            out[i] = p
+        else:
+            stack.append((tree.left[i], p + "L"))
+            stack.append((tree.right[i], p + "R"))
+    return out

@@ -1,0 +1,217 @@
+"""Python entry points for the tree-engine kernels (HIP on GPU, torch on CPU).
+
+`hist_build`, `partition` and `fill_nid` dispatch to libtree_hist.so on a
+GPU device; the torch implementations below are the fp32 references used
+on CPU and by the numerics tests.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _native
+
+_LDS_BUDGET = 64 * 1024   # bytes of LDS histogram per workgroup (2 WG / CU)
+_c_void = ctypes.c_void_p
+_c_int = ctypes.c_int
+_c_ll = ctypes.c_longlong
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _lib():
+    lib = _native.get_lib("tree_hist")
+    if lib is not None and not getattr(lib, "_typed", False):
+        lib.h2o_hist_build.argtypes = [_c_void, _c_int, _c_int, _c_void, _c_void, _c_void, _c_void, _c_int,
+                                       _c_int, _c_int, _c_int, _c_void, _c_int, _c_int, _c_int, _c_void]
+        lib.h2o_part_count.argtypes = [_c_void, _c_int, _c_ll, _c_ll, _c_void, _c_void, _c_int, _c_void,
+                                       _c_void, _c_int, _c_void, _c_void]
+        lib.h2o_part_scatter.argtypes = [_c_void, _c_int, _c_ll, _c_ll, _c_void, _c_void, _c_int, _c_void,
+                                         _c_void, _c_int, _c_void, _c_void, _c_void, _c_void]
+        lib.h2o_fill_nid.argtypes = [_c_void, _c_void, _c_int, _c_void, _c_void]
+        lib._typed = True
+    return lib
+
+
+def channels(mode: int) -> int:
+    return 3 if mode == 0 else (2 if mode == 1 else 1)
+
+
+def feature_group(F: int, Bs: int, mode: int, budget: int = _LDS_BUDGET) -> int:
+    C = channels(mode)
+    fg = budget // (Bs * C * 4)
+    fg = max(4, (fg // 4) * 4)
+    return min(fg, ((F + 3) // 4) * 4)
+
+
+def make_work(starts, counts, slots, chunk):
+    """Chunk node segments into (slot, start, count, chunk_id) work items (host)."""
+    items = []
+    for st, ct, sl in zip(starts, counts, slots):
+        if ct <= 0:
+            continue
+        k = 0
+        p = st
+        end = st + ct
+        while p < end:
+            c = min(chunk, end - p)
+            items.append((sl, p, c, k))
+            p += c
+            k += 1
+    return items
+
+
+def hist_build(bd, ridx, va, vb, mode, starts, counts, n_slots, use_native=None, target_blocks=2048):
+    """Histograms of the row segments [starts[i], starts[i]+counts[i]) of
+    ridx into slot i.  Returns hist [F, n_slots, Bs, C] float32."""
+    C = channels(mode)
+    dev = ridx.device
+    hist = torch.zeros((bd.F, n_slots, bd.Bs, C), dtype=torch.float64, device=dev)
+    native = dev.type == "cuda" if use_native is None else use_native
+    if native:
+        lib = _lib()
+        FG = feature_group(bd.F, bd.Bs, mode)
+        n_fg = (bd.F + FG - 1) // FG
+        total = int(sum(counts))
+        if total == 0:
+            return hist
+        tgt_chunks = max(1, target_blocks // n_fg)
+        chunk = max(2048, -(-total // tgt_chunks))
+        items = make_work(starts, counts, range(n_slots), chunk)
+        if not items:
+            return hist
+        work = torch.tensor(items, dtype=torch.int32).to(dev, non_blocking=True)
+        threads = 1024 if chunk >= 8192 else 256
+        rc = lib.h2o_hist_build(_ptr(bd.codes), bd.code_bytes, bd.Fp, _ptr(ridx), _ptr(va), _ptr(vb), _ptr(work),
+                                len(items), bd.F, FG, bd.Bs, _ptr(hist), n_slots, mode, threads, _stream())
+        if rc != 0:
+            raise RuntimeError(f"h2o_hist_build failed: hip error {rc}")
+        return hist
+    return _hist_build_torch(bd, ridx, va, vb, mode, starts, counts, hist)
+
+
+def _hist_build_torch(bd, ridx, va, vb, mode, starts, counts, hist):
+    F, Bs = bd.F, bd.Bs
+    C = channels(mode)
+    codes = bd.codes
+    for slot, (st, ct) in enumerate(zip(starts, counts)):
+        if ct <= 0:
+            continue
+        r = ridx[st: st + ct].long()
+        a = va[r].to(torch.float32)
+        if mode == 0:
+            w = vb[r].to(torch.float32) if vb is not None else torch.ones_like(a)
+            vals = torch.stack([w, w * a, w * a * a], 1)
+        elif mode == 1:
+            vals = torch.stack([a, vb[r].to(torch.float32)], 1)
+        else:
+            w = vb[r].to(torch.float32) if vb is not None else torch.ones_like(a)
+            vals = w.reshape(-1, 1)
+        cd = codes[r][:, :F].to(torch.int64)  # [n, F]
+        idx = (torch.arange(F, device=cd.device).reshape(1, F) * Bs + cd).reshape(-1)
+        flat = torch.zeros((F * Bs, C), dtype=torch.float64, device=cd.device)
+        v = vals.unsqueeze(1).expand(-1, F, C).reshape(-1, C).to(torch.float64)
+        flat.index_add_(0, idx, v)
+        hist[:, slot] = flat.reshape(F, Bs, C)
+    return hist
+
+
+def partition(bd, ridx, ridx_out, feats, masks, starts, counts, use_native=None, chunk=16384):
+    """Stable-partition each segment i by masks[i][code(row, feats[i])] (1 =
+    left).  Writes ridx_out and returns per-segment left counts (host list)."""
+    dev = ridx.device
+    n = len(starts)
+    if n == 0:
+        return []
+    native = dev.type == "cuda" if use_native is None else use_native
+    if native:
+        lib = _lib()
+        items = make_work(starts, counts, range(n), chunk)
+        if not items:
+            return [0] * n
+        work = torch.tensor(items, dtype=torch.int32).to(dev, non_blocking=True)
+        nw = len(items)
+        feat_t = torch.as_tensor(feats, dtype=torch.int32).to(dev)
+        masks = masks.to(torch.uint8).contiguous()
+        cnt = torch.empty(nw, dtype=torch.int32, device=dev)
+        if bd.codes_col is not None:
+            codes, rs, fs = bd.codes_col, 1, bd.nrows_local
+        else:
+            codes, rs, fs = bd.codes, bd.Fp, 1
+        rc = lib.h2o_part_count(_ptr(codes), bd.code_bytes, rs, fs, _ptr(ridx), _ptr(work), nw, _ptr(feat_t),
+                                _ptr(masks), bd.Bs, _ptr(cnt), _stream())
+        if rc != 0:
+            raise RuntimeError(f"h2o_part_count failed: {rc}")
+        # per-node exclusive scans of the chunk counts (chunks of a node are consecutive)
+        wk = torch.tensor(items, dtype=torch.int64)
+        cnt_h = cnt.cpu().to(torch.int64)
+        slot = wk[:, 0]
+        nleft = torch.zeros(n, dtype=torch.int64).index_add_(0, slot, cnt_h)
+        csum = torch.cumsum(cnt_h, 0) - cnt_h   # global exclusive
+        first = torch.zeros(n, dtype=torch.int64)
+        # exclusive within node = global exclusive - global exclusive at node's first chunk
+        node_first = {}
+        for i, s in enumerate(slot.tolist()):
+            node_first.setdefault(s, i)
+        first_idx = torch.tensor([node_first[s] for s in slot.tolist()], dtype=torch.int64)
+        lpre = csum - csum[first_idx]
+        posinnode = wk[:, 1] - torch.tensor(starts, dtype=torch.int64)[slot]
+        rpre = posinnode - lpre
+        st = torch.tensor(starts, dtype=torch.int64)[slot]
+        loff = (st + lpre).to(torch.int32)
+        roff = (st + nleft[slot] + rpre).to(torch.int32)
+        loff_d = loff.to(dev, non_blocking=True)
+        roff_d = roff.to(dev, non_blocking=True)
+        rc = lib.h2o_part_scatter(_ptr(codes), bd.code_bytes, rs, fs, _ptr(ridx), _ptr(work), nw, _ptr(feat_t),
+                                  _ptr(masks), bd.Bs, _ptr(loff_d), _ptr(roff_d), _ptr(ridx_out), _stream())
+        if rc != 0:
+            raise RuntimeError(f"h2o_part_scatter failed: {rc}")
+        return nleft.tolist()
+    out = []
+    for i, (st, ct) in enumerate(zip(starts, counts)):
+        seg = ridx[st: st + ct]
+        if bd.codes_col is not None:
+            c = bd.codes_col[feats[i]][seg.long()].to(torch.int64)
+        else:
+            c = bd.codes[seg.long(), feats[i]].to(torch.int64)
+        left = masks[i].to(torch.bool)[c]
+        l = seg[left]
+        r = seg[~left]
+        ridx_out[st: st + l.numel()] = l
+        ridx_out[st + l.numel(): st + ct] = r
+        out.append(int(l.numel()))
+    return out
+
+
+def fill_nid(ridx, leaf_ids, starts, counts, nrows, use_native=None):
+    """Per-row leaf index from leaf segments."""
+    dev = ridx.device
+    nid = torch.full((nrows,), -1, dtype=torch.int32, device=dev)
+    native = dev.type == "cuda" if use_native is None else use_native
+    if native:
+        lib = _lib()
+        items = [(lid, st, ct, 0) for lid, st, ct in zip(leaf_ids, starts, counts) if ct > 0]
+        # split long segments
+        items2 = []
+        for lid, st, ct, _ in items:
+            p = st
+            while p < st + ct:
+                c = min(65536, st + ct - p)
+                items2.append((lid, p, c, 0))
+                p += c
+        if items2:
+            work = torch.tensor(items2, dtype=torch.int32).to(dev, non_blocking=True)
+            rc = lib.h2o_fill_nid(_ptr(ridx), _ptr(work), len(items2), _ptr(nid), _stream())
+            if rc != 0:
+                raise RuntimeError(f"h2o_fill_nid failed: {rc}")
+        return nid
+    for lid, st, ct in zip(leaf_ids, starts, counts):
+        nid[ridx[st: st + ct].long()] = lid
+    return nid

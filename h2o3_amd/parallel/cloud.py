@@ -1,0 +1,118 @@
+"""Cloud formation: one process per GPU over torch.distributed.
+
+Replaces the reference's JVM cloud (water/H2O.java, water/Paxos.java,
+water/HeartBeatThread.java): instead of multicast/flatfile discovery and a
+Paxos-agreed member list, the launcher (torchrun / the bench driver) provides
+RANK / WORLD_SIZE / MASTER_ADDR and every rank joins one process group.  The
+backend is "nccl" (= RCCL over xGMI) when GPUs are present and "gloo" on CPU.
+
+Every rank holds a contiguous row shard of every Frame; collectives are
+issued SPMD by all ranks in the same order (like MRTask's reduce tree).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+import socket
+import time
+
+import torch
+import torch.distributed as dist
+
+_state = {"initialized": False, "device": None, "rank": 0, "world": 1, "local_rank": 0,
+          "backend": None, "start": time.time(), "owns_pg": False, "name": None}
+
+
+def _env_int(k, d):
+    try:
+        return int(os.environ.get(k, d))
+    except ValueError:
+        return d
+
+
+def init(device: str | None = None, backend: str | None = None, timeout_s: float = 1800.0,
+         name: str | None = None):
+    """Join (or create) the cloud.  Idempotent."""
+    if _state["initialized"]:
+        return info()
+    world = _env_int("WORLD_SIZE", 1)
+    rank = _env_int("RANK", 0)
+    local_rank = _env_int("LOCAL_RANK", rank)
+    want_gpu = torch.cuda.is_available() and (device is None or str(device).startswith("cuda"))
+    if device is None:
+        device = f"cuda:{local_rank % max(1, torch.cuda.device_count())}" if want_gpu else "cpu"
+    dev = torch.device(device)
+    if dev.type == "cuda":
+        torch.cuda.set_device(dev)
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29511")
+        be = backend or ("nccl" if dev.type == "cuda" else "gloo")
+        kw = {}
+        if be == "nccl":
+            kw["device_id"] = dev
+        dist.init_process_group(be, rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=timeout_s), **kw)
+        _state["owns_pg"] = True
+    if dist.is_initialized():
+        rank, world = dist.get_rank(), dist.get_world_size()
+        _state["backend"] = dist.get_backend()
+    _state.update(initialized=True, device=dev, rank=rank, world=world, local_rank=local_rank,
+                  name=name or f"h2o3_amd_{os.getpid()}")
+    return info()
+
+
+def ensure():
+    if not _state["initialized"]:
+        init()
+
+
+def device() -> torch.device:
+    ensure()
+    return _state["device"]
+
+
+def rank() -> int:
+    ensure()
+    return _state["rank"]
+
+
+def world() -> int:
+    ensure()
+    return _state["world"]
+
+
+def is_distributed() -> bool:
+    ensure()
+    return _state["world"] > 1
+
+
+def is_gpu() -> bool:
+    return device().type == "cuda"
+
+
+def info() -> dict:
+    d = _state["device"]
+    props = None
+    if d is not None and d.type == "cuda":
+        p = torch.cuda.get_device_properties(d)
+        props = {"name": p.name, "total_memory_gb": round(p.total_memory / 2**30, 1),
+                 "cus": getattr(p, "multi_processor_count", None),
+                 "arch": getattr(p, "gcnArchName", None)}
+    return {"cloud_name": _state["name"], "rank": _state["rank"], "cloud_size": _state["world"],
+            "device": str(d), "backend": _state["backend"], "gpu": props,
+            "uptime_s": round(time.time() - _state["start"], 1), "host": socket.gethostname()}
+
+
+def shutdown():
+    if _state["owns_pg"] and dist.is_initialized():
+        dist.destroy_process_group()
+    _state.update(initialized=False, owns_pg=False)
+
+
+def barrier():
+    if is_distributed():
+        if is_gpu():
+            dist.barrier(device_ids=[device().index])
+        else:
+            dist.barrier()
