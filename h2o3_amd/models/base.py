@@ -228,6 +228,12 @@ class H2OEstimator:
         x, y = self._resolve_columns(x, y, training_frame)
         p["response_column"] = y
         self._check_response(training_frame, y)
+        if y is not None and self._wants_categorical_response() and training_frame.vec(y).type != T_ENUM:
+            training_frame = training_frame[:, :]
+            training_frame[y] = training_frame[y].asfactor()
+            if validation_frame is not None and y in validation_frame.names:
+                validation_frame = validation_frame[:, :]
+                validation_frame[y] = validation_frame[y].asfactor()
         self._start_time = int(time.time() * 1000)
         t0 = time.time()
         spec = TrainSpec(training_frame, x, y, p.get("weights_column"), p.get("offset_column"),
@@ -245,6 +251,12 @@ class H2OEstimator:
 
     def _check_response(self, frame, y):
         pass
+
+    def _wants_categorical_response(self):
+        """Family/distribution implies classification (reference converts the
+        response to categorical, e.g. GLM binomial on a 0/1 column)."""
+        fam = str(self._parms.get("family") or self._parms.get("distribution") or "").lower()
+        return fam in ("binomial", "bernoulli", "multinomial", "ordinal", "quasibinomial_cls")
 
     def _fit(self, spec: TrainSpec):
         raise NotImplementedError

@@ -1,0 +1,80 @@
+import numpy as np
+import pandas as pd
+import pytest
+
+import h2o3_amd
+from h2o3_amd.estimators import H2OGeneralizedLinearEstimator as GLM
+
+
+def _frame(n=4000, seed=0, family="gaussian"):
+    rng = np.random.RandomState(seed)
+    X = rng.randn(n, 4)
+    eta = 0.5 + X[:, 0] - 2 * X[:, 1] + 0.3 * X[:, 2]
+    if family == "gaussian":
+        y = eta + 0.5 * rng.randn(n)
+    elif family == "binomial":
+        y = (rng.rand(n) < 1 / (1 + np.exp(-eta))).astype(int)
+    elif family == "poisson":
+        y = rng.poisson(np.exp(0.3 * eta)).astype(float)
+    df = pd.DataFrame(X, columns=list("abcd"))
+    df["y"] = y
+    return df
+
+
+def test_glm_gaussian_matches_ols():
+    df = _frame()
+    fr = h2o3_amd.H2OFrame(df)
+    m = GLM(family="gaussian", lambda_=0, compute_p_values=True)
+    m.train(y="y", training_frame=fr)
+    X = np.c_[df[list("abcd")].values, np.ones(len(df))]
+    b = np.linalg.lstsq(X, df["y"].values, rcond=None)[0]
+    c = m.coef()
+    np.testing.assert_allclose([c["a"], c["b"], c["c"], c["d"], c["Intercept"]], b, rtol=1e-5, atol=1e-6)
+    assert m.coef_with_p_values()["p_value"].iloc[1] < 1e-10
+
+
+def test_glm_binomial_matches_sklearn():
+    from sklearn.linear_model import LogisticRegression
+    df = _frame(family="binomial")
+    fr = h2o3_amd.H2OFrame(df)
+    m = GLM(family="binomial", lambda_=0)
+    m.train(y="y", training_frame=fr)
+    lr = LogisticRegression(penalty=None, tol=1e-10, max_iter=1000).fit(df[list("abcd")].values, df["y"].values)
+    c = m.coef()
+    np.testing.assert_allclose([c[k] for k in "abcd"], lr.coef_[0], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(c["Intercept"], lr.intercept_[0], rtol=1e-4, atol=1e-5)
+    assert m.auc() > 0.8
+
+
+def test_glm_elastic_net_matches_sklearn():
+    from sklearn.linear_model import ElasticNet
+    df = _frame(seed=3)
+    fr = h2o3_amd.H2OFrame(df)
+    m = GLM(family="gaussian", alpha=0.5, lambda_=0.05, standardize=False)
+    m.train(y="y", training_frame=fr)
+    en = ElasticNet(alpha=0.05, l1_ratio=0.5, tol=1e-12, max_iter=100000).fit(df[list("abcd")].values, df["y"].values)
+    c = m.coef()
+    np.testing.assert_allclose([c[k] for k in "abcd"], en.coef_, rtol=1e-3, atol=1e-4)
+
+
+def test_glm_poisson_and_lambda_search():
+    df = _frame(family="poisson", seed=4)
+    fr = h2o3_amd.H2OFrame(df)
+    m = GLM(family="poisson", lambda_search=True, nlambdas=20)
+    m.train(y="y", training_frame=fr)
+    c = m.coef()
+    assert abs(c["b"] - (-0.6)) < 0.1
+    assert len(m.getGLMRegularizationPath(m)["lambdas"]) == 20
+
+
+def test_glm_multinomial():
+    rng = np.random.RandomState(5)
+    X = rng.randn(3000, 3)
+    cls = np.argmax(np.c_[X[:, 0], X[:, 1], -X[:, 0] - X[:, 1]] * 2 + rng.randn(3000, 3) * 0.5, 1)
+    df = pd.DataFrame(X, columns=list("abc"))
+    df["y"] = np.array(["u", "v", "w"])[cls]
+    fr = h2o3_amd.H2OFrame(df)
+    m = GLM(family="multinomial", lambda_=0)
+    m.train(y="y", training_frame=fr)
+    assert m.logloss() < 0.6
+    assert m.predict(fr).ncols == 4

@@ -102,7 +102,7 @@ def test_gbm_gpu_end_to_end_quality():
     logit = X[:, 0] * 2 - X[:, 1] + X[:, 2] * X[:, 3]
     y = (rng.rand(n) < 1 / (1 + np.exp(-logit))).astype(int)
     df = pd.DataFrame(X, columns=[f"x{i}" for i in range(10)])
-    df["y"] = y.astype(str)
+    df["y"] = np.where(y == 1, "yes", "no")
     fr = h2o3_amd.H2OFrame(df)
     m = H2OGradientBoostingEstimator(ntrees=30, max_depth=5, seed=3)
     m.train(y="y", training_frame=fr)
