@@ -119,6 +119,9 @@ def main():
         ll = float(-(yy * torch.log(p) + (1 - yy) * torch.log(1 - p)).mean())
         extra["train_logloss_after"] = round(ll, 5)
         extra["trees_built"] = len(drv.forest)
+    from h2o3_amd.utils import timer
+    if timer.ENABLED and rank == 0:
+        print("phases(ms,count):", timer.report(), file=sys.stderr)
     if rank == 0:
         out = {"metric": metric, "value": round(value, 4), "unit": unit, "n_gpus": world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": round(1000 * el / args.steps, 3), "higher_is_better": True,

@@ -28,6 +28,7 @@ import torch
 from ...ops import tree_ops
 from ...parallel import cloud
 from ...parallel import collectives as coll
+from ...utils.timer import phase
 
 NEG_INF = float("-inf")
 
@@ -139,7 +140,8 @@ class TreeGrower:
 
     # ------------------------------------------------------------------ hist
     def _build_hist(self, ridx, va, vb, mode, starts, counts):
-        H = tree_ops.hist_build(self.bd, ridx, va, vb, mode, starts, counts, len(starts))
+        with phase("tree.hist"):
+            H = tree_ops.hist_build(self.bd, ridx, va, vb, mode, starts, counts, len(starts))
         if self.W > 1:
             if self.Fpad > self.bd.F:
                 H = torch.cat([H, torch.zeros((self.Fpad - self.bd.F,) + tuple(H.shape[1:]), dtype=H.dtype,
@@ -171,7 +173,7 @@ class TreeGrower:
             m = np.concatenate([m, np.zeros((n_nodes, self.Fpad - F), dtype=bool)], 1)
         return torch.from_numpy(m)
 
-    def _find_splits(self, H, col_mask, allowed_sets=None):
+    def _find_splits(self, H, col_mask, node_wyy=None):
         """H: [Fl, n, Bs, C] (local feature slice).  Returns dict of per-node
         tensors on device: gain, feat, na_left, mask[n, Bs], stats L/R [n,C],
         tot [n,C]."""
@@ -250,7 +252,7 @@ class TreeGrower:
         allg = torch.where(cm.unsqueeze(2), allg, torch.full_like(allg, NEG_INF))
         # min split improvement (relative to the node's squared error)
         if p.criterion != "xgb":
-            wyy_tot = T[..., 2] if C > 2 else torch.zeros_like(T[..., 0])
+            wyy_tot = node_wyy.view(-1, 1).to(T.dtype) if node_wyy is not None else torch.zeros_like(T[..., 0])
             se_before = (wyy_tot - score(T)).clamp_min(0).unsqueeze(2)
             allg = torch.where(allg > se_before * p.min_split_improvement, allg, torch.full_like(allg, NEG_INF))
             allg = torch.where(se_before > 0, allg, torch.full_like(allg, NEG_INF))
@@ -363,7 +365,17 @@ class TreeGrower:
             can_split = depth < p.max_depth
             if can_split:
                 cm = self._col_mask(n_front, depth)
-                sp = self._find_splits(H, cm)
+                node_wyy = None
+                if mode == 0:
+                    # node totals of w*y*y (only the total enters the SE split test)
+                    with phase("tree.wyy"):
+                        wv = vb if vb is not None else torch.ones_like(va)
+                        s = tree_ops.seg_sum2(ridx, wv * va * va, None, list(range(n_front)),
+                                              [f[1] for f in frontier], [f[2] for f in frontier], n_front)
+                        coll.allreduce_(s)
+                        node_wyy = s[:, 0]
+                with phase("tree.split"):
+                    sp = self._find_splits(H, cm, node_wyy)
                 gains = sp["gain"].cpu()
                 feats = sp["feat"].cpu()
                 Ls = sp["L"].cpu()
@@ -429,8 +441,9 @@ class TreeGrower:
                 wr = float(Rs[i][0] if mode != 1 else Rs[i][1])
                 new_pairs.append((lid, rid, j, wl <= wr))
             # partition
-            ridx2.copy_(ridx)
-            nleft = tree_ops.partition(bd, ridx, ridx2, part_feats, masks, part_starts, part_counts)
+            with phase("tree.partition"):
+                ridx2.copy_(ridx)
+                nleft = tree_ops.partition(bd, ridx, ridx2, part_feats, masks, part_starts, part_counts)
             ridx, ridx2 = ridx2, ridx
             for j, i in enumerate(split_ids):
                 nid_, st, ct, d = frontier[i][:4]
@@ -453,8 +466,10 @@ class TreeGrower:
         self._leaf_segments = []
         leaf_index = {nid_: k for k, nid_ in enumerate(leaves)}
         lids = [leaf_index[s[0]] for s in segs]
-        nid = tree_ops.fill_nid(ridx, lids, [s[1] for s in segs], [s[2] for s in segs], N)
+        with phase("tree.nid"):
+            nid = tree_ops.fill_nid(ridx, lids, [s[1] for s in segs], [s[2] for s in segs], N)
         self.ridx, self.ridx2 = ridx, ridx2
+        self.last_segs = (lids, [s[1] for s in segs], [s[2] for s in segs])
         leaf_tot_t = torch.stack([torch.as_tensor(x, dtype=torch.float64) for x in leaf_tot]) if leaf_tot else \
             torch.zeros((0, C), dtype=torch.float64)
         return tree, nid, leaves, leaf_tot_t

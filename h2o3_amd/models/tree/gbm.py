@@ -27,6 +27,8 @@ from ...parallel import collectives as coll
 from ..base import ScoreKeeper, _LESS_IS_BETTER
 from ..distributions import get_distribution
 from .engine import GrowParams, TreeGrower
+from ...ops import tree_ops
+from ...utils.timer import phase
 from .shared import Forest, SharedTreeEstimator
 
 GBM_DEFAULTS = dict(ntrees=50, max_depth=5, min_rows=10.0, nbins=20, nbins_top_level=1024, nbins_cats=1024,
@@ -186,17 +188,21 @@ class GBMDriver:
         if self.K == 1:
             f = self.f[:, 0]
             y = self.yb if self.spec.nclasses == 2 else torch.nan_to_num(self.yf)
-            z = self.dist.neg_half_gradient(y, f).to(torch.float32)
+            with phase("gbm.grad"):
+                z = self.dist.neg_half_gradient(y, f).to(torch.float32)
             if self.dist.family == "huber":
                 self._update_huber_delta(y, f, w)
                 z = self.dist.neg_half_gradient(y, f).to(torch.float32)
-            tree, nid, leaves, tot = self.grower.grow(z.contiguous(), w.contiguous(), 0)
-            vals = self._gamma(tree, nid, leaves, w, y, z, f, 0)
+            with phase("gbm.grow"):
+                tree, nid, leaves, tot = self.grower.grow(z.contiguous(), w.contiguous(), 0)
+            with phase("gbm.gamma"):
+                vals = self._gamma(tree, nid, leaves, w, y, z, f, 0)
             vals = np.clip(vals, -maxabs, maxabs)
             for li, node in enumerate(leaves):
                 tree.value[node] = float(lr * vals[li])
-            vt = torch.tensor(lr * vals, dtype=torch.float32, device=self.dev)
-            self.f[:, 0] += vt[nid.long()]
+            with phase("gbm.update"):
+                vt = torch.tensor(lr * vals, dtype=torch.float32, device=self.dev)
+                self.f[:, 0] += vt[nid.long()]
             self.forest.add(tree, 0)
         else:
             P = torch.softmax(self.f, 1)
@@ -240,29 +246,25 @@ class GBMDriver:
             coll.allreduce_(s)
             num, den = s[:L], s[L:]
             return (mt + torch.where(den > 0, num / den.clamp_min(1e-300), torch.zeros_like(num))).cpu().numpy()
-        num_r = self.dist.gamma_num(w, y, z, f).to(torch.float64)
-        den_r = self.dist.gamma_denom(w, y, z, f).to(torch.float64)
-        s = torch.zeros(2 * L, dtype=torch.float64, device=self.dev)
-        s[:L].index_add_(0, idx, num_r)
-        s[L:].index_add_(0, idx, den_r)
+        num_r = self.dist.gamma_num(w, y, z, f)
+        den_r = self.dist.gamma_denom(w, y, z, f)
+        lids, st, ct = self.grower.last_segs
+        s = tree_ops.seg_sum2(self.grower.ridx, num_r, den_r, lids, st, ct, L)
         coll.allreduce_(s)
         sh = s.cpu().numpy()
-        num, den = sh[:L], sh[L:]
+        num, den = sh[:, 0], sh[:, 1]
         if self.dist.link == "log" or self.dist.family in ("poisson", "gamma", "tweedie"):
             return np.array([self.dist.gamma(float(a), float(b)) for a, b in zip(num, den)])
         out = np.where(den != 0, num / np.where(den == 0, 1, den), 0.0)
         return out
 
     def _gamma_multi(self, nid, L, w, z):
-        idx = nid.long()
         K = self.K
-        w64, z64 = w.to(torch.float64), z.to(torch.float64)
-        s = torch.zeros(2 * L, dtype=torch.float64, device=self.dev)
-        s[:L].index_add_(0, idx, w64 * z64)
-        s[L:].index_add_(0, idx, w64 * z64.abs() * (1 - z64.abs()))
+        lids, st, ct = self.grower.last_segs
+        s = tree_ops.seg_sum2(self.grower.ridx, w * z, w * z.abs() * (1 - z.abs()), lids, st, ct, L)
         coll.allreduce_(s)
         sh = s.cpu().numpy()
-        num, den = sh[:L], sh[L:]
+        num, den = sh[:, 0], sh[:, 1]
         return (K - 1.0) / K * np.where(den > 1e-300, num / np.where(den > 1e-300, den, 1), 0.0)
 
     def predictions(self):

@@ -98,7 +98,7 @@ class Forest:
         if X.device.type == "cuda":
             lib = _native.get_lib("tree_predict")
             if not getattr(lib, "_typed", False):
-                lib.h2o_forest_predict.argtypes = [_c_void, ctypes.c_longlong] + [_c_void] * 12 + \
+                lib.h2o_forest_predict.argtypes = [_c_void, ctypes.c_longlong] + [_c_void] * 11 + \
                     [ctypes.c_int, ctypes.c_int, _c_void, _c_void, _c_void]
                 lib._typed = True
             X = X.contiguous().to(torch.float32)

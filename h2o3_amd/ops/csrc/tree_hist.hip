@@ -1,5 +1,5 @@
 // GPU tree engine kernels: per-node feature histograms (LDS-staged), stable
-// row partition, and per-row leaf assignment.
+// row partition, per-row leaf assignment and per-leaf segment sums.
 //
 // Re-design of the reference's ScoreBuildHistogram2 MRTask
 // (h2o-algos/src/main/java/hex/tree/ScoreBuildHistogram2.java) and the
@@ -8,80 +8,90 @@
 // kept grouped by tree node (ridx permutation + per-node segments), the
 // binned feature matrix is row-major uint8/uint16, and one workgroup
 // accumulates a [feature-group x bins x channels] histogram of one node's row
-// range in LDS before flushing the non-zero bins to HBM with float atomics.
+// range in LDS before flushing the non-zero bins to HBM with f64 atomics.
+//
+// Lane mapping (the CDNA4 part): a wave64 instruction covers FGL features x
+// (64/FGL) rows — lane = (row_sub, feature).  All lanes of one row read
+// consecutive code bytes of that row (coalesced), the row's gradient pair is
+// a broadcast load, and lanes update *different* features' histograms, so
+// same-address LDS atomic collisions inside a wave only happen between the
+// (64/FGL) rows of one instruction.  (The naive lane=row mapping made all 64
+// lanes hit one feature's 256 bins at once and was ~25x slower.)
 //
 // Channels (MODE):
-//   0 : H2O squared-error criterion  (w, w*y, w*y*y)   C = 3
-//   1 : second-order (XGBoost)       (g, h)            C = 2
-//   2 : weighted count               (w)               C = 1
+//   0 : H2O squared-error criterion  (w, w*y)     C = 2   (node sum w*y*y is a
+//       separate segment reduction: only the node total enters the split test)
+//   1 : second-order (XGBoost)       (g, h)       C = 2
+//   2 : weighted count               (w)          C = 1
 //
-// Histogram layout in HBM: hist[F][n_slots][Bs][C] (feature-major so a
+// Histogram layout in HBM: hist[F][n_slots][Bs][C] f64 (feature-major so a
 // multi-GPU reduce-scatter can shard by feature).
 #include "common.h"
 
-template <int MODE> struct Chan { static constexpr int C = MODE == 0 ? 3 : (MODE == 1 ? 2 : 1); };
+template <int MODE> struct Chan { static constexpr int C = MODE == 2 ? 1 : 2; };
 
-template <typename CodeT> struct Code4;
-template <> struct Code4<uint8_t> {
-  typedef uint32_t vec;
-  __device__ static inline void unpack(vec v, int* c) {
-    c[0] = v & 0xff; c[1] = (v >> 8) & 0xff; c[2] = (v >> 16) & 0xff; c[3] = v >> 24;
-  }
-};
-template <> struct Code4<uint16_t> {
-  typedef uint2 vec;
-  __device__ static inline void unpack(vec v, int* c) {
-    c[0] = v.x & 0xffff; c[1] = v.x >> 16; c[2] = v.y & 0xffff; c[3] = v.y >> 16;
-  }
-};
-
-// work[i] = (slot, pos_start, pos_count, unused)
+// work[i] = (slot, pos_start, pos_count, unused);  grid = (n_work, n_feature_groups)
 template <typename CodeT, int MODE>
-__global__ __launch_bounds__(1024) void hist_build_kernel(
+__global__ __launch_bounds__(512) void hist_build_kernel(
     const CodeT* __restrict__ codes, int Fp, const int* __restrict__ ridx,
     const float* __restrict__ va, const float* __restrict__ vb,
-    const int4* __restrict__ work, int F, int FG, int Bs,
+    const int4* __restrict__ work, int F, int Bs, int FGL,
     double* __restrict__ hist, int n_slots) {
   constexpr int C = Chan<MODE>::C;
+  const int RPW = 64 / FGL;                     // rows per wave instruction
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int4 wk = work[blockIdx.x];
-  const int fg0 = blockIdx.y * FG;
-  const int nf = min(FG, F - fg0);          // real features in this group
-  const int nf4 = min(FG, Fp - fg0);        // loadable (padded) features
+  const int fg0 = blockIdx.y * FGL;
+  const int nf = min(FGL, F - fg0);
   const int stride_f = Bs * C;
-  const int total = FG * stride_f;
+  const int total = FGL * stride_f;
   for (int i = threadIdx.x; i < total; i += blockDim.x) lds[i] = 0.f;
   __syncthreads();
 
+  const int lane = threadIdx.x & 63;
+  const int fl = lane % FGL;                    // feature within group
+  const int rs = lane / FGL;                    // row sub-index
+  const bool lane_ok = rs < RPW;                // 64 % FGL lanes idle
+  const bool fok = fl < nf && lane_ok;
+  const int nwaves = blockDim.x >> 6;
+  const int wv = threadIdx.x >> 6;
+  float* hbase = lds + fl * stride_f;
   const int pend = wk.y + wk.z;
-  for (int p = wk.y + threadIdx.x; p < pend; p += blockDim.x) {
-    const int r = ridx[p];
-    float c0, c1 = 0.f, c2 = 0.f;
-    if (MODE == 0) {
-      const float y = va[r];
-      const float w = vb ? vb[r] : 1.f;
-      if (w == 0.f) continue;
-      c0 = w; c1 = w * y; c2 = c1 * y;
-    } else if (MODE == 1) {
-      c0 = va[r]; c1 = vb[r];
-      if (c0 == 0.f && c1 == 0.f) continue;
-    } else {
-      c0 = vb ? vb[r] : 1.f;
-      if (c0 == 0.f) continue;
-    }
-    const CodeT* row = codes + (size_t)r * Fp + fg0;
-    for (int j = 0; j < nf4; j += 4) {
-      typename Code4<CodeT>::vec v = *reinterpret_cast<const typename Code4<CodeT>::vec*>(row + j);
-      int c[4];
-      Code4<CodeT>::unpack(v, c);
+  const int step = nwaves * RPW;
+  // 4 rows per lane per iteration to keep several gathers in flight
+  for (int p0 = wk.y + wv * RPW + (lane_ok ? rs : 0); p0 < pend; p0 += 4 * step) {
+    int rr[4];
+    float c0[4], c1[4];
+    int code[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        if (j + k < nf) {
-          float* h = lds + (j + k) * stride_f + c[k] * C;
-          lds_add(h, c0);
-          if (C > 1) lds_add(h + 1, c1);
-          if (C > 2) lds_add(h + 2, c2);
+    for (int u = 0; u < 4; ++u) {
+      const int p = p0 + u * step;
+      rr[u] = (p < pend && lane_ok) ? ridx[p] : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int r = rr[u];
+      if (r >= 0) {
+        if (MODE == 0) {
+          const float y = va[r];
+          const float w = vb ? vb[r] : 1.f;
+          c0[u] = w; c1[u] = w * y;
+        } else if (MODE == 1) {
+          c0[u] = va[r]; c1[u] = vb[r];
+        } else {
+          c0[u] = vb ? vb[r] : 1.f; c1[u] = 0.f;
         }
+        code[u] = fok ? (int)codes[(size_t)r * Fp + fg0 + fl] : 0;
+      } else {
+        c0[u] = 0.f; c1[u] = 0.f; code[u] = 0;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (rr[u] >= 0 && fok && (c0[u] != 0.f || c1[u] != 0.f)) {
+        float* h = hbase + code[u] * C;
+        lds_add(h, c0[u]);
+        if (C > 1) lds_add(h + 1, c1[u]);
       }
     }
   }
@@ -103,13 +113,13 @@ static int launch_hist(const void* codes, int Fp, const int* ridx, const float* 
                        int mode, int threads, hipStream_t s) {
   const int n_fg = (F + FG - 1) / FG;
   dim3 grid(n_work, n_fg);
-  const int C = mode == 0 ? 3 : (mode == 1 ? 2 : 1);
+  const int C = mode == 2 ? 1 : 2;
   size_t lds = (size_t)FG * Bs * C * sizeof(float);
   const CodeT* cc = (const CodeT*)codes;
   switch (mode) {
-    case 0: hipLaunchKernelGGL((hist_build_kernel<CodeT, 0>), grid, dim3(threads), lds, s, cc, Fp, ridx, va, vb, work, F, FG, Bs, hist, n_slots); break;
-    case 1: hipLaunchKernelGGL((hist_build_kernel<CodeT, 1>), grid, dim3(threads), lds, s, cc, Fp, ridx, va, vb, work, F, FG, Bs, hist, n_slots); break;
-    default: hipLaunchKernelGGL((hist_build_kernel<CodeT, 2>), grid, dim3(threads), lds, s, cc, Fp, ridx, va, vb, work, F, FG, Bs, hist, n_slots); break;
+    case 0: hipLaunchKernelGGL((hist_build_kernel<CodeT, 0>), grid, dim3(threads), lds, s, cc, Fp, ridx, va, vb, work, F, Bs, FG, hist, n_slots); break;
+    case 1: hipLaunchKernelGGL((hist_build_kernel<CodeT, 1>), grid, dim3(threads), lds, s, cc, Fp, ridx, va, vb, work, F, Bs, FG, hist, n_slots); break;
+    default: hipLaunchKernelGGL((hist_build_kernel<CodeT, 2>), grid, dim3(threads), lds, s, cc, Fp, ridx, va, vb, work, F, Bs, FG, hist, n_slots); break;
   }
   return (int)hipGetLastError();
 }
@@ -242,3 +252,39 @@ int h2o_fill_nid(const int* ridx, const int* work, int n_work, int* nid, hipStre
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Per-leaf sums of two row vectors over the leaf segments of the row
+// permutation (the GBM GammaPass numerator/denominator, DRF leaf means):
+// no per-row atomics onto a handful of leaf addresses — each block reduces a
+// chunk of one segment in registers/LDS and issues one f64 atomic per channel.
+// work[i] = (leaf, start, count, -)
+__global__ __launch_bounds__(256) void seg_sum2_kernel(const int* __restrict__ ridx, const float* __restrict__ a,
+                                                       const float* __restrict__ b, const int4* __restrict__ work,
+                                                       double* __restrict__ out) {
+  const int4 wk = work[blockIdx.x];
+  double sa = 0.0, sb = 0.0;
+  for (int p = wk.y + threadIdx.x; p < wk.y + wk.z; p += blockDim.x) {
+    const int r = ridx[p];
+    sa += (double)a[r];
+    if (b) sb += (double)b[r];
+  }
+  sa = wave_sum(sa);
+  sb = wave_sum(sb);
+  __shared__ double red[2][4];
+  if (lane_id() == 0) { red[0][wave_id()] = sa; red[1][wave_id()] = sb; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double ta = 0.0, tb = 0.0;
+    for (int w = 0; w < (int)(blockDim.x / 64); ++w) { ta += red[0][w]; tb += red[1][w]; }
+    gbl_add(out + 2 * wk.x, ta);
+    if (b) gbl_add(out + 2 * wk.x + 1, tb);
+  }
+}
+
+extern "C" int h2o_seg_sum2(const int* ridx, const float* a, const float* b, const int* work, int n_work, double* out,
+                            hipStream_t s) {
+  if (n_work <= 0) return 0;
+  hipLaunchKernelGGL(seg_sum2_kernel, dim3(n_work), dim3(256), 0, s, ridx, a, b, (const int4*)work, out);
+  return (int)hipGetLastError();
+}

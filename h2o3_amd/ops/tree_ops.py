@@ -12,7 +12,7 @@ import torch
 
 from . import _native
 
-_LDS_BUDGET = 64 * 1024   # bytes of LDS histogram per workgroup (2 WG / CU)
+_LDS_BUDGET = 80 * 1024   # bytes of LDS histogram per workgroup (2+ WG / CU)
 _c_void = ctypes.c_void_p
 _c_int = ctypes.c_int
 _c_ll = ctypes.c_longlong
@@ -41,14 +41,32 @@ def _lib():
 
 
 def channels(mode: int) -> int:
-    return 3 if mode == 0 else (2 if mode == 1 else 1)
+    return 1 if mode == 2 else 2
 
 
 def feature_group(F: int, Bs: int, mode: int, budget: int = _LDS_BUDGET) -> int:
+    """Features per workgroup (= lanes per row in the wave mapping).
+
+    Minimises wave-instructions per row, ~ n_groups / floor(64 / FGL), under
+    the LDS budget; ties go to fewer groups (less re-reading of row data)."""
+    import os
+    if os.environ.get("H2O3_HIST_FGL"):
+        return max(1, min(64, int(os.environ["H2O3_HIST_FGL"]), F))
     C = channels(mode)
-    fg = budget // (Bs * C * 4)
-    fg = max(4, (fg // 4) * 4)
-    return min(fg, ((F + 3) // 4) * 4)
+    fmax = max(1, min(64, budget // (Bs * C * 4)))
+    best = None
+    for ng in range(1, F + 1):
+        fgl = -(-F // ng)
+        if fgl > fmax:
+            continue
+        # wave-instructions per row + re-read of the row payload per group
+        cost = ng / (64 // fgl) + 0.05 * ng
+        key = (round(cost, 6), ng)
+        if best is None or key < best[0]:
+            best = (key, fgl)
+        if fgl == 1:
+            break
+    return best[1] if best else 1
 
 
 def make_work(starts, counts, slots, chunk):
@@ -88,7 +106,7 @@ def hist_build(bd, ridx, va, vb, mode, starts, counts, n_slots, use_native=None,
         if not items:
             return hist
         work = torch.tensor(items, dtype=torch.int32).to(dev, non_blocking=True)
-        threads = 1024 if chunk >= 8192 else 256
+        threads = 512 if chunk >= 8192 else 256
         rc = lib.h2o_hist_build(_ptr(bd.codes), bd.code_bytes, bd.Fp, _ptr(ridx), _ptr(va), _ptr(vb), _ptr(work),
                                 len(items), bd.F, FG, bd.Bs, _ptr(hist), n_slots, mode, threads, _stream())
         if rc != 0:
@@ -108,7 +126,7 @@ def _hist_build_torch(bd, ridx, va, vb, mode, starts, counts, hist):
         a = va[r].to(torch.float32)
         if mode == 0:
             w = vb[r].to(torch.float32) if vb is not None else torch.ones_like(a)
-            vals = torch.stack([w, w * a, w * a * a], 1)
+            vals = torch.stack([w, w * a], 1)
         elif mode == 1:
             vals = torch.stack([a, vb[r].to(torch.float32)], 1)
         else:
@@ -215,3 +233,31 @@ def fill_nid(ridx, leaf_ids, starts, counts, nrows, use_native=None):
     for lid, st, ct in zip(leaf_ids, starts, counts):
         nid[ridx[st: st + ct].long()] = lid
     return nid
+
+
+def seg_sum2(ridx, a, b, leaf_ids, starts, counts, n_leaves, use_native=None, chunk=65536):
+    """Per-leaf sums of a[r] (and b[r]) over leaf segments of ridx -> [L, 2] f64."""
+    dev = ridx.device
+    out = torch.zeros((n_leaves, 2), dtype=torch.float64, device=dev)
+    native = dev.type == "cuda" if use_native is None else use_native
+    if native:
+        lib = _lib()
+        if not getattr(lib, "_typed_seg", False):
+            lib.h2o_seg_sum2.argtypes = [_c_void, _c_void, _c_void, _c_void, _c_int, _c_void, _c_void]
+            lib._typed_seg = True
+        items = make_work(starts, counts, leaf_ids, chunk)
+        if not items:
+            return out
+        work = torch.tensor(items, dtype=torch.int32).to(dev, non_blocking=True)
+        a = a.to(torch.float32).contiguous()
+        b = None if b is None else b.to(torch.float32).contiguous()
+        rc = lib.h2o_seg_sum2(_ptr(ridx), _ptr(a), _ptr(b), _ptr(work), len(items), _ptr(out), _stream())
+        if rc != 0:
+            raise RuntimeError(f"h2o_seg_sum2 failed: {rc}")
+        return out
+    for lid, st, ct in zip(leaf_ids, starts, counts):
+        r = ridx[st: st + ct].long()
+        out[lid, 0] = a[r].to(torch.float64).sum()
+        if b is not None:
+            out[lid, 1] = b[r].to(torch.float64).sum()
+    return out
