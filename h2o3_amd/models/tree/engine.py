@@ -141,7 +141,7 @@ class TreeGrower:
     # ------------------------------------------------------------------ hist
     def _build_hist(self, ridx, va, vb, mode, starts, counts):
         with phase("tree.hist"):
-            H = tree_ops.hist_build(self.bd, ridx, va, vb, mode, starts, counts, len(starts))
+            H = tree_ops.hist_build(self.bd, ridx, va, vb, mode, starts, counts, len(starts), vmax=self._vmax)
         if self.W > 1:
             if self.Fpad > self.bd.F:
                 H = torch.cat([H, torch.zeros((self.Fpad - self.bd.F,) + tuple(H.shape[1:]), dtype=H.dtype,
@@ -326,6 +326,7 @@ class TreeGrower:
         N = bd.nrows_local
         C = tree_ops.channels(mode)
         torch.arange(N, dtype=torch.int32, device=self.dev, out=self.ridx)
+        self._vmax = tree_ops.channel_max(va, vb, mode) if self.dev.type == "cuda" else None
         ridx, ridx2 = self.ridx, self.ridx2
         tree = Tree()
         root = tree.add_node(0, 0.0)

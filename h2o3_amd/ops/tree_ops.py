@@ -30,7 +30,8 @@ def _lib():
     lib = _native.get_lib("tree_hist")
     if lib is not None and not getattr(lib, "_typed", False):
         lib.h2o_hist_build.argtypes = [_c_void, _c_int, _c_int, _c_void, _c_void, _c_void, _c_void, _c_int,
-                                       _c_int, _c_int, _c_int, _c_void, _c_int, _c_int, _c_int, _c_void]
+                                       _c_int, _c_int, _c_int, ctypes.c_float, ctypes.c_float, _c_void, _c_int, _c_int,
+                                       _c_int, _c_void]
         lib.h2o_part_count.argtypes = [_c_void, _c_int, _c_ll, _c_ll, _c_void, _c_void, _c_int, _c_void,
                                        _c_void, _c_int, _c_void, _c_void]
         lib.h2o_part_scatter.argtypes = [_c_void, _c_int, _c_ll, _c_ll, _c_void, _c_void, _c_int, _c_void,
@@ -53,7 +54,7 @@ def feature_group(F: int, Bs: int, mode: int, budget: int = _LDS_BUDGET) -> int:
     if os.environ.get("H2O3_HIST_FGL"):
         return max(1, min(64, int(os.environ["H2O3_HIST_FGL"]), F))
     C = channels(mode)
-    fmax = max(1, min(64, budget // (Bs * C * 4)))
+    fmax = max(1, min(64, budget // (Bs * C * 8)))
     best = None
     for ng in range(1, F + 1):
         fgl = -(-F // ng)
@@ -86,7 +87,32 @@ def make_work(starts, counts, slots, chunk):
     return items
 
 
-def hist_build(bd, ridx, va, vb, mode, starts, counts, n_slots, use_native=None, target_blocks=2048):
+def channel_max(va, vb, mode):
+    """Max |value| per histogram channel (host floats, one device sync)."""
+    if mode == 0:
+        w = vb if vb is not None else None
+        m1 = (va.abs() * (w.abs() if w is not None else 1)).max() if va.numel() else va.new_zeros(())
+        m0 = w.abs().max() if (w is not None and w.numel()) else va.new_ones(())
+    elif mode == 1:
+        m0, m1 = va.abs().max(), vb.abs().max()
+    else:
+        m0 = vb.abs().max() if vb is not None else va.new_ones(())
+        m1 = m0
+    t = torch.stack([m0.float(), m1.float()]).cpu().tolist()
+    return [x if x == x else 0.0 for x in t]
+
+
+def fixed_point_scale(maxv, nmax):
+    """Power-of-two scale S so that nmax values of magnitude <= maxv sum
+    below 2^62 in int64 (exact fixed-point histogram accumulation)."""
+    import math
+    if not maxv or maxv <= 0 or not math.isfinite(maxv):
+        return 1.0
+    k = math.floor(math.log2(2.0 ** 62 / (maxv * max(nmax, 1))))
+    return float(2.0 ** max(min(k, 100), -100))
+
+
+def hist_build(bd, ridx, va, vb, mode, starts, counts, n_slots, use_native=None, target_blocks=2048, vmax=None):
     """Histograms of the row segments [starts[i], starts[i]+counts[i]) of
     ridx into slot i.  Returns hist [F, n_slots, Bs, C] float32."""
     C = channels(mode)
@@ -107,8 +133,11 @@ def hist_build(bd, ridx, va, vb, mode, starts, counts, n_slots, use_native=None,
             return hist
         work = torch.tensor(items, dtype=torch.int32).to(dev, non_blocking=True)
         threads = 512 if chunk >= 8192 else 256
+        if vmax is None:
+            vmax = channel_max(va, vb, mode)
+        s0, s1 = (fixed_point_scale(m, chunk) for m in vmax)
         rc = lib.h2o_hist_build(_ptr(bd.codes), bd.code_bytes, bd.Fp, _ptr(ridx), _ptr(va), _ptr(vb), _ptr(work),
-                                len(items), bd.F, FG, bd.Bs, _ptr(hist), n_slots, mode, threads, _stream())
+                                len(items), bd.F, FG, bd.Bs, s0, s1, _ptr(hist), n_slots, mode, threads, _stream())
         if rc != 0:
             raise RuntimeError(f"h2o_hist_build failed: hip error {rc}")
         return hist
