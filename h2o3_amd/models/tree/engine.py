@@ -174,6 +174,77 @@ class TreeGrower:
         return torch.from_numpy(m)
 
     def _find_splits(self, H, col_mask, node_wyy=None):
+        """Dispatch: fused HIP kernel for numeric features on GPU (categorical
+        features, which need a per-node sort of bins, go through the torch path)."""
+        if self.dev.type != "cuda":
+            return self._find_splits_torch(H, col_mask, node_wyy)
+        Fl = H.shape[0]
+        fsl = slice(self.f0, self.f0 + Fl)
+        is_cat = self.is_cat_t[fsl].cpu()
+        if bool(is_cat.all()):
+            return self._find_splits_torch(H, col_mask, node_wyy)
+        cm_num = col_mask.clone()
+        cm_num[:, fsl] &= ~is_cat.view(1, -1)
+        res = self._find_splits_native(H, cm_num, node_wyy)
+        if bool(is_cat.any()):
+            cm_cat = col_mask.clone()
+            cm_cat[:, fsl] &= is_cat.view(1, -1)
+            rc = self._find_splits_torch(H, cm_cat, node_wyy, merge=False)
+            better = rc["gain"] > res["gain"]
+            for k in res:
+                if res[k] is None or k == "tot":
+                    continue
+                b = better.view(-1, *([1] * (res[k].dim() - 1))) if res[k].dim() > 1 else better
+                res[k] = torch.where(b, rc[k].to(res[k].dtype), res[k])
+        if self.W > 1:
+            res = self._merge_candidates(res, H.shape[1], H.shape[2], H.shape[3])
+        return res
+
+    def _find_splits_native(self, H, col_mask, node_wyy):
+        import ctypes
+        from ...ops import _native
+        p = self.p
+        Fl, n, Bs, C = H.shape
+        lib = _native.get_lib("tree_split")
+        if not getattr(lib, "_typed", False):
+            cv = ctypes.c_void_p
+            lib.h2o_split_find.argtypes = [cv, ctypes.c_int, ctypes.c_int, ctypes.c_int, cv, cv, cv] + \
+                [ctypes.c_double] * 5 + [ctypes.c_int, cv, cv]
+            lib._typed = True
+        fsl = slice(self.f0, self.f0 + Fl)
+        ok = col_mask[:, fsl].to(torch.uint8).contiguous().to(self.dev, non_blocking=True)
+        if self.f0 + Fl > self.bd.F:
+            ok[:, max(0, self.bd.F - self.f0):] = 0
+        mono = self.mono_t[fsl].to(torch.float32).contiguous()
+        H = H.contiguous()
+        wyy = node_wyy.to(torch.float64).contiguous() if node_wyy is not None else \
+            torch.zeros(n, dtype=torch.float64, device=self.dev)
+        out = torch.empty((n * Fl, 4), dtype=torch.float64, device=self.dev)
+        crit = 1 if p.criterion == "xgb" else 0
+        rc = lib.h2o_split_find(ctypes.c_void_p(H.data_ptr()), Fl, n, Bs, ctypes.c_void_p(wyy.data_ptr()),
+                                ctypes.c_void_p(ok.data_ptr()), ctypes.c_void_p(mono.data_ptr()),
+                                float(p.min_rows), float(p.min_split_improvement), float(p.reg_lambda),
+                                float(p.reg_alpha), float(p.gamma), crit, ctypes.c_void_p(out.data_ptr()),
+                                ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+        if rc != 0:
+            raise RuntimeError(f"h2o_split_find failed: {rc}")
+        gain = out[:, 0].view(n, Fl)
+        ints = out.view(torch.int32).view(n * Fl, 8)[:, 6:8]
+        best, fl = gain.max(1)
+        idx = torch.arange(n, device=self.dev) * Fl + fl
+        t = ints[idx, 0].long()
+        opt = ints[idx, 1].long()
+        Lw = out[idx, 1:3]
+        T = H[0].sum(1) if self.f0 < self.bd.F else torch.zeros((n, C), dtype=H.dtype, device=H.device)
+        B = Bs - 1
+        codes = torch.arange(Bs, device=self.dev).view(1, Bs)
+        mask = (codes <= t.view(n, 1)) & (codes < B)
+        mask = torch.where((opt == 2).view(n, 1), codes < B, mask)
+        mask[:, Bs - 1] = opt == 1
+        return {"gain": best, "feat": fl + self.f0, "t": t, "opt": opt, "na_left": opt == 1,
+                "mask": mask.to(torch.uint8), "L": Lw, "R": T - Lw, "tot": T}
+
+    def _find_splits_torch(self, H, col_mask, node_wyy=None, merge=True):
         """H: [Fl, n, Bs, C] (local feature slice).  Returns dict of per-node
         tensors on device: gain, feat, na_left, mask[n, Bs], stats L/R [n,C],
         tot [n,C]."""
@@ -295,7 +366,7 @@ class TreeGrower:
         mask[:, Bs - 1] = na_left
         res = {"gain": best, "feat": fl + self.f0, "t": t, "opt": opt, "na_left": na_left,
                "mask": mask.to(torch.uint8), "L": Lw, "R": Rw, "tot": T[:, 0] if Fl > 0 else None}
-        if self.W > 1:
+        if self.W > 1 and merge:
             res = self._merge_candidates(res, n, Bs, C)
         return res
 
@@ -334,12 +405,18 @@ class TreeGrower:
         frontier = [[root, 0, N, 0]]
         H_prev, prev_slot = None, {}
         pair_info = []     # for level>0: (left_id, right_id, parent_slot, build_left)
+        child_tot = {}     # node id -> channel totals from the parent's split record
         leaves, leaf_tot = [], []
         level = 0
         while frontier:
             n_front = len(frontier)
             slot_of = {nd[0]: i for i, nd in enumerate(frontier)}
-            if level == 0 or H_prev is None:
+            depth = frontier[0][3]
+            can_split = depth < p.max_depth
+            if not can_split and level > 0:
+                # last level: no histograms needed, leaf totals come from the parent split stats
+                H = None
+            elif level == 0 or H_prev is None:
                 build = list(range(n_front))
                 Hb = self._build_hist(ridx, va, vb, mode, [f[1] for f in frontier], [f[2] for f in frontier])
                 H = Hb
@@ -361,9 +438,7 @@ class TreeGrower:
                 if mode == 0:
                     # only w / wyy are non-negative; wy may be negative
                     H[:, ds, :, 1] = H_prev[:, ps, :, 1] - Hb[:, :, :, 1]
-            del Hb
-            depth = frontier[0][3]
-            can_split = depth < p.max_depth
+                del Hb
             if can_split:
                 cm = self._col_mask(n_front, depth)
                 node_wyy = None
@@ -384,7 +459,8 @@ class TreeGrower:
                 tots = sp["tot"].cpu()
             else:
                 # totals only
-                tots = self._totals(H)
+                tots = self._totals(H) if H is not None else \
+                    torch.stack([child_tot[nd[0]] for nd in frontier])
                 gains = None
             split_ids, split_slots = [], []
             for i, (nid_, st, ct, d) in enumerate(frontier):
@@ -441,6 +517,8 @@ class TreeGrower:
                 wl = float(Ls[i][0] if mode != 1 else Ls[i][1])
                 wr = float(Rs[i][0] if mode != 1 else Rs[i][1])
                 new_pairs.append((lid, rid, j, wl <= wr))
+                child_tot[lid] = Ls[i].to(torch.float64)
+                child_tot[rid] = Rs[i].to(torch.float64)
             # partition
             with phase("tree.partition"):
                 ridx2.copy_(ridx)

@@ -108,3 +108,29 @@ def test_gbm_gpu_end_to_end_quality():
     m.train(y="y", training_frame=fr)
     assert m.auc() > 0.85
     assert any("tree_hist" in p for p in _native.loaded_libs())
+
+
+@pytest.mark.parametrize("crit", ["se", "xgb"])
+def test_split_kernel_matches_torch(crit):
+    _need_gpu()
+    from h2o3_amd.models.tree.engine import GrowParams, TreeGrower
+    bd, _ = _binned(n=30000, cats=False)
+    p = GrowParams(criterion=crit, min_rows=5.0, max_depth=6)
+    gr = TreeGrower(bd, p)
+    n = 5
+    g = torch.Generator(device="cuda").manual_seed(3)
+    H = torch.rand((bd.F, n, bd.Bs, 2), generator=g, device="cuda", dtype=torch.float64) * 50
+    if crit == "se":
+        H[..., 1] = (torch.rand(H[..., 1].shape, generator=g, device="cuda", dtype=torch.float64) - 0.3) * H[..., 0]
+    H[:, :, 200:bd.Bs - 1] = 0  # empty upper bins
+    wyy = H[0].sum(1)[:, 0] * 10.0
+    cm = torch.ones((n, bd.F), dtype=torch.bool)
+    cm[1, 3] = False
+    a = gr._find_splits_native(H, cm, wyy)
+    b = gr._find_splits_torch(H, cm, wyy)
+    torch.testing.assert_close(a["gain"], b["gain"], rtol=1e-9, atol=1e-9)
+    assert torch.equal(a["feat"].cpu(), b["feat"].cpu())
+    assert torch.equal(a["t"].cpu(), b["t"].cpu())
+    assert torch.equal(a["opt"].cpu(), b["opt"].cpu())
+    assert torch.equal(a["mask"].cpu(), b["mask"].cpu())
+    torch.testing.assert_close(a["L"], b["L"].to(a["L"].dtype), rtol=1e-9, atol=1e-9)
