@@ -141,7 +141,11 @@ class TreeGrower:
     # ------------------------------------------------------------------ hist
     def _build_hist(self, ridx, va, vb, mode, starts, counts):
         with phase("tree.hist"):
-            H = tree_ops.hist_build(self.bd, ridx, va, vb, mode, starts, counts, len(starts), vmax=self._vmax)
+            H, wyy = tree_ops.hist_build(self.bd, ridx, va, vb, mode, starts, counts, len(starts), vmax=self._vmax,
+                                         want_wyy=True)
+        if wyy is not None:
+            coll.allreduce_(wyy)
+        self._last_wyy = wyy
         if self.W > 1:
             if self.Fpad > self.bd.F:
                 H = torch.cat([H, torch.zeros((self.Fpad - self.bd.F,) + tuple(H.shape[1:]), dtype=H.dtype,
@@ -404,6 +408,7 @@ class TreeGrower:
         # frontier entries: [node_id, start, count_local, depth]
         frontier = [[root, 0, N, 0]]
         H_prev, prev_slot = None, {}
+        wyy_prev, wyy_level = None, None
         pair_info = []     # for level>0: (left_id, right_id, parent_slot, build_left)
         child_tot = {}     # node id -> channel totals from the parent's split record
         leaves, leaf_tot = [], []
@@ -420,6 +425,7 @@ class TreeGrower:
                 build = list(range(n_front))
                 Hb = self._build_hist(ridx, va, vb, mode, [f[1] for f in frontier], [f[2] for f in frontier])
                 H = Hb
+                wyy_level = self._last_wyy
             else:
                 build_slots, der_slots, par_slots, sib_idx = [], [], [], []
                 for (lid, rid, pslot, build_left) in pair_info:
@@ -435,21 +441,19 @@ class TreeGrower:
                 ps = torch.tensor(par_slots, device=Hb.device)
                 H[:, bs] = Hb
                 H[:, ds] = (H_prev[:, ps] - Hb).clamp_min_(0) if mode != 1 else (H_prev[:, ps] - Hb)
+                if mode == 0 and self._last_wyy is not None:
+                    wyy_level = torch.empty(n_front, dtype=torch.float64, device=Hb.device)
+                    wyy_level[bs] = self._last_wyy
+                    wyy_level[ds] = wyy_prev[ps] - self._last_wyy
                 if mode == 0:
                     # only w / wyy are non-negative; wy may be negative
                     H[:, ds, :, 1] = H_prev[:, ps, :, 1] - Hb[:, :, :, 1]
                 del Hb
             if can_split:
                 cm = self._col_mask(n_front, depth)
-                node_wyy = None
-                if mode == 0:
-                    # node totals of w*y*y (only the total enters the SE split test)
-                    with phase("tree.wyy"):
-                        wv = vb if vb is not None else torch.ones_like(va)
-                        s = tree_ops.seg_sum2(ridx, wv * va * va, None, list(range(n_front)),
-                                              [f[1] for f in frontier], [f[2] for f in frontier], n_front)
-                        coll.allreduce_(s)
-                        node_wyy = s[:, 0]
+                # node totals of w*y*y (only the total enters the SE split test),
+                # fused into the histogram kernel; derived siblings by subtraction
+                node_wyy = wyy_level if mode == 0 else None
                 with phase("tree.split"):
                     sp = self._find_splits(H, cm, node_wyy)
                 gains = sp["gain"].cpu()
@@ -536,7 +540,9 @@ class TreeGrower:
                 if len(f) > 4:
                     self._pending_leaf_segs.append((f[0], f[1], f[2]))
             # parent hists for the next level (only split nodes)
-            H_prev = H[:, torch.tensor(split_ids, device=H.device)]
+            sid = torch.tensor(split_ids, device=H.device)
+            H_prev = H[:, sid]
+            wyy_prev = wyy_level[sid] if (mode == 0 and wyy_level is not None) else None
             pair_info = new_pairs
             frontier = new_front
             level += 1

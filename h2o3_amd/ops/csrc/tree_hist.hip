@@ -36,7 +36,7 @@ __global__ __launch_bounds__(512) void hist_build_kernel(
     const CodeT* __restrict__ codes, int Fp, const int* __restrict__ ridx,
     const float* __restrict__ va, const float* __restrict__ vb,
     const int4* __restrict__ work, int F, int Bs, int FGL, float s0, float s1,
-    double* __restrict__ hist, int n_slots) {
+    double* __restrict__ hist, int n_slots, double* __restrict__ wyy_out) {
   constexpr int C = Chan<MODE>::C;
   const int RPW = 64 / FGL;                     // rows per wave instruction
   extern __shared__ __attribute__((aligned(16))) unsigned long long ldsq[];
@@ -56,6 +56,10 @@ __global__ __launch_bounds__(512) void hist_build_kernel(
   const int nwaves = blockDim.x >> 6;
   const int wv = threadIdx.x >> 6;
   unsigned long long* hbase = ldsq + fl * stride_f;
+  // node sum of w*y*y (MODE 0): accumulated once per row by the fl==0 lanes of
+  // feature group 0, so the SE split test needs no extra pass over the rows
+  const bool do_wyy = (MODE == 0) && wyy_out != nullptr && blockIdx.y == 0 && fl == 0 && lane_ok;
+  double wyy = 0.0;
   const int pend = wk.y + wk.z;
   const int step = nwaves * RPW;
   // U rows per lane per iteration, every load unconditional (clamped index)
@@ -77,6 +81,7 @@ __global__ __launch_bounds__(512) void hist_build_kernel(
         const float y = va[r];
         const float w = HAS_VB ? vb[r] : 1.f;
         c0[u] = w; c1[u] = w * y;
+        if (do_wyy && p0 + u * step < pend) wyy += (double)(w * y) * (double)y;
       } else if (MODE == 1) {
         c0[u] = va[r]; c1[u] = vb[r];
       } else {
@@ -102,6 +107,10 @@ __global__ __launch_bounds__(512) void hist_build_kernel(
     }
   }
   __syncthreads();
+  if (MODE == 0 && wyy_out != nullptr && blockIdx.y == 0) {
+    wyy = wave_sum(wyy);
+    if (lane == 0) gbl_add(wyy_out + wk.x, wyy);
+  }
   const double inv0 = 1.0 / (double)s0, inv1 = 1.0 / (double)s1;
   const int tot_real = nf * stride_f;
   for (int i = threadIdx.x; i < tot_real; i += blockDim.x) {
@@ -118,14 +127,14 @@ __global__ __launch_bounds__(512) void hist_build_kernel(
 template <typename CodeT>
 static int launch_hist(const void* codes, int Fp, const int* ridx, const float* va, const float* vb,
                        const int4* work, int n_work, int F, int FG, int Bs, float s0, float s1, double* hist,
-                       int n_slots, int mode, int threads, hipStream_t s) {
+                       int n_slots, int mode, int threads, double* wyy, hipStream_t s) {
   const int n_fg = (F + FG - 1) / FG;
   dim3 grid(n_work, n_fg);
   const int C = mode == 2 ? 1 : 2;
   size_t lds = (size_t)FG * Bs * C * sizeof(unsigned long long);
   const CodeT* cc = (const CodeT*)codes;
   switch (mode) {
-#define H2O_LH(M, V) hipLaunchKernelGGL((hist_build_kernel<CodeT, M, V>), grid, dim3(threads), lds, s, cc, Fp, ridx, va, vb, work, F, Bs, FG, s0, s1, hist, n_slots)
+#define H2O_LH(M, V) hipLaunchKernelGGL((hist_build_kernel<CodeT, M, V>), grid, dim3(threads), lds, s, cc, Fp, ridx, va, vb, work, F, Bs, FG, s0, s1, hist, n_slots, wyy)
     case 0: if (vb) H2O_LH(0, true); else H2O_LH(0, false); break;
     case 1: H2O_LH(1, true); break;
     default: if (vb) H2O_LH(2, true); else H2O_LH(2, false); break;
@@ -145,29 +154,50 @@ static int launch_hist(const void* codes, int Fp, const int* ridx, const float* 
 // per node; pass 2 scatters each chunk stably.
 // code of (row r, feature f) = codes[r*rs + f*fs]  (row- or column-major)
 template <typename CodeT>
+__device__ __forceinline__ void load_items(const CodeT* __restrict__ codes, long long rs, long long fs, int f,
+                                           const int* __restrict__ ridx, int p0, int end, int (&r)[16],
+                                           int (&c)[16]) {
+  // 16 consecutive positions per thread; all loads unconditional (clamped)
+  if (p0 + 16 <= end && (p0 & 3) == 0) {
+    const int4* v = reinterpret_cast<const int4*>(ridx + p0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int4 x = v[q];
+      r[4 * q] = x.x; r[4 * q + 1] = x.y; r[4 * q + 2] = x.z; r[4 * q + 3] = x.w;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) r[k] = ridx[min(p0 + k, end - 1)];
+  }
+#pragma unroll
+  for (int k = 0; k < 16; ++k) c[k] = (int)codes[(size_t)r[k] * rs + (size_t)f * fs];
+}
+
+template <typename CodeT>
 __global__ __launch_bounds__(256) void part_count_kernel(
     const CodeT* __restrict__ codes, long long rs, long long fs, const int* __restrict__ ridx,
     const int4* __restrict__ work, const int* __restrict__ feat, const uint8_t* __restrict__ masks,
     int Bs, int* __restrict__ cnt) {
+  __shared__ uint8_t m[4096];
+  __shared__ int red[4];
   const int4 wk = work[blockIdx.x];
   const int f = feat[wk.x];
-  const uint8_t* m = masks + (size_t)wk.x * Bs;
+  for (int i = threadIdx.x; i < Bs; i += blockDim.x) m[i] = masks[(size_t)wk.x * Bs + i];
+  __syncthreads();
+  const int end = wk.y + wk.z;
   int local = 0;
-  for (int p = wk.y + threadIdx.x; p < wk.y + wk.z; p += blockDim.x) {
-    const int r = ridx[p];
-    const int c = codes[(size_t)r * rs + (size_t)f * fs];
-    local += m[c] ? 1 : 0;
+  for (int base = wk.y; base < end; base += 256 * 16) {
+    const int p0 = base + threadIdx.x * 16;
+    if (p0 >= end) continue;
+    int r[16], c[16];
+    load_items<CodeT>(codes, rs, fs, f, ridx, p0, end, r, c);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) local += (p0 + k < end && m[c[k]]) ? 1 : 0;
   }
-  // block reduce
-  __shared__ int red[4];
   for (int o = 32; o > 0; o >>= 1) local += __shfl_xor(local, o, 64);
   if (lane_id() == 0) red[wave_id()] = local;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    int t = 0;
-    for (int w = 0; w < (int)(blockDim.x / 64); ++w) t += red[w];
-    cnt[blockIdx.x] = t;
-  }
+  if (threadIdx.x == 0) cnt[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
 // loff[i], roff[i]: destination start of chunk i's left / right rows.
@@ -176,45 +206,67 @@ __global__ __launch_bounds__(256) void part_scatter_kernel(
     const CodeT* __restrict__ codes, long long rs, long long fs, const int* __restrict__ ridx,
     const int4* __restrict__ work, const int* __restrict__ feat, const uint8_t* __restrict__ masks,
     int Bs, const int* __restrict__ loff, const int* __restrict__ roff, int* __restrict__ out) {
+  __shared__ uint8_t m[4096];
+  __shared__ int wsum[4];
   const int4 wk = work[blockIdx.x];
   const int f = feat[wk.x];
-  const uint8_t* m = masks + (size_t)wk.x * Bs;
-  __shared__ int wl[4];
+  for (int i = threadIdx.x; i < Bs; i += blockDim.x) m[i] = masks[(size_t)wk.x * Bs + i];
+  __syncthreads();
   int lbase = loff[blockIdx.x], rbase = roff[blockIdx.x];
-  const int nw = blockDim.x / 64;
-  for (int t0 = wk.y; t0 < wk.y + wk.z; t0 += blockDim.x) {
-    const int p = t0 + threadIdx.x;
-    const bool valid = p < wk.y + wk.z;
-    int r = 0;
-    bool left = false;
-    if (valid) {
-      r = ridx[p];
-      left = m[codes[(size_t)r * rs + (size_t)f * fs]] != 0;
+  const int end = wk.y + wk.z;
+  const int lane = lane_id(), wv = wave_id();
+  for (int base = wk.y; base < end; base += 256 * 16) {
+    const int p0 = base + threadIdx.x * 16;
+    int r[16], c[16];
+    unsigned bits = 0;
+    int nl = 0, nv = 0;
+    if (p0 < end) {
+      load_items<CodeT>(codes, rs, fs, f, ridx, p0, end, r, c);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const bool v = p0 + k < end;
+        const bool L = v && m[c[k]];
+        bits |= (L ? 1u : 0u) << k;
+        nl += L ? 1 : 0;
+        nv += v ? 1 : 0;
+      }
     }
-    const unsigned long long bl = __ballot(valid && left);
-    const unsigned long long lt = (lane_id() == 0) ? 0ull : (~0ull >> (64 - lane_id()));
-    const int wpre = __popcll(bl & lt);
-    if (lane_id() == 0) wl[wave_id()] = __popcll(bl);
+    // block exclusive scan of nl (positions are in thread order)
+    int incl = nl;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int u = __shfl_up(incl, d, 64);
+      if (lane >= d) incl += u;
+    }
+    if (lane == 63) wsum[wv] = incl;
     __syncthreads();
-    int lpre = 0, ltot = 0;
-    for (int w = 0; w < nw; ++w) {
-      const int c = wl[w];
-      if (w < wave_id()) lpre += c;
-      ltot += c;
+    int wpre = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const int s = wsum[w];
+      wpre += (w < wv) ? s : 0;
+      tot += s;
     }
-    const int tile_n = min((int)blockDim.x, wk.y + wk.z - t0);
-    if (valid) {
-      const int li = lpre + wpre;              // lefts before me in tile
-      const int my_idx = threadIdx.x;          // position within tile
-      if (left) out[lbase + li] = r;
-      else out[rbase + (my_idx - li)] = r;
+    const int lpre = wpre + incl - nl;                 // lefts before this thread in the tile
+    const int tile_first = base;
+    const int pos_before = max(0, min(p0, end) - tile_first);  // valid positions before this thread
+    int li = lbase + lpre;
+    int ri = rbase + (pos_before - lpre);
+    if (p0 < end) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        if (p0 + k < end) {
+          if ((bits >> k) & 1u) out[li++] = r[k];
+          else out[ri++] = r[k];
+        }
+      }
     }
-    lbase += ltot;
-    rbase += tile_n - ltot;
+    const int tile_n = min(256 * 16, end - base);
+    lbase += tot;
+    rbase += tile_n - tot;
     __syncthreads();
   }
 }
-
 // nid[ridx[p]] = leaf for p in segment.  work[i] = (leaf_id, start, count, -)
 __global__ __launch_bounds__(256) void fill_nid_kernel(const int* __restrict__ ridx, const int4* __restrict__ work,
                                                        int* __restrict__ nid) {
@@ -226,11 +278,11 @@ extern "C" {
 
 int h2o_hist_build(const void* codes, int code_bytes, int Fp, const int* ridx, const float* va,
                    const float* vb, const int* work, int n_work, int F, int FG, int Bs, float s0, float s1,
-                   double* hist, int n_slots, int mode, int threads, hipStream_t s) {
+                   double* hist, int n_slots, int mode, int threads, double* wyy, hipStream_t s) {
   if (n_work <= 0) return 0;
   if (code_bytes == 1)
-    return launch_hist<uint8_t>(codes, Fp, ridx, va, vb, (const int4*)work, n_work, F, FG, Bs, s0, s1, hist, n_slots, mode, threads, s);
-  return launch_hist<uint16_t>(codes, Fp, ridx, va, vb, (const int4*)work, n_work, F, FG, Bs, s0, s1, hist, n_slots, mode, threads, s);
+    return launch_hist<uint8_t>(codes, Fp, ridx, va, vb, (const int4*)work, n_work, F, FG, Bs, s0, s1, hist, n_slots, mode, threads, wyy, s);
+  return launch_hist<uint16_t>(codes, Fp, ridx, va, vb, (const int4*)work, n_work, F, FG, Bs, s0, s1, hist, n_slots, mode, threads, wyy, s);
 }
 
 int h2o_part_count(const void* codes, int code_bytes, long long rs, long long fs, const int* ridx,

@@ -31,7 +31,7 @@ def _lib():
     if lib is not None and not getattr(lib, "_typed", False):
         lib.h2o_hist_build.argtypes = [_c_void, _c_int, _c_int, _c_void, _c_void, _c_void, _c_void, _c_int,
                                        _c_int, _c_int, _c_int, ctypes.c_float, ctypes.c_float, _c_void, _c_int, _c_int,
-                                       _c_int, _c_void]
+                                       _c_int, _c_void, _c_void]
         lib.h2o_part_count.argtypes = [_c_void, _c_int, _c_ll, _c_ll, _c_void, _c_void, _c_int, _c_void,
                                        _c_void, _c_int, _c_void, _c_void]
         lib.h2o_part_scatter.argtypes = [_c_void, _c_int, _c_ll, _c_ll, _c_void, _c_void, _c_int, _c_void,
@@ -112,12 +112,16 @@ def fixed_point_scale(maxv, nmax):
     return float(2.0 ** max(min(k, 100), -100))
 
 
-def hist_build(bd, ridx, va, vb, mode, starts, counts, n_slots, use_native=None, target_blocks=2048, vmax=None):
+def hist_build(bd, ridx, va, vb, mode, starts, counts, n_slots, use_native=None, target_blocks=2048, vmax=None,
+               want_wyy=False):
     """Histograms of the row segments [starts[i], starts[i]+counts[i]) of
-    ridx into slot i.  Returns hist [F, n_slots, Bs, C] float32."""
+    ridx into slot i.  Returns hist [F, n_slots, Bs, C] float64 (and, with
+    want_wyy in mode 0, the per-slot sum of w*y*y)."""
     C = channels(mode)
     dev = ridx.device
     hist = torch.zeros((bd.F, n_slots, bd.Bs, C), dtype=torch.float64, device=dev)
+    wyy = torch.zeros(n_slots, dtype=torch.float64, device=dev) if (want_wyy and mode == 0) else None
+    ret = (lambda: (hist, wyy)) if want_wyy else (lambda: hist)
     native = dev.type == "cuda" if use_native is None else use_native
     if native:
         lib = _lib()
@@ -125,23 +129,31 @@ def hist_build(bd, ridx, va, vb, mode, starts, counts, n_slots, use_native=None,
         n_fg = (bd.F + FG - 1) // FG
         total = int(sum(counts))
         if total == 0:
-            return hist
+            return ret()
         tgt_chunks = max(1, target_blocks // n_fg)
         chunk = max(2048, -(-total // tgt_chunks))
         items = make_work(starts, counts, range(n_slots), chunk)
         if not items:
-            return hist
+            return ret()
         work = torch.tensor(items, dtype=torch.int32).to(dev, non_blocking=True)
         threads = 512 if chunk >= 8192 else 256
         if vmax is None:
             vmax = channel_max(va, vb, mode)
         s0, s1 = (fixed_point_scale(m, chunk) for m in vmax)
         rc = lib.h2o_hist_build(_ptr(bd.codes), bd.code_bytes, bd.Fp, _ptr(ridx), _ptr(va), _ptr(vb), _ptr(work),
-                                len(items), bd.F, FG, bd.Bs, s0, s1, _ptr(hist), n_slots, mode, threads, _stream())
+                                len(items), bd.F, FG, bd.Bs, s0, s1, _ptr(hist), n_slots, mode, threads, _ptr(wyy),
+                                _stream())
         if rc != 0:
             raise RuntimeError(f"h2o_hist_build failed: hip error {rc}")
-        return hist
-    return _hist_build_torch(bd, ridx, va, vb, mode, starts, counts, hist)
+        return ret()
+    _hist_build_torch(bd, ridx, va, vb, mode, starts, counts, hist)
+    if wyy is not None:
+        for slot, (st, ct) in enumerate(zip(starts, counts)):
+            r = ridx[st: st + ct].long()
+            w = vb[r].to(torch.float64) if vb is not None else torch.ones(r.numel(), dtype=torch.float64, device=dev)
+            y = va[r].to(torch.float64)
+            wyy[slot] = (w * y * y).sum()
+    return ret()
 
 
 def _hist_build_torch(bd, ridx, va, vb, mode, starts, counts, hist):
