@@ -70,7 +70,7 @@ __global__ __launch_bounds__(512) void hist_build_kernel(
   const CodeT* cbase = codes + fg0 + fcl;
   for (int p0 = wk.y + wv * RPW + (lane_ok ? rs : 0); p0 < pend; p0 += U * step) {
     int rr[U];
-    float c0[U], c1[U];
+    float c0[U], c1[U], yv[U];
     int code[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) rr[u] = ridx[min(p0 + u * step, pend - 1)];
@@ -81,7 +81,7 @@ __global__ __launch_bounds__(512) void hist_build_kernel(
         const float y = va[r];
         const float w = HAS_VB ? vb[r] : 1.f;
         c0[u] = w; c1[u] = w * y;
-        if (do_wyy && p0 + u * step < pend) wyy += (double)(w * y) * (double)y;
+        yv[u] = y;
       } else if (MODE == 1) {
         c0[u] = va[r]; c1[u] = vb[r];
       } else {
@@ -95,7 +95,9 @@ __global__ __launch_bounds__(512) void hist_build_kernel(
     // (scripts/hist_microbench.hip: 1.78 vs 9.83 ms, 10M rows x 100 features).
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const bool ok = fok && (p0 + u * step < pend) && (c0[u] != 0.f || c1[u] != 0.f);
+      const bool inr = p0 + u * step < pend;
+      if (MODE == 0 && do_wyy && inr) wyy += (double)c1[u] * (double)yv[u];
+      const bool ok = fok && inr && (c0[u] != 0.f || c1[u] != 0.f);
       if (ok) {
         unsigned long long* h = hbase + code[u] * C;
         __hip_atomic_fetch_add(h, (unsigned long long)__float2ll_rn(c0[u] * s0), __ATOMIC_RELAXED,

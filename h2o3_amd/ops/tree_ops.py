@@ -71,20 +71,22 @@ def feature_group(F: int, Bs: int, mode: int, budget: int = _LDS_BUDGET) -> int:
 
 
 def make_work(starts, counts, slots, chunk):
-    """Chunk node segments into (slot, start, count, chunk_id) work items (host)."""
-    items = []
-    for st, ct, sl in zip(starts, counts, slots):
-        if ct <= 0:
-            continue
-        k = 0
-        p = st
-        end = st + ct
-        while p < end:
-            c = min(chunk, end - p)
-            items.append((sl, p, c, k))
-            p += c
-            k += 1
-    return items
+    """Chunk node segments into (slot, start, count, chunk_id) work items
+    (host, vectorized) -> int32 numpy array [n_items, 4]."""
+    import numpy as np
+    st = np.asarray(starts, dtype=np.int64).reshape(-1)
+    ct = np.asarray(counts, dtype=np.int64).reshape(-1)
+    sl = np.asarray(list(slots), dtype=np.int64).reshape(-1)
+    m = ct > 0
+    st, ct, sl = st[m], ct[m], sl[m]
+    if st.size == 0:
+        return np.zeros((0, 4), dtype=np.int32)
+    nch = (ct + chunk - 1) // chunk
+    rep = np.repeat(np.arange(st.size), nch)
+    k = np.arange(int(nch.sum())) - np.repeat(np.cumsum(nch) - nch, nch)
+    p = st[rep] + k * chunk
+    c = np.minimum(chunk, st[rep] + ct[rep] - p)
+    return np.stack([sl[rep], p, c, k], 1).astype(np.int32)
 
 
 def channel_max(va, vb, mode):
@@ -133,9 +135,9 @@ def hist_build(bd, ridx, va, vb, mode, starts, counts, n_slots, use_native=None,
         tgt_chunks = max(1, target_blocks // n_fg)
         chunk = max(2048, -(-total // tgt_chunks))
         items = make_work(starts, counts, range(n_slots), chunk)
-        if not items:
+        if len(items) == 0:
             return ret()
-        work = torch.tensor(items, dtype=torch.int32).to(dev, non_blocking=True)
+        work = torch.from_numpy(items).to(dev, non_blocking=True)
         threads = 512 if chunk >= 8192 else 256
         if vmax is None:
             vmax = channel_max(va, vb, mode)
@@ -193,9 +195,9 @@ def partition(bd, ridx, ridx_out, feats, masks, starts, counts, use_native=None,
     if native:
         lib = _lib()
         items = make_work(starts, counts, range(n), chunk)
-        if not items:
+        if len(items) == 0:
             return [0] * n
-        work = torch.tensor(items, dtype=torch.int32).to(dev, non_blocking=True)
+        work = torch.from_numpy(items).to(dev, non_blocking=True)
         nw = len(items)
         feat_t = torch.as_tensor(feats, dtype=torch.int32).to(dev)
         masks = masks.to(torch.uint8).contiguous()
@@ -208,26 +210,23 @@ def partition(bd, ridx, ridx_out, feats, masks, starts, counts, use_native=None,
                                 _ptr(masks), bd.Bs, _ptr(cnt), _stream())
         if rc != 0:
             raise RuntimeError(f"h2o_part_count failed: {rc}")
-        # per-node exclusive scans of the chunk counts (chunks of a node are consecutive)
-        wk = torch.tensor(items, dtype=torch.int64)
-        cnt_h = cnt.cpu().to(torch.int64)
-        slot = wk[:, 0]
-        nleft = torch.zeros(n, dtype=torch.int64).index_add_(0, slot, cnt_h)
-        csum = torch.cumsum(cnt_h, 0) - cnt_h   # global exclusive
-        first = torch.zeros(n, dtype=torch.int64)
-        # exclusive within node = global exclusive - global exclusive at node's first chunk
-        node_first = {}
-        for i, s in enumerate(slot.tolist()):
-            node_first.setdefault(s, i)
-        first_idx = torch.tensor([node_first[s] for s in slot.tolist()], dtype=torch.int64)
+        # per-node exclusive scans of the chunk counts (chunks of a node are
+        # consecutive in `items`), vectorized on the host
+        import numpy as np
+        cnt_h = cnt.cpu().numpy().astype(np.int64)
+        slot = items[:, 0].astype(np.int64)
+        nleft = np.bincount(slot, weights=cnt_h, minlength=n).astype(np.int64)
+        csum = np.cumsum(cnt_h) - cnt_h                       # global exclusive
+        first = np.ones(len(items), dtype=bool)
+        first[1:] = slot[1:] != slot[:-1]
+        first_idx = np.maximum.accumulate(np.where(first, np.arange(len(items)), 0))
         lpre = csum - csum[first_idx]
-        posinnode = wk[:, 1] - torch.tensor(starts, dtype=torch.int64)[slot]
-        rpre = posinnode - lpre
-        st = torch.tensor(starts, dtype=torch.int64)[slot]
-        loff = (st + lpre).to(torch.int32)
-        roff = (st + nleft[slot] + rpre).to(torch.int32)
-        loff_d = loff.to(dev, non_blocking=True)
-        roff_d = roff.to(dev, non_blocking=True)
+        st_arr = np.asarray(starts, dtype=np.int64)[slot]
+        rpre = (items[:, 1].astype(np.int64) - st_arr) - lpre
+        loff = (st_arr + lpre).astype(np.int32)
+        roff = (st_arr + nleft[slot] + rpre).astype(np.int32)
+        loff_d = torch.from_numpy(loff).to(dev, non_blocking=True)
+        roff_d = torch.from_numpy(roff).to(dev, non_blocking=True)
         rc = lib.h2o_part_scatter(_ptr(codes), bd.code_bytes, rs, fs, _ptr(ridx), _ptr(work), nw, _ptr(feat_t),
                                   _ptr(masks), bd.Bs, _ptr(loff_d), _ptr(roff_d), _ptr(ridx_out), _stream())
         if rc != 0:
@@ -256,18 +255,10 @@ def fill_nid(ridx, leaf_ids, starts, counts, nrows, use_native=None):
     native = dev.type == "cuda" if use_native is None else use_native
     if native:
         lib = _lib()
-        items = [(lid, st, ct, 0) for lid, st, ct in zip(leaf_ids, starts, counts) if ct > 0]
-        # split long segments
-        items2 = []
-        for lid, st, ct, _ in items:
-            p = st
-            while p < st + ct:
-                c = min(65536, st + ct - p)
-                items2.append((lid, p, c, 0))
-                p += c
-        if items2:
-            work = torch.tensor(items2, dtype=torch.int32).to(dev, non_blocking=True)
-            rc = lib.h2o_fill_nid(_ptr(ridx), _ptr(work), len(items2), _ptr(nid), _stream())
+        items = make_work(starts, counts, leaf_ids, 65536)
+        if len(items):
+            work = torch.from_numpy(items).to(dev, non_blocking=True)
+            rc = lib.h2o_fill_nid(_ptr(ridx), _ptr(work), len(items), _ptr(nid), _stream())
             if rc != 0:
                 raise RuntimeError(f"h2o_fill_nid failed: {rc}")
         return nid
@@ -287,9 +278,9 @@ def seg_sum2(ridx, a, b, leaf_ids, starts, counts, n_leaves, use_native=None, ch
             lib.h2o_seg_sum2.argtypes = [_c_void, _c_void, _c_void, _c_void, _c_int, _c_void, _c_void]
             lib._typed_seg = True
         items = make_work(starts, counts, leaf_ids, chunk)
-        if not items:
+        if len(items) == 0:
             return out
-        work = torch.tensor(items, dtype=torch.int32).to(dev, non_blocking=True)
+        work = torch.from_numpy(items).to(dev, non_blocking=True)
         a = a.to(torch.float32).contiguous()
         b = None if b is None else b.to(torch.float32).contiguous()
         rc = lib.h2o_seg_sum2(_ptr(ridx), _ptr(a), _ptr(b), _ptr(work), len(items), _ptr(out), _stream())
