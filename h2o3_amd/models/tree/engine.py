@@ -126,6 +126,8 @@ class TreeGrower:
         n = bd.nrows_local
         self.ridx = torch.empty(n, dtype=torch.int32, device=self.dev)
         self.ridx2 = torch.empty(n, dtype=torch.int32, device=self.dev)
+        # position-ordered copies of the two row channels, permuted with ridx
+        self._pay = [torch.empty(n, dtype=torch.float32, device=self.dev) for _ in range(4)]
         self.W = cloud.world()
         self.rank = cloud.rank()
         F = bd.F
@@ -142,6 +144,7 @@ class TreeGrower:
     def _build_hist(self, ridx, va, vb, mode, starts, counts):
         with phase("tree.hist"):
             H, wyy = tree_ops.hist_build(self.bd, ridx, va, vb, mode, starts, counts, len(starts), vmax=self._vmax,
+                                         posv=True,
                                          want_wyy=True)
         if wyy is not None:
             coll.allreduce_(wyy)
@@ -403,6 +406,13 @@ class TreeGrower:
         torch.arange(N, dtype=torch.int32, device=self.dev, out=self.ridx)
         self._vmax = tree_ops.channel_max(va, vb, mode) if self.dev.type == "cuda" else None
         ridx, ridx2 = self.ridx, self.ridx2
+        pa, pb, pa2, pb2 = self._pay
+        pa.copy_(va)
+        if vb is not None:
+            pb.copy_(vb)
+        else:
+            pb.fill_(1.0)
+        va, vb = pa, pb   # position order == row order while ridx is the identity
         tree = Tree()
         root = tree.add_node(0, 0.0)
         # frontier entries: [node_id, start, count_local, depth]
@@ -526,8 +536,13 @@ class TreeGrower:
             # partition
             with phase("tree.partition"):
                 ridx2.copy_(ridx)
-                nleft = tree_ops.partition(bd, ridx, ridx2, part_feats, masks, part_starts, part_counts)
+                pa2.copy_(pa)
+                pb2.copy_(pb)
+                nleft = tree_ops.partition(bd, ridx, ridx2, part_feats, masks, part_starts, part_counts,
+                                           payload=(pa, pb, pa2, pb2))
             ridx, ridx2 = ridx2, ridx
+            pa, pa2, pb, pb2 = pa2, pa, pb2, pb
+            va, vb = pa, pb
             for j, i in enumerate(split_ids):
                 nid_, st, ct, d = frontier[i][:4]
                 lid, rid = tree.left[nid_], tree.right[nid_]
@@ -554,6 +569,7 @@ class TreeGrower:
         with phase("tree.nid"):
             nid = tree_ops.fill_nid(ridx, lids, [s[1] for s in segs], [s[2] for s in segs], N)
         self.ridx, self.ridx2 = ridx, ridx2
+        self._pay = [pa, pb, pa2, pb2]
         self.last_segs = (lids, [s[1] for s in segs], [s[2] for s in segs])
         leaf_tot_t = torch.stack([torch.as_tensor(x, dtype=torch.float64) for x in leaf_tot]) if leaf_tot else \
             torch.zeros((0, C), dtype=torch.float64)

@@ -31,7 +31,7 @@
 template <int MODE> struct Chan { static constexpr int C = MODE == 2 ? 1 : 2; };
 
 // work[i] = (slot, pos_start, pos_count, unused);  grid = (n_work, n_feature_groups)
-template <typename CodeT, int MODE, bool HAS_VB>
+template <typename CodeT, int MODE, bool HAS_VB, bool POSV>
 __global__ __launch_bounds__(512) void hist_build_kernel(
     const CodeT* __restrict__ codes, int Fp, const int* __restrict__ ridx,
     const float* __restrict__ va, const float* __restrict__ vb,
@@ -77,15 +77,18 @@ __global__ __launch_bounds__(512) void hist_build_kernel(
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int r = rr[u];
+      // POSV: the gradient pair is stored in row-permutation (position) order
+      // and moved by the partition kernel, so it is read contiguously here
+      const int vi = POSV ? min(p0 + u * step, pend - 1) : r;
       if (MODE == 0) {
-        const float y = va[r];
-        const float w = HAS_VB ? vb[r] : 1.f;
+        const float y = va[vi];
+        const float w = HAS_VB ? vb[vi] : 1.f;
         c0[u] = w; c1[u] = w * y;
         yv[u] = y;
       } else if (MODE == 1) {
-        c0[u] = va[r]; c1[u] = vb[r];
+        c0[u] = va[vi]; c1[u] = vb[vi];
       } else {
-        c0[u] = HAS_VB ? vb[r] : 1.f; c1[u] = 0.f;
+        c0[u] = HAS_VB ? vb[vi] : 1.f; c1[u] = 0.f;
       }
       code[u] = (int)cbase[(size_t)r * Fp];
     }
@@ -129,18 +132,20 @@ __global__ __launch_bounds__(512) void hist_build_kernel(
 template <typename CodeT>
 static int launch_hist(const void* codes, int Fp, const int* ridx, const float* va, const float* vb,
                        const int4* work, int n_work, int F, int FG, int Bs, float s0, float s1, double* hist,
-                       int n_slots, int mode, int threads, double* wyy, hipStream_t s) {
+                       int n_slots, int mode, int threads, double* wyy, int posv, hipStream_t s) {
   const int n_fg = (F + FG - 1) / FG;
   dim3 grid(n_work, n_fg);
   const int C = mode == 2 ? 1 : 2;
   size_t lds = (size_t)FG * Bs * C * sizeof(unsigned long long);
   const CodeT* cc = (const CodeT*)codes;
   switch (mode) {
-#define H2O_LH(M, V) hipLaunchKernelGGL((hist_build_kernel<CodeT, M, V>), grid, dim3(threads), lds, s, cc, Fp, ridx, va, vb, work, F, Bs, FG, s0, s1, hist, n_slots, wyy)
+#define H2O_LH(M, V) if (posv) H2O_LH2(M, V, true); else H2O_LH2(M, V, false)
+#define H2O_LH2(M, V, PV) hipLaunchKernelGGL((hist_build_kernel<CodeT, M, V, PV>), grid, dim3(threads), lds, s, cc, Fp, ridx, va, vb, work, F, Bs, FG, s0, s1, hist, n_slots, wyy)
     case 0: if (vb) H2O_LH(0, true); else H2O_LH(0, false); break;
     case 1: H2O_LH(1, true); break;
     default: if (vb) H2O_LH(2, true); else H2O_LH(2, false); break;
 #undef H2O_LH
+#undef H2O_LH2
   }
   return (int)hipGetLastError();
 }
@@ -207,7 +212,9 @@ template <typename CodeT>
 __global__ __launch_bounds__(256) void part_scatter_kernel(
     const CodeT* __restrict__ codes, long long rs, long long fs, const int* __restrict__ ridx,
     const int4* __restrict__ work, const int* __restrict__ feat, const uint8_t* __restrict__ masks,
-    int Bs, const int* __restrict__ loff, const int* __restrict__ roff, int* __restrict__ out) {
+    int Bs, const int* __restrict__ loff, const int* __restrict__ roff, int* __restrict__ out,
+    const float* __restrict__ pa, const float* __restrict__ pb, float* __restrict__ pa_out,
+    float* __restrict__ pb_out) {
   __shared__ uint8_t m[4096];
   __shared__ int wsum[4];
   const int4 wk = work[blockIdx.x];
@@ -258,8 +265,10 @@ __global__ __launch_bounds__(256) void part_scatter_kernel(
 #pragma unroll
       for (int k = 0; k < 16; ++k) {
         if (p0 + k < end) {
-          if ((bits >> k) & 1u) out[li++] = r[k];
-          else out[ri++] = r[k];
+          // row payload (position-ordered gradient pair) moves with the row id
+          const int dst = ((bits >> k) & 1u) ? li++ : ri++;
+          out[dst] = r[k];
+          if (pa) { pa_out[dst] = pa[p0 + k]; pb_out[dst] = pb[p0 + k]; }
         }
       }
     }
@@ -280,11 +289,11 @@ extern "C" {
 
 int h2o_hist_build(const void* codes, int code_bytes, int Fp, const int* ridx, const float* va,
                    const float* vb, const int* work, int n_work, int F, int FG, int Bs, float s0, float s1,
-                   double* hist, int n_slots, int mode, int threads, double* wyy, hipStream_t s) {
+                   double* hist, int n_slots, int mode, int threads, double* wyy, int posv, hipStream_t s) {
   if (n_work <= 0) return 0;
   if (code_bytes == 1)
-    return launch_hist<uint8_t>(codes, Fp, ridx, va, vb, (const int4*)work, n_work, F, FG, Bs, s0, s1, hist, n_slots, mode, threads, wyy, s);
-  return launch_hist<uint16_t>(codes, Fp, ridx, va, vb, (const int4*)work, n_work, F, FG, Bs, s0, s1, hist, n_slots, mode, threads, wyy, s);
+    return launch_hist<uint8_t>(codes, Fp, ridx, va, vb, (const int4*)work, n_work, F, FG, Bs, s0, s1, hist, n_slots, mode, threads, wyy, posv, s);
+  return launch_hist<uint16_t>(codes, Fp, ridx, va, vb, (const int4*)work, n_work, F, FG, Bs, s0, s1, hist, n_slots, mode, threads, wyy, posv, s);
 }
 
 int h2o_part_count(const void* codes, int code_bytes, long long rs, long long fs, const int* ridx,
@@ -300,12 +309,13 @@ int h2o_part_count(const void* codes, int code_bytes, long long rs, long long fs
 
 int h2o_part_scatter(const void* codes, int code_bytes, long long rs, long long fs, const int* ridx,
                      const int* work, int n_work, const int* feat, const uint8_t* masks, int Bs,
-                     const int* loff, const int* roff, int* out, hipStream_t s) {
+                     const int* loff, const int* roff, int* out, const float* pa, const float* pb,
+                     float* pa_out, float* pb_out, hipStream_t s) {
   if (n_work <= 0) return 0;
   if (code_bytes == 1)
-    hipLaunchKernelGGL(part_scatter_kernel<uint8_t>, dim3(n_work), dim3(256), 0, s, (const uint8_t*)codes, rs, fs, ridx, (const int4*)work, feat, masks, Bs, loff, roff, out);
+    hipLaunchKernelGGL(part_scatter_kernel<uint8_t>, dim3(n_work), dim3(256), 0, s, (const uint8_t*)codes, rs, fs, ridx, (const int4*)work, feat, masks, Bs, loff, roff, out, pa, pb, pa_out, pb_out);
   else
-    hipLaunchKernelGGL(part_scatter_kernel<uint16_t>, dim3(n_work), dim3(256), 0, s, (const uint16_t*)codes, rs, fs, ridx, (const int4*)work, feat, masks, Bs, loff, roff, out);
+    hipLaunchKernelGGL(part_scatter_kernel<uint16_t>, dim3(n_work), dim3(256), 0, s, (const uint16_t*)codes, rs, fs, ridx, (const int4*)work, feat, masks, Bs, loff, roff, out, pa, pb, pa_out, pb_out);
   return (int)hipGetLastError();
 }
 

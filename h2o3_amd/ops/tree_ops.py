@@ -31,11 +31,12 @@ def _lib():
     if lib is not None and not getattr(lib, "_typed", False):
         lib.h2o_hist_build.argtypes = [_c_void, _c_int, _c_int, _c_void, _c_void, _c_void, _c_void, _c_int,
                                        _c_int, _c_int, _c_int, ctypes.c_float, ctypes.c_float, _c_void, _c_int, _c_int,
-                                       _c_int, _c_void, _c_void]
+                                       _c_int, _c_void, _c_int, _c_void]
         lib.h2o_part_count.argtypes = [_c_void, _c_int, _c_ll, _c_ll, _c_void, _c_void, _c_int, _c_void,
                                        _c_void, _c_int, _c_void, _c_void]
         lib.h2o_part_scatter.argtypes = [_c_void, _c_int, _c_ll, _c_ll, _c_void, _c_void, _c_int, _c_void,
-                                         _c_void, _c_int, _c_void, _c_void, _c_void, _c_void]
+                                         _c_void, _c_int, _c_void, _c_void, _c_void, _c_void, _c_void, _c_void,
+                                         _c_void, _c_void]
         lib.h2o_fill_nid.argtypes = [_c_void, _c_void, _c_int, _c_void, _c_void]
         lib._typed = True
     return lib
@@ -115,10 +116,11 @@ def fixed_point_scale(maxv, nmax):
 
 
 def hist_build(bd, ridx, va, vb, mode, starts, counts, n_slots, use_native=None, target_blocks=2048, vmax=None,
-               want_wyy=False):
+               want_wyy=False, posv=False):
     """Histograms of the row segments [starts[i], starts[i]+counts[i]) of
     ridx into slot i.  Returns hist [F, n_slots, Bs, C] float64 (and, with
-    want_wyy in mode 0, the per-slot sum of w*y*y)."""
+    want_wyy in mode 0, the per-slot sum of w*y*y).  posv: va/vb are stored
+    in position (row-permutation) order instead of row order."""
     C = channels(mode)
     dev = ridx.device
     hist = torch.zeros((bd.F, n_slots, bd.Bs, C), dtype=torch.float64, device=dev)
@@ -144,10 +146,19 @@ def hist_build(bd, ridx, va, vb, mode, starts, counts, n_slots, use_native=None,
         s0, s1 = (fixed_point_scale(m, chunk) for m in vmax)
         rc = lib.h2o_hist_build(_ptr(bd.codes), bd.code_bytes, bd.Fp, _ptr(ridx), _ptr(va), _ptr(vb), _ptr(work),
                                 len(items), bd.F, FG, bd.Bs, s0, s1, _ptr(hist), n_slots, mode, threads, _ptr(wyy),
-                                _stream())
+                                1 if posv else 0, _stream())
         if rc != 0:
             raise RuntimeError(f"h2o_hist_build failed: hip error {rc}")
         return ret()
+    if posv:
+        # expand position-ordered payloads to row order for the reference path
+        va_r = torch.empty_like(va)
+        va_r[ridx.long()] = va
+        vb_r = None
+        if vb is not None:
+            vb_r = torch.empty_like(vb)
+            vb_r[ridx.long()] = vb
+        va, vb = va_r, vb_r
     _hist_build_torch(bd, ridx, va, vb, mode, starts, counts, hist)
     if wyy is not None:
         for slot, (st, ct) in enumerate(zip(starts, counts)):
@@ -184,9 +195,11 @@ def _hist_build_torch(bd, ridx, va, vb, mode, starts, counts, hist):
     return hist
 
 
-def partition(bd, ridx, ridx_out, feats, masks, starts, counts, use_native=None, chunk=16384):
+def partition(bd, ridx, ridx_out, feats, masks, starts, counts, use_native=None, chunk=16384, payload=None):
     """Stable-partition each segment i by masks[i][code(row, feats[i])] (1 =
-    left).  Writes ridx_out and returns per-segment left counts (host list)."""
+    left).  Writes ridx_out and returns per-segment left counts (host list).
+    payload = (pa, pb, pa_out, pb_out): position-ordered float arrays moved
+    together with the row ids."""
     dev = ridx.device
     n = len(starts)
     if n == 0:
@@ -227,8 +240,10 @@ def partition(bd, ridx, ridx_out, feats, masks, starts, counts, use_native=None,
         roff = (st_arr + nleft[slot] + rpre).astype(np.int32)
         loff_d = torch.from_numpy(loff).to(dev, non_blocking=True)
         roff_d = torch.from_numpy(roff).to(dev, non_blocking=True)
+        pa, pb, pa_o, pb_o = payload if payload is not None else (None, None, None, None)
         rc = lib.h2o_part_scatter(_ptr(codes), bd.code_bytes, rs, fs, _ptr(ridx), _ptr(work), nw, _ptr(feat_t),
-                                  _ptr(masks), bd.Bs, _ptr(loff_d), _ptr(roff_d), _ptr(ridx_out), _stream())
+                                  _ptr(masks), bd.Bs, _ptr(loff_d), _ptr(roff_d), _ptr(ridx_out), _ptr(pa), _ptr(pb),
+                                  _ptr(pa_o), _ptr(pb_o), _stream())
         if rc != 0:
             raise RuntimeError(f"h2o_part_scatter failed: {rc}")
         return nleft.tolist()
@@ -244,6 +259,12 @@ def partition(bd, ridx, ridx_out, feats, masks, starts, counts, use_native=None,
         r = seg[~left]
         ridx_out[st: st + l.numel()] = l
         ridx_out[st + l.numel(): st + ct] = r
+        if payload is not None:
+            pa, pb, pa_o, pb_o = payload
+            for src, dst in ((pa, pa_o), (pb, pb_o)):
+                v = src[st: st + ct]
+                dst[st: st + l.numel()] = v[left]
+                dst[st + l.numel(): st + ct] = v[~left]
         out.append(int(l.numel()))
     return out
 
