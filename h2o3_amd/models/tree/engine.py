@@ -127,7 +127,11 @@ class TreeGrower:
         self.ridx = torch.empty(n, dtype=torch.int32, device=self.dev)
         self.ridx2 = torch.empty(n, dtype=torch.int32, device=self.dev)
         # position-ordered copies of the two row channels, permuted with ridx
-        self._pay = [torch.empty(n, dtype=torch.float32, device=self.dev) for _ in range(4)]
+        # (off by default: the extra scattered writes in the partition cost more
+        # than the contiguous histogram reads save — see PERF.md)
+        self.use_payload = False
+        self._pay = [torch.empty(n, dtype=torch.float32, device=self.dev) for _ in range(4)] \
+            if self.use_payload else [None] * 4
         self.W = cloud.world()
         self.rank = cloud.rank()
         F = bd.F
@@ -144,7 +148,7 @@ class TreeGrower:
     def _build_hist(self, ridx, va, vb, mode, starts, counts):
         with phase("tree.hist"):
             H, wyy = tree_ops.hist_build(self.bd, ridx, va, vb, mode, starts, counts, len(starts), vmax=self._vmax,
-                                         posv=True,
+                                         posv=self.use_payload,
                                          want_wyy=True)
         if wyy is not None:
             coll.allreduce_(wyy)
@@ -407,12 +411,13 @@ class TreeGrower:
         self._vmax = tree_ops.channel_max(va, vb, mode) if self.dev.type == "cuda" else None
         ridx, ridx2 = self.ridx, self.ridx2
         pa, pb, pa2, pb2 = self._pay
-        pa.copy_(va)
-        if vb is not None:
-            pb.copy_(vb)
-        else:
-            pb.fill_(1.0)
-        va, vb = pa, pb   # position order == row order while ridx is the identity
+        if self.use_payload:
+            pa.copy_(va)
+            if vb is not None:
+                pb.copy_(vb)
+            else:
+                pb.fill_(1.0)
+            va, vb = pa, pb   # position order == row order while ridx is the identity
         tree = Tree()
         root = tree.add_node(0, 0.0)
         # frontier entries: [node_id, start, count_local, depth]
@@ -536,13 +541,15 @@ class TreeGrower:
             # partition
             with phase("tree.partition"):
                 ridx2.copy_(ridx)
-                pa2.copy_(pa)
-                pb2.copy_(pb)
+                if self.use_payload:
+                    pa2.copy_(pa)
+                    pb2.copy_(pb)
                 nleft = tree_ops.partition(bd, ridx, ridx2, part_feats, masks, part_starts, part_counts,
-                                           payload=(pa, pb, pa2, pb2))
+                                           payload=(pa, pb, pa2, pb2) if self.use_payload else None)
             ridx, ridx2 = ridx2, ridx
-            pa, pa2, pb, pb2 = pa2, pa, pb2, pb
-            va, vb = pa, pb
+            if self.use_payload:
+                pa, pa2, pb, pb2 = pa2, pa, pb2, pb
+                va, vb = pa, pb
             for j, i in enumerate(split_ids):
                 nid_, st, ct, d = frontier[i][:4]
                 lid, rid = tree.left[nid_], tree.right[nid_]
