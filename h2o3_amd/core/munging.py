@@ -1,0 +1,739 @@
+"""Frame munging: the Rapids prims behind the H2OFrame API.
+
+Reference: water/rapids/ast/prims/mungers/* (AstGroup, AstMerge, AstSort,
+AstCut, AstFillNA, AstMelt, AstPivot, AstRankWithinGroupBy, AstTable...),
+water/rapids/ast/prims/advmath/* (AstQtile, AstKFold, AstStratifiedSplit,
+AstCorrelation, AstHist, AstImpute, AstUnique...), hex/quantile/Quantile.java,
+hex/SplitFrame.java, hex/createframe/*.
+
+Design: group-by / merge / sort use GPU primitives (torch.unique with
+inverse, argsort, searchsorted, index_add) on the HBM-resident columns.
+With several ranks, order-dependent ops gather the keys (small) and
+re-shard the result.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from ..parallel import cloud
+from ..parallel import collectives as coll
+from .frame import H2OFrame, _fmt_level, _local_slice, _reshard, _take, _to_enum, _vec_from_array
+from .vec import NUMERIC_TYPES, T_ENUM, T_INT, T_REAL, T_STR, T_TIME, Vec, make_enum, make_numeric, make_string
+
+
+def _dev():
+    return cloud.device()
+
+
+# ---------------------------------------------------------------- quantiles
+def quantile_values(v: Vec, probs, method="interpolate", weights=None):
+    x = v.as_float(torch.float64)
+    ok = ~torch.isnan(x)
+    x = x[ok]
+    w = None if weights is None else weights[ok].to(torch.float64)
+    if cloud.is_distributed():
+        x = coll.all_gather_var(x)
+        if w is not None:
+            w = coll.all_gather_var(w)
+    if x.numel() == 0:
+        return [float("nan")] * len(probs)
+    o = torch.argsort(x)
+    xs = x[o]
+    out = []
+    if w is not None:
+        ws = w[o]
+        cw = torch.cumsum(ws, 0)
+        tot = float(cw[-1])
+        for p in probs:
+            t = p * tot
+            i = int(torch.searchsorted(cw, torch.tensor([t], dtype=cw.dtype, device=cw.device)).clamp(max=xs.numel() - 1))
+            out.append(float(xs[i]))
+        return out
+    n = xs.numel()
+    for p in probs:
+        # reference (hex/quantile/Quantile.java): R type-7 interpolation
+        h = (n - 1) * p
+        lo = int(math.floor(h))
+        hi = min(lo + 1, n - 1)
+        if method in ("low",):
+            out.append(float(xs[lo]))
+        elif method in ("high",):
+            out.append(float(xs[hi]))
+        elif method == "average":
+            out.append(float((xs[lo] + xs[hi]) / 2) if h != lo else float(xs[lo]))
+        else:
+            out.append(float(xs[lo] + (h - lo) * (xs[hi] - xs[lo])))
+    return out
+
+
+def quantile(fr, prob=None, combine_method="interpolate", weights_column=None):
+    probs = prob if prob is not None else [0.001, 0.01, 0.1, 0.25, 0.333, 0.5, 0.667, 0.75, 0.9, 0.99, 0.999]
+    w = fr.vec(weights_column).as_float() if weights_column else None
+    data = {"Probs": probs}
+    for n, v in zip(fr.names, fr._vecs):
+        if n == weights_column:
+            continue
+        if v.is_numeric or v.is_time:
+            data[f"{n}Quantiles"] = quantile_values(v, probs, combine_method, w)
+        else:
+            data[f"{n}Quantiles"] = [float("nan")] * len(probs)
+    import pandas as pd
+    return H2OFrame(pd.DataFrame(data), _local=not cloud.is_distributed())
+
+
+# ---------------------------------------------------------------- unique / table
+def unique(fr, include_nas=False):
+    v = fr.gather()._vecs[0]
+    if v.type == T_ENUM:
+        codes = torch.unique(v.data)
+        if not include_nas:
+            codes = codes[codes >= 0]
+        return _reshard(H2OFrame.from_vecs([Vec(codes.to(torch.int32), T_ENUM, v.domain)], fr.names[:1]))
+    if v.on_host:
+        vals = sorted(set(x for x in v.data if x is not None or include_nas), key=lambda s: (s is None, s))
+        return _reshard(H2OFrame.from_vecs([make_string(vals)], fr.names[:1]))
+    x = v.as_float(torch.float64)
+    u = torch.unique(x[~torch.isnan(x)])
+    if include_nas and bool(torch.isnan(x).any()):
+        u = torch.cat([u, torch.tensor([float("nan")], dtype=u.dtype, device=u.device)])
+    return _reshard(H2OFrame.from_vecs([Vec(u.to(torch.float32) if v.data.dtype == torch.float32 else u, v.type)],
+                                       fr.names[:1]))
+
+
+def table(fr, data2=None, dense=True):
+    import pandas as pd
+    g = fr.gather()
+    if data2 is not None:
+        g = g.cbind(data2.gather())
+    cols = g.names[:2] if data2 is not None or g.ncols >= 2 else g.names[:1]
+    df = g[cols].as_data_frame()
+    res = df.groupby(cols, dropna=True).size().reset_index(name="Counts")
+    if not dense and len(cols) == 2:
+        res = res.pivot(index=cols[0], columns=cols[1], values="Counts").fillna(0).reset_index()
+    return H2OFrame(res, _local=True, column_types={c: "enum" for c in cols if g.vec(c).type == T_ENUM})
+
+
+def hist(fr, breaks="sturges"):
+    v = fr._vecs[0]
+    x = v.as_float(torch.float64)
+    x = x[~torch.isnan(x)]
+    if cloud.is_distributed():
+        x = coll.all_gather_var(x)
+    n = x.numel()
+    lo, hi = float(x.min()), float(x.max())
+    if isinstance(breaks, (list, tuple)):
+        edges = np.asarray(breaks, dtype=float)
+    else:
+        if breaks == "sturges" or breaks is None:
+            k = int(math.ceil(math.log2(max(n, 1)) + 1))
+        elif breaks == "rice":
+            k = int(math.ceil(2 * n ** (1 / 3)))
+        elif breaks == "sqrt":
+            k = int(math.ceil(math.sqrt(n)))
+        elif breaks == "doane":
+            k = int(math.ceil(math.log2(max(n, 1)) + 1))
+        elif breaks == "scott":
+            sd = float(x.std())
+            k = int(math.ceil((hi - lo) / (3.5 * sd / n ** (1 / 3)))) if sd > 0 else 1
+        elif breaks == "fd":
+            q = torch.quantile(x[: min(n, 1 << 24)], torch.tensor([0.25, 0.75], dtype=x.dtype, device=x.device))
+            iqr = float(q[1] - q[0])
+            k = int(math.ceil((hi - lo) / (2 * iqr / n ** (1 / 3)))) if iqr > 0 else 1
+        else:
+            k = int(breaks)
+        edges = np.linspace(lo, hi, k + 1)
+    e = torch.tensor(edges, dtype=x.dtype, device=x.device)
+    idx = torch.clamp(torch.searchsorted(e, x, right=True) - 1, 0, len(edges) - 2)
+    counts = torch.bincount(idx, minlength=len(edges) - 1).cpu().numpy()
+    import pandas as pd
+    mids = (edges[:-1] + edges[1:]) / 2
+    df = pd.DataFrame({"breaks": edges[1:], "counts": counts.astype(float), "mids_true": mids, "mids": mids,
+                       "density": counts / max(counts.sum(), 1) / np.diff(edges)})
+    return H2OFrame(df, _local=True)
+
+
+# ---------------------------------------------------------------- stats
+def _num_matrix(fr):
+    return torch.stack([v.as_float(torch.float64) for v in fr._vecs], 1)
+
+
+def cor(x, y=None, method="Pearson", use="everything"):
+    a = _num_matrix(x.gather())
+    b = _num_matrix(y.gather()) if y is not None else a
+    if method.lower() == "spearman":
+        a = torch.argsort(torch.argsort(a, 0), 0).to(torch.float64)
+        b = torch.argsort(torch.argsort(b, 0), 0).to(torch.float64)
+    ac = a - a.mean(0)
+    bc = b - b.mean(0)
+    c = (ac.T @ bc) / torch.sqrt(torch.outer((ac ** 2).sum(0), (bc ** 2).sum(0)))
+    if c.numel() == 1:
+        return float(c)
+    import pandas as pd
+    return H2OFrame(pd.DataFrame(c.cpu().numpy(), columns=(y or x).names), _local=True)
+
+
+def cov(x, y=None):
+    a = _num_matrix(x.gather())
+    b = _num_matrix(y.gather()) if y is not None else a
+    n = a.shape[0]
+    c = ((a - a.mean(0)).T @ (b - b.mean(0))) / (n - 1)
+    if c.numel() == 1:
+        return float(c)
+    import pandas as pd
+    return H2OFrame(pd.DataFrame(c.cpu().numpy(), columns=(y or x).names), _local=True)
+
+
+def distance(x, y, measure="l2"):
+    a = _num_matrix(x.gather())
+    b = _num_matrix(y.gather())
+    m = measure.lower()
+    if m == "l1":
+        d = torch.cdist(a, b, p=1)
+    elif m == "l2":
+        d = torch.cdist(a, b, p=2)
+    elif m == "cosine":
+        d = (a @ b.T) / torch.outer(a.norm(dim=1), b.norm(dim=1))
+    elif m == "cosine_sq":
+        d = ((a @ b.T) / torch.outer(a.norm(dim=1), b.norm(dim=1))) ** 2
+    else:
+        raise ValueError(measure)
+    return _reshard(H2OFrame.from_tensor(d))
+
+
+# ---------------------------------------------------------------- random / split
+def _global_uniform(fr, seed):
+    """Uniform [0,1) per global row, identical regardless of sharding."""
+    seed = 42 if seed is None or seed == -1 else int(seed)
+    g = torch.Generator(device="cpu").manual_seed(seed & 0x7FFFFFFFFFFF)
+    n = fr.nrows
+    off = fr.row_offset()
+    r = torch.rand(n, generator=g, dtype=torch.float64)[off: off + fr.nlocal]
+    return r.to(_dev())
+
+
+def runif(fr, seed=None):
+    r = _global_uniform(fr, seed)
+    return H2OFrame.from_vecs([Vec(r, T_REAL)], ["rnd"])
+
+
+def split_frame(fr, ratios, seed=None):
+    """reference: hex/SplitFrame.java (random per-row assignment)."""
+    r = _global_uniform(fr, seed)
+    edges = np.cumsum([0.0] + list(ratios))
+    out = []
+    for i in range(len(ratios) + 1):
+        lo = edges[i]
+        hi = edges[i + 1] if i < len(ratios) else 1.0 + 1e-12
+        m = (r >= lo) & (r < hi)
+        out.append(fr[m])
+    return out
+
+
+def kfold_column(fr, n_folds=3, seed=-1):
+    r = _global_uniform(fr, seed)
+    f = torch.floor(r * n_folds).clamp(max=n_folds - 1)
+    return H2OFrame.from_vecs([Vec(f.to(torch.float32), T_INT)], ["fold"])
+
+
+def modulo_kfold_column(fr, n_folds=3):
+    off = fr.row_offset()
+    f = (torch.arange(off, off + fr.nlocal, device=_dev()) % n_folds).to(torch.float32)
+    return H2OFrame.from_vecs([Vec(f, T_INT)], ["fold"])
+
+
+def stratified_kfold_column(fr, n_folds=3, seed=-1):
+    v = fr._vecs[0]
+    y = v.data if v.type == T_ENUM else v.as_float().nan_to_num(-1).to(torch.int64)
+    r = _global_uniform(fr, seed)
+    f = torch.zeros(fr.nlocal, dtype=torch.float32, device=_dev())
+    for c in torch.unique(y).tolist():
+        idx = torch.nonzero(y == c).flatten()
+        o = torch.argsort(r[idx])
+        f[idx[o]] = (torch.arange(idx.numel(), device=_dev()) % n_folds).to(torch.float32)
+    return H2OFrame.from_vecs([Vec(f, T_INT)], ["fold"])
+
+
+def stratified_split(fr, test_frac=0.2, seed=-1):
+    v = fr._vecs[0]
+    y = v.data if v.type == T_ENUM else v.as_float().nan_to_num(-1).to(torch.int64)
+    r = _global_uniform(fr, seed)
+    out = np.empty(fr.nlocal, dtype=object)
+    lab = torch.zeros(fr.nlocal, dtype=torch.int32, device=_dev())
+    for c in torch.unique(y).tolist():
+        idx = torch.nonzero(y == c).flatten()
+        o = torch.argsort(r[idx])
+        ntest = int(round(test_frac * idx.numel()))
+        lab[idx[o[:ntest]]] = 1
+    return H2OFrame.from_vecs([Vec(lab, T_ENUM, ["train", "test"])], ["test_train_split"])
+
+
+# ---------------------------------------------------------------- rbind
+def rbind(frames):
+    frames = [f if isinstance(f, H2OFrame) else H2OFrame(f) for f in frames]
+    base = frames[0]
+    vecs = []
+    for j, n in enumerate(base.names):
+        parts = [f._vecs[j] for f in frames]
+        t = parts[0].type
+        if any(p.type == T_ENUM for p in parts):
+            dom = []
+            for p in parts:
+                for d in (p.domain or []):
+                    if d not in dom:
+                        dom.append(d)
+            codes = []
+            for p in parts:
+                if p.type == T_ENUM:
+                    rm = torch.tensor([dom.index(d) for d in p.domain] or [0], dtype=torch.int32, device=_dev())
+                    codes.append(torch.where(p.data < 0, p.data, rm[p.data.clamp(min=0).long()]))
+                else:
+                    vals = p.to_numpy()
+                    codes.append(torch.tensor([dom.index(_fmt_level(x)) if x is not None and not (isinstance(x, float) and math.isnan(x)) and _fmt_level(x) in dom else -1 for x in vals], dtype=torch.int32, device=_dev()))
+            vecs.append(Vec(torch.cat(codes), T_ENUM, dom))
+        elif any(p.on_host for p in parts):
+            vecs.append(make_string(np.concatenate([np.asarray(p.to_numpy(), dtype=object) for p in parts])))
+        else:
+            dt = torch.float64 if any(p.data.dtype == torch.float64 for p in parts) else torch.float32
+            vv = Vec(torch.cat([p.as_float(dt) for p in parts]), t if all(p.type == t for p in parts) else T_REAL)
+            vecs.append(vv)
+    return H2OFrame.from_vecs(vecs, base.names)
+
+
+# ---------------------------------------------------------------- sort / merge / group-by
+def _key_tensor(v: Vec):
+    if v.type == T_ENUM:
+        return v.data.to(torch.float64)
+    if v.on_host:
+        arr = v.to_numpy()
+        uniq = sorted(set(x for x in arr if x is not None))
+        m = {s: i for i, s in enumerate(uniq)}
+        return torch.tensor([m[x] if x is not None else float("nan") for x in arr], dtype=torch.float64, device=_dev())
+    return v.as_float(torch.float64)
+
+
+def sort(fr, by, ascending=True):
+    g = fr.gather()
+    by = by if isinstance(by, (list, tuple)) else [by]
+    asc = ascending if isinstance(ascending, (list, tuple)) else [ascending] * len(by)
+    idx = torch.arange(g.nlocal, device=_dev())
+    for b, a in reversed(list(zip(by, asc))):
+        k = _key_tensor(g.vec(b))[idx]
+        k = torch.where(torch.isnan(k), torch.full_like(k, -math.inf), k)  # NAs first (reference)
+        o = torch.argsort(k if a else -k, stable=True)
+        idx = idx[o]
+    res = H2OFrame.from_vecs([_take(v, idx) for v in g._vecs], g.names)
+    for v in res._vecs:
+        v.replicated = g._vecs[0].replicated
+    return _reshard(res) if cloud.is_distributed() else res
+
+
+def _group_ids(frame, cols):
+    keys = [_key_tensor(frame.vec(c)) for c in cols]
+    K = torch.stack(keys, 1)
+    K = torch.where(torch.isnan(K), torch.full_like(K, -1e300), K)
+    uniq, inv = torch.unique(K, dim=0, return_inverse=True)
+    return uniq, inv
+
+
+class GroupBy:
+    """reference: AstGroup (group-by with aggregates count/sum/mean/min/max/sd/var/ss/nrow/median/mode)."""
+
+    def __init__(self, fr, by):
+        self.fr = fr.gather()
+        self.by = [fr.names[b] if isinstance(b, int) else b for b in (by if isinstance(by, (list, tuple)) else [by])]
+        self.aggs = []
+        self._res = None
+
+    def _add(self, op, col, na):
+        cols = [c for c in self.fr.names if c not in self.by] if col is None else (col if isinstance(col, (list, tuple)) else [col])
+        for c in cols:
+            self.aggs.append((op, c, na))
+        return self
+
+    def count(self, na="all"):
+        self.aggs.append(("nrow", None, na))
+        return self
+
+    def sum(self, col=None, na="all"): return self._add("sum", col, na)
+    def mean(self, col=None, na="all"): return self._add("mean", col, na)
+    def min(self, col=None, na="all"): return self._add("min", col, na)
+    def max(self, col=None, na="all"): return self._add("max", col, na)
+    def sd(self, col=None, na="all"): return self._add("sd", col, na)
+    def var(self, col=None, na="all"): return self._add("var", col, na)
+    def ss(self, col=None, na="all"): return self._add("ss", col, na)
+    def median(self, col=None, na="all"): return self._add("median", col, na)
+    def mode(self, col=None, na="all"): return self._add("mode", col, na)
+
+    def get_frame(self):
+        if self._res is not None:
+            return self._res
+        fr = self.fr
+        uniq, inv = _group_ids(fr, self.by)
+        G = uniq.shape[0]
+        out_vecs, out_names = [], []
+        for j, b in enumerate(self.by):
+            v = fr.vec(b)
+            col = uniq[:, j]
+            col = torch.where(col == -1e300, torch.full_like(col, float("nan")), col)
+            if v.type == T_ENUM:
+                out_vecs.append(Vec(torch.nan_to_num(col, nan=-1).to(torch.int32), T_ENUM, v.domain))
+            else:
+                out_vecs.append(Vec(col, v.type))
+            out_names.append(b)
+        for op, c, na in self.aggs:
+            if op == "nrow":
+                cnt = torch.bincount(inv, minlength=G).to(torch.float64)
+                out_vecs.append(Vec(cnt, T_INT))
+                out_names.append("nrow")
+                continue
+            x = fr.vec(c).as_float(torch.float64)
+            nan = torch.isnan(x)
+            if na == "rm" or na == "ignore":
+                xz = torch.where(nan, torch.zeros_like(x), x)
+                ok = (~nan).to(torch.float64)
+            else:
+                xz, ok = x, torch.ones_like(x)
+            s = torch.zeros(G, dtype=torch.float64, device=x.device).index_add_(0, inv, xz)
+            n = torch.zeros(G, dtype=torch.float64, device=x.device).index_add_(0, inv, ok)
+            if op == "sum":
+                r = s
+            elif op == "mean":
+                r = s / n
+            elif op in ("min", "max"):
+                fill = math.inf if op == "min" else -math.inf
+                r = torch.full((G,), fill, dtype=torch.float64, device=x.device)
+                r = r.scatter_reduce(0, inv, torch.where(nan, torch.full_like(x, fill), x), reduce="amin" if op == "min" else "amax")
+            elif op in ("sd", "var", "ss"):
+                mean = s / n
+                d = xz - mean[inv]
+                ss = torch.zeros(G, dtype=torch.float64, device=x.device).index_add_(0, inv, torch.where(ok > 0, d * d, torch.zeros_like(d)))
+                r = ss if op == "ss" else (ss / (n - 1) if op == "var" else torch.sqrt(ss / (n - 1)))
+            elif op in ("median", "mode"):
+                r = torch.empty(G, dtype=torch.float64, device=x.device)
+                o = torch.argsort(inv * 0 + x)
+                for gi in range(G):
+                    vals = x[inv == gi]
+                    vals = vals[~torch.isnan(vals)]
+                    if vals.numel() == 0:
+                        r[gi] = float("nan")
+                    elif op == "median":
+                        r[gi] = torch.quantile(vals, 0.5)
+                    else:
+                        u, cts = torch.unique(vals, return_counts=True)
+                        r[gi] = u[torch.argmax(cts)]
+            out_vecs.append(Vec(r, T_REAL))
+            out_names.append(f"{op}_{c}")
+        res = H2OFrame.from_vecs(out_vecs, out_names)
+        self._res = _reshard(res) if cloud.is_distributed() else res
+        return self._res
+
+    @property
+    def frame(self):
+        return self.get_frame()
+
+
+def merge(x, y, all_x=False, all_y=False, by_x=None, by_y=None):
+    """reference: water/rapids/Merge.java (radix-sort join).  Hash join on the
+    host for the key tuples, gather on the device."""
+    import pandas as pd
+    gx, gy = x.gather(), y.gather()
+    if by_x is None:
+        common = [n for n in gx.names if n in gy.names]
+        by_x = by_y = common
+    by_y = by_y or by_x
+    dx = gx.as_data_frame()
+    dy = gy.as_data_frame()
+    dx["__ix"] = np.arange(len(dx))
+    dy["__iy"] = np.arange(len(dy))
+    how = "outer" if (all_x and all_y) else ("left" if all_x else ("right" if all_y else "inner"))
+    m = dx[by_x + ["__ix"]].merge(dy[by_y + ["__iy"]], left_on=by_x, right_on=by_y, how=how, sort=True)
+    vecs, names = [], []
+    ix = m["__ix"].values
+    iy = m["__iy"].values
+    for n, v in zip(gx.names, gx._vecs):
+        vecs.append(_take_with_na(v, ix))
+        names.append(n)
+    for n, v in zip(gy.names, gy._vecs):
+        if n in by_y:
+            continue
+        nn = n if n not in names else n + "0"
+        vecs.append(_take_with_na(v, iy))
+        names.append(nn)
+    # fill keys for right-only rows
+    for kx, ky in zip(by_x, by_y):
+        j = names.index(kx)
+        miss = np.isnan(ix.astype(float)) if ix.dtype.kind == "f" else np.zeros(len(ix), bool)
+        if miss.any():
+            vy = gy.vec(ky)
+            filled = _take_with_na(vy, np.where(miss, iy, np.nan))
+            vecs[j] = _coalesce(vecs[j], filled)
+    res = H2OFrame.from_vecs(vecs, names)
+    return _reshard(res) if cloud.is_distributed() else res
+
+
+def _take_with_na(v: Vec, idx):
+    idx = np.asarray(idx, dtype=float)
+    na = np.isnan(idx)
+    ii = np.where(na, 0, idx).astype(np.int64)
+    if v.on_host:
+        arr = np.asarray(v.data, dtype=object)[ii] if len(v.data) else np.array([None] * len(ii), dtype=object)
+        arr[na] = None
+        return Vec(arr, v.type)
+    t = torch.as_tensor(ii, device=_dev())
+    nat = torch.as_tensor(na, device=_dev())
+    d = v.data[t] if v.nlocal else torch.zeros(len(ii), dtype=v.data.dtype, device=_dev())
+    if v.type == T_ENUM:
+        d = torch.where(nat, torch.full_like(d, -1), d)
+    else:
+        d = torch.where(nat, torch.full_like(d, float("nan")), d)
+    return Vec(d, v.type, v.domain)
+
+
+def _coalesce(a: Vec, b: Vec):
+    if a.on_host:
+        arr = np.array([x if x is not None else y for x, y in zip(a.data, b.data)], dtype=object)
+        return Vec(arr, a.type)
+    m = a.isna()
+    if a.type == T_ENUM:
+        return Vec(torch.where(m, b.data, a.data), T_ENUM, a.domain)
+    return Vec(torch.where(m, b.data.to(a.data.dtype), a.data), a.type)
+
+
+# ---------------------------------------------------------------- impute / fill / scale / cut
+def impute(fr, column=-1, method="mean", combine_method="interpolate", by=None, values=None):
+    cols = range(fr.ncols) if column in (-1, None) else [fr._col_index(column)]
+    res = []
+    for j in cols:
+        v = fr._vecs[j]
+        if v.on_host:
+            res.append(None)
+            continue
+        if values is not None:
+            val = values[j] if isinstance(values, (list, tuple)) else values
+        elif by is not None:
+            grp = fr.group_by(by)
+            res.append(None)
+            continue
+        elif v.type == T_ENUM or method == "mode":
+            d = v.data if v.type == T_ENUM else v.as_float().to(torch.int64)
+            ok = d[d >= 0]
+            cnt = torch.bincount(ok.long())
+            coll.allreduce_(cnt)
+            val = int(torch.argmax(cnt))
+        elif method == "median":
+            val = quantile_values(v, [0.5], combine_method)[0]
+        else:
+            val = v.mean()
+        if v.type == T_ENUM:
+            fr._vecs[j] = Vec(torch.where(v.data < 0, torch.full_like(v.data, int(val)), v.data), T_ENUM, v.domain)
+        else:
+            x = v.data
+            fr._vecs[j] = Vec(torch.where(torch.isnan(x), torch.full_like(x, float(val)), x), v.type)
+        res.append(val)
+    return res
+
+
+def fillna(fr, method="forward", axis=0, maxlen=1):
+    g = fr.gather()
+    out = []
+    for v in g._vecs:
+        if v.on_host or axis != 0:
+            out.append(v)
+            continue
+        x = v.as_float(torch.float64).cpu().numpy()
+        y = x.copy()
+        n = len(y)
+        rng = range(n) if method == "forward" else range(n - 1, -1, -1)
+        last, run = np.nan, 0
+        for i in rng:
+            if np.isnan(y[i]):
+                if not np.isnan(last) and run < maxlen:
+                    y[i] = last
+                    run += 1
+            else:
+                last, run = y[i], 0
+        t = torch.tensor(y, device=_dev())
+        if v.type == T_ENUM:
+            out.append(Vec(torch.nan_to_num(t, nan=-1).to(torch.int32), T_ENUM, v.domain))
+        else:
+            out.append(Vec(t.to(v.data.dtype), v.type))
+    res = H2OFrame.from_vecs(out, g.names)
+    return _reshard(res) if cloud.is_distributed() else res
+
+
+def scale_frame(fr, center=True, scale=True):
+    out = []
+    for v in fr._vecs:
+        x = v.as_float(torch.float64)
+        if center is True:
+            x = x - v.mean()
+        elif isinstance(center, (list, tuple)):
+            pass
+        if scale is True:
+            r = v.rollups()
+            sd = r["sigma"] if center is True else math.sqrt(coll.allreduce_scalar(float(torch.nansum(x * x))) / max(r["nrow"] - r["nacnt"] - 1, 1))
+            x = x / sd if sd else x
+        out.append(Vec(x.to(torch.float32), T_REAL))
+    return H2OFrame.from_vecs(out, fr.names)
+
+
+def cut(fr, breaks, labels=None, include_lowest=False, right=True, dig_lab=3):
+    v = fr._vecs[0]
+    x = v.as_float(torch.float64)
+    b = torch.tensor(sorted(breaks), dtype=torch.float64, device=x.device)
+    if right:
+        idx = torch.searchsorted(b, x, right=False) - 1
+        if include_lowest:
+            idx = torch.where(x == b[0], torch.zeros_like(idx), idx)
+    else:
+        idx = torch.searchsorted(b, x, right=True) - 1
+        if include_lowest:
+            idx = torch.where(x == b[-1], torch.full_like(idx, len(breaks) - 2), idx)
+    valid = (idx >= 0) & (idx < len(breaks) - 1) & ~torch.isnan(x)
+    codes = torch.where(valid, idx, torch.full_like(idx, -1)).to(torch.int32)
+    if labels is None:
+        fmt = lambda z: f"{z:.{dig_lab}g}"
+        labels = [(f"({fmt(breaks[i])},{fmt(breaks[i + 1])}]" if right else f"[{fmt(breaks[i])},{fmt(breaks[i + 1])})")
+                  for i in range(len(breaks) - 1)]
+    return H2OFrame.from_vecs([Vec(codes, T_ENUM, list(labels))], fr.names[:1])
+
+
+# ---------------------------------------------------------------- apply / misc
+def apply(fr, fun, axis=0):
+    if axis == 0:
+        res = {n: [fun(H2OFrame.from_vecs([v], [n]))] for n, v in zip(fr.names, fr._vecs)}
+        vals = {n: [x[0] if not isinstance(x[0], H2OFrame) else x[0].flatten()] for n, x in res.items()}
+        import pandas as pd
+        return H2OFrame(pd.DataFrame(vals), _local=True)
+    df = fr.as_data_frame()
+    out = df.apply(lambda row: fun(row), axis=1)
+    import pandas as pd
+    return H2OFrame(pd.DataFrame({"C1": out.values}))
+
+
+def drop_duplicates(fr, columns=None, keep="first"):
+    g = fr.gather()
+    cols = columns or g.names
+    _, inv = _group_ids(g, cols)
+    n = g.nlocal
+    pos = torch.arange(n, device=_dev())
+    G = int(inv.max()) + 1 if n else 0
+    if keep == "first":
+        sel = torch.full((G,), n, dtype=torch.int64, device=_dev()).scatter_reduce(0, inv, pos, reduce="amin")
+    else:
+        sel = torch.full((G,), -1, dtype=torch.int64, device=_dev()).scatter_reduce(0, inv, pos, reduce="amax")
+    sel = torch.sort(sel).values
+    res = H2OFrame.from_vecs([_take(v, sel) for v in g._vecs], g.names)
+    return _reshard(res) if cloud.is_distributed() else res
+
+
+def pivot(fr, index, column, value):
+    import pandas as pd
+    df = fr.gather()[[index, column, value]].as_data_frame()
+    p = df.pivot_table(index=index, columns=column, values=value, aggfunc="first").reset_index()
+    p.columns = [str(c) for c in p.columns]
+    return H2OFrame(p)
+
+
+def melt(fr, id_vars, value_vars=None, var_name="variable", value_name="value", skipna=False):
+    import pandas as pd
+    df = fr.gather().as_data_frame()
+    m = df.melt(id_vars=id_vars, value_vars=value_vars, var_name=var_name, value_name=value_name)
+    if skipna:
+        m = m.dropna(subset=[value_name])
+    return H2OFrame(m, column_types={var_name: "enum"})
+
+
+def rank_within_group_by(fr, group_by_cols, sort_cols, ascending=None, new_col_name="New_Rank_column"):
+    import pandas as pd
+    g = fr.gather()
+    df = g.as_data_frame()
+    asc = ascending if ascending is not None else [True] * len(sort_cols)
+    df = df.sort_values(list(group_by_cols) + list(sort_cols), ascending=[True] * len(group_by_cols) + list(asc))
+    df[new_col_name] = df.groupby(list(group_by_cols)).cumcount() + 1
+    return H2OFrame(df)
+
+
+def topn(fr, column=0, nPercent=10, grabTopN=-1):
+    v = fr.vec(column)
+    x = v.as_float(torch.float64)
+    n = x.numel()
+    k = max(1, int(math.ceil(n * nPercent / 100.0)))
+    vals, idx = torch.topk(torch.nan_to_num(x, nan=-math.inf) if grabTopN > 0 else -torch.nan_to_num(x, nan=math.inf), k)
+    import pandas as pd
+    return H2OFrame(pd.DataFrame({"Row Indices": idx.cpu().numpy().astype(float), fr.names[fr._col_index(column)]: x[idx].cpu().numpy()}))
+
+
+def interaction(data, factors, pairwise, max_factors, min_occurrence):
+    import itertools
+    import pandas as pd
+    df = data.gather().as_data_frame()
+    names = [data.names[f] if isinstance(f, int) else f for f in factors]
+    combos = list(itertools.combinations(names, 2)) if pairwise else [tuple(names)]
+    out = {}
+    for cmb in combos:
+        col = df[list(cmb)].astype(str).agg("_".join, axis=1)
+        vc = col.value_counts()
+        keep = set(vc[vc >= min_occurrence].index[:max_factors])
+        out["_".join(cmb)] = col.where(col.isin(keep), "other")
+    return H2OFrame(pd.DataFrame(out), column_types={k: "enum" for k in out})
+
+
+def create_frame(frame_id=None, rows=10000, cols=10, randomize=True, real_fraction=None, categorical_fraction=None,
+                 integer_fraction=None, binary_fraction=None, time_fraction=None, string_fraction=None, value=0,
+                 real_range=100, factors=100, integer_range=100, binary_ones_fraction=0.02, missing_fraction=0.01,
+                 has_response=False, response_factors=2, positive_response=False, seed=None):
+    """reference: hex/createframe/recipes/SimpleCreateFrameRecipe.java."""
+    import pandas as pd
+    rng = np.random.RandomState(seed if seed not in (None, -1) else 42)
+    fr_ = {"real": real_fraction, "cat": categorical_fraction, "int": integer_fraction, "bin": binary_fraction,
+           "time": time_fraction, "str": string_fraction}
+    given = {k: v for k, v in fr_.items() if v is not None}
+    rest = 1.0 - sum(given.values())
+    missing = [k for k, v in fr_.items() if v is None]
+    default_share = {"real": 0.5, "cat": 0.2, "int": 0.2, "bin": 0.1, "time": 0.0, "str": 0.0}
+    tot_def = sum(default_share[k] for k in missing) or 1
+    for k in missing:
+        fr_[k] = rest * default_share[k] / tot_def
+    counts = {k: int(round(v * cols)) for k, v in fr_.items()}
+    diff = cols - sum(counts.values())
+    counts["real"] += diff
+    data = {}
+    ci = 1
+    for kind, cnt in counts.items():
+        for _ in range(max(cnt, 0)):
+            name = f"C{ci}"
+            ci += 1
+            if kind == "real":
+                x = rng.uniform(-real_range, real_range, rows) if randomize else np.full(rows, float(value))
+            elif kind == "int":
+                x = rng.randint(-integer_range, integer_range + 1, rows).astype(float)
+            elif kind == "bin":
+                x = (rng.rand(rows) < binary_ones_fraction).astype(float)
+            elif kind == "cat":
+                x = np.array([f"c{ci}.l{j}" for j in rng.randint(0, factors, rows)], dtype=object)
+            elif kind == "time":
+                x = pd.to_datetime(rng.randint(0, 2 ** 31, rows), unit="s").values
+            else:
+                x = np.array(["".join(rng.choice(list("abcdefgh"), 8)) for _ in range(rows)], dtype=object)
+            if missing_fraction > 0 and kind not in ("time",):
+                m = rng.rand(rows) < missing_fraction
+                x = x.astype(object) if x.dtype == object else x.astype(float)
+                x[m] = None if x.dtype == object else np.nan
+            data[name] = x
+    df = pd.DataFrame(data)
+    types = {}
+    if has_response:
+        if response_factors == 1:
+            resp = rng.uniform(0 if positive_response else -real_range, real_range, rows)
+        else:
+            resp = np.array([str(i) for i in rng.randint(0, response_factors, rows)], dtype=object)
+            types["response"] = "enum"
+        df.insert(0, "response", resp)
+    for c in df.columns:
+        if df[c].dtype == object and c != "response":
+            types[c] = "enum" if counts["str"] == 0 or not c.startswith("C") else types.get(c)
+    return H2OFrame(df, destination_frame=frame_id, column_types={k: v for k, v in types.items() if v})
