@@ -1,3 +1,6 @@
 """Estimator classes (h2o.estimators.*)."""
 from ..models.tree.gbm import H2OGradientBoostingEstimator  # noqa: F401
 from ..models.glm.glm import H2OGeneralizedLinearEstimator  # noqa: F401
+from ..models.tree.drf import H2ORandomForestEstimator, H2OExtremelyRandomizedTreesEstimator  # noqa: F401
+from ..models.tree.xgboost import H2OXGBoostEstimator  # noqa: F401
+from ..models.tree.isofor import H2OIsolationForestEstimator, H2OExtendedIsolationForestEstimator  # noqa: F401

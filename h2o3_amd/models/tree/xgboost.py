@@ -1,0 +1,243 @@
+"""XGBoost-style second-order gradient boosting.
+
+Reference: h2o-extensions/xgboost (hex/tree/xgboost/XGBoost.java,
+BoosterParms.java) which wraps native XGBoost (tree_method hist/approx,
+grow_policy depthwise/lossguide, booster gbtree/dart/gblinear).  Here the
+booster is native to this framework: the same GPU tree engine with
+(g, h) histogram channels, gain = 1/2 [G_L^2/(H_L+l) + G_R^2/(H_R+l) -
+G^2/(H+l)] - gamma (with L1 soft-thresholding by alpha), leaf weight
+-G/(H+lambda) * eta, max_delta_step clipping, row/column subsampling and
+DART dropout.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from ...parallel import cloud
+from ...parallel import collectives as coll
+from ...ops import tree_ops
+from ..distributions import get_distribution
+from .engine import GrowParams, TreeGrower
+from .shared import Forest, SharedTreeEstimator
+
+XGB_DEFAULTS = dict(ntrees=50, max_depth=6, min_rows=1.0, min_child_weight=1.0, learn_rate=0.3, eta=0.3,
+                    sample_rate=1.0, subsample=1.0, col_sample_rate=1.0, colsample_bylevel=1.0,
+                    col_sample_rate_per_tree=1.0, colsample_bytree=1.0, colsample_bynode=1.0,
+                    max_abs_leafnode_pred=0.0, max_delta_step=0.0, monotone_constraints=None,
+                    interaction_constraints=None, score_tree_interval=0, min_split_improvement=0.0, gamma=0.0,
+                    nthread=-1, save_matrix_directory=None, build_tree_one_node=False, calibrate_model=False,
+                    calibration_frame=None, calibration_method="auto", max_bins=256, max_leaves=0,
+                    tree_method="auto", grow_policy="depthwise", booster="gbtree", reg_lambda=1.0, reg_alpha=0.0,
+                    dmatrix_type="auto", backend="auto", gpu_id=None, gainslift_bins=-1, sample_type="uniform",
+                    normalize_type="tree", rate_drop=0.0, one_drop=False, skip_drop=0.0, scale_pos_weight=1.0,
+                    distribution="auto", tweedie_power=1.5, categorical_encoding="auto", quiet_mode=True,
+                    checkpoint=None, stopping_rounds=0, stopping_metric="auto", stopping_tolerance=0.001,
+                    seed=-1, eval_metric=None, score_eval_metric_only=False)
+
+
+class H2OXGBoostEstimator(SharedTreeEstimator):
+    algo = "xgboost"
+    _defaults = XGB_DEFAULTS
+
+    def __init__(self, **kw):
+        # XGBoost-native aliases (reference BoosterParms maps both spellings)
+        alias = {"eta": "learn_rate", "subsample": "sample_rate", "colsample_bylevel": "col_sample_rate",
+                 "colsample_bytree": "col_sample_rate_per_tree", "min_child_weight": "min_rows",
+                 "gamma": "min_split_improvement", "max_bin": "max_bins"}
+        for a, b in alias.items():
+            if a in kw and b not in kw:
+                kw[b] = kw[a]
+        super().__init__(**kw)
+
+    @staticmethod
+    def available():
+        return True
+
+    def _n_tree_classes(self):
+        return self._K
+
+    def _fit(self, spec):
+        p = self._parms
+        dev = cloud.device()
+        bd = self._bin(spec, hist_type="QuantilesGlobal", nbins=max(2, int(p.get("max_bins", 256)) - 1))
+        N = bd.nrows_local
+        nc = spec.nclasses
+        dist_name = (p.get("distribution") or "auto").lower()
+        if dist_name == "auto":
+            dist_name = "bernoulli" if nc == 2 else ("multinomial" if nc > 2 else "gaussian")
+        self._dist = get_distribution(dist_name, nc, tweedie_power=p.get("tweedie_power", 1.5))
+        K = nc if nc > 2 else 1
+        self._K = K
+        y = spec.y_tensor()
+        w = spec.w_tensor()
+        base_w = torch.ones(N, dtype=torch.float32, device=dev) if w is None else w.to(torch.float32)
+        if spec.is_classification:
+            yc = y.to(torch.int64)
+            valid = yc >= 0
+            yv = (yc == 1).to(torch.float32) if K == 1 else None
+            Y = torch.nn.functional.one_hot(yc.clamp(min=0), K).to(torch.float32) if K > 1 else None
+            if K == 1 and float(p.get("scale_pos_weight", 1.0)) != 1.0:
+                base_w = torch.where(yc == 1, base_w * float(p["scale_pos_weight"]), base_w)
+        else:
+            yv = torch.nan_to_num(y.to(torch.float32))
+            valid = ~torch.isnan(y.to(torch.float32))
+        base_w = torch.where(valid, base_w, torch.zeros_like(base_w))
+        # base score: 0.5 probability / mean (XGBoost default base_score=0.5)
+        if K == 1:
+            if self._dist.link == "logit":
+                f0 = 0.0
+            elif self._dist.link == "log":
+                mu = coll.allreduce_scalar(float((base_w * yv).sum())) / max(coll.allreduce_scalar(float(base_w.sum())), 1e-12)
+                f0 = math.log(max(mu, 1e-10))
+            else:
+                f0 = coll.allreduce_scalar(float((base_w * yv).sum())) / max(coll.allreduce_scalar(float(base_w.sum())), 1e-12)
+            self._init_f = [f0]
+        else:
+            self._init_f = [0.0] * K
+        f = torch.tensor(self._init_f, dtype=torch.float32, device=dev).view(1, -1).repeat(N, 1)
+        gp = GrowParams(criterion="xgb", max_depth=int(p["max_depth"]) if int(p["max_depth"]) > 0 else 64,
+                        min_rows=float(p["min_rows"]), reg_lambda=float(p["reg_lambda"]),
+                        reg_alpha=float(p["reg_alpha"]), gamma=float(p["min_split_improvement"]),
+                        col_sample_rate=float(p["col_sample_rate"]) * float(p.get("colsample_bynode", 1.0)),
+                        max_leaves=int(p.get("max_leaves") or 0), seed=self._seed())
+        mc = p.get("monotone_constraints")
+        if mc:
+            gp.monotone = np.array([float(mc.get(n, 0)) for n in spec.x])
+        grower = TreeGrower(bd, gp)
+        forest = Forest()
+        eta = float(p["learn_rate"])
+        mds = float(p.get("max_delta_step") or 0.0)
+        mabs = float(p.get("max_abs_leafnode_pred") or 0.0)
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(self._seed() + cloud.rank())
+        rng = np.random.RandomState(self._seed())
+        booster = (p.get("booster") or "gbtree").lower()
+        dart = booster == "dart"
+        tree_w = []  # dart weights
+        ntrees = int(p["ntrees"])
+        sr = float(p["sample_rate"])
+        F = bd.F
+        for it in range(ntrees):
+            wt = base_w
+            if sr < 1.0:
+                wt = base_w * (torch.rand(N, generator=gen, device=dev) < sr)
+            r = float(p.get("col_sample_rate_per_tree", 1.0))
+            if r < 1.0:
+                kk = max(1, int(math.floor(r * F + 0.5)))
+                m = np.zeros(F, dtype=bool)
+                m[rng.choice(F, size=kk, replace=False)] = True
+                gp.tree_col_mask = m
+            dropped = []
+            f_use = f
+            if dart and len(forest) and rng.rand() >= float(p.get("skip_drop", 0.0)):
+                nit = len(forest) // K
+                rd = float(p.get("rate_drop", 0.0))
+                dropped = [i for i in range(nit) if rng.rand() < rd]
+                if not dropped and p.get("one_drop"):
+                    dropped = [int(rng.randint(nit))]
+                if dropped:
+                    f_use = f - self._contrib(forest, tree_w, dropped, K, bd, N)
+            if K == 1:
+                g, h = self._dist.grad_hess(yv, f_use[:, 0])
+                g, h = (g * wt).to(torch.float32).contiguous(), (h * wt).to(torch.float32).contiguous()
+                tree, nid, leaves, tot = grower.grow(g, h, 1)
+                vals = self._leaf_values(tot, eta, mds, mabs, gp)
+                for li, node in enumerate(leaves):
+                    tree.value[node] = float(vals[li])
+                delta = torch.tensor(vals, dtype=torch.float32, device=dev)[nid.long()].view(-1, 1)
+                trees_it = [tree]
+                deltas = [delta]
+            else:
+                P = torch.softmax(f_use, 1)
+                trees_it, deltas = [], []
+                for k in range(K):
+                    g = ((P[:, k] - Y[:, k]) * wt).contiguous()
+                    h = (torch.clamp(2 * P[:, k] * (1 - P[:, k]), min=1e-16) * wt).contiguous()
+                    tree, nid, leaves, tot = grower.grow(g, h, 1)
+                    vals = self._leaf_values(tot, eta, mds, mabs, gp)
+                    for li, node in enumerate(leaves):
+                        tree.value[node] = float(vals[li])
+                    trees_it.append(tree)
+                    deltas.append(torch.tensor(vals, dtype=torch.float32, device=dev)[nid.long()])
+            if dart and dropped:
+                kd = len(dropped)
+                nt = 1.0 / (kd + 1) if (p.get("normalize_type") or "tree") == "tree" else 1.0 / (1 + eta)
+                for tt in trees_it:
+                    for i in range(tt.n_nodes):
+                        tt.value[i] *= nt
+                scale = kd / (kd + 1.0) if (p.get("normalize_type") or "tree") == "tree" else 1.0 / (1 + eta)
+                contrib = self._contrib(forest, tree_w, dropped, K, bd, N)
+                for d in dropped:
+                    tree_w[d] *= scale
+                f = f - contrib * (1 - scale)
+                deltas = [d * nt for d in deltas]
+            for k, tt in enumerate(trees_it):
+                forest.add(tt, k)
+            tree_w.append(1.0)
+            if K == 1:
+                f = f + deltas[0]
+            else:
+                f = f + torch.stack(deltas, 1)
+        if dart:
+            # bake DART weights into leaf values
+            for it, wgt in enumerate(tree_w):
+                for k in range(K):
+                    tt = forest.trees[it * K + k]
+                    for i in range(tt.n_nodes):
+                        tt.value[i] *= wgt
+        self._forest = forest
+        self._train_f = f
+        vi = {n: 0.0 for n in spec.x}
+        for t in forest.trees:
+            for i in range(t.n_nodes):
+                if t.left[i] >= 0:
+                    vi[spec.x[t.feat[i]]] += max(t.gain[i], 0.0)
+        self._output["variable_importances"] = vi
+        self._output["model_summary"] = {"number_of_trees": len(forest) // K, "booster": booster}
+
+    def _contrib(self, forest, tree_w, dropped, K, bd, N):
+        X = self._score_matrix(self._spec.frame)
+        out = torch.zeros((N, K), dtype=torch.float32, device=X.device)
+        sub = Forest()
+        for d in dropped:
+            for k in range(K):
+                sub.add(forest.trees[d * K + k], k)
+        s = sub.predict(X, K)
+        # weights of dropped trees
+        return s * torch.tensor([tree_w[d] for d in dropped], device=X.device).mean() if dropped else out
+
+    @staticmethod
+    def _leaf_values(tot, eta, mds, mabs, gp):
+        tot = tot.numpy() if isinstance(tot, torch.Tensor) else np.asarray(tot)
+        G, H = tot[:, 0], tot[:, 1]
+        if gp.reg_alpha > 0:
+            G = np.sign(G) * np.maximum(np.abs(G) - gp.reg_alpha, 0)
+        v = -G / (H + gp.reg_lambda)
+        if mds > 0:
+            v = np.clip(v, -mds, mds)
+        v = v * eta
+        if mabs > 0:
+            v = np.clip(v, -mabs, mabs)
+        return v
+
+    def _seed(self):
+        s = self._parms.get("seed", -1)
+        return 777 if s is None or s == -1 else int(s) & 0x7FFFFFFF
+
+    def _predict_raw(self, frame):
+        X = self._score_matrix(frame)
+        K = self._K
+        f = self._forest.predict(X, K) + torch.tensor(self._init_f, dtype=torch.float32, device=X.device).view(1, -1)
+        if K > 1:
+            return torch.softmax(f, 1)
+        mu = self._dist.linkinv(f[:, 0])
+        if self._spec.nclasses == 2:
+            return torch.stack([1 - mu, mu], 1)
+        return mu.view(-1, 1)
+
+    def predict_contributions(self, test_data, **kw):
+        from .shap import tree_contributions
+        return tree_contributions(self, test_data)

@@ -1,0 +1,64 @@
+import numpy as np
+import pandas as pd
+
+import h2o3_amd
+from h2o3_amd.estimators import (H2OExtendedIsolationForestEstimator, H2OIsolationForestEstimator,
+                                 H2ORandomForestEstimator, H2OXGBoostEstimator)
+
+
+def _bin(n=3000, seed=0):
+    rng = np.random.RandomState(seed)
+    X = rng.randn(n, 6)
+    logit = 2 * X[:, 0] - X[:, 1] + X[:, 2] * X[:, 3]
+    y = (rng.rand(n) < 1 / (1 + np.exp(-logit))).astype(int)
+    df = pd.DataFrame(X, columns=[f"x{i}" for i in range(6)])
+    df["y"] = np.where(y == 1, "pos", "neg")
+    return h2o3_amd.H2OFrame(df)
+
+
+def test_drf_binomial_oob():
+    fr = _bin()
+    m = H2ORandomForestEstimator(ntrees=20, max_depth=10, seed=1)
+    m.train(y="y", training_frame=fr)
+    assert m.auc() > 0.8   # OOB AUC
+    p = m.predict(fr).as_data_frame()
+    assert np.allclose(p["neg"] + p["pos"], 1.0, atol=1e-5)
+
+
+def test_drf_regression_and_multinomial():
+    rng = np.random.RandomState(3)
+    X = rng.randn(2000, 3)
+    df = pd.DataFrame(X, columns=list("abc"))
+    df["y"] = X[:, 0] ** 2 + X[:, 1]
+    m = H2ORandomForestEstimator(ntrees=15, max_depth=12, seed=2)
+    m.train(y="y", training_frame=h2o3_amd.H2OFrame(df))
+    assert m.r2() > 0.7
+    df["cls"] = np.array(["u", "v", "w"])[np.argmax(X, 1)]
+    m2 = H2ORandomForestEstimator(ntrees=10, seed=2)
+    m2.train(x=["a", "b", "c"], y="cls", training_frame=h2o3_amd.H2OFrame(df.drop(columns=["y"])))
+    assert m2.mean_per_class_error() < 0.2
+
+
+def test_xgboost_binomial_and_dart():
+    fr = _bin(seed=4)
+    m = H2OXGBoostEstimator(ntrees=30, max_depth=4, seed=1)
+    m.train(y="y", training_frame=fr)
+    assert m.auc() > 0.85
+    m2 = H2OXGBoostEstimator(ntrees=10, max_depth=3, booster="dart", rate_drop=0.3, seed=1)
+    m2.train(y="y", training_frame=fr)
+    assert m2.auc() > 0.8
+
+
+def test_isolation_forests():
+    rng = np.random.RandomState(5)
+    X = rng.randn(2000, 3)
+    X[:20] += 8
+    fr = h2o3_amd.H2OFrame(pd.DataFrame(X, columns=list("abc")))
+    m = H2OIsolationForestEstimator(ntrees=40, seed=1)
+    m.train(training_frame=fr)
+    s = m.predict(fr).as_data_frame()["predict"].values
+    assert s[:20].mean() > s[20:].mean() + 0.2
+    e = H2OExtendedIsolationForestEstimator(ntrees=40, extension_level=2, seed=1)
+    e.train(training_frame=fr)
+    a = e.predict(fr).as_data_frame()["anomaly_score"].values
+    assert a[:20].mean() > a[20:].mean()
