@@ -4,3 +4,7 @@ from ..models.glm.glm import H2OGeneralizedLinearEstimator  # noqa: F401
 from ..models.tree.drf import H2ORandomForestEstimator, H2OExtremelyRandomizedTreesEstimator  # noqa: F401
 from ..models.tree.xgboost import H2OXGBoostEstimator  # noqa: F401
 from ..models.tree.isofor import H2OIsolationForestEstimator, H2OExtendedIsolationForestEstimator  # noqa: F401
+from ..models.clustering import (H2OKMeansEstimator, H2ONaiveBayesEstimator,  # noqa: F401
+                                 H2OPrincipalComponentAnalysisEstimator, H2OSingularValueDecompositionEstimator)
+from ..models.deeplearning import H2ODeepLearningEstimator  # noqa: F401
+H2OAutoEncoderEstimator = H2ODeepLearningEstimator

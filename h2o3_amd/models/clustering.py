@@ -1,0 +1,428 @@
+"""K-Means, PCA, SVD, Naive Bayes.
+
+References: hex/kmeans/KMeans.java (Lloyd iterations as MRTasks, init
+Random / PlusPlus / Furthest / User, standardize, estimate_k by the
+reduction in within-SS), hex/pca/PCA.java (GramSVD / Power / Randomized /
+GLRM methods, importance table), hex/svd/SVD.java, hex/naivebayes/
+NaiveBayes.java (Laplace smoothing, gaussian numeric likelihoods,
+min_sdev/eps_sdev, min_prob/eps_prob).
+
+MI355X design: the expanded design matrix is one HBM tensor; KMeans
+distances are a GEMM (||x||^2 - 2 X C^T + ||c||^2) and centroid sums are a
+second GEMM (onehot(assign)^T X) on the matrix cores — no per-row atomics;
+PCA/SVD take the weighted Gram from the f32-MFMA Gram kernel and finish
+with a tiny f64 eigendecomposition; every reduction is one all_reduce.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from ..core.frame import H2OFrame
+from ..core.vec import T_ENUM, T_INT, T_REAL, Vec
+from ..ops import linalg_ops
+from ..parallel import cloud
+from ..parallel import collectives as coll
+from . import metrics as mm
+from .base import H2OEstimator
+from .datainfo import DataInfo
+
+
+def _seed(p, default=1234):
+    s = p.get("seed", -1)
+    return default if s is None or s == -1 else int(s) & 0x7FFFFFFF
+
+
+# ====================================================================== KMeans
+KMEANS_DEFAULTS = dict(k=1, estimate_k=False, user_points=None, max_iterations=10, standardize=True, seed=-1,
+                       init="Furthest", categorical_encoding="auto", max_runtime_secs=0.0,
+                       cluster_size_constraints=None, score_each_iteration=False)
+
+
+class H2OKMeansEstimator(H2OEstimator):
+    algo = "kmeans"
+    supervised_learning = False
+    _defaults = KMEANS_DEFAULTS
+
+    def _fit(self, spec):
+        p = self._parms
+        di = DataInfo(spec.frame, spec.x, standardize=bool(p.get("standardize", True)), use_all_factor_levels=True,
+                      pad_to=0)
+        self._dinfo = di
+        X, ok = di.expand(spec.frame, dtype=torch.float32, pad=False)
+        X = X[ok]
+        w = spec.w_tensor()
+        w = None if w is None else w[ok]
+        gen = np.random.RandomState(_seed(p))
+        kmax = int(p.get("k", 1))
+        if p.get("estimate_k"):
+            best = None
+            prev = None
+            for k in range(1, kmax + 1):
+                C, assign, wss, it = self._lloyd(X, w, k, gen)
+                if prev is not None and (prev - wss) / max(prev, 1e-12) < 0.2 and k > 1:
+                    break
+                best = (C, assign, wss, it, k)
+                prev = wss
+            C, assign, wss, it, k = best
+        else:
+            C, assign, wss, it = self._lloyd(X, w, kmax, gen)
+        self._C_std = C
+        self._iterations = it
+        self._assign_train = assign
+        centers = C.cpu().numpy().astype(np.float64).copy()
+        if di.standardize:
+            base = di.n_cat_expanded
+            for j in range(len(di.num_cols)):
+                centers[:, base + j] = centers[:, base + j] * di.sigmas[j] + di.means[j]
+        self._output["centers"] = centers
+        self._output["centers_std"] = C.cpu().numpy()
+        self._output["coef_names"] = di.coef_names
+        self._output["model_summary"] = {"number_of_clusters": C.shape[0], "number_of_iterations": it}
+        self._train_X = X
+
+    def _dist(self, X, C):
+        return (X * X).sum(1, keepdim=True) - 2 * X @ C.T + (C * C).sum(1).view(1, -1)
+
+    def _init_centers(self, X, w, k, gen):
+        p = self._parms
+        init = (p.get("init") or "Furthest").lower()
+        n = X.shape[0]
+        up = p.get("user_points")
+        if up is not None:
+            U, _ = self._dinfo.expand(up, pad=False)
+            return U[:k].to(X.dtype)
+        Xg = coll.all_gather_var(X) if cloud.is_distributed() else X
+        ng = Xg.shape[0]
+        first = int(gen.randint(ng))
+        if init == "random":
+            idx = gen.choice(ng, size=min(k, ng), replace=False)
+            return Xg[torch.as_tensor(idx, device=X.device)].clone()
+        C = [Xg[first]]
+        d2 = ((Xg - C[0]) ** 2).sum(1)
+        for _ in range(1, k):
+            if init == "plusplus":
+                pr = (d2 / d2.sum()).double().cpu().numpy()
+                pr = pr / pr.sum()
+                i = int(gen.choice(ng, p=pr))
+            else:  # Furthest
+                i = int(torch.argmax(d2))
+            C.append(Xg[i])
+            d2 = torch.minimum(d2, ((Xg - Xg[i]) ** 2).sum(1))
+        return torch.stack(C)
+
+    def _lloyd(self, X, w, k, gen):
+        p = self._parms
+        C = self._init_centers(X, w, k, gen).to(X.dtype)
+        k = C.shape[0]
+        maxit = int(p.get("max_iterations", 10))
+        it = 0
+        ww = torch.ones(X.shape[0], dtype=X.dtype, device=X.device) if w is None else w.to(X.dtype)
+        assign = None
+        for it in range(1, maxit + 1):
+            D = self._dist(X, C)
+            assign = torch.argmin(D, 1)
+            A = torch.zeros((X.shape[0], k), dtype=X.dtype, device=X.device)
+            A.scatter_(1, assign.view(-1, 1), ww.view(-1, 1))
+            S = A.T @ X                     # centroid sums on the matrix cores
+            cnt = A.sum(0)
+            st = torch.cat([S.reshape(-1), cnt])
+            coll.allreduce_(st)
+            S, cnt = st[: k * X.shape[1]].view(k, -1), st[k * X.shape[1]:]
+            newC = torch.where(cnt.view(-1, 1) > 0, S / cnt.clamp_min(1e-30).view(-1, 1), C)
+            shift = float((newC - C).abs().max())
+            C = newC
+            if shift < 1e-6:
+                break
+        D = self._dist(X, C)
+        assign = torch.argmin(D, 1)
+        wss = coll.allreduce_scalar(float((D.gather(1, assign.view(-1, 1)).clamp_min(0).view(-1) * ww).sum()))
+        return C, assign, wss, it
+
+    def _predict_raw(self, frame):
+        X, _ = self._dinfo.expand(frame, pad=False)
+        D = self._dist(X.to(self._C_std.dtype), self._C_std)
+        return torch.argmin(D, 1).view(-1, 1).to(torch.float32)
+
+    def predict(self, test_data, **kw):
+        a = self._predict_raw(test_data)[:, 0]
+        return H2OFrame.from_vecs([Vec(a.contiguous(), T_INT)], ["predict"])
+
+    def _score_unsupervised(self, spec):
+        X = self._train_X
+        m = mm.clustering_metrics(X, self._C_std, self._assign_train)
+        self._training_metrics = m
+        if spec.valid is not None:
+            self._validation_metrics = self._unsupervised_perf(spec.valid)
+
+    def _unsupervised_perf(self, frame):
+        X, ok = self._dinfo.expand(frame, pad=False)
+        X = X[ok]
+        a = torch.argmin(self._dist(X, self._C_std), 1)
+        return mm.clustering_metrics(X, self._C_std, a)
+
+    def centers(self):
+        return self._output["centers"].tolist()
+
+    def centers_std(self):
+        return self._output["centers_std"].tolist()
+
+    def size(self, train=False, valid=False):
+        return self._training_metrics.get("size")
+
+    def tot_withinss(self, train=False, valid=False, xval=False):
+        return self._training_metrics.tot_withinss()
+
+    def betweenss(self, train=False, valid=False, xval=False):
+        return self._training_metrics.betweenss()
+
+    def totss(self, train=False, valid=False, xval=False):
+        return self._training_metrics.totss()
+
+    def withinss(self, train=False, valid=False, xval=False):
+        return self._training_metrics.withinss()
+
+    def num_iterations(self):
+        return self._iterations
+
+
+# ====================================================================== PCA / SVD
+def _transform_info(frame, x, transform, use_all):
+    t = (transform or "NONE").upper()
+    di = DataInfo(frame, x, standardize=t in ("STANDARDIZE", "DESCALE", "DEMEAN", "NORMALIZE"),
+                  use_all_factor_levels=use_all, pad_to=32)
+    if t in ("DEMEAN",):
+        di.sigmas = [1.0] * len(di.sigmas)
+    if t == "DESCALE":
+        di.means = [0.0] * len(di.means)
+    if t == "NORMALIZE":
+        out = []
+        for c in di.num_cols:
+            v = frame.vec(c)
+            r = v.rollups()
+            out.append(max(r["max"] - r["min"], 1e-12))
+        di.sigmas = out
+    return di
+
+
+PCA_DEFAULTS = dict(transform="none", k=1, max_iterations=1000, seed=-1, use_all_factor_levels=False,
+                    compute_metrics=True, impute_missing=False, pca_method="GramSVD", pca_impl="mtj_evd_symmmatrix",
+                    max_runtime_secs=0.0, export_checkpoints_dir=None)
+
+
+class H2OPrincipalComponentAnalysisEstimator(H2OEstimator):
+    algo = "pca"
+    supervised_learning = False
+    _defaults = PCA_DEFAULTS
+
+    def _fit(self, spec):
+        p = self._parms
+        di = _transform_info(spec.frame, spec.x, p.get("transform"), bool(p.get("use_all_factor_levels")))
+        self._dinfo = di
+        X, ok = di.expand(spec.frame)
+        X = X[ok]
+        n = coll.allreduce_scalar(float(X.shape[0]))
+        k = int(p.get("k", 1))
+        method = (p.get("pca_method") or "GramSVD").lower()
+        P = di.P
+        if method in ("gramsvd", "glrm"):
+            G = linalg_ops.weighted_gram(X)[:P, :P]
+            coll.allreduce_(G)
+            mean = X[:, :P].to(torch.float64).sum(0)
+            coll.allreduce_(mean)
+            mean = mean / n
+            if not di.standardize:
+                # covariance about the mean (reference demeans via the Gram's intercept row)
+                G = G - n * torch.outer(mean, mean)
+            cov = G / max(n - 1, 1)
+            evals, evecs = torch.linalg.eigh(cov.cpu())
+            order = torch.argsort(evals, descending=True)
+            evals, evecs = evals[order], evecs[:, order]
+        else:  # Power / Randomized: subspace iteration on X (GEMMs on device)
+            gen = torch.Generator(device="cpu").manual_seed(_seed(p))
+            Q = torch.randn((P, k + 5), generator=gen, dtype=torch.float64).to(X.device)
+            Xd = X[:, :P].to(torch.float64)
+            mean = Xd.sum(0)
+            coll.allreduce_(mean)
+            mean = mean / n
+            Xc = Xd - mean if not di.standardize else Xd
+            for _ in range(min(int(p.get("max_iterations", 1000)), 30)):
+                Z = Xc.T @ (Xc @ Q)
+                coll.allreduce_(Z)
+                Q, _ = torch.linalg.qr(Z)
+            B = Xc @ Q
+            S = B.T @ B
+            coll.allreduce_(S)
+            ev, U = torch.linalg.eigh(S.cpu())
+            order = torch.argsort(ev, descending=True)
+            evals = ev[order] / max(n - 1, 1)
+            evecs = (Q.cpu() @ U[:, order])
+        k = min(k, evecs.shape[1])
+        sd = torch.sqrt(evals.clamp_min(0))
+        tot = float(evals.clamp_min(0).sum())
+        self._evecs = evecs[:, :k].to(torch.float64)
+        self._mean = mean.cpu() if not di.standardize else torch.zeros(P, dtype=torch.float64)
+        var = evals[:k].clamp_min(0)
+        self._output["eigenvectors"] = self._evecs.numpy()
+        self._output["std_deviation"] = sd[:k].numpy()
+        self._output["importance"] = {"Standard deviation": sd[:k].tolist(),
+                                      "Proportion of Variance": (var / tot).tolist() if tot > 0 else [0.0] * k,
+                                      "Cumulative Proportion": (torch.cumsum(var, 0) / tot).tolist() if tot > 0 else [0.0] * k}
+        self._output["coef_names"] = di.coef_names
+        self._output["model_summary"] = self._output["importance"]
+        self._k = k
+
+    def _predict_raw(self, frame):
+        X, _ = self._dinfo.expand(frame)
+        Xd = X[:, : self._dinfo.P].to(torch.float64) - self._mean.to(X.device)
+        return Xd @ self._evecs.to(X.device)
+
+    def predict(self, test_data, **kw):
+        Z = self._predict_raw(test_data)
+        return H2OFrame.from_vecs([Vec(Z[:, j].contiguous(), T_REAL) for j in range(Z.shape[1])],
+                                  [f"PC{j + 1}" for j in range(Z.shape[1])])
+
+    transform = predict
+
+    def _score_unsupervised(self, spec):
+        self._training_metrics = mm.ModelMetricsDimReduction(nobs=spec.frame.nrows)
+
+    def varimp(self, use_pandas=False):
+        return self._output["importance"]
+
+    @property
+    def rotation(self):
+        return self._output["eigenvectors"]
+
+
+SVD_DEFAULTS = dict(transform="none", svd_method="GramSVD", nv=1, max_iterations=1000, seed=-1, keep_u=True,
+                    u_name=None, v_name=None, use_all_factor_levels=True, max_runtime_secs=0.0,
+                    export_checkpoints_dir=None)
+
+
+class H2OSingularValueDecompositionEstimator(H2OEstimator):
+    algo = "svd"
+    supervised_learning = False
+    _defaults = SVD_DEFAULTS
+
+    def _fit(self, spec):
+        p = self._parms
+        di = _transform_info(spec.frame, spec.x, p.get("transform"), bool(p.get("use_all_factor_levels", True)))
+        self._dinfo = di
+        X, ok = di.expand(spec.frame)
+        nv = int(p.get("nv", 1))
+        P = di.P
+        G = linalg_ops.weighted_gram(X)[:P, :P]
+        coll.allreduce_(G)
+        ev, V = torch.linalg.eigh(G.cpu())
+        order = torch.argsort(ev, descending=True)
+        ev, V = ev[order][:nv], V[:, order][:, :nv]
+        d = torch.sqrt(ev.clamp_min(0))
+        self._V = V
+        self._d = d
+        self._output["d"] = d.tolist()
+        self._output["v"] = V.numpy()
+        if p.get("keep_u", True):
+            U = (X[:, :P].to(torch.float64) @ V.to(X.device)) / d.to(X.device).clamp_min(1e-300)
+            self._u = H2OFrame.from_vecs([Vec(U[:, j].contiguous(), T_REAL) for j in range(U.shape[1])],
+                                         [f"u{j + 1}" for j in range(U.shape[1])])
+
+    def d(self):
+        return self._output["d"]
+
+    def v(self):
+        return self._output["v"]
+
+    def u(self):
+        return getattr(self, "_u", None)
+
+    def _predict_raw(self, frame):
+        X, _ = self._dinfo.expand(frame)
+        return X[:, : self._dinfo.P].to(torch.float64) @ self._V.to(X.device)
+
+    def predict(self, test_data, **kw):
+        Z = self._predict_raw(test_data)
+        return H2OFrame.from_vecs([Vec(Z[:, j].contiguous(), T_REAL) for j in range(Z.shape[1])],
+                                  [f"v{j + 1}" for j in range(Z.shape[1])])
+
+    def _score_unsupervised(self, spec):
+        self._training_metrics = mm.ModelMetricsDimReduction(nobs=spec.frame.nrows)
+
+
+# ====================================================================== Naive Bayes
+NB_DEFAULTS = dict(laplace=0.0, min_sdev=0.001, eps_sdev=0.0, min_prob=0.001, eps_prob=0.0,
+                   compute_metrics=True, seed=-1, max_confusion_matrix_size=20, balance_classes=False,
+                   class_sampling_factors=None, max_after_balance_size=5.0)
+
+
+class H2ONaiveBayesEstimator(H2OEstimator):
+    algo = "naivebayes"
+    _defaults = NB_DEFAULTS
+
+    def _fit(self, spec):
+        if not spec.is_classification:
+            raise ValueError("Naive Bayes requires a categorical response")
+        p = self._parms
+        K = spec.nclasses
+        y = spec.y_tensor().long()
+        ok = y >= 0
+        lap = float(p.get("laplace", 0.0))
+        cnt = torch.bincount(y[ok], minlength=K).to(torch.float64)
+        coll.allreduce_(cnt)
+        self._prior = (cnt + lap) / (cnt.sum() + K * lap) if lap > 0 else cnt / cnt.sum()
+        self._tables = {}
+        for c in spec.x:
+            v = spec.frame.vec(c)
+            if v.type == T_ENUM:
+                L = len(v.domain)
+                m = ok & (v.data >= 0)
+                t = torch.zeros((K, L), dtype=torch.float64, device=y.device)
+                t.index_put_((y[m], v.data[m].long()), torch.ones(int(m.sum()), dtype=torch.float64, device=y.device),
+                             accumulate=True)
+                coll.allreduce_(t)
+                prob = (t + lap) / (t.sum(1, keepdim=True) + L * lap)
+                self._tables[c] = ("cat", prob, list(v.domain))
+            else:
+                x = v.as_float(torch.float64)
+                m = ok & ~torch.isnan(x)
+                s1 = torch.zeros(K, dtype=torch.float64, device=y.device).index_add_(0, y[m], x[m])
+                s2 = torch.zeros(K, dtype=torch.float64, device=y.device).index_add_(0, y[m], x[m] ** 2)
+                n = torch.zeros(K, dtype=torch.float64, device=y.device).index_add_(0, y[m], torch.ones_like(x[m]))
+                st = torch.stack([s1, s2, n])
+                coll.allreduce_(st)
+                s1, s2, n = st
+                mean = s1 / n.clamp_min(1)
+                var = (s2 - n * mean ** 2) / (n - 1).clamp_min(1)
+                sd = torch.sqrt(var.clamp_min(0))
+                self._tables[c] = ("num", mean, sd)
+        self._output["apriori"] = self._prior.cpu().tolist()
+        self._output["pcond"] = {c: (t[1].cpu().numpy().tolist(), t[2] if t[0] == "cat" else t[2].cpu().tolist())
+                                 for c, t in self._tables.items()}
+
+    def _predict_raw(self, frame):
+        p = self._parms
+        n = frame.nlocal
+        logp = torch.log(self._prior.clamp_min(1e-300)).view(1, -1).repeat(n, 1).to(cloud.device())
+        min_sdev, eps_sdev = float(p["min_sdev"]), float(p["eps_sdev"])
+        min_prob, eps_prob = float(p["min_prob"]), float(p["eps_prob"])
+        for c, t in self._tables.items():
+            if c not in frame.names:
+                continue
+            v = frame.vec(c)
+            if t[0] == "cat":
+                codes = self._adapt_enum(v, t[2]).long()
+                pr = t[1].T[codes.clamp(min=0)]               # [n, K]
+                pr = torch.where(pr <= eps_prob, torch.full_like(pr, min_prob), pr)
+                contrib = torch.log(pr.clamp_min(1e-300))
+                contrib = torch.where((codes < 0).view(-1, 1), torch.zeros_like(contrib), contrib)
+            else:
+                x = v.as_float(torch.float64)
+                mean, sd = t[1], t[2]
+                sd = torch.where(sd <= eps_sdev, torch.full_like(sd, min_sdev), sd)
+                z = (x.view(-1, 1) - mean.view(1, -1)) / sd.view(1, -1)
+                contrib = -0.5 * z * z - torch.log(sd.view(1, -1) * math.sqrt(2 * math.pi))
+                contrib = torch.where(torch.isnan(x).view(-1, 1), torch.zeros_like(contrib), contrib)
+            logp = logp + contrib
+        return torch.softmax(logp, 1)
