@@ -1,0 +1,70 @@
+"""Leaderboard (reference: hex/leaderboard/Leaderboard.java).
+
+Rows sorted by the problem's default metric (AUC for binomial,
+mean_per_class_error for multinomial, mean_residual_deviance for
+regression), computed on the leaderboard frame when given, else on the
+cross-validation metrics, else validation, else training.
+"""
+from __future__ import annotations
+
+import math
+import time
+
+_DEFAULT = {2: "auc", 1: "mean_residual_deviance"}
+_COLS = {"binomial": ["auc", "logloss", "aucpr", "mean_per_class_error", "rmse", "mse"],
+         "multinomial": ["mean_per_class_error", "logloss", "rmse", "mse"],
+         "regression": ["rmse", "mse", "mae", "rmsle", "mean_residual_deviance"]}
+_KEY = {"auc": "AUC", "logloss": "logloss", "aucpr": "pr_auc", "mean_per_class_error": "mean_per_class_error",
+        "rmse": "RMSE", "mse": "MSE", "mae": "mae", "rmsle": "rmsle", "mean_residual_deviance": "mean_residual_deviance",
+        "deviance": "mean_residual_deviance"}
+
+
+class Leaderboard:
+    def __init__(self, models, sort_metric="AUTO", frame=None):
+        self.frame = frame
+        models = [m for m in models if m is not None]
+        self.kind = "regression"
+        if models and models[0]._spec is not None and models[0]._spec.nclasses == 2:
+            self.kind = "binomial"
+        elif models and models[0]._spec is not None and models[0]._spec.nclasses > 2:
+            self.kind = "multinomial"
+        sm = (sort_metric or "AUTO").lower()
+        if sm == "auto":
+            sm = {"binomial": "auc", "multinomial": "mean_per_class_error", "regression": "mean_residual_deviance"}[self.kind]
+        self.sort_metric = sm
+        self._cache = {}
+        dec = sm in ("auc", "aucpr")
+        self.models = sorted(models, key=lambda m: self._score(m, sm), reverse=dec)
+
+    def _metrics(self, m):
+        if m.model_id in self._cache:
+            return self._cache[m.model_id]
+        if self.frame is not None:
+            mt = m.model_performance(self.frame)
+        else:
+            mt = m._cross_validation_metrics or m._validation_metrics or m._training_metrics
+        self._cache[m.model_id] = mt
+        return mt
+
+    def _score(self, m, metric):
+        mt = self._metrics(m)
+        v = None if mt is None else mt.get(_KEY.get(metric, metric))
+        if v is None or (isinstance(v, float) and math.isnan(v)):
+            return -math.inf if metric in ("auc", "aucpr") else math.inf
+        return v
+
+    def as_frame(self, extra_columns=None):
+        import pandas as pd
+        from ..core.frame import H2OFrame
+        rows = []
+        for m in self.models:
+            r = {"model_id": m.model_id}
+            for c in _COLS[self.kind]:
+                v = self._score(m, c)
+                r[c] = v if math.isfinite(v) else float("nan")
+            if extra_columns in ("ALL", "training_time_ms") or (isinstance(extra_columns, list) and "training_time_ms" in extra_columns):
+                r["training_time_ms"] = int(m._run_time * 1000)
+            if extra_columns == "ALL" or (isinstance(extra_columns, list) and "algo" in extra_columns):
+                r["algo"] = m.algo
+            rows.append(r)
+        return H2OFrame(pd.DataFrame(rows), _local=True, column_types={"model_id": "string"})

@@ -8,3 +8,4 @@ from ..models.clustering import (H2OKMeansEstimator, H2ONaiveBayesEstimator,  # 
                                  H2OPrincipalComponentAnalysisEstimator, H2OSingularValueDecompositionEstimator)
 from ..models.deeplearning import H2ODeepLearningEstimator  # noqa: F401
 H2OAutoEncoderEstimator = H2ODeepLearningEstimator
+from ..models.ensemble import H2OStackedEnsembleEstimator  # noqa: F401

@@ -1,0 +1,178 @@
+"""Hyper-parameter grid search.
+
+Reference: hex/grid/GridSearch.java, HyperSpaceWalker.java
+(CartesianWalker / RandomDiscreteValueWalker with max_models,
+max_runtime_secs, early stopping on the grid's sort metric),
+hex/grid/Grid.java, h2o-py/h2o/grid/grid_search.py (client API:
+train / get_grid / sorted_metric_table / models / model_ids).
+"""
+from __future__ import annotations
+
+import itertools
+import math
+import random
+import time
+
+import numpy as np
+
+from ..core import dkv
+
+
+class H2OGridSearch:
+    def __init__(self, model, hyper_params, grid_id=None, search_criteria=None, export_checkpoints_dir=None,
+                 recovery_dir=None, parallelism=1):
+        self.model = model
+        self.hyper_params = dict(hyper_params)
+        self.grid_id = grid_id or dkv.make_key("Grid")
+        self.search_criteria = dict(search_criteria or {"strategy": "Cartesian"})
+        self.models = []
+        self.failed_params = []
+        self._sort_metric = None
+        self.export_checkpoints_dir = export_checkpoints_dir
+
+    def _estimator_factory(self):
+        m = self.model
+        if isinstance(m, type):
+            return lambda **kw: m(**kw)
+        base = dict(m._parms)
+        cls = type(m)
+        return lambda **kw: cls(**{**base, **kw})
+
+    def _combos(self):
+        keys = list(self.hyper_params)
+        vals = [v if isinstance(v, (list, tuple)) else [v] for v in (self.hyper_params[k] for k in keys)]
+        combos = [dict(zip(keys, c)) for c in itertools.product(*vals)]
+        sc = self.search_criteria
+        if (sc.get("strategy") or "Cartesian").lower() == "randomdiscrete":
+            rng = random.Random(sc.get("seed", 1234) if sc.get("seed", -1) != -1 else 1234)
+            rng.shuffle(combos)
+        return combos
+
+    def train(self, x=None, y=None, training_frame=None, offset_column=None, fold_column=None, weights_column=None,
+              validation_frame=None, **params):
+        sc = self.search_criteria
+        max_models = int(sc.get("max_models") or 0)
+        max_rt = float(sc.get("max_runtime_secs") or 0)
+        stop_rounds = int(sc.get("stopping_rounds") or 0)
+        t0 = time.time()
+        make = self._estimator_factory()
+        history = []
+        for combo in self._combos():
+            if max_models and len(self.models) >= max_models:
+                break
+            if max_rt and time.time() - t0 > max_rt:
+                break
+            kw = dict(params)
+            kw.update(combo)
+            kw["model_id"] = f"{self.grid_id}_model_{len(self.models) + 1}"
+            try:
+                est = make(**kw)
+                est.train(x=x, y=y, training_frame=training_frame, offset_column=offset_column,
+                          fold_column=fold_column, weights_column=weights_column, validation_frame=validation_frame)
+                est._grid_params = combo
+                self.models.append(est)
+                if stop_rounds:
+                    history.append(self._metric_of(est))
+                    if self._stop(history, sc):
+                        break
+            except Exception as e:  # reference keeps failures in the grid's failure list
+                self.failed_params.append((combo, repr(e)))
+        dkv.put(self.grid_id, self)
+        return self
+
+    def _default_metric(self):
+        if not self.models:
+            return "mse"
+        m = self.models[0]
+        if m._spec is None or not m.supervised_learning:
+            return "tot_withinss"
+        if m._spec.nclasses == 2:
+            return "auc"
+        if m._spec.nclasses > 2:
+            return "logloss"
+        return "residual_deviance"
+
+    def _metric_of(self, est, metric=None):
+        metric = (metric or self.search_criteria.get("stopping_metric") or self._default_metric()).lower()
+        mt = est._cross_validation_metrics or est._validation_metrics or est._training_metrics
+        if mt is None:
+            return float("nan")
+        key = {"auc": "AUC", "logloss": "logloss", "rmse": "RMSE", "mse": "MSE", "mae": "mae", "r2": "r2",
+               "residual_deviance": "mean_residual_deviance", "deviance": "mean_residual_deviance",
+               "mean_per_class_error": "mean_per_class_error", "aucpr": "pr_auc", "tot_withinss": "tot_withinss",
+               "rmsle": "rmsle"}.get(metric, metric)
+        v = mt.get(key)
+        return float("nan") if v is None else float(v)
+
+    @staticmethod
+    def _stop(history, sc):
+        from ..models.base import ScoreKeeper
+        k = int(sc.get("stopping_rounds") or 0)
+        metric = (sc.get("stopping_metric") or "auto").lower()
+        less = metric not in ("auc", "aucpr", "r2")
+        best = []
+        for v in history:
+            if not best:
+                best.append(v)
+            else:
+                best.append(min(best[-1], v) if less else max(best[-1], v))
+        return ScoreKeeper.stop_early(best, k, float(sc.get("stopping_tolerance", 0.001)), less)
+
+    def get_grid(self, sort_by=None, decreasing=None):
+        metric = (sort_by or self._default_metric()).lower()
+        if decreasing is None:
+            decreasing = metric in ("auc", "aucpr", "r2", "accuracy")
+        g = H2OGridSearch(self.model, self.hyper_params, self.grid_id, self.search_criteria)
+        g.models = sorted(self.models, key=lambda m: self._metric_of(m, metric), reverse=decreasing)
+        g._sort_metric = metric
+        g.failed_params = self.failed_params
+        return g
+
+    def sorted_metric_table(self):
+        import pandas as pd
+        metric = self._sort_metric or self._default_metric()
+        rows = []
+        for m in self.models:
+            r = dict(m._grid_params)
+            r["model_ids"] = m.model_id
+            r[metric] = self._metric_of(m, metric)
+            rows.append(r)
+        return pd.DataFrame(rows)
+
+    summary = sorted_metric_table
+
+    @property
+    def model_ids(self):
+        return [m.model_id for m in self.models]
+
+    def get_hyperparams(self, id, display=True):
+        m = self.models[id] if isinstance(id, int) else next(mm for mm in self.models if mm.model_id == id)
+        return [m._grid_params[k] for k in self.hyper_params]
+
+    def get_hyperparams_dict(self, id, display=True):
+        m = self.models[id] if isinstance(id, int) else next(mm for mm in self.models if mm.model_id == id)
+        return dict(m._grid_params)
+
+    def __getitem__(self, i):
+        return self.models[i]
+
+    def __len__(self):
+        return len(self.models)
+
+    def __iter__(self):
+        return iter(self.models)
+
+    def show(self):
+        print(self.sorted_metric_table())
+
+    # metric passthroughs (return dict model_id -> value like h2o-py)
+    def _all(self, name, **kw):
+        return {m.model_id: getattr(m, name)(**kw) for m in self.models}
+
+    def auc(self, train=False, valid=False, xval=False): return self._all("auc", train=train, valid=valid, xval=xval)
+    def logloss(self, train=False, valid=False, xval=False): return self._all("logloss", train=train, valid=valid, xval=xval)
+    def rmse(self, train=False, valid=False, xval=False): return self._all("rmse", train=train, valid=valid, xval=xval)
+    def mse(self, train=False, valid=False, xval=False): return self._all("mse", train=train, valid=valid, xval=xval)
+
+    def predict(self, test_data):
+        return {m.model_id: m.predict(test_data) for m in self.models}

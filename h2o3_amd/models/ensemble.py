@@ -1,0 +1,124 @@
+"""Stacked Ensemble.
+
+Reference: hex/ensemble/StackedEnsemble.java (level-one frame from the base
+models' cross-validation holdout predictions — or predictions on a
+`blending_frame` — then a metalearner), hex/ensemble/Metalearners.java
+(AUTO = GLM with non-negative coefficients and lambda search; glm / gbm /
+drf / deeplearning / naivebayes / xgboost), StackedEnsembleModel.java
+(scoring: base-model predictions -> metalearner).
+"""
+from __future__ import annotations
+
+import torch
+
+from ..core.frame import H2OFrame
+from ..core.vec import T_ENUM, T_REAL, Vec
+from .base import H2OEstimator
+
+SE_DEFAULTS = dict(base_models=[], metalearner_algorithm="auto", metalearner_nfolds=0,
+                   metalearner_fold_assignment=None, metalearner_fold_column=None, metalearner_params=None,
+                   metalearner_transform="NONE", max_runtime_secs=0.0, blending_frame=None, seed=-1,
+                   score_training_samples=10000, keep_levelone_frame=False, export_checkpoints_dir=None,
+                   auc_type="auto", gainslift_bins=-1)
+
+
+def _resolve_models(base):
+    from ..core import dkv
+    out = []
+    for b in base:
+        if isinstance(b, str):
+            o = dkv.get(b)
+        else:
+            o = b
+        if hasattr(o, "models") and not isinstance(o, H2OEstimator):   # a grid / automl leaderboard
+            out.extend(o.models)
+        elif o is not None:
+            out.append(o)
+    return out
+
+
+class H2OStackedEnsembleEstimator(H2OEstimator):
+    algo = "stackedensemble"
+    _defaults = SE_DEFAULTS
+
+    def train(self, x=None, y=None, training_frame=None, validation_frame=None, blending_frame=None, **kw):
+        if blending_frame is not None:
+            self._parms["blending_frame"] = blending_frame
+        base = _resolve_models(self._parms.get("base_models") or [])
+        self._base = base
+        if x is None and base:
+            x = base[0]._spec.x
+        return super().train(x=x, y=y, training_frame=training_frame, validation_frame=validation_frame, **kw)
+
+    def _level_one(self, models, frame, use_cv):
+        cols, names = [], []
+        for m in models:
+            if use_cv:
+                raw = getattr(m, "_cv_holdout", None)
+                if raw is None:
+                    raise ValueError(f"base model {m.model_id} has no cross-validation holdout predictions: train it "
+                                     "with nfolds>1 and keep_cross_validation_predictions=True (or use a blending_frame)")
+            else:
+                raw = m._predict_raw(frame)
+            if self._spec.nclasses == 2:
+                cols.append(raw[:, -1])
+                names.append(m.model_id)
+            elif self._spec.nclasses > 2:
+                for k in range(raw.shape[1]):
+                    cols.append(raw[:, k])
+                    names.append(f"{m.model_id}/{self._spec.response_domain[k]}")
+            else:
+                cols.append(raw[:, 0])
+                names.append(m.model_id)
+        vecs = [Vec(c.to(torch.float32).contiguous(), T_REAL) for c in cols]
+        return vecs, names
+
+    def _fit(self, spec):
+        from ..estimators import (H2OGeneralizedLinearEstimator, H2OGradientBoostingEstimator,
+                                  H2ORandomForestEstimator, H2ODeepLearningEstimator, H2ONaiveBayesEstimator,
+                                  H2OXGBoostEstimator)
+        p = self._parms
+        base = self._base
+        if not base:
+            raise ValueError("StackedEnsemble needs base_models")
+        blend = p.get("blending_frame")
+        frame = blend if blend is not None else spec.frame
+        vecs, names = self._level_one(base, frame, use_cv=blend is None)
+        y = frame.vec(spec.y)
+        lvl1 = H2OFrame.from_vecs(vecs + [y], names + [spec.y])
+        self._names = names
+        algo = (p.get("metalearner_algorithm") or "auto").lower()
+        mp = dict(p.get("metalearner_params") or {})
+        nf = int(p.get("metalearner_nfolds") or 0)
+        if nf:
+            mp.setdefault("nfolds", nf)
+        if p.get("seed", -1) not in (None, -1):
+            mp.setdefault("seed", p["seed"])
+        if algo in ("auto", "glm"):
+            if algo == "auto":
+                mp.setdefault("non_negative", True)
+                mp.setdefault("lambda_search", True)
+            fam = "binomial" if spec.nclasses == 2 else ("multinomial" if spec.nclasses > 2 else "gaussian")
+            mp.setdefault("family", fam)
+            meta = H2OGeneralizedLinearEstimator(**mp)
+        else:
+            cls = {"gbm": H2OGradientBoostingEstimator, "drf": H2ORandomForestEstimator,
+                   "deeplearning": H2ODeepLearningEstimator, "naivebayes": H2ONaiveBayesEstimator,
+                   "xgboost": H2OXGBoostEstimator}[algo]
+            meta = cls(**mp)
+        meta.train(x=names, y=spec.y, training_frame=lvl1)
+        self._meta = meta
+        if p.get("keep_levelone_frame"):
+            self._output["levelone_frame"] = lvl1
+        self._output["model_summary"] = {"base_models": [m.model_id for m in base], "metalearner": meta.algo}
+
+    def metalearner(self):
+        return self._meta
+
+    def _predict_raw(self, frame):
+        vecs, names = self._level_one(self._base, frame, use_cv=False)
+        lvl1 = H2OFrame.from_vecs(vecs, names)
+        return self._meta._predict_raw(lvl1)
+
+    def levelone_frame_id(self):
+        return self._output.get("levelone_frame")
