@@ -9,3 +9,4 @@ from ..models.clustering import (H2OKMeansEstimator, H2ONaiveBayesEstimator,  # 
 from ..models.deeplearning import H2ODeepLearningEstimator  # noqa: F401
 H2OAutoEncoderEstimator = H2ODeepLearningEstimator
 from ..models.ensemble import H2OStackedEnsembleEstimator  # noqa: F401
+from ..models.generic import H2OGenericEstimator  # noqa: F401

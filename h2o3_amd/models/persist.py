@@ -1,0 +1,74 @@
+"""Binary model save / load (h2o.save_model / h2o.load_model).
+
+Reference: hex/Model.exportBinaryModel / importBinaryModel (Java
+serialization of the whole model).  Here a saved model is a directory-free
+zip: the MOJO (all scoring state) + params.json + metrics.json — no pickle,
+so loading never executes code from the file.  A loaded model scores
+through the MOJO scorer and keeps its training / validation / CV metrics.
+"""
+from __future__ import annotations
+
+import io
+import json
+import os
+import zipfile
+
+import numpy as np
+
+
+def _metrics_dict(m):
+    if m is None:
+        return None
+    out = {"kind": m.kind}
+    for k, v in m._m.items():
+        if isinstance(v, (int, float, str, bool)) or v is None:
+            out[k] = v
+        elif k == "cm":
+            out[k] = {kk: (vv if not isinstance(vv, np.ndarray) else vv.tolist()) for kk, vv in v.items()}
+    return out
+
+
+def save_model(model, path="", force=False, filename=None):
+    from ..mojo.writer import build_mojo
+    os.makedirs(path or ".", exist_ok=True)
+    fn = os.path.join(path or ".", filename or model.model_id)
+    if os.path.exists(fn) and not force:
+        raise FileExistsError(fn)
+    params = {k: v for k, v in model._parms.items() if isinstance(v, (int, float, str, bool, list, type(None)))}
+    with zipfile.ZipFile(fn, "w", zipfile.ZIP_DEFLATED) as z:
+        z.writestr("mojo.zip", build_mojo(model))
+        z.writestr("params.json", json.dumps({"algo": model.algo, "model_id": model.model_id, "params": params}))
+        z.writestr("metrics.json", json.dumps({"training": _metrics_dict(model._training_metrics),
+                                               "validation": _metrics_dict(model._validation_metrics),
+                                               "xval": _metrics_dict(model._cross_validation_metrics),
+                                               "output": {k: v for k, v in model._output.items()
+                                                          if isinstance(v, (dict, list, float, int, str))}},
+                                              default=str))
+    return fn
+
+
+def load_model(path):
+    from . import metrics as mm
+    from .generic import H2OGenericEstimator
+    from ..core import dkv
+    with zipfile.ZipFile(path) as z:
+        mojo = z.read("mojo.zip")
+        meta = json.loads(z.read("params.json"))
+        mets = json.loads(z.read("metrics.json"))
+    tmp = path + ".mojo.zip"
+    with open(tmp, "wb") as f:
+        f.write(mojo)
+    est = H2OGenericEstimator.from_file(tmp, model_id=meta["model_id"])
+    est.algo = meta["algo"]
+    est._parms.update(meta["params"])
+    kinds = {"binomial": mm.ModelMetricsBinomial, "multinomial": mm.ModelMetricsMultinomial,
+             "regression": mm.ModelMetricsRegression, "clustering": mm.ModelMetricsClustering}
+    for attr, key in (("_training_metrics", "training"), ("_validation_metrics", "validation"),
+                      ("_cross_validation_metrics", "xval")):
+        d = mets.get(key)
+        if d:
+            cls = kinds.get(d.pop("kind", ""), mm.ModelMetrics)
+            setattr(est, attr, cls(**d))
+    est._output.update(mets.get("output") or {})
+    dkv.put(est.model_id, est)
+    return est

@@ -1,0 +1,286 @@
+"""Standalone MOJO scorer (numpy only — no torch, no GPU, no cluster).
+
+Reference: h2o-genmodel (hex/genmodel/MojoModel.java, ModelMojoReader.java,
+algos/*/ *MojoModel.score0, easy/EasyPredictModelWrapper.java).  Load a
+MOJO zip written by h2o3_amd.mojo.writer and score pandas DataFrames or
+row dicts: categorical values are mapped through the stored domains
+(unseen levels -> NA, like the reference's adaptation), numeric NA = NaN.
+"""
+from __future__ import annotations
+
+import io
+import json
+import math
+import zipfile
+
+import numpy as np
+
+
+def _sigmoid(x):
+    return 1.0 / (1.0 + np.exp(-x))
+
+
+def _softmax(z):
+    z = z - z.max(1, keepdims=True)
+    e = np.exp(z)
+    return e / e.sum(1, keepdims=True)
+
+
+class MojoModel:
+    def __init__(self, zbytes):
+        self._z = zipfile.ZipFile(io.BytesIO(zbytes))
+        self.meta = json.loads(self._z.read("model.json"))
+        self.info = {}
+        sec = None
+        for line in self._z.read("model.ini").decode().splitlines():
+            line = line.strip()
+            if line.startswith("["):
+                sec = line
+            elif sec == "[info]" and "=" in line:
+                k, v = line.split("=", 1)
+                self.info[k.strip()] = v.strip()
+        self.algo = self.meta["algo"]
+        self._arr = {}
+        for n in self._z.namelist():
+            if n.startswith("arrays/") and n.endswith(".npy"):
+                self._arr[n[7:-4]] = np.load(io.BytesIO(self._z.read(n)), allow_pickle=False)
+        self.nclasses = int(self.meta.get("nclasses", 1))
+        self.response_domain = self.meta.get("response_domain")
+        if self.algo == "stackedensemble":
+            self._base = [MojoModel(self._z.read(f"models/{i}.zip")) for i in range(len(self.meta["base"]))]
+            self._meta_model = MojoModel(self._z.read("models/meta.zip"))
+
+    @staticmethod
+    def load(path):
+        with open(path, "rb") as f:
+            return MojoModel(f.read())
+
+    # ---------------------------------------------------------------- inputs
+    def _col(self, df, c, dom=None):
+        if c not in df:
+            return np.full(len(df), np.nan)
+        s = df[c]
+        if dom is not None:
+            idx = {d: i for i, d in enumerate(dom)}
+            out = np.full(len(s), np.nan)
+            for i, v in enumerate(s.values if hasattr(s, "values") else s):
+                if v is None or (isinstance(v, float) and math.isnan(v)):
+                    continue
+                key = v if isinstance(v, str) else (str(int(v)) if float(v).is_integer() else str(v))
+                j = idx.get(key, idx.get(str(v)))
+                if j is not None:
+                    out[i] = j
+            return out
+        return np.asarray(s, dtype=np.float64)
+
+    def _tree_matrix(self, df):
+        xd = self.meta.get("x_domains", {})
+        return np.stack([self._col(df, c, xd.get(c)) for c in self.meta["x"]], 1) if self.meta["x"] else \
+            np.zeros((len(df), 0))
+
+    def _expand(self, df):
+        di = self.meta["di"]
+        n = len(df)
+        X = np.zeros((n, di["P"]))
+        for c in di["cat_cols"]:
+            codes = self._col(df, c, di["domains"][c])
+            codes = np.where(np.isnan(codes), di["cat_modes"][c], codes).astype(int)
+            if not di["use_all"]:
+                codes = codes - 1
+            ok = codes >= 0
+            X[np.nonzero(ok)[0], di["cat_offsets"][c] + codes[ok]] = 1.0
+        base = sum(len(d) if di["use_all"] else len(d) - 1 for d in (di["domains"][c] for c in di["cat_cols"]))
+        for j, c in enumerate(di["num_cols"]):
+            x = self._col(df, c)
+            x = np.where(np.isnan(x), di["plug"][j], x)
+            if di["standardize"]:
+                x = (x - di["means"][j]) / di["sigmas"][j]
+            X[:, base + j] = x
+        return X
+
+    # ---------------------------------------------------------------- scoring
+    def _forest(self, X, K, leaf=False):
+        A = self._arr
+        feat, thr, left, right = A["forest_feat"], A["forest_thr"], A["forest_left"], A["forest_right"]
+        nal, coff, clen, bits, val = A["forest_na_left"], A["forest_cat_off"], A["forest_cat_len"], \
+            A["forest_cat_bits"], A["forest_value"]
+        roots, tcls = A["forest_roots"], A["forest_tclass"]
+        n = X.shape[0]
+        out = np.zeros((n, K))
+        ar = np.arange(n)
+        for t in range(len(roots)):
+            nd = np.full(n, roots[t])
+            while True:
+                l = left[nd]
+                act = l >= 0
+                if not act.any():
+                    break
+                x = X[ar, feat[nd]]
+                isn = np.isnan(x)
+                co = coff[nd]
+                code = np.where(isn, -1, np.nan_to_num(x, nan=-1)).astype(np.int64)
+                inr = (code >= 0) & (code < clen[nd])
+                bit = bits[np.clip(co + np.maximum(code, 0), 0, len(bits) - 1)] != 0
+                gocat = np.where(isn | ~inr, nal[nd] != 0, bit)
+                # split values are f32 and compared in f32 (reference: float split points)
+                gonum = np.where(isn, nal[nd] != 0, x.astype(np.float32) < thr[nd].astype(np.float32))
+                go = np.where(co >= 0, gocat, gonum)
+                nd = np.where(act, np.where(go, l, right[nd]), nd)
+            out[ar, tcls[t]] += val[nd]
+        return out
+
+    def predict_raw(self, df):
+        m = self.meta
+        a = self.algo
+        if a in ("gbm", "xgboost"):
+            X = self._tree_matrix(df)
+            K = m["K"]
+            f = self._forest(X, K) + np.asarray(m["init_f"]).reshape(1, -1)
+            if K > 1:
+                return _softmax(f)
+            link = m["link"]
+            mu = _sigmoid(f[:, 0]) if link == "logit" else (np.exp(f[:, 0]) if link == "log" else f[:, 0])
+            return np.stack([1 - mu, mu], 1) if self.nclasses == 2 else mu.reshape(-1, 1)
+        if a == "drf":
+            X = self._tree_matrix(df)
+            K = m["K"]
+            s = self._forest(X, K) / max(1, m["ntrees"] // K)
+            if self.nclasses == 2 and m["binomial_single"]:
+                p1 = np.clip(s[:, 0], 0, 1)
+                return np.stack([1 - p1, p1], 1)
+            if self.nclasses > 1:
+                s = np.clip(s, 0, None)
+                return s / np.maximum(s.sum(1, keepdims=True), 1e-30)
+            return s[:, :1]
+        if a == "isolationforest":
+            X = self._tree_matrix(df)
+            ml = self._forest(X, 1)[:, 0] / m["ntrees"]
+            rng = m["max_len"] - m["min_len"]
+            sc = (m["max_len"] - ml) / rng if rng > 0 else np.zeros_like(ml)
+            return np.stack([sc, ml], 1)
+        if a == "glm":
+            X = self._expand(df)
+            if m.get("multi") == "multinomial":
+                return _softmax(X @ self._arr["B"] + self._arr["b0"].reshape(1, -1))
+            if m.get("multi") == "ordinal":
+                eta = X @ self._arr["beta"]
+                th = self._arr["theta"]
+                thc = np.cumsum(np.concatenate([th[:1], np.log1p(np.exp(th[1:]))]))
+                cdf = _sigmoid(thc.reshape(1, -1) - eta.reshape(-1, 1))
+                cdf = np.concatenate([np.zeros((len(eta), 1)), cdf, np.ones((len(eta), 1))], 1)
+                return np.clip(np.diff(cdf, axis=1), 0, None)
+            b = self._arr["beta_std"]
+            eta = X @ b[:-1] + b[-1]
+            link = m["link"]
+            if link == "logit":
+                mu = _sigmoid(eta)
+            elif link == "log":
+                mu = np.exp(eta)
+            elif link == "inverse":
+                mu = 1.0 / eta
+            else:
+                mu = eta
+            return np.stack([1 - mu, mu], 1) if self.nclasses == 2 else mu.reshape(-1, 1)
+        if a == "kmeans":
+            X = self._expand(df)
+            C = self._arr["centers_std"]
+            d = ((X[:, None, :] - C[None]) ** 2).sum(2)
+            return d.argmin(1).reshape(-1, 1).astype(float)
+        if a == "pca":
+            X = self._expand(df)
+            return (X - self._arr["mean"]) @ self._arr["evecs"]
+        if a == "deeplearning":
+            h = self._expand(df)
+            for L in m["layers"]:
+                kind, i = L[0], L[1]
+                if kind == "linear":
+                    h = h @ self._arr[f"W{i}"].T + self._arr[f"b{i}"]
+                elif kind == "maxout":
+                    z = h @ self._arr[f"W{i}"].T + self._arr[f"b{i}"]
+                    h = z.reshape(len(h), -1, L[2]).max(2)
+                elif kind == "tanh":
+                    h = np.tanh(h)
+                elif kind == "relu":
+                    h = np.maximum(h, 0)
+                elif kind == "elu":
+                    h = np.where(h > 0, h, np.expm1(h))
+            if m["autoencoder"]:
+                return h
+            if m["K"] > 1:
+                return _softmax(h)
+            return h * m["ysd"] + m["ymu"]
+        if a == "naivebayes":
+            n = len(df)
+            logp = np.log(np.maximum(self._arr["prior"], 1e-300))[None].repeat(n, 0)
+            nbp = m["nb_params"]
+            for c, spec in m["nb"].items():
+                if spec[0] == "cat":
+                    codes = self._col(df, c, spec[2])
+                    pr = self._arr[f"nb_{spec[1]}"].T[np.nan_to_num(codes, nan=0).astype(int)]
+                    pr = np.where(pr <= nbp["eps_prob"], nbp["min_prob"], pr)
+                    contrib = np.where(np.isnan(codes)[:, None], 0.0, np.log(np.maximum(pr, 1e-300)))
+                else:
+                    x = self._col(df, c)
+                    mean, sd = self._arr[f"nb_{spec[1]}_mean"], self._arr[f"nb_{spec[1]}_sd"]
+                    sd = np.where(sd <= nbp["eps_sdev"], nbp["min_sdev"], sd)
+                    z = (x[:, None] - mean[None]) / sd[None]
+                    contrib = np.where(np.isnan(x)[:, None], 0.0, -0.5 * z * z - np.log(sd[None] * math.sqrt(2 * math.pi)))
+                logp = logp + contrib
+            return _softmax(logp)
+        if a == "stackedensemble":
+            import pandas as pd
+            cols = {}
+            names = m["level1_names"]
+            j = 0
+            for b in self._base:
+                raw = b.predict_raw(df)
+                if self.nclasses == 2:
+                    cols[names[j]] = raw[:, -1]
+                    j += 1
+                elif self.nclasses > 2:
+                    for k in range(raw.shape[1]):
+                        cols[names[j]] = raw[:, k]
+                        j += 1
+                else:
+                    cols[names[j]] = raw[:, 0]
+                    j += 1
+            return self._meta_model.predict_raw(pd.DataFrame(cols))
+        raise NotImplementedError(a)
+
+    def predict(self, df):
+        """Returns a pandas DataFrame shaped like the in-cluster predict()."""
+        import pandas as pd
+        raw = self.predict_raw(df)
+        if self.algo == "isolationforest":
+            return pd.DataFrame({"predict": raw[:, 0], "mean_length": raw[:, 1]})
+        if self.nclasses > 1 and self.response_domain:
+            dom = self.response_domain
+            if self.nclasses == 2:
+                lab = np.where(raw[:, 1] >= 0.5, dom[1], dom[0])
+            else:
+                lab = np.array(dom, dtype=object)[raw.argmax(1)]
+            out = {"predict": lab}
+            for k, d in enumerate(dom):
+                out[d] = raw[:, k]
+            return pd.DataFrame(out)
+        if raw.shape[1] == 1:
+            return pd.DataFrame({"predict": raw[:, 0]})
+        return pd.DataFrame(raw, columns=[f"C{i + 1}" for i in range(raw.shape[1])])
+
+    def predict_row(self, row: dict):
+        import pandas as pd
+        return self.predict(pd.DataFrame([row])).iloc[0].to_dict()
+
+
+class EasyPredictModelWrapper:
+    """h2o-genmodel's convenience wrapper (predictBinomial / predictRegression...)."""
+
+    def __init__(self, model: MojoModel):
+        self.m = model
+
+    def predict(self, row: dict):
+        return self.m.predict_row(row)
+
+
+def load(path):
+    return MojoModel.load(path)

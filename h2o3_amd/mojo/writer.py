@@ -1,0 +1,215 @@
+"""MOJO export (Model ObJect, Optimized) — standalone scoring artifacts.
+
+Reference: h2o-genmodel (hex/genmodel/AbstractMojoWriter.java writes a zip
+with `model.ini` ([info]/[columns]/[domains]) plus algorithm blobs; every
+algo has a *MojoWriter: SharedTreeMojoWriter, GLMMojoWriter,
+KMeansMojoWriter, DeepLearningMojoWriter, PCAMojoWriter,
+StackedEnsembleMojoWriter, ...).
+
+Format here: zip containing
+  model.ini    — [info] algorithm / category / n_features / n_classes /
+                 mojo_version, [columns] feature + response names,
+                 [domains] categorical domains (one file per domain under
+                 domains/, like the reference)
+  model.json   — algorithm parameters (small)
+  arrays/*.npy — numeric blobs (numpy .npy, never pickled)
+  models/<i>/  — nested MOJOs (stacked ensembles)
+The matching reader (h2o3_amd.mojo.genmodel) needs only numpy.
+"""
+from __future__ import annotations
+
+import io
+import json
+import os
+import zipfile
+
+import numpy as np
+import torch
+
+MOJO_VERSION = "1.00"
+
+
+def _npy(arr):
+    b = io.BytesIO()
+    np.save(b, np.asarray(arr), allow_pickle=False)
+    return b.getvalue()
+
+
+class _Writer:
+    def __init__(self):
+        self.files = {}
+        self.meta = {}
+        self.arrays = {}
+
+    def add_array(self, name, arr):
+        self.arrays[name] = np.asarray(arr)
+
+    def to_zip_bytes(self, info, columns, domains):
+        b = io.BytesIO()
+        with zipfile.ZipFile(b, "w", zipfile.ZIP_DEFLATED) as z:
+            ini = ["[info]"] + [f"{k} = {v}" for k, v in info.items()] + ["", "[columns]"] + list(columns) + \
+                  ["", "[domains]"]
+            for i, (col, dom) in enumerate(domains):
+                ini.append(f"{col}: {len(dom)} d{i:03d}.txt")
+                z.writestr(f"domains/d{i:03d}.txt", "\n".join(dom))
+            z.writestr("model.ini", "\n".join(ini) + "\n")
+            z.writestr("model.json", json.dumps(self.meta, default=_json_default))
+            for k, v in self.arrays.items():
+                z.writestr(f"arrays/{k}.npy", _npy(v))
+            for k, v in self.files.items():
+                z.writestr(k, v)
+        return b.getvalue()
+
+
+def _json_default(o):
+    if isinstance(o, (np.integer,)):
+        return int(o)
+    if isinstance(o, (np.floating,)):
+        return float(o)
+    if isinstance(o, np.ndarray):
+        return o.tolist()
+    if isinstance(o, torch.Tensor):
+        return o.cpu().tolist()
+    return str(o)
+
+
+def _category(model):
+    spec = model._spec
+    if not model.supervised_learning:
+        return {"kmeans": "Clustering", "pca": "DimReduction", "svd": "DimReduction", "glrm": "DimReduction",
+                "isolationforest": "AnomalyDetection", "extendedisolationforest": "AnomalyDetection",
+                "deeplearning": "AutoEncoder"}.get(model.algo, "Unknown")
+    if spec.nclasses == 2:
+        return "Binomial"
+    if spec.nclasses > 2:
+        return "Multinomial"
+    return "Regression"
+
+
+def _dinfo_meta(w, di, prefix="di"):
+    w.meta[prefix] = {"cat_cols": di.cat_cols, "num_cols": di.num_cols, "domains": di.domains,
+                      "cat_offsets": di.cat_offsets, "use_all": di.use_all, "standardize": di.standardize,
+                      "means": di.means, "sigmas": di.sigmas, "plug": di.plug, "cat_modes": di.cat_modes,
+                      "P": di.P, "mvh": di.mvh}
+
+
+def _forest_arrays(w, forest, names):
+    P = forest.pack(torch.device("cpu"))
+    for k in ("feat", "thr", "left", "right", "na_left", "cat_off", "cat_len", "cat_bits", "value", "roots", "tclass"):
+        w.add_array(f"forest_{k}", P[k].cpu().numpy())
+
+
+def build_mojo(model) -> bytes:
+    w = _Writer()
+    algo = model.algo
+    spec = model._spec
+    w.meta["algo"] = algo
+    w.meta["x"] = list(spec.x) if spec is not None else []
+    w.meta["response"] = spec.y if spec is not None else None
+    w.meta["response_domain"] = spec.response_domain if spec is not None else None
+    w.meta["nclasses"] = spec.nclasses if spec is not None else 1
+    w.meta["model_id"] = model.model_id
+    domains = []
+    if algo in ("gbm", "drf", "xgboost", "isolationforest"):
+        w.meta["x_domains"] = getattr(model, "_x_domains", {})
+        _forest_arrays(w, model._forest, spec.x)
+        w.meta["K"] = model._n_tree_classes()
+        w.meta["ntrees"] = len(model._forest)
+        if algo in ("gbm", "xgboost"):
+            w.meta["init_f"] = list(model._init_f)
+            w.meta["link"] = model._dist.link
+            w.meta["family"] = model._dist.family
+            w.meta["tweedie_power"] = getattr(model._dist, "tweedie_power", 1.5)
+        if algo == "drf":
+            w.meta["binomial_single"] = bool(model._binomial_single)
+        if algo == "isolationforest":
+            w.meta["min_len"] = model._min_len
+            w.meta["max_len"] = model._max_len
+            w.meta["threshold"] = model._threshold
+    elif algo == "glm":
+        _dinfo_meta(w, model._dinfo)
+        if getattr(model, "_multi", None) is not None:
+            m = model._multi
+            w.meta["multi"] = m["kind"]
+            if m["kind"] == "multinomial":
+                w.add_array("B", m["B"].cpu().numpy())
+                w.add_array("b0", m["b0"].cpu().numpy())
+            else:
+                w.add_array("beta", m["beta"].cpu().numpy())
+                w.add_array("theta", m["theta"].cpu().numpy())
+        else:
+            w.add_array("beta_std", np.asarray(model._beta_std))
+            w.meta["family"] = model._fam.family
+            w.meta["link"] = model._fam.link
+            w.meta["tlp"] = model._fam.tlp
+    elif algo == "kmeans":
+        _dinfo_meta(w, model._dinfo)
+        w.add_array("centers_std", model._C_std.cpu().numpy())
+    elif algo in ("pca",):
+        _dinfo_meta(w, model._dinfo)
+        w.add_array("evecs", model._evecs.cpu().numpy())
+        w.add_array("mean", model._mean.cpu().numpy())
+    elif algo == "deeplearning":
+        _dinfo_meta(w, model._dinfo)
+        import torch.nn as nn
+        layers = []
+        for i, m in enumerate(model._net):
+            if isinstance(m, nn.Linear):
+                w.add_array(f"W{i}", m.weight.detach().cpu().numpy())
+                w.add_array(f"b{i}", m.bias.detach().cpu().numpy())
+                layers.append(["linear", i])
+            elif m.__class__.__name__ == "_Maxout":
+                w.add_array(f"W{i}", m.lin.weight.detach().cpu().numpy())
+                w.add_array(f"b{i}", m.lin.bias.detach().cpu().numpy())
+                layers.append(["maxout", i, m.k])
+            elif isinstance(m, (nn.Tanh, nn.ReLU, nn.ELU)):
+                layers.append([type(m).__name__.lower(), i])
+        w.meta["layers"] = layers
+        w.meta["autoencoder"] = bool(model._ae)
+        w.meta["K"] = model._K
+        w.meta["ymu"] = getattr(model, "_ymu", 0.0)
+        w.meta["ysd"] = getattr(model, "_ysd", 1.0)
+    elif algo == "naivebayes":
+        w.meta["nb"] = {}
+        w.add_array("prior", model._prior.cpu().numpy())
+        for i, (c, t) in enumerate(model._tables.items()):
+            if t[0] == "cat":
+                w.add_array(f"nb_{i}", t[1].cpu().numpy())
+                w.meta["nb"][c] = ["cat", i, t[2]]
+            else:
+                w.add_array(f"nb_{i}_mean", t[1].cpu().numpy())
+                w.add_array(f"nb_{i}_sd", t[2].cpu().numpy())
+                w.meta["nb"][c] = ["num", i]
+        w.meta["nb_params"] = {k: model._parms[k] for k in ("min_sdev", "eps_sdev", "min_prob", "eps_prob")}
+    elif algo == "stackedensemble":
+        subs = []
+        for i, bm in enumerate(model._base):
+            w.files[f"models/{i}.zip"] = build_mojo(bm)
+            subs.append(bm.model_id)
+        w.files["models/meta.zip"] = build_mojo(model._meta)
+        w.meta["base"] = subs
+        w.meta["level1_names"] = model._names
+    else:
+        raise NotImplementedError(f"MOJO export not supported for {algo}")
+    cols = list(spec.x) + ([spec.y] if spec is not None and spec.y else [])
+    xd = getattr(model, "_x_domains", None) or (model._dinfo.domains if hasattr(model, "_dinfo") else {})
+    for c in cols:
+        if c in xd:
+            domains.append((c, xd[c]))
+    if spec is not None and spec.response_domain:
+        domains.append((spec.y, spec.response_domain))
+    info = {"algorithm": algo, "category": _category(model), "mojo_version": MOJO_VERSION,
+            "n_features": len(spec.x) if spec else 0, "n_classes": spec.nclasses if spec else 1,
+            "supervised": str(model.supervised_learning).lower(), "uuid": model.model_id,
+            "h2o_version": "h2o3_amd-0.1.0"}
+    return w.to_zip_bytes(info, cols, domains)
+
+
+def write_mojo(model, path="."):
+    data = build_mojo(model)
+    if os.path.isdir(path) or not path.endswith(".zip"):
+        os.makedirs(path, exist_ok=True)
+        path = os.path.join(path, f"{model.model_id}.zip")
+    with open(path, "wb") as f:
+        f.write(data)
+    return path
