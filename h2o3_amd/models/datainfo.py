@@ -20,7 +20,7 @@ from ..parallel import cloud
 
 class DataInfo:
     def __init__(self, frame, x, standardize=True, use_all_factor_levels=False, missing_values_handling="MeanImputation",
-                 plug_values=None, pad_to=32, max_cat_levels=None, intercept=True):
+                 plug_values=None, pad_to=32, max_cat_levels=None, intercept=True, pad_extra=0):
         self.x = list(x)
         self.standardize = standardize
         self.use_all = use_all_factor_levels
@@ -62,7 +62,7 @@ class DataInfo:
             else:
                 self.cat_modes[c] = 0
         self.P = len(self.coef_names)
-        self.Pp = ((self.P + pad_to - 1) // pad_to) * pad_to if pad_to else self.P
+        self.Pp = ((self.P + pad_extra + pad_to - 1) // pad_to) * pad_to if pad_to else self.P
 
     def expand(self, frame, dtype=torch.float32, pad=True):
         """Returns (X [n, P or Pp], row_ok mask) on device."""

@@ -33,6 +33,7 @@ from ...parallel import cloud
 from ...parallel import collectives as coll
 from ..base import H2OEstimator
 from ..datainfo import DataInfo
+from ...utils.timer import phase
 from .. import metrics as mm
 
 GLM_DEFAULTS = dict(family="AUTO", tweedie_variance_power=0.0, dispersion_learning_rate=0.5,
@@ -221,7 +222,7 @@ class GLMDriver:
                         float(p.get("tweedie_link_power") or 1.0), float(p.get("theta") or 1e-10))
         self.dinfo = DataInfo(spec.frame, spec.x, standardize=bool(p.get("standardize", True)),
                               missing_values_handling=p.get("missing_values_handling"),
-                              plug_values=p.get("plug_values"))
+                              plug_values=p.get("plug_values"), pad_extra=2)
         self.X, ok = self.dinfo.expand(spec.frame)
         y = spec.y_tensor()
         if spec.is_classification:
@@ -306,33 +307,78 @@ class GLMDriver:
         mu = self.fam.linkinv(eta0)
         d = self.fam.dmu_deta(eta0, mu)
         r = self.w * (self.y - mu) * d / self.fam.variance(mu)
-        g = (self.X.to(torch.float64).T @ r)[: self.P] if self.X.dtype == torch.float64 else \
-            (self.X.T @ r.to(torch.float32)).to(torch.float64)[: self.P]
+        if self._native():
+            # X'r rides the fused Gram pass (column P of the augmented Gram)
+            g = linalg_ops.glm_irls(self.X, aug=self.P, W=r)[0][: self.P, self.P].contiguous()
+        else:
+            g = (self.X.to(torch.float64).T @ r)[: self.P]
         coll.allreduce_(g)
         g = g / self.wsum
         amax = float(g.abs().max()) if g.numel() else 0.0
         return amax / max(1e-2, self.alpha)
 
+    def _native(self):
+        return self.X.device.type == "cuda" and self.X.dtype == torch.float32 and self.Pp % 32 == 0 and \
+            self.Pp <= 512 and self.Pp >= self.P + 2
+
+    def _irls_stats_native(self):
+        """One fused kernel pass: eta, IRLS weights, deviance, augmented Gram."""
+        P = self.P
+        codes = linalg_ops.glm_fused_codes(self.fam.family, self.fam.link, self.fam.tlp)
+        if not hasattr(self, "_y32"):
+            self._y32 = self.y.to(torch.float32)
+            self._w32 = None if bool((self.w == 1).all()) else self.w.to(torch.float32)
+            self._off32 = None if self.offset is None else self.offset.to(torch.float32)
+        with phase("glm.irls_pass"):
+            if codes is not None:
+                bt = torch.zeros(self.Pp, dtype=torch.float32, device=self.X.device)
+                bt[:P] = torch.as_tensor(self.beta[:P], dtype=torch.float32)
+                Gf, dev = linalg_ops.glm_irls(self.X, aug=P, beta=bt, b0=float(self.beta[-1]), y=self._y32,
+                                              wprior=self._w32, offset=self._off32, codes=codes,
+                                              tvp=self.fam.tvp, theta=self.fam.theta)
+                dev = dev.view(1)
+            else:
+                eta = self._eta()
+                mu = self.fam.linkinv(eta)
+                d = self.fam.dmu_deta(eta, mu)
+                W = self.w * d * d / self.fam.variance(mu)
+                off = self.offset if self.offset is not None else 0.0
+                z = (eta - off) + (self.y - mu) / d
+                Gf, _ = linalg_ops.glm_irls(self.X, aug=P, W=W, z=z)
+                dev = (self.w * self.fam.deviance(self.y, mu)).sum().view(1)
+        return Gf[:P, :P], Gf[:P, P + 1].contiguous(), Gf[:P, P].contiguous(), Gf[P, P].view(1), \
+            Gf[P, P + 1].view(1), dev
+
     def _irls_stats(self):
-        eta = self._eta()
-        mu = self.fam.linkinv(eta)
-        d = self.fam.dmu_deta(eta, mu)
-        var = self.fam.variance(mu)
-        W = (self.w * d * d / var)
-        off = self.offset if self.offset is not None else 0.0
-        z = (eta - off) + (self.y - mu) / d
-        if self.fam.family == "gaussian" and self.fam.link == "identity":
-            W = self.w
-            z = self.y - off
-        Wf = W.to(torch.float32)
-        G = linalg_ops.weighted_gram(self.X, Wf)[: self.P, : self.P]
-        Wz = (W * z)
-        xz = (self.X.T @ Wz.to(torch.float32)).to(torch.float64)[: self.P] if self.X.device.type == "cuda" else \
-            (self.X.to(torch.float64).T @ Wz)[: self.P]
-        # intercept row/col: X'W 1 and sum W, sum Wz
-        xw = (self.X.T @ Wf).to(torch.float64)[: self.P]
-        sw, swz = W.sum().view(1), Wz.sum().view(1)
-        dev = (self.w * self.fam.deviance(self.y, mu)).sum().view(1)
+        if self._native():
+            G, xz, xw, sw, swz, dev = self._irls_stats_native()
+            return self._finish_stats(G, xz, xw, sw, swz, dev)
+        with phase("glm.eta"):
+            eta = self._eta()
+        with phase("glm.weights"):
+            mu = self.fam.linkinv(eta)
+            d = self.fam.dmu_deta(eta, mu)
+            var = self.fam.variance(mu)
+            W = (self.w * d * d / var)
+            off = self.offset if self.offset is not None else 0.0
+            z = (eta - off) + (self.y - mu) / d
+            if self.fam.family == "gaussian" and self.fam.link == "identity":
+                W = self.w
+                z = self.y - off
+            Wf = W.to(torch.float32)
+        with phase("glm.gram"):
+            G = linalg_ops.weighted_gram(self.X, Wf)[: self.P, : self.P]
+        with phase("glm.xtwz"):
+            Wz = (W * z)
+            xz = (self.X.T @ Wz.to(torch.float32)).to(torch.float64)[: self.P] if self.X.device.type == "cuda" else \
+                (self.X.to(torch.float64).T @ Wz)[: self.P]
+            # intercept row/col: X'W 1 and sum W, sum Wz
+            xw = (self.X.T @ Wf).to(torch.float64)[: self.P]
+            sw, swz = W.sum().view(1), Wz.sum().view(1)
+            dev = (self.w * self.fam.deviance(self.y, mu)).sum().view(1)
+        return self._finish_stats(G, xz, xw, sw, swz, dev)
+
+    def _finish_stats(self, G, xz, xw, sw, swz, dev):
         stats = torch.cat([G.reshape(-1), xz, xw, sw, swz, dev])
         coll.allreduce_(stats)
         P = self.P

@@ -19,8 +19,110 @@ def _lib():
     if lib is not None and not getattr(lib, "_typed", False):
         lib.h2o_gram.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_int, ctypes.c_void_p,
                                  ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        P, I, LL, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong, ctypes.c_float
+        lib.h2o_glm_irls.argtypes = [P, LL, I, P, I, I, I, P, F, P, P, P, I, I, F, F, P, P, I, P, P, P]
         lib._typed = True
     return lib
+
+
+def _pairs(T, device):
+    key = (T, device)
+    if key not in _pairs_cache:
+        pr = [(i, j) for i in range(T) for j in range(i, T)]
+        _pairs_cache[key] = (torch.tensor(pr, dtype=torch.int32, device=device), pr)
+    return _pairs_cache[key]
+
+
+def _assemble(tiles, pairs_t, T):
+    """[npairs, 32, 32] upper-triangle tiles -> symmetric [32T, 32T]."""
+    ii, jj = pairs_t[:, 0].long(), pairs_t[:, 1].long()
+    Gb = torch.zeros((T, T, 32, 32), dtype=torch.float64, device=tiles.device)
+    Gb[jj, ii] = tiles.transpose(1, 2)
+    Gb[ii, jj] = tiles
+    return Gb.permute(0, 2, 1, 3).reshape(32 * T, 32 * T)
+
+
+_LINK = {"identity": 0, "logit": 1, "log": 2, "inverse": 3}
+_VAR = {"gaussian": 0, "binomial": 1, "quasibinomial": 1, "fractionalbinomial": 1, "poisson": 2, "gamma": 3,
+        "tweedie": 4, "negativebinomial": 5}
+
+
+def glm_fused_codes(family, link, tlp=1.0):
+    """(link, var) codes of the fused IRLS kernel, or None when unsupported."""
+    if link == "tweedie":
+        link = "log" if tlp == 0 else ("identity" if tlp == 1 else None)
+    if link not in _LINK or family not in _VAR:
+        return None
+    return _LINK[link], _VAR[family]
+
+
+def _f32(t):
+    return None if t is None else t.to(torch.float32).contiguous()
+
+
+def _ptr(t):
+    return ctypes.c_void_p(0 if t is None else t.data_ptr())
+
+
+def glm_irls(X, aug=-1, beta=None, b0=0.0, y=None, wprior=None, offset=None, codes=(0, 0), tvp=0.0, theta=1e-10,
+             W=None, z=None, target_blocks=1024):
+    """One pass of the fused IRLS kernel (ops/csrc/gram.hip glm_irls_kernel).
+
+    Fused mode (beta given): per row eta = x.beta + b0 + offset, the family's
+    IRLS weight / working response, deviance.  External mode: W, z given.
+    Returns (G [Pp, Pp] f64 — columns `aug` / `aug+1` hold X'W / X'Wz and
+    their cross terms when aug >= 0 — and the f64 deviance, or None).
+    """
+    N, P = X.shape
+    lib = _lib()
+    if lib is None:
+        raise RuntimeError("gram extension not built (run __graft_entry__.build())")
+    T = P // 32
+    pairs_t, pr = _pairs(T, X.device)
+    npairs = len(pr)
+    groups = -(-npairs // 12)
+    splits = max(1, min(max(1, target_blocks // groups), N // 4096))
+    rpb = -(-N // splits)
+    rpb = ((rpb + 63) // 64) * 64
+    splits = -(-N // rpb)
+    out = torch.zeros((splits, npairs, 32, 32), dtype=torch.float64, device=X.device)
+    dev = torch.zeros(splits, dtype=torch.float64, device=X.device)
+    X = X.contiguous()
+    bt = _f32(beta)
+    keep = [_f32(y), _f32(wprior), _f32(offset), _f32(W), _f32(z)]
+    rc = lib.h2o_glm_irls(_ptr(X), N, P, _ptr(pairs_t), npairs, splits, rpb, _ptr(bt), float(b0), _ptr(keep[0]),
+                          _ptr(keep[1]), _ptr(keep[2]), int(codes[0]), int(codes[1]), float(tvp), float(theta),
+                          _ptr(keep[3]), _ptr(keep[4]), int(aug), _ptr(out), _ptr(dev),
+                          ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    if rc != 0:
+        raise RuntimeError(f"h2o_glm_irls failed: {rc}")
+    G = _assemble(out.sum(0), pairs_t, T)
+    return G, (dev.sum() if beta is not None else None)
+
+
+def glm_irls_reference(X, aug=-1, beta=None, b0=0.0, y=None, wprior=None, offset=None, fam=None, W=None, z=None):
+    """fp64 torch reference of glm_irls (tests / CPU)."""
+    Xd = X.to(torch.float64).clone()
+    dev = None
+    if beta is not None:
+        eta = Xd @ beta.to(torch.float64) + b0
+        off = offset.to(torch.float64) if offset is not None else 0.0
+        eta = eta + off
+        mu = fam.linkinv(eta)
+        pw = wprior.to(torch.float64) if wprior is not None else torch.ones_like(eta)
+        yd = y.to(torch.float64)
+        if fam.family == "gaussian" and fam.link == "identity":
+            W, z = pw, yd - off
+        else:
+            d = fam.dmu_deta(eta, mu)
+            W = pw * d * d / fam.variance(mu)
+            z = (eta - off) + (yd - mu) / d
+        dev = (pw * fam.deviance(yd, mu)).sum()
+    W = torch.ones(X.shape[0], dtype=torch.float64) if W is None else W.to(torch.float64)
+    if aug >= 0:
+        Xd[:, aug] = 1.0
+        Xd[:, aug + 1] = 0.0 if z is None else z.to(torch.float64)
+    return Xd.T @ (Xd * W.view(-1, 1)), dev
 
 
 def weighted_gram(X: torch.Tensor, w: torch.Tensor | None = None, use_native=None, target_blocks=2048):
@@ -32,13 +134,11 @@ def weighted_gram(X: torch.Tensor, w: torch.Tensor | None = None, use_native=Non
         if w is None:
             return Xd.T @ Xd
         return Xd.T @ (Xd * w.to(torch.float64).view(-1, 1))
+    if P <= 512:
+        return glm_irls(X, W=w)[0]
     lib = _lib()
     T = P // 32
-    key = (T, X.device)
-    if key not in _pairs_cache:
-        pr = [(i, j) for i in range(T) for j in range(i, T)]
-        _pairs_cache[key] = (torch.tensor(pr, dtype=torch.int32, device=X.device), pr)
-    pairs_t, pr = _pairs_cache[key]
+    pairs_t, pr = _pairs(T, X.device)
     npairs = len(pr)
     splits = max(1, min(target_blocks // npairs, N // 2048))
     rpb = -(-N // splits)
@@ -52,9 +152,4 @@ def weighted_gram(X: torch.Tensor, w: torch.Tensor | None = None, use_native=Non
                       ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
     if rc != 0:
         raise RuntimeError(f"h2o_gram failed: {rc}")
-    tiles = out.sum(0)  # [npairs, 32, 32]
-    ii, jj = pairs_t[:, 0].long(), pairs_t[:, 1].long()
-    Gb = torch.zeros((T, T, 32, 32), dtype=torch.float64, device=X.device)
-    Gb[jj, ii] = tiles.transpose(1, 2)
-    Gb[ii, jj] = tiles
-    return Gb.permute(0, 2, 1, 3).reshape(P, P)
+    return _assemble(out.sum(0), pairs_t, T)
