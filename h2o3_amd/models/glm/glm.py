@@ -325,6 +325,8 @@ class GLMDriver:
         """One fused kernel pass: eta, IRLS weights, deviance, augmented Gram."""
         P = self.P
         codes = linalg_ops.glm_fused_codes(self.fam.family, self.fam.link, self.fam.tlp)
+        if self.Pp & (self.Pp - 1):
+            codes = None  # fused path needs a power-of-two padded width
         if not hasattr(self, "_y32"):
             self._y32 = self.y.to(torch.float32)
             self._w32 = None if bool((self.w == 1).all()) else self.w.to(torch.float32)

@@ -16,8 +16,12 @@
 // the reference's double Gram at f32-MFMA speed); waves are reduced through
 // LDS and each block writes an f64 partial tile that the host sums.
 #include "common.h"
+#include <type_traits>
+#include <utility>
+#include <cstdlib>
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 __global__ __launch_bounds__(256) void gram_kernel(const float* __restrict__ X, const float* __restrict__ w,
                                                    long long N, int P, const int2* __restrict__ pairs,
@@ -87,28 +91,31 @@ extern "C" int h2o_gram(const float* X, const float* w, long long N, int P, cons
 // xy += w z x, likelihood += dev) and hex/gram/Gram.java.
 //
 // MI355X design: a 256-thread workgroup streams 64-row chunks of X through
-// LDS (row stride S = P (+32) so the two half-waves of an MFMA operand read
-// hit disjoint bank halves).  Per chunk: (1) the four waves compute
+// LDS (row stride S = P + 16 (mod 64) so the four row-quarters of an MFMA
+// operand read hit disjoint banks).  Per chunk: (1) the four waves compute
 // eta = x.beta for 16 rows each (beta held in registers, 64-lane dot + DPP
 // reduce); (2) wave 0 evaluates the family/link for its 64 rows (mu, IRLS
 // weight W, working response z, deviance) and overwrites two padding
 // columns of the staged chunk with 1 and z — so the SAME MFMA sweep also
 // produces X'W1, X'Wz, sum W and sum Wz (the augmented Gram [X 1 z]'W[X 1 z]);
-// (3) every wave runs v_mfma_f32_32x32x2f32 for up to PPW upper-triangle
-// 32x32 tile pairs straight out of LDS, folding f32 -> f32 -> f64 every 256 / 16K
+// (3) every wave runs v_mfma_f32_16x16x4f32 for up to 9 upper-triangle
+// 16x16 tile pairs straight out of LDS (P=128: 36 pairs = 4 waves x 9,
+// perfectly balanced over the SIMDs; less diagonal waste than 32x32), folding f32 -> f32 -> f64 every 256 / 16K
 // rows.  Each block owns an f64 partial tile (no atomics -> deterministic;
 // the caller zero-fills `out`).
 // Mode EXTERNAL (W, z supplied by the caller) serves families / links the
 // fused path does not cover and the plain weighted Gram (z == nullptr).
 // ---------------------------------------------------------------------------
 #define GI_RC 64
-#define GI_PPW 3
+#define GI_PPW 9   // 16x16 tile pairs per wave (36 per workgroup: P=128 is one exact group)
 
 struct GlmFamArgs {
   int link;     // 0 identity 1 logit 2 log 3 inverse
   int var;      // 0 gaussian 1 binomial 2 poisson 3 gamma 4 tweedie 5 negbin
   float tvp;    // tweedie variance power
   float theta;  // negative-binomial dispersion
+  int dbg;      // perf experiments only: bit0 skip MFMA sweep, bit1 skip HBM loads
+  int signed_w; // external weights may be negative (no sqrt(W) pre-scaling)
 };
 
 __device__ __forceinline__ float gi_linkinv(int link, float eta) {
@@ -168,102 +175,164 @@ __device__ __forceinline__ float gi_dev(const GlmFamArgs& f, float y, float mu) 
   }
 }
 
-template <bool FUSED>
+// upper-triangle pair p of T tiles -> (i, j), same order as linalg_ops._pairs
+__host__ __device__ constexpr int gi_pair_i(int T, int p) {
+  int i = 0;
+  while (p >= T - i) { p -= T - i; ++i; }
+  return i;
+}
+__host__ __device__ constexpr int gi_pair_j(int T, int p) {
+  int i = 0;
+  while (p >= T - i) { p -= T - i; ++i; }
+  return i + p;
+}
+
+template <int T, int SL, int Q>
+__device__ __forceinline__ void gi_mfma_q(const float* xr, const float* xw, f32x4* acc) {
+  constexpr int pp = SL + 4 * Q;
+  if constexpr (pp < T * (T + 1) / 2) {
+    constexpr int ti = gi_pair_i(T, pp), tj = gi_pair_j(T, pp);
+    acc[Q] = __builtin_amdgcn_mfma_f32_16x16x4f32(xr[ti], xw[tj], acc[Q], 0, 0, 0);
+  }
+}
+template <int T, int SL, int... Q>
+__device__ __forceinline__ void gi_mfma_all(std::integer_sequence<int, Q...>, const float* xr, const float* xw,
+                                            f32x4* acc) {
+  (gi_mfma_q<T, SL, Q>(xr, xw, acc), ...);
+}
+
+// Chunk rows (multiple of 4 = one 16x16x4 k-step); the staging registers hold
+// NV = ceil(RC*PP/1024) float4 per thread.
+template <int PP>
+struct GiCfg {
+  static constexpr int RC = PP <= 128 ? 64 : ((8192 / PP) / 4 * 4 < 16 ? 16 : (8192 / PP) / 4 * 4);
+  static constexpr int P4 = PP / 4;                        // float4 per row
+  static constexpr int NV = (RC * P4 + 255) / 256;         // float4 per thread
+  static constexpr bool EXACT = (RC * P4) % 256 == 0;
+  static constexpr int FOLD = RC >= 256 ? 1 : 256 / RC;   // chunks per f32 fold (~256 rows)
+  static constexpr int RPP = 256 / P4 > 0 ? 256 / P4 : 1;  // rows per staging pass
+  static constexpr bool POW2 = (PP & (PP - 1)) == 0;
+};
+
+template <int PP, bool FUSED>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void glm_irls_kernel(
-    const float* __restrict__ X, long long N, int P, int S, const int2* __restrict__ pairs, int n_pairs,
-    int rows_per_block, const float* __restrict__ beta, float b0, const float* __restrict__ y,
-    const float* __restrict__ wprior, const float* __restrict__ offset, GlmFamArgs fam,
-    const float* __restrict__ Wext, const float* __restrict__ zext, int aug, double* __restrict__ out,
-    double* __restrict__ dev_out) {
-  extern __shared__ float L[];          // [GI_RC][S]
-  __shared__ float wr[GI_RC];
-  __shared__ float eta_s[GI_RC];
+    const float* __restrict__ X, long long N, const int2* __restrict__ pairs, int n_pairs, int rows_per_block,
+    const float* __restrict__ beta, float b0, const float* __restrict__ y, const float* __restrict__ wprior,
+    const float* __restrict__ offset, GlmFamArgs fam, const float* __restrict__ Wext,
+    const float* __restrict__ zext, int aug, double* __restrict__ out, double* __restrict__ dev_out) {
+  using C = GiCfg<PP>;
+  constexpr int RC = C::RC, P4 = C::P4, NV = C::NV;
+  // row stride: the 4 row-quarters of an MFMA operand read land 16 banks apart
+  constexpr int S = PP + ((16 - (PP % 64)) & 63);
+  static_assert(!FUSED || C::POW2, "fused path needs a power-of-two padded width");
+  __shared__ float L[RC * S];
+  __shared__ float wr[RC];
+  __shared__ float eta_s[2][RC];
   const int split = blockIdx.x;
   const int grp = blockIdx.y;
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
-  const int kr = lane >> 5, cc = lane & 31;
+  const int kr = lane >> 4, cc = lane & 15;
   const long long rb0 = (long long)split * rows_per_block;
   const long long rb1 = min(N, rb0 + rows_per_block);
 
+  // tile pairs of this wave; the slot rotates with the block id so that the
+  // co-resident blocks of a CU spread the 3-pair slots over all four SIMDs
   int ci[GI_PPW], cj[GI_PPW];
   bool pv[GI_PPW];
+  const int slot = __builtin_amdgcn_readfirstlane((wv + split) & 3);  // wave-uniform -> SGPRs
 #pragma unroll
   for (int q = 0; q < GI_PPW; ++q) {
-    const int p = grp * (4 * GI_PPW) + wv + 4 * q;
+    const int p = grp * (4 * GI_PPW) + slot + 4 * q;
     pv[q] = p < n_pairs;
     const int2 t = pv[q] ? pairs[p] : make_int2(0, 0);
-    ci[q] = t.x * 32;
-    cj[q] = t.y * 32;
+    ci[q] = __builtin_amdgcn_readfirstlane(t.x * 16);
+    cj[q] = __builtin_amdgcn_readfirstlane(t.y * 16);
   }
-  float bet[8];
-  if (FUSED) {
+  int npv = 0;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int c = lane + 64 * k;
-      bet[k] = c < P ? beta[c] : 0.f;
-    }
-  }
-  // three-level accumulation: MFMA f32 (256 rows) -> f32 mid (<=16K rows)
-  // -> this block's own f64 output tile (plain read-modify-write, no atomics)
-  f32x16 mid[GI_PPW];
-  f32x16 acc[GI_PPW];
+  for (int q = 0; q < GI_PPW; ++q) npv += pv[q] ? 1 : 0;
+  // fused: every thread always stages the same 4 columns (POW2 width), so
+  // its slice of beta lives in 4 registers and eta is reduced from the
+  // staging registers before they ever reach LDS
+  const int c4 = threadIdx.x % P4;
+  float4 b4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (FUSED) b4 = *reinterpret_cast<const float4*>(beta + 4 * c4);
+
+  // mid-level f32 accumulators live in LDS (this wave's own slice, lane-major:
+  // conflict-free) to keep the VGPR budget for the MFMA pipeline
+  __shared__ float midL[4][GI_PPW * 4][64];
+  f32x4 acc[GI_PPW];
 #pragma unroll
   for (int q = 0; q < GI_PPW; ++q) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) { mid[q][i] = 0.f; acc[q][i] = 0.f; }
+    for (int i = 0; i < 4; ++i) { midL[wv][4 * q + i][lane] = 0.f; acc[q][i] = 0.f; }
   }
   double dev = 0.0;
-  const int P4 = P >> 2;
-  const int nvec = GI_RC * P4;
-  int since = 0;
-  for (long long r0 = rb0; r0 < rb1; r0 += GI_RC) {
-    // (0) stage the chunk (clamped rows past N are zero-weighted below)
-    for (int e = threadIdx.x; e < nvec; e += 256) {
-      const int rr = e / P4, c4 = e - rr * P4;
+
+  f32x4 V[NV];
+  float sy = 0.f, sw = 0.f, so = 0.f;  // wave 0: per-row scalars of the staged chunk
+  auto load_chunk = [&](long long r0) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int e = threadIdx.x + 256 * i;
+      const int ee = (C::EXACT || e < RC * P4) ? e : RC * P4 - 1;  // tail lanes re-load the last vector
+      const int rr = ee / P4, cq = ee - rr * P4;
       const long long g = min(r0 + rr, N - 1);
-      const float4 v = *reinterpret_cast<const float4*>(X + g * (long long)P + 4 * c4);
-      *reinterpret_cast<float4*>(L + rr * S + 4 * c4) = v;
+      V[i] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(X + g * (long long)PP) + cq);
+    }
+    if (wv == 0 && lane < RC) {
+      const long long g = min(r0 + lane, N - 1);
+      if (FUSED) {
+        sy = y[g];
+        sw = wprior ? wprior[g] : 1.f;
+        so = offset ? offset[g] : 0.f;
+      } else {
+        sw = Wext ? Wext[g] : 1.f;
+        sy = zext ? zext[g] : 0.f;
+      }
+    }
+  };
+
+  int since = 0;
+  if (rb0 < rb1) load_chunk(rb0);
+  for (long long r0 = rb0; r0 < rb1; r0 += RC) {
+    // (0) registers -> LDS (+ eta partial sums straight from the registers)
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int e = threadIdx.x + 256 * i;
+      const int ee = (C::EXACT || e < RC * P4) ? e : RC * P4 - 1;  // duplicate store of identical data
+      const int rr = ee / P4, cq = ee - rr * P4;
+      *reinterpret_cast<f32x4*>(L + rr * S + 4 * cq) = V[i];
+      if (FUSED) {
+        float s = V[i].x * b4.x + V[i].y * b4.y + V[i].z * b4.z + V[i].w * b4.w;
+        constexpr int G = P4 < 64 ? P4 : 64;
+#pragma unroll
+        for (int o = G / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+        if ((threadIdx.x & (G - 1)) == 0) eta_s[(threadIdx.x % P4) / 64][rr] = s;
+      }
     }
     __syncthreads();
-    if (FUSED) {
-      // (1) eta for 16 rows per wave
-      for (int j = 0; j < GI_RC / 4; ++j) {
-        const int rr = wv * (GI_RC / 4) + j;
-        float s = 0.f;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const int c = lane + 64 * k;
-          if (c < P) s += L[rr * S + c] * bet[k];
-        }
-        s = wave_sum(s);
-        if (lane == 0) eta_s[rr] = s;
-      }
-      __syncthreads();
-    }
-    // (2) family / link on wave 0: IRLS weight + working response
-    if (wv == 0) {
+    // (1) wave 0: family / link -> IRLS weight W and working response z
+    if (wv == 0 && lane < RC) {
       const long long r = r0 + lane;
       float W = 0.f, z = 0.f;
       if (r < rb1) {
         if (FUSED) {
-          const float off = offset ? offset[r] : 0.f;
-          const float eta = eta_s[lane] + b0 + off;
+          const float eta = eta_s[0][lane] + (P4 > 64 ? eta_s[1][lane] : 0.f) + b0 + so;
           const float mu = gi_linkinv(fam.link, eta);
-          const float yr = y[r];
-          const float pw = wprior ? wprior[r] : 1.f;
           if (fam.link == 0 && fam.var == 0) {
-            W = pw;
-            z = yr - off;
+            W = sw;
+            z = sy - so;
           } else {
             const float d = gi_dmu(fam.link, mu);
-            W = pw * d * d / gi_var(fam, mu);
-            z = (eta - off) + (yr - mu) / d;
+            W = sw * d * d / gi_var(fam, mu);
+            z = (eta - so) + (sy - mu) / d;
           }
-          if (pw != 0.f) dev += (double)(pw * gi_dev(fam, yr, mu));
+          if (sw != 0.f) dev += (double)(sw * gi_dev(fam, sy, mu));
         } else {
-          W = Wext ? Wext[r] : 1.f;
-          z = zext ? zext[r] : 0.f;
+          W = sw;
+          z = sy;
         }
       }
       wr[lane] = W;
@@ -272,42 +341,83 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         L[lane * S + aug + 1] = z;
       }
     }
+    // (2) prefetch the next chunk while this one is on the matrix cores
+    if (r0 + RC < rb1) load_chunk(r0 + RC);
     __syncthreads();
-    // (3) MFMA sweep over the chunk for this wave's tile pairs
-#pragma unroll 4
-    for (int k = 0; k < GI_RC / 2; ++k) {
-      const int rr = 2 * k + kr;
-      const float w = wr[rr];
-      const float* row = L + rr * S;
+    // (3) MFMA sweep; the pair count is wave-uniform, so branch once outside
+    // the loop and keep the body branch-free (LDS loads run ahead of MFMAs)
+    auto sweep = [&](auto npv_tag) {
+      constexpr int NPV = decltype(npv_tag)::value;
+#pragma unroll 2
+      for (int k = 0; k < RC / 4; ++k) {
+        const int rr = 4 * k + kr;
+        const float w = wr[rr];
+        const float* row = L + rr * S;
 #pragma unroll
-      for (int q = 0; q < GI_PPW; ++q) {
-        if (pv[q]) {
+        for (int q = 0; q < NPV; ++q) {
           const float a = row[ci[q] + cc];
           const float b = w * row[cj[q] + cc];
-          acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[q], 0, 0, 0);
+          acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[q], 0, 0, 0);
         }
       }
+    };
+    // P <= 128 (one pair group): the wave's pairs are compile-time, so each
+    // k-step reads every 16-column tile ONCE (T <= 8 LDS reads instead of
+    // 2 per pair) and weights it once; the 9 MFMAs then run from registers.
+    auto sweep_ct = [&](auto slot_tag) {
+      constexpr int SL = decltype(slot_tag)::value;
+      constexpr int T = PP / 16;
+#pragma unroll 2
+      for (int k = 0; k < RC / 4; ++k) {
+        const int rr = 4 * k + kr;
+        const float w = wr[rr];
+        const float* row = L + rr * S + cc;
+        float xr[T], xw[T];
+#pragma unroll
+        for (int t = 0; t < T; ++t) xr[t] = row[16 * t];
+#pragma unroll
+        for (int t = 0; t < T; ++t) xw[t] = w * xr[t];
+        gi_mfma_all<T, SL>(std::make_integer_sequence<int, GI_PPW>{}, xr, xw, acc);
+      }
+    };
+    if constexpr (PP <= 128) {
+      switch (slot) {
+        case 0: sweep_ct(std::integral_constant<int, 0>{}); break;
+        case 1: sweep_ct(std::integral_constant<int, 1>{}); break;
+        case 2: sweep_ct(std::integral_constant<int, 2>{}); break;
+        default: sweep_ct(std::integral_constant<int, 3>{}); break;
+      }
+    } else switch (npv) {
+      case 9: sweep(std::integral_constant<int, 9>{}); break;
+      case 8: sweep(std::integral_constant<int, 8>{}); break;
+      case 7: sweep(std::integral_constant<int, 7>{}); break;
+      case 6: sweep(std::integral_constant<int, 6>{}); break;
+      case 5: sweep(std::integral_constant<int, 5>{}); break;
+      case 4: sweep(std::integral_constant<int, 4>{}); break;
+      case 3: sweep(std::integral_constant<int, 3>{}); break;
+      case 2: sweep(std::integral_constant<int, 2>{}); break;
+      case 1: sweep(std::integral_constant<int, 1>{}); break;
+      default: break;
     }
     ++since;
-    const bool last = r0 + GI_RC >= rb1;
-    if ((since & 3) == 0 || last) {
+    const bool last = r0 + RC >= rb1;
+    if (since % C::FOLD == 0 || last) {
 #pragma unroll
       for (int q = 0; q < GI_PPW; ++q) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) { mid[q][i] += acc[q][i]; acc[q][i] = 0.f; }
+        for (int i = 0; i < 4; ++i) { midL[wv][4 * q + i][lane] += acc[q][i]; acc[q][i] = 0.f; }
       }
     }
-    if (since == 256 || last) {
+    if (since >= 64 * C::FOLD || last) {
 #pragma unroll
       for (int q = 0; q < GI_PPW; ++q) {
         if (!pv[q]) continue;
-        const int p = grp * (4 * GI_PPW) + wv + 4 * q;
-        double* o = out + ((size_t)split * n_pairs + p) * 1024;
+        const int p = grp * (4 * GI_PPW) + slot + 4 * q;
+        double* o = out + ((size_t)split * n_pairs + p) * 256;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int row = (i & 3) + 8 * (i >> 2) + 4 * kr;
-          o[row * 32 + cc] += (double)mid[q][i];
-          mid[q][i] = 0.f;
+        for (int i = 0; i < 4; ++i) {
+          o[(4 * kr + i) * 16 + cc] += (double)midL[wv][4 * q + i][lane];  // D[i][j]: i = 4*(lane/16)+v, j = lane%16
+          midL[wv][4 * q + i][lane] = 0.f;
         }
       }
       since = 0;
@@ -320,24 +430,314 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// Warp-specialised variant for padded widths <= 128 (the 100-column bench
+// shape): 512-thread workgroups, waves 0-3 are MFMA consumers, waves 4-7 are
+// producers.  LDS holds TWO 64-row chunks; while the consumers sweep chunk i
+// the producers write chunk i+1 (loaded from HBM one iteration earlier, so a
+// sweep of latency hiding; two chunks stay in flight), evaluate the family for their own 16 rows
+// (each producer wave owns whole rows: eta is a pure in-wave shuffle reduce)
+// and issue the loads of chunk i+3.  One barrier per chunk.  Consumers keep
+// the MFMA accumulators in registers (f32 over <= 1024 rows) and fold them
+// into the block's own f64 tile (no atomics, deterministic).
+// ---------------------------------------------------------------------------
+template <int PP, bool FUSED, bool SQW>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) void glm_irls_ws_kernel(
+    const float* __restrict__ X, long long N, int n_pairs, int rows_per_block, const float* __restrict__ beta,
+    float b0, const float* __restrict__ y, const float* __restrict__ wprior, const float* __restrict__ offset,
+    GlmFamArgs fam, const float* __restrict__ Wext, const float* __restrict__ zext, int aug,
+    double* __restrict__ out, double* __restrict__ dev_out) {
+  constexpr int RC = 64;
+  constexpr int P4 = PP / 4;
+  constexpr int T = PP / 16;
+  constexpr int S = PP + ((16 - (PP % 64)) & 63);
+  constexpr int RPW = 16;              // rows owned by one producer wave
+  constexpr int NVP = RPW * P4 / 64;   // float4 per producer lane per chunk
+  constexpr int RPV = 64 / P4;         // rows covered by one float4 slot of a wave
+  static_assert(PP <= 128 && (PP & (PP - 1)) == 0, "ws kernel: power-of-two width <= 128");
+  __shared__ float L[2][RC * S];
+  __shared__ float wr[2][RC];
+  __shared__ double dsum[4];
+  const int split = blockIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const long long rb0 = (long long)split * rows_per_block;
+  const long long rb1 = min(N, rb0 + rows_per_block);
+  const int nchunks = rb1 > rb0 ? (int)((rb1 - rb0 + RC - 1) / RC) : 0;
+
+  if (wv >= 4) {
+    // ============================ producers ============================
+    const int pw = wv - 4;
+    const int cq = lane % P4;
+    f32x4 b4 = {0.f, 0.f, 0.f, 0.f};
+    if (FUSED) b4 = *reinterpret_cast<const f32x4*>(beta + 4 * cq);
+    struct Stage {
+      f32x4 V[NVP];
+      float sy, sw, so;
+    };
+    // non-fused: two chunks in flight per producer lane; fused keeps one (the
+    // eta / family registers would otherwise spill at the 128-VGPR budget)
+    constexpr bool DEEP = !FUSED;
+    Stage A, B;
+    double dev = 0.0;
+    auto load = [&](int c, Stage& st) {
+      f32x4* V = st.V;
+      float& sy = st.sy;
+      float& sw = st.sw;
+      float& so = st.so;
+      const long long r0 = rb0 + (long long)c * RC + pw * RPW;
+      if (fam.dbg & 2) {
+#pragma unroll
+        for (int v = 0; v < NVP; ++v) V[v] = f32x4{0.f, 0.f, 0.f, (float)c};
+      } else {
+#pragma unroll
+        for (int v = 0; v < NVP; ++v) {
+          const long long g = min(r0 + v * RPV + lane / P4, N - 1);
+          V[v] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(X + g * (long long)PP) + cq);
+        }
+      }
+      if (lane < RPW) {
+        const long long g = min(r0 + lane, N - 1);
+        if (FUSED) {
+          sy = y[g];
+          sw = wprior ? wprior[g] : 1.f;
+          so = offset ? offset[g] : 0.f;
+        } else {
+          sw = Wext ? Wext[g] : 1.f;
+          sy = zext ? zext[g] : 0.f;
+        }
+      }
+    };
+    auto store = [&](int c, Stage& st) {
+      const f32x4* V = st.V;
+      const float sy = st.sy, sw = st.sw, so = st.so;
+      float* Lb = L[c & 1];
+      float etav = 0.f;
+      if (FUSED) {
+#pragma unroll
+        for (int v = 0; v < NVP; ++v) {
+          float sdot = V[v].x * b4.x + V[v].y * b4.y + V[v].z * b4.z + V[v].w * b4.w;
+#pragma unroll
+          for (int o = P4 / 2; o > 0; o >>= 1) sdot += __shfl_xor(sdot, o, 64);
+          // lane j (< 16) collects the eta of its row j = v*RPV + src/P4
+          const float got = __shfl(sdot, (lane % RPV) * P4, 64);
+          if (lane / RPV == v) etav = got;
+        }
+      }
+      float W = 0.f, z = 0.f;
+      if (lane < RPW) {
+        const long long r = rb0 + (long long)c * RC + pw * RPW + lane;
+        if (r < rb1) {
+          if (FUSED) {
+            const float eta = etav + b0 + so;
+            const float mu = gi_linkinv(fam.link, eta);
+            if (fam.link == 0 && fam.var == 0) {
+              W = sw;
+              z = sy - so;
+            } else {
+              const float d = gi_dmu(fam.link, mu);
+              W = sw * d * d / gi_var(fam, mu);
+              z = (eta - so) + (sy - mu) / d;
+            }
+            if (sw != 0.f) dev += (double)(sw * gi_dev(fam, sy, mu));
+          } else {
+            W = sw;
+            z = sy;
+          }
+        }
+      }
+      // SQW: rows are staged pre-scaled by sqrt(W) so the consumers' MFMA
+      // operands come straight from LDS (no VALU between LDS and MFMA)
+      const float sq = SQW ? sqrtf(fmaxf(W, 0.f)) : 1.f;
+#pragma unroll
+      for (int v = 0; v < NVP; ++v) {
+        const int rl = pw * RPW + v * RPV + lane / P4;
+        f32x4 val = V[v];
+        if (SQW) val *= __shfl(sq, v * RPV + lane / P4, 64);
+        *reinterpret_cast<f32x4*>(Lb + rl * S + 4 * cq) = val;
+      }
+      if (lane < RPW) {
+        const int rl = pw * RPW + lane;
+        if (!SQW) wr[c & 1][rl] = W;
+        if (aug >= 0) {
+          Lb[rl * S + aug] = sq;
+          Lb[rl * S + aug + 1] = sq * z;
+        }
+      }
+    };
+    if (nchunks > 0) {
+      load(0, A);
+      store(0, A);
+      if (nchunks > 1) load(1, A);
+      if (DEEP && nchunks > 2) load(2, B);
+    }
+    __syncthreads();
+    // iteration i stores chunk i+1 (stage A for even i, B for odd) and
+    // refills that stage with chunk i+3: two chunks always in flight
+    for (int i = 0; i < nchunks; ++i) {
+      if (!DEEP) {
+        if (i + 1 < nchunks) {
+          store(i + 1, A);
+          if (i + 2 < nchunks) load(i + 2, A);
+        }
+      } else if (i + 1 < nchunks) {
+        if ((i & 1) == 0) {
+          store(i + 1, A);
+          if (i + 3 < nchunks) load(i + 3, A);
+        } else {
+          store(i + 1, B);
+          if (i + 3 < nchunks) load(i + 3, B);
+        }
+      }
+      __syncthreads();
+    }
+    if (FUSED) {
+      dev = wave_sum(dev);
+      if (lane == 0) dsum[pw] = dev;
+    }
+    __syncthreads();
+    if (FUSED && threadIdx.x == 256) dev_out[split] = dsum[0] + dsum[1] + dsum[2] + dsum[3];
+  } else {
+    // ============================ consumers ============================
+    const int slot = __builtin_amdgcn_readfirstlane((wv + split) & 3);
+    const int kr = lane >> 4, cc = lane & 15;
+    f32x4 acc[GI_PPW];
+#pragma unroll
+    for (int q = 0; q < GI_PPW; ++q) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[q][e] = 0.f;
+    }
+    auto flush = [&]() __attribute__((always_inline)) {
+#pragma unroll
+      for (int q = 0; q < GI_PPW; ++q) {
+        const int p = slot + 4 * q;
+        if (p < n_pairs) {
+          double* o = out + ((size_t)split * n_pairs + p) * 256;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            o[(4 * kr + e) * 16 + cc] += (double)acc[q][e];
+            acc[q][e] = 0.f;
+          }
+        }
+      }
+    };
+    // the slot switch sits OUTSIDE the chunk loop (one register assignment for
+    // the accumulators); operands of k-step k+1 are loaded from LDS before the
+    // MFMAs of step k are issued (register double-buffer)
+    auto run = [&](auto slot_tag) __attribute__((always_inline)) {
+      constexpr int SL = decltype(slot_tag)::value;
+      __syncthreads();
+      for (int i = 0; i < nchunks; ++i) {
+        const float* Lb = L[i & 1] + kr * S + cc;
+        const float* wb = wr[i & 1] + kr;
+        if (!(fam.dbg & 1)) {
+          float xr[T], xn[T], xw[T];
+          float w = SQW ? 1.f : wb[0];
+#pragma unroll
+          for (int t = 0; t < T; ++t) xr[t] = Lb[16 * t];
+#pragma unroll 2
+          for (int k = 0; k < RC / 4; ++k) {
+            const int kn = k + 1 < RC / 4 ? k + 1 : k;
+            const float wn = SQW ? 1.f : wb[4 * kn];
+#pragma unroll
+            for (int t = 0; t < T; ++t) xn[t] = Lb[4 * kn * S + 16 * t];
+            if (SQW) {
+              gi_mfma_all<T, SL>(std::make_integer_sequence<int, GI_PPW>{}, xr, xr, acc);
+            } else {
+#pragma unroll
+              for (int t = 0; t < T; ++t) xw[t] = w * xr[t];
+              gi_mfma_all<T, SL>(std::make_integer_sequence<int, GI_PPW>{}, xr, xw, acc);
+            }
+#pragma unroll
+            for (int t = 0; t < T; ++t) xr[t] = xn[t];
+            w = wn;
+          }
+        }
+        if ((i & 15) == 15 || i + 1 == nchunks) flush();  // f32 over <= 1024 rows, then f64
+        __syncthreads();
+      }
+    };
+    switch (slot) {
+      case 0: run(std::integral_constant<int, 0>{}); break;
+      case 1: run(std::integral_constant<int, 1>{}); break;
+      case 2: run(std::integral_constant<int, 2>{}); break;
+      default: run(std::integral_constant<int, 3>{}); break;
+    }
+    __syncthreads();
+  }
+}
+
+template <int PP>
+static void gi_launch(bool fused, dim3 grid, hipStream_t s, const float* X, long long N, const int2* pairs,
+                      int n_pairs, int rpb, const float* beta, float b0, const float* y, const float* wprior,
+                      const float* offset, GlmFamArgs fam, const float* Wext, const float* zext, int aug,
+                      double* out, double* dev_out) {
+  if constexpr (PP <= 128 && (PP & (PP - 1)) == 0) {
+    // IRLS weights are >= 0 -> sqrt(W) pre-scaling; caller-signed weights
+    // (e.g. X'r for lambda_max) take the explicit-multiply path
+    if (fused)
+      hipLaunchKernelGGL((glm_irls_ws_kernel<PP, true, true>), dim3(grid.x), dim3(512), 0, s, X, N, n_pairs, rpb,
+                         beta, b0, y, wprior, offset, fam, Wext, zext, aug, out, dev_out);
+    else if (!fam.signed_w)
+      hipLaunchKernelGGL((glm_irls_ws_kernel<PP, false, true>), dim3(grid.x), dim3(512), 0, s, X, N, n_pairs, rpb,
+                         beta, b0, y, wprior, offset, fam, Wext, zext, aug, out, dev_out);
+    else
+      hipLaunchKernelGGL((glm_irls_ws_kernel<PP, false, false>), dim3(grid.x), dim3(512), 0, s, X, N, n_pairs, rpb,
+                         beta, b0, y, wprior, offset, fam, Wext, zext, aug, out, dev_out);
+    return;
+  }
+  if constexpr (GiCfg<PP>::POW2) {
+    if (fused) {
+      hipLaunchKernelGGL((glm_irls_kernel<PP, true>), grid, dim3(256), 0, s, X, N, pairs, n_pairs, rpb, beta, b0, y,
+                         wprior, offset, fam, Wext, zext, aug, out, dev_out);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((glm_irls_kernel<PP, false>), grid, dim3(256), 0, s, X, N, pairs, n_pairs, rpb, beta, b0, y,
+                     wprior, offset, fam, Wext, zext, aug, out, dev_out);
+}
+
+static int gi_dbg() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("H2O3_GI_DBG");
+    v = e ? atoi(e) : 0;
+  }
+  return v;
+}
+
+// rows_per_block must be a multiple of h2o_glm_irls_chunk(P).
+extern "C" int h2o_glm_irls_chunk(int P) {
+  const int r = (8192 / P) / 4 * 4;
+  return P <= 128 ? 64 : (r < 16 ? 16 : r);
+}
+
 extern "C" int h2o_glm_irls(const float* X, long long N, int P, const int* pairs, int n_pairs, int n_splits,
                             int rows_per_block, const float* beta, float b0, const float* y, const float* wprior,
                             const float* offset, int link, int var, float tvp, float theta, const float* Wext,
-                            const float* zext, int aug, double* out, double* dev_out, hipStream_t s) {
+                            const float* zext, int aug, int signed_w, double* out, double* dev_out,
+                            hipStream_t s) {
   if (N <= 0 || n_pairs <= 0) return 0;
   if (P % 32 != 0 || P > 512) return -1;
   if (aug >= 0 && aug + 1 >= P) return -2;
-  const int S = (P % 64 == 0) ? P + 32 : P;
-  const size_t lds = (size_t)GI_RC * S * sizeof(float);
+  if (beta && (P & (P - 1)) != 0) return -3;
+  if (rows_per_block % h2o_glm_irls_chunk(P) != 0) return -4;
   const int groups = (n_pairs + 4 * GI_PPW - 1) / (4 * GI_PPW);
   dim3 grid(n_splits, groups);
-  GlmFamArgs fam{link, var, tvp, theta};
-  if (beta) {
-    hipLaunchKernelGGL(glm_irls_kernel<true>, grid, dim3(256), lds, s, X, N, P, S, (const int2*)pairs, n_pairs,
-                       rows_per_block, beta, b0, y, wprior, offset, fam, Wext, zext, aug, out, dev_out);
-  } else {
-    hipLaunchKernelGGL(glm_irls_kernel<false>, grid, dim3(256), lds, s, X, N, P, S, (const int2*)pairs, n_pairs,
-                       rows_per_block, beta, b0, y, wprior, offset, fam, Wext, zext, aug, out, dev_out);
+  GlmFamArgs fam{link, var, tvp, theta, gi_dbg(), signed_w};
+  const bool fused = beta != nullptr;
+  const int2* pr = (const int2*)pairs;
+#define GI_CASE(pp)                                                                                          \
+  case pp:                                                                                                   \
+    gi_launch<pp>(fused, grid, s, X, N, pr, n_pairs, rows_per_block, beta, b0, y, wprior, offset, fam, Wext, \
+                  zext, aug, out, dev_out);                                                                  \
+    break;
+  switch (P) {
+    GI_CASE(32) GI_CASE(64) GI_CASE(96) GI_CASE(128) GI_CASE(160) GI_CASE(192) GI_CASE(224) GI_CASE(256)
+    GI_CASE(288) GI_CASE(320) GI_CASE(352) GI_CASE(384) GI_CASE(416) GI_CASE(448) GI_CASE(480) GI_CASE(512)
+    default: return -1;
   }
+#undef GI_CASE
   return (int)hipGetLastError();
 }

@@ -20,7 +20,8 @@ def _lib():
         lib.h2o_gram.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_int, ctypes.c_void_p,
                                  ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         P, I, LL, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong, ctypes.c_float
-        lib.h2o_glm_irls.argtypes = [P, LL, I, P, I, I, I, P, F, P, P, P, I, I, F, F, P, P, I, P, P, P]
+        lib.h2o_glm_irls.argtypes = [P, LL, I, P, I, I, I, P, F, P, P, P, I, I, F, F, P, P, I, I, P, P, P]
+        lib.h2o_glm_irls_chunk.argtypes = [I]
         lib._typed = True
     return lib
 
@@ -34,12 +35,13 @@ def _pairs(T, device):
 
 
 def _assemble(tiles, pairs_t, T):
-    """[npairs, 32, 32] upper-triangle tiles -> symmetric [32T, 32T]."""
+    """[npairs, t, t] upper-triangle tiles -> symmetric [tT, tT]."""
+    t = tiles.shape[-1]
     ii, jj = pairs_t[:, 0].long(), pairs_t[:, 1].long()
-    Gb = torch.zeros((T, T, 32, 32), dtype=torch.float64, device=tiles.device)
+    Gb = torch.zeros((T, T, t, t), dtype=torch.float64, device=tiles.device)
     Gb[jj, ii] = tiles.transpose(1, 2)
     Gb[ii, jj] = tiles
-    return Gb.permute(0, 2, 1, 3).reshape(32 * T, 32 * T)
+    return Gb.permute(0, 2, 1, 3).reshape(t * T, t * T)
 
 
 _LINK = {"identity": 0, "logit": 1, "log": 2, "inverse": 3}
@@ -65,11 +67,12 @@ def _ptr(t):
 
 
 def glm_irls(X, aug=-1, beta=None, b0=0.0, y=None, wprior=None, offset=None, codes=(0, 0), tvp=0.0, theta=1e-10,
-             W=None, z=None, target_blocks=1024):
+             W=None, z=None, signed=None, target_blocks=1024):
     """One pass of the fused IRLS kernel (ops/csrc/gram.hip glm_irls_kernel).
 
     Fused mode (beta given): per row eta = x.beta + b0 + offset, the family's
     IRLS weight / working response, deviance.  External mode: W, z given.
+    `signed`: external W may hold negative values (default: checked).
     Returns (G [Pp, Pp] f64 — columns `aug` / `aug+1` hold X'W / X'Wz and
     their cross terms when aug >= 0 — and the f64 deviance, or None).
     """
@@ -77,22 +80,25 @@ def glm_irls(X, aug=-1, beta=None, b0=0.0, y=None, wprior=None, offset=None, cod
     lib = _lib()
     if lib is None:
         raise RuntimeError("gram extension not built (run __graft_entry__.build())")
-    T = P // 32
+    T = P // 16  # 16x16 MFMA tiles
     pairs_t, pr = _pairs(T, X.device)
     npairs = len(pr)
-    groups = -(-npairs // 12)
+    groups = -(-npairs // 36)
     splits = max(1, min(max(1, target_blocks // groups), N // 4096))
     rpb = -(-N // splits)
-    rpb = ((rpb + 63) // 64) * 64
+    rc = lib.h2o_glm_irls_chunk(P)
+    rpb = ((rpb + rc - 1) // rc) * rc
     splits = -(-N // rpb)
-    out = torch.zeros((splits, npairs, 32, 32), dtype=torch.float64, device=X.device)
+    out = torch.zeros((splits, npairs, 16, 16), dtype=torch.float64, device=X.device)
     dev = torch.zeros(splits, dtype=torch.float64, device=X.device)
     X = X.contiguous()
     bt = _f32(beta)
     keep = [_f32(y), _f32(wprior), _f32(offset), _f32(W), _f32(z)]
+    if signed is None:
+        signed = beta is None and keep[3] is not None and bool((keep[3] < 0).any())
     rc = lib.h2o_glm_irls(_ptr(X), N, P, _ptr(pairs_t), npairs, splits, rpb, _ptr(bt), float(b0), _ptr(keep[0]),
                           _ptr(keep[1]), _ptr(keep[2]), int(codes[0]), int(codes[1]), float(tvp), float(theta),
-                          _ptr(keep[3]), _ptr(keep[4]), int(aug), _ptr(out), _ptr(dev),
+                          _ptr(keep[3]), _ptr(keep[4]), int(aug), int(bool(signed)), _ptr(out), _ptr(dev),
                           ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
     if rc != 0:
         raise RuntimeError(f"h2o_glm_irls failed: {rc}")

@@ -24,7 +24,7 @@ def _close(a, b, rtol=2e-4):
 
 @pytest.mark.parametrize("family,link", [("binomial", "logit"), ("poisson", "log"), ("gaussian", "identity"),
                                          ("gamma", "log"), ("tweedie", "log")])
-@pytest.mark.parametrize("P,Pp", [(30, 32), (100, 128), (200, 224)])
+@pytest.mark.parametrize("P,Pp", [(30, 32), (60, 64), (100, 128), (200, 256)])
 def test_glm_irls_fused(family, link, P, Pp):
     n = 50_003
     X, beta, g = _data(n, P, Pp)
@@ -47,7 +47,7 @@ def test_glm_irls_fused(family, link, P, Pp):
 
 
 def test_glm_irls_external_and_gram():
-    n, P, Pp = 77_777, 61, 64
+    n, P, Pp = 77_777, 90, 96
     X, _, g = _data(n, P, Pp, seed=3)
     W = torch.rand(n, generator=g)
     z = torch.randn(n, generator=g)
@@ -59,3 +59,15 @@ def test_glm_irls_external_and_gram():
     assert _close(G2, G2r)
     G3 = linalg_ops.weighted_gram(X[:1000].cuda())
     assert _close(G3, X[:1000].double().T @ X[:1000].double())
+
+
+@pytest.mark.parametrize("signed", [False, True])
+@pytest.mark.parametrize("P,Pp", [(61, 64), (100, 128), (200, 224), (400, 512)])
+def test_glm_irls_external_widths(P, Pp, signed):
+    n = 20_011
+    X, _, g = _data(n, P, Pp, seed=5)
+    W = torch.randn(n, generator=g) if signed else torch.rand(n, generator=g)
+    z = torch.randn(n, generator=g)
+    Gk, _ = linalg_ops.glm_irls(X.cuda(), aug=P, W=W.cuda(), z=z.cuda())
+    Gr, _ = linalg_ops.glm_irls_reference(X, aug=P, W=W, z=z)
+    assert _close(Gk[: P + 2, : P + 2], Gr[: P + 2, : P + 2])
