@@ -1,0 +1,60 @@
+"""Worker for tests/test_distributed.py: one rank of a gloo (CPU) cloud.
+
+Trains the same models on the same data as the single-process run and
+dumps global results (metrics, coefficients, tree structure) to JSON.
+"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def make_df(n=4000, seed=7):
+    import numpy as np
+    import pandas as pd
+    rng = np.random.default_rng(seed)
+    X = rng.normal(size=(n, 6))
+    logit = 1.5 * X[:, 0] - X[:, 1] + 0.5 * X[:, 2] * X[:, 3]
+    y = (rng.random(n) < 1 / (1 + np.exp(-logit))).astype(int)
+    df = pd.DataFrame(X, columns=[f"x{i}" for i in range(6)])
+    df["cat"] = np.where(X[:, 4] > 0, "a", "b")
+    df["yr"] = 2.0 * X[:, 0] + X[:, 5] + rng.normal(scale=0.1, size=n)
+    df["y"] = np.where(y == 1, "yes", "no")
+    return df
+
+
+def run(out_path):
+    import h2o3_amd as h2o
+    from h2o3_amd.estimators import (H2OGeneralizedLinearEstimator, H2OGradientBoostingEstimator,
+                                     H2OKMeansEstimator, H2ORandomForestEstimator)
+    h2o.init(verbose=False)
+    fr = h2o.H2OFrame(make_df())
+    x = [f"x{i}" for i in range(6)] + ["cat"]
+    res = {"nrow": fr.nrow}
+    gbm = H2OGradientBoostingEstimator(ntrees=5, max_depth=4, seed=1, min_rows=5)
+    gbm.train(x=x, y="y", training_frame=fr)
+    res["gbm_auc"] = gbm.auc()
+    res["gbm_logloss"] = gbm.logloss()
+    glm = H2OGeneralizedLinearEstimator(family="binomial", lambda_=0.0)
+    glm.train(x=x, y="y", training_frame=fr)
+    res["glm_coef"] = glm.coef()
+    res["glm_auc"] = glm.auc()
+    glmr = H2OGeneralizedLinearEstimator(family="gaussian", alpha=0.5, lambda_=0.01)
+    glmr.train(x=x, y="yr", training_frame=fr)
+    res["glmr_coef"] = glmr.coef()
+    drf = H2ORandomForestEstimator(ntrees=3, max_depth=5, seed=3, sample_rate=1.0, mtries=7)
+    drf.train(x=x, y="yr", training_frame=fr)
+    res["drf_rmse"] = drf.rmse()
+    km = H2OKMeansEstimator(k=3, seed=5, init="PlusPlus", standardize=True)
+    km.train(x=[f"x{i}" for i in range(6)], training_frame=fr)
+    res["km_tot_withinss"] = km.tot_withinss()
+    from h2o3_amd.parallel import cloud
+    if cloud.rank() == 0:
+        with open(out_path, "w") as f:
+            json.dump(res, f)
+    cloud.barrier()
+
+
+if __name__ == "__main__":
+    run(sys.argv[1])
