@@ -266,3 +266,25 @@ def __getattr__(name):
         from . import grid
         return grid
     raise AttributeError(name)
+
+
+def explain(models, frame, columns=None, top_n_features=5, include_explanations="ALL", exclude_explanations=(),
+            **kw):
+    """h2o.explain(): returns the explanation tables (no plotting stack here)."""
+    from .models.explain import explain as _ex
+    if hasattr(models, "leaderboard") and not isinstance(models, (list, tuple)):
+        models = list(models._models) if hasattr(models, "_models") else [models.leader]
+    return _ex(models, frame, columns=columns, top_n_features=top_n_features,
+               include_explanations=include_explanations, exclude_explanations=exclude_explanations)
+
+
+def explain_row(models, frame, row_index, columns=None, top_n_features=5, **kw):
+    from .models.explain import explain_row as _er
+    if hasattr(models, "leader") and not isinstance(models, (list, tuple)):
+        models = [models.leader]
+    return _er(models, frame, row_index, columns=columns, top_n_features=top_n_features)
+
+
+def permutation_importance(model, frame, metric="AUTO", n_samples=10000, n_repeats=1, features=None, seed=-1,
+                           use_pandas=True):
+    return model.permutation_importance(frame, metric, n_samples, n_repeats, features, seed)

@@ -517,6 +517,32 @@ class H2OEstimator:
         return s
 
     # ------------------------------------------------------------ persistence
+    # ---------------------------------------------------------------- explain
+    def partial_plot(self, data, cols=None, destination_key=None, nbins=20, weight_column=None, plot=False,
+                     plot_stddev=True, figsize=None, server=False, include_na=False, user_splits=None,
+                     col_pairs_2dpdp=None, save_to_file=None, row_index=None, targets=None, **kw):
+        from .explain import partial_dependence
+        return partial_dependence(self, data, cols or [], nbins=nbins, weight_column=weight_column,
+                                  include_na=include_na, user_splits=user_splits, targets=targets,
+                                  row_index=row_index)
+
+    def permutation_importance(self, frame, metric="AUTO", n_samples=10000, n_repeats=1, features=None, seed=-1,
+                               use_pandas=True):
+        from .explain import permutation_importance
+        return permutation_importance(self, frame, metric, n_samples, n_repeats, features, seed)
+
+    def h(self, frame, variables):
+        from .explain import h_statistic
+        return h_statistic(self, frame, variables)
+
+    def explain(self, frame, **kw):
+        from .explain import explain
+        return explain(self, frame, **kw)
+
+    def explain_row(self, frame, row_index, **kw):
+        from .explain import explain_row
+        return explain_row(self, frame, row_index, **kw)
+
     def download_mojo(self, path=".", get_genmodel_jar=False, genmodel_name="", **kw):
         from ..mojo import writer
         return writer.write_mojo(self, path)

@@ -162,6 +162,11 @@ class H2ORandomForestEstimator(SharedTreeEstimator):
             out = torch.stack([1 - p1, p1], 1)
         return out
 
+    def predict_contributions(self, test_data, output_format="Original", top_n=None, bottom_n=None,
+                              compare_abs=False, background_frame=None):
+        from .shap import tree_contributions
+        return tree_contributions(self, test_data, top_n=top_n, bottom_n=bottom_n, compare_abs=compare_abs)
+
     def _score_all(self, spec):
         raw = self._predict_raw(spec.frame)
         if getattr(self, "_oob_raw", None) is not None and not getattr(self, "_in_cv", False):

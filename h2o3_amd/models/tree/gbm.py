@@ -426,7 +426,7 @@ class H2OGradientBoostingEstimator(SharedTreeEstimator):
     def predict_contributions(self, test_data, output_format="Original", top_n=None, bottom_n=None,
                               compare_abs=False, background_frame=None):
         from .shap import tree_contributions
-        return tree_contributions(self, test_data)
+        return tree_contributions(self, test_data, top_n=top_n, bottom_n=bottom_n, compare_abs=compare_abs)
 
 
 def _weighted_quantile(x, w, q):
