@@ -10,3 +10,6 @@ from ..models.deeplearning import H2ODeepLearningEstimator  # noqa: F401
 H2OAutoEncoderEstimator = H2ODeepLearningEstimator
 from ..models.ensemble import H2OStackedEnsembleEstimator  # noqa: F401
 from ..models.generic import H2OGenericEstimator  # noqa: F401
+from ..models.isotonic import H2OIsotonicRegressionEstimator  # noqa: F401
+from ..models.targetencoder import H2OTargetEncoderEstimator  # noqa: F401
+from ..models.aggregator import H2OAggregatorEstimator  # noqa: F401
