@@ -14,3 +14,4 @@ from ..models.isotonic import H2OIsotonicRegressionEstimator  # noqa: F401
 from ..models.targetencoder import H2OTargetEncoderEstimator  # noqa: F401
 from ..models.aggregator import H2OAggregatorEstimator  # noqa: F401
 from ..models.coxph import H2OCoxProportionalHazardsEstimator  # noqa: F401
+from ..models.glrm import H2OGeneralizedLowRankEstimator  # noqa: F401

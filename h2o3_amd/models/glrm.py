@@ -1,0 +1,402 @@
+"""Generalized Low Rank Models.
+
+Reference: hex/glrm/GLRM.java + GLRMModel.java + hex/genmodel/algos/glrm
+(GlrmLoss: Quadratic, Absolute, Huber, Poisson, Hinge, Logistic,
+Periodic; multi-losses Categorical / Ordinal for enum columns;
+GlrmRegularizer: None, Quadratic, L2, L1, NonNegative, OneSparse,
+UnitOneSparse, Simplex; alternating proximal gradient on X and Y with the
+reference's step rule: grow 1.05x after an improving step, halve and
+retry otherwise; init Random / SVD / PlusPlus / User; transform of the
+numeric columns; archetypes Y, representation frame X, reconstruction =
+predict, `impute_original` undoes the transform).
+
+MI355X design: A (n x p_expanded, one-hot enum blocks), X (n x k) and Y
+(k x p) all live on the device; each half-iteration is two GEMMs (X Y and
+the gradient products) plus fused elementwise loss gradients obtained
+from torch autograd over the masked loss -- no per-row loops.  Row
+shards stay local (X is row-sharded like the data); the Y gradient is an
+all-reduce of a k x p matrix.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import pandas as pd
+import torch
+
+from ..core.frame import H2OFrame
+from ..core.vec import T_ENUM, T_REAL, Vec
+from ..parallel import cloud
+from ..parallel import collectives as coll
+from .base import H2OEstimator
+
+GLRM_DEFAULTS = dict(k=1, loss="Quadratic", loss_by_col=None, loss_by_col_idx=None, multi_loss="Categorical",
+                     period=1, regularization_x="None", regularization_y="None", gamma_x=0.0, gamma_y=0.0,
+                     max_iterations=1000, max_updates=2000, init_step_size=1.0, min_step_size=1e-4, seed=-1,
+                     init="PlusPlus", svd_method="Randomized", user_y=None, user_x=None, expand_user_y=True,
+                     impute_original=False, recover_svd=False, transform="NONE", representation_name=None)
+
+
+def _num_loss(name, a, u, period):
+    n = name.lower()
+    if n == "quadratic":
+        return (a - u) ** 2
+    if n == "absolute":
+        return (a - u).abs()
+    if n == "huber":
+        d = (a - u).abs()
+        return torch.where(d <= 1, 0.5 * d * d, d - 0.5)
+    if n == "poisson":
+        return torch.exp(u) - a * u + torch.where(a > 0, a * torch.log(a.clamp_min(1e-300)) - a, torch.zeros_like(a))
+    if n == "hinge":
+        aa = torch.where(a > 0, torch.ones_like(a), -torch.ones_like(a))
+        return torch.clamp(1 - aa * u, min=0)
+    if n == "logistic":
+        aa = torch.where(a > 0, torch.ones_like(a), -torch.ones_like(a))
+        return torch.nn.functional.softplus(-aa * u)
+    if n == "periodic":
+        return 1 - torch.cos((a - u) * (2 * math.pi / period))
+    raise ValueError(f"unknown loss {name}")
+
+
+def _reg(name, M):
+    n = (name or "None").lower()
+    if n == "none" or n == "nonnegative" or n in ("onesparse", "unitonesparse", "simplex"):
+        return M.new_zeros(())
+    if n == "quadratic":
+        return (M * M).sum()
+    if n == "l2":
+        return torch.sqrt((M * M).sum(1)).sum()
+    if n == "l1":
+        return M.abs().sum()
+    raise ValueError(f"unknown regularizer {name}")
+
+
+def _prox(name, M, step_gamma):
+    n = (name or "None").lower()
+    if n == "none":
+        return M
+    if n == "quadratic":
+        return M / (1 + 2 * step_gamma)
+    if n == "l2":
+        nr = torch.sqrt((M * M).sum(1, keepdim=True)).clamp_min(1e-300)
+        return M * torch.clamp(1 - step_gamma / nr, min=0)
+    if n == "l1":
+        return torch.sign(M) * torch.clamp(M.abs() - step_gamma, min=0)
+    if n == "nonnegative":
+        return M.clamp_min(0)
+    if n == "onesparse":
+        idx = M.argmax(1, keepdim=True)
+        out = torch.zeros_like(M)
+        out.scatter_(1, idx, M.gather(1, idx).clamp_min(0))
+        return out
+    if n == "unitonesparse":
+        idx = M.argmax(1, keepdim=True)
+        return torch.zeros_like(M).scatter_(1, idx, 1.0)
+    if n == "simplex":  # Euclidean projection onto the probability simplex (row-wise)
+        u, _ = torch.sort(M, 1, descending=True)
+        css = torch.cumsum(u, 1) - 1
+        ind = torch.arange(1, M.shape[1] + 1, device=M.device, dtype=M.dtype)
+        cond = u - css / ind > 0
+        rho = cond.to(torch.int64).cumsum(1).argmax(1, keepdim=True)
+        theta = css.gather(1, rho) / (rho + 1).to(M.dtype)
+        return torch.clamp(M - theta, min=0)
+    raise ValueError(f"unknown regularizer {name}")
+
+
+class H2OGeneralizedLowRankEstimator(H2OEstimator):
+    algo = "glrm"
+    supervised_learning = False
+    _defaults = GLRM_DEFAULTS
+
+    # ------------------------------------------------------------ data layout
+    def _layout(self, frame, cols, fit=False):
+        p = self._parms
+        blocks, mats, masks = [], [], []
+        dev = cloud.device()
+        if fit:
+            self._stats = {}
+        for c in cols:
+            v = frame.vec(c)
+            if v.type == T_ENUM or (not fit and c in self._doms):
+                dom = self._doms[c] if not fit else list(v.domain)
+                if fit:
+                    self._doms[c] = dom
+                codes = self._adapt_enum(v, dom).long() if not fit else v.data.long()
+                oh = torch.zeros((frame.nlocal, len(dom)), dtype=torch.float32, device=dev)
+                okr = codes >= 0
+                oh[torch.nonzero(okr).view(-1), codes[okr]] = 1.0
+                mats.append(oh)
+                masks.append(okr.view(-1, 1).expand(-1, len(dom)))
+                blocks.append(("cat", c, len(dom)))
+            else:
+                x = v.as_float(torch.float32)
+                if fit:
+                    okx = ~torch.isnan(x)
+                    s = torch.stack([x[okx].sum().double(), (x[okx].double() ** 2).sum(), okx.sum().double(),
+                                     torch.where(okx, x, torch.full_like(x, float("inf"))).min().double(),
+                                     torch.where(okx, x, torch.full_like(x, -float("inf"))).max().double()])
+                    s3, lo_, hi_ = s[:3].clone(), s[3:4].clone(), s[4:5].clone()
+                    coll.allreduce_(s3)
+                    coll.allreduce_(lo_, "min")
+                    coll.allreduce_(hi_, "max")
+                    s = torch.cat([s3, lo_, hi_])
+                    mu = float(s[0] / s[2])
+                    sd = math.sqrt(max(float(s[1] / s[2]) - mu * mu, 0) * float(s[2]) / max(float(s[2]) - 1, 1))
+                    self._stats[c] = (mu, sd if sd > 0 else 1.0, float(s[3]), float(s[4]))
+                mu, sd, lo, hi = self._stats[c]
+                tr = str(p.get("transform") or "NONE").upper()
+                if tr == "STANDARDIZE":
+                    x = (x - mu) / sd
+                elif tr == "NORMALIZE":
+                    x = (x - lo) / max(hi - lo, 1e-12)
+                elif tr == "DEMEAN":
+                    x = x - mu
+                elif tr == "DESCALE":
+                    x = x / sd
+                m = ~torch.isnan(x)
+                mats.append(torch.nan_to_num(x).view(-1, 1))
+                masks.append(m.view(-1, 1))
+                blocks.append(("num", c, 1))
+        A = torch.cat(mats, 1) if mats else torch.zeros((frame.nlocal, 0), device=dev)
+        M = torch.cat(masks, 1).to(torch.float32) if masks else torch.zeros_like(A)
+        return A, M, blocks
+
+    def _loss(self, A, M, U, blocks):
+        p = self._parms
+        lbc = {}
+        if p.get("loss_by_col"):
+            idx = p.get("loss_by_col_idx") or []
+            for name, i in zip(p["loss_by_col"], idx):
+                lbc[self._cols[i] if isinstance(i, int) else i] = name
+        tot = U.new_zeros(())
+        j = 0
+        ml = str(p.get("multi_loss") or "Categorical").lower()
+        for kind, c, w in blocks:
+            a, m, u = A[:, j:j + w], M[:, j:j + w], U[:, j:j + w]
+            if kind == "num":
+                L = _num_loss(lbc.get(c, p.get("loss") or "Quadratic"), a, u, float(p.get("period", 1)))
+                tot = tot + (L * m).sum()
+            else:
+                rowm = m[:, 0]
+                if ml == "ordinal":
+                    lvl = a.argmax(1, keepdim=True)
+                    ar = torch.arange(w, device=a.device).view(1, -1)
+                    L = torch.where(ar < lvl, torch.clamp(1 - u, min=0), torch.clamp(1 + u, min=0))
+                else:  # Categorical one-vs-all hinge
+                    L = torch.where(a > 0, torch.clamp(1 - u, min=0), torch.clamp(1 + u, min=0))
+                tot = tot + (L.sum(1) * rowm).sum()
+            j += w
+        return tot
+
+    # ------------------------------------------------------------ fit
+    def _fit(self, spec):
+        p = self._parms
+        self._doms = {}
+        self._cols = list(spec.x)
+        A, M, blocks = self._layout(spec.frame, self._cols, fit=True)
+        self._blocks = blocks
+        n, P = A.shape
+        k = int(p.get("k", 1))
+        seed = p.get("seed", -1)
+        g = torch.Generator(device="cpu").manual_seed(int(seed) if seed not in (-1, None) else 12345)
+        init = str(p.get("init") or "PlusPlus").lower()
+        if p.get("user_y") is not None:
+            Y = torch.as_tensor(np.asarray(p["user_y"].as_data_frame().values if hasattr(p["user_y"], "as_data_frame")
+                                           else p["user_y"], dtype=np.float32), device=A.device)
+        elif init == "svd":
+            U_, S_, V_ = torch.linalg.svd(A * M, full_matrices=False)
+            Y = (S_[:k].view(-1, 1) * V_[:k]) / math.sqrt(max(n, 1))
+        elif init == "plusplus":
+            # k-means++ seeded archetypes from data rows
+            idx = [int(torch.randint(n, (1,), generator=g))]
+            d2 = ((A - A[idx[0]]) ** 2).sum(1)
+            for _ in range(1, k):
+                pr = (d2 / d2.sum().clamp_min(1e-30)).cpu()
+                i = int(torch.multinomial(pr, 1, generator=g)) if float(d2.sum()) > 0 else int(torch.randint(n, (1,), generator=g))
+                idx.append(i)
+                d2 = torch.minimum(d2, ((A - A[i]) ** 2).sum(1))
+            Y = A[idx].clone()
+        else:
+            Y = torch.randn((k, P), generator=g).to(A.device)
+        if Y.shape[0] < k:
+            Y = torch.cat([Y, torch.randn((k - Y.shape[0], P), generator=g).to(A.device) * 0.01], 0)
+        X = self._init_x(A, M, Y, g)
+        gx, gy = float(p.get("gamma_x", 0.0)), float(p.get("gamma_y", 0.0))
+        rx, ry = p.get("regularization_x"), p.get("regularization_y")
+
+        def objective(X_, Y_):
+            return float(self._loss(A, M, X_ @ Y_, blocks)) + gx * float(_reg(rx, X_)) + gy * float(_reg(ry, Y_))
+
+        step = float(p.get("init_step_size", 1.0))
+        min_step = float(p.get("min_step_size", 1e-4))
+        obj = objective(X, Y)
+        hist = [obj]
+        it = 0
+        updates = 0
+        scale = 1.0 / max(n, 1)
+        max_it, max_up = int(p.get("max_iterations", 1000)), int(p.get("max_updates", 2000))
+        while it < max_it and updates < max_up and step >= min_step:
+            it += 1
+            # X update
+            Xv = X.clone().requires_grad_(True)
+            Lx = self._loss(A, M, Xv @ Y, blocks)
+            gX, = torch.autograd.grad(Lx, Xv)
+            Xn = _prox(rx, X - step * scale * gX, step * scale * gx)
+            # Y update
+            Yv = Y.clone().requires_grad_(True)
+            Ly = self._loss(A, M, Xn @ Yv, blocks)
+            gY, = torch.autograd.grad(Ly, Yv)
+            coll.allreduce_(gY)
+            Yn = _prox(ry, Y - step * scale * gY, step * scale * gy)
+            on = objective(Xn, Yn)
+            updates += 1
+            if on < obj:
+                rel = (obj - on) / max(abs(obj), 1e-300)
+                X, Y, obj = Xn, Yn, on
+                step *= 1.05
+                hist.append(obj)
+                if rel < 1e-8:
+                    break
+            else:
+                step /= 2
+        self._X, self._Y = X, Y
+        self._step = step
+        o = self._output
+        o["objective"] = obj
+        o["iterations"] = it
+        o["updates"] = updates
+        o["step_size"] = step
+        o["archetypes"] = self._archetypes_df()
+        o["scoring_history"] = hist
+        rep = p.get("representation_name") or f"GLRMLoading_{self.model_id}"
+        self._rep_name = rep
+        if p.get("recover_svd"):
+            Q, R = torch.linalg.qr(X.double())
+            U2, S2, V2 = torch.linalg.svd(R @ Y.double(), full_matrices=False)
+            o["singular_vals"] = S2.cpu().numpy()
+            o["eigenvectors"] = V2.T.cpu().numpy()
+        from ..core import dkv
+        dkv.put(rep, self.representation_frame())
+
+    def _init_x(self, A, M, Y, g):
+        # least squares start: X = A Y^T (Y Y^T)^-1 (quadratic-loss optimum for fixed Y)
+        k = Y.shape[0]
+        G = Y @ Y.T + 1e-6 * torch.eye(k, device=Y.device)
+        return torch.linalg.solve(G, Y @ (A * M).T).T.contiguous()
+
+    def _archetypes_df(self):
+        names = []
+        for kind, c, w in self._blocks:
+            if kind == "num":
+                names.append(c)
+            else:
+                names += [f"{c}.{d}" for d in self._doms[c]]
+        Y = self._Y.detach().cpu().numpy()
+        df = pd.DataFrame(Y, columns=names)
+        df.insert(0, "archetype", [f"Arch{i + 1}" for i in range(Y.shape[0])])
+        return df
+
+    def archetypes(self):
+        return self._output["archetypes"].drop(columns=["archetype"]).values
+
+    def representation_frame(self):
+        X = self._X.detach()
+        return H2OFrame.from_vecs([Vec(X[:, i].contiguous().to(torch.float32), T_REAL) for i in range(X.shape[1])],
+                                  [f"Arch{i + 1}" for i in range(X.shape[1])])
+
+    # ------------------------------------------------------------ scoring
+    def _solve_x(self, frame, iters=2000):
+        A, M, blocks = self._layout(frame, self._cols)
+        Y = self._Y.detach()
+        p = self._parms
+        rx, gx = p.get("regularization_x"), float(p.get("gamma_x", 0.0))
+        scale = 1.0 / max(A.shape[0], 1)
+        # start from the regularizer-feasible least-squares point with the
+        # training run's final (adapted) step size
+        X = _prox(rx, self._init_x(A, M, Y, None), 0.0)
+        step = max(float(getattr(self, "_step", 1.0)), 1e-3) * 4
+        obj = float(self._loss(A, M, X @ Y, blocks)) + gx * float(_reg(rx, X))
+        for _ in range(iters):
+            Xv = X.clone().requires_grad_(True)
+            gX, = torch.autograd.grad(self._loss(A, M, Xv @ Y, blocks), Xv)
+            Xn = _prox(rx, X - step * scale * gX, step * scale * gx)
+            on = float(self._loss(A, M, Xn @ Y, blocks)) + gx * float(_reg(rx, Xn))
+            if on < obj:
+                rel = (obj - on) / max(abs(obj), 1e-300)
+                X, obj, step = Xn, on, step * 1.05
+                if rel < 1e-9:
+                    break
+            else:
+                step /= 2
+                if step < 1e-8:
+                    break
+        return X, A, M
+
+    def _reconstruct(self, X):
+        p = self._parms
+        U = (X @ self._Y).detach()
+        vecs, names = [], []
+        j = 0
+        tr = str(p.get("transform") or "NONE").upper()
+        for kind, c, w in self._blocks:
+            u = U[:, j:j + w]
+            if kind == "num":
+                x = u[:, 0]
+                if p.get("impute_original"):
+                    mu, sd, lo, hi = self._stats[c]
+                    if tr == "STANDARDIZE":
+                        x = x * sd + mu
+                    elif tr == "NORMALIZE":
+                        x = x * (hi - lo) + lo
+                    elif tr == "DEMEAN":
+                        x = x + mu
+                    elif tr == "DESCALE":
+                        x = x * sd
+                vecs.append(Vec(x.contiguous().to(torch.float32), T_REAL))
+            else:
+                vecs.append(Vec(u.argmax(1).to(torch.int32), T_ENUM, self._doms[c]))
+            names.append(f"reconstr_{c}")
+            j += w
+        return H2OFrame.from_vecs(vecs, names)
+
+    def predict(self, test_data, **kw):
+        X, _, _ = self._solve_x(test_data)
+        return self._reconstruct(X)
+
+    def reconstruct(self, test_data, reverse_transform=False):
+        old = self._parms.get("impute_original")
+        self._parms["impute_original"] = reverse_transform
+        try:
+            return self.predict(test_data)
+        finally:
+            self._parms["impute_original"] = old
+
+    def transform_frame(self, test_data):
+        X, _, _ = self._solve_x(test_data)
+        return H2OFrame.from_vecs([Vec(X[:, i].contiguous(), T_REAL) for i in range(X.shape[1])],
+                                  [f"Arch{i + 1}" for i in range(X.shape[1])])
+
+    def _predict_raw(self, frame):
+        X, _, _ = self._solve_x(frame)
+        return (X @ self._Y).detach()
+
+    def _score_all(self, spec):
+        from . import metrics as mm
+        A, M, blocks = self._layout(spec.frame, self._cols)
+        U = (self._X @ self._Y).detach()
+        num = torch.tensor(0.0, device=U.device)
+        cat = torch.tensor(0.0, device=U.device)
+        j = 0
+        for kind, c, w in blocks:
+            if kind == "num":
+                num = num + (((A[:, j] - U[:, j]) ** 2) * M[:, j]).sum()
+            else:
+                pred = U[:, j:j + w].argmax(1)
+                truth = A[:, j:j + w].argmax(1)
+                cat = cat + ((pred != truth) & (M[:, j] > 0)).sum()
+            j += w
+        m = mm.ModelMetrics(numerr=float(num), caterr=float(cat), objective=self._output["objective"])
+        m.kind = "glrm"
+        self._training_metrics = m
