@@ -16,3 +16,4 @@ from ..models.aggregator import H2OAggregatorEstimator  # noqa: F401
 from ..models.coxph import H2OCoxProportionalHazardsEstimator  # noqa: F401
 from ..models.glrm import H2OGeneralizedLowRankEstimator  # noqa: F401
 from ..models.word2vec import H2OWord2vecEstimator  # noqa: F401
+from ..models.psvm import H2OSupportVectorMachineEstimator  # noqa: F401
