@@ -1,0 +1,219 @@
+"""RuleFit (Friedman & Popescu 2008).
+
+Reference: hex/rulefit/RuleFit.java, RuleFitModel.java, Rule.java,
+Condition.java, RuleEnsemble.java (tree ensembles of depths
+min_rule_length..max_rule_length generate candidate rules -- every
+non-root node is the conjunction of the conditions on its path -- rules
+become 0/1 features, optional linear terms are added, a sparse (lasso)
+GLM selects rules; rule_importance lists coefficient, support and rule
+text; remove_duplicates drops rules with identical support patterns).
+
+MI355X design: rule features are never evaluated condition-by-condition:
+the scoring kernel gives the leaf of every row in every tree, and a node's
+rule indicator is "leaf lies in the node's subtree", i.e. one gather
+through a [n_leaves, n_nodes] ancestor table per tree.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import pandas as pd
+import torch
+
+from ..core.frame import H2OFrame
+from ..core.vec import T_ENUM, T_INT, T_REAL, Vec
+from ..parallel import cloud
+from .base import H2OEstimator
+
+RULEFIT_DEFAULTS = dict(algorithm="AUTO", min_rule_length=3, max_rule_length=3, max_num_rules=-1,
+                        model_type="RULES_AND_LINEAR", rule_generation_ntrees=50, remove_duplicates=True,
+                        lambda_=None, distribution="AUTO", seed=-1, weights_column=None, max_categorical_levels=10)
+
+
+def _cond_text(tree, j, left, names, domains):
+    f = names[tree.feat[j]]
+    na = tree.na_left[j] == left
+    if tree.is_cat[j] and tree.cat_left[j] is not None:
+        dom = domains.get(f, [])
+        mask = tree.cat_left[j]
+        lv = [dom[i] for i in range(min(len(dom), len(mask))) if bool(mask[i]) == left]
+        s = f"({f} in {{{', '.join(map(str, lv))}}}"
+    else:
+        s = f"({f} {'<' if left else '>='} {float(tree.thr[j]):.6g}"
+    return s + (f" or {f} is NA)" if na else ")")
+
+
+class H2ORuleFitEstimator(H2OEstimator):
+    algo = "rulefit"
+    _defaults = RULEFIT_DEFAULTS
+
+    def _wants_categorical_response(self):
+        return str(self._parms.get("distribution") or "").lower() in ("bernoulli", "multinomial")
+
+    def _tree_models(self, spec):
+        from .tree.drf import H2ORandomForestEstimator
+        from .tree.gbm import H2OGradientBoostingEstimator
+        p = self._parms
+        algo = str(p.get("algorithm") or "AUTO").upper()
+        lo, hi = int(p.get("min_rule_length", 3)), int(p.get("max_rule_length", 3))
+        depths = list(range(lo, hi + 1))
+        nt = max(1, int(p.get("rule_generation_ntrees", 50)) // len(depths))
+        seed = p.get("seed", -1)
+        models = []
+        for d in depths:
+            kw = dict(ntrees=nt, max_depth=d, seed=seed if seed not in (-1, None) else 1234 + d)
+            if algo == "GBM":
+                m = H2OGradientBoostingEstimator(**kw, learn_rate=0.1)
+            else:
+                m = H2ORandomForestEstimator(**kw)
+            m.train(x=list(spec.x), y=spec.y, training_frame=spec.frame, weights_column=spec.weights_column)
+            models.append(m)
+        return models
+
+    def _rules(self):
+        """Enumerate rules: list of (model idx, tree idx, node id, text, length)."""
+        out = []
+        for mi, m in enumerate(self._trees):
+            names = list(m._spec.x)
+            doms = getattr(m, "_x_domains", {})
+            for ti, t in enumerate(m._forest.trees):
+                # path conditions per node
+                conds = {0: []}
+                stack = [0]
+                while stack:
+                    j = stack.pop()
+                    if t.left[j] < 0:
+                        continue
+                    for child, left in ((t.left[j], True), (t.right[j], False)):
+                        conds[child] = conds[j] + [_cond_text(t, j, left, names, doms)]
+                        stack.append(child)
+                for j, c in conds.items():
+                    if j == 0:
+                        continue
+                    out.append((mi, ti, j, " & ".join(c), len(c)))
+        return out
+
+    def _rule_matrix(self, frame):
+        cols = []
+        for mi, m in enumerate(self._trees):
+            X = m._score_matrix(frame)
+            leaf = m._forest.predict(X, m._n_tree_classes(), leaf=True).long()   # [n, T]
+            for ti, t in enumerate(m._forest.trees):
+                anc = self._anc[(mi, ti)]                                          # [n_nodes, n_nodes] bool
+                cols.append(anc[leaf[:, ti]])                                      # [n, n_nodes]
+        full = torch.cat(cols, 1) if cols else torch.zeros((frame.nlocal, 0), dtype=torch.bool)
+        return full[:, self._keep_cols]
+
+    def _fit(self, spec):
+        from .glm.glm import H2OGeneralizedLinearEstimator
+        p = self._parms
+        self._trees = self._tree_models(spec)
+        # ancestor tables: anc[leaf, node] = node on the path root->leaf
+        self._anc = {}
+        offsets = []
+        base = 0
+        for mi, m in enumerate(self._trees):
+            for ti, t in enumerate(m._forest.trees):
+                nn = t.n_nodes
+                A = torch.zeros((nn, nn), dtype=torch.bool)
+                par = {}
+                for j in range(nn):
+                    if t.left[j] >= 0:
+                        par[t.left[j]] = j
+                        par[t.right[j]] = j
+                for j in range(nn):
+                    k = j
+                    while k in par:
+                        A[j, k] = True
+                        k = par[k]
+                # column 0 (root) is not a rule
+                A[:, 0] = False
+                self._anc[(mi, ti)] = A.to(cloud.device())
+                offsets.append((mi, ti, base, nn))
+                base += nn
+        rules = self._rules()
+        col_of = {(mi, ti): b for mi, ti, b, _ in offsets}
+        idx = [col_of[(mi, ti)] + j for mi, ti, j, _, _ in rules]
+        self._keep_cols = torch.as_tensor(idx, dtype=torch.long, device=cloud.device())
+        R = self._rule_matrix(spec.frame)
+        texts = [r[3] for r in rules]
+        if p.get("remove_duplicates", True) and R.shape[1]:
+            # identical support patterns (hash of the packed column) -> keep the shortest rule
+            Rh = R.to(torch.float64)
+            g = torch.Generator(device="cpu").manual_seed(7)
+            g.manual_seed(7 + 1000003 * cloud.rank())
+            proj = Rh.T @ torch.rand(R.shape[0], 2, generator=g, dtype=torch.float64).to(Rh.device)
+            from ..parallel import collectives as coll
+            coll.allreduce_(proj)  # same keys on every rank
+            keys = [(round(float(a), 9), round(float(b), 9)) for a, b in proj.cpu().tolist()]
+            seen = {}
+            for i, k in enumerate(keys):
+                if k not in seen or rules[i][4] < rules[seen[k]][4]:
+                    seen[k] = i
+            keep = sorted(seen.values())
+            R = R[:, keep]
+            texts = [texts[i] for i in keep]
+            self._keep_cols = self._keep_cols[torch.as_tensor(keep, device=self._keep_cols.device)]
+        self._rule_texts = texts
+        mtype = str(p.get("model_type") or "RULES_AND_LINEAR").upper()
+        fr = self._design(spec.frame, R, mtype)
+        self._rule_names = [f"rule_{i}" for i in range(R.shape[1])]
+        glm_kw = dict(alpha=1.0, lambda_search=p.get("lambda_") is None, seed=p.get("seed", -1))
+        if p.get("lambda_") is not None:
+            glm_kw["lambda_"] = p["lambda_"]
+        dist = str(p.get("distribution") or "AUTO").lower()
+        if spec.nclasses == 2:
+            glm_kw["family"] = "binomial"
+        elif spec.nclasses > 2:
+            glm_kw["family"] = "multinomial"
+        elif dist not in ("auto", "gaussian"):
+            glm_kw["family"] = dist
+        self._glm = H2OGeneralizedLinearEstimator(**glm_kw)
+        xs = [c for c in fr.names if c != spec.y]
+        self._glm.train(x=xs, y=spec.y, training_frame=fr)
+        self._mtype = mtype
+        # rule importance table
+        coef = self._glm.coef() if spec.nclasses <= 2 else {}
+        rows = []
+        sup = R.to(torch.float64).mean(0).cpu().numpy() if R.shape[1] else np.zeros(0)
+        for i, nm in enumerate(self._rule_names):
+            c = coef.get(nm, 0.0)
+            if c != 0.0:
+                rows.append((nm, c, float(sup[i]), texts[i]))
+        if mtype != "RULES":
+            for x in spec.x:
+                for k, v in coef.items():
+                    if (k == f"linear.{x}" or k.startswith(f"linear.{x}.")) and v != 0.0:
+                        rows.append((k, v, 1.0, k))
+        rows.sort(key=lambda r: -abs(r[1]))
+        self._output["rule_importance"] = pd.DataFrame(rows, columns=["variable", "coefficient", "support", "rule"])
+
+    def _design(self, frame, R, mtype):
+        vecs, names = [], []
+        if mtype in ("RULES_AND_LINEAR", "RULES"):
+            for i in range(R.shape[1]):
+                vecs.append(Vec(R[:, i].to(torch.float32).contiguous(), T_INT))
+                names.append(f"rule_{i}")
+        if mtype in ("RULES_AND_LINEAR", "LINEAR"):
+            for x in self._spec.x:
+                v = frame.vec(x)
+                vecs.append(v)
+                names.append(f"linear.{x}")
+        if self._spec.y in frame.names:
+            vecs.append(frame.vec(self._spec.y))
+            names.append(self._spec.y)
+        return H2OFrame.from_vecs(vecs, names)
+
+    def rule_importance(self):
+        return self._output["rule_importance"]
+
+    def predict_rules(self, frame, rule_ids):
+        R = self._rule_matrix(frame)
+        ids = [int(r.split("_")[1]) for r in rule_ids]
+        return H2OFrame.from_vecs([Vec(R[:, i].to(torch.float32).contiguous(), T_INT) for i in ids], list(rule_ids))
+
+    def _predict_raw(self, frame):
+        R = self._rule_matrix(frame)
+        fr = self._design(frame, R, self._mtype)
+        return self._glm._predict_raw(fr)
