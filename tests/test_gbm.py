@@ -41,7 +41,7 @@ def test_gbm_regression_and_training_scoring_consistent():
     assert m.r2() > 0.9
     Xs = m._score_matrix(fr)
     f_score = m._forest.predict(Xs, 1)[:, 0] + m._init_f[0]
-    np.testing.assert_allclose(m._train_f[:, 0].numpy(), f_score.numpy(), rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(m._train_f[:, 0].cpu().numpy(), f_score.cpu().numpy(), rtol=1e-4, atol=1e-4)
 
 
 def test_gbm_multinomial():

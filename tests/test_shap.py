@@ -54,7 +54,7 @@ def test_tree_shap_matches_exact_shapley():
     for t in m._forest.trees[:2]:
         for r in (0, 5, 17):
             xr = X[:, r:r + 1]
-            phi = forest_contributions([t], xr, F)[0].numpy()
+            phi = forest_contributions([t], xr, F)[0].cpu().numpy()
             ex = _exact_shap(t, xr, F)
             np.testing.assert_allclose(phi[:-1], ex, atol=1e-6)
 
