@@ -18,3 +18,4 @@ from ..models.glrm import H2OGeneralizedLowRankEstimator  # noqa: F401
 from ..models.word2vec import H2OWord2vecEstimator  # noqa: F401
 from ..models.psvm import H2OSupportVectorMachineEstimator  # noqa: F401
 from ..models.rulefit import H2ORuleFitEstimator  # noqa: F401
+from ..models.glm.gam import H2OGeneralizedAdditiveEstimator  # noqa: F401

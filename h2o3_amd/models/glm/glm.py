@@ -170,6 +170,10 @@ def _solve_quadratic(G, b, l1, l2, intercept, beta0=None, non_negative=False, ma
     pen = np.ones(P) if penalty_mask is None else penalty_mask.astype(float)
     if intercept:
         pen[-1] = 0.0
+    nn = np.asarray(non_negative, dtype=bool) if np.ndim(non_negative) else np.full(P, bool(non_negative))
+    if intercept:
+        nn[-1] = False
+    non_negative = bool(nn.any())
     if l1 == 0 and not non_negative:
         A = G + np.diag(l2 * pen + 1e-10 * np.maximum(np.diag(G), 1e-12) * 0)
         try:
@@ -188,7 +192,7 @@ def _solve_quadratic(G, b, l1, l2, intercept, beta0=None, non_negative=False, ma
             old = beta[j]
             r = grad[j] + G[j, j] * old
             nb = _soft(r, l1 * pen[j]) / diag[j]
-            if non_negative and j != P - 1:
+            if nn[j]:
                 nb = max(nb, 0.0)
             if nb != old:
                 d = nb - old
@@ -406,8 +410,19 @@ class GLMDriver:
             bn = bn[:-1].copy()
         l1 = self.lam * self.alpha
         l2 = self.lam * (1 - self.alpha)
+        pen = self._penalty_matrix()
+        if pen is not None:
+            P = self.P
+            Gn = Gn.copy()
+            Gn[:P, :P] += pen
+        nonneg = bool(self.est._parms.get("non_negative"))
+        nn_names = self.est._parms.get("_nonneg_names")
+        if nn_names:
+            s_ = set(nn_names)
+            mask = np.array([nonneg or (c in s_) for c in self.dinfo.coef_names] + [False])
+            nonneg = mask if self.intercept else mask[:-1]
         new = _solve_quadratic(Gn, bn, l1, l2, self.intercept, beta0=self.beta if self.intercept else self.beta[:-1],
-                               non_negative=bool(self.est._parms.get("non_negative")))
+                               non_negative=nonneg)
         if not self.intercept:
             new = np.concatenate([new, [0.0]])
         diff = float(np.max(np.abs(new - self.beta))) if new.size else 0.0
@@ -419,6 +434,22 @@ class GLMDriver:
         self.last_obj = obj
         self.last_dev = dev
         return diff
+
+    def _penalty_matrix(self):
+        """Quadratic smoothing penalty (GAM): est._gam_penalty = (list of
+        (coef names, S matrix)) mapped onto this driver's coefficient order."""
+        if getattr(self, "_pen_cache", None) is not None:
+            return self._pen_cache[0]
+        spec = getattr(self.est, "_gam_penalty", None)
+        pen = None
+        if spec:
+            pos = {n: i for i, n in enumerate(self.dinfo.coef_names)}
+            pen = np.zeros((self.P, self.P))
+            for names, S in spec:
+                idx = [pos[n] for n in names]
+                pen[np.ix_(idx, idx)] += S
+        self._pen_cache = (pen,)
+        return pen
 
     def deviance(self, beta=None):
         eta = self._eta(beta)
