@@ -19,3 +19,5 @@ from ..models.word2vec import H2OWord2vecEstimator  # noqa: F401
 from ..models.psvm import H2OSupportVectorMachineEstimator  # noqa: F401
 from ..models.rulefit import H2ORuleFitEstimator  # noqa: F401
 from ..models.glm.gam import H2OGeneralizedAdditiveEstimator  # noqa: F401
+from ..models.glm.anovaglm import H2OANOVAGLMEstimator  # noqa: F401
+from ..models.glm.modelselection import H2OModelSelectionEstimator  # noqa: F401
