@@ -21,3 +21,4 @@ from ..models.rulefit import H2ORuleFitEstimator  # noqa: F401
 from ..models.glm.gam import H2OGeneralizedAdditiveEstimator  # noqa: F401
 from ..models.glm.anovaglm import H2OANOVAGLMEstimator  # noqa: F401
 from ..models.glm.modelselection import H2OModelSelectionEstimator  # noqa: F401
+from ..models.infogram import H2OInfogram  # noqa: F401
