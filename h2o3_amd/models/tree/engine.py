@@ -146,6 +146,21 @@ class TreeGrower:
 
     # ------------------------------------------------------------------ hist
     def _build_hist(self, ridx, va, vb, mode, starts, counts):
+        if mode == 3:
+            # uplift: treatment and control (w, w*y) histograms side by side
+            with phase("tree.hist"):
+                H1, _ = tree_ops.hist_build(self.bd, ridx, va, vb[0], 0, starts, counts, len(starts),
+                                            vmax=self._vmax, posv=False, want_wyy=True)
+                H2, _ = tree_ops.hist_build(self.bd, ridx, va, vb[1], 0, starts, counts, len(starts),
+                                            vmax=self._vmax, posv=False, want_wyy=True)
+            H = torch.cat([H1, H2], -1)
+            self._last_wyy = None
+            if self.W > 1:
+                if self.Fpad > self.bd.F:
+                    H = torch.cat([H, torch.zeros((self.Fpad - self.bd.F,) + tuple(H.shape[1:]), dtype=H.dtype,
+                                                  device=H.device)], 0)
+                H = coll.reduce_scatter_dim0(H)
+            return H
         with phase("tree.hist"):
             H, wyy = tree_ops.hist_build(self.bd, ridx, va, vb, mode, starts, counts, len(starts), vmax=self._vmax,
                                          posv=self.use_payload,
@@ -187,7 +202,7 @@ class TreeGrower:
     def _find_splits(self, H, col_mask, node_wyy=None):
         """Dispatch: fused HIP kernel for numeric features on GPU (categorical
         features, which need a per-node sort of bins, go through the torch path)."""
-        if self.dev.type != "cuda":
+        if self.dev.type != "cuda" or self.p.criterion.startswith("uplift"):
             return self._find_splits_torch(H, col_mask, node_wyy)
         Fl = H.shape[0]
         fsl = slice(self.f0, self.f0 + Fl)
@@ -268,8 +283,14 @@ class TreeGrower:
         fsl = slice(self.f0, self.f0 + Fl)
         is_cat = self.is_cat_t[fsl]
         order = None
+        uplift = p.criterion.startswith("uplift")
         if bool(is_cat.any()):
-            if p.criterion == "xgb":
+            if uplift:
+                pt = bins[..., 1] / bins[..., 0].clamp_min(1e-300)
+                pc = bins[..., 3] / bins[..., 2].clamp_min(1e-300)
+                key = torch.where((bins[..., 0] + bins[..., 2]) > 0, pt - pc,
+                                  torch.full_like(bins[..., 0], float("inf")))
+            elif p.criterion == "xgb":
                 key = torch.where(bins[..., 1] > 0, bins[..., 0] / bins[..., 1].clamp_min(1e-300),
                                   torch.full_like(bins[..., 0], float("inf")))
             else:
@@ -290,7 +311,22 @@ class TreeGrower:
         LB, RB = L + naE, R
         LC, RC = totnn.unsqueeze(2), naE
 
+        def diverg(S):
+            # uplift divergence between treatment and control response rates
+            wt, wc = S[..., 0], S[..., 2]
+            pt = (S[..., 1] / wt.clamp_min(1e-300)).clamp(1e-6, 1 - 1e-6)
+            pc = (S[..., 3] / wc.clamp_min(1e-300)).clamp(1e-6, 1 - 1e-6)
+            if p.criterion == "uplift_kl":
+                d = pt * torch.log(pt / pc) + (1 - pt) * torch.log((1 - pt) / (1 - pc))
+            elif p.criterion == "uplift_chisquared":
+                d = (pt - pc) ** 2 / pc + ((1 - pt) - (1 - pc)) ** 2 / (1 - pc)
+            else:  # euclidean
+                d = (pt - pc) ** 2 + ((1 - pt) - (1 - pc)) ** 2
+            return torch.where((wt > 0) & (wc > 0), d, torch.zeros_like(d))
+
         def score(S):
+            if uplift:
+                return diverg(S)
             if p.criterion == "xgb":
                 g, hh = S[..., 0], S[..., 1]
                 if p.reg_alpha > 0:
@@ -302,6 +338,14 @@ class TreeGrower:
         sT = score(T).unsqueeze(2)                         # [n, Fl, 1]
 
         def gain_of(LL, RR):
+            if uplift:
+                nl = LL[..., 0] + LL[..., 2]
+                nr = RR[..., 0] + RR[..., 2]
+                nt = (nl + nr).clamp_min(1e-300)
+                g = (nl / nt) * diverg(LL) + (nr / nt) * diverg(RR) - sT
+                ok = (nl >= p.min_rows) & (nr >= p.min_rows) & (LL[..., 0] > 0) & (LL[..., 2] > 0) & \
+                    (RR[..., 0] > 0) & (RR[..., 2] > 0)
+                return torch.where(ok, g, torch.full_like(g, NEG_INF))
             g = score(LL) + score(RR) - sT
             if p.criterion == "xgb":
                 g = 0.5 * g - p.gamma
@@ -322,6 +366,8 @@ class TreeGrower:
         gA = gain_of(LA, RA)
         gB = gain_of(LB, RB)
         has_na = (na[..., 0] > 0) if p.criterion != "xgb" else ((na[..., 1] > 0) | (na[..., 0] != 0))
+        if uplift:
+            has_na = (na[..., 0] + na[..., 2]) > 0
         gB = torch.where(has_na.unsqueeze(2), gB, torch.full_like(gB, NEG_INF))
         gC = gain_of(LC, RC)
         gC = torch.where(has_na.unsqueeze(2), gC, torch.full_like(gC, NEG_INF))
@@ -333,7 +379,9 @@ class TreeGrower:
         allg = torch.cat([gA, gB, gC], 2)                  # [n, Fl, 2(B-1)+1]
         allg = torch.where(cm.unsqueeze(2), allg, torch.full_like(allg, NEG_INF))
         # min split improvement (relative to the node's squared error)
-        if p.criterion != "xgb":
+        if uplift:
+            allg = torch.where(allg > 1e-12, allg, torch.full_like(allg, NEG_INF))
+        elif p.criterion != "xgb":
             wyy_tot = node_wyy.view(-1, 1).to(T.dtype) if node_wyy is not None else torch.zeros_like(T[..., 0])
             se_before = (wyy_tot - score(T)).clamp_min(0).unsqueeze(2)
             allg = torch.where(allg > se_before * p.min_split_improvement, allg, torch.full_like(allg, NEG_INF))
@@ -366,6 +414,8 @@ class TreeGrower:
             rank.scatter_(1, ordw, torch.arange(B, device=h.device).view(1, B).expand(n, B))
             in_left = rank <= t.view(n, 1)
             bins_w = h[ar_n, fl, :B, 0] if p.criterion != "xgb" else h[ar_n, fl, :B, 1]
+            if uplift:
+                bins_w = h[ar_n, fl, :B, 0] + h[ar_n, fl, :B, 2]
             empty = bins_w <= 0
             in_left = torch.where(empty, na_left.view(n, 1).expand(n, B), in_left)
             in_left = torch.where((opt == 2).view(n, 1), ~empty | na_left.view(n, 1), in_left)
@@ -484,9 +534,9 @@ class TreeGrower:
             split_ids, split_slots = [], []
             for i, (nid_, st, ct, d) in enumerate(frontier):
                 tot_i = tots[i]
-                tree.weight[nid_] = float(tot_i[0] if mode != 1 else tot_i[1])
+                tree.weight[nid_] = float(tot_i[0] if mode != 1 else tot_i[1]) + (float(tot_i[2]) if mode == 3 else 0.0)
                 ok = can_split and gains is not None and math.isfinite(float(gains[i]))
-                if ok and p.criterion != "xgb" and float(tot_i[0]) < 2 * p.min_rows:
+                if ok and p.criterion != "xgb" and float(tree.weight[nid_]) < 2 * p.min_rows:
                     ok = False
                 if ok and p.max_leaves and (len(leaves) + n_front + len(split_ids) + 1) > p.max_leaves:
                     ok = False
@@ -533,8 +583,8 @@ class TreeGrower:
                 part_starts.append(st)
                 part_counts.append(ct)
                 part_feats.append(f)
-                wl = float(Ls[i][0] if mode != 1 else Ls[i][1])
-                wr = float(Rs[i][0] if mode != 1 else Rs[i][1])
+                wl = float(Ls[i][0] if mode != 1 else Ls[i][1]) + (float(Ls[i][2]) if mode == 3 else 0.0)
+                wr = float(Rs[i][0] if mode != 1 else Rs[i][1]) + (float(Rs[i][2]) if mode == 3 else 0.0)
                 new_pairs.append((lid, rid, j, wl <= wr))
                 child_tot[lid] = Ls[i].to(torch.float64)
                 child_tot[rid] = Rs[i].to(torch.float64)

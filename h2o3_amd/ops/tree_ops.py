@@ -43,7 +43,8 @@ def _lib():
 
 
 def channels(mode: int) -> int:
-    return 1 if mode == 2 else 2
+    """Histogram channels: 0 (w, w*y), 1 (g, h), 2 (w), 3 uplift (wt, wt*y, wc, wc*y)."""
+    return 1 if mode == 2 else (4 if mode == 3 else 2)
 
 
 def feature_group(F: int, Bs: int, mode: int, budget: int = _LDS_BUDGET) -> int:
@@ -92,6 +93,9 @@ def make_work(starts, counts, slots, chunk):
 
 def channel_max(va, vb, mode):
     """Max |value| per histogram channel (host floats, one device sync)."""
+    if mode == 3:
+        a, b = channel_max(va, vb[0], 0), channel_max(va, vb[1], 0)
+        return [max(a[0], b[0]), max(a[1], b[1])]
     if mode == 0:
         w = vb if vb is not None else None
         m1 = (va.abs() * (w.abs() if w is not None else 1)).max() if va.numel() else va.new_zeros(())
