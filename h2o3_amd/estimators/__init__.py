@@ -23,3 +23,4 @@ from ..models.glm.anovaglm import H2OANOVAGLMEstimator  # noqa: F401
 from ..models.glm.modelselection import H2OModelSelectionEstimator  # noqa: F401
 from ..models.infogram import H2OInfogram  # noqa: F401
 from ..models.tree.uplift import H2OUpliftRandomForestEstimator  # noqa: F401
+from ..models.grep import H2OGrepModel  # noqa: F401

@@ -517,6 +517,29 @@ class H2OEstimator:
         return s
 
     # ------------------------------------------------------------ persistence
+    def train_segments(self, x=None, y=None, training_frame=None, offset_column=None, weights_column=None,
+                       validation_frame=None, max_runtime_secs=None, segments=None, segment_models_id=None,
+                       parallelism=1, verbose=False):
+        from .segments import train_segments
+        kw = {}
+        if weights_column is not None:
+            kw["weights_column"] = weights_column
+        if offset_column is not None:
+            kw["offset_column"] = offset_column
+        # `segments`: list of column names to group by, or an explicit
+        # enumeration (frame / list of dicts) of the segments to build
+        if isinstance(segments, str) or (isinstance(segments, (list, tuple)) and segments and
+                                         all(isinstance(c, str) for c in segments)):
+            seg_cols, enum = [segments] if isinstance(segments, str) else list(segments), None
+        else:
+            import pandas as pd
+            from ..core.frame import H2OFrame as _F
+            enum = segments.as_data_frame() if isinstance(segments, _F) else pd.DataFrame(segments)
+            seg_cols = list(enum.columns)
+        return train_segments(self, x=x, y=y, training_frame=training_frame, segment_columns=seg_cols,
+                              segments=enum, segment_models_id=segment_models_id, parallelism=parallelism,
+                              verbose=verbose, **kw)
+
     # ---------------------------------------------------------------- explain
     def partial_plot(self, data, cols=None, destination_key=None, nbins=20, weight_column=None, plot=False,
                      plot_stddev=True, figsize=None, server=False, include_na=False, user_splits=None,
