@@ -288,3 +288,15 @@ def explain_row(models, frame, row_index, columns=None, top_n_features=5, **kw):
 def permutation_importance(model, frame, metric="AUTO", n_samples=10000, n_repeats=1, features=None, seed=-1,
                            use_pandas=True):
     return model.permutation_importance(frame, metric, n_samples, n_repeats, features, seed)
+
+
+def jobs():
+    """All job records (water/Job.java list)."""
+    from .core.job import jobs as _jobs
+    return _jobs()
+
+
+def timeline():
+    """Cloud-wide event timeline (water/TimeLine.java)."""
+    from .utils.log import timeline as _tl
+    return _tl()

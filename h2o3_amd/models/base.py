@@ -236,14 +236,25 @@ class H2OEstimator:
                 validation_frame[y] = validation_frame[y].asfactor()
         self._start_time = int(time.time() * 1000)
         t0 = time.time()
+        from ..core.job import Job
+        from ..utils import log as _log
+        self._job = Job(f"{self.algo} model build", dest=self._id).start()
+        _log.event("model_build_start", algo=self.algo, model_id=self._id)
         spec = TrainSpec(training_frame, x, y, p.get("weights_column"), p.get("offset_column"),
                          p.get("fold_column"), validation_frame)
         self._spec = spec
         nfolds = int(p.get("nfolds") or 0)
-        if self.supervised_learning and (nfolds > 1 or p.get("fold_column")):
-            self._cross_validate(spec)
-        self._fit(spec)
-        self._score_all(spec)
+        try:
+            if self.supervised_learning and (nfolds > 1 or p.get("fold_column")):
+                self._cross_validate(spec)
+            self._fit(spec)
+            self._score_all(spec)
+        except Exception as e:
+            self._job.fail(e)
+            _log.event("model_build_failed", algo=self.algo, model_id=self._id, error=str(e))
+            raise
+        self._job.done()
+        _log.event("model_build_done", algo=self.algo, model_id=self._id, secs=round(time.time() - t0, 3))
         self._run_time = time.time() - t0
         self._end_time = int(time.time() * 1000)
         dkv.put(self._id, self)

@@ -46,3 +46,20 @@ def test_segment_models():
     for s, b in slope.items():
         m = sm.get_model(seg=s)
         assert abs(m.coef()["x"] - b) < 0.05
+
+
+def test_h2otree_jobs_timeline():
+    from h2o3_amd.estimators import H2OGradientBoostingEstimator
+    from h2o3_amd.tree import H2OTree
+    h2o.init()
+    rng = np.random.default_rng(0)
+    df = pd.DataFrame({"a": rng.normal(size=300), "k": rng.choice(["p", "q"], 300)})
+    df["y"] = df.a * 2 + (df.k == "p")
+    fr = h2o.H2OFrame(df)
+    m = H2OGradientBoostingEstimator(ntrees=3, max_depth=3)
+    m.train(x=["a", "k"], y="y", training_frame=fr)
+    t = H2OTree(m, 0)
+    assert len(t) == len(t.left_children) == len(t.predictions)
+    assert t.root_node.split_feature in ("a", "k")
+    assert m._job.status == "DONE"
+    assert any(e["event"] == "model_build_done" and e["model_id"] == m.model_id for e in h2o.timeline())
