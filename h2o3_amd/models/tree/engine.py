@@ -161,7 +161,7 @@ class TreeGrower:
                                                   device=H.device)], 0)
                 H = coll.reduce_scatter_dim0(H)
             return H
-        with phase("tree.hist"):
+        with phase("tree.hist"), phase(f"tree.hist.L{getattr(self, '_level', 0)}"):
             H, wyy = tree_ops.hist_build(self.bd, ridx, va, vb, mode, starts, counts, len(starts), vmax=self._vmax,
                                          posv=self.use_payload,
                                          want_wyy=True)
@@ -479,6 +479,7 @@ class TreeGrower:
         leaves, leaf_tot = [], []
         level = 0
         while frontier:
+            self._level = level
             n_front = len(frontier)
             slot_of = {nd[0]: i for i, nd in enumerate(frontier)}
             depth = frontier[0][3]

@@ -129,6 +129,134 @@ __global__ __launch_bounds__(512) void hist_build_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Quad-lane histogram kernel for uint8 codes (rows 16-byte aligned, Fp%16==0).
+// A workgroup owns 16 features; lane = (row_sub in 0..15, quad q in 0..3):
+// each lane loads ONE dword = 4 consecutive codes of its row and performs
+// 4 x C LDS atomics, so a wave instruction covers 16 rows x 16 features with
+// 4x fewer global load instructions than one byte per lane.  Per-feature LDS
+// regions are padded by C entries so equal bins of neighbouring features do
+// not land on the same LDS bank.  Blocks are ordered (chunk, feature-group)
+// with the group fastest and remapped XCD-contiguously, so the feature-group
+// blocks of one row chunk run on the same XCD and share its L2 for the row
+// gathers (codes, ridx, va, vb).
+// ---------------------------------------------------------------------------
+template <int MODE, bool HAS_VB, bool POSV>
+__global__ __launch_bounds__(512) void hist_quad_kernel(
+    const uint8_t* __restrict__ codes, int Fp, const int* __restrict__ ridx,
+    const float* __restrict__ va, const float* __restrict__ vb,
+    const int4* __restrict__ work, int n_work, int n_fg, int F, int Bs, float s0, float s1,
+    double* __restrict__ hist, int n_slots, double* __restrict__ wyy_out) {
+  constexpr int C = Chan<MODE>::C;
+  constexpr int FG = 16;
+  extern __shared__ __attribute__((aligned(16))) unsigned long long ldsq[];
+  const int nwg = n_work * n_fg;
+  const int lb = xcd_remap(blockIdx.x, nwg);
+  const int fgi = lb % n_fg;
+  const int4 wk = work[lb / n_fg];
+  const int fg0 = fgi * FG;
+  const int nf = min(FG, F - fg0);
+  const int stride_f = Bs * C + C;
+  const int total = FG * stride_f;
+  for (int i = threadIdx.x; i < total; i += blockDim.x) ldsq[i] = 0ull;
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int q = lane & 3;          // feature quad
+  const int rs = lane >> 2;        // row within the wave instruction (16)
+  const int wv = threadIdx.x >> 6;
+  const int nwaves = blockDim.x >> 6;
+  const bool do_wyy = (MODE == 0) && wyy_out != nullptr && fgi == 0 && q == 0;
+  double wyy = 0.0;
+  const int pend = wk.y + wk.z;
+  const int step = nwaves * 16;
+  constexpr int U = 4;
+  const uint8_t* cbase = codes + fg0 + 4 * q;
+  unsigned long long* hb[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) hb[k] = ldsq + (4 * q + k) * stride_f;
+  bool fk[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) fk[k] = 4 * q + k < nf;
+  for (int p0 = wk.y + wv * 16 + rs; p0 < pend; p0 += U * step) {
+    int rr[U];
+    unsigned int cw[U];
+    float c0[U], c1[U], yv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) rr[u] = ridx[min(p0 + u * step, pend - 1)];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int r = rr[u];
+      const int vi = POSV ? min(p0 + u * step, pend - 1) : r;
+      if (MODE == 0) {
+        const float y = va[vi];
+        const float w = HAS_VB ? vb[vi] : 1.f;
+        c0[u] = w; c1[u] = w * y; yv[u] = y;
+      } else if (MODE == 1) {
+        c0[u] = va[vi]; c1[u] = vb[vi]; yv[u] = 0.f;
+      } else {
+        c0[u] = HAS_VB ? vb[vi] : 1.f; c1[u] = 0.f; yv[u] = 0.f;
+      }
+      cw[u] = *reinterpret_cast<const unsigned int*>(cbase + (size_t)r * Fp);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const bool inr = p0 + u * step < pend;
+      if (MODE == 0 && do_wyy && inr) wyy += (double)c1[u] * (double)yv[u];
+      if (!inr || (c0[u] == 0.f && c1[u] == 0.f)) continue;
+      const unsigned long long a0 = (unsigned long long)__float2ll_rn(c0[u] * s0);
+      const unsigned long long a1 = (unsigned long long)__float2ll_rn(c1[u] * s1);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (!fk[k]) continue;
+        unsigned long long* h = hb[k] + ((cw[u] >> (8 * k)) & 0xffu) * C;
+        __hip_atomic_fetch_add(h, a0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (C > 1) __hip_atomic_fetch_add(h + 1, a1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
+  }
+  __syncthreads();
+  if (MODE == 0 && wyy_out != nullptr && fgi == 0) {
+    wyy = wave_sum(wyy);
+    if (lane == 0) gbl_add(wyy_out + wk.x, wyy);
+  }
+  const double inv0 = 1.0 / (double)s0, inv1 = 1.0 / (double)s1;
+  const int per_f = Bs * C;
+  const int tot_real = nf * per_f;
+  for (int i = threadIdx.x; i < tot_real; i += blockDim.x) {
+    const int j = i / per_f;
+    const int rem = i - j * per_f;
+    const long long v = (long long)ldsq[j * stride_f + rem];
+    if (v != 0) {
+      const double d = (double)v * ((C == 1 || (rem & 1) == 0) ? inv0 : inv1);
+      gbl_add(hist + ((size_t)(fg0 + j) * n_slots + wk.x) * per_f + rem, d);
+    }
+  }
+}
+
+extern "C" int h2o_hist_quad(const void* codes, int Fp, const int* ridx, const float* va, const float* vb,
+                             const int* work, int n_work, int F, int Bs, float s0, float s1, double* hist,
+                             int n_slots, int mode, int threads, double* wyy, int posv, hipStream_t s) {
+  if (n_work <= 0) return 0;
+  if (Fp % 16 != 0 || Bs > 256) return -1;
+  const int n_fg = (F + 15) / 16;
+  const int C = mode == 2 ? 1 : 2;
+  const size_t lds = (size_t)16 * (Bs * C + C) * sizeof(unsigned long long);
+  const dim3 grid(n_work * n_fg);
+  const uint8_t* cc = (const uint8_t*)codes;
+  const int4* wk = (const int4*)work;
+#define H2O_LQ2(M, V, PV) hipLaunchKernelGGL((hist_quad_kernel<M, V, PV>), grid, dim3(threads), lds, s, cc, Fp, ridx, \
+                                             va, vb, wk, n_work, n_fg, F, Bs, s0, s1, hist, n_slots, wyy)
+#define H2O_LQ(M, V) if (posv) H2O_LQ2(M, V, true); else H2O_LQ2(M, V, false)
+  switch (mode) {
+    case 0: if (vb) H2O_LQ(0, true); else H2O_LQ(0, false); break;
+    case 1: H2O_LQ(1, true); break;
+    default: if (vb) H2O_LQ(2, true); else H2O_LQ(2, false); break;
+  }
+#undef H2O_LQ
+#undef H2O_LQ2
+  return (int)hipGetLastError();
+}
+
 template <typename CodeT>
 static int launch_hist(const void* codes, int Fp, const int* ridx, const float* va, const float* vb,
                        const int4* work, int n_work, int F, int FG, int Bs, float s0, float s1, double* hist,

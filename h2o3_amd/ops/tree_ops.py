@@ -7,6 +7,7 @@ on CPU and by the numerics tests.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
@@ -32,6 +33,9 @@ def _lib():
         lib.h2o_hist_build.argtypes = [_c_void, _c_int, _c_int, _c_void, _c_void, _c_void, _c_void, _c_int,
                                        _c_int, _c_int, _c_int, ctypes.c_float, ctypes.c_float, _c_void, _c_int, _c_int,
                                        _c_int, _c_void, _c_int, _c_void]
+        lib.h2o_hist_quad.argtypes = [_c_void, _c_int, _c_void, _c_void, _c_void, _c_void, _c_int, _c_int, _c_int,
+                                      ctypes.c_float, ctypes.c_float, _c_void, _c_int, _c_int, _c_int, _c_void,
+                                      _c_int, _c_void]
         lib.h2o_part_count.argtypes = [_c_void, _c_int, _c_ll, _c_ll, _c_void, _c_void, _c_int, _c_void,
                                        _c_void, _c_int, _c_void, _c_void]
         lib.h2o_part_scatter.argtypes = [_c_void, _c_int, _c_ll, _c_ll, _c_void, _c_void, _c_int, _c_void,
@@ -133,7 +137,9 @@ def hist_build(bd, ridx, va, vb, mode, starts, counts, n_slots, use_native=None,
     native = dev.type == "cuda" if use_native is None else use_native
     if native:
         lib = _lib()
-        FG = feature_group(bd.F, bd.Bs, mode)
+        quad = bd.code_bytes == 1 and bd.Fp % 16 == 0 and bd.Bs <= 256 and \
+            os.environ.get("H2O3_HIST_KERNEL", "quad") == "quad"
+        FG = 16 if quad else feature_group(bd.F, bd.Bs, mode)
         n_fg = (bd.F + FG - 1) // FG
         total = int(sum(counts))
         if total == 0:
@@ -148,6 +154,13 @@ def hist_build(bd, ridx, va, vb, mode, starts, counts, n_slots, use_native=None,
         if vmax is None:
             vmax = channel_max(va, vb, mode)
         s0, s1 = (fixed_point_scale(m, chunk) for m in vmax)
+        if quad:
+            rc = lib.h2o_hist_quad(_ptr(bd.codes), bd.Fp, _ptr(ridx), _ptr(va), _ptr(vb), _ptr(work), len(items),
+                                   bd.F, bd.Bs, s0, s1, _ptr(hist), n_slots, mode, 512, _ptr(wyy),
+                                   1 if posv else 0, _stream())
+            if rc != 0:
+                raise RuntimeError(f"h2o_hist_quad failed: hip error {rc}")
+            return ret()
         rc = lib.h2o_hist_build(_ptr(bd.codes), bd.code_bytes, bd.Fp, _ptr(ridx), _ptr(va), _ptr(vb), _ptr(work),
                                 len(items), bd.F, FG, bd.Bs, s0, s1, _ptr(hist), n_slots, mode, threads, _ptr(wyy),
                                 1 if posv else 0, _stream())

@@ -29,8 +29,10 @@ def _binned(n=20000, F=13, nbins=255, seed=0, cats=True):
 
 
 @pytest.mark.parametrize("nbins,mode", [(255, 0), (255, 1), (20, 0), (1000, 0), (1000, 1)])
-def test_hist_build_matches_reference(nbins, mode):
+@pytest.mark.parametrize("kernel", ["quad", "old"])
+def test_hist_build_matches_reference(nbins, mode, kernel, monkeypatch):
     _need_gpu()
+    monkeypatch.setenv("H2O3_HIST_KERNEL", kernel)
     from h2o3_amd.ops import tree_ops
     bd, _ = _binned(nbins=nbins)
     n = bd.nrows_local
