@@ -423,7 +423,15 @@ class H2OEstimator:
 
     def predict(self, test_data, **kw):
         raw = self._predict_raw(test_data)
-        return self._pred_frame_from_raw(raw)
+        fr = self._pred_frame_from_raw(raw)
+        cal = getattr(self, "_calibrator", None)
+        if cal is not None and self._spec is not None and self._spec.nclasses == 2:
+            # reference CalibrationHelper: calibrated probabilities as extra columns
+            p1 = cal(raw[:, 1]).to(torch.float32)
+            fr = H2OFrame.from_vecs([fr.vec(n) for n in fr.names] + [Vec((1 - p1).contiguous(), T_REAL),
+                                                                     Vec(p1.contiguous(), T_REAL)],
+                                    list(fr.names) + ["cal_p0", "cal_p1"])
+        return fr
 
     def predict_leaf_node_assignment(self, test_data, type="Path"):
         raise NotImplementedError(f"{self.algo} has no leaf node assignment")

@@ -134,6 +134,9 @@ class H2ORandomForestEstimator(SharedTreeEstimator):
         has = oob_cnt > 0
         self._oob_raw = self._normalize(oobp)
         self._oob_mask = has
+        if p.get("calibrate_model") and p.get("calibration_frame") is not None:
+            from .calibration import fit_calibration
+            fit_calibration(self, p["calibration_frame"], p.get("calibration_method", "auto"))
 
     def _seed(self):
         s = self._parms.get("seed", -1)
@@ -155,12 +158,7 @@ class H2ORandomForestEstimator(SharedTreeEstimator):
         K = self._K
         sums = self._forest.predict(X, K)
         ntrees = max(1, len(self._forest) // K)
-        out = self._normalize(sums / ntrees)
-        cal = getattr(self, "_calibrator", None)
-        if cal is not None and self._spec.nclasses == 2:
-            p1 = cal(out[:, 1])
-            out = torch.stack([1 - p1, p1], 1)
-        return out
+        return self._normalize(sums / ntrees)
 
     def predict_contributions(self, test_data, output_format="Original", top_n=None, bottom_n=None,
                               compare_abs=False, background_frame=None):

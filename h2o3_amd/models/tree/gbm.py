@@ -399,9 +399,6 @@ class H2OGradientBoostingEstimator(SharedTreeEstimator):
             return torch.softmax(f, 1)
         mu = self._dist.linkinv(f[:, 0])
         if self._spec.nclasses == 2:
-            cal = getattr(self, "_calibrator", None)
-            if cal is not None:
-                mu = cal(mu)
             return torch.stack([1 - mu, mu], 1)
         return mu.view(-1, 1)
 
