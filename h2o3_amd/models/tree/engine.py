@@ -163,8 +163,8 @@ class TreeGrower:
             return H
         with phase("tree.hist"), phase(f"tree.hist.L{getattr(self, '_level', 0)}"):
             H, wyy = tree_ops.hist_build(self.bd, ridx, va, vb, mode, starts, counts, len(starts), vmax=self._vmax,
-                                         posv=self.use_payload,
-                                         want_wyy=True)
+                                         posv=self.use_payload, want_wyy=True,
+                                         unit_w=getattr(self, "_unit_w", False))
         if wyy is not None:
             coll.allreduce_(wyy)
         self._last_wyy = wyy
@@ -459,6 +459,9 @@ class TreeGrower:
         C = tree_ops.channels(mode)
         torch.arange(N, dtype=torch.int32, device=self.dev, out=self.ridx)
         self._vmax = tree_ops.channel_max(va, vb, mode) if self.dev.type == "cuda" else None
+        # 0/1 row weights (unweighted data, row sampling) -> packed histogram atomics
+        self._unit_w = mode == 0 and self.dev.type == "cuda" and (
+            vb is None or bool(((vb == 0) | (vb == 1)).all()))
         ridx, ridx2 = self.ridx, self.ridx2
         pa, pb, pa2, pb2 = self._pay
         if self.use_payload:

@@ -141,13 +141,21 @@ __global__ __launch_bounds__(512) void hist_build_kernel(
 // blocks of one row chunk run on the same XCD and share its L2 for the row
 // gathers (codes, ridx, va, vb).
 // ---------------------------------------------------------------------------
-template <int MODE, bool HAS_VB, bool POSV>
+// PACK (MODE 0, weights all 0/1): ONE 64-bit LDS atomic per (row, feature):
+// bits 63..40 = row count, bits 39..0 = sum of the biased fixed-point
+// response q + Bq (q = rint(y * s1), Bq = rint(vmax * s1) so every term is
+// >= 0 and no carry crosses into the count).  Decoded in the flush as
+// count and (low - count * Bq) / s1.  Halves the LDS atomics of the
+// unweighted GBM / sampled DRF histograms; the response is quantised at
+// 1/s1 = chunk * 2 * vmax / 2^40 (f32-level resolution, exact summation).
+template <int MODE, bool HAS_VB, bool POSV, bool PACK>
 __global__ __launch_bounds__(512) void hist_quad_kernel(
     const uint8_t* __restrict__ codes, int Fp, const int* __restrict__ ridx,
     const float* __restrict__ va, const float* __restrict__ vb,
     const int4* __restrict__ work, int n_work, int n_fg, int F, int Bs, float s0, float s1,
-    double* __restrict__ hist, int n_slots, double* __restrict__ wyy_out) {
+    double* __restrict__ hist, int n_slots, double* __restrict__ wyy_out, long long bq) {
   constexpr int C = Chan<MODE>::C;
+  constexpr int CL = PACK ? 1 : C;       // u64 entries per bin in LDS
   constexpr int FG = 16;
   extern __shared__ __attribute__((aligned(16))) unsigned long long ldsq[];
   const int nwg = n_work * n_fg;
@@ -156,7 +164,7 @@ __global__ __launch_bounds__(512) void hist_quad_kernel(
   const int4 wk = work[lb / n_fg];
   const int fg0 = fgi * FG;
   const int nf = min(FG, F - fg0);
-  const int stride_f = Bs * C + C;
+  const int stride_f = Bs * CL + CL;
   const int total = FG * stride_f;
   for (int i = threadIdx.x; i < total; i += blockDim.x) ldsq[i] = 0ull;
   __syncthreads();
@@ -203,12 +211,22 @@ __global__ __launch_bounds__(512) void hist_quad_kernel(
       const bool inr = p0 + u * step < pend;
       if (MODE == 0 && do_wyy && inr) wyy += (double)c1[u] * (double)yv[u];
       if (!inr || (c0[u] == 0.f && c1[u] == 0.f)) continue;
+      if (PACK) {
+        const unsigned long long a = (1ull << 40) + (unsigned long long)(__float2ll_rn(yv[u] * s1) + bq);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (!fk[k]) continue;
+          __hip_atomic_fetch_add(hb[k] + ((cw[u] >> (8 * k)) & 0xffu), a, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        continue;
+      }
       const unsigned long long a0 = (unsigned long long)__float2ll_rn(c0[u] * s0);
       const unsigned long long a1 = (unsigned long long)__float2ll_rn(c1[u] * s1);
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         if (!fk[k]) continue;
-        unsigned long long* h = hb[k] + ((cw[u] >> (8 * k)) & 0xffu) * C;
+        unsigned long long* h = hb[k] + ((cw[u] >> (8 * k)) & 0xffu) * CL;
         __hip_atomic_fetch_add(h, a0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (C > 1) __hip_atomic_fetch_add(h + 1, a1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
@@ -221,6 +239,22 @@ __global__ __launch_bounds__(512) void hist_quad_kernel(
   }
   const double inv0 = 1.0 / (double)s0, inv1 = 1.0 / (double)s1;
   const int per_f = Bs * C;
+  if (PACK) {
+    const int tot = nf * Bs;
+    for (int i = threadIdx.x; i < tot; i += blockDim.x) {
+      const int j = i / Bs;
+      const int b = i - j * Bs;
+      const unsigned long long v = ldsq[j * stride_f + b];
+      if (v != 0) {
+        const long long cnt = (long long)(v >> 40);
+        const long long low = (long long)(v & ((1ull << 40) - 1));
+        double* o = hist + ((size_t)(fg0 + j) * n_slots + wk.x) * per_f + 2 * b;
+        gbl_add(o, (double)cnt);
+        gbl_add(o + 1, (double)(low - cnt * bq) * inv1);
+      }
+    }
+    return;
+  }
   const int tot_real = nf * per_f;
   for (int i = threadIdx.x; i < tot_real; i += blockDim.x) {
     const int j = i / per_f;
@@ -233,20 +267,30 @@ __global__ __launch_bounds__(512) void hist_quad_kernel(
   }
 }
 
+// pack_bq >= 0 selects the packed single-atomic path (MODE 0, 0/1 weights).
 extern "C" int h2o_hist_quad(const void* codes, int Fp, const int* ridx, const float* va, const float* vb,
                              const int* work, int n_work, int F, int Bs, float s0, float s1, double* hist,
-                             int n_slots, int mode, int threads, double* wyy, int posv, hipStream_t s) {
+                             int n_slots, int mode, int threads, double* wyy, int posv, long long pack_bq,
+                             hipStream_t s) {
   if (n_work <= 0) return 0;
   if (Fp % 16 != 0 || Bs > 256) return -1;
+  const bool pack = pack_bq >= 0 && mode == 0;
   const int n_fg = (F + 15) / 16;
   const int C = mode == 2 ? 1 : 2;
-  const size_t lds = (size_t)16 * (Bs * C + C) * sizeof(unsigned long long);
+  const int CL = pack ? 1 : C;
+  const size_t lds = (size_t)16 * (Bs * CL + CL) * sizeof(unsigned long long);
   const dim3 grid(n_work * n_fg);
   const uint8_t* cc = (const uint8_t*)codes;
   const int4* wk = (const int4*)work;
-#define H2O_LQ2(M, V, PV) hipLaunchKernelGGL((hist_quad_kernel<M, V, PV>), grid, dim3(threads), lds, s, cc, Fp, ridx, \
-                                             va, vb, wk, n_work, n_fg, F, Bs, s0, s1, hist, n_slots, wyy)
-#define H2O_LQ(M, V) if (posv) H2O_LQ2(M, V, true); else H2O_LQ2(M, V, false)
+#define H2O_LQ2(M, V, PV, PK) hipLaunchKernelGGL((hist_quad_kernel<M, V, PV, PK>), grid, dim3(threads), lds, s, cc, \
+                                                 Fp, ridx, va, vb, wk, n_work, n_fg, F, Bs, s0, s1, hist, n_slots, \
+                                                 wyy, pack_bq)
+#define H2O_LQ(M, V) if (posv) H2O_LQ2(M, V, true, false); else H2O_LQ2(M, V, false, false)
+  if (pack) {
+    if (vb) { if (posv) H2O_LQ2(0, true, true, true); else H2O_LQ2(0, true, false, true); }
+    else { if (posv) H2O_LQ2(0, false, true, true); else H2O_LQ2(0, false, false, true); }
+    return (int)hipGetLastError();
+  }
   switch (mode) {
     case 0: if (vb) H2O_LQ(0, true); else H2O_LQ(0, false); break;
     case 1: H2O_LQ(1, true); break;

@@ -7,6 +7,7 @@ on CPU and by the numerics tests.
 from __future__ import annotations
 
 import ctypes
+import math
 import os
 
 import torch
@@ -35,7 +36,7 @@ def _lib():
                                        _c_int, _c_void, _c_int, _c_void]
         lib.h2o_hist_quad.argtypes = [_c_void, _c_int, _c_void, _c_void, _c_void, _c_void, _c_int, _c_int, _c_int,
                                       ctypes.c_float, ctypes.c_float, _c_void, _c_int, _c_int, _c_int, _c_void,
-                                      _c_int, _c_void]
+                                      _c_int, _c_ll, _c_void]
         lib.h2o_part_count.argtypes = [_c_void, _c_int, _c_ll, _c_ll, _c_void, _c_void, _c_int, _c_void,
                                        _c_void, _c_int, _c_void, _c_void]
         lib.h2o_part_scatter.argtypes = [_c_void, _c_int, _c_ll, _c_ll, _c_void, _c_void, _c_int, _c_void,
@@ -123,8 +124,16 @@ def fixed_point_scale(maxv, nmax):
     return float(2.0 ** max(min(k, 100), -100))
 
 
+def _pack_scale(vmax, chunk):
+    """(s1, bq) of the packed 40-bit response field: chunk * (2*bq + 1) < 2^40."""
+    vm = max(float(vmax), 1e-30)
+    k = math.floor(math.log2((2.0 ** 40 - 2 * chunk) / (2.0 * chunk * vm * 1.0001)))
+    s1 = 2.0 ** k
+    return s1, int(math.ceil(vm * s1))
+
+
 def hist_build(bd, ridx, va, vb, mode, starts, counts, n_slots, use_native=None, target_blocks=2048, vmax=None,
-               want_wyy=False, posv=False):
+               want_wyy=False, posv=False, unit_w=False):
     """Histograms of the row segments [starts[i], starts[i]+counts[i]) of
     ridx into slot i.  Returns hist [F, n_slots, Bs, C] float64 (and, with
     want_wyy in mode 0, the per-slot sum of w*y*y).  posv: va/vb are stored
@@ -155,9 +164,12 @@ def hist_build(bd, ridx, va, vb, mode, starts, counts, n_slots, use_native=None,
             vmax = channel_max(va, vb, mode)
         s0, s1 = (fixed_point_scale(m, chunk) for m in vmax)
         if quad:
+            bq = -1
+            if mode == 0 and unit_w and chunk < (1 << 23) and os.environ.get("H2O3_HIST_PACK", "1") == "1":
+                s1, bq = _pack_scale(vmax[1] if vb is None else max(vmax[1], 0.0), chunk)
             rc = lib.h2o_hist_quad(_ptr(bd.codes), bd.Fp, _ptr(ridx), _ptr(va), _ptr(vb), _ptr(work), len(items),
                                    bd.F, bd.Bs, s0, s1, _ptr(hist), n_slots, mode, 512, _ptr(wyy),
-                                   1 if posv else 0, _stream())
+                                   1 if posv else 0, bq, _stream())
             if rc != 0:
                 raise RuntimeError(f"h2o_hist_quad failed: hip error {rc}")
             return ret()

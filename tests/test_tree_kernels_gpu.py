@@ -136,3 +136,22 @@ def test_split_kernel_matches_torch(crit):
     assert torch.equal(a["opt"].cpu(), b["opt"].cpu())
     assert torch.equal(a["mask"].cpu(), b["mask"].cpu())
     torch.testing.assert_close(a["L"], b["L"].to(a["L"].dtype), rtol=1e-9, atol=1e-9)
+
+
+@pytest.mark.parametrize("weights", [None, "binary"])
+def test_hist_packed_single_atomic(weights):
+    """Packed (count | biased fixed-point response) 64-bit atomics vs fp64 torch."""
+    _need_gpu()
+    from h2o3_amd.ops import tree_ops
+    bd, _ = _binned(nbins=255)
+    n = bd.nrows_local
+    g = torch.Generator(device="cuda").manual_seed(3)
+    ridx = torch.randperm(n, generator=g, device="cuda").to(torch.int32)
+    va = torch.randn(n, generator=g, device="cuda")
+    vb = None if weights is None else (torch.rand(n, generator=g, device="cuda") < 0.6).to(torch.float32)
+    starts, counts = [0, 7000], [7000, 13000]
+    vmax = tree_ops.channel_max(va, vb, 0)
+    h_gpu = tree_ops.hist_build(bd, ridx, va, vb, 0, starts, counts, 2, use_native=True, unit_w=True, vmax=vmax)
+    h_ref = tree_ops.hist_build(bd, ridx, va, vb, 0, starts, counts, 2, use_native=False)
+    torch.testing.assert_close(h_gpu[..., 0], h_ref[..., 0], rtol=0, atol=1e-9)   # counts exact
+    torch.testing.assert_close(h_gpu[..., 1], h_ref[..., 1], rtol=1e-5, atol=1e-4)
