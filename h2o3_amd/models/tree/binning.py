@@ -179,6 +179,10 @@ def bin_frame_tensors(features, is_cat, cat_cards, names, hist_type="AUTO", nbin
     na = Bs - 1
     align = 16 // code_bytes
     Fp = ((F + align - 1) // align) * align
+    if Fp * code_bytes > 64:
+        # wide rows: pad to whole 128-byte cache lines so a scattered row gather
+        # (deep tree levels) touches ONE line instead of straddling two
+        Fp = ((Fp * code_bytes + 127) // 128) * 128 // code_bytes
     col = torch.empty((max(Fp, 1), N), dtype=dt, device=dev)
     if Fp > F:
         col[F:] = na if code_bytes == 1 else (na if na < 32768 else na - 65536)

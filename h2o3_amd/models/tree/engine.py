@@ -20,6 +20,7 @@ per-row leaf id for the leaf-value pass without any tree traversal.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -161,6 +162,8 @@ class TreeGrower:
                                                   device=H.device)], 0)
                 H = coll.reduce_scatter_dim0(H)
             return H
+        if mode == 0 and getattr(self, "_va_eff", None) is not None:
+            va, vb = self._va_eff, None   # 0/1 weights folded into NaN-masked responses
         with phase("tree.hist"), phase(f"tree.hist.L{getattr(self, '_level', 0)}"):
             H, wyy = tree_ops.hist_build(self.bd, ridx, va, vb, mode, starts, counts, len(starts), vmax=self._vmax,
                                          posv=self.use_payload, want_wyy=True,
@@ -462,6 +465,11 @@ class TreeGrower:
         # 0/1 row weights (unweighted data, row sampling) -> packed histogram atomics
         self._unit_w = mode == 0 and self.dev.type == "cuda" and (
             vb is None or bool(((vb == 0) | (vb == 1)).all()))
+        self._va_eff = None
+        quad = self.bd.code_bytes == 1 and self.bd.Bs <= 256 and self.bd.Fp % 16 == 0 and \
+            os.environ.get("H2O3_HIST_KERNEL", "quad") == "quad"
+        if self._unit_w and vb is not None and not self.use_payload and quad:
+            self._va_eff = torch.where(vb > 0, va, torch.full_like(va, float("nan")))
         ridx, ridx2 = self.ridx, self.ridx2
         pa, pb, pa2, pb2 = self._pay
         if self.use_payload:

@@ -196,9 +196,11 @@ __global__ __launch_bounds__(512) void hist_quad_kernel(
       const int r = rr[u];
       const int vi = POSV ? min(p0 + u * step, pend - 1) : r;
       if (MODE == 0) {
+        // without vb a NaN response marks a zero-weight row (out-of-bag /
+        // sampled-out): one gather per row instead of two
         const float y = va[vi];
-        const float w = HAS_VB ? vb[vi] : 1.f;
-        c0[u] = w; c1[u] = w * y; yv[u] = y;
+        const float w = HAS_VB ? vb[vi] : (y == y ? 1.f : 0.f);
+        c0[u] = w; c1[u] = w != 0.f ? w * y : 0.f; yv[u] = w != 0.f ? y : 0.f;
       } else if (MODE == 1) {
         c0[u] = va[vi]; c1[u] = vb[vi]; yv[u] = 0.f;
       } else {
