@@ -452,6 +452,96 @@ __global__ __launch_bounds__(256) void part_scatter_kernel(
     __syncthreads();
   }
 }
+// ---------------------------------------------------------------------------
+// Ballot partition (v2).  Pass 1 (flags): positions are walked in 256-wide
+// coalesced strides; each wave ballots its 64 go-left bits, stores them as
+// one u64 (flags[fbase + (p - start) / 64]) and the block counts lefts.
+// Pass 2 (compact): re-reads ridx coalesced + the flag words (no second
+// random code gather), ranks every position with popc over the ballot and
+// the running per-wave / per-block prefix, so each wave's lefts (rights)
+// land in ONE contiguous run -> coalesced stores, stable order.
+// ---------------------------------------------------------------------------
+template <typename CodeT>
+__global__ __launch_bounds__(256) void part_flags_kernel(
+    const CodeT* __restrict__ codes, long long rs, long long fs, const int* __restrict__ ridx,
+    const int4* __restrict__ work, const int* __restrict__ fbase, const int* __restrict__ feat,
+    const uint8_t* __restrict__ masks, int Bs, unsigned long long* __restrict__ flags, int* __restrict__ cnt) {
+  __shared__ uint8_t m[4096];
+  __shared__ int red[4];
+  const int4 wk = work[blockIdx.x];
+  const int f = feat[wk.x];
+  for (int i = threadIdx.x; i < Bs; i += blockDim.x) m[i] = masks[(size_t)wk.x * Bs + i];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int end = wk.y + wk.z;
+  const int fb = fbase[blockIdx.x];
+  int local = 0;
+  constexpr int U = 8;   // 8 strides of 256 positions in flight per thread
+  for (int base = wk.y; base < end; base += 256 * U) {
+    int r[U], c[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) r[u] = ridx[min(base + u * 256 + (int)threadIdx.x, end - 1)];
+#pragma unroll
+    for (int u = 0; u < U; ++u) c[u] = (int)codes[(size_t)r[u] * rs + (size_t)f * fs];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int p = base + u * 256 + (int)threadIdx.x;
+      const bool L = p < end && m[c[u]];
+      const unsigned long long bal = __ballot(L);
+      const int w0 = base + u * 256 + wv * 64;        // first position of this wave's 64
+      if (lane == 0 && w0 < end) flags[fb + (w0 - wk.y) / 64] = bal;
+      local += L ? 1 : 0;
+    }
+  }
+  local = (int)wave_sum((float)local);
+  if (lane == 0) red[wv] = local;
+  __syncthreads();
+  if (threadIdx.x == 0) cnt[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ __launch_bounds__(256) void part_compact_kernel(
+    const int* __restrict__ ridx, const int4* __restrict__ work, const int* __restrict__ fbase,
+    const unsigned long long* __restrict__ flags, const int* __restrict__ loff, const int* __restrict__ roff,
+    int* __restrict__ out, const float* __restrict__ pa, float* __restrict__ pa_out) {
+  __shared__ int wl[4], wr_[4];
+  const int4 wk = work[blockIdx.x];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int end = wk.y + wk.z;
+  const int fb = fbase[blockIdx.x];
+  int lbase = loff[blockIdx.x], rbase = roff[blockIdx.x];
+  const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  for (int base = wk.y; base < end; base += 256) {
+    const int p = base + threadIdx.x;
+    const bool v = p < end;
+    const int w0 = base + wv * 64;
+    const unsigned long long bal = (w0 < end) ? flags[fb + (w0 - wk.y) / 64] : 0ull;
+    const unsigned long long valid = __ballot(v);
+    const bool L = v && ((bal >> lane) & 1ull);
+    const int nl_w = __popcll(bal & valid);
+    const int nv_w = __popcll(valid);
+    if (lane == 0) { wl[wv] = nl_w; wr_[wv] = nv_w - nl_w; }
+    __syncthreads();
+    int lpre = 0, rpre = 0, ltot = 0, rtot = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      lpre += (w < wv) ? wl[w] : 0;
+      rpre += (w < wv) ? wr_[w] : 0;
+      ltot += wl[w];
+      rtot += wr_[w];
+    }
+    if (v) {
+      const int lr = __popcll(bal & valid & below);
+      const int rr = __popcll(~bal & valid & below);
+      const int dst = L ? (lbase + lpre + lr) : (rbase + rpre + rr);
+      out[dst] = ridx[p];
+      if (pa) pa_out[dst] = pa[p];
+    }
+    lbase += ltot;
+    rbase += rtot;
+    __syncthreads();
+  }
+}
+
 // nid[ridx[p]] = leaf for p in segment.  work[i] = (leaf_id, start, count, -)
 __global__ __launch_bounds__(256) void fill_nid_kernel(const int* __restrict__ ridx, const int4* __restrict__ work,
                                                        int* __restrict__ nid) {
@@ -468,6 +558,28 @@ int h2o_hist_build(const void* codes, int code_bytes, int Fp, const int* ridx, c
   if (code_bytes == 1)
     return launch_hist<uint8_t>(codes, Fp, ridx, va, vb, (const int4*)work, n_work, F, FG, Bs, s0, s1, hist, n_slots, mode, threads, wyy, posv, s);
   return launch_hist<uint16_t>(codes, Fp, ridx, va, vb, (const int4*)work, n_work, F, FG, Bs, s0, s1, hist, n_slots, mode, threads, wyy, posv, s);
+}
+
+int h2o_part_flags(const void* codes, int code_bytes, long long rs, long long fs, const int* ridx,
+                   const int* work, const int* fbase, int n_work, const int* feat, const uint8_t* masks, int Bs,
+                   unsigned long long* flags, int* cnt, hipStream_t s) {
+  if (n_work <= 0) return 0;
+  if (code_bytes == 1)
+    hipLaunchKernelGGL(part_flags_kernel<uint8_t>, dim3(n_work), dim3(256), 0, s, (const uint8_t*)codes, rs, fs,
+                       ridx, (const int4*)work, fbase, feat, masks, Bs, flags, cnt);
+  else
+    hipLaunchKernelGGL(part_flags_kernel<uint16_t>, dim3(n_work), dim3(256), 0, s, (const uint16_t*)codes, rs, fs,
+                       ridx, (const int4*)work, fbase, feat, masks, Bs, flags, cnt);
+  return (int)hipGetLastError();
+}
+
+int h2o_part_compact(const int* ridx, const int* work, const int* fbase, int n_work,
+                     const unsigned long long* flags, const int* loff, const int* roff, int* out, const float* pa,
+                     float* pa_out, hipStream_t s) {
+  if (n_work <= 0) return 0;
+  hipLaunchKernelGGL(part_compact_kernel, dim3(n_work), dim3(256), 0, s, ridx, (const int4*)work, fbase, flags, loff,
+                     roff, out, pa, pa_out);
+  return (int)hipGetLastError();
 }
 
 int h2o_part_count(const void* codes, int code_bytes, long long rs, long long fs, const int* ridx,

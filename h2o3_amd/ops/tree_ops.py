@@ -37,6 +37,10 @@ def _lib():
         lib.h2o_hist_quad.argtypes = [_c_void, _c_int, _c_void, _c_void, _c_void, _c_void, _c_int, _c_int, _c_int,
                                       ctypes.c_float, ctypes.c_float, _c_void, _c_int, _c_int, _c_int, _c_void,
                                       _c_int, _c_ll, _c_void]
+        lib.h2o_part_flags.argtypes = [_c_void, _c_int, _c_ll, _c_ll, _c_void, _c_void, _c_void, _c_int, _c_void,
+                                       _c_void, _c_int, _c_void, _c_void, _c_void]
+        lib.h2o_part_compact.argtypes = [_c_void, _c_void, _c_void, _c_int, _c_void, _c_void, _c_void, _c_void,
+                                         _c_void, _c_void, _c_void]
         lib.h2o_part_count.argtypes = [_c_void, _c_int, _c_ll, _c_ll, _c_void, _c_void, _c_int, _c_void,
                                        _c_void, _c_int, _c_void, _c_void]
         lib.h2o_part_scatter.argtypes = [_c_void, _c_int, _c_ll, _c_ll, _c_void, _c_void, _c_int, _c_void,
@@ -248,8 +252,18 @@ def partition(bd, ridx, ridx_out, feats, masks, starts, counts, use_native=None,
             codes, rs, fs = bd.codes_col, 1, bd.nrows_local
         else:
             codes, rs, fs = bd.codes, bd.Fp, 1
-        rc = lib.h2o_part_count(_ptr(codes), bd.code_bytes, rs, fs, _ptr(ridx), _ptr(work), nw, _ptr(feat_t),
-                                _ptr(masks), bd.Bs, _ptr(cnt), _stream())
+        ballot = os.environ.get("H2O3_PART", "ballot") == "ballot" and (payload is None or payload[1] is None)
+        if ballot:
+            import numpy as np
+            words = (items[:, 2].astype(np.int64) + 63) // 64
+            fb_h = (np.cumsum(words) - words).astype(np.int32)
+            fbase = torch.from_numpy(fb_h).to(dev, non_blocking=True)
+            flags = torch.empty(int(words.sum()) + 1, dtype=torch.int64, device=dev)
+            rc = lib.h2o_part_flags(_ptr(codes), bd.code_bytes, rs, fs, _ptr(ridx), _ptr(work), _ptr(fbase), nw,
+                                    _ptr(feat_t), _ptr(masks), bd.Bs, _ptr(flags), _ptr(cnt), _stream())
+        else:
+            rc = lib.h2o_part_count(_ptr(codes), bd.code_bytes, rs, fs, _ptr(ridx), _ptr(work), nw, _ptr(feat_t),
+                                    _ptr(masks), bd.Bs, _ptr(cnt), _stream())
         if rc != 0:
             raise RuntimeError(f"h2o_part_count failed: {rc}")
         # per-node exclusive scans of the chunk counts (chunks of a node are
@@ -270,6 +284,12 @@ def partition(bd, ridx, ridx_out, feats, masks, starts, counts, use_native=None,
         loff_d = torch.from_numpy(loff).to(dev, non_blocking=True)
         roff_d = torch.from_numpy(roff).to(dev, non_blocking=True)
         pa, pb, pa_o, pb_o = payload if payload is not None else (None, None, None, None)
+        if ballot:
+            rc = lib.h2o_part_compact(_ptr(ridx), _ptr(work), _ptr(fbase), nw, _ptr(flags), _ptr(loff_d),
+                                      _ptr(roff_d), _ptr(ridx_out), _ptr(pa), _ptr(pa_o), _stream())
+            if rc != 0:
+                raise RuntimeError(f"h2o_part_compact failed: {rc}")
+            return nleft.tolist()
         rc = lib.h2o_part_scatter(_ptr(codes), bd.code_bytes, rs, fs, _ptr(ridx), _ptr(work), nw, _ptr(feat_t),
                                   _ptr(masks), bd.Bs, _ptr(loff_d), _ptr(roff_d), _ptr(ridx_out), _ptr(pa), _ptr(pb),
                                   _ptr(pa_o), _ptr(pb_o), _stream())

@@ -47,17 +47,21 @@ def test_hist_build_matches_reference(nbins, mode, kernel, monkeypatch):
     torch.testing.assert_close(h_gpu, h_ref, rtol=1e-4, atol=1e-3)
 
 
-def test_partition_matches_reference():
+@pytest.mark.parametrize("impl", ["ballot", "old"])
+def test_partition_matches_reference(impl, monkeypatch):
     _need_gpu()
+    monkeypatch.setenv("H2O3_PART", impl)
     from h2o3_amd.ops import tree_ops
     bd, _ = _binned(n=50000)
     n = bd.nrows_local
     ridx = torch.arange(n, dtype=torch.int32, device="cuda")
     starts, counts = [0, 20000, 45000], [20000, 25000, 5000]
+    if impl == "ballot":
+        starts, counts = [0, 20003, 45001], [19999, 24998, 4999]   # unaligned segments
     feats = [0, 4, 7]
     masks = (torch.rand((3, bd.Bs), device="cuda") < 0.5).to(torch.uint8)
-    out_g = torch.empty_like(ridx)
-    out_r = torch.empty_like(ridx)
+    out_g = ridx.clone()
+    out_r = ridx.clone()
     nl_g = tree_ops.partition(bd, ridx, out_g, feats, masks, starts, counts, use_native=True, chunk=4096)
     nl_r = tree_ops.partition(bd, ridx, out_r, feats, masks, starts, counts, use_native=False)
     assert nl_g == nl_r
