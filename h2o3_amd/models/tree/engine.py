@@ -162,11 +162,16 @@ class TreeGrower:
                                                   device=H.device)], 0)
                 H = coll.reduce_scatter_dim0(H)
             return H
-        if mode == 0 and getattr(self, "_va_eff", None) is not None:
+        posv = self.use_payload
+        if mode == 0 and getattr(self, "_pos1", None) is not None:
+            # NaN-masked responses kept in POSITION order (moved by the partition
+            # compaction): the histogram reads them coalesced, no row gather
+            va, vb, posv = self._pos1[0], None, True
+        elif mode == 0 and getattr(self, "_va_eff", None) is not None:
             va, vb = self._va_eff, None   # 0/1 weights folded into NaN-masked responses
         with phase("tree.hist"), phase(f"tree.hist.L{getattr(self, '_level', 0)}"):
             H, wyy = tree_ops.hist_build(self.bd, ridx, va, vb, mode, starts, counts, len(starts), vmax=self._vmax,
-                                         posv=self.use_payload, want_wyy=True,
+                                         posv=posv, want_wyy=True,
                                          unit_w=getattr(self, "_unit_w", False))
         if wyy is not None:
             coll.allreduce_(wyy)
@@ -468,8 +473,13 @@ class TreeGrower:
         self._va_eff = None
         quad = self.bd.code_bytes == 1 and self.bd.Bs <= 256 and self.bd.Fp % 16 == 0 and \
             os.environ.get("H2O3_HIST_KERNEL", "quad") == "quad"
-        if self._unit_w and vb is not None and not self.use_payload and quad:
-            self._va_eff = torch.where(vb > 0, va, torch.full_like(va, float("nan")))
+        if self._unit_w and not self.use_payload and quad:
+            self._va_eff = torch.where(vb > 0, va, torch.full_like(va, float("nan"))) if vb is not None else va
+        self._pos1 = None
+        if self._va_eff is not None and os.environ.get("H2O3_POSV", "1") == "1" and \
+                os.environ.get("H2O3_PART", "ballot") == "ballot":
+            p0 = self._va_eff.clone() if self._va_eff is va else self._va_eff
+            self._pos1 = [p0, torch.empty_like(p0)]   # root: position order == row order
         ridx, ridx2 = self.ridx, self.ridx2
         pa, pb, pa2, pb2 = self._pay
         if self.use_payload:
@@ -606,8 +616,13 @@ class TreeGrower:
                 if self.use_payload:
                     pa2.copy_(pa)
                     pb2.copy_(pb)
+                pay = (pa, pb, pa2, pb2) if self.use_payload else None
+                if self._pos1 is not None:
+                    pay = (self._pos1[0], None, self._pos1[1], None)
                 nleft = tree_ops.partition(bd, ridx, ridx2, part_feats, masks, part_starts, part_counts,
-                                           payload=(pa, pb, pa2, pb2) if self.use_payload else None)
+                                           payload=pay)
+                if self._pos1 is not None:
+                    self._pos1.reverse()
             ridx, ridx2 = ridx2, ridx
             if self.use_payload:
                 pa, pa2, pb, pb2 = pa2, pa, pb2, pb
