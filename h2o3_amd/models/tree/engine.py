@@ -459,7 +459,7 @@ class TreeGrower:
         return out
 
     # ------------------------------------------------------------------ grow
-    def grow(self, va, vb, mode, tree_node_hook=None):
+    def grow(self, va, vb, mode, tree_node_hook=None, want_nid=True):
         """Grow one tree.  Returns (Tree, nid[N] leaf index per local row,
         leaf_nodes list (tree node ids, indexed by nid), leaf_tot [n_leaves, C])."""
         bd, p = self.bd, self.p
@@ -650,8 +650,10 @@ class TreeGrower:
         self._leaf_segments = []
         leaf_index = {nid_: k for k, nid_ in enumerate(leaves)}
         lids = [leaf_index[s[0]] for s in segs]
-        with phase("tree.nid"):
-            nid = tree_ops.fill_nid(ridx, lids, [s[1] for s in segs], [s[2] for s in segs], N)
+        nid = None
+        if want_nid:
+            with phase("tree.nid"):
+                nid = tree_ops.fill_nid(ridx, lids, [s[1] for s in segs], [s[2] for s in segs], N)
         self.ridx, self.ridx2 = ridx, ridx2
         self._pay = [pa, pb, pa2, pb2]
         self.last_segs = (lids, [s[1] for s in segs], [s[2] for s in segs])

@@ -193,10 +193,21 @@ class GBMDriver:
             if self.dist.family == "huber":
                 self._update_huber_delta(y, f, w)
                 z = self.dist.neg_half_gradient(y, f).to(torch.float32)
+            fused = self.dev.type == "cuda" and self.dist.family in ("gaussian", "bernoulli") and \
+                self.dist.link in ("identity", "logit")
             with phase("gbm.grow"):
-                tree, nid, leaves, tot = self.grower.grow(z.contiguous(), w.contiguous(), 0)
+                tree, nid, leaves, tot = self.grower.grow(z.contiguous(), w.contiguous(), 0, want_nid=not fused)
             with phase("gbm.gamma"):
-                vals = self._gamma(tree, nid, leaves, w, y, z, f, 0)
+                if fused:
+                    # one walk over the leaf segments: nid fill + gamma sums
+                    lids, st, ct = self.grower.last_segs
+                    nid, s_ = tree_ops.leaf_pass(self.grower.ridx, z, w, lids, st, ct, len(leaves), z.shape[0],
+                                                 1 if self.dist.family == "bernoulli" else 0)
+                    coll.allreduce_(s_)
+                    sh = s_.cpu().numpy()
+                    vals = np.where(sh[:, 1] != 0, sh[:, 0] / np.where(sh[:, 1] == 0, 1, sh[:, 1]), 0.0)
+                else:
+                    vals = self._gamma(tree, nid, leaves, w, y, z, f, 0)
             vals = np.clip(vals, -maxabs, maxabs)
             for li, node in enumerate(leaves):
                 tree.value[node] = float(lr * vals[li])

@@ -642,6 +642,61 @@ __global__ __launch_bounds__(256) void seg_sum2_kernel(const int* __restrict__ r
   }
 }
 
+// Fused leaf pass (GBM gaussian / bernoulli): nid[ridx[p]] = leaf and the
+// leaf's gamma sums in ONE walk over the leaf segments.
+//   mode 0 (gaussian):  (sum w z, sum w)
+//   mode 1 (bernoulli): (sum w z, sum w |z| (1 - |z|))   (z = y - p, so p(1-p) = |z|(1-|z|))
+// work[i] = (leaf_id, start, count, -)
+__global__ __launch_bounds__(256) void leaf_pass_kernel(const int* __restrict__ ridx, const float* __restrict__ z,
+                                                        const float* __restrict__ w, const int4* __restrict__ work,
+                                                        int mode, int* __restrict__ nid, double* __restrict__ out) {
+  const int4 wk = work[blockIdx.x];
+  double sa = 0.0, sb = 0.0;
+  const int end = wk.y + wk.z;
+  constexpr int U = 4;
+  for (int p0 = wk.y + threadIdx.x; p0 < end; p0 += U * 256) {
+    int r[U];
+    float zz[U], ww[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) r[u] = ridx[min(p0 + u * 256, end - 1)];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      zz[u] = z[r[u]];
+      ww[u] = w ? w[r[u]] : 1.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (p0 + u * 256 < end) {
+        nid[r[u]] = wk.x;
+        const double wz = (double)ww[u] * (double)zz[u];
+        sa += wz;
+        if (mode == 1) {
+          const double az = fabs((double)zz[u]);
+          sb += (double)ww[u] * az * (1.0 - az);
+        } else {
+          sb += (double)ww[u];
+        }
+      }
+    }
+  }
+  sa = wave_sum(sa);
+  sb = wave_sum(sb);
+  __shared__ double red[2][4];
+  if (lane_id() == 0) { red[0][wave_id()] = sa; red[1][wave_id()] = sb; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    gbl_add(out + 2 * wk.x, red[0][0] + red[0][1] + red[0][2] + red[0][3]);
+    gbl_add(out + 2 * wk.x + 1, red[1][0] + red[1][1] + red[1][2] + red[1][3]);
+  }
+}
+
+extern "C" int h2o_leaf_pass(const int* ridx, const float* z, const float* w, const int* work, int n_work, int mode,
+                             int* nid, double* out, hipStream_t s) {
+  if (n_work <= 0) return 0;
+  hipLaunchKernelGGL(leaf_pass_kernel, dim3(n_work), dim3(256), 0, s, ridx, z, w, (const int4*)work, mode, nid, out);
+  return (int)hipGetLastError();
+}
+
 extern "C" int h2o_seg_sum2(const int* ridx, const float* a, const float* b, const int* work, int n_work, double* out,
                             hipStream_t s) {
   if (n_work <= 0) return 0;

@@ -337,6 +337,28 @@ def fill_nid(ridx, leaf_ids, starts, counts, nrows, use_native=None):
     return nid
 
 
+def leaf_pass(ridx, z, w, leaf_ids, starts, counts, n_leaves, nrows, mode, chunk=65536):
+    """Fused nid fill + per-leaf gamma sums (native only).  Returns (nid, [L, 2] f64)."""
+    dev = ridx.device
+    lib = _lib()
+    if not getattr(lib, "_typed_leaf", False):
+        lib.h2o_leaf_pass.argtypes = [_c_void, _c_void, _c_void, _c_void, _c_int, _c_int, _c_void, _c_void, _c_void]
+        lib._typed_leaf = True
+    out = torch.zeros((n_leaves, 2), dtype=torch.float64, device=dev)
+    nid = torch.zeros(nrows, dtype=torch.int32, device=dev)
+    items = make_work(starts, counts, leaf_ids, chunk)
+    if len(items) == 0:
+        return nid, out
+    work = torch.from_numpy(items).to(dev, non_blocking=True)
+    z = z.to(torch.float32).contiguous()
+    w = None if w is None else w.to(torch.float32).contiguous()
+    rc = lib.h2o_leaf_pass(_ptr(ridx), _ptr(z), _ptr(w), _ptr(work), len(items), int(mode), _ptr(nid), _ptr(out),
+                           _stream())
+    if rc != 0:
+        raise RuntimeError(f"h2o_leaf_pass failed: {rc}")
+    return nid, out
+
+
 def seg_sum2(ridx, a, b, leaf_ids, starts, counts, n_leaves, use_native=None, chunk=65536):
     """Per-leaf sums of a[r] (and b[r]) over leaf segments of ridx -> [L, 2] f64."""
     dev = ridx.device
