@@ -148,7 +148,7 @@ __global__ __launch_bounds__(512) void hist_build_kernel(
 // count and (low - count * Bq) / s1.  Halves the LDS atomics of the
 // unweighted GBM / sampled DRF histograms; the response is quantised at
 // 1/s1 = chunk * 2 * vmax / 2^40 (f32-level resolution, exact summation).
-template <int MODE, bool HAS_VB, bool POSV, bool PACK>
+template <int MODE, bool HAS_VB, bool POSV, bool PACK, int FG = 16>
 __global__ __launch_bounds__(512) void hist_quad_kernel(
     const uint8_t* __restrict__ codes, int Fp, const int* __restrict__ ridx,
     const float* __restrict__ va, const float* __restrict__ vb,
@@ -156,7 +156,8 @@ __global__ __launch_bounds__(512) void hist_quad_kernel(
     double* __restrict__ hist, int n_slots, double* __restrict__ wyy_out, long long bq) {
   constexpr int C = Chan<MODE>::C;
   constexpr int CL = PACK ? 1 : C;       // u64 entries per bin in LDS
-  constexpr int FG = 16;
+  constexpr int LPR = FG / 4;            // lanes per row (one dword of codes each)
+  constexpr int RPW = 64 / LPR;          // rows per wave instruction
   extern __shared__ __attribute__((aligned(16))) unsigned long long ldsq[];
   const int nwg = n_work * n_fg;
   const int lb = xcd_remap(blockIdx.x, nwg);
@@ -169,14 +170,14 @@ __global__ __launch_bounds__(512) void hist_quad_kernel(
   for (int i = threadIdx.x; i < total; i += blockDim.x) ldsq[i] = 0ull;
   __syncthreads();
   const int lane = threadIdx.x & 63;
-  const int q = lane & 3;          // feature quad
-  const int rs = lane >> 2;        // row within the wave instruction (16)
+  const int q = lane % LPR;        // feature quad
+  const int rs = lane / LPR;       // row within the wave instruction
   const int wv = threadIdx.x >> 6;
   const int nwaves = blockDim.x >> 6;
   const bool do_wyy = (MODE == 0) && wyy_out != nullptr && fgi == 0 && q == 0;
   double wyy = 0.0;
   const int pend = wk.y + wk.z;
-  const int step = nwaves * 16;
+  const int step = nwaves * RPW;
   constexpr int U = 4;
   const uint8_t* cbase = codes + fg0 + 4 * q;
   unsigned long long* hb[4];
@@ -185,7 +186,7 @@ __global__ __launch_bounds__(512) void hist_quad_kernel(
   bool fk[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) fk[k] = 4 * q + k < nf;
-  for (int p0 = wk.y + wv * 16 + rs; p0 < pend; p0 += U * step) {
+  for (int p0 = wk.y + wv * RPW + rs; p0 < pend; p0 += U * step) {
     int rr[U];
     unsigned int cw[U];
     float c0[U], c1[U], yv[U];
@@ -273,14 +274,15 @@ __global__ __launch_bounds__(512) void hist_quad_kernel(
 extern "C" int h2o_hist_quad(const void* codes, int Fp, const int* ridx, const float* va, const float* vb,
                              const int* work, int n_work, int F, int Bs, float s0, float s1, double* hist,
                              int n_slots, int mode, int threads, double* wyy, int posv, long long pack_bq,
-                             hipStream_t s) {
+                             int fg, hipStream_t s) {
   if (n_work <= 0) return 0;
   if (Fp % 16 != 0 || Bs > 256) return -1;
   const bool pack = pack_bq >= 0 && mode == 0;
-  const int n_fg = (F + 15) / 16;
+  if (!pack || (fg != 32 && fg != 64) || Fp % fg != 0) fg = 16;
+  const int n_fg = (F + fg - 1) / fg;
   const int C = mode == 2 ? 1 : 2;
   const int CL = pack ? 1 : C;
-  const size_t lds = (size_t)16 * (Bs * CL + CL) * sizeof(unsigned long long);
+  const size_t lds = (size_t)fg * (Bs * CL + CL) * sizeof(unsigned long long);
   const dim3 grid(n_work * n_fg);
   const uint8_t* cc = (const uint8_t*)codes;
   const int4* wk = (const int4*)work;
@@ -289,8 +291,14 @@ extern "C" int h2o_hist_quad(const void* codes, int Fp, const int* ridx, const f
                                                  wyy, pack_bq)
 #define H2O_LQ(M, V) if (posv) H2O_LQ2(M, V, true, false); else H2O_LQ2(M, V, false, false)
   if (pack) {
-    if (vb) { if (posv) H2O_LQ2(0, true, true, true); else H2O_LQ2(0, true, false, true); }
-    else { if (posv) H2O_LQ2(0, false, true, true); else H2O_LQ2(0, false, false, true); }
+#define H2O_LQF(V, PV, G) hipLaunchKernelGGL((hist_quad_kernel<0, V, PV, true, G>), grid, dim3(threads), lds, s, cc, \
+                                             Fp, ridx, va, vb, wk, n_work, n_fg, F, Bs, s0, s1, hist, n_slots, \
+                                             wyy, pack_bq)
+#define H2O_LQG(V, PV) if (fg == 64) H2O_LQF(V, PV, 64); else if (fg == 32) H2O_LQF(V, PV, 32); else H2O_LQF(V, PV, 16)
+    if (vb) { if (posv) H2O_LQG(true, true); else H2O_LQG(true, false); }
+    else { if (posv) H2O_LQG(false, true); else H2O_LQG(false, false); }
+#undef H2O_LQG
+#undef H2O_LQF
     return (int)hipGetLastError();
   }
   switch (mode) {

@@ -36,7 +36,7 @@ def _lib():
                                        _c_int, _c_void, _c_int, _c_void]
         lib.h2o_hist_quad.argtypes = [_c_void, _c_int, _c_void, _c_void, _c_void, _c_void, _c_int, _c_int, _c_int,
                                       ctypes.c_float, ctypes.c_float, _c_void, _c_int, _c_int, _c_int, _c_void,
-                                      _c_int, _c_ll, _c_void]
+                                      _c_int, _c_ll, _c_int, _c_void]
         lib.h2o_part_flags.argtypes = [_c_void, _c_int, _c_ll, _c_ll, _c_void, _c_void, _c_void, _c_int, _c_void,
                                        _c_void, _c_int, _c_void, _c_void, _c_void]
         lib.h2o_part_compact.argtypes = [_c_void, _c_void, _c_void, _c_int, _c_void, _c_void, _c_void, _c_void,
@@ -152,7 +152,11 @@ def hist_build(bd, ridx, va, vb, mode, starts, counts, n_slots, use_native=None,
         lib = _lib()
         quad = bd.code_bytes == 1 and bd.Fp % 16 == 0 and bd.Bs <= 256 and \
             os.environ.get("H2O3_HIST_KERNEL", "quad") == "quad"
-        FG = 16 if quad else feature_group(bd.F, bd.Bs, mode)
+        qfg = int(os.environ.get("H2O3_HIST_FG", "16"))
+        pack_ok = quad and mode == 0 and unit_w and os.environ.get("H2O3_HIST_PACK", "1") == "1"
+        if not pack_ok or qfg not in (32, 64) or bd.Fp % qfg != 0:
+            qfg = 16
+        FG = qfg if quad else feature_group(bd.F, bd.Bs, mode)
         n_fg = (bd.F + FG - 1) // FG
         total = int(sum(counts))
         if total == 0:
@@ -173,7 +177,7 @@ def hist_build(bd, ridx, va, vb, mode, starts, counts, n_slots, use_native=None,
                 s1, bq = _pack_scale(vmax[1] if vb is None else max(vmax[1], 0.0), chunk)
             rc = lib.h2o_hist_quad(_ptr(bd.codes), bd.Fp, _ptr(ridx), _ptr(va), _ptr(vb), _ptr(work), len(items),
                                    bd.F, bd.Bs, s0, s1, _ptr(hist), n_slots, mode, 512, _ptr(wyy),
-                                   1 if posv else 0, bq, _stream())
+                                   1 if posv else 0, bq, qfg if bq >= 0 else 16, _stream())
             if rc != 0:
                 raise RuntimeError(f"h2o_hist_quad failed: hip error {rc}")
             return ret()

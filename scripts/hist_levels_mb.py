@@ -11,7 +11,7 @@ from h2o3_amd.models.tree.binning import BinnedData  # noqa: E402
 from h2o3_amd.ops import tree_ops  # noqa: E402
 
 N = int(os.environ.get("N", 100_000_000))
-F, Fp, Bs = 100, 112, 256
+F, Fp, Bs = 100, int(os.environ.get('FP', 128)), 256
 dev = "cuda"
 bd = BinnedData()
 bd.codes = torch.randint(0, 254, (N, Fp), dtype=torch.uint8, device=dev)
@@ -34,6 +34,10 @@ def run(name, ridx, starts, counts, reps=5, **kw):
 
 
 ident = torch.arange(N, dtype=torch.int32, device=dev)
+for fg in ("16", "32", "64"):
+    os.environ["H2O3_HIST_FG"] = fg
+    run(f"L0 all rows contiguous FG={fg}", ident, [0], [N], unit_w=True)
+os.environ["H2O3_HIST_FG"] = "16"
 run("L0 all rows contiguous", ident, [0], [N], unit_w=True)
 run("L0 all rows contiguous (no pack)", ident, [0], [N], unit_w=False)
 half = N // 2
