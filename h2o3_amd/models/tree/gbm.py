@@ -195,7 +195,7 @@ class GBMDriver:
                 self._update_huber_delta(y, f, w)
                 z = self.dist.neg_half_gradient(y, f).to(torch.float32)
             fused = self.dev.type == "cuda" and self.dist.family in ("gaussian", "bernoulli") and \
-                self.dist.link in ("identity", "logit") and os.environ.get("H2O3_FUSED_LEAF", "1") == "1"
+                self.dist.link in ("identity", "logit") and os.environ.get("H2O3_FUSED_LEAF", "0") == "1"
             with phase("gbm.grow"):
                 tree, nid, leaves, tot = self.grower.grow(z.contiguous(), w.contiguous(), 0, want_nid=not fused)
             with phase("gbm.gamma"):

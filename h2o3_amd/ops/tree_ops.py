@@ -152,7 +152,7 @@ def hist_build(bd, ridx, va, vb, mode, starts, counts, n_slots, use_native=None,
         lib = _lib()
         quad = bd.code_bytes == 1 and bd.Fp % 16 == 0 and bd.Bs <= 256 and \
             os.environ.get("H2O3_HIST_KERNEL", "quad") == "quad"
-        qfg = int(os.environ.get("H2O3_HIST_FG", "16"))
+        qfg = int(os.environ.get("H2O3_HIST_FG", "32"))
         pack_ok = quad and mode == 0 and unit_w and os.environ.get("H2O3_HIST_PACK", "1") == "1"
         if not pack_ok or qfg not in (32, 64) or bd.Fp % qfg != 0:
             qfg = 16
