@@ -77,6 +77,9 @@ class GBMDriver:
             valid = ~torch.isnan(self.yf)
         base_w = torch.ones(N, dtype=torch.float32, device=dev) if w is None else w.to(torch.float32)
         self.base_w = torch.where(valid, base_w, torch.zeros_like(base_w))
+        pp = est._parms
+        self._unit_weights = bool((self.base_w == 1).all()) and float(pp.get("sample_rate", 1.0)) >= 1.0 and \
+            pp.get("sample_rate_per_class") is None
         self.offset = spec.offset_tensor()
         # init prediction (reference: GBM.init -> initial value by distribution)
         if self.K == 1:
@@ -204,6 +207,17 @@ class GBMDriver:
                     lids, st, ct = self.grower.last_segs
                     nid, s_ = tree_ops.leaf_pass(self.grower.ridx, z, w, lids, st, ct, len(leaves), z.shape[0],
                                                  1 if self.dist.family == "bernoulli" else 0)
+                    coll.allreduce_(s_)
+                    sh = s_.cpu().numpy()
+                    vals = np.where(sh[:, 1] != 0, sh[:, 0] / np.where(sh[:, 1] == 0, 1, sh[:, 1]), 0.0)
+                elif self.dev.type == "cuda" and self.dist.family in ("gaussian", "bernoulli") and \
+                        self.dist.link in ("identity", "logit"):
+                    # gamma sums straight from the residual: den is w for gaussian and
+                    # w |z| (1 - |z|) = w p (1 - p) for bernoulli -> one gather per row
+                    lids, st, ct = self.grower.last_segs
+                    wu = None if self._unit_weights else w
+                    _, s_ = tree_ops.leaf_pass(self.grower.ridx, z, wu, lids, st, ct, len(leaves), z.shape[0],
+                                               1 if self.dist.family == "bernoulli" else 0, want_nid=False)
                     coll.allreduce_(s_)
                     sh = s_.cpu().numpy()
                     vals = np.where(sh[:, 1] != 0, sh[:, 0] / np.where(sh[:, 1] == 0, 1, sh[:, 1]), 0.0)

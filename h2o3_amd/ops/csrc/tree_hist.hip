@@ -675,7 +675,7 @@ __global__ __launch_bounds__(256) void leaf_pass_kernel(const int* __restrict__ 
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       if (p0 + u * 256 < end) {
-        nid[r[u]] = wk.x;
+        if (nid) nid[r[u]] = wk.x;
         const double wz = (double)ww[u] * (double)zz[u];
         sa += wz;
         if (mode == 1) {

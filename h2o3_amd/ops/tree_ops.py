@@ -341,15 +341,16 @@ def fill_nid(ridx, leaf_ids, starts, counts, nrows, use_native=None):
     return nid
 
 
-def leaf_pass(ridx, z, w, leaf_ids, starts, counts, n_leaves, nrows, mode, chunk=65536):
-    """Fused nid fill + per-leaf gamma sums (native only).  Returns (nid, [L, 2] f64)."""
+def leaf_pass(ridx, z, w, leaf_ids, starts, counts, n_leaves, nrows, mode, chunk=65536, want_nid=True):
+    """Per-leaf gamma sums from the raw residual z (one gather per row; w None
+    = unit weights), optionally fused with the nid fill.  Returns (nid, [L, 2] f64)."""
     dev = ridx.device
     lib = _lib()
     if not getattr(lib, "_typed_leaf", False):
         lib.h2o_leaf_pass.argtypes = [_c_void, _c_void, _c_void, _c_void, _c_int, _c_int, _c_void, _c_void, _c_void]
         lib._typed_leaf = True
     out = torch.zeros((n_leaves, 2), dtype=torch.float64, device=dev)
-    nid = torch.zeros(nrows, dtype=torch.int32, device=dev)
+    nid = torch.zeros(nrows, dtype=torch.int32, device=dev) if want_nid else None
     items = make_work(starts, counts, leaf_ids, chunk)
     if len(items) == 0:
         return nid, out
