@@ -259,8 +259,6 @@ class H2OExtendedIsolationForestEstimator(H2OEstimator):
                     P = len(nv)
             base += len(tr)
         P = P or 1
-        for tr in self._trees:
-            off = roots[len(lefts) and 0] if False else None
         base = 0
         for ti, tr in enumerate(self._trees):
             for nv, pt, l, r, v in tr:

@@ -227,6 +227,78 @@ class MojoModel:
                     contrib = np.where(np.isnan(x)[:, None], 0.0, -0.5 * z * z - np.log(sd[None] * math.sqrt(2 * math.pi)))
                 logp = logp + contrib
             return _softmax(logp)
+        if a == "extendedisolationforest":
+            X = np.nan_to_num(self._expand(df))
+            A = self._arr
+            n = X.shape[0]
+            tot = np.zeros(n)
+            for r in A["eif_roots"]:
+                nd = np.full(n, r)
+                for _ in range(m["height"] + 1):
+                    l = A["eif_left"][nd]
+                    act = l >= 0
+                    if not act.any():
+                        break
+                    proj = ((X - A["eif_point"][nd]) * A["eif_normal"][nd]).sum(1)
+                    nd = np.where(act, np.where(proj <= 0, l, A["eif_right"][nd]), nd)
+                tot += A["eif_value"][nd]
+            ml = tot / m["ntrees"]
+            psi = m["psi"]
+            c = 0.0 if psi <= 1 else (1.0 if psi == 2 else 2.0 * (math.log(psi - 1) + 0.5772156649) - 2.0 * (psi - 1) / psi)
+            return np.stack([np.power(2.0, -ml / c), ml], 1)
+        if a == "isotonicregression":
+            x = self._col(df, m["x"][0])
+            tx, ty = self._arr["thresholds_x"], self._arr["thresholds_y"]
+            p = np.interp(np.clip(x, tx[0], tx[-1]), tx, ty)
+            if m["out_of_bounds"].lower() != "clip":
+                p = np.where((x < tx[0]) | (x > tx[-1]), np.nan, p)
+            return np.where(np.isnan(x), np.nan, p).reshape(-1, 1)
+        if a == "coxph":
+            X = self._expand(df)
+            beta = self._arr["beta"]
+            lp = X @ beta
+            keys = list(self._arr["strata_keys"])
+            means = self._arr["strata_means"]
+            key = np.zeros(len(df), dtype=np.int64)
+            for c in m["stratify_by"]:
+                dom = m["strata_domains"].get(c)
+                codes = self._col(df, c, dom) if dom is not None else np.asarray(df[c], dtype=float)
+                codes = np.where(np.isnan(codes), -1, codes).astype(np.int64)
+                key = key * ((len(dom) + 1) if dom else 1_000_003) + codes + 1
+            base = np.array([means[keys.index(k)] @ beta if k in keys else np.nan for k in key])
+            return (lp - base).reshape(-1, 1)
+        if a == "upliftdrf":
+            X = self._tree_matrix(df)
+            s = self._forest(X, 2) / max(1, m["ntrees"])
+            return np.stack([s[:, 0] - s[:, 1], s[:, 0], s[:, 1]], 1)
+        if a == "word2vec":
+            vocab = self._z.read("vocabulary.txt").decode().split("\n")
+            idx = {w: i for i, w in enumerate(vocab)}
+            V = self._arr["vectors"]
+            col = df[df.columns[0]]
+            out = np.full((len(col), V.shape[1]), np.nan)
+            for i, wd in enumerate(col):
+                j = idx.get(wd) if isinstance(wd, str) else None
+                if j is not None:
+                    out[i] = V[j]
+            return out
+        if a == "targetencoder":
+            cols = []
+            tp = m["te_params"]
+            for c, t in m["te"].items():
+                dom = t["domain"]
+                codes = self._col(df, c, dom)
+                codes = np.where(np.isnan(codes), len(dom), codes).astype(int)
+                for k, suf in enumerate(m["suffix"]):
+                    num, den = np.asarray(t["num"][k])[codes], np.asarray(t["den"][k])[codes]
+                    prior = m["prior"][k]
+                    mean = np.where(den > 0, num / np.where(den > 0, den, 1), prior)
+                    if tp.get("blending"):
+                        kk, ff = float(tp.get("inflection_point", 10)), float(tp.get("smoothing", 20))
+                        lam = 1 / (1 + np.exp((kk - den) / ff))
+                        mean = lam * mean + (1 - lam) * prior
+                    cols.append(mean)
+            return np.stack(cols, 1) if cols else np.zeros((len(df), 0))
         if a == "stackedensemble":
             import pandas as pd
             cols = {}
@@ -253,6 +325,20 @@ class MojoModel:
         raw = self.predict_raw(df)
         if self.algo == "isolationforest":
             return pd.DataFrame({"predict": raw[:, 0], "mean_length": raw[:, 1]})
+        if self.algo == "extendedisolationforest":
+            return pd.DataFrame({"anomaly_score": raw[:, 0], "mean_length": raw[:, 1]})
+        if self.algo == "coxph":
+            return pd.DataFrame({"lp": raw[:, 0]})
+        if self.algo == "upliftdrf":
+            return pd.DataFrame(raw, columns=["uplift_predict", "p_y1_with_treatment", "p_y1_without_treatment"])
+        if self.algo == "word2vec":
+            return pd.DataFrame(raw, columns=[f"C{i + 1}" for i in range(raw.shape[1])])
+        if self.algo == "targetencoder":
+            names = [f"{c}{s}_te" for c in self.meta["te"] for s in self.meta["suffix"]]
+            out = df.copy()
+            for i, nm in enumerate(names):
+                out[nm] = raw[:, i]
+            return out
         if self.nclasses > 1 and self.response_domain:
             dom = self.response_domain
             if self.nclasses == 2:

@@ -78,7 +78,12 @@ def _category(model):
     if not model.supervised_learning:
         return {"kmeans": "Clustering", "pca": "DimReduction", "svd": "DimReduction", "glrm": "DimReduction",
                 "isolationforest": "AnomalyDetection", "extendedisolationforest": "AnomalyDetection",
-                "deeplearning": "AutoEncoder"}.get(model.algo, "Unknown")
+                "deeplearning": "AutoEncoder", "word2vec": "WordEmbedding",
+                "targetencoder": "TargetEncoder"}.get(model.algo, "Unknown")
+    if model.algo == "coxph":
+        return "CoxPH"
+    if model.algo == "upliftdrf":
+        return "BinomialUplift"
     if spec.nclasses == 2:
         return "Binomial"
     if spec.nclasses > 2:
@@ -181,6 +186,41 @@ def build_mojo(model) -> bytes:
                 w.add_array(f"nb_{i}_sd", t[2].cpu().numpy())
                 w.meta["nb"][c] = ["num", i]
         w.meta["nb_params"] = {k: model._parms[k] for k in ("min_sdev", "eps_sdev", "min_prob", "eps_prob")}
+    elif algo == "extendedisolationforest":
+        _dinfo_meta(w, model._dinfo)
+        for k in ("normal", "point", "left", "right", "value", "roots"):
+            w.add_array(f"eif_{k}", model._packed[k].cpu().numpy())
+        w.meta["psi"] = model._psi
+        w.meta["height"] = model._height
+        w.meta["ntrees"] = len(model._trees)
+    elif algo == "isotonicregression":
+        w.add_array("thresholds_x", np.asarray(model._tx))
+        w.add_array("thresholds_y", np.asarray(model._ty))
+        w.meta["out_of_bounds"] = str(model._parms.get("out_of_bounds", "NA"))
+    elif algo == "coxph":
+        _dinfo_meta(w, model._dinfo)
+        w.add_array("beta", model._beta.cpu().numpy())
+        keys = sorted(model._means)
+        w.add_array("strata_keys", np.asarray(keys, dtype=np.int64))
+        w.add_array("strata_means", np.stack([model._means[k].cpu().numpy() for k in keys]))
+        w.meta["stratify_by"] = list(model._parms.get("stratify_by") or [])
+        w.meta["strata_domains"] = getattr(model, "_strata_domains", {})
+    elif algo == "upliftdrf":
+        w.meta["x_domains"] = getattr(model, "_x_domains", {})
+        _forest_arrays(w, model._forest, spec.x)
+        w.meta["ntrees"] = len(model._forest) // 2
+    elif algo == "word2vec":
+        w.add_array("vectors", model._vecs.cpu().numpy())
+        w.files["vocabulary.txt"] = "\n".join(model._vocab)
+    elif algo == "targetencoder":
+        te = {}
+        for c, (dom, per) in model._tables.items():
+            te[c] = {"domain": dom, "num": [st[0].cpu().tolist() for st in per], "den": [st[1].cpu().tolist() for st in per]}
+        w.meta["te"] = te
+        w.meta["suffix"] = model._suffix
+        w.meta["prior"] = model._prior
+        w.meta["te_params"] = {k: model._parms.get(k) for k in ("blending", "inflection_point", "smoothing",
+                                                               "keep_original_categorical_columns")}
     elif algo == "stackedensemble":
         subs = []
         for i, bm in enumerate(model._base):
@@ -191,7 +231,7 @@ def build_mojo(model) -> bytes:
         w.meta["level1_names"] = model._names
     else:
         raise NotImplementedError(f"MOJO export not supported for {algo}")
-    cols = list(spec.x) + ([spec.y] if spec is not None and spec.y else [])
+    cols = (list(spec.x) + ([spec.y] if spec is not None and spec.y else [])) if spec is not None else []
     xd = getattr(model, "_x_domains", None) or (model._dinfo.domains if hasattr(model, "_dinfo") else {})
     for c in cols:
         if c in xd:
