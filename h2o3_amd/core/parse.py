@@ -40,8 +40,12 @@ def _files(path, pattern=None):
         if pattern:
             fs = [f for f in fs if re.search(pattern, os.path.basename(f))]
         return fs
+    if "://" in str(path):
+        from .persist import resolve
+        return [resolve(path)]
     g = sorted(glob.glob(path))
-    return g if g else [path]
+    from .persist import decompress
+    return [decompress(f) for f in g] if g else [path]
 
 
 def guess_sep(sample: str):

@@ -29,6 +29,7 @@ class H2OGridSearch:
         self.failed_params = []
         self._sort_metric = None
         self.export_checkpoints_dir = export_checkpoints_dir
+        self.recovery_dir = recovery_dir
 
     def _estimator_factory(self):
         m = self.model
@@ -57,7 +58,11 @@ class H2OGridSearch:
         t0 = time.time()
         make = self._estimator_factory()
         history = []
+        done = self._recover()
         for combo in self._combos():
+            key = repr(sorted(combo.items()))
+            if key in done:
+                continue
             if max_models and len(self.models) >= max_models:
                 break
             if max_rt and time.time() - t0 > max_rt:
@@ -71,6 +76,7 @@ class H2OGridSearch:
                           fold_column=fold_column, weights_column=weights_column, validation_frame=validation_frame)
                 est._grid_params = combo
                 self.models.append(est)
+                self._checkpoint(est, combo)
                 if stop_rounds:
                     history.append(self._metric_of(est))
                     if self._stop(history, sc):
@@ -79,6 +85,46 @@ class H2OGridSearch:
                 self.failed_params.append((combo, repr(e)))
         dkv.put(self.grid_id, self)
         return self
+
+    # ------------------------------------------------------------ recovery
+    # reference: hex/faulttolerance/Recovery.java + grid recovery_dir: every
+    # finished model and the grid state are written as they complete, so a
+    # restarted grid (same recovery_dir / grid_id) resumes where it stopped.
+    def _state_path(self):
+        import os
+        return os.path.join(self.recovery_dir, f"{self.grid_id}.grid.json")
+
+    def _checkpoint(self, est, combo):
+        import json
+        import os
+        from ..models.persist import save_model
+        for d in (self.export_checkpoints_dir, self.recovery_dir):
+            if d:
+                os.makedirs(d, exist_ok=True)
+                save_model(est, d, force=True)
+        if self.recovery_dir:
+            st = {"grid_id": self.grid_id, "hyper_params": {k: list(v) if isinstance(v, (list, tuple)) else v
+                                                            for k, v in self.hyper_params.items()},
+                  "search_criteria": self.search_criteria,
+                  "models": [{"model_id": m.model_id, "params": m._grid_params} for m in self.models]}
+            with open(self._state_path(), "w") as f:
+                json.dump(st, f, default=str)
+
+    def _recover(self):
+        import json
+        import os
+        from ..models.persist import load_model
+        if not self.recovery_dir or not os.path.exists(self._state_path()):
+            return set()
+        st = json.load(open(self._state_path()))
+        have = {m.model_id for m in self.models}
+        for rec in st["models"]:
+            if rec["model_id"] in have:
+                continue
+            m = load_model(os.path.join(self.recovery_dir, rec["model_id"]))
+            m._grid_params = rec["params"]
+            self.models.append(m)
+        return {repr(sorted(r["params"].items())) for r in st["models"]}
 
     def _default_metric(self):
         if not self.models:

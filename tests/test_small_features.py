@@ -63,3 +63,35 @@ def test_h2otree_jobs_timeline():
     assert t.root_node.split_feature in ("a", "k")
     assert m._job.status == "DONE"
     assert any(e["event"] == "model_build_done" and e["model_id"] == m.model_id for e in h2o.timeline())
+
+
+def test_persist_compressed_and_mrtask(tmp_path):
+    import gzip
+    import torch
+    from h2o3_amd.core.mrtask import map_reduce
+    h2o.init()
+    p = tmp_path / "d.csv.gz"
+    with gzip.open(p, "wt") as f:
+        f.write("a,b\n1,2\n3,4\n5,6\n")
+    fr = h2o.import_file(str(p))
+    assert fr.shape == (3, 2)
+    s = map_reduce(fr, lambda a, b: torch.stack([a.double().sum(), (a * b).double().sum()]))
+    assert s.tolist() == [9.0, 1 * 2 + 3 * 4 + 5 * 6]
+
+
+def test_grid_recovery(tmp_path):
+    from h2o3_amd.estimators import H2OGradientBoostingEstimator
+    from h2o3_amd.grid import H2OGridSearch
+    h2o.init()
+    rng = np.random.default_rng(0)
+    df = pd.DataFrame({"a": rng.normal(size=300)})
+    df["y"] = df.a * 2 + rng.normal(scale=0.1, size=300)
+    fr = h2o.H2OFrame(df)
+    g = H2OGridSearch(H2OGradientBoostingEstimator(ntrees=3), {"max_depth": [2, 3]}, grid_id="gr",
+                      recovery_dir=str(tmp_path))
+    g.train(x=["a"], y="y", training_frame=fr)
+    assert len(g.models) == 2
+    g2 = H2OGridSearch(H2OGradientBoostingEstimator(ntrees=3), {"max_depth": [2, 3, 4]}, grid_id="gr",
+                       recovery_dir=str(tmp_path))
+    g2.train(x=["a"], y="y", training_frame=fr)
+    assert len(g2.models) == 3   # two recovered, one new
