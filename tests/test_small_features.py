@@ -95,3 +95,20 @@ def test_grid_recovery(tmp_path):
                        recovery_dir=str(tmp_path))
     g2.train(x=["a"], y="y", training_frame=fr)
     assert len(g2.models) == 3   # two recovered, one new
+
+
+def test_sklearn_wrappers_and_transforms():
+    from h2o3_amd.sklearn import H2OGradientBoostingClassifier, H2OGeneralizedLinearRegressor
+    from h2o3_amd.transforms import H2OScaler
+    rng = np.random.default_rng(0)
+    X = rng.normal(size=(300, 3))
+    y = np.where(X[:, 0] + X[:, 1] > 0, "a", "b")
+    clf = H2OGradientBoostingClassifier(ntrees=10, max_depth=3).fit(X, y)
+    assert clf.score(X, y) > 0.9
+    assert clf.predict_proba(X).shape == (300, 2)
+    reg = H2OGeneralizedLinearRegressor(lambda_=0.0).fit(X, 2 * X[:, 0] + 1)
+    assert reg.score(X, 2 * X[:, 0] + 1) > 0.999
+    fr = h2o.H2OFrame(pd.DataFrame(X, columns=list("abc")))
+    sc = H2OScaler().fit(fr)
+    t = sc.transform(fr).as_data_frame()
+    assert abs(t["a"].mean()) < 1e-5 and abs(t["a"].std() - 1) < 1e-3
