@@ -262,6 +262,23 @@ class TreeGrower:
                                 ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
         if rc != 0:
             raise RuntimeError(f"h2o_split_find failed: {rc}")
+        if C == 2 and self.f0 < self.bd.F:
+            # fused per-node selection + mask kernel: few launches, one packed record
+            if not getattr(lib, "_typed_sel", False):
+                cv = ctypes.c_void_p
+                lib.h2o_split_select.argtypes = [cv, cv, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, cv,
+                                                 cv, cv]
+                lib._typed_sel = True
+            pk = torch.empty((n, 10), dtype=torch.float64, device=self.dev)
+            mask = torch.empty((n, Bs), dtype=torch.uint8, device=self.dev)
+            rc = lib.h2o_split_select(ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(H.data_ptr()), Fl, n, Bs,
+                                      self.f0, ctypes.c_void_p(pk.data_ptr()), ctypes.c_void_p(mask.data_ptr()),
+                                      ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+            if rc != 0:
+                raise RuntimeError(f"h2o_split_select failed: {rc}")
+            opt = pk[:, 3].long()
+            return {"gain": pk[:, 0], "feat": pk[:, 1].long(), "t": pk[:, 2].long(), "opt": opt,
+                    "na_left": opt == 1, "mask": mask, "L": pk[:, 4:6], "R": pk[:, 6:8], "tot": pk[:, 8:10]}
         gain = out[:, 0].view(n, Fl)
         ints = out.view(torch.int32).view(n * Fl, 8)[:, 6:8]
         best, fl = gain.max(1)
@@ -543,22 +560,31 @@ class TreeGrower:
                 node_wyy = wyy_level if mode == 0 else None
                 with phase("tree.split"):
                     sp = self._find_splits(H, cm, node_wyy)
-                gains = sp["gain"].cpu()
-                feats = sp["feat"].cpu()
-                Ls = sp["L"].cpu()
-                Rs = sp["R"].cpu()
-                tots = sp["tot"].cpu()
+                # ONE device->host transfer of every per-node scalar of the level
+                nn_ = n_front
+                pk = torch.cat([sp["gain"].view(nn_, 1).to(torch.float64), sp["feat"].view(nn_, 1).to(torch.float64),
+                                sp["t"].view(nn_, 1).to(torch.float64), sp["opt"].view(nn_, 1).to(torch.float64),
+                                sp["L"].to(torch.float64), sp["R"].to(torch.float64),
+                                sp["tot"].to(torch.float64)], 1).cpu().numpy()
+                gains = pk[:, 0].tolist()
+                feats = pk[:, 1].astype(np.int64).tolist()
+                t_l = pk[:, 2].astype(np.int64).tolist()
+                opt_l = pk[:, 3].astype(np.int64).tolist()
+                Ls = pk[:, 4:4 + C]
+                Rs = pk[:, 4 + C:4 + 2 * C]
+                tots = pk[:, 4 + 2 * C:4 + 3 * C]
             else:
                 # totals only
-                tots = self._totals(H) if H is not None else \
-                    torch.stack([child_tot[nd[0]] for nd in frontier])
+                tots = self._totals(H).numpy() if H is not None else \
+                    np.stack([child_tot[nd[0]] for nd in frontier])
                 gains = None
+            tots_l = tots.tolist()
             split_ids, split_slots = [], []
             for i, (nid_, st, ct, d) in enumerate(frontier):
-                tot_i = tots[i]
-                tree.weight[nid_] = float(tot_i[0] if mode != 1 else tot_i[1]) + (float(tot_i[2]) if mode == 3 else 0.0)
-                ok = can_split and gains is not None and math.isfinite(float(gains[i]))
-                if ok and p.criterion != "xgb" and float(tree.weight[nid_]) < 2 * p.min_rows:
+                tot_i = tots_l[i]
+                tree.weight[nid_] = (tot_i[0] if mode != 1 else tot_i[1]) + (tot_i[2] if mode == 3 else 0.0)
+                ok = can_split and gains is not None and math.isfinite(gains[i])
+                if ok and p.criterion != "xgb" and tree.weight[nid_] < 2 * p.min_rows:
                     ok = False
                 if ok and p.max_leaves and (len(leaves) + n_front + len(split_ids) + 1) > p.max_leaves:
                     ok = False
@@ -566,26 +592,26 @@ class TreeGrower:
                     split_ids.append(i)
                 else:
                     leaves.append(nid_)
-                    leaf_tot.append(tot_i)
+                    leaf_tot.append(tots[i])
                     # keep the segment for the nid pass
                     frontier[i].append("leaf")
             if not split_ids:
                 self._leaf_segments = [(f[0], f[1], f[2]) for f in frontier]
                 break
             # record splits in the tree
-            masks = sp["mask"][torch.tensor(split_ids, device=sp["mask"].device)]
-            masks_h = masks.cpu().numpy()
-            t_h = sp["t"].cpu()
-            opt_h = sp["opt"].cpu()
-            nal_h = sp["na_left"].cpu()
+            all_split = len(split_ids) == n_front
+            masks = sp["mask"] if all_split else sp["mask"][torch.tensor(split_ids, device=sp["mask"].device)]
+            any_cat = any(bd.is_cat[feats[i]] for i in split_ids)
+            masks_h = masks.cpu().numpy() if any_cat else None
             new_front, new_pairs = [], []
             part_starts, part_counts, part_feats = [], [], []
+            Ls_l, Rs_l = Ls.tolist(), Rs.tolist()
             for j, i in enumerate(split_ids):
                 nid_, st, ct, d = frontier[i][:4]
-                f = int(feats[i])
+                f = feats[i]
                 tree.feat[nid_] = f
-                tree.gain[nid_] = float(gains[i])
-                tree.na_left[nid_] = bool(nal_h[i])
+                tree.gain[nid_] = gains[i]
+                tree.na_left[nid_] = opt_l[i] == 1
                 if bd.is_cat[f]:
                     tree.is_cat[nid_] = True
                     card = bd.cat_card[f]
@@ -594,22 +620,23 @@ class TreeGrower:
                     tree.cat_left[nid_] = masks_h[j][np.minimum(lv, bd.Bs - 2)].astype(np.uint8)
                     tree.thr[nid_] = float("nan")
                 else:
-                    if int(opt_h[i]) == 2:
+                    if opt_l[i] == 2:
                         tree.thr[nid_] = float("inf")     # NA vs rest: every number goes left
                     else:
-                        tree.thr[nid_] = bd.split_value(f, int(t_h[i]))
-                    tree.split_code[nid_] = int(t_h[i])
-                lid = tree.add_node(d + 1, float(Ls[i][0]))
-                rid = tree.add_node(d + 1, float(Rs[i][0]))
+                        tree.thr[nid_] = bd.split_value(f, t_l[i])
+                    tree.split_code[nid_] = t_l[i]
+                Li, Ri = Ls_l[i], Rs_l[i]
+                lid = tree.add_node(d + 1, Li[0])
+                rid = tree.add_node(d + 1, Ri[0])
                 tree.left[nid_], tree.right[nid_] = lid, rid
                 part_starts.append(st)
                 part_counts.append(ct)
                 part_feats.append(f)
-                wl = float(Ls[i][0] if mode != 1 else Ls[i][1]) + (float(Ls[i][2]) if mode == 3 else 0.0)
-                wr = float(Rs[i][0] if mode != 1 else Rs[i][1]) + (float(Rs[i][2]) if mode == 3 else 0.0)
+                wl = (Li[0] if mode != 1 else Li[1]) + (Li[2] if mode == 3 else 0.0)
+                wr = (Ri[0] if mode != 1 else Ri[1]) + (Ri[2] if mode == 3 else 0.0)
                 new_pairs.append((lid, rid, j, wl <= wr))
-                child_tot[lid] = Ls[i].to(torch.float64)
-                child_tot[rid] = Rs[i].to(torch.float64)
+                child_tot[lid] = Ls[i]
+                child_tot[rid] = Rs[i]
             # partition
             with phase("tree.partition"):
                 ridx2.copy_(ridx)

@@ -174,3 +174,56 @@ extern "C" int h2o_split_find(const double* H, int Fl, int n, int Bs, const doub
                        lam, alpha, gamma, (SplitRec*)out);
   return (int)hipGetLastError();
 }
+
+// Per-node winner selection over the feature records of split_kernel and
+// the go-left code mask, so the host reads ONE packed [n, 10] record per level:
+//   pk[node] = {gain, feat(global), t, opt, L0, L1, R0, R1, T0, T1}
+// T = node totals from feature 0's histogram (H[0][node][:][c]); ties keep
+// the lowest feature (deterministic, matches torch max()).
+__global__ __launch_bounds__(64) void split_select_kernel(const SplitRec* __restrict__ rec, const double* __restrict__ H,
+                                                          int Fl, int n, int Bs, int f0, double* __restrict__ pk,
+                                                          uint8_t* __restrict__ mask) {
+  const int node = blockIdx.x;
+  const int lane = threadIdx.x;
+  double best = -INFINITY;
+  int bf = 0;
+  for (int f = lane; f < Fl; f += 64) {
+    const double g = rec[(size_t)node * Fl + f].gain;
+    if (g > best) { best = g; bf = f; }
+  }
+  // wave arg-max (lowest feature on ties)
+  for (int o = 32; o > 0; o >>= 1) {
+    const double og = __shfl_xor(best, o, 64);
+    const int of = __shfl_xor(bf, o, 64);
+    if (og > best || (og == best && of < bf)) { best = og; bf = of; }
+  }
+  double t0 = 0.0, t1 = 0.0;
+  for (int b = lane; b < Bs; b += 64) {
+    const double* h = H + ((size_t)node * Bs + b) * 2;   // feature 0
+    t0 += h[0];
+    t1 += h[1];
+  }
+  t0 = wave_sum(t0);
+  t1 = wave_sum(t1);
+  const SplitRec r = rec[(size_t)node * Fl + bf];
+  if (lane == 0) {
+    double* o = pk + (size_t)node * 10;
+    o[0] = best; o[1] = (double)(bf + f0); o[2] = (double)r.t; o[3] = (double)r.opt;
+    o[4] = r.lw; o[5] = r.ly; o[6] = t0 - r.lw; o[7] = t1 - r.ly; o[8] = t0; o[9] = t1;
+  }
+  const int B = Bs - 1;
+  for (int c = lane; c < Bs; c += 64) {
+    bool left;
+    if (c == Bs - 1) left = r.opt == 1;
+    else if (r.opt == 2) left = c < B;
+    else left = c <= r.t;
+    mask[(size_t)node * Bs + c] = left ? 1 : 0;
+  }
+}
+
+extern "C" int h2o_split_select(const void* rec, const double* H, int Fl, int n, int Bs, int f0, double* pk,
+                                uint8_t* mask, hipStream_t s) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(split_select_kernel, dim3(n), dim3(64), 0, s, (const SplitRec*)rec, H, Fl, n, Bs, f0, pk, mask);
+  return (int)hipGetLastError();
+}
