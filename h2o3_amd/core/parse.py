@@ -90,6 +90,18 @@ def import_file(path, destination_frame=None, header=0, sep=None, col_names=None
                        quotechar)
 
 
+def _guess_string(codes, sample=10000):
+    """String-vs-categorical guess (PreviewParseWriter.guessType: a column of
+    strings with almost no duplicates -- distinct >= 95% of the non-NA
+    values in the preview sample, more than one distinct value -- is T_STR)."""
+    c = np.asarray(codes[:sample])
+    c = c[c >= 0]
+    if c.size < 2:
+        return False
+    nd = np.unique(c).size
+    return nd > 1 and nd >= 0.95 * c.size
+
+
 def _import_csv(fs, dest, header, sep, col_names, col_types, na_strings, skipped, quotechar):
     from . import native_csv
     res = native_csv.parse_files(fs, sep=sep, header=header, na_strings=na_strings, quotechar=quotechar or '"')
@@ -124,6 +136,8 @@ def _import_csv(fs, dest, header, sep, col_names, col_types, na_strings, skipped
                              for x in col["values"][s:e]])
         elif kind == "cat":
             dom, codes = col["domain"], col["codes"]
+            if want is None and _guess_string(codes):
+                want = "string"
             if want in ("string", "uuid"):
                 arr = np.array(dom + [None], dtype=object)[np.where(codes < 0, len(dom), codes)]
                 v = make_string(arr[s:e])

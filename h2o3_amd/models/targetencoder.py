@@ -32,6 +32,16 @@ TE_DEFAULTS = dict(columns_to_encode=None, keep_original_categorical_columns=Tru
                    fold_column=None)
 
 
+def _sanitize(name):
+    """StringUtils.sanitizeIdentifier: non-identifier chars after the first -> '_'."""
+    s = str(name)
+    return s[:1] + "".join(ch if (ch.isalnum() or ch in "_$") else "_" for ch in s[1:])
+
+
+def _dlh(v):
+    return str(v or "None").lower().replace("_", "").replace("-", "")
+
+
 class H2OTargetEncoderEstimator(H2OEstimator):
     algo = "targetencoder"
     _defaults = TE_DEFAULTS
@@ -49,7 +59,7 @@ class H2OTargetEncoderEstimator(H2OEstimator):
         if spec.nclasses > 2:
             y = spec.y_tensor().long()
             return [(y == k).to(torch.float64) for k in range(1, spec.nclasses)], \
-                [f"_{spec.response_domain[k]}" for k in range(1, spec.nclasses)], y >= 0
+                [f"_{_sanitize(spec.response_domain[k])}" for k in range(1, spec.nclasses)], y >= 0
         if spec.nclasses == 2:
             y = spec.y_tensor().long()
             return [(y == 1).to(torch.float64)], [""], y >= 0
@@ -99,6 +109,7 @@ class H2OTargetEncoderEstimator(H2OEstimator):
                     fper.append(st)
                 self._fold_tables[c] = fper
         self._output["encoded_columns"] = [f"{c}{s}_te" for c in cols for s in suf]
+        self._train_names = list(spec.frame.names)
         self._output["priors"] = self._prior
 
     def _blend(self, num, den, prior):
@@ -123,7 +134,7 @@ class H2OTargetEncoderEstimator(H2OEstimator):
 
     def _transform(self, frame, as_training, noise):
         p = self._parms
-        dlh = str(p.get("data_leakage_handling") or "None").lower()
+        dlh = _dlh(p.get("data_leakage_handling"))
         if noise is None:
             noise = float(p.get("noise", 0.01)) if as_training else 0.0
         seed = p.get("seed", -1)
@@ -157,13 +168,31 @@ class H2OTargetEncoderEstimator(H2OEstimator):
                 if noise and noise > 0:
                     r = (torch.rand(enc.shape[0], generator=gen, dtype=torch.float64) * 2 - 1) * noise
                     enc = enc + r.to(enc.device)
-                out_vecs.append(Vec(enc.to(torch.float32), T_REAL))
+                out_vecs.append(Vec(enc.to(torch.float64).contiguous(), T_REAL))  # doubles, as the reference
                 out_names.append(f"{c}{suf}_te")
             if not p.get("keep_original_categorical_columns", True):
                 i = out_names.index(c)
                 out_vecs.pop(i)
                 out_names.pop(i)
-        return H2OFrame.from_vecs(out_vecs, out_names)
+        return self._reorder(H2OFrame.from_vecs(out_vecs, out_names))
+
+    def _reorder(self, fr):
+        """TargetEncoderModel.reorderColumns: non-categorical training
+        columns, TE columns, remaining categoricals, columns not seen in
+        training, then non-predictors (weights, offset, fold, response)."""
+        spec = self._spec
+        tail = [c for c in (spec.weights_column, spec.offset_column, self._parms.get("fold_column"), spec.y) if c]
+        train_cols = list(self._train_names)
+        enc = [n for n in self._output["encoded_columns"] if n in fr.names]
+        first, later = [], []
+        for c in train_cols:
+            if c in fr.names and c not in tail:
+                (later if fr.vec(c).type == T_ENUM else first).append(c)
+        seen = set(train_cols) | set(enc)
+        later += [c for c in fr.names if c not in seen]
+        later += [c for c in tail if c in fr.names]
+        order = first + enc + later
+        return fr[order] if order != list(fr.names) else fr
 
     def _cross_validate(self, spec):
         pass  # the fold column drives out-of-fold encoding, not model CV
