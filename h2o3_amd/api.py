@@ -290,6 +290,239 @@ def permutation_importance(model, frame, metric="AUTO", n_samples=10000, n_repea
     return model.permutation_importance(frame, metric, n_samples, n_repeats, features, seed)
 
 
+def connection():
+    """The 'connection' of an in-process cloud is the cloud itself."""
+    return cluster()
+
+
+def cluster_status():
+    cluster().show_status(True)
+
+
+def network_test():
+    """Collective bandwidth probe across the ranks (water/init/NetworkTest.java analogue):
+    times an all-reduce of 1 KB .. 64 MB and reports GB/s per size."""
+    import time
+    import torch
+    from .parallel import collectives as coll
+    dev = cloud.device()
+    rows = []
+    for nbytes in (1 << 10, 1 << 16, 1 << 20, 1 << 24, 1 << 26):
+        t = torch.ones(nbytes // 4, dtype=torch.float32, device=dev)
+        coll.allreduce_(t)
+        cloud.barrier()
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(5):
+            coll.allreduce_(t)
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / 5
+        rows.append({"bytes": nbytes, "seconds": dt, "GB/s": nbytes / max(dt, 1e-12) / 1e9})
+    import pandas as pd
+    return pd.DataFrame(rows)
+
+
+def estimate_cluster_mem(ncols, nrows, num_cols=0, string_cols=0, cat_cols=0, time_cols=0, uuid_cols=0):
+    """Estimated device memory (GB, rounded up) to hold a frame in this platform's
+    layout: f32 numerics, int32 enum codes, f64 epoch-ms times; strings/UUIDs live in
+    host memory and are counted at their average host size.  Same arguments and
+    validation as h2o-py/h2o/h2o.py:2408, which prices the JVM's compressed chunks."""
+    import math
+    for nm, v in (("ncols", ncols), ("nrows", nrows), ("num_cols", num_cols), ("string_cols", string_cols),
+                  ("cat_cols", cat_cols), ("time_cols", time_cols), ("uuid_cols", uuid_cols)):
+        if v < 0:
+            raise ValueError(f"{nm} can't be a negative number")
+    known = num_cols + string_cols + uuid_cols + cat_cols + time_cols
+    if known > ncols:
+        raise ValueError("There can not be more specific columns then columns in total")
+    unknown = ncols - known
+    per_row = 4 * (unknown + num_cols) + 4 * cat_cols + 8 * time_cols + 64 * string_cols + 16 * uuid_cols
+    # x2 headroom for model state (binned codes, gradients, histograms) + 256 MB runtime
+    return math.ceil((per_row * nrows * 2 + (256 << 20)) / (1 << 30))
+
+
+def as_list(data, use_pandas=True, header=True):
+    """Python object from a frame (h2o-py/h2o/h2o.py:1895)."""
+    return data.as_data_frame(use_pandas=use_pandas, header=header)
+
+
+def frame(frame_id):
+    """Metadata of a frame by id (columns, types, rows)."""
+    fr = dkv.get(frame_id)
+    if fr is None:
+        raise KeyError(frame_id)
+    return {"frame_id": frame_id, "rows": fr.nrows, "columns": [
+        {"label": n, "type": t} for n, t in fr.types.items()]}
+
+
+def import_frame(path=None, **kw):
+    return import_file(path, **kw)
+
+
+def lazy_import(path, pattern=None):
+    """Resolve the files an import would read (no parse)."""
+    from .core import parse as P
+    if hasattr(P, "resolve_paths"):
+        return P.resolve_paths(path, pattern)
+    import glob as _g
+    paths = path if isinstance(path, (list, tuple)) else [path]
+    out = []
+    for p in paths:
+        if os.path.isdir(p):
+            import re
+            out += sorted(os.path.join(p, f) for f in os.listdir(p) if not pattern or re.search(pattern, f))
+        else:
+            out += sorted(_g.glob(p)) or [p]
+    return out
+
+
+def parse_raw(setup, id=None, first_line_is_header=0):
+    """Parse the files of a parse_setup() result."""
+    paths = setup.get("source_frames") or setup.get("paths") or setup.get("path")
+    return import_file(paths, destination_frame=id or setup.get("destination_frame"),
+                       header=first_line_is_header or setup.get("check_header", 0),
+                       sep=setup.get("separator"), col_names=setup.get("column_names"),
+                       col_types=setup.get("column_types"), na_strings=setup.get("na_strings"))
+
+
+def parse(*a, **k):
+    """Deprecated no-op in the reference client."""
+    return None
+
+
+def import_sql_select(connection_url, select_query, username=None, password=None, optimize=True, **kw):
+    """SQL import through a DB-API connection: sqlite URLs (jdbc:sqlite:<path>) are
+    served by Python's sqlite3; other JDBC drivers are not available here."""
+    import sqlite3
+    import pandas as pd
+    url = connection_url
+    if url.startswith("jdbc:sqlite:"):
+        url = url[len("jdbc:sqlite:"):]
+    elif url.startswith("jdbc:"):
+        raise NotImplementedError("only jdbc:sqlite: URLs are supported (no JDBC drivers here)")
+    con = sqlite3.connect(url)
+    try:
+        df = pd.read_sql_query(select_query, con)
+    finally:
+        con.close()
+    return H2OFrame(df)
+
+
+def download_csv(data, filename):
+    data.as_data_frame().to_csv(filename, index=False)
+    return filename
+
+
+def download_pojo(model, path="", get_jar=True, jar_name=""):
+    """Java scoring source for the model (hex/Model.toJava); see mojo/pojo.py."""
+    from .mojo.pojo import download_pojo as _dp
+    return _dp(model, path)
+
+
+def save_frame(frame, path, force=True):
+    return frame.save(path, force=force)
+
+
+def load_frame(frame_id, path, force=True):
+    from .core.frame_io import load_frame as _lf
+    return _lf(frame_id, path, force)
+
+
+def save_grid(grid_directory, grid_id, save_params_references=False, export_cross_validation_predictions=False):
+    from .grid import save_grid as _sg
+    return _sg(grid_directory, grid_id)
+
+
+def load_grid(grid_file_path, load_params_references=False):
+    from .grid import load_grid as _lg
+    return _lg(grid_file_path)
+
+
+def resume(recovery_dir=None):
+    """Resume grids / AutoML runs interrupted while writing to `recovery_dir`
+    (hex/faulttolerance/Recovery.java)."""
+    from .grid import resume_all
+    return resume_all(recovery_dir)
+
+
+def upload_custom_metric(func, func_file="metrics.py", func_name=None, class_name=None, source_provider=None):
+    from .core.udf import upload_custom_metric as _u
+    return _u(func, func_file, func_name, class_name, source_provider)
+
+
+def upload_custom_distribution(func, func_file="distributions.py", func_name=None, class_name=None,
+                               source_provider=None):
+    from .core.udf import upload_custom_distribution as _u
+    return _u(func, func_file, func_name, class_name, source_provider)
+
+
+def load_dataset(relative_path):
+    """Small bundled datasets: "iris" (from scikit-learn's copy, with h2o's column
+    names) and any CSV found under $H2O3_AMD_DATA."""
+    name = relative_path[:-4] if relative_path.endswith(".csv") else relative_path
+    roots = [p for p in os.environ.get("H2O3_AMD_DATA", "").split(os.pathsep) if p]
+    for r in roots:
+        for cand in (os.path.join(r, relative_path), os.path.join(r, name + ".csv")):
+            if os.path.exists(cand):
+                return upload_file(cand)
+    if name == "iris":
+        import pandas as pd
+        from sklearn.datasets import load_iris
+        d = load_iris()
+        df = pd.DataFrame(d.data, columns=["sepal_len", "sepal_wid", "petal_len", "petal_wid"])
+        df["class"] = pd.Categorical.from_codes(d.target, ["Iris-setosa", "Iris-versicolor", "Iris-virginica"])
+        return H2OFrame(df)
+    raise ValueError(f"Data file {relative_path} cannot be found")
+
+
+def demo(funcname, interactive=False, echo=True, test=False):
+    """Run a tiny end-to-end demo ("gbm", "glm" or "deeplearning") on iris."""
+    from . import estimators as E
+    fr = load_dataset("iris")
+    cls = {"gbm": E.H2OGradientBoostingEstimator, "glm": E.H2OGeneralizedLinearEstimator,
+           "deeplearning": E.H2ODeepLearningEstimator}[funcname]
+    kw = {"family": "multinomial"} if funcname == "glm" else {}
+    m = cls(**kw)
+    m.train(y="class", training_frame=fr)
+    if echo:
+        print(m)
+    return m
+
+
+def rapids(expr):
+    """Evaluate a Rapids expression string (water/rapids/Rapids.java) — see core/rapids.py."""
+    from .core.rapids import rapids as _r
+    return _r(expr)
+
+
+def enable_expr_optimizations(flag):
+    """Frames execute eagerly on the GPU; there is no lazy expression tree to optimise."""
+    _progress["expr_opt"] = bool(flag)
+
+
+def is_expr_optimizations_enabled():
+    return _progress.get("expr_opt", True)
+
+
+def import_hive_table(*a, **k):
+    raise NotImplementedError("Hive import needs a Hive metastore/JDBC stack, not available here")
+
+
+def download_all_logs(dirname=".", filename=None, container=None):
+    """Write the cloud's log records + timeline to a zip (water/api/LogsHandler)."""
+    import json
+    import zipfile
+    from .utils.log import timeline as _tl
+    os.makedirs(dirname, exist_ok=True)
+    path = os.path.join(dirname, filename or "h2o3_amd_logs.zip")
+    with zipfile.ZipFile(path, "w") as z:
+        z.writestr("timeline.json", json.dumps(_tl(), default=str))
+        z.writestr("jobs.json", json.dumps([getattr(j, "__dict__", str(j)) for j in jobs()], default=str))
+    return path
+
+
 def jobs():
     """All job records (water/Job.java list)."""
     from .core.job import jobs as _jobs

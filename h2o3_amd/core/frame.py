@@ -24,7 +24,7 @@ from ..parallel import cloud
 from ..parallel import collectives as coll
 from . import dkv
 from .vec import (NUMERIC_TYPES, T_ENUM, T_INT, T_REAL, T_STR, T_TIME, T_UUID, Vec, make_enum,
-                  make_enum_from_strings, make_numeric, make_string, make_time)
+                  make_enum_from_strings, make_numeric, make_string, make_time)  # noqa: F401
 
 _TYPE_ALIASES = {"numeric": T_REAL, "real": T_REAL, "float": T_REAL, "double": T_REAL, "int": T_INT,
                  "integer": T_INT, "enum": T_ENUM, "factor": T_ENUM, "categorical": T_ENUM,
@@ -1001,6 +1001,377 @@ class H2OFrame:
         from .strings import entropy
         return entropy(self)
 
+    # ------------------------------------------------------------ misc Rapids prims (h2o-py/h2o/frame.py parity)
+    @property
+    def dtype(self):
+        """numpy dtype of the first column (h2o-py/h2o/frame.py:370)."""
+        v = self._vecs[0]
+        if v.type in (T_STR, T_UUID, T_ENUM):
+            return np.dtype(object)
+        if v.type == T_TIME:
+            return np.dtype("datetime64[ms]")
+        return np.dtype(np.int64) if v.type == T_INT and v.nacnt() == 0 else np.dtype(np.float64)
+
+    def any_na_rm(self):
+        """True if any value of any column is non-zero, NAs ignored (AstAnyNa/AstAny)."""
+        hit = 0.0
+        for v in self._vecs:
+            if v.on_host:
+                hit += float(sum(1 for x in v.data if x not in (None, "")))
+                continue
+            x = v.as_float()
+            hit += float(((x != 0) & ~torch.isnan(x)).sum())
+        return coll.allreduce_scalar(hit) > 0
+
+    def anyfactor(self):
+        """mungers/AstAnyFactor.java"""
+        return any(v.type == T_ENUM for v in self._vecs)
+
+    def categories(self):
+        """Levels of a single categorical column."""
+        if self.ncols != 1 or self._vecs[0].type != T_ENUM:
+            raise ValueError("categories() requires a single categorical column")
+        return list(self._vecs[0].domain)
+
+    def append_levels(self, levels):
+        """Append levels to the domain of every categorical column (mungers/AstAppendLevels.java)."""
+        out = []
+        for v in self._vecs:
+            if v.type != T_ENUM:
+                raise ValueError("append_levels applies to categorical columns only")
+            dom = list(v.domain) + [str(l) for l in levels if str(l) not in v.domain]
+            out.append(Vec(v.data, T_ENUM, dom))
+        return H2OFrame.from_vecs(out, self._names)
+
+    def set_level(self, level):
+        """Set every value of a categorical column to `level` (mungers/AstSetLevel.java)."""
+        out = []
+        for v in self._vecs:
+            if v.type != T_ENUM or level not in v.domain:
+                raise ValueError(f"level '{level}' not in the column domain")
+            out.append(Vec(torch.full_like(v.data, v.domain.index(level)), T_ENUM, list(v.domain)))
+        return H2OFrame.from_vecs(out, self._names)
+
+    def relevel_by_frequency(self, weights_column=None, top_n=-1):
+        """Most frequent level first (mungers/AstRelevelByFreq.java): ascending stable
+        sort of level weights, read back to front; with top_n only the top_n levels move."""
+        if top_n != -1 and (top_n <= 0 or int(top_n) != top_n):
+            raise ValueError(f"TopN argument needs to be a positive integer number, got: {top_n}")
+        w = self.vec(weights_column).as_float(torch.float64) if weights_column is not None else None
+        out = []
+        for v in self._vecs:
+            if v.type != T_ENUM:
+                out.append(v)
+                continue
+            k = len(v.domain)
+            ok = v.data >= 0
+            ww = torch.ones_like(v.data, dtype=torch.float64) if w is None else torch.nan_to_num(w)
+            lw = torch.zeros(k, dtype=torch.float64, device=v.data.device)
+            lw.index_add_(0, v.data[ok].long(), ww[ok])
+            lw = coll.allreduce_(lw).cpu().numpy()
+            order = list(np.argsort(lw, kind="stable"))
+            if top_n != -1 and top_n < k - 1:
+                top = [order[k - 1 - i] for i in range(top_n)]
+                new_order = [0] * k
+                for i, t in enumerate(top):
+                    new_order[k - 1 - i] = t
+                pos = k - top_n - 1
+                tops = set(top)
+                for i in range(k):
+                    if i in tops:
+                        continue
+                    new_order[pos] = i
+                    pos -= 1
+                order = new_order
+            newdom = [v.domain[order[k - 1 - i]] for i in range(k)]
+            remap = torch.empty(k, dtype=torch.int32)
+            for i, lvl in enumerate(order):
+                remap[lvl] = k - 1 - i
+            remap = remap.to(v.data.device)
+            codes = torch.where(ok, remap[v.data.clamp(min=0).long()], v.data)
+            out.append(Vec(codes, T_ENUM, newdom))
+        return H2OFrame.from_vecs(out, self._names)
+
+    def concat(self, frames, axis=1):
+        """cbind (axis=1) or rbind (axis=0) of this frame with `frames`."""
+        frames = list(frames) if isinstance(frames, (list, tuple)) else [frames]
+        if axis == 1:
+            out = self
+            for f in frames:
+                out = out.cbind(f)
+            return out
+        return self.rbind(frames)
+
+    def detach(self):
+        """Drop the DKV registration of this frame (the data stays with the object)."""
+        dkv.remove(self.frame_id)
+
+    @staticmethod
+    def get_frame(frame_id, **kw):
+        return dkv.get(frame_id)
+
+    @staticmethod
+    def from_python(python_obj, destination_frame=None, header=0, separator=",", column_names=None,
+                    column_types=None, na_strings=None, skipped_columns=None, **kw):
+        return H2OFrame(python_obj, destination_frame=destination_frame, header=header, separator=separator,
+                        column_names=column_names, column_types=column_types, na_strings=na_strings,
+                        skipped_columns=skipped_columns)
+
+    def get_summary(self):
+        return self.summary(return_data=True)
+
+    def show_summary(self):
+        self.summary()
+
+    def filter_na_cols(self, frac=0.2):
+        """Indices of the columns whose NA count is < frac * nrows (mungers/AstFilterNaCols.java)."""
+        lim = self.nrows * frac
+        return [i for i, v in enumerate(self._vecs) if v.nacnt() < lim]
+
+    def getrow(self):
+        """The single row of a 1-row frame as a list (mungers/AstGetrow.java)."""
+        if self.nrows != 1:
+            raise ValueError("getrow() requires a frame with exactly one row")
+        row = []
+        for v in self._gathered_vecs():
+            x = v.to_numpy()[0]
+            row.append(None if _is_na(x) else (float(x) if v.type in NUMERIC_TYPES else x))
+        return row
+
+    def _idx_extreme(self, skipna, axis, largest):
+        if axis == 1:
+            x = self.to_tensor(dtype=torch.float64)
+            nan = torch.isnan(x)
+            fill = -math.inf if largest else math.inf
+            xf = torch.where(nan, torch.full_like(x, fill), x)
+            r = (xf.argmax(1) if largest else xf.argmin(1)).to(torch.float64)
+            if not skipna:
+                r = torch.where(nan.any(1), torch.full_like(r, float("nan")), r)
+            return H2OFrame.from_vecs([Vec(r, T_INT)], ["which.max" if largest else "which.min"])
+        off = self.row_offset()
+        res = []
+        for v in self._vecs:
+            x = v.as_float(torch.float64)
+            nan = torch.isnan(x)
+            if not skipna and coll.allreduce_scalar(float(nan.sum())) > 0:
+                res.append(float("nan"))
+                continue
+            fill = -math.inf if largest else math.inf
+            xf = torch.where(nan, torch.full_like(x, fill), x)
+            if xf.numel():
+                i = int(xf.argmax() if largest else xf.argmin())
+                val, gi = float(xf[i]), float(i + off)
+            else:
+                val, gi = fill, float("nan")
+            if cloud.is_distributed():
+                cands = coll.all_gather_object((val, gi))
+                best = max(cands, key=lambda c: (c[0], -c[1])) if largest else min(cands, key=lambda c: (c[0], c[1]))
+                val, gi = best
+            res.append(gi if math.isfinite(val) else float("nan"))
+        return H2OFrame({n: [r] for n, r in zip(self._names, res)}, _local=True)
+
+    def idxmax(self, skipna=True, axis=0):
+        """Row index of the max per column (axis=0) or column index per row (axis=1) (AstWhichMax)."""
+        return self._idx_extreme(skipna, axis, True)
+
+    def idxmin(self, skipna=True, axis=0):
+        return self._idx_extreme(skipna, axis, False)
+
+    def which(self):
+        """Global row indices of the non-zero entries of a single column (AstWhich)."""
+        x = self._vecs[0].as_float()
+        idx = torch.nonzero((x != 0) & ~torch.isnan(x)).flatten().to(torch.float64) + self.row_offset()
+        return H2OFrame.from_vecs([Vec(idx, T_INT)], ["which"])
+
+    def isin(self, item):
+        """Elementwise membership test against a scalar or list of values."""
+        items = list(item) if isinstance(item, (list, tuple, set)) else [item]
+        out = []
+        for v in self._vecs:
+            if v.type == T_ENUM:
+                codes = [v.domain.index(str(i)) for i in items if str(i) in v.domain]
+                t = torch.tensor(codes or [-2], dtype=v.data.dtype, device=v.data.device)
+                m = torch.isin(v.data, t)
+            elif v.on_host:
+                s = set(str(i) for i in items)
+                m = torch.tensor([x is not None and str(x) in s for x in v.data], device=_dev())
+            else:
+                nums = [float(i) for i in items if _try_float(i)]
+                t = torch.tensor(nums or [float("nan")], dtype=torch.float64, device=v.data.device)
+                m = torch.isin(v.as_float(torch.float64), t)
+            out.append(Vec(m.to(torch.float32), T_INT))
+        return H2OFrame.from_vecs(out, self._names)
+
+    def match(self, table, nomatch=0, start_index=1):
+        """Position (start_index-based) of each value in `table`, else `nomatch` (AstMatch)."""
+        table = list(table) if isinstance(table, (list, tuple)) else [table]
+        out = []
+        for v in self._vecs:
+            if v.type == T_ENUM:
+                lut = [float(table.index(d) + start_index) if d in table else
+                       (float(table.index(_num_or(d)) + start_index) if _num_or(d) in table else float(nomatch))
+                       for d in v.domain] or [float(nomatch)]
+                lt = torch.tensor(lut, dtype=torch.float64, device=v.data.device)
+                r = torch.where(v.data >= 0, lt[v.data.clamp(min=0).long()],
+                                torch.full(v.data.shape, float(nomatch), dtype=torch.float64, device=v.data.device))
+            elif v.on_host:
+                pos = {str(t): i + start_index for i, t in reversed(list(enumerate(table)))}
+                r = torch.tensor([float(pos.get(str(x), nomatch)) if x is not None else float(nomatch)
+                                  for x in v.data], dtype=torch.float64, device=_dev())
+            else:
+                x = v.as_float(torch.float64)
+                r = torch.full_like(x, float(nomatch))
+                for i in reversed(range(len(table))):
+                    if _try_float(table[i]):
+                        r = torch.where(x == float(table[i]), torch.full_like(x, float(i + start_index)), r)
+            out.append(Vec(r, T_INT))
+        return H2OFrame.from_vecs(out, self._names)
+
+    def _moment(self, k, na_rm):
+        res = []
+        for v in self._vecs:
+            if not v.is_numeric or self.nrows == 0 or (not na_rm and v.nacnt() > 0):
+                res.append(float("nan"))
+                continue
+            x = v.as_float(torch.float64)
+            x = x[~torch.isnan(x)]
+            mu = v.mean()
+            d = x - mu
+            ss = coll.allreduce_scalar(float((d * d).sum()))
+            sk = coll.allreduce_scalar(float((d ** k).sum()))
+            n = self.nrows  # reference divides by the full length (AstHist.third/fourth_moment)
+            m2 = ss / n
+            res.append((sk / n) / (m2 ** (k / 2.0)) if m2 > 0 else float("nan"))
+        return res
+
+    def skewness(self, na_rm=False):
+        """Per-column skewness m3/m2^1.5 (advmath/AstSkewness.java)."""
+        return self._moment(3, na_rm)
+
+    def kurtosis(self, na_rm=False):
+        """Per-column (non-excess) kurtosis m4/m2^2 (advmath/AstKurtosis.java)."""
+        return self._moment(4, na_rm)
+
+    def insert_missing_values(self, fraction=0.1, seed=None):
+        """Replace ~fraction of all values with NA, in place (hex/MissingInserter.java)."""
+        gen = torch.Generator(device="cpu").manual_seed(int(seed if seed is not None and seed >= 0 else
+                                                            np.random.randint(1 << 30)) + cloud.rank())
+        for i, v in enumerate(self._vecs):
+            m = torch.rand(v.nlocal, generator=gen) < fraction
+            if v.on_host:
+                arr = np.array(v.data, dtype=object)
+                arr[m.numpy()] = None
+                nv = Vec(arr, v.type)
+            elif v.type == T_ENUM:
+                nv = Vec(torch.where(m.to(v.data.device), torch.full_like(v.data, -1), v.data), T_ENUM, v.domain)
+            else:
+                d = v.data if v.data.is_floating_point() else v.data.to(torch.float32)
+                nv = Vec(torch.where(m.to(d.device), torch.full_like(d, float("nan")), d), v.type)
+            self._vecs[i] = nv
+        return self
+
+    def interaction(self, factors, pairwise, max_factors, min_occurrence, destination_frame=None):
+        from .munging import interaction
+        return interaction(self, factors, pairwise, max_factors, min_occurrence)
+
+    def rep_len(self, length_out):
+        """Repeat rows (or the single column's values) cyclically to length_out (AstRepLen)."""
+        g = self.gather()
+        n = g.nrows
+        if self.ncols > 1 and n == 1:
+            # reference: replicate the columns of a one-row frame
+            k = length_out
+            vecs = [g._vecs[j % self.ncols] for j in range(k)]
+            return H2OFrame.from_vecs(vecs, [f"C{j + 1}" for j in range(k)])
+        idx = torch.arange(length_out, device=_dev()) % max(n, 1)
+        return _reshard(H2OFrame.from_vecs([_take(v, idx) for v in g._vecs], self._names))
+
+    def topNBottomN(self, column=0, nPercent=10, grabTopN=-1):
+        from .munging import topn
+        return topn(self, column, nPercent, grabTopN)
+
+    def bottomN(self, column=0, nPercent=10):
+        return self.topNBottomN(column, nPercent, -1)
+
+    def isax(self, num_words, max_cardinality, optimize_card=False, **kwargs):
+        """iSAX index of row-wise time series (timeseries/AstIsax.java): PAA word means
+        z-scored by the series mean/std, bucketed at the N(0,1) quantiles."""
+        from scipy.stats import norm
+        if num_words <= 0 or max_cardinality <= 0:
+            raise ValueError("num_words and max_cardinality must be > 0")
+        x = self.to_tensor(dtype=torch.float64)
+        step = max(self.ncols // num_words, 1)
+        words, sums, cnt, sse = [], 0.0, 0, 0.0
+        for w in range(num_words):
+            seg = x[:, w * step: (w + 1) * step]
+            if seg.shape[1] == 0:
+                break
+            m = seg.mean(1)
+            words.append(m)
+            sums = sums + seg.sum(1)
+            cnt += seg.shape[1]
+            # Welford inside a word, the reference's quirk
+            sse = sse + ((seg - m[:, None]) ** 2).sum(1)
+        mu = sums / cnt
+        sd = torch.sqrt(sse / (cnt - 1))
+        bounds = torch.tensor([norm.ppf(i / max_cardinality) for i in range(1, max_cardinality)],
+                              dtype=torch.float64, device=x.device)
+        toks = [torch.searchsorted(bounds, ((wm - mu) / sd).contiguous(), right=False).clamp(max=max_cardinality - 1)
+                for wm in words]
+        cards = [max_cardinality] * len(toks)
+        if optimize_card:
+            for i, t in enumerate(toks):
+                u = torch.unique(coll.all_gather_var(t) if cloud.is_distributed() else t)
+                cards[i] = int(u.numel())
+                if cards[i] < max_cardinality:
+                    toks[i] = torch.searchsorted(u, t)
+        tok_np = [t.cpu().numpy() for t in toks]
+        strs = ["_".join(f"{int(tok_np[w][r])}^{cards[w]}" for w in range(len(toks))) for r in range(x.shape[0])]
+        vecs = [make_string(strs)] + [Vec(t.to(torch.float64), T_INT) for t in toks]
+        return H2OFrame.from_vecs(vecs, ["iSax_index"] + [f"c{i}" for i in range(len(toks))])
+
+    @staticmethod
+    def mktime(year=1970, month=0, day=0, hour=0, minute=0, second=0, msec=0):
+        """Epoch milliseconds from calendar fields; month and day are 0-based like the
+        reference (time/AstMktime.java).  Arguments are scalars or single-column frames."""
+        import pandas as pd
+        parts = [year, month, day, hour, minute, second, msec]
+        n = max((p.nlocal for p in parts if isinstance(p, H2OFrame)), default=1)
+        cols = []
+        for p in parts:
+            if isinstance(p, H2OFrame):
+                cols.append(p._vecs[0].as_float(torch.float64).cpu().numpy())
+            else:
+                cols.append(np.full(n, float(p)))
+        y, mo, d, h, mi, s, ms = cols
+        bad = np.zeros(n, dtype=bool)
+        for c in cols:
+            bad |= np.isnan(c)
+        cl = [np.nan_to_num(c).astype(np.int64) for c in cols]
+        ts = pd.to_datetime(pd.DataFrame({"year": cl[0], "month": cl[1] + 1, "day": cl[2] + 1, "hour": cl[3],
+                                          "minute": cl[4], "second": cl[5]}), utc=True)
+        out = (ts.astype("int64") // 10 ** 6).values.astype(np.float64) + cl[6]
+        out[bad] = np.nan
+        return H2OFrame.from_vecs([make_time(out)], ["mktime"])
+
+    def save(self, path, force=True):
+        """Binary frame export (h2o.save_frame / Frame export): see core/frame_io.py."""
+        from .frame_io import save_frame
+        return save_frame(self, path, force=force)
+
+    def convert_H2OFrame_2_DMatrix(self, predictors, yresp, h2oXGBoostModel=None, in_place=False):
+        """Dense (X, y) numpy export; returns an xgboost.DMatrix when xgboost is importable."""
+        X = self.gather().to_tensor(predictors, dtype=torch.float32).cpu().numpy()
+        y = self.gather().vec(yresp).as_float(torch.float32).cpu().numpy()
+        try:
+            import xgboost
+            return xgboost.DMatrix(X, label=y)
+        except ImportError:
+            return X, y
+
+    def save_to_hive(self, jdbc_url, table_name, format="csv", table_path=None, tmp_path=None):
+        raise NotImplementedError("Hive export needs a JDBC/Hive stack, which this platform does not ship")
+
     # strings & time (delegated)
     def __getattr__(self, name):
         from . import strings, timeops
@@ -1027,6 +1398,14 @@ class H2OFrame:
 
 
 # ---------------------------------------------------------------- helpers
+def _num_or(s):
+    try:
+        f = float(s)
+        return int(f) if f.is_integer() else f
+    except (TypeError, ValueError):
+        return s
+
+
 def _try_float(x):
     try:
         float(x)

@@ -39,7 +39,7 @@ COMMON_DEFAULTS = dict(model_id=None, training_frame=None, validation_frame=None
                        score_each_iteration=False, distribution="auto")
 
 _LESS_IS_BETTER = {"deviance", "logloss", "mse", "rmse", "mae", "rmsle", "mean_per_class_error",
-                   "misclassification", "anomaly_score"}
+                   "misclassification", "anomaly_score", "custom"}
 
 
 class TrainSpec:
@@ -381,10 +381,36 @@ class H2OEstimator:
         if spec.nclasses == 2:
             yy = y.to(torch.float64)
             ok = yy >= 0
-            return mm.binomial_metrics(yy[ok], raw[ok][:, -1], None if w is None else w[ok], spec.response_domain)
-        if spec.nclasses > 2:
-            return mm.multinomial_metrics(y, raw, w, spec.response_domain)
-        return mm.regression_metrics(y.to(torch.float64), raw[:, 0], w, dist)
+            res = mm.binomial_metrics(yy[ok], raw[ok][:, -1], None if w is None else w[ok], spec.response_domain)
+        elif spec.nclasses > 2:
+            res = mm.multinomial_metrics(y, raw, w, spec.response_domain)
+        else:
+            res = mm.regression_metrics(y.to(torch.float64), raw[:, 0], w, dist)
+        cm = self._parms.get("custom_metric_func")
+        if cm is not None and res is not None:
+            self._attach_custom_metric(cm, res, spec, frame, raw, y, w)
+        return res
+
+    def _attach_custom_metric(self, ref, res, spec, frame, raw, y, w):
+        """custom_metric_func (water/udf/CMetricFunc): rows are [label, p0..pk-1]
+        for classifiers and [prediction] for regression, like the reference."""
+        from ..core.udf import custom_metric_value, metric_name
+        if spec.nclasses >= 2:
+            probs = raw.to(torch.float64)
+            if spec.nclasses == 2:
+                thr = res.find_threshold_by_max_metric("f1") if res.get("thresholds_and_metric_scores") else 0.5
+                label = (probs[:, -1] >= thr).to(torch.float64)
+                probs = torch.stack([1 - probs[:, -1], probs[:, -1]], 1) if probs.shape[1] == 1 else probs
+            else:
+                label = probs.argmax(1).to(torch.float64)
+            pred = torch.cat([label.view(-1, 1), probs], 1)
+            act = torch.where(y < 0, torch.full_like(y, float("nan"), dtype=torch.float64), y.to(torch.float64))
+        else:
+            pred = raw[:, :1].to(torch.float64)
+            act = y.to(torch.float64)
+        o = spec.offset_tensor(frame)
+        res._m["custom_metric_name"] = metric_name(ref)
+        res._m["custom_metric_value"] = custom_metric_value(ref, pred, act, w, o, self)
 
     def _score_all(self, spec):
         if not self.supervised_learning:

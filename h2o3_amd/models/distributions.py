@@ -273,6 +273,12 @@ def get_distribution(name, nclasses=1, **kw):
     n = (name or "AUTO")
     if n in ("AUTO", "auto"):
         n = "gaussian" if nclasses == 1 else ("bernoulli" if nclasses == 2 else "multinomial")
+    if n == "custom":
+        from ..core.udf import CustomDistribution
+        if kw.get("custom_distribution_func") is None:
+            raise ValueError("distribution='custom' needs custom_distribution_func (h2o.upload_custom_distribution)")
+        return CustomDistribution(kw.pop("custom_distribution_func"), **kw)
+    kw.pop("custom_distribution_func", None)
     if n not in _REG:
         raise ValueError(f"unsupported distribution {name}")
     return _REG[n](**kw)

@@ -23,6 +23,7 @@ import torch
 from ...parallel import cloud
 from ...parallel import collectives as coll
 from .. import metrics as mm
+from ..base import ScoreKeeper, _LESS_IS_BETTER
 from .engine import GrowParams, TreeGrower
 from .shared import Forest, SharedTreeEstimator
 
@@ -34,7 +35,7 @@ DRF_DEFAULTS = dict(ntrees=50, max_depth=20, min_rows=1.0, nbins=20, nbins_top_l
                     calibration_frame=None, calibration_method="auto", distribution="auto",
                     check_constant_response=True, score_tree_interval=0, balance_classes=False,
                     class_sampling_factors=None, max_after_balance_size=5.0, max_confusion_matrix_size=20,
-                    custom_metric_func=None)
+                    custom_metric_func=None, stopping_rounds=0, stopping_metric="auto", stopping_tolerance=0.001)
 
 
 class H2ORandomForestEstimator(SharedTreeEstimator):
@@ -94,6 +95,9 @@ class H2ORandomForestEstimator(SharedTreeEstimator):
         max_rt = float(p.get("max_runtime_secs") or 0)
         self._scoring_history = []
         interval = int(p.get("score_tree_interval") or 0)
+        stop_rounds = int(p.get("stopping_rounds") or 0)
+        metric_name = self._stopping_metric(spec)
+        history = []
         for t in range(ntrees):
             if srpc is not None and spec.is_classification:
                 rates = torch.tensor(srpc, dtype=torch.float32, device=dev)[ycode.clamp(min=0)]
@@ -118,8 +122,20 @@ class H2ORandomForestEstimator(SharedTreeEstimator):
                 oob_sum[:, k] += torch.where(oob, vt[nid.long()], torch.zeros(N, device=dev))
                 forest.add(tree, k)
             oob_cnt += (~inbag).to(torch.float32)
-            if interval and (t + 1) % interval == 0:
-                self._scoring_history.append({"number_of_trees": t + 1})
+            score_now = (interval and (t + 1) % interval == 0) or (stop_rounds and not interval) or t + 1 == ntrees
+            if score_now:
+                entry = {"number_of_trees": t + 1}
+                if stop_rounds or interval:
+                    self._forest = forest
+                    self._score_entry(entry, spec, oob_sum, oob_cnt)
+                self._scoring_history.append(entry)
+                if stop_rounds:
+                    key = ("validation_" if spec.valid is not None else "training_") + \
+                        ("custom" if metric_name.startswith("custom") else metric_name)
+                    history.append(entry.get(key))
+                    if ScoreKeeper.stop_early(history, stop_rounds, float(p.get("stopping_tolerance", 0.001)),
+                                              metric_name in _LESS_IS_BETTER):
+                        break
             if max_rt > 0 and time.time() - t0 > max_rt:
                 break
         self._forest = forest
@@ -137,6 +153,26 @@ class H2ORandomForestEstimator(SharedTreeEstimator):
         if p.get("calibrate_model") and p.get("calibration_frame") is not None:
             from .calibration import fit_calibration
             fit_calibration(self, p["calibration_frame"], p.get("calibration_method", "auto"))
+
+    def _stopping_metric(self, spec):
+        m = (self._parms.get("stopping_metric") or "auto").lower()
+        if m == "auto":
+            return "logloss" if spec.is_classification else "deviance"
+        return m
+
+    def _score_entry(self, entry, spec, oob_sum, oob_cnt):
+        """Scoring-history row: OOB training metrics (DRF.java scores OOB) plus
+        validation metrics of the forest so far."""
+        from .gbm import H2OGradientBoostingEstimator as _G
+        has = oob_cnt > 0
+        if bool(has.any()):
+            oobp = self._normalize(oob_sum / oob_cnt.clamp_min(1).view(-1, 1))
+            sub = spec.frame[has] if not bool(has.all()) else spec.frame
+            m = self._metrics_from_raw(spec, sub, oobp[has])
+            _G._add_metrics(entry, "training", m)
+        if spec.valid is not None:
+            _G._add_metrics(entry, "validation", self._metrics_from_raw(spec, spec.valid,
+                                                                        self._predict_raw(spec.valid)))
 
     def _seed(self):
         s = self._parms.get("seed", -1)

@@ -60,7 +60,8 @@ class GBMDriver:
             dist_name = "bernoulli"
         self.dist = get_distribution(dist_name, spec.nclasses, tweedie_power=p.get("tweedie_power", 1.5),
                                      quantile_alpha=p.get("quantile_alpha", 0.5),
-                                     huber_alpha=p.get("huber_alpha", 0.9))
+                                     huber_alpha=p.get("huber_alpha", 0.9),
+                                     custom_distribution_func=p.get("custom_distribution_func"))
         est._dist = self.dist
         dev = cloud.device()
         self.dev = dev
@@ -91,7 +92,9 @@ class GBMDriver:
             sw = coll.allreduce_scalar(float(self.base_w.sum()))
             sy = coll.allreduce_scalar(float((self.base_w * yv).sum()))
             mu = sy / sw if sw > 0 else 0.0
-            if self.dist.family in ("laplace", "quantile", "huber"):
+            if self.dist.family == "custom":
+                f0 = self.dist.init_f(yv, self.base_w, self.offset)
+            elif self.dist.family in ("laplace", "quantile", "huber"):
                 f0 = _weighted_quantile(yv[self.base_w > 0], self.base_w[self.base_w > 0],
                                         0.5 if self.dist.family != "quantile" else self.dist.quantile_alpha)
             elif self.dist.link == "logit":
@@ -101,7 +104,7 @@ class GBMDriver:
                 f0 = math.log(max(mu, 1e-10))
             else:
                 f0 = mu
-            if self.offset is not None and self.dist.link != "identity":
+            if self.offset is not None and self.dist.link != "identity" and self.dist.family != "custom":
                 f0 = self._newton_init(f0, yv)
             self.init_f = [f0]
         else:
@@ -329,7 +332,8 @@ class H2OGradientBoostingEstimator(SharedTreeEstimator):
                 entry = self._score_iteration(drv, spec)
                 self._scoring_history.append(entry)
                 if stop_rounds > 0:
-                    key = "validation_" + metric_name if spec.valid is not None else "training_" + metric_name
+                    suffix = "custom" if metric_name.startswith("custom") else metric_name
+                    key = ("validation_" if spec.valid is not None else "training_") + suffix
                     history.append(entry.get(key))
                     if ScoreKeeper.stop_early(history, stop_rounds, float(p["stopping_tolerance"]),
                                               metric_name in _LESS_IS_BETTER):
@@ -363,6 +367,8 @@ class H2OGradientBoostingEstimator(SharedTreeEstimator):
         m = (self._parms.get("stopping_metric") or "auto").lower()
         if m == "auto":
             return "logloss" if spec.is_classification else "deviance"
+        if m == "custom_increasing":
+            return "custom_increasing"
         return m
 
     def _score_iteration(self, drv, spec):
@@ -390,6 +396,8 @@ class H2OGradientBoostingEstimator(SharedTreeEstimator):
             v = m.get(k)
             if v is not None:
                 entry[f"{prefix}_{name}"] = v
+        if m.get("custom_metric_value") is not None:
+            entry[f"{prefix}_custom"] = m["custom_metric_value"]
         if m.get("cm") is not None and m.kind in ("binomial", "multinomial"):
             entry[f"{prefix}_classification_error"] = m["cm"]["total_error"]
             entry[f"{prefix}_misclassification"] = m["cm"]["total_error"]

@@ -152,6 +152,16 @@ class Forest:
 class SharedTreeEstimator(H2OEstimator):
     """Base of GBM / DRF / XGBoost / IsolationForest / UpliftDRF."""
 
+    def _cv_optimal_params(self, cv_models):
+        """Main model trains the mean number of trees the early-stopped CV models
+        kept (ModelBuilder.cv_computeAndSetOptimalParameters / SharedTree)."""
+        import math as _m
+        if int(self._parms.get("stopping_rounds") or 0) > 0 and cv_models and \
+                all(getattr(m, "_forest", None) is not None for m in cv_models):
+            nt = [len(m._forest) // max(1, getattr(m, "_K", 1)) for m in cv_models]
+            self._parms["ntrees"] = max(1, int(_m.ceil(sum(nt) / len(nt))))
+            self._parms["stopping_rounds"] = 0
+
     def _feature_inputs(self, frame: H2OFrame, x):
         feats, is_cat, cards = [], [], []
         domains = {}

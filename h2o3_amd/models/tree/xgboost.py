@@ -12,6 +12,7 @@ DART dropout.
 from __future__ import annotations
 
 import math
+import time
 
 import numpy as np
 import torch
@@ -21,6 +22,7 @@ from ...parallel import collectives as coll
 from ...ops import tree_ops
 from ..distributions import get_distribution
 from .engine import GrowParams, TreeGrower
+from ..base import ScoreKeeper, _LESS_IS_BETTER
 from .shared import Forest, SharedTreeEstimator
 
 XGB_DEFAULTS = dict(ntrees=50, max_depth=6, min_rows=1.0, min_child_weight=1.0, learn_rate=0.3, eta=0.3,
@@ -120,6 +122,15 @@ class H2OXGBoostEstimator(SharedTreeEstimator):
         ntrees = int(p["ntrees"])
         sr = float(p["sample_rate"])
         F = bd.F
+        interval = int(p.get("score_tree_interval") or 0)
+        stop_rounds = int(p.get("stopping_rounds") or 0)
+        metric_name = (p.get("stopping_metric") or "auto").lower()
+        if metric_name == "auto":
+            metric_name = "logloss" if spec.is_classification else "deviance"
+        history = []
+        self._scoring_history = []
+        max_rt = float(p.get("max_runtime_secs") or 0)
+        t0 = time.time()
         for it in range(ntrees):
             wt = base_w
             if sr < 1.0:
@@ -181,6 +192,21 @@ class H2OXGBoostEstimator(SharedTreeEstimator):
                 f = f + deltas[0]
             else:
                 f = f + torch.stack(deltas, 1)
+            n_it = it + 1
+            if (interval and n_it % interval == 0) or (stop_rounds and not interval) or n_it == ntrees:
+                entry = {"number_of_trees": n_it}
+                self._forest = forest
+                self._score_entry(entry, spec, f)
+                self._scoring_history.append(entry)
+                if stop_rounds:
+                    key = ("validation_" if spec.valid is not None else "training_") + \
+                        ("custom" if metric_name.startswith("custom") else metric_name)
+                    history.append(entry.get(key))
+                    if ScoreKeeper.stop_early(history, stop_rounds, float(p.get("stopping_tolerance", 0.001)),
+                                              metric_name in _LESS_IS_BETTER):
+                        break
+            if max_rt > 0 and time.time() - t0 > max_rt:
+                break
         if dart:
             # bake DART weights into leaf values
             for it, wgt in enumerate(tree_w):
@@ -197,6 +223,21 @@ class H2OXGBoostEstimator(SharedTreeEstimator):
                     vi[spec.x[t.feat[i]]] += max(t.gain[i], 0.0)
         self._output["variable_importances"] = vi
         self._output["model_summary"] = {"number_of_trees": len(forest) // K, "booster": booster}
+
+    def _raw_from_f(self, f):
+        if self._K > 1:
+            return torch.softmax(f, 1)
+        mu = self._dist.linkinv(f[:, 0])
+        if self._spec.nclasses == 2:
+            return torch.stack([1 - mu, mu], 1)
+        return mu.view(-1, 1)
+
+    def _score_entry(self, entry, spec, f):
+        from .gbm import H2OGradientBoostingEstimator as _G
+        _G._add_metrics(entry, "training", self._metrics_from_raw(spec, spec.frame, self._raw_from_f(f)))
+        if spec.valid is not None:
+            _G._add_metrics(entry, "validation", self._metrics_from_raw(spec, spec.valid,
+                                                                        self._predict_raw(spec.valid)))
 
     def _contrib(self, forest, tree_w, dropped, K, bd, N):
         X = self._score_matrix(self._spec.frame)
