@@ -217,6 +217,25 @@ def create_app() -> FastAPI:
     def timeline():
         return {"events": api.timeline()}
 
+    @app.post("/99/Rapids")
+    def rapids_exec(body: dict = Body(...)):
+        """Rapids expression evaluation (water/api/RapidsHandler.java): frame
+        results are stored under their key and described; scalars/lists/strings
+        come back inline."""
+        from ..core.rapids import RapidsError, rapids
+        try:
+            res = rapids(body.get("ast", ""))
+        except (RapidsError, KeyError, ValueError, TypeError) as e:
+            raise HTTPException(400, f"Rapids error: {e}")
+        if isinstance(res, H2OFrame):
+            dkv.put(res.frame_id, res)
+            return {"key": {"name": res.frame_id}, "num_rows": res.nrows, "num_cols": res.ncols}
+        if isinstance(res, str):
+            return {"string": res}
+        if isinstance(res, (list, tuple)):
+            return {"scalar": None, "ns": [_jsonable(x) for x in res]}
+        return {"scalar": _jsonable(res)}
+
     @app.get("/3/Metadata/endpoints")
     def endpoints():
         return {"routes": [{"url_pattern": r.path, "http_method": sorted(r.methods)[0]} for r in app.routes
