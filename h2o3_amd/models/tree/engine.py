@@ -203,20 +203,30 @@ class TreeGrower:
                 row = np.zeros(F, dtype=bool)
                 row[sel] = True
                 m[i] = row
+        all_true = bool(m.all())
         if self.Fpad > F:
             m = np.concatenate([m, np.zeros((n_nodes, self.Fpad - F), dtype=bool)], 1)
-        return torch.from_numpy(m)
+        t = torch.from_numpy(m)
+        t._all_true = all_true
+        return t
 
-    def _find_splits(self, H, col_mask, node_wyy=None):
+    def _find_splits(self, H, col_mask, node_wyy=None, want_pk=False):
         """Dispatch: fused HIP kernel for numeric features on GPU (categorical
         features, which need a per-node sort of bins, go through the torch path)."""
         if self.dev.type != "cuda" or self.p.criterion.startswith("uplift"):
             return self._find_splits_torch(H, col_mask, node_wyy)
         Fl = H.shape[0]
         fsl = slice(self.f0, self.f0 + Fl)
-        is_cat = self.is_cat_t[fsl].cpu()
+        if getattr(self, "_is_cat_cpu", None) is None:
+            self._is_cat_cpu = self.is_cat_t[fsl].cpu()
+        is_cat = self._is_cat_cpu
         if bool(is_cat.all()):
             return self._find_splits_torch(H, col_mask, node_wyy)
+        if not bool(is_cat.any()):
+            res = self._find_splits_native(H, col_mask, node_wyy, want_pk=want_pk)
+            if self.W > 1:
+                res = self._merge_candidates(res, H.shape[1], H.shape[2], H.shape[3])
+            return res
         cm_num = col_mask.clone()
         cm_num[:, fsl] &= ~is_cat.view(1, -1)
         res = self._find_splits_native(H, cm_num, node_wyy)
@@ -234,7 +244,7 @@ class TreeGrower:
             res = self._merge_candidates(res, H.shape[1], H.shape[2], H.shape[3])
         return res
 
-    def _find_splits_native(self, H, col_mask, node_wyy):
+    def _find_splits_native(self, H, col_mask, node_wyy, want_pk=False):
         import ctypes
         from ...ops import _native
         p = self.p
@@ -246,10 +256,20 @@ class TreeGrower:
                 [ctypes.c_double] * 5 + [ctypes.c_int, cv, cv]
             lib._typed = True
         fsl = slice(self.f0, self.f0 + Fl)
-        ok = col_mask[:, fsl].to(torch.uint8).contiguous().to(self.dev, non_blocking=True)
-        if self.f0 + Fl > self.bd.F:
-            ok[:, max(0, self.bd.F - self.f0):] = 0
-        mono = self.mono_t[fsl].to(torch.float32).contiguous()
+        cm = col_mask[:, fsl]
+        if getattr(col_mask, "_all_true", False) and self.f0 + Fl <= self.bd.F:
+            # no column sampling: a cached device mask of ones per frontier size
+            cache = self.__dict__.setdefault("_ok_cache", {})
+            ok = cache.get(n)
+            if ok is None:
+                ok = cache[n] = torch.ones((n, Fl), dtype=torch.uint8, device=self.dev)
+        else:
+            ok = cm.to(torch.uint8).contiguous().to(self.dev, non_blocking=True)
+            if self.f0 + Fl > self.bd.F:
+                ok[:, max(0, self.bd.F - self.f0):] = 0
+        if getattr(self, "_mono_f32", None) is None:
+            self._mono_f32 = self.mono_t[fsl].to(torch.float32).contiguous()
+        mono = self._mono_f32
         H = H.contiguous()
         wyy = node_wyy.to(torch.float64).contiguous() if node_wyy is not None else \
             torch.zeros(n, dtype=torch.float64, device=self.dev)
@@ -262,6 +282,26 @@ class TreeGrower:
                                 ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
         if rc != 0:
             raise RuntimeError(f"h2o_split_find failed: {rc}")
+        if C == 2 and self.f0 < self.bd.F and want_pk and self.W == 1:
+            # selection + split decision + partition inputs in one kernel; the
+            # packed record (12 doubles per node) is what the host fetches
+            if not getattr(lib, "_typed_sel2", False):
+                cv = ctypes.c_void_p
+                lib.h2o_split_select2.argtypes = [cv, cv, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                  ctypes.c_double, ctypes.c_int, cv, cv, cv, cv]
+                lib._typed_sel2 = True
+            pk = torch.empty((n, 12), dtype=torch.float64, device=self.dev)
+            mask = torch.empty((n, Bs), dtype=torch.uint8, device=self.dev)
+            feat_i = torch.empty(n, dtype=torch.int32, device=self.dev)
+            min_w2 = -1.0 if p.criterion == "xgb" else 2.0 * float(p.min_rows)
+            rc = lib.h2o_split_select2(ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(H.data_ptr()), Fl, n, Bs,
+                                       self.f0, min_w2, 12, ctypes.c_void_p(pk.data_ptr()),
+                                       ctypes.c_void_p(mask.data_ptr()), ctypes.c_void_p(feat_i.data_ptr()),
+                                       ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+            if rc != 0:
+                raise RuntimeError(f"h2o_split_select2 failed: {rc}")
+            return {"pk": pk, "feat_i32": feat_i, "mask": mask, "gain": pk[:, 0], "feat": pk[:, 1], "t": pk[:, 2],
+                    "opt": pk[:, 3], "L": pk[:, 4:6], "R": pk[:, 6:8], "tot": pk[:, 8:10]}
         if C == 2 and self.f0 < self.bd.F:
             # fused per-node selection + mask kernel: few launches, one packed record
             if not getattr(lib, "_typed_sel", False):
@@ -516,6 +556,8 @@ class TreeGrower:
         child_tot = {}     # node id -> channel totals from the parent's split record
         leaves, leaf_tot = [], []
         level = 0
+        async_part = self.dev.type == "cuda" and not p.max_leaves and not self.use_payload and \
+            os.environ.get("H2O3_ASYNC_PART", "1") == "1" and os.environ.get("H2O3_PART", "ballot") == "ballot"
         while frontier:
             self._level = level
             n_front = len(frontier)
@@ -539,6 +581,16 @@ class TreeGrower:
                     par_slots.append(pslot)
                 Hb = self._build_hist(ridx, va, vb, mode, [frontier[s][1] for s in build_slots],
                                       [frontier[s][2] for s in build_slots])
+            if level > 0 and H_prev is not None and (can_split or level == 0) and self.dev.type == "cuda":
+                # copy + parent-minus-built subtraction in one kernel
+                clamp = {0: 0b1, 1: 0b0}.get(mode, (1 << tree_ops.channels(mode)) - 1)
+                wb = self._last_wyy if mode == 0 else None
+                H, wyy_n = tree_ops.hist_sibling(Hb, H_prev, build_slots, der_slots, par_slots, n_front, clamp,
+                                                 wyy_b=wb, wyy_prev=wyy_prev if wb is not None else None)
+                if wyy_n is not None:
+                    wyy_level = wyy_n
+                del Hb
+            elif level > 0 and H_prev is not None and can_split:
                 H = torch.empty((Hb.shape[0], n_front) + tuple(Hb.shape[2:]), dtype=Hb.dtype, device=Hb.device)
                 bs = torch.tensor(build_slots, device=Hb.device)
                 ds = torch.tensor(der_slots, device=Hb.device)
@@ -553,19 +605,53 @@ class TreeGrower:
                     # only w / wyy are non-negative; wy may be negative
                     H[:, ds, :, 1] = H_prev[:, ps, :, 1] - Hb[:, :, :, 1]
                 del Hb
+            nleft_pre = None
             if can_split:
                 cm = self._col_mask(n_front, depth)
                 # node totals of w*y*y (only the total enters the SE split test),
                 # fused into the histogram kernel; derived siblings by subtraction
                 node_wyy = wyy_level if mode == 0 else None
                 with phase("tree.split"):
-                    sp = self._find_splits(H, cm, node_wyy)
-                # ONE device->host transfer of every per-node scalar of the level
+                    sp = self._find_splits(H, cm, node_wyy, want_pk=async_part)
                 nn_ = n_front
-                pk = torch.cat([sp["gain"].view(nn_, 1).to(torch.float64), sp["feat"].view(nn_, 1).to(torch.float64),
-                                sp["t"].view(nn_, 1).to(torch.float64), sp["opt"].view(nn_, 1).to(torch.float64),
-                                sp["L"].to(torch.float64), sp["R"].to(torch.float64),
-                                sp["tot"].to(torch.float64)], 1).cpu().numpy()
+                if async_part and "pk" in sp:
+                    pkd = sp["pk"]
+                    with phase("tree.partition"):
+                        ridx2.copy_(ridx)
+                        pay = (self._pos1[0], None, self._pos1[1], None) if self._pos1 is not None else None
+                        tree_ops.partition_async(bd, ridx, ridx2, sp["feat_i32"], sp["mask"],
+                                                 [f[1] for f in frontier], [f[2] for f in frontier],
+                                                 payload=pay, pk=pkd, pk_col=11)
+                    pk = pkd.cpu().numpy()
+                    ok_h = pk[:, 10] > 0
+                    nleft_pre = pk[:, 11].astype(np.int64).tolist()
+                cols = [] if nleft_pre is not None else [sp["gain"].view(nn_, 1).to(torch.float64), sp["feat"].view(nn_, 1).to(torch.float64),
+                        sp["t"].view(nn_, 1).to(torch.float64), sp["opt"].view(nn_, 1).to(torch.float64),
+                        sp["L"].to(torch.float64), sp["R"].to(torch.float64), sp["tot"].to(torch.float64)]
+                if async_part and nleft_pre is None:
+                    # split decision + partition of the whole frontier on the device: no
+                    # host round trip between the split search and the row partition
+                    tot_d = sp["tot"].to(torch.float64)
+                    w_d = (tot_d[:, 0] if mode != 1 else tot_d[:, 1]) + (tot_d[:, 2] if mode == 3 else 0.0)
+                    ok_d = torch.isfinite(sp["gain"].to(torch.float64))
+                    if p.criterion != "xgb":
+                        ok_d &= w_d >= 2 * p.min_rows
+                    feat_all = torch.where(ok_d, sp["feat"].to(torch.int64), torch.zeros_like(sp["feat"].to(torch.int64)))
+                    mask_all = torch.where(ok_d.view(-1, 1), sp["mask"].to(torch.uint8),
+                                           torch.ones_like(sp["mask"], dtype=torch.uint8))
+                    with phase("tree.partition"):
+                        ridx2.copy_(ridx)
+                        pay = (self._pos1[0], None, self._pos1[1], None) if self._pos1 is not None else None
+                        nleft_d = tree_ops.partition_async(bd, ridx, ridx2, feat_all, mask_all,
+                                                           [f[1] for f in frontier], [f[2] for f in frontier],
+                                                           payload=pay)
+                    cols += [ok_d.view(nn_, 1).to(torch.float64), nleft_d.view(nn_, 1).to(torch.float64)]
+                # ONE device->host transfer of every per-node scalar of the level
+                if cols:
+                    pk = torch.cat(cols, 1).cpu().numpy()
+                    if async_part:
+                        ok_h = pk[:, 4 + 3 * C] > 0
+                        nleft_pre = pk[:, 5 + 3 * C].astype(np.int64).tolist()
                 gains = pk[:, 0].tolist()
                 feats = pk[:, 1].astype(np.int64).tolist()
                 t_l = pk[:, 2].astype(np.int64).tolist()
@@ -583,9 +669,12 @@ class TreeGrower:
             for i, (nid_, st, ct, d) in enumerate(frontier):
                 tot_i = tots_l[i]
                 tree.weight[nid_] = (tot_i[0] if mode != 1 else tot_i[1]) + (tot_i[2] if mode == 3 else 0.0)
-                ok = can_split and gains is not None and math.isfinite(gains[i])
-                if ok and p.criterion != "xgb" and tree.weight[nid_] < 2 * p.min_rows:
-                    ok = False
+                if nleft_pre is not None:
+                    ok = bool(ok_h[i])
+                else:
+                    ok = can_split and gains is not None and math.isfinite(gains[i])
+                    if ok and p.criterion != "xgb" and tree.weight[nid_] < 2 * p.min_rows:
+                        ok = False
                 if ok and p.max_leaves and (len(leaves) + n_front + len(split_ids) + 1) > p.max_leaves:
                     ok = False
                 if ok:
@@ -597,11 +686,17 @@ class TreeGrower:
                     frontier[i].append("leaf")
             if not split_ids:
                 self._leaf_segments = [(f[0], f[1], f[2]) for f in frontier]
+                if nleft_pre is not None:
+                    ridx, ridx2 = ridx2, ridx   # the (identity) partition already ran
+                    if self._pos1 is not None:
+                        self._pos1.reverse()
                 break
             # record splits in the tree
             all_split = len(split_ids) == n_front
-            masks = sp["mask"] if all_split else sp["mask"][torch.tensor(split_ids, device=sp["mask"].device)]
             any_cat = any(bd.is_cat[feats[i]] for i in split_ids)
+            masks = None
+            if any_cat or nleft_pre is None:
+                masks = sp["mask"] if all_split else sp["mask"][torch.tensor(split_ids, device=sp["mask"].device)]
             masks_h = masks.cpu().numpy() if any_cat else None
             new_front, new_pairs = [], []
             part_starts, part_counts, part_feats = [], [], []
@@ -638,18 +733,23 @@ class TreeGrower:
                 child_tot[lid] = Ls[i]
                 child_tot[rid] = Rs[i]
             # partition
-            with phase("tree.partition"):
-                ridx2.copy_(ridx)
-                if self.use_payload:
-                    pa2.copy_(pa)
-                    pb2.copy_(pb)
-                pay = (pa, pb, pa2, pb2) if self.use_payload else None
-                if self._pos1 is not None:
-                    pay = (self._pos1[0], None, self._pos1[1], None)
-                nleft = tree_ops.partition(bd, ridx, ridx2, part_feats, masks, part_starts, part_counts,
-                                           payload=pay)
+            if nleft_pre is not None:
+                nleft = [nleft_pre[i] for i in split_ids]
                 if self._pos1 is not None:
                     self._pos1.reverse()
+            else:
+                with phase("tree.partition"):
+                    ridx2.copy_(ridx)
+                    if self.use_payload:
+                        pa2.copy_(pa)
+                        pb2.copy_(pb)
+                    pay = (pa, pb, pa2, pb2) if self.use_payload else None
+                    if self._pos1 is not None:
+                        pay = (self._pos1[0], None, self._pos1[1], None)
+                    nleft = tree_ops.partition(bd, ridx, ridx2, part_feats, masks, part_starts, part_counts,
+                                               payload=pay)
+                    if self._pos1 is not None:
+                        self._pos1.reverse()
             ridx, ridx2 = ridx2, ridx
             if self.use_payload:
                 pa, pa2, pb, pb2 = pa2, pa, pb2, pb

@@ -550,6 +550,94 @@ __global__ __launch_bounds__(256) void part_compact_kernel(
   }
 }
 
+
+// Histogram subtraction for the next level: built children are copied, their
+// siblings are parent - built.  slots = [build_slot[nb], der_slot[nb],
+// par_slot[nb]] (int32).  Channels whose bit is set in clamp_mask are clamped at
+// 0 (weights, counts); the others (w*y, gradients) may be negative.  One block
+// per (feature, pair), threads over the Bs*C values; wyy (per-node sum w*y*y)
+// follows the same rule (block (0, pair) writes it).
+__global__ __launch_bounds__(256) void hist_sibling_kernel(const double* __restrict__ Hb,
+                                                           const double* __restrict__ Hp,
+                                                           const int* __restrict__ slots, int nb, int np, int nf,
+                                                           int BsC, int C, int clamp_mask,
+                                                           double* __restrict__ H, const double* __restrict__ wyy_b,
+                                                           const double* __restrict__ wyy_p,
+                                                           double* __restrict__ wyy_out) {
+  const int j = blockIdx.x;          // pair
+  const int f = blockIdx.y;          // feature
+  const int bs = slots[j], ds = slots[nb + j], ps = slots[2 * nb + j];
+  const double* hb = Hb + ((size_t)f * nb + j) * BsC;
+  const double* hp = Hp + ((size_t)f * np + ps) * BsC;
+  double* ob = H + ((size_t)f * nf + bs) * BsC;
+  double* od = H + ((size_t)f * nf + ds) * BsC;
+  for (int i = threadIdx.x; i < BsC; i += blockDim.x) {
+    const double b = hb[i];
+    double d = hp[i] - b;
+    if ((clamp_mask >> (i % C)) & 1) d = fmax(d, 0.0);
+    ob[i] = b;
+    od[i] = d;
+  }
+  if (wyy_b != nullptr && f == 0 && threadIdx.x == 0) {
+    wyy_out[bs] = wyy_b[j];
+    wyy_out[ds] = wyy_p[ps] - wyy_b[j];
+  }
+}
+
+// Compaction offsets of the sync-free partition, one workgroup: per chunk i of
+// node s = meta[0][i] (chunks of a node are consecutive), lpre = left rows of
+// the node's earlier chunks; loff = start + lpre, roff = start + nleft[s] +
+// (pos - lpre).  Writes nleft (double) into pk[s * stride + col].
+__global__ __launch_bounds__(1024) void part_offsets_kernel(const int* __restrict__ cnt,
+                                                            const long long* __restrict__ meta, int nw, int n,
+                                                            int* __restrict__ loff, int* __restrict__ roff,
+                                                            long long* __restrict__ nleft, double* __restrict__ pk,
+                                                            int stride, int col) {
+  __shared__ long long part[1024];
+  __shared__ long long carry;
+  const long long* slot = meta;
+  const long long* first = meta + nw;
+  const long long* st = meta + 2 * (long long)nw;
+  const long long* pos = meta + 3 * (long long)nw;
+  for (int s = threadIdx.x; s < n; s += blockDim.x) nleft[s] = 0;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  // pass 1: node totals
+  for (int i = threadIdx.x; i < nw; i += blockDim.x) atomicAdd((unsigned long long*)&nleft[slot[i]],
+                                                               (unsigned long long)cnt[i]);
+  __syncthreads();
+  // pass 2: global exclusive scan of cnt, tile by tile
+  for (int base = 0; base < nw; base += blockDim.x) {
+    const int i = base + threadIdx.x;
+    const long long v = i < nw ? (long long)cnt[i] : 0;
+    part[threadIdx.x] = v;
+    __syncthreads();
+    for (int o = 1; o < (int)blockDim.x; o <<= 1) {
+      const long long t = threadIdx.x >= (unsigned)o ? part[threadIdx.x - o] : 0;
+      __syncthreads();
+      part[threadIdx.x] += t;
+      __syncthreads();
+    }
+    const long long excl = carry + part[threadIdx.x] - v;
+    if (i < nw) loff[i] = (int)excl;   // global exclusive prefix, rebased per node below
+    __syncthreads();
+    if (threadIdx.x == blockDim.x - 1) carry += part[threadIdx.x];
+    __syncthreads();
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < nw; i += blockDim.x) roff[i] = loff[first[i]];   // node's first-chunk prefix
+  __syncthreads();
+  for (int i = threadIdx.x; i < nw; i += blockDim.x) {
+    const long long lpre = (long long)loff[i] - (long long)roff[i];
+    const long long s = slot[i];
+    loff[i] = (int)(st[i] + lpre);
+    roff[i] = (int)(st[i] + nleft[s] + pos[i] - lpre);
+  }
+  __syncthreads();
+  if (pk != nullptr)
+    for (int s = threadIdx.x; s < n; s += blockDim.x) pk[(size_t)s * stride + col] = (double)nleft[s];
+}
+
 // nid[ridx[p]] = leaf for p in segment.  work[i] = (leaf_id, start, count, -)
 __global__ __launch_bounds__(256) void fill_nid_kernel(const int* __restrict__ ridx, const int4* __restrict__ work,
                                                        int* __restrict__ nid) {
@@ -578,6 +666,23 @@ int h2o_part_flags(const void* codes, int code_bytes, long long rs, long long fs
   else
     hipLaunchKernelGGL(part_flags_kernel<uint16_t>, dim3(n_work), dim3(256), 0, s, (const uint16_t*)codes, rs, fs,
                        ridx, (const int4*)work, fbase, feat, masks, Bs, flags, cnt);
+  return (int)hipGetLastError();
+}
+
+int h2o_hist_sibling(const double* Hb, const double* Hp, const int* slots, int nb, int np, int nf, int F, int BsC,
+                     int C, int clamp_mask, double* H, const double* wyy_b, const double* wyy_p, double* wyy_out,
+                     hipStream_t s) {
+  if (nb <= 0 || F <= 0) return 0;
+  hipLaunchKernelGGL(hist_sibling_kernel, dim3(nb, F), dim3(256), 0, s, Hb, Hp, slots, nb, np, nf, BsC, C, clamp_mask,
+                     H, wyy_b, wyy_p, wyy_out);
+  return (int)hipGetLastError();
+}
+
+int h2o_part_offsets(const int* cnt, const long long* meta, int nw, int n, int* loff, int* roff, long long* nleft,
+                     double* pk, int stride, int col, hipStream_t s) {
+  if (nw <= 0) return 0;
+  hipLaunchKernelGGL(part_offsets_kernel, dim3(1), dim3(1024), 0, s, cnt, meta, nw, n, loff, roff, nleft, pk, stride,
+                     col);
   return (int)hipGetLastError();
 }
 

@@ -227,3 +227,63 @@ extern "C" int h2o_split_select(const void* rec, const double* H, int Fl, int n,
   hipLaunchKernelGGL(split_select_kernel, dim3(n), dim3(64), 0, s, (const SplitRec*)rec, H, Fl, n, Bs, f0, pk, mask);
   return (int)hipGetLastError();
 }
+
+// split_select_kernel + the split decision of the level, so the host never has
+// to look at the record before the partition runs: ok = finite gain and (SE
+// criterion) node weight >= min_w2 = 2*min_rows (min_w2 < 0 disables the test).
+// Nodes that do not split get feature 0 and an all-ones mask (every row stays
+// left = in place).  pk rows are `stride` doubles: the 10 fields of
+// split_select_kernel, then ok; the partition fills field 11 (left count).
+__global__ __launch_bounds__(64) void split_select2_kernel(const SplitRec* __restrict__ rec,
+                                                           const double* __restrict__ H, int Fl, int n, int Bs,
+                                                           int f0, double min_w2, int stride,
+                                                           double* __restrict__ pk, uint8_t* __restrict__ mask,
+                                                           int* __restrict__ feat_out) {
+  const int node = blockIdx.x;
+  const int lane = threadIdx.x;
+  double best = -INFINITY;
+  int bf = 0;
+  for (int f = lane; f < Fl; f += 64) {
+    const double g = rec[(size_t)node * Fl + f].gain;
+    if (g > best) { best = g; bf = f; }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const double og = __shfl_xor(best, o, 64);
+    const int of = __shfl_xor(bf, o, 64);
+    if (og > best || (og == best && of < bf)) { best = og; bf = of; }
+  }
+  double t0 = 0.0, t1 = 0.0;
+  for (int b = lane; b < Bs; b += 64) {
+    const double* h = H + ((size_t)node * Bs + b) * 2;   // feature 0
+    t0 += h[0];
+    t1 += h[1];
+  }
+  t0 = wave_sum(t0);
+  t1 = wave_sum(t1);
+  const SplitRec r = rec[(size_t)node * Fl + bf];
+  const bool ok = isfinite(best) && (min_w2 < 0.0 || t0 >= min_w2);
+  if (lane == 0) {
+    double* o = pk + (size_t)node * stride;
+    o[0] = best; o[1] = (double)(bf + f0); o[2] = (double)r.t; o[3] = (double)r.opt;
+    o[4] = r.lw; o[5] = r.ly; o[6] = t0 - r.lw; o[7] = t1 - r.ly; o[8] = t0; o[9] = t1;
+    o[10] = ok ? 1.0 : 0.0;
+    feat_out[node] = ok ? bf + f0 : 0;
+  }
+  const int B = Bs - 1;
+  for (int c = lane; c < Bs; c += 64) {
+    bool left;
+    if (!ok) left = true;
+    else if (c == Bs - 1) left = r.opt == 1;
+    else if (r.opt == 2) left = c < B;
+    else left = c <= r.t;
+    mask[(size_t)node * Bs + c] = left ? 1 : 0;
+  }
+}
+
+extern "C" int h2o_split_select2(const void* rec, const double* H, int Fl, int n, int Bs, int f0, double min_w2,
+                                 int stride, double* pk, uint8_t* mask, int* feat_out, hipStream_t s) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(split_select2_kernel, dim3(n), dim3(64), 0, s, (const SplitRec*)rec, H, Fl, n, Bs, f0, min_w2,
+                     stride, pk, mask, feat_out);
+  return (int)hipGetLastError();
+}

@@ -322,6 +322,98 @@ def partition(bd, ridx, ridx_out, feats, masks, starts, counts, use_native=None,
     return out
 
 
+def partition_async(bd, ridx, ridx_out, feat_d, masks, starts, counts, chunk=16384, payload=None, pk=None,
+                    pk_col=0):
+    """Sync-free ballot partition of EVERY segment i by masks[i][code(row,
+    feat_d[i])] (feat_d, masks on device; a segment whose mask is all ones stays
+    in place).  The per-chunk left counts are scanned into compaction offsets by
+    one device kernel, so the host never waits between the flag and compaction
+    passes; returns the per-segment left counts as a DEVICE int64 tensor (and,
+    with pk, also writes them as doubles into column pk_col of the [n, stride]
+    split record, so they come back with the level's single host transfer).
+    payload = (pa, None, pa_out, None)."""
+    import numpy as np
+    dev = ridx.device
+    n = len(starts)
+    lib = _lib()
+    if not getattr(lib, "_typed_async", False):
+        lib.h2o_part_offsets.argtypes = [_c_void, _c_void, _c_int, _c_int, _c_void, _c_void, _c_void, _c_void,
+                                         _c_int, _c_int, _c_void]
+        lib._typed_async = True
+    items = make_work(starts, counts, range(n), chunk)
+    nleft = torch.zeros(n, dtype=torch.int64, device=dev)
+    if len(items) == 0:
+        if pk is not None:
+            pk[:, pk_col] = 0.0
+        return nleft
+    nw = len(items)
+    words = (items[:, 2].astype(np.int64) + 63) // 64
+    fb_h = (np.cumsum(words) - words).astype(np.int64)
+    slot = items[:, 0].astype(np.int64)
+    first = np.ones(nw, dtype=bool)
+    first[1:] = slot[1:] != slot[:-1]
+    first_idx = np.maximum.accumulate(np.where(first, np.arange(nw), 0))
+    st_arr = np.asarray(starts, dtype=np.int64)[slot]
+    pos = items[:, 1].astype(np.int64) - st_arr
+    # ONE host->device upload: per-chunk meta (int64 x4), the work items and the
+    # flag-word bases (int32 views of the same buffer)
+    meta_h = np.concatenate([np.stack([slot, first_idx, st_arr, pos], 0).reshape(-1).view(np.int32),
+                             items.reshape(-1), fb_h.astype(np.int32)])
+    buf = torch.from_numpy(meta_h).to(dev, non_blocking=True)
+    meta = buf[: 8 * nw].view(torch.int64)
+    work = buf[8 * nw: 12 * nw]
+    fbase = buf[12 * nw:]
+    feat_t = feat_d if feat_d.dtype == torch.int32 else feat_d.to(torch.int32)
+    masks = masks if masks.dtype == torch.uint8 else masks.to(torch.uint8)
+    cnt = torch.empty(nw, dtype=torch.int32, device=dev)
+    if bd.codes_col is not None:
+        codes, rs, fs = bd.codes_col, 1, bd.nrows_local
+    else:
+        codes, rs, fs = bd.codes, bd.Fp, 1
+    flags = torch.empty(int(words.sum()) + 1, dtype=torch.int64, device=dev)
+    rc = lib.h2o_part_flags(_ptr(codes), bd.code_bytes, rs, fs, _ptr(ridx), _ptr(work), _ptr(fbase), nw,
+                            _ptr(feat_t), _ptr(masks), bd.Bs, _ptr(flags), _ptr(cnt), _stream())
+    if rc != 0:
+        raise RuntimeError(f"h2o_part_flags failed: {rc}")
+    loff = torch.empty(nw, dtype=torch.int32, device=dev)
+    roff = torch.empty(nw, dtype=torch.int32, device=dev)
+    stride = pk.stride(0) if pk is not None else 0
+    rc = lib.h2o_part_offsets(_ptr(cnt), _ptr(meta), nw, n, _ptr(loff), _ptr(roff), _ptr(nleft), _ptr(pk),
+                              stride, pk_col, _stream())
+    if rc != 0:
+        raise RuntimeError(f"h2o_part_offsets failed: {rc}")
+    pa, _, pa_o, _ = payload if payload is not None else (None, None, None, None)
+    rc = lib.h2o_part_compact(_ptr(ridx), _ptr(work), _ptr(fbase), nw, _ptr(flags), _ptr(loff), _ptr(roff),
+                              _ptr(ridx_out), _ptr(pa), _ptr(pa_o), _stream())
+    if rc != 0:
+        raise RuntimeError(f"h2o_part_compact failed: {rc}")
+    return nleft
+
+
+def hist_sibling(Hb, H_prev, build_slots, der_slots, par_slots, n_front, clamp_mask, wyy_b=None, wyy_prev=None):
+    """Next-level histograms in one kernel: built children copied, siblings =
+    parent - built (clamped at 0 on the channels of clamp_mask).  Returns
+    (H [F, n_front, Bs, C], wyy [n_front] or None)."""
+    import numpy as np
+    lib = _lib()
+    if not getattr(lib, "_typed_sib", False):
+        lib.h2o_hist_sibling.argtypes = [_c_void, _c_void, _c_void, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
+                                         _c_int, _c_void, _c_void, _c_void, _c_void, _c_void]
+        lib._typed_sib = True
+    F, nb, Bs, C = Hb.shape
+    H = torch.empty((F, n_front, Bs, C), dtype=Hb.dtype, device=Hb.device)
+    slots = torch.from_numpy(np.asarray([build_slots, der_slots, par_slots], dtype=np.int32).reshape(-1)).to(
+        Hb.device, non_blocking=True)
+    wyy = torch.empty(n_front, dtype=torch.float64, device=Hb.device) if wyy_b is not None else None
+    Hb = Hb.contiguous()
+    Hp = H_prev.contiguous()
+    rc = lib.h2o_hist_sibling(_ptr(Hb), _ptr(Hp), _ptr(slots), nb, Hp.shape[1], n_front, F, Bs * C, C, clamp_mask,
+                              _ptr(H), _ptr(wyy_b), _ptr(wyy_prev), _ptr(wyy), _stream())
+    if rc != 0:
+        raise RuntimeError(f"h2o_hist_sibling failed: {rc}")
+    return H, wyy
+
+
 def fill_nid(ridx, leaf_ids, starts, counts, nrows, use_native=None):
     """Per-row leaf index from leaf segments."""
     dev = ridx.device

@@ -68,6 +68,82 @@ def test_partition_matches_reference(impl, monkeypatch):
     assert torch.equal(out_g, out_r)
 
 
+def test_partition_async_matches_reference():
+    """Sync-free partition (device-side offset scan, all-ones mask = node kept
+    in place) against the torch reference, with a position-ordered payload."""
+    _need_gpu()
+    from h2o3_amd.ops import tree_ops
+    bd, _ = _binned(n=50000)
+    n = bd.nrows_local
+    ridx = torch.randperm(n, device="cuda").to(torch.int32)
+    starts, counts = [0, 20003, 30000, 45001], [19999, 9997, 15001, 4999]
+    feats = [0, 4, 2, 7]
+    masks = (torch.rand((4, bd.Bs), device="cuda") < 0.5).to(torch.uint8)
+    masks[2] = 1   # a node that does not split: rows stay where they are
+    pay = torch.randn(n, device="cuda")
+    out_g, pay_g = ridx.clone(), pay.clone()
+    out_r = ridx.clone()
+    nl_g = tree_ops.partition_async(bd, ridx, out_g, torch.tensor(feats, device="cuda"), masks, starts, counts,
+                                    chunk=4096, payload=(pay, None, pay_g, None))
+    nl_r = tree_ops.partition(bd, ridx, out_r, feats, masks, starts, counts, use_native=False)
+    assert nl_g.cpu().tolist() == nl_r
+    assert torch.equal(out_g, out_r)
+    # payload moved with the rows: pay is position ordered
+    pos_of = torch.empty(n, dtype=torch.long, device="cuda")
+    pos_of[ridx.long()] = torch.arange(n, device="cuda")
+    seg = torch.zeros(n, dtype=torch.bool, device="cuda")
+    for s, c in zip(starts, counts):
+        seg[s:s + c] = True
+    assert torch.equal(pay_g[seg], pay[pos_of[out_g.long()]][seg])
+
+
+@pytest.mark.parametrize("mode,clamp", [(0, 0b1), (1, 0b0), (3, 0b1111)])
+def test_hist_sibling_matches_torch(mode, clamp):
+    _need_gpu()
+    from h2o3_amd.ops import tree_ops
+    C = tree_ops.channels(mode)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    F, npar, Bs = 7, 5, 33
+    Hp = torch.rand((F, npar, Bs, C), generator=g, device="cuda", dtype=torch.float64)
+    Hb = torch.rand((F, npar, Bs, C), generator=g, device="cuda", dtype=torch.float64) * 0.7
+    bs, ds, ps = [0, 3, 4, 7, 9], [1, 2, 5, 6, 8], [0, 1, 2, 3, 4]
+    wb = torch.rand(5, generator=g, device="cuda", dtype=torch.float64)
+    wp = torch.rand(5, generator=g, device="cuda", dtype=torch.float64) + 1
+    H, wyy = tree_ops.hist_sibling(Hb, Hp, bs, ds, ps, 10, clamp, wyy_b=wb, wyy_prev=wp)
+    ref = torch.empty((F, 10, Bs, C), dtype=torch.float64, device="cuda")
+    ref[:, bs] = Hb
+    d = Hp[:, ps] - Hb
+    for c in range(C):
+        if (clamp >> c) & 1:
+            d[..., c] = d[..., c].clamp_min(0)
+    ref[:, ds] = d
+    torch.testing.assert_close(H, ref)
+    wr = torch.empty(10, dtype=torch.float64, device="cuda")
+    wr[bs] = wb
+    wr[ds] = wp[ps] - wb
+    torch.testing.assert_close(wyy, wr)
+
+
+def test_grow_async_matches_sync(monkeypatch):
+    """The sync-free level loop grows the same tree as the two-sync loop."""
+    _need_gpu()
+    from h2o3_amd.models.tree.engine import GrowParams, TreeGrower
+    bd, feats = _binned(n=60000, cats=False)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    y = (feats[0].nan_to_num() + 0.3 * torch.randn(60000, generator=g, device="cuda")).contiguous()
+    w = torch.ones(60000, device="cuda")
+    trees = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("H2O3_ASYNC_PART", flag)
+        gr = TreeGrower(bd, GrowParams(max_depth=6, min_rows=10))
+        tree, nid, leaves, tot = gr.grow(y, w, 0)
+        trees.append((tree, nid.cpu(), tot))
+    (ta, na, sa), (tb, nb, sb) = trees
+    assert ta.feat == tb.feat and ta.left == tb.left and ta.split_code == tb.split_code
+    assert torch.equal(na, nb)
+    torch.testing.assert_close(sa, sb)
+
+
 def test_forest_predict_matches_host():
     _need_gpu()
     import pandas as pd
