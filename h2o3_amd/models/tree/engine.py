@@ -766,9 +766,16 @@ class TreeGrower:
                 if len(f) > 4:
                     self._pending_leaf_segs.append((f[0], f[1], f[2]))
             # parent hists for the next level (only split nodes)
-            sid = torch.tensor(split_ids, device=H.device)
-            H_prev = H[:, sid]
-            wyy_prev = wyy_level[sid] if (mode == 0 and wyy_level is not None) else None
+            if self.dev.type == "cuda":
+                # the sibling kernel indexes the parent level directly: keep the
+                # whole level and remap the pairs' parent slots
+                H_prev = H
+                wyy_prev = wyy_level if mode == 0 else None
+                new_pairs = [(l_, r_, split_ids[j_], bl_) for (l_, r_, j_, bl_) in new_pairs]
+            else:
+                sid = torch.tensor(split_ids, device=H.device)
+                H_prev = H[:, sid]
+                wyy_prev = wyy_level[sid] if (mode == 0 and wyy_level is not None) else None
             pair_info = new_pairs
             frontier = new_front
             level += 1

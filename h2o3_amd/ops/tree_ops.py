@@ -144,8 +144,15 @@ def hist_build(bd, ridx, va, vb, mode, starts, counts, n_slots, use_native=None,
     in position (row-permutation) order instead of row order."""
     C = channels(mode)
     dev = ridx.device
-    hist = torch.zeros((bd.F, n_slots, bd.Bs, C), dtype=torch.float64, device=dev)
-    wyy = torch.zeros(n_slots, dtype=torch.float64, device=dev) if (want_wyy and mode == 0) else None
+    nh = bd.F * n_slots * bd.Bs * C
+    if want_wyy and mode == 0:
+        # one zero-fill for the histogram and the per-slot w*y*y sums
+        buf = torch.zeros(nh + n_slots, dtype=torch.float64, device=dev)
+        hist = buf[:nh].view(bd.F, n_slots, bd.Bs, C)
+        wyy = buf[nh:]
+    else:
+        hist = torch.zeros((bd.F, n_slots, bd.Bs, C), dtype=torch.float64, device=dev)
+        wyy = None
     ret = (lambda: (hist, wyy)) if want_wyy else (lambda: hist)
     native = dev.type == "cuda" if use_native is None else use_native
     if native:
@@ -341,8 +348,9 @@ def partition_async(bd, ridx, ridx_out, feat_d, masks, starts, counts, chunk=163
                                          _c_int, _c_int, _c_void]
         lib._typed_async = True
     items = make_work(starts, counts, range(n), chunk)
-    nleft = torch.zeros(n, dtype=torch.int64, device=dev)
+    nleft = torch.empty(n, dtype=torch.int64, device=dev)   # zeroed by the offsets kernel
     if len(items) == 0:
+        nleft.zero_()
         if pk is not None:
             pk[:, pk_col] = 0.0
         return nleft
