@@ -20,7 +20,14 @@ from ..parallel import cloud
 
 class DataInfo:
     def __init__(self, frame, x, standardize=True, use_all_factor_levels=False, missing_values_handling="MeanImputation",
-                 plug_values=None, pad_to=32, max_cat_levels=None, intercept=True, pad_extra=0):
+                 plug_values=None, pad_to=32, max_cat_levels=None, intercept=True, pad_extra=0, interactions=None):
+        # interactions: list of (a, b) column pairs -> extra features (glm/interactions.py)
+        self.ia_recipe = None
+        if interactions:
+            from .glm.interactions import apply_recipe, build_recipe
+            self.ia_recipe = build_recipe(frame, interactions)
+            frame, new_x = apply_recipe(frame, self.ia_recipe)
+            x = list(x) + new_x
         self.x = list(x)
         self.standardize = standardize
         self.use_all = use_all_factor_levels
@@ -66,6 +73,9 @@ class DataInfo:
 
     def expand(self, frame, dtype=torch.float32, pad=True):
         """Returns (X [n, P or Pp], row_ok mask) on device."""
+        if self.ia_recipe:
+            from .glm.interactions import apply_recipe
+            frame = apply_recipe(frame, self.ia_recipe)[0]
         n = frame.nlocal
         dev = cloud.device()
         P = self.Pp if pad else self.P

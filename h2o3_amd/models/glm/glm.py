@@ -164,9 +164,21 @@ def _soft(x, t):
 
 
 def _solve_quadratic(G, b, l1, l2, intercept, beta0=None, non_negative=False, max_iter=1000, tol=1e-10,
-                     penalty_mask=None):
-    """min 1/2 b'Gb - b'x + l1|b|_1 + l2/2|b|^2 (last coef = intercept, unpenalized)."""
+                     penalty_mask=None, lower=None, upper=None, active=None):
+    """min 1/2 b'Gb - b'x + l1|b|_1 + l2/2|b|^2 (last coef = intercept, unpenalized),
+    optionally with box constraints lower <= b <= upper (beta_constraints) and a
+    subset of active coefficients (the others fixed at 0: collinear columns)."""
     P = G.shape[0]
+    if active is not None and not bool(np.all(active)):
+        idx = np.nonzero(active)[0]
+        sub = _solve_quadratic(G[np.ix_(idx, idx)], b[idx], l1, l2, intercept and bool(active[-1]),
+                               None if beta0 is None else beta0[idx],
+                               non_negative if not np.ndim(non_negative) else np.asarray(non_negative)[idx],
+                               max_iter, tol, None if penalty_mask is None else penalty_mask[idx],
+                               None if lower is None else lower[idx], None if upper is None else upper[idx])
+        out = np.zeros(P)
+        out[idx] = sub
+        return out
     pen = np.ones(P) if penalty_mask is None else penalty_mask.astype(float)
     if intercept:
         pen[-1] = 0.0
@@ -174,14 +186,18 @@ def _solve_quadratic(G, b, l1, l2, intercept, beta0=None, non_negative=False, ma
     if intercept:
         nn[-1] = False
     non_negative = bool(nn.any())
-    if l1 == 0 and not non_negative:
+    lo = np.full(P, -np.inf) if lower is None else np.asarray(lower, dtype=np.float64)
+    hi = np.full(P, np.inf) if upper is None else np.asarray(upper, dtype=np.float64)
+    lo = np.where(nn, np.maximum(lo, 0.0), lo)
+    boxed = bool(np.isfinite(lo).any() or np.isfinite(hi).any())
+    if l1 == 0 and not boxed:
         A = G + np.diag(l2 * pen + 1e-10 * np.maximum(np.diag(G), 1e-12) * 0)
         try:
             L = np.linalg.cholesky(A + np.eye(P) * 1e-12 * max(1.0, np.abs(np.diag(A)).max()))
             return np.linalg.solve(L.T, np.linalg.solve(L, b))
         except np.linalg.LinAlgError:
             return np.linalg.lstsq(A, b, rcond=None)[0]
-    beta = np.zeros(P) if beta0 is None else beta0.copy()
+    beta = np.zeros(P) if beta0 is None else np.clip(beta0.copy(), lo, hi)
     diag = np.diag(G) + l2 * pen
     grad = b - G @ beta
     for it in range(max_iter):
@@ -191,9 +207,7 @@ def _solve_quadratic(G, b, l1, l2, intercept, beta0=None, non_negative=False, ma
                 continue
             old = beta[j]
             r = grad[j] + G[j, j] * old
-            nb = _soft(r, l1 * pen[j]) / diag[j]
-            if nn[j]:
-                nb = max(nb, 0.0)
+            nb = min(max(_soft(r, l1 * pen[j]) / diag[j], lo[j]), hi[j])
             if nb != old:
                 d = nb - old
                 grad -= G[:, j] * d
@@ -224,9 +238,12 @@ class GLMDriver:
             link_eff = link
         self.fam = _Fam(fam, link_eff, float(p.get("tweedie_variance_power") or 0.0),
                         float(p.get("tweedie_link_power") or 1.0), float(p.get("theta") or 1e-10))
+        from .interactions import interaction_pairs
         self.dinfo = DataInfo(spec.frame, spec.x, standardize=bool(p.get("standardize", True)),
                               missing_values_handling=p.get("missing_values_handling"),
-                              plug_values=p.get("plug_values"), pad_extra=2)
+                              plug_values=p.get("plug_values"), pad_extra=2,
+                              interactions=interaction_pairs(spec.x, p.get("interactions"),
+                                                             p.get("interaction_pairs")))
         self.X, ok = self.dinfo.expand(spec.frame)
         y = spec.y_tensor()
         if spec.is_classification:
@@ -251,7 +268,8 @@ class GLMDriver:
         solver = (p.get("solver") or "AUTO").upper()
         if alpha is None:
             alpha = 0.0 if solver == "L_BFGS" else 0.5
-        self.alpha = float(alpha[0] if isinstance(alpha, (list, tuple)) else alpha)
+        self.alphas = [float(a) for a in alpha] if isinstance(alpha, (list, tuple)) else [float(alpha)]
+        self.alpha = self.alphas[0]
         self.beta = np.zeros(self.P + 1)
         if self.intercept:
             mu0 = min(max(self.ymu, 1e-10), 1 - 1e-10) if self.fam.link == "logit" else self.ymu
@@ -259,6 +277,12 @@ class GLMDriver:
                 self.beta[-1] = self.fam.link_fn(mu0) if self.offset is None else 0.0
             except (ValueError, ZeroDivisionError):
                 self.beta[-1] = 0.0
+        self._init_beta = self.beta.copy()
+        self._setup_constraints(p.get("beta_constraints"))
+        sv = p.get("startval")
+        if sv is not None:
+            self._set_startval(sv)
+        self.active = None     # collinear-column mask (remove_collinear_columns)
         self.iter = 0
         self.lambda_max = self._lambda_max()
         lam = p.get("lambda_")
@@ -289,6 +313,95 @@ class GLMDriver:
         self.obj_eps = oe if oe > 0 else (1e-4 if p.get("lambda_search") else (1e-6 if self.lam == 0 else 1e-4))
         self.converged = False
         self.last_obj = float("inf")
+
+    # ---- constraints (GLM.java: beta_constraints frame names/lower_bounds/
+    # upper_bounds/beta_given/rho; bounds are given on the original scale and
+    # mapped to the standardized coefficients: b_std = b * sigma)
+    def _setup_constraints(self, bc):
+        P = self.P
+        self.lower = self.upper = None
+        self.rho = None
+        if bc is None:
+            return
+        import pandas as pd
+        df = bc.as_data_frame() if hasattr(bc, "as_data_frame") else pd.DataFrame(bc)
+        lo = np.full(P + 1, -np.inf)
+        hi = np.full(P + 1, np.inf)
+        given = np.zeros(P + 1)
+        rho = np.zeros(P + 1)
+        pos = {n: i for i, n in enumerate(self.dinfo.coef_names)}
+        scale = np.ones(P + 1)
+        if self.dinfo.standardize:
+            base = self.dinfo.n_cat_expanded
+            for j in range(len(self.dinfo.num_cols)):
+                scale[base + j] = self.dinfo.sigmas[j]
+        for _, r in df.iterrows():
+            name = str(r["names"])
+            targets = [pos[name]] if name in pos else \
+                [i for n, i in pos.items() if n.startswith(name + ".")]   # a categorical column: all its levels
+            if not targets:
+                raise ValueError(f"beta_constraints: unknown coefficient '{name}'")
+            for i in targets:
+                if "lower_bounds" in r and pd.notna(r["lower_bounds"]):
+                    lo[i] = float(r["lower_bounds"]) * scale[i]
+                if "upper_bounds" in r and pd.notna(r["upper_bounds"]):
+                    hi[i] = float(r["upper_bounds"]) * scale[i]
+                if "beta_given" in r and pd.notna(r["beta_given"]):
+                    given[i] = float(r["beta_given"]) * scale[i]
+                    rho[i] = float(r["rho"]) if "rho" in r and pd.notna(r["rho"]) else 1.0
+        if np.any(lo > hi):
+            raise ValueError("beta_constraints: lower bound above upper bound")
+        self.lower, self.upper = lo, hi
+        if rho.any():
+            self.rho, self.beta_given = rho, given
+        self.beta = np.clip(self.beta, lo, hi)
+
+    def _set_startval(self, sv):
+        """startval: initial coefficients on the original scale (names -> value,
+        or a list in coef order with the intercept last)."""
+        b = self.beta.copy()
+        if isinstance(sv, dict):
+            pos = {n: i for i, n in enumerate(self.dinfo.coef_names)}
+            for n, v in sv.items():
+                if n == "Intercept":
+                    b[-1] = float(v)
+                elif n in pos:
+                    b[pos[n]] = float(v)
+        else:
+            sv = list(sv)
+            b[: len(sv)] = sv
+        if self.dinfo.standardize:
+            base = self.dinfo.n_cat_expanded
+            for j in range(len(self.dinfo.num_cols)):
+                b[-1] += b[base + j] * self.dinfo.means[j]
+                b[base + j] *= self.dinfo.sigmas[j]
+        self.beta = b
+        self._init_beta = b.copy()
+
+    def _find_collinear(self, Gn):
+        """Greedy Cholesky with a pivot tolerance over the standardized Gram
+        (GLM.java removeCollinearColumns via Gram.qrCholesky): a column whose
+        residual variance after the columns kept so far is < 1e-7 of its own
+        variance is dropped (coefficient fixed at 0)."""
+        n = Gn.shape[0]
+        keep = np.ones(n, dtype=bool)
+        L = np.zeros((n, n))
+        kept = []
+        order = ([n - 1] + list(range(n - 1))) if self.intercept else list(range(n))   # intercept first
+        for j in order:
+            v = Gn[j, j]
+            if kept:
+                lj = np.linalg.solve(L[np.ix_(kept, kept)], Gn[kept, j]) if kept else np.zeros(0)
+                r = v - float(lj @ lj)
+            else:
+                lj, r = np.zeros(0), v
+            if r <= 1e-7 * max(v, 1e-300) and kept:
+                keep[j] = False
+                continue
+            L[j, kept] = lj
+            L[j, j] = math.sqrt(max(r, 1e-300))
+            kept.append(j)
+        return keep
 
     # ---- device-side pieces
     def _eta(self, beta=None):
@@ -415,14 +528,27 @@ class GLMDriver:
             P = self.P
             Gn = Gn.copy()
             Gn[:P, :P] += pen
+        if self.rho is not None:
+            # proximal term rho/2 (b - beta_given)^2 of beta_constraints
+            Gn = Gn.copy()
+            bn = bn.copy()
+            k = Gn.shape[0]
+            Gn[np.diag_indices(k)] += self.rho[:k]
+            bn += (self.rho * self.beta_given)[:k]
+        if self.est._parms.get("remove_collinear_columns") and self.active is None:
+            self.active = self._find_collinear(Gn)
+            self.removed_cols = [self.dinfo.coef_names[i] for i in range(self.P) if not self.active[i]]
         nonneg = bool(self.est._parms.get("non_negative"))
         nn_names = self.est._parms.get("_nonneg_names")
         if nn_names:
             s_ = set(nn_names)
             mask = np.array([nonneg or (c in s_) for c in self.dinfo.coef_names] + [False])
             nonneg = mask if self.intercept else mask[:-1]
+        k = Gn.shape[0]
         new = _solve_quadratic(Gn, bn, l1, l2, self.intercept, beta0=self.beta if self.intercept else self.beta[:-1],
-                               non_negative=nonneg)
+                               non_negative=nonneg, lower=None if self.lower is None else self.lower[:k],
+                               upper=None if self.upper is None else self.upper[:k],
+                               active=None if self.active is None else self.active[:k])
         if not self.intercept:
             new = np.concatenate([new, [0.0]])
         diff = float(np.max(np.abs(new - self.beta))) if new.size else 0.0
@@ -476,6 +602,9 @@ class H2OGeneralizedLinearEstimator(H2OEstimator):
         if fam in ("multinomial", "ordinal"):
             from .glm_multi import fit_multinomial
             return fit_multinomial(self, spec, fam)
+        if p.get("HGLM"):
+            from .hglm import fit_hglm
+            return fit_hglm(self, spec)
         solver = (p.get("solver") or "AUTO").upper()
         drv = GLMDriver(self, spec)
         self._drv_family = drv.family
@@ -486,30 +615,64 @@ class H2OGeneralizedLinearEstimator(H2OEstimator):
         max_rt = float(p.get("max_runtime_secs") or 0)
         path = []
         self._scoring_history = []
-        for li, lam in enumerate(drv.lambdas):
-            drv.lam = lam
-            drv.converged = False
-            drv.last_obj = float("inf")
-            its = 0
-            while its < maxit and not drv.converged:
-                drv.step()
-                its += 1
-                self._scoring_history.append({"iteration": drv.iter, "lambda": lam,
-                                              "deviance_train": drv.last_dev / drv.wsum, "objective": drv.last_obj})
-            dev = drv.deviance()
-            beta, icpt = drv.dinfo.destandardize(drv.beta[:-1], drv.beta[-1])
-            path.append({"lambda": lam, "alpha": drv.alpha, "beta_std": drv.beta.copy(), "beta": beta, "icpt": icpt,
-                         "deviance": dev, "explained_deviance_train": None})
-            if max_rt > 0 and time.time() - t0 > max_rt:
-                break
-        # pick submodel: best by validation deviance if given, else last
+        max_active = int(p.get("max_active_predictors") or -1)
+        user_lams = p.get("lambda_")
+        for alpha in drv.alphas:
+            # one regularization path per alpha (GLM.java: alpha x lambda grid)
+            if alpha != drv.alpha or len(drv.alphas) > 1:
+                drv.alpha = alpha
+                drv.beta = drv._init_beta.copy()
+                if p.get("lambda_search") or user_lams is None:
+                    drv.lambda_max = drv._lambda_max()
+                    lmr = drv.lambda_min_ratio
+                    if p.get("lambda_search") and user_lams is None:
+                        nl = int(p.get("nlambdas") or -1)
+                        nl = 100 if nl == -1 else nl
+                        dec = lmr ** (1.0 / max(nl - 1, 1))
+                        drv.lambdas = [drv.lambda_max * dec ** i for i in range(nl)]
+                    elif user_lams is None:
+                        drv.lambdas = [10 * lmr * drv.lambda_max]
+            for li, lam in enumerate(drv.lambdas):
+                drv.lam = lam
+                drv.converged = False
+                drv.last_obj = float("inf")
+                if p.get("cold_start") and li > 0:
+                    drv.beta = drv._init_beta.copy()
+                its = 0
+                while its < maxit and not drv.converged:
+                    drv.step()
+                    its += 1
+                    self._scoring_history.append({"iteration": drv.iter, "alpha": alpha, "lambda": lam,
+                                                  "deviance_train": drv.last_dev / drv.wsum,
+                                                  "objective": drv.last_obj})
+                dev = drv.deviance()
+                beta, icpt = drv.dinfo.destandardize(drv.beta[:-1], drv.beta[-1])
+                path.append({"lambda": lam, "alpha": alpha, "beta_std": drv.beta.copy(), "beta": beta,
+                             "icpt": icpt, "deviance": dev, "explained_deviance_train": None})
+                if max_active > 0 and int(np.sum(np.abs(drv.beta[:-1]) > 0)) > max_active:
+                    break   # GLM.java: stop the path once too many predictors are active
+                if max_rt > 0 and time.time() - t0 > max_rt:
+                    break
+        # pick submodel: best by validation deviance if given, else (several
+        # alphas) by training deviance of each alpha's last lambda, else last
         best = len(path) - 1
-        if p.get("lambda_search") and spec.valid is not None and len(path) > 1:
-            vdrv_devs = []
-            for sm in path:
-                vdrv_devs.append(self._dev_on(spec.valid, sm, drv))
+        if spec.valid is not None and len(path) > 1 and (p.get("lambda_search") or len(drv.alphas) > 1):
+            vdrv_devs = [self._dev_on(spec.valid, sm, drv) for sm in path]
             best = int(np.argmin(vdrv_devs))
+        elif len(drv.alphas) > 1:
+            ends = [i for i in range(len(path)) if i == len(path) - 1 or path[i + 1]["alpha"] != path[i]["alpha"]]
+            best = min(ends, key=lambda i: path[i]["deviance"])
         sm = path[best]
+        drv.alpha = sm["alpha"]
+        pr = float(p.get("prior") or -1)
+        if pr > 0 and drv.family == "binomial" and drv.intercept:
+            # prior correction of the intercept for over/under-sampled data (GLMModel)
+            ym = min(max(drv.ymu, 1e-10), 1 - 1e-10)
+            corr = math.log(pr / (1 - pr)) - math.log(ym / (1 - ym))
+            sm = dict(sm)
+            sm["beta_std"] = sm["beta_std"].copy()
+            sm["beta_std"][-1] += corr
+            sm["icpt"] += corr
         self._drv = drv
         self._beta_std = sm["beta_std"]
         self._beta = sm["beta"]
@@ -557,6 +720,10 @@ class H2OGeneralizedLinearEstimator(H2OEstimator):
                                          "number_of_active_predictors": int(np.sum(np.abs(self._beta) > 0)),
                                          "number_of_iterations": drv.iter}
         self._output["aic"] = self._aic(drv, res_dev, nz)
+        if self._parms.get("calc_like"):
+            self._output["loglikelihood"] = self._loglik(drv)
+        if getattr(drv, "removed_cols", None):
+            self._output["removed_collinear_columns"] = list(drv.removed_cols)
         if self._parms.get("compute_p_values"):
             self._p_values(drv)
         self._output["regularization_path"] = {"lambdas": [s["lambda"] for s in self._path],
@@ -596,6 +763,24 @@ class H2OGeneralizedLinearEstimator(H2OEstimator):
             ll = float((drv.w * (drv.y * torch.log(mu.clamp_min(1e-300)) - mu - torch.lgamma(drv.y + 1))).sum())
             return -2 * coll.allreduce_scalar(ll) + 2 * k
         return float("nan")
+
+    def _loglik(self, drv):
+        """Log-likelihood of the fitted model (calc_like; GLMModel likelihood)."""
+        eta = drv._eta()
+        mu = drv.fam.linkinv(eta)
+        y, w, f = drv.y, drv.w, drv.family
+        if f in ("binomial", "quasibinomial", "fractionalbinomial"):
+            m = mu.clamp(1e-15, 1 - 1e-15)
+            ll = (w * (y * torch.log(m) + (1 - y) * torch.log(1 - m))).sum()
+        elif f == "poisson":
+            ll = (w * (y * torch.log(mu.clamp_min(1e-300)) - mu - torch.lgamma(y + 1))).sum()
+        elif f == "gaussian":
+            rss = coll.allreduce_scalar(float((w * (y - mu) ** 2).sum()))
+            n = drv.wsum
+            return -0.5 * n * (math.log(2 * math.pi * rss / n) + 1)
+        else:
+            return float("nan")
+        return coll.allreduce_scalar(float(ll))
 
     def _p_values(self, drv):
         Ga, b, dev = drv._irls_stats()
@@ -681,7 +866,14 @@ class H2OGeneralizedLinearEstimator(H2OEstimator):
             eta = eta + torch.nan_to_num(frame.vec(off).as_float(torch.float64))
         return eta
 
+    def coefs_random(self):
+        """Random effects per random column and level (HGLM)."""
+        return dict(self._output.get("ubeta", {}))
+
     def _predict_raw(self, frame):
+        if getattr(self, "_hglm", None) is not None:
+            from .hglm import predict_hglm
+            return predict_hglm(self, frame)
         if getattr(self, "_multi", None) is not None:
             from .glm_multi import predict_multi
             return predict_multi(self, frame)
@@ -693,7 +885,8 @@ class H2OGeneralizedLinearEstimator(H2OEstimator):
 
     def _metrics_from_raw(self, spec, frame, raw, w=None):
         m = super()._metrics_from_raw(spec, frame, raw, w)
-        if m is not None and getattr(self, "_multi", None) is None and frame is spec.frame:
+        if m is not None and getattr(self, "_multi", None) is None and getattr(self, "_hglm", None) is None \
+                and frame is spec.frame:
             m._m["null_deviance"] = self._output.get("null_deviance")
             m._m["residual_deviance"] = self._output.get("residual_deviance")
             m._m["AIC"] = self._output.get("aic")

@@ -49,8 +49,10 @@ def _loss_grad_ordinal(X, y, w, beta, theta, wsum, K):
 
 def fit_multinomial(est, spec, fam):
     p = est._parms
+    from .interactions import interaction_pairs
     dinfo = DataInfo(spec.frame, spec.x, standardize=bool(p.get("standardize", True)),
-                     missing_values_handling=p.get("missing_values_handling"), plug_values=p.get("plug_values"))
+                     missing_values_handling=p.get("missing_values_handling"), plug_values=p.get("plug_values"),
+                     interactions=interaction_pairs(spec.x, p.get("interactions"), p.get("interaction_pairs")))
     X, ok = dinfo.expand(spec.frame)
     y = spec.y_tensor()
     ok &= y >= 0

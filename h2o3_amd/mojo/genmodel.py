@@ -78,8 +78,41 @@ class MojoModel:
         return np.stack([self._col(df, c, xd.get(c)) for c in self.meta["x"]], 1) if self.meta["x"] else \
             np.zeros((len(df), 0))
 
+    def _interactions(self, df, recipe):
+        """Replay the GLM interaction recipe (models/glm/interactions.py) on a
+        pandas frame."""
+        import pandas as pd
+        df = df.copy()
+        for r in recipe:
+            a, b = df.get(r["a"]), df.get(r["b"])
+            if r["kind"] == "nn":
+                df[r["name"]] = pd.to_numeric(a, errors="coerce").astype(float) * \
+                    pd.to_numeric(b, errors="coerce").astype(float)
+            elif r["kind"] == "cc":
+                lv = set(r["levels"])
+                vals = [f"{x}_{y}" if x is not None and y is not None and f"{x}_{y}" in lv else None
+                        for x, y in zip(a.astype(object).where(a.notna(), None).map(self._lvl),
+                                        b.astype(object).where(b.notna(), None).map(self._lvl))]
+                df[r["name"]] = vals
+            else:
+                xv = pd.to_numeric(b, errors="coerce").astype(float).fillna(0.0).values
+                av = a.astype(object).where(a.notna(), None).map(self._lvl)
+                for lvl in r["levels"]:
+                    df[f"{r['name']}.{lvl}"] = np.where(av == lvl, xv, 0.0)
+        return df
+
+    @staticmethod
+    def _lvl(v):
+        if v is None:
+            return None
+        if isinstance(v, float) and v.is_integer():
+            return str(int(v))
+        return str(v)
+
     def _expand(self, df):
         di = self.meta["di"]
+        if di.get("ia"):
+            df = self._interactions(df, di["ia"])
         n = len(df)
         X = np.zeros((n, di["P"]))
         for c in di["cat_cols"]:

@@ -95,7 +95,7 @@ def _dinfo_meta(w, di, prefix="di"):
     w.meta[prefix] = {"cat_cols": di.cat_cols, "num_cols": di.num_cols, "domains": di.domains,
                       "cat_offsets": di.cat_offsets, "use_all": di.use_all, "standardize": di.standardize,
                       "means": di.means, "sigmas": di.sigmas, "plug": di.plug, "cat_modes": di.cat_modes,
-                      "P": di.P, "mvh": di.mvh}
+                      "P": di.P, "mvh": di.mvh, "ia": getattr(di, "ia_recipe", None)}
 
 
 def _forest_arrays(w, forest, names):
