@@ -101,6 +101,51 @@ def tp_basis(x: torch.Tensor, knots: np.ndarray):
     return X, S
 
 
+def _tp_m(d):
+    return (d + 1) // 2 + 1
+
+
+def _poly_terms(d, m):
+    """Exponent tuples of the monomials of total degree < m in d variables."""
+    import itertools
+    return [e for e in itertools.product(range(m), repeat=d) if sum(e) < m]
+
+
+def _tp_eta(r, d, m):
+    p = 2 * m - d
+    if d % 2 == 0:
+        return torch.where(r > 0, r ** p * torch.log(r.clamp_min(1e-300)), torch.zeros_like(r)) \
+            if isinstance(r, torch.Tensor) else np.where(r > 0, r ** p * np.log(np.maximum(r, 1e-300)), 0.0)
+    return r ** p
+
+
+def tp_multi_basis(X: torch.Tensor, knots: np.ndarray):
+    """d-dimensional thin-plate regression spline (ThinPlateRegressionUtils):
+    radial part eta(|x - knot|) projected on the null space of the polynomial
+    constraint T' a = 0, plus the non-constant polynomial terms (degree < m,
+    m = floor((d+1)/2) + 1).  Returns ([n, k - M + M - 1], penalty)."""
+    n, d = X.shape
+    m = _tp_m(d)
+    terms = _poly_terms(d, m)
+    kn = np.asarray(knots, dtype=np.float64)
+    k = kn.shape[0]
+    Tk = np.stack([np.prod(kn ** np.asarray(e), 1) for e in terms], 1)          # [k, M]
+    Q, _ = np.linalg.qr(Tk, mode="complete")
+    ZT = Q[:, len(terms):]
+    knt = torch.as_tensor(kn, dtype=torch.float64, device=X.device)
+    r = torch.cdist(X.to(torch.float64), knt)
+    E = _tp_eta(r, d, m)
+    Xs = E @ torch.as_tensor(ZT, device=X.device)
+    poly = [torch.prod(X.to(torch.float64) ** torch.as_tensor(e, dtype=torch.float64, device=X.device), 1)
+            for e in terms if sum(e) > 0]
+    out = torch.cat([Xs] + [p.view(-1, 1) for p in poly], 1)
+    rk = np.sqrt(((kn[:, None, :] - kn[None, :, :]) ** 2).sum(-1))
+    Ekk = _tp_eta(rk, d, m)
+    S = np.zeros((out.shape[1], out.shape[1]))
+    S[: ZT.shape[1], : ZT.shape[1]] = ZT.T @ Ekk @ ZT
+    return out, S
+
+
 def _bspline(x: torch.Tensor, knots: np.ndarray, order: int):
     """B-spline basis of `order` (degree order-1) with clamped boundary knots."""
     t = np.concatenate([[knots[0]] * (order - 1), knots, [knots[-1]] * (order - 1)])
@@ -140,6 +185,10 @@ def is_basis(x, knots, order):
     return I, _diff_penalty(I.shape[1])
 
 
+def _gname(c):
+    return "_".join(c) if isinstance(c, tuple) else c
+
+
 # ---------------------------------------------------------------- estimator
 class H2OGeneralizedAdditiveEstimator(H2OGeneralizedLinearEstimator):
     algo = "gam"
@@ -160,6 +209,10 @@ class H2OGeneralizedAdditiveEstimator(H2OGeneralizedLinearEstimator):
             per("splines_non_negative", True)
 
     def _basis(self, frame, c, bs, knots, order):
+        if isinstance(c, tuple):
+            cols = [torch.where(torch.isnan(v), torch.full_like(v, self._col_means[cc]), v)
+                    for cc, v in ((cc, frame.vec(cc).as_float(torch.float64)) for cc in c)]
+            return tp_multi_basis(torch.stack(cols, 1), knots)
         x = frame.vec(c).as_float(torch.float64)
         x = torch.where(torch.isnan(x), torch.full_like(x, self._col_means[c]), x)
         if bs == 0:
@@ -174,8 +227,9 @@ class H2OGeneralizedAdditiveEstimator(H2OGeneralizedLinearEstimator):
 
     def _gam_frame(self, frame, fit=False):
         vecs, names = [], []
+        flat = {cc for c in self._gam_cols for cc in (c if isinstance(c, tuple) else (c,))}
         for c in frame.names:
-            if c in self._gam_cols and not self._parms.get("keep_gam_cols"):
+            if c in flat and not self._parms.get("keep_gam_cols"):
                 continue
             vecs.append(frame.vec(c))
             names.append(c)
@@ -191,25 +245,34 @@ class H2OGeneralizedAdditiveEstimator(H2OGeneralizedLinearEstimator):
                 else:
                     Q, _ = np.linalg.qr(cs.cpu().numpy().reshape(-1, 1), mode="complete")
                     Z = Q[:, 1:]
+                # penalty normalisation of the reference (GenCSSplineGamOneColumn.postGlobal):
+                # S *= max_row(sum|basis|)^2 / ||S||_inf, then centred, x scale, x2 in the Gram
+                rs = X.abs().sum(1).max()
+                rs = float(coll.allreduce_(rs.view(1).clone(), "max")[0])
+                inf = float(np.abs(S).sum(1).max()) if S.size else 0.0
+                if inf > 0 and (bs != 1 or self._parms.get("scale_tp_penalty_mat")):
+                    S = S * (rs * rs / inf)   # thin plate: only with scale_tp_penalty_mat (GAM.java:560)
                 self._Z.append(Z)
-                self._S.append(Z.T @ S @ Z)
+                self._S.append(2.0 * (Z.T @ S @ Z))
             Xc = X @ torch.as_tensor(self._Z[gi], dtype=X.dtype, device=X.device)
             suf = _SUFFIX[bs]
             for i in range(Xc.shape[1]):
                 vecs.append(Vec(Xc[:, i].to(torch.float32).contiguous(), T_REAL))
-                names.append(f"{c}_{suf}_{i}")
+                names.append(f"{_gname(c)}_{suf}_{i}")
         return H2OFrame.from_vecs(vecs, names)
 
     def train(self, x=None, y=None, training_frame=None, validation_frame=None, **kw):
         p = self._parms
         gc, bs, nk, scale, orders, nonneg = self._smoothers()
-        if any(isinstance(c, tuple) for c in gc):
-            raise NotImplementedError("multi-column (thin plate) smoothers: only single-column smoothers supported")
+        bs = [1 if isinstance(c, tuple) else b for c, b in zip(gc, bs)]   # several columns: thin plate only
         self._gam_cols, self._bs, self._orders = list(gc), [int(b) for b in bs], [int(o) for o in orders]
         self._knots, self._Z, self._S = [], [], []
         self._col_means = {}
         kids = p.get("knot_ids")
         for gi, c in enumerate(gc):
+            if isinstance(c, tuple):
+                self._knots.append(self._tp_knots(training_frame, c, nk[gi]))
+                continue
             v = training_frame.vec(c)
             xs = v.as_float(torch.float64)
             xs = xs[~torch.isnan(xs)]
@@ -225,24 +288,46 @@ class H2OGeneralizedAdditiveEstimator(H2OGeneralizedLinearEstimator):
             self._knots.append(knots)
         gfr = self._gam_frame(training_frame, fit=True)
         vfr = self._gam_frame(validation_frame) if validation_frame is not None else None
-        xs_ = [c for c in (x or [n for n in training_frame.names if n != y]) if c not in gc]
-        gam_names = [n for n in gfr.names if any(n.startswith(f"{c}_{_SUFFIX[b]}_") for c, b in zip(gc, self._bs))]
+        flat = {cc for c in gc for cc in (c if isinstance(c, tuple) else (c,))}
+        xs_ = [c for c in (x or [n for n in training_frame.names if n != y]) if c not in flat]
+        gam_names = [n for n in gfr.names if any(n.startswith(f"{_gname(c)}_{_SUFFIX[b]}_")
+                                                 for c, b in zip(gc, self._bs))]
         self._gam_penalty = []
         for gi, c in enumerate(gc):
-            nm = [n for n in gam_names if n.startswith(f"{c}_{_SUFFIX[self._bs[gi]]}_")]
+            nm = [n for n in gam_names if n.startswith(f"{_gname(c)}_{_SUFFIX[self._bs[gi]]}_")]
             self._gam_penalty.append((nm, float(scale[gi]) * self._S[gi]))
         if any(nonneg[gi] for gi in range(len(gc)) if self._bs[gi] == 2):
             self._parms.setdefault("_nonneg_names", [n for gi, c in enumerate(gc) if self._bs[gi] == 2
                                                      for n in gam_names if n.startswith(f"{c}_is_")])
-        keep = xs_ + ([c for c in gc] if p.get("keep_gam_cols") else [])
+        keep = xs_ + (sorted(flat) if p.get("keep_gam_cols") else [])
         super().train(x=[c for c in keep if c in gfr.names] + gam_names, y=y, training_frame=gfr,
                       validation_frame=vfr, **kw)
         self._output["knots"] = [k.tolist() for k in self._knots]
         self._output["gam_columns"] = self._gam_cols
         return self
 
+    def _tp_knots(self, frame, cols, k):
+        """Knots of a multi-column thin plate smoother: num_knots distinct data
+        rows drawn with the model seed (GAM.java picks knot rows from the data)."""
+        xs = []
+        for cc in cols:
+            v = frame.vec(cc).as_float(torch.float64)
+            self._col_means[cc] = float(coll.allreduce_scalar(float(torch.nansum(v)))) / max(
+                coll.allreduce_scalar(float((~torch.isnan(v)).sum())), 1)
+            xs.append(coll.all_gather_var(torch.where(torch.isnan(v), torch.full_like(v, self._col_means[cc]), v)))
+        Xa = torch.stack(xs, 1).cpu().numpy()
+        uniq = np.unique(Xa, axis=0)
+        d = len(cols)
+        M = len(_poly_terms(d, _tp_m(d)))
+        k = int(k) if k is not None else max(10, M + 2)
+        k = max(k, M + 1)
+        seed = self._parms.get("seed", -1)
+        rng = np.random.RandomState(1234 if seed in (None, -1) else int(seed) & 0x7FFFFFFF)
+        idx = rng.choice(len(uniq), size=min(k, len(uniq)), replace=False)
+        return uniq[np.sort(idx)]
+
     def _predict_raw(self, frame):
-        if any(n.startswith(tuple(f"{c}_{_SUFFIX[b]}_" for c, b in zip(self._gam_cols, self._bs)))
+        if any(n.startswith(tuple(f"{_gname(c)}_{_SUFFIX[b]}_" for c, b in zip(self._gam_cols, self._bs)))
                for n in frame.names):
             return super()._predict_raw(frame)
         return super()._predict_raw(self._gam_frame(frame))

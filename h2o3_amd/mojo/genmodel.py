@@ -101,6 +101,29 @@ class MojoModel:
                     df[f"{r['name']}.{lvl}"] = np.where(av == lvl, xv, 0.0)
         return df
 
+    def _gam_columns(self, df):
+        """Smoother columns <col>_<cr|tp|is|ms>_<i> from the stored knots and
+        centering matrices (mojo/gam_np.py)."""
+        from .gam_np import basis
+        g = self.meta["gam"]
+        suf = {0: "cr", 1: "tp", 2: "is", 3: "ms"}
+        df = df.copy()
+        from .gam_np import tp_multi_basis
+        for gi, c in enumerate(g["cols"]):
+            if isinstance(c, (list, tuple)):
+                Xm = np.stack([np.where(np.isnan(self._col(df, cc)), g["means"][cc], self._col(df, cc))
+                               for cc in c], 1)
+                Xc = tp_multi_basis(Xm, g["knots"][gi]) @ self._arr[f"gamZ{gi}"]
+                name = "_".join(c)
+            else:
+                x = self._col(df, c)
+                x = np.where(np.isnan(x), g["means"][c], x)
+                Xc = basis(x, g["bs"][gi], g["knots"][gi], g["orders"][gi]) @ self._arr[f"gamZ{gi}"]
+                name = c
+            for i in range(Xc.shape[1]):
+                df[f"{name}_{suf[g['bs'][gi]]}_{i}"] = Xc[:, i].astype(np.float32).astype(np.float64)
+        return df
+
     @staticmethod
     def _lvl(v):
         if v is None:
@@ -191,6 +214,9 @@ class MojoModel:
             rng = m["max_len"] - m["min_len"]
             sc = (m["max_len"] - ml) / rng if rng > 0 else np.zeros_like(ml)
             return np.stack([sc, ml], 1)
+        if a == "gam":
+            df = self._gam_columns(df)
+            a = "glm"
         if a == "glm":
             X = self._expand(df)
             if m.get("multi") == "multinomial":

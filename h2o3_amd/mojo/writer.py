@@ -131,8 +131,16 @@ def build_mojo(model) -> bytes:
             w.meta["min_len"] = model._min_len
             w.meta["max_len"] = model._max_len
             w.meta["threshold"] = model._threshold
-    elif algo == "glm":
+    elif algo in ("glm", "gam"):
+        if getattr(model, "_hglm", None) is not None:
+            raise NotImplementedError("MOJO export of HGLM models is not supported (as in the reference)")
         _dinfo_meta(w, model._dinfo)
+        if algo == "gam":
+            w.meta["gam"] = {"cols": model._gam_cols, "bs": model._bs, "orders": model._orders,
+                             "knots": [k.tolist() for k in model._knots], "means": model._col_means,
+                             "keep": bool(model._parms.get("keep_gam_cols"))}
+            for gi, Z in enumerate(model._Z):
+                w.add_array(f"gamZ{gi}", np.asarray(Z))
         if getattr(model, "_multi", None) is not None:
             m = model._multi
             w.meta["multi"] = m["kind"]

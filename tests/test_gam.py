@@ -41,7 +41,7 @@ def test_gam_fits_nonlinear_signal():
     fr = h2o.H2OFrame(df)
     for bs in (0, 1, 3):
         m = H2OGeneralizedAdditiveEstimator(family="gaussian", gam_columns=["x1", "x2"], num_knots=[12, 6], bs=[bs, 0],
-                                            scale=[0.001, 0.001])
+                                            scale=[0.0005, 0.0005])
         m.train(x=[], y="y", training_frame=fr)
         p = m.predict(fr).as_data_frame()["predict"].values
         assert np.sqrt(np.mean((p - y) ** 2)) < 0.15, bs
@@ -51,3 +51,29 @@ def test_gam_fits_nonlinear_signal():
     grid = h2o.H2OFrame(pd.DataFrame({"x2": np.linspace(0, 1, 50)}))
     pg = m.predict(grid).as_data_frame()["predict"].values
     assert (np.diff(pg) >= -1e-6).all()
+
+
+def test_gam_multicolumn_thin_plate_and_mojo():
+    from h2o3_amd.mojo.genmodel import MojoModel
+    from h2o3_amd.mojo.writer import build_mojo
+    h2o.init()
+    rng = np.random.default_rng(0)
+    n = 3000
+    x1, x2, x3 = rng.uniform(-2, 2, n), rng.uniform(-2, 2, n), rng.uniform(0, 1, n)
+    y = np.sin(x1 * x2) + x3 + rng.normal(scale=0.1, size=n)
+    df = pd.DataFrame({"x1": x1, "x2": x2, "x3": x3, "y": y})
+    fr = h2o.H2OFrame(df)
+    m = H2OGeneralizedAdditiveEstimator(family="gaussian", gam_columns=[["x1", "x2"], "x3"], num_knots=[40, 5],
+                                        bs=[1, 0], scale=[1e-4, 1e-3], seed=1)
+    m.train(x=[], y="y", training_frame=fr)
+    p = m.predict(fr).as_data_frame()["predict"].values
+    assert np.sqrt(np.mean((p - y) ** 2)) < 0.25
+    pm = np.asarray(MojoModel(build_mojo(m)).predict(df.drop(columns=["y"]))).reshape(-1)
+    np.testing.assert_allclose(pm, p, atol=1e-4)
+    # single-column smoothers of every kind through the MOJO
+    m2 = H2OGeneralizedAdditiveEstimator(family="gaussian", gam_columns=["x1", "x2", "x3"], bs=[0, 2, 3],
+                                         num_knots=[6, 5, 5])
+    m2.train(x=[], y="y", training_frame=fr)
+    p2 = m2.predict(fr).as_data_frame()["predict"].values
+    pm2 = np.asarray(MojoModel(build_mojo(m2)).predict(df.drop(columns=["y"]))).reshape(-1)
+    np.testing.assert_allclose(pm2, p2, atol=1e-4)
