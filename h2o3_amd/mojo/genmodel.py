@@ -49,6 +49,10 @@ class MojoModel:
         if self.algo == "stackedensemble":
             self._base = [MojoModel(self._z.read(f"models/{i}.zip")) for i in range(len(self.meta["base"]))]
             self._meta_model = MojoModel(self._z.read("models/meta.zip"))
+        if self.algo == "rulefit":
+            self._rf_trees = [MojoModel(self._z.read(f"models/tree_{i}.zip"))
+                              for i in range(len(self.meta["rf_trees"]))]
+            self._rf_glm = MojoModel(self._z.read("models/glm.zip"))
 
     @staticmethod
     def load(path):
@@ -155,6 +159,35 @@ class MojoModel:
         return X
 
     # ---------------------------------------------------------------- scoring
+    def _leaves(self, X):
+        """Terminal node id of every row in every tree: [n, T]."""
+        A = self._arr
+        feat, thr, left, right = A["forest_feat"], A["forest_thr"], A["forest_left"], A["forest_right"]
+        nal, coff, clen, bits = A["forest_na_left"], A["forest_cat_off"], A["forest_cat_len"], A["forest_cat_bits"]
+        roots = A["forest_roots"]
+        n = X.shape[0]
+        ar = np.arange(n)
+        out = np.zeros((n, len(roots)), dtype=np.int64)
+        for t in range(len(roots)):
+            nd = np.full(n, roots[t])
+            while True:
+                l = left[nd]
+                act = l >= 0
+                if not act.any():
+                    break
+                x = X[ar, feat[nd]]
+                isn = np.isnan(x)
+                co = coff[nd]
+                code = np.where(isn, -1, np.nan_to_num(x, nan=-1)).astype(np.int64)
+                inr = (code >= 0) & (code < clen[nd])
+                bit = bits[np.clip(co + np.maximum(code, 0), 0, len(bits) - 1)] != 0
+                gocat = np.where(isn | ~inr, nal[nd] != 0, bit)
+                gonum = np.where(isn, nal[nd] != 0, x.astype(np.float32) < thr[nd].astype(np.float32))
+                go = np.where(co >= 0, gocat, gonum)
+                nd = np.where(act, np.where(go, l, right[nd]), nd)
+            out[:, t] = nd - roots[t]
+        return out
+
     def _forest(self, X, K, leaf=False):
         A = self._arr
         feat, thr, left, right = A["forest_feat"], A["forest_thr"], A["forest_left"], A["forest_right"]
@@ -214,6 +247,22 @@ class MojoModel:
             rng = m["max_len"] - m["min_len"]
             sc = (m["max_len"] - ml) / rng if rng > 0 else np.zeros_like(ml)
             return np.stack([sc, ml], 1)
+        if a == "rulefit":
+            import pandas as pd
+            cols = []
+            for mi, tm in enumerate(self._rf_trees):
+                leaves = tm._leaves(tm._tree_matrix(df))
+                for ti in range(m["rf_trees"][mi]):
+                    cols.append(self._arr[f"anc_{mi}_{ti}"][leaves[:, ti]])
+            R = np.concatenate(cols, 1)[:, self._arr["keep_cols"]] if cols else np.zeros((len(df), 0))
+            d = {}
+            if m["mtype"] in ("RULES_AND_LINEAR", "RULES"):
+                for i, nm in enumerate(m["rule_names"]):
+                    d[nm] = R[:, i].astype(np.float64)
+            if m["mtype"] in ("RULES_AND_LINEAR", "LINEAR"):
+                for x in m["x"]:
+                    d[f"linear.{x}"] = df[x].values if x in df else np.full(len(df), np.nan)
+            return self._rf_glm.predict_raw(pd.DataFrame(d))
         if a == "gam":
             df = self._gam_columns(df)
             a = "glm"

@@ -229,6 +229,20 @@ def build_mojo(model) -> bytes:
         w.meta["prior"] = model._prior
         w.meta["te_params"] = {k: model._parms.get(k) for k in ("blending", "inflection_point", "smoothing",
                                                                "keep_original_categorical_columns")}
+    elif algo == "rulefit":
+        # nested tree MOJOs (leaf assignment) + ancestor tables -> rule columns,
+        # then the nested GLM MOJO on [rule_i..., linear.<x>...]
+        w.meta["rf_trees"] = []
+        for mi, tm in enumerate(model._trees):
+            w.files[f"models/tree_{mi}.zip"] = build_mojo(tm)
+            nt = len(tm._forest.trees)
+            w.meta["rf_trees"].append(nt)
+            for ti in range(nt):
+                w.add_array(f"anc_{mi}_{ti}", model._anc[(mi, ti)].cpu().numpy().astype(np.uint8))
+        w.add_array("keep_cols", model._keep_cols.cpu().numpy().astype(np.int64))
+        w.files["models/glm.zip"] = build_mojo(model._glm)
+        w.meta["mtype"] = model._mtype
+        w.meta["rule_names"] = model._rule_names
     elif algo == "stackedensemble":
         subs = []
         for i, bm in enumerate(model._base):

@@ -67,3 +67,23 @@ def test_mojo_uplift_w2v_te():
     te.train(x=["k"], y="t", training_frame=tfr)
     np.testing.assert_allclose(_rt(te, te_df)["k_te"].values, te.transform(tfr).as_data_frame()["k_te"].values,
                                atol=1e-5)
+
+
+def test_rulefit_mojo_matches_in_memory_scoring():
+    import numpy as np
+    import pandas as pd
+    import h2o3_amd as h2o
+    from h2o3_amd.estimators import H2ORuleFitEstimator
+    from h2o3_amd.mojo.genmodel import MojoModel
+    from h2o3_amd.mojo.writer import build_mojo
+    h2o.init(verbose=False)
+    rng = np.random.RandomState(0)
+    n = 1500
+    df = pd.DataFrame({"a": rng.randn(n), "b": rng.randn(n), "c": rng.choice(["u", "v", "w"], n)})
+    df["y"] = np.where((df.a > 0.3) & (df.c != "u"), "yes", "no")
+    fr = h2o.H2OFrame(df)
+    m = H2ORuleFitEstimator(max_rule_length=3, max_num_rules=20, seed=1)
+    m.train(y="y", training_frame=fr)
+    pm = np.asarray(MojoModel(build_mojo(m)).predict_raw(df.drop(columns=["y"])))
+    ph = m.predict(fr).as_data_frame()
+    np.testing.assert_allclose(pm[:, -1], ph.iloc[:, -1].values, atol=1e-6)
