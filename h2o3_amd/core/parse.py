@@ -78,6 +78,9 @@ def import_file(path, destination_frame=None, header=0, sep=None, col_names=None
         return _import_arrow(fs, "parquet", destination_frame, col_types)
     if ext == ".orc":
         return _import_arrow(fs, "orc", destination_frame, col_types)
+    if ext == ".avro":
+        from .avro import import_avro
+        return import_avro(fs, destination_frame, col_types)
     if ext in (".svm", ".svmlight", ".libsvm"):
         return _import_svmlight(fs, destination_frame)
     if ext == ".arff":
