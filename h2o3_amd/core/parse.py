@@ -24,7 +24,7 @@ import torch
 
 from ..parallel import cloud
 from .frame import H2OFrame, _local_slice, _vec_from_array
-from .vec import T_ENUM, T_INT, T_REAL, T_STR, T_TIME, Vec, make_enum, make_numeric, make_string, make_time
+from .vec import T_ENUM, T_INT, T_REAL, T_STR, T_TIME, T_UUID, Vec, make_enum, make_numeric, make_string, make_time
 
 _DEFAULT_NA = {"", "NA", "N/A", "NaN", "nan", "null", "NULL", "?", "-", "na", "n/a"}
 
@@ -93,6 +93,9 @@ def import_file(path, destination_frame=None, header=0, sep=None, col_names=None
                        quotechar)
 
 
+_UUID_RE = __import__("re").compile(r"^[0-9a-fA-F]{8}-[0-9a-fA-F]{4}-[0-9a-fA-F]{4}-[0-9a-fA-F]{4}-[0-9a-fA-F]{12}$")
+
+
 def _guess_string(codes, sample=10000):
     """String-vs-categorical guess (PreviewParseWriter.guessType: a column of
     strings with almost no duplicates -- distinct >= 95% of the non-NA
@@ -139,11 +142,15 @@ def _import_csv(fs, dest, header, sep, col_names, col_types, na_strings, skipped
                              for x in col["values"][s:e]])
         elif kind == "cat":
             dom, codes = col["domain"], col["codes"]
+            if want is None and dom and all(_UUID_RE.match(d) for d in dom[:1000]):
+                want = "uuid"   # ParseSetup guesses T_UUID for 8-4-4-4-12 hex tokens
             if want is None and _guess_string(codes):
                 want = "string"
             if want in ("string", "uuid"):
                 arr = np.array(dom + [None], dtype=object)[np.where(codes < 0, len(dom), codes)]
                 v = make_string(arr[s:e])
+                if want == "uuid":
+                    v.type = T_UUID
             elif want in ("real", "int", "numeric"):
                 vals = []
                 for d in dom:

@@ -885,7 +885,13 @@ class H2OGeneralizedLinearEstimator(H2OEstimator):
 
     def _metrics_from_raw(self, spec, frame, raw, w=None):
         m = super()._metrics_from_raw(spec, frame, raw, w)
-        if m is not None and getattr(self, "_multi", None) is None and getattr(self, "_hglm", None) is None \
+        multi = getattr(self, "_multi", None)
+        if m is not None and multi is not None and multi.get("kind") == "ordinal":
+            # ordinal family -> ModelMetricsOrdinal (hex/ModelMetricsOrdinal.java): same hit ratios,
+            # logloss and confusion matrix as multinomial, own category
+            m.__class__ = mm.ModelMetricsOrdinal
+            m.kind = "ordinal"
+        if m is not None and multi is None and getattr(self, "_hglm", None) is None \
                 and frame is spec.frame:
             m._m["null_deviance"] = self._output.get("null_deviance")
             m._m["residual_deviance"] = self._output.get("residual_deviance")

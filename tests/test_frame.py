@@ -67,3 +67,14 @@ def test_strings_and_time():
     assert fr["s"].tolower().levels()[0] == ["ab", "cd"]
     t = h2o.H2OFrame(pd.DataFrame({"t": pd.to_datetime(["2020-05-17", "2021-12-31"])}))
     assert t["t"].year().as_data_frame()["t"].tolist() == [2020, 2021]
+
+
+def test_uuid_column_guess(tmp_path):
+    import uuid
+    import h2o3_amd as h2o
+    h2o.init()
+    p = tmp_path / "u.csv"
+    p.write_text("id,x\n" + "".join(f"{uuid.UUID(int=i * 7919 + 12345)},{i}\n" for i in range(50)))
+    fr = h2o.import_file(str(p))
+    assert fr.types["id"] == "uuid"
+    assert fr["id"].as_data_frame().iloc[0, 0] == str(uuid.UUID(int=12345))
