@@ -611,6 +611,11 @@ class H2OEstimator:
         from .explain import explain_row
         return explain_row(self, frame, row_index, **kw)
 
+    def download_pojo(self, path="", get_genmodel_jar=False, genmodel_name=""):
+        """Java POJO scoring source (mojo/pojo.py); prints it when path is ""."""
+        from ..mojo.pojo import download_pojo
+        return download_pojo(self, path)
+
     def download_mojo(self, path=".", get_genmodel_jar=False, genmodel_name="", **kw):
         from ..mojo import writer
         return writer.write_mojo(self, path)
