@@ -617,7 +617,8 @@ class TreeGrower:
                 if async_part and "pk" in sp:
                     pkd = sp["pk"]
                     with phase("tree.partition"):
-                        ridx2.copy_(ridx)
+                        # no ridx2 <- ridx copy: every frontier segment is rewritten (non-splitting
+                        # nodes in place), earlier leaves are identical in both buffers already
                         pay = (self._pos1[0], None, self._pos1[1], None) if self._pos1 is not None else None
                         tree_ops.partition_async(bd, ridx, ridx2, sp["feat_i32"], sp["mask"],
                                                  [f[1] for f in frontier], [f[2] for f in frontier],
@@ -640,7 +641,6 @@ class TreeGrower:
                     mask_all = torch.where(ok_d.view(-1, 1), sp["mask"].to(torch.uint8),
                                            torch.ones_like(sp["mask"], dtype=torch.uint8))
                     with phase("tree.partition"):
-                        ridx2.copy_(ridx)
                         pay = (self._pos1[0], None, self._pos1[1], None) if self._pos1 is not None else None
                         nleft_d = tree_ops.partition_async(bd, ridx, ridx2, feat_all, mask_all,
                                                            [f[1] for f in frontier], [f[2] for f in frontier],

@@ -200,12 +200,28 @@ class GBMDriver:
             if self.dist.family == "huber":
                 self._update_huber_delta(y, f, w)
                 z = self.dist.neg_half_gradient(y, f).to(torch.float32)
-            fused = self.dev.type == "cuda" and self.dist.family in ("gaussian", "bernoulli") and \
-                self.dist.link in ("identity", "logit") and os.environ.get("H2O3_FUSED_LEAF", "0") == "1"
+            simple = self.dev.type == "cuda" and self.dist.family in ("gaussian", "bernoulli") and \
+                self.dist.link in ("identity", "logit")
+            fused = simple and os.environ.get("H2O3_FUSED_LEAF", "0") == "1"
+            # position-ordered residual payload + segment update: no per-row leaf ids at all
+            posleaf = simple and not fused and self.K == 1 and self.f.shape[1] == 1 and \
+                os.environ.get("H2O3_POS_LEAF", "1") == "1"
             with phase("gbm.grow"):
-                tree, nid, leaves, tot = self.grower.grow(z.contiguous(), w.contiguous(), 0, want_nid=not fused)
+                tree, nid, leaves, tot = self.grower.grow(z.contiguous(), w.contiguous(), 0,
+                                                          want_nid=not (fused or posleaf))
+            zpos = self.grower._pos1[0] if (posleaf and getattr(self.grower, "_pos1", None) is not None) else None
+            if posleaf and zpos is None:
+                posleaf = False
+                nid = tree_ops.fill_nid(self.grower.ridx, *self.grower.last_segs, z.shape[0])
             with phase("gbm.gamma"):
-                if fused:
+                if posleaf:
+                    lids, st, ct = self.grower.last_segs
+                    s_ = tree_ops.leaf_pos_sums(zpos, lids, st, ct, len(leaves),
+                                                1 if self.dist.family == "bernoulli" else 0)
+                    coll.allreduce_(s_)
+                    sh = s_.cpu().numpy()
+                    vals = np.where(sh[:, 1] != 0, sh[:, 0] / np.where(sh[:, 1] == 0, 1, sh[:, 1]), 0.0)
+                elif fused:
                     # one walk over the leaf segments: nid fill + gamma sums
                     lids, st, ct = self.grower.last_segs
                     nid, s_ = tree_ops.leaf_pass(self.grower.ridx, z, w, lids, st, ct, len(leaves), z.shape[0],
@@ -231,7 +247,11 @@ class GBMDriver:
                 tree.value[node] = float(lr * vals[li])
             with phase("gbm.update"):
                 vt = torch.tensor(lr * vals, dtype=torch.float32, device=self.dev)
-                self.f[:, 0] += vt[nid.long()]
+                if posleaf:
+                    lids, st, ct = self.grower.last_segs
+                    tree_ops.leaf_update(self.grower.ridx, self.f, vt, lids, st, ct)
+                else:
+                    self.f[:, 0] += vt[nid.long()]
             self.forest.add(tree, 0)
         else:
             P = torch.softmax(self.f, 1)

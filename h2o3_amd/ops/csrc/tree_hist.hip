@@ -638,6 +638,48 @@ __global__ __launch_bounds__(1024) void part_offsets_kernel(const int* __restric
     for (int s = threadIdx.x; s < n; s += blockDim.x) pk[(size_t)s * stride + col] = (double)nleft[s];
 }
 
+
+// Leaf gamma sums from the POSITION-ordered NaN-masked residual payload the
+// partition already moved with the rows (contiguous reads, no row gather);
+// NaN = zero-weight row.  mode 0: (sum z, count), mode 1 (bernoulli): (sum z,
+// sum |z|(1-|z|)).  work[i] = (leaf, start, count, -).
+__global__ __launch_bounds__(256) void leaf_pos_kernel(const float* __restrict__ zp, const int4* __restrict__ work,
+                                                       int mode, double* __restrict__ out) {
+  const int4 wk = work[blockIdx.x];
+  double sa = 0.0, sb = 0.0;
+  const int end = wk.y + wk.z;
+  for (int p = wk.y + threadIdx.x; p < end; p += 256) {
+    const float z = zp[p];
+    if (z == z) {
+      sa += (double)z;
+      if (mode == 1) {
+        const double az = fabs((double)z);
+        sb += az * (1.0 - az);
+      } else {
+        sb += 1.0;
+      }
+    }
+  }
+  sa = wave_sum(sa);
+  sb = wave_sum(sb);
+  __shared__ double red[2][4];
+  if (lane_id() == 0) { red[0][wave_id()] = sa; red[1][wave_id()] = sb; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    gbl_add(out + 2 * wk.x, red[0][0] + red[0][1] + red[0][2] + red[0][3]);
+    gbl_add(out + 2 * wk.x + 1, red[1][0] + red[1][1] + red[1][2] + red[1][3]);
+  }
+}
+
+// f[ridx[p]] += val[leaf] over the leaf segments: the prediction update without
+// materialising per-row leaf ids.
+__global__ __launch_bounds__(256) void leaf_update_kernel(const int* __restrict__ ridx, const int4* __restrict__ work,
+                                                          const float* __restrict__ val, float* __restrict__ f) {
+  const int4 wk = work[blockIdx.x];
+  const float v = val[wk.x];
+  for (int p = wk.y + threadIdx.x; p < wk.y + wk.z; p += 256) f[ridx[p]] += v;
+}
+
 // nid[ridx[p]] = leaf for p in segment.  work[i] = (leaf_id, start, count, -)
 __global__ __launch_bounds__(256) void fill_nid_kernel(const int* __restrict__ ridx, const int4* __restrict__ work,
                                                        int* __restrict__ nid) {
@@ -814,5 +856,18 @@ extern "C" int h2o_seg_sum2(const int* ridx, const float* a, const float* b, con
                             hipStream_t s) {
   if (n_work <= 0) return 0;
   hipLaunchKernelGGL(seg_sum2_kernel, dim3(n_work), dim3(256), 0, s, ridx, a, b, (const int4*)work, out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int h2o_leaf_pos(const float* zp, const int* work, int n_work, int mode, double* out, hipStream_t s) {
+  if (n_work <= 0) return 0;
+  hipLaunchKernelGGL(leaf_pos_kernel, dim3(n_work), dim3(256), 0, s, zp, (const int4*)work, mode, out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int h2o_leaf_update(const int* ridx, const int* work, int n_work, const float* val, float* f,
+                               hipStream_t s) {
+  if (n_work <= 0) return 0;
+  hipLaunchKernelGGL(leaf_update_kernel, dim3(n_work), dim3(256), 0, s, ridx, (const int4*)work, val, f);
   return (int)hipGetLastError();
 }

@@ -464,6 +464,39 @@ def leaf_pass(ridx, z, w, leaf_ids, starts, counts, n_leaves, nrows, mode, chunk
     return nid, out
 
 
+def leaf_pos_sums(zpos, leaf_ids, starts, counts, n_leaves, mode, chunk=65536):
+    """Per-leaf gamma sums from the position-ordered NaN-masked residual
+    payload (contiguous reads).  Returns [L, 2] f64 on device."""
+    lib = _lib()
+    if not getattr(lib, "_typed_lpos", False):
+        lib.h2o_leaf_pos.argtypes = [_c_void, _c_void, _c_int, _c_int, _c_void, _c_void]
+        lib.h2o_leaf_update.argtypes = [_c_void, _c_void, _c_int, _c_void, _c_void, _c_void]
+        lib._typed_lpos = True
+    out = torch.zeros((n_leaves, 2), dtype=torch.float64, device=zpos.device)
+    items = make_work(starts, counts, leaf_ids, chunk)
+    if len(items):
+        work = torch.from_numpy(items).to(zpos.device, non_blocking=True)
+        rc = lib.h2o_leaf_pos(_ptr(zpos), _ptr(work), len(items), int(mode), _ptr(out), _stream())
+        if rc != 0:
+            raise RuntimeError(f"h2o_leaf_pos failed: {rc}")
+    return out
+
+
+def leaf_update(ridx, f, vals, leaf_ids, starts, counts, chunk=65536):
+    """f[ridx[p]] += vals[leaf(p)] over the leaf segments (f: contiguous f32)."""
+    lib = _lib()
+    if not getattr(lib, "_typed_lpos", False):
+        lib.h2o_leaf_pos.argtypes = [_c_void, _c_void, _c_int, _c_int, _c_void, _c_void]
+        lib.h2o_leaf_update.argtypes = [_c_void, _c_void, _c_int, _c_void, _c_void, _c_void]
+        lib._typed_lpos = True
+    items = make_work(starts, counts, leaf_ids, chunk)
+    if len(items):
+        work = torch.from_numpy(items).to(f.device, non_blocking=True)
+        rc = lib.h2o_leaf_update(_ptr(ridx), _ptr(work), len(items), _ptr(vals), _ptr(f), _stream())
+        if rc != 0:
+            raise RuntimeError(f"h2o_leaf_update failed: {rc}")
+
+
 def seg_sum2(ridx, a, b, leaf_ids, starts, counts, n_leaves, use_native=None, chunk=65536):
     """Per-leaf sums of a[r] (and b[r]) over leaf segments of ridx -> [L, 2] f64."""
     dev = ridx.device

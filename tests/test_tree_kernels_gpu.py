@@ -235,3 +235,28 @@ def test_hist_packed_single_atomic(weights):
     h_ref = tree_ops.hist_build(bd, ridx, va, vb, 0, starts, counts, 2, use_native=False)
     torch.testing.assert_close(h_gpu[..., 0], h_ref[..., 0], rtol=0, atol=1e-9)   # counts exact
     torch.testing.assert_close(h_gpu[..., 1], h_ref[..., 1], rtol=1e-5, atol=1e-4)
+
+
+def test_gbm_position_leaf_path_matches_nid_path(monkeypatch):
+    """Leaf sums from the position-ordered payload + segment f-update give the
+    same boosted model as the per-row leaf-id path."""
+    _need_gpu()
+    import numpy as np
+    import pandas as pd
+    import h2o3_amd as h2o
+    from h2o3_amd.estimators import H2OGradientBoostingEstimator
+    h2o.init(device="cuda:0", verbose=False)
+    rng = np.random.RandomState(0)
+    n = 50000
+    X = rng.randn(n, 6).astype(np.float32)
+    y = (X[:, 0] + 0.5 * X[:, 1] ** 2 + 0.3 * rng.randn(n) > 0.4).astype(int)
+    df = pd.DataFrame(X, columns=[f"x{i}" for i in range(6)])
+    df["y"] = np.where(y == 1, "a", "b")
+    fr = h2o.H2OFrame(df)
+    preds = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("H2O3_POS_LEAF", flag)
+        m = H2OGradientBoostingEstimator(ntrees=8, max_depth=5, seed=3)
+        m.train(y="y", training_frame=fr)
+        preds.append(m.predict(fr).as_data_frame()["a"].values)
+    np.testing.assert_allclose(preds[0], preds[1], atol=2e-5)
