@@ -501,6 +501,130 @@ class H2OEstimator:
     def mean_residual_deviance(self, train=False, valid=False, xval=False): return self._pick("mean_residual_deviance", train, valid, xval)
     def confusion_matrix(self, train=False, valid=False, xval=False, **kw): return self._pick("confusion_matrix", train, valid, xval)
 
+    # ---- threshold metrics of binomial models (h2o-py model/models/binomial.py);
+    # several of train/valid/xval -> dict keyed by "train"/"valid"/"xval"
+    def _thr_metric(self, name, thresholds=None, train=False, valid=False, xval=False, **kw):
+        picks = [(k, getattr(self, a)) for k, a, f in (("train", "_training_metrics", train),
+                                                        ("valid", "_validation_metrics", valid),
+                                                        ("xval", "_cross_validation_metrics", xval)) if f]
+        if not picks:
+            picks = [("train", self._training_metrics)]
+        out = {}
+        for k, m in picks:
+            fn = getattr(m, name, None) if m is not None else None
+            out[k] = None if fn is None else (fn(thresholds, **kw) if thresholds is not None or kw else fn())
+        return out[picks[0][0]] if len(out) == 1 else out
+
+    def F1(self, thresholds=None, train=False, valid=False, xval=False): return self._thr_metric("F1", thresholds, train, valid, xval)
+    def F2(self, thresholds=None, train=False, valid=False, xval=False): return self._thr_metric("F2", thresholds, train, valid, xval)
+    def F0point5(self, thresholds=None, train=False, valid=False, xval=False): return self._thr_metric("F0point5", thresholds, train, valid, xval)
+    def accuracy(self, thresholds=None, train=False, valid=False, xval=False): return self._thr_metric("accuracy", thresholds, train, valid, xval)
+    def error(self, thresholds=None, train=False, valid=False, xval=False): return self._thr_metric("error", thresholds, train, valid, xval)
+    def precision(self, thresholds=None, train=False, valid=False, xval=False): return self._thr_metric("precision", thresholds, train, valid, xval)
+    def recall(self, thresholds=None, train=False, valid=False, xval=False): return self._thr_metric("recall", thresholds, train, valid, xval)
+    def sensitivity(self, thresholds=None, train=False, valid=False, xval=False): return self._thr_metric("recall", thresholds, train, valid, xval)
+    def tpr(self, thresholds=None, train=False, valid=False, xval=False): return self._thr_metric("tpr", thresholds, train, valid, xval)
+    def tnr(self, thresholds=None, train=False, valid=False, xval=False): return self._thr_metric("tnr", thresholds, train, valid, xval)
+    def fnr(self, thresholds=None, train=False, valid=False, xval=False): return self._thr_metric("fnr", thresholds, train, valid, xval)
+    def fpr(self, thresholds=None, train=False, valid=False, xval=False): return self._thr_metric("fpr", thresholds, train, valid, xval)
+    def fallout(self, thresholds=None, train=False, valid=False, xval=False): return self._thr_metric("fpr", thresholds, train, valid, xval)
+    def missrate(self, thresholds=None, train=False, valid=False, xval=False): return self._thr_metric("fnr", thresholds, train, valid, xval)
+    def specificity(self, thresholds=None, train=False, valid=False, xval=False): return self._thr_metric("specificity", thresholds, train, valid, xval)
+    def mcc(self, thresholds=None, train=False, valid=False, xval=False): return self._thr_metric("mcc", thresholds, train, valid, xval)
+    def max_per_class_error(self, thresholds=None, train=False, valid=False, xval=False): return self._thr_metric("max_per_class_error", thresholds, train, valid, xval)
+
+    def metric(self, metric, thresholds=None, train=False, valid=False, xval=False):
+        return self._pick_metrics(train, valid, xval).metric(metric, thresholds)
+
+    def _pick_metrics(self, train=False, valid=False, xval=False):
+        if xval:
+            return self._cross_validation_metrics
+        if valid:
+            return self._validation_metrics
+        return self._training_metrics
+
+    def roc(self, train=False, valid=False, xval=False):
+        return self._pick_metrics(train, valid, xval).roc()
+
+    def gains_lift(self, train=False, valid=False, xval=False):
+        return self._pick_metrics(train, valid, xval).gains_lift()
+
+    def kolmogorov_smirnov(self):
+        return self._training_metrics.kolmogorov_smirnov()
+
+    def find_threshold_by_max_metric(self, metric, train=False, valid=False, xval=False):
+        return self._pick_metrics(train, valid, xval).find_threshold_by_max_metric(metric)
+
+    def find_idx_by_threshold(self, threshold, train=False, valid=False, xval=False):
+        return self._pick_metrics(train, valid, xval).find_idx_by_threshold(threshold)
+
+    def hit_ratio_table(self, train=False, valid=False, xval=False):
+        return self._pick_metrics(train, valid, xval).hit_ratio_table()
+
+    def training_model_metrics(self):
+        return self._training_metrics.as_dict() if self._training_metrics is not None else None
+
+    # ---- model bookkeeping (h2o-py model_base.py)
+    @property
+    def start_time(self):
+        return self._start_time
+
+    @property
+    def end_time(self):
+        return self._end_time
+
+    @property
+    def run_time(self):
+        return int(self._run_time * 1000)
+
+    @property
+    def full_parameters(self):
+        return self.params
+
+    @property
+    def default_params(self):
+        return {k: v["default"] for k, v in self.params.items()}
+
+    @property
+    def have_mojo(self):
+        from ..mojo import writer
+        try:
+            writer.build_mojo(self)
+            return True
+        except Exception:
+            return False
+
+    @property
+    def have_pojo(self):
+        try:
+            from ..mojo.pojo import to_java
+            to_java(self)
+            return True
+        except Exception:
+            return False
+
+    def download_model(self, path="", filename=None, **kw):
+        from .persist import save_model
+        return save_model(self, path or ".", force=True, filename=filename)
+
+    def score_history(self):
+        return self.scoring_history()
+
+    def xval_keys(self):
+        return [m.model_id for m in self._cv_models]
+
+    def xvals(self):
+        return list(self._cv_models)
+
+    def get_summary(self):
+        return self._output.get("model_summary")
+
+    def show_summary(self):
+        print(self._output.get("model_summary"))
+
+    def detach(self):
+        dkv.remove(self.model_id)
+
     def scoring_history(self):
         import pandas as pd
         return pd.DataFrame(self._scoring_history)

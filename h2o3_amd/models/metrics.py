@@ -81,13 +81,51 @@ class ModelMetrics:
         return float(tt["threshold"][int(np.argmax(tt[metric]))])
 
     def F1(self, thresholds=None): return self.metric("f1", thresholds)
+    def F2(self, thresholds=None): return self.metric("f2", thresholds)
+    def F0point5(self, thresholds=None): return self.metric("f0point5", thresholds)
     def accuracy(self, thresholds=None): return self.metric("accuracy", thresholds)
     def precision(self, thresholds=None): return self.metric("precision", thresholds)
     def recall(self, thresholds=None): return self.metric("recall", thresholds)
+    sensitivity = recall
     def tpr(self, thresholds=None): return self.metric("tpr", thresholds)
+    def tnr(self, thresholds=None): return self.metric("tnr", thresholds)
+    def fnr(self, thresholds=None): return self.metric("fnr", thresholds)
     def fpr(self, thresholds=None): return self.metric("fpr", thresholds)
+    fallout = fpr
+    missrate = fnr
     def specificity(self, thresholds=None): return self.metric("specificity", thresholds)
     def mcc(self, thresholds=None): return self.metric("absolute_mcc", thresholds)
+
+    def error(self, thresholds=None):
+        acc = self.metric("accuracy", thresholds)
+        return None if acc is None else [[t, 1 - a] for t, a in acc]
+
+    def max_per_class_error(self, thresholds=None):
+        m = self.metric("min_per_class_accuracy", thresholds)
+        return None if m is None else [[t, 1 - a] for t, a in m]
+
+    def thresholds_and_metric_scores(self):
+        import pandas as pd
+        tt = self._m.get("thresholds_and_metric_scores")
+        return None if tt is None else pd.DataFrame(tt)
+
+    def thresholds(self):
+        tt = self._m.get("thresholds_and_metric_scores")
+        return None if tt is None else list(tt["threshold"])
+
+    def find_idx_by_threshold(self, threshold):
+        tt = self._m["thresholds_and_metric_scores"]
+        return int(np.argmin(np.abs(np.asarray(tt["threshold"]) - threshold)))
+
+    def roc(self):
+        """(fpr list, tpr list) over the threshold table."""
+        tt = self._m.get("thresholds_and_metric_scores")
+        return None if tt is None else (list(tt["fpr"]), list(tt["tpr"]))
+
+    def kolmogorov_smirnov(self):
+        """max(tpr - fpr) over thresholds (GainsLift KS of the reference)."""
+        tt = self._m.get("thresholds_and_metric_scores")
+        return None if tt is None else float(np.max(np.asarray(tt["tpr"]) - np.asarray(tt["fpr"])))
 
     def gains_lift(self):
         return self._m.get("gains_lift_table")

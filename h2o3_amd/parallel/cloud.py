@@ -47,7 +47,7 @@ def init(device: str | None = None, backend: str | None = None, timeout_s: float
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29511")
-        be = backend or ("nccl" if dev.type == "cuda" else "gloo")
+        be = backend or os.environ.get("H2O3_DIST_BACKEND") or ("nccl" if dev.type == "cuda" else "gloo")
         kw = {}
         if be == "nccl":
             kw["device_id"] = dev
@@ -112,7 +112,7 @@ def shutdown():
 
 def barrier():
     if is_distributed():
-        if is_gpu():
+        if is_gpu() and dist.get_backend() == "nccl":
             dist.barrier(device_ids=[device().index])
         else:
             dist.barrier()

@@ -16,14 +16,18 @@ import torch.distributed as dist
 from . import cloud
 
 
+def _rccl() -> bool:
+    """True when the process group is NCCL (= RCCL over xGMI on ROCm); gloo
+    (CPU clouds, or a one-GPU multi-rank rehearsal) lacks reduce_scatter /
+    all_gather_into_tensor and takes the portable paths below."""
+    return cloud.is_gpu() and dist.get_backend() == "nccl"
+
+
 def allreduce_(t: torch.Tensor, op: str = "sum") -> torch.Tensor:
     if not cloud.is_distributed():
         return t
     rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
-    if t.dtype == torch.float64 and cloud.is_gpu():
-        dist.all_reduce(t, op=rop)
-    else:
-        dist.all_reduce(t, op=rop)
+    dist.all_reduce(t, op=rop)
     return t
 
 
@@ -61,7 +65,7 @@ def reduce_scatter_dim0(t: torch.Tensor) -> torch.Tensor:
         return t
     assert t.shape[0] % w == 0
     out = torch.empty((t.shape[0] // w,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-    if cloud.is_gpu():
+    if _rccl():
         dist.reduce_scatter_tensor(out, t.contiguous())
     else:  # gloo has no reduce_scatter: all_reduce + slice
         dist.all_reduce(t)
@@ -74,7 +78,7 @@ def all_gather_dim0(t: torch.Tensor) -> torch.Tensor:
     if w == 1:
         return t
     out = torch.empty((t.shape[0] * w,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-    if cloud.is_gpu():
+    if _rccl():
         dist.all_gather_into_tensor(out, t.contiguous())
     else:
         parts = [torch.empty_like(t) for _ in range(w)]
@@ -107,8 +111,7 @@ def broadcast_object(obj, src: int = 0):
     if not cloud.is_distributed():
         return obj
     lst = [obj]
-    dist.broadcast_object_list(lst, src=src,
-                               device=cloud.device() if cloud.is_gpu() else None)
+    dist.broadcast_object_list(lst, src=src, device=cloud.device() if _rccl() else None)
     return lst[0]
 
 

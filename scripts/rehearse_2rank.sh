@@ -1,0 +1,12 @@
+# Two ranks on ONE GPU over gloo: exercises the multi-rank GPU code path
+# (feature reduce-scatter, candidate merge, sibling kernel on the local slice)
+# without RCCL (which refuses two ranks on one device).  Not a perf run.
+set -e
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+H2O3_DIST_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --standalone --nnodes=1 --nproc-per-node 2 \
+  bench.py --gpus 2 --rows 4000000 --steps 3 --warmup 1 > gpurun_out/rehearse2.log 2>&1
+grep '"metric"' gpurun_out/rehearse2.log | cut -c1-300
+H2O3_DIST_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --standalone --nnodes=1 --nproc-per-node 2 \
+  bench.py --gpus 2 --algo glm --rows 4000000 --steps 3 --warmup 1 > gpurun_out/rehearse2_glm.log 2>&1
+grep '"metric"' gpurun_out/rehearse2_glm.log | cut -c1-300
