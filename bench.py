@@ -11,7 +11,8 @@ partition, gamma (leaf value) pass and prediction update — nothing skipped.
 The total data size is fixed (strong scaling): with N GPUs every rank holds
 100M/N rows and histograms are reduce-scattered over RCCL.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--rows R] [--algo gbm|glm]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--rows R] [--algo gbm|glm|drf]
+       [--cols C] [--cat-cols K --cat-card L]   (DRF config: --algo drf --rows 50000000 --cols 500 --cat-cols 100)
 """
 import argparse
 import json
@@ -30,7 +31,10 @@ def main():
     ap.add_argument("--rows", type=int, default=100_000_000)
     ap.add_argument("--cols", type=int, default=100)
     ap.add_argument("--max-depth", type=int, default=8)
-    ap.add_argument("--algo", default="gbm", choices=["gbm", "glm"])
+    ap.add_argument("--algo", default="gbm", choices=["gbm", "glm", "drf"])
+    ap.add_argument("--cat-cols", type=int, default=0,
+                    help="replace this many of the --cols columns by categoricals (DRF config: mixed num/cat)")
+    ap.add_argument("--cat-card", type=int, default=1000, help="cardinality of the categorical columns")
     ap.add_argument("--histogram-type", default="QuantilesGlobal")
     ap.add_argument("--nbins", type=int, default=255)
     args = ap.parse_args()
@@ -54,7 +58,15 @@ def main():
     beta[: min(10, F)] = torch.randn(min(10, F), generator=gb)
     cols = []
     logit = torch.zeros(rows_local, device=dev)
+    n_cat = min(args.cat_cols, F)
+    cat_eff = torch.randn(args.cat_card, generator=gb) * 0.5
     for j in range(F):
+        if j >= F - n_cat:
+            c = torch.randint(0, args.cat_card, (rows_local,), generator=g, device=dev, dtype=torch.int32)
+            if j == F - n_cat:
+                logit += cat_eff.to(dev)[c.long()]
+            cols.append(c)
+            continue
         c = torch.randn(rows_local, generator=g, device=dev)
         if beta[j] != 0:
             logit += float(beta[j]) * c
@@ -65,7 +77,9 @@ def main():
     from h2o3_amd.core.frame import H2OFrame
     from h2o3_amd.core.vec import Vec, T_REAL, T_ENUM
     names = [f"x{j}" for j in range(F)]
-    vecs = [Vec(c, T_REAL) for c in cols] + [Vec(y, T_ENUM, ["0", "1"])]
+    dom = [f"L{i}" for i in range(args.cat_card)]
+    vecs = [Vec(c, T_ENUM, dom) if c.dtype == torch.int32 else Vec(c, T_REAL) for c in cols] + \
+        [Vec(y, T_ENUM, ["0", "1"])]
     fr = H2OFrame.from_vecs(vecs, names + ["y"])
     from h2o3_amd.models.base import TrainSpec
 
@@ -81,6 +95,18 @@ def main():
         metric = "gbm_trees_per_sec"
         unit = "trees/s"
         model = "GBM binomial 100Mx100 ntrees=500 max_depth=8"
+    elif args.algo == "drf":
+        from h2o3_amd.models.tree.drf import DRFDriver, H2ORandomForestEstimator
+        est = H2ORandomForestEstimator(ntrees=1000, max_depth=args.max_depth if args.max_depth != 8 else 20,
+                                       seed=42, histogram_type=args.histogram_type, nbins=args.nbins,
+                                       ignore_const_cols=False)
+        spec = TrainSpec(fr, names, "y")
+        est._spec = spec
+        drv = DRFDriver(est, spec)
+        step = drv.step
+        metric = "drf_trees_per_sec"
+        unit = "trees/s"
+        model = f"DRF binomial {args.rows // 1_000_000}Mx{F} ({n_cat} cat, card {args.cat_card}) ntrees=1000"
     else:
         from h2o3_amd.models.glm.glm import GLMDriver, H2OGeneralizedLinearEstimator
         est = H2OGeneralizedLinearEstimator(family="binomial", solver="IRLSM", lambda_=0.0)

@@ -47,49 +47,7 @@ class H2ORandomForestEstimator(SharedTreeEstimator):
 
     def _fit(self, spec):
         p = self._parms
-        # AUTO -> 254 global quantile bins: the reference re-bins every node
-        # adaptively (nbins_top_level -> nbins), a global 20-bin grid would be
-        # far coarser than that at depth (measured: 79% vs 99% train accuracy)
-        bd = self._bin(spec)
-        dev = cloud.device()
-        N = bd.nrows_local
-        F = bd.F
-        ncls = spec.nclasses
-        double = bool(p.get("binomial_double_trees"))
-        K = ncls if (ncls > 2 or (ncls == 2 and double)) else 1
-        self._K = K
-        self._binomial_single = ncls == 2 and K == 1
-        mtries = int(p.get("mtries", -1))
-        if mtries == -1:
-            mtries = max(1, int(math.floor(math.sqrt(F)))) if ncls > 1 else max(1, F // 3)
-        elif mtries == -2:
-            mtries = F
-        gp = GrowParams(criterion="se", max_depth=int(p["max_depth"]) if p["max_depth"] > 0 else 64,
-                        min_rows=float(p["min_rows"]), min_split_improvement=float(p["min_split_improvement"]),
-                        mtries=mtries if mtries < F else -1,
-                        col_sample_rate_change_per_level=float(p["col_sample_rate_change_per_level"]),
-                        seed=self._seed())
-        grower = TreeGrower(bd, gp)
-        y = spec.y_tensor()
-        w = spec.w_tensor()
-        base_w = torch.ones(N, dtype=torch.float32, device=dev) if w is None else w.to(torch.float32)
-        if spec.is_classification:
-            ycode = y.to(torch.int64)
-            valid = ycode >= 0
-            targets = [((ycode == (1 if self._binomial_single else k)).to(torch.float32)) for k in range(K)]
-        else:
-            yf = y.to(torch.float32)
-            valid = ~torch.isnan(yf)
-            targets = [torch.nan_to_num(yf)]
-        base_w = torch.where(valid, base_w, torch.zeros_like(base_w))
-        forest = Forest()
-        oob_sum = torch.zeros((N, K), dtype=torch.float32, device=dev)
-        oob_cnt = torch.zeros(N, dtype=torch.float32, device=dev)
-        gen = torch.Generator(device=dev)
-        gen.manual_seed(self._seed() + cloud.rank())
-        rng = np.random.RandomState(self._seed())
-        sr = float(p["sample_rate"])
-        srpc = p.get("sample_rate_per_class")
+        drv = DRFDriver(self, spec)
         ntrees = int(p["ntrees"])
         t0 = time.time()
         max_rt = float(p.get("max_runtime_secs") or 0)
@@ -99,35 +57,13 @@ class H2ORandomForestEstimator(SharedTreeEstimator):
         metric_name = self._stopping_metric(spec)
         history = []
         for t in range(ntrees):
-            if srpc is not None and spec.is_classification:
-                rates = torch.tensor(srpc, dtype=torch.float32, device=dev)[ycode.clamp(min=0)]
-                inbag = torch.rand(N, generator=gen, device=dev) < rates
-            else:
-                inbag = torch.rand(N, generator=gen, device=dev) < sr
-            wt = (base_w * inbag).contiguous()
-            r = float(p.get("col_sample_rate_per_tree", 1.0))
-            if r < 1.0:
-                kk = max(1, int(math.floor(r * F + 0.5)))
-                m = np.zeros(F, dtype=bool)
-                m[rng.choice(F, size=kk, replace=False)] = True
-                gp.tree_col_mask = m
-            for k in range(K):
-                tree, nid, leaves, tot = grower.grow(targets[k].contiguous(), wt, 0)
-                tot = tot.numpy() if isinstance(tot, torch.Tensor) else np.asarray(tot)
-                vals = np.where(tot[:, 0] > 0, tot[:, 1] / np.where(tot[:, 0] > 0, tot[:, 0], 1), 0.0)
-                for li, node in enumerate(leaves):
-                    tree.value[node] = float(vals[li])
-                vt = torch.tensor(vals, dtype=torch.float32, device=dev)
-                oob = ~inbag
-                oob_sum[:, k] += torch.where(oob, vt[nid.long()], torch.zeros(N, device=dev))
-                forest.add(tree, k)
-            oob_cnt += (~inbag).to(torch.float32)
+            drv.step()
             score_now = (interval and (t + 1) % interval == 0) or (stop_rounds and not interval) or t + 1 == ntrees
             if score_now:
                 entry = {"number_of_trees": t + 1}
                 if stop_rounds or interval:
-                    self._forest = forest
-                    self._score_entry(entry, spec, oob_sum, oob_cnt)
+                    self._forest = drv.forest
+                    self._score_entry(entry, spec, drv.oob_sum, drv.oob_cnt)
                 self._scoring_history.append(entry)
                 if stop_rounds:
                     key = ("validation_" if spec.valid is not None else "training_") + \
@@ -138,6 +74,7 @@ class H2ORandomForestEstimator(SharedTreeEstimator):
                         break
             if max_rt > 0 and time.time() - t0 > max_rt:
                 break
+        forest, K = drv.forest, drv.K
         self._forest = forest
         self._output["variable_importances"] = self._varimp_from_forest(forest, spec.x)
         self._output["model_summary"] = {"number_of_trees": len(forest) // K,
@@ -145,11 +82,10 @@ class H2ORandomForestEstimator(SharedTreeEstimator):
                                          "max_depth": max((tt.max_depth() for tt in forest.trees), default=0),
                                          "mean_leaves": float(np.mean([len(tt.leaves()) for tt in forest.trees]))}
         # out-of-bag predictions -> training metrics (reference reports OOB)
-        cnt = oob_cnt.clamp_min(1).view(-1, 1)
-        oobp = oob_sum / cnt
-        has = oob_cnt > 0
+        cnt = drv.oob_cnt.clamp_min(1).view(-1, 1)
+        oobp = drv.oob_sum / cnt
         self._oob_raw = self._normalize(oobp)
-        self._oob_mask = has
+        self._oob_mask = drv.oob_cnt > 0
         if p.get("calibrate_model") and p.get("calibration_frame") is not None:
             from .calibration import fit_calibration
             fit_calibration(self, p["calibration_frame"], p.get("calibration_method", "auto"))
@@ -210,6 +146,89 @@ class H2ORandomForestEstimator(SharedTreeEstimator):
             self._training_metrics = self._metrics_from_raw(spec, spec.frame, raw)
         if spec.valid is not None:
             self._validation_metrics = self._metrics_from_raw(spec, spec.valid, self._predict_raw(spec.valid))
+
+
+class DRFDriver:
+    """Random-forest state; `step()` grows one forest iteration (K class trees)
+    on a fresh row sample and folds its out-of-bag predictions in."""
+
+    def __init__(self, est, spec):
+        p = est._parms
+        self.est, self.spec = est, spec
+        # AUTO -> 254 global quantile bins: the reference re-bins every node
+        # adaptively (nbins_top_level -> nbins), a global 20-bin grid would be
+        # far coarser than that at depth (measured: 79% vs 99% train accuracy)
+        bd = est._bin(spec)
+        self.bd = bd
+        dev = cloud.device()
+        self.dev = dev
+        N = bd.nrows_local
+        F = bd.F
+        ncls = spec.nclasses
+        double = bool(p.get("binomial_double_trees"))
+        K = ncls if (ncls > 2 or (ncls == 2 and double)) else 1
+        self.K = est._K = K
+        est._binomial_single = ncls == 2 and K == 1
+        mtries = int(p.get("mtries", -1))
+        if mtries == -1:
+            mtries = max(1, int(math.floor(math.sqrt(F)))) if ncls > 1 else max(1, F // 3)
+        elif mtries == -2:
+            mtries = F
+        self.gp = GrowParams(criterion="se", max_depth=int(p["max_depth"]) if p["max_depth"] > 0 else 64,
+                             min_rows=float(p["min_rows"]), min_split_improvement=float(p["min_split_improvement"]),
+                             mtries=mtries if mtries < F else -1,
+                             col_sample_rate_change_per_level=float(p["col_sample_rate_change_per_level"]),
+                             seed=est._seed())
+        self.grower = TreeGrower(bd, self.gp)
+        y = spec.y_tensor()
+        w = spec.w_tensor()
+        base_w = torch.ones(N, dtype=torch.float32, device=dev) if w is None else w.to(torch.float32)
+        if spec.is_classification:
+            self.ycode = y.to(torch.int64)
+            valid = self.ycode >= 0
+            self.targets = [((self.ycode == (1 if est._binomial_single else k)).to(torch.float32))
+                            for k in range(K)]
+        else:
+            yf = y.to(torch.float32)
+            valid = ~torch.isnan(yf)
+            self.targets = [torch.nan_to_num(yf)]
+        self.base_w = torch.where(valid, base_w, torch.zeros_like(base_w))
+        self.forest = Forest()
+        self.oob_sum = torch.zeros((N, K), dtype=torch.float32, device=dev)
+        self.oob_cnt = torch.zeros(N, dtype=torch.float32, device=dev)
+        self.gen = torch.Generator(device=dev)
+        self.gen.manual_seed(est._seed() + cloud.rank())
+        self.rng = np.random.RandomState(est._seed())
+        self.iter = 0
+
+    def step(self):
+        p, spec, dev = self.est._parms, self.spec, self.dev
+        N, F = self.bd.nrows_local, self.bd.F
+        srpc = p.get("sample_rate_per_class")
+        if srpc is not None and spec.is_classification:
+            rates = torch.tensor(srpc, dtype=torch.float32, device=dev)[self.ycode.clamp(min=0)]
+            inbag = torch.rand(N, generator=self.gen, device=dev) < rates
+        else:
+            inbag = torch.rand(N, generator=self.gen, device=dev) < float(p["sample_rate"])
+        wt = (self.base_w * inbag).contiguous()
+        r = float(p.get("col_sample_rate_per_tree", 1.0))
+        if r < 1.0:
+            kk = max(1, int(math.floor(r * F + 0.5)))
+            m = np.zeros(F, dtype=bool)
+            m[self.rng.choice(F, size=kk, replace=False)] = True
+            self.gp.tree_col_mask = m
+        oob = ~inbag
+        for k in range(self.K):
+            tree, nid, leaves, tot = self.grower.grow(self.targets[k].contiguous(), wt, 0)
+            tot = tot.numpy() if isinstance(tot, torch.Tensor) else np.asarray(tot)
+            vals = np.where(tot[:, 0] > 0, tot[:, 1] / np.where(tot[:, 0] > 0, tot[:, 0], 1), 0.0)
+            for li, node in enumerate(leaves):
+                tree.value[node] = float(vals[li])
+            vt = torch.tensor(vals, dtype=torch.float32, device=dev)
+            self.oob_sum[:, k] += torch.where(oob, vt[nid.long()], torch.zeros(N, device=dev))
+            self.forest.add(tree, k)
+        self.oob_cnt += oob.to(torch.float32)
+        self.iter += 1
 
 
 class H2OExtremelyRandomizedTreesEstimator(H2ORandomForestEstimator):

@@ -144,6 +144,8 @@ class TreeGrower:
         mono = params.monotone if params.monotone is not None else np.zeros(F)
         self.mono_t = torch.tensor(list(mono) + [0] * (self.Fpad - F), dtype=torch.float64, device=self.dev)
         self.rng = np.random.RandomState(params.seed & 0x7FFFFFFF)
+        if os.environ.get("H2O3_HIST_BUDGET"):
+            params.hist_mem_budget = int(os.environ["H2O3_HIST_BUDGET"])
 
     # ------------------------------------------------------------------ hist
     def _build_hist(self, ridx, va, vb, mode, starts, counts):
@@ -231,9 +233,8 @@ class TreeGrower:
         cm_num[:, fsl] &= ~is_cat.view(1, -1)
         res = self._find_splits_native(H, cm_num, node_wyy)
         if bool(is_cat.any()):
-            cm_cat = col_mask.clone()
-            cm_cat[:, fsl] &= is_cat.view(1, -1)
-            rc = self._find_splits_torch(H, cm_cat, node_wyy, merge=False)
+            cat_local = torch.nonzero(is_cat).flatten().tolist()
+            rc = self._cat_splits_pairs(H, col_mask, cat_local, node_wyy)
             better = rc["gain"] > res["gain"]
             for k in res:
                 if res[k] is None or k == "tot":
@@ -335,18 +336,160 @@ class TreeGrower:
         return {"gain": best, "feat": fl + self.f0, "t": t, "opt": opt, "na_left": opt == 1,
                 "mask": mask.to(torch.uint8), "L": Lw, "R": T - Lw, "tot": T}
 
-    def _find_splits_torch(self, H, col_mask, node_wyy=None, merge=True):
+    def _cat_splits_pairs(self, H, col_mask, sub, node_wyy):
+        """Categorical splits scored only on the eligible (node, feature) pairs
+        (mtries / column sampling usually leave a few per node): levels sorted
+        by mean response per pair (DTree.findBestSplitPoint for categoricals),
+        prefix sums, the three NA options, best pair per node by a segment
+        arg-max (lowest feature on ties)."""
+        p = self.p
+        Fl, n, Bs, C = H.shape
+        B = Bs - 1
+        dev = H.device
+        sub_t = torch.as_tensor(sub, dtype=torch.long, device=dev)
+        gidx = sub_t + self.f0
+        cm = col_mask.to(dev)[:, gidx] & (gidx < self.bd.F).view(1, -1)
+        nz = torch.nonzero(cm)
+        ninf = torch.full((n,), NEG_INF, dtype=torch.float64, device=dev)
+        out = {"gain": ninf, "feat": torch.zeros(n, dtype=torch.long, device=dev),
+               "t": torch.zeros(n, dtype=torch.long, device=dev), "opt": torch.zeros(n, dtype=torch.long, device=dev),
+               "na_left": torch.zeros(n, dtype=torch.bool, device=dev),
+               "mask": torch.zeros((n, Bs), dtype=torch.uint8, device=dev),
+               "L": torch.zeros((n, C), dtype=torch.float64, device=dev),
+               "R": torch.zeros((n, C), dtype=torch.float64, device=dev), "tot": None}
+        if nz.shape[0] == 0:
+            return out
+        node_i, j = nz[:, 0], nz[:, 1]
+        P = node_i.numel()
+        h = H[sub_t[j], node_i].to(torch.float64)                 # [P, Bs, C]
+        bins, na = h[:, :B], h[:, B]
+        xgb = p.criterion == "xgb"
+        if xgb:
+            key = torch.where(bins[..., 1] > 0, bins[..., 0] / bins[..., 1].clamp_min(1e-300),
+                              torch.full_like(bins[..., 0], float("inf")))
+        else:
+            key = torch.where(bins[..., 0] > 0, bins[..., 1] / bins[..., 0].clamp_min(1e-300),
+                              torch.full_like(bins[..., 0], float("inf")))
+        order = torch.argsort(key, dim=1, stable=True)             # [P, B]
+        bs_ = torch.gather(bins, 1, order.unsqueeze(-1).expand(-1, -1, C))
+        cum = torch.cumsum(bs_, 1)
+        totnn = cum[:, -1]
+        L = cum[:, :-1]
+        R = totnn.unsqueeze(1) - L
+        T = totnn + na
+        naE = na.unsqueeze(1)
+
+        def score(S):
+            if xgb:
+                g, hh = S[..., 0], S[..., 1]
+                if p.reg_alpha > 0:
+                    g = torch.sign(g) * torch.clamp(g.abs() - p.reg_alpha, min=0)
+                return g * g / (hh + p.reg_lambda)
+            w, wy = S[..., 0], S[..., 1]
+            return torch.where(w > 0, wy * wy / w.clamp_min(1e-300), torch.zeros_like(w))
+
+        sT = score(T).unsqueeze(1)
+
+        def gain_of(LL, RR):
+            g = score(LL) + score(RR) - sT
+            if xgb:
+                g = 0.5 * g - p.gamma
+                ok = (LL[..., 1] >= max(p.min_rows, 1e-12)) & (RR[..., 1] >= max(p.min_rows, 1e-12))
+            else:
+                wl, wr = LL[..., 0], RR[..., 0]
+                ok = (wl >= p.min_rows) & (wr >= p.min_rows) & (wl > 0) & (wr > 0)
+                pl = (LL[..., 1] / wl.clamp_min(1e-300)).to(torch.float32)
+                pr = (RR[..., 1] / wr.clamp_min(1e-300)).to(torch.float32)
+                ok &= pl != pr
+            return torch.where(ok, g, torch.full_like(g, NEG_INF))
+
+        gA = gain_of(L, R + naE)
+        gB = gain_of(L + naE, R)
+        gC = gain_of(totnn.unsqueeze(1), naE)
+        has_na = ((na[..., 1] > 0) | (na[..., 0] != 0)) if xgb else (na[..., 0] > 0)
+        gB = torch.where(has_na.unsqueeze(1), gB, torch.full_like(gB, NEG_INF))
+        gC = torch.where(has_na.unsqueeze(1), gC, torch.full_like(gC, NEG_INF))
+        allg = torch.cat([gA, gB, gC], 1)                          # [P, 2(B-1)+1]
+        if xgb:
+            allg = torch.where(allg > 0, allg, torch.full_like(allg, NEG_INF))
+        else:
+            wyy = node_wyy.to(torch.float64)[node_i].view(-1, 1) if node_wyy is not None else \
+                torch.zeros((P, 1), dtype=torch.float64, device=dev)
+            se_before = (wyy - score(T).unsqueeze(1)).clamp_min(0)
+            allg = torch.where((allg > se_before * p.min_split_improvement) & (se_before > 0), allg,
+                               torch.full_like(allg, NEG_INF))
+        best, k = allg.max(1)
+        node_best = ninf.clone().scatter_reduce(0, node_i, best, reduce="amax", include_self=True)
+        cand = torch.where((best == node_best[node_i]) & torch.isfinite(best), torch.arange(P, device=dev),
+                           torch.full((P,), P, device=dev))
+        win = torch.full((n,), P, dtype=torch.long, device=dev).scatter_reduce(0, node_i, cand, reduce="amin",
+                                                                              include_self=True)
+        has = win < P
+        if not bool(has.any()):
+            return out
+        nodes = torch.nonzero(has).flatten()
+        wp = win[nodes]
+        nt = B - 1
+        kk = k[wp]
+        opt = torch.where(kk < nt, torch.zeros_like(kk), torch.where(kk < 2 * nt, torch.ones_like(kk),
+                                                                     torch.full_like(kk, 2)))
+        t = torch.where(opt == 0, kk, torch.where(opt == 1, kk - nt, torch.zeros_like(kk)))
+        na_left = opt == 1
+        Lw = torch.where((opt == 2).view(-1, 1), totnn[wp],
+                         L[wp, t.clamp(max=nt - 1)] + torch.where(na_left.view(-1, 1), na[wp], torch.zeros_like(na[wp])))
+        ordw = order[wp]
+        rank = torch.empty_like(ordw)
+        rank.scatter_(1, ordw, torch.arange(B, device=dev).view(1, B).expand(ordw.shape[0], B))
+        in_left = rank <= t.view(-1, 1)
+        bw = h[wp, :B, 1] if xgb else h[wp, :B, 0]
+        empty = bw <= 0
+        in_left = torch.where(empty, na_left.view(-1, 1).expand_as(in_left), in_left)
+        in_left = torch.where((opt == 2).view(-1, 1), ~empty | na_left.view(-1, 1), in_left)
+        mask = torch.cat([in_left, na_left.view(-1, 1).expand(-1, Bs - B)], 1).to(torch.uint8)
+        out["gain"] = out["gain"].index_put((nodes,), best[wp])
+        out["feat"] = out["feat"].index_put((nodes,), gidx[j[wp]])
+        out["t"] = out["t"].index_put((nodes,), t)
+        out["opt"] = out["opt"].index_put((nodes,), opt)
+        out["na_left"] = out["na_left"].index_put((nodes,), na_left)
+        out["mask"] = out["mask"].index_put((nodes,), mask)
+        out["L"] = out["L"].index_put((nodes,), Lw)
+        out["R"] = out["R"].index_put((nodes,), T[wp] - Lw)
+        return out
+
+    def _find_splits_torch(self, H, col_mask, node_wyy=None, merge=True, sub=None):
         """H: [Fl, n, Bs, C] (local feature slice).  Returns dict of per-node
         tensors on device: gain, feat, na_left, mask[n, Bs], stats L/R [n,C],
-        tot [n,C]."""
+        tot [n,C].  sub: local feature indices to score (e.g. the categorical
+        ones); large frontiers are scored in node chunks to bound memory."""
+        Fl0, n0, Bs0, C0 = H.shape
+        if sub is not None:
+            sub_t = torch.as_tensor(sub, dtype=torch.long, device=H.device)
+            gidx = sub_t + self.f0
+            H = H.index_select(0, sub_t)
+        else:
+            gidx = torch.arange(self.f0, self.f0 + Fl0, device=H.device)
+        Fs = H.shape[0]
+        # chunk the frontier: ~12 live [nc, Fs, Bs, C] float64 temporaries <= ~3 GB
+        nc = max(1, int(3e9 // max(1, 12 * Fs * Bs0 * C0 * 8)))
+        if n0 > nc:
+            parts = [self._find_splits_torch_core(H[:, i:i + nc], col_mask[i:i + nc], gidx,
+                                                  None if node_wyy is None else node_wyy[i:i + nc])
+                     for i in range(0, n0, nc)]
+            res = {k: (torch.cat([q[k] for q in parts], 0) if parts[0][k] is not None else None) for k in parts[0]}
+        else:
+            res = self._find_splits_torch_core(H, col_mask, gidx, node_wyy)
+        if self.W > 1 and merge:
+            res = self._merge_candidates(res, n0, Bs0, C0)
+        return res
+
+    def _find_splits_torch_core(self, H, col_mask, gidx, node_wyy=None):
         p = self.p
         Fl, n, Bs, C = H.shape
         B = Bs - 1
         h = H.permute(1, 0, 2, 3).to(torch.float64)       # [n, Fl, Bs, C]
         bins = h[:, :, :B]
         na = h[:, :, B]                                    # [n, Fl, C]
-        fsl = slice(self.f0, self.f0 + Fl)
-        is_cat = self.is_cat_t[fsl]
+        is_cat = self.is_cat_t[gidx]
         order = None
         uplift = p.criterion.startswith("uplift")
         if bool(is_cat.any()):
@@ -424,7 +567,7 @@ class TreeGrower:
                 predl = LL[..., 1] / wl.clamp_min(1e-300)
                 predr = RR[..., 1] / wr.clamp_min(1e-300)
                 ok &= predl.to(torch.float32) != predr.to(torch.float32)
-            mono = self.mono_t[fsl].view(1, Fl, 1)
+            mono = self.mono_t[gidx].view(1, Fl, 1)
             ok &= ~((mono > 0) & (predl > predr)) & ~((mono < 0) & (predl < predr))
             return torch.where(ok, g, torch.full_like(g, NEG_INF))
 
@@ -437,10 +580,7 @@ class TreeGrower:
         gC = gain_of(LC, RC)
         gC = torch.where(has_na.unsqueeze(2), gC, torch.full_like(gC, NEG_INF))
         # feature eligibility (column sampling, padding, interaction constraints)
-        cm = col_mask[:, fsl].to(h.device)
-        if self.f0 + Fl > self.bd.F:
-            cm = cm.clone()
-            cm[:, max(0, self.bd.F - self.f0):] = False
+        cm = col_mask.to(h.device)[:, gidx] & (gidx < self.bd.F).view(1, -1)
         allg = torch.cat([gA, gB, gC], 2)                  # [n, Fl, 2(B-1)+1]
         allg = torch.where(cm.unsqueeze(2), allg, torch.full_like(allg, NEG_INF))
         # min split improvement (relative to the node's squared error)
@@ -490,10 +630,8 @@ class TreeGrower:
             mask = mask_num
         mask = mask.clone()
         mask[:, Bs - 1] = na_left
-        res = {"gain": best, "feat": fl + self.f0, "t": t, "opt": opt, "na_left": na_left,
+        res = {"gain": best, "feat": gidx[fl], "t": t, "opt": opt, "na_left": na_left,
                "mask": mask.to(torch.uint8), "L": Lw, "R": Rw, "tot": T[:, 0] if Fl > 0 else None}
-        if self.W > 1 and merge:
-            res = self._merge_candidates(res, n, Bs, C)
         return res
 
     def _merge_candidates(self, res, n, Bs, C):
@@ -564,7 +702,16 @@ class TreeGrower:
             slot_of = {nd[0]: i for i, nd in enumerate(frontier)}
             depth = frontier[0][3]
             can_split = depth < p.max_depth
-            if not can_split and level > 0:
+            C_ = tree_ops.channels(mode)
+            level_bytes = self.Fpad * n_front * bd.Bs * C_ * 8
+            prev_bytes = 0 if H_prev is None else H_prev.numel() * 8
+            chunked = can_split and (level_bytes + prev_bytes) > p.hist_mem_budget and n_front > 1
+            if chunked:
+                # frontier too wide for one level of histograms (deep DRF trees, wide
+                # high-cardinality data): histograms of node batches straight from the
+                # rows, split records concatenated, no parent level kept (no subtraction)
+                H, H_prev, wyy_level = None, None, None
+            elif not can_split and level > 0:
                 # last level: no histograms needed, leaf totals come from the parent split stats
                 H = None
             elif level == 0 or H_prev is None:
@@ -612,7 +759,19 @@ class TreeGrower:
                 # fused into the histogram kernel; derived siblings by subtraction
                 node_wyy = wyy_level if mode == 0 else None
                 with phase("tree.split"):
-                    sp = self._find_splits(H, cm, node_wyy, want_pk=async_part)
+                    if chunked:
+                        per = max(1, int(p.hist_mem_budget // max(1, self.Fpad * bd.Bs * C_ * 8)))
+                        parts = []
+                        for a in range(0, n_front, per):
+                            fr_ = frontier[a:a + per]
+                            Hc = self._build_hist(ridx, va, vb, mode, [f[1] for f in fr_], [f[2] for f in fr_])
+                            wyy_c = self._last_wyy if mode == 0 else None
+                            parts.append(self._find_splits(Hc, cm[a:a + per], wyy_c, want_pk=False))
+                            del Hc
+                        sp = {k: (torch.cat([q[k] for q in parts], 0) if parts[0].get(k) is not None else None)
+                              for k in parts[0]}
+                    else:
+                        sp = self._find_splits(H, cm, node_wyy, want_pk=async_part)
                 nn_ = n_front
                 if async_part and "pk" in sp:
                     pkd = sp["pk"]
@@ -766,7 +925,9 @@ class TreeGrower:
                 if len(f) > 4:
                     self._pending_leaf_segs.append((f[0], f[1], f[2]))
             # parent hists for the next level (only split nodes)
-            if self.dev.type == "cuda":
+            if H is None:
+                H_prev, wyy_prev = None, None   # chunked level: next level builds from rows
+            elif self.dev.type == "cuda":
                 # the sibling kernel indexes the parent level directly: keep the
                 # whole level and remap the pairs' parent slots
                 H_prev = H

@@ -260,3 +260,28 @@ def test_gbm_position_leaf_path_matches_nid_path(monkeypatch):
         m.train(y="y", training_frame=fr)
         preds.append(m.predict(fr).as_data_frame()["a"].values)
     np.testing.assert_allclose(preds[0], preds[1], atol=2e-5)
+
+
+@pytest.mark.parametrize("crit", ["se", "xgb"])
+def test_cat_pair_splits_match_dense_torch(crit):
+    """Pair-based categorical scoring == dense torch scoring on the eligible features."""
+    _need_gpu()
+    from h2o3_amd.models.tree.engine import GrowParams, TreeGrower
+    bd, _ = _binned(n=20000, F=13, cats=True)
+    gr = TreeGrower(bd, GrowParams(criterion=crit, min_rows=5))
+    g = torch.Generator(device="cuda").manual_seed(11)
+    n, Bs = 9, bd.Bs
+    H = torch.rand((gr.Fpad, n, Bs, 2), generator=g, device="cuda", dtype=torch.float64) * 50
+    if crit == "se":
+        H[..., 1] = (torch.rand(H[..., 1].shape, generator=g, device="cuda", dtype=torch.float64) - 0.3) * H[..., 0]
+    cm = torch.rand((n, gr.Fpad), generator=torch.Generator().manual_seed(2)) < 0.6
+    wyy = torch.full((n,), 1e6, dtype=torch.float64, device="cuda")
+    cat_local = [j for j in range(gr.Fpad) if j < bd.F and bd.is_cat[j]]
+    a = gr._cat_splits_pairs(H, cm, cat_local, wyy)
+    b = gr._find_splits_torch(H, cm, wyy, merge=False, sub=cat_local)
+    fin = torch.isfinite(b["gain"])
+    assert torch.equal(torch.isfinite(a["gain"]), fin)
+    torch.testing.assert_close(a["gain"][fin], b["gain"][fin])
+    assert torch.equal(a["feat"][fin], b["feat"][fin])
+    assert torch.equal(a["mask"][fin], b["mask"][fin])
+    torch.testing.assert_close(a["L"][fin], b["L"][fin])

@@ -62,3 +62,26 @@ def test_isolation_forests():
     e.train(training_frame=fr)
     a = e.predict(fr).as_data_frame()["anomaly_score"].values
     assert a[:20].mean() > a[20:].mean()
+
+
+def test_chunked_levels_match_unchunked(monkeypatch):
+    """Frontier wider than the histogram memory budget: node-batched levels
+    without subtraction grow the same tree."""
+    import numpy as np
+    import pandas as pd
+    import h2o3_amd as h2o
+    from h2o3_amd.estimators import H2ORandomForestEstimator
+    h2o.init(verbose=False)
+    rng = np.random.RandomState(0)
+    n = 3000
+    df = pd.DataFrame({"a": rng.randn(n), "b": rng.randn(n), "c": rng.choice([f"k{i}" for i in range(30)], n)})
+    df["y"] = np.where(df.a + (df.c.str[1:].astype(int) % 3 == 0) + 0.3 * rng.randn(n) > 0.5, "p", "q")
+    fr = h2o.H2OFrame(df)
+    preds = []
+    for budget in (None, "20000"):
+        if budget:
+            monkeypatch.setenv("H2O3_HIST_BUDGET", budget)
+        m = H2ORandomForestEstimator(ntrees=3, max_depth=8, seed=5)
+        m.train(y="y", training_frame=fr)
+        preds.append(m.predict(fr).as_data_frame()["p"].values)
+    np.testing.assert_allclose(preds[0], preds[1], atol=1e-6)
