@@ -216,6 +216,15 @@ class TreeGrower:
         """Dispatch: fused HIP kernel for numeric features on GPU (categorical
         features, which need a per-node sort of bins, go through the torch path)."""
         if self.dev.type != "cuda" or self.p.criterion.startswith("uplift"):
+            Fl_ = H.shape[0]
+            cmf = col_mask[:, self.f0:self.f0 + Fl_]
+            if not self.p.criterion.startswith("uplift") and cmf.numel() and float(cmf.float().mean()) < 0.5:
+                # few eligible features per node (DRF mtries): score only those pairs
+                res = self._cat_splits_pairs(H, col_mask, list(range(Fl_)), node_wyy)
+                res["tot"] = H[0].to(torch.float64).sum(1) if Fl_ > 0 else None
+                if self.W > 1:
+                    res = self._merge_candidates(res, H.shape[1], H.shape[2], H.shape[3])
+                return res
             return self._find_splits_torch(H, col_mask, node_wyy)
         Fl = H.shape[0]
         fsl = slice(self.f0, self.f0 + Fl)
@@ -364,13 +373,16 @@ class TreeGrower:
         h = H[sub_t[j], node_i].to(torch.float64)                 # [P, Bs, C]
         bins, na = h[:, :B], h[:, B]
         xgb = p.criterion == "xgb"
+        pcat = self.is_cat_t[gidx[j]]                              # numeric pairs keep bin order
         if xgb:
             key = torch.where(bins[..., 1] > 0, bins[..., 0] / bins[..., 1].clamp_min(1e-300),
                               torch.full_like(bins[..., 0], float("inf")))
         else:
             key = torch.where(bins[..., 0] > 0, bins[..., 1] / bins[..., 0].clamp_min(1e-300),
                               torch.full_like(bins[..., 0], float("inf")))
+        key = torch.where(pcat.view(-1, 1), key, torch.arange(B, device=dev, dtype=key.dtype).view(1, B))
         order = torch.argsort(key, dim=1, stable=True)             # [P, B]
+        mono = self.mono_t[gidx[j]].view(-1, 1)
         bs_ = torch.gather(bins, 1, order.unsqueeze(-1).expand(-1, -1, C))
         cum = torch.cumsum(bs_, 1)
         totnn = cum[:, -1]
@@ -398,9 +410,13 @@ class TreeGrower:
             else:
                 wl, wr = LL[..., 0], RR[..., 0]
                 ok = (wl >= p.min_rows) & (wr >= p.min_rows) & (wl > 0) & (wr > 0)
-                pl = (LL[..., 1] / wl.clamp_min(1e-300)).to(torch.float32)
-                pr = (RR[..., 1] / wr.clamp_min(1e-300)).to(torch.float32)
-                ok &= pl != pr
+                pl = (LL[..., 1] / wl.clamp_min(1e-300))
+                pr = (RR[..., 1] / wr.clamp_min(1e-300))
+                ok &= pl.to(torch.float32) != pr.to(torch.float32)
+            if xgb:
+                pl = -LL[..., 0] / (LL[..., 1] + p.reg_lambda)
+                pr = -RR[..., 0] / (RR[..., 1] + p.reg_lambda)
+            ok &= ~((mono > 0) & (pl > pr)) & ~((mono < 0) & (pl < pr))
             return torch.where(ok, g, torch.full_like(g, NEG_INF))
 
         gA = gain_of(L, R + naE)
@@ -442,7 +458,7 @@ class TreeGrower:
         rank.scatter_(1, ordw, torch.arange(B, device=dev).view(1, B).expand(ordw.shape[0], B))
         in_left = rank <= t.view(-1, 1)
         bw = h[wp, :B, 1] if xgb else h[wp, :B, 0]
-        empty = bw <= 0
+        empty = (bw <= 0) & pcat[wp].view(-1, 1)     # empty categorical levels follow the NAs
         in_left = torch.where(empty, na_left.view(-1, 1).expand_as(in_left), in_left)
         in_left = torch.where((opt == 2).view(-1, 1), ~empty | na_left.view(-1, 1), in_left)
         mask = torch.cat([in_left, na_left.view(-1, 1).expand(-1, Bs - B)], 1).to(torch.uint8)

@@ -1,4 +1,5 @@
 import numpy as np
+import pytest
 import pandas as pd
 
 import h2o3_amd
@@ -85,3 +86,40 @@ def test_chunked_levels_match_unchunked(monkeypatch):
         m.train(y="y", training_frame=fr)
         preds.append(m.predict(fr).as_data_frame()["p"].values)
     np.testing.assert_allclose(preds[0], preds[1], atol=1e-6)
+
+
+@pytest.mark.parametrize("crit", ["se", "xgb"])
+def test_pair_splits_match_dense(crit):
+    """Pair scoring (numeric + categorical, monotone constraints) equals the dense torch split search."""
+    import numpy as np
+    import torch
+    import h2o3_amd as h2o
+    from h2o3_amd.models.tree.binning import bin_frame_tensors
+    from h2o3_amd.models.tree.engine import GrowParams, TreeGrower
+    h2o.init(verbose=False)
+    g = torch.Generator().manual_seed(0)
+    F, n = 9, 11
+    feats, is_cat, cards = [], [], []
+    for j in range(F):
+        if j % 3 == 2:
+            feats.append(torch.randint(-1, 6, (500,), generator=g).to(torch.int32)); is_cat.append(True); cards.append(6)
+        else:
+            feats.append(torch.randn(500, generator=g)); is_cat.append(False); cards.append(0)
+    bd = bin_frame_tensors(feats, is_cat, cards, [f"f{j}" for j in range(F)], hist_type="QuantilesGlobal", nbins=30)
+    mono = np.zeros(F)
+    mono[0], mono[1] = 1, -1
+    gr = TreeGrower(bd, GrowParams(criterion=crit, min_rows=3, monotone=mono))
+    H = torch.rand((gr.Fpad, n, bd.Bs, 2), generator=g, dtype=torch.float64) * 40
+    if crit == "se":
+        H[..., 1] = (torch.rand(H[..., 1].shape, generator=g, dtype=torch.float64) - 0.4) * H[..., 0]
+    else:
+        H[..., 0] -= 20
+    cm = torch.rand((n, gr.Fpad), generator=g) < 0.4
+    wyy = torch.full((n,), 1e6, dtype=torch.float64)
+    a = gr._cat_splits_pairs(H, cm, list(range(gr.Fpad)), wyy)
+    b = gr._find_splits_torch(H, cm, wyy, merge=False)
+    fin = torch.isfinite(b["gain"])
+    assert torch.equal(torch.isfinite(a["gain"]), fin)
+    torch.testing.assert_close(a["gain"][fin], b["gain"][fin])
+    assert torch.equal(a["feat"][fin], b["feat"][fin])
+    assert torch.equal(a["mask"][fin], b["mask"][fin])
