@@ -217,6 +217,141 @@ def create_app() -> FastAPI:
     def timeline():
         return {"events": api.timeline()}
 
+    @app.post("/3/ParseSetup")
+    def parse_setup(body: dict = Body(...)):
+        """ParseSetupHandler: guessed separator / header for the source files."""
+        src = body.get("source_frames") or body.get("paths") or []
+        src = [s["name"] if isinstance(s, dict) else s for s in (src if isinstance(src, list) else [src])]
+        if not src:
+            raise HTTPException(400, "source_frames required")
+        from ..core import parse as P
+        st = P.parse_setup(src[0] if len(src) == 1 else src)
+        return _jsonable({"source_frames": [{"name": s} for s in src], "separator": ord(st["separator"]),
+                          "check_header": st.get("header", 0), "destination_frame": body.get("destination_frame")})
+
+    @app.post("/3/Parse")
+    def parse(body: dict = Body(...)):
+        src = [s["name"] if isinstance(s, dict) else s for s in body.get("source_frames", [])]
+        sep = body.get("separator")
+        fr = api.import_file(src if len(src) > 1 else src[0], destination_frame=body.get("destination_frame"),
+                             sep=chr(sep) if isinstance(sep, int) else sep, header=body.get("check_header", 0),
+                             col_names=body.get("column_names"), col_types=body.get("column_types"))
+        fid = body.get("destination_frame") or fr.frame_id
+        dkv.put(fid, fr)
+        return {"job": {"key": {"name": f"parse_{fid}"}, "status": "DONE", "progress": 1.0,
+                        "dest": {"name": fid}}, "destination_frame": {"name": fid}}
+
+    @app.get("/3/DownloadDataset")
+    def download_dataset(frame_id: str):
+        from fastapi.responses import PlainTextResponse
+        fr = dkv.get(frame_id)
+        if not isinstance(fr, H2OFrame):
+            raise HTTPException(404, f"frame {frame_id} not found")
+        return PlainTextResponse(fr.as_data_frame().to_csv(index=False), media_type="text/csv")
+
+    @app.get("/3/Models/{mid}/mojo")
+    def model_mojo(mid: str):
+        from fastapi.responses import Response
+        from ..mojo.writer import build_mojo
+        m = dkv.get(mid)
+        if m is None:
+            raise HTTPException(404, f"model {mid} not found")
+        try:
+            data = build_mojo(m)
+        except NotImplementedError as e:
+            raise HTTPException(400, str(e))
+        return Response(content=data, media_type="application/zip",
+                        headers={"Content-Disposition": f'attachment; filename="{mid}.zip"'})
+
+    @app.get("/3/Models.java/{mid}")
+    def model_pojo(mid: str):
+        from fastapi.responses import PlainTextResponse
+        from ..mojo.pojo import to_java
+        m = dkv.get(mid)
+        if m is None:
+            raise HTTPException(404, f"model {mid} not found")
+        try:
+            return PlainTextResponse(to_java(m), media_type="text/plain")
+        except NotImplementedError as e:
+            raise HTTPException(400, str(e))
+
+    @app.post("/3/ModelMetrics/models/{mid}/frames/{fid}")
+    def model_metrics(mid: str, fid: str):
+        m, fr = dkv.get(mid), dkv.get(fid)
+        if m is None or not isinstance(fr, H2OFrame):
+            raise HTTPException(404, "model or frame not found")
+        mm_ = m.model_performance(fr)
+        return {"model_metrics": [{k: _jsonable(v) for k, v in mm_._m.items() if isinstance(v, (int, float, str))}]}
+
+    @app.post("/99/Grid/{algo}")
+    def grid(algo: str, body: dict = Body(...)):
+        """GridSearchHandler: hyper_parameters + search_criteria over one algo."""
+        from ..grid import H2OGridSearch
+        cls = _algo_cls(algo)
+        p = dict(body)
+        tf = dkv.get(p.pop("training_frame", None))
+        if not isinstance(tf, H2OFrame):
+            raise HTTPException(400, "training_frame not found")
+        vf = p.pop("validation_frame", None)
+        hyper = p.pop("hyper_parameters", {})
+        crit = p.pop("search_criteria", None)
+        gid = p.pop("grid_id", None)
+        y = p.pop("response_column", None)
+        g = H2OGridSearch(cls(**p), hyper, grid_id=gid, search_criteria=crit)
+        g.train(y=y, training_frame=tf, validation_frame=dkv.get(vf) if vf else None)
+        return {"job": {"key": {"name": f"grid_{g.grid_id}"}, "status": "DONE", "progress": 1.0,
+                        "dest": {"name": g.grid_id}}}
+
+    @app.get("/99/Grids/{gid}")
+    def grid_get(gid: str):
+        g = dkv.get(gid)
+        if g is None or not hasattr(g, "model_ids"):
+            raise HTTPException(404, f"grid {gid} not found")
+        tab = g.get_grid().sorted_metric_table()
+        return _jsonable({"grid_id": {"name": gid}, "model_ids": [{"name": m} for m in g.model_ids],
+                          "failure_details": [e for _, e in g.failed_params],
+                          "summary_table": tab.to_dict(orient="list")})
+
+    @app.post("/99/AutoMLBuilder")
+    def automl(body: dict = Body(...)):
+        """AutoMLBuilderHandler: build_control / input_spec / build_models."""
+        from ..automl import H2OAutoML
+        bc, ispec, bm = body.get("build_control", {}), body.get("input_spec", {}), body.get("build_models", {})
+        tf = dkv.get(ispec.get("training_frame"))
+        if not isinstance(tf, H2OFrame):
+            raise HTTPException(400, "input_spec.training_frame not found")
+        sc = bc.get("stopping_criteria", {})
+        aml = H2OAutoML(project_name=bc.get("project_name"), nfolds=bc.get("nfolds", -1),
+                        max_models=sc.get("max_models"), max_runtime_secs=sc.get("max_runtime_secs"),
+                        seed=sc.get("seed"), exclude_algos=bm.get("exclude_algos"),
+                        include_algos=bm.get("include_algos"), sort_metric=ispec.get("sort_metric", "AUTO"))
+        aml.train(y=ispec.get("response_column"), training_frame=tf,
+                  validation_frame=dkv.get(ispec["validation_frame"]) if ispec.get("validation_frame") else None,
+                  leaderboard_frame=dkv.get(ispec["leaderboard_frame"]) if ispec.get("leaderboard_frame") else None)
+        return {"job": {"key": {"name": f"automl_{aml.project_name}"}, "status": "DONE", "progress": 1.0,
+                        "dest": {"name": aml.project_name}}}
+
+    @app.get("/99/Leaderboards/{project}")
+    def leaderboard(project: str):
+        aml = dkv.get(project)
+        if aml is None or not hasattr(aml, "leaderboard"):
+            raise HTTPException(404, f"AutoML project {project} not found")
+        lb = aml.leaderboard.as_data_frame()
+        return _jsonable({"project_name": project, "models": [{"name": m} for m in lb["model_id"]],
+                          "table": lb.to_dict(orient="list")})
+
+    @app.get("/3/About")
+    def about():
+        i = cloud.info()
+        return {"entries": [{"name": "Build project version", "value": "h2o3_amd-0.1.0"},
+                            {"name": "Device", "value": str(i.get("device"))},
+                            {"name": "Cloud size", "value": str(i.get("world"))}]}
+
+    @app.get("/3/Capabilities")
+    def capabilities():
+        return {"capabilities": [{"name": n} for n in ("Algos", "AutoML", "Grid", "MOJO", "POJO", "Rapids",
+                                                      "HIP-gfx950", "RCCL")]}
+
     @app.post("/99/Rapids")
     def rapids_exec(body: dict = Body(...)):
         """Rapids expression evaluation (water/api/RapidsHandler.java): frame

@@ -30,3 +30,37 @@ def test_rest_roundtrip():
     assert c.delete("/3/DKV/train.hex").status_code == 200
     assert c.get("/3/Frames/train.hex").status_code == 404
     assert len(c.get("/3/Metadata/endpoints").json()["routes"]) > 10
+
+
+def test_rest_parse_grid_automl_mojo(tmp_path):
+    h2o.init()
+    c = TestClient(create_app())
+    rng = np.random.default_rng(1)
+    df = pd.DataFrame({"a": rng.normal(size=300), "b": rng.normal(size=300)})
+    df["y"] = np.where(df.a - df.b > 0, "p", "n")
+    p = tmp_path / "d.csv"
+    df.to_csv(p, index=False)
+    st = c.post("/3/ParseSetup", json={"source_frames": [str(p)]}).json()
+    assert st["separator"] == ord(",")
+    r = c.post("/3/Parse", json={"source_frames": [str(p)], "destination_frame": "d.hex", "separator": 44}).json()
+    assert r["destination_frame"]["name"] == "d.hex"
+    assert "a,b,y" in c.get("/3/DownloadDataset", params={"frame_id": "d.hex"}).text
+    g = c.post("/99/Grid/gbm", json={"training_frame": "d.hex", "response_column": "y", "ntrees": 3,
+                                      "hyper_parameters": {"max_depth": [2, 3]}, "grid_id": "g_rest"}).json()
+    assert g["job"]["status"] == "DONE"
+    gj = c.get("/99/Grids/g_rest").json()
+    assert len(gj["model_ids"]) == 2
+    mid = gj["model_ids"][0]["name"]
+    z = c.get(f"/3/Models/{mid}/mojo")
+    assert z.status_code == 200 and z.content[:2] == b"PK"
+    assert "extends GenModel" in c.get(f"/3/Models.java/{mid}").text
+    mm = c.post(f"/3/ModelMetrics/models/{mid}/frames/d.hex").json()
+    assert mm["model_metrics"][0]["AUC"] > 0.8
+    a = c.post("/99/AutoMLBuilder", json={"build_control": {"project_name": "aml_rest", "nfolds": 2,
+                                                            "stopping_criteria": {"max_models": 2, "seed": 1}},
+                                          "input_spec": {"training_frame": "d.hex", "response_column": "y"},
+                                          "build_models": {"include_algos": ["GLM", "GBM"]}}).json()
+    assert a["job"]["dest"]["name"] == "aml_rest"
+    lb = c.get("/99/Leaderboards/aml_rest").json()
+    assert len(lb["models"]) >= 2
+    assert c.get("/3/About").status_code == 200
