@@ -148,7 +148,14 @@ __global__ __launch_bounds__(512) void hist_build_kernel(
 // count and (low - count * Bq) / s1.  Halves the LDS atomics of the
 // unweighted GBM / sampled DRF histograms; the response is quantised at
 // 1/s1 = chunk * 2 * vmax / 2^40 (f32-level resolution, exact summation).
-template <int MODE, bool HAS_VB, bool POSV, bool PACK, int FG = 16>
+// BINMAJOR (PACK only, FG 16/32): the LDS histogram is laid out [bin][feature]
+// instead of [feature][bin], and the rows sharing a 16-lane LDS group walk
+// their 4 codes in rotated order, so the 16 lanes of every group update 16
+// DIFFERENT features of whatever bins they hit: with 64-bit entries the bank
+// pair is 2*(bin*FG + f) mod 64 = 2f (+32 for odd bins at FG=16), distinct per
+// lane -> conflict-free LDS atomics for random bins (the [feature][bin] layout
+// conflicts at random).
+template <int MODE, bool HAS_VB, bool POSV, bool PACK, int FG = 16, bool BINMAJOR = false>
 __global__ __launch_bounds__(512) void hist_quad_kernel(
     const uint8_t* __restrict__ codes, int Fp, const int* __restrict__ ridx,
     const float* __restrict__ va, const float* __restrict__ vb,
@@ -181,11 +188,16 @@ __global__ __launch_bounds__(512) void hist_quad_kernel(
   constexpr int U = 4;
   const uint8_t* cbase = codes + fg0 + 4 * q;
   unsigned long long* hb[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) hb[k] = ldsq + (4 * q + k) * stride_f;
   bool fk[4];
+  int kk[4];    // code byte handled at step k (rotated per row inside a 16-lane group)
+  constexpr int RPG = 16 / LPR > 0 ? 16 / LPR : 1;     // rows per 16-lane LDS group
+  const int rot = BINMAJOR ? (rs % RPG) * (4 / RPG) : 0;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) fk[k] = 4 * q + k < nf;
+  for (int k = 0; k < 4; ++k) {
+    kk[k] = (k + rot) & 3;
+    hb[k] = BINMAJOR ? ldsq + (4 * q + kk[k]) : ldsq + (4 * q + k) * stride_f;
+    fk[k] = 4 * q + kk[k] < nf;
+  }
   for (int p0 = wk.y + wv * RPW + rs; p0 < pend; p0 += U * step) {
     int rr[U];
     unsigned int cw[U];
@@ -219,7 +231,8 @@ __global__ __launch_bounds__(512) void hist_quad_kernel(
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           if (!fk[k]) continue;
-          __hip_atomic_fetch_add(hb[k] + ((cw[u] >> (8 * k)) & 0xffu), a, __ATOMIC_RELAXED,
+          const unsigned int code = (cw[u] >> (8 * kk[k])) & 0xffu;
+          __hip_atomic_fetch_add(hb[k] + (BINMAJOR ? code * FG : code), a, __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         continue;
@@ -229,7 +242,7 @@ __global__ __launch_bounds__(512) void hist_quad_kernel(
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         if (!fk[k]) continue;
-        unsigned long long* h = hb[k] + ((cw[u] >> (8 * k)) & 0xffu) * CL;
+        unsigned long long* h = hb[k] + ((cw[u] >> (8 * kk[k])) & 0xffu) * CL;
         __hip_atomic_fetch_add(h, a0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (C > 1) __hip_atomic_fetch_add(h + 1, a1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
@@ -245,9 +258,10 @@ __global__ __launch_bounds__(512) void hist_quad_kernel(
   if (PACK) {
     const int tot = nf * Bs;
     for (int i = threadIdx.x; i < tot; i += blockDim.x) {
-      const int j = i / Bs;
-      const int b = i - j * Bs;
-      const unsigned long long v = ldsq[j * stride_f + b];
+      // bin-major: consecutive threads read consecutive features of a bin (no LDS conflicts)
+      const int j = BINMAJOR ? i % nf : i / Bs;
+      const int b = BINMAJOR ? i / nf : i - j * Bs;
+      const unsigned long long v = BINMAJOR ? ldsq[b * FG + j] : ldsq[j * stride_f + b];
       if (v != 0) {
         const long long cnt = (long long)(v >> 40);
         const long long low = (long long)(v & ((1ull << 40) - 1));
@@ -270,11 +284,48 @@ __global__ __launch_bounds__(512) void hist_quad_kernel(
   }
 }
 
+template <bool V, bool PV, int G, bool BM>
+static void launch_pack1(dim3 grid, int threads, size_t lds, hipStream_t s, const uint8_t* cc, int Fp, const int* ridx,
+                         const float* va, const float* vb, const int4* wk, int n_work, int n_fg, int F, int Bs,
+                         float s0, float s1, double* hist, int n_slots, double* wyy, long long bq) {
+  hipLaunchKernelGGL((hist_quad_kernel<0, V, PV, true, G, BM>), grid, dim3(threads), lds, s, cc, Fp, ridx, va, vb, wk,
+                     n_work, n_fg, F, Bs, s0, s1, hist, n_slots, wyy, bq);
+}
+
+template <bool V, bool PV>
+static void launch_pack(int fg, int binmajor, dim3 grid, int threads, size_t lds, hipStream_t s, const uint8_t* cc,
+                        int Fp, const int* ridx, const float* va, const float* vb, const int4* wk, int n_work,
+                        int n_fg, int F, int Bs, float s0, float s1, double* hist, int n_slots, double* wyy,
+                        long long bq) {
+  if (fg == 64)
+    launch_pack1<V, PV, 64, false>(grid, threads, lds, s, cc, Fp, ridx, va, vb, wk, n_work, n_fg, F, Bs, s0, s1, hist, n_slots, wyy, bq);
+  else if (fg == 32 && binmajor)
+    launch_pack1<V, PV, 32, true>(grid, threads, lds, s, cc, Fp, ridx, va, vb, wk, n_work, n_fg, F, Bs, s0, s1, hist, n_slots, wyy, bq);
+  else if (fg == 32)
+    launch_pack1<V, PV, 32, false>(grid, threads, lds, s, cc, Fp, ridx, va, vb, wk, n_work, n_fg, F, Bs, s0, s1, hist, n_slots, wyy, bq);
+  else if (binmajor)
+    launch_pack1<V, PV, 16, true>(grid, threads, lds, s, cc, Fp, ridx, va, vb, wk, n_work, n_fg, F, Bs, s0, s1, hist, n_slots, wyy, bq);
+  else
+    launch_pack1<V, PV, 16, false>(grid, threads, lds, s, cc, Fp, ridx, va, vb, wk, n_work, n_fg, F, Bs, s0, s1, hist, n_slots, wyy, bq);
+}
+
 // pack_bq >= 0 selects the packed single-atomic path (MODE 0, 0/1 weights).
+extern "C" int h2o_hist_quad2(const void* codes, int Fp, const int* ridx, const float* va, const float* vb,
+                              const int* work, int n_work, int F, int Bs, float s0, float s1, double* hist,
+                              int n_slots, int mode, int threads, double* wyy, int posv, long long pack_bq,
+                              int fg, int binmajor, hipStream_t s);
 extern "C" int h2o_hist_quad(const void* codes, int Fp, const int* ridx, const float* va, const float* vb,
                              const int* work, int n_work, int F, int Bs, float s0, float s1, double* hist,
                              int n_slots, int mode, int threads, double* wyy, int posv, long long pack_bq,
                              int fg, hipStream_t s) {
+  return h2o_hist_quad2(codes, Fp, ridx, va, vb, work, n_work, F, Bs, s0, s1, hist, n_slots, mode, threads, wyy,
+                        posv, pack_bq, fg, 0, s);
+}
+
+extern "C" int h2o_hist_quad2(const void* codes, int Fp, const int* ridx, const float* va, const float* vb,
+                              const int* work, int n_work, int F, int Bs, float s0, float s1, double* hist,
+                              int n_slots, int mode, int threads, double* wyy, int posv, long long pack_bq,
+                              int fg, int binmajor, hipStream_t s) {
   if (n_work <= 0) return 0;
   if (Fp % 16 != 0 || Bs > 256) return -1;
   const bool pack = pack_bq >= 0 && mode == 0;
@@ -291,14 +342,10 @@ extern "C" int h2o_hist_quad(const void* codes, int Fp, const int* ridx, const f
                                                  wyy, pack_bq)
 #define H2O_LQ(M, V) if (posv) H2O_LQ2(M, V, true, false); else H2O_LQ2(M, V, false, false)
   if (pack) {
-#define H2O_LQF(V, PV, G) hipLaunchKernelGGL((hist_quad_kernel<0, V, PV, true, G>), grid, dim3(threads), lds, s, cc, \
-                                             Fp, ridx, va, vb, wk, n_work, n_fg, F, Bs, s0, s1, hist, n_slots, \
-                                             wyy, pack_bq)
-#define H2O_LQG(V, PV) if (fg == 64) H2O_LQF(V, PV, 64); else if (fg == 32) H2O_LQF(V, PV, 32); else H2O_LQF(V, PV, 16)
-    if (vb) { if (posv) H2O_LQG(true, true); else H2O_LQG(true, false); }
-    else { if (posv) H2O_LQG(false, true); else H2O_LQG(false, false); }
-#undef H2O_LQG
-#undef H2O_LQF
+    if (vb) { if (posv) launch_pack<true, true>(fg, binmajor, grid, threads, lds, s, cc, Fp, ridx, va, vb, wk, n_work, n_fg, F, Bs, s0, s1, hist, n_slots, wyy, pack_bq);
+              else launch_pack<true, false>(fg, binmajor, grid, threads, lds, s, cc, Fp, ridx, va, vb, wk, n_work, n_fg, F, Bs, s0, s1, hist, n_slots, wyy, pack_bq); }
+    else { if (posv) launch_pack<false, true>(fg, binmajor, grid, threads, lds, s, cc, Fp, ridx, va, vb, wk, n_work, n_fg, F, Bs, s0, s1, hist, n_slots, wyy, pack_bq);
+           else launch_pack<false, false>(fg, binmajor, grid, threads, lds, s, cc, Fp, ridx, va, vb, wk, n_work, n_fg, F, Bs, s0, s1, hist, n_slots, wyy, pack_bq); }
     return (int)hipGetLastError();
   }
   switch (mode) {

@@ -285,3 +285,24 @@ def test_cat_pair_splits_match_dense_torch(crit):
     assert torch.equal(a["feat"][fin], b["feat"][fin])
     assert torch.equal(a["mask"][fin], b["mask"][fin])
     torch.testing.assert_close(a["L"][fin], b["L"][fin])
+
+
+@pytest.mark.parametrize("fg", ["16", "32"])
+@pytest.mark.parametrize("binmajor", ["0", "1"])
+def test_packed_hist_binmajor_matches_reference(fg, binmajor, monkeypatch):
+    """Packed single-atomic histogram, [bin][feature] conflict-free LDS layout vs
+    [feature][bin] and the torch reference."""
+    _need_gpu()
+    monkeypatch.setenv("H2O3_HIST_FG", fg)
+    monkeypatch.setenv("H2O3_HIST_BINMAJOR", binmajor)
+    from h2o3_amd.ops import tree_ops
+    bd, _ = _binned(n=40000, F=37, nbins=255, cats=False)
+    n = bd.nrows_local
+    g = torch.Generator(device="cuda").manual_seed(4)
+    ridx = torch.randperm(n, generator=g, device="cuda").to(torch.int32)
+    va = torch.randn(n, generator=g, device="cuda")
+    vb = (torch.rand(n, generator=g, device="cuda") < 0.7).to(torch.float32)
+    starts, counts = [0, 11000, 30000], [11000, 19000, 10000]
+    h_gpu = tree_ops.hist_build(bd, ridx, va, vb, 0, starts, counts, 3, use_native=True, unit_w=True)
+    h_ref = tree_ops.hist_build(bd, ridx, va, vb, 0, starts, counts, 3, use_native=False)
+    torch.testing.assert_close(h_gpu, h_ref, rtol=1e-4, atol=1e-3)
