@@ -485,6 +485,11 @@ class GLMDriver:
                 W = self.w
                 z = self.y - off
             Wf = W.to(torch.float32)
+        if self.X.device.type == "cuda" and self.Pp > 512 and bool((W >= 0).all()):
+            with phase("glm.gram"):
+                G, xw, xz, sw, swz = linalg_ops.weighted_gram_aug(self.X, W, z, self.P)
+                dev = (self.w * self.fam.deviance(self.y, mu)).sum().view(1)
+            return self._finish_stats(G, xz, xw, sw.view(1), swz.view(1), dev)
         with phase("glm.gram"):
             G = linalg_ops.weighted_gram(self.X, Wf)[: self.P, : self.P]
         with phase("glm.xtwz"):

@@ -71,3 +71,24 @@ def test_glm_irls_external_widths(P, Pp, signed):
     Gk, _ = linalg_ops.glm_irls(X.cuda(), aug=P, W=W.cuda(), z=z.cuda())
     Gr, _ = linalg_ops.glm_irls_reference(X, aug=P, W=W, z=z)
     assert _close(Gk[: P + 2, : P + 2], Gr[: P + 2, : P + 2])
+
+
+def test_weighted_gram_aug_matches_fp64():
+    """Wide-design augmented Gram (library GEMM path) vs fp64 torch."""
+    import torch
+    if not torch.cuda.is_available():
+        import pytest
+        pytest.skip("no GPU")
+    from h2o3_amd.ops import linalg_ops
+    g = torch.Generator(device="cuda").manual_seed(0)
+    N, P = 300000, 600
+    X = torch.randn(N, P + 8, generator=g, device="cuda")
+    W = torch.rand(N, generator=g, device="cuda", dtype=torch.float64)
+    z = torch.randn(N, generator=g, device="cuda", dtype=torch.float64)
+    G, xw, xz, sw, swz = linalg_ops.weighted_gram_aug(X, W, z, P, step=100000)
+    Xd = X[:, :P].double()
+    torch.testing.assert_close(G, Xd.T @ (Xd * W.view(-1, 1)), rtol=2e-4, atol=2e-2)
+    torch.testing.assert_close(xw, Xd.T @ W, rtol=2e-4, atol=2e-2)
+    torch.testing.assert_close(xz, Xd.T @ (W * z), rtol=2e-4, atol=2e-2)
+    torch.testing.assert_close(sw, W.sum(), rtol=1e-5, atol=1e-3)
+    torch.testing.assert_close(swz, (W * z).sum(), rtol=1e-4, atol=1e-2)
