@@ -145,6 +145,11 @@ def main():
         ll = float(-(yy * torch.log(p) + (1 - yy) * torch.log(1 - p)).mean())
         extra["train_logloss_after"] = round(ll, 5)
         extra["trees_built"] = len(drv.forest)
+    if args.algo == "glm":
+        # convergence sanity (not timed): deviance of the last iteration and the
+        # final coefficient step
+        extra["train_deviance_per_row"] = round(float(drv.last_dev) / float(drv.wsum), 6)
+        extra["iters"] = int(drv.iter)
     from h2o3_amd.utils import timer
     if timer.ENABLED and rank == 0:
         print("phases(ms,count):", timer.report(), file=sys.stderr)
@@ -153,8 +158,10 @@ def main():
                "warmup": args.warmup, "ms_per_step": round(1000 * el / args.steps, 3), "higher_is_better": True,
                "scaling": "strong", "vs_baseline": None, "dtype": "fp32",
                "data": "synthetic (random normal features, logistic label), generated on device",
-               "config": {"model": model, "rows": args.rows, "cols": F, "max_depth": args.max_depth,
-                          "histogram_type": args.histogram_type, "nbins": args.nbins,
+               "config": {"model": model, "rows": args.rows, "cols": F,
+                          **({} if args.algo == "glm" else {"max_depth": est._parms.get("max_depth"),
+                                                            "histogram_type": args.histogram_type,
+                                                            "nbins": args.nbins}),
                           "global_batch": args.rows, "seq_len": None, "parallelism": f"dp{world}"},
                **extra}
         print(json.dumps(out))

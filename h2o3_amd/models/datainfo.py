@@ -71,14 +71,14 @@ class DataInfo:
         self.P = len(self.coef_names)
         self.Pp = ((self.P + pad_extra + pad_to - 1) // pad_to) * pad_to if pad_to else self.P
 
-    def expand(self, frame, dtype=torch.float32, pad=True):
-        """Returns (X [n, P or Pp], row_ok mask) on device."""
+    def expand(self, frame, dtype=torch.float32, pad=True, width=None):
+        """Returns (X [n, P or Pp, or `width` columns], row_ok mask) on device."""
         if self.ia_recipe:
             from .glm.interactions import apply_recipe
             frame = apply_recipe(frame, self.ia_recipe)[0]
         n = frame.nlocal
         dev = cloud.device()
-        P = self.Pp if pad else self.P
+        P = int(width) if width else (self.Pp if pad else self.P)
         X = torch.zeros((n, P), dtype=dtype, device=dev)
         ok = torch.ones(n, dtype=torch.bool, device=dev)
         for c in self.cat_cols:

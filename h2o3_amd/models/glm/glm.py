@@ -244,7 +244,12 @@ class GLMDriver:
                               plug_values=p.get("plug_values"), pad_extra=2,
                               interactions=interaction_pairs(spec.x, p.get("interactions"),
                                                              p.get("interaction_pairs")))
-        self.X, ok = self.dinfo.expand(spec.frame)
+        # Pp = 128 runs the warp-specialised IRLS kernel, which reads rows of
+        # round_up(P, 4) floats: at P = 100 the 28 padding columns (22 % of the
+        # HBM stream) are never stored
+        Pn = (self.dinfo.P + 3) // 4 * 4
+        narrow = cloud.device().type == "cuda" and self.dinfo.Pp == 128 and Pn < 128
+        self.X, ok = self.dinfo.expand(spec.frame, width=Pn if narrow else None)
         y = spec.y_tensor()
         if spec.is_classification:
             yy = (y == 1).to(torch.float64) if fam != "multinomial" else y.to(torch.float64)
@@ -406,7 +411,7 @@ class GLMDriver:
     # ---- device-side pieces
     def _eta(self, beta=None):
         b = self.beta if beta is None else beta
-        bt = torch.zeros(self.Pp, dtype=torch.float32, device=self.X.device)
+        bt = torch.zeros(self.X.shape[1], dtype=torch.float32, device=self.X.device)
         bt[: self.P] = torch.as_tensor(b[: self.P], dtype=torch.float32)
         eta = (self.X @ bt).to(torch.float64) + b[-1]
         if self.offset is not None:
@@ -426,7 +431,7 @@ class GLMDriver:
         r = self.w * (self.y - mu) * d / self.fam.variance(mu)
         if self._native():
             # X'r rides the fused Gram pass (column P of the augmented Gram)
-            g = linalg_ops.glm_irls(self.X, aug=self.P, W=r)[0][: self.P, self.P].contiguous()
+            g = linalg_ops.glm_irls(self.X, aug=self.P, W=r, width=self.Pp)[0][: self.P, self.P].contiguous()
         else:
             g = (self.X.to(torch.float64).T @ r)[: self.P]
         coll.allreduce_(g)
@@ -454,7 +459,7 @@ class GLMDriver:
                 bt[:P] = torch.as_tensor(self.beta[:P], dtype=torch.float32)
                 Gf, dev = linalg_ops.glm_irls(self.X, aug=P, beta=bt, b0=float(self.beta[-1]), y=self._y32,
                                               wprior=self._w32, offset=self._off32, codes=codes,
-                                              tvp=self.fam.tvp, theta=self.fam.theta)
+                                              tvp=self.fam.tvp, theta=self.fam.theta, width=self.Pp)
                 dev = dev.view(1)
             else:
                 eta = self._eta()
@@ -463,7 +468,7 @@ class GLMDriver:
                 W = self.w * d * d / self.fam.variance(mu)
                 off = self.offset if self.offset is not None else 0.0
                 z = (eta - off) + (self.y - mu) / d
-                Gf, _ = linalg_ops.glm_irls(self.X, aug=P, W=W, z=z)
+                Gf, _ = linalg_ops.glm_irls(self.X, aug=P, W=W, z=z, width=self.Pp)
                 dev = (self.w * self.fam.deviance(self.y, mu)).sum().view(1)
         return Gf[:P, :P], Gf[:P, P + 1].contiguous(), Gf[:P, P].contiguous(), Gf[P, P].view(1), \
             Gf[P, P + 1].view(1), dev

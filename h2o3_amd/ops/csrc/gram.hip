@@ -114,8 +114,11 @@ struct GlmFamArgs {
   int var;      // 0 gaussian 1 binomial 2 poisson 3 gamma 4 tweedie 5 negbin
   float tvp;    // tweedie variance power
   float theta;  // negative-binomial dispersion
-  int dbg;      // perf experiments only: bit0 skip MFMA sweep, bit1 skip HBM loads
+  int dbg;      // perf experiments only: bit0 skip MFMA sweep, bit1 skip HBM loads of X,
+                // bit2 skip y/w/offset loads, bit3 skip the eta dot products, bit4 eta and
+                // sqrt(W) by ds_bpermute instead of DPP + LDS (ws kernel)
   int signed_w; // external weights may be negative (no sqrt(W) pre-scaling)
+  int bf3;      // P = 128 ws path: bf16x3 MFMA operands instead of f32
 };
 
 __device__ __forceinline__ float gi_linkinv(int link, float eta) {
@@ -199,6 +202,38 @@ template <int T, int SL, int... Q>
 __device__ __forceinline__ void gi_mfma_all(std::integer_sequence<int, Q...>, const float* xr, const float* xw,
                                             f32x4* acc) {
   (gi_mfma_q<T, SL, Q>(xr, xw, acc), ...);
+}
+
+// quad_perm DPP move (0xB1: lane ^ 1, 0x4E: lane ^ 2), a VALU op instead of ds_bpermute
+template <int CTRL>
+__device__ __forceinline__ float gi_dpp(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
+}
+
+// bf16x3 path: every staged value is split x = hi + lo (hi = bf16(x), lo =
+// bf16(x - hi)) and each f32 product is rebuilt from hi*hi + hi*lo + lo*hi on
+// the 16x16x32 bf16 MFMA (lo*lo ~ 2^-16 relative is dropped): 3 bf16 MFMAs of
+// 16 cycles replace 8 f32 16x16x4 MFMAs of 32 cycles for the same 32 rows.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+template <int T, int SL, int Q, int M>
+__device__ __forceinline__ void gi_mfma3_q(const bf16x8* ah, const bf16x8* al, f32x4* acc) {
+  constexpr int pp = SL + 4 * Q;
+  if constexpr (pp < T * (T + 1) / 2) {
+    constexpr int ti = gi_pair_i(T, pp), tj = gi_pair_j(T, pp);
+    if constexpr (M == 0) acc[Q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[ti], ah[tj], acc[Q], 0, 0, 0);
+    if constexpr (M == 1) acc[Q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[ti], al[tj], acc[Q], 0, 0, 0);
+    if constexpr (M == 2) acc[Q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[ti], ah[tj], acc[Q], 0, 0, 0);
+  }
+}
+// all hi*hi first, then the two cross terms: consecutive MFMAs hit different
+// accumulators
+template <int T, int SL, int... Q>
+__device__ __forceinline__ void gi_mfma3_all(std::integer_sequence<int, Q...>, const bf16x8* ah, const bf16x8* al,
+                                             f32x4* acc) {
+  (gi_mfma3_q<T, SL, Q, 0>(ah, al, acc), ...);
+  (gi_mfma3_q<T, SL, Q, 1>(ah, al, acc), ...);
+  (gi_mfma3_q<T, SL, Q, 2>(ah, al, acc), ...);
 }
 
 // Chunk rows (multiple of 4 = one 16x16x4 k-step); the staging registers hold
@@ -442,12 +477,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 // the MFMA accumulators in registers (f32 over <= 1024 rows) and fold them
 // into the block's own f64 tile (no atomics, deterministic).
 // ---------------------------------------------------------------------------
-template <int PP, bool FUSED, bool SQW>
+template <int PP, bool FUSED, bool SQW, bool BF3>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) void glm_irls_ws_kernel(
-    const float* __restrict__ X, long long N, int n_pairs, int rows_per_block, const float* __restrict__ beta,
-    float b0, const float* __restrict__ y, const float* __restrict__ wprior, const float* __restrict__ offset,
-    GlmFamArgs fam, const float* __restrict__ Wext, const float* __restrict__ zext, int aug,
-    double* __restrict__ out, double* __restrict__ dev_out) {
+    const float* __restrict__ X, long long N, int ldx, int n_pairs, int rows_per_block,
+    const float* __restrict__ beta, float b0, const float* __restrict__ y, const float* __restrict__ wprior,
+    const float* __restrict__ offset, GlmFamArgs fam, const float* __restrict__ Wext,
+    const float* __restrict__ zext, int aug, double* __restrict__ out, double* __restrict__ dev_out) {
   constexpr int RC = 64;
   constexpr int P4 = PP / 4;
   constexpr int T = PP / 16;
@@ -456,9 +491,23 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   constexpr int NVP = RPW * P4 / 64;   // float4 per producer lane per chunk
   constexpr int RPV = 64 / P4;         // rows covered by one float4 slot of a wave
   static_assert(PP <= 128 && (PP & (PP - 1)) == 0, "ws kernel: power-of-two width <= 128");
-  __shared__ float L[2][RC * S];
+  // BF3 LDS image: feature-major [feature][KS] bf16 hi and lo planes; the 64
+  // chunk rows are permuted (producer wave pw, lane half par, slot v ->
+  // k = 16 pw + 8 par + v) so each producer lane writes 8 rows of one feature
+  // as one 16-byte store and each consumer lane reads its 16x16x32 operand
+  // (8 consecutive k of one feature) as one ds_read_b128.  KS = 72 puts the 16
+  // features of an operand read on 16 distinct 4-bank groups.
+  constexpr int KS = 72;
+  static_assert(!BF3 || (PP == 128 && SQW), "bf16x3 path: P = 128, sqrt(W)-scaled rows");
+  __shared__ float L[2][BF3 ? 4 : RC * S];
+  __shared__ __attribute__((aligned(16))) __bf16 LB[2][2][BF3 ? PP * KS : 8];
   __shared__ float wr[2][RC];
   __shared__ double dsum[4];
+  // P = 128 producer scratch: eta partials [wave][row 16][quad 8] and the
+  // per-row sqrt(W) [wave][16] (replaces 48 + 8 ds_bpermute per chunk)
+  constexpr bool QRED = P4 == 32;
+  __shared__ __attribute__((aligned(16))) float es[QRED ? 4 : 1][QRED ? 128 : 4];
+  __shared__ __attribute__((aligned(16))) float sqs[QRED ? 4 : 1][QRED ? 16 : 4];
   const int split = blockIdx.x;
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
@@ -491,13 +540,19 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
 #pragma unroll
         for (int v = 0; v < NVP; ++v) V[v] = f32x4{0.f, 0.f, 0.f, (float)c};
       } else {
+        // X rows are ldx floats (ldx <= PP, ldx % 4 == 0): the PP - ldx
+        // padding columns never leave HBM, their lanes stage zeros
+        const bool live = 4 * cq < ldx;
 #pragma unroll
         for (int v = 0; v < NVP; ++v) {
           const long long g = min(r0 + v * RPV + lane / P4, N - 1);
-          V[v] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(X + g * (long long)PP) + cq);
+          V[v] = live ? __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(X + g * (long long)ldx) + cq)
+                      : f32x4{0.f, 0.f, 0.f, 0.f};
         }
       }
-      if (lane < RPW) {
+      if (lane < RPW && (fam.dbg & 4)) {
+        sy = 0.f; sw = 1.f; so = 0.f;
+      } else if (lane < RPW) {
         const long long g = min(r0 + lane, N - 1);
         if (FUSED) {
           sy = y[g];
@@ -514,7 +569,33 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       const float sy = st.sy, sw = st.sw, so = st.so;
       float* Lb = L[c & 1];
       float etav = 0.f;
-      if (FUSED) {
+      const bool qred = QRED && !(fam.dbg & 16);
+      if (FUSED && qred) {
+        if (!(fam.dbg & 8)) {
+          // lane-local 4-feature dot products of its 8 rows, quad sums by DPP,
+          // then the 8 quad partials of a row meet in LDS: row j's lane (< 16)
+          // reads them back as two b128 (eta lands where the family runs)
+          float ps[NVP];
+#pragma unroll
+          for (int v = 0; v < NVP; ++v) ps[v] = V[v].x * b4.x + V[v].y * b4.y + V[v].z * b4.z + V[v].w * b4.w;
+#pragma unroll
+          for (int v = 0; v < NVP; ++v) ps[v] += gi_dpp<0xB1>(ps[v]);
+#pragma unroll
+          for (int v = 0; v < NVP; ++v) ps[v] += gi_dpp<0x4E>(ps[v]);
+          const int r = lane & 3, q = (lane >> 2) & 7, par = lane >> 5;
+          float* S = es[pw];
+#pragma unroll
+          for (int m = 0; m < NVP / 4; ++m) {
+            const float val = r == 0 ? ps[4 * m] : r == 1 ? ps[4 * m + 1] : r == 2 ? ps[4 * m + 2] : ps[4 * m + 3];
+            S[(2 * (r + 4 * m) + par) * 8 + q] = val;
+          }
+          if (lane < RPW) {
+            const f32x4 a = *reinterpret_cast<const f32x4*>(S + lane * 8);
+            const f32x4 b = *reinterpret_cast<const f32x4*>(S + lane * 8 + 4);
+            etav = (a.x + a.y) + (a.z + a.w) + ((b.x + b.y) + (b.z + b.w));
+          }
+        }
+      } else if (FUSED && !(fam.dbg & 8)) {
 #pragma unroll
         for (int v = 0; v < NVP; ++v) {
           float sdot = V[v].x * b4.x + V[v].y * b4.y + V[v].z * b4.z + V[v].w * b4.w;
@@ -550,6 +631,49 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       // SQW: rows are staged pre-scaled by sqrt(W) so the consumers' MFMA
       // operands come straight from LDS (no VALU between LDS and MFMA)
       const float sq = SQW ? sqrtf(fmaxf(W, 0.f)) : 1.f;
+      if constexpr (BF3) {
+        __bf16* Hb = LB[c & 1][0];
+        __bf16* Lb2 = LB[c & 1][1];
+        const int par = lane / P4;
+        // row j = 2 v + par: lanes < 16 publish sqrt(W) as [par][v], every
+        // lane reads its 8 rows' factors as two broadcast b128
+        float sv[NVP];
+        if (qred) {
+          float* Q = sqs[pw];
+          if (lane < RPW) Q[(lane & 1) * 8 + (lane >> 1)] = sq;
+          const f32x4 q0 = *reinterpret_cast<const f32x4*>(Q + par * 8);
+          const f32x4 q1 = *reinterpret_cast<const f32x4*>(Q + par * 8 + 4);
+          sv[0] = q0.x; sv[1] = q0.y; sv[2] = q0.z; sv[3] = q0.w;
+          sv[4] = q1.x; sv[5] = q1.y; sv[6] = q1.z; sv[7] = q1.w;
+        } else {
+#pragma unroll
+          for (int v = 0; v < NVP; ++v) sv[v] = __shfl(sq, v * RPV + par, 64);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          bf16x8 h, l;
+#pragma unroll
+          for (int v = 0; v < NVP; ++v) {
+            const float x = V[v][e] * sv[v];
+            const __bf16 hb = (__bf16)x;
+            h[v] = hb;
+            l[v] = (__bf16)(x - (float)hb);
+          }
+          const int off = (4 * cq + e) * KS + pw * RPW + par * 8;
+          *reinterpret_cast<bf16x8*>(Hb + off) = h;
+          *reinterpret_cast<bf16x8*>(Lb2 + off) = l;
+        }
+        if (lane < RPW && aug >= 0) {
+          const int k = pw * RPW + (lane % RPV) * 8 + lane / RPV;
+          const float a0 = sq, a1 = sq * z;
+          const __bf16 h0 = (__bf16)a0, h1 = (__bf16)a1;
+          Hb[aug * KS + k] = h0;
+          Lb2[aug * KS + k] = (__bf16)(a0 - (float)h0);
+          Hb[(aug + 1) * KS + k] = h1;
+          Lb2[(aug + 1) * KS + k] = (__bf16)(a1 - (float)h1);
+        }
+        return;
+      }
 #pragma unroll
       for (int v = 0; v < NVP; ++v) {
         const int rl = pw * RPW + v * RPV + lane / P4;
@@ -631,7 +755,22 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       for (int i = 0; i < nchunks; ++i) {
         const float* Lb = L[i & 1] + kr * S + cc;
         const float* wb = wr[i & 1] + kr;
-        if (!(fam.dbg & 1)) {
+        if constexpr (BF3) {
+          if (!(fam.dbg & 1)) {
+            const __bf16* Hb = LB[i & 1][0] + cc * KS + kr * 8;
+            const __bf16* Lo = LB[i & 1][1] + cc * KS + kr * 8;
+#pragma unroll 1
+            for (int ks = 0; ks < RC / 32; ++ks) {
+              bf16x8 ah[T], al[T];
+#pragma unroll
+              for (int t = 0; t < T; ++t) {
+                ah[t] = *reinterpret_cast<const bf16x8*>(Hb + 16 * t * KS + 32 * ks);
+                al[t] = *reinterpret_cast<const bf16x8*>(Lo + 16 * t * KS + 32 * ks);
+              }
+              gi_mfma3_all<T, SL>(std::make_integer_sequence<int, GI_PPW>{}, ah, al, acc);
+            }
+          }
+        } else if (!(fam.dbg & 1)) {
           float xr[T], xn[T], xw[T];
           float w = SQW ? 1.f : wb[0];
 #pragma unroll
@@ -669,22 +808,33 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
 }
 
 template <int PP>
-static void gi_launch(bool fused, dim3 grid, hipStream_t s, const float* X, long long N, const int2* pairs,
+static void gi_launch(bool fused, dim3 grid, hipStream_t s, const float* X, long long N, int ldx, const int2* pairs,
                       int n_pairs, int rpb, const float* beta, float b0, const float* y, const float* wprior,
                       const float* offset, GlmFamArgs fam, const float* Wext, const float* zext, int aug,
                       double* out, double* dev_out) {
   if constexpr (PP <= 128 && (PP & (PP - 1)) == 0) {
     // IRLS weights are >= 0 -> sqrt(W) pre-scaling; caller-signed weights
     // (e.g. X'r for lambda_max) take the explicit-multiply path
+    if constexpr (PP == 128) {
+      if (fam.bf3 && !fam.signed_w) {
+        if (fused)
+          hipLaunchKernelGGL((glm_irls_ws_kernel<PP, true, true, true>), dim3(grid.x), dim3(512), 0, s, X, N, ldx,
+                             n_pairs, rpb, beta, b0, y, wprior, offset, fam, Wext, zext, aug, out, dev_out);
+        else
+          hipLaunchKernelGGL((glm_irls_ws_kernel<PP, false, true, true>), dim3(grid.x), dim3(512), 0, s, X, N, ldx,
+                             n_pairs, rpb, beta, b0, y, wprior, offset, fam, Wext, zext, aug, out, dev_out);
+        return;
+      }
+    }
     if (fused)
-      hipLaunchKernelGGL((glm_irls_ws_kernel<PP, true, true>), dim3(grid.x), dim3(512), 0, s, X, N, n_pairs, rpb,
-                         beta, b0, y, wprior, offset, fam, Wext, zext, aug, out, dev_out);
+      hipLaunchKernelGGL((glm_irls_ws_kernel<PP, true, true, false>), dim3(grid.x), dim3(512), 0, s, X, N, ldx, n_pairs,
+                         rpb, beta, b0, y, wprior, offset, fam, Wext, zext, aug, out, dev_out);
     else if (!fam.signed_w)
-      hipLaunchKernelGGL((glm_irls_ws_kernel<PP, false, true>), dim3(grid.x), dim3(512), 0, s, X, N, n_pairs, rpb,
-                         beta, b0, y, wprior, offset, fam, Wext, zext, aug, out, dev_out);
+      hipLaunchKernelGGL((glm_irls_ws_kernel<PP, false, true, false>), dim3(grid.x), dim3(512), 0, s, X, N, ldx, n_pairs,
+                         rpb, beta, b0, y, wprior, offset, fam, Wext, zext, aug, out, dev_out);
     else
-      hipLaunchKernelGGL((glm_irls_ws_kernel<PP, false, false>), dim3(grid.x), dim3(512), 0, s, X, N, n_pairs, rpb,
-                         beta, b0, y, wprior, offset, fam, Wext, zext, aug, out, dev_out);
+      hipLaunchKernelGGL((glm_irls_ws_kernel<PP, false, false, false>), dim3(grid.x), dim3(512), 0, s, X, N, ldx, n_pairs,
+                         rpb, beta, b0, y, wprior, offset, fam, Wext, zext, aug, out, dev_out);
     return;
   }
   if constexpr (GiCfg<PP>::POW2) {
@@ -696,6 +846,13 @@ static void gi_launch(bool fused, dim3 grid, hipStream_t s, const float* X, long
   }
   hipLaunchKernelGGL((glm_irls_kernel<PP, false>), grid, dim3(256), 0, s, X, N, pairs, n_pairs, rpb, beta, b0, y,
                      wprior, offset, fam, Wext, zext, aug, out, dev_out);
+}
+
+// H2O3_GLM_BF3: 1 (default) bf16x3 MFMA for the P = 128 ws path, 0 f32 MFMA
+// (read per call: one getenv per IRLS pass)
+static int gi_bf3() {
+  const char* e = getenv("H2O3_GLM_BF3");
+  return e ? atoi(e) : 1;
 }
 
 static int gi_dbg() {
@@ -713,24 +870,26 @@ extern "C" int h2o_glm_irls_chunk(int P) {
   return P <= 128 ? 64 : (r < 16 ? 16 : r);
 }
 
-extern "C" int h2o_glm_irls(const float* X, long long N, int P, const int* pairs, int n_pairs, int n_splits,
+extern "C" int h2o_glm_irls(const float* X, long long N, int P, int ldx, const int* pairs, int n_pairs, int n_splits,
                             int rows_per_block, const float* beta, float b0, const float* y, const float* wprior,
                             const float* offset, int link, int var, float tvp, float theta, const float* Wext,
                             const float* zext, int aug, int signed_w, double* out, double* dev_out,
                             hipStream_t s) {
   if (N <= 0 || n_pairs <= 0) return 0;
   if (P % 32 != 0 || P > 512) return -1;
+  // narrow row storage (ldx < P) only on the warp-specialised path
+  if (ldx % 4 != 0 || ldx > P || (ldx < P && (P > 128 || (P & (P - 1)) != 0))) return -5;
   if (aug >= 0 && aug + 1 >= P) return -2;
   if (beta && (P & (P - 1)) != 0) return -3;
   if (rows_per_block % h2o_glm_irls_chunk(P) != 0) return -4;
   const int groups = (n_pairs + 4 * GI_PPW - 1) / (4 * GI_PPW);
   dim3 grid(n_splits, groups);
-  GlmFamArgs fam{link, var, tvp, theta, gi_dbg(), signed_w};
+  GlmFamArgs fam{link, var, tvp, theta, gi_dbg(), signed_w, gi_bf3()};
   const bool fused = beta != nullptr;
   const int2* pr = (const int2*)pairs;
 #define GI_CASE(pp)                                                                                          \
   case pp:                                                                                                   \
-    gi_launch<pp>(fused, grid, s, X, N, pr, n_pairs, rows_per_block, beta, b0, y, wprior, offset, fam, Wext, \
+    gi_launch<pp>(fused, grid, s, X, N, ldx, pr, n_pairs, rows_per_block, beta, b0, y, wprior, offset, fam, Wext, \
                   zext, aug, out, dev_out);                                                                  \
     break;
   switch (P) {

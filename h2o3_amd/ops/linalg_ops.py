@@ -21,7 +21,7 @@ def _lib():
         lib.h2o_gram.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_int, ctypes.c_void_p,
                                  ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         P, I, LL, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong, ctypes.c_float
-        lib.h2o_glm_irls.argtypes = [P, LL, I, P, I, I, I, P, F, P, P, P, I, I, F, F, P, P, I, I, P, P, P]
+        lib.h2o_glm_irls.argtypes = [P, LL, I, I, P, I, I, I, P, F, P, P, P, I, I, F, F, P, P, I, I, P, P, P]
         lib.h2o_glm_irls_chunk.argtypes = [I]
         lib._typed = True
     return lib
@@ -68,7 +68,7 @@ def _ptr(t):
 
 
 def glm_irls(X, aug=-1, beta=None, b0=0.0, y=None, wprior=None, offset=None, codes=(0, 0), tvp=0.0, theta=1e-10,
-             W=None, z=None, signed=None, target_blocks=1024):
+             W=None, z=None, signed=None, target_blocks=1024, width=None):
     """One pass of the fused IRLS kernel (ops/csrc/gram.hip glm_irls_kernel).
 
     Fused mode (beta given): per row eta = x.beta + b0 + offset, the family's
@@ -76,8 +76,11 @@ def glm_irls(X, aug=-1, beta=None, b0=0.0, y=None, wprior=None, offset=None, cod
     `signed`: external W may hold negative values (default: checked).
     Returns (G [Pp, Pp] f64 — columns `aug` / `aug+1` hold X'W / X'Wz and
     their cross terms when aug >= 0 — and the f64 deviance, or None).
+    `width`: logical padded width Pp when X is stored narrower (X [N, ldx],
+    ldx % 4 == 0, columns ldx..Pp-1 implicitly zero; Pp = 128 ws path only).
     """
-    N, P = X.shape
+    N, ldx = X.shape
+    P = int(width) if width else ldx
     lib = _lib()
     if lib is None:
         raise RuntimeError("gram extension not built (run __graft_entry__.build())")
@@ -97,7 +100,7 @@ def glm_irls(X, aug=-1, beta=None, b0=0.0, y=None, wprior=None, offset=None, cod
     keep = [_f32(y), _f32(wprior), _f32(offset), _f32(W), _f32(z)]
     if signed is None:
         signed = beta is None and keep[3] is not None and bool((keep[3] < 0).any())
-    rc = lib.h2o_glm_irls(_ptr(X), N, P, _ptr(pairs_t), npairs, splits, rpb, _ptr(bt), float(b0), _ptr(keep[0]),
+    rc = lib.h2o_glm_irls(_ptr(X), N, P, ldx, _ptr(pairs_t), npairs, splits, rpb, _ptr(bt), float(b0), _ptr(keep[0]),
                           _ptr(keep[1]), _ptr(keep[2]), int(codes[0]), int(codes[1]), float(tvp), float(theta),
                           _ptr(keep[3]), _ptr(keep[4]), int(aug), int(bool(signed)), _ptr(out), _ptr(dev),
                           ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))

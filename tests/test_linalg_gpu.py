@@ -92,3 +92,67 @@ def test_weighted_gram_aug_matches_fp64():
     torch.testing.assert_close(xz, Xd.T @ (W * z), rtol=2e-4, atol=2e-2)
     torch.testing.assert_close(sw, W.sum(), rtol=1e-5, atol=1e-3)
     torch.testing.assert_close(swz, (W * z).sum(), rtol=1e-4, atol=1e-2)
+
+
+@pytest.mark.parametrize("bf3", ["1", "0"])
+def test_glm_irls_bf3_elementwise(monkeypatch, bf3):
+    """P = 100 (padded 128) runs the warp-specialised kernel; H2O3_GLM_BF3
+    selects bf16x3 (hi*hi + hi*lo + lo*hi on 16x16x32 bf16 MFMA) or f32
+    16x16x4 MFMA.  Both must match fp64 entry by entry, not just at the max."""
+    monkeypatch.setenv("H2O3_GLM_BF3", bf3)
+    n, P, Pp = 300_007, 100, 128
+    X, beta, g = _data(n, P, Pp, seed=11)
+    X[:, 7] = 3.0 + 0.01 * X[:, 7]          # near-constant column: large mean, small spread
+    y = (torch.rand(n, generator=g) < torch.sigmoid(X @ beta)).float()
+    fam = _Fam("binomial", "logit")
+    codes = linalg_ops.glm_fused_codes("binomial", "logit")
+    Gk, dk = linalg_ops.glm_irls(X.cuda(), aug=P, beta=beta.cuda(), b0=-0.1, y=y.cuda(), codes=codes)
+    Gr, dr = linalg_ops.glm_irls_reference(X, aug=P, beta=beta, b0=-0.1, y=y, fam=fam)
+    A, B = Gk[: P + 2, : P + 2].cpu(), Gr[: P + 2, : P + 2]
+    diag = B.diagonal().abs().sqrt()
+    rel = (A - B).abs() / (diag.view(-1, 1) * diag.view(1, -1))   # error relative to sqrt(G_ii G_jj)
+    assert rel.max().item() < 2e-5
+    assert abs(dk.item() - dr.item()) / abs(dr.item()) < 1e-4
+
+
+def test_glm_fit_bf3_matches_f32(monkeypatch):
+    """End-to-end IRLSM fit: bf16x3 and f32 MFMA Gram give the same model."""
+    import numpy as np
+    from h2o3_amd.core.frame import H2OFrame
+    from h2o3_amd.models.glm.glm import H2OGeneralizedLinearEstimator
+    g = np.random.default_rng(2)
+    n, P = 200_000, 100
+    X = g.standard_normal((n, P)).astype(np.float32)
+    b = 0.2 * g.standard_normal(P)
+    y = (g.random(n) < 1 / (1 + np.exp(-(X @ b)))).astype(int)
+    cols = {f"x{j}": X[:, j] for j in range(P)}
+    cols["y"] = y
+    fr = H2OFrame(cols)
+    fr["y"] = fr["y"].asfactor()
+    coefs = []
+    for v in ("1", "0"):
+        monkeypatch.setenv("H2O3_GLM_BF3", v)
+        m = H2OGeneralizedLinearEstimator(family="binomial", lambda_=0.0)
+        m.train(y="y", training_frame=fr)
+        coefs.append(np.array([m.coef()[k] for k in sorted(m.coef())]))
+    np.testing.assert_allclose(coefs[0], coefs[1], rtol=0, atol=2e-5)
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_glm_irls_narrow_rows(fused):
+    """X stored as [N, 100] (ldx = 100) with logical width 128 gives the same
+    augmented Gram as the zero-padded [N, 128] matrix."""
+    n, P, Pp = 123_457, 100, 128
+    X, beta, g = _data(n, P, Pp, seed=13)
+    Xn = X[:, :P].contiguous()
+    if fused:
+        y = (torch.rand(n, generator=g) < torch.sigmoid(X @ beta)).float()
+        codes = linalg_ops.glm_fused_codes("binomial", "logit")
+        kw = dict(aug=P, beta=beta.cuda(), b0=0.3, y=y.cuda(), codes=codes)
+    else:
+        kw = dict(aug=P, W=torch.randn(n, generator=g).cuda(), z=torch.randn(n, generator=g).cuda())
+    Gp, dp = linalg_ops.glm_irls(X.cuda(), **kw)
+    Gn, dn = linalg_ops.glm_irls(Xn.cuda(), width=Pp, **kw)
+    torch.testing.assert_close(Gn, Gp, rtol=1e-9, atol=1e-9)
+    if fused:
+        torch.testing.assert_close(dn, dp, rtol=1e-9, atol=1e-9)
