@@ -163,6 +163,28 @@ def _soft(x, t):
     return math.copysign(max(abs(x) - t, 0.0), x)
 
 
+_CD = []
+
+
+def _native_cd():
+    """C++ coordinate descent (h2o3_amd/native/glm_solver.cpp), None if unbuilt."""
+    if not _CD:
+        fn = None
+        try:
+            import ctypes
+            from ...ops import _native
+            lib = _native.get_lib("glm_solver", required=False)
+            if lib is not None:
+                fn = lib.h2o_glm_cd
+                vp, d, i = ctypes.c_void_p, ctypes.c_double, ctypes.c_int
+                fn.argtypes = [i, vp, vp, vp, vp, vp, d, d, vp, i, d]
+                fn.restype = i
+        except Exception:  # noqa: BLE001
+            fn = None
+        _CD.append(fn)
+    return _CD[0]
+
+
 def _solve_quadratic(G, b, l1, l2, intercept, beta0=None, non_negative=False, max_iter=1000, tol=1e-10,
                      penalty_mask=None, lower=None, upper=None, active=None):
     """min 1/2 b'Gb - b'x + l1|b|_1 + l2/2|b|^2 (last coef = intercept, unpenalized),
@@ -191,13 +213,25 @@ def _solve_quadratic(G, b, l1, l2, intercept, beta0=None, non_negative=False, ma
     lo = np.where(nn, np.maximum(lo, 0.0), lo)
     boxed = bool(np.isfinite(lo).any() or np.isfinite(hi).any())
     if l1 == 0 and not boxed:
-        A = G + np.diag(l2 * pen + 1e-10 * np.maximum(np.diag(G), 1e-12) * 0)
+        import scipy.linalg as sla
+        A = G + np.diag(l2 * pen)
         try:
-            L = np.linalg.cholesky(A + np.eye(P) * 1e-12 * max(1.0, np.abs(np.diag(A)).max()))
-            return np.linalg.solve(L.T, np.linalg.solve(L, b))
+            cf = sla.cho_factor(A + np.eye(P) * 1e-12 * max(1.0, np.abs(np.diag(A)).max()), lower=True,
+                                check_finite=False)
+            return sla.cho_solve(cf, b, check_finite=False)
         except np.linalg.LinAlgError:
             return np.linalg.lstsq(A, b, rcond=None)[0]
     beta = np.zeros(P) if beta0 is None else np.clip(beta0.copy(), lo, hi)
+    cd = _native_cd()
+    if cd is not None:
+        import ctypes
+        Gc = np.ascontiguousarray(G, dtype=np.float64)
+        arrs = [Gc, np.ascontiguousarray(b, dtype=np.float64), np.ascontiguousarray(pen, dtype=np.float64),
+                np.ascontiguousarray(lo), np.ascontiguousarray(hi)]
+        beta = np.ascontiguousarray(beta, dtype=np.float64)
+        ptr = [a.ctypes.data_as(ctypes.c_void_p) for a in arrs]
+        cd(P, *ptr, float(l1), float(l2), beta.ctypes.data_as(ctypes.c_void_p), int(max_iter), float(tol))
+        return beta
     diag = np.diag(G) + l2 * pen
     grad = b - G @ beta
     for it in range(max_iter):
@@ -477,6 +511,21 @@ class GLMDriver:
         if self._native():
             G, xz, xw, sw, swz, dev = self._irls_stats_native()
             return self._finish_stats(G, xz, xw, sw, swz, dev)
+        codes = linalg_ops.glm_fused_codes(self.fam.family, self.fam.link, self.fam.tlp)
+        if self.X.device.type == "cuda" and self.Pp > 512 and self.P + 2 <= 1024 and codes is not None and \
+                linalg_ops._wide_mode() == "bf3":
+            # one fused pass: eta + family + bf16 hi/lo split, then one bf16 GEMM
+            with phase("glm.wide_pass"):
+                if not hasattr(self, "_y32"):
+                    self._y32 = self.y.to(torch.float32)
+                    self._w32 = self.w.to(torch.float32)
+                    self._off32 = None if self.offset is None else self.offset.to(torch.float32)
+                P = self.P
+                bt = torch.as_tensor(self.beta[:P], dtype=torch.float32, device=self.X.device)
+                Gf, dev = linalg_ops.glm_wide_irls(self.X, P, bt, float(self.beta[-1]), self._y32, self._w32,
+                                                   self._off32, codes, self.fam.tvp, self.fam.theta)
+            return self._finish_stats(Gf[:P, :P], Gf[:P, P + 1].contiguous(), Gf[:P, P].contiguous(),
+                                      Gf[P, P].view(1), Gf[P, P + 1].view(1), dev.view(1))
         with phase("glm.eta"):
             eta = self._eta()
         with phase("glm.weights"):

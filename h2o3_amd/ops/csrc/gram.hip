@@ -19,6 +19,7 @@
 #include <type_traits>
 #include <utility>
 #include <cstdlib>
+#include <algorithm>
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -898,5 +899,162 @@ extern "C" int h2o_glm_irls(const float* X, long long N, int P, int ldx, const i
     default: return -1;
   }
 #undef GI_CASE
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Wide GLMs (P > 512): one streaming pass turns the augmented, sqrt(W)-scaled
+// rows a = sqrt(W) [x | 1 | z | 0 ...] (Pa columns) into bf16 hi / lo halves
+// stored side by side, HL[r] = [hi(a) | lo(a)] (row stride 2 Pa).  The Gram
+// then needs ONE library GEMM: C = hi^T [hi | lo] (bf16 in, f32 out) holds
+// hi'hi and hi'lo, and lo'hi = (hi'lo)^T by symmetry, so
+// G = C[:, :Pa] + C[:, Pa:] + C[:, Pa:]^T -- two bf16 GEMM blocks per Gram
+// instead of one f32 GEMM at 1/16 of the bf16 matrix rate (lo*lo, ~2^-16
+// relative, is dropped).  One thread per 4 columns of a row: a float4 load,
+// two 8-byte stores.
+// ---------------------------------------------------------------------------
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256) void gram_split_kernel(const float* __restrict__ X, int ldx, int P, int Pa,
+                                                         const float* __restrict__ W, const float* __restrict__ z,
+                                                         long long rows, __bf16* __restrict__ HL) {
+  const int q4 = Pa / 4;
+  const long long total = rows * q4;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (long long)gridDim.x * blockDim.x) {
+    const long long r = t / q4;
+    const int c = (int)(t - r * q4) * 4;
+    const float s = sqrtf(fmaxf(W ? W[r] : 1.f, 0.f));
+    f32x4 v;
+    if (c + 3 < P && (ldx & 3) == 0) {
+      v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(X + r * ldx + c));
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int cc = c + e;
+        v[e] = cc < P ? X[r * ldx + cc] : cc == P ? 1.f : (cc == P + 1 && z) ? z[r] : 0.f;
+      }
+    }
+    bf16x4 h, l;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float a = v[e] * s;
+      h[e] = (__bf16)a;
+      l[e] = (__bf16)(a - (float)h[e]);
+    }
+    __bf16* o = HL + r * (2LL * Pa) + c;
+    *reinterpret_cast<bf16x4*>(o) = h;
+    *reinterpret_cast<bf16x4*>(o + Pa) = l;
+  }
+}
+
+extern "C" int h2o_gram_split(const float* X, int ldx, int P, int Pa, const float* W, const float* z,
+                              long long rows, void* HL, hipStream_t s) {
+  if (rows <= 0) return 0;
+  if (Pa % 4 != 0 || Pa < P + 2 || ldx < P) return -1;
+  const long long work = rows * (Pa / 4);
+  const int grid = (int)std::min<long long>((work + 255) / 256, 256LL * 64);
+  hipLaunchKernelGGL(gram_split_kernel, dim3(grid), dim3(256), 0, s, X, ldx, P, Pa, W, z, rows, (__bf16*)HL);
+  return (int)hipGetLastError();
+}
+
+// Fused wide IRLS pass: one wave per row (the row's Pa <= 1024 columns sit in
+// 16 registers per lane), eta = x.beta by a wave reduction, the family's
+// IRLS weight / working response / deviance on every lane (wave-uniform), and
+// the [hi | lo] split of sqrt(W) [x | 1 | z] -- X is read from HBM once per
+// IRLS iteration; the library GEMM that follows reads only the bf16 halves.
+// Deviance: one f64 partial per block (deterministic; the host sums).
+template <int NQ>
+__global__ __launch_bounds__(256) void glm_wide_split_kernel(
+    const float* __restrict__ X, int ldx, int P, int Pa, long long rows, const float* __restrict__ beta, float b0,
+    const float* __restrict__ y, const float* __restrict__ wprior, const float* __restrict__ offset,
+    GlmFamArgs fam, __bf16* __restrict__ HL, double* __restrict__ dev_out) {
+  __shared__ double dsum[4];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  f32x4 b[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const int c = 4 * (lane + 64 * q);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) b[q][e] = c + e < P ? beta[c + e] : 0.f;
+  }
+  double dev = 0.0;
+  const long long nw = (long long)gridDim.x * 4;
+  for (long long r = (long long)blockIdx.x * 4 + wv; r < rows; r += nw) {
+    f32x4 v[NQ];
+    float dot = 0.f;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int c = 4 * (lane + 64 * q);
+      if (c + 3 < P) {
+        v[q] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(X + r * ldx + c));
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[q][e] = c + e < P ? X[r * ldx + c + e] : 0.f;
+      }
+      dot += v[q].x * b[q].x + v[q].y * b[q].y + v[q].z * b[q].z + v[q].w * b[q].w;
+    }
+    dot = wave_sum(dot);
+    const float sy = y[r], sw = wprior ? wprior[r] : 1.f, so = offset ? offset[r] : 0.f;
+    const float eta = dot + b0 + so;
+    const float mu = gi_linkinv(fam.link, eta);
+    float W, z;
+    if (fam.link == 0 && fam.var == 0) {
+      W = sw;
+      z = sy - so;
+    } else {
+      const float d = gi_dmu(fam.link, mu);
+      W = sw * d * d / gi_var(fam, mu);
+      z = (eta - so) + (sy - mu) / d;
+    }
+    if (lane == 0 && sw != 0.f) dev += (double)(sw * gi_dev(fam, sy, mu));
+    const float s = sqrtf(fmaxf(W, 0.f));
+    __bf16* o = HL + r * (2LL * Pa);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int c = 4 * (lane + 64 * q);
+      if (c >= Pa) break;
+      f32x4 a = v[q];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (c + e == P) a[e] = 1.f;
+        if (c + e == P + 1) a[e] = z;
+      }
+      bf16x4 h, l;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float t = a[e] * s;
+        h[e] = (__bf16)t;
+        l[e] = (__bf16)(t - (float)h[e]);
+      }
+      *reinterpret_cast<bf16x4*>(o + c) = h;
+      *reinterpret_cast<bf16x4*>(o + Pa + c) = l;
+    }
+  }
+  dev = wave_sum(dev);
+  if (lane == 0) dsum[wv] = dev;
+  __syncthreads();
+  if (threadIdx.x == 0) dev_out[blockIdx.x] = dsum[0] + dsum[1] + dsum[2] + dsum[3];
+}
+
+// Pa <= 1024 (P <= 1022), Pa % 4 == 0; dev_out holds `blocks` doubles.
+extern "C" int h2o_glm_wide_split(const float* X, int ldx, int P, int Pa, long long rows, const float* beta, float b0,
+                                  const float* y, const float* wprior, const float* offset, int link, int var,
+                                  float tvp, float theta, void* HL, double* dev_out, int blocks, hipStream_t s) {
+  if (rows <= 0) return 0;
+  if (Pa % 4 != 0 || Pa < P + 2 || ldx < P || blocks <= 0) return -1;
+  GlmFamArgs fam{link, var, tvp, theta, 0, 0, 0};
+  if (Pa <= 256)
+    hipLaunchKernelGGL(glm_wide_split_kernel<1>, dim3(blocks), dim3(256), 0, s, X, ldx, P, Pa, rows, beta, b0, y,
+                       wprior, offset, fam, (__bf16*)HL, dev_out);
+  else if (Pa <= 512)
+    hipLaunchKernelGGL(glm_wide_split_kernel<2>, dim3(blocks), dim3(256), 0, s, X, ldx, P, Pa, rows, beta, b0, y,
+                       wprior, offset, fam, (__bf16*)HL, dev_out);
+  else if (Pa <= 1024)
+    hipLaunchKernelGGL(glm_wide_split_kernel<4>, dim3(blocks), dim3(256), 0, s, X, ldx, P, Pa, rows, beta, b0, y,
+                       wprior, offset, fam, (__bf16*)HL, dev_out);
+  else
+    return -2;
   return (int)hipGetLastError();
 }

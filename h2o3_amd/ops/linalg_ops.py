@@ -23,6 +23,8 @@ def _lib():
         P, I, LL, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong, ctypes.c_float
         lib.h2o_glm_irls.argtypes = [P, LL, I, I, P, I, I, I, P, F, P, P, P, I, I, F, F, P, P, I, I, P, P, P]
         lib.h2o_glm_irls_chunk.argtypes = [I]
+        lib.h2o_gram_split.argtypes = [P, I, I, I, P, P, LL, P, P]
+        lib.h2o_glm_wide_split.argtypes = [P, I, I, I, LL, P, F, P, P, P, I, I, F, F, P, P, I, P]
         lib._typed = True
     return lib
 
@@ -146,7 +148,9 @@ def weighted_gram(X: torch.Tensor, w: torch.Tensor | None = None, use_native=Non
         return Xd.T @ (Xd * w.to(torch.float64).view(-1, 1))
     if P <= 512:
         return glm_irls(X, W=w)[0]
-    if os.environ.get("H2O3_WIDE_GRAM", "gemm") == "gemm" and (w is None or bool((w >= 0).all())):
+    if _wide_mode() == "bf3" and (w is None or bool((w >= 0).all())):
+        return gram_aug_bf3(X, w, None, P)[:P, :P]
+    if _wide_mode() == "gemm" and (w is None or bool((w >= 0).all())):
         # wide designs: a plain library GEMM (rocBLAS/hipBLASLt fp32, 136 TFLOP/s at
         # N=12.5M, P=1024 vs 24 for the 32x32 tile-pair kernel, scripts/glm_wide_mb.py)
         # over 1M-row chunks of sqrt(W)-scaled rows, accumulated in f64
@@ -177,6 +181,81 @@ def weighted_gram(X: torch.Tensor, w: torch.Tensor | None = None, use_native=Non
     return _assemble(out.sum(0), pairs_t, T)
 
 
+def _wide_mode():
+    return os.environ.get("H2O3_WIDE_GRAM", "bf3")
+
+
+def gram_aug_bf3(X, W, z, P, step=1 << 19):
+    """Augmented Gram of sqrt(W) [X[:, :P] | 1 | z] (z may be None) as
+    [Pa, Pa] f64, Pa = round_up(P + 2, 64): per row chunk one HIP pass
+    (gram_split_kernel) writes [hi | lo] bf16 halves and one bf16 GEMM with
+    f32 output, C = hi^T [hi | lo], gives hi'hi + hi'lo + (hi'lo)^T."""
+    lib = _lib()
+    if lib is None:
+        raise RuntimeError("gram extension not built (run __graft_entry__.build())")
+    N, ldx = X.shape
+    X = X.contiguous()
+    Pa = -(-(P + 2) // 64) * 64
+    W32, z32 = _f32(W), _f32(z)
+    st = min(step, max(N, 1))
+    HL = torch.empty((st, 2 * Pa), dtype=torch.bfloat16, device=X.device)
+    G = torch.zeros((Pa, Pa), dtype=torch.float64, device=X.device)
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    for a in range(0, N, st):
+        r = min(st, N - a)
+        rc = lib.h2o_gram_split(ctypes.c_void_p(X.data_ptr() + a * ldx * 4), ldx, P, Pa,
+                                ctypes.c_void_p(0 if W32 is None else W32.data_ptr() + a * 4),
+                                ctypes.c_void_p(0 if z32 is None else z32.data_ptr() + a * 4), r, _ptr(HL), stream)
+        if rc != 0:
+            raise RuntimeError(f"h2o_gram_split failed: {rc}")
+        H = HL[:r]
+        C = torch.mm(H[:, :Pa].T, H, out_dtype=torch.float32)
+        G += C[:, :Pa].to(torch.float64)
+        cross = C[:, Pa:].to(torch.float64)
+        G += cross + cross.T
+    return G
+
+
+def glm_wide_irls(X, P, beta, b0, y, wprior=None, offset=None, codes=(1, 1), tvp=0.0, theta=1e-10, step=1 << 19):
+    """Fused IRLS pass for wide GLMs (P + 2 <= 1024): per row chunk one HIP
+    kernel (glm_wide_split_kernel: eta, IRLS weight, working response,
+    deviance, bf16 [hi | lo] split of sqrt(W) [x | 1 | z]) and one bf16 GEMM
+    with f32 output.  Returns (G [Pa, Pa] f64 augmented Gram, deviance f64)."""
+    lib = _lib()
+    if lib is None:
+        raise RuntimeError("gram extension not built (run __graft_entry__.build())")
+    N, ldx = X.shape
+    X = X.contiguous()
+    Pa = -(-(P + 2) // 64) * 64
+    if Pa > 1024:
+        raise ValueError("glm_wide_irls: P + 2 must be <= 1024")
+    bt = _f32(beta)
+    keep = [_f32(y), _f32(wprior), _f32(offset)]
+    st = min(step, max(N, 1))
+    HL = torch.empty((st, 2 * Pa), dtype=torch.bfloat16, device=X.device)
+    blocks = 2048
+    dev = torch.zeros((-(-N // st), blocks), dtype=torch.float64, device=X.device)
+    G = torch.zeros((Pa, Pa), dtype=torch.float64, device=X.device)
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+    def off(t, a):
+        return ctypes.c_void_p(0 if t is None else t.data_ptr() + a * 4)
+
+    for i, a in enumerate(range(0, N, st)):
+        r = min(st, N - a)
+        rc = lib.h2o_glm_wide_split(ctypes.c_void_p(X.data_ptr() + a * ldx * 4), ldx, P, Pa, r, _ptr(bt),
+                                    float(b0), off(keep[0], a), off(keep[1], a), off(keep[2], a), int(codes[0]),
+                                    int(codes[1]), float(tvp), float(theta), _ptr(HL), _ptr(dev[i]), blocks, stream)
+        if rc != 0:
+            raise RuntimeError(f"h2o_glm_wide_split failed: {rc}")
+        H = HL[:r]
+        C = torch.mm(H[:, :Pa].T, H, out_dtype=torch.float32)
+        G += C[:, :Pa].to(torch.float64)
+        cross = C[:, Pa:].to(torch.float64)
+        G += cross + cross.T
+    return G, dev.sum()
+
+
 def weighted_gram_aug(X: torch.Tensor, W: torch.Tensor, z: torch.Tensor, P: int, step: int = 1 << 20):
     """Augmented weighted Gram of [X[:, :P] | 1 | z] for wide GLMs in ONE
     library GEMM per 1M-row chunk (rocBLAS/hipBLASLt fp32, f64 accumulation):
@@ -185,6 +264,9 @@ def weighted_gram_aug(X: torch.Tensor, W: torch.Tensor, z: torch.Tensor, P: int,
     rate on ROCm (~475 ms vs the Gram's ~240 ms at N=12.5M, P=1000), riding
     them on the Gram as two extra columns costs ~0.2%."""
     N = X.shape[0]
+    if X.device.type == "cuda" and _wide_mode() == "bf3":
+        G = gram_aug_bf3(X, W, z, P)
+        return G[:P, :P], G[:P, P], G[:P, P + 1], G[P, P], G[P, P + 1]
     G = torch.zeros((P + 2, P + 2), dtype=torch.float64, device=X.device)
     for a in range(0, N, step):
         s = W[a:a + step].to(torch.float32).clamp_min(0).sqrt()

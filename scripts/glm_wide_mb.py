@@ -64,6 +64,17 @@ def bf16x3_out32():
     return G
 
 
+def bf3_split():
+    return linalg_ops.gram_aug_bf3(X, w, None, P - 2)[: P - 2, : P - 2]
+
+
+def fp32_aug():
+    return fp32()[: P - 2, : P - 2]
+
+
+timeit("fp32 GEMM (aug width)", fp32_aug)
+timeit("bf16 hi|lo split + 1 GEMM (HIP+hipBLASLt)", bf3_split)
+ref = None
 timeit("fp64 ref (X'WX via fp32 GEMM)", fp32)
 timeit("HIP weighted_gram (32x32 tiles)", hip)
 try:

@@ -85,3 +85,26 @@ def test_hglm_random_intercepts():
     assert m._output["varfix"] == pytest.approx(1.0, abs=0.1)
     ue = np.array([m.coefs_random()["g"][f"G{i}"] for i in range(G)])
     assert np.corrcoef(u, ue)[0, 1] > 0.99
+
+
+def test_native_cd_matches_python_cd():
+    """C++ coordinate descent (native/glm_solver.cpp) == the reference-style
+    Python CD on a penalised, boxed quadratic."""
+    import numpy as np
+    from h2o3_amd.models.glm import glm as glm_mod
+    rng = np.random.default_rng(0)
+    P = 40
+    A = rng.standard_normal((400, P))
+    G = A.T @ A / 400
+    b = rng.standard_normal(P)
+    lo = np.full(P, -0.3)
+    hi = np.full(P, 0.5)
+    nat = glm_mod._solve_quadratic(G, b, 0.05, 0.01, True, lower=lo, upper=hi)
+    cd = glm_mod._CD[:]
+    try:
+        glm_mod._CD[:] = [None]
+        py = glm_mod._solve_quadratic(G, b, 0.05, 0.01, True, lower=lo, upper=hi)
+    finally:
+        glm_mod._CD[:] = cd
+    assert np.abs(nat - py).max() < 1e-7
+    assert (nat == 0).sum() > 0 and nat.min() >= -0.3 - 1e-12 and nat[:-1].max() <= 0.5 + 1e-12

@@ -156,3 +156,46 @@ def test_glm_irls_narrow_rows(fused):
     torch.testing.assert_close(Gn, Gp, rtol=1e-9, atol=1e-9)
     if fused:
         torch.testing.assert_close(dn, dp, rtol=1e-9, atol=1e-9)
+
+
+@pytest.mark.parametrize("family,link", [("binomial", "logit"), ("poisson", "log"), ("gaussian", "identity")])
+def test_glm_wide_irls_matches_fp64(family, link):
+    """Fused wide pass (eta + family + bf16 hi/lo split + one bf16 GEMM) vs
+    the fp64 reference, P = 601 (odd width: scalar tail loads)."""
+    n, P, Pp = 40_009, 601, 640
+    X, beta, g = _data(n, P, Pp, seed=17)
+    beta *= 0.3
+    eta = X @ beta - 0.2
+    if family == "binomial":
+        y = (torch.rand(n, generator=g) < torch.sigmoid(eta)).float()
+    elif family == "gaussian":
+        y = eta + torch.randn(n, generator=g)
+    else:
+        y = torch.distributions.Poisson(torch.exp(eta.clamp(max=3))).sample()
+    w = torch.rand(n, generator=g) + 0.5
+    off = 0.1 * torch.randn(n, generator=g)
+    fam = _Fam(family, link)
+    codes = linalg_ops.glm_fused_codes(family, link)
+    Xn = X[:, :P].contiguous()
+    Gk, dk = linalg_ops.glm_wide_irls(Xn.cuda(), P, beta[:P].cuda(), -0.2, y.cuda(), w.cuda(), off.cuda(), codes,
+                                      step=16_384)
+    Gr, dr = linalg_ops.glm_irls_reference(X, aug=P, beta=beta, b0=-0.2, y=y, wprior=w, offset=off, fam=fam)
+    A, B = Gk[: P + 2, : P + 2].cpu(), Gr[: P + 2, : P + 2]
+    diag = B.diagonal().abs().sqrt().clamp_min(1e-12)
+    rel = (A - B).abs() / (diag.view(-1, 1) * diag.view(1, -1))
+    assert rel.max().item() < 5e-5
+    assert abs(dk.item() - dr.item()) / abs(dr.item()) < 1e-4
+
+
+def test_gram_aug_bf3_matches_fp64():
+    n, P = 30_011, 700
+    g = torch.Generator().manual_seed(4)
+    X = torch.randn(n, P, generator=g)
+    W = torch.rand(n, generator=g)
+    z = torch.randn(n, generator=g)
+    G = linalg_ops.gram_aug_bf3(X.cuda(), W.cuda(), z.cuda(), P, step=8192).cpu()
+    A = torch.cat([X.double(), torch.ones(n, 1, dtype=torch.float64), z.double().view(-1, 1)], 1)
+    R = A.T @ (A * W.double().view(-1, 1))
+    diag = R.diagonal().sqrt()
+    rel = (G[: P + 2, : P + 2] - R).abs() / (diag.view(-1, 1) * diag.view(1, -1))
+    assert rel.max().item() < 5e-5
