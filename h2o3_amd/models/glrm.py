@@ -73,6 +73,18 @@ def _reg(name, M):
     raise ValueError(f"unknown regularizer {name}")
 
 
+def _reg_rows(name, M):
+    """Per-row regularizer values (rows of X are independent at scoring)."""
+    n = (name or "None").lower()
+    if n == "quadratic":
+        return (M * M).sum(1)
+    if n == "l2":
+        return torch.sqrt((M * M).sum(1))
+    if n == "l1":
+        return M.abs().sum(1)
+    return M.new_zeros((M.shape[0],))
+
+
 def _prox(name, M, step_gamma):
     n = (name or "None").lower()
     if n == "none":
@@ -163,21 +175,21 @@ class H2OGeneralizedLowRankEstimator(H2OEstimator):
         M = torch.cat(masks, 1).to(torch.float32) if masks else torch.zeros_like(A)
         return A, M, blocks
 
-    def _loss(self, A, M, U, blocks):
+    def _loss(self, A, M, U, blocks, per_row=False):
         p = self._parms
         lbc = {}
         if p.get("loss_by_col"):
             idx = p.get("loss_by_col_idx") or []
             for name, i in zip(p["loss_by_col"], idx):
                 lbc[self._cols[i] if isinstance(i, int) else i] = name
-        tot = U.new_zeros(())
+        tot = U.new_zeros((U.shape[0],))
         j = 0
         ml = str(p.get("multi_loss") or "Categorical").lower()
         for kind, c, w in blocks:
             a, m, u = A[:, j:j + w], M[:, j:j + w], U[:, j:j + w]
             if kind == "num":
                 L = _num_loss(lbc.get(c, p.get("loss") or "Quadratic"), a, u, float(p.get("period", 1)))
-                tot = tot + (L * m).sum()
+                tot = tot + (L * m)[:, 0]
             else:
                 rowm = m[:, 0]
                 if ml == "ordinal":
@@ -186,9 +198,9 @@ class H2OGeneralizedLowRankEstimator(H2OEstimator):
                     L = torch.where(ar < lvl, torch.clamp(1 - u, min=0), torch.clamp(1 + u, min=0))
                 else:  # Categorical one-vs-all hinge
                     L = torch.where(a > 0, torch.clamp(1 - u, min=0), torch.clamp(1 + u, min=0))
-                tot = tot + (L.sum(1) * rowm).sum()
+                tot = tot + L.sum(1) * rowm
             j += w
-        return tot
+        return tot if per_row else tot.sum()
 
     # ------------------------------------------------------------ fit
     def _fit(self, spec):
@@ -307,32 +319,46 @@ class H2OGeneralizedLowRankEstimator(H2OEstimator):
                                   [f"Arch{i + 1}" for i in range(X.shape[1])])
 
     # ------------------------------------------------------------ scoring
-    def _solve_x(self, frame, iters=2000):
+    def _solve_x(self, frame, iters=None):
+        """Rows of X for new data with Y fixed, every row independent like the
+        reference's per-row scorer (hex/genmodel/algos/glrm/GlrmMojoModel.java
+        score0): proximal gradient with a per-row step that grows 1.05x after
+        an improving step and halves otherwise; a row stops when its relative
+        improvement drops below 1e-9 or its step below 1e-8.  Vectorised over
+        all rows on the device; the MOJO scorer (mojo/genmodel.py) runs the
+        same recurrence in numpy."""
         A, M, blocks = self._layout(frame, self._cols)
         Y = self._Y.detach()
         p = self._parms
         rx, gx = p.get("regularization_x"), float(p.get("gamma_x", 0.0))
-        scale = 1.0 / max(A.shape[0], 1)
-        # start from the regularizer-feasible least-squares point with the
-        # training run's final (adapted) step size
+        iters = int(iters or self._score_iters())
+        n = A.shape[0]
         X = _prox(rx, self._init_x(A, M, Y, None), 0.0)
-        step = max(float(getattr(self, "_step", 1.0)), 1e-3) * 4
-        obj = float(self._loss(A, M, X @ Y, blocks)) + gx * float(_reg(rx, X))
+        step = torch.full((n, 1), self._score_step(), dtype=X.dtype, device=X.device)
+        obj = self._loss(A, M, X @ Y, blocks, per_row=True) + gx * _reg_rows(rx, X)
+        live = torch.ones(n, dtype=torch.bool, device=X.device)
         for _ in range(iters):
             Xv = X.clone().requires_grad_(True)
             gX, = torch.autograd.grad(self._loss(A, M, Xv @ Y, blocks), Xv)
-            Xn = _prox(rx, X - step * scale * gX, step * scale * gx)
-            on = float(self._loss(A, M, Xn @ Y, blocks)) + gx * float(_reg(rx, Xn))
-            if on < obj:
-                rel = (obj - on) / max(abs(obj), 1e-300)
-                X, obj, step = Xn, on, step * 1.05
-                if rel < 1e-9:
-                    break
-            else:
-                step /= 2
-                if step < 1e-8:
-                    break
-        return X, A, M
+            Xn = _prox(rx, X - step * gX, step * gx)
+            on = self._loss(A, M, Xn @ Y, blocks, per_row=True) + gx * _reg_rows(rx, Xn)
+            better = (on < obj) & live
+            rel = (obj - on) / obj.abs().clamp_min(1e-300)
+            X = torch.where(better.view(-1, 1), Xn, X)
+            obj = torch.where(better, on, obj)
+            step = torch.where(better.view(-1, 1), step * 1.05, torch.where(live.view(-1, 1), step / 2, step))
+            live = live & ~(better & (rel < 1e-9)) & (step.view(-1) >= 1e-8)
+            if not bool(live.any()):
+                break
+        return X.detach(), A, M
+
+    def _score_step(self):
+        # 1 / (2 ||Y||_F^2) bounds the quadratic loss's curvature in x: a
+        # descent step for every row from the first iteration
+        return 0.5 / max(float((self._Y.detach().double() ** 2).sum()), 1e-12)
+
+    def _score_iters(self):
+        return 2000
 
     def _reconstruct(self, X):
         p = self._parms

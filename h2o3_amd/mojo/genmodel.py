@@ -289,6 +289,8 @@ class MojoModel:
             else:
                 mu = eta
             return np.stack([1 - mu, mu], 1) if self.nclasses == 2 else mu.reshape(-1, 1)
+        if a == "glrm":
+            return self._glrm_reconstruct(df)
         if a == "kmeans":
             X = self._expand(df)
             C = self._arr["centers_std"]
@@ -427,9 +429,197 @@ class MojoModel:
             return self._meta_model.predict_raw(pd.DataFrame(cols))
         raise NotImplementedError(a)
 
+    # ---------------------------------------------------------------- GLRM
+    def _glrm_layout(self, df):
+        g = self.meta["glrm"]
+        mats, masks = [], []
+        for kind, c, w in g["blocks"]:
+            if kind == "cat":
+                codes = self._col(df, c, g["doms"][c])
+                ok = ~np.isnan(codes)
+                oh = np.zeros((len(codes), w))
+                oh[np.nonzero(ok)[0], codes[ok].astype(int)] = 1.0
+                mats.append(oh)
+                masks.append(np.repeat(ok.reshape(-1, 1), w, 1))
+            else:
+                x = self._col(df, c)
+                mu, sd, lo, hi = g["stats"][c]
+                tr = g["transform"]
+                if tr == "STANDARDIZE":
+                    x = (x - mu) / sd
+                elif tr == "NORMALIZE":
+                    x = (x - lo) / max(hi - lo, 1e-12)
+                elif tr == "DEMEAN":
+                    x = x - mu
+                elif tr == "DESCALE":
+                    x = x / sd
+                masks.append((~np.isnan(x)).reshape(-1, 1))
+                mats.append(np.nan_to_num(x).reshape(-1, 1))
+        return np.concatenate(mats, 1), np.concatenate(masks, 1).astype(np.float64)
+
+    def _glrm_loss_grad(self, A, M, U, want_grad=True):
+        """Per-row loss and dLoss/dU (hex/genmodel/algos/glrm/GlrmLoss.java)."""
+        g = self.meta["glrm"]
+        tot = np.zeros(U.shape[0])
+        G = np.zeros_like(U) if want_grad else None
+        j = 0
+        ml = g["multi_loss"].lower()
+        for kind, c, w in g["blocks"]:
+            a, m, u = A[:, j:j + w], M[:, j:j + w], U[:, j:j + w]
+            if kind == "num":
+                name = g["loss_by_col"].get(c, g["loss"]).lower()
+                a, m, u = a[:, 0], m[:, 0], u[:, 0]
+                d = u - a
+                if name == "quadratic":
+                    L, dL = d * d, 2 * d
+                elif name == "absolute":
+                    L, dL = np.abs(d), np.sign(d)
+                elif name == "huber":
+                    ad = np.abs(d)
+                    L = np.where(ad <= 1, 0.5 * ad * ad, ad - 0.5)
+                    dL = np.where(ad <= 1, d, np.sign(d))
+                elif name == "poisson":
+                    L = np.exp(u) - a * u + np.where(a > 0, a * np.log(np.maximum(a, 1e-300)) - a, 0.0)
+                    dL = np.exp(u) - a
+                elif name in ("hinge", "logistic"):
+                    aa = np.where(a > 0, 1.0, -1.0)
+                    if name == "hinge":
+                        L = np.maximum(1 - aa * u, 0)
+                        dL = np.where(1 - aa * u >= 0, -aa, 0.0)
+                    else:
+                        L = np.logaddexp(0, -aa * u)
+                        dL = -aa / (1 + np.exp(aa * u))
+                elif name == "periodic":
+                    cc = 2 * math.pi / g["period"]
+                    L = 1 - np.cos((a - u) * cc)
+                    dL = -cc * np.sin((a - u) * cc)
+                else:
+                    raise ValueError(name)
+                tot += L * m
+                if want_grad:
+                    G[:, j] = dL * m
+            else:
+                rowm = m[:, 0]
+                if ml == "ordinal":
+                    lvl = a.argmax(1).reshape(-1, 1)
+                    below = np.arange(w).reshape(1, -1) < lvl
+                else:
+                    below = a > 0
+                L = np.where(below, np.maximum(1 - u, 0), np.maximum(1 + u, 0))
+                tot += L.sum(1) * rowm
+                if want_grad:
+                    G[:, j:j + w] = np.where(below, np.where(1 - u >= 0, -1.0, 0.0),
+                                             np.where(1 + u >= 0, 1.0, 0.0)) * rowm.reshape(-1, 1)
+            j += w
+        return tot, G
+
+    @staticmethod
+    def _glrm_reg(name, X):
+        n = (name or "None").lower()
+        if n == "quadratic":
+            return (X * X).sum(1)
+        if n == "l2":
+            return np.sqrt((X * X).sum(1))
+        if n == "l1":
+            return np.abs(X).sum(1)
+        return np.zeros(X.shape[0])
+
+    @staticmethod
+    def _glrm_prox(name, X, sg):
+        n = (name or "None").lower()
+        if n == "none":
+            return X
+        if n == "quadratic":
+            return X / (1 + 2 * sg)
+        if n == "l2":
+            nr = np.maximum(np.sqrt((X * X).sum(1, keepdims=True)), 1e-300)
+            return X * np.maximum(1 - sg / nr, 0)
+        if n == "l1":
+            return np.sign(X) * np.maximum(np.abs(X) - sg, 0)
+        if n == "nonnegative":
+            return np.maximum(X, 0)
+        if n in ("onesparse", "unitonesparse"):
+            idx = X.argmax(1)
+            out = np.zeros_like(X)
+            r = np.arange(X.shape[0])
+            out[r, idx] = np.maximum(X[r, idx], 0) if n == "onesparse" else 1.0
+            return out
+        if n == "simplex":
+            u = -np.sort(-X, 1)
+            css = np.cumsum(u, 1) - 1
+            ind = np.arange(1, X.shape[1] + 1)
+            rho = ((u - css / ind) > 0).cumsum(1).argmax(1)
+            theta = css[np.arange(X.shape[0]), rho] / (rho + 1)
+            return np.maximum(X - theta.reshape(-1, 1), 0)
+        raise ValueError(name)
+
+    def _glrm_solve_x(self, A, M):
+        """Per-row proximal gradient on x with Y fixed (same recurrence as the
+        in-cluster GLRM predict: least-squares start, 1/(2||Y||^2) first step,
+        x1.05 on improvement, /2 otherwise)."""
+        g = self.meta["glrm"]
+        Y = self._arr["Y"]
+        k = Y.shape[0]
+        rx, gx = g["regularization_x"], g["gamma_x"]
+        Gm = Y @ Y.T + 1e-6 * np.eye(k)
+        X = self._glrm_prox(rx, np.linalg.solve(Gm, Y @ (A * M).T).T, 0.0)
+        n = X.shape[0]
+        step = np.full((n, 1), 0.5 / max(float((Y * Y).sum()), 1e-12))
+        obj = self._glrm_loss_grad(A, M, X @ Y, False)[0] + gx * self._glrm_reg(rx, X)
+        live = np.ones(n, dtype=bool)
+        for _ in range(int(g["iters"])):
+            gX = self._glrm_loss_grad(A, M, X @ Y)[1] @ Y.T
+            Xn = self._glrm_prox(rx, X - step * gX, step * gx)
+            on = self._glrm_loss_grad(A, M, Xn @ Y, False)[0] + gx * self._glrm_reg(rx, Xn)
+            better = (on < obj) & live
+            rel = (obj - on) / np.maximum(np.abs(obj), 1e-300)
+            X = np.where(better.reshape(-1, 1), Xn, X)
+            obj = np.where(better, on, obj)
+            step = np.where(better.reshape(-1, 1), step * 1.05, np.where(live.reshape(-1, 1), step / 2, step))
+            live = live & ~(better & (rel < 1e-9)) & (step.reshape(-1) >= 1e-8)
+            if not live.any():
+                break
+        return X
+
+    def _glrm_reconstruct(self, df):
+        A, M = self._glrm_layout(df)
+        X = self._glrm_solve_x(A, M)
+        self._glrm_x = X
+        return X @ self._arr["Y"]
+
+    def glrm_reconstruct(self, df):
+        """DataFrame of reconstr_<col> like GLRM predict()/reconstruct()."""
+        import pandas as pd
+        g = self.meta["glrm"]
+        U = self._glrm_reconstruct(df)
+        out = {}
+        j = 0
+        for kind, c, w in g["blocks"]:
+            u = U[:, j:j + w]
+            if kind == "num":
+                x = u[:, 0].copy()
+                if g["impute_original"]:
+                    mu, sd, lo, hi = g["stats"][c]
+                    tr = g["transform"]
+                    if tr == "STANDARDIZE":
+                        x = x * sd + mu
+                    elif tr == "NORMALIZE":
+                        x = x * (hi - lo) + lo
+                    elif tr == "DEMEAN":
+                        x = x + mu
+                    elif tr == "DESCALE":
+                        x = x * sd
+                out[f"reconstr_{c}"] = x
+            else:
+                out[f"reconstr_{c}"] = np.array(g["doms"][c], dtype=object)[u.argmax(1)]
+            j += w
+        return pd.DataFrame(out)
+
     def predict(self, df):
         """Returns a pandas DataFrame shaped like the in-cluster predict()."""
         import pandas as pd
+        if self.algo == "glrm":
+            return self.glrm_reconstruct(df)
         raw = self.predict_raw(df)
         if self.algo == "isolationforest":
             return pd.DataFrame({"predict": raw[:, 0], "mean_length": raw[:, 1]})

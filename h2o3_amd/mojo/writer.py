@@ -155,6 +155,22 @@ def build_mojo(model) -> bytes:
             w.meta["family"] = model._fam.family
             w.meta["link"] = model._fam.link
             w.meta["tlp"] = model._fam.tlp
+    elif algo == "glrm":
+        p = model._parms
+        lbc = {}
+        if p.get("loss_by_col"):
+            for name, i in zip(p["loss_by_col"], p.get("loss_by_col_idx") or []):
+                lbc[model._cols[i] if isinstance(i, int) else i] = name
+        w.meta["glrm"] = {"blocks": [list(b) for b in model._blocks], "doms": model._doms,
+                          "stats": {c: list(v) for c, v in model._stats.items()},
+                          "transform": str(p.get("transform") or "NONE").upper(),
+                          "loss": p.get("loss") or "Quadratic", "loss_by_col": lbc,
+                          "multi_loss": str(p.get("multi_loss") or "Categorical"), "period": float(p.get("period", 1)),
+                          "regularization_x": p.get("regularization_x") or "None",
+                          "gamma_x": float(p.get("gamma_x", 0.0)), "impute_original": bool(p.get("impute_original")),
+                          "iters": int(model._score_iters())}
+        w.meta["x_domains"] = model._doms
+        w.add_array("Y", model._Y.detach().cpu().numpy().astype(np.float64))
     elif algo == "kmeans":
         _dinfo_meta(w, model._dinfo)
         w.add_array("centers_std", model._C_std.cpu().numpy())
