@@ -83,6 +83,7 @@ def main():
     fr = H2OFrame.from_vecs(vecs, names + ["y"])
     from h2o3_amd.models.base import TrainSpec
 
+    extra_cfg = {}
     if args.algo == "gbm":
         from h2o3_amd.models.tree.gbm import GBMDriver, H2OGradientBoostingEstimator
         est = H2OGradientBoostingEstimator(ntrees=500, max_depth=args.max_depth, seed=42,
@@ -116,7 +117,9 @@ def main():
         step = drv.step
         metric = "glm_iters_per_sec"
         unit = "iters/s"
-        model = "GLM binomial IRLSM 100Mx100"
+        model = f"GLM binomial IRLSM {args.rows / 1e6:g}Mx{F}"
+        extra_cfg = {"gram_precision": "bf16x3 split operands (hi*hi + hi*lo + lo*hi) on MFMA, f32 accumulate, "
+                                       "f64 across row blocks"}
 
     def sync():
         torch.cuda.synchronize() if dev.type == "cuda" else None
@@ -162,7 +165,7 @@ def main():
                           **({} if args.algo == "glm" else {"max_depth": est._parms.get("max_depth"),
                                                             "histogram_type": args.histogram_type,
                                                             "nbins": args.nbins}),
-                          "global_batch": args.rows, "seq_len": None, "parallelism": f"dp{world}"},
+                          "global_batch": args.rows, "seq_len": None, "parallelism": f"dp{world}", **extra_cfg},
                **extra}
         print(json.dumps(out))
 
