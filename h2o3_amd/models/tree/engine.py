@@ -350,7 +350,9 @@ class TreeGrower:
         (mtries / column sampling usually leave a few per node): levels sorted
         by mean response per pair (DTree.findBestSplitPoint for categoricals),
         prefix sums, the three NA options, best pair per node by a segment
-        arg-max (lowest feature on ties)."""
+        arg-max (lowest feature on ties).  On the GPU every pair is one
+        workgroup of the HIP kernel `cat_pair_kernel` (tree_split.hip); the
+        winners' split masks are then rebuilt from their own bins."""
         p = self.p
         Fl, n, Bs, C = H.shape
         B = Bs - 1
@@ -370,11 +372,61 @@ class TreeGrower:
             return out
         node_i, j = nz[:, 0], nz[:, 1]
         P = node_i.numel()
-        h = H[sub_t[j], node_i].to(torch.float64)                 # [P, Bs, C]
-        bins, na = h[:, :B], h[:, B]
         xgb = p.criterion == "xgb"
         pcat = self.is_cat_t[gidx[j]]                              # numeric pairs keep bin order
-        if xgb:
+        mono_p = self.mono_t[gidx[j]]
+        if dev.type == "cuda" and C >= 2 and B <= 4096 and H.dtype == torch.float64:
+            best, k = self._pairs_native(H, sub_t[j], node_i, pcat, mono_p, node_wyy)
+        else:
+            st = self._pair_stats(H[sub_t[j], node_i].to(torch.float64), pcat)
+            allg = self._pair_gains(st, mono_p.view(-1, 1), node_wyy, node_i)
+            best, k = allg.max(1)
+        node_best = ninf.clone().scatter_reduce(0, node_i, best, reduce="amax", include_self=True)
+        cand = torch.where((best == node_best[node_i]) & torch.isfinite(best), torch.arange(P, device=dev),
+                           torch.full((P,), P, device=dev))
+        win = torch.full((n,), P, dtype=torch.long, device=dev).scatter_reduce(0, node_i, cand, reduce="amin",
+                                                                              include_self=True)
+        has = win < P
+        if not bool(has.any()):
+            return out
+        nodes = torch.nonzero(has).flatten()
+        wp = win[nodes]
+        # the winners' sorted order / prefix sums, from their own bins only
+        st = self._pair_stats(H[sub_t[j[wp]], node_i[wp]].to(torch.float64), pcat[wp])
+        h, order, L, totnn, na, T = st["h"], st["order"], st["L"], st["totnn"], st["na"], st["T"]
+        nt = B - 1
+        kk = k[wp]
+        opt = torch.where(kk < nt, torch.zeros_like(kk), torch.where(kk < 2 * nt, torch.ones_like(kk),
+                                                                     torch.full_like(kk, 2)))
+        t = torch.where(opt == 0, kk, torch.where(opt == 1, kk - nt, torch.zeros_like(kk)))
+        na_left = opt == 1
+        ar = torch.arange(wp.numel(), device=dev)
+        Lw = torch.where((opt == 2).view(-1, 1), totnn,
+                         L[ar, t.clamp(max=nt - 1)] + torch.where(na_left.view(-1, 1), na, torch.zeros_like(na)))
+        rank = torch.empty_like(order)
+        rank.scatter_(1, order, torch.arange(B, device=dev).view(1, B).expand(order.shape[0], B))
+        in_left = rank <= t.view(-1, 1)
+        bw = h[:, :B, 1] if xgb else h[:, :B, 0]
+        empty = (bw <= 0) & pcat[wp].view(-1, 1)     # empty categorical levels follow the NAs
+        in_left = torch.where(empty, na_left.view(-1, 1).expand_as(in_left), in_left)
+        in_left = torch.where((opt == 2).view(-1, 1), ~empty | na_left.view(-1, 1), in_left)
+        mask = torch.cat([in_left, na_left.view(-1, 1).expand(-1, Bs - B)], 1).to(torch.uint8)
+        out["gain"] = out["gain"].index_put((nodes,), best[wp])
+        out["feat"] = out["feat"].index_put((nodes,), gidx[j[wp]])
+        out["t"] = out["t"].index_put((nodes,), t)
+        out["opt"] = out["opt"].index_put((nodes,), opt)
+        out["na_left"] = out["na_left"].index_put((nodes,), na_left)
+        out["mask"] = out["mask"].index_put((nodes,), mask)
+        out["L"] = out["L"].index_put((nodes,), Lw)
+        out["R"] = out["R"].index_put((nodes,), T - Lw)
+        return out
+
+    def _pair_stats(self, h, pcat):
+        """Sorted order and prefix sums of pair histograms h [P, Bs, C] f64."""
+        B = h.shape[1] - 1
+        dev = h.device
+        bins, na = h[:, :B], h[:, B]
+        if self.p.criterion == "xgb":
             key = torch.where(bins[..., 1] > 0, bins[..., 0] / bins[..., 1].clamp_min(1e-300),
                               torch.full_like(bins[..., 0], float("inf")))
         else:
@@ -382,14 +434,20 @@ class TreeGrower:
                               torch.full_like(bins[..., 0], float("inf")))
         key = torch.where(pcat.view(-1, 1), key, torch.arange(B, device=dev, dtype=key.dtype).view(1, B))
         order = torch.argsort(key, dim=1, stable=True)             # [P, B]
-        mono = self.mono_t[gidx[j]].view(-1, 1)
-        bs_ = torch.gather(bins, 1, order.unsqueeze(-1).expand(-1, -1, C))
+        bs_ = torch.gather(bins, 1, order.unsqueeze(-1).expand(-1, -1, h.shape[2]))
         cum = torch.cumsum(bs_, 1)
         totnn = cum[:, -1]
         L = cum[:, :-1]
-        R = totnn.unsqueeze(1) - L
-        T = totnn + na
+        return {"h": h, "na": na, "order": order, "L": L, "totnn": totnn, "R": totnn.unsqueeze(1) - L,
+                "T": totnn + na}
+
+    def _pair_gains(self, st, mono, node_wyy, node_i):
+        """[P, 2(B-1)+1] gains of every threshold x NA option (torch path)."""
+        p = self.p
+        xgb = p.criterion == "xgb"
+        L, R, totnn, na, T = st["L"], st["R"], st["totnn"], st["na"], st["T"]
         naE = na.unsqueeze(1)
+        P = L.shape[0]
 
         def score(S):
             if xgb:
@@ -427,50 +485,42 @@ class TreeGrower:
         gC = torch.where(has_na.unsqueeze(1), gC, torch.full_like(gC, NEG_INF))
         allg = torch.cat([gA, gB, gC], 1)                          # [P, 2(B-1)+1]
         if xgb:
-            allg = torch.where(allg > 0, allg, torch.full_like(allg, NEG_INF))
-        else:
-            wyy = node_wyy.to(torch.float64)[node_i].view(-1, 1) if node_wyy is not None else \
-                torch.zeros((P, 1), dtype=torch.float64, device=dev)
-            se_before = (wyy - score(T).unsqueeze(1)).clamp_min(0)
-            allg = torch.where((allg > se_before * p.min_split_improvement) & (se_before > 0), allg,
-                               torch.full_like(allg, NEG_INF))
-        best, k = allg.max(1)
-        node_best = ninf.clone().scatter_reduce(0, node_i, best, reduce="amax", include_self=True)
-        cand = torch.where((best == node_best[node_i]) & torch.isfinite(best), torch.arange(P, device=dev),
-                           torch.full((P,), P, device=dev))
-        win = torch.full((n,), P, dtype=torch.long, device=dev).scatter_reduce(0, node_i, cand, reduce="amin",
-                                                                              include_self=True)
-        has = win < P
-        if not bool(has.any()):
-            return out
-        nodes = torch.nonzero(has).flatten()
-        wp = win[nodes]
-        nt = B - 1
-        kk = k[wp]
-        opt = torch.where(kk < nt, torch.zeros_like(kk), torch.where(kk < 2 * nt, torch.ones_like(kk),
-                                                                     torch.full_like(kk, 2)))
-        t = torch.where(opt == 0, kk, torch.where(opt == 1, kk - nt, torch.zeros_like(kk)))
-        na_left = opt == 1
-        Lw = torch.where((opt == 2).view(-1, 1), totnn[wp],
-                         L[wp, t.clamp(max=nt - 1)] + torch.where(na_left.view(-1, 1), na[wp], torch.zeros_like(na[wp])))
-        ordw = order[wp]
-        rank = torch.empty_like(ordw)
-        rank.scatter_(1, ordw, torch.arange(B, device=dev).view(1, B).expand(ordw.shape[0], B))
-        in_left = rank <= t.view(-1, 1)
-        bw = h[wp, :B, 1] if xgb else h[wp, :B, 0]
-        empty = (bw <= 0) & pcat[wp].view(-1, 1)     # empty categorical levels follow the NAs
-        in_left = torch.where(empty, na_left.view(-1, 1).expand_as(in_left), in_left)
-        in_left = torch.where((opt == 2).view(-1, 1), ~empty | na_left.view(-1, 1), in_left)
-        mask = torch.cat([in_left, na_left.view(-1, 1).expand(-1, Bs - B)], 1).to(torch.uint8)
-        out["gain"] = out["gain"].index_put((nodes,), best[wp])
-        out["feat"] = out["feat"].index_put((nodes,), gidx[j[wp]])
-        out["t"] = out["t"].index_put((nodes,), t)
-        out["opt"] = out["opt"].index_put((nodes,), opt)
-        out["na_left"] = out["na_left"].index_put((nodes,), na_left)
-        out["mask"] = out["mask"].index_put((nodes,), mask)
-        out["L"] = out["L"].index_put((nodes,), Lw)
-        out["R"] = out["R"].index_put((nodes,), T[wp] - Lw)
-        return out
+            return torch.where(allg > 0, allg, torch.full_like(allg, NEG_INF))
+        wyy = node_wyy.to(torch.float64)[node_i].view(-1, 1) if node_wyy is not None else \
+            torch.zeros((P, 1), dtype=torch.float64, device=L.device)
+        se_before = (wyy - score(T).unsqueeze(1)).clamp_min(0)
+        return torch.where((allg > se_before * p.min_split_improvement) & (se_before > 0), allg,
+                           torch.full_like(allg, NEG_INF))
+
+    def _pairs_native(self, H, fslot, node_i, pcat, mono_p, node_wyy):
+        """(best gain, k) per pair from the HIP pair kernel."""
+        import ctypes
+        from ...ops import _native
+        p = self.p
+        Fl, n, Bs, C = H.shape
+        lib = _native.get_lib("tree_split")
+        if not getattr(lib, "_typed_pairs", False):
+            cv, ci, cd = ctypes.c_void_p, ctypes.c_int, ctypes.c_double
+            lib.h2o_cat_pairs.argtypes = [cv, ci, ci, ci, ci, cv, cv, cv, cv, cv, cd, cd, cd, cd, cd, ci, cv, cv]
+            lib._typed_pairs = True
+        H = H.contiguous()
+        P = fslot.numel()
+        pf = fslot.to(torch.int32).contiguous()
+        pn = node_i.to(torch.int32).contiguous()
+        pc = pcat.to(torch.uint8).contiguous()
+        pm = mono_p.to(torch.float32).contiguous()
+        wyy = node_wyy.to(torch.float64).contiguous() if node_wyy is not None else None
+        res = torch.empty((P, 2), dtype=torch.float64, device=H.device)
+
+        def ptr(t):
+            return ctypes.c_void_p(0 if t is None else t.data_ptr())
+        rc = lib.h2o_cat_pairs(ptr(H), n, Bs, C, P, ptr(pf), ptr(pn), ptr(pc), ptr(pm), ptr(wyy),
+                               float(p.min_rows), float(p.min_split_improvement), float(p.reg_lambda),
+                               float(p.reg_alpha), float(p.gamma), 1 if p.criterion == "xgb" else 0, ptr(res),
+                               ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+        if rc != 0:
+            raise RuntimeError(f"h2o_cat_pairs failed: {rc}")
+        return res[:, 0].contiguous(), res[:, 1].to(torch.long)
 
     def _find_splits_torch(self, H, col_mask, node_wyy=None, merge=True, sub=None):
         """H: [Fl, n, Bs, C] (local feature slice).  Returns dict of per-node

@@ -287,3 +287,201 @@ extern "C" int h2o_split_select2(const void* rec, const double* H, int Fl, int n
                      stride, pk, mask, feat_out);
   return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------
+// Pair-based categorical split search (DTree.findBestSplitPoint for enum
+// columns: levels ordered by mean response, then the ordered prefix splits).
+// One workgroup per eligible (node, feature) pair -- with mtries / column
+// sampling only a few features per node are eligible, so pairs, not the full
+// [node x feature] grid, are the unit of work.  The pair's bins are read
+// straight out of the level histogram H [Fl][n][Bs][C] (no gathered copy),
+// (key, bin) is bitonic-sorted in LDS (ties by bin index == a stable sort),
+// the sorted channels are prefix-summed in f64, every thread scores its
+// thresholds for the three NA placements and a block arg-max (lowest
+// concatenated index on ties, like torch's max over [A | B | C]) writes
+// (gain, k) per pair.  Numeric pairs keep bin order (no sort).
+// out[2p] = gain (-inf if none), out[2p+1] = k in [0, 2(B-1)].
+// ---------------------------------------------------------------------------
+template <int CRIT, int BP>
+__global__ __launch_bounds__(256) void cat_pair_kernel(const double* __restrict__ H, int n, int Bs, int C,
+                                                       const int* __restrict__ pf, const int* __restrict__ pn,
+                                                       const unsigned char* __restrict__ pcat,
+                                                       const float* __restrict__ pmono,
+                                                       const double* __restrict__ node_wyy, double min_rows,
+                                                       double msi, double lam, double alpha, double gamma,
+                                                       double* __restrict__ out) {
+  __shared__ double sk[BP];   // sort key, then channel-0 prefix sums
+  __shared__ double s1[BP];   // channel-1 prefix sums
+  __shared__ int si[BP];      // bin index (sort payload)
+  __shared__ double red_g[4];
+  __shared__ int red_k[4];
+  const int p = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int B = Bs - 1;
+  const double* h = H + ((size_t)pf[p] * n + pn[p]) * (size_t)Bs * C;
+  const bool cat = pcat[p] != 0;
+  for (int b = tid; b < BP; b += 256) {
+    double key = INFINITY;
+    if (b < B) {
+      if (!cat) {
+        key = (double)b;
+      } else if (CRIT == 1) {
+        const double g = h[(size_t)b * C], hh = h[(size_t)b * C + 1];
+        key = hh > 0 ? g / hh : INFINITY;
+      } else {
+        const double w = h[(size_t)b * C], wy = h[(size_t)b * C + 1];
+        key = w > 0 ? wy / w : INFINITY;
+      }
+    }
+    sk[b] = key;
+    si[b] = b;
+  }
+  __syncthreads();
+  if (cat) {
+    for (int k = 2; k <= BP; k <<= 1) {
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int i = tid; i < BP; i += 256) {
+          const int l = i ^ j;
+          if (l > i) {
+            const double a = sk[i], c = sk[l];
+            const int ia = si[i], ic = si[l];
+            const bool gt = a > c || (a == c && ia > ic);
+            const bool up = (i & k) == 0;
+            if (gt == up) { sk[i] = c; sk[l] = a; si[i] = ic; si[l] = ia; }
+          }
+        }
+        __syncthreads();
+      }
+    }
+  }
+  // gather the sorted channels; per-thread serial prefix over a contiguous run
+  constexpr int PER = BP / 256;
+  double c0[PER], c1[PER];
+  double a0 = 0, a1 = 0;
+#pragma unroll
+  for (int e = 0; e < PER; ++e) {
+    const int b = tid * PER + e;
+    double v0 = 0, v1 = 0;
+    if (b < B) {
+      const int j = si[b];
+      v0 = h[(size_t)j * C];
+      v1 = h[(size_t)j * C + 1];
+    }
+    a0 += v0; a1 += v1;
+    c0[e] = a0; c1[e] = a1;
+  }
+  __syncthreads();
+  // exclusive scan of the per-thread totals (Hillis-Steele over 256 in LDS)
+  sk[tid] = a0; s1[tid] = a1;
+  __syncthreads();
+  for (int d = 1; d < 256; d <<= 1) {
+    const double u0 = tid >= d ? sk[tid - d] : 0.0, u1 = tid >= d ? s1[tid - d] : 0.0;
+    __syncthreads();
+    sk[tid] += u0; s1[tid] += u1;
+    __syncthreads();
+  }
+  const double off0 = tid > 0 ? sk[tid - 1] : 0.0, off1 = tid > 0 ? s1[tid - 1] : 0.0;
+  const double tw = sk[255], ty = s1[255];
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < PER; ++e) {
+    sk[tid * PER + e] = off0 + c0[e];
+    s1[tid * PER + e] = off1 + c1[e];
+  }
+  __syncthreads();
+  const double nw = h[(size_t)B * C], ny = h[(size_t)B * C + 1];
+  const double Tw = tw + nw, Ty = ty + ny;
+  const double sT = score<CRIT>(Tw, Ty, lam, alpha);
+  const bool has_na = CRIT == 1 ? (ny > 0 || nw != 0) : (nw > 0);
+  const double mo = pmono ? (double)pmono[p] : 0.0;
+  double se_before = 0;
+  bool dead = false;
+  if (CRIT == 0) {
+    se_before = fmax((node_wyy ? node_wyy[pn[p]] : 0.0) - sT, 0.0);
+    dead = !(se_before > 0);
+  }
+  const int nt = B - 1;
+  double bg = -INFINITY;
+  int bk = 0x7fffffff;
+  if (!dead) {
+    for (int i = tid; i < nt; i += 256) {
+      const double lw = sk[i], ly = s1[i];
+      const double rw = tw - lw, ry = ty - ly;
+      {
+        const double RW = rw + nw, RY = ry + ny;
+        if (valid_split<CRIT>(lw, ly, RW, RY, min_rows, lam, mo)) {
+          double g = score<CRIT>(lw, ly, lam, alpha) + score<CRIT>(RW, RY, lam, alpha) - sT;
+          if (CRIT == 1) g = 0.5 * g - gamma;
+          if (g > bg || (g == bg && i < bk)) { bg = g; bk = i; }
+        }
+      }
+      if (has_na) {
+        const double LW = lw + nw, LY = ly + ny;
+        if (valid_split<CRIT>(LW, LY, rw, ry, min_rows, lam, mo)) {
+          double g = score<CRIT>(LW, LY, lam, alpha) + score<CRIT>(rw, ry, lam, alpha) - sT;
+          if (CRIT == 1) g = 0.5 * g - gamma;
+          if (g > bg || (g == bg && nt + i < bk)) { bg = g; bk = nt + i; }
+        }
+      }
+    }
+    if (tid == 0 && has_na && valid_split<CRIT>(tw, ty, nw, ny, min_rows, lam, mo)) {
+      double g = score<CRIT>(tw, ty, lam, alpha) + score<CRIT>(nw, ny, lam, alpha) - sT;
+      if (CRIT == 1) g = 0.5 * g - gamma;
+      if (g > bg || (g == bg && 2 * nt < bk)) { bg = g; bk = 2 * nt; }
+    }
+  }
+  // block arg-max: larger gain, then lower k
+  const int lane = tid & 63, wv = tid >> 6;
+  for (int o = 32; o > 0; o >>= 1) {
+    const double og = __shfl_xor(bg, o, 64);
+    const int ok = __shfl_xor(bk, o, 64);
+    if (og > bg || (og == bg && ok < bk)) { bg = og; bk = ok; }
+  }
+  if (lane == 0) { red_g[wv] = bg; red_k[wv] = bk; }
+  __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < 4; ++w)
+      if (red_g[w] > bg || (red_g[w] == bg && red_k[w] < bk)) { bg = red_g[w]; bk = red_k[w]; }
+    bool keep = bg > -INFINITY;
+    if (CRIT == 0) keep = keep && bg > se_before * msi;
+    else keep = keep && bg > 0;
+    out[2 * (size_t)p] = keep ? bg : -INFINITY;
+    out[2 * (size_t)p + 1] = keep ? (double)bk : 0.0;
+  }
+}
+
+template <int CRIT>
+static int cat_pair_launch(int BP, dim3 g, hipStream_t s, const double* H, int n, int Bs, int C, const int* pf,
+                           const int* pn, const unsigned char* pcat, const float* pmono, const double* wyy,
+                           double min_rows, double msi, double lam, double alpha, double gamma, double* out) {
+#define CPK(bp)                                                                                                \
+  case bp:                                                                                                     \
+    hipLaunchKernelGGL((cat_pair_kernel<CRIT, bp>), g, dim3(256), 0, s, H, n, Bs, C, pf, pn, pcat, pmono, wyy, \
+                       min_rows, msi, lam, alpha, gamma, out);                                                 \
+    return 0;
+  switch (BP) {
+    CPK(256) CPK(512) CPK(1024) CPK(2048) CPK(4096)
+    default: return -2;
+  }
+#undef CPK
+}
+
+// P pairs (pf: local feature slot, pn: node) of the level histogram H
+// [Fl][n][Bs][C] f64; Bs - 1 <= 4096.
+extern "C" int h2o_cat_pairs(const double* H, int n, int Bs, int C, int P, const int* pf, const int* pn,
+                             const unsigned char* pcat, const float* pmono, const double* node_wyy, double min_rows,
+                             double msi, double lam, double alpha, double gamma, int crit, double* out,
+                             hipStream_t s) {
+  if (P <= 0) return 0;
+  if (C < 2 || Bs < 2) return -1;
+  int BP = 256;
+  while (BP < Bs - 1) BP <<= 1;
+  if (BP > 4096) return -2;
+  const dim3 g(P);
+  const int rc = crit == 1 ? cat_pair_launch<1>(BP, g, s, H, n, Bs, C, pf, pn, pcat, pmono, node_wyy, min_rows,
+                                                  msi, lam, alpha, gamma, out)
+                           : cat_pair_launch<0>(BP, g, s, H, n, Bs, C, pf, pn, pcat, pmono, node_wyy, min_rows,
+                                                msi, lam, alpha, gamma, out);
+  if (rc) return rc;
+  return (int)hipGetLastError();
+}

@@ -306,3 +306,37 @@ def test_packed_hist_binmajor_matches_reference(fg, binmajor, monkeypatch):
     h_gpu = tree_ops.hist_build(bd, ridx, va, vb, 0, starts, counts, 3, use_native=True, unit_w=True)
     h_ref = tree_ops.hist_build(bd, ridx, va, vb, 0, starts, counts, 3, use_native=False)
     torch.testing.assert_close(h_gpu, h_ref, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("crit", ["se", "xgb"])
+@pytest.mark.parametrize("nb", [200, 1000, 3000])
+def test_cat_pair_kernel_matches_torch_gains(crit, nb):
+    """HIP cat_pair_kernel (bitonic (key, bin) sort + f64 scan + 3 NA options)
+    == the torch pair path's arg-max, numeric and categorical pairs, monotone
+    constraints, empty levels and NA bins."""
+    _need_gpu()
+    from h2o3_amd.models.tree.engine import GrowParams, TreeGrower
+    bd, _ = _binned(n=5000, F=6, cats=True)
+    gr = TreeGrower(bd, GrowParams(criterion=crit, min_rows=3, min_split_improvement=1e-7))
+    g = torch.Generator(device="cuda").manual_seed(nb)
+    n, Bs, F = 40, nb + 1, 5
+    H = torch.rand((F, n, Bs, 2), generator=g, device="cuda", dtype=torch.float64) * 20
+    if crit == "se":
+        H[..., 1] = (torch.rand(H[..., 1].shape, generator=g, device="cuda", dtype=torch.float64) - 0.4) * H[..., 0]
+    H[..., : nb // 7, :] *= (torch.rand((F, n, nb // 7, 1), generator=g, device="cuda") < 0.5)  # empty levels
+    H[1, :, -1] = 0                                    # feature 1: no NAs
+    P = 150
+    fslot = torch.randint(0, F, (P,), generator=g, device="cuda")
+    node = torch.randint(0, n, (P,), generator=g, device="cuda")
+    pcat = torch.rand(P, generator=g, device="cuda") < 0.7
+    mono = torch.randint(-1, 2, (P,), generator=g, device="cuda").to(torch.float64)
+    mono[pcat] = 0
+    wyy = H[0].sum(1)[:, 1] ** 2 / H[0].sum(1)[:, 0] * 3 + 50
+    best, k = gr._pairs_native(H, fslot, node, pcat, mono, wyy)
+    st = gr._pair_stats(H[fslot, node], pcat)
+    allg = gr._pair_gains(st, mono.view(-1, 1), wyy, node)
+    bt, kt = allg.max(1)
+    fin = torch.isfinite(bt)
+    assert torch.equal(torch.isfinite(best), fin)
+    torch.testing.assert_close(best[fin], bt[fin], rtol=1e-9, atol=1e-9)
+    assert torch.equal(k[fin], kt[fin])
