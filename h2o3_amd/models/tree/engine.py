@@ -71,6 +71,20 @@ class Tree:
     depth: list = field(default_factory=list)
     split_code: list = field(default_factory=list) # code threshold (numeric) for debugging
 
+    def add_children(self, depth, wl, wr):
+        """Append a (left, right) node pair per entry of wl / wr; returns the
+        id of the first new node (pairs are consecutive)."""
+        k = 2 * len(wl)
+        base = len(self.feat)
+        w = [0.0] * k
+        w[0::2] = [float(x) for x in wl]
+        w[1::2] = [float(x) for x in wr]
+        self.feat += [-1] * k; self.left += [-1] * k; self.right += [-1] * k; self.thr += [0.0] * k
+        self.na_left += [False] * k; self.is_cat += [False] * k; self.cat_left += [None] * k
+        self.value += [0.0] * k; self.weight += w; self.gain += [0.0] * k
+        self.depth += [depth] * k; self.split_code += [-1] * k
+        return base
+
     def add_node(self, depth, weight):
         self.feat.append(-1); self.left.append(-1); self.right.append(-1); self.thr.append(0.0)
         self.na_left.append(False); self.is_cat.append(False); self.cat_left.append(None)
@@ -199,12 +213,23 @@ class TreeGrower:
         elif rate < 1.0:
             k = max(1, int(math.floor(rate * base.sum() + 0.5)))
         if k is not None and k < base.sum():
+            # k random eligible features per node, all nodes at once: the k
+            # smallest of per-(node, feature) uniform keys (on the device when
+            # the histograms are there -- deep DRF levels have 10^4+ nodes)
             elig = np.nonzero(base)[0]
-            for i in range(n_nodes):
-                sel = self.rng.choice(elig, size=k, replace=False)
-                row = np.zeros(F, dtype=bool)
-                row[sel] = True
-                m[i] = row
+            if self.dev.type == "cuda":
+                gen = torch.Generator(device=self.dev)
+                gen.manual_seed(int(self.rng.randint(0, 2 ** 31 - 1)))
+                keys = torch.rand((n_nodes, len(elig)), generator=gen, device=self.dev)
+                sel = torch.topk(keys, k, dim=1, largest=False).indices
+                mt = torch.zeros((n_nodes, self.Fpad), dtype=torch.bool, device=self.dev)
+                mt.scatter_(1, torch.as_tensor(elig, device=self.dev)[sel], True)
+                mt._all_true = False
+                return mt
+            keys = self.rng.random_sample((n_nodes, len(elig)))
+            sel = np.argpartition(keys, k - 1, axis=1)[:, :k]
+            m = np.zeros((n_nodes, F), dtype=bool)
+            m[np.arange(n_nodes).reshape(-1, 1), elig[sel]] = True
         all_true = bool(m.all())
         if self.Fpad > F:
             m = np.concatenate([m, np.zeros((n_nodes, self.Fpad - F), dtype=bool)], 1)
@@ -239,7 +264,7 @@ class TreeGrower:
                 res = self._merge_candidates(res, H.shape[1], H.shape[2], H.shape[3])
             return res
         cm_num = col_mask.clone()
-        cm_num[:, fsl] &= ~is_cat.view(1, -1)
+        cm_num[:, fsl] &= ~is_cat.to(cm_num.device).view(1, -1)
         res = self._find_splits_native(H, cm_num, node_wyy)
         if bool(is_cat.any()):
             cat_local = torch.nonzero(is_cat).flatten().tolist()
@@ -925,7 +950,13 @@ class TreeGrower:
             masks_h = masks.cpu().numpy() if any_cat else None
             new_front, new_pairs = [], []
             part_starts, part_counts, part_feats = [], [], []
-            Ls_l, Rs_l = Ls.tolist(), Rs.tolist()
+            si = np.asarray(split_ids, dtype=np.int64)
+            Lsel, Rsel = Ls[si], Rs[si]
+            wl_a = (Lsel[:, 0] if mode != 1 else Lsel[:, 1]) + (Lsel[:, 2] if mode == 3 else 0.0)
+            wr_a = (Rsel[:, 0] if mode != 1 else Rsel[:, 1]) + (Rsel[:, 2] if mode == 3 else 0.0)
+            build_left = (wl_a <= wr_a).tolist()
+            first = tree.add_children(frontier[split_ids[0]][3] + 1, Lsel[:, 0].tolist(), Rsel[:, 0].tolist())
+            lvmaps = self.__dict__.setdefault("_lvmaps", {})
             for j, i in enumerate(split_ids):
                 nid_, st, ct, d = frontier[i][:4]
                 f = feats[i]
@@ -934,10 +965,10 @@ class TreeGrower:
                 tree.na_left[nid_] = opt_l[i] == 1
                 if bd.is_cat[f]:
                     tree.is_cat[nid_] = True
-                    card = bd.cat_card[f]
-                    g = bd.cat_group[f]
-                    lv = np.arange(card) // g
-                    tree.cat_left[nid_] = masks_h[j][np.minimum(lv, bd.Bs - 2)].astype(np.uint8)
+                    lvm = lvmaps.get(f)
+                    if lvm is None:
+                        lvm = lvmaps[f] = np.minimum(np.arange(bd.cat_card[f]) // bd.cat_group[f], bd.Bs - 2)
+                    tree.cat_left[nid_] = masks_h[j][lvm]
                     tree.thr[nid_] = float("nan")
                 else:
                     if opt_l[i] == 2:
@@ -945,18 +976,15 @@ class TreeGrower:
                     else:
                         tree.thr[nid_] = bd.split_value(f, t_l[i])
                     tree.split_code[nid_] = t_l[i]
-                Li, Ri = Ls_l[i], Rs_l[i]
-                lid = tree.add_node(d + 1, Li[0])
-                rid = tree.add_node(d + 1, Ri[0])
+                lid = first + 2 * j
+                rid = lid + 1
                 tree.left[nid_], tree.right[nid_] = lid, rid
                 part_starts.append(st)
                 part_counts.append(ct)
                 part_feats.append(f)
-                wl = (Li[0] if mode != 1 else Li[1]) + (Li[2] if mode == 3 else 0.0)
-                wr = (Ri[0] if mode != 1 else Ri[1]) + (Ri[2] if mode == 3 else 0.0)
-                new_pairs.append((lid, rid, j, wl <= wr))
-                child_tot[lid] = Ls[i]
-                child_tot[rid] = Rs[i]
+                new_pairs.append((lid, rid, j, build_left[j]))
+                child_tot[lid] = Lsel[j]
+                child_tot[rid] = Rsel[j]
             # partition
             if nleft_pre is not None:
                 nleft = [nleft_pre[i] for i in split_ids]
@@ -1018,7 +1046,8 @@ class TreeGrower:
         self.ridx, self.ridx2 = ridx, ridx2
         self._pay = [pa, pb, pa2, pb2]
         self.last_segs = (lids, [s[1] for s in segs], [s[2] for s in segs])
-        leaf_tot_t = torch.stack([torch.as_tensor(x, dtype=torch.float64) for x in leaf_tot]) if leaf_tot else \
+        leaf_tot_t = torch.from_numpy(np.asarray(np.stack([np.asarray(x, dtype=np.float64) for x in leaf_tot]),
+                                                 dtype=np.float64)) if leaf_tot else \
             torch.zeros((0, C), dtype=torch.float64)
         return tree, nid, leaves, leaf_tot_t
 

@@ -7,3 +7,5 @@ H2O3_PROFILE=1 timeout -k 10 400 python bench.py --algo drf --rows ${ROWS:-10000
   --steps 5 --warmup 1 > gpurun_out/drf_bench.log 2>&1
 grep '"metric"' gpurun_out/drf_bench.log | cut -c1-300
 grep phases gpurun_out/drf_bench.log | cut -c1-400 || true
+timeout -k 10 300 python bench.py --steps 10 --warmup 2 > gpurun_out/gbm_bench.log 2>&1
+tail -n 1 gpurun_out/gbm_bench.log | cut -c1-250

@@ -1,0 +1,25 @@
+"""Statistical line sampler of TreeGrower.grow (host-side hotspots); BENCH_ARGS = bench.py args."""
+import sys, threading, time, collections
+import os; sys.argv=['bench.py']+os.environ.get('BENCH_ARGS','--algo drf --rows 300000 --cols 60 --cat-cols 10 --cat-card 100 --steps 2 --warmup 0').split()
+sys.path.insert(0, os.environ.get('GRAFT_REPO_ROOT', '/root/repo'))
+import bench
+main_id = threading.get_ident()
+cnt = collections.Counter()
+stop = False
+def sampler():
+    while not stop:
+        f = sys._current_frames().get(main_id)
+        # find the innermost frame inside engine.py grow
+        while f is not None:
+            if f.f_code.co_name == 'grow' and f.f_code.co_filename.endswith('engine.py'):
+                cnt[f.f_lineno] += 1
+                break
+            f = f.f_back
+        time.sleep(0.0005)
+t = threading.Thread(target=sampler, daemon=True); t.start()
+bench.main()
+stop = True
+tot = sum(cnt.values())
+src = open(os.environ.get('GRAFT_REPO_ROOT', '/root/repo') + '/h2o3_amd/models/tree/engine.py').read().splitlines()
+for ln, c in cnt.most_common(25):
+    print(f"{c:6d} {100*c/tot:5.1f}% L{ln}: {src[ln-1].strip()[:100]}")
