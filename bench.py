@@ -23,34 +23,11 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--rows", type=int, default=100_000_000)
-    ap.add_argument("--cols", type=int, default=100)
-    ap.add_argument("--max-depth", type=int, default=8)
-    ap.add_argument("--algo", default="gbm", choices=["gbm", "glm", "drf"])
-    ap.add_argument("--cat-cols", type=int, default=0,
-                    help="replace this many of the --cols columns by categoricals (DRF config: mixed num/cat)")
-    ap.add_argument("--cat-card", type=int, default=1000, help="cardinality of the categorical columns")
-    ap.add_argument("--histogram-type", default="QuantilesGlobal")
-    ap.add_argument("--nbins", type=int, default=255)
-    args = ap.parse_args()
-
+def make_frame(args, dev, rank, rows_local):
+    """Synthetic data of the benchmark shape (random, generated on device):
+    args.cols features (the last args.cat_cols categorical), binomial y."""
     import torch
-    import torch.distributed as dist
-    import h2o3_amd
-    from h2o3_amd.parallel import cloud
-
-    h2o3_amd.init(verbose=False)
-    world, rank = cloud.world(), cloud.rank()
-    dev = cloud.device()
-    rows_local = args.rows // world + (1 if rank < args.rows % world else 0)
     F = args.cols
-
-    # ---- synthetic data of the benchmark shape (random, generated on device)
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
     gb = torch.Generator(device="cpu").manual_seed(42)
@@ -81,6 +58,37 @@ def main():
     vecs = [Vec(c, T_ENUM, dom) if c.dtype == torch.int32 else Vec(c, T_REAL) for c in cols] + \
         [Vec(y, T_ENUM, ["0", "1"])]
     fr = H2OFrame.from_vecs(vecs, names + ["y"])
+    return fr, names, y
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--rows", type=int, default=100_000_000)
+    ap.add_argument("--cols", type=int, default=100)
+    ap.add_argument("--max-depth", type=int, default=8)
+    ap.add_argument("--algo", default="gbm", choices=["gbm", "glm", "drf"])
+    ap.add_argument("--cat-cols", type=int, default=0,
+                    help="replace this many of the --cols columns by categoricals (DRF config: mixed num/cat)")
+    ap.add_argument("--cat-card", type=int, default=1000, help="cardinality of the categorical columns")
+    ap.add_argument("--histogram-type", default="QuantilesGlobal")
+    ap.add_argument("--nbins", type=int, default=255)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    import h2o3_amd
+    from h2o3_amd.parallel import cloud
+
+    h2o3_amd.init(verbose=False)
+    world, rank = cloud.world(), cloud.rank()
+    dev = cloud.device()
+    rows_local = args.rows // world + (1 if rank < args.rows % world else 0)
+    F = args.cols
+
+    fr, names, y = make_frame(args, dev, rank, rows_local)
     from h2o3_amd.models.base import TrainSpec
 
     extra_cfg = {}
