@@ -745,17 +745,23 @@ class TreeGrower:
         return out
 
     # ------------------------------------------------------------------ grow
-    def grow(self, va, vb, mode, tree_node_hook=None, want_nid=True):
+    def grow(self, va, vb, mode, tree_node_hook=None, want_nid=True, vmax=None, unit_w=None):
         """Grow one tree.  Returns (Tree, nid[N] leaf index per local row,
-        leaf_nodes list (tree node ids, indexed by nid), leaf_tot [n_leaves, C])."""
+        leaf_nodes list (tree node ids, indexed by nid), leaf_tot [n_leaves, C]).
+        vmax / unit_w: caller-known bounds (max |channel| for the fixed-point
+        histogram scale, 0/1 row weights) that spare the two device syncs at
+        the start of the tree."""
         bd, p = self.bd, self.p
         N = bd.nrows_local
         C = tree_ops.channels(mode)
         torch.arange(N, dtype=torch.int32, device=self.dev, out=self.ridx)
-        self._vmax = tree_ops.channel_max(va, vb, mode) if self.dev.type == "cuda" else None
+        if self.dev.type != "cuda":
+            self._vmax = None
+        else:
+            self._vmax = list(vmax) if vmax is not None else tree_ops.channel_max(va, vb, mode)
         # 0/1 row weights (unweighted data, row sampling) -> packed histogram atomics
         self._unit_w = mode == 0 and self.dev.type == "cuda" and (
-            vb is None or bool(((vb == 0) | (vb == 1)).all()))
+            vb is None or (bool(unit_w) if unit_w is not None else bool(((vb == 0) | (vb == 1)).all())))
         self._va_eff = None
         quad = self.bd.code_bytes == 1 and self.bd.Bs <= 256 and self.bd.Fp % 16 == 0 and \
             os.environ.get("H2O3_HIST_KERNEL", "quad") == "quad"

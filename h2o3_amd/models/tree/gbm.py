@@ -206,9 +206,16 @@ class GBMDriver:
             # position-ordered residual payload + segment update: no per-row leaf ids at all
             posleaf = simple and not fused and self.K == 1 and self.f.shape[1] == 1 and \
                 os.environ.get("H2O3_POS_LEAF", "1") == "1"
+            if getattr(self, "_base_unit", None) is None:
+                bw = self.base_w
+                self._base_unit = bool(((bw == 0) | (bw == 1)).all())
+            # bernoulli residuals y - p lie in (-1, 1): with 0/1 weights both
+            # histogram channels are bounded by 1 (no per-tree max reduction)
+            vmax_h = [1.0, 1.0] if (self.dist.family == "bernoulli" and self._base_unit) else None
             with phase("gbm.grow"):
                 tree, nid, leaves, tot = self.grower.grow(z.contiguous(), w.contiguous(), 0,
-                                                          want_nid=not (fused or posleaf))
+                                                          want_nid=not (fused or posleaf), vmax=vmax_h,
+                                                          unit_w=self._base_unit)
             zpos = self.grower._pos1[0] if (posleaf and getattr(self.grower, "_pos1", None) is not None) else None
             if posleaf and zpos is None:
                 posleaf = False
