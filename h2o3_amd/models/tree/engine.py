@@ -299,7 +299,8 @@ class TreeGrower:
             if ok is None:
                 ok = cache[n] = torch.ones((n, Fl), dtype=torch.uint8, device=self.dev)
         else:
-            ok = cm.to(torch.uint8).contiguous().to(self.dev, non_blocking=True)
+            ok = cm.to(torch.uint8).contiguous()
+            ok = ok.pin_memory().to(self.dev, non_blocking=True) if ok.device.type == "cpu" else ok
             if self.f0 + Fl > self.bd.F:
                 ok[:, max(0, self.bd.F - self.f0):] = 0
         if getattr(self, "_mono_f32", None) is None:
@@ -952,7 +953,8 @@ class TreeGrower:
             any_cat = any(bd.is_cat[feats[i]] for i in split_ids)
             masks = None
             if any_cat or nleft_pre is None:
-                masks = sp["mask"] if all_split else sp["mask"][torch.tensor(split_ids, device=sp["mask"].device)]
+                masks = sp["mask"] if all_split else sp["mask"][tree_ops._h2d(np.asarray(split_ids, dtype=np.int64),
+                                                                              sp["mask"].device)]
             masks_h = masks.cpu().numpy() if any_cat else None
             new_front, new_pairs = [], []
             part_starts, part_counts, part_feats = [], [], []

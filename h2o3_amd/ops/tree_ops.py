@@ -10,6 +10,7 @@ import ctypes
 import math
 import os
 
+import numpy as np
 import torch
 
 from . import _native
@@ -19,6 +20,17 @@ _c_void = ctypes.c_void_p
 _c_int = ctypes.c_int
 _c_ll = ctypes.c_longlong
 
+
+
+def _h2d(a, dev):
+    """Host array -> device without a stream sync: staged through the pinned
+    caching host allocator, so the copy is asynchronous (a pageable-memory
+    source makes the runtime wait for the stream, serialising the host's
+    level loop with the GPU)."""
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    if dev.type == "cuda":
+        return t.pin_memory().to(dev, non_blocking=True)
+    return t.to(dev)
 
 def _ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
@@ -87,7 +99,6 @@ def feature_group(F: int, Bs: int, mode: int, budget: int = _LDS_BUDGET) -> int:
 def make_work(starts, counts, slots, chunk):
     """Chunk node segments into (slot, start, count, chunk_id) work items
     (host, vectorized) -> int32 numpy array [n_items, 4]."""
-    import numpy as np
     st = np.asarray(starts, dtype=np.int64).reshape(-1)
     ct = np.asarray(counts, dtype=np.int64).reshape(-1)
     sl = np.asarray(list(slots), dtype=np.int64).reshape(-1)
@@ -176,7 +187,7 @@ def hist_build(bd, ridx, va, vb, mode, starts, counts, n_slots, use_native=None,
         items = make_work(starts, counts, range(n_slots), chunk)
         if len(items) == 0:
             return ret()
-        work = torch.from_numpy(items).to(dev, non_blocking=True)
+        work = _h2d(items, dev)
         threads = 512 if chunk >= 8192 else 256
         if vmax is None:
             vmax = channel_max(va, vb, mode)
@@ -258,9 +269,9 @@ def partition(bd, ridx, ridx_out, feats, masks, starts, counts, use_native=None,
         items = make_work(starts, counts, range(n), chunk)
         if len(items) == 0:
             return [0] * n
-        work = torch.from_numpy(items).to(dev, non_blocking=True)
+        work = _h2d(items, dev)
         nw = len(items)
-        feat_t = torch.as_tensor(feats, dtype=torch.int32).to(dev)
+        feat_t = _h2d(np.asarray(feats, dtype=np.int32), dev)
         masks = masks.to(torch.uint8).contiguous()
         cnt = torch.empty(nw, dtype=torch.int32, device=dev)
         if bd.codes_col is not None:
@@ -269,10 +280,9 @@ def partition(bd, ridx, ridx_out, feats, masks, starts, counts, use_native=None,
             codes, rs, fs = bd.codes, bd.Fp, 1
         ballot = os.environ.get("H2O3_PART", "ballot") == "ballot" and (payload is None or payload[1] is None)
         if ballot:
-            import numpy as np
             words = (items[:, 2].astype(np.int64) + 63) // 64
             fb_h = (np.cumsum(words) - words).astype(np.int32)
-            fbase = torch.from_numpy(fb_h).to(dev, non_blocking=True)
+            fbase = _h2d(fb_h, dev)
             flags = torch.empty(int(words.sum()) + 1, dtype=torch.int64, device=dev)
             rc = lib.h2o_part_flags(_ptr(codes), bd.code_bytes, rs, fs, _ptr(ridx), _ptr(work), _ptr(fbase), nw,
                                     _ptr(feat_t), _ptr(masks), bd.Bs, _ptr(flags), _ptr(cnt), _stream())
@@ -283,7 +293,6 @@ def partition(bd, ridx, ridx_out, feats, masks, starts, counts, use_native=None,
             raise RuntimeError(f"h2o_part_count failed: {rc}")
         # per-node exclusive scans of the chunk counts (chunks of a node are
         # consecutive in `items`), vectorized on the host
-        import numpy as np
         cnt_h = cnt.cpu().numpy().astype(np.int64)
         slot = items[:, 0].astype(np.int64)
         nleft = np.bincount(slot, weights=cnt_h, minlength=n).astype(np.int64)
@@ -296,8 +305,8 @@ def partition(bd, ridx, ridx_out, feats, masks, starts, counts, use_native=None,
         rpre = (items[:, 1].astype(np.int64) - st_arr) - lpre
         loff = (st_arr + lpre).astype(np.int32)
         roff = (st_arr + nleft[slot] + rpre).astype(np.int32)
-        loff_d = torch.from_numpy(loff).to(dev, non_blocking=True)
-        roff_d = torch.from_numpy(roff).to(dev, non_blocking=True)
+        loff_d = _h2d(loff, dev)
+        roff_d = _h2d(roff, dev)
         pa, pb, pa_o, pb_o = payload if payload is not None else (None, None, None, None)
         if ballot:
             rc = lib.h2o_part_compact(_ptr(ridx), _ptr(work), _ptr(fbase), nw, _ptr(flags), _ptr(loff_d),
@@ -343,7 +352,6 @@ def partition_async(bd, ridx, ridx_out, feat_d, masks, starts, counts, chunk=163
     with pk, also writes them as doubles into column pk_col of the [n, stride]
     split record, so they come back with the level's single host transfer).
     payload = (pa, None, pa_out, None)."""
-    import numpy as np
     dev = ridx.device
     n = len(starts)
     lib = _lib()
@@ -371,7 +379,7 @@ def partition_async(bd, ridx, ridx_out, feat_d, masks, starts, counts, chunk=163
     # flag-word bases (int32 views of the same buffer)
     meta_h = np.concatenate([np.stack([slot, first_idx, st_arr, pos], 0).reshape(-1).view(np.int32),
                              items.reshape(-1), fb_h.astype(np.int32)])
-    buf = torch.from_numpy(meta_h).to(dev, non_blocking=True)
+    buf = _h2d(meta_h, dev)
     meta = buf[: 8 * nw].view(torch.int64)
     work = buf[8 * nw: 12 * nw]
     fbase = buf[12 * nw:]
@@ -406,7 +414,6 @@ def hist_sibling(Hb, H_prev, build_slots, der_slots, par_slots, n_front, clamp_m
     """Next-level histograms in one kernel: built children copied, siblings =
     parent - built (clamped at 0 on the channels of clamp_mask).  Returns
     (H [F, n_front, Bs, C], wyy [n_front] or None)."""
-    import numpy as np
     lib = _lib()
     if not getattr(lib, "_typed_sib", False):
         lib.h2o_hist_sibling.argtypes = [_c_void, _c_void, _c_void, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
@@ -414,8 +421,7 @@ def hist_sibling(Hb, H_prev, build_slots, der_slots, par_slots, n_front, clamp_m
         lib._typed_sib = True
     F, nb, Bs, C = Hb.shape
     H = torch.empty((F, n_front, Bs, C), dtype=Hb.dtype, device=Hb.device)
-    slots = torch.from_numpy(np.asarray([build_slots, der_slots, par_slots], dtype=np.int32).reshape(-1)).to(
-        Hb.device, non_blocking=True)
+    slots = _h2d(np.asarray([build_slots, der_slots, par_slots], dtype=np.int32).reshape(-1), Hb.device)
     wyy = torch.empty(n_front, dtype=torch.float64, device=Hb.device) if wyy_b is not None else None
     Hb = Hb.contiguous()
     Hp = H_prev.contiguous()
@@ -435,7 +441,7 @@ def fill_nid(ridx, leaf_ids, starts, counts, nrows, use_native=None):
         lib = _lib()
         items = make_work(starts, counts, leaf_ids, 65536)
         if len(items):
-            work = torch.from_numpy(items).to(dev, non_blocking=True)
+            work = _h2d(items, dev)
             rc = lib.h2o_fill_nid(_ptr(ridx), _ptr(work), len(items), _ptr(nid), _stream())
             if rc != 0:
                 raise RuntimeError(f"h2o_fill_nid failed: {rc}")
@@ -458,7 +464,7 @@ def leaf_pass(ridx, z, w, leaf_ids, starts, counts, n_leaves, nrows, mode, chunk
     items = make_work(starts, counts, leaf_ids, chunk)
     if len(items) == 0:
         return nid, out
-    work = torch.from_numpy(items).to(dev, non_blocking=True)
+    work = _h2d(items, dev)
     z = z.to(torch.float32).contiguous()
     w = None if w is None else w.to(torch.float32).contiguous()
     rc = lib.h2o_leaf_pass(_ptr(ridx), _ptr(z), _ptr(w), _ptr(work), len(items), int(mode), _ptr(nid), _ptr(out),
@@ -479,7 +485,7 @@ def leaf_pos_sums(zpos, leaf_ids, starts, counts, n_leaves, mode, chunk=65536):
     out = torch.zeros((n_leaves, 2), dtype=torch.float64, device=zpos.device)
     items = make_work(starts, counts, leaf_ids, chunk)
     if len(items):
-        work = torch.from_numpy(items).to(zpos.device, non_blocking=True)
+        work = _h2d(items, zpos.device)
         rc = lib.h2o_leaf_pos(_ptr(zpos), _ptr(work), len(items), int(mode), _ptr(out), _stream())
         if rc != 0:
             raise RuntimeError(f"h2o_leaf_pos failed: {rc}")
@@ -495,7 +501,7 @@ def leaf_update(ridx, f, vals, leaf_ids, starts, counts, chunk=65536):
         lib._typed_lpos = True
     items = make_work(starts, counts, leaf_ids, chunk)
     if len(items):
-        work = torch.from_numpy(items).to(f.device, non_blocking=True)
+        work = _h2d(items, f.device)
         rc = lib.h2o_leaf_update(_ptr(ridx), _ptr(work), len(items), _ptr(vals), _ptr(f), _stream())
         if rc != 0:
             raise RuntimeError(f"h2o_leaf_update failed: {rc}")
@@ -514,7 +520,7 @@ def seg_sum2(ridx, a, b, leaf_ids, starts, counts, n_leaves, use_native=None, ch
         items = make_work(starts, counts, leaf_ids, chunk)
         if len(items) == 0:
             return out
-        work = torch.from_numpy(items).to(dev, non_blocking=True)
+        work = _h2d(items, dev)
         a = a.to(torch.float32).contiguous()
         b = None if b is None else b.to(torch.float32).contiguous()
         rc = lib.h2o_seg_sum2(_ptr(ridx), _ptr(a), _ptr(b), _ptr(work), len(items), _ptr(out), _stream())
