@@ -130,6 +130,7 @@ class GBMDriver:
             gp.monotone = np.array([float(mc.get(n, 0)) for n in spec.x])
         self.gp = gp
         self.grower = TreeGrower(self.bd, gp)
+        self._pending = None
         self.forest = Forest()
         self.lr = float(p["learn_rate"])
         self.iter = 0
@@ -160,6 +161,28 @@ class GBMDriver:
                 if abs(g) < 1e-8:
                     break
         return f0
+
+    @property
+    def forest(self):
+        self._resolve_pending()
+        return self._forest_obj
+
+    @forest.setter
+    def forest(self, fo):
+        self._pending = None
+        self._forest_obj = fo
+
+    def _resolve_pending(self):
+        """Fill the last tree's leaf values from its async device->host copy."""
+        pend = getattr(self, "_pending", None)
+        if pend is None:
+            return
+        self._pending = None
+        tree, leaves, hv, ev = pend
+        ev.synchronize()
+        v = hv.numpy().tolist()
+        for li, node in enumerate(leaves):
+            tree.value[node] = float(v[li])
 
     def _row_weights(self):
         p = self.est._parms
@@ -220,15 +243,32 @@ class GBMDriver:
             if posleaf and zpos is None:
                 posleaf = False
                 nid = tree_ops.fill_nid(self.grower.ridx, *self.grower.last_segs, z.shape[0])
-            with phase("gbm.gamma"):
-                if posleaf:
-                    lids, st, ct = self.grower.last_segs
+            if posleaf:
+                # leaf values stay on the device: the prediction update runs
+                # without a host round trip and the tree's host copy of the
+                # values arrives by an async pinned copy, resolved the next time
+                # the forest is touched (no GPU bubble between trees)
+                lids, st, ct = self.grower.last_segs
+                with phase("gbm.gamma"):
                     s_ = tree_ops.leaf_pos_sums(zpos, lids, st, ct, len(leaves),
                                                 1 if self.dist.family == "bernoulli" else 0)
                     coll.allreduce_(s_)
-                    sh = s_.cpu().numpy()
-                    vals = np.where(sh[:, 1] != 0, sh[:, 0] / np.where(sh[:, 1] == 0, 1, sh[:, 1]), 0.0)
-                elif fused:
+                    den = s_[:, 1]
+                    vals_d = torch.where(den != 0, s_[:, 0] / torch.where(den == 0, torch.ones_like(den), den),
+                                         torch.zeros_like(den)).clamp(-maxabs, maxabs) * lr
+                with phase("gbm.update"):
+                    tree_ops.leaf_update(self.grower.ridx, self.f, vals_d.to(torch.float32), lids, st, ct)
+                hv = torch.empty(vals_d.shape, dtype=torch.float64, pin_memory=True)
+                hv.copy_(vals_d, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record()
+                self._resolve_pending()
+                self._forest_obj.add(tree, 0)
+                self._pending = (tree, list(leaves), hv, ev)
+                self.iter += 1
+                return
+            with phase("gbm.gamma"):
+                if fused:
                     # one walk over the leaf segments: nid fill + gamma sums
                     lids, st, ct = self.grower.last_segs
                     nid, s_ = tree_ops.leaf_pass(self.grower.ridx, z, w, lids, st, ct, len(leaves), z.shape[0],

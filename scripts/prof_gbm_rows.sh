@@ -1,0 +1,35 @@
+# Per-tree GPU busy time vs wall span from a kernel trace (ROWS rows, depth 8).
+set -e
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+R=${ROWS:-12500000}
+OUT=gpurun_out/rocprof_gbm_$R
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT -o run --output-format csv -- python3 bench.py --rows $R --steps 10 --warmup 2 > $OUT.log 2>&1
+python3 - "$OUT/run_kernel_trace.csv" > gpurun_out/gbm_${R}_pertree.txt <<'PY'
+import csv, sys, collections
+tr = list(csv.DictReader(open(sys.argv[1])))
+tr.sort(key=lambda r: int(r["Start_Timestamp"]))
+idx = [i for i, r in enumerate(tr) if "hist_quad" in r["Kernel_Name"]]
+st = idx[::8]
+a, b = st[-9], st[-1]
+sub = tr[a:b]
+tot = collections.defaultdict(float); cnt = collections.Counter()
+busy = 0; prev = int(sub[0]["Start_Timestamp"]); gaps = []; gapk = []; last_k = ""
+for r in sub:
+    s_, e_ = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+    k = r["Kernel_Name"][:60]; tot[k] += (e_ - s_) / 1e6 / 8; cnt[k] += 1
+    if s_ > prev: gaps.append(s_ - prev); gapk.append((s_ - prev, last_k, r["Kernel_Name"][:50]))
+    last_k = r["Kernel_Name"][:50]
+    busy += e_ - s_; prev = max(prev, e_)
+span = (int(tr[b]["Start_Timestamp"]) - int(tr[a]["Start_Timestamp"])) / 1e6 / 8
+print(f"per tree (last 8 trees): span {span:.2f} ms, kernel busy {busy/1e6/8:.2f} ms, launches {len(sub)/8:.0f}, idle gaps {sum(gaps)/1e6/8:.2f} ms in {len(gaps)/8:.0f} gaps")
+gaps.sort(reverse=True)
+print("largest gaps (us):", [round(g / 1e3) for g in gaps[:12]])
+gapk.sort(reverse=True)
+for g, a_, b_ in gapk[:10]:
+    print(f"  gap {g/1e3:7.0f} us after {a_} -> before {b_}")
+for k, v in sorted(tot.items(), key=lambda kv: -kv[1])[:14]:
+    print(f"{v:8.3f} ms {cnt[k]/8:6.1f}x  {k}")
+PY
+rm -f $OUT/run_kernel_trace.csv
+cat gpurun_out/gbm_${R}_pertree.txt
