@@ -617,12 +617,25 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             if (fam.link == 0 && fam.var == 0) {
               W = sw;
               z = sy - so;
+              if (sw != 0.f) dev += (double)(sw * gi_dev(fam, sy, mu));
+            } else if (fam.link == 1 && fam.var == 1) {
+              // canonical binomial: dmu/deta == variance, so W = w d and one
+              // reciprocal; 0/1 responses need one log for the deviance
+              const float d = fmaxf(mu * (1.f - mu), 1e-10f);
+              W = sw * d;
+              z = (eta - so) + (sy - mu) * __frcp_rn(d);
+              if (sw != 0.f) {
+                const float m = fminf(fmaxf(mu, 1e-15f), 1.f - 1e-7f);
+                const float dv = sy == 1.f ? -2.f * __logf(m) : sy == 0.f ? -2.f * __logf(1.f - m)
+                                                                         : gi_dev(fam, sy, mu);
+                dev += (double)(sw * dv);
+              }
             } else {
               const float d = gi_dmu(fam.link, mu);
               W = sw * d * d / gi_var(fam, mu);
               z = (eta - so) + (sy - mu) / d;
+              if (sw != 0.f) dev += (double)(sw * gi_dev(fam, sy, mu));
             }
-            if (sw != 0.f) dev += (double)(sw * gi_dev(fam, sy, mu));
           } else {
             W = sw;
             z = sy;
