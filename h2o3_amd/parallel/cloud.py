@@ -11,6 +11,7 @@ issued SPMD by all ranks in the same order (like MRTask's reduce tree).
 """
 from __future__ import annotations
 
+import atexit
 import datetime
 import os
 import socket
@@ -54,6 +55,7 @@ def init(device: str | None = None, backend: str | None = None, timeout_s: float
         dist.init_process_group(be, rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=timeout_s), **kw)
         _state["owns_pg"] = True
+        atexit.register(shutdown)
     if dist.is_initialized():
         rank, world = dist.get_rank(), dist.get_world_size()
         _state["backend"] = dist.get_backend()
@@ -105,7 +107,13 @@ def info() -> dict:
 
 
 def shutdown():
+    # Tear the owned process group down explicitly: letting interpreter exit
+    # destroy a live gloo group races its worker threads (std::terminate).
     if _state["owns_pg"] and dist.is_initialized():
+        try:
+            dist.barrier()
+        except Exception:
+            pass
         dist.destroy_process_group()
     _state.update(initialized=False, owns_pg=False)
 

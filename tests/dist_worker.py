@@ -54,6 +54,7 @@ def run(out_path):
         with open(out_path, "w") as f:
             json.dump(res, f)
     cloud.barrier()
+    cloud.shutdown()
 
 
 if __name__ == "__main__":
