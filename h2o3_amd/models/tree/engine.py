@@ -162,7 +162,7 @@ class TreeGrower:
             params.hist_mem_budget = int(os.environ["H2O3_HIST_BUDGET"])
 
     # ------------------------------------------------------------------ hist
-    def _build_hist(self, ridx, va, vb, mode, starts, counts):
+    def _build_hist(self, ridx, va, vb, mode, starts, counts, need_mask=None):
         if mode == 3:
             # uplift: treatment and control (w, w*y) histograms side by side
             with phase("tree.hist"):
@@ -188,7 +188,7 @@ class TreeGrower:
         with phase("tree.hist"), phase(f"tree.hist.L{getattr(self, '_level', 0)}"):
             H, wyy = tree_ops.hist_build(self.bd, ridx, va, vb, mode, starts, counts, len(starts), vmax=self._vmax,
                                          posv=posv, want_wyy=True,
-                                         unit_w=getattr(self, "_unit_w", False))
+                                         unit_w=getattr(self, "_unit_w", False), need_mask=need_mask)
         if wyy is not None:
             coll.allreduce_(wyy)
         self._last_wyy = wyy
@@ -198,6 +198,19 @@ class TreeGrower:
                                               device=H.device)], 0)
             H = coll.reduce_scatter_dim0(H)
         return H  # [Fl, n, Bs, C]
+
+    def _hist_need(self, cm):
+        """Per-node features whose histograms the split search reads: the
+        sampled columns plus each rank's first local feature (node totals come
+        from H[0]).  None = all (no column sampling / no GPU kernels)."""
+        if self.dev.type != "cuda" or getattr(cm, "_all_true", False) or self.p.criterion.startswith("uplift") \
+                or os.environ.get("H2O3_HIST_NEED", "1") == "0":
+            return None
+        need = cm.to(self.dev, dtype=torch.bool).clone()
+        for r in range(self.W):
+            if r * self.Fl < self.bd.F:
+                need[:, r * self.Fl] = True
+        return need
 
     # ------------------------------------------------------------------ splits
     def _col_mask(self, n_nodes, depth):
@@ -860,9 +873,11 @@ class TreeGrower:
                     if chunked:
                         per = max(1, int(p.hist_mem_budget // max(1, self.Fpad * bd.Bs * C_ * 8)))
                         parts = []
+                        need = self._hist_need(cm)
                         for a in range(0, n_front, per):
                             fr_ = frontier[a:a + per]
-                            Hc = self._build_hist(ridx, va, vb, mode, [f[1] for f in fr_], [f[2] for f in fr_])
+                            Hc = self._build_hist(ridx, va, vb, mode, [f[1] for f in fr_], [f[2] for f in fr_],
+                                                  need_mask=None if need is None else need[a:a + per])
                             wyy_c = self._last_wyy if mode == 0 else None
                             parts.append(self._find_splits(Hc, cm[a:a + per], wyy_c, want_pk=False))
                             del Hc

@@ -36,11 +36,14 @@ __global__ __launch_bounds__(512) void hist_build_kernel(
     const CodeT* __restrict__ codes, int Fp, const int* __restrict__ ridx,
     const float* __restrict__ va, const float* __restrict__ vb,
     const int4* __restrict__ work, int F, int Bs, int FGL, float s0, float s1,
-    double* __restrict__ hist, int n_slots, double* __restrict__ wyy_out) {
+    double* __restrict__ hist, int n_slots, double* __restrict__ wyy_out, const uint8_t* __restrict__ need) {
   constexpr int C = Chan<MODE>::C;
   const int RPW = 64 / FGL;                     // rows per wave instruction
   extern __shared__ __attribute__((aligned(16))) unsigned long long ldsq[];
   const int4 wk = work[blockIdx.x];
+  // need[slot * n_fg + group] == 0: no feature of this group is eligible at
+  // this node (DRF mtries / column sampling) -> the histogram stays zero
+  if (need != nullptr && need[(size_t)wk.x * gridDim.y + blockIdx.y] == 0) return;
   const int fg0 = blockIdx.y * FGL;
   const int nf = min(FGL, F - fg0);
   const int stride_f = Bs * C;
@@ -160,7 +163,8 @@ __global__ __launch_bounds__(512) void hist_quad_kernel(
     const uint8_t* __restrict__ codes, int Fp, const int* __restrict__ ridx,
     const float* __restrict__ va, const float* __restrict__ vb,
     const int4* __restrict__ work, int n_work, int n_fg, int F, int Bs, float s0, float s1,
-    double* __restrict__ hist, int n_slots, double* __restrict__ wyy_out, long long bq) {
+    double* __restrict__ hist, int n_slots, double* __restrict__ wyy_out, long long bq,
+    const uint8_t* __restrict__ need) {
   constexpr int C = Chan<MODE>::C;
   constexpr int CL = PACK ? 1 : C;       // u64 entries per bin in LDS
   constexpr int LPR = FG / 4;            // lanes per row (one dword of codes each)
@@ -170,6 +174,7 @@ __global__ __launch_bounds__(512) void hist_quad_kernel(
   const int lb = xcd_remap(blockIdx.x, nwg);
   const int fgi = lb % n_fg;
   const int4 wk = work[lb / n_fg];
+  if (need != nullptr && need[(size_t)wk.x * n_fg + fgi] == 0) return;   // no eligible feature in this group
   const int fg0 = fgi * FG;
   const int nf = min(FG, F - fg0);
   const int stride_f = Bs * CL + CL;
@@ -287,45 +292,46 @@ __global__ __launch_bounds__(512) void hist_quad_kernel(
 template <bool V, bool PV, int G, bool BM>
 static void launch_pack1(dim3 grid, int threads, size_t lds, hipStream_t s, const uint8_t* cc, int Fp, const int* ridx,
                          const float* va, const float* vb, const int4* wk, int n_work, int n_fg, int F, int Bs,
-                         float s0, float s1, double* hist, int n_slots, double* wyy, long long bq) {
+                         float s0, float s1, double* hist, int n_slots, double* wyy, long long bq,
+                         const uint8_t* need) {
   hipLaunchKernelGGL((hist_quad_kernel<0, V, PV, true, G, BM>), grid, dim3(threads), lds, s, cc, Fp, ridx, va, vb, wk,
-                     n_work, n_fg, F, Bs, s0, s1, hist, n_slots, wyy, bq);
+                     n_work, n_fg, F, Bs, s0, s1, hist, n_slots, wyy, bq, need);
 }
 
 template <bool V, bool PV>
 static void launch_pack(int fg, int binmajor, dim3 grid, int threads, size_t lds, hipStream_t s, const uint8_t* cc,
                         int Fp, const int* ridx, const float* va, const float* vb, const int4* wk, int n_work,
                         int n_fg, int F, int Bs, float s0, float s1, double* hist, int n_slots, double* wyy,
-                        long long bq) {
+                        long long bq, const uint8_t* need) {
   if (fg == 64)
-    launch_pack1<V, PV, 64, false>(grid, threads, lds, s, cc, Fp, ridx, va, vb, wk, n_work, n_fg, F, Bs, s0, s1, hist, n_slots, wyy, bq);
+    launch_pack1<V, PV, 64, false>(grid, threads, lds, s, cc, Fp, ridx, va, vb, wk, n_work, n_fg, F, Bs, s0, s1, hist, n_slots, wyy, bq, need);
   else if (fg == 32 && binmajor)
-    launch_pack1<V, PV, 32, true>(grid, threads, lds, s, cc, Fp, ridx, va, vb, wk, n_work, n_fg, F, Bs, s0, s1, hist, n_slots, wyy, bq);
+    launch_pack1<V, PV, 32, true>(grid, threads, lds, s, cc, Fp, ridx, va, vb, wk, n_work, n_fg, F, Bs, s0, s1, hist, n_slots, wyy, bq, need);
   else if (fg == 32)
-    launch_pack1<V, PV, 32, false>(grid, threads, lds, s, cc, Fp, ridx, va, vb, wk, n_work, n_fg, F, Bs, s0, s1, hist, n_slots, wyy, bq);
+    launch_pack1<V, PV, 32, false>(grid, threads, lds, s, cc, Fp, ridx, va, vb, wk, n_work, n_fg, F, Bs, s0, s1, hist, n_slots, wyy, bq, need);
   else if (binmajor)
-    launch_pack1<V, PV, 16, true>(grid, threads, lds, s, cc, Fp, ridx, va, vb, wk, n_work, n_fg, F, Bs, s0, s1, hist, n_slots, wyy, bq);
+    launch_pack1<V, PV, 16, true>(grid, threads, lds, s, cc, Fp, ridx, va, vb, wk, n_work, n_fg, F, Bs, s0, s1, hist, n_slots, wyy, bq, need);
   else
-    launch_pack1<V, PV, 16, false>(grid, threads, lds, s, cc, Fp, ridx, va, vb, wk, n_work, n_fg, F, Bs, s0, s1, hist, n_slots, wyy, bq);
+    launch_pack1<V, PV, 16, false>(grid, threads, lds, s, cc, Fp, ridx, va, vb, wk, n_work, n_fg, F, Bs, s0, s1, hist, n_slots, wyy, bq, need);
 }
 
 // pack_bq >= 0 selects the packed single-atomic path (MODE 0, 0/1 weights).
 extern "C" int h2o_hist_quad2(const void* codes, int Fp, const int* ridx, const float* va, const float* vb,
                               const int* work, int n_work, int F, int Bs, float s0, float s1, double* hist,
                               int n_slots, int mode, int threads, double* wyy, int posv, long long pack_bq,
-                              int fg, int binmajor, hipStream_t s);
+                              int fg, int binmajor, const uint8_t* need, hipStream_t s);
 extern "C" int h2o_hist_quad(const void* codes, int Fp, const int* ridx, const float* va, const float* vb,
                              const int* work, int n_work, int F, int Bs, float s0, float s1, double* hist,
                              int n_slots, int mode, int threads, double* wyy, int posv, long long pack_bq,
                              int fg, hipStream_t s) {
   return h2o_hist_quad2(codes, Fp, ridx, va, vb, work, n_work, F, Bs, s0, s1, hist, n_slots, mode, threads, wyy,
-                        posv, pack_bq, fg, 0, s);
+                        posv, pack_bq, fg, 0, nullptr, s);
 }
 
 extern "C" int h2o_hist_quad2(const void* codes, int Fp, const int* ridx, const float* va, const float* vb,
                               const int* work, int n_work, int F, int Bs, float s0, float s1, double* hist,
                               int n_slots, int mode, int threads, double* wyy, int posv, long long pack_bq,
-                              int fg, int binmajor, hipStream_t s) {
+                              int fg, int binmajor, const uint8_t* need, hipStream_t s) {
   if (n_work <= 0) return 0;
   if (Fp % 16 != 0 || Bs > 256) return -1;
   const bool pack = pack_bq >= 0 && mode == 0;
@@ -339,13 +345,13 @@ extern "C" int h2o_hist_quad2(const void* codes, int Fp, const int* ridx, const 
   const int4* wk = (const int4*)work;
 #define H2O_LQ2(M, V, PV, PK) hipLaunchKernelGGL((hist_quad_kernel<M, V, PV, PK>), grid, dim3(threads), lds, s, cc, \
                                                  Fp, ridx, va, vb, wk, n_work, n_fg, F, Bs, s0, s1, hist, n_slots, \
-                                                 wyy, pack_bq)
+                                                 wyy, pack_bq, need)
 #define H2O_LQ(M, V) if (posv) H2O_LQ2(M, V, true, false); else H2O_LQ2(M, V, false, false)
   if (pack) {
-    if (vb) { if (posv) launch_pack<true, true>(fg, binmajor, grid, threads, lds, s, cc, Fp, ridx, va, vb, wk, n_work, n_fg, F, Bs, s0, s1, hist, n_slots, wyy, pack_bq);
-              else launch_pack<true, false>(fg, binmajor, grid, threads, lds, s, cc, Fp, ridx, va, vb, wk, n_work, n_fg, F, Bs, s0, s1, hist, n_slots, wyy, pack_bq); }
-    else { if (posv) launch_pack<false, true>(fg, binmajor, grid, threads, lds, s, cc, Fp, ridx, va, vb, wk, n_work, n_fg, F, Bs, s0, s1, hist, n_slots, wyy, pack_bq);
-           else launch_pack<false, false>(fg, binmajor, grid, threads, lds, s, cc, Fp, ridx, va, vb, wk, n_work, n_fg, F, Bs, s0, s1, hist, n_slots, wyy, pack_bq); }
+    if (vb) { if (posv) launch_pack<true, true>(fg, binmajor, grid, threads, lds, s, cc, Fp, ridx, va, vb, wk, n_work, n_fg, F, Bs, s0, s1, hist, n_slots, wyy, pack_bq, need);
+              else launch_pack<true, false>(fg, binmajor, grid, threads, lds, s, cc, Fp, ridx, va, vb, wk, n_work, n_fg, F, Bs, s0, s1, hist, n_slots, wyy, pack_bq, need); }
+    else { if (posv) launch_pack<false, true>(fg, binmajor, grid, threads, lds, s, cc, Fp, ridx, va, vb, wk, n_work, n_fg, F, Bs, s0, s1, hist, n_slots, wyy, pack_bq, need);
+           else launch_pack<false, false>(fg, binmajor, grid, threads, lds, s, cc, Fp, ridx, va, vb, wk, n_work, n_fg, F, Bs, s0, s1, hist, n_slots, wyy, pack_bq, need); }
     return (int)hipGetLastError();
   }
   switch (mode) {
@@ -361,7 +367,8 @@ extern "C" int h2o_hist_quad2(const void* codes, int Fp, const int* ridx, const 
 template <typename CodeT>
 static int launch_hist(const void* codes, int Fp, const int* ridx, const float* va, const float* vb,
                        const int4* work, int n_work, int F, int FG, int Bs, float s0, float s1, double* hist,
-                       int n_slots, int mode, int threads, double* wyy, int posv, hipStream_t s) {
+                       int n_slots, int mode, int threads, double* wyy, int posv, const uint8_t* need,
+                       hipStream_t s) {
   const int n_fg = (F + FG - 1) / FG;
   dim3 grid(n_work, n_fg);
   const int C = mode == 2 ? 1 : 2;
@@ -369,7 +376,7 @@ static int launch_hist(const void* codes, int Fp, const int* ridx, const float* 
   const CodeT* cc = (const CodeT*)codes;
   switch (mode) {
 #define H2O_LH(M, V) if (posv) H2O_LH2(M, V, true); else H2O_LH2(M, V, false)
-#define H2O_LH2(M, V, PV) hipLaunchKernelGGL((hist_build_kernel<CodeT, M, V, PV>), grid, dim3(threads), lds, s, cc, Fp, ridx, va, vb, work, F, Bs, FG, s0, s1, hist, n_slots, wyy)
+#define H2O_LH2(M, V, PV) hipLaunchKernelGGL((hist_build_kernel<CodeT, M, V, PV>), grid, dim3(threads), lds, s, cc, Fp, ridx, va, vb, work, F, Bs, FG, s0, s1, hist, n_slots, wyy, need)
     case 0: if (vb) H2O_LH(0, true); else H2O_LH(0, false); break;
     case 1: H2O_LH(1, true); break;
     default: if (vb) H2O_LH(2, true); else H2O_LH(2, false); break;
@@ -738,11 +745,12 @@ extern "C" {
 
 int h2o_hist_build(const void* codes, int code_bytes, int Fp, const int* ridx, const float* va,
                    const float* vb, const int* work, int n_work, int F, int FG, int Bs, float s0, float s1,
-                   double* hist, int n_slots, int mode, int threads, double* wyy, int posv, hipStream_t s) {
+                   double* hist, int n_slots, int mode, int threads, double* wyy, int posv, const uint8_t* need,
+                   hipStream_t s) {
   if (n_work <= 0) return 0;
   if (code_bytes == 1)
-    return launch_hist<uint8_t>(codes, Fp, ridx, va, vb, (const int4*)work, n_work, F, FG, Bs, s0, s1, hist, n_slots, mode, threads, wyy, posv, s);
-  return launch_hist<uint16_t>(codes, Fp, ridx, va, vb, (const int4*)work, n_work, F, FG, Bs, s0, s1, hist, n_slots, mode, threads, wyy, posv, s);
+    return launch_hist<uint8_t>(codes, Fp, ridx, va, vb, (const int4*)work, n_work, F, FG, Bs, s0, s1, hist, n_slots, mode, threads, wyy, posv, need, s);
+  return launch_hist<uint16_t>(codes, Fp, ridx, va, vb, (const int4*)work, n_work, F, FG, Bs, s0, s1, hist, n_slots, mode, threads, wyy, posv, need, s);
 }
 
 int h2o_part_flags(const void* codes, int code_bytes, long long rs, long long fs, const int* ridx,

@@ -42,13 +42,13 @@ def _lib():
     if lib is not None and not getattr(lib, "_typed", False):
         lib.h2o_hist_build.argtypes = [_c_void, _c_int, _c_int, _c_void, _c_void, _c_void, _c_void, _c_int,
                                        _c_int, _c_int, _c_int, ctypes.c_float, ctypes.c_float, _c_void, _c_int, _c_int,
-                                       _c_int, _c_void, _c_int, _c_void]
+                                       _c_int, _c_void, _c_int, _c_void, _c_void]
         lib.h2o_hist_quad.argtypes = [_c_void, _c_int, _c_void, _c_void, _c_void, _c_void, _c_int, _c_int, _c_int,
                                       ctypes.c_float, ctypes.c_float, _c_void, _c_int, _c_int, _c_int, _c_void,
                                       _c_int, _c_ll, _c_int, _c_void]
         lib.h2o_hist_quad2.argtypes = [_c_void, _c_int, _c_void, _c_void, _c_void, _c_void, _c_int, _c_int, _c_int,
                                        ctypes.c_float, ctypes.c_float, _c_void, _c_int, _c_int, _c_int, _c_void,
-                                       _c_int, _c_ll, _c_int, _c_int, _c_void]
+                                       _c_int, _c_ll, _c_int, _c_int, _c_void, _c_void]
         lib.h2o_part_flags.argtypes = [_c_void, _c_int, _c_ll, _c_ll, _c_void, _c_void, _c_void, _c_int, _c_void,
                                        _c_void, _c_int, _c_void, _c_void, _c_void]
         lib.h2o_part_compact.argtypes = [_c_void, _c_void, _c_void, _c_int, _c_void, _c_void, _c_void, _c_void,
@@ -148,11 +148,14 @@ def _pack_scale(vmax, chunk):
 
 
 def hist_build(bd, ridx, va, vb, mode, starts, counts, n_slots, use_native=None, target_blocks=2048, vmax=None,
-               want_wyy=False, posv=False, unit_w=False):
+               want_wyy=False, posv=False, unit_w=False, need_mask=None):
     """Histograms of the row segments [starts[i], starts[i]+counts[i]) of
     ridx into slot i.  Returns hist [F, n_slots, Bs, C] float64 (and, with
     want_wyy in mode 0, the per-slot sum of w*y*y).  posv: va/vb are stored
-    in position (row-permutation) order instead of row order."""
+    in position (row-permutation) order instead of row order.
+    need_mask: optional [n_slots, >=F] bool tensor of the features that will be
+    scored per slot (DRF mtries); feature groups with no needed feature are
+    skipped by the kernels and their histogram entries stay zero."""
     C = channels(mode)
     dev = ridx.device
     nh = bd.F * n_slots * bd.Bs * C
@@ -185,6 +188,15 @@ def hist_build(bd, ridx, va, vb, mode, starts, counts, n_slots, use_native=None,
         if len(items) == 0:
             return ret()
         work = _h2d(items, dev)
+
+        def _need(fg):
+            if need_mask is None:
+                return None
+            m = need_mask[:, :bd.F].to(device=dev, dtype=torch.bool)
+            ng = (bd.F + fg - 1) // fg
+            if ng * fg > bd.F:
+                m = torch.cat([m, torch.zeros((m.shape[0], ng * fg - bd.F), dtype=torch.bool, device=dev)], 1)
+            return m.view(m.shape[0], ng, fg).any(2).to(torch.uint8).contiguous()
         threads = 512 if chunk >= 8192 else 256
         if vmax is None:
             vmax = channel_max(va, vb, mode)
@@ -194,15 +206,17 @@ def hist_build(bd, ridx, va, vb, mode, starts, counts, n_slots, use_native=None,
             if mode == 0 and unit_w and chunk < (1 << 23) and os.environ.get("H2O3_HIST_PACK", "1") == "1":
                 s1, bq = _pack_scale(vmax[1] if vb is None else max(vmax[1], 0.0), chunk)
             binmajor = 1 if os.environ.get("H2O3_HIST_BINMAJOR", "0") == "1" else 0  # A/B: 47.9 vs 46.1 ms/tree, off
+            need = _need(qfg if bq >= 0 else 16)
             rc = lib.h2o_hist_quad2(_ptr(bd.codes), bd.Fp, _ptr(ridx), _ptr(va), _ptr(vb), _ptr(work), len(items),
                                     bd.F, bd.Bs, s0, s1, _ptr(hist), n_slots, mode, 512, _ptr(wyy),
-                                    1 if posv else 0, bq, qfg if bq >= 0 else 16, binmajor, _stream())
+                                    1 if posv else 0, bq, qfg if bq >= 0 else 16, binmajor, _ptr(need), _stream())
             if rc != 0:
                 raise RuntimeError(f"h2o_hist_quad failed: hip error {rc}")
             return ret()
+        need = _need(FG)
         rc = lib.h2o_hist_build(_ptr(bd.codes), bd.code_bytes, bd.Fp, _ptr(ridx), _ptr(va), _ptr(vb), _ptr(work),
                                 len(items), bd.F, FG, bd.Bs, s0, s1, _ptr(hist), n_slots, mode, threads, _ptr(wyy),
-                                1 if posv else 0, _stream())
+                                1 if posv else 0, _ptr(need), _stream())
         if rc != 0:
             raise RuntimeError(f"h2o_hist_build failed: hip error {rc}")
         return ret()

@@ -340,3 +340,56 @@ def test_cat_pair_kernel_matches_torch_gains(crit, nb):
     assert torch.equal(torch.isfinite(best), fin)
     torch.testing.assert_close(best[fin], bt[fin], rtol=1e-9, atol=1e-9)
     assert torch.equal(k[fin], kt[fin])
+
+
+@pytest.mark.parametrize("nbins", [255, 1000])
+@pytest.mark.parametrize("kernel", ["quad", "old"])
+def test_hist_need_mask_skips_groups(nbins, kernel, monkeypatch):
+    """need_mask (DRF mtries): groups holding a needed feature match the
+    unmasked native histogram exactly; groups with none stay zero."""
+    _need_gpu()
+    monkeypatch.setenv("H2O3_HIST_KERNEL", kernel)
+    from h2o3_amd.ops import tree_ops
+    bd, _ = _binned(F=40, nbins=nbins, cats=False)
+    n = bd.nrows_local
+    g = torch.Generator(device="cuda").manual_seed(3)
+    ridx = torch.randperm(n, generator=g, device="cuda").to(torch.int32)
+    va = torch.randn(n, generator=g, device="cuda")
+    vb = torch.rand(n, generator=g, device="cuda")
+    starts, counts = [0, 6000, 13000], [6000, 7000, 7000]
+    need = torch.zeros((3, bd.F), dtype=torch.bool, device="cuda")
+    need[0, [0, 3]] = True
+    need[1, [0, 37]] = True
+    need[2, [0, 20, 21]] = True
+    full = tree_ops.hist_build(bd, ridx, va, vb, 1, starts, counts, 3, use_native=True)
+    part = tree_ops.hist_build(bd, ridx, va, vb, 1, starts, counts, 3, use_native=True, need_mask=need)
+    for s in range(3):
+        for f in torch.nonzero(need[s]).flatten().tolist():
+            torch.testing.assert_close(part[f, s], full[f, s], rtol=0, atol=0)
+    # features far from every needed one (group size <= 16) are skipped
+    assert float(part[10, 0].abs().sum()) == 0.0
+    assert float(part[5, 1].abs().sum()) == 0.0
+
+
+def test_drf_chunked_need_mask_same_model(monkeypatch):
+    """Deep chunked DRF levels with the need mask grow the same trees as
+    with full histograms."""
+    _need_gpu()
+    import pandas as pd
+    import h2o3_amd
+    from h2o3_amd.estimators import H2ORandomForestEstimator
+    h2o3_amd.init(device="cuda:0", verbose=False)
+    rng = np.random.RandomState(0)
+    n, F = 20000, 48
+    X = rng.randn(n, F).astype(np.float32)
+    df = pd.DataFrame(X, columns=[f"x{i}" for i in range(F)])
+    df["y"] = X[:, 0] + X[:, 7] * X[:, 30] + 0.1 * rng.randn(n)
+    fr = h2o3_amd.H2OFrame(df)
+    monkeypatch.setenv("H2O3_HIST_BUDGET", str(1 << 20))   # force the chunked path
+    preds = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("H2O3_HIST_NEED", flag)
+        m = H2ORandomForestEstimator(ntrees=3, max_depth=12, seed=7, mtries=6)
+        m.train(y="y", training_frame=fr)
+        preds.append(m.predict(fr).as_data_frame().values[:, 0])
+    np.testing.assert_allclose(preds[0], preds[1], rtol=1e-6, atol=1e-6)
