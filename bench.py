@@ -115,7 +115,7 @@ def main():
         step = drv.step
         metric = "drf_trees_per_sec"
         unit = "trees/s"
-        model = f"DRF binomial {args.rows // 1_000_000}Mx{F} ({n_cat} cat, card {args.cat_card}) ntrees=1000"
+        model = f"DRF binomial {args.rows // 1_000_000}Mx{F} ({args.cat_cols} cat, card {args.cat_card}) ntrees=1000"
     else:
         from h2o3_amd.models.glm.glm import GLMDriver, H2OGeneralizedLinearEstimator
         est = H2OGeneralizedLinearEstimator(family="binomial", solver="IRLSM", lambda_=0.0)

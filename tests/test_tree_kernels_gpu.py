@@ -367,8 +367,16 @@ def test_hist_need_mask_skips_groups(nbins, kernel, monkeypatch):
         for f in torch.nonzero(need[s]).flatten().tolist():
             torch.testing.assert_close(part[f, s], full[f, s], rtol=0, atol=0)
     # features far from every needed one (group size <= 16) are skipped
-    assert float(part[10, 0].abs().sum()) == 0.0
-    assert float(part[5, 1].abs().sum()) == 0.0
+    # every other (feature, slot) histogram is either the full one (same
+    # group as a needed feature) or skipped (all zero); some must be skipped
+    skipped = 0
+    for s in range(3):
+        for f in range(bd.F):
+            if float(part[f, s].abs().sum()) == 0.0 and float(full[f, s].abs().sum()) > 0.0:
+                skipped += 1
+            else:
+                torch.testing.assert_close(part[f, s], full[f, s], rtol=0, atol=0)
+    assert skipped > 0
 
 
 def test_drf_chunked_need_mask_same_model(monkeypatch):
