@@ -27,6 +27,7 @@
 // Histogram layout in HBM: hist[F][n_slots][Bs][C] f64 (feature-major so a
 // multi-GPU reduce-scatter can shard by feature).
 #include "common.h"
+#include <stdlib.h>
 
 template <int MODE> struct Chan { static constexpr int C = MODE == 2 ? 1 : 2; };
 
@@ -133,17 +134,23 @@ __global__ __launch_bounds__(512) void hist_build_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// Quad-lane histogram kernel for uint8 codes (rows 16-byte aligned, Fp%16==0).
-// A workgroup owns 16 features; lane = (row_sub in 0..15, quad q in 0..3):
-// each lane loads ONE dword = 4 consecutive codes of its row and performs
-// 4 x C LDS atomics, so a wave instruction covers 16 rows x 16 features with
-// 4x fewer global load instructions than one byte per lane.  Per-feature LDS
-// regions are padded by C entries so equal bins of neighbouring features do
-// not land on the same LDS bank.  Blocks are ordered (chunk, feature-group)
-// with the group fastest and remapped XCD-contiguously, so the feature-group
-// blocks of one row chunk run on the same XCD and share its L2 for the row
-// gathers (codes, ridx, va, vb).
-// ---------------------------------------------------------------------------
+// Grouped-lane histogram kernel for uint8 codes (rows 8-byte aligned).
+// A workgroup owns one group of fgw features (runtime, a multiple of 4*LW,
+// at most 64*LW); lane = (row_sub, slot q): each lane loads LW dwords = 4*LW
+// consecutive codes of its row and performs 4*LW x C LDS atomics, so a wave
+// instruction covers floor(64 / (fgw / 4LW)) rows.  Per-feature LDS regions
+// are padded by C entries.  Blocks are ordered (chunk, group) with the group
+// fastest and remapped XCD-contiguously, so the group blocks of one row chunk
+// run on the same XCD and share its L2 lines for the row gathers.
+//
+// What bounds it (MI355X, scripts/hist_fsweep_mb.py + scripts/pmc_hist.sh):
+// the cost is per group PASS over the rows, not per feature -- F = 100 at
+// 4 x 32 lanes took as long as F = 128, and a separate tail launch for
+// features 96..99 cost as much as a full pass because it re-reads every
+// 128-B code row from HBM.  So the host picks the FEWEST groups that fit the
+// LDS budget (F = 100 -> 3 groups of 36 features: 9 lanes per row, 7 rows per
+// wave instruction, 63 of 64 lanes busy) in ONE launch.
+//
 // PACK (MODE 0, weights all 0/1): ONE 64-bit LDS atomic per (row, feature):
 // bits 63..40 = row count, bits 39..0 = sum of the biased fixed-point
 // response q + Bq (q = rint(y * s1), Bq = rint(vmax * s1) so every term is
@@ -151,80 +158,111 @@ __global__ __launch_bounds__(512) void hist_build_kernel(
 // count and (low - count * Bq) / s1.  Halves the LDS atomics of the
 // unweighted GBM / sampled DRF histograms; the response is quantised at
 // 1/s1 = chunk * 2 * vmax / 2^40 (f32-level resolution, exact summation).
-// BINMAJOR (PACK only, FG 16/32): the LDS histogram is laid out [bin][feature]
-// instead of [feature][bin], and the rows sharing a 16-lane LDS group walk
-// their 4 codes in rotated order, so the 16 lanes of every group update 16
-// DIFFERENT features of whatever bins they hit: with 64-bit entries the bank
-// pair is 2*(bin*FG + f) mod 64 = 2f (+32 for odd bins at FG=16), distinct per
-// lane -> conflict-free LDS atomics for random bins (the [feature][bin] layout
-// conflicts at random).
-template <int MODE, bool HAS_VB, bool POSV, bool PACK, int FG = 16, bool BINMAJOR = false>
+//
+// PIPE: the code/response gathers of iteration i+1 and the row indices of
+// iteration i+2 are issued before the atomics of iteration i (PMC on the
+// unpipelined loop: SQ_WAIT_ANY = 69% of wave cycles, waves parked on the
+// dependent ridx -> codes gathers; pipelined: root 6.8 -> 5.5 ms, depth-3
+// level 4.2 -> 2.9 ms at 100M x 100).  Loads use clamped indices, so no
+// branch guards them.
+// ---------------------------------------------------------------------------
+template <int LW> struct CodeW { using T = unsigned int; };
+template <> struct CodeW<2> { using T = uint2; };
+__device__ __forceinline__ unsigned int code_at(unsigned int w, int hi, int sh) { return (w >> sh) & 0xffu; }
+__device__ __forceinline__ unsigned int code_at(uint2 w, int hi, int sh) { return ((hi ? w.y : w.x) >> sh) & 0xffu; }
+
+template <int MODE, bool HAS_VB, bool POSV, bool PACK, bool PIPE = true, int LW = 1>
 __global__ __launch_bounds__(512) void hist_quad_kernel(
     const uint8_t* __restrict__ codes, int Fp, const int* __restrict__ ridx,
     const float* __restrict__ va, const float* __restrict__ vb,
-    const int4* __restrict__ work, int n_work, int n_fg, int F, int Bs, float s0, float s1,
+    const int4* __restrict__ work, int n_work, int n_fg, int fgw, int F, int foff, int Bs, float s0, float s1,
     double* __restrict__ hist, int n_slots, double* __restrict__ wyy_out, long long bq,
     const uint8_t* __restrict__ need) {
+  using CT = typename CodeW<LW>::T;
   constexpr int C = Chan<MODE>::C;
   constexpr int CL = PACK ? 1 : C;       // u64 entries per bin in LDS
-  constexpr int LPR = FG / 4;            // lanes per row (one dword of codes each)
-  constexpr int RPW = 64 / LPR;          // rows per wave instruction
+  constexpr int NK = 4 * LW;             // features per lane
+  constexpr int U = 4;                   // rows per lane per iteration
   extern __shared__ __attribute__((aligned(16))) unsigned long long ldsq[];
   const int nwg = n_work * n_fg;
   const int lb = xcd_remap(blockIdx.x, nwg);
   const int fgi = lb % n_fg;
   const int4 wk = work[lb / n_fg];
   if (need != nullptr && need[(size_t)wk.x * n_fg + fgi] == 0) return;   // no eligible feature in this group
-  const int fg0 = fgi * FG;
-  const int nf = min(FG, F - fg0);
+  const int fg0 = foff + fgi * fgw;
+  const int nf = min(fgw, F - fg0);
+  const int LPR = fgw / NK;              // lanes per row
+  const int RPW = 64 / LPR;              // rows per wave instruction (64 % LPR lanes idle)
   const int stride_f = Bs * CL + CL;
-  const int total = FG * stride_f;
+  const int total = fgw * stride_f;
   for (int i = threadIdx.x; i < total; i += blockDim.x) ldsq[i] = 0ull;
   __syncthreads();
   const int lane = threadIdx.x & 63;
-  const int q = lane % LPR;        // feature quad
+  const int q = lane % LPR;        // feature slot of the lane
   const int rs = lane / LPR;       // row within the wave instruction
+  const bool lane_ok = rs < RPW;
   const int wv = threadIdx.x >> 6;
   const int nwaves = blockDim.x >> 6;
-  const bool do_wyy = (MODE == 0) && wyy_out != nullptr && fgi == 0 && q == 0;
+  const bool do_wyy = (MODE == 0) && wyy_out != nullptr && fgi == 0 && q == 0 && lane_ok;
   double wyy = 0.0;
   const int pend = wk.y + wk.z;
   const int step = nwaves * RPW;
-  constexpr int U = 4;
-  const uint8_t* cbase = codes + fg0 + 4 * q;
-  unsigned long long* hb[4];
-  bool fk[4];
-  int kk[4];    // code byte handled at step k (rotated per row inside a 16-lane group)
-  constexpr int RPG = 16 / LPR > 0 ? 16 / LPR : 1;     // rows per 16-lane LDS group
-  const int rot = BINMAJOR ? (rs % RPG) * (4 / RPG) : 0;
+  const uint8_t* cbase = codes + fg0 + NK * q;
+  unsigned long long* hb[NK];
+  bool fk[NK];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    kk[k] = (k + rot) & 3;
-    hb[k] = BINMAJOR ? ldsq + (4 * q + kk[k]) : ldsq + (4 * q + k) * stride_f;
-    fk[k] = 4 * q + kk[k] < nf;
+  for (int k = 0; k < NK; ++k) {
+    hb[k] = ldsq + (NK * q + k) * stride_f;
+    fk[k] = lane_ok && NK * q + k < nf;
   }
-  for (int p0 = wk.y + wv * RPW + rs; p0 < pend; p0 += U * step) {
-    int rr[U];
-    unsigned int cw[U];
-    float c0[U], c1[U], yv[U];
+  const int p_first = wk.y + wv * RPW + (lane_ok ? rs : 0);
+  int rA[U], rB[U];
+  CT cwA[U];
+  float xaA[U], xbA[U];
+  auto load_r = [&](int p, int (&r)[U]) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) rr[u] = ridx[min(p0 + u * step, pend - 1)];
+    for (int u = 0; u < U; ++u) r[u] = ridx[min(p + u * step, pend - 1)];
+  };
+  auto load_v = [&](int p, const int (&r)[U], CT (&cw)[U], float (&xa)[U], float (&xb)[U]) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int r = rr[u];
-      const int vi = POSV ? min(p0 + u * step, pend - 1) : r;
+      const int vi = POSV ? min(p + u * step, pend - 1) : r[u];
+      xa[u] = (MODE == 2) ? 0.f : va[vi];
+      xb[u] = (HAS_VB || MODE == 1) ? vb[vi] : 1.f;
+      cw[u] = *reinterpret_cast<const CT*>(cbase + (size_t)r[u] * Fp);
+    }
+  };
+  if (PIPE) {
+    load_r(p_first, rA);
+    load_v(p_first, rA, cwA, xaA, xbA);
+    load_r(p_first + U * step, rB);
+  }
+  for (int p0 = p_first; p0 < pend; p0 += U * step) {
+    CT cw[U];
+    float c0[U], c1[U], yv[U], xa[U], xb[U];
+    if (PIPE) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) { cw[u] = cwA[u]; xa[u] = xaA[u]; xb[u] = xbA[u]; }
+      load_v(p0 + U * step, rB, cwA, xaA, xbA);
+      load_r(p0 + 2 * U * step, rB);
+    } else {
+      int rr[U];
+      load_r(p0, rr);
+      load_v(p0, rr, cw, xa, xb);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
       if (MODE == 0) {
         // without vb a NaN response marks a zero-weight row (out-of-bag /
         // sampled-out): one gather per row instead of two
-        const float y = va[vi];
-        const float w = HAS_VB ? vb[vi] : (y == y ? 1.f : 0.f);
+        const float y = xa[u];
+        const float w = HAS_VB ? xb[u] : (y == y ? 1.f : 0.f);
         c0[u] = w; c1[u] = w != 0.f ? w * y : 0.f; yv[u] = w != 0.f ? y : 0.f;
       } else if (MODE == 1) {
-        c0[u] = va[vi]; c1[u] = vb[vi]; yv[u] = 0.f;
+        c0[u] = xa[u]; c1[u] = xb[u]; yv[u] = 0.f;
       } else {
-        c0[u] = HAS_VB ? vb[vi] : 1.f; c1[u] = 0.f; yv[u] = 0.f;
+        c0[u] = xb[u]; c1[u] = 0.f; yv[u] = 0.f;
       }
-      cw[u] = *reinterpret_cast<const unsigned int*>(cbase + (size_t)r * Fp);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -234,10 +272,9 @@ __global__ __launch_bounds__(512) void hist_quad_kernel(
       if (PACK) {
         const unsigned long long a = (1ull << 40) + (unsigned long long)(__float2ll_rn(yv[u] * s1) + bq);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < NK; ++k) {
           if (!fk[k]) continue;
-          const unsigned int code = (cw[u] >> (8 * kk[k])) & 0xffu;
-          __hip_atomic_fetch_add(hb[k] + (BINMAJOR ? code * FG : code), a, __ATOMIC_RELAXED,
+          __hip_atomic_fetch_add(hb[k] + code_at(cw[u], k >> 2, 8 * (k & 3)), a, __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         continue;
@@ -245,9 +282,9 @@ __global__ __launch_bounds__(512) void hist_quad_kernel(
       const unsigned long long a0 = (unsigned long long)__float2ll_rn(c0[u] * s0);
       const unsigned long long a1 = (unsigned long long)__float2ll_rn(c1[u] * s1);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
+      for (int k = 0; k < NK; ++k) {
         if (!fk[k]) continue;
-        unsigned long long* h = hb[k] + ((cw[u] >> (8 * kk[k])) & 0xffu) * CL;
+        unsigned long long* h = hb[k] + code_at(cw[u], k >> 2, 8 * (k & 3)) * CL;
         __hip_atomic_fetch_add(h, a0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (C > 1) __hip_atomic_fetch_add(h + 1, a1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
@@ -263,10 +300,9 @@ __global__ __launch_bounds__(512) void hist_quad_kernel(
   if (PACK) {
     const int tot = nf * Bs;
     for (int i = threadIdx.x; i < tot; i += blockDim.x) {
-      // bin-major: consecutive threads read consecutive features of a bin (no LDS conflicts)
-      const int j = BINMAJOR ? i % nf : i / Bs;
-      const int b = BINMAJOR ? i / nf : i - j * Bs;
-      const unsigned long long v = BINMAJOR ? ldsq[b * FG + j] : ldsq[j * stride_f + b];
+      const int j = i / Bs;
+      const int b = i - j * Bs;
+      const unsigned long long v = ldsq[j * stride_f + b];
       if (v != 0) {
         const long long cnt = (long long)(v >> 40);
         const long long low = (long long)(v & ((1ull << 40) - 1));
@@ -289,78 +325,71 @@ __global__ __launch_bounds__(512) void hist_quad_kernel(
   }
 }
 
-template <bool V, bool PV, int G, bool BM>
-static void launch_pack1(dim3 grid, int threads, size_t lds, hipStream_t s, const uint8_t* cc, int Fp, const int* ridx,
-                         const float* va, const float* vb, const int4* wk, int n_work, int n_fg, int F, int Bs,
-                         float s0, float s1, double* hist, int n_slots, double* wyy, long long bq,
-                         const uint8_t* need) {
-  hipLaunchKernelGGL((hist_quad_kernel<0, V, PV, true, G, BM>), grid, dim3(threads), lds, s, cc, Fp, ridx, va, vb, wk,
-                     n_work, n_fg, F, Bs, s0, s1, hist, n_slots, wyy, bq, need);
+struct QuadArgs {
+  dim3 grid; int threads; size_t lds; hipStream_t s;
+  const uint8_t* cc; int Fp; const int* ridx; const float* va; const float* vb; const int4* wk;
+  int n_work, n_fg, fgw, F, foff, Bs; float s0, s1; double* hist; int n_slots; double* wyy; long long bq;
+  const uint8_t* need;
+};
+
+template <int M, bool V, bool PV, bool PK, bool PIPE = true, int LW = 1>
+static void lq(const QuadArgs& a) {
+  hipLaunchKernelGGL((hist_quad_kernel<M, V, PV, PK, PIPE, LW>), a.grid, dim3(a.threads), a.lds, a.s, a.cc, a.Fp,
+                     a.ridx, a.va, a.vb, a.wk, a.n_work, a.n_fg, a.fgw, a.F, a.foff, a.Bs, a.s0, a.s1, a.hist,
+                     a.n_slots, a.wyy, a.bq, a.need);
 }
 
-template <bool V, bool PV>
-static void launch_pack(int fg, int binmajor, dim3 grid, int threads, size_t lds, hipStream_t s, const uint8_t* cc,
-                        int Fp, const int* ridx, const float* va, const float* vb, const int4* wk, int n_work,
-                        int n_fg, int F, int Bs, float s0, float s1, double* hist, int n_slots, double* wyy,
-                        long long bq, const uint8_t* need) {
-  if (fg == 64)
-    launch_pack1<V, PV, 64, false>(grid, threads, lds, s, cc, Fp, ridx, va, vb, wk, n_work, n_fg, F, Bs, s0, s1, hist, n_slots, wyy, bq, need);
-  else if (fg == 32 && binmajor)
-    launch_pack1<V, PV, 32, true>(grid, threads, lds, s, cc, Fp, ridx, va, vb, wk, n_work, n_fg, F, Bs, s0, s1, hist, n_slots, wyy, bq, need);
-  else if (fg == 32)
-    launch_pack1<V, PV, 32, false>(grid, threads, lds, s, cc, Fp, ridx, va, vb, wk, n_work, n_fg, F, Bs, s0, s1, hist, n_slots, wyy, bq, need);
-  else if (binmajor)
-    launch_pack1<V, PV, 16, true>(grid, threads, lds, s, cc, Fp, ridx, va, vb, wk, n_work, n_fg, F, Bs, s0, s1, hist, n_slots, wyy, bq, need);
-  else
-    launch_pack1<V, PV, 16, false>(grid, threads, lds, s, cc, Fp, ridx, va, vb, wk, n_work, n_fg, F, Bs, s0, s1, hist, n_slots, wyy, bq, need);
+static int env_int(const char* k, int d) {
+  const char* v = getenv(k);
+  return v ? atoi(v) : d;
 }
 
+// A/B switches: H2O3_HIST_PIPE=0 (unpipelined loop), H2O3_HIST_LW=2 (8 codes
+// per lane: one dwordx2 gather; measured 0-6% faster on scattered deep levels,
+// 5-10% slower at the contiguous root, off by default)
+template <int M, bool V, bool PV, bool PK>
+static void lq_var(int lw, const QuadArgs& a) {
+  static const int pipe = env_int("H2O3_HIST_PIPE", 1);
+  if (!pipe) lq<M, V, PV, PK, false>(a);
+  else if (lw == 2) lq<M, V, PV, PK, true, 2>(a);
+  else lq<M, V, PV, PK>(a);
+}
+
+template <int M, bool V>
+static void lq_pv(int posv, int pack, int lw, const QuadArgs& a) {
+  if (pack) { if (posv) lq_var<M, V, true, true>(lw, a); else lq_var<M, V, false, true>(lw, a); }
+  else { if (posv) lq_var<M, V, true, false>(lw, a); else lq_var<M, V, false, false>(lw, a); }
+}
+
+// Histograms of features [foff, F) in n_fg = ceil((F - foff) / fgw) groups of
+// fgw features (a multiple of 4, at most 64; tree_ops.quad_groups picks it).
 // pack_bq >= 0 selects the packed single-atomic path (MODE 0, 0/1 weights).
-extern "C" int h2o_hist_quad2(const void* codes, int Fp, const int* ridx, const float* va, const float* vb,
-                              const int* work, int n_work, int F, int Bs, float s0, float s1, double* hist,
-                              int n_slots, int mode, int threads, double* wyy, int posv, long long pack_bq,
-                              int fg, int binmajor, const uint8_t* need, hipStream_t s);
-extern "C" int h2o_hist_quad(const void* codes, int Fp, const int* ridx, const float* va, const float* vb,
-                             const int* work, int n_work, int F, int Bs, float s0, float s1, double* hist,
-                             int n_slots, int mode, int threads, double* wyy, int posv, long long pack_bq,
-                             int fg, hipStream_t s) {
-  return h2o_hist_quad2(codes, Fp, ridx, va, vb, work, n_work, F, Bs, s0, s1, hist, n_slots, mode, threads, wyy,
-                        posv, pack_bq, fg, 0, nullptr, s);
-}
-
-extern "C" int h2o_hist_quad2(const void* codes, int Fp, const int* ridx, const float* va, const float* vb,
-                              const int* work, int n_work, int F, int Bs, float s0, float s1, double* hist,
-                              int n_slots, int mode, int threads, double* wyy, int posv, long long pack_bq,
-                              int fg, int binmajor, const uint8_t* need, hipStream_t s) {
-  if (n_work <= 0) return 0;
-  if (Fp % 16 != 0 || Bs > 256) return -1;
+extern "C" int h2o_hist_quad3(const void* codes, int Fp, const int* ridx, const float* va, const float* vb,
+                              const int* work, int n_work, int F, int foff, int Bs, float s0, float s1,
+                              double* hist, int n_slots, int mode, int threads, double* wyy, int posv,
+                              long long pack_bq, int fgw, const uint8_t* need, hipStream_t s) {
+  if (n_work <= 0 || foff >= F) return 0;
+  if (Fp % 4 != 0 || foff % 4 != 0 || Bs > 256 || mode < 0 || mode > 2) return -1;
+  if (fgw < 4 || fgw > 64 || fgw % 4 != 0) return -2;
   const bool pack = pack_bq >= 0 && mode == 0;
-  if (!pack || (fg != 32 && fg != 64) || Fp % fg != 0) fg = 16;
-  const int n_fg = (F + fg - 1) / fg;
+  const int n_fg = (F - foff + fgw - 1) / fgw;
+  if (foff + n_fg * fgw > Fp) return -3;       // every code dword read lies inside the row
+  static const int lw_env = env_int("H2O3_HIST_LW", 1);
+  const int lw = (lw_env == 2 && fgw % 8 == 0 && foff % 8 == 0 && Fp % 8 == 0) ? 2 : 1;
   const int C = mode == 2 ? 1 : 2;
   const int CL = pack ? 1 : C;
-  const size_t lds = (size_t)fg * (Bs * CL + CL) * sizeof(unsigned long long);
-  const dim3 grid(n_work * n_fg);
-  const uint8_t* cc = (const uint8_t*)codes;
-  const int4* wk = (const int4*)work;
-#define H2O_LQ2(M, V, PV, PK) hipLaunchKernelGGL((hist_quad_kernel<M, V, PV, PK>), grid, dim3(threads), lds, s, cc, \
-                                                 Fp, ridx, va, vb, wk, n_work, n_fg, F, Bs, s0, s1, hist, n_slots, \
-                                                 wyy, pack_bq, need)
-#define H2O_LQ(M, V) if (posv) H2O_LQ2(M, V, true, false); else H2O_LQ2(M, V, false, false)
-  if (pack) {
-    if (vb) { if (posv) launch_pack<true, true>(fg, binmajor, grid, threads, lds, s, cc, Fp, ridx, va, vb, wk, n_work, n_fg, F, Bs, s0, s1, hist, n_slots, wyy, pack_bq, need);
-              else launch_pack<true, false>(fg, binmajor, grid, threads, lds, s, cc, Fp, ridx, va, vb, wk, n_work, n_fg, F, Bs, s0, s1, hist, n_slots, wyy, pack_bq, need); }
-    else { if (posv) launch_pack<false, true>(fg, binmajor, grid, threads, lds, s, cc, Fp, ridx, va, vb, wk, n_work, n_fg, F, Bs, s0, s1, hist, n_slots, wyy, pack_bq, need);
-           else launch_pack<false, false>(fg, binmajor, grid, threads, lds, s, cc, Fp, ridx, va, vb, wk, n_work, n_fg, F, Bs, s0, s1, hist, n_slots, wyy, pack_bq, need); }
-    return (int)hipGetLastError();
-  }
+  QuadArgs a;
+  a.grid = dim3(n_work * n_fg); a.threads = threads;
+  a.lds = (size_t)fgw * (Bs * CL + CL) * sizeof(unsigned long long); a.s = s;
+  if (a.lds > 160 * 1024) return -4;
+  a.cc = (const uint8_t*)codes; a.Fp = Fp; a.ridx = ridx; a.va = va; a.vb = vb; a.wk = (const int4*)work;
+  a.n_work = n_work; a.n_fg = n_fg; a.fgw = fgw; a.F = F; a.foff = foff; a.Bs = Bs; a.s0 = s0; a.s1 = s1;
+  a.hist = hist; a.n_slots = n_slots; a.wyy = wyy; a.bq = pack_bq; a.need = need;
   switch (mode) {
-    case 0: if (vb) H2O_LQ(0, true); else H2O_LQ(0, false); break;
-    case 1: H2O_LQ(1, true); break;
-    default: if (vb) H2O_LQ(2, true); else H2O_LQ(2, false); break;
+    case 0: if (vb) lq_pv<0, true>(posv, pack, lw, a); else lq_pv<0, false>(posv, pack, lw, a); break;
+    case 1: lq_pv<1, true>(posv, 0, lw, a); break;
+    default: if (vb) lq_pv<2, true>(posv, 0, lw, a); else lq_pv<2, false>(posv, 0, lw, a); break;
   }
-#undef H2O_LQ
-#undef H2O_LQ2
   return (int)hipGetLastError();
 }
 

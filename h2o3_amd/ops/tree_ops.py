@@ -43,12 +43,9 @@ def _lib():
         lib.h2o_hist_build.argtypes = [_c_void, _c_int, _c_int, _c_void, _c_void, _c_void, _c_void, _c_int,
                                        _c_int, _c_int, _c_int, ctypes.c_float, ctypes.c_float, _c_void, _c_int, _c_int,
                                        _c_int, _c_void, _c_int, _c_void, _c_void]
-        lib.h2o_hist_quad.argtypes = [_c_void, _c_int, _c_void, _c_void, _c_void, _c_void, _c_int, _c_int, _c_int,
-                                      ctypes.c_float, ctypes.c_float, _c_void, _c_int, _c_int, _c_int, _c_void,
-                                      _c_int, _c_ll, _c_int, _c_void]
-        lib.h2o_hist_quad2.argtypes = [_c_void, _c_int, _c_void, _c_void, _c_void, _c_void, _c_int, _c_int, _c_int,
-                                       ctypes.c_float, ctypes.c_float, _c_void, _c_int, _c_int, _c_int, _c_void,
-                                       _c_int, _c_ll, _c_int, _c_int, _c_void, _c_void]
+        lib.h2o_hist_quad3.argtypes = [_c_void, _c_int, _c_void, _c_void, _c_void, _c_void, _c_int, _c_int, _c_int,
+                                       _c_int, ctypes.c_float, ctypes.c_float, _c_void, _c_int, _c_int, _c_int,
+                                       _c_void, _c_int, _c_ll, _c_int, _c_void, _c_void]
         lib.h2o_part_flags.argtypes = [_c_void, _c_int, _c_ll, _c_ll, _c_void, _c_void, _c_void, _c_int, _c_void,
                                        _c_void, _c_int, _c_void, _c_void, _c_void]
         lib.h2o_part_compact.argtypes = [_c_void, _c_void, _c_void, _c_int, _c_void, _c_void, _c_void, _c_void,
@@ -91,6 +88,23 @@ def feature_group(F: int, Bs: int, mode: int, budget: int = _LDS_BUDGET) -> int:
         if fgl == 1:
             break
     return best[1] if best else 1
+
+
+def quad_groups(F: int, Fp: int, Bs: int, pack: bool, budget: int = _LDS_BUDGET):
+    """(n_fg, fgw) of the grouped-lane histogram kernel: the FEWEST feature
+    groups whose LDS histogram (fgw x (Bs + 1) x channels x 8 B) fits the
+    per-workgroup budget (2 workgroups per CU), widths a multiple of 4 and at
+    most 64, all in one launch (the kernel's cost is per group pass over the
+    rows: scripts/hist_fsweep_mb.py).  F = 100, 256 bins, packed -> 3 x 36."""
+    CL = 1 if pack else 2
+    fmax = max(4, min(64, (budget // ((Bs * CL + CL) * 8)) // 4 * 4))
+    fmax = int(os.environ.get("H2O3_HIST_FGW", fmax))
+    n_fg = -(-F // fmax)
+    while True:
+        fgw = -(-(-(-F // n_fg)) // 4) * 4
+        if n_fg * fgw <= Fp or fgw <= 4:
+            return n_fg, fgw
+        n_fg += 1
 
 
 def make_work(starts, counts, slots, chunk):
@@ -171,19 +185,22 @@ def hist_build(bd, ridx, va, vb, mode, starts, counts, n_slots, use_native=None,
     native = dev.type == "cuda" if use_native is None else use_native
     if native:
         lib = _lib()
-        quad = bd.code_bytes == 1 and bd.Fp % 16 == 0 and bd.Bs <= 256 and \
-            os.environ.get("H2O3_HIST_KERNEL", "quad") == "quad"
-        qfg = int(os.environ.get("H2O3_HIST_FG", "32"))
-        pack_ok = quad and mode == 0 and unit_w and os.environ.get("H2O3_HIST_PACK", "1") == "1"
-        if not pack_ok or qfg not in (32, 64) or bd.Fp % qfg != 0:
-            qfg = 16
-        FG = qfg if quad else feature_group(bd.F, bd.Bs, mode)
-        n_fg = (bd.F + FG - 1) // FG
+        kern = os.environ.get("H2O3_HIST_KERNEL", "quad")
         total = int(sum(counts))
         if total == 0:
             return ret()
+        quad = bd.code_bytes == 1 and bd.Fp % 4 == 0 and bd.Bs <= 256 and kern == "quad" and mode in (0, 1, 2)
+        pack = quad and mode == 0 and unit_w and os.environ.get("H2O3_HIST_PACK", "1") == "1"
+        if quad:
+            n_fg, fgw = quad_groups(bd.F, bd.Fp, bd.Bs, pack)
+        else:
+            FG = feature_group(bd.F, bd.Bs, mode)
+            n_fg = (bd.F + FG - 1) // FG
         tgt_chunks = max(1, target_blocks // n_fg)
         chunk = max(2048, -(-total // tgt_chunks))
+        if pack and chunk >= (1 << 23):
+            pack = False
+            n_fg, fgw = quad_groups(bd.F, bd.Fp, bd.Bs, False)
         items = make_work(starts, counts, range(n_slots), chunk)
         if len(items) == 0:
             return ret()
@@ -203,15 +220,14 @@ def hist_build(bd, ridx, va, vb, mode, starts, counts, n_slots, use_native=None,
         s0, s1 = (fixed_point_scale(m, chunk) for m in vmax)
         if quad:
             bq = -1
-            if mode == 0 and unit_w and chunk < (1 << 23) and os.environ.get("H2O3_HIST_PACK", "1") == "1":
+            if pack:
                 s1, bq = _pack_scale(vmax[1] if vb is None else max(vmax[1], 0.0), chunk)
-            binmajor = 1 if os.environ.get("H2O3_HIST_BINMAJOR", "0") == "1" else 0  # A/B: 47.9 vs 46.1 ms/tree, off
-            need = _need(qfg if bq >= 0 else 16)
-            rc = lib.h2o_hist_quad2(_ptr(bd.codes), bd.Fp, _ptr(ridx), _ptr(va), _ptr(vb), _ptr(work), len(items),
-                                    bd.F, bd.Bs, s0, s1, _ptr(hist), n_slots, mode, 512, _ptr(wyy),
-                                    1 if posv else 0, bq, qfg if bq >= 0 else 16, binmajor, _ptr(need), _stream())
+            need = _need(fgw)
+            rc = lib.h2o_hist_quad3(_ptr(bd.codes), bd.Fp, _ptr(ridx), _ptr(va), _ptr(vb), _ptr(work), len(items),
+                                    bd.F, 0, bd.Bs, s0, s1, _ptr(hist), n_slots, mode, 512, _ptr(wyy),
+                                    1 if posv else 0, bq, fgw, _ptr(need), _stream())
             if rc != 0:
-                raise RuntimeError(f"h2o_hist_quad failed: hip error {rc}")
+                raise RuntimeError(f"h2o_hist_quad3 failed: error {rc} (F={bd.F}, Fp={bd.Fp}, fgw={fgw})")
             return ret()
         need = _need(FG)
         rc = lib.h2o_hist_build(_ptr(bd.codes), bd.code_bytes, bd.Fp, _ptr(ridx), _ptr(va), _ptr(vb), _ptr(work),

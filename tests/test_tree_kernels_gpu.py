@@ -28,7 +28,7 @@ def _binned(n=20000, F=13, nbins=255, seed=0, cats=True):
     return bd, feats
 
 
-@pytest.mark.parametrize("nbins,mode", [(255, 0), (255, 1), (20, 0), (1000, 0), (1000, 1)])
+@pytest.mark.parametrize("nbins,mode", [(255, 0), (255, 1), (255, 2), (20, 0), (1000, 0), (1000, 1)])
 @pytest.mark.parametrize("kernel", ["quad", "old"])
 def test_hist_build_matches_reference(nbins, mode, kernel, monkeypatch):
     _need_gpu()
@@ -287,14 +287,15 @@ def test_cat_pair_splits_match_dense_torch(crit):
     torch.testing.assert_close(a["L"][fin], b["L"][fin])
 
 
-@pytest.mark.parametrize("fg", ["16", "32"])
-@pytest.mark.parametrize("binmajor", ["0", "1"])
-def test_packed_hist_binmajor_matches_reference(fg, binmajor, monkeypatch):
-    """Packed single-atomic histogram, [bin][feature] conflict-free LDS layout vs
-    [feature][bin] and the torch reference."""
+@pytest.mark.parametrize("fgw", ["4", "12", "36", "64"])
+@pytest.mark.parametrize("lw", ["1", "2"])
+def test_packed_hist_group_widths_match_reference(fgw, lw, monkeypatch):
+    """Packed single-atomic histogram at forced group widths (idle lanes when
+    64 % lanes-per-row != 0, partial last group) vs the torch reference.
+    H2O3_HIST_LW is read once per process; both values give correct results."""
     _need_gpu()
-    monkeypatch.setenv("H2O3_HIST_FG", fg)
-    monkeypatch.setenv("H2O3_HIST_BINMAJOR", binmajor)
+    monkeypatch.setenv("H2O3_HIST_FGW", fgw)
+    monkeypatch.setenv("H2O3_HIST_LW", lw)
     from h2o3_amd.ops import tree_ops
     bd, _ = _binned(n=40000, F=37, nbins=255, cats=False)
     n = bd.nrows_local
@@ -379,16 +380,17 @@ def test_hist_need_mask_skips_groups(nbins, kernel, monkeypatch):
     assert skipped > 0
 
 
-def test_drf_chunked_need_mask_same_model(monkeypatch):
+@pytest.mark.parametrize("F", [48, 64])
+def test_drf_chunked_need_mask_same_model(F, monkeypatch):
     """Deep chunked DRF levels with the need mask grow the same trees as
-    with full histograms."""
+    with full histograms (F = 64: the packed single-atomic path)."""
     _need_gpu()
     import pandas as pd
     import h2o3_amd
     from h2o3_amd.estimators import H2ORandomForestEstimator
     h2o3_amd.init(device="cuda:0", verbose=False)
     rng = np.random.RandomState(0)
-    n, F = 20000, 48
+    n = 20000
     X = rng.randn(n, F).astype(np.float32)
     df = pd.DataFrame(X, columns=[f"x{i}" for i in range(F)])
     df["y"] = X[:, 0] + X[:, 7] * X[:, 30] + 0.1 * rng.randn(n)
@@ -401,3 +403,57 @@ def test_drf_chunked_need_mask_same_model(monkeypatch):
         m.train(y="y", training_frame=fr)
         preds.append(m.predict(fr).as_data_frame().values[:, 0])
     np.testing.assert_allclose(preds[0], preds[1], rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("kernel,fg", [("quad", "8"), ("quad", "36"), ("quad", "64"), ("old", "0")])
+@pytest.mark.parametrize("F", [64, 100])
+def test_packed_need_mask_matches_full(kernel, fg, F, monkeypatch):
+    """Packed single-atomic path (mode 0, 0/1 weights) with a need mask: the
+    host-side group count must match the kernel's; needed features equal the
+    unmasked histogram exactly, and the result matches fp64 torch."""
+    _need_gpu()
+    monkeypatch.setenv("H2O3_HIST_KERNEL", kernel)
+    if kernel == "quad":
+        monkeypatch.setenv("H2O3_HIST_FGW", fg)
+    from h2o3_amd.ops import tree_ops
+    bd, _ = _binned(n=30000, F=F, nbins=255, cats=False)
+    n = bd.nrows_local
+    g = torch.Generator(device="cuda").manual_seed(5)
+    ridx = torch.randperm(n, generator=g, device="cuda").to(torch.int32)
+    va = torch.randn(n, generator=g, device="cuda")
+    vb = (torch.rand(n, generator=g, device="cuda") < 0.8).to(torch.float32)
+    starts, counts = [0, 9000, 21000], [9000, 12000, 9000]
+    need = torch.zeros((3, bd.F), dtype=torch.bool, device="cuda")
+    need[0, [1, F - 1]] = True
+    need[1, [33]] = True
+    need[2, [0, 40, F - 2]] = True
+    vmax = tree_ops.channel_max(va, vb, 0)
+    full = tree_ops.hist_build(bd, ridx, va, vb, 0, starts, counts, 3, use_native=True, unit_w=True, vmax=vmax)
+    part = tree_ops.hist_build(bd, ridx, va, vb, 0, starts, counts, 3, use_native=True, unit_w=True, vmax=vmax,
+                               need_mask=need)
+    ref = tree_ops.hist_build(bd, ridx, va, vb, 0, starts, counts, 3, use_native=False)
+    torch.testing.assert_close(full[..., 0], ref[..., 0], rtol=0, atol=1e-9)
+    torch.testing.assert_close(full[..., 1], ref[..., 1], rtol=1e-5, atol=1e-4)
+    for s in range(3):
+        for f in torch.nonzero(need[s]).flatten().tolist():
+            torch.testing.assert_close(part[f, s], full[f, s], rtol=0, atol=0)
+    if kernel == "quad" and F > int(fg):   # more than one group: some (slot, group) blocks were skipped
+        assert float(part.abs().sum()) < float(full.abs().sum())
+
+
+@pytest.mark.parametrize("F", [1, 3, 5, 37, 100, 130])
+def test_quad_kernel_feature_groups(F):
+    """Quad kernel at the default group choice: uneven last group, partial
+    last dword, one-feature frames; packed and two-entry layouts."""
+    _need_gpu()
+    from h2o3_amd.ops import tree_ops
+    bd, _ = _binned(n=12000, F=F, nbins=255, cats=False)
+    n = bd.nrows_local
+    g = torch.Generator(device="cuda").manual_seed(F)
+    ridx = torch.randperm(n, generator=g, device="cuda").to(torch.int32)
+    va = torch.randn(n, generator=g, device="cuda")
+    starts, counts = [0, 2500], [2500, 9500]
+    for unit_w in (True, False):
+        h = tree_ops.hist_build(bd, ridx, va, None, 0, starts, counts, 2, use_native=True, unit_w=unit_w)
+        r = tree_ops.hist_build(bd, ridx, va, None, 0, starts, counts, 2, use_native=False)
+        torch.testing.assert_close(h, r, rtol=1e-5, atol=1e-4)
