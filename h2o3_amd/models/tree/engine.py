@@ -313,7 +313,7 @@ class TreeGrower:
                 ok = cache[n] = torch.ones((n, Fl), dtype=torch.uint8, device=self.dev)
         else:
             ok = cm.to(torch.uint8).contiguous()
-            ok = ok.to(self.dev, non_blocking=True) if ok.device.type == "cpu" else ok
+            ok = tree_ops._h2d(ok.numpy(), self.dev) if ok.device.type == "cpu" else ok
             if self.f0 + Fl > self.bd.F:
                 ok[:, max(0, self.bd.F - self.f0):] = 0
         if getattr(self, "_mono_f32", None) is None:

@@ -183,6 +183,9 @@ class GBMDriver:
         v = hv.numpy().tolist()
         for li, node in enumerate(leaves):
             tree.value[node] = float(v[li])
+        # a pack taken before the values landed holds zero leaf values: drop it
+        if self._forest_obj is not None:
+            self._forest_obj._packed = None
 
     def _row_weights(self):
         p = self.est._parms

@@ -172,7 +172,7 @@ __device__ __forceinline__ unsigned int code_at(unsigned int w, int hi, int sh) 
 __device__ __forceinline__ unsigned int code_at(uint2 w, int hi, int sh) { return ((hi ? w.y : w.x) >> sh) & 0xffu; }
 
 template <int MODE, bool HAS_VB, bool POSV, bool PACK, bool PIPE = true, int LW = 1>
-__global__ __launch_bounds__(512) void hist_quad_kernel(
+__global__ __launch_bounds__(1024) void hist_quad_kernel(
     const uint8_t* __restrict__ codes, int Fp, const int* __restrict__ ridx,
     const float* __restrict__ va, const float* __restrict__ vb,
     const int4* __restrict__ work, int n_work, int n_fg, int fgw, int F, int foff, int Bs, float s0, float s1,

@@ -22,12 +22,52 @@ _c_ll = ctypes.c_longlong
 
 
 
+class _PinnedRing:
+    """Reusable pinned staging buffers for the small per-level host->device
+    uploads (work items, per-chunk metadata, column masks).  A copy from a
+    pinned slot is truly asynchronous; the slot's event is waited on before
+    the slot is reused, so the host never overwrites bytes a pending copy
+    still reads (no reliance on pageable-memory staging semantics)."""
+
+    def __init__(self, n=16):
+        self.bufs = [None] * n
+        self.events = [None] * n
+        self.i = 0
+
+    def upload(self, a: np.ndarray, dev):
+        k = self.i
+        self.i = (self.i + 1) % len(self.bufs)
+        ev = self.events[k]
+        if ev is not None:
+            ev.synchronize()
+        nb = max(a.nbytes, 8)
+        buf = self.bufs[k]
+        if buf is None or buf.numel() < nb:
+            buf = self.bufs[k] = torch.empty(max(nb, 1 << 16), dtype=torch.uint8, pin_memory=True)
+        tdt = torch.from_numpy(a[:0]).dtype
+        stage = buf[:a.nbytes].view(tdt).view(a.shape)
+        stage.copy_(torch.from_numpy(a))
+        out = stage.to(dev, non_blocking=True)
+        if ev is None:
+            ev = self.events[k] = torch.cuda.Event()
+        ev.record()
+        return out
+
+
+_ring = None
+
+
 def _h2d(a, dev):
-    """Small host array -> device as a non-blocking copy (no stream sync;
-    A/B on the GBM bench: staging through the pinned caching allocator costs
-    more host time than it saves)."""
-    t = torch.from_numpy(np.ascontiguousarray(a))
-    return t.to(dev, non_blocking=True) if dev.type == "cuda" else t
+    """Small host array -> device without a stream sync, staged through a
+    reusable pinned ring (one pinned allocation per slot, not per call)."""
+    a = np.ascontiguousarray(a)
+    if dev.type != "cuda":
+        return torch.from_numpy(a)
+    global _ring
+    if _ring is None:
+        _ring = _PinnedRing()
+    return _ring.upload(a, dev)
+
 
 def _ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
@@ -191,8 +231,11 @@ def hist_build(bd, ridx, va, vb, mode, starts, counts, n_slots, use_native=None,
             return ret()
         quad = bd.code_bytes == 1 and bd.Fp % 4 == 0 and bd.Bs <= 256 and kern == "quad" and mode in (0, 1, 2)
         pack = quad and mode == 0 and unit_w and os.environ.get("H2O3_HIST_PACK", "1") == "1"
+        # H2O3_HIST_BIG=1 (A/B): one 1024-thread workgroup per CU with up to 160 KB of LDS histogram
+        big = os.environ.get("H2O3_HIST_BIG", "0") == "1"
+        qbudget = 156 * 1024 if big else _LDS_BUDGET
         if quad:
-            n_fg, fgw = quad_groups(bd.F, bd.Fp, bd.Bs, pack)
+            n_fg, fgw = quad_groups(bd.F, bd.Fp, bd.Bs, pack, qbudget)
         else:
             FG = feature_group(bd.F, bd.Bs, mode)
             n_fg = (bd.F + FG - 1) // FG
@@ -200,7 +243,7 @@ def hist_build(bd, ridx, va, vb, mode, starts, counts, n_slots, use_native=None,
         chunk = max(2048, -(-total // tgt_chunks))
         if pack and chunk >= (1 << 23):
             pack = False
-            n_fg, fgw = quad_groups(bd.F, bd.Fp, bd.Bs, False)
+            n_fg, fgw = quad_groups(bd.F, bd.Fp, bd.Bs, False, qbudget)
         items = make_work(starts, counts, range(n_slots), chunk)
         if len(items) == 0:
             return ret()
@@ -224,7 +267,7 @@ def hist_build(bd, ridx, va, vb, mode, starts, counts, n_slots, use_native=None,
                 s1, bq = _pack_scale(vmax[1] if vb is None else max(vmax[1], 0.0), chunk)
             need = _need(fgw)
             rc = lib.h2o_hist_quad3(_ptr(bd.codes), bd.Fp, _ptr(ridx), _ptr(va), _ptr(vb), _ptr(work), len(items),
-                                    bd.F, 0, bd.Bs, s0, s1, _ptr(hist), n_slots, mode, 512, _ptr(wyy),
+                                    bd.F, 0, bd.Bs, s0, s1, _ptr(hist), n_slots, mode, 1024 if big else 512, _ptr(wyy),
                                     1 if posv else 0, bq, fgw, _ptr(need), _stream())
             if rc != 0:
                 raise RuntimeError(f"h2o_hist_quad3 failed: error {rc} (F={bd.F}, Fp={bd.Fp}, fgw={fgw})")

@@ -15,13 +15,24 @@ import atexit
 import datetime
 import os
 import socket
+import sys
 import time
 
 import torch
 import torch.distributed as dist
 
 _state = {"initialized": False, "device": None, "rank": 0, "world": 1, "local_rank": 0,
-          "backend": None, "start": time.time(), "owns_pg": False, "name": None}
+          "backend": None, "start": time.time(), "owns_pg": False, "name": None, "failed": False}
+
+
+def _mark_failed_hook(prev):
+    """sys.excepthook wrapper: an uncaught exception marks this rank as failed,
+    so the exit-time teardown does not wait in a barrier for peers that may be
+    blocked in a collective this rank will never join."""
+    def hook(tp, val, tb):
+        _state["failed"] = True
+        prev(tp, val, tb)
+    return hook
 
 
 def _env_int(k, d):
@@ -55,7 +66,8 @@ def init(device: str | None = None, backend: str | None = None, timeout_s: float
         dist.init_process_group(be, rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=timeout_s), **kw)
         _state["owns_pg"] = True
-        atexit.register(shutdown)
+        sys.excepthook = _mark_failed_hook(sys.excepthook)
+        atexit.register(_atexit_shutdown)
     if dist.is_initialized():
         rank, world = dist.get_rank(), dist.get_world_size()
         _state["backend"] = dist.get_backend()
@@ -106,16 +118,34 @@ def info() -> dict:
             "uptime_s": round(time.time() - _state["start"], 1), "host": socket.gethostname()}
 
 
-def shutdown():
-    # Tear the owned process group down explicitly: letting interpreter exit
-    # destroy a live gloo group races its worker threads (std::terminate).
+def shutdown(clean: bool = True, barrier_timeout_s: float = 60.0):
+    """Tear the owned process group down explicitly (letting interpreter exit
+    destroy a live gloo group races its worker threads: std::terminate).
+
+    clean=True: all ranks are finishing together -> rendezvous first (gloo:
+    monitored_barrier with a short timeout, so a dead peer is reported instead
+    of waiting out the 30-minute collective timeout).  clean=False (this rank
+    failed): no barrier -- it could pair with a peer's pending collective --
+    just drop the group so the process exits and its peers' collectives fail
+    fast on the broken connection."""
     if _state["owns_pg"] and dist.is_initialized():
+        if clean:
+            try:
+                if dist.get_backend() == "gloo":
+                    dist.monitored_barrier(timeout=datetime.timedelta(seconds=barrier_timeout_s))
+                else:
+                    barrier()
+            except Exception:
+                pass
         try:
-            dist.barrier()
+            dist.destroy_process_group()
         except Exception:
             pass
-        dist.destroy_process_group()
     _state.update(initialized=False, owns_pg=False)
+
+
+def _atexit_shutdown():
+    shutdown(clean=not _state["failed"])
 
 
 def barrier():

@@ -77,3 +77,32 @@ def test_drf_and_kmeans_close(results):
     # DRF row sampling / kmeans++ seeding are rank-local streams: same quality, not bitwise
     assert abs(one["drf_rmse"] - two["drf_rmse"]) < 0.1 * one["drf_rmse"]
     assert abs(one["km_tot_withinss"] - two["km_tot_withinss"]) < 0.05 * one["km_tot_withinss"]
+
+
+def test_failed_rank_exits_fast():
+    """A rank that dies on an exception exits without an exit-time barrier,
+    and its peer's pending collective fails on the broken connection instead
+    of waiting out the 30-minute collective timeout."""
+    import time
+    port = _free_port()
+    procs = []
+    t0 = time.time()
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), CUDA_VISIBLE_DEVICES="", OMP_NUM_THREADS="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "dist_fail_worker.py")], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+    outs = []
+    for p in procs:
+        try:
+            o, _ = p.communicate(timeout=240)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            o, _ = p.communicate()
+            outs.append(None)
+            continue
+        outs.append(o.decode(errors="replace"))
+    assert all(o is not None for o in outs), "a rank hung after its peer failed"
+    assert procs[1].returncode != 0 and "simulated failure" in outs[1]
+    assert procs[0].returncode != 0 and "unexpected" not in outs[0]
+    assert time.time() - t0 < 200
