@@ -56,6 +56,12 @@ class MojoModel:
 
     @staticmethod
     def load(path):
+        """Load a MOJO: this platform's layout (model.json + arrays/), or the
+        reference's h2o-genmodel layout (model.ini + trees/ / domains/ ...,
+        zip or unpacked directory) via mojo.h2o_mojo."""
+        from . import h2o_mojo
+        if h2o_mojo.is_h2o_layout(path):
+            return h2o_mojo.H2OMojoModel(path)
         with open(path, "rb") as f:
             return MojoModel(f.read())
 

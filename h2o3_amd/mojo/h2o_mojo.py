@@ -1,0 +1,956 @@
+"""Reader + numpy scorer for MOJOs in the reference's (h2o-genmodel) layout.
+
+The reference's MOJO zip holds `model.ini` ([info] key = value pairs, the
+[columns] list, the [domains] map), `domains/dNNN.txt` level files and
+per-algorithm payloads -- compressed tree byte streams `trees/tCC_GGG.bin`
+(+ `_aux.bin` node statistics) for GBM / DRF, `beta` / `cat_offsets` / means
+in model.ini for GLM, `center_i` for K-Means, nested sub-MOJOs under
+`models/<algo>/<key>/` for Stacked Ensembles.  This module reads that layout
+(zip file or unpacked directory) and scores pandas frames with vectorised
+numpy, so MOJOs exported by the reference import into this platform
+(`H2OGenericEstimator.from_file` / `h2o.import_mojo`).
+
+Parity references (behaviour studied, not translated):
+  hex/genmodel/ModelMojoReader.java            (ini / domain parsing)
+  hex/genmodel/algos/tree/SharedTreeMojoReader.java, SharedTreeMojoModel.java:129
+                                               (tree byte format, scoreTree v1.0 / 1.1 / >= 1.2)
+  hex/genmodel/utils/GenmodelBitSet.java       (categorical split bitsets)
+  hex/genmodel/algos/gbm/GbmMojoModel.java     (unifyPreds: init_f, link, multinomial rescale)
+  hex/genmodel/algos/drf/DrfMojoModel.java     (tree averaging, binomial class-0 trees)
+  hex/genmodel/algos/glm/Glm*MojoModel.java    (cat offsets, mean imputation, ordinal / multinomial)
+  hex/genmodel/algos/kmeans/KMeansMojoModel.java, GenModel.KMeans_distance
+  hex/genmodel/algos/ensemble/StackedEnsembleMojoModel.java (base model remap, logit transform)
+
+Instead of walking one row at a time through the byte stream (the
+reference's scoreTree), every tree is decoded ONCE into flat node arrays and
+all rows descend level by level together.
+"""
+from __future__ import annotations
+
+import io
+import math
+import os
+import struct
+import zipfile
+
+import numpy as np
+
+# NaSplitDir (hex/genmodel/algos/tree/NaSplitDir.java)
+_NSD_NA_VS_REST, _NSD_NA_LEFT, _NSD_LEFT = 1, 2, 4
+
+
+_ALGO_BY_NAME = {
+    "Distributed Random Forest": "drf", "Gradient Boosting Method": "gbm", "Gradient Boosting Machine": "gbm",
+    "Generalized Low Rank Modeling": "glrm", "Generalized Low Rank Model": "glrm",
+    "Generalized Linear Modeling": "glm", "Generalized Linear Model": "glm", "Generalized Additive Model": "gam",
+    "Word2Vec": "word2vec", "TargetEncoder": "targetencoder", "Isolation Forest": "isolationforest",
+    "Extended Isolation Forest": "extendedisolationforest", "K-means": "kmeans", "Deep Learning": "deeplearning",
+    "deep learning": "deeplearning", "Support Vector Machine (*Spark*)": "svm", "StackedEnsemble": "stackedensemble",
+    "Stacked Ensemble": "stackedensemble", "k-LIME": "klime", "MOJO Pipeline": "pipeline",
+    "Principal Components Analysis": "pca", "Cox Proportional Hazards": "coxph", "RuleFit": "rulefit",
+}
+
+
+# ----------------------------------------------------------------- backends
+class _Backend:
+    """Zip archive or directory, optionally rooted at a nested prefix (the
+    Stacked Ensemble's submodel_dir_i)."""
+
+    def __init__(self, src, prefix=""):
+        self.prefix = prefix
+        if isinstance(src, (_ZipSrc, _DirSrc)):
+            self.src = src
+        elif isinstance(src, (bytes, bytearray)):
+            self.src = _ZipSrc(zipfile.ZipFile(io.BytesIO(bytes(src))))
+        elif os.path.isdir(src):
+            self.src = _DirSrc(src)
+        else:
+            self.src = _ZipSrc(zipfile.ZipFile(src))
+
+    def nested(self, sub):
+        return _Backend(self.src, self.prefix + sub)
+
+    def exists(self, name):
+        return self.src.exists(self.prefix + name)
+
+    def read(self, name) -> bytes:
+        return self.src.read(self.prefix + name)
+
+    def text(self, name) -> list:
+        return self.read(name).decode("utf-8").splitlines()
+
+
+class _ZipSrc:
+    def __init__(self, z):
+        self.z = z
+        self.names = set(z.namelist())
+
+    def exists(self, n):
+        return n in self.names
+
+    def read(self, n):
+        return self.z.read(n)
+
+
+class _DirSrc:
+    def __init__(self, d):
+        self.d = d
+
+    def exists(self, n):
+        return os.path.exists(os.path.join(self.d, n))
+
+    def read(self, n):
+        with open(os.path.join(self.d, n), "rb") as f:
+            return f.read()
+
+
+def _parse_val(s: str):
+    """[info] value -> python (ParseUtils.tryParse: null, booleans, numbers,
+    [a, b, ...] arrays, else the raw string)."""
+    s = s.strip()
+    if s == "null":
+        return None
+    if s in ("true", "false"):
+        return s == "true"
+    if s.startswith("[") and s.endswith("]"):
+        body = s[1:-1].strip()
+        if not body:
+            return []
+        out = []
+        for t in body.split(","):
+            v = _parse_val(t)
+            out.append(v)
+        return out
+    try:
+        if s.lstrip("-").isdigit():
+            return int(s)
+        return float(s)          # also NaN / Infinity
+    except ValueError:
+        return s
+
+
+def is_h2o_layout(src) -> bool:
+    """True when src (path / bytes) is a reference-layout MOJO: model.ini
+    without this platform's model.json."""
+    try:
+        b = _Backend(src)
+    except Exception:
+        return False
+    return b.exists("model.ini") and not b.exists("model.json")
+
+
+# --------------------------------------------------------------- tree decode
+class _Tree:
+    """One compressed tree decoded into flat node arrays.  Children are node
+    indices (>= 0) or leaves encoded as -(leaf_index + 1)."""
+
+    __slots__ = ("col", "kind", "split", "na_left", "bs_off", "bs_n", "bs_pos", "left", "right", "leaf", "raw",
+                 "root_leaf")
+
+    def __init__(self, buf: bytes, version: float):
+        self.raw = np.frombuffer(buf, dtype=np.uint8)
+        col, kind, split, na_left, bs_off, bs_n, bs_pos, left, right = ([] for _ in range(9))
+        leaf = []
+        self.root_leaf = None
+        b = buf
+
+        def f32(p):
+            return struct.unpack_from("<f", b, p)[0]
+
+        def u16(p):
+            return struct.unpack_from("<H", b, p)[0]
+
+        def u32(p):
+            return struct.unpack_from("<i", b, p)[0]
+
+        # explicit stack: (position, parent node index, is_right)
+        if u16(1) == 65535:
+            self.root_leaf = f32(3)
+        else:
+            stack = [(0, -1, False)]
+            while stack:
+                pos, parent, is_right = stack.pop()
+                node_type = b[pos]
+                c = u16(pos + 1)
+                nsd = b[pos + 3]
+                p = pos + 4
+                na_vs_rest = nsd == _NSD_NA_VS_REST
+                equal = node_type & 12
+                k, sv, bo, bn, bp = 0, 0.0, 0, 0, 0
+                if na_vs_rest:
+                    k = 2
+                elif equal == 0:
+                    sv = f32(p)
+                    p += 4
+                elif equal == 8:                     # 32-bit inline bitset, offset 0
+                    k, bo, bn, bp = 1, 0, 32, p
+                    p += 4
+                else:                                # general bitset
+                    k = 1
+                    bo = u16(p)
+                    if version >= 1.2:
+                        bn = u32(p + 2)
+                        bp = p + 6
+                        p = bp + ((bn - 1) >> 3) + 1
+                    else:
+                        nbytes = u16(p + 2)
+                        bn = nbytes << 3
+                        bp = p + 4
+                        p = bp + nbytes
+                idx = len(col)
+                col.append(c)
+                kind.append(k)
+                split.append(sv)
+                na_left.append(nsd in (_NSD_NA_LEFT, _NSD_LEFT))
+                bs_off.append(bo)
+                bs_n.append(bn)
+                bs_pos.append(bp)
+                left.append(0)
+                right.append(0)
+                if parent >= 0:
+                    (right if is_right else left)[parent] = idx
+                lmask = node_type & 51
+                rmask = (node_type & 0xC0) >> 2
+                # left subtree: size field of lmask+1 bytes unless it is a leaf
+                if lmask & 16:
+                    left[idx] = -(len(leaf) + 1)
+                    leaf.append(f32(p))
+                    rpos = p + 4
+                else:
+                    nsz = lmask + 1
+                    size = int.from_bytes(b[p:p + nsz], "little")
+                    lpos = p + nsz
+                    rpos = lpos + size
+                    stack.append((lpos, idx, False))
+                if rmask & 16:
+                    right[idx] = -(len(leaf) + 1)
+                    leaf.append(f32(rpos))
+                else:
+                    stack.append((rpos, idx, True))
+        self.col = np.asarray(col, dtype=np.int64)
+        self.kind = np.asarray(kind, dtype=np.int8)
+        self.split = np.asarray(split, dtype=np.float32).astype(np.float64)
+        self.na_left = np.asarray(na_left, dtype=bool)
+        self.bs_off = np.asarray(bs_off, dtype=np.int64)
+        self.bs_n = np.asarray(bs_n, dtype=np.int64)
+        self.bs_pos = np.asarray(bs_pos, dtype=np.int64)
+        self.left = np.asarray(left, dtype=np.int64)
+        self.right = np.asarray(right, dtype=np.int64)
+        self.leaf = np.asarray(leaf, dtype=np.float32).astype(np.float64)
+
+    def score(self, X: np.ndarray, dom_len: np.ndarray | None, version: float, paths: list | None = None) -> np.ndarray:
+        """Leaf value per row of X [n, ncols] (category indices for enums).
+        paths: optional list of n strings, extended in place with the row's
+        'L'/'R' decisions (leaf assignment, SharedTreeMojoModel.getDecisionPath)."""
+        n = X.shape[0]
+        if self.root_leaf is not None:
+            return np.full(n, self.root_leaf)
+        out = np.empty(n)
+        rows = np.arange(n)
+        node = np.zeros(n, dtype=np.int64)
+        while rows.size:
+            c = self.col[node]
+            d = X[rows, c]
+            kind = self.kind[node]
+            nan = np.isnan(d)
+            di = np.where(nan, 0, d).astype(np.int64)
+            right = np.zeros(rows.size, dtype=bool)
+            num = kind == 0
+            right[num] = d[num] >= self.split[node[num]]
+            bsm = kind == 1
+            if bsm.any():
+                nb = node[bsm]
+                rel = di[bsm] - self.bs_off[nb]
+                inr = (rel >= 0) & (rel < self.bs_n[nb])
+                relc = np.clip(rel, 0, None)
+                byte = self.raw[np.minimum(self.bs_pos[nb] + (relc >> 3), self.raw.size - 1)]
+                contains = ((byte >> (relc & 7)) & 1).astype(bool) & inr
+                right[bsm] = contains
+                if version >= 1.1:
+                    tmp = nan[bsm] | ~inr
+                    nan[bsm] = tmp
+            if version >= 1.2 and dom_len is not None:
+                dl = dom_len[c]
+                nan |= (dl > 0) & (di >= dl) & ~np.isnan(d)
+            go_right = np.where(nan, ~self.na_left[node], right)
+            if paths is not None:
+                for r, gr in zip(rows.tolist(), go_right.tolist()):
+                    paths[r] += "R" if gr else "L"
+            nxt = np.where(go_right, self.right[node], self.left[node])
+            done = nxt < 0
+            if done.any():
+                out[rows[done]] = self.leaf[-nxt[done] - 1]
+            keep = ~done
+            rows, node = rows[keep], nxt[keep]
+        return out
+
+
+# ------------------------------------------------------------------- models
+class H2OMojoModel:
+    """A reference-layout MOJO.  predict(df) returns the reference's output
+    columns (predict, p0, p1, ... / cluster / predict); predict_raw(df)
+    returns the class-probability (or value) matrix used by Generic metrics."""
+
+    def __init__(self, src, backend: _Backend | None = None):
+        self.be = backend if backend is not None else _Backend(src)
+        self.info, self.columns, dom_files = self._parse_ini()
+        # ModelMojoFactory dispatches on the long "algorithm" name; "algo" is
+        # missing from some early MOJOs
+        self.algo = _ALGO_BY_NAME.get(str(self.info.get("algorithm")), str(self.info.get("algo")))
+        self.version = float(self.info.get("mojo_version", 1.0))
+        self.nclasses = int(self.info.get("n_classes", 1) or 1)
+        self.nfeatures = int(self.info.get("n_features", len(self.columns)))
+        self.supervised = bool(self.info.get("supervised", False))
+        self.category = str(self.info.get("category", ""))
+        self.default_threshold = float(self.info.get("default_threshold", 0.5) or 0.5)
+        self.domains = [None] * len(self.columns)
+        esc = bool(self.info.get("escape_domain_values", False))
+        for ci, (cnt, fname) in dom_files.items():
+            if ci >= len(self.columns):
+                continue
+            lines = self.be.text("domains/" + fname)
+            if esc:
+                lines = [ln.replace("\\n", "\n") for ln in lines]
+            if len(lines) < cnt:
+                raise ValueError(f"domain file {fname}: {len(lines)} levels, expected {cnt}")
+            self.domains[ci] = lines[:cnt]
+        self.response = self.columns[-1] if self.supervised else None
+        self.features = self.columns[:self.nfeatures]
+        self.response_domain = self.domains[-1] if self.supervised else None
+        self.dom_len = np.array([len(d) if d is not None else 0 for d in self.domains], dtype=np.int64)
+        self.meta = {"algo": self.algo, "x": list(self.features), "response": self.response,
+                     "nclasses": self.nclasses, "response_domain": self.response_domain, "format": "h2o"}
+        loader = getattr(self, f"_load_{self.algo}", None)
+        if loader is None:
+            raise NotImplementedError(f"reference MOJO algo '{self.algo}' is not supported by this reader")
+        loader()
+
+    # ------------------------------------------------------------ ini parse
+    def _parse_ini(self):
+        info, cols, doms = {}, [], {}
+        sec = None
+        for line in self.be.text("model.ini"):
+            line = line.strip()
+            if not line or line.startswith("#"):
+                continue
+            if line in ("[info]", "[columns]", "[domains]"):
+                sec = line
+                continue
+            if sec == "[info]":
+                k, _, v = line.partition("=")
+                k = k.strip()
+                info[k] = v.strip() if k == "uuid" else _parse_val(v)
+            elif sec == "[columns]":
+                cols.append(line)
+            elif sec == "[domains]":
+                ci, _, rest = line.partition(":")
+                cnt, _, fname = rest.strip().partition(" ")
+                doms[int(ci)] = (int(cnt), fname.strip())
+        return info, cols, doms
+
+    def kv(self, k, default=None):
+        v = self.info.get(k, default)
+        return default if v is None else v
+
+    # -------------------------------------------------------------- loaders
+    def _load_trees(self):
+        tpc = self.info.get("n_trees_per_class")
+        if tpc is None:
+            bdt = self.info.get("binomial_double_trees")
+            tpc = 1 if (self.nclasses == 2 and not bdt) else self.nclasses
+        self.ntree_groups = int(self.kv("n_trees", 0))
+        self.ntrees_per_group = int(tpc)
+        self.trees = [[None] * self.ntree_groups for _ in range(self.ntrees_per_group)]
+        for j in range(self.ntree_groups):
+            for i in range(self.ntrees_per_group):
+                name = "trees/t%02d_%03d.bin" % (i, j)
+                if self.be.exists(name):
+                    self.trees[i][j] = _Tree(self.be.read(name), self.version)
+        self.calib_beta = None
+        if self.info.get("calib_method") is not None:
+            if self.info["calib_method"] != "platt":
+                raise ValueError(f"unknown calibration method {self.info['calib_method']}")
+            self.calib_beta = list(self.kv("calib_glm_beta", []))
+        enc = str(self.kv("_genmodel_encoding", "AUTO"))
+        if enc not in ("AUTO", "Enum", "SortByResponse"):
+            raise NotImplementedError(f"tree MOJO with categorical encoding {enc} is not supported")
+
+    def _load_gbm(self):
+        self._load_trees()
+        self.family = str(self.kv("distribution"))
+        self.init_f = float(self.kv("init_f", 0.0))
+        link = self.info.get("link_function")
+        if link is None:
+            link = {"bernoulli": "logit", "fractionalbinomial": "logit", "quasibinomial": "logit",
+                    "modified_huber": "logit", "ordinal": "logit", "multinomial": "log", "poisson": "log",
+                    "gamma": "log", "tweedie": "log"}.get(self.family, "identity")
+        self.link = str(link)
+
+    def _load_drf(self):
+        self._load_trees()
+        self.binomial_double_trees = bool(self.kv("binomial_double_trees", False))
+
+    def _load_glm(self):
+        self.use_all_levels = bool(self.kv("use_all_factor_levels", False))
+        self.cats = int(self.kv("cats", -1))
+        self.cat_modes = list(self.kv("cat_modes", []))
+        self.cat_offsets = list(self.kv("cat_offsets", [0]))
+        self.nums = int(self.kv("nums", -1))
+        self.num_means = list(self.kv("num_means", []))
+        self.mean_imputation = bool(self.kv("mean_imputation", False))
+        self.beta = np.asarray(self.kv("beta"), dtype=np.float64)
+        self.family = str(self.kv("family"))
+        self.glm_link = str(self.kv("link", "identity"))
+        self.tweedie_link_power = float(self.kv("tweedie_link_power", 0.0))
+
+    def _load_kmeans(self):
+        self.standardize = bool(self.kv("standardize", False))
+        if self.standardize:
+            self.km_means = np.asarray(self.kv("standardize_means"), dtype=np.float64)
+            mults = self.info.get("standardize_mults")
+            self.km_mults = None if mults is None else np.asarray(mults, dtype=np.float64)
+            self.km_modes = np.asarray(self.kv("standardize_modes"), dtype=np.int64)
+        k = int(self.kv("center_num"))
+        self.centers = np.asarray([self.kv(f"center_{i}") for i in range(k)], dtype=np.float64)
+
+    def _load_stackedensemble(self):
+        subs = {}
+        for i in range(int(self.kv("submodel_count", 0))):
+            key = str(self.kv(f"submodel_key_{i}"))
+            subs[key] = H2OMojoModel(None, backend=self.be.nested(str(self.kv(f"submodel_dir_{i}"))))
+        tr = str(self.kv("metalearner_transform", "NONE"))
+        if tr not in ("NONE", "Logit"):
+            raise NotImplementedError(f"metalearner transform {tr}")
+        self.logit_transform = tr == "Logit"
+        self.metalearner = subs[str(self.kv("metalearner"))]
+        self.base = []
+        for i in range(int(self.kv("base_models_num", 0))):
+            key = self.info.get(f"base_model{i}")
+            if key is None:
+                self.base.append(None)
+                continue
+            m = subs[str(key)]
+            mapping = []
+            for f in m.features:
+                if f not in self.columns:
+                    raise ValueError(f"model {key} needs input column {f} missing from the ensemble")
+                mapping.append(self.columns.index(f))
+            self.base.append((m, np.asarray(mapping, dtype=np.int64)))
+
+    def _load_isolationforest(self):
+        self._load_trees()
+        self.min_path_length = int(self.kv("min_path_length", 0))
+        self.max_path_length = int(self.kv("max_path_length", 0))
+        self.output_anomaly_flag = bool(self.kv("output_anomaly_flag", False))
+
+    def _load_extendedisolationforest(self):
+        self.eif_ntrees = int(self.kv("ntrees", 0))
+        self.eif_sample_size = int(self.kv("sample_size", 0))
+        self.eif_trees = [self._eif_decode(self.be.read("trees/t%02d.bin" % t)) for t in range(self.eif_ntrees)]
+
+    @staticmethod
+    def _eif_decode(buf):
+        """ExtendedIsolationForestMojoModel tree blob (little endian): int32 branching-array size
+        k, then records (int32 node number, 'N' + k normal f64 + k point f64 |
+        'L' + int32 rows), node numbers heap-ordered (children 2i+1, 2i+2)."""
+        k = struct.unpack_from("<i", buf, 0)[0]
+        p = 4
+        nodes = {}
+        while p + 5 <= len(buf):
+            num = struct.unpack_from("<i", buf, p)[0]
+            typ = buf[p + 4]
+            p += 5
+            if typ == ord("N"):
+                v = np.frombuffer(buf, dtype="<f8", count=2 * k, offset=p).astype(np.float64)
+                nodes[num] = ("N", v[:k], v[k:])
+                p += 16 * k
+            elif typ == ord("L"):
+                nodes[num] = ("L", struct.unpack_from("<i", buf, p)[0])
+                p += 4
+            else:
+                break      # zero padding after the last record (the blob is a fixed-size buffer)
+        return nodes
+
+    def _load_word2vec(self):
+        vocab = int(self.kv("vocab_size", -1))
+        vec = int(self.kv("vec_size", -1))
+        raw = self.be.read("vectors")
+        if len(raw) != vocab * vec * 4:
+            raise ValueError(f"corrupted word2vec vectors: {len(raw)} bytes")
+        V = np.frombuffer(raw, dtype=">f4").astype(np.float32).reshape(vocab, vec)
+        words = [w.strip().replace("\\n", "\n") for w in self.be.text("vocabulary")]
+        if len(words) != vocab:
+            raise ValueError("corrupted word2vec vocabulary")
+        self.vec_size = vec
+        self.embeddings = {w: V[i] for i, w in enumerate(words)}
+
+    def transform(self, word):
+        """Word2Vec embedding of one word (None if out of vocabulary)."""
+        v = self.embeddings.get(word)
+        return None if v is None else v.copy()
+
+    def _load_deeplearning(self):
+        self.dl_nums = int(self.kv("nums"))
+        self.dl_cats = int(self.kv("cats"))
+        self.dl_cat_offsets = list(self.kv("cat_offsets", [0]))
+        self.dl_norm_mul = self.info.get("norm_mul") or []
+        self.dl_norm_sub = self.info.get("norm_sub") or []
+        self.dl_resp_mul = self.info.get("norm_resp_mul")
+        self.dl_resp_sub = self.info.get("norm_resp_sub")
+        self.dl_use_all = bool(self.kv("use_all_factor_levels", False))
+        self.dl_activation = str(self.kv("activation"))
+        self.dl_family = str(self.kv("distribution"))
+        self.dl_units = list(self.kv("neural_network_sizes", []))
+        self.dl_dropout = list(self.kv("hidden_dropout_ratios", []))
+        self.dl_layers = []
+        for li in range(len(self.dl_units) - 1):
+            b = np.asarray(self.kv(f"bias_layer{li}", []), dtype=np.float64)
+            w = np.asarray(self.kv(f"weight_layer{li}", []), dtype=np.float32).astype(np.float64)
+            self.dl_layers.append((w, b))
+        enc = str(self.kv("_genmodel_encoding", "AUTO")) if self.version >= 1.10 else "AUTO"
+        if enc not in ("AUTO", "OneHotInternal"):
+            raise NotImplementedError(f"deep learning MOJO with categorical encoding {enc} is not supported")
+        nl = len(self.dl_units) - 1
+        out_act = self.dl_activation if self.category == "AutoEncoder" else (
+            "Softmax" if self.nclasses > 1 else "Linear")
+        self.dl_acts = [self.dl_activation] * (nl - 1) + [out_act]
+
+    # --------------------------------------------------------------- inputs
+    def row_matrix(self, df) -> np.ndarray:
+        """DataFrame (or dict of columns) -> [n, ncolumns] doubles in the MOJO's
+        column order: enum levels -> domain index (unseen / missing -> NaN,
+        like EasyPredictModelWrapper with convertUnknownCategoricalLevelsToNa),
+        numbers parsed from numerics or strings."""
+        import pandas as pd
+        if isinstance(df, dict):
+            multi = any(isinstance(v, (list, tuple, np.ndarray, pd.Series)) for v in df.values())
+            df = pd.DataFrame(df) if multi else pd.DataFrame([df])
+        n = len(df)
+        X = np.full((n, len(self.columns)), np.nan)
+        for j, c in enumerate(self.columns):
+            if c not in df:
+                continue
+            vals = df[c].values
+            dom = self.domains[j]
+            if dom is not None:
+                idx = {d: i for i, d in enumerate(dom)}
+                for r, v in enumerate(vals):
+                    if v is None or (isinstance(v, float) and math.isnan(v)):
+                        continue
+                    if isinstance(v, str):
+                        k = idx.get(v)
+                    else:
+                        fv = float(v)
+                        k = idx.get(str(int(fv)) if fv.is_integer() else str(v), idx.get(str(v)))
+                    if k is not None:
+                        X[r, j] = k
+            else:
+                try:
+                    X[:, j] = np.asarray(pd.to_numeric(pd.Series(vals), errors="coerce"), dtype=np.float64)
+                except Exception:
+                    pass
+        return X
+
+    # -------------------------------------------------------------- scoring
+    def score0(self, X: np.ndarray) -> np.ndarray:
+        """Rows [n, ncolumns] -> preds [n, 1 + K] exactly like MojoModel.score0
+        (preds[:, 0] = label index / value / cluster)."""
+        return getattr(self, f"_score_{self.algo}")(np.array(X, dtype=np.float64, copy=True))
+
+    def _tree_sums(self, X):
+        K = self.nclasses
+        preds = np.zeros((X.shape[0], 1 + K if K > 1 else 1))
+        off = 0 if K == 1 else 1
+        dl = self.dom_len if self.version >= 1.2 else None
+        for ci in range(self.ntrees_per_group):
+            acc = preds[:, off + ci]
+            for t in self.trees[ci]:
+                if t is not None:
+                    acc += t.score(X, dl, self.version)
+        return preds
+
+    def _label(self, preds):
+        if preds.shape[1] == 3:
+            preds[:, 0] = (preds[:, 2] >= self.default_threshold).astype(np.float64)
+        else:
+            preds[:, 0] = np.argmax(preds[:, 1:], axis=1)
+        return preds
+
+    def _calibrate(self, preds):
+        if self.calib_beta is None or preds.shape[1] != 3:
+            return preds
+        b = self.calib_beta
+        # PlattScalingMojoHelper: p1 = logitInv(p0 * beta[0] + beta[1])
+        p1 = 1.0 / (np.exp(-(preds[:, 1] * b[0] + b[1])) + 1.0)
+        self.calibrated = np.stack([1 - p1, p1], 1)
+        return preds
+
+    @staticmethod
+    def _link_inv(link, f):
+        if link == "log":
+            return np.minimum(1e19, np.exp(f))
+        if link in ("logit", "ologit"):
+            return 1.0 / (1.0 + np.exp(-f))
+        if link == "ologlog":
+            return 1.0 - np.exp(-np.exp(f))
+        if link == "inverse":
+            xx = np.where(f < 0, np.minimum(-1e-5, f), np.maximum(-1e-5, f))
+            return 1.0 / xx
+        return f
+
+    def _score_gbm(self, X):
+        preds = self._tree_sums(X)
+        fam = self.family
+        if fam in ("bernoulli", "quasibinomial", "modified_huber"):
+            f = preds[:, 1] + self.init_f
+            preds[:, 2] = self._link_inv(self.link, f)
+            preds[:, 1] = 1.0 - preds[:, 2]
+        elif fam == "multinomial":
+            if self.nclasses == 2:
+                preds[:, 1] += self.init_f
+                preds[:, 2] = -preds[:, 1]
+            z = preds[:, 1:]
+            z = np.exp(z - z.max(1, keepdims=True))
+            preds[:, 1:] = z / z.sum(1, keepdims=True)
+        else:
+            preds[:, 0] = self._link_inv(self.link, preds[:, 0] + self.init_f)
+            return preds
+        return self._calibrate(self._label(preds))
+
+    def _score_drf(self, X):
+        preds = self._tree_sums(X)
+        if self.nclasses == 1:
+            preds[:, 0] /= self.ntree_groups
+            return preds
+        if self.nclasses == 2 and not self.binomial_double_trees:
+            preds[:, 1] /= self.ntree_groups
+            preds[:, 2] = 1.0 - preds[:, 1]
+        else:
+            s = preds[:, 1:].sum(1, keepdims=True)
+            preds[:, 1:] = np.where(s > 0, preds[:, 1:] / np.where(s > 0, s, 1.0), preds[:, 1:])
+        return self._calibrate(self._label(preds))
+
+    def _glm_impute(self, X):
+        if not self.mean_imputation:
+            return
+        nc = max(self.cats, 0)
+        for i in range(nc):
+            m = np.isnan(X[:, i])
+            X[m, i] = self.cat_modes[i]
+        for i in range(max(self.nums, 0)):
+            m = np.isnan(X[:, nc + i])
+            X[m, nc + i] = self.num_means[i]
+
+    def _glm_eta(self, X, beta, P):
+        """Linear predictor for one class block of beta (length P)."""
+        n = X.shape[0]
+        eta = np.zeros(n)
+        offs = self.cat_offsets
+        for i in range(len(offs) - 1):
+            v = X[:, i]
+            ok = ~np.isnan(v)
+            iv = np.where(ok, v, 0).astype(np.int64)
+            if not self.use_all_levels:
+                ok &= iv != 0
+                iv = iv - 1
+            iv = iv + offs[i]
+            ok &= iv < offs[i + 1]
+            eta += np.where(ok, beta[np.clip(iv, 0, P - 1)], 0.0)
+        nc = max(self.cats, 0)
+        noff = offs[nc] if nc < len(offs) else 0
+        nn = self.nums if self.nums >= 0 else P - 1 - noff
+        # sequential accumulation in the reference's order (cats, nums,
+        # intercept): bit-identical etas keep threshold ties (mu == the stored
+        # default_threshold) on the same side as the reference scorer
+        for i in range(nn):
+            eta += beta[noff + i] * X[:, nc + i]
+        return eta + beta[P - 1]
+
+    def _score_glm(self, X):
+        self._glm_impute(X)
+        n = X.shape[0]
+        fam = self.family
+        if fam in ("multinomial", "ordinal"):
+            K = self.nclasses
+            P = self.beta.size // K
+            etas = np.stack([self._glm_eta(X, self.beta[c * P:(c + 1) * P], P) for c in range(K)], 1)
+            preds = np.zeros((n, 1 + K))
+            if fam == "multinomial":
+                # the reference clamps the row max at >= 0 before exponentiating
+                mx = np.maximum(etas.max(1, keepdims=True), 0.0)
+                e = np.exp(etas - mx)
+                preds[:, 1:] = e / e.sum(1, keepdims=True)
+            else:
+                cdf_prev = np.zeros(n)
+                for c in range(K - 1):
+                    cdf = 1.0 / (1.0 + np.exp(-etas[:, c]))
+                    preds[:, c + 1] = cdf - cdf_prev
+                    cdf_prev = cdf
+                preds[:, K] = 1.0 - cdf_prev
+            preds[:, 0] = np.argmax(preds[:, 1:], axis=1)
+            return preds
+        eta = self._glm_eta(X, self.beta, self.beta.size)
+        link = self.glm_link
+        if link == "tweedie":
+            p = self.tweedie_link_power
+            mu = np.maximum(2e-16, np.exp(eta)) if p == 0 else np.power(eta, 1.0 / p)
+        elif link == "inverse":
+            xx = np.where(eta < 0, np.minimum(-1e-5, eta), np.maximum(1e-5, eta))
+            mu = 1.0 / xx
+        else:
+            mu = self._link_inv(link, eta)
+        if fam in ("binomial", "fractionalbinomial", "quasibinomial"):
+            preds = np.zeros((n, 3))
+            preds[:, 0] = (mu >= self.default_threshold).astype(np.float64)
+            preds[:, 1] = 1.0 - mu
+            preds[:, 2] = mu
+            return preds
+        return mu.reshape(n, 1)
+
+    def _score_kmeans(self, X):
+        X = X[:, :self.centers.shape[1]]
+        if self.standardize:
+            for i in range(X.shape[1]):
+                m = np.isnan(X[:, i])
+                if self.km_modes[i] == -1:
+                    X[m, i] = self.km_means[i]
+                    if self.km_mults is not None:
+                        X[:, i] = (X[:, i] - self.km_means[i]) * self.km_mults[i]
+                else:
+                    X[m, i] = self.km_modes[i]
+        cat = np.array([d is not None for d in self.domains[:X.shape[1]]])
+        nan = np.isnan(X)
+        pts = (~nan).sum(1).astype(np.float64)
+        dist = np.zeros((X.shape[0], self.centers.shape[0]))
+        for k, c in enumerate(self.centers):
+            dd = np.where(cat, (X != c).astype(np.float64), (X - c) ** 2)
+            dd = np.where(nan, 0.0, dd)
+            s = dd.sum(1)
+            scale = np.where((pts > 0) & (pts < X.shape[1]), X.shape[1] / np.maximum(pts, 1), 1.0)
+            dist[:, k] = s * scale
+        self.last_distances = dist
+        return np.argmin(dist, axis=1).reshape(-1, 1).astype(np.float64)
+
+    def _score_stackedensemble(self, X):
+        n = X.shape[0]
+        K = self.nclasses
+        nb = len(self.base)
+        # one slot per base model (per class for multinomial); unused models
+        # (pruned by the metalearner) keep their slots at 0, as in the reference
+        B = np.zeros((n, nb * K if K > 2 else nb))
+        for i, b in enumerate(self.base):
+            if b is None:
+                continue
+            m, mapping = b
+            p = m.score0(X[:, mapping])
+            if K > 2:
+                B[:, i * K:(i + 1) * K] = p[:, 1:1 + K]
+            elif K == 2:
+                B[:, i] = p[:, 2]
+            else:
+                B[:, i] = p[:, 0]
+        if self.logit_transform and K >= 2:
+            q = np.clip(B, 1e-9, 1 - 1e-9)
+            x = q / (1 - q)
+            B = np.where(x == 0, -19.0, np.maximum(-19.0, np.log(np.where(x > 0, x, 1.0))))
+        # the metalearner's columns are the base predictions (+ its response)
+        Xm = np.full((n, len(self.metalearner.columns)), np.nan)
+        Xm[:, :B.shape[1]] = B
+        return self.metalearner.score0(Xm)
+
+    def _score_isolationforest(self, X):
+        preds = self._tree_sums(X)
+        tot = preds[:, 0]
+        n = X.shape[0]
+        mean_len = tot / self.ntree_groups if self.ntree_groups >= 1 else np.zeros(n)
+        lo, hi = self.min_path_length, self.max_path_length
+        score = (hi - tot) / (hi - lo) if hi > lo else np.ones(n)
+        if self.output_anomaly_flag:
+            return np.stack([(score > self.default_threshold).astype(np.float64), score, mean_len], 1)
+        return np.stack([score, mean_len], 1)
+
+    @staticmethod
+    def _avg_path_unsuccessful(nrows):
+        n = np.asarray(nrows, dtype=np.float64)
+        h = np.log(np.maximum(n - 1, 1)) + 0.5772156649
+        return np.where(n < 2, 0.0, np.where(n == 2, 1.0, 2 * h - 2.0 * (n - 1.0) / np.maximum(n, 1)))
+
+    def _score_extendedisolationforest(self, X):
+        n = X.shape[0]
+        tot = np.zeros(n)
+        for nodes in self.eif_trees:
+            num = np.zeros(n, dtype=np.int64)
+            height = np.zeros(n)
+            out = np.full(n, -1.0)
+            active = np.arange(n)
+            while active.size:
+                nxt_active = []
+                for nd in np.unique(num[active]).tolist():
+                    sel = active[num[active] == nd]
+                    rec = nodes.get(nd)
+                    if rec is None:
+                        continue
+                    if rec[0] == "L":
+                        out[sel] = height[sel] + float(self._avg_path_unsuccessful(rec[1]))
+                        continue
+                    _, nv, pv = rec
+                    mul = ((X[np.ix_(sel, np.arange(nv.size))] - pv) * nv).sum(1)
+                    height[sel] += 1
+                    num[sel] = np.where(mul <= 0, 2 * nd + 1, 2 * nd + 2)
+                    nxt_active.append(sel)
+                active = np.concatenate(nxt_active) if nxt_active else np.zeros(0, dtype=np.int64)
+            tot += out
+        path = tot / max(self.eif_ntrees, 1)
+        score = np.power(2.0, -path / float(self._avg_path_unsuccessful(self.eif_sample_size)))
+        return np.stack([score, path], 1)
+
+    def _dl_input(self, X):
+        """GenModel.setInput: one-hot categoricals (NA / unseen -> the extra
+        last level of the variable), standardised numerics, missing -> 0."""
+        n = X.shape[0]
+        offs = self.dl_cat_offsets
+        nc, nn = self.dl_cats, self.dl_nums
+        width = offs[nc] + nn
+        A = np.zeros((n, width))
+        for i in range(nc):
+            v = X[:, i]
+            nan = np.isnan(v)
+            c = np.where(nan, 0, v).astype(np.int64)
+            if self.dl_use_all:
+                t = c + offs[i]
+            else:
+                t = np.where(c != 0, c - 1 + offs[i], -1)
+            t = np.where(nan, offs[i + 1] - 1, t)
+            t = np.where(t >= offs[i + 1], offs[i + 1] - 1, t)
+            ok = t >= 0
+            A[np.nonzero(ok)[0], t[ok]] = 1.0
+        for j in range(nn):
+            d = X[:, nc + j]
+            if len(self.dl_norm_mul):
+                d = (d - self.dl_norm_sub[j]) * self.dl_norm_mul[j]
+            A[:, offs[nc] + j] = np.where(np.isnan(d), 0.0, d)
+        return A
+
+    @staticmethod
+    def _dl_affine(x, w, b, out_size):
+        """NeuralNetwork.formNNInputs in the reference's summation order (8
+        partial sums over column blocks, then the tail, then the bias)."""
+        n, cols = x.shape
+        W = w.reshape(out_size, cols)
+        res = np.zeros((n, out_size))
+        multiple = (cols // 8) * 8 - 1
+        extra = cols - cols % 8
+        ps = [np.zeros((n, out_size)) for _ in range(8)]
+        col = 0
+        while col < multiple:
+            for k in range(8):
+                ps[k] += x[:, col + k:col + k + 1] * W[:, col + k][None, :]
+            col += 8
+        res += ps[0] + ps[1] + ps[2] + ps[3]
+        res += ps[4] + ps[5] + ps[6] + ps[7]
+        for c in range(extra, cols):
+            res += x[:, c:c + 1] * W[:, c][None, :]
+        return res + b[None, :out_size]
+
+    def _score_deeplearning(self, X):
+        h = self._dl_input(X)
+        for li, (w, b) in enumerate(self.dl_layers):
+            act = self.dl_acts[li]
+            out = self.dl_units[li + 1]
+            drop = self.dl_dropout[li] if li < len(self.dl_dropout) else 0.0
+            if act.startswith("Maxout"):
+                k = b.size // out
+                W = w.reshape(out, h.shape[1], k)
+                z = np.einsum("ni,oik->nok", h, W) + b.reshape(out, k)[None]
+                h = z.max(2)
+            else:
+                z = self._dl_affine(h, w, b, out)
+                if act == "Softmax":
+                    e = np.exp(z - z.max(1, keepdims=True))
+                    h = e / e.sum(1, keepdims=True)
+                elif act == "Linear":
+                    h = z
+                elif act.startswith("ExpRectifier"):
+                    h = np.where(z >= 0, z, np.exp(z) - 1)
+                elif act.startswith("Rectifier"):
+                    h = 0.5 * (z + np.abs(z))
+                elif act.startswith("Tanh"):
+                    h = 1.0 - 2.0 / (1.0 + np.exp(2.0 * z))
+                else:
+                    raise NotImplementedError(f"activation {act}")
+            if act.endswith("WithDropout") and drop > 0:
+                h = h * (1.0 - drop)
+        n = X.shape[0]
+        if self.category == "AutoEncoder":
+            out = h.copy()
+            if len(self.dl_norm_mul):
+                k0 = out.shape[1] - self.dl_nums
+                out[:, k0:] = out[:, k0:] / np.asarray(self.dl_norm_mul) + np.asarray(self.dl_norm_sub)
+            return out
+        if self.nclasses > 1:
+            preds = np.zeros((n, 1 + self.nclasses))
+            preds[:, 1:] = h
+            return self._label(preds)
+        v = h[:, 0]
+        if self.dl_resp_mul is not None:
+            v = v / self.dl_resp_mul[0] + self.dl_resp_sub[0]
+        fam = self.dl_family
+        if fam in ("bernoulli", "quasibinomial", "modified_huber", "ordinal"):
+            v = 1.0 / (1.0 + np.minimum(1e19, np.exp(-v)))
+        elif fam in ("multinomial", "poisson", "gamma", "tweedie"):
+            v = np.minimum(1e19, np.exp(v))
+        return v.reshape(n, 1)
+
+    def decision_paths(self, df):
+        """Leaf assignment per (row, tree) as 'L'/'R' strings (tree models)."""
+        X = self.row_matrix(df)
+        dl = self.dom_len if self.version >= 1.2 else None
+        out = []
+        for ci in range(self.ntrees_per_group):
+            for t in self.trees[ci]:
+                paths = [""] * X.shape[0]
+                if t is not None:
+                    t.score(X, dl, self.version, paths)
+                out.append(paths)
+        return [list(r) for r in zip(*out)]
+
+    # ------------------------------------------------------------- outputs
+    def predict_raw(self, df) -> np.ndarray:
+        """[n, K] class probabilities (classification) or [n, 1] values /
+        cluster ids (Generic model metrics)."""
+        preds = self.score0(self.row_matrix(df))
+        if self.nclasses > 1 and preds.shape[1] > 1:
+            return preds[:, 1:]
+        return preds[:, :1]
+
+    def predict(self, df):
+        import pandas as pd
+        preds = self.score0(self.row_matrix(df))
+        if self.algo == "kmeans":
+            return pd.DataFrame({"predict": preds[:, 0].astype(np.int64)})
+        if self.algo == "isolationforest":
+            cols = ["predict", "score", "mean_length"] if self.output_anomaly_flag else ["predict", "mean_length"]
+            return pd.DataFrame(preds, columns=cols)
+        if self.algo == "extendedisolationforest":
+            return pd.DataFrame(preds, columns=["anomaly_score", "mean_length"])
+        if self.category == "AutoEncoder":
+            return pd.DataFrame(preds, columns=[f"reconstr_{i}" for i in range(preds.shape[1])])
+        if self.nclasses > 1 and preds.shape[1] > 1:
+            dom = self.response_domain or [str(i) for i in range(self.nclasses)]
+            lab = np.array(dom, dtype=object)[preds[:, 0].astype(np.int64)]
+            out = {"predict": lab}
+            for k, d in enumerate(dom):
+                out[d] = preds[:, 1 + k]
+            cal = getattr(self, "calibrated", None)
+            if cal is not None and self.calib_beta is not None:
+                out["cal_" + dom[0]] = cal[:, 0]
+                out["cal_" + dom[1]] = cal[:, 1]
+            return pd.DataFrame(out)
+        return pd.DataFrame({"predict": preds[:, 0]})
+
+    def predict_row(self, row: dict):
+        return self.predict(row).iloc[0].to_dict()
+
+
+def load(src) -> H2OMojoModel:
+    return H2OMojoModel(src)

@@ -4,6 +4,14 @@ import zipfile
 
 
 def describe(path):
+    """model.ini text, metadata and file list of a MOJO in either layout
+    (this platform's model.json, or the reference's model.ini-only layout)."""
     with zipfile.ZipFile(path) as z:
-        return {"ini": z.read("model.ini").decode(), "meta": json.loads(z.read("model.json")),
-                "files": z.namelist()}
+        names = z.namelist()
+        ini = z.read("model.ini").decode()
+        if "model.json" in names:
+            meta = json.loads(z.read("model.json"))
+        else:
+            from .h2o_mojo import H2OMojoModel
+            meta = H2OMojoModel(path).meta
+        return {"ini": ini, "meta": meta, "files": names}
