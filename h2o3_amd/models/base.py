@@ -740,8 +740,22 @@ class H2OEstimator:
         from ..mojo.pojo import download_pojo
         return download_pojo(self, path)
 
-    def download_mojo(self, path=".", get_genmodel_jar=False, genmodel_name="", **kw):
+    def download_mojo(self, path=".", get_genmodel_jar=False, genmodel_name="", format="native", **kw):
+        """Write the model's MOJO zip.  format="native": this platform's layout
+        (every algorithm, numpy scorer in mojo/genmodel.py); format="h2o": the
+        reference's h2o-genmodel layout (GBM / DRF / GLM), readable by the
+        reference's Java MojoModel and by mojo/h2o_mojo.py."""
         from ..mojo import writer
+        if format == "h2o":
+            import os as _os
+            from ..mojo.h2o_writer import build_h2o_mojo
+            data = build_h2o_mojo(self)
+            if _os.path.isdir(path) or not path.endswith(".zip"):
+                _os.makedirs(path, exist_ok=True)
+                path = _os.path.join(path, f"{self.model_id}.zip")
+            with open(path, "wb") as f:
+                f.write(data)
+            return path
         return writer.write_mojo(self, path)
 
     save_mojo = download_mojo

@@ -1,0 +1,108 @@
+"""Reference-layout MOJO export (mojo/h2o_writer.py) round-trips through the
+reference-layout reader (mojo/h2o_mojo.py, pinned against the reference's own
+genmodel fixtures in tests/test_mojo_reference.py): predictions of the
+exported MOJO equal the in-platform predictions."""
+import numpy as np
+import pandas as pd
+import pytest
+
+
+@pytest.fixture(scope="module")
+def data():
+    import h2o3_amd as h2o
+    h2o.init(verbose=False)
+    rng = np.random.RandomState(3)
+    n = 1500
+    X = rng.randn(n, 4)
+    X[rng.rand(n) < 0.08, 1] = np.nan
+    cat = rng.choice(list("abcdefghij"), n)
+    big = rng.choice([f"L{i}" for i in range(45)], n)       # > 32 levels: general bitset
+    logit = X[:, 0] - 0.7 * np.nan_to_num(X[:, 1]) + (cat == "c") * 1.5 - (big == "L7") * 2
+    df = pd.DataFrame(X, columns=list("pqrs"))
+    df["cat"] = cat
+    df["big"] = big
+    df["yb"] = np.where(rng.rand(n) < 1 / (1 + np.exp(-logit)), "yes", "no")
+    df["yr"] = logit + 0.1 * rng.randn(n)
+    df["ym"] = np.where(logit > 1, "hi", np.where(logit < -1, "lo", "mid"))
+    return df, h2o.H2OFrame(df)
+
+
+def _roundtrip(model, df, tmp_path):
+    """Score the exported MOJO on the float32 values the platform's frame
+    holds (numeric Vecs are f32 in HBM): the reference scorer compares the
+    row's double against float32 split values, so scoring the unrounded f64
+    inputs can flip rows that sit exactly on a split point."""
+    from h2o3_amd.mojo import h2o_mojo
+    path = model.download_mojo(str(tmp_path), format="h2o")
+    m = h2o_mojo.load(path)
+    d32 = df.copy()
+    for c in d32.columns:
+        if d32[c].dtype.kind == "f":
+            d32[c] = d32[c].astype(np.float32).astype(np.float64)
+    return m, m.predict(d32)
+
+
+X = ["p", "q", "r", "s", "cat", "big"]
+
+
+@pytest.mark.parametrize("y", ["yb", "yr", "ym"])
+def test_gbm_h2o_mojo_roundtrip(data, y, tmp_path):
+    from h2o3_amd.estimators import H2OGradientBoostingEstimator
+    df, fr = data
+    g = H2OGradientBoostingEstimator(ntrees=8, max_depth=4, seed=1)
+    g.train(x=X, y=y, training_frame=fr)
+    ours = g.predict(fr).as_data_frame()
+    m, theirs = _roundtrip(g, df, tmp_path)
+    cols = [c for c in ours.columns if c != "predict"] or ["predict"]
+    np.testing.assert_allclose(theirs[cols].values.astype(float), ours[cols].values.astype(float), atol=2e-5)
+    if y != "yr":
+        assert (theirs["predict"].astype(str).values == ours["predict"].astype(str).values).mean() > 0.999
+
+
+@pytest.mark.parametrize("y", ["yb", "yr", "ym"])
+def test_drf_h2o_mojo_roundtrip(data, y, tmp_path):
+    from h2o3_amd.estimators import H2ORandomForestEstimator
+    df, fr = data
+    d = H2ORandomForestEstimator(ntrees=6, max_depth=6, seed=2)
+    d.train(x=X, y=y, training_frame=fr)
+    ours = d.predict(fr).as_data_frame()
+    m, theirs = _roundtrip(d, df, tmp_path)
+    cols = [c for c in ours.columns if c != "predict"] or ["predict"]
+    np.testing.assert_allclose(theirs[cols].values.astype(float), ours[cols].values.astype(float), atol=2e-5)
+
+
+@pytest.mark.parametrize("family,y", [("binomial", "yb"), ("gaussian", "yr"), ("multinomial", "ym"),
+                                      ("poisson", "yr")])
+def test_glm_h2o_mojo_roundtrip(data, family, y, tmp_path):
+    from h2o3_amd.estimators import H2OGeneralizedLinearEstimator
+    df, fr = data
+    d2 = df.copy()
+    if family == "poisson":
+        d2["yr"] = np.round(np.exp(np.clip(df["yr"].values, -2, 2) * 0.5))
+        import h2o3_amd as h2o
+        fr2 = h2o.H2OFrame(d2)
+    else:
+        fr2 = fr
+    g = H2OGeneralizedLinearEstimator(family=family, lambda_=0.0)
+    g.train(x=X, y=y, training_frame=fr2)
+    ours = g.predict(fr2).as_data_frame()
+    m, theirs = _roundtrip(g, d2, tmp_path)
+    cols = [c for c in ours.columns if c != "predict"] or ["predict"]
+    np.testing.assert_allclose(theirs[cols].values.astype(float), ours[cols].values.astype(float), rtol=1e-4,
+                               atol=1e-5)
+
+
+def test_h2o_mojo_files_layout(data, tmp_path):
+    import zipfile
+    from h2o3_amd.estimators import H2OGradientBoostingEstimator
+    df, fr = data
+    g = H2OGradientBoostingEstimator(ntrees=3, max_depth=3, seed=1)
+    g.train(x=X, y="yb", training_frame=fr)
+    path = g.download_mojo(str(tmp_path), format="h2o")
+    names = zipfile.ZipFile(path).namelist()
+    assert "model.ini" in names and "model.json" not in names
+    assert {"trees/t00_000.bin", "trees/t00_000_aux.bin", "trees/t00_002.bin"} <= set(names)
+    ini = zipfile.ZipFile(path).read("model.ini").decode()
+    for key in ("algorithm = Gradient Boosting Machine", "n_trees = 3", "distribution = bernoulli",
+                "mojo_version = 1.40", "[columns]", "[domains]"):
+        assert key in ini
