@@ -787,6 +787,7 @@ class TreeGrower:
             p0 = self._va_eff.clone() if self._va_eff is va else self._va_eff
             self._pos1 = [p0, torch.empty_like(p0)]   # root: position order == row order
         ridx, ridx2 = self.ridx, self.ridx2
+        self._la = None
         pa, pb, pa2, pb2 = self._pay
         if self.use_payload:
             pa.copy_(va)
@@ -817,7 +818,17 @@ class TreeGrower:
             level_bytes = self.Fpad * n_front * bd.Bs * C_ * 8
             prev_bytes = 0 if H_prev is None else H_prev.numel() * 8
             chunked = can_split and (level_bytes + prev_bytes) > p.hist_mem_budget and n_front > 1
-            if chunked:
+            la, self._la = self._la, None
+            if la is not None and (chunked or not can_split or la[0].shape[1] < n_front):
+                la = None   # defensive: the look-ahead only matches a full next level
+            if la is not None:
+                # this level's histograms were built on the device before the
+                # host read the previous level's decisions (_lookahead)
+                H = la[0][:, :n_front].contiguous()
+                wyy_level = la[1][:n_front] if la[1] is not None else None
+                if os.environ.get("H2O3_LA_CHECK") == "1":
+                    self._la_check(la, pair_info, slot_of)
+            elif chunked:
                 # frontier too wide for one level of histograms (deep DRF trees, wide
                 # high-cardinality data): histograms of node batches straight from the
                 # rows, split records concatenated, no parent level kept (no subtraction)
@@ -839,7 +850,9 @@ class TreeGrower:
                     par_slots.append(pslot)
                 Hb = self._build_hist(ridx, va, vb, mode, [frontier[s][1] for s in build_slots],
                                       [frontier[s][2] for s in build_slots])
-            if level > 0 and H_prev is not None and (can_split or level == 0) and self.dev.type == "cuda":
+            if la is not None:
+                pass
+            elif level > 0 and H_prev is not None and (can_split or level == 0) and self.dev.type == "cuda":
                 # copy + parent-minus-built subtraction in one kernel
                 clamp = {0: 0b1, 1: 0b0}.get(mode, (1 << tree_ops.channels(mode)) - 1)
                 wb = self._last_wyy if mode == 0 else None
@@ -895,7 +908,12 @@ class TreeGrower:
                         tree_ops.partition_async(bd, ridx, ridx2, sp["feat_i32"], sp["mask"],
                                                  [f[1] for f in frontier], [f[2] for f in frontier],
                                                  payload=pay, pk=pkd, pk_col=11)
-                    pk = pkd.cpu().numpy()
+                    # the record's copy is queued BEFORE the look-ahead kernels, so
+                    # the host gets it while the GPU builds the next level
+                    pk_h = self._d2h_async(pkd)
+                    self._maybe_lookahead(pkd, (10, 11, 4 + (mode == 1), 6 + (mode == 1)), frontier, mode, va, vb,
+                                          ridx2, H, wyy_level, depth, level_bytes, chunked)
+                    pk = self._d2h_wait(pk_h)
                     ok_h = pk[:, 10] > 0
                     nleft_pre = pk[:, 11].astype(np.int64).tolist()
                 cols = [] if nleft_pre is not None else [sp["gain"].view(nn_, 1).to(torch.float64), sp["feat"].view(nn_, 1).to(torch.float64),
@@ -920,7 +938,13 @@ class TreeGrower:
                     cols += [ok_d.view(nn_, 1).to(torch.float64), nleft_d.view(nn_, 1).to(torch.float64)]
                 # ONE device->host transfer of every per-node scalar of the level
                 if cols:
-                    pk = torch.cat(cols, 1).cpu().numpy()
+                    rec = torch.cat(cols, 1)
+                    pk_h = self._d2h_async(rec)
+                    if async_part:
+                        self._maybe_lookahead(rec, (4 + 3 * C, 5 + 3 * C, 4 + (mode == 1), 4 + C + (mode == 1)),
+                                              frontier, mode, va, vb, ridx2, H, wyy_level, depth, level_bytes,
+                                              chunked)
+                    pk = self._d2h_wait(pk_h)
                     if async_part:
                         ok_h = pk[:, 4 + 3 * C] > 0
                         nleft_pre = pk[:, 5 + 3 * C].astype(np.int64).tolist()
@@ -1073,6 +1097,81 @@ class TreeGrower:
                                                  dtype=np.float64)) if leaf_tot else \
             torch.zeros((0, C), dtype=torch.float64)
         return tree, nid, leaves, leaf_tot_t
+
+    def _d2h_async(self, t):
+        """Queue a device->host copy of t into a reusable pinned slot; returns
+        (host view, event).  CPU tensors pass through."""
+        if t.device.type != "cuda":
+            return (t, None)
+        ring = self.__dict__.setdefault("_d2h_ring", [None, None])
+        k = self.__dict__.get("_d2h_k", 0)
+        self._d2h_k = k ^ 1
+        buf = ring[k]
+        if buf is None or buf.numel() < t.numel():
+            buf = ring[k] = torch.empty(max(t.numel(), 4096), dtype=t.dtype, pin_memory=True)
+        h = buf[:t.numel()].view(t.shape)
+        h.copy_(t, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return (h, ev)
+
+    @staticmethod
+    def _d2h_wait(hev):
+        h, ev = hev
+        if ev is not None:
+            ev.synchronize()
+        return h.numpy().copy()
+
+    def _maybe_lookahead(self, rec, cols, frontier, mode, va, vb, ridx_next, H, wyy_level, depth, level_bytes,
+                         chunked):
+        """Launch the NEXT level's histograms now (device-built work list,
+        tree_ops.hist_build_dev + hist_sibling_dev), before the host syncs on
+        this level's split record: the host bookkeeping of this level then runs
+        while the GPU builds the next level's histograms.  Only for a full next
+        level (every node may split) that fits the histogram budget; else the
+        next level is built after the sync as before."""
+        self._la = None
+        p = self.p
+        if os.environ.get("H2O3_LOOKAHEAD", "1") != "1" or self.dev.type != "cuda" or chunked or H is None or \
+                depth + 1 >= p.max_depth or mode not in (0, 1) or p.max_leaves:
+            return
+        n = len(frontier)
+        if 2 * level_bytes + H.numel() * 8 > p.hist_mem_budget:
+            return
+        posv = False
+        va_n, vb_n = va, vb
+        if mode == 0 and getattr(self, "_pos1", None) is not None:
+            va_n, vb_n, posv = self._pos1[1], None, True     # the payload the partition just moved
+        elif mode == 0 and getattr(self, "_va_eff", None) is not None:
+            va_n, vb_n = self._va_eff, None
+        with phase("tree.hist"), phase("tree.hist.lookahead"):
+            r = tree_ops.hist_build_dev(self.bd, ridx_next, va_n, vb_n, mode, rec, cols,
+                                        [f[1] for f in frontier], [f[2] for f in frontier], self._vmax, posv=posv,
+                                        unit_w=getattr(self, "_unit_w", False))
+            if r is None:
+                return
+            Hb, wyy_b, slots, cnts = r
+            if wyy_b is not None:
+                coll.allreduce_(wyy_b)
+            if self.W > 1:
+                if self.Fpad > self.bd.F:
+                    Hb = torch.cat([Hb, torch.zeros((self.Fpad - self.bd.F,) + tuple(Hb.shape[1:]), dtype=Hb.dtype,
+                                                    device=Hb.device)], 0)
+                Hb = coll.reduce_scatter_dim0(Hb)
+            clamp = {0: 0b1, 1: 0b0}.get(mode, (1 << tree_ops.channels(mode)) - 1)
+            Hn, wyy_n = tree_ops.hist_sibling_dev(Hb, H, slots, cnts, clamp, wyy_b=wyy_b if mode == 0 else None,
+                                                  wyy_prev=wyy_level if mode == 0 else None)
+        self._la = (Hn, wyy_n, slots, cnts)
+
+    def _la_check(self, la, pair_info, slot_of):
+        """Debug (H2O3_LA_CHECK=1): the device-built pair slots equal the host's."""
+        slots, cnts = la[2].cpu().numpy(), la[3].cpu().numpy()
+        nb = len(pair_info)
+        assert int(cnts[0]) == nb, (int(cnts[0]), nb)
+        nl = len(slots) // 3
+        for j, (lid, rid, pslot, build_left) in enumerate(pair_info):
+            b, d = (lid, rid) if build_left else (rid, lid)
+            assert slots[j] == slot_of[b] and slots[nl + j] == slot_of[d] and slots[2 * nl + j] == pslot, j
 
     def _totals(self, H):
         """Per-node channel totals [n, C] (global), from feature 0."""

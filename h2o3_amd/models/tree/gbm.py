@@ -261,7 +261,13 @@ class GBMDriver:
                                          torch.zeros_like(den)).clamp(-maxabs, maxabs) * lr
                 with phase("gbm.update"):
                     tree_ops.leaf_update(self.grower.ridx, self.f, vals_d.to(torch.float32), lids, st, ct)
-                hv = torch.empty(vals_d.shape, dtype=torch.float64, pin_memory=True)
+                # two reusable pinned slots: tree t's values land in one while
+                # tree t-1's (read by _resolve_pending below) sit in the other
+                ring = self.__dict__.setdefault("_hv_ring", [None, None])
+                k_ = self.iter & 1
+                if ring[k_] is None or ring[k_].numel() < vals_d.numel():
+                    ring[k_] = torch.empty(max(vals_d.numel(), 1024), dtype=torch.float64, pin_memory=True)
+                hv = ring[k_][:vals_d.numel()]
                 hv.copy_(vals_d, non_blocking=True)
                 ev = torch.cuda.Event()
                 ev.record()

@@ -177,14 +177,19 @@ __global__ __launch_bounds__(1024) void hist_quad_kernel(
     const float* __restrict__ va, const float* __restrict__ vb,
     const int4* __restrict__ work, int n_work, int n_fg, int fgw, int F, int foff, int Bs, float s0, float s1,
     double* __restrict__ hist, int n_slots, double* __restrict__ wyy_out, long long bq,
-    const uint8_t* __restrict__ need) {
+    const uint8_t* __restrict__ need, const int* __restrict__ n_work_dev) {
   using CT = typename CodeW<LW>::T;
   constexpr int C = Chan<MODE>::C;
   constexpr int CL = PACK ? 1 : C;       // u64 entries per bin in LDS
   constexpr int NK = 4 * LW;             // features per lane
   constexpr int U = 4;                   // rows per lane per iteration
   extern __shared__ __attribute__((aligned(16))) unsigned long long ldsq[];
-  const int nwg = n_work * n_fg;
+  // n_work_dev: the work list was built on the device (child_work_kernel) and
+  // the grid is an upper bound -- blocks past the real count leave at once.
+  // The XCD remap runs over the REAL block count (remapping over the padded
+  // grid put every live block on the first XCDs: +20% level time)
+  const int nwg = n_work_dev != nullptr ? n_work_dev[1] * n_fg : n_work * n_fg;
+  if ((int)blockIdx.x >= nwg) return;
   const int lb = xcd_remap(blockIdx.x, nwg);
   const int fgi = lb % n_fg;
   const int4 wk = work[lb / n_fg];
@@ -329,14 +334,14 @@ struct QuadArgs {
   dim3 grid; int threads; size_t lds; hipStream_t s;
   const uint8_t* cc; int Fp; const int* ridx; const float* va; const float* vb; const int4* wk;
   int n_work, n_fg, fgw, F, foff, Bs; float s0, s1; double* hist; int n_slots; double* wyy; long long bq;
-  const uint8_t* need;
+  const uint8_t* need; const int* n_work_dev;
 };
 
 template <int M, bool V, bool PV, bool PK, bool PIPE = true, int LW = 1>
 static void lq(const QuadArgs& a) {
   hipLaunchKernelGGL((hist_quad_kernel<M, V, PV, PK, PIPE, LW>), a.grid, dim3(a.threads), a.lds, a.s, a.cc, a.Fp,
                      a.ridx, a.va, a.vb, a.wk, a.n_work, a.n_fg, a.fgw, a.F, a.foff, a.Bs, a.s0, a.s1, a.hist,
-                     a.n_slots, a.wyy, a.bq, a.need);
+                     a.n_slots, a.wyy, a.bq, a.need, a.n_work_dev);
 }
 
 static int env_int(const char* k, int d) {
@@ -364,10 +369,26 @@ static void lq_pv(int posv, int pack, int lw, const QuadArgs& a) {
 // Histograms of features [foff, F) in n_fg = ceil((F - foff) / fgw) groups of
 // fgw features (a multiple of 4, at most 64; tree_ops.quad_groups picks it).
 // pack_bq >= 0 selects the packed single-atomic path (MODE 0, 0/1 weights).
+extern "C" int h2o_hist_quad4(const void* codes, int Fp, const int* ridx, const float* va, const float* vb,
+                              const int* work, int n_work, int F, int foff, int Bs, float s0, float s1,
+                              double* hist, int n_slots, int mode, int threads, double* wyy, int posv,
+                              long long pack_bq, int fgw, const uint8_t* need, const int* n_work_dev,
+                              hipStream_t s);
 extern "C" int h2o_hist_quad3(const void* codes, int Fp, const int* ridx, const float* va, const float* vb,
                               const int* work, int n_work, int F, int foff, int Bs, float s0, float s1,
                               double* hist, int n_slots, int mode, int threads, double* wyy, int posv,
                               long long pack_bq, int fgw, const uint8_t* need, hipStream_t s) {
+  return h2o_hist_quad4(codes, Fp, ridx, va, vb, work, n_work, F, foff, Bs, s0, s1, hist, n_slots, mode, threads,
+                        wyy, posv, pack_bq, fgw, need, nullptr, s);
+}
+
+// n_work_dev != nullptr: n_work is the CAPACITY of the device-built work list
+// (grid upper bound); the real count is n_work_dev[1].
+extern "C" int h2o_hist_quad4(const void* codes, int Fp, const int* ridx, const float* va, const float* vb,
+                              const int* work, int n_work, int F, int foff, int Bs, float s0, float s1,
+                              double* hist, int n_slots, int mode, int threads, double* wyy, int posv,
+                              long long pack_bq, int fgw, const uint8_t* need, const int* n_work_dev,
+                              hipStream_t s) {
   if (n_work <= 0 || foff >= F) return 0;
   if (Fp % 4 != 0 || foff % 4 != 0 || Bs > 256 || mode < 0 || mode > 2) return -1;
   if (fgw < 4 || fgw > 64 || fgw % 4 != 0) return -2;
@@ -384,7 +405,7 @@ extern "C" int h2o_hist_quad3(const void* codes, int Fp, const int* ridx, const 
   if (a.lds > 160 * 1024) return -4;
   a.cc = (const uint8_t*)codes; a.Fp = Fp; a.ridx = ridx; a.va = va; a.vb = vb; a.wk = (const int4*)work;
   a.n_work = n_work; a.n_fg = n_fg; a.fgw = fgw; a.F = F; a.foff = foff; a.Bs = Bs; a.s0 = s0; a.s1 = s1;
-  a.hist = hist; a.n_slots = n_slots; a.wyy = wyy; a.bq = pack_bq; a.need = need;
+  a.hist = hist; a.n_slots = n_slots; a.wyy = wyy; a.bq = pack_bq; a.need = need; a.n_work_dev = n_work_dev;
   switch (mode) {
     case 0: if (vb) lq_pv<0, true>(posv, pack, lw, a); else lq_pv<0, false>(posv, pack, lw, a); break;
     case 1: lq_pv<1, true>(posv, 0, lw, a); break;
@@ -646,8 +667,10 @@ __global__ __launch_bounds__(256) void hist_sibling_kernel(const double* __restr
                                                            int BsC, int C, int clamp_mask,
                                                            double* __restrict__ H, const double* __restrict__ wyy_b,
                                                            const double* __restrict__ wyy_p,
-                                                           double* __restrict__ wyy_out) {
+                                                           double* __restrict__ wyy_out,
+                                                           const int* __restrict__ nb_dev) {
   const int j = blockIdx.x;          // pair
+  if (nb_dev != nullptr && j >= nb_dev[0]) return;   // device-built pair list: grid is an upper bound
   const int f = blockIdx.y;          // feature
   const int bs = slots[j], ds = slots[nb + j], ps = slots[2 * nb + j];
   const double* hb = Hb + ((size_t)f * nb + j) * BsC;
@@ -676,7 +699,6 @@ __global__ __launch_bounds__(1024) void part_offsets_kernel(const int* __restric
                                                             int* __restrict__ loff, int* __restrict__ roff,
                                                             long long* __restrict__ nleft, double* __restrict__ pk,
                                                             int stride, int col) {
-  __shared__ long long part[1024];
   __shared__ long long carry;
   const long long* slot = meta;
   const long long* first = meta + nw;
@@ -685,29 +707,45 @@ __global__ __launch_bounds__(1024) void part_offsets_kernel(const int* __restric
   for (int s = threadIdx.x; s < n; s += blockDim.x) nleft[s] = 0;
   if (threadIdx.x == 0) carry = 0;
   __syncthreads();
-  // pass 1: node totals
-  for (int i = threadIdx.x; i < nw; i += blockDim.x) atomicAdd((unsigned long long*)&nleft[slot[i]],
-                                                               (unsigned long long)cnt[i]);
-  __syncthreads();
-  // pass 2: global exclusive scan of cnt, tile by tile
+  // pass 2: global exclusive scan of cnt, 1024 chunks per tile: inclusive
+  // scan inside each wave by shuffles, wave totals scanned by wave 0 -- two
+  // barriers per tile (the Hillis-Steele LDS scan took 20; 113 us -> ~10 us
+  // per level at 6k chunks)
+  __shared__ long long wtot[16];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
   for (int base = 0; base < nw; base += blockDim.x) {
     const int i = base + threadIdx.x;
     const long long v = i < nw ? (long long)cnt[i] : 0;
-    part[threadIdx.x] = v;
-    __syncthreads();
-    for (int o = 1; o < (int)blockDim.x; o <<= 1) {
-      const long long t = threadIdx.x >= (unsigned)o ? part[threadIdx.x - o] : 0;
-      __syncthreads();
-      part[threadIdx.x] += t;
-      __syncthreads();
+    long long x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const long long t = __shfl_up(x, o, 64);
+      if (lane >= o) x += t;
     }
-    const long long excl = carry + part[threadIdx.x] - v;
-    if (i < nw) loff[i] = (int)excl;   // global exclusive prefix, rebased per node below
+    if (lane == 63) wtot[wv] = x;
     __syncthreads();
-    if (threadIdx.x == blockDim.x - 1) carry += part[threadIdx.x];
+    if (wv == 0) {
+      long long w = lane < nwv ? wtot[lane] : 0;
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        const long long t = __shfl_up(w, o, 64);
+        if (lane >= o) w += t;
+      }
+      if (lane < nwv) wtot[lane] = w;   // inclusive prefix of wave totals
+    }
+    __syncthreads();
+    const long long before = (wv > 0 ? wtot[wv - 1] : 0) + carry;
+    if (i < nw) loff[i] = (int)(before + x - v);   // global exclusive prefix, rebased per node below
+    __syncthreads();
+    if (threadIdx.x == 0) carry += wtot[nwv - 1];
     __syncthreads();
   }
   __syncthreads();
+  // node totals from the scan (chunks of a node are consecutive): the node's
+  // last chunk holds prefix_end - prefix_start -- no same-address atomics
+  for (int i = threadIdx.x; i < nw; i += blockDim.x)
+    if (i == nw - 1 || first[i + 1] != first[i])
+      nleft[slot[i]] = (long long)loff[i] + cnt[i] - (long long)loff[first[i]];
   for (int i = threadIdx.x; i < nw; i += blockDim.x) roff[i] = loff[first[i]];   // node's first-chunk prefix
   __syncthreads();
   for (int i = threadIdx.x; i < nw; i += blockDim.x) {
@@ -800,7 +838,98 @@ int h2o_hist_sibling(const double* Hb, const double* Hp, const int* slots, int n
                      hipStream_t s) {
   if (nb <= 0 || F <= 0) return 0;
   hipLaunchKernelGGL(hist_sibling_kernel, dim3(nb, F), dim3(256), 0, s, Hb, Hp, slots, nb, np, nf, BsC, C, clamp_mask,
-                     H, wyy_b, wyy_p, wyy_out);
+                     H, wyy_b, wyy_p, wyy_out, nullptr);
+  return (int)hipGetLastError();
+}
+
+// Same with the pair count read on the device (counts[0]); nb = capacity.
+int h2o_hist_sibling_dev(const double* Hb, const double* Hp, const int* slots, int nb, int np, int nf, int F,
+                         int BsC, int C, int clamp_mask, double* H, const double* wyy_b, const double* wyy_p,
+                         double* wyy_out, const int* counts, hipStream_t s) {
+  if (nb <= 0 || F <= 0) return 0;
+  hipLaunchKernelGGL(hist_sibling_kernel, dim3(nb, F), dim3(256), 0, s, Hb, Hp, slots, nb, np, nf, BsC, C, clamp_mask,
+                     H, wyy_b, wyy_p, wyy_out, counts);
+  return (int)hipGetLastError();
+}
+
+// Next-level histogram work built on the device right after a level's
+// partition, so the level's histograms start before the host has read the
+// split decisions (the host bookkeeping then overlaps GPU work).  One
+// workgroup.  For frontier node i (segment st[i], ct[i]) that splits
+// (rec[i*stride + ok_col] > 0) with nleft = rec[..nl_col]: pair j = rank of i
+// among splitting nodes; the built child is the lighter one (weights
+// rec[wl_col] <= rec[wr_col] -> left, the host's rule); its segment is
+// chunked into work items (j, start, count, k).  slots = [build | der | par]
+// (stride n): build = 2j + !left, der = 2j + left, par = i.
+// counts[0] = #pairs, counts[1] = #work items (capped at cap).
+__global__ __launch_bounds__(1024) void child_work_kernel(const long long* __restrict__ st,
+                                                          const long long* __restrict__ ct,
+                                                          const double* __restrict__ rec, int stride, int ok_col,
+                                                          int nl_col, int wl_col, int wr_col, int n, int chunk,
+                                                          int cap, int4* __restrict__ work, int* __restrict__ slots,
+                                                          int* __restrict__ counts) {
+  __shared__ long long wtot[2][16];
+  __shared__ long long carry[2];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+  if (threadIdx.x == 0) carry[0] = carry[1] = 0;
+  __syncthreads();
+  for (int base = 0; base < n; base += blockDim.x) {
+    const int i = base + threadIdx.x;
+    long long sp = 0, nch = 0, start = 0, cnt = 0;
+    bool bl = true;
+    if (i < n && rec[(size_t)i * stride + ok_col] > 0) {
+      const long long nl = (long long)rec[(size_t)i * stride + nl_col];
+      bl = rec[(size_t)i * stride + wl_col] <= rec[(size_t)i * stride + wr_col];
+      cnt = bl ? nl : ct[i] - nl;
+      start = bl ? st[i] : st[i] + nl;
+      sp = 1;
+      nch = (cnt + chunk - 1) / chunk;
+    }
+    long long a = sp, b = nch;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const long long ta = __shfl_up(a, o, 64), tb = __shfl_up(b, o, 64);
+      if (lane >= o) { a += ta; b += tb; }
+    }
+    if (lane == 63) { wtot[0][wv] = a; wtot[1][wv] = b; }
+    __syncthreads();
+    if (wv == 0) {
+      long long x = lane < nwv ? wtot[0][lane] : 0, y = lane < nwv ? wtot[1][lane] : 0;
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        const long long tx = __shfl_up(x, o, 64), ty = __shfl_up(y, o, 64);
+        if (lane >= o) { x += tx; y += ty; }
+      }
+      if (lane < nwv) { wtot[0][lane] = x; wtot[1][lane] = y; }
+    }
+    __syncthreads();
+    const long long j = carry[0] + (wv > 0 ? wtot[0][wv - 1] : 0) + a - sp;
+    const long long it0 = carry[1] + (wv > 0 ? wtot[1][wv - 1] : 0) + b - nch;
+    if (sp) {
+      slots[j] = (int)(2 * j + (bl ? 0 : 1));
+      slots[n + j] = (int)(2 * j + (bl ? 1 : 0));
+      slots[2 * n + j] = i;
+      for (long long k = 0; k < nch && it0 + k < cap; ++k) {
+        const long long p = start + k * chunk;
+        work[it0 + k] = make_int4((int)j, (int)p, (int)min((long long)chunk, cnt - k * chunk), (int)k);
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) { carry[0] += wtot[0][nwv - 1]; carry[1] += wtot[1][nwv - 1]; }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    counts[0] = (int)carry[0];
+    counts[1] = (int)min(carry[1], (long long)cap);
+  }
+}
+
+int h2o_child_work(const long long* st, const long long* ct, const double* rec, int stride, int ok_col, int nl_col,
+                   int wl_col, int wr_col, int n, int chunk, int cap, int* work, int* slots, int* counts,
+                   hipStream_t s) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(child_work_kernel, dim3(1), dim3(1024), 0, s, st, ct, rec, stride, ok_col, nl_col, wl_col, wr_col,
+                     n, chunk, cap, (int4*)work, slots, counts);
   return (int)hipGetLastError();
 }
 

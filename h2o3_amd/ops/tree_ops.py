@@ -480,6 +480,85 @@ def partition_async(bd, ridx, ridx_out, feat_d, masks, starts, counts, chunk=163
     return nleft
 
 
+def hist_build_dev(bd, ridx, va, vb, mode, rec, rec_cols, starts, counts, vmax, posv=False, unit_w=False,
+                   target_blocks=2048):
+    """Next-level histograms of the lighter child of every splitting node,
+    with the work list built ON THE DEVICE from the level's split record
+    (child_work_kernel): launched right after the partition, before the host
+    reads the split decisions, so the host's level bookkeeping overlaps GPU
+    work.  rec: [n, stride] f64 device record; rec_cols = (ok, nleft, wl, wr)
+    column indices.  Returns (Hb [F, n, Bs, C] with pair j in slot j, wyy [n]
+    or None, slots [3n] int32 (build | der | par), counts [2] int32 (#pairs,
+    #items)) -- capacities n = len(starts) -- or None when the quad kernel does
+    not apply (the caller then builds after the host sync as before)."""
+    dev = ridx.device
+    if dev.type != "cuda" or bd.code_bytes != 1 or bd.Fp % 4 != 0 or bd.Bs > 256 or mode not in (0, 1, 2) or \
+            os.environ.get("H2O3_HIST_KERNEL", "quad") != "quad":
+        return None
+    lib = _lib()
+    if not getattr(lib, "_typed_dev", False):
+        lib.h2o_child_work.argtypes = [_c_void, _c_void, _c_void] + [_c_int] * 8 + [_c_void, _c_void, _c_void,
+                                                                                  _c_void]
+        lib.h2o_hist_quad4.argtypes = [_c_void, _c_int, _c_void, _c_void, _c_void, _c_void, _c_int, _c_int, _c_int,
+                                       _c_int, ctypes.c_float, ctypes.c_float, _c_void, _c_int, _c_int, _c_int,
+                                       _c_void, _c_int, _c_ll, _c_int, _c_void, _c_void, _c_void]
+        lib.h2o_hist_sibling_dev.argtypes = [_c_void, _c_void, _c_void, _c_int, _c_int, _c_int, _c_int, _c_int,
+                                             _c_int, _c_int, _c_void, _c_void, _c_void, _c_void, _c_void, _c_void]
+        lib._typed_dev = True
+    n = len(starts)
+    C = channels(mode)
+    pack = mode == 0 and unit_w and os.environ.get("H2O3_HIST_PACK", "1") == "1"
+    n_fg, fgw = quad_groups(bd.F, bd.Fp, bd.Bs, pack)
+    total = int(sum(counts))
+    chunk = max(2048, -(-((total + 1) // 2) // max(1, target_blocks // n_fg)))
+    if pack and chunk >= (1 << 23):
+        pack = False
+        n_fg, fgw = quad_groups(bd.F, bd.Fp, bd.Bs, False)
+    cap = n + total // chunk + 1
+    stc = np.concatenate([np.asarray(starts, dtype=np.int64), np.asarray(counts, dtype=np.int64)])
+    stc_d = _h2d(stc, dev)
+    ibuf = torch.empty(4 * cap + 3 * n + 2, dtype=torch.int32, device=dev)
+    work, slots, cnts = ibuf[:4 * cap], ibuf[4 * cap:4 * cap + 3 * n], ibuf[4 * cap + 3 * n:]
+    ok_c, nl_c, wl_c, wr_c = rec_cols
+    rc = lib.h2o_child_work(_ptr(stc_d), _ptr(stc_d[n:]), _ptr(rec), rec.stride(0), ok_c, nl_c, wl_c, wr_c, n, chunk,
+                            cap, _ptr(work), _ptr(slots), _ptr(cnts), _stream())
+    if rc != 0:
+        raise RuntimeError(f"h2o_child_work failed: {rc}")
+    nh = bd.F * n * bd.Bs * C
+    want_wyy = mode == 0
+    buf = torch.zeros(nh + (n if want_wyy else 0), dtype=torch.float64, device=dev)
+    Hb = buf[:nh].view(bd.F, n, bd.Bs, C)
+    wyy = buf[nh:] if want_wyy else None
+    if vmax is None:
+        vmax = channel_max(va, vb, mode)
+    s0, s1 = (fixed_point_scale(m, chunk) for m in vmax)
+    bq = -1
+    if pack:
+        s1, bq = _pack_scale(vmax[1] if vb is None else max(vmax[1], 0.0), chunk)
+    rc = lib.h2o_hist_quad4(_ptr(bd.codes), bd.Fp, _ptr(ridx), _ptr(va), _ptr(vb), _ptr(work), cap, bd.F, 0, bd.Bs,
+                            s0, s1, _ptr(Hb), n, mode, 512, _ptr(wyy), 1 if posv else 0, bq, fgw, None, _ptr(cnts),
+                            _stream())
+    if rc != 0:
+        raise RuntimeError(f"h2o_hist_quad4 failed: {rc}")
+    return Hb, wyy, slots, cnts
+
+
+def hist_sibling_dev(Hb, H_prev, slots, cnts, clamp_mask, wyy_b=None, wyy_prev=None):
+    """hist_sibling with the device-built pair list of hist_build_dev: output
+    capacity 2 * n pairs (n = Hb.shape[1]); the caller slices the first
+    2 * #pairs slots once the host knows #pairs."""
+    lib = _lib()
+    F, nb, Bs, C = Hb.shape
+    H = torch.empty((F, 2 * nb, Bs, C), dtype=Hb.dtype, device=Hb.device)
+    wyy = torch.empty(2 * nb, dtype=torch.float64, device=Hb.device) if wyy_b is not None else None
+    Hp = H_prev.contiguous()
+    rc = lib.h2o_hist_sibling_dev(_ptr(Hb), _ptr(Hp), _ptr(slots), nb, Hp.shape[1], 2 * nb, F, Bs * C, C, clamp_mask,
+                                  _ptr(H), _ptr(wyy_b), _ptr(wyy_prev), _ptr(wyy), _ptr(cnts), _stream())
+    if rc != 0:
+        raise RuntimeError(f"h2o_hist_sibling_dev failed: {rc}")
+    return H, wyy
+
+
 def hist_sibling(Hb, H_prev, build_slots, der_slots, par_slots, n_front, clamp_mask, wyy_b=None, wyy_prev=None):
     """Next-level histograms in one kernel: built children copied, siblings =
     parent - built (clamped at 0 on the channels of clamp_mask).  Returns

@@ -457,3 +457,39 @@ def test_quad_kernel_feature_groups(F):
         h = tree_ops.hist_build(bd, ridx, va, None, 0, starts, counts, 2, use_native=True, unit_w=unit_w)
         r = tree_ops.hist_build(bd, ridx, va, None, 0, starts, counts, 2, use_native=False)
         torch.testing.assert_close(h, r, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("dist", ["bernoulli", "gaussian"])
+def test_lookahead_levels_same_model(dist, monkeypatch):
+    """Next-level histograms built from the device-side work list before the
+    host sync (engine._maybe_lookahead) grow the same trees as the host-built
+    path; H2O3_LA_CHECK asserts the device pair slots equal the host's."""
+    _need_gpu()
+    import pandas as pd
+    import h2o3_amd
+    from h2o3_amd.estimators import H2OGradientBoostingEstimator, H2OXGBoostEstimator
+    h2o3_amd.init(device="cuda:0", verbose=False)
+    rng = np.random.RandomState(4)
+    n = 60000
+    X = rng.randn(n, 12).astype(np.float32)
+    X[rng.rand(n) < 0.05, 3] = np.nan
+    df = pd.DataFrame(X, columns=[f"x{i}" for i in range(12)])
+    df["c"] = rng.choice(list("abcdefg"), n)
+    lin = X[:, 0] + np.nan_to_num(X[:, 3]) * X[:, 1] + (df["c"] == "b") * 0.8
+    df["y"] = np.where(rng.rand(n) < 1 / (1 + np.exp(-lin)), "p", "q") if dist == "bernoulli" else lin
+    fr = h2o3_amd.H2OFrame(df)
+    monkeypatch.setenv("H2O3_LA_CHECK", "1")
+    preds = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("H2O3_LOOKAHEAD", flag)
+        m = H2OGradientBoostingEstimator(ntrees=6, max_depth=7, seed=3, distribution=dist)
+        m.train(y="y", training_frame=fr)
+        preds.append(m.predict(fr).as_data_frame().values[:, -1].astype(float))
+    np.testing.assert_allclose(preds[0], preds[1], rtol=1e-6, atol=1e-6)
+    preds = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("H2O3_LOOKAHEAD", flag)
+        m = H2OXGBoostEstimator(ntrees=4, max_depth=6, seed=3)
+        m.train(y="y", training_frame=fr)
+        preds.append(m.predict(fr).as_data_frame().values[:, -1].astype(float))
+    np.testing.assert_allclose(preds[0], preds[1], rtol=1e-6, atol=1e-6)
