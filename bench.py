@@ -69,7 +69,8 @@ def main():
     ap.add_argument("--rows", type=int, default=100_000_000)
     ap.add_argument("--cols", type=int, default=100)
     ap.add_argument("--max-depth", type=int, default=8)
-    ap.add_argument("--algo", default="gbm", choices=["gbm", "glm", "drf"])
+    ap.add_argument("--algo", default="gbm", choices=["gbm", "glm", "drf", "kmeans"])
+    ap.add_argument("--k", type=int, default=16, help="K-Means clusters (--algo kmeans)")
     ap.add_argument("--cat-cols", type=int, default=0,
                     help="replace this many of the --cols columns by categoricals (DRF config: mixed num/cat)")
     ap.add_argument("--cat-card", type=int, default=1000, help="cardinality of the categorical columns")
@@ -116,6 +117,29 @@ def main():
         metric = "drf_trees_per_sec"
         unit = "trees/s"
         model = f"DRF binomial {args.rows // 1_000_000}Mx{F} ({args.cat_cols} cat, card {args.cat_card}) ntrees=1000"
+    elif args.algo == "kmeans":
+        # one step = one Lloyd iteration: fused HIP pass (distances, arg-min,
+        # per-cluster sums) + all-reduce + center update
+        from h2o3_amd.models.kmeans import H2OKMeansEstimator
+        from h2o3_amd.ops import cluster_ops
+        from h2o3_amd.parallel import collectives as coll
+        est = H2OKMeansEstimator(k=args.k, seed=42, standardize=False)
+        spec = TrainSpec(fr, names, None)
+        from h2o3_amd.models.datainfo import DataInfo
+        est._dinfo = DataInfo(fr, names, standardize=False, use_all_factor_levels=True, pad_to=4)
+        Xk, _ = est._design(fr)
+        del fr
+        C = [est._init_centers(Xk, None, args.k, __import__("numpy").random.RandomState(1))]
+        asg = torch.full((Xk.shape[0],), -1, dtype=torch.int32, device=dev)
+
+        def step():
+            st = cluster_ops.lloyd_pass(Xk, C[0], None, asg)
+            coll.allreduce_(st.vec)
+            C[0] = torch.where(st.weights.view(-1, 1) > 0, st.sums / st.weights.clamp_min(1e-300).view(-1, 1), C[0])
+        metric = "kmeans_iters_per_sec"
+        unit = "iters/s"
+        model = f"KMeans k={args.k} {args.rows / 1e6:g}Mx{F}"
+        extra_cfg = {"distance_precision": "f32 MFMA (v_mfma_f32_16x16x4_f32), f64 cross-workgroup sums"}
     else:
         from h2o3_amd.models.glm.glm import GLMDriver, H2OGeneralizedLinearEstimator
         est = H2OGeneralizedLinearEstimator(family="binomial", solver="IRLSM", lambda_=0.0)
@@ -170,7 +194,7 @@ def main():
                "scaling": "strong", "vs_baseline": None, "dtype": "fp32",
                "data": "synthetic (random normal features, logistic label), generated on device",
                "config": {"model": model, "rows": args.rows, "cols": F,
-                          **({} if args.algo == "glm" else {"max_depth": est._parms.get("max_depth"),
+                          **({} if args.algo in ("glm", "kmeans") else {"max_depth": est._parms.get("max_depth"),
                                                             "histogram_type": args.histogram_type,
                                                             "nbins": args.nbins}),
                           "global_batch": args.rows, "seq_len": None, "parallelism": f"dp{world}", **extra_cfg},

@@ -7,10 +7,8 @@ GLRM methods, importance table), hex/svd/SVD.java, hex/naivebayes/
 NaiveBayes.java (Laplace smoothing, gaussian numeric likelihoods,
 min_sdev/eps_sdev, min_prob/eps_prob).
 
-MI355X design: the expanded design matrix is one HBM tensor; KMeans
-distances are a GEMM (||x||^2 - 2 X C^T + ||c||^2) and centroid sums are a
-second GEMM (onehot(assign)^T X) on the matrix cores — no per-row atomics;
-PCA/SVD take the weighted Gram from the f32-MFMA Gram kernel and finish
+MI355X design: the expanded design matrix is one HBM tensor; K-Means
+lives in models/kmeans.py (one fused HIP pass per Lloyd iteration); PCA/SVD take the weighted Gram from the f32-MFMA Gram kernel and finish
 with a tiny f64 eigendecomposition; every reduction is one all_reduce.
 """
 from __future__ import annotations
@@ -36,156 +34,7 @@ def _seed(p, default=1234):
 
 
 # ====================================================================== KMeans
-KMEANS_DEFAULTS = dict(k=1, estimate_k=False, user_points=None, max_iterations=10, standardize=True, seed=-1,
-                       init="Furthest", categorical_encoding="auto", max_runtime_secs=0.0,
-                       cluster_size_constraints=None, score_each_iteration=False)
-
-
-class H2OKMeansEstimator(H2OEstimator):
-    algo = "kmeans"
-    supervised_learning = False
-    _defaults = KMEANS_DEFAULTS
-
-    def _fit(self, spec):
-        p = self._parms
-        di = DataInfo(spec.frame, spec.x, standardize=bool(p.get("standardize", True)), use_all_factor_levels=True,
-                      pad_to=0)
-        self._dinfo = di
-        X, ok = di.expand(spec.frame, dtype=torch.float32, pad=False)
-        X = X[ok]
-        w = spec.w_tensor()
-        w = None if w is None else w[ok]
-        gen = np.random.RandomState(_seed(p))
-        kmax = int(p.get("k", 1))
-        if p.get("estimate_k"):
-            best = None
-            prev = None
-            for k in range(1, kmax + 1):
-                C, assign, wss, it = self._lloyd(X, w, k, gen)
-                if prev is not None and (prev - wss) / max(prev, 1e-12) < 0.2 and k > 1:
-                    break
-                best = (C, assign, wss, it, k)
-                prev = wss
-            C, assign, wss, it, k = best
-        else:
-            C, assign, wss, it = self._lloyd(X, w, kmax, gen)
-        self._C_std = C
-        self._iterations = it
-        self._assign_train = assign
-        centers = C.cpu().numpy().astype(np.float64).copy()
-        if di.standardize:
-            base = di.n_cat_expanded
-            for j in range(len(di.num_cols)):
-                centers[:, base + j] = centers[:, base + j] * di.sigmas[j] + di.means[j]
-        self._output["centers"] = centers
-        self._output["centers_std"] = C.cpu().numpy()
-        self._output["coef_names"] = di.coef_names
-        self._output["model_summary"] = {"number_of_clusters": C.shape[0], "number_of_iterations": it}
-        self._train_X = X
-
-    def _dist(self, X, C):
-        return (X * X).sum(1, keepdim=True) - 2 * X @ C.T + (C * C).sum(1).view(1, -1)
-
-    def _init_centers(self, X, w, k, gen):
-        p = self._parms
-        init = (p.get("init") or "Furthest").lower()
-        n = X.shape[0]
-        up = p.get("user_points")
-        if up is not None:
-            U, _ = self._dinfo.expand(up, pad=False)
-            return U[:k].to(X.dtype)
-        Xg = coll.all_gather_var(X) if cloud.is_distributed() else X
-        ng = Xg.shape[0]
-        first = int(gen.randint(ng))
-        if init == "random":
-            idx = gen.choice(ng, size=min(k, ng), replace=False)
-            return Xg[torch.as_tensor(idx, device=X.device)].clone()
-        C = [Xg[first]]
-        d2 = ((Xg - C[0]) ** 2).sum(1)
-        for _ in range(1, k):
-            if init == "plusplus":
-                pr = (d2 / d2.sum()).double().cpu().numpy()
-                pr = pr / pr.sum()
-                i = int(gen.choice(ng, p=pr))
-            else:  # Furthest
-                i = int(torch.argmax(d2))
-            C.append(Xg[i])
-            d2 = torch.minimum(d2, ((Xg - Xg[i]) ** 2).sum(1))
-        return torch.stack(C)
-
-    def _lloyd(self, X, w, k, gen):
-        p = self._parms
-        C = self._init_centers(X, w, k, gen).to(X.dtype)
-        k = C.shape[0]
-        maxit = int(p.get("max_iterations", 10))
-        it = 0
-        ww = torch.ones(X.shape[0], dtype=X.dtype, device=X.device) if w is None else w.to(X.dtype)
-        assign = None
-        for it in range(1, maxit + 1):
-            D = self._dist(X, C)
-            assign = torch.argmin(D, 1)
-            A = torch.zeros((X.shape[0], k), dtype=X.dtype, device=X.device)
-            A.scatter_(1, assign.view(-1, 1), ww.view(-1, 1))
-            S = A.T @ X                     # centroid sums on the matrix cores
-            cnt = A.sum(0)
-            st = torch.cat([S.reshape(-1), cnt])
-            coll.allreduce_(st)
-            S, cnt = st[: k * X.shape[1]].view(k, -1), st[k * X.shape[1]:]
-            newC = torch.where(cnt.view(-1, 1) > 0, S / cnt.clamp_min(1e-30).view(-1, 1), C)
-            shift = float((newC - C).abs().max())
-            C = newC
-            if shift < 1e-6:
-                break
-        D = self._dist(X, C)
-        assign = torch.argmin(D, 1)
-        wss = coll.allreduce_scalar(float((D.gather(1, assign.view(-1, 1)).clamp_min(0).view(-1) * ww).sum()))
-        return C, assign, wss, it
-
-    def _predict_raw(self, frame):
-        X, _ = self._dinfo.expand(frame, pad=False)
-        D = self._dist(X.to(self._C_std.dtype), self._C_std)
-        return torch.argmin(D, 1).view(-1, 1).to(torch.float32)
-
-    def predict(self, test_data, **kw):
-        a = self._predict_raw(test_data)[:, 0]
-        return H2OFrame.from_vecs([Vec(a.contiguous(), T_INT)], ["predict"])
-
-    def _score_unsupervised(self, spec):
-        X = self._train_X
-        m = mm.clustering_metrics(X, self._C_std, self._assign_train)
-        self._training_metrics = m
-        if spec.valid is not None:
-            self._validation_metrics = self._unsupervised_perf(spec.valid)
-
-    def _unsupervised_perf(self, frame):
-        X, ok = self._dinfo.expand(frame, pad=False)
-        X = X[ok]
-        a = torch.argmin(self._dist(X, self._C_std), 1)
-        return mm.clustering_metrics(X, self._C_std, a)
-
-    def centers(self):
-        return self._output["centers"].tolist()
-
-    def centers_std(self):
-        return self._output["centers_std"].tolist()
-
-    def size(self, train=False, valid=False):
-        return self._training_metrics.get("size")
-
-    def tot_withinss(self, train=False, valid=False, xval=False):
-        return self._training_metrics.tot_withinss()
-
-    def betweenss(self, train=False, valid=False, xval=False):
-        return self._training_metrics.betweenss()
-
-    def totss(self, train=False, valid=False, xval=False):
-        return self._training_metrics.totss()
-
-    def withinss(self, train=False, valid=False, xval=False):
-        return self._training_metrics.withinss()
-
-    def num_iterations(self):
-        return self._iterations
+from .kmeans import KMEANS_DEFAULTS, H2OKMeansEstimator  # noqa: E402,F401  (fused HIP Lloyd pass)
 
 
 # ====================================================================== PCA / SVD

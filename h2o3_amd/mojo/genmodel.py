@@ -299,6 +299,9 @@ class MojoModel:
             return self._glrm_reconstruct(df)
         if a == "kmeans":
             X = self._expand(df)
+            nc = sum(len(d) if self.meta["di"]["use_all"] else len(d) - 1
+                     for d in (self.meta["di"]["domains"][c] for c in self.meta["di"]["cat_cols"]))
+            X[:, :nc] *= float(m.get("cat_scale", 1.0))
             C = self._arr["centers_std"]
             d = ((X[:, None, :] - C[None]) ** 2).sum(2)
             return d.argmin(1).reshape(-1, 1).astype(float)

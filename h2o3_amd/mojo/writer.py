@@ -173,7 +173,9 @@ def build_mojo(model) -> bytes:
         w.add_array("Y", model._Y.detach().cpu().numpy().astype(np.float64))
     elif algo == "kmeans":
         _dinfo_meta(w, model._dinfo)
-        w.add_array("centers_std", model._C_std.cpu().numpy())
+        # clustering space: one-hot categoricals at cat_scale (mismatch distance 1)
+        w.meta["cat_scale"] = float(getattr(model, "_cat_scale", 1.0))
+        w.add_array("centers_std", model._C_std[:, :model._dinfo.P].cpu().numpy())
     elif algo in ("pca",):
         _dinfo_meta(w, model._dinfo)
         w.add_array("evecs", model._evecs.cpu().numpy())

@@ -1,0 +1,149 @@
+"""K-Means Lloyd pass entry point: the fused HIP kernel (ops/csrc/kmeans.hip)
+on the GPU, an equivalent torch path on the CPU.
+
+`lloyd_pass(X, C, ...)` assigns every row of X [N, P] to its closest center
+of C [k, P] (squared euclidean, ties to the lowest index) and, with
+``accumulate=True``, returns the per-cluster statistics of the pass in f64:
+column sums, weights, within-cluster SS (distances to the *input* centers,
+like the reference LloydsIterationTask's _cSqr) and the number of rows
+whose assignment changed.  Reference: hex/kmeans/KMeans.java:731
+(LloydsIterationTask.map).
+"""
+from __future__ import annotations
+
+import ctypes
+import torch
+
+from . import _native
+
+_cv, _ci, _cll = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong
+
+
+def _lib():
+    lib = _native.get_lib("kmeans")
+    if lib is not None and not getattr(lib, "_typed", False):
+        lib.h2o_kmeans_lloyd.argtypes = [_cv, _cv, _cll, _ci, _cv, _cv, _ci, _cv, _cv, _cv, _cv, _ci, _ci, _cv]
+        lib.h2o_kmeans_reduce.argtypes = [_cv, _ci, _cll, _cv, _cv]
+        lib.h2o_kmeans_max_k.argtypes = [_ci, _ci]
+        lib.h2o_kmeans_part_stride.argtypes = [_ci, _ci]
+        lib.h2o_kmeans_part_stride.restype = _cll
+        lib.h2o_kmeans_resident_per_cu.argtypes = [_ci, _ci, _ci]
+        lib._typed = True
+    return lib
+
+
+_CU = {}
+
+
+def _cu_count(dev):
+    if dev not in _CU:
+        _CU[dev] = torch.cuda.get_device_properties(dev).multi_processor_count
+    return _CU[dev]
+
+
+def _ptr(t):
+    return _cv(0 if t is None else t.data_ptr())
+
+
+class LloydStats:
+    """Per-cluster statistics of one pass, packed in ONE f64 vector
+    [k*P sums | k weights | k withinss | changed] so a multi-GPU reduce is
+    a single all-reduce of `vec`."""
+
+    def __init__(self, vec, k, P):
+        self.vec, self.k, self.P = vec, k, P
+
+    @property
+    def sums(self):
+        return self.vec[:self.k * self.P].view(self.k, self.P)
+
+    @property
+    def weights(self):
+        return self.vec[self.k * self.P:self.k * self.P + self.k]
+
+    @property
+    def withinss(self):
+        return self.vec[self.k * self.P + self.k:self.k * self.P + 2 * self.k]
+
+    @property
+    def changed(self):
+        return float(self.vec[-1])
+
+
+def native_ok(X, k, accumulate=True):
+    """The fused kernel takes f32 row-major X with P % 4 == 0, P <= 256 and
+    k up to an LDS-dependent bound (h2o_kmeans_max_k)."""
+    if X.device.type != "cuda" or X.dtype != torch.float32 or X.dim() != 2:
+        return False
+    P = X.shape[1]
+    lib = _lib()
+    return lib is not None and 0 < k <= int(lib.h2o_kmeans_max_k(P, 1 if accumulate else 0))
+
+
+def lloyd_pass(X, C, w=None, assign=None, accumulate=True, dmin=None, use_native=None, n_groups=None):
+    """One pass over X.  assign: int32 [N] buffer, read as the previous
+    assignment (changed count) and overwritten with the new one (may be
+    None).  dmin: f32 [N] buffer for per-row squared distances to the
+    closest center (may be None).  Returns LloydStats (accumulate=True) or
+    None."""
+    N, P = X.shape
+    k = C.shape[0]
+    native = native_ok(X, k, accumulate) if use_native is None else use_native
+    C32 = C.to(device=X.device, dtype=torch.float32).contiguous()
+    if not native:
+        return _lloyd_torch(X, C32, w, assign, accumulate, dmin)
+    lib = _lib()
+    cn = (C.to(torch.float64) ** 2).sum(1).to(device=X.device, dtype=torch.float32).contiguous()
+    X = X.contiguous()
+    wt = None if w is None else w.to(device=X.device, dtype=torch.float32).contiguous()
+    if n_groups is None:
+        # persistent grid = exactly the resident workgroups (no tail wave)
+        ntiles = (N + 63) // 64
+        per_cu = int(lib.h2o_kmeans_resident_per_cu(k, P, 1 if accumulate else 0))
+        n_groups = max(1, min(ntiles, max(per_cu, 1) * _cu_count(X.device)))
+    part = None
+    stride = int(lib.h2o_kmeans_part_stride(k, P))
+    if accumulate:
+        part = torch.empty((n_groups, stride), dtype=torch.float32, device=X.device)
+    stream = _cv(torch.cuda.current_stream().cuda_stream)
+    rc = lib.h2o_kmeans_lloyd(_ptr(X), _ptr(wt), N, P, _ptr(C32), _ptr(cn), k, _ptr(assign), _ptr(assign), _ptr(dmin),
+                              _ptr(part), n_groups, 1 if accumulate else 0, stream)
+    if rc != 0:
+        raise RuntimeError(f"h2o_kmeans_lloyd failed: {rc}")
+    if not accumulate:
+        return None
+    out = torch.empty(stride, dtype=torch.float64, device=X.device)
+    rc = lib.h2o_kmeans_reduce(_ptr(part), n_groups, stride, _ptr(out), stream)
+    if rc != 0:
+        raise RuntimeError(f"h2o_kmeans_reduce failed: {rc}")
+    return LloydStats(out, k, P)
+
+
+def _lloyd_torch(X, C, w, assign, accumulate, dmin, chunk=1 << 20):
+    """Reference path (CPU / unsupported shapes): same outputs, f64 sums."""
+    N, P = X.shape
+    k = C.shape[0]
+    dev = X.device
+    cn = (C.to(torch.float64) ** 2).sum(1).to(torch.float32)
+    out = torch.zeros(k * P + 2 * k + 1, dtype=torch.float64, device=dev)
+    st = LloydStats(out, k, P)
+    sums, wsum, wss = st.sums, st.weights, st.withinss
+    for a in range(0, N, chunk):
+        Xc = X[a:a + chunk].to(torch.float32)
+        d = cn.view(1, -1) - 2.0 * (Xc @ C.T)
+        best, idx = d.min(1)
+        d2 = ((Xc.to(torch.float64) ** 2).sum(1) + best.to(torch.float64)).clamp_min(0)
+        idx32 = idx.to(torch.int32)
+        if assign is not None:
+            if accumulate:
+                out[-1] += (assign[a:a + chunk] != idx32).sum().to(torch.float64)
+            assign[a:a + chunk] = idx32
+        if dmin is not None:
+            dmin[a:a + chunk] = d2.to(dmin.dtype)
+        if accumulate:
+            wc = torch.ones(Xc.shape[0], dtype=torch.float64, device=dev) if w is None else \
+                w[a:a + chunk].to(torch.float64)
+            sums.index_add_(0, idx, Xc.to(torch.float64) * wc.view(-1, 1))
+            wsum.index_add_(0, idx, wc)
+            wss.index_add_(0, idx, wc * d2)
+    return st if accumulate else None

@@ -1,0 +1,396 @@
+// Fused K-Means Lloyd pass: distances on the f32 matrix cores, per-row
+// arg-min, per-cluster sums / weights / within-SS, assignment changes — one
+// read of X per iteration.
+//
+// Reference: hex/kmeans/KMeans.java (Lloyds MRTask: per row the closest
+// center by squared distance, then per-cluster column sums, row counts and
+// within-cluster SS reduced across the cloud; IterationTask / TotSS), all
+// in double on the CPU.
+//
+// MI355X design: X is a dense row-major f32 [N, P] in HBM.  A persistent
+// workgroup of 4 waves walks 64-row tiles (grid-stride, XCD-aware order):
+//   1. the tile (64 contiguous rows = one contiguous span of X) is loaded
+//      with coalesced dwordx4 loads one tile ahead in registers (with the
+//      rows' weights / old assignments: the loop body issues no other global
+//      load, so no vmcnt wait ever drains the prefetch) and stored to LDS
+//      (row stride P16+4 dwords, P16 = P rounded up to 16, zero tail);
+//   2. every wave owns 16 rows and computes their dot products with all
+//      centers with v_mfma_f32_16x16x4_f32 (exact f32 products) — lane group
+//      g = lane>>4 takes the k-range [g*P16/4, (g+1)*P16/4), so A (rows) and B
+//      (centers, resident in LDS for the whole pass) are read as float4;
+//   3. d = |c|^2 - 2 x.c, arg-min over the 16 lanes that share a row (xor
+//      shuffles, lowest index wins ties like torch.argmin);
+//   4. per-cluster sums in LDS: thread (row group, column) owns one column
+//      of a private [k, P] copy, reads four rows' sums in one round trip,
+//      merges rows of the same cluster in registers and writes each sum
+//      back once — no atomics (a returnless ds_add_f32 per (row, column)
+//      measured 5x slower than the rest of the pass; one-hot MFMA and
+//      per-center register selects were 2-3x slower than this); weights
+//      and within-SS (|x|^2 + d_min) per cluster by LDS atomics (2 per row).
+// Each workgroup writes one f32 partial; h2o_kmeans_reduce folds the
+// partials in f64.  No global atomics.
+#include "common.h"
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define KM_ROWS 64
+#define KM_THREADS 256
+
+// partial layout per workgroup: [k*P sums][k weights][k withinss][1 changed]
+__host__ __device__ inline long long km_part_stride(int k, int P) { return (long long)k * P + 2LL * k + 1; }
+
+template <int KT, int MAXV, bool ACC>
+__global__ __launch_bounds__(KM_THREADS) void kmeans_lloyd_kernel(
+    const float* __restrict__ X, const float* __restrict__ w, long long N, int P, const float* __restrict__ Cin,
+    const float* __restrict__ cn, int k, int* assign, const int* assign_old,
+    float* __restrict__ dmin_out, float* __restrict__ part, int vrg_in, int dbg) {
+  extern __shared__ __align__(16) float lds[];
+  const int P16 = (P + 15) & ~15;            // k-range padded so each lane group gets a float4 multiple
+  const int S = P16 + 4;                     // LDS row stride (dwords)
+  const int nq = (k + 15) >> 4;              // 16-center chunks in use (<= KT)
+  const int KP = nq * 16;                    // centers padded to the MFMA tile
+  float* Xs = lds;                           // [64][S]
+  float* Cs = Xs + KM_ROWS * S;              // [KP][S]
+  float* cns = Cs + KP * S;                  // [KP]
+  // per-cluster sums: vrg private copies [vrg][k][P]; thread (vh, vc) owns
+  // column vc of copy vh, so the read-modify-writes need no atomics
+  const int vpr = P <= 64 ? 64 : (P <= 128 ? 128 : 256);
+  const int vrg = vrg_in;
+  const int vc = (int)threadIdx.x % vpr, vh = (int)threadIdx.x / vpr;
+  float* Ssum = cns + KP;                    // [vrg][k][P] (ACC)
+  float* Swt = Ssum + (ACC ? vrg * k * P : 0);  // [k]
+  float* Sss = Swt + (ACC ? k : 0);          // [k]
+  float* xsq = Sss + (ACC ? k : 0);          // [64]
+  float* dmn = xsq + KM_ROWS;                // [64]
+  int* asg = (int*)(dmn + KM_ROWS);          // [64]
+  float* wts = (float*)(asg + KM_ROWS);      // [64] row weights of the tile
+  __shared__ int changed_s;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wv = tid >> 6;
+  const int g = lane >> 4;                   // k-group of this lane
+  const int li = lane & 15;
+  const int Pq = P16 >> 2;                   // k-range per lane group (multiple of 4)
+
+  // centers -> LDS (padded rows: zeros, |c|^2 = +inf never wins)
+  for (int e = tid; e < KP * S; e += KM_THREADS) {
+    const int j = e / S, c = e - j * S;
+    Cs[e] = (j < k && c < P) ? Cin[(long long)j * P + c] : 0.f;
+  }
+  for (int j = tid; j < KP; j += KM_THREADS) cns[j] = j < k ? cn[j] : INFINITY;
+  if (ACC) {
+    for (int e = tid; e < vrg * k * P + 2 * k; e += KM_THREADS) Ssum[e] = 0.f;   // Ssum, Swt, Sss contiguous
+  }
+  if (tid == 0) changed_s = 0;
+  // X tile columns P..P16 stay zero (the staging below writes only c < P)
+  for (int e = tid; e < KM_ROWS * S; e += KM_THREADS) Xs[e] = 0.f;
+
+  const long long ntiles = (N + KM_ROWS - 1) / KM_ROWS;
+  const int G = gridDim.x;
+  const int bid = xcd_remap(blockIdx.x, G);
+  // each thread moves up to MAXV float4 of a tile; their LDS offsets are the
+  // same for every tile (computed once: no divisions in the loop)
+  const int nv4 = (KM_ROWS * P) >> 2;
+  int xo[MAXV];
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int v = tid + i * KM_THREADS;
+    const int e = v * 4;
+    const int r = e / P;                     // P % 4 == 0: a float4 never straddles rows
+    xo[i] = v < nv4 ? r * S + (e - r * P) : -1;
+  }
+  // prefetch set of a tile: its X floats + (threads < 64) row weight and old assignment
+  f32x4 pre[MAXV];
+  float pre_w = 1.f;
+  int pre_a = -1;
+  auto load_tile = [&](long long t) {
+    const long long r0 = t * KM_ROWS;
+    const long long lim = (N - r0) * P;      // valid floats in this tile
+    const f32x4* src = (const f32x4*)(X + r0 * P);
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+      const int v = tid + i * KM_THREADS;
+      f32x4 q = {0.f, 0.f, 0.f, 0.f};
+      if (!(dbg & 8) && xo[i] >= 0 && 4LL * v < lim) q = src[v];
+      pre[i] = q;
+    }
+    if (tid < KM_ROWS && r0 + tid < N) {
+      if (ACC && w) pre_w = w[r0 + tid];
+      if (ACC && assign_old) pre_a = assign_old[r0 + tid];
+    }
+  };
+  // per-row results of the previous tile, stored just before the next prefetch
+  long long out_r = -1;
+  int out_a = 0;
+  float out_d = 0.f;
+
+  long long t = bid;
+  if (t < ntiles) load_tile(t);
+  __syncthreads();
+
+  for (; t < ntiles; t += G) {
+    const long long r0 = t * KM_ROWS;
+    // registers -> LDS (row-strided) + the rows' scalars
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i)
+      if (!(dbg & 16) && xo[i] >= 0) *(f32x4*)(Xs + xo[i]) = pre[i];
+    int cur_a = pre_a;
+    if (tid < KM_ROWS) wts[tid] = r0 + tid < N ? pre_w : 0.f;   // tail rows weigh nothing
+    __syncthreads();
+    if (t + G < ntiles) load_tile(t + G);    // next tile in flight during the math
+    // previous tile's row outputs: issued right behind the prefetch, they
+    // drain during this tile's math (the next top-of-loop wait covers both)
+    if (out_r >= 0) {
+      if (assign) assign[out_r] = out_a;
+      if (dmin_out) dmin_out[out_r] = out_d;
+      out_r = -1;
+    }
+
+    // ---- distances: wave wv owns rows 16*wv .. 16*wv+15
+    f32x4 acc[KT];
+#pragma unroll
+    for (int q = 0; q < KT; ++q) acc[q] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const float* xa = Xs + (16 * wv + li) * S + g * Pq;
+    const float* cb = Cs + li * S + g * Pq;
+    float sq = 0.f;
+    for (int s = 0; s < ((dbg & 1) ? 0 : Pq); s += 4) {
+      const f32x4 a4 = *(const f32x4*)(xa + s);
+      sq += a4[0] * a4[0] + a4[1] * a4[1] + a4[2] * a4[2] + a4[3] * a4[3];
+#pragma unroll
+      for (int q = 0; q < KT; ++q) {
+        if (q < nq) {
+          const f32x4 b4 = *(const f32x4*)(cb + q * 16 * S + s);
+          acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[0], b4[0], acc[q], 0, 0, 0);
+          acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[1], b4[1], acc[q], 0, 0, 0);
+          acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[2], b4[2], acc[q], 0, 0, 0);
+          acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[3], b4[3], acc[q], 0, 0, 0);
+        }
+      }
+    }
+    // |x|^2 of row li: sum over the 4 lane groups
+    sq += __shfl_xor(sq, 16, 64);
+    sq += __shfl_xor(sq, 32, 64);
+    if (g == 0) xsq[16 * wv + li] = sq;
+    // arg-min: lane holds rows 4g+r (r = reg), center q*16+li
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float best = INFINITY;
+      int bi = 0x7fffffff;
+#pragma unroll
+      for (int q = 0; q < KT; ++q) {
+        const int j = q * 16 + li;
+        const float d = q < nq ? cns[j] - 2.f * acc[q][r] : INFINITY;
+        if (d < best) { best = d; bi = j; }
+      }
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        const float ob = __shfl_xor(best, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        if (ob < best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+      }
+      if (li == 0) {
+        const int row = 16 * wv + 4 * g + r;
+        dmn[row] = best;
+        asg[row] = bi < k ? bi : 0;
+      }
+    }
+    __syncthreads();
+    // ---- per-row results + per-cluster weights / within-SS
+    if (!(dbg & 4) && tid < KM_ROWS && r0 + tid < N) {
+      const int a = asg[tid];
+      const float d2 = fmaxf(xsq[tid] + dmn[tid], 0.f);
+      if (ACC && assign_old && cur_a != a) atomicAdd(&changed_s, 1);
+      out_r = r0 + tid;
+      out_a = a;
+      out_d = d2;
+      if (ACC) {
+        const float wr = wts[tid];
+        if (wr != 0.f) {
+          lds_add(Swt + a, wr);
+          lds_add(Sss + a, wr * d2);
+        }
+      }
+    }
+    if (ACC && !(dbg & 2) && vh < vrg && vc < P) {
+      // ---- per-cluster sums: thread (vh, vc) walks rows vh, vh+vrg, ... four
+      // at a time: the four sums are read first (one LDS round trip), rows
+      // of the same cluster are merged in registers, each distinct cluster
+      // written back once.  No atomics: a returnless ds_add_f32 per
+      // (row, column) measured 5x slower than the rest of the pass.
+      float* Sv = Ssum + vh * k * P + vc;
+      for (int r = vh; r < KM_ROWS; r += 4 * vrg) {
+        int a[4];
+        float x[4], v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int rr = r + u * vrg;
+          const bool ok = rr < KM_ROWS;
+          a[u] = ok ? asg[rr] : asg[r];
+          x[u] = ok ? wts[rr] * Xs[rr * S + vc] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = Sv[a[u] * P];
+#pragma unroll
+        for (int u = 1; u < 4; ++u) {
+          // fold row u into the first earlier row of the same cluster
+          if (a[u] == a[0]) { x[0] += x[u]; a[u] = -1; }
+          else if (u > 1 && a[u] == a[1]) { x[1] += x[u]; a[u] = -1; }
+          else if (u > 2 && a[u] == a[2]) { x[2] += x[u]; a[u] = -1; }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (a[u] >= 0) Sv[a[u] * P] = v[u] + x[u];
+      }
+    }
+    __syncthreads();
+  }
+  if (out_r >= 0) {
+    if (assign) assign[out_r] = out_a;
+    if (dmin_out) dmin_out[out_r] = out_d;
+  }
+  if (ACC) {
+    float* o = part + (long long)blockIdx.x * km_part_stride(k, P);
+    for (int e = tid; e < k * P; e += KM_THREADS) {
+      float sv = 0.f;
+      for (int h = 0; h < vrg; ++h) sv += Ssum[h * k * P + e];
+      o[e] = sv;
+    }
+    for (int e = tid; e < 2 * k; e += KM_THREADS) o[k * P + e] = Swt[e];   // Swt, Sss contiguous
+    if (tid == 0) o[k * P + 2 * k] = (float)changed_s;
+  }
+}
+
+// out[e] = sum_g part[g][e] in f64 (e over the whole partial record)
+__global__ __launch_bounds__(256) void kmeans_reduce_kernel(const float* __restrict__ part, int G, long long stride,
+                                                            double* __restrict__ out) {
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= stride) return;
+  double s = 0.0;
+  for (int gi = 0; gi < G; ++gi) s += (double)part[(long long)gi * stride + e];
+  out[e] = s;
+}
+
+static int km_kt(int k) {   // the template instance a given k runs on
+  const int kt = (k + 15) / 16;
+  return kt <= 1 ? 1 : kt <= 2 ? 2 : kt <= 4 ? 4 : kt <= 8 ? 8 : 16;
+}
+
+static size_t km_lds_bytes(int KT, int k, int P, bool acc, int vrg) {
+  (void)KT;
+  const int P16 = (P + 15) & ~15, S = P16 + 4, KP = ((k + 15) / 16) * 16;
+  size_t f = (size_t)KM_ROWS * S + (size_t)KP * S + KP + (acc ? (size_t)vrg * k * P + 2 * k : 0) + 4 * KM_ROWS;
+  return f * 4;
+}
+
+// private sum copies per workgroup: every thread busy (256 / vpr row groups)
+// when the LDS allows, else fewer
+static int km_vrg(int k, int P, bool acc) {
+  const int vpr = P <= 64 ? 64 : (P <= 128 ? 128 : 256);
+  int vrg = KM_THREADS / vpr;
+  while (vrg > 1 && km_lds_bytes(0, k, P, acc, vrg) > 96 * 1024) vrg >>= 1;
+  return vrg;
+}
+
+static int g_km_dbg = 0;   // microbenchmark phase-skip flags (h2o_kmeans_set_debug); 0 in production
+
+template <int KT, int MAXV, bool ACC>
+static int km_launch2(const float* X, const float* w, long long N, int P, const float* C, const float* cn, int k,
+                      int* assign, const int* assign_old, float* dmin, float* part, int G, hipStream_t s) {
+  const int vrg = km_vrg(k, P, ACC);
+  const size_t lds = km_lds_bytes(KT, k, P, ACC, vrg);
+  auto kern = kmeans_lloyd_kernel<KT, MAXV, ACC>;
+  hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(kern, dim3(G), dim3(KM_THREADS), lds, s, X, w, N, P, C, cn, k, assign, assign_old, dmin, part,
+                     vrg, g_km_dbg);
+  H2O_CHECK_LAUNCH();
+}
+
+template <int KT>
+static int km_launch(const float* X, const float* w, long long N, int P, const float* C, const float* cn, int k,
+                     int* assign, const int* assign_old, float* dmin, float* part, int G, int acc, hipStream_t s) {
+  // MAXV = float4 per thread per 64-row tile = ceil(P / 16)
+  if (P <= 64) return acc ? km_launch2<KT, 4, true>(X, w, N, P, C, cn, k, assign, assign_old, dmin, part, G, s)
+                          : km_launch2<KT, 4, false>(X, w, N, P, C, cn, k, assign, assign_old, dmin, part, G, s);
+  if (P <= 128) return acc ? km_launch2<KT, 8, true>(X, w, N, P, C, cn, k, assign, assign_old, dmin, part, G, s)
+                           : km_launch2<KT, 8, false>(X, w, N, P, C, cn, k, assign, assign_old, dmin, part, G, s);
+  return acc ? km_launch2<KT, 16, true>(X, w, N, P, C, cn, k, assign, assign_old, dmin, part, G, s)
+             : km_launch2<KT, 16, false>(X, w, N, P, C, cn, k, assign, assign_old, dmin, part, G, s);
+}
+
+template <int KT, int MAXV, bool ACC>
+static int km_resident2(int k, int P) {
+  int per_cu = 0;
+  const size_t lds = km_lds_bytes(KT, k, P, ACC, km_vrg(k, P, ACC));
+  auto kern = kmeans_lloyd_kernel<KT, MAXV, ACC>;
+  if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, KM_THREADS, lds) != hipSuccess) return 0;
+  return per_cu;
+}
+
+template <int KT>
+static int km_resident(int k, int P, int acc) {
+  if (P <= 64) return acc ? km_resident2<KT, 4, true>(k, P) : km_resident2<KT, 4, false>(k, P);
+  if (P <= 128) return acc ? km_resident2<KT, 8, true>(k, P) : km_resident2<KT, 8, false>(k, P);
+  return acc ? km_resident2<KT, 16, true>(k, P) : km_resident2<KT, 16, false>(k, P);
+}
+
+extern "C" {
+
+// Largest k the fused kernel takes for a given P (LDS limit); 0 = unsupported P.
+int h2o_kmeans_max_k(int P, int acc) {
+  if (P <= 0 || P > 256 || (P & 3)) return 0;
+  int best = 0;
+  for (int k = 16; k <= 256; k += 16) {
+    if (km_lds_bytes(km_kt(k), k, P, acc != 0, km_vrg(k, P, acc != 0)) <= 160 * 1024) best = k;
+  }
+  return best;
+}
+
+long long h2o_kmeans_part_stride(int k, int P) { return km_part_stride(k, P); }
+
+// Phase-skip flags for scripts/kmeans_mb.py (1 MFMA, 2 sums, 4 row stats,
+// 8 global loads, 16 LDS staging).  Results are wrong with any flag set.
+void h2o_kmeans_set_debug(int flags) { g_km_dbg = flags; }
+
+// Workgroups of the Lloyd kernel resident per CU for (k, P, acc): the
+// persistent grid is sized to exactly fill the chip (no tail of late
+// workgroups walking a full share of tiles alone).
+int h2o_kmeans_resident_per_cu(int k, int P, int acc) {
+  if (P <= 0 || P > 256 || (P & 3) || k <= 0 || k > 256) return 0;
+  const int kt = km_kt(k);
+  if (kt <= 1) return km_resident<1>(k, P, acc);
+  if (kt <= 2) return km_resident<2>(k, P, acc);
+  if (kt <= 4) return km_resident<4>(k, P, acc);
+  if (kt <= 8) return km_resident<8>(k, P, acc);
+  return km_resident<16>(k, P, acc);
+}
+
+// One Lloyd pass.  X [N, P] f32 row-major (P % 4 == 0, P <= 256), C [k, P]
+// f32, cn [k] = |c|^2.  acc=1: per-workgroup partials into part
+// [G, km_part_stride] (then h2o_kmeans_reduce); acc=0: assignment only.
+// assign / assign_old / dmin / w may be null.  Returns a hipError_t.
+int h2o_kmeans_lloyd(const float* X, const float* w, long long N, int P, const float* C, const float* cn, int k,
+                     int* assign, const int* assign_old, float* dmin, float* part, int G, int acc, hipStream_t s) {
+  if (N <= 0) return 0;
+  if (P <= 0 || P > 256 || (P & 3) || k <= 0 || k > 256 || G <= 0) return (int)hipErrorInvalidValue;
+  const int kt = km_kt(k);
+  if (km_lds_bytes(kt, k, P, acc != 0, km_vrg(k, P, acc != 0)) > 160 * 1024) return (int)hipErrorInvalidValue;
+  if (acc && !part) return (int)hipErrorInvalidValue;
+  if (kt <= 1) return km_launch<1>(X, w, N, P, C, cn, k, assign, assign_old, dmin, part, G, acc, s);
+  if (kt <= 2) return km_launch<2>(X, w, N, P, C, cn, k, assign, assign_old, dmin, part, G, acc, s);
+  if (kt <= 4) return km_launch<4>(X, w, N, P, C, cn, k, assign, assign_old, dmin, part, G, acc, s);
+  if (kt <= 8) return km_launch<8>(X, w, N, P, C, cn, k, assign, assign_old, dmin, part, G, acc, s);
+  return km_launch<16>(X, w, N, P, C, cn, k, assign, assign_old, dmin, part, G, acc, s);
+}
+
+int h2o_kmeans_reduce(const float* part, int G, long long stride, double* out, hipStream_t s) {
+  if (G <= 0 || stride <= 0) return 0;
+  const long long nb = (stride + 255) / 256;
+  hipLaunchKernelGGL(kmeans_reduce_kernel, dim3((unsigned)nb), dim3(256), 0, s, part, G, stride, out);
+  H2O_CHECK_LAUNCH();
+}
+
+}  // extern "C"

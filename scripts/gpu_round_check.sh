@@ -1,3 +1,4 @@
+# GPU tests + smoke + GBM/GLM default benches (one gpurun call).
 set -e
 export TMPDIR=/tmp
 mkdir -p gpurun_out
@@ -7,3 +8,5 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 tail -n 2 gpurun_out/smoke.log
 timeout -k 10 400 python bench.py > gpurun_out/bench_default.log 2>&1
 tail -1 gpurun_out/bench_default.log | cut -c1-400
+timeout -k 10 400 python bench.py --algo glm > gpurun_out/bench_glm.log 2>&1
+tail -1 gpurun_out/bench_glm.log | cut -c1-400
