@@ -1,35 +1,56 @@
 """Deep Learning (multi-layer perceptron, autoencoder).
 
 Reference: hex/deeplearning/DeepLearning.java, DeepLearningModel.java,
-Neurons.java (Tanh / Rectifier / Maxout / ExpRectifier (+WithDropout)),
-Dropout.java, DeepLearningTask.java (Hogwild SGD per node, model averaging
-across nodes), ADADELTA adaptive rate (rho, epsilon), momentum schedule,
-L1/L2, input/hidden dropout, autoencoder with reconstruction error, Gedeon
-variable importance, deep features.
+DeepLearningModelInfo.java, Neurons.java (Tanh / Rectifier / Maxout /
+ExpRectifier, each +WithDropout; Softmax / Linear outputs), Dropout.java,
+DeepLearningTask.java.  Semantics kept from the reference:
+  * layer-wise UniformAdaptive / Uniform / Normal init, user initial weights
+    and biases, pretrained_autoencoder;
+  * ADADELTA per weight (rho, epsilon) with the bias rate driven by the
+    row's mean squared weight gradient (Neurons.update_bias), or plain SGD:
+    rate / (1 + rate_annealing * samples) * rate_decay^layer, momentum ramp
+    momentum_start -> momentum_stable over momentum_ramp samples, Nesterov;
+  * L1 / L2 on weights and biases, max_w2 per-neuron row rescale;
+  * unit dropout without rescaling while training, activations scaled by
+    (1 - ratio) at test time; input dropout;
+  * Softmax + CrossEntropy / Quadratic, Linear output with the
+    distribution's gradient (gaussian, poisson, gamma, tweedie, laplace,
+    quantile, huber), standardized regression response;
+  * autoencoder (reconstruction gradient, sparsity_beta / average_activation),
+    anomaly(), deepfeatures(), Gedeon variable importance;
+  * scoring every iteration (train_samples_per_iteration), early stopping
+    (stopping_rounds / metric / tolerance, classification_stop,
+    regression_stop), overwrite_with_best_model, max_runtime_secs,
+    checkpoint restart.
 
-MI355X design: the standardized / one-hot design matrix is one HBM tensor;
-training runs mini-batches (the reference's per-row Hogwild updates are a
-CPU-cache idiom) of bf16-capable GEMMs through torch on the GPU, the
-optimizer is ADADELTA with the reference's defaults; with several GPUs each
-rank trains on its row shard and gradients are averaged with a bucketed
-RCCL all-reduce every step (synchronous data parallel instead of the
-reference's periodic model averaging).
+MI355X design: the standardized design matrix is one HBM tensor; a training
+step is mini-batch data parallel: the dense products go to the library GEMM
+(hipBLASLt), every element-wise / per-neuron part is a hand-written HIP
+kernel (ops/csrc/dl.hip: fused bias + activation + hashed dropout forward,
+fused backward with bias-gradient column sums, one per-neuron-row update
+kernel doing gradient + L1/L2 + ADADELTA / momentum + max_w2 + bias update,
+softmax + output gradient).  The reference's per-row Hogwild updates are a
+CPU-cache idiom; here a mini-batch gradient (mini_batch_size, at least 32
+rows) is applied per step, and with several GPUs the gradients of every
+layer are averaged by one bucketed RCCL all-reduce per step (synchronous
+data parallel instead of the reference's periodic model averaging).
 """
 from __future__ import annotations
 
+import copy
 import math
 import time
 
 import numpy as np
 import torch
-import torch.nn as nn
 
 from ..core.frame import H2OFrame
 from ..core.vec import T_REAL, Vec
+from ..ops import dl_ops
 from ..parallel import cloud
 from ..parallel import collectives as coll
 from . import metrics as mm
-from .base import H2OEstimator
+from .base import H2OEstimator, ScoreKeeper, _LESS_IS_BETTER
 from .datainfo import DataInfo
 
 DL_DEFAULTS = dict(activation="Rectifier", hidden=[200, 200], epochs=10.0, train_samples_per_iteration=-2,
@@ -53,27 +74,27 @@ DL_DEFAULTS = dict(activation="Rectifier", hidden=[200, 200], epochs=10.0, train
                    class_sampling_factors=None, max_after_balance_size=5.0, max_confusion_matrix_size=20,
                    use_all_factor_levels=True, checkpoint=None, overwrite_with_best_model=True)
 
-
-class _Maxout(nn.Module):
-    def __init__(self, fin, fout, k=2):
-        super().__init__()
-        self.lin = nn.Linear(fin, fout * k)
-        self.k = k
-        self.fout = fout
-
-    def forward(self, x):
-        return self.lin(x).view(x.shape[0], self.fout, self.k).max(2).values
+_MIN_GPU_BATCH = 32
 
 
-def _act(name):
-    n = name.lower().replace("withdropout", "")
-    if n == "tanh":
-        return nn.Tanh()
-    if n == "rectifier":
-        return nn.ReLU()
-    if n == "exprectifier":
-        return nn.ELU()
-    return None
+def _act_name(activation):
+    a = (activation or "Rectifier").lower()
+    drop = a.endswith("withdropout")
+    base = a.replace("withdropout", "")
+    return {"tanh": "tanh", "rectifier": "rectifier", "maxout": "maxout", "exprectifier": "exprectifier"}[base], drop
+
+
+class _Layer:
+    """One dense layer: W [out*k, in] (k = 2 for maxout), b [out*k]."""
+
+    def __init__(self, fin, fout, act, drop, k=1):
+        self.fin, self.fout, self.act, self.drop, self.k = fin, fout, act, drop, k
+        self.W = None
+        self.b = None
+        self.state = {}
+
+    def state_dict(self):
+        return {"W": self.W.detach().cpu().clone(), "b": self.b.detach().cpu().clone()}
 
 
 class H2ODeepLearningEstimator(H2OEstimator):
@@ -85,51 +106,89 @@ class H2ODeepLearningEstimator(H2OEstimator):
         if self._parms.get("autoencoder"):
             self.supervised_learning = False
 
-    def _build_net(self, P, out_dim):
-        p = self._parms
-        hidden = list(p.get("hidden") or [200, 200])
-        act = p.get("activation", "Rectifier")
-        drop = "withdropout" in act.lower()
-        hdr = p.get("hidden_dropout_ratios") or ([0.5] * len(hidden) if drop else [0.0] * len(hidden))
-        layers = []
-        if float(p.get("input_dropout_ratio", 0) or 0) > 0:
-            layers.append(nn.Dropout(float(p["input_dropout_ratio"])))
-        fin = P
-        self._hidden_idx = []
-        for h, d in zip(hidden, hdr):
-            if act.lower().startswith("maxout"):
-                layers.append(_Maxout(fin, h))
-            else:
-                layers.append(nn.Linear(fin, h))
-                layers.append(_act(act))
-            self._hidden_idx.append(len(layers) - 1)
-            if d and d > 0:
-                layers.append(nn.Dropout(d))
-            fin = h
-        layers.append(nn.Linear(fin, out_dim))
-        net = nn.Sequential(*layers)
-        # UniformAdaptive init (reference Neurons: U(-sqrt(6/(fan_in+fan_out)), +))
-        g = torch.Generator().manual_seed(self._seed())
-        scale = float(p.get("initial_weight_scale", 1.0))
-        dist = (p.get("initial_weight_distribution") or "UniformAdaptive").lower()
-        for m in net.modules():
-            if isinstance(m, nn.Linear):
-                fi, fo = m.in_features, m.out_features
-                with torch.no_grad():
-                    if dist == "uniform":
-                        m.weight.uniform_(-scale, scale, generator=g)
-                    elif dist == "normal":
-                        m.weight.normal_(0, scale, generator=g)
-                    else:
-                        r = math.sqrt(6.0 / (fi + fo))
-                        m.weight.uniform_(-r, r, generator=g)
-                    m.bias.zero_()
-        return net.to(cloud.device())
-
     def _seed(self):
         s = self._parms.get("seed", -1)
         return 12345 if s is None or s == -1 else int(s) & 0x7FFFFFFF
 
+    # ------------------------------------------------------------------ network
+    def _build(self, P, out_dim, classification):
+        p = self._parms
+        hidden = list(p.get("hidden") or [200, 200])
+        act, with_drop = _act_name(p.get("activation"))
+        hdr = p.get("hidden_dropout_ratios")
+        if hdr is None:
+            hdr = [0.5] * len(hidden) if with_drop else [0.0] * len(hidden)
+        if len(hdr) != len(hidden):
+            raise ValueError("hidden_dropout_ratios must have one entry per hidden layer")
+        if not with_drop and any(h > 0 for h in hdr):
+            raise ValueError("hidden_dropout_ratios requires a *WithDropout activation")
+        layers, fin = [], P
+        for h, d in zip(hidden, hdr):
+            layers.append(_Layer(fin, h, act, float(d), 2 if act == "maxout" else 1))
+            fin = h
+        out_act = "softmax" if classification else "linear"
+        layers.append(_Layer(fin, out_dim, out_act, 0.0))
+        g = torch.Generator().manual_seed(self._seed())
+        dist = (p.get("initial_weight_distribution") or "UniformAdaptive").lower()
+        scale = float(p.get("initial_weight_scale", 1.0))
+        iw, ib = p.get("initial_weights"), p.get("initial_biases")
+        dev = cloud.device()
+        for li, L in enumerate(layers):
+            rows = L.fout * L.k
+            if dist == "uniform":
+                W = (torch.rand((rows, L.fin), generator=g) * 2 - 1) * scale
+            elif dist == "normal":
+                W = torch.randn((rows, L.fin), generator=g) * scale
+            else:   # UniformAdaptive (Neurons.randomize: +-sqrt(6 / (fan_in + fan_out)))
+                r = math.sqrt(6.0 / (L.fin + L.fout))
+                W = (torch.rand((rows, L.fin), generator=g) * 2 - 1) * r
+            b = torch.zeros(rows)
+            if iw is not None and li < len(iw) and iw[li] is not None:
+                W = self._frame_matrix(iw[li]).view(rows, L.fin)
+            if ib is not None and li < len(ib) and ib[li] is not None:
+                b = self._frame_matrix(ib[li]).view(rows)
+            L.W = W.to(dev, torch.float32).contiguous()
+            L.b = b.to(dev, torch.float32).contiguous()
+        pre = p.get("pretrained_autoencoder")
+        if pre is not None:
+            from ..core import dkv
+            ae = dkv.get(pre) if isinstance(pre, str) else pre
+            for L, A in zip(layers[:-1], ae._layers[:len(layers) - 1]):
+                if A.W.shape != L.W.shape:
+                    raise ValueError("pretrained_autoencoder hidden layers do not match this network")
+                L.W.copy_(A.W)
+                L.b.copy_(A.b)
+        return layers
+
+    @staticmethod
+    def _frame_matrix(fr):
+        from ..core import dkv
+        fr = dkv.get(fr) if isinstance(fr, str) else fr
+        cols = [fr.vec(c).as_float(torch.float32) for c in fr.names]
+        return torch.stack(cols, 1).cpu()
+
+    def _forward(self, X, train, seed=0, keep=None):
+        """Returns (activations list [A_0 = input, ...], pre-activations list,
+        output probabilities / values).  keep: (in_mask) for input dropout."""
+        p = self._parms
+        A = X
+        ratio_in = float(p.get("input_dropout_ratio") or 0.0)
+        if train and ratio_in > 0:
+            A = X * dl_ops.keep_mask(seed ^ 0x5bd1e995, X.shape[0], X.shape[1], ratio_in, X.device)
+        acts, zs = [A], []
+        for li, L in enumerate(self._layers[:-1]):
+            Z = A @ L.W.t()
+            Ah = dl_ops.fwd(Z, L.b, L.act, L.drop, seed=seed + 7919 * (li + 1), train=train,
+                            test_scale=1.0 - L.drop)
+            zs.append(Z)
+            acts.append(Ah)
+            A = Ah
+        Lo = self._layers[-1]
+        Zo = A @ Lo.W.t()
+        zs.append(Zo)
+        return acts, zs
+
+    # ------------------------------------------------------------------ fit
     def _fit(self, spec):
         p = self._parms
         torch.manual_seed(self._seed())
@@ -139,7 +198,12 @@ class H2ODeepLearningEstimator(H2OEstimator):
         self._dinfo = di
         X, ok = di.expand(spec.frame, pad=False)
         ae = bool(p.get("autoencoder"))
-        K = spec.nclasses if spec.is_classification else 1
+        self._ae = ae
+        K = spec.nclasses if (spec.is_classification and not ae) else 1
+        self._K = K
+        Y = None
+        from .distributions import get_distribution
+        dname = (p.get("distribution") or "auto")
         if not ae:
             y = spec.y_tensor()
             if spec.is_classification:
@@ -148,123 +212,277 @@ class H2ODeepLearningEstimator(H2OEstimator):
             else:
                 yf = y.to(torch.float32)
                 ok = ok & ~torch.isnan(yf)
-                # standardize regression targets (reference normalizes the response)
-                self._ymu = coll.allreduce_scalar(float(yf[ok].sum())) / max(coll.allreduce_scalar(float(ok.sum())), 1)
-                var = coll.allreduce_scalar(float(((yf[ok] - self._ymu) ** 2).sum())) / max(coll.allreduce_scalar(float(ok.sum())) - 1, 1)
+                n_ok = coll.allreduce_scalar(float(ok.sum()))
+                self._ymu = coll.allreduce_scalar(float(yf[ok].sum())) / max(n_ok, 1)
+                var = coll.allreduce_scalar(float(((yf[ok] - self._ymu) ** 2).sum())) / max(n_ok - 1, 1)
                 self._ysd = math.sqrt(var) if var > 0 else 1.0
+                if dname.lower() not in ("auto", "gaussian", "laplace", "quantile", "huber"):
+                    self._ymu, self._ysd = 0.0, 1.0   # log-link families train on the raw response
                 Y = ((yf - self._ymu) / self._ysd).view(-1, 1)
-        X = X[ok]
-        if not ae:
-            Y = Y[ok]
+        self._dist = get_distribution(dname if not spec.is_classification else "AUTO", max(K, 1),
+                                      tweedie_power=float(p.get("tweedie_power", 1.5)),
+                                      quantile_alpha=float(p.get("quantile_alpha", 0.5)),
+                                      huber_alpha=float(p.get("huber_alpha", 0.9)))
+        if not bool(ok.all()):
+            X = X[ok]
+            Y = Y[ok] if Y is not None else None
         w = spec.w_tensor()
-        w = None if w is None else w[ok]
+        w = None if w is None else w[ok].to(torch.float32)
         P = X.shape[1]
-        out_dim = P if ae else (K if K > 1 else 1)
-        if p.get("checkpoint") is not None:
+        out_dim = P if ae else K
+        ckpt = p.get("checkpoint")
+        if ckpt is not None:
             from ..core import dkv
-            prev = dkv.get(p["checkpoint"]) if isinstance(p["checkpoint"], str) else p["checkpoint"]
-            net = prev._net
+            prev = dkv.get(ckpt) if isinstance(ckpt, str) else ckpt
+            self._layers = copy.deepcopy(prev._layers)
+            self._processed = getattr(prev, "_processed", 0.0)
         else:
-            net = self._build_net(P, out_dim)
-        self._net = net
-        if bool(p.get("adaptive_rate", True)):
-            opt = torch.optim.Adadelta(net.parameters(), lr=1.0, rho=float(p["rho"]), eps=float(p["epsilon"]))
+            self._layers = self._build(P, out_dim, K > 1)
+            self._processed = 0.0
+        self._train_loop(spec, X, Y, w, ae, K)
+        self._output["model_summary"] = {
+            "layers": [P] + [L.fout for L in self._layers],
+            "activation": p.get("activation"), "epochs": self._epochs_done,
+            "units": [L.fout for L in self._layers],
+            "dropout": [float(p.get("input_dropout_ratio") or 0.0)] + [L.drop for L in self._layers[:-1]]}
+        if p.get("variable_importances", True) and not ae:
+            self._output["variable_importances"] = self._gedeon(di)
+
+    def _loss_name(self, K, ae):
+        loss = (self._parms.get("loss") or "Automatic").lower()
+        if loss == "automatic":
+            return "crossentropy" if K > 1 else "quadratic"
+        return loss
+
+    def _output_grad(self, Zo, yb, wb, inv_n, K, ae, xb):
+        """dE/dnet of the output layer (already / n) and the per-row loss."""
+        Lo = self._layers[-1]
+        if K > 1:
+            loss = self._loss_name(K, ae)
+            _, dZ, lo = dl_ops.softmax(Zo, Lo.b, yb, wb, inv_n, "quadratic" if loss == "quadratic" else "crossentropy")
+            return dZ, lo
+        Zo += Lo.b.view(1, -1)
+        t = xb if ae else yb
+        loss = self._loss_name(K, ae)
+        d = Zo - t
+        if loss == "absolute":
+            g, lo = torch.sign(d), d.abs()
+        elif loss == "huber":
+            delta = float(self._parms.get("huber_alpha", 0.9))
+            g = torch.clamp(d, -delta, delta)
+            lo = torch.where(d.abs() <= delta, 0.5 * d * d, delta * (d.abs() - 0.5 * delta))
+        elif loss == "quantile":
+            a = float(self._parms.get("quantile_alpha", 0.5))
+            g = torch.where(d > 0, torch.full_like(d, 1 - a), torch.full_like(d, -a))
+            lo = torch.where(d > 0, (1 - a) * d, -a * d)
+        elif not ae and self._dist.family not in ("gaussian",):
+            # Linear.setOutputLayerGradient: g = -2 * negHalfGradient(t, y)
+            g = -2.0 * self._dist.neg_half_gradient(t, Zo)
+            lo = d * d
         else:
-            opt = torch.optim.SGD(net.parameters(), lr=float(p["rate"]), momentum=float(p.get("momentum_stable", 0)),
-                                  nesterov=bool(p.get("nesterov_accelerated_gradient")) and float(p.get("momentum_stable", 0)) > 0)
-        l1, l2 = float(p.get("l1", 0)), float(p.get("l2", 0))
+            g, lo = 2.0 * d, d * d
+        lo = lo.sum(1)
+        if wb is not None:
+            g = g * wb.view(-1, 1)
+            lo = lo * wb
+        return g * inv_n, lo
+
+    def _train_loop(self, spec, X, Y, w, ae, K):
+        p = self._parms
         n = X.shape[0]
+        W_ = cloud.world()
         ntot = coll.allreduce_scalar(float(n))
         epochs = float(p.get("epochs", 10))
-        bs = max(int(p.get("mini_batch_size", 1)), 32)   # GPU minibatch (reference default 1 = Hogwild per row)
-        bs = min(bs if p.get("mini_batch_size", 1) > 1 else 256, max(n, 1))
-        steps = int(math.ceil(epochs * ntot / (bs * cloud.world())))
-        loss_name = (p.get("loss") or "Automatic").lower()
-        gen = torch.Generator(device=X.device).manual_seed(self._seed() + cloud.rank())
+        mbs = int(p.get("mini_batch_size") or 1)
+        # mini_batch_size=1 (the reference's per-row updates): a GPU batch that
+        # still gives >= ~256 updates per epoch (ADADELTA's step size does not
+        # grow with the batch, so progress per epoch follows the update count)
+        bs = max(mbs, _MIN_GPU_BATCH) if mbs > 1 else int(min(1024, max(_MIN_GPU_BATCH, ntot // (256 * W_))))
+        bs = max(1, min(bs, n))
+        total_samples = epochs * ntot
+        tspi = int(p.get("train_samples_per_iteration", -2))
+        per_iter = ntot if tspi in (-2, -1, 0) else max(float(tspi), bs * W_)
+        ada = bool(p.get("adaptive_rate", True))
+        rate0, anneal, decay = float(p["rate"]), float(p["rate_annealing"]), float(p["rate_decay"])
+        mom_start, mom_ramp, mom_stable = float(p["momentum_start"]), float(p["momentum_ramp"]), \
+            float(p["momentum_stable"])
+        has_mom = (not ada) and (mom_start > 0 or mom_stable > 0)
+        l1, l2 = float(p.get("l1", 0)), float(p.get("l2", 0))
+        max_w2 = float(p.get("max_w2") or 3.4028235e38)
+        sparsity = float(p.get("sparsity_beta") or 0.0) if ae else 0.0
+        avg_act = [torch.zeros(L.fout, device=X.device) for L in self._layers[:-1]] if sparsity > 0 else None
+        gen = torch.Generator(device=X.device).manual_seed(self._seed() * 31 + cloud.rank())
         t0 = time.time()
         max_rt = float(p.get("max_runtime_secs") or 0)
         self._scoring_history = []
-        net.train()
-        params = [q for q in net.parameters()]
-        lr0 = float(p.get("rate", 0.005))
-        for step in range(max(1, steps)):
-            idx = torch.randint(0, max(n, 1), (bs,), generator=gen, device=X.device)
-            xb = X[idx]
-            out = net(xb)
-            if ae:
-                loss = ((out - xb) ** 2).mean()
-            elif K > 1:
-                loss = nn.functional.cross_entropy(out, Y[idx], reduction="none")
-                loss = (loss * w[idx]).mean() if w is not None else loss.mean()
-            else:
-                d = out - Y[idx]
-                if loss_name == "absolute":
-                    l_ = d.abs()
-                elif loss_name == "huber":
-                    l_ = torch.nn.functional.huber_loss(out, Y[idx], reduction="none")
-                else:
-                    l_ = d * d
-                loss = (l_.view(-1) * w[idx]).mean() if w is not None else l_.mean()
-            if l1 > 0 or l2 > 0:
-                for m in net.modules():
-                    if isinstance(m, nn.Linear):
-                        if l1 > 0:
-                            loss = loss + l1 * m.weight.abs().sum()
-                        if l2 > 0:
-                            loss = loss + 0.5 * l2 * (m.weight ** 2).sum()
-            opt.zero_grad(set_to_none=False)
-            loss.backward()
-            if cloud.is_distributed():
-                grads = [q.grad for q in params if q.grad is not None]
-                coll.allreduce_many_(grads)
-                for g_ in grads:
-                    g_.div_(cloud.world())
-            if not p.get("adaptive_rate", True):
-                for gr in opt.param_groups:
-                    gr["lr"] = lr0 / (1 + float(p.get("rate_annealing", 1e-6)) * step * bs)
-            opt.step()
+        stop_rounds = int(p.get("stopping_rounds") or 0)
+        smetric = (p.get("stopping_metric") or "auto").lower()
+        if smetric == "auto":
+            smetric = "logloss" if K > 1 else ("mse" if ae else "deviance")
+        history, best = [], None
+        step_seed = self._seed() * 1000003
+        perm, pos = None, n
+        samples_done = 0.0
+        next_score = per_iter
+        it = 0
+        while samples_done < total_samples:
+            if pos + bs > n:
+                perm = torch.randperm(n, generator=gen, device=X.device)
+                pos = 0
+            idx = perm[pos:pos + bs]
+            pos += bs
+            xb = X.index_select(0, idx)
+            yb = None if Y is None else Y.index_select(0, idx)
+            wb = None if w is None else w.index_select(0, idx)
+            step_seed = (step_seed * 6364136223846793005 + 1442695040888963407) & ((1 << 63) - 1)
+            acts, zs = self._forward(xb, True, step_seed)
+            dZ, _ = self._output_grad(zs[-1], yb, wb, 1.0 / bs, K, ae, xb)
+            grads = []
+            for li in range(len(self._layers) - 1, -1, -1):
+                L = self._layers[li]
+                Aprev = acts[li]
+                if li == len(self._layers) - 1:
+                    db = dZ.sum(0)
+                dW = dZ.t() @ Aprev
+                grads.append((li, dW, db))
+                if li > 0:
+                    dA = dZ @ L.W
+                    Lp = self._layers[li - 1]
+                    dZ, db = dl_ops.bwd(dA, acts[li], zs[li - 1], Lp.act, Lp.drop, seed=step_seed + 7919 * li)
+            if W_ > 1:
+                flat = [g for (_, a, b_) in grads for g in (a, b_)]
+                coll.allreduce_many_(flat)
+                for g in flat:
+                    g.div_(W_)
+            if avg_act is not None:
+                for li in range(len(self._layers) - 1):
+                    avg_act[li].mul_(0.999).add_(0.001 * acts[li + 1].mean(0))
+            self._processed += bs * W_
+            m = mom_start
+            if mom_ramp > 0:
+                m = mom_stable if self._processed >= mom_ramp else \
+                    mom_start + (mom_stable - mom_start) * self._processed / mom_ramp
+            for (li, dW, db) in grads:
+                L = self._layers[li]
+                r = rate0 / (1 + anneal * self._processed) * decay ** li
+                up = dl_ops.UpdateParams(ada=ada, rho=float(p["rho"]), eps=float(p["epsilon"]),
+                                         rate=r * (1 - m) if not ada else 0.0, momentum=m,
+                                         nesterov=bool(p.get("nesterov_accelerated_gradient", True)),
+                                         has_momenta=has_mom, l1=l1, l2=l2, max_w2=max_w2,
+                                         sparsity_beta=sparsity,
+                                         average_activation=float(p.get("average_activation") or 0.0))
+                dl_ops.update(L.W, dW.contiguous(), L.b, db.contiguous(), L.state, up,
+                              avg_act=avg_act[li] if (avg_act is not None and li < len(avg_act)) else None)
+            samples_done += bs * W_
+            if samples_done >= next_score or samples_done >= total_samples:
+                it += 1
+                next_score += per_iter
+                self._epochs_done = samples_done / max(ntot, 1)
+                entry = self._score_history_entry(spec, X, Y, w, ae, K, t0)
+                self._scoring_history.append(entry)
+                val = entry.get(("validation_" if spec.valid is not None else "training_") + smetric)
+                history.append(val)
+                if val is not None and p.get("overwrite_with_best_model", True):
+                    better = best is None or (val < best[0] if smetric in _LESS_IS_BETTER else val > best[0])
+                    if better:
+                        best = (val, [(L.W.clone(), L.b.clone()) for L in self._layers])
+                if self._stop_on_error(entry, K, ae):
+                    break
+                if stop_rounds > 0 and ScoreKeeper.stop_early(history, stop_rounds,
+                                                              float(p.get("stopping_tolerance", 0.0)),
+                                                              smetric in _LESS_IS_BETTER):
+                    break
             if max_rt > 0 and time.time() - t0 > max_rt:
                 break
-            if step % max(1, steps // 10) == 0:
-                self._scoring_history.append({"iterations": step, "epochs": step * bs * cloud.world() / max(ntot, 1),
-                                              "training_loss": float(loss.detach())})
-        net.eval()
-        self._K = K
-        self._ae = ae
-        if p.get("variable_importances", True) and not ae:
-            self._output["variable_importances"] = self._gedeon(di)
-        self._output["model_summary"] = {"layers": [P] + list(p.get("hidden") or []) + [out_dim],
-                                         "activation": p.get("activation"), "epochs": epochs}
+        self._epochs_done = samples_done / max(ntot, 1)
+        if best is not None and p.get("overwrite_with_best_model", True):
+            for L, (Wb, bb) in zip(self._layers, best[1]):
+                L.W.copy_(Wb)
+                L.b.copy_(bb)
+
+    def _stop_on_error(self, entry, K, ae):
+        """classification_stop / regression_stop on the training error."""
+        p = self._parms
+        if K > 1:
+            cs = float(p.get("classification_stop", 0.0))
+            err = entry.get("training_classification_error")
+            return cs >= 0 and err is not None and err <= cs
+        rs = float(p.get("regression_stop", 1e-6))
+        mse = entry.get("training_mse")
+        return rs >= 0 and mse is not None and mse <= rs
+
+    def _score_history_entry(self, spec, X, Y, w, ae, K, t0):
+        from .tree.gbm import H2OGradientBoostingEstimator as _G
+        p = self._parms
+        entry = {"timestamp": time.time(), "duration_s": time.time() - t0, "epochs": self._epochs_done,
+                 "samples": self._processed}
+        ns = int(p.get("score_training_samples") or 0)
+        Xs, Ys = X, Y
+        if 0 < ns < X.shape[0]:
+            sel = torch.randperm(X.shape[0], device=X.device)[:ns]
+            Xs = X[sel]
+            Ys = None if Y is None else Y[sel]
+        with torch.no_grad():
+            out = self._predict_matrix(Xs)
+        if ae:
+            entry["training_mse"] = float(((out - Xs) ** 2).mean())
+            return entry
+        if K > 1:
+            yy = Ys
+            raw = out
+            if K == 2:
+                m = mm.binomial_metrics(yy.to(torch.float64), raw[:, 1], None, spec.response_domain)
+            else:
+                m = mm.multinomial_metrics(yy, raw, None, spec.response_domain)
+        else:
+            pred = out[:, 0] * self._ysd + self._ymu
+            m = mm.regression_metrics((Ys[:, 0] * self._ysd + self._ymu).to(torch.float64), pred, None, self._dist)
+        _G._add_metrics(entry, "training", m)
+        if spec.valid is not None:
+            vm = self._metrics_from_raw(spec, spec.valid, self._predict_raw(spec.valid))
+            _G._add_metrics(entry, "validation", vm)
+        return entry
+
+    # ------------------------------------------------------------------ scoring
+    def _predict_matrix(self, X):
+        """Output-layer values for a design matrix: class probabilities,
+        standardized regression values or the reconstruction."""
+        acts, zs = self._forward(X, False)
+        Zo = zs[-1]
+        Lo = self._layers[-1]
+        if self._K > 1:
+            P, _, _ = dl_ops.softmax(Zo, Lo.b, None, want_grad=False)
+            return P
+        Zo += Lo.b.view(1, -1)
+        return Zo
+
+    def _predict_raw(self, frame):
+        X, _ = self._dinfo.expand(frame, pad=False)
+        with torch.no_grad():
+            out = self._predict_matrix(X)
+        if self._ae or self._K > 1:
+            return out
+        f = out * self._ysd + self._ymu
+        if self._dist.family not in ("gaussian", "laplace", "quantile", "huber"):
+            f = self._dist.linkinv(f)
+        return f
 
     def _gedeon(self, di):
         """Gedeon (1997) input importance from the weight matrices."""
-        lins = [m for m in self._net.modules() if isinstance(m, nn.Linear)]
         with torch.no_grad():
             imp = None
-            for m in reversed(lins):
-                W = m.weight.abs()
+            for L in reversed(self._layers):
+                W = L.W.abs()
+                if L.k > 1:
+                    W = W.view(L.fout, L.k, L.fin).sum(1)
                 W = W / W.sum(1, keepdim=True).clamp_min(1e-30)
                 imp = W if imp is None else imp @ W
             v = imp.sum(0)
-        names = di.coef_names
         vi = {}
-        for n_, val in zip(names, v.tolist()):
+        for n_, val in zip(di.coef_names, v.tolist()):
             base = n_.split(".")[0] if n_ not in di.num_cols else n_
             vi[base] = vi.get(base, 0.0) + val
         return vi
-
-    def _forward(self, frame):
-        X, _ = self._dinfo.expand(frame, pad=False)
-        with torch.no_grad():
-            return self._net(X), X
-
-    def _predict_raw(self, frame):
-        out, X = self._forward(frame)
-        if self._ae:
-            return out
-        if self._K > 1:
-            return torch.softmax(out, 1)
-        return (out * self._ysd + self._ymu)
 
     def predict(self, test_data, **kw):
         if self._ae:
@@ -274,7 +492,9 @@ class H2ODeepLearningEstimator(H2OEstimator):
         return super().predict(test_data, **kw)
 
     def anomaly(self, test_data, per_feature=False):
-        out, X = self._forward(test_data)
+        X, _ = self._dinfo.expand(test_data, pad=False)
+        with torch.no_grad():
+            out = self._predict_matrix(X)
         err = (out - X) ** 2
         if per_feature:
             return H2OFrame.from_vecs([Vec(err[:, j].contiguous(), T_REAL) for j in range(err.shape[1])],
@@ -283,22 +503,25 @@ class H2ODeepLearningEstimator(H2OEstimator):
 
     def deepfeatures(self, test_data, layer):
         X, _ = self._dinfo.expand(test_data, pad=False)
-        idx = self._hidden_idx[layer]
         with torch.no_grad():
-            h = self._net[: idx + 1](X)
+            acts, _ = self._forward(X, False)
+        h = acts[layer + 1]
         return H2OFrame.from_vecs([Vec(h[:, j].contiguous(), T_REAL) for j in range(h.shape[1])],
                                   [f"DF.L{layer + 1}.C{j + 1}" for j in range(h.shape[1])])
 
     def weights(self, matrix_id=0):
-        lins = [m for m in self._net.modules() if isinstance(m, nn.Linear)]
-        return H2OFrame.from_tensor(lins[matrix_id].weight.detach())
+        return H2OFrame.from_tensor(self._layers[matrix_id].W.detach())
 
     def biases(self, vector_id=0):
-        lins = [m for m in self._net.modules() if isinstance(m, nn.Linear)]
-        return H2OFrame.from_tensor(lins[vector_id].bias.detach().view(-1, 1))
+        return H2OFrame.from_tensor(self._layers[vector_id].b.detach().view(-1, 1))
 
     def _score_unsupervised(self, spec):
         if self._ae:
-            out, X = self._forward(spec.frame)
+            X, _ = self._dinfo.expand(spec.frame, pad=False)
+            with torch.no_grad():
+                out = self._predict_matrix(X)
             mse = float(((out - X) ** 2).mean())
             self._training_metrics = mm.ModelMetricsAutoEncoder(MSE=mse, RMSE=math.sqrt(mse), nobs=spec.frame.nrows)
+
+    def scoring_history(self):
+        return self._scoring_history

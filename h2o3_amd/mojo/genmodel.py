@@ -323,6 +323,8 @@ class MojoModel:
                     h = np.maximum(h, 0)
                 elif kind == "elu":
                     h = np.where(h > 0, h, np.expm1(h))
+                elif kind == "scale":
+                    h = h * L[2]
             if m["autoencoder"]:
                 return h
             if m["K"] > 1:

@@ -182,19 +182,19 @@ def build_mojo(model) -> bytes:
         w.add_array("mean", model._mean.cpu().numpy())
     elif algo == "deeplearning":
         _dinfo_meta(w, model._dinfo)
-        import torch.nn as nn
         layers = []
-        for i, m in enumerate(model._net):
-            if isinstance(m, nn.Linear):
-                w.add_array(f"W{i}", m.weight.detach().cpu().numpy())
-                w.add_array(f"b{i}", m.bias.detach().cpu().numpy())
+        act_kind = {"tanh": "tanh", "rectifier": "relu", "exprectifier": "elu"}
+        for i, L in enumerate(model._layers):
+            w.add_array(f"W{i}", L.W.detach().cpu().numpy())
+            w.add_array(f"b{i}", L.b.detach().cpu().numpy())
+            if L.k > 1:
+                layers.append(["maxout", i, L.k])
+            else:
                 layers.append(["linear", i])
-            elif m.__class__.__name__ == "_Maxout":
-                w.add_array(f"W{i}", m.lin.weight.detach().cpu().numpy())
-                w.add_array(f"b{i}", m.lin.bias.detach().cpu().numpy())
-                layers.append(["maxout", i, m.k])
-            elif isinstance(m, (nn.Tanh, nn.ReLU, nn.ELU)):
-                layers.append([type(m).__name__.lower(), i])
+                if L.act in act_kind:
+                    layers.append([act_kind[L.act], i])
+            if L.drop > 0:
+                layers.append(["scale", i, 1.0 - L.drop])   # test-time dropout scaling
         w.meta["layers"] = layers
         w.meta["autoencoder"] = bool(model._ae)
         w.meta["K"] = model._K

@@ -33,3 +33,238 @@ def test_autoencoder_anomaly():
     a = m.anomaly(fr)
     assert a.nrows == 2000
     assert m.deepfeatures(fr, 0).ncols == 3
+
+
+# ---------------------------------------------------------------- reference semantics
+import math
+
+import pytest
+import torch
+
+from h2o3_amd.ops import dl_ops
+
+
+def _frame_cls(n=2000, seed=3):
+    rng = np.random.RandomState(seed)
+    X = rng.randn(n, 6)
+    logit = 2 * X[:, 0] - X[:, 1] + X[:, 2] * X[:, 3]
+    y = (rng.rand(n) < 1 / (1 + np.exp(-logit))).astype(int)
+    df = pd.DataFrame(X, columns=[f"x{i}" for i in range(6)])
+    df["y"] = np.where(y == 1, "yes", "no")
+    df["r"] = X[:, 0] * 2 + np.sin(X[:, 1]) + 0.05 * rng.randn(n)
+    df["cnt"] = rng.poisson(np.exp(0.5 * X[:, 0]))
+    return h2o3_amd.H2OFrame(df), [f"x{i}" for i in range(6)]
+
+
+def test_manual_backprop_matches_autograd():
+    """The step's hand-written backward (GEMMs + dl_ops.bwd) equals autograd
+    of the same forward (no dropout)."""
+    torch.manual_seed(0)
+    m = H2ODeepLearningEstimator(hidden=[7, 5], activation="Tanh", seed=4)
+    layers = m._build(4, 3, True)
+    m._layers = layers
+    m._parms["input_dropout_ratio"] = 0.0
+    X = torch.randn(16, 4)
+    y = torch.randint(0, 3, (16,))
+    acts, zs = m._forward(X.clone(), True, 1)
+    _, dZ, _ = dl_ops.softmax(zs[-1], layers[-1].b, y, None, 1.0 / 16)
+    grads = {}
+    for li in range(len(layers) - 1, -1, -1):
+        L = layers[li]
+        if li == len(layers) - 1:
+            db = dZ.sum(0)
+        grads[li] = (dZ.t() @ acts[li], db)
+        if li > 0:
+            dZ, db = dl_ops.bwd(dZ @ L.W, acts[li], zs[li - 1], layers[li - 1].act)
+    Ws = [L.W.clone().requires_grad_(True) for L in layers]
+    bs = [L.b.clone().requires_grad_(True) for L in layers]
+    h = X
+    for i in range(len(layers) - 1):
+        h = torch.tanh(h @ Ws[i].t() + bs[i])
+    loss = torch.nn.functional.cross_entropy(h @ Ws[-1].t() + bs[-1], y)
+    loss.backward()
+    for li in range(len(layers)):
+        torch.testing.assert_close(grads[li][0], Ws[li].grad, rtol=1e-4, atol=1e-6)
+        torch.testing.assert_close(grads[li][1], bs[li].grad, rtol=1e-4, atol=1e-6)
+
+
+def test_adadelta_row_update_matches_reference_formulas():
+    """Neurons.bprop + computeAdaDeltaRateForWeight / ForBias, per row."""
+    rng = np.random.RandomState(5)
+    U, I = 3, 5
+    W = torch.tensor(rng.randn(U, I), dtype=torch.float32)
+    b = torch.tensor(rng.randn(U), dtype=torch.float32)
+    dW = torch.tensor(rng.randn(U, I), dtype=torch.float32)
+    db = torch.tensor(rng.randn(U), dtype=torch.float32)
+    rho, eps, l1, l2 = 0.95, 1e-6, 1e-3, 1e-2
+    Wn, bn = W.double().numpy().copy(), b.double().numpy().copy()
+    E = np.zeros((U, I, 2))
+    Eb = np.zeros((U, 2))
+    for _ in range(3):   # three steps exercise the accumulators
+        st = {} if _ == 0 else st
+        for r in range(U):
+            g2s = 0.0
+            for c in range(I):
+                g = dW[r, c].item() + np.sign(Wn[r, c]) * l1 + Wn[r, c] * l2
+                E[r, c, 1] = rho * E[r, c, 1] + (1 - rho) * g * g
+                rate = math.sqrt((E[r, c, 0] + eps) / (E[r, c, 1] + eps))
+                E[r, c, 0] = rho * E[r, c, 0] + (1 - rho) * rate * rate * g * g
+                Wn[r, c] -= rate * g
+                g2s += g * g
+            avg = g2s / I
+            pg = db[r].item() + np.sign(bn[r]) * l1 + bn[r] * l2
+            Eb[r, 1] = rho * Eb[r, 1] + (1 - rho) * avg
+            rate = math.sqrt((Eb[r, 0] + eps) / (Eb[r, 1] + eps))
+            Eb[r, 0] = rho * Eb[r, 0] + (1 - rho) * rate * rate * avg
+            bn[r] -= rate * pg
+        dl_ops.update(W, dW, b, db, st, dl_ops.UpdateParams(ada=True, rho=rho, eps=eps, l1=l1, l2=l2))
+    np.testing.assert_allclose(W.numpy(), Wn, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(b.numpy(), bn, rtol=1e-5, atol=1e-6)
+
+
+def test_momentum_nesterov_and_max_w2():
+    W = torch.ones((2, 4))
+    b = torch.zeros(2)
+    dW = torch.full((2, 4), 0.5)
+    db = torch.full((2,), 0.1)
+    st = {}
+    up = dl_ops.UpdateParams(ada=False, rate=0.1, momentum=0.5, nesterov=True, has_momenta=True, max_w2=2.0)
+    dl_ops.update(W, dW, b, db, st, up)
+    # nesterov: m = 0.5*0 - g = -0.5 ; w = 1 + 0.1*(-0.5) = 0.95 -> row |w|^2 = 3.61 > 2 -> rescale
+    s = math.sqrt(2.0 / (4 * 0.95 ** 2))
+    np.testing.assert_allclose(W.numpy(), np.full((2, 4), 0.95 * s), rtol=1e-6)
+    np.testing.assert_allclose(b.numpy(), np.full(2, -0.01), rtol=1e-6)
+
+
+def test_dropout_mask_rate_and_test_scaling():
+    mask = dl_ops.keep_mask(12345, 2000, 300, 0.3, "cpu")
+    assert abs(float(mask.float().mean()) - 0.7) < 0.005
+    # same seed -> same bits (forward and backward recompute them)
+    assert bool((mask == dl_ops.keep_mask(12345, 2000, 300, 0.3, "cpu")).all())
+    Z = torch.randn(4, 3)
+    A = dl_ops.fwd(Z.clone(), torch.zeros(3), "rectifier", 0.5, train=False, test_scale=0.5)
+    torch.testing.assert_close(A, torch.relu(Z) * 0.5)
+
+
+@pytest.mark.parametrize("act", ["TanhWithDropout", "RectifierWithDropout", "Maxout", "ExpRectifier"])
+def test_activations_train(act):
+    fr, x = _frame_cls()
+    m = H2ODeepLearningEstimator(hidden=[24, 24], epochs=15, seed=1, activation=act)
+    m.train(x=x, y="y", training_frame=fr)
+    assert m.auc() > 0.8, (act, m.auc())
+    p = m.predict(fr)
+    assert p.ncols == 3
+
+
+def test_regression_losses_and_distributions():
+    fr, x = _frame_cls()
+    for kw in ({"loss": "Huber"}, {"loss": "Absolute"}, {"loss": "Quantile", "quantile_alpha": 0.5}):
+        m = H2ODeepLearningEstimator(hidden=[16], epochs=20, seed=2, **kw)
+        m.train(x=x, y="r", training_frame=fr)
+        assert m.r2() > 0.8, (kw, m.r2())
+    mp = H2ODeepLearningEstimator(hidden=[16], epochs=20, seed=2, distribution="poisson")
+    mp.train(x=x, y="cnt", training_frame=fr)
+    pred = mp.predict(fr).as_data_frame().iloc[:, 0].values
+    assert (pred > 0).all()
+    cnt = fr.as_data_frame()["cnt"].values
+    assert np.corrcoef(pred, cnt)[0, 1] > 0.3
+
+
+def test_early_stopping_and_best_model():
+    fr, x = _frame_cls(n=3000)
+    tr, va = fr.split_frame(ratios=[0.7], seed=1)
+    m = H2ODeepLearningEstimator(hidden=[32, 32], epochs=200, seed=3, stopping_rounds=2, stopping_tolerance=0.05,
+                                 train_samples_per_iteration=500)
+    m.train(x=x, y="y", training_frame=tr, validation_frame=va)
+    hist = m.scoring_history()
+    assert len(hist) < 200 * 2100 / 500          # stopped early
+    assert "validation_logloss" in hist[-1]
+    best = min(h["validation_logloss"] for h in hist)
+    assert m.logloss(valid=True) <= best * 1.02  # overwrite_with_best_model
+
+
+def test_checkpoint_and_pretrained_autoencoder():
+    fr, x = _frame_cls()
+    ae = H2ODeepLearningEstimator(autoencoder=True, hidden=[12], epochs=5, seed=1, activation="Tanh")
+    ae.train(x=x, training_frame=fr)
+    m = H2ODeepLearningEstimator(hidden=[12], epochs=5, seed=1, activation="Tanh", pretrained_autoencoder=ae)
+    m.train(x=x, y="y", training_frame=fr)
+    assert m.auc() > 0.8
+    m2 = H2ODeepLearningEstimator(hidden=[12], epochs=5, seed=1, activation="Tanh", checkpoint=m)
+    m2.train(x=x, y="y", training_frame=fr)
+    assert m2._processed > m._processed
+    assert m2.auc() > 0.8
+
+
+def test_sparse_autoencoder_and_rate_schedule():
+    fr, x = _frame_cls()
+    ae = H2ODeepLearningEstimator(autoencoder=True, hidden=[8], epochs=3, seed=1, activation="Tanh",
+                                  sparsity_beta=0.1, average_activation=-0.5)
+    ae.train(x=x, training_frame=fr)
+    assert ae.anomaly(fr).nrows == fr.nrows
+    m = H2ODeepLearningEstimator(hidden=[16], epochs=10, seed=1, adaptive_rate=False, rate=0.01,
+                                 momentum_start=0.5, momentum_stable=0.9, momentum_ramp=1000, rate_decay=0.9,
+                                 l1=1e-5, l2=1e-5, max_w2=10.0)
+    m.train(x=x, y="y", training_frame=fr)
+    assert m.auc() > 0.8
+    for L in m._layers:
+        assert float((L.W ** 2).sum(1).max()) <= 10.0 * (1 + 1e-5)
+
+
+# ---------------------------------------------------------------- GPU kernels
+@pytest.mark.gpu
+@pytest.mark.parametrize("act", ["tanh", "rectifier", "exprectifier", "maxout"])
+def test_dl_kernels_match_torch(act):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from h2o3_amd.ops import _native
+    g = torch.Generator(device="cuda").manual_seed(7)
+    B, U, I = 777, 300, 129
+    k = 2 if act == "maxout" else 1
+    Z = torch.randn((B, U * k), generator=g, device="cuda")
+    b = torch.randn(U * k, generator=g, device="cuda")
+    Zn, Zt = Z.clone(), Z.clone()
+    An = dl_ops.fwd(Zn, b, act, 0.3, seed=99, train=True)
+    At = dl_ops.fwd(Zt, b, act, 0.3, seed=99, train=True, use_native=False)
+    assert "libdl.so" in " ".join(_native.loaded_libs())
+    torch.testing.assert_close(An, At, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(Zn, Zt)
+    dA = torch.randn((B, U), generator=g, device="cuda")
+    dZn, dbn = dl_ops.bwd(dA, An, Zn, act, 0.3, seed=99)
+    dZt, dbt = dl_ops.bwd(dA, At, Zt, act, 0.3, seed=99, use_native=False)
+    torch.testing.assert_close(dZn, dZt, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(dbn, dbt, rtol=1e-4, atol=1e-3)
+    # per-row update, ADADELTA and Nesterov momentum with max_w2
+    for up in (dl_ops.UpdateParams(ada=True, l1=1e-4, l2=1e-3, max_w2=5.0),
+               dl_ops.UpdateParams(ada=False, rate=0.01, momentum=0.9, has_momenta=True, nesterov=True, max_w2=5.0)):
+        W = torch.randn((U, I), generator=g, device="cuda") * 0.3
+        bb = torch.randn(U, generator=g, device="cuda")
+        dW = torch.randn((U, I), generator=g, device="cuda")
+        db = torch.randn(U, generator=g, device="cuda")
+        Wt, bt, sn, stt = W.clone(), bb.clone(), {}, {}
+        for _ in range(3):
+            dl_ops.update(W, dW, bb, db, sn, up)
+            dl_ops.update(Wt, dW, bt, db, stt, up, use_native=False)
+        torch.testing.assert_close(W, Wt, rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close(bb, bt, rtol=1e-4, atol=1e-5)
+    # softmax + CE gradient
+    Zs = torch.randn((B, 5), generator=g, device="cuda")
+    y = torch.randint(0, 5, (B,), generator=g, device="cuda")
+    y[::11] = -1
+    bs = torch.randn(5, generator=g, device="cuda")
+    Pn, gn, ln = dl_ops.softmax(Zs.clone(), bs, y, None, 1.0 / B)
+    Pt, gt, lt = dl_ops.softmax(Zs.clone(), bs, y, None, 1.0 / B, use_native=False)
+    torch.testing.assert_close(Pn, Pt, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(gn, gt, rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(ln, lt, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_dl_estimator_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    fr, x = _frame_cls(n=20000)
+    m = H2ODeepLearningEstimator(hidden=[64, 64], epochs=5, seed=1, activation="RectifierWithDropout",
+                                 input_dropout_ratio=0.1)
+    m.train(x=x, y="y", training_frame=fr)
+    assert m.auc() > 0.85
