@@ -564,6 +564,125 @@ class H2OEstimator:
     def training_model_metrics(self):
         return self._training_metrics.as_dict() if self._training_metrics is not None else None
 
+    # ---- DataInfo normalization (model_base.py normmul/normsub/respmul/respsub/catoffsets)
+    def _di(self):
+        di = getattr(self, "_dinfo", None)
+        if di is None:
+            raise AttributeError("this model has no design-matrix normalization (no DataInfo)")
+        return di
+
+    def normmul(self):
+        di = self._di()
+        return [1.0 / s for s in di.sigmas] if di.standardize else None
+
+    def normsub(self):
+        di = self._di()
+        return list(di.means) if di.standardize else None
+
+    def respmul(self):
+        sd = getattr(self, "_ysd", None)
+        return None if sd is None else 1.0 / sd
+
+    def respsub(self):
+        return getattr(self, "_ymu", None)
+
+    def catoffsets(self):
+        di = self._di()
+        offs, acc = [0], 0
+        for c in di.cat_cols:
+            acc += len(di.domains[c]) - (0 if di.use_all else 1)
+            offs.append(acc)
+        return offs
+
+    def pprint_coef(self):
+        coefs = getattr(self, "coef", None)
+        if coefs is None:
+            print("No coefficients for this model")
+            return
+        c = coefs()
+        for k, v in sorted(c.items(), key=lambda kv: -abs(kv[1])):
+            print(f"{k:>30s} {v: .6g}")
+
+    def predicted_vs_actual_by_variable(self, frame, predicted, variable, use_pandas=False):
+        """Per-level weighted means of prediction and actual for a categorical
+        variable (water/rapids/prims/AstPredictedVsActualByVar.java); the last
+        row is the NA level."""
+        import pandas as pd
+        if not self.supervised_learning:
+            raise ValueError("Only supervised models are supported for calculating predicted v actual")
+        if self._spec.nclasses > 2:
+            raise ValueError("Multinomial classification models are not supported by predicted v actual")
+        if frame.nrows != predicted.nrows:
+            raise ValueError("Input frame and frame of predictions need to have same number of rows.")
+        v = frame.vec(variable)
+        if v.type != T_ENUM:
+            raise ValueError(f"'{variable}' is not categorical")
+        L = len(v.domain)
+        level = torch.where(v.data < 0, torch.full_like(v.data, L), v.data).long()
+        pv = predicted.vec(predicted.names[0])
+        pr = pv.data.to(torch.float64) if pv.type == T_ENUM else pv.as_float(torch.float64)
+        act = self._spec.y_tensor(frame).to(torch.float64)
+        ok = act >= 0 if self._spec.is_classification else ~torch.isnan(act)
+        w = self._spec.w_tensor(frame)
+        w = torch.ones_like(act) if w is None else w.to(torch.float64)
+        w = torch.where(ok, w, torch.zeros_like(w))
+        st = torch.zeros((3, L + 1), dtype=torch.float64, device=act.device)
+        st[0].index_add_(0, level, w * torch.where(ok, pr, torch.zeros_like(pr)))
+        st[1].index_add_(0, level, w * torch.where(ok, act, torch.zeros_like(act)))
+        st[2].index_add_(0, level, w)
+        coll.allreduce_(st)
+        den = torch.where(st[2] > 0, st[2], torch.ones_like(st[2]))
+        res = (st[:2] / den).cpu().numpy()
+        df = pd.DataFrame({variable: list(v.domain) + [None], predicted.names[0]: res[0], "actual": res[1]})
+        return df.set_index(variable) if use_pandas else df
+
+    def _plot_or_data(self, kind, data, server=False):
+        """Plots need matplotlib; without it (this image) the plot's data is
+        returned so callers still get the numbers."""
+        try:
+            import matplotlib  # noqa: F401
+        except ImportError:
+            import warnings
+            warnings.warn(f"matplotlib is not installed: {kind} returns its data instead of a figure")
+            return data
+        import matplotlib
+        if server:
+            matplotlib.use("Agg")
+        import matplotlib.pyplot as plt
+        fig, ax = plt.subplots()
+        names, vals = zip(*data) if data else ((), ())
+        ax.barh(list(names)[::-1], list(vals)[::-1])
+        ax.set_title(kind)
+        if not server:
+            plt.show()
+        return fig
+
+    def varimp_plot(self, num_of_features=None, server=False, save_plot_path=None):
+        vi = self.varimp()
+        if vi is None:
+            return None
+        rows = [(r[0], r[2]) for r in vi] if isinstance(vi, list) and vi and isinstance(vi[0], (tuple, list)) \
+            else sorted(((k, v) for k, v in dict(vi).items()), key=lambda kv: -kv[1])
+        return self._plot_or_data("Variable Importance", rows[:num_of_features or 10], server)
+
+    def std_coef_plot(self, num_of_features=None, server=False, save_plot_path=None):
+        cn = getattr(self, "coef_norm", None)
+        if cn is None:
+            raise AttributeError("std_coef_plot needs a model with standardized coefficients")
+        rows = sorted(((k, abs(v)) for k, v in cn().items() if k != "Intercept"), key=lambda kv: -kv[1])
+        return self._plot_or_data("Standardized Coef. Magnitudes", rows[:num_of_features or 10], server)
+
+    def permutation_importance_plot(self, frame, metric="AUTO", n_samples=10000, n_repeats=1, features=None,
+                                    seed=-1, num_of_features=10, server=False, save_plot_path=None):
+        from .explain import permutation_importance
+        pi = permutation_importance(self, frame, metric=metric, n_samples=n_samples, n_repeats=n_repeats,
+                                    features=features, seed=seed)
+        if hasattr(pi, "columns") and "Relative Importance" in pi.columns:
+            rows = list(zip(pi["Variable"], pi["Relative Importance"]))
+        else:
+            rows = list(zip(pi.iloc[:, 0], pi.iloc[:, 1:].mean(1))) if hasattr(pi, "iloc") else list(pi)
+        return self._plot_or_data("Permutation Variable Importance", rows[:num_of_features], server)
+
     # ---- model bookkeeping (h2o-py model_base.py)
     @property
     def start_time(self):

@@ -11,6 +11,7 @@ import ctypes
 import math
 
 import numpy as np
+import pandas as pd
 import torch
 
 from ...core.frame import H2OFrame
@@ -252,6 +253,43 @@ class SharedTreeEstimator(H2OEstimator):
     @property
     def ntrees_built(self):
         return len(self._forest) // max(1, self._n_tree_classes())
+
+    def ntrees_actual(self):
+        """Trees actually built (early stopping may stop before ntrees)."""
+        return self.ntrees_built
+
+    def feature_interaction(self, max_interaction_depth=100, max_tree_depth=100, max_deepening=-1, path=None):
+        """Feature interaction tables (hex/FeatureInteractions.java): one
+        table per interaction depth, leaf statistics, split value histograms."""
+        from .interactions import feature_interactions, interaction_tables
+        K = self._n_tree_classes()
+        fis = feature_interactions(self._forest, list(self._spec.x), len(self._forest) // max(K, 1), K,
+                                   max_interaction_depth, max_tree_depth, max_deepening)
+        tables = interaction_tables(fis)
+        if path is not None:
+            with pd.ExcelWriter(path) as xw:
+                for i, t in enumerate(tables):
+                    t.to_excel(xw, sheet_name=t.attrs.get("table_header", f"t{i}")[:31], index=False)
+        return tables
+
+    def feature_frequencies(self, test_data):
+        """Per row: how often each feature is used on its decision paths,
+        summed over the trees."""
+        from .interactions import feature_frequencies
+        X = self._score_matrix(test_data)
+        leaf = self._forest.predict(X, self._n_tree_classes(), leaf=True)
+        fq = feature_frequencies(self._forest, leaf, len(self._spec.x))
+        return H2OFrame.from_vecs([Vec(fq[:, j].contiguous(), T_REAL) for j in range(fq.shape[1])],
+                                  list(self._spec.x))
+
+    def update_tree_weights(self, frame, weights_column):
+        """Re-populate node covers from `frame` weighted by `weights_column`
+        (SharedTreeModel.updateTreeWeights); TreeSHAP then explains that
+        sub-population."""
+        from .interactions import update_tree_weights
+        X = self._score_matrix(frame)
+        leaf = self._forest.predict(X, self._n_tree_classes(), leaf=True)
+        update_tree_weights(self._forest, leaf, frame.vec(weights_column).as_float(torch.float64))
 
     def get_tree(self, tree_number=0, tree_class=None):
         K = self._n_tree_classes()
