@@ -131,9 +131,10 @@ def main():
         del fr
         C = [est._init_centers(Xk, None, args.k, __import__("numpy").random.RandomState(1))]
         asg = torch.full((Xk.shape[0],), -1, dtype=torch.int32, device=dev)
+        xabs = cluster_ops.abs_bound(Xk)
 
         def step():
-            st = cluster_ops.lloyd_pass(Xk, C[0], None, asg)
+            st = cluster_ops.lloyd_pass(Xk, C[0], None, asg, xabs_max=xabs)
             coll.allreduce_(st.vec)
             C[0] = torch.where(st.weights.view(-1, 1) > 0, st.sums / st.weights.clamp_min(1e-300).view(-1, 1), C[0])
         metric = "kmeans_iters_per_sec"

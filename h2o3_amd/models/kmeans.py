@@ -167,7 +167,7 @@ class H2OKMeansEstimator(H2OEstimator):
         hist = []
         st = None
         while True:
-            st = cluster_ops.lloyd_pass(X, C, w, assign, accumulate=True)
+            st = cluster_ops.lloyd_pass(X, C, w, assign, accumulate=True, xabs_max=self._xabs(X, w))
             coll.allreduce_(st.vec)
             wts = st.weights
             newC = torch.where(wts.view(-1, 1) > 0, st.sums / wts.clamp_min(1e-300).view(-1, 1), C)
@@ -189,6 +189,13 @@ class H2OKMeansEstimator(H2OEstimator):
             if st.changed < max(1.0, nrows_tot * TOLERANCE) or it >= maxit or (t_end and time.time() > t_end):
                 break
         return C, st, it, hist
+
+    def _xabs(self, X, w):
+        """max |w x| of the training matrix, once per fit (fixed-point sums)."""
+        key = (X.data_ptr(), X.shape, None if w is None else w.data_ptr())
+        if getattr(self, "_xabs_key", None) != key:
+            self._xabs_key, self._xabs_val = key, cluster_ops.abs_bound(X, w)
+        return self._xabs_val
 
     def _worst_row(self, X, C):
         dmin = torch.empty(X.shape[0], dtype=torch.float32, device=X.device)

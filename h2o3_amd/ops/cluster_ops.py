@@ -16,18 +16,18 @@ import torch
 
 from . import _native
 
-_cv, _ci, _cll = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong
+_cv, _ci, _cll, _cf = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong, ctypes.c_float
 
 
 def _lib():
     lib = _native.get_lib("kmeans")
     if lib is not None and not getattr(lib, "_typed", False):
-        lib.h2o_kmeans_lloyd.argtypes = [_cv, _cv, _cll, _ci, _cv, _cv, _ci, _cv, _cv, _cv, _cv, _ci, _ci, _cv]
+        lib.h2o_kmeans_lloyd.argtypes = [_cv, _cv, _cll, _ci, _cv, _cv, _ci, _cv, _cv, _cv, _cv, _ci, _ci, _cf, _cv]
         lib.h2o_kmeans_reduce.argtypes = [_cv, _ci, _cll, _cv, _cv]
         lib.h2o_kmeans_max_k.argtypes = [_ci, _ci]
         lib.h2o_kmeans_part_stride.argtypes = [_ci, _ci]
         lib.h2o_kmeans_part_stride.restype = _cll
-        lib.h2o_kmeans_resident_per_cu.argtypes = [_ci, _ci, _ci]
+        lib.h2o_kmeans_resident_per_cu.argtypes = [_ci, _ci, _ci, _cf]
         lib._typed = True
     return lib
 
@@ -80,12 +80,23 @@ def native_ok(X, k, accumulate=True):
     return lib is not None and 0 < k <= int(lib.h2o_kmeans_max_k(P, 1 if accumulate else 0))
 
 
-def lloyd_pass(X, C, w=None, assign=None, accumulate=True, dmin=None, use_native=None, n_groups=None):
+def abs_bound(X, w=None):
+    """max |w x| over the matrix (one pass; callers cache it per X): bounds
+    the 64-bit fixed-point cluster sums of the kernel."""
+    m = float(X.abs().max()) if X.numel() else 0.0
+    if w is not None and w.numel():
+        m *= float(w.abs().max())
+    return m
+
+
+def lloyd_pass(X, C, w=None, assign=None, accumulate=True, dmin=None, use_native=None, n_groups=None,
+               xabs_max=None):
     """One pass over X.  assign: int32 [N] buffer, read as the previous
     assignment (changed count) and overwritten with the new one (may be
     None).  dmin: f32 [N] buffer for per-row squared distances to the
-    closest center (may be None).  Returns LloydStats (accumulate=True) or
-    None."""
+    closest center (may be None).  xabs_max: max |w x| (abs_bound) enables
+    the kernel's 64-bit fixed-point cluster sums.  Returns LloydStats
+    (accumulate=True) or None."""
     N, P = X.shape
     k = C.shape[0]
     native = native_ok(X, k, accumulate) if use_native is None else use_native
@@ -96,10 +107,16 @@ def lloyd_pass(X, C, w=None, assign=None, accumulate=True, dmin=None, use_native
     cn = (C.to(torch.float64) ** 2).sum(1).to(device=X.device, dtype=torch.float32).contiguous()
     X = X.contiguous()
     wt = None if w is None else w.to(device=X.device, dtype=torch.float32).contiguous()
+    ntiles = (N + 63) // 64
+    fx = 0.0
+    if accumulate and xabs_max is not None:
+        # per-workgroup |sum| < 2^62 for any grid up to one workgroup per CU
+        rows_wg = 64 * (-(-ntiles // _cu_count(X.device)))
+        fx = float(2.0 ** 62 / (max(xabs_max, 1e-30) * rows_wg)) if xabs_max > 0 else 1.0
+        fx = min(fx, 2.0 ** 100)
     if n_groups is None:
         # persistent grid = exactly the resident workgroups (no tail wave)
-        ntiles = (N + 63) // 64
-        per_cu = int(lib.h2o_kmeans_resident_per_cu(k, P, 1 if accumulate else 0))
+        per_cu = int(lib.h2o_kmeans_resident_per_cu(k, P, 1 if accumulate else 0, fx))
         n_groups = max(1, min(ntiles, max(per_cu, 1) * _cu_count(X.device)))
     part = None
     stride = int(lib.h2o_kmeans_part_stride(k, P))
@@ -107,7 +124,7 @@ def lloyd_pass(X, C, w=None, assign=None, accumulate=True, dmin=None, use_native
         part = torch.empty((n_groups, stride), dtype=torch.float32, device=X.device)
     stream = _cv(torch.cuda.current_stream().cuda_stream)
     rc = lib.h2o_kmeans_lloyd(_ptr(X), _ptr(wt), N, P, _ptr(C32), _ptr(cn), k, _ptr(assign), _ptr(assign), _ptr(dmin),
-                              _ptr(part), n_groups, 1 if accumulate else 0, stream)
+                              _ptr(part), n_groups, 1 if accumulate else 0, fx, stream)
     if rc != 0:
         raise RuntimeError(f"h2o_kmeans_lloyd failed: {rc}")
     if not accumulate:

@@ -43,7 +43,7 @@ template <int KT, int MAXV, bool ACC>
 __global__ __launch_bounds__(KM_THREADS) void kmeans_lloyd_kernel(
     const float* __restrict__ X, const float* __restrict__ w, long long N, int P, const float* __restrict__ Cin,
     const float* __restrict__ cn, int k, int* assign, const int* assign_old,
-    float* __restrict__ dmin_out, float* __restrict__ part, int vrg_in, int dbg) {
+    float* __restrict__ dmin_out, float* __restrict__ part, int vrg_in, float fx_scale, int dbg) {
   extern __shared__ __align__(16) float lds[];
   const int P16 = (P + 15) & ~15;            // k-range padded so each lane group gets a float4 multiple
   const int S = P16 + 4;                     // LDS row stride (dwords)
@@ -57,8 +57,11 @@ __global__ __launch_bounds__(KM_THREADS) void kmeans_lloyd_kernel(
   const int vpr = P <= 64 ? 64 : (P <= 128 ? 128 : 256);
   const int vrg = vrg_in;
   const int vc = (int)threadIdx.x % vpr, vh = (int)threadIdx.x / vpr;
-  float* Ssum = cns + KP;                    // [vrg][k][P] (ACC)
-  float* Swt = Ssum + (ACC ? vrg * k * P : 0);  // [k]
+  // vrg == 0: one [k][P] copy of 64-bit fixed-point sums (returnless
+  // ds_add_u64: ~5 per CU-clock vs 0.33 for ds_add_f32, scripts/lds_atomic_mb.hip)
+  const int sum_f = vrg == 0 ? 2 * k * P : vrg * k * P;   // floats of LDS for the sums
+  float* Ssum = cns + KP;                    // [vrg][k][P] f32, or [k][P] u64 (ACC)
+  float* Swt = Ssum + (ACC ? sum_f : 0);     // [k]
   float* Sss = Swt + (ACC ? k : 0);          // [k]
   float* xsq = Sss + (ACC ? k : 0);          // [64]
   float* dmn = xsq + KM_ROWS;                // [64]
@@ -80,7 +83,7 @@ __global__ __launch_bounds__(KM_THREADS) void kmeans_lloyd_kernel(
   }
   for (int j = tid; j < KP; j += KM_THREADS) cns[j] = j < k ? cn[j] : INFINITY;
   if (ACC) {
-    for (int e = tid; e < vrg * k * P + 2 * k; e += KM_THREADS) Ssum[e] = 0.f;   // Ssum, Swt, Sss contiguous
+    for (int e = tid; e < sum_f + 2 * k; e += KM_THREADS) Ssum[e] = 0.f;   // Ssum, Swt, Sss contiguous
   }
   if (tid == 0) changed_s = 0;
   // X tile columns P..P16 stay zero (the staging below writes only c < P)
@@ -212,7 +215,24 @@ __global__ __launch_bounds__(KM_THREADS) void kmeans_lloyd_kernel(
         }
       }
     }
-    if (ACC && !(dbg & 2) && vh < vrg && vc < P) {
+    if (ACC && !(dbg & 2) && vrg == 0) {
+      // ---- per-cluster sums as 64-bit fixed point: thread -> (row, column)
+      // pairs, columns fastest (consecutive lanes, consecutive words)
+      unsigned long long* S64 = reinterpret_cast<unsigned long long*>(Ssum);
+      const long long nrow = min((long long)KM_ROWS, N - r0);
+      const int tot = (int)nrow * P;
+      int r = tid / P, c = tid - (tid / P) * P;
+      const int dr = KM_THREADS / P, dc = KM_THREADS - (KM_THREADS / P) * P;
+      for (int e = tid; e < tot; e += KM_THREADS) {
+        const float v = wts[r] * Xs[r * S + c];
+        if (v != 0.f)
+          __hip_atomic_fetch_add(S64 + asg[r] * P + c, (unsigned long long)__float2ll_rn(v * fx_scale),
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        r += dr; c += dc;
+        if (c >= P) { c -= P; ++r; }
+      }
+    }
+    if (ACC && !(dbg & 2) && vrg > 0 && vh < vrg && vc < P) {
       // ---- per-cluster sums: thread (vh, vc) walks rows vh, vh+vrg, ... four
       // at a time: the four sums are read first (one LDS round trip), rows
       // of the same cluster are merged in registers, each distinct cluster
@@ -251,10 +271,16 @@ __global__ __launch_bounds__(KM_THREADS) void kmeans_lloyd_kernel(
   }
   if (ACC) {
     float* o = part + (long long)blockIdx.x * km_part_stride(k, P);
-    for (int e = tid; e < k * P; e += KM_THREADS) {
-      float sv = 0.f;
-      for (int h = 0; h < vrg; ++h) sv += Ssum[h * k * P + e];
-      o[e] = sv;
+    if (vrg == 0) {
+      const unsigned long long* S64 = reinterpret_cast<const unsigned long long*>(Ssum);
+      const double inv = 1.0 / (double)fx_scale;
+      for (int e = tid; e < k * P; e += KM_THREADS) o[e] = (float)((double)(long long)S64[e] * inv);
+    } else {
+      for (int e = tid; e < k * P; e += KM_THREADS) {
+        float sv = 0.f;
+        for (int h = 0; h < vrg; ++h) sv += Ssum[h * k * P + e];
+        o[e] = sv;
+      }
     }
     for (int e = tid; e < 2 * k; e += KM_THREADS) o[k * P + e] = Swt[e];   // Swt, Sss contiguous
     if (tid == 0) o[k * P + 2 * k] = (float)changed_s;
@@ -279,13 +305,16 @@ static int km_kt(int k) {   // the template instance a given k runs on
 static size_t km_lds_bytes(int KT, int k, int P, bool acc, int vrg) {
   (void)KT;
   const int P16 = (P + 15) & ~15, S = P16 + 4, KP = ((k + 15) / 16) * 16;
-  size_t f = (size_t)KM_ROWS * S + (size_t)KP * S + KP + (acc ? (size_t)vrg * k * P + 2 * k : 0) + 4 * KM_ROWS;
+  const size_t sum_f = vrg == 0 ? 2 * (size_t)k * P : (size_t)vrg * k * P;
+  size_t f = (size_t)KM_ROWS * S + (size_t)KP * S + KP + (acc ? sum_f + 2 * k : 0) + 4 * KM_ROWS;
   return f * 4;
 }
 
-// private sum copies per workgroup: every thread busy (256 / vpr row groups)
-// when the LDS allows, else fewer
-static int km_vrg(int k, int P, bool acc) {
+// sums layout: 0 = one 64-bit fixed-point copy (when a scale is given and
+// it fits), else private f32 copies per workgroup -- every thread busy
+// (256 / vpr row groups) when the LDS allows, else fewer
+static int km_vrg(int k, int P, bool acc, float fx_scale) {
+  if (acc && fx_scale > 0.f && km_lds_bytes(0, k, P, acc, 0) <= 96 * 1024) return 0;
   const int vpr = P <= 64 ? 64 : (P <= 128 ? 128 : 256);
   int vrg = KM_THREADS / vpr;
   while (vrg > 1 && km_lds_bytes(0, k, P, acc, vrg) > 96 * 1024) vrg >>= 1;
@@ -296,33 +325,34 @@ static int g_km_dbg = 0;   // microbenchmark phase-skip flags (h2o_kmeans_set_de
 
 template <int KT, int MAXV, bool ACC>
 static int km_launch2(const float* X, const float* w, long long N, int P, const float* C, const float* cn, int k,
-                      int* assign, const int* assign_old, float* dmin, float* part, int G, hipStream_t s) {
-  const int vrg = km_vrg(k, P, ACC);
+                      int* assign, const int* assign_old, float* dmin, float* part, int G, float fx, hipStream_t s) {
+  const int vrg = km_vrg(k, P, ACC, fx);
   const size_t lds = km_lds_bytes(KT, k, P, ACC, vrg);
   auto kern = kmeans_lloyd_kernel<KT, MAXV, ACC>;
   hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(kern, dim3(G), dim3(KM_THREADS), lds, s, X, w, N, P, C, cn, k, assign, assign_old, dmin, part,
-                     vrg, g_km_dbg);
+                     vrg, fx, g_km_dbg);
   H2O_CHECK_LAUNCH();
 }
 
 template <int KT>
 static int km_launch(const float* X, const float* w, long long N, int P, const float* C, const float* cn, int k,
-                     int* assign, const int* assign_old, float* dmin, float* part, int G, int acc, hipStream_t s) {
+                     int* assign, const int* assign_old, float* dmin, float* part, int G, int acc, float fx,
+                     hipStream_t s) {
   // MAXV = float4 per thread per 64-row tile = ceil(P / 16)
-  if (P <= 64) return acc ? km_launch2<KT, 4, true>(X, w, N, P, C, cn, k, assign, assign_old, dmin, part, G, s)
-                          : km_launch2<KT, 4, false>(X, w, N, P, C, cn, k, assign, assign_old, dmin, part, G, s);
-  if (P <= 128) return acc ? km_launch2<KT, 8, true>(X, w, N, P, C, cn, k, assign, assign_old, dmin, part, G, s)
-                           : km_launch2<KT, 8, false>(X, w, N, P, C, cn, k, assign, assign_old, dmin, part, G, s);
-  return acc ? km_launch2<KT, 16, true>(X, w, N, P, C, cn, k, assign, assign_old, dmin, part, G, s)
-             : km_launch2<KT, 16, false>(X, w, N, P, C, cn, k, assign, assign_old, dmin, part, G, s);
+  if (P <= 64) return acc ? km_launch2<KT, 4, true>(X, w, N, P, C, cn, k, assign, assign_old, dmin, part, G, fx, s)
+                          : km_launch2<KT, 4, false>(X, w, N, P, C, cn, k, assign, assign_old, dmin, part, G, fx, s);
+  if (P <= 128) return acc ? km_launch2<KT, 8, true>(X, w, N, P, C, cn, k, assign, assign_old, dmin, part, G, fx, s)
+                           : km_launch2<KT, 8, false>(X, w, N, P, C, cn, k, assign, assign_old, dmin, part, G, fx, s);
+  return acc ? km_launch2<KT, 16, true>(X, w, N, P, C, cn, k, assign, assign_old, dmin, part, G, fx, s)
+             : km_launch2<KT, 16, false>(X, w, N, P, C, cn, k, assign, assign_old, dmin, part, G, fx, s);
 }
 
 template <int KT, int MAXV, bool ACC>
-static int km_resident2(int k, int P) {
+static int km_resident2(int k, int P, float fx) {
   int per_cu = 0;
-  const size_t lds = km_lds_bytes(KT, k, P, ACC, km_vrg(k, P, ACC));
+  const size_t lds = km_lds_bytes(KT, k, P, ACC, km_vrg(k, P, ACC, fx));
   auto kern = kmeans_lloyd_kernel<KT, MAXV, ACC>;
   if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return 0;
@@ -331,10 +361,10 @@ static int km_resident2(int k, int P) {
 }
 
 template <int KT>
-static int km_resident(int k, int P, int acc) {
-  if (P <= 64) return acc ? km_resident2<KT, 4, true>(k, P) : km_resident2<KT, 4, false>(k, P);
-  if (P <= 128) return acc ? km_resident2<KT, 8, true>(k, P) : km_resident2<KT, 8, false>(k, P);
-  return acc ? km_resident2<KT, 16, true>(k, P) : km_resident2<KT, 16, false>(k, P);
+static int km_resident(int k, int P, int acc, float fx) {
+  if (P <= 64) return acc ? km_resident2<KT, 4, true>(k, P, fx) : km_resident2<KT, 4, false>(k, P, fx);
+  if (P <= 128) return acc ? km_resident2<KT, 8, true>(k, P, fx) : km_resident2<KT, 8, false>(k, P, fx);
+  return acc ? km_resident2<KT, 16, true>(k, P, fx) : km_resident2<KT, 16, false>(k, P, fx);
 }
 
 extern "C" {
@@ -344,7 +374,7 @@ int h2o_kmeans_max_k(int P, int acc) {
   if (P <= 0 || P > 256 || (P & 3)) return 0;
   int best = 0;
   for (int k = 16; k <= 256; k += 16) {
-    if (km_lds_bytes(km_kt(k), k, P, acc != 0, km_vrg(k, P, acc != 0)) <= 160 * 1024) best = k;
+    if (km_lds_bytes(km_kt(k), k, P, acc != 0, km_vrg(k, P, acc != 0, 0.f)) <= 160 * 1024) best = k;
   }
   return best;
 }
@@ -358,32 +388,34 @@ void h2o_kmeans_set_debug(int flags) { g_km_dbg = flags; }
 // Workgroups of the Lloyd kernel resident per CU for (k, P, acc): the
 // persistent grid is sized to exactly fill the chip (no tail of late
 // workgroups walking a full share of tiles alone).
-int h2o_kmeans_resident_per_cu(int k, int P, int acc) {
+int h2o_kmeans_resident_per_cu(int k, int P, int acc, float fx_scale) {
   if (P <= 0 || P > 256 || (P & 3) || k <= 0 || k > 256) return 0;
   const int kt = km_kt(k);
-  if (kt <= 1) return km_resident<1>(k, P, acc);
-  if (kt <= 2) return km_resident<2>(k, P, acc);
-  if (kt <= 4) return km_resident<4>(k, P, acc);
-  if (kt <= 8) return km_resident<8>(k, P, acc);
-  return km_resident<16>(k, P, acc);
+  if (kt <= 1) return km_resident<1>(k, P, acc, fx_scale);
+  if (kt <= 2) return km_resident<2>(k, P, acc, fx_scale);
+  if (kt <= 4) return km_resident<4>(k, P, acc, fx_scale);
+  if (kt <= 8) return km_resident<8>(k, P, acc, fx_scale);
+  return km_resident<16>(k, P, acc, fx_scale);
 }
 
 // One Lloyd pass.  X [N, P] f32 row-major (P % 4 == 0, P <= 256), C [k, P]
-// f32, cn [k] = |c|^2.  acc=1: per-workgroup partials into part
+// f32, cn [k] = |c|^2.  fx_scale > 0: per-cluster sums as 64-bit fixed point
+// x * fx_scale (the caller bounds sum |w x| * fx_scale < 2^62 per workgroup).  acc=1: per-workgroup partials into part
 // [G, km_part_stride] (then h2o_kmeans_reduce); acc=0: assignment only.
 // assign / assign_old / dmin / w may be null.  Returns a hipError_t.
 int h2o_kmeans_lloyd(const float* X, const float* w, long long N, int P, const float* C, const float* cn, int k,
-                     int* assign, const int* assign_old, float* dmin, float* part, int G, int acc, hipStream_t s) {
+                     int* assign, const int* assign_old, float* dmin, float* part, int G, int acc, float fx_scale,
+                     hipStream_t s) {
   if (N <= 0) return 0;
   if (P <= 0 || P > 256 || (P & 3) || k <= 0 || k > 256 || G <= 0) return (int)hipErrorInvalidValue;
   const int kt = km_kt(k);
-  if (km_lds_bytes(kt, k, P, acc != 0, km_vrg(k, P, acc != 0)) > 160 * 1024) return (int)hipErrorInvalidValue;
+  if (km_lds_bytes(kt, k, P, acc != 0, km_vrg(k, P, acc != 0, fx_scale)) > 160 * 1024) return (int)hipErrorInvalidValue;
   if (acc && !part) return (int)hipErrorInvalidValue;
-  if (kt <= 1) return km_launch<1>(X, w, N, P, C, cn, k, assign, assign_old, dmin, part, G, acc, s);
-  if (kt <= 2) return km_launch<2>(X, w, N, P, C, cn, k, assign, assign_old, dmin, part, G, acc, s);
-  if (kt <= 4) return km_launch<4>(X, w, N, P, C, cn, k, assign, assign_old, dmin, part, G, acc, s);
-  if (kt <= 8) return km_launch<8>(X, w, N, P, C, cn, k, assign, assign_old, dmin, part, G, acc, s);
-  return km_launch<16>(X, w, N, P, C, cn, k, assign, assign_old, dmin, part, G, acc, s);
+  if (kt <= 1) return km_launch<1>(X, w, N, P, C, cn, k, assign, assign_old, dmin, part, G, acc, fx_scale, s);
+  if (kt <= 2) return km_launch<2>(X, w, N, P, C, cn, k, assign, assign_old, dmin, part, G, acc, fx_scale, s);
+  if (kt <= 4) return km_launch<4>(X, w, N, P, C, cn, k, assign, assign_old, dmin, part, G, acc, fx_scale, s);
+  if (kt <= 8) return km_launch<8>(X, w, N, P, C, cn, k, assign, assign_old, dmin, part, G, acc, fx_scale, s);
+  return km_launch<16>(X, w, N, P, C, cn, k, assign, assign_old, dmin, part, G, acc, fx_scale, s);
 }
 
 int h2o_kmeans_reduce(const float* part, int G, long long stride, double* out, hipStream_t s) {

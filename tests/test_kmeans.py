@@ -187,9 +187,10 @@ if cloud.rank() == 0:
 
 # ---------------------------------------------------------------- GPU kernel
 @pytest.mark.gpu
+@pytest.mark.parametrize("fx", [False, True])
 @pytest.mark.parametrize("N,P,k", [(100_003, 12, 5), (70_001, 100, 40), (33_333, 256, 16), (20_000, 36, 130),
                                    (65, 4, 1)])
-def test_lloyd_kernel_matches_f64_reference(N, P, k):
+def test_lloyd_kernel_matches_f64_reference(N, P, k, fx):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from h2o3_amd.ops import _native
@@ -201,7 +202,8 @@ def test_lloyd_kernel_matches_f64_reference(N, P, k):
     a = torch.full((N,), -1, dtype=torch.int32, device="cuda")
     dmin = torch.empty(N, dtype=torch.float32, device="cuda")
     assert cluster_ops.native_ok(X, k)
-    st = cluster_ops.lloyd_pass(X, C, w, a, dmin=dmin)
+    xa = cluster_ops.abs_bound(X, w) if fx else None
+    st = cluster_ops.lloyd_pass(X, C, w, a, dmin=dmin, xabs_max=xa)
     assert "libkmeans.so" in " ".join(_native.loaded_libs())
     torch.cuda.synchronize()
     Xd = X.double()
@@ -225,7 +227,7 @@ def test_lloyd_kernel_matches_f64_reference(N, P, k):
     torch.testing.assert_close(dmin.double(), dsel, rtol=1e-4, atol=1e-3 * P)
     torch.testing.assert_close(st.withinss, (oh * dsel.view(-1, 1)).sum(0), rtol=1e-4, atol=1e-2 * P)
     # second pass from the same centers: nothing changes
-    st2 = cluster_ops.lloyd_pass(X, C, w, a)
+    st2 = cluster_ops.lloyd_pass(X, C, w, a, xabs_max=xa)
     assert float(st2.changed) == 0
     # assignment-only mode agrees
     a2 = torch.empty(N, dtype=torch.int32, device="cuda")
