@@ -269,20 +269,38 @@ def __getattr__(name):
 
 
 def explain(models, frame, columns=None, top_n_features=5, include_explanations="ALL", exclude_explanations=(),
-            **kw):
-    """h2o.explain(): returns the explanation tables (no plotting stack here)."""
+            plot=False, render=None, **kw):
+    """h2o.explain(): explanation tables per section, plus matplotlib
+    figures under out["plots"] with plot=True (render=True is an alias)."""
     from .models.explain import explain as _ex
     if hasattr(models, "leaderboard") and not isinstance(models, (list, tuple)):
         models = list(models._models) if hasattr(models, "_models") else [models.leader]
     return _ex(models, frame, columns=columns, top_n_features=top_n_features,
-               include_explanations=include_explanations, exclude_explanations=exclude_explanations)
+               include_explanations=include_explanations, exclude_explanations=exclude_explanations,
+               plot=bool(plot or render))
 
 
-def explain_row(models, frame, row_index, columns=None, top_n_features=5, **kw):
+def explain_row(models, frame, row_index, columns=None, top_n_features=5, plot=False, render=None, **kw):
     from .models.explain import explain_row as _er
     if hasattr(models, "leader") and not isinstance(models, (list, tuple)):
         models = [models.leader]
-    return _er(models, frame, row_index, columns=columns, top_n_features=top_n_features)
+    return _er(models, frame, row_index, columns=columns, top_n_features=top_n_features, plot=bool(plot or render))
+
+
+def _xp(name):
+    def f(*a, **k):
+        from .models import explain_plots
+        return getattr(explain_plots, name)(*a, **k)
+    f.__name__ = name
+    f.__doc__ = f"h2o.{name} (h2o-py/h2o/explanation/_explain.py); see models/explain_plots.py"
+    return f
+
+
+varimp_heatmap = _xp("varimp_heatmap")
+model_correlation_heatmap = _xp("model_correlation_heatmap")
+model_correlation = _xp("model_correlation")
+pd_multi_plot = _xp("pd_multi_plot")
+varimp = _xp("varimp")
 
 
 def permutation_importance(model, frame, metric="AUTO", n_samples=10000, n_repeats=1, features=None, seed=-1,

@@ -636,6 +636,39 @@ class H2OEstimator:
         df = pd.DataFrame({variable: list(v.domain) + [None], predicted.names[0]: res[0], "actual": res[1]})
         return df.set_index(variable) if use_pandas else df
 
+    # ---- explanation plots (h2o-py ModelBase.pd_plot / ice_plot / shap_* / ...)
+    def pd_plot(self, frame, column, **kw):
+        from .explain_plots import pd_plot
+        return pd_plot(self, frame, column, **kw)
+
+    def ice_plot(self, frame, column, **kw):
+        from .explain_plots import ice_plot
+        return ice_plot(self, frame, column, **kw)
+
+    def shap_summary_plot(self, frame, **kw):
+        from .explain_plots import shap_summary_plot
+        return shap_summary_plot(self, frame, **kw)
+
+    def shap_explain_row_plot(self, frame, row_index, **kw):
+        from .explain_plots import shap_explain_row_plot
+        return shap_explain_row_plot(self, frame, row_index, **kw)
+
+    def residual_analysis_plot(self, frame, **kw):
+        from .explain_plots import residual_analysis_plot
+        return residual_analysis_plot(self, frame, **kw)
+
+    def learning_curve_plot(self, metric="AUTO", **kw):
+        from .explain_plots import learning_curve_plot
+        return learning_curve_plot(self, metric, **kw)
+
+    def explain(self, frame, **kw):
+        from .explain import explain
+        return explain([self], frame, **kw)
+
+    def explain_row(self, frame, row_index, **kw):
+        from .explain import explain_row
+        return explain_row([self], frame, row_index, **kw)
+
     def _plot_or_data(self, kind, data, server=False):
         """Plots need matplotlib; without it (this image) the plot's data is
         returned so callers still get the numbers."""

@@ -10,9 +10,9 @@ permuted, n_repeats, n_samples), hex/tree/FriedmanPopescusH.java
 residual analysis, leaderboard).
 
 Everything here is built from the model's batched device predict(): one
-scoring pass per grid point / permutation, no per-row host work.  Plots
-are not produced (no plotting stack in this build); every function returns
-the tables the reference plots.
+scoring pass per grid point / permutation, no per-row host work.  explain()
+returns the tables the reference plots and, with plot=True, the matplotlib
+figures too (models/explain_plots.py).
 """
 from __future__ import annotations
 
@@ -219,12 +219,18 @@ def h_statistic(model, frame: H2OFrame, variables, max_rows=200, seed=0):
 
 # ------------------------------------------------------------------ explain()
 def explain(models, frame: H2OFrame, columns=None, top_n_features=5, include_explanations="ALL",
-            exclude_explanations=(), **kw):
-    """Data behind h2o.explain(): dict of tables keyed like the reference's
-    explanation sections."""
+            exclude_explanations=(), plot=False, **kw):
+    """h2o.explain(): dict of tables keyed like the reference's explanation
+    sections; plot=True adds out["plots"][section] figures (varimp heatmap,
+    model correlation, SHAP summary, PD / PD-multi, ICE, residual analysis,
+    learning curve)."""
     if not isinstance(models, (list, tuple)):
         models = [models]
     ex = set(exclude_explanations or ())
+    if include_explanations not in (None, "ALL"):
+        inc = {include_explanations} if isinstance(include_explanations, str) else set(include_explanations)
+        ex |= {"leaderboard", "varimp", "pdp", "shap_summary", "residual_analysis", "confusion_matrix", "ice",
+               "varimp_heatmap", "model_correlation_heatmap", "learning_curve"} - inc
     out = {}
     m0 = models[0]
     if len(models) > 1 and "leaderboard" not in ex:
@@ -257,17 +263,51 @@ def explain(models, frame: H2OFrame, columns=None, top_n_features=5, include_exp
         out["residual_analysis"] = pd.DataFrame({"fitted": p, "residual": y - p})
     if "confusion_matrix" not in ex and m0._spec.nclasses >= 2:
         out["confusion_matrix"] = m0.model_performance(frame).confusion_matrix()
+    if plot:
+        from . import explain_plots as xp
+        figs = {}
+        if len(models) > 1:
+            if "varimp_heatmap" not in ex:
+                try:
+                    figs["varimp_heatmap"] = xp.varimp_heatmap(models)
+                except RuntimeError:
+                    pass
+            if "model_correlation_heatmap" not in ex:
+                figs["model_correlation_heatmap"] = xp.model_correlation_heatmap(models, frame)
+            if "pdp" not in ex:
+                figs["pdp"] = {c: xp.pd_multi_plot(models, frame, c) for c in cols}
+        else:
+            if "varimp" not in ex and out.get("varimp"):
+                figs["varimp"] = m0.varimp_plot(server=True)
+            if "pdp" not in ex:
+                figs["pdp"] = {c: xp.pd_plot(m0, frame, c) for c in cols}
+            if "ice" not in ex:
+                figs["ice"] = {c: xp.ice_plot(m0, frame, c) for c in cols}
+        if "shap_summary" in out:
+            figs["shap_summary"] = xp.shap_summary_plot(m0, frame)
+        if "residual_analysis" in out:
+            figs["residual_analysis"] = xp.residual_analysis_plot(m0, frame)
+        if "learning_curve" not in ex:
+            figs["learning_curve"] = xp.learning_curve_plot(m0)
+        out["plots"] = figs
     return out
 
 
-def explain_row(models, frame: H2OFrame, row_index, columns=None, top_n_features=5, **kw):
+def explain_row(models, frame: H2OFrame, row_index, columns=None, top_n_features=5, plot=False, **kw):
     if not isinstance(models, (list, tuple)):
         models = [models]
     m0 = models[0]
     row = frame[int(row_index), :]
     out = {}
-    if m0.algo in ("gbm", "drf", "xgboost") and m0._spec.nclasses <= 2:
+    shap = m0.algo in ("gbm", "drf", "xgboost") and m0._spec.nclasses <= 2
+    if shap:
         out["shap_explain_row"] = m0.predict_contributions(row).as_data_frame()
     cols = columns or list(m0._spec.x)[:top_n_features]
     out["ice"] = {c: partial_dependence(m0, frame, c, row_index=row_index)[0] for c in cols}
+    if plot:
+        from . import explain_plots as xp
+        figs = {"ice": {c: xp.pd_plot(m0, frame, c, row_index=row_index) for c in cols}}
+        if shap:
+            figs["shap_explain_row"] = xp.shap_explain_row_plot(m0, frame, row_index)
+        out["plots"] = figs
     return out

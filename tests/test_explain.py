@@ -60,3 +60,38 @@ def test_explain_tables():
     assert len(ex["pdp"]) == 2
     er = h2o.explain_row(m, fr, 3)
     assert "shap_explain_row" in er
+
+
+def test_explain_plots_and_heatmaps(tmp_path):
+    """explain(plot=True) draws every section (matplotlib Agg); heatmap data
+    follows the reference's varimp / model_correlation definitions."""
+    import matplotlib
+    matplotlib.use("Agg")
+    from h2o3_amd.models import explain_plots as xp
+    h2o.init()
+    fr = _fr()
+    x = list("abcd") + ["k"]
+    m1 = H2OGradientBoostingEstimator(ntrees=10, max_depth=3, seed=1)
+    m1.train(x=x, y="y", training_frame=fr)
+    m2 = H2OGradientBoostingEstimator(ntrees=5, max_depth=2, seed=2)
+    m2.train(x=x, y="y", training_frame=fr)
+    m3 = H2OGradientBoostingEstimator(ntrees=8, max_depth=4, seed=3)
+    m3.train(x=x, y="y", training_frame=fr)
+    ex = h2o.explain(m1, fr, top_n_features=2, plot=True)
+    figs = ex["plots"]
+    assert {"pdp", "ice", "shap_summary", "learning_curve"} <= set(figs)
+    for f in list(figs["pdp"].values()) + [figs["shap_summary"], figs["learning_curve"]]:
+        assert hasattr(f, "savefig")
+    figs["shap_summary"].savefig(tmp_path / "shap.png")
+    assert (tmp_path / "shap.png").stat().st_size > 1000
+    vi = xp.varimp([m1, m2, m3])
+    assert set(vi.columns) == {m1.model_id, m2.model_id, m3.model_id}
+    assert np.allclose(vi.max(0).values, 1.0)      # each model scaled to its top variable
+    mc = xp.model_correlation([m1, m2, m3], fr)
+    assert np.allclose(np.diag(mc.values), 1.0) and (mc.values <= 1 + 1e-9).all()
+    exm = h2o.explain([m1, m2, m3], fr, top_n_features=1, plot=True)
+    assert "varimp_heatmap" in exm["plots"] and "model_correlation_heatmap" in exm["plots"]
+    er = m1.explain_row(fr, 2, plot=True)
+    assert hasattr(er["plots"]["shap_explain_row"], "savefig")
+    import matplotlib.pyplot as plt
+    plt.close("all")
