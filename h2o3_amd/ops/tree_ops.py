@@ -201,7 +201,25 @@ def _pack_scale(vmax, chunk):
     return s1, int(math.ceil(vm * s1))
 
 
-def hist_build(bd, ridx, va, vb, mode, starts, counts, n_slots, use_native=None, target_blocks=2048, vmax=None,
+# Rows per histogram workgroup: every workgroup zeroes and flushes a full
+# feature-group histogram (fixed cost), so chunks aim at ~64K rows while
+# keeping >= 512 workgroups to fill the chip (scripts/hist_tb_mb.py: 12.5M rows
+# root 0.90 -> 0.76 ms, 100M rows 5.05 -> 4.93 ms vs a fixed 2048 workgroups).
+_HIST_CHUNK_ROWS = 65536
+_HIST_MIN_BLOCKS = 512
+
+
+def hist_chunk(total, n_fg, target_blocks=None):
+    """Rows per work item for `total` rows over n_fg feature groups."""
+    tb = os.environ.get("H2O3_HIST_TB", target_blocks)
+    if tb is not None:
+        n_chunks = max(1, int(tb) // n_fg)
+    else:
+        n_chunks = max(-(-_HIST_MIN_BLOCKS // n_fg), -(-total // _HIST_CHUNK_ROWS))
+    return max(2048, -(-total // n_chunks))
+
+
+def hist_build(bd, ridx, va, vb, mode, starts, counts, n_slots, use_native=None, target_blocks=None, vmax=None,
                want_wyy=False, posv=False, unit_w=False, need_mask=None):
     """Histograms of the row segments [starts[i], starts[i]+counts[i]) of
     ridx into slot i.  Returns hist [F, n_slots, Bs, C] float64 (and, with
@@ -239,8 +257,7 @@ def hist_build(bd, ridx, va, vb, mode, starts, counts, n_slots, use_native=None,
         else:
             FG = feature_group(bd.F, bd.Bs, mode)
             n_fg = (bd.F + FG - 1) // FG
-        tgt_chunks = max(1, target_blocks // n_fg)
-        chunk = max(2048, -(-total // tgt_chunks))
+        chunk = hist_chunk(total, n_fg, target_blocks)
         if pack and chunk >= (1 << 23):
             pack = False
             n_fg, fgw = quad_groups(bd.F, bd.Fp, bd.Bs, False, qbudget)
@@ -481,7 +498,7 @@ def partition_async(bd, ridx, ridx_out, feat_d, masks, starts, counts, chunk=163
 
 
 def hist_build_dev(bd, ridx, va, vb, mode, rec, rec_cols, starts, counts, vmax, posv=False, unit_w=False,
-                   target_blocks=2048):
+                   target_blocks=None):
     """Next-level histograms of the lighter child of every splitting node,
     with the work list built ON THE DEVICE from the level's split record
     (child_work_kernel): launched right after the partition, before the host
@@ -510,7 +527,7 @@ def hist_build_dev(bd, ridx, va, vb, mode, rec, rec_cols, starts, counts, vmax, 
     pack = mode == 0 and unit_w and os.environ.get("H2O3_HIST_PACK", "1") == "1"
     n_fg, fgw = quad_groups(bd.F, bd.Fp, bd.Bs, pack)
     total = int(sum(counts))
-    chunk = max(2048, -(-((total + 1) // 2) // max(1, target_blocks // n_fg)))
+    chunk = hist_chunk((total + 1) // 2, n_fg, target_blocks)   # the lighter children: <= half the rows
     if pack and chunk >= (1 << 23):
         pack = False
         n_fg, fgw = quad_groups(bd.F, bd.Fp, bd.Bs, False)
