@@ -30,7 +30,16 @@ from .glm import H2OGeneralizedLinearEstimator
 
 ANOVA_DEFAULTS = dict(family="AUTO", link="family_default", highest_interaction_term=2, type=3, lambda_=0.0,
                       alpha=0.0, standardize=True, compute_p_values=True, save_transformed_framekeys=False,
-                      nparallelism=4, seed=-1, max_iterations=0, early_stopping=False)
+                      nparallelism=4, seed=-1, max_iterations=0, early_stopping=False,
+                      # GLM parameters forwarded to every inner GLM (anovaglm.py in h2o-py)
+                      tweedie_variance_power=0.0, tweedie_link_power=1.0, theta=1e-10, solver="AUTO",
+                      missing_values_handling="MeanImputation", plug_values=None, non_negative=False, prior=-1.0,
+                      lambda_search=False, balance_classes=False, class_sampling_factors=None,
+                      max_after_balance_size=5.0)
+
+_GLM_PASS = ("tweedie_variance_power", "tweedie_link_power", "theta", "solver", "missing_values_handling",
+             "plug_values", "non_negative", "prior", "lambda_search", "balance_classes", "class_sampling_factors",
+             "max_after_balance_size", "max_iterations", "early_stopping", "seed")
 
 
 class H2OANOVAGLMEstimator(H2OEstimator):
@@ -85,9 +94,12 @@ class H2OANOVAGLMEstimator(H2OEstimator):
         fam = p.get("family") or "AUTO"
 
         def glm(xs):
+            fw = {k: p[k] for k in _GLM_PASS if k in p}
+            if not fw.get("max_iterations"):
+                fw.pop("max_iterations", None)
             m = H2OGeneralizedLinearEstimator(family=fam, link=p.get("link"), lambda_=p.get("lambda_", 0.0),
                                               alpha=p.get("alpha", 0.0), standardize=p.get("standardize", True),
-                                              compute_p_values=False)
+                                              compute_p_values=False, **fw)
             m.train(x=xs, y=self._y, training_frame=tf, weights_column=self._w)
             return m
 

@@ -53,7 +53,7 @@ GLM_DEFAULTS = dict(family="AUTO", tweedie_variance_power=0.0, dispersion_learni
                     fix_dispersion_parameter=False, generate_variable_inflation_factors=False,
                     fix_tweedie_variance_power=True, HGLM=False, random_columns=None, rand_family=None,
                     rand_link=None, gainslift_bins=-1, linear_constraints=None, influence=None,
-                    score_iteration_interval=-1, seed=-1)
+                    score_iteration_interval=-1, seed=-1, checkpoint=None)
 
 _DEFAULT_LINK = {"gaussian": "identity", "binomial": "logit", "quasibinomial": "logit",
                  "fractionalbinomial": "logit", "poisson": "log", "gamma": "inverse", "tweedie": "tweedie",
@@ -319,6 +319,13 @@ class GLMDriver:
         self._init_beta = self.beta.copy()
         self._setup_constraints(p.get("beta_constraints"))
         sv = p.get("startval")
+        ck = p.get("checkpoint")
+        if ck is not None and sv is None:
+            # checkpoint: continue from a previous model's coefficients (GLM.java
+            # restarts the solver from the checkpointed model's beta)
+            from ...core import dkv
+            prev = dkv.get(ck) if isinstance(ck, str) else ck
+            sv = prev.coef()
         if sv is not None:
             self._set_startval(sv)
         self.active = None     # collinear-column mask (remove_collinear_columns)

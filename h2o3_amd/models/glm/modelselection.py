@@ -35,7 +35,21 @@ from .glm import H2OGeneralizedLinearEstimator
 MS_DEFAULTS = dict(mode="maxr", max_predictor_number=1, min_predictor_number=1, p_values_threshold=0.0,
                    family="AUTO", link="family_default", lambda_=0.0, alpha=0.0, standardize=True,
                    intercept=True, nparallelism=0, build_glm_model=True, influence=None, seed=-1,
-                   compute_p_values=True, max_iterations=0)
+                   compute_p_values=True, max_iterations=0,
+                   # GLM parameters forwarded to the inner GLMs (model_selection.py in h2o-py)
+                   score_iteration_interval=-1, tweedie_variance_power=0.0, tweedie_link_power=1.0, theta=1e-10,
+                   solver="AUTO", lambda_search=False, early_stopping=True, nlambdas=-1,
+                   missing_values_handling="MeanImputation", plug_values=None, remove_collinear_columns=False,
+                   non_negative=False, objective_epsilon=-1.0, beta_epsilon=1e-4, gradient_epsilon=-1.0,
+                   startval=None, prior=-1.0, cold_start=False, lambda_min_ratio=-1.0, beta_constraints=None,
+                   max_active_predictors=-1, obj_reg=-1.0, balance_classes=False, class_sampling_factors=None,
+                   max_after_balance_size=5.0, max_confusion_matrix_size=20)
+
+_GLM_PASS = ("score_iteration_interval", "tweedie_variance_power", "tweedie_link_power", "theta", "solver",
+             "lambda_search", "early_stopping", "nlambdas", "missing_values_handling", "plug_values",
+             "remove_collinear_columns", "non_negative", "objective_epsilon", "beta_epsilon", "gradient_epsilon",
+             "prior", "cold_start", "lambda_min_ratio", "beta_constraints", "max_active_predictors", "obj_reg",
+             "balance_classes", "class_sampling_factors", "max_after_balance_size", "seed")
 
 
 class H2OModelSelectionEstimator(H2OEstimator):
@@ -109,10 +123,13 @@ class H2OModelSelectionEstimator(H2OEstimator):
 
     def _glm(self, spec, preds):
         p = self._parms
+        fw = {k: p[k] for k in _GLM_PASS if k in p}
+        if int(p.get("max_iterations") or 0) > 0:
+            fw["max_iterations"] = int(p["max_iterations"])
         m = H2OGeneralizedLinearEstimator(family=p.get("family") or "AUTO", link=p.get("link"),
                                           lambda_=p.get("lambda_", 0.0), alpha=p.get("alpha", 0.0),
                                           standardize=p.get("standardize", True), intercept=p.get("intercept", True),
-                                          compute_p_values=True)
+                                          compute_p_values=True, **fw)
         m.train(x=list(preds), y=spec.y, training_frame=spec.frame, weights_column=spec.weights_column)
         return m
 

@@ -35,7 +35,8 @@ GLRM_DEFAULTS = dict(k=1, loss="Quadratic", loss_by_col=None, loss_by_col_idx=No
                      period=1, regularization_x="None", regularization_y="None", gamma_x=0.0, gamma_y=0.0,
                      max_iterations=1000, max_updates=2000, init_step_size=1.0, min_step_size=1e-4, seed=-1,
                      init="PlusPlus", svd_method="Randomized", user_y=None, user_x=None, expand_user_y=True,
-                     impute_original=False, recover_svd=False, transform="NONE", representation_name=None)
+                     impute_original=False, recover_svd=False, transform="NONE", representation_name=None,
+                     loading_name=None)
 
 
 def _num_loss(name, a, u, period):
@@ -282,7 +283,8 @@ class H2OGeneralizedLowRankEstimator(H2OEstimator):
         o["step_size"] = step
         o["archetypes"] = self._archetypes_df()
         o["scoring_history"] = hist
-        rep = p.get("representation_name") or f"GLRMLoading_{self.model_id}"
+        # loading_name: the reference's deprecated alias of representation_name
+        rep = p.get("representation_name") or p.get("loading_name") or f"GLRMLoading_{self.model_id}"
         self._rep_name = rep
         if p.get("recover_svd"):
             Q, R = torch.linalg.qr(X.double())

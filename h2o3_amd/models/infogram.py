@@ -31,7 +31,16 @@ from .base import H2OEstimator
 
 INFOGRAM_DEFAULTS = dict(algorithm="AUTO", algorithm_params=None, protected_columns=None, total_information_threshold=-1.0,
                          net_information_threshold=-1.0, relevance_index_threshold=-1.0, safety_index_threshold=-1.0,
-                         data_fraction=1.0, top_n_features=50, seed=-1)
+                         data_fraction=1.0, top_n_features=50, seed=-1,
+                         # forwarded to the infogram's models when the algorithm takes them
+                         standardize=True, plug_values=None, max_iterations=0, balance_classes=False,
+                         class_sampling_factors=None, max_after_balance_size=5.0)
+
+_FORWARD = {"glm": ("standardize", "plug_values", "max_iterations", "balance_classes", "class_sampling_factors",
+                    "max_after_balance_size"),
+            "deeplearning": ("standardize", "balance_classes", "class_sampling_factors", "max_after_balance_size"),
+            "gbm": ("balance_classes", "class_sampling_factors", "max_after_balance_size"),
+            "drf": ("balance_classes", "class_sampling_factors", "max_after_balance_size")}
 
 
 class H2OInfogram(H2OEstimator):
@@ -48,6 +57,11 @@ class H2OInfogram(H2OEstimator):
         kw = dict(p.get("algorithm_params") or {})
         if p.get("seed", -1) not in (-1, None):
             kw.setdefault("seed", p["seed"])
+        for k in _FORWARD.get("gbm" if algo == "auto" else algo, ()):
+            if k == "max_iterations" and not p.get(k):
+                continue
+            if p.get(k) is not None:
+                kw.setdefault(k, p[k])
         cls = {"auto": H2OGradientBoostingEstimator, "gbm": H2OGradientBoostingEstimator,
                "drf": H2ORandomForestEstimator, "glm": H2OGeneralizedLinearEstimator,
                "deeplearning": H2ODeepLearningEstimator}[algo]

@@ -36,7 +36,7 @@ UPLIFT_DEFAULTS = dict(ntrees=50, max_depth=20, min_rows=1.0, nbins=20, nbins_to
                        col_sample_rate_change_per_level=1.0, histogram_type="auto", categorical_encoding="auto",
                        distribution="bernoulli", treatment_column="treatment", uplift_metric="AUTO",
                        auuc_type="AUTO", auuc_nbins=-1, score_tree_interval=0, check_constant_response=True,
-                       custom_metric_func=None, stopping_rounds=0)
+                       custom_metric_func=None, stopping_rounds=0, sample_rate_per_class=None)
 
 
 def auuc_metrics(uplift: torch.Tensor, y: torch.Tensor, treat: torch.Tensor, nbins=1000, auuc_type="qini"):
@@ -165,8 +165,14 @@ class H2OUpliftRandomForestEstimator(SharedTreeEstimator):
         gen.manual_seed(self._seed() + cloud.rank())
         forest = Forest()
         sr = float(p["sample_rate"])
+        srpc = p.get("sample_rate_per_class")
+        if srpc is not None:
+            # per-class row sampling rates (SharedTree sample_rate_per_class)
+            ycls = y.clamp(min=0).long()
+            sr_row = torch.tensor([float(r) for r in srpc], dtype=torch.float32, device=dev)[ycls]
         for t in range(int(p["ntrees"])):
-            inbag = torch.rand(N, generator=gen, device=dev) < sr
+            u = torch.rand(N, generator=gen, device=dev)
+            inbag = u < (sr_row if srpc is not None else sr)
             wt = (base_w * inbag * T).contiguous()
             wc = (base_w * inbag * (1 - T)).contiguous()
             tree, nid, leaves, tot = grower.grow(y.contiguous(), (wt, wc), 3)
