@@ -69,7 +69,9 @@ def main():
     ap.add_argument("--rows", type=int, default=100_000_000)
     ap.add_argument("--cols", type=int, default=100)
     ap.add_argument("--max-depth", type=int, default=8)
-    ap.add_argument("--algo", default="gbm", choices=["gbm", "glm", "drf", "kmeans"])
+    ap.add_argument("--algo", default="gbm", choices=["gbm", "glm", "drf", "kmeans", "dl"])
+    ap.add_argument("--hidden", default="200,200", help="DL hidden layers (--algo dl)")
+    ap.add_argument("--batch", type=int, default=1024, help="DL mini-batch rows (--algo dl)")
     ap.add_argument("--k", type=int, default=16, help="K-Means clusters (--algo kmeans)")
     ap.add_argument("--cat-cols", type=int, default=0,
                     help="replace this many of the --cols columns by categoricals (DRF config: mixed num/cat)")
@@ -141,6 +143,37 @@ def main():
         unit = "iters/s"
         model = f"KMeans k={args.k} {args.rows / 1e6:g}Mx{F}"
         extra_cfg = {"distance_precision": "f32 MFMA (v_mfma_f32_16x16x4_f32), f64 cross-workgroup sums"}
+    elif args.algo == "dl":
+        # one step = one mini-batch training step of the MLP (forward, backward,
+        # per-row ADADELTA update); value = training samples / s
+        from h2o3_amd.models.deeplearning import H2ODeepLearningEstimator
+        from h2o3_amd.models.datainfo import DataInfo
+        hidden = [int(h) for h in args.hidden.split(",")]
+        est = H2ODeepLearningEstimator(hidden=hidden, activation="RectifierWithDropout", seed=42,
+                                       input_dropout_ratio=0.1)
+        est._dinfo = DataInfo(fr, names, standardize=True, use_all_factor_levels=True, pad_to=0)
+        Xd, _ = est._dinfo.expand(fr, pad=False)
+        Yd = y.long()
+        del fr
+        est._layers = est._build(Xd.shape[1], 2, True)
+        est._processed = 0.0
+        hp = dict(K=2, ae=False, bs=args.batch, ada=True, rate0=0.005, anneal=1e-6, decay=1.0, mom_start=0.0,
+                  mom_ramp=1e6, mom_stable=0.0, has_mom=False, l1=0.0, l2=0.0, max_w2=3.4e38, sparsity=0.0)
+        gdl = torch.Generator(device=dev).manual_seed(7)
+        nloc = Xd.shape[0]
+        gstep = est._step_graph(Xd, Yd, None, hp, None) if est._graph_ok(Xd, hp, None) else None
+
+        def step():
+            idx = torch.randint(0, nloc, (args.batch,), generator=gdl, device=dev)
+            if gstep is not None:
+                gstep["idx"].copy_(idx)
+                gstep["g"].replay()
+            else:
+                est._train_step(Xd.index_select(0, idx), Yd.index_select(0, idx), None, 1000, hp)
+        metric = "dl_samples_per_sec"
+        unit = "samples/s"
+        model = f"DeepLearning MLP {args.cols}-{args.hidden}-2 RectifierWithDropout, batch {args.batch}"
+        extra_cfg = {"hidden": hidden, "batch": args.batch, "hip_graph": gstep is not None}
     else:
         from h2o3_amd.models.glm.glm import GLMDriver, H2OGeneralizedLinearEstimator
         est = H2OGeneralizedLinearEstimator(family="binomial", solver="IRLSM", lambda_=0.0)
@@ -172,6 +205,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     value = args.steps / el
+    if args.algo == "dl":
+        value = args.steps * args.batch * world / el
     extra = {}
     if args.algo == "gbm":
         # training-quality sanity (not timed): logloss of the boosted model so far
@@ -195,7 +230,7 @@ def main():
                "scaling": "strong", "vs_baseline": None, "dtype": "fp32",
                "data": "synthetic (random normal features, logistic label), generated on device",
                "config": {"model": model, "rows": args.rows, "cols": F,
-                          **({} if args.algo in ("glm", "kmeans") else {"max_depth": est._parms.get("max_depth"),
+                          **({} if args.algo in ("glm", "kmeans", "dl") else {"max_depth": est._parms.get("max_depth"),
                                                             "histogram_type": args.histogram_type,
                                                             "nbins": args.nbins}),
                           "global_batch": args.rows, "seq_len": None, "parallelism": f"dp{world}", **extra_cfg},

@@ -167,19 +167,21 @@ class H2ODeepLearningEstimator(H2OEstimator):
         cols = [fr.vec(c).as_float(torch.float32) for c in fr.names]
         return torch.stack(cols, 1).cpu()
 
-    def _forward(self, X, train, seed=0, keep=None):
-        """Returns (activations list [A_0 = input, ...], pre-activations list,
-        output probabilities / values).  keep: (in_mask) for input dropout."""
+    def _forward(self, X, train, seed=0, seed_dev=None):
+        """Returns (activations list [A_0 = input, ...], pre-activations list).
+        Dropout masks hash (seed + per-layer offset [+ *seed_dev])."""
         p = self._parms
         A = X
         ratio_in = float(p.get("input_dropout_ratio") or 0.0)
         if train and ratio_in > 0:
-            A = X * dl_ops.keep_mask(seed ^ 0x5bd1e995, X.shape[0], X.shape[1], ratio_in, X.device)
+            # input dropout: the forward kernel with a linear activation and no bias
+            A = dl_ops.fwd(X.clone(), None, "linear", ratio_in, seed=seed + 0x5bd1e995, train=True,
+                           seed_dev=seed_dev)
         acts, zs = [A], []
         for li, L in enumerate(self._layers[:-1]):
             Z = A @ L.W.t()
             Ah = dl_ops.fwd(Z, L.b, L.act, L.drop, seed=seed + 7919 * (li + 1), train=train,
-                            test_scale=1.0 - L.drop)
+                            test_scale=1.0 - L.drop, seed_dev=seed_dev)
             zs.append(Z)
             acts.append(Ah)
             A = Ah
@@ -320,59 +322,33 @@ class H2ODeepLearningEstimator(H2OEstimator):
         if smetric == "auto":
             smetric = "logloss" if K > 1 else ("mse" if ae else "deviance")
         history, best = [], None
+        hp = dict(K=K, ae=ae, bs=bs, ada=ada, rate0=rate0, anneal=anneal, decay=decay, mom_start=mom_start,
+                  mom_ramp=mom_ramp, mom_stable=mom_stable, has_mom=has_mom, l1=l1, l2=l2, max_w2=max_w2,
+                  sparsity=sparsity)
         step_seed = self._seed() * 1000003
         perm, pos = None, n
         samples_done = 0.0
         next_score = per_iter
         it = 0
+        graph = self._step_graph(X, Y, w, hp, avg_act) if self._graph_ok(X, hp, avg_act) else None
         while samples_done < total_samples:
             if pos + bs > n:
                 perm = torch.randperm(n, generator=gen, device=X.device)
                 pos = 0
             idx = perm[pos:pos + bs]
             pos += bs
-            xb = X.index_select(0, idx)
-            yb = None if Y is None else Y.index_select(0, idx)
-            wb = None if w is None else w.index_select(0, idx)
-            step_seed = (step_seed * 6364136223846793005 + 1442695040888963407) & ((1 << 63) - 1)
-            acts, zs = self._forward(xb, True, step_seed)
-            dZ, _ = self._output_grad(zs[-1], yb, wb, 1.0 / bs, K, ae, xb)
-            grads = []
-            for li in range(len(self._layers) - 1, -1, -1):
-                L = self._layers[li]
-                Aprev = acts[li]
-                if li == len(self._layers) - 1:
-                    db = dZ.sum(0)
-                dW = dZ.t() @ Aprev
-                grads.append((li, dW, db))
-                if li > 0:
-                    dA = dZ @ L.W
-                    Lp = self._layers[li - 1]
-                    dZ, db = dl_ops.bwd(dA, acts[li], zs[li - 1], Lp.act, Lp.drop, seed=step_seed + 7919 * li)
-            if W_ > 1:
-                flat = [g for (_, a, b_) in grads for g in (a, b_)]
-                coll.allreduce_many_(flat)
-                for g in flat:
-                    g.div_(W_)
-            if avg_act is not None:
-                for li in range(len(self._layers) - 1):
-                    avg_act[li].mul_(0.999).add_(0.001 * acts[li + 1].mean(0))
+            if graph is not None:
+                # ONE graph launch per step: the batch gather, forward, backward,
+                # updates and the dropout-seed advance were captured once
+                graph["idx"].copy_(idx)
+                graph["g"].replay()
+            else:
+                xb = X.index_select(0, idx)
+                yb = None if Y is None else Y.index_select(0, idx)
+                wb = None if w is None else w.index_select(0, idx)
+                step_seed = (step_seed * 6364136223846793005 + 1442695040888963407) & ((1 << 63) - 1)
+                self._train_step(xb, yb, wb, step_seed, hp, avg_act)
             self._processed += bs * W_
-            m = mom_start
-            if mom_ramp > 0:
-                m = mom_stable if self._processed >= mom_ramp else \
-                    mom_start + (mom_stable - mom_start) * self._processed / mom_ramp
-            for (li, dW, db) in grads:
-                L = self._layers[li]
-                r = rate0 / (1 + anneal * self._processed) * decay ** li
-                up = dl_ops.UpdateParams(ada=ada, rho=float(p["rho"]), eps=float(p["epsilon"]),
-                                         rate=r * (1 - m) if not ada else 0.0, momentum=m,
-                                         nesterov=bool(p.get("nesterov_accelerated_gradient", True)),
-                                         has_momenta=has_mom, l1=l1, l2=l2, max_w2=max_w2,
-                                         sparsity_beta=sparsity,
-                                         average_activation=float(p.get("average_activation") or 0.0))
-                dl_ops.update(L.W, dW.contiguous(), L.b, db.contiguous(), L.state, up,
-                              avg_act=avg_act[li] if (avg_act is not None and li < len(avg_act)) else None)
             samples_done += bs * W_
             if samples_done >= next_score or samples_done >= total_samples:
                 it += 1
@@ -399,6 +375,88 @@ class H2ODeepLearningEstimator(H2OEstimator):
             for L, (Wb, bb) in zip(self._layers, best[1]):
                 L.W.copy_(Wb)
                 L.b.copy_(bb)
+
+    def _train_step(self, xb, yb, wb, step_seed, hp, avg_act=None, seed_dev=None):
+        """One mini-batch step: forward, output gradient, backward through the
+        HIP bwd kernel + GEMMs, (all-reduce), per-row update kernels.  With
+        seed_dev the dropout seed is read from device memory (graph replays)."""
+        p = self._parms
+        K, ae, bs = hp["K"], hp["ae"], xb.shape[0]
+        W_ = cloud.world()
+        acts, zs = self._forward(xb, True, step_seed, seed_dev)
+        dZ, _ = self._output_grad(zs[-1], yb, wb, 1.0 / bs, K, ae, xb)
+        grads = []
+        for li in range(len(self._layers) - 1, -1, -1):
+            L = self._layers[li]
+            if li == len(self._layers) - 1:
+                db = dZ.sum(0)
+            dW = dZ.t() @ acts[li]
+            grads.append((li, dW, db))
+            if li > 0:
+                dA = dZ @ L.W
+                Lp = self._layers[li - 1]
+                dZ, db = dl_ops.bwd(dA, acts[li], zs[li - 1], Lp.act, Lp.drop, seed=step_seed + 7919 * li,
+                                    seed_dev=seed_dev)
+        if W_ > 1:
+            flat = [g for (_, a, b_) in grads for g in (a, b_)]
+            coll.allreduce_many_(flat)
+            for g in flat:
+                g.div_(W_)
+        if avg_act is not None:
+            for li in range(len(self._layers) - 1):
+                avg_act[li].mul_(0.999).add_(0.001 * acts[li + 1].mean(0))
+        m = hp["mom_start"]
+        if hp["mom_ramp"] > 0:
+            m = hp["mom_stable"] if self._processed >= hp["mom_ramp"] else \
+                hp["mom_start"] + (hp["mom_stable"] - hp["mom_start"]) * self._processed / hp["mom_ramp"]
+        for (li, dW, db) in grads:
+            L = self._layers[li]
+            r = hp["rate0"] / (1 + hp["anneal"] * self._processed) * hp["decay"] ** li
+            up = dl_ops.UpdateParams(ada=hp["ada"], rho=float(p["rho"]), eps=float(p["epsilon"]),
+                                     rate=r * (1 - m) if not hp["ada"] else 0.0, momentum=m,
+                                     nesterov=bool(p.get("nesterov_accelerated_gradient", True)),
+                                     has_momenta=hp["has_mom"], l1=hp["l1"], l2=hp["l2"], max_w2=hp["max_w2"],
+                                     sparsity_beta=hp["sparsity"],
+                                     average_activation=float(p.get("average_activation") or 0.0))
+            dl_ops.update(L.W, dW.contiguous(), L.b, db.contiguous(), L.state, up,
+                          avg_act=avg_act[li] if (avg_act is not None and li < len(avg_act)) else None)
+
+    def _graph_ok(self, X, hp, avg_act):
+        """HIP-graph the step when nothing in it changes between steps on the
+        host side: ADADELTA (no rate / momentum schedule), one rank (no
+        collective inside the graph), no sparsity running averages."""
+        import os
+        return X.device.type == "cuda" and cloud.world() == 1 and hp["ada"] and avg_act is None and \
+            os.environ.get("H2O3_DL_GRAPH", "1") == "1"
+
+    def _step_graph(self, X, Y, w, hp, avg_act):
+        """Capture gather + step + seed advance into one hipGraph (static
+        batch buffers, weights / ADADELTA state updated in place)."""
+        bs = hp["bs"]
+        dev = X.device
+        gs = {"idx": torch.zeros(bs, dtype=torch.int64, device=dev),
+              "seed": torch.tensor([self._seed() * 1000003 & ((1 << 62) - 1)], dtype=torch.int64, device=dev)}
+
+        def body():
+            xb = X.index_select(0, gs["idx"])
+            yb = None if Y is None else Y.index_select(0, gs["idx"])
+            wb = None if w is None else w.index_select(0, gs["idx"])
+            dl_ops.seed_advance(gs["seed"])
+            self._train_step(xb, yb, wb, 0, hp, avg_act, seed_dev=gs["seed"])
+        cur = torch.cuda.current_stream()
+        side = torch.cuda.Stream()
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            for i in range(2):      # warm-up steps create the optimizer state and pick GEMM algos
+                gs["idx"].copy_(torch.arange(i * bs, (i + 1) * bs, device=dev) % X.shape[0])
+                body()
+                self._processed += bs
+        cur.wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            body()
+        gs["g"] = g
+        return gs
 
     def _stop_on_error(self, entry, K, ae):
         """classification_stop / regression_stop on the training error."""

@@ -67,19 +67,21 @@ __device__ __forceinline__ float dl_dact(int act, float a) {
 // test_scale = 1 - ratio for the reference's dropout activations).
 __global__ __launch_bounds__(256) void dl_fwd_kernel(float* __restrict__ Z, const float* __restrict__ bias,
                                                      float* __restrict__ A, int B, int U, int act, unsigned thr,
-                                                     unsigned long long seed, int mode, float test_scale) {
+                                                     unsigned long long seed, const unsigned long long* seed_dev,
+                                                     int mode, float test_scale) {
+  if (seed_dev) seed += *seed_dev;   // graph replays: the step seed lives in device memory
   const long long n = (long long)B * U;
   for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long long)gridDim.x * 256) {
     const int row = (int)(e / U), u = (int)(e - (long long)row * U);
     float a;
     if (act == ACT_MAXOUT) {
       float* z = Z + (long long)row * 2 * U + 2 * u;
-      const float z0 = z[0] + bias[2 * u], z1 = z[1] + bias[2 * u + 1];
+      const float z0 = z[0] + (bias ? bias[2 * u] : 0.f), z1 = z[1] + (bias ? bias[2 * u + 1] : 0.f);
       z[0] = z0;
       z[1] = z1;
       a = fmaxf(z0, z1);
     } else {
-      const float z = Z[e] + bias[u];
+      const float z = Z[e] + (bias ? bias[u] : 0.f);
       Z[e] = z;
       a = dl_act(act, z);
     }
@@ -97,7 +99,9 @@ __global__ __launch_bounds__(256) void dl_fwd_kernel(float* __restrict__ Z, cons
 __global__ __launch_bounds__(256) void dl_bwd_kernel(const float* __restrict__ dA, const float* __restrict__ A,
                                                      const float* __restrict__ Z, float* __restrict__ dZ,
                                                      float* __restrict__ dbias, int B, int U, int act, unsigned thr,
-                                                     unsigned long long seed, int rows_per_block) {
+                                                     unsigned long long seed, const unsigned long long* seed_dev,
+                                                     int rows_per_block) {
+  if (seed_dev) seed += *seed_dev;
   const int u = blockIdx.x * 256 + threadIdx.x;
   if (u >= U) return;
   const int r0 = blockIdx.y * rows_per_block;
@@ -278,19 +282,32 @@ __global__ __launch_bounds__(256) void dl_softmax_kernel(float* __restrict__ Z, 
 
 extern "C" {
 
+// Step-seed advance (an LCG step of the device seed): captured once in the
+// training-step graph, so every replay draws new dropout masks.
+__global__ void dl_seed_kernel(unsigned long long* s) {
+  if (threadIdx.x == 0) s[0] = s[0] * 6364136223846793005ull + 1442695040888963407ull;
+}
+
+extern "C" int h2o_dl_seed_advance(unsigned long long* s, hipStream_t st) {
+  hipLaunchKernelGGL(dl_seed_kernel, dim3(1), dim3(64), 0, st, s);
+  H2O_CHECK_LAUNCH();
+}
+
 int h2o_dl_fwd(float* Z, const float* bias, float* A, int B, int U, int act, float drop_ratio,
-               unsigned long long seed, int mode, float test_scale, hipStream_t s) {
+               unsigned long long seed, const unsigned long long* seed_dev, int mode, float test_scale,
+               hipStream_t s) {
   if (B <= 0 || U <= 0) return 0;
   const unsigned thr = drop_ratio <= 0.f ? 0u : (unsigned)fminf(drop_ratio * 4294967296.f, 4294967295.f);
   const long long n = (long long)B * U;
   const int grid = (int)std::min<long long>((n + 255) / 256, 4096);
-  hipLaunchKernelGGL(dl_fwd_kernel, dim3(grid), dim3(256), 0, s, Z, bias, A, B, U, act, thr, seed, mode, test_scale);
+  hipLaunchKernelGGL(dl_fwd_kernel, dim3(grid), dim3(256), 0, s, Z, bias, A, B, U, act, thr, seed, seed_dev, mode,
+                     test_scale);
   H2O_CHECK_LAUNCH();
 }
 
 // dbias must be zeroed by the caller (atomics accumulate into it)
 int h2o_dl_bwd(const float* dA, const float* A, const float* Z, float* dZ, float* dbias, int B, int U, int act,
-               float drop_ratio, unsigned long long seed, hipStream_t s) {
+               float drop_ratio, unsigned long long seed, const unsigned long long* seed_dev, hipStream_t s) {
   if (B <= 0 || U <= 0) return 0;
   const unsigned thr = drop_ratio <= 0.f ? 0u : (unsigned)fminf(drop_ratio * 4294967296.f, 4294967295.f);
   const int gx = (U + 255) / 256;
@@ -298,7 +315,8 @@ int h2o_dl_bwd(const float* dA, const float* A, const float* Z, float* dZ, float
   int gy = std::max(1, std::min((B + 15) / 16, (2048 + gx - 1) / gx));
   const int rpb = (B + gy - 1) / gy;
   gy = (B + rpb - 1) / rpb;
-  hipLaunchKernelGGL(dl_bwd_kernel, dim3(gx, gy), dim3(256), 0, s, dA, A, Z, dZ, dbias, B, U, act, thr, seed, rpb);
+  hipLaunchKernelGGL(dl_bwd_kernel, dim3(gx, gy), dim3(256), 0, s, dA, A, Z, dZ, dbias, B, U, act, thr, seed, seed_dev,
+                     rpb);
   H2O_CHECK_LAUNCH();
 }
 

@@ -24,8 +24,9 @@ _cv, _ci, _cf, _cull = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_u
 def _lib():
     lib = _native.get_lib("dl")
     if lib is not None and not getattr(lib, "_typed", False):
-        lib.h2o_dl_fwd.argtypes = [_cv, _cv, _cv, _ci, _ci, _ci, _cf, _cull, _ci, _cf, _cv]
-        lib.h2o_dl_bwd.argtypes = [_cv, _cv, _cv, _cv, _cv, _ci, _ci, _ci, _cf, _cull, _cv]
+        lib.h2o_dl_fwd.argtypes = [_cv, _cv, _cv, _ci, _ci, _ci, _cf, _cull, _cv, _ci, _cf, _cv]
+        lib.h2o_dl_bwd.argtypes = [_cv, _cv, _cv, _cv, _cv, _ci, _ci, _ci, _cf, _cull, _cv, _cv]
+        lib.h2o_dl_seed_advance.argtypes = [_cv, _cv]
         lib.h2o_dl_update.argtypes = [_cv] * 9 + [_ci, _ci] + [_cf] * 7 + [_ci] * 3 + [_cf, _cf, _cv]
         lib.h2o_dl_softmax.argtypes = [_cv] * 7 + [_ci, _ci, _cf, _ci, _cv]
         lib._typed = True
@@ -78,17 +79,34 @@ def keep_mask(seed: int, B: int, U: int, ratio: float, device) -> torch.Tensor:
 
 
 # ---------------------------------------------------------------- forward
-def fwd(Z, bias, act: str, drop_ratio=0.0, seed=0, train=True, test_scale=1.0, use_native=None):
-    """Z [B, U*k] (bias added in place), returns A [B, U]."""
+def seed_advance(seed_dev, use_native=None):
+    """One LCG step of a device-resident step seed (int64 [1]); the training
+    step graph captures it so every replay draws new dropout masks."""
+    if _native_ok(seed_dev, use_native):
+        _check(_lib().h2o_dl_seed_advance(_p(seed_dev), _s()), "h2o_dl_seed_advance")
+        return
+    v = (int(seed_dev.item()) * 6364136223846793005 + 1442695040888963407) & _M
+    seed_dev.fill_(_i64(v))
+
+
+def _eff_seed(seed, seed_dev):
+    return (seed + (int(seed_dev.item()) & _M)) & _M if seed_dev is not None else seed
+
+
+def fwd(Z, bias, act: str, drop_ratio=0.0, seed=0, train=True, test_scale=1.0, use_native=None, seed_dev=None):
+    """Z [B, U*k] (bias added in place; bias may be None), returns A [B, U].
+    seed_dev: optional device int64 [1] added to `seed` inside the kernel."""
     a = ACT[act]
     B = Z.shape[0]
     U = Z.shape[1] // (2 if a == 4 else 1)
     if _native_ok(Z, use_native):
         A = torch.empty((B, U), dtype=torch.float32, device=Z.device)
-        _check(_lib().h2o_dl_fwd(_p(Z), _p(bias), _p(A), B, U, a, float(drop_ratio), seed & _M, 0 if train else 1,
-                                 float(test_scale), _s()), "h2o_dl_fwd")
+        _check(_lib().h2o_dl_fwd(_p(Z), _p(bias), _p(A), B, U, a, float(drop_ratio), seed & _M, _p(seed_dev),
+                                 0 if train else 1, float(test_scale), _s()), "h2o_dl_fwd")
         return A
-    Z += bias.view(1, -1)
+    seed = _eff_seed(seed, seed_dev)
+    if bias is not None:
+        Z += bias.view(1, -1)
     if a == 4:
         A = Z.view(B, U, 2).max(2).values
     elif a == 1:
@@ -107,7 +125,7 @@ def fwd(Z, bias, act: str, drop_ratio=0.0, seed=0, train=True, test_scale=1.0, u
     return A
 
 
-def bwd(dA, A, Z, act: str, drop_ratio=0.0, seed=0, use_native=None):
+def bwd(dA, A, Z, act: str, drop_ratio=0.0, seed=0, use_native=None, seed_dev=None):
     """Returns (dZ [B, U*k], db [U*k])."""
     a = ACT[act]
     B, U = dA.shape
@@ -116,8 +134,9 @@ def bwd(dA, A, Z, act: str, drop_ratio=0.0, seed=0, use_native=None):
         dZ = torch.empty((B, U * k), dtype=torch.float32, device=dA.device)
         db = torch.zeros(U * k, dtype=torch.float32, device=dA.device)
         _check(_lib().h2o_dl_bwd(_p(dA.contiguous()), _p(A), _p(Z), _p(dZ), _p(db), B, U, a, float(drop_ratio),
-                                 seed & _M, _s()), "h2o_dl_bwd")
+                                 seed & _M, _p(seed_dev), _s()), "h2o_dl_bwd")
         return dZ, db
+    seed = _eff_seed(seed, seed_dev)
     g = dA * keep_mask(seed, B, U, drop_ratio, dA.device) if drop_ratio > 0 else dA
     if a == 4:
         z = Z.view(B, U, 2)

@@ -268,3 +268,36 @@ def test_dl_estimator_gpu():
                                  input_dropout_ratio=0.1)
     m.train(x=x, y="y", training_frame=fr)
     assert m.auc() > 0.85
+
+
+@pytest.mark.gpu
+def test_dl_step_graph_matches_eager():
+    """The hipGraph-captured step (gather + forward + backward + updates +
+    seed advance) equals the same steps launched eagerly."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    g = torch.Generator(device="cuda").manual_seed(1)
+    X = torch.randn((5000, 12), generator=g, device="cuda")
+    Y = (X[:, 0] > 0).long()
+    hp = dict(K=2, ae=False, bs=256, ada=True, rate0=0.005, anneal=1e-6, decay=1.0, mom_start=0.0, mom_ramp=1e6,
+              mom_stable=0.0, has_mom=False, l1=1e-5, l2=1e-5, max_w2=10.0, sparsity=0.0)
+    mk = lambda: H2ODeepLearningEstimator(hidden=[32, 16], activation="RectifierWithDropout", seed=3,
+                                          input_dropout_ratio=0.1)
+    a, b = mk(), mk()
+    for m in (a, b):
+        m._layers = m._build(12, 2, True)
+        m._processed = 0.0
+    idxs = [torch.randint(0, 5000, (256,), generator=g, device="cuda") for _ in range(3)]
+    gs = a._step_graph(X, Y, None, hp, None)
+    for idx in idxs:
+        gs["idx"].copy_(idx)
+        gs["g"].replay()
+    seed = torch.tensor([b._seed() * 1000003 & ((1 << 62) - 1)], dtype=torch.int64, device="cuda")
+    seq = [torch.arange(i * 256, (i + 1) * 256, device="cuda") % 5000 for i in range(2)] + idxs
+    for idx in seq:
+        dl_ops.seed_advance(seed)
+        b._train_step(X.index_select(0, idx), Y.index_select(0, idx), None, 0, hp, None, seed_dev=seed)
+    torch.cuda.synchronize()
+    for La, Lb in zip(a._layers, b._layers):
+        torch.testing.assert_close(La.W, Lb.W, rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(La.b, Lb.b, rtol=1e-5, atol=1e-6)
