@@ -213,36 +213,53 @@ class TreeGrower:
         return need
 
     # ------------------------------------------------------------------ splits
-    def _col_mask(self, n_nodes, depth):
-        """[n, Fpad] bool mask of features eligible per node."""
+    def _col_sel(self, n_nodes, depth):
+        """Per-node sampled columns as a [n, k] int64 tensor of global feature
+        ids in ascending order (k random eligible features per node: the k
+        smallest of per-(node, feature) uniform keys, on the device when the
+        data is -- deep DRF levels have 10^4+ nodes), or None when every
+        eligible feature is scored.  Consumes the tree's RNG exactly like the
+        mask path so both give the same samples."""
         p = self.p
         F = self.bd.F
         base = np.ones(F, dtype=bool) if p.tree_col_mask is None else p.tree_col_mask.astype(bool)
-        m = np.tile(base, (n_nodes, 1))
         rate = p.col_sample_rate * (p.col_sample_rate_change_per_level ** depth)
         k = None
         if p.mtries is not None and p.mtries > 0:
             k = p.mtries
         elif rate < 1.0:
             k = max(1, int(math.floor(rate * base.sum() + 0.5)))
-        if k is not None and k < base.sum():
-            # k random eligible features per node, all nodes at once: the k
-            # smallest of per-(node, feature) uniform keys (on the device when
-            # the histograms are there -- deep DRF levels have 10^4+ nodes)
-            elig = np.nonzero(base)[0]
-            if self.dev.type == "cuda":
-                gen = torch.Generator(device=self.dev)
-                gen.manual_seed(int(self.rng.randint(0, 2 ** 31 - 1)))
-                keys = torch.rand((n_nodes, len(elig)), generator=gen, device=self.dev)
-                sel = torch.topk(keys, k, dim=1, largest=False).indices
-                mt = torch.zeros((n_nodes, self.Fpad), dtype=torch.bool, device=self.dev)
-                mt.scatter_(1, torch.as_tensor(elig, device=self.dev)[sel], True)
-                mt._all_true = False
-                return mt
-            keys = self.rng.random_sample((n_nodes, len(elig)))
-            sel = np.argpartition(keys, k - 1, axis=1)[:, :k]
-            m = np.zeros((n_nodes, F), dtype=bool)
-            m[np.arange(n_nodes).reshape(-1, 1), elig[sel]] = True
+        if k is None or k >= base.sum():
+            return None
+        elig = np.nonzero(base)[0]
+        if self.dev.type == "cuda":
+            gen = torch.Generator(device=self.dev)
+            gen.manual_seed(int(self.rng.randint(0, 2 ** 31 - 1)))
+            keys = torch.rand((n_nodes, len(elig)), generator=gen, device=self.dev)
+            sel = torch.topk(keys, k, dim=1, largest=False).indices
+            el = self.__dict__.setdefault("_elig_dev", {})
+            key = elig.tobytes()
+            if key not in el:
+                el.clear()
+                el[key] = torch.as_tensor(elig, device=self.dev)
+            return torch.sort(el[key][sel], dim=1).values
+        keys = self.rng.random_sample((n_nodes, len(elig)))
+        sel = np.argpartition(keys, k - 1, axis=1)[:, :k]
+        return torch.from_numpy(np.sort(elig[sel], axis=1))
+
+    def _col_mask(self, n_nodes, depth, sel=None):
+        """[n, Fpad] bool mask of features eligible per node."""
+        p = self.p
+        F = self.bd.F
+        if sel is None:
+            sel = self._col_sel(n_nodes, depth)
+        if sel is not None:
+            m = torch.zeros((n_nodes, self.Fpad), dtype=torch.bool, device=sel.device)
+            m.scatter_(1, sel, True)
+            m._all_true = False
+            return m
+        base = np.ones(F, dtype=bool) if p.tree_col_mask is None else p.tree_col_mask.astype(bool)
+        m = np.tile(base, (n_nodes, 1))
         all_true = bool(m.all())
         if self.Fpad > F:
             m = np.concatenate([m, np.zeros((n_nodes, self.Fpad - F), dtype=bool)], 1)
@@ -410,8 +427,6 @@ class TreeGrower:
         if nz.shape[0] == 0:
             return out
         node_i, j = nz[:, 0], nz[:, 1]
-        P = node_i.numel()
-        xgb = p.criterion == "xgb"
         pcat = self.is_cat_t[gidx[j]]                              # numeric pairs keep bin order
         mono_p = self.mono_t[gidx[j]]
         if dev.type == "cuda" and C >= 2 and B <= 4096 and H.dtype == torch.float64:
@@ -420,6 +435,201 @@ class TreeGrower:
             st = self._pair_stats(H[sub_t[j], node_i].to(torch.float64), pcat)
             allg = self._pair_gains(st, mono_p.view(-1, 1), node_wyy, node_i)
             best, k = allg.max(1)
+        return self._pair_winners(out, best, k, node_i, gidx[j], pcat, lambda wp: H[sub_t[j[wp]], node_i[wp]])
+
+    def _sample_k(self, depth):
+        """(k, n_eligible): columns scored per node at this depth."""
+        p = self.p
+        base_n = self.bd.F if p.tree_col_mask is None else int(np.count_nonzero(p.tree_col_mask))
+        rate = p.col_sample_rate * (p.col_sample_rate_change_per_level ** depth)
+        if p.mtries is not None and p.mtries > 0:
+            k = p.mtries
+        elif rate < 1.0:
+            k = max(1, int(math.floor(rate * base_n + 0.5)))
+        else:
+            k = base_n
+        return min(k, base_n), base_n
+
+    def _sampled_cols(self, depth):
+        """True when the split search at this depth sees a per-node subset
+        of the columns (mtries / col_sample_rate(_change_per_level) /
+        col_sample_rate_per_tree)."""
+        k, ne = self._sample_k(depth)
+        return k < self.bd.F
+
+    def _direct_level(self, mode, depth, chunked):
+        """Row-direct pair histograms for this level (tree_ops.pair_hist):
+        column-sampled splits where at most a quarter of the features are
+        scored per node (DRF's sqrt(F) mtries) or the level histogram would
+        need node batching (H2O3_PAIR_DIRECT=auto); at every sampled level
+        (=1); never (=0).  Measured on the DRF config (10M x 500, 100
+        categoricals of cardinality 1000): 995 ms/tree with level histograms,
+        ~500 ms/tree with pair histograms at every sampled level."""
+        env = os.environ.get("H2O3_PAIR_DIRECT", "auto")
+        if env == "0" or mode not in (0, 1) or self.p.criterion.startswith("uplift") or \
+                not self._sampled_cols(depth):
+            return False
+        if self.dev.type == "cuda" and self.bd.codes_col is None:
+            return False
+        k, _ = self._sample_k(depth)
+        return env == "1" or chunked or 4 * k <= self.bd.F
+
+    def _pair_direct_splits(self, ridx, va, vb, mode, frontier, cm):
+        """Best split of every frontier node from row-direct histograms of its
+        sampled (node, feature) pairs only: pair histograms built from the rows
+        (HIP `pair_hist_kernel`), scored per pair (`cat_pair_kernel`: numeric
+        bin order or categorical levels sorted by mean response, three NA
+        options), per-node winner + mask (_pair_winners).  Pairs are processed
+        in node batches under hist_mem_budget.  Every rank sums the pair
+        histograms (all-reduce) and scores all pairs, so no candidate merge."""
+        p = self.p
+        bd, dev = self.bd, self.dev
+        F, Bs, C = bd.F, bd.Bs, 2
+        n = len(frontier)
+        posv = False
+        if mode == 0 and getattr(self, "_pos1", None) is not None:
+            va, vb, posv = self._pos1[0], None, True
+        elif mode == 0 and getattr(self, "_va_eff", None) is not None:
+            va, vb = self._va_eff, None
+        st = np.asarray([f[1] for f in frontier], dtype=np.int64)
+        ct = np.asarray([f[2] for f in frontier], dtype=np.int64)
+        nz = torch.nonzero(cm[:, :F]).cpu().numpy()           # node-major pairs
+        pn_all, pf_all = nz[:, 0].astype(np.int64), nz[:, 1].astype(np.int64)
+        per_pairs = max(1, int(p.hist_mem_budget // (Bs * C * 8)))
+        cum = np.cumsum(np.bincount(pn_all, minlength=n))     # pairs of nodes [0, i]
+        parts = []
+        a = 0
+        while a < n:
+            base = int(cum[a - 1]) if a > 0 else 0
+            b = min(n, max(a + 1, int(np.searchsorted(cum, base + per_pairs, side="right"))))
+            lo, hi = base, int(cum[b - 1])
+            parts.append(self._pair_direct_part(ridx, va, vb, mode, posv, st[a:b], ct[a:b], pn_all[lo:hi] - a,
+                                                pf_all[lo:hi]))
+            a = b
+        if len(parts) == 1:
+            return parts[0]
+        return {k: torch.cat([q[k] for q in parts], 0) for k in parts[0]}
+
+    def _pair_direct_dev(self, ridx, va, vb, mode, frontier, sel):
+        """Device-resident version of _pair_direct_splits: pairs from the
+        [n, k] column sample on the device, pair histograms
+        (pair_hist_kernel), per-pair scoring (cat_pair_kernel) and the
+        per-node winner / record / mask (pair_select_kernel) -- the level's
+        split record comes out in the packed form of split_select2, so the
+        async partition and the single host transfer of the level apply."""
+        import ctypes
+        from ...ops import _native
+        p = self.p
+        bd, dev = self.bd, self.dev
+        Bs = bd.Bs
+        if sel is None:
+            # no per-node sampling (only the per-tree column mask): every eligible feature
+            base = np.ones(bd.F, dtype=bool) if p.tree_col_mask is None else p.tree_col_mask.astype(bool)
+            elig = torch.as_tensor(np.nonzero(base)[0], device=dev)
+            sel = elig.view(1, -1).expand(len(frontier), -1)
+        n, k = sel.shape
+        posv = False
+        if mode == 0 and getattr(self, "_pos1", None) is not None:
+            va, vb, posv = self._pos1[0], None, True
+        elif mode == 0 and getattr(self, "_va_eff", None) is not None:
+            va, vb = self._va_eff, None
+        lib = _native.get_lib("tree_split")
+        if not getattr(lib, "_typed_psel", False):
+            cv, ci, cd = ctypes.c_void_p, ctypes.c_int, ctypes.c_double
+            lib.h2o_pair_select.argtypes = [cv, ci, ci, ci, cv, cv, cv, ci, cd, ci, cv, cv, cv, cv]
+            lib._typed_psel = True
+        if getattr(self, "_fcat_u8", None) is None:
+            self._fcat_u8 = self.is_cat_t[:bd.F].to(torch.uint8).contiguous()
+        st = np.asarray([f[1] for f in frontier], dtype=np.int64)
+        ct = np.asarray([f[2] for f in frontier], dtype=np.int64)
+        per = max(1, int(p.hist_mem_budget // (k * Bs * 2 * 8)))
+        pk = torch.empty((n, 12), dtype=torch.float64, device=dev)
+        mask = torch.empty((n, Bs), dtype=torch.uint8, device=dev)
+        feat_i = torch.empty(n, dtype=torch.int32, device=dev)
+        min_w2 = -1.0 if p.criterion == "xgb" else 2.0 * float(p.min_rows)
+        for a in range(0, n, per):
+            b = min(n, a + per)
+            sl = sel[a:b]
+            with phase("tree.hist"), phase("tree.hist.pairs"):
+                Hp, wyy_n, pfeat = tree_ops.pair_hist_dev(bd, ridx, va, vb, mode, st[a:b], ct[a:b], sl, self._vmax,
+                                                          posv=posv)
+            if self.W > 1:
+                coll.allreduce_(Hp)
+                if wyy_n is not None:
+                    coll.allreduce_(wyy_n)
+            P = (b - a) * k
+            fl = pfeat.long()
+            best_k = self._pairs_native(Hp.view(1, P, Bs, 2), torch.zeros(P, dtype=torch.long, device=dev),
+                                        torch.arange(P, device=dev), self.is_cat_t[fl], self.mono_t[fl],
+                                        wyy_n.repeat_interleave(k) if wyy_n is not None else None, raw=True)
+            rc = lib.h2o_pair_select(ctypes.c_void_p(Hp.data_ptr()), b - a, Bs, k, ctypes.c_void_p(best_k.data_ptr()),
+                                     ctypes.c_void_p(pfeat.data_ptr()), ctypes.c_void_p(self._fcat_u8.data_ptr()),
+                                     1 if p.criterion == "xgb" else 0, min_w2, 12,
+                                     ctypes.c_void_p(pk[a:b].data_ptr()), ctypes.c_void_p(mask[a:b].data_ptr()),
+                                     ctypes.c_void_p(feat_i[a:b].data_ptr()),
+                                     ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+            if rc != 0:
+                raise RuntimeError(f"h2o_pair_select failed: {rc}")
+            del Hp
+        return {"pk": pk, "feat_i32": feat_i, "mask": mask, "gain": pk[:, 0], "feat": pk[:, 1].long(),
+                "t": pk[:, 2].long(), "opt": pk[:, 3].long(), "L": pk[:, 4:6], "R": pk[:, 6:8], "tot": pk[:, 8:10]}
+
+    def _pair_direct_part(self, ridx, va, vb, mode, posv, st, ct, pn, pf):
+        p = self.p
+        dev = self.dev
+        n = st.size
+        Bs, C = self.bd.Bs, 2
+        out = {"gain": torch.full((n,), NEG_INF, dtype=torch.float64, device=dev),
+               "feat": torch.zeros(n, dtype=torch.long, device=dev),
+               "t": torch.zeros(n, dtype=torch.long, device=dev), "opt": torch.zeros(n, dtype=torch.long, device=dev),
+               "na_left": torch.zeros(n, dtype=torch.bool, device=dev),
+               "mask": torch.zeros((n, Bs), dtype=torch.uint8, device=dev),
+               "L": torch.zeros((n, C), dtype=torch.float64, device=dev),
+               "R": torch.zeros((n, C), dtype=torch.float64, device=dev),
+               "tot": torch.zeros((n, C), dtype=torch.float64, device=dev)}
+        with phase("tree.hist"), phase("tree.hist.pairs"):
+            Hp, wyy_n = tree_ops.pair_hist(self.bd, ridx, va, vb, mode, st, ct, pn, pf, vmax=self._vmax, posv=posv,
+                                           want_wyy=mode == 0)
+        if self.W > 1:
+            coll.allreduce_(Hp)
+            if wyy_n is not None:
+                coll.allreduce_(wyy_n)
+        P = pn.size
+        if P == 0:
+            return out
+        pn_t = tree_ops._h2d(pn, dev)
+        first = np.ones(P, dtype=bool)
+        first[1:] = pn[1:] != pn[:-1]
+        fi = np.nonzero(first)[0]
+        out["tot"] = out["tot"].index_put((pn_t[tree_ops._h2d(fi, dev)],),
+                                          Hp[tree_ops._h2d(fi, dev)].sum(1))
+        fglob = tree_ops._h2d(pf, dev)
+        pcat = self.is_cat_t[fglob]
+        mono_p = self.mono_t[fglob]
+        wyy_p = wyy_n[pn_t] if wyy_n is not None else None
+        ar = torch.arange(P, device=dev)
+        if dev.type == "cuda" and Bs - 1 <= 4096:
+            best, k = self._pairs_native(Hp.view(1, P, Bs, C), torch.zeros(P, dtype=torch.long, device=dev), ar,
+                                         pcat, mono_p, wyy_p)
+        else:
+            stt = self._pair_stats(Hp, pcat)
+            allg = self._pair_gains(stt, mono_p.view(-1, 1), wyy_p, ar)
+            best, k = allg.max(1)
+        return self._pair_winners(out, best, k, pn_t, fglob, pcat, lambda wp: Hp[wp])
+
+    def _pair_winners(self, out, best, k, node_i, fglob, pcat, hist_of):
+        """Per-node winner among scored (node, feature) pairs (largest gain,
+        lowest pair index on ties) and its split record: threshold / NA option
+        from k, left statistics and the go-left code mask rebuilt from the
+        winner's own bins (hist_of(wp) -> [len(wp), Bs, C])."""
+        p = self.p
+        n = out["gain"].shape[0]
+        dev = best.device
+        P = best.numel()
+        ninf = torch.full((n,), NEG_INF, dtype=torch.float64, device=dev)
+        B = self.bd.Bs - 1
+        Bs = self.bd.Bs
+        xgb = p.criterion == "xgb"
         node_best = ninf.clone().scatter_reduce(0, node_i, best, reduce="amax", include_self=True)
         cand = torch.where((best == node_best[node_i]) & torch.isfinite(best), torch.arange(P, device=dev),
                            torch.full((P,), P, device=dev))
@@ -431,7 +641,7 @@ class TreeGrower:
         nodes = torch.nonzero(has).flatten()
         wp = win[nodes]
         # the winners' sorted order / prefix sums, from their own bins only
-        st = self._pair_stats(H[sub_t[j[wp]], node_i[wp]].to(torch.float64), pcat[wp])
+        st = self._pair_stats(hist_of(wp).to(torch.float64), pcat[wp])
         h, order, L, totnn, na, T = st["h"], st["order"], st["L"], st["totnn"], st["na"], st["T"]
         nt = B - 1
         kk = k[wp]
@@ -451,7 +661,7 @@ class TreeGrower:
         in_left = torch.where((opt == 2).view(-1, 1), ~empty | na_left.view(-1, 1), in_left)
         mask = torch.cat([in_left, na_left.view(-1, 1).expand(-1, Bs - B)], 1).to(torch.uint8)
         out["gain"] = out["gain"].index_put((nodes,), best[wp])
-        out["feat"] = out["feat"].index_put((nodes,), gidx[j[wp]])
+        out["feat"] = out["feat"].index_put((nodes,), fglob[wp])
         out["t"] = out["t"].index_put((nodes,), t)
         out["opt"] = out["opt"].index_put((nodes,), opt)
         out["na_left"] = out["na_left"].index_put((nodes,), na_left)
@@ -531,7 +741,7 @@ class TreeGrower:
         return torch.where((allg > se_before * p.min_split_improvement) & (se_before > 0), allg,
                            torch.full_like(allg, NEG_INF))
 
-    def _pairs_native(self, H, fslot, node_i, pcat, mono_p, node_wyy):
+    def _pairs_native(self, H, fslot, node_i, pcat, mono_p, node_wyy, raw=False):
         """(best gain, k) per pair from the HIP pair kernel."""
         import ctypes
         from ...ops import _native
@@ -559,6 +769,8 @@ class TreeGrower:
                                ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
         if rc != 0:
             raise RuntimeError(f"h2o_cat_pairs failed: {rc}")
+        if raw:
+            return res
         return res[:, 0].contiguous(), res[:, 1].to(torch.long)
 
     def _find_splits_torch(self, H, col_mask, node_wyy=None, merge=True, sub=None):
@@ -818,6 +1030,8 @@ class TreeGrower:
             level_bytes = self.Fpad * n_front * bd.Bs * C_ * 8
             prev_bytes = 0 if H_prev is None else H_prev.numel() * 8
             chunked = can_split and (level_bytes + prev_bytes) > p.hist_mem_budget and n_front > 1
+            direct = can_split and self._direct_level(mode, depth, chunked)
+            chunked = chunked or direct
             la, self._la = self._la, None
             if la is not None and (chunked or not can_split or la[0].shape[1] < n_front):
                 la = None   # defensive: the look-ahead only matches a full next level
@@ -878,12 +1092,17 @@ class TreeGrower:
                 del Hb
             nleft_pre = None
             if can_split:
-                cm = self._col_mask(n_front, depth)
+                sel = self._col_sel(n_front, depth) if direct else None
+                cm = None if (direct and self.dev.type == "cuda") else self._col_mask(n_front, depth, sel=sel)
                 # node totals of w*y*y (only the total enters the SE split test),
                 # fused into the histogram kernel; derived siblings by subtraction
                 node_wyy = wyy_level if mode == 0 else None
                 with phase("tree.split"):
-                    if chunked:
+                    if direct and self.dev.type == "cuda":
+                        sp = self._pair_direct_dev(ridx, va, vb, mode, frontier, sel)
+                    elif direct:
+                        sp = self._pair_direct_splits(ridx, va, vb, mode, frontier, cm)
+                    elif chunked:
                         per = max(1, int(p.hist_mem_budget // max(1, self.Fpad * bd.Bs * C_ * 8)))
                         parts = []
                         need = self._hist_need(cm)
@@ -994,7 +1213,14 @@ class TreeGrower:
             if any_cat or nleft_pre is None:
                 masks = sp["mask"] if all_split else sp["mask"][tree_ops._h2d(np.asarray(split_ids, dtype=np.int64),
                                                                               sp["mask"].device)]
-            masks_h = masks.cpu().numpy() if any_cat else None
+            masks_h = None
+            if any_cat:
+                # only the categorical splits' mask rows cross to the host (one
+                # gather + copy); node j's row is masks_h[crow[j]]
+                cj = [j for j, i in enumerate(split_ids) if bd.is_cat[feats[i]]]
+                crow = {j: q for q, j in enumerate(cj)}
+                masks_h = masks[tree_ops._h2d(np.asarray(cj, dtype=np.int64), masks.device)].cpu().numpy() \
+                    if len(cj) < len(split_ids) else masks.cpu().numpy()
             new_front, new_pairs = [], []
             part_starts, part_counts, part_feats = [], [], []
             si = np.asarray(split_ids, dtype=np.int64)
@@ -1014,8 +1240,11 @@ class TreeGrower:
                     tree.is_cat[nid_] = True
                     lvm = lvmaps.get(f)
                     if lvm is None:
-                        lvm = lvmaps[f] = np.minimum(np.arange(bd.cat_card[f]) // bd.cat_group[f], bd.Bs - 2)
-                    tree.cat_left[nid_] = masks_h[j][lvm]
+                        card = bd.cat_card[f]
+                        # ungrouped levels map 1:1 to codes: a slice (view) of the level's mask rows
+                        lvm = lvmaps[f] = slice(0, card) if (bd.cat_group[f] == 1 and card <= bd.Bs - 1) else \
+                            np.minimum(np.arange(card) // bd.cat_group[f], bd.Bs - 2)
+                    tree.cat_left[nid_] = masks_h[crow[j]][lvm]
                     tree.thr[nid_] = float("nan")
                 else:
                     if opt_l[i] == 2:

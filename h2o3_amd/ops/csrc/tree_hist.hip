@@ -1084,3 +1084,135 @@ extern "C" int h2o_leaf_update(const int* ridx, const int* work, int n_work, con
   hipLaunchKernelGGL(leaf_update_kernel, dim3(n_work), dim3(256), 0, s, ridx, (const int4*)work, val, f);
   return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------
+// Row-direct (node, feature) PAIR histograms for column-sampled frontiers
+// (DRF mtries, col_sample_rate at deep levels).  Reference: DRF samples
+// mtries columns per node and ScoreBuildHistogram only fills those columns'
+// DHistograms (hex/tree/drf/DRF.java, hex/tree/DTree.java:UndecidedNode
+// scoreCols).  A level histogram [F][n][Bs][C] is mostly empty there (22 of
+// 500 features per node) and, at 10^4 nodes x 1024 bins, larger than the
+// memory budget -- so the old path rebuilt it in node batches from every row's
+// full code row.  Here ONE workgroup builds ONE pair's histogram in LDS from
+// the node's rows: the split feature's code comes from the column-major copy
+// (codes_col[f][row], a 1- or 2-byte gather), the responses from the
+// position-ordered payload or by row.  int64 fixed-point LDS atomics (exact,
+// order-independent sums, like the level kernels).  Output is a compact
+// [P][Bs][C] f64 buffer: a plain store when the node's rows fit one work item
+// (no zero-fill of the buffer), f64 global atomics when a large node is spread
+// over several items (those pairs' rows are pre-zeroed by the caller).
+// work[i] = (pair, start, count, flags): bit0 = the pair's only work item
+// (store), bit1 = also sum w*y*y into pwyy[pair] (one pair per node, MODE 0).
+// MODE 0: channels (w, w*y), NaN response = zero-weight row when !HAS_VB;
+// MODE 1: (g, h) = (va, vb).
+// ---------------------------------------------------------------------------
+template <typename CodeT, int MODE, bool HAS_VB, bool POSV>
+__global__ __launch_bounds__(256) void pair_hist_kernel(const CodeT* __restrict__ codes_col, long long ncol,
+                                                        const int* __restrict__ ridx, const float* __restrict__ va,
+                                                        const float* __restrict__ vb,
+                                                        const int4* __restrict__ work,
+                                                        const int* __restrict__ pfeat, int Bs, float s0, float s1,
+                                                        double* __restrict__ Hp, double* __restrict__ pwyy) {
+  constexpr int C = 2;
+  extern __shared__ __attribute__((aligned(16))) unsigned long long lh[];
+  __shared__ double red[4];
+  const int4 wk = work[blockIdx.x];
+  const int pair = wk.x;
+  const CodeT* cc = codes_col + (size_t)pfeat[pair] * (size_t)ncol;
+  const int nb = Bs * C;
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) lh[i] = 0ull;
+  __syncthreads();
+  const bool do_wyy = MODE == 0 && (wk.w & 2) != 0 && pwyy != nullptr;
+  double wyy = 0.0;
+  const int end = wk.y + wk.z;
+  constexpr int U = 4;
+  for (int p0 = wk.y + (int)threadIdx.x; p0 < end; p0 += U * 256) {
+    int r[U];
+    unsigned int c[U];
+    float xa[U], xb[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) r[u] = ridx[min(p0 + u * 256, end - 1)];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int vi = POSV ? min(p0 + u * 256, end - 1) : r[u];
+      c[u] = (unsigned int)cc[r[u]];
+      xa[u] = va[vi];
+      xb[u] = HAS_VB ? vb[vi] : 1.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (p0 + u * 256 >= end) continue;
+      float c0, c1;
+      if (MODE == 0) {
+        const float y = xa[u];
+        const float w = HAS_VB ? xb[u] : (y == y ? 1.f : 0.f);
+        if (w == 0.f) continue;
+        c0 = w;
+        c1 = w * y;
+        if (do_wyy) wyy += (double)c1 * (double)y;
+      } else {
+        c0 = xa[u];
+        c1 = xb[u];
+      }
+      unsigned long long* h = lh + c[u] * C;
+      __hip_atomic_fetch_add(h, (unsigned long long)__float2ll_rn(c0 * s0), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
+      __hip_atomic_fetch_add(h + 1, (unsigned long long)__float2ll_rn(c1 * s1), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  }
+  __syncthreads();
+  const double i0 = 1.0 / (double)s0, i1 = 1.0 / (double)s1;
+  double* o = Hp + (size_t)pair * nb;
+  const bool single = (wk.w & 1) != 0;
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) {
+    const long long v = (long long)lh[i];
+    const double d = (double)v * ((i & 1) ? i1 : i0);
+    if (single) o[i] = d;
+    else if (v != 0) gbl_add(o + i, d);
+  }
+  if (do_wyy) {
+    wyy = wave_sum(wyy);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = wyy;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const double t = red[0] + red[1] + red[2] + red[3];
+      if (single) pwyy[pair] = t;
+      else gbl_add(pwyy + pair, t);
+    }
+  }
+}
+
+template <typename CodeT, int MODE>
+static void pair_hist_launch(bool has_vb, bool posv, int n_work, size_t lds, hipStream_t s, const void* codes_col,
+                             long long ncol, const int* ridx, const float* va, const float* vb, const int4* work,
+                             const int* pfeat, int Bs, float s0, float s1, double* Hp, double* pwyy) {
+  const CodeT* cc = (const CodeT*)codes_col;
+#define PHL(V, PV)                                                                                                \
+  hipLaunchKernelGGL((pair_hist_kernel<CodeT, MODE, V, PV>), dim3(n_work), dim3(256), lds, s, cc, ncol, ridx, va, \
+                     vb, work, pfeat, Bs, s0, s1, Hp, pwyy)
+  if (has_vb) { if (posv) PHL(true, true); else PHL(true, false); }
+  else { if (posv) PHL(false, true); else PHL(false, false); }
+#undef PHL
+}
+
+// codes_col: [F][ncol] column-major codes (code_bytes 1 or 2); work: n_work x
+// int4 (pair, start, count, flags); pfeat[pair] = global feature; Hp:
+// [P][Bs][2] f64; pwyy: [P] f64 (MODE 0, may be null).
+extern "C" int h2o_pair_hist(const void* codes_col, int code_bytes, long long ncol, const int* ridx, const float* va,
+                             const float* vb, const int* work, int n_work, const int* pfeat, int Bs, int mode,
+                             int posv, float s0, float s1, double* Hp, double* pwyy, hipStream_t s) {
+  if (n_work <= 0) return 0;
+  if (Bs < 2 || Bs > 4096 || (mode != 0 && mode != 1) || (mode == 1 && vb == nullptr)) return -1;
+  const size_t lds = (size_t)Bs * 2 * sizeof(unsigned long long);
+  const int4* w = (const int4*)work;
+  const bool hv = vb != nullptr;
+  if (code_bytes == 1) {
+    if (mode == 0) pair_hist_launch<uint8_t, 0>(hv, posv, n_work, lds, s, codes_col, ncol, ridx, va, vb, w, pfeat, Bs, s0, s1, Hp, pwyy);
+    else pair_hist_launch<uint8_t, 1>(hv, posv, n_work, lds, s, codes_col, ncol, ridx, va, vb, w, pfeat, Bs, s0, s1, Hp, pwyy);
+  } else {
+    if (mode == 0) pair_hist_launch<uint16_t, 0>(hv, posv, n_work, lds, s, codes_col, ncol, ridx, va, vb, w, pfeat, Bs, s0, s1, Hp, pwyy);
+    else pair_hist_launch<uint16_t, 1>(hv, posv, n_work, lds, s, codes_col, ncol, ridx, va, vb, w, pfeat, Bs, s0, s1, Hp, pwyy);
+  }
+  return (int)hipGetLastError();
+}

@@ -485,3 +485,178 @@ extern "C" int h2o_cat_pairs(const double* H, int n, int Bs, int C, int P, const
   if (rc) return rc;
   return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------
+// Per-node winner + split record of the row-direct pair path.  The frontier's
+// pairs are node-major with kp pairs per node (the node's sampled features in
+// ascending order); res[2p] = gain, res[2p + 1] = k from cat_pair_kernel.
+// One workgroup per node: winner = largest gain, lowest feature on ties (the
+// reference scans columns in order and keeps the first best); the record and
+// go-left mask are rebuilt from the winner's own histogram Hp[pair] (for a
+// categorical winner the (mean response, bin) order is re-sorted in LDS, the
+// same key and tie rule as the scoring kernel), so the level needs no host
+// round trip: the output is split_select2_kernel's packed record
+//   pk[node] = {gain, feat, t, opt, L0, L1, R0, R1, T0, T1, ok}
+// plus mask[node][Bs] (all ones when the node does not split) and feat_out.
+// T = node totals from the winner's (or the first pair's) histogram.
+// ---------------------------------------------------------------------------
+template <int CRIT, int BP>
+__global__ __launch_bounds__(256) void pair_select_kernel(const double* __restrict__ Hp, int Bs, int kp,
+                                                          const double* __restrict__ res,
+                                                          const int* __restrict__ pfeat,
+                                                          const unsigned char* __restrict__ fcat, double min_w2,
+                                                          int stride, double* __restrict__ pk,
+                                                          uint8_t* __restrict__ mask, int* __restrict__ feat_out) {
+  __shared__ double sk[BP];
+  __shared__ int si[BP];
+  __shared__ double rg[4];
+  __shared__ int rj[4];
+  __shared__ double rs[4][4];
+  const int node = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int B = Bs - 1;
+  // winner over the node's kp pairs
+  double bg = -INFINITY;
+  int bj = 0x7fffffff;
+  for (int j = tid; j < kp; j += 256) {
+    const double g = res[2 * ((size_t)node * kp + j)];
+    if (g > bg || (g == bg && j < bj)) { bg = g; bj = j; }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const double og = __shfl_xor(bg, o, 64);
+    const int oj = __shfl_xor(bj, o, 64);
+    if (og > bg || (og == bg && oj < bj)) { bg = og; bj = oj; }
+  }
+  if (lane == 0) { rg[wv] = bg; rj[wv] = bj; }
+  __syncthreads();
+  bg = rg[0]; bj = rj[0];
+  for (int w = 1; w < 4; ++w)
+    if (rg[w] > bg || (rg[w] == bg && rj[w] < bj)) { bg = rg[w]; bj = rj[w]; }
+  const bool win = bg > -INFINITY && bj < kp;
+  const size_t pw = (size_t)node * kp + (win ? bj : 0);
+  const double* h = Hp + pw * (size_t)Bs * 2;
+  const int f = pfeat[pw];
+  const bool cat = win && fcat[f] != 0;
+  const int kk = win ? (int)res[2 * pw + 1] : 0;
+  const int nt = B - 1;
+  const int opt = kk < nt ? 0 : (kk < 2 * nt ? 1 : 2);
+  const int t = opt == 0 ? kk : (opt == 1 ? kk - nt : 0);
+  const bool na_left = opt == 1;
+  // rank of every non-NA bin in the split order
+  for (int b = tid; b < BP; b += 256) {
+    double key = INFINITY;
+    if (b < B) {
+      if (!cat) {
+        key = (double)b;
+      } else {
+        const double a0 = h[2 * (size_t)b], a1 = h[2 * (size_t)b + 1];
+        key = CRIT == 1 ? (a1 > 0 ? a0 / a1 : INFINITY) : (a0 > 0 ? a1 / a0 : INFINITY);
+      }
+    }
+    sk[b] = key;
+    si[b] = b;
+  }
+  __syncthreads();
+  if (cat) {
+    for (int k = 2; k <= BP; k <<= 1) {
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int i = tid; i < BP; i += 256) {
+          const int l = i ^ j;
+          if (l > i) {
+            const double a = sk[i], c = sk[l];
+            const int ia = si[i], ic = si[l];
+            const bool gt = a > c || (a == c && ia > ic);
+            const bool up = (i & k) == 0;
+            if (gt == up) { sk[i] = c; sk[l] = a; si[i] = ic; si[l] = ia; }
+          }
+        }
+        __syncthreads();
+      }
+    }
+  }
+  // sk[] is free now: reuse it as rank-by-bin
+  int* rank = reinterpret_cast<int*>(sk);   // BP ints fit in BP doubles
+  for (int r = tid; r < BP; r += 256) rank[si[r]] = r;
+  __syncthreads();
+  // left / total sums and the mask
+  double l0 = 0, l1 = 0, t0 = 0, t1 = 0, n0 = 0, n1 = 0;
+  for (int b = tid; b < Bs; b += 256) {
+    const double a0 = h[2 * (size_t)b], a1 = h[2 * (size_t)b + 1];
+    t0 += a0; t1 += a1;
+    bool left;
+    if (b >= B) {
+      left = na_left;
+    } else {
+      n0 += a0; n1 += a1;
+      const bool in_left = rank[b] <= t;
+      const double bw = CRIT == 1 ? a1 : a0;
+      const bool empty = cat && bw <= 0;
+      if (opt == 2) left = !empty || na_left;
+      else left = empty ? na_left : in_left;
+      if (opt != 2 && in_left) { l0 += a0; l1 += a1; }
+    }
+    mask[(size_t)node * Bs + b] = left ? 1 : 0;   // overwritten below when the node does not split
+  }
+  double v[6] = {l0, l1, t0, t1, n0, n1};
+#pragma unroll
+  for (int q = 0; q < 6; ++q) v[q] = wave_sum(v[q]);
+  __syncthreads();
+  __shared__ double red6[6][4];
+  if (lane == 0) {
+#pragma unroll
+    for (int q = 0; q < 6; ++q) red6[q][wv] = v[q];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 6; ++q) v[q] = red6[q][0] + red6[q][1] + red6[q][2] + red6[q][3];
+  const double na0 = v[2] - v[4], na1 = v[3] - v[5];
+  double L0, L1;
+  if (opt == 2) { L0 = v[4]; L1 = v[5]; }
+  else { L0 = v[0] + (na_left ? na0 : 0.0); L1 = v[1] + (na_left ? na1 : 0.0); }
+  const bool ok = win && isfinite(bg) && (min_w2 < 0.0 || v[2] >= min_w2);
+  if (tid == 0) {
+    double* o = pk + (size_t)node * stride;
+    o[0] = bg; o[1] = (double)f; o[2] = (double)t; o[3] = (double)opt;
+    o[4] = L0; o[5] = L1; o[6] = v[2] - L0; o[7] = v[3] - L1; o[8] = v[2]; o[9] = v[3];
+    o[10] = ok ? 1.0 : 0.0;
+    feat_out[node] = ok ? f : 0;
+  }
+  if (!ok) {
+    __syncthreads();
+    for (int b = tid; b < Bs; b += 256) mask[(size_t)node * Bs + b] = 1;
+  }
+}
+
+template <int CRIT>
+static int pair_select_launch(int BP, int n, hipStream_t s, const double* Hp, int Bs, int kp, const double* res,
+                              const int* pfeat, const unsigned char* fcat, double min_w2, int stride, double* pk,
+                              uint8_t* mask, int* feat_out) {
+#define PSK(bp)                                                                                                   \
+  case bp:                                                                                                        \
+    hipLaunchKernelGGL((pair_select_kernel<CRIT, bp>), dim3(n), dim3(256), 0, s, Hp, Bs, kp, res, pfeat, fcat, \
+                       min_w2, stride, pk, mask, feat_out);                                                       \
+    return 0;
+  switch (BP) {
+    PSK(256) PSK(512) PSK(1024) PSK(2048) PSK(4096)
+    default: return -2;
+  }
+#undef PSK
+}
+
+// n nodes x kp pairs (node-major); Hp [n*kp][Bs][2] f64; res [n*kp][2]
+// (cat_pair_kernel output); pfeat [n*kp] global feature ids; fcat [F] u8.
+extern "C" int h2o_pair_select(const double* Hp, int n, int Bs, int kp, const double* res, const int* pfeat,
+                               const unsigned char* fcat, int crit, double min_w2, int stride, double* pk,
+                               uint8_t* mask, int* feat_out, hipStream_t s) {
+  if (n <= 0) return 0;
+  if (kp <= 0 || Bs < 3 || stride < 11) return -1;
+  int BP = 256;
+  while (BP < Bs - 1) BP <<= 1;
+  if (BP > 4096) return -2;
+  const int rc = crit == 1 ? pair_select_launch<1>(BP, n, s, Hp, Bs, kp, res, pfeat, fcat, min_w2, stride, pk, mask,
+                                                   feat_out)
+                           : pair_select_launch<0>(BP, n, s, Hp, Bs, kp, res, pfeat, fcat, min_w2, stride, pk, mask,
+                                                   feat_out);
+  if (rc) return rc;
+  return (int)hipGetLastError();
+}

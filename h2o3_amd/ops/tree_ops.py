@@ -172,7 +172,9 @@ def channel_max(va, vb, mode):
         return [max(a[0], b[0]), max(a[1], b[1])]
     if mode == 0:
         w = vb if vb is not None else None
-        m1 = (va.abs() * (w.abs() if w is not None else 1)).max() if va.numel() else va.new_zeros(())
+        # NaN responses are zero-weight rows (NaN-masked payloads): not part of the bound
+        m1 = torch.nan_to_num(va.abs() * (w.abs() if w is not None else 1), nan=0.0).max() if va.numel() \
+            else va.new_zeros(())
         m0 = w.abs().max() if (w is not None and w.numel()) else va.new_ones(())
     elif mode == 1:
         m0, m1 = va.abs().max(), vb.abs().max()
@@ -339,6 +341,153 @@ def _hist_build_torch(bd, ridx, va, vb, mode, starts, counts, hist):
         flat.index_add_(0, idx, v)
         hist[:, slot] = flat.reshape(F, Bs, C)
     return hist
+
+
+_PAIR_CHUNK = 16384
+
+
+def pair_hist(bd, ridx, va, vb, mode, node_st, node_ct, pair_node, pair_feat, vmax=None, posv=False,
+              want_wyy=False, use_native=None, chunk=_PAIR_CHUNK):
+    """Histograms of (node, feature) PAIRS straight from the rows (the
+    mtries-sampled columns of a wide frontier, DRF deep levels): pair i covers
+    the rows of node pair_node[i] (segment [node_st, node_st + node_ct) of
+    ridx) on feature pair_feat[i] (global index).  node_st / node_ct /
+    pair_node / pair_feat are host int arrays; pairs of one node must be
+    consecutive.  Returns (Hp [P, Bs, 2] float64, wyy [n_nodes] float64 or
+    None): wyy = per-node sum of w*y*y (mode 0), taken from each node's first
+    pair.  mode 0: (w, w*y) with vb = weights (or NaN-masked va when vb is
+    None); mode 1: (g, h).  HIP kernel `pair_hist_kernel` (tree_hist.hip) on
+    the GPU, an index_add reference otherwise."""
+    assert mode in (0, 1)
+    dev = ridx.device
+    st = np.asarray(node_st, dtype=np.int64)
+    ct = np.asarray(node_ct, dtype=np.int64)
+    pn = np.asarray(pair_node, dtype=np.int64)
+    pf = np.asarray(pair_feat, dtype=np.int64)
+    P, n = pn.size, st.size
+    Bs = bd.Bs
+    first = np.ones(P, dtype=bool)
+    first[1:] = pn[1:] != pn[:-1]
+    wyy_n = torch.zeros(n, dtype=torch.float64, device=dev) if (want_wyy and mode == 0) else None
+    native = (dev.type == "cuda" and bd.codes_col is not None) if use_native is None else use_native
+    if P == 0:
+        return torch.zeros((0, Bs, 2), dtype=torch.float64, device=dev), wyy_n
+    if native:
+        lib = _lib()
+        if not getattr(lib, "_typed_pair", False):
+            lib.h2o_pair_hist.argtypes = [_c_void, _c_int, _c_ll, _c_void, _c_void, _c_void, _c_void, _c_int,
+                                          _c_void, _c_int, _c_int, _c_int, ctypes.c_float, ctypes.c_float, _c_void,
+                                          _c_void, _c_void]
+            lib._typed_pair = True
+        pct = ct[pn]
+        nch = np.maximum((pct + chunk - 1) // chunk, 0)
+        live = pct > 0
+        rep = np.repeat(np.arange(P), nch)
+        k = np.arange(int(nch.sum())) - np.repeat(np.cumsum(nch) - nch, nch)
+        start = st[pn][rep] + k * chunk
+        cnt = np.minimum(chunk, pct[rep] - k * chunk)
+        flags = (nch[rep] == 1).astype(np.int64) | first[rep].astype(np.int64) * 2
+        items = np.stack([rep, start, cnt, flags], 1).astype(np.int32)
+        Hp = torch.empty((P, Bs, 2), dtype=torch.float64, device=dev)
+        multi = np.nonzero((nch > 1) | ~live)[0]
+        if multi.size:
+            Hp.index_fill_(0, _h2d(multi.astype(np.int64), dev), 0.0)
+        pwyy = torch.zeros(P, dtype=torch.float64, device=dev) if wyy_n is not None else None
+        if len(items):
+            buf = _h2d(np.concatenate([items.reshape(-1), pf.astype(np.int32)]), dev)
+            work, pfd = buf[:4 * len(items)], buf[4 * len(items):]
+            if vmax is None:
+                vmax = channel_max(va, vb, mode)
+            s0, s1 = (fixed_point_scale(m, min(chunk, int(pct.max()))) for m in vmax)
+            rc = lib.h2o_pair_hist(_ptr(bd.codes_col), bd.code_bytes, bd.codes_col.stride(0), _ptr(ridx), _ptr(va),
+                                   _ptr(vb), _ptr(work), len(items), _ptr(pfd), Bs, mode, 1 if posv else 0, s0, s1,
+                                   _ptr(Hp), _ptr(pwyy), _stream())
+            if rc != 0:
+                raise RuntimeError(f"h2o_pair_hist failed: {rc}")
+        if wyy_n is not None:
+            fi = np.nonzero(first)[0]
+            wyy_n[_h2d(pn[fi], dev)] = pwyy[_h2d(fi.astype(np.int64), dev)]
+        return Hp, wyy_n
+    # reference path: expand every pair's rows, one index_add
+    if posv:
+        va_r = torch.empty_like(va)
+        va_r[ridx.long()] = va
+        vb_r = None
+        if vb is not None:
+            vb_r = torch.empty_like(vb)
+            vb_r[ridx.long()] = vb
+        va, vb = va_r, vb_r
+    pct = torch.as_tensor(ct[pn], device=dev)
+    tot = int(pct.sum())
+    Hp = torch.zeros((P, Bs, 2), dtype=torch.float64, device=dev)
+    if tot == 0:
+        return Hp, wyy_n
+    prep = torch.repeat_interleave(torch.arange(P, device=dev), pct)
+    off = torch.arange(tot, device=dev) - torch.repeat_interleave(torch.cumsum(pct, 0) - pct, pct)
+    pos = torch.as_tensor(st[pn], device=dev)[prep] + off
+    rows = ridx[pos].long()
+    feat = torch.as_tensor(pf, device=dev)[prep]
+    code = bd.codes_col[feat, rows].to(torch.int64) if bd.codes_col is not None else \
+        bd.codes[rows, feat].to(torch.int64)
+    code = code & 0xFFFF if bd.code_bytes == 2 else code
+    a = va[rows].to(torch.float64)
+    if mode == 0:
+        w = vb[rows].to(torch.float64) if vb is not None else (~torch.isnan(a)).to(torch.float64)
+        a = torch.nan_to_num(a) if vb is None else a
+        vals = torch.stack([w, w * a], 1)
+    else:
+        vals = torch.stack([a, vb[rows].to(torch.float64)], 1)
+    Hp.view(-1, 2).index_add_(0, prep * Bs + code, vals)
+    if wyy_n is not None:
+        fp = torch.as_tensor(first, device=dev)[prep]
+        nodes = torch.as_tensor(pn, device=dev)[prep]
+        wyy_n.index_add_(0, nodes[fp], (vals[:, 1] * a)[fp])
+    return Hp, wyy_n
+
+
+def pair_hist_dev(bd, ridx, va, vb, mode, node_st, node_ct, sel, vmax, posv=False, chunk=_PAIR_CHUNK):
+    """pair_hist for a frontier whose pairs are given ON THE DEVICE: sel
+    [n, k] global feature ids per node (node-major pairs p = i * k + j), so
+    no pair list crosses to the host.  node_st / node_ct: host arrays.  The
+    work list is the host's per-node chunk table expanded by k on the device.
+    Returns (Hp [n*k, Bs, 2] f64, wyy [n] f64 or None, pfeat [n*k] int32)."""
+    dev = ridx.device
+    lib = _lib()
+    if not getattr(lib, "_typed_pair", False):
+        lib.h2o_pair_hist.argtypes = [_c_void, _c_int, _c_ll, _c_void, _c_void, _c_void, _c_void, _c_int,
+                                      _c_void, _c_int, _c_int, _c_int, ctypes.c_float, ctypes.c_float, _c_void,
+                                      _c_void, _c_void]
+        lib._typed_pair = True
+    st = np.asarray(node_st, dtype=np.int64)
+    ct = np.asarray(node_ct, dtype=np.int64)
+    n, k = sel.shape
+    P = n * k
+    Bs = bd.Bs
+    nch = (ct + chunk - 1) // chunk
+    rep = np.repeat(np.arange(n), nch)
+    c = np.arange(int(nch.sum())) - np.repeat(np.cumsum(nch) - nch, nch)
+    tab = np.stack([rep, st[rep] + c * chunk, np.minimum(chunk, ct[rep] - c * chunk), (nch[rep] == 1)], 1)
+    multi = np.nonzero((nch > 1) | (ct == 0))[0]
+    tab_d = _h2d(np.concatenate([tab.astype(np.int32).reshape(-1), multi.astype(np.int32)]), dev)
+    m = len(tab)
+    items = tab_d[:4 * m].view(m, 1, 4).expand(m, k, 4).clone()
+    j = torch.arange(k, dtype=torch.int32, device=dev).view(1, k)
+    items[:, :, 0] = items[:, :, 0] * k + j
+    items[:, :, 3] += (j == 0).to(torch.int32) * 2
+    pfeat = sel.to(torch.int32).reshape(-1).contiguous()
+    Hp = torch.empty((P, Bs, 2), dtype=torch.float64, device=dev)
+    if multi.size:
+        Hp.view(n, -1).index_fill_(0, tab_d[4 * m:].long(), 0.0)
+    want_wyy = mode == 0
+    pwyy = torch.zeros(P, dtype=torch.float64, device=dev) if want_wyy else None
+    if m:
+        s0, s1 = (fixed_point_scale(v, min(chunk, int(ct.max()))) for v in vmax)
+        rc = lib.h2o_pair_hist(_ptr(bd.codes_col), bd.code_bytes, bd.codes_col.stride(0), _ptr(ridx), _ptr(va),
+                               _ptr(vb), _ptr(items), m * k, _ptr(pfeat), Bs, mode, 1 if posv else 0, s0, s1,
+                               _ptr(Hp), _ptr(pwyy), _stream())
+        if rc != 0:
+            raise RuntimeError(f"h2o_pair_hist failed: {rc}")
+    return Hp, (pwyy.view(n, k)[:, 0].contiguous() if want_wyy else None), pfeat
 
 
 def partition(bd, ridx, ridx_out, feats, masks, starts, counts, use_native=None, chunk=16384, payload=None):

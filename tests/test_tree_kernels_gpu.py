@@ -396,6 +396,7 @@ def test_drf_chunked_need_mask_same_model(F, monkeypatch):
     df["y"] = X[:, 0] + X[:, 7] * X[:, 30] + 0.1 * rng.randn(n)
     fr = h2o3_amd.H2OFrame(df)
     monkeypatch.setenv("H2O3_HIST_BUDGET", str(1 << 20))   # force the chunked path
+    monkeypatch.setenv("H2O3_PAIR_DIRECT", "0")             # the node-batched level histograms
     preds = []
     for flag in ("0", "1"):
         monkeypatch.setenv("H2O3_HIST_NEED", flag)
@@ -492,4 +493,61 @@ def test_lookahead_levels_same_model(dist, monkeypatch):
         m = H2OXGBoostEstimator(ntrees=4, max_depth=6, seed=3)
         m.train(y="y", training_frame=fr)
         preds.append(m.predict(fr).as_data_frame().values[:, -1].astype(float))
+    np.testing.assert_allclose(preds[0], preds[1], rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("nbins", [255, 1000])
+@pytest.mark.parametrize("mode,weights,posv", [(0, False, False), (0, True, False), (0, False, True), (1, True, False)])
+@pytest.mark.parametrize("chunk", [16384, 700])
+def test_pair_hist_matches_reference(nbins, mode, weights, posv, chunk):
+    """Row-direct pair histograms (pair_hist_kernel, 1- and 2-byte codes,
+    single-item stores and multi-item atomics) vs the index_add reference."""
+    _need_gpu()
+    from h2o3_amd.ops import tree_ops
+    bd, _ = _binned(nbins=nbins)
+    n = bd.nrows_local
+    g = torch.Generator(device="cuda").manual_seed(3)
+    ridx = torch.randperm(n, generator=g, device="cuda").to(torch.int32)
+    va = torch.randn(n, generator=g, device="cuda")
+    if mode == 0 and not weights:
+        va[torch.rand(n, generator=g, device="cuda") < 0.1] = float("nan")   # zero-weight rows
+    vb = torch.rand(n, generator=g, device="cuda") if weights else None
+    st, ct = [0, 3000, 3100, 9000], [3000, 100, 5900, 11000]
+    pn = [0, 0, 1, 2, 2, 2, 3, 3]
+    pf = [1, 4, 0, 2, 4, 12, 3, 9]
+    kw = dict(posv=posv, want_wyy=True, chunk=chunk)
+    Hg, wg = tree_ops.pair_hist(bd, ridx, va, vb, mode, st, ct, pn, pf, use_native=True, **kw)
+    Hr, wr = tree_ops.pair_hist(bd, ridx, va, vb, mode, st, ct, pn, pf, use_native=False, **kw)
+    torch.testing.assert_close(Hg, Hr, rtol=1e-5, atol=1e-4)
+    if mode == 0:
+        torch.testing.assert_close(wg, wr, rtol=1e-5, atol=1e-3)
+    # every pair of a node sums to the node totals
+    tot = Hg.sum(1)
+    torch.testing.assert_close(tot[0], tot[1])
+    torch.testing.assert_close(tot[3], tot[5])
+
+
+@pytest.mark.parametrize("cats", [False, True])
+def test_drf_direct_pairs_same_model(cats, monkeypatch):
+    """DRF with mtries grown from row-direct pair histograms at every level
+    gives the same forest as the level-histogram path."""
+    _need_gpu()
+    import pandas as pd
+    import h2o3_amd
+    from h2o3_amd.estimators import H2ORandomForestEstimator
+    h2o3_amd.init(device="cuda:0", verbose=False)
+    rng = np.random.RandomState(0)
+    n, F = 20000, 40
+    X = rng.randn(n, F).astype(np.float32)
+    df = pd.DataFrame(X, columns=[f"x{i}" for i in range(F)])
+    if cats:
+        df["c"] = pd.Categorical([f"L{v}" for v in rng.randint(0, 300, n)])
+    df["y"] = X[:, 0] + X[:, 7] * X[:, 30] + 0.1 * rng.randn(n)
+    fr = h2o3_amd.H2OFrame(df)
+    preds = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("H2O3_PAIR_DIRECT", flag)
+        m = H2ORandomForestEstimator(ntrees=3, max_depth=14, seed=7, mtries=6)
+        m.train(y="y", training_frame=fr)
+        preds.append(m.predict(fr).as_data_frame().values[:, 0])
     np.testing.assert_allclose(preds[0], preds[1], rtol=1e-6, atol=1e-6)

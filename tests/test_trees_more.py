@@ -123,3 +123,54 @@ def test_pair_splits_match_dense(crit):
     torch.testing.assert_close(a["gain"][fin], b["gain"][fin])
     assert torch.equal(a["feat"][fin], b["feat"][fin])
     assert torch.equal(a["mask"][fin], b["mask"][fin])
+
+
+@pytest.mark.parametrize("algo", ["drf", "gbm_colsample", "xgb_colsample"])
+def test_direct_pair_levels_match_level_histograms(algo, monkeypatch):
+    """Column-sampled levels grown from row-direct (node, feature) pair
+    histograms (tree_ops.pair_hist, H2O3_PAIR_DIRECT=1) give the same trees
+    as the level-histogram path (=0): numeric + categorical + NA features."""
+    from h2o3_amd.estimators import H2OGradientBoostingEstimator
+    h2o3_amd.init(verbose=False)
+    rng = np.random.RandomState(1)
+    n = 2500
+    X = rng.randn(n, 8)
+    X[rng.rand(n, 8) < 0.05] = np.nan
+    df = pd.DataFrame(X, columns=[f"x{i}" for i in range(8)])
+    df["c"] = rng.choice([f"k{i}" for i in range(12)], n)
+    df["y"] = np.where(np.nan_to_num(X[:, 0]) - np.nan_to_num(X[:, 2]) + (df.c.str[1:].astype(int) % 3 == 0)
+                       + 0.3 * rng.randn(n) > 0.3, "p", "q")
+    fr = h2o3_amd.H2OFrame(df)
+    preds = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("H2O3_PAIR_DIRECT", flag)
+        if algo == "drf":
+            m = H2ORandomForestEstimator(ntrees=3, max_depth=10, mtries=3, seed=5)
+        elif algo == "gbm_colsample":
+            m = H2OGradientBoostingEstimator(ntrees=4, max_depth=6, col_sample_rate=0.5, seed=5)
+        else:
+            m = H2OXGBoostEstimator(ntrees=4, max_depth=6, col_sample_rate=0.5, seed=5)
+        m.train(y="y", training_frame=fr)
+        preds.append(m.predict(fr).as_data_frame()["p"].values)
+    np.testing.assert_allclose(preds[0], preds[1], atol=1e-6)
+
+
+def test_pair_hist_reference_matches_level_hist():
+    """pair_hist (reference path) equals the matching slices of hist_build."""
+    import torch
+    from h2o3_amd.models.tree.binning import bin_frame_tensors
+    from h2o3_amd.ops import tree_ops
+    g = torch.Generator().manual_seed(0)
+    n, F = 4000, 6
+    feats = [torch.randn(n, generator=g) for _ in range(F)]
+    bd = bin_frame_tensors(feats, [False] * F, [0] * F, [f"f{i}" for i in range(F)], nbins=50)
+    ridx = torch.randperm(n, generator=g).to(torch.int32)
+    va, vb = torch.randn(n, generator=g), torch.rand(n, generator=g)
+    st, ct = [0, 1500], [1500, 2500]
+    H = tree_ops.hist_build(bd, ridx, va, vb, 0, st, ct, 2, use_native=False)
+    pn, pf = [0, 0, 1], [2, 5, 1]
+    Hp, wyy = tree_ops.pair_hist(bd, ridx, va, vb, 0, st, ct, pn, pf, want_wyy=True, use_native=False)
+    for i, (a, f) in enumerate(zip(pn, pf)):
+        torch.testing.assert_close(Hp[i], H[f, a])
+    r = ridx[:1500].long()
+    torch.testing.assert_close(wyy[0], (vb[r].double() * va[r].double() ** 2).sum())
