@@ -222,14 +222,14 @@ class H2OExtendedIsolationForestEstimator(H2OEstimator):
 
     def _grow(self, S, ext, rng):
         P = S.shape[1]
-        nodes = []  # (normal[P], point[P], left, right, value)
+        nodes = []  # (normal[P], point[P], left, right, value, rows)
 
         def build(idx, d):
             me = len(nodes)
             nodes.append(None)
             rows = S[idx]
             if d >= self._height or len(idx) <= 1:
-                nodes[me] = (None, None, -1, -1, d + c_factor(len(idx)))
+                nodes[me] = (None, None, -1, -1, d + c_factor(len(idx)), len(idx))
                 return me
             nvec = rng.normal(size=P)
             zero = rng.choice(P, size=max(0, P - ext - 1), replace=False)
@@ -239,11 +239,11 @@ class H2OExtendedIsolationForestEstimator(H2OEstimator):
             proj = (np.nan_to_num(rows) - pt) @ nvec
             left = proj <= 0
             if left.all() or (~left).all():
-                nodes[me] = (None, None, -1, -1, d + c_factor(len(idx)))
+                nodes[me] = (None, None, -1, -1, d + c_factor(len(idx)), len(idx))
                 return me
             l = build(idx[left], d + 1)
             r = build(idx[~left], d + 1)
-            nodes[me] = (nvec, pt, l, r, 0.0)
+            nodes[me] = (nvec, pt, l, r, 0.0, len(idx))
             return me
         build(np.arange(len(S)), 0)
         return nodes
@@ -254,14 +254,15 @@ class H2OExtendedIsolationForestEstimator(H2OEstimator):
         base = 0
         for tr in self._trees:
             roots.append(base)
-            for nv, pt, l, r, v in tr:
-                if P is None and nv is not None:
-                    P = len(nv)
+            for nd in tr:
+                if P is None and nd[0] is not None:
+                    P = len(nd[0])
             base += len(tr)
         P = P or 1
         base = 0
         for ti, tr in enumerate(self._trees):
-            for nv, pt, l, r, v in tr:
+            for nd in tr:
+                nv, pt, l, r, v = nd[:5]
                 normals.append(nv if nv is not None else np.zeros(P))
                 points.append(pt if pt is not None else np.zeros(P))
                 lefts.append(l + base if l >= 0 else -1)

@@ -1,6 +1,8 @@
 """MOJO export in the reference's h2o-genmodel layout.
 
-`build_h2o_mojo(model)` writes GBM, DRF and GLM models as the reference's
+`build_h2o_mojo(model)` writes GBM, DRF, GLM, K-Means, Isolation Forest,
+Extended Isolation Forest, Deep Learning, Word2Vec and Stacked Ensemble
+models as the reference's
 MOJO zip -- model.ini ([info] / [columns] / [domains]), domains/dNNN.txt and,
 for trees, the compressed tree byte streams trees/tCC_GGG.bin with their
 _aux.bin node records -- so the reference's Java scorer (h2o-genmodel
@@ -14,6 +16,9 @@ Format parity (behaviour studied, not translated):
                                              tree byte layout read by scoreTree (mojo 1.40)
   hex/genmodel/algos/tree/SharedTreeMojoModel.java:704  AuxInfo records (40 bytes per split)
   hex/genmodel/algos/gbm/GbmMojoModel.java, drf/DrfMojoModel.java, glm/Glm*MojoModel.java
+  hex/genmodel/algos/kmeans/KMeansMojoReader.java, isofor/IsolationForestMojoReader.java,
+  isoforextended/ExtendedIsolationForestMojoReader.java, deeplearning/DeeplearningMojoReader.java,
+  word2vec/Word2VecMojoReader.java, ensemble/StackedEnsembleMojoReader.java
 """
 from __future__ import annotations
 
@@ -57,9 +62,26 @@ class _Zip:
     def write(self, name, data):
         self.z.writestr(name, data)
 
+    def nested(self, prefix):
+        return _Prefixed(self, prefix)
+
     def close(self) -> bytes:
         self.z.close()
         return self.buf.getvalue()
+
+
+class _Prefixed:
+    """Writes into a parent zip under a directory prefix (Stacked Ensemble
+    sub-models: models/<algo>/<key>/...)."""
+
+    def __init__(self, z, prefix):
+        self.z, self.prefix = z, prefix
+
+    def write(self, name, data):
+        self.z.write(self.prefix + name, data)
+
+    def nested(self, prefix):
+        return _Prefixed(self.z, self.prefix + prefix)
 
 
 def _threshold(model):
@@ -72,11 +94,12 @@ def _threshold(model):
     return thr
 
 
-def _header(model, algo_short, algo_full, category, columns, nfeatures, nclasses, domains, mojo_version, extra):
+def _header(model, algo_short, algo_full, category, columns, nfeatures, nclasses, domains, mojo_version, extra,
+            supervised=True):
     info = {
         "h2o_version": "3.46.0.99999", "mojo_version": mojo_version, "license": "Apache License Version 2.0",
         "algo": algo_short, "algorithm": algo_full, "endianness": "LITTLE_ENDIAN", "category": category,
-        "uuid": str(abs(hash(model.model_id)) % (1 << 62)), "supervised": True, "n_features": nfeatures,
+        "uuid": str(abs(hash(model.model_id)) % (1 << 62)), "supervised": supervised, "n_features": nfeatures,
         "n_classes": nclasses, "n_columns": len(columns), "n_domains": sum(d is not None for d in domains),
         "balance_classes": False, "default_threshold": _threshold(model),
         "prior_class_distrib": None, "model_class_distrib": None,
@@ -186,19 +209,20 @@ def _encode_aux(tree, leaf_map=None):
     return bytes(out)
 
 
-def _tree_model(model, z, algo_short, algo_full, extra, leaf_maps):
+def _tree_model(model, z, algo_short, algo_full, extra, leaf_maps, supervised=True, category=None):
     spec = model._spec
     x = list(spec.x)
     xd = getattr(model, "_x_domains", {}) or {}
-    columns = x + [spec.y]
-    domains = [xd.get(c) for c in x] + [list(spec.response_domain) if spec.response_domain else None]
+    columns = x + ([spec.y] if supervised else [])
+    domains = [xd.get(c) for c in x] + ([list(spec.response_domain) if spec.response_domain else None]
+                                        if supervised else [])
     K = model._n_tree_classes()
     ng = len(model._forest) // max(K, 1)
-    cat = "Binomial" if spec.nclasses == 2 else "Multinomial" if spec.nclasses > 2 else "Regression"
+    cat = category or ("Binomial" if spec.nclasses == 2 else "Multinomial" if spec.nclasses > 2 else "Regression")
     info = {"n_trees": ng, "n_trees_per_class": K, "_genmodel_encoding": "AUTO"}
     info.update(extra)
-    ini, files = _header(model, algo_short, algo_full, cat, columns, len(x), spec.nclasses, domains,
-                         TREE_MOJO_VERSION, info)
+    ini, files = _header(model, algo_short, algo_full, cat, columns, len(x), spec.nclasses if supervised else 1,
+                         domains, TREE_MOJO_VERSION, info, supervised=supervised)
     z.write("model.ini", ini)
     for k, v in files.items():
         z.write(k, v)
@@ -299,17 +323,222 @@ def _glm(model, z):
         z.write(k, v)
 
 
+# ------------------------------------------------------------ isolation forests
+def _isofor(model, z):
+    """IsolationForestMojoModel: tree sums of path lengths, normalised by the
+    integer min / max total path length of the training rows (the reference
+    keeps them as ints: IsolationForestMojoModel.java:7)."""
+    nt = max(1, len(model._forest))
+    extra = {"min_path_length": int(round(model._min_len * nt)), "max_path_length": int(round(model._max_len * nt)),
+             "output_anomaly_flag": model._threshold is not None}
+    if model._threshold is not None:
+        extra["default_threshold"] = float(model._threshold)
+    _tree_model(model, z, "isolationforest", "Isolation Forest", extra, lambda k, g: None, supervised=False,
+                category="AnomalyDetection")
+
+
+def _eif(model, z):
+    """ExtendedIsolationForestMojoModel: one blob per tree -- int32 vector size
+    k, then heap-numbered records (int32 node number; 'N' + k normal f64 + k
+    point f64, or 'L' + int32 rows)."""
+    di = model._dinfo
+    if di.cat_cols:
+        raise NotImplementedError("reference-layout Extended Isolation Forest MOJOs score numeric columns only")
+    x = list(di.num_cols)
+    P = len(x)
+    ini, files = _header(model, "extendedisolationforest", "Extended Isolation Forest", "AnomalyDetection", x, P, 1,
+                         [None] * P, "1.00", {"ntrees": len(model._trees), "sample_size": int(model._psi)},
+                         supervised=False)
+    z.write("model.ini", ini)
+    for k, v in files.items():
+        z.write(k, v)
+    for t, nodes in enumerate(model._trees):
+        out = bytearray(struct.pack("<i", P))
+        stack = [(0, 0)]                       # (our node index, heap number)
+        recs = []
+        while stack:
+            i, num = stack.pop()
+            nd = nodes[i]
+            if nd[2] < 0:
+                if len(nd) < 6:
+                    raise NotImplementedError("this Extended Isolation Forest predates leaf row counts: retrain it")
+                recs.append((num, b"L" + struct.pack("<i", int(nd[5]))))
+            else:
+                recs.append((num, b"N" + np.asarray(nd[0], dtype="<f8").tobytes() +
+                             np.asarray(nd[1], dtype="<f8").tobytes()))
+                stack.append((nd[3], 2 * num + 2))
+                stack.append((nd[2], 2 * num + 1))
+        for num, body in sorted(recs):
+            out += struct.pack("<i", num) + body
+        z.write("trees/t%02d.bin" % t, bytes(out))
+
+
+# ------------------------------------------------------------------ K-Means
+def _kmeans(model, z):
+    """KMeansMojoModel: columns in the clustering order (categoricals first),
+    per-column standardisation means / multipliers / modes (-1 = numeric) and
+    the centers in that space -- a categorical center is its level index (the
+    one-hot block of our clustering space holds the mode at 1/sqrt(2), so the
+    mismatch distance is the reference's 0/1)."""
+    di = model._dinfo
+    cats, nums = list(di.cat_cols), list(di.num_cols)
+    columns = cats + nums
+    domains = [list(di.domains[c]) for c in cats] + [None] * len(nums)
+    C = model._C_std[:, :di.P].detach().cpu().numpy().astype(np.float64)
+    centers = []
+    for r in range(C.shape[0]):
+        row = []
+        for c in cats:
+            off, L = di.cat_offsets[c], len(di.domains[c])
+            row.append(float(np.argmax(C[r, off:off + L])))
+        row += [float(v) for v in C[r, di.n_cat_expanded:di.P]]
+        centers.append(row)
+    extra = {"standardize": bool(di.standardize), "center_num": len(centers)}
+    if di.standardize:
+        extra["standardize_means"] = [0.0] * len(cats) + [float(m) for m in di.means]
+        extra["standardize_mults"] = [0.0] * len(cats) + [1.0 / float(s) for s in di.sigmas]
+        extra["standardize_modes"] = [int(di.cat_modes[c]) for c in cats] + [-1] * len(nums)
+    for i, row in enumerate(centers):
+        extra[f"center_{i}"] = row
+    ini, files = _header(model, "kmeans", "K-means", "Clustering", columns, len(columns), 1, domains, "1.00", extra,
+                         supervised=False)
+    z.write("model.ini", ini)
+    for k, v in files.items():
+        z.write(k, v)
+
+
+# ------------------------------------------------------------ Deep Learning
+_DL_ACT = {"tanh": "Tanh", "rectifier": "Rectifier", "maxout": "Maxout", "exprectifier": "ExpRectifier"}
+
+
+def _deeplearning(model, z):
+    """DeepLearningMojoModel: one-hot categoricals with a trailing missing
+    bucket per variable (GenModel.setInput), standardised numerics
+    (norm_mul = 1 / sigma, norm_sub = mean), the regression response scale,
+    and row-major float weights per layer.  Our NA handling (categorical
+    mode, numeric mean) is expressed exactly: the missing bucket's weights
+    are the mode level's, a missing numeric standardises to 0."""
+    if model._ae:
+        raise NotImplementedError("reference-layout MOJO export of deep learning autoencoders is not implemented")
+    di = model._dinfo
+    spec = model._spec
+    cats, nums = list(di.cat_cols), list(di.num_cols)
+    columns = cats + nums + [spec.y]
+    domains = [list(di.domains[c]) for c in cats] + [None] * len(nums) + \
+        [list(spec.response_domain) if spec.response_domain else None]
+    # expanded input map: reference column -> our design column (or -1 = zero)
+    offs, src = [0], []
+    for c in cats:
+        L = len(di.domains[c])
+        lv = list(range(L)) if di.use_all else list(range(1, L))
+        ours = [di.cat_offsets[c] + (l if di.use_all else l - 1) for l in lv]
+        mode = int(di.cat_modes[c])
+        na = di.cat_offsets[c] + (mode if di.use_all else mode - 1) if (di.use_all or mode > 0) else -1
+        src += ours + [na]
+        offs.append(offs[-1] + len(ours) + 1)
+    src += [di.n_cat_expanded + j for j in range(len(nums))]
+    src = np.asarray(src, dtype=np.int64)
+    layers = model._layers
+    act_name = str(model._parms.get("activation") or "Rectifier")
+    units = [len(src)] + [L.fout for L in layers]
+    extra = {"nums": len(nums), "cats": len(cats), "cat_offsets": offs, "use_all_factor_levels": bool(di.use_all),
+             "activation": act_name, "distribution": model._dist.family if spec.nclasses <= 1 else
+             ("bernoulli" if spec.nclasses == 2 else "multinomial"),
+             "mean_imputation": True, "cat_modes": [int(di.cat_modes[c]) for c in cats], "mini_batch_size": 1,
+             "neural_network_sizes": units,
+             "hidden_dropout_ratios": [float(L.drop) for L in layers[:-1]], "_genmodel_encoding": "AUTO"}
+    if di.standardize and nums:
+        extra["norm_mul"] = [1.0 / float(s) for s in di.sigmas]
+        extra["norm_sub"] = [float(m) for m in di.means]
+    if spec.nclasses <= 1:
+        extra["norm_resp_mul"] = [1.0 / float(model._ysd)]
+        extra["norm_resp_sub"] = [float(model._ymu)]
+    for li, L in enumerate(layers):
+        W = L.W.detach().cpu().numpy().astype(np.float64)
+        b = L.b.detach().cpu().numpy().astype(np.float64)
+        if li == 0:
+            Wr = np.zeros((W.shape[0], len(src)))
+            ok = src >= 0
+            Wr[:, ok] = W[:, src[ok]]
+            W = Wr
+        if L.k > 1:
+            # ours: row 2u + j; the reference: [unit][input][piece]
+            W = W.reshape(L.fout, L.k, -1).transpose(0, 2, 1)
+        extra[f"weight_layer{li}"] = [float(v) for v in np.asarray(W, dtype=np.float32).reshape(-1)]
+        extra[f"bias_layer{li}"] = [float(v) for v in b]
+    cat = "Binomial" if spec.nclasses == 2 else "Multinomial" if spec.nclasses > 2 else "Regression"
+    ini, files = _header(model, "deeplearning", "Deep Learning", cat, columns, len(cats) + len(nums), spec.nclasses,
+                         domains, "1.10", extra)
+    z.write("model.ini", ini)
+    for k, v in files.items():
+        z.write(k, v)
+
+
+# ----------------------------------------------------------------- Word2Vec
+def _word2vec(model, z):
+    """Word2VecMojoModel: `vocabulary` (one word per line, newlines escaped)
+    and `vectors` (big-endian float32, vocab x vec_size)."""
+    V = model._vecs.detach().cpu().numpy().astype(">f4")
+    ini, files = _header(model, "word2vec", "Word2Vec", "WordEmbedding", ["C1"], 1, 1, [None], "1.00",
+                         {"vec_size": int(V.shape[1]), "vocab_size": int(V.shape[0])}, supervised=False)
+    z.write("model.ini", ini)
+    z.write("vocabulary", "\n".join(w.replace("\n", "\\n") for w in model._vocab) + "\n")
+    z.write("vectors", V.tobytes())
+
+
+# ---------------------------------------------------------- Stacked Ensemble
+def _stackedensemble(model, z):
+    """StackedEnsembleMojoModel: every base model and the metalearner as a
+    nested reference-layout MOJO under models/<algo>/<key>/, the base models'
+    inputs remapped by column name from the ensemble's columns."""
+    spec = model._spec
+    x = list(spec.x)
+    for bm in model._base:
+        for c in bm._spec.x:
+            if c not in x:
+                x.append(c)
+    columns = x + [spec.y]
+    xd = {}
+    for bm in model._base:
+        xd.update(getattr(bm, "_x_domains", None) or (bm._dinfo.domains if hasattr(bm, "_dinfo") else {}))
+    domains = [xd.get(c) for c in x] + [list(spec.response_domain) if spec.response_domain else None]
+    subs = list(model._base) + [model._meta]
+    extra = {"submodel_count": len(subs), "base_models_num": len(model._base), "metalearner": model._meta.model_id,
+             "metalearner_transform": "NONE"}
+    for i, m in enumerate(subs):
+        d = f"models/{m.algo}/{m.model_id}/"
+        extra[f"submodel_key_{i}"] = m.model_id
+        extra[f"submodel_dir_{i}"] = d
+        _write_algo(m, z.nested(d))
+    for i, m in enumerate(model._base):
+        extra[f"base_model{i}"] = m.model_id
+    cat = "Binomial" if spec.nclasses == 2 else "Multinomial" if spec.nclasses > 2 else "Regression"
+    ini, files = _header(model, "stackedensemble", "StackedEnsemble", cat, columns, len(x), spec.nclasses, domains,
+                         "1.01", extra)
+    z.write("model.ini", ini)
+    for k, v in files.items():
+        z.write(k, v)
+
+
+_WRITERS = {"gbm": _gbm, "drf": _drf, "glm": _glm, "kmeans": _kmeans, "isolationforest": _isofor,
+            "extendedisolationforest": _eif, "deeplearning": _deeplearning, "word2vec": _word2vec,
+            "stackedensemble": _stackedensemble}
+
+
+def _write_algo(model, z):
+    if model.algo == "glm" and getattr(model, "_hglm", None) is not None:
+        raise NotImplementedError("HGLM models have no MOJO (as in the reference)")
+    w = _WRITERS.get(model.algo)
+    if w is None:
+        raise NotImplementedError(f"reference-layout MOJO export is not implemented for {model.algo} "
+                                  f"(supported: {', '.join(sorted(_WRITERS))})")
+    w(model, z)
+
+
 def build_h2o_mojo(model) -> bytes:
-    """MOJO zip bytes in the reference's layout (GBM, DRF, GLM)."""
+    """MOJO zip bytes in the reference's layout (GBM, DRF, GLM, K-Means,
+    Isolation Forest, Extended Isolation Forest, Deep Learning, Word2Vec,
+    Stacked Ensemble)."""
     z = _Zip()
-    if model.algo == "gbm":
-        _gbm(model, z)
-    elif model.algo == "drf":
-        _drf(model, z)
-    elif model.algo == "glm":
-        if getattr(model, "_hglm", None) is not None:
-            raise NotImplementedError("HGLM models have no MOJO (as in the reference)")
-        _glm(model, z)
-    else:
-        raise NotImplementedError(f"reference-layout MOJO export is implemented for gbm, drf and glm, not {model.algo}")
+    _write_algo(model, z)
     return z.close()

@@ -106,3 +106,93 @@ def test_h2o_mojo_files_layout(data, tmp_path):
     for key in ("algorithm = Gradient Boosting Machine", "n_trees = 3", "distribution = bernoulli",
                 "mojo_version = 1.40", "[columns]", "[domains]"):
         assert key in ini
+
+
+def test_kmeans_h2o_mojo_roundtrip(data, tmp_path):
+    from h2o3_amd.estimators import H2OKMeansEstimator
+    df, fr = data
+    km = H2OKMeansEstimator(k=4, seed=3, standardize=True)
+    km.train(x=["p", "r", "s", "cat"], training_frame=fr)
+    ours = km.predict(fr).as_data_frame()["predict"].values
+    m, theirs = _roundtrip(km, df, tmp_path)
+    assert m.algo == "kmeans" and not m.supervised
+    assert (theirs["predict"].values == ours).mean() > 0.998
+
+
+def test_isolationforest_h2o_mojo_roundtrip(data, tmp_path):
+    from h2o3_amd.estimators import H2OIsolationForestEstimator
+    df, fr = data
+    iso = H2OIsolationForestEstimator(ntrees=20, seed=4, sample_size=128)
+    iso.train(x=["p", "q", "r", "s"], training_frame=fr)
+    ours = iso.predict(fr).as_data_frame()
+    m, theirs = _roundtrip(iso, df, tmp_path)
+    np.testing.assert_allclose(theirs["mean_length"].values, ours["mean_length"].values, atol=1e-4)
+    # the reference stores the normalising min / max TOTAL path lengths as ints
+    rng_ = (iso._max_len - iso._min_len) * 20
+    np.testing.assert_allclose(theirs["predict"].values, ours["predict"].values, atol=1.0 / rng_ + 1e-6)
+
+
+def test_extended_isolationforest_h2o_mojo_roundtrip(data, tmp_path):
+    from h2o3_amd.estimators import H2OExtendedIsolationForestEstimator
+    df, fr = data
+    eif = H2OExtendedIsolationForestEstimator(ntrees=15, sample_size=64, extension_level=2, seed=5)
+    eif.train(x=["p", "r", "s"], training_frame=fr)
+    ours = eif.predict(fr).as_data_frame()
+    m, theirs = _roundtrip(eif, df, tmp_path)
+    np.testing.assert_allclose(theirs["mean_length"].values, ours["mean_length"].values, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(theirs["anomaly_score"].values, ours["anomaly_score"].values, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("y,act", [("yb", "Rectifier"), ("yr", "Tanh"), ("ym", "RectifierWithDropout"),
+                                   ("yb", "Maxout")])
+def test_deeplearning_h2o_mojo_roundtrip(data, y, act, tmp_path):
+    from h2o3_amd.estimators import H2ODeepLearningEstimator
+    df, fr = data
+    dl = H2ODeepLearningEstimator(hidden=[12, 7], epochs=3, seed=6, activation=act, reproducible=True)
+    dl.train(x=X, y=y, training_frame=fr)
+    ours = dl.predict(fr).as_data_frame()
+    m, theirs = _roundtrip(dl, df, tmp_path)
+    cols = [c for c in ours.columns if c != "predict"] or ["predict"]
+    np.testing.assert_allclose(theirs[cols].values.astype(float), ours[cols].values.astype(float), rtol=2e-4,
+                               atol=2e-4)
+
+
+def test_word2vec_h2o_mojo_roundtrip(tmp_path):
+    import h2o3_amd as h2o
+    from h2o3_amd.estimators import H2OWord2vecEstimator
+    from h2o3_amd.mojo import h2o_mojo
+    rng = np.random.RandomState(0)
+    vocab = [f"w{i}" for i in range(30)]
+    words = []
+    for _ in range(300):
+        words += list(rng.choice(vocab, 6)) + [None]
+    fr = h2o.H2OFrame(pd.DataFrame({"w": words}), column_types=["string"])
+    w2v = H2OWord2vecEstimator(vec_size=8, epochs=2, min_word_freq=1, seed=1)
+    w2v.train(training_frame=fr)
+    m = h2o_mojo.load(w2v.download_mojo(str(tmp_path), format="h2o"))
+    assert m.vec_size == 8 and len(m.embeddings) == len(w2v._vocab)
+    for i, w in enumerate(w2v._vocab[:10]):
+        np.testing.assert_allclose(m.transform(w), w2v._vecs[i].cpu().numpy(), rtol=1e-6)
+
+
+@pytest.mark.parametrize("y", ["yb", "yr", "ym"])
+def test_stackedensemble_h2o_mojo_roundtrip(data, y, tmp_path):
+    from h2o3_amd.estimators import (H2OGradientBoostingEstimator, H2OGeneralizedLinearEstimator,
+                                     H2ORandomForestEstimator, H2OStackedEnsembleEstimator)
+    df, fr = data
+    kw = dict(nfolds=3, keep_cross_validation_predictions=True, fold_assignment="Modulo", seed=1)
+    g = H2OGradientBoostingEstimator(ntrees=5, max_depth=3, **kw)
+    g.train(x=X, y=y, training_frame=fr)
+    d = H2ORandomForestEstimator(ntrees=4, max_depth=5, **kw)
+    d.train(x=X, y=y, training_frame=fr)
+    fam = {"yb": "binomial", "yr": "gaussian", "ym": "multinomial"}[y]
+    gl = H2OGeneralizedLinearEstimator(family=fam, **kw)
+    gl.train(x=["p", "r", "s", "cat"], y=y, training_frame=fr)
+    se = H2OStackedEnsembleEstimator(base_models=[g, d, gl])
+    se.train(x=X, y=y, training_frame=fr)
+    ours = se.predict(fr).as_data_frame()
+    m, theirs = _roundtrip(se, df, tmp_path)
+    assert m.algo == "stackedensemble" and len(m.base) == 3
+    cols = [c for c in ours.columns if c != "predict"] or ["predict"]
+    np.testing.assert_allclose(theirs[cols].values.astype(float), ours[cols].values.astype(float), rtol=1e-4,
+                               atol=1e-4)
