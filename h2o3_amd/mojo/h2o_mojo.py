@@ -47,7 +47,7 @@ _ALGO_BY_NAME = {
     "Extended Isolation Forest": "extendedisolationforest", "K-means": "kmeans", "Deep Learning": "deeplearning",
     "deep learning": "deeplearning", "Support Vector Machine (*Spark*)": "svm", "StackedEnsemble": "stackedensemble",
     "Stacked Ensemble": "stackedensemble", "k-LIME": "klime", "MOJO Pipeline": "pipeline",
-    "Principal Components Analysis": "pca", "Cox Proportional Hazards": "coxph", "RuleFit": "rulefit",
+    "Principal Components Analysis": "pca", "Principal Component Analysis": "pca", "Cox Proportional Hazards": "coxph", "RuleFit": "rulefit",
 }
 
 
@@ -484,6 +484,23 @@ class H2OMojoModel:
         self.vec_size = vec
         self.embeddings = {w: V[i] for i, w in enumerate(words)}
 
+    def _load_pca(self):
+        """PCAMojoReader: k components, categorical offsets, normSub / normMul
+        of the numerics, the eigenvectors as a BIG-endian double blob
+        (java.nio.ByteBuffer default order), [eigenvector_size][k]."""
+        self.pca_k = int(self.kv("k"))
+        self.pca_use_all = bool(self.kv("use_all_factor_levels", False))
+        self.pca_perm = list(self.kv("permutation", []))
+        self.pca_ncats = int(self.kv("ncats", 0))
+        self.pca_nnums = int(self.kv("nnums", 0))
+        self.pca_norm_sub = list(self.kv("normSub", [])) if self.pca_nnums else []
+        self.pca_norm_mul = list(self.kv("normMul", [])) if self.pca_nnums else []
+        self.pca_cat_offsets = list(self.kv("catOffsets", [0]))
+        size = int(self.kv("eigenvector_size"))
+        raw = self.be.read("eigenvectors_raw")
+        self.pca_evecs = np.frombuffer(raw, dtype=">f8", count=size * self.pca_k).astype(np.float64) \
+            .reshape(size, self.pca_k)
+
     def transform(self, word):
         """Word2Vec embedding of one word (None if out of vocabulary)."""
         v = self.embeddings.get(word)
@@ -731,6 +748,27 @@ class H2OMojoModel:
         self.last_distances = dist
         return np.argmin(dist, axis=1).reshape(-1, 1).astype(np.float64)
 
+    def _score_pca(self, X):
+        """PCAMojoModel.score0: categorical level rows of the eigenvectors
+        (missing / unseen levels skipped), numerics (x - sub) * mul."""
+        n = X.shape[0]
+        E = self.pca_evecs
+        offs = self.pca_cat_offsets
+        perm = self.pca_perm or list(range(self.pca_ncats + self.pca_nnums))
+        out = np.zeros((n, self.pca_k))
+        for j in range(self.pca_ncats):
+            v = X[:, perm[j]]
+            ok = ~np.isnan(v)
+            lvl = np.where(ok, v, 0).astype(np.int64) - (0 if self.pca_use_all else 1)
+            last = offs[j + 1] - offs[j] - 1
+            ok &= (lvl >= 0) & (lvl <= last)
+            out += np.where(ok[:, None], E[np.clip(offs[j] + lvl, 0, E.shape[0] - 1)], 0.0)
+        base = offs[self.pca_ncats]
+        for j in range(self.pca_nnums):
+            x = (X[:, perm[self.pca_ncats + j]] - self.pca_norm_sub[j]) * self.pca_norm_mul[j]
+            out += x[:, None] * E[base + j][None, :]
+        return out
+
     def _score_stackedensemble(self, X):
         n = X.shape[0]
         K = self.nclasses
@@ -933,6 +971,8 @@ class H2OMojoModel:
             return pd.DataFrame(preds, columns=cols)
         if self.algo == "extendedisolationforest":
             return pd.DataFrame(preds, columns=["anomaly_score", "mean_length"])
+        if self.algo == "pca":
+            return pd.DataFrame(preds, columns=[f"PC{i + 1}" for i in range(preds.shape[1])])
         if self.category == "AutoEncoder":
             return pd.DataFrame(preds, columns=[f"reconstr_{i}" for i in range(preds.shape[1])])
         if self.nclasses > 1 and preds.shape[1] > 1:

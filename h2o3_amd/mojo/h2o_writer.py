@@ -474,6 +474,44 @@ def _deeplearning(model, z):
         z.write(k, v)
 
 
+# ---------------------------------------------------------------------- PCA
+def _pca(model, z):
+    """PCAMojoReader layout: columns in DataInfo order (categoricals, then
+    numerics; identity permutation), normSub / normMul of the numerics and
+    the [P][k] eigenvectors as a big-endian double blob.  Our transform NONE
+    centres the data; that is expressible only without categoricals."""
+    di = model._dinfo
+    cats, nums = list(di.cat_cols), list(di.num_cols)
+    mean = model._mean.detach().cpu().numpy().astype(np.float64)[:di.P]
+    if cats and np.any(mean[:di.n_cat_expanded] != 0):
+        raise NotImplementedError("reference-layout PCA MOJOs cannot centre one-hot columns: "
+                                  "use transform='STANDARDIZE' (or another scaling) with categoricals")
+    base = di.n_cat_expanded
+    if di.standardize:
+        sub = [float(m) for m in di.means]
+        mul = [1.0 / float(s) for s in di.sigmas]
+    else:
+        sub = [float(mean[base + j]) for j in range(len(nums))]
+        mul = [1.0] * len(nums)
+    offs = [0]
+    for c in cats:
+        L = len(di.domains[c])
+        offs.append(offs[-1] + (L if di.use_all else L - 1))
+    E = model._evecs.detach().cpu().numpy().astype(np.float64)[:di.P]
+    extra = {"use_all_factor_levels": bool(di.use_all), "pca_methods": str(model._parms.get("pca_method", "GramSVD")),
+             "pca_impl": str(model._parms.get("pca_impl", "mtj_evd_symmmatrix")), "k": int(E.shape[1]),
+             "permutation": list(range(len(cats) + len(nums))), "ncats": len(cats), "nnums": len(nums),
+             "normSub": sub, "normMul": mul, "catOffsets": offs, "eigenvector_size": int(E.shape[0])}
+    columns = cats + nums
+    domains = [list(di.domains[c]) for c in cats] + [None] * len(nums)
+    ini, files = _header(model, "pca", "Principal Components Analysis", "DimReduction", columns, len(columns),
+                         int(E.shape[1]), domains, "1.00", extra, supervised=False)
+    z.write("model.ini", ini)
+    for k, v in files.items():
+        z.write(k, v)
+    z.write("eigenvectors_raw", E.astype(">f8").tobytes())
+
+
 # ----------------------------------------------------------------- Word2Vec
 def _word2vec(model, z):
     """Word2VecMojoModel: `vocabulary` (one word per line, newlines escaped)
@@ -522,7 +560,7 @@ def _stackedensemble(model, z):
 
 _WRITERS = {"gbm": _gbm, "drf": _drf, "glm": _glm, "kmeans": _kmeans, "isolationforest": _isofor,
             "extendedisolationforest": _eif, "deeplearning": _deeplearning, "word2vec": _word2vec,
-            "stackedensemble": _stackedensemble}
+            "stackedensemble": _stackedensemble, "pca": _pca}
 
 
 def _write_algo(model, z):
@@ -538,7 +576,7 @@ def _write_algo(model, z):
 def build_h2o_mojo(model) -> bytes:
     """MOJO zip bytes in the reference's layout (GBM, DRF, GLM, K-Means,
     Isolation Forest, Extended Isolation Forest, Deep Learning, Word2Vec,
-    Stacked Ensemble)."""
+    Stacked Ensemble, PCA)."""
     z = _Zip()
     _write_algo(model, z)
     return z.close()

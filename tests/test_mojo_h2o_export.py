@@ -196,3 +196,15 @@ def test_stackedensemble_h2o_mojo_roundtrip(data, y, tmp_path):
     cols = [c for c in ours.columns if c != "predict"] or ["predict"]
     np.testing.assert_allclose(theirs[cols].values.astype(float), ours[cols].values.astype(float), rtol=1e-4,
                                atol=1e-4)
+
+
+@pytest.mark.parametrize("transform,x", [("STANDARDIZE", ["p", "r", "s", "cat"]), ("NONE", ["p", "r", "s"]),
+                                         ("NORMALIZE", ["p", "r", "cat", "big"])])
+def test_pca_h2o_mojo_roundtrip(data, transform, x, tmp_path):
+    from h2o3_amd.estimators import H2OPrincipalComponentAnalysisEstimator
+    df, fr = data
+    pca = H2OPrincipalComponentAnalysisEstimator(k=3, transform=transform)
+    pca.train(x=x, training_frame=fr)
+    ours = pca.predict(fr).as_data_frame()
+    m, theirs = _roundtrip(pca, df, tmp_path)
+    np.testing.assert_allclose(theirs.values, ours.values[:, :3].astype(float), rtol=1e-4, atol=1e-4)
