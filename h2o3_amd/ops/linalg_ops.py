@@ -181,6 +181,25 @@ def weighted_gram(X: torch.Tensor, w: torch.Tensor | None = None, use_native=Non
     return _assemble(out.sum(0), pairs_t, T)
 
 
+# Row chunks per batched Gram GEMM: C_b = hi_b^T [hi_b | lo_b] for g chunks of
+# 512K rows in ONE strided-batched bf16 GEMM (f32 out, each chunk's f32
+# accumulation stays 512K rows long; chunks summed in f64).  One GEMM per
+# chunk has only 4 x 8 output tiles of 256 x 256 -- scripts/glm_wide_bmm_mb.py
+# at 12.5M x 1024: 66.7 ms per pass per chunk vs 45.9 ms batched by 4
+# (1142 TFLOP/s bf16).
+_WIDE_GROUP = int(os.environ.get("H2O3_WIDE_GROUP", 4))
+
+
+def _gram_group(H, st, Pa, G):
+    """G += sum over the row chunks of H [g*st, 2Pa] of hi'hi + hi'lo + lo'hi."""
+    g = H.shape[0] // st
+    H3 = H.view(g, st, 2 * Pa)
+    C = torch.bmm(H3[:, :, :Pa].transpose(1, 2), H3, out_dtype=torch.float32).to(torch.float64).sum(0)
+    G += C[:, :Pa]
+    cross = C[:, Pa:]
+    G += cross + cross.T
+
+
 def _wide_mode():
     return os.environ.get("H2O3_WIDE_GRAM", "bf3")
 
@@ -198,21 +217,24 @@ def gram_aug_bf3(X, W, z, P, step=1 << 19):
     Pa = -(-(P + 2) // 64) * 64
     W32, z32 = _f32(W), _f32(z)
     st = min(step, max(N, 1))
-    HL = torch.empty((st, 2 * Pa), dtype=torch.bfloat16, device=X.device)
+    nch = -(-N // st)
+    grp = min(nch, _WIDE_GROUP)
+    HL = torch.empty((grp * st, 2 * Pa), dtype=torch.bfloat16, device=X.device)
     G = torch.zeros((Pa, Pa), dtype=torch.float64, device=X.device)
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    for a in range(0, N, st):
+    for i, a in enumerate(range(0, N, st)):
         r = min(st, N - a)
+        j = i % grp
         rc = lib.h2o_gram_split(ctypes.c_void_p(X.data_ptr() + a * ldx * 4), ldx, P, Pa,
                                 ctypes.c_void_p(0 if W32 is None else W32.data_ptr() + a * 4),
-                                ctypes.c_void_p(0 if z32 is None else z32.data_ptr() + a * 4), r, _ptr(HL), stream)
+                                ctypes.c_void_p(0 if z32 is None else z32.data_ptr() + a * 4), r,
+                                ctypes.c_void_p(HL.data_ptr() + j * st * 2 * Pa * 2), stream)
         if rc != 0:
             raise RuntimeError(f"h2o_gram_split failed: {rc}")
-        H = HL[:r]
-        C = torch.mm(H[:, :Pa].T, H, out_dtype=torch.float32)
-        G += C[:, :Pa].to(torch.float64)
-        cross = C[:, Pa:].to(torch.float64)
-        G += cross + cross.T
+        if r < st:
+            HL[j * st + r:(j + 1) * st].zero_()
+        if j == grp - 1 or i == nch - 1:
+            _gram_group(HL[:(j + 1) * st], st, Pa, G)
     return G
 
 
@@ -232,9 +254,11 @@ def glm_wide_irls(X, P, beta, b0, y, wprior=None, offset=None, codes=(1, 1), tvp
     bt = _f32(beta)
     keep = [_f32(y), _f32(wprior), _f32(offset)]
     st = min(step, max(N, 1))
-    HL = torch.empty((st, 2 * Pa), dtype=torch.bfloat16, device=X.device)
+    nch = -(-N // st)
+    grp = min(nch, _WIDE_GROUP)
+    HL = torch.empty((grp * st, 2 * Pa), dtype=torch.bfloat16, device=X.device)
     blocks = 2048
-    dev = torch.zeros((-(-N // st), blocks), dtype=torch.float64, device=X.device)
+    dev = torch.zeros((nch, blocks), dtype=torch.float64, device=X.device)
     G = torch.zeros((Pa, Pa), dtype=torch.float64, device=X.device)
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
@@ -243,16 +267,18 @@ def glm_wide_irls(X, P, beta, b0, y, wprior=None, offset=None, codes=(1, 1), tvp
 
     for i, a in enumerate(range(0, N, st)):
         r = min(st, N - a)
+        j = i % grp
         rc = lib.h2o_glm_wide_split(ctypes.c_void_p(X.data_ptr() + a * ldx * 4), ldx, P, Pa, r, _ptr(bt),
                                     float(b0), off(keep[0], a), off(keep[1], a), off(keep[2], a), int(codes[0]),
-                                    int(codes[1]), float(tvp), float(theta), _ptr(HL), _ptr(dev[i]), blocks, stream)
+                                    int(codes[1]), float(tvp), float(theta),
+                                    ctypes.c_void_p(HL.data_ptr() + j * st * 2 * Pa * 2), _ptr(dev[i]), blocks,
+                                    stream)
         if rc != 0:
             raise RuntimeError(f"h2o_glm_wide_split failed: {rc}")
-        H = HL[:r]
-        C = torch.mm(H[:, :Pa].T, H, out_dtype=torch.float32)
-        G += C[:, :Pa].to(torch.float64)
-        cross = C[:, Pa:].to(torch.float64)
-        G += cross + cross.T
+        if r < st:
+            HL[j * st + r:(j + 1) * st].zero_()
+        if j == grp - 1 or i == nch - 1:
+            _gram_group(HL[:(j + 1) * st], st, Pa, G)
     return G, dev.sum()
 
 
