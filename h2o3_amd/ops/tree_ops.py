@@ -578,7 +578,17 @@ def partition(bd, ridx, ridx_out, feats, masks, starts, counts, use_native=None,
     return out
 
 
-def partition_async(bd, ridx, ridx_out, feat_d, masks, starts, counts, chunk=16384, payload=None, pk=None,
+def _part_chunk(total):
+    """Rows per partition work item: 16K at 100M rows (6K+ workgroups); at
+    smaller row counts down to 4K so the flag / compaction passes still see
+    ~2K workgroups (12.5M rows: 763 -> 2035)."""
+    env = os.environ.get("H2O3_PART_CHUNK")
+    if env:
+        return int(env)
+    return int(max(4096, min(16384, -(-int(total) // 2048 // 64) * 64)))
+
+
+def partition_async(bd, ridx, ridx_out, feat_d, masks, starts, counts, chunk=None, payload=None, pk=None,
                     pk_col=0):
     """Sync-free ballot partition of EVERY segment i by masks[i][code(row,
     feat_d[i])] (feat_d, masks on device; a segment whose mask is all ones stays
@@ -595,6 +605,8 @@ def partition_async(bd, ridx, ridx_out, feat_d, masks, starts, counts, chunk=163
         lib.h2o_part_offsets.argtypes = [_c_void, _c_void, _c_int, _c_int, _c_void, _c_void, _c_void, _c_void,
                                          _c_int, _c_int, _c_void]
         lib._typed_async = True
+    if chunk is None:
+        chunk = _part_chunk(sum(counts))
     items = make_work(starts, counts, range(n), chunk)
     nleft = torch.empty(n, dtype=torch.int64, device=dev)   # zeroed by the offsets kernel
     if len(items) == 0:
