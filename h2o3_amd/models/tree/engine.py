@@ -971,7 +971,14 @@ class TreeGrower:
         return out
 
     # ------------------------------------------------------------------ grow
-    def grow(self, va, vb, mode, tree_node_hook=None, want_nid=True, vmax=None, unit_w=None):
+    def pos_payload_ok(self):
+        """True when grow() keeps the 0/1-weighted mode-0 response as a
+        position-ordered NaN-masked payload (quad histogram kernels)."""
+        return self.dev.type == "cuda" and not self.use_payload and self.bd.code_bytes == 1 and \
+            self.bd.Bs <= 256 and self.bd.Fp % 16 == 0 and os.environ.get("H2O3_HIST_KERNEL", "quad") == "quad" \
+            and os.environ.get("H2O3_POSV", "1") == "1" and os.environ.get("H2O3_PART", "ballot") == "ballot"
+
+    def grow(self, va, vb, mode, tree_node_hook=None, want_nid=True, vmax=None, unit_w=None, va_scratch=False):
         """Grow one tree.  Returns (Tree, nid[N] leaf index per local row,
         leaf_nodes list (tree node ids, indexed by nid), leaf_tot [n_leaves, C]).
         vmax / unit_w: caller-known bounds (max |channel| for the fixed-point
@@ -996,7 +1003,9 @@ class TreeGrower:
         self._pos1 = None
         if self._va_eff is not None and os.environ.get("H2O3_POSV", "1") == "1" and \
                 os.environ.get("H2O3_PART", "ballot") == "ballot":
-            p0 = self._va_eff.clone() if self._va_eff is va else self._va_eff
+            # va_scratch: the caller hands over va (a NaN-masked residual it
+            # will not read again) as the root payload -- no copy
+            p0 = self._va_eff.clone() if (self._va_eff is va and not va_scratch) else self._va_eff
             self._pos1 = [p0, torch.empty_like(p0)]   # root: position order == row order
         ridx, ridx2 = self.ridx, self.ridx2
         self._la = None

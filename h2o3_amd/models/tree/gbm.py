@@ -221,11 +221,6 @@ class GBMDriver:
         if self.K == 1:
             f = self.f[:, 0]
             y = self.yb if self.spec.nclasses == 2 else torch.nan_to_num(self.yf)
-            with phase("gbm.grad"):
-                z = self.dist.neg_half_gradient(y, f).to(torch.float32)
-            if self.dist.family == "huber":
-                self._update_huber_delta(y, f, w)
-                z = self.dist.neg_half_gradient(y, f).to(torch.float32)
             simple = self.dev.type == "cuda" and self.dist.family in ("gaussian", "bernoulli") and \
                 self.dist.link in ("identity", "logit")
             fused = simple and os.environ.get("H2O3_FUSED_LEAF", "0") == "1"
@@ -235,13 +230,29 @@ class GBMDriver:
             if getattr(self, "_base_unit", None) is None:
                 bw = self.base_w
                 self._base_unit = bool(((bw == 0) | (bw == 1)).all())
+            # one-pass residual straight into the grower's root payload (NaN =
+            # weight 0): the 0/1-weight position-ordered path of grow()
+            onepass = posleaf and self._base_unit and self.grower.pos_payload_ok() and \
+                os.environ.get("H2O3_GBM_GRAD", "1") == "1"
+            with phase("gbm.grad"):
+                if onepass:
+                    z = tree_ops.gbm_grad(y, f, None if self._unit_weights else w, self.dist.family)
+                else:
+                    z = self.dist.neg_half_gradient(y, f).to(torch.float32)
+            if self.dist.family == "huber":
+                self._update_huber_delta(y, f, w)
+                z = self.dist.neg_half_gradient(y, f).to(torch.float32)
             # bernoulli residuals y - p lie in (-1, 1): with 0/1 weights both
             # histogram channels are bounded by 1 (no per-tree max reduction)
             vmax_h = [1.0, 1.0] if (self.dist.family == "bernoulli" and self._base_unit) else None
             with phase("gbm.grow"):
-                tree, nid, leaves, tot = self.grower.grow(z.contiguous(), w.contiguous(), 0,
-                                                          want_nid=not (fused or posleaf), vmax=vmax_h,
-                                                          unit_w=self._base_unit)
+                if onepass:
+                    tree, nid, leaves, tot = self.grower.grow(z, None, 0, want_nid=False, vmax=vmax_h,
+                                                              unit_w=True, va_scratch=True)
+                else:
+                    tree, nid, leaves, tot = self.grower.grow(z.contiguous(), w.contiguous(), 0,
+                                                              want_nid=not (fused or posleaf), vmax=vmax_h,
+                                                              unit_w=self._base_unit)
             zpos = self.grower._pos1[0] if (posleaf and getattr(self.grower, "_pos1", None) is not None) else None
             if posleaf and zpos is None:
                 posleaf = False

@@ -28,6 +28,7 @@
 // multi-GPU reduce-scatter can shard by feature).
 #include "common.h"
 #include <stdlib.h>
+#include <algorithm>
 
 template <int MODE> struct Chan { static constexpr int C = MODE == 2 ? 1 : 2; };
 
@@ -1239,5 +1240,34 @@ extern "C" int h2o_pair_hist(const void* codes_col, int code_bytes, long long nc
     if (mode == 0) pair_hist_launch<uint16_t, 0>(hv, posv, n_work, lds, s, codes_col, ncol, ridx, va, vb, w, pfeat, Bs, s0, s1, Hp, pwyy);
     else pair_hist_launch<uint16_t, 1>(hv, posv, n_work, lds, s, codes_col, ncol, ridx, va, vb, w, pfeat, Bs, s0, s1, Hp, pwyy);
   }
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// GBM residual for the position-ordered payload in ONE pass (the torch chain
+// sigmoid / sub / where / clone read and wrote the 100M-row vectors five
+// times): z = y - f (mode 0, gaussian) or y - 1 / (1 + exp(-f)) (mode 1,
+// bernoulli), NaN where the row weight is 0 (out-of-sample rows; the
+// histogram and leaf kernels treat NaN as weight 0).  Reference:
+// hex/tree/gbm/GBM.java ComputePredAndRes / Distribution.negHalfGradient.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void gbm_grad_kernel(const float* __restrict__ y, const float* __restrict__ f,
+                                                       const float* __restrict__ w, int mode, long long n,
+                                                       float* __restrict__ z) {
+  const long long stride = (long long)gridDim.x * 256;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    const float fi = f[i];
+    const float p = mode == 1 ? 1.f / (1.f + expf(-fi)) : fi;
+    float v = y[i] - p;
+    if (w != nullptr && !(w[i] > 0.f)) v = __builtin_nanf("");
+    z[i] = v;
+  }
+}
+
+extern "C" int h2o_gbm_grad(const float* y, const float* f, const float* w, int mode, long long n, float* z,
+                            hipStream_t s) {
+  if (n <= 0) return 0;
+  const long long blocks = std::min<long long>((n + 255) / 256, 8192);
+  hipLaunchKernelGGL(gbm_grad_kernel, dim3((unsigned)blocks), dim3(256), 0, s, y, f, w, mode, n, z);
   return (int)hipGetLastError();
 }

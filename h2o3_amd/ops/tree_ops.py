@@ -490,6 +490,31 @@ def pair_hist_dev(bd, ridx, va, vb, mode, node_st, node_ct, sel, vmax, posv=Fals
     return Hp, (pwyy.view(n, k)[:, 0].contiguous() if want_wyy else None), pfeat
 
 
+def gbm_grad(y, f, w, family, out=None):
+    """GBM residual in one HIP pass (gbm_grad_kernel): y - f (gaussian) or
+    y - sigmoid(f) (bernoulli), NaN where w == 0 (w may be None).  f32."""
+    mode = {"gaussian": 0, "bernoulli": 1}[family]
+    n = y.numel()
+    z = out if out is not None else torch.empty(n, dtype=torch.float32, device=y.device)
+    if y.device.type != "cuda":
+        p = f if mode == 0 else torch.sigmoid(f)
+        v = (y - p).to(torch.float32)
+        if w is not None:
+            v = torch.where(w > 0, v, torch.full_like(v, float("nan")))
+        z.copy_(v)
+        return z
+    lib = _lib()
+    if not getattr(lib, "_typed_grad", False):
+        lib.h2o_gbm_grad.argtypes = [_c_void, _c_void, _c_void, _c_int, _c_ll, _c_void, _c_void]
+        lib._typed_grad = True
+    yc, fc = y.contiguous().to(torch.float32), f.contiguous().to(torch.float32)
+    wc = w.contiguous().to(torch.float32) if w is not None else None
+    rc = lib.h2o_gbm_grad(_ptr(yc), _ptr(fc), _ptr(wc), mode, n, _ptr(z), _stream())
+    if rc != 0:
+        raise RuntimeError(f"h2o_gbm_grad failed: {rc}")
+    return z
+
+
 def partition(bd, ridx, ridx_out, feats, masks, starts, counts, use_native=None, chunk=16384, payload=None):
     """Stable-partition each segment i by masks[i][code(row, feats[i])] (1 =
     left).  Writes ridx_out and returns per-segment left counts (host list).
