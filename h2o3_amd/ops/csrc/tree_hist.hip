@@ -1271,3 +1271,48 @@ extern "C" int h2o_gbm_grad(const float* y, const float* f, const float* w, int 
   hipLaunchKernelGGL(gbm_grad_kernel, dim3((unsigned)blocks), dim3(256), 0, s, y, f, w, mode, n, z);
   return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------
+// Partition work items built on the device: the host uploads only the
+// per-segment (start, count, first-chunk index, first-flag-word index) table
+// (O(frontier) numbers) and every chunk's record -- work int4 (segment,
+// start, count, k), the offsets kernel's meta (segment, first chunk of the
+// segment, segment start, position in segment) and the flag-word base -- is
+// written here (the host numpy version cost ~0.2 ms per level at 2K chunks).
+// seg: [4][n] int64.  chunk % 64 == 0.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void part_items_kernel(const long long* __restrict__ seg, int n, int chunk, int nw,
+                                                         int4* __restrict__ work, long long* __restrict__ meta,
+                                                         int* __restrict__ fbase) {
+  const long long* st = seg;
+  const long long* ct = seg + n;
+  const long long* cb = seg + 2 * (long long)n;
+  const long long* wb = seg + 3 * (long long)n;
+  for (int c = blockIdx.x * 256 + threadIdx.x; c < nw; c += gridDim.x * 256) {
+    int lo = 0, hi = n - 1;   // last segment whose first chunk index is <= c
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (cb[mid] <= c) lo = mid;
+      else hi = mid - 1;
+    }
+    const int s = lo;
+    const long long k = c - cb[s];
+    const long long start = st[s] + k * chunk;
+    const long long cnt = min((long long)chunk, ct[s] - k * chunk);
+    work[c] = make_int4(s, (int)start, (int)cnt, (int)k);
+    meta[c] = s;
+    meta[(long long)nw + c] = cb[s];
+    meta[2 * (long long)nw + c] = st[s];
+    meta[3 * (long long)nw + c] = k * chunk;
+    fbase[c] = (int)(wb[s] + k * (chunk / 64));
+  }
+}
+
+extern "C" int h2o_part_items(const long long* seg, int n, int chunk, int nw, int* work, long long* meta,
+                              int* fbase, hipStream_t s) {
+  if (nw <= 0) return 0;
+  if (chunk % 64 != 0 || n <= 0) return -1;
+  const int blocks = std::min((nw + 255) / 256, 1024);
+  hipLaunchKernelGGL(part_items_kernel, dim3(blocks), dim3(256), 0, s, seg, n, chunk, nw, (int4*)work, meta, fbase);
+  return (int)hipGetLastError();
+}

@@ -632,30 +632,45 @@ def partition_async(bd, ridx, ridx_out, feat_d, masks, starts, counts, chunk=Non
         lib._typed_async = True
     if chunk is None:
         chunk = _part_chunk(sum(counts))
-    items = make_work(starts, counts, range(n), chunk)
     nleft = torch.empty(n, dtype=torch.int64, device=dev)   # zeroed by the offsets kernel
-    if len(items) == 0:
+    st = np.asarray(starts, dtype=np.int64).reshape(-1)
+    ct = np.asarray(counts, dtype=np.int64).reshape(-1)
+    nch = (ct + chunk - 1) // chunk
+    nw = int(nch.sum())
+    if nw == 0:
         nleft.zero_()
         if pk is not None:
             pk[:, pk_col] = 0.0
         return nleft
-    nw = len(items)
-    words = (items[:, 2].astype(np.int64) + 63) // 64
-    fb_h = (np.cumsum(words) - words).astype(np.int64)
-    slot = items[:, 0].astype(np.int64)
-    first = np.ones(nw, dtype=bool)
-    first[1:] = slot[1:] != slot[:-1]
-    first_idx = np.maximum.accumulate(np.where(first, np.arange(nw), 0))
-    st_arr = np.asarray(starts, dtype=np.int64)[slot]
-    pos = items[:, 1].astype(np.int64) - st_arr
-    # ONE host->device upload: per-chunk meta (int64 x4), the work items and the
-    # flag-word bases (int32 views of the same buffer)
-    meta_h = np.concatenate([np.stack([slot, first_idx, st_arr, pos], 0).reshape(-1).view(np.int32),
-                             items.reshape(-1), fb_h.astype(np.int32)])
-    buf = _h2d(meta_h, dev)
+    wd = (ct + 63) // 64
+    total_words = int(wd.sum())
+    buf = torch.empty(13 * nw, dtype=torch.int32, device=dev)
     meta = buf[: 8 * nw].view(torch.int64)
     work = buf[8 * nw: 12 * nw]
     fbase = buf[12 * nw:]
+    if chunk % 64 == 0 and os.environ.get("H2O3_PART_ITEMS", "dev") == "dev":
+        # per-chunk records written on the device from the O(frontier) segment table
+        if not getattr(lib, "_typed_items", False):
+            lib.h2o_part_items.argtypes = [_c_void, _c_int, _c_int, _c_int, _c_void, _c_void, _c_void, _c_void]
+            lib._typed_items = True
+        seg = _h2d(np.concatenate([st, ct, np.cumsum(nch) - nch, np.cumsum(wd) - wd]), dev)
+        rc = lib.h2o_part_items(_ptr(seg), n, chunk, nw, _ptr(work), _ptr(meta), _ptr(fbase), _stream())
+        if rc != 0:
+            raise RuntimeError(f"h2o_part_items failed: {rc}")
+    else:
+        items = make_work(starts, counts, range(n), chunk)
+        words = (items[:, 2].astype(np.int64) + 63) // 64
+        fb_h = (np.cumsum(words) - words).astype(np.int64)
+        slot = items[:, 0].astype(np.int64)
+        first = np.ones(nw, dtype=bool)
+        first[1:] = slot[1:] != slot[:-1]
+        first_idx = np.maximum.accumulate(np.where(first, np.arange(nw), 0))
+        st_arr = st[slot]
+        pos = items[:, 1].astype(np.int64) - st_arr
+        # ONE host->device upload: per-chunk meta (int64 x4), the work items and the
+        # flag-word bases (int32 views of the same buffer)
+        buf.copy_(_h2d(np.concatenate([np.stack([slot, first_idx, st_arr, pos], 0).reshape(-1).view(np.int32),
+                                       items.reshape(-1), fb_h.astype(np.int32)]), dev))
     feat_t = feat_d if feat_d.dtype == torch.int32 else feat_d.to(torch.int32)
     masks = masks if masks.dtype == torch.uint8 else masks.to(torch.uint8)
     cnt = torch.empty(nw, dtype=torch.int32, device=dev)
@@ -663,7 +678,7 @@ def partition_async(bd, ridx, ridx_out, feat_d, masks, starts, counts, chunk=Non
         codes, rs, fs = bd.codes_col, 1, bd.nrows_local
     else:
         codes, rs, fs = bd.codes, bd.Fp, 1
-    flags = torch.empty(int(words.sum()) + 1, dtype=torch.int64, device=dev)
+    flags = torch.empty(total_words + 1, dtype=torch.int64, device=dev)
     rc = lib.h2o_part_flags(_ptr(codes), bd.code_bytes, rs, fs, _ptr(ridx), _ptr(work), _ptr(fbase), nw,
                             _ptr(feat_t), _ptr(masks), bd.Bs, _ptr(flags), _ptr(cnt), _stream())
     if rc != 0:

@@ -68,18 +68,21 @@ def test_partition_matches_reference(impl, monkeypatch):
     assert torch.equal(out_g, out_r)
 
 
-def test_partition_async_matches_reference():
+@pytest.mark.parametrize("items", ["dev", "host"])
+def test_partition_async_matches_reference(items, monkeypatch):
     """Sync-free partition (device-side offset scan, all-ones mask = node kept
-    in place) against the torch reference, with a position-ordered payload."""
+    in place, work items built on the device or the host, an empty segment)
+    against the torch reference, with a position-ordered payload."""
     _need_gpu()
+    monkeypatch.setenv("H2O3_PART_ITEMS", items)
     from h2o3_amd.ops import tree_ops
     bd, _ = _binned(n=50000)
     n = bd.nrows_local
     ridx = torch.randperm(n, device="cuda").to(torch.int32)
-    starts, counts = [0, 20003, 30000, 45001], [19999, 9997, 15001, 4999]
-    feats = [0, 4, 2, 7]
-    masks = (torch.rand((4, bd.Bs), device="cuda") < 0.5).to(torch.uint8)
-    masks[2] = 1   # a node that does not split: rows stay where they are
+    starts, counts = [0, 20003, 30000, 30000, 45001], [19999, 9997, 0, 15001, 4999]
+    feats = [0, 4, 1, 2, 7]
+    masks = (torch.rand((5, bd.Bs), device="cuda") < 0.5).to(torch.uint8)
+    masks[3] = 1   # a node that does not split: rows stay where they are
     pay = torch.randn(n, device="cuda")
     out_g, pay_g = ridx.clone(), pay.clone()
     out_r = ridx.clone()
