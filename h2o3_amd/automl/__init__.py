@@ -186,9 +186,15 @@ class H2OAutoML:
         self._t0 = time.time()
 
     # ------------------------------------------------------------------ helpers
+    _VERB = {"debug": 0, "info": 1, "warn": 2, "warning": 2, "error": 3}
+
     def _log(self, stage, msg, level="Info"):
         self.event_log_rows.append({"timestamp": time.strftime("%H:%M:%S"), "level": level, "stage": stage,
                                     "message": msg})
+        # the reference client prints the event log at or above `verbosity`
+        v = self._VERB.get(str(self.verbosity or "warn").lower(), 2)
+        if self.verbosity is not None and self._VERB.get(str(level).lower(), 1) >= v:
+            print(f"{time.strftime('%H:%M:%S')}: {msg}", flush=True)
 
     def _allowed(self, algo):
         a = algo.lower()
