@@ -553,26 +553,61 @@ class TreeGrower:
             with phase("tree.hist"), phase("tree.hist.pairs"):
                 Hp, wyy_n, pfeat = tree_ops.pair_hist_dev(bd, ridx, va, vb, mode, st[a:b], ct[a:b], sl, self._vmax,
                                                           posv=posv)
+            nb = b - a
             if self.W > 1:
-                coll.allreduce_(Hp)
-                if wyy_n is not None:
-                    coll.allreduce_(wyy_n)
-            P = (b - a) * k
-            fl = pfeat.long()
-            best_k = self._pairs_native(Hp.view(1, P, Bs, 2), torch.zeros(P, dtype=torch.long, device=dev),
-                                        torch.arange(P, device=dev), self.is_cat_t[fl], self.mono_t[fl],
-                                        wyy_n.repeat_interleave(k) if wyy_n is not None else None, raw=True)
-            rc = lib.h2o_pair_select(ctypes.c_void_p(Hp.data_ptr()), b - a, Bs, k, ctypes.c_void_p(best_k.data_ptr()),
-                                     ctypes.c_void_p(pfeat.data_ptr()), ctypes.c_void_p(self._fcat_u8.data_ptr()),
-                                     1 if p.criterion == "xgb" else 0, min_w2, 12,
-                                     ctypes.c_void_p(pk[a:b].data_ptr()), ctypes.c_void_p(mask[a:b].data_ptr()),
-                                     ctypes.c_void_p(feat_i[a:b].data_ptr()),
-                                     ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
-            if rc != 0:
-                raise RuntimeError(f"h2o_pair_select failed: {rc}")
+                # node-sharded reduction: every rank receives the summed pair
+                # histograms of 1/W of the nodes (reduce_scatter moves half the
+                # bytes of an all-reduce), scores and selects those nodes, and
+                # only the small per-node records are all-gathered
+                W = self.W
+                npad = -(-nb // W) * W
+                Hv = Hp.view(nb, -1)
+                wv = wyy_n if wyy_n is not None else torch.zeros(nb, dtype=torch.float64, device=dev)
+                if npad > nb:
+                    Hv = torch.cat([Hv, torch.zeros((npad - nb, Hv.shape[1]), dtype=Hv.dtype, device=dev)], 0)
+                    wv = torch.cat([wv, torch.zeros(npad - nb, dtype=wv.dtype, device=dev)], 0)
+                    pfeat = torch.cat([pfeat, torch.zeros((npad - nb) * k, dtype=pfeat.dtype, device=dev)], 0)
+                nl = npad // W
+                lo = self.rank * nl
+                Hl = coll.reduce_scatter_dim0(Hv.contiguous())
+                wl = coll.reduce_scatter_dim0(wv.contiguous()) if wyy_n is not None else None
+                del Hp, Hv
+                pk_l = torch.empty((nl, 12), dtype=torch.float64, device=dev)
+                mask_l = torch.empty((nl, Bs), dtype=torch.uint8, device=dev)
+                feat_l = torch.empty(nl, dtype=torch.int32, device=dev)
+                self._pair_score_select(lib, Hl, nl, k, pfeat[lo * k:(lo + nl) * k].contiguous(), wl, min_w2,
+                                        pk_l, mask_l, feat_l)
+                pk[a:b] = coll.all_gather_dim0(pk_l)[:nb]
+                mask[a:b] = coll.all_gather_dim0(mask_l)[:nb]
+                feat_i[a:b] = coll.all_gather_dim0(feat_l)[:nb]
+                continue
+            self._pair_score_select(lib, Hp, nb, k, pfeat, wyy_n, min_w2, pk[a:b], mask[a:b], feat_i[a:b])
             del Hp
         return {"pk": pk, "feat_i32": feat_i, "mask": mask, "gain": pk[:, 0], "feat": pk[:, 1].long(),
                 "t": pk[:, 2].long(), "opt": pk[:, 3].long(), "L": pk[:, 4:6], "R": pk[:, 6:8], "tot": pk[:, 8:10]}
+
+    def _pair_score_select(self, lib, Hp, n, k, pfeat, wyy_n, min_w2, pk, mask, feat_i):
+        """Score the n*k pairs of Hp (cat_pair_kernel) and write the n nodes'
+        records / masks / features (pair_select_kernel) into the given
+        contiguous output views."""
+        import ctypes
+        p = self.p
+        dev = self.dev
+        Bs = self.bd.Bs
+        P = n * k
+        if n <= 0:
+            return
+        fl = pfeat.long()
+        best_k = self._pairs_native(Hp.view(1, P, Bs, 2), torch.zeros(P, dtype=torch.long, device=dev),
+                                    torch.arange(P, device=dev), self.is_cat_t[fl], self.mono_t[fl],
+                                    wyy_n.repeat_interleave(k) if wyy_n is not None else None, raw=True)
+        rc = lib.h2o_pair_select(ctypes.c_void_p(Hp.data_ptr()), n, Bs, k, ctypes.c_void_p(best_k.data_ptr()),
+                                 ctypes.c_void_p(pfeat.data_ptr()), ctypes.c_void_p(self._fcat_u8.data_ptr()),
+                                 1 if p.criterion == "xgb" else 0, min_w2, 12, ctypes.c_void_p(pk.data_ptr()),
+                                 ctypes.c_void_p(mask.data_ptr()), ctypes.c_void_p(feat_i.data_ptr()),
+                                 ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+        if rc != 0:
+            raise RuntimeError(f"h2o_pair_select failed: {rc}")
 
     def _pair_direct_part(self, ridx, va, vb, mode, posv, st, ct, pn, pf):
         p = self.p
