@@ -244,10 +244,20 @@ class H2OEstimator:
                          p.get("fold_column"), validation_frame)
         self._spec = spec
         nfolds = int(p.get("nfolds") or 0)
+        # max_runtime_secs bounds the WHOLE build, cross-validation included
+        # (reference ModelBuilder: the CV models share the budget)
+        max_rt = float(p.get("max_runtime_secs") or 0)
+        self._deadline = t0 + max_rt if max_rt > 0 else None
         try:
             if self.supervised_learning and (nfolds > 1 or p.get("fold_column")):
                 self._cross_validate(spec)
-            self._fit(spec)
+            if self._deadline is not None:
+                p["max_runtime_secs"] = max(1e-3, self._deadline - time.time())
+            try:
+                self._fit(spec)
+            finally:
+                if self._deadline is not None:
+                    p["max_runtime_secs"] = max_rt
             self._score_all(spec)
         except Exception as e:
             self._job.fail(e)
@@ -329,6 +339,10 @@ class H2OEstimator:
             sub._parms = dict(self._parms)
             sub._parms["nfolds"] = 0
             sub._parms["fold_column"] = None
+            dl = getattr(self, "_deadline", None)
+            if dl is not None:
+                # fold i gets an equal share of what is left for the k - i folds and the main model
+                sub._parms["max_runtime_secs"] = max(1e-3, (dl - time.time()) / (k - i + 1))
             sub._id = f"{self._id}_cv_{i + 1}"
             sub._cv_models = []
             sub._scoring_history = []

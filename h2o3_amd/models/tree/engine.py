@@ -131,6 +131,59 @@ class Tree:
         return out
 
 
+class _TreeBuf:
+    """Growable per-node numpy arrays for one tree under construction: the
+    level loop records the splits of a whole level with vectorized
+    assignments (the per-node Python bookkeeping cost seconds per tree at
+    depth 20 / 10^5 nodes); to_tree() hands back the list-based Tree."""
+
+    _FIELDS = (("feat", np.int64, -1), ("left", np.int64, -1), ("right", np.int64, -1), ("thr", np.float64, 0.0),
+               ("na_left", bool, False), ("is_cat", bool, False), ("value", np.float64, 0.0),
+               ("weight", np.float64, 0.0), ("gain", np.float64, 0.0), ("depth", np.int64, 0),
+               ("split_code", np.int64, -1))
+
+    def __init__(self, cap=256):
+        self.n = 1                       # the root
+        self.cap = cap
+        for name, dt, fill in self._FIELDS:
+            setattr(self, name, np.full(cap, fill, dtype=dt))
+        self.cat_left = {}
+
+    def _grow(self, need):
+        cap = self.cap
+        while cap < need:
+            cap *= 2
+        if cap == self.cap:
+            return
+        for name, dt, fill in self._FIELDS:
+            a = np.full(cap, fill, dtype=dt)
+            a[:self.n] = getattr(self, name)[:self.n]
+            setattr(self, name, a)
+        self.cap = cap
+
+    def add_children(self, depth, wl, wr):
+        """(left, right) node pairs for every entry of wl / wr; returns the
+        first new id (pairs are consecutive)."""
+        k = 2 * len(wl)
+        base = self.n
+        self._grow(base + k)
+        self.weight[base:base + k:2] = wl
+        self.weight[base + 1:base + k:2] = wr
+        self.depth[base:base + k] = depth
+        self.n = base + k
+        return base
+
+    def to_tree(self):
+        n = self.n
+        t = Tree()
+        for name, _, _ in self._FIELDS:
+            setattr(t, name, getattr(self, name)[:n].tolist())
+        t.cat_left = [None] * n
+        for i, m in self.cat_left.items():
+            t.cat_left[i] = m
+        return t
+
+
 class TreeGrower:
     """Grows one tree over a BinnedData with a given channel mode."""
 
@@ -474,7 +527,7 @@ class TreeGrower:
         k, _ = self._sample_k(depth)
         return env == "1" or chunked or 4 * k <= self.bd.F
 
-    def _pair_direct_splits(self, ridx, va, vb, mode, frontier, cm):
+    def _pair_direct_splits(self, ridx, va, vb, mode, f_st, f_ct, cm):
         """Best split of every frontier node from row-direct histograms of its
         sampled (node, feature) pairs only: pair histograms built from the rows
         (HIP `pair_hist_kernel`), scored per pair (`cat_pair_kernel`: numeric
@@ -485,14 +538,14 @@ class TreeGrower:
         p = self.p
         bd, dev = self.bd, self.dev
         F, Bs, C = bd.F, bd.Bs, 2
-        n = len(frontier)
+        n = len(f_st)
         posv = False
         if mode == 0 and getattr(self, "_pos1", None) is not None:
             va, vb, posv = self._pos1[0], None, True
         elif mode == 0 and getattr(self, "_va_eff", None) is not None:
             va, vb = self._va_eff, None
-        st = np.asarray([f[1] for f in frontier], dtype=np.int64)
-        ct = np.asarray([f[2] for f in frontier], dtype=np.int64)
+        st = np.asarray(f_st, dtype=np.int64)
+        ct = np.asarray(f_ct, dtype=np.int64)
         nz = torch.nonzero(cm[:, :F]).cpu().numpy()           # node-major pairs
         pn_all, pf_all = nz[:, 0].astype(np.int64), nz[:, 1].astype(np.int64)
         per_pairs = max(1, int(p.hist_mem_budget // (Bs * C * 8)))
@@ -510,7 +563,7 @@ class TreeGrower:
             return parts[0]
         return {k: torch.cat([q[k] for q in parts], 0) for k in parts[0]}
 
-    def _pair_direct_dev(self, ridx, va, vb, mode, frontier, sel):
+    def _pair_direct_dev(self, ridx, va, vb, mode, f_st, f_ct, sel):
         """Device-resident version of _pair_direct_splits: pairs from the
         [n, k] column sample on the device, pair histograms
         (pair_hist_kernel), per-pair scoring (cat_pair_kernel) and the
@@ -526,7 +579,7 @@ class TreeGrower:
             # no per-node sampling (only the per-tree column mask): every eligible feature
             base = np.ones(bd.F, dtype=bool) if p.tree_col_mask is None else p.tree_col_mask.astype(bool)
             elig = torch.as_tensor(np.nonzero(base)[0], device=dev)
-            sel = elig.view(1, -1).expand(len(frontier), -1)
+            sel = elig.view(1, -1).expand(len(f_st), -1)
         n, k = sel.shape
         posv = False
         if mode == 0 and getattr(self, "_pos1", None) is not None:
@@ -540,8 +593,8 @@ class TreeGrower:
             lib._typed_psel = True
         if getattr(self, "_fcat_u8", None) is None:
             self._fcat_u8 = self.is_cat_t[:bd.F].to(torch.uint8).contiguous()
-        st = np.asarray([f[1] for f in frontier], dtype=np.int64)
-        ct = np.asarray([f[2] for f in frontier], dtype=np.int64)
+        st = np.asarray(f_st, dtype=np.int64)
+        ct = np.asarray(f_ct, dtype=np.int64)
         per = max(1, int(p.hist_mem_budget // (k * Bs * 2 * 8)))
         pk = torch.empty((n, 12), dtype=torch.float64, device=dev)
         mask = torch.empty((n, Bs), dtype=torch.uint8, device=dev)
@@ -1052,23 +1105,29 @@ class TreeGrower:
             else:
                 pb.fill_(1.0)
             va, vb = pa, pb   # position order == row order while ridx is the identity
-        tree = Tree()
-        root = tree.add_node(0, 0.0)
-        # frontier entries: [node_id, start, count_local, depth]
-        frontier = [[root, 0, N, 0]]
-        H_prev, prev_slot = None, {}
+        tb = _TreeBuf()
+        # frontier as arrays (all nodes of a level share the depth): node ids,
+        # row segments [st, st + ct) of ridx, channel totals from the parent's
+        # split record (used when the last level builds no histograms)
+        f_id = np.zeros(1, dtype=np.int64)
+        f_st = np.zeros(1, dtype=np.int64)
+        f_ct = np.full(1, N, dtype=np.int64)
+        f_tot = None
+        depth = 0
+        H_prev = None
         wyy_prev, wyy_level = None, None
-        pair_info = []     # for level>0: (left_id, right_id, parent_slot, build_left)
-        child_tot = {}     # node id -> channel totals from the parent's split record
-        leaves, leaf_tot = [], []
+        # (build slot, derived slot, parent slot) of the node pairs of this level
+        p_build = p_der = p_par = None
+        leaf_parts = []    # per level: (node ids, starts, counts, totals [k, C])
         level = 0
         async_part = self.dev.type == "cuda" and not p.max_leaves and not self.use_payload and \
             os.environ.get("H2O3_ASYNC_PART", "1") == "1" and os.environ.get("H2O3_PART", "ballot") == "ballot"
-        while frontier:
+        is_cat_np = np.asarray(bd.is_cat, dtype=bool)
+        cutmat = self._cut_matrix()
+        lvmaps = self.__dict__.setdefault("_lvmaps", {})
+        while f_id.size:
             self._level = level
-            n_front = len(frontier)
-            slot_of = {nd[0]: i for i, nd in enumerate(frontier)}
-            depth = frontier[0][3]
+            n_front = int(f_id.size)
             can_split = depth < p.max_depth
             C_ = tree_ops.channels(mode)
             level_bytes = self.Fpad * n_front * bd.Bs * C_ * 8
@@ -1085,45 +1144,35 @@ class TreeGrower:
                 H = la[0][:, :n_front].contiguous()
                 wyy_level = la[1][:n_front] if la[1] is not None else None
                 if os.environ.get("H2O3_LA_CHECK") == "1":
-                    self._la_check(la, pair_info, slot_of)
+                    self._la_check(la, p_build, p_der, p_par)
             elif chunked:
-                # frontier too wide for one level of histograms (deep DRF trees, wide
-                # high-cardinality data): histograms of node batches straight from the
-                # rows, split records concatenated, no parent level kept (no subtraction)
+                # frontier too wide for one level of histograms, or column-sampled
+                # levels on the pair path: no parent level kept (no subtraction)
                 H, H_prev, wyy_level = None, None, None
             elif not can_split and level > 0:
                 # last level: no histograms needed, leaf totals come from the parent split stats
                 H = None
             elif level == 0 or H_prev is None:
-                build = list(range(n_front))
-                Hb = self._build_hist(ridx, va, vb, mode, [f[1] for f in frontier], [f[2] for f in frontier])
-                H = Hb
+                H = self._build_hist(ridx, va, vb, mode, f_st, f_ct)
                 wyy_level = self._last_wyy
             else:
-                build_slots, der_slots, par_slots, sib_idx = [], [], [], []
-                for (lid, rid, pslot, build_left) in pair_info:
-                    b, d = (lid, rid) if build_left else (rid, lid)
-                    build_slots.append(slot_of[b])
-                    der_slots.append(slot_of[d])
-                    par_slots.append(pslot)
-                Hb = self._build_hist(ridx, va, vb, mode, [frontier[s][1] for s in build_slots],
-                                      [frontier[s][2] for s in build_slots])
+                Hb = self._build_hist(ridx, va, vb, mode, f_st[p_build], f_ct[p_build])
             if la is not None:
                 pass
             elif level > 0 and H_prev is not None and (can_split or level == 0) and self.dev.type == "cuda":
                 # copy + parent-minus-built subtraction in one kernel
                 clamp = {0: 0b1, 1: 0b0}.get(mode, (1 << tree_ops.channels(mode)) - 1)
                 wb = self._last_wyy if mode == 0 else None
-                H, wyy_n = tree_ops.hist_sibling(Hb, H_prev, build_slots, der_slots, par_slots, n_front, clamp,
+                H, wyy_n = tree_ops.hist_sibling(Hb, H_prev, p_build, p_der, p_par, n_front, clamp,
                                                  wyy_b=wb, wyy_prev=wyy_prev if wb is not None else None)
                 if wyy_n is not None:
                     wyy_level = wyy_n
                 del Hb
             elif level > 0 and H_prev is not None and can_split:
                 H = torch.empty((Hb.shape[0], n_front) + tuple(Hb.shape[2:]), dtype=Hb.dtype, device=Hb.device)
-                bs = torch.tensor(build_slots, device=Hb.device)
-                ds = torch.tensor(der_slots, device=Hb.device)
-                ps = torch.tensor(par_slots, device=Hb.device)
+                bs = torch.as_tensor(p_build, device=Hb.device)
+                ds = torch.as_tensor(p_der, device=Hb.device)
+                ps = torch.as_tensor(p_par, device=Hb.device)
                 H[:, bs] = Hb
                 H[:, ds] = (H_prev[:, ps] - Hb).clamp_min_(0) if mode != 1 else (H_prev[:, ps] - Hb)
                 if mode == 0 and self._last_wyy is not None:
@@ -1135,6 +1184,7 @@ class TreeGrower:
                     H[:, ds, :, 1] = H_prev[:, ps, :, 1] - Hb[:, :, :, 1]
                 del Hb
             nleft_pre = None
+            ok_h = None
             if can_split:
                 sel = self._col_sel(n_front, depth) if direct else None
                 cm = None if (direct and self.dev.type == "cuda") else self._col_mask(n_front, depth, sel=sel)
@@ -1143,16 +1193,15 @@ class TreeGrower:
                 node_wyy = wyy_level if mode == 0 else None
                 with phase("tree.split"):
                     if direct and self.dev.type == "cuda":
-                        sp = self._pair_direct_dev(ridx, va, vb, mode, frontier, sel)
+                        sp = self._pair_direct_dev(ridx, va, vb, mode, f_st, f_ct, sel)
                     elif direct:
-                        sp = self._pair_direct_splits(ridx, va, vb, mode, frontier, cm)
+                        sp = self._pair_direct_splits(ridx, va, vb, mode, f_st, f_ct, cm)
                     elif chunked:
                         per = max(1, int(p.hist_mem_budget // max(1, self.Fpad * bd.Bs * C_ * 8)))
                         parts = []
                         need = self._hist_need(cm)
                         for a in range(0, n_front, per):
-                            fr_ = frontier[a:a + per]
-                            Hc = self._build_hist(ridx, va, vb, mode, [f[1] for f in fr_], [f[2] for f in fr_],
+                            Hc = self._build_hist(ridx, va, vb, mode, f_st[a:a + per], f_ct[a:a + per],
                                                   need_mask=None if need is None else need[a:a + per])
                             wyy_c = self._last_wyy if mode == 0 else None
                             parts.append(self._find_splits(Hc, cm[a:a + per], wyy_c, want_pk=False))
@@ -1168,20 +1217,20 @@ class TreeGrower:
                         # no ridx2 <- ridx copy: every frontier segment is rewritten (non-splitting
                         # nodes in place), earlier leaves are identical in both buffers already
                         pay = (self._pos1[0], None, self._pos1[1], None) if self._pos1 is not None else None
-                        tree_ops.partition_async(bd, ridx, ridx2, sp["feat_i32"], sp["mask"],
-                                                 [f[1] for f in frontier], [f[2] for f in frontier],
+                        tree_ops.partition_async(bd, ridx, ridx2, sp["feat_i32"], sp["mask"], f_st, f_ct,
                                                  payload=pay, pk=pkd, pk_col=11)
                     # the record's copy is queued BEFORE the look-ahead kernels, so
                     # the host gets it while the GPU builds the next level
                     pk_h = self._d2h_async(pkd)
-                    self._maybe_lookahead(pkd, (10, 11, 4 + (mode == 1), 6 + (mode == 1)), frontier, mode, va, vb,
-                                          ridx2, H, wyy_level, depth, level_bytes, chunked)
+                    self._maybe_lookahead(pkd, (10, 11, 4 + (mode == 1), 6 + (mode == 1)), f_st, f_ct, mode, va,
+                                          vb, ridx2, H, wyy_level, depth, level_bytes, chunked)
                     pk = self._d2h_wait(pk_h)
                     ok_h = pk[:, 10] > 0
-                    nleft_pre = pk[:, 11].astype(np.int64).tolist()
-                cols = [] if nleft_pre is not None else [sp["gain"].view(nn_, 1).to(torch.float64), sp["feat"].view(nn_, 1).to(torch.float64),
-                        sp["t"].view(nn_, 1).to(torch.float64), sp["opt"].view(nn_, 1).to(torch.float64),
-                        sp["L"].to(torch.float64), sp["R"].to(torch.float64), sp["tot"].to(torch.float64)]
+                    nleft_pre = pk[:, 11].astype(np.int64)
+                cols = [] if nleft_pre is not None else [
+                    sp["gain"].view(nn_, 1).to(torch.float64), sp["feat"].view(nn_, 1).to(torch.float64),
+                    sp["t"].view(nn_, 1).to(torch.float64), sp["opt"].view(nn_, 1).to(torch.float64),
+                    sp["L"].to(torch.float64), sp["R"].to(torch.float64), sp["tot"].to(torch.float64)]
                 if async_part and nleft_pre is None:
                     # split decision + partition of the whole frontier on the device: no
                     # host round trip between the split search and the row partition
@@ -1190,13 +1239,13 @@ class TreeGrower:
                     ok_d = torch.isfinite(sp["gain"].to(torch.float64))
                     if p.criterion != "xgb":
                         ok_d &= w_d >= 2 * p.min_rows
-                    feat_all = torch.where(ok_d, sp["feat"].to(torch.int64), torch.zeros_like(sp["feat"].to(torch.int64)))
+                    feat_all = torch.where(ok_d, sp["feat"].to(torch.int64),
+                                           torch.zeros_like(sp["feat"].to(torch.int64)))
                     mask_all = torch.where(ok_d.view(-1, 1), sp["mask"].to(torch.uint8),
                                            torch.ones_like(sp["mask"], dtype=torch.uint8))
                     with phase("tree.partition"):
                         pay = (self._pos1[0], None, self._pos1[1], None) if self._pos1 is not None else None
-                        nleft_d = tree_ops.partition_async(bd, ridx, ridx2, feat_all, mask_all,
-                                                           [f[1] for f in frontier], [f[2] for f in frontier],
+                        nleft_d = tree_ops.partition_async(bd, ridx, ridx2, feat_all, mask_all, f_st, f_ct,
                                                            payload=pay)
                     cols += [ok_d.view(nn_, 1).to(torch.float64), nleft_d.view(nn_, 1).to(torch.float64)]
                 # ONE device->host transfer of every per-node scalar of the level
@@ -1205,109 +1254,103 @@ class TreeGrower:
                     pk_h = self._d2h_async(rec)
                     if async_part:
                         self._maybe_lookahead(rec, (4 + 3 * C, 5 + 3 * C, 4 + (mode == 1), 4 + C + (mode == 1)),
-                                              frontier, mode, va, vb, ridx2, H, wyy_level, depth, level_bytes,
+                                              f_st, f_ct, mode, va, vb, ridx2, H, wyy_level, depth, level_bytes,
                                               chunked)
                     pk = self._d2h_wait(pk_h)
                     if async_part:
                         ok_h = pk[:, 4 + 3 * C] > 0
-                        nleft_pre = pk[:, 5 + 3 * C].astype(np.int64).tolist()
-                gains = pk[:, 0].tolist()
-                feats = pk[:, 1].astype(np.int64).tolist()
-                t_l = pk[:, 2].astype(np.int64).tolist()
-                opt_l = pk[:, 3].astype(np.int64).tolist()
+                        nleft_pre = pk[:, 5 + 3 * C].astype(np.int64)
+                gains = pk[:, 0]
+                feats = pk[:, 1].astype(np.int64)
+                t_a = pk[:, 2].astype(np.int64)
+                opt_a = pk[:, 3].astype(np.int64)
                 Ls = pk[:, 4:4 + C]
                 Rs = pk[:, 4 + C:4 + 2 * C]
                 tots = pk[:, 4 + 2 * C:4 + 3 * C]
             else:
                 # totals only
-                tots = self._totals(H).numpy() if H is not None else \
-                    np.stack([child_tot[nd[0]] for nd in frontier])
+                tots = self._totals(H).numpy() if H is not None else f_tot
                 gains = None
-            tots_l = tots.tolist()
-            split_ids, split_slots = [], []
-            for i, (nid_, st, ct, d) in enumerate(frontier):
-                tot_i = tots_l[i]
-                tree.weight[nid_] = (tot_i[0] if mode != 1 else tot_i[1]) + (tot_i[2] if mode == 3 else 0.0)
-                if nleft_pre is not None:
-                    ok = bool(ok_h[i])
-                else:
-                    ok = can_split and gains is not None and math.isfinite(gains[i])
-                    if ok and p.criterion != "xgb" and tree.weight[nid_] < 2 * p.min_rows:
-                        ok = False
-                if ok and p.max_leaves and (len(leaves) + n_front + len(split_ids) + 1) > p.max_leaves:
-                    ok = False
-                if ok:
-                    split_ids.append(i)
-                else:
-                    leaves.append(nid_)
-                    leaf_tot.append(tots[i])
-                    # keep the segment for the nid pass
-                    frontier[i].append("leaf")
-            if not split_ids:
-                self._leaf_segments = [(f[0], f[1], f[2]) for f in frontier]
+            tots = np.asarray(tots, dtype=np.float64)
+            w_a = (tots[:, 0] if mode != 1 else tots[:, 1]) + (tots[:, 2] if mode == 3 else 0.0)
+            tb.weight[f_id] = w_a
+            if ok_h is not None:
+                ok = np.asarray(ok_h, dtype=bool).copy()
+            elif can_split and gains is not None:
+                ok = np.isfinite(gains)
+                if p.criterion != "xgb":
+                    ok &= w_a >= 2 * p.min_rows
+            else:
+                ok = np.zeros(n_front, dtype=bool)
+            if p.max_leaves:
+                # leaf budget, node by node in frontier order (the leaves of this
+                # level counted as they are decided)
+                n_leaves = sum(part[0].size for part in leaf_parts)
+                n_split = 0
+                for i in range(n_front):
+                    if ok[i] and (n_leaves + n_front + n_split + 1) > p.max_leaves:
+                        ok[i] = False
+                    if ok[i]:
+                        n_split += 1
+                    else:
+                        n_leaves += 1
+            lf = ~ok
+            if lf.any():
+                leaf_parts.append((f_id[lf], f_st[lf], f_ct[lf], tots[lf]))
+            sids = np.nonzero(ok)[0]
+            if sids.size == 0:
                 if nleft_pre is not None:
                     ridx, ridx2 = ridx2, ridx   # the (identity) partition already ran
                     if self._pos1 is not None:
                         self._pos1.reverse()
                 break
-            # record splits in the tree
-            all_split = len(split_ids) == n_front
-            any_cat = any(bd.is_cat[feats[i]] for i in split_ids)
-            masks = None
-            if any_cat or nleft_pre is None:
-                masks = sp["mask"] if all_split else sp["mask"][tree_ops._h2d(np.asarray(split_ids, dtype=np.int64),
-                                                                              sp["mask"].device)]
-            masks_h = None
-            if any_cat:
-                # only the categorical splits' mask rows cross to the host (one
-                # gather + copy); node j's row is masks_h[crow[j]]
-                cj = [j for j, i in enumerate(split_ids) if bd.is_cat[feats[i]]]
-                crow = {j: q for q, j in enumerate(cj)}
-                masks_h = masks[tree_ops._h2d(np.asarray(cj, dtype=np.int64), masks.device)].cpu().numpy() \
-                    if len(cj) < len(split_ids) else masks.cpu().numpy()
-            new_front, new_pairs = [], []
-            part_starts, part_counts, part_feats = [], [], []
-            si = np.asarray(split_ids, dtype=np.int64)
-            Lsel, Rsel = Ls[si], Rs[si]
+            # record the splits in the tree (vectorized over the level)
+            k = int(sids.size)
+            nid_s = f_id[sids]
+            f_s = feats[sids]
+            opt_s = opt_a[sids]
+            t_s = t_a[sids]
+            Lsel, Rsel = Ls[sids], Rs[sids]
             wl_a = (Lsel[:, 0] if mode != 1 else Lsel[:, 1]) + (Lsel[:, 2] if mode == 3 else 0.0)
             wr_a = (Rsel[:, 0] if mode != 1 else Rsel[:, 1]) + (Rsel[:, 2] if mode == 3 else 0.0)
-            build_left = (wl_a <= wr_a).tolist()
-            first = tree.add_children(frontier[split_ids[0]][3] + 1, Lsel[:, 0].tolist(), Rsel[:, 0].tolist())
-            lvmaps = self.__dict__.setdefault("_lvmaps", {})
-            for j, i in enumerate(split_ids):
-                nid_, st, ct, d = frontier[i][:4]
-                f = feats[i]
-                tree.feat[nid_] = f
-                tree.gain[nid_] = gains[i]
-                tree.na_left[nid_] = opt_l[i] == 1
-                if bd.is_cat[f]:
-                    tree.is_cat[nid_] = True
+            build_left = wl_a <= wr_a
+            first = tb.add_children(depth + 1, Lsel[:, 0], Rsel[:, 0])
+            lid = first + 2 * np.arange(k, dtype=np.int64)
+            tb.feat[nid_s] = f_s
+            tb.gain[nid_s] = gains[sids]
+            tb.na_left[nid_s] = opt_s == 1
+            tb.left[nid_s] = lid
+            tb.right[nid_s] = lid + 1
+            cat_s = is_cat_np[f_s]
+            num = ~cat_s
+            if num.any():
+                tb.thr[nid_s[num]] = np.where(opt_s[num] == 2, np.inf, cutmat[f_s[num], np.minimum(t_s[num],
+                                                                                                   cutmat.shape[1] - 1)])
+                tb.split_code[nid_s[num]] = t_s[num]
+            all_split = k == n_front
+            masks = None
+            if cat_s.any() or nleft_pre is None:
+                masks = sp["mask"] if all_split else sp["mask"][tree_ops._h2d(sids, sp["mask"].device)]
+            if cat_s.any():
+                # only the categorical splits' mask rows cross to the host (one gather + copy)
+                cj = np.nonzero(cat_s)[0]
+                masks_h = masks[tree_ops._h2d(cj, masks.device)].cpu().numpy() if cj.size < k else \
+                    masks.cpu().numpy()
+                tb.is_cat[nid_s[cj]] = True
+                tb.thr[nid_s[cj]] = np.nan
+                for q, j in enumerate(cj.tolist()):
+                    f = int(f_s[j])
                     lvm = lvmaps.get(f)
                     if lvm is None:
                         card = bd.cat_card[f]
                         # ungrouped levels map 1:1 to codes: a slice (view) of the level's mask rows
                         lvm = lvmaps[f] = slice(0, card) if (bd.cat_group[f] == 1 and card <= bd.Bs - 1) else \
                             np.minimum(np.arange(card) // bd.cat_group[f], bd.Bs - 2)
-                    tree.cat_left[nid_] = masks_h[crow[j]][lvm]
-                    tree.thr[nid_] = float("nan")
-                else:
-                    if opt_l[i] == 2:
-                        tree.thr[nid_] = float("inf")     # NA vs rest: every number goes left
-                    else:
-                        tree.thr[nid_] = bd.split_value(f, t_l[i])
-                    tree.split_code[nid_] = t_l[i]
-                lid = first + 2 * j
-                rid = lid + 1
-                tree.left[nid_], tree.right[nid_] = lid, rid
-                part_starts.append(st)
-                part_counts.append(ct)
-                part_feats.append(f)
-                new_pairs.append((lid, rid, j, build_left[j]))
-                child_tot[lid] = Lsel[j]
-                child_tot[rid] = Rsel[j]
+                    tb.cat_left[int(nid_s[j])] = masks_h[q][lvm]
+            st_s, ct_s = f_st[sids], f_ct[sids]
             # partition
             if nleft_pre is not None:
-                nleft = [nleft_pre[i] for i in split_ids]
+                nleft = nleft_pre[sids]
                 if self._pos1 is not None:
                     self._pos1.reverse()
             else:
@@ -1319,56 +1362,58 @@ class TreeGrower:
                     pay = (pa, pb, pa2, pb2) if self.use_payload else None
                     if self._pos1 is not None:
                         pay = (self._pos1[0], None, self._pos1[1], None)
-                    nleft = tree_ops.partition(bd, ridx, ridx2, part_feats, masks, part_starts, part_counts,
-                                               payload=pay)
+                    nleft = np.asarray(tree_ops.partition(bd, ridx, ridx2, f_s, masks, st_s, ct_s, payload=pay),
+                                       dtype=np.int64)
                     if self._pos1 is not None:
                         self._pos1.reverse()
             ridx, ridx2 = ridx2, ridx
             if self.use_payload:
                 pa, pa2, pb, pb2 = pa2, pa, pb2, pb
                 va, vb = pa, pb
-            for j, i in enumerate(split_ids):
-                nid_, st, ct, d = frontier[i][:4]
-                lid, rid = tree.left[nid_], tree.right[nid_]
-                nl = nleft[j]
-                new_front.append([lid, st, nl, d + 1])
-                new_front.append([rid, st + nl, ct - nl, d + 1])
-            # keep leaf segments of this level
-            self._pending_leaf_segs = getattr(self, "_pending_leaf_segs", [])
-            for f in frontier:
-                if len(f) > 4:
-                    self._pending_leaf_segs.append((f[0], f[1], f[2]))
+            # next frontier: (left, right) of every split node, in order
+            f_id = np.stack([lid, lid + 1], 1).reshape(-1)
+            f_st = np.stack([st_s, st_s + nleft], 1).reshape(-1)
+            f_ct = np.stack([nleft, ct_s - nleft], 1).reshape(-1)
+            f_tot = np.stack([Lsel, Rsel], 1).reshape(2 * k, -1)
+            jj = 2 * np.arange(k, dtype=np.int64)
+            p_build = jj + (~build_left)
+            p_der = jj + build_left
             # parent hists for the next level (only split nodes)
             if H is None:
                 H_prev, wyy_prev = None, None   # chunked level: next level builds from rows
+                p_par = np.arange(k, dtype=np.int64)
             elif self.dev.type == "cuda":
                 # the sibling kernel indexes the parent level directly: keep the
-                # whole level and remap the pairs' parent slots
+                # whole level and point the pairs at their parents' slots
                 H_prev = H
                 wyy_prev = wyy_level if mode == 0 else None
-                new_pairs = [(l_, r_, split_ids[j_], bl_) for (l_, r_, j_, bl_) in new_pairs]
+                p_par = sids.astype(np.int64)
             else:
-                sid = torch.tensor(split_ids, device=H.device)
+                sid = torch.as_tensor(sids, device=H.device)
                 H_prev = H[:, sid]
                 wyy_prev = wyy_level[sid] if (mode == 0 and wyy_level is not None) else None
-            pair_info = new_pairs
-            frontier = new_front
+                p_par = np.arange(k, dtype=np.int64)
+            depth += 1
             level += 1
-        segs = getattr(self, "_pending_leaf_segs", []) + getattr(self, "_leaf_segments", [])
-        self._pending_leaf_segs = []
-        self._leaf_segments = []
-        leaf_index = {nid_: k for k, nid_ in enumerate(leaves)}
-        lids = [leaf_index[s[0]] for s in segs]
+        tree = tb.to_tree()
+        if leaf_parts:
+            leaf_ids = np.concatenate([q[0] for q in leaf_parts])
+            leaf_st = np.concatenate([q[1] for q in leaf_parts])
+            leaf_ct = np.concatenate([q[2] for q in leaf_parts])
+            leaf_tot_np = np.concatenate([q[3] for q in leaf_parts], 0)
+        else:
+            leaf_ids = leaf_st = leaf_ct = np.zeros(0, dtype=np.int64)
+            leaf_tot_np = np.zeros((0, C))
+        leaves = leaf_ids.tolist()
+        lids = list(range(len(leaves)))
         nid = None
         if want_nid:
             with phase("tree.nid"):
-                nid = tree_ops.fill_nid(ridx, lids, [s[1] for s in segs], [s[2] for s in segs], N)
+                nid = tree_ops.fill_nid(ridx, lids, leaf_st.tolist(), leaf_ct.tolist(), N)
         self.ridx, self.ridx2 = ridx, ridx2
         self._pay = [pa, pb, pa2, pb2]
-        self.last_segs = (lids, [s[1] for s in segs], [s[2] for s in segs])
-        leaf_tot_t = torch.from_numpy(np.asarray(np.stack([np.asarray(x, dtype=np.float64) for x in leaf_tot]),
-                                                 dtype=np.float64)) if leaf_tot else \
-            torch.zeros((0, C), dtype=torch.float64)
+        self.last_segs = (lids, leaf_st.tolist(), leaf_ct.tolist())
+        leaf_tot_t = torch.from_numpy(np.ascontiguousarray(leaf_tot_np, dtype=np.float64))
         return tree, nid, leaves, leaf_tot_t
 
     def _d2h_async(self, t):
@@ -1395,7 +1440,7 @@ class TreeGrower:
             ev.synchronize()
         return h.numpy().copy()
 
-    def _maybe_lookahead(self, rec, cols, frontier, mode, va, vb, ridx_next, H, wyy_level, depth, level_bytes,
+    def _maybe_lookahead(self, rec, cols, f_st, f_ct, mode, va, vb, ridx_next, H, wyy_level, depth, level_bytes,
                          chunked):
         """Launch the NEXT level's histograms now (device-built work list,
         tree_ops.hist_build_dev + hist_sibling_dev), before the host syncs on
@@ -1408,7 +1453,6 @@ class TreeGrower:
         if os.environ.get("H2O3_LOOKAHEAD", "1") != "1" or self.dev.type != "cuda" or chunked or H is None or \
                 depth + 1 >= p.max_depth or mode not in (0, 1) or p.max_leaves:
             return
-        n = len(frontier)
         if 2 * level_bytes + H.numel() * 8 > p.hist_mem_budget:
             return
         posv = False
@@ -1418,9 +1462,8 @@ class TreeGrower:
         elif mode == 0 and getattr(self, "_va_eff", None) is not None:
             va_n, vb_n = self._va_eff, None
         with phase("tree.hist"), phase("tree.hist.lookahead"):
-            r = tree_ops.hist_build_dev(self.bd, ridx_next, va_n, vb_n, mode, rec, cols,
-                                        [f[1] for f in frontier], [f[2] for f in frontier], self._vmax, posv=posv,
-                                        unit_w=getattr(self, "_unit_w", False))
+            r = tree_ops.hist_build_dev(self.bd, ridx_next, va_n, vb_n, mode, rec, cols, f_st, f_ct, self._vmax,
+                                        posv=posv, unit_w=getattr(self, "_unit_w", False))
             if r is None:
                 return
             Hb, wyy_b, slots, cnts = r
@@ -1436,15 +1479,28 @@ class TreeGrower:
                                                   wyy_prev=wyy_level if mode == 0 else None)
         self._la = (Hn, wyy_n, slots, cnts)
 
-    def _la_check(self, la, pair_info, slot_of):
+    def _la_check(self, la, p_build, p_der, p_par):
         """Debug (H2O3_LA_CHECK=1): the device-built pair slots equal the host's."""
         slots, cnts = la[2].cpu().numpy(), la[3].cpu().numpy()
-        nb = len(pair_info)
+        nb = len(p_build)
         assert int(cnts[0]) == nb, (int(cnts[0]), nb)
         nl = len(slots) // 3
-        for j, (lid, rid, pslot, build_left) in enumerate(pair_info):
-            b, d = (lid, rid) if build_left else (rid, lid)
-            assert slots[j] == slot_of[b] and slots[nl + j] == slot_of[d] and slots[2 * nl + j] == pslot, j
+        assert np.array_equal(slots[:nb], p_build) and np.array_equal(slots[nl:nl + nb], p_der) and \
+            np.array_equal(slots[2 * nl:2 * nl + nb], p_par)
+
+    def _cut_matrix(self):
+        """[F, max_cuts + 1] numeric split values by (feature, threshold code):
+        cuts[f][t], +inf past the last cut (BinnedData.split_value)."""
+        cm = getattr(self, "_cutmat", None)
+        if cm is None:
+            bd = self.bd
+            w = 1 + max([len(c) for c in bd.cuts if c is not None] or [0])
+            cm = np.full((bd.F, w), np.inf)
+            for f, c in enumerate(bd.cuts):
+                if c is not None and len(c):
+                    cm[f, :len(c)] = c
+            self._cutmat = cm
+        return cm
 
     def _totals(self, H):
         """Per-node channel totals [n, C] (global), from feature 0."""
