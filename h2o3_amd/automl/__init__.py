@@ -450,7 +450,7 @@ class H2OAutoML:
             if tag in self._done_steps:
                 continue
             if algo != "StackedEnsemble" and not self._budget_left():
-                break
+                continue     # out of time: skip the remaining base-model steps, still build the ensembles
             if not self._allowed(algo):
                 continue
             self._run_step(algo, step, data, classification)
