@@ -1209,6 +1209,134 @@ __global__ __launch_bounds__(256) void pair_hist_kernel(const CodeT* __restrict_
   }
 }
 
+// Several pairs of the SAME node per workgroup (KP <= 4 consecutive pairs,
+// LDS = KP x Bs x 2 x 8 B): the node's row ids and responses are read once per
+// group instead of once per pair; every pair still gathers its own code.
+// work[i].w: bit0 = single item (store), bit1 = wyy (group holds the node's
+// first pair), bits 8..15 = pairs in the group.
+template <typename CodeT, int MODE, bool HAS_VB, bool POSV, int KP>
+__global__ __launch_bounds__(256) void pair_hist_multi_kernel(const CodeT* __restrict__ codes_col, long long ncol,
+                                                              const int* __restrict__ ridx,
+                                                              const float* __restrict__ va,
+                                                              const float* __restrict__ vb,
+                                                              const int4* __restrict__ work,
+                                                              const int* __restrict__ pfeat, int Bs, float s0,
+                                                              float s1, double* __restrict__ Hp,
+                                                              double* __restrict__ pwyy) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long lh[];
+  __shared__ double red[4];
+  const int4 wk = work[blockIdx.x];
+  const int pair0 = wk.x;
+  const int np = (wk.w >> 8) & 0xff;
+  const CodeT* cc[KP];
+#pragma unroll
+  for (int j = 0; j < KP; ++j) cc[j] = codes_col + (size_t)pfeat[pair0 + min(j, np - 1)] * (size_t)ncol;
+  const int nb = Bs * 2;
+  for (int i = threadIdx.x; i < KP * nb; i += blockDim.x) lh[i] = 0ull;
+  __syncthreads();
+  const bool do_wyy = MODE == 0 && (wk.w & 2) != 0 && pwyy != nullptr;
+  double wyy = 0.0;
+  const int end = wk.y + wk.z;
+  constexpr int U = 2;
+  for (int p0 = wk.y + (int)threadIdx.x; p0 < end; p0 += U * 256) {
+    int r[U];
+    unsigned int c[U][KP];
+    float xa[U], xb[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) r[u] = ridx[min(p0 + u * 256, end - 1)];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int vi = POSV ? min(p0 + u * 256, end - 1) : r[u];
+      xa[u] = va[vi];
+      xb[u] = HAS_VB ? vb[vi] : 1.f;
+#pragma unroll
+      for (int j = 0; j < KP; ++j) c[u][j] = (unsigned int)cc[j][r[u]];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (p0 + u * 256 >= end) continue;
+      float c0, c1;
+      if (MODE == 0) {
+        const float y = xa[u];
+        const float w = HAS_VB ? xb[u] : (y == y ? 1.f : 0.f);
+        if (w == 0.f) continue;
+        c0 = w;
+        c1 = w * y;
+        if (do_wyy) wyy += (double)c1 * (double)y;
+      } else {
+        c0 = xa[u];
+        c1 = xb[u];
+      }
+      const unsigned long long a0 = (unsigned long long)__float2ll_rn(c0 * s0);
+      const unsigned long long a1 = (unsigned long long)__float2ll_rn(c1 * s1);
+#pragma unroll
+      for (int j = 0; j < KP; ++j) {
+        if (j < np) {
+          unsigned long long* h = lh + j * nb + c[u][j] * 2;
+          __hip_atomic_fetch_add(h, a0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          __hip_atomic_fetch_add(h + 1, a1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  const double i0 = 1.0 / (double)s0, i1 = 1.0 / (double)s1;
+  double* o = Hp + (size_t)pair0 * nb;
+  const bool single = (wk.w & 1) != 0;
+  for (int i = threadIdx.x; i < np * nb; i += blockDim.x) {
+    const long long v = (long long)lh[i];
+    const double d = (double)v * ((i & 1) ? i1 : i0);
+    if (single) o[i] = d;
+    else if (v != 0) gbl_add(o + i, d);
+  }
+  if (do_wyy) {
+    wyy = wave_sum(wyy);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = wyy;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const double t = red[0] + red[1] + red[2] + red[3];
+      if (single) pwyy[pair0] = t;
+      else gbl_add(pwyy + pair0, t);
+    }
+  }
+}
+
+template <typename CodeT, int MODE>
+static void pair_hist_multi_launch(bool has_vb, bool posv, int n_work, size_t lds, hipStream_t s,
+                                   const void* codes_col, long long ncol, const int* ridx, const float* va,
+                                   const float* vb, const int4* work, const int* pfeat, int Bs, float s0, float s1,
+                                   double* Hp, double* pwyy) {
+  const CodeT* cc = (const CodeT*)codes_col;
+#define PHM(V, PV)                                                                                          \
+  hipLaunchKernelGGL((pair_hist_multi_kernel<CodeT, MODE, V, PV, 4>), dim3(n_work), dim3(256), lds, s, cc, \
+                     ncol, ridx, va, vb, work, pfeat, Bs, s0, s1, Hp, pwyy)
+  if (has_vb) { if (posv) PHM(true, true); else PHM(true, false); }
+  else { if (posv) PHM(false, true); else PHM(false, false); }
+#undef PHM
+}
+
+// Grouped version of h2o_pair_hist: work[i].w bits 8..15 = pairs in the group
+// (<= 4, consecutive pairs of one node starting at work[i].x).
+extern "C" int h2o_pair_hist4(const void* codes_col, int code_bytes, long long ncol, const int* ridx,
+                              const float* va, const float* vb, const int* work, int n_work, const int* pfeat,
+                              int Bs, int mode, int posv, float s0, float s1, double* Hp, double* pwyy,
+                              hipStream_t s) {
+  if (n_work <= 0) return 0;
+  if (Bs < 2 || Bs > 4096 || (mode != 0 && mode != 1) || (mode == 1 && vb == nullptr)) return -1;
+  const size_t lds = (size_t)4 * Bs * 2 * sizeof(unsigned long long);
+  if (lds > 160 * 1024) return -2;
+  const int4* w = (const int4*)work;
+  const bool hv = vb != nullptr;
+  if (code_bytes == 1) {
+    if (mode == 0) pair_hist_multi_launch<uint8_t, 0>(hv, posv, n_work, lds, s, codes_col, ncol, ridx, va, vb, w, pfeat, Bs, s0, s1, Hp, pwyy);
+    else pair_hist_multi_launch<uint8_t, 1>(hv, posv, n_work, lds, s, codes_col, ncol, ridx, va, vb, w, pfeat, Bs, s0, s1, Hp, pwyy);
+  } else {
+    if (mode == 0) pair_hist_multi_launch<uint16_t, 0>(hv, posv, n_work, lds, s, codes_col, ncol, ridx, va, vb, w, pfeat, Bs, s0, s1, Hp, pwyy);
+    else pair_hist_multi_launch<uint16_t, 1>(hv, posv, n_work, lds, s, codes_col, ncol, ridx, va, vb, w, pfeat, Bs, s0, s1, Hp, pwyy);
+  }
+  return (int)hipGetLastError();
+}
+
 template <typename CodeT, int MODE>
 static void pair_hist_launch(bool has_vb, bool posv, int n_work, size_t lds, hipStream_t s, const void* codes_col,
                              long long ncol, const int* ridx, const float* va, const float* vb, const int4* work,

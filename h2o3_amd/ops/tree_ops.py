@@ -344,6 +344,8 @@ def _hist_build_torch(bd, ridx, va, vb, mode, starts, counts, hist):
 
 
 _PAIR_CHUNK = 16384
+# pairs of one node per workgroup in pair_hist_dev (1 = one pair per workgroup)
+_PAIR_KP = int(os.environ.get("H2O3_PAIR_KP", 4))
 
 
 def pair_hist(bd, ridx, va, vb, mode, node_st, node_ct, pair_node, pair_feat, vmax=None, posv=False,
@@ -470,10 +472,21 @@ def pair_hist_dev(bd, ridx, va, vb, mode, node_st, node_ct, sel, vmax, posv=Fals
     multi = np.nonzero((nch > 1) | (ct == 0))[0]
     tab_d = _h2d(np.concatenate([tab.astype(np.int32).reshape(-1), multi.astype(np.int32)]), dev)
     m = len(tab)
-    items = tab_d[:4 * m].view(m, 1, 4).expand(m, k, 4).clone()
-    j = torch.arange(k, dtype=torch.int32, device=dev).view(1, k)
-    items[:, :, 0] = items[:, :, 0] * k + j
-    items[:, :, 3] += (j == 0).to(torch.int32) * 2
+    kp = _PAIR_KP if k > 1 else 1
+    if kp > 1:
+        # groups of up to kp consecutive pairs of one node per workgroup
+        ng = -(-k // kp)
+        items = tab_d[:4 * m].view(m, 1, 4).expand(m, ng, 4).clone()
+        g = torch.arange(ng, dtype=torch.int32, device=dev).view(1, ng)
+        items[:, :, 0] = items[:, :, 0] * k + g * kp
+        items[:, :, 3] += (g == 0).to(torch.int32) * 2 + torch.clamp(k - g * kp, max=kp) * 256
+        n_items = m * ng
+    else:
+        items = tab_d[:4 * m].view(m, 1, 4).expand(m, k, 4).clone()
+        j = torch.arange(k, dtype=torch.int32, device=dev).view(1, k)
+        items[:, :, 0] = items[:, :, 0] * k + j
+        items[:, :, 3] += (j == 0).to(torch.int32) * 2
+        n_items = m * k
     pfeat = sel.to(torch.int32).reshape(-1).contiguous()
     Hp = torch.empty((P, Bs, 2), dtype=torch.float64, device=dev)
     if multi.size:
@@ -482,9 +495,13 @@ def pair_hist_dev(bd, ridx, va, vb, mode, node_st, node_ct, sel, vmax, posv=Fals
     pwyy = torch.zeros(P, dtype=torch.float64, device=dev) if want_wyy else None
     if m:
         s0, s1 = (fixed_point_scale(v, min(chunk, int(ct.max()))) for v in vmax)
-        rc = lib.h2o_pair_hist(_ptr(bd.codes_col), bd.code_bytes, bd.codes_col.stride(0), _ptr(ridx), _ptr(va),
-                               _ptr(vb), _ptr(items), m * k, _ptr(pfeat), Bs, mode, 1 if posv else 0, s0, s1,
-                               _ptr(Hp), _ptr(pwyy), _stream())
+        fn = lib.h2o_pair_hist4 if kp > 1 else lib.h2o_pair_hist
+        if kp > 1 and not getattr(lib, "_typed_pair4", False):
+            lib.h2o_pair_hist4.argtypes = lib.h2o_pair_hist.argtypes
+            lib._typed_pair4 = True
+        rc = fn(_ptr(bd.codes_col), bd.code_bytes, bd.codes_col.stride(0), _ptr(ridx), _ptr(va), _ptr(vb),
+                _ptr(items), n_items, _ptr(pfeat), Bs, mode, 1 if posv else 0, s0, s1, _ptr(Hp), _ptr(pwyy),
+                _stream())
         if rc != 0:
             raise RuntimeError(f"h2o_pair_hist failed: {rc}")
     return Hp, (pwyy.view(n, k)[:, 0].contiguous() if want_wyy else None), pfeat

@@ -554,3 +554,35 @@ def test_drf_direct_pairs_same_model(cats, monkeypatch):
         m.train(y="y", training_frame=fr)
         preds.append(m.predict(fr).as_data_frame().values[:, 0])
     np.testing.assert_allclose(preds[0], preds[1], rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("nbins", [255, 1000])
+@pytest.mark.parametrize("weights", [False, True])
+def test_pair_hist_dev_grouped_matches_reference(nbins, weights, monkeypatch):
+    """Device-pair histograms with 4 pairs of a node per workgroup
+    (pair_hist_multi_kernel, incl. a partial group and multi-item nodes) equal
+    the one-pair-per-workgroup kernel and the index_add reference."""
+    _need_gpu()
+    from h2o3_amd.ops import tree_ops
+    bd, _ = _binned(nbins=nbins)
+    n = bd.nrows_local
+    g = torch.Generator(device="cuda").manual_seed(5)
+    ridx = torch.randperm(n, generator=g, device="cuda").to(torch.int32)
+    va = torch.randn(n, generator=g, device="cuda")
+    vb = torch.rand(n, generator=g, device="cuda") if weights else None
+    if not weights:
+        va[torch.rand(n, generator=g, device="cuda") < 0.1] = float("nan")
+    st, ct = [0, 3000, 3100, 9000], [3000, 100, 5900, 11000]
+    sel = torch.stack([torch.randperm(bd.F, generator=g, device="cuda")[:6].sort().values for _ in range(4)])
+    vmax = tree_ops.channel_max(va, vb, 0)
+    out = {}
+    for kp in (1, 4):
+        monkeypatch.setattr(tree_ops, "_PAIR_KP", kp)
+        out[kp] = tree_ops.pair_hist_dev(bd, ridx, va, vb, 0, st, ct, sel, vmax, chunk=2048)
+    torch.testing.assert_close(out[4][0], out[1][0], rtol=1e-12, atol=1e-9)
+    torch.testing.assert_close(out[4][1], out[1][1], rtol=1e-12, atol=1e-9)
+    pn = np.repeat(np.arange(4), 6)
+    pf = sel.cpu().numpy().reshape(-1)
+    Hr, wr = tree_ops.pair_hist(bd, ridx, va, vb, 0, st, ct, pn, pf, want_wyy=True, use_native=False)
+    torch.testing.assert_close(out[4][0], Hr, rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(out[4][1], wr, rtol=1e-5, atol=1e-3)
