@@ -501,6 +501,71 @@ class H2OMojoModel:
         self.pca_evecs = np.frombuffer(raw, dtype=">f8", count=size * self.pca_k).astype(np.float64) \
             .reshape(size, self.pca_k)
 
+    def _load_xgboost(self):
+        """XGBoostMojoReader.java:14: one-hot layout keys + the native booster
+        blob (mojo/xgb_booster.py); cats come first in the column order."""
+        from .xgb_booster import Booster
+        self.xgb_nums = int(self.kv("nums", 0))
+        self.xgb_cats = int(self.kv("cats", 0))
+        self.xgb_cat_offsets = np.asarray(self.kv("cat_offsets", [0]), dtype=np.int64)
+        self.xgb_use_all = bool(self.kv("use_all_factor_levels", True))
+        self.xgb_sparse = bool(self.kv("sparse", False))
+        if bool(self.kv("has_offset", False)):
+            raise NotImplementedError("XGBoost MOJOs trained with an offset column are not supported")
+        self.booster = Booster.parse(self.be.read("boosterBytes"))
+        if self.be.exists("auxNodeWeights"):
+            self._xgb_aux_weights(self.be.read("auxNodeWeights"))
+        self.calib_beta = None
+        if self.info.get("calib_method") is not None:
+            if self.info["calib_method"] != "platt":
+                raise ValueError(f"unknown calibration method {self.info['calib_method']}")
+            self.calib_beta = list(self.kv("calib_glm_beta", []))
+
+    def _xgb_aux_weights(self, raw):
+        """AuxNodeWeightsHelper.java: int32 tree count, then per tree an int32
+        node count and that many f64 node weights (big endian), replacing the
+        booster's hessian sums (weighted training)."""
+        p = 0
+        nt = struct.unpack_from("<i", raw, p)[0]
+        p += 4
+        for t in range(nt):
+            nn = struct.unpack_from("<i", raw, p)[0]
+            p += 4
+            w = np.frombuffer(raw, dtype="<f8", count=nn, offset=p)
+            p += 8 * nn
+            if t < len(self.booster.trees):
+                self.booster.trees[t][1]["sum_hess"][:nn] = w
+
+    def xgb_features(self, X: np.ndarray) -> np.ndarray:
+        """Rows in MOJO column order -> the booster's f32 feature matrix
+        (OneHotEncoderFactory.java: one indicator per level plus an NA level
+        per categorical, then the numerics; sparse models treat 0 and
+        not-hot as missing)."""
+        n = X.shape[0]
+        offs = self.xgb_cat_offsets
+        ncat_feat = int(offs[self.xgb_cats]) if self.xgb_cats else 0
+        not_hot = np.float32(np.nan) if self.xgb_sparse else np.float32(0.0)
+        F = np.full((n, ncat_feat + self.xgb_nums), not_hot, dtype=np.float32)
+        rows = np.arange(n)
+        for c in range(self.xgb_cats):
+            v = X[:, c]
+            hi = offs[c + 1] - 1
+            nan = np.isnan(v)
+            iv = np.where(nan, 0, v).astype(np.int64)
+            if self.xgb_use_all:
+                hot = iv + offs[c]
+            else:
+                hot = np.where(iv != 0, iv - 1 + offs[c], -1)
+            hot = np.where(hot >= offs[c + 1], hi, hot)
+            hot = np.where(nan, hi, hot)
+            ok = hot >= 0
+            F[rows[ok], hot[ok]] = 1.0
+        num = X[:, self.xgb_cats:self.xgb_cats + self.xgb_nums].astype(np.float32)
+        if self.xgb_sparse:
+            num = np.where(num == 0, np.float32(np.nan), num)
+        F[:, ncat_feat:] = num
+        return F
+
     def transform(self, word):
         """Word2Vec embedding of one word (None if out of vocabulary)."""
         v = self.embeddings.get(word)
@@ -632,6 +697,22 @@ class H2OMojoModel:
         else:
             preds[:, 0] = self._link_inv(self.link, preds[:, 0] + self.init_f)
             return preds
+        return self._calibrate(self._label(preds))
+
+    def _score_xgboost(self, X):
+        """XGBoostMojoModel.toPreds: binomial p1 = booster output, p0 = 1 - p1;
+        multinomial class probabilities; regression the transformed margin."""
+        out = self.booster.predict(self.xgb_features(X))
+        K = self.nclasses
+        if K > 2:
+            preds = np.zeros((X.shape[0], 1 + K))
+            preds[:, 1:] = out[:, :K]
+        elif K == 2:
+            preds = np.zeros((X.shape[0], 3))
+            preds[:, 2] = out[:, 0]
+            preds[:, 1] = 1.0 - out[:, 0]
+        else:
+            return out[:, :1].astype(np.float64)
         return self._calibrate(self._label(preds))
 
     def _score_drf(self, X):

@@ -1,8 +1,8 @@
 """MOJO export in the reference's h2o-genmodel layout.
 
-`build_h2o_mojo(model)` writes GBM, DRF, GLM, K-Means, Isolation Forest,
-Extended Isolation Forest, Deep Learning, Word2Vec and Stacked Ensemble
-models as the reference's
+`build_h2o_mojo(model)` writes GBM, DRF, XGBoost, GLM, K-Means, Isolation
+Forest, Extended Isolation Forest, Deep Learning, Word2Vec, PCA and Stacked
+Ensemble models as the reference's
 MOJO zip -- model.ini ([info] / [columns] / [domains]), domains/dNNN.txt and,
 for trees, the compressed tree byte streams trees/tCC_GGG.bin with their
 _aux.bin node records -- so the reference's Java scorer (h2o-genmodel
@@ -19,6 +19,8 @@ Format parity (behaviour studied, not translated):
   hex/genmodel/algos/kmeans/KMeansMojoReader.java, isofor/IsolationForestMojoReader.java,
   isoforextended/ExtendedIsolationForestMojoReader.java, deeplearning/DeeplearningMojoReader.java,
   word2vec/Word2VecMojoReader.java, ensemble/StackedEnsembleMojoReader.java
+  h2o-genmodel-extensions/xgboost: XGBoostMojoReader.java, OneHotEncoderFactory.java (one-hot feature
+                                             space + native booster blob, mojo/xgb_booster.py)
 """
 from __future__ import annotations
 
@@ -265,6 +267,141 @@ def _drf(model, z):
         # the reference's single binomial DRF tree scores P(class 0)
         return (lambda v: 1.0 - v) if single else None
     _tree_model(model, z, "drf", "Distributed Random Forest", extra, leaf_maps)
+
+
+# ---------------------------------------------------------------- XGBoost
+_XGB_OBJ = {"bernoulli": "binary:logistic", "multinomial": "multi:softprob", "gaussian": "reg:squarederror",
+            "poisson": "count:poisson", "gamma": "reg:gamma", "tweedie": "reg:tweedie"}
+_XGB_MAX_NODES = 1 << 22
+
+
+def _xgb_tree(tree, col_feat, cat_base, cat_card, leaf_add=0.0):
+    """Our Tree -> XGBoost node / stat arrays over the one-hot feature space.
+
+    Numeric splits map 1:1 (x < thr left, NA -> default direction).  A
+    categorical split on column c (level mask going left, NA / unseen levels
+    by na_left) becomes a chain of indicator tests over the smaller side S of
+    the split: each chain node tests one level of S (hot = 1 >= 0.5 goes
+    right, into a copy of S's subtree), the last chain node's left child is
+    the other side's subtree.  Singleton sides (one-hot style splits) need no
+    copies."""
+    from .xgb_booster import nodes_from_lists, stats_from_lists
+    parent, cleft, cright, feat, dleft, info = [], [], [], [], [], []
+    loss, hess, bw = [], [], []
+
+    def new(par, is_left, i):
+        nid = len(cleft)
+        if nid >= _XGB_MAX_NODES:
+            raise NotImplementedError("categorical splits expand this tree beyond the XGBoost MOJO node limit")
+        parent.append(-1 if par < 0 else (par | ((1 << 31) if is_left else 0)))
+        cleft.append(-1); cright.append(-1); feat.append(0); dleft.append(0); info.append(0.0)
+        loss.append(float(tree.gain[i]) if tree.left[i] >= 0 else 0.0)
+        hess.append(float(tree.weight[i])); bw.append(float(tree.value[i]))
+        return nid
+
+    def emit(i, par, is_left):
+        if tree.left[i] >= 0 and tree.is_cat[i]:
+            card = cat_card[int(tree.feat[i])]
+            m = np.asarray(tree.cat_left[i]).astype(bool)
+            goes_left = np.array([bool(m[v]) if v < len(m) else bool(tree.na_left[i]) for v in range(card)] +
+                                 [bool(tree.na_left[i])])
+            lv, rv = np.flatnonzero(goes_left), np.flatnonzero(~goes_left)
+            if len(lv) == 0 or len(rv) == 0:    # degenerate: every level on one side
+                return emit(int(tree.left[i]) if len(rv) == 0 else int(tree.right[i]), par, is_left)
+        nid = new(par, is_left, i)
+        if tree.left[i] < 0:
+            info[nid] = float(tree.value[i]) + leaf_add
+            return nid
+        f = int(tree.feat[i])
+        l, r = int(tree.left[i]), int(tree.right[i])
+        if not tree.is_cat[i]:
+            feat[nid] = col_feat[f]
+            dleft[nid] = 1 if tree.na_left[i] else 0
+            info[nid] = float(np.float32(tree.thr[i]))
+            cleft[nid] = emit(l, nid, True)
+            cright[nid] = emit(r, nid, False)
+            return nid
+        s_levels, s_child, o_child = (lv, l, r) if len(lv) <= len(rv) else (rv, r, l)
+        cur = nid
+        for k, v in enumerate(s_levels):
+            feat[cur] = cat_base[f] + int(v)
+            dleft[cur] = 1
+            info[cur] = 0.5
+            cright[cur] = emit(s_child, cur, False)
+            if k + 1 < len(s_levels):
+                nxt = new(cur, True, i)
+                cleft[cur] = nxt
+                cur = nxt
+            else:
+                cleft[cur] = emit(o_child, cur, True)
+        return nid
+
+    emit(0, -1, True)
+    return (nodes_from_lists(parent, cleft, cright, feat, dleft, info), stats_from_lists(loss, hess, bw))
+
+
+def _xgboost(model, z):
+    """XGBoostMojoWriter layout: model.ini (nums / cats / cat_offsets / sparse
+    ...), feature_map and the native booster blob (mojo/xgb_booster.py).
+    Columns are written categoricals first, as the reference's one-hot
+    DataInfo orders them; each categorical contributes one indicator per
+    level plus an NA indicator."""
+    from .xgb_booster import Booster, margin_to_prob
+    spec = model._spec
+    x = list(spec.x)
+    xd = getattr(model, "_x_domains", {}) or {}
+    cats = [c for c in x if xd.get(c) is not None]
+    nums = [c for c in x if xd.get(c) is None]
+    offs = [0]
+    for c in cats:
+        offs.append(offs[-1] + len(xd[c]) + 1)
+    col_feat, cat_base, cat_card = {}, {}, {}
+    for j, c in enumerate(x):
+        if c in xd and xd[c] is not None:
+            ci = cats.index(c)
+            cat_base[j], cat_card[j] = offs[ci], len(xd[c])
+        else:
+            col_feat[j] = offs[-1] + nums.index(c)
+    obj = _XGB_OBJ.get(model._dist.family)
+    if obj is None:
+        raise NotImplementedError(f"XGBoost MOJO export: no XGBoost objective for distribution {model._dist.family}")
+    K = model._n_tree_classes()
+    init_f = [float(v) for v in model._init_f]
+    b = Booster()
+    b.name_obj, b.name_gbm = obj, "gbtree"
+    b.num_feature = offs[-1] + len(nums)
+    b.major_version, b.minor_version = 1, 6
+    if K > 1:
+        b.num_class, b.num_output_group = K, K
+        b.base_score = 0.0                        # identity ProbToMargin; class offsets folded into tree 0
+    else:
+        b.num_class, b.num_output_group = 0, 1
+        b.base_score = margin_to_prob(obj, init_f[0])
+    for t, tree in enumerate(model._forest.trees):
+        k = int(model._forest.tclass[t])
+        add = init_f[k] if (K > 1 and t // K == 0) else 0.0
+        b.trees.append(_xgb_tree(tree, col_feat, cat_base, cat_card, add))
+        b.tree_info.append(k if K > 1 else 0)
+    fmap = []
+    for c in cats:
+        for lev in xd[c]:
+            fmap.append(f"{len(fmap)} {c}.{lev} i")
+        fmap.append(f"{len(fmap)} {c}.missing(NA) i")
+    for c in nums:
+        fmap.append(f"{len(fmap)} {c} q")
+    columns = cats + nums + [spec.y]
+    domains = [list(xd[c]) for c in cats] + [None] * len(nums) + \
+        [list(spec.response_domain) if spec.response_domain else None]
+    cat = "Binomial" if spec.nclasses == 2 else "Multinomial" if spec.nclasses > 2 else "Regression"
+    extra = {"nums": len(nums), "cats": len(cats), "cat_offsets": offs, "use_all_factor_levels": True,
+             "sparse": False, "booster": "gbtree", "ntrees": len(model._forest) // max(K, 1),
+             "use_java_scoring_by_default": True, "has_offset": False}
+    ini, files = _header(model, "xgboost", "XGBoost", cat, columns, len(x), spec.nclasses, domains, "1.10", extra)
+    z.write("model.ini", ini)
+    for k_, v in files.items():
+        z.write(k_, v)
+    z.write("feature_map", "\n".join(fmap) + "\n")
+    z.write("boosterBytes", b.to_bytes())
 
 
 # -------------------------------------------------------------------- GLM
@@ -560,7 +697,7 @@ def _stackedensemble(model, z):
 
 _WRITERS = {"gbm": _gbm, "drf": _drf, "glm": _glm, "kmeans": _kmeans, "isolationforest": _isofor,
             "extendedisolationforest": _eif, "deeplearning": _deeplearning, "word2vec": _word2vec,
-            "stackedensemble": _stackedensemble, "pca": _pca}
+            "stackedensemble": _stackedensemble, "pca": _pca, "xgboost": _xgboost}
 
 
 def _write_algo(model, z):
@@ -574,9 +711,9 @@ def _write_algo(model, z):
 
 
 def build_h2o_mojo(model) -> bytes:
-    """MOJO zip bytes in the reference's layout (GBM, DRF, GLM, K-Means,
-    Isolation Forest, Extended Isolation Forest, Deep Learning, Word2Vec,
-    Stacked Ensemble, PCA)."""
+    """MOJO zip bytes in the reference's layout (GBM, DRF, XGBoost, GLM,
+    K-Means, Isolation Forest, Extended Isolation Forest, Deep Learning,
+    Word2Vec, Stacked Ensemble, PCA)."""
     z = _Zip()
     _write_algo(model, z)
     return z.close()

@@ -208,3 +208,21 @@ def test_pca_h2o_mojo_roundtrip(data, transform, x, tmp_path):
     ours = pca.predict(fr).as_data_frame()
     m, theirs = _roundtrip(pca, df, tmp_path)
     np.testing.assert_allclose(theirs.values, ours.values[:, :3].astype(float), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("y", ["yb", "yr", "ym"])
+def test_xgboost_h2o_mojo_roundtrip(data, y, tmp_path):
+    """XGBoost export in the reference's XGBoost MOJO layout (one-hot feature
+    space + native booster blob): categorical bitset splits become chains of
+    indicator tests, NA levels the extra indicator per column."""
+    from h2o3_amd.estimators import H2OXGBoostEstimator
+    df, fr = data
+    g = H2OXGBoostEstimator(ntrees=6, max_depth=4, seed=1)
+    g.train(x=X, y=y, training_frame=fr)
+    ours = g.predict(fr).as_data_frame()
+    m, theirs = _roundtrip(g, df, tmp_path)
+    assert m.algo == "xgboost"
+    cols = [c for c in ours.columns if c != "predict"] or ["predict"]
+    np.testing.assert_allclose(theirs[cols].values.astype(float), ours[cols].values.astype(float), atol=2e-5)
+    if y != "yr":
+        assert (theirs["predict"].astype(str).values == ours["predict"].astype(str).values).mean() > 0.999

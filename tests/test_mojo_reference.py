@@ -163,3 +163,50 @@ def test_generic_estimator_imports_reference_mojo(tmp_path):
     assert abs(float(out["1"][0]) - 0.1777305) < 1e-5
     m = h2o.import_mojo(R + "algos/pipeline/glm_model.zip")
     assert m._mojo.algo == "glm"
+
+
+# ------------------------------------------------------------------ XGBoost
+XR = "/root/reference/h2o-genmodel-extensions/xgboost/src/test/resources/hex/genmodel/algos/xgboost/"
+PROSTATE = "/root/reference/h2o-py/h2o/h2o_data/prostate.csv"
+
+
+@pytest.mark.skipif(not os.path.isdir(XR) or not os.path.exists(PROSTATE), reason="xgboost fixtures not present")
+def test_xgboost_java_mojo_training_mse():
+    """xgboost_java.zip (50-tree reg:squarederror booster on prostate, AGE
+    response): the MOJO's own modelDetails.json records training MSE
+    3.3232581458216086 and MAE 1.229596690127724 over the 380 rows;
+    XGBoostJavaMojoModelTest.testConvertWithWeights pins the root weight 380."""
+    import pandas as pd
+    from h2o3_amd.mojo import h2o_mojo
+    m = h2o_mojo.load(XR + "xgboost_java.zip")
+    assert m.algo == "xgboost" and m.booster.name_obj == "reg:squarederror" and len(m.booster.trees) == 50
+    assert float(m.booster.trees[0][1]["sum_hess"][0]) == 380.0
+    df = pd.read_csv(PROSTATE)
+    p = m.predict(df)["predict"].values
+    err = p - df["AGE"].values
+    assert abs((err ** 2).mean() - 3.3232581458216086) < 1e-6
+    assert abs(np.abs(err).mean() - 1.229596690127724) < 1e-6
+
+
+@pytest.mark.skipif(not os.path.isdir(XR), reason="xgboost fixtures not present")
+def test_xgboost_multinomial_sparse_mojo():
+    """xgboost.zip: multi:softprob booster over a 246-wide one-hot feature
+    space (31 categoricals, 14 numerics, sparse = true: 0 -> missing).  The
+    booster re-serializes byte-for-byte in length and scores valid class
+    probabilities for rows with unseen / missing levels."""
+    import zipfile
+    import pandas as pd
+    from h2o3_amd.mojo import h2o_mojo
+    from h2o3_amd.mojo.xgb_booster import Booster
+    raw = zipfile.ZipFile(XR + "xgboost.zip").read("boosterBytes")
+    b = Booster.parse(raw)
+    assert (b.num_feature, b.num_class, b.name_obj, len(b.trees)) == (246, 3, "multi:softprob", 15)
+    assert len(b.to_bytes()) == len(raw)
+    m = h2o_mojo.load(XR + "xgboost.zip")
+    assert m.xgb_sparse and m.xgb_cats == 31 and m.xgb_nums == 14
+    p = m.predict(pd.DataFrame([{"race": "Caucasian", "age": "[70-80)", "time_in_hospital": 3,
+                                 "num_medications": 12, "diabetesMed": "Yes"},
+                                {"race": "NotALevel", "number_inpatient": 0}]))
+    probs = p[["<30", ">30", "NO"]].values
+    np.testing.assert_allclose(probs.sum(1), 1.0, atol=1e-9)
+    assert set(p["predict"]) <= {"<30", ">30", "NO"}
