@@ -536,6 +536,71 @@ class H2OMojoModel:
             if t < len(self.booster.trees):
                 self.booster.trees[t][1]["sum_hess"][:nn] = w
 
+    def _rect(self, title):
+        """ModelMojoReader.readRectangularDoubleArray: <title>_size1/_size2 in
+        model.ini, a big-endian f64 blob."""
+        s1, s2 = int(self.kv(title + "_size1", 0)), int(self.kv(title + "_size2", 0))
+        if s1 * s2 == 0:
+            return np.zeros((s1, s2))
+        return np.frombuffer(self.be.read(title), dtype=">f8", count=s1 * s2).astype(np.float64).reshape(s1, s2)
+
+    def _load_coxph(self):
+        """CoxPHMojoReader.java: coefficients over [expanded cats | nums],
+        per-stratum covariate means (the linear predictor is centred by the
+        row's stratum), strata keys = the strata columns' values, which lead
+        the column order."""
+        self.cox_coef = np.asarray(self.kv("coef", []), dtype=np.float64)
+        self.cox_cats = int(self.kv("cats", 0))
+        self.cox_cat_offsets = np.asarray(self.kv("cat_offsets", [0]), dtype=np.int64)
+        self.cox_use_all = bool(self.kv("use_all_factor_levels", False))
+        mc, mn = self._rect("x_mean_cat"), self._rect("x_mean_num")
+        nstrata = int(self.kv("strata_count", 0))
+        self.cox_strata = {}
+        for i in range(nstrata):
+            key = tuple(int(v) for v in self.kv(f"strata_{i}"))
+            self.cox_strata[key] = i
+        self.cox_strata_len = len(next(iter(self.cox_strata))) if self.cox_strata else 0
+        ns = mc.shape[1] if mc.shape[0] else 0
+        self.cox_lp_base = np.array([mc[s] @ self.cox_coef[:mc.shape[1]] + mn[s] @ self.cox_coef[ns:ns + mn.shape[1]]
+                                     for s in range(max(nstrata, 1))]) if max(mc.shape[0], mn.shape[0]) else np.zeros(1)
+        self.cox_ia = None
+        if self.info.get("interaction_targets") is not None:
+            self.cox_ia = (list(self.kv("interactions_1")), list(self.kv("interactions_2")),
+                           list(self.kv("interaction_targets")))
+
+    def _score_coxph(self, X):
+        """CoxPHMojoModel.score0: categorical coefficients + numeric dot
+        product - the stratum's centring term."""
+        n = X.shape[0]
+        if self.cox_ia is not None:
+            for a, b, t in zip(*self.cox_ia):
+                miss = np.isnan(X[:, t])
+                X[miss, t] = X[miss, a] * X[miss, b]
+        sl = self.cox_strata_len
+        F = X[:, sl:]
+        lp = np.zeros(n)
+        offs = self.cox_cat_offsets
+        low = 0 if self.cox_use_all else 1
+        for c in range(self.cox_cats):
+            v = F[:, c]
+            idx = np.where(np.isnan(v), -1, v).astype(np.int64) - low
+            x = idx + offs[c]
+            ok = (idx >= 0) & (x < offs[c + 1])
+            lp += np.where(ok, self.cox_coef[np.clip(x, 0, len(self.cox_coef) - 1)], 0.0)
+            lp[np.isnan(v)] = np.nan
+        diff = int(offs[self.cox_cats]) - self.cox_cats
+        nnum = len(self.cox_coef) - int(offs[self.cox_cats])
+        if nnum > 0:
+            lp += F[:, self.cox_cats:self.cox_cats + nnum] @ self.cox_coef[diff + self.cox_cats:]
+        if self.cox_strata:
+            keys = X[:, :sl]
+            s = np.array([self.cox_strata.get(tuple(int(v) for v in r), -1) if not np.isnan(r).any() else -1
+                          for r in keys])
+            base = np.where(s >= 0, self.cox_lp_base[np.maximum(s, 0)], np.nan)
+        else:
+            base = self.cox_lp_base[0]
+        return (lp - base).reshape(n, 1)
+
     def xgb_features(self, X: np.ndarray) -> np.ndarray:
         """Rows in MOJO column order -> the booster's f32 feature matrix
         (OneHotEncoderFactory.java: one indicator per level plus an NA level
@@ -1054,6 +1119,8 @@ class H2OMojoModel:
             return pd.DataFrame(preds, columns=["anomaly_score", "mean_length"])
         if self.algo == "pca":
             return pd.DataFrame(preds, columns=[f"PC{i + 1}" for i in range(preds.shape[1])])
+        if self.algo == "coxph":
+            return pd.DataFrame({"lp": preds[:, 0]})
         if self.category == "AutoEncoder":
             return pd.DataFrame(preds, columns=[f"reconstr_{i}" for i in range(preds.shape[1])])
         if self.nclasses > 1 and preds.shape[1] > 1:

@@ -404,6 +404,60 @@ def _xgboost(model, z):
     z.write("boosterBytes", b.to_bytes())
 
 
+# ------------------------------------------------------------------ CoxPH
+def _rect_blob(z, extra, title, a):
+    """AbstractMojoWriter.writeRectangularDoubleArray: sizes in [info], a
+    big-endian f64 blob."""
+    a = np.asarray(a, dtype=np.float64)
+    extra[title + "_size1"] = int(a.shape[0])
+    extra[title + "_size2"] = int(a.shape[1]) if a.ndim > 1 else 0
+    z.write(title, a.astype(">f8").tobytes())
+
+
+def _coxph(model, z):
+    """CoxPHMojoWriter layout: coef over [expanded cats | nums], per-stratum
+    covariate means split into x_mean_cat / x_mean_num, strata keys as the
+    strata columns' level codes; the strata columns lead the column list."""
+    di = model._dinfo
+    if getattr(di, "ia_recipe", None):
+        raise NotImplementedError("CoxPH MOJO export with interaction columns is not implemented")
+    spec = model._spec
+    p = model._parms
+    cats, nums = list(di.cat_cols), list(di.num_cols)
+    sb = list(p.get("stratify_by") or [])
+    sdom = getattr(model, "_strata_domains", {})
+    offs = [0]
+    for c in cats:
+        offs.append(offs[-1] + (len(di.domains[c]) if di.use_all else len(di.domains[c]) - 1))
+    beta = model._beta.detach().cpu().numpy().astype(np.float64)
+    if len(beta) != offs[-1] + len(nums):
+        raise NotImplementedError("CoxPH MOJO export: unexpected coefficient layout")
+    keys = list(model._strata_keys)
+    mc = np.stack([model._means[s].detach().cpu().numpy()[:offs[-1]] for s in keys])
+    mn = np.stack([model._means[s].detach().cpu().numpy()[offs[-1]:] for s in keys])
+    extra = {"coef": list(beta), "cats": len(cats), "cat_offsets": offs, "use_all_factor_levels": bool(di.use_all)}
+    _rect_blob(z, extra, "x_mean_cat", mc)
+    _rect_blob(z, extra, "x_mean_num", mn)
+    extra["strata_count"] = len(keys) if sb else 0
+    if sb:
+        for i, k in enumerate(keys):
+            codes = []
+            k = int(k)
+            for c in reversed(sb):
+                base = len(sdom[c]) + 1 if c in sdom else 1_000_003
+                codes.append(k % base - 1)
+                k //= base
+            extra[f"strata_{i}"] = [float(v) for v in reversed(codes)]
+    columns = sb + cats + nums + [spec.y]
+    domains = [list(sdom[c]) if c in sdom else None for c in sb] + [list(di.domains[c]) for c in cats] + \
+        [None] * len(nums) + [list(spec.response_domain) if spec.response_domain else None]
+    ini, files = _header(model, "coxph", "Cox Proportional Hazards", "CoxPH", columns, len(columns) - 1, 1,
+                         domains, "1.00", extra)
+    z.write("model.ini", ini)
+    for k_, v in files.items():
+        z.write(k_, v)
+
+
 # -------------------------------------------------------------------- GLM
 def _glm(model, z):
     di = model._dinfo
@@ -697,7 +751,8 @@ def _stackedensemble(model, z):
 
 _WRITERS = {"gbm": _gbm, "drf": _drf, "glm": _glm, "kmeans": _kmeans, "isolationforest": _isofor,
             "extendedisolationforest": _eif, "deeplearning": _deeplearning, "word2vec": _word2vec,
-            "stackedensemble": _stackedensemble, "pca": _pca, "xgboost": _xgboost}
+            "stackedensemble": _stackedensemble, "pca": _pca, "xgboost": _xgboost,
+            "coxph": _coxph}
 
 
 def _write_algo(model, z):
@@ -712,7 +767,7 @@ def _write_algo(model, z):
 
 def build_h2o_mojo(model) -> bytes:
     """MOJO zip bytes in the reference's layout (GBM, DRF, XGBoost, GLM,
-    K-Means, Isolation Forest, Extended Isolation Forest, Deep Learning,
+    CoxPH, K-Means, Isolation Forest, Extended Isolation Forest, Deep Learning,
     Word2Vec, Stacked Ensemble, PCA)."""
     z = _Zip()
     _write_algo(model, z)

@@ -71,3 +71,27 @@ def test_coxph_stratified_and_categorical():
     t = m._output["coefficients_table"]
     assert list(t["names"]) == ["g.q", "x1", "x2"]
     assert abs(m.coef()["x1"] - 0.7) < 0.25
+
+
+@pytest.mark.parametrize("use_all", [False, True])
+def test_coxph_h2o_mojo_roundtrip(use_all, tmp_path):
+    """Reference-layout CoxPH MOJO (CoxPHMojoWriter layout: coef, x_mean_cat /
+    x_mean_num blobs, strata_i keys) scored by the reference-layout reader
+    equals the in-platform centred linear predictor."""
+    from h2o3_amd.mojo import h2o_mojo
+    h2o.init()
+    df = _data(500, seed=5)
+    rng = np.random.default_rng(5)
+    df["g"] = rng.choice(["p", "q", "r"], len(df))
+    df["s"] = rng.choice(["s1", "s2", "s3"], len(df))
+    fr = h2o.H2OFrame(df)
+    m = H2OCoxProportionalHazardsEstimator(stop_column="stop", stratify_by=["s"], use_all_factor_levels=use_all)
+    m.train(x=["x1", "x2", "g"], y="event", training_frame=fr)
+    ours = m.predict(fr).as_data_frame()["lp"].values
+    mj = h2o_mojo.load(m.download_mojo(str(tmp_path), format="h2o"))
+    assert mj.algo == "coxph" and mj.cox_strata_len == 1 and len(mj.cox_strata) == 3
+    d32 = df.copy()
+    for c in ("x1", "x2"):
+        d32[c] = d32[c].astype(np.float32).astype(np.float64)
+    theirs = mj.predict(d32)["lp"].values
+    np.testing.assert_allclose(theirs, ours, atol=2e-5)
