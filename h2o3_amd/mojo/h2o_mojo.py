@@ -20,6 +20,9 @@ Parity references (behaviour studied, not translated):
   hex/genmodel/algos/glm/Glm*MojoModel.java    (cat offsets, mean imputation, ordinal / multinomial)
   hex/genmodel/algos/kmeans/KMeansMojoModel.java, GenModel.KMeans_distance
   hex/genmodel/algos/ensemble/StackedEnsembleMojoModel.java (base model remap, logit transform)
+  hex/genmodel/algos/coxph/CoxPHMojoModel.java, svm/SvmMojoModel.java
+  h2o-genmodel-extensions/xgboost XGBoostJavaMojoModel.java, OneHotEncoderFactory.java
+                                               (native booster blob: mojo/xgb_booster.py)
 
 Instead of walking one row at a time through the byte stream (the
 reference's scoreTree), every tree is decoded ONCE into flat node arrays and
@@ -535,6 +538,35 @@ class H2OMojoModel:
             p += 8 * nn
             if t < len(self.booster.trees):
                 self.booster.trees[t][1]["sum_hess"][:nn] = w
+
+    def _load_svm(self):
+        """SvmMojoReader.java (Sparkling Water's linear SVM): weights over the
+        raw feature values, intercept, label threshold, optional mean
+        imputation."""
+        self.svm_mean_imp = bool(self.kv("meanImputation", False))
+        self.svm_means = np.asarray(self.kv("means", []), dtype=np.float64) if self.svm_mean_imp else None
+        self.svm_w = np.asarray(self.kv("weights", []), dtype=np.float64)
+        self.svm_b = float(self.kv("interceptor", 0.0))
+        self.svm_default_thr = float(self.kv("defaultThreshold", 0.0))
+        self.svm_thr = float(self.kv("threshold", 0.0))
+
+    def _score_svm(self, X):
+        """SvmMojoModel.score0: margin = b + w.x; binomial label = margin >
+        threshold, p1 = the margin clamped to the default threshold's side."""
+        P = len(self.svm_w)
+        V = X[:, :P]
+        if self.svm_mean_imp:
+            V = np.where(np.isnan(V), self.svm_means[:P], V)
+        pred = self.svm_b + V @ self.svm_w
+        if self.nclasses == 1:
+            return pred.reshape(-1, 1)
+        out = np.zeros((X.shape[0], 3))
+        pos = pred > self.svm_thr
+        dt = self.svm_default_thr
+        out[:, 2] = np.where(pos, np.where(pred < dt, dt, pred), np.where(pred >= dt, dt - 1, pred))
+        out[:, 1] = np.where(pos, out[:, 2] - 1, out[:, 2] + 1)
+        out[:, 0] = pos.astype(np.float64)
+        return out
 
     def _rect(self, title):
         """ModelMojoReader.readRectangularDoubleArray: <title>_size1/_size2 in

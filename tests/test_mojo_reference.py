@@ -210,3 +210,18 @@ def test_xgboost_multinomial_sparse_mojo():
     probs = p[["<30", ">30", "NO"]].values
     np.testing.assert_allclose(probs.sum(1), 1.0, atol=1e-9)
     assert set(p["predict"]) <= {"<30", ">30", "NO"}
+
+
+def test_svm_mojo():
+    """SvmMojoModelTest.testPredict: all-zero row -> label 1, all-one row ->
+    label 0 (Sparkling Water linear SVM fixture, mean imputation on)."""
+    from h2o3_amd.mojo import h2o_mojo
+    m = h2o_mojo.load(R + "algos/svm")
+    assert m.algo == "svm" and m.nclasses == 2
+    X = np.array([[0.0] * 6 + [np.nan], [1.0] * 6 + [np.nan]])
+    preds = m.score0(X)
+    assert list(preds[:, 0]) == [1.0, 0.0]
+    # NaN features are mean-imputed: equals scoring the means explicitly
+    Xn = np.full((1, 7), np.nan)
+    Xm = np.concatenate([np.asarray(m.svm_means[:6]), [np.nan]]).reshape(1, 7)
+    np.testing.assert_allclose(m.score0(Xn), m.score0(Xm))
