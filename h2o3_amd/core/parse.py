@@ -41,8 +41,8 @@ def _files(path, pattern=None):
             fs = [f for f in fs if re.search(pattern, os.path.basename(f))]
         return fs
     if "://" in str(path):
-        from .persist import resolve
-        return [resolve(path)]
+        from .persist import resolve_all
+        return resolve_all(path)
     g = sorted(glob.glob(path))
     from .persist import decompress
     return [decompress(f) for f in g] if g else [path]
@@ -252,13 +252,18 @@ def _import_arff(fn, dest):
 
 
 def export_file(frame, path, force=False, sep=",", header=True, format="csv"):
-    if os.path.exists(path) and not force:
+    from .persist import is_remote, upload, _tmpfile
+    remote = is_remote(path)
+    if not remote and os.path.exists(path) and not force:
         raise FileExistsError(path)
     df = frame.as_data_frame()
     if cloud.rank() != 0:
         return path
+    out = _tmpfile(os.path.splitext(path)[1]) if remote else path
     if format == "parquet" or path.endswith(".parquet"):
-        df.to_parquet(path)
+        df.to_parquet(out)
     else:
-        df.to_csv(path, sep=sep, header=header, index=False, na_rep="")
+        df.to_csv(out, sep=sep, header=header, index=False, na_rep="")
+    if remote:
+        upload(out, path)      # s3:// gs:// hdfs:// (core/persist.py)
     return path

@@ -1,26 +1,49 @@
-"""Persistence back-ends (where files come from).
+"""Persistence back-ends (where files come from and go to).
 
 Reference: water/persist/{PersistManager, PersistNFS, PersistHTTP,
-PersistS3, PersistHdfs, PersistGcs}.java.  Supported here: local paths and
-file:// URIs, http(s):// (downloaded to a temporary file), and transparent
-decompression of .gz / .bz2 / .zip / .xz inputs before parsing (the
-reference's ZipUtil decompression in ParseDataset).  Object stores (s3://,
-gs://, hdfs://) raise a clear error: this build has no cloud SDKs and no
-egress.
+PersistS3, PersistHdfs, PersistGcs}.java.  Supported here:
+
+* local paths and file:// URIs;
+* http(s):// (downloaded to a temporary file);
+* s3:// (s3a://, s3n://): the S3 REST API with AWS Signature V4 request
+  signing done here (no SDK) -- credentials from AWS_ACCESS_KEY_ID /
+  AWS_SECRET_ACCESS_KEY (/ AWS_SESSION_TOKEN), region from AWS_REGION /
+  AWS_DEFAULT_REGION, a custom endpoint (MinIO, Ceph, ...) from
+  AWS_ENDPOINT_URL / AWS_S3_ENDPOINT (path-style addressing); unsigned when
+  no credentials are set (public buckets).  A key ending in "/" imports every
+  object under that prefix (ListObjectsV2), like the reference's folder import;
+* gs://: the Cloud Storage JSON API (media download / upload), bearer token
+  from GOOGLE_OAUTH_ACCESS_TOKEN, endpoint override STORAGE_EMULATOR_HOST;
+* hdfs:// (maprfs://): the WebHDFS REST API of the name node (op=OPEN /
+  CREATE / LISTSTATUS), port from the URI or H2O3_WEBHDFS_PORT (9870), user
+  from HADOOP_USER_NAME;
+* transparent decompression of .gz / .bz2 / .zip / .xz inputs before parsing
+  (the reference's ZipUtil decompression in ParseDataset).
+
+The object-store clients speak the services' public HTTP protocols with the
+standard library only, so they work wherever the endpoint is reachable;
+tests/test_persist.py drives them against local protocol servers and pins the
+SigV4 signer to AWS's published example.
 """
 from __future__ import annotations
 
 import bz2
+import datetime as _dt
 import gzip
+import hashlib
+import hmac
+import json
 import lzma
 import os
 import shutil
 import tempfile
 import urllib.parse
 import urllib.request
+import xml.etree.ElementTree as ET
 import zipfile
 
 _TMP = []
+_EMPTY_SHA = hashlib.sha256(b"").hexdigest()
 
 
 def _tmpfile(suffix=""):
@@ -30,19 +53,216 @@ def _tmpfile(suffix=""):
     return p
 
 
+def _download(req, suffix="") -> str:
+    out = _tmpfile(suffix)
+    with urllib.request.urlopen(req) as r, open(out, "wb") as f:
+        shutil.copyfileobj(r, f)
+    return out
+
+
+# ------------------------------------------------------------------- S3 / SigV4
+def _sha(b: bytes) -> str:
+    return hashlib.sha256(b).hexdigest()
+
+
+def _hm(key: bytes, msg: str) -> bytes:
+    return hmac.new(key, msg.encode("utf-8"), hashlib.sha256).digest()
+
+
+def sigv4_headers(method: str, url: str, region: str, access_key: str, secret_key: str, headers=None,
+                  payload_hash: str = _EMPTY_SHA, amz_date: str | None = None, session_token: str | None = None,
+                  service: str = "s3") -> dict:
+    """AWS Signature Version 4 (header form): returns the request headers
+    including Authorization.  Canonical request = method, URI-encoded path,
+    sorted query, sorted lower-case headers, signed header list, payload
+    hash; string to sign = algorithm, date, scope, hash of the canonical
+    request; key = HMAC chain over date / region / service / aws4_request."""
+    u = urllib.parse.urlsplit(url)
+    amz_date = amz_date or _dt.datetime.now(_dt.timezone.utc).strftime("%Y%m%dT%H%M%SZ")
+    day = amz_date[:8]
+    h = {k.lower(): str(v).strip() for k, v in (headers or {}).items()}
+    h["host"] = u.netloc
+    h["x-amz-date"] = amz_date
+    h["x-amz-content-sha256"] = payload_hash
+    if session_token:
+        h["x-amz-security-token"] = session_token
+    path = urllib.parse.quote(urllib.parse.unquote(u.path) or "/", safe="/-_.~")
+    q = urllib.parse.parse_qsl(u.query, keep_blank_values=True)
+    cq = "&".join(f"{urllib.parse.quote(k, safe='-_.~')}={urllib.parse.quote(v, safe='-_.~')}"
+                  for k, v in sorted(q))
+    names = sorted(h)
+    canon = "\n".join([method, path, cq, "".join(f"{k}:{h[k]}\n" for k in names), ";".join(names), payload_hash])
+    scope = f"{day}/{region}/{service}/aws4_request"
+    sts = "\n".join(["AWS4-HMAC-SHA256", amz_date, scope, _sha(canon.encode("utf-8"))])
+    key = _hm(_hm(_hm(_hm(("AWS4" + secret_key).encode("utf-8"), day), region), service), "aws4_request")
+    sig = hmac.new(key, sts.encode("utf-8"), hashlib.sha256).hexdigest()
+    h["authorization"] = (f"AWS4-HMAC-SHA256 Credential={access_key}/{scope}, SignedHeaders={';'.join(names)}, "
+                          f"Signature={sig}")
+    return h
+
+
+def _s3_cfg():
+    region = os.environ.get("AWS_REGION") or os.environ.get("AWS_DEFAULT_REGION") or "us-east-1"
+    ep = os.environ.get("AWS_ENDPOINT_URL") or os.environ.get("AWS_S3_ENDPOINT")
+    return region, ep, os.environ.get("AWS_ACCESS_KEY_ID"), os.environ.get("AWS_SECRET_ACCESS_KEY"), \
+        os.environ.get("AWS_SESSION_TOKEN")
+
+
+def _s3_url(bucket, key, query=""):
+    region, ep, *_ = _s3_cfg()
+    k = urllib.parse.quote(key, safe="/-_.~")
+    if ep:
+        base = f"{ep.rstrip('/')}/{bucket}/{k}"          # path-style for custom endpoints
+    else:
+        base = f"https://{bucket}.s3.{region}.amazonaws.com/{k}"
+    return base + ("?" + query if query else "")
+
+
+def _s3_request(method, url, data=None, headers=None):
+    region, _, ak, sk, tok = _s3_cfg()
+    hdrs = dict(headers or {})
+    if ak and sk:
+        hdrs = sigv4_headers(method, url, region, ak, sk, hdrs, _sha(data or b""), session_token=tok)
+    return urllib.request.Request(url, data=data, method=method, headers=hdrs)
+
+
+def _s3_list(bucket, prefix):
+    keys, token = [], None
+    while True:
+        q = {"list-type": "2", "prefix": prefix}
+        if token:
+            q["continuation-token"] = token
+        url = _s3_url(bucket, "", urllib.parse.urlencode(q, quote_via=urllib.parse.quote))
+        with urllib.request.urlopen(_s3_request("GET", url)) as r:
+            root = ET.fromstring(r.read())
+        ns = root.tag.split("}")[0] + "}" if root.tag.startswith("{") else ""
+        keys += [c.findtext(ns + "Key") for c in root.findall(ns + "Contents")]
+        if (root.findtext(ns + "IsTruncated") or "false").lower() != "true":
+            return [k for k in keys if k and not k.endswith("/")]
+        token = root.findtext(ns + "NextContinuationToken")
+
+
+def _s3_get(u) -> list:
+    bucket, key = u.netloc, u.path.lstrip("/")
+    keys = _s3_list(bucket, key) if (not key or key.endswith("/")) else [key]
+    return [decompress(_download(_s3_request("GET", _s3_url(bucket, k)), os.path.splitext(k)[1])) for k in keys]
+
+
+# ------------------------------------------------------------------------ GCS
+def _gcs_base():
+    emu = os.environ.get("STORAGE_EMULATOR_HOST")
+    if emu:
+        return emu if emu.startswith("http") else "http://" + emu
+    return "https://storage.googleapis.com"
+
+
+def _gcs_headers():
+    tok = os.environ.get("GOOGLE_OAUTH_ACCESS_TOKEN")
+    return {"Authorization": f"Bearer {tok}"} if tok else {}
+
+
+def _gcs_get(u) -> list:
+    bucket, obj = u.netloc, u.path.lstrip("/")
+    names = [obj]
+    if not obj or obj.endswith("/"):
+        url = f"{_gcs_base()}/storage/v1/b/{bucket}/o?prefix={urllib.parse.quote(obj, safe='')}"
+        with urllib.request.urlopen(urllib.request.Request(url, headers=_gcs_headers())) as r:
+            names = [it["name"] for it in json.loads(r.read()).get("items", []) if not it["name"].endswith("/")]
+    out = []
+    for n in names:
+        url = f"{_gcs_base()}/storage/v1/b/{bucket}/o/{urllib.parse.quote(n, safe='')}?alt=media"
+        out.append(decompress(_download(urllib.request.Request(url, headers=_gcs_headers()),
+                                        os.path.splitext(n)[1])))
+    return out
+
+
+# ----------------------------------------------------------------------- HDFS
+def _webhdfs_url(u, path, op, extra=""):
+    port = u.port or int(os.environ.get("H2O3_WEBHDFS_PORT", "9870"))
+    user = os.environ.get("HADOOP_USER_NAME")
+    q = f"op={op}" + (f"&user.name={urllib.parse.quote(user)}" if user else "") + extra
+    return f"http://{u.hostname}:{port}/webhdfs/v1{urllib.parse.quote(path, safe='/-_.~')}?{q}"
+
+
+def _hdfs_get(u) -> list:
+    with urllib.request.urlopen(_webhdfs_url(u, u.path, "GETFILESTATUS")) as r:
+        st = json.loads(r.read())["FileStatus"]
+    paths = [u.path]
+    if st.get("type") == "DIRECTORY":
+        with urllib.request.urlopen(_webhdfs_url(u, u.path, "LISTSTATUS")) as r:
+            ents = json.loads(r.read())["FileStatuses"]["FileStatus"]
+        paths = [u.path.rstrip("/") + "/" + e["pathSuffix"] for e in ents if e.get("type") == "FILE"]
+    # OPEN answers with a 307 redirect to a data node; urllib follows it
+    return [decompress(_download(_webhdfs_url(u, p, "OPEN"), os.path.splitext(p)[1])) for p in paths]
+
+
+# -------------------------------------------------------------------- public
+def resolve_all(uri: str) -> list:
+    """Local paths for a URI: one per object (prefix / directory URIs of the
+    object stores expand to every file under them)."""
+    u = urllib.parse.urlparse(uri)
+    if u.scheme in ("s3", "s3a", "s3n"):
+        return _s3_get(u)
+    if u.scheme == "gs":
+        return _gcs_get(u)
+    if u.scheme in ("hdfs", "maprfs", "webhdfs"):
+        return _hdfs_get(u)
+    return [resolve(uri)]
+
+
 def resolve(uri: str) -> str:
     """Local path for a URI (downloading / decompressing as needed)."""
     u = urllib.parse.urlparse(uri)
     if u.scheme in ("http", "https"):
-        out = _tmpfile(os.path.splitext(u.path)[1])
-        with urllib.request.urlopen(uri) as r, open(out, "wb") as f:
-            shutil.copyfileobj(r, f)
-        return decompress(out)
-    if u.scheme in ("s3", "s3a", "s3n", "gs", "hdfs", "maprfs"):
-        raise NotImplementedError(f"{u.scheme}:// persistence is not available in this build (no object-store SDK)")
+        return decompress(_download(uri, os.path.splitext(u.path)[1]))
+    if u.scheme in ("s3", "s3a", "s3n", "gs", "hdfs", "maprfs", "webhdfs"):
+        paths = resolve_all(uri)
+        if len(paths) != 1:
+            raise ValueError(f"{uri} names {len(paths)} objects; import it as a folder")
+        return paths[0]
     if u.scheme == "file":
         uri = u.path
     return decompress(uri)
+
+
+def upload(local_path: str, uri: str) -> None:
+    """Write a local file to an object-store URI (Frame / model export to
+    s3:// gs:// hdfs://, as PersistManager.create does in the reference)."""
+    u = urllib.parse.urlparse(uri)
+    with open(local_path, "rb") as f:
+        data = f.read()
+    if u.scheme in ("s3", "s3a", "s3n"):
+        req = _s3_request("PUT", _s3_url(u.netloc, u.path.lstrip("/")), data=data)
+    elif u.scheme == "gs":
+        url = (f"{_gcs_base()}/upload/storage/v1/b/{u.netloc}/o?uploadType=media&name="
+               f"{urllib.parse.quote(u.path.lstrip('/'), safe='')}")
+        req = urllib.request.Request(url, data=data, method="POST",
+                                     headers={**_gcs_headers(), "Content-Type": "application/octet-stream"})
+    elif u.scheme in ("hdfs", "maprfs", "webhdfs"):
+        # CREATE: the name node redirects to a data node, the data goes there
+        first = urllib.request.Request(_webhdfs_url(u, u.path, "CREATE", "&overwrite=true"), method="PUT")
+        opener = urllib.request.build_opener(_NoRedirect)
+        try:
+            with opener.open(first) as r:
+                loc = r.headers.get("Location")
+        except urllib.error.HTTPError as e:
+            if e.code not in (301, 302, 303, 307, 308):
+                raise
+            loc = e.headers.get("Location")
+        req = urllib.request.Request(loc or first.full_url, data=data, method="PUT")
+    else:
+        raise ValueError(f"not an object-store URI: {uri}")
+    with urllib.request.urlopen(req) as r:
+        r.read()
+
+
+class _NoRedirect(urllib.request.HTTPRedirectHandler):
+    def redirect_request(self, req, fp, code, msg, headers, newurl):
+        return None
+
+
+def is_remote(uri: str) -> bool:
+    return urllib.parse.urlparse(str(uri)).scheme in ("s3", "s3a", "s3n", "gs", "hdfs", "maprfs", "webhdfs")
 
 
 def decompress(path: str) -> str:

@@ -29,6 +29,15 @@ def _metrics_dict(m):
 
 
 def save_model(model, path="", force=False, filename=None):
+    from ..core.persist import is_remote, upload
+    if is_remote(path):
+        # object store: write locally, then upload (PersistManager.create)
+        import tempfile
+        with tempfile.TemporaryDirectory() as td:
+            local = save_model(model, td, force=True, filename=filename)
+            dest = path.rstrip("/") + "/" + os.path.basename(local)
+            upload(local, dest)
+        return dest
     from ..mojo.writer import build_mojo
     os.makedirs(path or ".", exist_ok=True)
     fn = os.path.join(path or ".", filename or model.model_id)
@@ -48,6 +57,9 @@ def save_model(model, path="", force=False, filename=None):
 
 
 def load_model(path):
+    from ..core.persist import is_remote, resolve
+    if is_remote(path):
+        path = resolve(path)
     from . import metrics as mm
     from .generic import H2OGenericEstimator
     from ..core import dkv
