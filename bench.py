@@ -11,7 +11,11 @@ partition, gamma (leaf value) pass and prediction update — nothing skipped.
 The total data size is fixed (strong scaling): with N GPUs every rank holds
 100M/N rows and histograms are reduce-scattered over RCCL.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--rows R] [--algo gbm|glm|drf]
+The GLM half of the headline metric (GLM binomial IRLSM iterations/s on the
+same frame) is measured after the GBM steps and reported as extra keys
+(glm_iters_per_sec, glm_ms_per_iter) of the same JSON line; --no-glm skips it.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--rows R] [--algo gbm|glm|drf] [--no-glm]
        [--cols C] [--cat-cols K --cat-card L]   (DRF config: --algo drf --rows 50000000 --cols 500 --cat-cols 100)
 """
 import argparse
@@ -78,6 +82,9 @@ def main():
     ap.add_argument("--cat-card", type=int, default=1000, help="cardinality of the categorical columns")
     ap.add_argument("--histogram-type", default="QuantilesGlobal")
     ap.add_argument("--nbins", type=int, default=255)
+    ap.add_argument("--no-glm", action="store_true",
+                    help="--algo gbm: skip the companion GLM measurement (the headline metric is GBM trees/s + "
+                         "GLM iters/s on the same 100M x 100 frame; the GLM figure is reported as extra keys)")
     args = ap.parse_args()
 
     import torch
@@ -106,7 +113,7 @@ def main():
         step = drv.step
         metric = "gbm_trees_per_sec"
         unit = "trees/s"
-        model = "GBM binomial 100Mx100 ntrees=500 max_depth=8"
+        model = f"GBM binomial {args.rows / 1e6:g}Mx{F} ntrees=500 max_depth={args.max_depth}"
     elif args.algo == "drf":
         from h2o3_amd.models.tree.drf import DRFDriver, H2ORandomForestEstimator
         est = H2ORandomForestEstimator(ntrees=1000, max_depth=args.max_depth if args.max_depth != 8 else 20,
@@ -221,6 +228,30 @@ def main():
         # final coefficient step
         extra["train_deviance_per_row"] = round(float(drv.last_dev) / float(drv.wsum), 6)
         extra["iters"] = int(drv.iter)
+    if args.algo == "gbm" and not args.no_glm:
+        # companion half of the headline metric: GLM binomial IRLSM iterations/s
+        # on the SAME frame, timed separately with the same barrier + sync
+        # discipline (the GBM value / ms_per_step above are not affected)
+        from h2o3_amd.models.glm.glm import GLMDriver, H2OGeneralizedLinearEstimator
+        gest = H2OGeneralizedLinearEstimator(family="binomial", solver="IRLSM", lambda_=0.0)
+        gspec = TrainSpec(fr, names, "y")
+        gest._spec = gspec
+        gdrv = GLMDriver(gest, gspec)
+        for _ in range(args.warmup):
+            gdrv.step()
+        sync()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            gdrv.step()
+        sync()
+        gel = time.perf_counter() - t1
+        if world > 1:
+            t = torch.tensor([gel], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            gel = float(t.item())
+        extra["glm_iters_per_sec"] = round(args.steps / gel, 4)
+        extra["glm_ms_per_iter"] = round(1000 * gel / args.steps, 3)
+        extra["glm_model"] = f"GLM binomial IRLSM {args.rows / 1e6:g}Mx{F} (same frame, {args.steps} timed iterations)"
     from h2o3_amd.utils import timer
     if timer.ENABLED and rank == 0:
         print("phases(ms,count):", timer.report(), file=sys.stderr)
