@@ -88,6 +88,49 @@ class TrainSpec:
         return None
 
 
+class ScoreSchedule:
+    """When an iterative tree builder scores (SharedTree.java:792
+    doScoringAndSaveModel): every score_tree_interval trees when set, always
+    with score_each_iteration and at the final tree; otherwise time-based --
+    every iteration during the first initial_score_interval ms (4 s), then at
+    most every score_interval ms (4 s) and only while scoring stays under a
+    10% duty cycle.  time_based=False keeps scoring to the final iteration
+    (no early stopping asked for: nothing consumes the intermediate history)."""
+
+    def __init__(self, parms, time_based=True):
+        self.interval = int(parms.get("score_tree_interval") or 0)
+        self.each = bool(parms.get("score_each_iteration"))
+        self.init_ms = float(parms.get("initial_score_interval") or 4000)
+        self.score_ms = float(parms.get("score_interval") or 4000)
+        self.time_based = time_based
+        self.first = None
+        self.last_start = 0.0
+        self.last_end = 0.0
+
+    def due(self, it, final=False):
+        import time as _t
+        now = _t.time() * 1000.0
+        if self.first is None:
+            self.first = now
+        if self.each or final:
+            return True
+        if self.interval > 0:
+            return it % self.interval == 0
+        if not self.time_based:
+            return False
+        since = now - self.last_start
+        return (now - self.first < self.init_ms) or \
+            (since > self.score_ms and (self.last_end - self.last_start) / max(since, 1e-9) < 0.1)
+
+    def started(self):
+        import time as _t
+        self.last_start = _t.time() * 1000.0
+
+    def ended(self):
+        import time as _t
+        self.last_end = _t.time() * 1000.0
+
+
 class ScoreKeeper:
     """Early stopping on a moving average (hex/ScoreKeeper.java:stopEarly)."""
 

@@ -23,7 +23,7 @@ import torch
 from ...parallel import cloud
 from ...parallel import collectives as coll
 from .. import metrics as mm
-from ..base import ScoreKeeper, _LESS_IS_BETTER
+from ..base import ScoreKeeper, ScoreSchedule, _LESS_IS_BETTER
 from .engine import GrowParams, TreeGrower
 from .shared import Forest, SharedTreeEstimator
 
@@ -56,14 +56,16 @@ class H2ORandomForestEstimator(SharedTreeEstimator):
         stop_rounds = int(p.get("stopping_rounds") or 0)
         metric_name = self._stopping_metric(spec)
         history = []
+        sched = ScoreSchedule(p, time_based=stop_rounds > 0)
         for t in range(ntrees):
             drv.step()
-            score_now = (interval and (t + 1) % interval == 0) or (stop_rounds and not interval) or t + 1 == ntrees
-            if score_now:
+            if sched.due(t + 1, final=t + 1 == ntrees):
                 entry = {"number_of_trees": t + 1}
-                if stop_rounds or interval:
+                if stop_rounds or interval or sched.each:
+                    sched.started()
                     self._forest = drv.forest
                     self._score_entry(entry, spec, drv.oob_sum, drv.oob_cnt)
+                    sched.ended()
                 self._scoring_history.append(entry)
                 if stop_rounds:
                     key = ("validation_" if spec.valid is not None else "training_") + \

@@ -25,7 +25,7 @@ import torch
 from ...core.frame import H2OFrame
 from ...parallel import cloud
 from ...parallel import collectives as coll
-from ..base import ScoreKeeper, _LESS_IS_BETTER
+from ..base import ScoreKeeper, ScoreSchedule, _LESS_IS_BETTER
 from ..distributions import get_distribution
 from .engine import GrowParams, TreeGrower
 from ...ops import tree_ops
@@ -411,12 +411,13 @@ class H2OGradientBoostingEstimator(SharedTreeEstimator):
         history = []
         max_rt = float(p.get("max_runtime_secs") or 0)
         self._scoring_history = []
+        sched = ScoreSchedule(p, time_based=stop_rounds > 0)
         while drv.iter < ntrees:
             drv.step()
-            score_now = (interval > 0 and drv.iter % interval == 0) or (stop_rounds > 0 and interval == 0) or \
-                p.get("score_each_iteration") or drv.iter == ntrees
-            if score_now:
+            if sched.due(drv.iter, final=drv.iter == ntrees):
+                sched.started()
                 entry = self._score_iteration(drv, spec)
+                sched.ended()
                 self._scoring_history.append(entry)
                 if stop_rounds > 0:
                     suffix = "custom" if metric_name.startswith("custom") else metric_name

@@ -22,7 +22,7 @@ from ...parallel import collectives as coll
 from ...ops import tree_ops
 from ..distributions import get_distribution
 from .engine import GrowParams, TreeGrower
-from ..base import ScoreKeeper, _LESS_IS_BETTER
+from ..base import ScoreKeeper, ScoreSchedule, _LESS_IS_BETTER
 from .shared import Forest, SharedTreeEstimator
 
 XGB_DEFAULTS = dict(ntrees=50, max_depth=6, min_rows=1.0, min_child_weight=1.0, learn_rate=0.3, eta=0.3,
@@ -131,6 +131,7 @@ class H2OXGBoostEstimator(SharedTreeEstimator):
         self._scoring_history = []
         max_rt = float(p.get("max_runtime_secs") or 0)
         t0 = time.time()
+        sched = ScoreSchedule(p, time_based=stop_rounds > 0)
         for it in range(ntrees):
             wt = base_w
             if sr < 1.0:
@@ -193,10 +194,12 @@ class H2OXGBoostEstimator(SharedTreeEstimator):
             else:
                 f = f + torch.stack(deltas, 1)
             n_it = it + 1
-            if (interval and n_it % interval == 0) or (stop_rounds and not interval) or n_it == ntrees:
+            if sched.due(n_it, final=n_it == ntrees):
                 entry = {"number_of_trees": n_it}
                 self._forest = forest
+                sched.started()
                 self._score_entry(entry, spec, f)
+                sched.ended()
                 self._scoring_history.append(entry)
                 if stop_rounds:
                     key = ("validation_" if spec.valid is not None else "training_") + \
