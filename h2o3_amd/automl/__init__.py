@@ -51,6 +51,18 @@ _EXPLOIT_STEPS = {"GBM": ["lr_annealing"], "XGBoost": ["lr_search"]}
 _MAX_TREES = 10000  # reference: ntrees=10000, early stopping decides
 
 
+def _work(algo, step):
+    """(priority group, weight) of a plan step (ModelingStep.java:505 / 575:
+    default models weigh 10, grids 30; WorkAllocations.remainingWorkRatio)."""
+    if algo == "StackedEnsemble":
+        return "se", 10
+    if step.startswith("grid"):
+        return "grid", 30
+    if step in ("lr_annealing", "lr_search"):
+        return "exploit", 10
+    return "default", 10
+
+
 def _estimators():
     from .. import estimators as E
     return {"XGBoost": E.H2OXGBoostEstimator, "GLM": E.H2OGeneralizedLinearEstimator,
@@ -210,7 +222,23 @@ class H2OAutoML:
             return False
         if self.max_runtime_secs and time.time() - self._t0 > self.max_runtime_secs:
             return False
+        dl = getattr(self, "_step_deadline", None)
+        if dl is not None and time.time() > dl:
+            return False       # this grid step's share of the budget is spent
         return True
+
+    def _assign_step_time(self, item, pending):
+        """Time share of one step (ModelingStep.java:550): remaining budget x
+        its weight / the remaining weight of the steps in its priority group
+        plus the Stacked Ensembles, so one slow early model (e.g. a DRF
+        running to early stopping) cannot eat the whole budget."""
+        self._step_deadline = None
+        if not self.max_runtime_secs or item[0] == "StackedEnsemble":
+            return
+        left = self.max_runtime_secs - (time.time() - self._t0)
+        grp, w = _work(*item)
+        rem = sum(_work(*it)[1] for it in pending if _work(*it)[0] in (grp, "se"))
+        self._step_deadline = time.time() + max(1.0, left * w / max(rem, w))
 
     def _seed(self):
         return self.seed if self.seed not in (None, -1) else 42
@@ -234,6 +262,9 @@ class H2OAutoML:
         rt = self.max_runtime_secs_per_model
         if self.max_runtime_secs:
             left = max(1.0, self.max_runtime_secs - (time.time() - self._t0))
+            dl = getattr(self, "_step_deadline", None)
+            if dl is not None:
+                left = min(left, max(1.0, dl - time.time()))
             rt = min(rt, left) if rt else left
         if rt:
             c["max_runtime_secs"] = rt
@@ -333,8 +364,12 @@ class H2OAutoML:
             return
         t = time.time()
         try:
+            # StackedEnsembleStepsProvider.java:146: the metalearner is
+            # cross-validated with the AutoML nfolds, so the ensemble carries
+            # cross-validation metrics comparable with the base models'
+            se_kw = {"metalearner_nfolds": self.nfolds} if (self.nfolds and data["blending"] is None) else {}
             se = H2OStackedEnsembleEstimator(base_models=base, model_id=f"{name}_AutoML_{self.project_name}",
-                                             seed=self._seed())
+                                             seed=self._seed(), **se_kw)
             se.train(x=data["x"], y=data["y"], training_frame=data["train"], validation_frame=data["valid"],
                      blending_frame=data["blending"])
         except Exception as e:
@@ -445,15 +480,18 @@ class H2OAutoML:
         if self.exploitation_ratio == 0:
             exploit = []
         self._write_state(args)
-        for algo, step in explore + exploit + ses:
+        order = [s for s in explore + exploit + ses if self._allowed(s[0])]
+        for i, (algo, step) in enumerate(order):
             tag = f"{algo}:{step}"
             if tag in self._done_steps:
                 continue
+            self._step_deadline = None
             if algo != "StackedEnsemble" and not self._budget_left():
                 continue     # out of time: skip the remaining base-model steps, still build the ensembles
-            if not self._allowed(algo):
-                continue
+            self._assign_step_time((algo, step), [it for it in order[i:]
+                                                  if f"{it[0]}:{it[1]}" not in self._done_steps])
             self._run_step(algo, step, data, classification)
+            self._step_deadline = None
             self._done_steps.append(tag)
             self._write_state(args)
         self._leaderboard = Leaderboard(self.models, sort_metric=self.sort_metric, frame=leaderboard_frame)

@@ -108,6 +108,12 @@ class H2OStackedEnsembleEstimator(H2OEstimator):
             meta = cls(**mp)
         meta.train(x=names, y=spec.y, training_frame=lvl1)
         self._meta = meta
+        if getattr(meta, "_cross_validation_metrics", None) is not None:
+            # StackedEnsembleModel.java:371: the ensemble's cross-validation
+            # metrics are the metalearner's, cross-validated on the level-one
+            # frame of base-model holdout predictions (honest, unlike training
+            # metrics of base models refit on all rows)
+            self._cross_validation_metrics = meta._cross_validation_metrics
         if p.get("keep_levelone_frame"):
             self._output["levelone_frame"] = lvl1
         self._output["model_summary"] = {"base_models": [m.model_id for m in base], "metalearner": meta.algo}

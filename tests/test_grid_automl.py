@@ -59,3 +59,45 @@ def test_automl_small():
     assert aml.leader is not None
     assert "auc" in lb.columns
     assert aml.leader.predict(fr).nrows == fr.nrows
+
+
+def test_automl_stacked_ensemble_metrics_are_cross_validated():
+    """StackedEnsembleModel.java:371 / StackedEnsembleStepsProvider.java:146:
+    in AutoML the metalearner is cross-validated with the AutoML nfolds and the
+    ensemble's leaderboard metrics are those CV metrics.  On a pure-noise
+    response no model -- ensembles included -- may look better than chance
+    (training metrics of base models refit on all rows would)."""
+    import numpy as np
+    import pandas as pd
+    import h2o3_amd as h2o
+    from h2o3_amd.automl import H2OAutoML
+    h2o.init(verbose=False)
+    rng = np.random.RandomState(0)
+    n = 3000
+    df = pd.DataFrame(rng.randn(n, 6), columns=list("abcdef"))
+    df["y"] = np.where(rng.rand(n) < 0.5, "yes", "no")
+    aml = H2OAutoML(max_models=3, nfolds=3, seed=1, verbosity=None, include_algos=["GLM", "XGBoost",
+                                                                                   "StackedEnsemble"])
+    aml.train(y="y", training_frame=h2o.H2OFrame(df))
+    lb = aml.leaderboard.as_data_frame()
+    se = lb[lb["model_id"].str.startswith("StackedEnsemble")]
+    assert len(se) >= 1
+    assert (se["auc"] < 0.56).all()
+    for m in aml.models:
+        if m.algo == "stackedensemble":
+            assert m._cross_validation_metrics is not None
+
+
+def test_automl_time_allocation_by_work_weight():
+    """ModelingStep.java:550: a step gets remaining budget x weight / remaining
+    weight of its priority group + the Stacked Ensembles."""
+    from h2o3_amd.automl import H2OAutoML
+    aml = H2OAutoML(max_runtime_secs=100, seed=1)
+    import time
+    aml._t0 = time.time()
+    pending = [("DRF", "def_1"), ("GBM", "def_1"), ("XGBoost", "grid_1"), ("StackedEnsemble", "all")]
+    aml._assign_step_time(pending[0], pending)
+    share = aml._step_deadline - time.time()
+    assert 30 < share < 34          # 100 s x 10 / (10 + 10 + 10 SE)
+    aml._assign_step_time(pending[2], pending[2:])
+    assert 70 < aml._step_deadline - time.time() < 76   # grid: 30 / (30 + 10)
