@@ -1409,7 +1409,7 @@ class TreeGrower:
         nid = None
         if want_nid:
             with phase("tree.nid"):
-                nid = tree_ops.fill_nid(ridx, lids, leaf_st.tolist(), leaf_ct.tolist(), N)
+                nid = tree_ops.fill_nid(ridx, np.arange(len(leaves), dtype=np.int64), leaf_st, leaf_ct, N)
         self.ridx, self.ridx2 = ridx, ridx2
         self._pay = [pa, pb, pa2, pb2]
         self.last_segs = (lids, leaf_st.tolist(), leaf_ct.tolist())

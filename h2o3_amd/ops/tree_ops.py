@@ -819,6 +819,10 @@ def hist_sibling(Hb, H_prev, build_slots, der_slots, par_slots, n_front, clamp_m
 def fill_nid(ridx, leaf_ids, starts, counts, nrows, use_native=None):
     """Per-row leaf index from leaf segments."""
     dev = ridx.device
+    if dev.type == "cuda" and use_native is None:
+        nid = _fill_nid_tiled(ridx, leaf_ids, starts, counts, nrows)
+        if nid is not None:
+            return nid
     nid = torch.full((nrows,), -1, dtype=torch.int32, device=dev)
     native = dev.type == "cuda" if use_native is None else use_native
     if native:
@@ -832,6 +836,34 @@ def fill_nid(ridx, leaf_ids, starts, counts, nrows, use_native=None):
         return nid
     for lid, st, ct in zip(leaf_ids, starts, counts):
         nid[ridx[st: st + ct].long()] = lid
+    return nid
+
+
+def _fill_nid_tiled(ridx, leaf_ids, starts, counts, nrows):
+    """Leaf segments that tile [0, nrows) of the row permutation (every row
+    ends in exactly one leaf): position -> segment by one device searchsorted
+    over the sorted segment starts, then one scatter through ridx.  Deep DRF
+    trees have ~10^5 leaves: this replaces a per-leaf work list (host list
+    conversion + one workgroup per tiny segment).  None if the segments do not
+    tile the rows."""
+    st = np.asarray(starts, dtype=np.int64).reshape(-1)
+    ct = np.asarray(counts, dtype=np.int64).reshape(-1)
+    lid = np.asarray(leaf_ids, dtype=np.int64).reshape(-1)
+    m = ct > 0
+    st, ct, lid = st[m], ct[m], lid[m]
+    if st.size == 0 or st.size != ct.size:
+        return None
+    o = np.argsort(st, kind="stable")
+    st, ct, lid = st[o], ct[o], lid[o]
+    if st[0] != 0 or st[-1] + ct[-1] != nrows or (st.size > 1 and not np.array_equal(st[1:], st[:-1] + ct[:-1])):
+        return None
+    dev = ridx.device
+    bounds = _h2d(st, dev)
+    lid_d = _h2d(lid.astype(np.int32), dev)
+    pos = torch.arange(nrows, device=dev, dtype=torch.int64)
+    seg = torch.searchsorted(bounds, pos, right=True) - 1
+    nid = torch.empty(nrows, dtype=torch.int32, device=dev)
+    nid[ridx[:nrows].long()] = lid_d[seg]
     return nid
 
 

@@ -586,3 +586,32 @@ def test_pair_hist_dev_grouped_matches_reference(nbins, weights, monkeypatch):
     Hr, wr = tree_ops.pair_hist(bd, ridx, va, vb, 0, st, ct, pn, pf, want_wyy=True, use_native=False)
     torch.testing.assert_close(out[4][0], Hr, rtol=1e-5, atol=1e-4)
     torch.testing.assert_close(out[4][1], wr, rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.gpu
+def test_fill_nid_tiled_matches_reference():
+    """Device searchsorted + scatter leaf ids (segments tiling the row
+    permutation, incl. empty leaves and unsorted segment order) equal the
+    per-segment torch reference; non-tiling segments fall back."""
+    import numpy as np
+    import torch
+    from h2o3_amd.ops import tree_ops
+    dev = torch.device("cuda")
+    rng = np.random.RandomState(3)
+    N = 200_003
+    cuts = np.sort(rng.choice(np.arange(1, N), 5000, replace=False))
+    st = np.concatenate([[0], cuts])
+    ct = np.diff(np.concatenate([st, [N]]))
+    st = np.concatenate([st, [N // 2]])          # an empty leaf
+    ct = np.concatenate([ct, [0]])
+    perm = rng.permutation(len(st))
+    st, ct = st[perm], ct[perm]
+    lids = np.arange(len(st))
+    ridx = torch.as_tensor(rng.permutation(N).astype(np.int32), device=dev)
+    ref = tree_ops.fill_nid(ridx.cpu(), list(lids), st.tolist(), ct.tolist(), N, use_native=False)
+    got = tree_ops.fill_nid(ridx, lids, st, ct, N)
+    assert torch.equal(got.cpu(), ref)
+    # a gap in the tiling -> reference path (rows outside every leaf keep -1)
+    got2 = tree_ops.fill_nid(ridx, lids[1:], st[1:], ct[1:], N)
+    ref2 = tree_ops.fill_nid(ridx.cpu(), list(lids[1:]), st[1:].tolist(), ct[1:].tolist(), N, use_native=False)
+    assert torch.equal(got2.cpu(), ref2)
