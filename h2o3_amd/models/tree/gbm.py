@@ -211,6 +211,38 @@ class GBMDriver:
         m[self.rng.choice(F, size=k, replace=False)] = True
         return m
 
+    # f: the running raw prediction [N, K].  With the scatter leaf update the
+    # last tree's per-row leaf values wait in _dpend and are folded into f by
+    # the next residual pass; any other reader of f flushes them first.
+    @property
+    def f(self):
+        d = self.__dict__.get("_dpend")
+        if d is not None:
+            self._dpend = None
+            self._f[:, 0].add_(d)
+        return self._f
+
+    @f.setter
+    def f(self, v):
+        self._dpend = None
+        self._f = v
+
+    def _scatter_ok(self, st, ct):
+        """The scatter update writes every row: only when the leaf segments
+        tile all N positions of the row permutation."""
+        if os.environ.get("H2O3_LEAF_SCATTER", "1") != "1":
+            return False
+        st = np.asarray(st, dtype=np.int64)
+        ct = np.asarray(ct, dtype=np.int64)
+        m = ct > 0
+        st, ct = st[m], ct[m]
+        if st.size == 0:
+            return False
+        o = np.argsort(st, kind="stable")
+        st, ct = st[o], ct[o]
+        return bool(st[0] == 0 and st[-1] + ct[-1] == self._f.shape[0] and
+                    (st.size == 1 or np.array_equal(st[1:], st[:-1] + ct[:-1])))
+
     def step(self):
         """One boosting iteration."""
         p = self.est._parms
@@ -219,7 +251,9 @@ class GBMDriver:
         lr = self.lr * (float(p.get("learn_rate_annealing", 1.0)) ** self.iter)
         maxabs = float(p.get("max_abs_leafnode_pred", 1.79e308))
         if self.K == 1:
-            f = self.f[:, 0]
+            dpend = self.__dict__.get("_dpend")
+            self._dpend = None
+            f = self._f[:, 0]
             y = self.yb if self.spec.nclasses == 2 else torch.nan_to_num(self.yf)
             simple = self.dev.type == "cuda" and self.dist.family in ("gaussian", "bernoulli") and \
                 self.dist.link in ("identity", "logit")
@@ -234,9 +268,12 @@ class GBMDriver:
             # weight 0): the 0/1-weight position-ordered path of grow()
             onepass = posleaf and self._base_unit and self.grower.pos_payload_ok() and \
                 os.environ.get("H2O3_GBM_GRAD", "1") == "1"
+            if dpend is not None and not onepass:
+                f.add_(dpend)
+                dpend = None
             with phase("gbm.grad"):
                 if onepass:
-                    z = tree_ops.gbm_grad(y, f, None if self._unit_weights else w, self.dist.family)
+                    z = tree_ops.gbm_grad(y, f, None if self._unit_weights else w, self.dist.family, d=dpend)
                 else:
                     z = self.dist.neg_half_gradient(y, f).to(torch.float32)
             if self.dist.family == "huber":
@@ -271,7 +308,16 @@ class GBMDriver:
                     vals_d = torch.where(den != 0, s_[:, 0] / torch.where(den == 0, torch.ones_like(den), den),
                                          torch.zeros_like(den)).clamp(-maxabs, maxabs) * lr
                 with phase("gbm.update"):
-                    tree_ops.leaf_update(self.grower.ridx, self.f, vals_d.to(torch.float32), lids, st, ct)
+                    if onepass and self._scatter_ok(st, ct):
+                        # write-only scatter of the per-row leaf value; the next
+                        # residual pass adds it into f (no random read-modify-write)
+                        db = self.__dict__.get("_dbuf")
+                        if db is None or db.numel() != f.numel():
+                            db = self._dbuf = torch.empty_like(f)
+                        tree_ops.leaf_scatter(self.grower.ridx, db, vals_d.to(torch.float32), lids, st, ct)
+                        self._dpend = db
+                    else:
+                        tree_ops.leaf_update(self.grower.ridx, self._f, vals_d.to(torch.float32), lids, st, ct)
                 # two reusable pinned slots: tree t's values land in one while
                 # tree t-1's (read by _resolve_pending below) sit in the other
                 ring = self.__dict__.setdefault("_hv_ring", [None, None])

@@ -822,6 +822,16 @@ __global__ __launch_bounds__(256) void leaf_update_kernel(const int* __restrict_
   for (int p = wk.y + threadIdx.x; p < wk.y + wk.z; p += 256) f[ridx[p]] += v;
 }
 
+// d[ridx[p]] = val[leaf] over the leaf segments: a write-only scatter of the
+// per-row leaf value (no read of f), folded into f by the next tree's
+// residual pass (gbm_grad_kernel with d) or an explicit contiguous add.
+__global__ __launch_bounds__(256) void leaf_scatter_kernel(const int* __restrict__ ridx, const int4* __restrict__ work,
+                                                           const float* __restrict__ val, float* __restrict__ d) {
+  const int4 wk = work[blockIdx.x];
+  const float v = val[wk.x];
+  for (int p = wk.y + threadIdx.x; p < wk.y + wk.z; p += 256) d[ridx[p]] = v;
+}
+
 // nid[ridx[p]] = leaf for p in segment.  work[i] = (leaf_id, start, count, -)
 __global__ __launch_bounds__(256) void fill_nid_kernel(const int* __restrict__ ridx, const int4* __restrict__ work,
                                                        int* __restrict__ nid) {
@@ -1104,6 +1114,13 @@ extern "C" int h2o_leaf_pos(const float* zp, const int* work, int n_work, int mo
   return (int)hipGetLastError();
 }
 
+extern "C" int h2o_leaf_scatter(const int* ridx, const int* work, int n_work, const float* val, float* d,
+                                hipStream_t s) {
+  if (n_work <= 0) return 0;
+  hipLaunchKernelGGL(leaf_scatter_kernel, dim3(n_work), dim3(256), 0, s, ridx, (const int4*)work, val, d);
+  return (int)hipGetLastError();
+}
+
 extern "C" int h2o_leaf_update(const int* ridx, const int* work, int n_work, const float* val, float* f,
                                hipStream_t s) {
   if (n_work <= 0) return 0;
@@ -1379,12 +1396,16 @@ extern "C" int h2o_pair_hist(const void* codes_col, int code_bytes, long long nc
 // histogram and leaf kernels treat NaN as weight 0).  Reference:
 // hex/tree/gbm/GBM.java ComputePredAndRes / Distribution.negHalfGradient.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void gbm_grad_kernel(const float* __restrict__ y, const float* __restrict__ f,
+__global__ __launch_bounds__(256) void gbm_grad_kernel(const float* __restrict__ y, float* __restrict__ f,
                                                        const float* __restrict__ w, int mode, long long n,
-                                                       float* __restrict__ z) {
+                                                       float* __restrict__ z, const float* __restrict__ d) {
   const long long stride = (long long)gridDim.x * 256;
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
-    const float fi = f[i];
+    float fi = f[i];
+    if (d != nullptr) {          // previous tree's per-row leaf values (leaf_scatter_kernel)
+      fi += d[i];
+      f[i] = fi;
+    }
     const float p = mode == 1 ? 1.f / (1.f + expf(-fi)) : fi;
     float v = y[i] - p;
     if (w != nullptr && !(w[i] > 0.f)) v = __builtin_nanf("");
@@ -1392,11 +1413,11 @@ __global__ __launch_bounds__(256) void gbm_grad_kernel(const float* __restrict__
   }
 }
 
-extern "C" int h2o_gbm_grad(const float* y, const float* f, const float* w, int mode, long long n, float* z,
-                            hipStream_t s) {
+extern "C" int h2o_gbm_grad(const float* y, float* f, const float* w, int mode, long long n, float* z,
+                            const float* d, hipStream_t s) {
   if (n <= 0) return 0;
   const long long blocks = std::min<long long>((n + 255) / 256, 8192);
-  hipLaunchKernelGGL(gbm_grad_kernel, dim3((unsigned)blocks), dim3(256), 0, s, y, f, w, mode, n, z);
+  hipLaunchKernelGGL(gbm_grad_kernel, dim3((unsigned)blocks), dim3(256), 0, s, y, f, w, mode, n, z, d);
   return (int)hipGetLastError();
 }
 

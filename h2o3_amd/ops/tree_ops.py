@@ -507,12 +507,17 @@ def pair_hist_dev(bd, ridx, va, vb, mode, node_st, node_ct, sel, vmax, posv=Fals
     return Hp, (pwyy.view(n, k)[:, 0].contiguous() if want_wyy else None), pfeat
 
 
-def gbm_grad(y, f, w, family, out=None):
+def gbm_grad(y, f, w, family, out=None, d=None):
     """GBM residual in one HIP pass (gbm_grad_kernel): y - f (gaussian) or
-    y - sigmoid(f) (bernoulli), NaN where w == 0 (w may be None).  f32."""
+    y - sigmoid(f) (bernoulli), NaN where w == 0 (w may be None).  f32.
+    d: pending per-row leaf values of the previous tree (leaf_scatter), added
+    into f (in place) by the same pass."""
     mode = {"gaussian": 0, "bernoulli": 1}[family]
     n = y.numel()
     z = out if out is not None else torch.empty(n, dtype=torch.float32, device=y.device)
+    if d is not None and (y.device.type != "cuda" or not f.is_contiguous() or f.dtype != torch.float32):
+        f.add_(d.view_as(f))
+        d = None
     if y.device.type != "cuda":
         p = f if mode == 0 else torch.sigmoid(f)
         v = (y - p).to(torch.float32)
@@ -522,11 +527,11 @@ def gbm_grad(y, f, w, family, out=None):
         return z
     lib = _lib()
     if not getattr(lib, "_typed_grad", False):
-        lib.h2o_gbm_grad.argtypes = [_c_void, _c_void, _c_void, _c_int, _c_ll, _c_void, _c_void]
+        lib.h2o_gbm_grad.argtypes = [_c_void, _c_void, _c_void, _c_int, _c_ll, _c_void, _c_void, _c_void]
         lib._typed_grad = True
     yc, fc = y.contiguous().to(torch.float32), f.contiguous().to(torch.float32)
     wc = w.contiguous().to(torch.float32) if w is not None else None
-    rc = lib.h2o_gbm_grad(_ptr(yc), _ptr(fc), _ptr(wc), mode, n, _ptr(z), _stream())
+    rc = lib.h2o_gbm_grad(_ptr(yc), _ptr(fc), _ptr(wc), mode, n, _ptr(z), _ptr(d), _stream())
     if rc != 0:
         raise RuntimeError(f"h2o_gbm_grad failed: {rc}")
     return z
@@ -906,6 +911,26 @@ def leaf_pos_sums(zpos, leaf_ids, starts, counts, n_leaves, mode, chunk=65536):
         if rc != 0:
             raise RuntimeError(f"h2o_leaf_pos failed: {rc}")
     return out
+
+
+def leaf_scatter(ridx, d, vals, leaf_ids, starts, counts, chunk=65536):
+    """d[ridx[p]] = vals[leaf] over the leaf segments (write-only scatter;
+    every row of the tiling is written)."""
+    if d.device.type != "cuda":
+        for lid, st, ct in zip(leaf_ids, starts, counts):
+            d[ridx[st: st + ct].long()] = vals[lid]
+        return d
+    lib = _lib()
+    if not getattr(lib, "_typed_lscat", False):
+        lib.h2o_leaf_scatter.argtypes = [_c_void, _c_void, _c_int, _c_void, _c_void, _c_void]
+        lib._typed_lscat = True
+    items = make_work(starts, counts, leaf_ids, chunk)
+    if len(items):
+        work = _h2d(items, d.device)
+        rc = lib.h2o_leaf_scatter(_ptr(ridx), _ptr(work), len(items), _ptr(vals), _ptr(d), _stream())
+        if rc != 0:
+            raise RuntimeError(f"h2o_leaf_scatter failed: {rc}")
+    return d
 
 
 def leaf_update(ridx, f, vals, leaf_ids, starts, counts, chunk=65536):

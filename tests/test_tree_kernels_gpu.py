@@ -615,3 +615,32 @@ def test_fill_nid_tiled_matches_reference():
     got2 = tree_ops.fill_nid(ridx, lids[1:], st[1:], ct[1:], N)
     ref2 = tree_ops.fill_nid(ridx.cpu(), list(lids[1:]), st[1:].tolist(), ct[1:].tolist(), N, use_native=False)
     assert torch.equal(got2.cpu(), ref2)
+
+
+@pytest.mark.gpu
+def test_gbm_leaf_scatter_update_matches_rmw(monkeypatch):
+    """The write-only leaf scatter (per-row leaf values folded into f by the
+    next residual pass) trains the same model as the in-place f[ridx[p]] += v
+    update, with and without row sampling (sampled-out rows are NaN-masked
+    but still tiled into leaves)."""
+    import numpy as np
+    import torch
+    import h2o3_amd as h2o
+    from h2o3_amd.core.frame import H2OFrame
+    from h2o3_amd.core.vec import Vec, T_REAL, T_ENUM
+    from h2o3_amd.estimators import H2OGradientBoostingEstimator
+    h2o.init(verbose=False)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    N, P = 300_000, 16
+    X = torch.randn((N, P), generator=g, device="cuda")
+    y = (torch.rand(N, generator=g, device="cuda") < torch.sigmoid(X[:, 0] - X[:, 1])).to(torch.int32)
+    fr = H2OFrame.from_vecs([Vec(X[:, j].contiguous(), T_REAL) for j in range(P)] + [Vec(y, T_ENUM, ["0", "1"])],
+                            [f"x{j}" for j in range(P)] + ["y"])
+    for sr in (1.0, 0.7):
+        preds = []
+        for flag in ("1", "0"):
+            monkeypatch.setenv("H2O3_LEAF_SCATTER", flag)
+            m = H2OGradientBoostingEstimator(ntrees=6, max_depth=5, seed=3, sample_rate=sr)
+            m.train(y="y", training_frame=fr)
+            preds.append(m.predict(fr).as_data_frame()["1"].values)
+        np.testing.assert_allclose(preds[0], preds[1], rtol=0, atol=1e-6)
