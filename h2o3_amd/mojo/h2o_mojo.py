@@ -539,6 +539,98 @@ class H2OMojoModel:
             if t < len(self.booster.trees):
                 self.booster.trees[t][1]["sum_hess"][:nn] = w
 
+    def _load_targetencoder(self):
+        """TargetEncoderMojoReader.java: per-column encoding maps (level ->
+        numerator, denominator[, target class]; the last level is NA), the NA
+        presence map, blending parameters and the input -> output column
+        maps (legacy MOJOs without maps encode every mapped column to
+        <col>_te / <col>_<k>_te)."""
+        d = "feature_engineering/target_encoding/"
+        self.te_blend = bool(self.kv("with_blending", False))
+        self.te_k = float(self.kv("inflection_point", 0.0) or 0.0)
+        self.te_f = float(self.kv("smoothing", 0.0) or 0.0)
+        self.te_maps = {}
+        sec = None
+        for line in self.be.text(d + "encoding_map.ini"):
+            line = line.strip()
+            if not line:
+                continue
+            if line.startswith("[") and line.endswith("]"):
+                sec = line[1:-1]
+                self.te_maps[sec] = {}
+                continue
+            lev, _, rest = line.partition("=")
+            vals = [float(t) for t in rest.split()]
+            tc = int(vals[2]) if len(vals) > 2 else -1
+            self.te_maps[sec].setdefault(int(lev.strip()), {})[tc] = (vals[0], vals[1])
+        self.te_has_na = {}
+        if self.be.exists(d + "te_column_name_to_missing_values_presence.ini"):
+            for line in self.be.text(d + "te_column_name_to_missing_values_presence.ini"):
+                if "=" in line:
+                    k, _, v = line.partition("=")
+                    self.te_has_na[k.strip()] = int(v.strip()) == 1
+
+        def maps(name):
+            out, cur, key = [], None, None
+            if not self.be.exists(d + name):
+                return out
+            for line in self.be.text(d + name):
+                if line in ("[from]", "[to]", "[to_domain]"):
+                    if line == "[from]":
+                        cur = {"from": [], "to": [], "to_domain": []}
+                        out.append(cur)
+                    key = line[1:-1]
+                    continue
+                if cur is not None and line:
+                    cur[key].append(line)
+            return out
+        self.te_inenc = maps("input_encoding_columns_map.ini")
+        self.te_inout = maps("input_output_columns_map.ini")
+        nout = self.nclasses - 1 if self.nclasses > 1 else 1
+        if not self.te_inenc:
+            for c in self.te_maps:
+                self.te_inenc.append({"from": [c], "to": [c], "to_domain": []})
+                outs = [f"{c}_{i + 1}_te" for i in range(nout)] if nout > 1 else [f"{c}_te"]
+                self.te_inout.append({"from": [c], "to": outs, "to_domain": []})
+        for m in self.te_inenc:
+            if len(m["from"]) > 1:
+                raise NotImplementedError("target-encoding MOJOs over column interactions are not supported")
+        self.te_out_names = [n for m in self.te_inout for n in m["to"]]
+
+    def _te_prior(self, enc, tc):
+        num = sum(v[tc][0] for v in enc.values())
+        den = sum(v[tc][1] for v in enc.values())
+        return num / den
+
+    def _score_targetencoder(self, X):
+        """TargetEncoderMojoModel.score0: posterior mean num / den of the
+        row's level (blended with the prior by lambda = 1 / (1 + exp((k - n)
+        / f)) when blending); missing / unseen levels use the NA level if the
+        column had NAs in training, else the prior."""
+        cols = {c: i for i, c in enumerate(self.columns)}
+        tcs = list(range(1, self.nclasses)) if self.nclasses > 2 else [-1]
+        outs = []
+        for m in self.te_inenc:
+            c, te = m["from"][0], m["to"][0]
+            enc = self.te_maps[te]
+            v = X[:, cols[c]]
+            na_cat = len(enc) - 1
+            for tc in tcs:
+                prior = self._te_prior(enc, tc)
+                num = np.array([enc[k][tc][0] for k in range(len(enc))])
+                den = np.array([enc[k][tc][1] for k in range(len(enc))])
+                miss = np.isnan(v) | (np.nan_to_num(v, nan=-1) >= na_cat) | (np.nan_to_num(v, nan=-1) < 0)
+                lev = np.where(miss, na_cat, np.nan_to_num(v, nan=0)).astype(np.int64)
+                with np.errstate(divide="ignore", invalid="ignore"):
+                    post = num[lev] / den[lev]
+                    if self.te_blend:
+                        lam = 1.0 / (1.0 + np.exp((self.te_k - np.floor(den[lev])) / self.te_f))
+                        post = lam * post + (1 - lam) * prior
+                if not self.te_has_na.get(te, False):
+                    post = np.where(miss, prior, post)
+                outs.append(post)
+        return np.stack(outs, 1) if outs else np.zeros((X.shape[0], 0))
+
     def _load_svm(self):
         """SvmMojoReader.java (Sparkling Water's linear SVM): weights over the
         raw feature values, intercept, label threshold, optional mean
@@ -1153,6 +1245,8 @@ class H2OMojoModel:
             return pd.DataFrame(preds, columns=[f"PC{i + 1}" for i in range(preds.shape[1])])
         if self.algo == "coxph":
             return pd.DataFrame({"lp": preds[:, 0]})
+        if self.algo == "targetencoder":
+            return pd.DataFrame(preds, columns=self.te_out_names)
         if self.category == "AutoEncoder":
             return pd.DataFrame(preds, columns=[f"reconstr_{i}" for i in range(preds.shape[1])])
         if self.nclasses > 1 and preds.shape[1] > 1:

@@ -404,6 +404,60 @@ def _xgboost(model, z):
     z.write("boosterBytes", b.to_bytes())
 
 
+# ---------------------------------------------------------- TargetEncoder
+def _targetencoder(model, z):
+    """TargetEncoderMojoWriter layout: model.ini (blending parameters,
+    non_predictors), feature_engineering/target_encoding/encoding_map.ini
+    ([column] sections of `level = numerator denominator [target class]`, the
+    last level being the NA level), the NA-presence map and the input ->
+    encoded-column / input -> output-column maps."""
+    spec = model._spec
+    p = model._parms
+    cols = list(model._cols)
+    te_dir = "feature_engineering/target_encoding/"
+    multi = spec.nclasses > 2
+    enc_lines, na_lines, inenc, inout = [], [], [], []
+    for c in cols:
+        dom, per = model._tables[c]
+        L = len(dom) + 1
+        enc_lines.append(f"[{c}]")
+        for lev in range(L):
+            for ci, st in enumerate(per):
+                num, den = float(st[0][lev]), float(st[1][lev])
+                if multi:
+                    enc_lines.append(f"{lev} = {num!r} {den!r} {ci + 1}")
+                else:
+                    enc_lines.append(f"{lev} = {num!r} {den!r}")
+        has_na = any(float(st[1][L - 1]) > 0 for st in per)
+        na_lines.append(f"{c} = {1 if has_na else 0}")
+        inenc += ["[from]", c, "[to]", c]
+        inout += ["[from]", c, "[to]"] + [f"{c}{sfx}_te" for sfx in model._suffix]
+    x = [n for n in spec.x]
+    columns = x + [spec.y]
+    xd = {}
+    for n in x:
+        v = spec.frame.vec(n)
+        xd[n] = list(v.domain) if v.domain is not None else None
+    domains = [xd[n] for n in x] + [list(spec.response_domain) if spec.response_domain else None]
+    nonpred = [c for c in (spec.weights_column, spec.offset_column, p.get("fold_column"), spec.y) if c]
+    extra = {"keep_original_categorical_columns": bool(p.get("keep_original_categorical_columns", True)),
+             "with_blending": bool(p.get("blending"))}
+    if p.get("blending"):
+        extra.update(inflection_point=float(p.get("inflection_point", 10.0)),
+                     smoothing=float(p.get("smoothing", 20.0)))
+    extra["non_predictors"] = ";".join(nonpred)
+    cat = "Binomial" if spec.nclasses == 2 else "Multinomial" if spec.nclasses > 2 else "Regression"
+    ini, files = _header(model, "targetencoder", "TargetEncoder", cat, columns, len(x), spec.nclasses, domains,
+                         "1.00", extra)
+    z.write("model.ini", ini)
+    for k_, v in files.items():
+        z.write(k_, v)
+    z.write(te_dir + "encoding_map.ini", "\n".join(enc_lines) + "\n")
+    z.write(te_dir + "te_column_name_to_missing_values_presence.ini", "\n".join(na_lines) + "\n")
+    z.write(te_dir + "input_encoding_columns_map.ini", "\n".join(inenc) + "\n")
+    z.write(te_dir + "input_output_columns_map.ini", "\n".join(inout) + "\n")
+
+
 # ------------------------------------------------------------------ CoxPH
 def _rect_blob(z, extra, title, a):
     """AbstractMojoWriter.writeRectangularDoubleArray: sizes in [info], a
@@ -752,7 +806,7 @@ def _stackedensemble(model, z):
 _WRITERS = {"gbm": _gbm, "drf": _drf, "glm": _glm, "kmeans": _kmeans, "isolationforest": _isofor,
             "extendedisolationforest": _eif, "deeplearning": _deeplearning, "word2vec": _word2vec,
             "stackedensemble": _stackedensemble, "pca": _pca, "xgboost": _xgboost,
-            "coxph": _coxph}
+            "coxph": _coxph, "targetencoder": _targetencoder}
 
 
 def _write_algo(model, z):

@@ -226,3 +226,34 @@ def test_xgboost_h2o_mojo_roundtrip(data, y, tmp_path):
     np.testing.assert_allclose(theirs[cols].values.astype(float), ours[cols].values.astype(float), atol=2e-5)
     if y != "yr":
         assert (theirs["predict"].astype(str).values == ours["predict"].astype(str).values).mean() > 0.999
+
+
+@pytest.mark.parametrize("y,blending", [("yb", False), ("yb", True), ("yr", True), ("ym", False)])
+def test_targetencoder_h2o_mojo_roundtrip(data, y, blending, tmp_path):
+    """Reference-layout TargetEncoder MOJO (encoding_map.ini + column maps):
+    the reader's encodings equal the in-platform transform (NA levels, unseen
+    levels -> NA / prior, blending, one column per non-first class)."""
+    from h2o3_amd.estimators import H2OTargetEncoderEstimator
+    from h2o3_amd.mojo import h2o_mojo
+    import h2o3_amd as h2o
+    df, fr = data
+    df = df.copy()
+    df.loc[df.index[:40], "cat"] = None                      # NA level present in training
+    fr2 = h2o.H2OFrame(df)
+    te = H2OTargetEncoderEstimator(blending=blending, inflection_point=5, smoothing=3)
+    te.train(x=["cat", "big"], y=y, training_frame=fr2)
+    ours = te.transform(fr2, as_training=False).as_data_frame()
+    m = h2o_mojo.load(te.download_mojo(str(tmp_path), format="h2o"))
+    assert m.algo == "targetencoder"
+    theirs = m.predict(df)
+    for c in theirs.columns:
+        np.testing.assert_allclose(theirs[c].values, ours[c].values, rtol=1e-9, atol=1e-12)
+    # unseen level: 'big' had no NAs in training -> prior mean
+    row = df.iloc[:1].copy()
+    row["big"] = "never_seen"
+    enc = m.predict(row)
+    big_cols = [c for c in enc.columns if c.startswith("big")]
+    for c in big_cols:
+        cls = c[len("big"):-len("_te")]
+        k = 1 if not cls else list(te._spec.response_domain).index(cls.lstrip("_"))
+        assert enc[c].iloc[0] == pytest.approx(te._prior[max(k - 1, 0)] if len(te._prior) > 1 else te._prior[0])
