@@ -195,6 +195,12 @@ class DRFDriver:
             valid = ~torch.isnan(yf)
             self.targets = [torch.nan_to_num(yf)]
         self.base_w = torch.where(valid, base_w, torch.zeros_like(base_w))
+        # caller-known histogram bounds (grow() would otherwise run two
+        # full-column reductions + device syncs per tree): the in-bag weights
+        # are base_w * {0, 1}, so the base weights' bounds hold for every tree
+        self._unit_w = bool(((self.base_w == 0) | (self.base_w == 1)).all())
+        self._vmax = [max(float(self.base_w.abs().max()) if N else 1.0, 1e-30),
+                      max([float((self.base_w * t.abs()).max()) if N else 0.0 for t in self.targets] + [1e-30])]
         self.forest = Forest()
         self.oob_sum = torch.zeros((N, K), dtype=torch.float32, device=dev)
         self.oob_cnt = torch.zeros(N, dtype=torch.float32, device=dev)
@@ -221,7 +227,8 @@ class DRFDriver:
             self.gp.tree_col_mask = m
         oob = ~inbag
         for k in range(self.K):
-            tree, nid, leaves, tot = self.grower.grow(self.targets[k].contiguous(), wt, 0)
+            tree, nid, leaves, tot = self.grower.grow(self.targets[k].contiguous(), wt, 0, vmax=self._vmax,
+                                                      unit_w=self._unit_w)
             tot = tot.numpy() if isinstance(tot, torch.Tensor) else np.asarray(tot)
             vals = np.where(tot[:, 0] > 0, tot[:, 1] / np.where(tot[:, 0] > 0, tot[:, 0], 1), 0.0)
             for li, node in enumerate(leaves):

@@ -103,7 +103,7 @@ class Tree:
         return [i for i in range(self.n_nodes) if self.left[i] < 0]
 
     def max_depth(self):
-        return max(self.depth) if self.depth else 0
+        return int(max(self.depth)) if len(self.depth) else 0
 
     def to_arrays(self):
         return {k: np.asarray(getattr(self, k)) for k in ("feat", "left", "right", "thr", "na_left", "is_cat",
@@ -174,10 +174,13 @@ class _TreeBuf:
         return base
 
     def to_tree(self):
+        """Tree over numpy per-node arrays (copies; no per-node Python lists:
+        the list conversion cost ~5 ms per depth-20 DRF tree).  Index,
+        assignment and len() behave like the list form."""
         n = self.n
         t = Tree()
         for name, _, _ in self._FIELDS:
-            setattr(t, name, getattr(self, name)[:n].tolist())
+            setattr(t, name, getattr(self, name)[:n].copy())
         t.cat_left = [None] * n
         for i, m in self.cat_left.items():
             t.cat_left[i] = m
@@ -286,7 +289,11 @@ class TreeGrower:
             return None
         elig = np.nonzero(base)[0]
         if self.dev.type == "cuda":
-            gen = torch.Generator(device=self.dev)
+            # one device generator per grower, re-seeded per level (creating a
+            # device generator per level cost more than the sampling itself)
+            gen = self.__dict__.get("_sel_gen")
+            if gen is None:
+                gen = self._sel_gen = torch.Generator(device=self.dev)
             gen.manual_seed(int(self.rng.randint(0, 2 ** 31 - 1)))
             keys = torch.rand((n_nodes, len(elig)), generator=gen, device=self.dev)
             sel = torch.topk(keys, k, dim=1, largest=False).indices
