@@ -142,7 +142,8 @@ def test_grow_async_matches_sync(monkeypatch):
         tree, nid, leaves, tot = gr.grow(y, w, 0)
         trees.append((tree, nid.cpu(), tot))
     (ta, na, sa), (tb, nb, sb) = trees
-    assert ta.feat == tb.feat and ta.left == tb.left and ta.split_code == tb.split_code
+    assert list(ta.feat) == list(tb.feat) and list(ta.left) == list(tb.left) and \
+        list(ta.split_code) == list(tb.split_code)
     assert torch.equal(na, nb)
     torch.testing.assert_close(sa, sb)
 
