@@ -289,20 +289,15 @@ class TreeGrower:
             return None
         elig = np.nonzero(base)[0]
         if self.dev.type == "cuda":
-            # one device generator per grower, re-seeded per level (creating a
-            # device generator per level cost more than the sampling itself)
-            gen = self.__dict__.get("_sel_gen")
-            if gen is None:
-                gen = self._sel_gen = torch.Generator(device=self.dev)
-            gen.manual_seed(int(self.rng.randint(0, 2 ** 31 - 1)))
-            keys = torch.rand((n_nodes, len(elig)), generator=gen, device=self.dev)
-            sel = torch.topk(keys, k, dim=1, largest=False).indices
+            # one HIP launch: per-node selection sampling, rows come out sorted
+            # (was rand + top-k + gather + segmented sort, with a host sync)
+            seed = int(self.rng.randint(0, 2 ** 31 - 1))
             el = self.__dict__.setdefault("_elig_dev", {})
             key = elig.tobytes()
             if key not in el:
                 el.clear()
-                el[key] = torch.as_tensor(elig, device=self.dev)
-            return torch.sort(el[key][sel], dim=1).values
+                el[key] = torch.as_tensor(elig.astype(np.int64), device=self.dev)
+            return tree_ops.col_sample(n_nodes, el[key], k, seed)
         keys = self.rng.random_sample((n_nodes, len(elig)))
         sel = np.argpartition(keys, k - 1, axis=1)[:, :k]
         return torch.from_numpy(np.sort(elig[sel], axis=1))

@@ -832,6 +832,33 @@ __global__ __launch_bounds__(256) void leaf_scatter_kernel(const int* __restrict
   for (int p = wk.y + threadIdx.x; p < wk.y + wk.z; p += 256) d[ridx[p]] = v;
 }
 
+// Per-node column sampling without replacement (DRF mtries, GBM
+// col_sample_rate): one thread per node runs selection sampling (Knuth's
+// algorithm S) over the m eligible features -- feature j is taken with
+// probability (k - taken) / (m - j) -- so the k ids come out already in
+// ascending order, with no random-key sort / top-k (which cost ~8 launches
+// and a host sync per tree level).  Uniforms from a splitmix64 hash of
+// (seed, node, j): deterministic for a seed.
+__device__ __forceinline__ unsigned long long smix64(unsigned long long x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+__global__ __launch_bounds__(256) void col_sample_kernel(int n, int m, const long long* __restrict__ elig, int k,
+                                                         unsigned long long seed, long long* __restrict__ out) {
+  const int node = blockIdx.x * blockDim.x + threadIdx.x;
+  if (node >= n) return;
+  const unsigned long long base = smix64(seed ^ ((unsigned long long)node * 0xD1B54A32D192ED03ull));
+  long long* o = out + (size_t)node * k;
+  int taken = 0;
+  for (int j = 0; j < m && taken < k; ++j) {
+    const double u = (double)(smix64(base + (unsigned long long)j) >> 11) * (1.0 / 9007199254740992.0);
+    if (u * (double)(m - j) < (double)(k - taken)) o[taken++] = elig[j];
+  }
+}
+
 // nid[ridx[p]] = leaf for p in segment.  work[i] = (leaf_id, start, count, -)
 __global__ __launch_bounds__(256) void fill_nid_kernel(const int* __restrict__ ridx, const int4* __restrict__ work,
                                                        int* __restrict__ nid) {
@@ -1111,6 +1138,14 @@ extern "C" int h2o_seg_sum2(const int* ridx, const float* a, const float* b, con
 extern "C" int h2o_leaf_pos(const float* zp, const int* work, int n_work, int mode, double* out, hipStream_t s) {
   if (n_work <= 0) return 0;
   hipLaunchKernelGGL(leaf_pos_kernel, dim3(n_work), dim3(256), 0, s, zp, (const int4*)work, mode, out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int h2o_col_sample(int n, int m, const long long* elig, int k, unsigned long long seed, long long* out,
+                              hipStream_t s) {
+  if (n <= 0 || k <= 0) return 0;
+  if (k > m) return 1;
+  hipLaunchKernelGGL(col_sample_kernel, dim3((n + 255) / 256), dim3(256), 0, s, n, m, elig, k, seed, out);
   return (int)hipGetLastError();
 }
 

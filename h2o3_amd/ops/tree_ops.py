@@ -913,6 +913,23 @@ def leaf_pos_sums(zpos, leaf_ids, starts, counts, n_leaves, mode, chunk=65536):
     return out
 
 
+def col_sample(n, elig_d, k, seed):
+    """[n, k] int64 per-node feature samples without replacement from the
+    eligible global feature ids elig_d (device int64, ascending), each row
+    ascending (HIP selection sampling, col_sample_kernel)."""
+    dev = elig_d.device
+    out = torch.empty((n, k), dtype=torch.int64, device=dev)
+    lib = _lib()
+    if not getattr(lib, "_typed_csamp", False):
+        lib.h2o_col_sample.argtypes = [_c_int, _c_int, _c_void, _c_int, ctypes.c_ulonglong, _c_void, _c_void]
+        lib._typed_csamp = True
+    rc = lib.h2o_col_sample(int(n), int(elig_d.numel()), _ptr(elig_d), int(k), int(seed) & ((1 << 64) - 1),
+                            _ptr(out), _stream())
+    if rc != 0:
+        raise RuntimeError(f"h2o_col_sample failed: {rc}")
+    return out
+
+
 def leaf_scatter(ridx, d, vals, leaf_ids, starts, counts, chunk=65536):
     """d[ridx[p]] = vals[leaf] over the leaf segments (write-only scatter;
     every row of the tiling is written)."""

@@ -645,3 +645,25 @@ def test_gbm_leaf_scatter_update_matches_rmw(monkeypatch):
             m.train(y="y", training_frame=fr)
             preds.append(m.predict(fr).as_data_frame()["1"].values)
         np.testing.assert_allclose(preds[0], preds[1], rtol=0, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_col_sample_kernel_uniform_sorted_distinct():
+    """Per-node selection sampling: every row holds k distinct eligible ids in
+    ascending order; inclusion frequencies are uniform (k / m each) and the
+    pair co-occurrence matches sampling without replacement."""
+    import numpy as np
+    import torch
+    from h2o3_amd.ops import tree_ops
+    elig = np.array([0, 2, 3, 5, 8, 9, 11, 14, 15, 20], dtype=np.int64)
+    n, k, m = 200_000, 3, len(elig)
+    out = tree_ops.col_sample(n, torch.as_tensor(elig, device="cuda"), k, 12345).cpu().numpy()
+    assert out.shape == (n, k)
+    assert np.all(np.diff(out, axis=1) > 0)
+    assert np.isin(out, elig).all()
+    freq = np.array([(out == e).sum() for e in elig]) / n
+    np.testing.assert_allclose(freq, k / m, atol=0.006)
+    both = ((out == elig[0]).any(1) & (out == elig[1]).any(1)).mean()
+    assert abs(both - k * (k - 1) / (m * (m - 1))) < 0.004
+    out2 = tree_ops.col_sample(n, torch.as_tensor(elig, device="cuda"), k, 12345).cpu().numpy()
+    assert np.array_equal(out, out2)
