@@ -611,10 +611,12 @@ class GLMDriver:
             mask = np.array([nonneg or (c in s_) for c in self.dinfo.coef_names] + [False])
             nonneg = mask if self.intercept else mask[:-1]
         k = Gn.shape[0]
-        new = _solve_quadratic(Gn, bn, l1, l2, self.intercept, beta0=self.beta if self.intercept else self.beta[:-1],
-                               non_negative=nonneg, lower=None if self.lower is None else self.lower[:k],
-                               upper=None if self.upper is None else self.upper[:k],
-                               active=None if self.active is None else self.active[:k])
+        with phase("glm.solve"):
+            new = _solve_quadratic(Gn, bn, l1, l2, self.intercept,
+                                   beta0=self.beta if self.intercept else self.beta[:-1],
+                                   non_negative=nonneg, lower=None if self.lower is None else self.lower[:k],
+                                   upper=None if self.upper is None else self.upper[:k],
+                                   active=None if self.active is None else self.active[:k])
         if not self.intercept:
             new = np.concatenate([new, [0.0]])
         diff = float(np.max(np.abs(new - self.beta))) if new.size else 0.0

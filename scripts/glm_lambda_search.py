@@ -35,6 +35,9 @@ def main():
                       "lambdas_fit": len(lams) if lams is not None else None, "nonzero_coefs": nz,
                       "lambda_best": est._output.get("lambda_best"),
                       "ms_per_iteration": round(1000 * el / max(1, int(it or 1)), 1)}))
+    from h2o3_amd.utils import timer
+    if timer.ENABLED:
+        print("phases(ms,count):", timer.report())
 
 
 if __name__ == "__main__":
