@@ -227,6 +227,31 @@ class H2OAutoML:
             return False       # this grid step's share of the budget is spent
         return True
 
+    def _set_stopping_tolerance(self, frame):
+        """AutoML.java:357: an unset stopping tolerance adapts to the training
+        frame, min(0.05, max(0.001, 1 / sqrt((1 - NA fraction) * nrows)))
+        (HyperSpaceSearchCriteria.default_stopping_tolerance_for_frame); a user
+        value under 70% of that default draws a warning."""
+        n = int(frame.nrows)
+        ncols = max(1, len(frame.names))
+        na = 0
+        for c in frame.names:
+            try:
+                na += int(frame.vec(c).nacnt())
+            except Exception:
+                pass
+        naf = min(1.0, na / max(1, n * ncols))
+        dflt = min(0.05, max(0.001, 1.0 / math.sqrt(max(1e-12, (1 - naf) * max(n, 1)))))
+        if self.stopping_tolerance in (None, -1, "AUTO"):
+            self.stopping_tolerance = dflt
+            self._log("Validation", f"Setting stopping tolerance adaptively based on the training frame: {dflt}")
+        else:
+            self._log("Validation", f"Stopping tolerance set by the user: {self.stopping_tolerance}")
+            if float(self.stopping_tolerance) < 0.7 * dflt:
+                self._log("Validation", f"Stopping tolerance set by the user is < 70% of the recommended default of "
+                                        f"{dflt}, so models may take a long time to converge or may not converge "
+                                        f"at all.", level="Warn")
+
     def _assign_step_time(self, item, pending):
         """Time share of one step (ModelingStep.java:550): remaining budget x
         its weight / the remaining weight of the steps in its priority group
@@ -460,6 +485,7 @@ class H2OAutoML:
             args = _resume_state["args"]
             self._done_steps = list(_resume_state["done_steps"])
         self._log("Workflow", f"AutoML build started: {self.project_name}")
+        self._set_stopping_tolerance(training_frame)
         train, xx = self._preprocess(training_frame, x, y, classification)
         valid = validation_frame
         if self._te is not None and valid is not None:

@@ -101,3 +101,25 @@ def test_automl_time_allocation_by_work_weight():
     assert 30 < share < 34          # 100 s x 10 / (10 + 10 + 10 SE)
     aml._assign_step_time(pending[2], pending[2:])
     assert 70 < aml._step_deadline - time.time() < 76   # grid: 30 / (30 + 10)
+
+
+import pytest  # noqa: E402
+
+
+def test_automl_adaptive_stopping_tolerance():
+    """AutoML.java:357: unset stopping_tolerance = min(0.05, max(0.001,
+    1/sqrt((1 - NA fraction) * nrows)))."""
+    import numpy as np
+    import pandas as pd
+    import h2o3_amd as h2o
+    from h2o3_amd.automl import H2OAutoML
+    h2o.init(verbose=False)
+    df = pd.DataFrame({"a": np.arange(4000, dtype=float), "b": np.ones(4000)})
+    df.loc[:999, "a"] = np.nan                      # NA fraction 1000 / 8000
+    fr = h2o.H2OFrame(df)
+    aml = H2OAutoML(max_models=1)
+    aml._set_stopping_tolerance(fr)
+    assert aml.stopping_tolerance == pytest.approx(1 / np.sqrt(0.875 * 4000))
+    big = H2OAutoML(max_models=1, stopping_tolerance=0.0001)
+    big._set_stopping_tolerance(fr)
+    assert big.stopping_tolerance == 0.0001
