@@ -1,0 +1,35 @@
+"""Grouped sums without contended floating-point atomics.
+
+`index_add_` / `bincount(weights=)` of millions of rows into a handful of
+bins (class counts, per-class moments, per-cluster sums) serialises on a few
+addresses: measured on MI355X, one f64 index_add_ of 2M rows into 2 bins took
+~0.36 s (Naive Bayes on 2M x 50 spent 55 s in them).  For small bin counts
+the sums are a one-hot GEMM on the matrix cores instead (f64 in, f64
+accumulate; rows processed in chunks so the one-hot block stays ~256 MB);
+large bin counts keep index_add_ (the atomics spread over many addresses).
+"""
+from __future__ import annotations
+
+import torch
+
+_ONEHOT_MAX_BINS = 1024
+_ONEHOT_BLOCK = 1 << 25          # elements of one [rows, bins] one-hot block
+
+
+def group_sum(idx: torch.Tensor, vals: torch.Tensor, nbins: int, dtype=torch.float64) -> torch.Tensor:
+    """Sums of vals ([N] or [N, C]) grouped by idx (integer in [0, nbins)).
+    Returns [nbins] (1-D vals) or [nbins, C]."""
+    one_d = vals.dim() == 1
+    v = (vals.view(-1, 1) if one_d else vals).to(dtype)
+    idx = idx.reshape(-1).to(torch.int64)
+    C = v.shape[1]
+    if idx.device.type != "cuda" or nbins > _ONEHOT_MAX_BINS or idx.numel() == 0:
+        out = torch.zeros((nbins, C), dtype=dtype, device=v.device).index_add_(0, idx, v)
+        return out[:, 0] if one_d else out
+    out = torch.zeros((nbins, C), dtype=dtype, device=v.device)
+    chunk = max(1 << 16, _ONEHOT_BLOCK // max(nbins, 1))
+    ar = torch.arange(nbins, device=idx.device).view(1, -1)
+    for a in range(0, idx.numel(), chunk):
+        oh = (idx[a:a + chunk].view(-1, 1) == ar).to(dtype)      # [c, nbins]
+        out.addmm_(oh.T, v[a:a + chunk])
+    return out[:, 0] if one_d else out

@@ -683,10 +683,10 @@ class H2OEstimator:
         w = self._spec.w_tensor(frame)
         w = torch.ones_like(act) if w is None else w.to(torch.float64)
         w = torch.where(ok, w, torch.zeros_like(w))
-        st = torch.zeros((3, L + 1), dtype=torch.float64, device=act.device)
-        st[0].index_add_(0, level, w * torch.where(ok, pr, torch.zeros_like(pr)))
-        st[1].index_add_(0, level, w * torch.where(ok, act, torch.zeros_like(act)))
-        st[2].index_add_(0, level, w)
+        from ..core.groupsum import group_sum
+        st = group_sum(level, torch.stack([w * torch.where(ok, pr, torch.zeros_like(pr)),
+                                           w * torch.where(ok, act, torch.zeros_like(act)), w], 1),
+                       L + 1).T.contiguous()
         coll.allreduce_(st)
         den = torch.where(st[2] > 0, st[2], torch.ones_like(st[2]))
         res = (st[:2] / den).cpu().numpy()

@@ -23,6 +23,7 @@ from ..core.vec import T_ENUM, T_INT, T_REAL, Vec
 from ..ops import linalg_ops
 from ..parallel import cloud
 from ..parallel import collectives as coll
+from ..core.groupsum import group_sum
 from . import metrics as mm
 from .base import H2OEstimator
 from .datainfo import DataInfo
@@ -227,19 +228,17 @@ class H2ONaiveBayesEstimator(H2OEstimator):
             if v.type == T_ENUM:
                 L = len(v.domain)
                 m = ok & (v.data >= 0)
-                t = torch.zeros((K, L), dtype=torch.float64, device=y.device)
-                t.index_put_((y[m], v.data[m].long()), torch.ones(int(m.sum()), dtype=torch.float64, device=y.device),
-                             accumulate=True)
+                # (class, level) counts: integer bincount over the combined key
+                t = torch.bincount(y[m] * L + v.data[m].long(), minlength=K * L).to(torch.float64).view(K, L)
                 coll.allreduce_(t)
                 prob = (t + lap) / (t.sum(1, keepdim=True) + L * lap)
                 self._tables[c] = ("cat", prob, list(v.domain))
             else:
                 x = v.as_float(torch.float64)
                 m = ok & ~torch.isnan(x)
-                s1 = torch.zeros(K, dtype=torch.float64, device=y.device).index_add_(0, y[m], x[m])
-                s2 = torch.zeros(K, dtype=torch.float64, device=y.device).index_add_(0, y[m], x[m] ** 2)
-                n = torch.zeros(K, dtype=torch.float64, device=y.device).index_add_(0, y[m], torch.ones_like(x[m]))
-                st = torch.stack([s1, s2, n])
+                xm = x[m]
+                # per-class moments as one one-hot GEMM (no contended f64 atomics)
+                st = group_sum(y[m], torch.stack([xm, xm * xm, torch.ones_like(xm)], 1), K).T.contiguous()
                 coll.allreduce_(st)
                 s1, s2, n = st
                 mean = s1 / n.clamp_min(1)

@@ -404,8 +404,9 @@ def clustering_metrics(X, centers, assign, w=None):
     w = torch.ones(X.shape[0], dtype=torch.float64, device=X.device) if w is None else w.to(torch.float64)
     d = ((X - C[assign]) ** 2).sum(1) * w
     k = C.shape[0]
-    within = torch.zeros(k, dtype=torch.float64, device=X.device).index_add_(0, assign, d)
-    sizes = torch.zeros(k, dtype=torch.float64, device=X.device).index_add_(0, assign, w)
+    from ..core.groupsum import group_sum
+    ws = group_sum(assign, torch.stack([d, w], 1), k)
+    within, sizes = ws[:, 0].contiguous(), ws[:, 1].contiguous()
     sw = w.sum()
     mean = (X * w.view(-1, 1)).sum(0)
     stats = torch.cat([within, sizes, sw.view(1), mean])

@@ -109,9 +109,9 @@ class GBMDriver:
             self.init_f = [f0]
         else:
             # multinomial: reference initialises f_k = log(prior_k) - mean
-            cnt = torch.zeros(self.K, dtype=torch.float64, device=dev)
             ok = self.ycode >= 0
-            cnt.index_add_(0, self.ycode[ok], self.base_w[ok].to(torch.float64))
+            from ...core.groupsum import group_sum
+            cnt = group_sum(self.ycode[ok], self.base_w[ok], self.K)
             coll.allreduce_(cnt)
             pri = (cnt / cnt.sum()).clamp_min(1e-10)
             lp = torch.log(pri)

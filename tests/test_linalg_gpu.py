@@ -199,3 +199,18 @@ def test_gram_aug_bf3_matches_fp64():
     diag = R.diagonal().sqrt()
     rel = (G[: P + 2, : P + 2] - R).abs() / (diag.view(-1, 1) * diag.view(1, -1))
     assert rel.max().item() < 5e-5
+
+
+@pytest.mark.gpu
+def test_group_sum_matches_index_add():
+    """One-hot GEMM grouped sums (core/groupsum.py) equal the f64 index_add_
+    reference for few bins, and the large-bin fallback is index_add_ itself."""
+    import torch
+    from h2o3_amd.core.groupsum import group_sum
+    g = torch.Generator(device="cuda").manual_seed(1)
+    for nb in (2, 7, 300, 5000):
+        idx = torch.randint(0, nb, (1_000_003,), generator=g, device="cuda")
+        v = torch.randn((1_000_003, 3), generator=g, device="cuda", dtype=torch.float64)
+        ref = torch.zeros((nb, 3), dtype=torch.float64, device="cuda").index_add_(0, idx, v)
+        torch.testing.assert_close(group_sum(idx, v, nb), ref, rtol=1e-10, atol=1e-9)
+        torch.testing.assert_close(group_sum(idx, v[:, 1], nb), ref[:, 1], rtol=1e-10, atol=1e-9)
