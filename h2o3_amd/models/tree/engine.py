@@ -100,10 +100,10 @@ class Tree:
         return self.left[i] < 0
 
     def leaves(self):
-        return [i for i in range(self.n_nodes) if self.left[i] < 0]
+        return np.nonzero(np.asarray(self.left, dtype=np.int64) < 0)[0].tolist()
 
     def max_depth(self):
-        return int(max(self.depth)) if len(self.depth) else 0
+        return int(np.max(np.asarray(self.depth))) if len(self.depth) else 0
 
     def to_arrays(self):
         return {k: np.asarray(getattr(self, k)) for k in ("feat", "left", "right", "thr", "na_left", "is_cat",

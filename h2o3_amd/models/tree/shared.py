@@ -29,6 +29,21 @@ def _ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
 
 
+def forest_varimp(forest, names):
+    """Sum of positive split gains per feature over every split node
+    (vectorized over each tree's node arrays)."""
+    acc = np.zeros(len(names), dtype=np.float64)
+    for t in forest.trees:
+        l_ = np.asarray(t.left, dtype=np.int64)
+        if l_.size == 0:
+            continue
+        sp = l_ >= 0
+        f_ = np.asarray(t.feat, dtype=np.int64)[sp]
+        g_ = np.maximum(np.asarray(t.gain, dtype=np.float64)[sp], 0.0)
+        np.add.at(acc, f_, g_)
+    return {n: float(acc[j]) for j, n in enumerate(names)}
+
+
 class Forest:
     """Flattened struct-of-arrays forest for the scoring kernel."""
 
@@ -50,37 +65,51 @@ class Forest:
         key = (str(device), len(trees))
         if self._packed is not None and self._packed[0] == key:
             return self._packed[1]
+        # vectorized per tree (trees of deep DRF models have ~10^5 nodes; a
+        # per-node Python loop here cost seconds per scoring)
         feat, thr, left, right, nal, coff, clen, val, roots, bits = [], [], [], [], [], [], [], [], [], []
         base = 0
         nb = 0
         for t in trees:
+            n = t.n_nodes
             roots.append(base)
-            for i in range(t.n_nodes):
-                feat.append(max(t.feat[i], 0))
-                thr.append(t.thr[i] if not math.isnan(t.thr[i]) else 0.0)
-                left.append(t.left[i] + base if t.left[i] >= 0 else -1)
-                right.append(t.right[i] + base if t.right[i] >= 0 else -1)
-                nal.append(1 if t.na_left[i] else 0)
-                if t.is_cat[i] and t.cat_left[i] is not None:
-                    coff.append(nb)
-                    clen.append(len(t.cat_left[i]))
-                    bits.extend(int(b) for b in t.cat_left[i])
-                    nb += len(t.cat_left[i])
-                else:
-                    coff.append(-1)
-                    clen.append(0)
-                val.append(t.value[i])
-            base += t.n_nodes
+            f_ = np.asarray(t.feat, dtype=np.int64)
+            th = np.asarray(t.thr, dtype=np.float64)
+            l_ = np.asarray(t.left, dtype=np.int64)
+            r_ = np.asarray(t.right, dtype=np.int64)
+            feat.append(np.maximum(f_, 0))
+            thr.append(np.where(np.isnan(th), 0.0, th))
+            left.append(np.where(l_ >= 0, l_ + base, -1))
+            right.append(np.where(r_ >= 0, r_ + base, -1))
+            nal.append(np.asarray(t.na_left, dtype=bool).astype(np.uint8))
+            co = np.full(n, -1, dtype=np.int64)
+            cl = np.zeros(n, dtype=np.int64)
+            for i in np.nonzero(np.asarray(t.is_cat, dtype=bool))[0]:
+                m = t.cat_left[i]
+                if m is None:
+                    continue
+                mb = np.asarray(m).astype(np.uint8).reshape(-1)
+                co[i] = nb
+                cl[i] = mb.size
+                bits.append(mb)
+                nb += mb.size
+            coff.append(co)
+            clen.append(cl)
+            val.append(np.asarray(t.value, dtype=np.float64))
+            base += n
+
+        def cat(parts, dt):
+            return np.concatenate(parts).astype(dt) if parts else np.zeros(0, dtype=dt)
         d = device
-        P = {"feat": torch.tensor(feat, dtype=torch.int32, device=d),
-             "thr": torch.tensor(thr, dtype=torch.float32, device=d),
-             "left": torch.tensor(left, dtype=torch.int32, device=d),
-             "right": torch.tensor(right, dtype=torch.int32, device=d),
-             "na_left": torch.tensor(nal, dtype=torch.uint8, device=d),
-             "cat_off": torch.tensor(coff, dtype=torch.int32, device=d),
-             "cat_len": torch.tensor(clen, dtype=torch.int32, device=d),
-             "cat_bits": torch.tensor(bits or [0], dtype=torch.uint8, device=d),
-             "value": torch.tensor(val, dtype=torch.float32, device=d),
+        P = {"feat": torch.as_tensor(cat(feat, np.int32), device=d),
+             "thr": torch.as_tensor(cat(thr, np.float32), device=d),
+             "left": torch.as_tensor(cat(left, np.int32), device=d),
+             "right": torch.as_tensor(cat(right, np.int32), device=d),
+             "na_left": torch.as_tensor(cat(nal, np.uint8), device=d),
+             "cat_off": torch.as_tensor(cat(coff, np.int32), device=d),
+             "cat_len": torch.as_tensor(cat(clen, np.int32), device=d),
+             "cat_bits": torch.as_tensor(cat(bits, np.uint8) if bits else np.zeros(1, dtype=np.uint8), device=d),
+             "value": torch.as_tensor(cat(val, np.float32), device=d),
              "roots": torch.tensor(roots, dtype=torch.int32, device=d),
              "tclass": torch.tensor(self.tclass[: len(trees)], dtype=torch.int32, device=d),
              "T": len(trees)}
@@ -213,12 +242,7 @@ class SharedTreeEstimator(H2OEstimator):
         return torch.stack(cols, 0).contiguous()
 
     def _varimp_from_forest(self, forest: Forest, names):
-        vi = {n: 0.0 for n in names}
-        for t in forest.trees:
-            for i in range(t.n_nodes):
-                if t.left[i] >= 0:
-                    vi[names[t.feat[i]]] += max(t.gain[i], 0.0)
-        return vi
+        return forest_varimp(forest, names)
 
     def predict_leaf_node_assignment(self, test_data, type="Path"):
         X = self._score_matrix(test_data)

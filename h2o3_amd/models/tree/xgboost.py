@@ -219,12 +219,8 @@ class H2OXGBoostEstimator(SharedTreeEstimator):
                         tt.value[i] *= wgt
         self._forest = forest
         self._train_f = f
-        vi = {n: 0.0 for n in spec.x}
-        for t in forest.trees:
-            for i in range(t.n_nodes):
-                if t.left[i] >= 0:
-                    vi[spec.x[t.feat[i]]] += max(t.gain[i], 0.0)
-        self._output["variable_importances"] = vi
+        from .shared import forest_varimp
+        self._output["variable_importances"] = forest_varimp(forest, spec.x)
         self._output["model_summary"] = {"number_of_trees": len(forest) // K, "booster": booster}
 
     def _raw_from_f(self, f):
