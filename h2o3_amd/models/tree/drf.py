@@ -231,8 +231,11 @@ class DRFDriver:
                                                       unit_w=self._unit_w)
             tot = tot.numpy() if isinstance(tot, torch.Tensor) else np.asarray(tot)
             vals = np.where(tot[:, 0] > 0, tot[:, 1] / np.where(tot[:, 0] > 0, tot[:, 0], 1), 0.0)
-            for li, node in enumerate(leaves):
-                tree.value[node] = float(vals[li])
+            if isinstance(tree.value, np.ndarray):
+                tree.value[np.asarray(leaves, dtype=np.int64)] = vals[:len(leaves)]
+            else:
+                for li, node in enumerate(leaves):
+                    tree.value[node] = float(vals[li])
             vt = torch.tensor(vals, dtype=torch.float32, device=dev)
             self.oob_sum[:, k] += torch.where(oob, vt[nid.long()], torch.zeros(N, device=dev))
             self.forest.add(tree, k)
