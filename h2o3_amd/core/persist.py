@@ -142,10 +142,11 @@ def _s3_list(bucket, prefix):
         token = root.findtext(ns + "NextContinuationToken")
 
 
-def _s3_get(u) -> list:
+def _s3_get(u, raw=False) -> list:
     bucket, key = u.netloc, u.path.lstrip("/")
     keys = _s3_list(bucket, key) if (not key or key.endswith("/")) else [key]
-    return [decompress(_download(_s3_request("GET", _s3_url(bucket, k)), os.path.splitext(k)[1])) for k in keys]
+    dec = (lambda x: x) if raw else decompress
+    return [dec(_download(_s3_request("GET", _s3_url(bucket, k)), os.path.splitext(k)[1])) for k in keys]
 
 
 # ------------------------------------------------------------------------ GCS
@@ -161,7 +162,7 @@ def _gcs_headers():
     return {"Authorization": f"Bearer {tok}"} if tok else {}
 
 
-def _gcs_get(u) -> list:
+def _gcs_get(u, raw=False) -> list:
     bucket, obj = u.netloc, u.path.lstrip("/")
     names = [obj]
     if not obj or obj.endswith("/"):
@@ -169,9 +170,10 @@ def _gcs_get(u) -> list:
         with urllib.request.urlopen(urllib.request.Request(url, headers=_gcs_headers())) as r:
             names = [it["name"] for it in json.loads(r.read()).get("items", []) if not it["name"].endswith("/")]
     out = []
+    dec = (lambda x: x) if raw else decompress
     for n in names:
         url = f"{_gcs_base()}/storage/v1/b/{bucket}/o/{urllib.parse.quote(n, safe='')}?alt=media"
-        out.append(decompress(_download(urllib.request.Request(url, headers=_gcs_headers()),
+        out.append(dec(_download(urllib.request.Request(url, headers=_gcs_headers()),
                                         os.path.splitext(n)[1])))
     return out
 
@@ -184,7 +186,7 @@ def _webhdfs_url(u, path, op, extra=""):
     return f"http://{u.hostname}:{port}/webhdfs/v1{urllib.parse.quote(path, safe='/-_.~')}?{q}"
 
 
-def _hdfs_get(u) -> list:
+def _hdfs_get(u, raw=False) -> list:
     with urllib.request.urlopen(_webhdfs_url(u, u.path, "GETFILESTATUS")) as r:
         st = json.loads(r.read())["FileStatus"]
     paths = [u.path]
@@ -193,36 +195,63 @@ def _hdfs_get(u) -> list:
             ents = json.loads(r.read())["FileStatuses"]["FileStatus"]
         paths = [u.path.rstrip("/") + "/" + e["pathSuffix"] for e in ents if e.get("type") == "FILE"]
     # OPEN answers with a 307 redirect to a data node; urllib follows it
-    return [decompress(_download(_webhdfs_url(u, p, "OPEN"), os.path.splitext(p)[1])) for p in paths]
+    dec = (lambda x: x) if raw else decompress
+    return [dec(_download(_webhdfs_url(u, p, "OPEN"), os.path.splitext(p)[1])) for p in paths]
 
 
 # -------------------------------------------------------------------- public
-def resolve_all(uri: str) -> list:
+def resolve_all(uri: str, raw: bool = False) -> list:
     """Local paths for a URI: one per object (prefix / directory URIs of the
-    object stores expand to every file under them)."""
+    object stores expand to every file under them).  raw=True keeps the
+    downloaded bytes as they are (binary models whose name ends in .zip / .gz
+    are not data archives)."""
     u = urllib.parse.urlparse(uri)
     if u.scheme in ("s3", "s3a", "s3n"):
-        return _s3_get(u)
+        return _s3_get(u, raw)
     if u.scheme == "gs":
-        return _gcs_get(u)
+        return _gcs_get(u, raw)
     if u.scheme in ("hdfs", "maprfs", "webhdfs"):
-        return _hdfs_get(u)
-    return [resolve(uri)]
+        return _hdfs_get(u, raw)
+    return [resolve(uri, raw)]
 
 
-def resolve(uri: str) -> str:
-    """Local path for a URI (downloading / decompressing as needed)."""
+def resolve(uri: str, raw: bool = False) -> str:
+    """Local path for a URI (downloading, and decompressing unless raw)."""
     u = urllib.parse.urlparse(uri)
+    dec = (lambda x: x) if raw else decompress
     if u.scheme in ("http", "https"):
-        return decompress(_download(uri, os.path.splitext(u.path)[1]))
+        return dec(_download(uri, os.path.splitext(u.path)[1]))
     if u.scheme in ("s3", "s3a", "s3n", "gs", "hdfs", "maprfs", "webhdfs"):
-        paths = resolve_all(uri)
+        paths = resolve_all(uri, raw)
         if len(paths) != 1:
             raise ValueError(f"{uri} names {len(paths)} objects; import it as a folder")
         return paths[0]
     if u.scheme == "file":
         uri = u.path
-    return decompress(uri)
+    return dec(uri)
+
+
+def exists(uri: str) -> bool:
+    """Whether an object-store URI names an existing object (S3 HEAD, GCS
+    object metadata, WebHDFS GETFILESTATUS); used to honour force=False."""
+    u = urllib.parse.urlparse(uri)
+    if u.scheme in ("s3", "s3a", "s3n"):
+        req = _s3_request("HEAD", _s3_url(u.netloc, u.path.lstrip("/")))
+    elif u.scheme == "gs":
+        req = urllib.request.Request(f"{_gcs_base()}/storage/v1/b/{u.netloc}/o/"
+                                     f"{urllib.parse.quote(u.path.lstrip('/'), safe='')}", headers=_gcs_headers())
+    elif u.scheme in ("hdfs", "maprfs", "webhdfs"):
+        req = _webhdfs_url(u, u.path, "GETFILESTATUS")
+    else:
+        return os.path.exists(u.path if u.scheme == "file" else uri)
+    try:
+        with urllib.request.urlopen(req) as r:
+            r.read()
+        return True
+    except urllib.error.HTTPError as e:
+        if e.code == 404:
+            return False
+        raise
 
 
 def upload(local_path: str, uri: str) -> None:

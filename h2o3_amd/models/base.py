@@ -94,8 +94,10 @@ class ScoreSchedule:
     with score_each_iteration and at the final tree; otherwise time-based --
     every iteration during the first initial_score_interval ms (4 s), then at
     most every score_interval ms (4 s) and only while scoring stays under a
-    10% duty cycle.  time_based=False keeps scoring to the final iteration
-    (no early stopping asked for: nothing consumes the intermediate history)."""
+    10% duty cycle -- with or without early stopping, as in the reference.
+    Callers pass final=True at the last iteration and on a max_runtime_secs
+    stop, so the history always ends at the returned model.
+    time_based=False (not used by the tree builders) scores only at final."""
 
     def __init__(self, parms, time_based=True):
         self.interval = int(parms.get("score_tree_interval") or 0)

@@ -446,15 +446,29 @@ class H2ODeepLearningEstimator(H2OEstimator):
         cur = torch.cuda.current_stream()
         side = torch.cuda.Stream()
         side.wait_stream(cur)
+        # The warm-up steps only allocate the optimizer state and let the GEMM
+        # library pick its algorithms: weights, biases, optimizer state and the
+        # dropout seed are snapshotted first and restored after capture, so the
+        # model trains on exactly the batches the caller replays (and the
+        # sample counters are untouched).
+        saved = [(L.W.clone(), L.b.clone(), {k: v.clone() for k, v in L.state.items() if v is not None})
+                 for L in self._layers]
+        seed0 = gs["seed"].clone()
         with torch.cuda.stream(side):
-            for i in range(2):      # warm-up steps create the optimizer state and pick GEMM algos
+            for i in range(2):
                 gs["idx"].copy_(torch.arange(i * bs, (i + 1) * bs, device=dev) % X.shape[0])
                 body()
-                self._processed += bs
         cur.wait_stream(side)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             body()
+        for L, (Wb, bb, st) in zip(self._layers, saved):
+            L.W.copy_(Wb)
+            L.b.copy_(bb)
+            for k, v in L.state.items():
+                if v is not None:
+                    v.copy_(st[k]) if k in st else v.zero_()   # state created by the warm-up starts at 0
+        gs["seed"].copy_(seed0)
         gs["g"] = g
         return gs
 

@@ -29,13 +29,16 @@ def _metrics_dict(m):
 
 
 def save_model(model, path="", force=False, filename=None):
-    from ..core.persist import is_remote, upload
+    from ..core.persist import exists, is_remote, upload
     if is_remote(path):
-        # object store: write locally, then upload (PersistManager.create)
+        # object store: write locally, then upload (PersistManager.create);
+        # an existing object is only replaced with force=True, as on disk
         import tempfile
+        dest = path.rstrip("/") + "/" + (filename or model.model_id)
+        if not force and exists(dest):
+            raise FileExistsError(dest)
         with tempfile.TemporaryDirectory() as td:
             local = save_model(model, td, force=True, filename=filename)
-            dest = path.rstrip("/") + "/" + os.path.basename(local)
             upload(local, dest)
         return dest
     from ..mojo.writer import build_mojo
@@ -59,7 +62,8 @@ def save_model(model, path="", force=False, filename=None):
 def load_model(path):
     from ..core.persist import is_remote, resolve
     if is_remote(path):
-        path = resolve(path)
+        # the saved model IS a zip: download it as is (no archive unpacking)
+        path = resolve(path, raw=True)
     from . import metrics as mm
     from .generic import H2OGenericEstimator
     from ..core import dkv

@@ -52,20 +52,20 @@ class H2ORandomForestEstimator(SharedTreeEstimator):
         t0 = time.time()
         max_rt = float(p.get("max_runtime_secs") or 0)
         self._scoring_history = []
-        interval = int(p.get("score_tree_interval") or 0)
         stop_rounds = int(p.get("stopping_rounds") or 0)
         metric_name = self._stopping_metric(spec)
         history = []
-        sched = ScoreSchedule(p, time_based=stop_rounds > 0)
+        sched = ScoreSchedule(p)
         for t in range(ntrees):
             drv.step()
-            if sched.due(t + 1, final=t + 1 == ntrees):
+            # a max_runtime_secs stop scores the last tree into the history too
+            timed_out = max_rt > 0 and time.time() - t0 > max_rt
+            if sched.due(t + 1, final=t + 1 == ntrees or timed_out):
                 entry = {"number_of_trees": t + 1}
-                if stop_rounds or interval or sched.each:
-                    sched.started()
-                    self._forest = drv.forest
-                    self._score_entry(entry, spec, drv.oob_sum, drv.oob_cnt)
-                    sched.ended()
+                sched.started()
+                self._forest = drv.forest
+                self._score_entry(entry, spec, drv.oob_sum, drv.oob_cnt)
+                sched.ended()
                 self._scoring_history.append(entry)
                 if stop_rounds:
                     key = ("validation_" if spec.valid is not None else "training_") + \
@@ -74,7 +74,7 @@ class H2ORandomForestEstimator(SharedTreeEstimator):
                     if ScoreKeeper.stop_early(history, stop_rounds, float(p.get("stopping_tolerance", 0.001)),
                                               metric_name in _LESS_IS_BETTER):
                         break
-            if max_rt > 0 and time.time() - t0 > max_rt:
+            if timed_out:
                 break
         forest, K = drv.forest, drv.K
         self._forest = forest

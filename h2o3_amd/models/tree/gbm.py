@@ -457,10 +457,12 @@ class H2OGradientBoostingEstimator(SharedTreeEstimator):
         history = []
         max_rt = float(p.get("max_runtime_secs") or 0)
         self._scoring_history = []
-        sched = ScoreSchedule(p, time_based=stop_rounds > 0)
+        sched = ScoreSchedule(p)
         while drv.iter < ntrees:
             drv.step()
-            if sched.due(drv.iter, final=drv.iter == ntrees):
+            # a max_runtime_secs stop scores the last tree into the history too
+            timed_out = max_rt > 0 and time.time() - t0 > max_rt
+            if sched.due(drv.iter, final=drv.iter == ntrees or timed_out):
                 sched.started()
                 entry = self._score_iteration(drv, spec)
                 sched.ended()
@@ -472,7 +474,7 @@ class H2OGradientBoostingEstimator(SharedTreeEstimator):
                     if ScoreKeeper.stop_early(history, stop_rounds, float(p["stopping_tolerance"]),
                                               metric_name in _LESS_IS_BETTER):
                         break
-            if max_rt > 0 and time.time() - t0 > max_rt:
+            if timed_out:
                 break
         self._forest = drv.forest
         self._init_f = drv.init_f

@@ -131,7 +131,7 @@ class H2OXGBoostEstimator(SharedTreeEstimator):
         self._scoring_history = []
         max_rt = float(p.get("max_runtime_secs") or 0)
         t0 = time.time()
-        sched = ScoreSchedule(p, time_based=stop_rounds > 0)
+        sched = ScoreSchedule(p)
         for it in range(ntrees):
             wt = base_w
             if sr < 1.0:
@@ -194,7 +194,9 @@ class H2OXGBoostEstimator(SharedTreeEstimator):
             else:
                 f = f + torch.stack(deltas, 1)
             n_it = it + 1
-            if sched.due(n_it, final=n_it == ntrees):
+            # a max_runtime_secs stop scores the last iteration into the history too
+            timed_out = max_rt > 0 and time.time() - t0 > max_rt
+            if sched.due(n_it, final=n_it == ntrees or timed_out):
                 entry = {"number_of_trees": n_it}
                 self._forest = forest
                 sched.started()
@@ -208,7 +210,7 @@ class H2OXGBoostEstimator(SharedTreeEstimator):
                     if ScoreKeeper.stop_early(history, stop_rounds, float(p.get("stopping_tolerance", 0.001)),
                                               metric_name in _LESS_IS_BETTER):
                         break
-            if max_rt > 0 and time.time() - t0 > max_rt:
+            if timed_out:
                 break
         if dart:
             # bake DART weights into leaf values

@@ -121,7 +121,7 @@ def lloyd_pass(X, C, w=None, assign=None, accumulate=True, dmin=None, use_native
     part = None
     stride = int(lib.h2o_kmeans_part_stride(k, P))
     if accumulate:
-        part = torch.empty((n_groups, stride), dtype=torch.float32, device=X.device)
+        part = torch.empty((n_groups, stride), dtype=torch.float64, device=X.device)
     stream = _cv(torch.cuda.current_stream().cuda_stream)
     rc = lib.h2o_kmeans_lloyd(_ptr(X), _ptr(wt), N, P, _ptr(C32), _ptr(cn), k, _ptr(assign), _ptr(assign), _ptr(dmin),
                               _ptr(part), n_groups, 1 if accumulate else 0, fx, stream)

@@ -27,14 +27,19 @@
 //      measured 5x slower than the rest of the pass; one-hot MFMA and
 //      per-center register selects were 2-3x slower than this); weights
 //      and within-SS (|x|^2 + d_min) per cluster by LDS atomics (2 per row).
-// Each workgroup writes one f32 partial; h2o_kmeans_reduce folds the
-// partials in f64.  No global atomics.
+// Each workgroup writes one f64 partial (the fixed-point sums converted
+// straight to f64; the f32 LDS weights / within-SS are folded into f64
+// registers after every 64-row tile, the f32 private-copy sums into the f64
+// partial every KM_FOLD tiles, so no f32 sum ever spans more than a few
+// thousand rows); h2o_kmeans_reduce adds the partials in f64.  No global
+// atomics.  Reference accumulates in double (KMeans.java LloydsIterationTask).
 #include "common.h"
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 #define KM_ROWS 64
 #define KM_THREADS 256
+#define KM_FOLD 16        // tiles between folds of the f32 private sums into the f64 partial
 
 // partial layout per workgroup: [k*P sums][k weights][k withinss][1 changed]
 __host__ __device__ inline long long km_part_stride(int k, int P) { return (long long)k * P + 2LL * k + 1; }
@@ -43,7 +48,7 @@ template <int KT, int MAXV, bool ACC>
 __global__ __launch_bounds__(KM_THREADS) void kmeans_lloyd_kernel(
     const float* __restrict__ X, const float* __restrict__ w, long long N, int P, const float* __restrict__ Cin,
     const float* __restrict__ cn, int k, int* assign, const int* assign_old,
-    float* __restrict__ dmin_out, float* __restrict__ part, int vrg_in, float fx_scale, int dbg) {
+    float* __restrict__ dmin_out, double* __restrict__ part, int vrg_in, float fx_scale, int dbg) {
   extern __shared__ __align__(16) float lds[];
   const int P16 = (P + 15) & ~15;            // k-range padded so each lane group gets a float4 multiple
   const int S = P16 + 4;                     // LDS row stride (dwords)
@@ -68,6 +73,9 @@ __global__ __launch_bounds__(KM_THREADS) void kmeans_lloyd_kernel(
   int* asg = (int*)(dmn + KM_ROWS);          // [64]
   float* wts = (float*)(asg + KM_ROWS);      // [64] row weights of the tile
   __shared__ int changed_s;
+  double* o = ACC ? part + (long long)blockIdx.x * km_part_stride(k, P) : nullptr;
+  double wacc[2] = {0.0, 0.0};               // f64 weights / within-SS of entries tid, tid + 256 of [Swt | Sss]
+  int nfold = 0;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -86,6 +94,8 @@ __global__ __launch_bounds__(KM_THREADS) void kmeans_lloyd_kernel(
     for (int e = tid; e < sum_f + 2 * k; e += KM_THREADS) Ssum[e] = 0.f;   // Ssum, Swt, Sss contiguous
   }
   if (tid == 0) changed_s = 0;
+  if (ACC && vrg > 0)
+    for (int e = tid; e < k * P; e += KM_THREADS) o[e] = 0.0;   // folded f32 sums land here
   // X tile columns P..P16 stay zero (the staging below writes only c < P)
   for (int e = tid; e < KM_ROWS * S; e += KM_THREADS) Xs[e] = 0.f;
 
@@ -264,36 +274,56 @@ __global__ __launch_bounds__(KM_THREADS) void kmeans_lloyd_kernel(
       }
     }
     __syncthreads();
+    if (ACC) {
+      // weights / within-SS of this tile: f32 LDS -> f64 registers, LDS re-zeroed
+      // (the next tile's row stats are written only after the next barrier)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int e = tid + h * KM_THREADS;
+        if (e < 2 * k) { wacc[h] += (double)Swt[e]; Swt[e] = 0.f; }
+      }
+      if (vrg > 0 && ++nfold == KM_FOLD) {
+        nfold = 0;
+        for (int e = tid; e < k * P; e += KM_THREADS) {
+          float sv = 0.f;
+          for (int h = 0; h < vrg; ++h) { sv += Ssum[h * k * P + e]; Ssum[h * k * P + e] = 0.f; }
+          o[e] += (double)sv;
+        }
+      }
+    }
   }
   if (out_r >= 0) {
     if (assign) assign[out_r] = out_a;
     if (dmin_out) dmin_out[out_r] = out_d;
   }
   if (ACC) {
-    float* o = part + (long long)blockIdx.x * km_part_stride(k, P);
     if (vrg == 0) {
       const unsigned long long* S64 = reinterpret_cast<const unsigned long long*>(Ssum);
       const double inv = 1.0 / (double)fx_scale;
-      for (int e = tid; e < k * P; e += KM_THREADS) o[e] = (float)((double)(long long)S64[e] * inv);
+      for (int e = tid; e < k * P; e += KM_THREADS) o[e] = (double)(long long)S64[e] * inv;
     } else {
       for (int e = tid; e < k * P; e += KM_THREADS) {
         float sv = 0.f;
         for (int h = 0; h < vrg; ++h) sv += Ssum[h * k * P + e];
-        o[e] = sv;
+        o[e] += (double)sv;
       }
     }
-    for (int e = tid; e < 2 * k; e += KM_THREADS) o[k * P + e] = Swt[e];   // Swt, Sss contiguous
-    if (tid == 0) o[k * P + 2 * k] = (float)changed_s;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int e = tid + h * KM_THREADS;
+      if (e < 2 * k) o[k * P + e] = wacc[h];   // Swt, Sss contiguous
+    }
+    if (tid == 0) o[k * P + 2 * k] = (double)changed_s;
   }
 }
 
 // out[e] = sum_g part[g][e] in f64 (e over the whole partial record)
-__global__ __launch_bounds__(256) void kmeans_reduce_kernel(const float* __restrict__ part, int G, long long stride,
+__global__ __launch_bounds__(256) void kmeans_reduce_kernel(const double* __restrict__ part, int G, long long stride,
                                                             double* __restrict__ out) {
   const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
   if (e >= stride) return;
   double s = 0.0;
-  for (int gi = 0; gi < G; ++gi) s += (double)part[(long long)gi * stride + e];
+  for (int gi = 0; gi < G; ++gi) s += part[(long long)gi * stride + e];
   out[e] = s;
 }
 
@@ -325,7 +355,7 @@ static int g_km_dbg = 0;   // microbenchmark phase-skip flags (h2o_kmeans_set_de
 
 template <int KT, int MAXV, bool ACC>
 static int km_launch2(const float* X, const float* w, long long N, int P, const float* C, const float* cn, int k,
-                      int* assign, const int* assign_old, float* dmin, float* part, int G, float fx, hipStream_t s) {
+                      int* assign, const int* assign_old, float* dmin, double* part, int G, float fx, hipStream_t s) {
   const int vrg = km_vrg(k, P, ACC, fx);
   const size_t lds = km_lds_bytes(KT, k, P, ACC, vrg);
   auto kern = kmeans_lloyd_kernel<KT, MAXV, ACC>;
@@ -338,7 +368,7 @@ static int km_launch2(const float* X, const float* w, long long N, int P, const 
 
 template <int KT>
 static int km_launch(const float* X, const float* w, long long N, int P, const float* C, const float* cn, int k,
-                     int* assign, const int* assign_old, float* dmin, float* part, int G, int acc, float fx,
+                     int* assign, const int* assign_old, float* dmin, double* part, int G, int acc, float fx,
                      hipStream_t s) {
   // MAXV = float4 per thread per 64-row tile = ceil(P / 16)
   if (P <= 64) return acc ? km_launch2<KT, 4, true>(X, w, N, P, C, cn, k, assign, assign_old, dmin, part, G, fx, s)
@@ -404,7 +434,7 @@ int h2o_kmeans_resident_per_cu(int k, int P, int acc, float fx_scale) {
 // [G, km_part_stride] (then h2o_kmeans_reduce); acc=0: assignment only.
 // assign / assign_old / dmin / w may be null.  Returns a hipError_t.
 int h2o_kmeans_lloyd(const float* X, const float* w, long long N, int P, const float* C, const float* cn, int k,
-                     int* assign, const int* assign_old, float* dmin, float* part, int G, int acc, float fx_scale,
+                     int* assign, const int* assign_old, float* dmin, double* part, int G, int acc, float fx_scale,
                      hipStream_t s) {
   if (N <= 0) return 0;
   if (P <= 0 || P > 256 || (P & 3) || k <= 0 || k > 256 || G <= 0) return (int)hipErrorInvalidValue;
@@ -418,7 +448,7 @@ int h2o_kmeans_lloyd(const float* X, const float* w, long long N, int P, const f
   return km_launch<16>(X, w, N, P, C, cn, k, assign, assign_old, dmin, part, G, acc, fx_scale, s);
 }
 
-int h2o_kmeans_reduce(const float* part, int G, long long stride, double* out, hipStream_t s) {
+int h2o_kmeans_reduce(const double* part, int G, long long stride, double* out, hipStream_t s) {
   if (G <= 0 || stride <= 0) return 0;
   const long long nb = (stride + 255) / 256;
   hipLaunchKernelGGL(kmeans_reduce_kernel, dim3((unsigned)nb), dim3(256), 0, s, part, G, stride, out);

@@ -1,0 +1,73 @@
+"""Worker for tests/test_distributed_gpu.py: one rank of a gloo cloud whose
+ranks all share cuda:0 (RCCL refuses two ranks on one device, gloo moves the
+GPU tensors through the host).  Every HIP kernel of the multi-rank tree path
+runs: feature reduce-scatter of level histograms, and for DRF with mtries the
+node-sharded pair path (pair histograms reduce-scattered by node, per-rank
+pair scoring / selection, all-gather of the per-node records), which only
+works when every rank draws the same column sample and pads the node count
+the same way.
+
+Dumps the grown trees (per node: split feature, threshold, NA direction,
+child ids) and predictions on the full frame to JSON (rank 0).
+"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def make_df(n=20000, F=40, seed=11):
+    import numpy as np
+    import pandas as pd
+    rng = np.random.default_rng(seed)
+    X = rng.normal(size=(n, F))
+    X[rng.random((n, F)) < 0.02] = np.nan
+    logit = 1.5 * np.nan_to_num(X[:, 0]) - np.nan_to_num(X[:, 1]) + 0.7 * np.nan_to_num(X[:, 2] * X[:, 3])
+    df = pd.DataFrame(X, columns=[f"x{i}" for i in range(F)])
+    df["c0"] = np.array(list("abcdefghij"))[rng.integers(0, 10, n)]
+    logit += np.where(df["c0"].isin(["a", "c", "f"]), 1.0, -0.5)
+    df["y"] = np.where(rng.random(n) < 1 / (1 + np.exp(-logit)), "yes", "no")
+    df["yr"] = logit + rng.normal(scale=0.3, size=n)
+    return df
+
+
+def _trees(m):
+    out = []
+    for t in m._forest.trees:
+        out.append({"feat": [int(v) for v in t.feat], "left": [int(v) for v in t.left],
+                    "thr": [float(v) for v in t.thr]})
+    return out
+
+
+def run(out_path):
+    import h2o3_amd as h2o
+    from h2o3_amd.estimators import H2OGradientBoostingEstimator, H2ORandomForestEstimator
+    h2o.init(verbose=False)
+    from h2o3_amd.parallel import cloud
+    assert cloud.device().type == "cuda" or os.environ.get("H2O3_WORKER_CPU_OK") == "1"
+    df = make_df()
+    fr = h2o.H2OFrame(df)
+    x = [c for c in df.columns if c not in ("y", "yr")]
+    res = {"world": cloud.world(), "backend": cloud.info()["backend"]}
+    # DRF, mtries = sqrt(41) -> 6 of 41 features per node: the row-direct pair path
+    drf = H2ORandomForestEstimator(ntrees=3, max_depth=8, seed=3, sample_rate=1.0, mtries=6, min_rows=20)
+    drf.train(x=x, y="yr", training_frame=fr)
+    res["drf_trees"] = _trees(drf)
+    res["drf_pred"] = drf.predict(fr).as_data_frame()["predict"].tolist()
+    # GBM binomial: level histograms reduce-scattered by feature
+    gbm = H2OGradientBoostingEstimator(ntrees=4, max_depth=6, seed=1, min_rows=20)
+    gbm.train(x=x, y="y", training_frame=fr)
+    res["gbm_trees"] = _trees(gbm)
+    res["gbm_logloss"] = gbm.logloss()
+    from h2o3_amd.ops import _native
+    res["native"] = _native.loaded_libs()
+    if cloud.rank() == 0:
+        with open(out_path, "w") as f:
+            json.dump(res, f)
+    cloud.barrier()
+    cloud.shutdown()
+
+
+if __name__ == "__main__":
+    run(sys.argv[1])

@@ -250,3 +250,33 @@ def test_kmeans_estimator_gpu_uses_kernel():
     m2 = H2OKMeansEstimator(k=6, seed=3, estimate_k=False)
     m2.train(training_frame=fr)
     assert len(m2.centers()) == 6 and sum(m2.size()) == len(df)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fx", [False, True])
+def test_lloyd_kernel_large_n_f64_accumulation(fx):
+    """20M rows (~80K rows per workgroup): the per-workgroup partials are f64
+    and no f32 running sum spans more than a few thousand rows, so the
+    cluster sums, weights and within-SS match an f64 reduction of the same
+    per-row quantities far below f32 resolution of the totals."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    N, P, k = 20_000_000, 8, 4
+    g = torch.Generator(device="cuda").manual_seed(5)
+    X = torch.randn((N, P), generator=g, device="cuda") + 3.0
+    C = X[:k].double()
+    w = torch.rand(N, generator=g, device="cuda")
+    a = torch.full((N,), -1, dtype=torch.int32, device="cuda")
+    dmin = torch.empty(N, dtype=torch.float32, device="cuda")
+    xa = cluster_ops.abs_bound(X, w) if fx else None
+    st = cluster_ops.lloyd_pass(X, C, w, a, dmin=dmin, xabs_max=xa)
+    torch.cuda.synchronize()
+    idx = a.long()
+    wd = w.double()
+    oh = torch.nn.functional.one_hot(idx, k).double() * wd.view(-1, 1)   # f64 GEMMs, no contended atomics
+    sums = oh.T @ X.double()
+    wts = oh.sum(0)
+    wss = oh.T @ dmin.double()
+    torch.testing.assert_close(st.sums, sums, rtol=1e-7, atol=0)
+    torch.testing.assert_close(st.weights, wts, rtol=1e-7, atol=0)
+    torch.testing.assert_close(st.withinss, wss, rtol=1e-6, atol=0)

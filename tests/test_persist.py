@@ -53,6 +53,8 @@ class _H(http.server.BaseHTTPRequestHandler):
             op = q.get("op")
             if op == "GETFILESTATUS":
                 is_dir = any(k[1].startswith(p.rstrip("/") + "/") for k in STORE if k[0] == "hdfs")
+                if not is_dir and ("hdfs", p) not in STORE:
+                    return self._send(404)
                 t = "DIRECTORY" if is_dir and ("hdfs", p) not in STORE else "FILE"
                 return self._send(200, json.dumps({"FileStatus": {"type": t}}).encode())
             if op == "LISTSTATUS":
@@ -75,6 +77,9 @@ class _H(http.server.BaseHTTPRequestHandler):
             bucket = parts[4]
             if len(parts) > 6 and q.get("alt") == "media":
                 return self._send(200, STORE[("gs", bucket + "/" + "/".join(parts[6:]))])
+            if len(parts) > 6:       # object metadata
+                key = ("gs", bucket + "/" + "/".join(parts[6:]))
+                return self._send(200, b"{}") if key in STORE else self._send(404)
             pre = q.get("prefix", "")
             items = [{"name": k[1].split("/", 1)[1]} for k in STORE
                      if k[0] == "gs" and k[1].startswith(bucket + "/" + pre)]
@@ -98,9 +103,17 @@ class _H(http.server.BaseHTTPRequestHandler):
                    "<IsTruncated>false</IsTruncated></ListBucketResult>")
             return self._send(200, xml.encode())
         data = STORE.get(("s3", bucket + "/" + key))
+        if self.command == "HEAD":
+            self.send_response(200 if data is not None else 404)
+            self.send_header("Content-Length", str(len(data or b"")))
+            self.end_headers()
+            return None
         return self._send(200, data) if data is not None else self._send(404)
 
     def do_GET(self):
+        self._route()
+
+    def do_HEAD(self):
         self._route()
 
     def do_PUT(self):
@@ -178,3 +191,30 @@ def test_gcs_and_hdfs_roundtrip(server, monkeypatch):
     m2 = h2o.load_model(dest)
     np.testing.assert_allclose(m2.predict(fr).as_data_frame()["predict"].values,
                                g.predict(fr).as_data_frame()["predict"].values, rtol=1e-5)
+
+
+def test_remote_model_named_zip_and_force(server, monkeypatch):
+    """A saved model whose object name ends in .zip is downloaded as is (it is
+    the model zip, not a data archive); saving over an existing object needs
+    force=True on every object store, as on a local disk."""
+    import h2o3_amd as h2o
+    from h2o3_amd.estimators import H2OGradientBoostingEstimator
+    h2o.init(verbose=False)
+    monkeypatch.setenv("AWS_ENDPOINT_URL", "http://" + server)
+    monkeypatch.setenv("AWS_ACCESS_KEY_ID", AK)
+    monkeypatch.setenv("AWS_SECRET_ACCESS_KEY", SK)
+    monkeypatch.setenv("AWS_REGION", "us-east-1")
+    monkeypatch.setenv("STORAGE_EMULATOR_HOST", "http://" + server)
+    fr = h2o.H2OFrame(pd.read_csv(__import__("io").BytesIO(_csv(40, 7))))
+    g = H2OGradientBoostingEstimator(ntrees=2, max_depth=2, seed=1)
+    g.train(x=["b"], y="a", training_frame=fr)
+    want = g.predict(fr).as_data_frame()["predict"].values
+    host, port = server.split(":")
+    for base in ("s3://bkt/models", "gs://gb/models", f"hdfs://{host}:{port}/models"):
+        dest = h2o.save_model(g, base, filename="gbm_model.zip")
+        assert dest.endswith("/gbm_model.zip")
+        m2 = h2o.load_model(dest)
+        np.testing.assert_allclose(m2.predict(fr).as_data_frame()["predict"].values, want, rtol=1e-5)
+        with pytest.raises(FileExistsError):
+            h2o.save_model(g, base, filename="gbm_model.zip")
+        assert h2o.save_model(g, base, filename="gbm_model.zip", force=True) == dest

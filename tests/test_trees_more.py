@@ -174,3 +174,24 @@ def test_pair_hist_reference_matches_level_hist():
         torch.testing.assert_close(Hp[i], H[f, a])
     r = ridx[:1500].long()
     torch.testing.assert_close(wyy[0], (vb[r].double() * va[r].double() ** 2).sum())
+
+
+@pytest.mark.parametrize("algo", ["gbm", "drf", "xgboost"])
+def test_time_based_scoring_without_early_stopping(algo):
+    """SharedTree.doScoringAndSaveModel: with score_tree_interval = 0 the
+    builders score on the time schedule (every tree in the first 4 s) whether
+    or not early stopping is on, and a max_runtime_secs stop scores the last
+    tree, so the history always ends at the returned model."""
+    from h2o3_amd.estimators import H2OGradientBoostingEstimator
+    cls = {"gbm": H2OGradientBoostingEstimator, "drf": H2ORandomForestEstimator, "xgboost": H2OXGBoostEstimator}[algo]
+    fr = _bin(n=1500)
+    m = cls(ntrees=4, max_depth=3, seed=1)
+    m.train(y="y", training_frame=fr)
+    hist = m._scoring_history
+    assert [h["number_of_trees"] for h in hist][-4:] == [1, 2, 3, 4]
+    assert all("training_logloss" in h for h in hist[-4:])
+    m2 = cls(ntrees=10_000, max_depth=3, seed=1, max_runtime_secs=1.0)
+    m2.train(y="y", training_frame=fr)
+    n = len(m2._forest) // max(1, getattr(m2, "_K", 1))
+    assert n < 10_000
+    assert m2._scoring_history[-1]["number_of_trees"] == n
