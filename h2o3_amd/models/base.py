@@ -874,6 +874,12 @@ class H2OEstimator:
         return self._output.get("cross_validation_metrics_summary")
 
     @property
+    def actual_params(self):
+        """Parameters the model was built with, auto values resolved
+        (model_base.py actual_params: {name: actual value})."""
+        return {k: v["actual"] for k, v in self.params.items()}
+
+    @property
     def actual_params_(self):
         return dict(self._parms)
 

@@ -30,6 +30,15 @@ for g, a_, b_ in gapk[:10]:
     print(f"  gap {g/1e3:7.0f} us after {a_} -> before {b_}")
 for k, v in sorted(tot.items(), key=lambda kv: -kv[1])[:14]:
     print(f"{v:8.3f} ms {cnt[k]/8:6.1f}x  {k}")
+# per-level times of the level kernels (mean over the 8 trees, in launch order)
+for name in ("hist_quad", "part_flags", "part_compact", "hist_sibling", "split_kernel"):
+    ks = [r for r in sub if name in r["Kernel_Name"]]
+    per = len(ks) // 8
+    if per == 0:
+        continue
+    lv = [sum((int(ks[t * per + i]["End_Timestamp"]) - int(ks[t * per + i]["Start_Timestamp"])) for t in range(8)) / 8e3
+          for i in range(per)]
+    print(f"{name:14s} per level (us):", [round(x) for x in lv])
 PY
 rm -f $OUT/run_kernel_trace.csv
 cat gpurun_out/gbm_${R}_pertree.txt
