@@ -178,7 +178,6 @@ class H2OEstimator:
         self._run_time = 0.0
         self._start_time = 0
         self._end_time = 0
-        self.actual_params = {}
 
     # ------------------------------------------------------------ params
     def __getattr__(self, name):
