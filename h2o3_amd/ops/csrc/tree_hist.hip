@@ -415,6 +415,261 @@ extern "C" int h2o_hist_quad4(const void* codes, int Fp, const int* ridx, const 
   return (int)hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Bank-conflict-free bin-major histogram kernel (uint8 codes, the default).
+//
+// PMC on hist_quad_kernel (scripts/pmc_gbm.sh, 100M x 100 GBM): 65% of the
+// LDS-array cycles were bank-conflict cycles (7.5 extra cycles per
+// ds_add_u64) and ~11 VALU instructions ran per LDS atomic (the f32 -> int64
+// conversion alone is ~14 instructions, the per-row w*y*y sum in f64 for
+// every lane, per-feature exec masks).  With the [feature][bin] layout the
+// bank of an atomic is (feature*257 + code) mod 16: random for random codes.
+//
+// Layout here: [bin][slot] (x channel) u64 -- a bin row of G feature slots
+// (PITCH = G * CL u64 = 128..512 B, a multiple of 128 B, so the bank of an
+// entry depends on its slot only).  Lane (rs, q) of a wave instruction (LPR =
+// G/4 lanes per row, RPW = 64/LPR rows) holds the dword of codes 4q..4q+3 of
+// its row; in atomic k it adds byte kk = (k + rs) & 3 into slot kk*LPR + q.
+// The 16 lanes of an LDS lane group then hit 16 distinct slots mod 16 (and
+// 32 lanes distinct slots mod 32 for G >= 32) whatever the codes are: one
+// LDS cycle per group.  The rotation costs nothing (per-lane shift).
+//
+// Fixed point without the int64 conversion sequence: fma in f64 against a
+// 2^52-scale magic constant leaves rint(v * s) (+ bias) in the mantissa bits
+// (3 VALU ops: cvt, fma, and/sub).  PACK (MODE 0, 0/1 weights): ONE atomic of
+// (count << 40) + biased response, as in hist_quad_kernel.
+//
+// Flush: a wave reads 4 bins x 16 slots (consecutive LDS words) and adds
+// 4 consecutive bins of 16 features to HBM: 64-B contiguous f64 atomics.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ unsigned long long fx_signed(float v, float s) {
+  // 2^52 + 2^51: |v*s| < 2^51 lands in the mantissa, two's complement after the subtract
+  const double d = __fma_rn((double)v, (double)s, 6755399441055744.0);
+  return (unsigned long long)(__double_as_longlong(d) - 0x4338000000000000LL);
+}
+
+template <int G, int CL, int MODE, bool HAS_VB, bool POSV, bool PACK>
+__global__ __launch_bounds__(1024) void hist_bm_kernel(
+    const uint8_t* __restrict__ codes, int Fp, const int* __restrict__ ridx,
+    const float* __restrict__ va, const float* __restrict__ vb,
+    const int4* __restrict__ work, int n_work, int n_fg, int F, int foff, int Bs, float s0, float s1,
+    double* __restrict__ hist, int n_slots, double* __restrict__ wyy_out, long long bq,
+    const uint8_t* __restrict__ need, const int* __restrict__ n_work_dev) {
+  constexpr int C = Chan<MODE>::C;
+  constexpr int LPR = G / 4;              // lanes per row (4 codes per lane)
+  constexpr int RPW = 64 / LPR;           // rows per wave instruction
+  constexpr int PITCH = G * CL;           // u64 entries per bin row
+  constexpr int U = 4;                    // rows per lane per iteration
+  static_assert(CL == 1 || C == 2, "two LDS channels need a two-channel mode");
+  extern __shared__ __attribute__((aligned(16))) unsigned long long ldsq[];
+  const int nwg = n_work_dev != nullptr ? n_work_dev[1] * n_fg : n_work * n_fg;
+  if ((int)blockIdx.x >= nwg) return;
+  const int lb = xcd_remap(blockIdx.x, nwg);
+  const int fgi = lb % n_fg;
+  int4 wk = work[lb / n_fg];
+  // workgroup-uniform: keep the segment in SGPRs (the buffer descriptors below need it there)
+  wk.x = __builtin_amdgcn_readfirstlane(wk.x);
+  wk.y = __builtin_amdgcn_readfirstlane(wk.y);
+  wk.z = __builtin_amdgcn_readfirstlane(wk.z);
+  if (need != nullptr && need[(size_t)wk.x * n_fg + fgi] == 0) return;   // no eligible feature in this group
+  const int fg0 = foff + fgi * G;
+  const int nf = min(G, F - fg0);
+  {
+    const int n2 = Bs * PITCH / 2;
+    ulonglong2* z = reinterpret_cast<ulonglong2*>(ldsq);
+    for (int i = threadIdx.x; i < n2; i += blockDim.x) z[i] = make_ulonglong2(0ull, 0ull);
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int q = lane % LPR;
+  const int rs = lane / LPR;
+  const int wv = threadIdx.x >> 6;
+  const int nwaves = __builtin_amdgcn_readfirstlane((int)(blockDim.x >> 6));
+  unsigned sh[4], sb[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int kk = (k + rs) & 3;
+    sh[k] = 8u * kk;
+    sb[k] = (unsigned)((kk * LPR + q) * 8);
+  }
+  const bool blk_wyy = MODE == 0 && wyy_out != nullptr && fgi == 0;   // workgroup-uniform
+  double wyyd = 0.0;
+  const int pend = wk.y + wk.z;
+  const int step = nwaves * RPW;
+  const uint8_t* cbase = codes + fg0 + 4 * q;
+  const int p_first = wk.y + wv * RPW + rs;
+  const double cpk = 4503599627370496.0 + 1099511627776.0 + (double)bq;   // 2^52 + 2^40 + bq
+  // position-indexed arrays through buffer descriptors sized to [0, pend):
+  // loads past the segment return 0 (no clamp), the row offset is one VGPR
+  // and the unrolled stride u*step goes into the scalar offset
+  const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc((void*)ridx, (short)0, pend * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)va, (short)0, POSV ? pend * 4 : 0,
+                                                                      0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)vb, (short)0,
+                                                                      (POSV && vb) ? pend * 4 : 0, 0x00020000);
+  int rA[U], rB[U];
+  unsigned cwA[U];
+  float xaA[U], xbA[U];
+  auto load_r = [&](int p, int (&r)[U]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) r[u] = __builtin_amdgcn_raw_buffer_load_b32(rr, p * 4, u * step * 4, 0);
+  };
+  auto load_v = [&](int p, const int (&r)[U], unsigned (&cw)[U], float (&xa)[U], float (&xb)[U]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (POSV) {
+        xa[u] = (MODE == 2) ? 0.f : __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(ra, p * 4, u * step * 4, 0));
+        xb[u] = (HAS_VB || MODE == 1) ? __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rb, p * 4, u * step * 4, 0))
+                                      : 1.f;
+      } else {
+        xa[u] = (MODE == 2) ? 0.f : va[r[u]];
+        xb[u] = (HAS_VB || MODE == 1) ? vb[r[u]] : 1.f;
+      }
+      cw[u] = *reinterpret_cast<const unsigned*>(cbase + (size_t)(unsigned)r[u] * (unsigned)Fp);
+    }
+  };
+  load_r(p_first, rA);
+  load_v(p_first, rA, cwA, xaA, xbA);
+  load_r(p_first + U * step, rB);
+  for (int p0 = p_first; p0 < pend; p0 += U * step) {
+    unsigned cw[U];
+    float xa[U], xb[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) { cw[u] = cwA[u]; xa[u] = xaA[u]; xb[u] = xbA[u]; }
+    load_v(p0 + U * step, rB, cwA, xaA, xbA);
+    load_r(p0 + 2 * U * step, rB);
+    float wpart = 0.f;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const bool inr = p0 + u * step < pend;
+      float c0, c1, yv = 0.f;
+      if (MODE == 0) {
+        // without vb a NaN response marks a zero-weight row (one gather per row)
+        const float y = xa[u];
+        const float w = HAS_VB ? xb[u] : (y == y ? 1.f : 0.f);
+        c0 = w;
+        c1 = w != 0.f ? w * y : 0.f;
+        yv = w != 0.f ? y : 0.f;
+        if (inr) wpart += c1 * yv;
+      } else if (MODE == 1) {
+        c0 = xa[u]; c1 = xb[u];
+      } else {
+        c0 = xb[u]; c1 = 0.f;
+      }
+      if (!inr || (c0 == 0.f && c1 == 0.f)) continue;
+      unsigned long long a0, a1 = 0ull;
+      if (PACK) {
+        const double d = __fma_rn((double)yv, (double)s1, cpk);   // weights are 0/1: count 1, response y
+        a0 = (unsigned long long)__double_as_longlong(d) & 0x000FFFFFFFFFFFFFull;
+      } else {
+        a0 = fx_signed(c0, s0);
+        if (CL == 2) a1 = fx_signed(c1, s1);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const unsigned code = __builtin_amdgcn_ubfe(cw[u], sh[k], 8);
+        unsigned long long* h = reinterpret_cast<unsigned long long*>(
+            reinterpret_cast<char*>(ldsq) + code * (unsigned)(PITCH * 8) + sb[k]);
+        __hip_atomic_fetch_add(h, a0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (CL == 2) __hip_atomic_fetch_add(h + G, a1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
+    if (blk_wyy) wyyd += (double)wpart;
+  }
+  __syncthreads();
+  if (blk_wyy) {
+    double v = q == 0 ? wyyd : 0.0;      // the LPR lanes of a row saw the same rows
+    v = wave_sum(v);
+    if (lane == 0) gbl_add(wyy_out + wk.x, v);
+  }
+  const double inv0 = 1.0 / (double)s0, inv1 = 1.0 / (double)s1;
+  const int si = lane & 15, bi = lane >> 4;
+  constexpr int NSG = G / 16;
+  const int nbq = (Bs + 3) >> 2;
+  for (int e = wv; e < nbq * NSG; e += nwaves) {
+    const int b = (e / NSG) * 4 + bi;
+    const int slot = (e % NSG) * 16 + si;
+    const int fl = 4 * (slot % LPR) + slot / LPR;
+    if (b >= Bs || fl >= nf) continue;
+    double* o = hist + ((size_t)(fg0 + fl) * n_slots + wk.x) * (size_t)(Bs * C) + (size_t)b * C;
+    const unsigned long long v = ldsq[b * PITCH + slot];
+    if (PACK) {
+      if (v != 0ull) {
+        const long long cnt = (long long)(v >> 40);
+        const long long low = (long long)(v & ((1ull << 40) - 1));
+        gbl_add(o, (double)cnt);
+        gbl_add(o + 1, (double)(low - cnt * bq) * inv1);
+      }
+    } else {
+      if (v != 0ull) gbl_add(o, (double)(long long)v * inv0);
+      if (CL == 2) {
+        const unsigned long long v1 = ldsq[b * PITCH + G + slot];
+        if (v1 != 0ull) gbl_add(o + 1, (double)(long long)v1 * inv1);
+      }
+    }
+  }
+}
+
+template <int G, int CL, int M, bool V, bool PV, bool PK>
+static int lbm(const QuadArgs& a) {
+  auto kern = hist_bm_kernel<G, CL, M, V, PV, PK>;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return (int)e;
+    attr = true;
+  }
+  hipLaunchKernelGGL(kern, a.grid, dim3(a.threads), a.lds, a.s, a.cc, a.Fp, a.ridx, a.va, a.vb, a.wk, a.n_work,
+                     a.n_fg, a.F, a.foff, a.Bs, a.s0, a.s1, a.hist, a.n_slots, a.wyy, a.bq, a.need, a.n_work_dev);
+  return (int)hipGetLastError();
+}
+
+template <int G, int CL, int M, bool PK>
+static int lbm_v(bool vb, bool posv, const QuadArgs& a) {
+  if (M == 1) return posv ? lbm<G, CL, M, true, true, PK>(a) : lbm<G, CL, M, true, false, PK>(a);
+  if (vb) return posv ? lbm<G, CL, M, true, true, PK>(a) : lbm<G, CL, M, true, false, PK>(a);
+  return posv ? lbm<G, CL, M, false, true, PK>(a) : lbm<G, CL, M, false, false, PK>(a);
+}
+
+template <int G>
+static int lbm_g(int mode, bool pack, bool vb, bool posv, const QuadArgs& a) {
+  if (pack) return lbm_v<G, 1, 0, true>(vb, posv, a);
+  if (mode == 2) return lbm_v<G, 1, 2, false>(vb, posv, a);
+  if constexpr (G <= 32) {
+    if (mode == 0) return lbm_v<G, 2, 0, false>(vb, posv, a);
+    return lbm_v<G, 2, 1, false>(vb, posv, a);
+  }
+  return (int)hipErrorInvalidValue;
+}
+
+// Bin-major conflict-free histograms of features [foff, F) in n_fg = ceil((F -
+// foff) / G) groups of G in {16, 32, 64} features (G <= 32 for the two-channel
+// modes); every group's code dwords lie inside the row (foff + n_fg*G <= Fp).
+// pack_bq >= 0 selects the packed single-atomic path (MODE 0, 0/1 weights).
+// n_work_dev != nullptr: device-built work list (n_work = capacity).
+extern "C" int h2o_hist_bm(const void* codes, int Fp, const int* ridx, const float* va, const float* vb,
+                           const int* work, int n_work, int F, int foff, int Bs, float s0, float s1,
+                           double* hist, int n_slots, int mode, double* wyy, int posv, long long pack_bq, int G,
+                           const uint8_t* need, const int* n_work_dev, hipStream_t s) {
+  if (n_work <= 0 || foff >= F) return 0;
+  if (Fp % 4 != 0 || foff % 4 != 0 || Bs > 256 || Bs % 4 != 0 || mode < 0 || mode > 2) return -1;
+  const bool pack = pack_bq >= 0 && mode == 0;
+  const int CL = (pack || mode == 2) ? 1 : 2;
+  if (!(G == 16 || G == 32 || G == 64) || (CL == 2 && G == 64)) return -2;
+  const int n_fg = (F - foff + G - 1) / G;
+  if (foff + n_fg * G > Fp) return -3;       // every code dword read lies inside the row
+  QuadArgs a;
+  a.grid = dim3(n_work * n_fg); a.threads = 1024;
+  a.lds = (size_t)Bs * G * CL * sizeof(unsigned long long); a.s = s;
+  if (a.lds > 160 * 1024) return -4;
+  a.cc = (const uint8_t*)codes; a.Fp = Fp; a.ridx = ridx; a.va = va; a.vb = vb; a.wk = (const int4*)work;
+  a.n_work = n_work; a.n_fg = n_fg; a.fgw = G; a.F = F; a.foff = foff; a.Bs = Bs; a.s0 = s0; a.s1 = s1;
+  a.hist = hist; a.n_slots = n_slots; a.wyy = wyy; a.bq = pack_bq; a.need = need; a.n_work_dev = n_work_dev;
+  if (G == 64) return lbm_g<64>(mode, pack, vb != nullptr, posv != 0, a);
+  if (G == 32) return lbm_g<32>(mode, pack, vb != nullptr, posv != 0, a);
+  return lbm_g<16>(mode, pack, vb != nullptr, posv != 0, a);
+}
+
 template <typename CodeT>
 static int launch_hist(const void* codes, int Fp, const int* ridx, const float* va, const float* vb,
                        const int4* work, int n_work, int F, int FG, int Bs, float s0, float s1, double* hist,

@@ -86,6 +86,9 @@ def _lib():
         lib.h2o_hist_quad3.argtypes = [_c_void, _c_int, _c_void, _c_void, _c_void, _c_void, _c_int, _c_int, _c_int,
                                        _c_int, ctypes.c_float, ctypes.c_float, _c_void, _c_int, _c_int, _c_int,
                                        _c_void, _c_int, _c_ll, _c_int, _c_void, _c_void]
+        lib.h2o_hist_bm.argtypes = [_c_void, _c_int, _c_void, _c_void, _c_void, _c_void, _c_int, _c_int, _c_int,
+                                    _c_int, ctypes.c_float, ctypes.c_float, _c_void, _c_int, _c_int, _c_void, _c_int,
+                                    _c_ll, _c_int, _c_void, _c_void, _c_void]
         lib.h2o_part_flags.argtypes = [_c_void, _c_int, _c_ll, _c_ll, _c_void, _c_void, _c_void, _c_int, _c_void,
                                        _c_void, _c_int, _c_void, _c_void, _c_void]
         lib.h2o_part_compact.argtypes = [_c_void, _c_void, _c_void, _c_int, _c_void, _c_void, _c_void, _c_void,
@@ -145,6 +148,28 @@ def quad_groups(F: int, Fp: int, Bs: int, pack: bool, budget: int = _LDS_BUDGET)
         if n_fg * fgw <= Fp or fgw <= 4:
             return n_fg, fgw
         n_fg += 1
+
+
+def bm_groups(F: int, Fp: int, Bs: int, one_channel: bool):
+    """(n_fg, G) of the bank-conflict-free bin-major kernel (hist_bm_kernel):
+    G in {64, 32, 16} features per group (G <= 32 with two LDS channels), the
+    FEWEST groups whose code dwords stay inside the Fp-byte row and whose LDS
+    histogram (Bs x G x channels x 8 B) fits 160 KB; None when no width fits
+    (the grouped-lane kernel then runs).  F = 100 (Fp 128), 256 bins: packed
+    -> 2 x 64 (128 KB), two channels -> 4 x 32."""
+    if os.environ.get("H2O3_HIST_BM", "1") != "1" or Bs > 256 or Bs % 4 or Fp % 4:
+        return None
+    cl = 1 if one_channel else 2
+    best = None
+    for G in (64, 32, 16):
+        if cl == 2 and G == 64:
+            continue
+        n_fg = -(-F // G)
+        if n_fg * G > Fp or Bs * G * cl * 8 > 160 * 1024:
+            continue
+        if best is None or n_fg < best[0]:
+            best = (n_fg, G)
+    return best
 
 
 def make_work(starts, counts, slots, chunk):
@@ -254,15 +279,18 @@ def hist_build(bd, ridx, va, vb, mode, starts, counts, n_slots, use_native=None,
         # H2O3_HIST_BIG=1 (A/B): one 1024-thread workgroup per CU with up to 160 KB of LDS histogram
         big = os.environ.get("H2O3_HIST_BIG", "0") == "1"
         qbudget = 156 * 1024 if big else _LDS_BUDGET
+        bm = None
         if quad:
-            n_fg, fgw = quad_groups(bd.F, bd.Fp, bd.Bs, pack, qbudget)
+            bm = bm_groups(bd.F, bd.Fp, bd.Bs, pack or mode == 2)
+            n_fg, fgw = bm if bm is not None else quad_groups(bd.F, bd.Fp, bd.Bs, pack, qbudget)
         else:
             FG = feature_group(bd.F, bd.Bs, mode)
             n_fg = (bd.F + FG - 1) // FG
         chunk = hist_chunk(total, n_fg, target_blocks)
         if pack and chunk >= (1 << 23):
             pack = False
-            n_fg, fgw = quad_groups(bd.F, bd.Fp, bd.Bs, False, qbudget)
+            bm = bm_groups(bd.F, bd.Fp, bd.Bs, mode == 2)
+            n_fg, fgw = bm if bm is not None else quad_groups(bd.F, bd.Fp, bd.Bs, False, qbudget)
         items = make_work(starts, counts, range(n_slots), chunk)
         if len(items) == 0:
             return ret()
@@ -285,6 +313,13 @@ def hist_build(bd, ridx, va, vb, mode, starts, counts, n_slots, use_native=None,
             if pack:
                 s1, bq = _pack_scale(vmax[1] if vb is None else max(vmax[1], 0.0), chunk)
             need = _need(fgw)
+            if bm is not None:
+                rc = lib.h2o_hist_bm(_ptr(bd.codes), bd.Fp, _ptr(ridx), _ptr(va), _ptr(vb), _ptr(work), len(items),
+                                     bd.F, 0, bd.Bs, s0, s1, _ptr(hist), n_slots, mode, _ptr(wyy), 1 if posv else 0,
+                                     bq, fgw, _ptr(need), None, _stream())
+                if rc != 0:
+                    raise RuntimeError(f"h2o_hist_bm failed: error {rc} (F={bd.F}, Fp={bd.Fp}, G={fgw})")
+                return ret()
             rc = lib.h2o_hist_quad3(_ptr(bd.codes), bd.Fp, _ptr(ridx), _ptr(va), _ptr(vb), _ptr(work), len(items),
                                     bd.F, 0, bd.Bs, s0, s1, _ptr(hist), n_slots, mode, 1024 if big else 512, _ptr(wyy),
                                     1 if posv else 0, bq, fgw, _ptr(need), _stream())
@@ -748,12 +783,14 @@ def hist_build_dev(bd, ridx, va, vb, mode, rec, rec_cols, starts, counts, vmax, 
     n = len(starts)
     C = channels(mode)
     pack = mode == 0 and unit_w and os.environ.get("H2O3_HIST_PACK", "1") == "1"
-    n_fg, fgw = quad_groups(bd.F, bd.Fp, bd.Bs, pack)
+    bm = bm_groups(bd.F, bd.Fp, bd.Bs, pack or mode == 2)
+    n_fg, fgw = bm if bm is not None else quad_groups(bd.F, bd.Fp, bd.Bs, pack)
     total = int(sum(counts))
     chunk = hist_chunk((total + 1) // 2, n_fg, target_blocks)   # the lighter children: <= half the rows
     if pack and chunk >= (1 << 23):
         pack = False
-        n_fg, fgw = quad_groups(bd.F, bd.Fp, bd.Bs, False)
+        bm = bm_groups(bd.F, bd.Fp, bd.Bs, mode == 2)
+        n_fg, fgw = bm if bm is not None else quad_groups(bd.F, bd.Fp, bd.Bs, False)
     cap = n + total // chunk + 1
     stc = np.concatenate([np.asarray(starts, dtype=np.int64), np.asarray(counts, dtype=np.int64)])
     stc_d = _h2d(stc, dev)
@@ -775,6 +812,13 @@ def hist_build_dev(bd, ridx, va, vb, mode, rec, rec_cols, starts, counts, vmax, 
     bq = -1
     if pack:
         s1, bq = _pack_scale(vmax[1] if vb is None else max(vmax[1], 0.0), chunk)
+    if bm is not None:
+        rc = lib.h2o_hist_bm(_ptr(bd.codes), bd.Fp, _ptr(ridx), _ptr(va), _ptr(vb), _ptr(work), cap, bd.F, 0, bd.Bs,
+                             s0, s1, _ptr(Hb), n, mode, _ptr(wyy), 1 if posv else 0, bq, fgw, None, _ptr(cnts),
+                             _stream())
+        if rc != 0:
+            raise RuntimeError(f"h2o_hist_bm failed: {rc}")
+        return Hb, wyy, slots, cnts
     rc = lib.h2o_hist_quad4(_ptr(bd.codes), bd.Fp, _ptr(ridx), _ptr(va), _ptr(vb), _ptr(work), cap, bd.F, 0, bd.Bs,
                             s0, s1, _ptr(Hb), n, mode, 512, _ptr(wyy), 1 if posv else 0, bq, fgw, None, _ptr(cnts),
                             _stream())

@@ -667,3 +667,68 @@ def test_col_sample_kernel_uniform_sorted_distinct():
     assert abs(both - k * (k - 1) / (m * (m - 1))) < 0.004
     out2 = tree_ops.col_sample(n, torch.as_tensor(elig, device="cuda"), k, 12345).cpu().numpy()
     assert np.array_equal(out, out2)
+
+
+@pytest.mark.parametrize("F", [13, 37, 64, 100])
+@pytest.mark.parametrize("mode,pack", [(0, True), (0, False), (1, False), (2, False)])
+@pytest.mark.parametrize("posv", [False, True])
+def test_hist_bm_kernel_matches_reference(F, mode, pack, posv, monkeypatch):
+    """Bank-conflict-free bin-major kernel (hist_bm_kernel, G = 64 / 32 / 16
+    feature slots per bin row, rotated code bytes per row) vs the fp64 torch
+    reference, for the packed, two-channel and count layouts, row- and
+    position-ordered payloads, partial last groups."""
+    _need_gpu()
+    monkeypatch.setenv("H2O3_HIST_BM", "1")
+    from h2o3_amd.ops import tree_ops
+    bd, _ = _binned(n=30000, F=F, nbins=255, cats=F < 50)
+    bm = tree_ops.bm_groups(bd.F, bd.Fp, bd.Bs, pack or mode == 2)
+    assert bm is not None
+    if F == 100:
+        assert bm == ((2, 64) if (pack or mode == 2) else (4, 32))
+    n = bd.nrows_local
+    g = torch.Generator(device="cuda").manual_seed(F + mode)
+    ridx = torch.randperm(n, generator=g, device="cuda").to(torch.int32)
+    va = torch.randn(n, generator=g, device="cuda")
+    if pack:
+        vb = (torch.rand(n, generator=g, device="cuda") < 0.7).to(torch.float32)
+    else:
+        vb = torch.rand(n, generator=g, device="cuda")
+    starts, counts = [0, 9000, 21000], [9000, 12000, 9000]
+    vmax = tree_ops.channel_max(va, vb, mode)
+    h_gpu, w_gpu = tree_ops.hist_build(bd, ridx, va, vb, mode, starts, counts, 3, use_native=True, unit_w=pack,
+                                       vmax=vmax, posv=posv, want_wyy=True)
+    h_ref, w_ref = tree_ops.hist_build(bd, ridx, va, vb, mode, starts, counts, 3, use_native=False, posv=posv,
+                                       want_wyy=True)
+    torch.testing.assert_close(h_gpu, h_ref, rtol=1e-5, atol=1e-4)
+    if mode == 0:
+        torch.testing.assert_close(w_gpu, w_ref, rtol=1e-5, atol=1e-3)
+    # the grouped-lane kernel gives the same histograms
+    monkeypatch.setenv("H2O3_HIST_BM", "0")
+    h_q = tree_ops.hist_build(bd, ridx, va, vb, mode, starts, counts, 3, use_native=True, unit_w=pack, vmax=vmax,
+                              posv=posv)
+    torch.testing.assert_close(h_gpu, h_q, rtol=1e-5, atol=1e-4)
+
+
+def test_gbm_same_model_bm_and_quad(monkeypatch):
+    """GBM grown with the bin-major histogram kernel vs the grouped-lane kernel:
+    same trees (the fixed-point sums only differ in the last bits)."""
+    _need_gpu()
+    import pandas as pd
+    import h2o3_amd as h2o
+    from h2o3_amd.estimators import H2OGradientBoostingEstimator
+    h2o.init(device="cuda:0", verbose=False)
+    rng = np.random.RandomState(7)
+    n, F = 60000, 70
+    X = rng.randn(n, F).astype(np.float32)
+    y = (X[:, 0] - X[:, 3] + 0.5 * X[:, 5] * X[:, 6] + 0.3 * rng.randn(n) > 0).astype(int)
+    df = pd.DataFrame(X, columns=[f"x{i}" for i in range(F)])
+    df["y"] = np.where(y == 1, "a", "b")
+    fr = h2o.H2OFrame(df)
+    out = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("H2O3_HIST_BM", flag)
+        m = H2OGradientBoostingEstimator(ntrees=6, max_depth=6, seed=3)
+        m.train(y="y", training_frame=fr)
+        out[flag] = (m.logloss(), [list(t.feat) for t in m._forest.trees])
+    assert abs(out["1"][0] - out["0"][0]) < 1e-5
+    assert out["1"][1] == out["0"][1]
