@@ -498,7 +498,7 @@ __global__ __launch_bounds__(1024) void hist_bm_kernel(
   const int step = nwaves * RPW;
   const uint8_t* cbase = codes + fg0 + 4 * q;
   const int p_first = wk.y + wv * RPW + rs;
-  const double cpk = 4503599627370496.0 + 1099511627776.0 + (double)bq;   // 2^52 + 2^40 + bq
+  const unsigned long long pk_off = (1ull << 40) + (unsigned long long)bq;   // count 1 + response bias
   // position-indexed arrays through buffer descriptors sized to [0, pend):
   // loads past the segment return 0 (no clamp), the row offset is one VGPR
   // and the unrolled stride u*step goes into the scalar offset
@@ -538,7 +538,6 @@ __global__ __launch_bounds__(1024) void hist_bm_kernel(
     for (int u = 0; u < U; ++u) { cw[u] = cwA[u]; xa[u] = xaA[u]; xb[u] = xbA[u]; }
     load_v(p0 + U * step, rB, cwA, xaA, xbA);
     load_r(p0 + 2 * U * step, rB);
-    float wpart = 0.f;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const bool inr = p0 + u * step < pend;
@@ -550,7 +549,9 @@ __global__ __launch_bounds__(1024) void hist_bm_kernel(
         c0 = w;
         c1 = w != 0.f ? w * y : 0.f;
         yv = w != 0.f ? y : 0.f;
-        if (inr) wpart += c1 * yv;
+        // per-row f64 products, like every other histogram kernel (the node
+        // total enters the split gains: same rounding -> same trees)
+        if (blk_wyy && inr) wyyd += (double)c1 * (double)yv;
       } else if (MODE == 1) {
         c0 = xa[u]; c1 = xb[u];
       } else {
@@ -559,8 +560,9 @@ __global__ __launch_bounds__(1024) void hist_bm_kernel(
       if (!inr || (c0 == 0.f && c1 == 0.f)) continue;
       unsigned long long a0, a1 = 0ull;
       if (PACK) {
-        const double d = __fma_rn((double)yv, (double)s1, cpk);   // weights are 0/1: count 1, response y
-        a0 = (unsigned long long)__double_as_longlong(d) & 0x000FFFFFFFFFFFFFull;
+        // weights are 0/1: count 1, response y; the even magic constant of
+        // fx_signed rounds ties like __float2ll_rn, the bias is added after
+        a0 = fx_signed(yv, s1) + pk_off;
       } else {
         a0 = fx_signed(c0, s0);
         if (CL == 2) a1 = fx_signed(c1, s1);
@@ -574,7 +576,6 @@ __global__ __launch_bounds__(1024) void hist_bm_kernel(
         if (CL == 2) __hip_atomic_fetch_add(h + G, a1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     }
-    if (blk_wyy) wyyd += (double)wpart;
   }
   __syncthreads();
   if (blk_wyy) {

@@ -298,6 +298,7 @@ def test_packed_hist_group_widths_match_reference(fgw, lw, monkeypatch):
     64 % lanes-per-row != 0, partial last group) vs the torch reference.
     H2O3_HIST_LW is read once per process; both values give correct results."""
     _need_gpu()
+    monkeypatch.setenv("H2O3_HIST_BM", "0")     # the grouped-lane kernel's widths
     monkeypatch.setenv("H2O3_HIST_FGW", fgw)
     monkeypatch.setenv("H2O3_HIST_LW", lw)
     from h2o3_amd.ops import tree_ops
@@ -410,14 +411,15 @@ def test_drf_chunked_need_mask_same_model(F, monkeypatch):
     np.testing.assert_allclose(preds[0], preds[1], rtol=1e-6, atol=1e-6)
 
 
-@pytest.mark.parametrize("kernel,fg", [("quad", "8"), ("quad", "36"), ("quad", "64"), ("old", "0")])
+@pytest.mark.parametrize("kernel,fg", [("quad", "8"), ("quad", "36"), ("quad", "64"), ("old", "0"), ("bm", "64")])
 @pytest.mark.parametrize("F", [64, 100])
 def test_packed_need_mask_matches_full(kernel, fg, F, monkeypatch):
     """Packed single-atomic path (mode 0, 0/1 weights) with a need mask: the
     host-side group count must match the kernel's; needed features equal the
     unmasked histogram exactly, and the result matches fp64 torch."""
     _need_gpu()
-    monkeypatch.setenv("H2O3_HIST_KERNEL", kernel)
+    monkeypatch.setenv("H2O3_HIST_KERNEL", "quad" if kernel == "bm" else kernel)
+    monkeypatch.setenv("H2O3_HIST_BM", "1" if kernel == "bm" else "0")
     if kernel == "quad":
         monkeypatch.setenv("H2O3_HIST_FGW", fg)
     from h2o3_amd.ops import tree_ops
@@ -442,7 +444,7 @@ def test_packed_need_mask_matches_full(kernel, fg, F, monkeypatch):
     for s in range(3):
         for f in torch.nonzero(need[s]).flatten().tolist():
             torch.testing.assert_close(part[f, s], full[f, s], rtol=0, atol=0)
-    if kernel == "quad" and F > int(fg):   # more than one group: some (slot, group) blocks were skipped
+    if kernel in ("quad", "bm") and F > int(fg):   # more than one group: some (slot, group) blocks were skipped
         assert float(part.abs().sum()) < float(full.abs().sum())
 
 
