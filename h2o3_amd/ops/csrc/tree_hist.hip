@@ -448,7 +448,7 @@ __device__ __forceinline__ unsigned long long fx_signed(float v, float s) {
   return (unsigned long long)(__double_as_longlong(d) - 0x4338000000000000LL);
 }
 
-template <int G, int CL, int MODE, bool HAS_VB, bool POSV, bool PACK>
+template <int G, int CL, int MODE, bool HAS_VB, bool POSV, bool PACK, int LW = 2>
 __global__ __launch_bounds__(1024) void hist_bm_kernel(
     const uint8_t* __restrict__ codes, int Fp, const int* __restrict__ ridx,
     const float* __restrict__ va, const float* __restrict__ vb,
@@ -456,11 +456,15 @@ __global__ __launch_bounds__(1024) void hist_bm_kernel(
     double* __restrict__ hist, int n_slots, double* __restrict__ wyy_out, long long bq,
     const uint8_t* __restrict__ need, const int* __restrict__ n_work_dev) {
   constexpr int C = Chan<MODE>::C;
-  constexpr int LPR = G / 4;              // lanes per row (4 codes per lane)
+  constexpr int NK = 4 * LW;              // codes per lane (LW dwords)
+  constexpr int LPR = G / NK;             // lanes per row
   constexpr int RPW = 64 / LPR;           // rows per wave instruction
   constexpr int PITCH = G * CL;           // u64 entries per bin row
   constexpr int U = 4;                    // rows per lane per iteration
+  constexpr int PD = 2;                   // iterations in the load ring
+  using CT = typename CodeW<LW>::T;
   static_assert(CL == 1 || C == 2, "two LDS channels need a two-channel mode");
+  static_assert(LPR >= 1, "group narrower than one lane's codes");
   extern __shared__ __attribute__((aligned(16))) unsigned long long ldsq[];
   const int nwg = n_work_dev != nullptr ? n_work_dev[1] * n_fg : n_work * n_fg;
   if ((int)blockIdx.x >= nwg) return;
@@ -485,10 +489,13 @@ __global__ __launch_bounds__(1024) void hist_bm_kernel(
   const int rs = lane / LPR;
   const int wv = threadIdx.x >> 6;
   const int nwaves = __builtin_amdgcn_readfirstlane((int)(blockDim.x >> 6));
-  unsigned sh[4], sb[4];
+  // atomic k of a row takes code kk = (k & ~3) | ((k + rs) & 3) of the lane's
+  // NK codes (the dword is fixed by k, the byte rotates with the row) into
+  // slot kk*LPR + q: the rows of an LDS lane group hit disjoint slots
+  unsigned sh[NK], sb[NK];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int kk = (k + rs) & 3;
+  for (int k = 0; k < NK; ++k) {
+    const int kk = (k & ~3) | ((k + rs) & 3);
     sh[k] = 8u * kk;
     sb[k] = (unsigned)((kk * LPR + q) * 8);
   }
@@ -496,7 +503,7 @@ __global__ __launch_bounds__(1024) void hist_bm_kernel(
   double wyyd = 0.0;
   const int pend = wk.y + wk.z;
   const int step = nwaves * RPW;
-  const uint8_t* cbase = codes + fg0 + 4 * q;
+  const uint8_t* cbase = codes + fg0 + NK * q;
   const int p_first = wk.y + wv * RPW + rs;
   const unsigned long long pk_off = (1ull << 40) + (unsigned long long)bq;   // count 1 + response bias
   // position-indexed arrays through buffer descriptors sized to [0, pend):
@@ -507,14 +514,18 @@ __global__ __launch_bounds__(1024) void hist_bm_kernel(
                                                                       0x00020000);
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)vb, (short)0,
                                                                       (POSV && vb) ? pend * 4 : 0, 0x00020000);
-  int rA[U], rB[U];
-  unsigned cwA[U];
-  float xaA[U], xbA[U];
+  // Register ring of PD iterations, no copies: stage d of a round processes
+  // iteration i from ring slot d, then refills slot d with the gathers of
+  // iteration i + PD (row ids loaded a round earlier) and the row ids of
+  // iteration i + 2 PD.
+  int R[PD][U];
+  CT CW[PD][U];
+  float XA[PD][U], XB[PD][U];
   auto load_r = [&](int p, int (&r)[U]) {
 #pragma unroll
     for (int u = 0; u < U; ++u) r[u] = __builtin_amdgcn_raw_buffer_load_b32(rr, p * 4, u * step * 4, 0);
   };
-  auto load_v = [&](int p, const int (&r)[U], unsigned (&cw)[U], float (&xa)[U], float (&xb)[U]) {
+  auto load_v = [&](int p, const int (&r)[U], CT (&cw)[U], float (&xa)[U], float (&xb)[U]) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       if (POSV) {
@@ -525,56 +536,64 @@ __global__ __launch_bounds__(1024) void hist_bm_kernel(
         xa[u] = (MODE == 2) ? 0.f : va[r[u]];
         xb[u] = (HAS_VB || MODE == 1) ? vb[r[u]] : 1.f;
       }
-      cw[u] = *reinterpret_cast<const unsigned*>(cbase + (size_t)(unsigned)r[u] * (unsigned)Fp);
+      cw[u] = *reinterpret_cast<const CT*>(cbase + (size_t)(unsigned)r[u] * (unsigned)Fp);
     }
   };
-  load_r(p_first, rA);
-  load_v(p_first, rA, cwA, xaA, xbA);
-  load_r(p_first + U * step, rB);
-  for (int p0 = p_first; p0 < pend; p0 += U * step) {
-    unsigned cw[U];
-    float xa[U], xb[U];
+  const int IT = U * step;                 // positions per iteration (all waves)
 #pragma unroll
-    for (int u = 0; u < U; ++u) { cw[u] = cwA[u]; xa[u] = xaA[u]; xb[u] = xbA[u]; }
-    load_v(p0 + U * step, rB, cwA, xaA, xbA);
-    load_r(p0 + 2 * U * step, rB);
+  for (int d = 0; d < PD; ++d) load_r(p_first + d * IT, R[d]);
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const bool inr = p0 + u * step < pend;
-      float c0, c1, yv = 0.f;
-      if (MODE == 0) {
-        // without vb a NaN response marks a zero-weight row (one gather per row)
-        const float y = xa[u];
-        const float w = HAS_VB ? xb[u] : (y == y ? 1.f : 0.f);
-        c0 = w;
-        c1 = w != 0.f ? w * y : 0.f;
-        yv = w != 0.f ? y : 0.f;
-        // per-row f64 products, like every other histogram kernel (the node
-        // total enters the split gains: same rounding -> same trees)
-        if (blk_wyy && inr) wyyd += (double)c1 * (double)yv;
-      } else if (MODE == 1) {
-        c0 = xa[u]; c1 = xb[u];
-      } else {
-        c0 = xb[u]; c1 = 0.f;
-      }
-      if (!inr || (c0 == 0.f && c1 == 0.f)) continue;
-      unsigned long long a0, a1 = 0ull;
-      if (PACK) {
-        // weights are 0/1: count 1, response y; the even magic constant of
-        // fx_signed rounds ties like __float2ll_rn, the bias is added after
-        a0 = fx_signed(yv, s1) + pk_off;
-      } else {
-        a0 = fx_signed(c0, s0);
-        if (CL == 2) a1 = fx_signed(c1, s1);
-      }
+  for (int d = 0; d < PD; ++d) {
+    load_v(p_first + d * IT, R[d], CW[d], XA[d], XB[d]);
+    load_r(p_first + (PD + d) * IT, R[d]);
+  }
+  for (int p0r = p_first; p0r < pend; p0r += PD * IT) {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const unsigned code = __builtin_amdgcn_ubfe(cw[u], sh[k], 8);
-        unsigned long long* h = reinterpret_cast<unsigned long long*>(
-            reinterpret_cast<char*>(ldsq) + code * (unsigned)(PITCH * 8) + sb[k]);
-        __hip_atomic_fetch_add(h, a0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (CL == 2) __hip_atomic_fetch_add(h + G, a1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    for (int d = 0; d < PD; ++d) {
+      const int p0 = p0r + d * IT;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const bool inr = p0 + u * step < pend;
+        float c0, c1, yv = 0.f;
+        if (MODE == 0) {
+          // without vb a NaN response marks a zero-weight row (one gather per row)
+          const float y = XA[d][u];
+          const float w = HAS_VB ? XB[d][u] : (y == y ? 1.f : 0.f);
+          c0 = w;
+          c1 = w != 0.f ? w * y : 0.f;
+          yv = w != 0.f ? y : 0.f;
+          // per-row f64 products, like every other histogram kernel (the node
+          // total enters the split gains: same rounding -> same trees)
+          if (blk_wyy && inr) wyyd += (double)c1 * (double)yv;
+        } else if (MODE == 1) {
+          c0 = XA[d][u]; c1 = XB[d][u];
+        } else {
+          c0 = XB[d][u]; c1 = 0.f;
+        }
+        if (!inr || (c0 == 0.f && c1 == 0.f)) continue;
+        unsigned long long a0, a1 = 0ull;
+        if (PACK) {
+          // weights are 0/1: count 1, response y; the even magic constant of
+          // fx_signed rounds ties like __float2ll_rn, the bias is added after
+          a0 = fx_signed(yv, s1) + pk_off;
+        } else {
+          a0 = fx_signed(c0, s0);
+          if (CL == 2) a1 = fx_signed(c1, s1);
+        }
+#pragma unroll
+        for (int k = 0; k < NK; ++k) {
+          unsigned word;
+          if constexpr (LW == 2) word = (k & 4) ? CW[d][u].y : CW[d][u].x;
+          else word = CW[d][u];
+          const unsigned code = __builtin_amdgcn_ubfe(word, sh[k] & 31u, 8);
+          unsigned long long* h = reinterpret_cast<unsigned long long*>(
+              reinterpret_cast<char*>(ldsq) + code * (unsigned)(PITCH * 8) + sb[k]);
+          __hip_atomic_fetch_add(h, a0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (CL == 2) __hip_atomic_fetch_add(h + G, a1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
       }
+      load_v(p0 + PD * IT, R[d], CW[d], XA[d], XB[d]);
+      load_r(p0 + 2 * PD * IT, R[d]);
     }
   }
   __syncthreads();
@@ -590,7 +609,7 @@ __global__ __launch_bounds__(1024) void hist_bm_kernel(
   for (int e = wv; e < nbq * NSG; e += nwaves) {
     const int b = (e / NSG) * 4 + bi;
     const int slot = (e % NSG) * 16 + si;
-    const int fl = 4 * (slot % LPR) + slot / LPR;
+    const int fl = NK * (slot % LPR) + slot / LPR;
     if (b >= Bs || fl >= nf) continue;
     double* o = hist + ((size_t)(fg0 + fl) * n_slots + wk.x) * (size_t)(Bs * C) + (size_t)b * C;
     const unsigned long long v = ldsq[b * PITCH + slot];
@@ -611,9 +630,9 @@ __global__ __launch_bounds__(1024) void hist_bm_kernel(
   }
 }
 
-template <int G, int CL, int M, bool V, bool PV, bool PK>
-static int lbm(const QuadArgs& a) {
-  auto kern = hist_bm_kernel<G, CL, M, V, PV, PK>;
+template <int G, int CL, int M, bool V, bool PV, bool PK, int LW>
+static int lbm_u(const QuadArgs& a) {
+  auto kern = hist_bm_kernel<G, CL, M, V, PV, PK, LW>;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -623,6 +642,14 @@ static int lbm(const QuadArgs& a) {
   hipLaunchKernelGGL(kern, a.grid, dim3(a.threads), a.lds, a.s, a.cc, a.Fp, a.ridx, a.va, a.vb, a.wk, a.n_work,
                      a.n_fg, a.F, a.foff, a.Bs, a.s0, a.s1, a.hist, a.n_slots, a.wyy, a.bq, a.need, a.n_work_dev);
   return (int)hipGetLastError();
+}
+
+// H2O3_HIST_BM_LW: codes per lane (1 -> 4, 2 -> 8; A/B of the per-row work amortisation)
+template <int G, int CL, int M, bool V, bool PV, bool PK>
+static int lbm(const QuadArgs& a) {
+  static const int lw = env_int("H2O3_HIST_BM_LW", 2);
+  // G = 16: 8 rows share a 16-lane group, too many for 4 byte rotations -> 4 codes per lane
+  return (lw == 1 || G == 16) ? lbm_u<G, CL, M, V, PV, PK, 1>(a) : lbm_u<G, CL, M, V, PV, PK, 2>(a);
 }
 
 template <int G, int CL, int M, bool PK>
