@@ -217,6 +217,11 @@ __device__ __forceinline__ float gi_dpp(float x) {
 // 16 cycles replace 8 f32 16x16x4 MFMAs of 32 cycles for the same 32 rows.
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
+// XOR swizzle of the 8-row k-blocks of feature f in the bf16x3 LDS image
+// (glm_irls_ws_kernel): conflict-free producer b128 stores and consumer b128
+// operand reads (searched over pads / swizzles against the gfx950 lane groups)
+__device__ __forceinline__ int gi_swz(int f) { return (f ^ (f >> 2)) & 7; }
+
 template <int T, int SL, int Q, int M>
 __device__ __forceinline__ void gi_mfma3_q(const bf16x8* ah, const bf16x8* al, f32x4* acc) {
   constexpr int pp = SL + 4 * Q;
@@ -496,9 +501,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   // chunk rows are permuted (producer wave pw, lane half par, slot v ->
   // k = 16 pw + 8 par + v) so each producer lane writes 8 rows of one feature
   // as one 16-byte store and each consumer lane reads its 16x16x32 operand
-  // (8 consecutive k of one feature) as one ds_read_b128.  KS = 72 puts the 16
-  // features of an operand read on 16 distinct 4-bank groups.
-  constexpr int KS = 72;
+  // (8 consecutive k of one feature) as one ds_read_b128.  The 8-row k-blocks
+  // of feature f sit XOR-swizzled at block (kb ^ swz(f)), swz(f) = (f ^ f>>2)
+  // & 7, KS = 64: the 8 lanes of a ds_write_b128 group (8 consecutive
+  // features) and the 16 lanes of a ds_read_b128 group (16 features x 2
+  // k-blocks) land on distinct bank quads.  PMC with the padded KS = 72
+  // layout: 6.35 bank-conflict cycles per LDS instruction (4-way on the
+  // producer stores, 2-way on the operand reads).
+  constexpr int KS = 64;
   static_assert(!BF3 || (PP == 128 && SQW), "bf16x3 path: P = 128, sqrt(W)-scaled rows");
   __shared__ float L[2][BF3 ? 4 : RC * S];
   __shared__ __attribute__((aligned(16))) __bf16 LB[2][2][BF3 ? PP * KS : 8];
@@ -673,7 +683,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             h[v] = hb;
             l[v] = (__bf16)(x - (float)hb);
           }
-          const int off = (4 * cq + e) * KS + pw * RPW + par * 8;
+          const int f = 4 * cq + e;
+          const int off = f * KS + (((2 * pw + par) ^ gi_swz(f)) << 3);
           *reinterpret_cast<bf16x8*>(Hb + off) = h;
           *reinterpret_cast<bf16x8*>(Lb2 + off) = l;
         }
@@ -681,10 +692,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
           const int k = pw * RPW + (lane % RPV) * 8 + lane / RPV;
           const float a0 = sq, a1 = sq * z;
           const __bf16 h0 = (__bf16)a0, h1 = (__bf16)a1;
-          Hb[aug * KS + k] = h0;
-          Lb2[aug * KS + k] = (__bf16)(a0 - (float)h0);
-          Hb[(aug + 1) * KS + k] = h1;
-          Lb2[(aug + 1) * KS + k] = (__bf16)(a1 - (float)h1);
+          const int k0 = aug * KS + ((((k >> 3) ^ gi_swz(aug)) << 3) | (k & 7));
+          const int k1 = (aug + 1) * KS + ((((k >> 3) ^ gi_swz(aug + 1)) << 3) | (k & 7));
+          Hb[k0] = h0;
+          Lb2[k0] = (__bf16)(a0 - (float)h0);
+          Hb[k1] = h1;
+          Lb2[k1] = (__bf16)(a1 - (float)h1);
         }
         return;
       }
@@ -771,15 +784,23 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         const float* wb = wr[i & 1] + kr;
         if constexpr (BF3) {
           if (!(fam.dbg & 1)) {
-            const __bf16* Hb = LB[i & 1][0] + cc * KS + kr * 8;
-            const __bf16* Lo = LB[i & 1][1] + cc * KS + kr * 8;
+            const __bf16* Hb = LB[i & 1][0];
+            const __bf16* Lo = LB[i & 1][1];
+            // feature f = 16 t + cc, k-block kr + 4 ks: gi_swz(f) = s0 ^ 4 (t & 1)
+            // with s0 = gi_swz(cc), so the swizzled offset is one of two
+            // per-lane bases (k-block bit 2 flipped by ks ^ t) + 16 t KS
+            const int s0 = gi_swz(cc);
+            const int B0 = cc * KS + ((kr ^ s0) << 3);
+            const int B1 = B0 ^ 32;
 #pragma unroll 1
             for (int ks = 0; ks < RC / 32; ++ks) {
               bf16x8 ah[T], al[T];
+              const int Be = ks ? B1 : B0, Bo = ks ? B0 : B1;
 #pragma unroll
               for (int t = 0; t < T; ++t) {
-                ah[t] = *reinterpret_cast<const bf16x8*>(Hb + 16 * t * KS + 32 * ks);
-                al[t] = *reinterpret_cast<const bf16x8*>(Lo + 16 * t * KS + 32 * ks);
+                const int off = 16 * t * KS + ((t & 1) ? Bo : Be);
+                ah[t] = *reinterpret_cast<const bf16x8*>(Hb + off);
+                al[t] = *reinterpret_cast<const bf16x8*>(Lo + off);
               }
               gi_mfma3_all<T, SL>(std::make_integer_sequence<int, GI_PPW>{}, ah, al, acc);
             }
