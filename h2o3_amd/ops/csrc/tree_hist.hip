@@ -335,7 +335,7 @@ struct QuadArgs {
   dim3 grid; int threads; size_t lds; hipStream_t s;
   const uint8_t* cc; int Fp; const int* ridx; const float* va; const float* vb; const int4* wk;
   int n_work, n_fg, fgw, F, foff, Bs; float s0, s1; double* hist; int n_slots; double* wyy; long long bq;
-  const uint8_t* need; const int* n_work_dev;
+  const uint8_t* need; const int* n_work_dev; unsigned long long* part = nullptr;
 };
 
 template <int M, bool V, bool PV, bool PK, bool PIPE = true, int LW = 1>
@@ -454,7 +454,8 @@ __global__ __launch_bounds__(1024) void hist_bm_kernel(
     const float* __restrict__ va, const float* __restrict__ vb,
     const int4* __restrict__ work, int n_work, int n_fg, int F, int foff, int Bs, float s0, float s1,
     double* __restrict__ hist, int n_slots, double* __restrict__ wyy_out, long long bq,
-    const uint8_t* __restrict__ need, const int* __restrict__ n_work_dev) {
+    const uint8_t* __restrict__ need, const int* __restrict__ n_work_dev, unsigned long long* __restrict__ part,
+    int dbg) {
   constexpr int C = Chan<MODE>::C;
   constexpr int NK = 4 * LW;              // codes per lane (LW dwords)
   constexpr int LPR = G / NK;             // lanes per row
@@ -570,7 +571,7 @@ __global__ __launch_bounds__(1024) void hist_bm_kernel(
         } else {
           c0 = XB[d][u]; c1 = 0.f;
         }
-        if (!inr || (c0 == 0.f && c1 == 0.f)) continue;
+        if (!inr || (c0 == 0.f && c1 == 0.f) || (dbg & 2)) continue;
         unsigned long long a0, a1 = 0ull;
         if (PACK) {
           // weights are 0/1: count 1, response y; the even magic constant of
@@ -602,10 +603,21 @@ __global__ __launch_bounds__(1024) void hist_bm_kernel(
     v = wave_sum(v);
     if (lane == 0) gbl_add(wyy_out + wk.x, v);
   }
+  if (part != nullptr) {
+    // partial image out with plain coalesced stores; hist_bm_reduce_kernel
+    // sums the partials of each node (a float-atomic flush of every entry ran
+    // at ~1.3 TB/s of added bytes: 35% of a deep level at 12.5M rows)
+    if (dbg & 1) return;
+    const int n2 = Bs * PITCH / 2;
+    const ulonglong2* src = reinterpret_cast<const ulonglong2*>(ldsq);
+    ulonglong2* dst = reinterpret_cast<ulonglong2*>(part + ((size_t)(lb / n_fg) * n_fg + fgi) * (size_t)(Bs * PITCH));
+    for (int i2 = threadIdx.x; i2 < n2; i2 += blockDim.x) dst[i2] = src[i2];
+    return;
+  }
   const double inv0 = 1.0 / (double)s0, inv1 = 1.0 / (double)s1;
   const int si = lane & 15, bi = lane >> 4;
   constexpr int NSG = G / 16;
-  const int nbq = (Bs + 3) >> 2;
+  const int nbq = (dbg & 1) ? 0 : (Bs + 3) >> 2;
   for (int e = wv; e < nbq * NSG; e += nwaves) {
     const int b = (e / NSG) * 4 + bi;
     const int slot = (e % NSG) * 16 + si;
@@ -617,8 +629,15 @@ __global__ __launch_bounds__(1024) void hist_bm_kernel(
       if (v != 0ull) {
         const long long cnt = (long long)(v >> 40);
         const long long low = (long long)(v & ((1ull << 40) - 1));
-        gbl_add(o, (double)cnt);
-        gbl_add(o + 1, (double)(low - cnt * bq) * inv1);
+        if (dbg & 4) {   // timing probe only: integer (L2) atomics at the same addresses
+          unsigned long long* ou = reinterpret_cast<unsigned long long*>(o);
+          __hip_atomic_fetch_add(ou, (unsigned long long)cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_add(ou + 1, (unsigned long long)(low - cnt * bq), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+          gbl_add(o, (double)cnt);
+          gbl_add(o + 1, (double)(low - cnt * bq) * inv1);
+        }
       }
     } else {
       if (v != 0ull) gbl_add(o, (double)(long long)v * inv0);
@@ -630,6 +649,12 @@ __global__ __launch_bounds__(1024) void hist_bm_kernel(
   }
 }
 
+// microbenchmark phase switches (scripts/hist_bm_mb.py): 1 = no flush, 2 = no
+// LDS atomics, 4 = flush with integer atomics.  Results are wrong with any
+// bit set; 0 in production.
+static int g_bm_dbg = 0;
+extern "C" void h2o_hist_bm_set_debug(int flags) { g_bm_dbg = flags; }
+
 template <int G, int CL, int M, bool V, bool PV, bool PK, int LW>
 static int lbm_u(const QuadArgs& a) {
   auto kern = hist_bm_kernel<G, CL, M, V, PV, PK, LW>;
@@ -640,7 +665,8 @@ static int lbm_u(const QuadArgs& a) {
     attr = true;
   }
   hipLaunchKernelGGL(kern, a.grid, dim3(a.threads), a.lds, a.s, a.cc, a.Fp, a.ridx, a.va, a.vb, a.wk, a.n_work,
-                     a.n_fg, a.F, a.foff, a.Bs, a.s0, a.s1, a.hist, a.n_slots, a.wyy, a.bq, a.need, a.n_work_dev);
+                     a.n_fg, a.F, a.foff, a.Bs, a.s0, a.s1, a.hist, a.n_slots, a.wyy, a.bq, a.need, a.n_work_dev,
+                     a.part, g_bm_dbg);
   return (int)hipGetLastError();
 }
 
@@ -670,15 +696,76 @@ static int lbm_g(int mode, bool pack, bool vb, bool posv, const QuadArgs& a) {
   return (int)hipErrorInvalidValue;
 }
 
+// Sum of the per-workgroup partial images of hist_bm_kernel by node: block
+// (tile, group, item chunk) reads a 16-bin x 16-slot tile of up to BM_RED
+// consecutive items' partials (16 x 128-B rows per load, coalesced), sums in
+// int64 (exact, like the LDS accumulation) while the items belong to one
+// node and adds each node's sums to the f64 histogram (16 features x 16
+// consecutive bins per wave-instruction: 256-B contiguous runs).
+#define BM_RED 32
+__global__ __launch_bounds__(256) void hist_bm_reduce_kernel(
+    const unsigned long long* __restrict__ part, const int4* __restrict__ work, int n_work,
+    const int* __restrict__ n_work_dev, int n_fg, int F, int foff, int G, int CL, int lpr, int nk, int Bs, int C,
+    int pack, long long bq, float s0, float s1, const uint8_t* __restrict__ need, double* __restrict__ hist,
+    int n_slots) {
+  const int nw = n_work_dev != nullptr ? n_work_dev[1] : n_work;
+  const int i0 = blockIdx.z * BM_RED;
+  if (i0 >= nw) return;
+  const int i1 = min(nw, i0 + BM_RED);
+  const int g = blockIdx.y;
+  const int PITCH = G * CL;
+  const int nbt = Bs / 16;
+  const int b = (blockIdx.x % nbt) * 16 + (threadIdx.x >> 4);
+  const int sl = (blockIdx.x / nbt) * 16 + (threadIdx.x & 15);
+  const int ch = sl / G, slot = sl - ch * G;
+  const int fg0 = foff + g * G;
+  const int fl = nk * (slot % lpr) + slot / lpr;
+  const bool live = fl < min(G, F - fg0);
+  const double inv0 = 1.0 / (double)s0, inv1 = 1.0 / (double)s1;
+  const size_t E = (size_t)Bs * PITCH;
+  const size_t eoff = (size_t)b * PITCH + sl;
+  long long a0 = 0, a1 = 0;   // PACK: count, response; else: channel value
+  int cur = -1;
+  auto flush = [&]() {
+    if (cur < 0 || !live || (a0 == 0 && a1 == 0)) return;
+    double* o = hist + ((size_t)(fg0 + fl) * n_slots + cur) * (size_t)(Bs * C) + (size_t)b * C;
+    if (pack) {
+      gbl_add(o, (double)a0);
+      gbl_add(o + 1, (double)a1 * inv1);
+    } else {
+      gbl_add(o + ch, (double)a0 * (ch == 0 ? inv0 : inv1));
+    }
+  };
+  for (int i = i0; i < i1; ++i) {
+    const int s = work[i].x;
+    if (need != nullptr && need[(size_t)s * n_fg + g] == 0) continue;   // the workgroup skipped it
+    if (s != cur) {
+      flush();
+      cur = s; a0 = 0; a1 = 0;
+    }
+    const unsigned long long v = part[((size_t)i * n_fg + g) * E + eoff];
+    if (pack) {
+      const long long cnt = (long long)(v >> 40);
+      a0 += cnt;
+      a1 += (long long)(v & ((1ull << 40) - 1)) - cnt * bq;
+    } else {
+      a0 += (long long)v;
+    }
+  }
+  flush();
+}
+
 // Bin-major conflict-free histograms of features [foff, F) in n_fg = ceil((F -
 // foff) / G) groups of G in {16, 32, 64} features (G <= 32 for the two-channel
 // modes); every group's code dwords lie inside the row (foff + n_fg*G <= Fp).
 // pack_bq >= 0 selects the packed single-atomic path (MODE 0, 0/1 weights).
 // n_work_dev != nullptr: device-built work list (n_work = capacity).
+// part != nullptr: [n_work][n_fg][Bs][G*CL] u64 scratch for the two-pass
+// flush (partial images + hist_bm_reduce_kernel); nullptr: f64 atomic flush.
 extern "C" int h2o_hist_bm(const void* codes, int Fp, const int* ridx, const float* va, const float* vb,
                            const int* work, int n_work, int F, int foff, int Bs, float s0, float s1,
                            double* hist, int n_slots, int mode, double* wyy, int posv, long long pack_bq, int G,
-                           const uint8_t* need, const int* n_work_dev, hipStream_t s) {
+                           const uint8_t* need, const int* n_work_dev, unsigned long long* part, hipStream_t s) {
   if (n_work <= 0 || foff >= F) return 0;
   if (Fp % 4 != 0 || foff % 4 != 0 || Bs > 256 || Bs % 4 != 0 || mode < 0 || mode > 2) return -1;
   const bool pack = pack_bq >= 0 && mode == 0;
@@ -693,9 +780,19 @@ extern "C" int h2o_hist_bm(const void* codes, int Fp, const int* ridx, const flo
   a.cc = (const uint8_t*)codes; a.Fp = Fp; a.ridx = ridx; a.va = va; a.vb = vb; a.wk = (const int4*)work;
   a.n_work = n_work; a.n_fg = n_fg; a.fgw = G; a.F = F; a.foff = foff; a.Bs = Bs; a.s0 = s0; a.s1 = s1;
   a.hist = hist; a.n_slots = n_slots; a.wyy = wyy; a.bq = pack_bq; a.need = need; a.n_work_dev = n_work_dev;
-  if (G == 64) return lbm_g<64>(mode, pack, vb != nullptr, posv != 0, a);
-  if (G == 32) return lbm_g<32>(mode, pack, vb != nullptr, posv != 0, a);
-  return lbm_g<16>(mode, pack, vb != nullptr, posv != 0, a);
+  a.part = part;
+  const int rc = G == 64 ? lbm_g<64>(mode, pack, vb != nullptr, posv != 0, a)
+               : G == 32 ? lbm_g<32>(mode, pack, vb != nullptr, posv != 0, a)
+                         : lbm_g<16>(mode, pack, vb != nullptr, posv != 0, a);
+  if (rc != 0 || part == nullptr || (g_bm_dbg & 1)) return rc;
+  static const int lw_env = env_int("H2O3_HIST_BM_LW", 2);
+  const int lw = (lw_env == 1 || G == 16) ? 1 : 2;   // as lbm() picks it
+  const int nk = 4 * lw, lpr = G / nk;
+  const int C = mode == 2 ? 1 : 2;
+  dim3 rg((Bs / 16) * (G * CL / 16), n_fg, (n_work + BM_RED - 1) / BM_RED);
+  hipLaunchKernelGGL(hist_bm_reduce_kernel, rg, dim3(256), 0, s, part, (const int4*)work, n_work, n_work_dev, n_fg,
+                     F, foff, G, CL, lpr, nk, Bs, C, pack ? 1 : 0, pack_bq, s0, s1, need, hist, n_slots);
+  return (int)hipGetLastError();
 }
 
 template <typename CodeT>

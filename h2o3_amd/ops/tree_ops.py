@@ -88,7 +88,7 @@ def _lib():
                                        _c_void, _c_int, _c_ll, _c_int, _c_void, _c_void]
         lib.h2o_hist_bm.argtypes = [_c_void, _c_int, _c_void, _c_void, _c_void, _c_void, _c_int, _c_int, _c_int,
                                     _c_int, ctypes.c_float, ctypes.c_float, _c_void, _c_int, _c_int, _c_void, _c_int,
-                                    _c_ll, _c_int, _c_void, _c_void, _c_void]
+                                    _c_ll, _c_int, _c_void, _c_void, _c_void, _c_void]
         lib.h2o_part_flags.argtypes = [_c_void, _c_int, _c_ll, _c_ll, _c_void, _c_void, _c_void, _c_int, _c_void,
                                        _c_void, _c_int, _c_void, _c_void, _c_void]
         lib.h2o_part_compact.argtypes = [_c_void, _c_void, _c_void, _c_int, _c_void, _c_void, _c_void, _c_void,
@@ -172,6 +172,16 @@ def bm_groups(F: int, Fp: int, Bs: int, one_channel: bool):
     return best
 
 
+def bm_part(n_items, n_fg, Bs, G, one_channel, dev):
+    """Scratch of the two-pass flush of hist_bm_kernel: one u64 partial image
+    [Bs][G * channels] per (work item, group); None = f64 atomic flush
+    (H2O3_HIST_BM_RED=0)."""
+    if os.environ.get("H2O3_HIST_BM_RED", "1") != "1":
+        return None
+    cl = 1 if one_channel else 2
+    return torch.empty(int(n_items) * n_fg * Bs * G * cl, dtype=torch.int64, device=dev)
+
+
 def make_work(starts, counts, slots, chunk):
     """Chunk node segments into (slot, start, count, chunk_id) work items
     (host, vectorized) -> int32 numpy array [n_items, 4]."""
@@ -229,10 +239,11 @@ def _pack_scale(vmax, chunk):
 
 
 # Rows per histogram workgroup: every workgroup zeroes and flushes a full
-# feature-group histogram (fixed cost), so chunks aim at ~64K rows while
-# keeping >= 512 workgroups to fill the chip (scripts/hist_tb_mb.py: 12.5M rows
-# root 0.90 -> 0.76 ms, 100M rows 5.05 -> 4.93 ms vs a fixed 2048 workgroups).
-_HIST_CHUNK_ROWS = 65536
+# feature-group histogram (fixed cost), so chunks aim at ~128K rows while
+# keeping >= 512 workgroups to fill the chip (scripts/hist_bm_mb.py with the
+# two-pass flush of the bin-major kernel: 100M-row root 3.69 -> 3.35 ms,
+# 12.5M-row root 0.59 -> 0.47 ms vs 64K rows, deeper levels unchanged).
+_HIST_CHUNK_ROWS = 131072
 _HIST_MIN_BLOCKS = 512
 
 
@@ -242,7 +253,8 @@ def hist_chunk(total, n_fg, target_blocks=None):
     if tb is not None:
         n_chunks = max(1, int(tb) // n_fg)
     else:
-        n_chunks = max(-(-_HIST_MIN_BLOCKS // n_fg), -(-total // _HIST_CHUNK_ROWS))
+        rows = int(os.environ.get("H2O3_HIST_CHUNK", _HIST_CHUNK_ROWS))
+        n_chunks = max(-(-_HIST_MIN_BLOCKS // n_fg), -(-total // rows))
     return max(2048, -(-total // n_chunks))
 
 
@@ -314,9 +326,10 @@ def hist_build(bd, ridx, va, vb, mode, starts, counts, n_slots, use_native=None,
                 s1, bq = _pack_scale(vmax[1] if vb is None else max(vmax[1], 0.0), chunk)
             need = _need(fgw)
             if bm is not None:
+                part = bm_part(len(items), n_fg, bd.Bs, fgw, pack or mode == 2, dev)
                 rc = lib.h2o_hist_bm(_ptr(bd.codes), bd.Fp, _ptr(ridx), _ptr(va), _ptr(vb), _ptr(work), len(items),
                                      bd.F, 0, bd.Bs, s0, s1, _ptr(hist), n_slots, mode, _ptr(wyy), 1 if posv else 0,
-                                     bq, fgw, _ptr(need), None, _stream())
+                                     bq, fgw, _ptr(need), None, _ptr(part), _stream())
                 if rc != 0:
                     raise RuntimeError(f"h2o_hist_bm failed: error {rc} (F={bd.F}, Fp={bd.Fp}, G={fgw})")
                 return ret()
@@ -813,9 +826,10 @@ def hist_build_dev(bd, ridx, va, vb, mode, rec, rec_cols, starts, counts, vmax, 
     if pack:
         s1, bq = _pack_scale(vmax[1] if vb is None else max(vmax[1], 0.0), chunk)
     if bm is not None:
+        part = bm_part(cap, n_fg, bd.Bs, fgw, pack or mode == 2, dev)
         rc = lib.h2o_hist_bm(_ptr(bd.codes), bd.Fp, _ptr(ridx), _ptr(va), _ptr(vb), _ptr(work), cap, bd.F, 0, bd.Bs,
                              s0, s1, _ptr(Hb), n, mode, _ptr(wyy), 1 if posv else 0, bq, fgw, None, _ptr(cnts),
-                             _stream())
+                             _ptr(part), _stream())
         if rc != 0:
             raise RuntimeError(f"h2o_hist_bm failed: {rc}")
         return Hb, wyy, slots, cnts
