@@ -344,8 +344,11 @@ class TreeGrower:
         if bool(is_cat.all()):
             return self._find_splits_torch(H, col_mask, node_wyy)
         if not bool(is_cat.any()):
-            res = self._find_splits_native(H, col_mask, node_wyy, want_pk=want_pk)
-            if self.W > 1:
+            # want_pk on a numeric-only frame: every rank takes the packed-record
+            # path (split_select2 + one record merge), so the collectives match
+            res = self._find_splits_native(H, col_mask, node_wyy,
+                                           want_pk=want_pk and not any(self.bd.is_cat))
+            if self.W > 1 and "pk" not in res:
                 res = self._merge_candidates(res, H.shape[1], H.shape[2], H.shape[3])
             return res
         cm_num = col_mask.clone()
@@ -403,7 +406,7 @@ class TreeGrower:
                                 ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
         if rc != 0:
             raise RuntimeError(f"h2o_split_find failed: {rc}")
-        if C == 2 and self.f0 < self.bd.F and want_pk and self.W == 1:
+        if C == 2 and want_pk and (self.W > 1 or self.f0 < self.bd.F):
             # selection + split decision + partition inputs in one kernel; the
             # packed record (12 doubles per node) is what the host fetches
             if not getattr(lib, "_typed_sel2", False):
@@ -414,13 +417,22 @@ class TreeGrower:
             pk = torch.empty((n, 12), dtype=torch.float64, device=self.dev)
             mask = torch.empty((n, Bs), dtype=torch.uint8, device=self.dev)
             feat_i = torch.empty(n, dtype=torch.int32, device=self.dev)
-            min_w2 = -1.0 if p.criterion == "xgb" else 2.0 * float(p.min_rows)
-            rc = lib.h2o_split_select2(ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(H.data_ptr()), Fl, n, Bs,
-                                       self.f0, min_w2, 12, ctypes.c_void_p(pk.data_ptr()),
-                                       ctypes.c_void_p(mask.data_ptr()), ctypes.c_void_p(feat_i.data_ptr()),
-                                       ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
-            if rc != 0:
-                raise RuntimeError(f"h2o_split_select2 failed: {rc}")
+            if self.f0 < self.bd.F:
+                min_w2 = -1.0 if p.criterion == "xgb" else 2.0 * float(p.min_rows)
+                rc = lib.h2o_split_select2(ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(H.data_ptr()), Fl, n,
+                                           Bs, self.f0, min_w2, 12, ctypes.c_void_p(pk.data_ptr()),
+                                           ctypes.c_void_p(mask.data_ptr()), ctypes.c_void_p(feat_i.data_ptr()),
+                                           ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+                if rc != 0:
+                    raise RuntimeError(f"h2o_split_select2 failed: {rc}")
+            else:
+                # a rank holding only padding features: a never-winning record
+                pk.zero_()
+                pk[:, 0] = NEG_INF
+                mask.zero_()
+                feat_i.zero_()
+            if self.W > 1:
+                pk, mask, feat_i = self._merge_records(pk, mask)
             return {"pk": pk, "feat_i32": feat_i, "mask": mask, "gain": pk[:, 0], "feat": pk[:, 1], "t": pk[:, 2],
                     "opt": pk[:, 3], "L": pk[:, 4:6], "R": pk[:, 6:8], "tot": pk[:, 8:10]}
         if C == 2 and self.f0 < self.bd.F:
@@ -1040,6 +1052,22 @@ class TreeGrower:
         res = {"gain": best, "feat": gidx[fl], "t": t, "opt": opt, "na_left": na_left,
                "mask": mask.to(torch.uint8), "L": Lw, "R": Rw, "tot": T[:, 0] if Fl > 0 else None}
         return res
+
+    def _merge_records(self, pk, mask):
+        """Multi-GPU merge of the per-rank packed split records (split_select2
+        over each rank's feature slice): two all-gathers (records, go-left
+        masks as bytes), the highest gain wins per node, ties to the lowest
+        rank (= lowest feature).  Node totals are global on every rank (the
+        histograms were reduce-scattered), so the winner's record is complete."""
+        W = self.W
+        n = pk.shape[0]
+        g = coll.all_gather_dim0(pk.contiguous()).view(W, n, -1)
+        gm = coll.all_gather_dim0(mask.contiguous()).view(W, n, -1)
+        best_r = torch.argmax(g[:, :, 0], 0)
+        ar = torch.arange(n, device=pk.device)
+        pk_w = g[best_r, ar].contiguous()
+        mask_w = gm[best_r, ar].contiguous()
+        return pk_w, mask_w, pk_w[:, 1].to(torch.int32)
 
     def _merge_candidates(self, res, n, Bs, C):
         W = self.W

@@ -60,6 +60,13 @@ def run(out_path):
     gbm.train(x=x, y="y", training_frame=fr)
     res["gbm_trees"] = _trees(gbm)
     res["gbm_logloss"] = gbm.logloss()
+    # numeric-only frame: the packed-record split path (per-rank split_select2,
+    # record + mask all-gather, async partition, look-ahead histograms)
+    xn = [c for c in x if c != "c0"]
+    gbm2 = H2OGradientBoostingEstimator(ntrees=4, max_depth=7, seed=1, min_rows=20)
+    gbm2.train(x=xn, y="y", training_frame=fr)
+    res["gbm2_trees"] = _trees(gbm2)
+    res["gbm2_logloss"] = gbm2.logloss()
     from h2o3_amd.ops import _native
     res["native"] = _native.loaded_libs()
     if cloud.rank() == 0:

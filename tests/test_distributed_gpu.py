@@ -59,7 +59,7 @@ def test_two_ranks_one_gpu_grow_same_trees(tmp_path):
     two = _run(2, str(tmp_path / "w2.json"))
     assert one["world"] == 1 and two["world"] == 2 and two["backend"] == "gloo"
     assert any("libtree_hist.so" in s for s in two["native"]) and any("libtree_split.so" in s for s in two["native"])
-    for key in ("drf_trees", "gbm_trees"):
+    for key in ("drf_trees", "gbm_trees", "gbm2_trees"):
         assert len(one[key]) == len(two[key])
         for t1, t2 in zip(one[key], two[key]):
             assert t1["feat"] == t2["feat"], key
@@ -67,3 +67,4 @@ def test_two_ranks_one_gpu_grow_same_trees(tmp_path):
             np.testing.assert_allclose(t1["thr"], t2["thr"], rtol=1e-6, atol=1e-9)
     np.testing.assert_allclose(one["drf_pred"], two["drf_pred"], rtol=1e-5, atol=1e-5)
     assert abs(one["gbm_logloss"] - two["gbm_logloss"]) < 1e-5
+    assert abs(one["gbm2_logloss"] - two["gbm2_logloss"]) < 1e-5
