@@ -214,7 +214,7 @@ class TreeGrower:
         mono = params.monotone if params.monotone is not None else np.zeros(F)
         self.mono_t = torch.tensor(list(mono) + [0] * (self.Fpad - F), dtype=torch.float64, device=self.dev)
         self.rng = np.random.RandomState(params.seed & 0x7FFFFFFF)
-        if os.environ.get("H2O3_HIST_BUDGET"):
+        if tree_ops.env("H2O3_HIST_BUDGET"):
             params.hist_mem_budget = int(os.environ["H2O3_HIST_BUDGET"])
 
     # ------------------------------------------------------------------ hist
@@ -260,7 +260,7 @@ class TreeGrower:
         sampled columns plus each rank's first local feature (node totals come
         from H[0]).  None = all (no column sampling / no GPU kernels)."""
         if self.dev.type != "cuda" or getattr(cm, "_all_true", False) or self.p.criterion.startswith("uplift") \
-                or os.environ.get("H2O3_HIST_NEED", "1") == "0":
+                or tree_ops.env("H2O3_HIST_NEED", "1") == "0":
             return None
         need = cm.to(self.dev, dtype=torch.bool).clone()
         for r in range(self.W):
@@ -403,7 +403,7 @@ class TreeGrower:
                                 ctypes.c_void_p(ok.data_ptr()), ctypes.c_void_p(mono.data_ptr()),
                                 float(p.min_rows), float(p.min_split_improvement), float(p.reg_lambda),
                                 float(p.reg_alpha), float(p.gamma), crit, ctypes.c_void_p(out.data_ptr()),
-                                ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+                                tree_ops._stream())
         if rc != 0:
             raise RuntimeError(f"h2o_split_find failed: {rc}")
         if C == 2 and want_pk and (self.W > 1 or self.f0 < self.bd.F):
@@ -422,7 +422,7 @@ class TreeGrower:
                 rc = lib.h2o_split_select2(ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(H.data_ptr()), Fl, n,
                                            Bs, self.f0, min_w2, 12, ctypes.c_void_p(pk.data_ptr()),
                                            ctypes.c_void_p(mask.data_ptr()), ctypes.c_void_p(feat_i.data_ptr()),
-                                           ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+                                           tree_ops._stream())
                 if rc != 0:
                     raise RuntimeError(f"h2o_split_select2 failed: {rc}")
             else:
@@ -446,7 +446,7 @@ class TreeGrower:
             mask = torch.empty((n, Bs), dtype=torch.uint8, device=self.dev)
             rc = lib.h2o_split_select(ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(H.data_ptr()), Fl, n, Bs,
                                       self.f0, ctypes.c_void_p(pk.data_ptr()), ctypes.c_void_p(mask.data_ptr()),
-                                      ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+                                      tree_ops._stream())
             if rc != 0:
                 raise RuntimeError(f"h2o_split_select failed: {rc}")
             opt = pk[:, 3].long()
@@ -532,7 +532,7 @@ class TreeGrower:
         (=1); never (=0).  Measured on the DRF config (10M x 500, 100
         categoricals of cardinality 1000): 995 ms/tree with level histograms,
         ~500 ms/tree with pair histograms at every sampled level."""
-        env = os.environ.get("H2O3_PAIR_DIRECT", "auto")
+        env = tree_ops.env("H2O3_PAIR_DIRECT", "auto")
         if env == "0" or mode not in (0, 1) or self.p.criterion.startswith("uplift") or \
                 not self._sampled_cols(depth):
             return False
@@ -672,7 +672,7 @@ class TreeGrower:
                                  ctypes.c_void_p(pfeat.data_ptr()), ctypes.c_void_p(self._fcat_u8.data_ptr()),
                                  1 if p.criterion == "xgb" else 0, min_w2, 12, ctypes.c_void_p(pk.data_ptr()),
                                  ctypes.c_void_p(mask.data_ptr()), ctypes.c_void_p(feat_i.data_ptr()),
-                                 ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+                                 tree_ops._stream())
         if rc != 0:
             raise RuntimeError(f"h2o_pair_select failed: {rc}")
 
@@ -868,7 +868,7 @@ class TreeGrower:
         rc = lib.h2o_cat_pairs(ptr(H), n, Bs, C, P, ptr(pf), ptr(pn), ptr(pc), ptr(pm), ptr(wyy),
                                float(p.min_rows), float(p.min_split_improvement), float(p.reg_lambda),
                                float(p.reg_alpha), float(p.gamma), 1 if p.criterion == "xgb" else 0, ptr(res),
-                               ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+                               tree_ops._stream())
         if rc != 0:
             raise RuntimeError(f"h2o_cat_pairs failed: {rc}")
         if raw:
@@ -1093,10 +1093,16 @@ class TreeGrower:
         """True when grow() keeps the 0/1-weighted mode-0 response as a
         position-ordered NaN-masked payload (quad histogram kernels)."""
         return self.dev.type == "cuda" and not self.use_payload and self.bd.code_bytes == 1 and \
-            self.bd.Bs <= 256 and self.bd.Fp % 16 == 0 and os.environ.get("H2O3_HIST_KERNEL", "quad") == "quad" \
-            and os.environ.get("H2O3_POSV", "1") == "1" and os.environ.get("H2O3_PART", "ballot") == "ballot"
+            self.bd.Bs <= 256 and self.bd.Fp % 16 == 0 and tree_ops.env("H2O3_HIST_KERNEL", "quad") == "quad" \
+            and tree_ops.env("H2O3_POSV", "1") == "1" and tree_ops.env("H2O3_PART", "ballot") == "ballot"
 
     def grow(self, va, vb, mode, tree_node_hook=None, want_nid=True, vmax=None, unit_w=None, va_scratch=False):
+        """Grow one tree (environment switches read once per tree); see _grow."""
+        with tree_ops.env_scope():
+            return self._grow(va, vb, mode, tree_node_hook=tree_node_hook, want_nid=want_nid, vmax=vmax,
+                              unit_w=unit_w, va_scratch=va_scratch)
+
+    def _grow(self, va, vb, mode, tree_node_hook=None, want_nid=True, vmax=None, unit_w=None, va_scratch=False):
         """Grow one tree.  Returns (Tree, nid[N] leaf index per local row,
         leaf_nodes list (tree node ids, indexed by nid), leaf_tot [n_leaves, C]).
         vmax / unit_w: caller-known bounds (max |channel| for the fixed-point
@@ -1105,6 +1111,7 @@ class TreeGrower:
         bd, p = self.bd, self.p
         N = bd.nrows_local
         C = tree_ops.channels(mode)
+        self._stream_obj = torch.cuda.current_stream() if self.dev.type == "cuda" else None
         torch.arange(N, dtype=torch.int32, device=self.dev, out=self.ridx)
         if self.dev.type != "cuda":
             self._vmax = None
@@ -1115,12 +1122,12 @@ class TreeGrower:
             vb is None or (bool(unit_w) if unit_w is not None else bool(((vb == 0) | (vb == 1)).all())))
         self._va_eff = None
         quad = self.bd.code_bytes == 1 and self.bd.Bs <= 256 and self.bd.Fp % 16 == 0 and \
-            os.environ.get("H2O3_HIST_KERNEL", "quad") == "quad"
+            tree_ops.env("H2O3_HIST_KERNEL", "quad") == "quad"
         if self._unit_w and not self.use_payload and quad:
             self._va_eff = torch.where(vb > 0, va, torch.full_like(va, float("nan"))) if vb is not None else va
         self._pos1 = None
-        if self._va_eff is not None and os.environ.get("H2O3_POSV", "1") == "1" and \
-                os.environ.get("H2O3_PART", "ballot") == "ballot":
+        if self._va_eff is not None and tree_ops.env("H2O3_POSV", "1") == "1" and \
+                tree_ops.env("H2O3_PART", "ballot") == "ballot":
             # va_scratch: the caller hands over va (a NaN-masked residual it
             # will not read again) as the root payload -- no copy
             p0 = self._va_eff.clone() if (self._va_eff is va and not va_scratch) else self._va_eff
@@ -1151,7 +1158,7 @@ class TreeGrower:
         leaf_parts = []    # per level: (node ids, starts, counts, totals [k, C])
         level = 0
         async_part = self.dev.type == "cuda" and not p.max_leaves and not self.use_payload and \
-            os.environ.get("H2O3_ASYNC_PART", "1") == "1" and os.environ.get("H2O3_PART", "ballot") == "ballot"
+            tree_ops.env("H2O3_ASYNC_PART", "1") == "1" and tree_ops.env("H2O3_PART", "ballot") == "ballot"
         is_cat_np = np.asarray(bd.is_cat, dtype=bool)
         cutmat = self._cut_matrix()
         lvmaps = self.__dict__.setdefault("_lvmaps", {})
@@ -1173,7 +1180,7 @@ class TreeGrower:
                 # host read the previous level's decisions (_lookahead)
                 H = la[0][:, :n_front].contiguous()
                 wyy_level = la[1][:n_front] if la[1] is not None else None
-                if os.environ.get("H2O3_LA_CHECK") == "1":
+                if tree_ops.env("H2O3_LA_CHECK") == "1":
                     self._la_check(la, p_build, p_der, p_par)
             elif chunked:
                 # frontier too wide for one level of histograms, or column-sampled
@@ -1459,15 +1466,20 @@ class TreeGrower:
             buf = ring[k] = torch.empty(max(t.numel(), 4096), dtype=t.dtype, pin_memory=True)
         h = buf[:t.numel()].view(t.shape)
         h.copy_(t, non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
-        return (h, ev)
+        # one reusable event per slot, recorded on the stream cached by grow()
+        evs = self.__dict__.setdefault("_d2h_ev", [None, None])
+        if evs[k] is None:
+            evs[k] = torch.cuda.Event()
+        st = getattr(self, "_stream_obj", None)
+        evs[k].record(st if st is not None else torch.cuda.current_stream())
+        return (h, evs[k])
 
     @staticmethod
     def _d2h_wait(hev):
         h, ev = hev
         if ev is not None:
             ev.synchronize()
+            tree_ops.host_synced()   # every copy queued before the record has completed
         return h.numpy().copy()
 
     def _maybe_lookahead(self, rec, cols, f_st, f_ct, mode, va, vb, ridx_next, H, wyy_level, depth, level_bytes,
@@ -1480,7 +1492,7 @@ class TreeGrower:
         next level is built after the sync as before."""
         self._la = None
         p = self.p
-        if os.environ.get("H2O3_LOOKAHEAD", "1") != "1" or self.dev.type != "cuda" or chunked or H is None or \
+        if tree_ops.env("H2O3_LOOKAHEAD", "1") != "1" or self.dev.type != "cuda" or chunked or H is None or \
                 depth + 1 >= p.max_depth or mode not in (0, 1) or p.max_leaves:
             return
         if 2 * level_bytes + H.numel() * 8 > p.hist_mem_budget:

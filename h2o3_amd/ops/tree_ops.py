@@ -22,35 +22,57 @@ _c_ll = ctypes.c_longlong
 
 
 
+# Host-synchronisation epoch: bumped whenever the host has waited for the
+# stream to drain (host_synced()), so a staging slot written before the last
+# bump is known to be consumed -- no per-upload event record / query.
+_sync_epoch = 0
+
+
+def host_synced():
+    """Tell the upload ring that every copy queued so far has completed (the
+    caller just waited on an event recorded after them, on the same stream)."""
+    global _sync_epoch
+    _sync_epoch += 1
+
+
 class _PinnedRing:
-    """Reusable pinned staging buffers for the small per-level host->device
-    uploads (work items, per-chunk metadata, column masks).  A copy from a
-    pinned slot is truly asynchronous; the slot's event is waited on before
-    the slot is reused, so the host never overwrites bytes a pending copy
-    still reads (no reliance on pageable-memory staging semantics)."""
+    """Reusable staging for the small per-level host->device uploads (work
+    items, per-chunk metadata, column masks): pinned host slots and device
+    slots, both reused.  A copy from a pinned slot is truly asynchronous; a
+    slot is only rewritten after the host has synchronised with the stream
+    since its last use (else it synchronises first), so no pending copy ever
+    reads overwritten bytes.  Device slots are consumed by kernels queued
+    after the copy on the same stream, and a later copy into the slot is
+    queued behind them: stream order keeps them intact.  (Per-upload events
+    and device allocations cost ~30 us of host time per upload.)"""
 
     def __init__(self, n=16):
         self.bufs = [None] * n
-        self.events = [None] * n
+        self.dbufs = [None] * n
+        self.epoch = [-1] * n
         self.i = 0
 
     def upload(self, a: np.ndarray, dev):
         k = self.i
         self.i = (self.i + 1) % len(self.bufs)
-        ev = self.events[k]
-        if ev is not None:
-            ev.synchronize()
+        if self.epoch[k] == _sync_epoch:
+            torch.cuda.current_stream(dev).synchronize()
+            host_synced()
         nb = max(a.nbytes, 8)
         buf = self.bufs[k]
         if buf is None or buf.numel() < nb:
-            buf = self.bufs[k] = torch.empty(max(nb, 1 << 16), dtype=torch.uint8, pin_memory=True)
+            cap = max(nb, 1 << 16)
+            buf = self.bufs[k] = torch.empty(cap, dtype=torch.uint8, pin_memory=True)
+            self.dbufs[k] = torch.empty(cap, dtype=torch.uint8, device=dev)
+        dbuf = self.dbufs[k]
+        if dbuf.device != torch.device(dev) if not isinstance(dev, torch.device) else dbuf.device != dev:
+            dbuf = self.dbufs[k] = torch.empty(buf.numel(), dtype=torch.uint8, device=dev)
         tdt = torch.from_numpy(a[:0]).dtype
         stage = buf[:a.nbytes].view(tdt).view(a.shape)
-        stage.copy_(torch.from_numpy(a))
-        out = stage.to(dev, non_blocking=True)
-        if ev is None:
-            ev = self.events[k] = torch.cuda.Event()
-        ev.record()
+        stage.numpy()[...] = a
+        out = dbuf[:a.nbytes].view(tdt).view(a.shape)
+        out.copy_(stage, non_blocking=True)
+        self.epoch[k] = _sync_epoch
         return out
 
 
@@ -73,7 +95,47 @@ def _ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
 
 
+# Environment switches read on the per-level hot path: inside a tree build
+# (env_scope) each key is read once per tree, elsewhere every call reads
+# os.environ (tests flip switches between direct kernel calls).
+_ENV_CACHE = None
+
+
+def env(key, default=None):
+    c = _ENV_CACHE
+    if c is None:
+        return os.environ.get(key, default)
+    k = (key, default)
+    v = c.get(k, c)
+    if v is c:
+        v = c[k] = os.environ.get(key, default)
+    return v
+
+
+class env_scope:
+    """Cache environment switches for the duration of one tree build."""
+
+    def __enter__(self):
+        global _ENV_CACHE
+        self._prev = _ENV_CACHE
+        _ENV_CACHE = {}
+        return self
+
+    def __exit__(self, *exc):
+        global _ENV_CACHE
+        _ENV_CACHE = self._prev
+        return False
+
+
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+_get_device = getattr(torch._C, "_cuda_getDevice", None)
+
+
 def _stream():
+    """Current HIP stream as a ctypes pointer (the raw C getters: ~10x cheaper
+    than torch.cuda.current_stream(), called for every kernel launch)."""
+    if _raw_stream is not None and _get_device is not None:
+        return ctypes.c_void_p(_raw_stream(_get_device()))
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
@@ -114,7 +176,7 @@ def feature_group(F: int, Bs: int, mode: int, budget: int = _LDS_BUDGET) -> int:
     Minimises wave-instructions per row, ~ n_groups / floor(64 / FGL), under
     the LDS budget; ties go to fewer groups (less re-reading of row data)."""
     import os
-    if os.environ.get("H2O3_HIST_FGL"):
+    if env("H2O3_HIST_FGL"):
         return max(1, min(64, int(os.environ["H2O3_HIST_FGL"]), F))
     C = channels(mode)
     fmax = max(1, min(64, budget // (Bs * C * 8)))
@@ -141,7 +203,7 @@ def quad_groups(F: int, Fp: int, Bs: int, pack: bool, budget: int = _LDS_BUDGET)
     rows: scripts/hist_fsweep_mb.py).  F = 100, 256 bins, packed -> 3 x 36."""
     CL = 1 if pack else 2
     fmax = max(4, min(64, (budget // ((Bs * CL + CL) * 8)) // 4 * 4))
-    fmax = int(os.environ.get("H2O3_HIST_FGW", fmax))
+    fmax = int(env("H2O3_HIST_FGW", fmax))
     n_fg = -(-F // fmax)
     while True:
         fgw = -(-(-(-F // n_fg)) // 4) * 4
@@ -157,7 +219,7 @@ def bm_groups(F: int, Fp: int, Bs: int, one_channel: bool):
     histogram (Bs x G x channels x 8 B) fits 160 KB; None when no width fits
     (the grouped-lane kernel then runs).  F = 100 (Fp 128), 256 bins: packed
     -> 2 x 64 (128 KB), two channels -> 4 x 32."""
-    if os.environ.get("H2O3_HIST_BM", "1") != "1" or Bs > 256 or Bs % 4 or Fp % 4:
+    if env("H2O3_HIST_BM", "1") != "1" or Bs > 256 or Bs % 4 or Fp % 4:
         return None
     cl = 1 if one_channel else 2
     best = None
@@ -176,7 +238,7 @@ def bm_part(n_items, n_fg, Bs, G, one_channel, dev):
     """Scratch of the two-pass flush of hist_bm_kernel: one u64 partial image
     [Bs][G * channels] per (work item, group); None = f64 atomic flush
     (H2O3_HIST_BM_RED=0)."""
-    if os.environ.get("H2O3_HIST_BM_RED", "1") != "1":
+    if env("H2O3_HIST_BM_RED", "1") != "1":
         return None
     cl = 1 if one_channel else 2
     return torch.empty(int(n_items) * n_fg * Bs * G * cl, dtype=torch.int64, device=dev)
@@ -249,11 +311,11 @@ _HIST_MIN_BLOCKS = 512
 
 def hist_chunk(total, n_fg, target_blocks=None):
     """Rows per work item for `total` rows over n_fg feature groups."""
-    tb = os.environ.get("H2O3_HIST_TB", target_blocks)
+    tb = env("H2O3_HIST_TB", target_blocks)
     if tb is not None:
         n_chunks = max(1, int(tb) // n_fg)
     else:
-        rows = int(os.environ.get("H2O3_HIST_CHUNK", _HIST_CHUNK_ROWS))
+        rows = int(env("H2O3_HIST_CHUNK", _HIST_CHUNK_ROWS))
         n_chunks = max(-(-_HIST_MIN_BLOCKS // n_fg), -(-total // rows))
     return max(2048, -(-total // n_chunks))
 
@@ -282,14 +344,14 @@ def hist_build(bd, ridx, va, vb, mode, starts, counts, n_slots, use_native=None,
     native = dev.type == "cuda" if use_native is None else use_native
     if native:
         lib = _lib()
-        kern = os.environ.get("H2O3_HIST_KERNEL", "quad")
+        kern = env("H2O3_HIST_KERNEL", "quad")
         total = int(sum(counts))
         if total == 0:
             return ret()
         quad = bd.code_bytes == 1 and bd.Fp % 4 == 0 and bd.Bs <= 256 and kern == "quad" and mode in (0, 1, 2)
-        pack = quad and mode == 0 and unit_w and os.environ.get("H2O3_HIST_PACK", "1") == "1"
+        pack = quad and mode == 0 and unit_w and env("H2O3_HIST_PACK", "1") == "1"
         # H2O3_HIST_BIG=1 (A/B): one 1024-thread workgroup per CU with up to 160 KB of LDS histogram
-        big = os.environ.get("H2O3_HIST_BIG", "0") == "1"
+        big = env("H2O3_HIST_BIG", "0") == "1"
         qbudget = 156 * 1024 if big else _LDS_BUDGET
         bm = None
         if quad:
@@ -609,7 +671,7 @@ def partition(bd, ridx, ridx_out, feats, masks, starts, counts, use_native=None,
             codes, rs, fs = bd.codes_col, 1, bd.nrows_local
         else:
             codes, rs, fs = bd.codes, bd.Fp, 1
-        ballot = os.environ.get("H2O3_PART", "ballot") == "ballot" and (payload is None or payload[1] is None)
+        ballot = env("H2O3_PART", "ballot") == "ballot" and (payload is None or payload[1] is None)
         if ballot:
             words = (items[:, 2].astype(np.int64) + 63) // 64
             fb_h = (np.cumsum(words) - words).astype(np.int32)
@@ -677,9 +739,9 @@ def _part_chunk(total):
     """Rows per partition work item: 16K at 100M rows (6K+ workgroups); at
     smaller row counts down to 4K so the flag / compaction passes still see
     ~2K workgroups (12.5M rows: 763 -> 2035)."""
-    env = os.environ.get("H2O3_PART_CHUNK")
-    if env:
-        return int(env)
+    ev = env("H2O3_PART_CHUNK")
+    if ev:
+        return int(ev)
     return int(max(4096, min(16384, -(-int(total) // 2048 // 64) * 64)))
 
 
@@ -718,7 +780,7 @@ def partition_async(bd, ridx, ridx_out, feat_d, masks, starts, counts, chunk=Non
     meta = buf[: 8 * nw].view(torch.int64)
     work = buf[8 * nw: 12 * nw]
     fbase = buf[12 * nw:]
-    if chunk % 64 == 0 and os.environ.get("H2O3_PART_ITEMS", "dev") == "dev":
+    if chunk % 64 == 0 and env("H2O3_PART_ITEMS", "dev") == "dev":
         # per-chunk records written on the device from the O(frontier) segment table
         if not getattr(lib, "_typed_items", False):
             lib.h2o_part_items.argtypes = [_c_void, _c_int, _c_int, _c_int, _c_void, _c_void, _c_void, _c_void]
@@ -781,7 +843,7 @@ def hist_build_dev(bd, ridx, va, vb, mode, rec, rec_cols, starts, counts, vmax, 
     not apply (the caller then builds after the host sync as before)."""
     dev = ridx.device
     if dev.type != "cuda" or bd.code_bytes != 1 or bd.Fp % 4 != 0 or bd.Bs > 256 or mode not in (0, 1, 2) or \
-            os.environ.get("H2O3_HIST_KERNEL", "quad") != "quad":
+            env("H2O3_HIST_KERNEL", "quad") != "quad":
         return None
     lib = _lib()
     if not getattr(lib, "_typed_dev", False):
@@ -795,7 +857,7 @@ def hist_build_dev(bd, ridx, va, vb, mode, rec, rec_cols, starts, counts, vmax, 
         lib._typed_dev = True
     n = len(starts)
     C = channels(mode)
-    pack = mode == 0 and unit_w and os.environ.get("H2O3_HIST_PACK", "1") == "1"
+    pack = mode == 0 and unit_w and env("H2O3_HIST_PACK", "1") == "1"
     bm = bm_groups(bd.F, bd.Fp, bd.Bs, pack or mode == 2)
     n_fg, fgw = bm if bm is not None else quad_groups(bd.F, bd.Fp, bd.Bs, pack)
     total = int(sum(counts))

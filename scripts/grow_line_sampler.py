@@ -22,7 +22,7 @@ def sampler():
         if inner is not None:
             cnt2[(inner.f_code.co_filename.split('/h2o3_amd/')[1], inner.f_code.co_name, inner.f_lineno)] += 1
         while f is not None:
-            if f.f_code.co_name == 'grow' and f.f_code.co_filename.endswith('engine.py'):
+            if f.f_code.co_name in ('grow', '_grow') and f.f_code.co_filename.endswith('engine.py'):
                 cnt[f.f_lineno] += 1
                 break
             f = f.f_back
