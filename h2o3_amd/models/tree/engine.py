@@ -245,15 +245,29 @@ class TreeGrower:
             H, wyy = tree_ops.hist_build(self.bd, ridx, va, vb, mode, starts, counts, len(starts), vmax=self._vmax,
                                          posv=posv, want_wyy=True,
                                          unit_w=getattr(self, "_unit_w", False), need_mask=need_mask)
-        if wyy is not None:
-            coll.allreduce_(wyy)
-        self._last_wyy = wyy
         if self.W > 1:
-            if self.Fpad > self.bd.F:
-                H = torch.cat([H, torch.zeros((self.Fpad - self.bd.F,) + tuple(H.shape[1:]), dtype=H.dtype,
-                                              device=H.device)], 0)
-            H = coll.reduce_scatter_dim0(H)
+            H, wyy = self._rs_hist_wyy(H, wyy)
+        self._last_wyy = wyy
         return H  # [Fl, n, Bs, C]
+
+    def _rs_hist_wyy(self, H, wyy):
+        """Multi-GPU reduce of a level histogram [F, n, Bs, C]: reduce-scatter
+        by feature (each rank keeps its Fl features), with the per-node w*y*y
+        sums riding along -- every rank's chunk carries a copy of its local
+        wyy, so the scattered chunk ends in the global sums: ONE collective
+        per level instead of reduce_scatter + all_reduce."""
+        W = self.W
+        if self.Fpad > self.bd.F:
+            H = torch.cat([H, torch.zeros((self.Fpad - self.bd.F,) + tuple(H.shape[1:]), dtype=H.dtype,
+                                          device=H.device)], 0)
+        if wyy is None:
+            return coll.reduce_scatter_dim0(H), None
+        n = wyy.numel()
+        loc = H.shape[1:]
+        buf = torch.cat([H.reshape(W, -1), wyy.to(H.dtype).view(1, n).expand(W, n)], 1)
+        out = coll.reduce_scatter_dim0(buf).view(-1)
+        chunk = out.numel() - n
+        return out[:chunk].view((self.Fl,) + tuple(loc)), out[chunk:]
 
     def _hist_need(self, cm):
         """Per-node features whose histograms the split search reads: the
@@ -1060,13 +1074,17 @@ class TreeGrower:
         rank (= lowest feature).  Node totals are global on every rank (the
         histograms were reduce-scattered), so the winner's record is complete."""
         W = self.W
-        n = pk.shape[0]
-        g = coll.all_gather_dim0(pk.contiguous()).view(W, n, -1)
-        gm = coll.all_gather_dim0(mask.contiguous()).view(W, n, -1)
-        best_r = torch.argmax(g[:, :, 0], 0)
+        n, Bs = mask.shape
+        # ONE all-gather: the record's bytes and the mask bytes side by side
+        rb = pk.shape[1] * 8
+        buf = torch.cat([pk.contiguous().view(torch.uint8).view(n, rb), mask.contiguous()], 1)
+        g = coll.all_gather_dim0(buf).view(W, n, rb + Bs)
+        gains = g[:, :, :8].contiguous().view(torch.float64).view(W, n)
+        best_r = torch.argmax(gains, 0)
         ar = torch.arange(n, device=pk.device)
-        pk_w = g[best_r, ar].contiguous()
-        mask_w = gm[best_r, ar].contiguous()
+        win = g[best_r, ar]
+        pk_w = win[:, :rb].contiguous().view(torch.float64).view(n, -1)
+        mask_w = win[:, rb:].contiguous()
         return pk_w, mask_w, pk_w[:, 1].to(torch.int32)
 
     def _merge_candidates(self, res, n, Bs, C):
@@ -1509,13 +1527,8 @@ class TreeGrower:
             if r is None:
                 return
             Hb, wyy_b, slots, cnts = r
-            if wyy_b is not None:
-                coll.allreduce_(wyy_b)
             if self.W > 1:
-                if self.Fpad > self.bd.F:
-                    Hb = torch.cat([Hb, torch.zeros((self.Fpad - self.bd.F,) + tuple(Hb.shape[1:]), dtype=Hb.dtype,
-                                                    device=Hb.device)], 0)
-                Hb = coll.reduce_scatter_dim0(Hb)
+                Hb, wyy_b = self._rs_hist_wyy(Hb, wyy_b)
             clamp = {0: 0b1, 1: 0b0}.get(mode, (1 << tree_ops.channels(mode)) - 1)
             Hn, wyy_n = tree_ops.hist_sibling_dev(Hb, H, slots, cnts, clamp, wyy_b=wyy_b if mode == 0 else None,
                                                   wyy_prev=wyy_level if mode == 0 else None)
