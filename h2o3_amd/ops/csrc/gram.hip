@@ -124,7 +124,7 @@ struct GlmFamArgs {
 
 __device__ __forceinline__ float gi_linkinv(int link, float eta) {
   switch (link) {
-    case 1: return 1.f / (1.f + __expf(-eta));
+    case 1: return __frcp_rn(1.f + __expf(-eta));   // v_rcp_f32: no IEEE division sequence per row
     case 2: return __expf(fminf(eta, 80.f));
     case 3: return 1.f / (fabsf(eta) < 1e-10f ? (eta < 0.f ? -1e-10f : 1e-10f) : eta);
     default: return eta;

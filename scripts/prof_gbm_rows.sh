@@ -9,7 +9,7 @@ python3 - "$OUT/run_kernel_trace.csv" > gpurun_out/gbm_${R}_pertree.txt <<'PY'
 import csv, sys, collections
 tr = list(csv.DictReader(open(sys.argv[1])))
 tr.sort(key=lambda r: int(r["Start_Timestamp"]))
-idx = [i for i, r in enumerate(tr) if "hist_quad" in r["Kernel_Name"] or "hist_bm" in r["Kernel_Name"]]
+idx = [i for i, r in enumerate(tr) if "hist_quad" in r["Kernel_Name"] or "hist_bm_kernel" in r["Kernel_Name"]]
 st = idx[::8]
 a, b = st[-9], st[-1]
 sub = tr[a:b]
@@ -31,7 +31,7 @@ for g, a_, b_ in gapk[:10]:
 for k, v in sorted(tot.items(), key=lambda kv: -kv[1])[:14]:
     print(f"{v:8.3f} ms {cnt[k]/8:6.1f}x  {k}")
 # per-level times of the level kernels (mean over the 8 trees, in launch order)
-for name in ("hist_bm", "hist_quad", "part_flags", "part_compact", "hist_sibling", "split_kernel"):
+for name in ("hist_bm_kernel", "hist_bm_reduce", "hist_quad", "part_flags", "part_compact", "hist_sibling", "split_kernel"):
     ks = [r for r in sub if name in r["Kernel_Name"]]
     per = len(ks) // 8
     if per == 0:
