@@ -96,8 +96,22 @@ def parse_setup(raw_frames, destination_frame=None, header=0, separator=None, co
     return P.parse_setup(raw_frames, header=header, sep=separator)
 
 
-def import_sql_table(*a, **k):
-    raise NotImplementedError("JDBC import is not available (no JDBC drivers in this environment)")
+def import_sql_table(connection_url, table, username=None, password=None, columns=None, optimize=True,
+                     fetch_mode=None, num_chunks_hint=None):
+    """Import a whole SQL table (water/jdbc/SQLManager.java importSqlTable): SELECT of
+    the listed columns (all by default) through the same DB-API path as
+    import_sql_select.  fetch_mode / num_chunks_hint only steer the reference's
+    per-node JDBC readers and are accepted for compatibility."""
+    import re
+    if not re.fullmatch(r"[A-Za-z_][A-Za-z0-9_.$]*", str(table)):
+        raise ValueError(f"invalid SQL table name {table!r}")
+    if columns:
+        cols = [columns] if isinstance(columns, str) else list(columns)
+        sel = ", ".join('"' + str(c).replace('"', '""') + '"' for c in cols)
+    else:
+        sel = "*"
+    return import_sql_select(connection_url, f"SELECT {sel} FROM {table}", username=username, password=password,
+                             optimize=optimize, fetch_mode=fetch_mode)
 
 
 def export_file(frame, path, force=False, sep=",", compression=None, parts=1, header=True, quote_header=True,

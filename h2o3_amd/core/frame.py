@@ -1373,6 +1373,14 @@ class H2OFrame:
         raise NotImplementedError("Hive export needs a JDBC/Hive stack, which this platform does not ship")
 
     # strings & time (delegated)
+    @staticmethod
+    def moment(year=None, month=None, day=None, hour=None, minute=None, second=None, msec=None, date=None,
+               time=None):
+        """Time column from its parts (h2o-py frame.py H2OFrame.moment, a staticmethod)."""
+        from . import timeops
+        return timeops.moment(year=year, month=month, day=day, hour=hour, minute=minute, second=second, msec=msec,
+                              date=date, time=time)
+
     def __getattr__(self, name):
         from . import strings, timeops
         if name.startswith("__"):

@@ -85,6 +85,23 @@ def test_top_level_helpers(tmp_path):
     con.close()
     s = h2o.import_sql_select(f"jdbc:sqlite:{db}", "select * from t where a > 1", "", "")
     assert s.nrows == 1
+    t = h2o.import_sql_table(f"jdbc:sqlite:{db}", "t", "", "", columns=["b"], fetch_mode="SINGLE")
+    assert t.shape == (2, 1) and t.names == ["b"]
+    assert h2o.import_sql_table(f"jdbc:sqlite:{db}", "t", "", "").shape == (2, 2)
+    with pytest.raises(ValueError):
+        h2o.import_sql_table(f"jdbc:sqlite:{db}", "t; drop table t", "", "")
+
+
+def test_frame_moment():
+    import datetime
+    one = h2o.H2OFrame.moment(2020, 2, 30)          # invalid date -> NA (AstMoment)
+    assert one.shape == (1, 1) and one.types == {"time": "time"} and one.isna().sum() == 1
+    fr = h2o.H2OFrame(pd.DataFrame({"y": [2020, 2021], "m": [1, 12]}))
+    t = h2o.H2OFrame.moment(year=fr["y"], month=fr["m"], day=15, hour=3)
+    assert t.nrows == 2 and t.year().as_data_frame()["time"].tolist() == [2020, 2021]
+    assert t.month().as_data_frame()["time"].tolist() == [1, 12]
+    d = h2o.H2OFrame.moment(date=datetime.date(2021, 5, 6), time=datetime.time(1, 2, 3))
+    assert d.hour().as_data_frame()["time"].tolist() == [1]
 
 
 class _MaeMetric:
