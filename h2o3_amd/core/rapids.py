@@ -293,7 +293,7 @@ def _unary(name):
 
 
 def _cols(fr, sel):
-    if isinstance(sel, (int, float)):
+    if isinstance(sel, (int, float, str)):
         sel = [sel]
     if sel and isinstance(sel[0], str):
         return fr[list(sel)]
@@ -493,8 +493,23 @@ PRIMS["is.factor"] = lambda x: [float(b) for b in x.isfactor()]
 PRIMS["is.numeric"] = lambda x: [float(b) for b in x.isnumeric()]
 PRIMS["is.character"] = lambda x: [float(b) for b in x.isstring()]
 PRIMS["ifelse"] = _ifelse
-PRIMS["levels"] = lambda x: _F()({f"C{j + 1}": pd_series(lv) for j, lv in enumerate(x.levels())}, _local=True) \
-    if x.ncols > 1 else x.levels()[0]
+def _levels(x):
+    """AstLevels: one categorical column per input column holding the codes
+    0..card-1 of its domain (NA-padded to the largest domain)."""
+    from .vec import T_ENUM, Vec
+    lv = x.levels()
+    n = max([len(d or []) for d in lv] + [0])
+    dev = x._vecs[0].data.device if x.ncols else None
+    vecs = []
+    for d in lv:
+        d = list(d or [])
+        codes = torch.full((n,), -1, dtype=torch.int32, device=dev)
+        codes[:len(d)] = torch.arange(len(d), dtype=torch.int32, device=dev)
+        vecs.append(Vec(codes, T_ENUM, d))
+    return _F().from_vecs(vecs, [f"C{j + 1}" for j in range(len(lv))])
+
+
+PRIMS["levels"] = _levels
 PRIMS["nlevels"] = lambda x: float(x.nlevels()[0])
 PRIMS["setDomain"] = lambda x, inplace, levels: x.set_levels(levels)
 PRIMS["relevel"] = lambda x, lvl: x.relevel(lvl)
@@ -552,9 +567,10 @@ PRIMS["stratified_kfold_column"] = lambda x, n, seed=-1.0: x.stratified_kfold_co
 PRIMS["h2o.random_stratified_split"] = lambda x, frac, seed=-1.0: x.stratified_split(frac, int(seed))
 PRIMS["isax"] = lambda x, nw, mc, opt=0.0: x.isax(int(nw), int(mc), bool(opt))
 PRIMS["apply"] = _apply
-PRIMS["append"] = lambda dst, src, name: _append(dst, src, name)
+PRIMS["append"] = lambda dst, *pairs: _append(dst, *pairs)
 PRIMS[":="] = _assign_cols
-PRIMS["ls"] = lambda: dkv.keys()
+PRIMS["ls"] = lambda: _F().from_vecs([__import__("h2o3_amd.core.vec", fromlist=["x"]).make_string(
+    np.asarray(sorted(dkv.keys()), dtype=object))], ["key"])   # AstLs: a one-column frame of the keys
 PRIMS["mktime"] = lambda *a: _F().mktime(*[x if _is_frame(x) else float(x) for x in a])
 PRIMS["as.Date"] = lambda x, fmt: x.as_date(fmt)
 PRIMS["getTimeZone"] = lambda: __import__("h2o3_amd.core.timeops", fromlist=["x"]).get_timezone()
@@ -588,9 +604,16 @@ def _rename(fr, idx, names):
     return out
 
 
-def _append(dst, src, name):
-    out = dst  # in place, like AstAppend
-    out[name] = src if _is_frame(src) else float(src)
+def _append(dst, *pairs):
+    """AstAppend: (append dst (src name)+) -> a NEW frame sharing dst's
+    columns plus each src (a one-column frame, number or string) under name."""
+    if not pairs or len(pairs) % 2:
+        raise RapidsError("append expects dst followed by (src name) pairs")
+    out = _F().from_vecs(list(dst._vecs), list(dst.names))
+    for src, name in zip(pairs[0::2], pairs[1::2]):
+        if _is_frame(src) and src.ncols != 1:
+            raise RapidsError("Can only append one column")
+        out[str(name)] = src if _is_frame(src) else (src if isinstance(src, str) else float(src))
     return out
 
 

@@ -1,22 +1,37 @@
-"""REST API (subset of the reference's /3 endpoints).
+"""REST API speaking the reference's /3 protocol.
 
-Reference: water/api/RequestServer.java + the schema handlers under
-water/api/ (CloudHandler, ImportFilesHandler, ParseHandler, FramesHandler,
-ModelBuilderHandler, ModelsHandler, ModelMetricsHandler (predictions),
-JobsHandler, DKVHandler, TimelineHandler, MetadataHandler).  JSON shapes
-follow the reference's field names where clients read them (frame_id /
-model_id as {"name": ...}, job {"key", "status", "progress", "dest"}).
+Reference: water/api/RequestServer.java and the handlers under water/api/
+(CloudHandler, MetadataHandler, SessionsHandler (/4/sessions), PostFile,
+ParseSetupHandler, ParseHandler, FramesHandler, DownloadDataHandler,
+ModelBuilderHandler, ModelsHandler, ModelMetricsHandler, JobsHandler,
+DKVHandler, RapidsHandler, GridSearchHandler, AutoMLBuilderHandler,
+TimelineHandler, AboutHandler).
+
+Requests are accepted the way the reference clients send them -- form
+fields (x-www-form-urlencoded or multipart) in H2O's list syntax, query
+strings for GETs -- and also as JSON bodies.  Responses carry the schema
+``__meta`` blocks the clients dispatch on (see schemas.py), so the
+reference's own Python client (h2o-py: h2o.connect / H2OFrame / estimators
+/ predict / model_performance / Rapids frame munging) runs against this
+server; tests/test_rest_wire.py drives it end to end.
 
 Model builds run synchronously inside the request on the serving process
-(the compute itself runs on the GPU through the same estimators the
-Python API uses).  Multi-rank clouds are driven SPMD from Python; the
-REST server serves a single-process (world size 1) cloud.
+(the compute itself runs on the GPU through the same estimators the Python
+API uses); the returned job is already DONE when the client starts polling.
+Requests are served one at a time (GPU work of one process is issued from
+one host thread).  Multi-rank clouds are driven SPMD from Python; the REST
+server serves a single-process cloud.
 """
 from __future__ import annotations
 
-import math
+import json as _json
+import os
+import tempfile
+import time
+import uuid
 
-from fastapi import Body, FastAPI, HTTPException
+from fastapi import FastAPI, Request
+from fastapi.responses import JSONResponse, PlainTextResponse, Response
 
 import importlib
 
@@ -24,357 +39,792 @@ api = importlib.import_module("h2o3_amd.api")  # the module (the package re-expo
 from ..core import dkv
 from ..core.frame import H2OFrame
 from ..parallel import cloud
+from . import schemas as S
+
+_ALGOS = {"gbm": "H2OGradientBoostingEstimator", "glm": "H2OGeneralizedLinearEstimator",
+          "drf": "H2ORandomForestEstimator", "xgboost": "H2OXGBoostEstimator",
+          "deeplearning": "H2ODeepLearningEstimator", "kmeans": "H2OKMeansEstimator",
+          "pca": "H2OPrincipalComponentAnalysisEstimator", "svd": "H2OSingularValueDecompositionEstimator",
+          "naivebayes": "H2ONaiveBayesEstimator", "isolationforest": "H2OIsolationForestEstimator",
+          "extendedisolationforest": "H2OExtendedIsolationForestEstimator", "glrm": "H2OGeneralizedLowRankEstimator",
+          "coxph": "H2OCoxProportionalHazardsEstimator", "gam": "H2OGeneralizedAdditiveEstimator",
+          "rulefit": "H2ORuleFitEstimator", "isotonicregression": "H2OIsotonicRegressionEstimator",
+          "upliftdrf": "H2OUpliftRandomForestEstimator", "psvm": "H2OSupportVectorMachineEstimator",
+          "word2vec": "H2OWord2vecEstimator", "targetencoder": "H2OTargetEncoderEstimator",
+          "aggregator": "H2OAggregatorEstimator", "anovaglm": "H2OANOVAGLMEstimator",
+          "modelselection": "H2OModelSelectionEstimator", "stackedensemble": "H2OStackedEnsembleEstimator",
+          "infogram": "H2OInfogram", "hglm": "H2OGeneralizedLinearEstimator"}
+
+# parameters naming frames / models that are resolved from the key store
+_FRAME_PARAMS = {"training_frame", "validation_frame", "calibration_frame", "blending_frame", "user_points",
+                 "beta_constraints", "plug_values", "linear_constraints", "pre_trained", "user_x", "user_y",
+                 "leaderboard_frame", "loading_frame", "offset_frame"}
+_MODEL_PARAMS = {"checkpoint", "pretrained_autoencoder", "metalearner_model"}
+# client-side bookkeeping the estimators do not take
+_DROP_PARAMS = {"_rest_version", "ignored_columns", "response_column", "training_frame", "validation_frame", "x",
+                "interactions_only"}
+
+_TYPE_NAMES = {"real": "Numeric", "int": "Numeric", "enum": "Enum", "string": "String", "time": "Time",
+               "uuid": "UUID", "bad": "BAD"}
+_TYPE_IN = {"numeric": "numeric", "real": "real", "int": "int", "enum": "enum", "categorical": "enum",
+            "factor": "enum", "string": "string", "time": "time", "uuid": "uuid", "bad": "numeric"}
+
+
+class _HTTPError(Exception):
+    def __init__(self, status, msg, exc=None, builder=False):
+        super().__init__(msg)
+        self.status, self.msg, self.exc, self.builder = status, msg, exc, builder
 
 
 def _algo_cls(algo):
     from .. import estimators as E
-    table = {"gbm": E.H2OGradientBoostingEstimator, "glm": E.H2OGeneralizedLinearEstimator,
-             "drf": E.H2ORandomForestEstimator, "xgboost": E.H2OXGBoostEstimator,
-             "deeplearning": E.H2ODeepLearningEstimator, "kmeans": E.H2OKMeansEstimator,
-             "pca": E.H2OPrincipalComponentAnalysisEstimator, "svd": E.H2OSingularValueDecompositionEstimator,
-             "naivebayes": E.H2ONaiveBayesEstimator, "isolationforest": E.H2OIsolationForestEstimator,
-             "extendedisolationforest": E.H2OExtendedIsolationForestEstimator, "glrm": E.H2OGeneralizedLowRankEstimator,
-             "coxph": E.H2OCoxProportionalHazardsEstimator, "gam": E.H2OGeneralizedAdditiveEstimator,
-             "rulefit": E.H2ORuleFitEstimator, "isotonicregression": E.H2OIsotonicRegressionEstimator,
-             "upliftdrf": E.H2OUpliftRandomForestEstimator, "psvm": E.H2OSupportVectorMachineEstimator,
-             "word2vec": E.H2OWord2vecEstimator, "targetencoder": E.H2OTargetEncoderEstimator,
-             "aggregator": E.H2OAggregatorEstimator, "anovaglm": E.H2OANOVAGLMEstimator,
-             "modelselection": E.H2OModelSelectionEstimator, "stackedensemble": E.H2OStackedEnsembleEstimator}
-    if algo not in table:
-        raise HTTPException(404, f"unknown algo {algo}")
-    return table[algo]
+    name = _ALGOS.get(algo.lower())
+    cls = getattr(E, name, None) if name else None
+    if cls is None:
+        raise _HTTPError(404, f"Unknown algo: {algo}")
+    return cls
 
 
-def _jsonable(v):
-    if isinstance(v, float) and (math.isnan(v) or math.isinf(v)):
-        return None
-    if isinstance(v, (int, float, str, bool)) or v is None:
-        return v
-    if isinstance(v, dict):
-        return {str(k): _jsonable(x) for k, x in v.items()}
-    if isinstance(v, (list, tuple)):
-        return [_jsonable(x) for x in v]
-    try:
-        import numpy as np
-        if isinstance(v, np.generic):
-            return _jsonable(v.item())
-        if isinstance(v, np.ndarray):
-            return _jsonable(v.tolist())
-    except ImportError:
-        pass
-    return str(v)
+def _multipart(body: bytes, ctype: str) -> list[tuple[str, str | None, bytes]]:
+    """multipart/form-data body -> [(field name, filename or None, bytes)]
+    (stdlib email parser; python-multipart is not available here)."""
+    from email.parser import BytesParser
+    from email.policy import HTTP
+    msg = BytesParser(policy=HTTP).parsebytes(b"Content-Type: " + ctype.encode() + b"\r\n\r\n" + body)
+    out = []
+    for part in msg.iter_parts():
+        name = part.get_param("name", header="content-disposition")
+        out.append((name, part.get_filename(), part.get_payload(decode=True) or b""))
+    return out
 
 
-def _frame_json(fid, fr: H2OFrame, rows=10):
-    cols = []
-    for n in fr.names:
-        v = fr.vec(n)
-        c = {"label": n, "type": v.type, "domain": v.domain}
-        if v.is_numeric:
-            r = v.rollups()
-            c.update(min=r.get("min"), max=r.get("max"), mean=r.get("mean"), sigma=r.get("sigma"),
-                     missing_count=r.get("nas"))
-        cols.append(c)
-    head = fr.head(rows).as_data_frame() if fr.nrow else None
-    return _jsonable({"frame_id": {"name": fid}, "rows": fr.nrow, "column_count": fr.ncol, "columns": cols,
-                      "data": head.to_dict(orient="list") if head is not None else {}})
+async def _params(request: Request) -> dict:
+    """Query + form (urlencoded / multipart, files excluded) + JSON body,
+    decoded from the client's encoding (schemas.parse_value)."""
+    from urllib.parse import parse_qsl
+    raw = dict(request.query_params)
+    ctype = request.headers.get("content-type", "")
+    if ctype.startswith("application/json"):
+        body = await request.body()
+        if body:
+            j = _json.loads(body)
+            if isinstance(j, dict):
+                return {**S.parse_params(raw), **j}
+    elif ctype.startswith("application/x-www-form-urlencoded"):
+        raw.update(parse_qsl((await request.body()).decode("utf-8"), keep_blank_values=True))
+    elif ctype.startswith("multipart/form-data"):
+        for name, fname, data in _multipart(await request.body(), ctype):
+            if fname is None and name:
+                raw[name] = data.decode("utf-8", "replace")
+    return S.parse_params(raw)
 
 
-def _model_json(mid, m):
-    out = {"model_id": {"name": mid}, "algo": m.algo, "parameters": {k: _jsonable(v) for k, v in m._parms.items()
-                                                                    if not hasattr(v, "as_data_frame")},
-           "output": {"model_category": m.type if hasattr(m, "type") else None}}
-    tm = m._training_metrics
-    if tm is not None:
-        out["output"]["training_metrics"] = {k: _jsonable(v) for k, v in tm._m.items()
-                                             if isinstance(v, (int, float, str)) or v is None}
-    return _jsonable(out)
+def _frame(fid, what="frame") -> H2OFrame:
+    fr = dkv.get(fid) if fid is not None else None
+    if not isinstance(fr, H2OFrame):
+        raise _HTTPError(404, f"Object '{fid}' not found for argument: {what}")
+    return fr
+
+
+def _model(mid):
+    from ..models.base import H2OEstimator
+    m = dkv.get(mid) if mid is not None else None
+    if not isinstance(m, H2OEstimator):
+        raise _HTTPError(404, f"Object '{mid}' not found for argument: key")
+    return m
+
+
+def _put_frame(fr: H2OFrame, fid=None) -> str:
+    fid = fid or fr.frame_id
+    if fr.frame_id != fid:
+        try:
+            fr.frame_id = fid
+        except AttributeError:
+            pass
+    dkv.put(fid, fr)
+    return fid
+
+
+class _Uploads:
+    """Raw uploaded files (the reference's raw ByteVec keys from PostFile /
+    ImportFiles): key -> local path, plus the parse-setup guess per key."""
+
+    def __init__(self):
+        self.dir = tempfile.mkdtemp(prefix="h2o3_amd_upload_")
+        self.paths: dict[str, list[str]] = {}
+        self.setups: dict[str, tuple] = {}
+
+    def add_bytes(self, data: bytes, name: str | None = None) -> str:
+        k = name or f"upload_{uuid.uuid4().hex[:16]}"
+        p = os.path.join(self.dir, k.replace("/", "_"))
+        with open(p, "wb") as f:
+            f.write(data)
+        self.paths[k] = [p]
+        return k
+
+    def resolve(self, keys) -> list[str]:
+        out = []
+        for k in keys:
+            out += self.paths.get(k, [k])
+        return out
 
 
 def create_app() -> FastAPI:
     app = FastAPI(title="h2o3_amd REST API", version="3")
+    uploads = _Uploads()
+    sessions: dict[str, float] = {}
+    t_start = time.time()
 
-    @app.get("/3/Cloud")
-    def cloud_status():
+    @app.exception_handler(_HTTPError)
+    async def _err(request: Request, e: _HTTPError):
+        return JSONResponse(S.error_v3(e.msg, e.status, e.exc, builder=e.builder, url=str(request.url.path)),
+                            status_code=e.status)
+
+    def route(method, path):
+        """Register an async handler taking (params, request, **path)."""
+        def deco(fn):
+            async def h(request: Request):
+                p = await _params(request)
+                # handlers run on the event-loop thread: requests are served one at a time
+                try:
+                    out = fn(p, request, **request.path_params)
+                    if hasattr(out, "__await__"):
+                        out = await out
+                except _HTTPError:
+                    raise
+                except (KeyError, ValueError, TypeError, RuntimeError, AssertionError, IndexError,
+                        NotImplementedError) as e:
+                    raise _HTTPError(400 if not isinstance(e, KeyError) else 404, str(e), e)
+                if isinstance(out, Response):
+                    return out
+                return JSONResponse(S.jsonable(out))
+            h.__name__ = fn.__name__
+            app.add_api_route(path, h, methods=[method], name=f"{method} {path}")
+            return fn
+        return deco
+
+    # ------------------------------------------------------------ cloud
+    @route("GET", "/3/Cloud")
+    def cloud_status(p, r):
+        return S.cloud_v3(cloud.info(), t_start)
+
+    @route("HEAD", "/3/Cloud")
+    def cloud_head(p, r):
+        return Response(status_code=200)
+
+    @route("GET", "/3/Metadata/schemas/{name}")
+    def schema_meta(p, r, name):
+        m = S.schema_metadata(name)
+        if m is None:
+            raise _HTTPError(404, f"Schema {name} not found")
+        return m
+
+    @route("GET", "/3/Metadata/endpoints")
+    def endpoints(p, r):
+        routes = [{"__meta": S.meta("RouteV3", "Iced"), "url_pattern": rt.path,
+                   "http_method": sorted(rt.methods)[0], "summary": rt.name, "input_schema": None,
+                   "output_schema": None} for rt in app.routes if hasattr(rt, "methods")]
+        return {"__meta": S.meta("MetadataV3", "Iced"), "routes": routes, "schemas": []}
+
+    @route("POST", "/4/sessions")
+    def session_open(p, r):
+        sid = f"_sid_{uuid.uuid4().hex[:8]}"
+        sessions[sid] = time.time()
+        return {"__meta": S.meta("SessionIdV4", "Iced", 4), "session_key": sid}
+
+    @route("DELETE", "/4/sessions/{sid}")
+    def session_close(p, r, sid):
+        sessions.pop(sid, None)
+        return {"__meta": S.meta("SessionIdV4", "Iced", 4), "session_key": sid}
+
+    @route("GET", "/3/InitID")
+    def init_id(p, r):
+        sid = f"_sid_{uuid.uuid4().hex[:8]}"
+        sessions[sid] = time.time()
+        return {"__meta": S.meta("InitIDV3", "Iced"), "session_key": sid, "session_properties_allowed": False}
+
+    @route("GET", "/3/About")
+    def about(p, r):
         i = cloud.info()
-        return _jsonable({"cloud_name": i.get("name"), "cloud_size": i.get("world"), "cloud_healthy": True,
-                          "consensus": True, "locked": False, "version": "h2o3_amd-0.1.0",
-                          "nodes": [{"h2o": f"rank{r}", "healthy": True} for r in range(i.get("world", 1))],
-                          "backend": i.get("backend"), "device": str(i.get("device"))})
+        ent = [("Build project version", S.VERSION), ("Built by", "h2o3_amd"), ("Device", str(i.get("device"))),
+               ("Cloud size", str(i.get("cloud_size")))]
+        return {"__meta": S.meta("AboutV3", "Iced"),
+                "entries": [{"__meta": S.meta("AboutEntryV3", "Iced"), "name": a, "value": b} for a, b in ent]}
 
-    @app.post("/3/ImportFiles")
-    def import_files(path: str, destination_frame: str | None = None):
-        fr = api.import_file(path, destination_frame=destination_frame)
-        fid = destination_frame or fr.frame_id
-        dkv.put(fid, fr)
-        return {"destination_frames": [fid], "files": [path], "fails": []}
+    @route("GET", "/3/Capabilities")
+    def capabilities(p, r):
+        return {"capabilities": [{"name": n} for n in ("Algos", "AutoML", "Grid", "MOJO", "POJO", "Rapids",
+                                                      "HIP-gfx950", "RCCL")]}
 
-    @app.post("/3/PostFile")
-    def post_file(body: dict = Body(...)):
-        import pandas as pd
-        df = pd.DataFrame(body["data"])
-        fr = H2OFrame(df)
-        fid = body.get("destination_frame") or fr.frame_id
-        dkv.put(fid, fr)
-        return {"destination_frame": fid}
+    @route("GET", "/3/Capabilities/API")
+    def capabilities_api(p, r):
+        return {"capabilities": [{"name": "/3"}, {"name": "/4"}, {"name": "/99"}]}
 
-    @app.get("/3/Frames")
-    def frames():
-        return {"frames": [{"frame_id": {"name": k}, "rows": dkv.get(k).nrow, "columns": dkv.get(k).ncol}
-                           for k in dkv.keys() if isinstance(dkv.get(k), H2OFrame)]}
+    @route("GET", "/3/Timeline")
+    def timeline(p, r):
+        return {"__meta": S.meta("TimelineV3", "Timeline"), "events": api.timeline()}
 
-    @app.get("/3/Frames/{fid}")
-    def frame(fid: str, row_count: int = 10):
-        fr = dkv.get(fid)
-        if not isinstance(fr, H2OFrame):
-            raise HTTPException(404, f"frame {fid} not found")
-        return {"frames": [_frame_json(fid, fr, row_count)]}
+    @route("POST", "/3/GarbageCollect")
+    def gc(p, r):
+        import gc as _gc
+        _gc.collect()
+        return {}
 
-    @app.get("/3/Frames/{fid}/summary")
-    def frame_summary(fid: str):
-        return frame(fid, 0)
+    @route("GET", "/3/Logs/nodes/{node}/files/{name}")
+    def logs(p, r, node, name):
+        return {"__meta": S.meta("LogsV3", "Iced"), "nodeidx": node, "name": name, "log": ""}
 
-    @app.post("/3/ModelBuilders/{algo}")
-    def build(algo: str, params: dict = Body(...)):
+    # ----------------------------------------------------------- import
+    @route("POST", "/3/PostFile")
+    async def post_file(p, r):
+        ctype = r.headers.get("content-type", "")
+        if ctype.startswith("application/json"):
+            # JSON upload of columns (h2o3_amd extension): {"data": {col: [...]}, "destination_frame": ...}
+            import pandas as pd
+            fr = H2OFrame(pd.DataFrame(p["data"]))
+            fid = _put_frame(fr, p.get("destination_frame"))
+            return {"destination_frame": fid, "total_bytes": 0}
+        if ctype.startswith("multipart/form-data"):
+            files = [d for _, fname, d in _multipart(await r.body(), ctype) if fname is not None]
+            if not files:
+                raise _HTTPError(400, "PostFile: no file part")
+            data = files[0]
+            name = p.get("destination_frame") or None
+        else:
+            data = await r.body()
+            name = p.get("destination_frame") or None
+        k = uploads.add_bytes(data, name)
+        return {"__meta": S.meta("PostFileV3", "Iced"), "destination_frame": k, "total_bytes": len(data)}
+
+    app.add_api_route("/3/PostFile.bin", app.routes[-1].endpoint, methods=["POST"], name="POST /3/PostFile.bin")
+
+    @route("GET", "/3/ImportFiles")
+    def import_files(p, r):
+        from ..core.parse import _files
+        path = p.get("path")
+        if not path:
+            raise _HTTPError(400, "ImportFiles: path is required")
+        fs = _files(path, p.get("pattern"))
+        keys = []
+        for f in fs:
+            k = f if "://" not in f else os.path.basename(f)
+            uploads.paths[k] = [f]
+            keys.append(k)
+        return {"__meta": S.meta("ImportFilesV3", "Iced"), "path": path, "pattern": p.get("pattern"),
+                "files": fs, "destination_frames": keys, "fails": [], "dels": []}
+
+    app.add_api_route("/3/ImportFiles", app.routes[-1].endpoint, methods=["POST"], name="POST /3/ImportFiles")
+
+    def _guess(srcs, header, sep):
+        """Parse (cached) with the guessed setup -> (frame, separator)."""
+        from ..core import parse as P
+        key_ = (tuple(srcs), header, sep)
+        hit = uploads.setups.get(key_)
+        if hit is not None:
+            return hit
+        files = uploads.resolve(srcs)
+        st = P.parse_setup(files if len(files) > 1 else files[0], sep=sep)
+        s = sep or st["separator"]
+        fr = P.import_file(files if len(files) > 1 else files[0], sep=s, header=header)
+        uploads.setups[key_] = (fr, s)
+        return fr, s
+
+    def _src_keys(v):
+        if v is None:
+            return []
+        v = v if isinstance(v, list) else [v]
+        return [s["name"] if isinstance(s, dict) else str(s) for s in v]
+
+    def _header(v):
+        return 1 if v in (1, True, "1") else (-1 if v in (-1, "-1") else 0)
+
+    @route("POST", "/3/ParseSetup")
+    def parse_setup(p, r):
+        srcs = _src_keys(p.get("source_frames") or p.get("paths"))
+        if not srcs:
+            raise _HTTPError(400, "source_frames required")
+        sep = p.get("separator")
+        sep = chr(sep) if isinstance(sep, int) else sep
+        hdr = _header(p.get("check_header", 0))
+        fr, s = _guess(srcs, hdr, sep)
+        base = os.path.splitext(os.path.basename(uploads.resolve(srcs)[0]))[0]
+        dest = p.get("destination_frame") or (base.replace("-", "_").replace(".", "_") + ".hex")
+        preview = fr.head(min(10, fr.nrow)).as_data_frame() if fr.nrow else None
+        data = [] if preview is None else [[None if v != v else str(v) for v in row] for row in preview.values.tolist()]
+        return {"__meta": S.meta("ParseSetupV3", "ParseSetup"),
+                "source_frames": [S.key(k) for k in srcs], "parse_type": "CSV", "separator": ord(s),
+                "single_quotes": False, "check_header": hdr if hdr != 0 else 1, "column_names": list(fr.names),
+                "column_types": [_TYPE_NAMES.get(fr.vec(n).type, "Numeric") for n in fr.names],
+                "na_strings": None, "column_name_filter": None, "column_offset": 0, "column_count": fr.ncol,
+                "destination_frame": dest, "header_lines": 1 if hdr != -1 else 0, "number_columns": fr.ncol,
+                "data": data, "chunk_size": 4194304, "total_filtered_column_count": fr.ncol,
+                "custom_non_data_line_markers": None, "partition_by": None, "escapechar": 0,
+                "quotechar": None, "skipped_columns": None, "force_col_types": False,
+                "tz_adjust_to_local": False, "warnings": []}
+
+    @route("POST", "/3/Parse")
+    def parse(p, r):
+        from ..core import parse as P
+        srcs = _src_keys(p.get("source_frames"))
+        if not srcs:
+            raise _HTTPError(400, "source_frames required")
+        sep = p.get("separator")
+        sep = chr(sep) if isinstance(sep, int) else sep
+        hdr = _header(p.get("check_header", 0))
+        dest = p.get("destination_frame") or (os.path.basename(srcs[0]) + ".hex")
+        names = p.get("column_names")
+        types = p.get("column_types")
+        skipped = p.get("skipped_columns")
+        fr, s = _guess(srcs, hdr, sep)
+        guessed = [_TYPE_NAMES.get(fr.vec(n).type, "Numeric") for n in fr.names]
+        want = [str(t) for t in types] if types else guessed
+        if (types and [t.lower() for t in want] != [t.lower() for t in guessed]) or skipped or \
+                p.get("na_strings"):
+            files = uploads.resolve(srcs)
+            ct = [_TYPE_IN.get(str(t).lower(), "numeric") for t in want] if types else None
+            fr = P.import_file(files if len(files) > 1 else files[0], sep=s, header=hdr, col_types=ct,
+                               skipped_columns=skipped, na_strings=p.get("na_strings") or None)
+        else:
+            fr = fr.deep_copy()
+        if names:
+            names = [str(n) for n in names]
+            if len(names) == fr.ncol and names != list(fr.names):
+                fr.names = names
+        fid = _put_frame(fr, dest)
+        if p.get("delete_on_done", True):
+            for k in srcs:
+                uploads.setups = {kk: v for kk, v in uploads.setups.items() if k not in kk[0]}
+        return {"__meta": S.meta("ParseV3", "Parse"), "destination_frame": S.key(fid),
+                "job": S.job_v3(key_name=f"parse_{fid}", dest=fid, description="Parse"), "rows": fr.nrow}
+
+    # ----------------------------------------------------------- frames
+    @route("GET", "/3/Frames")
+    def frames(p, r):
+        fs = [(k, dkv.get(k)) for k in dkv.keys()]
+        return {"__meta": S.meta("FramesListV3", "Frames"),
+                "frames": [S.frame_base_v3(k, f) for k, f in fs if isinstance(f, H2OFrame)]}
+
+    def _frame_get(p, fid, rollups=True, percentiles=False):
+        fr = _frame(fid)
+        rc = p.get("row_count", 10)
+        return {"__meta": S.meta("FramesV3", "Frames"), "frame_id": S.key(fid),
+                "frames": [S.frame_v3(fid, fr, int(p.get("row_offset", 0) or 0), -1 if rc is None else int(rc),
+                                      int(p.get("column_offset", 0) or 0), int(p.get("column_count", -1)),
+                                      int(p.get("full_column_count", -1)), rollups=rollups,
+                                      percentiles=percentiles)]}
+
+    @route("GET", "/3/Frames/{fid}")
+    def frame(p, r, fid):
+        return _frame_get(p, fid)
+
+    @route("GET", "/3/Frames/{fid}/light")
+    def frame_light(p, r, fid):
+        return _frame_get(p, fid, rollups=False)
+
+    @route("GET", "/3/Frames/{fid}/summary")
+    def frame_summary(p, r, fid):
+        return _frame_get({"row_count": p.get("row_count", 0)}, fid, percentiles=True)
+
+    @route("GET", "/3/Frames/{fid}/columns/{col}/summary")
+    def column_summary(p, r, fid, col):
+        fr = _frame(fid)
+        return _frame_get({"row_count": 0}, _put_frame(fr[[col]], f"{fid}_{col}_summary"), percentiles=True)
+
+    @route("DELETE", "/3/Frames/{fid}")
+    def frame_delete(p, r, fid):
+        dkv.remove(fid)
+        return {"__meta": S.meta("FramesV3", "Frames"), "frame_id": S.key(fid)}
+
+    @route("DELETE", "/3/Frames")
+    def frames_delete(p, r):
+        for k in list(dkv.keys()):
+            if isinstance(dkv.get(k), H2OFrame):
+                dkv.remove(k)
+        return {}
+
+    @route("GET", "/3/DownloadDataset")
+    def download_dataset(p, r):
+        fr = _frame(p.get("frame_id"), "frame_id")
+        df = fr.as_data_frame()
+        return PlainTextResponse(df.to_csv(index=False, na_rep=""), media_type="text/csv")
+
+    app.add_api_route("/3/DownloadDataset.bin", app.routes[-1].endpoint, methods=["GET"],
+                      name="GET /3/DownloadDataset.bin")
+
+    @route("POST", "/3/SplitFrame")
+    def split_frame(p, r):
+        fr = _frame(p.get("dataset"), "dataset")
+        ratios = [float(x) for x in (p.get("ratios") or [0.75])]
+        dests = p.get("destination_frames")
+        parts = fr.split_frame(ratios=ratios, destination_frames=dests, seed=p.get("seed"))
+        keys = [_put_frame(f, (dests[i] if dests and i < len(dests) else None)) for i, f in enumerate(parts)]
+        return {"__meta": S.meta("SplitFrameV3", "SplitFrame"), "key": S.key(keys[0]),
+                "job": S.job_v3(key_name=f"split_{keys[0]}", dest=keys[0], description="SplitFrame"),
+                "destination_frames": [S.key(k) for k in keys]}
+
+    @route("POST", "/3/CreateFrame")
+    def create_frame(p, r):
+        kw = {k: v for k, v in p.items() if k not in ("dest", "_exclude_fields")}
+        fr = api.create_frame(**{("frame_id" if k == "destination_frame" else k): v for k, v in kw.items()})
+        fid = _put_frame(fr, p.get("dest") or p.get("destination_frame"))
+        return {"__meta": S.meta("CreateFrameV3", "CreateFrame"), "destination_frame": S.key(fid),
+                "job": S.job_v3(key_name=f"create_{fid}", dest=fid, description="CreateFrame")}
+
+    # ----------------------------------------------------------- models
+    def _resolve_params(p):
+        out = {}
+        for k, v in p.items():
+            if k in _FRAME_PARAMS and isinstance(v, str):
+                out[k] = _frame(v, k)
+            elif k in _MODEL_PARAMS and isinstance(v, str) and v:
+                out[k] = dkv.get(v) or v
+            else:
+                out[k] = v
+        return out
+
+    def _build(algo, p):
         cls = _algo_cls(algo)
-        p = dict(params)
-        tf = dkv.get(p.pop("training_frame", None))
-        if not isinstance(tf, H2OFrame):
-            raise HTTPException(400, "training_frame not found")
-        vf = p.pop("validation_frame", None)
-        vf = dkv.get(vf) if vf else None
-        y = p.pop("response_column", None)
-        x = p.pop("x", None)
-        ignored = p.pop("ignored_columns", None) or []
-        if x is None:
-            x = [c for c in tf.names if c != y and c not in ignored]
-        m = cls(**p)
+        p = _resolve_params(p)
+        tf = p.get("training_frame")
+        if not isinstance(tf, H2OFrame) and algo != "stackedensemble":
+            raise _HTTPError(400, "ERRR on field: _train: Missing training frame", builder=True)
+        vf = p.get("validation_frame")
+        y = p.get("response_column")
+        ignored = set(p.get("ignored_columns") or [])
+        special = {y, p.get("weights_column"), p.get("offset_column"), p.get("fold_column"),
+                   p.get("treatment_column")}
+        x = p.get("x")
+        if x is None and isinstance(tf, H2OFrame):
+            x = [c for c in tf.names if c not in special and c not in ignored]
+        kw = {k: v for k, v in p.items() if k not in _DROP_PARAMS and v is not None}
+        if algo == "hglm":
+            kw["HGLM"] = True
+        m = cls(**kw)
         try:
             if m.supervised_learning:
                 m.train(x=x, y=y, training_frame=tf, validation_frame=vf)
             else:
-                m.train(x=x, training_frame=tf)
-        except Exception as e:  # noqa: BLE001 - reported to the client as a failed job
-            raise HTTPException(400, f"model build failed: {e}")
-        j = m._job
-        return {"job": {"key": {"name": j.key}, "status": j.status, "progress": j.progress,
-                        "dest": {"name": m.model_id}}, "messages": []}
+                m.train(x=x, training_frame=tf, validation_frame=vf) if vf is not None else \
+                    m.train(x=x, training_frame=tf)
+        except _HTTPError:
+            raise
+        except Exception as e:  # noqa: BLE001 - reported to the client as an H2OModelBuilderError
+            raise _HTTPError(400, f"Illegal argument(s) for {algo} model: {e}", e, builder=True)
+        dkv.put(m.model_id, m)
+        return m
 
-    @app.get("/3/Models")
-    def models():
+    @route("POST", "/3/ModelBuilders/{algo}")
+    def build(p, r, algo):
+        m = _build(algo, p)
+        j = getattr(m, "_job", None)
+        return {"__meta": S.meta(f"{algo.capitalize()}V3", "ModelBuilder"), "algo": algo,
+                "job": S.job_v3(j, dest=m.model_id, dest_kind="Model") if j is not None else
+                S.job_v3(key_name=f"job_{m.model_id}", dest=m.model_id, dest_kind="Model",
+                         description=f"{algo} Model Build"),
+                "messages": [], "error_count": 0, "parameters": None}
+
+    @route("POST", "/3/ModelBuilders/{algo}/parameters")
+    def validate_params(p, r, algo):
+        _algo_cls(algo)
+        return {"__meta": S.meta("ModelParametersSchemaV3", "ModelBuilder"), "algo": algo, "messages": [],
+                "error_count": 0, "parameters": None}
+
+    @route("GET", "/3/ModelBuilders/{algo}")
+    def builder_info(p, r, algo):
+        cls = _algo_cls(algo)
+        est = cls()
+        params = [S._param_entry(k, v, v) for k, v in est._parms.items()]
+        return {"__meta": S.meta("ModelBuildersV3", "Iced"),
+                "model_builders": {algo: {"algo": algo, "algo_full_name": cls.__name__, "parameters": params,
+                                          "can_build": ["Binomial", "Multinomial", "Regression"],
+                                          "visibility": "Stable", "supervised": cls.supervised_learning}}}
+
+    @route("GET", "/3/Models")
+    def models(p, r):
         from ..models.base import H2OEstimator
-        return {"models": [_model_json(k, dkv.get(k)) for k in dkv.keys() if isinstance(dkv.get(k), H2OEstimator)]}
+        ms = [(k, dkv.get(k)) for k in dkv.keys()]
+        return {"__meta": S.meta("ModelsV3", "Models"),
+                "models": [S.model_v3(k, m) for k, m in ms if isinstance(m, H2OEstimator)]}
 
-    @app.get("/3/Models/{mid}")
-    def model(mid: str):
-        m = dkv.get(mid)
-        if m is None:
-            raise HTTPException(404, f"model {mid} not found")
-        return {"models": [_model_json(mid, m)]}
+    @route("GET", "/3/Models/{mid}")
+    def model(p, r, mid):
+        return {"__meta": S.meta("ModelsV3", "Models"), "models": [S.model_v3(mid, _model(mid))]}
 
-    @app.post("/3/Predictions/models/{mid}/frames/{fid}")
-    def predict(mid: str, fid: str, predictions_frame: str | None = None):
-        m, fr = dkv.get(mid), dkv.get(fid)
-        if m is None or not isinstance(fr, H2OFrame):
-            raise HTTPException(404, "model or frame not found")
-        pr = m.predict(fr)
-        key = predictions_frame or f"prediction_{mid}_on_{fid}"
-        dkv.put(key, pr)
-        perf = None
-        try:
-            if m._spec is not None and m._spec.y in fr.names:
-                mm_ = m.model_performance(fr)
-                perf = {k: _jsonable(v) for k, v in mm_._m.items() if isinstance(v, (int, float, str))}
-        except Exception:  # noqa: BLE001 - metrics are optional for scoring
-            perf = None
-        return {"predictions_frame": {"name": key}, "model_metrics": [perf] if perf else []}
+    @route("GET", "/99/Models/{mid}")
+    def model99(p, r, mid):
+        return model(p, r, mid)
 
-    @app.get("/3/Jobs")
-    def jobs():
-        return {"jobs": [{"key": {"name": j.key}, "description": j.description, "status": j.status,
-                          "progress": j.progress, "dest": {"name": j.dest}, "msec": int(j.run_time * 1000),
-                          "exception": j.exception} for j in api.jobs()]}
+    @route("DELETE", "/3/Models/{mid}")
+    def model_delete(p, r, mid):
+        dkv.remove(mid)
+        return {"__meta": S.meta("ModelsV3", "Models"), "models": []}
 
-    @app.get("/3/Jobs/{jid}")
-    def job(jid: str):
-        for j in api.jobs():
-            if j.key == jid:
-                return {"jobs": [{"key": {"name": j.key}, "status": j.status, "progress": j.progress,
-                                  "dest": {"name": j.dest}}]}
-        raise HTTPException(404, f"job {jid} not found")
-
-    @app.delete("/3/DKV/{key}")
-    def delete(key: str):
-        dkv.remove(key)
-        return {"key": key}
-
-    @app.delete("/3/DKV")
-    def delete_all():
-        dkv.remove_all()
-        return {}
-
-    @app.get("/3/Timeline")
-    def timeline():
-        return {"events": api.timeline()}
-
-    @app.post("/3/ParseSetup")
-    def parse_setup(body: dict = Body(...)):
-        """ParseSetupHandler: guessed separator / header for the source files."""
-        src = body.get("source_frames") or body.get("paths") or []
-        src = [s["name"] if isinstance(s, dict) else s for s in (src if isinstance(src, list) else [src])]
-        if not src:
-            raise HTTPException(400, "source_frames required")
-        from ..core import parse as P
-        st = P.parse_setup(src[0] if len(src) == 1 else src)
-        return _jsonable({"source_frames": [{"name": s} for s in src], "separator": ord(st["separator"]),
-                          "check_header": st.get("header", 0), "destination_frame": body.get("destination_frame")})
-
-    @app.post("/3/Parse")
-    def parse(body: dict = Body(...)):
-        src = [s["name"] if isinstance(s, dict) else s for s in body.get("source_frames", [])]
-        sep = body.get("separator")
-        fr = api.import_file(src if len(src) > 1 else src[0], destination_frame=body.get("destination_frame"),
-                             sep=chr(sep) if isinstance(sep, int) else sep, header=body.get("check_header", 0),
-                             col_names=body.get("column_names"), col_types=body.get("column_types"))
-        fid = body.get("destination_frame") or fr.frame_id
-        dkv.put(fid, fr)
-        return {"job": {"key": {"name": f"parse_{fid}"}, "status": "DONE", "progress": 1.0,
-                        "dest": {"name": fid}}, "destination_frame": {"name": fid}}
-
-    @app.get("/3/DownloadDataset")
-    def download_dataset(frame_id: str):
-        from fastapi.responses import PlainTextResponse
-        fr = dkv.get(frame_id)
-        if not isinstance(fr, H2OFrame):
-            raise HTTPException(404, f"frame {frame_id} not found")
-        return PlainTextResponse(fr.as_data_frame().to_csv(index=False), media_type="text/csv")
-
-    @app.get("/3/Models/{mid}/mojo")
-    def model_mojo(mid: str):
-        from fastapi.responses import Response
+    @route("GET", "/3/Models/{mid}/mojo")
+    def model_mojo(p, r, mid):
         from ..mojo.writer import build_mojo
-        m = dkv.get(mid)
-        if m is None:
-            raise HTTPException(404, f"model {mid} not found")
-        try:
-            data = build_mojo(m)
-        except NotImplementedError as e:
-            raise HTTPException(400, str(e))
+        data = build_mojo(_model(mid))
         return Response(content=data, media_type="application/zip",
                         headers={"Content-Disposition": f'attachment; filename="{mid}.zip"'})
 
-    @app.get("/3/Models.java/{mid}")
-    def model_pojo(mid: str):
-        from fastapi.responses import PlainTextResponse
+    @route("GET", "/3/Models.java/{mid}")
+    def model_pojo(p, r, mid):
         from ..mojo.pojo import to_java
-        m = dkv.get(mid)
-        if m is None:
-            raise HTTPException(404, f"model {mid} not found")
+        return PlainTextResponse(to_java(_model(mid)), media_type="text/plain",
+                                 headers={"Content-Disposition": f'attachment; filename="{mid}.java"'})
+
+    def _predict(p, mid, fid, v4=False):
+        m, fr = _model(mid), _frame(fid)
+        dest = p.get("predictions_frame")
+        if p.get("leaf_node_assignment"):
+            pr = m.predict_leaf_node_assignment(fr, type=p.get("leaf_node_assignment_type") or "Path")
+        elif p.get("predict_contributions"):
+            pr = m.predict_contributions(fr)
+        elif p.get("reconstruction_error"):
+            pr = m.anomaly(fr)
+        elif p.get("deep_features_hidden_layer") is not None and int(p["deep_features_hidden_layer"]) >= 0:
+            pr = m.deepfeatures(fr, int(p["deep_features_hidden_layer"]))
+        elif p.get("predict_staged_proba"):
+            pr = m.staged_predict_proba(fr)
+        elif p.get("exemplar_index") is not None and int(p["exemplar_index"]) >= 0:
+            pr = m.aggregated_frame
+        else:
+            pr = m.predict(fr)
+        key_ = _put_frame(pr, dest or f"prediction_{mid}_on_{fid}")
+        mm = None
+        spec = getattr(m, "_spec", None)
+        if spec is not None and spec.y and spec.y in fr.names:
+            try:
+                mm = S.metrics_v3(m.model_performance(fr), m, fid, S.model_category(m))
+            except Exception:  # noqa: BLE001 - metrics are optional for scoring
+                mm = None
+        if v4:
+            return {"__meta": S.meta("JobV4", "Job", 4),
+                    "key": S.key(f"predict_{key_}", "Job"), "dest": S.key(key_), "status": "DONE",
+                    "job": S.job_v3(key_name=f"predict_{key_}", dest=key_, description="Prediction"),
+                    "predictions_frame": S.key(key_)}
+        return {"__meta": S.meta("ModelMetricsListSchemaV3", "ModelMetricsList"), "model": S.key(mid, "Model"),
+                "frame": S.key(fid), "predictions_frame": S.key(key_), "model_metrics": [mm] if mm else []}
+
+    @route("POST", "/3/Predictions/models/{mid}/frames/{fid}")
+    def predict(p, r, mid, fid):
+        return _predict(p, mid, fid)
+
+    @route("POST", "/4/Predictions/models/{mid}/frames/{fid}")
+    def predict4(p, r, mid, fid):
+        return _predict(p, mid, fid, v4=True)
+
+    @route("POST", "/3/ModelMetrics/models/{mid}/frames/{fid}")
+    def model_metrics(p, r, mid, fid):
+        m, fr = _model(mid), _frame(fid)
+        mm = S.metrics_v3(m.model_performance(fr), m, fid, S.model_category(m))
+        return {"__meta": S.meta("ModelMetricsListSchemaV3", "ModelMetricsList"), "model": S.key(mid, "Model"),
+                "frame": S.key(fid), "model_metrics": [mm]}
+
+    @route("GET", "/3/ModelMetrics/models/{mid}/frames/{fid}")
+    def model_metrics_get(p, r, mid, fid):
+        return model_metrics(p, r, mid, fid)
+
+    # -------------------------------------------------------------- jobs
+    @route("GET", "/3/Jobs")
+    def jobs(p, r):
+        return {"__meta": S.meta("JobsV3", "Jobs"),
+                "jobs": [S.job_v3(j, dest_kind="Model") for j in api.jobs()]}
+
+    @route("GET", "/3/Jobs/{jid}")
+    def job(p, r, jid):
+        for j in api.jobs():
+            if j.key == jid:
+                return {"__meta": S.meta("JobsV3", "Jobs"), "job_id": S.key(jid, "Job"),
+                        "jobs": [S.job_v3(j, dest_kind="Model")]}
+        # synthetic jobs of synchronous requests (parse, split, predictions) are finished by construction
+        return {"__meta": S.meta("JobsV3", "Jobs"), "job_id": S.key(jid, "Job"),
+                "jobs": [S.job_v3(key_name=jid, dest=jid.split("_", 1)[-1], description=jid.split("_", 1)[0])]}
+
+    @route("POST", "/3/Jobs/{jid}/cancel")
+    def job_cancel(p, r, jid):
+        for j in api.jobs():
+            if j.key == jid:
+                j.cancel()
+        return {}
+
+    # --------------------------------------------------------------- DKV
+    @route("DELETE", "/3/DKV/{key_}")
+    def delete(p, r, key_):
+        dkv.remove(key_)
+        return {"__meta": S.meta("RemoveV3", "Iced"), "key": S.key(key_)}
+
+    @route("DELETE", "/3/DKV")
+    def delete_all(p, r):
+        retained = set(p.get("retained_keys") or [])
+        for k in list(dkv.keys()):
+            if k not in retained:
+                dkv.remove(k)
+        return {"__meta": S.meta("RemoveAllV3", "Iced")}
+
+    # ------------------------------------------------------------ Rapids
+    @route("POST", "/99/Rapids")
+    def rapids_exec(p, r):
+        """Rapids expression evaluation (water/api/RapidsHandler.java): frame
+        results are stored under their key and described; scalars/lists/strings
+        come back inline (RapidsFrameV3 / RapidsNumberV3 / RapidsStringV3...)."""
+        from ..core.rapids import RapidsError, rapids
         try:
-            return PlainTextResponse(to_java(m), media_type="text/plain")
-        except NotImplementedError as e:
-            raise HTTPException(400, str(e))
+            res = rapids(p.get("ast", ""))
+        except (RapidsError, KeyError, ValueError, TypeError, IndexError) as e:
+            raise _HTTPError(400, f"Rapids error: {e}", e)
+        if isinstance(res, H2OFrame):
+            if dkv.get(res.frame_id) is not res:
+                dkv.put(res.frame_id, res)
+            return {"__meta": S.meta("RapidsFrameV3", "Iced", 99), "key": S.key(res.frame_id),
+                    "num_rows": res.nrows, "num_cols": res.ncols}
+        if isinstance(res, str):
+            return {"__meta": S.meta("RapidsStringV3", "Iced", 99), "string": res}
+        if isinstance(res, (list, tuple)):
+            if res and all(isinstance(x, str) for x in res):
+                return {"__meta": S.meta("RapidsStringsV3", "Iced", 99), "string": list(res)}
+            return {"__meta": S.meta("RapidsNumbersV3", "Iced", 99), "scalar": [S.num(x) for x in res]}
+        if res is None:
+            return {"__meta": S.meta("RapidsNoneV3", "Iced", 99)}
+        return {"__meta": S.meta("RapidsNumberV3", "Iced", 99), "scalar": S.num(res)}
 
-    @app.post("/3/ModelMetrics/models/{mid}/frames/{fid}")
-    def model_metrics(mid: str, fid: str):
-        m, fr = dkv.get(mid), dkv.get(fid)
-        if m is None or not isinstance(fr, H2OFrame):
-            raise HTTPException(404, "model or frame not found")
-        mm_ = m.model_performance(fr)
-        return {"model_metrics": [{k: _jsonable(v) for k, v in mm_._m.items() if isinstance(v, (int, float, str))}]}
-
-    @app.post("/99/Grid/{algo}")
-    def grid(algo: str, body: dict = Body(...)):
+    # --------------------------------------------------------- grid / automl
+    @route("POST", "/99/Grid/{algo}")
+    def grid(p, r, algo):
         """GridSearchHandler: hyper_parameters + search_criteria over one algo."""
         from ..grid import H2OGridSearch
         cls = _algo_cls(algo)
-        p = dict(body)
-        tf = dkv.get(p.pop("training_frame", None))
-        if not isinstance(tf, H2OFrame):
-            raise HTTPException(400, "training_frame not found")
-        vf = p.pop("validation_frame", None)
-        hyper = p.pop("hyper_parameters", {})
+        p = _resolve_params(p)
+        hyper = p.pop("hyper_parameters", {}) or {}
+        if isinstance(hyper, str):
+            hyper = _json.loads(hyper)
         crit = p.pop("search_criteria", None)
+        if isinstance(crit, str):
+            crit = _json.loads(crit)
         gid = p.pop("grid_id", None)
+        tf, vf = p.pop("training_frame", None), p.pop("validation_frame", None)
         y = p.pop("response_column", None)
-        g = H2OGridSearch(cls(**p), hyper, grid_id=gid, search_criteria=crit)
-        g.train(y=y, training_frame=tf, validation_frame=dkv.get(vf) if vf else None)
-        return {"job": {"key": {"name": f"grid_{g.grid_id}"}, "status": "DONE", "progress": 1.0,
-                        "dest": {"name": g.grid_id}}}
+        ignored = set(p.pop("ignored_columns", None) or [])
+        x = [c for c in tf.names if c != y and c not in ignored] if isinstance(tf, H2OFrame) else None
+        p.pop("_rest_version", None)
+        g = H2OGridSearch(cls(**{k: v for k, v in p.items() if v is not None}), hyper, grid_id=gid,
+                          search_criteria=crit)
+        g.train(x=x, y=y, training_frame=tf, validation_frame=vf)
+        dkv.put(g.grid_id, g)
+        for mid in g.model_ids:
+            mm = g.get_model(mid) if hasattr(g, "get_model") else dkv.get(mid)
+            if mm is not None:
+                dkv.put(mid, mm)
+        return {"__meta": S.meta("GridSearchSchemaV99", "Grid", 99), "grid_id": S.key(g.grid_id, "Grid"),
+                "job": S.job_v3(key_name=f"grid_{g.grid_id}", dest=g.grid_id, dest_kind="Grid",
+                                description="GridSearch"),
+                "total_models": len(g.model_ids)}
 
-    @app.get("/99/Grids/{gid}")
-    def grid_get(gid: str):
+    def _metric_of(mid, name):
+        """Sort key of a grid model (hex/grid/Grid.java sorting): the metric of
+        the cross-validation, else validation, else training metrics."""
+        m = dkv.get(mid)
+        if m is None:
+            return float("nan")
+        mm = m._cross_validation_metrics or m._validation_metrics or m._training_metrics
+        if mm is None:
+            return float("nan")
+        n = name.lower()
+        alias = {"auc": "AUC", "mse": "MSE", "rmse": "RMSE", "aucpr": "pr_auc", "pr_auc": "pr_auc",
+                 "gini": "Gini", "aic": "AIC"}
+        v = mm.get(alias.get(n, n))
+        if v is None and mm.get("thresholds_and_metric_scores") is not None:
+            col = mm["thresholds_and_metric_scores"].get(n)
+            v = max(col) if col is not None and len(col) else None
+        try:
+            return float(v)
+        except (TypeError, ValueError):
+            return float("nan")
+
+    @route("GET", "/99/Grids/{gid}")
+    def grid_get(p, r, gid):
         g = dkv.get(gid)
         if g is None or not hasattr(g, "model_ids"):
-            raise HTTPException(404, f"grid {gid} not found")
+            raise _HTTPError(404, f"grid {gid} not found")
         tab = g.get_grid().sorted_metric_table()
-        return _jsonable({"grid_id": {"name": gid}, "model_ids": [{"name": m} for m in g.model_ids],
-                          "failure_details": [e for _, e in g.failed_params],
-                          "summary_table": tab.to_dict(orient="list")})
+        ids = list(g.model_ids)
+        if p.get("sort_by"):
+            import math
+            vals = {mid: _metric_of(mid, str(p["sort_by"])) for mid in ids}
+            dec = bool(p.get("decreasing"))
+            ids.sort(key=lambda k: (math.isnan(vals[k]), -vals[k] if dec else vals[k]))
+        return {"__meta": S.meta("GridSchemaV99", "Grid", 99), "grid_id": S.key(gid, "Grid"),
+                "model_ids": [S.key(m, "Model") for m in ids],
+                "failed_params": [], "failure_details": [e for _, e in g.failed_params],
+                "failure_stack_traces": [], "failed_raw_params": [],
+                "hyper_names": list(getattr(g, "hyper_params", {}) or {}),
+                "summary_table": S.twodim_from_df("Hyper-Parameter Search Summary", tab),
+                "scoring_history": None, "warning_details": [], "export_checkpoints_dir": None,
+                "training_metrics": [], "validation_metrics": [], "cross_validation_metrics": [],
+                "cross_validation_metrics_summary": []}
 
-    @app.post("/99/AutoMLBuilder")
-    def automl(body: dict = Body(...)):
+    @route("GET", "/99/Grids")
+    def grids(p, r):
+        gs = [k for k in dkv.keys() if hasattr(dkv.get(k), "model_ids") and not hasattr(dkv.get(k), "leaderboard")]
+        return {"__meta": S.meta("GridsV99", "Grids", 99), "grids": [grid_get({}, r, k) for k in gs]}
+
+    @route("POST", "/99/AutoMLBuilder")
+    def automl(p, r):
         """AutoMLBuilderHandler: build_control / input_spec / build_models."""
         from ..automl import H2OAutoML
-        bc, ispec, bm = body.get("build_control", {}), body.get("input_spec", {}), body.get("build_models", {})
-        tf = dkv.get(ispec.get("training_frame"))
-        if not isinstance(tf, H2OFrame):
-            raise HTTPException(400, "input_spec.training_frame not found")
+        bc, ispec, bm = p.get("build_control", {}), p.get("input_spec", {}), p.get("build_models", {})
+        tf = _frame(ispec.get("training_frame"), "training_frame")
         sc = bc.get("stopping_criteria", {})
         aml = H2OAutoML(project_name=bc.get("project_name"), nfolds=bc.get("nfolds", -1),
                         max_models=sc.get("max_models"), max_runtime_secs=sc.get("max_runtime_secs"),
                         seed=sc.get("seed"), exclude_algos=bm.get("exclude_algos"),
                         include_algos=bm.get("include_algos"), sort_metric=ispec.get("sort_metric", "AUTO"))
-        aml.train(y=ispec.get("response_column"), training_frame=tf,
+        y = ispec.get("response_column")
+        ign = set(ispec.get("ignored_columns") or [])
+        x = [c for c in tf.names if c != y and c not in ign]
+        aml.train(x=x, y=y, training_frame=tf,
                   validation_frame=dkv.get(ispec["validation_frame"]) if ispec.get("validation_frame") else None,
                   leaderboard_frame=dkv.get(ispec["leaderboard_frame"]) if ispec.get("leaderboard_frame") else None)
-        return {"job": {"key": {"name": f"automl_{aml.project_name}"}, "status": "DONE", "progress": 1.0,
-                        "dest": {"name": aml.project_name}}}
+        dkv.put(aml.project_name, aml)
+        return {"__meta": S.meta("AutoMLBuildSpecV99", "AutoMLBuildSpec", 99),
+                "job": S.job_v3(key_name=f"automl_{aml.project_name}", dest=aml.project_name, dest_kind="AutoML",
+                                description="AutoML"),
+                "build_control": {"project_name": aml.project_name}}
 
-    @app.get("/99/Leaderboards/{project}")
-    def leaderboard(project: str):
+    def _lb_table(aml):
+        lb = aml.leaderboard.as_data_frame()
+        cols = {c: lb[c].tolist() for c in lb.columns}
+        return lb, S.twodim("Leaderboard", cols, "models sorted by the leaderboard metric",
+                            row_headers=[str(i) for i in range(len(lb))])
+
+    @route("GET", "/99/Leaderboards/{project}")
+    def leaderboard(p, r, project):
         aml = dkv.get(project)
         if aml is None or not hasattr(aml, "leaderboard"):
-            raise HTTPException(404, f"AutoML project {project} not found")
-        lb = aml.leaderboard.as_data_frame()
-        return _jsonable({"project_name": project, "models": [{"name": m} for m in lb["model_id"]],
-                          "table": lb.to_dict(orient="list")})
+            raise _HTTPError(404, f"AutoML project {project} not found")
+        lb, tab = _lb_table(aml)
+        return {"__meta": S.meta("LeaderboardV99", "Leaderboard", 99), "project_name": project,
+                "models": [S.key(m, "Model") for m in lb["model_id"]], "table": tab,
+                "sort_metric": lb.columns[1] if lb.shape[1] > 1 else None}
 
-    @app.get("/3/About")
-    def about():
-        i = cloud.info()
-        return {"entries": [{"name": "Build project version", "value": "h2o3_amd-0.1.0"},
-                            {"name": "Device", "value": str(i.get("device"))},
-                            {"name": "Cloud size", "value": str(i.get("world"))}]}
-
-    @app.get("/3/Capabilities")
-    def capabilities():
-        return {"capabilities": [{"name": n} for n in ("Algos", "AutoML", "Grid", "MOJO", "POJO", "Rapids",
-                                                      "HIP-gfx950", "RCCL")]}
-
-    @app.post("/99/Rapids")
-    def rapids_exec(body: dict = Body(...)):
-        """Rapids expression evaluation (water/api/RapidsHandler.java): frame
-        results are stored under their key and described; scalars/lists/strings
-        come back inline."""
-        from ..core.rapids import RapidsError, rapids
-        try:
-            res = rapids(body.get("ast", ""))
-        except (RapidsError, KeyError, ValueError, TypeError) as e:
-            raise HTTPException(400, f"Rapids error: {e}")
-        if isinstance(res, H2OFrame):
-            dkv.put(res.frame_id, res)
-            return {"key": {"name": res.frame_id}, "num_rows": res.nrows, "num_cols": res.ncols}
-        if isinstance(res, str):
-            return {"string": res}
-        if isinstance(res, (list, tuple)):
-            return {"scalar": None, "ns": [_jsonable(x) for x in res]}
-        return {"scalar": _jsonable(res)}
-
-    @app.get("/3/Metadata/endpoints")
-    def endpoints():
-        return {"routes": [{"url_pattern": r.path, "http_method": sorted(r.methods)[0]} for r in app.routes
-                           if hasattr(r, "methods")]}
+    @route("GET", "/99/AutoML/{project}")
+    def automl_get(p, r, project):
+        """AutoMLHandler: project state (leaderboard + event log tables)."""
+        lbj = leaderboard(p, r, project)
+        aml = dkv.get(project)
+        rows = list(getattr(aml, "event_log_rows", []) or [])
+        info = getattr(aml, "training_info", None) or {}
+        ev = {k: [str(e.get(k, "")) for e in rows] + [""] * len(info)
+              for k in ("timestamp", "level", "stage", "message")}
+        ev["name"] = [""] * len(rows) + [str(k) for k in info]
+        ev["value"] = [""] * len(rows) + [str(v) for v in info.values()]
+        n = len(rows) + len(info)
+        return {"__meta": S.meta("AutoMLV99", "AutoML", 99),
+                "automl_id": {"__meta": S.meta("AutoMLKeyV3", "Key<AutoML>"), "name": project},
+                "project_name": project, "leaderboard": lbj, "leaderboard_table": lbj["table"],
+                "event_log": {"events": rows},
+                "event_log_table": S.twodim("Event Log", ev, "AutoML events", row_headers=[str(i) for i in range(n)]),
+                "modeling_steps": [{"name": a, "steps": []} for a in
+                                   sorted({str(m).split("_")[0] for m in lbj["table"]["data"][1]})]}
 
     return app
 

@@ -49,7 +49,8 @@ def test_frame_prims(fr):
     ap = R("(apply (cols rap1 [0 2]) 2 {x . (sumNA x)})").as_data_frame()
     assert ap.iloc[0].tolist() == [11, 2]
     assert R("(toupper (cols rap1 'b'))").levels()[0] == ["X", "Y", "Z"]
-    assert R("(levels (cols rap1 'b'))") == ["x", "y", "z"]
+    lv = R("(levels (cols rap1 'b'))")   # AstLevels: a categorical column of the domain
+    assert lv.as_data_frame()["C1"].tolist() == ["x", "y", "z"]
     assert R("(sort rap1 [0] [0])").as_data_frame()["a"].tolist()[:3] == [5.0, 3.0, 2.0]
     assert R("(year (mktime 2021 5 3 0 0 0 0))").as_data_frame().iloc[0, 0] == 2021
     R("(:= rap1 99 [0] [1])")
