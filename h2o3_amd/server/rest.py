@@ -243,6 +243,29 @@ def create_app() -> FastAPI:
         sessions[sid] = time.time()
         return {"__meta": S.meta("InitIDV3", "Iced"), "session_key": sid, "session_properties_allowed": False}
 
+    app.add_api_route("/3/InitID", app.routes[-1].endpoint, methods=["POST"], name="POST /3/InitID")
+
+    @route("POST", "/3/LogAndEcho")
+    def log_and_echo(p, r):
+        """LogAndEchoHandler (h2o-r writes its session markers here)."""
+        from ..utils import log as _log
+        msg = str(p.get("message", ""))
+        try:
+            _log.info(msg)
+        except Exception:  # noqa: BLE001 - logging never fails a request
+            pass
+        return {"__meta": S.meta("LogAndEchoV3", "Iced"), "message": msg}
+
+    @route("GET", "/3/Capabilities/Core")
+    def capabilities_core(p, r):
+        return {"capabilities": [{"name": "Core"}, {"name": "Rapids"}, {"name": "MOJO"}]}
+
+    @route("POST", "/3/Shutdown")
+    def shutdown(p, r):
+        """ShutdownHandler: the cloud stays up in-process; the request is
+        acknowledged so the reference clients' h2o.shutdown() completes."""
+        return {"__meta": S.meta("ShutdownV3", "Iced")}
+
     @route("GET", "/3/About")
     def about(p, r):
         i = cloud.info()
