@@ -647,6 +647,154 @@ def create_app() -> FastAPI:
     def model_metrics_get(p, r, mid, fid):
         return model_metrics(p, r, mid, fid)
 
+    # ------------------------------------------------ persistence / misc
+    def _models_list(mid):
+        return {"__meta": S.meta("ModelsV3", "Models"), "models": [S.model_v3(mid, _model(mid))]}
+
+    @route("GET", "/99/Models.bin/{mid}")
+    def model_save(p, r, mid):
+        """ModelsHandler.exportModel: write the model binary under `dir` on the server."""
+        m = _model(mid)
+        path = str(p.get("dir") or "")
+        out = api.save_model(m, os.path.dirname(path) or ".", force=bool(p.get("force", False)),
+                             filename=os.path.basename(path) or None)
+        return {"__meta": S.meta("ModelExportV3", "Iced"), "model_id": S.key(mid, "Model"), "dir": out}
+
+    @route("POST", "/99/Models.bin/{mid}")
+    def model_load(p, r, mid=""):
+        """ModelsHandler.importModel: load a binary model from `dir` on the server."""
+        m = api.load_model(str(p.get("dir")))
+        dkv.put(m.model_id, m)
+        return _models_list(m.model_id)
+
+    app.add_api_route("/99/Models.bin/", app.routes[-1].endpoint, methods=["POST"], name="POST /99/Models.bin/")
+
+    @route("POST", "/99/Models.upload.bin/{mid}")
+    def model_upload(p, r, mid=""):
+        """Load a model binary that was sent with PostFile (its raw key in `dir`)."""
+        src = uploads.resolve([str(p.get("dir"))])[0]
+        m = api.load_model(src)
+        dkv.put(m.model_id, m)
+        return _models_list(m.model_id)
+
+    app.add_api_route("/99/Models.upload.bin/", app.routes[-1].endpoint, methods=["POST"],
+                      name="POST /99/Models.upload.bin/")
+
+    @route("GET", "/3/Models.fetch.bin/{mid}")
+    def model_fetch(p, r, mid):
+        """The model binary as a download (h2o.download_model)."""
+        m = _model(mid)
+        d = tempfile.mkdtemp(prefix="h2o3_amd_fetch_")
+        path = api.save_model(m, d, force=True)
+        with open(path, "rb") as f:
+            data = f.read()
+        return Response(content=data, media_type="application/octet-stream",
+                        headers={"Content-Disposition": f'attachment; filename="{mid}"'})
+
+    @route("GET", "/99/Models.mojo/{mid}")
+    def model_save_mojo(p, r, mid):
+        from ..mojo.writer import build_mojo
+        path = str(p.get("dir"))
+        if os.path.exists(path) and not p.get("force", False):
+            raise _HTTPError(400, f"File {path} already exists")
+        os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+        with open(path, "wb") as f:
+            f.write(build_mojo(_model(mid)))
+        return {"__meta": S.meta("ModelExportV3", "Iced"), "model_id": S.key(mid, "Model"), "dir": path}
+
+    @route("POST", "/3/Frames/{fid}/export")
+    def frame_export(p, r, fid):
+        fr = _frame(fid)
+        sep = p.get("separator", 44)
+        api.export_file(fr, str(p.get("path")), force=bool(p.get("force", False)),
+                        sep=chr(sep) if isinstance(sep, int) else str(sep), header=bool(p.get("header", True)),
+                        format=str(p.get("format") or "csv"))
+        return {"__meta": S.meta("FramesV3", "Frames"),
+                "job": S.job_v3(key_name=f"export_{fid}", dest=fid, description="Export File")}
+
+    @route("POST", "/3/ModelMetrics/predictions_frame/{pf}/actuals_frame/{af}")
+    def make_metrics(p, r, pf, af):
+        pred, act = _frame(pf, "predictions_frame"), _frame(af, "actuals_frame")
+        w = _frame(p["weights_frame"]) if p.get("weights_frame") else None
+        mm = api.make_metrics(pred, act, domain=p.get("domain"), distribution=p.get("distribution"), weights=w,
+                              auc_type=p.get("auc_type") or "NONE")
+        return {"__meta": S.meta("ModelMetricsMakerSchemaV3", "Iced"), "model_metrics": S.metrics_v3(mm)}
+
+    @route("POST", "/3/MissingInserter")
+    def missing_inserter(p, r):
+        fid = p.get("dataset")
+        fr = _frame(fid, "dataset")
+        fr.insert_missing_values(fraction=float(p.get("fraction", 0.1)), seed=p.get("seed"))
+        return S.job_v3(key_name=f"missing_{fid}", dest=fid, description="Insert Missing Values")
+
+    @route("POST", "/3/Interaction")
+    def interaction(p, r):
+        fr = _frame(p.get("source_frame"), "source_frame")
+        facs = p.get("factor_columns") or []
+        facs = [fr.names[int(f)] if isinstance(f, int) else str(f) for f in facs]
+        out = api.interaction(fr, facs, bool(p.get("pairwise", False)), int(p.get("max_factors", 100)),
+                              int(p.get("min_occurrence", 1)))
+        fid = _put_frame(out, p.get("dest"))
+        return S.job_v3(key_name=f"interaction_{fid}", dest=fid, description="Interactions")
+
+    @route("POST", "/3/ImportFilesMulti")
+    def import_files_multi(p, r):
+        from ..core.parse import _files
+        keys, files = [], []
+        for path in p.get("paths") or []:
+            for f in _files(path, p.get("pattern")):
+                uploads.paths[f] = [f]
+                keys.append(f)
+                files.append(f)
+        return {"__meta": S.meta("ImportFilesMultiV3", "Iced"), "paths": p.get("paths"), "files": files,
+                "destination_frames": keys, "fails": [], "dels": []}
+
+    @route("POST", "/99/ImportSQLTable")
+    def import_sql(p, r):
+        if p.get("select_query"):
+            fr = api.import_sql_select(p["connection_url"], p["select_query"], p.get("username"), p.get("password"))
+        else:
+            cols = p.get("columns")
+            cols = [c.strip() for c in cols.split(",")] if isinstance(cols, str) else cols
+            fr = api.import_sql_table(p["connection_url"], p["table"], p.get("username"), p.get("password"),
+                                      columns=cols)
+        fid = _put_frame(fr)
+        return S.job_v3(key_name=f"sql_{fid}", dest=fid, description="Import SQL Table")
+
+    @route("POST", "/3/PartialDependence/")
+    def partial_dependence(p, r):
+        """PartialDependenceHandler: 1-D partial dependence tables per column
+        (per target class when `targets` is given), kept under destination_key."""
+        m, fr = _model(p.get("model_id")), _frame(p.get("frame_id"))
+        cols = p.get("cols") or [c for c in (m._spec.x if m._spec is not None else [])]
+        w = p.get("weight_column_index")
+        wname = fr.names[int(w)] if isinstance(w, int) and w >= 0 else None
+        row = p.get("row_index")
+        tabs = m.partial_plot(fr, cols=list(cols), nbins=int(p.get("nbins", 20)), weight_column=wname,
+                              include_na=bool(p.get("add_missing_na", False)), targets=p.get("targets"),
+                              row_index=None if row is None or int(row) < 0 else int(row))
+        dest = p.get("destination_key") or f"pdp_{uuid.uuid4().hex[:8]}"
+        pdp[dest] = {"model_id": m.model_id, "frame_id": fr.frame_id, "tables": tabs}
+        return S.job_v3(key_name=f"pdp_{dest}", dest=dest, description="PartialDependencePlot")
+
+    pdp: dict = {}
+
+    @route("GET", "/3/PartialDependence/{dest}")
+    def partial_dependence_get(p, r, dest):
+        rec = pdp.get(dest)
+        if rec is None:
+            raise _HTTPError(404, f"partial dependence {dest} not found")
+        tabs = []
+        for t in rec["tables"]:
+            df = t if hasattr(t, "columns") else t.as_data_frame()
+            tabs.append(S.twodim_from_df(f"PartialDependence for {df.columns[0]}", df))
+        return {"__meta": S.meta("PartialDependenceV3", "PartialDependence"), "model_id": S.key(rec["model_id"], "Model"),
+                "frame_id": S.key(rec["frame_id"]), "destination_key": S.key(dest), "partial_dependence_data": tabs}
+
+    @route("GET", "/3/NetworkTest")
+    def network_test(p, r):
+        return {"__meta": S.meta("NetworkTestV3", "Iced"), "table": S.twodim("Network Test", {"bandwidth": [0.0]})}
+
     # -------------------------------------------------------------- jobs
     @route("GET", "/3/Jobs")
     def jobs(p, r):

@@ -83,3 +83,7 @@ def test_reference_python_client_end_to_end(server_url):
     assert out["table"] == [3, 2] and out["group_by"] == [3, 2] and out["cbind"] == 7
     assert out["nunique"] == [3] and out["isna"] == 0 and out["ascharacter"] == "string"
     assert out["aml_leader"] and out["aml_lb"][0] == 2
+    assert out["saved"] and abs(out["loaded_auc"] - va_auc) < 1e-9
+    assert out["exported_rows"] == out["split"][0]
+    assert abs(out["make_metrics_auc"] - va_auc) < 1e-6
+    assert out["pdp_rows"] >= 2 and 5 <= out["missing"] <= 40

@@ -90,4 +90,20 @@ aml = H2OAutoML(max_models=2, seed=1, include_algos=["GLM", "GBM"], nfolds=2, pr
 aml.train(x=["a", "b"], y="y", training_frame=fr)
 step("aml_leader", aml.leader.model_id)
 step("aml_lb", list(aml.leaderboard.as_data_frame().shape))
+d2 = tempfile.mkdtemp()
+saved = h2o.save_model(m, path=d2, force=True)
+step("saved", os.path.exists(saved))
+m3 = h2o.load_model(saved)
+step("loaded_auc", m3.model_performance(te).auc())
+csv_path = os.path.join(d2, "fr.csv")
+h2o.export_file(tr, csv_path, force=True)
+step("exported_rows", sum(1 for _ in open(csv_path)) - 1)
+pte = m.predict(te)
+mm = h2o.make_metrics(pte["yes"], te["y"])
+step("make_metrics_auc", mm.auc())
+pd_tabs = m.partial_plot(te, cols=["a"], plot=False, nbins=5)
+step("pdp_rows", pd_tabs[0].as_data_frame().shape[0] if hasattr(pd_tabs[0], "as_data_frame") else len(pd_tabs[0].cell_values))
+fm = h2o.H2OFrame(pd.DataFrame({"u": rng.normal(size=50), "v": rng.normal(size=50)}))
+fm.insert_missing_values(fraction=0.2, seed=1)
+step("missing", int(fm.isna().sum()))
 print("RESULT", json.dumps(out, default=str))
