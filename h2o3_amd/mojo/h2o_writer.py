@@ -127,88 +127,131 @@ def _f32(v):
     return struct.pack("<f", float(np.float32(v)))
 
 
+def _subtree_counts(left, right):
+    """Split nodes under each node (itself included), bottom-up: children are
+    always numbered after their parent (Tree.add_children appends)."""
+    n = len(left)
+    ns = np.zeros(n, dtype=np.int64)
+    for i in range(n - 1, -1, -1):
+        if left[i] >= 0:
+            ns[i] = 1 + ns[left[i]] + ns[right[i]]
+    return ns
+
+
 def _encode_tree(tree, leaf_map=None):
     """Our Tree (x < thr goes left; cat_left = level mask going left) -> the
     reference's pre-order byte stream.  leaf_map(value) transforms leaf values
-    (e.g. DRF binomial class-0 probabilities)."""
+    (e.g. DRF binomial class-0 probabilities).  Subtree byte sizes are
+    computed bottom-up, then the stream is written front to back with an
+    explicit stack (deep DRF trees have 10^5-10^6 nodes)."""
     lm = leaf_map or (lambda v: v)
-
-    def is_leaf(i):
-        return tree.left[i] < 0
-
-    if is_leaf(0):
+    left = np.asarray(tree.left, dtype=np.int64)
+    right = np.asarray(tree.right, dtype=np.int64)
+    if left[0] < 0:
         return b"\x00" + struct.pack("<H", 65535) + _f32(lm(tree.value[0]))
-
-    def enc(i):
+    n = len(left)
+    thr = np.asarray(tree.thr, dtype=np.float64)
+    feat = np.asarray(tree.feat, dtype=np.int64)
+    if int(feat[left >= 0].max(initial=0)) >= 65535:
+        raise ValueError("reference tree MOJOs address at most 65534 columns")
+    heads = [None] * n            # node type byte + column + NA direction + split payload, per split node
+    size = np.zeros(n, dtype=np.int64)
+    for i in range(n - 1, -1, -1):
+        l = left[i]
+        if l < 0:
+            continue
+        r = right[i]
         node_type = 0
-        body = bytearray()
-        f = int(tree.feat[i])
-        if f >= 65535:
-            raise ValueError("reference tree MOJOs address at most 65534 columns")
         if tree.is_cat[i]:
             mask = np.asarray(tree.cat_left[i]).astype(bool)
-            right = ~mask                         # bitset bit set -> go right
-            nbits = len(right)
+            rb = ~mask                            # bitset bit set -> go right
+            nbits = len(rb)
             nsd = _NSD_NA_LEFT if tree.na_left[i] else _NSD_NA_RIGHT
             if nbits <= 32:
                 node_type |= 8
                 bits = np.zeros(32, dtype=bool)
-                bits[:nbits] = right
+                bits[:nbits] = rb
                 split = np.packbits(bits, bitorder="little").tobytes()
             else:
                 node_type |= 12
-                split = struct.pack("<Hi", 0, nbits) + np.packbits(right, bitorder="little").tobytes()
-        elif not np.isfinite(tree.thr[i]) and tree.thr[i] > 0:
+                split = struct.pack("<Hi", 0, nbits) + np.packbits(rb, bitorder="little").tobytes()
+        elif not np.isfinite(thr[i]) and thr[i] > 0:
             nsd = _NSD_NA_VS_REST                 # every number left, NA right
             split = b""
         else:
             nsd = _NSD_NA_LEFT if tree.na_left[i] else _NSD_NA_RIGHT
-            split = _f32(tree.thr[i])
-        l, r = int(tree.left[i]), int(tree.right[i])
-        if is_leaf(l):
+            split = _f32(thr[i])
+        sz = 4 + len(split)
+        if left[l] < 0:
             node_type |= 48
-            left_bytes = _f32(lm(tree.value[l]))
+            sz += 4
         else:
-            sub = enc(l)
-            n = len(sub)
-            width = 1 if n < (1 << 8) else 2 if n < (1 << 16) else 3 if n < (1 << 24) else 4
+            sl = int(size[l])
+            width = 1 if sl < (1 << 8) else 2 if sl < (1 << 16) else 3 if sl < (1 << 24) else 4
             node_type |= width - 1
-            left_bytes = n.to_bytes(width, "little") + sub
-        if is_leaf(r):
+            sz += width + sl
+        if left[r] < 0:
             node_type |= 0xC0
-            right_bytes = _f32(lm(tree.value[r]))
+            sz += 4
         else:
-            right_bytes = enc(r)
-        body += bytes([node_type]) + struct.pack("<H", f) + bytes([nsd]) + split + left_bytes + right_bytes
-        return bytes(body)
+            sz += int(size[r])
+        size[i] = sz
+        heads[i] = bytes([node_type]) + struct.pack("<H", int(feat[i])) + bytes([nsd]) + split
+    out = bytearray()
+    stack = [("node", 0)]
+    while stack:
+        kind, i = stack.pop()
+        if kind == "leaf":
+            out += _f32(lm(tree.value[i]))
+            continue
+        l, r = int(left[i]), int(right[i])
+        out += heads[i]
+        if left[l] >= 0:
+            sl = int(size[l])
+            out += sl.to_bytes((heads[i][0] & 3) + 1, "little")
+        # pre-order: left part, then right part (stack: push right first)
+        stack.append(("leaf", r) if left[r] < 0 else ("node", r))
+        stack.append(("leaf", l) if left[l] < 0 else ("node", l))
+    return bytes(out)
 
-    return enc(0)
+
+_AUX = np.dtype([("nid", "<i4"), ("nsl", "<i4"), ("wl", "<f4"), ("wr", "<f4"), ("pl", "<f4"), ("pr", "<f4"),
+                 ("sel", "<f4"), ("ser", "<f4"), ("l", "<i4"), ("r", "<i4")])
 
 
 def _encode_aux(tree, leaf_map=None):
     """AuxInfo records (pre-order over split nodes): nid, #split nodes in the
     left subtree, child weights, child predictions, squared errors (0: not
-    tracked), child node ids."""
+    tracked), child node ids -- one structured array, written at once."""
     lm = leaf_map or (lambda v: v)
-    out = bytearray()
-
-    def n_splits(i):
-        if tree.left[i] < 0:
-            return 0
-        return 1 + n_splits(tree.left[i]) + n_splits(tree.right[i])
-
-    def walk(i):
-        if tree.left[i] < 0:
-            return
-        l, r = int(tree.left[i]), int(tree.right[i])
-        out.extend(struct.pack("<ii", i, n_splits(l)))
-        out.extend(struct.pack("<ffff", tree.weight[l], tree.weight[r], lm(tree.value[l]), lm(tree.value[r])))
-        out.extend(struct.pack("<ffii", 0.0, 0.0, l, r))
-        walk(l)
-        walk(r)
-
-    walk(0)
-    return bytes(out)
+    left = np.asarray(tree.left, dtype=np.int64)
+    right = np.asarray(tree.right, dtype=np.int64)
+    if left[0] < 0:
+        return b""
+    ns = _subtree_counts(left, right)
+    order = []
+    stack = [0]
+    while stack:
+        i = stack.pop()
+        if left[i] < 0:
+            continue
+        order.append(i)
+        stack.append(int(right[i]))
+        stack.append(int(left[i]))
+    order = np.asarray(order, dtype=np.int64)
+    l, r = left[order], right[order]
+    w = np.asarray(tree.weight, dtype=np.float64)
+    v = np.asarray(tree.value, dtype=np.float64)
+    rec = np.zeros(order.size, dtype=_AUX)
+    rec["nid"], rec["nsl"] = order, ns[l]
+    rec["wl"], rec["wr"] = w[l], w[r]
+    if leaf_map is None:
+        rec["pl"], rec["pr"] = v[l], v[r]
+    else:
+        rec["pl"] = [lm(x) for x in v[l]]
+        rec["pr"] = [lm(x) for x in v[r]]
+    rec["l"], rec["r"] = l, r
+    return rec.tobytes()
 
 
 def _tree_model(model, z, algo_short, algo_full, extra, leaf_maps, supervised=True, category=None):

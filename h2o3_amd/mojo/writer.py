@@ -46,7 +46,10 @@ class _Writer:
 
     def to_zip_bytes(self, info, columns, domains):
         b = io.BytesIO()
-        with zipfile.ZipFile(b, "w", zipfile.ZIP_DEFLATED) as z:
+        # deflate level 1: forests of deep DRF models reach GBs of node arrays,
+        # where level 6 costs minutes for a few % of size; nested model zips
+        # (stacked ensembles, RuleFit) are stored, not deflated a second time
+        with zipfile.ZipFile(b, "w", zipfile.ZIP_DEFLATED, compresslevel=1) as z:
             ini = ["[info]"] + [f"{k} = {v}" for k, v in info.items()] + ["", "[columns]"] + list(columns) + \
                   ["", "[domains]"]
             for i, (col, dom) in enumerate(domains):
@@ -57,7 +60,7 @@ class _Writer:
             for k, v in self.arrays.items():
                 z.writestr(f"arrays/{k}.npy", _npy(v))
             for k, v in self.files.items():
-                z.writestr(k, v)
+                z.writestr(k, v, compress_type=zipfile.ZIP_STORED if k.endswith(".zip") else None)
         return b.getvalue()
 
 

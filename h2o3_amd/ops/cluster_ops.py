@@ -28,6 +28,8 @@ def _lib():
         lib.h2o_kmeans_part_stride.argtypes = [_ci, _ci]
         lib.h2o_kmeans_part_stride.restype = _cll
         lib.h2o_kmeans_resident_per_cu.argtypes = [_ci, _ci, _ci, _cf]
+        lib.h2o_kmeans_sums.argtypes = [_cv, _cv, _cll, _ci, _ci, _cv, _cv, _cv, _cv, _ci, _cf, _cv]
+        lib.h2o_kmeans_sums_resident_per_cu.argtypes = [_ci, _ci]
         lib._typed = True
     return lib
 
@@ -114,15 +116,17 @@ def lloyd_pass(X, C, w=None, assign=None, accumulate=True, dmin=None, use_native
         rows_wg = 64 * (-(-ntiles // _cu_count(X.device)))
         fx = float(2.0 ** 62 / (max(xabs_max, 1e-30) * rows_wg)) if xabs_max > 0 else 1.0
         fx = min(fx, 2.0 ** 100)
+    stride = int(lib.h2o_kmeans_part_stride(k, P))
+    stream = _cv(torch.cuda.current_stream().cuda_stream)
+    if accumulate and fx > 0 and n_groups is None and _split_ok(lib, k, P, fx):
+        return _lloyd_split(lib, X, C32, cn, wt, k, P, ntiles, assign, dmin, xabs_max, stride, stream)
     if n_groups is None:
         # persistent grid = exactly the resident workgroups (no tail wave)
         per_cu = int(lib.h2o_kmeans_resident_per_cu(k, P, 1 if accumulate else 0, fx))
         n_groups = max(1, min(ntiles, max(per_cu, 1) * _cu_count(X.device)))
     part = None
-    stride = int(lib.h2o_kmeans_part_stride(k, P))
     if accumulate:
         part = torch.empty((n_groups, stride), dtype=torch.float64, device=X.device)
-    stream = _cv(torch.cuda.current_stream().cuda_stream)
     rc = lib.h2o_kmeans_lloyd(_ptr(X), _ptr(wt), N, P, _ptr(C32), _ptr(cn), k, _ptr(assign), _ptr(assign), _ptr(dmin),
                               _ptr(part), n_groups, 1 if accumulate else 0, fx, stream)
     if rc != 0:
@@ -133,6 +137,56 @@ def lloyd_pass(X, C, w=None, assign=None, accumulate=True, dmin=None, use_native
     rc = lib.h2o_kmeans_reduce(_ptr(part), n_groups, stride, _ptr(out), stream)
     if rc != 0:
         raise RuntimeError(f"h2o_kmeans_reduce failed: {rc}")
+    return LloydStats(out, k, P)
+
+
+def _split_ok(lib, k, P, fx):
+    """Large-k split path (assignment pass + sums pass) when the fused kernel
+    would run one workgroup per CU (its LDS holds X tile + centers + sums)
+    and the sums kernel fits; H2O3_KM_SPLIT=1 / 0 forces it on / off."""
+    import os
+    mode = os.environ.get("H2O3_KM_SPLIT", "auto")
+    if mode == "0":
+        return False
+    if int(lib.h2o_kmeans_sums_resident_per_cu(k, P)) < 1:
+        return False
+    return mode == "1" or int(lib.h2o_kmeans_resident_per_cu(k, P, 1, fx)) <= 1
+
+
+def _lloyd_split(lib, X, C32, cn, wt, k, P, ntiles, assign, dmin, xabs_max, stride, stream):
+    """Two HIP passes: the Lloyd kernel in assignment-only mode (new
+    assignment + per-row d2, X tile and centers in LDS) then
+    kmeans_sums_kernel (64-bit fixed-point per-cluster sums, weights,
+    within-SS, changed count) -- see kmeans.hip."""
+    N = X.shape[0]
+    dev = X.device
+    cus = _cu_count(dev)
+    asg_new = torch.empty(N, dtype=torch.int32, device=dev)
+    d2 = dmin if (dmin is not None and dmin.dtype == torch.float32 and dmin.is_contiguous()) else \
+        torch.empty(N, dtype=torch.float32, device=dev)
+    per_cu = int(lib.h2o_kmeans_resident_per_cu(k, P, 0, 0.0))
+    g1 = max(1, min(ntiles, max(per_cu, 1) * cus))
+    rc = lib.h2o_kmeans_lloyd(_ptr(X), _ptr(wt), N, P, _ptr(C32), _ptr(cn), k, _ptr(asg_new), None, _ptr(d2),
+                              None, g1, 0, 0.0, stream)
+    if rc != 0:
+        raise RuntimeError(f"h2o_kmeans_lloyd (assignment pass) failed: {rc}")
+    g2 = max(1, min(ntiles, max(int(lib.h2o_kmeans_sums_resident_per_cu(k, P)), 1) * cus))
+    rows_wg = 64 * (-(-ntiles // g2))
+    fx = float(2.0 ** 62 / (max(xabs_max, 1e-30) * rows_wg)) if xabs_max > 0 else 1.0
+    fx = min(fx, 2.0 ** 100)
+    part = torch.empty((g2, stride), dtype=torch.float64, device=dev)
+    rc = lib.h2o_kmeans_sums(_ptr(X), _ptr(wt), N, P, k, _ptr(asg_new), _ptr(assign), _ptr(d2), _ptr(part), g2, fx,
+                             stream)
+    if rc != 0:
+        raise RuntimeError(f"h2o_kmeans_sums failed: {rc}")
+    out = torch.empty(stride, dtype=torch.float64, device=dev)
+    rc = lib.h2o_kmeans_reduce(_ptr(part), g2, stride, _ptr(out), stream)
+    if rc != 0:
+        raise RuntimeError(f"h2o_kmeans_reduce failed: {rc}")
+    if assign is not None:
+        assign.copy_(asg_new)
+    if dmin is not None and d2 is not dmin:
+        dmin.copy_(d2)
     return LloydStats(out, k, P)
 
 

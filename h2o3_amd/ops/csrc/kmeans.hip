@@ -327,6 +327,95 @@ __global__ __launch_bounds__(256) void kmeans_reduce_kernel(const double* __rest
   out[e] = s;
 }
 
+// Large-k split path, second half: per-cluster sums of an assignment that
+// the Lloyd kernel (acc = 0) already wrote.  At large k the fused kernel's
+// LDS (X tile + centers + sums) allows one resident workgroup per CU and
+// the whole pass runs latency-bound (profiles/kmeans_100m_k64_phase_mb.txt:
+// 89 ms at k = 64, 49 ms of it in the sums).  Here the assignment pass keeps
+// only X tile + centers in LDS, and this kernel keeps only the [k][P] 64-bit
+// fixed-point sums: consecutive lanes take consecutive columns of a tile
+// (coalesced 4-B loads, consecutive u64 LDS words: at most 2 lanes per bank
+// pair, no same-address collisions within a wave-instruction), one
+// returnless ds_add_u64 per (row, column).  Row weights / within-SS / changed
+// assignments as in the fused kernel; one f64 partial per workgroup.
+__global__ __launch_bounds__(KM_THREADS) void kmeans_sums_kernel(
+    const float* __restrict__ X, const float* __restrict__ w, long long N, int P, int k,
+    const int* __restrict__ asg, const int* __restrict__ asg_old, const float* __restrict__ d2,
+    double* __restrict__ part, float fx_scale) {
+  extern __shared__ __align__(16) unsigned long long S64[];   // [k][P]
+  float* Swt = (float*)(S64 + (size_t)k * P);                   // [k]
+  float* Sss = Swt + k;                                          // [k]
+  int* tasg = (int*)(Sss + k);                                   // [64]
+  float* tw = (float*)(tasg + KM_ROWS);                          // [64]
+  __shared__ int changed_s;
+  const int tid = threadIdx.x;
+  for (int e = tid; e < k * P; e += KM_THREADS) S64[e] = 0ull;
+  for (int e = tid; e < 2 * k; e += KM_THREADS) Swt[e] = 0.f;
+  if (tid == 0) changed_s = 0;
+  double wacc[2] = {0.0, 0.0};
+  const long long ntiles = (N + KM_ROWS - 1) / KM_ROWS;
+  const int G = gridDim.x;
+  const int bid = xcd_remap(blockIdx.x, G);
+  const int dr = KM_THREADS / P, dc = KM_THREADS - (KM_THREADS / P) * P;
+  const int r_init = tid / P, c_init = tid - (tid / P) * P;
+  __syncthreads();
+  for (long long t = bid; t < ntiles; t += G) {
+    const long long r0 = t * KM_ROWS;
+    const long long nrow = min((long long)KM_ROWS, N - r0);
+    if (tid < KM_ROWS) {
+      int a = 0;
+      float wr = 0.f;
+      if (tid < nrow) {
+        const long long r = r0 + tid;
+        a = asg[r];
+        wr = w ? w[r] : 1.f;
+        if (asg_old && asg_old[r] != a) atomicAdd(&changed_s, 1);
+        if (wr != 0.f) {
+          lds_add(Swt + a, wr);
+          lds_add(Sss + a, wr * d2[r]);
+        }
+      }
+      tasg[tid] = a;
+      tw[tid] = wr;
+    }
+    __syncthreads();
+    const float* src = X + r0 * P;
+    const int tot = (int)nrow * P;
+    int r = r_init, c = c_init;
+    for (int e = tid; e < tot; e += KM_THREADS) {
+      const float wr = tw[r];
+      const float v = wr * src[e];
+      if (v != 0.f)
+        __hip_atomic_fetch_add(S64 + tasg[r] * P + c, (unsigned long long)__float2ll_rn(v * fx_scale),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      r += dr; c += dc;
+      if (c >= P) { c -= P; ++r; }
+    }
+    __syncthreads();
+    // weights / within-SS of this tile: f32 LDS -> f64 registers, LDS re-zeroed
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int e = tid + h * KM_THREADS;
+      if (e < 2 * k) { wacc[h] += (double)Swt[e]; Swt[e] = 0.f; }
+    }
+    // the next tile's row stats are added only after its first barrier
+  }
+  __syncthreads();
+  double* o = part + (long long)blockIdx.x * km_part_stride(k, P);
+  const double inv = 1.0 / (double)fx_scale;
+  for (int e = tid; e < k * P; e += KM_THREADS) o[e] = (double)(long long)S64[e] * inv;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int e = tid + h * KM_THREADS;
+    if (e < 2 * k) o[(long long)k * P + e] = wacc[h];
+  }
+  if (tid == 0) o[(long long)k * P + 2 * k] = (double)changed_s;
+}
+
+static size_t km_sums_lds_bytes(int k, int P) {
+  return (size_t)k * P * 8 + (size_t)2 * k * 4 + 2 * KM_ROWS * 4;
+}
+
 static int km_kt(int k) {   // the template instance a given k runs on
   const int kt = (k + 15) / 16;
   return kt <= 1 ? 1 : kt <= 2 ? 2 : kt <= 4 ? 4 : kt <= 8 ? 8 : 16;
@@ -446,6 +535,37 @@ int h2o_kmeans_lloyd(const float* X, const float* w, long long N, int P, const f
   if (kt <= 4) return km_launch<4>(X, w, N, P, C, cn, k, assign, assign_old, dmin, part, G, acc, fx_scale, s);
   if (kt <= 8) return km_launch<8>(X, w, N, P, C, cn, k, assign, assign_old, dmin, part, G, acc, fx_scale, s);
   return km_launch<16>(X, w, N, P, C, cn, k, assign, assign_old, dmin, part, G, acc, fx_scale, s);
+}
+
+// Large-k split path: LDS bytes / resident workgroups per CU of the sums
+// kernel, and the launch.  asg: the new assignment (Lloyd kernel, acc = 0),
+// asg_old: the previous one (changed count; may be null), d2: the per-row
+// squared distances it wrote (dmin), fx_scale > 0 as for h2o_kmeans_lloyd.
+int h2o_kmeans_sums_resident_per_cu(int k, int P) {
+  const size_t lds = km_sums_lds_bytes(k, P);
+  if (lds > 160 * 1024) return 0;
+  if (hipFuncSetAttribute((const void*)kmeans_sums_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+      hipSuccess)
+    return 0;
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kmeans_sums_kernel, KM_THREADS, lds) != hipSuccess)
+    return 0;
+  return per_cu;
+}
+
+int h2o_kmeans_sums(const float* X, const float* w, long long N, int P, int k, const int* asg, const int* asg_old,
+                    const float* d2, double* part, int G, float fx_scale, hipStream_t s) {
+  if (N <= 0) return 0;
+  if (P <= 0 || P > 256 || k <= 0 || k > 256 || G <= 0 || !part || !asg || !d2 || !(fx_scale > 0.f))
+    return (int)hipErrorInvalidValue;
+  const size_t lds = km_sums_lds_bytes(k, P);
+  if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
+  hipError_t e = hipFuncSetAttribute((const void*)kmeans_sums_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)lds);
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(kmeans_sums_kernel, dim3(G), dim3(KM_THREADS), lds, s, X, w, N, P, k, asg, asg_old, d2, part,
+                     fx_scale);
+  H2O_CHECK_LAUNCH();
 }
 
 int h2o_kmeans_reduce(const double* part, int G, long long stride, double* out, hipStream_t s) {

@@ -155,8 +155,10 @@ class _Uploads:
         self.setups: dict[str, tuple] = {}
 
     def add_bytes(self, data: bytes, name: str | None = None) -> str:
+        import re
         k = name or f"upload_{uuid.uuid4().hex[:16]}"
-        p = os.path.join(self.dir, k.replace("/", "_"))
+        # the key names the file inside the upload directory: no separators, no dot-files
+        p = os.path.join(self.dir, re.sub(r"[^A-Za-z0-9._-]", "_", k).lstrip(".") or "upload")
         with open(p, "wb") as f:
             f.write(data)
         self.paths[k] = [p]

@@ -46,12 +46,18 @@ wall = time.time() - t0
 lb = aml.leaderboard.as_data_frame() if hasattr(aml.leaderboard, "as_data_frame") else aml.leaderboard
 print(lb.head(25).to_string(), flush=True)
 leader = aml.leader
-os.makedirs("gpurun_out/automl", exist_ok=True)
-p_native = leader.download_mojo("gpurun_out/automl")
+# MOJOs go to local scratch (an ensemble over deep forests is GBs: not for gpurun_out/)
+import tempfile  # noqa: E402
+mdir = tempfile.mkdtemp(prefix="automl_mojo_")
+t1 = time.time()
+p_native = leader.download_mojo(mdir)
+mojo_s = time.time() - t1
+mojo_mb = os.path.getsize(p_native) / 2 ** 20
 try:
-    p_h2o = leader.download_mojo("gpurun_out/automl/h2o", format="h2o")
+    p_h2o = leader.download_mojo(os.path.join(mdir, "h2o"), format="h2o")
 except NotImplementedError as e:
     p_h2o = f"not exported: {e}"
 print(json.dumps({"rows": N, "cols": P, "budget_s": BUDGET, "wall_s": round(wall, 1),
                   "n_models": len(lb), "leader": leader.model_id, "leader_auc": float(lb.iloc[0]["auc"]),
-                  "mojo": p_native, "mojo_h2o": p_h2o}), flush=True)
+                  "mojo": os.path.basename(p_native), "mojo_mb": round(mojo_mb, 1), "mojo_s": round(mojo_s, 1),
+                  "mojo_h2o": p_h2o if p_h2o.startswith("not") else os.path.basename(p_h2o)}), flush=True)

@@ -4,7 +4,7 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 R=${ROWS:-12500000}
 OUT=gpurun_out/rocprof_gbm_$R
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT -o run --output-format csv -- python3 bench.py --rows $R --steps 10 --warmup 2 > $OUT.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT -o run --output-format csv -- python3 bench.py --rows $R --steps 10 --warmup 2 --no-glm > $OUT.log 2>&1
 python3 - "$OUT/run_kernel_trace.csv" > gpurun_out/gbm_${R}_pertree.txt <<'PY'
 import csv, sys, collections
 tr = list(csv.DictReader(open(sys.argv[1])))

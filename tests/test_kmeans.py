@@ -280,3 +280,32 @@ def test_lloyd_kernel_large_n_f64_accumulation(fx):
     torch.testing.assert_close(st.sums, sums, rtol=1e-7, atol=0)
     torch.testing.assert_close(st.weights, wts, rtol=1e-7, atol=0)
     torch.testing.assert_close(st.withinss, wss, rtol=1e-6, atol=0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,P,k", [(200_003, 100, 64), (50_001, 36, 130), (9_999, 8, 3)])
+def test_lloyd_split_path_matches_fused(N, P, k, monkeypatch):
+    """Large-k split path (assignment pass + kmeans_sums_kernel) vs the fused
+    kernel: same assignment / distances, same f64 statistics (both 64-bit
+    fixed-point sums), same changed count."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    g = torch.Generator(device="cuda").manual_seed(N + k)
+    X = torch.randn((N, P), generator=g, device="cuda")
+    C = X[torch.randperm(N, generator=g, device="cuda")[:k]].double() + 0.01
+    w = torch.rand(N, generator=g, device="cuda")
+    w[::5] = 0
+    xa = cluster_ops.abs_bound(X, w)
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("H2O3_KM_SPLIT", mode)
+        a = torch.full((N,), -1, dtype=torch.int32, device="cuda")
+        a[::3] = 0
+        dmin = torch.empty(N, dtype=torch.float32, device="cuda")
+        st = cluster_ops.lloyd_pass(X, C, w, a, dmin=dmin, xabs_max=xa)
+        torch.cuda.synchronize()
+        out[mode] = (a.clone(), dmin.clone(), st.vec.clone())
+    assert bool((out["0"][0] == out["1"][0]).all())
+    assert bool((out["0"][1] == out["1"][1]).all())
+    torch.testing.assert_close(out["1"][2], out["0"][2], rtol=1e-9, atol=1e-6)
+    assert float(out["1"][2][-1]) == float(out["0"][2][-1]) > 0
