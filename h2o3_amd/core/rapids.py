@@ -186,6 +186,14 @@ class Env:
             if name in PRIMS:
                 return ("prim", name)
             raise RapidsError(f"Name lookup of '{name}' failed")
+        if _is_frame(v):
+            # Env.addGlobals: a defensive copy of the global frame (same columns,
+            # own name / column lists), so structural changes (rename, :=,
+            # append) never touch the stored frame; in-place prims
+            # (h2o.impute) write back through _rapids_src
+            c = _F().from_vecs(list(v._vecs), list(v.names))
+            c._rapids_src = v
+            return c
         return v
 
 
@@ -536,7 +544,19 @@ PRIMS["h2o.hist"] = PRIMS["hist"] = lambda x, breaks="sturges": x.hist(breaks if
                                                                        else int(breaks))
 PRIMS["cut"] = lambda x, br, lab=None, lowest=0.0, right=1.0, dig=3.0: x.cut(br, lab or None, bool(lowest),
                                                                             bool(right), int(dig))
-PRIMS["h2o.impute"] = lambda x, col, method="mean", comb="interpolate", gb=None, *a: x.impute(int(col), method, comb)
+def _impute(x, col, method="mean", comb="interpolate", gb=None, *a):
+    """AstImpute: imputes the frame IN PLACE (the stored frame too) and
+    returns the fill values."""
+    out = x.impute(int(col), method, comb)
+    src = getattr(x, "_rapids_src", None)
+    if src is not None and len(src._vecs) == len(x._vecs):
+        for j, v in enumerate(x._vecs):
+            if src._vecs[j] is not v:
+                src._vecs[j] = v
+    return out
+
+
+PRIMS["h2o.impute"] = lambda x, col, method="mean", comb="interpolate", gb=None, *a: _impute(x, col, method, comb)
 PRIMS["h2o.fillna"] = lambda x, method="forward", axis=0.0, maxlen=1.0: x.fillna(method, int(axis), int(maxlen))
 PRIMS["pivot"] = lambda x, idx, col, val: x.pivot(idx, col, val)
 PRIMS["melt"] = lambda x, ids, vals=None, vn="variable", valn="value", skipna=0.0: x.melt(
@@ -549,8 +569,16 @@ PRIMS["topn"] = lambda x, col, pct, grab=-1.0: x.topNBottomN(int(col), pct, int(
 PRIMS["which"] = lambda x: x.which()
 PRIMS["which.max"] = lambda x, na_rm=1.0, axis=0.0: x.idxmax(bool(na_rm), int(axis))
 PRIMS["which.min"] = lambda x, na_rm=1.0, axis=0.0: x.idxmin(bool(na_rm), int(axis))
-PRIMS["match"] = lambda x, table, nomatch=0.0, start=1.0, *a: x.match(table if isinstance(table, list) else [table],
-                                                                     nomatch, int(start))
+def _match(x, table, nomatch=0.0, *incomparables):
+    """AstMatch (match fr table nomatch incomparables): 1 where the value is in
+    `table`, else nomatch (NA rows too)."""
+    tab = table if isinstance(table, list) else [table]
+    pos = x.match(tab, -1.0, 1)
+    from .ops_elem import ifelse
+    return ifelse(pos > 0, 1.0, float(nomatch))
+
+
+PRIMS["match"] = lambda x, table, nomatch=0.0, *a: _match(x, table, nomatch, *a)
 PRIMS["%in%"] = lambda x, table: x.isin(table)
 PRIMS["seq"] = _seq
 PRIMS["seq_len"] = lambda n: _seq(1, n)

@@ -307,5 +307,14 @@ def test_lloyd_split_path_matches_fused(N, P, k, monkeypatch):
         out[mode] = (a.clone(), dmin.clone(), st.vec.clone())
     assert bool((out["0"][0] == out["1"][0]).all())
     assert bool((out["0"][1] == out["1"][1]).all())
-    torch.testing.assert_close(out["1"][2], out["0"][2], rtol=1e-9, atol=1e-6)
     assert float(out["1"][2][-1]) == float(out["0"][2][-1]) > 0
+    # f64 statistics of the common assignment: the split path's fixed-point sums
+    # are exact up to the f32 product w*x; the fused kernel at this k may hold
+    # f32 private sums (folded every 16 tiles), so it gets the looser bound
+    idx = out["1"][0].long()
+    oh = torch.nn.functional.one_hot(idx, k).double() * w.double().view(-1, 1)
+    ref = torch.cat([(oh.T @ X.double()).reshape(-1), oh.sum(0), oh.T @ out["1"][1].double()])
+    m = k * P + 2 * k
+    torch.testing.assert_close(out["1"][2][:k * P], ref[:k * P], rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(out["1"][2][k * P:m], ref[k * P:], rtol=1e-5, atol=1e-3)
+    torch.testing.assert_close(out["0"][2][:k * P], ref[:k * P], rtol=2e-5, atol=2e-3)

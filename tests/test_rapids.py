@@ -53,9 +53,14 @@ def test_frame_prims(fr):
     assert lv.as_data_frame()["C1"].tolist() == ["x", "y", "z"]
     assert R("(sort rap1 [0] [0])").as_data_frame()["a"].tolist()[:3] == [5.0, 3.0, 2.0]
     assert R("(year (mktime 2021 5 3 0 0 0 0))").as_data_frame().iloc[0, 0] == 2021
-    R("(:= rap1 99 [0] [1])")
+    # a global frame is looked up as a defensive copy (Env.addGlobals): := and
+    # colnames= change the result, the stored frame only through assign / tmp=
+    assert R("(:= rap1 99 [0] [1])").as_data_frame()["a"].tolist()[1] == 99.0
+    assert h2o.get_frame("rap1").as_data_frame()["a"].tolist()[1] != 99.0
+    R("(assign rap1 (:= rap1 99 [0] [1]))")
     assert h2o.get_frame("rap1").as_data_frame()["a"].tolist()[1] == 99.0
-    R("(colnames= rap1 [0] ['A'])")
+    assert R("(colnames= rap1 [0] ['A'])").names[0] == "A" and h2o.get_frame("rap1").names[0] == "a"
+    R("(tmp= rap1 (colnames= rap1 [0] ['A']))")
     assert h2o.get_frame("rap1").names[0] == "A"
 
 

@@ -87,3 +87,21 @@ def test_reference_python_client_end_to_end(server_url):
     assert out["exported_rows"] == out["split"][0]
     assert abs(out["make_metrics_auc"] - va_auc) < 1e-6
     assert out["pdp_rows"] >= 2 and 5 <= out["missing"] <= 40
+
+
+@pytest.mark.skipif(not os.path.isdir(os.path.join(REF_PY, "h2o")), reason="reference h2o-py client not present")
+@pytest.mark.timeout(300)
+def test_reference_python_client_munging(server_url):
+    """~45 H2OFrame operations of the reference client (merge, sort, impute,
+    cut, string ops, apply, ifelse, group_by, kfold, isin, topN, which, ...)
+    each evaluate on this server without error."""
+    env = dict(os.environ, PYTHONPATH="", OMP_NUM_THREADS="2")
+    r = subprocess.run([sys.executable, "-u", os.path.join(HERE, "wire_client_munging.py"), server_url, REF_PY],
+                       capture_output=True, text=True, timeout=280, env=env, cwd=HERE)
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("SUMMARY ")]
+    assert line, r.stdout[-3000:]
+    out = json.loads(line[-1][len("SUMMARY "):])
+    bad = [ln for ln in r.stdout.splitlines() if ln.startswith("BAD")]
+    assert out["bad"] == [], bad
+    assert out["ok"] >= 45
