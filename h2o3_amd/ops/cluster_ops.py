@@ -150,6 +150,8 @@ def _split_ok(lib, k, P, fx):
         return False
     if int(lib.h2o_kmeans_sums_resident_per_cu(k, P)) < 1:
         return False
+    # 100M x 100 (profiles/kmeans_split_ab_r3.txt): k = 64 94 -> 41 ms, k = 128
+    # 119 -> 91 ms; at k = 16 the fused kernel (2+ workgroups per CU) stays ahead
     return mode == "1" or int(lib.h2o_kmeans_resident_per_cu(k, P, 1, fx)) <= 1
 
 

@@ -338,7 +338,8 @@ __global__ __launch_bounds__(256) void kmeans_reduce_kernel(const double* __rest
 // pair, no same-address collisions within a wave-instruction), one
 // returnless ds_add_u64 per (row, column).  Row weights / within-SS / changed
 // assignments as in the fused kernel; one f64 partial per workgroup.
-__global__ __launch_bounds__(KM_THREADS) void kmeans_sums_kernel(
+#define KMS_THREADS 1024   // sums pass: 16 waves per workgroup hide the X loads at one workgroup per CU
+__global__ __launch_bounds__(KMS_THREADS) void kmeans_sums_kernel(
     const float* __restrict__ X, const float* __restrict__ w, long long N, int P, int k,
     const int* __restrict__ asg, const int* __restrict__ asg_old, const float* __restrict__ d2,
     double* __restrict__ part, float fx_scale) {
@@ -349,14 +350,14 @@ __global__ __launch_bounds__(KM_THREADS) void kmeans_sums_kernel(
   float* tw = (float*)(tasg + KM_ROWS);                          // [64]
   __shared__ int changed_s;
   const int tid = threadIdx.x;
-  for (int e = tid; e < k * P; e += KM_THREADS) S64[e] = 0ull;
-  for (int e = tid; e < 2 * k; e += KM_THREADS) Swt[e] = 0.f;
+  for (int e = tid; e < k * P; e += KMS_THREADS) S64[e] = 0ull;
+  for (int e = tid; e < 2 * k; e += KMS_THREADS) Swt[e] = 0.f;
   if (tid == 0) changed_s = 0;
   double wacc[2] = {0.0, 0.0};
   const long long ntiles = (N + KM_ROWS - 1) / KM_ROWS;
   const int G = gridDim.x;
   const int bid = xcd_remap(blockIdx.x, G);
-  const int dr = KM_THREADS / P, dc = KM_THREADS - (KM_THREADS / P) * P;
+  const int dr = KMS_THREADS / P, dc = KMS_THREADS - (KMS_THREADS / P) * P;
   const int r_init = tid / P, c_init = tid - (tid / P) * P;
   __syncthreads();
   for (long long t = bid; t < ntiles; t += G) {
@@ -382,7 +383,7 @@ __global__ __launch_bounds__(KM_THREADS) void kmeans_sums_kernel(
     const float* src = X + r0 * P;
     const int tot = (int)nrow * P;
     int r = r_init, c = c_init;
-    for (int e = tid; e < tot; e += KM_THREADS) {
+    for (int e = tid; e < tot; e += KMS_THREADS) {
       const float wr = tw[r];
       const float v = wr * src[e];
       if (v != 0.f)
@@ -395,7 +396,7 @@ __global__ __launch_bounds__(KM_THREADS) void kmeans_sums_kernel(
     // weights / within-SS of this tile: f32 LDS -> f64 registers, LDS re-zeroed
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const int e = tid + h * KM_THREADS;
+      const int e = tid + h * KMS_THREADS;
       if (e < 2 * k) { wacc[h] += (double)Swt[e]; Swt[e] = 0.f; }
     }
     // the next tile's row stats are added only after its first barrier
@@ -403,10 +404,10 @@ __global__ __launch_bounds__(KM_THREADS) void kmeans_sums_kernel(
   __syncthreads();
   double* o = part + (long long)blockIdx.x * km_part_stride(k, P);
   const double inv = 1.0 / (double)fx_scale;
-  for (int e = tid; e < k * P; e += KM_THREADS) o[e] = (double)(long long)S64[e] * inv;
+  for (int e = tid; e < k * P; e += KMS_THREADS) o[e] = (double)(long long)S64[e] * inv;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-    const int e = tid + h * KM_THREADS;
+    const int e = tid + h * KMS_THREADS;
     if (e < 2 * k) o[(long long)k * P + e] = wacc[h];
   }
   if (tid == 0) o[(long long)k * P + 2 * k] = (double)changed_s;
@@ -548,7 +549,7 @@ int h2o_kmeans_sums_resident_per_cu(int k, int P) {
       hipSuccess)
     return 0;
   int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kmeans_sums_kernel, KM_THREADS, lds) != hipSuccess)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kmeans_sums_kernel, KMS_THREADS, lds) != hipSuccess)
     return 0;
   return per_cu;
 }
@@ -563,7 +564,7 @@ int h2o_kmeans_sums(const float* X, const float* w, long long N, int P, int k, c
   hipError_t e = hipFuncSetAttribute((const void*)kmeans_sums_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)lds);
   if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(kmeans_sums_kernel, dim3(G), dim3(KM_THREADS), lds, s, X, w, N, P, k, asg, asg_old, d2, part,
+  hipLaunchKernelGGL(kmeans_sums_kernel, dim3(G), dim3(KMS_THREADS), lds, s, X, w, N, P, k, asg, asg_old, d2, part,
                      fx_scale);
   H2O_CHECK_LAUNCH();
 }

@@ -315,6 +315,6 @@ def test_lloyd_split_path_matches_fused(N, P, k, monkeypatch):
     oh = torch.nn.functional.one_hot(idx, k).double() * w.double().view(-1, 1)
     ref = torch.cat([(oh.T @ X.double()).reshape(-1), oh.sum(0), oh.T @ out["1"][1].double()])
     m = k * P + 2 * k
-    torch.testing.assert_close(out["1"][2][:k * P], ref[:k * P], rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(out["1"][2][:k * P], ref[:k * P], rtol=1e-6, atol=1e-4)
     torch.testing.assert_close(out["1"][2][k * P:m], ref[k * P:], rtol=1e-5, atol=1e-3)
     torch.testing.assert_close(out["0"][2][:k * P], ref[:k * P], rtol=2e-5, atol=2e-3)
