@@ -794,9 +794,18 @@ class H2OGeneralizedLinearEstimator(H2OEstimator):
             self._output["removed_collinear_columns"] = list(drv.removed_cols)
         if self._parms.get("compute_p_values"):
             self._p_values(drv)
-        self._output["regularization_path"] = {"lambdas": [s["lambda"] for s in self._path],
-                                               "coefficients": [dict(zip(names + ["Intercept"], list(s["beta"]) + [s["icpt"]]))
-                                                                for s in self._path]}
+        # hex/glm/GLMModel.getRegularizationPath (GetGLMRegPathHandler): per
+        # submodel lambda, alpha, explained training deviance 1 - dev / null dev,
+        # and the coefficients (original and standardized scale)
+        nd = float(self._output.get("null_deviance") or 0.0)
+        self._output["regularization_path"] = {
+            "lambdas": [s["lambda"] for s in self._path],
+            "alphas": [s.get("alpha") for s in self._path],
+            "explained_deviance_train": [(1.0 - float(s["deviance"]) / nd) if nd > 0 else None for s in self._path],
+            "explained_deviance_valid": None,
+            "coefficients": [dict(zip(names + ["Intercept"], list(s["beta"]) + [s["icpt"]])) for s in self._path],
+            "coefficients_std": [dict(zip(names + ["Intercept"], [float(b) for b in s["beta_std"]]))
+                                 for s in self._path]}
 
     def _null_deviance(self, drv):
         mu = torch.full_like(drv.y, drv.ymu)

@@ -536,6 +536,10 @@ def create_app() -> FastAPI:
         except Exception as e:  # noqa: BLE001 - reported to the client as an H2OModelBuilderError
             raise _HTTPError(400, f"Illegal argument(s) for {algo} model: {e}", e, builder=True)
         dkv.put(m.model_id, m)
+        for cm in getattr(m, "_cv_models", None) or []:   # cross_validation_models are fetched by key
+            dkv.put(cm.model_id, cm)
+        if algo == "stackedensemble" and getattr(m, "_meta", None) is not None:
+            dkv.put(m._meta.model_id, m._meta)                # output.metalearner is fetched by key
         return m
 
     @route("POST", "/3/ModelBuilders/{algo}")
@@ -547,6 +551,9 @@ def create_app() -> FastAPI:
                 S.job_v3(key_name=f"job_{m.model_id}", dest=m.model_id, dest_kind="Model",
                          description=f"{algo} Model Build"),
                 "messages": [], "error_count": 0, "parameters": None}
+
+    app.add_api_route("/99/ModelBuilders/{algo}", app.routes[-1].endpoint, methods=["POST"],
+                      name="POST /99/ModelBuilders/{algo}")
 
     @route("POST", "/3/ModelBuilders/{algo}/parameters")
     def validate_params(p, r, algo):
@@ -622,6 +629,13 @@ def create_app() -> FastAPI:
                 mm = S.metrics_v3(m.model_performance(fr), m, fid, S.model_category(m))
             except Exception:  # noqa: BLE001 - metrics are optional for scoring
                 mm = None
+        if mm is None:
+            # prediction-only result (anomaly / leaf assignment / contributions...): the
+            # reference still returns a metrics record carrying the predictions frame
+            mm = {"__meta": S.meta("ModelMetricsBaseV3", "ModelMetricsBase"), "model": S.key(mid, "Model"),
+                  "frame": S.key(fid), "predictions": S.frame_base_v3(key_, pr)}
+        else:
+            mm["predictions"] = S.frame_base_v3(key_, pr)
         if v4:
             return {"__meta": S.meta("JobV4", "Job", 4),
                     "key": S.key(f"predict_{key_}", "Job"), "dest": S.key(key_), "status": "DONE",
@@ -792,6 +806,24 @@ def create_app() -> FastAPI:
             tabs.append(S.twodim_from_df(f"PartialDependence for {df.columns[0]}", df))
         return {"__meta": S.meta("PartialDependenceV3", "PartialDependence"), "model_id": S.key(rec["model_id"], "Model"),
                 "frame_id": S.key(rec["frame_id"]), "destination_key": S.key(dest), "partial_dependence_data": tabs}
+
+    @route("GET", "/3/GetGLMRegPath")
+    def glm_reg_path(p, r):
+        """GetGLMRegPathHandler: the lambda path of a GLM (coefficient rows in
+        coefficient_names order)."""
+        m = _model(p.get("model"))
+        rp = (m._output or {}).get("regularization_path")
+        if rp is None:
+            raise _HTTPError(400, f"model {m.model_id} has no regularization path")
+        names = list(rp["coefficients"][0].keys()) if rp["coefficients"] else []
+        out = {"__meta": S.meta("GLMRegularizationPathV3", "Iced"), "model": S.key(m.model_id, "Model"),
+               "lambdas": rp["lambdas"], "alphas": rp.get("alphas"),
+               "explained_deviance_train": rp.get("explained_deviance_train"),
+               "explained_deviance_valid": rp.get("explained_deviance_valid"), "coefficient_names": names,
+               "coefficients": [[c.get(n) for n in names] for c in rp["coefficients"]],
+               "coefficients_std": [[c.get(n) for n in names] for c in rp["coefficients_std"]]
+               if rp.get("coefficients_std") else None}
+        return out
 
     @route("GET", "/3/NetworkTest")
     def network_test(p, r):

@@ -610,6 +610,13 @@ def model_v3(mid, m) -> dict:
     for k, v in (("response_column", getattr(spec, "y", None)), ("training_frame", frame)):
         if v is not None and k not in m.params:
             params.append(_param_entry(k, v, None))
+    for e in params:
+        if e["name"] == "response_column" and isinstance(e["actual_value"], str):
+            # ColSpecifierV3, as the reference clients read it (actual_params: column_name)
+            col = {"__meta": meta("ColSpecifierV3", "VecSpecifier"), "column_name": e["actual_value"],
+                   "is_member_of_frames": None}
+            e["actual_value"] = e["input_value"] = col
+            e["type"] = "VecSpecifier"
     return jsonable({"__meta": meta("ModelSchemaV3", "Model"), "model_id": key(mid, "Model"), "algo": m.algo,
                      "algo_full_name": type(m).__name__.replace("H2O", "").replace("Estimator", ""),
                      "response_column_name": getattr(spec, "y", None),
@@ -649,5 +656,19 @@ def _algo_output(m, output):
                 for j, n in enumerate(names[:cs.shape[1]]):
                     cols[str(n)] = [float(x) for x in cs[:, j]]
                 output["centers_std"] = twodim("Cluster Means (standardized)", cols)
+    imp = o.get("importance")
+    if isinstance(imp, dict) and imp:
+        # PCA / SVD / GLRM importance of components: rows = statistics, columns pc1..pck
+        rows = list(imp)
+        kk = len(next(iter(imp.values())))
+        tab = twodim("Importance of components", {f"pc{j + 1}": [float(imp[r][j]) for r in rows] for j in range(kk)},
+                     row_headers=rows)
+        output["importance"] = tab
+        if o.get("model_summary") is imp:
+            output["model_summary"] = tab
+    meta_m = getattr(m, "_meta", None)
+    if getattr(m, "algo", "") == "stackedensemble" and meta_m is not None:
+        output["metalearner"] = key(meta_m.model_id, "Model")
+        output["base_models"] = [key(b.model_id, "Model") for b in getattr(m, "_base", [])]
     if "ntrees" in o or hasattr(m, "_forest"):
         output["ntrees"] = o.get("ntrees", len(getattr(m, "_forest", []) or []))

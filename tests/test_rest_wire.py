@@ -105,3 +105,19 @@ def test_reference_python_client_munging(server_url):
     bad = [ln for ln in r.stdout.splitlines() if ln.startswith("BAD")]
     assert out["bad"] == [], bad
     assert out["ok"] >= 45
+
+
+@pytest.mark.skipif(not os.path.isdir(os.path.join(REF_PY, "h2o")), reason="reference h2o-py client not present")
+@pytest.mark.timeout(300)
+def test_reference_python_client_models(server_url):
+    """Model-level accessors of the reference client (tests/wire_client_models.py)."""
+    env = dict(os.environ, PYTHONPATH="", OMP_NUM_THREADS="2")
+    r = subprocess.run([sys.executable, "-u", os.path.join(HERE, "wire_client_models.py"), server_url, REF_PY],
+                       capture_output=True, text=True, timeout=280, env=env, cwd=HERE)
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("SUMMARY ")]
+    assert line, r.stdout[-3000:]
+    out = json.loads(line[-1][len("SUMMARY "):])
+    bad = [ln for ln in r.stdout.splitlines() if ln.startswith("BAD")]
+    assert out["bad"] == [], bad
+    assert out["ok"] >= 30
