@@ -223,6 +223,7 @@ class H2ONaiveBayesEstimator(H2OEstimator):
         coll.allreduce_(cnt)
         self._prior = (cnt + lap) / (cnt.sum() + K * lap) if lap > 0 else cnt / cnt.sum()
         self._tables = {}
+        num_cols = []
         for c in spec.x:
             v = spec.frame.vec(c)
             if v.type == T_ENUM:
@@ -234,17 +235,29 @@ class H2ONaiveBayesEstimator(H2OEstimator):
                 prob = (t + lap) / (t.sum(1, keepdim=True) + L * lap)
                 self._tables[c] = ("cat", prob, list(v.domain))
             else:
-                x = v.as_float(torch.float64)
-                m = ok & ~torch.isnan(x)
-                xm = x[m]
-                # per-class moments as one one-hot GEMM (no contended f64 atomics)
-                st = group_sum(y[m], torch.stack([xm, xm * xm, torch.ones_like(xm)], 1), K).T.contiguous()
-                coll.allreduce_(st)
-                s1, s2, n = st
-                mean = s1 / n.clamp_min(1)
-                var = (s2 - n * mean ** 2) / (n - 1).clamp_min(1)
-                sd = torch.sqrt(var.clamp_min(0))
-                self._tables[c] = ("num", mean, sd)
+                num_cols.append(c)
+        if num_cols:
+            # every numeric column's per-class moments in one pass: one-hot(class)^T
+            # [x | x^2 | non-NA] as f64 GEMMs over row chunks (NaN rows of a column
+            # drop out of that column only, as in NaiveBayes.java's per-column NA skip)
+            P = len(num_cols)
+            yk = torch.where(ok, y, torch.zeros_like(y))
+            wok = ok.to(torch.float64)
+            st = torch.zeros((K, 3 * P), dtype=torch.float64, device=y.device)
+            n = y.shape[0]
+            step = max(1, (1 << 26) // max(3 * P, 1))
+            for a in range(0, n, step):
+                X = torch.stack([spec.frame.vec(c).as_float(torch.float64)[a:a + step] for c in num_cols], 1)
+                M = (~torch.isnan(X)).to(torch.float64) * wok[a:a + step].view(-1, 1)
+                X = torch.nan_to_num(X) * M
+                st += group_sum(yk[a:a + step], torch.cat([X, X * X, M], 1), K)
+            coll.allreduce_(st)
+            s1, s2, cnt_c = st[:, :P], st[:, P:2 * P], st[:, 2 * P:]
+            mean = s1 / cnt_c.clamp_min(1)
+            var = (s2 - cnt_c * mean ** 2) / (cnt_c - 1).clamp_min(1)
+            sd = torch.sqrt(var.clamp_min(0))
+            for j, c in enumerate(num_cols):
+                self._tables[c] = ("num", mean[:, j].contiguous(), sd[:, j].contiguous())
         self._output["apriori"] = self._prior.cpu().tolist()
         self._output["pcond"] = {c: (t[1].cpu().numpy().tolist(), t[2] if t[0] == "cat" else t[2].cpu().tolist())
                                  for c, t in self._tables.items()}
@@ -255,22 +268,28 @@ class H2ONaiveBayesEstimator(H2OEstimator):
         logp = torch.log(self._prior.clamp_min(1e-300)).view(1, -1).repeat(n, 1).to(cloud.device())
         min_sdev, eps_sdev = float(p["min_sdev"]), float(p["eps_sdev"])
         min_prob, eps_prob = float(p["min_prob"]), float(p["eps_prob"])
+        num = [(c, t) for c, t in self._tables.items() if t[0] == "num" and c in frame.names]
         for c, t in self._tables.items():
-            if c not in frame.names:
+            if c not in frame.names or t[0] != "cat":
                 continue
             v = frame.vec(c)
-            if t[0] == "cat":
-                codes = self._adapt_enum(v, t[2]).long()
-                pr = t[1].T[codes.clamp(min=0)]               # [n, K]
-                pr = torch.where(pr <= eps_prob, torch.full_like(pr, min_prob), pr)
-                contrib = torch.log(pr.clamp_min(1e-300))
-                contrib = torch.where((codes < 0).view(-1, 1), torch.zeros_like(contrib), contrib)
-            else:
-                x = v.as_float(torch.float64)
-                mean, sd = t[1], t[2]
-                sd = torch.where(sd <= eps_sdev, torch.full_like(sd, min_sdev), sd)
-                z = (x.view(-1, 1) - mean.view(1, -1)) / sd.view(1, -1)
-                contrib = -0.5 * z * z - torch.log(sd.view(1, -1) * math.sqrt(2 * math.pi))
-                contrib = torch.where(torch.isnan(x).view(-1, 1), torch.zeros_like(contrib), contrib)
-            logp = logp + contrib
+            codes = self._adapt_enum(v, t[2]).long()
+            pr = t[1].T[codes.clamp(min=0)]               # [n, K]
+            pr = torch.where(pr <= eps_prob, torch.full_like(pr, min_prob), pr)
+            contrib = torch.log(pr.clamp_min(1e-300))
+            logp = logp + torch.where((codes < 0).view(-1, 1), torch.zeros_like(contrib), contrib)
+        if num:
+            # all numeric columns at once: Gaussian log densities [rows, P, K] per row chunk
+            mean = torch.stack([t[1] for _, t in num], 0)                # [P, K]
+            sd = torch.stack([t[2] for _, t in num], 0)
+            sd = torch.where(sd <= eps_sdev, torch.full_like(sd, min_sdev), sd)
+            lnorm = torch.log(sd * math.sqrt(2 * math.pi))
+            K = mean.shape[1]
+            step = max(1, (1 << 25) // max(len(num) * K, 1))
+            for a in range(0, n, step):
+                X = torch.stack([frame.vec(c).as_float(torch.float64)[a:a + step] for c, _ in num], 1)
+                z = (X.unsqueeze(2) - mean.unsqueeze(0)) / sd.unsqueeze(0)
+                contrib = -0.5 * z * z - lnorm.unsqueeze(0)
+                contrib = torch.where(torch.isnan(X).unsqueeze(2), torch.zeros_like(contrib), contrib)
+                logp[a:a + step] += contrib.sum(1)
         return torch.softmax(logp, 1)
