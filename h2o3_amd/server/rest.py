@@ -417,8 +417,16 @@ def create_app() -> FastAPI:
                 fr.names = names
         fid = _put_frame(fr, dest)
         if p.get("delete_on_done", True):
+            # the raw upload is consumed by the parse (ParseHandler delete_on_done)
             for k in srcs:
                 uploads.setups = {kk: v for kk, v in uploads.setups.items() if k not in kk[0]}
+                for f in uploads.paths.get(k, []):
+                    if os.path.dirname(f) == uploads.dir:
+                        try:
+                            os.remove(f)
+                        except OSError:
+                            pass
+                        uploads.paths.pop(k, None)
         return {"__meta": S.meta("ParseV3", "Parse"), "destination_frame": S.key(fid),
                 "job": S.job_v3(key_name=f"parse_{fid}", dest=fid, description="Parse"), "rows": fr.nrow}
 
