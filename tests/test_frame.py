@@ -78,3 +78,25 @@ def test_uuid_column_guess(tmp_path):
     fr = h2o.import_file(str(p))
     assert fr.types["id"] == "uuid"
     assert fr["id"].as_data_frame().iloc[0, 0] == str(uuid.UUID(int=12345))
+
+
+def test_fillna_forward_backward_both_axes():
+    """AstFillNA: at most maxlen consecutive NAs filled, down columns or along rows."""
+    import numpy as np
+    import pandas as pd
+    import h2o3_amd as h
+    nan = float("nan")
+    df = pd.DataFrame({"a": [1, nan, nan, nan, 5, nan], "b": [nan, 2, nan, 4, nan, nan],
+                       "c": [nan, nan, 3, nan, nan, 6]})
+    fr = h.H2OFrame(df)
+
+    def same(got, want):
+        np.testing.assert_array_equal(np.asarray(got, dtype=float), np.asarray(want, dtype=float))
+    same(fr.fillna("forward", 0, 2).as_data_frame().values,
+         [[1, nan, nan], [1, 2, nan], [1, 2, 3], [nan, 4, 3], [5, 4, 3], [5, 4, 6]])
+    same(fr.fillna("backward", 0, 1).as_data_frame().values,
+         [[1, 2, nan], [nan, 2, 3], [nan, 4, 3], [5, 4, nan], [5, nan, 6], [nan, nan, 6]])
+    same(fr.fillna("forward", 1, 1).as_data_frame().values,
+         [[1, 1, nan], [nan, 2, 2], [nan, nan, 3], [nan, 4, 4], [5, 5, nan], [nan, nan, 6]])
+    same(fr.fillna("backward", 1, 5).as_data_frame().values,
+         [[1, nan, nan], [2, 2, nan], [3, 3, 3], [4, 4, nan], [5, nan, nan], [6, 6, 6]])
