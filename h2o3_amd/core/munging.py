@@ -464,42 +464,185 @@ class GroupBy:
 
 
 def merge(x, y, all_x=False, all_y=False, by_x=None, by_y=None):
-    """reference: water/rapids/Merge.java (radix-sort join).  Hash join on the
-    host for the key tuples, gather on the device."""
-    import pandas as pd
+    """reference: water/rapids/ast/prims/mungers/AstMerge.java + Merge.java /
+    BinaryMerge.java (radix-sort join).  Inner, left (all_x) or right (all_y)
+    join on the key columns, result ordered by key; rows whose key has an NA
+    never match (Merge.java drops NA-key rows of the right frame).
+
+    Device path: both sides' keys get common order-preserving integer ids
+    (per-column ranks over the union of values -- categorical keys by level
+    name -- combined mixed-radix), the right frame is sorted by id, every left
+    row finds its match range with two searchsorted calls, and the output row
+    pairs come from one repeat_interleave; columns are gathered on the device.
+    String / UUID key columns take the host (pandas) path."""
+    if all_x and all_y:
+        raise ValueError("all.x=TRUE and all.y=TRUE is not supported.  Choose one only.")
     gx, gy = x.gather(), y.gather()
     if by_x is None:
         common = [n for n in gx.names if n in gy.names]
         by_x = by_y = common
-    by_y = by_y or by_x
-    dx = gx.as_data_frame()
-    dy = gy.as_data_frame()
-    dx["__ix"] = np.arange(len(dx))
-    dy["__iy"] = np.arange(len(dy))
-    how = "outer" if (all_x and all_y) else ("left" if all_x else ("right" if all_y else "inner"))
-    m = dx[by_x + ["__ix"]].merge(dy[by_y + ["__iy"]], left_on=by_x, right_on=by_y, how=how, sort=True)
+    by_x = [gx.names[c] if isinstance(c, int) else c for c in by_x]
+    by_y = [gy.names[c] if isinstance(c, int) else c for c in (by_y or by_x)]
+    if not by_x:
+        raise ValueError("merge: no common columns to join on")
+    keys = _join_key_ids(gx, gy, by_x, by_y)
+    if keys is None:
+        res = _merge_host(gx, gy, all_x, all_y, by_x, by_y)
+    else:
+        kx, ky = keys
+        if all_y:
+            iy, ix = _join_pairs(ky, kx, keep_left=True)     # right join = left join from y's side
+        else:
+            ix, iy = _join_pairs(kx, ky, keep_left=all_x)
+        res = _merged_frame(gx, gy, ix, iy, by_x, by_y)
+    return _reshard(res) if cloud.is_distributed() else res
+
+
+def _join_key_ids(gx, gy, by_x, by_y):
+    """(kx, ky) int64 key ids shared by both frames (-1 = NA key), ordered like
+    the key tuples; None when a key column pair needs the host path."""
+    dev = _dev()
+    ranks_x, ranks_y, cards = [], [], []
+    na_x = torch.zeros(gx.nlocal, dtype=torch.bool, device=dev)
+    na_y = torch.zeros(gy.nlocal, dtype=torch.bool, device=dev)
+    for cx, cy in zip(by_x, by_y):
+        vx, vy = gx.vec(cx), gy.vec(cy)
+        if vx.on_host or vy.on_host:
+            return None
+        if (vx.type == T_ENUM) != (vy.type == T_ENUM):
+            return None
+        if vx.type == T_ENUM:
+            union = sorted(set(vx.domain or []) | set(vy.domain or []))
+            pos = {d: i for i, d in enumerate(union)}
+
+            def ids(v):
+                lut = torch.tensor([pos[d] for d in (v.domain or [])] or [0], dtype=torch.float64, device=dev)
+                c = v.data.long()
+                return torch.where(c >= 0, lut[c.clamp(min=0)], torch.full(c.shape, float("nan"), dtype=torch.float64,
+                                                                          device=dev))
+            ax, ay = ids(vx), ids(vy)
+        else:
+            ax, ay = vx.as_float(torch.float64), vy.as_float(torch.float64)
+        na_x |= torch.isnan(ax)
+        na_y |= torch.isnan(ay)
+        both = torch.cat([ax, ay])
+        ok = ~torch.isnan(both)
+        u = torch.unique(both[ok])
+        cards.append(max(int(u.numel()), 1))
+        r = torch.searchsorted(u, torch.nan_to_num(both, nan=0.0))
+        ranks_x.append(r[:gx.nlocal])
+        ranks_y.append(r[gx.nlocal:])
+    tot = 1
+    for c in cards:
+        tot *= c
+    if tot >= (1 << 62):
+        return None
+    kx = torch.zeros(gx.nlocal, dtype=torch.int64, device=dev)
+    ky = torch.zeros(gy.nlocal, dtype=torch.int64, device=dev)
+    for rx, ry, c in zip(ranks_x, ranks_y, cards):
+        kx = kx * c + rx
+        ky = ky * c + ry
+    return torch.where(na_x, torch.full_like(kx, -1), kx), torch.where(na_y, torch.full_like(ky, -1), ky)
+
+
+def _join_pairs(kl, kr, keep_left):
+    """Row index pairs (il, ir) of the join of key ids kl (left) with kr
+    (right), ordered by (key, left row, right row); ir = -1 for kept
+    unmatched left rows (keep_left), whose NA keys sort last."""
+    dev = kl.device
+    okr = kr >= 0
+    rows_r = torch.nonzero(okr).view(-1)
+    kr_ok = kr[rows_r]
+    o = torch.argsort(kr_ok, stable=True)
+    kr_s, rr_s = kr_ok[o], rows_r[o]
+    lo = torch.searchsorted(kr_s, kl, right=False)
+    hi = torch.searchsorted(kr_s, kl, right=True)
+    cnt = torch.where(kl >= 0, hi - lo, torch.zeros_like(lo))
+    out_cnt = torch.clamp(cnt, min=1) if keep_left else cnt
+    left_rows = torch.arange(kl.numel(), device=dev)
+    # left rows in key order (stable: original order within a key), NA keys last
+    kl_sort = torch.where(kl >= 0, kl, torch.full_like(kl, torch.iinfo(torch.int64).max))
+    lord = torch.argsort(kl_sort, stable=True)
+    reps = out_cnt[lord]
+    il = torch.repeat_interleave(left_rows[lord], reps)
+    start = torch.repeat_interleave(lo[lord], reps)
+    first = torch.cumsum(reps, 0) - reps
+    within = torch.arange(il.numel(), device=dev) - torch.repeat_interleave(first, reps)
+    matched = torch.repeat_interleave(cnt[lord] > 0, reps)
+    ir = torch.where(matched, rr_s[(start + within).clamp(max=max(rr_s.numel() - 1, 0))] if rr_s.numel() else
+                     torch.zeros_like(il), torch.full_like(il, -1))
+    return il, ir
+
+
+def _take_dev(v: Vec, idx):
+    """Rows idx (int64 device tensor, -1 = NA row) of v."""
+    na = idx < 0
+    ii = idx.clamp(min=0)
+    if v.on_host:
+        arr = np.asarray(v.data, dtype=object)[ii.cpu().numpy()] if len(v.data) else \
+            np.array([None] * idx.numel(), dtype=object)
+        arr[na.cpu().numpy()] = None
+        return Vec(arr, v.type)
+    d = v.data[ii] if v.nlocal else torch.zeros(idx.numel(), dtype=v.data.dtype, device=idx.device)
+    if v.type == T_ENUM:
+        d = torch.where(na, torch.full_like(d, -1), d)
+    else:
+        d = torch.where(na, torch.full_like(d, float("nan")), d)
+    return Vec(d, v.type, v.domain)
+
+
+def _merged_frame(gx, gy, ix, iy, by_x, by_y):
     vecs, names = [], []
-    ix = m["__ix"].values
-    iy = m["__iy"].values
     for n, v in zip(gx.names, gx._vecs):
-        vecs.append(_take_with_na(v, ix))
+        vecs.append(_take_dev(v, ix))
         names.append(n)
     for n, v in zip(gy.names, gy._vecs):
         if n in by_y:
             continue
         nn = n if n not in names else n + "0"
-        vecs.append(_take_with_na(v, iy))
+        vecs.append(_take_dev(v, iy))
         names.append(nn)
-    # fill keys for right-only rows
-    for kx, ky in zip(by_x, by_y):
-        j = names.index(kx)
-        miss = np.isnan(ix.astype(float)) if ix.dtype.kind == "f" else np.zeros(len(ix), bool)
-        if miss.any():
-            vy = gy.vec(ky)
-            filled = _take_with_na(vy, np.where(miss, iy, np.nan))
+    miss = ix < 0
+    if bool(miss.any()):
+        # right-join rows without a left match: their keys come from the right frame
+        for kx, ky in zip(by_x, by_y):
+            j = names.index(kx)
+            filled = _take_dev(gy.vec(ky), torch.where(miss, iy, torch.full_like(iy, -1)))
+            if vecs[j].type == T_ENUM and filled.type == T_ENUM and vecs[j].domain != filled.domain:
+                filled = _recode(filled, vecs[j].domain)   # left domain, right-only levels appended
+                vecs[j] = Vec(vecs[j].data, T_ENUM, filled.domain)
             vecs[j] = _coalesce(vecs[j], filled)
-    res = H2OFrame.from_vecs(vecs, names)
-    return _reshard(res) if cloud.is_distributed() else res
+    return H2OFrame.from_vecs(vecs, names)
+
+
+def _recode(v: Vec, domain):
+    """Categorical v re-expressed in `domain` (levels missing from it are
+    appended)."""
+    dom = list(domain)
+    pos = {d: i for i, d in enumerate(dom)}
+    for d in v.domain or []:
+        if d not in pos:
+            pos[d] = len(dom)
+            dom.append(d)
+    lut = torch.tensor([pos[d] for d in (v.domain or [])] or [0], dtype=torch.int32, device=v.data.device)
+    c = v.data.long()
+    return Vec(torch.where(c >= 0, lut[c.clamp(min=0)], torch.full_like(v.data, -1)), T_ENUM, dom)
+
+
+def _merge_host(gx, gy, all_x, all_y, by_x, by_y):
+    """Host hash join (string / UUID keys): pandas over the key columns, NA
+    keys never match, rows gathered on the device."""
+    dx = gx[by_x].as_data_frame()
+    dy = gy[by_y].as_data_frame()
+    dx["__ix"] = np.arange(len(dx))
+    dy["__iy"] = np.arange(len(dy))
+    dy = dy.dropna(subset=by_y)
+    how = "left" if all_x else ("right" if all_y else "inner")
+    dxm = dx if all_x else dx.dropna(subset=by_x)
+    m = dxm.merge(dy, left_on=by_x, right_on=by_y, how=how, sort=True)
+    ix = torch.as_tensor(np.nan_to_num(m["__ix"].to_numpy(dtype=float), nan=-1).astype(np.int64), device=_dev())
+    iy = torch.as_tensor(np.nan_to_num(m["__iy"].to_numpy(dtype=float), nan=-1).astype(np.int64), device=_dev())
+    return _merged_frame(gx, gy, ix, iy, by_x, by_y)
 
 
 def _take_with_na(v: Vec, idx):

@@ -100,3 +100,44 @@ def test_fillna_forward_backward_both_axes():
          [[1, 1, nan], [nan, 2, 2], [nan, nan, 3], [nan, 4, 4], [5, 5, nan], [nan, nan, 6]])
     same(fr.fillna("backward", 1, 5).as_data_frame().values,
          [[1, nan, nan], [2, 2, nan], [3, 3, 3], [4, 4, nan], [5, nan, nan], [6, 6, 6]])
+
+
+@pytest.mark.parametrize("how", ["inner", "left", "right"])
+def test_merge_sort_join_matches_pandas(how):
+    """Device sort-join vs pandas on the same keys (categorical keys with
+    different domains on each side, a numeric second key, duplicates on both
+    sides, NA keys that never match -- Merge.java drops NA-key right rows)."""
+    import numpy as np
+    import pandas as pd
+    import h2o3_amd as h
+    rng = np.random.default_rng(7)
+    n, m = 300, 80
+    lx = pd.DataFrame({"k": rng.choice(["a", "b", "c", "d", None], n), "j": rng.integers(0, 3, n).astype(float),
+                       "v": rng.normal(size=n)})
+    ry = pd.DataFrame({"k": rng.choice(["b", "c", "d", "e", None], m), "j": rng.integers(0, 3, m).astype(float),
+                       "w": rng.normal(size=m)})
+    lx.loc[::17, "j"] = np.nan
+    fx, fy = h.H2OFrame(lx), h.H2OFrame(ry)
+    got = fx.merge(fy, all_x=how == "left", all_y=how == "right").as_data_frame()
+    ref = lx.dropna(subset=["k", "j"]) if how == "inner" else lx
+    refy = ry.dropna(subset=["k", "j"])
+    if how == "inner":
+        want = ref.merge(refy, on=["k", "j"], how="inner", sort=True)
+    elif how == "left":
+        want = lx.assign(_na=lx[["k", "j"]].isna().any(axis=1))
+        a = want[~want._na].merge(refy, on=["k", "j"], how="left", sort=True)
+        b = want[want._na].assign(w=np.nan)
+        want = pd.concat([a, b]).drop(columns="_na")
+    else:
+        # all_y = a left join from the right frame's side (AstMerge swaps the frames):
+        # its NA-key rows are kept unmatched, the left frame's NA-key rows dropped
+        want = lx.dropna(subset=["k", "j"]).merge(ry, on=["k", "j"], how="right")
+    cols = ["k", "j", "v", "w"]
+    g = got[cols].reset_index(drop=True)
+    w = want[cols].reset_index(drop=True)
+    assert len(g) == len(w)
+    if how == "right":
+        key = lambda d: d.fillna(-999).sort_values(cols).reset_index(drop=True)   # noqa: E731
+        pd.testing.assert_frame_equal(key(g), key(w), check_dtype=False, atol=1e-6)
+    else:
+        pd.testing.assert_frame_equal(g.fillna(-999), w.fillna(-999), check_dtype=False, atol=1e-6)
