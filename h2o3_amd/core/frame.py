@@ -838,7 +838,9 @@ class H2OFrame:
 
     def cor(self, y=None, na_rm=False, use=None, method="Pearson"):
         from .munging import cor
-        return cor(self, y, method=method)
+        if use is None:
+            use = "complete.obs" if na_rm else "everything"
+        return cor(self, y, method=method, use=use)
 
     def median(self, na_rm=True):
         from .munging import quantile_values

@@ -160,15 +160,36 @@ def _num_matrix(fr):
     return torch.stack([v.as_float(torch.float64) for v in fr._vecs], 1)
 
 
+def _cross(ac, bc):
+    """ac^T bc for [N, p] x [N, q] f64: per column pair reductions when p*q is
+    small (a K = N f64 GEMM of a few columns runs on a poorly shaped library
+    kernel: ~2 s at 20M rows), the GEMM otherwise."""
+    p, q = ac.shape[1], bc.shape[1]
+    if p * q <= 64:
+        return torch.stack([torch.stack([(ac[:, i] * bc[:, j]).sum() for j in range(q)]) for i in range(p)])
+    return ac.T @ bc
+
+
 def cor(x, y=None, method="Pearson", use="everything"):
+    """AstCorrelation: use = "everything" (NAs propagate), "all.obs" (NAs are
+    an error) or "complete.obs" (rows with an NA in any column are dropped)."""
     a = _num_matrix(x.gather())
     b = _num_matrix(y.gather()) if y is not None else a
+    use = (use or "everything").lower()
+    if use not in ("everything", "all.obs", "complete.obs"):
+        raise ValueError(f"use must be everything, all.obs or complete.obs, got {use}")
+    if use != "everything":
+        bad = torch.isnan(a).any(1) | torch.isnan(b).any(1)
+        if use == "all.obs" and bool(bad.any()):
+            raise ValueError("Missing values in the data: use complete.obs or everything")
+        if bool(bad.any()):
+            a, b = a[~bad], b[~bad]
     if method.lower() == "spearman":
         a = torch.argsort(torch.argsort(a, 0), 0).to(torch.float64)
         b = torch.argsort(torch.argsort(b, 0), 0).to(torch.float64)
     ac = a - a.mean(0)
     bc = b - b.mean(0)
-    c = (ac.T @ bc) / torch.sqrt(torch.outer((ac ** 2).sum(0), (bc ** 2).sum(0)))
+    c = _cross(ac, bc) / torch.sqrt(torch.outer((ac ** 2).sum(0), (bc ** 2).sum(0)))
     if c.numel() == 1:
         return float(c)
     import pandas as pd
@@ -179,7 +200,7 @@ def cov(x, y=None):
     a = _num_matrix(x.gather())
     b = _num_matrix(y.gather()) if y is not None else a
     n = a.shape[0]
-    c = ((a - a.mean(0)).T @ (b - b.mean(0))) / (n - 1)
+    c = _cross(a - a.mean(0), b - b.mean(0)) / (n - 1)
     if c.numel() == 1:
         return float(c)
     import pandas as pd

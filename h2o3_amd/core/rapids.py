@@ -475,7 +475,8 @@ PRIMS["mean"] = lambda x, na_rm=0.0, axis=0.0: (x.mean(skipna=bool(na_rm), axis=
 PRIMS["median"] = lambda x, na_rm=1.0: x.median(bool(na_rm))[0] if x.ncols == 1 else x.median(bool(na_rm))
 PRIMS["sd"] = lambda x, na_rm=1.0: x.sd(bool(na_rm))[0] if x.ncols == 1 else x.sd(bool(na_rm))
 PRIMS["var"] = lambda x, y=None, use="everything", symmetric=1.0: x.var(y if _is_frame(y) else None)
-PRIMS["cor"] = lambda x, y=None, use="everything", method="Pearson": x.cor(y if _is_frame(y) else None, method=method)
+PRIMS["cor"] = lambda x, y=None, use="everything", method="Pearson": x.cor(y if _is_frame(y) else None,
+                                                                             use=str(use), method=method)
 PRIMS["nrow"] = lambda x: float(x.nrows)
 PRIMS["ncol"] = lambda x: float(x.ncols)
 PRIMS["dim"] = lambda x: [float(x.nrows), float(x.ncols)]

@@ -141,3 +141,19 @@ def test_merge_sort_join_matches_pandas(how):
         pd.testing.assert_frame_equal(key(g), key(w), check_dtype=False, atol=1e-6)
     else:
         pd.testing.assert_frame_equal(g.fillna(-999), w.fillna(-999), check_dtype=False, atol=1e-6)
+
+
+def test_cor_use_modes():
+    """AstCorrelation use=: everything propagates NAs, complete.obs drops NA rows,
+    all.obs rejects them; na_rm=True means complete.obs."""
+    import numpy as np
+    import pandas as pd
+    import h2o3_amd as h
+    df = pd.DataFrame({"a": [1, 2, np.nan, 4, 5.0], "b": [2, 1, 3, 5, 4.0], "c": [1, 3, 2, 5, 4.0]})
+    fr = h.H2OFrame(df)
+    assert np.isnan(fr.cor().as_data_frame().iloc[0, 1])
+    got = fr.cor(na_rm=True).as_data_frame().values
+    np.testing.assert_allclose(got, df.dropna().corr().values, rtol=1e-6)
+    with pytest.raises(ValueError):
+        fr.cor(use="all.obs")
+    assert abs(fr["b"].cor(fr["c"]) - df.b.corr(df.c)) < 1e-9
