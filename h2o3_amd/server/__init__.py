@@ -1,1 +1,1 @@
-from .rest import create_app, start  # noqa: F401
+from .rest import create_app, create_server_app, start  # noqa: F401

@@ -12,8 +12,15 @@ def main():
     ap.add_argument("--ip", default="127.0.0.1")
     ap.add_argument("--port", type=int, default=54321)
     ap.add_argument("--log-level", default="warning")
+    ap.add_argument("--hash-login", action="store_true", help="HTTP Basic auth against --login-conf (Jetty realm file)")
+    ap.add_argument("--login-conf", default=None, help="realm file: 'user: password[,role]' (plain, MD5:, OBF:)")
+    ap.add_argument("--ssl-certfile", default=None, help="PEM certificate: serve HTTPS")
+    ap.add_argument("--ssl-keyfile", default=None, help="PEM private key for --ssl-certfile")
     a = ap.parse_args()
-    start(ip=a.ip, port=a.port, log_level=a.log_level)
+    if a.hash_login and not a.login_conf:
+        ap.error("--hash-login needs --login-conf")
+    start(ip=a.ip, port=a.port, log_level=a.log_level, login_conf=a.login_conf if a.hash_login else None,
+          ssl_certfile=a.ssl_certfile, ssl_keyfile=a.ssl_keyfile)
 
 
 if __name__ == "__main__":

@@ -1042,8 +1042,21 @@ def create_app() -> FastAPI:
     return app
 
 
-def start(ip="127.0.0.1", port=54321, log_level="warning"):
-    """Serve the REST API (blocking) on rank 0 of a single-process cloud."""
+def create_server_app(login_conf=None, realm="h2o"):
+    """The REST app, behind HTTP Basic authentication when a HashLoginService
+    realm file is given (auth.py)."""
+    app = create_app()
+    if login_conf:
+        from .auth import basic_auth_middleware, load_realm
+        return basic_auth_middleware(app, load_realm(login_conf), realm)
+    return app
+
+
+def start(ip="127.0.0.1", port=54321, log_level="warning", login_conf=None, ssl_certfile=None, ssl_keyfile=None):
+    """Serve the REST API (blocking) on rank 0 of a single-process cloud;
+    login_conf enables Basic auth (the reference's -hash_login), the PEM
+    pair enables HTTPS."""
     import uvicorn
     api.init()
-    uvicorn.run(create_app(), host=ip, port=port, log_level=log_level)
+    uvicorn.run(create_server_app(login_conf), host=ip, port=port, log_level=log_level,
+                ssl_certfile=ssl_certfile, ssl_keyfile=ssl_keyfile)

@@ -64,3 +64,25 @@ def test_rest_parse_grid_automl_mojo(tmp_path):
     lb = c.get("/99/Leaderboards/aml_rest").json()
     assert len(lb["models"]) >= 2
     assert c.get("/3/About").status_code == 200
+
+
+def test_rest_basic_auth_realm_file(tmp_path):
+    """-hash_login: Basic auth against a Jetty realm file (plain, MD5:, OBF:)."""
+    import base64
+    import hashlib
+    from h2o3_amd.server import create_server_app
+    from h2o3_amd.server.auth import deobfuscate
+    realm = tmp_path / "realm.properties"
+    realm.write_text("# users\nalice: wonderland,admin\nbob: MD5:%s\ncarol: OBF:1yta1t331v8w1v9q1t331ytc,user\n"
+                     % hashlib.md5(b"builder").hexdigest())
+    assert deobfuscate("OBF:1yta1t331v8w1v9q1t331ytc") == "secret"
+    h2o.init()
+    c = TestClient(create_server_app(str(realm)))
+
+    def hdr(u, p):
+        return {"Authorization": "Basic " + base64.b64encode(f"{u}:{p}".encode()).decode()}
+    r = c.get("/3/Cloud")
+    assert r.status_code == 401 and "Basic" in r.headers["www-authenticate"]
+    assert c.get("/3/Cloud", headers=hdr("alice", "nope")).status_code == 401
+    for u, p in (("alice", "wonderland"), ("bob", "builder"), ("carol", "secret")):
+        assert c.get("/3/Cloud", headers=hdr(u, p)).json()["cloud_healthy"]

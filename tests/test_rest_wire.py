@@ -121,3 +121,41 @@ def test_reference_python_client_models(server_url):
     bad = [ln for ln in r.stdout.splitlines() if ln.startswith("BAD")]
     assert out["bad"] == [], bad
     assert out["ok"] >= 30
+
+
+@pytest.mark.skipif(not os.path.isdir(os.path.join(REF_PY, "h2o")), reason="reference h2o-py client not present")
+@pytest.mark.timeout(200)
+def test_reference_python_client_basic_auth(tmp_path):
+    """The reference client with auth=(user, password) against a server
+    started with a realm file; without credentials the connect fails."""
+    import uvicorn
+    from h2o3_amd.server import create_server_app
+    realm = tmp_path / "realm.properties"
+    realm.write_text("ana: s3cret,user\n")
+    port = _free_port()
+    srv = uvicorn.Server(uvicorn.Config(create_server_app(str(realm)), host="127.0.0.1", port=port,
+                                        log_level="warning"))
+    th = threading.Thread(target=srv.run, daemon=True)
+    th.start()
+    t0 = time.time()
+    while not srv.started and time.time() - t0 < 30:
+        time.sleep(0.05)
+    code = ("import sys, os; sys.path[:0] = [os.path.join(%r, 'refclient_shim'), %r]\n"
+            "import h2o\n"
+            "h2o.connect(url=%r, auth=('ana', 's3cret'), verbose=False)\n"
+            "fr = h2o.H2OFrame({'a': [1, 2, 3]})\n"
+            "print('ROWS', fr.nrows)\n"
+            "try:\n"
+            "    h2o.connect(url=%r, verbose=False)\n"
+            "    print('NOAUTH ok')\n"
+            "except Exception as e:\n"
+            "    print('NOAUTH rejected', type(e).__name__)\n") % (HERE, REF_PY, f"http://127.0.0.1:{port}",
+                                                                 f"http://127.0.0.1:{port}")
+    try:
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=150,
+                           env=dict(os.environ, PYTHONPATH=""), cwd=HERE)
+    finally:
+        srv.should_exit = True
+        th.join(timeout=10)
+    assert "ROWS 3" in r.stdout, (r.stdout[-2000:], r.stderr[-2000:])
+    assert "NOAUTH rejected" in r.stdout, r.stdout[-2000:]
