@@ -205,6 +205,23 @@ def create_app() -> FastAPI:
             return fn
         return deco
 
+    # ------------------------------------------------------------- Flow UI
+    def _flow_page():
+        with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "static", "flow.html"),
+                  encoding="utf-8") as f:
+            return f.read()
+
+    from fastapi.responses import HTMLResponse, RedirectResponse
+
+    @app.get("/", include_in_schema=False)
+    async def root():
+        return RedirectResponse("/flow/index.html")
+
+    @app.get("/flow/index.html", include_in_schema=False)
+    async def flow():
+        """Minimal Flow (h2o-web): one static page over the /3 endpoints."""
+        return HTMLResponse(_flow_page())
+
     # ------------------------------------------------------------ cloud
     @route("GET", "/3/Cloud")
     def cloud_status(p, r):

@@ -86,3 +86,13 @@ def test_rest_basic_auth_realm_file(tmp_path):
     assert c.get("/3/Cloud", headers=hdr("alice", "nope")).status_code == 401
     for u, p in (("alice", "wonderland"), ("bob", "builder"), ("carol", "secret")):
         assert c.get("/3/Cloud", headers=hdr(u, p)).json()["cloud_healthy"]
+
+
+def test_flow_page_served():
+    h2o.init()
+    c = TestClient(create_app())
+    r = c.get("/", follow_redirects=True)
+    assert r.status_code == 200 and "h2o3_amd Flow" in r.text
+    for ep in ("/3/Cloud", "/3/Frames", "/3/Models", "/3/Jobs", "/3/ImportFiles", "/3/ParseSetup", "/3/Parse",
+               "/3/ModelBuilders/", "/3/Predictions/models/", "/99/Rapids"):
+        assert ep in r.text          # the page drives the same REST endpoints the clients use
