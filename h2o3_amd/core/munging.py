@@ -705,9 +705,8 @@ def impute(fr, column=-1, method="mean", combine_method="interpolate", by=None, 
             continue
         if values is not None:
             val = values[j] if isinstance(values, (list, tuple)) else values
-        elif by is not None:
-            grp = fr.group_by(by)
-            res.append(None)
+        elif by is not None and len(by if isinstance(by, (list, tuple)) else [by]):
+            res.append(_impute_by_group(fr, j, method, combine_method, by))
             continue
         elif v.type == T_ENUM or method == "mode":
             d = v.data if v.type == T_ENUM else v.as_float().to(torch.int64)
@@ -726,6 +725,74 @@ def impute(fr, column=-1, method="mean", combine_method="interpolate", by=None, 
             fr._vecs[j] = Vec(torch.where(torch.isnan(x), torch.full_like(x, float(val)), x), v.type)
         res.append(val)
     return res
+
+
+def _impute_by_group(fr, j, method, combine_method, by):
+    """AstImpute with group-by columns: each NA of column j takes its group's
+    mean / median / mode (hex.rapids AstImpute + AstGroup); groups whose
+    column is all NA stay NA.  Group ids come from the gathered key columns
+    (every rank the same), the fills of this rank's rows are sliced out.
+    -> frame of the group keys and their fill value."""
+    import pandas as pd
+    g = fr.gather() if cloud.is_distributed() else fr
+    by = list(by) if isinstance(by, (list, tuple)) else [by]
+    bycols = [g.names[b] if isinstance(b, (int, float)) else b for b in (int(b) if isinstance(b, float) else b
+                                                                          for b in by)]
+    uniq, gid = _group_ids(g, bycols)
+    G = int(uniq.shape[0])
+    v = g._vecs[j]
+    enum = v.type == T_ENUM
+    x = v.data.to(torch.float64) if enum else v.as_float(torch.float64)
+    ok = (x >= 0) if enum else ~torch.isnan(x)
+    gv, xv = gid[ok], x[ok]
+    if enum or method == "mode":
+        codes = xv.to(torch.int64)
+        L = int(codes.max()) + 1 if codes.numel() else 1
+        cnt = torch.bincount(gv * L + codes, minlength=G * L).view(G, L)
+        fill = torch.argmax(cnt, 1).to(torch.float64)
+        fill = torch.where(cnt.sum(1) > 0, fill, torch.full_like(fill, float("nan")))
+    elif method == "median":
+        order = torch.argsort(xv, stable=True)
+        order = order[torch.argsort(gv[order], stable=True)]
+        xs = xv[order]
+        n = torch.bincount(gv, minlength=G)
+        start = torch.cumsum(n, 0) - n
+        lo = (start + (n - 1).clamp_min(0) // 2).clamp_max(max(xs.numel() - 1, 0))
+        hi = (start + n // 2).clamp_max(max(xs.numel() - 1, 0))
+        cm = str(combine_method).lower()
+        if xs.numel() == 0:
+            fill = torch.full((G,), float("nan"), dtype=torch.float64, device=x.device)
+        else:
+            a, b = xs[lo], xs[hi]
+            fill = a if cm in ("lo", "low") else b if cm in ("hi", "high") else (a + b) / 2
+            fill = torch.where(n > 0, fill, torch.full_like(fill, float("nan")))
+    else:
+        s = torch.zeros(G, dtype=torch.float64, device=x.device).index_add_(0, gv, xv)
+        n = torch.bincount(gv, minlength=G).to(torch.float64)
+        fill = s / n
+    row_fill = fill[gid]
+    lv = fr._vecs[j]
+    if cloud.is_distributed():
+        off = fr.row_offset()
+        row_fill = row_fill[off:off + lv.data.shape[0]]
+    if lv.type == T_ENUM:
+        miss = (lv.data < 0) & ~torch.isnan(row_fill)
+        fr._vecs[j] = Vec(torch.where(miss, torch.nan_to_num(row_fill, nan=-1).to(lv.data.dtype), lv.data),
+                          T_ENUM, lv.domain)
+    else:
+        lx = lv.data
+        fr._vecs[j] = Vec(torch.where(torch.isnan(lx), row_fill.to(lx.dtype), lx), lv.type)
+    keys = {}
+    for k, c in enumerate(bycols):
+        kv = g.vec(c)
+        col = uniq[:, k].cpu().numpy()
+        if kv.type == T_ENUM:
+            keys[c] = [kv.domain[int(t)] if t >= 0 else None for t in col]
+        else:
+            keys[c] = [None if t == -1e300 else t for t in col]
+    fv = fill.cpu().numpy()
+    keys[g.names[j]] = [v.domain[int(t)] if t == t else None for t in fv] if enum else fv.tolist()
+    return H2OFrame(pd.DataFrame(keys), _local=not cloud.is_distributed())
 
 
 def _ffill(x, maxlen, dim):

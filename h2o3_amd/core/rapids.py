@@ -185,6 +185,8 @@ class Env:
         if v is None:
             if name in PRIMS:
                 return ("prim", name)
+            if name == "_":                            # the clients' "argument not given" placeholder
+                return None
             raise RapidsError(f"Name lookup of '{name}' failed")
         if _is_frame(v):
             # Env.addGlobals: a defensive copy of the global frame (same columns,
@@ -547,8 +549,9 @@ PRIMS["cut"] = lambda x, br, lab=None, lowest=0.0, right=1.0, dig=3.0: x.cut(br,
                                                                             bool(right), int(dig))
 def _impute(x, col, method="mean", comb="interpolate", gb=None, *a):
     """AstImpute: imputes the frame IN PLACE (the stored frame too) and
-    returns the fill values."""
-    out = x.impute(int(col), method, comb)
+    returns the fill values (the group-by frame of fills with gb columns)."""
+    by = [int(g) for g in gb] if isinstance(gb, (list, tuple)) and len(gb) else None
+    out = x.impute(int(col), method, comb, by=by)
     src = getattr(x, "_rapids_src", None)
     if src is not None and len(src._vecs) == len(x._vecs):
         for j, v in enumerate(x._vecs):
@@ -557,7 +560,7 @@ def _impute(x, col, method="mean", comb="interpolate", gb=None, *a):
     return out
 
 
-PRIMS["h2o.impute"] = lambda x, col, method="mean", comb="interpolate", gb=None, *a: _impute(x, col, method, comb)
+PRIMS["h2o.impute"] = lambda x, col, method="mean", comb="interpolate", gb=None, *a: _impute(x, col, method, comb, gb)
 PRIMS["h2o.fillna"] = lambda x, method="forward", axis=0.0, maxlen=1.0: x.fillna(method, int(axis), int(maxlen))
 PRIMS["pivot"] = lambda x, idx, col, val: x.pivot(idx, col, val)
 PRIMS["melt"] = lambda x, ids, vals=None, vn="variable", valn="value", skipna=0.0: x.melt(

@@ -667,6 +667,9 @@ class H2OGeneralizedLinearEstimator(H2OEstimator):
         fam = (p.get("family") or "AUTO").lower()
         if fam == "auto":
             fam = "binomial" if spec.nclasses == 2 else ("multinomial" if spec.nclasses > 2 else "gaussian")
+        if fam in ("gaussian", "poisson", "gamma", "tweedie", "negativebinomial") and spec.nclasses >= 2:
+            # GLM.init (hex/glm/GLM.java:847)
+            raise ValueError("ERRR on field: _response: Regression requires numeric response, got categorical.")
         if fam in ("multinomial", "ordinal"):
             from .glm_multi import fit_multinomial
             return fit_multinomial(self, spec, fam)

@@ -214,11 +214,16 @@ def regression_metrics(y, pred, w=None, distribution=None):
     ymean = _wsum(w * y) / sw if sw > 0 else float("nan")
     var = _wsum(w * (y - ymean) ** 2) / sw if sw > 0 else float("nan")
     r2 = 1 - mse / var if var and var > 0 else float("nan")
-    if bool((y > -1).all()) and bool((pred > -1).all()):
+    # the rmsle domain check is agreed over ranks (a rank-local test would
+    # leave the ranks issuing different collectives)
+    bad = _wsum(((y <= -1) | (pred <= -1)).to(torch.float64))
+    if bad == 0 and sw > 0:
         rmsle = math.sqrt(_wsum(w * (torch.log1p(pred) - torch.log1p(y)) ** 2) / sw)
     else:
         rmsle = float("nan")
-    if distribution is not None and distribution.family not in ("gaussian",):
+    if sw <= 0:
+        dev = float("nan")
+    elif distribution is not None and distribution.family not in ("gaussian",):
         dev = _wsum(distribution.deviance(w, y, pred)) / sw
     else:
         dev = mse

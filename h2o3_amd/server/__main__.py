@@ -16,11 +16,13 @@ def main():
     ap.add_argument("--login-conf", default=None, help="realm file: 'user: password[,role]' (plain, MD5:, OBF:)")
     ap.add_argument("--ssl-certfile", default=None, help="PEM certificate: serve HTTPS")
     ap.add_argument("--ssl-keyfile", default=None, help="PEM private key for --ssl-certfile")
+    ap.add_argument("--flow-dir", default=None, help="NodePersistentStorage directory for saved Flow notebooks "
+                                                     "(default $H2O3_FLOW_DIR or ~/h2oflows)")
     a = ap.parse_args()
     if a.hash_login and not a.login_conf:
         ap.error("--hash-login needs --login-conf")
     start(ip=a.ip, port=a.port, log_level=a.log_level, login_conf=a.login_conf if a.hash_login else None,
-          ssl_certfile=a.ssl_certfile, ssl_keyfile=a.ssl_keyfile)
+          ssl_certfile=a.ssl_certfile, ssl_keyfile=a.ssl_keyfile, flow_dir=a.flow_dir)
 
 
 if __name__ == "__main__":

@@ -85,6 +85,44 @@ def _algo_cls(algo):
     return cls
 
 
+_NUMERIC_STR = None
+
+
+def _coerce_params(cls, p):
+    """Model parameters arriving as strings in JSON bodies (Flow sends
+    "ntrees": "100", "learn_rate": "0.01") are parsed into the parameter's
+    type, as the reference's schema layer does (water/api/Schema.java
+    parse): by the type of the builder's default, numbers for numeric text
+    when the default is None (keys, columns and frames are left alone)."""
+    import re
+    global _NUMERIC_STR
+    if _NUMERIC_STR is None:
+        _NUMERIC_STR = re.compile(r"[-+]?(\d+\.?\d*|\.\d+)([eE][-+]?\d+)?")
+    try:
+        defaults = cls()._parms
+    except Exception:  # noqa: BLE001 - no coercion when the defaults are unavailable
+        return p
+    out = {}
+    for k, v in p.items():
+        d = defaults.get(k)
+        if isinstance(v, str) and not isinstance(d, str) and k not in _FRAME_PARAMS | _MODEL_PARAMS and \
+                not k.endswith(("_id", "_column", "_columns", "_frame")):
+            t = v.strip()
+            if isinstance(d, bool):
+                v = t.lower() in ("true", "1")
+            elif _NUMERIC_STR.fullmatch(t):
+                f = float(t)
+                v = float(t) if isinstance(d, float) else (int(f) if f.is_integer() and "." not in t
+                                                          and "e" not in t.lower() else f)
+            elif isinstance(d, (list, dict)) and t[:1] in "[{":
+                try:
+                    v = _json.loads(t)
+                except ValueError:
+                    pass
+        out[k] = v
+    return out
+
+
 def _multipart(body: bytes, ctype: str) -> list[tuple[str, str | None, bytes]]:
     """multipart/form-data body -> [(field name, filename or None, bytes)]
     (stdlib email parser; python-multipart is not available here)."""
@@ -171,7 +209,7 @@ class _Uploads:
         return out
 
 
-def create_app() -> FastAPI:
+def create_app(flow_dir: str | None = None) -> FastAPI:
     app = FastAPI(title="h2o3_amd REST API", version="3")
     uploads = _Uploads()
     sessions: dict[str, float] = {}
@@ -182,9 +220,25 @@ def create_app() -> FastAPI:
         return JSONResponse(S.error_v3(e.msg, e.status, e.exc, builder=e.builder, url=str(request.url.path)),
                             status_code=e.status)
 
+    import re as _re
+    from urllib.parse import unquote as _unquote
+    app.state.flow_routes = []      # (method, path regex, handler, jsonify): flow.LocalTransport
+
+    def _jsonify(out):
+        if isinstance(out, Response):
+            return out.body.decode("utf-8", "replace")
+        return S.jsonable(out)
+
     def route(method, path):
         """Register an async handler taking (params, request, **path)."""
+        rx = _re.compile(_re.sub(r"\{(\w+)\}", r"(?P<\1>[^/]+)", _re.escape(path).replace(r"\{", "{")
+                                 .replace(r"\}", "}")))
+
+        def local(fn):
+            return lambda p, r, **kw: fn(p, r, **{k: _unquote(v) for k, v in kw.items()})
+
         def deco(fn):
+            app.state.flow_routes.append((method, rx, local(fn), _jsonify))
             async def h(request: Request):
                 p = await _params(request)
                 # handlers run on the event-loop thread: requests are served one at a time
@@ -219,7 +273,7 @@ def create_app() -> FastAPI:
 
     @app.get("/flow/index.html", include_in_schema=False)
     async def flow():
-        """Minimal Flow (h2o-web): one static page over the /3 endpoints."""
+        """Flow notebook (h2o-web): cells run through POST /flow/cell (flow.py)."""
         return HTMLResponse(_flow_page())
 
     # ------------------------------------------------------------ cloud
@@ -534,7 +588,7 @@ def create_app() -> FastAPI:
 
     def _build(algo, p):
         cls = _algo_cls(algo)
-        p = _resolve_params(p)
+        p = _resolve_params(_coerce_params(cls, p))
         tf = p.get("training_frame")
         if not isinstance(tf, H2OFrame) and algo != "stackedensemble":
             raise _HTTPError(400, "ERRR on field: _train: Missing training frame", builder=True)
@@ -923,7 +977,7 @@ def create_app() -> FastAPI:
         """GridSearchHandler: hyper_parameters + search_criteria over one algo."""
         from ..grid import H2OGridSearch
         cls = _algo_cls(algo)
-        p = _resolve_params(p)
+        p = _resolve_params(_coerce_params(cls, p))
         hyper = p.pop("hyper_parameters", {}) or {}
         if isinstance(hyper, str):
             hyper = _json.loads(hyper)
@@ -1056,24 +1110,121 @@ def create_app() -> FastAPI:
                 "modeling_steps": [{"name": a, "steps": []} for a in
                                    sorted({str(m).split("_")[0] for m in lbj["table"]["data"][1]})]}
 
+    # ---------------------------------------------- Flow notebooks / NPS
+    from .flow import ROUTINES, FlowError, FlowRunner, FlowSyntaxError, LocalTransport
+    flow_runner = FlowRunner(LocalTransport(app))
+
+    @app.post("/flow/cell", include_in_schema=False)
+    async def flow_cell(request: Request):
+        """Run one notebook cell server-side (flow.py); variables persist
+        across cells like Flow's notebook sandbox."""
+        body = await request.json()
+        try:
+            res = flow_runner.run_cell(body.get("input", ""), body.get("type", "cs"))
+        except (FlowError, FlowSyntaxError) as e:
+            return JSONResponse({"ok": False, "error": str(e)}, status_code=400)
+        return JSONResponse({"ok": True, "result": S.jsonable(res)})
+
+    @app.get("/flow/routines", include_in_schema=False)
+    async def flow_routines():
+        return JSONResponse({"routines": sorted(ROUTINES)})
+
+    nps_dir = flow_dir if flow_dir is not None else os.environ.get(
+        "H2O3_FLOW_DIR", os.path.join(os.path.expanduser("~"), "h2oflows"))
+    _nps_cat = _re.compile(r"[-a-zA-Z0-9]+")
+    _nps_name = _re.compile(r"[-a-zA-Z0-9_ ()]+")
+
+    def _nps_path(category, name=None):
+        """water/init/NodePersistentStorage.java: validated category / key
+        names, one file per entry under <flow_dir>/<category>/."""
+        if not nps_dir:
+            raise _HTTPError(400, "NodePersistentStorage directory not specified (try setting -flow_dir)")
+        if not category or not _nps_cat.fullmatch(category):
+            raise _HTTPError(400, f"NodePersistentStorage illegal category ({category})")
+        if name is None:
+            return os.path.join(nps_dir, category)
+        if not _nps_name.fullmatch(name):
+            raise _HTTPError(400, f"NodePersistentStorage illegal name ({name})")
+        return os.path.join(nps_dir, category, name)
+
+    def _nps(**kw):
+        return {"__meta": S.meta("NodePersistentStorageV3", "Iced"), "category": None, "name": None,
+                "value": None, "configured": bool(nps_dir), "exists": False, **kw}
+
+    @route("GET", "/3/NodePersistentStorage/configured")
+    def nps_configured(p, r):
+        return _nps()
+
+    @route("GET", "/3/NodePersistentStorage/categories/{category}/names/{name}/exists")
+    def nps_exists_name(p, r, category, name):
+        return _nps(category=category, name=name, exists=os.path.exists(_nps_path(category, name)))
+
+    @route("GET", "/3/NodePersistentStorage/categories/{category}/exists")
+    def nps_exists(p, r, category):
+        return _nps(category=category, exists=os.path.isdir(_nps_path(category)))
+
+    def _nps_put(category, name, value):
+        path = _nps_path(category, name)
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        tmp = os.path.join(nps_dir, "_tmp")
+        os.makedirs(tmp, exist_ok=True)
+        fd, tpath = tempfile.mkstemp(dir=tmp)
+        with os.fdopen(fd, "w", encoding="utf-8") as f:
+            f.write(value if isinstance(value, str) else _json.dumps(value))
+        os.replace(tpath, path)                     # write to _tmp, then rename (reference put)
+        return _nps(category=category, name=name)
+
+    @route("POST", "/3/NodePersistentStorage/{category}/{name}")
+    def nps_put_name(p, r, category, name):
+        return _nps_put(category, name, p.get("value", ""))
+
+    @route("POST", "/3/NodePersistentStorage/{category}")
+    def nps_put(p, r, category):
+        return _nps_put(category, str(uuid.uuid4()), p.get("value", ""))
+
+    @route("GET", "/3/NodePersistentStorage/{category}/{name}")
+    def nps_get(p, r, category, name):
+        path = _nps_path(category, name)
+        if not os.path.exists(path):
+            raise _HTTPError(404, f"NodePersistentStorage: {category}/{name} not found")
+        with open(path, encoding="utf-8") as f:
+            return _nps(category=category, name=name, value=f.read())
+
+    @route("GET", "/3/NodePersistentStorage/{category}")
+    def nps_list(p, r, category):
+        d = _nps_path(category)
+        names = sorted(os.listdir(d)) if os.path.isdir(d) else []
+        entries = [{"__meta": S.meta("NodePersistentStorageEntryV3", "Iced"), "category": category, "name": n,
+                    "size": os.path.getsize(os.path.join(d, n)),
+                    "timestamp_millis": int(os.path.getmtime(os.path.join(d, n)) * 1000)} for n in names]
+        return {**_nps(category=category), "entries": entries}
+
+    @route("DELETE", "/3/NodePersistentStorage/{category}/{name}")
+    def nps_delete(p, r, category, name):
+        path = _nps_path(category, name)
+        if os.path.exists(path):
+            os.remove(path)
+        return _nps(category=category, name=name)
+
     return app
 
 
-def create_server_app(login_conf=None, realm="h2o"):
+def create_server_app(login_conf=None, realm="h2o", flow_dir=None):
     """The REST app, behind HTTP Basic authentication when a HashLoginService
     realm file is given (auth.py)."""
-    app = create_app()
+    app = create_app(flow_dir)
     if login_conf:
         from .auth import basic_auth_middleware, load_realm
         return basic_auth_middleware(app, load_realm(login_conf), realm)
     return app
 
 
-def start(ip="127.0.0.1", port=54321, log_level="warning", login_conf=None, ssl_certfile=None, ssl_keyfile=None):
+def start(ip="127.0.0.1", port=54321, log_level="warning", login_conf=None, ssl_certfile=None, ssl_keyfile=None,
+          flow_dir=None):
     """Serve the REST API (blocking) on rank 0 of a single-process cloud;
     login_conf enables Basic auth (the reference's -hash_login), the PEM
     pair enables HTTPS."""
     import uvicorn
     api.init()
-    uvicorn.run(create_server_app(login_conf), host=ip, port=port, log_level=log_level,
+    uvicorn.run(create_server_app(login_conf, flow_dir=flow_dir), host=ip, port=port, log_level=log_level,
                 ssl_certfile=ssl_certfile, ssl_keyfile=ssl_keyfile)
