@@ -86,9 +86,17 @@ def import_file(path, destination_frame=None, header=0, sep=None, col_names=None
     if ext == ".arff":
         return _import_arff(fs[0], destination_frame)
     if ext in (".xls", ".xlsx"):
-        import pandas as pd
-        df = pd.read_excel(fs[0])
-        return H2OFrame(df, destination_frame=destination_frame, column_types=col_types)
+        # first worksheet decoded in-house (core/excel.py, XlsParser.java), then the CSV path's guessing
+        from .excel import read_excel_rows, rows_to_csv
+        from .persist import _tmpfile
+        tmp = _tmpfile(".csv")
+        with open(tmp, "w", encoding="utf-8") as f:
+            f.write(rows_to_csv(read_excel_rows(fs[0])))
+        try:
+            return _import_csv([tmp], destination_frame, header, ",", col_names, col_types, na_strings,
+                               skipped_columns, '"')
+        finally:
+            os.remove(tmp)
     return _import_csv(fs, destination_frame, header, sep, col_names, col_types, na_strings, skipped_columns,
                        quotechar)
 

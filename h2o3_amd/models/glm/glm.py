@@ -291,6 +291,12 @@ class GLMDriver:
         else:
             yy = y.to(torch.float64)
             ok &= ~torch.isnan(yy)
+            if fam == "binomial":
+                # GLM.init (hex/glm/GLM.java:866): a numeric response must be 0/1
+                nonbin = coll.allreduce_scalar(float((ok & (yy != 0) & (yy != 1)).sum()))
+                if nonbin > 0:
+                    raise ValueError("ERRR on field: _family: Binomial requires the response to be a 2-class "
+                                     "categorical or a binary column (0/1)")
         w = spec.w_tensor()
         w = torch.ones_like(yy) if w is None else w.to(torch.float64)
         self.w = torch.where(ok, w, torch.zeros_like(w))
@@ -302,6 +308,9 @@ class GLMDriver:
         self.intercept = bool(p.get("intercept", True))
         self.wsum = coll.allreduce_scalar(float(self.w.sum()))
         self.nobs = coll.allreduce_scalar(float((self.w > 0).sum()))
+        if self.wsum <= 0:
+            raise ValueError("ERRR on field: _train: Training data has no rows with a valid response and "
+                             "positive weight")
         self.ymu = coll.allreduce_scalar(float((self.w * self.y).sum())) / self.wsum
         alpha = p.get("alpha")
         solver = (p.get("solver") or "AUTO").upper()
@@ -670,6 +679,9 @@ class H2OGeneralizedLinearEstimator(H2OEstimator):
         if fam in ("gaussian", "poisson", "gamma", "tweedie", "negativebinomial") and spec.nclasses >= 2:
             # GLM.init (hex/glm/GLM.java:847)
             raise ValueError("ERRR on field: _response: Regression requires numeric response, got categorical.")
+        if fam == "multinomial" and spec.nclasses <= 2:
+            raise ValueError("ERRR on field: _family: Multinomial requires a categorical response with at least 3 "
+                             "levels (for 2 class problem use family=binomial.")
         if fam in ("multinomial", "ordinal"):
             from .glm_multi import fit_multinomial
             return fit_multinomial(self, spec, fam)

@@ -604,10 +604,19 @@ def _inspect(r, args):
             for v in x:
                 walk(v, path)
     walk(data)
+    if isinstance(obj, dict) and obj.get("kind") == "prediction" and isinstance(data, dict):
+        mm = (data.get("model_metrics") or [{}])[0]
+        scal = {k: v for k, v in mm.items() if isinstance(v, (int, float, str)) and not k.startswith("__")}
+        tables["Prediction"] = {"__meta": {"schema_type": "TwoDimTable"}, "name": "Prediction",
+                                "columns": [{"name": "metric"}, {"name": "value"}],
+                                "data": [list(scal), [scal[k] for k in scal]]}
     if name is None:
         return _result("tables", tables, of=obj.get("kind") if isinstance(obj, dict) else None)
     low = {k.lower(): k for k in tables}
-    key = low.get(str(name).lower()) or next((k for k in tables if str(name).lower() in k.lower()), None)
+    # Flow names inspections "output - Coefficients", "output - training_metrics - Gains/Lift Table"
+    cands = [str(name).lower(), str(name).split(" - ")[-1].lower()]
+    key = next((low[c] for c in cands if c in low), None) or \
+        next((k for c in cands for k in tables if c in k.lower()), None)
     if key is None:
         if str(name).lower() in ("summary", "parameters") and isinstance(data, dict):
             return _result("table", data.get("summary_table") if name == "summary" else data.get("parameters"),

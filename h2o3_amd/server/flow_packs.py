@@ -6,7 +6,7 @@ h2o-docs/src/product/flow/packs/{test-small,test-medium,test-large,examples}
 reference tree, but every ``parseFiles`` cell declares the file's layout:
 column names, column types, separator, header and parse type.  This module
 writes a synthetic file of exactly that layout for every parsed path
-(CSV / ARFF / SVMLight, gz / zip compressed by extension), shaped so the
+(CSV / ARFF / SVMLight / XLS, gz / zip compressed by extension), shaped so the
 models the notebook builds on it are valid (a response used with a
 binomial family or bernoulli distribution is 0/1, poisson / tweedie counts
 are non-negative, gamma responses positive, weights positive), then runs
@@ -178,8 +178,6 @@ def synthesize(nb, root, rows=200, seed=0) -> list[str]:
     specs, kinds = scan(nb)
     out = []
     for k, spec in enumerate(specs):
-        if str(spec.get("parse_type", "CSV")).upper() == "XLS":
-            raise NotImplementedError("XLS data is not synthesized")
         names, types, cols = synth_table(spec, kinds, rows, seed + k)
         for p in spec.get("paths") or spec.get("source_frames"):
             path = _local(root, p)
@@ -188,6 +186,12 @@ def synthesize(nb, root, rows=200, seed=0) -> list[str]:
             if os.path.exists(path):
                 continue
             os.makedirs(os.path.dirname(path), exist_ok=True)
+            if str(spec.get("parse_type", "CSV")).upper() == "XLS":
+                from ..core.excel import write_xls, write_xlsx
+                table = [names] + [list(r) for r in zip(*cols)]
+                (write_xlsx if path.endswith(".xlsx") else write_xls)(path, table)
+                out.append(path)
+                continue
             with open(path, "wb") as f:
                 f.write(_encode(spec, names, types, cols, path))
             out.append(path)
@@ -201,15 +205,16 @@ def run_pack(notebooks, root, transport, rows=200, automl_secs=20, clear=None, l
         if clear is not None:
             clear()
         t0 = time.time()
+        nb_root = os.path.join(root, os.path.splitext(os.path.basename(nb))[0])   # own data per notebook
         try:
-            synthesize(nb, root, rows)
+            synthesize(nb, nb_root, rows)
         except NotImplementedError as e:
             rec = {"notebook": os.path.relpath(nb, PACKS) if nb.startswith(PACKS) else nb, "skipped": str(e)}
             results.append(rec)
             if log:
                 log(rec)
             continue
-        runner = FlowRunner(transport, path_map=lambda p: _local(root, p), automl_max_runtime_secs=automl_secs)
+        runner = FlowRunner(transport, path_map=lambda p, r=nb_root: _local(r, p), automl_max_runtime_secs=automl_secs)
         res = runner.run_notebook(nb, stop_on_error=False)
         cs = [(i, r) for i, t, r in res if t == "cs"]
         errs = [(i, str(r)) for i, r in cs if isinstance(r, Exception)]
@@ -230,6 +235,7 @@ def main(argv=None):
     ap.add_argument("--limit", type=int, default=0)
     ap.add_argument("--match", default="")
     ap.add_argument("--out", default=None, help="JSON lines of per-notebook results")
+    ap.add_argument("--verbose", action="store_true", help="print each notebook before it runs")
     a = ap.parse_args(argv)
     import importlib
     api = importlib.import_module("h2o3_amd.api")
@@ -238,7 +244,7 @@ def main(argv=None):
     api.init()
     app = create_app(flow_dir=tempfile.mkdtemp(prefix="nps_"))
     t = LocalTransport(app)
-    nbs = sorted(glob.glob(os.path.join(PACKS, a.pack, "*.flow")))
+    nbs = [n for pack in a.pack.split(",") for n in sorted(glob.glob(os.path.join(PACKS, pack, "*.flow")))]
     nbs = [n for n in nbs if a.match in n][: a.limit or None]
     root = tempfile.mkdtemp(prefix="flowdata_")
     fh = open(a.out, "w") if a.out else None
@@ -253,7 +259,13 @@ def main(argv=None):
         if fh:
             fh.write(json.dumps(rec) + "\n")
             fh.flush()
-    res = run_pack(nbs, root, t, a.rows, clear=lambda: t("DELETE", "/3/DKV"), log=log)
+    def clear():
+        t("DELETE", "/3/DKV")
+    res = []
+    for nb in nbs:
+        if a.verbose:
+            print(f"start {os.path.relpath(nb, PACKS)}", flush=True)
+        res += run_pack([nb], root, t, a.rows, clear=clear, log=log)
     ran = [r for r in res if "skipped" not in r]
     full = sum(r["failed"] == 0 for r in ran)
     cells = sum(r["cells"] for r in ran)

@@ -108,6 +108,8 @@ def _coerce_params(cls, p):
         if isinstance(v, str) and not isinstance(d, str) and k not in _FRAME_PARAMS | _MODEL_PARAMS and \
                 not k.endswith(("_id", "_column", "_columns", "_frame")):
             t = v.strip()
+            if len(t) > 1 and t[-1] in "fFdDlL" and _NUMERIC_STR.fullmatch(t[:-1]):
+                t = t[:-1]                             # Java literals: Float.parseFloat("1.0f")
             if isinstance(d, bool):
                 v = t.lower() in ("true", "1")
             elif _NUMERIC_STR.fullmatch(t):
@@ -440,7 +442,7 @@ def create_app(flow_dir: str | None = None) -> FastAPI:
         if not srcs:
             raise _HTTPError(400, "source_frames required")
         sep = p.get("separator")
-        sep = chr(sep) if isinstance(sep, int) else sep
+        sep = (chr(sep) if 0 < sep < 128 else None) if isinstance(sep, int) else sep   # -1: guess
         hdr = _header(p.get("check_header", 0))
         fr, s = _guess(srcs, hdr, sep)
         base = os.path.splitext(os.path.basename(uploads.resolve(srcs)[0]))[0]
@@ -465,7 +467,7 @@ def create_app(flow_dir: str | None = None) -> FastAPI:
         if not srcs:
             raise _HTTPError(400, "source_frames required")
         sep = p.get("separator")
-        sep = chr(sep) if isinstance(sep, int) else sep
+        sep = (chr(sep) if 0 < sep < 128 else None) if isinstance(sep, int) else sep   # -1: guess
         hdr = _header(p.get("check_header", 0))
         dest = p.get("destination_frame") or (os.path.basename(srcs[0]) + ".hex")
         names = p.get("column_names")

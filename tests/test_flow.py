@@ -94,6 +94,20 @@ def _write_csv(path, n=150, seed=0):
 
 
 def test_notebook_end_to_end_local(app, tmp_path):
+    _demo_notebook(app, tmp_path)
+
+
+@pytest.mark.gpu
+def test_notebook_end_to_end_gpu(app, tmp_path):
+    """The same notebook with the cloud on the GPU: every routine's model
+    build / predict / munging runs through the device paths."""
+    import torch
+    from h2o3_amd.parallel import cloud
+    assert torch.cuda.is_available() and cloud.device().type == "cuda"
+    _demo_notebook(app, tmp_path)
+
+
+def _demo_notebook(app, tmp_path):
     csv = tmp_path / "d.csv"
     _write_csv(csv)
     nb = {"version": "1.0.0", "cells": [
