@@ -315,32 +315,70 @@ __global__ __launch_bounds__(256) void cat_pair_kernel(const double* __restrict_
   __shared__ int si[BP];      // bin index (sort payload)
   __shared__ double red_g[4];
   __shared__ int red_k[4];
+  __shared__ int nfin[256];   // per-thread count of occupied levels, then its exclusive scan
+  constexpr int PER = BP / 256;
   const int p = blockIdx.x;
   const int tid = threadIdx.x;
   const int B = Bs - 1;
   const double* h = H + ((size_t)pf[p] * n + pn[p]) * (size_t)Bs * C;
   const bool cat = pcat[p] != 0;
-  for (int b = tid; b < BP; b += 256) {
-    double key = INFINITY;
-    if (b < B) {
-      if (!cat) {
-        key = (double)b;
-      } else if (CRIT == 1) {
-        const double g = h[(size_t)b * C], hh = h[(size_t)b * C + 1];
-        key = hh > 0 ? g / hh : INFINITY;
-      } else {
-        const double w = h[(size_t)b * C], wy = h[(size_t)b * C + 1];
-        key = w > 0 ? wy / w : INFINITY;
-      }
+  int M = BP;                 // sorted prefix length
+  if (!cat) {
+    for (int b = tid; b < BP; b += 256) {
+      sk[b] = b < B ? (double)b : INFINITY;
+      si[b] = b;
     }
-    sk[b] = key;
-    si[b] = b;
+  } else {
+    // Occupied levels (finite key) first, in bin order, then the empty ones
+    // in bin order: the empty levels' INF keys already sit in their final
+    // (bin-index) order, so only the occupied prefix -- a few dozen levels
+    // of a 1000-level column in a deep node -- goes through the bitonic
+    // network.  Same order, hence the same k, as sorting all BP keys.
+    double key[PER];
+    int cnt = 0;
+#pragma unroll
+    for (int e = 0; e < PER; ++e) {
+      const int b = tid * PER + e;
+      double kk = INFINITY;
+      if (b < B) {
+        if (CRIT == 1) {
+          const double g = h[(size_t)b * C], hh = h[(size_t)b * C + 1];
+          kk = hh > 0 ? g / hh : INFINITY;
+        } else {
+          const double w = h[(size_t)b * C], wy = h[(size_t)b * C + 1];
+          kk = w > 0 ? wy / w : INFINITY;
+        }
+      }
+      key[e] = kk;
+      cnt += kk < INFINITY ? 1 : 0;
+    }
+    nfin[tid] = cnt;
+    __syncthreads();
+    for (int d = 1; d < 256; d <<= 1) {            // inclusive Hillis-Steele scan
+      const int u = tid >= d ? nfin[tid - d] : 0;
+      __syncthreads();
+      nfin[tid] += u;
+      __syncthreads();
+    }
+    const int m = nfin[255];
+    int before = nfin[tid] - cnt;                  // occupied levels ahead of this thread's run
+#pragma unroll
+    for (int e = 0; e < PER; ++e) {
+      const int b = tid * PER + e;
+      const bool occ = key[e] < INFINITY;
+      const int pos = occ ? before : m + b - before;
+      sk[pos] = key[e];
+      si[pos] = b;
+      before += occ ? 1 : 0;
+    }
+    M = 2;
+    while (M < m) M <<= 1;
   }
   __syncthreads();
   if (cat) {
-    for (int k = 2; k <= BP; k <<= 1) {
+    for (int k = 2; k <= M; k <<= 1) {
       for (int j = k >> 1; j > 0; j >>= 1) {
-        for (int i = tid; i < BP; i += 256) {
+        for (int i = tid; i < M; i += 256) {
           const int l = i ^ j;
           if (l > i) {
             const double a = sk[i], c = sk[l];
@@ -355,7 +393,6 @@ __global__ __launch_bounds__(256) void cat_pair_kernel(const double* __restrict_
     }
   }
   // gather the sorted channels; per-thread serial prefix over a contiguous run
-  constexpr int PER = BP / 256;
   double c0[PER], c1[PER];
   double a0 = 0, a1 = 0;
 #pragma unroll

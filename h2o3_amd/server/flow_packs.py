@@ -226,6 +226,30 @@ def run_pack(notebooks, root, transport, rows=200, automl_secs=20, clear=None, l
     return results
 
 
+def write_report(res, path, pack, rows):
+    """Per-notebook table; failures split into validation errors the
+    reference's builders raise as well (``ERRR on field``: the notebook's
+    declared column types contradict the requested family) and the rest."""
+    ran = [r for r in res if "skipped" not in r]
+    full = sum(r["failed"] == 0 for r in ran)
+    lines = [f"Flow pack(s) {pack}: {len(ran)} notebooks run on synthetic data ({rows} rows per parsed file, "
+             f"layout from each parseFiles cell), in-process server on the CPU",
+             f"{full}/{len(ran)} notebooks with every cell ok; {sum(r['ok'] for r in ran)}/"
+             f"{sum(r['cells'] for r in ran)} cs cells ok; {len(res) - len(ran)} skipped", ""]
+    ref_err = [r for r in ran if r["failed"] and all("ERRR on field" in e for _, e in r["errors"])]
+    other = [r for r in ran if r["failed"] and r not in ref_err]
+    lines.append(f"failing cells that are builder validation errors the reference raises too "
+                 f"({len(ref_err)} notebooks):")
+    lines += [f"  {r['notebook']}: cell {r['errors'][0][0]}: {r['errors'][0][1][:150]}" for r in ref_err]
+    lines.append(f"other failures ({len(other)} notebooks):")
+    lines += [f"  {r['notebook']}: cell {r['errors'][0][0]}: {r['errors'][0][1][:150]}" for r in other]
+    lines += ["", "per notebook: ok/cells seconds"]
+    lines += [f"  {r['notebook']}: {r['ok']}/{r['cells']} {r['secs']}" if "skipped" not in r else
+              f"  {r['notebook']}: skipped ({r['skipped']})" for r in res]
+    with open(path, "w") as f:
+        f.write("\n".join(lines) + "\n")
+
+
 def main(argv=None):
     import argparse
     import tempfile
@@ -236,6 +260,7 @@ def main(argv=None):
     ap.add_argument("--match", default="")
     ap.add_argument("--out", default=None, help="JSON lines of per-notebook results")
     ap.add_argument("--verbose", action="store_true", help="print each notebook before it runs")
+    ap.add_argument("--report", default=None, help="text summary (profiles/flow_packs_*.txt)")
     a = ap.parse_args(argv)
     import importlib
     api = importlib.import_module("h2o3_amd.api")
@@ -266,6 +291,8 @@ def main(argv=None):
         if a.verbose:
             print(f"start {os.path.relpath(nb, PACKS)}", flush=True)
         res += run_pack([nb], root, t, a.rows, clear=clear, log=log)
+    if a.report:
+        write_report(res, a.report, a.pack, a.rows)
     ran = [r for r in res if "skipped" not in r]
     full = sum(r["failed"] == 0 for r in ran)
     cells = sum(r["cells"] for r in ran)
