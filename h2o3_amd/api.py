@@ -565,3 +565,19 @@ def timeline():
     """Cloud-wide event timeline (water/TimeLine.java)."""
     from .utils.log import timeline as _tl
     return _tl()
+
+
+# ---- h2o.scoring / h2o.persist (reference h2o-py h2o/scoring.py, h2o/persist/persist.py)
+def make_leaderboard(object, leaderboard_frame=None, sort_metric="AUTO", extra_columns=[], scoring_data="AUTO"):
+    from .automl.leaderboard import make_leaderboard as _mk
+    return _mk(object, leaderboard_frame, sort_metric, extra_columns, scoring_data)
+
+
+def set_s3_credentials(secret_key_id, secret_access_key, session_token=None):
+    from .core.persist import set_s3_credentials as _set
+    _set(secret_key_id, secret_access_key, session_token)
+
+
+def remove_s3_credentials():
+    from .core.persist import remove_s3_credentials as _rm
+    _rm()

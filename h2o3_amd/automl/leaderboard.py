@@ -68,3 +68,30 @@ class Leaderboard:
                 r["algo"] = m.algo
             rows.append(r)
         return H2OFrame(pd.DataFrame(rows), _local=True, column_types={"model_id": "string"})
+
+
+def make_leaderboard(object, leaderboard_frame=None, sort_metric="AUTO", extra_columns=(), scoring_data="AUTO"):
+    """Leaderboard frame over models, grids and AutoML runs (reference h2o-py
+    h2o/scoring.py make_leaderboard -> hex/leaderboard/Leaderboard.java):
+    scored on leaderboard_frame when given, else on the xval / valid / train
+    metrics (scoring_data narrows that choice)."""
+    def models_of(o):
+        if isinstance(o, (list, tuple)):
+            return [m for x in o for m in models_of(x)]
+        if hasattr(o, "models") and not hasattr(o, "model_id"):
+            return list(o.models)
+        if isinstance(o, str):
+            from ..core import dkv
+            return models_of(dkv.get(o))
+        return [o]
+    models = models_of(object)
+    sd = str(scoring_data).lower()
+    if leaderboard_frame is None and sd in ("train", "valid", "xval"):
+        attr = {"train": "_training_metrics", "valid": "_validation_metrics", "xval": "_cross_validation_metrics"}[sd]
+        lb = Leaderboard(models, sort_metric)
+        lb._cache = {m.model_id: getattr(m, attr) for m in models}
+        lb.models = sorted(models, key=lambda m: lb._score(m, lb.sort_metric),
+                           reverse=lb.sort_metric in ("auc", "aucpr"))
+    else:
+        lb = Leaderboard(models, sort_metric, leaderboard_frame)
+    return lb.as_frame(list(extra_columns) if extra_columns else None)

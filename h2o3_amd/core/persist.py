@@ -101,9 +101,28 @@ def sigv4_headers(method: str, url: str, region: str, access_key: str, secret_ke
     return h
 
 
+_S3_CREDS: dict = {}
+
+
+def set_s3_credentials(secret_key_id, secret_access_key, session_token=None):
+    """Session S3 credentials, used before the AWS_* environment (reference
+    h2o-py h2o/persist/persist.py -> POST /3/PersistS3)."""
+    if not secret_key_id:
+        raise ValueError("Secret key ID must be specified")
+    if not secret_access_key:
+        raise ValueError("Secret access key must be specified")
+    _S3_CREDS.update(key=secret_key_id, secret=secret_access_key, token=session_token)
+
+
+def remove_s3_credentials():
+    _S3_CREDS.clear()
+
+
 def _s3_cfg():
     region = os.environ.get("AWS_REGION") or os.environ.get("AWS_DEFAULT_REGION") or "us-east-1"
     ep = os.environ.get("AWS_ENDPOINT_URL") or os.environ.get("AWS_S3_ENDPOINT")
+    if _S3_CREDS:
+        return region, ep, _S3_CREDS["key"], _S3_CREDS["secret"], _S3_CREDS.get("token")
     return region, ep, os.environ.get("AWS_ACCESS_KEY_ID"), os.environ.get("AWS_SECRET_ACCESS_KEY"), \
         os.environ.get("AWS_SESSION_TOKEN")
 

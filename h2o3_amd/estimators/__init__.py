@@ -7,7 +7,15 @@ from ..models.tree.isofor import H2OIsolationForestEstimator, H2OExtendedIsolati
 from ..models.clustering import (H2OKMeansEstimator, H2ONaiveBayesEstimator,  # noqa: F401
                                  H2OPrincipalComponentAnalysisEstimator, H2OSingularValueDecompositionEstimator)
 from ..models.deeplearning import H2ODeepLearningEstimator  # noqa: F401
-H2OAutoEncoderEstimator = H2ODeepLearningEstimator
+
+
+class H2OAutoEncoderEstimator(H2ODeepLearningEstimator):
+    """Deep Learning with autoencoder=True by default (h2o-py
+    estimators/deeplearning.py H2OAutoEncoderEstimator)."""
+
+    def __init__(self, **kw):
+        kw.setdefault("autoencoder", True)
+        super().__init__(**kw)
 from ..models.ensemble import H2OStackedEnsembleEstimator  # noqa: F401
 from ..models.generic import H2OGenericEstimator  # noqa: F401
 from ..models.isotonic import H2OIsotonicRegressionEstimator  # noqa: F401

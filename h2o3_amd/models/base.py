@@ -88,6 +88,11 @@ class TrainSpec:
         return None
 
 
+def scoring_names(domain):
+    from ..mojo.genmodel import scoring_names as _names     # hex/Model.java makeScoringNames
+    return _names(domain)
+
+
 class ScoreSchedule:
     """When an iterative tree builder scores (SharedTree.java:792
     doScoringAndSaveModel): every score_tree_interval trees when set, always
@@ -490,19 +495,20 @@ class H2OEstimator:
             thr = threshold
             if thr is None:
                 tm = self._training_metrics
-                thr = tm["max_f1_threshold"] if tm is not None and tm.get("max_f1_threshold") is not None else 0.5
+                thr = tm["max_f1_threshold"] if tm is not None and tm.get("max_f1_threshold") is not None else \
+                    float(self._output.get("default_threshold", 0.5))
                 if self._validation_metrics is not None and self._validation_metrics.get("max_f1_threshold") is not None:
                     thr = self._validation_metrics["max_f1_threshold"]
             lab = (p1 >= thr).to(torch.int32)
             lab = torch.where(torch.isnan(p1), torch.full_like(lab, -1), lab)
             vecs = [Vec(lab, T_ENUM, spec.response_domain), Vec((1 - p1).to(torch.float32), T_REAL),
                     Vec(p1.to(torch.float32), T_REAL)]
-            return H2OFrame.from_vecs(vecs, ["predict"] + list(spec.response_domain))
+            return H2OFrame.from_vecs(vecs, scoring_names(spec.response_domain))
         if spec.nclasses > 2:
             lab = torch.argmax(raw, 1).to(torch.int32)
             vecs = [Vec(lab, T_ENUM, spec.response_domain)] + [Vec(raw[:, k].to(torch.float32).contiguous(), T_REAL)
                                                                for k in range(raw.shape[1])]
-            return H2OFrame.from_vecs(vecs, ["predict"] + list(spec.response_domain))
+            return H2OFrame.from_vecs(vecs, scoring_names(spec.response_domain))
         return H2OFrame.from_vecs([Vec(raw[:, 0].to(torch.float32).contiguous(), T_REAL)], ["predict"])
 
     def predict(self, test_data, **kw):

@@ -945,6 +945,46 @@ class H2OGeneralizedLinearEstimator(H2OEstimator):
         return self._output.get("residual_degrees_of_freedom")
 
     @staticmethod
+    def makeGLMModel(model, coefs, threshold=0.5):
+        """A copy of a trained binomial / regression GLM with user-given
+        coefficients (h2o-py glm.py makeGLMModel -> hex/glm/
+        MakeGLMModelHandler.java): coefs maps coefficient names (incl.
+        "Intercept") to original-scale values; coefficients not named keep
+        their values; the binomial decision threshold is set."""
+        import copy
+        if getattr(model, "_multi", None) is not None or getattr(model, "_hglm", None) is not None:
+            raise ValueError("makeGLMModel supports binomial and regression GLMs")
+        names = list(model._dinfo.coef_names)
+        unknown = [k for k in coefs if k != "Intercept" and k not in names]
+        if unknown:
+            raise ValueError(f"unknown coefficient names: {unknown}")
+        beta = np.array(model._beta, dtype=np.float64).copy()
+        for j, n in enumerate(names):
+            if n in coefs:
+                beta[j] = float(coefs[n])
+        icpt = float(coefs.get("Intercept", model._icpt))
+        # original scale -> the standardized space the scorer uses (inverse of DataInfo.destandardize)
+        bstd = beta.copy()
+        istd = icpt
+        di = model._dinfo
+        if di.standardize:
+            base = di.n_cat_expanded
+            for j in range(len(di.num_cols)):
+                bstd[base + j] = beta[base + j] * di.sigmas[j]
+                istd += beta[base + j] * di.means[j]
+        m = copy.copy(model)
+        m._output = copy.deepcopy(model._output)
+        m._beta, m._icpt = beta, icpt
+        m._beta_std = np.concatenate([bstd, [istd]])
+        m._output["coefficients"] = {"Intercept": icpt, **{n: float(b) for n, b in zip(names, beta)}}
+        m._output["standardized_coefficients"] = {"Intercept": istd,
+                                                  **{n: float(b) for n, b in zip(names, bstd)}}
+        m._output["default_threshold"] = float(threshold)
+        m._training_metrics = m._validation_metrics = m._cross_validation_metrics = None
+        m._id = f"{model.model_id}_makeGLMModel"
+        return m
+
+    @staticmethod
     def getGLMRegularizationPath(model):
         return model._output["regularization_path"]
 

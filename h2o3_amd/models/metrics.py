@@ -423,3 +423,50 @@ def clustering_metrics(X, centers, assign, w=None):
     return ModelMetricsClustering(tot_withinss=tw, totss=totss, betweenss=totss - tw,
                                   withinss=within.cpu().tolist(), size=sizes.cpu().tolist(),
                                   nobs=int(float(sw)))
+
+
+# ---- sklearn-style regression metric functions over single-column frames
+# (h2o-py h2o/model/models/regression.py h2o_mean_absolute_error & co.)
+def _pair(y_actual, y_predicted, weights=None):
+    a = y_actual.vec(y_actual.names[0]).as_float(torch.float64) if hasattr(y_actual, "vec") else \
+        torch.as_tensor(y_actual, dtype=torch.float64)
+    p = y_predicted.vec(y_predicted.names[0]).as_float(torch.float64) if hasattr(y_predicted, "vec") else \
+        torch.as_tensor(y_predicted, dtype=torch.float64, device=a.device)
+    w = None
+    if weights is not None:
+        w = weights.vec(weights.names[0]).as_float(torch.float64) if hasattr(weights, "vec") else \
+            torch.as_tensor(weights, dtype=torch.float64, device=a.device)
+    ok = ~torch.isnan(a) & ~torch.isnan(p)
+    return a[ok], p[ok], (torch.ones_like(a[ok]) if w is None else w[ok])
+
+
+def h2o_mean_absolute_error(y_actual, y_predicted, weights=None):
+    a, p, w = _pair(y_actual, y_predicted, weights)
+    return _wsum(w * (a - p).abs()) / _wsum(w)
+
+
+def h2o_mean_squared_error(y_actual, y_predicted, weights=None):
+    a, p, w = _pair(y_actual, y_predicted, weights)
+    return _wsum(w * (a - p) ** 2) / _wsum(w)
+
+
+def h2o_median_absolute_error(y_actual, y_predicted):
+    a, p, _ = _pair(y_actual, y_predicted)
+    return float(torch.median((a - p).abs()))
+
+
+def h2o_explained_variance_score(y_actual, y_predicted, weights=None):
+    a, p, w = _pair(y_actual, y_predicted, weights)
+    sw = _wsum(w)
+    d = a - p
+    md, ma = _wsum(w * d) / sw, _wsum(w * a) / sw
+    vd, va = _wsum(w * (d - md) ** 2) / sw, _wsum(w * (a - ma) ** 2) / sw
+    return 1.0 - vd / va if va > 0 else 0.0
+
+
+def h2o_r2_score(y_actual, y_predicted, weights=None):
+    a, p, w = _pair(y_actual, y_predicted, weights)
+    sw = _wsum(w)
+    ma = _wsum(w * a) / sw
+    ss_res, ss_tot = _wsum(w * (a - p) ** 2), _wsum(w * (a - ma) ** 2)
+    return 1.0 - ss_res / ss_tot if ss_tot > 0 else float("nan")

@@ -57,6 +57,9 @@ class H2ORuleFitEstimator(H2OEstimator):
         p = self._parms
         algo = str(p.get("algorithm") or "AUTO").upper()
         lo, hi = int(p.get("min_rule_length", 3)), int(p.get("max_rule_length", 3))
+        if lo > hi:                                        # RuleFitModel.java:79
+            raise ValueError(f"min_rule_length cannot be greater than max_rule_length. Current values:  "
+                             f"min_rule_length = {lo}, max_rule_length = {hi}.")
         depths = list(range(lo, hi + 1))
         nt = max(1, int(p.get("rule_generation_ntrees", 50)) // len(depths))
         seed = p.get("seed", -1)

@@ -16,6 +16,17 @@ import zipfile
 import numpy as np
 
 
+def scoring_names(domain):
+    """Prediction columns (hex/Model.java makeScoringNames): "predict", then
+    one probability column per class, integer labels prefixed with "p"."""
+    out = ["predict"]
+    for d in domain:
+        d = str(d)
+        t = d[1:] if d[:1] in "+-" else d
+        out.append("p" + d if t.isdigit() and -2**31 <= int(d) < 2**31 else d)
+    return out
+
+
 def _sigmoid(x):
     return 1.0 / (1.0 + np.exp(-x))
 
@@ -655,7 +666,7 @@ class MojoModel:
             else:
                 lab = np.array(dom, dtype=object)[raw.argmax(1)]
             out = {"predict": lab}
-            for k, d in enumerate(dom):
+            for k, d in enumerate(scoring_names(dom)[1:]):
                 out[d] = raw[:, k]
             return pd.DataFrame(out)
         if raw.shape[1] == 1:

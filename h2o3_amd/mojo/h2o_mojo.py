@@ -1253,7 +1253,8 @@ class H2OMojoModel:
             dom = self.response_domain or [str(i) for i in range(self.nclasses)]
             lab = np.array(dom, dtype=object)[preds[:, 0].astype(np.int64)]
             out = {"predict": lab}
-            for k, d in enumerate(dom):
+            from .genmodel import scoring_names
+            for k, d in enumerate(scoring_names(dom)[1:]):
                 out[d] = preds[:, 1 + k]
             cal = getattr(self, "calibrated", None)
             if cal is not None and self.calib_beta is not None:

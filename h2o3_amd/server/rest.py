@@ -1208,6 +1208,9 @@ def create_app(flow_dir: str | None = None) -> FastAPI:
             os.remove(path)
         return _nps(category=category, name=name)
 
+    from . import rest_more
+    rest_more.register(app, route, {"api": api, "uploads": uploads,
+                                    "uptime_ms": lambda: (time.time() - t_start) * 1000})
     return app
 
 

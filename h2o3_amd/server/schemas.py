@@ -442,7 +442,7 @@ def model_category(m) -> str:
         return "AnomalyDetection"
     spec = getattr(m, "_spec", None)
     if spec is not None and getattr(spec, "is_classification", False):
-        return "Binomial" if len(getattr(spec, "domain", None) or []) == 2 else "Multinomial"
+        return "Binomial" if getattr(spec, "nclasses", 0) == 2 else "Multinomial"
     return "Regression" if m.supervised_learning else "Unknown"
 
 
@@ -642,19 +642,26 @@ def _algo_output(m, output):
             if k in o:
                 output[k] = o[k]
     if "centers" in o:
-        c = np.asarray(o["centers"], dtype=np.float64)
+        # categorical columns' centers are their level names (KMeansModel output centers table)
+        c = np.asarray(o["centers"], dtype=object)
         names = o.get("coef_names") or [f"C{j + 1}" for j in range(c.shape[1] if c.ndim == 2 else 0)]
+
+        def _cell(x):
+            try:
+                return float(x)
+            except (TypeError, ValueError):
+                return str(x)
         if c.ndim == 2:
             cols = {"centroid": list(range(1, c.shape[0] + 1))}
             for j, n in enumerate(names[:c.shape[1]]):
-                cols[str(n)] = [float(x) for x in c[:, j]]
+                cols[str(n)] = [_cell(x) for x in c[:, j]]
             output["centers"] = twodim("Cluster Means", cols)
             cs = o.get("centers_std")
             if cs is not None:
-                cs = np.asarray(cs, dtype=np.float64)
+                cs = np.asarray(cs, dtype=object)
                 cols = {"centroid": list(range(1, cs.shape[0] + 1))}
                 for j, n in enumerate(names[:cs.shape[1]]):
-                    cols[str(n)] = [float(x) for x in cs[:, j]]
+                    cols[str(n)] = [_cell(x) for x in cs[:, j]]
                 output["centers_std"] = twodim("Cluster Means (standardized)", cols)
     imp = o.get("importance")
     if isinstance(imp, dict) and imp:

@@ -29,7 +29,7 @@ def test_stacked_ensemble_binomial():
     p = m.predict_row({"AGE": "65", "RACE": "1", "DPROS": "2", "DCAPS": "1", "PSA": "1.4", "VOL": "0",
                        "GLEASON": "6"})
     assert p["predict"] == "0"
-    np.testing.assert_allclose([p["0"], p["1"]], [0.8222695, 0.1777305], atol=1e-5)
+    np.testing.assert_allclose([p["p0"], p["p1"]], [0.8222695, 0.1777305], atol=1e-5)
     assert [b[0].algo for b in m.base] == ["gbm", "drf", "drf"]
 
 
@@ -42,7 +42,7 @@ def test_stacked_ensemble_regression_and_multinomial():
     p = mm.predict_row({"CAPSULE": "0", "AGE": "65", "DPROS": "2", "DCAPS": "1", "PSA": "1.4", "VOL": "0",
                         "GLEASON": "6"})
     assert p["predict"] == "1"
-    np.testing.assert_allclose([p["0"], p["1"], p["2"]], [0.006592327, 0.901237, 0.09217069], atol=1e-5)
+    np.testing.assert_allclose([p["p0"], p["p1"], p["p2"]], [0.006592327, 0.901237, 0.09217069], atol=1e-5)
 
 
 def test_stacked_ensemble_pruned_base_models():
@@ -58,7 +58,7 @@ def test_stacked_ensemble_with_deep_learning_base():
            "sibsp": 1.0, "parch": 2.0, "ticket": 113781.0, "fare": 151.55, "cabin": "C22 C26", "embarked": "S",
            "boat": 11.0, "body": float("nan"), "home.dest": "Montreal, PQ / Chesterville, ON"}
     p = m.predict_row(row)
-    assert p["predict"] in ("0", "1") and abs(p["0"] + p["1"] - 1) < 1e-9
+    assert p["predict"] in ("0", "1") and abs(p["p0"] + p["p1"] - 1) < 1e-9
     assert "deeplearning" in [b[0].algo for b in m.base if b]
 
 
@@ -106,7 +106,7 @@ def test_gbm_calibrated_and_leaf_paths():
            "USAvgT": 0.2, "USRainDays": 1.153, "USSlope": 8.3, "USNative": 0.34, "DSDam": 0.0, "Method": "electric"}
     p = m.predict_row(row)
     assert p["predict"] == "1"
-    np.testing.assert_allclose([p["0"], p["1"]], [0.5416688, 0.4583312], atol=1e-5)
+    np.testing.assert_allclose([p["p0"], p["p1"]], [0.5416688, 0.4583312], atol=1e-5)
     np.testing.assert_allclose([p["cal_0"], p["cal_1"]], [0.3920402, 0.6079598], atol=1e-5)
     assert m.decision_paths({})[0] == ["LRLR", "LRLR", "LRLR", "LRLR", "LRLR", "RLLRR", "RLLRL", "RLLLL",
                                        "LRLRL", "RRLRL"]
@@ -160,7 +160,7 @@ def test_generic_estimator_imports_reference_mojo(tmp_path):
     fr = h2o.H2OFrame(pd.DataFrame({"AGE": [65.0], "RACE": ["1"], "DPROS": ["2"], "DCAPS": [1.0], "PSA": [1.4],
                                     "VOL": [0.0], "GLEASON": [6.0]}))
     out = g.predict(fr).as_data_frame()
-    assert abs(float(out["1"][0]) - 0.1777305) < 1e-5
+    assert abs(float(out["p1"][0]) - 0.1777305) < 1e-5
     m = h2o.import_mojo(R + "algos/pipeline/glm_model.zip")
     assert m._mojo.algo == "glm"
 

@@ -93,6 +93,7 @@ def test_flow_page_served():
     c = TestClient(create_app())
     r = c.get("/", follow_redirects=True)
     assert r.status_code == 200 and "h2o3_amd Flow" in r.text
-    for ep in ("/3/Cloud", "/3/Frames", "/3/Models", "/3/Jobs", "/3/ImportFiles", "/3/ParseSetup", "/3/Parse",
-               "/3/ModelBuilders/", "/3/Predictions/models/", "/99/Rapids"):
-        assert ep in r.text          # the page drives the same REST endpoints the clients use
+    # the notebook page runs cells through /flow/cell and keeps notebooks in NodePersistentStorage
+    for ep in ("/3/Cloud", "/3/Frames", "/3/Models", "/flow/cell", "/flow/routines",
+               "/3/NodePersistentStorage/notebook"):
+        assert ep in r.text

@@ -124,6 +124,23 @@ def test_reference_python_client_models(server_url):
 
 
 @pytest.mark.skipif(not os.path.isdir(os.path.join(REF_PY, "h2o")), reason="reference h2o-py client not present")
+@pytest.mark.timeout(300)
+def test_reference_python_client_inspection_and_persistence(server_url):
+    """H2OTree, Word2Vec, feature interactions, H, rules, TE transform,
+    makeGLMModel, frame / grid save-load, sessions (tests/wire_client_more.py)."""
+    env = dict(os.environ, PYTHONPATH="", OMP_NUM_THREADS="2")
+    r = subprocess.run([sys.executable, "-u", os.path.join(HERE, "wire_client_more.py"), server_url, REF_PY],
+                       capture_output=True, text=True, timeout=280, env=env, cwd=HERE)
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("SUMMARY ")]
+    assert line, r.stdout[-3000:]
+    out = json.loads(line[-1][len("SUMMARY "):])
+    bad = [ln for ln in r.stdout.splitlines() if ln.startswith("BAD")]
+    assert out["bad"] == [], bad
+    assert out["ok"] >= 16
+
+
+@pytest.mark.skipif(not os.path.isdir(os.path.join(REF_PY, "h2o")), reason="reference h2o-py client not present")
 @pytest.mark.timeout(200)
 def test_reference_python_client_basic_auth(tmp_path):
     """The reference client with auth=(user, password) against a server

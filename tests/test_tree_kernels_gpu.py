@@ -656,7 +656,7 @@ def test_gbm_leaf_scatter_update_matches_rmw(monkeypatch):
             monkeypatch.setenv("H2O3_LEAF_SCATTER", flag)
             m = H2OGradientBoostingEstimator(ntrees=6, max_depth=5, seed=3, sample_rate=sr)
             m.train(y="y", training_frame=fr)
-            preds.append(m.predict(fr).as_data_frame()["1"].values)
+            preds.append(m.predict(fr).as_data_frame()["p1"].values)
         np.testing.assert_allclose(preds[0], preds[1], rtol=0, atol=1e-6)
 
 
