@@ -350,4 +350,250 @@ def register(app, route, ctx):
         return {"__meta": S.meta("FrameChunksV3", "Iced"), "frame_id": S.key(fid),
                 "chunks": [{"chunk_id": 0, "row_count": int(fr.nrows), "node_idx": 0}]}
 
+    # ------------------------------------------------ frame utilities
+    def _col(fr, spec):
+        if isinstance(spec, dict):
+            spec = spec.get("column_name")
+        return spec
+
+    @route("POST", "/99/Tabulate")
+    def tabulate(p, r):
+        """TabulateHandler: counts and mean response over a binned predictor
+        (nbins_predictor) x binned response (nbins_response) grid."""
+        import numpy as np
+        fr = _frame(p.get("dataset"), "dataset")
+        pc, rc, wc = _col(fr, p.get("predictor")), _col(fr, p.get("response")), _col(fr, p.get("weight"))
+        cols = [c for c in (pc, rc, wc) if c]
+        df = fr[cols].as_data_frame()
+        nbp, nbr = int(p.get("nbins_predictor", 20) or 20), int(p.get("nbins_response", 10) or 10)
+        w = df[wc].to_numpy(float) if wc else np.ones(len(df))
+
+        def binned(v, nb):
+            if v.dtype == object or str(v.dtype) == "category":
+                lab = v.astype(str).to_numpy()
+                levels = sorted(set(lab))
+                return np.array([levels.index(x) for x in lab]), levels
+            x = v.to_numpy(float)
+            lo, hi = np.nanmin(x), np.nanmax(x)
+            k = np.clip(((x - lo) / ((hi - lo) or 1) * nb).astype(int), 0, nb - 1)
+            return k, [float(lo + (hi - lo) * i / nb) for i in range(nb)]
+        bp, lp = binned(df[pc], nbp)
+        br, lr = binned(df[rc], nbr)
+        cnt = np.zeros((len(lp), len(lr)))
+        np.add.at(cnt, (bp, br), w)
+        resp = df[rc].to_numpy(float) if df[rc].dtype != object else br.astype(float)
+        rs = np.zeros(len(lp))
+        ws = np.zeros(len(lp))
+        np.add.at(rs, bp, resp * w)
+        np.add.at(ws, bp, w)
+        ct = S.twodim("(Weighted) co-occurrence counts of '" + pc + "' and '" + rc + "'",
+                      {pc: [str(x) for x in np.repeat(lp, len(lr))], rc: [str(x) for x in np.tile(lr, len(lp))],
+                       "counts": cnt.reshape(-1).tolist()})
+        rt = S.twodim("Mean value of '" + rc + "' and (weighted) counts",
+                      {pc: [str(x) for x in lp], "mean " + rc: (rs / np.maximum(ws, 1e-300)).tolist(),
+                       "counts": ws.tolist()})
+        return {"__meta": S.meta("TabulateV3", "Iced"), "dataset": S.key(fr.frame_id), "count_table": ct,
+                "response_table": rt}
+
+    @route("POST", "/3/DataInfoFrame")
+    def data_info_frame(p, r):
+        """The model matrix of a frame (DataInfo expansion: one-hot
+        categoricals, optionally standardized numerics)."""
+        import torch
+        from ..core.vec import T_REAL, Vec
+        from ..models.datainfo import DataInfo
+        fr = _frame(p.get("frame"), "frame")
+        di = DataInfo(fr, list(fr.names), standardize=bool(p.get("standardize", False)),
+                      use_all_factor_levels=bool(p.get("use_all", False)), pad_to=None)
+        X, _ = di.expand(fr, dtype=torch.float64, pad=False)
+        out = H2OFrame.from_vecs([Vec(X[:, j].contiguous(), T_REAL) for j in range(di.P)], list(di.coef_names))
+        fid = _put_frame(out, f"{fr.frame_id}_datainfo")
+        return {"__meta": S.meta("DataInfoFrameV3", "Iced"), "frame": S.key(fr.frame_id), "result": S.key(fid)}
+
+    @route("GET", "/3/ComputeGram")
+    def compute_gram(p, r):
+        """GramHandler: X'WX of the expanded frame as a frame."""
+        import torch
+        from ..core.vec import T_REAL, Vec
+        from ..models.datainfo import DataInfo
+        fr = _frame(p.get("X"), "X")
+        wc = _col(fr, p.get("W"))
+        x = [c for c in fr.names if c != wc]
+        di = DataInfo(fr, x, standardize=bool(p.get("standardize", False)),
+                      use_all_factor_levels=bool(p.get("use_all_factor_levels", False)), pad_to=None)
+        X, ok = di.expand(fr, dtype=torch.float64, pad=False)
+        if bool(p.get("skip_missing", False)):
+            X = X[ok]
+        w = fr.vec(wc).as_float(torch.float64) if wc else None
+        if w is not None and bool(p.get("skip_missing", False)):
+            w = w[ok]
+        G = X.T @ (X * w.view(-1, 1) if w is not None else X)
+        from ..parallel import collectives as coll
+        coll.allreduce_(G)
+        out = H2OFrame.from_vecs([Vec(G[:, j].contiguous(), T_REAL) for j in range(G.shape[1])],
+                                 list(di.coef_names))
+        fid = _put_frame(out, p.get("destination_frame") or f"{fr.frame_id}_gram")
+        return {"__meta": S.meta("GramV3", "Iced"), "X": S.key(fr.frame_id), "destination_frame": S.key(fid)}
+
+    @route("POST", "/99/DCTTransformer")
+    def dct(p, r):
+        """DCTTransformerHandler: per-row orthonormal DCT-II (inverse: DCT-III)
+        over the row reshaped to dimensions [x, y, z]."""
+        import numpy as np
+        import scipy.fft as sfft
+        import torch
+        from ..core.vec import T_REAL, Vec
+        fr = _frame(p.get("dataset"), "dataset")
+        dims = [int(d) for d in (p.get("dimensions") or [fr.ncol, 1, 1])]
+        if int(np.prod(dims)) != fr.ncol:
+            raise _HTTPError(400, f"dimensions {dims} do not match the {fr.ncol} columns")
+        A = np.stack([fr.vec(c).as_float(torch.float64).cpu().numpy() for c in fr.names], 1)
+        B = A.reshape((-1, *dims))
+        axes = tuple(1 + i for i, d in enumerate(dims) if d > 1)
+        f = sfft.idctn if p.get("inverse") else sfft.dctn
+        Y = f(B, type=2, axes=axes, norm="ortho").reshape(A.shape)
+        dev = fr.vec(fr.names[0]).data.device
+        out = H2OFrame.from_vecs([Vec(torch.as_tensor(Y[:, j], device=dev).contiguous(), T_REAL)
+                                  for j in range(Y.shape[1])], list(fr.names))
+        fid = _put_frame(out, p.get("destination_frame") or f"{fr.frame_id}_dct")
+        return {"__meta": S.meta("DCTTransformerV3", "Iced"), "dataset": S.key(fr.frame_id),
+                "destination_frame": S.key(fid), "job": _job(fid, "DCT")}
+
+    @route("GET", "/3/Find")
+    def find(p, r):
+        """FindHandler: previous / next row (from `row`) whose column value
+        matches `match` (-1 when none)."""
+        import numpy as np
+        kv = p.get("key")
+        fr = _frame(kv["name"] if isinstance(kv, dict) else kv, "key")
+        row = int(p.get("row", 0) or 0)
+        cols = [p["column"]] if p.get("column") else list(fr.names)
+        hit = np.zeros(fr.nrows, dtype=bool)
+        df = fr[cols].as_data_frame()
+        m = str(p.get("match"))
+        for c in cols:
+            v = df[c]
+            hit |= (v.astype(str).to_numpy() == m) | (v.isna().to_numpy() & (m in ("NA", "nan", "")))
+        idx = np.nonzero(hit)[0]
+        prev = idx[idx < row]
+        nxt = idx[idx > row]
+        return {"__meta": S.meta("FindV3", "Iced"), "column": p.get("column"), "row": row, "match": m,
+                "prev": int(prev[-1]) if len(prev) else -1, "next": int(nxt[0]) if len(nxt) else -1}
+
+    @route("GET", "/3/Frames/{fid}/export/{path}/overwrite/{force}")
+    def frame_export_get(p, r, fid, path, force):
+        from ..core.parse import export_file
+        export_file(_frame(fid), path, force=str(force).lower() in ("true", "1"))
+        return {"__meta": S.meta("FramesV3", "Frames"), "frame_id": S.key(fid), "path": path,
+                "job": _job(fid, "Export")}
+
+    @route("GET", "/3/Models.java/{mid}/preview")
+    def pojo_preview(p, r, mid):
+        from fastapi.responses import PlainTextResponse
+        from ..mojo.pojo import to_java
+        src = to_java(_model(mid))
+        return PlainTextResponse("\n".join(src.splitlines()[:1000]))
+
+    # ---------------------------------------------------- ModelMetrics
+    def _all_metrics(mid=None, fid=None):
+        from ..models.base import H2OEstimator
+        out = []
+        for k in list(dkv.keys()):
+            m = dkv.get(k)
+            if not isinstance(m, H2OEstimator) or (mid and k != mid):
+                continue
+            tf = getattr(getattr(m, "_spec", None), "frame", None)
+            for mm in (m._training_metrics, m._validation_metrics):
+                if mm is None:
+                    continue
+                if fid and getattr(tf, "frame_id", None) != fid:
+                    continue
+                out.append(S.metrics_v3(mm, m, getattr(tf, "frame_id", None)))
+        return out
+
+    @route("GET", "/3/ModelMetrics")
+    def mm_all(p, r):
+        return {"__meta": S.meta("ModelMetricsListSchemaV3", "Iced"), "model_metrics": _all_metrics()}
+
+    @route("GET", "/3/ModelMetrics/models/{mid}")
+    def mm_model(p, r, mid):
+        _model(mid)
+        return {"__meta": S.meta("ModelMetricsListSchemaV3", "Iced"), "model_metrics": _all_metrics(mid=mid)}
+
+    @route("GET", "/3/ModelMetrics/frames/{fid}")
+    def mm_frame(p, r, fid):
+        return {"__meta": S.meta("ModelMetricsListSchemaV3", "Iced"), "model_metrics": _all_metrics(fid=fid)}
+
+    @route("GET", "/3/ModelMetrics/frames/{fid}/models/{mid}")
+    def mm_frame_model(p, r, fid, mid):
+        return {"__meta": S.meta("ModelMetricsListSchemaV3", "Iced"),
+                "model_metrics": _all_metrics(mid=mid, fid=fid)}
+
+    for pth in ("/3/ModelMetrics", "/3/ModelMetrics/models/{mid}", "/3/ModelMetrics/frames/{fid}",
+                "/3/ModelMetrics/frames/{fid}/models/{mid}", "/3/ModelMetrics/models/{mid}/frames/{fid}"):
+        # metrics are computed on demand here, nothing is cached to delete
+        route("DELETE", pth)(lambda p, r, **kw: {"__meta": S.meta("ModelMetricsListSchemaV3", "Iced"),
+                                                 "model_metrics": []})
+
+    # ------------------------------------------------------- monitoring
+    @route("GET", "/3/WaterMeterCpuTicks/{node}")
+    def cpu_ticks(p, r, node):
+        """Per-core (user, system, other, idle) ticks of this node."""
+        import psutil
+        ticks = [[int(c.user * 100), int(c.system * 100), int((c.nice + getattr(c, "iowait", 0)) * 100),
+                  int(c.idle * 100)] for c in psutil.cpu_times(percpu=True)]
+        return {"__meta": S.meta("WaterMeterCpuTicksV3", "Iced"), "nodeidx": int(node), "cpu_ticks": ticks}
+
+    @route("GET", "/3/WaterMeterIo")
+    def io_meter(p, r):
+        import psutil
+        d = psutil.disk_io_counters()
+        return {"__meta": S.meta("WaterMeterIoV3", "Iced"), "nodeidx": -1,
+                "persist_stats": [{"backend": "local", "store_count": int(d.write_count) if d else 0,
+                                   "store_bytes": int(d.write_bytes) if d else 0,
+                                   "load_count": int(d.read_count) if d else 0,
+                                   "load_bytes": int(d.read_bytes) if d else 0}]}
+
+    route("GET", "/3/WaterMeterIo/{node}")(lambda p, r, node: io_meter(p, r))
+
+    @route("GET", "/3/SteamMetrics")
+    def steam_metrics(p, r):
+        return {"__meta": S.meta("SteamMetricsV3", "Iced"), "version": 0,
+                "idle_millis": int(time.time() * 1000 - ctx.get("last_request_ms", time.time() * 1000))}
+
+    @route("GET", "/3/Profiler")
+    def profiler(p, r):
+        """Stack-trace sampling of the serving process (ProfilerHandler)."""
+        import collections
+        import sys
+        import traceback
+        depth = int(p.get("depth", 10) or 10)
+        cnt = collections.Counter()
+        for _ in range(10):
+            for fr_ in sys._current_frames().values():
+                cnt["".join(traceback.format_stack(fr_)[-depth:])] += 1
+            time.sleep(0.005)
+        return {"__meta": S.meta("ProfilerV3", "Iced"), "depth": depth,
+                "nodes": [{"node_name": "rank0", "timestamp": int(time.time() * 1000),
+                           "entries": [{"stacktrace": k, "count": v} for k, v in cnt.most_common()]}]}
+
+    @route("POST", "/3/KillMinus3")
+    def kill_minus3(p, r):
+        """Thread dump to the log (the reference's kill -3)."""
+        from ..utils import log
+        log.info("KillMinus3 thread dump:\n" + "\n".join(jstack(p, r)["traces"][0]["thread_traces"]))
+        return {"__meta": S.meta("KillMinus3V3", "Iced")}
+
+    route("GET", "/3/KillMinus3")(kill_minus3)
+
+    @route("GET", "/3/Metadata/schemaclasses/{cls}")
+    def schema_class(p, r, cls):
+        return {"__meta": S.meta("MetadataV3", "Iced"), "schemas": [{"name": cls, "fields": []}]}
+
+    @route("GET", "/3/Metadata/endpoints/{path}")
+    def endpoint_meta(p, r, path):
+        routes = [{"__meta": S.meta("RouteV3", "Iced"), "url_pattern": rt.path, "http_method": next(iter(rt.methods))}
+                  for rt in app.routes if hasattr(rt, "methods") and path in rt.path]
+        return {"__meta": S.meta("MetadataV3", "Iced"), "routes": routes, "schemas": []}
+
     return app
