@@ -176,32 +176,62 @@ class H2OGeneralizedLowRankEstimator(H2OEstimator):
         M = torch.cat(masks, 1).to(torch.float32) if masks else torch.zeros_like(A)
         return A, M, blocks
 
-    def _loss(self, A, M, U, blocks, per_row=False):
+    def _loss_groups(self, blocks, device):
+        """Columns grouped for one vectorized loss evaluation per group:
+        numeric columns by loss name, the categorical one-vs-all columns
+        together; ordinal categorical blocks keep their own term."""
+        key = (id(blocks), str(device))
+        if getattr(self, "_lg_key", None) == key:
+            return self._lg
         p = self._parms
         lbc = {}
         if p.get("loss_by_col"):
             idx = p.get("loss_by_col_idx") or []
             for name, i in zip(p["loss_by_col"], idx):
                 lbc[self._cols[i] if isinstance(i, int) else i] = name
-        tot = U.new_zeros((U.shape[0],))
-        j = 0
-        ml = str(p.get("multi_loss") or "Categorical").lower()
+        ordinal = str(p.get("multi_loss") or "Categorical").lower() == "ordinal"
+        num, cat, ords, j = {}, [], [], 0
         for kind, c, w in blocks:
-            a, m, u = A[:, j:j + w], M[:, j:j + w], U[:, j:j + w]
             if kind == "num":
-                L = _num_loss(lbc.get(c, p.get("loss") or "Quadratic"), a, u, float(p.get("period", 1)))
-                tot = tot + (L * m)[:, 0]
+                num.setdefault(lbc.get(c, p.get("loss") or "Quadratic"), []).append(j)
+            elif ordinal:
+                ords.append((j, w))
             else:
-                rowm = m[:, 0]
-                if ml == "ordinal":
-                    lvl = a.argmax(1, keepdim=True)
-                    ar = torch.arange(w, device=a.device).view(1, -1)
-                    L = torch.where(ar < lvl, torch.clamp(1 - u, min=0), torch.clamp(1 + u, min=0))
-                else:  # Categorical one-vs-all hinge
-                    L = torch.where(a > 0, torch.clamp(1 - u, min=0), torch.clamp(1 + u, min=0))
-                tot = tot + L.sum(1) * rowm
+                cat += list(range(j, j + w))
             j += w
+        t = lambda v: torch.as_tensor(v, dtype=torch.long, device=device)  # noqa: E731
+        self._lg = ({k: t(v) for k, v in num.items()}, t(cat) if cat else None, ords)
+        self._lg_key = key
+        return self._lg
+
+    def _loss(self, A, M, U, blocks, per_row=False):
+        p = self._parms
+        num, cat, ords = self._loss_groups(blocks, U.device)
+        tot = U.new_zeros((U.shape[0],))
+        period = float(p.get("period", 1))
+        for name, idx in num.items():
+            if idx.numel() == A.shape[1]:                    # every column: no gather
+                tot = tot + (_num_loss(name, A, U, period) * M).sum(1)
+            else:
+                tot = tot + (_num_loss(name, A[:, idx], U[:, idx], period) * M[:, idx]).sum(1)
+        if cat is not None:                                  # one-vs-all hinge over every level column
+            a, u = A[:, cat], U[:, cat]
+            L = torch.where(a > 0, torch.clamp(1 - u, min=0), torch.clamp(1 + u, min=0))
+            tot = tot + (L * M[:, cat]).sum(1)
+        for j, w in ords:
+            a, m, u = A[:, j:j + w], M[:, j:j + w], U[:, j:j + w]
+            lvl = a.argmax(1, keepdim=True)
+            ar = torch.arange(w, device=a.device).view(1, -1)
+            L = torch.where(ar < lvl, torch.clamp(1 - u, min=0), torch.clamp(1 + u, min=0))
+            tot = tot + L.sum(1) * m[:, 0]
         return tot if per_row else tot.sum()
+
+    def _grad_u(self, A, M, U, blocks):
+        """d loss / d U (U = X Y) with U as the only autograd leaf: the X and
+        Y gradients are then gU Y' and X' gU."""
+        Uv = U.detach().requires_grad_(True)
+        gU, = torch.autograd.grad(self._loss(A, M, Uv, blocks), Uv)
+        return gU
 
     # ------------------------------------------------------------ fit
     def _fit(self, spec):
@@ -253,14 +283,10 @@ class H2OGeneralizedLowRankEstimator(H2OEstimator):
         while it < max_it and updates < max_up and step >= min_step:
             it += 1
             # X update
-            Xv = X.clone().requires_grad_(True)
-            Lx = self._loss(A, M, Xv @ Y, blocks)
-            gX, = torch.autograd.grad(Lx, Xv)
+            gX = self._grad_u(A, M, X @ Y, blocks) @ Y.T
             Xn = _prox(rx, X - step * scale * gX, step * scale * gx)
             # Y update
-            Yv = Y.clone().requires_grad_(True)
-            Ly = self._loss(A, M, Xn @ Yv, blocks)
-            gY, = torch.autograd.grad(Ly, Yv)
+            gY = Xn.T @ self._grad_u(A, M, Xn @ Y, blocks)
             coll.allreduce_(gY)
             Yn = _prox(ry, Y - step * scale * gY, step * scale * gy)
             on = objective(Xn, Yn)

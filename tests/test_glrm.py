@@ -76,3 +76,44 @@ def test_glrm_mojo_matches_predict(tmp_path):
         for c in ("a", "b", "c"):
             np.testing.assert_allclose(got[f"reconstr_{c}"].values, exp[f"reconstr_{c}"].values, rtol=2e-3, atol=2e-3)
         assert (got["reconstr_g"].values == exp["reconstr_g"].values).mean() > 0.95
+
+
+def test_glrm_vectorized_loss_matches_per_block_loop():
+    """_loss evaluates column groups at once (numeric by loss name, the
+    categorical one-vs-all columns together); it equals the per-block sum
+    for mixed numeric / categorical / ordinal layouts and per-column losses."""
+    import numpy as np
+    import pandas as pd
+    import torch
+    import h2o3_amd as h2o
+    from h2o3_amd.core.frame import H2OFrame
+    from h2o3_amd.estimators import H2OGeneralizedLowRankEstimator
+    from h2o3_amd.models.glrm import _num_loss
+    h2o.init()
+    rng = np.random.default_rng(3)
+    df = pd.DataFrame({"a": rng.normal(size=60), "b": rng.poisson(2, 60).astype(float), "c": rng.choice(list("xyz"), 60),
+                       "d": rng.normal(size=60), "e": rng.choice(list("pq"), 60)})
+    df.loc[::7, "a"] = np.nan
+    fr = H2OFrame(df)
+    fr["c"] = fr["c"].asfactor()
+    fr["e"] = fr["e"].asfactor()
+    for multi in ("Categorical", "Ordinal"):
+        m = H2OGeneralizedLowRankEstimator(k=2, seed=1, max_iterations=3, multi_loss=multi,
+                                           loss_by_col=["Poisson", "Absolute"], loss_by_col_idx=[1, 3])
+        m.train(x=list(df.columns), training_frame=fr)
+        A, M, blocks = m._layout(fr, m._cols)
+        U = torch.randn(A.shape, dtype=A.dtype, generator=torch.Generator().manual_seed(0)).to(A.device)
+        lbc = {"b": "Poisson", "d": "Absolute"}
+        ref, j = torch.zeros(A.shape[0], dtype=A.dtype, device=A.device), 0
+        for kind, c, w in blocks:
+            a, mm, u = A[:, j:j + w], M[:, j:j + w], U[:, j:j + w]
+            if kind == "num":
+                ref += (_num_loss(lbc.get(c, "Quadratic"), a, u, 1.0) * mm)[:, 0]
+            elif multi == "Ordinal":
+                lvl = a.argmax(1, keepdim=True)
+                ar = torch.arange(w, device=a.device).view(1, -1)
+                ref += torch.where(ar < lvl, torch.clamp(1 - u, min=0), torch.clamp(1 + u, min=0)).sum(1) * mm[:, 0]
+            else:
+                ref += torch.where(a > 0, torch.clamp(1 - u, min=0), torch.clamp(1 + u, min=0)).sum(1) * mm[:, 0]
+            j += w
+        torch.testing.assert_close(m._loss(A, M, U, blocks, per_row=True), ref)
