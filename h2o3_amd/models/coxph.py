@@ -35,61 +35,94 @@ COX_DEFAULTS = dict(start_column=None, stop_column=None, stratify_by=None, ties=
                     interaction_pairs=None, calc_cumhaz=True, single_node_mode=False)
 
 
+class _Seg:
+    """Segmented sums by a fixed integer key: rows sorted by key once, each
+    sum is a cumulative sum over the sorted values differenced at the key
+    boundaries.  Replaces index_add_ into few bins (every row of a stratum
+    without a start column lands in bin 0: a million f64 atomics on one
+    address serialise)."""
+
+    def __init__(self, key, m):
+        self.order = torch.argsort(key, stable=True)
+        ks = key[self.order]
+        self.bounds = torch.searchsorted(ks, torch.arange(m + 1, device=key.device, dtype=ks.dtype))
+
+    def __call__(self, v):
+        cs = torch.cumsum(v[self.order], 0)
+        cs = torch.cat([torch.zeros_like(cs[:1]), cs], 0)
+        return cs[self.bounds[1:]] - cs[self.bounds[:-1]]
+
+
+class _Stratum:
+    """Risk-set structure of one stratum, independent of beta: event times,
+    each row's risk interval (jstart, jstop] in event-time indices, the
+    events per time and the Efron (time, l) expansion."""
+
+    def __init__(self, X, start, stop, ev, w, efron):
+        self.X, self.w = X, w
+        self.evm = ev > 0
+        self.times = torch.unique(stop[self.evm])
+        m = self.m = self.times.numel()
+        if m == 0:
+            return
+        jstop = torch.searchsorted(self.times, stop, right=True)
+        jstart = torch.searchsorted(self.times, start, right=True) if start is not None else torch.zeros_like(jstop)
+        self.valid = jstop > jstart
+        self.jstart, self.jstop = jstart, jstop
+        self.seg_start = _Seg(jstart[self.valid], m + 1)
+        self.seg_stop = _Seg(jstop[self.valid], m + 1)
+        self.je = je = torch.searchsorted(self.times, stop[self.evm])
+        self.seg_ev = _Seg(je, m)
+        self.dcnt = dcnt = torch.bincount(je, minlength=m)
+        wsum = self.seg_ev(w[self.evm])
+        self.wbar = wsum / dcnt.clamp_min(1).to(X.dtype)
+        self.jl = jl = torch.repeat_interleave(torch.arange(m, device=X.device), dcnt)
+        start_of = torch.cumsum(dcnt, 0) - dcnt
+        l_ = torch.arange(jl.numel(), device=X.device) - start_of[jl]
+        self.frac = (l_.to(X.dtype) / dcnt[jl].to(X.dtype)) if efron else \
+            torch.zeros(jl.numel(), dtype=X.dtype, device=X.device)
+        self.seg_jl = _Seg(jl, m)
+        self.wl = self.wbar[jl]
+        self.Xev_w = (w[self.evm].view(-1, 1) * X[self.evm]).sum(0)
+
+    def terms(self, beta):
+        """loglik, gradient, Hessian (negative) at beta (float64)."""
+        X, w = self.X, self.w
+        P = X.shape[1]
+        if self.m == 0:
+            z = torch.zeros(P, dtype=X.dtype, device=X.device)
+            return 0.0, z, torch.zeros((P, P), dtype=X.dtype, device=X.device)
+        eta = X @ beta
+        r = w * torch.exp(eta)
+        rx = r.view(-1, 1) * X
+        v = self.valid
+        R0 = torch.cumsum(self.seg_start(r[v]) - self.seg_stop(r[v]), 0)[:self.m]
+        R1 = torch.cumsum(self.seg_start(rx[v]) - self.seg_stop(rx[v]), 0)[:self.m]
+        D0 = self.seg_ev(r[self.evm])
+        D1 = self.seg_ev(rx[self.evm])
+        jl, frac, wl = self.jl, self.frac, self.wl
+        R0l = R0[jl] - frac * D0[jl]
+        R1l = R1[jl] - frac.view(-1, 1) * D1[jl]
+        ll = float((w[self.evm] * eta[self.evm]).sum() - (wl * torch.log(R0l)).sum())
+        grad = self.Xev_w - ((wl / R0l).view(-1, 1) * R1l).sum(0)
+        # Hessian part 1: sum over (j,l) of wbar (R2 - frac D2) / R0l as per-row weights
+        c = wl / R0l
+        C = self.seg_jl(c)
+        Cf = self.seg_jl(c * frac)
+        Pc = torch.cat([torch.zeros(1, dtype=X.dtype, device=X.device), torch.cumsum(C, 0)])
+        a = torch.where(v, Pc[self.jstop] - Pc[self.jstart], torch.zeros_like(r))
+        a_ev = torch.zeros_like(r)
+        a_ev[self.evm] = Cf[self.je]
+        a = r * (a - a_ev)
+        H1 = linalg_ops.weighted_gram(X.to(torch.float32), a.to(torch.float32)) if (
+            X.device.type == "cuda" and P % 32 == 0) else X.T @ (X * a.view(-1, 1))
+        H2 = R1l.T @ (R1l * (wl / (R0l * R0l)).view(-1, 1))
+        return ll, grad, H1.to(X.dtype) - H2
+
+
 def _stratum_terms(X, start, stop, ev, w, beta, efron):
     """loglik, gradient, Hessian (negative) for one stratum (float64 tensors)."""
-    P = X.shape[1]
-    eta = X @ beta
-    r = w * torch.exp(eta)
-    evm = ev > 0
-    times = torch.unique(stop[evm])
-    m = times.numel()
-    if m == 0:
-        z = torch.zeros(P, dtype=X.dtype, device=X.device)
-        return 0.0, z, torch.zeros((P, P), dtype=X.dtype, device=X.device)
-    # risk interval (jstart, jstop] in event-time indices
-    jstop = torch.searchsorted(times, stop, right=True)
-    jstart = torch.searchsorted(times, start, right=True) if start is not None else torch.zeros_like(jstop)
-    valid = jstop > jstart
-    R0d = torch.zeros(m + 1, dtype=X.dtype, device=X.device)
-    R1d = torch.zeros((m + 1, P), dtype=X.dtype, device=X.device)
-    R0d.index_add_(0, jstart[valid], r[valid])
-    R0d.index_add_(0, jstop[valid], -r[valid])
-    rx = r.view(-1, 1) * X
-    R1d.index_add_(0, jstart[valid], rx[valid])
-    R1d.index_add_(0, jstop[valid], -rx[valid])
-    R0 = torch.cumsum(R0d, 0)[:m]
-    R1 = torch.cumsum(R1d, 0)[:m]
-    # events at each time
-    je = torch.searchsorted(times, stop[evm])
-    D0 = torch.zeros(m, dtype=X.dtype, device=X.device).index_add_(0, je, r[evm])
-    D1 = torch.zeros((m, P), dtype=X.dtype, device=X.device).index_add_(0, je, rx[evm])
-    dcnt = torch.bincount(je, minlength=m)
-    wsum = torch.zeros(m, dtype=X.dtype, device=X.device).index_add_(0, je, w[evm])
-    wbar = wsum / dcnt.clamp_min(1).to(X.dtype)
-    # Efron expansion: one entry per (time j, l < d_j)
-    jl = torch.repeat_interleave(torch.arange(m, device=X.device), dcnt)
-    start_of = torch.cumsum(dcnt, 0) - dcnt
-    l = torch.arange(jl.numel(), device=X.device) - start_of[jl]
-    frac = (l.to(X.dtype) / dcnt[jl].to(X.dtype)) if efron else torch.zeros(jl.numel(), dtype=X.dtype,
-                                                                             device=X.device)
-    R0l = R0[jl] - frac * D0[jl]
-    R1l = R1[jl] - frac.view(-1, 1) * D1[jl]
-    wl = wbar[jl]
-    ll = float((w[evm] * eta[evm]).sum() - (wl * torch.log(R0l)).sum())
-    grad = (w[evm].view(-1, 1) * X[evm]).sum(0) - ((wl / R0l).view(-1, 1) * R1l).sum(0)
-    # Hessian part 1: sum over (j,l) of wbar (R2 - frac D2) / R0l as per-row weights
-    c = wl / R0l
-    C = torch.zeros(m, dtype=X.dtype, device=X.device).index_add_(0, jl, c)
-    Cf = torch.zeros(m, dtype=X.dtype, device=X.device).index_add_(0, jl, c * frac)
-    Pc = torch.cat([torch.zeros(1, dtype=X.dtype, device=X.device), torch.cumsum(C, 0)])
-    a = torch.where(valid, Pc[jstop] - Pc[jstart], torch.zeros_like(r))
-    a_ev = torch.zeros_like(r)
-    a_ev[evm] = Cf[je]
-    a = r * (a - a_ev)
-    H1 = linalg_ops.weighted_gram(X.to(torch.float32), a.to(torch.float32)) if (
-        X.device.type == "cuda" and P % 32 == 0) else X.T @ (X * a.view(-1, 1))
-    H2 = R1l.T @ (R1l * (wl / (R0l * R0l)).view(-1, 1))
-    return ll, grad, H1.to(X.dtype) - H2
+    return _Stratum(X, start, stop, ev, w, efron).terms(beta)
 
 
 class H2OCoxProportionalHazardsEstimator(H2OEstimator):
@@ -152,12 +185,14 @@ class H2OCoxProportionalHazardsEstimator(H2OEstimator):
         lre = float(p.get("lre_min", 9.0))
         groups = [(strata == s) for s in us]
 
+        strat = [_Stratum(X[g], start[g] if start is not None else None, stop[g], ev[g], w[g], efron)
+                 for g in groups]
+
         def terms(b):
             L, G, H = 0.0, torch.zeros(P, dtype=torch.float64, device=X.device), \
                 torch.zeros((P, P), dtype=torch.float64, device=X.device)
-            for g in groups:
-                l_, g_, h_ = _stratum_terms(X[g], start[g] if start is not None else None, stop[g], ev[g], w[g], b,
-                                            efron)
+            for st in strat:
+                l_, g_, h_ = st.terms(b)
                 L += l_
                 G += g_
                 H += h_

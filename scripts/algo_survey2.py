@@ -65,11 +65,20 @@ cases = [
     ("xgboost_dart", lambda: E.H2OXGBoostEstimator(ntrees=30, booster="dart", seed=1), dict(x=x, y="y"), fr),
     ("kmeans_estimate_k", lambda: E.H2OKMeansEstimator(k=20, estimate_k=True, seed=1), dict(x=xs), fr),
 ]
+import signal  # noqa: E402
+
+
+def _alarm(signum, frame):
+    raise TimeoutError("case exceeded 150 s")
+
+
+signal.signal(signal.SIGALRM, _alarm)
 only = os.environ.get("ONLY")
 for name, mk, kw, data in cases:
     if only and name not in only.split(","):
         continue
     t0 = time.time()
+    signal.alarm(150)
     try:
         if name == "gbm_cv_se":
             b1 = E.H2OGradientBoostingEstimator(ntrees=20, nfolds=3, keep_cross_validation_predictions=True, seed=1)
@@ -87,3 +96,5 @@ for name, mk, kw, data in cases:
         print(json.dumps({"algo": name, "rows": data.nrows, "train_s": round(time.time() - t0, 2)}), flush=True)
     except Exception as e:  # keep surveying the rest
         print(json.dumps({"algo": name, "error": repr(e)[:300], "after_s": round(time.time() - t0, 2)}), flush=True)
+    finally:
+        signal.alarm(0)

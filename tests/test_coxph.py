@@ -95,3 +95,16 @@ def test_coxph_h2o_mojo_roundtrip(use_all, tmp_path):
         d32[c] = d32[c].astype(np.float32).astype(np.float64)
     theirs = mj.predict(d32)["lp"].values
     np.testing.assert_allclose(theirs, ours, atol=2e-5)
+
+
+def test_segmented_sums_match_index_add():
+    """_Seg (sort once, cumsum differences) == index_add_ into few bins."""
+    import torch
+    from h2o3_amd.models.coxph import _Seg
+    g = torch.Generator().manual_seed(0)
+    key = torch.randint(0, 7, (5000,), generator=g)
+    key[:100] = 0
+    v = torch.randn(5000, 3, generator=g, dtype=torch.float64)
+    ref = torch.zeros(9, 3, dtype=torch.float64).index_add_(0, key, v)
+    torch.testing.assert_close(_Seg(key, 9)(v), ref)
+    torch.testing.assert_close(_Seg(key, 9)(v[:, 0]), ref[:, 0])
