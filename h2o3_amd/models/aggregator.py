@@ -32,6 +32,47 @@ AGG_DEFAULTS = dict(target_num_exemplars=5000, rel_tol_num_exemplars=0.5, transf
                     seed=-1)
 
 
+def _leader(C: torch.Tensor, radius2: float, budget=None, block=1024):
+    """Sequential leader pass over candidate rows C (in order): a row becomes
+    an exemplar unless it lies within radius of an earlier accepted one.
+    Blocked: the distances to the exemplars accepted in earlier blocks are
+    one GPU matrix product, only the survivors of a block are resolved
+    sequentially against each other (their pairwise closeness precomputed
+    in f64).  Returns accepted positions into C."""
+    acc: list[int] = []
+    A = C[:0].to(torch.float64)
+    for s in range(0, C.shape[0], block):
+        cb = C[s:s + block].to(torch.float64)
+        if A.shape[0]:
+            d = (cb * cb).sum(1, keepdim=True) + (A * A).sum(1).view(1, -1) - 2 * cb @ A.T
+            fi = torch.nonzero(d.min(1).values > radius2).view(-1)
+        else:
+            fi = torch.arange(cb.shape[0], device=C.device)
+        if fi.numel() == 0:
+            continue
+        F = cb[fi]
+        nb = F.shape[0]
+        # in-block greedy as a fixed point: a row is accepted once every earlier
+        # close row is rejected, rejected once an earlier close row is accepted
+        L = (torch.cdist(F, F) ** 2 <= radius2) & torch.ones(nb, nb, dtype=torch.bool, device=C.device).tril(-1)
+        und = torch.ones(nb, dtype=torch.bool, device=C.device)
+        accd = torch.zeros_like(und)
+        while bool(und.any()):
+            live = und | accd
+            new_acc = und & ~(L & live.view(1, -1)).any(1)
+            new_rej = und & (L & accd.view(1, -1)).any(1)
+            accd |= new_acc
+            und &= ~(new_acc | new_rej)
+        keep = torch.nonzero(accd).view(-1)
+        if budget is not None and len(acc) + keep.numel() > budget:
+            keep = keep[:max(budget - len(acc) + 1, 0)]
+        acc.extend(int(s + t) for t in fi[keep].cpu().tolist())
+        A = torch.cat([A, F[keep]], 0)
+        if budget is not None and len(acc) > budget:
+            break
+    return acc
+
+
 def _exemplars(X: torch.Tensor, radius2: float, chunk=65536, max_ex=None):
     """Greedy leader clustering.  Returns (exemplar row indices, assignment)."""
     n = X.shape[0]
@@ -46,19 +87,9 @@ def _exemplars(X: torch.Tensor, radius2: float, chunk=65536, max_ex=None):
             far = torch.ones(xb.shape[0], dtype=torch.bool, device=X.device)
         cand = torch.nonzero(far).view(-1)
         if cand.numel():
-            C = xb[cand]
-            # sequential leader pass restricted to the candidates (small)
-            Ch = C.cpu().to(torch.float64).numpy()
-            new = []
-            for i in range(Ch.shape[0]):
-                if new:
-                    dd = ((Ch[new] - Ch[i]) ** 2).sum(1)
-                    if dd.min() <= radius2:
-                        continue
-                new.append(i)
-                if max_ex is not None and len(ex_idx) + len(new) > max_ex:
-                    break
-            sel = cand[torch.as_tensor(new, device=X.device)]
+            budget = None if max_ex is None else max_ex - sum(int(t.numel()) for t in ex_idx)
+            new = _leader(xb[cand], radius2, budget)
+            sel = cand[torch.as_tensor(new, device=X.device, dtype=torch.long)]
             ex_idx.append(sel + s)
             E = torch.cat([E, xb[sel]], 0)
             if max_ex is not None and E.shape[0] > max_ex:

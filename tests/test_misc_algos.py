@@ -90,3 +90,23 @@ def test_aggregator_reduces_rows():
     af = ag.aggregated_frame.as_data_frame()
     assert 50 <= len(af) <= 150
     assert int(af["counts"].sum()) == 6000
+
+
+def test_aggregator_blocked_leader_matches_sequential():
+    """_leader (blocked: GPU distances to earlier blocks' exemplars, pairwise
+    closeness within a block) picks exactly the exemplars of the plain
+    sequential leader pass."""
+    import numpy as np
+    import torch
+    from h2o3_amd.models.aggregator import _leader
+    g = torch.Generator().manual_seed(5)
+    C = torch.rand((3000, 4), generator=g, dtype=torch.float64)
+    r2 = 0.05
+    ref = []
+    Cn = C.numpy()
+    for i in range(Cn.shape[0]):
+        if ref and (((Cn[ref] - Cn[i]) ** 2).sum(1) <= r2).any():
+            continue
+        ref.append(i)
+    assert _leader(C, r2, block=256) == ref
+    assert _leader(C, r2, budget=10, block=64) == ref[:11]
