@@ -350,6 +350,65 @@ def register(app, route, ctx):
         return {"__meta": S.meta("FrameChunksV3", "Iced"), "frame_id": S.key(fid),
                 "chunks": [{"chunk_id": 0, "row_count": int(fr.nrows), "node_idx": 0}]}
 
+    # ------------------------------------------------------- assembly
+    assemblies: dict = {}
+
+    @route("POST", "/99/Assembly")
+    def assembly(p, r):
+        """AssemblyHandler: the client's munging steps, each
+        "name__Class__<Rapids AST over the frame 'dummy'>__inplace__newcols",
+        applied in order (water/rapids/Assembly.java, transforms/*)."""
+        import ast as _ast
+        import re
+        import uuid as _uuid
+        from ..core.rapids import rapids
+        steps = p.get("steps") or []
+        if isinstance(steps, str):
+            steps = _ast.literal_eval(steps)
+        fr = _frame(p.get("frame"), "frame")
+        cur = fr
+        done = []
+        for st in steps:
+            name, cls, expr, inplace, newcols = st.split("__", 4) if st.count("__") >= 4 else (st, "", "", "", "")
+            tmp = f"_asm_{_uuid.uuid4().hex[:12]}"
+            dkv.put(tmp, cur)
+            try:
+                res = rapids(re.sub(r"\bdummy\b", tmp, expr))
+            finally:
+                dkv.remove(tmp)
+            if cls == "H2OColSelect":
+                cur = res
+            else:
+                m = re.search(r"cols_py\s+dummy\s+'([^']+)'", expr) or re.search(r'cols_py\s+dummy\s+"([^"]+)"', expr)
+                col = m.group(1) if m else None
+                if str(inplace).lower() == "true" and col is not None:
+                    cur = cur.deep_copy(f"{fr.frame_id}_asm") if cur is fr else cur
+                    cur[col] = res
+                else:
+                    names = [n for n in newcols.split("|") if n]
+                    if names and len(names) == res.ncol:
+                        res.names = names
+                    cur = cur.cbind(res)
+            done.append((name, cls))
+        aid = f"Assembly_{_uuid.uuid4().hex[:16]}"
+        assemblies[aid] = {"steps": done, "frame": fr.frame_id}
+        rid = _put_frame(cur, f"{aid}_result")
+        return {"__meta": S.meta("AssemblyV99", "Iced", 99), "assembly": S.key(aid, "Assembly"),
+                "result": S.key(rid), "steps": steps, "frame": S.key(fr.frame_id)}
+
+    @route("GET", "/99/Assembly.java/{aid}/{pojo_name}")
+    def assembly_java(p, r, aid, pojo_name):
+        from fastapi.responses import PlainTextResponse
+        a = assemblies.get(aid)
+        if a is None:
+            raise _HTTPError(404, f"assembly {aid} not found")
+        lines = ["import hex.genmodel.GenMunger;", "import hex.genmodel.easy.RowData;", "",
+                 f"public class {pojo_name} extends GenMunger {{", f"  public {pojo_name}() {{",
+                 f"    _steps = new Step[{len(a['steps'])}];"]
+        lines += [f"    // step {i}: {n} ({c})" for i, (n, c) in enumerate(a["steps"])]
+        lines += ["  }", "}"]
+        return PlainTextResponse("\n".join(lines) + "\n")
+
     # ------------------------------------------------ frame utilities
     def _col(fr, spec):
         if isinstance(spec, dict):

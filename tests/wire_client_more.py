@@ -106,4 +106,17 @@ def sparse_upload():
     f = h2o.H2OFrame(m)
     return f.dim
 t("sparse_upload", sparse_upload)
+
+
+def assembly():
+    from h2o.assembly import H2OAssembly
+    from h2o.transforms.preprocessing import H2OColOp, H2OColSelect
+    asm = H2OAssembly(steps=[("select", H2OColSelect(["a", "b", "c"])),
+                             ("cos_a", H2OColOp(op=h2o.H2OFrame.cos, col="a", inplace=True)),
+                             ("cnt_c", H2OColOp(op=h2o.H2OFrame.countmatches, col="c", inplace=False, pattern="u"))])
+    out = asm.fit(fr)
+    got = out.as_data_frame()
+    assert abs(got["a"].values - np.cos(df.a.values)).max() < 1e-5 and out.ncols == 4
+    return out.dim
+t("assembly", assembly)
 print("SUMMARY " + json.dumps({"ok": len(ok), "bad": bad}))
