@@ -350,6 +350,19 @@ def register(app, route, ctx):
         return {"__meta": S.meta("FrameChunksV3", "Iced"), "frame_id": S.key(fid),
                 "chunks": [{"chunk_id": 0, "row_count": int(fr.nrows), "node_idx": 0}]}
 
+    @route("POST", "/3/ModelBuilders/{algo}/model_id")
+    def calc_model_id(p, r, algo):
+        """ModelBuildersHandler.calcModelId: a fresh unique model key."""
+        from .rest import _algo_cls
+        _algo_cls(algo)
+        return {"__meta": S.meta("ModelIdV3", "Iced"), "model_id": dkv.make_key(algo)}
+
+    @route("GET", "/99/Sample")
+    def sample(p, r):
+        """The reference's example experimental endpoint: cloud status."""
+        from ..parallel import cloud
+        return S.cloud_v3(cloud.info(), time.time() - ctx["uptime_ms"]() / 1000)
+
     # ------------------------------------------------------- assembly
     assemblies: dict = {}
 
