@@ -357,6 +357,13 @@ def register(app, route, ctx):
         _algo_cls(algo)
         return {"__meta": S.meta("ModelIdV3", "Iced"), "model_id": dkv.make_key(algo)}
 
+    @route("GET", "/99/Rapids/help")
+    def rapids_help(p, r):
+        """RapidsHandler.genHelp: the primitive names the interpreter knows."""
+        from ..core.rapids import PRIMS
+        return {"__meta": S.meta("RapidsHelpV3", "Iced", 99),
+                "syntax": [{"name": k, "pattern": f"({k} ...)", "description": ""} for k in sorted(PRIMS)]}
+
     @route("GET", "/99/Sample")
     def sample(p, r):
         """The reference's example experimental endpoint: cloud status."""
