@@ -649,3 +649,125 @@ def _append(dst, *pairs):
     return out
 
 
+
+
+# ---- model / utility prims the reference client sends over /99/Rapids
+# (water/rapids/ast/prims/models/*, advmath/AstMad, reducers/AstSumAxis,
+# time/AstMoment, misc/AstMillis, AstRename, hex/leaderboard AstMakeLeaderboard)
+def _frame_of_df(df):
+    return _F()(df)
+
+
+def _names_or_idx(fr, c):
+    if isinstance(c, (int, float)):
+        return fr.names[int(c)]
+    return str(c)
+
+
+def _perm_varimp(model, frame, metric="AUTO", n_samples=10000, n_repeats=1, features=None, seed=-1):
+    feats = None if features in (None, [], "") else [str(f) for f in (features if isinstance(features, list)
+                                                                       else [features])]
+    out = model.permutation_importance(frame, str(metric), int(n_samples), int(n_repeats), feats, int(seed))
+    return _frame_of_df(out.reset_index() if hasattr(out, "reset_index") and "Variable" not in out.columns else out)
+
+
+def _pva(model, frame, variable, predicted):
+    return _frame_of_df(model.predicted_vs_actual_by_variable(frame, predicted, str(variable), use_pandas=True))
+
+
+def _make_lb(models, lb_frame="", sort_metric="AUTO", extra_columns=None, scoring_data="AUTO"):
+    from ..automl.leaderboard import make_leaderboard
+    ids = models if isinstance(models, list) else [models]
+    objs = [dkv.get(str(m)) if isinstance(m, str) else m for m in ids]
+    lbf = dkv.get(lb_frame) if isinstance(lb_frame, str) and lb_frame else (lb_frame if _is_frame(lb_frame) else None)
+    ex = [str(e) for e in extra_columns] if isinstance(extra_columns, list) else \
+        ([] if extra_columns in (None, "") else [str(extra_columns)])
+    return make_leaderboard(objs, lbf, str(sort_metric), ex, str(scoring_data))
+
+
+def _sum_axis(fr, skipna=1.0, axis=0.0):
+    import torch as _t
+    from .vec import T_REAL, Vec
+    X = _t.stack([fr.vec(c).as_float(_t.float64) for c in fr.names], 1)
+    if bool(skipna):
+        X = _t.nan_to_num(X, nan=0.0)
+    if int(axis) == 1:
+        return _F().from_vecs([Vec(X.sum(1).to(_t.float32).contiguous(), T_REAL)], ["sum"])
+    from ..parallel import collectives as coll
+    s = X.sum(0)
+    coll.allreduce_(s)
+    return _F()(__import__("pandas").DataFrame({c: [float(v)] for c, v in zip(fr.names, s.tolist())}))
+
+
+def _reset_threshold(model, threshold):
+    """AstModelResetThreshold: the model's binomial threshold becomes
+    `threshold`; returns the old one."""
+    old = getattr(model, "_threshold_override", None)
+    if old is None:
+        tm = model._training_metrics
+        old = tm.get("max_f1_threshold") if tm is not None else None
+    model._threshold_override = float(threshold)
+    return _F()(__import__("pandas").DataFrame({"old_threshold": [float("nan") if old is None else float(old)]}))
+
+
+def _mad(fr, combine="interpolate", const=1.4826):
+    import torch as _t
+    x = fr.vec(fr.names[0]).as_float(_t.float64)
+    x = x[~_t.isnan(x)]
+    med = _t.quantile(x, 0.5) if x.numel() else _t.tensor(float("nan"))
+    return float(const) * float(_t.quantile((x - med).abs(), 0.5)) if x.numel() else float("nan")
+
+
+def _mode(fr):
+    import torch as _t
+    v = fr.vec(fr.names[0])
+    d = v.data.to(_t.int64)
+    d = d[d >= 0]
+    return float(_t.argmax(_t.bincount(d))) if d.numel() else float("nan")
+
+
+def _rename_key(old, new):
+    obj = dkv.get(str(old))
+    if obj is None:
+        raise RapidsError(f"rename: no key {old}")
+    dkv.put(str(new), obj)
+    dkv.remove(str(old))
+    if hasattr(obj, "frame_id"):
+        try:
+            obj.frame_id = str(new)
+        except AttributeError:
+            pass
+    return None
+
+
+def _tf_idf(fr, doc_col, text_col, preprocess=1.0, case_sensitive=1.0):
+    from ..information_retrieval import tf_idf
+    return tf_idf(fr, _names_or_idx(fr, doc_col), _names_or_idx(fr, text_col), bool(preprocess), bool(case_sensitive))
+
+
+def _moment(*parts):
+    from .frame import H2OFrame
+    keys = ("year", "month", "day", "hour", "minute", "second", "msec")
+    return H2OFrame.moment(**{k: v for k, v in zip(keys, parts) if v is not None})
+
+
+PRIMS.update({
+    "PermutationVarImp": _perm_varimp,
+    "predicted.vs.actual.by.var": _pva,
+    "makeLeaderboard": _make_lb,
+    "sumaxis": _sum_axis,
+    "model.reset.threshold": _reset_threshold,
+    "rulefit.predict.rules": lambda m, fr, ids: m.predict_rules(fr, [str(i) for i in (ids if isinstance(ids, list)
+                                                                                       else [ids])]),
+    "tf-idf": _tf_idf,
+    "word2vec.to.frame": lambda m: m.to_frame(),
+    "tree.update.weights": lambda m, fr, w: (m.update_tree_weights(fr, str(w)), 0.0)[1],
+    "segment_models_as_frame": lambda s: s.as_frame(),
+    "transform": lambda m, fr: m.transform_frame(fr),
+    "result": lambda m: m.result(),
+    "moment": _moment,
+    "h2o.mad": _mad,
+    "mode": _mode,
+    "millis": lambda: float(int(__import__("time").time() * 1000)),
+    "rename": _rename_key,
+})

@@ -492,7 +492,7 @@ class H2OEstimator:
         spec = spec or self._spec
         if spec.nclasses == 2:
             p1 = raw[:, -1]
-            thr = threshold
+            thr = threshold if threshold is not None else getattr(self, "_threshold_override", None)
             if thr is None:
                 tm = self._training_metrics
                 thr = tm["max_f1_threshold"] if tm is not None and tm.get("max_f1_threshold") is not None else \

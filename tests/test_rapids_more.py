@@ -1,0 +1,46 @@
+"""Rapids prims the reference client sends for model utilities
+(PermutationVarImp, makeLeaderboard, model.reset.threshold, sumaxis,
+h2o.mad, mode, rename, millis) -- checked against numpy / the in-process
+API."""
+import numpy as np
+import pandas as pd
+
+import h2o3_amd as h2o
+from h2o3_amd.core import dkv
+from h2o3_amd.core.frame import H2OFrame
+from h2o3_amd.core.rapids import rapids
+from h2o3_amd.estimators import H2OGradientBoostingEstimator
+
+
+def test_model_and_reducer_prims():
+    h2o.init()
+    rng = np.random.default_rng(0)
+    n = 300
+    df = pd.DataFrame({"a": rng.normal(size=n), "b": rng.normal(size=n), "c": rng.choice(list("xyz"), n)})
+    df["y"] = np.where(df.a + df.b > 0, "p", "n")
+    fr = H2OFrame(df)
+    fr["c"] = fr["c"].asfactor()
+    fr["y"] = fr["y"].asfactor()
+    dkv.put("rp.hex", fr)
+    m = H2OGradientBoostingEstimator(ntrees=3, model_id="rp_gbm", seed=1)
+    m.train(x=["a", "b", "c"], y="y", training_frame=fr)
+    dkv.put("rp_gbm", m)
+    pvi = rapids('(PermutationVarImp rp_gbm rp.hex "AUTO" 1000 1 [] 1)')
+    assert pvi.nrow == 3
+    rs = rapids("(sumaxis (cols rp.hex [0 1]) 1 1)").as_data_frame().iloc[:, 0].values
+    np.testing.assert_allclose(rs, df.a + df.b, rtol=1e-5, atol=1e-5)
+    cs = rapids("(sumaxis (cols rp.hex [0 1]) 1 0)").as_data_frame().values[0]
+    np.testing.assert_allclose(cs, [df.a.sum(), df.b.sum()], rtol=1e-5)
+    old = rapids("(model.reset.threshold rp_gbm 0.99)").as_data_frame().values[0, 0]
+    assert 0 < old < 1
+    p = m.predict(fr).as_data_frame()
+    assert (p["predict"] == np.where(p["p"] >= 0.99, "p", "n")).all()
+    x = df.a.values
+    np.testing.assert_allclose(rapids('(h2o.mad (cols rp.hex [0]) "interpolate" 1.4826)'),
+                               1.4826 * np.median(np.abs(x - np.median(x))), rtol=1e-4)
+    assert rapids("(mode (cols rp.hex [2]))") == float(np.argmax(np.bincount(pd.Categorical(df.c).codes)))
+    lb = rapids('(makeLeaderboard ["rp_gbm"] "rp.hex" "AUTO" [] "AUTO")')
+    assert lb.nrow == 1
+    rapids('(rename "rp.hex" "rp2.hex")')
+    assert dkv.get("rp2.hex") is not None and dkv.get("rp.hex") is None
+    assert rapids("(millis)") > 1.6e12
