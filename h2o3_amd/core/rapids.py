@@ -771,3 +771,36 @@ PRIMS.update({
     "millis": lambda: float(int(__import__("time").time() * 1000)),
     "rename": _rename_key,
 })
+
+
+def _perfect_auc(probs, actuals):
+    """AstPerfectAUC: exact (tie-averaged) AUC of a probability column
+    against 0/1 actuals."""
+    import torch as _t
+    from ..models.metrics import _auc_exact
+    p = probs.vec(probs.names[0]).as_float(_t.float64)
+    a = actuals.vec(actuals.names[0])
+    y = a.data.to(_t.float64) if a.type == "enum" else a.as_float(_t.float64)
+    ok = ~_t.isnan(p) & ~_t.isnan(y)
+    return float(_auc_exact(p[ok], y[ok], _t.ones_like(p[ok]))[0])
+
+
+def _ddply(fr, cols, fun):
+    """AstDdply: fun applied to the rows of each group of `cols` -> one row
+    per group: the group keys, then the function's value(s)."""
+    import pandas as pd
+    g = fr.gather()
+    keys = [g.names[int(c)] if isinstance(c, (int, float)) else str(c) for c in (cols if isinstance(cols, list)
+                                                                              else [cols])]
+    df = g[keys].as_data_frame()
+    out = []
+    for kv, idx in df.groupby(keys, sort=True, dropna=False).indices.items():
+        sub = g[[int(i) for i in idx], :]
+        v = call(fun, [sub])
+        vals = v.as_data_frame().iloc[0].tolist() if _is_frame(v) else [float(v)]
+        out.append(list(kv if isinstance(kv, tuple) else (kv,)) + vals)
+    ncol = max((len(r) for r in out), default=len(keys) + 1)
+    return _F()(pd.DataFrame(out, columns=keys + [f"ddply_C{j + 1}" for j in range(ncol - len(keys))]))
+
+
+PRIMS.update({"perfectAUC": _perfect_auc, "ddply": _ddply})

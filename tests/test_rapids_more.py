@@ -44,3 +44,19 @@ def test_model_and_reducer_prims():
     rapids('(rename "rp.hex" "rp2.hex")')
     assert dkv.get("rp2.hex") is not None and dkv.get("rp.hex") is None
     assert rapids("(millis)") > 1.6e12
+
+
+def test_perfect_auc_and_ddply():
+    from sklearn.metrics import roc_auc_score
+    h2o.init()
+    rng = np.random.default_rng(1)
+    n = 200
+    df = pd.DataFrame({"p": rng.random(n), "y": rng.integers(0, 2, n), "g": rng.choice(list("ab"), n),
+                       "v": rng.normal(size=n)})
+    fr = H2OFrame(df)
+    fr["g"] = fr["g"].asfactor()
+    dkv.put("dd.hex", fr)
+    np.testing.assert_allclose(rapids("(perfectAUC (cols dd.hex [0]) (cols dd.hex [1]))"),
+                               roc_auc_score(df.y, df.p), rtol=1e-9)
+    out = rapids("(ddply dd.hex [2] { x . (mean (cols x 3) 1 0) })").as_data_frame()
+    np.testing.assert_allclose(out["ddply_C1"].values, df.groupby("g").v.mean().values, rtol=1e-5)
