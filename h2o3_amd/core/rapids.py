@@ -804,3 +804,40 @@ def _ddply(fr, cols, fun):
 
 
 PRIMS.update({"perfectAUC": _perfect_auc, "ddply": _ddply})
+
+
+def _pav(fr):
+    """AstPoolAdjacentViolators: frame (y, X, weights) -> the isotonic fit's
+    thresholds (y, X) (hex/isotonic/PoolAdjacentViolatorsDriver.runPAV)."""
+    import pandas as pd
+    from ..models.isotonic import H2OIsotonicRegressionEstimator
+    if fr.ncols != 3:
+        raise RapidsError("Input frame is expected to have 3 columns: y, X, weights.")
+    y, x, w = fr.names
+    m = H2OIsotonicRegressionEstimator(weights_column=w)
+    m.train(x=[x], y=y, training_frame=fr)
+    return _F()(pd.DataFrame({y: m._ty, x: m._tx}))
+
+
+def _grouped_permute(fr, perm_col, group_by, permute_by, keep_col):
+    """AstGroupedPermute: within each group, every row whose permute_by
+    level is 0 paired with every row whose level is 1 -> (group keys,
+    In = keep value of the first, Out = keep value of the second, InAmnt,
+    OutAmnt = their perm_col values)."""
+    import pandas as pd
+    g = fr.gather().as_data_frame()
+    names = list(g.columns)
+    gb = [names[int(c)] for c in (group_by if isinstance(group_by, list) else [group_by])]
+    pc, pb, kc = names[int(perm_col)], names[int(permute_by)], names[int(keep_col)]
+    levels = sorted(g[pb].dropna().unique())
+    rows = []
+    for key, sub in g.groupby(gb, sort=True):
+        a = sub[sub[pb] == levels[0]] if levels else sub.iloc[:0]
+        b = sub[sub[pb] == levels[1]] if len(levels) > 1 else sub.iloc[:0]
+        for _, ra in a.iterrows():
+            for _, rb in b.iterrows():
+                rows.append(list(key if isinstance(key, tuple) else (key,)) + [ra[kc], rb[kc], ra[pc], rb[pc]])
+    return _F()(pd.DataFrame(rows, columns=gb + ["In", "Out", "InAmnt", "OutAmnt"]))
+
+
+PRIMS.update({"isotonic.pav": _pav, "grouped_permute": _grouped_permute})

@@ -60,3 +60,17 @@ def test_perfect_auc_and_ddply():
                                roc_auc_score(df.y, df.p), rtol=1e-9)
     out = rapids("(ddply dd.hex [2] { x . (mean (cols x 3) 1 0) })").as_data_frame()
     np.testing.assert_allclose(out["ddply_C1"].values, df.groupby("g").v.mean().values, rtol=1e-5)
+
+
+def test_isotonic_pav_and_grouped_permute():
+    h2o.init()
+    rng = np.random.default_rng(2)
+    n = 100
+    x = rng.random(n)
+    dkv.put("pav.hex", H2OFrame(pd.DataFrame({"y": x + rng.normal(size=n) * 0.1, "x": x, "w": np.ones(n)})))
+    out = rapids("(isotonic.pav pav.hex)").as_data_frame()
+    assert (np.diff(out["y"].values) >= -1e-12).all() and (np.diff(out["x"].values) >= 0).all()
+    df = pd.DataFrame({"g": [1, 1, 1, 2, 2], "side": [0, 1, 1, 0, 1], "amt": [5.0, 6, 7, 8, 9], "id": [10, 11, 12, 13, 14]})
+    dkv.put("gp.hex", H2OFrame(df))
+    gp = rapids("(grouped_permute gp.hex 2 [0] 1 3)").as_data_frame()
+    assert len(gp) == 2 + 1 and list(gp.columns) == ["g", "In", "Out", "InAmnt", "OutAmnt"]
