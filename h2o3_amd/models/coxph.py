@@ -37,20 +37,24 @@ COX_DEFAULTS = dict(start_column=None, stop_column=None, stratify_by=None, ties=
 
 class _Seg:
     """Segmented sums by a fixed integer key: rows sorted by key once, each
-    sum is a cumulative sum over the sorted values differenced at the key
-    boundaries.  Replaces index_add_ into few bins (every row of a stratum
-    without a start column lands in bin 0: a million f64 atomics on one
-    address serialise)."""
+    sum a direct segmented reduction over the sorted values (no differencing
+    of a global prefix sum: r = w e^eta spans many orders of magnitude, and a
+    small per-event-time sum would cancel against the running total).
+    Replaces index_add_ into few bins (every row of a stratum without a start
+    column lands in bin 0: a million f64 atomics on one address serialise)."""
 
     def __init__(self, key, m):
         self.order = torch.argsort(key, stable=True)
         ks = key[self.order]
-        self.bounds = torch.searchsorted(ks, torch.arange(m + 1, device=key.device, dtype=ks.dtype))
+        bounds = torch.searchsorted(ks, torch.arange(m + 1, device=key.device, dtype=ks.dtype))
+        self.lengths = (bounds[1:] - bounds[:-1]).to(torch.int64)
+        self.m = m
 
     def __call__(self, v):
-        cs = torch.cumsum(v[self.order], 0)
-        cs = torch.cat([torch.zeros_like(cs[:1]), cs], 0)
-        return cs[self.bounds[1:]] - cs[self.bounds[:-1]]
+        vs = v[self.order]
+        if vs.shape[0] == 0:
+            return torch.zeros((self.m,) + tuple(v.shape[1:]), dtype=v.dtype, device=v.device)
+        return torch.segment_reduce(vs, "sum", lengths=self.lengths, axis=0, unsafe=True, initial=0.0)
 
 
 class _Stratum:

@@ -1475,7 +1475,7 @@ class TreeGrower:
         """Queue a device->host copy of t into a reusable pinned slot; returns
         (host view, event).  CPU tensors pass through."""
         if t.device.type != "cuda":
-            return (t, None)
+            return (t, None, 0)
         ring = self.__dict__.setdefault("_d2h_ring", [None, None])
         k = self.__dict__.get("_d2h_k", 0)
         self._d2h_k = k ^ 1
@@ -1490,14 +1490,15 @@ class TreeGrower:
             evs[k] = torch.cuda.Event()
         st = getattr(self, "_stream_obj", None)
         evs[k].record(st if st is not None else torch.cuda.current_stream())
-        return (h, evs[k])
+        # uploads staged after this record (the look-ahead) are NOT covered
+        return (h, evs[k], tree_ops.upload_mark())
 
     @staticmethod
     def _d2h_wait(hev):
-        h, ev = hev
+        h, ev = hev[0], hev[1]
         if ev is not None:
             ev.synchronize()
-            tree_ops.host_synced()   # every copy queued before the record has completed
+            tree_ops.host_synced(hev[2])   # every upload queued before the record has completed
         return h.numpy().copy()
 
     def _maybe_lookahead(self, rec, cols, f_st, f_ct, mode, va, vb, ridx_next, H, wyy_level, depth, level_bytes,

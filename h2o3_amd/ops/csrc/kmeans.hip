@@ -399,7 +399,9 @@ __global__ __launch_bounds__(KMS_THREADS) void kmeans_sums_kernel(
       const int e = tid + h * KMS_THREADS;
       if (e < 2 * k) { wacc[h] += (double)Swt[e]; Swt[e] = 0.f; }
     }
-    // the next tile's row stats are added only after its first barrier
+    // Swt/Sss entries are owned by every wave (2k may exceed 64): wave 0 must
+    // not lds_add the next tile's row stats before all waves folded + zeroed
+    __syncthreads();
   }
   __syncthreads();
   double* o = part + (long long)blockIdx.x * km_part_stride(k, P);

@@ -714,8 +714,9 @@ __global__ __launch_bounds__(256) void hist_bm_reduce_kernel(
   const int i1 = min(nw, i0 + BM_RED);
   const int g = blockIdx.y;
   const int PITCH = G * CL;
-  const int nbt = Bs / 16;
+  const int nbt = (Bs + 15) / 16;   // Bs % 16 may be 4, 8 or 12 (few-bin frames)
   const int b = (blockIdx.x % nbt) * 16 + (threadIdx.x >> 4);
+  if (b >= Bs) return;               // no barriers below: idle lanes of a partial tile leave
   const int sl = (blockIdx.x / nbt) * 16 + (threadIdx.x & 15);
   const int ch = sl / G, slot = sl - ch * G;
   const int fg0 = foff + g * G;
@@ -789,7 +790,7 @@ extern "C" int h2o_hist_bm(const void* codes, int Fp, const int* ridx, const flo
   const int lw = (lw_env == 1 || G == 16) ? 1 : 2;   // as lbm() picks it
   const int nk = 4 * lw, lpr = G / nk;
   const int C = mode == 2 ? 1 : 2;
-  dim3 rg((Bs / 16) * (G * CL / 16), n_fg, (n_work + BM_RED - 1) / BM_RED);
+  dim3 rg(((Bs + 15) / 16) * (G * CL / 16), n_fg, (n_work + BM_RED - 1) / BM_RED);
   hipLaunchKernelGGL(hist_bm_reduce_kernel, rg, dim3(256), 0, s, part, (const int4*)work, n_work, n_work_dev, n_fg,
                      F, foff, G, CL, lpr, nk, Bs, C, pack ? 1 : 0, pack_bq, s0, s1, need, hist, n_slots);
   return (int)hipGetLastError();

@@ -22,40 +22,56 @@ _c_ll = ctypes.c_longlong
 
 
 
-# Host-synchronisation epoch: bumped whenever the host has waited for the
-# stream to drain (host_synced()), so a staging slot written before the last
-# bump is known to be consumed -- no per-upload event record / query.
-_sync_epoch = 0
+# Upload sequence numbers: every staged upload gets the next number; the
+# host learns that all uploads numbered below `_synced_upto` have completed
+# when it waits on an event recorded after them on the same stream
+# (host_synced(mark) with mark = upload_mark() taken at the record), so a
+# staging slot is rewritten without a stream sync once its upload is below
+# the mark -- no per-upload event record / query.
+_upload_seq = 0
+_synced_upto = 0
 
 
-def host_synced():
-    """Tell the upload ring that every copy queued so far has completed (the
-    caller just waited on an event recorded after them, on the same stream)."""
-    global _sync_epoch
-    _sync_epoch += 1
+def upload_mark():
+    """Sequence number of the next upload: record it together with an event;
+    every upload before it is complete once the event is."""
+    return _upload_seq
+
+
+def host_synced(mark=None):
+    """Tell the upload ring that every copy queued before `mark` (an
+    upload_mark() taken when the waited-on event was recorded) has completed;
+    mark=None: the caller drained the whole stream."""
+    global _synced_upto
+    m = _upload_seq if mark is None else mark
+    if m > _synced_upto:
+        _synced_upto = m
 
 
 class _PinnedRing:
     """Reusable staging for the small per-level host->device uploads (work
     items, per-chunk metadata, column masks): pinned host slots and device
     slots, both reused.  A copy from a pinned slot is truly asynchronous; a
-    slot is only rewritten after the host has synchronised with the stream
-    since its last use (else it synchronises first), so no pending copy ever
-    reads overwritten bytes.  Device slots are consumed by kernels queued
-    after the copy on the same stream, and a later copy into the slot is
-    queued behind them: stream order keeps them intact.  (Per-upload events
-    and device allocations cost ~30 us of host time per upload.)"""
+    slot is only rewritten once its previous upload is known complete
+    (sequence number below the synced mark), else the host synchronises
+    first, so no pending copy ever reads overwritten bytes.  Device slots are
+    consumed by kernels queued after the copy on the same stream, and a later
+    copy into the slot is queued behind them: stream order keeps them intact.
+    A returned device tensor ALIASES its slot: it must be consumed (by work
+    queued on the stream) before len(ring) further uploads.  (Per-upload
+    events and device allocations cost ~30 us of host time per upload.)"""
 
     def __init__(self, n=16):
         self.bufs = [None] * n
         self.dbufs = [None] * n
-        self.epoch = [-1] * n
+        self.seq = [-1] * n
         self.i = 0
 
     def upload(self, a: np.ndarray, dev):
+        global _upload_seq
         k = self.i
         self.i = (self.i + 1) % len(self.bufs)
-        if self.epoch[k] == _sync_epoch:
+        if self.seq[k] >= _synced_upto:
             torch.cuda.current_stream(dev).synchronize()
             host_synced()
         nb = max(a.nbytes, 8)
@@ -72,7 +88,8 @@ class _PinnedRing:
         stage.numpy()[...] = a
         out = dbuf[:a.nbytes].view(tdt).view(a.shape)
         out.copy_(stage, non_blocking=True)
-        self.epoch[k] = _sync_epoch
+        self.seq[k] = _upload_seq
+        _upload_seq += 1
         return out
 
 

@@ -283,7 +283,7 @@ def test_lloyd_kernel_large_n_f64_accumulation(fx):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("N,P,k", [(200_003, 100, 64), (50_001, 36, 130), (9_999, 8, 3)])
+@pytest.mark.parametrize("N,P,k", [(200_003, 100, 64), (50_001, 36, 130), (9_999, 8, 3), (400_001, 16, 128)])
 def test_lloyd_split_path_matches_fused(N, P, k, monkeypatch):
     """Large-k split path (assignment pass + kmeans_sums_kernel) vs the fused
     kernel: same assignment / distances, same f64 statistics (both 64-bit

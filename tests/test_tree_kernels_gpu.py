@@ -745,3 +745,54 @@ def test_gbm_same_model_bm_and_quad(monkeypatch):
         out[flag] = (m.logloss(), [list(t.feat) for t in m._forest.trees])
     assert abs(out["1"][0] - out["0"][0]) < 1e-5
     assert out["1"][1] == out["0"][1]
+
+
+@pytest.mark.parametrize("nbins", [2, 4, 6, 12])
+@pytest.mark.parametrize("mode,pack", [(0, True), (0, False), (2, False)])
+def test_hist_bm_few_bins_matches_reference(nbins, mode, pack, monkeypatch):
+    """Few-bin frames give a bin stride Bs that is not a multiple of 16 (8 for
+    <= 7 bins): the two-pass reduce must cover the partial 16-bin tile."""
+    _need_gpu()
+    monkeypatch.setenv("H2O3_HIST_BM", "1")
+    from h2o3_amd.ops import tree_ops
+    bd, _ = _binned(n=30000, F=40, nbins=nbins, cats=False)
+    assert bd.Bs % 4 == 0
+    n = bd.nrows_local
+    g = torch.Generator(device="cuda").manual_seed(nbins)
+    ridx = torch.randperm(n, generator=g, device="cuda").to(torch.int32)
+    va = torch.randn(n, generator=g, device="cuda")
+    vb = (torch.rand(n, generator=g, device="cuda") < 0.7).to(torch.float32) if pack else \
+        torch.rand(n, generator=g, device="cuda")
+    starts, counts = [0, 9000, 21000], [9000, 12000, 9000]
+    vmax = tree_ops.channel_max(va, vb, mode)
+    h_gpu = tree_ops.hist_build(bd, ridx, va, vb, mode, starts, counts, 3, use_native=True, unit_w=pack, vmax=vmax)
+    h_ref = tree_ops.hist_build(bd, ridx, va, vb, mode, starts, counts, 3, use_native=False)
+    torch.testing.assert_close(h_gpu, h_ref, rtol=1e-5, atol=1e-4)
+
+
+def test_gbm_all_binary_frame_gpu_matches_cpu():
+    """GBM on a frame of 0/1 features only (Bs = 8): the GPU model equals the
+    CPU (torch reference) model."""
+    _need_gpu()
+    import pandas as pd
+    import h2o3_amd as h2o
+    from h2o3_amd.estimators import H2OGradientBoostingEstimator
+    rng = np.random.RandomState(11)
+    n, F = 40000, 24
+    X = (rng.rand(n, F) < 0.4).astype(np.float32)
+    y = ((X[:, 0] + X[:, 1] * X[:, 2] + 0.3 * rng.randn(n)) > 0.6).astype(int)
+    df = pd.DataFrame(X, columns=[f"b{i}" for i in range(F)])
+    df["y"] = np.where(y == 1, "a", "b")
+    from h2o3_amd.parallel import cloud
+    out = {}
+    for dev in ("cuda:0", "cpu"):
+        cloud.shutdown()
+        h2o.init(device=dev, verbose=False)
+        fr = h2o.H2OFrame(df)
+        m = H2OGradientBoostingEstimator(ntrees=5, max_depth=5, seed=3)
+        m.train(y="y", training_frame=fr)
+        out[dev] = (m.logloss(), [list(t.feat) for t in m._forest.trees])
+    cloud.shutdown()
+    h2o.init(device="cuda:0", verbose=False)
+    assert out["cuda:0"][1] == out["cpu"][1]
+    assert abs(out["cuda:0"][0] - out["cpu"][0]) < 1e-5
