@@ -22,7 +22,8 @@ import torch
 import torch.distributed as dist
 
 _state = {"initialized": False, "device": None, "rank": 0, "world": 1, "local_rank": 0,
-          "backend": None, "start": time.time(), "owns_pg": False, "name": None, "failed": False}
+          "backend": None, "start": time.time(), "owns_pg": False, "name": None, "failed": False,
+          "ctl": None, "healthy": True, "dead": [], "hb": None}
 
 
 def _mark_failed_hook(prev):
@@ -71,8 +72,16 @@ def init(device: str | None = None, backend: str | None = None, timeout_s: float
     if dist.is_initialized():
         rank, world = dist.get_rank(), dist.get_world_size()
         _state["backend"] = dist.get_backend()
+        # control plane: host-side decisions / commands travel on a gloo group
+        # (the data plane is RCCL on GPU clouds; a CPU broadcast there would
+        # need a device round trip)
+        _state["ctl"] = None if dist.get_backend() == "gloo" else dist.new_group(
+            backend="gloo", timeout=datetime.timedelta(seconds=timeout_s))
     _state.update(initialized=True, device=dev, rank=rank, world=world, local_rank=local_rank,
-                  name=name or f"h2o3_amd_{os.getpid()}")
+                  name=name or f"h2o3_amd_{os.getpid()}", healthy=True, dead=[])
+    if world > 1 and dist.is_initialized() and os.environ.get("H2O3_HEARTBEAT", "1") != "0":
+        from . import heartbeat
+        _state["hb"] = heartbeat.start()
     return info()
 
 
@@ -105,6 +114,47 @@ def is_gpu() -> bool:
     return device().type == "cuda"
 
 
+def ctl_group():
+    """The gloo group for host-side control traffic (None = the default group)."""
+    return _state["ctl"]
+
+
+def agree(values, src: int = 0) -> list:
+    """Every rank returns rank `src`'s values (a short list of numbers): the
+    per-iteration decisions that depend on one host's clock or on a REST
+    cancel request (scoring schedule, max_runtime_secs, job cancel) must be
+    taken identically on every rank, or the SPMD collective sequence splits."""
+    vals = [float(v) for v in values]
+    if not is_distributed():
+        return vals
+    t = torch.tensor(vals, dtype=torch.float64)
+    dist.broadcast(t, src, group=_state["ctl"])
+    return t.tolist()
+
+
+def broadcast_obj(obj, src: int = 0):
+    """Broadcast a picklable host object from `src` on the control group."""
+    if not is_distributed():
+        return obj
+    lst = [obj]
+    dist.broadcast_object_list(lst, src=src, group=_state["ctl"])
+    return lst[0]
+
+
+def healthy() -> bool:
+    return bool(_state["healthy"])
+
+
+def dead_ranks() -> list:
+    return list(_state["dead"])
+
+
+def mark_unhealthy(dead):
+    """Heartbeat verdict: ranks that stopped beating (parallel/heartbeat.py)."""
+    _state["healthy"] = False
+    _state["dead"] = sorted(set(_state["dead"]) | set(dead))
+
+
 def info() -> dict:
     d = _state["device"]
     props = None
@@ -115,7 +165,8 @@ def info() -> dict:
                  "arch": getattr(p, "gcnArchName", None)}
     return {"cloud_name": _state["name"], "rank": _state["rank"], "cloud_size": _state["world"],
             "device": str(d), "backend": _state["backend"], "gpu": props,
-            "uptime_s": round(time.time() - _state["start"], 1), "host": socket.gethostname()}
+            "uptime_s": round(time.time() - _state["start"], 1), "host": socket.gethostname(),
+            "healthy": _state["healthy"], "dead_ranks": list(_state["dead"])}
 
 
 def shutdown(clean: bool = True, barrier_timeout_s: float = 60.0):
@@ -128,6 +179,10 @@ def shutdown(clean: bool = True, barrier_timeout_s: float = 60.0):
     failed): no barrier -- it could pair with a peer's pending collective --
     just drop the group so the process exits and its peers' collectives fail
     fast on the broken connection."""
+    hb = _state.get("hb")
+    if hb is not None:
+        hb.stop()
+        _state["hb"] = None
     if _state["owns_pg"] and dist.is_initialized():
         if clean:
             try:
@@ -141,7 +196,7 @@ def shutdown(clean: bool = True, barrier_timeout_s: float = 60.0):
             dist.destroy_process_group()
         except Exception:
             pass
-    _state.update(initialized=False, owns_pg=False)
+    _state.update(initialized=False, owns_pg=False, ctl=None)
 
 
 def _atexit_shutdown():

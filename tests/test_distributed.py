@@ -106,3 +106,34 @@ def test_failed_rank_exits_fast():
     assert procs[1].returncode != 0 and "simulated failure" in outs[1]
     assert procs[0].returncode != 0 and "unexpected" not in outs[0]
     assert time.time() - t0 < 200
+
+
+def test_heartbeat_reports_hung_rank():
+    """A frozen rank (SIGSTOP: its connections stay open, so the collective
+    never errors) is named by the survivor's heartbeat within the suspect
+    window, and the survivor leaves its pending collective with status 3
+    instead of waiting out the 1800 s collective timeout
+    (water/HeartBeatThread.java TIMEOUT)."""
+    import signal
+    import time
+    port = _free_port()
+    procs = []
+    t0 = time.time()
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), CUDA_VISIBLE_DEVICES="", OMP_NUM_THREADS="1", H2O3_HB_INTERVAL="1",
+                   H2O3_HB_SUSPECT="8")
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "dist_hang_worker.py")], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+    try:
+        o0, _ = procs[0].communicate(timeout=90)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(signal.SIGKILL)
+                p.wait()
+    out = o0.decode(errors="replace")
+    assert procs[0].returncode == 3, out[-2000:]
+    assert "rank(s) [1] missed heartbeats" in out, out[-2000:]
+    assert "unexpected" not in out
+    assert time.time() - t0 < 90
