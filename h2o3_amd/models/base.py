@@ -129,6 +129,10 @@ class ScoreSchedule:
         return (now - self.first < self.init_ms) or \
             (since > self.score_ms and (self.last_end - self.last_start) / max(since, 1e-9) < 0.1)
 
+    def clock_dependent(self):
+        """True when due() reads the wall clock (ranks could disagree)."""
+        return self.time_based and not self.each and self.interval <= 0
+
     def started(self):
         import time as _t
         self.last_start = _t.time() * 1000.0
@@ -285,9 +289,12 @@ class H2OEstimator:
                 validation_frame[y] = validation_frame[y].asfactor()
         self._start_time = int(time.time() * 1000)
         t0 = time.time()
-        from ..core.job import Job
+        from ..core import job as _jobmod
         from ..utils import log as _log
-        self._job = Job(f"{self.algo} model build", dest=self._id).start()
+        pend = _jobmod.take_pending()
+        self._job = (pend or _jobmod.Job(f"{self.algo} model build", dest=self._id,
+                                         parent=_jobmod.current())).start()
+        _jobmod.push(self._job)
         _log.event("model_build_start", algo=self.algo, model_id=self._id)
         spec = TrainSpec(training_frame, x, y, p.get("weights_column"), p.get("offset_column"),
                          p.get("fold_column"), validation_frame)
@@ -312,6 +319,8 @@ class H2OEstimator:
             self._job.fail(e)
             _log.event("model_build_failed", algo=self.algo, model_id=self._id, error=str(e))
             raise
+        finally:
+            _jobmod.pop(self._job)
         self._job.done()
         _log.event("model_build_done", algo=self.algo, model_id=self._id, secs=round(time.time() - t0, 3))
         self._run_time = time.time() - t0
@@ -321,6 +330,32 @@ class H2OEstimator:
 
     def _check_response(self, frame, y):
         pass
+
+    def _tick(self, it, total, sched=None, final=False, t0=None, max_rt=0.0, msg=None, deadline=None):
+        """Per-iteration control point of an iterative builder (trees, epochs,
+        IRLS / Lloyd iterations): job progress + cancellation
+        (water/Job.java:206 update, :isStopping), and the decisions that hang
+        on one host's clock -- is a scoring round due (ScoreSchedule), has
+        max_runtime_secs run out -- taken as rank 0 takes them, so every rank
+        scores and stops at the same iteration and the collective sequence
+        stays aligned.  Returns (score_now, timed_out)."""
+        timed_out = bool(max_rt and max_rt > 0 and t0 is not None and time.time() - t0 > max_rt)
+        if deadline is not None:
+            timed_out = timed_out or time.time() > deadline
+            max_rt = max_rt or 1.0
+        score = sched.due(it, final=final or timed_out) if sched is not None else False
+        job = getattr(self, "_job", None)
+        dist_ = cloud.is_distributed()
+        need = dist_ and (bool(max_rt and max_rt > 0) or (sched is not None and sched.clock_dependent()))
+        if job is None:
+            if need:
+                score, timed_out = (bool(v) for v in cloud.agree([score, timed_out]))
+            return score, timed_out
+        vals = job.tick(it / max(total, 1), msg=msg, extra=(score, timed_out) if (need or
+                                                                            (dist_ and job._spmd_any())) else ())
+        if vals:
+            score, timed_out = bool(vals[0]), bool(vals[1])
+        return score, timed_out
 
     def _wants_categorical_response(self):
         """Family/distribution implies classification (reference converts the

@@ -330,6 +330,7 @@ class H2ODeepLearningEstimator(H2OEstimator):
         samples_done = 0.0
         next_score = per_iter
         it = 0
+        nstep = 0
         graph = self._step_graph(X, Y, w, hp, avg_act) if self._graph_ok(X, hp, avg_act) else None
         while samples_done < total_samples:
             if pos + bs > n:
@@ -368,8 +369,13 @@ class H2ODeepLearningEstimator(H2OEstimator):
                                                               float(p.get("stopping_tolerance", 0.0)),
                                                               smetric in _LESS_IS_BETTER):
                     break
-            if max_rt > 0 and time.time() - t0 > max_rt:
-                break
+            # job progress / cancel and the max_runtime_secs clock, agreed across
+            # ranks every 64 mini-batches (not per step: a 0.14 ms step)
+            nstep += 1
+            if nstep % 64 == 0 or samples_done >= total_samples:
+                _, timed_out = self._tick(samples_done, total_samples, None, False, t0, max_rt)
+                if timed_out:
+                    break
         self._epochs_done = samples_done / max(ntot, 1)
         if best is not None and p.get("overwrite_with_best_model", True):
             for L, (Wb, bb) in zip(self._layers, best[1]):

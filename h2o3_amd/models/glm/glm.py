@@ -725,6 +725,7 @@ class H2OGeneralizedLinearEstimator(H2OEstimator):
                 while its < maxit and not drv.converged:
                     drv.step()
                     its += 1
+                    self._tick(li + its / maxit, len(drv.lambdas) + 1)
                     self._scoring_history.append({"iteration": drv.iter, "alpha": alpha, "lambda": lam,
                                                   "deviance_train": drv.last_dev / drv.wsum,
                                                   "objective": drv.last_obj})
@@ -734,7 +735,7 @@ class H2OGeneralizedLinearEstimator(H2OEstimator):
                              "icpt": icpt, "deviance": dev, "explained_deviance_train": None})
                 if max_active > 0 and int(np.sum(np.abs(drv.beta[:-1]) > 0)) > max_active:
                     break   # GLM.java: stop the path once too many predictors are active
-                if max_rt > 0 and time.time() - t0 > max_rt:
+                if self._tick(li + 1, len(drv.lambdas) + 1, None, False, t0, max_rt)[1]:
                     break
         # pick submodel: best by validation deviance if given, else (several
         # alphas) by training deviance of each alpha's last lambda, else last

@@ -282,6 +282,7 @@ class H2OGeneralizedLowRankEstimator(H2OEstimator):
         max_it, max_up = int(p.get("max_iterations", 1000)), int(p.get("max_updates", 2000))
         while it < max_it and updates < max_up and step >= min_step:
             it += 1
+            self._tick(it, max_it)
             # X update
             gX = self._grad_u(A, M, X @ Y, blocks) @ Y.T
             Xn = _prox(rx, X - step * scale * gX, step * scale * gx)

@@ -186,7 +186,8 @@ class H2OKMeansEstimator(H2OEstimator):
             hist.append({"timestamp": time.time(), "iterations": it, "number_of_reassigned_observations": st.changed,
                          "within_cluster_sum_of_squares": float(st.withinss.sum())})
             C = newC
-            if st.changed < max(1.0, nrows_tot * TOLERANCE) or it >= maxit or (t_end and time.time() > t_end):
+            if self._tick(it, maxit, deadline=t_end)[1] or st.changed < max(1.0, nrows_tot * TOLERANCE) or \
+                    it >= maxit:
                 break
         return C, st, it, hist
 
@@ -289,7 +290,7 @@ class H2OKMeansEstimator(H2OEstimator):
                     break
                 self._k_history.append(k)
                 best = (C.clone(), st, it, assign.clone())
-                if k == K or (t_end and time.time() > t_end):
+                if self._tick(k, K, deadline=t_end)[1] or k == K:
                     break
                 C = self._split_largest(X, w, C, assign)
         else:
@@ -368,7 +369,7 @@ class H2OKMeansEstimator(H2OEstimator):
                          "within_cluster_sum_of_squares": float(D[np.arange(n), a].sum())})
             prev = a
             C = newC
-            if changed < max(1.0, n * TOLERANCE) or (t_end and time.time() > t_end):
+            if self._tick(it, maxit, deadline=t_end)[1] or changed < max(1.0, n * TOLERANCE):
                 break
         self._constrained_assign = prev
         Ct = torch.as_tensor(C, dtype=torch.float64, device=X.device)

@@ -59,8 +59,8 @@ class H2ORandomForestEstimator(SharedTreeEstimator):
         for t in range(ntrees):
             drv.step()
             # a max_runtime_secs stop scores the last tree into the history too
-            timed_out = max_rt > 0 and time.time() - t0 > max_rt
-            if sched.due(t + 1, final=t + 1 == ntrees or timed_out):
+            score, timed_out = self._tick(t + 1, ntrees, sched, t + 1 == ntrees, t0, max_rt)
+            if score:
                 entry = {"number_of_trees": t + 1}
                 sched.started()
                 self._forest = drv.forest

@@ -461,8 +461,8 @@ class H2OGradientBoostingEstimator(SharedTreeEstimator):
         while drv.iter < ntrees:
             drv.step()
             # a max_runtime_secs stop scores the last tree into the history too
-            timed_out = max_rt > 0 and time.time() - t0 > max_rt
-            if sched.due(drv.iter, final=drv.iter == ntrees or timed_out):
+            score, timed_out = self._tick(drv.iter, ntrees, sched, drv.iter == ntrees, t0, max_rt)
+            if score:
                 sched.started()
                 entry = self._score_iteration(drv, spec)
                 sched.ended()

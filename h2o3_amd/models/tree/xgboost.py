@@ -195,8 +195,8 @@ class H2OXGBoostEstimator(SharedTreeEstimator):
                 f = f + torch.stack(deltas, 1)
             n_it = it + 1
             # a max_runtime_secs stop scores the last iteration into the history too
-            timed_out = max_rt > 0 and time.time() - t0 > max_rt
-            if sched.due(n_it, final=n_it == ntrees or timed_out):
+            score, timed_out = self._tick(n_it, ntrees, sched, n_it == ntrees, t0, max_rt)
+            if score:
                 entry = {"number_of_trees": n_it}
                 self._forest = forest
                 sched.started()
