@@ -220,12 +220,26 @@ class H2OAutoML:
     def _budget_left(self):
         if self.max_models and self._n_base() >= self.max_models:
             return False
+        out = True
         if self.max_runtime_secs and time.time() - self._t0 > self.max_runtime_secs:
-            return False
+            out = False
         dl = getattr(self, "_step_deadline", None)
         if dl is not None and time.time() > dl:
-            return False       # this grid step's share of the budget is spent
-        return True
+            out = False       # this grid step's share of the budget is spent
+        # the clock is rank 0's (every rank must start the same models), and a
+        # REST cancel of the AutoML job stops here between models
+        from ..core import job as jobmod
+        from ..parallel import cloud
+        j = jobmod.current()
+        clocked = bool(self.max_runtime_secs) or dl is not None
+        if j is not None:
+            prog = (self._n_base() / self.max_models) if self.max_models else \
+                ((time.time() - self._t0) / self.max_runtime_secs if self.max_runtime_secs else 0.0)
+            out = bool(j.tick(min(prog, 0.99), extra=(out,) if clocked else ())[0]) if clocked else \
+                (j.tick(min(prog, 0.99)) or out)
+        elif clocked and cloud.is_distributed():
+            out = bool(cloud.agree([out])[0])
+        return out
 
     def _set_stopping_tolerance(self, frame):
         """AutoML.java:357: an unset stopping tolerance adapts to the training
@@ -308,6 +322,9 @@ class H2OAutoML:
             est.train(x=data["x"], y=data["y"], training_frame=data["train"], weights_column=data["weights"],
                       fold_column=data["fold"], validation_frame=data["valid"])
         except Exception as e:
+            from ..core.job import JobCancelled
+            if isinstance(e, JobCancelled):
+                raise
             self._log("ModelTraining", f"{name} failed: {e!r}", level="Warn")
             return None
         self.models.append(est)
@@ -398,6 +415,9 @@ class H2OAutoML:
             se.train(x=data["x"], y=data["y"], training_frame=data["train"], validation_frame=data["valid"],
                      blending_frame=data["blending"])
         except Exception as e:
+            from ..core.job import JobCancelled
+            if isinstance(e, JobCancelled):
+                raise
             self._log("ModelTraining", f"{name} failed: {e!r}", level="Warn")
             return
         self.models.append(se)
@@ -542,7 +562,7 @@ class H2OAutoML:
     @property
     def event_log(self):
         import pandas as pd
-        return H2OFrame(pd.DataFrame(self.event_log_rows), _local=True) if self.event_log_rows else None
+        return H2OFrame(pd.DataFrame(self.event_log_rows)) if self.event_log_rows else None
 
     def get_best_model(self, algorithm=None, criterion=None):
         lb = Leaderboard(self.models, sort_metric=criterion or self.sort_metric)

@@ -67,7 +67,7 @@ class Leaderboard:
             if extra_columns == "ALL" or (isinstance(extra_columns, list) and "algo" in extra_columns):
                 r["algo"] = m.algo
             rows.append(r)
-        return H2OFrame(pd.DataFrame(rows), _local=True, column_types={"model_id": "string"})
+        return H2OFrame(pd.DataFrame(rows), column_types={"model_id": "string"})
 
 
 def make_leaderboard(object, leaderboard_frame=None, sort_metric="AUTO", extra_columns=(), scoring_data="AUTO"):

@@ -20,7 +20,10 @@ _counters: dict = {}
 def make_key(prefix: str = "key") -> str:
     with _lock:
         c = _counters.setdefault(prefix, itertools.count(1))
-        return f"{prefix}_{next(c)}"
+        k = f"{prefix}_{next(c)}"
+    from ..parallel import collectives
+    collectives._trace(f"make_key:{k}")     # H2O3_TRACE_COLL: keys must agree across ranks too
+    return k
 
 
 def put(key: str, obj, weak: bool = False):

@@ -288,6 +288,11 @@ class H2OFrame:
     def __len__(self):
         return self.nrows
 
+    def __bool__(self):
+        # truthiness must not be a collective: `frame or other` on one rank
+        # only would split the SPMD collective sequence
+        return True
+
     @property
     def types(self):
         return {n: v.type for n, v in zip(self._names, self._vecs)}
@@ -331,10 +336,12 @@ class H2OFrame:
         return int(sum(alln[: cloud.rank()]))
 
     # ------------------------------------------------------------ conversion
-    def as_data_frame(self, use_pandas=True, header=True, use_multi_thread=False):
+    def as_data_frame(self, use_pandas=True, header=True, use_multi_thread=False, local=False):
+        """pandas view of the whole frame (gathered on every rank), or of this
+        rank's row shard only (local=True: per-rank host scoring)."""
         import pandas as pd
         data = {}
-        for n, v in zip(self._names, self._gathered_vecs()):
+        for n, v in zip(self._names, self._vecs if local else self._gathered_vecs()):
             if v.type == T_TIME:
                 a = v.data.cpu().numpy()
                 data[n] = pd.to_datetime(pd.Series(a), unit="ms")
@@ -817,7 +824,7 @@ class H2OFrame:
             else:
                 res.append(r["mean"])
         if return_frame:
-            return H2OFrame({n: [m] for n, m in zip(self._names, res)}, _local=True)
+            return H2OFrame({n: [m] for n, m in zip(self._names, res)})
         return res[0] if len(res) == 1 else res
 
     def min(self):
@@ -1170,7 +1177,7 @@ class H2OFrame:
                 best = max(cands, key=lambda c: (c[0], -c[1])) if largest else min(cands, key=lambda c: (c[0], c[1]))
                 val, gi = best
             res.append(gi if math.isfinite(val) else float("nan"))
-        return H2OFrame({n: [r] for n, r in zip(self._names, res)}, _local=True)
+        return H2OFrame({n: [r] for n, r in zip(self._names, res)})
 
     def idxmax(self, skipna=True, axis=0):
         """Row index of the max per column (axis=0) or column index per row (axis=1) (AstWhichMax)."""

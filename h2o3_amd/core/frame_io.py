@@ -24,9 +24,14 @@ _FORMAT = "h2o3_amd.frame.v1"
 
 
 def save_frame(frame, path, force=True):
+    # rank 0 reads the file system and decides; every rank writes where it
+    # says (a rank that looked after another rank's makedirs would pick a
+    # different directory)
     d = os.path.join(path, frame.frame_id) if os.path.isdir(path) and not os.path.exists(
         os.path.join(path, "frame.json")) else path
-    if os.path.exists(os.path.join(d, "frame.json")) and not force:
+    exists = os.path.exists(os.path.join(d, "frame.json"))
+    d, exists = coll.broadcast_object((d, exists))
+    if exists and not force:
         raise FileExistsError(f"{d} exists (use force=True)")
     os.makedirs(d, exist_ok=True)
     rank = cloud.rank()

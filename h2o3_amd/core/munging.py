@@ -113,7 +113,7 @@ def table(fr, data2=None, dense=True):
     res = df.groupby(cols, dropna=True).size().reset_index(name="Counts")
     if not dense and len(cols) == 2:
         res = res.pivot(index=cols[0], columns=cols[1], values="Counts").fillna(0).reset_index()
-    return H2OFrame(res, _local=True, column_types={c: "enum" for c in cols if g.vec(c).type == T_ENUM})
+    return H2OFrame(res, column_types={c: "enum" for c in cols if g.vec(c).type == T_ENUM})
 
 
 def hist(fr, breaks="sturges"):
@@ -152,7 +152,7 @@ def hist(fr, breaks="sturges"):
     mids = (edges[:-1] + edges[1:]) / 2
     df = pd.DataFrame({"breaks": edges[1:], "counts": counts.astype(float), "mids_true": mids, "mids": mids,
                        "density": counts / max(counts.sum(), 1) / np.diff(edges)})
-    return H2OFrame(df, _local=True)
+    return H2OFrame(df)
 
 
 # ---------------------------------------------------------------- stats
@@ -193,7 +193,7 @@ def cor(x, y=None, method="Pearson", use="everything"):
     if c.numel() == 1:
         return float(c)
     import pandas as pd
-    return H2OFrame(pd.DataFrame(c.cpu().numpy(), columns=(y or x).names), _local=True)
+    return H2OFrame(pd.DataFrame(c.cpu().numpy(), columns=(y or x).names))
 
 
 def cov(x, y=None):
@@ -204,7 +204,7 @@ def cov(x, y=None):
     if c.numel() == 1:
         return float(c)
     import pandas as pd
-    return H2OFrame(pd.DataFrame(c.cpu().numpy(), columns=(y or x).names), _local=True)
+    return H2OFrame(pd.DataFrame(c.cpu().numpy(), columns=(y or x).names))
 
 
 def distance(x, y, measure="l2"):
@@ -887,7 +887,7 @@ def apply(fr, fun, axis=0):
         res = {n: [fun(H2OFrame.from_vecs([v], [n]))] for n, v in zip(fr.names, fr._vecs)}
         vals = {n: [x[0] if not isinstance(x[0], H2OFrame) else x[0].flatten()] for n, x in res.items()}
         import pandas as pd
-        return H2OFrame(pd.DataFrame(vals), _local=True)
+        return H2OFrame(pd.DataFrame(vals))
     df = fr.as_data_frame()
     out = df.apply(lambda row: fun(row), axis=1)
     import pandas as pd

@@ -262,7 +262,8 @@ def _import_arff(fn, dest):
 def export_file(frame, path, force=False, sep=",", header=True, format="csv"):
     from .persist import is_remote, upload, _tmpfile
     remote = is_remote(path)
-    if not remote and os.path.exists(path) and not force:
+    from ..parallel import collectives as coll
+    if not remote and coll.broadcast_object(os.path.exists(path)) and not force:    # rank 0's view
         raise FileExistsError(path)
     df = frame.as_data_frame()
     if cloud.rank() != 0:

@@ -267,7 +267,7 @@ def _is_frame(x):
 
 
 def _scalar_frame(x):
-    return _F()({"C1": [x]}, _local=True)
+    return _F()({"C1": [x]})
 
 
 def _binop(op):
@@ -408,7 +408,7 @@ def _apply(fr, margin, fun):
     if margin == 2:
         outs = [call(fun, [fr[:, j]]) for j in range(fr.ncols)]
         if all(not _is_frame(o) for o in outs):
-            return _F()({n: [o] for n, o in zip(fr.names, outs)}, _local=True)
+            return _F()({n: [o] for n, o in zip(fr.names, outs)})
         res = outs[0]
         for o in outs[1:]:
             res = res.cbind(o)
@@ -517,7 +517,8 @@ def _levels(x):
         codes = torch.full((n,), -1, dtype=torch.int32, device=dev)
         codes[:len(d)] = torch.arange(len(d), dtype=torch.int32, device=dev)
         vecs.append(Vec(codes, T_ENUM, d))
-    return _F().from_vecs(vecs, [f"C{j + 1}" for j in range(len(lv))])
+    from .frame import _reshard
+    return _reshard(_F().from_vecs(vecs, [f"C{j + 1}" for j in range(len(lv))]))   # same table on every rank
 
 
 PRIMS["levels"] = _levels

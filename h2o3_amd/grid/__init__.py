@@ -16,6 +16,8 @@ import time
 import numpy as np
 
 from ..core import dkv
+from ..core import job as jobmod
+from ..parallel import cloud
 
 
 class H2OGridSearch:
@@ -62,13 +64,22 @@ class H2OGridSearch:
         if self.recovery_dir:
             self._save_train_inputs(x, y, training_frame, validation_frame, weights_column, offset_column,
                                     fold_column, params)
-        for combo in self._combos():
+        combos = self._combos()
+        for combo in combos:
             key = repr(sorted(combo.items()))
             if key in done:
                 continue
             if max_models and len(self.models) >= max_models:
                 break
-            if max_rt and time.time() - t0 > max_rt:
+            timed = bool(max_rt and time.time() - t0 > max_rt)
+            # rank 0's clock decides (SPMD), and a REST cancel of the grid job stops here
+            j = jobmod.current()
+            if j is not None:
+                tot = min(max_models, len(combos)) if max_models else len(combos)
+                timed = bool(j.tick(len(self.models) / max(tot, 1), extra=(timed,))[0])
+            elif max_rt and cloud.is_distributed():
+                timed = bool(cloud.agree([timed])[0])
+            if timed:
                 break
             kw = dict(params)
             kw.update(combo)
@@ -85,6 +96,8 @@ class H2OGridSearch:
                     if self._stop(history, sc):
                         break
             except Exception as e:  # reference keeps failures in the grid's failure list
+                if isinstance(e, jobmod.JobCancelled):
+                    raise
                 self.failed_params.append((combo, repr(e)))
         dkv.put(self.grid_id, self)
         return self
@@ -105,12 +118,13 @@ class H2OGridSearch:
         from ..core.frame_io import save_frame
         os.makedirs(self.recovery_dir, exist_ok=True)
         fdir = f"{self.grid_id}.train_frame"
-        if not os.path.exists(os.path.join(self.recovery_dir, fdir, "frame.json")):
+        from ..parallel import collectives as coll
+        if not coll.broadcast_object(os.path.exists(os.path.join(self.recovery_dir, fdir, "frame.json"))):
             save_frame(training_frame, os.path.join(self.recovery_dir, fdir))
         vdir = None
         if validation_frame is not None:
             vdir = f"{self.grid_id}.valid_frame"
-            if not os.path.exists(os.path.join(self.recovery_dir, vdir, "frame.json")):
+            if not coll.broadcast_object(os.path.exists(os.path.join(self.recovery_dir, vdir, "frame.json"))):
                 save_frame(validation_frame, os.path.join(self.recovery_dir, vdir))
         self._train_rec = {"frame_dir": fdir, "valid_dir": vdir, "x": x, "y": y, "weights_column": weights_column,
                            "offset_column": offset_column, "fold_column": fold_column,

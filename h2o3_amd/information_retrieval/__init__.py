@@ -37,7 +37,7 @@ def tf_idf(frame, document_id_col, text_col, preprocess=True, case_sensitive=Tru
         docs.extend([d] * len(toks))
         words.extend(toks)
     if not words:
-        return H2OFrame(pd.DataFrame({"DocID": [], "Word": [], "TF": [], "IDF": [], "TF-IDF": []}), _local=True)
+        return H2OFrame(pd.DataFrame({"DocID": [], "Word": [], "TF": [], "IDF": [], "TF-IDF": []}))
     dev = cloud.device()
     dvals, dcodes = np.unique(np.asarray(docs), return_inverse=True)
     wvals, wcodes = np.unique(np.asarray(words, dtype=object).astype(str), return_inverse=True)
@@ -54,4 +54,4 @@ def tf_idf(frame, document_id_col, text_col, preprocess=True, case_sensitive=Tru
     out = pd.DataFrame({"DocID": dvals[kd.cpu().numpy()], "Word": wvals[kw.cpu().numpy()],
                         "TF": tfv.cpu().numpy().astype(np.int64), "IDF": idf[kw].cpu().numpy(),
                         "TF-IDF": (tfv * idf[kw]).cpu().numpy()})
-    return H2OFrame(out, _local=True, column_types={"Word": "string"})
+    return H2OFrame(out, column_types={"Word": "string"})

@@ -66,7 +66,7 @@ class TrainSpec:
         return self.nclasses > 1
 
     def yvec(self, frame=None):
-        return (frame or self.frame).vec(self.y)
+        return (frame if frame is not None else self.frame).vec(self.y)
 
     def y_tensor(self, frame=None, dtype=torch.float32):
         v = self.yvec(frame)
@@ -75,14 +75,14 @@ class TrainSpec:
         return v.as_float(dtype)
 
     def w_tensor(self, frame=None):
-        fr = frame or self.frame
+        fr = frame if frame is not None else self.frame
         if self.weights_column and self.weights_column in fr.names:
             w = fr.vec(self.weights_column).as_float()
             return torch.nan_to_num(w, nan=0.0)
         return None
 
     def offset_tensor(self, frame=None):
-        fr = frame or self.frame
+        fr = frame if frame is not None else self.frame
         if self.offset_column and self.offset_column in fr.names:
             return torch.nan_to_num(fr.vec(self.offset_column).as_float(), nan=0.0)
         return None

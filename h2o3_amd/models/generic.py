@@ -37,13 +37,13 @@ class H2OGenericEstimator(H2OEstimator):
         return self
 
     def _predict_raw(self, frame):
-        df = frame.as_data_frame()
+        df = frame.as_data_frame(local=True)          # each rank scores its own row shard
         raw = self._mojo.predict_raw(df)
         return torch.as_tensor(np.asarray(raw, dtype=np.float64), device=cloud.device())
 
     def predict(self, test_data, **kw):
         import pandas as pd
-        return H2OFrame(self._mojo.predict(test_data.as_data_frame()))
+        return H2OFrame(self._mojo.predict(test_data.as_data_frame(local=True)), _local=True)
 
     def model_performance(self, test_data=None, **kw):
         spec = TrainSpec(test_data, self._x, self._y)

@@ -127,7 +127,7 @@ class H2OANOVAGLMEstimator(H2OEstimator):
         self._tf = tf if p.get("save_transformed_framekeys") else None
 
     def result(self):
-        return H2OFrame(self._result, _local=True)
+        return H2OFrame(self._result)
 
     def summary(self):
         return self._result

@@ -188,7 +188,7 @@ class H2OModelSelectionEstimator(H2OEstimator):
         for c in ("coefficient_names", "z_values", "p_values"):
             if c in df:
                 df[c] = [", ".join(map(str, v)) for v in df[c]]
-        return H2OFrame(df, _local=True)
+        return H2OFrame(df)
 
     def get_best_R2_values(self):
         return list(self._result["best_r2_value"]) if "best_r2_value" in self._result else None

@@ -139,7 +139,7 @@ class H2OInfogram(H2OEstimator):
         self._base = base
 
     def get_admissible_score_frame(self):
-        return H2OFrame(self._table, _local=True)
+        return H2OFrame(self._table)
 
     def get_admissible_features(self):
         return self._output["admissible_features"]

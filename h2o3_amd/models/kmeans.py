@@ -55,6 +55,17 @@ def _seed(p, default=1234):
     return default if s is None or s == -1 else int(s) & 0x7FFFFFFF
 
 
+def _row_uniform(rows, seed):
+    """Counter-based uniform in (0, 1) per global row index (integer hash,
+    32-bit lanes in int64 so no product overflows)."""
+    m = 0xFFFFFFFF
+    x = (rows ^ (int(seed) & m)) & m
+    x = (((x >> 16) ^ x) * 0x45D9F3B) & m
+    x = (((x >> 16) ^ x) * 0x45D9F3B) & m
+    x = (x >> 16) ^ x
+    return (x.to(torch.float64) + 0.5) / 4294967296.0
+
+
 class H2OKMeansEstimator(H2OEstimator):
     algo = "kmeans"
     supervised_learning = False
@@ -121,14 +132,18 @@ class H2OKMeansEstimator(H2OEstimator):
             return C
         # 5 rounds of k-means|| oversampling (SumSqr + Sampler)
         dmin = torch.empty(X.shape[0], dtype=torch.float32, device=X.device)
-        gen = torch.Generator(device=X.device)
-        gen.manual_seed(int(rng.randint(0, 2 ** 31 - 1)) + cloud.rank())
-        for _ in range(5):
+        # the sampler's uniform is a hash of (seed, round, GLOBAL row): the same
+        # candidates whatever the row sharding (1 rank or N), unlike a per-rank
+        # generator stream
+        off, _ = self._offsets(X.shape[0])
+        grow = torch.arange(X.shape[0], device=X.device, dtype=torch.int64) + int(off)
+        seed0 = int(rng.randint(0, 2 ** 31 - 1))
+        for rnd in range(5):
             cluster_ops.lloyd_pass(X, C, accumulate=False, dmin=dmin)
             tot = coll.allreduce_scalar(float(dmin.to(torch.float64).sum()))
             if tot <= 0:
                 break
-            u = torch.rand(X.shape[0], generator=gen, device=X.device, dtype=torch.float64)
+            u = _row_uniform(grow, seed0 * 7919 + rnd)
             pick = torch.nonzero(3.0 * k * dmin.to(torch.float64) > u * tot).flatten()
             S = coll.all_gather_var(X[pick].to(torch.float64))
             C = torch.cat([C, S.to(C.device)], 0)

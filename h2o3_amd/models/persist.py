@@ -37,15 +37,24 @@ def save_model(model, path="", force=False, filename=None):
         dest = path.rstrip("/") + "/" + (filename or model.model_id)
         if not force and exists(dest):
             raise FileExistsError(dest)
+        from ..parallel import cloud
         with tempfile.TemporaryDirectory() as td:
             local = save_model(model, td, force=True, filename=filename)
-            upload(local, dest)
+            if cloud.rank() == 0:
+                upload(local, dest)
+        cloud.barrier()
         return dest
     from ..mojo.writer import build_mojo
+    from ..parallel import cloud
+    from ..parallel import collectives as coll
     os.makedirs(path or ".", exist_ok=True)
     fn = os.path.join(path or ".", filename or model.model_id)
-    if os.path.exists(fn) and not force:
+    # rank 0 checks and writes (the model is replicated); every rank agrees
+    if coll.broadcast_object(os.path.exists(fn)) and not force:
         raise FileExistsError(fn)
+    if cloud.rank() != 0:
+        cloud.barrier()
+        return fn
     params = {k: v for k, v in model._parms.items() if isinstance(v, (int, float, str, bool, list, type(None)))}
     with zipfile.ZipFile(fn, "w", zipfile.ZIP_DEFLATED) as z:
         z.writestr("mojo.zip", build_mojo(model))
@@ -56,6 +65,7 @@ def save_model(model, path="", force=False, filename=None):
                                                "output": {k: v for k, v in model._output.items()
                                                           if isinstance(v, (dict, list, float, int, str))}},
                                               default=str))
+    cloud.barrier()
     return fn
 
 

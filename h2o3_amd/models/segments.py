@@ -29,7 +29,7 @@ class H2OSegmentModels:
         self._models = {}
 
     def as_frame(self):
-        return H2OFrame(pd.DataFrame(self._rows), _local=True)
+        return H2OFrame(pd.DataFrame(self._rows))
 
     def get_model(self, **segment):
         key = tuple(sorted(segment.items()))

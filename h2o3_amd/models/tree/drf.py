@@ -103,9 +103,13 @@ class H2ORandomForestEstimator(SharedTreeEstimator):
         validation metrics of the forest so far."""
         from .gbm import H2OGradientBoostingEstimator as _G
         has = oob_cnt > 0
-        if bool(has.any()):
+        # branch on the GLOBAL state: a rank-local any()/all() would split the
+        # SPMD sequence (metrics collectives, frame keys) when one rank's shard
+        # happens to be fully covered
+        n_has = coll.allreduce_scalar(float(has.sum()))
+        if n_has > 0:
             oobp = self._normalize(oob_sum / oob_cnt.clamp_min(1).view(-1, 1))
-            sub = spec.frame[has] if not bool(has.all()) else spec.frame
+            sub = spec.frame[has] if n_has < spec.frame.nrows else spec.frame
             m = self._metrics_from_raw(spec, sub, oobp[has])
             _G._add_metrics(entry, "training", m)
         if spec.valid is not None:

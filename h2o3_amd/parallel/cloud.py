@@ -128,6 +128,8 @@ def agree(values, src: int = 0) -> list:
     if not is_distributed():
         return vals
     t = torch.tensor(vals, dtype=torch.float64)
+    from . import collectives
+    collectives._trace("agree", t)
     dist.broadcast(t, src, group=_state["ctl"])
     return t.tolist()
 

@@ -15,6 +15,32 @@ import torch.distributed as dist
 
 from . import cloud
 
+# Collective sequence tracing (H2O3_TRACE_COLL=<dir>): every rank appends one
+# line per collective -- sequence number, op, shape, and the calling
+# h2o3_amd frames -- to <dir>/coll_rank<r>.log.  Diffing two ranks' logs
+# names the first call site where the SPMD sequences diverge (a rank-local
+# branch around a collective), the usual cause of a multi-rank hang.
+_TRACE = {"dir": None, "f": None, "seq": 0}
+
+
+def _trace(op, t=None):
+    d = _TRACE["dir"]
+    if d is None:
+        import os
+        d = _TRACE["dir"] = os.environ.get("H2O3_TRACE_COLL", "")
+    if not d:
+        return
+    import os
+    import traceback
+    if _TRACE["f"] is None:
+        os.makedirs(d, exist_ok=True)
+        _TRACE["f"] = open(os.path.join(d, f"coll_rank{cloud.rank()}.log"), "w", buffering=1)
+    fr = [f"{os.path.basename(x.filename)}:{x.lineno}:{x.name}" for x in traceback.extract_stack()[:-2]
+          if "h2o3_amd" in x.filename and "collectives.py" not in x.filename][-6:]
+    shape = tuple(t.shape) if hasattr(t, "shape") else ""
+    _TRACE["f"].write(f"{_TRACE['seq']} {op} {shape} {' < '.join(reversed(fr))}\n")
+    _TRACE["seq"] += 1
+
 
 def _rccl() -> bool:
     """True when the process group is NCCL (= RCCL over xGMI on ROCm); gloo
@@ -27,6 +53,7 @@ def allreduce_(t: torch.Tensor, op: str = "sum") -> torch.Tensor:
     if not cloud.is_distributed():
         return t
     rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
+    _trace("all_reduce", t)
     dist.all_reduce(t, op=rop)
     return t
 
@@ -65,6 +92,7 @@ def reduce_scatter_dim0(t: torch.Tensor) -> torch.Tensor:
         return t
     assert t.shape[0] % w == 0
     out = torch.empty((t.shape[0] // w,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    _trace("reduce_scatter", t)
     if _rccl():
         dist.reduce_scatter_tensor(out, t.contiguous())
     else:  # gloo has no reduce_scatter: all_reduce + slice
@@ -78,6 +106,7 @@ def all_gather_dim0(t: torch.Tensor) -> torch.Tensor:
     if w == 1:
         return t
     out = torch.empty((t.shape[0] * w,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    _trace("all_gather", t)
     if _rccl():
         dist.all_gather_into_tensor(out, t.contiguous())
     else:
@@ -103,6 +132,7 @@ def all_gather_var(t: torch.Tensor) -> torch.Tensor:
 
 def broadcast_(t: torch.Tensor, src: int = 0) -> torch.Tensor:
     if cloud.is_distributed():
+        _trace("broadcast", t)
         dist.broadcast(t, src)
     return t
 
@@ -111,6 +141,7 @@ def broadcast_object(obj, src: int = 0):
     if not cloud.is_distributed():
         return obj
     lst = [obj]
+    _trace("broadcast_object")
     dist.broadcast_object_list(lst, src=src, device=cloud.device() if _rccl() else None)
     return lst[0]
 
@@ -119,5 +150,6 @@ def all_gather_object(obj) -> list:
     if not cloud.is_distributed():
         return [obj]
     out = [None] * cloud.world()
+    _trace("all_gather_object")
     dist.all_gather_object(out, obj)
     return out

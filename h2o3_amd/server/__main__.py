@@ -8,6 +8,10 @@ from .rest import start
 
 
 def main():
+    import faulthandler
+    import signal
+    # `kill -USR1 <pid>` dumps every thread's stack (diagnosing a stuck rank)
+    faulthandler.register(signal.SIGUSR1, all_threads=True)
     ap = argparse.ArgumentParser(prog="python -m h2o3_amd.server")
     ap.add_argument("--ip", default="127.0.0.1")
     ap.add_argument("--port", type=int, default=54321)

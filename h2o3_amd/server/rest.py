@@ -15,15 +15,18 @@ reference's own Python client (h2o-py: h2o.connect / H2OFrame / estimators
 / predict / model_performance / Rapids frame munging) runs against this
 server; tests/test_rest_wire.py drives it end to end.
 
-Model builds run synchronously inside the request on the serving process
-(the compute itself runs on the GPU through the same estimators the Python
-API uses); the returned job is already DONE when the client starts polling.
-Requests are served one at a time (GPU work of one process is issued from
-one host thread).  Multi-rank clouds are driven SPMD from Python; the REST
-server serves a single-process cloud.
+One REST endpoint drives the whole multi-GPU cloud (spmd.py): rank 0
+serves HTTP, every request that touches frames, models or collectives is
+replayed as a command on every rank by rank 0's executor thread (ranks
+1..N-1 run `spmd.worker_loop`), and model / grid / AutoML builds answer with
+the RUNNING job at once and keep training on the executor, so `/3/Jobs`
+polls see live progress and `/3/Jobs/{id}/cancel` stops a build at its next
+tree / iteration.  Launch a cloud with
+`torchrun --nproc-per-node N -m h2o3_amd.server`.
 """
 from __future__ import annotations
 
+import asyncio
 import json as _json
 import os
 import tempfile
@@ -40,6 +43,14 @@ from ..core import dkv
 from ..core.frame import H2OFrame
 from ..parallel import cloud
 from . import schemas as S
+from . import spmd
+
+# requests served straight from rank 0's state on the HTTP thread (no
+# collective, no command replay): clients poll / cancel jobs and read the
+# cloud status while a build holds the executor
+_LOCAL_PREFIXES = ("/3/Cloud", "/3/Metadata", "/4/sessions", "/3/InitID", "/3/Capabilities", "/3/About",
+                   "/3/Jobs", "/3/NodePersistentStorage", "/3/Ping", "/3/Logs", "/3/JStack", "/3/WaterMeter",
+                   "/3/SteamMetrics", "/3/Profiler", "/3/SessionProperties", "/3/Typeahead", "/3/LogAndEcho")
 
 _ALGOS = {"gbm": "H2OGradientBoostingEstimator", "glm": "H2OGeneralizedLinearEstimator",
           "drf": "H2ORandomForestEstimator", "xgboost": "H2OXGBoostEstimator",
@@ -196,7 +207,7 @@ class _Uploads:
 
     def add_bytes(self, data: bytes, name: str | None = None) -> str:
         import re
-        k = name or f"upload_{uuid.uuid4().hex[:16]}"
+        k = name or f"upload_{spmd.rand_hex(16)}"
         # the key names the file inside the upload directory: no separators, no dot-files
         p = os.path.join(self.dir, re.sub(r"[^A-Za-z0-9._-]", "_", k).lstrip(".") or "upload")
         with open(p, "wb") as f:
@@ -211,8 +222,12 @@ class _Uploads:
         return out
 
 
-def create_app(flow_dir: str | None = None) -> FastAPI:
+def create_app(flow_dir: str | None = None, serve: bool = True) -> FastAPI:
+    """The REST app.  serve=False (ranks 1..N-1 of a multi-rank cloud): the
+    same handler table, replayed from rank 0's commands by
+    spmd.worker_loop(app.state.run_command); no HTTP."""
     app = FastAPI(title="h2o3_amd REST API", version="3")
+    table = {}                        # (method, path) -> handler(p, r, **path)
     uploads = _Uploads()
     sessions: dict[str, float] = {}
     t_start = time.time()
@@ -231,6 +246,36 @@ def create_app(flow_dir: str | None = None) -> FastAPI:
             return out.body.decode("utf-8", "replace")
         return S.jsonable(out)
 
+    def _to_response(out):
+        if isinstance(out, Response):
+            return out
+        return JSONResponse(S.jsonable(out))
+
+    def run_command(cmd, loop):
+        """Execute one replayed command on this rank (spmd.execute)."""
+        if cmd["kind"] == "flow":
+            res = flow_runner.run_cell(cmd["input"], cmd["type"])
+            return JSONResponse({"ok": True, "result": S.jsonable(res)})
+        fn = table[(cmd["method"], cmd["path"])]
+        req = spmd.Req(**cmd["req"])
+        try:
+            out = fn(cmd["p"], req, **cmd["kw"])
+            if hasattr(out, "__await__"):
+                out = loop.run_until_complete(out)
+        except _HTTPError:
+            raise
+        except (KeyError, ValueError, TypeError, RuntimeError, AssertionError, IndexError,
+                NotImplementedError) as e:
+            raise _HTTPError(400 if not isinstance(e, KeyError) else 404, str(e), e)
+        if isinstance(out, spmd.Deferred):
+            out.response = _to_response(out.response)
+            return out
+        return _to_response(out)
+
+    app.state.run_command = run_command
+    executor = spmd.Executor(run_command) if serve else None
+    app.state.executor = executor
+
     def route(method, path):
         """Register an async handler taking (params, request, **path)."""
         rx = _re.compile(_re.sub(r"\{(\w+)\}", r"(?P<\1>[^/]+)", _re.escape(path).replace(r"\{", "{")
@@ -239,23 +284,36 @@ def create_app(flow_dir: str | None = None) -> FastAPI:
         def local(fn):
             return lambda p, r, **kw: fn(p, r, **{k: _unquote(v) for k, v in kw.items()})
 
+        is_local = path.startswith(_LOCAL_PREFIXES)
+
         def deco(fn):
             app.state.flow_routes.append((method, rx, local(fn), _jsonify))
+            table[(method, path)] = fn
+
             async def h(request: Request):
                 p = await _params(request)
-                # handlers run on the event-loop thread: requests are served one at a time
+                if is_local:
+                    try:
+                        out = fn(p, request, **request.path_params)
+                        if hasattr(out, "__await__"):
+                            out = await out
+                    except _HTTPError:
+                        raise
+                    except (KeyError, ValueError, TypeError, RuntimeError, AssertionError, IndexError,
+                            NotImplementedError) as e:
+                        raise _HTTPError(400 if not isinstance(e, KeyError) else 404, str(e), e)
+                    return _to_response(out)
+                # replayed on every rank by the executor (spmd.py)
+                req = {"method": request.method, "path": request.url.path, "headers": dict(request.headers),
+                       "body": await request.body(), "query": dict(request.query_params)}
+                cmd = {"kind": "route", "method": method, "path": path, "p": p, "kw": dict(request.path_params),
+                       "req": req, "defer": True}
                 try:
-                    out = fn(p, request, **request.path_params)
-                    if hasattr(out, "__await__"):
-                        out = await out
+                    return await asyncio.wrap_future(executor.submit(cmd))
                 except _HTTPError:
                     raise
-                except (KeyError, ValueError, TypeError, RuntimeError, AssertionError, IndexError,
-                        NotImplementedError) as e:
-                    raise _HTTPError(400 if not isinstance(e, KeyError) else 404, str(e), e)
-                if isinstance(out, Response):
-                    return out
-                return JSONResponse(S.jsonable(out))
+                except RuntimeError as e:
+                    raise _HTTPError(503 if not cloud.healthy() else 400, str(e), e)
             h.__name__ = fn.__name__
             app.add_api_route(path, h, methods=[method], name=f"{method} {path}")
             return fn
@@ -337,8 +395,13 @@ def create_app(flow_dir: str | None = None) -> FastAPI:
 
     @route("POST", "/3/Shutdown")
     def shutdown(p, r):
-        """ShutdownHandler: the cloud stays up in-process; the request is
-        acknowledged so the reference clients' h2o.shutdown() completes."""
+        """ShutdownHandler: a served cloud (rest.start) stops HTTP after the
+        answer and then every rank (the executor's stop command ends the
+        workers' loops); an embedded app just acknowledges."""
+        srv = getattr(app.state, "uvicorn", None)
+        if srv is not None:
+            import threading as _th
+            _th.Timer(0.5, lambda: setattr(srv, "should_exit", True)).start()
         return {"__meta": S.meta("ShutdownV3", "Iced")}
 
     @route("GET", "/3/About")
@@ -588,7 +651,11 @@ def create_app(flow_dir: str | None = None) -> FastAPI:
                 out[k] = v
         return out
 
-    def _build(algo, p):
+    def _build(algo, p, defer=False):
+        """ModelBuilderHandler: validate + create the builder now; train now
+        (defer=False: Flow cells, sync callers) or return (model, job, work)
+        for the executor to run after answering with the RUNNING job."""
+        from ..core import job as jobmod
         cls = _algo_cls(algo)
         p = _resolve_params(_coerce_params(cls, p))
         tf = p.get("training_frame")
@@ -605,33 +672,54 @@ def create_app(flow_dir: str | None = None) -> FastAPI:
         kw = {k: v for k, v in p.items() if k not in _DROP_PARAMS and v is not None}
         if algo == "hglm":
             kw["HGLM"] = True
-        m = cls(**kw)
         try:
-            if m.supervised_learning:
-                m.train(x=x, y=y, training_frame=tf, validation_frame=vf)
-            else:
-                m.train(x=x, training_frame=tf, validation_frame=vf) if vf is not None else \
-                    m.train(x=x, training_frame=tf)
+            m = cls(**kw)
+        except (ValueError, TypeError) as e:      # parameter validation (ModelBuilder.init error(...))
+            raise _HTTPError(412, f"Illegal argument(s) for {algo} model: {e}", e, builder=True)
+        job = jobmod.Job(f"{algo} Model Build", dest=m.model_id).start()
+        job.spmd = cloud.is_distributed()
+
+        def work():
+            jobmod.set_pending(job)
+            try:
+                if m.supervised_learning:
+                    m.train(x=x, y=y, training_frame=tf, validation_frame=vf)
+                else:
+                    m.train(x=x, training_frame=tf, validation_frame=vf) if vf is not None else \
+                        m.train(x=x, training_frame=tf)
+            finally:
+                jobmod.take_pending()
+            dkv.put(m.model_id, m)
+            for cm in getattr(m, "_cv_models", None) or []:   # cross_validation_models are fetched by key
+                dkv.put(cm.model_id, cm)
+            if algo == "stackedensemble" and getattr(m, "_meta", None) is not None:
+                dkv.put(m._meta.model_id, m._meta)                # output.metalearner is fetched by key
+
+        if defer:
+            return m, job, work
+        try:
+            work()
         except _HTTPError:
             raise
+        except jobmod.JobCancelled as e:
+            raise _HTTPError(400, f"{algo} model build cancelled", e, builder=True)
         except Exception as e:  # noqa: BLE001 - reported to the client as an H2OModelBuilderError
             raise _HTTPError(400, f"Illegal argument(s) for {algo} model: {e}", e, builder=True)
-        dkv.put(m.model_id, m)
-        for cm in getattr(m, "_cv_models", None) or []:   # cross_validation_models are fetched by key
-            dkv.put(cm.model_id, cm)
-        if algo == "stackedensemble" and getattr(m, "_meta", None) is not None:
-            dkv.put(m._meta.model_id, m._meta)                # output.metalearner is fetched by key
+        if job.is_running:
+            job.done()
         return m
 
     @route("POST", "/3/ModelBuilders/{algo}")
     def build(p, r, algo):
-        m = _build(algo, p)
-        j = getattr(m, "_job", None)
-        return {"__meta": S.meta(f"{algo.capitalize()}V3", "ModelBuilder"), "algo": algo,
-                "job": S.job_v3(j, dest=m.model_id, dest_kind="Model") if j is not None else
+        defer = spmd.defer_allowed()
+        out = _build(algo, p, defer=defer)
+        m, job, work = out if defer else (out, getattr(out, "_job", None), None)
+        resp = {"__meta": S.meta(f"{algo.capitalize()}V3", "ModelBuilder"), "algo": algo,
+                "job": S.job_v3(job, dest=m.model_id, dest_kind="Model") if job is not None else
                 S.job_v3(key_name=f"job_{m.model_id}", dest=m.model_id, dest_kind="Model",
                          description=f"{algo} Model Build"),
                 "messages": [], "error_count": 0, "parameters": None}
+        return spmd.Deferred(resp, work, job) if defer else resp
 
     app.add_api_route("/99/ModelBuilders/{algo}", app.routes[-1].endpoint, methods=["POST"],
                       name="POST /99/ModelBuilders/{algo}")
@@ -870,7 +958,7 @@ def create_app(flow_dir: str | None = None) -> FastAPI:
         tabs = m.partial_plot(fr, cols=list(cols), nbins=int(p.get("nbins", 20)), weight_column=wname,
                               include_na=bool(p.get("add_missing_na", False)), targets=p.get("targets"),
                               row_index=None if row is None or int(row) < 0 else int(row))
-        dest = p.get("destination_key") or f"pdp_{uuid.uuid4().hex[:8]}"
+        dest = p.get("destination_key") or f"pdp_{spmd.rand_hex(8)}"
         pdp[dest] = {"model_id": m.model_id, "frame_id": fr.frame_id, "tables": tabs}
         return S.job_v3(key_name=f"pdp_{dest}", dest=dest, description="PartialDependencePlot")
 
@@ -992,18 +1080,32 @@ def create_app(flow_dir: str | None = None) -> FastAPI:
         ignored = set(p.pop("ignored_columns", None) or [])
         x = [c for c in tf.names if c != y and c not in ignored] if isinstance(tf, H2OFrame) else None
         p.pop("_rest_version", None)
+        from ..core import job as jobmod
         g = H2OGridSearch(cls(**{k: v for k, v in p.items() if v is not None}), hyper, grid_id=gid,
                           search_criteria=crit)
-        g.train(x=x, y=y, training_frame=tf, validation_frame=vf)
-        dkv.put(g.grid_id, g)
-        for mid in g.model_ids:
-            mm = g.get_model(mid) if hasattr(g, "get_model") else dkv.get(mid)
-            if mm is not None:
-                dkv.put(mid, mm)
-        return {"__meta": S.meta("GridSearchSchemaV99", "Grid", 99), "grid_id": S.key(g.grid_id, "Grid"),
-                "job": S.job_v3(key_name=f"grid_{g.grid_id}", dest=g.grid_id, dest_kind="Grid",
-                                description="GridSearch"),
-                "total_models": len(g.model_ids)}
+        job = jobmod.Job("GridSearch", dest=g.grid_id, dest_kind="Grid").start()
+        job.spmd = cloud.is_distributed()
+        dkv.put(g.grid_id, g)           # visible (and growing) while the search runs
+
+        def work():
+            try:
+                g.train(x=x, y=y, training_frame=tf, validation_frame=vf)
+            finally:
+                dkv.put(g.grid_id, g)
+                for mid in g.model_ids:
+                    mm = g.get_model(mid) if hasattr(g, "get_model") else dkv.get(mid)
+                    if mm is not None:
+                        dkv.put(mid, mm)
+
+        resp = {"__meta": S.meta("GridSearchSchemaV99", "Grid", 99), "grid_id": S.key(g.grid_id, "Grid"),
+                "job": None, "total_models": 0}
+        if spmd.defer_allowed():
+            resp["job"] = S.job_v3(job)
+            return spmd.Deferred(resp, work, job)
+        spmd.Deferred(resp, work, job).run()
+        resp["job"] = S.job_v3(job)
+        resp["total_models"] = len(g.model_ids)
+        return resp
 
     def _metric_of(mid, name):
         """Sort key of a grid model (hex/grid/Grid.java sorting): the metric of
@@ -1064,17 +1166,32 @@ def create_app(flow_dir: str | None = None) -> FastAPI:
                         max_models=sc.get("max_models"), max_runtime_secs=sc.get("max_runtime_secs"),
                         seed=sc.get("seed"), exclude_algos=bm.get("exclude_algos"),
                         include_algos=bm.get("include_algos"), sort_metric=ispec.get("sort_metric", "AUTO"))
+        from ..core import job as jobmod
         y = ispec.get("response_column")
         ign = set(ispec.get("ignored_columns") or [])
         x = [c for c in tf.names if c != y and c not in ign]
-        aml.train(x=x, y=y, training_frame=tf,
-                  validation_frame=dkv.get(ispec["validation_frame"]) if ispec.get("validation_frame") else None,
-                  leaderboard_frame=dkv.get(ispec["leaderboard_frame"]) if ispec.get("leaderboard_frame") else None)
-        dkv.put(aml.project_name, aml)
-        return {"__meta": S.meta("AutoMLBuildSpecV99", "AutoMLBuildSpec", 99),
-                "job": S.job_v3(key_name=f"automl_{aml.project_name}", dest=aml.project_name, dest_kind="AutoML",
-                                description="AutoML"),
+        job = jobmod.Job("AutoML", dest=aml.project_name, dest_kind="AutoML",
+                         key=f"automl_{aml.project_name}_{dkv.make_key('amljob')}").start()
+        job.spmd = cloud.is_distributed()
+
+        def work():
+            try:
+                aml.train(x=x, y=y, training_frame=tf,
+                          validation_frame=dkv.get(ispec["validation_frame"]) if ispec.get("validation_frame")
+                          else None,
+                          leaderboard_frame=dkv.get(ispec["leaderboard_frame"]) if ispec.get("leaderboard_frame")
+                          else None)
+            finally:
+                dkv.put(aml.project_name, aml)
+
+        resp = {"__meta": S.meta("AutoMLBuildSpecV99", "AutoMLBuildSpec", 99), "job": None,
                 "build_control": {"project_name": aml.project_name}}
+        if spmd.defer_allowed():
+            resp["job"] = S.job_v3(job)
+            return spmd.Deferred(resp, work, job)
+        spmd.Deferred(resp, work, job).run()
+        resp["job"] = S.job_v3(job)
+        return resp
 
     def _lb_table(aml):
         lb = aml.leaderboard.as_data_frame()
@@ -1121,11 +1238,11 @@ def create_app(flow_dir: str | None = None) -> FastAPI:
         """Run one notebook cell server-side (flow.py); variables persist
         across cells like Flow's notebook sandbox."""
         body = await request.json()
+        cmd = {"kind": "flow", "input": body.get("input", ""), "type": body.get("type", "cs"), "defer": False}
         try:
-            res = flow_runner.run_cell(body.get("input", ""), body.get("type", "cs"))
+            return await asyncio.wrap_future(executor.submit(cmd))
         except (FlowError, FlowSyntaxError) as e:
             return JSONResponse({"ok": False, "error": str(e)}, status_code=400)
-        return JSONResponse({"ok": True, "result": S.jsonable(res)})
 
     @app.get("/flow/routines", include_in_schema=False)
     async def flow_routines():
@@ -1226,10 +1343,28 @@ def create_server_app(login_conf=None, realm="h2o", flow_dir=None):
 
 def start(ip="127.0.0.1", port=54321, log_level="warning", login_conf=None, ssl_certfile=None, ssl_keyfile=None,
           flow_dir=None):
-    """Serve the REST API (blocking) on rank 0 of a single-process cloud;
-    login_conf enables Basic auth (the reference's -hash_login), the PEM
-    pair enables HTTPS."""
+    """Serve the REST API (blocking).  In a multi-rank cloud (torchrun
+    --nproc-per-node N -m h2o3_amd.server) rank 0 serves HTTP and replays
+    every command on ranks 1..N-1, which run spmd.worker_loop until rank 0
+    shuts the cloud down; login_conf enables Basic auth (the reference's
+    -hash_login), the PEM pair enables HTTPS."""
     import uvicorn
     api.init()
-    uvicorn.run(create_server_app(login_conf, flow_dir=flow_dir), host=ip, port=port, log_level=log_level,
-                ssl_certfile=ssl_certfile, ssl_keyfile=ssl_keyfile)
+    if cloud.rank() != 0:
+        app = create_app(flow_dir, serve=False)
+        spmd.worker_loop(app.state.run_command)
+        return
+    inner = create_app(flow_dir)
+    outer = inner
+    if login_conf:
+        from .auth import basic_auth_middleware, load_realm
+        outer = basic_auth_middleware(inner, load_realm(login_conf), "h2o")
+    server = uvicorn.Server(uvicorn.Config(outer, host=ip, port=port, log_level=log_level,
+                                           ssl_certfile=ssl_certfile, ssl_keyfile=ssl_keyfile))
+    inner.state.uvicorn = server
+    try:
+        server.run()
+    finally:
+        ex = inner.state.executor
+        if ex is not None and not ex.stopped and cloud.healthy():
+            ex.submit({"kind": "stop"}).result(timeout=600)

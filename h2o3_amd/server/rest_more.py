@@ -380,8 +380,8 @@ def register(app, route, ctx):
         applied in order (water/rapids/Assembly.java, transforms/*)."""
         import ast as _ast
         import re
-        import uuid as _uuid
         from ..core.rapids import rapids
+        from .spmd import rand_hex
         steps = p.get("steps") or []
         if isinstance(steps, str):
             steps = _ast.literal_eval(steps)
@@ -390,7 +390,7 @@ def register(app, route, ctx):
         done = []
         for st in steps:
             name, cls, expr, inplace, newcols = st.split("__", 4) if st.count("__") >= 4 else (st, "", "", "", "")
-            tmp = f"_asm_{_uuid.uuid4().hex[:12]}"
+            tmp = f"_asm_{rand_hex(12)}"
             dkv.put(tmp, cur)
             try:
                 res = rapids(re.sub(r"\bdummy\b", tmp, expr))
@@ -410,7 +410,7 @@ def register(app, route, ctx):
                         res.names = names
                     cur = cur.cbind(res)
             done.append((name, cls))
-        aid = f"Assembly_{_uuid.uuid4().hex[:16]}"
+        aid = f"Assembly_{rand_hex(16)}"
         assemblies[aid] = {"steps": done, "frame": fr.frame_id}
         rid = _put_frame(cur, f"{aid}_result")
         return {"__meta": S.meta("AssemblyV99", "Iced", 99), "assembly": S.key(aid, "Assembly"),

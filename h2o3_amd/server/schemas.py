@@ -304,15 +304,20 @@ def error_v3(msg: str, status: int, exc: BaseException | None = None, builder: b
 def job_v3(job=None, *, key_name=None, dest=None, dest_kind="Frame", description="", status="DONE",
            exception=None) -> dict:
     """JobV3; `job` is an h2o3_amd Job record or None (synthetic finished job)."""
+    msg, stack, warns = None, None, None
     if job is not None:
         key_name = job.key
         dest = job.dest
+        dest_kind = getattr(job, "dest_kind", None) or dest_kind
         description = job.description or description
         status = job.status
         exception = job.exception
         start = int((job.start_time or time.time()) * 1000)
         msec = int(1000 * ((job.end_time or time.time()) - (job.start_time or time.time())))
         progress = float(job.progress)
+        msg = getattr(job, "progress_msg", None) or None
+        stack = getattr(job, "stacktrace", None)
+        warns = list(getattr(job, "warnings", None) or []) or None
     else:
         start, msec, progress = int(time.time() * 1000), 0, 1.0 if status == "DONE" else 0.0
     status = {"CREATED": "CREATED", "RUNNING": "RUNNING", "DONE": "DONE", "CANCELLED": "CANCELLED",
@@ -320,9 +325,9 @@ def job_v3(job=None, *, key_name=None, dest=None, dest_kind="Frame", description
     dk = key(dest, dest_kind) if dest is not None else None
     return {"__meta": meta("JobV3", "Job"), "key": key(key_name, "Job"), "description": description,
             "status": status, "progress": progress if status != "DONE" else 1.0,
-            "progress_msg": "Done." if status == "DONE" else status, "start_time": start, "msec": msec,
-            "dest": dk, "warnings": None, "exception": None if exception is None else str(exception),
-            "stacktrace": None, "auto_recoverable": False, "ready_for_view": status == "DONE"}
+            "progress_msg": "Done." if status == "DONE" else (msg or status), "start_time": start, "msec": msec,
+            "dest": dk, "warnings": warns, "exception": None if exception is None else str(exception),
+            "stacktrace": stack, "auto_recoverable": False, "ready_for_view": status == "DONE"}
 
 
 # ----------------------------------------------------------- frames

@@ -7,6 +7,16 @@ import h2o3_amd as h2o
 from h2o3_amd.server import create_app
 
 
+def _wait(c, job, timeout=120):
+    """Poll /3/Jobs/{key} like h2o-py's H2OJob.poll until the job leaves RUNNING."""
+    import time
+    t0 = time.time()
+    while job["status"] in ("CREATED", "RUNNING") and time.time() - t0 < timeout:
+        time.sleep(0.05)
+        job = c.get(f"/3/Jobs/{job['key']['name']}").json()["jobs"][0]
+    return job
+
+
 def test_rest_roundtrip():
     h2o.init()
     c = TestClient(create_app())
@@ -20,7 +30,7 @@ def test_rest_roundtrip():
     assert fj["rows"] == 200 and fj["column_count"] == 3
     r = c.post("/3/ModelBuilders/gbm", json={"training_frame": "train.hex", "response_column": "y", "ntrees": 5,
                                               "model_id": "gbm_rest"})
-    job = r.json()["job"]
+    job = _wait(c, r.json()["job"])
     assert job["status"] == "DONE" and job["dest"]["name"] == "gbm_rest"
     mj = c.get("/3/Models/gbm_rest").json()["models"][0]
     assert mj["algo"] == "gbm" and mj["output"]["training_metrics"]["AUC"] > 0.9
@@ -47,7 +57,7 @@ def test_rest_parse_grid_automl_mojo(tmp_path):
     assert "a,b,y" in c.get("/3/DownloadDataset", params={"frame_id": "d.hex"}).text
     g = c.post("/99/Grid/gbm", json={"training_frame": "d.hex", "response_column": "y", "ntrees": 3,
                                       "hyper_parameters": {"max_depth": [2, 3]}, "grid_id": "g_rest"}).json()
-    assert g["job"]["status"] == "DONE"
+    assert _wait(c, g["job"])["status"] == "DONE"
     gj = c.get("/99/Grids/g_rest").json()
     assert len(gj["model_ids"]) == 2
     mid = gj["model_ids"][0]["name"]
@@ -61,6 +71,7 @@ def test_rest_parse_grid_automl_mojo(tmp_path):
                                           "input_spec": {"training_frame": "d.hex", "response_column": "y"},
                                           "build_models": {"include_algos": ["GLM", "GBM"]}}).json()
     assert a["job"]["dest"]["name"] == "aml_rest"
+    assert _wait(c, a["job"], timeout=300)["status"] == "DONE"
     lb = c.get("/99/Leaderboards/aml_rest").json()
     assert len(lb["models"]) >= 2
     assert c.get("/3/About").status_code == 200
