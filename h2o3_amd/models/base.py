@@ -163,10 +163,36 @@ class ScoreKeeper:
         return not (last > ref * (1 + tol) if ref >= 0 else last > ref * (1 - tol))
 
 
+def _encoding_wrapper(fn):
+    """Route a frame-taking scoring method through the model's fitted
+    categorical encoding (idempotent on already-encoded frames)."""
+    import functools
+
+    @functools.wraps(fn)
+    def w(self, frame, *a, **k):
+        enc = self.__dict__.get("_catenc")
+        if enc is not None and frame is not None and hasattr(frame, "_vecs"):
+            frame = enc.transform(frame)
+        return fn(self, frame, *a, **k)
+    w._catenc_wrapped = True
+    return w
+
+
 class H2OEstimator:
     algo = "base"
     supervised_learning = True
     _defaults: dict = {}
+    # methods that turn a scoring frame into model inputs: wrapped so a model
+    # trained with a categorical_encoding sees encoded frames everywhere
+    _ENCODED_METHODS = ("_predict_raw", "_score_matrix", "_design", "predict_leaf_node_assignment",
+                        "staged_predict_proba", "predict_contributions", "_unsupervised_perf")
+
+    def __init_subclass__(cls, **kw):
+        super().__init_subclass__(**kw)
+        for name in cls._ENCODED_METHODS:
+            fn = cls.__dict__.get(name)
+            if fn is not None and callable(fn) and not getattr(fn, "_catenc_wrapped", False):
+                setattr(cls, name, _encoding_wrapper(fn))
 
     def __init__(self, **kwargs):
         parms = dict(COMMON_DEFAULTS)
@@ -287,6 +313,19 @@ class H2OEstimator:
             if validation_frame is not None and y in validation_frame.names:
                 validation_frame = validation_frame[:, :]
                 validation_frame[y] = validation_frame[y].asfactor()
+        # categorical_encoding (hex/Model.java:355, FrameUtils.categoricalEncoder):
+        # fitted on the training frame, kept on the model, applied to every
+        # frame it scores (see _encode / __init_subclass__)
+        from . import catenc as _catenc
+        self._catenc = None
+        enc = _catenc.for_estimator(self)
+        if enc is not None:
+            enc.fit(training_frame, x, y, p.get("weights_column"))
+            training_frame = enc.transform(training_frame)
+            if validation_frame is not None:
+                validation_frame = enc.transform(validation_frame)
+            x = list(enc.out_names)
+            self._catenc = enc
         self._start_time = int(time.time() * 1000)
         t0 = time.time()
         from ..core import job as _jobmod

@@ -238,6 +238,8 @@ class MojoModel:
     def predict_raw(self, df):
         m = self.meta
         a = self.algo
+        if m.get("catenc") and not getattr(df, "_catenc_done", False):
+            df = encode_df(df, m["catenc"])
         if a in ("gbm", "xgboost"):
             X = self._tree_matrix(df)
             K = m["K"]
@@ -690,3 +692,57 @@ class EasyPredictModelWrapper:
 
 def load(path):
     return MojoModel.load(path)
+
+
+def _level_index(v, pos):
+    if v is None or (isinstance(v, float) and v != v):
+        return -1
+    if isinstance(v, str):
+        return pos.get(v, -1)
+    key = str(int(v)) if float(v).is_integer() else str(v)
+    return pos.get(key, pos.get(str(v), -1))
+
+
+def encode_df(df, d):
+    """The model's categorical_encoding on a pandas frame (the numpy twin of
+    models/catenc.py CategoricalEncoder.transform; h2o-genmodel
+    CategoricalEncoding)."""
+    import pandas as pd
+    sch = d["scheme"]
+    out, exp = {}, {}
+    for c in df.columns:
+        st = d["cols"].get(c)
+        if st is None or c not in d["x_in"]:
+            out[c] = df[c].values
+            continue
+        dom = st["domain"]
+        L = len(dom)
+        pos = {v: i for i, v in enumerate(dom)}
+        codes = np.array([_level_index(v, pos) for v in df[c].tolist()], dtype=np.int64)
+        if sch == "OneHotExplicit":
+            idx = np.where(codes < 0, L, codes)
+            for j, nm in enumerate([f"{c}.{x}" for x in dom] + [f"{c}.missing(NA)"]):
+                exp[nm] = (idx == j).astype(np.float64)
+        elif sch == "Binary":
+            val = np.where(codes < 0, 0, codes + 1)
+            nb = 1 + int(np.floor(np.log2(L))) if L > 0 else 1
+            for k in range(nb):
+                exp[f"{c}:{k}"] = ((val >> k) & 1).astype(np.float64)
+        elif sch == "LabelEncoder":
+            out[c] = np.where(codes < 0, np.nan, codes.astype(np.float64))
+        elif sch == "EnumLimited":
+            if not st.get("limited"):
+                out[c] = df[c].values
+            else:
+                lut = np.asarray(st["lut"], dtype=np.int64)
+                nc = lut[np.where(codes < 0, L, codes)]
+                nd = np.array(list(st["new_domain"]) + [None], dtype=object)
+                out[st["name"]] = nd[np.where(nc < 0, len(nd) - 1, nc)]
+        elif sch == "Eigen":
+            proj = np.asarray(st["proj"], dtype=np.float32).astype(np.float64)
+            out[f"{c}.Eigen"] = np.where(codes < 0, np.nan, proj[np.clip(codes, 0, None)] if L else 0.0)
+        else:   # SortByResponse: same level names, reordered domain (names carry the meaning)
+            out[c] = df[c].values
+    res = pd.DataFrame({**out, **exp}, index=df.index)
+    res._catenc_done = True
+    return res

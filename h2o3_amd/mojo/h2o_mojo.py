@@ -374,9 +374,8 @@ class H2OMojoModel:
             if self.info["calib_method"] != "platt":
                 raise ValueError(f"unknown calibration method {self.info['calib_method']}")
             self.calib_beta = list(self.kv("calib_glm_beta", []))
-        enc = str(self.kv("_genmodel_encoding", "AUTO"))
-        if enc not in ("AUTO", "Enum", "SortByResponse"):
-            raise NotImplementedError(f"tree MOJO with categorical encoding {enc} is not supported")
+        enc = str(self.kv("_genmodel_encoding", "AUTO")) if self.version >= 1.40 else "AUTO"
+        self.catenc = self._orig_encoding(enc)
 
     def _load_gbm(self):
         self._load_trees()
@@ -779,12 +778,54 @@ class H2OMojoModel:
             w = np.asarray(self.kv(f"weight_layer{li}", []), dtype=np.float32).astype(np.float64)
             self.dl_layers.append((w, b))
         enc = str(self.kv("_genmodel_encoding", "AUTO")) if self.version >= 1.10 else "AUTO"
-        if enc not in ("AUTO", "OneHotInternal"):
-            raise NotImplementedError(f"deep learning MOJO with categorical encoding {enc} is not supported")
+        self.catenc = self._orig_encoding(enc)
         nl = len(self.dl_units) - 1
         out_act = self.dl_activation if self.category == "AutoEncoder" else (
             "Softmax" if self.nclasses > 1 else "Linear")
         self.dl_acts = [self.dl_activation] * (nl - 1) + [out_act]
+
+    def _orig_encoding(self, enc):
+        """A non-AUTO categorical_encoding (hex.genmodel.CategoricalEncoding):
+        the original columns / domains (_orig_names, _orig_domain_values_i,
+        _orig_projection_array) turned into the encoding record that
+        mojo/genmodel.encode_df replays before the model columns are read
+        (OneHotEncoder, BinaryEncoder, LabelEncoder, EnumLimitedEncoder,
+        EigenEncoder of h2o-genmodel's easy package)."""
+        if enc in ("AUTO", "Enum", "SortByResponse", "OneHotInternal"):
+            return None
+        if enc not in ("OneHotExplicit", "Binary", "LabelEncoder", "EnumLimited", "Eigen"):
+            raise NotImplementedError(f"MOJO categorical encoding {enc} is not supported")
+        n = int(self.kv("_n_orig_names", 0) or 0)
+        names = self.be.text("_orig_names")[:n] if n else []
+        nd = int(self.kv("_n_orig_domain_values", 0) or 0)
+        doms = []
+        for i in range(nd):
+            m = int(self.kv(f"_m_orig_domain_values_{i}", 0) or 0)
+            doms.append([x.replace("\\n", "\n") for x in self.be.text(f"_orig_domain_values_{i}")[:m]]
+                        if m > 0 else None)
+        resp = self.response
+        x_in = [c for c in names if c != resp]
+        proj = list(self.kv("_orig_projection_array", []) or [])
+        cols, pos = {}, 0
+        for i, c in enumerate(names):
+            d = doms[i] if i < len(doms) else None
+            if c == resp or d is None:
+                continue
+            st = {"domain": list(d)}
+            if enc == "EnumLimited":
+                mc = next((cc for cc in self.columns if cc.startswith(c + ".top_") and cc.endswith("_levels")), c)
+                nd_ = list(self.domains[self.columns.index(mc)] or []) if mc in self.columns else []
+                st["limited"] = mc != c
+                if st["limited"]:
+                    other = nd_.index("other") if "other" in nd_ else -1
+                    idx = {v: j for j, v in enumerate(nd_)}
+                    st["lut"] = [idx.get(v, other) for v in d] + [idx.get("NA", other)]
+                    st["new_domain"], st["name"] = nd_, mc
+            elif enc == "Eigen":
+                st["proj"] = proj[pos:pos + len(d)]
+                pos += len(d)
+            cols[c] = st
+        return {"scheme": enc, "max_levels": 10, "x_in": x_in, "cols": cols}
 
     # --------------------------------------------------------------- inputs
     def row_matrix(self, df) -> np.ndarray:
@@ -796,6 +837,9 @@ class H2OMojoModel:
         if isinstance(df, dict):
             multi = any(isinstance(v, (list, tuple, np.ndarray, pd.Series)) for v in df.values())
             df = pd.DataFrame(df) if multi else pd.DataFrame([df])
+        if getattr(self, "catenc", None) and not getattr(df, "_catenc_done", False):
+            from .genmodel import encode_df
+            df = encode_df(df, self.catenc)
         n = len(df)
         X = np.full((n, len(self.columns)), np.nan)
         for j, c in enumerate(self.columns):

@@ -254,6 +254,32 @@ def _encode_aux(tree, leaf_map=None):
     return rec.tobytes()
 
 
+def _encoding_kv(model, supervised=True):
+    """categorical_encoding of the model in the reference layout
+    (SharedTreeMojoWriter / DeepLearningMojoWriter: _genmodel_encoding,
+    _orig_names, _orig_domain_values_i, _orig_projection_array); returns
+    (info keys, extra files)."""
+    enc = getattr(model, "_catenc", None)
+    if enc is None:
+        return {"_genmodel_encoding": "AUTO"}, {}
+    spec = model._spec
+    names = list(enc.x_in) + ([spec.y] if supervised and spec.y else [])
+    doms = [enc.cols[c]["domain"] if c in enc.cols else None for c in enc.x_in]
+    if supervised and spec.y:
+        doms.append(list(spec.response_domain) if spec.response_domain else None)
+    info = {"_genmodel_encoding": enc.scheme, "_n_orig_names": len(names), "_n_orig_domain_values": len(doms)}
+    esc = lambda v: "\n".join(str(x).replace("\n", "\\n") for x in v) + "\n"   # noqa: E731
+    files = {"_orig_names": esc(names)}
+    for i, d in enumerate(doms):
+        info[f"_m_orig_domain_values_{i}"] = 0 if d is None else len(d)
+        if d is not None:
+            files[f"_orig_domain_values_{i}"] = esc(d)
+    if enc.scheme == "Eigen":
+        info["_orig_projection_array"] = [float(v) for c in enc.x_in if c in enc.cols
+                                          for v in enc.cols[c]["proj"]]
+    return info, files
+
+
 def _tree_model(model, z, algo_short, algo_full, extra, leaf_maps, supervised=True, category=None):
     spec = model._spec
     x = list(spec.x)
@@ -264,10 +290,12 @@ def _tree_model(model, z, algo_short, algo_full, extra, leaf_maps, supervised=Tr
     K = model._n_tree_classes()
     ng = len(model._forest) // max(K, 1)
     cat = category or ("Binomial" if spec.nclasses == 2 else "Multinomial" if spec.nclasses > 2 else "Regression")
-    info = {"n_trees": ng, "n_trees_per_class": K, "_genmodel_encoding": "AUTO"}
+    enc_info, enc_files = _encoding_kv(model, supervised)
+    info = {"n_trees": ng, "n_trees_per_class": K, **enc_info}
     info.update(extra)
     ini, files = _header(model, algo_short, algo_full, cat, columns, len(x), spec.nclasses if supervised else 1,
                          domains, TREE_MOJO_VERSION, info, supervised=supervised)
+    files.update(enc_files)
     z.write("model.ini", ini)
     for k, v in files.items():
         z.write(k, v)
@@ -734,7 +762,9 @@ def _deeplearning(model, z):
              ("bernoulli" if spec.nclasses == 2 else "multinomial"),
              "mean_imputation": True, "cat_modes": [int(di.cat_modes[c]) for c in cats], "mini_batch_size": 1,
              "neural_network_sizes": units,
-             "hidden_dropout_ratios": [float(L.drop) for L in layers[:-1]], "_genmodel_encoding": "AUTO"}
+             "hidden_dropout_ratios": [float(L.drop) for L in layers[:-1]]}
+    enc_info, enc_files = _encoding_kv(model)
+    extra.update(enc_info)
     if di.standardize and nums:
         extra["norm_mul"] = [1.0 / float(s) for s in di.sigmas]
         extra["norm_sub"] = [float(m) for m in di.means]
@@ -757,6 +787,7 @@ def _deeplearning(model, z):
     cat = "Binomial" if spec.nclasses == 2 else "Multinomial" if spec.nclasses > 2 else "Regression"
     ini, files = _header(model, "deeplearning", "Deep Learning", cat, columns, len(cats) + len(nums), spec.nclasses,
                          domains, "1.10", extra)
+    files.update(enc_files)
     z.write("model.ini", ini)
     for k, v in files.items():
         z.write(k, v)

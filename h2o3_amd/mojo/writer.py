@@ -117,6 +117,8 @@ def build_mojo(model) -> bytes:
     w.meta["response_domain"] = spec.response_domain if spec is not None else None
     w.meta["nclasses"] = spec.nclasses if spec is not None else 1
     w.meta["model_id"] = model.model_id
+    if getattr(model, "_catenc", None) is not None:
+        w.meta["catenc"] = model._catenc.to_dict()     # categorical_encoding, replayed by the scorer
     domains = []
     if algo in ("gbm", "drf", "xgboost", "isolationforest"):
         w.meta["x_domains"] = getattr(model, "_x_domains", {})

@@ -28,14 +28,17 @@ def _free_port():
     return p
 
 
-def _launch(world):
+def _launch(world, gpu=False):
     http = _free_port()
     mport = _free_port()
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(mport), CUDA_VISIBLE_DEVICES="", OMP_NUM_THREADS="2",
-                   PYTHONPATH=ROOT, H2O3_SPMD_IDLE_S="5")
+                   MASTER_PORT=str(mport), OMP_NUM_THREADS="2", PYTHONPATH=ROOT, H2O3_SPMD_IDLE_S="5")
+        if gpu:
+            env["H2O3_DIST_BACKEND"] = "gloo"      # N ranks share the box's one GPU: gloo data plane
+        else:
+            env["CUDA_VISIBLE_DEVICES"] = ""
         procs.append(subprocess.Popen([sys.executable, "-u", "-m", "h2o3_amd.server", "--port", str(http)],
                                       env=env, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
                                       start_new_session=True))
@@ -207,3 +210,42 @@ def test_reference_python_client_munging_models_more_on_two_ranks(cloud2):
     test_rest_wire.test_reference_python_client_munging(cloud2)
     test_rest_wire.test_reference_python_client_models(cloud2)
     test_rest_wire.test_reference_python_client_inspection_and_persistence(cloud2)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_two_rank_gpu_cloud_over_rest():
+    """Both ranks on the GPU (sharing the box's one device): the executor
+    thread binds the rank's HIP device, a GBM built over REST equals the
+    1-rank GPU model, and a long build cancels cleanly."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    df = _data(20000, 3)
+    out = {}
+    for world in (1, 2):
+        url, procs = _launch(world, gpu=True)
+        try:
+            j = requests.get(url + "/3/Cloud").json()
+            assert j["cloud_size"] == world
+            _upload(url, df, "g.hex")
+            g = _build(url, "gbm", {"training_frame": "g.hex", "response_column": "y", "ntrees": 10,
+                                    "max_depth": 5, "seed": 3, "model_id": "gbm_gpu", "ignored_columns": ["r"]})
+            out[world] = g["training_metrics"]["logloss"]
+            if world == 2:
+                r = requests.post(url + "/3/ModelBuilders/gbm", json={"training_frame": "g.hex",
+                                                                      "response_column": "y", "ntrees": 100000,
+                                                                      "model_id": "gbm_long"})
+                job = r.json()["job"]
+                t0 = time.time()
+                while time.time() - t0 < 60:
+                    job = requests.get(url + f"/3/Jobs/{job['key']['name']}").json()["jobs"][0]
+                    if job["progress"] > 0:
+                        break
+                    time.sleep(0.05)
+                requests.post(url + f"/3/Jobs/{job['key']['name']}/cancel")
+                assert _wait(url, job, timeout=60)["status"] == "CANCELLED"
+                assert requests.get(url + "/3/Frames/g.hex").json()["frames"][0]["rows"] == 20000
+        finally:
+            _stop(url, procs)
+    assert abs(out[1] - out[2]) < 1e-5
