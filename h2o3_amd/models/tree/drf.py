@@ -49,6 +49,9 @@ class H2ORandomForestEstimator(SharedTreeEstimator):
         p = self._parms
         drv = DRFDriver(self, spec)
         ntrees = int(p["ntrees"])
+        start = 0
+        if p.get("checkpoint") is not None:
+            start = self._resume_from(drv, p["checkpoint"])
         t0 = time.time()
         max_rt = float(p.get("max_runtime_secs") or 0)
         self._scoring_history = []
@@ -56,7 +59,7 @@ class H2ORandomForestEstimator(SharedTreeEstimator):
         metric_name = self._stopping_metric(spec)
         history = []
         sched = ScoreSchedule(p)
-        for t in range(ntrees):
+        for t in range(start, ntrees):
             drv.step()
             # a max_runtime_secs stop scores the last tree into the history too
             score, timed_out = self._tick(t + 1, ntrees, sched, t + 1 == ntrees, t0, max_rt)
@@ -84,6 +87,7 @@ class H2ORandomForestEstimator(SharedTreeEstimator):
                                          "max_depth": max((tt.max_depth() for tt in forest.trees), default=0),
                                          "mean_leaves": float(np.mean([len(tt.leaves()) for tt in forest.trees]))}
         # out-of-bag predictions -> training metrics (reference reports OOB)
+        self._oob_state = (drv.oob_sum, drv.oob_cnt)     # kept for checkpoint continuation
         cnt = drv.oob_cnt.clamp_min(1).view(-1, 1)
         oobp = drv.oob_sum / cnt
         self._oob_raw = self._normalize(oobp)
@@ -97,6 +101,25 @@ class H2ORandomForestEstimator(SharedTreeEstimator):
         if m == "auto":
             return "logloss" if spec.is_classification else "deviance"
         return m
+
+    def _resume_from(self, drv, ck):
+        """Continue a forest (SharedTree.java:144): the checkpoint's trees are
+        kept, the OOB state is the checkpoint's when it was trained on these
+        rows (else rebuilt from its trees' in-bag draws is impossible: start
+        from its predictions as OOB estimates), and the iteration counter
+        resumes so the per-tree randomness continues the same stream."""
+        from .shared import checkpoint_model
+        prev, done = checkpoint_model(ck, "drf", self)
+        if prev._K != drv.K:
+            raise ValueError("checkpoint: the checkpoint model has a different number of classes / tree classes")
+        for t, k in zip(prev._forest.trees, prev._forest.tclass):
+            drv.forest.add(t, k)
+        st = getattr(prev, "_oob_state", None)
+        if st is not None and st[0].shape == drv.oob_sum.shape:
+            drv.oob_sum.copy_(st[0])
+            drv.oob_cnt.copy_(st[1])
+        drv.iter = done
+        return done
 
     def _score_entry(self, entry, spec, oob_sum, oob_cnt):
         """Scoring-history row: OOB training metrics (DRF.java scores OOB) plus
@@ -216,6 +239,8 @@ class DRFDriver:
     def step(self):
         p, spec, dev = self.est._parms, self.spec, self.dev
         N, F = self.bd.nrows_local, self.bd.F
+        from .shared import reseed_iteration
+        reseed_iteration(self, self.est._seed(), self.iter)
         srpc = p.get("sample_rate_per_class")
         if srpc is not None and spec.is_classification:
             rates = torch.tensor(srpc, dtype=torch.float32, device=dev)[self.ycode.clamp(min=0)]

@@ -52,6 +52,7 @@ class GrowParams:
     seed: int = 0
     hist_mem_budget: int = 8 << 30
     interaction_sets: list | None = None  # list of sets of feature ids
+    leaf_budget_by_gain: bool = False   # max_leaves spent on the highest-gain nodes first (lossguide)
 
 
 @dataclass
@@ -316,10 +317,36 @@ class TreeGrower:
         sel = np.argpartition(keys, k - 1, axis=1)[:, :k]
         return torch.from_numpy(np.sort(elig[sel], axis=1))
 
-    def _col_mask(self, n_nodes, depth, sel=None):
+    def _col_mask_allowed(self, allow, depth):
+        """Per-node mask under interaction constraints: the branch's allowed
+        features (BranchInteractionConstraints), column sampling among them
+        (DTree.UndecidedNode.scoreCols samples from the columns that still
+        have histograms)."""
+        p = self.p
+        F = self.bd.F
+        base = np.ones(F, dtype=bool) if p.tree_col_mask is None else p.tree_col_mask.astype(bool)
+        m = allow & base[None, :]
+        rate = p.col_sample_rate * (p.col_sample_rate_change_per_level ** depth)
+        for i in range(m.shape[0]):
+            elig = np.nonzero(m[i])[0]
+            k = p.mtries if (p.mtries is not None and p.mtries > 0) else (
+                max(1, int(math.floor(rate * elig.size + 0.5))) if rate < 1.0 else elig.size)
+            if 0 < k < elig.size:
+                keep = self.rng.choice(elig, size=k, replace=False)
+                m[i] = False
+                m[i, keep] = True
+        if self.Fpad > F:
+            m = np.concatenate([m, np.zeros((m.shape[0], self.Fpad - F), dtype=bool)], 1)
+        t = torch.from_numpy(np.ascontiguousarray(m))
+        t._all_true = False
+        return t
+
+    def _col_mask(self, n_nodes, depth, sel=None, allow=None):
         """[n, Fpad] bool mask of features eligible per node."""
         p = self.p
         F = self.bd.F
+        if allow is not None:
+            return self._col_mask_allowed(allow, depth)
         if sel is None:
             sel = self._col_sel(n_nodes, depth)
         if sel is not None:
@@ -335,6 +362,26 @@ class TreeGrower:
         t = torch.from_numpy(m)
         t._all_true = all_true
         return t
+
+    def _interaction_map(self):
+        """(allow [F, F] bool: features that may follow a split on f, root [F]
+        bool) from GrowParams.interaction_sets, or None."""
+        sets = self.p.interaction_sets
+        if not sets:
+            return None
+        F = self.bd.F
+        cached = self.__dict__.get("_ics_cache")
+        if cached is not None:
+            return cached
+        allow = np.zeros((F, F), dtype=bool)
+        root = np.zeros(F, dtype=bool)
+        for st in sets:
+            idx = np.asarray(sorted(st), dtype=np.int64)
+            root[idx] = True
+            for f in idx:
+                allow[f, idx] = True
+        self._ics_cache = (allow, root)
+        return self._ics_cache
 
     def _find_splits(self, H, col_mask, node_wyy=None, want_pk=False):
         """Dispatch: fused HIP kernel for numeric features on GPU (categorical
@@ -1178,6 +1225,11 @@ class TreeGrower:
         async_part = self.dev.type == "cuda" and not p.max_leaves and not self.use_payload and \
             tree_ops.env("H2O3_ASYNC_PART", "1") == "1" and tree_ops.env("H2O3_PART", "ballot") == "ballot"
         is_cat_np = np.asarray(bd.is_cat, dtype=bool)
+        # interaction constraints (GlobalInteractionConstraints /
+        # BranchInteractionConstraints): the features each frontier node may
+        # still split on; the root may use every feature named in a set
+        ics = self._interaction_map()
+        f_allow = ics[1][None, :].copy() if ics is not None else None
         cutmat = self._cut_matrix()
         lvmaps = self.__dict__.setdefault("_lvmaps", {})
         while f_id.size:
@@ -1188,7 +1240,7 @@ class TreeGrower:
             level_bytes = self.Fpad * n_front * bd.Bs * C_ * 8
             prev_bytes = 0 if H_prev is None else H_prev.numel() * 8
             chunked = can_split and (level_bytes + prev_bytes) > p.hist_mem_budget and n_front > 1
-            direct = can_split and self._direct_level(mode, depth, chunked)
+            direct = can_split and f_allow is None and self._direct_level(mode, depth, chunked)
             chunked = chunked or direct
             la, self._la = self._la, None
             if la is not None and (chunked or not can_split or la[0].shape[1] < n_front):
@@ -1242,7 +1294,8 @@ class TreeGrower:
             ok_h = None
             if can_split:
                 sel = self._col_sel(n_front, depth) if direct else None
-                cm = None if (direct and self.dev.type == "cuda") else self._col_mask(n_front, depth, sel=sel)
+                cm = None if (direct and self.dev.type == "cuda") else self._col_mask(n_front, depth, sel=sel,
+                                                                                      allow=f_allow)
                 # node totals of w*y*y (only the total enters the SE split test),
                 # fused into the histogram kernel; derived siblings by subtraction
                 node_wyy = wyy_level if mode == 0 else None
@@ -1339,10 +1392,15 @@ class TreeGrower:
                 ok = np.zeros(n_front, dtype=bool)
             if p.max_leaves:
                 # leaf budget, node by node in frontier order (the leaves of this
-                # level counted as they are decided)
+                # level counted as they are decided); lossguide spends it on the
+                # largest loss reductions first (XGBoost's best-first expansion
+                # order among the nodes of a level)
                 n_leaves = sum(part[0].size for part in leaf_parts)
                 n_split = 0
-                for i in range(n_front):
+                order = range(n_front)
+                if p.leaf_budget_by_gain and gains is not None:
+                    order = np.argsort(-np.where(ok, gains, -np.inf), kind="stable")
+                for i in order:
                     if ok[i] and (n_leaves + n_front + n_split + 1) > p.max_leaves:
                         ok[i] = False
                     if ok[i]:
@@ -1430,6 +1488,10 @@ class TreeGrower:
             f_st = np.stack([st_s, st_s + nleft], 1).reshape(-1)
             f_ct = np.stack([nleft, ct_s - nleft], 1).reshape(-1)
             f_tot = np.stack([Lsel, Rsel], 1).reshape(2 * k, -1)
+            if f_allow is not None:
+                # nextLevelInteractionConstraints: branch set ∩ the split feature's set
+                ca = f_allow[sids] & ics[0][f_s]
+                f_allow = np.repeat(ca, 2, axis=0)
             jj = 2 * np.arange(k, dtype=np.int64)
             p_build = jj + (~build_left)
             p_der = jj + build_left

@@ -125,9 +125,19 @@ class GBMDriver:
                         col_sample_rate=float(p["col_sample_rate"]),
                         col_sample_rate_change_per_level=float(p["col_sample_rate_change_per_level"]),
                         seed=self._seed())
-        mc = p.get("monotone_constraints")
-        if mc:
-            gp.monotone = np.array([float(mc.get(n, 0)) for n in spec.x])
+        from . import constraints as cons
+        gp.monotone = cons.monotone_vector(p.get("monotone_constraints"), list(spec.x))
+        self.mono_on = gp.monotone is not None
+        if self.mono_on:
+            cons.check_monotone_family(self.dist.family)
+        ic = p.get("interaction_constraints")
+        if ic:
+            from ..catenc import canon
+            if canon(p.get("categorical_encoding")) not in ("AUTO", "OneHotInternal"):
+                raise ValueError("interaction_constraints: Interaction constraints can be used when the "
+                                 "categorical encoding is set to AUTO (one_hot_internal or OneHotInternal) only.")
+            gp.interaction_sets = cons.interaction_sets(ic, list(spec.x), p)
+        self.noise_bw = float(p.get("pred_noise_bandwidth") or 0.0)
         self.gp = gp
         self.grower = TreeGrower(self.bd, gp)
         self._pending = None
@@ -246,6 +256,8 @@ class GBMDriver:
     def step(self):
         """One boosting iteration."""
         p = self.est._parms
+        from .shared import reseed_iteration
+        reseed_iteration(self, self._seed(), self.iter)
         w = self._row_weights()
         self.gp.tree_col_mask = self._tree_col_mask()
         lr = self.lr * (float(p.get("learn_rate_annealing", 1.0)) ** self.iter)
@@ -255,8 +267,10 @@ class GBMDriver:
             self._dpend = None
             f = self._f[:, 0]
             y = self.yb if self.spec.nclasses == 2 else torch.nan_to_num(self.yf)
+            # monotone bounds / prediction noise need the leaf values on the host
+            # before the prediction update: not the device-resident leaf path
             simple = self.dev.type == "cuda" and self.dist.family in ("gaussian", "bernoulli") and \
-                self.dist.link in ("identity", "logit")
+                self.dist.link in ("identity", "logit") and not self.mono_on and self.noise_bw == 0
             fused = simple and os.environ.get("H2O3_FUSED_LEAF", "0") == "1"
             # position-ordered residual payload + segment update: no per-row leaf ids at all
             posleaf = simple and not fused and self.K == 1 and self.f.shape[1] == 1 and \
@@ -353,13 +367,19 @@ class GBMDriver:
                     coll.allreduce_(s_)
                     sh = s_.cpu().numpy()
                     vals = np.where(sh[:, 1] != 0, sh[:, 0] / np.where(sh[:, 1] == 0, 1, sh[:, 1]), 0.0)
+                    self._last_den = sh[:, 1]
                 else:
+                    self._last_den = None
                     vals = self._gamma(tree, nid, leaves, w, y, z, f, 0)
             vals = np.clip(vals, -maxabs, maxabs)
+            if self.mono_on:
+                from .constraints import monotone_clamp
+                dens = self._last_den if self._last_den is not None else np.asarray(tree.weight)[leaves]
+                vals = monotone_clamp(tree, leaves, vals, dens, self.gp.monotone)
             for li, node in enumerate(leaves):
                 tree.value[node] = float(lr * vals[li])
             with phase("gbm.update"):
-                vt = torch.tensor(lr * vals, dtype=torch.float32, device=self.dev)
+                vt = torch.tensor(lr * vals * self._noise(0, len(leaves)), dtype=torch.float32, device=self.dev)
                 if posleaf:
                     lids, st, ct = self.grower.last_segs
                     tree_ops.leaf_update(self.grower.ridx, self.f, vt, lids, st, ct)
@@ -376,12 +396,20 @@ class GBMDriver:
                 vals = np.clip(vals, -maxabs, maxabs)
                 for li, node in enumerate(leaves):
                     tree.value[node] = float(lr * vals[li])
-                vt = torch.tensor(lr * vals, dtype=torch.float32, device=self.dev)
+                vt = torch.tensor(lr * vals * self._noise(k, len(leaves)), dtype=torch.float32, device=self.dev)
                 new.append(vt[nid.long()])
                 self.forest.add(tree, k)
             for k in range(self.K):
                 self.f[:, k] += new[k]
         self.iter += 1
+
+    def _noise(self, k, nleaves):
+        """pred_noise_bandwidth factors of this tree's leaves (1 when off)."""
+        if self.noise_bw == 0:
+            return 1.0
+        from .constraints import noise_factors
+        return noise_factors(self._seed(), k, int(self.est._parms.get("ntrees", 0)), self.iter, nleaves,
+                             self.noise_bw)
 
     def _update_huber_delta(self, y, f, w):
         r = (y - f).abs()
@@ -415,6 +443,7 @@ class GBMDriver:
         coll.allreduce_(s)
         sh = s.cpu().numpy()
         num, den = sh[:, 0], sh[:, 1]
+        self._last_den = den
         if self.dist.link == "log" or self.dist.family in ("poisson", "gamma", "tweedie"):
             return np.array([self.dist.gamma(float(a), float(b)) for a, b in zip(num, den)])
         out = np.where(den != 0, num / np.where(den == 0, 1, den), 0.0)
@@ -476,6 +505,10 @@ class H2OGradientBoostingEstimator(SharedTreeEstimator):
                         break
             if timed_out:
                 break
+            ckdir = p.get("in_training_checkpoints_dir")
+            if ckdir and drv.iter % max(1, int(p.get("in_training_checkpoints_tree_interval") or 1)) == 0 and \
+                    drv.iter < ntrees:
+                self._in_training_checkpoint(drv, ckdir)
         self._forest = drv.forest
         self._init_f = drv.init_f
         self._output["variable_importances"] = self._varimp_from_forest(drv.forest, spec.x)
@@ -492,6 +525,28 @@ class H2OGradientBoostingEstimator(SharedTreeEstimator):
         if p.get("calibrate_model") and p.get("calibration_frame") is not None:
             from .calibration import fit_calibration
             fit_calibration(self, p["calibration_frame"], p.get("calibration_method", "auto"))
+
+    def _in_training_checkpoint(self, drv, ckdir):
+        """GBM.java:921 doInTrainingCheckpoint: the model so far, exported as a
+        binary model `<dir>/<model_id>.ntrees_<n>` under key `<model_id>.<n>`
+        (reloadable with h2o.load_model, usable as a `checkpoint`)."""
+        import copy
+        import os
+        from ..persist import save_model
+        n = drv.iter
+        snap = copy.copy(self)
+        snap.__dict__ = dict(self.__dict__)
+        snap._parms = dict(self._parms)
+        snap._output = dict(self._output)
+        f = Forest()
+        for t, k in zip(drv.forest.trees, drv.forest.tclass):
+            f.add(t, k)
+        snap._forest, snap._init_f, snap._K = f, list(drv.init_f), drv.K
+        snap._id = f"{self._id}.{n}"
+        snap._driver = None
+        snap._output["model_summary"] = {"number_of_trees": n}
+        os.makedirs(ckdir, exist_ok=True)
+        save_model(snap, path=ckdir, force=True, filename=f"{self._id}.ntrees_{n}")
 
     def _cv_optimal_params(self, cv_models):
         if int(self._parms.get("stopping_rounds") or 0) > 0 and cv_models:
@@ -539,10 +594,8 @@ class H2OGradientBoostingEstimator(SharedTreeEstimator):
             entry[f"{prefix}_misclassification"] = m["cm"]["total_error"]
 
     def _resume_from(self, drv, ck):
-        from ...core import dkv
-        prev = dkv.get(ck) if isinstance(ck, str) else ck
-        if prev is None:
-            raise ValueError(f"checkpoint {ck} not found")
+        from .shared import checkpoint_model
+        prev, _ = checkpoint_model(ck, "gbm", self)
         drv.forest = Forest()
         for t, k in zip(prev._forest.trees, prev._forest.tclass):
             drv.forest.add(t, k)

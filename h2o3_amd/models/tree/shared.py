@@ -29,6 +29,42 @@ def _ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
 
 
+def iter_seed(seed, it, salt=0):
+    """Seed of boosting / forest iteration `it`: every tree's randomness
+    (row sample, per-tree and per-node column samples) is a function of
+    (seed, iteration) only, so a build continued from a checkpoint draws
+    exactly what an uninterrupted build draws for the same trees
+    (SharedTree.java:144 checkpoint restart)."""
+    return (int(seed) * 1000003 + int(it) * 7919 + int(salt) * 104729 + 12345) & 0x7FFFFFFF
+
+
+def reseed_iteration(drv, seed, it):
+    """Re-seed a driver's generators for iteration `it` (row sampling:
+    rank-dependent torch generator; host column sampling: rank-independent)."""
+    from ...parallel import cloud
+    drv.gen.manual_seed(iter_seed(seed, it, 1) + cloud.rank())
+    drv.rng = np.random.RandomState(iter_seed(seed, it, 2))
+    drv.grower.rng = np.random.RandomState(iter_seed(seed, it, 3))
+
+
+def checkpoint_model(ck, algo, est):
+    """The checkpoint model a build continues (hex/ModelBuilder checkpoint
+    checks: same algorithm, same response, the new ntrees must exceed the
+    checkpoint's)."""
+    from ...core import dkv
+    prev = dkv.get(ck) if isinstance(ck, str) else ck
+    if prev is None:
+        raise ValueError(f"checkpoint: model {ck} not found")
+    if getattr(prev, "algo", None) != algo:
+        raise ValueError(f"checkpoint: model {getattr(prev, 'model_id', ck)} is a {getattr(prev, 'algo', '?')} "
+                         f"model, not {algo}")
+    done = len(prev._forest) // max(1, prev._n_tree_classes())
+    if int(est._parms["ntrees"]) <= done:
+        raise ValueError(f"checkpoint: ntrees ({est._parms['ntrees']}) must be larger than the checkpoint "
+                         f"model's number of trees ({done})")
+    return prev, done
+
+
 def forest_varimp(forest, names):
     """Sum of positive split gains per feature over every split node
     (vectorized over each tree's node arrays)."""

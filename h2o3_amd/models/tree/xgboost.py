@@ -85,6 +85,7 @@ class H2OXGBoostEstimator(SharedTreeEstimator):
                 base_w = torch.where(yc == 1, base_w * float(p["scale_pos_weight"]), base_w)
         else:
             yv = torch.nan_to_num(y.to(torch.float32))
+            Y = None
             valid = ~torch.isnan(y.to(torch.float32))
         base_w = torch.where(valid, base_w, torch.zeros_like(base_w))
         # base score: 0.5 probability / mean (XGBoost default base_score=0.5)
@@ -100,26 +101,48 @@ class H2OXGBoostEstimator(SharedTreeEstimator):
         else:
             self._init_f = [0.0] * K
         f = torch.tensor(self._init_f, dtype=torch.float32, device=dev).view(1, -1).repeat(N, 1)
+        self._gblinear = None
+        if (p.get("booster") or "gbtree").lower() == "gblinear":
+            return self._fit_gblinear(spec, yv, Y, base_w, f, K)
+        tm = (p.get("tree_method") or "auto").lower()
+        if tm not in ("auto", "hist", "approx"):
+            raise ValueError(f"tree_method '{p.get('tree_method')}' is not supported: the trees are grown from "
+                             "quantile histograms (tree_method hist / approx); exact split enumeration is not "
+                             "implemented")
         gp = GrowParams(criterion="xgb", max_depth=int(p["max_depth"]) if int(p["max_depth"]) > 0 else 64,
                         min_rows=float(p["min_rows"]), reg_lambda=float(p["reg_lambda"]),
                         reg_alpha=float(p["reg_alpha"]), gamma=float(p["min_split_improvement"]),
                         col_sample_rate=float(p["col_sample_rate"]) * float(p.get("colsample_bynode", 1.0)),
                         max_leaves=int(p.get("max_leaves") or 0), seed=self._seed())
-        mc = p.get("monotone_constraints")
-        if mc:
-            gp.monotone = np.array([float(mc.get(n, 0)) for n in spec.x])
+        from . import constraints as cons
+        gp.monotone = cons.monotone_vector(p.get("monotone_constraints"), list(spec.x))
+        if p.get("interaction_constraints"):
+            gp.interaction_sets = cons.interaction_sets(p["interaction_constraints"], list(spec.x), p)
+        policy = (p.get("grow_policy") or "depthwise").lower()
+        if policy not in ("depthwise", "lossguide"):
+            raise ValueError(f"grow_policy must be depthwise or lossguide, got {p.get('grow_policy')}")
+        if policy == "lossguide":
+            # best-first: the leaf budget goes to the largest loss reductions;
+            # max_depth 0 means unlimited under lossguide (XGBoostModel.java:54)
+            gp.leaf_budget_by_gain = True
+            if int(p["max_depth"]) <= 0:
+                gp.max_depth = 64
         grower = TreeGrower(bd, gp)
         forest = Forest()
         eta = float(p["learn_rate"])
         mds = float(p.get("max_delta_step") or 0.0)
         mabs = float(p.get("max_abs_leafnode_pred") or 0.0)
-        gen = torch.Generator(device=dev)
-        gen.manual_seed(self._seed() + cloud.rank())
-        rng = np.random.RandomState(self._seed())
         booster = (p.get("booster") or "gbtree").lower()
         dart = booster == "dart"
         tree_w = []  # dart weights
         ntrees = int(p["ntrees"])
+        weighted_drop = (p.get("sample_type") or "uniform").lower() == "weighted"
+        if (p.get("sample_type") or "uniform").lower() not in ("uniform", "weighted"):
+            raise ValueError(f"sample_type must be uniform or weighted, got {p.get('sample_type')}")
+        start = 0
+        if p.get("checkpoint") is not None:
+            start, f, tree_w = self._resume_from(p["checkpoint"], forest, f, K)
+        from .shared import iter_seed
         sr = float(p["sample_rate"])
         F = bd.F
         interval = int(p.get("score_tree_interval") or 0)
@@ -132,7 +155,13 @@ class H2OXGBoostEstimator(SharedTreeEstimator):
         max_rt = float(p.get("max_runtime_secs") or 0)
         t0 = time.time()
         sched = ScoreSchedule(p)
-        for it in range(ntrees):
+        for it in range(start, ntrees):
+            # per-iteration randomness (checkpoint continuation draws what an
+            # uninterrupted build draws)
+            gen = torch.Generator(device=dev)
+            gen.manual_seed(iter_seed(self._seed(), it, 1) + cloud.rank())
+            rng = np.random.RandomState(iter_seed(self._seed(), it, 2))
+            grower.rng = np.random.RandomState(iter_seed(self._seed(), it, 3))
             wt = base_w
             if sr < 1.0:
                 wt = base_w * (torch.rand(N, generator=gen, device=dev) < sr)
@@ -147,7 +176,13 @@ class H2OXGBoostEstimator(SharedTreeEstimator):
             if dart and len(forest) and rng.rand() >= float(p.get("skip_drop", 0.0)):
                 nit = len(forest) // K
                 rd = float(p.get("rate_drop", 0.0))
-                dropped = [i for i in range(nit) if rng.rand() < rd]
+                if weighted_drop:
+                    # sample_type weighted: drop probability proportional to the tree weight
+                    tw = np.asarray(tree_w[:nit], dtype=np.float64)
+                    pr = rd * nit * tw / max(tw.sum(), 1e-300)
+                    dropped = [i for i in range(nit) if rng.rand() < pr[i]]
+                else:
+                    dropped = [i for i in range(nit) if rng.rand() < rd]
                 if not dropped and p.get("one_drop"):
                     dropped = [int(rng.randint(nit))]
                 if dropped:
@@ -156,7 +191,7 @@ class H2OXGBoostEstimator(SharedTreeEstimator):
                 g, h = self._dist.grad_hess(yv, f_use[:, 0])
                 g, h = (g * wt).to(torch.float32).contiguous(), (h * wt).to(torch.float32).contiguous()
                 tree, nid, leaves, tot = grower.grow(g, h, 1)
-                vals = self._leaf_values(tot, eta, mds, mabs, gp)
+                vals = self._leaf_values(tot, eta, mds, mabs, gp, tree, leaves)
                 for li, node in enumerate(leaves):
                     tree.value[node] = float(vals[li])
                 delta = torch.tensor(vals, dtype=torch.float32, device=dev)[nid.long()].view(-1, 1)
@@ -169,7 +204,7 @@ class H2OXGBoostEstimator(SharedTreeEstimator):
                     g = ((P[:, k] - Y[:, k]) * wt).contiguous()
                     h = (torch.clamp(2 * P[:, k] * (1 - P[:, k]), min=1e-16) * wt).contiguous()
                     tree, nid, leaves, tot = grower.grow(g, h, 1)
-                    vals = self._leaf_values(tot, eta, mds, mabs, gp)
+                    vals = self._leaf_values(tot, eta, mds, mabs, gp, tree, leaves)
                     for li, node in enumerate(leaves):
                         tree.value[node] = float(vals[li])
                     trees_it.append(tree)
@@ -225,6 +260,89 @@ class H2OXGBoostEstimator(SharedTreeEstimator):
         self._output["variable_importances"] = forest_varimp(forest, spec.x)
         self._output["model_summary"] = {"number_of_trees": len(forest) // K, "booster": booster}
 
+    @staticmethod
+    def _coord_delta(G, H, w, alpha, lam):
+        """XGBoost's CoordinateDelta (src/linear/coordinate_common.h): the L1/L2
+        regularised Newton step of one coefficient, never crossing zero."""
+        Gl = G + lam * w
+        Hl = H + lam
+        tmp = w - Gl / torch.where(Hl > 0, Hl, torch.ones_like(Hl))
+        up = torch.maximum(-(Gl + alpha) / Hl, -w)
+        dn = torch.minimum(-(Gl - alpha) / Hl, -w)
+        d = torch.where(tmp >= 0, up, dn)
+        return torch.where(H < 1e-5, torch.zeros_like(d), d)
+
+    def _fit_gblinear(self, spec, yv, Y, base_w, f, K):
+        """booster = gblinear (XGBoostModel.java:54): boosted linear model.
+        Each round: the bias Newton step, then every coefficient's
+        regularised coordinate step from the same gradient pairs (XGBoost's
+        shotgun updater, done as two GEMVs over the design in HBM: X^T g and
+        (X.X)^T h), all scaled by eta.  Penalties are denormalised by the
+        total row weight as XGBoost does (LinearTrainParam)."""
+        from ..datainfo import DataInfo
+        p = self._parms
+        di = DataInfo(spec.frame, spec.x, standardize=False, use_all_factor_levels=True, pad_to=1)
+        X = di.expand(spec.frame, pad=False)[0].to(torch.float32)
+        self._gbl_di = di
+        P = X.shape[1]
+        dev = X.device
+        wsum = coll.allreduce_scalar(float(base_w.sum()))
+        lam = float(p.get("reg_lambda", 1.0)) * wsum
+        alpha = float(p.get("reg_alpha", 0.0)) * wsum
+        eta = float(p["learn_rate"])
+        W = torch.zeros((P, K), dtype=torch.float64, device=dev)
+        b = torch.tensor(self._init_f, dtype=torch.float64, device=dev)
+        X2 = X * X
+        ntrees = int(p["ntrees"])
+        t0 = time.time()
+        max_rt = float(p.get("max_runtime_secs") or 0)
+        sched = ScoreSchedule(p)
+        self._scoring_history = []
+        f = f.to(torch.float64)
+        for it in range(ntrees):
+            if K == 1:
+                g, h = self._dist.grad_hess(yv, f[:, 0].to(torch.float32))
+                g, h = (g * base_w).to(torch.float64).view(-1, 1), (h * base_w).to(torch.float64).view(-1, 1)
+            else:
+                Pm = torch.softmax(f, 1)
+                g = ((Pm - Y) * base_w.view(-1, 1)).to(torch.float64)
+                h = (torch.clamp(2 * Pm * (1 - Pm), min=1e-16) * base_w.view(-1, 1)).to(torch.float64)
+            sg = torch.cat([g.sum(0), h.sum(0)])
+            coll.allreduce_(sg)
+            db = eta * torch.where(sg[K:] > 0, -sg[:K] / sg[K:].clamp_min(1e-300), torch.zeros_like(sg[:K]))
+            b = b + db
+            f = f + db.view(1, -1)
+            g = g + h * db.view(1, -1)                      # gradient pairs after the bias step
+            G = X.T.to(torch.float64) @ g
+            Hs = X2.T.to(torch.float64) @ h
+            coll.allreduce_many_([G, Hs])
+            dW = eta * self._coord_delta(G, Hs, W, alpha, lam)
+            W = W + dW
+            f = f + (X.to(torch.float64) @ dW)
+            score, timed_out = self._tick(it + 1, ntrees, sched, it + 1 == ntrees, t0, max_rt)
+            if score:
+                self._gblinear = (W, b)
+                entry = {"number_of_trees": it + 1}
+                self._score_entry(entry, spec, f.to(torch.float32))
+                self._scoring_history.append(entry)
+            if timed_out:
+                break
+        self._gblinear = (W, b)
+        self._forest = Forest()
+        self._train_f = f.to(torch.float32)
+        names = di.coef_names
+        imp = W.abs().sum(1).cpu().numpy()
+        order = np.argsort(-imp)
+        mx = float(imp.max()) if imp.size and imp.max() > 0 else 1.0
+        tot = float(imp.sum()) or 1.0
+        self._output["variable_importances"] = {"variable": [names[i] for i in order],
+                                                "relative_importance": [float(imp[i]) for i in order],
+                                                "scaled_importance": [float(imp[i] / mx) for i in order],
+                                                "percentage": [float(imp[i] / tot) for i in order]}
+        self._output["model_summary"] = {"number_of_trees": 0, "booster": "gblinear"}
+        self._output["coefficients"] = {n: W[i].cpu().tolist() for i, n in enumerate(names)}
+        self._output["intercept"] = b.cpu().tolist()
+
     def _raw_from_f(self, f):
         if self._K > 1:
             return torch.softmax(f, 1)
@@ -252,7 +370,7 @@ class H2OXGBoostEstimator(SharedTreeEstimator):
         return s * torch.tensor([tree_w[d] for d in dropped], device=X.device).mean() if dropped else out
 
     @staticmethod
-    def _leaf_values(tot, eta, mds, mabs, gp):
+    def _leaf_values(tot, eta, mds, mabs, gp, tree=None, leaves=None):
         tot = tot.numpy() if isinstance(tot, torch.Tensor) else np.asarray(tot)
         G, H = tot[:, 0], tot[:, 1]
         if gp.reg_alpha > 0:
@@ -260,19 +378,45 @@ class H2OXGBoostEstimator(SharedTreeEstimator):
         v = -G / (H + gp.reg_lambda)
         if mds > 0:
             v = np.clip(v, -mds, mds)
+        if gp.monotone is not None and tree is not None:
+            # XGBoost's monotone bounds (mid-point of the children's weights),
+            # leaf weights clamped into them
+            from .constraints import monotone_clamp
+            v = monotone_clamp(tree, leaves, v, H + gp.reg_lambda, gp.monotone)
         v = v * eta
         if mabs > 0:
             v = np.clip(v, -mabs, mabs)
         return v
+
+    def _resume_from(self, ck, forest, f, K):
+        """checkpoint (XGBoost.java:126, :429): the checkpoint's trees, its raw
+        predictions on the training rows, and the iteration counter."""
+        from .shared import checkpoint_model
+        prev, done = checkpoint_model(ck, "xgboost", self)
+        if prev._K != K:
+            raise ValueError("checkpoint: the checkpoint model has a different number of tree classes")
+        if (prev._parms.get("booster") or "gbtree").lower() != (self._parms.get("booster") or "gbtree").lower():
+            raise ValueError("checkpoint: booster must match the checkpoint model's")
+        for t, k in zip(prev._forest.trees, prev._forest.tclass):
+            forest.add(t, k)
+        X = self._score_matrix(self._spec.frame)
+        f = f + prev._forest.predict(X, K)
+        return done, f, [1.0] * done
 
     def _seed(self):
         s = self._parms.get("seed", -1)
         return 777 if s is None or s == -1 else int(s) & 0x7FFFFFFF
 
     def _predict_raw(self, frame):
-        X = self._score_matrix(frame)
         K = self._K
-        f = self._forest.predict(X, K) + torch.tensor(self._init_f, dtype=torch.float32, device=X.device).view(1, -1)
+        if getattr(self, "_gblinear", None) is not None:
+            W, b = self._gblinear
+            Xd = self._gbl_di.expand(frame, pad=False)[0].to(torch.float64)
+            f = (Xd @ W + b.view(1, -1)).to(torch.float32)
+        else:
+            X = self._score_matrix(frame)
+            f = self._forest.predict(X, K) + torch.tensor(self._init_f, dtype=torch.float32,
+                                                          device=X.device).view(1, -1)
         if K > 1:
             return torch.softmax(f, 1)
         mu = self._dist.linkinv(f[:, 0])
@@ -281,5 +425,7 @@ class H2OXGBoostEstimator(SharedTreeEstimator):
         return mu.view(-1, 1)
 
     def predict_contributions(self, test_data, **kw):
+        if getattr(self, "_gblinear", None) is not None:
+            raise NotImplementedError("predict_contributions is not available for booster=gblinear (no trees)")
         from .shap import tree_contributions
         return tree_contributions(self, test_data)
