@@ -37,7 +37,7 @@ class H2OGridSearch:
         m = self.model
         if isinstance(m, type):
             return lambda **kw: m(**kw)
-        base = dict(m._parms)
+        base = m._user_parms()
         cls = type(m)
         return lambda **kw: cls(**{**base, **kw})
 
@@ -320,7 +320,8 @@ def load_grid(grid_file_path):
         raise ValueError(f"{grid_file_path} is not a saved h2o3_amd grid")
     d = os.path.dirname(grid_file_path)
     cls = _estimator_class(st["estimator"])
-    base = cls(**{k: v for k, v in st["base_params"].items() if k != "model_id"}) if st["base_params"] else cls
+    base = cls(**cls._accepted({k: v for k, v in st["base_params"].items() if k != "model_id"})) \
+        if st["base_params"] else cls
     g = H2OGridSearch(base, st["hyper_params"], grid_id=st["grid_id"], search_criteria=st["search_criteria"])
     for rec in st["models"]:
         m = load_model(os.path.join(d, rec["model_id"]))
@@ -350,7 +351,7 @@ def resume_all(recovery_dir):
         if "estimator" not in st or "train" not in st:
             continue
         cls = _estimator_class(st["estimator"])
-        base = cls(**{k: v for k, v in st.get("base_params", {}).items() if k != "model_id"})
+        base = cls(**cls._accepted({k: v for k, v in st.get("base_params", {}).items() if k != "model_id"}))
         g = H2OGridSearch(base, st["hyper_params"], grid_id=st["grid_id"], search_criteria=st["search_criteria"],
                           recovery_dir=recovery_dir)
         tr = st["train"]

@@ -109,6 +109,7 @@ def _assign(X, E, chunk=65536):
 
 
 class H2OAggregatorEstimator(H2OEstimator):
+    _extra_params = ("seed",)   # deterministic sampling (not a reference client argument)
     algo = "aggregator"
     supervised_learning = False
     _defaults = AGG_DEFAULTS

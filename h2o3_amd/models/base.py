@@ -194,9 +194,42 @@ class H2OEstimator:
             if fn is not None and callable(fn) and not getattr(fn, "_catenc_wrapped", False):
                 setattr(cls, name, _encoding_wrapper(fn))
 
+    # parameters this implementation accepts beyond the reference client's
+    # table for the class (internal plumbing, aliases)
+    _extra_params: tuple = ()
+
+    @classmethod
+    def _param_names(cls):
+        """The estimator's parameter table: the reference client's names for
+        this class (or the nearest ancestor that has one), plus _extra_params;
+        None when the reference has no such estimator."""
+        from .param_tables import PARAMS
+        for k in cls.__mro__:
+            t = PARAMS.get(k.__name__)
+            if t is not None:
+                return set(t) | set(cls._extra_params)
+        return None
+
+    @classmethod
+    def _accepted(cls, parms):
+        """`parms` without the names this estimator does not take (internal
+        clones of a validated estimator carry every shared default)."""
+        names = cls._param_names()
+        return dict(parms) if names is None else {k: v for k, v in parms.items() if k in names}
+
+    def _user_parms(self):
+        return self._accepted(self._parms)
+
     def __init__(self, **kwargs):
         parms = dict(COMMON_DEFAULTS)
         parms.update(self._defaults)
+        names = self._param_names()
+        if names is not None:
+            unknown = sorted(k for k in kwargs if k not in names)
+            if unknown:
+                # the reference client's estimators take no such keyword, and
+                # ModelBuilder.init reports unknown fields as errors
+                raise TypeError(f"{type(self).__name__}: unknown parameter(s) {unknown}")
         for k, v in kwargs.items():
             parms[k] = v
         self._parms = parms

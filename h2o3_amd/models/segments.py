@@ -47,7 +47,7 @@ def train_segments(estimator, x=None, y=None, training_frame=None, segment_colum
         combos = sorted(set(tuple(r) for r in df.itertuples(index=False)), key=lambda t: tuple(map(str, t)))
     out = H2OSegmentModels(segment_models_id)
     cls = type(estimator)
-    parms = {k: v for k, v in estimator._parms.items() if k != "model_id"}
+    parms = {k: v for k, v in estimator._user_parms().items() if k != "model_id"}
     for combo in combos:
         mask = torch.ones(training_frame.nlocal, dtype=torch.bool)
         for c, v in zip(segment_columns, combo):

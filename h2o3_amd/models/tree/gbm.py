@@ -44,7 +44,7 @@ GBM_DEFAULTS = dict(ntrees=50, max_depth=5, min_rows=10.0, nbins=20, nbins_top_l
                     monotone_constraints=None, check_constant_response=True, interaction_constraints=None,
                     score_tree_interval=0, balance_classes=False, class_sampling_factors=None,
                     max_after_balance_size=5.0, max_confusion_matrix_size=20, in_training_checkpoints_dir=None,
-                    in_training_checkpoints_tree_interval=1, auto_rebalance=True)
+                    in_training_checkpoints_tree_interval=1)
 
 
 class GBMDriver:

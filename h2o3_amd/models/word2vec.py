@@ -63,6 +63,7 @@ def _huffman(counts):
 
 
 class H2OWord2vecEstimator(H2OEstimator):
+    _extra_params = ("seed",)   # deterministic sampling (not a reference client argument)
     algo = "word2vec"
     supervised_learning = False
     _defaults = W2V_DEFAULTS

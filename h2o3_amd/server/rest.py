@@ -1075,6 +1075,8 @@ def create_app(flow_dir: str | None = None, serve: bool = True) -> FastAPI:
         if isinstance(crit, str):
             crit = _json.loads(crit)
         gid = p.pop("grid_id", None)
+        p.pop("parallelism", None)              # GridSearchHandler-level (models build one at a time here)
+        recovery_dir = p.pop("recovery_dir", None)
         tf, vf = p.pop("training_frame", None), p.pop("validation_frame", None)
         y = p.pop("response_column", None)
         ignored = set(p.pop("ignored_columns", None) or [])
@@ -1082,7 +1084,7 @@ def create_app(flow_dir: str | None = None, serve: bool = True) -> FastAPI:
         p.pop("_rest_version", None)
         from ..core import job as jobmod
         g = H2OGridSearch(cls(**{k: v for k, v in p.items() if v is not None}), hyper, grid_id=gid,
-                          search_criteria=crit)
+                          search_criteria=crit, **({"recovery_dir": recovery_dir} if recovery_dir else {}))
         job = jobmod.Job("GridSearch", dest=g.grid_id, dest_kind="Grid").start()
         job.spmd = cloud.is_distributed()
         dkv.put(g.grid_id, g)           # visible (and growing) while the search runs
