@@ -539,7 +539,7 @@ class H2OEstimator:
         (reference: ModelBuilder.cv_computeAndSetOptimalParameters)."""
 
     # ------------------------------------------------------------ scoring
-    def _metrics_from_raw(self, spec, frame, raw, w=None):
+    def _metrics_from_raw(self, spec, frame, raw, w=None, auc_type=None):
         if raw is None:
             return None
         y = spec.y_tensor(frame) if spec.y and spec.y in frame.names else None
@@ -551,9 +551,12 @@ class H2OEstimator:
         if spec.nclasses == 2:
             yy = y.to(torch.float64)
             ok = yy >= 0
-            res = mm.binomial_metrics(yy[ok], raw[ok][:, -1], None if w is None else w[ok], spec.response_domain)
+            res = mm.binomial_metrics(yy[ok], raw[ok][:, -1], None if w is None else w[ok], spec.response_domain,
+                                      gainslift_bins=self._parms.get("gainslift_bins", -1))
         elif spec.nclasses > 2:
-            res = mm.multinomial_metrics(y, raw, w, spec.response_domain)
+            res = mm.multinomial_metrics(y, raw, w, spec.response_domain,
+                                         auc_type=auc_type or self._parms.get("auc_type") or "AUTO",
+                                         max_cm_size=self._parms.get("max_confusion_matrix_size"))
         else:
             res = mm.regression_metrics(y.to(torch.float64), raw[:, 0], w, dist)
         cm = self._parms.get("custom_metric_func")
@@ -643,7 +646,7 @@ class H2OEstimator:
         if not self.supervised_learning:
             return self._unsupervised_perf(test_data)
         raw = self._predict_raw(test_data)
-        return self._metrics_from_raw(self._spec, test_data, raw)
+        return self._metrics_from_raw(self._spec, test_data, raw, auc_type=auc_type)
 
     def _unsupervised_perf(self, frame):
         return None
@@ -660,6 +663,10 @@ class H2OEstimator:
 
     def auc(self, train=False, valid=False, xval=False): return self._pick("auc", train, valid, xval)
     def aucpr(self, train=False, valid=False, xval=False): return self._pick("aucpr", train, valid, xval)
+    def multinomial_auc_table(self, train=False, valid=False, xval=False):
+        return self._pick("multinomial_auc_table", train, valid, xval)
+    def multinomial_aucpr_table(self, train=False, valid=False, xval=False):
+        return self._pick("multinomial_aucpr_table", train, valid, xval)
     pr_auc = aucpr
     def logloss(self, train=False, valid=False, xval=False): return self._pick("logloss", train, valid, xval)
     def mse(self, train=False, valid=False, xval=False): return self._pick("mse", train, valid, xval)

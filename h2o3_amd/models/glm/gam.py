@@ -332,8 +332,8 @@ class H2OGeneralizedAdditiveEstimator(H2OGeneralizedLinearEstimator):
             return super()._predict_raw(frame)
         return super()._predict_raw(self._gam_frame(frame))
 
-    def _metrics_from_raw(self, spec, frame, raw, w=None):
-        return super()._metrics_from_raw(spec, frame, raw, w)
+    def _metrics_from_raw(self, spec, frame, raw, w=None, auc_type=None):
+        return super()._metrics_from_raw(spec, frame, raw, w, auc_type=auc_type)
 
     def model_performance(self, test_data=None, **kw):
         if test_data is not None and not any("_cr_" in n or "_tp_" in n or "_is_" in n or "_ms_" in n

@@ -1016,8 +1016,8 @@ class H2OGeneralizedLinearEstimator(H2OEstimator):
             return torch.stack([1 - mu, mu], 1)
         return mu.view(-1, 1)
 
-    def _metrics_from_raw(self, spec, frame, raw, w=None):
-        m = super()._metrics_from_raw(spec, frame, raw, w)
+    def _metrics_from_raw(self, spec, frame, raw, w=None, auc_type=None):
+        m = super()._metrics_from_raw(spec, frame, raw, w, auc_type=auc_type)
         multi = getattr(self, "_multi", None)
         if m is not None and multi is not None and multi.get("kind") == "ordinal":
             # ordinal family -> ModelMetricsOrdinal (hex/ModelMetricsOrdinal.java): same hit ratios,

@@ -523,6 +523,15 @@ def metrics_v3(mm, model=None, frame_id=None, category=None) -> dict | None:
         out["cm"] = _cm_table(d["cm"])
     if d.get("hit_ratio_table") is not None:
         out["hit_ratio_table"] = twodim_from_df("Top-K Hit Ratios", d["hit_ratio_table"])
+    for tk, metric in (("multinomial_auc_table", "AUC"), ("multinomial_aucpr_table", "auc_pr")):
+        rows = d.get(tk)
+        if rows:
+            # MultinomialAUC.getTable: row header "Type", then the two class domains and the value
+            out[tk] = twodim(f"Multinomial {metric} values",
+                             {"first_class_domain": [r["first_class_domain"] for r in rows],
+                              "second_class_domain": [r["second_class_domain"] for r in rows],
+                              metric: [r["value"] for r in rows]},
+                             row_headers=[r["type"] for r in rows], row_header_name="Type")
     if cat == "Clustering":
         ws, sz = d.get("withinss"), d.get("size")
         if ws is not None:

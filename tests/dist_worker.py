@@ -49,6 +49,20 @@ def run(out_path):
     km = H2OKMeansEstimator(k=3, seed=5, init="PlusPlus", standardize=True)
     km.train(x=[f"x{i}" for i in range(6)], training_frame=fr)
     res["km_tot_withinss"] = km.tot_withinss()
+    # multinomial metrics + multinomial AUC: sums and merged sketches, no row gathers
+    import numpy as np
+    df3 = make_df()
+    df3["y3"] = np.where(df3.x0 > 0.5, "hi", np.where(df3.x0 < -0.5, "lo", "mid"))
+    fr3 = h2o.H2OFrame(df3)
+    g3 = H2OGradientBoostingEstimator(ntrees=5, max_depth=3, seed=1, auc_type="MACRO_OVO")
+    g3.train(x=x, y="y3", training_frame=fr3)
+    m3 = g3.model_performance(fr3)
+    res["multi"] = {"logloss": m3.logloss(), "auc": m3.auc(), "aucpr": m3.aucpr(),
+                    "cm": m3["cm"]["matrix"], "hr": [r["hit_ratio"] for r in m3["hit_ratio_table"]],
+                    "wovr": g3.model_performance(fr3, auc_type="WEIGHTED_OVR").auc()}
+    mb = gbm.model_performance(fr)
+    res["bin_tab_rows"] = len(mb["thresholds_and_metric_scores"]["threshold"])
+    res["bin_prauc"] = mb.aucpr()
     from h2o3_amd.parallel import cloud
     if cloud.rank() == 0:
         with open(out_path, "w") as f:

@@ -10,6 +10,7 @@ import socket
 import subprocess
 import sys
 
+import numpy as np
 import pytest
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -62,6 +63,20 @@ def test_gbm_matches_single_process(results):
     one, two = results
     assert abs(one["gbm_auc"] - two["gbm_auc"]) < 1e-5
     assert abs(one["gbm_logloss"] - two["gbm_logloss"]) < 1e-5
+
+
+def test_metrics_from_merged_sketches_match_single_process(results):
+    """Binomial metrics at W > 1 come from the merged logit histogram (AUC2's
+    role), multinomial ones from sums + the [K, K, bins] AUC sketch: no rows
+    gathered, and the values equal the single-process ones."""
+    one, two = results
+    a, b = one["multi"], two["multi"]
+    assert abs(a["logloss"] - b["logloss"]) < 1e-6
+    assert a["cm"] == b["cm"] and np.allclose(a["hr"], b["hr"], atol=1e-12)
+    assert abs(a["auc"] - b["auc"]) < 1e-9 and abs(a["wovr"] - b["wovr"]) < 1e-9 and a["auc"] > 0.8
+    assert abs(a["aucpr"] - b["aucpr"]) < 1e-9
+    assert abs(one["bin_prauc"] - two["bin_prauc"]) < 2e-3
+    assert 50 < two["bin_tab_rows"] <= 400
 
 
 def test_glm_matches_single_process(results):
