@@ -168,12 +168,21 @@ def _encoding_wrapper(fn):
     categorical encoding (idempotent on already-encoded frames)."""
     import functools
 
+    correct = fn.__name__ == "_predict_raw"
+
     @functools.wraps(fn)
     def w(self, frame, *a, **k):
         enc = self.__dict__.get("_catenc")
         if enc is not None and frame is not None and hasattr(frame, "_vecs"):
             frame = enc.transform(frame)
-        return fn(self, frame, *a, **k)
+        out = fn(self, frame, *a, **k)
+        prior = self.__dict__.get("_prior_class_dist")
+        if correct and prior is not None and isinstance(out, torch.Tensor) and out.dim() == 2 and \
+                out.shape[1] == len(prior):
+            # balance_classes: back to the prior class distribution (GenModel.correctProbabilities)
+            from .balance import correct_probabilities
+            out = correct_probabilities(out, prior, self._model_class_dist)
+        return out
     w._catenc_wrapped = True
     return w
 
@@ -346,6 +355,13 @@ class H2OEstimator:
             if validation_frame is not None and y in validation_frame.names:
                 validation_frame = validation_frame[:, :]
                 validation_frame[y] = validation_frame[y].asfactor()
+        # balance_classes (ModelBuilder.init -> MRUtils.sampleFrameStratified)
+        from . import balance as _balance
+        self._prior_class_dist = self._model_class_dist = None
+        if p.get("class_sampling_factors") is not None and not p.get("balance_classes"):
+            raise ValueError("class_sampling_factors: class_sampling_factors requires balance_classes to be "
+                             "enabled.")
+        training_frame = _balance.apply(self, training_frame, y)
         # categorical_encoding (hex/Model.java:355, FrameUtils.categoricalEncoder):
         # fitted on the training frame, kept on the model, applied to every
         # frame it scores (see _encode / __init_subclass__)
@@ -398,6 +414,12 @@ class H2OEstimator:
         self._run_time = time.time() - t0
         self._end_time = int(time.time() * 1000)
         dkv.put(self._id, self)
+        if p.get("export_checkpoints_dir"):
+            # ModelBuilder: every finished model is exported as a binary model into the directory
+            import os as _os
+            from .persist import save_model
+            _os.makedirs(p["export_checkpoints_dir"], exist_ok=True)
+            save_model(self, path=p["export_checkpoints_dir"], force=True)
         return self
 
     def _check_response(self, frame, y):
@@ -986,6 +1008,8 @@ class H2OEstimator:
             self._pred_frame_from_raw(self._cv_holdout) if getattr(self, "_cv_holdout", None) is not None else None)
 
     def cross_validation_fold_assignment(self):
+        if not self._parms.get("keep_cross_validation_fold_assignment"):
+            return None          # kept only when asked (ModelBuilder cv_computeAndSetOptimalParameters)
         f = self._cv_fold_assignment
         return None if f is None else H2OFrame.from_vecs([Vec(f.to(torch.float32), T_INT)], ["fold_assignment"])
 

@@ -216,6 +216,30 @@ class Forest:
 
 
 class SharedTreeEstimator(H2OEstimator):
+    def _check_response(self, frame, y):
+        """SharedTree.init: a constant response is an error unless
+        check_constant_response is off; r2_stopping is deprecated there and
+        ignored with a warning."""
+        p = self._parms
+        if y is not None and p.get("check_constant_response", True) and y in frame.names:
+            v = frame.vec(y)
+            if v.type == "enum":
+                codes = v.data
+                import torch as _t
+                present = _t.zeros(len(v.domain or []) + 1, dtype=_t.float64, device=codes.device)
+                present.index_add_(0, (codes.long() + 1).clamp_min(0), _t.ones_like(codes, dtype=_t.float64))
+                from ...parallel import collectives as _coll
+                _coll.allreduce_(present)
+                if int((present[1:] > 0).sum()) < 2:
+                    raise ValueError("ERRR on field: _response: Response cannot be constant.")
+            elif v.is_const():
+                raise ValueError("ERRR on field: _response: Response cannot be constant.")
+        r2 = p.get("r2_stopping")
+        if r2 is not None and float(r2) < 1.79e308:
+            import warnings
+            warnings.warn("r2_stopping is no longer supported and will be ignored if set - please use "
+                          "stopping_rounds, stopping_metric and stopping_tolerance instead.")
+
     """Base of GBM / DRF / XGBoost / IsolationForest / UpliftDRF."""
 
     def _cv_optimal_params(self, cv_models):
