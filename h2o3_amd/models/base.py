@@ -358,10 +358,15 @@ class H2OEstimator:
         # balance_classes (ModelBuilder.init -> MRUtils.sampleFrameStratified)
         from . import balance as _balance
         self._prior_class_dist = self._model_class_dist = None
-        if p.get("class_sampling_factors") is not None and not p.get("balance_classes"):
-            raise ValueError("class_sampling_factors: class_sampling_factors requires balance_classes to be "
-                             "enabled.")
-        training_frame = _balance.apply(self, training_frame, y)
+        if getattr(self, "_balance_hidden", False):
+            # GLM.init hides the three balance parameters ("Not applicable since
+            # class balancing is not required for GLM"): accepted and ignored
+            pass
+        else:
+            if p.get("class_sampling_factors") is not None and not p.get("balance_classes"):
+                raise ValueError("class_sampling_factors: class_sampling_factors requires balance_classes to be "
+                                 "enabled.")
+            training_frame = _balance.apply(self, training_frame, y)
         # categorical_encoding (hex/Model.java:355, FrameUtils.categoricalEncoder):
         # fitted on the training frame, kept on the model, applied to every
         # frame it scores (see _encode / __init_subclass__)

@@ -95,18 +95,34 @@ class H2OStackedEnsembleEstimator(H2OEstimator):
         if p.get("seed", -1) not in (None, -1):
             mp.setdefault("seed", p["seed"])
         if algo in ("auto", "glm"):
-            if algo == "auto":
-                mp.setdefault("non_negative", True)
-                mp.setdefault("lambda_search", True)
             fam = "binomial" if spec.nclasses == 2 else ("multinomial" if spec.nclasses > 2 else "gaussian")
             mp.setdefault("family", fam)
+            if algo == "auto":
+                # Metalearners.AUTOMetalearner.setCustomParams: non-negative
+                # weights (not for multinomial / ordinal), no standardization,
+                # lambda search without early stopping when a validation
+                # frame is given, scoring history every 5 iterations otherwise
+                mp.setdefault("non_negative", str(mp["family"]).lower() not in ("multinomial", "ordinal"))
+                mp.setdefault("standardize", False)
+                mp.setdefault("generate_scoring_history", True)
+                if spec.valid is not None:
+                    mp.setdefault("lambda_search", True)
+                    mp.setdefault("early_stopping", False)
+                else:
+                    mp.setdefault("score_iteration_interval", 5)
             meta = H2OGeneralizedLinearEstimator(**mp)
         else:
             cls = {"gbm": H2OGradientBoostingEstimator, "drf": H2ORandomForestEstimator,
                    "deeplearning": H2ODeepLearningEstimator, "naivebayes": H2ONaiveBayesEstimator,
                    "xgboost": H2OXGBoostEstimator}[algo]
             meta = cls(**mp)
-        meta.train(x=names, y=spec.y, training_frame=lvl1)
+        lvl1_valid = None
+        if spec.valid is not None and algo in ("auto", "glm"):
+            # StackedEnsemble.java: the metalearner sees a level-one validation
+            # frame of base-model predictions on the validation rows
+            vv, _ = self._level_one(base, spec.valid, use_cv=False)
+            lvl1_valid = H2OFrame.from_vecs(vv + [spec.valid.vec(spec.y)], names + [spec.y])
+        meta.train(x=names, y=spec.y, training_frame=lvl1, validation_frame=lvl1_valid)
         self._meta = meta
         if getattr(meta, "_cross_validation_metrics", None) is not None:
             # StackedEnsembleModel.java:371: the ensemble's cross-validation

@@ -31,12 +31,12 @@ from ...core.vec import T_ENUM, T_REAL, Vec
 from ...ops import linalg_ops
 from ...parallel import cloud
 from ...parallel import collectives as coll
-from ..base import H2OEstimator
+from ..base import H2OEstimator, ScoreKeeper, ScoreSchedule, _LESS_IS_BETTER
 from ..datainfo import DataInfo
 from ...utils.timer import phase
 from .. import metrics as mm
 
-GLM_DEFAULTS = dict(family="AUTO", tweedie_variance_power=0.0, dispersion_learning_rate=0.5,
+GLM_DEFAULTS = dict(family="AUTO", tweedie_variance_power=0.0,
                     tweedie_link_power=1.0, theta=1e-10, solver="AUTO", alpha=None, lambda_=None,
                     lambda_search=False, early_stopping=True, nlambdas=-1, standardize=True,
                     missing_values_handling="MeanImputation", plug_values=None, compute_p_values=False,
@@ -49,11 +49,9 @@ GLM_DEFAULTS = dict(family="AUTO", tweedie_variance_power=0.0, dispersion_learni
                     balance_classes=False, class_sampling_factors=None, max_after_balance_size=5.0,
                     max_confusion_matrix_size=20, max_runtime_secs=0.0, custom_metric_func=None,
                     generate_scoring_history=False, auc_type="auto", dispersion_epsilon=1e-4,
-                    tweedie_epsilon=8e-17, max_iterations_dispersion=3000, build_null_model=False,
-                    fix_dispersion_parameter=False, generate_variable_inflation_factors=False,
-                    fix_tweedie_variance_power=True, HGLM=False, random_columns=None, rand_family=None,
-                    rand_link=None, gainslift_bins=-1, linear_constraints=None, influence=None,
-                    score_iteration_interval=-1, seed=-1, checkpoint=None)
+                    max_iterations_dispersion=3000, build_null_model=False,
+                    fix_dispersion_parameter=False, HGLM=False, random_columns=None, rand_family=None,
+                    rand_link=None, score_iteration_interval=-1, seed=-1, checkpoint=None)
 
 _DEFAULT_LINK = {"gaussian": "identity", "binomial": "logit", "quasibinomial": "logit",
                  "fractionalbinomial": "logit", "poisson": "log", "gamma": "inverse", "tweedie": "tweedie",
@@ -312,6 +310,10 @@ class GLMDriver:
             raise ValueError("ERRR on field: _train: Training data has no rows with a valid response and "
                              "positive weight")
         self.ymu = coll.allreduce_scalar(float((self.w * self.y).sum())) / self.wsum
+        # obj_reg: the objective is obj_reg * (-log-likelihood) + penalty
+        # (GLM.java:1063, default 1 / sum of weights)
+        orr = float(p.get("obj_reg") if p.get("obj_reg") is not None else -1.0)
+        self.obj_reg = orr if orr > 0 else 1.0 / self.wsum
         alpha = p.get("alpha")
         solver = (p.get("solver") or "AUTO").upper()
         if alpha is None:
@@ -343,6 +345,8 @@ class GLMDriver:
         lam = p.get("lambda_")
         if lam is None:
             lam = p.get("Lambda")
+        nl = int(p.get("nlambdas") or -1)
+        self.nlambdas = (30 if self.alpha == 0 else 100) if nl == -1 else nl    # GLM.java:951
         lmr = float(p.get("lambda_min_ratio") or -1)
         if lmr == -1:
             lmr = 1e-4 if (self.nobs / 16) > self.P else 1e-2
@@ -350,8 +354,7 @@ class GLMDriver:
                 lmr *= 1e-2
         self.lambda_min_ratio = lmr
         if p.get("lambda_search"):
-            nl = int(p.get("nlambdas") or -1)
-            nl = 100 if nl == -1 else nl
+            nl = self.nlambdas
             if lam is None:
                 dec = lmr ** (1.0 / max(nl - 1, 1))
                 self.lambdas = [self.lambda_max * dec ** i for i in range(nl)]
@@ -366,6 +369,13 @@ class GLMDriver:
         self.beta_eps = float(p.get("beta_epsilon") or 1e-4)
         oe = float(p.get("objective_epsilon") or -1)
         self.obj_eps = oe if oe > 0 else (1e-4 if p.get("lambda_search") else (1e-6 if self.lam == 0 else 1e-4))
+        ge = float(p.get("gradient_epsilon") if p.get("gradient_epsilon") is not None else -1.0)
+        if ge <= 0:                                                     # GLM.java:1182
+            ge = (1e-6 if self.lambdas[0] == 0 else 1e-4) * (1e-2 if p.get("lambda_search") else 1.0)
+        self.grad_eps = ge
+        # stopping_rounds without lambda search switches GLM's own convergence
+        # test off in favour of ScoreKeeper early stopping (GLM.java:946, :3137)
+        self.early_stop_enabled = (not p.get("lambda_search")) and int(p.get("stopping_rounds") or 0) > 0
         self.converged = False
         self.last_obj = float("inf")
 
@@ -485,7 +495,7 @@ class GLMDriver:
         else:
             g = (self.X.to(torch.float64).T @ r)[: self.P]
         coll.allreduce_(g)
-        g = g / self.wsum
+        g = g * self.obj_reg
         amax = float(g.abs().max()) if g.numel() else 0.0
         return amax / max(1e-2, self.alpha)
 
@@ -591,8 +601,8 @@ class GLMDriver:
     def step(self):
         """One IRLS iteration (Gram on the matrix cores + host solve)."""
         Ga, b, dev = self._irls_stats()
-        n = self.wsum
-        Gn, bn = Ga / n, b / n
+        r = self.obj_reg
+        Gn, bn = Ga * r, b * r
         if not self.intercept:
             Gn = Gn[:-1, :-1].copy()
             bn = bn[:-1].copy()
@@ -620,6 +630,19 @@ class GLMDriver:
             mask = np.array([nonneg or (c in s_) for c in self.dinfo.coef_names] + [False])
             nonneg = mask if self.intercept else mask[:-1]
         k = Gn.shape[0]
+        # gradient of the penalized objective at the current beta (the IRLS
+        # quadratic is exact to first order there): ComputationState.converged
+        # stops when its max |.| (l1 subgradient) is under gradient_epsilon
+        bcur = self.beta if self.intercept else self.beta[:-1]
+        gq = Gn @ bcur - bn
+        pen_idx = slice(0, self.P)
+        gq[pen_idx] += l2 * bcur[pen_idx]
+        gl1 = np.where(bcur[pen_idx] != 0, gq[pen_idx] + l1 * np.sign(bcur[pen_idx]),
+                       np.sign(gq[pen_idx]) * np.maximum(np.abs(gq[pen_idx]) - l1, 0.0))
+        gv = np.abs(np.concatenate([gl1, gq[self.P:]]))
+        if self.active is not None:
+            gv = np.where(self.active[:k], gv, 0.0)
+        gmax = float(gv.max()) if gv.size else 0.0
         with phase("glm.solve"):
             new = _solve_quadratic(Gn, bn, l1, l2, self.intercept,
                                    beta0=self.beta if self.intercept else self.beta[:-1],
@@ -631,9 +654,12 @@ class GLMDriver:
         diff = float(np.max(np.abs(new - self.beta))) if new.size else 0.0
         self.beta = new
         self.iter += 1
-        obj = dev / (2 * n) + l1 * np.abs(new[:-1]).sum() + l2 / 2 * (new[:-1] ** 2).sum()
+        obj = dev * r / 2 + l1 * np.abs(new[:-1]).sum() + l2 / 2 * (new[:-1] ** 2).sum()
+        self.last_grad = gmax
         self.converged = diff < self.beta_eps or abs(self.last_obj - obj) < self.obj_eps * max(abs(obj), 1e-12) or \
-            (self.fam.family == "gaussian" and self.fam.link == "identity")
+            (self.fam.family == "gaussian" and self.fam.link == "identity") or (self.iter > 1 and gmax < self.grad_eps)
+        if self.early_stop_enabled and not (self.fam.family == "gaussian" and self.fam.link == "identity"):
+            self.converged = False
         self.last_obj = obj
         self.last_dev = dev
         return diff
@@ -663,6 +689,7 @@ class GLMDriver:
 class H2OGeneralizedLinearEstimator(H2OEstimator):
     algo = "glm"
     _defaults = GLM_DEFAULTS
+    _balance_hidden = True
 
     def __init__(self, **kw):
         if "lambda" in kw:
@@ -682,6 +709,11 @@ class H2OGeneralizedLinearEstimator(H2OEstimator):
         if fam == "multinomial" and spec.nclasses <= 2:
             raise ValueError("ERRR on field: _family: Multinomial requires a categorical response with at least 3 "
                              "levels (for 2 class problem use family=binomial.")
+        self._validate_glm(spec, fam)
+        if fam == "multinomial" and spec.offset_column:
+            # GLM.java:978: offset has no effect on multinomial and is ignored
+            import warnings
+            warnings.warn("offset_column has no effect on multinomial and will be ignored.")
         if fam in ("multinomial", "ordinal"):
             from .glm_multi import fit_multinomial
             return fit_multinomial(self, spec, fam)
@@ -689,18 +721,35 @@ class H2OGeneralizedLinearEstimator(H2OEstimator):
             from .hglm import fit_hglm
             return fit_hglm(self, spec)
         solver = (p.get("solver") or "AUTO").upper()
+        if p.get("build_null_model"):
+            # GLM.java:933 removePredictors: an intercept-only model
+            spec.x = []
         drv = GLMDriver(self, spec)
         self._drv_family = drv.family
         maxit = int(p.get("max_iterations") or -1)
         if maxit == -1:
-            maxit = 50 if solver != "L_BFGS" else 1000
+            # GLM.java:1035 (iterations accumulate over the lambda path)
+            if solver == "L_BFGS":
+                maxit = 10 * max(20, drv.P >> 2) * (10 if drv.alpha > 0 else 1)
+            else:
+                maxit = 10 * drv.nlambdas if p.get("lambda_search") else 50
         t0 = time.time()
         max_rt = float(p.get("max_runtime_secs") or 0)
         path = []
         self._scoring_history = []
         max_active = int(p.get("max_active_predictors") or -1)
         user_lams = p.get("lambda_")
-        for alpha in drv.alphas:
+        stop_rounds = int(p.get("stopping_rounds") or 0)
+        sched = ScoreSchedule({"score_each_iteration": p.get("score_each_iteration"),
+                               "score_tree_interval": p.get("score_iteration_interval")
+                               if int(p.get("score_iteration_interval") or -1) > 0 else 0})
+        metric_name = self._stopping_metric_name(spec)
+        history = []
+        scoring = bool(p.get("generate_scoring_history")) or drv.early_stop_enabled
+        early_stop = False
+        null_train = self._null_deviance(drv)
+        null_valid = self._null_deviance_on(spec.valid, drv) if spec.valid is not None else None
+        for ai, alpha in enumerate(drv.alphas):
             # one regularization path per alpha (GLM.java: alpha x lambda grid)
             if alpha != drv.alpha or len(drv.alphas) > 1:
                 drv.alpha = alpha
@@ -709,33 +758,66 @@ class H2OGeneralizedLinearEstimator(H2OEstimator):
                     drv.lambda_max = drv._lambda_max()
                     lmr = drv.lambda_min_ratio
                     if p.get("lambda_search") and user_lams is None:
-                        nl = int(p.get("nlambdas") or -1)
-                        nl = 100 if nl == -1 else nl
+                        nl = drv.nlambdas
                         dec = lmr ** (1.0 / max(nl - 1, 1))
                         drv.lambdas = [drv.lambda_max * dec ** i for i in range(nl)]
                     elif user_lams is None:
                         drv.lambdas = [10 * lmr * drv.lambda_max]
+            # lambda-search early stopping (GLM.java:2923-2993): relative
+            # deviance improvements of the last 5 submodels
+            hist_tr, hist_te = [0.0] * 5, [0.0] * 5
+            old_tr, old_te = null_train, null_valid
+            nsub = 0
             for li, lam in enumerate(drv.lambdas):
+                if drv.iter >= maxit or early_stop:
+                    break
                 drv.lam = lam
                 drv.converged = False
                 drv.last_obj = float("inf")
                 if p.get("cold_start") and li > 0:
                     drv.beta = drv._init_beta.copy()
-                its = 0
-                while its < maxit and not drv.converged:
+                while drv.iter < maxit and not drv.converged:
                     drv.step()
-                    its += 1
-                    self._tick(li + its / maxit, len(drv.lambdas) + 1)
-                    self._scoring_history.append({"iteration": drv.iter, "alpha": alpha, "lambda": lam,
-                                                  "deviance_train": drv.last_dev / drv.wsum,
-                                                  "objective": drv.last_obj})
+                    score, timed_out = self._tick(drv.iter, maxit, sched if scoring else None, False, t0, max_rt)
+                    entry = {"iteration": drv.iter, "timestamp": time.time(), "duration": time.time() - t0,
+                             "alpha": alpha, "lambda": lam, "negative_log_likelihood": drv.last_dev / 2,
+                             "objective": drv.last_obj, "deviance_train": drv.last_dev / drv.wsum,
+                             "gradient": drv.last_grad}
+                    if score:
+                        sched.started()
+                        self._iter_score(drv, spec, entry)
+                        sched.ended()
+                    self._scoring_history.append(entry)
+                    if score and drv.early_stop_enabled:
+                        key = ("validation_" if spec.valid is not None else "training_") + metric_name
+                        history.append(entry.get(key))
+                        if ScoreKeeper.stop_early(history, stop_rounds, float(p.get("stopping_tolerance", 1e-3)),
+                                                  metric_name in _LESS_IS_BETTER):
+                            early_stop = True
+                            break
+                    if timed_out:
+                        break
                 dev = drv.deviance()
                 beta, icpt = drv.dinfo.destandardize(drv.beta[:-1], drv.beta[-1])
-                path.append({"lambda": lam, "alpha": alpha, "beta_std": drv.beta.copy(), "beta": beta,
-                             "icpt": icpt, "deviance": dev, "explained_deviance_train": None})
+                sm = {"lambda": lam, "alpha": alpha, "beta_std": drv.beta.copy(), "beta": beta,
+                      "icpt": icpt, "deviance": dev, "explained_deviance_train": None, "iteration": drv.iter}
+                path.append(sm)
                 if max_active > 0 and int(np.sum(np.abs(drv.beta[:-1]) > 0)) > max_active:
                     break   # GLM.java: stop the path once too many predictors are active
-                if self._tick(li + 1, len(drv.lambdas) + 1, None, False, t0, max_rt)[1]:
+                if p.get("lambda_search"):
+                    dev_te = self._dev_on(spec.valid, sm, drv) if spec.valid is not None else None
+                    hist_tr[nsub % 5] = (old_tr - dev) / old_tr if old_tr else 0.0
+                    old_tr = dev
+                    if dev_te is not None:
+                        hist_te[nsub % 5] = (old_te - dev_te) / old_te if old_te else 0.0
+                        old_te = dev_te
+                    nsub += 1
+                    if lam < drv.lambda_max and p.get("early_stopping", True) and drv.iter >= 5:
+                        if max(hist_tr) < 1e-4:
+                            break
+                        if dev_te is not None and int(p.get("nfolds") or 0) <= 1 and max(hist_te) < 0:
+                            break
+                if self._tick(drv.iter, maxit, None, False, t0, max_rt)[1]:
                     break
         # pick submodel: best by validation deviance if given, else (several
         # alphas) by training deviance of each alpha's last lambda, else last
@@ -777,7 +859,168 @@ class H2OGeneralizedLinearEstimator(H2OEstimator):
         y = self._spec.y_tensor(frame)
         yy = (y == 1).to(torch.float64) if self._spec.is_classification else y.to(torch.float64)
         m = ok & (~torch.isnan(yy) if not self._spec.is_classification else (y >= 0))
-        return float(drv.fam.deviance(yy[m], mu[m]).sum())
+        return coll.allreduce_scalar(float(drv.fam.deviance(yy[m], mu[m]).sum()))
+
+    def _null_deviance_on(self, frame, drv):
+        """Deviance of the intercept-only (training mean) model on `frame`."""
+        y = self._spec.y_tensor(frame)
+        yy = (y == 1).to(torch.float64) if self._spec.is_classification else y.to(torch.float64)
+        m = ~torch.isnan(yy) if not self._spec.is_classification else (y >= 0)
+        mu = torch.full_like(yy[m], min(max(drv.ymu, 1e-10), 1 - 1e-10) if drv.fam.link == "logit" else drv.ymu)
+        return coll.allreduce_scalar(float(drv.fam.deviance(yy[m], mu).sum()))
+
+    def _stopping_metric_name(self, spec):
+        m = (self._parms.get("stopping_metric") or "auto").lower()
+        if m == "auto":
+            return "logloss" if spec.is_classification else "deviance"
+        return m
+
+    def _iter_score(self, drv, spec, entry):
+        """Training (and validation) metrics of the current coefficients
+        (GLM.java scoreAndUpdateModel; generate_scoring_history and
+        stopping_rounds read them)."""
+        from ..tree.gbm import H2OGradientBoostingEstimator as _G
+        self._beta_std, self._dinfo, self._fam = drv.beta.copy(), drv.dinfo, drv.fam
+        mu = drv.fam.linkinv(drv._eta())
+        raw = torch.stack([1 - mu, mu], 1) if spec.nclasses == 2 else mu.view(-1, 1)
+        _G._add_metrics(entry, "training", self._metrics_from_raw(spec, spec.frame, raw))
+        if spec.valid is not None:
+            _G._add_metrics(entry, "validation", self._metrics_from_raw(spec, spec.valid,
+                                                                        self._predict_raw(spec.valid)))
+
+    def _validate_glm(self, spec, fam):
+        """GLM.init (hex/glm/GLM.java:846-1017) parameter checks."""
+        p = self._parms
+        solver = (p.get("solver") or "AUTO").upper()
+        link = (p.get("link") or "family_default").lower()
+        if solver in ("GRADIENT_DESCENT_LH", "GRADIENT_DESCENT_SQERR") and fam != "ordinal":
+            raise ValueError("ERRR on field: _solver: Solvers GRADIENT_DESCENT_LH and GRADIENT_DESCENT_SQERR are "
+                             "only supported for ordinal regression.  Do not choose them unless you specify your "
+                             "family to be ordinal")
+        if (p.get("family") or "AUTO").lower() == "auto" and link != "family_default":
+            nc = spec.nclasses
+            ok = ("identity", "log", "inverse") if nc <= 1 else (("logit",) if nc == 2 else ("multinomial",))
+            if link not in ok:
+                raise ValueError(f"ERRR on field: _family: AUTO for underlying response requires the link to be "
+                                 f"family_default or {', '.join(ok)}.")
+        if fam in ("poisson", "negativebinomial", "gamma"):
+            y = spec.y_tensor().to(torch.float64)
+            ymin = coll.allreduce_scalar(float(torch.nan_to_num(y, nan=float("inf")).min()) if y.numel()
+                                         else float("inf"), op="min")
+            if fam == "gamma" and ymin <= 0:
+                raise ValueError("ERRR on field: _family: Response value for gamma distribution must be greater "
+                                 "than 0.")
+            if fam != "gamma" and ymin < 0:
+                raise ValueError("ERRR on field: _family: Poisson and Negative Binomial require response >= 0")
+            if fam == "negativebinomial":
+                th = float(p.get("theta") or 1e-10)
+                if th <= 0 or th > 1:
+                    raise ValueError("ERRR on field: _family: Illegal Negative Binomial theta value.  Valid theta "
+                                     "values be > 0 and <= 1.")
+        if fam == "ordinal":
+            if spec.nclasses <= 2:
+                raise ValueError("ERRR on field: _family: Ordinal requires a categorical response with at least 3 "
+                                 "levels (for 2 class problem use family=binomial.")
+            if link in ("oprobit", "ologlog"):
+                raise ValueError("ERRR on field: _link: Ordinal regression only supports ologit as link.")
+            if spec.offset_column:
+                raise ValueError("ERRR on field: offset_column: does not work with ordinal family right now.  Will "
+                                 "be fixed in the future.")
+        if fam == "fractionalbinomial":
+            y = spec.y_tensor().to(torch.float64)
+            y = y[~torch.isnan(y)]
+            lo = coll.allreduce_scalar(float(y.min()) if y.numel() else 0.0, op="min")
+            hi = coll.allreduce_scalar(float(y.max()) if y.numel() else 0.0, op="max")
+            if lo < 0 or hi > 1:
+                raise ValueError(f"ERRR on field: response: Response '{spec.y}' must be between 0 and 1 for "
+                                 f"fractional_binomial family. Min: {lo:f}, Max: {hi:f}")
+        mvh = (p.get("missing_values_handling") or "MeanImputation").lower()
+        if p.get("plug_values") is not None and mvh != "plugvalues":
+            raise ValueError("ERRR on field: _missing_values_handling: When plug values are provided - Missing "
+                             "Values Handling needs to be explicitly set to PlugValues.")
+        if p.get("plug_values") is None and mvh == "plugvalues":
+            raise ValueError("ERRR on field: _missing_values_handling: No plug values frame provided for Missing "
+                             "Values Handling = PlugValues.")
+        disp_fams = ("tweedie", "gamma", "negativebinomial")
+        if p.get("build_null_model") and fam not in disp_fams:
+            raise ValueError("ERRR on field: build_null_model: is only supported for tweedie, gamma and "
+                             "negativebinomial familes")
+        if p.get("max_iterations") is not None and int(p.get("max_iterations")) == 0:
+            raise ValueError("ERRR on field: _max_iterations: if specified, must be >= 1.")
+        if p.get("lambda_search") and int(p.get("stopping_rounds") or 0) > 0:
+            raise ValueError("ERRR on field: early stop: cannot run when lambda_search=True.  Lambda_search has its "
+                             "own early-stopping mechanism")
+        if fam in ("multinomial", "ordinal") and (p.get("beta_constraints") is not None or p.get("non_negative")):
+            what = "non_negative" if p.get("non_negative") else "beta_constraints"
+            raise ValueError(f"ERRR on field: {what}: does not work with {fam} family.")
+        method = (p.get("dispersion_parameter_method") or "pearson").lower()
+        if method not in ("pearson", "deviance", "ml"):
+            raise ValueError(f"dispersion_parameter_method must be one of pearson, deviance, ml; got {method}")
+        if method == "ml":
+            if fam != "gamma":
+                raise ValueError("ERRR on field: dispersion_parameter_mode: ml can only be used for family gamma.")
+            if int(p.get("max_iterations_dispersion") or 0) <= 0:
+                raise ValueError("ERRR on field: max_iterations_dispersion: must > 0.")
+            if float(p.get("dispersion_epsilon") if p.get("dispersion_epsilon") is not None else 1e-4) < 0:
+                raise ValueError("ERRR on field: dispersion_epsilon: must >= 0.")
+        if p.get("fix_dispersion_parameter") and fam not in disp_fams:
+            raise ValueError("ERRR on field: fix_dispersion_parameter: is only supported for gamma, tweedie, "
+                             "negativebinomial families.")
+        if float(p.get("init_dispersion_parameter") if p.get("init_dispersion_parameter") is not None else 1) <= 0:
+            raise ValueError("ERRR on field: init_dispersion_parameter: must exceed 0.0.")
+        if p.get("compute_p_values") and p.get("beta_constraints") is not None:
+            raise ValueError("ERRR on field: _compute_p_values: P-values can not be computed for constrained "
+                             "problems")
+
+    def _estimate_dispersion(self, drv):
+        """Dispersion parameter for the p-values (GLM.java:2320-2344):
+        1 for binomial / poisson, init_dispersion_parameter when fixed,
+        else Pearson (sum w (y - mu)^2 / V(mu)) or deviance sum over
+        nobs - 1 - #active predictors, or the maximum-likelihood estimate
+        for gamma (GLM.java:2375 estimateMLSE: Newton on 1/phi with the
+        di/trigamma sums as one fused device pass per iteration).
+        Returns (dispersion, estimated)."""
+        p = self._parms
+        fam = drv.family
+        init = float(p.get("init_dispersion_parameter") or 1.0)
+        if fam in ("binomial", "poisson") or p.get("fix_dispersion_parameter"):
+            return (1.0 if fam in ("binomial", "poisson") and not p.get("fix_dispersion_parameter") else init), False
+        method = (p.get("dispersion_parameter_method") or "pearson").lower()
+        mu = drv.fam.linkinv(drv._eta())
+        w, y = drv.w, drv.y
+        nact = drv.P - (int((~drv.active[: drv.P]).sum()) if drv.active is not None else 0)
+        if method in ("pearson", "deviance"):
+            if method == "deviance":
+                s = (w * drv.fam.deviance(y, mu)).nan_to_num(0.0).sum()
+            elif fam == "tweedie":
+                s = (w * (y - mu) ** 2 / mu.abs().pow(drv.fam.tvp)).nan_to_num(0.0).sum()
+            else:
+                s = (w * (y - mu) ** 2 / drv.fam.variance(mu)).nan_to_num(0.0).sum()
+            return coll.allreduce_scalar(float(s)) / max(drv.nobs - 1 - nact, 1), True
+        # ml (gamma)
+        pos = (y > 0) & (w > 0)
+        wp, yp, mp = w[pos], y[pos], mu[pos]
+        tmp = wp * yp / mp
+        st = torch.stack([wp.sum(), (wp * torch.log(tmp)).sum(), tmp.sum()])
+        coll.allreduce_(st)
+        wsum, sum_ln, sum_yu = (float(v) for v in st)
+        const = wsum + sum_ln - sum_yu
+        alpha = 1.0 / init
+        eps = float(p.get("dispersion_epsilon") if p.get("dispersion_epsilon") is not None else 1e-4)
+        for _ in range(int(p.get("max_iterations_dispersion") or 3000)):
+            dt = torch.stack([(wp * torch.special.digamma(wp * alpha)).sum(),
+                              (wp * wp * torch.special.polygamma(1, wp * alpha)).sum()])
+            coll.allreduce_(dt)
+            num = wsum * math.log(alpha) - float(dt[0]) + const
+            den = wsum / alpha - float(dt[1])
+            if den == 0 or not math.isfinite(num / den):
+                break
+            change = num / den
+            if abs(change) < eps:
+                alpha -= change
+                break
+            alpha = alpha - change if alpha - change >= 0 else alpha * 0.5
+        return 1.0 / alpha, True
 
     def _finalize_outputs(self, drv, sm):
         names = drv.dinfo.coef_names
@@ -885,18 +1128,13 @@ class H2OGeneralizedLinearEstimator(H2OEstimator):
         except np.linalg.LinAlgError:
             inv = np.linalg.pinv(Ga)
         nz = P + (1 if drv.intercept else 0)
-        if drv.family in ("gaussian", "gamma", "tweedie", "quasibinomial"):
-            eta = drv._eta()
-            mu = drv.fam.linkinv(eta)
-            pear = float((drv.w * (drv.y - mu) ** 2 / drv.fam.variance(mu)).sum())
-            disp = coll.allreduce_scalar(pear) / max(drv.nobs - nz, 1)
-        else:
-            disp = 1.0
+        disp, estimated = self._estimate_dispersion(drv)
         se_std = np.sqrt(np.maximum(np.diag(inv), 0) * disp)
         from scipy import stats
         beta = drv.beta if drv.intercept else drv.beta[:-1]
         z = beta / np.where(se_std > 0, se_std, np.nan)
-        if drv.family in ("gaussian", "gamma", "tweedie", "quasibinomial"):
+        if estimated:
+            # GLMModel.setZValues: Student t with nobs - rank degrees of freedom
             pv = 2 * stats.t.sf(np.abs(z), max(drv.nobs - nz, 1))
         else:
             pv = 2 * stats.norm.sf(np.abs(z))
@@ -911,6 +1149,7 @@ class H2OGeneralizedLinearEstimator(H2OEstimator):
         self._output["z_values"] = dict(zip(names, z.tolist()))
         self._output["p_values"] = dict(zip(names, pv.tolist()))
         self._output["dispersion"] = disp
+        self._output["dispersion_estimated"] = estimated
 
     # ---- accessors (h2o-py GLM API)
     def coef(self):

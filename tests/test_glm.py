@@ -64,7 +64,12 @@ def test_glm_poisson_and_lambda_search():
     m.train(y="y", training_frame=fr)
     c = m.coef()
     assert abs(c["b"] - (-0.6)) < 0.1
-    assert len(m.getGLMRegularizationPath(m)["lambdas"]) == 20
+    # early_stopping (GLM.java:2977) ends the path once 5 submodels improve
+    # training deviance by < 1e-4; without it the whole path is fitted
+    assert len(m.getGLMRegularizationPath(m)["lambdas"]) < 20
+    m2 = GLM(family="poisson", lambda_search=True, nlambdas=20, early_stopping=False)
+    m2.train(y="y", training_frame=fr)
+    assert len(m2.getGLMRegularizationPath(m2)["lambdas"]) == 20
 
 
 def test_glm_multinomial():
