@@ -149,6 +149,10 @@ class H2OAggregatorEstimator(H2OEstimator):
             span = float(((samp.max(0).values - samp.min(0).values) ** 2).sum())
             lo_r, hi_r = 1e-8 * max(span, 1e-12), max(span, 1e-12)
             r2 = math.sqrt(lo_r * hi_r)
+            # Aggregator.java:197: stop once the exemplar count has not grown for
+            # num_iteration_without_new_exemplar too-few rounds
+            stall_max = int(p.get("num_iteration_without_new_exemplar", 500))
+            prev, stall = -1, 0
             for _ in range(30):
                 ex_s, _ = _exemplars(samp, r2, max_ex=int(target * (1 + tol) * 4))
                 k = ex_s.numel() * (n / samp.shape[0]) ** 0.5 if samp.shape[0] < n else ex_s.numel()
@@ -158,6 +162,11 @@ class H2OAggregatorEstimator(H2OEstimator):
                     lo_r = r2
                 else:
                     hi_r = r2
+                    if ex_s.numel() == prev:
+                        stall += 1
+                    if stall > stall_max:
+                        break
+                    prev = ex_s.numel()
                 r2 = math.sqrt(lo_r * hi_r)
             for _ in range(20):
                 ex_p, E = _exemplars(Xs, r2, max_ex=int(target * (1 + tol)) + 1)

@@ -39,10 +39,10 @@ from .kmeans import KMEANS_DEFAULTS, H2OKMeansEstimator  # noqa: E402,F401  (fus
 
 
 # ====================================================================== PCA / SVD
-def _transform_info(frame, x, transform, use_all):
+def _transform_info(frame, x, transform, use_all, mvh="MeanImputation"):
     t = (transform or "NONE").upper()
     di = DataInfo(frame, x, standardize=t in ("STANDARDIZE", "DESCALE", "DEMEAN", "NORMALIZE"),
-                  use_all_factor_levels=use_all, pad_to=32)
+                  use_all_factor_levels=use_all, pad_to=32, missing_values_handling=mvh)
     if t in ("DEMEAN",):
         di.sigmas = [1.0] * len(di.sigmas)
     if t == "DESCALE":
@@ -57,6 +57,50 @@ def _transform_info(frame, x, transform, use_all):
     return di
 
 
+def _top_eig(G, k, method, iters, seed):
+    """Top-k eigenpairs of the symmetric (all-reduced, identical on every
+    rank) Gram G by hex/svd/SVD.java's methods: GramSVD = exact
+    eigendecomposition, Power = power iterations with deflation (stops at
+    1e-10 change or max_iterations), Randomized = max_iterations subspace
+    iterations from a seeded Gaussian block then a Rayleigh-Ritz step."""
+    G = G.to(torch.float64).cpu()
+    P = G.shape[0]
+    k = min(k, P)
+    m = (method or "GramSVD").lower()
+    gen = torch.Generator(device="cpu").manual_seed(seed)
+    if m == "power":
+        V = torch.zeros((P, k), dtype=torch.float64)
+        lam = torch.zeros(k, dtype=torch.float64)
+        R = G.clone()
+        for j in range(k):
+            v = torch.randn(P, generator=gen, dtype=torch.float64)
+            v = v / v.norm().clamp_min(1e-300)
+            for _ in range(max(1, iters)):
+                w = R @ v
+                nw = w.norm()
+                if float(nw) == 0:
+                    break
+                w = w / nw
+                done = float((w - v).abs().max()) < 1e-10
+                v = w
+                if done:
+                    break
+            lam[j] = v @ (R @ v)
+            V[:, j] = v
+            R = R - lam[j] * torch.outer(v, v)
+        return lam, V
+    if m == "randomized":
+        Q = torch.randn((P, k), generator=gen, dtype=torch.float64)
+        for _ in range(max(1, iters)):
+            Q, _ = torch.linalg.qr(G @ Q)
+        lb, W = torch.linalg.eigh(Q.T @ G @ Q)
+        order = torch.argsort(lb, descending=True)
+        return lb[order], Q @ W[:, order]
+    lam, V = torch.linalg.eigh(G)
+    order = torch.argsort(lam, descending=True)[:k]
+    return lam[order], V[:, order]
+
+
 PCA_DEFAULTS = dict(transform="none", k=1, max_iterations=1000, seed=-1, use_all_factor_levels=False,
                     compute_metrics=True, impute_missing=False, pca_method="GramSVD", pca_impl="mtj_evd_symmmatrix",
                     max_runtime_secs=0.0, export_checkpoints_dir=None)
@@ -69,10 +113,11 @@ class H2OPrincipalComponentAnalysisEstimator(H2OEstimator):
 
     def _fit(self, spec):
         p = self._parms
-        di = _transform_info(spec.frame, spec.x, p.get("transform"), bool(p.get("use_all_factor_levels")))
+        di = _transform_info(spec.frame, spec.x, p.get("transform"), bool(p.get("use_all_factor_levels")),
+                             mvh="MeanImputation" if p.get("impute_missing") else "Skip")
         self._dinfo = di
         X, ok = di.expand(spec.frame)
-        X = X[ok]
+        X = X[ok]          # impute_missing=False: rows with an NA are skipped (PCA.java)
         n = coll.allreduce_scalar(float(X.shape[0]))
         k = int(p.get("k", 1))
         method = (p.get("pca_method") or "GramSVD").lower()
@@ -87,9 +132,16 @@ class H2OPrincipalComponentAnalysisEstimator(H2OEstimator):
                 # covariance about the mean (reference demeans via the Gram's intercept row)
                 G = G - n * torch.outer(mean, mean)
             cov = G / max(n - 1, 1)
-            evals, evecs = torch.linalg.eigh(cov.cpu())
-            order = torch.argsort(evals, descending=True)
-            evals, evecs = evals[order], evecs[:, order]
+            impl = str(p.get("pca_impl") or "mtj_evd_symmmatrix").lower()
+            if impl == "mtj_svd_densematrix":
+                # PCAImplementation.MTJ_SVD_DENSEMATRIX: singular values of the
+                # covariance (= its eigenvalues, PSD), not an eigensolver
+                U_, S_, _ = torch.linalg.svd(cov.cpu())
+                evals, evecs = S_, U_
+            else:   # MTJ_EVD_DENSEMATRIX / MTJ_EVD_SYMMMATRIX / JAMA: symmetric eigensolver
+                evals, evecs = torch.linalg.eigh(cov.cpu())
+                order = torch.argsort(evals, descending=True)
+                evals, evecs = evals[order], evecs[:, order]
         else:  # Power / Randomized: subspace iteration on X (GEMMs on device)
             gen = torch.Generator(device="cpu").manual_seed(_seed(p))
             Q = torch.randn((P, k + 5), generator=gen, dtype=torch.float64).to(X.device)
@@ -137,7 +189,9 @@ class H2OPrincipalComponentAnalysisEstimator(H2OEstimator):
     transform = predict
 
     def _score_unsupervised(self, spec):
-        self._training_metrics = mm.ModelMetricsDimReduction(nobs=spec.frame.nrows)
+        # compute_metrics=False: no training metrics (PCAModel.makeMetricBuilder skipped)
+        self._training_metrics = mm.ModelMetricsDimReduction(nobs=spec.frame.nrows) \
+            if self._parms.get("compute_metrics", True) else None
 
     def varimp(self, use_pandas=False):
         return self._output["importance"]
@@ -166,9 +220,7 @@ class H2OSingularValueDecompositionEstimator(H2OEstimator):
         P = di.P
         G = linalg_ops.weighted_gram(X)[:P, :P]
         coll.allreduce_(G)
-        ev, V = torch.linalg.eigh(G.cpu())
-        order = torch.argsort(ev, descending=True)
-        ev, V = ev[order][:nv], V[:, order][:, :nv]
+        ev, V = _top_eig(G, nv, p.get("svd_method") or "GramSVD", int(p.get("max_iterations", 1000)), _seed(p))
         d = torch.sqrt(ev.clamp_min(0))
         self._V = V
         self._d = d
@@ -178,6 +230,16 @@ class H2OSingularValueDecompositionEstimator(H2OEstimator):
             U = (X[:, :P].to(torch.float64) @ V.to(X.device)) / d.to(X.device).clamp_min(1e-300)
             self._u = H2OFrame.from_vecs([Vec(U[:, j].contiguous(), T_REAL) for j in range(U.shape[1])],
                                          [f"u{j + 1}" for j in range(U.shape[1])])
+            # u_name / v_name: DKV keys of the U and V frames (SVDModel._u_key / _v_key)
+            from ..core import dkv
+            uk = p.get("u_name") or f"SVDUMatrix_{self.model_id}"
+            dkv.put(uk, self._u)
+            self._output["u_key"] = {"name": uk}
+        import pandas as pd
+        vk = p.get("v_name") or f"SVDVMatrix_{self.model_id}"
+        from ..core import dkv
+        dkv.put(vk, H2OFrame(pd.DataFrame(V.numpy(), columns=[f"Vec{j + 1}" for j in range(V.shape[1])])))
+        self._output["v_key"] = {"name": vk}
 
     def d(self):
         return self._output["d"]
@@ -210,6 +272,13 @@ NB_DEFAULTS = dict(laplace=0.0, min_sdev=0.001, eps_sdev=0.0, min_prob=0.001, ep
 class H2ONaiveBayesEstimator(H2OEstimator):
     algo = "naivebayes"
     _defaults = NB_DEFAULTS
+
+    def _score_all(self, spec):
+        # compute_metrics=False (NaiveBayes.java): no training / validation metrics
+        if not self._parms.get("compute_metrics", True):
+            self._training_metrics = self._validation_metrics = None
+            return
+        super()._score_all(spec)
 
     def _fit(self, spec):
         if not spec.is_classification:

@@ -164,8 +164,24 @@ class H2OCoxProportionalHazardsEstimator(H2OEstimator):
         fr = spec.frame
         self._strata_domains = {c: list(fr.vec(c).domain) for c in (p.get("stratify_by") or [])
                                 if fr.vec(c).domain is not None}
-        di = DataInfo(fr, spec.x, standardize=False, use_all_factor_levels=bool(p.get("use_all_factor_levels")),
-                      missing_values_handling="Skip", pad_to=0)
+        # interactions / interaction_pairs / interactions_only (Model.InteractionSpec):
+        # interactions-only columns feed the interaction features but are not
+        # main effects themselves
+        from .glm.interactions import interaction_pairs
+        io = [c for c in (p.get("interactions_only") or []) if c]
+        for c in io:
+            if c not in fr.names:
+                raise ValueError(f"ERRR on field: interactions_only: {c} not found in the training frame")
+        pairs = interaction_pairs(spec.x, p.get("interactions"), p.get("interaction_pairs"))
+        used = {c for pr in pairs for c in pr}
+        for c in io:
+            if c not in used:
+                import warnings
+                warnings.warn(f"Column '{c}' was marked to be used for interactions only but it is not actually "
+                              "required in any interaction.")
+        x_main = [c for c in spec.x if c not in io]
+        di = DataInfo(fr, x_main, standardize=False, use_all_factor_levels=bool(p.get("use_all_factor_levels")),
+                      missing_values_handling="Skip", pad_to=0, interactions=pairs or None)
         self._dinfo = di
         X, ok = di.expand(fr, dtype=torch.float64, pad=False)
         stop = fr.vec(p["stop_column"]).as_float(torch.float64)
@@ -246,6 +262,115 @@ class H2OCoxProportionalHazardsEstimator(H2OEstimator):
         o["loglik_test"] = 2 * (ll - self._null_loglik)
         lp = self._lp_tensor(X, strata)
         o["concordance"] = _concordance(stop, ev, lp, strata)
+        if p.get("calc_cumhaz", True):
+            self._cumhaz(X, stop, ev, w, strata, efron)
+
+    def _cumhaz(self, X, stop, ev, w, strata, efron):
+        """calc_cumhaz (CoxPH.java:503 calcCumhaz_0): the Breslow baseline
+        hazard / survival per stratum at every distinct stop time, with
+        risks exp((x - mean) . beta) (numeric covariates de-meaned as the
+        reference's DEMEAN DataInfo), and the cumulative hazard of the
+        mean covariate vector with its two variance terms (Efron or
+        Breslow tie handling) for survfit-style curves.  One sort + segment
+        sums on the device; the per-time recursion is a cumsum."""
+        di = self._dinfo
+        beta = self._beta
+        xc = X.clone()
+        nb = di.n_cat_expanded
+        if xc.shape[1] > nb:
+            xc[:, nb:] = xc[:, nb:] - xc[:, nb:].mean(0, keepdim=True)
+        risk = w * torch.exp(xc @ beta)
+        times, tix = torch.unique(stop, return_inverse=True)
+        T = times.numel()
+        keys = self._strata_keys
+        S = len(keys)
+        sidx = torch.zeros_like(tix)
+        for i, k in enumerate(keys):
+            sidx = torch.where(strata == k, torch.full_like(tix, i), sidx)
+        flat = sidx * T + tix
+        def seg(v):
+            out = torch.zeros(S * T, dtype=torch.float64, device=X.device)
+            out.index_add_(0, flat, v)
+            return out.view(S, T)
+        size_ev = seg(w * ev)
+        risk_all = seg(risk)
+        total = torch.zeros(S, dtype=torch.float64, device=X.device)
+        total.index_add_(0, sidx, risk)
+        # risk still at stake before time t: total minus the rows that left earlier
+        at_risk = total.view(-1, 1) - (torch.cumsum(risk_all, 1) - risk_all)
+        haz = torch.where(size_ev > 0, size_ev / at_risk.clamp_min(1e-300), torch.zeros_like(size_ev))
+        surv = torch.exp(-torch.cumsum(haz, 1))
+        tn = times.cpu().numpy()
+        names = ["t"] + ([",".join(str(v) for v in self._strata_label(k)) for k in keys] if self._strata_domains
+                         else [])
+        hz_cols = {"t": tn}
+        sv_cols = {"t": tn}
+        if not self._strata_domains:
+            hz_cols["baseline hazard"] = haz[0].cpu().numpy()
+            sv_cols["baseline survival"] = surv[0].cpu().numpy()
+        else:
+            for i, nm in enumerate(names[1:]):
+                hz_cols[nm] = haz[i].cpu().numpy()
+                sv_cols[nm] = surv[i].cpu().numpy()
+        self._output["baseline_hazard"] = H2OFrame(pd.DataFrame(hz_cols))
+        self._output["baseline_survival"] = H2OFrame(pd.DataFrame(sv_cols))
+        # cumhaz_0 / var_cumhaz_1 / var_cumhaz_2 over the times with any row
+        ev_cnt = seg(ev * (w > 0)).sum(0)
+        sz = size_ev.sum(0)
+        rs_all = risk_all.sum(0)
+        rcum = torch.flip(torch.cumsum(torch.flip(rs_all, [0]), 0), [0])      # risk of stop >= t
+        xr = torch.zeros((T, X.shape[1]), dtype=torch.float64, device=X.device)
+        xr.index_add_(0, tix, xc * risk.view(-1, 1))
+        rcum_x = torch.flip(torch.cumsum(torch.flip(xr, [0]), 0), [0])
+        rev = torch.zeros(T, dtype=torch.float64, device=X.device)
+        rev.index_add_(0, tix, risk * ev)
+        xrev = torch.zeros_like(xr)
+        xrev.index_add_(0, tix, xc * (risk * ev).view(-1, 1))
+        present = torch.zeros(T, dtype=torch.bool, device=X.device)
+        present[tix] = True
+        ch = torch.zeros(T, dtype=torch.float64, device=X.device)
+        v1 = torch.zeros_like(ch)
+        v2 = torch.zeros_like(xr)
+        if efron:
+            cmax = int(ev_cnt.max().item()) if T else 0
+            for e in range(cmax):
+                m = ev_cnt > e
+                frac = torch.where(m, e / ev_cnt.clamp_min(1), torch.zeros_like(ev_cnt))
+                h = torch.where(m, 1.0 / (rcum - frac * rev).clamp_min(1e-300), torch.zeros_like(rcum))
+                avg = torch.where(m, sz / ev_cnt.clamp_min(1), torch.zeros_like(sz))
+                ch += avg * h
+                v1 += avg * h * h
+                v2 += (avg * h * h).view(-1, 1) * (rcum_x - frac.view(-1, 1) * xrev)
+        else:
+            ch = sz / rcum.clamp_min(1e-300)
+            v1 = sz / (rcum * rcum).clamp_min(1e-300)
+            v2 = (rcum_x / rcum.clamp_min(1e-300).view(-1, 1)) * ch.view(-1, 1)
+        keep = present
+        self._output["cumhaz_0"] = torch.cumsum(ch[keep], 0).cpu().numpy()
+        self._output["var_cumhaz_1"] = torch.cumsum(v1[keep], 0).cpu().numpy()
+        self._output["var_cumhaz_2"] = torch.cumsum(v2[keep], 0).cpu().numpy()
+        self._output["time"] = tn[keep.cpu().numpy()]
+
+    def _strata_label(self, key):
+        """Level names of a stratum key built by _strata (mixed radix)."""
+        sb = self._parms.get("stratify_by") or []
+        out = []
+        k = int(key)
+        for c in reversed(sb):
+            dom = self._strata_domains.get(c)
+            base = len(dom) + 1 if dom else 1_000_003
+            code = k % base - 1
+            k //= base
+            out.append(dom[code] if dom and 0 <= code < len(dom) else "NA" if dom else code)
+        return list(reversed(out))
+
+    @property
+    def baseline_hazard_frame(self):
+        return self._output.get("baseline_hazard")
+
+    @property
+    def baseline_survival_frame(self):
+        return self._output.get("baseline_survival")
 
     def _lp_tensor(self, X, strata):
         lp = X @ self._beta

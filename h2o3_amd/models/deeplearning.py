@@ -31,9 +31,12 @@ fused backward with bias-gradient column sums, one per-neuron-row update
 kernel doing gradient + L1/L2 + ADADELTA / momentum + max_w2 + bias update,
 softmax + output gradient).  The reference's per-row Hogwild updates are a
 CPU-cache idiom; here a mini-batch gradient (mini_batch_size, at least 32
-rows) is applied per step, and with several GPUs the gradients of every
-layer are averaged by one bucketed RCCL all-reduce per step (synchronous
-data parallel instead of the reference's periodic model averaging).
+rows) is applied per step.  With several GPUs each rank trains its own
+copy for an iteration with no collective in the (graph-captured) step and
+the models are averaged by one bucketed RCCL all-reduce per iteration -- the
+reference's model averaging (DeepLearningTask.reduce), with its elastic
+averaging, replicate_training_data, single_node_mode and the
+target_ratio_comm_to_comp auto-tuning of the iteration size.
 """
 from __future__ import annotations
 
@@ -75,6 +78,27 @@ DL_DEFAULTS = dict(activation="Rectifier", hidden=[200, 200], epochs=10.0, train
                    use_all_factor_levels=True, checkpoint=None, overwrite_with_best_model=True)
 
 _MIN_GPU_BATCH = 32
+
+
+def _murmur3_int(v, seed):
+    """32-bit murmur3 of one big-endian int (the hash trick of
+    Neurons.Input.setInput)."""
+    c1, c2, m32 = 0xCC9E2D51, 0x1B873593, 0xFFFFFFFF
+    k = int.from_bytes(int(v & m32).to_bytes(4, "big"), "little")
+    h = seed & m32
+    k = (k * c1) & m32
+    k = ((k << 15) | (k >> 17)) & m32
+    k = (k * c2) & m32
+    h ^= k
+    h = ((h << 13) | (h >> 19)) & m32
+    h = (h * 5 + 0xE6546B64) & m32
+    h ^= 4
+    h ^= h >> 16
+    h = (h * 0x85EBCA6B) & m32
+    h ^= h >> 13
+    h = (h * 0xC2B2AE35) & m32
+    h ^= h >> 16
+    return h
 
 
 def _act_name(activation):
@@ -190,6 +214,86 @@ class H2ODeepLearningEstimator(H2OEstimator):
         zs.append(Zo)
         return acts, zs
 
+    # ------------------------------------------------------------------ inputs
+    def _validate_dl(self, spec, di):
+        """DeepLearningParameters.validate (DeepLearningModel.java:1760-1940)."""
+        p = self._parms
+        if not 0 <= float(p.get("score_duty_cycle", 0.1)) <= 1:
+            raise ValueError("ERRR on field: _score_duty_cycle: Score duty cycle must be >= 0 and <=1.")
+        if int(p.get("score_validation_samples") or 0) < 0:
+            raise ValueError("ERRR on field: _score_validation_samples: Number of training samples for scoring must "
+                             "be >= 0 (0 for all).")
+        if int(p.get("max_categorical_features", 2147483647)) < 1:
+            raise ValueError("ERRR on field: _max_categorical_features: max_categorical_features must be at least 1.")
+        if p.get("elastic_averaging"):
+            if not 0 <= float(p.get("elastic_averaging_moving_rate", 0.9)) <= 1:
+                raise ValueError("ERRR on field: _elastic_averaging_moving_rate: Elastic averaging moving rate must "
+                                 "be between 0 and 1.")
+            if float(p.get("elastic_averaging_regularization", 1e-3)) < 0:
+                raise ValueError("ERRR on field: _elastic_averaging_regularization: Elastic averaging "
+                                 "regularization strength must be >= 0.")
+            if p.get("sparse"):
+                raise ValueError("ERRR on field: _elastic_averaging: Cannot use elastic averaging with sparse input.")
+        if str(p.get("score_validation_sampling") or "Uniform").lower() not in ("uniform", "stratified"):
+            raise ValueError("score_validation_sampling must be Uniform or Stratified")
+        if p.get("reproducible") and p.get("seed", -1) in (None, -1):
+            import warnings
+            warnings.warn("reproducible=True without a seed: the run is deterministic for the default seed only")
+
+    def _hash_slots(self, di):
+        """max_categorical_features (Neurons.Input.setInput, hash trick): the
+        one-hot categorical columns are folded into that many slots by a
+        seeded murmur3 hash of the expanded column index; numeric columns
+        stay.  Returns the slot of every categorical column, or None."""
+        p = self._parms
+        mc = int(p.get("max_categorical_features", 2147483647))
+        ncat = di.n_cat_expanded
+        if mc >= ncat:
+            return None
+        if p.get("autoencoder"):
+            raise ValueError("max_categorical_features below the categorical width is not supported for "
+                             "autoencoders (the reconstruction would be of hashed slots)")
+        seed = int(p.get("seed", -1) if p.get("seed", -1) is not None else -1)
+        slots = np.array([_murmur3_int(j, seed) % mc for j in range(ncat)], dtype=np.int64)
+        return torch.as_tensor(slots, device=cloud.device())
+
+    def _design(self, frame):
+        """(X, ok): the expanded input matrix, categorical columns hashed into
+        max_categorical_features slots when that is below their count."""
+        X, ok = self._dinfo.expand(frame, pad=False)
+        slots = getattr(self, "_cat_slots", None)
+        if slots is None:
+            return X, ok
+        ncat = self._dinfo.n_cat_expanded
+        mc = int(self._parms.get("max_categorical_features"))
+        H = torch.zeros((X.shape[0], mc), dtype=X.dtype, device=X.device)
+        H.index_add_(1, slots, X[:, :ncat])
+        return torch.cat([H, X[:, ncat:]], 1).contiguous(), ok
+
+    def _valid_sample(self, spec):
+        """score_validation_samples / score_validation_sampling
+        (DeepLearning.java:428): the validation frame scored during training
+        is a seeded uniform or class-stratified sample of that many rows."""
+        p = self._parms
+        ns = int(p.get("score_validation_samples") or 0)
+        vf = spec.valid
+        if vf is None or ns <= 0 or ns >= vf.nrows:
+            return vf
+        g = torch.Generator(device=cloud.device())
+        g.manual_seed((self._seed() + 1) * 1000003 + cloud.rank())
+        frac = ns / vf.nrows
+        if str(p.get("score_validation_sampling") or "Uniform").lower() == "stratified" and spec.is_classification:
+            y = spec.y_tensor(vf).long()
+            u = torch.rand(y.numel(), generator=g, device=y.device)
+            keep = torch.zeros_like(u, dtype=torch.bool)
+            for k in range(spec.nclasses):
+                m = y == k
+                keep |= m & (u < frac)
+            keep |= (y < 0) & (u < frac)
+        else:
+            keep = torch.rand(vf.nlocal, generator=g, device=cloud.device()) < frac
+        return vf[keep]
+
     # ------------------------------------------------------------------ fit
     def _fit(self, spec):
         p = self._parms
@@ -198,7 +302,9 @@ class H2ODeepLearningEstimator(H2OEstimator):
                       use_all_factor_levels=bool(p.get("use_all_factor_levels", True)),
                       missing_values_handling=p.get("missing_values_handling"), pad_to=0)
         self._dinfo = di
-        X, ok = di.expand(spec.frame, pad=False)
+        self._validate_dl(spec, di)
+        self._cat_slots = self._hash_slots(di)
+        X, ok = self._design(spec.frame)
         ae = bool(p.get("autoencoder"))
         self._ae = ae
         K = spec.nclasses if (spec.is_classification and not ae) else 1
@@ -290,20 +396,50 @@ class H2ODeepLearningEstimator(H2OEstimator):
         return g * inv_n, lo
 
     def _train_loop(self, spec, X, Y, w, ae, K):
+        """Iterations of train_samples_per_iteration samples.  One GPU runs
+        mini-batch steps (hipGraph-captured).  Several GPUs run the
+        reference's model averaging (DeepLearningTask.reduce/postGlobal):
+        every rank trains its own copy for the iteration with no collective
+        in the step, then ONE all-reduce averages weights, biases and the
+        ADADELTA / momentum state; with elastic_averaging the consensus is
+        the moving time-average of the per-iteration averages
+        (DeepLearningModelInfo.timeAverage) and local models keep training,
+        pulled toward it by elastic_averaging_regularization.  With
+        train_samples_per_iteration=-2 the iteration size is re-tuned each
+        iteration so that averaging costs target_ratio_comm_to_comp of the
+        compute time (DeepLearningModel.java:310)."""
         p = self._parms
-        n = X.shape[0]
         W_ = cloud.world()
-        ntot = coll.allreduce_scalar(float(n))
+        single = W_ > 1 and bool(p.get("single_node_mode"))
+        replicate = W_ > 1 and (bool(p.get("replicate_training_data", True)) or single)
+        if replicate:
+            # replicate_training_data: every rank holds the whole training set
+            X = coll.all_gather_var(X)
+            Y = None if Y is None else coll.all_gather_var(Y)
+            w = None if w is None else coll.all_gather_var(w)
+        n = X.shape[0]
+        ntot = n if replicate else coll.allreduce_scalar(float(n))
+        contrib = 1 if single else W_          # ranks whose samples count
         epochs = float(p.get("epochs", 10))
         mbs = int(p.get("mini_batch_size") or 1)
         # mini_batch_size=1 (the reference's per-row updates): a GPU batch that
         # still gives >= ~256 updates per epoch (ADADELTA's step size does not
         # grow with the batch, so progress per epoch follows the update count)
-        bs = max(mbs, _MIN_GPU_BATCH) if mbs > 1 else int(min(1024, max(_MIN_GPU_BATCH, ntot // (256 * W_))))
-        bs = max(1, min(bs, n))
+        bs = max(mbs, _MIN_GPU_BATCH) if mbs > 1 else int(min(1024, max(_MIN_GPU_BATCH, ntot // (256 * contrib))))
+        n_min = n if replicate or W_ == 1 else int(coll.allreduce_scalar(float(n), op="min"))
+        bs = max(1, min(bs, n_min))      # the same batch on every rank keeps the step counts aligned
         total_samples = epochs * ntot
         tspi = int(p.get("train_samples_per_iteration", -2))
-        per_iter = ntot if tspi in (-2, -1, 0) else max(float(tspi), bs * W_)
+        if tspi == 0:
+            per_iter = float(ntot)
+        elif tspi == -1:
+            per_iter = float(ntot * contrib if replicate else ntot)
+        elif tspi == -2:
+            per_iter = float(ntot) if contrib == 1 else float(min(ntot * contrib, max(16 * bs * contrib, 1)))
+        else:
+            per_iter = max(float(tspi), float(bs * contrib))
+        auto_tune = tspi == -2 and contrib > 1
+        target_ratio = float(p.get("target_ratio_comm_to_comp", 0.05))
         ada = bool(p.get("adaptive_rate", True))
         rate0, anneal, decay = float(p["rate"]), float(p["rate_annealing"]), float(p["rate_decay"])
         mom_start, mom_ramp, mom_stable = float(p["momentum_start"]), float(p["momentum_ramp"]), \
@@ -314,6 +450,13 @@ class H2ODeepLearningEstimator(H2OEstimator):
         sparsity = float(p.get("sparsity_beta") or 0.0) if ae else 0.0
         avg_act = [torch.zeros(L.fout, device=X.device) for L in self._layers[:-1]] if sparsity > 0 else None
         gen = torch.Generator(device=X.device).manual_seed(self._seed() * 31 + cloud.rank())
+        # shuffle_training_data: a fresh permutation per pass; otherwise the
+        # rows are walked in order -- unless one pass is one iteration over a
+        # single-chunk shard, where DeepLearning.java:448 turns shuffling on
+        shuffle = bool(p.get("shuffle_training_data")) or per_iter >= ntot or auto_tune
+        elastic = contrib > 1 and bool(p.get("elastic_averaging"))
+        self._ea = None
+        self._ea_started = False
         t0 = time.time()
         max_rt = float(p.get("max_runtime_secs") or 0)
         self._scoring_history = []
@@ -324,63 +467,170 @@ class H2ODeepLearningEstimator(H2OEstimator):
         history, best = [], None
         hp = dict(K=K, ae=ae, bs=bs, ada=ada, rate0=rate0, anneal=anneal, decay=decay, mom_start=mom_start,
                   mom_ramp=mom_ramp, mom_stable=mom_stable, has_mom=has_mom, l1=l1, l2=l2, max_w2=max_w2,
-                  sparsity=sparsity)
-        step_seed = self._seed() * 1000003
+                  sparsity=sparsity, ea_reg=float(p.get("elastic_averaging_regularization", 1e-3)) if elastic else 0.0)
+        if elastic:
+            self._ea = [(L.W.clone(), L.b.clone()) for L in self._layers]
+        step_seed = self._seed() * 1000003 + 7 * cloud.rank()
         perm, pos = None, n
         samples_done = 0.0
-        next_score = per_iter
+        next_iter = per_iter
         it = 0
         nstep = 0
+        valid_sample = self._valid_sample(spec)
+        score_iv = float(p.get("score_interval", 5.0))
+        duty = float(p.get("score_duty_cycle", 0.1))
+        last_start = last_end = None
+        iter_t0 = time.time()
+        det = bool(p.get("reproducible"))
+        prev_det = torch.are_deterministic_algorithms_enabled()
+        if det:
+            torch.use_deterministic_algorithms(True, warn_only=True)
         graph = self._step_graph(X, Y, w, hp, avg_act) if self._graph_ok(X, hp, avg_act) else None
-        while samples_done < total_samples:
-            if pos + bs > n:
-                perm = torch.randperm(n, generator=gen, device=X.device)
-                pos = 0
-            idx = perm[pos:pos + bs]
-            pos += bs
-            if graph is not None:
-                # ONE graph launch per step: the batch gather, forward, backward,
-                # updates and the dropout-seed advance were captured once
-                graph["idx"].copy_(idx)
-                graph["g"].replay()
-            else:
-                xb = X.index_select(0, idx)
-                yb = None if Y is None else Y.index_select(0, idx)
-                wb = None if w is None else w.index_select(0, idx)
-                step_seed = (step_seed * 6364136223846793005 + 1442695040888963407) & ((1 << 63) - 1)
-                self._train_step(xb, yb, wb, step_seed, hp, avg_act)
-            self._processed += bs * W_
-            samples_done += bs * W_
-            if samples_done >= next_score or samples_done >= total_samples:
-                it += 1
-                next_score += per_iter
-                self._epochs_done = samples_done / max(ntot, 1)
-                entry = self._score_history_entry(spec, X, Y, w, ae, K, t0)
-                self._scoring_history.append(entry)
-                val = entry.get(("validation_" if spec.valid is not None else "training_") + smetric)
-                history.append(val)
-                if val is not None and p.get("overwrite_with_best_model", True):
-                    better = best is None or (val < best[0] if smetric in _LESS_IS_BETTER else val > best[0])
-                    if better:
-                        best = (val, [(L.W.clone(), L.b.clone()) for L in self._layers])
-                if self._stop_on_error(entry, K, ae):
-                    break
-                if stop_rounds > 0 and ScoreKeeper.stop_early(history, stop_rounds,
-                                                              float(p.get("stopping_tolerance", 0.0)),
-                                                              smetric in _LESS_IS_BETTER):
-                    break
-            # job progress / cancel and the max_runtime_secs clock, agreed across
-            # ranks every 64 mini-batches (not per step: a 0.14 ms step)
-            nstep += 1
-            if nstep % 64 == 0 or samples_done >= total_samples:
-                _, timed_out = self._tick(samples_done, total_samples, None, False, t0, max_rt)
-                if timed_out:
-                    break
+        try:
+            while samples_done < total_samples:
+                if pos + bs > n:
+                    perm = torch.randperm(n, generator=gen, device=X.device) if shuffle else \
+                        torch.arange(n, device=X.device)
+                    pos = 0
+                idx = perm[pos:pos + bs]
+                pos += bs
+                if graph is not None:
+                    # ONE graph launch per step: the batch gather, forward, backward,
+                    # updates and the dropout-seed advance were captured once
+                    graph["idx"].copy_(idx)
+                    graph["g"].replay()
+                else:
+                    xb = X.index_select(0, idx)
+                    yb = None if Y is None else Y.index_select(0, idx)
+                    wb = None if w is None else w.index_select(0, idx)
+                    step_seed = (step_seed * 6364136223846793005 + 1442695040888963407) & ((1 << 63) - 1)
+                    self._train_step(xb, yb, wb, step_seed, hp, avg_act)
+                self._processed += bs * contrib
+                samples_done += bs * contrib
+                nstep += 1
+                final = samples_done >= total_samples
+                if samples_done >= next_iter or final:
+                    it += 1
+                    t_comp = time.time() - iter_t0
+                    t_comm = 0.0
+                    if contrib > 1 or single:
+                        tc = time.time()
+                        self._average_models(single, elastic)
+                        t_comm = time.time() - tc
+                    if auto_tune and t_comp > 0:
+                        # DeepLearningModel.java:310: keep comm / comp near the target
+                        corr = (t_comm / t_comp) / max(target_ratio, 1e-9)
+                        if corr > 0 and (corr < 0.8 or corr > 1.2):
+                            per_iter = min(float(ntot * contrib), max(float(bs * contrib), per_iter / corr))
+                        per_iter = float(cloud.agree([per_iter])[0]) if cloud.is_distributed() else per_iter
+                    next_iter = samples_done + per_iter
+                    self._epochs_done = samples_done / max(ntot, 1)
+                    now = time.time()
+                    due = final or bool(p.get("score_each_iteration")) or last_start is None or (
+                        (now - last_start) > score_iv and
+                        (last_end - last_start) / max(now - last_start, 1e-9) < duty)
+                    if cloud.is_distributed():
+                        due = bool(cloud.agree([due])[0])
+                    if due:
+                        last_start = time.time()
+                        swapped = None
+                        if elastic and self._ea_started:
+                            # the consensus model is "the" model: score (and keep) it
+                            swapped = [(L.W.clone(), L.b.clone()) for L in self._layers]
+                            for L, (We, be) in zip(self._layers, self._ea):
+                                L.W.copy_(We)
+                                L.b.copy_(be)
+                        entry = self._score_history_entry(spec, X, Y, w, ae, K, t0, valid_sample)
+                        last_end = time.time()
+                        self._scoring_history.append(entry)
+                        val = entry.get(("validation_" if valid_sample is not None else "training_") + smetric)
+                        history.append(val)
+                        if val is not None and p.get("overwrite_with_best_model", True):
+                            better = best is None or (val < best[0] if smetric in _LESS_IS_BETTER else val > best[0])
+                            if better:
+                                best = (val, [(L.W.clone(), L.b.clone()) for L in self._layers])
+                        if swapped is not None:
+                            for L, (Wl, bl) in zip(self._layers, swapped):
+                                L.W.copy_(Wl)
+                                L.b.copy_(bl)
+                        if self._stop_on_error(entry, K, ae):
+                            break
+                        if stop_rounds > 0 and ScoreKeeper.stop_early(history, stop_rounds,
+                                                                      float(p.get("stopping_tolerance", 0.0)),
+                                                                      smetric in _LESS_IS_BETTER):
+                            break
+                    iter_t0 = time.time()
+                # job progress / cancel and the max_runtime_secs clock, agreed across
+                # ranks every 64 mini-batches (not per step: a 0.14 ms step)
+                if nstep % 64 == 0 or final:
+                    _, timed_out = self._tick(samples_done, total_samples, None, False, t0, max_rt)
+                    if timed_out:
+                        if contrib > 1 or single:
+                            self._average_models(single, elastic)
+                        break
+        finally:
+            if det:
+                torch.use_deterministic_algorithms(prev_det, warn_only=True)
         self._epochs_done = samples_done / max(ntot, 1)
+        if elastic and self._ea is not None:
+            # the consensus (elastic average) is the model
+            for L, (We, be) in zip(self._layers, self._ea):
+                L.W.copy_(We)
+                L.b.copy_(be)
         if best is not None and p.get("overwrite_with_best_model", True):
             for L, (Wb, bb) in zip(self._layers, best[1]):
                 L.W.copy_(Wb)
                 L.b.copy_(bb)
+        if p.get("export_weights_and_biases"):
+            self._export_weights()
+
+    def _average_models(self, single, elastic):
+        """Model averaging at an iteration boundary: one bucketed all-reduce of
+        every layer's weights, biases and optimizer state (divided by the
+        number of ranks), or rank 0's model broadcast (single_node_mode)."""
+        W_ = cloud.world()
+        ts = []
+        for L in self._layers:
+            ts += [L.W, L.b] + [v for _, v in sorted(L.state.items()) if v is not None]
+        if single:
+            for t in ts:
+                coll.broadcast_(t, 0)
+            return
+        if elastic:
+            local = [(L.W.clone(), L.b.clone()) for L in self._layers]
+        coll.allreduce_many_(ts)
+        for t in ts:
+            t.div_(W_)
+        if elastic:
+            # DeepLearningModelInfo.timeAverage: consensus <- (1 - pa) consensus
+            # + pa * node average; the local models resume from their own weights
+            pa = float(self._parms.get("elastic_averaging_moving_rate", 0.9))
+            first = getattr(self, "_ea_started", False) is False
+            for (We, be), L in zip(self._ea, self._layers):
+                if first or pa == 1:
+                    We.copy_(L.W)
+                    be.copy_(L.b)
+                else:
+                    We.mul_(1 - pa).add_(L.W, alpha=pa)
+                    be.mul_(1 - pa).add_(L.b, alpha=pa)
+            self._ea_started = True
+            for L, (Wl, bl) in zip(self._layers, local):
+                L.W.copy_(Wl)
+                L.b.copy_(bl)
+
+    def _export_weights(self):
+        """export_weights_and_biases (DeepLearning.java:354): one frame per
+        weight matrix and bias vector in the DKV, keyed by the model id."""
+        from ..core import dkv
+        wk, bk = [], []
+        for i, L in enumerate(self._layers):
+            kw, kb = f"{self.model_id}.weights.{i}", f"{self.model_id}.biases.{i}"
+            dkv.put(kw, H2OFrame.from_tensor(L.W.detach().float()))
+            dkv.put(kb, H2OFrame.from_tensor(L.b.detach().float().view(-1, 1)))
+            wk.append({"name": kw})
+            bk.append({"name": kb})
+        self._output["weights"] = wk
+        self._output["biases"] = bk
 
     def _train_step(self, xb, yb, wb, step_seed, hp, avg_act=None, seed_dev=None):
         """One mini-batch step: forward, output gradient, backward through the
@@ -403,11 +653,12 @@ class H2ODeepLearningEstimator(H2OEstimator):
                 Lp = self._layers[li - 1]
                 dZ, db = dl_ops.bwd(dA, acts[li], zs[li - 1], Lp.act, Lp.drop, seed=step_seed + 7919 * li,
                                     seed_dev=seed_dev)
-        if W_ > 1:
-            flat = [g for (_, a, b_) in grads for g in (a, b_)]
-            coll.allreduce_many_(flat)
-            for g in flat:
-                g.div_(W_)
+        ea = getattr(self, "_ea", None)
+        if ea is not None and hp.get("ea_reg", 0.0) > 0 and getattr(self, "_ea_started", False):
+            # elastic averaging (Neurons.java:262): gradient += reg * (w - w_consensus)
+            reg = hp["ea_reg"]
+            grads = [(li, dW + reg * (self._layers[li].W - ea[li][0]),
+                      db + reg * (self._layers[li].b - ea[li][1])) for (li, dW, db) in grads]
         if avg_act is not None:
             for li in range(len(self._layers) - 1):
                 avg_act[li].mul_(0.999).add_(0.001 * acts[li + 1].mean(0))
@@ -429,10 +680,12 @@ class H2ODeepLearningEstimator(H2OEstimator):
 
     def _graph_ok(self, X, hp, avg_act):
         """HIP-graph the step when nothing in it changes between steps on the
-        host side: ADADELTA (no rate / momentum schedule), one rank (no
-        collective inside the graph), no sparsity running averages."""
+        host side: ADADELTA (no rate / momentum schedule), no sparsity
+        running averages, no elastic-averaging pull (its consensus changes
+        between iterations).  Model averaging keeps collectives out of the
+        step, so several ranks graph their steps too."""
         import os
-        return X.device.type == "cuda" and cloud.world() == 1 and hp["ada"] and avg_act is None and \
+        return X.device.type == "cuda" and hp["ada"] and avg_act is None and not hp.get("ea_reg") and \
             os.environ.get("H2O3_DL_GRAPH", "1") == "1"
 
     def _step_graph(self, X, Y, w, hp, avg_act):
@@ -489,7 +742,7 @@ class H2ODeepLearningEstimator(H2OEstimator):
         mse = entry.get("training_mse")
         return rs >= 0 and mse is not None and mse <= rs
 
-    def _score_history_entry(self, spec, X, Y, w, ae, K, t0):
+    def _score_history_entry(self, spec, X, Y, w, ae, K, t0, valid=None):
         from .tree.gbm import H2OGradientBoostingEstimator as _G
         p = self._parms
         entry = {"timestamp": time.time(), "duration_s": time.time() - t0, "epochs": self._epochs_done,
@@ -516,8 +769,8 @@ class H2ODeepLearningEstimator(H2OEstimator):
             pred = out[:, 0] * self._ysd + self._ymu
             m = mm.regression_metrics((Ys[:, 0] * self._ysd + self._ymu).to(torch.float64), pred, None, self._dist)
         _G._add_metrics(entry, "training", m)
-        if spec.valid is not None:
-            vm = self._metrics_from_raw(spec, spec.valid, self._predict_raw(spec.valid))
+        if valid is not None:
+            vm = self._metrics_from_raw(spec, valid, self._predict_raw(valid))
             _G._add_metrics(entry, "validation", vm)
         return entry
 
@@ -535,7 +788,7 @@ class H2ODeepLearningEstimator(H2OEstimator):
         return Zo
 
     def _predict_raw(self, frame):
-        X, _ = self._dinfo.expand(frame, pad=False)
+        X, _ = self._design(frame)
         with torch.no_grad():
             out = self._predict_matrix(X)
         if self._ae or self._K > 1:
@@ -570,7 +823,7 @@ class H2ODeepLearningEstimator(H2OEstimator):
         return super().predict(test_data, **kw)
 
     def anomaly(self, test_data, per_feature=False):
-        X, _ = self._dinfo.expand(test_data, pad=False)
+        X, _ = self._design(test_data)
         with torch.no_grad():
             out = self._predict_matrix(X)
         err = (out - X) ** 2
@@ -580,7 +833,7 @@ class H2ODeepLearningEstimator(H2OEstimator):
         return H2OFrame.from_vecs([Vec(err.mean(1).contiguous(), T_REAL)], ["Reconstruction.MSE"])
 
     def deepfeatures(self, test_data, layer):
-        X, _ = self._dinfo.expand(test_data, pad=False)
+        X, _ = self._design(test_data)
         with torch.no_grad():
             acts, _ = self._forward(X, False)
         h = acts[layer + 1]
@@ -588,14 +841,24 @@ class H2ODeepLearningEstimator(H2OEstimator):
                                   [f"DF.L{layer + 1}.C{j + 1}" for j in range(h.shape[1])])
 
     def weights(self, matrix_id=0):
-        return H2OFrame.from_tensor(self._layers[matrix_id].W.detach())
+        """Weight matrix frame (needs export_weights_and_biases=True, as the
+        reference's model.weights())."""
+        from ..core import dkv
+        ws = self._output.get("weights")
+        if not ws:
+            raise ValueError("weights are only available with export_weights_and_biases=True")
+        return dkv.get(ws[matrix_id]["name"])
 
     def biases(self, vector_id=0):
-        return H2OFrame.from_tensor(self._layers[vector_id].b.detach().view(-1, 1))
+        from ..core import dkv
+        bs_ = self._output.get("biases")
+        if not bs_:
+            raise ValueError("biases are only available with export_weights_and_biases=True")
+        return dkv.get(bs_[vector_id]["name"])
 
     def _score_unsupervised(self, spec):
         if self._ae:
-            X, _ = self._dinfo.expand(spec.frame, pad=False)
+            X, _ = self._design(spec.frame)
             with torch.no_grad():
                 out = self._predict_matrix(X)
             mse = float(((out - X) ** 2).mean())

@@ -70,6 +70,10 @@ class H2OStackedEnsembleEstimator(H2OEstimator):
             else:
                 cols.append(raw[:, 0])
                 names.append(m.model_id)
+        if str(self._parms.get("metalearner_transform") or "NONE").lower() == "logit" and self._spec.nclasses >= 2:
+            # MetalearnerTransform.Logit (StackedEnsembleModel.java:95): logit of
+            # the base-model probabilities, clamped to [1e-9, 1 - 1e-9]
+            cols = [torch.logit(c.to(torch.float64).clamp(1e-9, 1 - 1e-9)) for c in cols]
         vecs = [Vec(c.to(torch.float32).contiguous(), T_REAL) for c in cols]
         return vecs, names
 
@@ -85,13 +89,29 @@ class H2OStackedEnsembleEstimator(H2OEstimator):
         frame = blend if blend is not None else spec.frame
         vecs, names = self._level_one(base, frame, use_cv=blend is None)
         y = frame.vec(spec.y)
-        lvl1 = H2OFrame.from_vecs(vecs + [y], names + [spec.y])
+        mt = str(p.get("metalearner_transform") or "NONE").lower()
+        if mt not in ("none", "logit"):
+            raise ValueError(f"metalearner_transform must be NONE or Logit, got {mt}")
+        fcol = p.get("metalearner_fold_column")
+        nf = int(p.get("metalearner_nfolds") or 0)
+        if fcol and nf:
+            raise ValueError("Cannot specify fold_column and nfolds at the same time.")
+        extra_v, extra_n = [], []
+        if fcol:
+            if fcol not in frame.names:
+                raise ValueError(f"metalearner_fold_column '{fcol}' is not in the training frame")
+            extra_v, extra_n = [frame.vec(fcol)], [fcol]
+        lvl1 = H2OFrame.from_vecs(vecs + extra_v + [y], names + extra_n + [spec.y])
         self._names = names
         algo = (p.get("metalearner_algorithm") or "auto").lower()
         mp = dict(p.get("metalearner_params") or {})
-        nf = int(p.get("metalearner_nfolds") or 0)
-        if nf:
+        # Metalearner.setCrossValidationParams
+        if fcol:
+            mp.setdefault("fold_column", fcol)
+        elif nf:
             mp.setdefault("nfolds", nf)
+            if nf > 1 and p.get("metalearner_fold_assignment"):
+                mp.setdefault("fold_assignment", p["metalearner_fold_assignment"])
         if p.get("seed", -1) not in (None, -1):
             mp.setdefault("seed", p["seed"])
         if algo in ("auto", "glm"):

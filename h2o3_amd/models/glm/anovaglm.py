@@ -87,7 +87,18 @@ class H2OANOVAGLMEstimator(H2OEstimator):
         p = self._parms
         self._x, self._y, self._w = list(spec.x), spec.y, spec.weights_column
         self._doms = {c: list(spec.frame.vec(c).domain) for c in self._x if spec.frame.vec(c).type == T_ENUM}
+        # ANOVAGLM.java:105-121 init checks
+        if len(self._x) < 2:
+            raise ValueError("ERRR on field: predictors: there must be at least two predictors.")
         h = int(p.get("highest_interaction_term", 2))
+        if h == 0:
+            h = len(self._x)
+        if h < 1 or h > len(self._x):
+            raise ValueError("ERRR on field: highest_interaction_term: must be >= 1 or <= number of predictors.")
+        if spec.nclasses > 2:
+            raise ValueError("ERRR on field: family: multinomial and ordinal are not supported at this point.")
+        if int(p.get("type", 3)) != 3:
+            raise ValueError("type: only type III sums of squares are supported (as in the reference)")
         self._terms = [t for k in range(1, min(h, len(self._x)) + 1) for t in itertools.combinations(self._x, k)]
         tf, term_cols = self._transformed(spec.frame)
         all_cols = [c for t in term_cols.values() for c in t]

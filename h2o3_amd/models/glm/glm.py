@@ -802,8 +802,13 @@ class H2OGeneralizedLinearEstimator(H2OEstimator):
                 sm = {"lambda": lam, "alpha": alpha, "beta_std": drv.beta.copy(), "beta": beta,
                       "icpt": icpt, "deviance": dev, "explained_deviance_train": None, "iteration": drv.iter}
                 path.append(sm)
-                if max_active > 0 and int(np.sum(np.abs(drv.beta[:-1]) > 0)) > max_active:
-                    break   # GLM.java: stop the path once too many predictors are active
+                if max_active > 0 and int(np.sum(np.abs(drv.beta[:-1]) > 0)) + (1 if drv.intercept else 0) \
+                        > max_active:
+                    # GLM.java: the path stops once too many predictors are
+                    # active; the submodel returned is the last one within it
+                    if len(path) > 1:
+                        path.pop()
+                    break
                 if p.get("lambda_search"):
                     dev_te = self._dev_on(spec.valid, sm, drv) if spec.valid is not None else None
                     hist_tr[nsub % 5] = (old_tr - dev) / old_tr if old_tr else 0.0

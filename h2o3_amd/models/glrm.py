@@ -245,27 +245,42 @@ class H2OGeneralizedLowRankEstimator(H2OEstimator):
         seed = p.get("seed", -1)
         g = torch.Generator(device="cpu").manual_seed(int(seed) if seed not in (-1, None) else 12345)
         init = str(p.get("init") or "PlusPlus").lower()
-        if p.get("user_y") is not None:
-            Y = torch.as_tensor(np.asarray(p["user_y"].as_data_frame().values if hasattr(p["user_y"], "as_data_frame")
-                                           else p["user_y"], dtype=np.float32), device=A.device)
+        if init == "user" and p.get("user_y") is None and p.get("user_x") is None:
+            raise ValueError("ERRR on field: _init: init = User requires user_y and/or user_x")
+        if p.get("user_y") is not None and init == "user":
+            Y = self._user_y(p["user_y"], blocks, k).to(A.device)
+        elif init == "user":
+            Y = torch.randn((k, P), generator=g).to(A.device)
         elif init == "svd":
-            U_, S_, V_ = torch.linalg.svd(A * M, full_matrices=False)
-            Y = (S_[:k].view(-1, 1) * V_[:k]) / math.sqrt(max(n, 1))
+            Y = self._svd_init(A, M, k, spec.frame.nrows, g)
         elif init == "plusplus":
-            # k-means++ seeded archetypes from data rows
-            idx = [int(torch.randint(n, (1,), generator=g))]
-            d2 = ((A - A[idx[0]]) ** 2).sum(1)
-            for _ in range(1, k):
-                pr = (d2 / d2.sum().clamp_min(1e-30)).cpu()
-                i = int(torch.multinomial(pr, 1, generator=g)) if float(d2.sum()) > 0 else int(torch.randint(n, (1,), generator=g))
-                idx.append(i)
-                d2 = torch.minimum(d2, ((A - A[i]) ** 2).sum(1))
-            Y = A[idx].clone()
+            # k-means++ seeded archetypes from data rows (rank 0's rows,
+            # broadcast so every rank starts from the same Y)
+            nl = A.shape[0]
+            if nl:
+                idx = [int(torch.randint(nl, (1,), generator=g))]
+                d2 = ((A - A[idx[0]]) ** 2).sum(1)
+                for _ in range(1, k):
+                    pr = (d2 / d2.sum().clamp_min(1e-30)).cpu()
+                    i = int(torch.multinomial(pr, 1, generator=g)) if float(d2.sum()) > 0 \
+                        else int(torch.randint(nl, (1,), generator=g))
+                    idx.append(i)
+                    d2 = torch.minimum(d2, ((A - A[i]) ** 2).sum(1))
+                Y = A[idx].clone()
+            else:
+                Y = torch.zeros((k, P), device=A.device)
+            if cloud.is_distributed():
+                Y = coll.broadcast_(Y.contiguous(), 0)
         else:
             Y = torch.randn((k, P), generator=g).to(A.device)
         if Y.shape[0] < k:
             Y = torch.cat([Y, torch.randn((k - Y.shape[0], P), generator=g).to(A.device) * 0.01], 0)
-        X = self._init_x(A, M, Y, g)
+        if p.get("user_x") is not None and init == "user":
+            X = self._user_x(p["user_x"], spec.frame, k).to(A.device)
+        else:
+            X = None
+        if X is None:
+            X = self._init_x(A, M, Y, g)
         gx, gy = float(p.get("gamma_x", 0.0)), float(p.get("gamma_y", 0.0))
         rx, ry = p.get("regularization_x"), p.get("regularization_y")
 
@@ -320,6 +335,105 @@ class H2OGeneralizedLowRankEstimator(H2OEstimator):
             o["eigenvectors"] = V2.T.cpu().numpy()
         from ..core import dkv
         dkv.put(rep, self.representation_frame())
+
+    def _user_y(self, uy, blocks, k):
+        """GLRM.java:404 initialXY (init=User): user_y holds k rows; with
+        expand_user_y its columns are the original ones (a categorical column
+        gives the level index, expanded to its one-hot block), otherwise it
+        is already in the expanded layout."""
+        df = uy.as_data_frame() if hasattr(uy, "as_data_frame") else __import__("pandas").DataFrame(uy)
+        P = sum(w for _, _, w in blocks)
+        expand = bool(self._parms.get("expand_user_y", True))
+        ncol = len(blocks) if expand else P
+        if df.shape[1] != ncol:
+            raise ValueError(f"ERRR on field: _user_y: The user-specified Y must have the same number of columns "
+                             f"({ncol}) as the training observations")
+        if df.shape[0] != k:
+            raise ValueError(f"ERRR on field: _user_y: The user-specified Y must have k = {k} rows")
+        if df.isna().values.any():
+            raise ValueError("ERRR on field: _user_y: The user-specified Y cannot contain any missing values")
+        if not expand:
+            Y = np.asarray(df.values, dtype=np.float64)
+        else:
+            Y = np.zeros((k, P))
+            j = 0
+            for ci, (kind, c, w) in enumerate(blocks):
+                col = df.iloc[:, ci]
+                if kind == "cat":
+                    dom = self._doms[c]
+                    for r in range(k):
+                        v = col.iloc[r]
+                        lv = dom.index(v) if isinstance(v, str) and v in dom else int(float(v))
+                        if 0 <= lv < w:
+                            Y[r, j + lv] = 1.0
+                else:
+                    Y[:, j] = col.values.astype(np.float64)
+                j += w
+        if not np.any(Y):
+            raise ValueError("ERRR on field: _user_y: The user-specified Y cannot all be zero")
+        return torch.as_tensor(Y, dtype=torch.float32)
+
+    def _user_x(self, ux, frame, k):
+        """user_x: the initial representation X (one row per training row,
+        k columns), taken shard by shard like the training frame."""
+        if ux.nrows != frame.nrows:
+            raise ValueError("ERRR on field: _user_x: The user-specified X must have the same number of rows "
+                             f"({frame.nrows}) as the training observations")
+        if ux.ncols != k:
+            raise ValueError(f"ERRR on field: _user_x: The user-specified X must have k = {k} columns")
+        X = torch.stack([ux.vec(c).as_float(torch.float32) for c in ux.names], 1)
+        if bool(torch.isnan(X).any()):
+            raise ValueError("ERRR on field: _user_x: The user-specified X cannot contain any missing values")
+        if coll.allreduce_scalar(float(X.abs().sum())) == 0:
+            raise ValueError("ERRR on field: _user_x: The user-specified X cannot all be zero")
+        return X
+
+    def _svd_init(self, A, M, k, n, g):
+        """init = SVD (GLRM.java:458): the top-k right singular vectors of
+        the training matrix from its all-reduced Gram (identical on every
+        rank), by the svd_method of hex/svd/SVD.java: GramSVD = exact
+        eigendecomposition, Power = power iterations with deflation,
+        Randomized = k subspace iterations from a seeded Gaussian start."""
+        Am = (A * M).double()
+        G = Am.T @ Am
+        coll.allreduce_(G)
+        P = G.shape[0]
+        method = str(self._parms.get("svd_method") or "Randomized").lower()
+        if method == "gramsvd":
+            lam, V = torch.linalg.eigh(G)
+            order = torch.argsort(lam, descending=True)[:k]
+            lam, V = lam[order], V[:, order]
+        elif method == "power":
+            V = torch.zeros((P, k), dtype=torch.float64, device=G.device)
+            lam = torch.zeros(k, dtype=torch.float64, device=G.device)
+            R = G.clone()
+            iters = max(1, min(int(self._parms.get("max_iterations", 1000)), 1000))
+            for j in range(k):
+                v = torch.randn(P, generator=g, dtype=torch.float64).to(G.device)
+                v = v / v.norm().clamp_min(1e-300)
+                for _ in range(iters):
+                    w = R @ v
+                    nw = w.norm()
+                    if float(nw) == 0:
+                        break
+                    w = w / nw
+                    if float((w - v).abs().max()) < 1e-10:
+                        v = w
+                        break
+                    v = w
+                lam[j] = v @ (R @ v)
+                V[:, j] = v
+                R = R - lam[j] * torch.outer(v, v)
+        else:   # randomized subspace iteration, k passes (GLRM.java:468)
+            Q = torch.randn((P, k), generator=g, dtype=torch.float64).to(G.device)
+            for _ in range(max(1, k)):
+                Q, _ = torch.linalg.qr(G @ Q)
+            B = Q.T @ G @ Q
+            lb, W = torch.linalg.eigh(B)
+            order = torch.argsort(lb, descending=True)
+            lam, V = lb[order], Q @ W[:, order]
+        Y = (torch.sqrt(lam.clamp_min(0)).view(-1, 1) * V.T) / math.sqrt(max(n, 1))
+        return Y.to(torch.float32)
 
     def _init_x(self, A, M, Y, g):
         # least squares start: X = A Y^T (Y Y^T)^-1 (quadratic-loss optimum for fixed Y)

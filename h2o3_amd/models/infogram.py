@@ -99,6 +99,20 @@ class H2OInfogram(H2OEstimator):
 
     def _fit(self, spec):
         p = self._parms
+        frac = float(p.get("data_fraction", 1.0))
+        if not 0 < frac <= 1:
+            raise ValueError("ERRR on field: data_fraction: must be in (0, 1].")
+        if frac < 1:
+            # data_fraction (Infogram.java): the infogram's models see a seeded
+            # row sample of the training frame (each rank samples its shard)
+            import copy
+            from ..parallel import cloud
+            seed = p.get("seed", -1)
+            g = torch.Generator(device=cloud.device())
+            g.manual_seed(((int(seed) if seed not in (None, -1) else 1234) * 1000003 + cloud.rank()) & 0x7FFFFFFF)
+            keep = torch.rand(spec.frame.nlocal, generator=g, device=cloud.device()) < frac
+            spec = copy.copy(spec)
+            spec.frame = spec.frame[keep]
         prot = list(p.get("protected_columns") or [])
         xs = [c for c in spec.x if c not in prot]
         fair = bool(prot)

@@ -114,7 +114,21 @@ class H2OSupportVectorMachineEstimator(H2OEstimator):
     def _wants_categorical_response(self):
         return True
 
+    def _score_all(self, spec):
+        # PSVM.java:200: training metrics only with disable_training_metrics=False
+        # (the default skips the O(n * #SV) scoring pass); validation always
+        if not self._parms.get("disable_training_metrics", True):
+            self._training_metrics = self._metrics_from_raw(spec, spec.frame, self._predict_raw(spec.frame))
+        else:
+            self._training_metrics = None
+        if spec.valid is not None:
+            self._validation_metrics = self._metrics_from_raw(spec, spec.valid, self._predict_raw(spec.valid))
+
     def _fit(self, spec):
+        kt = str(self._parms.get("kernel_type") or "gaussian").lower()
+        if kt != "gaussian":
+            # PSVMModel.KernelType has the gaussian kernel only
+            raise ValueError(f"kernel_type: unsupported kernel '{kt}' (only 'gaussian')")
         p = self._parms
         if spec.nclasses != 2:
             raise ValueError("PSVM supports binary classification only")

@@ -172,6 +172,13 @@ class H2ORuleFitEstimator(H2OEstimator):
             glm_kw["family"] = "multinomial"
         elif dist not in ("auto", "gaussian"):
             glm_kw["family"] = dist
+        mnr = int(p.get("max_num_rules", -1) or -1)
+        if mnr > 0:
+            # RuleFit.java:228: the Lasso path stops once more than
+            # max_num_rules + 1 predictors are active
+            glm_kw["max_active_predictors"] = mnr + 1
+            glm_kw["lambda_search"] = True
+            glm_kw.pop("lambda_", None)
         self._glm = H2OGeneralizedLinearEstimator(**glm_kw)
         xs = [c for c in fr.names if c != spec.y]
         self._glm.train(x=xs, y=spec.y, training_frame=fr)

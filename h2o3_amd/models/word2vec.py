@@ -29,6 +29,8 @@ from ..core.vec import T_REAL, T_STR, Vec, make_enum_from_strings
 from ..parallel import cloud
 from .base import H2OEstimator
 
+_MAX_EXP = 6.0      # WordVectorTrainer.MAX_EXP
+
 W2V_DEFAULTS = dict(vec_size=100, window_size=5, sent_sample_rate=1e-3, norm_model="HSM", epochs=5,
                     min_word_freq=5, init_learning_rate=0.025, word_model="SkipGram", pre_trained=None, seed=-1)
 
@@ -136,6 +138,12 @@ class H2OWord2vecEstimator(H2OEstimator):
         win = int(p.get("window_size", 5))
         processed = 0
         B = int(min(16384, max(256, 32 * V)))
+        wm = str(p.get("word_model") or "SkipGram").lower().replace("_", "")
+        if wm not in ("skipgram", "cbow"):
+            raise ValueError(f"word_model must be SkipGram or CBOW, got {p.get('word_model')}")
+        if str(p.get("norm_model") or "HSM").lower() != "hsm":
+            raise ValueError("norm_model: only HSM (hierarchical softmax) is available (Word2Vec.NormModel)")
+        cbow = wm == "cbow"
         for ep in range(epochs):
             # frequent-word sub-sampling (word2vec formula)
             if ss > 0:
@@ -148,6 +156,40 @@ class H2OWord2vecEstimator(H2OEstimator):
             n = t_e.numel()
             # dynamic window: reduced window b ~ U[0, win)
             red = torch.randint(0, win, (n,), generator=g).to(dev)
+            if cbow:
+                # CBOW (WordVectorTrainer.CBOW): the mean of the window's input
+                # vectors predicts the centre word through the Huffman tree, the
+                # hidden error goes back to every window word
+                offs = torch.tensor([o for o in range(-win, win + 1) if o != 0], device=dev)
+                J = torch.arange(n, device=dev).view(-1, 1) + offs.view(1, -1)
+                okm = (J >= 0) & (J < n)
+                Jc = J.clamp(0, n - 1)
+                okm = okm & (s_e[Jc] == s_e.view(-1, 1)) & (offs.abs().view(1, -1) <= (win - red).view(-1, 1))
+                order = torch.randperm(n, generator=g).to(dev)
+                for s in range(0, n, B):
+                    prog = (processed + s) / max(epochs * total_words, 1)
+                    lr = max(lr0 * (1 - prog), lr0 * 1e-4)
+                    idx = order[s:s + B]
+                    m = okm[idx]
+                    bag = m.sum(1)
+                    ctxw = t_e[Jc[idx]]                                  # [b, 2w]
+                    h = (syn0[ctxw] * m.unsqueeze(2)).sum(1) / bag.clamp_min(1).unsqueeze(1)
+                    c = t_e[idx]
+                    pts, cds = pt_t[c], code_t[c]
+                    S1 = syn1[pts]
+                    dot = (S1 * h.unsqueeze(1)).sum(2)
+                    valid = (cds >= 0) & (bag > 0).view(-1, 1) & (dot.abs() < _MAX_EXP)
+                    gsc = ((1 - cds) - torch.sigmoid(dot)) * lr * valid
+                    neu1e = (gsc.unsqueeze(2) * S1).sum(1)
+                    pv = pts[valid]
+                    c1 = (torch.bincount(pv, minlength=syn1.shape[0]).to(h.dtype) / 8).clamp_min(1)
+                    syn1.index_add_(0, pv, (gsc.unsqueeze(2) * h.unsqueeze(1))[valid] / c1[pv].unsqueeze(1))
+                    wi = ctxw[m]
+                    upd = neu1e.unsqueeze(1).expand(-1, m.shape[1], -1)[m]
+                    c0 = (torch.bincount(wi, minlength=syn0.shape[0]).to(h.dtype) / 8).clamp_min(1)
+                    syn0.index_add_(0, wi, upd / c0[wi].unsqueeze(1))
+                processed += n
+                continue
             cen, ctx = [], []
             for off in range(-win, win + 1):
                 if off == 0:
@@ -172,9 +214,11 @@ class H2OWord2vecEstimator(H2OEstimator):
                 h = syn0[w_in]             # [b, d]
                 pts = pt_t[c]              # [b, L]
                 cds = code_t[c]
-                valid = cds >= 0
                 S1 = syn1[pts]             # [b, L, d]
-                f_ = torch.sigmoid((S1 * h.unsqueeze(1)).sum(2))
+                dot = (S1 * h.unsqueeze(1)).sum(2)
+                # hierarchicalSoftmaxSG skips nodes with |f| >= MAX_EXP (6)
+                valid = (cds >= 0) & (dot.abs() < _MAX_EXP)
+                f_ = torch.sigmoid(dot)
                 gsc = ((1 - cds) - f_) * lr * valid
                 neu1e = (gsc.unsqueeze(2) * S1).sum(1)
                 # batched Hogwild: rows hit several times in one batch get the

@@ -450,6 +450,9 @@ class MojoModel:
                 else:
                     cols[names[j]] = raw[:, 0]
                     j += 1
+            if str(m.get("metalearner_transform", "NONE")).lower() == "logit" and self.nclasses >= 2:
+                cols = {k: np.log(np.clip(v, 1e-9, 1 - 1e-9) / (1 - np.clip(v, 1e-9, 1 - 1e-9)))
+                        for k, v in cols.items()}
             return self._meta_model.predict_raw(pd.DataFrame(cols))
         raise NotImplementedError(a)
 

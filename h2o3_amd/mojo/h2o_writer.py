@@ -734,6 +734,8 @@ def _deeplearning(model, z):
     and row-major float weights per layer.  Our NA handling (categorical
     mode, numeric mean) is expressed exactly: the missing bucket's weights
     are the mode level's, a missing numeric standardises to 0."""
+    if getattr(model, "_cat_slots", None) is not None:
+        raise NotImplementedError("MOJO export of a DL model with hashed categoricals (max_categorical_features)")
     if model._ae:
         raise NotImplementedError("reference-layout MOJO export of deep learning autoencoders is not implemented")
     di = model._dinfo
@@ -861,7 +863,8 @@ def _stackedensemble(model, z):
     domains = [xd.get(c) for c in x] + [list(spec.response_domain) if spec.response_domain else None]
     subs = list(model._base) + [model._meta]
     extra = {"submodel_count": len(subs), "base_models_num": len(model._base), "metalearner": model._meta.model_id,
-             "metalearner_transform": "NONE"}
+             "metalearner_transform": "Logit" if str(model._parms.get("metalearner_transform") or "NONE").lower()
+             == "logit" else "NONE"}
     for i, m in enumerate(subs):
         d = f"models/{m.algo}/{m.model_id}/"
         extra[f"submodel_key_{i}"] = m.model_id

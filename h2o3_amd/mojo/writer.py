@@ -185,6 +185,8 @@ def build_mojo(model) -> bytes:
         _dinfo_meta(w, model._dinfo)
         w.add_array("evecs", model._evecs.cpu().numpy())
         w.add_array("mean", model._mean.cpu().numpy())
+    elif algo == "deeplearning" and getattr(model, "_cat_slots", None) is not None:
+        raise NotImplementedError("MOJO export of a DL model with hashed categoricals (max_categorical_features)")
     elif algo == "deeplearning":
         _dinfo_meta(w, model._dinfo)
         layers = []
@@ -274,6 +276,7 @@ def build_mojo(model) -> bytes:
         w.files["models/meta.zip"] = build_mojo(model._meta)
         w.meta["base"] = subs
         w.meta["level1_names"] = model._names
+        w.meta["metalearner_transform"] = str(model._parms.get("metalearner_transform") or "NONE")
     else:
         raise NotImplementedError(f"MOJO export not supported for {algo}")
     cols = (list(spec.x) + ([spec.y] if spec is not None and spec.y else [])) if spec is not None else []

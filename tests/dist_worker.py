@@ -60,6 +60,21 @@ def run(out_path):
     res["multi"] = {"logloss": m3.logloss(), "auc": m3.auc(), "aucpr": m3.aucpr(),
                     "cm": m3["cm"]["matrix"], "hr": [r["hit_ratio"] for r in m3["hit_ratio_table"]],
                     "wovr": g3.model_performance(fr3, auc_type="WEIGHTED_OVR").auc()}
+    # Deep Learning: model averaging per iteration (default), elastic averaging,
+    # sharded data (no replication) and single-node mode -- every rank must end
+    # with the same model
+    from h2o3_amd.estimators import H2ODeepLearningEstimator
+    from h2o3_amd.parallel import collectives as coll
+    dl_res = {}
+    for tag, kw in (("avg", {}), ("elastic", dict(elastic_averaging=True)),
+                    ("shard", dict(replicate_training_data=False, train_samples_per_iteration=1000)),
+                    ("single", dict(single_node_mode=True))):
+        dl = H2ODeepLearningEstimator(hidden=[16], epochs=4, seed=3, **kw)
+        dl.train(x=x, y="y", training_frame=fr)
+        sig = float(sum(float(L.W.double().sum()) + float(L.b.double().sum()) for L in dl._layers))
+        sigs = coll.all_gather_object(sig)
+        dl_res[tag] = {"auc": dl.auc(), "same": max(sigs) - min(sigs) < 1e-9 * max(1.0, abs(sig))}
+    res["dl"] = dl_res
     mb = gbm.model_performance(fr)
     res["bin_tab_rows"] = len(mb["thresholds_and_metric_scores"]["threshold"])
     res["bin_prauc"] = mb.aucpr()

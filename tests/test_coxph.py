@@ -108,3 +108,47 @@ def test_segmented_sums_match_index_add():
     ref = torch.zeros(9, 3, dtype=torch.float64).index_add_(0, key, v)
     torch.testing.assert_close(_Seg(key, 9)(v), ref)
     torch.testing.assert_close(_Seg(key, 9)(v[:, 0]), ref[:, 0])
+
+
+def test_coxph_baseline_hazard_breslow():
+    """calc_cumhaz (CoxPH.java:503): Breslow baseline hazard at each distinct
+    stop time = weighted events / risk still at stake, risks exp((x - mean).b)."""
+    h2o.init()
+    df = _data(300, seed=5)
+    fr = h2o.H2OFrame(df)
+    m = H2OCoxProportionalHazardsEstimator(stop_column="stop", ties="breslow")
+    m.train(x=["x1", "x2"], y="event", training_frame=fr)
+    b = np.array([m.coef()["x1"], m.coef()["x2"]])
+    X = df[["x1", "x2"]].values
+    r = np.exp((X - X.mean(0)) @ b)
+    times = np.unique(df.stop.values)
+    want_h = np.array([df.event.values[df.stop.values == t].sum() / r[df.stop.values >= t].sum() for t in times])
+    bh = m.baseline_hazard_frame.as_data_frame()
+    bs = m.baseline_survival_frame.as_data_frame()
+    assert list(bh.columns) == ["t", "baseline hazard"]
+    np.testing.assert_allclose(bh["t"].values, times)
+    np.testing.assert_allclose(bh["baseline hazard"].values, want_h, rtol=1e-6, atol=1e-12)
+    np.testing.assert_allclose(bs["baseline survival"].values, np.exp(-np.cumsum(want_h)), rtol=1e-6)
+    ch = m._output["cumhaz_0"]
+    assert np.all(np.diff(ch) >= 0) and ch[-1] == pytest.approx(np.cumsum(want_h)[-1], rel=1e-6)
+
+
+def test_coxph_interactions_and_interactions_only():
+    h2o.init()
+    df = _data(500, seed=6)
+    df["x3"] = np.random.default_rng(6).normal(size=len(df))
+    fr = h2o.H2OFrame(df)
+    m = H2OCoxProportionalHazardsEstimator(stop_column="stop", interaction_pairs=[("x1", "x3")],
+                                           interactions_only=["x3"])
+    m.train(x=["x1", "x2", "x3"], y="event", training_frame=fr)
+    names = list(m._output["coefficients_table"]["names"])
+    assert "x3" not in names and "x1_x3" in names and "x1" in names
+    # the interaction column is the product of its parents
+    X = np.c_[df.x1, df.x2, df.x1 * df.x3]
+    ref = minimize(_negll, np.zeros(3), args=(X, np.full(len(df), -np.inf), df.stop.values, df.event.values, True),
+                   method="BFGS", options={"gtol": 1e-9})
+    c = m.coef()
+    np.testing.assert_allclose([c["x1"], c["x2"], c["x1_x3"]], ref.x, atol=1e-4)
+    with pytest.raises(ValueError, match="interactions_only"):
+        H2OCoxProportionalHazardsEstimator(stop_column="stop", interactions_only=["zz"]).train(
+            x=["x1", "x2"], y="event", training_frame=fr)

@@ -173,8 +173,9 @@ def test_regression_losses_and_distributions():
 def test_early_stopping_and_best_model():
     fr, x = _frame_cls(n=3000)
     tr, va = fr.split_frame(ratios=[0.7], seed=1)
+    # score every iteration: no minimum interval, no duty-cycle cap
     m = H2ODeepLearningEstimator(hidden=[32, 32], epochs=200, seed=3, stopping_rounds=2, stopping_tolerance=0.05,
-                                 train_samples_per_iteration=500)
+                                 train_samples_per_iteration=500, score_interval=0, score_duty_cycle=1.0)
     m.train(x=x, y="y", training_frame=tr, validation_frame=va)
     hist = m.scoring_history()
     assert len(hist) < 200 * 2100 / 500          # stopped early
@@ -303,3 +304,79 @@ def test_dl_step_graph_matches_eager():
         torch.testing.assert_close(La.b, Lb.b, rtol=1e-5, atol=1e-6)
         torch.testing.assert_close(La.state["ada"], Lb.state["ada"], rtol=1e-5, atol=1e-7)
     assert a._processed == 0.0
+
+
+def _cat_frame(n=3000, seed=4):
+    rng = np.random.RandomState(seed)
+    lv = np.array([f"L{i}" for i in range(40)])
+    c = rng.choice(lv, n)
+    eff = dict(zip(lv, rng.randn(40)))
+    x1 = rng.randn(n)
+    y = (np.array([eff[v] for v in c]) + x1 + 0.3 * rng.randn(n)) > 0
+    df = pd.DataFrame({"c": c, "x1": x1, "y": np.where(y, "a", "b")})
+    return df, h2o3_amd.H2OFrame(df)
+
+
+def test_max_categorical_features_hash_trick():
+    """max_categorical_features (Neurons.Input.setInput): 40 one-hot levels
+    hashed into 8 input slots; the input layer shrinks and scoring hashes
+    the same way."""
+    import pytest
+    df, fr = _cat_frame()
+    m = H2ODeepLearningEstimator(hidden=[16], epochs=10, seed=1, max_categorical_features=8)
+    m.train(x=["c", "x1"], y="y", training_frame=fr)
+    assert m._layers[0].fin == 8 + 1
+    full = H2ODeepLearningEstimator(hidden=[16], epochs=10, seed=1)
+    full.train(x=["c", "x1"], y="y", training_frame=fr)
+    assert full._layers[0].fin == 40 + 1
+    assert 0.6 < m.auc() < full.auc() + 0.02         # collisions cost accuracy, never help much
+    p1 = m.predict(fr).as_data_frame().iloc[:, -1].values
+    p2 = m.predict(h2o3_amd.H2OFrame(df.iloc[::-1].reset_index(drop=True))).as_data_frame().iloc[:, -1].values
+    np.testing.assert_allclose(p1[::-1], p2, atol=1e-6)
+    with pytest.raises(ValueError, match="max_categorical_features"):
+        H2ODeepLearningEstimator(max_categorical_features=0).train(x=["c", "x1"], y="y", training_frame=fr)
+
+
+def test_export_weights_shuffle_reproducible_and_checks():
+    import pytest
+    _, fr = _cat_frame(1500, seed=5)
+    m = H2ODeepLearningEstimator(hidden=[8], epochs=2, seed=2, export_weights_and_biases=True)
+    m.train(x=["c", "x1"], y="y", training_frame=fr)
+    W0 = m.weights(0).as_data_frame().values
+    np.testing.assert_allclose(W0, m._layers[0].W.cpu().numpy(), atol=1e-6)
+    assert m.biases(1).nrows == 2
+    q = H2ODeepLearningEstimator(hidden=[8], epochs=2, seed=2)
+    q.train(x=["c", "x1"], y="y", training_frame=fr)
+    with pytest.raises(ValueError, match="export_weights_and_biases"):
+        q.weights(0)
+    # iterations smaller than the data: row order is kept unless shuffle_training_data
+    kw = dict(hidden=[8], epochs=3, seed=2, train_samples_per_iteration=300)
+    a = H2ODeepLearningEstimator(shuffle_training_data=False, **kw)
+    a.train(x=["c", "x1"], y="y", training_frame=fr)
+    b = H2ODeepLearningEstimator(shuffle_training_data=True, **kw)
+    b.train(x=["c", "x1"], y="y", training_frame=fr)
+    assert not np.allclose(a._layers[0].W.cpu().numpy(), b._layers[0].W.cpu().numpy())
+    r1 = H2ODeepLearningEstimator(reproducible=True, **kw)
+    r1.train(x=["c", "x1"], y="y", training_frame=fr)
+    r2 = H2ODeepLearningEstimator(reproducible=True, **kw)
+    r2.train(x=["c", "x1"], y="y", training_frame=fr)
+    np.testing.assert_array_equal(r1._layers[0].W.cpu().numpy(), r2._layers[0].W.cpu().numpy())
+    with pytest.raises(ValueError, match="duty"):
+        H2ODeepLearningEstimator(score_duty_cycle=2).train(x=["c", "x1"], y="y", training_frame=fr)
+    with pytest.raises(ValueError, match="moving rate"):
+        H2ODeepLearningEstimator(elastic_averaging=True, elastic_averaging_moving_rate=2).train(
+            x=["c", "x1"], y="y", training_frame=fr)
+
+
+def test_score_validation_samples():
+    df, fr = _cat_frame(3000, seed=6)
+    tr, va = fr.split_frame(ratios=[0.5], seed=1)
+    m = H2ODeepLearningEstimator(hidden=[8], epochs=2, seed=2, score_validation_samples=200,
+                                 score_validation_sampling="Stratified")
+    m.train(x=["c", "x1"], y="y", training_frame=tr, validation_frame=va)
+    full = H2ODeepLearningEstimator(hidden=[8], epochs=2, seed=2)
+    full.train(x=["c", "x1"], y="y", training_frame=tr, validation_frame=va)
+    h1, h2 = m.scoring_history()[-1], full.scoring_history()[-1]
+    # same training, the history's validation numbers come from a 200-row sample
+    assert h1["training_logloss"] == h2["training_logloss"]
+    assert h1["validation_logloss"] != h2["validation_logloss"]

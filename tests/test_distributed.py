@@ -94,6 +94,15 @@ def test_drf_and_kmeans_close(results):
     assert abs(one["km_tot_withinss"] - two["km_tot_withinss"]) < 0.05 * one["km_tot_withinss"]
 
 
+def test_deeplearning_model_averaging(results):
+    """DeepLearningTask model averaging at W=2: one all-reduce per iteration,
+    identical models on every rank, and a useful model for every mode."""
+    for res in results:
+        for tag, d in res["dl"].items():
+            assert d["same"], tag
+            assert d["auc"] > 0.8, (tag, d["auc"])
+
+
 def test_failed_rank_exits_fast():
     """A rank that dies on an exception exits without an exit-time barrier,
     and its peer's pending collective fails on the broken connection instead

@@ -38,3 +38,28 @@ def test_word2vec_synonyms_and_transform():
     assert t.nrow == 2 and t.ncol == 16
     wf = m.to_frame()
     assert wf.nrow == 12 and wf.ncol == 17
+
+
+def test_word2vec_cbow_and_model_checks():
+    """word_model=CBOW (WordVectorTrainer.CBOW): window mean -> centre word."""
+    import pytest
+    h2o.init()
+    rng = np.random.default_rng(1)
+    groups = [["cat", "dog", "mouse", "horse"], ["red", "green", "blue", "yellow"], ["one", "two", "three", "four"]]
+    toks = []
+    for _ in range(1500):
+        g = groups[rng.integers(3)]
+        toks += list(rng.choice(g, 5)) + [None]
+    fr = h2o.H2OFrame(pd.DataFrame({"w": toks}), column_types=["string"])
+    kw = dict(vec_size=16, window_size=3, epochs=10, min_word_freq=5, seed=1, sent_sample_rate=0.0,
+              init_learning_rate=0.05)
+    cb = H2OWord2vecEstimator(word_model="CBOW", **kw)
+    cb.train(training_frame=fr)
+    assert set(cb.find_synonyms("cat", 3)) <= {"dog", "mouse", "horse"}
+    sg = H2OWord2vecEstimator(**kw)
+    sg.train(training_frame=fr)
+    a = cb.to_frame().as_data_frame().iloc[:, 1:].values
+    b = sg.to_frame().as_data_frame().iloc[:, 1:].values
+    assert not np.allclose(a, b)
+    with pytest.raises(ValueError, match="word_model"):
+        H2OWord2vecEstimator(word_model="glove", **kw).train(training_frame=fr)
