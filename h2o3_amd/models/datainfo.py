@@ -46,7 +46,13 @@ class DataInfo:
             off += len(lv)
         self.n_cat_expanded = off
         self.means, self.sigmas = [], []
-        plug = plug_values or {}
+        plug = plug_values if plug_values is not None else {}
+        if hasattr(plug, "as_data_frame"):
+            # the reference takes plug values as a one-row frame (GLM.java:970)
+            pdf = plug.as_data_frame()
+            if len(pdf) != 1:
+                raise ValueError("ERRR on field: _plug_values: Plug values frame needs to have exactly 1 row.")
+            plug = {c: float(pdf[c].iloc[0]) for c in pdf.columns if pdf[c].dtype.kind in "fiub"}
         for c in self.num_cols:
             v = frame.vec(c)
             r = v.rollups()

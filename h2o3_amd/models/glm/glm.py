@@ -433,8 +433,12 @@ class GLMDriver:
                 elif n in pos:
                     b[pos[n]] = float(v)
         else:
-            sv = list(sv)
-            b[: len(sv)] = sv
+            sv = [float(v) for v in sv]
+            if len(sv) != len(b):
+                raise ValueError(f"Initial coefficient length ({len(sv)}) does not equal to actual GLM coefficient "
+                                 f"length({len(b)}).  The order of coefficients should be the following:\n"
+                                 + "\n".join(self.dinfo.coef_names) + "\n Intercept.")
+            b[:] = sv
         if self.dinfo.standardize:
             base = self.dinfo.n_cat_expanded
             for j in range(len(self.dinfo.num_cols)):
@@ -908,6 +912,9 @@ class H2OGeneralizedLinearEstimator(H2OEstimator):
             if link not in ok:
                 raise ValueError(f"ERRR on field: _family: AUTO for underlying response requires the link to be "
                                  f"family_default or {', '.join(ok)}.")
+        if fam == "binomial" and spec.nclasses > 2:
+            raise ValueError("ERRR on field: _family: Binomial requires the response to be a 2-class categorical "
+                             "or a binary column (0/1)")
         if fam in ("poisson", "negativebinomial", "gamma"):
             y = spec.y_tensor().to(torch.float64)
             ymin = coll.allreduce_scalar(float(torch.nan_to_num(y, nan=float("inf")).min()) if y.numel()

@@ -49,7 +49,7 @@ _GLM_PASS = ("score_iteration_interval", "tweedie_variance_power", "tweedie_link
              "lambda_search", "early_stopping", "nlambdas", "missing_values_handling", "plug_values",
              "remove_collinear_columns", "non_negative", "objective_epsilon", "beta_epsilon", "gradient_epsilon",
              "prior", "cold_start", "lambda_min_ratio", "beta_constraints", "max_active_predictors", "obj_reg",
-             "balance_classes", "class_sampling_factors", "max_after_balance_size", "seed")
+             "balance_classes", "class_sampling_factors", "max_after_balance_size", "seed", "startval")
 
 
 class H2OModelSelectionEstimator(H2OEstimator):
@@ -121,6 +121,42 @@ class H2OModelSelectionEstimator(H2OEstimator):
             best[k] = list(cur)
         return best
 
+    def _check_init(self, spec, mode, preds):
+        """ModelSelection.java initModelSelectionParameters."""
+        p = self._parms
+        fam = str(p.get("family") or "AUTO").lower()
+        if mode not in ("maxr", "allsubsets", "maxrsweep", "backward"):
+            raise ValueError(f"mode must be one of allsubsets, maxr, maxrsweep, backward; got {mode}")
+        if mode != "backward":
+            if spec.nclasses > 1:
+                raise ValueError("ERRR on field: response: 'allsubsets' and 'maxr' only works with regression.")
+            if fam not in ("auto", "gaussian"):
+                raise ValueError("ERRR on field: _family: ModelSelection only supports Gaussian family for "
+                                 "'allsubset' and 'maxr' mode.")
+            k = int(p.get("max_predictor_number", 1))
+            if k < 1 or k > len(preds):
+                raise ValueError("ERRR on field: max_predictor_number: max_predictor_number must exceed 0 and be no "
+                                 "greater than the number of predictors of the training frame.")
+        else:
+            if spec.valid is not None:
+                raise ValueError("ERRR on field: validation_frame: is not supported for ModelSelection "
+                                 "mode='backward'")
+            if p.get("lambda_search"):
+                raise ValueError("ERRR on field: lambda_search: backward selection does not support lambda_search.")
+            lam = p.get("lambda_")
+            if lam not in (None, 0, 0.0) and not (isinstance(lam, (list, tuple)) and list(lam) == [0]):
+                raise ValueError("ERRR on field: lambda: must be set to 0 for backward selection")
+            if fam in ("multinomial", "ordinal"):
+                raise ValueError("ERRR on field: family: backward selection does not support multinomial or ordinal")
+            mn = int(p.get("min_predictor_number", 1))
+            if mn <= 0:
+                raise ValueError("ERRR on field: min_predictor_number: must be >= 1.")
+            if mn > len(preds):
+                raise ValueError("ERRR on field: min_predictor_number: cannot exceed the total number of predictors "
+                                 f"({len(preds)})in the dataset.")
+        if int(p.get("nparallelism", 0) or 0) < 0:
+            raise ValueError("ERRR on field: nparallelism: must be >= 0.")
+
     def _glm(self, spec, preds):
         p = self._parms
         fw = {k: p[k] for k in _GLM_PASS if k in p}
@@ -129,7 +165,8 @@ class H2OModelSelectionEstimator(H2OEstimator):
         m = H2OGeneralizedLinearEstimator(family=p.get("family") or "AUTO", link=p.get("link"),
                                           lambda_=p.get("lambda_", 0.0), alpha=p.get("alpha", 0.0),
                                           standardize=p.get("standardize", True), intercept=p.get("intercept", True),
-                                          compute_p_values=True, **fw)
+                                          compute_p_values=bool(p.get("compute_p_values", True)) or
+                                          str(p.get("mode") or "maxr").lower() == "backward", **fw)
         m.train(x=list(preds), y=spec.y, training_frame=spec.frame, weights_column=spec.weights_column)
         return m
 
@@ -137,6 +174,7 @@ class H2OModelSelectionEstimator(H2OEstimator):
         p = self._parms
         mode = str(p.get("mode") or "maxr").lower()
         preds = list(spec.x)
+        self._check_init(spec, mode, preds)
         kmax = min(int(p.get("max_predictor_number", 1)), len(preds))
         rows = []
         self._models = {}

@@ -62,6 +62,8 @@ class H2OInfogram(H2OEstimator):
                 continue
             if p.get(k) is not None:
                 kw.setdefault(k, p[k])
+        if algo == "glm" and kw.get("plug_values") is not None:
+            kw.setdefault("missing_values_handling", "PlugValues")    # plug values imply PlugValues imputation
         cls = {"auto": H2OGradientBoostingEstimator, "gbm": H2OGradientBoostingEstimator,
                "drf": H2ORandomForestEstimator, "glm": H2OGeneralizedLinearEstimator,
                "deeplearning": H2ODeepLearningEstimator}[algo]

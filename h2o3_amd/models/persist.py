@@ -2,9 +2,11 @@
 
 Reference: hex/Model.exportBinaryModel / importBinaryModel (Java
 serialization of the whole model).  Here a saved model is a directory-free
-zip: the MOJO (all scoring state) + params.json + metrics.json — no pickle,
-so loading never executes code from the file.  A loaded model scores
-through the MOJO scorer and keeps its training / validation / CV metrics.
+zip: the full estimator state (models/state_io.py: plain containers +
+tensors, read back with torch.load(weights_only=True)), the MOJO when the
+algorithm has one, params.json and metrics.json -- no pickle, so loading
+never executes code from the file.  A loaded model is the same estimator:
+it scores, keeps its outputs and metrics, and can be a checkpoint.
 """
 from __future__ import annotations
 
@@ -55,9 +57,17 @@ def save_model(model, path="", force=False, filename=None):
     if cloud.rank() != 0:
         cloud.barrier()
         return fn
-    params = {k: v for k, v in model._parms.items() if isinstance(v, (int, float, str, bool, list, type(None)))}
+    params = {k: _jsonable(v) for k, v in model._parms.items()
+              if isinstance(v, (int, float, str, bool, list, type(None)))}
+    from .state_io import dumps
+    try:
+        mojo = build_mojo(model)
+    except NotImplementedError:
+        mojo = None          # no MOJO for this algorithm: the state archive carries it
     with zipfile.ZipFile(fn, "w", zipfile.ZIP_DEFLATED) as z:
-        z.writestr("mojo.zip", build_mojo(model))
+        z.writestr("state.pt", dumps(model))
+        if mojo is not None:
+            z.writestr("mojo.zip", mojo)
         z.writestr("params.json", json.dumps({"algo": model.algo, "model_id": model.model_id, "params": params}))
         z.writestr("metrics.json", json.dumps({"training": _metrics_dict(model._training_metrics),
                                                "validation": _metrics_dict(model._validation_metrics),
@@ -69,6 +79,14 @@ def save_model(model, path="", force=False, filename=None):
     return fn
 
 
+def _jsonable(v):
+    if isinstance(v, list):
+        return [_jsonable(x) for x in v]
+    if isinstance(v, (int, float, str, bool, type(None))):
+        return v
+    return getattr(v, "model_id", None) or getattr(v, "frame_id", None) or type(v).__name__
+
+
 def load_model(path):
     from ..core.persist import is_remote, resolve
     if is_remote(path):
@@ -78,6 +96,12 @@ def load_model(path):
     from .generic import H2OGenericEstimator
     from ..core import dkv
     with zipfile.ZipFile(path) as z:
+        names = set(z.namelist())
+        if "state.pt" in names:
+            from .state_io import loads
+            est = loads(z.read("state.pt"))
+            dkv.put(est.model_id, est)
+            return est
         mojo = z.read("mojo.zip")
         meta = json.loads(z.read("params.json"))
         mets = json.loads(z.read("metrics.json"))

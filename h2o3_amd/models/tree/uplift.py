@@ -134,6 +134,10 @@ class H2OUpliftRandomForestEstimator(SharedTreeEstimator):
         return (v.as_float(torch.float32) > 0).to(torch.float32)
 
     def _fit(self, spec):
+        dist = str(self._parms.get("distribution") or "bernoulli").lower()
+        if dist not in ("auto", "bernoulli"):
+            raise ValueError(f"ERRR on field: _distribution: Distribution {dist} is not supported for Uplift DRF; "
+                             "only bernoulli (binomial response) is.")
         p = self._parms
         if spec.nclasses != 2:
             raise ValueError("UpliftDRF supports binomial responses only")
