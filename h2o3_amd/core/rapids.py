@@ -336,7 +336,8 @@ def _reduce(name, na_rm_default=False):
             t = v.as_float(torch.float64)
             ok = ~torch.isnan(t)
             na_rm = na_rm_default or (rest and bool(rest[0]))
-            if not na_rm and not bool(ok.all()):
+            from ..parallel import collectives as _c
+            if not na_rm and _c.allreduce_scalar(float((~ok).sum())) > 0:     # an NA on any rank
                 vals.append(math.nan)
                 continue
             t = t[ok]
@@ -344,7 +345,8 @@ def _reduce(name, na_rm_default=False):
             if name == "sum":
                 vals.append(coll.allreduce_scalar(float(t.sum())))
             elif name == "prod":
-                vals.append(float(torch.prod(t)))
+                # exact product over every rank's shard (no log-sum rounding)
+                vals.append(float(np.prod(coll.all_gather_object(float(torch.prod(t))))))
             elif name == "min":
                 vals.append(coll.allreduce_scalar(float(t.min()) if t.numel() else math.inf, "min"))
             elif name == "max":
@@ -386,12 +388,11 @@ def _assign_cols(dst, src, cols, rows):
         val = src[:, j] if _is_frame(src) and src.ncols > 1 else src
         name = fr.names[c] if c < fr.ncols else f"C{c + 1}"
         if isinstance(rows, list) and rows:
-            mask = torch.zeros(fr.nlocal, dtype=torch.bool, device=fr.vec(0).data.device)
-            off = fr.row_offset()
-            for r in rows:
-                r = int(r) - off
-                if 0 <= r < fr.nlocal:
-                    mask[r] = True
+            dev = fr.vec(0).data.device
+            mask = torch.zeros(fr.nlocal, dtype=torch.bool, device=dev)
+            r = torch.as_tensor([int(v) for v in rows], dtype=torch.int64, device=dev) - fr.row_offset()
+            r = r[(r >= 0) & (r < fr.nlocal)]
+            mask[r] = True                 # one scatter for the whole row list
             base = fr[name]
             from .ops_elem import ifelse
             mf = _F().from_vecs([type(fr.vec(0))(mask.to(torch.float32), "int")], ["m"])
@@ -401,6 +402,54 @@ def _assign_cols(dst, src, cols, rows):
             val = ifelse(rows, val, fr[name])
         fr[name] = val
     return fr
+
+
+_ROW_REDUCERS = {"sum", "sumNA", "mean", "min", "minNA", "max", "maxNA", "prod", "prod.na", "sd", "var"}
+
+
+def _rowwise(fr, fun):
+    """apply(fr, 1, f) for a reducer f (a primitive, or a one-argument lambda
+    whose body is a reducer of its argument with constant options): one
+    reduction along the columns of the shard's [rows, cols] matrix on the
+    device, the result sharded like fr (AstApply margin 1 without a row loop)."""
+    name, extra = None, []
+    if isinstance(fun, tuple) and fun[0] == "prim":
+        name = fun[1]
+    elif isinstance(fun, tuple) and fun[0] == "lambda":
+        f = fun[1]
+        body = f.body
+        if len(f.ids) == 1 and isinstance(body, tuple) and body[0] not in ("numlist", "strlist") and body[1]:
+            head, *args = body[1]
+            if isinstance(head, _Id) and str(head) in _ROW_REDUCERS and args and isinstance(args[0], _Id) \
+                    and args[0] == f.ids[0] and all(isinstance(a, float) for a in args[1:]):
+                name, extra = str(head), list(args[1:])
+    if name not in _ROW_REDUCERS:
+        return None
+    from .vec import T_ENUM, T_REAL, Vec
+    if any(fr.vec(j).type == T_ENUM or fr.vec(j).on_host for j in range(fr.ncols)):
+        return None
+    M = torch.stack([fr.vec(j).as_float(torch.float64) for j in range(fr.ncols)], 1)
+    na_rm = name.endswith("NA") or name == "prod.na" or (bool(extra[0]) if extra else name in ("sd", "var"))
+    base = name.replace("NA", "").replace(".na", "")
+    nan = torch.isnan(M)
+    if base == "sum":
+        out = torch.nansum(M, 1)
+    elif base == "mean":
+        out = torch.nanmean(M, 1)
+    elif base == "min":
+        out = torch.where(nan, torch.full_like(M, math.inf), M).min(1).values
+    elif base == "max":
+        out = torch.where(nan, torch.full_like(M, -math.inf), M).max(1).values
+    elif base == "prod":
+        out = torch.where(nan, torch.ones_like(M), M).prod(1)
+    else:
+        cnt = (~nan).sum(1).to(torch.float64)
+        mu = torch.nanmean(M, 1, keepdim=True)
+        var = torch.nansum((M - mu) ** 2, 1) / (cnt - 1).clamp_min(1)
+        out = torch.sqrt(var) if base == "sd" else var
+    if not na_rm:
+        out = torch.where(nan.any(1), torch.full_like(out, math.nan), out)
+    return _F().from_vecs([Vec(out.contiguous(), T_REAL)], ["C1"])
 
 
 def _apply(fr, margin, fun):
@@ -414,6 +463,9 @@ def _apply(fr, margin, fun):
             res = res.cbind(o)
         res.names = fr.names[:res.ncols]
         return res
+    fast = _rowwise(fr, fun)
+    if fast is not None:
+        return fast
     rows = []
     g = fr.gather()
     for i in range(g.nrows):

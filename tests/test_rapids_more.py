@@ -74,3 +74,33 @@ def test_isotonic_pav_and_grouped_permute():
     dkv.put("gp.hex", H2OFrame(df))
     gp = rapids("(grouped_permute gp.hex 2 [0] 1 3)").as_data_frame()
     assert len(gp) == 2 + 1 and list(gp.columns) == ["g", "In", "Out", "InAmnt", "OutAmnt"]
+
+
+def test_rowwise_apply_prod_and_row_assign():
+    """apply(margin=1) with a reducer runs as one device reduction (matches
+    the per-row loop), prod is exact, := with a row list scatters once."""
+    import numpy as np
+    import pandas as pd
+    import h2o3_amd as h2o
+    from h2o3_amd.core import dkv, rapids
+    h2o.init(device="cpu", verbose=False)
+    rng = np.random.default_rng(0)
+    df = pd.DataFrame(rng.normal(size=(50, 3)), columns=list("abc"))
+    df.loc[3, "a"] = np.nan
+    fr = h2o.H2OFrame(df)
+    fr.frame_id = "RW"
+    dkv.put("RW", fr)
+    fast = rapids.rapids("(apply RW 1 {x . (sum x)})").as_data_frame().iloc[:, 0].values
+    loop = rapids.rapids("(apply RW 1 {x . (+ (sum x) 0)})").as_data_frame().iloc[:, 0].values
+    np.testing.assert_allclose(fast, loop, equal_nan=True)
+    np.testing.assert_allclose(fast, df.sum(1, skipna=False).values, rtol=1e-5, atol=1e-6, equal_nan=True)
+    m = rapids.rapids("(apply RW 1 {x . (mean x 1)})").as_data_frame().iloc[:, 0].values
+    np.testing.assert_allclose(m, df.mean(1).values, rtol=1e-5, atol=1e-6)
+    sd = rapids.rapids("(apply RW 1 {x . (sd x 1)})").as_data_frame().iloc[:, 0].values
+    np.testing.assert_allclose(sd, df.std(1).values, rtol=1e-5, atol=1e-6)
+    small = h2o.H2OFrame(pd.DataFrame({"v": [1.5, 2.0, -3.0, 4.0]}))
+    small.frame_id = "PR"
+    dkv.put("PR", small)
+    assert rapids.rapids("(prod PR)") == -36.0
+    r = rapids.rapids("(:= RW 7 [1] [0 5 49])").as_data_frame()["b"]
+    assert r[0] == 7 and r[5] == 7 and r[49] == 7 and r[1] != 7
