@@ -336,6 +336,9 @@ def _key_tensor(v: Vec):
 
 
 def sort(fr, by, ascending=True):
+    from . import dist_munge
+    if dist_munge.eligible(fr):
+        return dist_munge.sort(fr, by, ascending)
     g = fr.gather()
     by = by if isinstance(by, (list, tuple)) else [by]
     asc = ascending if isinstance(ascending, (list, tuple)) else [ascending] * len(by)
@@ -391,7 +394,7 @@ class GroupBy:
     """reference: AstGroup (group-by with aggregates count/sum/mean/min/max/sd/var/ss/nrow/median/mode)."""
 
     def __init__(self, fr, by):
-        self.fr = fr.gather()
+        self.fr = fr
         self.by = [fr.names[b] if isinstance(b, int) else b for b in (by if isinstance(by, (list, tuple)) else [by])]
         self.aggs = []
         self._res = None
@@ -419,7 +422,13 @@ class GroupBy:
     def get_frame(self):
         if self._res is not None:
             return self._res
-        fr = self.fr
+        from . import dist_munge
+        if dist_munge.eligible(self.fr):
+            res = dist_munge.group_by(self.fr, self.by, self.aggs)
+            if res is not None:
+                self._res = _reshard(res)
+                return self._res
+        fr = self.fr.gather() if cloud.is_distributed() else self.fr
         uniq, inv = _group_ids(fr, self.by)
         G = uniq.shape[0]
         out_vecs, out_names = [], []
@@ -498,6 +507,17 @@ def merge(x, y, all_x=False, all_y=False, by_x=None, by_y=None):
     String / UUID key columns take the host (pandas) path."""
     if all_x and all_y:
         raise ValueError("all.x=TRUE and all.y=TRUE is not supported.  Choose one only.")
+    from . import dist_munge
+    if dist_munge.eligible(x, y):
+        bx = by_x if by_x is not None else [n for n in x.names if n in y.names]
+        bx = [x.names[c] if isinstance(c, int) else c for c in bx]
+        byy = by_y if by_y is not None else (by_x if by_x is not None else bx)
+        byy = [y.names[c] if isinstance(c, int) else c for c in byy]
+        if not bx:
+            raise ValueError("merge: no common columns to join on")
+        res = dist_munge.merge(x, y, all_x, all_y, bx, byy)
+        if res is not None:
+            return res
     gx, gy = x.gather(), y.gather()
     if by_x is None:
         common = [n for n in gx.names if n in gy.names]

@@ -130,6 +130,18 @@ def all_gather_var(t: torch.Tensor) -> torch.Tensor:
     return torch.cat([g[i * m: i * m + ns[i]] for i in range(w)], 0)
 
 
+def all_to_all_single_(out: torch.Tensor, inp: torch.Tensor, out_splits=None, in_splits=None) -> torch.Tensor:
+    """Personalised exchange along dim 0 (RCCL alltoall / gloo): rank r's
+    rows in_splits[d] go to rank d, `out` receives out_splits[s] rows from
+    every rank s in rank order."""
+    _trace("all_to_all_single", inp)
+    if not cloud.is_distributed():
+        out.copy_(inp)
+        return out
+    dist.all_to_all_single(out, inp, out_splits, in_splits)
+    return out
+
+
 def broadcast_(t: torch.Tensor, src: int = 0) -> torch.Tensor:
     if cloud.is_distributed():
         _trace("broadcast", t)

@@ -75,6 +75,25 @@ def run(out_path):
         sigs = coll.all_gather_object(sig)
         dl_res[tag] = {"auc": dl.auc(), "same": max(sigs) - min(sigs) < 1e-9 * max(1.0, abs(sig))}
     res["dl"] = dl_res
+    # munging without frame gathers: sort / group-by / merge equal the one-rank results
+    import pandas as pd
+    rng = np.random.default_rng(11)
+    nm = 600
+    dm = pd.DataFrame({"k1": rng.integers(0, 7, nm).astype(float), "k2": rng.choice(["u", "v", "w"], nm),
+                       "v": rng.normal(size=nm), "t": rng.integers(0, 1000, nm).astype(float)})
+    dm.loc[::37, "v"] = np.nan
+    dm.loc[::53, "k1"] = np.nan
+    fm = h2o.H2OFrame(dm)
+    srt = fm.sort(["k2", "k1", "t"], ascending=[True, False, True]).as_data_frame()
+    res["mung_sort"] = srt.astype(str).values.tolist()
+    gb = fm.group_by(["k2", "k1"]).count().sum("v", na="rm").mean("v", na="rm").min("v").max("v").sd("v", na="rm") \
+        .median("t").get_frame().as_data_frame()
+    res["mung_gb"] = gb.round(9).astype(str).values.tolist()
+    dy = pd.DataFrame({"k1": np.arange(0, 9).astype(float), "w": np.arange(9) * 10.0})
+    fy = h2o.H2OFrame(dy)
+    for how, kw in (("inner", {}), ("left", {"all_x": True}), ("right", {"all_y": True})):
+        mg = fm[["k1", "t"]].merge(fy, **kw).as_data_frame()
+        res[f"mung_merge_{how}"] = mg.round(9).astype(str).values.tolist()
     mb = gbm.model_performance(fr)
     res["bin_tab_rows"] = len(mb["thresholds_and_metric_scores"]["threshold"])
     res["bin_prauc"] = mb.aucpr()

@@ -103,6 +103,15 @@ def test_deeplearning_model_averaging(results):
             assert d["auc"] > 0.8, (tag, d["auc"])
 
 
+def test_munging_without_gathers_matches_single_process(results):
+    """dist_munge: sort by range exchange, group-by by reduced partials,
+    merge by range-partitioned local joins -- identical rows in identical
+    order to the one-rank run."""
+    one, two = results
+    for k in ("mung_sort", "mung_gb", "mung_merge_inner", "mung_merge_left", "mung_merge_right"):
+        assert one[k] == two[k], k
+
+
 def test_failed_rank_exits_fast():
     """A rank that dies on an exception exits without an exit-time barrier,
     and its peer's pending collective fails on the broken connection instead
