@@ -43,10 +43,15 @@ def _trace(op, t=None):
 
 
 def _rccl() -> bool:
-    """True when the process group is NCCL (= RCCL over xGMI on ROCm); gloo
-    (CPU clouds, or a one-GPU multi-rank rehearsal) lacks reduce_scatter /
-    all_gather_into_tensor and takes the portable paths below."""
+    """True when the process group is NCCL (= RCCL over xGMI on ROCm)."""
     return cloud.is_gpu() and dist.get_backend() == "nccl"
+
+
+def _tensor_coll(t) -> bool:
+    """reduce_scatter_tensor / all_gather_into_tensor: RCCL, and gloo on CPU
+    tensors (so the CPU multi-rank tests run the RCCL call sequence); gloo
+    with device tensors (a one-GPU multi-rank rehearsal) lacks them."""
+    return _rccl() or t.device.type == "cpu"
 
 
 def allreduce_(t: torch.Tensor, op: str = "sum") -> torch.Tensor:
@@ -93,9 +98,9 @@ def reduce_scatter_dim0(t: torch.Tensor) -> torch.Tensor:
     assert t.shape[0] % w == 0
     out = torch.empty((t.shape[0] // w,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
     _trace("reduce_scatter", t)
-    if _rccl():
+    if _tensor_coll(t):
         dist.reduce_scatter_tensor(out, t.contiguous())
-    else:  # gloo has no reduce_scatter: all_reduce + slice
+    else:
         dist.all_reduce(t)
         out.copy_(t.view(w, -1, *t.shape[1:])[cloud.rank()])
     return out
@@ -107,7 +112,7 @@ def all_gather_dim0(t: torch.Tensor) -> torch.Tensor:
         return t
     out = torch.empty((t.shape[0] * w,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
     _trace("all_gather", t)
-    if _rccl():
+    if _tensor_coll(t):
         dist.all_gather_into_tensor(out, t.contiguous())
     else:
         parts = [torch.empty_like(t) for _ in range(w)]
@@ -138,7 +143,12 @@ def all_to_all_single_(out: torch.Tensor, inp: torch.Tensor, out_splits=None, in
     if not cloud.is_distributed():
         out.copy_(inp)
         return out
-    dist.all_to_all_single(out, inp, out_splits, in_splits)
+    if _tensor_coll(inp):
+        dist.all_to_all_single(out, inp, out_splits, in_splits)
+    else:   # gloo with device tensors: stage through host memory
+        o = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits)
+        out.copy_(o)
     return out
 
 
