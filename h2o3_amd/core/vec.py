@@ -27,21 +27,51 @@ import torch
 
 from ..parallel import cloud
 from ..parallel import collectives as coll
+from .memory import MANAGER as _MM
 
 T_REAL, T_INT, T_ENUM, T_STR, T_TIME, T_UUID, T_BAD = "real", "int", "enum", "string", "time", "uuid", "bad"
 NUMERIC_TYPES = (T_REAL, T_INT)
 
 
 class Vec:
-    __slots__ = ("data", "type", "domain", "_rollups", "_nrow_global", "replicated")
+    __slots__ = ("_d", "_sp", "_clean", "type", "domain", "_rollups", "_nrow_global", "replicated", "__weakref__")
 
     def __init__(self, data, vtype: str = T_REAL, domain=None):
-        self.data = data
+        self._sp = None
+        self._clean = None
+        self._d = data
+        if _MM.budget is not None:
+            _MM.track(self)
         self.type = vtype
         self.domain = list(domain) if domain is not None else None
         self._rollups = None
         self._nrow_global = None
         self.replicated = False  # True when every rank holds the full column
+
+    # ------------------------------------------------------------------ storage
+    @property
+    def data(self):
+        """The column tensor (reloaded from the host / disk spill tier when the
+        memory manager evicted it; core/memory.py)."""
+        if self._sp is not None:
+            return _MM.reload(self)
+        if _MM.budget is not None:
+            _MM.touch(self)
+        return self._d
+
+    @data.setter
+    def data(self, value):
+        if _MM.budget is not None:
+            _MM.untrack(self)
+        self._sp = None
+        self._clean = None
+        self._d = value
+        if _MM.budget is not None:
+            _MM.track(self)
+
+    @property
+    def spilled(self):
+        return self._sp is not None
 
     # ------------------------------------------------------------------ basics
     @property
@@ -62,14 +92,16 @@ class Vec:
 
     @property
     def on_host(self):
-        return not isinstance(self.data, torch.Tensor)
+        return self._sp is None and not isinstance(self._d, torch.Tensor)
 
     def __len__(self):
-        return len(self.data)
+        return self.nlocal
 
     @property
     def nlocal(self):
-        return len(self.data)
+        if self._sp is not None:
+            return self._sp[3]           # spilled: the row count without a reload
+        return len(self._d)
 
     def nrow(self):
         if self._nrow_global is None:

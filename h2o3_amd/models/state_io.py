@@ -68,6 +68,10 @@ class _Packer:
         if isinstance(obj, pd.Series):
             return {"__series": self.pack(obj.to_numpy(), depth + 1), "name": str(obj.name),
                     "index": self.pack(obj.index.to_numpy(), depth + 1)}
+        from ..core.vec import Vec
+        if isinstance(obj, Vec):
+            return {"__vec": {"data": self.pack(obj.data, depth + 1), "type": obj.type,
+                              "domain": self.pack(obj.domain, depth + 1), "replicated": bool(obj.replicated)}}
         cls = type(obj)
         mod = cls.__module__ or ""
         if not (mod.startswith(_PREFIX) and hasattr(obj, "__dict__")):
@@ -130,6 +134,12 @@ class _Unpacker:
         if "__series" in x:
             import pandas as pd
             return pd.Series(self.unpack(x["__series"]), name=x["name"], index=self.unpack(x["index"]))
+        if "__vec" in x:
+            from ..core.vec import Vec
+            d = x["__vec"]
+            v = Vec(self.unpack(d["data"]), d["type"], self.unpack(d["domain"]))
+            v.replicated = d["replicated"]
+            return v
         if "__skip" in x:
             return None
         if "__ref" in x:

@@ -388,6 +388,14 @@ class GBMDriver:
             self.forest.add(tree, 0)
         else:
             P = torch.softmax(self.f, 1)
+            if getattr(self, "_base_unit", None) is None:
+                bw = self.base_w
+                self._base_unit = bool(((bw == 0) | (bw == 1)).all())
+            if self.dev.type == "cuda" and self._base_unit and self.noise_bw == 0 and \
+                    self.grower.pos_payload_ok() and os.environ.get("H2O3_POS_LEAF", "1") == "1":
+                self._step_multi_dev(P, w, lr, maxabs)
+                self.iter += 1
+                return
             new = []
             for k in range(self.K):
                 z = (self.Y[:, k] - P[:, k]).contiguous()
@@ -402,6 +410,51 @@ class GBMDriver:
             for k in range(self.K):
                 self.f[:, k] += new[k]
         self.iter += 1
+
+    def _step_multi_dev(self, P, w, lr, maxabs):
+        """Multinomial iteration on the position-ordered path: each class tree
+        keeps its NaN-masked residual as the grower's payload, the gamma sums
+        ((K-1)/K * sum z / sum |z|(1-|z|)) come from contiguous reads of it,
+        the leaf values stay on the device and are scattered into a per-class
+        delta -- no per-row leaf ids, no host gamma -- and ONE host copy per
+        iteration brings every class tree's leaf values back."""
+        K = self.K
+        wc = w.contiguous()
+        deltas, vals_l, trees = [], [], []
+        for k in range(K):
+            z = (self.Y[:, k] - P[:, k]).contiguous()
+            tree, nid, leaves, tot = self.grower.grow(z, wc, 0, want_nid=False, vmax=[1.0, 1.0], unit_w=True)
+            zpos = self.grower._pos1[0] if getattr(self.grower, "_pos1", None) is not None else None
+            lids, st, ct = self.grower.last_segs
+            L = len(leaves)
+            if zpos is not None:
+                s_ = tree_ops.leaf_pos_sums(zpos, lids, st, ct, L, 1)
+            else:
+                s_ = tree_ops.seg_sum2(self.grower.ridx, wc * z, wc * z.abs() * (1 - z.abs()), lids, st, ct, L)
+            coll.allreduce_(s_)
+            den = s_[:, 1]
+            v = torch.where(den > 1e-300, s_[:, 0] / torch.where(den > 1e-300, den, torch.ones_like(den)),
+                            torch.zeros_like(den))
+            v = ((K - 1.0) / K * v).clamp(-maxabs, maxabs) * lr
+            d = torch.empty(self.f.shape[0], dtype=torch.float32, device=self.dev) if self._scatter_ok(st, ct) \
+                else torch.zeros(self.f.shape[0], dtype=torch.float32, device=self.dev)
+            vf = v.to(torch.float32)
+            if self._scatter_ok(st, ct):
+                tree_ops.leaf_scatter(self.grower.ridx, d, vf, lids, st, ct)
+            else:
+                tree_ops.leaf_update(self.grower.ridx, d, vf, lids, st, ct)
+            deltas.append(d)
+            vals_l.append(v)
+            trees.append((tree, list(leaves)))
+        for k in range(K):
+            self.f[:, k] += deltas[k]
+        host = torch.cat(vals_l).cpu().numpy()
+        o = 0
+        for k, (tree, leaves) in enumerate(trees):
+            for li, node in enumerate(leaves):
+                tree.value[node] = float(host[o + li])
+            o += len(leaves)
+            self.forest.add(tree, k)
 
     def _noise(self, k, nleaves):
         """pred_noise_bandwidth factors of this tree's leaves (1 when off)."""

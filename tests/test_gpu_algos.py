@@ -81,3 +81,24 @@ def test_native_libraries_loaded():
     names = " ".join(_native.loaded_libs())
     for lib in ("tree_hist", "tree_split", "tree_predict", "gram"):
         assert lib in names, (lib, names)
+
+
+def test_multinomial_gbm_device_path_matches_host_path(frame, monkeypatch):
+    """Multinomial GBM on the position-ordered path (device gamma, one host
+    copy per iteration) grows the same trees as the per-row leaf-id path."""
+    df = frame.as_data_frame()
+    df["y3"] = np.where(df["x0"] > 0.5, "hi", np.where(df["x0"] < -0.5, "lo", "mid"))
+    fr = h2o3_amd.H2OFrame(df)
+    x = [f"x{i}" for i in range(6)] + ["cat"]
+    out = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("H2O3_POS_LEAF", flag)
+        m = E.H2OGradientBoostingEstimator(ntrees=6, max_depth=4, seed=1)
+        m.train(x=x, y="y3", training_frame=fr)
+        out[flag] = (m, m.predict(fr).as_data_frame().iloc[:, 1:].values)
+    (a, pa), (b, pb) = out["1"], out["0"]
+    assert len(a._forest.trees) == len(b._forest.trees) == 18
+    for t1, t2 in zip(a._forest.trees, b._forest.trees):
+        assert list(np.asarray(t1.feat)) == list(np.asarray(t2.feat))
+    np.testing.assert_allclose(pa, pb, atol=2e-4)
+    assert a.logloss() < 0.3
