@@ -167,7 +167,8 @@ def fit_multinomial(est, spec, fam):
     maxit = maxit if maxit > 0 else 200
     oe = float(p.get("objective_epsilon") or -1)
     ge = float(p.get("gradient_epsilon") or -1)
-    tol = oe if oe > 0 else 1e-7
+    # GLM.java:1176: objective_epsilon defaults to 1e-4 on a lambda search
+    tol = oe if oe > 0 else (1e-4 if p.get("lambda_search") else 1e-7)
     gtol = ge if ge > 0 else 1e-8
     valid = None
     if spec.valid is not None:
@@ -391,6 +392,7 @@ def _optimize(f_g, x0, l1, n_pen, max_iter=200, tol=1e-7, gtol=1e-8):
     y = x.clone()
     t = 1.0
     f, g = f_g(y)
+    f_prev = None
     for it in range(max_iter * 5):
         while True:
             z = y - g / L
@@ -402,9 +404,10 @@ def _optimize(f_g, x0, l1, n_pen, max_iter=200, tol=1e-7, gtol=1e-8):
             L *= 2
         tn = (1 + math.sqrt(1 + 4 * t * t)) / 2
         yn = z + ((t - 1) / tn) * (z - x)
-        if float((z - x).abs().max()) < 1e-7:
+        if float((z - x).abs().max()) < 1e-7 or (f_prev is not None and abs(f_prev - fz) < tol * max(1.0, abs(fz))):
             x = z
             break
+        f_prev = fz
         x, t, y = z, tn, yn
         f, g = f_g(y)
         L = max(L * 0.9, 1e-6)

@@ -61,6 +61,35 @@ def _num_loss(name, a, u, period):
     raise ValueError(f"unknown loss {name}")
 
 
+def _num_impute(name, u):
+    """GlrmLoss.impute: the data value a numeric loss reconstructs from u."""
+    n = name.lower()
+    if n == "poisson":
+        return torch.exp(u)
+    if n in ("logistic", "hinge"):
+        return (u > 0).to(u.dtype)
+    return u
+
+
+def _cat_impute(multi_loss, U):
+    """GlrmLoss.mimpute: Categorical -> argmax; Ordinal -> the level a whose
+    ordinal loss sum_{i<a} (1 - min(1, u_i)) + (w-1-a) is smallest."""
+    if multi_loss.lower() != "ordinal":
+        return U.argmax(1)
+    w = U.shape[1]
+    if w <= 1:
+        return torch.zeros(U.shape[0], dtype=torch.long, device=U.device)
+    dec = torch.cumsum(torch.clamp(U[:, :w - 1], max=1.0), 1)            # sum_{i<a} min(1, u_i), a = 1..w-1
+    loss = torch.cat([torch.zeros_like(dec[:, :1]), -dec], 1)              # relative to the a = 0 loss
+    best = torch.zeros(U.shape[0], dtype=torch.long, device=U.device)
+    bl = loss[:, 0].clone()
+    for a in range(1, w):                                                  # strict improvement only (first minimum)
+        b = loss[:, a] < bl
+        best = torch.where(b, torch.full_like(best, a), best)
+        bl = torch.where(b, loss[:, a], bl)
+    return best
+
+
 def _reg(name, M):
     n = (name or "None").lower()
     if n == "none" or n == "nonnegative" or n in ("onesparse", "unitonesparse", "simplex"):
@@ -176,6 +205,18 @@ class H2OGeneralizedLowRankEstimator(H2OEstimator):
         M = torch.cat(masks, 1).to(torch.float32) if masks else torch.zeros_like(A)
         return A, M, blocks
 
+    def _col_loss(self, c):
+        """Loss of numeric column c (loss_by_col overrides loss)."""
+        p = self._parms
+        if p.get("loss_by_col"):
+            for name, i in zip(p["loss_by_col"], p.get("loss_by_col_idx") or []):
+                if (self._cols[i] if isinstance(i, int) else i) == c:
+                    return name
+        return p.get("loss") or "Quadratic"
+
+    def _multi_loss(self):
+        return "Ordinal" if str(self._parms.get("multi_loss") or "Categorical").lower() == "ordinal" else "Categorical"
+
     def _loss_groups(self, blocks, device):
         """Columns grouped for one vectorized loss evaluation per group:
         numeric columns by loss name, the categorical one-vs-all columns
@@ -219,10 +260,11 @@ class H2OGeneralizedLowRankEstimator(H2OEstimator):
             L = torch.where(a > 0, torch.clamp(1 - u, min=0), torch.clamp(1 + u, min=0))
             tot = tot + (L * M[:, cat]).sum(1)
         for j, w in ords:
-            a, m, u = A[:, j:j + w], M[:, j:j + w], U[:, j:j + w]
-            lvl = a.argmax(1, keepdim=True)
-            ar = torch.arange(w, device=a.device).view(1, -1)
-            L = torch.where(ar < lvl, torch.clamp(1 - u, min=0), torch.clamp(1 + u, min=0))
+            # GlrmLoss.Ordinal: sum_{i < w-1} (a > i ? max(1 - u_i, 0) : 1)
+            a, m, u = A[:, j:j + w - 1], M[:, j:j + w], U[:, j:j + w - 1]
+            lvl = A[:, j:j + w].argmax(1, keepdim=True)
+            ar = torch.arange(w - 1, device=a.device).view(1, -1)
+            L = torch.where(lvl > ar, torch.clamp(1 - u, min=0), torch.ones_like(u))
             tot = tot + L.sum(1) * m[:, 0]
         return tot if per_row else tot.sum()
 
@@ -512,7 +554,7 @@ class H2OGeneralizedLowRankEstimator(H2OEstimator):
         for kind, c, w in self._blocks:
             u = U[:, j:j + w]
             if kind == "num":
-                x = u[:, 0]
+                x = _num_impute(self._col_loss(c), u[:, 0])
                 if p.get("impute_original"):
                     mu, sd, lo, hi = self._stats[c]
                     if tr == "STANDARDIZE":
@@ -525,7 +567,7 @@ class H2OGeneralizedLowRankEstimator(H2OEstimator):
                         x = x * sd
                 vecs.append(Vec(x.contiguous().to(torch.float32), T_REAL))
             else:
-                vecs.append(Vec(u.argmax(1).to(torch.int32), T_ENUM, self._doms[c]))
+                vecs.append(Vec(_cat_impute(self._multi_loss(), u).to(torch.int32), T_ENUM, self._doms[c]))
             names.append(f"reconstr_{c}")
             j += w
         return H2OFrame.from_vecs(vecs, names)

@@ -3,15 +3,15 @@
 Reference: hex/rulefit/RuleFit.java, RuleFitModel.java, Rule.java,
 Condition.java, RuleEnsemble.java (tree ensembles of depths
 min_rule_length..max_rule_length generate candidate rules -- every
-non-root node is the conjunction of the conditions on its path -- rules
+leaf is the conjunction of the (merged) conditions on its path -- rules
 become 0/1 features, optional linear terms are added, a sparse (lasso)
 GLM selects rules; rule_importance lists coefficient, support and rule
 text; remove_duplicates drops rules with identical support patterns).
 
 MI355X design: rule features are never evaluated condition-by-condition:
-the scoring kernel gives the leaf of every row in every tree, and a node's
-rule indicator is "leaf lies in the node's subtree", i.e. one gather
-through a [n_leaves, n_nodes] ancestor table per tree.
+the scoring kernel gives the leaf of every row in every tree, and a rule
+(a leaf's path) indicator is "the row's leaf is this leaf" -- one gather
+through a per-tree identity table.
 """
 from __future__ import annotations
 
@@ -75,26 +75,63 @@ class H2ORuleFitEstimator(H2OEstimator):
         return models
 
     def _rules(self):
-        """Enumerate rules: list of (model idx, tree idx, node id, text, length)."""
+        """Rules = tree LEAVES (Rule.extractRulesFromTree): the conjunction of
+        the path's conditions with conditions on one feature and operator
+        merged (thresholds tightened, level sets intersected; NA matches only
+        if every merged condition admits it), sorted by feature name, named
+        M<model>T<tree>N<node>.  Returns (model idx, tree idx, leaf id, text,
+        #conditions, varname, [(feature, op, threshold or level codes, NA)])."""
         out = []
         for mi, m in enumerate(self._trees):
             names = list(m._spec.x)
             doms = getattr(m, "_x_domains", {})
             for ti, t in enumerate(m._forest.trees):
-                # path conditions per node
-                conds = {0: []}
-                stack = [0]
-                while stack:
-                    j = stack.pop()
-                    if t.left[j] < 0:
+                left = np.asarray(t.left)
+                right = np.asarray(t.right)
+                par = {}
+                for j in range(len(left)):
+                    if left[j] >= 0:
+                        par[int(left[j])] = (j, True)
+                        par[int(right[j])] = (j, False)
+                for leaf in range(len(left)):
+                    if left[leaf] >= 0:
                         continue
-                    for child, left in ((t.left[j], True), (t.right[j], False)):
-                        conds[child] = conds[j] + [_cond_text(t, j, left, names, doms)]
-                        stack.append(child)
-                for j, c in conds.items():
-                    if j == 0:
-                        continue
-                    out.append((mi, ti, j, " & ".join(c), len(c)))
+                    conds = {}
+                    k = leaf
+                    while k in par:
+                        j, is_left = par[k]
+                        f = names[t.feat[j]]
+                        na = bool(t.na_left[j] == is_left)
+                        if t.is_cat[j] and t.cat_left[j] is not None:
+                            mask = t.cat_left[j]
+                            dom = doms.get(f, [])
+                            lv = {i for i in range(len(dom)) if i < len(mask) and bool(mask[i]) == is_left}
+                            key = (f, "in")
+                            if key in conds:
+                                conds[key] = (conds[key][0] & lv, conds[key][1] and na)
+                            else:
+                                conds[key] = (lv, na)
+                        else:
+                            op = "<" if is_left else ">="
+                            thr = float(t.thr[j])
+                            key = (f, op)
+                            if key in conds:
+                                old = conds[key][0]
+                                thr = min(old, thr) if op == "<" else max(old, thr)
+                                conds[key] = (thr, conds[key][1] and na)
+                            else:
+                                conds[key] = (thr, na)
+                        k = j
+                    parts, struct = [], []
+                    for (f, op), (v, na) in sorted(conds.items(), key=lambda kv: kv[0]):
+                        struct.append((f, op, sorted(v) if op == "in" else v, na))
+                        if op == "in":
+                            dom = doms.get(f, [])
+                            s_ = f"({f} in {{{', '.join(str(dom[i]) for i in sorted(v))}}}"
+                        else:
+                            s_ = f"({f} {op} {v:.6g}"
+                        parts.append(s_ + (f" or {f} is NA)" if na else ")"))
+                    out.append((mi, ti, leaf, " & ".join(parts), len(parts), f"M{mi}T{ti}N{leaf}", struct))
         return out
 
     def _rule_matrix(self, frame):
@@ -119,28 +156,18 @@ class H2ORuleFitEstimator(H2OEstimator):
         for mi, m in enumerate(self._trees):
             for ti, t in enumerate(m._forest.trees):
                 nn = t.n_nodes
-                A = torch.zeros((nn, nn), dtype=torch.bool)
-                par = {}
-                for j in range(nn):
-                    if t.left[j] >= 0:
-                        par[t.left[j]] = j
-                        par[t.right[j]] = j
-                for j in range(nn):
-                    k = j
-                    while k in par:
-                        A[j, k] = True
-                        k = par[k]
-                # column 0 (root) is not a rule
-                A[:, 0] = False
+                # a row satisfies exactly one rule per tree: its leaf's
+                A = torch.eye(nn, dtype=torch.bool)
                 self._anc[(mi, ti)] = A.to(cloud.device())
                 offsets.append((mi, ti, base, nn))
                 base += nn
         rules = self._rules()
         col_of = {(mi, ti): b for mi, ti, b, _ in offsets}
-        idx = [col_of[(mi, ti)] + j for mi, ti, j, _, _ in rules]
+        idx = [col_of[(r[0], r[1])] + r[2] for r in rules]
         self._keep_cols = torch.as_tensor(idx, dtype=torch.long, device=cloud.device())
         R = self._rule_matrix(spec.frame)
         texts = [r[3] for r in rules]
+        varnames = [r[5] for r in rules]
         if p.get("remove_duplicates", True) and R.shape[1]:
             # identical support patterns (hash of the packed column) -> keep the shortest rule
             Rh = R.to(torch.float64)
@@ -157,11 +184,12 @@ class H2ORuleFitEstimator(H2OEstimator):
             keep = sorted(seen.values())
             R = R[:, keep]
             texts = [texts[i] for i in keep]
+            varnames = [varnames[i] for i in keep]
             self._keep_cols = self._keep_cols[torch.as_tensor(keep, device=self._keep_cols.device)]
         self._rule_texts = texts
         mtype = str(p.get("model_type") or "RULES_AND_LINEAR").upper()
+        self._rule_names = list(varnames)
         fr = self._design(spec.frame, R, mtype)
-        self._rule_names = [f"rule_{i}" for i in range(R.shape[1])]
         glm_kw = dict(alpha=1.0, lambda_search=p.get("lambda_") is None, seed=p.get("seed", -1))
         if p.get("lambda_") is not None:
             glm_kw["lambda_"] = p["lambda_"]
@@ -204,7 +232,7 @@ class H2ORuleFitEstimator(H2OEstimator):
         if mtype in ("RULES_AND_LINEAR", "RULES"):
             for i in range(R.shape[1]):
                 vecs.append(Vec(R[:, i].to(torch.float32).contiguous(), T_INT))
-                names.append(f"rule_{i}")
+                names.append(self._rule_names[i])
         if mtype in ("RULES_AND_LINEAR", "LINEAR"):
             for x in self._spec.x:
                 v = frame.vec(x)
@@ -220,7 +248,8 @@ class H2ORuleFitEstimator(H2OEstimator):
 
     def predict_rules(self, frame, rule_ids):
         R = self._rule_matrix(frame)
-        ids = [int(r.split("_")[1]) for r in rule_ids]
+        pos = {n: i for i, n in enumerate(self._rule_names)}
+        ids = [pos[r] for r in rule_ids]
         return H2OFrame.from_vecs([Vec(R[:, i].to(torch.float32).contiguous(), T_INT) for i in ids], list(rule_ids))
 
     def _predict_raw(self, frame):

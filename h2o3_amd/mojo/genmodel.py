@@ -37,6 +37,32 @@ def _softmax(z):
     return e / e.sum(1, keepdims=True)
 
 
+
+def _glrm_impute(name, u):
+    """GlrmLoss.impute of a numeric loss."""
+    n = name.lower()
+    if n == "poisson":
+        return np.exp(u)
+    if n in ("logistic", "hinge"):
+        return (u > 0).astype(np.float64)
+    return u
+
+
+def _glrm_mimpute(multi_loss, U):
+    """GlrmLoss.mimpute: argmax (Categorical) or the first level minimising
+    the ordinal loss (Ordinal)."""
+    if multi_loss.lower() != "ordinal" or U.shape[1] <= 1:
+        return U.argmax(1)
+    w = U.shape[1]
+    loss = np.concatenate([np.zeros((U.shape[0], 1)), -np.cumsum(np.minimum(U[:, :w - 1], 1.0), 1)], 1)
+    best = np.zeros(U.shape[0], dtype=np.int64)
+    bl = loss[:, 0].copy()
+    for a in range(1, w):
+        b = loss[:, a] < bl
+        best[b] = a
+        bl[b] = loss[b, a]
+    return best
+
 class MojoModel:
     def __init__(self, zbytes):
         self._z = zipfile.ZipFile(io.BytesIO(zbytes))
@@ -528,15 +554,19 @@ class MojoModel:
             else:
                 rowm = m[:, 0]
                 if ml == "ordinal":
+                    # GlrmLoss.Ordinal: sum_{i < w-1} (a > i ? max(1 - u_i, 0) : 1)
                     lvl = a.argmax(1).reshape(-1, 1)
-                    below = np.arange(w).reshape(1, -1) < lvl
+                    ar = np.arange(w).reshape(1, -1)
+                    below = ar < lvl
+                    L = np.where(below, np.maximum(1 - u, 0), np.where(ar < w - 1, 1.0, 0.0))
+                    dL = np.where(below & (1 - u >= 0), -1.0, 0.0)
                 else:
                     below = a > 0
-                L = np.where(below, np.maximum(1 - u, 0), np.maximum(1 + u, 0))
+                    L = np.where(below, np.maximum(1 - u, 0), np.maximum(1 + u, 0))
+                    dL = np.where(below, np.where(1 - u >= 0, -1.0, 0.0), np.where(1 + u >= 0, 1.0, 0.0))
                 tot += L.sum(1) * rowm
                 if want_grad:
-                    G[:, j:j + w] = np.where(below, np.where(1 - u >= 0, -1.0, 0.0),
-                                             np.where(1 + u >= 0, 1.0, 0.0)) * rowm.reshape(-1, 1)
+                    G[:, j:j + w] = dL * rowm.reshape(-1, 1)
             j += w
         return tot, G
 
@@ -624,7 +654,7 @@ class MojoModel:
         for kind, c, w in g["blocks"]:
             u = U[:, j:j + w]
             if kind == "num":
-                x = u[:, 0].copy()
+                x = _glrm_impute(g["loss_by_col"].get(c, g["loss"]), u[:, 0].copy())
                 if g["impute_original"]:
                     mu, sd, lo, hi = g["stats"][c]
                     tr = g["transform"]
@@ -638,7 +668,7 @@ class MojoModel:
                         x = x * sd
                 out[f"reconstr_{c}"] = x
             else:
-                out[f"reconstr_{c}"] = np.array(g["doms"][c], dtype=object)[u.argmax(1)]
+                out[f"reconstr_{c}"] = np.array(g["doms"][c], dtype=object)[_glrm_mimpute(g["multi_loss"], u)]
             j += w
         return pd.DataFrame(out)
 

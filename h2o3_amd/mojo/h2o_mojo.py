@@ -415,6 +415,178 @@ class H2OMojoModel:
         k = int(self.kv("center_num"))
         self.centers = np.asarray([self.kv(f"center_{i}") for i in range(k)], dtype=np.float64)
 
+    def _load_rulefit(self):
+        """RuleFitMojoReader: the linear model (a nested GLM MOJO), the rule
+        ensemble per (depth, tree) and the linear-name mapping."""
+        key = str(self.kv("linear_model"))
+        d = None
+        for i in range(int(self.kv("submodel_count", 0))):
+            if str(self.kv(f"submodel_key_{i}")) == key:
+                d = str(self.kv(f"submodel_dir_{i}"))
+        self.rf_linear = H2OMojoModel(None, backend=self.be.nested(d))
+        self.rf_type = int(self.kv("model_type"))
+        self.rf_depth, self.rf_ntrees = int(self.kv("depth")), int(self.kv("ntrees"))
+        self.rf_rules = {}
+        if self.rf_type != 0:
+            for i in range(self.rf_depth):
+                for j in range(self.rf_ntrees):
+                    rules = []
+                    for k in range(int(self.kv(f"num_rules_M{i}T{j}"))):
+                        rid = f"{i}_{j}_{k}"
+                        conds = []
+                        for c in range(int(self.kv(f"num_conditions_rule_id_{rid}"))):
+                            cid = f"{c}_{rid}"
+                            typ, op = int(self.kv(f"type_{cid}")), int(self.kv(f"operator_{cid}"))
+                            if typ == 0:
+                                thr = [int(self.kv(f"cat_treshold_length_{t}_{cid}"))
+                                       for t in range(int(self.kv(f"cat_treshold_length_{cid}")))]
+                            else:
+                                thr = float(self.kv(f"num_treshold{cid}"))
+                            conds.append((int(self.kv(f"feature_index_{cid}")), typ, op, thr,
+                                          bool(self.kv(f"nas_included_{cid}"))))
+                        rules.append((str(self.kv(f"var_name_rule_id_{rid}")), conds))
+                    self.rf_rules[(i, j)] = rules
+        self.rf_linear_names = [str(self.kv(f"linear_names_{i}")) for i in range(int(self.kv("linear_names_len")))]
+
+    def _load_glrm(self):
+        """GlrmMojoReader (mojo 1.10): permutation / normalisation, one
+        GlrmLoss per permuted column, archetypes [nrowY][ncolY] big-endian."""
+        self.gl_ncolA, self.gl_ncolY = int(self.kv("ncolA")), int(self.kv("ncolY"))
+        self.gl_nrowY, self.gl_ncolX = int(self.kv("nrowY")), int(self.kv("ncolX"))
+        self.gl_regx = str(self.kv("regularizationX", "None"))
+        self.gl_gammax = float(self.kv("gammaX", 0.0))
+        self.gl_ncats, self.gl_nnums = int(self.kv("num_categories")), int(self.kv("num_numeric"))
+        self.gl_sub = np.asarray(self.kv("norm_sub", []) or [], dtype=np.float64)
+        self.gl_mul = np.asarray(self.kv("norm_mul", []) or [], dtype=np.float64)
+        self.gl_perm = [int(v) for v in self.kv("cols_permutation")]
+        self.gl_losses = [ln.strip() for ln in self.be.text("losses") if ln.strip()][:self.gl_ncolA]
+        self.gl_levels = [int(v) for v in (self.kv("num_levels_per_category", []) or [])]
+        raw = self.be.read("archetypes")
+        self.gl_Y = np.frombuffer(raw, dtype=">f8", count=self.gl_nrowY * self.gl_ncolY).astype(np.float64) \
+            .reshape(self.gl_nrowY, self.gl_ncolY)
+        self.gl_seed = int(self.kv("seed", 0))
+        self.gl_reverse = bool(self.kv("reverse_transform", True))
+        self.gl_rcnt = 0                      # GlrmMojoModel._rcnt: row counter added to the seed
+
+    def _glrm_obj_grad(self, x, A, want_grad):
+        """GlrmMojoModel.objective / gradientL for every row at once."""
+        n = x.shape[0]
+        Y = self.gl_Y
+        obj = np.zeros(n)
+        grad = np.zeros_like(x) if want_grad else None
+        off = 0
+        for j in range(self.gl_ncats):
+            L = self.gl_levels[j]
+            a = A[:, j]
+            ok = ~np.isnan(a)
+            ai = np.where(ok, a, 0).astype(np.int64)
+            u = x @ Y[:, off:off + L]
+            r = np.arange(n)
+            if self.gl_losses[j] == "Ordinal":
+                ar = np.arange(L).reshape(1, -1)
+                below = (ar < ai.reshape(-1, 1)) & (ar < L - 1)
+                lo = np.where(below, np.maximum(1 - u, 0), np.where(ar < L - 1, 1.0, 0.0)).sum(1)
+                gl = np.where(below & (1 - u > 0), -1.0, 0.0)
+            else:
+                ua = u[r, ai]
+                lo = np.maximum(1 + u, 0).sum(1) + np.maximum(1 - ua, 0) - np.maximum(1 + ua, 0)
+                gl = (1 + u > 0).astype(np.float64)
+                gl[r, ai] = np.where(1 - ua > 0, -1.0, 0.0)
+            obj += np.where(ok, lo, 0.0)
+            if want_grad:
+                grad += np.where(ok[:, None], gl @ Y[:, off:off + L].T, 0.0)
+            off += L
+        for j in range(self.gl_ncats, self.gl_ncolA):
+            js = j - self.gl_ncats
+            a = (A[:, j] - self.gl_sub[js]) * self.gl_mul[js]
+            ok = ~np.isnan(a)
+            a0 = np.where(ok, a, 0.0)
+            u = x @ Y[:, off + js]
+            lo, gl = _glrm_loss(self.gl_losses[j], u, a0)
+            obj += np.where(ok, lo, 0.0)
+            if want_grad:
+                grad += np.where(ok, gl, 0.0)[:, None] * Y[:, off + js][None, :]
+        obj += self.gl_gammax * _glrm_regularize(self.gl_regx, x)
+        return obj, grad
+
+    def _score_glrm(self, X):
+        """GlrmMojoModel.score0: x from N(0, 1) draws of java.util.Random(seed
+        + row counter), projected by the X regulariser, then up to 100
+        proximal-gradient steps, each trying the 10 step sizes 0.5^i (scaled
+        by 1/obj when obj > 10) and keeping the best; a row stops once its
+        relative improvement is negative or below 1e-10."""
+        n = X.shape[0]
+        k = self.gl_ncolX
+        A = np.empty((n, self.gl_ncolA))
+        for i in range(self.gl_ncats):
+            v = X[:, self.gl_perm[i]]
+            A[:, i] = np.where(v >= self.gl_levels[i], np.nan, v)          # unseen levels -> NA
+        for i in range(self.gl_ncats, self.gl_ncolA):
+            A[:, i] = X[:, self.gl_perm[i]]
+        seeds = self.gl_seed + self.gl_rcnt + np.arange(n, dtype=np.int64)
+        self.gl_rcnt += n
+        x = _JavaRandom(seeds).gaussians(k)
+        x = _glrm_prox(self.gl_regx, x, 1.0, project=True)
+        alphas = 0.5 ** np.arange(1, 11)
+        old, _ = self._glrm_obj_grad(x, A, False)
+        live = np.ones(n, dtype=bool)
+        for _ in range(100):
+            if not live.any():
+                break
+            _, g = self._glrm_obj_grad(x, A, True)
+            scale = np.where(old > 10, 1.0 / np.where(old == 0, 1.0, old), 1.0)
+            best = np.full(n, np.finfo(np.float64).max)
+            bestx = np.zeros_like(x)
+            hit0 = np.zeros(n, dtype=bool)
+            for al in alphas:
+                a_ = (al * scale)[:, None]
+                xn = _glrm_prox(self.gl_regx, x - a_ * g, a_[:, 0] * self.gl_gammax)
+                on, _ = self._glrm_obj_grad(xn, A, False)
+                take = (best > on) & ~hit0
+                bestx[take] = xn[take]
+                best = np.where(take, on, best)
+                hit0 |= on == 0
+            zero = old == 0                                     # applyBestAlpha: already at zero loss
+            obj = np.where(zero, 0.0, best)
+            upd = live & ~zero & (best < old)
+            x[upd] = bestx[upd]
+            with np.errstate(divide="ignore", invalid="ignore"):
+                imp = 1 - obj / old
+            live &= ~((imp < 0) | (imp < 1e-10))
+            old = np.where(live | upd, obj, old)
+        self.glrm_x = x
+        return x
+
+    def glrm_impute(self, x):
+        """GlrmMojoModel.impute_data: the reconstructed row (categorical level
+        indices and numerics, back-transformed when reverse_transform)."""
+        n = x.shape[0]
+        out = np.zeros((n, self.gl_ncolA))
+        Y = self.gl_Y
+        off = 0
+        for d in range(self.gl_ncats):
+            L = self.gl_levels[d]
+            u = x @ Y[:, off:off + L]
+            if self.gl_losses[d] == "Ordinal" and L > 1:
+                loss = np.concatenate([np.zeros((n, 1)), -np.cumsum(np.minimum(u[:, :L - 1], 1.0), 1)], 1)
+                lv = np.zeros(n, dtype=np.int64)
+                bl = loss[:, 0].copy()
+                for a in range(1, L):
+                    b = loss[:, a] < bl
+                    lv[b] = a
+                    bl[b] = loss[b, a]
+            else:
+                lv = u.argmax(1)
+            out[:, self.gl_perm[d]] = lv
+            off += L
+        for d in range(self.gl_ncats, self.gl_ncolA):
+            ds = d - self.gl_ncats
+            v = _glrm_loss_impute(self.gl_losses[d], x @ Y[:, off + ds])
+            if self.gl_reverse:
+                v = v / self.gl_mul[ds] + self.gl_sub[ds]
+            out[:, self.gl_perm[d]] = v
+        return out
+
     def _load_stackedensemble(self):
         subs = {}
         for i in range(int(self.kv("submodel_count", 0))):
@@ -1083,6 +1255,41 @@ class H2OMojoModel:
             out += x[:, None] * E[base + j][None, :]
         return out
 
+    def _score_rulefit(self, X):
+        """RuleFitMojoModel.score0: per (depth, tree) the last rule whose
+        conditions all hold gives the level of categorical M<i>T<j>
+        (MojoRuleEnsemble.decode), then the rows are mapped by name onto the
+        linear model's columns (map()) and scored by it."""
+        n = X.shape[0]
+        lin = self.rf_linear
+        test = []
+        if self.rf_type != 0:
+            for i in range(self.rf_depth):
+                for j in range(self.rf_ntrees):
+                    name = f"M{i}T{j}"
+                    dom = lin.domains[lin.columns.index(name)]
+                    val = np.full(n, np.nan)
+                    for var, conds in self.rf_rules[(i, j)]:
+                        ok = np.ones(n, dtype=bool)
+                        for fi, typ, op, thr, nas in conds:
+                            col = X[:, fi]
+                            isna = np.isnan(col)
+                            if typ == 0:
+                                hit = np.isin(col, np.asarray(thr, dtype=np.float64))
+                            elif op == 0:
+                                hit = col < thr
+                            else:
+                                hit = col >= thr
+                            ok &= np.where(isna, nas, hit & ~isna)
+                        val = np.where(ok, float(dom.index(var)) if var in dom else np.nan, val)
+                    test.append(val)
+        if self.rf_type != 2:
+            test += [X[:, c] for c in range(X.shape[1]) if c < len(self.features)]
+        Xl = np.full((n, len(lin.columns)), np.nan)
+        for i, nm in enumerate(self.rf_linear_names):
+            Xl[:, lin.columns.index(nm)] = test[i]
+        return lin.score0(Xl)
+
     def _score_stackedensemble(self, X):
         n = X.shape[0]
         K = self.nclasses
@@ -1287,6 +1494,13 @@ class H2OMojoModel:
             return pd.DataFrame(preds, columns=["anomaly_score", "mean_length"])
         if self.algo == "pca":
             return pd.DataFrame(preds, columns=[f"PC{i + 1}" for i in range(preds.shape[1])])
+        if self.algo == "glrm":
+            rec = self.glrm_impute(preds)
+            out = {}
+            for j, c in enumerate(self.columns):
+                dom = self.domains[j]
+                out[f"reconstr_{c}"] = np.array(dom, dtype=object)[rec[:, j].astype(np.int64)] if dom else rec[:, j]
+            return pd.DataFrame(out)
         if self.algo == "coxph":
             return pd.DataFrame({"lp": preds[:, 0]})
         if self.algo == "targetencoder":
@@ -1309,6 +1523,149 @@ class H2OMojoModel:
 
     def predict_row(self, row: dict):
         return self.predict(row).iloc[0].to_dict()
+
+
+class _JavaRandom:
+    """java.util.Random, vectorised over one generator per row (48-bit LCG;
+    uint64 products wrap mod 2^64, so the low 48 bits stay exact)."""
+    _MUL, _ADD, _MASK = np.uint64(0x5DEECE66D), np.uint64(0xB), np.uint64((1 << 48) - 1)
+
+    def __init__(self, seeds):
+        s = np.asarray(seeds, dtype=np.int64).astype(np.uint64)
+        self.s = (s ^ self._MUL) & self._MASK
+
+    def _next(self, bits, rows):
+        with np.errstate(over="ignore"):
+            self.s[rows] = (self.s[rows] * self._MUL + self._ADD) & self._MASK
+        return (self.s[rows] >> np.uint64(48 - bits)).astype(np.int64)
+
+    def _double(self, rows):
+        return ((self._next(26, rows) << 27) + self._next(27, rows)) * (1.0 / (1 << 53))
+
+    def gaussians(self, k):
+        """k successive nextGaussian() values per generator (polar method:
+        pairs (v1 m, v2 m), the second one cached for the next call)."""
+        n = self.s.shape[0]
+        out = np.zeros((n, k))
+        for t in range(0, k, 2):
+            v1, v2, m = np.zeros(n), np.zeros(n), np.zeros(n)
+            todo = np.arange(n)
+            while todo.size:
+                a = 2 * self._double(todo) - 1
+                b = 2 * self._double(todo) - 1
+                ss = a * a + b * b
+                ok = (ss < 1) & (ss != 0)
+                r = todo[ok]
+                v1[r], v2[r] = a[ok], b[ok]
+                m[r] = np.sqrt(-2 * np.log(ss[ok]) / ss[ok])
+                todo = todo[~ok]
+            out[:, t] = v1 * m
+            if t + 1 < k:
+                out[:, t + 1] = v2 * m
+        return out
+
+
+def _glrm_loss(name, u, a):
+    """GlrmLoss loss / lgrad of a numeric column."""
+    if name == "Quadratic":
+        return (u - a) ** 2, 2 * (u - a)
+    if name == "Absolute":
+        return np.abs(u - a), np.sign(u - a)
+    if name == "Huber":
+        x = u - a
+        return (np.where(x > 1, x - 0.5, np.where(x < -1, -x - 0.5, 0.5 * x * x)),
+                np.where(x > 1, 1.0, np.where(x < -1, -1.0, x)))
+    if name == "Poisson":
+        with np.errstate(divide="ignore", invalid="ignore"):
+            extra = np.where(a == 0, 0.0, -a * u + a * np.log(np.where(a > 0, a, 1.0)) - a)
+        return np.exp(u) + extra, np.exp(u) - a
+    if name == "Logistic":
+        s = 1 - 2 * a
+        return np.log1p(np.exp(s * u)), s / (1 + np.exp(-s * u))
+    if name == "Hinge":
+        s = 1 - 2 * a
+        return np.maximum(1 + s * u, 0), np.where(1 + s * u > 0, s, 0.0)
+    if name.startswith("Periodic"):
+        f = 2 * math.pi / float(name[name.index("(") + 1:name.index(")")])
+        return 1 - np.cos((u - a) * f), f * np.sin((u - a) * f)
+    raise NotImplementedError(f"GLRM loss {name}")
+
+
+def _glrm_loss_impute(name, u):
+    if name == "Poisson":
+        return np.exp(u)
+    if name in ("Logistic", "Hinge"):
+        return (u > 0).astype(np.float64)
+    return u
+
+
+def _glrm_regularize(name, x):
+    """GlrmRegularizer.regularize per row (indicator regularisers are 0 inside
+    their set, +inf outside)."""
+    if name == "Quadratic":
+        return (x * x).sum(1)
+    if name == "L2":
+        return np.sqrt((x * x).sum(1))
+    if name == "L1":
+        return np.abs(x).sum(1)
+    if name == "NonNegative":
+        return np.where((x < 0).any(1), np.inf, 0.0)
+    if name == "OneSparse":
+        return np.where(((x < 0).any(1)) | ((x > 0).sum(1) != 1), np.inf, 0.0)
+    if name == "UnitOneSparse":
+        ok = ((x == 1).sum(1) == 1) & ((x == 0).sum(1) == x.shape[1] - 1)
+        return np.where(ok, 0.0, np.inf)
+    if name == "Simplex":
+        s = x.sum(1)
+        ok = ~(x < 0).any(1) & (np.abs(s - 1) <= 1e-10 * np.maximum(1, np.abs(x).sum(1)) * x.shape[1])
+        return np.where(ok, 0.0, np.inf)
+    return np.zeros(x.shape[0])
+
+
+def _glrm_prox(name, u, delta, project=False):
+    """GlrmRegularizer.rproxgrad(u, delta) per row (delta = 0 returns u, as
+    in the reference); project=True is GlrmRegularizer.project."""
+    delta = np.broadcast_to(np.asarray(delta, dtype=np.float64), (u.shape[0],))
+    if name in ("None",) or (project and name in ("Quadratic", "L2", "L1")):
+        return u
+    if project and name == "Simplex":
+        inside = _glrm_regularize("Simplex", u) == 0
+        out = _glrm_prox("Simplex", u, 1.0)
+        return np.where(inside[:, None], u, out)
+    keep = (delta == 0)[:, None]
+    if name == "Quadratic":
+        v = u / (1 + 2 * delta)[:, None]
+    elif name == "L2":
+        nr = np.sqrt((u * u).sum(1))
+        with np.errstate(divide="ignore", invalid="ignore"):
+            w = 1 - delta / nr
+        v = np.where((w < 0)[:, None], 0.0, w[:, None] * u)
+    elif name == "L1":
+        d = delta[:, None]
+        v = np.maximum(u - d, 0) + np.minimum(u + d, 0)
+    elif name == "NonNegative":
+        v = np.maximum(u, 0)
+    elif name in ("OneSparse", "UnitOneSparse"):
+        idx = u.argmax(1)
+        r = np.arange(u.shape[0])
+        v = np.zeros_like(u)
+        v[r, idx] = (np.where(u[r, idx] > 0, u[r, idx], 1e-6)) if name == "OneSparse" else 1.0
+    elif name == "Simplex":
+        # Chen & Ye projection onto the simplex
+        n = u.shape[1]
+        srt = np.sort(u, 1)
+        csum = np.cumsum(srt[:, ::-1], 1)[:, ::-1]            # csum[:, i] = sum_{j >= i} srt[:, j]
+        t = (csum[:, 0] - 1) / n
+        found = np.zeros(u.shape[0], dtype=bool)
+        for i in range(n - 1, 0, -1):
+            tmp = (csum[:, i] - 1) / (n - i)
+            hit = ~found & (tmp >= srt[:, i - 1])
+            t = np.where(hit, tmp, t)
+            found |= hit
+        v = np.maximum(u - t[:, None], 0)
+    else:
+        raise NotImplementedError(f"GLRM regularizer {name}")
+    return np.where(keep, u, v)
 
 
 def load(src) -> H2OMojoModel:

@@ -880,10 +880,175 @@ def _stackedensemble(model, z):
         z.write(k, v)
 
 
-_WRITERS = {"gbm": _gbm, "drf": _drf, "glm": _glm, "kmeans": _kmeans, "isolationforest": _isofor,
+# ------------------------------------------------------------------ RuleFit
+def _rulefit(model, z):
+    """RuleFitMojoModel (hex/genmodel/algos/rulefit): the rule ensemble as
+    per-(model, tree) lists of leaf rules with their conditions, and the
+    linear model as a nested GLM MOJO whose rule columns are categoricals
+    M<i>T<j> (level = the row's leaf rule, a never-matched first level keeps
+    every rule's beta explicit) next to the linear terms."""
+    spec = model._spec
+    if spec.nclasses > 2:
+        raise NotImplementedError("reference-layout MOJO export of multinomial RuleFit models")
+    x = list(spec.x)
+    xd = {}
+    for tm in model._trees:
+        xd.update(getattr(tm, "_x_domains", None) or {})
+    mt = {"LINEAR": 0, "RULES_AND_LINEAR": 1, "RULES": 2}[model._mtype]
+    rules = model._rules()
+    coef = model._glm.coef()
+    icpt = float(coef.get("Intercept", 0.0))
+    depth = len(model._trees)
+    ntrees = len(model._trees[0]._forest.trees) if model._trees else 0
+    extra = {"model_type": mt, "depth": depth, "ntrees": ntrees}
+    groups = {}
+    for r in rules:
+        groups.setdefault((r[0], r[1]), []).append(r)
+    cat_cols, cat_doms, cat_betas = [], [], []
+    for i in range(depth):
+        for j in range(ntrees):
+            rs = groups.get((i, j), [])
+            extra[f"num_rules_M{i}T{j}"] = len(rs)
+            name = f"M{i}T{j}"
+            cat_cols.append(name)
+            cat_doms.append(["__no_rule__"] + [r[5] for r in rs])
+            cat_betas.append([0.0] + [float(coef.get(r[5], 0.0)) for r in rs])
+            for k, r in enumerate(rs):
+                rid = f"{i}_{j}_{k}"
+                extra[f"num_conditions_rule_id_{rid}"] = len(r[6])
+                extra[f"prediction_value_rule_id_{rid}"] = 0.0
+                extra[f"language_rule_rule_id_{rid}"] = r[3]
+                extra[f"coefficient_rule_id_{rid}"] = float(coef.get(r[5], 0.0))
+                extra[f"var_name_rule_id_{rid}"] = r[5]
+                for c, (f, op, v, na) in enumerate(r[6]):
+                    cid = f"{c}_{rid}"
+                    extra[f"feature_index_{cid}"] = x.index(f)
+                    extra[f"feature_name_{cid}"] = f
+                    extra[f"nas_included_{cid}"] = bool(na)
+                    if op == "in":
+                        dom = xd.get(f, [])
+                        extra[f"type_{cid}"] = 0
+                        extra[f"operator_{cid}"] = 2
+                        extra[f"language_cat_treshold_length_{cid}"] = len(v)
+                        extra[f"cat_treshold_length_{cid}"] = len(v)
+                        for t, lv in enumerate(v):
+                            extra[f"language_cat_treshold_{t}_{cid}"] = str(dom[lv]) if lv < len(dom) else str(lv)
+                            extra[f"cat_treshold_length_{t}_{cid}"] = int(lv)
+                        extra[f"language_condition{cid}"] = f"({f} in {{...}})"
+                    else:
+                        extra[f"type_{cid}"] = 1
+                        extra[f"operator_{cid}"] = 0 if op == "<" else 1
+                        extra[f"num_treshold{cid}"] = float(v)
+                        extra[f"language_condition{cid}"] = f"({f} {op} {float(v):.6g})"
+    lin_cats = [c for c in x if c in xd and mt != 2]
+    lin_nums = [c for c in x if c not in xd and mt != 2]
+    gcols_cat = (cat_cols if mt != 0 else []) + [f"linear.{c}" for c in lin_cats]
+    gdoms = (cat_doms if mt != 0 else []) + [list(xd[c]) for c in lin_cats]
+    betas = list(cat_betas) if mt != 0 else []
+    for c in lin_cats:
+        betas.append([float(coef.get(f"linear.{c}.{lv}", 0.0)) for lv in xd[c]])
+    gnums = [f"linear.{c}" for c in lin_nums]
+    beta = [b for bl in betas for b in bl] + [float(coef.get(n, 0.0)) for n in gnums] + [icpt]
+    offs = [0]
+    for d in gdoms:
+        offs.append(offs[-1] + len(d))
+    key = f"{model.model_id}_linear"
+    gdi = model._glm._dinfo
+    plug = dict(zip(gdi.num_cols, gdi.plug))
+    modes = [0] * (len(cat_cols) if mt != 0 else 0) + [int(gdi.cat_modes.get(f"linear.{c}", 0)) for c in lin_cats]
+    gextra = {"use_all_factor_levels": True, "cats": len(gcols_cat), "cat_offsets": offs, "nums": len(gnums),
+              "mean_imputation": True, "num_means": [float(plug.get(n, 0.0)) for n in gnums], "cat_modes": modes,
+              "beta": beta, "family": model._glm._fam.family, "link": model._glm._fam.link}
+    cat = "Binomial" if spec.nclasses == 2 else "Regression"
+    resp_dom = [list(spec.response_domain) if spec.response_domain else None]
+    gini, gfiles = _header(model._glm, "glm", "Generalized Linear Modeling", cat, gcols_cat + gnums + [spec.y],
+                           len(gcols_cat) + len(gnums), spec.nclasses, gdoms + [None] * len(gnums) + resp_dom,
+                           GLM_MOJO_VERSION, gextra)
+    sub = z.nested(f"models/glm/{key}/")
+    sub.write("model.ini", gini)
+    for k_, v_ in gfiles.items():
+        sub.write(k_, v_)
+    linear_names = (cat_cols if mt != 0 else []) + ([f"linear.{c}" for c in x] if mt != 2 else [])
+    extra.update({"submodel_count": 1, "submodel_key_0": key, "submodel_dir_0": f"models/glm/{key}/",
+                  "linear_model": key, "data_from_rules_codes_len": len(cat_cols) if mt != 0 else 0,
+                  "weights_column": model._parms.get("weights_column") or "null",
+                  "linear_names_len": len(linear_names)})
+    for i, n in enumerate(cat_cols if mt != 0 else []):
+        extra[f"data_from_rules_codes_{i}"] = n
+    for i, n in enumerate(linear_names):
+        extra[f"linear_names_{i}"] = n
+    columns = x + [spec.y]
+    domains = [xd.get(c) for c in x] + resp_dom
+    ini, files = _header(model, "rulefit", "rulefit", cat, columns, len(x), spec.nclasses, domains, "1.00", extra)
+    z.write("model.ini", ini)
+    for k_, v_ in files.items():
+        z.write(k_, v_)
+
+
+def _glrm(model, z):
+    """GlrmMojoWriter layout (mojo 1.10): the DataInfo permutation puts the
+    categorical columns first; norm_sub / norm_mul express the numeric
+    transform; `losses` holds one GlrmLoss name per (permuted) column;
+    `archetypes` is Y [k][ncolY] in the permuted one-hot layout, as a
+    big-endian double blob (java.nio.ByteBuffer order)."""
+    p = model._parms
+    cols = list(model._cols)
+    blocks = model._blocks
+    cats = [i for i, (kind, _, _) in enumerate(blocks) if kind == "cat"]
+    nums = [i for i, (kind, _, _) in enumerate(blocks) if kind == "num"]
+    perm = cats + nums
+    starts, j = [], 0
+    for _, _, w in blocks:
+        starts.append(j)
+        j += w
+    Y = model._Y.detach().cpu().numpy().astype(np.float64)
+    order = [c for i in perm for c in range(starts[i], starts[i] + blocks[i][2])]
+    Yp = Y[:, order]
+    num_levels = [blocks[i][2] for i in cats]
+    offs = [0]
+    for L in num_levels:
+        offs.append(offs[-1] + L)
+    tr = str(p.get("transform") or "NONE").upper()
+    sub, mul = [], []
+    for i in nums:
+        mu, sd, lo, hi = model._stats[blocks[i][1]]
+        s_, m_ = {"STANDARDIZE": (mu, 1.0 / sd), "NORMALIZE": (lo, 1.0 / max(hi - lo, 1e-12)),
+                  "DEMEAN": (mu, 1.0), "DESCALE": (0.0, 1.0 / sd)}.get(tr, (0.0, 1.0))
+        sub.append(float(s_))
+        mul.append(float(m_))
+    losses = [model._multi_loss()] * len(cats)
+    for i in nums:
+        nm = model._col_loss(blocks[i][1])
+        nm = {k.lower(): k for k in ("Quadratic", "Absolute", "Huber", "Poisson", "Periodic", "Logistic",
+                                     "Hinge")}.get(str(nm).lower(), nm)
+        losses.append(f"Periodic({int(p.get('period', 1))})" if nm == "Periodic" else nm)
+    regs = {k.lower(): k for k in ("None", "Quadratic", "L2", "L1", "NonNegative", "OneSparse", "UnitOneSparse",
+                                   "Simplex")}
+    inits = {k.lower(): k for k in ("Random", "SVD", "PlusPlus", "User", "Power")}
+    seed = p.get("seed", -1)
+    extra = {"initialization": inits.get(str(p.get("init") or "PlusPlus").lower(), "PlusPlus"),
+             "regularizationX": regs.get(str(p.get("regularization_x") or "None").lower(), "None"),
+             "regularizationY": regs.get(str(p.get("regularization_y") or "None").lower(), "None"),
+             "gammaX": float(p.get("gamma_x", 0.0)), "gammaY": float(p.get("gamma_y", 0.0)),
+             "ncolX": int(Y.shape[0]), "seed": int(seed) if seed not in (None, -1) else 12345,
+             "reverse_transform": bool(p.get("impute_original")), "cols_permutation": perm,
+             "num_categories": len(cats), "num_numeric": len(nums), "norm_sub": sub, "norm_mul": mul,
+             "transposed": False, "ncolA": len(blocks), "ncolY": int(Y.shape[1]), "nrowY": int(Y.shape[0]),
+             "num_levels_per_category": num_levels, "catOffsets": offs}
+    domains = [list(model._doms[c]) if c in model._doms else None for c in cols]
+    ini, files = _header(model, "glrm", "Generalized Low Rank Modeling", "DimReduction", cols, len(cols),
+                         1, domains, "1.10", extra, supervised=False)
+    z.write("model.ini", ini)
+    for k_, v_ in files.items():
+        z.write(k_, v_)
+    z.write("losses", "\n".join(losses) + "\n")
+    z.write("archetypes", Yp.astype(">f8").tobytes())
+
+
+_WRITERS = {"rulefit": _rulefit, "gbm": _gbm, "drf": _drf, "glm": _glm, "kmeans": _kmeans, "isolationforest": _isofor,
             "extendedisolationforest": _eif, "deeplearning": _deeplearning, "word2vec": _word2vec,
             "stackedensemble": _stackedensemble, "pca": _pca, "xgboost": _xgboost,
-            "coxph": _coxph, "targetencoder": _targetencoder}
+            "coxph": _coxph, "targetencoder": _targetencoder, "glrm": _glrm}
 
 
 def _write_algo(model, z):

@@ -110,10 +110,61 @@ def test_glrm_vectorized_loss_matches_per_block_loop():
             if kind == "num":
                 ref += (_num_loss(lbc.get(c, "Quadratic"), a, u, 1.0) * mm)[:, 0]
             elif multi == "Ordinal":
-                lvl = a.argmax(1, keepdim=True)
-                ar = torch.arange(w, device=a.device).view(1, -1)
-                ref += torch.where(ar < lvl, torch.clamp(1 - u, min=0), torch.clamp(1 + u, min=0)).sum(1) * mm[:, 0]
+                # GlrmLoss.Ordinal.mloss, one row at a time
+                lv = a.argmax(1).tolist()
+                for r in range(a.shape[0]):
+                    if mm[r, 0] > 0:
+                        ref[r] += sum(max(1 - float(u[r, i]), 0) if lv[r] > i else 1.0 for i in range(w - 1))
             else:
                 ref += torch.where(a > 0, torch.clamp(1 - u, min=0), torch.clamp(1 + u, min=0)).sum(1) * mm[:, 0]
             j += w
         torch.testing.assert_close(m._loss(A, M, U, blocks, per_row=True), ref)
+
+
+def test_glrm_reference_layout_mojo(tmp_path):
+    """GlrmMojoWriter / GlrmMojoReader layout (cats-first permutation,
+    norm_sub / norm_mul, one GlrmLoss per column, big-endian archetypes):
+    the reference scorer (random-start per-row prox-gradient, 100 steps)
+    recovers the model's representation of new rows -- for quadratic loss
+    the x-problem is strictly convex, so both solvers meet at its optimum."""
+    from h2o3_amd.mojo import h2o_mojo
+    h2o.init()
+    rng = np.random.default_rng(4)
+    n = 400
+    Z = rng.normal(size=(n, 2))
+    df = pd.DataFrame({"a": Z[:, 0] + 3, "b": Z[:, 1] + 0.1 * rng.normal(size=n),
+                       "c": (Z[:, 0] - Z[:, 1]) * 10,
+                       "g": np.where(Z[:, 0] > 0.3, "hi", np.where(Z[:, 0] < -0.3, "lo", "mid"))})
+    df.loc[::17, "b"] = np.nan
+    fr = h2o.H2OFrame(df)
+    # SVD init: orthogonal archetypes, a well-conditioned x-problem for the
+    # reference's fixed-budget per-row scorer
+    m = H2OGeneralizedLowRankEstimator(k=2, transform="STANDARDIZE", max_iterations=500, seed=5, init="SVD",
+                                       svd_method="GramSVD", impute_original=True, loss="Quadratic")
+    m.train(x=["a", "b", "c"], training_frame=fr)
+    mj = h2o_mojo.load(m.download_mojo(str(tmp_path / "num"), format="h2o"))
+    assert mj.algo == "glrm" and mj.gl_perm == [0, 1, 2]
+    test = df.iloc[:80]
+    x_ours = m.transform_frame(h2o.H2OFrame(test)).as_data_frame().values
+    X = mj.row_matrix(test)
+    x_mojo = mj.score0(X)
+    # x itself is ill-determined along Y's weak direction; the objective and
+    # the reconstruction x Y are not
+    o_mojo, o_ours = mj._glrm_obj_grad(x_mojo, X, False)[0], mj._glrm_obj_grad(x_ours, X, False)[0]
+    assert np.max(o_mojo - o_ours) < 5e-3, np.max(o_mojo - o_ours)
+    mj.gl_rcnt = 0
+    rec = mj.predict(test)
+    exp = m.predict(h2o.H2OFrame(test)).as_data_frame()
+    for c in "abc":
+        np.testing.assert_allclose(rec[f"reconstr_{c}"].values, exp[f"reconstr_{c}"].values, rtol=1e-2, atol=1e-2)
+    # the row counter advances the per-row seed like GlrmMojoModel._rcnt
+    assert mj.gl_rcnt == 80
+    # categoricals first in the permuted layout; hinge losses for the one-hot block
+    m2 = H2OGeneralizedLowRankEstimator(k=3, transform="STANDARDIZE", max_iterations=500, seed=5, loss="Quadratic")
+    m2.train(x=["a", "g", "c"], training_frame=fr)
+    mj2 = h2o_mojo.load(m2.download_mojo(str(tmp_path / "mix"), format="h2o"))
+    assert mj2.gl_perm == [1, 0, 2] and mj2.gl_losses == ["Categorical", "Quadratic", "Quadratic"]
+    assert mj2.gl_levels == [3] and mj2.gl_Y.shape == (3, 5)
+    rec2 = mj2.predict(test)
+    exp2 = m2.predict(h2o.H2OFrame(test)).as_data_frame()
+    assert (rec2["reconstr_g"].values == exp2["reconstr_g"].values).mean() >= 0.9

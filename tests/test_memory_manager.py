@@ -42,7 +42,7 @@ def test_gbm_on_frame_three_times_the_budget(tmp_path):
     df = _frame(1_000_000, 192)                          # 768 MB of float32 columns
     x = [c for c in df.columns if c != "y"]
     ref_fr = h2o.H2OFrame(df)
-    ref = H2OGradientBoostingEstimator(ntrees=2, max_depth=3, seed=1, nbins=16)
+    ref = H2OGradientBoostingEstimator(ntrees=1, max_depth=3, seed=1, nbins=16)
     ref.train(x=x, y="y", training_frame=ref_fr)
     p_ref = ref.predict(ref_fr).as_data_frame().iloc[:, -1].values
     del ref_fr
@@ -52,7 +52,7 @@ def test_gbm_on_frame_three_times_the_budget(tmp_path):
         del df
         st0 = memory.stats()
         assert st0["resident_bytes"] <= 256 << 20 and st0["spills"] > 0
-        m = H2OGradientBoostingEstimator(ntrees=2, max_depth=3, seed=1, nbins=16)
+        m = H2OGradientBoostingEstimator(ntrees=1, max_depth=3, seed=1, nbins=16)
         m.train(x=x, y="y", training_frame=fr)
         p = m.predict(fr).as_data_frame().iloc[:, -1].values
         st = memory.stats()

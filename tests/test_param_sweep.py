@@ -314,7 +314,8 @@ _V = {
     "agg": {"transform": "DEMEAN", "categorical_encoding": "Eigen"},
     "w2v": {"epochs": 4},
     "psvm": {"max_iterations": 1},
-    "rulefit": {"lambda_": 0.5, "distribution": "bernoulli", "algorithm": "GBM"},
+    "rulefit": {"lambda_": 0.5, "distribution": "bernoulli", "algorithm": "GBM",
+                "auc_type": ("MACRO_OVO", {"_y": "ym", "rule_generation_ntrees": 2, "max_rule_length": 1})},
     "iso": {},
     "te": {"seed": (7, {"noise": 0.5})},
     "uplift": {"max_depth": 2, "mtries": 1, "sample_rate": 0.5, "histogram_type": "Random",

@@ -29,4 +29,38 @@ def test_rulefit_regression_and_binomial():
                              model_type="RULES")
     mb.train(x=list("abcd"), y="yb", training_frame=fr2)
     assert mb.auc() > 0.95
-    assert mb.predict_rules(fr2, ["rule_0"]).ncol == 1
+    # rules are leaves, named M<model>T<tree>N<node> (Rule.extractRulesFromTree);
+    # a row satisfies exactly one leaf rule per tree
+    name = mb._rule_names[0]
+    assert name.startswith("M0T0N")
+    pr = mb.predict_rules(fr2, [n for n in mb._rule_names if n.startswith("M0T0N")]).as_data_frame()
+    assert (pr.sum(axis=1) == 1).all()
+
+
+def test_rulefit_reference_layout_mojo(tmp_path):
+    """RuleFitMojoModel layout (rules per depth/tree + nested GLM over M<i>T<j>
+    categoricals): the reference-layout reader scores like the model."""
+    from h2o3_amd.mojo import h2o_mojo
+    h2o.init()
+    rng = np.random.default_rng(2)
+    n = 1200
+    X = rng.uniform(0, 1, size=(n, 3))
+    df = pd.DataFrame(X, columns=list("abc"))
+    df["g"] = rng.choice(["u", "v", "w"], n)
+    df.loc[::29, "a"] = np.nan
+    y = 2.0 * ((df["a"].fillna(0) > 0.5) & (df["g"] == "v")) + X[:, 1] + rng.normal(scale=0.1, size=n)
+    df["y"] = y
+    df["yb"] = np.where(y > 1.2, "hi", "lo")
+    fr = h2o.H2OFrame(df)
+    for mtype, yy in (("RULES_AND_LINEAR", "y"), ("RULES", "yb"), ("LINEAR", "y")):
+        m = H2ORuleFitEstimator(min_rule_length=1, max_rule_length=2, rule_generation_ntrees=6, seed=3,
+                                model_type=mtype)
+        m.train(x=["a", "b", "c", "g"], y=yy, training_frame=fr)
+        ours = m.predict(fr).as_data_frame().iloc[:, -1].values
+        ref = h2o_mojo.load(m.download_mojo(str(tmp_path / f"rf_{mtype}"), format="h2o"))
+        # the frame holds float32 values: score the same values
+        d32 = df.copy()
+        for c in "abc":
+            d32[c] = d32[c].astype(np.float32).astype(np.float64)
+        got = np.asarray(ref.predict_raw(d32))[:, -1]
+        np.testing.assert_allclose(got, ours, rtol=1e-5, atol=1e-5)
