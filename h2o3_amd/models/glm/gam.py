@@ -54,7 +54,10 @@ def _cr_matrices(knots):
 
 
 def cr_basis(x: torch.Tensor, knots: np.ndarray):
-    """Natural cubic regression spline basis [n, k] (coefficients = f(knots))."""
+    """Natural cubic regression spline basis [n, k] (coefficients = f(knots)),
+    as GamUtilsCubicRegression.expandOneGamCol: the knot interval by
+    locateBin (x <= k_0 -> first, x >= k_last -> last interval) and the
+    interval's cubic continued outside the knot range."""
     k = len(knots)
     Fp_np, S = _cr_matrices(knots)
     dev, dt = x.device, torch.float64
@@ -64,41 +67,90 @@ def cr_basis(x: torch.Tensor, knots: np.ndarray):
     xd = x.to(dt)
     j = (torch.searchsorted(kn, xd, right=True) - 1).clamp(0, k - 2)
     xl, xr, hj = kn[j], kn[j + 1], h[j]
-    xc = xd.clamp(float(kn[0]), float(kn[-1]))
-    am, ap = (xr - xc) / hj, (xc - xl) / hj
-    cm = ((xr - xc) ** 3 / hj - hj * (xr - xc)) / 6
-    cp = ((xc - xl) ** 3 / hj - hj * (xc - xl)) / 6
+    am, ap = (xr - xd) / hj, (xd - xl) / hj
+    cm = ((xr - xd) ** 3 / hj - hj * (xr - xd)) / 6
+    cp = ((xd - xl) ** 3 / hj - hj * (xd - xl)) / 6
     n = x.shape[0]
     X = cm.view(-1, 1) * Fp[j] + cp.view(-1, 1) * Fp[j + 1]
     r = torch.arange(n, device=dev)
     X[r, j] += am
     X[r, j + 1] += ap
-    # linear extrapolation outside the knot range (natural spline)
-    e = torch.eye(k, dtype=dt, device=dev)
-    d0 = (e[1] - e[0]) / h[0] - h[0] / 6 * Fp[1]
-    d1 = (e[-1] - e[-2]) / h[-1] + h[-1] / 6 * Fp[-2]
-    lo, hi = xd < kn[0], xd > kn[-1]
-    X = torch.where(lo.view(-1, 1), e[0] + (xd - kn[0]).view(-1, 1) * d0, X)
-    X = torch.where(hi.view(-1, 1), e[-1] + (xd - kn[-1]).view(-1, 1) * d1, X)
     return X, S
 
 
-def tp_basis(x: torch.Tensor, knots: np.ndarray):
-    """1-D thin-plate regression spline (m=2): E(x, knots) Z_T plus the linear
-    null-space term; returns ([n, k-1], penalty)."""
-    k = len(knots)
-    kn = torch.as_tensor(knots, dtype=torch.float64, device=x.device)
-    xd = x.to(torch.float64)
-    E = (xd.view(-1, 1) - kn.view(1, -1)).abs() ** 3 / 12.0
-    Ekk = (np.abs(knots.reshape(-1, 1) - knots.reshape(1, -1)) ** 3) / 12.0
-    T = np.stack([np.ones(k), knots], 1)
+def tp_constant(m, d):
+    """GamUtilsThinPlateRegression.calTPConstantTerm."""
+    from math import factorial, pi
+    if d % 2 == 0:
+        return (-1) ** (m + 1 + d // 2) / (2 ** (2 * m - 1) * pi ** (d / 2.0) * factorial(m - 1) *
+                                           factorial(m - d // 2))
+    return (-1) ** m * m / (factorial(2 * m) * pi ** ((d - 1) / 2.0))
+
+
+def tp_distance(X, knots, m, ostd=None):
+    """c * r^(2m-d) (times log r^(2m-d) for even d) between rows and knots
+    (GamUtilsThinPlateRegression.calculateDistance); numpy or torch."""
+    d = knots.shape[1]
+    c = tp_constant(m, d)
+    if isinstance(X, torch.Tensor):
+        kn = torch.as_tensor(knots, dtype=torch.float64, device=X.device)
+        diff = X.to(torch.float64).unsqueeze(1) - kn.unsqueeze(0)
+        if ostd is not None:
+            diff = diff * torch.as_tensor(ostd, dtype=torch.float64, device=X.device)
+        dist = torch.sqrt((diff * diff).sum(-1)) ** (2 * m - d)
+        val = c * dist
+        if d % 2 == 0:
+            val = torch.where(dist != 0, val * torch.log(dist.clamp_min(1e-300)), val)
+        return val
+    diff = np.asarray(X, dtype=np.float64)[:, None, :] - knots[None, :, :]
+    if ostd is not None:
+        diff = diff * np.asarray(ostd)
+    dist = np.sqrt((diff * diff).sum(-1)) ** (2 * m - d)
+    val = c * dist
+    if d % 2 == 0:
+        val = np.where(dist != 0, val * np.log(np.where(dist != 0, dist, 1.0)), val)
+    return val
+
+
+def tp_poly(X, terms, means=None, ostd=None):
+    """Polynomial null-space basis (GamUtilsThinPlateRegression.calculatePolynomialBasis;
+    with standardisation each predictor enters as x - mean * (1/std), as the
+    reference computes it)."""
+    Xd = X.to(torch.float64)
+    if means is not None:
+        Xd = Xd - torch.as_tensor(np.asarray(means) * np.asarray(ostd), dtype=torch.float64, device=X.device)
+    cols = [torch.prod(Xd ** torch.as_tensor(e, dtype=torch.float64, device=X.device), 1) for e in terms]
+    return torch.stack(cols, 1)
+
+
+def tp_setup(knots, means, ostd, standardize):
+    """Per-smoother thin-plate constants (GAM.java ThinPlateRegressionSmootherWithKnots):
+    polynomial terms (degree < m, constant included), zCS = orthonormal
+    complement of the polynomial values at the (demeaned) knots, and the
+    penalty zCS' E_kk zCS expanded with zero rows for the polynomial part."""
+    kn = np.asarray(knots, dtype=np.float64)
+    k, d = kn.shape
+    m = _tp_m(d)
+    terms = _poly_terms(d, m)
+    M = len(terms)
+    dm = (kn - np.asarray(means)) * (np.asarray(ostd) if standardize else 1.0)
+    T = np.stack([np.prod(dm ** np.asarray(e), 1) for e in terms], 1)          # [k, M]
     Q, _ = np.linalg.qr(T, mode="complete")
-    ZT = Q[:, 2:]                                   # k x (k-2), T' ZT = 0
-    Xs = E @ torch.as_tensor(ZT, device=x.device)
-    X = torch.cat([Xs, xd.view(-1, 1)], 1)
-    S = np.zeros((k - 1, k - 1))
-    S[: k - 2, : k - 2] = ZT.T @ Ekk @ ZT
-    return X, S
+    zCS = Q[:, M:]                                                            # [k, k - M]
+    Ekk = tp_distance(kn, kn, m, ostd if standardize else None)
+    S = np.zeros((k, k))
+    S[: k - M, : k - M] = zCS.T @ Ekk @ zCS
+    return {"m": m, "M": M, "terms": terms, "zCS": zCS, "S": S}
+
+
+def tp_ref_basis(X: torch.Tensor, knots: np.ndarray, setup, means, ostd, standardize):
+    """Thin-plate regression spline with knots [n, k]: distances projected on
+    zCS (k - M columns) followed by the M polynomial terms."""
+    kn = np.asarray(knots, dtype=np.float64)
+    E = tp_distance(X, kn, setup["m"], ostd if standardize else None)
+    Xcs = E @ torch.as_tensor(setup["zCS"], dtype=torch.float64, device=X.device)
+    P = tp_poly(X, setup["terms"], means if standardize else None, ostd if standardize else None)
+    return torch.cat([Xcs, P], 1), setup["S"]
 
 
 def _tp_m(d):
@@ -109,41 +161,6 @@ def _poly_terms(d, m):
     """Exponent tuples of the monomials of total degree < m in d variables."""
     import itertools
     return [e for e in itertools.product(range(m), repeat=d) if sum(e) < m]
-
-
-def _tp_eta(r, d, m):
-    p = 2 * m - d
-    if d % 2 == 0:
-        return torch.where(r > 0, r ** p * torch.log(r.clamp_min(1e-300)), torch.zeros_like(r)) \
-            if isinstance(r, torch.Tensor) else np.where(r > 0, r ** p * np.log(np.maximum(r, 1e-300)), 0.0)
-    return r ** p
-
-
-def tp_multi_basis(X: torch.Tensor, knots: np.ndarray):
-    """d-dimensional thin-plate regression spline (ThinPlateRegressionUtils):
-    radial part eta(|x - knot|) projected on the null space of the polynomial
-    constraint T' a = 0, plus the non-constant polynomial terms (degree < m,
-    m = floor((d+1)/2) + 1).  Returns ([n, k - M + M - 1], penalty)."""
-    n, d = X.shape
-    m = _tp_m(d)
-    terms = _poly_terms(d, m)
-    kn = np.asarray(knots, dtype=np.float64)
-    k = kn.shape[0]
-    Tk = np.stack([np.prod(kn ** np.asarray(e), 1) for e in terms], 1)          # [k, M]
-    Q, _ = np.linalg.qr(Tk, mode="complete")
-    ZT = Q[:, len(terms):]
-    knt = torch.as_tensor(kn, dtype=torch.float64, device=X.device)
-    r = torch.cdist(X.to(torch.float64), knt)
-    E = _tp_eta(r, d, m)
-    Xs = E @ torch.as_tensor(ZT, device=X.device)
-    poly = [torch.prod(X.to(torch.float64) ** torch.as_tensor(e, dtype=torch.float64, device=X.device), 1)
-            for e in terms if sum(e) > 0]
-    out = torch.cat([Xs] + [p.view(-1, 1) for p in poly], 1)
-    rk = np.sqrt(((kn[:, None, :] - kn[None, :, :]) ** 2).sum(-1))
-    Ekk = _tp_eta(rk, d, m)
-    S = np.zeros((out.shape[1], out.shape[1]))
-    S[: ZT.shape[1], : ZT.shape[1]] = ZT.T @ Ekk @ ZT
-    return out, S
 
 
 def _bspline(x: torch.Tensor, knots: np.ndarray, order: int):
@@ -208,17 +225,17 @@ class H2OGeneralizedAdditiveEstimator(H2OGeneralizedLinearEstimator):
         return gc, per("bs", 0), per("num_knots", None), per("scale", 1.0), per("spline_orders", 2), \
             per("splines_non_negative", True)
 
-    def _basis(self, frame, c, bs, knots, order):
-        if isinstance(c, tuple):
+    def _basis(self, frame, c, bs, knots, order, gi=None):
+        if bs == 1:
+            cc_ = c if isinstance(c, tuple) else (c,)
             cols = [torch.where(torch.isnan(v), torch.full_like(v, self._col_means[cc]), v)
-                    for cc, v in ((cc, frame.vec(cc).as_float(torch.float64)) for cc in c)]
-            return tp_multi_basis(torch.stack(cols, 1), knots)
+                    for cc, v in ((cc, frame.vec(cc).as_float(torch.float64)) for cc in cc_)]
+            t = self._tp[gi]
+            return tp_ref_basis(torch.stack(cols, 1), knots, t, t["means"], t["ostd"], t["standardize"])
         x = frame.vec(c).as_float(torch.float64)
         x = torch.where(torch.isnan(x), torch.full_like(x, self._col_means[c]), x)
         if bs == 0:
             return cr_basis(x, knots)
-        if bs == 1:
-            return tp_basis(x, knots)
         if bs == 2:
             return is_basis(x, knots, order)
         if bs == 3:
@@ -235,7 +252,7 @@ class H2OGeneralizedAdditiveEstimator(H2OGeneralizedLinearEstimator):
             names.append(c)
         for gi, c in enumerate(self._gam_cols):
             bs, knots, order = self._bs[gi], self._knots[gi], self._orders[gi]
-            X, S = self._basis(frame, c, bs, knots, order)
+            X, S = self._basis(frame, c, bs, knots, order, gi)
             if fit:
                 w = torch.ones(X.shape[0], dtype=X.dtype, device=X.device)
                 cs = (X * w.view(-1, 1)).sum(0)
@@ -268,10 +285,12 @@ class H2OGeneralizedAdditiveEstimator(H2OGeneralizedLinearEstimator):
         self._gam_cols, self._bs, self._orders = list(gc), [int(b) for b in bs], [int(o) for o in orders]
         self._knots, self._Z, self._S = [], [], []
         self._col_means = {}
+        self._tp = {}
         kids = p.get("knot_ids")
         for gi, c in enumerate(gc):
             if isinstance(c, tuple):
                 self._knots.append(self._tp_knots(training_frame, c, nk[gi]))
+                self._tp[gi] = self._tp_setup(training_frame, c, self._knots[gi])
                 continue
             v = training_frame.vec(c)
             xs = v.as_float(torch.float64)
@@ -285,6 +304,11 @@ class H2OGeneralizedAdditiveEstimator(H2OGeneralizedLinearEstimator):
                 k = nk[gi] if nk[gi] is not None else (10 if self._bs[gi] in (0, 1) else 6)
                 qs = np.linspace(0, 1, int(k))
                 knots = np.unique(np.quantile(xs.cpu().numpy(), qs))
+            if self._bs[gi] == 1:
+                knots = knots.reshape(-1, 1)
+                self._knots.append(knots)
+                self._tp[gi] = self._tp_setup(training_frame, (c,), knots)
+                continue
             self._knots.append(knots)
         gfr = self._gam_frame(training_frame, fit=True)
         vfr = self._gam_frame(validation_frame) if validation_frame is not None else None
@@ -305,6 +329,25 @@ class H2OGeneralizedAdditiveEstimator(H2OGeneralizedLinearEstimator):
         self._output["knots"] = [k.tolist() for k in self._knots]
         self._output["gam_columns"] = self._gam_cols
         return self
+
+    def _tp_setup(self, frame, cols, knots):
+        """Raw means / inverse standard deviations of the smoother's columns
+        (GAM.java:519-526) and the thin-plate constants (tp_setup)."""
+        means, ostd = [], []
+        for cc in cols:
+            v = frame.vec(cc).as_float(torch.float64)
+            ok = ~torch.isnan(v)
+            st = torch.stack([v[ok].sum(), (v[ok] ** 2).sum(), ok.sum().to(torch.float64)])
+            coll.allreduce_(st)
+            s1, s2, cnt = (float(t) for t in st)
+            mu = s1 / max(cnt, 1.0)
+            var = max(s2 - cnt * mu * mu, 0.0) / max(cnt - 1.0, 1.0)
+            means.append(mu)
+            ostd.append(1.0 / np.sqrt(var) if var > 0 else 1.0)
+        std = bool(self._parms.get("standardize_tp_gam_cols"))
+        t = tp_setup(knots, means, ostd, std)
+        t.update(means=np.asarray(means), ostd=np.asarray(ostd), standardize=std)
+        return t
 
     def _tp_knots(self, frame, cols, k):
         """Knots of a multi-column thin plate smoother: num_knots distinct data

@@ -1,6 +1,6 @@
 """numpy evaluation of the GAM smoother bases for the standalone scorer.
 
-Mirror of models/glm/gam.py (cr_basis / tp_basis / is_basis / ms_basis),
+Mirror of models/glm/gam.py (cr_basis / tp_ref_basis / is_basis / ms_basis),
 written against numpy only so a GAM MOJO scores without torch (reference:
 hex/genmodel/algos/gam/GamMojoModel.java evaluates the same splines)."""
 from __future__ import annotations
@@ -23,36 +23,48 @@ def _cr_matrices(knots):
 
 
 def cr_basis(x, knots):
+    """GamUtilsCubicRegression.expandOneGamCol (cubic continued outside the knots)."""
     kn = np.asarray(knots, dtype=np.float64)
     k = len(kn)
     Fp = _cr_matrices(kn)
     h = np.diff(kn)
     j = np.clip(np.searchsorted(kn, x, side="right") - 1, 0, k - 2)
     xl, xr, hj = kn[j], kn[j + 1], h[j]
-    xc = np.clip(x, kn[0], kn[-1])
-    am, ap = (xr - xc) / hj, (xc - xl) / hj
-    cm = ((xr - xc) ** 3 / hj - hj * (xr - xc)) / 6
-    cp = ((xc - xl) ** 3 / hj - hj * (xc - xl)) / 6
+    am, ap = (xr - x) / hj, (x - xl) / hj
+    cm = ((xr - x) ** 3 / hj - hj * (xr - x)) / 6
+    cp = ((x - xl) ** 3 / hj - hj * (x - xl)) / 6
     X = cm[:, None] * Fp[j] + cp[:, None] * Fp[j + 1]
     r = np.arange(len(x))
     X[r, j] += am
     X[r, j + 1] += ap
-    e = np.eye(k)
-    d0 = (e[1] - e[0]) / h[0] - h[0] / 6 * Fp[1]
-    d1 = (e[-1] - e[-2]) / h[-1] + h[-1] / 6 * Fp[-2]
-    lo, hi = x < kn[0], x > kn[-1]
-    X = np.where(lo[:, None], e[0] + (x - kn[0])[:, None] * d0, X)
-    X = np.where(hi[:, None], e[-1] + (x - kn[-1])[:, None] * d1, X)
     return X
 
 
-def tp_basis(x, knots):
-    kn = np.asarray(knots, dtype=np.float64)
-    k = len(kn)
-    E = np.abs(x[:, None] - kn[None, :]) ** 3 / 12.0
-    T = np.stack([np.ones(k), kn], 1)
-    Q, _ = np.linalg.qr(T, mode="complete")
-    return np.concatenate([E @ Q[:, 2:], x[:, None]], 1)
+def tp_constant(m, d):
+    from math import factorial, pi
+    if d % 2 == 0:
+        return (-1) ** (m + 1 + d // 2) / (2 ** (2 * m - 1) * pi ** (d / 2.0) * factorial(m - 1) *
+                                           factorial(m - d // 2))
+    return (-1) ** m * m / (factorial(2 * m) * pi ** ((d - 1) / 2.0))
+
+
+def tp_basis(X, knots, zcs, terms, means, ostd, standardize):
+    """Thin plate with knots: c r^(2m-d) [log] distances on zCS, then the
+    polynomial terms (numpy twin of models/glm/gam.py:tp_ref_basis)."""
+    kn = np.asarray(knots, dtype=np.float64).reshape(len(knots), -1)
+    X = np.asarray(X, dtype=np.float64).reshape(X.shape[0], -1)
+    d = kn.shape[1]
+    m = (d + 1) // 2 + 1
+    diff = X[:, None, :] - kn[None, :, :]
+    if standardize:
+        diff = diff * np.asarray(ostd)
+    dist = np.sqrt((diff * diff).sum(-1)) ** (2 * m - d)
+    E = tp_constant(m, d) * dist
+    if d % 2 == 0:
+        E = np.where(dist != 0, E * np.log(np.where(dist != 0, dist, 1.0)), E)
+    Xp = X - np.asarray(means) * np.asarray(ostd) if standardize else X
+    poly = np.stack([np.prod(Xp ** np.asarray(e, dtype=np.float64), 1) for e in terms], 1)
+    return np.concatenate([E @ np.asarray(zcs), poly], 1)
 
 
 def _bspline(x, knots, order):
@@ -78,8 +90,6 @@ def basis(x, bs, knots, order):
     knots = np.asarray(knots, dtype=np.float64)
     if bs == 0:
         return cr_basis(x, knots)
-    if bs == 1:
-        return tp_basis(x, knots)
     if bs == 2:
         B = _bspline(x, knots, order + 1)
         return np.flip(np.cumsum(np.flip(B, 1), 1), 1)[:, 1:]
@@ -88,18 +98,47 @@ def basis(x, bs, knots, order):
     raise ValueError(bs)
 
 
-def tp_multi_basis(X, knots):
-    """numpy twin of models/glm/gam.py:tp_multi_basis."""
-    import itertools
-    n, d = X.shape
-    m = (d + 1) // 2 + 1
-    terms = [e for e in itertools.product(range(m), repeat=d) if sum(e) < m]
+# ----------------------------------------------------------- reference I-splines
+def _fill_knots(knots, m):
+    """GamUtilsISplines.fillKnots: m-1 copies of each boundary knot added."""
+    kn = list(np.asarray(knots, dtype=np.float64))
+    up = max(m - 1, 0)
+    return np.asarray([kn[0]] * up + kn + [kn[-1]] * up)
+
+
+def _bspline_eval(x, t, i, order):
+    """NBSplinesTypeII.BSplineBasis.evaluate of basis i of `order` over the
+    filled knot sequence t (half-open support, 0 outside)."""
+    kn = t[i:i + order + 1]
+    inside = (x >= kn[0]) & (x < kn[-1])
+    if order == 1:
+        return inside.astype(np.float64)
+    d0 = kn[order - 1] - kn[0]
+    d1 = kn[order] - kn[1]
+    a = (x - kn[0]) * (1.0 / d0 if d0 != 0 else 0.0) * _bspline_eval(x, t, i, order - 1)
+    b = (kn[order] - x) * (1.0 / d1 if d1 != 0 else 0.0) * _bspline_eval(x, t, i + 1, order - 1)
+    return np.where(inside, a + b, 0.0)
+
+
+def ispline_basis(x, knots, order):
+    """ISplines.gamifyVal for every value: basis j is 0 below its first knot,
+    1 from its (order)-th knot on, else the sum of the order+1 B-splines from
+    index j+1 (sumNBSpline)."""
+    x = np.asarray(x, dtype=np.float64)
     kn = np.asarray(knots, dtype=np.float64)
-    Tk = np.stack([np.prod(kn ** np.asarray(e), 1) for e in terms], 1)
-    Q, _ = np.linalg.qr(Tk, mode="complete")
-    ZT = Q[:, len(terms):]
-    r = np.sqrt(((X[:, None, :] - kn[None, :, :]) ** 2).sum(-1))
-    p = 2 * m - d
-    E = np.where(r > 0, r ** p * np.log(np.maximum(r, 1e-300)), 0.0) if d % 2 == 0 else r ** p
-    poly = [np.prod(X ** np.asarray(e, dtype=np.float64), 1)[:, None] for e in terms if sum(e) > 0]
-    return np.concatenate([E @ ZT] + poly, 1)
+    nI = len(kn) + order - 2
+    tI = _fill_knots(kn, order)
+    tB = _fill_knots(kn, order + 1)
+    nB = len(kn) + order + 1 - 2
+    Bv = [_bspline_eval(x, tB, b, order + 1) for b in range(nB)]
+    out = np.zeros((x.shape[0], nI))
+    for j in range(nI):
+        ik = tI[j:j + order + 1]
+        acc = np.zeros_like(x)
+        live = np.ones(x.shape[0], dtype=bool)
+        for b in range(j + 1, nB):
+            bk = tB[b:b + order + 2]
+            live &= ~(x < bk[0])
+            acc += np.where(live, np.where(x >= bk[-1], 1.0, Bv[b]), 0.0)
+        out[:, j] = np.where(x < ik[0], 0.0, np.where(x >= ik[order], 1.0, acc))
+    return out

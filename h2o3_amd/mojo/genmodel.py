@@ -151,17 +151,19 @@ class MojoModel:
     def _gam_columns(self, df):
         """Smoother columns <col>_<cr|tp|is|ms>_<i> from the stored knots and
         centering matrices (mojo/gam_np.py)."""
-        from .gam_np import basis
+        from .gam_np import basis, tp_basis
         g = self.meta["gam"]
         suf = {0: "cr", 1: "tp", 2: "is", 3: "ms"}
         df = df.copy()
-        from .gam_np import tp_multi_basis
         for gi, c in enumerate(g["cols"]):
-            if isinstance(c, (list, tuple)):
+            if g["bs"][gi] == 1:
+                cc_ = list(c) if isinstance(c, (list, tuple)) else [c]
                 Xm = np.stack([np.where(np.isnan(self._col(df, cc)), g["means"][cc], self._col(df, cc))
-                               for cc in c], 1)
-                Xc = tp_multi_basis(Xm, g["knots"][gi]) @ self._arr[f"gamZ{gi}"]
-                name = "_".join(c)
+                               for cc in cc_], 1)
+                t = g["tp"][str(gi)]
+                Xc = tp_basis(Xm, g["knots"][gi], self._arr[f"gamZcs{gi}"], t["terms"], t["means"], t["ostd"],
+                              t["standardize"]) @ self._arr[f"gamZ{gi}"]
+                name = "_".join(cc_) if isinstance(c, (list, tuple)) else c
             else:
                 x = self._col(df, c)
                 x = np.where(np.isnan(x), g["means"][c], x)

@@ -587,6 +587,129 @@ class H2OMojoModel:
             out[:, self.gl_perm[d]] = v
         return out
 
+    def _load_gam(self):
+        """GamMojoReader: the GLM part (scored by the GLM scorer on
+        beta_center) and per smoother (bs-sorted: cubic regression, I-spline,
+        thin plate) the knots, Z', B^-1 D, zCS', polynomial exponents and raw
+        means / inverse standard deviations."""
+        fam = str(self.kv("family"))
+        self.family = {"bernoulli": "binomial"}.get(fam, fam)
+        self.glm_link = str(self.kv("link", "identity"))
+        self.tweedie_link_power = float(self.kv("tweedie_link_power", 0.0))
+        self.use_all_levels = bool(self.kv("use_all_factor_levels", False))
+        self.cats = int(self.kv("cats", -1))
+        self.cat_offsets = list(self.kv("cat_offsets", [0]))
+        self.nums = int(self.kv("numsCenter"))
+        self.mean_imputation = bool(self.kv("mean_imputation", False))
+        self.cat_modes = list(self.kv("catNAFills", []) or [])
+        self.num_means = list(self.kv("numNAFillsCenter", []) or [])
+        K = self.nclasses
+        if self.family in ("multinomial", "ordinal"):
+            L = int(self.kv("beta center length per class"))
+            self.beta = np.frombuffer(self.be.read("beta_multinomial_centering"), dtype=">f8",
+                                      count=K * L).astype(np.float64)
+        else:
+            self.beta = np.asarray(self.kv("beta_center"), dtype=np.float64)
+        nk = [int(v) for v in self.kv("num_knots_sorted")]
+        bs = [int(v) for v in self.kv("bs_sorted")]
+        dims = [int(v) for v in self.kv("_d")]
+        cols = self.be.text("gam_columns_sorted")
+        ng = len(nk)
+        self.gm_cols, p = [], 0
+        for g in range(ng):
+            self.gm_cols.append(cols[p:p + dims[g]])
+            p += dims[g]
+        orders = [int(v) for v in (self.kv("spline_orders_sorted", []) or [])]
+        ntp = int(self.kv("num_TP_col", 0))
+        Ms = [int(v) for v in (self.kv("_M", []) or [])]
+        kb = io.BytesIO(self.be.read("knots"))
+        zb = io.BytesIO(self.be.read("zTranspose"))
+        rd = lambda b, r, c: np.frombuffer(b.read(8 * r * c), dtype=">f8").astype(np.float64).reshape(r, c)  # noqa
+        self.gm = []
+        ti = 0
+        binv = io.BytesIO(self.be.read("_binvD")) if self.be.exists("_binvD") else None
+        if ntp:
+            zcs = io.BytesIO(self.be.read("zTransposeCS"))
+            poly = io.BytesIO(self.be.read("polynomialBasisList"))
+            mraw = io.BytesIO(self.be.read("gamColMeansRaw"))
+            sraw = io.BytesIO(self.be.read("gamColStdRaw"))
+        std = bool(self.kv("standardize", False))
+        for g in range(ng):
+            k = nk[g]
+            knots = rd(kb, dims[g], k)
+            nb = k + orders[g] - 2 if bs[g] == 2 else k - 1
+            zt = rd(zb, nb, k)
+            e = {"bs": bs[g], "knots": knots, "zt": zt, "ncen": nb}
+            if bs[g] == 0:
+                e["binvD"] = rd(binv, k - 2, k)
+            elif bs[g] == 2:
+                e["order"] = orders[g]
+            elif bs[g] == 1:
+                M = Ms[ti]
+                d = dims[g]
+                e["zcsT"] = rd(zcs, k - M, k)
+                e["terms"] = np.frombuffer(poly.read(4 * M * d), dtype=">i4").astype(np.int64).reshape(M, d)
+                e["means"] = rd(mraw, 1, d)[0]
+                e["ostd"] = rd(sraw, 1, d)[0]
+                e["standardize"] = std
+                ti += 1
+            else:
+                raise NotImplementedError(f"GAM spline type {bs[g]}")
+            self.gm.append(e)
+        self.gm_start = self.nfeatures - int(self.kv("num_expanded_gam_columns_center"))
+
+    def _gamify(self, df, X):
+        """GamMojoModelBase.addExpandGamCols: when the centred smoother columns
+        are absent, evaluate every smoother from its raw input column(s) (a
+        missing input leaves its columns NA for mean imputation)."""
+        from .gam_np import ispline_basis, tp_constant
+        if not np.all(np.isnan(X[:, self.gm_start:self.nfeatures])):
+            return
+        j = self.gm_start
+        n = X.shape[0]
+        for gi, e in enumerate(self.gm):
+            cols = []
+            for c in self.gm_cols[gi]:
+                cols.append(np.asarray(pd_numeric(df[c]) if c in df else np.full(n, np.nan), dtype=np.float64))
+            V = np.stack(cols, 1)
+            ok = ~np.isnan(V).any(1)
+            Vz = np.where(np.isnan(V), 0.0, V)
+            if e["bs"] == 0:
+                kn = e["knots"][0]
+                x = Vz[:, 0]
+                k = kn.size
+                h = np.diff(kn)
+                b = np.clip(np.searchsorted(kn, x, side="right") - 1, 0, k - 2)
+                cm = ((kn[b + 1] - x) ** 3 / h[b] - h[b] * (kn[b + 1] - x)) / 6
+                cp = ((x - kn[b]) ** 3 / h[b] - h[b] * (x - kn[b])) / 6
+                Fp = np.vstack([np.zeros(k), e["binvD"], np.zeros(k)])
+                B = cm[:, None] * Fp[b] + cp[:, None] * Fp[b + 1]
+                r = np.arange(n)
+                B[r, b] += (kn[b + 1] - x) / h[b]
+                B[r, b + 1] += (x - kn[b]) / h[b]
+                out = B @ e["zt"].T
+            elif e["bs"] == 2:
+                out = ispline_basis(Vz[:, 0], e["knots"][0], e["order"])
+            else:
+                kn = e["knots"].T                                   # [k, d]
+                d = kn.shape[1]
+                m = (d + 1) // 2 + 1
+                diff = Vz[:, None, :] - kn[None, :, :]
+                if e["standardize"]:
+                    diff = diff * e["ostd"]
+                dist = np.sqrt((diff * diff).sum(-1)) ** (2 * m - d)
+                E = tp_constant(m, d) * dist
+                if d % 2 == 0:
+                    E = np.where(dist != 0, E * np.log(np.where(dist != 0, dist, 1.0)), E)
+                Vp = Vz - e["means"] * e["ostd"] if e["standardize"] else Vz
+                P = np.stack([np.prod(Vp ** t, 1) for t in e["terms"].astype(np.float64)], 1)
+                out = np.concatenate([E @ e["zcsT"].T, P], 1) @ e["zt"].T
+            X[:, j:j + e["ncen"]] = np.where(ok[:, None], out, np.nan)
+            j += e["ncen"]
+
+    def _score_gam(self, X):
+        return self._score_glm(X)
+
     def _load_stackedensemble(self):
         subs = {}
         for i in range(int(self.kv("submodel_count", 0))):
@@ -1036,6 +1159,8 @@ class H2OMojoModel:
                     X[:, j] = np.asarray(pd.to_numeric(pd.Series(vals), errors="coerce"), dtype=np.float64)
                 except Exception:
                     pass
+        if self.algo == "gam":
+            self._gamify(df, X)
         return X
 
     # -------------------------------------------------------------- scoring
@@ -1666,6 +1791,11 @@ def _glrm_prox(name, u, delta, project=False):
     else:
         raise NotImplementedError(f"GLRM regularizer {name}")
     return np.where(keep, u, v)
+
+
+def pd_numeric(col):
+    import pandas as pd
+    return pd.to_numeric(col, errors="coerce").values
 
 
 def load(src) -> H2OMojoModel:

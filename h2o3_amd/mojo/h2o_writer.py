@@ -1045,10 +1045,169 @@ def _glrm(model, z):
     z.write("archetypes", Yp.astype(">f8").tobytes())
 
 
+def _be_f8(rows):
+    """java.nio.ByteBuffer putDouble order (big endian), rows flattened."""
+    flat = [float(v) for r in rows for v in np.asarray(r, dtype=np.float64).reshape(-1)]
+    return np.asarray(flat, dtype=">f8").tobytes()
+
+
+def _gam(model, z):
+    """GAMMojoWriter layout (mojo 1.00): the GLM part (cats first, then the
+    plain numerics, then the centred smoother columns in bs-sorted order --
+    cubic regression, I-spline, thin plate -- and the intercept) with
+    beta_center for scoring and beta (uncentred smoother coefficients Z b);
+    per smoother the knots, zTranspose (Z'), the cubic-spline B^-1 D
+    (_binvD), the thin-plate zCS', polynomial exponent lists, raw means and
+    inverse standard deviations.  Text files hold the column-name lists."""
+    if any(b == 3 for b in model._bs):
+        raise NotImplementedError("the reference GAM MOJO scorer has no M-spline (bs=3) smoothers")
+    from ..models.glm.gam import _SUFFIX, _cr_matrices, _gname
+    di = model._dinfo
+    spec = model._spec
+    gcols = list(model._gam_cols)
+    rank = {0: 0, 2: 1, 1: 2}
+    order = sorted(range(len(gcols)), key=lambda g: (rank[model._bs[g]], g))
+    cen_names, nc_names, gam_set = {}, {}, set()
+    for g in range(len(gcols)):
+        nm, suf = _gname(gcols[g]), _SUFFIX[model._bs[g]]
+        Z = np.asarray(model._Z[g])
+        cen_names[g] = [f"{nm}_{suf}_{i}" for i in range(Z.shape[1])]
+        nc_names[g] = [f"{nm}_{suf}_nc_{i}" for i in range(Z.shape[0])]
+        gam_set.update(cen_names[g])
+    cats = list(di.cat_cols)
+    plain = [c for c in di.num_cols if c not in gam_set]
+    gam_cols_sorted = [n for g in order for n in cen_names[g]]
+    nums = plain + gam_cols_sorted
+    pos = {c: j for j, c in enumerate(di.num_cols)}
+    P = di.P
+    base = di.n_cat_expanded
+    offs = [0]
+    for c in cats:
+        offs.append(offs[-1] + (len(di.domains[c]) if di.use_all else len(di.domains[c]) - 1))
+    plug = list(di.plug)
+    # a missing smoother input: the model scores the basis at the column mean,
+    # so the centred columns' fill values are that basis row
+    fills = {}
+    for g in range(len(gcols)):
+        cc_ = gcols[g] if isinstance(gcols[g], tuple) else (gcols[g],)
+        import pandas as pd
+        from ..core.frame import H2OFrame
+        one = H2OFrame(pd.DataFrame({c: [model._col_means[c]] for c in cc_}))
+        Xg, _ = model._basis(one, gcols[g], model._bs[g], model._knots[g], model._orders[g], g)
+        row = (Xg @ __import__("torch").as_tensor(model._Z[g], dtype=Xg.dtype)).cpu().numpy()[0]
+        fills.update(dict(zip(cen_names[g], row.tolist())))
+    num_fill = [float(plug[pos[c]]) if c in plain else float(fills[c]) for c in nums]
+
+    def beta_blocks(b_std, icpt_std):
+        beta, icpt = di.destandardize(np.asarray(b_std, dtype=np.float64)[:P], icpt_std)
+        center = list(beta[:base]) + [float(beta[base + pos[c]]) for c in nums] + [icpt]
+        nc = list(beta[:base]) + [float(beta[base + pos[c]]) for c in plain]
+        for g in order:
+            bc = np.asarray([beta[base + pos[c]] for c in cen_names[g]])
+            nc += list(np.asarray(model._Z[g]) @ bc)
+        return center, nc + [icpt]
+
+    multi = getattr(model, "_multi", None)
+    fam = model._fam.family if multi is None else multi["kind"]
+    if multi is None:
+        b = np.asarray(model._beta_std, dtype=np.float64)
+        bc, bnc = beta_blocks(b[:P], b[P] if b.size > P else b[-1])
+        beta_kv = {"beta": bnc, "beta length per class": len(bnc), "beta_center": bc,
+                   "beta center length per class": len(bc)}
+        blobs = {}
+        cat = "Binomial" if spec.nclasses == 2 else "Regression"
+    elif multi["kind"] == "multinomial":
+        B = multi["B"].cpu().numpy().astype(np.float64)
+        b0 = multi["b0"].cpu().numpy().astype(np.float64)
+        rows_c, rows_nc = [], []
+        for c in range(B.shape[1]):
+            bc, bnc = beta_blocks(B[:P, c], b0[c])
+            rows_c.append(bc)
+            rows_nc.append(bnc)
+        beta_kv = {"beta length per class": len(rows_nc[0]), "beta center length per class": len(rows_c[0])}
+        blobs = {"beta_multinomial": _be_f8(rows_nc), "beta_multinomial_centering": _be_f8(rows_c)}
+        cat = "Multinomial"
+    else:
+        raise NotImplementedError(f"reference-layout GAM MOJO for {multi['kind']} models")
+    family = {"binomial": "bernoulli"}.get(fam, fam)
+    link = "multinomial" if multi is not None else model._fam.link
+    gs = [gcols[g] for g in order]
+    as_list = lambda c: list(c) if isinstance(c, tuple) else [c]          # noqa: E731
+    tp = [g for g in order if model._bs[g] == 1]
+    iss = [g for g in order if model._bs[g] == 2]
+    csg = [g for g in order if model._bs[g] == 0]
+    nk = [len(model._knots[g]) for g in range(len(gcols))]
+    extra = {"use_all_factor_levels": bool(di.use_all), "cats": len(cats), "cat_offsets": offs,
+             "numsCenter": len(nums), "num": len(nums) + len(gcols),
+             "mean_imputation": di.mvh == "meanimputation"}
+    if extra["mean_imputation"]:
+        extra["numNAFillsCenter"] = num_fill
+        extra["catNAFills"] = [int(di.cat_modes[c]) for c in cats]
+    extra.update(family=family, link=link)
+    if fam == "tweedie":
+        extra["tweedie_link_power"] = float(model._fam.tlp)
+    extra.update({"num_knots": nk, "num_knots_sorted": [nk[g] for g in order],
+                  "gam_column_dim": [len(as_list(c)) for c in gcols],
+                  "gam_column_dim_sorted": [len(as_list(c)) for c in gs],
+                  "num_expanded_gam_columns": sum(len(nc_names[g]) for g in order),
+                  "num_expanded_gam_columns_center": len(gam_cols_sorted)})
+    names_nc = cats + plain + [n for g in order for n in nc_names[g]]
+    extra.update({"total feature size": len(names_nc), "gamColName_dim": [len(nc_names[g]) for g in order]})
+    extra.update(beta_kv)
+    extra.update({"bs": list(model._bs), "bs_sorted": [model._bs[g] for g in order],
+                  "_d": [len(as_list(c)) for c in gs], "num_CS_col": len(csg), "num_IS_col": len(iss)})
+    if iss:
+        extra["spline_orders_sorted"] = [int(model._orders[g]) for g in order]
+        extra["spline_orders"] = [int(o) for o in model._orders]
+    if tp:
+        extra.update({"_M": [int(model._tp[g]["M"]) for g in tp], "_m": [int(model._tp[g]["m"]) for g in tp],
+                      "num_knots_TP": [nk[g] for g in tp],
+                      # the scorer's thin-plate standardisation flag
+                      "standardize": any(bool(model._tp[g]["standardize"]) for g in tp), "num_TP_col": len(tp)})
+    else:
+        extra["num_TP_col"] = 0
+    columns = cats + nums + [spec.y]
+    domains = [list(di.domains[c]) for c in cats] + [None] * len(nums) + \
+        [list(spec.response_domain) if spec.response_domain else None]
+    ini, files = _header(model, "gam", "Generalized Additive Model", cat, columns, len(cats) + len(nums),
+                         spec.nclasses, domains, "1.00", extra)
+    z.write("model.ini", ini)
+    for k_, v_ in files.items():
+        z.write(k_, v_)
+    txt = lambda rows: "\n".join(str(r) for r in rows) + "\n"                 # noqa: E731
+    z.write("gam_columns", txt([c for col in gcols for c in as_list(col)]))
+    z.write("gam_columns_sorted", txt([c for col in gs for c in as_list(col)]))
+    z.write("_names_no_centering", txt(names_nc))
+    z.write("gamColNames", txt([n for g in order for n in nc_names[g]]))
+    z.write("gamColNamesCenter", txt(gam_cols_sorted))
+    for k_, v_ in blobs.items():
+        z.write(k_, v_)
+    knot_rows, zt_rows = [], []
+    for g in order:
+        kn = np.asarray(model._knots[g], dtype=np.float64)
+        kn = kn.reshape(len(kn), -1)
+        knot_rows += [kn[:, j] for j in range(kn.shape[1])]
+        Z = np.asarray(model._Z[g], dtype=np.float64)
+        if model._bs[g] == 2:                       # I-splines are not centred: the reader skips this block
+            zt_rows += [np.zeros(nk[g])] * Z.shape[1]
+        else:
+            zt_rows += list(Z.T)
+    z.write("knots", _be_f8(knot_rows))
+    z.write("zTranspose", _be_f8(zt_rows))
+    if csg:
+        z.write("_binvD", _be_f8([r for g in csg for r in _cr_matrices(np.asarray(model._knots[g]))[0][1:-1]]))
+    if tp:
+        ints = [int(e) for g in tp for term in model._tp[g]["terms"] for e in term]
+        z.write("polynomialBasisList", np.asarray(ints, dtype=">i4").tobytes())
+        z.write("zTransposeCS", _be_f8([r for g in tp for r in np.asarray(model._tp[g]["zCS"]).T]))
+        z.write("gamColMeansRaw", _be_f8([model._tp[g]["means"] for g in tp]))
+        z.write("gamColStdRaw", _be_f8([model._tp[g]["ostd"] for g in tp]))
+
+
 _WRITERS = {"rulefit": _rulefit, "gbm": _gbm, "drf": _drf, "glm": _glm, "kmeans": _kmeans, "isolationforest": _isofor,
             "extendedisolationforest": _eif, "deeplearning": _deeplearning, "word2vec": _word2vec,
             "stackedensemble": _stackedensemble, "pca": _pca, "xgboost": _xgboost,
-            "coxph": _coxph, "targetencoder": _targetencoder, "glrm": _glrm}
+            "coxph": _coxph, "targetencoder": _targetencoder, "glrm": _glrm, "gam": _gam}
 
 
 def _write_algo(model, z):

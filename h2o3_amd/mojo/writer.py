@@ -143,9 +143,16 @@ def build_mojo(model) -> bytes:
         if algo == "gam":
             w.meta["gam"] = {"cols": model._gam_cols, "bs": model._bs, "orders": model._orders,
                              "knots": [k.tolist() for k in model._knots], "means": model._col_means,
-                             "keep": bool(model._parms.get("keep_gam_cols"))}
+                             "keep": bool(model._parms.get("keep_gam_cols")),
+                             "tp": {str(gi): {"terms": [list(e) for e in t["terms"]],
+                                              "means": [float(v) for v in t["means"]],
+                                              "ostd": [float(v) for v in t["ostd"]],
+                                              "standardize": bool(t["standardize"])}
+                                    for gi, t in getattr(model, "_tp", {}).items()}}
             for gi, Z in enumerate(model._Z):
                 w.add_array(f"gamZ{gi}", np.asarray(Z))
+            for gi, t in getattr(model, "_tp", {}).items():
+                w.add_array(f"gamZcs{gi}", np.asarray(t["zCS"]))
         if getattr(model, "_multi", None) is not None:
             m = model._multi
             w.meta["multi"] = m["kind"]

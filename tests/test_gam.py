@@ -77,3 +77,57 @@ def test_gam_multicolumn_thin_plate_and_mojo():
     p2 = m2.predict(fr).as_data_frame()["predict"].values
     pm2 = np.asarray(MojoModel(build_mojo(m2)).predict(df.drop(columns=["y"]))).reshape(-1)
     np.testing.assert_allclose(pm2, p2, atol=1e-4)
+
+
+def test_gam_reference_layout_mojo(tmp_path):
+    """GAMMojoWriter / GamMojoReader layout: smoothers in bs-sorted order
+    (cubic regression, I-spline, thin plate), beta_center on the centred
+    columns, knots / Z' / B^-1 D / zCS' / polynomial exponents as blobs; the
+    reader re-evaluates every smoother from the raw columns (cubic spline by
+    GamUtilsCubicRegression, I-splines by ISplines, thin plate by
+    GamUtilsThinPlateRegression) and scores like the model."""
+    from h2o3_amd.mojo import h2o_mojo
+    h2o.init()
+    rng = np.random.default_rng(3)
+    n = 1500
+    df = pd.DataFrame({"x1": rng.uniform(-3, 3, n), "x2": rng.uniform(0, 1, n), "x3": rng.normal(size=n),
+                       "x4": rng.normal(size=n), "g": rng.choice(["a", "b", "c"], n)})
+    eta = np.sin(2 * df.x1) + 2 * df.x2 ** 2 + 0.3 * df.x3 * df.x4 + (df.g == "b") * 0.5
+    df["y"] = eta + rng.normal(scale=0.1, size=n)
+    df["yb"] = np.where(eta + rng.logistic(size=n) * 0.3 > 0.8, "hi", "lo")
+    fr = h2o.H2OFrame(df)
+    cases = [
+        dict(family="gaussian", gam_columns=["x1", "x2"], bs=[0, 2], num_knots=[8, 5], spline_orders=[1, 3]),
+        dict(family="binomial", gam_columns=[["x3", "x4"], "x1"], bs=[1, 0], num_knots=[12, 6]),
+        dict(family="gaussian", gam_columns=["x2"], bs=[1], num_knots=[7], standardize_tp_gam_cols=True),
+    ]
+    base = df.iloc[:200].copy()
+    base.loc[base.index[5], "x1"] = 3.4                        # outside the knot range: cubic continuation
+    for i, kw in enumerate(cases):
+        test = base.copy()
+        if i != 1:
+            test.loc[test.index[::13], "x3"] = np.nan         # plain predictor NA: mean imputation
+        test.loc[test.index[::17], "g"] = None                 # categorical NA: mode imputation
+        y = "yb" if kw["family"] == "binomial" else "y"
+        m = H2OGeneralizedAdditiveEstimator(scale=[0.001] * len(kw["gam_columns"]), lambda_=0.0, **kw)
+        m.train(x=["x3", "g"] if i != 1 else ["g"], y=y, training_frame=fr)
+        mj = h2o_mojo.load(m.download_mojo(str(tmp_path / f"gam{i}"), format="h2o"))
+        assert mj.algo == "gam"
+        ours = m.predict(h2o.H2OFrame(test)).as_data_frame()
+        got = mj.predict(test)
+        if kw["family"] == "binomial":
+            np.testing.assert_allclose(got["hi"].values, ours["hi"].values, rtol=1e-4, atol=1e-5)
+        else:
+            np.testing.assert_allclose(got["predict"].values, ours["predict"].values, rtol=1e-4, atol=1e-4)
+
+
+def test_isplines_match_reference_recursion():
+    """models/glm/gam.py:is_basis equals the reference's ISplines.gamifyVal
+    (NBSplinesTypeII recursion over the filled knot sequence), inside and
+    outside the knot range."""
+    from h2o3_amd.mojo.gam_np import ispline_basis
+    knots = np.array([0.0, 0.2, 0.45, 0.7, 1.0])
+    x = np.concatenate([np.linspace(-0.2, 1.2, 29), [0.0, 0.2, 1.0]])
+    for order in (1, 2, 3):
+        np.testing.assert_allclose(is_basis(torch.as_tensor(x), knots, order)[0].numpy(),
+                                   ispline_basis(x, knots, order), atol=1e-12)

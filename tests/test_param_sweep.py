@@ -508,6 +508,9 @@ def _train(key, kw, data, tmp, extra_files_dir=None):
     if "x0x" in (tkw.get("x") or []):
         fr = fr[:, :]
         fr["x0x"] = fr["x0"] * 2.0
+    if tkw.get("_text"):
+        for k, v in list(args.items()):
+            args[k] = _resolve(v, data, tmp, key)
     if tkw.pop("_text", False):
         m = cls(**args)
         m.train(training_frame=data["text"])
