@@ -15,18 +15,33 @@ from h2o3_amd.estimators import (H2OGeneralizedLinearEstimator, H2OGradientBoost
 from h2o3_amd.mojo.pojo import to_java
 
 
+def _expr(e):
+    e = re.sub(r"\(float\) (data\[\d+\])", r"f32(\1)", e)
+    e = re.sub(r"(?<![\w.])(-?\d+\.\d+(e-?\d+)?|-?\d+e-?\d+)f\b", r"f32(\1)", e)
+    e = re.sub(r"\(int\) (\w+(?:\[[^\]]*\])?)", r"int(\1)", e)
+    for a_, b_ in (("!Double.isNaN", "not math.isnan"), ("Double.isNaN", "math.isnan"),
+                   ("Double.POSITIVE_INFINITY", "math.inf"), ("Double.NEGATIVE_INFINITY", "-math.inf"),
+                   ("Math.exp", "math.exp"), ("Math.log", "math.log"), ("Math.sqrt", "math.sqrt"),
+                   ("Math.abs", "abs"), ("Math.max", "max"), ("Math.min", "min"), ("||", " or "), ("&&", " and ")):
+        e = e.replace(a_, b_)
+    return e
+
+
 def _java_to_python(src):
-    """Translate the POJO's static tree methods, BITS arrays and score0 body."""
-    py = ["import math", "def inBits(bits, v):", "    c = int(v)", "    return 0 <= c < len(bits) and bits[c] != 0",
+    """Translate the POJO's constant arrays, static tree methods and score0
+    (the generator's fixed grammar: declarations, for loops over int ranges,
+    if / else blocks, arithmetic, Math.* calls, ternary labels)."""
+    py = ["import math", "import numpy as _np", "def f32(x):", "    return float(_np.float32(x))",
+          "def inBits(bits, v):", "    c = int(v)", "    return 0 <= c < len(bits) and bits[c] != 0",
           "def nz(v, plug):", "    return plug if math.isnan(v) else v",
           "def level(v, mode, lvl):", "    c = mode if math.isnan(v) else int(v)", "    return 1.0 if c == lvl else 0.0"]
     ind = 0
     in_fn = False
     for raw in src.splitlines():
         ln = raw.strip()
-        m = re.match(r"static final byte\[\] (BITS_\d+) = new byte\[\] \{(.*)\};", ln)
+        m = re.match(r"static final (?:byte|int|double)\[\] (\w+) = new \w+\[\] \{(.*)\};", ln)
         if m:
-            py.append(f"{m.group(1)} = [{m.group(2)}]")
+            py.append(f"{m.group(1)} = [{_expr(m.group(2))}]")
             continue
         m = re.match(r"static double (tree_\d+)\(double\[\] data\) \{", ln)
         if m or ln.startswith("public final double[] score0"):
@@ -40,13 +55,12 @@ def _java_to_python(src):
         if ln == "}" and ind == 1:
             in_fn = False
             continue
-        e = ln
-        e = re.sub(r"\(float\) (data\[\d+\])", r"f32(\1)", e)
-        e = re.sub(r"(-?\d+\.\d+(e-?\d+)?|-?\d+e-?\d+)f\b", r"f32(\1)", e)
-        e = e.replace("Double.isNaN", "math.isnan").replace("Math.exp", "math.exp").replace("Math.max", "max") \
-            .replace("Math.min", "min").replace("Double.NEGATIVE_INFINITY", "-math.inf").replace("||", " or ") \
-            .replace("&&", " and ").replace("!math.isnan", "not math.isnan")
-        e = re.sub(r"(\w+) \? (\w+) : (.*)", lambda mm: mm.group(0), e)
+        e = _expr(ln)
+        m = re.match(r"for \(int (\w+) = (.+); \1 < (.+); \1\+\+\) \{$", e)
+        if m:
+            py.append("    " * ind + f"for {m.group(1)} in range({m.group(2)}, {m.group(3)}):")
+            ind += 1
+            continue
         if e.startswith("if (") and e.endswith(") {"):
             cond = e[4:-3]
             if " ? " in cond:
@@ -61,18 +75,27 @@ def _java_to_python(src):
             ind -= 1
         elif e.startswith("return"):
             py.append("    " * ind + e.rstrip(";"))
-        elif e.startswith("double[] f = new double["):
-            k = int(re.search(r"\[(\d+)\]", e.split("=")[1]).group(1))
-            py.append("    " * ind + f"f = [0.0] * {k}")
         else:
-            stmt = e.rstrip(";").replace("double ", "")
+            m = re.match(r"(?:double|int)\[\] (\w+) = new (?:double|int)\[(.+)\];", e)
+            if m:
+                py.append("    " * ind + f"{m.group(1)} = [0.0] * ({m.group(2)})")
+                continue
+            stmt = re.sub(r"^(?:double|int) ", "", e.rstrip(";"))
             stmt = re.sub(r"(\S+) >= (\S+) \? 1 : 0", r"(1 if \1 >= \2 else 0)", stmt)
             for part in stmt.split("; "):
                 py.append("    " * ind + part.strip().rstrip(";"))
-    py.insert(1, "import numpy as _np\ndef f32(x):\n    return float(_np.float32(x))")
     ns = {}
     exec("\n".join(py), ns)
     return ns["score0"]
+
+
+def _names_domains(src):
+    names = re.findall(r'"((?:[^"\\]|\\.)*)"', re.search(r"NAMES = new String\[\] \{(.*)\};", src).group(1))
+    dl = re.search(r"DOMAINS = new String\[\]\[\] \{(.*)\};", src).group(1)
+    doms = []
+    for part in re.findall(r"null|new String\[\] \{[^}]*\}", dl):
+        doms.append(None if part == "null" else re.findall(r'"((?:[^"\\]|\\.)*)"', part))
+    return names, doms
 
 
 @pytest.fixture(scope="module")
@@ -116,3 +139,51 @@ def test_pojo_scores_like_the_model(data, algo):
     ref = m.predict(fr).as_data_frame()["yes"].values
     got = np.array([score0(list(x), [0.0, 0.0, 0.0])[2] for x in X])
     np.testing.assert_allclose(got, ref, atol=1e-5)
+
+
+@pytest.mark.parametrize("algo", ["kmeans", "pca", "deeplearning", "naivebayes", "dl_reg"])
+def test_pojo_more_algos(data, algo):
+    """K-Means / PCA / Deep Learning / Naive Bayes POJOs score like the model."""
+    from h2o3_amd.estimators import (H2ODeepLearningEstimator, H2OKMeansEstimator, H2ONaiveBayesEstimator,
+                                     H2OPrincipalComponentAnalysisEstimator)
+    fr = h2o.H2OFrame(data)
+    x = ["a", "b", "c"]
+    if algo == "kmeans":
+        m = H2OKMeansEstimator(k=3, seed=1, standardize=True)
+        m.train(x=x, training_frame=fr)
+    elif algo == "pca":
+        m = H2OPrincipalComponentAnalysisEstimator(k=2, transform="STANDARDIZE", seed=1)
+        m.train(x=x, training_frame=fr)
+    elif algo == "deeplearning":
+        m = H2ODeepLearningEstimator(hidden=[6, 5], epochs=3, seed=1, reproducible=True, activation="Tanh")
+        m.train(x=x, y="y", training_frame=fr)
+    elif algo == "dl_reg":
+        m = H2ODeepLearningEstimator(hidden=[4], epochs=3, seed=1, reproducible=True, activation="RectifierWithDropout",
+                                     hidden_dropout_ratios=[0.2])
+        m.train(x=x, y="r", training_frame=fr)
+    else:
+        m = H2ONaiveBayesEstimator(laplace=0.5)
+        m.train(x=x, y="y", training_frame=fr)
+    src = to_java(m)
+    assert "extends GenModel" in src and src.count("{") == src.count("}")
+    score0 = _java_to_python(src)
+    names, doms = _names_domains(src)
+    X = _rows(data, names[:len([n for n in names if n in data.columns and n not in ("y", "r")])],
+              {n: d for n, d in zip(names, doms) if d})
+    pred = m.predict(fr).as_data_frame()
+    if algo == "kmeans":
+        got = np.array([score0(list(r), [0.0])[0] for r in X])
+        np.testing.assert_array_equal(got.astype(int), pred["predict"].values.astype(int))
+    elif algo == "pca":
+        got = np.array([score0(list(r), [0.0, 0.0]) for r in X])
+        # PCAModel.toJavaPredictBody lets a missing numeric propagate (the
+        # in-cluster predict mean-imputes it)
+        na = data["a"].isna().values
+        assert np.isnan(got[na]).all()
+        np.testing.assert_allclose(got[~na], pred[["PC1", "PC2"]].values[~na], rtol=1e-5, atol=1e-5)
+    elif algo == "dl_reg":
+        got = np.array([score0(list(r), [0.0])[0] for r in X])
+        np.testing.assert_allclose(got, pred["predict"].values, rtol=1e-4, atol=1e-4)
+    else:
+        got = np.array([score0(list(r), [0.0, 0.0, 0.0])[2] for r in X])
+        np.testing.assert_allclose(got, pred["yes"].values, rtol=1e-4, atol=1e-5)
