@@ -200,6 +200,57 @@ def _gram_group(H, st, Pa, G):
     G += cross + cross.T
 
 
+def _overlap_ok(X, nch, grp):
+    """Split / GEMM overlap needs >1 group of chunks on a GPU (H2O3_WIDE_OVERLAP=0 turns it off)."""
+    return X.device.type == "cuda" and nch > grp and os.environ.get("H2O3_WIDE_OVERLAP", "1") == "1"
+
+
+def _pipelined_groups(split, HL, N, st, grp, Pa, G):
+    """Double-buffered row-chunk groups: the memory-bound split kernels of
+    group g+1 run on a side stream while the compute-bound batched GEMM of
+    group g runs on the current stream; events order each buffer's reuse
+    (split g+2 waits for GEMM g) and the GEMM of g for its splits."""
+    main = torch.cuda.current_stream()
+    side = _side_stream(HL.device)
+    bufs = [HL, torch.empty_like(HL)]
+    side.wait_stream(main)                       # inputs written on the main stream
+    gemm_done = [None, None]
+    nch = -(-N // st)
+    groups = [list(range(g0, min(g0 + grp, nch))) for g0 in range(0, nch, grp)]
+    for gi, chunks in enumerate(groups):
+        b = gi & 1
+        buf = bufs[b]
+        with torch.cuda.stream(side):
+            if gemm_done[b] is not None:
+                side.wait_event(gemm_done[b])
+            sid = ctypes.c_void_p(side.cuda_stream)
+            for j, i in enumerate(chunks):
+                a = i * st
+                r = min(st, N - a)
+                split(i, a, r, buf, j, sid)
+                if r < st:
+                    buf[j * st + r:(j + 1) * st].zero_()
+            ready = torch.cuda.Event()
+            ready.record(side)
+        main.wait_event(ready)
+        _gram_group(buf[:len(chunks) * st], st, Pa, G)
+        ev = torch.cuda.Event()
+        ev.record(main)
+        gemm_done[b] = ev
+        buf.record_stream(side)
+    main.wait_stream(side)                        # deviance partials written by the last splits
+
+
+_SIDE = {}
+
+
+def _side_stream(dev):
+    k = str(dev)
+    if k not in _SIDE:
+        _SIDE[k] = torch.cuda.Stream(device=dev)
+    return _SIDE[k]
+
+
 def _wide_mode():
     return os.environ.get("H2O3_WIDE_GRAM", "bf3")
 
@@ -222,15 +273,21 @@ def gram_aug_bf3(X, W, z, P, step=1 << 19):
     HL = torch.empty((grp * st, 2 * Pa), dtype=torch.bfloat16, device=X.device)
     G = torch.zeros((Pa, Pa), dtype=torch.float64, device=X.device)
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    for i, a in enumerate(range(0, N, st)):
-        r = min(st, N - a)
-        j = i % grp
+    def split(i, a, r, buf, j, strm):
         rc = lib.h2o_gram_split(ctypes.c_void_p(X.data_ptr() + a * ldx * 4), ldx, P, Pa,
                                 ctypes.c_void_p(0 if W32 is None else W32.data_ptr() + a * 4),
                                 ctypes.c_void_p(0 if z32 is None else z32.data_ptr() + a * 4), r,
-                                ctypes.c_void_p(HL.data_ptr() + j * st * 2 * Pa * 2), stream)
+                                ctypes.c_void_p(buf.data_ptr() + j * st * 2 * Pa * 2), strm)
         if rc != 0:
             raise RuntimeError(f"h2o_gram_split failed: {rc}")
+
+    if _overlap_ok(X, nch, grp):
+        _pipelined_groups(split, HL, N, st, grp, Pa, G)
+        return G
+    for i, a in enumerate(range(0, N, st)):
+        r = min(st, N - a)
+        j = i % grp
+        split(i, a, r, HL, j, stream)
         if r < st:
             HL[j * st + r:(j + 1) * st].zero_()
         if j == grp - 1 or i == nch - 1:
@@ -265,16 +322,22 @@ def glm_wide_irls(X, P, beta, b0, y, wprior=None, offset=None, codes=(1, 1), tvp
     def off(t, a):
         return ctypes.c_void_p(0 if t is None else t.data_ptr() + a * 4)
 
-    for i, a in enumerate(range(0, N, st)):
-        r = min(st, N - a)
-        j = i % grp
+    def split(i, a, r, buf, j, strm):
         rc = lib.h2o_glm_wide_split(ctypes.c_void_p(X.data_ptr() + a * ldx * 4), ldx, P, Pa, r, _ptr(bt),
                                     float(b0), off(keep[0], a), off(keep[1], a), off(keep[2], a), int(codes[0]),
                                     int(codes[1]), float(tvp), float(theta),
-                                    ctypes.c_void_p(HL.data_ptr() + j * st * 2 * Pa * 2), _ptr(dev[i]), blocks,
-                                    stream)
+                                    ctypes.c_void_p(buf.data_ptr() + j * st * 2 * Pa * 2), _ptr(dev[i]), blocks,
+                                    strm)
         if rc != 0:
             raise RuntimeError(f"h2o_glm_wide_split failed: {rc}")
+
+    if _overlap_ok(X, nch, grp):
+        _pipelined_groups(split, HL, N, st, grp, Pa, G)
+        return G, dev.sum()
+    for i, a in enumerate(range(0, N, st)):
+        r = min(st, N - a)
+        j = i % grp
+        split(i, a, r, HL, j, stream)
         if r < st:
             HL[j * st + r:(j + 1) * st].zero_()
         if j == grp - 1 or i == nch - 1:
