@@ -201,8 +201,9 @@ def _gram_group(H, st, Pa, G):
 
 
 def _overlap_ok(X, nch, grp):
-    """Split / GEMM overlap needs >1 group of chunks on a GPU (H2O3_WIDE_OVERLAP=0 turns it off)."""
-    return X.device.type == "cuda" and nch > grp and os.environ.get("H2O3_WIDE_OVERLAP", "1") == "1"
+    """Split / GEMM overlap (opt-in, H2O3_WIDE_OVERLAP=1: measured slower at 12.5M x 1000, the split
+    kernels steal CUs from the GEMM -- profiles/glm_wide_overlap_ab_r4.txt); needs > 1 group of chunks."""
+    return X.device.type == "cuda" and nch > grp and os.environ.get("H2O3_WIDE_OVERLAP", "0") == "1"
 
 
 def _pipelined_groups(split, HL, N, st, grp, Pa, G):
