@@ -734,7 +734,11 @@ def create_app(flow_dir: str | None = None, serve: bool = True) -> FastAPI:
     def builder_info(p, r, algo):
         cls = _algo_cls(algo)
         est = cls()
-        params = [S._param_entry(k, v, v) for k, v in est._parms.items()]
+        from ..models.param_meta import META
+        from ..models.param_tables import PARAMS
+        names = PARAMS.get(cls.__name__) or list(est._parms)
+        pm = META.get(cls.__name__, {})
+        params = [S._param_entry(k, est._parms.get(k), est._parms.get(k), pm.get(k, {})) for k in names]
         return {"__meta": S.meta("ModelBuildersV3", "Iced"),
                 "model_builders": {algo: {"algo": algo, "algo_full_name": cls.__name__, "parameters": params,
                                           "can_build": ["Binomial", "Multinomial", "Regression"],

@@ -543,7 +543,40 @@ def metrics_v3(mm, model=None, frame_id=None, category=None) -> dict | None:
 
 
 # ------------------------------------------------------------ models
-def _param_entry(name, actual, default):
+_CRITICAL = {"model_id", "training_frame", "validation_frame", "nfolds", "response_column", "ignored_columns",
+             "ntrees", "max_depth", "learn_rate", "family", "solver", "alpha", "lambda_", "lambda_search", "k",
+             "hidden", "epochs", "activation", "distribution", "gam_columns", "base_models", "metalearner_algorithm",
+             "x", "y", "max_iterations", "transform", "pca_method", "loss", "init", "estimator", "treatment_column",
+             "uplift_metric", "vec_size", "stop_column", "start_column"}
+_EXPERT = ("checkpoint", "export_", "_dir", "custom_", "keep_cross_validation", "max_runtime_secs", "score_",
+           "calibrat", "gainslift", "auc_type", "build_tree_one_node", "in_training", "max_confusion", "quiet_mode",
+           "diagnostics", "verbose", "max_after_balance", "class_sampling", "pred_noise", "_eps", "epsilon",
+           "single_node", "replicate", "shuffle", "reproducible", "sparse", "col_major", "elastic", "fast_mode",
+           "force_load_balance", "initial_", "average_activation", "sparsity_beta", "max_categorical_features",
+           "mini_batch", "use_all_factor_levels", "non_negative", "gradient_epsilon", "objective_epsilon",
+           "beta_epsilon", "prior", "cold_start", "dispersion", "fix_", "generate_", "obj_reg", "max_active",
+           "interaction_pairs", "plug_values", "rand_family", "rand_link", "startval", "theta")
+
+
+def _ref_type(t, actual):
+    """Reference client type string (h2o-py docstrings) -> the REST schema type name."""
+    t = (t or "").replace(" ", "")
+    if t.startswith("Literal["):
+        return "enum"
+    if "H2OFrame" in t:
+        return "Key<Frame>"
+    if "H2OEstimator" in t or "ModelBase" in t:
+        return "Key<Model>"
+    m = {"int": "int", "float": "double", "bool": "boolean", "str": "string", "List[str]": "string[]",
+         "List[int]": "int[]", "List[float]": "double[]", "dict": "KeyValue[]", "List[List[str]]": "string[][]"}
+    if t in m:
+        return m[t]
+    if t.startswith("List[") or t.startswith("Union[None,List"):
+        return "string[]"
+    return None
+
+
+def _param_entry(name, actual, default, meta_=None):
     def enc(v):
         if hasattr(v, "frame_id") and hasattr(v, "names"):
             return key(v.frame_id)
@@ -556,10 +589,17 @@ def _param_entry(name, actual, default):
     typ = ("boolean" if isinstance(actual, bool) else "int" if isinstance(actual, int) else
            "double" if isinstance(actual, float) else "string[]" if isinstance(actual, (list, tuple)) else
            "Key<Frame>" if isinstance(a, dict) and a.get("type") == "Key<Frame>" else "string")
-    return {"__meta": meta("ModelParameterSchemaV3", "Iced"), "name": name, "label": name, "help": name,
-            "required": False, "type": typ, "default_value": dv, "actual_value": a, "input_value": a,
-            "level": "critical", "values": [], "is_member_of_frames": [], "is_mutually_exclusive_with": [],
-            "gridable": False}
+    help_, values, level = name, [], "critical"
+    if meta_ is not None:
+        typ = _ref_type(meta_.get("type"), actual) or typ
+        values = list(meta_.get("values") or [])
+        help_ = meta_.get("help") or name
+        level = "critical" if name in _CRITICAL else \
+            "expert" if any(x in name for x in _EXPERT) else "secondary"
+    return {"__meta": meta("ModelParameterSchemaV3", "Iced"), "name": name, "label": name, "help": help_,
+            "required": name in ("training_frame",) and meta_ is not None, "type": typ, "default_value": dv,
+            "actual_value": a, "input_value": a, "level": level, "values": values, "is_member_of_frames": [],
+            "is_mutually_exclusive_with": [], "gridable": typ in ("int", "double", "enum", "boolean")}
 
 
 def model_v3(mid, m) -> dict:

@@ -212,3 +212,56 @@ def test_reference_flow_packs_run_on_synthetic_data(app, tmp_path):
     bad = [(r["notebook"], r["errors"]) for r in res if r.get("failed")]
     assert not bad, bad
     assert sum(r["cells"] for r in res) > 50
+
+
+def test_flow_page_script_and_charts(tmp_path):
+    """The Flow page's script parses (node --check) and its inline-SVG charts
+    render a scoring-history polyline, variable-importance bars and a ROC
+    curve from ModelSchemaV3-shaped tables."""
+    import re
+    import shutil
+    import subprocess
+    from pathlib import Path
+    node = shutil.which("node")
+    if node is None:
+        pytest.skip("no node.js")
+    src = (Path(__file__).resolve().parents[1] / "h2o3_amd" / "server" / "static" / "flow.html").read_text()
+    js = re.search(r"<script>(.*)</script>", src, re.S).group(1)
+    (tmp_path / "flow.js").write_text(js)
+    subprocess.run([node, "--check", str(tmp_path / "flow.js")], check=True)
+    body = js[:js.rindex("(async () => {")]               # function definitions, not the page bootstrap
+    harness = body + r'''
+const T = (name, cols) => ({__meta: {schema_type: "TwoDimTable"}, name,
+  columns: Object.keys(cols).map(n => ({name: n})), data: Object.values(cols)});
+const host = {innerHTML: "", appendChild() {}};
+global.document = {createElement: () => ({append() {}, appendChild() {}, set onclick(f) {}, className: ""})};
+const m = {model_id: {name: "m1"}, output: {
+  scoring_history: T("sh", {number_of_trees: [0, 1, 2, 3], training_logloss: [0.69, 0.5, 0.4, 0.35],
+                            validation_logloss: [0.69, 0.55, 0.47, 0.44]}),
+  variable_importances: T("vi", {variable: ["a", "b"], scaled_importance: [1.0, 0.4]}),
+  training_metrics: {AUC: 0.9, thresholds_and_metric_scores: T("thr", {fpr: [0, 0.1, 0.5, 1], tpr: [0, 0.6, 0.9, 1]})}}};
+modelCharts(host, m);
+console.log(JSON.stringify({poly: (host.innerHTML.match(/<polyline/g) || []).length,
+                            rect: (host.innerHTML.match(/<rect/g) || []).length,
+                            roc: host.innerHTML.includes("ROC (AUC 0.900000)")}));
+'''
+    (tmp_path / "h.js").write_text(harness)
+    out = subprocess.run([node, str(tmp_path / "h.js")], check=True, capture_output=True, text=True).stdout
+    import json
+    r = json.loads(out.strip().splitlines()[-1])
+    assert r == {"poly": 3, "rect": 2, "roc": True}
+
+
+def test_model_builder_parameter_metadata(app):
+    """/3/ModelBuilders/{algo}: the reference client's parameter list with
+    typed entries (enum values, help, critical / secondary / expert levels)
+    that Flow's buildModel form renders."""
+    from fastapi.testclient import TestClient
+    c = TestClient(app)
+    ps = c.get("/3/ModelBuilders/gbm").json()["model_builders"]["gbm"]["parameters"]
+    by = {p["name"]: p for p in ps}
+    assert by["distribution"]["type"] == "enum" and "bernoulli" in by["distribution"]["values"]
+    assert by["ntrees"]["type"] == "int" and by["ntrees"]["level"] == "critical"
+    assert by["training_frame"]["type"] == "Key<Frame>"
+    assert by["sample_rate"]["help"].startswith("Row sample rate")
+    assert {p["level"] for p in ps} == {"critical", "secondary", "expert"}
