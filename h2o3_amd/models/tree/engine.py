@@ -602,6 +602,20 @@ class TreeGrower:
         k, _ = self._sample_k(depth)
         return env == "1" or chunked or 4 * k <= self.bd.F
 
+    def _all_levels_direct(self, mode):
+        """True when every level of the tree takes the device pair path (a
+        fixed per-node column sample of at most a quarter of the features),
+        so no level-histogram kernel ever reads the response by row."""
+        p = self.p
+        if mode != 0 or self.dev.type != "cuda" or self.bd.codes_col is None or p.criterion.startswith("uplift"):
+            return False
+        if tree_ops.env("H2O3_PAIR_DIRECT", "auto") == "0":
+            return False
+        if not (p.mtries is not None and p.mtries > 0) or p.col_sample_rate_change_per_level != 1.0:
+            return False
+        k, _ = self._sample_k(0)
+        return k < self.bd.F and 4 * k <= self.bd.F
+
     def _pair_direct_splits(self, ridx, va, vb, mode, f_st, f_ct, cm):
         """Best split of every frontier node from row-direct histograms of its
         sampled (node, feature) pairs only: pair histograms built from the rows
@@ -1188,7 +1202,10 @@ class TreeGrower:
         self._va_eff = None
         quad = self.bd.code_bytes == 1 and self.bd.Bs <= 256 and self.bd.Fp % 16 == 0 and \
             tree_ops.env("H2O3_HIST_KERNEL", "quad") == "quad"
-        if self._unit_w and not self.use_payload and quad:
+        # every level on the row-direct pair path (DRF's mtries << F): the
+        # pair kernels read the position-ordered payload at any histogram width
+        all_direct = self._all_levels_direct(mode) and tree_ops.env("H2O3_DRF_POSV", "1") == "1"
+        if self._unit_w and not self.use_payload and (quad or all_direct):
             self._va_eff = torch.where(vb > 0, va, torch.full_like(va, float("nan"))) if vb is not None else va
         self._pos1 = None
         if self._va_eff is not None and tree_ops.env("H2O3_POSV", "1") == "1" and \

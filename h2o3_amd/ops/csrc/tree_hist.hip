@@ -1594,9 +1594,15 @@ __global__ __launch_bounds__(256) void pair_hist_kernel(const CodeT* __restrict_
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int vi = POSV ? min(p0 + u * 256, end - 1) : r[u];
-      c[u] = (unsigned int)cc[r[u]];
       xa[u] = va[vi];
       xb[u] = HAS_VB ? vb[vi] : 1.f;
+    }
+    // zero-weight rows (out-of-bag / NaN response) skip their code gather:
+    // DRF trees carry the whole frame through the partition
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const bool live = MODE != 0 || (HAS_VB ? xb[u] != 0.f : xa[u] == xa[u]);
+      c[u] = live ? (unsigned int)cc[r[u]] : 0u;
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -1682,8 +1688,13 @@ __global__ __launch_bounds__(256) void pair_hist_multi_kernel(const CodeT* __res
       const int vi = POSV ? min(p0 + u * 256, end - 1) : r[u];
       xa[u] = va[vi];
       xb[u] = HAS_VB ? vb[vi] : 1.f;
+    }
+    // zero-weight rows (out-of-bag / NaN response) skip their KP code gathers
 #pragma unroll
-      for (int j = 0; j < KP; ++j) c[u][j] = (unsigned int)cc[j][r[u]];
+    for (int u = 0; u < U; ++u) {
+      const bool live = MODE != 0 || (HAS_VB ? xb[u] != 0.f : xa[u] == xa[u]);
+#pragma unroll
+      for (int j = 0; j < KP; ++j) c[u][j] = live ? (unsigned int)cc[j][r[u]] : 0u;
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
