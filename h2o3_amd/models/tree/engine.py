@@ -790,9 +790,12 @@ class TreeGrower:
         if n <= 0:
             return
         fl = pfeat.long()
+        if getattr(self, "_nbins_t", None) is None:
+            self._nbins_t = torch.as_tensor(np.asarray(self.bd.nbins[:self.bd.F], dtype=np.int32), device=dev)
         best_k = self._pairs_native(Hp.view(1, P, Bs, 2), torch.zeros(P, dtype=torch.long, device=dev),
                                     torch.arange(P, device=dev), self.is_cat_t[fl], self.mono_t[fl],
-                                    wyy_n.repeat_interleave(k) if wyy_n is not None else None, raw=True)
+                                    wyy_n.repeat_interleave(k) if wyy_n is not None else None, raw=True,
+                                    pbins=self._nbins_t[fl])
         rc = lib.h2o_pair_select(ctypes.c_void_p(Hp.data_ptr()), n, Bs, k, ctypes.c_void_p(best_k.data_ptr()),
                                  ctypes.c_void_p(pfeat.data_ptr()), ctypes.c_void_p(self._fcat_u8.data_ptr()),
                                  1 if p.criterion == "xgb" else 0, min_w2, 12, ctypes.c_void_p(pk.data_ptr()),
@@ -968,8 +971,10 @@ class TreeGrower:
         return torch.where((allg > se_before * p.min_split_improvement) & (se_before > 0), allg,
                            torch.full_like(allg, NEG_INF))
 
-    def _pairs_native(self, H, fslot, node_i, pcat, mono_p, node_wyy, raw=False):
-        """(best gain, k) per pair from the HIP pair kernel."""
+    def _pairs_native(self, H, fslot, node_i, pcat, mono_p, node_wyy, raw=False, pbins=None):
+        """(best gain, k) per pair from the HIP pair kernel.  pbins (bins of each
+        pair's feature): pairs of narrow (< 256-bin) features are scored by the
+        256-wide kernel instance, the rest at the full histogram width."""
         import ctypes
         from ...ops import _native
         p = self.p
@@ -990,6 +995,21 @@ class TreeGrower:
 
         def ptr(t):
             return ctypes.c_void_p(0 if t is None else t.data_ptr())
+        if pbins is not None and Bs - 1 > 256 and tree_ops.env("H2O3_PAIR_NARROW", "1") == "1":
+            if not getattr(lib, "_typed_pairs2", False):
+                cv, ci, cd = ctypes.c_void_p, ctypes.c_int, ctypes.c_double
+                lib.h2o_cat_pairs2.argtypes = [cv, ci, ci, ci, ci, cv, cv, cv, cv, cv, cd, cd, cd, cd, cd, ci, cv,
+                                               cv, ci, cv, cv]
+                lib._typed_pairs2 = True
+            lists = torch.empty(2 * P + 2, dtype=torch.int32, device=H.device)
+            pb = pbins.to(torch.int32).contiguous()
+            rc = lib.h2o_cat_pairs2(ptr(H), n, Bs, C, P, ptr(pf), ptr(pn), ptr(pc), ptr(pm), ptr(wyy),
+                                    float(p.min_rows), float(p.min_split_improvement), float(p.reg_lambda),
+                                    float(p.reg_alpha), float(p.gamma), 1 if p.criterion == "xgb" else 0, ptr(res),
+                                    ptr(pb), 255, ptr(lists), tree_ops._stream())
+            if rc != 0:
+                raise RuntimeError(f"h2o_cat_pairs2 failed: {rc}")
+            return res if raw else (res[:, 0].contiguous(), res[:, 1].to(torch.long))
         rc = lib.h2o_cat_pairs(ptr(H), n, Bs, C, P, ptr(pf), ptr(pn), ptr(pc), ptr(pm), ptr(wyy),
                                float(p.min_rows), float(p.min_split_improvement), float(p.reg_lambda),
                                float(p.reg_alpha), float(p.gamma), 1 if p.criterion == "xgb" else 0, ptr(res),

@@ -309,7 +309,8 @@ __global__ __launch_bounds__(256) void cat_pair_kernel(const double* __restrict_
                                                        const float* __restrict__ pmono,
                                                        const double* __restrict__ node_wyy, double min_rows,
                                                        double msi, double lam, double alpha, double gamma,
-                                                       double* __restrict__ out) {
+                                                       double* __restrict__ out, const int* __restrict__ plist,
+                                                       const int* __restrict__ pcount, int Bscan) {
   __shared__ double sk[BP];   // sort key, then channel-0 prefix sums
   __shared__ double s1[BP];   // channel-1 prefix sums
   __shared__ int si[BP];      // bin index (sort payload)
@@ -317,15 +318,24 @@ __global__ __launch_bounds__(256) void cat_pair_kernel(const double* __restrict_
   __shared__ int red_k[4];
   __shared__ int nfin[256];   // per-thread count of occupied levels, then its exclusive scan
   constexpr int PER = BP / 256;
-  const int p = blockIdx.x;
+  // plist: this launch scores the pcount[0] pairs listed (narrow / wide
+  // split of a level's pairs); the grid is an upper bound, the rest exit
+  int p = blockIdx.x;
+  if (plist != nullptr) {
+    if (p >= pcount[0]) return;
+    p = plist[p];
+  }
   const int tid = threadIdx.x;
-  const int B = Bs - 1;
+  const int B = Bs - 1;       // NA bin index; k = i | nt + i | 2 nt over the full width
+  // bins scanned: a feature with at most Bscan bins leaves [Bscan, B) empty;
+  // thresholds there repeat the all-left partition and lose the lowest-k tie
+  const int Bsc = min(B, Bscan);
   const double* h = H + ((size_t)pf[p] * n + pn[p]) * (size_t)Bs * C;
   const bool cat = pcat[p] != 0;
   int M = BP;                 // sorted prefix length
   if (!cat) {
     for (int b = tid; b < BP; b += 256) {
-      sk[b] = b < B ? (double)b : INFINITY;
+      sk[b] = b < Bsc ? (double)b : INFINITY;
       si[b] = b;
     }
   } else {
@@ -340,7 +350,7 @@ __global__ __launch_bounds__(256) void cat_pair_kernel(const double* __restrict_
     for (int e = 0; e < PER; ++e) {
       const int b = tid * PER + e;
       double kk = INFINITY;
-      if (b < B) {
+      if (b < Bsc) {
         if (CRIT == 1) {
           const double g = h[(size_t)b * C], hh = h[(size_t)b * C + 1];
           kk = hh > 0 ? g / hh : INFINITY;
@@ -399,7 +409,7 @@ __global__ __launch_bounds__(256) void cat_pair_kernel(const double* __restrict_
   for (int e = 0; e < PER; ++e) {
     const int b = tid * PER + e;
     double v0 = 0, v1 = 0;
-    if (b < B) {
+    if (b < Bsc) {
       const int j = si[b];
       v0 = h[(size_t)j * C];
       v1 = h[(size_t)j * C + 1];
@@ -440,8 +450,9 @@ __global__ __launch_bounds__(256) void cat_pair_kernel(const double* __restrict_
   const int nt = B - 1;
   double bg = -INFINITY;
   int bk = 0x7fffffff;
+  const int nts = min(nt, Bsc);
   if (!dead) {
-    for (int i = tid; i < nt; i += 256) {
+    for (int i = tid; i < nts; i += 256) {
       const double lw = sk[i], ly = s1[i];
       const double rw = tw - lw, ry = ty - ly;
       {
@@ -490,11 +501,12 @@ __global__ __launch_bounds__(256) void cat_pair_kernel(const double* __restrict_
 template <int CRIT>
 static int cat_pair_launch(int BP, dim3 g, hipStream_t s, const double* H, int n, int Bs, int C, const int* pf,
                            const int* pn, const unsigned char* pcat, const float* pmono, const double* wyy,
-                           double min_rows, double msi, double lam, double alpha, double gamma, double* out) {
+                           double min_rows, double msi, double lam, double alpha, double gamma, double* out,
+                           const int* plist = nullptr, const int* pcount = nullptr, int Bscan = 1 << 30) {
 #define CPK(bp)                                                                                                \
   case bp:                                                                                                     \
     hipLaunchKernelGGL((cat_pair_kernel<CRIT, bp>), g, dim3(256), 0, s, H, n, Bs, C, pf, pn, pcat, pmono, wyy, \
-                       min_rows, msi, lam, alpha, gamma, out);                                                 \
+                       min_rows, msi, lam, alpha, gamma, out, plist, pcount, Bscan);                           \
     return 0;
   switch (BP) {
     CPK(256) CPK(512) CPK(1024) CPK(2048) CPK(4096)
@@ -519,6 +531,64 @@ extern "C" int h2o_cat_pairs(const double* H, int n, int Bs, int C, int P, const
                                                   msi, lam, alpha, gamma, out)
                            : cat_pair_launch<0>(BP, g, s, H, n, Bs, C, pf, pn, pcat, pmono, node_wyy, min_rows,
                                                 msi, lam, alpha, gamma, out);
+  if (rc) return rc;
+  return (int)hipGetLastError();
+}
+
+// Narrow / wide pair lists for h2o_cat_pairs2: pairs whose feature has at
+// most narrow_max bins go to lists[0..cnt0), the others to lists[P..P+cnt1)
+// (wave-aggregated atomics; order inside a list is irrelevant -- every pair
+// writes its own out[2p]).
+__global__ __launch_bounds__(256) void pair_lists_kernel(const int* __restrict__ pbins, int P, int narrow_max,
+                                                         int* __restrict__ lists, int* __restrict__ cnt) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = p < P;
+  const bool nar = live && pbins[p] <= narrow_max;
+  const int lane = threadIdx.x & 63;
+  const unsigned long long act = __ballot(live);
+  if (act == 0ull) return;
+  const unsigned long long bn = __ballot(nar);
+  const unsigned long long bw = act & ~bn;
+  const int leader = __ffsll((long long)act) - 1;
+  int baseN = 0, baseW = 0;
+  if (lane == leader) {
+    baseN = atomicAdd(cnt, (int)__popcll(bn));
+    baseW = atomicAdd(cnt + 1, (int)__popcll(bw));
+  }
+  baseN = __shfl(baseN, leader, 64);
+  baseW = __shfl(baseW, leader, 64);
+  const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  if (!live) return;
+  if (nar) lists[baseN + __popcll(bn & below)] = p;
+  else lists[P + baseW + __popcll(bw & below)] = p;
+}
+
+// h2o_cat_pairs with the level's pairs split by width: pairs of features with
+// <= narrow_max (< 256) bins run the BP = 256 instance (a quarter of the LDS
+// scans and scoring of the 1024-wide one), the rest the full-width instance.
+// pbins[P]: bins of each pair's feature; lists: int[2P + 2] scratch.
+extern "C" int h2o_cat_pairs2(const double* H, int n, int Bs, int C, int P, const int* pf, const int* pn,
+                              const unsigned char* pcat, const float* pmono, const double* node_wyy,
+                              double min_rows, double msi, double lam, double alpha, double gamma, int crit,
+                              double* out, const int* pbins, int narrow_max, int* lists, hipStream_t s) {
+  if (P <= 0) return 0;
+  if (C < 2 || Bs < 2 || narrow_max < 1 || narrow_max > 255) return -1;
+  int BP = 256;
+  while (BP < Bs - 1) BP <<= 1;
+  if (BP > 4096) return -2;
+  int* cnt = lists + 2 * (size_t)P;
+  hipMemsetAsync(cnt, 0, 2 * sizeof(int), s);
+  hipLaunchKernelGGL(pair_lists_kernel, dim3((P + 255) / 256), dim3(256), 0, s, pbins, P, narrow_max, lists, cnt);
+  const dim3 g(P);
+  int rc = crit == 1 ? cat_pair_launch<1>(256, g, s, H, n, Bs, C, pf, pn, pcat, pmono, node_wyy, min_rows, msi,
+                                          lam, alpha, gamma, out, lists, cnt, narrow_max)
+                     : cat_pair_launch<0>(256, g, s, H, n, Bs, C, pf, pn, pcat, pmono, node_wyy, min_rows, msi,
+                                          lam, alpha, gamma, out, lists, cnt, narrow_max);
+  if (rc) return rc;
+  rc = crit == 1 ? cat_pair_launch<1>(BP, g, s, H, n, Bs, C, pf, pn, pcat, pmono, node_wyy, min_rows, msi, lam,
+                                      alpha, gamma, out, lists + P, cnt + 1, Bs - 1)
+                 : cat_pair_launch<0>(BP, g, s, H, n, Bs, C, pf, pn, pcat, pmono, node_wyy, min_rows, msi, lam,
+                                      alpha, gamma, out, lists + P, cnt + 1, Bs - 1);
   if (rc) return rc;
   return (int)hipGetLastError();
 }

@@ -796,3 +796,43 @@ def test_gbm_all_binary_frame_gpu_matches_cpu():
     h2o.init(device="cuda:0", verbose=False)
     assert out["cuda:0"][1] == out["cpu"][1]
     assert abs(out["cuda:0"][0] - out["cpu"][0]) < 1e-5
+
+
+@pytest.mark.parametrize("classify", [False, True])
+def test_drf_pair_path_narrow_scoring_and_posv_same_trees(classify, monkeypatch):
+    """DRF on the row-direct pair path with a 1000-level categorical (1025-bin
+    histograms) and numeric columns of <= 255 bins: scoring the narrow pairs
+    with the 256-wide kernel instance (H2O3_PAIR_NARROW) and carrying the
+    response as the position-ordered payload (H2O3_DRF_POSV) grow exactly the
+    trees of the reference configuration."""
+    _need_gpu()
+    import pandas as pd
+    import h2o3_amd
+    from h2o3_amd.estimators import H2ORandomForestEstimator
+    h2o3_amd.init(device="cuda:0", verbose=False)
+    rng = np.random.RandomState(3)
+    n = 30000
+    F = 24
+    X = rng.randn(n, F).astype(np.float32)
+    df = pd.DataFrame(X, columns=[f"x{i}" for i in range(F)])
+    df.loc[::11, "x3"] = np.nan
+    lv = rng.randint(0, 1000, n)
+    df["c"] = pd.Categorical([f"L{v}" for v in lv])
+    eff = rng.randn(1000)
+    yv = X[:, 0] + X[:, 5] * X[:, 9] + eff[lv] + 0.3 * rng.randn(n)
+    df["y"] = np.where(yv > 0.3, "a", "b") if classify else yv
+    fr = h2o3_amd.H2OFrame(df)
+    if classify:
+        fr["y"] = fr["y"].asfactor()
+    out = []
+    for narrow, posv in (("0", "0"), ("1", "1")):
+        monkeypatch.setenv("H2O3_PAIR_NARROW", narrow)
+        monkeypatch.setenv("H2O3_DRF_POSV", posv)
+        m = H2ORandomForestEstimator(ntrees=3, max_depth=14, seed=11, mtries=5)
+        m.train(y="y", training_frame=fr)
+        out.append(m)
+    for t0, t1 in zip(out[0]._forest.trees, out[1]._forest.trees):
+        assert t0.n_nodes == t1.n_nodes
+        np.testing.assert_array_equal(np.asarray(t0.feat), np.asarray(t1.feat))
+        np.testing.assert_array_equal(np.asarray(t0.thr), np.asarray(t1.thr))
+        np.testing.assert_allclose(np.asarray(t0.value), np.asarray(t1.value), rtol=1e-9, atol=1e-12)
