@@ -652,6 +652,17 @@ class TreeGrower:
         k, _ = self._sample_k(depth)
         return env == "1" or chunked or 4 * k <= self.bd.F
 
+    def _narrow_bins(self):
+        """Per-feature code counts [F] int32 on the device when the pair path
+        may bound its work by each feature's bins (histograms wider than 256
+        bins: H2O3_PAIR_NARROW), else None."""
+        if self.dev.type != "cuda" or self.bd.Bs - 1 <= 256 or tree_ops.env("H2O3_PAIR_NARROW", "1") != "1":
+            return None
+        if getattr(self, "_nbins_t", None) is None:
+            nb = np.minimum(np.asarray(self.bd.nbins[:self.bd.F], dtype=np.int64), self.bd.Bs - 1)
+            self._nbins_t = torch.as_tensor(nb.astype(np.int32), device=self.dev)
+        return self._nbins_t
+
     def _all_levels_direct(self, mode):
         """True when every level of the tree takes the device pair path (a
         fixed per-node column sample of at most a quarter of the features),
@@ -744,7 +755,7 @@ class TreeGrower:
             sl = sel[a:b]
             with phase("tree.hist"), phase("tree.hist.pairs"):
                 Hp, wyy_n, pfeat = tree_ops.pair_hist_dev(bd, ridx, va, vb, mode, st[a:b], ct[a:b], sl, self._vmax,
-                                                          posv=posv)
+                                                          posv=posv, fbins=self._narrow_bins())
             nb = b - a
             if self.W > 1:
                 # node-sharded reduction: every rank receives the summed pair
@@ -790,17 +801,27 @@ class TreeGrower:
         if n <= 0:
             return
         fl = pfeat.long()
-        if getattr(self, "_nbins_t", None) is None:
-            self._nbins_t = torch.as_tensor(np.asarray(self.bd.nbins[:self.bd.F], dtype=np.int32), device=dev)
+        nb_t = self._narrow_bins()
         best_k = self._pairs_native(Hp.view(1, P, Bs, 2), torch.zeros(P, dtype=torch.long, device=dev),
                                     torch.arange(P, device=dev), self.is_cat_t[fl], self.mono_t[fl],
                                     wyy_n.repeat_interleave(k) if wyy_n is not None else None, raw=True,
-                                    pbins=self._nbins_t[fl])
-        rc = lib.h2o_pair_select(ctypes.c_void_p(Hp.data_ptr()), n, Bs, k, ctypes.c_void_p(best_k.data_ptr()),
-                                 ctypes.c_void_p(pfeat.data_ptr()), ctypes.c_void_p(self._fcat_u8.data_ptr()),
-                                 1 if p.criterion == "xgb" else 0, min_w2, 12, ctypes.c_void_p(pk.data_ptr()),
-                                 ctypes.c_void_p(mask.data_ptr()), ctypes.c_void_p(feat_i.data_ptr()),
-                                 tree_ops._stream())
+                                    pbins=nb_t[fl] if nb_t is not None else None)
+        if nb_t is not None:
+            if not getattr(lib, "_typed_psel2", False):
+                cv, ci, cd = ctypes.c_void_p, ctypes.c_int, ctypes.c_double
+                lib.h2o_pair_select2.argtypes = [cv, ci, ci, ci, cv, cv, cv, ci, cd, ci, cv, cv, cv, cv, cv]
+                lib._typed_psel2 = True
+            rc = lib.h2o_pair_select2(ctypes.c_void_p(Hp.data_ptr()), n, Bs, k, ctypes.c_void_p(best_k.data_ptr()),
+                                      ctypes.c_void_p(pfeat.data_ptr()), ctypes.c_void_p(self._fcat_u8.data_ptr()),
+                                      1 if p.criterion == "xgb" else 0, min_w2, 12, ctypes.c_void_p(pk.data_ptr()),
+                                      ctypes.c_void_p(mask.data_ptr()), ctypes.c_void_p(feat_i.data_ptr()),
+                                      ctypes.c_void_p(nb_t.data_ptr()), tree_ops._stream())
+        else:
+            rc = lib.h2o_pair_select(ctypes.c_void_p(Hp.data_ptr()), n, Bs, k, ctypes.c_void_p(best_k.data_ptr()),
+                                     ctypes.c_void_p(pfeat.data_ptr()), ctypes.c_void_p(self._fcat_u8.data_ptr()),
+                                     1 if p.criterion == "xgb" else 0, min_w2, 12, ctypes.c_void_p(pk.data_ptr()),
+                                     ctypes.c_void_p(mask.data_ptr()), ctypes.c_void_p(feat_i.data_ptr()),
+                                     tree_ops._stream())
         if rc != 0:
             raise RuntimeError(f"h2o_pair_select failed: {rc}")
 

@@ -1661,7 +1661,8 @@ __global__ __launch_bounds__(256) void pair_hist_multi_kernel(const CodeT* __res
                                                               const int4* __restrict__ work,
                                                               const int* __restrict__ pfeat, int Bs, float s0,
                                                               float s1, double* __restrict__ Hp,
-                                                              double* __restrict__ pwyy) {
+                                                              double* __restrict__ pwyy,
+                                                              const int* __restrict__ fbins) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long lh[];
   __shared__ double red[4];
   const int4 wk = work[blockIdx.x];
@@ -1727,7 +1728,20 @@ __global__ __launch_bounds__(256) void pair_hist_multi_kernel(const CodeT* __res
   const double i0 = 1.0 / (double)s0, i1 = 1.0 / (double)s1;
   double* o = Hp + (size_t)pair0 * nb;
   const bool single = (wk.w & 1) != 0;
+  // fbins: a pair's feature has fbins[f] codes below the NA bin (Bs - 1); the
+  // always-empty bins between them are not written (the scoring and select
+  // kernels read only [0, fbins) and the NA bin of narrow pairs) -- at deep
+  // levels the 1025-bin outputs of the 256-bin numeric pairs were most of the
+  // kernel's HBM writes
+  int fb[KP];
+#pragma unroll
+  for (int j = 0; j < KP; ++j) fb[j] = (fbins != nullptr && j < np) ? min(fbins[pfeat[pair0 + j]], Bs - 1) : Bs - 1;
   for (int i = threadIdx.x; i < np * nb; i += blockDim.x) {
+    const int j = i / nb, b = (i - j * nb) >> 1;
+    int fbj = fb[0];
+#pragma unroll
+    for (int q = 1; q < KP; ++q) fbj = j == q ? fb[q] : fbj;
+    if (b >= fbj && b < Bs - 1) continue;
     const long long v = (long long)lh[i];
     const double d = (double)v * ((i & 1) ? i1 : i0);
     if (single) o[i] = d;
@@ -1749,11 +1763,11 @@ template <typename CodeT, int MODE>
 static void pair_hist_multi_launch(bool has_vb, bool posv, int n_work, size_t lds, hipStream_t s,
                                    const void* codes_col, long long ncol, const int* ridx, const float* va,
                                    const float* vb, const int4* work, const int* pfeat, int Bs, float s0, float s1,
-                                   double* Hp, double* pwyy) {
+                                   double* Hp, double* pwyy, const int* fbins) {
   const CodeT* cc = (const CodeT*)codes_col;
 #define PHM(V, PV)                                                                                          \
   hipLaunchKernelGGL((pair_hist_multi_kernel<CodeT, MODE, V, PV, 4>), dim3(n_work), dim3(256), lds, s, cc, \
-                     ncol, ridx, va, vb, work, pfeat, Bs, s0, s1, Hp, pwyy)
+                     ncol, ridx, va, vb, work, pfeat, Bs, s0, s1, Hp, pwyy, fbins)
   if (has_vb) { if (posv) PHM(true, true); else PHM(true, false); }
   else { if (posv) PHM(false, true); else PHM(false, false); }
 #undef PHM
@@ -1761,10 +1775,32 @@ static void pair_hist_multi_launch(bool has_vb, bool posv, int n_work, size_t ld
 
 // Grouped version of h2o_pair_hist: work[i].w bits 8..15 = pairs in the group
 // (<= 4, consecutive pairs of one node starting at work[i].x).
+static int pair_hist4_impl(const void* codes_col, int code_bytes, long long ncol, const int* ridx,
+                           const float* va, const float* vb, const int* work, int n_work, const int* pfeat,
+                           int Bs, int mode, int posv, float s0, float s1, double* Hp, double* pwyy,
+                           hipStream_t s, const int* fbins);
+
 extern "C" int h2o_pair_hist4(const void* codes_col, int code_bytes, long long ncol, const int* ridx,
                               const float* va, const float* vb, const int* work, int n_work, const int* pfeat,
                               int Bs, int mode, int posv, float s0, float s1, double* Hp, double* pwyy,
                               hipStream_t s) {
+  return pair_hist4_impl(codes_col, code_bytes, ncol, ridx, va, vb, work, n_work, pfeat, Bs, mode, posv, s0, s1,
+                         Hp, pwyy, s, nullptr);
+}
+
+// h2o_pair_hist4 that leaves each pair's bins [fbins[f], Bs - 1) unwritten.
+extern "C" int h2o_pair_hist4b(const void* codes_col, int code_bytes, long long ncol, const int* ridx,
+                               const float* va, const float* vb, const int* work, int n_work, const int* pfeat,
+                               int Bs, int mode, int posv, float s0, float s1, double* Hp, double* pwyy,
+                               hipStream_t s, const int* fbins) {
+  return pair_hist4_impl(codes_col, code_bytes, ncol, ridx, va, vb, work, n_work, pfeat, Bs, mode, posv, s0, s1,
+                         Hp, pwyy, s, fbins);
+}
+
+static int pair_hist4_impl(const void* codes_col, int code_bytes, long long ncol, const int* ridx,
+                           const float* va, const float* vb, const int* work, int n_work, const int* pfeat,
+                           int Bs, int mode, int posv, float s0, float s1, double* Hp, double* pwyy,
+                           hipStream_t s, const int* fbins) {
   if (n_work <= 0) return 0;
   if (Bs < 2 || Bs > 4096 || (mode != 0 && mode != 1) || (mode == 1 && vb == nullptr)) return -1;
   const size_t lds = (size_t)4 * Bs * 2 * sizeof(unsigned long long);
@@ -1772,11 +1808,11 @@ extern "C" int h2o_pair_hist4(const void* codes_col, int code_bytes, long long n
   const int4* w = (const int4*)work;
   const bool hv = vb != nullptr;
   if (code_bytes == 1) {
-    if (mode == 0) pair_hist_multi_launch<uint8_t, 0>(hv, posv, n_work, lds, s, codes_col, ncol, ridx, va, vb, w, pfeat, Bs, s0, s1, Hp, pwyy);
-    else pair_hist_multi_launch<uint8_t, 1>(hv, posv, n_work, lds, s, codes_col, ncol, ridx, va, vb, w, pfeat, Bs, s0, s1, Hp, pwyy);
+    if (mode == 0) pair_hist_multi_launch<uint8_t, 0>(hv, posv, n_work, lds, s, codes_col, ncol, ridx, va, vb, w, pfeat, Bs, s0, s1, Hp, pwyy, fbins);
+    else pair_hist_multi_launch<uint8_t, 1>(hv, posv, n_work, lds, s, codes_col, ncol, ridx, va, vb, w, pfeat, Bs, s0, s1, Hp, pwyy, fbins);
   } else {
-    if (mode == 0) pair_hist_multi_launch<uint16_t, 0>(hv, posv, n_work, lds, s, codes_col, ncol, ridx, va, vb, w, pfeat, Bs, s0, s1, Hp, pwyy);
-    else pair_hist_multi_launch<uint16_t, 1>(hv, posv, n_work, lds, s, codes_col, ncol, ridx, va, vb, w, pfeat, Bs, s0, s1, Hp, pwyy);
+    if (mode == 0) pair_hist_multi_launch<uint16_t, 0>(hv, posv, n_work, lds, s, codes_col, ncol, ridx, va, vb, w, pfeat, Bs, s0, s1, Hp, pwyy, fbins);
+    else pair_hist_multi_launch<uint16_t, 1>(hv, posv, n_work, lds, s, codes_col, ncol, ridx, va, vb, w, pfeat, Bs, s0, s1, Hp, pwyy, fbins);
   }
   return (int)hipGetLastError();
 }

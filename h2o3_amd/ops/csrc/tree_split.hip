@@ -310,7 +310,8 @@ __global__ __launch_bounds__(256) void cat_pair_kernel(const double* __restrict_
                                                        const double* __restrict__ node_wyy, double min_rows,
                                                        double msi, double lam, double alpha, double gamma,
                                                        double* __restrict__ out, const int* __restrict__ plist,
-                                                       const int* __restrict__ pcount, int Bscan) {
+                                                       const int* __restrict__ pcount, int Bscan,
+                                                       const int* __restrict__ pbins) {
   __shared__ double sk[BP];   // sort key, then channel-0 prefix sums
   __shared__ double s1[BP];   // channel-1 prefix sums
   __shared__ int si[BP];      // bin index (sort payload)
@@ -329,7 +330,7 @@ __global__ __launch_bounds__(256) void cat_pair_kernel(const double* __restrict_
   const int B = Bs - 1;       // NA bin index; k = i | nt + i | 2 nt over the full width
   // bins scanned: a feature with at most Bscan bins leaves [Bscan, B) empty;
   // thresholds there repeat the all-left partition and lose the lowest-k tie
-  const int Bsc = min(B, Bscan);
+  const int Bsc = pbins != nullptr ? min(min(B, Bscan), pbins[p]) : min(B, Bscan);
   const double* h = H + ((size_t)pf[p] * n + pn[p]) * (size_t)Bs * C;
   const bool cat = pcat[p] != 0;
   int M = BP;                 // sorted prefix length
@@ -502,11 +503,12 @@ template <int CRIT>
 static int cat_pair_launch(int BP, dim3 g, hipStream_t s, const double* H, int n, int Bs, int C, const int* pf,
                            const int* pn, const unsigned char* pcat, const float* pmono, const double* wyy,
                            double min_rows, double msi, double lam, double alpha, double gamma, double* out,
-                           const int* plist = nullptr, const int* pcount = nullptr, int Bscan = 1 << 30) {
+                           const int* plist = nullptr, const int* pcount = nullptr, int Bscan = 1 << 30,
+                           const int* pbins = nullptr) {
 #define CPK(bp)                                                                                                \
   case bp:                                                                                                     \
     hipLaunchKernelGGL((cat_pair_kernel<CRIT, bp>), g, dim3(256), 0, s, H, n, Bs, C, pf, pn, pcat, pmono, wyy, \
-                       min_rows, msi, lam, alpha, gamma, out, plist, pcount, Bscan);                           \
+                       min_rows, msi, lam, alpha, gamma, out, plist, pcount, Bscan, pbins);                    \
     return 0;
   switch (BP) {
     CPK(256) CPK(512) CPK(1024) CPK(2048) CPK(4096)
@@ -581,14 +583,14 @@ extern "C" int h2o_cat_pairs2(const double* H, int n, int Bs, int C, int P, cons
   hipLaunchKernelGGL(pair_lists_kernel, dim3((P + 255) / 256), dim3(256), 0, s, pbins, P, narrow_max, lists, cnt);
   const dim3 g(P);
   int rc = crit == 1 ? cat_pair_launch<1>(256, g, s, H, n, Bs, C, pf, pn, pcat, pmono, node_wyy, min_rows, msi,
-                                          lam, alpha, gamma, out, lists, cnt, narrow_max)
+                                          lam, alpha, gamma, out, lists, cnt, narrow_max, pbins)
                      : cat_pair_launch<0>(256, g, s, H, n, Bs, C, pf, pn, pcat, pmono, node_wyy, min_rows, msi,
-                                          lam, alpha, gamma, out, lists, cnt, narrow_max);
+                                          lam, alpha, gamma, out, lists, cnt, narrow_max, pbins);
   if (rc) return rc;
   rc = crit == 1 ? cat_pair_launch<1>(BP, g, s, H, n, Bs, C, pf, pn, pcat, pmono, node_wyy, min_rows, msi, lam,
-                                      alpha, gamma, out, lists + P, cnt + 1, Bs - 1)
+                                      alpha, gamma, out, lists + P, cnt + 1, Bs - 1, pbins)
                  : cat_pair_launch<0>(BP, g, s, H, n, Bs, C, pf, pn, pcat, pmono, node_wyy, min_rows, msi, lam,
-                                      alpha, gamma, out, lists + P, cnt + 1, Bs - 1);
+                                      alpha, gamma, out, lists + P, cnt + 1, Bs - 1, pbins);
   if (rc) return rc;
   return (int)hipGetLastError();
 }
@@ -613,7 +615,8 @@ __global__ __launch_bounds__(256) void pair_select_kernel(const double* __restri
                                                           const int* __restrict__ pfeat,
                                                           const unsigned char* __restrict__ fcat, double min_w2,
                                                           int stride, double* __restrict__ pk,
-                                                          uint8_t* __restrict__ mask, int* __restrict__ feat_out) {
+                                                          uint8_t* __restrict__ mask, int* __restrict__ feat_out,
+                                                          const int* __restrict__ fbins) {
   __shared__ double sk[BP];
   __shared__ int si[BP];
   __shared__ double rg[4];
@@ -649,10 +652,12 @@ __global__ __launch_bounds__(256) void pair_select_kernel(const double* __restri
   const int opt = kk < nt ? 0 : (kk < 2 * nt ? 1 : 2);
   const int t = opt == 0 ? kk : (opt == 1 ? kk - nt : 0);
   const bool na_left = opt == 1;
+  // bins of the winner's feature: [Bw, B) hold no rows (and may be unwritten)
+  const int Bw = fbins != nullptr ? min(B, fbins[f]) : B;
   // rank of every non-NA bin in the split order
   for (int b = tid; b < BP; b += 256) {
     double key = INFINITY;
-    if (b < B) {
+    if (b < Bw) {
       if (!cat) {
         key = (double)b;
       } else {
@@ -688,7 +693,8 @@ __global__ __launch_bounds__(256) void pair_select_kernel(const double* __restri
   // left / total sums and the mask
   double l0 = 0, l1 = 0, t0 = 0, t1 = 0, n0 = 0, n1 = 0;
   for (int b = tid; b < Bs; b += 256) {
-    const double a0 = h[2 * (size_t)b], a1 = h[2 * (size_t)b + 1];
+    const bool live = b < Bw || b >= B;
+    const double a0 = live ? h[2 * (size_t)b] : 0.0, a1 = live ? h[2 * (size_t)b + 1] : 0.0;
     t0 += a0; t1 += a1;
     bool left;
     if (b >= B) {
@@ -737,11 +743,11 @@ __global__ __launch_bounds__(256) void pair_select_kernel(const double* __restri
 template <int CRIT>
 static int pair_select_launch(int BP, int n, hipStream_t s, const double* Hp, int Bs, int kp, const double* res,
                               const int* pfeat, const unsigned char* fcat, double min_w2, int stride, double* pk,
-                              uint8_t* mask, int* feat_out) {
+                              uint8_t* mask, int* feat_out, const int* fbins = nullptr) {
 #define PSK(bp)                                                                                                   \
   case bp:                                                                                                        \
     hipLaunchKernelGGL((pair_select_kernel<CRIT, bp>), dim3(n), dim3(256), 0, s, Hp, Bs, kp, res, pfeat, fcat, \
-                       min_w2, stride, pk, mask, feat_out);                                                       \
+                       min_w2, stride, pk, mask, feat_out, fbins);                                                \
     return 0;
   switch (BP) {
     PSK(256) PSK(512) PSK(1024) PSK(2048) PSK(4096)
@@ -764,6 +770,24 @@ extern "C" int h2o_pair_select(const double* Hp, int n, int Bs, int kp, const do
                                                    feat_out)
                            : pair_select_launch<0>(BP, n, s, Hp, Bs, kp, res, pfeat, fcat, min_w2, stride, pk, mask,
                                                    feat_out);
+  if (rc) return rc;
+  return (int)hipGetLastError();
+}
+
+// h2o_pair_select for pair histograms written up to each feature's bins
+// (fbins [F]: codes below the NA bin; h2o_pair_hist4b).
+extern "C" int h2o_pair_select2(const double* Hp, int n, int Bs, int kp, const double* res, const int* pfeat,
+                                const unsigned char* fcat, int crit, double min_w2, int stride, double* pk,
+                                uint8_t* mask, int* feat_out, const int* fbins, hipStream_t s) {
+  if (n <= 0) return 0;
+  if (kp <= 0 || Bs < 3 || stride < 11) return -1;
+  int BP = 256;
+  while (BP < Bs - 1) BP <<= 1;
+  if (BP > 4096) return -2;
+  const int rc = crit == 1 ? pair_select_launch<1>(BP, n, s, Hp, Bs, kp, res, pfeat, fcat, min_w2, stride, pk, mask,
+                                                   feat_out, fbins)
+                           : pair_select_launch<0>(BP, n, s, Hp, Bs, kp, res, pfeat, fcat, min_w2, stride, pk, mask,
+                                                   feat_out, fbins);
   if (rc) return rc;
   return (int)hipGetLastError();
 }

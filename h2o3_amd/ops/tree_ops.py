@@ -574,7 +574,7 @@ def pair_hist(bd, ridx, va, vb, mode, node_st, node_ct, pair_node, pair_feat, vm
     return Hp, wyy_n
 
 
-def pair_hist_dev(bd, ridx, va, vb, mode, node_st, node_ct, sel, vmax, posv=False, chunk=_PAIR_CHUNK):
+def pair_hist_dev(bd, ridx, va, vb, mode, node_st, node_ct, sel, vmax, posv=False, chunk=_PAIR_CHUNK, fbins=None):
     """pair_hist for a frontier whose pairs are given ON THE DEVICE: sel
     [n, k] global feature ids per node (node-major pairs p = i * k + j), so
     no pair list crosses to the host.  node_st / node_ct: host arrays.  The
@@ -625,10 +625,16 @@ def pair_hist_dev(bd, ridx, va, vb, mode, node_st, node_ct, sel, vmax, posv=Fals
         fn = lib.h2o_pair_hist4 if kp > 1 else lib.h2o_pair_hist
         if kp > 1 and not getattr(lib, "_typed_pair4", False):
             lib.h2o_pair_hist4.argtypes = lib.h2o_pair_hist.argtypes
+            lib.h2o_pair_hist4b.argtypes = lib.h2o_pair_hist.argtypes + [_c_void]
             lib._typed_pair4 = True
-        rc = fn(_ptr(bd.codes_col), bd.code_bytes, bd.codes_col.stride(0), _ptr(ridx), _ptr(va), _ptr(vb),
+        args = [_ptr(bd.codes_col), bd.code_bytes, bd.codes_col.stride(0), _ptr(ridx), _ptr(va), _ptr(vb),
                 _ptr(items), n_items, _ptr(pfeat), Bs, mode, 1 if posv else 0, s0, s1, _ptr(Hp), _ptr(pwyy),
-                _stream())
+                _stream()]
+        if kp > 1 and fbins is not None:
+            # bins past each feature's own codes stay unwritten (see h2o_pair_hist4b)
+            rc = lib.h2o_pair_hist4b(*args, _ptr(fbins))
+        else:
+            rc = fn(*args)
         if rc != 0:
             raise RuntimeError(f"h2o_pair_hist failed: {rc}")
     return Hp, (pwyy.view(n, k)[:, 0].contiguous() if want_wyy else None), pfeat
