@@ -29,6 +29,13 @@ def make_df(n=20000, F=40, seed=11):
     logit += np.where(df["c0"].isin(["a", "c", "f"]), 1.0, -0.5)
     df["y"] = np.where(rng.random(n) < 1 / (1 + np.exp(-logit)), "yes", "no")
     df["yr"] = logit + rng.normal(scale=0.3, size=n)
+    # a 600-level categorical (histograms wider than 256 bins: the narrow /
+    # wide pair scoring split) and 0/1 row weights (zero-weight rows skip
+    # their code gathers)
+    lv = rng.integers(0, 600, n)
+    df["hc"] = np.array([f"h{v}" for v in range(600)])[lv]
+    df["yr"] += rng.normal(size=600)[lv]
+    df["w01"] = (rng.random(n) > 0.2).astype(float)
     return df
 
 
@@ -48,13 +55,19 @@ def run(out_path):
     assert cloud.device().type == "cuda" or os.environ.get("H2O3_WORKER_CPU_OK") == "1"
     df = make_df()
     fr = h2o.H2OFrame(df)
-    x = [c for c in df.columns if c not in ("y", "yr")]
+    x = [c for c in df.columns if c not in ("y", "yr", "hc", "w01")]
     res = {"world": cloud.world(), "backend": cloud.info()["backend"]}
     # DRF, mtries = sqrt(41) -> 6 of 41 features per node: the row-direct pair path
     drf = H2ORandomForestEstimator(ntrees=3, max_depth=8, seed=3, sample_rate=1.0, mtries=6, min_rows=20)
     drf.train(x=x, y="yr", training_frame=fr)
     res["drf_trees"] = _trees(drf)
     res["drf_pred"] = drf.predict(fr).as_data_frame()["predict"].tolist()
+    # DRF on the all-pair-path layout: position-ordered response payload,
+    # 600-level categorical, zero-weight rows
+    drf2 = H2ORandomForestEstimator(ntrees=2, max_depth=10, seed=5, sample_rate=1.0, mtries=6, min_rows=10,
+                                    weights_column="w01")
+    drf2.train(x=x + ["hc"], y="yr", training_frame=fr)
+    res["drf2_trees"] = _trees(drf2)
     # GBM binomial: level histograms reduce-scattered by feature
     gbm = H2OGradientBoostingEstimator(ntrees=4, max_depth=6, seed=1, min_rows=20)
     gbm.train(x=x, y="y", training_frame=fr)
