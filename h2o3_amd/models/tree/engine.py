@@ -652,6 +652,19 @@ class TreeGrower:
         k, _ = self._sample_k(depth)
         return env == "1" or chunked or 4 * k <= self.bd.F
 
+    def _flush_masks(self, tb):
+        """Collect the categorical mask rows of the previous level from the
+        pinned staging buffer into the tree (waits on the copy's event: by the
+        time the next level's record arrived it has completed)."""
+        pend = self.__dict__.get("_mask_pend")
+        if pend is None:
+            return
+        nodes, feats, shape, ev = pend
+        ev.synchronize()
+        n = int(np.prod(shape))
+        tb.cat_parts.append((nodes, feats, self._mask_stage[:n].numpy().reshape(shape).copy()))
+        self._mask_pend = None
+
     def _narrow_bins(self):
         """Per-feature code counts [F] int32 on the device when the pair path
         may bound its work by each feature's bins (histograms wider than 256
@@ -1299,6 +1312,7 @@ class TreeGrower:
         if self._unit_w and not self.use_payload and (quad or all_direct):
             self._va_eff = torch.where(vb > 0, va, torch.full_like(va, float("nan"))) if vb is not None else va
         self._pos1 = None
+        self._mask_pend = None
         if self._va_eff is not None and tree_ops.env("H2O3_POSV", "1") == "1" and \
                 tree_ops.env("H2O3_PART", "ballot") == "ballot":
             # va_scratch: the caller hands over va (a NaN-masked residual it
@@ -1441,6 +1455,7 @@ class TreeGrower:
                     self._maybe_lookahead(pkd, (10, 11, 4 + (mode == 1), 6 + (mode == 1)), f_st, f_ct, mode, va,
                                           vb, ridx2, H, wyy_level, depth, level_bytes, chunked)
                     pk = self._d2h_wait(pk_h)
+                    self._flush_masks(tb)
                     ok_h = pk[:, 10] > 0
                     nleft_pre = pk[:, 11].astype(np.int64)
                 cols = [] if nleft_pre is not None else [
@@ -1473,6 +1488,7 @@ class TreeGrower:
                                               f_st, f_ct, mode, va, vb, ridx2, H, wyy_level, depth, level_bytes,
                                               chunked)
                     pk = self._d2h_wait(pk_h)
+                    self._flush_masks(tb)
                     if async_part:
                         ok_h = pk[:, 4 + 3 * C] > 0
                         nleft_pre = pk[:, 5 + 3 * C].astype(np.int64)
@@ -1555,8 +1571,23 @@ class TreeGrower:
             if cat_s.any():
                 # only the categorical splits' mask rows cross to the host (one gather + copy)
                 cj = np.nonzero(cat_s)[0]
-                masks_h = masks[tree_ops._h2d(cj, masks.device)].cpu().numpy() if cj.size < k else \
-                    masks.cpu().numpy()
+                mk = masks[tree_ops._h2d(cj, masks.device)] if cj.size < k else masks
+                masks_h = None
+                if mk.is_cuda and tree_ops.env("H2O3_ASYNC_MASKS", "1") == "1":
+                    # asynchronous copy into a pinned staging buffer: the rows are
+                    # collected after the next level's record arrives (the GPU has
+                    # long finished the copy by then) instead of a blocking .cpu()
+                    self._flush_masks(tb)
+                    need = mk.numel()
+                    st_buf = self.__dict__.get("_mask_stage")
+                    if st_buf is None or st_buf.numel() < need:
+                        st_buf = self._mask_stage = torch.empty(max(need, 1 << 20), dtype=torch.uint8,
+                                                                pin_memory=True)
+                    st_buf[:need].view(mk.shape).copy_(mk, non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record()
+                else:
+                    masks_h = mk.cpu().numpy()
                 tb.is_cat[nid_s[cj]] = True
                 tb.thr[nid_s[cj]] = np.nan
                 fcj = f_s[cj]
@@ -1566,7 +1597,10 @@ class TreeGrower:
                         card = bd.cat_card[f]
                         tb.cat_lvm[f] = np.arange(card) if (bd.cat_group[f] == 1 and card <= bd.Bs - 1) else \
                             np.minimum(np.arange(card) // bd.cat_group[f], bd.Bs - 2)
-                tb.cat_parts.append((nid_s[cj].astype(np.int64), fcj.astype(np.int64), masks_h))
+                if masks_h is not None:
+                    tb.cat_parts.append((nid_s[cj].astype(np.int64), fcj.astype(np.int64), masks_h))
+                else:
+                    self._mask_pend = (nid_s[cj].astype(np.int64), fcj.astype(np.int64), tuple(mk.shape), ev)
             st_s, ct_s = f_st[sids], f_ct[sids]
             # partition
             if nleft_pre is not None:
@@ -1619,6 +1653,7 @@ class TreeGrower:
                 p_par = np.arange(k, dtype=np.int64)
             depth += 1
             level += 1
+        self._flush_masks(tb)
         tree = tb.to_tree()
         if leaf_parts:
             leaf_ids = np.concatenate([q[0] for q in leaf_parts])
