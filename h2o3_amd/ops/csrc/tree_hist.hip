@@ -1210,7 +1210,15 @@ __global__ __launch_bounds__(256) void leaf_scatter_kernel(const int* __restrict
                                                            const float* __restrict__ val, float* __restrict__ d) {
   const int4 wk = work[blockIdx.x];
   const float v = val[wk.x];
-  for (int p = wk.y + threadIdx.x; p < wk.y + wk.z; p += 256) d[ridx[p]] = v;
+  const int end = wk.y + wk.z;
+  // 4 row ids loaded before the 4 random stores: more scatter writes in
+  // flight per thread than the load -> store -> load chain
+  int p = wk.y + threadIdx.x;
+  for (; p + 3 * 256 < end; p += 4 * 256) {
+    const int r0 = ridx[p], r1 = ridx[p + 256], r2 = ridx[p + 512], r3 = ridx[p + 768];
+    d[r0] = v; d[r1] = v; d[r2] = v; d[r3] = v;
+  }
+  for (; p < end; p += 256) d[ridx[p]] = v;
 }
 
 // Per-node column sampling without replacement (DRF mtries, GBM
