@@ -517,12 +517,7 @@ class H2OMojoModel:
         relative improvement is negative or below 1e-10."""
         n = X.shape[0]
         k = self.gl_ncolX
-        A = np.empty((n, self.gl_ncolA))
-        for i in range(self.gl_ncats):
-            v = X[:, self.gl_perm[i]]
-            A[:, i] = np.where(v >= self.gl_levels[i], np.nan, v)          # unseen levels -> NA
-        for i in range(self.gl_ncats, self.gl_ncolA):
-            A[:, i] = X[:, self.gl_perm[i]]
+        A = self.glrm_row_data(X)
         seeds = self.gl_seed + self.gl_rcnt + np.arange(n, dtype=np.int64)
         self.gl_rcnt += n
         x = _JavaRandom(seeds).gaussians(k)
@@ -556,6 +551,17 @@ class H2OMojoModel:
             old = np.where(live | upd, obj, old)
         self.glrm_x = x
         return x
+
+    def glrm_row_data(self, X):
+        """GlrmMojoModel.getRowData: the permuted row (categoricals first),
+        unseen categorical levels as NA."""
+        A = np.empty((X.shape[0], self.gl_ncolA))
+        for i in range(self.gl_ncats):
+            v = X[:, self.gl_perm[i]]
+            A[:, i] = np.where(v >= self.gl_levels[i], np.nan, v)
+        for i in range(self.gl_ncats, self.gl_ncolA):
+            A[:, i] = X[:, self.gl_perm[i]]
+        return A
 
     def glrm_impute(self, x):
         """GlrmMojoModel.impute_data: the reconstructed row (categorical level

@@ -168,3 +168,35 @@ def test_glrm_reference_layout_mojo(tmp_path):
     rec2 = mj2.predict(test)
     exp2 = m2.predict(h2o.H2OFrame(test)).as_data_frame()
     assert (rec2["reconstr_g"].values == exp2["reconstr_g"].values).mean() >= 0.9
+
+
+def test_reference_glrm_mojo_fixture():
+    """The reference's own GLRM MOJO (h2o-genmodel test resources, 12 columns,
+    8 categorical, transposed archetypes, seed > 2^32) loads through the
+    reference-layout reader: GlrmMojoModelTest's rows, its unseen-level-to-NA
+    rule (testConvertUnseenEnumsToNA), and finite, reproducible scores whose
+    objective is below that of the random starting point."""
+    import os
+    from h2o3_amd.mojo import h2o_mojo
+    d = "/root/reference/h2o-genmodel/src/test/resources/hex/genmodel/algos/glrm"
+    if not os.path.exists(os.path.join(d, "model.ini")):
+        pytest.skip("reference fixture not available")
+    mj = h2o_mojo.load(d)
+    assert mj.algo == "glrm" and mj.gl_ncolX == 4 and mj.gl_Y.shape == (4, 264)
+    rows = np.array([[0.0, 1.0, 5.0, 2.0, 741, 912, 5.0, 79.0, 82.0, 447.0, 1.0, 1.0],
+                     [0.0, 1.0, 9.0, 6.0, 729.0, 847.0, 5.0, 79.0, 82.0, 447.0, 0.0, -1],
+                     [0.0, 1.0, 10.0, 0.0, 749.0, 922.0, 5.0, 79.0, 82.0, 447.0, 1.0, 1.0]])
+    perm = [7, 8, 2, 0, 6, 3, 1, 10, 4, 5, 9, 11]
+    levels = [101, 93, 31, 14, 10, 7, 2, 2, -1, -1, -1, -1]
+    changed = rows.copy()
+    for r in range(3):
+        changed[r, perm[r]] = levels[r] + 10.0
+        assert np.isnan(mj.glrm_row_data(changed[r:r + 1])[0, r])
+    x1 = mj.score0(rows.copy())
+    mj.gl_rcnt = 0
+    x2 = mj.score0(rows.copy())
+    assert np.isfinite(x1).all() and np.array_equal(x1, x2)
+    from h2o3_amd.mojo.h2o_mojo import _JavaRandom
+    A = mj.glrm_row_data(rows)
+    x0 = _JavaRandom(mj.gl_seed + np.arange(3, dtype=np.int64)).gaussians(4)
+    assert np.all(mj._glrm_obj_grad(x1, A, False)[0] < mj._glrm_obj_grad(x0, A, False)[0])
