@@ -716,6 +716,52 @@ class H2OMojoModel:
     def _score_gam(self, X):
         return self._score_glm(X)
 
+    def _load_pipeline(self):
+        """MojoPipelineReader: sub-models under models/<alias>/, the main
+        model's generated input columns (generated_column_name_i <- prediction
+        generated_column_index_i of sub-model generated_column_model_i), the
+        other main-model inputs taken from the pipeline row by name."""
+        subs = {}
+        for i in range(int(self.kv("submodel_count", 0))):
+            subs[str(self.kv(f"submodel_key_{i}"))] = H2OMojoModel(
+                None, backend=self.be.nested(str(self.kv(f"submodel_dir_{i}"))))
+        main_alias = str(self.kv("main_model"))
+        self.pl_main = subs[main_alias]
+        gen = []
+        for i in range(int(self.kv("generated_column_count", 0))):
+            gen.append((str(self.kv(f"generated_column_name_{i}")), str(self.kv(f"generated_column_model_{i}")),
+                        int(self.kv(f"generated_column_index_{i}", 0))))
+        names = list(self.columns)
+        gen_names = {g[0] for g in gen}
+        mf = self.pl_main.features
+        self.pl_direct = [(mf.index(c), names.index(c)) for c in mf if c not in gen_names]
+        self.pl_subs = []
+        for alias, m in subs.items():
+            if alias == main_alias:
+                continue
+            inp = [names.index(c) for c in m.features]
+            outs = [(mf.index(g[0]), g[2]) for g in gen if g[1] == alias]
+            self.pl_subs.append((m, np.asarray(inp, dtype=np.int64), outs))
+        self.nclasses = self.pl_main.nclasses
+        self.category = self.pl_main.category
+        self.response_domain = self.pl_main.response_domain
+        self.default_threshold = self.pl_main.default_threshold
+
+    def _score_pipeline(self, X):
+        """MojoPipeline.score0: sub-model predictions fill the generated
+        columns of the main model's input row, then the main model scores."""
+        n = X.shape[0]
+        row = np.full((n, len(self.pl_main.columns)), np.nan)
+        for t, s_ in self.pl_direct:
+            row[:, t] = X[:, s_]
+        for m, inp, outs in self.pl_subs:
+            sub = np.full((n, len(m.columns)), np.nan)
+            sub[:, :inp.size] = X[:, inp]
+            preds = m.score0(sub)
+            for t, j in outs:
+                row[:, t] = preds[:, j]
+        return self.pl_main.score0(row)
+
     def _load_stackedensemble(self):
         subs = {}
         for i in range(int(self.kv("submodel_count", 0))):
@@ -1618,6 +1664,7 @@ class H2OMojoModel:
         preds = self.score0(self.row_matrix(df))
         if self.algo == "kmeans":
             return pd.DataFrame({"predict": preds[:, 0].astype(np.int64)})
+
         if self.algo == "isolationforest":
             cols = ["predict", "score", "mean_length"] if self.output_anomaly_flag else ["predict", "mean_length"]
             return pd.DataFrame(preds, columns=cols)

@@ -1227,3 +1227,62 @@ def build_h2o_mojo(model) -> bytes:
     z = _Zip()
     _write_algo(model, z)
     return z.close()
+
+
+def build_mojo_pipeline(models, mapping, main_alias) -> bytes:
+    """MojoPipelineBuilder / MojoPipelineWriter: one zip holding every
+    sub-model under models/<alias>/ and a model.ini whose columns are the
+    sub-models' inputs followed by the main model's non-generated columns
+    (its response included); mapping = {generated column: "alias:prediction
+    index"} feeds the main model's inputs from the other models' scores.
+    models: {alias: MOJO zip path or bytes}."""
+    from .h2o_mojo import H2OMojoModel
+    loaded, blobs = {}, {}
+    for alias, src in models.items():
+        data = src if isinstance(src, (bytes, bytearray)) else open(src, "rb").read()
+        blobs[alias] = bytes(data)
+        loaded[alias] = H2OMojoModel(bytes(data))
+    if main_alias not in loaded:
+        raise ValueError(f"Main model is missing. There is no model with alias '{main_alias}'.")
+    final = loaded[main_alias]
+    schema = {}
+    for alias, m in loaded.items():
+        if alias == main_alias:
+            continue
+        for c, d in zip(m.features, m.domains[:len(m.features)]):
+            if c in schema and schema[c] != d:
+                raise ValueError(f"Domains of column '{c}' differ.")
+            schema.setdefault(c, d)
+    for c, d in zip(final.columns, final.domains):
+        if c not in mapping:
+            schema[c] = d
+    columns = list(schema)
+    domains = [schema[c] for c in columns]
+    extra = {"submodel_count": len(loaded)}
+    for i, alias in enumerate(loaded):
+        extra[f"submodel_key_{i}"] = alias
+        extra[f"submodel_dir_{i}"] = f"models/{alias}/"
+    extra["generated_column_count"] = len(mapping)
+    for i, (col, spec) in enumerate(mapping.items()):
+        alias, idx = spec.rsplit(":", 1)
+        extra[f"generated_column_name_{i}"] = col
+        extra[f"generated_column_model_{i}"] = alias
+        extra[f"generated_column_index_{i}"] = int(idx)
+    extra["main_model"] = main_alias
+
+    class _M:                                  # header fields of the pipeline's own descriptor
+        model_id = f"pipeline_{main_alias}"
+        _training_metrics = None
+        _validation_metrics = None
+    nf = len(columns) - (1 if final.supervised else 0)
+    ini, files = _header(_M, "pipeline", "MOJO Pipeline", final.category, columns, nf, final.nclasses, domains,
+                         "1.00", extra, supervised=final.supervised)
+    z = _Zip()
+    z.write("model.ini", ini)
+    for k_, v_ in files.items():
+        z.write(k_, v_)
+    for alias, data in blobs.items():
+        src = zipfile.ZipFile(io.BytesIO(data))
+        for name in src.namelist():
+            z.write(f"models/{alias}/{name}", src.read(name))
+    return z.close()
