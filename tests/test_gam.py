@@ -131,3 +131,27 @@ def test_isplines_match_reference_recursion():
     for order in (1, 2, 3):
         np.testing.assert_allclose(is_basis(torch.as_tensor(x), knots, order)[0].numpy(),
                                    ispline_basis(x, knots, order), atol=1e-12)
+
+
+def test_gam_reference_layout_mojo_multinomial(tmp_path):
+    """Multinomial GAM in the GAMMojoWriter layout: beta_multinomial(_centering)
+    as rectangular big-endian blobs, softmax of the per-class etas."""
+    from h2o3_amd.mojo import h2o_mojo
+    h2o.init()
+    rng = np.random.default_rng(8)
+    n = 1500
+    x1, x2 = rng.uniform(-2, 2, n), rng.normal(size=n)
+    s = np.sin(2 * x1) + 0.5 * x2
+    df = pd.DataFrame({"x1": x1, "x2": x2,
+                       "y": np.where(s > 0.5, "hi", np.where(s < -0.5, "lo", "mid"))})
+    fr = h2o.H2OFrame(df)
+    fr["y"] = fr["y"].asfactor()
+    m = H2OGeneralizedAdditiveEstimator(family="multinomial", gam_columns=["x1"], bs=[0], num_knots=[7],
+                                        scale=[0.001], lambda_=0.0)
+    m.train(x=["x2"], y="y", training_frame=fr)
+    mj = h2o_mojo.load(m.download_mojo(str(tmp_path / "gm"), format="h2o"))
+    test = df.iloc[:150]
+    ours = m.predict(h2o.H2OFrame(test)).as_data_frame()
+    got = mj.predict(test)
+    for lv in ("hi", "lo", "mid"):
+        np.testing.assert_allclose(got[lv].values, ours[lv].values, rtol=1e-4, atol=1e-5)
