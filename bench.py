@@ -27,6 +27,12 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 
+_GLM_PRECISION = ("Hessian X'WX: bf16x3 split operands (hi*hi + hi*lo + lo*hi) on MFMA, f32 accumulate, f64 across "
+                  "row blocks; gradient X'(w (y - mu)): f32 VALU products, f64 sums, in the same pass; Newton step "
+                  "beta + H^-1 g, so the converged coefficients are those of the exact gradient "
+                  "(scripts/glm_precision.py)")
+
+
 def make_frame(args, dev, rank, rows_local):
     """Synthetic data of the benchmark shape (random, generated on device):
     args.cols features (the last args.cat_cols categorical), binomial y."""
@@ -65,6 +71,21 @@ def make_frame(args, dev, rank, rows_local):
     return fr, names, y
 
 
+def _launch(n):
+    """Run this script on n ranks (one process per GPU) under
+    torch.distributed.run on 127.0.0.1 and return its exit status."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -86,6 +107,15 @@ def main():
                     help="--algo gbm: skip the companion GLM measurement (the headline metric is GBM trees/s + "
                          "GLM iters/s on the same 100M x 100 frame; the GLM figure is reported as extra keys)")
     args = ap.parse_args()
+
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is None and args.gpus > 1:
+        # self-launch: one rank per GPU as child processes of torch.distributed.run,
+        # started before this process touches the GPU
+        return _launch(args.gpus)
+    if ws is not None and int(ws) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws}", file=sys.stderr)
+        return 2
 
     import torch
     import torch.distributed as dist
@@ -191,8 +221,7 @@ def main():
         metric = "glm_iters_per_sec"
         unit = "iters/s"
         model = f"GLM binomial IRLSM {args.rows / 1e6:g}Mx{F}"
-        extra_cfg = {"gram_precision": "bf16x3 split operands (hi*hi + hi*lo + lo*hi) on MFMA, f32 accumulate, "
-                                       "f64 across row blocks"}
+        extra_cfg = {"gram_precision": _GLM_PRECISION}
 
     def sync():
         torch.cuda.synchronize() if dev.type == "cuda" else None
@@ -252,6 +281,7 @@ def main():
         extra["glm_iters_per_sec"] = round(args.steps / gel, 4)
         extra["glm_ms_per_iter"] = round(1000 * gel / args.steps, 3)
         extra["glm_model"] = f"GLM binomial IRLSM {args.rows / 1e6:g}Mx{F} (same frame, {args.steps} timed iterations)"
+        extra["glm_precision"] = _GLM_PRECISION
     from h2o3_amd.utils import timer
     if timer.ENABLED and rank == 0:
         print("phases(ms,count):", timer.report(), file=sys.stderr)
@@ -270,4 +300,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

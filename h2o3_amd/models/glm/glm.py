@@ -21,6 +21,7 @@ same quadratic subproblem the reference hands to ADMM).
 from __future__ import annotations
 
 import math
+import os
 import time
 
 import numpy as np
@@ -340,6 +341,8 @@ class GLMDriver:
         if sv is not None:
             self._set_startval(sv)
         self.active = None     # collinear-column mask (remove_collinear_columns)
+        self._hprec = None     # Hessian precision tier (None: not chosen yet), see _check_tier
+        self.hessian_kappa = None
         self.iter = 0
         self.lambda_max = self._lambda_max()
         lam = p.get("lambda_")
@@ -517,13 +520,26 @@ class GLMDriver:
             self._y32 = self.y.to(torch.float32)
             self._w32 = None if bool((self.w == 1).all()) else self.w.to(torch.float32)
             self._off32 = None if self.offset is None else self.offset.to(torch.float32)
+        self._gexact = None
+        bf3 = None if self._hprec is None else self._hprec == "bf3"
         with phase("glm.irls_pass"):
             if codes is not None:
                 bt = torch.zeros(self.Pp, dtype=torch.float32, device=self.X.device)
                 bt[:P] = torch.as_tensor(self.beta[:P], dtype=torch.float32)
-                Gf, dev = linalg_ops.glm_irls(self.X, aug=P, beta=bt, b0=float(self.beta[-1]), y=self._y32,
-                                              wprior=self._w32, offset=self._off32, codes=codes,
-                                              tvp=self.fam.tvp, theta=self.fam.theta, width=self.Pp)
+                if linalg_ops.glm_grad_supported(self.Pp):
+                    # Hessian on the matrix cores + exact gradient channel (Newton on
+                    # the exact gradient: see _finish_stats)
+                    Gf, dev, gx = linalg_ops.glm_irls(self.X, aug=P, beta=bt, b0=float(self.beta[-1]),
+                                                      y=self._y32, wprior=self._w32, offset=self._off32,
+                                                      codes=codes, tvp=self.fam.tvp, theta=self.fam.theta,
+                                                      width=self.Pp, grad=True, bf3=bf3)
+                    self._gexact = torch.cat([gx[:P], gx[self.Pp:self.Pp + 1]])
+                    self._gbeta = np.concatenate([self.beta[:P].astype(np.float32).astype(np.float64),
+                                                  [float(np.float32(self.beta[-1]))]])
+                else:
+                    Gf, dev = linalg_ops.glm_irls(self.X, aug=P, beta=bt, b0=float(self.beta[-1]), y=self._y32,
+                                                  wprior=self._w32, offset=self._off32, codes=codes,
+                                                  tvp=self.fam.tvp, theta=self.fam.theta, width=self.Pp, bf3=bf3)
                 dev = dev.view(1)
             else:
                 eta = self._eta()
@@ -537,7 +553,42 @@ class GLMDriver:
         return Gf[:P, :P], Gf[:P, P + 1].contiguous(), Gf[:P, P].contiguous(), Gf[P, P].view(1), \
             Gf[P, P + 1].view(1), dev
 
+    # Hessian precision tiers of the Newton step beta + H^-1 g (g from the exact
+    # gradient channel): the iteration contracts at rate ~ kappa * eps(H), so the
+    # tier is picked from the Jacobi-scaled condition number kappa of the system
+    # matrix.  bf16x3 MFMA (eps ~ 2e-5) while kappa < 2e3, f32 MFMA (eps ~ 1e-7)
+    # while kappa < 5e5, beyond that fp64 (the reference's Gram precision,
+    # hex/gram/Gram.java:17) on the device's f64 GEMMs.
+    _TIER_LIMITS = (("bf3", 2e3), ("f32", 5e5), ("f64", float("inf")))
+
+    def _tier_for(self, kappa):
+        for name, lim in self._TIER_LIMITS:
+            if kappa < lim:
+                return name
+        return "f64"
+
+    @staticmethod
+    def _scaled_cond(A, active=None):
+        idx = np.arange(A.shape[0]) if active is None else np.flatnonzero(active[:A.shape[0]])
+        d = np.diag(A)[idx]
+        idx = idx[d > 0]
+        if idx.size == 0:
+            return 1.0
+        d = np.sqrt(np.diag(A)[idx])
+        S = A[np.ix_(idx, idx)] / np.outer(d, d)
+        # LAPACK Cholesky + 1-norm condition estimate (dpotrf / dpocon: ~0.1 ms at
+        # P = 100, where a threaded eigvalsh costs ~10 ms per IRLS iteration)
+        from scipy.linalg import lapack
+        c, info = lapack.dpotrf(S, lower=1, clean=0)
+        if info != 0:
+            return float("inf")
+        rc, info = lapack.dpocon(c, float(np.abs(S).sum(0).max()), uplo="L")
+        return float(1.0 / rc) if info == 0 and rc > 0 else float("inf")
+
     def _irls_stats(self):
+        self._gexact = None
+        if self._hprec == "f64" and self.X.device.type == "cuda":
+            return self._irls_stats_f64()
         if self._native():
             G, xz, xw, sw, swz, dev = self._irls_stats_native()
             return self._finish_stats(G, xz, xw, sw, swz, dev)
@@ -552,8 +603,12 @@ class GLMDriver:
                     self._off32 = None if self.offset is None else self.offset.to(torch.float32)
                 P = self.P
                 bt = torch.as_tensor(self.beta[:P], dtype=torch.float32, device=self.X.device)
-                Gf, dev = linalg_ops.glm_wide_irls(self.X, P, bt, float(self.beta[-1]), self._y32, self._w32,
-                                                   self._off32, codes, self.fam.tvp, self.fam.theta)
+                Gf, dev, gx = linalg_ops.glm_wide_irls(self.X, P, bt, float(self.beta[-1]), self._y32,
+                                                       self._w32, self._off32, codes, self.fam.tvp, self.fam.theta)
+                if os.environ.get("H2O3_GLM_EXACT_GRAD", "1") != "0":
+                    self._gexact = gx[:P + 1]
+                    self._gbeta = np.concatenate([self.beta[:P].astype(np.float32).astype(np.float64),
+                                                  [float(np.float32(self.beta[-1]))]])
             return self._finish_stats(Gf[:P, :P], Gf[:P, P + 1].contiguous(), Gf[:P, P].contiguous(),
                                       Gf[P, P].view(1), Gf[P, P + 1].view(1), dev.view(1))
         with phase("glm.eta"):
@@ -586,25 +641,76 @@ class GLMDriver:
             dev = (self.w * self.fam.deviance(self.y, mu)).sum().view(1)
         return self._finish_stats(G, xz, xw, sw, swz, dev)
 
+    def _irls_stats_f64(self, step=1 << 21):
+        """fp64 IRLS statistics on the device (chunked f64 GEMMs): Gram,
+        exact gradient X'r (r = w (y - mu) dmu/deta / var) and deviance at the
+        f64 coefficients.  The top precision tier for ill-conditioned designs."""
+        P = self.P
+        X = self.X
+        dv = X.device
+        bt = torch.as_tensor(self.beta[:P], dtype=torch.float64, device=dv)
+        Ga = torch.zeros((P + 1, P + 1), dtype=torch.float64, device=dv)
+        g = torch.zeros(P + 1, dtype=torch.float64, device=dv)
+        dev = torch.zeros(1, dtype=torch.float64, device=dv)
+        ident = self.fam.family == "gaussian" and self.fam.link == "identity"
+        with phase("glm.irls_f64"):
+            for a in range(0, X.shape[0], step):
+                Xc = X[a:a + step, :P].to(torch.float64)
+                eta = Xc @ bt + float(self.beta[-1])
+                if self.offset is not None:
+                    eta = eta + self.offset[a:a + step]
+                w, y = self.w[a:a + step], self.y[a:a + step]
+                mu = self.fam.linkinv(eta)
+                if ident:
+                    W, r = w, w * (y - eta)
+                else:
+                    d = self.fam.dmu_deta(eta, mu)
+                    wd = w * d / self.fam.variance(mu)
+                    W, r = wd * d, wd * (y - mu)
+                Xa = torch.cat([Xc, torch.ones((Xc.shape[0], 1), dtype=torch.float64, device=dv)], 1)
+                del Xc
+                Ga += (Xa * W.view(-1, 1)).T @ Xa
+                g += Xa.T @ r
+                dev += (w * self.fam.deviance(y, mu)).sum()
+        self._gexact = g
+        self._gbeta = self.beta.copy()
+        z = torch.zeros(P, dtype=torch.float64, device=dv)
+        return self._finish_stats(Ga[:P, :P], z, Ga[:P, P].contiguous(), Ga[P, P].view(1),
+                                  torch.zeros(1, dtype=torch.float64, device=dv), dev)
+
     def _finish_stats(self, G, xz, xw, sw, swz, dev):
-        stats = torch.cat([G.reshape(-1), xz, xw, sw, swz, dev])
+        """All-reduce the IRLS sufficient statistics; returns (Gram [P+1, P+1]
+        with the intercept last, right-hand side b, deviance).
+
+        With the exact-gradient channel (self._gexact = X'r, r = w (y - mu)
+        dmu/deta / var, at the f32 coefficients the kernel used) the
+        right-hand side is G beta_f + g instead of the Gram's own X'Wz column:
+        identical in exact arithmetic (X'Wz = X'W eta + X'r), but the solve is
+        then a Newton step on an exact gradient, whose fixed point g = 0 does
+        not depend on the precision of the bf16x3 Hessian."""
+        gx = getattr(self, "_gexact", None)
+        parts = [G.reshape(-1), xz, xw, sw, swz, dev] + ([gx] if gx is not None else [])
+        stats = torch.cat(parts)
         coll.allreduce_(stats)
         P = self.P
         o = 0
         G = stats[o:o + P * P].view(P, P); o += P * P
         xz = stats[o:o + P]; o += P
         xw = stats[o:o + P]; o += P
-        sw, swz, dev = float(stats[o]), float(stats[o + 1]), float(stats[o + 2])
+        sw, swz, dev = float(stats[o]), float(stats[o + 1]), float(stats[o + 2]); o += 3
         Ga = np.zeros((P + 1, P + 1))
         Ga[:P, :P] = G.cpu().numpy()
         Ga[:P, P] = Ga[P, :P] = xw.cpu().numpy()
         Ga[P, P] = sw
-        b = np.concatenate([xz.cpu().numpy(), [swz]])
+        if gx is not None:
+            g = stats[o:o + P + 1].cpu().numpy()
+            b = Ga @ self._gbeta + g
+        else:
+            b = np.concatenate([xz.cpu().numpy(), [swz]])
         return Ga, b, dev
 
-    def step(self):
-        """One IRLS iteration (Gram on the matrix cores + host solve)."""
-        Ga, b, dev = self._irls_stats()
+    def _system(self, Ga, b):
+        """The penalized quadratic the IRLS step solves: (Gn, bn, l1, l2)."""
         r = self.obj_reg
         Gn, bn = Ga * r, b * r
         if not self.intercept:
@@ -624,6 +730,50 @@ class GLMDriver:
             k = Gn.shape[0]
             Gn[np.diag_indices(k)] += self.rho[:k]
             bn += (self.rho * self.beta_given)[:k]
+        return Gn, bn, l1, l2
+
+    def _check_tier(self, Ga, b):
+        """Hessian precision tier from the scaled condition number of this
+        iteration's system (checked at iterations 1, 2, 4, 8, ...); when the
+        tier must rise, the statistics are recomputed at the new tier."""
+        if self.X.device.type != "cuda" or os.environ.get("H2O3_GLM_TIERS", "1") == "0":
+            return Ga, b
+        it = self.iter + 1
+        if it & (it - 1):
+            return Ga, b
+        Gn, _, _, l2 = self._system(Ga, b)
+        if l2 > 0:
+            Gn = Gn.copy()
+            Gn[np.arange(self.P), np.arange(self.P)] += l2
+        kappa = self._scaled_cond(Gn, self.active)
+        self.hessian_kappa = kappa
+        order = [t for t, _ in self._TIER_LIMITS]
+        wide = not self._native()
+        cur = self._hprec
+        if cur is None:
+            ws_bf3 = self.Pp == 128 and os.environ.get("H2O3_GLM_BF3", "1") != "0"
+            cur = "bf3" if (ws_bf3 if not wide else self._gexact is not None) else "f32"
+        want = self._tier_for(kappa)
+        if want == "f32" and (wide or self._gexact is None):
+            # no f32 path with the gradient channel here: straight to fp64
+            want = "f64"
+        if order.index(want) > order.index(cur):
+            self._hprec = want
+            Ga, b, dev = self._irls_stats()
+            self._stats_dev = dev
+            return self._check_tier(Ga, b) if want != "f64" else (Ga, b)
+        if self._hprec is None:
+            self._hprec = cur
+        return Ga, b
+
+    def step(self):
+        """One IRLS iteration (Gram on the matrix cores + host solve)."""
+        Ga, b, dev = self._irls_stats()
+        self._stats_dev = dev
+        Ga, b = self._check_tier(Ga, b)
+        dev = self._stats_dev
+        r = self.obj_reg
+        Gn, bn, l1, l2 = self._system(Ga, b)
         if self.est._parms.get("remove_collinear_columns") and self.active is None:
             self.active = self._find_collinear(Gn)
             self.removed_cols = [self.dinfo.coef_names[i] for i in range(self.P) if not self.active[i]]

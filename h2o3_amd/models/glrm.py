@@ -327,7 +327,11 @@ class H2OGeneralizedLowRankEstimator(H2OEstimator):
         rx, ry = p.get("regularization_x"), p.get("regularization_y")
 
         def objective(X_, Y_):
-            return float(self._loss(A, M, X_ @ Y_, blocks)) + gx * float(_reg(rx, X_)) + gy * float(_reg(ry, Y_))
+            # X is row-sharded (loss and its regularizer are summed over the
+            # ranks), Y is replicated: every rank sees the same objective, so the
+            # step-size control flow (and the collective count) agrees
+            loc = self._loss(A, M, X_ @ Y_, blocks) + gx * _reg(rx, X_)
+            return coll.allreduce_scalar(float(loc)) + gy * float(_reg(ry, Y_))
 
         step = float(p.get("init_step_size", 1.0))
         min_step = float(p.get("min_step_size", 1e-4))
@@ -335,7 +339,7 @@ class H2OGeneralizedLowRankEstimator(H2OEstimator):
         hist = [obj]
         it = 0
         updates = 0
-        scale = 1.0 / max(n, 1)
+        scale = 1.0 / max(int(spec.frame.nrows), 1)    # global rows: the same Y step on every rank
         max_it, max_up = int(p.get("max_iterations", 1000)), int(p.get("max_updates", 2000))
         while it < max_it and updates < max_up and step >= min_step:
             it += 1

@@ -54,28 +54,38 @@ def save_model(model, path="", force=False, filename=None):
     # rank 0 checks and writes (the model is replicated); every rank agrees
     if coll.broadcast_object(os.path.exists(fn)) and not force:
         raise FileExistsError(fn)
-    if cloud.rank() != 0:
-        cloud.barrier()
-        return fn
-    params = {k: _jsonable(v) for k, v in model._parms.items()
-              if isinstance(v, (int, float, str, bool, list, type(None)))}
     from .state_io import dumps
-    try:
-        mojo = build_mojo(model)
-    except NotImplementedError:
-        mojo = None          # no MOJO for this algorithm: the state archive carries it
-    with zipfile.ZipFile(fn, "w", zipfile.ZIP_DEFLATED) as z:
-        z.writestr("state.pt", dumps(model))
-        if mojo is not None:
-            z.writestr("mojo.zip", mojo)
-        z.writestr("params.json", json.dumps({"algo": model.algo, "model_id": model.model_id, "params": params}))
-        z.writestr("metrics.json", json.dumps({"training": _metrics_dict(model._training_metrics),
-                                               "validation": _metrics_dict(model._validation_metrics),
-                                               "xval": _metrics_dict(model._cross_validation_metrics),
-                                               "output": {k: v for k, v in model._output.items()
-                                                          if isinstance(v, (dict, list, float, int, str))}},
-                                              default=str))
-    cloud.barrier()
+    # every rank packs (row-sharded state -- CV holdout predictions, GLRM X,
+    # SVD U frames -- is all-gathered so the archive holds every row)
+    state = dumps(model, gather=cloud.world() > 1)
+    err = None
+    if cloud.rank() == 0:
+        try:
+            params = {k: _jsonable(v) for k, v in model._parms.items()
+                      if isinstance(v, (int, float, str, bool, list, type(None)))}
+            try:
+                mojo = build_mojo(model)
+            except NotImplementedError:
+                mojo = None          # no MOJO for this algorithm: the state archive carries it
+            with zipfile.ZipFile(fn, "w", zipfile.ZIP_DEFLATED) as z:
+                z.writestr("state.pt", state)
+                if mojo is not None:
+                    z.writestr("mojo.zip", mojo)
+                z.writestr("params.json", json.dumps({"algo": model.algo, "model_id": model.model_id,
+                                                      "params": params}))
+                z.writestr("metrics.json", json.dumps({"training": _metrics_dict(model._training_metrics),
+                                                       "validation": _metrics_dict(model._validation_metrics),
+                                                       "xval": _metrics_dict(model._cross_validation_metrics),
+                                                       "output": {k: v for k, v in model._output.items()
+                                                                  if isinstance(v, (dict, list, float, int, str))}},
+                                                      default=str))
+        except Exception as e:          # noqa: BLE001 -- re-raised on every rank below
+            err = f"{type(e).__name__}: {e}"
+    # a failure on rank 0 is raised on every rank (no rank left waiting in a
+    # barrier that the writer's next collective would pair with)
+    err = coll.broadcast_object(err)
+    if err is not None:
+        raise RuntimeError(f"save_model failed on rank 0: {err}")
     return fn
 
 

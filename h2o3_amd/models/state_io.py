@@ -23,12 +23,22 @@ import torch
 
 _PREFIX = "h2o3_amd."
 _SKIP_ATTRS = {"_job", "_drv", "_lg", "_lg_key", "_pen_cache", "_graph", "_ea"}
+# estimator attributes holding per-rank ROW SHARDS as plain tensors (dim 0 =
+# this rank's rows): cross-validation holdout predictions, the GLRM row
+# representation X
+_SHARDED_ATTRS = {"_cv_holdout", "_X"}
 
 
 class _Packer:
-    def __init__(self):
+    """gather=True (multi-rank save, called on EVERY rank in the same order):
+    row-sharded state -- non-replicated Vecs and the _SHARDED_ATTRS tensors of
+    estimators -- is all-gathered into whole-frame arrays marked "sharded", so
+    the archive holds every row; loading re-shards them to the loading cloud."""
+
+    def __init__(self, gather=False):
         self.tensors = []
         self.memo = {}
+        self.gather = gather
 
     def t(self, x):
         self.tensors.append(x.detach().to("cpu").contiguous().clone())
@@ -70,6 +80,15 @@ class _Packer:
                     "index": self.pack(obj.index.to_numpy(), depth + 1)}
         from ..core.vec import Vec
         if isinstance(obj, Vec):
+            if self.gather and not obj.replicated:
+                from ..parallel import collectives as coll
+                if obj.on_host:
+                    data = np.array(sum(coll.all_gather_object(list(obj.data)), []), dtype=object)
+                else:
+                    data = coll.all_gather_var(obj.data)
+                return {"__vec": {"data": self.pack(data, depth + 1), "type": obj.type,
+                                  "domain": self.pack(obj.domain, depth + 1), "replicated": False,
+                                  "sharded": True}}
             return {"__vec": {"data": self.pack(obj.data, depth + 1), "type": obj.type,
                               "domain": self.pack(obj.domain, depth + 1), "replicated": bool(obj.replicated)}}
         cls = type(obj)
@@ -94,8 +113,16 @@ class _Packer:
             state["_parms"] = parms
         for k in _SKIP_ATTRS:
             state.pop(k, None)
-        return {"__obj": f"{mod}:{cls.__qualname__}", "id": ref,
-                "state": {"__dict": {k: self.pack(v, depth + 1) for k, v in state.items()}}}
+        packed = {}
+        for k, v in state.items():
+            if self.gather and k in _SHARDED_ATTRS and isinstance(obj, H2OEstimator) and \
+                    isinstance(v, torch.Tensor) and v.dim() >= 1:
+                from ..parallel import collectives as coll
+                packed[k] = {"__t": self.t(coll.all_gather_var(v.detach().contiguous())), "dev": v.device.type,
+                             "sharded": True}
+            else:
+                packed[k] = self.pack(v, depth + 1)
+        return {"__obj": f"{mod}:{cls.__qualname__}", "id": ref, "state": {"__dict": packed}}
 
 
 class _Unpacker:
@@ -113,6 +140,8 @@ class _Unpacker:
             return x
         if "__t" in x:
             t = self.tensors[x["__t"]]
+            if x.get("sharded"):
+                t = self._local(t)
             return t.to(self.device) if x.get("dev") == "cuda" and self.device.type == "cuda" else t
         if "__np" in x:
             return self.tensors[x["__np"]].numpy()
@@ -137,7 +166,10 @@ class _Unpacker:
         if "__vec" in x:
             from ..core.vec import Vec
             d = x["__vec"]
-            v = Vec(self.unpack(d["data"]), d["type"], self.unpack(d["domain"]))
+            data = self.unpack(d["data"])
+            if d.get("sharded"):
+                data = self._local(data)
+            v = Vec(data, d["type"], self.unpack(d["domain"]))
             v.replicated = d["replicated"]
             return v
         if "__skip" in x:
@@ -160,14 +192,23 @@ class _Unpacker:
         return {k: self.unpack(v) for k, v in x.items()}
 
     @staticmethod
+    def _local(t):
+        """This rank's row shard of a whole-frame array saved by a gathering
+        pack (the frame layout of core/frame._local_slice)."""
+        from ..core.frame import _local_slice
+        a, b = _local_slice(len(t))
+        return t[a:b]
+
+    @staticmethod
     def _hashable(k):
         if isinstance(k, list):
             return tuple(_Unpacker._hashable(v) for v in k)
         return k
 
 
-def dumps(est) -> bytes:
-    p = _Packer()
+def dumps(est, gather=False) -> bytes:
+    """gather=True: multi-rank save, a collective -- every rank must call it."""
+    p = _Packer(gather)
     tree = p.pack(est)
     buf = io.BytesIO()
     torch.save({"format": 1, "tree": tree, "tensors": p.tensors}, buf)

@@ -483,12 +483,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 // the MFMA accumulators in registers (f32 over <= 1024 rows) and fold them
 // into the block's own f64 tile (no atomics, deterministic).
 // ---------------------------------------------------------------------------
+//
+// Exact-gradient channel (FUSED + SQW, grad_out != nullptr): the producers
+// also accumulate g = X' r with r = W (z - eta + offset) = w (y - mu) dmu/deta
+// / var on the VALU as exact f64 products x r (an f32 x f32 product fits a
+// double) summed in f64, folded into per-wave f64 LDS slots every chunk, and
+// the block writes grad_out[split][PP + 1] (column PP = sum r, the intercept).
+// f64 products matter for ill-conditioned designs: independent f32 product
+// roundings of two near-collinear columns do not cancel along their weak
+// difference direction, and the Newton step divides by that eigenvalue.
+// The host then forms the IRLS right-hand side as G beta + g, so the Newton
+// step beta + G^-1 g has an exact fixed point (g = 0) whatever the precision
+// of the bf16x3 Hessian G: its precision only sets the convergence rate.
+// Reference: hex/glm/GLMTask.java:1507 (GLMIterationTask, double _xy) and
+// hex/gram/Gram.java:17 (double _xx).
 template <int PP, bool FUSED, bool SQW, bool BF3>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) void glm_irls_ws_kernel(
     const float* __restrict__ X, long long N, int ldx, int n_pairs, int rows_per_block,
     const float* __restrict__ beta, float b0, const float* __restrict__ y, const float* __restrict__ wprior,
     const float* __restrict__ offset, GlmFamArgs fam, const float* __restrict__ Wext,
-    const float* __restrict__ zext, int aug, double* __restrict__ out, double* __restrict__ dev_out) {
+    const float* __restrict__ zext, int aug, double* __restrict__ out, double* __restrict__ dev_out,
+    double* __restrict__ grad_out) {
   constexpr int RC = 64;
   constexpr int P4 = PP / 4;
   constexpr int T = PP / 16;
@@ -519,6 +534,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   constexpr bool QRED = P4 == 32;
   __shared__ __attribute__((aligned(16))) float es[QRED ? 4 : 1][QRED ? 128 : 4];
   __shared__ __attribute__((aligned(16))) float sqs[QRED ? 4 : 1][QRED ? 16 : 4];
+  // exact-gradient channel: per producer lane 4 f64 feature slots, per wave the
+  // per-row residuals r laid out like sqs
+  constexpr bool GRAD = FUSED && SQW;
+  __shared__ __attribute__((aligned(16))) double gs[GRAD ? 4 : 1][GRAD ? P4 : 1][GRAD ? 4 : 1];
+  __shared__ __attribute__((aligned(16))) float rqs[GRAD ? 4 : 1][GRAD ? 16 : 4];
+  __shared__ double gsum_s[4];
+  const bool want_grad = GRAD && grad_out != nullptr;
   const int split = blockIdx.x;
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
@@ -541,6 +563,45 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     constexpr bool DEEP = !FUSED;
     Stage A, B;
     double dev = 0.0;
+    double gsum = 0.0;   // lanes < 16: sum of r over this wave's rows (intercept gradient)
+    if (want_grad && lane < P4) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) gs[pw][lane][e] = 0.0;
+    }
+    // exact-gradient channel: the lane's NVP rows (row v RPV + lane / P4) times
+    // its 4 features as exact f64 products (f32 x f32 fits a double), summed in
+    // f64 over the lanes holding the same features, folded into LDS by lanes < P4
+    auto grad_acc = [&](const f32x4* V, float rres, bool qred) __attribute__((always_inline)) {
+      float rv[NVP];
+      if (QRED && qred) {
+        float* Q = rqs[pw];
+        if (lane < RPW) Q[(lane & 1) * 8 + (lane >> 1)] = rres;
+        const int par = lane / P4;
+        const f32x4 q0 = *reinterpret_cast<const f32x4*>(Q + par * 8);
+        const f32x4 q1 = *reinterpret_cast<const f32x4*>(Q + par * 8 + 4);
+        rv[0] = q0.x; rv[1] = q0.y; rv[2] = q0.z; rv[3] = q0.w;
+        rv[4] = q1.x; rv[5] = q1.y; rv[6] = q1.z; rv[7] = q1.w;
+      } else {
+#pragma unroll
+        for (int v = 0; v < NVP; ++v) rv[v] = __shfl(rres, v * RPV + lane / P4, 64);
+      }
+      double a[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        a[e] = 0.0;
+#pragma unroll
+        for (int v = 0; v < NVP; ++v) a[e] = fma((double)V[v][e], (double)rv[v], a[e]);
+      }
+#pragma unroll
+      for (int o = P4; o < 64; o <<= 1) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) a[e] += __shfl_xor(a[e], o, 64);
+      }
+      if (lane < P4) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) gs[pw][lane][e] += a[e];
+      }
+    };
     auto load = [&](int c, Stage& st) {
       f32x4* V = st.V;
       float& sy = st.sy;
@@ -617,7 +678,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
           if (lane / RPV == v) etav = got;
         }
       }
-      float W = 0.f, z = 0.f;
+      float W = 0.f, z = 0.f, rres = 0.f;
       if (lane < RPW) {
         const long long r = rb0 + (long long)c * RC + pw * RPW + lane;
         if (r < rb1) {
@@ -627,6 +688,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             if (fam.link == 0 && fam.var == 0) {
               W = sw;
               z = sy - so;
+              rres = sw * (sy - eta);
               if (sw != 0.f) dev += (double)(sw * gi_dev(fam, sy, mu));
             } else if (fam.link == 1 && fam.var == 1) {
               // canonical binomial: dmu/deta == variance, so W = w d and one
@@ -634,6 +696,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
               const float d = fmaxf(mu * (1.f - mu), 1e-10f);
               W = sw * d;
               z = (eta - so) + (sy - mu) * __frcp_rn(d);
+              rres = sw * (sy - mu);
               if (sw != 0.f) {
                 const float m = fminf(fmaxf(mu, 1e-15f), 1.f - 1e-7f);
                 const float dv = sy == 1.f ? -2.f * __logf(m) : sy == 0.f ? -2.f * __logf(1.f - m)
@@ -642,8 +705,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
               }
             } else {
               const float d = gi_dmu(fam.link, mu);
-              W = sw * d * d / gi_var(fam, mu);
+              const float wd = sw * d / gi_var(fam, mu);
+              W = wd * d;
               z = (eta - so) + (sy - mu) / d;
+              rres = wd * (sy - mu);
               if (sw != 0.f) dev += (double)(sw * gi_dev(fam, sy, mu));
             }
           } else {
@@ -651,6 +716,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             z = sy;
           }
         }
+        if (want_grad) gsum += (double)rres;
       }
       // SQW: rows are staged pre-scaled by sqrt(W) so the consumers' MFMA
       // operands come straight from LDS (no VALU between LDS and MFMA)
@@ -688,6 +754,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
           *reinterpret_cast<bf16x8*>(Hb + off) = h;
           *reinterpret_cast<bf16x8*>(Lb2 + off) = l;
         }
+        if constexpr (GRAD) {
+          if (want_grad) grad_acc(V, rres, qred);   // after the bf16 stores: the sqrt(W) factors are dead
+        }
         if (lane < RPW && aug >= 0) {
           const int k = pw * RPW + (lane % RPV) * 8 + lane / RPV;
           const float a0 = sq, a1 = sq * z;
@@ -707,6 +776,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         f32x4 val = V[v];
         if (SQW) val *= __shfl(sq, v * RPV + lane / P4, 64);
         *reinterpret_cast<f32x4*>(Lb + rl * S + 4 * cq) = val;
+      }
+      if constexpr (GRAD) {
+        if (want_grad) grad_acc(V, rres, qred);
       }
       if (lane < RPW) {
         const int rl = pw * RPW + lane;
@@ -747,8 +819,25 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       dev = wave_sum(dev);
       if (lane == 0) dsum[pw] = dev;
     }
+    if (want_grad) {
+      gsum = wave_sum(gsum);
+      if (lane == 0) gsum_s[pw] = gsum;
+    }
     __syncthreads();
     if (FUSED && threadIdx.x == 256) dev_out[split] = dsum[0] + dsum[1] + dsum[2] + dsum[3];
+    if constexpr (GRAD) {
+      if (want_grad) {
+        // feature f = 4 cq + e: slot [cq][e] of every producer wave
+        const int t = threadIdx.x - 256;
+        if (t < PP) {
+          const int cq2 = t >> 2, e = t & 3;
+          const double g = (gs[0][cq2][e] + gs[1][cq2][e]) + (gs[2][cq2][e] + gs[3][cq2][e]);
+          grad_out[(size_t)split * (PP + 1) + t] = g;
+        } else if (t == PP) {
+          grad_out[(size_t)split * (PP + 1) + PP] = gsum_s[0] + gsum_s[1] + gsum_s[2] + gsum_s[3];
+        }
+      }
+    }
   } else {
     // ============================ consumers ============================
     const int slot = __builtin_amdgcn_readfirstlane((wv + split) & 3);
@@ -846,7 +935,7 @@ template <int PP>
 static void gi_launch(bool fused, dim3 grid, hipStream_t s, const float* X, long long N, int ldx, const int2* pairs,
                       int n_pairs, int rpb, const float* beta, float b0, const float* y, const float* wprior,
                       const float* offset, GlmFamArgs fam, const float* Wext, const float* zext, int aug,
-                      double* out, double* dev_out) {
+                      double* out, double* dev_out, double* grad_out) {
   if constexpr (PP <= 128 && (PP & (PP - 1)) == 0) {
     // IRLS weights are >= 0 -> sqrt(W) pre-scaling; caller-signed weights
     // (e.g. X'r for lambda_max) take the explicit-multiply path
@@ -854,22 +943,22 @@ static void gi_launch(bool fused, dim3 grid, hipStream_t s, const float* X, long
       if (fam.bf3 && !fam.signed_w) {
         if (fused)
           hipLaunchKernelGGL((glm_irls_ws_kernel<PP, true, true, true>), dim3(grid.x), dim3(512), 0, s, X, N, ldx,
-                             n_pairs, rpb, beta, b0, y, wprior, offset, fam, Wext, zext, aug, out, dev_out);
+                             n_pairs, rpb, beta, b0, y, wprior, offset, fam, Wext, zext, aug, out, dev_out, grad_out);
         else
           hipLaunchKernelGGL((glm_irls_ws_kernel<PP, false, true, true>), dim3(grid.x), dim3(512), 0, s, X, N, ldx,
-                             n_pairs, rpb, beta, b0, y, wprior, offset, fam, Wext, zext, aug, out, dev_out);
+                             n_pairs, rpb, beta, b0, y, wprior, offset, fam, Wext, zext, aug, out, dev_out, nullptr);
         return;
       }
     }
     if (fused)
       hipLaunchKernelGGL((glm_irls_ws_kernel<PP, true, true, false>), dim3(grid.x), dim3(512), 0, s, X, N, ldx, n_pairs,
-                         rpb, beta, b0, y, wprior, offset, fam, Wext, zext, aug, out, dev_out);
+                         rpb, beta, b0, y, wprior, offset, fam, Wext, zext, aug, out, dev_out, grad_out);
     else if (!fam.signed_w)
       hipLaunchKernelGGL((glm_irls_ws_kernel<PP, false, true, false>), dim3(grid.x), dim3(512), 0, s, X, N, ldx, n_pairs,
-                         rpb, beta, b0, y, wprior, offset, fam, Wext, zext, aug, out, dev_out);
+                         rpb, beta, b0, y, wprior, offset, fam, Wext, zext, aug, out, dev_out, nullptr);
     else
       hipLaunchKernelGGL((glm_irls_ws_kernel<PP, false, false, false>), dim3(grid.x), dim3(512), 0, s, X, N, ldx, n_pairs,
-                         rpb, beta, b0, y, wprior, offset, fam, Wext, zext, aug, out, dev_out);
+                         rpb, beta, b0, y, wprior, offset, fam, Wext, zext, aug, out, dev_out, nullptr);
     return;
   }
   if constexpr (GiCfg<PP>::POW2) {
@@ -884,7 +973,7 @@ static void gi_launch(bool fused, dim3 grid, hipStream_t s, const float* X, long
 }
 
 // H2O3_GLM_BF3: 1 (default) bf16x3 MFMA for the P = 128 ws path, 0 f32 MFMA
-// (read per call: one getenv per IRLS pass)
+// (read per call: one getenv per IRLS pass; a caller's bf3 >= 0 overrides it)
 static int gi_bf3() {
   const char* e = getenv("H2O3_GLM_BF3");
   return e ? atoi(e) : 1;
@@ -909,7 +998,7 @@ extern "C" int h2o_glm_irls(const float* X, long long N, int P, int ldx, const i
                             int rows_per_block, const float* beta, float b0, const float* y, const float* wprior,
                             const float* offset, int link, int var, float tvp, float theta, const float* Wext,
                             const float* zext, int aug, int signed_w, double* out, double* dev_out,
-                            hipStream_t s) {
+                            double* grad_out, int bf3, hipStream_t s) {
   if (N <= 0 || n_pairs <= 0) return 0;
   if (P % 32 != 0 || P > 512) return -1;
   // narrow row storage (ldx < P) only on the warp-specialised path
@@ -919,13 +1008,16 @@ extern "C" int h2o_glm_irls(const float* X, long long N, int P, int ldx, const i
   if (rows_per_block % h2o_glm_irls_chunk(P) != 0) return -4;
   const int groups = (n_pairs + 4 * GI_PPW - 1) / (4 * GI_PPW);
   dim3 grid(n_splits, groups);
-  GlmFamArgs fam{link, var, tvp, theta, gi_dbg(), signed_w, gi_bf3()};
+  GlmFamArgs fam{link, var, tvp, theta, gi_dbg(), signed_w, bf3 < 0 ? gi_bf3() : bf3};
   const bool fused = beta != nullptr;
+  // the exact-gradient channel rides the fused ws kernel (P <= 128, power of
+  // two) only (grad_out: [n_splits][P + 1] doubles)
+  if (grad_out && !(fused && P <= 128 && (P & (P - 1)) == 0 && !signed_w)) return -6;
   const int2* pr = (const int2*)pairs;
 #define GI_CASE(pp)                                                                                          \
   case pp:                                                                                                   \
     gi_launch<pp>(fused, grid, s, X, N, ldx, pr, n_pairs, rows_per_block, beta, b0, y, wprior, offset, fam, Wext, \
-                  zext, aug, out, dev_out);                                                                  \
+                  zext, aug, out, dev_out, grad_out);                                                        \
     break;
   switch (P) {
     GI_CASE(32) GI_CASE(64) GI_CASE(96) GI_CASE(128) GI_CASE(160) GI_CASE(192) GI_CASE(224) GI_CASE(256)
@@ -1002,8 +1094,12 @@ template <int NQ>
 __global__ __launch_bounds__(256) void glm_wide_split_kernel(
     const float* __restrict__ X, int ldx, int P, int Pa, long long rows, const float* __restrict__ beta, float b0,
     const float* __restrict__ y, const float* __restrict__ wprior, const float* __restrict__ offset,
-    GlmFamArgs fam, __bf16* __restrict__ HL, double* __restrict__ dev_out) {
+    GlmFamArgs fam, __bf16* __restrict__ HL, double* __restrict__ dev_out, double* __restrict__ grad_out) {
+  // grad_out (optional): [gridDim.x][Pa] f64, this block's slot += X' r over
+  // its rows of the chunk (r = w (y - mu) dmu/deta / var: the exact-gradient
+  // channel, see glm_irls_ws_kernel); column P holds sum r
   __shared__ double dsum[4];
+  __shared__ float gsh[4][NQ * 256];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   f32x4 b[NQ];
@@ -1014,6 +1110,10 @@ __global__ __launch_bounds__(256) void glm_wide_split_kernel(
     for (int e = 0; e < 4; ++e) b[q][e] = c + e < P ? beta[c + e] : 0.f;
   }
   double dev = 0.0;
+  f32x4 ga[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) ga[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float gi = 0.f;
   const long long nw = (long long)gridDim.x * 4;
   for (long long r = (long long)blockIdx.x * 4 + wv; r < rows; r += nw) {
     f32x4 v[NQ];
@@ -1033,16 +1133,24 @@ __global__ __launch_bounds__(256) void glm_wide_split_kernel(
     const float sy = y[r], sw = wprior ? wprior[r] : 1.f, so = offset ? offset[r] : 0.f;
     const float eta = dot + b0 + so;
     const float mu = gi_linkinv(fam.link, eta);
-    float W, z;
+    float W, z, rres;
     if (fam.link == 0 && fam.var == 0) {
       W = sw;
       z = sy - so;
+      rres = sw * (sy - eta);
     } else {
       const float d = gi_dmu(fam.link, mu);
-      W = sw * d * d / gi_var(fam, mu);
+      const float wd = sw * d / gi_var(fam, mu);
+      W = wd * d;
       z = (eta - so) + (sy - mu) / d;
+      rres = wd * (sy - mu);
     }
     if (lane == 0 && sw != 0.f) dev += (double)(sw * gi_dev(fam, sy, mu));
+    if (grad_out) {
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) ga[q] += v[q] * rres;
+      gi += rres;
+    }
     const float s = sqrtf(fmaxf(W, 0.f));
     __bf16* o = HL + r * (2LL * Pa);
 #pragma unroll
@@ -1068,26 +1176,40 @@ __global__ __launch_bounds__(256) void glm_wide_split_kernel(
   }
   dev = wave_sum(dev);
   if (lane == 0) dsum[wv] = dev;
+  if (grad_out) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int c = 4 * (lane + 64 * q);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) gsh[wv][c + e] = c + e == P ? gi : ga[q][e];
+    }
+  }
   __syncthreads();
   if (threadIdx.x == 0) dev_out[blockIdx.x] = dsum[0] + dsum[1] + dsum[2] + dsum[3];
+  if (grad_out) {
+    for (int c = threadIdx.x; c < Pa; c += 256)
+      grad_out[(size_t)blockIdx.x * Pa + c] +=
+          ((double)gsh[0][c] + (double)gsh[1][c]) + ((double)gsh[2][c] + (double)gsh[3][c]);
+  }
 }
 
 // Pa <= 1024 (P <= 1022), Pa % 4 == 0; dev_out holds `blocks` doubles.
 extern "C" int h2o_glm_wide_split(const float* X, int ldx, int P, int Pa, long long rows, const float* beta, float b0,
                                   const float* y, const float* wprior, const float* offset, int link, int var,
-                                  float tvp, float theta, void* HL, double* dev_out, int blocks, hipStream_t s) {
+                                  float tvp, float theta, void* HL, double* dev_out, int blocks, double* grad_out,
+                                  hipStream_t s) {
   if (rows <= 0) return 0;
   if (Pa % 4 != 0 || Pa < P + 2 || ldx < P || blocks <= 0) return -1;
   GlmFamArgs fam{link, var, tvp, theta, 0, 0, 0};
   if (Pa <= 256)
     hipLaunchKernelGGL(glm_wide_split_kernel<1>, dim3(blocks), dim3(256), 0, s, X, ldx, P, Pa, rows, beta, b0, y,
-                       wprior, offset, fam, (__bf16*)HL, dev_out);
+                       wprior, offset, fam, (__bf16*)HL, dev_out, grad_out);
   else if (Pa <= 512)
     hipLaunchKernelGGL(glm_wide_split_kernel<2>, dim3(blocks), dim3(256), 0, s, X, ldx, P, Pa, rows, beta, b0, y,
-                       wprior, offset, fam, (__bf16*)HL, dev_out);
+                       wprior, offset, fam, (__bf16*)HL, dev_out, grad_out);
   else if (Pa <= 1024)
     hipLaunchKernelGGL(glm_wide_split_kernel<4>, dim3(blocks), dim3(256), 0, s, X, ldx, P, Pa, rows, beta, b0, y,
-                       wprior, offset, fam, (__bf16*)HL, dev_out);
+                       wprior, offset, fam, (__bf16*)HL, dev_out, grad_out);
   else
     return -2;
   return (int)hipGetLastError();

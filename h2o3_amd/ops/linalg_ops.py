@@ -21,10 +21,10 @@ def _lib():
         lib.h2o_gram.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_int, ctypes.c_void_p,
                                  ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         P, I, LL, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong, ctypes.c_float
-        lib.h2o_glm_irls.argtypes = [P, LL, I, I, P, I, I, I, P, F, P, P, P, I, I, F, F, P, P, I, I, P, P, P]
+        lib.h2o_glm_irls.argtypes = [P, LL, I, I, P, I, I, I, P, F, P, P, P, I, I, F, F, P, P, I, I, P, P, P, I, P]
         lib.h2o_glm_irls_chunk.argtypes = [I]
         lib.h2o_gram_split.argtypes = [P, I, I, I, P, P, LL, P, P]
-        lib.h2o_glm_wide_split.argtypes = [P, I, I, I, LL, P, F, P, P, P, I, I, F, F, P, P, I, P]
+        lib.h2o_glm_wide_split.argtypes = [P, I, I, I, LL, P, F, P, P, P, I, I, F, F, P, P, I, P, P]
         lib._typed = True
     return lib
 
@@ -70,7 +70,7 @@ def _ptr(t):
 
 
 def glm_irls(X, aug=-1, beta=None, b0=0.0, y=None, wprior=None, offset=None, codes=(0, 0), tvp=0.0, theta=1e-10,
-             W=None, z=None, signed=None, target_blocks=1024, width=None):
+             W=None, z=None, signed=None, target_blocks=1024, width=None, grad=False, bf3=None):
     """One pass of the fused IRLS kernel (ops/csrc/gram.hip glm_irls_kernel).
 
     Fused mode (beta given): per row eta = x.beta + b0 + offset, the family's
@@ -80,6 +80,11 @@ def glm_irls(X, aug=-1, beta=None, b0=0.0, y=None, wprior=None, offset=None, cod
     their cross terms when aug >= 0 — and the f64 deviance, or None).
     `width`: logical padded width Pp when X is stored narrower (X [N, ldx],
     ldx % 4 == 0, columns ldx..Pp-1 implicitly zero; Pp = 128 ws path only).
+    `grad=True` (fused mode, Pp in 32 / 64 / 128): also return the exact
+    gradient channel g [Pp + 1] f64 = X'r, r = w (y - mu) dmu/deta / var
+    (exact f64 products of the f32 values, f64 sums; g[Pp] = sum r) as a
+    third element.
+    `bf3`: override H2O3_GLM_BF3 for this call (False: f32 MFMA Gram).
     """
     N, ldx = X.shape
     P = int(width) if width else ldx
@@ -97,19 +102,31 @@ def glm_irls(X, aug=-1, beta=None, b0=0.0, y=None, wprior=None, offset=None, cod
     splits = -(-N // rpb)
     out = torch.zeros((splits, npairs, 16, 16), dtype=torch.float64, device=X.device)
     dev = torch.zeros(splits, dtype=torch.float64, device=X.device)
+    gout = torch.empty((splits, P + 1), dtype=torch.float64, device=X.device) if grad else None
     X = X.contiguous()
     bt = _f32(beta)
     keep = [_f32(y), _f32(wprior), _f32(offset), _f32(W), _f32(z)]
     if signed is None:
         signed = beta is None and keep[3] is not None and bool((keep[3] < 0).any())
-    rc = lib.h2o_glm_irls(_ptr(X), N, P, ldx, _ptr(pairs_t), npairs, splits, rpb, _ptr(bt), float(b0), _ptr(keep[0]),
-                          _ptr(keep[1]), _ptr(keep[2]), int(codes[0]), int(codes[1]), float(tvp), float(theta),
-                          _ptr(keep[3]), _ptr(keep[4]), int(aug), int(bool(signed)), _ptr(out), _ptr(dev),
+    rc = lib.h2o_glm_irls(_ptr(X), N, P, ldx, _ptr(pairs_t), npairs, splits, rpb, _ptr(bt), float(b0),
+                          _ptr(keep[0]), _ptr(keep[1]), _ptr(keep[2]), int(codes[0]), int(codes[1]), float(tvp),
+                          float(theta), _ptr(keep[3]), _ptr(keep[4]), int(aug), int(bool(signed)), _ptr(out),
+                          _ptr(dev), _ptr(gout), -1 if bf3 is None else int(bool(bf3)),
                           ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
     if rc != 0:
         raise RuntimeError(f"h2o_glm_irls failed: {rc}")
     G = _assemble(out.sum(0), pairs_t, T)
+    if grad:
+        return G, dev.sum(), gout.sum(0)
     return G, (dev.sum() if beta is not None else None)
+
+
+def glm_grad_supported(width):
+    """True when glm_irls(grad=True) runs at this padded width (the fused
+    warp-specialised kernel: Pp in 32 / 64 / 128).  H2O3_GLM_EXACT_GRAD=0
+    turns the channel off (A/B only: the IRLS right-hand side then comes from
+    the Gram's own X'Wz column)."""
+    return int(width) in (32, 64, 128) and os.environ.get("H2O3_GLM_EXACT_GRAD", "1") != "0"
 
 
 def glm_irls_reference(X, aug=-1, beta=None, b0=0.0, y=None, wprior=None, offset=None, fam=None, W=None, z=None):
@@ -147,7 +164,9 @@ def weighted_gram(X: torch.Tensor, w: torch.Tensor | None = None, use_native=Non
             return Xd.T @ Xd
         return Xd.T @ (Xd * w.to(torch.float64).view(-1, 1))
     if P <= 512:
-        return glm_irls(X, W=w)[0]
+        # f32 MFMA (f64 across row blocks): PCA / SVD / GLRM-init and p-values
+        # read these values directly, so no bf16x3 products here
+        return glm_irls(X, W=w, bf3=False)[0]
     if _wide_mode() == "bf3" and (w is None or bool((w >= 0).all())):
         return gram_aug_bf3(X, w, None, P)[:P, :P]
     if _wide_mode() == "gemm" and (w is None or bool((w >= 0).all())):
@@ -300,7 +319,9 @@ def glm_wide_irls(X, P, beta, b0, y, wprior=None, offset=None, codes=(1, 1), tvp
     """Fused IRLS pass for wide GLMs (P + 2 <= 1024): per row chunk one HIP
     kernel (glm_wide_split_kernel: eta, IRLS weight, working response,
     deviance, bf16 [hi | lo] split of sqrt(W) [x | 1 | z]) and one bf16 GEMM
-    with f32 output.  Returns (G [Pa, Pa] f64 augmented Gram, deviance f64)."""
+    with f32 output.  Returns (G [Pa, Pa] f64 augmented Gram, deviance f64,
+    g [Pa] f64 exact-gradient channel X'r with g[P] = sum r, r = w (y - mu)
+    dmu/deta / var: f32 VALU products over <= 64 rows per lane, f64 beyond)."""
     lib = _lib()
     if lib is None:
         raise RuntimeError("gram extension not built (run __graft_entry__.build())")
@@ -317,6 +338,7 @@ def glm_wide_irls(X, P, beta, b0, y, wprior=None, offset=None, codes=(1, 1), tvp
     HL = torch.empty((grp * st, 2 * Pa), dtype=torch.bfloat16, device=X.device)
     blocks = 2048
     dev = torch.zeros((nch, blocks), dtype=torch.float64, device=X.device)
+    gbuf = torch.zeros((blocks, Pa), dtype=torch.float64, device=X.device)
     G = torch.zeros((Pa, Pa), dtype=torch.float64, device=X.device)
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
@@ -328,13 +350,13 @@ def glm_wide_irls(X, P, beta, b0, y, wprior=None, offset=None, codes=(1, 1), tvp
                                     float(b0), off(keep[0], a), off(keep[1], a), off(keep[2], a), int(codes[0]),
                                     int(codes[1]), float(tvp), float(theta),
                                     ctypes.c_void_p(buf.data_ptr() + j * st * 2 * Pa * 2), _ptr(dev[i]), blocks,
-                                    strm)
+                                    _ptr(gbuf), strm)
         if rc != 0:
             raise RuntimeError(f"h2o_glm_wide_split failed: {rc}")
 
     if _overlap_ok(X, nch, grp):
         _pipelined_groups(split, HL, N, st, grp, Pa, G)
-        return G, dev.sum()
+        return G, dev.sum(), gbuf.sum(0)
     for i, a in enumerate(range(0, N, st)):
         r = min(st, N - a)
         j = i % grp
@@ -343,7 +365,7 @@ def glm_wide_irls(X, P, beta, b0, y, wprior=None, offset=None, codes=(1, 1), tvp
             HL[j * st + r:(j + 1) * st].zero_()
         if j == grp - 1 or i == nch - 1:
             _gram_group(HL[:(j + 1) * st], st, Pa, G)
-    return G, dev.sum()
+    return G, dev.sum(), gbuf.sum(0)
 
 
 def weighted_gram_aug(X: torch.Tensor, W: torch.Tensor, z: torch.Tensor, P: int, step: int = 1 << 20):

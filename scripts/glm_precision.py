@@ -1,8 +1,9 @@
 """GLM coefficient parity at the bench scale.
 
 Fits the bench's binomial IRLSM problem (100M x 100, synthetic, standardized
-design) to convergence twice -- Gram on bf16x3 split operands (default) and
-on f32 MFMA (H2O3_GLM_BF3=0) -- then runs an independent fp64 IRLS on the
+design) to convergence three times -- bf16x3 Hessian with the exact f32/f64
+gradient channel (default), bf16x3 Gram with its own X'Wz right-hand side
+(H2O3_GLM_EXACT_GRAD=0) and f32 MFMA (H2O3_GLM_BF3=0) -- then runs an independent fp64 IRLS on the
 very same device design matrix (f32 values are exact in f64; Gram, X'Wz,
 solve all in fp64) and reports per-iteration time of both MFMA paths and the
 coefficient differences against the fp64 solution.
@@ -45,8 +46,10 @@ def main():
     est._spec = spec
     res = {"rows": a.rows, "cols": a.cols, "model": "GLM binomial IRLSM, lambda=0, standardized design"}
     drv = None
-    for mode in ("1", "0"):
-        os.environ["H2O3_GLM_BF3"] = mode
+    modes = {"bf16x3_exact_grad": ("1", "1"), "bf16x3_gram_rhs": ("1", "0"), "f32": ("0", "1")}
+    for name, (bf3, exact) in modes.items():
+        os.environ["H2O3_GLM_BF3"] = bf3
+        os.environ["H2O3_GLM_EXACT_GRAD"] = exact
         drv = GLMDriver(est, spec)
         times = []
         while not drv.converged and drv.iter < 25:
@@ -55,10 +58,10 @@ def main():
             drv.step()
             sync()
             times.append(time.time() - t0)
-        res["bf16x3" if mode == "1" else "f32"] = {
+        res[name] = {
             "iterations": drv.iter, "ms_per_iter_median": 1000 * statistics.median(times),
             "ms_per_iter_all": [round(1000 * t, 3) for t in times], "beta_std": drv.beta.tolist()}
-        print(mode, drv.iter, 1000 * statistics.median(times), flush=True)
+        print(name, drv.iter, 1000 * statistics.median(times), flush=True)
     # independent fp64 IRLS on the same design (drv.X holds the standardized f32 rows)
     X, y, w = drv.X, drv.y, drv.w
     P = drv.P
@@ -92,7 +95,7 @@ def main():
     import numpy as np
     ref = np.array(b64)
     scale = max(float(np.abs(ref).max()), 1e-300)
-    for k in ("bf16x3", "f32"):
+    for k in modes:
         bb = np.array(res[k]["beta_std"])
         res[k]["max_abs_diff_vs_fp64"] = float(np.abs(bb - ref).max())
         res[k]["max_rel_diff_vs_fp64"] = float((np.abs(bb - ref) / np.maximum(np.abs(ref), 1e-3)).max())

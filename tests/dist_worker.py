@@ -97,12 +97,47 @@ def run(out_path):
     mb = gbm.model_performance(fr)
     res["bin_tab_rows"] = len(mb["thresholds_and_metric_scores"]["threshold"])
     res["bin_prauc"] = mb.aucpr()
+    res["persist"] = _persist_roundtrip(h2o, fr, x, os.path.dirname(out_path))
     from h2o3_amd.parallel import cloud
     if cloud.rank() == 0:
         with open(out_path, "w") as f:
             json.dump(res, f)
     cloud.barrier()
     cloud.shutdown()
+
+
+def _persist_roundtrip(h2o, fr, x, out_dir):
+    """Binary save / load of models with row-sharded state: a CV GBM with
+    kept holdout predictions and a GLRM (per-row X).  The archive must hold
+    every row and the loaded model must hold this rank's shard again."""
+    import torch
+    from h2o3_amd.estimators import H2OGeneralizedLowRankEstimator, H2OGradientBoostingEstimator
+    from h2o3_amd.parallel import cloud
+    from h2o3_amd.parallel import collectives as coll
+    out = {}
+    d = os.path.join(out_dir, f"models_w{cloud.world()}")
+    cv = H2OGradientBoostingEstimator(ntrees=3, max_depth=3, seed=1, nfolds=2, fold_assignment="Modulo",
+                                      keep_cross_validation_predictions=True)
+    cv.train(x=x, y="y", training_frame=fr)
+    p = h2o.save_model(cv, d, force=True)
+    lm = h2o.load_model(p)
+    hold0 = coll.all_gather_var(cv._cv_holdout.double())
+    hold1 = coll.all_gather_var(lm._cv_holdout.double())
+    out["cv_holdout_local_rows_ok"] = bool(coll.all_gather_object(lm._cv_holdout.shape[0] == fr.nlocal) ==
+                                           [True] * cloud.world())
+    out["cv_holdout_equal"] = bool(torch.equal(hold0, hold1))
+    out["cv_holdout_sum"] = round(float(hold1.sum()), 9)
+    cvp = lm.cross_validation_holdout_predictions()
+    out["cv_pred_rows"] = cvp.nrow
+    glrm = H2OGeneralizedLowRankEstimator(k=2, seed=3, max_iterations=20)
+    glrm.train(x=[f"x{i}" for i in range(6)], training_frame=fr)
+    p = h2o.save_model(glrm, d, force=True)
+    lg = h2o.load_model(p)
+    x0 = coll.all_gather_var(glrm._X.detach().double())
+    x1 = coll.all_gather_var(lg._X.detach().double())
+    out["glrm_x_equal"] = bool(torch.equal(x0, x1))
+    out["glrm_x_rows"] = int(x1.shape[0])
+    return out
 
 
 if __name__ == "__main__":

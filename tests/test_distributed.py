@@ -54,6 +54,18 @@ def results(tmp_path_factory):
     return one, two
 
 
+def test_persist_sharded_state(results):
+    """save_model / load_model of models with row-sharded state (CV holdout
+    predictions, GLRM X) on 2 ranks: the archive holds all rows, each loaded
+    rank holds its shard, and the values equal the saved ones."""
+    one, two = results
+    for r in (one, two):
+        p = r["persist"]
+        assert p["cv_holdout_equal"] and p["cv_holdout_local_rows_ok"] and p["glrm_x_equal"], p
+        assert p["cv_pred_rows"] == 4000 and p["glrm_x_rows"] == 4000, p
+    assert abs(one["persist"]["cv_holdout_sum"] - two["persist"]["cv_holdout_sum"]) < 1e-6
+
+
 def test_rows_sharded(results):
     one, two = results
     assert one["nrow"] == two["nrow"] == 4000

@@ -177,14 +177,159 @@ def test_glm_wide_irls_matches_fp64(family, link):
     fam = _Fam(family, link)
     codes = linalg_ops.glm_fused_codes(family, link)
     Xn = X[:, :P].contiguous()
-    Gk, dk = linalg_ops.glm_wide_irls(Xn.cuda(), P, beta[:P].cuda(), -0.2, y.cuda(), w.cuda(), off.cuda(), codes,
-                                      step=16_384)
+    Gk, dk, gk = linalg_ops.glm_wide_irls(Xn.cuda(), P, beta[:P].cuda(), -0.2, y.cuda(), w.cuda(), off.cuda(),
+                                          codes, step=16_384)
     Gr, dr = linalg_ops.glm_irls_reference(X, aug=P, beta=beta, b0=-0.2, y=y, wprior=w, offset=off, fam=fam)
     A, B = Gk[: P + 2, : P + 2].cpu(), Gr[: P + 2, : P + 2]
     diag = B.diagonal().abs().sqrt().clamp_min(1e-12)
     rel = (A - B).abs() / (diag.view(-1, 1) * diag.view(1, -1))
     assert rel.max().item() < 5e-5
     assert abs(dk.item() - dr.item()) / abs(dr.item()) < 1e-4
+    # exact-gradient channel: X'r and sum r against fp64
+    gr = _grad_reference(X[:, :P], beta[:P], -0.2, y, w, off, fam)
+    _assert_grad_close(torch.cat([gk[:P], gk[P:P + 1]]).cpu(), gr, X[:, :P], y, w)
+
+
+def _grad_reference(X, beta, b0, y, w, off, fam):
+    """fp64 X'r (+ sum r last), r = w (y - mu) dmu/deta / var."""
+    Xd = X.double()
+    eta = Xd @ beta.double() + b0 + (0.0 if off is None else off.double())
+    mu = fam.linkinv(eta)
+    wd = torch.ones_like(eta) if w is None else w.double()
+    if fam.family == "gaussian" and fam.link == "identity":
+        r = wd * (y.double() - eta)
+    else:
+        r = wd * (y.double() - mu) * fam.dmu_deta(eta, mu) / fam.variance(mu)
+    return torch.cat([Xd.T @ r, r.sum().view(1)])
+
+
+def _assert_grad_close(gk, gr, X, y, w):
+    # error bound: f32 rounding of the per-row terms, relative to sum |x r|
+    # (the gradient itself may be near zero by cancellation)
+    scale = (X.double().abs().sum(0).max() * (y.double().abs().max() + 1) *
+             (1.0 if w is None else float(w.max()))).item()
+    err = (gk.double() - gr).abs().max().item()
+    assert err / scale < 1e-6, (err, scale)
+
+
+@pytest.mark.parametrize("family,link", [("binomial", "logit"), ("poisson", "log"), ("gaussian", "identity"),
+                                         ("gamma", "log"), ("tweedie", "log")])
+@pytest.mark.parametrize("narrow,bf3,P,Pp", [(False, True, 100, 128), (True, True, 100, 128),
+                                             (True, False, 100, 128), (False, False, 50, 64),
+                                             (False, False, 30, 32)])
+def test_glm_irls_grad_channel(family, link, narrow, bf3, P, Pp):
+    """Exact-gradient channel of the fused ws kernel (bf16x3 or f32 Hessian):
+    g = X'r and sum r with exact f64 products / f64 sums vs fp64 torch."""
+    n = 200_003
+    X, beta, g = _data(n, P, Pp, seed=21)
+    eta = X @ beta + 0.2
+    if family == "binomial":
+        y = (torch.rand(n, generator=g) < torch.sigmoid(eta)).float()
+    elif family == "gaussian":
+        y = eta + torch.randn(n, generator=g)
+    else:
+        y = torch.distributions.Poisson(torch.exp(eta)).sample() + (0.5 if family == "gamma" else 0.0)
+    w = torch.rand(n, generator=g) + 0.5
+    off = 0.1 * torch.randn(n, generator=g)
+    fam = _Fam(family, link, tvp=1.5 if family == "tweedie" else 0.0)
+    codes = linalg_ops.glm_fused_codes(family, link)
+    Xk = X[:, :P].contiguous() if narrow else X
+    Gk, dk, gk = linalg_ops.glm_irls(Xk.cuda(), aug=P, beta=beta.cuda(), b0=0.2, y=y.cuda(), wprior=w.cuda(),
+                                     offset=off.cuda(), codes=codes, tvp=fam.tvp, theta=fam.theta, width=Pp,
+                                     grad=True, bf3=bf3)
+    assert gk.shape == (Pp + 1,)
+    assert gk[P:Pp].abs().max().item() == 0.0          # padding / augmented columns carry no gradient
+    gr = _grad_reference(X[:, :P], beta[:P], 0.2, y, w, off, fam)
+    _assert_grad_close(torch.cat([gk[:P], gk[Pp:]]).cpu(), gr, X[:, :P], y, w)
+    # the Hessian and deviance of the same pass are unchanged by the channel
+    G0, d0 = linalg_ops.glm_irls(Xk.cuda(), aug=P, beta=beta.cuda(), b0=0.2, y=y.cuda(), wprior=w.cuda(),
+                                 offset=off.cuda(), codes=codes, tvp=fam.tvp, theta=fam.theta, width=Pp, bf3=bf3)
+    assert torch.equal(G0, Gk) and torch.equal(d0, dk)
+
+
+def _fp64_irls(X, y, beta0, iters=30):
+    """Reference fp64 IRLS (binomial, intercept last) on a host design."""
+    Xa = torch.cat([X.double(), torch.ones(X.shape[0], 1, dtype=torch.float64, device=X.device)], 1)
+    b = torch.as_tensor(beta0, dtype=torch.float64, device=X.device).clone()
+    for _ in range(iters):
+        eta = Xa @ b
+        mu = torch.sigmoid(eta)
+        W = (mu * (1 - mu)).clamp_min(1e-10)
+        G = Xa.T @ (Xa * W.view(-1, 1))
+        nb = b + torch.linalg.solve(G, Xa.T @ (y.double() - mu))
+        if (nb - b).abs().max() < 1e-13:
+            b = nb
+            break
+        b = nb
+    return b, G
+
+
+def _glm_fit_modes(Xh, y, modes, monkeypatch, iters=30):
+    import numpy as np
+    from h2o3_amd.models.base import TrainSpec
+    from h2o3_amd.core.frame import H2OFrame
+    from h2o3_amd.models.glm.glm import GLMDriver, H2OGeneralizedLinearEstimator
+    P = Xh.shape[1]
+    cols = {f"x{j}": Xh[:, j] for j in range(P)}
+    cols["y"] = y
+    fr = H2OFrame(cols)
+    fr["y"] = fr["y"].asfactor()
+    res, drvs = {}, {}
+    for name, env in modes.items():
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        est = H2OGeneralizedLinearEstimator(family="binomial", solver="IRLSM", lambda_=0.0)
+        spec = TrainSpec(fr, [f"x{j}" for j in range(P)], "y")
+        est._spec = spec
+        drv = GLMDriver(est, spec)
+        assert drv.X.is_cuda
+        for _ in range(iters):
+            drv.step()
+        res[name], drvs[name] = drv.beta.copy(), drv
+    return res, drvs
+
+
+_DEFAULT = {"H2O3_GLM_BF3": "1", "H2O3_GLM_EXACT_GRAD": "1", "H2O3_GLM_TIERS": "1"}
+_LEGACY_F32 = {"H2O3_GLM_BF3": "0", "H2O3_GLM_EXACT_GRAD": "0", "H2O3_GLM_TIERS": "0"}
+_LEGACY_BF3 = {"H2O3_GLM_BF3": "1", "H2O3_GLM_EXACT_GRAD": "0", "H2O3_GLM_TIERS": "0"}
+
+
+@pytest.mark.parametrize("noise,tier", [(1e-3, "f64"), (2e-2, "f32"), (None, "bf3")])
+def test_glm_conditioning_tiers_match_fp64(monkeypatch, noise, tier):
+    """Newton on the exact gradient channel with the Hessian precision tier
+    picked from the scaled condition number: a well-conditioned design stays
+    on bf16x3, two columns at correlation 1 - 2e-4 (kappa ~ 1e4) move to the
+    f32 Hessian, correlation 1 - 5e-7 (kappa >= 1e6) to fp64.  Every tier
+    lands on the fp64 IRLS solution; at kappa >= 1e6 the legacy paths (Gram
+    right-hand side, no tiers) are off by orders of magnitude more."""
+    import numpy as np
+    g = np.random.default_rng(5)
+    n, P = 400_000, 100
+    Xh = g.standard_normal((n, P)).astype(np.float32)
+    if noise is not None:
+        Xh[:, 1] = Xh[:, 0] + noise * g.standard_normal(n).astype(np.float32)
+    b = np.zeros(P)
+    b[:10] = g.standard_normal(10)
+    b[0], b[1] = 1.0, -0.5
+    y = (g.random(n) < 1 / (1 + np.exp(-(Xh.astype(np.float64) @ b)))).astype(int)
+    modes = {"default": _DEFAULT}
+    if tier == "f64":
+        modes.update({"f32": _LEGACY_F32, "bf3_rhs": _LEGACY_BF3})
+    res, drvs = _glm_fit_modes(Xh, y, modes, monkeypatch)
+    drv = drvs["default"]
+    assert drv._hprec == tier, (drv._hprec, drv.hessian_kappa)
+    Xs = drv.X[:, :P].float()
+    ref, G = _fp64_irls(Xs, drv.y, drv._init_beta)
+    ref = ref.cpu().numpy()
+    ev = torch.linalg.eigvalsh((G[:P, :P] / n).cpu())
+    kappa = (ev.max() / ev.min()).item()
+    if tier == "f64":
+        assert kappa >= 1e6
+    scale = np.abs(ref).max()
+    err = {k: np.abs(v - ref).max() / scale for k, v in res.items()}
+    assert err["default"] < 1e-6, (err, kappa)
+    if tier == "f64":
+        assert err["f32"] > 100 * err["default"] and err["bf3_rhs"] > 100 * err["default"], err
 
 
 def test_gram_aug_bf3_matches_fp64():
@@ -231,9 +376,9 @@ def test_wide_split_gemm_overlap_matches_sequential(monkeypatch):
     out = {}
     for mode in ("0", "1"):
         monkeypatch.setenv("H2O3_WIDE_OVERLAP", mode)
-        G, d = linalg_ops.glm_wide_irls(X, P, beta, 0.1, y, None, None, codes, step=4096)
+        G, d, gx = linalg_ops.glm_wide_irls(X, P, beta, 0.1, y, None, None, codes, step=4096)
         Ga = linalg_ops.gram_aug_bf3(X, W, y, P, step=4096)
         torch.cuda.synchronize()
-        out[mode] = (G.cpu(), d.cpu(), Ga.cpu())
+        out[mode] = (G.cpu(), d.cpu(), Ga.cpu(), gx.cpu())
     for a, b in zip(out["0"], out["1"]):
         assert torch.equal(a, b)
