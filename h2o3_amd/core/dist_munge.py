@@ -14,8 +14,10 @@ rank owning their key range; each rank then sorts / joins its range with
 the same device code as the one-rank path, so the result is the one-rank
 result, sharded in rank order.  Group-by never moves rows: per-group partial
 sums / counts / extrema are reduced with one bucketed all-reduce (a second
-one for the centred sums of squares); only median / mode gather the
-(group, value) pairs of their column.
+one for the centred sums of squares); median / mode route each group's
+(group, value) pairs to the rank owning that group range.  Sort moves only
+the keys to find each row's global position (sampled splitters, no key
+gather), then every column once to its position's owner.
 
 Frames with host (string / UUID) columns keep the gather path.
 """
@@ -73,29 +75,82 @@ def _splitters(sample, W):
 
 
 # ------------------------------------------------------------------ sort
+def _lex_ge(K, s):
+    """Row-wise K >= s (lexicographic) for a key matrix K [n, d] and one
+    splitter row s [d]."""
+    cmp = torch.zeros(K.shape[0], dtype=torch.int8, device=K.device)
+    for j in range(K.shape[1]):
+        d = torch.sign(K[:, j] - s[j]).to(torch.int8)
+        cmp = torch.where(cmp == 0, d, cmp)
+    return cmp >= 0
+
+
+def sort_positions(keys, samples_per_rank=256):
+    """Global 0-based stable sort position (int64) of every local row for f64
+    sort keys (NaN mapped beforehand, descending keys negated).  RadixOrder /
+    AstSort without gathering keys: each rank contributes a sample of key
+    rows, the W-1 splitters of the merged sample define key ranges, every row
+    (keys + global row id, so ties keep row order and ranges split evenly)
+    goes once to its range owner, which sorts its range; the positions go
+    back with a second all_to_all.  At one rank: one local lexsort."""
+    from .dist_ops import lexsort
+    dev = _dev()
+    n = keys[0].numel() if keys else 0
+    W, r = cloud.world(), cloud.rank()
+    off = int(sum(coll.all_gather_object(int(n))[:r])) if W > 1 else 0
+    gid = torch.arange(n, device=dev, dtype=torch.int64) + off
+    K = torch.stack([k.to(torch.float64) for k in keys] + [gid.to(torch.float64)], 1)
+    if W == 1:
+        pos = torch.empty(n, dtype=torch.int64, device=dev)
+        pos[lexsort([K[:, j] for j in range(K.shape[1])])] = torch.arange(n, device=dev)
+        return pos
+    g = torch.Generator(device=dev)
+    g.manual_seed(7919 + r)
+    m = min(n, samples_per_rank)
+    samp = K[torch.randperm(n, generator=g, device=dev)[:m]] if m else K[:0]
+    S = coll.all_gather_var(samp)
+    S = S[lexsort([S[:, j] for j in range(S.shape[1])])]
+    if S.shape[0]:
+        q = ((torch.arange(1, W, device=dev, dtype=torch.float64) / W) * (S.shape[0] - 1)).round().long()
+        spl = S[q]
+    else:
+        spl = S
+    dest = torch.zeros(n, dtype=torch.int64, device=dev)
+    for i in range(spl.shape[0]):
+        dest += _lex_ge(K, spl[i]).to(torch.int64)
+    src = torch.full((n,), r, dtype=torch.int64, device=dev)
+    loc = torch.arange(n, device=dev, dtype=torch.int64)
+    got = exchange([Vec(K, T_REAL), Vec(src, T_INT), Vec(loc, T_INT)], dest)
+    RK = got[0].data
+    o = lexsort([RK[:, j] for j in range(RK.shape[1])])
+    cnt = coll.all_gather_object(int(RK.shape[0]))
+    base = int(sum(cnt[:r]))
+    rpos = torch.empty(RK.shape[0], dtype=torch.int64, device=dev)
+    rpos[o] = torch.arange(RK.shape[0], device=dev) + base
+    back = exchange([Vec(rpos, T_INT), Vec(got[2].data, T_INT)], got[1].data)
+    pos = torch.empty(n, dtype=torch.int64, device=dev)
+    pos[back[1].data] = back[0].data
+    return pos
+
+
 def sort(fr, by, ascending):
     """Globally sorted frame (NAs first, stable), sharded in rank order:
-    output rank r holds sorted positions [r*N/W, (r+1)*N/W)."""
+    output rank r holds sorted positions [r*N/W, (r+1)*N/W).  Only the key
+    columns travel to compute positions (sort_positions); every frame column
+    then moves once, straight to the rank owning its sorted position."""
     from .munging import _key_tensor
     by = by if isinstance(by, (list, tuple)) else [by]
     asc = ascending if isinstance(ascending, (list, tuple)) else [ascending] * len(by)
     dev = _dev()
-    W, r = cloud.world(), cloud.rank()
+    W = cloud.world()
     n = fr.nlocal
-    # the key columns only (not the frame) are all-gathered; every rank computes
-    # the same permutation the one-rank path computes
-    keys = [coll.all_gather_var(_key_tensor(fr.vec(b))) for b in by]
-    N = keys[0].numel() if keys else 0
-    idx = torch.arange(N, device=dev)
-    for k, a in reversed(list(zip(keys, asc))):
-        k = k[idx]
+    keys = []
+    for b, a in zip(by, asc):
+        k = _key_tensor(fr.vec(b))
         k = torch.where(torch.isnan(k), torch.full_like(k, -math.inf), k)
-        idx = idx[torch.argsort(k if a else -k, stable=True)]
-    del keys
-    pos = torch.empty(N, dtype=torch.int64, device=dev)
-    pos[idx] = torch.arange(N, device=dev)
-    off = fr.row_offset()
-    mypos = pos[off:off + n]
+        keys.append(k if a else -k)
+    mypos = sort_positions(keys)
+    N = int(coll.allreduce_scalar(float(n)))
     bounds = torch.tensor([(N * q) // W for q in range(W + 1)], dtype=torch.int64, device=dev)
     dest = (torch.searchsorted(bounds, mypos, right=True) - 1).clamp(0, W - 1)
     got = exchange(list(fr._vecs) + [Vec(mypos, T_INT)], dest)
@@ -219,21 +274,9 @@ def group_by(fr, by, aggs):
         elif op in ("sd", "var", "ss"):
             ss = SQ[sq_idx[(op, c, na)]]
             res = ss if op == "ss" else (ss / (nn - 1) if op == "var" else torch.sqrt(ss / (nn - 1)))
-        else:   # median / mode: the (group, value) pairs of this column only
-            x = fr.vec(c).as_float(torch.float64)
-            ga = coll.all_gather_var(gid)
-            xa = coll.all_gather_var(x)
-            res = torch.empty(G, dtype=torch.float64, device=dev)
-            for gi in range(G):
-                vv = xa[ga == gi]
-                vv = vv[~torch.isnan(vv)]
-                if vv.numel() == 0:
-                    res[gi] = float("nan")
-                elif op == "median":
-                    res[gi] = torch.quantile(vv, 0.5)
-                else:
-                    u, cts = torch.unique(vv, return_counts=True)
-                    res[gi] = u[torch.argmax(cts)]
+        else:   # median / mode: rows routed to the owner of their group range
+            from .dist_ops import group_median_mode
+            res = group_median_mode(gid, fr.vec(c).as_float(torch.float64), G, op)
         out_vecs.append(Vec(res, T_REAL))
         out_names.append(f"{op}_{c}")
     for v in out_vecs:

@@ -981,7 +981,7 @@ class H2OFrame:
 
     def rank_within_group_by(self, group_by_cols, sort_cols, ascending=None, new_col_name="New_Rank_column", sort_cols_sorted=False):
         from .munging import rank_within_group_by
-        return rank_within_group_by(self, group_by_cols, sort_cols, ascending, new_col_name)
+        return rank_within_group_by(self, group_by_cols, sort_cols, ascending, new_col_name, sort_cols_sorted)
 
     def topN(self, column=0, nPercent=10, grabTopN=-1):
         from .munging import topn

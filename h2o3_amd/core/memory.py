@@ -148,6 +148,13 @@ class MemoryManager:
             self.resident -= nb
             self.spills += 1
             return
+        if clean is not None and clean[0][0] == "disk":
+            # reloaded from disk, then modified: that older spill file is stale
+            _unlink(clean[0][1])
+            try:
+                v._clean = None
+            except AttributeError:
+                pass
         to_disk = dev.type == "cpu" or (self.host_cap is not None and self.host_bytes + nb > self.host_cap)
         if to_disk:
             d = self.spill_dir or os.path.join(tempfile.gettempdir(), f"h2o3_spill_{os.getpid()}")
@@ -165,6 +172,11 @@ class MemoryManager:
             h.copy_(t, non_blocking=False)
             v._sp = ("host", h, str(dev), int(t.shape[0]) if t.dim() else 0)
             self.host_bytes += nb
+            # a Vec collected while spilled returns its host bytes to the cap
+            try:
+                v._spf = weakref.finalize(v, _host_release, weakref.ref(self), nb)
+            except AttributeError:
+                pass
         v._d = None
         self._lru.pop(key, None)
         self.resident -= nb
@@ -179,6 +191,10 @@ class MemoryManager:
                 clean = (sp, t._version)       # the file stays valid until t is modified in place
             else:
                 t = payload.to(dev, non_blocking=False)
+                fin = getattr(vec, "_spf", None)
+                if fin is not None:
+                    fin.detach()
+                    vec._spf = None
                 self.host_bytes -= self._nbytes(payload)
                 clean = None
             vec._sp = None
@@ -190,6 +206,12 @@ class MemoryManager:
             self.reloads += 1
             self.track(vec)
             return t
+
+
+def _host_release(mref, nb):
+    m = mref()
+    if m is not None:
+        m.host_bytes -= nb
 
 
 def _unlink(path):

@@ -8,8 +8,10 @@ hex/SplitFrame.java, hex/createframe/*.
 
 Design: group-by / merge / sort use GPU primitives (torch.unique with
 inverse, argsort, searchsorted, index_add) on the HBM-resident columns.
-With several ranks, order-dependent ops gather the keys (small) and
-re-shard the result.
+With several ranks, sort / group-by / merge route rows with all_to_all
+(core/dist_munge.py) and quantile / unique / table / hist / cor / cov /
+pivot / melt / rank_within_group_by / interaction / drop_duplicates reduce
+per-rank partials (core/dist_ops.py): no frame gathers, no pandas.
 """
 from __future__ import annotations
 
@@ -30,132 +32,42 @@ def _dev():
 
 # ---------------------------------------------------------------- quantiles
 def quantile_values(v: Vec, probs, method="interpolate", weights=None):
-    x = v.as_float(torch.float64)
-    ok = ~torch.isnan(x)
-    x = x[ok]
-    w = None if weights is None else weights[ok].to(torch.float64)
-    if cloud.is_distributed():
-        x = coll.all_gather_var(x)
-        if w is not None:
-            w = coll.all_gather_var(w)
-    if x.numel() == 0:
-        return [float("nan")] * len(probs)
-    o = torch.argsort(x)
-    xs = x[o]
-    out = []
-    if w is not None:
-        ws = w[o]
-        cw = torch.cumsum(ws, 0)
-        tot = float(cw[-1])
-        for p in probs:
-            t = p * tot
-            i = int(torch.searchsorted(cw, torch.tensor([t], dtype=cw.dtype, device=cw.device)).clamp(max=xs.numel() - 1))
-            out.append(float(xs[i]))
-        return out
-    n = xs.numel()
-    for p in probs:
-        # reference (hex/quantile/Quantile.java): R type-7 interpolation
-        h = (n - 1) * p
-        lo = int(math.floor(h))
-        hi = min(lo + 1, n - 1)
-        if method in ("low",):
-            out.append(float(xs[lo]))
-        elif method in ("high",):
-            out.append(float(xs[hi]))
-        elif method == "average":
-            out.append(float((xs[lo] + xs[hi]) / 2) if h != lo else float(xs[lo]))
-        else:
-            out.append(float(xs[lo] + (h - lo) * (xs[hi] - xs[lo])))
-    return out
+    """Exact quantiles by distributed histogram refinement (core/dist_ops.py,
+    hex/quantile/Quantile.java): no column gather at any W."""
+    from .dist_ops import quantile_values as qv
+    return qv(v, probs, method, weights)
 
 
 def quantile(fr, prob=None, combine_method="interpolate", weights_column=None):
+    from .dist_ops import _sharded_from_replicated
     probs = prob if prob is not None else [0.001, 0.01, 0.1, 0.25, 0.333, 0.5, 0.667, 0.75, 0.9, 0.99, 0.999]
     w = fr.vec(weights_column).as_float() if weights_column else None
-    data = {"Probs": probs}
+    dev = _dev()
+    vecs, names = [Vec(torch.tensor(probs, dtype=torch.float64, device=dev), T_REAL)], ["Probs"]
     for n, v in zip(fr.names, fr._vecs):
         if n == weights_column:
             continue
-        if v.is_numeric or v.is_time:
-            data[f"{n}Quantiles"] = quantile_values(v, probs, combine_method, w)
-        else:
-            data[f"{n}Quantiles"] = [float("nan")] * len(probs)
-    import pandas as pd
-    return H2OFrame(pd.DataFrame(data), _local=not cloud.is_distributed())
+        q = quantile_values(v, probs, combine_method, w) if (v.is_numeric or v.is_time) else [float("nan")] * len(probs)
+        vecs.append(Vec(torch.tensor(q, dtype=torch.float64, device=dev), T_REAL))
+        names.append(f"{n}Quantiles")
+    return _sharded_from_replicated(vecs, names)
 
 
-# ---------------------------------------------------------------- unique / table
 def unique(fr, include_nas=False):
-    v = fr.gather()._vecs[0]
-    if v.type == T_ENUM:
-        codes = torch.unique(v.data)
-        if not include_nas:
-            codes = codes[codes >= 0]
-        return _reshard(H2OFrame.from_vecs([Vec(codes.to(torch.int32), T_ENUM, v.domain)], fr.names[:1]))
-    if v.on_host:
-        vals = sorted(set(x for x in v.data if x is not None or include_nas), key=lambda s: (s is None, s))
-        return _reshard(H2OFrame.from_vecs([make_string(vals)], fr.names[:1]))
-    x = v.as_float(torch.float64)
-    u = torch.unique(x[~torch.isnan(x)])
-    if include_nas and bool(torch.isnan(x).any()):
-        u = torch.cat([u, torch.tensor([float("nan")], dtype=u.dtype, device=u.device)])
-    return _reshard(H2OFrame.from_vecs([Vec(u.to(torch.float32) if v.data.dtype == torch.float32 else u, v.type)],
-                                       fr.names[:1]))
+    from .dist_ops import unique as _u
+    return _u(fr, include_nas)
 
 
 def table(fr, data2=None, dense=True):
-    import pandas as pd
-    g = fr.gather()
-    if data2 is not None:
-        g = g.cbind(data2.gather())
-    cols = g.names[:2] if data2 is not None or g.ncols >= 2 else g.names[:1]
-    df = g[cols].as_data_frame()
-    res = df.groupby(cols, dropna=True).size().reset_index(name="Counts")
-    if not dense and len(cols) == 2:
-        res = res.pivot(index=cols[0], columns=cols[1], values="Counts").fillna(0).reset_index()
-    return H2OFrame(res, column_types={c: "enum" for c in cols if g.vec(c).type == T_ENUM})
+    from .dist_ops import table as _t
+    return _t(fr, data2, dense)
 
 
 def hist(fr, breaks="sturges"):
-    v = fr._vecs[0]
-    x = v.as_float(torch.float64)
-    x = x[~torch.isnan(x)]
-    if cloud.is_distributed():
-        x = coll.all_gather_var(x)
-    n = x.numel()
-    lo, hi = float(x.min()), float(x.max())
-    if isinstance(breaks, (list, tuple)):
-        edges = np.asarray(breaks, dtype=float)
-    else:
-        if breaks == "sturges" or breaks is None:
-            k = int(math.ceil(math.log2(max(n, 1)) + 1))
-        elif breaks == "rice":
-            k = int(math.ceil(2 * n ** (1 / 3)))
-        elif breaks == "sqrt":
-            k = int(math.ceil(math.sqrt(n)))
-        elif breaks == "doane":
-            k = int(math.ceil(math.log2(max(n, 1)) + 1))
-        elif breaks == "scott":
-            sd = float(x.std())
-            k = int(math.ceil((hi - lo) / (3.5 * sd / n ** (1 / 3)))) if sd > 0 else 1
-        elif breaks == "fd":
-            q = torch.quantile(x[: min(n, 1 << 24)], torch.tensor([0.25, 0.75], dtype=x.dtype, device=x.device))
-            iqr = float(q[1] - q[0])
-            k = int(math.ceil((hi - lo) / (2 * iqr / n ** (1 / 3)))) if iqr > 0 else 1
-        else:
-            k = int(breaks)
-        edges = np.linspace(lo, hi, k + 1)
-    e = torch.tensor(edges, dtype=x.dtype, device=x.device)
-    idx = torch.clamp(torch.searchsorted(e, x, right=True) - 1, 0, len(edges) - 2)
-    counts = torch.bincount(idx, minlength=len(edges) - 1).cpu().numpy()
-    import pandas as pd
-    mids = (edges[:-1] + edges[1:]) / 2
-    df = pd.DataFrame({"breaks": edges[1:], "counts": counts.astype(float), "mids_true": mids, "mids": mids,
-                       "density": counts / max(counts.sum(), 1) / np.diff(edges)})
-    return H2OFrame(df)
+    from .dist_ops import hist as _h
+    return _h(fr, breaks)
 
 
-# ---------------------------------------------------------------- stats
 def _num_matrix(fr):
     return torch.stack([v.as_float(torch.float64) for v in fr._vecs], 1)
 
@@ -171,40 +83,14 @@ def _cross(ac, bc):
 
 
 def cor(x, y=None, method="Pearson", use="everything"):
-    """AstCorrelation: use = "everything" (NAs propagate), "all.obs" (NAs are
-    an error) or "complete.obs" (rows with an NA in any column are dropped)."""
-    a = _num_matrix(x.gather())
-    b = _num_matrix(y.gather()) if y is not None else a
-    use = (use or "everything").lower()
-    if use not in ("everything", "all.obs", "complete.obs"):
-        raise ValueError(f"use must be everything, all.obs or complete.obs, got {use}")
-    if use != "everything":
-        bad = torch.isnan(a).any(1) | torch.isnan(b).any(1)
-        if use == "all.obs" and bool(bad.any()):
-            raise ValueError("Missing values in the data: use complete.obs or everything")
-        if bool(bad.any()):
-            a, b = a[~bad], b[~bad]
-    if method.lower() == "spearman":
-        a = torch.argsort(torch.argsort(a, 0), 0).to(torch.float64)
-        b = torch.argsort(torch.argsort(b, 0), 0).to(torch.float64)
-    ac = a - a.mean(0)
-    bc = b - b.mean(0)
-    c = _cross(ac, bc) / torch.sqrt(torch.outer((ac ** 2).sum(0), (bc ** 2).sum(0)))
-    if c.numel() == 1:
-        return float(c)
-    import pandas as pd
-    return H2OFrame(pd.DataFrame(c.cpu().numpy(), columns=(y or x).names))
+    """AstCorrelation without gathers (core/dist_ops.cor)."""
+    from .dist_ops import cor as _c
+    return _c(x, y, method, use)
 
 
 def cov(x, y=None):
-    a = _num_matrix(x.gather())
-    b = _num_matrix(y.gather()) if y is not None else a
-    n = a.shape[0]
-    c = _cross(a - a.mean(0), b - b.mean(0)) / (n - 1)
-    if c.numel() == 1:
-        return float(c)
-    import pandas as pd
-    return H2OFrame(pd.DataFrame(c.cpu().numpy(), columns=(y or x).names))
+    from .dist_ops import cov as _c
+    return _c(x, y)
 
 
 def distance(x, y, measure="l2"):
@@ -470,18 +356,8 @@ class GroupBy:
                 ss = torch.zeros(G, dtype=torch.float64, device=x.device).index_add_(0, inv, torch.where(ok > 0, d * d, torch.zeros_like(d)))
                 r = ss if op == "ss" else (ss / (n - 1) if op == "var" else torch.sqrt(ss / (n - 1)))
             elif op in ("median", "mode"):
-                r = torch.empty(G, dtype=torch.float64, device=x.device)
-                o = torch.argsort(inv * 0 + x)
-                for gi in range(G):
-                    vals = x[inv == gi]
-                    vals = vals[~torch.isnan(vals)]
-                    if vals.numel() == 0:
-                        r[gi] = float("nan")
-                    elif op == "median":
-                        r[gi] = torch.quantile(vals, 0.5)
-                    else:
-                        u, cts = torch.unique(vals, return_counts=True)
-                        r[gi] = u[torch.argmax(cts)]
+                from .dist_ops import segment_median_mode
+                r = segment_median_mode(inv, x, G, op)
             out_vecs.append(Vec(r, T_REAL))
             out_names.append(f"{op}_{c}")
         res = H2OFrame.from_vecs(out_vecs, out_names)
@@ -915,46 +791,24 @@ def apply(fr, fun, axis=0):
 
 
 def drop_duplicates(fr, columns=None, keep="first"):
-    g = fr.gather()
-    cols = columns or g.names
-    _, inv = _group_ids(g, cols)
-    n = g.nlocal
-    pos = torch.arange(n, device=_dev())
-    G = int(inv.max()) + 1 if n else 0
-    if keep == "first":
-        sel = torch.full((G,), n, dtype=torch.int64, device=_dev()).scatter_reduce(0, inv, pos, reduce="amin")
-    else:
-        sel = torch.full((G,), -1, dtype=torch.int64, device=_dev()).scatter_reduce(0, inv, pos, reduce="amax")
-    sel = torch.sort(sel).values
-    res = H2OFrame.from_vecs([_take(v, sel) for v in g._vecs], g.names)
-    return _reshard(res) if cloud.is_distributed() else res
+    from .dist_ops import drop_duplicates as _d
+    return _d(fr, columns, keep)
 
 
 def pivot(fr, index, column, value):
-    import pandas as pd
-    df = fr.gather()[[index, column, value]].as_data_frame()
-    p = df.pivot_table(index=index, columns=column, values=value, aggfunc="first").reset_index()
-    p.columns = [str(c) for c in p.columns]
-    return H2OFrame(p)
+    from .dist_ops import pivot as _p
+    return _p(fr, index, column, value)
 
 
 def melt(fr, id_vars, value_vars=None, var_name="variable", value_name="value", skipna=False):
-    import pandas as pd
-    df = fr.gather().as_data_frame()
-    m = df.melt(id_vars=id_vars, value_vars=value_vars, var_name=var_name, value_name=value_name)
-    if skipna:
-        m = m.dropna(subset=[value_name])
-    return H2OFrame(m, column_types={var_name: "enum"})
+    from .dist_ops import melt as _m
+    return _m(fr, id_vars, value_vars, var_name, value_name, skipna)
 
 
-def rank_within_group_by(fr, group_by_cols, sort_cols, ascending=None, new_col_name="New_Rank_column"):
-    import pandas as pd
-    g = fr.gather()
-    df = g.as_data_frame()
-    asc = ascending if ascending is not None else [True] * len(sort_cols)
-    df = df.sort_values(list(group_by_cols) + list(sort_cols), ascending=[True] * len(group_by_cols) + list(asc))
-    df[new_col_name] = df.groupby(list(group_by_cols)).cumcount() + 1
-    return H2OFrame(df)
+def rank_within_group_by(fr, group_by_cols, sort_cols, ascending=None, new_col_name="New_Rank_column",
+                         sort_cols_sorted=False):
+    from .dist_ops import rank_within_group_by as _r
+    return _r(fr, group_by_cols, sort_cols, ascending, new_col_name, sort_cols_sorted)
 
 
 def topn(fr, column=0, nPercent=10, grabTopN=-1):
@@ -968,18 +822,8 @@ def topn(fr, column=0, nPercent=10, grabTopN=-1):
 
 
 def interaction(data, factors, pairwise, max_factors, min_occurrence):
-    import itertools
-    import pandas as pd
-    df = data.gather().as_data_frame()
-    names = [data.names[f] if isinstance(f, int) else f for f in factors]
-    combos = list(itertools.combinations(names, 2)) if pairwise else [tuple(names)]
-    out = {}
-    for cmb in combos:
-        col = df[list(cmb)].astype(str).agg("_".join, axis=1)
-        vc = col.value_counts()
-        keep = set(vc[vc >= min_occurrence].index[:max_factors])
-        out["_".join(cmb)] = col.where(col.isin(keep), "other")
-    return H2OFrame(pd.DataFrame(out), column_types={k: "enum" for k in out})
+    from .dist_ops import interaction as _i
+    return _i(data, factors, pairwise, max_factors, min_occurrence)
 
 
 def create_frame(frame_id=None, rows=10000, cols=10, randomize=True, real_fraction=None, categorical_fraction=None,

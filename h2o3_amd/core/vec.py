@@ -34,7 +34,7 @@ NUMERIC_TYPES = (T_REAL, T_INT)
 
 
 class Vec:
-    __slots__ = ("_d", "_sp", "_clean", "type", "domain", "_rollups", "_nrow_global", "replicated", "__weakref__")
+    __slots__ = ("_d", "_sp", "_clean", "_spf", "type", "domain", "_rollups", "_nrow_global", "replicated", "__weakref__")
 
     def __init__(self, data, vtype: str = T_REAL, domain=None):
         self._sp = None

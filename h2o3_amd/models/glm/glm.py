@@ -214,12 +214,20 @@ def _solve_quadratic(G, b, l1, l2, intercept, beta0=None, non_negative=False, ma
     if l1 == 0 and not boxed:
         import scipy.linalg as sla
         A = G + np.diag(l2 * pen)
-        try:
-            cf = sla.cho_factor(A + np.eye(P) * 1e-12 * max(1.0, np.abs(np.diag(A)).max()), lower=True,
-                                check_finite=False)
-            return sla.cho_solve(cf, b, check_finite=False)
-        except np.linalg.LinAlgError:
-            return np.linalg.lstsq(A, b, rcond=None)[0]
+        # a ridge only when the plain factorization fails, and then relative to
+        # each diagonal entry: an absolute ridge eps * max(diag) biases the
+        # Newton fixed point (g = eps beta) of unstandardized designs by ~1e-5
+        dA = np.diag(A)
+        floor = 1e-12 * max(1.0, float(np.abs(dA).max()) if dA.size else 1.0)
+        dead = dA <= 0
+        for ridge in ((0.0, 1e-12, 1e-9) if not dead.any() else (1e-12, 1e-9)):
+            try:
+                Ar = A if ridge == 0.0 else A + np.diag(np.where(dead, floor, ridge * np.abs(dA)))
+                cf = sla.cho_factor(Ar, lower=True, check_finite=False)
+                return sla.cho_solve(cf, b, check_finite=False)
+            except np.linalg.LinAlgError:
+                continue
+        return np.linalg.lstsq(A, b, rcond=None)[0]
     beta = np.zeros(P) if beta0 is None else np.clip(beta0.copy(), lo, hi)
     cd = _native_cd()
     if cd is not None:
@@ -478,6 +486,12 @@ class GLMDriver:
     # ---- device-side pieces
     def _eta(self, beta=None):
         b = self.beta if beta is None else beta
+        if self.X.device.type == "cpu":
+            # host path: f64 like the reference (f32 linear predictors move an
+            # unstandardized design's solution by ~1e-4)
+            bt = torch.as_tensor(b[: self.P], dtype=torch.float64)
+            eta = self.X[:, : self.P].to(torch.float64) @ bt + b[-1]
+            return eta + self.offset if self.offset is not None else eta
         bt = torch.zeros(self.X.shape[1], dtype=torch.float32, device=self.X.device)
         bt[: self.P] = torch.as_tensor(b[: self.P], dtype=torch.float32)
         eta = (self.X @ bt).to(torch.float64) + b[-1]
@@ -587,7 +601,9 @@ class GLMDriver:
 
     def _irls_stats(self):
         self._gexact = None
-        if self._hprec == "f64" and self.X.device.type == "cuda":
+        if self._hprec == "f64" or self.X.device.type == "cpu":
+            # fp64 tier on the device, and always on the host (the reference's
+            # double Gram / gradient, hex/gram/Gram.java:17)
             return self._irls_stats_f64()
         if self._native():
             G, xz, xw, sw, swz, dev = self._irls_stats_native()

@@ -54,8 +54,12 @@ def _store():
 
 
 class Heartbeat:
-    def __init__(self, rank, world, interval, suspect_s, store=None):
+    def __init__(self, rank, world, interval, suspect_s, store=None, epoch=""):
         self.rank, self.world = rank, world
+        # keys are scoped by a per-init epoch agreed by the ranks: a cloud
+        # re-initialised on the same rendezvous store must not read the
+        # previous session's "departed" counters as its peers' state
+        self.epoch = str(epoch)
         self.interval, self.suspect_s = float(interval), float(suspect_s)
         self.store = store if store is not None else _store()
         self._stop = threading.Event()
@@ -65,7 +69,7 @@ class Heartbeat:
         self.th = threading.Thread(target=self._run, name="h2o3-heartbeat", daemon=True)
 
     def key(self, r):
-        return f"h2o3_hb/{r}"
+        return f"h2o3_hb/{self.epoch}/{r}" if self.epoch else f"h2o3_hb/{r}"
 
     def _run(self):
         while not self._stop.is_set():
@@ -129,6 +133,12 @@ def start(rank=None, world=None):
     suspect = float(os.environ.get("H2O3_HB_SUSPECT", 60))
     r = cloud._state["rank"] if rank is None else rank
     w = cloud._state["world"] if world is None else world
+    epoch = ""
     if dist.is_initialized():
         r, w = dist.get_rank(), dist.get_world_size()
-    return Heartbeat(r, w, interval, suspect).start()
+        # one random epoch id for this init, broadcast from rank 0 over the
+        # control plane (gloo) -- every rank calls start() from cloud.init
+        obj = [os.urandom(8).hex() if r == 0 else None]
+        dist.broadcast_object_list(obj, src=0, group=cloud._state.get("ctl"))
+        epoch = obj[0]
+    return Heartbeat(r, w, interval, suspect, epoch=epoch).start()

@@ -98,12 +98,54 @@ def run(out_path):
     res["bin_tab_rows"] = len(mb["thresholds_and_metric_scores"]["threshold"])
     res["bin_prauc"] = mb.aucpr()
     res["persist"] = _persist_roundtrip(h2o, fr, x, os.path.dirname(out_path))
+    res["dist_ops"] = _dist_ops(h2o)
     from h2o3_amd.parallel import cloud
     if cloud.rank() == 0:
         with open(out_path, "w") as f:
             json.dump(res, f)
     cloud.barrier()
     cloud.shutdown()
+
+
+def _dist_ops(h2o):
+    """Shard-local munging prims (core/dist_ops.py): the results must not
+    depend on the number of ranks."""
+    import numpy as np
+    import pandas as pd
+    rng = np.random.default_rng(21)
+    n = 5000
+    df = pd.DataFrame({"a": rng.integers(0, 6, n).astype(float), "b": rng.choice(["x", "y", "z", "w"], n),
+                       "v": rng.normal(size=n), "t": rng.integers(0, 40, n).astype(float),
+                       "c": rng.choice(["p", "q", "r"], n)})
+    df.loc[::17, "v"] = np.nan
+    df.loc[::29, "a"] = np.nan
+    fr = h2o.H2OFrame(df)
+    fr["c"] = fr["c"].asfactor()
+    fr["b"] = fr["b"].asfactor()
+
+    def rows(f):
+        d = f.as_data_frame()
+        return [[None if (isinstance(v, float) and v != v) else (round(v, 9) if isinstance(v, float) else str(v))
+                 for v in r] for r in d.values.tolist()]
+    out = {}
+    out["quantile"] = rows(fr[["v", "t"]].quantile([0.01, 0.25, 0.5, 0.9]))
+    out["quantile_w"] = rows(fr[["v", "t"]].quantile([0.2, 0.7], weights_column="t"))
+    out["table1"] = rows(fr["t"].table())
+    out["table2"] = rows(fr[["b", "a"]].table())
+    out["table_sparse"] = rows(fr[["b", "c"]].table(dense=False))
+    out["unique"] = rows(fr["a"].unique())
+    out["hist"] = rows(fr["v"].hist(breaks=12))
+    out["cor"] = rows(fr[["v", "t", "a"]].cor(use="complete.obs"))
+    out["spearman"] = rows(fr[["v", "t"]].cor(use="complete.obs", method="Spearman"))
+    out["dedup"] = rows(fr.drop_duplicates(["a", "b"], keep="last"))
+    out["pivot"] = rows(fr[fr["a"] >= 0].pivot("a", "c", "v"))
+    out["melt"] = rows(fr[["t", "v", "a"]].melt(["t"], skipna=True))
+    out["rank"] = rows(fr.rank_within_group_by(["b"], ["t", "v"], [True, False], "rk"))
+    out["inter"] = rows(fr.interaction(["b", "c"], pairwise=False, max_factors=7, min_occurrence=2))
+    gb = fr.group_by(["b"]).median("v", na="rm").mode("t").get_frame()
+    out["gb_med_mode"] = rows(gb)
+    out["sort_dups"] = rows(fr.sort(["c", "t"], ascending=[False, True]))
+    return out
 
 
 def _persist_roundtrip(h2o, fr, x, out_dir):

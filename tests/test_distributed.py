@@ -54,6 +54,16 @@ def results(tmp_path_factory):
     return one, two
 
 
+@pytest.mark.parametrize("op", ["quantile", "quantile_w", "table1", "table2", "table_sparse", "unique", "hist", "cor",
+                                "spearman", "dedup", "pivot", "melt", "rank", "inter", "gb_med_mode", "sort_dups"])
+def test_dist_ops_match_one_rank(results, op):
+    """Quantile / table / unique / hist / cor / pivot / melt / rank-within-group /
+    interaction / drop_duplicates / median-mode / sort computed shard-locally
+    on 2 ranks equal the one-rank results (no frame gathers on either)."""
+    one, two = results
+    assert one["dist_ops"][op] == two["dist_ops"][op]
+
+
 def test_persist_sharded_state(results):
     """save_model / load_model of models with row-sharded state (CV holdout
     predictions, GLRM X) on 2 ranks: the archive holds all rows, each loaded

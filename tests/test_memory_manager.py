@@ -65,3 +65,32 @@ def test_gbm_on_frame_three_times_the_budget(tmp_path):
     for t1, t2 in zip(ref._forest.trees, m._forest.trees):
         assert list(np.asarray(t1.feat)) == list(np.asarray(t2.feat))
     np.testing.assert_allclose(p, p_ref, rtol=1e-6, atol=1e-7)
+
+
+
+@pytest.mark.gpu
+def test_host_spill_bytes_released_when_vec_dies():
+    """A Vec collected while spilled to host memory returns its bytes to the
+    host tier, and reload returns them too (host_bytes only fell
+    on reload, so after churn every later spill went to disk)."""
+    import gc
+    import torch
+    from h2o3_amd.core.memory import MemoryManager
+    from h2o3_amd.core.vec import T_REAL, Vec
+    mm = MemoryManager()
+    mm.set_budget(1 << 40, host_cap=1 << 40)
+    vs = [Vec(torch.randn(1 << 16, device="cuda"), T_REAL) for _ in range(3)]
+    for v in vs:
+        mm.track(v)
+    nb = (1 << 16) * 4
+    for v in vs:
+        mm._spill(id(v), v)
+    assert mm.host_bytes == 3 * nb
+    mm.reload(vs[0])
+    assert mm.host_bytes == 2 * nb
+    del vs[1]
+    gc.collect()
+    assert mm.host_bytes == nb
+    del vs
+    gc.collect()
+    assert mm.host_bytes == 0
