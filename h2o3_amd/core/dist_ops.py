@@ -130,6 +130,71 @@ def kth_smallest(x: torch.Tensor, k: int) -> float:
         cand = cand[bins == j]
 
 
+def kth_smallest_many(x: torch.Tensor, ks) -> dict:
+    """{k: k-th smallest (0-based)} for many ranks k at once over every rank's
+    x (no NaN): each refinement pass is ONE pass over the surviving
+    candidates -- every targeted bin of the previous pass becomes a group with
+    its own exact [min, max] range and 1024 sub-bins, counted with one
+    all-reduced bincount over all groups -- and groups with few values (or a
+    single value) are finished exactly from a gather of their values."""
+    ks_l = sorted(set(int(k) for k in ks))
+    if not ks_l:
+        return {}
+    dev = x.device
+    cand = x.to(torch.float64)
+    gid = torch.zeros(cand.numel(), dtype=torch.int64, device=dev)
+    tk = torch.tensor(ks_l, dtype=torch.int64, device=dev)       # target ranks
+    tg = torch.zeros_like(tk)                                      # their group
+    goff = torch.zeros(1, dtype=torch.int64, device=dev)          # rank offset per group
+    res = torch.full((tk.numel(),), math.nan, dtype=torch.float64, device=dev)
+    tpos = torch.arange(tk.numel(), device=dev)                   # slot of each live target in res
+    while tk.numel():
+        G = goff.numel()
+        cnt = _ar(torch.bincount(gid, minlength=G))
+        inf = torch.full((G,), math.inf, dtype=torch.float64, device=dev)
+        mm = torch.stack([inf.scatter_reduce(0, gid, cand, "amin"), inf.scatter_reduce(0, gid, -cand, "amin")])
+        _ar(mm, "min")
+        mn, mx = mm[0], -mm[1]
+        small = (cnt <= _GATHER_AT) | (mn == mx)
+        if bool(small.any()):
+            pick = small[gid]
+            gv, gg = _gather(cand[pick]), _gather(gid[pick])
+            o = lexsort([gg.to(torch.float64), gv])
+            gv, gg = gv[o], gg[o]
+            st = torch.searchsorted(gg, torch.arange(G, device=dev))
+            ts = small[tg]
+            g_s = tg[ts]
+            pos = (st[g_s] + tk[ts] - goff[g_s]).clamp(0, max(gv.numel() - 1, 0))
+            val = torch.where(mn[g_s] == mx[g_s], mn[g_s], gv[pos] if gv.numel() else mn[g_s])
+            res[tpos[ts]] = val
+            tk, tg, tpos = tk[~ts], tg[~ts], tpos[~ts]
+        if not tk.numel():
+            break
+        # refine the remaining groups: 1024 sub-bins over each group's exact range
+        rem = ~small
+        remap = torch.cumsum(rem.to(torch.int64), 0) - 1
+        keep = rem[gid]
+        cand, gid = cand[keep], remap[gid[keep]]
+        R = int(rem.sum())
+        a, span, off_r = mn[rem], (mx - mn)[rem], goff[rem]
+        sub = ((cand - a[gid]) * (_BINS / span[gid])).floor().clamp_(0, _BINS - 1).long()
+        idx = gid * _BINS + sub
+        cum = torch.cumsum(_ar(torch.bincount(idx, minlength=R * _BINS)).view(R, _BINS), 1)
+        tr = remap[tg]
+        j = torch.searchsorted(cum[tr], (tk - off_r[tr]).view(-1, 1), right=True).view(-1)
+        below = torch.where(j > 0, cum[tr, (j - 1).clamp(min=0)], torch.zeros_like(j))
+        key = tr * _BINS + j
+        ukey, inv = torch.unique(key, return_inverse=True)
+        noff = torch.zeros(ukey.numel(), dtype=torch.int64, device=dev).scatter_(0, inv, off_r[tr] + below)
+        lut = torch.full((R * _BINS,), -1, dtype=torch.int64, device=dev)
+        lut[ukey] = torch.arange(ukey.numel(), device=dev)
+        ng = lut[idx]
+        live = ng >= 0
+        cand, gid = cand[live], ng[live]
+        tg, goff = inv, noff
+    return dict(zip(ks_l, res.tolist()))
+
+
 def weighted_lower(x: torch.Tensor, w: torch.Tensor, t: float) -> float:
     """Smallest value v with (sum of weights of values <= v) >= t over every
     rank's (x, w) -- the weighted quantile rule of quantile_values."""

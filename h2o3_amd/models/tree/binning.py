@@ -14,10 +14,18 @@ coalesced gathers).  Every histogram type maps to a set of per-feature cut
 points; a split "code <= t" is exactly the float rule ``x < cuts[t]`` used at
 scoring time, so training and scoring never disagree.
 
-  QuantilesGlobal : nbins equal-frequency cut points (global sketch)
-  UniformAdaptive : uniform grid over [min, max] with nbins_top_level cells
+  QuantilesGlobal : nbins equal-frequency cut points (exact global order
+                    statistics over every row of every rank)
+  UniformAdaptive : the reference's top-level grid -- nbins_top_level uniform
+                    cells over the exact [min, max] (one cell per integer for
+                    narrow integer columns); each node then splits only at
+                    max(nbins_top_level >> depth, nbins) uniform cuts over its
+                    own observed range (engine.TreeGrower._adapt_hist,
+                    DHistogram.java:366-386, DTree.java:337)
+  Random          : the same grid, random cut subsets redrawn per node
+  RoundRobin      : the same grid; each tree draws UniformAdaptive / Random /
+                    QuantilesGlobal (DHistogram.java:226-233)
   UniformRobust   : uniform grid, outlier-robust range (0.1/99.9 pct)
-  Random          : sorted uniform random cut points in [min, max]
   AUTO            : QuantilesGlobal with max(nbins, 254) bins, capped at 254
                     (the GPU-native default)
 Categorical columns: code = level (levels beyond nbins_cats are grouped
@@ -63,6 +71,10 @@ class BinnedData:
         self.names = []
         self.code_bytes = 1
         self.nrows_local = 0
+        self.hist_type = "auto"      # lower-case histogram_type the cuts were built for
+        self.nbins_node = 20         # nbins: floor of the per-node adaptive bin count
+        self.nbins_top = 1024        # nbins_top_level
+        self.qbounds = None          # RoundRobin: per-feature quantile boundary codes
 
     @property
     def dtype(self):
@@ -91,10 +103,61 @@ def _sample_rows(n, k, gen_device, seed):
     return torch.randint(0, n, (k,), generator=g, device=gen_device)
 
 
+def _global_finite(x):
+    """(finite values of this rank's column as f64, global count, global min,
+    global max, all values integral) -- exact, from all-reduces (the Vec
+    rollups' min / max, not a row sample)."""
+    xs = x[torch.isfinite(x)].to(torch.float64)
+    n = xs.numel()
+    big = float("inf")
+    st = torch.tensor([float(n), float(xs.min()) if n else big, -float(xs.max()) if n else big,
+                       float(bool((xs != torch.round(xs)).any())) if n else 0.0], dtype=torch.float64,
+                      device=xs.device)
+    if cloud.is_distributed():
+        cnt = st[:1].clone()
+        coll.allreduce_(cnt)
+        mm = st[1:].clone()
+        mm[2] = -mm[2]                    # "any non-integral" as a min of negatives
+        coll.allreduce_(mm, "min")
+        return xs, int(cnt[0]), float(mm[0]), -float(mm[1]), -float(mm[2]) == 0.0
+    return xs, n, float(st[1]), -float(st[2]), float(st[3]) == 0.0
+
+
+def _exact_quantile_cuts(xs, n, lo, B, seed):
+    """Cut points at the order statistics round(q (n-1)), q = k / B (exact,
+    distributed histogram refinement: core/dist_ops.kth_smallest_many), or
+    the midpoints between the distinct values when there are at most B."""
+    from ...core.dist_ops import kth_smallest_many
+    idx = _sample_rows(xs.shape[0], 1 << 20, xs.device, seed)
+    samp = xs[idx] if idx is not None else xs
+    u = torch.unique(coll.all_gather_var(torch.unique(samp)) if cloud.is_distributed() else samp)
+    if u.numel() <= B:
+        # few distinct values in the sample: exact when every value is one of them
+        pos = torch.searchsorted(u, xs).clamp(max=max(u.numel() - 1, 0))
+        miss = torch.tensor([float((u[pos] != xs).sum()) if u.numel() else float(xs.numel())],
+                            dtype=torch.float64, device=xs.device)
+        if cloud.is_distributed():
+            coll.allreduce_(miss)
+        if float(miss[0]) == 0.0:
+            uu = u.cpu().numpy()
+            return (uu[:-1] + uu[1:]) / 2.0 if len(uu) > 1 else np.zeros(0)
+    q = np.linspace(0, 1, B + 1)[1:-1]
+    ks = np.round(q * (n - 1)).astype(np.int64)
+    vals = kth_smallest_many(xs, ks.tolist())
+    c = np.unique(np.array([vals[int(k)] for k in ks], dtype=np.float64))
+    return c[c > lo]
+
+
 def compute_cuts(cols, is_cat, hist_type="AUTO", nbins=20, nbins_top_level=1024, nbins_cats=1024,
                  seed=1234, sample=1 << 20):
-    """Per-feature cut points (list of float64 numpy arrays) and bin counts."""
-    dev = cloud.device()
+    """Per-feature cut points (list of float64 numpy arrays) and bin counts.
+
+    QuantilesGlobal / AUTO: exact global quantiles (all rows, every rank).
+    UniformAdaptive / Random / RoundRobin: the reference's top-level grid
+    (DHistogram.initialHist): nbins_top_level uniform cells over the exact
+    column [min, max], or one cell per integer when an integer column spans
+    at most that many values; the per-node adaptive re-binning happens in
+    the split search (engine.TreeGrower._adapt_hist)."""
     ht = (hist_type or "AUTO").lower()
     cuts, nb_list, groups = [], [], []
     for j, (col, cat) in enumerate(zip(cols, is_cat)):
@@ -109,55 +172,54 @@ def compute_cuts(cols, is_cat, hist_type="AUTO", nbins=20, nbins_top_level=1024,
                 groups.append(g)
             cuts.append(None)
             continue
-        x = col
-        if ht in ("auto", "quantilesglobal"):
-            B = min(254, max(nbins, 254)) if ht == "auto" else min(max(nbins, 2), 4095)
-        elif ht in ("uniformadaptive",):
-            B = min(max(nbins_top_level, nbins), 4095)
-        else:
-            B = min(max(nbins, 2), 4095)
-        idx = _sample_rows(x.shape[0], sample, x.device, seed + j)
-        xs = x[idx] if idx is not None else x
-        xs = xs[torch.isfinite(xs)].to(torch.float64)
-        if cloud.is_distributed():
-            xs = coll.all_gather_var(xs)
-        if xs.numel() == 0:
+        xs, n, lo, hi, is_int = _global_finite(col)
+        if n == 0:
             cuts.append(np.zeros(0))
             nb_list.append(1)
             groups.append(1)
             continue
-        lo, hi = float(xs.min()), float(xs.max())
         if ht in ("auto", "quantilesglobal"):
-            u = torch.unique(xs)
-            if u.numel() <= B:
-                # few distinct values: cut exactly between them
-                uu = u.cpu().numpy()
-                c = (uu[:-1] + uu[1:]) / 2.0 if len(uu) > 1 else np.zeros(0)
-                # cut "x < c" must separate uu[i] and uu[i+1]; midpoints do
-            else:
-                q = torch.linspace(0, 1, B + 1, dtype=torch.float64, device=xs.device)[1:-1]
-                srt = torch.sort(xs).values
-                pos = (q * (srt.numel() - 1)).round().long()
-                c = torch.unique(srt[pos]).cpu().numpy()
-                # a cut equal to the min would create an empty first bin
-                c = c[c > lo]
-        elif ht == "random":
-            g = np.random.RandomState(seed + j)
-            c = np.unique(np.sort(g.uniform(lo, hi, size=B - 1)))
-        else:
-            if ht == "uniformrobust" and xs.numel() > 100:
-                srt = torch.sort(xs).values
-                lo = float(srt[int(0.001 * (srt.numel() - 1))])
-                hi = float(srt[int(0.999 * (srt.numel() - 1))])
+            B = min(254, max(nbins, 254)) if ht == "auto" else min(max(nbins, 2), 4095)
+            c = _exact_quantile_cuts(xs, n, lo, B, seed + j)
+        elif ht in ("uniformadaptive", "random", "roundrobin"):
+            B = min(max(nbins_top_level, nbins), 4095)
             if hi <= lo:
                 c = np.zeros(0)
+            elif is_int and hi - lo + 1 <= B:
+                c = np.arange(lo + 0.5, hi, 1.0)          # one cell per integer value
             else:
-                c = np.linspace(lo, hi, B + 1)[1:-1]
-                c = np.unique(c)
+                c = np.unique(np.linspace(lo, hi, B + 1)[1:-1])
+        else:
+            B = min(max(nbins, 2), 4095)
+            if ht == "uniformrobust" and n > 100:
+                from ...core.dist_ops import kth_smallest_many
+                k1, k2 = int(0.001 * (n - 1)), int(0.999 * (n - 1))
+                v = kth_smallest_many(xs, [k1, k2])
+                lo, hi = v[k1], v[k2]
+            c = np.zeros(0) if hi <= lo else np.unique(np.linspace(lo, hi, B + 1)[1:-1])
         cuts.append(np.asarray(c, dtype=np.float64))
         nb_list.append(len(c) + 1)
         groups.append(1)
     return cuts, nb_list, groups
+
+
+def quantile_bounds(cols, is_cat, cuts, nbins, seed=1234):
+    """RoundRobin trees that draw QuantilesGlobal: for each numeric feature
+    the fine-grid boundaries (code t: "code <= t" left) nearest to its nbins
+    global quantile cuts, so those trees split only there."""
+    out = []
+    for j, (col, cat) in enumerate(zip(cols, is_cat)):
+        if cat or cuts[j] is None or len(cuts[j]) == 0:
+            out.append(None)
+            continue
+        xs, n, lo, hi, _ = _global_finite(col)
+        q = _exact_quantile_cuts(xs, n, lo, max(nbins, 2), seed + j)
+        fine = np.asarray(cuts[j])
+        t = np.clip(np.searchsorted(fine, q), 0, len(fine) - 1)
+        alt = np.clip(t - 1, 0, len(fine) - 1)
+        t = np.where(np.abs(fine[alt] - q) < np.abs(fine[t] - q), alt, t)
+        out.append(np.unique(t.astype(np.int64)))
+    return out
 
 
 def bin_frame_tensors(features, is_cat, cat_cards, names, hist_type="AUTO", nbins=20, nbins_top_level=1024,
@@ -218,6 +280,11 @@ def bin_frame_tensors(features, is_cat, cat_cards, names, hist_type="AUTO", nbin
     bd.names = list(names)
     bd.code_bytes = code_bytes
     bd.nrows_local = N
+    bd.hist_type = (hist_type or "AUTO").lower()
+    bd.nbins_node = int(nbins)
+    bd.nbins_top = int(max(nbins_top_level, nbins))
+    bd.qbounds = quantile_bounds([features[j] if not is_cat[j] else None for j in range(F)], is_cat, bd.cuts,
+                                 nbins, seed) if bd.hist_type == "roundrobin" else None
     bd.codes = col.t().contiguous()  # [N, Fp]
     bd.codes_col = col[:F] if want_col_major else None
     if not want_col_major:

@@ -53,6 +53,7 @@ class GrowParams:
     hist_mem_budget: int = 8 << 30
     interaction_sets: list | None = None  # list of sets of feature ids
     leaf_budget_by_gain: bool = False   # max_leaves spent on the highest-gain nodes first (lossguide)
+    use_bounds: bool = True        # monotone node bounds clamp (True) or veto (False) splits (GBMModel.java:84)
 
 
 @dataclass
@@ -368,28 +369,37 @@ class TreeGrower:
         return torch.from_numpy(np.sort(elig[sel], axis=1))
 
     def _col_mask_allowed(self, allow, depth):
-        """Per-node mask under interaction constraints: the branch's allowed
-        features (BranchInteractionConstraints), column sampling among them
-        (DTree.UndecidedNode.scoreCols samples from the columns that still
-        have histograms)."""
+        """Per-node mask under interaction constraints, on the device: the
+        branch's allowed features (BranchInteractionConstraints) intersected
+        with the per-tree column mask, then column sampling among them
+        (DTree.UndecidedNode.scoreCols samples from the columns that still have
+        histograms): k smallest of per-(node, feature) uniform keys among each
+        node's eligible features -- no per-node host loop."""
         p = self.p
         F = self.bd.F
-        base = np.ones(F, dtype=bool) if p.tree_col_mask is None else p.tree_col_mask.astype(bool)
-        m = allow & base[None, :]
+        dev = allow.device
+        base = torch.ones(F, dtype=torch.bool, device=dev) if p.tree_col_mask is None else \
+            torch.as_tensor(p.tree_col_mask.astype(bool), device=dev)
+        m = allow & base.view(1, -1)
+        n = m.shape[0]
         rate = p.col_sample_rate * (p.col_sample_rate_change_per_level ** depth)
-        for i in range(m.shape[0]):
-            elig = np.nonzero(m[i])[0]
-            k = p.mtries if (p.mtries is not None and p.mtries > 0) else (
-                max(1, int(math.floor(rate * elig.size + 0.5))) if rate < 1.0 else elig.size)
-            if 0 < k < elig.size:
-                keep = self.rng.choice(elig, size=k, replace=False)
-                m[i] = False
-                m[i, keep] = True
+        if (p.mtries is not None and p.mtries > 0) or rate < 1.0:
+            cnt = m.sum(1)
+            if p.mtries is not None and p.mtries > 0:
+                k = torch.full_like(cnt, int(p.mtries))
+            else:
+                k = torch.floor(rate * cnt.to(torch.float64) + 0.5).to(cnt.dtype).clamp(min=1)
+            g = torch.Generator(device=dev)
+            g.manual_seed(int(self.rng.randint(0, 2 ** 31 - 1)))
+            keys = torch.rand((n, F), generator=g, device=dev)
+            keys = torch.where(m, keys, torch.full_like(keys, 2.0))
+            rank = torch.argsort(torch.argsort(keys, 1), 1)
+            m = m & (rank < k.view(-1, 1))
         if self.Fpad > F:
-            m = np.concatenate([m, np.zeros((m.shape[0], self.Fpad - F), dtype=bool)], 1)
-        t = torch.from_numpy(np.ascontiguousarray(m))
-        t._all_true = False
-        return t
+            m = torch.cat([m, torch.zeros((n, self.Fpad - F), dtype=torch.bool, device=dev)], 1)
+        m = m.contiguous()
+        m._all_true = False
+        return m
 
     def _col_mask(self, n_nodes, depth, sel=None, allow=None):
         """[n, Fpad] bool mask of features eligible per node."""
@@ -433,15 +443,159 @@ class TreeGrower:
         self._ics_cache = (allow, root)
         return self._ics_cache
 
+    # ------------------------------------------------------------------ monotone node bounds
+    def _bnd_dev(self, n):
+        """[n, 2] f64 (lo, hi) prediction bounds of the frontier nodes being
+        scored, or None when no node is bounded."""
+        b = getattr(self, "_bnd", None)
+        if b is None:
+            return None
+        off = getattr(self, "_bnd_off", 0)
+        return b[off:off + n]
+
+    def _bound_cost(self, Lb, Rb, lo, hi):
+        """(gain penalty of clamping the children's constants into [lo, hi],
+        violated?) for left / right channel sums [..., C]."""
+        p = self.p
+        if p.criterion == "xgb":
+            al, ar = Lb[..., 1] + p.reg_lambda, Rb[..., 1] + p.reg_lambda
+            pl, pr = -Lb[..., 0] / al, -Rb[..., 0] / ar
+            al, ar = 0.5 * al, 0.5 * ar
+        else:
+            al, ar = Lb[..., 0], Rb[..., 0]
+            pl, pr = Lb[..., 1] / al.clamp_min(1e-300), Rb[..., 1] / ar.clamp_min(1e-300)
+        cl, cr = torch.minimum(torch.maximum(pl, lo), hi), torch.minimum(torch.maximum(pr, lo), hi)
+        viol = (cl != pl) | (cr != pr)
+        return al * (cl - pl) ** 2 + ar * (cr - pr) ** 2, viol
+
+    def _bound_winners(self, res):
+        """Per-node check of already selected winners (categorical pair
+        paths): clamp penalty or veto for splits outside the node bounds."""
+        n = res["gain"].shape[0]
+        bnd = self._bnd_dev(n)
+        if bnd is None:
+            return res
+        pen, viol = self._bound_cost(res["L"].to(torch.float64), res["R"].to(torch.float64), bnd[:, 0], bnd[:, 1])
+        g = res["gain"].to(torch.float64)
+        g = torch.where(viol & torch.isfinite(g), g - pen if self.p.use_bounds else torch.full_like(g, NEG_INF), g)
+        res = dict(res)
+        res["gain"] = g
+        return res
+
+    def _child_bounds(self, lo, hi, f_s, cat_s, Lsel, Rsel, mode):
+        """Constraints.withNewConstraint for the children of the split nodes:
+        bounds at the midpoint of the (clamped) child predictions on
+        increasing / decreasing columns, inherited otherwise."""
+        p = self.p
+        mono = np.asarray(p.monotone, dtype=np.float64)
+        c = np.where(cat_s | (f_s >= mono.size), 0.0, mono[np.minimum(f_s, mono.size - 1)])
+        if p.criterion == "xgb":
+            pl = -Lsel[:, 0] / (Lsel[:, 1] + p.reg_lambda)
+            pr = -Rsel[:, 0] / (Rsel[:, 1] + p.reg_lambda)
+        else:
+            pl = Lsel[:, 1] / np.maximum(Lsel[:, 0], 1e-300)
+            pr = Rsel[:, 1] / np.maximum(Rsel[:, 0], 1e-300)
+        mid = 0.5 * (np.clip(pl, lo, hi) + np.clip(pr, lo, hi))
+        lo_l, hi_l, lo_r, hi_r = lo.copy(), hi.copy(), lo.copy(), hi.copy()
+        inc, dec = c > 0, c < 0
+        hi_l[inc] = np.minimum(hi[inc], mid[inc])
+        lo_r[inc] = np.maximum(lo[inc], mid[inc])
+        lo_l[dec] = np.maximum(lo[dec], mid[dec])
+        hi_r[dec] = np.minimum(hi[dec], mid[dec])
+        return np.stack([lo_l, lo_r], 1).reshape(-1), np.stack([hi_l, hi_r], 1).reshape(-1)
+
+    # ------------------------------------------------------------------ adaptive bins
+    _RR_TYPES = ("uniformadaptive", "uniformadaptive", "random", "quantilesglobal")
+
+    def _tree_hist_type(self):
+        """Histogram type of the tree being grown: RoundRobin cycles the
+        reference's ROUND_ROBIN_CANDIDATES (AUTO counts as UniformAdaptive,
+        SharedTreeModel.java:59) tree by tree."""
+        ht = getattr(self.bd, "hist_type", "auto")
+        if ht == "roundrobin":
+            return self._RR_TYPES[(int(self.p.seed) + getattr(self, "_tree_no", 0)) % 4]
+        return ht
+
+    def _adapt_hist(self, H):
+        """Per-node adaptive binning of the numeric features (reference
+        UniformAdaptive / Random, DHistogram.java:366-386, DTree.java:337).  The
+        level histogram is on the fixed fine grid of nbins_top_level cells; the
+        reference re-bins each (node, column) into
+        nb = max(nbins_top_level >> depth, nbins) uniform bins over the node's
+        observed range.  Here each run of fine bins that falls into one coarse
+        bin is folded into the run's LAST fine bin: every cumulative sum at an
+        allowed boundary is unchanged and every other boundary repeats the sums
+        of the previous allowed one, so any split search on the folded
+        histogram picks only coarse boundaries (ties go to the lower code).
+        Random draws the cut subset per (tree, level, node, feature); a
+        RoundRobin tree on QuantilesGlobal keeps only the boundaries next to the
+        global quantiles.  Categorical features and the NA bin are untouched."""
+        ht = self._tree_hist_type()
+        if ht not in ("uniformadaptive", "random", "quantilesglobal") or \
+                getattr(self.bd, "hist_type", "auto") not in ("uniformadaptive", "random", "roundrobin"):
+            return H
+        Fl, n, Bs, C = H.shape
+        B = Bs - 1
+        depth = getattr(self, "_depth", 0)
+        nb = max(self.bd.nbins_top >> depth, self.bd.nbins_node)
+        f0 = self.f0
+        isnum = ~self.is_cat_t[f0:f0 + Fl]
+        if ht == "uniformadaptive" and nb >= B:
+            return H
+        dev = H.device
+        Hn = H[:, :, :B]
+        occ = (Hn != 0).any(-1)                                   # [Fl, n, B]
+        idx = torch.arange(B, device=dev)
+        first = torch.where(occ, idx, B).amin(-1, keepdim=True)
+        last = torch.where(occ, idx, -1).amax(-1, keepdim=True)
+        L = (last - first + 1).clamp(min=1)
+        inr = (idx >= first) & (idx <= last)
+        if ht == "uniformadaptive":
+            coarse = torch.div((idx - first).clamp(min=0) * nb, L, rounding_mode="floor")
+            nxt = torch.div((idx + 1 - first).clamp(min=0) * nb, L, rounding_mode="floor")
+            is_end = inr & ((coarse != nxt) | (idx == last))
+            is_end = is_end | (inr & (L <= nb))                   # narrow range: every boundary
+        elif ht == "random":
+            # per (tree, level, node, feature, bin) uniform draw: keep ~nb - 1 cuts
+            key = (torch.arange(Fl, device=dev).view(-1, 1, 1) + f0) * 1000003 + \
+                torch.arange(n, device=dev).view(1, -1, 1) * 7919 + idx.view(1, 1, -1) * 104729 + \
+                (int(self.p.seed) * 31 + getattr(self, "_tree_no", 0) * 131 + depth * 17)
+            key = (key * 0x9E3779B1) & 0xFFFFFFFF
+            key = ((key ^ (key >> 15)) * 0x2C1B3C6D) & 0xFFFFFFFF
+            u = (key ^ (key >> 12)).to(torch.float64) / 4294967296.0
+            pk = ((nb - 1) / (L - 1).clamp(min=1).to(torch.float64))
+            is_end = inr & ((u < pk) | (idx == last))
+        else:
+            qm = self.__dict__.get("_qmask")
+            if qm is None:
+                qm = torch.zeros((self.Fpad, B), dtype=torch.bool, device=dev)
+                for j, qb in enumerate(self.bd.qbounds or []):
+                    if qb is not None and len(qb):
+                        qm[j, torch.as_tensor(np.minimum(qb, B - 1), device=dev)] = True
+                self._qmask = qm
+            is_end = inr & (qm[f0:f0 + Fl].view(Fl, 1, B) | (idx == last))
+        is_end = is_end | ~isnum.view(Fl, 1, 1)                   # categorical: unchanged
+        cs = torch.cumsum(Hn.to(torch.float64), 2)
+        E = torch.where(is_end, idx, -1)
+        pe_incl = torch.cummax(E, 2).values
+        pe = torch.cat([torch.full_like(pe_incl[:, :, :1], -1), pe_incl[:, :, :-1]], 2)
+        base = torch.where((pe >= 0).unsqueeze(-1), torch.gather(cs, 2, pe.clamp(min=0).unsqueeze(-1).expand(-1, -1, -1, C)),
+                           torch.zeros_like(cs))
+        Hf = torch.where(is_end.unsqueeze(-1), cs - base, torch.zeros_like(cs)).to(H.dtype)
+        Hf = torch.where(isnum.view(Fl, 1, 1, 1), Hf, Hn)
+        return torch.cat([Hf, H[:, :, B:]], 2).contiguous()
+
     def _find_splits(self, H, col_mask, node_wyy=None, want_pk=False):
         """Dispatch: fused HIP kernel for numeric features on GPU (categorical
         features, which need a per-node sort of bins, go through the torch path)."""
+        H = self._adapt_hist(H)
         if self.dev.type != "cuda" or self.p.criterion.startswith("uplift"):
             Fl_ = H.shape[0]
             cmf = col_mask[:, self.f0:self.f0 + Fl_]
             if not self.p.criterion.startswith("uplift") and cmf.numel() and float(cmf.float().mean()) < 0.5:
                 # few eligible features per node (DRF mtries): score only those pairs
                 res = self._cat_splits_pairs(H, col_mask, list(range(Fl_)), node_wyy)
+                res = self._bound_winners(res)
                 res["tot"] = H[0].to(torch.float64).sum(1) if Fl_ > 0 else None
                 if self.W > 1:
                     res = self._merge_candidates(res, H.shape[1], H.shape[2], H.shape[3])
@@ -467,7 +621,7 @@ class TreeGrower:
         res = self._find_splits_native(H, cm_num, node_wyy)
         if bool(is_cat.any()):
             cat_local = torch.nonzero(is_cat).flatten().tolist()
-            rc = self._cat_splits_pairs(H, col_mask, cat_local, node_wyy)
+            rc = self._bound_winners(self._cat_splits_pairs(H, col_mask, cat_local, node_wyy))
             better = rc["gain"] > res["gain"]
             for k in res:
                 if res[k] is None or k == "tot":
@@ -510,11 +664,18 @@ class TreeGrower:
             torch.zeros(n, dtype=torch.float64, device=self.dev)
         out = torch.empty((n * Fl, 4), dtype=torch.float64, device=self.dev)
         crit = 1 if p.criterion == "xgb" else 0
-        rc = lib.h2o_split_find(ctypes.c_void_p(H.data_ptr()), Fl, n, Bs, ctypes.c_void_p(wyy.data_ptr()),
-                                ctypes.c_void_p(ok.data_ptr()), ctypes.c_void_p(mono.data_ptr()),
-                                float(p.min_rows), float(p.min_split_improvement), float(p.reg_lambda),
-                                float(p.reg_alpha), float(p.gamma), crit, ctypes.c_void_p(out.data_ptr()),
-                                tree_ops._stream())
+        bnd = self._bnd_dev(n)
+        if not getattr(lib, "_typed_b", False):
+            cv = ctypes.c_void_p
+            lib.h2o_split_find_b.argtypes = [cv, ctypes.c_int, ctypes.c_int, ctypes.c_int, cv, cv, cv] + \
+                [ctypes.c_double] * 5 + [ctypes.c_int, cv, cv, ctypes.c_int, cv]
+            lib._typed_b = True
+        rc = lib.h2o_split_find_b(ctypes.c_void_p(H.data_ptr()), Fl, n, Bs, ctypes.c_void_p(wyy.data_ptr()),
+                                  ctypes.c_void_p(ok.data_ptr()), ctypes.c_void_p(mono.data_ptr()),
+                                  float(p.min_rows), float(p.min_split_improvement), float(p.reg_lambda),
+                                  float(p.reg_alpha), float(p.gamma), crit, ctypes.c_void_p(out.data_ptr()),
+                                  ctypes.c_void_p(0 if bnd is None else bnd.data_ptr()), int(bool(p.use_bounds)),
+                                  tree_ops._stream())
         if rc != 0:
             raise RuntimeError(f"h2o_split_find failed: {rc}")
         if C == 2 and want_pk and (self.W > 1 or self.f0 < self.bd.F):
@@ -1192,6 +1353,19 @@ class TreeGrower:
         else:
             allg = torch.where(allg > 0, allg, torch.full_like(allg, NEG_INF))
         K = allg.shape[2]
+        bnd = self._bnd_dev(n)
+        if bnd is not None and not uplift and Fl > 0:
+            # monotone node bounds on each column's best split (DTree.java:1386-1445)
+            bk = allg.argmax(2)                                        # [n, Fl]
+            gk = allg.gather(2, bk.unsqueeze(2)).squeeze(2)
+            LL_all = torch.cat([LA, LB, LC.expand(-1, -1, 1, -1)], 2)
+            RR_all = torch.cat([RA, RB, RC.expand(-1, -1, 1, -1)], 2)
+            ix = bk.view(n, Fl, 1, 1).expand(-1, -1, 1, C)
+            Lb, Rb = LL_all.gather(2, ix).squeeze(2), RR_all.gather(2, ix).squeeze(2)
+            pen, viol = self._bound_cost(Lb, Rb, bnd[:, 0].view(n, 1), bnd[:, 1].view(n, 1))
+            gk = torch.where(viol & torch.isfinite(gk),
+                             gk - pen if p.use_bounds else torch.full_like(gk, NEG_INF), gk)
+            allg = torch.full_like(allg, NEG_INF).scatter_(2, bk.unsqueeze(2), gk.unsqueeze(2))
         flat = allg.reshape(n, Fl * K)
         best, arg = flat.max(1)
         fl = arg // K
@@ -1294,6 +1468,8 @@ class TreeGrower:
         bd, p = self.bd, self.p
         N = bd.nrows_local
         C = tree_ops.channels(mode)
+        self._tree_no = getattr(self, "_tree_no", -1) + 1
+        self._adaptive = getattr(bd, "hist_type", "auto") in ("uniformadaptive", "random", "roundrobin")
         self._stream_obj = torch.cuda.current_stream() if self.dev.type == "cuda" else None
         torch.arange(N, dtype=torch.int32, device=self.dev, out=self.ridx)
         if self.dev.type != "cuda":
@@ -1351,8 +1527,14 @@ class TreeGrower:
         # BranchInteractionConstraints): the features each frontier node may
         # still split on; the root may use every feature named in a set
         ics = self._interaction_map()
-        f_allow = ics[1][None, :].copy() if ics is not None else None
+        f_allow = torch.as_tensor(ics[1][None, :].copy(), device=self.dev) if ics is not None else None
+        ics_t = torch.as_tensor(ics[0], device=self.dev) if ics is not None else None
         cutmat = self._cut_matrix()
+        # monotone node prediction bounds (Constraints._min / _max), per frontier node
+        mono_b = p.monotone is not None and bool(np.any(np.asarray(p.monotone) != 0))
+        f_lo = np.full(1, -np.inf) if mono_b else None
+        f_hi = np.full(1, np.inf) if mono_b else None
+        self._bnd, self._bnd_off = None, 0
 
         while f_id.size:
             self._level = level
@@ -1362,7 +1544,14 @@ class TreeGrower:
             level_bytes = self.Fpad * n_front * bd.Bs * C_ * 8
             prev_bytes = 0 if H_prev is None else H_prev.numel() * 8
             chunked = can_split and (level_bytes + prev_bytes) > p.hist_mem_budget and n_front > 1
-            direct = can_split and f_allow is None and self._direct_level(mode, depth, chunked)
+            self._depth = depth
+            direct = can_split and f_allow is None and not self._adaptive and not mono_b and \
+                self._direct_level(mode, depth, chunked)
+            if mono_b and bool(np.isfinite(f_lo).any() | np.isfinite(f_hi).any()):
+                self._bnd = torch.as_tensor(np.stack([f_lo, f_hi], 1), dtype=torch.float64, device=self.dev)
+            else:
+                self._bnd = None
+            self._bnd_off = 0
             chunked = chunked or direct
             la, self._la = self._la, None
             if la is not None and (chunked or not can_split or la[0].shape[1] < n_front):
@@ -1434,8 +1623,10 @@ class TreeGrower:
                             Hc = self._build_hist(ridx, va, vb, mode, f_st[a:a + per], f_ct[a:a + per],
                                                   need_mask=None if need is None else need[a:a + per])
                             wyy_c = self._last_wyy if mode == 0 else None
+                            self._bnd_off = a
                             parts.append(self._find_splits(Hc, cm[a:a + per], wyy_c, want_pk=False))
                             del Hc
+                        self._bnd_off = 0
                         sp = {k: (torch.cat([q[k] for q in parts], 0) if parts[0].get(k) is not None else None)
                               for k in parts[0]}
                     else:
@@ -1631,8 +1822,11 @@ class TreeGrower:
             f_tot = np.stack([Lsel, Rsel], 1).reshape(2 * k, -1)
             if f_allow is not None:
                 # nextLevelInteractionConstraints: branch set ∩ the split feature's set
-                ca = f_allow[sids] & ics[0][f_s]
-                f_allow = np.repeat(ca, 2, axis=0)
+                ca = f_allow[tree_ops._h2d(sids, self.dev)] & ics_t[tree_ops._h2d(f_s, self.dev)]
+                f_allow = torch.repeat_interleave(ca, 2, dim=0)
+            if mono_b:
+                f_lo, f_hi = self._child_bounds(f_lo[sids], f_hi[sids], f_s, cat_s, np.asarray(Lsel, dtype=np.float64),
+                                                np.asarray(Rsel, dtype=np.float64), mode)
             jj = 2 * np.arange(k, dtype=np.int64)
             p_build = jj + (~build_left)
             p_der = jj + build_left

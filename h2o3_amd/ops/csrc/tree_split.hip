@@ -67,7 +67,8 @@ __global__ __launch_bounds__(256) void split_kernel(const double* __restrict__ H
                                                     const unsigned char* __restrict__ feat_ok,  // [n][Fl]
                                                     const float* __restrict__ mono,            // [Fl]
                                                     double min_rows, double msi, double lam, double alpha,
-                                                    double gamma, SplitRec* __restrict__ out) {
+                                                    double gamma, SplitRec* __restrict__ out,
+                                                    const double* __restrict__ bnd, int use_bounds) {
   const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (gw >= n * Fl) return;
   const int node = gw / Fl;
@@ -157,21 +158,54 @@ __global__ __launch_bounds__(256) void split_kernel(const double* __restrict__ H
       best.gain = og; best.t = ot; best.opt = oo; best.lw = ow; best.ly = oy;
     }
   }
+  // node prediction bounds of monotone constraints (Constraints.java; applied
+  // to this column's best split as DTree.java:1386-1445 does): a child
+  // prediction outside [lo, hi] either vetoes the split (use_bounds == 0) or
+  // is clamped, and the gain loses what the clamped constant costs
+  // (w (c - mean)^2 for squared error, (h + lambda) (c - c*)^2 / 2 second order)
+  if (bnd && lane == 0 && best.gain > -INFINITY) {
+    const double lo = bnd[2 * node], hi = bnd[2 * node + 1];
+    if (lo > -INFINITY || hi < INFINITY) {
+      const double lw = best.lw, ly = best.ly, rw = Tw - lw, ry = Ty - ly;
+      double pl, pr, al, ar;
+      if (CRIT == 1) { al = ly + lam; ar = ry + lam; pl = -lw / al; pr = -rw / ar; al *= 0.5; ar *= 0.5; }
+      else { al = lw; ar = rw; pl = ly / lw; pr = ry / rw; }
+      const double cl = fmin(fmax(pl, lo), hi), cr = fmin(fmax(pr, lo), hi);
+      if (cl != pl || cr != pr) {
+        if (!use_bounds) best.gain = -INFINITY;
+        else best.gain -= al * (cl - pl) * (cl - pl) + ar * (cr - pr) * (cr - pr);
+      }
+    }
+  }
   if (lane == 0) out[(size_t)node * Fl + f] = best;
 }
+
+extern "C" int h2o_split_find_b(const double* H, int Fl, int n, int Bs, const double* node_wyy,
+                                const unsigned char* feat_ok, const float* mono, double min_rows, double msi,
+                                double lam, double alpha, double gamma, int crit, void* out, const double* bnd,
+                                int use_bounds, hipStream_t s);
 
 extern "C" int h2o_split_find(const double* H, int Fl, int n, int Bs, const double* node_wyy,
                               const unsigned char* feat_ok, const float* mono, double min_rows, double msi,
                               double lam, double alpha, double gamma, int crit, void* out, hipStream_t s) {
+  return h2o_split_find_b(H, Fl, n, Bs, node_wyy, feat_ok, mono, min_rows, msi, lam, alpha, gamma, crit, out,
+                          nullptr, 0, s);
+}
+
+// bnd: [n][2] node prediction bounds (lo, hi; +-inf = none) or nullptr
+extern "C" int h2o_split_find_b(const double* H, int Fl, int n, int Bs, const double* node_wyy,
+                                const unsigned char* feat_ok, const float* mono, double min_rows, double msi,
+                                double lam, double alpha, double gamma, int crit, void* out, const double* bnd,
+                                int use_bounds, hipStream_t s) {
   if (n <= 0 || Fl <= 0) return 0;
   const int waves = n * Fl;
   dim3 grid((waves + 3) / 4);
   if (crit == 1)
     hipLaunchKernelGGL(split_kernel<1>, grid, dim3(256), 0, s, H, Fl, n, Bs, node_wyy, feat_ok, mono, min_rows, msi,
-                       lam, alpha, gamma, (SplitRec*)out);
+                       lam, alpha, gamma, (SplitRec*)out, bnd, use_bounds);
   else
     hipLaunchKernelGGL(split_kernel<0>, grid, dim3(256), 0, s, H, Fl, n, Bs, node_wyy, feat_ok, mono, min_rows, msi,
-                       lam, alpha, gamma, (SplitRec*)out);
+                       lam, alpha, gamma, (SplitRec*)out, bnd, use_bounds);
   return (int)hipGetLastError();
 }
 

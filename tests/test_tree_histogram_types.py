@@ -1,0 +1,138 @@
+"""Reference histogram semantics of the tree engine (binning.py +
+engine.TreeGrower._adapt_hist) and monotone node bounds inside the split
+search (engine._bound_cost, tree_split.hip split_kernel).
+
+Reference: hex/tree/DHistogram.java:226-233 (RoundRobin), :366-386 (bins of a
+node over its own range), DTree.java:337 (adj_nbins = max(nbins_prev >> 1,
+nbins)), SharedTreeModel.java:55-72 (nbins 20, nbins_top_level 1024),
+GlobalQuantilesCalc, DTree.java:1386-1445 + Constraints.java (node bounds).
+"""
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+import h2o3_amd as h2o
+from h2o3_amd.estimators import H2OGradientBoostingEstimator
+from h2o3_amd.models.tree.binning import bin_frame_tensors
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _init():
+    h2o.init(verbose=False)
+
+
+def _step_frame(n=20000, seed=0):
+    rng = np.random.default_rng(seed)
+    x = rng.random(n)
+    y = 3.0 * (x > 0.1) + 1.0 * (x > 0.5317) + 0.01 * rng.normal(size=n)
+    return pd.DataFrame({"x": x, "y": y})
+
+
+def _allowed_right_child(codes, lo_code, nb):
+    """Coarse boundaries of a node whose rows have fine codes `codes`."""
+    first, last = int(codes.min()), int(codes.max())
+    L = last - first + 1
+    b = np.arange(first, last + 1)
+    coarse = np.floor((b - first) * nb / L)
+    nxt = np.floor((b + 1 - first) * nb / L)
+    return set(b[(coarse != nxt) | (b == last)].tolist()) if L > nb else set(b.tolist())
+
+
+def test_uniform_adaptive_child_splits_on_its_coarse_grid():
+    df = _step_frame()
+    fr = h2o.H2OFrame(df)
+    kw = dict(ntrees=1, max_depth=2, learn_rate=1.0, min_rows=1, seed=1, nbins=20, nbins_top_level=128,
+              distribution="gaussian")
+    m = H2OGradientBoostingEstimator(histogram_type="UniformAdaptive", **kw)
+    m.train(x=["x"], y="y", training_frame=fr)
+    t = m._forest.trees[0]
+    root_thr = t.thr[0]
+    assert abs(root_thr - 0.1) < 1.5 / 128                     # root: the 128-cell top-level grid
+    r = t.right[0]
+    assert t.left[r] >= 0, "right child must split"
+    # fine codes of the right child's rows on the 128-cell uniform grid
+    lo, hi = df.x.min(), df.x.max()
+    cuts = np.unique(np.linspace(lo, hi, 129)[1:-1])
+    codes = np.searchsorted(cuts, df.x.values[df.x.values >= root_thr], side="right")
+    allowed = _allowed_right_child(codes, 0, max(128 >> 1, 20))
+    assert len(allowed) < codes.max() - codes.min() + 1          # the grid really is coarser here
+    assert int(t.split_code[r]) in allowed
+    # the same data with the global quantile grid is not restricted this way
+    q = H2OGradientBoostingEstimator(histogram_type="QuantilesGlobal", **dict(kw, nbins=1000))
+    q.train(x=["x"], y="y", training_frame=fr)
+    qt = q._forest.trees[0]
+    assert abs(qt.thr[qt.right[0]] - 0.5317) < 0.003
+
+
+def test_quantiles_global_cuts_are_exact_order_statistics():
+    rng = np.random.default_rng(3)
+    x = np.concatenate([rng.exponential(size=30000), np.full(5000, 0.7)]).astype(np.float32)
+    bd = bin_frame_tensors([torch.tensor(x)], [False], [0], ["x"], hist_type="QuantilesGlobal", nbins=50)
+    xs = np.sort(x.astype(np.float64))
+    ks = np.round(np.linspace(0, 1, 51)[1:-1] * (len(xs) - 1)).astype(int)
+    ref = np.unique(xs[ks])
+    ref = ref[ref > xs[0]]
+    np.testing.assert_array_equal(bd.cuts[0], ref.astype(np.float32).astype(np.float64))
+
+
+def test_uniform_grid_uses_exact_range_and_integer_cells():
+    rng = np.random.default_rng(4)
+    x = rng.normal(size=50000).astype(np.float32)
+    x[123] = 40.0                                                 # one far value sets the range
+    k = rng.integers(3, 60, 50000).astype(np.float32)
+    bd = bin_frame_tensors([torch.tensor(x), torch.tensor(k)], [False, False], [0, 0], ["x", "k"],
+                           hist_type="UniformAdaptive", nbins=20, nbins_top_level=1024)
+    assert bd.cuts[0][-1] > 39.0 and bd.nbins[0] == 1024
+    np.testing.assert_allclose(bd.cuts[1], np.arange(3.5, 59.0, 1.0))     # one cell per integer
+    assert bd.nbins[1] == 57
+
+
+def test_round_robin_cycles_tree_types_and_random_redraws():
+    df = _step_frame(4000)
+    fr = h2o.H2OFrame(df)
+    m = H2OGradientBoostingEstimator(ntrees=4, max_depth=3, histogram_type="RoundRobin", seed=5, nbins=20,
+                                     nbins_top_level=64)
+    m.train(x=["x"], y="y", training_frame=fr)
+    from h2o3_amd.models.tree.engine import TreeGrower
+    seq = [TreeGrower._RR_TYPES[(5 + t) % 4] for t in range(4)]
+    assert set(seq) == {"uniformadaptive", "random", "quantilesglobal"}
+    # Random: a node's folded histogram keeps about nb - 1 of its boundaries
+    from h2o3_amd.models.tree.engine import GrowParams
+    bd = bin_frame_tensors([torch.tensor(df.x.values.astype(np.float32))], [False], [0], ["x"],
+                           hist_type="Random", nbins=20, nbins_top_level=1024)
+    g = TreeGrower(bd, GrowParams(seed=7))
+    g._tree_no, g._depth = 0, 3                                   # nb = max(1024 >> 3, 20) = 128
+    H = torch.zeros((1, 2, bd.Bs, 2), dtype=torch.float64)
+    H[0, :, : bd.nbins[0], 0] = 1.0
+    H[0, :, : bd.nbins[0], 1] = torch.arange(bd.nbins[0], dtype=torch.float64)
+    Hf = g._adapt_hist(H)
+    kept = (Hf[0, :, : bd.nbins[0], 0] != 0).sum(1)
+    assert torch.all((kept > 90) & (kept < 170)), kept
+    assert not torch.equal(Hf[0, 0], Hf[0, 1])                   # redrawn per node
+    torch.testing.assert_close(Hf[..., :bd.nbins[0], :].sum(2), H[..., :bd.nbins[0], :].sum(2))
+
+
+def test_monotone_bounds_in_split_search():
+    """A node bounded to [lo, hi]: a split whose child means leave the bounds
+    loses w (c - mean)^2 per clamped child (use_bounds), or is vetoed."""
+    from h2o3_amd.models.tree.engine import GrowParams, TreeGrower
+    x = torch.arange(16, dtype=torch.float32)
+    bd = bin_frame_tensors([x], [False], [0], ["x"], hist_type="QuantilesGlobal", nbins=16)
+    Bs = bd.Bs
+    H = torch.zeros((1, 1, Bs, 2), dtype=torch.float64)
+    y = torch.tensor([0.0] * 8 + [10.0] * 8, dtype=torch.float64)
+    H[0, 0, :16, 0] = 1.0
+    H[0, 0, :16, 1] = y
+    wyy = (y * y).sum().view(1)
+    res = {}
+    for ub in (True, False):
+        g = TreeGrower(bd, GrowParams(min_rows=1, monotone=np.array([1.0]), use_bounds=ub))
+        g._bnd, g._bnd_off = torch.tensor([[2.0, 8.0]], dtype=torch.float64), 0
+        res[ub] = g._find_splits_torch(H, torch.ones((1, 1), dtype=torch.bool), wyy)
+        g._bnd = None
+        free = g._find_splits_torch(H, torch.ones((1, 1), dtype=torch.bool), wyy)
+    # unbounded best: means 0 | 10 at t = 7, gain 400; clamped to 2 | 8: 400 - 8*4 - 8*4
+    assert float(free["gain"][0]) == pytest.approx(400.0)
+    assert float(res[True]["gain"][0]) == pytest.approx(400.0 - 64.0)
+    assert not np.isfinite(float(res[False]["gain"][0]))

@@ -222,6 +222,38 @@ def test_split_kernel_matches_torch(crit):
     torch.testing.assert_close(a["L"], b["L"].to(a["L"].dtype), rtol=1e-9, atol=1e-9)
 
 
+@pytest.mark.parametrize("crit", ["se", "xgb"])
+@pytest.mark.parametrize("use_bounds", [True, False])
+def test_split_kernel_monotone_bounds_match_torch(crit, use_bounds):
+    """Node prediction bounds (monotone constraints) inside the HIP split
+    kernel equal the torch path: each column's best split clamped (gain
+    penalty) or vetoed, then the best column per node."""
+    _need_gpu()
+    from h2o3_amd.models.tree.engine import GrowParams, TreeGrower
+    bd, _ = _binned(n=30000, cats=False)
+    mono = np.zeros(bd.F)
+    mono[[0, 2]] = [1.0, -1.0]
+    p = GrowParams(criterion=crit, min_rows=5.0, max_depth=6, monotone=mono, use_bounds=use_bounds)
+    gr = TreeGrower(bd, p)
+    n = 6
+    g = torch.Generator(device="cuda").manual_seed(5)
+    H = torch.rand((bd.F, n, bd.Bs, 2), generator=g, device="cuda", dtype=torch.float64) * 50
+    if crit == "se":
+        H[..., 1] = (torch.rand(H[..., 1].shape, generator=g, device="cuda", dtype=torch.float64) - 0.3) * H[..., 0]
+    H[:, :, 200:bd.Bs - 1] = 0
+    wyy = H[0].sum(1)[:, 0] * 10.0
+    cm = torch.ones((n, bd.F), dtype=torch.bool)
+    lo = torch.tensor([-np.inf, -0.1, 0.05, -np.inf, -1.0, 0.2], dtype=torch.float64)
+    hi = torch.tensor([np.inf, 0.1, np.inf, 0.02, 1.0, 0.3], dtype=torch.float64)
+    gr._bnd, gr._bnd_off = torch.stack([lo, hi], 1).cuda(), 0
+    a = gr._find_splits_native(H, cm, wyy)
+    b = gr._find_splits_torch(H, cm, wyy)
+    torch.testing.assert_close(a["gain"], b["gain"], rtol=1e-9, atol=1e-9)
+    ok = torch.isfinite(b["gain"])
+    assert torch.equal(a["feat"].cpu()[ok.cpu()], b["feat"].cpu()[ok.cpu()])
+    assert torch.equal(a["t"].cpu()[ok.cpu()], b["t"].cpu()[ok.cpu()])
+
+
 @pytest.mark.parametrize("weights", [None, "binary"])
 def test_hist_packed_single_atomic(weights):
     """Packed (count | biased fixed-point response) 64-bit atomics vs fp64 torch."""
