@@ -933,22 +933,24 @@ class TreeGrower:
             nb = b - a
             if self.W > 1:
                 # node-sharded reduction: every rank receives the summed pair
-                # histograms of 1/W of the nodes (reduce_scatter moves half the
-                # bytes of an all-reduce), scores and selects those nodes, and
-                # only the small per-node records are all-gathered
+                # histograms of 1/W of the nodes, packed at each feature's own
+                # width (sparse at deep levels: _pair_exchange), scores and
+                # selects those nodes, and only the small per-node records are
+                # all-gathered
                 W = self.W
                 npad = -(-nb // W) * W
-                Hv = Hp.view(nb, -1)
                 wv = wyy_n if wyy_n is not None else torch.zeros(nb, dtype=torch.float64, device=dev)
-                if npad > nb:
-                    Hv = torch.cat([Hv, torch.zeros((npad - nb, Hv.shape[1]), dtype=Hv.dtype, device=dev)], 0)
-                    wv = torch.cat([wv, torch.zeros(npad - nb, dtype=wv.dtype, device=dev)], 0)
-                    pfeat = torch.cat([pfeat, torch.zeros((npad - nb) * k, dtype=pfeat.dtype, device=dev)], 0)
                 nl = npad // W
                 lo = self.rank * nl
-                Hl = coll.reduce_scatter_dim0(Hv.contiguous())
+                pn_all = torch.arange(nb, device=dev).repeat_interleave(k)
+                Hmine = self._pair_exchange(Hp.view(nb * k, Bs, 2), pfeat.long(), pn_all, nb, full=False)
+                if npad > nb:
+                    wv = torch.cat([wv, torch.zeros(npad - nb, dtype=wv.dtype, device=dev)], 0)
+                    pfeat = torch.cat([pfeat, torch.zeros((npad - nb) * k, dtype=pfeat.dtype, device=dev)], 0)
+                Hl = torch.zeros((nl * k, Bs, 2), dtype=Hp.dtype, device=dev)
+                Hl[:Hmine.shape[0]] = Hmine
                 wl = coll.reduce_scatter_dim0(wv.contiguous()) if wyy_n is not None else None
-                del Hp, Hv
+                del Hp, Hmine
                 pk_l = torch.empty((nl, 12), dtype=torch.float64, device=dev)
                 mask_l = torch.empty((nl, Bs), dtype=torch.uint8, device=dev)
                 feat_l = torch.empty(nl, dtype=torch.int32, device=dev)
@@ -962,6 +964,77 @@ class TreeGrower:
             del Hp
         return {"pk": pk, "feat_i32": feat_i, "mask": mask, "gain": pk[:, 0], "feat": pk[:, 1].long(),
                 "t": pk[:, 2].long(), "opt": pk[:, 3].long(), "L": pk[:, 4:6], "R": pk[:, 6:8], "tot": pk[:, 8:10]}
+
+    # ------------------------------------------------------------------ multi-GPU pair exchange
+    def _pair_exchange(self, Hp, pf, pn, n, full):
+        """Sum the (node, feature) pair histograms of every rank without
+        shipping empty bins.  Hp: [P, Bs, C] dense rows of node-major pairs
+        (pair p belongs to node pn[p], feature pf[p]); node q is owned by rank
+        q // ceil(n / W).
+
+        Each pair row is packed at its feature's OWN width (bins + NA: <= 256
+        for the numeric columns, the cardinality for a categorical) instead of
+        the frame-wide stride Bs, the packed rows of every owner are laid out
+        back to back, and the level is summed either by ONE reduce-scatter of
+        the packed [W, Lmax] buffer or -- when the bins that are non-zero on
+        the busiest rank cost less than half of that (deep levels: nodes of a
+        few dozen rows fill a few bins of each 1000-level histogram) -- by ONE
+        all_to_all of (position, value) pairs summed by the owner.  Returns the
+        owner's dense [P_own, Bs, C] rows (pairs of its nodes, in order), or
+        with full=True every pair's summed dense row (packed all-gather).
+        Reference: hex/tree/DHistogram.java:366 -- the reference ships
+        per-node histograms of nbins = 20 numeric bins."""
+        W, r = self.W, self.rank
+        dev = Hp.device
+        P, Bs, C = Hp.shape
+        nl = -(-n // W)
+        if getattr(self, "_pw_t", None) is None or self._pw_t.device != dev:
+            nb = np.minimum(np.asarray(self.bd.nbins[:self.bd.F], dtype=np.int64), Bs - 1) + 1
+            self._pw_t = torch.as_tensor(nb, device=dev)
+        w = self._pw_t[pf]
+        owner = torch.div(pn, nl, rounding_mode="floor")
+        cw = torch.cumsum(w, 0)
+        start = cw - w
+        E = int(cw[-1]) if P else 0
+        own_cnt = torch.bincount(owner, minlength=W)
+        own_first = torch.cumsum(own_cnt, 0) - own_cnt                  # first pair of each owner
+        ch_start = torch.where(own_cnt > 0, start[own_first.clamp(max=max(P - 1, 0))] if P else own_cnt,
+                               torch.zeros_like(own_cnt))
+        Lq = torch.zeros(W, dtype=torch.int64, device=dev).index_add_(0, owner, w)
+        Lh = Lq.tolist()
+        Lmax = max(1, max(Lh))
+        pe = torch.repeat_interleave(torch.arange(P, device=dev), w)     # element -> pair
+        j = torch.arange(E, device=dev) - start[pe]                      # element -> packed bin
+        dense_idx = pe * Bs + torch.where(j == w[pe] - 1, torch.full_like(j, Bs - 1), j)
+        oe = owner[pe]
+        pos = start[pe] + j - ch_start[oe]                               # position in its owner's chunk
+        vals = Hp.reshape(P * Bs, C)[dense_idx]                          # [E, C]
+        nzm = (vals != 0).any(1)
+        dense_b = W * Lmax * C * 8
+        mx = torch.tensor([float(int(nzm.sum()) * (4 + 8 * C))], dtype=torch.float64, device=dev)
+        coll.allreduce_(mx, "max")
+        if float(mx[0]) < 0.5 * dense_b:
+            # sparse: (position, value) of the non-zero bins to their owner
+            from ...core.dist_munge import exchange
+            from ...core.vec import T_INT, T_REAL, Vec
+            got = exchange([Vec(pos[nzm].to(torch.int32), T_INT), Vec(vals[nzm].contiguous(), T_REAL)], oe[nzm])
+            chunk = torch.zeros((Lmax, C), dtype=Hp.dtype, device=dev).index_add_(
+                0, got[0].data.long(), got[1].data.to(Hp.dtype))
+        else:
+            buf = torch.zeros((W, Lmax, C), dtype=Hp.dtype, device=dev)
+            buf[oe, pos] = vals
+            chunk = coll.reduce_scatter_dim0(buf.view(W * Lmax, C))
+        if full:
+            allc = coll.all_gather_dim0(chunk).view(W, Lmax, C)
+            out = torch.zeros((P * Bs, C), dtype=Hp.dtype, device=dev)
+            out[dense_idx] = allc[oe, pos]
+            return out.view(P, Bs, C)
+        mine = oe == r
+        p0 = int(own_first[r]) if P else 0
+        Pr = int(own_cnt[r])
+        out = torch.zeros((max(Pr, 0) * Bs, C), dtype=Hp.dtype, device=dev)
+        out[dense_idx[mine] - p0 * Bs] = chunk[pos[mine]]
+        return out.view(Pr, Bs, C)
 
     def _pair_score_select(self, lib, Hp, n, k, pfeat, wyy_n, min_w2, pk, mask, feat_i):
         """Score the n*k pairs of Hp (cat_pair_kernel) and write the n nodes'
@@ -1016,7 +1089,8 @@ class TreeGrower:
             Hp, wyy_n = tree_ops.pair_hist(self.bd, ridx, va, vb, mode, st, ct, pn, pf, vmax=self._vmax, posv=posv,
                                            want_wyy=mode == 0)
         if self.W > 1:
-            coll.allreduce_(Hp)
+            if pn.size:
+                Hp = self._pair_exchange(Hp, tree_ops._h2d(pf, dev), tree_ops._h2d(pn, dev), n, full=True)
             if wyy_n is not None:
                 coll.allreduce_(wyy_n)
         P = pn.size
@@ -1536,8 +1610,11 @@ class TreeGrower:
         f_hi = np.full(1, np.inf) if mono_b else None
         self._bnd, self._bnd_off = None, 0
 
+        coll._TAG.append("tree.L0")
+        ntag = len(coll._TAG)
         while f_id.size:
             self._level = level
+            coll._TAG[ntag - 1] = f"tree.L{level}"       # collective bytes per level (coll.bytes_report)
             n_front = int(f_id.size)
             can_split = depth < p.max_depth
             C_ = tree_ops.channels(mode)
@@ -1847,6 +1924,7 @@ class TreeGrower:
                 p_par = np.arange(k, dtype=np.int64)
             depth += 1
             level += 1
+        del coll._TAG[ntag - 1:]
         self._flush_masks(tb)
         tree = tb.to_tree()
         if leaf_parts:

@@ -23,7 +23,44 @@ from . import cloud
 _TRACE = {"dir": None, "f": None, "seq": 0}
 
 
+# Byte accounting (always on, negligible cost): payload bytes this rank hands
+# to each collective, summed per (tag, op).  `tag(...)` scopes a region
+# (e.g. "tree.L7"); `bytes_report()` / `reset_bytes()` read / clear the table.
+# The payload is the tensor a rank contributes (all_gather: its slice;
+# reduce_scatter / all_reduce: the full buffer; all_to_all: its send buffer).
+_BYTES: dict = {}
+_TAG = ["-"]
+
+
+class tag:
+    def __init__(self, name):
+        self.name = str(name)
+
+    def __enter__(self):
+        _TAG.append(self.name)
+        return self
+
+    def __exit__(self, *a):
+        _TAG.pop()
+
+
+def bytes_report():
+    return dict(_BYTES)
+
+
+def reset_bytes():
+    _BYTES.clear()
+
+
+def _account(op, t):
+    if t is None or not hasattr(t, "numel"):
+        return
+    k = (_TAG[-1], op)
+    _BYTES[k] = _BYTES.get(k, 0) + t.numel() * t.element_size()
+
+
 def _trace(op, t=None):
+    _account(op, t)
     d = _TRACE["dir"]
     if d is None:
         import os

@@ -99,12 +99,41 @@ def run(out_path):
     res["bin_prauc"] = mb.aucpr()
     res["persist"] = _persist_roundtrip(h2o, fr, x, os.path.dirname(out_path))
     res["dist_ops"] = _dist_ops(h2o)
+    res["drf_pairs"] = _drf_pairs(h2o)
     from h2o3_amd.parallel import cloud
     if cloud.rank() == 0:
         with open(out_path, "w") as f:
             json.dump(res, f)
     cloud.barrier()
     cloud.shutdown()
+
+
+def _drf_pairs(h2o):
+    """DRF with mtries << F (the row-direct pair-histogram path) on numeric
+    and high-cardinality categorical features: the trees must not depend on
+    the number of ranks (packed / sparse pair exchange)."""
+    import numpy as np
+    import pandas as pd
+    from h2o3_amd.estimators import H2ORandomForestEstimator
+    from h2o3_amd.parallel import collectives as coll
+    rng = np.random.default_rng(5)
+    n, F = 6000, 40
+    X = rng.normal(size=(n, F))
+    df = pd.DataFrame(X, columns=[f"f{i}" for i in range(F)])
+    for c in range(4):
+        df[f"c{c}"] = [f"L{v}" for v in rng.integers(0, 60, n)]
+    df["y"] = X[:, 0] + 0.5 * X[:, 1] * X[:, 2] + (df["c0"].str[1:].astype(int) % 7) * 0.2 + 0.1 * rng.normal(size=n)
+    fr = h2o.H2OFrame(df)
+    for c in range(4):
+        fr[f"c{c}"] = fr[f"c{c}"].asfactor()
+    coll.reset_bytes()
+    m = H2ORandomForestEstimator(ntrees=2, max_depth=10, mtries=6, seed=11, sample_rate=1.0, min_rows=2)
+    m.train(y="y", training_frame=fr)
+    trees = [[list(map(int, t.feat)), [round(float(v), 9) if np.isfinite(v) else str(v) for v in t.thr]]
+             for t in m._forest.trees]
+    by = coll.bytes_report()
+    return {"trees": trees, "rmse": round(m.rmse(), 9),
+            "a2a_levels": sorted({k[0] for k, v in by.items() if k[1] == "all_to_all_single" and k[0].startswith("tree")})}
 
 
 def _dist_ops(h2o):

@@ -64,6 +64,16 @@ def test_dist_ops_match_one_rank(results, op):
     assert one["dist_ops"][op] == two["dist_ops"][op]
 
 
+def test_drf_pair_exchange_same_trees(results):
+    """DRF on the pair path (mtries 6 of 44 features, 4 categoricals of
+    cardinality 60): identical trees at 1 and 2 ranks with the packed /
+    sparse pair exchange; the deep levels took the sparse all_to_all."""
+    one, two = results
+    assert one["drf_pairs"]["trees"] == two["drf_pairs"]["trees"]
+    assert one["drf_pairs"]["rmse"] == two["drf_pairs"]["rmse"]
+    assert two["drf_pairs"]["a2a_levels"], "no level used the sparse exchange"
+
+
 def test_persist_sharded_state(results):
     """save_model / load_model of models with row-sharded state (CV holdout
     predictions, GLRM X) on 2 ranks: the archive holds all rows, each loaded
