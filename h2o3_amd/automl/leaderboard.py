@@ -54,8 +54,13 @@ class Leaderboard:
         return v
 
     def as_frame(self, extra_columns=None):
-        import pandas as pd
         from ..core.frame import H2OFrame
+        return H2OFrame(self.as_pandas(extra_columns), column_types={"model_id": "string"})
+
+    def as_pandas(self, extra_columns=None):
+        """The leaderboard rows as a host table (replicated on every rank; no
+        frame, so REST reads need no collectives)."""
+        import pandas as pd
         rows = []
         for m in self.models:
             r = {"model_id": m.model_id}
@@ -67,7 +72,7 @@ class Leaderboard:
             if extra_columns == "ALL" or (isinstance(extra_columns, list) and "algo" in extra_columns):
                 r["algo"] = m.algo
             rows.append(r)
-        return H2OFrame(pd.DataFrame(rows), column_types={"model_id": "string"})
+        return pd.DataFrame(rows, columns=["model_id"] + list(_COLS[self.kind]) if not rows else None)
 
 
 def make_leaderboard(object, leaderboard_frame=None, sort_metric="AUTO", extra_columns=(), scoring_data="AUTO"):

@@ -18,6 +18,8 @@ _counters: dict = {}
 
 
 def make_key(prefix: str = "key") -> str:
+    from ..parallel import collectives
+    collectives._guard_check("make_key")     # a read served off the executor must not advance key counters
     with _lock:
         c = _counters.setdefault(prefix, itertools.count(1))
         k = f"{prefix}_{next(c)}"

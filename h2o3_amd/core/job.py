@@ -38,6 +38,9 @@ class Job:
         self.warnings = []
         self._cancel = False
         self.spmd = False          # set by the REST executor: cancel agreed across ranks on every tick
+        prev = dkv.get(self.key) if key else None
+        if isinstance(prev, Job) and prev._cancel:
+            self._cancel = True    # a queued (CREATED) build cancelled before it started
         dkv.put(self.key, self)
 
     def start(self):
@@ -62,8 +65,14 @@ class Job:
         if msg is not None:
             self.progress_msg = msg
         vals = [1.0 if self.cancel_requested else 0.0] + [float(e) for e in extra]
-        if (self._spmd_any() or extra) and cloud.is_distributed():
+        self._nticks = getattr(self, "_nticks", 0) + 1
+        # cancel-only ticks agree every 4th iteration (a count, so every rank
+        # picks the same ticks): one control-plane broadcast per 4 trees
+        # instead of per tree; decisions in `extra` are agreed every tick
+        if (extra or (self._spmd_any() and self._nticks % 4 == 1)) and cloud.is_distributed():
             vals = cloud.agree(vals)
+        elif cloud.is_distributed() and self._spmd_any():
+            vals[0] = 0.0
         if vals[0]:
             self._cancel = True
             raise JobCancelled(self.key)

@@ -138,6 +138,8 @@ def broadcast_obj(obj, src: int = 0):
     """Broadcast a picklable host object from `src` on the control group."""
     if not is_distributed():
         return obj
+    from . import collectives
+    collectives._trace("broadcast_obj")
     lst = [obj]
     dist.broadcast_object_list(lst, src=src, group=_state["ctl"])
     return lst[0]
@@ -207,6 +209,8 @@ def _atexit_shutdown():
 
 def barrier():
     if is_distributed():
+        from . import collectives
+        collectives._trace("barrier")
         if is_gpu() and dist.get_backend() == "nccl":
             dist.barrier(device_ids=[device().index])
         else:

@@ -59,7 +59,35 @@ def _account(op, t):
     _BYTES[k] = _BYTES.get(k, 0) + t.numel() * t.element_size()
 
 
+class CollectiveForbidden(RuntimeError):
+    """A collective was issued inside `forbid()` (a read served off the
+    SPMD executor must not join the cloud's collective sequence)."""
+
+
+_guard = __import__("threading").local()
+
+
+class forbid:
+    """Thread-scoped guard: any collective issued by this thread inside the
+    block raises CollectiveForbidden instead of running (rank 0's HTTP thread
+    serves reads while the executor thread drives the cloud)."""
+
+    def __enter__(self):
+        self._prev = getattr(_guard, "on", False)
+        _guard.on = True
+        return self
+
+    def __exit__(self, *a):
+        _guard.on = self._prev
+
+
+def _guard_check(op):
+    if getattr(_guard, "on", False) and cloud.is_distributed():
+        raise CollectiveForbidden(op)
+
+
 def _trace(op, t=None):
+    _guard_check(op)
     _account(op, t)
     d = _TRACE["dir"]
     if d is None:

@@ -29,6 +29,7 @@ from __future__ import annotations
 import asyncio
 import json as _json
 import os
+import sys
 import tempfile
 import time
 import uuid
@@ -48,6 +49,13 @@ from . import spmd
 # requests served straight from rank 0's state on the HTTP thread (no
 # collective, no command replay): clients poll / cancel jobs and read the
 # cloud status while a build holds the executor
+# GETs served on the HTTP thread while a build runs (collectives refused:
+# collectives.forbid; a read that needs one is queued as usual)
+_READ_PREFIXES = ("/3/Frames", "/3/Models", "/99/Models", "/99/Leaderboards", "/99/AutoML", "/3/ModelBuilders",
+                  "/99/Grids", "/3/Grids", "/3/ModelMetrics", "/3/DKV", "/99/Rapids/help")
+# builds accepted while another build runs: CREATED job at once, run later
+_BUILD_ROUTES = {"/3/ModelBuilders/{algo}": "model", "/99/Grid/{algo}": "grid", "/99/AutoMLBuilder": "automl"}
+
 _LOCAL_PREFIXES = ("/3/Cloud", "/3/Metadata", "/4/sessions", "/3/InitID", "/3/Capabilities", "/3/About",
                    "/3/Jobs", "/3/NodePersistentStorage", "/3/Ping", "/3/Logs", "/3/JStack", "/3/WaterMeter",
                    "/3/SteamMetrics", "/3/Profiler", "/3/SessionProperties", "/3/Typeahead", "/3/LogAndEcho")
@@ -193,6 +201,18 @@ def _put_frame(fr: H2OFrame, fid=None) -> str:
         except AttributeError:
             pass
     dkv.put(fid, fr)
+    # row counts and rollups now, on every rank (this runs replayed on the
+    # executor): later frame reads are served from these caches without
+    # collectives, also while a build runs (the reference's parse ends with
+    # the rollups too, water/parser/ParseDataset.java)
+    if cloud.is_distributed():
+        for v in fr._vecs:
+            v.nrow()
+            if v.is_numeric and not v.on_host:
+                try:
+                    v.rollups()
+                except Exception:  # noqa: BLE001 - a column without rollups is read through the executor
+                    pass
     return fid
 
 
@@ -276,6 +296,51 @@ def create_app(flow_dir: str | None = None, serve: bool = True) -> FastAPI:
     executor = spmd.Executor(run_command) if serve else None
     app.state.executor = executor
 
+    def _queue_build(kind, cmd, path_params):
+        """A build that arrives while another one runs: fix its job key and
+        destination now (hints broadcast with the command, so every rank uses
+        them), answer with the CREATED job, and let the executor run it in
+        turn (ModelBuilderHandler / GridSearchHandler / AutoMLBuilderHandler
+        return the job without waiting, water/api/ModelBuilderHandler.java:51)."""
+        from ..core import job as jobmod
+        import secrets
+        q = secrets.token_hex(6)
+        p = dict(cmd["p"])
+        algo = path_params.get("algo", "automl")
+        if kind == "model":
+            dest = p.get("model_id") or f"{algo}_model_q{q}"
+            p["model_id"] = dest
+            desc, dk = f"{algo} Model Build", "Model"
+        elif kind == "grid":
+            dest = p.get("grid_id") or f"Grid_{algo}_q{q}"
+            p["grid_id"] = dest
+            desc, dk = "GridSearch", "Grid"
+        else:
+            bc = dict(p.get("build_control") or {})
+            dest = bc.get("project_name") or f"automl_q{q}"
+            bc["project_name"] = dest
+            p["build_control"] = bc
+            desc, dk = "AutoML", "AutoML"
+        key = f"job_q{q}"
+        job = jobmod.Job(desc, dest=dest, key=key, dest_kind=dk)        # CREATED, rank 0's job table
+        cmd = dict(cmd, p=p, hints={"job_key": key})
+
+        def _done(f):
+            e = f.exception()
+            if e is not None and job.status == "CREATED":
+                job.fail(e)
+        executor.submit(cmd).add_done_callback(_done)
+        if kind == "model":
+            return JSONResponse(S.jsonable({"__meta": S.meta(f"{algo.capitalize()}V3", "ModelBuilder"), "algo": algo,
+                                            "job": S.job_v3(job, dest=dest, dest_kind="Model"), "messages": [],
+                                            "error_count": 0, "parameters": None}))
+        if kind == "grid":
+            return JSONResponse(S.jsonable({"__meta": S.meta("GridSearchSchemaV99", "Grid", 99),
+                                            "grid_id": S.key(dest, "Grid"), "job": S.job_v3(job),
+                                            "total_models": 0}))
+        return JSONResponse(S.jsonable({"__meta": S.meta("AutoMLBuildSpecV99", "AutoMLBuildSpec", 99),
+                                        "job": S.job_v3(job), "build_control": {"project_name": dest}}))
+
     def route(method, path):
         """Register an async handler taking (params, request, **path)."""
         rx = _re.compile(_re.sub(r"\{(\w+)\}", r"(?P<\1>[^/]+)", _re.escape(path).replace(r"\{", "{")
@@ -303,11 +368,40 @@ def create_app(flow_dir: str | None = None, serve: bool = True) -> FastAPI:
                             NotImplementedError) as e:
                         raise _HTTPError(400 if not isinstance(e, KeyError) else 404, str(e), e)
                     return _to_response(out)
+                if method == "GET" and path.startswith(_READ_PREFIXES) and executor is not None and \
+                        cloud.is_distributed() and executor.busy():
+                    # a read while a build runs: on this thread, no collectives
+                    from ..parallel import collectives as _coll
+                    try:
+                        with _coll.forbid():
+                            out = fn(p, request, **request.path_params)
+                            if hasattr(out, "__await__"):
+                                out = await out
+                        return _to_response(out)
+                    except _HTTPError:
+                        raise
+                    except _coll.CollectiveForbidden as e:
+                        if os.environ.get("H2O3_REST_DEBUG"):
+                            import traceback as _tb
+                            print(f"read {path} needs a collective ({e}):", "".join(_tb.format_exception(type(e), e, e.__traceback__)[-8:]),
+                                  file=sys.stderr, flush=True)
+                        # needs the cloud: queue it below
+                    except (KeyError, ValueError, TypeError, AssertionError, IndexError, NotImplementedError) as e:
+                        raise _HTTPError(400 if not isinstance(e, KeyError) else 404, str(e), e)
+                    except RuntimeError as e:
+                        if os.environ.get("H2O3_REST_DEBUG"):
+                            import traceback as _tb
+                            print(f"read {path} failed off the executor: {e!r}", _tb.format_exc(), file=sys.stderr,
+                                  flush=True)
+                        # e.g. a dict the build is mutating: queue it
                 # replayed on every rank by the executor (spmd.py)
                 req = {"method": request.method, "path": request.url.path, "headers": dict(request.headers),
                        "body": await request.body(), "query": dict(request.query_params)}
                 cmd = {"kind": "route", "method": method, "path": path, "p": p, "kw": dict(request.path_params),
                        "req": req, "defer": True}
+                kind = _BUILD_ROUTES.get(path) if method == "POST" else None
+                if kind is not None and executor is not None and executor.busy():
+                    return _queue_build(kind, cmd, request.path_params)
                 try:
                     return await asyncio.wrap_future(executor.submit(cmd))
                 except _HTTPError:
@@ -569,9 +663,20 @@ def create_app(flow_dir: str | None = None, serve: bool = True) -> FastAPI:
     # ----------------------------------------------------------- frames
     @route("GET", "/3/Frames")
     def frames(p, r):
-        fs = [(k, dkv.get(k)) for k in dkv.keys()]
-        return {"__meta": S.meta("FramesListV3", "Frames"),
-                "frames": [S.frame_base_v3(k, f) for k, f in fs if isinstance(f, H2OFrame)]}
+        from ..parallel import collectives as _coll
+        fs = [(k, dkv.get(k)) for k in list(dkv.keys())]
+        out = []
+        for k, f in fs:
+            if not isinstance(f, H2OFrame):
+                continue
+            try:
+                out.append(S.frame_base_v3(k, f))
+            except _coll.CollectiveForbidden:
+                # a frame whose row count was never reduced, listed while a build
+                # runs: its key only (h2o.ls() reads the keys)
+                out.append({"__meta": S.meta("FrameBaseV3", "Frame"), "frame_id": S.key(k), "byte_size": -1,
+                            "is_text": False, "rows": -1, "columns": f.ncol})
+        return {"__meta": S.meta("FramesListV3", "Frames"), "frames": out}
 
     def _frame_get(p, fid, rollups=True, percentiles=False):
         fr = _frame(fid)
@@ -676,7 +781,7 @@ def create_app(flow_dir: str | None = None, serve: bool = True) -> FastAPI:
             m = cls(**kw)
         except (ValueError, TypeError) as e:      # parameter validation (ModelBuilder.init error(...))
             raise _HTTPError(412, f"Illegal argument(s) for {algo} model: {e}", e, builder=True)
-        job = jobmod.Job(f"{algo} Model Build", dest=m.model_id).start()
+        job = jobmod.Job(f"{algo} Model Build", dest=m.model_id, key=spmd.hint("job_key")).start()
         job.spmd = cloud.is_distributed()
 
         def work():
@@ -1089,7 +1194,7 @@ def create_app(flow_dir: str | None = None, serve: bool = True) -> FastAPI:
         from ..core import job as jobmod
         g = H2OGridSearch(cls(**{k: v for k, v in p.items() if v is not None}), hyper, grid_id=gid,
                           search_criteria=crit, **({"recovery_dir": recovery_dir} if recovery_dir else {}))
-        job = jobmod.Job("GridSearch", dest=g.grid_id, dest_kind="Grid").start()
+        job = jobmod.Job("GridSearch", dest=g.grid_id, dest_kind="Grid", key=spmd.hint("job_key")).start()
         job.spmd = cloud.is_distributed()
         dkv.put(g.grid_id, g)           # visible (and growing) while the search runs
 
@@ -1158,7 +1263,7 @@ def create_app(flow_dir: str | None = None, serve: bool = True) -> FastAPI:
 
     @route("GET", "/99/Grids")
     def grids(p, r):
-        gs = [k for k in dkv.keys() if hasattr(dkv.get(k), "model_ids") and not hasattr(dkv.get(k), "leaderboard")]
+        gs = [k for k in dkv.keys() if hasattr(dkv.get(k), "model_ids") and not hasattr(type(dkv.get(k)), "leaderboard")]
         return {"__meta": S.meta("GridsV99", "Grids", 99), "grids": [grid_get({}, r, k) for k in gs]}
 
     @route("POST", "/99/AutoMLBuilder")
@@ -1177,7 +1282,7 @@ def create_app(flow_dir: str | None = None, serve: bool = True) -> FastAPI:
         ign = set(ispec.get("ignored_columns") or [])
         x = [c for c in tf.names if c != y and c not in ign]
         job = jobmod.Job("AutoML", dest=aml.project_name, dest_kind="AutoML",
-                         key=f"automl_{aml.project_name}_{dkv.make_key('amljob')}").start()
+                         key=spmd.hint("job_key") or f"automl_{aml.project_name}_{dkv.make_key('amljob')}").start()
         job.spmd = cloud.is_distributed()
 
         def work():
@@ -1200,7 +1305,8 @@ def create_app(flow_dir: str | None = None, serve: bool = True) -> FastAPI:
         return resp
 
     def _lb_table(aml):
-        lb = aml.leaderboard.as_data_frame()
+        lbo = getattr(aml, "_leaderboard", None)
+        lb = lbo.as_pandas() if hasattr(lbo, "as_pandas") else aml.leaderboard.as_data_frame()
         cols = {c: lb[c].tolist() for c in lb.columns}
         return lb, S.twodim("Leaderboard", cols, "models sorted by the leaderboard metric",
                             row_headers=[str(i) for i in range(len(lb))])
@@ -1208,7 +1314,7 @@ def create_app(flow_dir: str | None = None, serve: bool = True) -> FastAPI:
     @route("GET", "/99/Leaderboards/{project}")
     def leaderboard(p, r, project):
         aml = dkv.get(project)
-        if aml is None or not hasattr(aml, "leaderboard"):
+        if aml is None or not hasattr(type(aml), "leaderboard"):
             raise _HTTPError(404, f"AutoML project {project} not found")
         lb, tab = _lb_table(aml)
         return {"__meta": S.meta("LeaderboardV99", "Leaderboard", 99), "project_name": project,

@@ -229,7 +229,7 @@ def register(app, route, ctx):
 
     @route("GET", "/99/Leaderboards")
     def leaderboards(p, r):
-        names = [k for k in dkv.keys() if hasattr(dkv.get(k), "leaderboard")]
+        names = [k for k in dkv.keys() if hasattr(type(dkv.get(k)), "leaderboard")]
         return {"__meta": S.meta("LeaderboardsV99", "Iced", 99),
                 "leaderboards": [{"project_name": k} for k in names]}
 

@@ -22,7 +22,13 @@ node holding the data" -- it is *replayed* on every rank:
   is sent to the client.
 * a model / grid / AutoML build returns a `Deferred`: the executor answers
   the HTTP request with the RUNNING job at once, then runs the build on the
-  same thread.  Requests that only read rank-0 state (`/3/Jobs`, `/3/Cloud`,
+  same thread.  A build request that arrives while another build runs is
+  answered at once with a CREATED job whose key / destination rank 0 fixes
+  up front (`hint`); it runs when the executor gets to it.  Read-only GETs
+  (frames, models, grids, leaderboards, AutoML state) are served on the HTTP
+  thread while a build runs, under a guard that refuses any collective
+  (parallel/collectives.forbid): a read that would need one (an uncached
+  rollup) is queued on the executor like before.  Requests that only read rank-0 state (`/3/Jobs`, `/3/Cloud`,
   metadata, Flow notebook storage) are served by the HTTP thread directly,
   so a client polls live progress and can cancel while the build runs;
   the cancel flag reaches every rank through the per-iteration agreement in
@@ -59,6 +65,12 @@ def seed(nonce):
 def rand_hex(n=16):
     """Random-looking hex id, identical on every rank for one command."""
     return "".join("%x" % _rng.getrandbits(4) for _ in range(n))
+
+
+def hint(name):
+    """A value rank 0 fixed for this command before it was queued (the job
+    key / destination of a build accepted while another one runs)."""
+    return (getattr(_ctx, "hints", None) or {}).get(name)
 
 
 def defer_allowed():
@@ -127,6 +139,10 @@ class Executor:
             self._th.start()
         return self
 
+    def busy(self) -> bool:
+        """A command (a build) is running or queued on the executor."""
+        return self.current is not None or not self.q.empty() or getattr(self, "_running", False)
+
     def submit(self, cmd) -> concurrent.futures.Future:
         fut: concurrent.futures.Future = concurrent.futures.Future()
         if not cloud.healthy():
@@ -163,7 +179,11 @@ class Executor:
                 self.stopped = True
                 fut.set_result(None)
                 return
-            execute(cmd, fut, loop, self)
+            self._running = True
+            try:
+                execute(cmd, fut, loop, self)
+            finally:
+                self._running = False
 
 
 def _bind_device():
@@ -178,6 +198,7 @@ def execute(cmd, fut, loop, ex=None):
     """Run one command on this rank; fut (rank 0 only) gets the response."""
     seed(cmd.get("nonce", 0))
     _ctx.allow_defer = bool(cmd.get("defer", False))
+    _ctx.hints = cmd.get("hints")
     try:
         out = ex.run_command(cmd, loop) if ex is not None else _run_local(cmd, loop)
     except BaseException as e:  # noqa: BLE001 - handed to the HTTP thread

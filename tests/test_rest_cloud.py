@@ -34,7 +34,7 @@ def _launch(world, gpu=False):
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(mport), OMP_NUM_THREADS="2", PYTHONPATH=ROOT, H2O3_SPMD_IDLE_S="5")
+                   MASTER_PORT=str(mport), OMP_NUM_THREADS="2", PYTHONPATH=ROOT, H2O3_SPMD_IDLE_S="5", H2O3_REST_DEBUG="1")
         if gpu:
             env["H2O3_DIST_BACKEND"] = "gloo"      # N ranks share the box's one GPU: gloo data plane
         else:
@@ -183,6 +183,55 @@ def test_cancel_stops_a_long_gbm(cloud2):
     fr = requests.get(cloud2 + "/3/Frames/cancel.hex").json()["frames"][0]
     assert fr["rows"] == 20000
     assert requests.get(cloud2 + "/3/Models/gbm_cancel").status_code == 404
+
+
+def test_reads_and_queued_builds_during_a_build(cloud2):
+    """While a 10k-tree GBM runs on the 2-rank cloud, frame / model /
+    leaderboard / AutoML-event-log reads answer within 1 s each (served off
+    the executor, collectives refused), and a second build is accepted at
+    once as a CREATED job that runs after the first one."""
+    _upload(cloud2, _data(3000, 4), "aml.hex")
+    r = requests.post(cloud2 + "/99/AutoMLBuilder", json={
+        "build_control": {"project_name": "aml_conc", "nfolds": 0, "stopping_criteria": {"max_models": 1, "seed": 1}},
+        "input_spec": {"training_frame": "aml.hex", "response_column": "y", "ignored_columns": ["r"]},
+        "build_models": {"include_algos": ["GLM"]}})
+    assert r.status_code == 200, r.text
+    assert _wait(cloud2, r.json()["job"])["status"] == "DONE"
+    _upload(cloud2, _data(20000, 5), "long.hex")
+    r = requests.post(cloud2 + "/3/ModelBuilders/gbm", json={"training_frame": "long.hex", "response_column": "y",
+                                                              "ntrees": 10000, "max_depth": 5, "model_id": "gbm_long"})
+    job = r.json()["job"]
+    key = job["key"]["name"]
+    t0 = time.time()
+    while time.time() - t0 < 120:
+        job = requests.get(cloud2 + f"/3/Jobs/{key}").json()["jobs"][0]
+        if job["progress"] > 0:
+            break
+        time.sleep(0.05)
+    assert job["status"] == "RUNNING"
+    for path in ("/3/Frames", "/3/Frames/aml.hex", "/3/Models", "/99/Leaderboards/aml_conc", "/99/AutoML/aml_conc"):
+        t1 = time.time()
+        rr = requests.get(cloud2 + path, timeout=30)
+        dt = time.time() - t1
+        assert rr.status_code == 200, (path, rr.text[:300])
+        assert dt < 1.0, (path, dt)
+    assert any(f["frame_id"]["name"] == "long.hex" for f in requests.get(cloud2 + "/3/Frames").json()["frames"])
+    ev = requests.get(cloud2 + "/99/AutoML/aml_conc").json()
+    assert ev.get("event_log") is not None or ev.get("leaderboard") is not None
+    # a second build while the first runs: CREATED at once, runs afterwards
+    t1 = time.time()
+    r2 = requests.post(cloud2 + "/3/ModelBuilders/glm", json={"training_frame": "aml.hex", "response_column": "r",
+                                                               "model_id": "glm_queued", "ignored_columns": ["y"]},
+                       timeout=30)
+    assert time.time() - t1 < 1.0 and r2.status_code == 200, r2.text
+    j2 = r2.json()["job"]
+    assert j2["status"] == "CREATED"
+    assert requests.get(cloud2 + f"/3/Jobs/{j2['key']['name']}").json()["jobs"][0]["status"] == "CREATED"
+    assert requests.post(cloud2 + f"/3/Jobs/{key}/cancel").status_code == 200
+    assert _wait(cloud2, job, timeout=60)["status"] == "CANCELLED"
+    j2 = _wait(cloud2, j2, timeout=120)
+    assert j2["status"] == "DONE", j2
+    assert requests.get(cloud2 + "/3/Models/glm_queued").status_code == 200
 
 
 @pytest.mark.skipif(not os.path.isdir("/root/reference/h2o-py/h2o") and not os.environ.get("H2O_PY_REFERENCE"),
