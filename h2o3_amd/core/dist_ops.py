@@ -132,32 +132,50 @@ def kth_smallest(x: torch.Tensor, k: int) -> float:
 
 def kth_smallest_many(x: torch.Tensor, ks) -> dict:
     """{k: k-th smallest (0-based)} for many ranks k at once over every rank's
-    x (no NaN): each refinement pass is ONE pass over the surviving
-    candidates -- every targeted bin of the previous pass becomes a group with
-    its own exact [min, max] range and 1024 sub-bins, counted with one
-    all-reduced bincount over all groups -- and groups with few values (or a
-    single value) are finished exactly from a gather of their values."""
+    x (no NaN), exact.  Quantile.java's refinement, vectorised over targets:
+    each pass is ONE pass over the surviving candidates -- every targeted bin
+    of the previous pass becomes a group with its own 1024 sub-bins over the
+    bin's edges, counted by one all-reduced bincount over all groups -- and
+    groups with few values are finished exactly from a gather of their values.
+    No per-group min / max scatter (a handful of slots taking 10^8 atomic
+    updates): ranges come from the bin edges, and a group whose range has
+    shrunk to rounding width gets its exact min / max by a masked reduction."""
     ks_l = sorted(set(int(k) for k in ks))
     if not ks_l:
         return {}
     dev = x.device
     cand = x.to(torch.float64)
-    gid = torch.zeros(cand.numel(), dtype=torch.int64, device=dev)
+    lo, hi = _range(cand)
     tk = torch.tensor(ks_l, dtype=torch.int64, device=dev)       # target ranks
+    res = torch.full((tk.numel(),), math.nan, dtype=torch.float64, device=dev)
+    if lo == hi:
+        return dict(zip(ks_l, [lo] * len(ks_l)))
+    gid = torch.zeros(cand.numel(), dtype=torch.int64, device=dev)
     tg = torch.zeros_like(tk)                                      # their group
     goff = torch.zeros(1, dtype=torch.int64, device=dev)          # rank offset per group
-    res = torch.full((tk.numel(),), math.nan, dtype=torch.float64, device=dev)
-    tpos = torch.arange(tk.numel(), device=dev)                   # slot of each live target in res
+    ga = torch.tensor([lo], dtype=torch.float64, device=dev)      # group range [a, a + span]
+    gspan = torch.tensor([hi - lo], dtype=torch.float64, device=dev)
+    tpos = torch.arange(tk.numel(), device=dev)
+    level = 0
     while tk.numel():
         G = goff.numel()
         cnt = _ar(torch.bincount(gid, minlength=G))
-        inf = torch.full((G,), math.inf, dtype=torch.float64, device=dev)
-        mm = torch.stack([inf.scatter_reduce(0, gid, cand, "amin"), inf.scatter_reduce(0, gid, -cand, "amin")])
-        _ar(mm, "min")
-        mn, mx = mm[0], -mm[1]
-        small = (cnt <= _GATHER_AT) | (mn == mx)
+        # a range at rounding width (or a group still large after 4 passes,
+        # i.e. narrowed 1024^4-fold: repeated values): exact min / max of those
+        tiny = (gspan <= torch.maximum(ga.abs(), (ga + gspan).abs()) * 1e-12) | (level >= 4)
+        level += 1
+        const = torch.zeros(G, dtype=torch.bool, device=dev)
+        for g in torch.nonzero(tiny & (cnt > _GATHER_AT)).view(-1).tolist():
+            v = cand[gid == g]
+            a, b = _range(v)
+            if a == b:
+                const[g] = True
+                ga[g] = a
+            else:
+                ga[g], gspan[g] = a, b - a
+        small = (cnt <= _GATHER_AT) | const
         if bool(small.any()):
-            pick = small[gid]
+            pick = small[gid] & ~const[gid]
             gv, gg = _gather(cand[pick]), _gather(gid[pick])
             o = lexsort([gg.to(torch.float64), gv])
             gv, gg = gv[o], gg[o]
@@ -165,18 +183,18 @@ def kth_smallest_many(x: torch.Tensor, ks) -> dict:
             ts = small[tg]
             g_s = tg[ts]
             pos = (st[g_s] + tk[ts] - goff[g_s]).clamp(0, max(gv.numel() - 1, 0))
-            val = torch.where(mn[g_s] == mx[g_s], mn[g_s], gv[pos] if gv.numel() else mn[g_s])
+            val = torch.where(const[g_s], ga[g_s], gv[pos] if gv.numel() else ga[g_s])
             res[tpos[ts]] = val
             tk, tg, tpos = tk[~ts], tg[~ts], tpos[~ts]
         if not tk.numel():
             break
-        # refine the remaining groups: 1024 sub-bins over each group's exact range
         rem = ~small
         remap = torch.cumsum(rem.to(torch.int64), 0) - 1
         keep = rem[gid]
         cand, gid = cand[keep], remap[gid[keep]]
         R = int(rem.sum())
-        a, span, off_r = mn[rem], (mx - mn)[rem], goff[rem]
+        a, span, off_r = ga[rem], gspan[rem], goff[rem]
+        # floor of a monotone map: sub-bins respect the value order
         sub = ((cand - a[gid]) * (_BINS / span[gid])).floor().clamp_(0, _BINS - 1).long()
         idx = gid * _BINS + sub
         cum = torch.cumsum(_ar(torch.bincount(idx, minlength=R * _BINS)).view(R, _BINS), 1)
@@ -186,12 +204,17 @@ def kth_smallest_many(x: torch.Tensor, ks) -> dict:
         key = tr * _BINS + j
         ukey, inv = torch.unique(key, return_inverse=True)
         noff = torch.zeros(ukey.numel(), dtype=torch.int64, device=dev).scatter_(0, inv, off_r[tr] + below)
+        ur, uj = torch.div(ukey, _BINS, rounding_mode="floor"), ukey % _BINS
+        w = span[ur] / _BINS
+        na = a[ur] + uj.to(torch.float64) * w
+        # the edge sub-bins absorb the clamp: keep the group's full outer range there
+        nspan = torch.where(uj == _BINS - 1, a[ur] + span[ur] - na, w)
         lut = torch.full((R * _BINS,), -1, dtype=torch.int64, device=dev)
         lut[ukey] = torch.arange(ukey.numel(), device=dev)
         ng = lut[idx]
         live = ng >= 0
         cand, gid = cand[live], ng[live]
-        tg, goff = inv, noff
+        tg, goff, ga, gspan = inv, noff, na, nspan
     return dict(zip(ks_l, res.tolist()))
 
 

@@ -546,7 +546,8 @@ class GLMDriver:
                     Gf, dev, gx = linalg_ops.glm_irls(self.X, aug=P, beta=bt, b0=float(self.beta[-1]),
                                                       y=self._y32, wprior=self._w32, offset=self._off32,
                                                       codes=codes, tvp=self.fam.tvp, theta=self.fam.theta,
-                                                      width=self.Pp, grad=True, bf3=bf3)
+                                                      width=self.Pp, grad=True, bf3=bf3,
+                                                      grad_f64=self._hprec not in (None, "bf3"))
                     self._gexact = torch.cat([gx[:P], gx[self.Pp:self.Pp + 1]])
                     self._gbeta = np.concatenate([self.beta[:P].astype(np.float32).astype(np.float64),
                                                   [float(np.float32(self.beta[-1]))]])

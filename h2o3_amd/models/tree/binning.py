@@ -26,8 +26,8 @@ scoring time, so training and scoring never disagree.
   RoundRobin      : the same grid; each tree draws UniformAdaptive / Random /
                     QuantilesGlobal (DHistogram.java:226-233)
   UniformRobust   : uniform grid, outlier-robust range (0.1/99.9 pct)
-  AUTO            : QuantilesGlobal with max(nbins, 254) bins, capped at 254
-                    (the GPU-native default)
+  AUTO            : 254 quantile cells from a 1M-row sample, range from the
+                    exact min / max (the GPU-native default)
 Categorical columns: code = level (levels beyond nbins_cats are grouped
 into contiguous buckets, as the reference does for high cardinality).
 NA (and any out-of-domain value) maps to the last code of the histogram
@@ -123,6 +123,23 @@ def _global_finite(x):
     return xs, n, float(st[1]), -float(st[2]), float(st[3]) == 0.0
 
 
+def _sample_quantile_cuts(xs, lo, B, seed):
+    """AUTO: quantile cuts from a 1M-row sample (all-gathered over ranks)."""
+    idx = _sample_rows(xs.shape[0], 1 << 20, xs.device, seed)
+    samp = xs[idx] if idx is not None else xs
+    if cloud.is_distributed():
+        samp = coll.all_gather_var(samp)
+    u = torch.unique(samp)
+    if u.numel() <= B:
+        uu = u.cpu().numpy()
+        return (uu[:-1] + uu[1:]) / 2.0 if len(uu) > 1 else np.zeros(0)
+    q = torch.linspace(0, 1, B + 1, dtype=torch.float64, device=samp.device)[1:-1]
+    srt = torch.sort(samp).values
+    pos = (q * (srt.numel() - 1)).round().long()
+    c = torch.unique(srt[pos]).cpu().numpy()
+    return c[c > lo]
+
+
 def _exact_quantile_cuts(xs, n, lo, B, seed):
     """Cut points at the order statistics round(q (n-1)), q = k / B (exact,
     distributed histogram refinement: core/dist_ops.kth_smallest_many), or
@@ -152,7 +169,8 @@ def compute_cuts(cols, is_cat, hist_type="AUTO", nbins=20, nbins_top_level=1024,
                  seed=1234, sample=1 << 20):
     """Per-feature cut points (list of float64 numpy arrays) and bin counts.
 
-    QuantilesGlobal / AUTO: exact global quantiles (all rows, every rank).
+    QuantilesGlobal: exact global quantiles (all rows, every rank); AUTO:
+    254 cells from a 1M-row sample.
     UniformAdaptive / Random / RoundRobin: the reference's top-level grid
     (DHistogram.initialHist): nbins_top_level uniform cells over the exact
     column [min, max], or one cell per integer when an integer column spans
@@ -178,9 +196,11 @@ def compute_cuts(cols, is_cat, hist_type="AUTO", nbins=20, nbins_top_level=1024,
             nb_list.append(1)
             groups.append(1)
             continue
-        if ht in ("auto", "quantilesglobal"):
-            B = min(254, max(nbins, 254)) if ht == "auto" else min(max(nbins, 2), 4095)
-            c = _exact_quantile_cuts(xs, n, lo, B, seed + j)
+        if ht == "auto":
+            # the GPU-native default: 254 quantile cells from a 1M-row sample
+            c = _sample_quantile_cuts(xs, lo, min(254, max(nbins, 254)), seed + j)
+        elif ht == "quantilesglobal":
+            c = _exact_quantile_cuts(xs, n, lo, min(max(nbins, 2), 4095), seed + j)
         elif ht in ("uniformadaptive", "random", "roundrobin"):
             B = min(max(nbins_top_level, nbins), 4095)
             if hi <= lo:

@@ -120,6 +120,7 @@ struct GlmFamArgs {
                 // sqrt(W) by ds_bpermute instead of DPP + LDS (ws kernel)
   int signed_w; // external weights may be negative (no sqrt(W) pre-scaling)
   int bf3;      // P = 128 ws path: bf16x3 MFMA operands instead of f32
+  int grad_f64; // exact-gradient channel: f64 products (1) or f32 products summed per chunk, f64 beyond (0)
 };
 
 __device__ __forceinline__ float gi_linkinv(int link, float eta) {
@@ -585,21 +586,43 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
 #pragma unroll
         for (int v = 0; v < NVP; ++v) rv[v] = __shfl(rres, v * RPV + lane / P4, 64);
       }
-      double a[4];
+      if (fam.grad_f64) {
+        // exact products: ill-conditioned designs (the f32 / f64 Hessian tiers)
+        double a[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        a[e] = 0.0;
+        for (int e = 0; e < 4; ++e) {
+          a[e] = 0.0;
 #pragma unroll
-        for (int v = 0; v < NVP; ++v) a[e] = fma((double)V[v][e], (double)rv[v], a[e]);
-      }
+          for (int v = 0; v < NVP; ++v) a[e] = fma((double)V[v][e], (double)rv[v], a[e]);
+        }
 #pragma unroll
-      for (int o = P4; o < 64; o <<= 1) {
+        for (int o = P4; o < 64; o <<= 1) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) a[e] += __shfl_xor(a[e], o, 64);
-      }
-      if (lane < P4) {
+          for (int e = 0; e < 4; ++e) a[e] += __shfl_xor(a[e], o, 64);
+        }
+        if (lane < P4) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) gs[pw][lane][e] += a[e];
+          for (int e = 0; e < 4; ++e) gs[pw][lane][e] += a[e];
+        }
+      } else {
+        // f32 products over the lane's rows of the chunk, f64 beyond (the
+        // bf16x3 tier: condition number < 2e3, product rounding is harmless)
+        float a[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          a[e] = 0.f;
+#pragma unroll
+          for (int v = 0; v < NVP; ++v) a[e] = fmaf(V[v][e], rv[v], a[e]);
+        }
+#pragma unroll
+        for (int o = P4; o < 64; o <<= 1) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) a[e] += __shfl_xor(a[e], o, 64);
+        }
+        if (lane < P4) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) gs[pw][lane][e] += (double)a[e];
+        }
       }
     };
     auto load = [&](int c, Stage& st) {
@@ -998,7 +1021,7 @@ extern "C" int h2o_glm_irls(const float* X, long long N, int P, int ldx, const i
                             int rows_per_block, const float* beta, float b0, const float* y, const float* wprior,
                             const float* offset, int link, int var, float tvp, float theta, const float* Wext,
                             const float* zext, int aug, int signed_w, double* out, double* dev_out,
-                            double* grad_out, int bf3, hipStream_t s) {
+                            double* grad_out, int bf3, int grad_f64, hipStream_t s) {
   if (N <= 0 || n_pairs <= 0) return 0;
   if (P % 32 != 0 || P > 512) return -1;
   // narrow row storage (ldx < P) only on the warp-specialised path
@@ -1008,7 +1031,7 @@ extern "C" int h2o_glm_irls(const float* X, long long N, int P, int ldx, const i
   if (rows_per_block % h2o_glm_irls_chunk(P) != 0) return -4;
   const int groups = (n_pairs + 4 * GI_PPW - 1) / (4 * GI_PPW);
   dim3 grid(n_splits, groups);
-  GlmFamArgs fam{link, var, tvp, theta, gi_dbg(), signed_w, bf3 < 0 ? gi_bf3() : bf3};
+  GlmFamArgs fam{link, var, tvp, theta, gi_dbg(), signed_w, bf3 < 0 ? gi_bf3() : bf3, grad_f64};
   const bool fused = beta != nullptr;
   // the exact-gradient channel rides the fused ws kernel (P <= 128, power of
   // two) only (grad_out: [n_splits][P + 1] doubles)
@@ -1200,7 +1223,7 @@ extern "C" int h2o_glm_wide_split(const float* X, int ldx, int P, int Pa, long l
                                   hipStream_t s) {
   if (rows <= 0) return 0;
   if (Pa % 4 != 0 || Pa < P + 2 || ldx < P || blocks <= 0) return -1;
-  GlmFamArgs fam{link, var, tvp, theta, 0, 0, 0};
+  GlmFamArgs fam{link, var, tvp, theta, 0, 0, 0, 0};
   if (Pa <= 256)
     hipLaunchKernelGGL(glm_wide_split_kernel<1>, dim3(blocks), dim3(256), 0, s, X, ldx, P, Pa, rows, beta, b0, y,
                        wprior, offset, fam, (__bf16*)HL, dev_out, grad_out);

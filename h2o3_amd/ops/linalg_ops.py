@@ -21,7 +21,7 @@ def _lib():
         lib.h2o_gram.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_int, ctypes.c_void_p,
                                  ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         P, I, LL, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong, ctypes.c_float
-        lib.h2o_glm_irls.argtypes = [P, LL, I, I, P, I, I, I, P, F, P, P, P, I, I, F, F, P, P, I, I, P, P, P, I, P]
+        lib.h2o_glm_irls.argtypes = [P, LL, I, I, P, I, I, I, P, F, P, P, P, I, I, F, F, P, P, I, I, P, P, P, I, I, P]
         lib.h2o_glm_irls_chunk.argtypes = [I]
         lib.h2o_gram_split.argtypes = [P, I, I, I, P, P, LL, P, P]
         lib.h2o_glm_wide_split.argtypes = [P, I, I, I, LL, P, F, P, P, P, I, I, F, F, P, P, I, P, P]
@@ -70,7 +70,7 @@ def _ptr(t):
 
 
 def glm_irls(X, aug=-1, beta=None, b0=0.0, y=None, wprior=None, offset=None, codes=(0, 0), tvp=0.0, theta=1e-10,
-             W=None, z=None, signed=None, target_blocks=1024, width=None, grad=False, bf3=None):
+             W=None, z=None, signed=None, target_blocks=1024, width=None, grad=False, bf3=None, grad_f64=True):
     """One pass of the fused IRLS kernel (ops/csrc/gram.hip glm_irls_kernel).
 
     Fused mode (beta given): per row eta = x.beta + b0 + offset, the family's
@@ -82,8 +82,9 @@ def glm_irls(X, aug=-1, beta=None, b0=0.0, y=None, wprior=None, offset=None, cod
     ldx % 4 == 0, columns ldx..Pp-1 implicitly zero; Pp = 128 ws path only).
     `grad=True` (fused mode, Pp in 32 / 64 / 128): also return the exact
     gradient channel g [Pp + 1] f64 = X'r, r = w (y - mu) dmu/deta / var
-    (exact f64 products of the f32 values, f64 sums; g[Pp] = sum r) as a
-    third element.
+    (exact f64 products of the f32 values, f64 sums -- or, grad_f64=False,
+    f32 products summed over a lane's rows of a chunk, f64 beyond; g[Pp] =
+    sum r) as a third element.
     `bf3`: override H2O3_GLM_BF3 for this call (False: f32 MFMA Gram).
     """
     N, ldx = X.shape
@@ -111,7 +112,7 @@ def glm_irls(X, aug=-1, beta=None, b0=0.0, y=None, wprior=None, offset=None, cod
     rc = lib.h2o_glm_irls(_ptr(X), N, P, ldx, _ptr(pairs_t), npairs, splits, rpb, _ptr(bt), float(b0),
                           _ptr(keep[0]), _ptr(keep[1]), _ptr(keep[2]), int(codes[0]), int(codes[1]), float(tvp),
                           float(theta), _ptr(keep[3]), _ptr(keep[4]), int(aug), int(bool(signed)), _ptr(out),
-                          _ptr(dev), _ptr(gout), -1 if bf3 is None else int(bool(bf3)),
+                          _ptr(dev), _ptr(gout), -1 if bf3 is None else int(bool(bf3)), int(bool(grad_f64)),
                           ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
     if rc != 0:
         raise RuntimeError(f"h2o_glm_irls failed: {rc}")

@@ -91,6 +91,6 @@ def test_host_spill_bytes_released_when_vec_dies():
     del vs[1]
     gc.collect()
     assert mm.host_bytes == nb
-    del vs
+    del vs, v
     gc.collect()
     assert mm.host_bytes == 0
