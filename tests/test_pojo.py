@@ -43,6 +43,10 @@ def _java_to_python(src):
         if m:
             py.append(f"{m.group(1)} = [{_expr(m.group(2))}]")
             continue
+        m = re.match(r"static final double\[\]\[\] (\w+) = new double\[\]\[\] \{(.*)\};", ln)
+        if m:
+            py.append(f"{m.group(1)} = [{_expr(m.group(2)).replace('{', '[').replace('}', ']')}]")
+            continue
         m = re.match(r"static double (tree_\d+)\(double\[\] data\) \{", ln)
         if m or ln.startswith("public final double[] score0"):
             name = m.group(1) if m else "score0"
@@ -187,3 +191,24 @@ def test_pojo_more_algos(data, algo):
     else:
         got = np.array([score0(list(r), [0.0, 0.0, 0.0])[2] for r in X])
         np.testing.assert_allclose(got, pred["yes"].values, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("family", ["multinomial", "ordinal"])
+def test_pojo_glm_multinomial_ordinal(data, family):
+    """Multinomial / ordinal GLM POJO (GLMModel.java:1827-1865): class
+    probabilities of the generated score0 equal the model's."""
+    df = data.copy()
+    df["k"] = np.where(df.a.fillna(0) < -0.4, "lo", np.where(df.a.fillna(0) > 0.5, "hi", "mid"))
+    fr = h2o.H2OFrame(df)
+    fr["k"] = fr["k"].asfactor()
+    m = H2OGeneralizedLinearEstimator(family=family, lambda_=0 if family == "multinomial" else 1e-4)
+    m.train(x=["a", "b", "c"], y="k", training_frame=fr)
+    src = to_java(m)
+    assert "extends GenModel" in src and src.count("{") == src.count("}")
+    score0 = _java_to_python(src)
+    doms = {c: d for c, d in m._dinfo.domains.items()}
+    X = _rows(df, ["a", "b", "c"], doms)
+    pred = m.predict(fr).as_data_frame()
+    lv = list(fr["k"]._vecs[0].domain) if hasattr(fr["k"], "_vecs") else ["hi", "lo", "mid"]
+    got = np.array([score0(list(x), [0.0] * 4)[1:] for x in X])
+    np.testing.assert_allclose(got, pred[lv].values, atol=1e-6)
