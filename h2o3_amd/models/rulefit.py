@@ -79,13 +79,20 @@ class H2ORuleFitEstimator(H2OEstimator):
         the path's conditions with conditions on one feature and operator
         merged (thresholds tightened, level sets intersected; NA matches only
         if every merged condition admits it), sorted by feature name, named
-        M<model>T<tree>N<node>.  Returns (model idx, tree idx, leaf id, text,
-        #conditions, varname, [(feature, op, threshold or level codes, NA)])."""
+        M<model>T<tree>N<node> -- plus _<class> for the per-class trees of a
+        multinomial ensemble (Rule.java:107-118, the tree number counting
+        iterations).  Returns (model idx, tree idx, leaf id, text,
+        #conditions, varname, [(feature, op, threshold or level codes, NA)],
+        forest position, class idx or None)."""
         out = []
+        sp = self._spec
+        classes = list(sp.response_domain) if sp.nclasses > 2 else None
         for mi, m in enumerate(self._trees):
             names = list(m._spec.x)
             doms = getattr(m, "_x_domains", {})
-            for ti, t in enumerate(m._forest.trees):
+            K = m._n_tree_classes() if classes else 1
+            for ft, t in enumerate(m._forest.trees):
+                ti, kc = (ft // K, int(m._forest.tclass[ft])) if classes else (ft, None)
                 left = np.asarray(t.left)
                 right = np.asarray(t.right)
                 par = {}
@@ -131,7 +138,8 @@ class H2ORuleFitEstimator(H2OEstimator):
                         else:
                             s_ = f"({f} {op} {v:.6g}"
                         parts.append(s_ + (f" or {f} is NA)" if na else ")"))
-                    out.append((mi, ti, leaf, " & ".join(parts), len(parts), f"M{mi}T{ti}N{leaf}", struct))
+                    vn = f"M{mi}T{ti}N{leaf}" + (f"_{classes[kc]}" if classes else "")
+                    out.append((mi, ti, leaf, " & ".join(parts), len(parts), vn, struct, ft, kc))
         return out
 
     def _rule_matrix(self, frame):
@@ -163,7 +171,7 @@ class H2ORuleFitEstimator(H2OEstimator):
                 base += nn
         rules = self._rules()
         col_of = {(mi, ti): b for mi, ti, b, _ in offsets}
-        idx = [col_of[(r[0], r[1])] + r[2] for r in rules]
+        idx = [col_of[(r[0], r[7])] + r[2] for r in rules]
         self._keep_cols = torch.as_tensor(idx, dtype=torch.long, device=cloud.device())
         R = self._rule_matrix(spec.frame)
         texts = [r[3] for r in rules]
@@ -215,7 +223,17 @@ class H2ORuleFitEstimator(H2OEstimator):
         coef = self._glm.coef() if spec.nclasses <= 2 else {}
         rows = []
         sup = R.to(torch.float64).mean(0).cpu().numpy() if R.shape[1] else np.zeros(0)
-        for i, nm in enumerate(self._rule_names):
+        if spec.nclasses > 2:
+            # multinomial: a rule's coefficient in the linear model of its own
+            # tree's class (RuleFitUtils.getRules strips the class suffix)
+            tabs = self._glm._output.get("coefficients_table_multinomials", {})
+            cls_of = {r[5]: r[8] for r in rules}
+            dom = list(spec.response_domain)
+            for i, nm in enumerate(self._rule_names):
+                c = float(tabs.get(dom[cls_of[nm]], {}).get(nm, 0.0))
+                if c != 0.0:
+                    rows.append((nm, c, float(sup[i]), texts[i]))
+        for i, nm in enumerate(self._rule_names if spec.nclasses <= 2 else []):
             c = coef.get(nm, 0.0)
             if c != 0.0:
                 rows.append((nm, c, float(sup[i]), texts[i]))

@@ -1440,32 +1440,44 @@ class H2OMojoModel:
         n = X.shape[0]
         lin = self.rf_linear
         test = []
+        rdom = self.domains[self.columns.index(self.response)] if self.response in self.columns else None
+        classes = list(rdom) if rdom is not None and len(rdom) > 2 else None
         if self.rf_type != 0:
             for i in range(self.rf_depth):
                 for j in range(self.rf_ntrees):
-                    name = f"M{i}T{j}"
-                    dom = lin.domains[lin.columns.index(name)]
-                    val = np.full(n, np.nan)
-                    for var, conds in self.rf_rules[(i, j)]:
-                        ok = np.ones(n, dtype=bool)
-                        for fi, typ, op, thr, nas in conds:
-                            col = X[:, fi]
-                            isna = np.isnan(col)
-                            if typ == 0:
-                                hit = np.isin(col, np.asarray(thr, dtype=np.float64))
-                            elif op == 0:
-                                hit = col < thr
-                            else:
-                                hit = col >= thr
-                            ok &= np.where(isna, nas, hit & ~isna)
-                        val = np.where(ok, float(dom.index(var)) if var in dom else np.nan, val)
-                    test.append(val)
+                    rules = self.rf_rules[(i, j)]
+                    for k in range(len(classes) if classes else 1):
+                        # multinomial (MojoRuleEnsemble.transformRow): the
+                        # rules of class k decode into column M<i>T<j>C<k>
+                        name = f"M{i}T{j}C{k}" if classes else f"M{i}T{j}"
+                        rs = [r for r in rules if r[0].endswith(classes[k])] if classes else rules
+                        test.append(self._rulefit_decode(X, rs, lin.domains[lin.columns.index(name)]))
         if self.rf_type != 2:
             test += [X[:, c] for c in range(X.shape[1]) if c < len(self.features)]
         Xl = np.full((n, len(lin.columns)), np.nan)
         for i, nm in enumerate(self.rf_linear_names):
             Xl[:, lin.columns.index(nm)] = test[i]
         return lin.score0(Xl)
+
+    @staticmethod
+    def _rulefit_decode(X, rules, dom):
+        """MojoRuleEnsemble.decode: the level of the last rule that holds."""
+        n = X.shape[0]
+        val = np.full(n, np.nan)
+        for var, conds in rules:
+            ok = np.ones(n, dtype=bool)
+            for fi, typ, op, thr, nas in conds:
+                col = X[:, fi]
+                isna = np.isnan(col)
+                if typ == 0:
+                    hit = np.isin(col, np.asarray(thr, dtype=np.float64))
+                elif op == 0:
+                    hit = col < thr
+                else:
+                    hit = col >= thr
+                ok &= np.where(isna, nas, hit & ~isna)
+            val = np.where(ok, float(dom.index(var)) if var in dom else np.nan, val)
+        return val
 
     def _score_stackedensemble(self, X):
         n = X.shape[0]

@@ -587,6 +587,8 @@ def _coxph(model, z):
 def _glm(model, z):
     di = model._dinfo
     if getattr(di, "ia_recipe", None):
+        # GLMModel.haveMojo() is false for models with interactions
+        # (GLMModel.java:1979): the reference exports none either
         raise NotImplementedError("reference-layout GLM MOJOs carry no interaction columns")
     spec = model._spec
     cats, nums = list(di.cat_cols), list(di.num_cols)
@@ -886,39 +888,49 @@ def _rulefit(model, z):
     per-(model, tree) lists of leaf rules with their conditions, and the
     linear model as a nested GLM MOJO whose rule columns are categoricals
     M<i>T<j> (level = the row's leaf rule, a never-matched first level keeps
-    every rule's beta explicit) next to the linear terms."""
+    every rule's beta explicit) next to the linear terms.  Multinomial:
+    one categorical M<i>T<j>C<k> per class tree, the rules of a (model,
+    tree) written class by class (RuleFitMojoWriter.java:64-100,
+    RuleEnsemble.createGLMTrainFrame) and a multinomial nested GLM whose
+    class-c block holds every column's class-c betas."""
     spec = model._spec
-    if spec.nclasses > 2:
-        raise NotImplementedError("reference-layout MOJO export of multinomial RuleFit models")
+    K = spec.nclasses
+    classes = list(spec.response_domain) if K > 2 else None
     x = list(spec.x)
     xd = {}
     for tm in model._trees:
         xd.update(getattr(tm, "_x_domains", None) or {})
     mt = {"LINEAR": 0, "RULES_AND_LINEAR": 1, "RULES": 2}[model._mtype]
     rules = model._rules()
-    coef = model._glm.coef()
-    icpt = float(coef.get("Intercept", 0.0))
+    if classes:
+        tabs = model._glm._output["coefficients_table_multinomials"]
+        coefs = [dict(tabs[c]) for c in classes]
+    else:
+        coefs = [model._glm.coef()]
     depth = len(model._trees)
-    ntrees = len(model._trees[0]._forest.trees) if model._trees else 0
+    ntrees = len(model._trees[0]._forest.trees) // (model._trees[0]._n_tree_classes() if classes else 1) \
+        if model._trees else 0
     extra = {"model_type": mt, "depth": depth, "ntrees": ntrees}
     groups = {}
     for r in rules:
-        groups.setdefault((r[0], r[1]), []).append(r)
+        groups.setdefault((r[0], r[1], r[8]), []).append(r)
     cat_cols, cat_doms, cat_betas = [], [], []
     for i in range(depth):
         for j in range(ntrees):
-            rs = groups.get((i, j), [])
-            extra[f"num_rules_M{i}T{j}"] = len(rs)
-            name = f"M{i}T{j}"
-            cat_cols.append(name)
-            cat_doms.append(["__no_rule__"] + [r[5] for r in rs])
-            cat_betas.append([0.0] + [float(coef.get(r[5], 0.0)) for r in rs])
-            for k, r in enumerate(rs):
+            rs_all = []
+            for k in (range(K) if classes else [None]):
+                rs = groups.get((i, j, k), [])
+                rs_all += rs
+                cat_cols.append(f"M{i}T{j}C{k}" if classes else f"M{i}T{j}")
+                cat_doms.append(["__no_rule__"] + [r[5] for r in rs])
+                cat_betas.append([[0.0] + [float(cf.get(r[5], 0.0)) for r in rs] for cf in coefs])
+            extra[f"num_rules_M{i}T{j}"] = len(rs_all)
+            for k, r in enumerate(rs_all):
                 rid = f"{i}_{j}_{k}"
                 extra[f"num_conditions_rule_id_{rid}"] = len(r[6])
                 extra[f"prediction_value_rule_id_{rid}"] = 0.0
                 extra[f"language_rule_rule_id_{rid}"] = r[3]
-                extra[f"coefficient_rule_id_{rid}"] = float(coef.get(r[5], 0.0))
+                extra[f"coefficient_rule_id_{rid}"] = float(coefs[r[8] or 0].get(r[5], 0.0))
                 extra[f"var_name_rule_id_{rid}"] = r[5]
                 for c, (f, op, v, na) in enumerate(r[6]):
                     cid = f"{c}_{rid}"
@@ -944,11 +956,13 @@ def _rulefit(model, z):
     lin_nums = [c for c in x if c not in xd and mt != 2]
     gcols_cat = (cat_cols if mt != 0 else []) + [f"linear.{c}" for c in lin_cats]
     gdoms = (cat_doms if mt != 0 else []) + [list(xd[c]) for c in lin_cats]
-    betas = list(cat_betas) if mt != 0 else []
-    for c in lin_cats:
-        betas.append([float(coef.get(f"linear.{c}.{lv}", 0.0)) for lv in xd[c]])
     gnums = [f"linear.{c}" for c in lin_nums]
-    beta = [b for bl in betas for b in bl] + [float(coef.get(n, 0.0)) for n in gnums] + [icpt]
+    beta = []
+    for ci, cf in enumerate(coefs):
+        bl = [cb[ci] for cb in cat_betas] if mt != 0 else []
+        bl += [[float(cf.get(f"linear.{c}.{lv}", 0.0)) for lv in xd[c]] for c in lin_cats]
+        beta += [b for blk in bl for b in blk] + [float(cf.get(n, 0.0)) for n in gnums] + \
+            [float(cf.get("Intercept", 0.0))]
     offs = [0]
     for d in gdoms:
         offs.append(offs[-1] + len(d))
@@ -956,13 +970,14 @@ def _rulefit(model, z):
     gdi = model._glm._dinfo
     plug = dict(zip(gdi.num_cols, gdi.plug))
     modes = [0] * (len(cat_cols) if mt != 0 else 0) + [int(gdi.cat_modes.get(f"linear.{c}", 0)) for c in lin_cats]
+    fam, link = ("multinomial", "multinomial") if classes else (model._glm._fam.family, model._glm._fam.link)
     gextra = {"use_all_factor_levels": True, "cats": len(gcols_cat), "cat_offsets": offs, "nums": len(gnums),
               "mean_imputation": True, "num_means": [float(plug.get(n, 0.0)) for n in gnums], "cat_modes": modes,
-              "beta": beta, "family": model._glm._fam.family, "link": model._glm._fam.link}
-    cat = "Binomial" if spec.nclasses == 2 else "Regression"
+              "beta": beta, "family": fam, "link": link}
+    cat = "Multinomial" if classes else "Binomial" if K == 2 else "Regression"
     resp_dom = [list(spec.response_domain) if spec.response_domain else None]
     gini, gfiles = _header(model._glm, "glm", "Generalized Linear Modeling", cat, gcols_cat + gnums + [spec.y],
-                           len(gcols_cat) + len(gnums), spec.nclasses, gdoms + [None] * len(gnums) + resp_dom,
+                           len(gcols_cat) + len(gnums), K, gdoms + [None] * len(gnums) + resp_dom,
                            GLM_MOJO_VERSION, gextra)
     sub = z.nested(f"models/glm/{key}/")
     sub.write("model.ini", gini)
@@ -979,7 +994,7 @@ def _rulefit(model, z):
         extra[f"linear_names_{i}"] = n
     columns = x + [spec.y]
     domains = [xd.get(c) for c in x] + resp_dom
-    ini, files = _header(model, "rulefit", "rulefit", cat, columns, len(x), spec.nclasses, domains, "1.00", extra)
+    ini, files = _header(model, "rulefit", "rulefit", cat, columns, len(x), K, domains, "1.00", extra)
     z.write("model.ini", ini)
     for k_, v_ in files.items():
         z.write(k_, v_)

@@ -64,3 +64,35 @@ def test_rulefit_reference_layout_mojo(tmp_path):
             d32[c] = d32[c].astype(np.float32).astype(np.float64)
         got = np.asarray(ref.predict_raw(d32))[:, -1]
         np.testing.assert_allclose(got, ours, rtol=1e-5, atol=1e-5)
+
+
+def test_rulefit_multinomial_reference_layout_mojo(tmp_path):
+    """Multinomial RuleFit: rules named M<i>T<j>N<node>_<class> (Rule.java:115),
+    one categorical M<i>T<j>C<k> per class tree in the nested multinomial GLM
+    (RuleEnsemble.createGLMTrainFrame); the reader's per-class decode
+    (MojoRuleEnsemble.transformRow) reproduces the in-memory probabilities."""
+    from h2o3_amd.mojo import h2o_mojo
+    h2o.init()
+    rng = np.random.default_rng(5)
+    n = 1500
+    X = rng.uniform(0, 1, size=(n, 3))
+    df = pd.DataFrame(X, columns=list("abc"))
+    df["g"] = rng.choice(["u", "v"], n)
+    df.loc[::31, "b"] = np.nan
+    lab = np.where(X[:, 0] > 0.6, "hi", np.where((X[:, 1] < 0.3) & (df["g"] == "u"), "mid", "lo"))
+    df["y"] = lab
+    fr = h2o.H2OFrame(df)
+    d32 = df.copy()
+    for c in "abc":
+        d32[c] = d32[c].astype(np.float32).astype(np.float64)
+    for mtype in ("RULES_AND_LINEAR", "RULES"):
+        m = H2ORuleFitEstimator(min_rule_length=1, max_rule_length=2, rule_generation_ntrees=4, seed=3,
+                                model_type=mtype, lambda_=1e-3)
+        m.train(x=["a", "b", "c", "g"], y="y", training_frame=fr)
+        assert all(any(nm.endswith("_" + k) for k in ("hi", "lo", "mid")) for nm in m._rule_names)
+        assert len(m.rule_importance()) > 0
+        ours = m.predict(fr).as_data_frame()
+        ref = h2o_mojo.load(m.download_mojo(str(tmp_path / f"rfm_{mtype}"), format="h2o"))
+        got = np.asarray(ref.predict_raw(d32))
+        np.testing.assert_allclose(got[:, -3:], ours[["hi", "lo", "mid"]].values, rtol=1e-5, atol=1e-5)
+        assert (ours["predict"] == ours["predict"].iloc[0]).mean() < 0.9
