@@ -633,12 +633,16 @@ class H2ODeepLearningEstimator(H2OEstimator):
         self._output["biases"] = bk
 
     def _train_step(self, xb, yb, wb, step_seed, hp, avg_act=None, seed_dev=None):
-        """One mini-batch step: forward, output gradient, backward through the
-        HIP bwd kernel + GEMMs, (all-reduce), per-row update kernels.  With
-        seed_dev the dropout seed is read from device memory (graph replays)."""
-        p = self._parms
+        """One mini-batch step.  On the GPU, networks the fused kernels cover
+        run dl_ops.mlp_step (three hand-written kernels, no library GEMM);
+        otherwise forward, output gradient, backward through the HIP bwd
+        kernel + GEMMs, per-row update kernels.  With seed_dev the dropout
+        seed is read from device memory (graph replays)."""
         K, ae, bs = hp["K"], hp["ae"], xb.shape[0]
-        W_ = cloud.world()
+        kind = self._fused_kind(hp, avg_act) if xb.device.type == "cuda" else None
+        if kind is not None:
+            self._fused_step(xb, None, yb, wb, step_seed, hp, kind, seed_dev, False)
+            return
         acts, zs = self._forward(xb, True, step_seed, seed_dev)
         dZ, _ = self._output_grad(zs[-1], yb, wb, 1.0 / bs, K, ae, xb)
         grads = []
@@ -662,21 +666,60 @@ class H2ODeepLearningEstimator(H2OEstimator):
         if avg_act is not None:
             for li in range(len(self._layers) - 1):
                 avg_act[li].mul_(0.999).add_(0.001 * acts[li + 1].mean(0))
+        for (li, dW, db) in grads:
+            L = self._layers[li]
+            dl_ops.update(L.W, dW.contiguous(), L.b, db.contiguous(), L.state, self._update_params(hp, li),
+                          avg_act=avg_act[li] if (avg_act is not None and li < len(avg_act)) else None)
+
+    def _update_params(self, hp, li):
+        """Per-layer update knobs at the current sample count: rate annealing
+        and decay per layer, the momentum ramp (Neurons.java rate / momentum)."""
+        p = self._parms
         m = hp["mom_start"]
         if hp["mom_ramp"] > 0:
             m = hp["mom_stable"] if self._processed >= hp["mom_ramp"] else \
                 hp["mom_start"] + (hp["mom_stable"] - hp["mom_start"]) * self._processed / hp["mom_ramp"]
-        for (li, dW, db) in grads:
-            L = self._layers[li]
-            r = hp["rate0"] / (1 + hp["anneal"] * self._processed) * hp["decay"] ** li
-            up = dl_ops.UpdateParams(ada=hp["ada"], rho=float(p["rho"]), eps=float(p["epsilon"]),
-                                     rate=r * (1 - m) if not hp["ada"] else 0.0, momentum=m,
-                                     nesterov=bool(p.get("nesterov_accelerated_gradient", True)),
-                                     has_momenta=hp["has_mom"], l1=hp["l1"], l2=hp["l2"], max_w2=hp["max_w2"],
-                                     sparsity_beta=hp["sparsity"],
-                                     average_activation=float(p.get("average_activation") or 0.0))
-            dl_ops.update(L.W, dW.contiguous(), L.b, db.contiguous(), L.state, up,
-                          avg_act=avg_act[li] if (avg_act is not None and li < len(avg_act)) else None)
+        r = hp["rate0"] / (1 + hp["anneal"] * self._processed) * hp["decay"] ** li
+        return dl_ops.UpdateParams(ada=hp["ada"], rho=float(p["rho"]), eps=float(p["epsilon"]),
+                                   rate=r * (1 - m) if not hp["ada"] else 0.0, momentum=m,
+                                   nesterov=bool(p.get("nesterov_accelerated_gradient", True)),
+                                   has_momenta=hp["has_mom"], l1=hp["l1"], l2=hp["l2"], max_w2=hp["max_w2"],
+                                   sparsity_beta=hp["sparsity"],
+                                   average_activation=float(p.get("average_activation") or 0.0))
+
+    def _fused_kind(self, hp, avg_act):
+        """Output kind of the fused HIP step (dl_ops.mlp_step: 0 softmax +
+        CrossEntropy, 1 softmax + Quadratic, 2 linear + Quadratic Gaussian),
+        or None for the networks it does not cover: maxout units,
+        autoencoders, other regression losses / distributions, sparsity and
+        elastic-averaging terms, layers beyond the LDS budget."""
+        import os
+        if os.environ.get("H2O3_DL_FUSED", "1") != "1" or avg_act is not None or hp.get("ea_reg", 0.0) > 0 \
+                or hp["ae"]:
+            return None
+        if any(L.act not in dl_ops._FUSED_ACTS or L.k != 1 for L in self._layers[:-1]) or self._layers[-1].k != 1:
+            return None
+        K = hp["K"]
+        loss = self._loss_name(K, False)
+        if K > 1:
+            kind = 1 if loss == "quadratic" else 0
+        else:
+            dist = getattr(self, "_dist", None)
+            if loss != "quadratic" or (dist is not None and dist.family != "gaussian"):
+                return None
+            kind = 2
+        widths = [self._layers[0].W.shape[1]] + [L.W.shape[0] for L in self._layers]
+        return kind if dl_ops.mlp_fits(widths) else None
+
+    def _fused_step(self, X, idx, Y, w, step_seed, hp, kind, seed_dev, advance):
+        p = self._parms
+        bs = int(idx.shape[0]) if idx is not None else int(X.shape[0])
+        if not hasattr(self, "_mlp_bufs"):
+            self._mlp_bufs = {}
+        dl_ops.mlp_step(X, idx, Y, w, self._layers, [L.act for L in self._layers[:-1]],
+                        [L.drop for L in self._layers[:-1]], float(p.get("input_dropout_ratio") or 0.0), kind,
+                        1.0 / bs, [self._update_params(hp, li) for li in range(len(self._layers))],
+                        seed=step_seed, seed_dev=seed_dev, advance=advance, bufs=self._mlp_bufs)
 
     def _graph_ok(self, X, hp, avg_act):
         """HIP-graph the step when nothing in it changes between steps on the
@@ -696,7 +739,14 @@ class H2ODeepLearningEstimator(H2OEstimator):
         gs = {"idx": torch.zeros(bs, dtype=torch.int64, device=dev),
               "seed": torch.tensor([self._seed() * 1000003 & ((1 << 62) - 1)], dtype=torch.int64, device=dev)}
 
+        kind = self._fused_kind(hp, avg_act)
+
         def body():
+            if kind is not None:
+                # the whole step in three kernels: gather + forward + backward,
+                # weight gradients, updates + seed advance
+                self._fused_step(X, gs["idx"], Y, w, 0, hp, kind, gs["seed"], True)
+                return
             xb = X.index_select(0, gs["idx"])
             yb = None if Y is None else Y.index_select(0, gs["idx"])
             wb = None if w is None else w.index_select(0, gs["idx"])

@@ -251,7 +251,7 @@ class TreeGrower:
         self.ridx2 = torch.empty(n, dtype=torch.int32, device=self.dev)
         # position-ordered copies of the two row channels, permuted with ridx
         # (off by default: the extra scattered writes in the partition cost more
-        # than the contiguous histogram reads save — see PERF.md)
+        # than the contiguous histogram reads save — A/B in profiles/README.md)
         self.use_payload = False
         self._pay = [torch.empty(n, dtype=torch.float32, device=self.dev) for _ in range(4)] \
             if self.use_payload else [None] * 4

@@ -1,5 +1,10 @@
-// Deep Learning (MLP) kernels: the fused element-wise / per-neuron parts of
-// a training step; the dense products run on the library GEMM (hipBLASLt).
+// Deep Learning (MLP) kernels.  The training step of a dense MLP runs as
+// three hand-written kernels (dl_mlp_*, f32 MFMA v_mfma_f32_16x16x4_f32 --
+// exact f32 products, the reference's float arithmetic); the element-wise
+// kernels below remain for the configurations the fused step does not take
+// (maxout, autoencoders, non-Gaussian regression losses, sparsity /
+// elastic-averaging terms) and for scoring, whose dense products use the
+// library GEMM.
 //
 // Reference: hex/deeplearning/Neurons.java — fprop (gemv + bias + activation
 // + Dropout.fillBytes unit masks, test-time activation scaling by
@@ -140,6 +145,71 @@ struct DLUpdate {
   float sparsity_beta, average_activation;  // autoencoder sparsity term on the bias
 };
 
+// Per-weight part of the reference's bprop: gradient + L1/L2, then ADADELTA
+// or momentum / Nesterov.  Returns the new weight; *g2 gets grad^2 (ADADELTA).
+__device__ __forceinline__ float dl_upd_weight(float wv, float gw, float* a2, float* m, const DLUpdate& p,
+                                               float* g2) {
+  const float grad = gw + (wv > 0.f ? p.l1 : (wv < 0.f ? -p.l1 : 0.f)) + wv * p.l2;
+  float nw;
+  *g2 = 0.f;
+  if (p.ada) {
+    const float gg = grad * grad;
+    *g2 = gg;
+    const float eg2 = p.rho * a2[1] + (1.f - p.rho) * gg;
+    const float rate = sqrtf((a2[0] + p.eps) / (eg2 + p.eps));
+    a2[1] = eg2;
+    a2[0] = p.rho * a2[0] + (1.f - p.rho) * rate * rate * gg;
+    nw = wv - rate * grad;
+  } else if (!p.nesterov) {
+    const float delta = -p.rate * grad;
+    nw = wv + delta;
+    if (p.has_momenta) {
+      nw += p.momentum * m[0];
+      m[0] = delta;
+    }
+  } else {
+    float tmp = -grad;
+    if (p.has_momenta) {
+      m[0] = m[0] * p.momentum + tmp;
+      tmp = m[0];
+    }
+    nw = wv + p.rate * tmp;
+  }
+  return nw;
+}
+
+// The bias update of a neuron row given the row's mean squared gradient.
+__device__ __forceinline__ void dl_upd_bias(float* bias, const float* dbias, float* ada_b, float* mom_b,
+                                            const float* avg_act, int row, float avg_g2, const DLUpdate& p) {
+  const float bv = bias[row];
+  const float pg = dbias[row] + (bv > 0.f ? p.l1 : (bv < 0.f ? -p.l1 : 0.f)) + bv * p.l2;
+  float rate = p.rate;
+  if (p.ada) {
+    float* ab = ada_b + 2 * row;
+    ab[1] = p.rho * ab[1] + (1.f - p.rho) * avg_g2;
+    rate = sqrtf((ab[0] + p.eps) / (ab[1] + p.eps));
+    ab[0] = p.rho * ab[0] + (1.f - p.rho) * rate * rate * avg_g2;
+  }
+  float nb;
+  if (!p.nesterov || p.ada) {
+    const float delta = -rate * pg;
+    nb = bv + delta;
+    if (p.has_momenta && !p.ada) {
+      nb += p.momentum * mom_b[row];
+      mom_b[row] = delta;
+    }
+  } else {
+    float d = -pg;
+    if (p.has_momenta) {
+      mom_b[row] = mom_b[row] * p.momentum + d;
+      d = mom_b[row];
+    }
+    nb = bv + rate * d;
+  }
+  if (avg_act && p.sparsity_beta > 0.f) nb -= rate * p.sparsity_beta * (avg_act[row] - p.average_activation);
+  bias[row] = nb;
+}
+
 // One workgroup per neuron row: W [U, I], dW [U, I] (mean gradient over the
 // mini-batch), ada [U, I, 2] = (E[dx^2], E[g^2]), mom [U, I], bias / dbias /
 // ada_b [U, 2] / mom_b [U]; avg_act [U] (sparsity, may be null).
@@ -155,36 +225,10 @@ __global__ __launch_bounds__(256) void dl_update_kernel(float* __restrict__ W, c
   const float* gw = dW + (long long)row * I;
   float g2sum = 0.f;
   for (int c = threadIdx.x; c < I; c += 256) {
-    const float wv = w[c];
-    const float grad = gw[c] + (wv > 0.f ? p.l1 : (wv < 0.f ? -p.l1 : 0.f)) + wv * p.l2;
-    float nw;
-    if (p.ada) {
-      float* a2 = ada + 2 * ((long long)row * I + c);
-      const float g2 = grad * grad;
-      g2sum += g2;
-      const float eg2 = p.rho * a2[1] + (1.f - p.rho) * g2;
-      const float rate = sqrtf((a2[0] + p.eps) / (eg2 + p.eps));
-      a2[1] = eg2;
-      a2[0] = p.rho * a2[0] + (1.f - p.rho) * rate * rate * g2;
-      nw = wv - rate * grad;
-    } else if (!p.nesterov) {
-      const float delta = -p.rate * grad;
-      nw = wv + delta;
-      if (p.has_momenta) {
-        float* m = mom + (long long)row * I + c;
-        nw += p.momentum * m[0];
-        m[0] = delta;
-      }
-    } else {
-      float tmp = -grad;
-      if (p.has_momenta) {
-        float* m = mom + (long long)row * I + c;
-        m[0] = m[0] * p.momentum + tmp;
-        tmp = m[0];
-      }
-      nw = wv + p.rate * tmp;
-    }
-    w[c] = nw;
+    float g2;
+    w[c] = dl_upd_weight(w[c], gw[c], ada + 2 * ((long long)row * I + c), mom ? mom + (long long)row * I + c : nullptr,
+                         p, &g2);
+    g2sum += g2;
   }
   __shared__ float red[256];
   float r2 = 0.f;
@@ -212,35 +256,7 @@ __global__ __launch_bounds__(256) void dl_update_kernel(float* __restrict__ W, c
     const float scale = sqrtf(p.max_w2 / rsum);
     for (int c = threadIdx.x; c < I; c += 256) w[c] *= scale;
   }
-  if (threadIdx.x == 0) {
-    const float bv = bias[row];
-    const float pg = dbias[row] + (bv > 0.f ? p.l1 : (bv < 0.f ? -p.l1 : 0.f)) + bv * p.l2;
-    float rate = p.rate;
-    if (p.ada) {
-      float* ab = ada_b + 2 * row;
-      ab[1] = p.rho * ab[1] + (1.f - p.rho) * avg_g2;
-      rate = sqrtf((ab[0] + p.eps) / (ab[1] + p.eps));
-      ab[0] = p.rho * ab[0] + (1.f - p.rho) * rate * rate * avg_g2;
-    }
-    float nb;
-    if (!p.nesterov || p.ada) {
-      const float delta = -rate * pg;
-      nb = bv + delta;
-      if (p.has_momenta && !p.ada) {
-        nb += p.momentum * mom_b[row];
-        mom_b[row] = delta;
-      }
-    } else {
-      float d = -pg;
-      if (p.has_momenta) {
-        mom_b[row] = mom_b[row] * p.momentum + d;
-        d = mom_b[row];
-      }
-      nb = bv + rate * d;
-    }
-    if (avg_act && p.sparsity_beta > 0.f) nb -= rate * p.sparsity_beta * (avg_act[row] - p.average_activation);
-    bias[row] = nb;
-  }
+  if (threadIdx.x == 0) dl_upd_bias(bias, dbias, ada_b, mom_b, avg_act, row, avg_g2, p);
 }
 
 // Softmax output: Z [B, K] (+ bias in place) -> P [B, K]; with labels y
@@ -278,6 +294,375 @@ __global__ __launch_bounds__(256) void dl_softmax_kernel(float* __restrict__ Z, 
     }
     if (loss_out && j == t) loss_out[row] = -wr * __logf(fmaxf(p, 1e-30f));
   }
+}
+
+// ---------------------------------------------------------------------------
+// Fused MLP training step (dense layers, tanh / rectifier / exprectifier /
+// linear units with hashed dropout, softmax or Gaussian linear output).
+//
+//   dl_mlp_fb_kernel   one workgroup per 16 batch rows: gathers the rows
+//                      (idx), input dropout, every layer's forward on f32
+//                      MFMA with bias + activation + dropout fused into the
+//                      epilogue, the output gradient, then the backward
+//                      dA = dZ W (MFMA) with act' and the dropout mask fused.
+//                      Activations and gradients stay in LDS between layers;
+//                      the ones the weight gradient needs (A_l, dZ_l) are
+//                      also written to HBM.
+//   dl_mlp_dw_kernel   one workgroup per 16x16 tile of a dW_l = dZ_l^T A_l:
+//                      4 waves split the batch rows, fold through LDS; the
+//                      tiles of the first column also write db_l = sum dZ_l.
+//   dl_mlp_upd_kernel  one wave per neuron row of every layer: the reference
+//                      per-row bprop tail (dl_upd_weight / dl_upd_bias, the
+//                      max_w2 rescale) and the step-seed advance.
+//
+// MFMA: v_mfma_f32_16x16x4_f32, lane l supplies A[l & 15][k = l >> 4] and
+// B[k = l >> 4][l & 15], C[4 (l >> 4) + r][l & 15] in acc[r].  Each lane's
+// k for a step s is k0 + 4 (l >> 4) + s, so one float4 LDS read feeds four
+// MFMAs.  The f32 products are exact, as in the reference's float loops.
+// ---------------------------------------------------------------------------
+#define DL_MAXL 8
+#define DL_ROWS 16
+typedef float dl_f32x4 __attribute__((ext_vector_type(4)));
+
+struct DLNet {
+  int nl, B, K, out_kind;        // out_kind: 0 softmax + CE, 1 softmax + quadratic, 2 linear + quadratic
+  int ldx;
+  float inv_n;
+  int width[DL_MAXL + 1];        // width[0] = inputs, width[l + 1] = units of layer l
+  int act[DL_MAXL];              // activation of the hidden layer l (its output is A_{l+1})
+  unsigned thr[DL_MAXL + 1];     // dropout thresholds: [0] input, [l] of A_l
+  int lds_a[DL_MAXL + 1];        // LDS offsets (floats) of A_l (l < nl) and of the logits (l = nl)
+  int stride[DL_MAXL + 1];       // their row strides
+  int lds_d0, lds_d1, ldsw;      // dZ ping-pong buffers and their row stride
+  const float* W[DL_MAXL];       // [width[l+1], width[l]]
+  const float* b[DL_MAXL];
+  float* A[DL_MAXL];             // [B, width[l]] (A_0 = the input after dropout)
+  float* dZ[DL_MAXL];            // [B, width[l+1]]
+};
+
+__device__ __forceinline__ dl_f32x4 dl_mfma4(float4 a, float4 b, dl_f32x4 c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b.y, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b.z, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b.w, c, 0, 0, 0);
+  return c;
+}
+
+__device__ __forceinline__ unsigned long long dl_lcg(unsigned long long s) {
+  return s * 6364136223846793005ull + 1442695040888963407ull;
+}
+
+__global__ __launch_bounds__(256) void dl_mlp_fb_kernel(const DLNet net, const float* __restrict__ X,
+                                                        const long long* __restrict__ idx,
+                                                        const long long* __restrict__ ycls,
+                                                        const float* __restrict__ yreg,
+                                                        const float* __restrict__ wts, unsigned long long seed,
+                                                        const unsigned long long* seed_dev, int advance) {
+  extern __shared__ float lds[];
+  if (seed_dev) seed += advance ? dl_lcg(*seed_dev) : *seed_dev;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g4 = 4 * (lane >> 4), c16 = lane & 15;
+  const int r0 = blockIdx.x * DL_ROWS;
+  const int B = net.B;
+  // ---- input rows (gathered) with input dropout -> LDS A_0 and HBM A_0
+  {
+    const int P = net.width[0], S = net.stride[0];
+    float* a0 = lds + net.lds_a[0];
+    for (int e = tid; e < DL_ROWS * S; e += 256) {
+      const int r = e / S, c = e - r * S;
+      const int rg = r0 + r;
+      float v = 0.f;
+      if (rg < B && c < P) {
+        const long long src = idx ? idx[rg] : (long long)rg;
+        v = X[src * net.ldx + c];
+        if (!dl_keep(seed + 0x5bd1e995ull, (unsigned)rg, (unsigned)c, net.thr[0])) v = 0.f;
+        net.A[0][(long long)rg * P + c] = v;
+      }
+      a0[e] = v;
+    }
+  }
+  __syncthreads();
+  // ---- forward
+  for (int l = 0; l < net.nl; ++l) {
+    const int I = net.width[l], U = net.width[l + 1];
+    const int Si = net.stride[l], So = net.stride[l + 1];
+    const float* ain = lds + net.lds_a[l];
+    float* aout = lds + net.lds_a[l + 1];
+    const bool last = l == net.nl - 1;
+    const int NT = (U + 15) >> 4, KP = (I + 15) & ~15;
+    const float* __restrict__ W = net.W[l];
+    const bool vec = (I & 3) == 0;
+    const int act = last ? 0 : net.act[l];
+    const unsigned thr = last ? 0u : net.thr[l + 1];
+    const unsigned long long lseed = seed + 7919ull * (unsigned long long)(l + 1);
+    for (int t0 = wave; t0 < NT; t0 += 16) {
+      dl_f32x4 acc[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] = (dl_f32x4){0.f, 0.f, 0.f, 0.f};
+      for (int k0 = 0; k0 < KP; k0 += 16) {
+        const int kk = k0 + g4;
+        const float4 a = *reinterpret_cast<const float4*>(ain + c16 * Si + kk);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int t = t0 + 4 * j;
+          if (t < NT) {
+            const int u = t * 16 + c16;
+            float4 w = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (u < U) {
+              const float* wr = W + (long long)u * I + kk;
+              if (vec && kk + 3 < I) {
+                w = *reinterpret_cast<const float4*>(wr);
+              } else {
+                w.x = kk < I ? wr[0] : 0.f;
+                w.y = kk + 1 < I ? wr[1] : 0.f;
+                w.z = kk + 2 < I ? wr[2] : 0.f;
+                w.w = kk + 3 < I ? wr[3] : 0.f;
+              }
+            }
+            acc[j] = dl_mfma4(a, w, acc[j]);
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int t = t0 + 4 * j;
+        if (t < NT) {
+          const int u = t * 16 + c16;
+          const float bu = u < U ? net.b[l][u] : 0.f;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = g4 + r, rg = r0 + row;
+            const float z = acc[j][r] + bu;
+            if (last) {
+              aout[row * So + u] = u < U ? z : 0.f;
+            } else {
+              float a = u < U ? dl_act(act, z) : 0.f;
+              if (!dl_keep(lseed, (unsigned)rg, (unsigned)u, thr)) a = 0.f;
+              aout[row * So + u] = a;
+              if (rg < B && u < U) net.A[l + 1][(long long)rg * U + u] = a;
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // ---- output gradient dE/dnet (already * w / n), rows in threads 0..15
+  float* dcur = lds + net.lds_d0;
+  float* dnext = lds + net.lds_d1;
+  {
+    const int K = net.K, So = net.stride[net.nl], Kp = (K + 15) & ~15;
+    const float* zo = lds + net.lds_a[net.nl];
+    if (tid < DL_ROWS) {
+      const int row = tid, rg = r0 + row;
+      float wr = 0.f;
+      long long t = -1;
+      float yv = 0.f;
+      if (rg < B) {
+        const long long src = idx ? idx[rg] : (long long)rg;
+        wr = wts ? wts[src] : 1.f;
+        if (net.out_kind < 2) {
+          t = ycls[src];
+          if (t < 0) wr = 0.f;
+        } else {
+          yv = yreg[src];
+        }
+      }
+      float* dz = dcur + row * net.ldsw;
+      float* gdz = net.dZ[net.nl - 1] + (long long)rg * K;
+      if (net.out_kind < 2) {
+        float mx = -INFINITY;
+        for (int k = 0; k < K; ++k) mx = fmaxf(mx, zo[row * So + k]);
+        float s = 0.f;
+        for (int k = 0; k < K; ++k) s += __expf(zo[row * So + k] - mx);
+        const float inv = 1.f / s;
+        for (int k = 0; k < K; ++k) {
+          const float p = __expf(zo[row * So + k] - mx) * inv;
+          const float tt = (k == t) ? 1.f : 0.f;
+          const float gk = (net.out_kind == 0 ? (p - tt) : (p - tt) * (1.f - p) * p) * wr * net.inv_n;
+          dz[k] = gk;
+          if (rg < B) gdz[k] = gk;
+        }
+      } else {
+        const float gk = 2.f * (zo[row * So] - yv) * wr * net.inv_n;
+        dz[0] = gk;
+        if (rg < B) gdz[0] = gk;
+      }
+      for (int k = K; k < Kp; ++k) dz[k] = 0.f;
+    }
+  }
+  __syncthreads();
+  // ---- backward: dA_l = dZ_l W_l, dZ_{l-1} = dA_l act'(A_l) mask_l
+  for (int l = net.nl - 1; l >= 1; --l) {
+    const int U = net.width[l + 1], I = net.width[l];
+    const int NT = (I + 15) >> 4, KP = (U + 15) & ~15;
+    const float* __restrict__ W = net.W[l];
+    const float* al = lds + net.lds_a[l];
+    const int Sa = net.stride[l];
+    const int act = net.act[l - 1];
+    const unsigned thr = net.thr[l];
+    const unsigned long long lseed = seed + 7919ull * (unsigned long long)l;
+    for (int t0 = wave; t0 < NT; t0 += 16) {
+      dl_f32x4 acc[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] = (dl_f32x4){0.f, 0.f, 0.f, 0.f};
+      for (int k0 = 0; k0 < KP; k0 += 16) {
+        const int kk = k0 + g4;
+        const float4 d = *reinterpret_cast<const float4*>(dcur + c16 * net.ldsw + kk);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int t = t0 + 4 * j;
+          if (t < NT) {
+            const int i = t * 16 + c16;
+            float4 w = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (i < I) {
+              const float* wc = W + (long long)kk * I + i;
+              w.x = kk < U ? wc[0] : 0.f;
+              w.y = kk + 1 < U ? wc[I] : 0.f;
+              w.z = kk + 2 < U ? wc[2 * I] : 0.f;
+              w.w = kk + 3 < U ? wc[3 * I] : 0.f;
+            }
+            acc[j] = dl_mfma4(d, w, acc[j]);
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int t = t0 + 4 * j;
+        if (t < NT) {
+          const int i = t * 16 + c16;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = g4 + r, rg = r0 + row;
+            float g = 0.f;
+            if (i < I && dl_keep(lseed, (unsigned)rg, (unsigned)i, thr)) g = acc[j][r] * dl_dact(act, al[row * Sa + i]);
+            dnext[row * net.ldsw + i] = g;
+            if (rg < B && i < I) net.dZ[l - 1][(long long)rg * I + i] = g;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    float* tmp = dcur;
+    dcur = dnext;
+    dnext = tmp;
+  }
+}
+
+struct DLGrad {
+  int nl, B;
+  int width[DL_MAXL + 1];
+  int tiles_i[DL_MAXL];
+  int tile_start[DL_MAXL + 1];
+  const float* A[DL_MAXL];
+  const float* dZ[DL_MAXL];
+  float* dW[DL_MAXL];
+  float* db[DL_MAXL];
+};
+
+__global__ __launch_bounds__(256) void dl_mlp_dw_kernel(const DLGrad g) {
+  __shared__ float red[4][16][17];
+  __shared__ float dbr[4][16];
+  const int bid = blockIdx.x;
+  int l = 0;
+  while (l + 1 < g.nl && bid >= g.tile_start[l + 1]) ++l;
+  const int local = bid - g.tile_start[l];
+  const int ut = local / g.tiles_i[l], it = local - ut * g.tiles_i[l];
+  const int U = g.width[l + 1], I = g.width[l], B = g.B;
+  const float* __restrict__ dz = g.dZ[l];
+  const float* __restrict__ a = g.A[l];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g4 = 4 * (lane >> 4), c16 = lane & 15;
+  const int u = ut * 16 + c16, i = it * 16 + c16;
+  const bool uok = u < U, iok = i < I, want_db = it == 0;
+  dl_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  float dbs = 0.f;
+  // wave w takes rows [16 q, 16 q + 16) for q = w, w + 4, ...; two row
+  // chunks per trip so eight loads are in flight before the MFMAs
+  for (int r16 = wave * 16; r16 < B; r16 += 128) {
+    float4 x[2], y[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int rr = r16 + 64 * h + g4;
+      x[h].x = (rr < B && uok) ? dz[(long long)rr * U + u] : 0.f;
+      x[h].y = (rr + 1 < B && uok) ? dz[(long long)(rr + 1) * U + u] : 0.f;
+      x[h].z = (rr + 2 < B && uok) ? dz[(long long)(rr + 2) * U + u] : 0.f;
+      x[h].w = (rr + 3 < B && uok) ? dz[(long long)(rr + 3) * U + u] : 0.f;
+      y[h].x = (rr < B && iok) ? a[(long long)rr * I + i] : 0.f;
+      y[h].y = (rr + 1 < B && iok) ? a[(long long)(rr + 1) * I + i] : 0.f;
+      y[h].z = (rr + 2 < B && iok) ? a[(long long)(rr + 2) * I + i] : 0.f;
+      y[h].w = (rr + 3 < B && iok) ? a[(long long)(rr + 3) * I + i] : 0.f;
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      acc = dl_mfma4(x[h], y[h], acc);
+      if (want_db) dbs += (x[h].x + x[h].y) + (x[h].z + x[h].w);
+    }
+  }
+  // C[m = u][n = i]: this lane holds u = ut*16 + g4 + r, i = it*16 + c16
+#pragma unroll
+  for (int r = 0; r < 4; ++r) red[wave][g4 + r][c16] = acc[r];
+  if (want_db) {
+    dbs += __shfl_xor(dbs, 16, 64);
+    dbs += __shfl_xor(dbs, 32, 64);
+    if (lane < 16) dbr[wave][lane] = dbs;
+  }
+  __syncthreads();
+  const int t = threadIdx.x, m = t >> 4, n = t & 15;
+  const int uu = ut * 16 + m, ii = it * 16 + n;
+  if (uu < U && ii < I)
+    g.dW[l][(long long)uu * I + ii] = (red[0][m][n] + red[1][m][n]) + (red[2][m][n] + red[3][m][n]);
+  if (want_db && t < 16 && ut * 16 + t < U)
+    g.db[l][ut * 16 + t] = (dbr[0][t] + dbr[1][t]) + (dbr[2][t] + dbr[3][t]);
+}
+
+struct DLUpdMulti {
+  int nl;
+  int width[DL_MAXL + 1];
+  int row_start[DL_MAXL + 1];
+  float* W[DL_MAXL];
+  const float* dW[DL_MAXL];
+  float* ada[DL_MAXL];
+  float* mom[DL_MAXL];
+  float* bias[DL_MAXL];
+  const float* db[DL_MAXL];
+  float* ada_b[DL_MAXL];
+  float* mom_b[DL_MAXL];
+  DLUpdate p[DL_MAXL];
+};
+
+__global__ __launch_bounds__(256) void dl_mlp_upd_kernel(const DLUpdMulti q, unsigned long long* seed_dev,
+                                                         int advance) {
+  const int lane = threadIdx.x & 63;
+  const int grow = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (advance && seed_dev && grow == 0 && lane == 0) seed_dev[0] = dl_lcg(seed_dev[0]);
+  if (grow >= q.row_start[q.nl]) return;
+  int l = 0;
+  while (l + 1 < q.nl && grow >= q.row_start[l + 1]) ++l;
+  const int row = grow - q.row_start[l], I = q.width[l];
+  const DLUpdate& p = q.p[l];
+  float* w = q.W[l] + (long long)row * I;
+  const float* gw = q.dW[l] + (long long)row * I;
+  float* ada = q.ada[l];
+  float* mom = q.mom[l];
+  float g2sum = 0.f, r2 = 0.f;
+  for (int c = lane; c < I; c += 64) {
+    float g2;
+    const float nw = dl_upd_weight(w[c], gw[c], ada + 2 * ((long long)row * I + c),
+                                   mom ? mom + (long long)row * I + c : nullptr, p, &g2);
+    w[c] = nw;
+    g2sum += g2;
+    r2 += nw * nw;
+  }
+  g2sum = wave_sum(g2sum);
+  if (p.max_w2 < 3.0e38f) {
+    r2 = wave_sum(r2);
+    if (r2 > p.max_w2) {
+      const float scale = sqrtf(p.max_w2 / r2);
+      for (int c = lane; c < I; c += 64) w[c] *= scale;
+    }
+  }
+  if (lane == 0) dl_upd_bias(q.bias[l], q.db[l], q.ada_b[l], q.mom_b[l], nullptr, row, g2sum / (float)max(I, 1), p);
 }
 
 extern "C" {
@@ -340,4 +725,99 @@ int h2o_dl_softmax(float* Z, const float* bias, float* P, const long long* y, co
   H2O_CHECK_LAUNCH();
 }
 
+// Fused training step of a dense MLP (dl_mlp_* kernels).  Arrays are per
+// layer (nl = hidden layers + output): width[nl + 1], act[nl - 1],
+// drop[nl] ([0] input dropout, [l] of hidden layer l-1's output), W/b/A/dZ/
+// dW/db/ada/mom/ada_b/mom_b[nl], ups[nl].  X [n, ldx] with idx [B] (int64,
+// null = rows 0..B-1); ycls (int64, classification) or yreg (float);
+// wts per row (may be null).  Returns -2 when the network does not fit the
+// fused kernels (the caller runs the unfused step).
+int h2o_dl_mlp_step(int nl, const int* width, const int* act, const float* drop, const float* const* W,
+                    const float* const* b, float* const* A, float* const* dZ, float* const* dW, float* const* db,
+                    float* const* ada, float* const* mom, float* const* ada_b, float* const* mom_b,
+                    const DLUpdate* ups, const float* X, int ldx, const long long* idx, const long long* ycls,
+                    const float* yreg, const float* wts, int B, int out_kind, float inv_n, unsigned long long seed,
+                    unsigned long long* seed_dev, int advance, hipStream_t s) {
+  if (nl < 1 || nl > DL_MAXL || B <= 0) return -2;
+  DLNet net{};
+  net.nl = nl;
+  net.B = B;
+  net.K = width[nl];
+  net.out_kind = out_kind;
+  net.ldx = ldx;
+  net.inv_n = inv_n;
+  int off = 0, maxw = 0;
+  for (int l = 0; l <= nl; ++l) {
+    net.width[l] = width[l];
+    const int pw = (width[l] + 15) & ~15;
+    net.lds_a[l] = off;
+    net.stride[l] = pw + 4;
+    off += DL_ROWS * (pw + 4);
+    if (l >= 1) maxw = std::max(maxw, pw);
+    if (l < nl) net.thr[l] = drop[l] <= 0.f ? 0u : (unsigned)fminf(drop[l] * 4294967296.f, 4294967295.f);
+  }
+  if (out_kind == 2 && width[nl] != 1) return -2;
+  if (width[nl] > 64) return -2;
+  net.ldsw = maxw + 4;
+  net.lds_d0 = off;
+  off += DL_ROWS * net.ldsw;
+  net.lds_d1 = off;
+  off += DL_ROWS * net.ldsw;
+  const size_t lds_bytes = (size_t)off * sizeof(float);
+  if (lds_bytes > 160 * 1024) return -2;
+  for (int l = 0; l < nl; ++l) {
+    if (l < nl - 1) net.act[l] = act[l];
+    net.W[l] = W[l];
+    net.b[l] = b[l];
+    net.A[l] = A[l];
+    net.dZ[l] = dZ[l];
+  }
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)dl_mlp_fb_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(dl_mlp_fb_kernel, dim3((B + DL_ROWS - 1) / DL_ROWS), dim3(256), lds_bytes, s, net, X, idx, ycls,
+                     yreg, wts, seed, seed_dev, advance);
+  DLGrad g{};
+  g.nl = nl;
+  g.B = B;
+  int nt = 0;
+  for (int l = 0; l < nl; ++l) {
+    g.width[l] = width[l];
+    g.tiles_i[l] = (width[l] + 15) >> 4;
+    g.tile_start[l] = nt;
+    nt += g.tiles_i[l] * ((width[l + 1] + 15) >> 4);
+    g.A[l] = A[l];
+    g.dZ[l] = dZ[l];
+    g.dW[l] = dW[l];
+    g.db[l] = db[l];
+  }
+  g.width[nl] = width[nl];
+  g.tile_start[nl] = nt;
+  hipLaunchKernelGGL(dl_mlp_dw_kernel, dim3(nt), dim3(256), 0, s, g);
+  DLUpdMulti q{};
+  q.nl = nl;
+  int nr = 0;
+  for (int l = 0; l < nl; ++l) {
+    q.width[l] = width[l];
+    q.row_start[l] = nr;
+    nr += width[l + 1];
+    q.W[l] = const_cast<float*>(W[l]);
+    q.dW[l] = dW[l];
+    q.ada[l] = ada[l];
+    q.mom[l] = mom[l];
+    q.bias[l] = const_cast<float*>(b[l]);
+    q.db[l] = db[l];
+    q.ada_b[l] = ada_b[l];
+    q.mom_b[l] = mom_b[l];
+    q.p[l] = ups[l];
+  }
+  q.width[nl] = width[nl];
+  q.row_start[nl] = nr;
+  hipLaunchKernelGGL(dl_mlp_upd_kernel, dim3((nr + 3) / 4), dim3(256), 0, s, q, seed_dev, advance);
+  H2O_CHECK_LAUNCH();
+}
+
 }  // extern "C"
+

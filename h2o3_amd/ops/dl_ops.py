@@ -8,6 +8,9 @@ update:  per neuron row: grad + L1/L2, ADADELTA or momentum / Nesterov,
          max_w2 rescale, bias update — Neurons.bprop / update_bias;
 softmax: probabilities + CrossEntropy / Quadratic output gradient —
          Neurons.Softmax.setOutputLayerGradient.
+mlp_step: the whole training step of a dense MLP in three hand-written
+         kernels (f32 MFMA forward + backward per 16-row tile, dW tiles,
+         per-row updates of every layer) — no library GEMM.
 """
 from __future__ import annotations
 
@@ -29,6 +32,8 @@ def _lib():
         lib.h2o_dl_seed_advance.argtypes = [_cv, _cv]
         lib.h2o_dl_update.argtypes = [_cv] * 9 + [_ci, _ci] + [_cf] * 7 + [_ci] * 3 + [_cf, _cf, _cv]
         lib.h2o_dl_softmax.argtypes = [_cv] * 7 + [_ci, _ci, _cf, _ci, _cv]
+        lib.h2o_dl_mlp_step.argtypes = [_ci] + [_cv] * 15 + [_ci] + [_cv] * 4 + [_ci, _ci, _cf, _cull, _cv, _ci,
+                                                                            _cv]
         lib._typed = True
     return lib
 
@@ -257,3 +262,83 @@ def softmax(Z, bias, y=None, w=None, inv_n=1.0, loss="crossentropy", want_grad=T
     py = P.gather(1, yl.clamp_min(0).view(-1, 1)).view(-1)
     lo = -wr * torch.log(py.clamp_min(1e-30))
     return P, dZ, lo
+
+
+# ---------------------------------------------------------------- fused step
+class _DLUpdate(ctypes.Structure):
+    _fields_ = [("rho", _cf), ("eps", _cf), ("rate", _cf), ("momentum", _cf), ("l1", _cf), ("l2", _cf),
+                ("max_w2", _cf), ("ada", _ci), ("nesterov", _ci), ("has_momenta", _ci),
+                ("sparsity_beta", _cf), ("average_activation", _cf)]
+
+
+MLP_MAX_LAYERS = 8
+_FUSED_ACTS = ("tanh", "rectifier", "exprectifier", "linear")
+
+
+def mlp_fits(widths) -> bool:
+    """The fused step keeps one 16-row tile of every layer's input plus two
+    gradient buffers in LDS (160 KB per workgroup); <= 8 layers, <= 64
+    outputs."""
+    nl = len(widths) - 1
+    if nl < 1 or nl > MLP_MAX_LAYERS or widths[-1] > 64:
+        return False
+    pad = [((w + 15) // 16) * 16 + 4 for w in widths]
+    floats = 16 * sum(pad) + 2 * 16 * (max(pad[1:]))
+    return floats * 4 <= 160 * 1024
+
+
+def _ensure_state(W, state, has_momenta):
+    U, I = W.shape
+    if "ada" not in state:
+        state["ada"] = torch.zeros((U, I, 2), dtype=torch.float32, device=W.device)
+        state["ada_b"] = torch.zeros((U, 2), dtype=torch.float32, device=W.device)
+        state["mom"] = torch.zeros((U, I), dtype=torch.float32, device=W.device) if has_momenta else None
+        state["mom_b"] = torch.zeros(U, dtype=torch.float32, device=W.device) if has_momenta else None
+
+
+def mlp_step(X, idx, y, w, layers, acts, drops, in_drop, out_kind, inv_n, ups, seed=0, seed_dev=None,
+             advance=False, bufs=None):
+    """One fused training step (dl.hip dl_mlp_*).  X [n, P] f32 (rows idx
+    [B] int64, or the first B = len(X) rows when idx is None); y int64 labels
+    (out_kind 0 CrossEntropy / 1 Quadratic softmax) or f32 [n(,1)] targets
+    (out_kind 2, linear output + quadratic loss); w row weights or None.
+    layers: objects with W [U, I], b [U], state; acts / drops per hidden
+    layer; ups: UpdateParams per layer.  Weights, biases and ADADELTA /
+    momentum state are updated in place.  bufs: optional dict reused across
+    calls for the A / dZ / dW / db scratch.  seed_dev + advance: the device
+    step seed is advanced (LCG) and the new value used, as seed_advance()
+    followed by the unfused step."""
+    lib = _lib()
+    nl = len(layers)
+    B = int(idx.shape[0]) if idx is not None else int(X.shape[0])
+    widths = [int(layers[0].W.shape[1])] + [int(L.W.shape[0]) for L in layers]
+    dev = X.device
+    bufs = {} if bufs is None else bufs
+    key = (B, tuple(widths))
+    if bufs.get("key") != key:
+        bufs.clear()
+        bufs["key"] = key
+        bufs["A"] = [torch.empty((B, widths[l]), dtype=torch.float32, device=dev) for l in range(nl)]
+        bufs["dZ"] = [torch.empty((B, widths[l + 1]), dtype=torch.float32, device=dev) for l in range(nl)]
+        bufs["dW"] = [torch.empty_like(L.W) for L in layers]
+        bufs["db"] = [torch.empty_like(L.b) for L in layers]
+    for L, up in zip(layers, ups):
+        _ensure_state(L.W, L.state, up.has_momenta)
+    arr = lambda ts: (_cv * nl)(*[0 if t is None else t.data_ptr() for t in ts])
+    wid = (_ci * (nl + 1))(*widths)
+    actc = (_ci * max(1, nl - 1))(*([ACT[a] for a in acts] or [0]))
+    dropc = (_cf * nl)(*([float(in_drop)] + [float(d) for d in drops]))
+    upc = (_DLUpdate * nl)(*[_DLUpdate(up.rho, up.eps, up.rate, up.momentum, up.l1, up.l2,
+                                       float(up.max_w2) if up.max_w2 is not None and up.max_w2 < 3.0e38 else 3.4e38,
+                                       int(up.ada), int(up.nesterov), int(up.has_momenta), up.sparsity_beta,
+                                       up.average_activation) for up in ups])
+    Xc = X if X.is_contiguous() else X.contiguous()
+    ycls = y if out_kind < 2 else None
+    yreg = y.reshape(-1) if out_kind == 2 else None
+    rc = lib.h2o_dl_mlp_step(nl, wid, actc, dropc, arr([L.W for L in layers]), arr([L.b for L in layers]),
+                             arr(bufs["A"]), arr(bufs["dZ"]), arr(bufs["dW"]), arr(bufs["db"]),
+                             arr([L.state["ada"] for L in layers]), arr([L.state["mom"] for L in layers]),
+                             arr([L.state["ada_b"] for L in layers]), arr([L.state["mom_b"] for L in layers]),
+                             upc, _p(Xc), int(Xc.shape[1]), _p(idx), _p(ycls), _p(yreg), _p(w), B, int(out_kind),
+                             float(inv_n), seed & _M, _p(seed_dev), int(bool(advance)), _s())
+    _check(rc, "h2o_dl_mlp_step")

@@ -380,3 +380,90 @@ def test_score_validation_samples():
     # same training, the history's validation numbers come from a 200-row sample
     assert h1["training_logloss"] == h2["training_logloss"]
     assert h1["validation_logloss"] != h2["validation_logloss"]
+
+
+def _fused_vs_unfused(mk, P, K, B, Y, w, hp, steps=3, graph=False):
+    """Train two copies of the same network for `steps` mini-batches, one
+    through the fused HIP step and one through the unfused path (library
+    GEMMs + element-wise kernels); returns the two layer lists."""
+    import os
+    g = torch.Generator(device="cuda").manual_seed(11)
+    X = torch.randn((4000, P), generator=g, device="cuda")
+    a, b = mk(), mk()
+    for m in (a, b):
+        m._layers = m._build(P, K, K > 1)
+        m._processed = 0.0
+    idxs = [torch.randint(0, 4000, (B,), generator=g, device="cuda") for _ in range(steps)]
+    old = os.environ.get("H2O3_DL_FUSED")
+    try:
+        for m, flag in ((a, "1"), (b, "0")):
+            os.environ["H2O3_DL_FUSED"] = flag
+            assert (m._fused_kind(hp, None) is not None) == (flag == "1")
+            for t, idx in enumerate(idxs):
+                m._train_step(X.index_select(0, idx), Y.index_select(0, idx),
+                              None if w is None else w.index_select(0, idx), 1000 + t, hp)
+    finally:
+        if old is None:
+            os.environ.pop("H2O3_DL_FUSED", None)
+        else:
+            os.environ["H2O3_DL_FUSED"] = old
+    torch.cuda.synchronize()
+    return a._layers, b._layers
+
+
+def _assert_layers_close(La, Lb):
+    for x, y in zip(La, Lb):
+        for ta, tb in ((x.W, y.W), (x.b, y.b), (x.state["ada"], y.state["ada"])):
+            # f32 sums in another order; an ADADELTA step is ~sign(g) sqrt(eps / (1 - rho))
+            # at the first steps, so a gradient within rounding of 0 may flip one weight
+            bad = ((ta - tb).abs() > 2e-5 + 2e-4 * tb.abs()).sum().item()
+            assert bad <= 2, (bad, (ta - tb).abs().max().item())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["bench", "tanh_multiclass_ragged", "regression_elu", "momentum"])
+def test_dl_fused_step_matches_unfused(case):
+    """The fused HIP MLP step (dl.hip dl_mlp_*: f32 MFMA forward/backward per
+    16-row tile, dW tiles, per-row updates) gives the weights, biases and
+    ADADELTA state of the unfused step (hipBLASLt GEMMs + element-wise
+    kernels) on the same batches and dropout seeds."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from h2o3_amd.ops import _native
+    g = torch.Generator(device="cuda").manual_seed(5)
+    base = dict(ae=False, ada=True, rate0=0.005, anneal=1e-6, decay=1.0, mom_start=0.0, mom_ramp=1e6,
+                mom_stable=0.0, has_mom=False, l1=0.0, l2=0.0, max_w2=3.4e38, sparsity=0.0)
+    if case == "bench":
+        P, K, B = 100, 2, 1024
+        Y = torch.randint(0, 2, (4000,), generator=g, device="cuda")
+        mk = lambda: H2ODeepLearningEstimator(hidden=[200, 200], activation="RectifierWithDropout", seed=42,
+                                              input_dropout_ratio=0.1)
+        w = None
+    elif case == "tanh_multiclass_ragged":
+        P, K, B = 13, 5, 333
+        Y = torch.randint(0, 5, (4000,), generator=g, device="cuda")
+        mk = lambda: H2ODeepLearningEstimator(hidden=[37, 19], activation="TanhWithDropout", seed=3,
+                                              hidden_dropout_ratios=[0.2, 0.3])
+        w = torch.rand(4000, generator=g, device="cuda") + 0.5
+        base.update(l1=1e-4, l2=1e-3, max_w2=2.0)
+    elif case == "regression_elu":
+        P, K, B = 24, 1, 100
+        Y = torch.randn((4000, 1), generator=g, device="cuda")
+        mk = lambda: H2ODeepLearningEstimator(hidden=[50], activation="ExpRectifier", seed=8)
+        w = None
+    else:
+        P, K, B = 32, 3, 256
+        Y = torch.randint(0, 3, (4000,), generator=g, device="cuda")
+        mk = lambda: H2ODeepLearningEstimator(hidden=[64, 32], activation="Rectifier", seed=9,
+                                              adaptive_rate=False, momentum_start=0.5, momentum_stable=0.9,
+                                              nesterov_accelerated_gradient=True)
+        w = None
+        base.update(ada=False, rate0=0.01, has_mom=True, mom_start=0.5, mom_stable=0.9, mom_ramp=1000.0,
+                    decay=0.9, max_w2=5.0)
+    hp = dict(base, K=K, bs=B)
+    La, Lb = _fused_vs_unfused(mk, P, K, B, Y, w, hp)
+    assert "libdl.so" in " ".join(_native.loaded_libs())
+    _assert_layers_close(La, Lb)
+    if not hp["ada"]:
+        for x, y in zip(La, Lb):
+            torch.testing.assert_close(x.state["mom"], y.state["mom"], rtol=2e-4, atol=2e-5)
