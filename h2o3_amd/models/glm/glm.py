@@ -620,9 +620,13 @@ class GLMDriver:
                     self._off32 = None if self.offset is None else self.offset.to(torch.float32)
                 P = self.P
                 bt = torch.as_tensor(self.beta[:P], dtype=torch.float32, device=self.X.device)
+                exact = os.environ.get("H2O3_GLM_EXACT_GRAD", "1") != "0"
+                # fused: eta pass + one hand-written MFMA Gram kernel over the f32
+                # rows (needs the exact gradient: its Gram has no z column)
                 Gf, dev, gx = linalg_ops.glm_wide_irls(self.X, P, bt, float(self.beta[-1]), self._y32,
-                                                       self._w32, self._off32, codes, self.fam.tvp, self.fam.theta)
-                if os.environ.get("H2O3_GLM_EXACT_GRAD", "1") != "0":
+                                                       self._w32, self._off32, codes, self.fam.tvp, self.fam.theta,
+                                                       fused=exact and linalg_ops.wide_fused_enabled())
+                if exact:
                     self._gexact = gx[:P + 1]
                     self._gbeta = np.concatenate([self.beta[:P].astype(np.float32).astype(np.float64),
                                                   [float(np.float32(self.beta[-1]))]])

@@ -1117,7 +1117,10 @@ template <int NQ>
 __global__ __launch_bounds__(256) void glm_wide_split_kernel(
     const float* __restrict__ X, int ldx, int P, int Pa, long long rows, const float* __restrict__ beta, float b0,
     const float* __restrict__ y, const float* __restrict__ wprior, const float* __restrict__ offset,
-    GlmFamArgs fam, __bf16* __restrict__ HL, double* __restrict__ dev_out, double* __restrict__ grad_out) {
+    GlmFamArgs fam, __bf16* __restrict__ HL, double* __restrict__ dev_out, double* __restrict__ grad_out,
+    float* __restrict__ wout) {
+  // HL null: no bf16 planes; wout[r] = the row's IRLS weight instead (the
+  // fused wide Gram kernel below reads X and these weights).
   // grad_out (optional): [gridDim.x][Pa] f64, this block's slot += X' r over
   // its rows of the chunk (r = w (y - mu) dmu/deta / var: the exact-gradient
   // channel, see glm_irls_ws_kernel); column P holds sum r
@@ -1174,6 +1177,10 @@ __global__ __launch_bounds__(256) void glm_wide_split_kernel(
       for (int q = 0; q < NQ; ++q) ga[q] += v[q] * rres;
       gi += rres;
     }
+    if (!HL) {
+      if (lane == 0) wout[r] = fmaxf(W, 0.f);
+      continue;
+    }
     const float s = sqrtf(fmaxf(W, 0.f));
     __bf16* o = HL + r * (2LL * Pa);
 #pragma unroll
@@ -1220,20 +1227,199 @@ __global__ __launch_bounds__(256) void glm_wide_split_kernel(
 extern "C" int h2o_glm_wide_split(const float* X, int ldx, int P, int Pa, long long rows, const float* beta, float b0,
                                   const float* y, const float* wprior, const float* offset, int link, int var,
                                   float tvp, float theta, void* HL, double* dev_out, int blocks, double* grad_out,
-                                  hipStream_t s) {
+                                  float* wout, hipStream_t s) {
   if (rows <= 0) return 0;
-  if (Pa % 4 != 0 || Pa < P + 2 || ldx < P || blocks <= 0) return -1;
+  if (Pa % 4 != 0 || Pa < P + 2 || ldx < P || blocks <= 0 || (!HL && !wout)) return -1;
   GlmFamArgs fam{link, var, tvp, theta, 0, 0, 0, 0};
   if (Pa <= 256)
     hipLaunchKernelGGL(glm_wide_split_kernel<1>, dim3(blocks), dim3(256), 0, s, X, ldx, P, Pa, rows, beta, b0, y,
-                       wprior, offset, fam, (__bf16*)HL, dev_out, grad_out);
+                       wprior, offset, fam, (__bf16*)HL, dev_out, grad_out, wout);
   else if (Pa <= 512)
     hipLaunchKernelGGL(glm_wide_split_kernel<2>, dim3(blocks), dim3(256), 0, s, X, ldx, P, Pa, rows, beta, b0, y,
-                       wprior, offset, fam, (__bf16*)HL, dev_out, grad_out);
+                       wprior, offset, fam, (__bf16*)HL, dev_out, grad_out, wout);
   else if (Pa <= 1024)
     hipLaunchKernelGGL(glm_wide_split_kernel<4>, dim3(blocks), dim3(256), 0, s, X, ldx, P, Pa, rows, beta, b0, y,
-                       wprior, offset, fam, (__bf16*)HL, dev_out, grad_out);
+                       wprior, offset, fam, (__bf16*)HL, dev_out, grad_out, wout);
   else
     return -2;
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Fused wide weighted Gram: C = [X | 1]' diag(w) [X | 1] straight from the
+// f32 rows of X (no bf16 planes in HBM, no library GEMM).
+//
+// Tiles: 128 x 128 blocks (bi <= bj) of the (NB*128)^2 Gram, column P is the
+// intercept's 1, columns past it are 0.  A workgroup owns one tile pair and
+// one row slice: chunks of 64 rows c = s, s + S, s + 2S, ...  The npairs
+// workgroups of a slice are consecutive logical ids after the XCD remap, so
+// they run on one XCD at the same time and read each 64-row chunk of X from
+// HBM once, then from that XCD's L2.
+//
+// Per chunk every thread loads eight 8-row column vectors (coalesced: a wave
+// reads 64 consecutive columns of one row per load), scales the A panel by
+// the row weights, splits x = hi + lo (bf16) and stores them k-contiguous in
+// LDS ([column][row], pitch 72 bf16: conflict-free b128 operand reads); the
+// next chunk's loads are issued before this chunk's MFMAs.  Each wave owns a
+// 64 x 64 quarter of the tile: 16 accumulators of v_mfma_f32_16x16x32_bf16,
+// three MFMAs per product (hi hi + hi lo + lo hi, the lo lo term ~2^-16
+// relative dropped).  The f32 accumulators are folded into the workgroup's
+// own f64 slot every `fold` chunks (64 K rows at fold 1024) and at the end;
+// the host sums the slices in f64.
+// ---------------------------------------------------------------------------
+#define WG_T 128
+#define WG_KR 64
+#define WG_PITCH 72
+
+__device__ __forceinline__ void wg_pair(int p, int NB, int* bi, int* bj) {
+  int i = 0;
+  while (p >= NB - i) {
+    p -= NB - i;
+    ++i;
+  }
+  *bi = i;
+  *bj = i + p;
+}
+
+__global__ __launch_bounds__(256, 2) void glm_wide_gram_kernel(const float* __restrict__ X, int ldx, int P,
+                                                               long long N, const float* __restrict__ Wr, int NB,
+                                                               int npairs, int S, int fold,
+                                                               double* __restrict__ part) {
+  extern __shared__ __bf16 wg_lds[];
+  __bf16* sAh = wg_lds;
+  __bf16* sAl = sAh + WG_T * WG_PITCH;
+  __bf16* sBh = sAl + WG_T * WG_PITCH;
+  __bf16* sBl = sBh + WG_T * WG_PITCH;
+  const int nblk = npairs * S;
+  const int L = xcd_remap(blockIdx.x, nblk);
+  const int sl = L / npairs, pr = L - sl * npairs;
+  int bi, bj;
+  wg_pair(pr, NB, &bi, &bj);
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int mi = wv >> 1, ni = wv & 1;
+  const long long nchunk = (N + WG_KR - 1) / WG_KR;
+  // loader slots: q = 0..7 -> panel q >> 2 (A = bi, B = bj), column
+  // tid & 127, row group ((tid >> 7) + 2 q) & 7 -- wave-uniform, so the row
+  // offsets are scalar and the weights scalar loads; X through a buffer
+  // descriptor rebased per chunk (rows past N read as 0 by the range check)
+  const int t7 = __builtin_amdgcn_readfirstlane(tid >> 7);
+  const int colb = tid & 127;
+  const int gcA = bi * WG_T + colb, gcB = bj * WG_T + colb;
+  const float fillA = gcA == P ? 1.f : 0.f, fillB = gcB == P ? 1.f : 0.f;
+  const bool inA = gcA < P, inB = gcB < P;
+  float xr[8][8];
+  auto load = [&](long long c) {
+    const long long row0 = c * WG_KR;
+    const int nr = (int)((N - row0) < WG_KR ? (N - row0) : WG_KR);
+    const __amdgpu_buffer_rsrc_t rx =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(X + row0 * ldx), (short)0, nr * ldx * 4, 0x00020000);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int pan = q >> 2;
+      const int rg = (t7 + 2 * q) & 7;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int rr = rg * 8 + e;
+        float x = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rx, (pan ? gcB : gcA) * 4, rr * ldx * 4, 0));
+        x = (pan ? inB : inA) ? x : (pan ? fillB : fillA);
+        if (!pan) x *= rr < nr ? Wr[row0 + rr] : 0.f;
+        xr[q][e] = x;
+      }
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int pan = q >> 2, col = colb, rg = (t7 + 2 * q) & 7;
+      bf16x8 h, l;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        h[e] = (__bf16)xr[q][e];
+        l[e] = (__bf16)(xr[q][e] - (float)h[e]);
+      }
+      const int off = col * WG_PITCH + rg * 8;
+      *reinterpret_cast<bf16x8*>((pan ? sBh : sAh) + off) = h;
+      *reinterpret_cast<bf16x8*>((pan ? sBl : sAl) + off) = l;
+    }
+  };
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  double* my = part + (size_t)L * (WG_T * WG_T);
+  auto fold_out = [&]() {
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = 64 * mi + 16 * a + 4 * (lane >> 4) + r, j = 64 * ni + 16 * b + (lane & 15);
+          my[i * WG_T + j] += (double)acc[a][b][r];
+        }
+        acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+  };
+  long long c = sl;
+  if (c < nchunk) load(c);
+  int since = 0;
+  while (c < nchunk) {
+    __syncthreads();  // the previous chunk's operand reads are done
+    store();
+    __syncthreads();
+    const long long cn = c + S;
+    if (cn < nchunk) load(cn);  // in flight during this chunk's MFMAs
+#pragma unroll
+    for (int ks = 0; ks < WG_KR / 32; ++ks) {
+      const int ko = ks * 32 + 8 * (lane >> 4);
+      bf16x8 ah[4], al[4];
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        const int off = (64 * mi + 16 * a + (lane & 15)) * WG_PITCH + ko;
+        ah[a] = *reinterpret_cast<const bf16x8*>(sAh + off);
+        al[a] = *reinterpret_cast<const bf16x8*>(sAl + off);
+      }
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        // one B column tile at a time (8 registers); the 12 MFMAs on four
+        // accumulators keep dependent issues 4 apart
+        const int off = (64 * ni + 16 * b + (lane & 15)) * WG_PITCH + ko;
+        const bf16x8 bh = *reinterpret_cast<const bf16x8*>(sBh + off);
+        const bf16x8 bl = *reinterpret_cast<const bf16x8*>(sBl + off);
+#pragma unroll
+        for (int a = 0; a < 4; ++a) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[a], bh, acc[a][b], 0, 0, 0);
+#pragma unroll
+        for (int a = 0; a < 4; ++a) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[a], bl, acc[a][b], 0, 0, 0);
+#pragma unroll
+        for (int a = 0; a < 4; ++a) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[a], bh, acc[a][b], 0, 0, 0);
+      }
+    }
+    if (++since == fold) {
+      fold_out();
+      since = 0;
+    }
+    c = cn;
+  }
+  if (since) fold_out();
+}
+
+// part: [npairs * S][128][128] f64, zeroed by the caller; slot L holds
+// pair L % npairs (bi <= bj, row-major over the upper triangle of the NB x NB
+// tile grid) for slice L / npairs.  NB = ceil((P + 1) / 128).
+extern "C" int h2o_glm_wide_gram(const float* X, int ldx, int P, long long N, const float* Wr, int S, int fold,
+                                 double* part, hipStream_t s) {
+  if (N <= 0) return 0;
+  if (ldx < P || S <= 0 || fold <= 0) return -1;
+  const int NB = (P + 1 + WG_T - 1) / WG_T;
+  const int npairs = NB * (NB + 1) / 2;
+  const size_t lds = 4 * WG_T * WG_PITCH * sizeof(__bf16);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)glm_wide_gram_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  hipLaunchKernelGGL(glm_wide_gram_kernel, dim3(npairs * S), dim3(256), lds, s, X, ldx, P, N, Wr, NB, npairs, S, fold,
+                     part);
   return (int)hipGetLastError();
 }

@@ -24,7 +24,8 @@ def _lib():
         lib.h2o_glm_irls.argtypes = [P, LL, I, I, P, I, I, I, P, F, P, P, P, I, I, F, F, P, P, I, I, P, P, P, I, I, P]
         lib.h2o_glm_irls_chunk.argtypes = [I]
         lib.h2o_gram_split.argtypes = [P, I, I, I, P, P, LL, P, P]
-        lib.h2o_glm_wide_split.argtypes = [P, I, I, I, LL, P, F, P, P, P, I, I, F, F, P, P, I, P, P]
+        lib.h2o_glm_wide_split.argtypes = [P, I, I, I, LL, P, F, P, P, P, I, I, F, F, P, P, I, P, P, P]
+        lib.h2o_glm_wide_gram.argtypes = [P, I, I, LL, P, I, I, P, P]
         lib._typed = True
     return lib
 
@@ -316,13 +317,46 @@ def gram_aug_bf3(X, W, z, P, step=1 << 19):
     return G
 
 
-def glm_wide_irls(X, P, beta, b0, y, wprior=None, offset=None, codes=(1, 1), tvp=0.0, theta=1e-10, step=1 << 19):
-    """Fused IRLS pass for wide GLMs (P + 2 <= 1024): per row chunk one HIP
-    kernel (glm_wide_split_kernel: eta, IRLS weight, working response,
-    deviance, bf16 [hi | lo] split of sqrt(W) [x | 1 | z]) and one bf16 GEMM
-    with f32 output.  Returns (G [Pa, Pa] f64 augmented Gram, deviance f64,
-    g [Pa] f64 exact-gradient channel X'r with g[P] = sum r, r = w (y - mu)
-    dmu/deta / var: f32 VALU products over <= 64 rows per lane, f64 beyond)."""
+def wide_fused_enabled():
+    """The fused wide Gram (glm_wide_gram_kernel) is the default wide pass;
+    H2O3_GLM_WIDE_FUSED=0 selects the split + library GEMM pass."""
+    return os.environ.get("H2O3_GLM_WIDE_FUSED", "1") != "0"
+
+
+def _wide_gram_assemble(part, S, NB, P):
+    """Sum the slices' f64 tile partials and mirror the upper-triangle tiles
+    into the full (P + 2)^2 Gram (the z column left 0)."""
+    T = part.view(S, -1, 128, 128).sum(0)
+    npairs = T.shape[0]
+    bi = torch.tensor([i for i in range(NB) for _ in range(i, NB)], device=part.device)
+    bj = torch.tensor([j for i in range(NB) for j in range(i, NB)], device=part.device)
+    assert bi.numel() == npairs
+    dg = bi == bj                        # diagonal tiles: both halves computed, symmetrize
+    T[dg] = 0.5 * (T[dg] + T[dg].transpose(1, 2))
+    G = torch.zeros((NB * 128, NB * 128), dtype=torch.float64, device=part.device)
+    Gt = G.view(NB, 128, NB, 128).permute(0, 2, 1, 3)
+    Gt[bj, bi] = T.transpose(1, 2)
+    Gt[bi, bj] = T
+    out = torch.zeros((P + 2, P + 2), dtype=torch.float64, device=part.device)
+    out[:P + 1, :P + 1] = G[:P + 1, :P + 1]
+    return out
+
+
+def glm_wide_irls(X, P, beta, b0, y, wprior=None, offset=None, codes=(1, 1), tvp=0.0, theta=1e-10, step=1 << 19,
+                  fused=False):
+    """Fused IRLS pass for wide GLMs (P + 2 <= 1024).
+
+    fused=True (needs the exact-gradient channel: the Gram carries no z
+    column): per row chunk glm_wide_split_kernel computes eta, the IRLS
+    weight, deviance and X'r and writes only the row weights; then ONE
+    glm_wide_gram_kernel launch builds [X | 1]' W [X | 1] straight from the
+    f32 rows (bf16x3 MFMA, f64 folds) -- no bf16 planes, no library GEMM.
+    fused=False: the kernel writes bf16 [hi | lo] planes of sqrt(W) [x | 1 |
+    z] and one bf16 library GEMM per chunk group forms the Gram.
+
+    Returns (G [Pa, Pa] f64 augmented Gram, deviance f64, g [Pa] f64
+    exact-gradient channel X'r with g[P] = sum r, r = w (y - mu) dmu/deta /
+    var: f32 VALU products over <= 64 rows per lane, f64 beyond)."""
     lib = _lib()
     if lib is None:
         raise RuntimeError("gram extension not built (run __graft_entry__.build())")
@@ -335,6 +369,29 @@ def glm_wide_irls(X, P, beta, b0, y, wprior=None, offset=None, codes=(1, 1), tvp
     keep = [_f32(y), _f32(wprior), _f32(offset)]
     st = min(step, max(N, 1))
     nch = -(-N // st)
+    if fused:
+        blocks = 2048
+        dev = torch.zeros((nch, blocks), dtype=torch.float64, device=X.device)
+        gbuf = torch.zeros((blocks, Pa), dtype=torch.float64, device=X.device)
+        wr = torch.empty(N, dtype=torch.float32, device=X.device)
+        stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        offp = lambda t, a: ctypes.c_void_p(0 if t is None else t.data_ptr() + a * 4)
+        for i, a in enumerate(range(0, N, st)):
+            r = min(st, N - a)
+            rc = lib.h2o_glm_wide_split(ctypes.c_void_p(X.data_ptr() + a * ldx * 4), ldx, P, Pa, r, _ptr(bt),
+                                        float(b0), offp(keep[0], a), offp(keep[1], a), offp(keep[2], a),
+                                        int(codes[0]), int(codes[1]), float(tvp), float(theta), None, _ptr(dev[i]),
+                                        blocks, _ptr(gbuf), offp(wr, a), stream)
+            if rc != 0:
+                raise RuntimeError(f"h2o_glm_wide_split failed: {rc}")
+        NB = -(-(P + 1) // 128)
+        npairs = NB * (NB + 1) // 2
+        S = max(1, 512 // npairs)
+        part = torch.zeros((npairs * S, 128, 128), dtype=torch.float64, device=X.device)
+        rc = lib.h2o_glm_wide_gram(_ptr(X), ldx, P, N, _ptr(wr), S, 1024, _ptr(part), stream)
+        if rc != 0:
+            raise RuntimeError(f"h2o_glm_wide_gram failed: {rc}")
+        return _wide_gram_assemble(part, S, NB, P), dev.sum(), gbuf.sum(0)
     grp = min(nch, _WIDE_GROUP)
     HL = torch.empty((grp * st, 2 * Pa), dtype=torch.bfloat16, device=X.device)
     blocks = 2048
@@ -351,7 +408,7 @@ def glm_wide_irls(X, P, beta, b0, y, wprior=None, offset=None, codes=(1, 1), tvp
                                     float(b0), off(keep[0], a), off(keep[1], a), off(keep[2], a), int(codes[0]),
                                     int(codes[1]), float(tvp), float(theta),
                                     ctypes.c_void_p(buf.data_ptr() + j * st * 2 * Pa * 2), _ptr(dev[i]), blocks,
-                                    _ptr(gbuf), strm)
+                                    _ptr(gbuf), None, strm)
         if rc != 0:
             raise RuntimeError(f"h2o_glm_wide_split failed: {rc}")
 

@@ -390,9 +390,11 @@ def _fused_vs_unfused(mk, P, K, B, Y, w, hp, steps=3, graph=False):
     g = torch.Generator(device="cuda").manual_seed(11)
     X = torch.randn((4000, P), generator=g, device="cuda")
     a, b = mk(), mk()
+    from h2o3_amd.models.distributions import get_distribution
     for m in (a, b):
         m._layers = m._build(P, K, K > 1)
         m._processed = 0.0
+        m._dist = get_distribution("AUTO" if K > 1 else "gaussian", K)
     idxs = [torch.randint(0, 4000, (B,), generator=g, device="cuda") for _ in range(steps)]
     old = os.environ.get("H2O3_DL_FUSED")
     try:

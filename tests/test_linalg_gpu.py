@@ -158,10 +158,13 @@ def test_glm_irls_narrow_rows(fused):
         torch.testing.assert_close(dn, dp, rtol=1e-9, atol=1e-9)
 
 
+@pytest.mark.parametrize("fused", [False, True])
 @pytest.mark.parametrize("family,link", [("binomial", "logit"), ("poisson", "log"), ("gaussian", "identity")])
-def test_glm_wide_irls_matches_fp64(family, link):
-    """Fused wide pass (eta + family + bf16 hi/lo split + one bf16 GEMM) vs
-    the fp64 reference, P = 601 (odd width: scalar tail loads)."""
+def test_glm_wide_irls_matches_fp64(family, link, fused):
+    """Wide pass vs the fp64 reference, P = 601 (odd width: scalar tail
+    loads), n = 40009 (a ragged last 64-row chunk).  fused=False: eta +
+    family + bf16 hi/lo split + one bf16 library GEMM; fused=True: eta pass +
+    the hand-written MFMA Gram kernel over the f32 rows (no z column)."""
     n, P, Pp = 40_009, 601, 640
     X, beta, g = _data(n, P, Pp, seed=17)
     beta *= 0.3
@@ -178,9 +181,10 @@ def test_glm_wide_irls_matches_fp64(family, link):
     codes = linalg_ops.glm_fused_codes(family, link)
     Xn = X[:, :P].contiguous()
     Gk, dk, gk = linalg_ops.glm_wide_irls(Xn.cuda(), P, beta[:P].cuda(), -0.2, y.cuda(), w.cuda(), off.cuda(),
-                                          codes, step=16_384)
+                                          codes, step=16_384, fused=fused)
     Gr, dr = linalg_ops.glm_irls_reference(X, aug=P, beta=beta, b0=-0.2, y=y, wprior=w, offset=off, fam=fam)
-    A, B = Gk[: P + 2, : P + 2].cpu(), Gr[: P + 2, : P + 2]
+    m = P + 1 if fused else P + 2
+    A, B = Gk[:m, :m].cpu(), Gr[:m, :m]
     diag = B.diagonal().abs().sqrt().clamp_min(1e-12)
     rel = (A - B).abs() / (diag.view(-1, 1) * diag.view(1, -1))
     assert rel.max().item() < 5e-5
@@ -382,3 +386,32 @@ def test_wide_split_gemm_overlap_matches_sequential(monkeypatch):
         out[mode] = (G.cpu(), d.cpu(), Ga.cpu(), gx.cpu())
     for a, b in zip(out["0"], out["1"]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,P", [(100, 1000), (200_003, 1000), (70_001, 127), (5_000, 128)])
+def test_glm_wide_fused_gram_matches_fp64(n, P):
+    """glm_wide_gram_kernel alone: [X | 1]' W [X | 1] from the f32 rows vs
+    fp64, at widths that fill 8 column tiles (P = 1000, the BASELINE wide
+    config's width), exactly one tile with and without the intercept spilling
+    into a second (127 / 128), with fewer chunks than slices (n = 100) and a
+    ragged last chunk."""
+    g = torch.Generator().manual_seed(n + P)
+    X = torch.randn(n, P, generator=g)
+    X[:, :3] *= 40.0                                # columns of very different scale
+    beta = 0.02 * torch.randn(P, generator=g)
+    y = (torch.rand(n, generator=g) < 0.4).float()
+    codes = linalg_ops.glm_fused_codes("binomial", "logit")
+    G, _, _ = linalg_ops.glm_wide_irls(X.cuda(), P, beta.cuda(), 0.1, y.cuda(), None, None, codes, step=1 << 16,
+                                       fused=True)
+    eta = X.double() @ beta.double() + 0.1
+    mu = torch.sigmoid(eta)
+    W = mu * (1 - mu)
+    Xa = torch.cat([X.double(), torch.ones(n, 1, dtype=torch.float64)], 1)
+    ref = Xa.T @ (Xa * W.view(-1, 1))
+    A = G[:P + 1, :P + 1].cpu()
+    d = ref.diagonal().sqrt()
+    rel = (A - ref).abs() / (d.view(-1, 1) * d.view(1, -1))
+    assert rel.max().item() < 3e-5, rel.max().item()
+    assert torch.equal(A, A.T)
+    assert float(G[P + 1].abs().sum()) == 0.0
