@@ -143,24 +143,46 @@ class ScoreSchedule:
 
 
 class ScoreKeeper:
-    """Early stopping on a moving average (hex/ScoreKeeper.java:stopEarly)."""
+    """Early stopping on moving averages (hex/ScoreKeeper.java:278 stopEarly)."""
+
+    # StoppingMetric(..., lowerBoundBy0, ...) (ScoreKeeper.java:133-147)
+    _LOWER_BOUND_0 = frozenset(["logloss", "mse", "rmse", "mae", "rmsle", "auc", "aucpr", "misclassification",
+                                "mean_per_class_error"])
 
     @staticmethod
-    def stop_early(history, k, tol, less_is_better=True):
-        if k <= 0 or len(history) < 2 * k:
+    def stop_early(history, k, tol, less_is_better=True, metric=None):
+        """k + 1 simple moving averages (window k) over the last 2k scoring
+        events: the first is the reference, the other k the new ones.  Stop
+        when the best new average improves on the reference by less than the
+        relative tolerance (ratio >= 1 - tol, or <= 1 + tol for metrics where
+        more is better).  Never stop on a NaN average, on averages of mixed
+        sign (deviance / R^2 crossing 0) or when the best new average has
+        another sign than the reference; always stop when a metric bounded
+        below by 0 has a reference average of exactly 0.  `history` holds
+        the scoring events after the model's initial (zero-iteration) event,
+        which the reference skips."""
+        n = len(history)
+        if k <= 0 or n < 2 * k:
             return False
-        vals = [v for v in history if v is not None and not math.isnan(v)]
-        if len(vals) < 2 * k:
+        vals = [float("nan") if v is None else float(v) for v in history]
+        avgs = []
+        for i in range(k + 1):
+            s = n - 2 * k + i
+            a = sum(vals[s:s + k]) / k
+            if math.isnan(a):
+                return False
+            avgs.append(a)
+        ref, new = avgs[0], avgs[1:]
+        lo, hi = min(new), max(new)
+        if metric is not None and str(metric).lower() in ScoreKeeper._LOWER_BOUND_0 and ref == 0.0:
+            return True
+        extreme = lo if less_is_better else hi
+        if np.sign(max(avgs)) != np.sign(min(avgs)) or np.sign(extreme) != np.sign(ref):
             return False
-        # reference: compare the best moving average of the last k against the one before
-        last = np.mean(vals[-k:])
-        ref = np.mean(vals[-2 * k:-k])
-        best_ref = min(np.mean(vals[i - k:i]) for i in range(k, len(vals) - k + 1)) if less_is_better else \
-            max(np.mean(vals[i - k:i]) for i in range(k, len(vals) - k + 1))
-        ref = best_ref
-        if less_is_better:
-            return not (last < ref * (1 - tol) if ref >= 0 else last < ref * (1 + tol))
-        return not (last > ref * (1 + tol) if ref >= 0 else last > ref * (1 - tol))
+        if ref == 0.0:
+            return False                              # 0 / 0 in the reference: NaN ratio
+        ratio = extreme / ref
+        return ratio >= 1 - tol if less_is_better else ratio <= 1 + tol
 
 
 def _encoding_wrapper(fn):

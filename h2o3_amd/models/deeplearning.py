@@ -557,7 +557,7 @@ class H2ODeepLearningEstimator(H2OEstimator):
                             break
                         if stop_rounds > 0 and ScoreKeeper.stop_early(history, stop_rounds,
                                                                       float(p.get("stopping_tolerance", 0.0)),
-                                                                      smetric in _LESS_IS_BETTER):
+                                                                      smetric in _LESS_IS_BETTER, metric=smetric):
                             break
                     iter_t0 = time.time()
                 # job progress / cancel and the max_runtime_secs clock, agreed across

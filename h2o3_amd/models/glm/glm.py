@@ -967,7 +967,7 @@ class H2OGeneralizedLinearEstimator(H2OEstimator):
                         key = ("validation_" if spec.valid is not None else "training_") + metric_name
                         history.append(entry.get(key))
                         if ScoreKeeper.stop_early(history, stop_rounds, float(p.get("stopping_tolerance", 1e-3)),
-                                                  metric_name in _LESS_IS_BETTER):
+                                                  metric_name in _LESS_IS_BETTER, metric=metric_name):
                             early_stop = True
                             break
                     if timed_out:

@@ -260,7 +260,10 @@ class GBMDriver:
         reseed_iteration(self, self._seed(), self.iter)
         w = self._row_weights()
         self.gp.tree_col_mask = self._tree_col_mask()
-        lr = self.lr * (float(p.get("learn_rate_annealing", 1.0)) ** self.iter)
+        # GBM.effective_learning_rate (GBM.java:726): learn_rate *
+        # annealing^(trees already built - 1) while the leaves of the next tree
+        # are fitted -- the first tree uses learn_rate / annealing
+        lr = self.lr * (float(p.get("learn_rate_annealing", 1.0)) ** (self.iter - 1))
         maxabs = float(p.get("max_abs_leafnode_pred", 1.79e308))
         if self.K == 1:
             dpend = self.__dict__.get("_dpend")
@@ -540,10 +543,14 @@ class H2OGradientBoostingEstimator(SharedTreeEstimator):
         max_rt = float(p.get("max_runtime_secs") or 0)
         self._scoring_history = []
         sched = ScoreSchedule(p)
+        anneal = float(p.get("learn_rate_annealing", 1.0))
         while drv.iter < ntrees:
             drv.step()
+            # GBM.java:586: stop once the effective learning rate of the next
+            # tree, learn_rate * annealing^(ntrees - 1), drops below 1e-6
+            lr_stop = anneal < 1.0 and float(p["learn_rate"]) * anneal ** (drv.iter - 1) < 1e-6
             # a max_runtime_secs stop scores the last tree into the history too
-            score, timed_out = self._tick(drv.iter, ntrees, sched, drv.iter == ntrees, t0, max_rt)
+            score, timed_out = self._tick(drv.iter, ntrees, sched, drv.iter == ntrees or lr_stop, t0, max_rt)
             if score:
                 sched.started()
                 entry = self._score_iteration(drv, spec)
@@ -554,9 +561,9 @@ class H2OGradientBoostingEstimator(SharedTreeEstimator):
                     key = ("validation_" if spec.valid is not None else "training_") + suffix
                     history.append(entry.get(key))
                     if ScoreKeeper.stop_early(history, stop_rounds, float(p["stopping_tolerance"]),
-                                              metric_name in _LESS_IS_BETTER):
+                                              metric_name in _LESS_IS_BETTER, metric=metric_name):
                         break
-            if timed_out:
+            if timed_out or lr_stop:
                 break
             ckdir = p.get("in_training_checkpoints_dir")
             if ckdir and drv.iter % max(1, int(p.get("in_training_checkpoints_tree_interval") or 1)) == 0 and \

@@ -243,7 +243,7 @@ class H2OXGBoostEstimator(SharedTreeEstimator):
                         ("custom" if metric_name.startswith("custom") else metric_name)
                     history.append(entry.get(key))
                     if ScoreKeeper.stop_early(history, stop_rounds, float(p.get("stopping_tolerance", 0.001)),
-                                              metric_name in _LESS_IS_BETTER):
+                                              metric_name in _LESS_IS_BETTER, metric=metric_name):
                         break
             if timed_out:
                 break

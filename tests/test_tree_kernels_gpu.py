@@ -868,3 +868,61 @@ def test_drf_pair_path_narrow_scoring_and_posv_same_trees(classify, monkeypatch)
         np.testing.assert_array_equal(np.asarray(t0.feat), np.asarray(t1.feat))
         np.testing.assert_array_equal(np.asarray(t0.thr), np.asarray(t1.thr))
         np.testing.assert_allclose(np.asarray(t0.value), np.asarray(t1.value), rtol=1e-9, atol=1e-12)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_pair_narrow_scoring_matches_torch_reference(mode):
+    """The DRF device pair path with narrow bins (h2o_pair_hist4b leaves each
+    pair's bins past its feature's own codes unwritten; cat_pair_kernel and
+    pair_select2 scan only [0, nbins_f) + NA) picks, per node, the gain,
+    feature and threshold of the torch split search (_find_splits_torch) run
+    on the fp64 torch pair histograms of the same rows -- a 1000-level
+    categorical makes Bs = 1025 while the numeric columns have <= 255 bins or
+    a dozen integer levels."""
+    _need_gpu()
+    from h2o3_amd.models.tree.binning import bin_frame_tensors
+    from h2o3_amd.models.tree.engine import GrowParams, TreeGrower
+    from h2o3_amd.ops import tree_ops
+    g = torch.Generator(device="cuda").manual_seed(21)
+    n = 24000
+    feats, is_cat, cards = [], [], []
+    for j in range(7):
+        x = torch.randn(n, generator=g, device="cuda")
+        if j == 2:
+            x = torch.randint(0, 12, (n,), generator=g, device="cuda").float()     # 12 integer levels
+        x[torch.rand(n, generator=g, device="cuda") < 0.04] = float("nan")
+        feats.append(x), is_cat.append(False), cards.append(0)
+    c = torch.randint(-1, 1000, (n,), generator=g, device="cuda").to(torch.int32)
+    feats.append(c), is_cat.append(True), cards.append(1000)
+    bd = bin_frame_tensors(feats, is_cat, cards, [f"f{j}" for j in range(8)], hist_type="QuantilesGlobal",
+                           nbins=255)
+    assert bd.Bs - 1 > 256
+    eff = torch.randn(1000, generator=g, device="cuda")
+    y = feats[0].nan_to_num(0) + 0.5 * feats[2].nan_to_num(0) + eff[c.clamp_min(0).long()] + \
+        0.3 * torch.randn(n, generator=g, device="cuda")
+    if mode == 0:
+        va, vb = y, None
+    else:
+        va, vb = y, torch.rand(n, generator=g, device="cuda") + 0.5
+    gr = TreeGrower(bd, GrowParams(min_rows=5, seed=3))
+    assert gr._narrow_bins() is not None
+    gr._vmax = tree_ops.channel_max(va, vb, mode)
+    ridx = torch.randperm(n, generator=g, device="cuda").to(torch.int32)
+    st, ct = np.array([0, 9000, 9400]), np.array([9000, 400, 14600])
+    k = 4
+    sel = torch.stack([torch.tensor(s, device="cuda") for s in ([0, 2, 5, 7], [1, 2, 3, 7], [2, 4, 6, 7])])
+    res = gr._pair_direct_dev(ridx, va, vb, mode, st, ct, sel)
+    pn = np.repeat(np.arange(3), k)
+    pf = sel.cpu().numpy().reshape(-1)
+    Hr, wr = tree_ops.pair_hist(bd, ridx, va, vb, mode, st, ct, pn, pf, want_wyy=mode == 0, use_native=False)
+    F = bd.F
+    H = torch.zeros((gr.Fpad, 3, bd.Bs, 2), dtype=torch.float64, device="cuda")
+    allowed = torch.zeros((3, gr.Fpad), dtype=torch.bool, device="cuda")
+    for p_, (i, f) in enumerate(zip(pn, pf)):
+        H[f, i] = Hr[p_]
+        allowed[i, f] = True
+    ref = gr._find_splits_torch(H[:F], allowed[:, :F], node_wyy=wr)
+    torch.testing.assert_close(res["gain"].cpu(), ref["gain"].cpu().to(torch.float64), rtol=1e-6, atol=1e-6)
+    assert res["feat"].cpu().tolist() == ref["feat"].cpu().tolist()
+    num = res["feat"].cpu() != 7                       # numeric winners: the same threshold bin
+    assert res["t"].cpu()[num].tolist() == ref["t"].cpu()[num].tolist()
