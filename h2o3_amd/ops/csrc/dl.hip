@@ -309,7 +309,7 @@ __global__ __launch_bounds__(256) void dl_softmax_kernel(float* __restrict__ Z, 
 //                      the ones the weight gradient needs (A_l, dZ_l) are
 //                      also written to HBM.
 //   dl_mlp_dw_kernel   one workgroup per 16x16 tile of a dW_l = dZ_l^T A_l:
-//                      4 waves split the batch rows, fold through LDS; the
+//                      8 waves split the batch rows, fold through LDS; the
 //                      tiles of the first column also write db_l = sum dZ_l.
 //   dl_mlp_upd_kernel  one wave per neuron row of every layer: the reference
 //                      per-row bprop tail (dl_upd_weight / dl_upd_bias, the
@@ -395,31 +395,48 @@ __global__ __launch_bounds__(256) void dl_mlp_fb_kernel(const DLNet net, const f
     const int act = last ? 0 : net.act[l];
     const unsigned thr = last ? 0u : net.thr[l + 1];
     const unsigned long long lseed = seed + 7919ull * (unsigned long long)(l + 1);
+    const int nk = KP >> 4;
+    // W float4 of tile t (output units t*16 + c16) at k step ks (-> k = 16 ks + g4)
+    auto wload = [&](int t, int ks) -> float4 {
+      float4 w = make_float4(0.f, 0.f, 0.f, 0.f);
+      const int u = t * 16 + c16, kk = ks * 16 + g4;
+      if (t < NT && u < U) {
+        const float* wr = W + (long long)u * I + kk;
+        if (vec && kk + 3 < I) {
+          w = *reinterpret_cast<const float4*>(wr);
+        } else {
+          w.x = kk < I ? wr[0] : 0.f;
+          w.y = kk + 1 < I ? wr[1] : 0.f;
+          w.z = kk + 2 < I ? wr[2] : 0.f;
+          w.w = kk + 3 < I ? wr[3] : 0.f;
+        }
+      }
+      return w;
+    };
     for (int t0 = wave; t0 < NT; t0 += 16) {
       dl_f32x4 acc[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[j] = (dl_f32x4){0.f, 0.f, 0.f, 0.f};
-      for (int k0 = 0; k0 < KP; k0 += 16) {
-        const int kk = k0 + g4;
-        const float4 a = *reinterpret_cast<const float4*>(ain + c16 * Si + kk);
+      // 4-deep register ring of weight loads: the L2 latency of step ks + 4
+      // hides behind the MFMAs of steps ks .. ks + 3
+      float4 wq[4][4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int t = t0 + 4 * j;
-          if (t < NT) {
-            const int u = t * 16 + c16;
-            float4 w = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (u < U) {
-              const float* wr = W + (long long)u * I + kk;
-              if (vec && kk + 3 < I) {
-                w = *reinterpret_cast<const float4*>(wr);
-              } else {
-                w.x = kk < I ? wr[0] : 0.f;
-                w.y = kk + 1 < I ? wr[1] : 0.f;
-                w.z = kk + 2 < I ? wr[2] : 0.f;
-                w.w = kk + 3 < I ? wr[3] : 0.f;
-              }
+      for (int d = 0; d < 4; ++d)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) wq[d][j] = d < nk ? wload(t0 + 4 * j, d) : make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int kb = 0; kb < nk; kb += 4) {
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          const int ks = kb + d;
+          if (ks < nk) {
+            const float4 a = *reinterpret_cast<const float4*>(ain + c16 * Si + ks * 16 + g4);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (t0 + 4 * j < NT) acc[j] = dl_mfma4(a, wq[d][j], acc[j]);
+            if (ks + 4 < nk) {
+#pragma unroll
+              for (int j = 0; j < 4; ++j) wq[d][j] = wload(t0 + 4 * j, ks + 4);
             }
-            acc[j] = dl_mfma4(a, w, acc[j]);
           }
         }
       }
@@ -502,27 +519,42 @@ __global__ __launch_bounds__(256) void dl_mlp_fb_kernel(const DLNet net, const f
     const int act = net.act[l - 1];
     const unsigned thr = net.thr[l];
     const unsigned long long lseed = seed + 7919ull * (unsigned long long)l;
+    const int nk = KP >> 4;
+    // W column slice of tile t (inputs t*16 + c16) at k step ks: rows 16 ks + g4 .. +3
+    auto wload = [&](int t, int ks) -> float4 {
+      float4 w = make_float4(0.f, 0.f, 0.f, 0.f);
+      const int i = t * 16 + c16, kk = ks * 16 + g4;
+      if (t < NT && i < I) {
+        const float* wc = W + (long long)kk * I + i;
+        w.x = kk < U ? wc[0] : 0.f;
+        w.y = kk + 1 < U ? wc[I] : 0.f;
+        w.z = kk + 2 < U ? wc[2 * I] : 0.f;
+        w.w = kk + 3 < U ? wc[3 * I] : 0.f;
+      }
+      return w;
+    };
     for (int t0 = wave; t0 < NT; t0 += 16) {
       dl_f32x4 acc[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[j] = (dl_f32x4){0.f, 0.f, 0.f, 0.f};
-      for (int k0 = 0; k0 < KP; k0 += 16) {
-        const int kk = k0 + g4;
-        const float4 d = *reinterpret_cast<const float4*>(dcur + c16 * net.ldsw + kk);
+      float4 wq[4][4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int t = t0 + 4 * j;
-          if (t < NT) {
-            const int i = t * 16 + c16;
-            float4 w = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (i < I) {
-              const float* wc = W + (long long)kk * I + i;
-              w.x = kk < U ? wc[0] : 0.f;
-              w.y = kk + 1 < U ? wc[I] : 0.f;
-              w.z = kk + 2 < U ? wc[2 * I] : 0.f;
-              w.w = kk + 3 < U ? wc[3 * I] : 0.f;
+      for (int d = 0; d < 4; ++d)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) wq[d][j] = d < nk ? wload(t0 + 4 * j, d) : make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int kb = 0; kb < nk; kb += 4) {
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          const int ks = kb + d;
+          if (ks < nk) {
+            const float4 dv = *reinterpret_cast<const float4*>(dcur + c16 * net.ldsw + ks * 16 + g4);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (t0 + 4 * j < NT) acc[j] = dl_mfma4(dv, wq[d][j], acc[j]);
+            if (ks + 4 < nk) {
+#pragma unroll
+              for (int j = 0; j < 4; ++j) wq[d][j] = wload(t0 + 4 * j, ks + 4);
             }
-            acc[j] = dl_mfma4(d, w, acc[j]);
           }
         }
       }
@@ -560,9 +592,9 @@ struct DLGrad {
   float* db[DL_MAXL];
 };
 
-__global__ __launch_bounds__(256) void dl_mlp_dw_kernel(const DLGrad g) {
-  __shared__ float red[4][16][17];
-  __shared__ float dbr[4][16];
+__global__ __launch_bounds__(512) void dl_mlp_dw_kernel(const DLGrad g) {
+  __shared__ float red[8][16][17];
+  __shared__ float dbr[8][16];
   const int bid = blockIdx.x;
   int l = 0;
   while (l + 1 < g.nl && bid >= g.tile_start[l + 1]) ++l;
@@ -577,26 +609,36 @@ __global__ __launch_bounds__(256) void dl_mlp_dw_kernel(const DLGrad g) {
   const bool uok = u < U, iok = i < I, want_db = it == 0;
   dl_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   float dbs = 0.f;
-  // wave w takes rows [16 q, 16 q + 16) for q = w, w + 4, ...; two row
-  // chunks per trip so eight loads are in flight before the MFMAs
-  for (int r16 = wave * 16; r16 < B; r16 += 128) {
-    float4 x[2], y[2];
+  // wave w takes the 16-row chunks q = w, w + 8, ...; a 4-deep ring of
+  // chunk loads keeps the L2 latency behind the MFMAs
+  const int nq = (B + 15) >> 4;
+  auto ld = [&](int q, float4& x, float4& y) {
+    const int rr = q * 16 + g4;
+    x.x = (rr < B && uok) ? dz[(long long)rr * U + u] : 0.f;
+    x.y = (rr + 1 < B && uok) ? dz[(long long)(rr + 1) * U + u] : 0.f;
+    x.z = (rr + 2 < B && uok) ? dz[(long long)(rr + 2) * U + u] : 0.f;
+    x.w = (rr + 3 < B && uok) ? dz[(long long)(rr + 3) * U + u] : 0.f;
+    y.x = (rr < B && iok) ? a[(long long)rr * I + i] : 0.f;
+    y.y = (rr + 1 < B && iok) ? a[(long long)(rr + 1) * I + i] : 0.f;
+    y.z = (rr + 2 < B && iok) ? a[(long long)(rr + 2) * I + i] : 0.f;
+    y.w = (rr + 3 < B && iok) ? a[(long long)(rr + 3) * I + i] : 0.f;
+  };
+  float4 xq[4], yq[4];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int rr = r16 + 64 * h + g4;
-      x[h].x = (rr < B && uok) ? dz[(long long)rr * U + u] : 0.f;
-      x[h].y = (rr + 1 < B && uok) ? dz[(long long)(rr + 1) * U + u] : 0.f;
-      x[h].z = (rr + 2 < B && uok) ? dz[(long long)(rr + 2) * U + u] : 0.f;
-      x[h].w = (rr + 3 < B && uok) ? dz[(long long)(rr + 3) * U + u] : 0.f;
-      y[h].x = (rr < B && iok) ? a[(long long)rr * I + i] : 0.f;
-      y[h].y = (rr + 1 < B && iok) ? a[(long long)(rr + 1) * I + i] : 0.f;
-      y[h].z = (rr + 2 < B && iok) ? a[(long long)(rr + 2) * I + i] : 0.f;
-      y[h].w = (rr + 3 < B && iok) ? a[(long long)(rr + 3) * I + i] : 0.f;
-    }
+  for (int d = 0; d < 4; ++d) {
+    const int q = wave + 8 * d;
+    if (q < nq) ld(q, xq[d], yq[d]);
+    else xq[d] = yq[d] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  for (int qb = wave; qb < nq; qb += 32) {
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      acc = dl_mfma4(x[h], y[h], acc);
-      if (want_db) dbs += (x[h].x + x[h].y) + (x[h].z + x[h].w);
+    for (int d = 0; d < 4; ++d) {
+      const int q = qb + 8 * d;
+      if (q < nq) {
+        acc = dl_mfma4(xq[d], yq[d], acc);
+        if (want_db) dbs += (xq[d].x + xq[d].y) + (xq[d].z + xq[d].w);
+        if (q + 32 < nq) ld(q + 32, xq[d], yq[d]);
+      }
     }
   }
   // C[m = u][n = i]: this lane holds u = ut*16 + g4 + r, i = it*16 + c16
@@ -608,12 +650,21 @@ __global__ __launch_bounds__(256) void dl_mlp_dw_kernel(const DLGrad g) {
     if (lane < 16) dbr[wave][lane] = dbs;
   }
   __syncthreads();
-  const int t = threadIdx.x, m = t >> 4, n = t & 15;
-  const int uu = ut * 16 + m, ii = it * 16 + n;
-  if (uu < U && ii < I)
-    g.dW[l][(long long)uu * I + ii] = (red[0][m][n] + red[1][m][n]) + (red[2][m][n] + red[3][m][n]);
-  if (want_db && t < 16 && ut * 16 + t < U)
-    g.db[l][ut * 16 + t] = (dbr[0][t] + dbr[1][t]) + (dbr[2][t] + dbr[3][t]);
+  const int t = threadIdx.x;
+  if (t < 256) {
+    const int m = t >> 4, n = t & 15;
+    const int uu = ut * 16 + m, ii = it * 16 + n;
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) v += red[w][m][n];
+    if (uu < U && ii < I) g.dW[l][(long long)uu * I + ii] = v;
+  }
+  if (want_db && t < 16 && ut * 16 + t < U) {
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) v += dbr[w][t];
+    g.db[l][ut * 16 + t] = v;
+  }
 }
 
 struct DLUpdMulti {
@@ -795,7 +846,7 @@ int h2o_dl_mlp_step(int nl, const int* width, const int* act, const float* drop,
   }
   g.width[nl] = width[nl];
   g.tile_start[nl] = nt;
-  hipLaunchKernelGGL(dl_mlp_dw_kernel, dim3(nt), dim3(256), 0, s, g);
+  hipLaunchKernelGGL(dl_mlp_dw_kernel, dim3(nt), dim3(512), 0, s, g);
   DLUpdMulti q{};
   q.nl = nl;
   int nr = 0;

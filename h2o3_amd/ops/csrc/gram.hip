@@ -1284,12 +1284,13 @@ __device__ __forceinline__ void wg_pair(int p, int NB, int* bi, int* bj) {
 __global__ __launch_bounds__(256, 2) void glm_wide_gram_kernel(const float* __restrict__ X, int ldx, int P,
                                                                long long N, const float* __restrict__ Wr, int NB,
                                                                int npairs, int S, int fold,
-                                                               double* __restrict__ part) {
+                                                               double* __restrict__ part, int dbg) {
   extern __shared__ __bf16 wg_lds[];
   __bf16* sAh = wg_lds;
   __bf16* sAl = sAh + WG_T * WG_PITCH;
   __bf16* sBh = sAl + WG_T * WG_PITCH;
   __bf16* sBl = sBh + WG_T * WG_PITCH;
+  float* sW = reinterpret_cast<float*>(sBl + WG_T * WG_PITCH);   // the chunk's 64 row weights
   const int nblk = npairs * S;
   const int L = xcd_remap(blockIdx.x, nblk);
   const int sl = L / npairs, pr = L - sl * npairs;
@@ -1308,24 +1309,24 @@ __global__ __launch_bounds__(256, 2) void glm_wide_gram_kernel(const float* __re
   const float fillA = gcA == P ? 1.f : 0.f, fillB = gcB == P ? 1.f : 0.f;
   const bool inA = gcA < P, inB = gcB < P;
   float xr[8][8];
+  float wpre = 0.f;
+  // issue-only: the raw values land in xr / wpre while this chunk's MFMAs
+  // run; the column fill and the row weights are applied in store()
   auto load = [&](long long c) {
     const long long row0 = c * WG_KR;
     const int nr = (int)((N - row0) < WG_KR ? (N - row0) : WG_KR);
     const __amdgpu_buffer_rsrc_t rx =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(X + row0 * ldx), (short)0, nr * ldx * 4, 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc((void*)(X + row0 * ldx), (short)0, (dbg & 1) ? 0 : nr * ldx * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)(Wr + row0), (short)0, nr * 4, 0x00020000);
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const int pan = q >> 2;
       const int rg = (t7 + 2 * q) & 7;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int rr = rg * 8 + e;
-        float x = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rx, (pan ? gcB : gcA) * 4, rr * ldx * 4, 0));
-        x = (pan ? inB : inA) ? x : (pan ? fillB : fillA);
-        if (!pan) x *= rr < nr ? Wr[row0 + rr] : 0.f;
-        xr[q][e] = x;
-      }
+      for (int e = 0; e < 8; ++e)
+        xr[q][e] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rx, (pan ? gcB : gcA) * 4, (rg * 8 + e) * ldx * 4, 0));
     }
+    if (tid < WG_KR) wpre = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rw, tid * 4, 0, 0));  // 0 past N
   };
   auto store = [&]() {
 #pragma unroll
@@ -1334,8 +1335,10 @@ __global__ __launch_bounds__(256, 2) void glm_wide_gram_kernel(const float* __re
       bf16x8 h, l;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        h[e] = (__bf16)xr[q][e];
-        l[e] = (__bf16)(xr[q][e] - (float)h[e]);
+        float x = (pan ? inB : inA) ? xr[q][e] : (pan ? fillB : fillA);
+        if (!pan) x *= sW[rg * 8 + e];
+        h[e] = (__bf16)x;
+        l[e] = (__bf16)(x - (float)h[e]);
       }
       const int off = col * WG_PITCH + rg * 8;
       *reinterpret_cast<bf16x8*>((pan ? sBh : sAh) + off) = h;
@@ -1365,7 +1368,9 @@ __global__ __launch_bounds__(256, 2) void glm_wide_gram_kernel(const float* __re
   if (c < nchunk) load(c);
   int since = 0;
   while (c < nchunk) {
-    __syncthreads();  // the previous chunk's operand reads are done
+    __syncthreads();  // the previous chunk's operand / weight reads are done
+    if (tid < WG_KR) sW[tid] = wpre;
+    __syncthreads();
     store();
     __syncthreads();
     const long long cn = c + S;
@@ -1407,19 +1412,187 @@ __global__ __launch_bounds__(256, 2) void glm_wide_gram_kernel(const float* __re
 // part: [npairs * S][128][128] f64, zeroed by the caller; slot L holds
 // pair L % npairs (bi <= bj, row-major over the upper triangle of the NB x NB
 // tile grid) for slice L / npairs.  NB = ceil((P + 1) / 128).
+// dbg bit 0 (timing only): the X descriptor gets zero records, so every X
+// load is dropped by the range check while the instruction stream stays.
 extern "C" int h2o_glm_wide_gram(const float* X, int ldx, int P, long long N, const float* Wr, int S, int fold,
-                                 double* part, hipStream_t s) {
+                                 double* part, int dbg, hipStream_t s) {
   if (N <= 0) return 0;
   if (ldx < P || S <= 0 || fold <= 0) return -1;
   const int NB = (P + 1 + WG_T - 1) / WG_T;
   const int npairs = NB * (NB + 1) / 2;
-  const size_t lds = 4 * WG_T * WG_PITCH * sizeof(__bf16);
+  const size_t lds = 4 * WG_T * WG_PITCH * sizeof(__bf16) + WG_KR * sizeof(float);
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)glm_wide_gram_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
   hipLaunchKernelGGL(glm_wide_gram_kernel, dim3(npairs * S), dim3(256), lds, s, X, ldx, P, N, Wr, NB, npairs, S, fold,
-                     part);
+                     part, dbg);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// 256 x 256 tile version (default): one workgroup of 8 waves per CU, each
+// wave a 128 x 64 piece on v_mfma_f32_32x32x16_bf16 (8 accumulators of 16
+// registers).  Per 32-row chunk a wave reads 24 KB of operands from LDS for
+// 48 MFMAs (1536 cycles): 62 B/clk per CU at two waves per SIMD, half the
+// LDS bandwidth -- the 128 x 128 version above reads 1.4x the operand bytes
+// per MFMA cycle and is LDS-bound (PMC: MFMA busy 31%, 8.6e8 bank-conflict
+// cycles).  Diagonal tiles skip their lower-left quarter (the transpose of
+// the upper-right one).
+// ---------------------------------------------------------------------------
+#define WG2_T 256
+#define WG2_KR 32
+#define WG2_PITCH 40
+
+__global__ __launch_bounds__(512, 1) void glm_wide_gram256_kernel(const float* __restrict__ X, int ldx, int P,
+                                                                  long long N, const float* __restrict__ Wr, int NB,
+                                                                  int npairs, int S, int fold,
+                                                                  double* __restrict__ part, int dbg) {
+  extern __shared__ __bf16 wg2_lds[];
+  __bf16* sAh = wg2_lds;
+  __bf16* sAl = sAh + WG2_T * WG2_PITCH;
+  __bf16* sBh = sAl + WG2_T * WG2_PITCH;
+  __bf16* sBl = sBh + WG2_T * WG2_PITCH;
+  float* sW = reinterpret_cast<float*>(sBl + WG2_T * WG2_PITCH);
+  const int nblk = npairs * S;
+  const int L = xcd_remap(blockIdx.x, nblk);
+  const int sl = L / npairs, pr = L - sl * npairs;
+  int bi, bj;
+  wg_pair(pr, NB, &bi, &bj);
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int mi = wv >> 2, nq = wv & 3;      // rows 128 mi .., columns 64 nq ..
+  const bool skip = bi == bj && mi == 1 && nq < 2;  // lower-left quarter of a diagonal tile
+  const long long nchunk = (N + WG2_KR - 1) / WG2_KR;
+  // loader: thread = column tid & 255 of panel (q >> 1), row groups
+  // ((tid >> 8) + 2 q) & 3 -- wave-uniform
+  const int t8 = __builtin_amdgcn_readfirstlane(tid >> 8);
+  const int colb = tid & 255;
+  const int gcA = bi * WG2_T + colb, gcB = bj * WG2_T + colb;
+  const float fillA = gcA == P ? 1.f : 0.f, fillB = gcB == P ? 1.f : 0.f;
+  const bool inA = gcA < P, inB = gcB < P;
+  float xr[4][8];
+  float wpre = 0.f;
+  auto load = [&](long long c) {
+    const long long row0 = c * WG2_KR;
+    const int nr = (int)((N - row0) < WG2_KR ? (N - row0) : WG2_KR);
+    const __amdgpu_buffer_rsrc_t rx =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(X + row0 * ldx), (short)0, (dbg & 1) ? 0 : nr * ldx * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)(Wr + row0), (short)0, nr * 4, 0x00020000);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int pan = q >> 1, rg = (t8 + 2 * q) & 3;
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        xr[q][e] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rx, (pan ? gcB : gcA) * 4, (rg * 8 + e) * ldx * 4, 0));
+    }
+    if (tid < WG2_KR) wpre = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rw, tid * 4, 0, 0));
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int pan = q >> 1, rg = (t8 + 2 * q) & 3;
+      bf16x8 h, l;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float x = (pan ? inB : inA) ? xr[q][e] : (pan ? fillB : fillA);
+        if (!pan) x *= sW[rg * 8 + e];
+        h[e] = (__bf16)x;
+        l[e] = (__bf16)(x - (float)h[e]);
+      }
+      const int off = colb * WG2_PITCH + rg * 8;
+      *reinterpret_cast<bf16x8*>((pan ? sBh : sAh) + off) = h;
+      *reinterpret_cast<bf16x8*>((pan ? sBl : sAl) + off) = l;
+    }
+  };
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  double* my = part + (size_t)L * (WG2_T * WG2_T);
+  auto fold_out = [&]() {
+    // opaque copies: the 128 fold addresses are not loop-invariant for the
+    // compiler, so they are not hoisted out of the chunk loop into registers
+    double* mb = my;
+    int ln = lane;
+    asm volatile("" : "+s"(mb), "+v"(ln));
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          // 32x32 C layout: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
+          const int i = 128 * mi + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * (ln >> 5);
+          const int j = 64 * nq + 32 * b + (ln & 31);
+          gbl_add(mb + i * WG2_T + j, (double)acc[a][b][r]);   // no-return atomic: nothing to hold in registers
+          acc[a][b][r] = 0.f;
+        }
+        __builtin_amdgcn_sched_barrier(0);   // one accumulator at a time: no hoisting across them
+      }
+  };
+  long long c = sl;
+  if (c < nchunk) load(c);
+  int since = 0;
+  while (c < nchunk) {
+    __syncthreads();
+    if (tid < WG2_KR) sW[tid] = wpre;
+    __syncthreads();
+    store();
+    __syncthreads();
+    const long long cn = c + S;
+    if (cn < nchunk) load(cn);
+    if (!skip) {
+#pragma unroll
+      for (int ks = 0; ks < WG2_KR / 16; ++ks) {
+        const int ko = ks * 16 + 8 * (lane >> 5);
+        bf16x8 ah[4], al[4];
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          const int off = (128 * mi + 32 * a + (lane & 31)) * WG2_PITCH + ko;
+          ah[a] = *reinterpret_cast<const bf16x8*>(sAh + off);
+          al[a] = *reinterpret_cast<const bf16x8*>(sAl + off);
+        }
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const int off = (64 * nq + 32 * b + (lane & 31)) * WG2_PITCH + ko;
+          const bf16x8 bh = *reinterpret_cast<const bf16x8*>(sBh + off);
+          const bf16x8 bl = *reinterpret_cast<const bf16x8*>(sBl + off);
+#pragma unroll
+          for (int a = 0; a < 4; ++a) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bh, acc[a][b], 0, 0, 0);
+#pragma unroll
+          for (int a = 0; a < 4; ++a) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bl, acc[a][b], 0, 0, 0);
+#pragma unroll
+          for (int a = 0; a < 4; ++a) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[a], bh, acc[a][b], 0, 0, 0);
+        }
+      }
+    }
+    if (++since == fold) {
+      if (!skip) fold_out();
+      since = 0;
+    }
+    c = cn;
+  }
+  if (since && !skip) fold_out();
+}
+
+extern "C" int h2o_glm_wide_gram256(const float* X, int ldx, int P, long long N, const float* Wr, int S, int fold,
+                                    double* part, int dbg, hipStream_t s) {
+  if (N <= 0) return 0;
+  if (ldx < P || S <= 0 || fold <= 0) return -1;
+  const int NB = (P + 1 + WG2_T - 1) / WG2_T;
+  const int npairs = NB * (NB + 1) / 2;
+  const size_t lds = 4 * WG2_T * WG2_PITCH * sizeof(__bf16) + WG2_KR * sizeof(float);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)glm_wide_gram256_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    attr = true;
+  }
+  hipLaunchKernelGGL(glm_wide_gram256_kernel, dim3(npairs * S), dim3(512), lds, s, X, ldx, P, N, Wr, NB, npairs, S,
+                     fold, part, dbg);
   return (int)hipGetLastError();
 }

@@ -25,7 +25,8 @@ def _lib():
         lib.h2o_glm_irls_chunk.argtypes = [I]
         lib.h2o_gram_split.argtypes = [P, I, I, I, P, P, LL, P, P]
         lib.h2o_glm_wide_split.argtypes = [P, I, I, I, LL, P, F, P, P, P, I, I, F, F, P, P, I, P, P, P]
-        lib.h2o_glm_wide_gram.argtypes = [P, I, I, LL, P, I, I, P, P]
+        lib.h2o_glm_wide_gram.argtypes = [P, I, I, LL, P, I, I, P, I, P]
+        lib.h2o_glm_wide_gram256.argtypes = [P, I, I, LL, P, I, I, P, I, P]
         lib._typed = True
     return lib
 
@@ -323,23 +324,48 @@ def wide_fused_enabled():
     return os.environ.get("H2O3_GLM_WIDE_FUSED", "1") != "0"
 
 
-def _wide_gram_assemble(part, S, NB, P):
+def _wide_gram_assemble(part, S, NB, P, T=128):
     """Sum the slices' f64 tile partials and mirror the upper-triangle tiles
-    into the full (P + 2)^2 Gram (the z column left 0)."""
-    T = part.view(S, -1, 128, 128).sum(0)
-    npairs = T.shape[0]
+    into the full (P + 2)^2 Gram (the z column left 0).  T = 256 tiles: the
+    kernel skipped the lower-left quarter of diagonal tiles (taken here from
+    the upper-right one)."""
+    Tt = part.view(S, -1, T, T).sum(0)
+    npairs = Tt.shape[0]
     bi = torch.tensor([i for i in range(NB) for _ in range(i, NB)], device=part.device)
     bj = torch.tensor([j for i in range(NB) for j in range(i, NB)], device=part.device)
     assert bi.numel() == npairs
-    dg = bi == bj                        # diagonal tiles: both halves computed, symmetrize
-    T[dg] = 0.5 * (T[dg] + T[dg].transpose(1, 2))
-    G = torch.zeros((NB * 128, NB * 128), dtype=torch.float64, device=part.device)
-    Gt = G.view(NB, 128, NB, 128).permute(0, 2, 1, 3)
-    Gt[bj, bi] = T.transpose(1, 2)
-    Gt[bi, bj] = T
+    dg = bi == bj                        # diagonal tiles: symmetrize
+    D = Tt[dg]
+    if T == 256:
+        D[:, 128:, :128] = D[:, :128, 128:].transpose(1, 2)
+    Tt[dg] = 0.5 * (D + D.transpose(1, 2))
+    G = torch.zeros((NB * T, NB * T), dtype=torch.float64, device=part.device)
+    Gt = G.view(NB, T, NB, T).permute(0, 2, 1, 3)
+    Gt[bj, bi] = Tt.transpose(1, 2)
+    Gt[bi, bj] = Tt
     out = torch.zeros((P + 2, P + 2), dtype=torch.float64, device=part.device)
     out[:P + 1, :P + 1] = G[:P + 1, :P + 1]
     return out
+
+
+def wide_gram(X, P, wr, stream=None):
+    """[X | 1]' diag(wr) [X | 1] (f64, (P + 2)^2 with a zero z column) by the
+    hand-written MFMA kernel: 256 x 256 tiles (glm_wide_gram256_kernel,
+    default) or 128 x 128 (H2O3_WIDE_TILE=128, glm_wide_gram_kernel)."""
+    lib = _lib()
+    N, ldx = X.shape
+    T = int(os.environ.get("H2O3_WIDE_TILE", 256))
+    NB = -(-(P + 1) // T)
+    npairs = NB * (NB + 1) // 2
+    per_cu = 1 if T == 256 else 2
+    S = int(os.environ.get("H2O3_WIDE_SLICES", 0)) or max(1, 256 * per_cu // npairs)
+    part = torch.zeros((npairs * S, T, T), dtype=torch.float64, device=X.device)
+    stream = stream or ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    fn = lib.h2o_glm_wide_gram256 if T == 256 else lib.h2o_glm_wide_gram
+    rc = fn(_ptr(X), ldx, P, N, _ptr(wr), S, 1024, _ptr(part), 0, stream)
+    if rc != 0:
+        raise RuntimeError(f"h2o_glm_wide_gram failed: {rc}")
+    return _wide_gram_assemble(part, S, NB, P, T)
 
 
 def glm_wide_irls(X, P, beta, b0, y, wprior=None, offset=None, codes=(1, 1), tvp=0.0, theta=1e-10, step=1 << 19,
@@ -384,14 +410,7 @@ def glm_wide_irls(X, P, beta, b0, y, wprior=None, offset=None, codes=(1, 1), tvp
                                         blocks, _ptr(gbuf), offp(wr, a), stream)
             if rc != 0:
                 raise RuntimeError(f"h2o_glm_wide_split failed: {rc}")
-        NB = -(-(P + 1) // 128)
-        npairs = NB * (NB + 1) // 2
-        S = max(1, 512 // npairs)
-        part = torch.zeros((npairs * S, 128, 128), dtype=torch.float64, device=X.device)
-        rc = lib.h2o_glm_wide_gram(_ptr(X), ldx, P, N, _ptr(wr), S, 1024, _ptr(part), stream)
-        if rc != 0:
-            raise RuntimeError(f"h2o_glm_wide_gram failed: {rc}")
-        return _wide_gram_assemble(part, S, NB, P), dev.sum(), gbuf.sum(0)
+        return wide_gram(X, P, wr, stream), dev.sum(), gbuf.sum(0)
     grp = min(nch, _WIDE_GROUP)
     HL = torch.empty((grp * st, 2 * Pa), dtype=torch.bfloat16, device=X.device)
     blocks = 2048

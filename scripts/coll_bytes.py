@@ -42,6 +42,8 @@ def main():
     rows_local = a.rows // W + (1 if r < a.rows % W else 0)
     args = SimpleNamespace(cols=a.cols, cat_cols=a.cat_cols, cat_card=a.cat_card)
     fr, names, _ = bench.make_frame(args, dev, r, rows_local)
+    if r == 0:
+        print(f"frame ready: {rows_local} local rows x {a.cols} cols on {W} ranks", flush=True)
     if a.algo == "gbm":
         from h2o3_amd.models.tree.gbm import GBMDriver, H2OGradientBoostingEstimator
         est = H2OGradientBoostingEstimator(ntrees=500, max_depth=8, seed=42, histogram_type="QuantilesGlobal",
@@ -56,6 +58,8 @@ def main():
         spec = TrainSpec(fr, names, "y")
         est._spec = spec
         drv = DRFDriver(est, spec)
+    if r == 0:
+        print("binned; growing trees", flush=True)
     trees = []
     for t in range(a.trees):
         coll.reset_bytes()

@@ -4,8 +4,11 @@ H2O3_GI_DBG (bit0 skip MFMA, bit1 skip HBM loads), H2O3_MB_GRAD (0: no
 gradient channel, 1: f32 products, 2: f64 products)."""
 import os
 import sys
+
 import torch
-from h2o3_amd.ops import linalg_ops
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from h2o3_amd.ops import linalg_ops  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 100_000_000
 ldx = int(sys.argv[2]) if len(sys.argv) > 2 else 100

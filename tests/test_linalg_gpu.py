@@ -389,13 +389,16 @@ def test_wide_split_gemm_overlap_matches_sequential(monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,P", [(100, 1000), (200_003, 1000), (70_001, 127), (5_000, 128)])
-def test_glm_wide_fused_gram_matches_fp64(n, P):
+@pytest.mark.parametrize("tile", [256, 128])
+@pytest.mark.parametrize("n,P", [(100, 1000), (200_003, 1000), (70_001, 127), (5_000, 255), (9_000, 300)])
+def test_glm_wide_fused_gram_matches_fp64(n, P, tile, monkeypatch):
     """glm_wide_gram_kernel alone: [X | 1]' W [X | 1] from the f32 rows vs
     fp64, at widths that fill 8 column tiles (P = 1000, the BASELINE wide
     config's width), exactly one tile with and without the intercept spilling
     into a second (127 / 128), with fewer chunks than slices (n = 100) and a
-    ragged last chunk."""
+    ragged last chunk; both tile sizes (256: the default, diagonal tiles
+    skip their lower-left quarter)."""
+    monkeypatch.setenv("H2O3_WIDE_TILE", str(tile))
     g = torch.Generator().manual_seed(n + P)
     X = torch.randn(n, P, generator=g)
     X[:, :3] *= 40.0                                # columns of very different scale

@@ -870,8 +870,8 @@ def test_drf_pair_path_narrow_scoring_and_posv_same_trees(classify, monkeypatch)
         np.testing.assert_allclose(np.asarray(t0.value), np.asarray(t1.value), rtol=1e-9, atol=1e-12)
 
 
-@pytest.mark.parametrize("mode", [0, 1])
-def test_pair_narrow_scoring_matches_torch_reference(mode):
+@pytest.mark.parametrize("weighted", [False, True])
+def test_pair_narrow_scoring_matches_torch_reference(weighted):
     """The DRF device pair path with narrow bins (h2o_pair_hist4b leaves each
     pair's bins past its feature's own codes unwritten; cat_pair_kernel and
     pair_select2 scan only [0, nbins_f) + NA) picks, per node, the gain,
@@ -900,10 +900,8 @@ def test_pair_narrow_scoring_matches_torch_reference(mode):
     eff = torch.randn(1000, generator=g, device="cuda")
     y = feats[0].nan_to_num(0) + 0.5 * feats[2].nan_to_num(0) + eff[c.clamp_min(0).long()] + \
         0.3 * torch.randn(n, generator=g, device="cuda")
-    if mode == 0:
-        va, vb = y, None
-    else:
-        va, vb = y, torch.rand(n, generator=g, device="cuda") + 0.5
+    mode = 0
+    va, vb = y, (torch.rand(n, generator=g, device="cuda") + 0.5 if weighted else None)
     gr = TreeGrower(bd, GrowParams(min_rows=5, seed=3))
     assert gr._narrow_bins() is not None
     gr._vmax = tree_ops.channel_max(va, vb, mode)
@@ -922,6 +920,7 @@ def test_pair_narrow_scoring_matches_torch_reference(mode):
         H[f, i] = Hr[p_]
         allowed[i, f] = True
     ref = gr._find_splits_torch(H[:F], allowed[:, :F], node_wyy=wr)
+    assert bool(torch.isfinite(ref["gain"]).all())
     torch.testing.assert_close(res["gain"].cpu(), ref["gain"].cpu().to(torch.float64), rtol=1e-6, atol=1e-6)
     assert res["feat"].cpu().tolist() == ref["feat"].cpu().tolist()
     num = res["feat"].cpu() != 7                       # numeric winners: the same threshold bin
