@@ -630,8 +630,9 @@ class GLMDriver:
                     self._gexact = gx[:P + 1]
                     self._gbeta = np.concatenate([self.beta[:P].astype(np.float32).astype(np.float64),
                                                   [float(np.float32(self.beta[-1]))]])
-            return self._finish_stats(Gf[:P, :P], Gf[:P, P + 1].contiguous(), Gf[:P, P].contiguous(),
-                                      Gf[P, P].view(1), Gf[P, P + 1].view(1), dev.view(1))
+            with phase("glm.finish"):
+                return self._finish_stats(Gf[:P, :P], Gf[:P, P + 1].contiguous(), Gf[:P, P].contiguous(),
+                                          Gf[P, P].view(1), Gf[P, P + 1].view(1), dev.view(1))
         with phase("glm.eta"):
             eta = self._eta()
         with phase("glm.weights"):
@@ -791,7 +792,8 @@ class GLMDriver:
         """One IRLS iteration (Gram on the matrix cores + host solve)."""
         Ga, b, dev = self._irls_stats()
         self._stats_dev = dev
-        Ga, b = self._check_tier(Ga, b)
+        with phase("glm.tier"):
+            Ga, b = self._check_tier(Ga, b)
         dev = self._stats_dev
         r = self.obj_reg
         Gn, bn, l1, l2 = self._system(Ga, b)

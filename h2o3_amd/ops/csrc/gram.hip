@@ -1367,6 +1367,7 @@ __global__ __launch_bounds__(256, 2) void glm_wide_gram_kernel(const float* __re
   long long c = sl;
   if (c < nchunk) load(c);
   int since = 0;
+  long long cfold = c + (long long)fold * S;   // fold once the chunk index passes this
   while (c < nchunk) {
     __syncthreads();  // the previous chunk's operand / weight reads are done
     if (tid < WG_KR) sW[tid] = wpre;
@@ -1400,11 +1401,13 @@ __global__ __launch_bounds__(256, 2) void glm_wide_gram_kernel(const float* __re
         for (int a = 0; a < 4; ++a) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[a], bh, acc[a][b], 0, 0, 0);
       }
     }
-    if (++since == fold) {
+    ++since;
+    c = cn;
+    if (c >= cfold) {
       fold_out();
       since = 0;
+      cfold = c + (long long)fold * S;
     }
-    c = cn;
   }
   if (since) fold_out();
 }
@@ -1434,27 +1437,29 @@ extern "C" int h2o_glm_wide_gram(const float* X, int ldx, int P, long long N, co
 // ---------------------------------------------------------------------------
 // 256 x 256 tile version (default): one workgroup of 8 waves per CU, each
 // wave a 128 x 64 piece on v_mfma_f32_32x32x16_bf16 (8 accumulators of 16
-// registers).  Per 32-row chunk a wave reads 24 KB of operands from LDS for
-// 48 MFMAs (1536 cycles): 62 B/clk per CU at two waves per SIMD, half the
-// LDS bandwidth -- the 128 x 128 version above reads 1.4x the operand bytes
-// per MFMA cycle and is LDS-bound (PMC: MFMA busy 31%, 8.6e8 bank-conflict
-// cycles).  Diagonal tiles skip their lower-left quarter (the transpose of
-// the upper-right one).
+// registers).  LDS holds two chunk buffers: while the MFMAs read chunk t,
+// the same waves convert and store chunk t + 1 (its f32 values arrived in
+// registers during the previous chunk) into the other buffer -- one barrier
+// per chunk, and the VALU conversion interleaves with the MFMA stream
+// instead of running in a phase of its own (PMC of the single-buffer
+// version: MFMA busy 36%, 35% of wave cycles parked at barriers / waits).
+// Columns are stored k-contiguous, pitch 32 bf16, with the 8-row k-blocks
+// XOR-swizzled by (column >> 2) & 3: conflict-free b128 stores and operand
+// reads.  Diagonal tiles skip their lower-left quarter (the transpose of the
+// upper-right one).
 // ---------------------------------------------------------------------------
 #define WG2_T 256
 #define WG2_KR 32
-#define WG2_PITCH 40
+#define WG2_BUF (4 * WG2_T * WG2_KR)   // bf16 per chunk buffer (A hi, A lo, B hi, B lo)
+
+__device__ __forceinline__ int wg2_off(int col, int kb) { return col * WG2_KR + ((kb ^ ((col >> 2) & 3)) << 3); }
 
 __global__ __launch_bounds__(512, 1) void glm_wide_gram256_kernel(const float* __restrict__ X, int ldx, int P,
                                                                   long long N, const float* __restrict__ Wr, int NB,
                                                                   int npairs, int S, int fold,
                                                                   double* __restrict__ part, int dbg) {
   extern __shared__ __bf16 wg2_lds[];
-  __bf16* sAh = wg2_lds;
-  __bf16* sAl = sAh + WG2_T * WG2_PITCH;
-  __bf16* sBh = sAl + WG2_T * WG2_PITCH;
-  __bf16* sBl = sBh + WG2_T * WG2_PITCH;
-  float* sW = reinterpret_cast<float*>(sBl + WG2_T * WG2_PITCH);
+  float* sW = reinterpret_cast<float*>(wg2_lds + 2 * WG2_BUF);   // [2][32] row weights
   const int nblk = npairs * S;
   const int L = xcd_remap(blockIdx.x, nblk);
   const int sl = L / npairs, pr = L - sl * npairs;
@@ -1464,6 +1469,8 @@ __global__ __launch_bounds__(512, 1) void glm_wide_gram256_kernel(const float* _
   const int mi = wv >> 2, nq = wv & 3;      // rows 128 mi .., columns 64 nq ..
   const bool skip = bi == bj && mi == 1 && nq < 2;  // lower-left quarter of a diagonal tile
   const long long nchunk = (N + WG2_KR - 1) / WG2_KR;
+  // chunks of this slice: c = sl + t S, t = 0 .. nt - 1
+  const long long nt = sl < nchunk ? (nchunk - 1 - sl) / S + 1 : 0;
   // loader: thread = column tid & 255 of panel (q >> 1), row groups
   // ((tid >> 8) + 2 q) & 3 -- wave-uniform
   const int t8 = __builtin_amdgcn_readfirstlane(tid >> 8);
@@ -1473,12 +1480,12 @@ __global__ __launch_bounds__(512, 1) void glm_wide_gram256_kernel(const float* _
   const bool inA = gcA < P, inB = gcB < P;
   float xr[4][8];
   float wpre = 0.f;
-  auto load = [&](long long c) {
-    const long long row0 = c * WG2_KR;
-    const int nr = (int)((N - row0) < WG2_KR ? (N - row0) : WG2_KR);
+  auto load_x = [&](long long t) {
+    const long long row0 = (sl + t * S) * WG2_KR;
+    const long long left = N - row0;
+    const int nr = (int)(left < WG2_KR ? (left > 0 ? left : 0) : WG2_KR);   // past N: every load reads 0
     const __amdgpu_buffer_rsrc_t rx =
         __builtin_amdgcn_make_buffer_rsrc((void*)(X + row0 * ldx), (short)0, (dbg & 1) ? 0 : nr * ldx * 4, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)(Wr + row0), (short)0, nr * 4, 0x00020000);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int pan = q >> 1, rg = (t8 + 2 * q) & 3;
@@ -1486,24 +1493,33 @@ __global__ __launch_bounds__(512, 1) void glm_wide_gram256_kernel(const float* _
       for (int e = 0; e < 8; ++e)
         xr[q][e] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rx, (pan ? gcB : gcA) * 4, (rg * 8 + e) * ldx * 4, 0));
     }
-    if (tid < WG2_KR) wpre = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rw, tid * 4, 0, 0));
   };
-  auto store = [&]() {
+  auto load_w = [&](long long t) -> float {   // threads < 32: the chunk's row weight (0 past N)
+    const long long row0 = (sl + t * S) * WG2_KR;
+    const long long left = N - row0;
+    const int nr = (int)(left < WG2_KR ? (left > 0 ? left : 0) : WG2_KR);
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)(Wr + row0), (short)0, nr * 4, 0x00020000);
+    return __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rw, tid * 4, 0, 0));
+  };
+  auto store_q = [&](int buf, int q) {
+    __bf16* base = wg2_lds + buf * WG2_BUF;
+    const float* w = sW + buf * WG2_KR;
+    const int pan = q >> 1, rg = (t8 + 2 * q) & 3;
+    bf16x8 h, l;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int pan = q >> 1, rg = (t8 + 2 * q) & 3;
-      bf16x8 h, l;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        float x = (pan ? inB : inA) ? xr[q][e] : (pan ? fillB : fillA);
-        if (!pan) x *= sW[rg * 8 + e];
-        h[e] = (__bf16)x;
-        l[e] = (__bf16)(x - (float)h[e]);
-      }
-      const int off = colb * WG2_PITCH + rg * 8;
-      *reinterpret_cast<bf16x8*>((pan ? sBh : sAh) + off) = h;
-      *reinterpret_cast<bf16x8*>((pan ? sBl : sAl) + off) = l;
+    for (int e = 0; e < 8; ++e) {
+      float x = (pan ? inB : inA) ? xr[q][e] : (pan ? fillB : fillA);
+      if (!pan) x *= w[rg * 8 + e];
+      h[e] = (__bf16)x;
+      l[e] = (__bf16)(x - (float)h[e]);
     }
+    const int off = wg2_off(colb, rg);
+    *reinterpret_cast<bf16x8*>(base + (pan ? 2 : 0) * WG2_T * WG2_KR + off) = h;
+    *reinterpret_cast<bf16x8*>(base + (pan ? 3 : 1) * WG2_T * WG2_KR + off) = l;
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) store_q(buf, q);
   };
   f32x16 acc[4][2];
 #pragma unroll
@@ -1531,52 +1547,67 @@ __global__ __launch_bounds__(512, 1) void glm_wide_gram256_kernel(const float* _
           gbl_add(mb + i * WG2_T + j, (double)acc[a][b][r]);   // no-return atomic: nothing to hold in registers
           acc[a][b][r] = 0.f;
         }
-        __builtin_amdgcn_sched_barrier(0);   // one accumulator at a time: no hoisting across them
       }
   };
-  long long c = sl;
-  if (c < nchunk) load(c);
-  int since = 0;
-  while (c < nchunk) {
-    __syncthreads();
-    if (tid < WG2_KR) sW[tid] = wpre;
-    __syncthreads();
-    store();
-    __syncthreads();
-    const long long cn = c + S;
-    if (cn < nchunk) load(cn);
-    if (!skip) {
+  // one chunk's MFMAs on buffer `buf`, with the conversion + store of the
+  // next chunk's q-th slice into buffer `nbuf` after each (ks, b) sub-step:
+  // straight-line code, so the scheduler interleaves VALU with the MFMAs
+  auto compute_store = [&](int buf, int nbuf) {
+    const __bf16* sAh = wg2_lds + buf * WG2_BUF;
+    const __bf16* sAl = sAh + WG2_T * WG2_KR;
+    const __bf16* sBh = sAl + WG2_T * WG2_KR;
+    const __bf16* sBl = sBh + WG2_T * WG2_KR;
 #pragma unroll
-      for (int ks = 0; ks < WG2_KR / 16; ++ks) {
-        const int ko = ks * 16 + 8 * (lane >> 5);
-        bf16x8 ah[4], al[4];
+    for (int ks = 0; ks < WG2_KR / 16; ++ks) {
+      const int kb = 2 * ks + (lane >> 5);
+      bf16x8 ah[4], al[4];
 #pragma unroll
-        for (int a = 0; a < 4; ++a) {
-          const int off = (128 * mi + 32 * a + (lane & 31)) * WG2_PITCH + ko;
-          ah[a] = *reinterpret_cast<const bf16x8*>(sAh + off);
-          al[a] = *reinterpret_cast<const bf16x8*>(sAl + off);
-        }
+      for (int a = 0; a < 4; ++a) {
+        const int off = wg2_off(128 * mi + 32 * a + (lane & 31), kb);
+        ah[a] = *reinterpret_cast<const bf16x8*>(sAh + off);
+        al[a] = *reinterpret_cast<const bf16x8*>(sAl + off);
+      }
 #pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          const int off = (64 * nq + 32 * b + (lane & 31)) * WG2_PITCH + ko;
-          const bf16x8 bh = *reinterpret_cast<const bf16x8*>(sBh + off);
-          const bf16x8 bl = *reinterpret_cast<const bf16x8*>(sBl + off);
+      for (int b = 0; b < 2; ++b) {
+        const int off = wg2_off(64 * nq + 32 * b + (lane & 31), kb);
+        const bf16x8 bh = *reinterpret_cast<const bf16x8*>(sBh + off);
+        const bf16x8 bl = *reinterpret_cast<const bf16x8*>(sBl + off);
 #pragma unroll
-          for (int a = 0; a < 4; ++a) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bh, acc[a][b], 0, 0, 0);
+        for (int a = 0; a < 4; ++a) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bh, acc[a][b], 0, 0, 0);
 #pragma unroll
-          for (int a = 0; a < 4; ++a) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bl, acc[a][b], 0, 0, 0);
+        for (int a = 0; a < 4; ++a) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bl, acc[a][b], 0, 0, 0);
 #pragma unroll
-          for (int a = 0; a < 4; ++a) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[a], bh, acc[a][b], 0, 0, 0);
-        }
+        for (int a = 0; a < 4; ++a) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[a], bh, acc[a][b], 0, 0, 0);
+        store_q(nbuf, 2 * ks + b);
       }
     }
-    if (++since == fold) {
-      if (!skip) fold_out();
-      since = 0;
+  };
+  if (nt == 0) return;
+  // prologue: chunk 0 in buffer 0, chunk 1's values in flight
+  if (tid < WG2_KR) sW[tid] = load_w(0);
+  load_x(0);
+  __syncthreads();
+  store(0);
+  if (tid < WG2_KR) sW[WG2_KR + tid] = nt > 1 ? load_w(1) : 0.f;
+  __syncthreads();
+  if (nt > 1) load_x(1);
+  if (tid < WG2_KR && nt > 2) wpre = load_w(2);
+  // chunk groups of `fold` with the fold between them; every chunk runs
+  // the same straight-line body (a diagonal tile's skipped quarter computes
+  // and is never folded; the store past the last chunk writes the unused
+  // buffer), so MFMA and conversion interleave within one basic block
+  for (long long t0 = 0; t0 < nt; t0 += fold) {
+    const long long t1 = t0 + fold < nt ? t0 + fold : nt;
+    for (long long t = t0; t < t1; ++t) {
+      const int cur = (int)(t & 1);
+      compute_store(cur, cur ^ 1);
+      if (tid < WG2_KR) sW[cur * WG2_KR + tid] = wpre;   // weights of chunk t + 2 (buffer cur is free after the barrier)
+      __syncthreads();
+      load_x(t + 2);
+      if (tid < WG2_KR) wpre = load_w(t + 3);
     }
-    c = cn;
+    if (!skip) fold_out();
   }
-  if (since && !skip) fold_out();
 }
 
 extern "C" int h2o_glm_wide_gram256(const float* X, int ldx, int P, long long N, const float* Wr, int S, int fold,
@@ -1585,7 +1616,7 @@ extern "C" int h2o_glm_wide_gram256(const float* X, int ldx, int P, long long N,
   if (ldx < P || S <= 0 || fold <= 0) return -1;
   const int NB = (P + 1 + WG2_T - 1) / WG2_T;
   const int npairs = NB * (NB + 1) / 2;
-  const size_t lds = 4 * WG2_T * WG2_PITCH * sizeof(__bf16) + WG2_KR * sizeof(float);
+  const size_t lds = 2 * WG2_BUF * sizeof(__bf16) + 2 * WG2_KR * sizeof(float);
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)glm_wide_gram256_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -13,7 +13,7 @@ timeout -k 10 300 python -u scripts/wide_gram_mb.py > gpurun_out/r5_wide_gram_mb
 cat gpurun_out/r5_wide_gram_mb2.txt
 timeout -k 10 300 python -u scripts/glm_wide_step_mb.py > gpurun_out/r5_wide_mb2.txt 2>&1 || { tail -20 gpurun_out/r5_wide_mb2.txt; exit 1; }
 cat gpurun_out/r5_wide_mb2.txt
-timeout -k 10 300 python -u bench.py --algo glm --rows 12500000 --cols 1000 --steps 3 --warmup 1 \
+H2O3_PROFILE=1 timeout -k 10 300 python -u bench.py --algo glm --rows 12500000 --cols 1000 --steps 6 --warmup 1 \
   > gpurun_out/r5_glm_wide2.json 2> gpurun_out/r5_glm_wide2.err || { tail -20 gpurun_out/r5_glm_wide2.err; exit 1; }
 cat gpurun_out/r5_glm_wide2.json
 timeout -s KILL 150 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE \
