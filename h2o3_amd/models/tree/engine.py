@@ -1010,22 +1010,34 @@ class TreeGrower:
         pos = start[pe] + j - ch_start[oe]                               # position in its owner's chunk
         vals = Hp.reshape(P * Bs, C)[dense_idx]                          # [E, C]
         nzm = (vals != 0).any(1)
-        dense_b = W * Lmax * C * 8
-        mx = torch.tensor([float(int(nzm.sum()) * (4 + 8 * C))], dtype=torch.float64, device=dev)
-        coll.allreduce_(mx, "max")
-        if float(mx[0]) < 0.5 * dense_b:
-            # sparse: (position, value) of the non-zero bins to their owner
+        nnz = int(nzm.sum())
+        # lossless integer transport: unweighted / bootstrap-count classification
+        # histograms hold whole numbers (w = counts, wy = class counts); when every
+        # rank's values are integers below 2^27 the level ships int32 (a sum of
+        # 8 ranks stays exact), half the bytes of f64
+        big = float(vals.abs().max()) if vals.numel() else 0.0
+        not_int = 0.0 if (big < 2.0 ** 27 and bool((vals == torch.round(vals)).all())) else 1.0
+        stat = torch.tensor([float(nnz), not_int], dtype=torch.float64, device=dev)
+        coll.allreduce_(stat, "max")
+        ints = float(stat[1]) == 0.0
+        vb_ = 4 if ints else 8
+        dense_b = W * Lmax * C * vb_
+        tdt = torch.int32 if ints else Hp.dtype
+        if float(stat[0]) * (4 + vb_ * C) < dense_b:
+            # sparse: (position, value) of the non-zero bins to their owner, when
+            # that ships fewer bytes than the dense reduce-scatter
             from ...core.dist_munge import exchange
             from ...core.vec import T_INT, T_REAL, Vec
-            got = exchange([Vec(pos[nzm].to(torch.int32), T_INT), Vec(vals[nzm].contiguous(), T_REAL)], oe[nzm])
+            vsend = vals[nzm].to(tdt).contiguous()
+            got = exchange([Vec(pos[nzm].to(torch.int32), T_INT), Vec(vsend, T_INT if ints else T_REAL)], oe[nzm])
             chunk = torch.zeros((Lmax, C), dtype=Hp.dtype, device=dev).index_add_(
                 0, got[0].data.long(), got[1].data.to(Hp.dtype))
         else:
-            buf = torch.zeros((W, Lmax, C), dtype=Hp.dtype, device=dev)
-            buf[oe, pos] = vals
-            chunk = coll.reduce_scatter_dim0(buf.view(W * Lmax, C))
+            buf = torch.zeros((W, Lmax, C), dtype=tdt, device=dev)
+            buf[oe, pos] = vals.to(tdt)
+            chunk = coll.reduce_scatter_dim0(buf.view(W * Lmax, C)).to(Hp.dtype)
         if full:
-            allc = coll.all_gather_dim0(chunk).view(W, Lmax, C)
+            allc = coll.all_gather_dim0(chunk.to(tdt)).view(W, Lmax, C).to(Hp.dtype)
             out = torch.zeros((P * Bs, C), dtype=Hp.dtype, device=dev)
             out[dense_idx] = allc[oe, pos]
             return out.view(P, Bs, C)

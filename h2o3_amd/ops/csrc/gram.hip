@@ -1454,6 +1454,7 @@ extern "C" int h2o_glm_wide_gram(const float* X, int ldx, int P, long long N, co
 
 __device__ __forceinline__ int wg2_off(int col, int kb) { return col * WG2_KR + ((kb ^ ((col >> 2) & 3)) << 3); }
 
+template <bool BF3>
 __global__ __launch_bounds__(512, 1) void glm_wide_gram256_kernel(const float* __restrict__ X, int ldx, int P,
                                                                   long long N, const float* __restrict__ Wr, int NB,
                                                                   int npairs, int S, int fold,
@@ -1511,11 +1512,11 @@ __global__ __launch_bounds__(512, 1) void glm_wide_gram256_kernel(const float* _
       float x = (pan ? inB : inA) ? xr[q][e] : (pan ? fillB : fillA);
       if (!pan) x *= w[rg * 8 + e];
       h[e] = (__bf16)x;
-      l[e] = (__bf16)(x - (float)h[e]);
+      if constexpr (BF3) l[e] = (__bf16)(x - (float)h[e]);
     }
     const int off = wg2_off(colb, rg);
     *reinterpret_cast<bf16x8*>(base + (pan ? 2 : 0) * WG2_T * WG2_KR + off) = h;
-    *reinterpret_cast<bf16x8*>(base + (pan ? 3 : 1) * WG2_T * WG2_KR + off) = l;
+    if constexpr (BF3) *reinterpret_cast<bf16x8*>(base + (pan ? 3 : 1) * WG2_T * WG2_KR + off) = l;
   };
   auto store = [&](int buf) {
 #pragma unroll
@@ -1565,19 +1566,21 @@ __global__ __launch_bounds__(512, 1) void glm_wide_gram256_kernel(const float* _
       for (int a = 0; a < 4; ++a) {
         const int off = wg2_off(128 * mi + 32 * a + (lane & 31), kb);
         ah[a] = *reinterpret_cast<const bf16x8*>(sAh + off);
-        al[a] = *reinterpret_cast<const bf16x8*>(sAl + off);
+        if constexpr (BF3) al[a] = *reinterpret_cast<const bf16x8*>(sAl + off);
       }
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
         const int off = wg2_off(64 * nq + 32 * b + (lane & 31), kb);
         const bf16x8 bh = *reinterpret_cast<const bf16x8*>(sBh + off);
-        const bf16x8 bl = *reinterpret_cast<const bf16x8*>(sBl + off);
 #pragma unroll
         for (int a = 0; a < 4; ++a) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bh, acc[a][b], 0, 0, 0);
+        if constexpr (BF3) {
+          const bf16x8 bl = *reinterpret_cast<const bf16x8*>(sBl + off);
 #pragma unroll
-        for (int a = 0; a < 4; ++a) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bl, acc[a][b], 0, 0, 0);
+          for (int a = 0; a < 4; ++a) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bl, acc[a][b], 0, 0, 0);
 #pragma unroll
-        for (int a = 0; a < 4; ++a) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[a], bh, acc[a][b], 0, 0, 0);
+          for (int a = 0; a < 4; ++a) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[a], bh, acc[a][b], 0, 0, 0);
+        }
         store_q(nbuf, 2 * ks + b);
       }
     }
@@ -1610,8 +1613,11 @@ __global__ __launch_bounds__(512, 1) void glm_wide_gram256_kernel(const float* _
   }
 }
 
+// bf3 = 0: one bf16 MFMA per product (hi * hi, ~2^-9 relative): the
+// Hessian of a well-conditioned system, whose Newton step on the exact
+// gradient still converges to the exact-gradient fixed point
 extern "C" int h2o_glm_wide_gram256(const float* X, int ldx, int P, long long N, const float* Wr, int S, int fold,
-                                    double* part, int dbg, hipStream_t s) {
+                                    double* part, int dbg, int bf3, hipStream_t s) {
   if (N <= 0) return 0;
   if (ldx < P || S <= 0 || fold <= 0) return -1;
   const int NB = (P + 1 + WG2_T - 1) / WG2_T;
@@ -1619,11 +1625,17 @@ extern "C" int h2o_glm_wide_gram256(const float* X, int ldx, int P, long long N,
   const size_t lds = 2 * WG2_BUF * sizeof(__bf16) + 2 * WG2_KR * sizeof(float);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)glm_wide_gram256_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)glm_wide_gram256_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    (void)hipFuncSetAttribute((const void*)glm_wide_gram256_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);
     attr = true;
   }
-  hipLaunchKernelGGL(glm_wide_gram256_kernel, dim3(npairs * S), dim3(512), lds, s, X, ldx, P, N, Wr, NB, npairs, S,
-                     fold, part, dbg);
+  if (bf3)
+    hipLaunchKernelGGL(glm_wide_gram256_kernel<true>, dim3(npairs * S), dim3(512), lds, s, X, ldx, P, N, Wr, NB,
+                       npairs, S, fold, part, dbg);
+  else
+    hipLaunchKernelGGL(glm_wide_gram256_kernel<false>, dim3(npairs * S), dim3(512), lds, s, X, ldx, P, N, Wr, NB,
+                       npairs, S, fold, part, dbg);
   return (int)hipGetLastError();
 }

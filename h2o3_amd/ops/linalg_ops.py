@@ -26,7 +26,7 @@ def _lib():
         lib.h2o_gram_split.argtypes = [P, I, I, I, P, P, LL, P, P]
         lib.h2o_glm_wide_split.argtypes = [P, I, I, I, LL, P, F, P, P, P, I, I, F, F, P, P, I, P, P, P]
         lib.h2o_glm_wide_gram.argtypes = [P, I, I, LL, P, I, I, P, I, P]
-        lib.h2o_glm_wide_gram256.argtypes = [P, I, I, LL, P, I, I, P, I, P]
+        lib.h2o_glm_wide_gram256.argtypes = [P, I, I, LL, P, I, I, P, I, I, P]
         lib._typed = True
     return lib
 
@@ -348,10 +348,11 @@ def _wide_gram_assemble(part, S, NB, P, T=128):
     return out
 
 
-def wide_gram(X, P, wr, stream=None):
+def wide_gram(X, P, wr, stream=None, bf3=True):
     """[X | 1]' diag(wr) [X | 1] (f64, (P + 2)^2 with a zero z column) by the
     hand-written MFMA kernel: 256 x 256 tiles (glm_wide_gram256_kernel,
-    default) or 128 x 128 (H2O3_WIDE_TILE=128, glm_wide_gram_kernel)."""
+    default) or 128 x 128 (H2O3_WIDE_TILE=128, glm_wide_gram_kernel).
+    bf3=False (256 tiles): one bf16 MFMA per product instead of three."""
     lib = _lib()
     N, ldx = X.shape
     T = int(os.environ.get("H2O3_WIDE_TILE", 256))
@@ -361,8 +362,10 @@ def wide_gram(X, P, wr, stream=None):
     S = int(os.environ.get("H2O3_WIDE_SLICES", 0)) or max(1, 256 * per_cu // npairs)
     part = torch.zeros((npairs * S, T, T), dtype=torch.float64, device=X.device)
     stream = stream or ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    fn = lib.h2o_glm_wide_gram256 if T == 256 else lib.h2o_glm_wide_gram
-    rc = fn(_ptr(X), ldx, P, N, _ptr(wr), S, 1024, _ptr(part), 0, stream)
+    if T == 256:
+        rc = lib.h2o_glm_wide_gram256(_ptr(X), ldx, P, N, _ptr(wr), S, 1024, _ptr(part), 0, int(bool(bf3)), stream)
+    else:
+        rc = lib.h2o_glm_wide_gram(_ptr(X), ldx, P, N, _ptr(wr), S, 1024, _ptr(part), 0, stream)
     if rc != 0:
         raise RuntimeError(f"h2o_glm_wide_gram failed: {rc}")
     return _wide_gram_assemble(part, S, NB, P, T)

@@ -75,6 +75,12 @@ def main():
                       "levels": dict(sorted(levels.items(), key=lambda kv: (len(kv[0]), kv[0])))})
         if r == 0:
             print(f"tree {t}: {tot / 1e6:.1f} MB handed to collectives by rank 0", flush=True)
+            for lv, ops in trees[-1]["levels"].items():
+                print(f"  {lv}: " + ", ".join(f"{op} {b / 1e6:.2f} MB" for op, b in ops.items()), flush=True)
+            # partial results survive a later failure
+            os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
+            with open(a.out + ".partial", "w") as f:
+                json.dump({"algo": a.algo, "world": W, "trees": trees}, f, indent=1)
     allr = coll.all_gather_object([tr["bytes_total"] for tr in trees])
     if r == 0:
         res = {"algo": a.algo, "rows": a.rows, "cols": a.cols, "cat_cols": a.cat_cols, "cat_card": a.cat_card,

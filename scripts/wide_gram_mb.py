@@ -1,5 +1,6 @@
 """Fused wide Gram kernels alone at 12.5M x 1000: time per launch of the
-256 x 256-tile kernel (default) and the 128 x 128 one, plus timing-only arms
+256 x 256-tile kernel (bf16x3 default, and the one-MFMA bf16 Hessian) and the
+128 x 128 one, plus timing-only arms
 whose X loads are dropped by the buffer range check (dbg=1: MFMA + LDS +
 conversion cost without HBM/L2 traffic).  argv: rows (default 12.5M)."""
 import ctypes
@@ -17,13 +18,14 @@ lib = linalg_ops._lib()
 X = torch.randn(N, P, device="cuda")
 w = torch.rand(N, device="cuda")
 stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-for T, S, dbg in ((256, 25, 0), (256, 25, 1), (256, 50, 0), (128, 14, 0), (128, 14, 1)):
+for T, S, dbg, bf3 in ((256, 25, 0, 1), (256, 25, 1, 1), (256, 25, 0, 0), (256, 25, 1, 0), (128, 14, 0, 1)):
     NB = -(-(P + 1) // T)
     npairs = NB * (NB + 1) // 2
     part = torch.zeros((npairs * S, T, T), dtype=torch.float64, device="cuda")
+    args = [ctypes.c_void_p(X.data_ptr()), P, P, N, ctypes.c_void_p(w.data_ptr()), S, 1024,
+            ctypes.c_void_p(part.data_ptr()), dbg] + ([bf3] if T == 256 else []) + [stream]
     fn = lib.h2o_glm_wide_gram256 if T == 256 else lib.h2o_glm_wide_gram
-    f = lambda: fn(ctypes.c_void_p(X.data_ptr()), P, P, N, ctypes.c_void_p(w.data_ptr()), S, 1024,  # noqa: E731
-                   ctypes.c_void_p(part.data_ptr()), dbg, stream)
+    f = lambda: fn(*args)  # noqa: E731
     assert f() == 0
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -33,4 +35,4 @@ for T, S, dbg in ((256, 25, 0), (256, 25, 1), (256, 50, 0), (128, 14, 0), (128, 
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / 3
-    print(f"T={T} S={S:3d} dbg={dbg}: {ms:7.2f} ms/launch", flush=True)
+    print(f"T={T} S={S:3d} dbg={dbg} bf3={bf3}: {ms:7.2f} ms/launch", flush=True)

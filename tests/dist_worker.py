@@ -132,7 +132,14 @@ def _drf_pairs(h2o):
     trees = [[list(map(int, t.feat)), [round(float(v), 9) if np.isfinite(v) else str(v) for v in t.thr]]
              for t in m._forest.trees]
     by = coll.bytes_report()
-    return {"trees": trees, "rmse": round(m.rmse(), 9),
+    # classification: whole-number histograms (bootstrap counts, class counts)
+    # take the lossless int32 transport
+    fr["yc"] = (fr["y"] > 0.2).asfactor()
+    mc = H2ORandomForestEstimator(ntrees=2, max_depth=10, mtries=6, seed=12, sample_rate=1.0, min_rows=2)
+    mc.train(x=[c for c in fr.names if c not in ("y", "yc")], y="yc", training_frame=fr)
+    trees_c = [[list(map(int, t.feat)), [round(float(v), 9) if np.isfinite(v) else str(v) for v in t.thr]]
+               for t in mc._forest.trees]
+    return {"trees": trees, "rmse": round(m.rmse(), 9), "trees_c": trees_c, "logloss_c": round(mc.logloss(), 9),
             "a2a_levels": sorted({k[0] for k, v in by.items() if k[1] == "all_to_all_single" and k[0].startswith("tree")})}
 
 

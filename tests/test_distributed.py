@@ -72,6 +72,9 @@ def test_drf_pair_exchange_same_trees(results):
     assert one["drf_pairs"]["trees"] == two["drf_pairs"]["trees"]
     assert one["drf_pairs"]["rmse"] == two["drf_pairs"]["rmse"]
     assert two["drf_pairs"]["a2a_levels"], "no level used the sparse exchange"
+    # classification (whole-number histograms: the int32 transport)
+    assert one["drf_pairs"]["trees_c"] == two["drf_pairs"]["trees_c"]
+    assert one["drf_pairs"]["logloss_c"] == two["drf_pairs"]["logloss_c"]
 
 
 def test_persist_sharded_state(results):
