@@ -571,10 +571,17 @@ class GLMDriver:
     # Hessian precision tiers of the Newton step beta + H^-1 g (g from the exact
     # gradient channel): the iteration contracts at rate ~ kappa * eps(H), so the
     # tier is picked from the Jacobi-scaled condition number kappa of the system
-    # matrix.  bf16x3 MFMA (eps ~ 2e-5) while kappa < 2e3, f32 MFMA (eps ~ 1e-7)
-    # while kappa < 5e5, beyond that fp64 (the reference's Gram precision,
-    # hex/gram/Gram.java:17) on the device's f64 GEMMs.
-    _TIER_LIMITS = (("bf3", 2e3), ("f32", 5e5), ("f64", float("inf")))
+    # matrix.  Plain bf16 MFMA (eps ~ 4e-3, the fused wide Gram only) while
+    # kappa < 8, bf16x3 MFMA (eps ~ 2e-5) while kappa < 2e3, f32 MFMA
+    # (eps ~ 1e-7) while kappa < 5e5, beyond that fp64 (the reference's Gram
+    # precision, hex/gram/Gram.java:17) on the device's f64 GEMMs.
+    _TIER_LIMITS = (("bf16", 8.0), ("bf3", 2e3), ("f32", 5e5), ("f64", float("inf")))
+
+    def _wide_bf16_ok(self):
+        """The plain-bf16 Hessian tier exists for the fused wide Gram only
+        (H2O3_GLM_WIDE_BF16=0 disables it)."""
+        return linalg_ops.wide_fused_enabled() and os.environ.get("H2O3_GLM_WIDE_BF16", "1") != "0" and \
+            os.environ.get("H2O3_WIDE_TILE", "256") == "256"
 
     def _tier_for(self, kappa):
         for name, lim in self._TIER_LIMITS:
@@ -623,9 +630,13 @@ class GLMDriver:
                 exact = os.environ.get("H2O3_GLM_EXACT_GRAD", "1") != "0"
                 # fused: eta pass + one hand-written MFMA Gram kernel over the f32
                 # rows (needs the exact gradient: its Gram has no z column)
+                fused = exact and linalg_ops.wide_fused_enabled()
+                # before the first condition estimate the fused path starts at the
+                # plain bf16 Hessian tier when allowed (raised at iteration 1 if kappa says so)
+                hp = self._hprec or ("bf16" if fused and self._wide_bf16_ok() else "bf3")
                 Gf, dev, gx = linalg_ops.glm_wide_irls(self.X, P, bt, float(self.beta[-1]), self._y32,
                                                        self._w32, self._off32, codes, self.fam.tvp, self.fam.theta,
-                                                       fused=exact and linalg_ops.wide_fused_enabled())
+                                                       fused=fused, bf3=hp != "bf16")
                 if exact:
                     self._gexact = gx[:P + 1]
                     self._gbeta = np.concatenate([self.beta[:P].astype(np.float32).astype(np.float64),
@@ -772,10 +783,13 @@ class GLMDriver:
         order = [t for t, _ in self._TIER_LIMITS]
         wide = not self._native()
         cur = self._hprec
+        bf16_ok = wide and self._gexact is not None and self._wide_bf16_ok()
         if cur is None:
             ws_bf3 = self.Pp == 128 and os.environ.get("H2O3_GLM_BF3", "1") != "0"
-            cur = "bf3" if (ws_bf3 if not wide else self._gexact is not None) else "f32"
+            cur = ("bf16" if bf16_ok else "bf3") if (ws_bf3 if not wide else self._gexact is not None) else "f32"
         want = self._tier_for(kappa)
+        if want == "bf16" and not bf16_ok:
+            want = "bf3"
         if want == "f32" and (wide or self._gexact is None):
             # no f32 path with the gradient channel here: straight to fp64
             want = "f64"

@@ -372,11 +372,12 @@ def wide_gram(X, P, wr, stream=None, bf3=True):
 
 
 def glm_wide_irls(X, P, beta, b0, y, wprior=None, offset=None, codes=(1, 1), tvp=0.0, theta=1e-10, step=1 << 19,
-                  fused=False):
+                  fused=False, bf3=True):
     """Fused IRLS pass for wide GLMs (P + 2 <= 1024).
 
     fused=True (needs the exact-gradient channel: the Gram carries no z
-    column): per row chunk glm_wide_split_kernel computes eta, the IRLS
+    column; bf3=False: a one-MFMA bf16 Hessian for the GLM's lowest
+    precision tier): per row chunk glm_wide_split_kernel computes eta, the IRLS
     weight, deviance and X'r and writes only the row weights; then ONE
     glm_wide_gram_kernel launch builds [X | 1]' W [X | 1] straight from the
     f32 rows (bf16x3 MFMA, f64 folds) -- no bf16 planes, no library GEMM.
@@ -413,7 +414,7 @@ def glm_wide_irls(X, P, beta, b0, y, wprior=None, offset=None, codes=(1, 1), tvp
                                         blocks, _ptr(gbuf), offp(wr, a), stream)
             if rc != 0:
                 raise RuntimeError(f"h2o_glm_wide_split failed: {rc}")
-        return wide_gram(X, P, wr, stream), dev.sum(), gbuf.sum(0)
+        return wide_gram(X, P, wr, stream, bf3=bf3), dev.sum(), gbuf.sum(0)
     grp = min(nch, _WIDE_GROUP)
     HL = torch.empty((grp * st, 2 * Pa), dtype=torch.bfloat16, device=X.device)
     blocks = 2048

@@ -336,6 +336,32 @@ def test_glm_conditioning_tiers_match_fp64(monkeypatch, noise, tier):
         assert err["f32"] > 100 * err["default"] and err["bf3_rhs"] > 100 * err["default"], err
 
 
+@pytest.mark.parametrize("noise,tier", [(None, "bf16"), (0.3, "bf3"), (2e-2, "f64")])
+def test_glm_wide_tiers_match_fp64(monkeypatch, noise, tier):
+    """Wide design (P = 600: the fused wide pass -- eta kernel + hand-written
+    Gram): a well-conditioned design runs on the one-MFMA bf16 Hessian
+    (kappa < 8), a moderately correlated pair (kappa ~ 50) on bf16x3, a
+    strongly correlated one (kappa ~ 1e4) on fp64 (the wide path has no f32
+    tier).  Every tier lands on the fp64 IRLS solution."""
+    import numpy as np
+    g = np.random.default_rng(8)
+    n, P = 120_000, 600
+    Xh = g.standard_normal((n, P)).astype(np.float32)
+    if noise is not None:
+        Xh[:, 1] = Xh[:, 0] + noise * g.standard_normal(n).astype(np.float32)
+    b = np.zeros(P)
+    b[:12] = 0.4 * g.standard_normal(12)
+    y = (g.random(n) < 1 / (1 + np.exp(-(Xh.astype(np.float64) @ b)))).astype(int)
+    res, drvs = _glm_fit_modes(Xh, y, {"default": _DEFAULT}, monkeypatch, iters=12)
+    drv = drvs["default"]
+    assert drv._hprec == tier, (drv._hprec, drv.hessian_kappa)
+    Xs = drv.X[:, :P].float()
+    ref, _ = _fp64_irls(Xs, drv.y, drv._init_beta)
+    ref = ref.cpu().numpy()
+    err = np.abs(res["default"] - ref).max() / np.abs(ref).max()
+    assert err < 1e-6, (err, drv.hessian_kappa)
+
+
 def test_gram_aug_bf3_matches_fp64():
     n, P = 30_011, 700
     g = torch.Generator().manual_seed(4)
