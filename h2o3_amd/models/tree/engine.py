@@ -1003,11 +1003,15 @@ class TreeGrower:
         Lq = torch.zeros(W, dtype=torch.int64, device=dev).index_add_(0, owner, w)
         Lh = Lq.tolist()
         Lmax = max(1, max(Lh))
-        pe = torch.repeat_interleave(torch.arange(P, device=dev), w)     # element -> pair
-        j = torch.arange(E, device=dev) - start[pe]                      # element -> packed bin
-        dense_idx = pe * Bs + torch.where(j == w[pe] - 1, torch.full_like(j, Bs - 1), j)
-        oe = owner[pe]
-        pos = start[pe] + j - ch_start[oe]                               # position in its owner's chunk
+        # element index arrays in int32 when they fit (a deep DRF level holds
+        # 1e8 packed bins: 4 bytes instead of 8 per bin and array)
+        it = torch.int32 if P * Bs < 2 ** 31 and E < 2 ** 31 else torch.int64
+        pe = torch.repeat_interleave(torch.arange(P, device=dev, dtype=it), w)   # element -> pair
+        j = torch.arange(E, device=dev, dtype=it) - start.to(it)[pe]            # element -> packed bin
+        dense_idx = pe * Bs + torch.where(j == w.to(it)[pe] - 1, torch.full_like(j, Bs - 1), j)
+        oe = owner.to(it)[pe]
+        pos = start.to(it)[pe] + j - ch_start.to(it)[oe]                      # position in its owner's chunk
+        del pe, j
         vals = Hp.reshape(P * Bs, C)[dense_idx]                          # [E, C]
         nzm = (vals != 0).any(1)
         nnz = int(nzm.sum())
@@ -1016,7 +1020,13 @@ class TreeGrower:
         # rank's values are integers below 2^27 the level ships int32 (a sum of
         # 8 ranks stays exact), half the bytes of f64
         big = float(vals.abs().max()) if vals.numel() else 0.0
-        not_int = 0.0 if (big < 2.0 ** 27 and bool((vals == torch.round(vals)).all())) else 1.0
+        not_int = 0.0 if big < 2.0 ** 27 else 1.0
+        step_ = 1 << 24
+        for a_ in range(0, vals.shape[0] if not_int == 0.0 else 0, step_):
+            v_ = vals[a_:a_ + step_]
+            if bool((v_ != torch.round(v_)).any()):
+                not_int = 1.0
+                break
         stat = torch.tensor([float(nnz), not_int], dtype=torch.float64, device=dev)
         coll.allreduce_(stat, "max")
         ints = float(stat[1]) == 0.0
