@@ -257,6 +257,9 @@ def main():
         # final coefficient step
         extra["train_deviance_per_row"] = round(float(drv.last_dev) / float(drv.wsum), 6)
         extra["iters"] = int(drv.iter)
+        extra["hessian_tier"] = getattr(drv, "_hprec", None)
+        k_ = getattr(drv, "hessian_kappa", None)
+        extra["hessian_kappa"] = None if k_ is None else round(float(k_), 3)
     if args.algo == "gbm" and not args.no_glm:
         # companion half of the headline metric: GLM binomial IRLSM iterations/s
         # on the SAME frame, timed separately with the same barrier + sync

@@ -572,10 +572,10 @@ class GLMDriver:
     # gradient channel): the iteration contracts at rate ~ kappa * eps(H), so the
     # tier is picked from the Jacobi-scaled condition number kappa of the system
     # matrix.  Plain bf16 MFMA (eps ~ 4e-3, the fused wide Gram only) while
-    # kappa < 8, bf16x3 MFMA (eps ~ 2e-5) while kappa < 2e3, f32 MFMA
+    # kappa < 32, bf16x3 MFMA (eps ~ 2e-5) while kappa < 2e3, f32 MFMA
     # (eps ~ 1e-7) while kappa < 5e5, beyond that fp64 (the reference's Gram
     # precision, hex/gram/Gram.java:17) on the device's f64 GEMMs.
-    _TIER_LIMITS = (("bf16", 8.0), ("bf3", 2e3), ("f32", 5e5), ("f64", float("inf")))
+    _TIER_LIMITS = (("bf16", 32.0), ("bf3", 2e3), ("f32", 5e5), ("f64", float("inf")))
 
     def _wide_bf16_ok(self):
         """The plain-bf16 Hessian tier exists for the fused wide Gram only
@@ -596,15 +596,20 @@ class GLMDriver:
         idx = idx[d > 0]
         if idx.size == 0:
             return 1.0
-        d = np.sqrt(np.diag(A)[idx])
-        S = A[np.ix_(idx, idx)] / np.outer(d, d)
+        d = 1.0 / np.sqrt(np.diag(A)[idx])
+        # one copy (no fancy-index gather when every column takes part), scaled in place
+        S = np.array(A, dtype=np.float64, order="F") if idx.size == A.shape[0] else \
+            np.asfortranarray(A[np.ix_(idx, idx)])
+        S *= d[:, None]
+        S *= d[None, :]
         # LAPACK Cholesky + 1-norm condition estimate (dpotrf / dpocon: ~0.1 ms at
         # P = 100, where a threaded eigvalsh costs ~10 ms per IRLS iteration)
         from scipy.linalg import lapack
-        c, info = lapack.dpotrf(S, lower=1, clean=0)
+        anorm = float(np.abs(S).sum(0).max())
+        c, info = lapack.dpotrf(S, lower=1, clean=0, overwrite_a=1)
         if info != 0:
             return float("inf")
-        rc, info = lapack.dpocon(c, float(np.abs(S).sum(0).max()), uplo="L")
+        rc, info = lapack.dpocon(c, anorm, uplo="L")
         return float(1.0 / rc) if info == 0 and rc > 0 else float("inf")
 
     def _irls_stats(self):
