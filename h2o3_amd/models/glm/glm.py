@@ -728,23 +728,24 @@ class GLMDriver:
         not depend on the precision of the bf16x3 Hessian."""
         gx = getattr(self, "_gexact", None)
         parts = [G.reshape(-1), xz, xw, sw, swz, dev] + ([gx] if gx is not None else [])
-        stats = torch.cat(parts)
+        stats = torch.cat([t.reshape(-1).to(torch.float64) for t in parts])
         coll.allreduce_(stats)
+        host = stats.cpu().numpy()               # one device -> host copy
         P = self.P
         o = 0
-        G = stats[o:o + P * P].view(P, P); o += P * P
-        xz = stats[o:o + P]; o += P
-        xw = stats[o:o + P]; o += P
-        sw, swz, dev = float(stats[o]), float(stats[o + 1]), float(stats[o + 2]); o += 3
-        Ga = np.zeros((P + 1, P + 1))
-        Ga[:P, :P] = G.cpu().numpy()
-        Ga[:P, P] = Ga[P, :P] = xw.cpu().numpy()
+        G = host[o:o + P * P].reshape(P, P); o += P * P
+        xz = host[o:o + P]; o += P
+        xw = host[o:o + P]; o += P
+        sw, swz, dev = float(host[o]), float(host[o + 1]), float(host[o + 2]); o += 3
+        Ga = np.empty((P + 1, P + 1))
+        Ga[:P, :P] = G
+        Ga[:P, P] = Ga[P, :P] = xw
         Ga[P, P] = sw
         if gx is not None:
-            g = stats[o:o + P + 1].cpu().numpy()
+            g = host[o:o + P + 1]
             b = Ga @ self._gbeta + g
         else:
-            b = np.concatenate([xz.cpu().numpy(), [swz]])
+            b = np.concatenate([xz, [swz]])
         return Ga, b, dev
 
     def _system(self, Ga, b):

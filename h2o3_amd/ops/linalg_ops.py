@@ -358,17 +358,27 @@ def wide_gram(X, P, wr, stream=None, bf3=True):
     T = int(os.environ.get("H2O3_WIDE_TILE", 256))
     NB = -(-(P + 1) // T)
     npairs = NB * (NB + 1) // 2
+    from ..utils.timer import phase
     per_cu = 1 if T == 256 else 2
     S = int(os.environ.get("H2O3_WIDE_SLICES", 0)) or max(1, 256 * per_cu // npairs)
-    part = torch.zeros((npairs * S, T, T), dtype=torch.float64, device=X.device)
+    # f32 runs between f64 folds: 32K rows for bf16x3 products; the plain bf16
+    # Hessian (~2^-9 per product) folds once at the end (a 500K-row f32 run adds
+    # ~1e-4 relative, far below its own rounding) -- 64K atomics per workgroup
+    # instead of one per fold per 32K rows
+    fold = 1024 if bf3 or T != 256 else 1 << 30
+    with phase("glm.wide_gram.zero"):
+        part = torch.zeros((npairs * S, T, T), dtype=torch.float64, device=X.device)
     stream = stream or ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    if T == 256:
-        rc = lib.h2o_glm_wide_gram256(_ptr(X), ldx, P, N, _ptr(wr), S, 1024, _ptr(part), 0, int(bool(bf3)), stream)
-    else:
-        rc = lib.h2o_glm_wide_gram(_ptr(X), ldx, P, N, _ptr(wr), S, 1024, _ptr(part), 0, stream)
+    with phase("glm.wide_gram.kernel"):
+        if T == 256:
+            rc = lib.h2o_glm_wide_gram256(_ptr(X), ldx, P, N, _ptr(wr), S, fold, _ptr(part), 0, int(bool(bf3)),
+                                          stream)
+        else:
+            rc = lib.h2o_glm_wide_gram(_ptr(X), ldx, P, N, _ptr(wr), S, fold, _ptr(part), 0, stream)
     if rc != 0:
         raise RuntimeError(f"h2o_glm_wide_gram failed: {rc}")
-    return _wide_gram_assemble(part, S, NB, P, T)
+    with phase("glm.wide_gram.assemble"):
+        return _wide_gram_assemble(part, S, NB, P, T)
 
 
 def glm_wide_irls(X, P, beta, b0, y, wprior=None, offset=None, codes=(1, 1), tvp=0.0, theta=1e-10, step=1 << 19,
@@ -400,21 +410,25 @@ def glm_wide_irls(X, P, beta, b0, y, wprior=None, offset=None, codes=(1, 1), tvp
     st = min(step, max(N, 1))
     nch = -(-N // st)
     if fused:
+        from ..utils.timer import phase
         blocks = 2048
         dev = torch.zeros((nch, blocks), dtype=torch.float64, device=X.device)
         gbuf = torch.zeros((blocks, Pa), dtype=torch.float64, device=X.device)
         wr = torch.empty(N, dtype=torch.float32, device=X.device)
         stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
         offp = lambda t, a: ctypes.c_void_p(0 if t is None else t.data_ptr() + a * 4)
-        for i, a in enumerate(range(0, N, st)):
-            r = min(st, N - a)
-            rc = lib.h2o_glm_wide_split(ctypes.c_void_p(X.data_ptr() + a * ldx * 4), ldx, P, Pa, r, _ptr(bt),
-                                        float(b0), offp(keep[0], a), offp(keep[1], a), offp(keep[2], a),
-                                        int(codes[0]), int(codes[1]), float(tvp), float(theta), None, _ptr(dev[i]),
-                                        blocks, _ptr(gbuf), offp(wr, a), stream)
-            if rc != 0:
-                raise RuntimeError(f"h2o_glm_wide_split failed: {rc}")
-        return wide_gram(X, P, wr, stream, bf3=bf3), dev.sum(), gbuf.sum(0)
+        with phase("glm.wide_eta"):
+            for i, a in enumerate(range(0, N, st)):
+                r = min(st, N - a)
+                rc = lib.h2o_glm_wide_split(ctypes.c_void_p(X.data_ptr() + a * ldx * 4), ldx, P, Pa, r, _ptr(bt),
+                                            float(b0), offp(keep[0], a), offp(keep[1], a), offp(keep[2], a),
+                                            int(codes[0]), int(codes[1]), float(tvp), float(theta), None,
+                                            _ptr(dev[i]), blocks, _ptr(gbuf), offp(wr, a), stream)
+                if rc != 0:
+                    raise RuntimeError(f"h2o_glm_wide_split failed: {rc}")
+        with phase("glm.wide_gram"):
+            G = wide_gram(X, P, wr, stream, bf3=bf3)
+        return G, dev.sum(), gbuf.sum(0)
     grp = min(nch, _WIDE_GROUP)
     HL = torch.empty((grp * st, 2 * Pa), dtype=torch.bfloat16, device=X.device)
     blocks = 2048
