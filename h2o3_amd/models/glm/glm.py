@@ -1324,7 +1324,15 @@ class H2OGeneralizedLinearEstimator(H2OEstimator):
         return coll.allreduce_scalar(float(ll))
 
     def _p_values(self, drv):
-        Ga, b, dev = drv._irls_stats()
+        # the covariance comes from an fp64 Hessian at the final coefficients
+        # (the reference's double Gram), not from the Newton step's bf16x3 / bf16
+        # tier: the step only needed its precision for the convergence rate
+        prev = drv._hprec
+        drv._hprec = "f64"
+        try:
+            Ga, b, dev = drv._irls_stats()
+        finally:
+            drv._hprec = prev
         P = drv.P
         if not drv.intercept:
             Ga = Ga[:P, :P]

@@ -170,10 +170,10 @@ def weighted_gram(X: torch.Tensor, w: torch.Tensor | None = None, use_native=Non
         # f32 MFMA (f64 across row blocks): PCA / SVD / GLRM-init and p-values
         # read these values directly, so no bf16x3 products here
         return glm_irls(X, W=w, bf3=False)[0]
-    if _wide_mode() == "bf3" and (w is None or bool((w >= 0).all())):
-        return gram_aug_bf3(X, w, None, P)[:P, :P]
-    if _wide_mode() == "gemm" and (w is None or bool((w >= 0).all())):
-        # wide designs: a plain library GEMM (rocBLAS/hipBLASLt fp32, 136 TFLOP/s at
+    if w is None or bool((w >= 0).all()):
+        # wide designs: f32 products (PCA / SVD / GLRM-init / p-values read these
+        # values directly -- the bf16x3 and bf16 Grams serve only the IRLS
+        # Hessian): a plain library GEMM (rocBLAS/hipBLASLt fp32, 136 TFLOP/s at
         # N=12.5M, P=1024 vs 24 for the 32x32 tile-pair kernel, scripts/glm_wide_mb.py)
         # over 1M-row chunks of sqrt(W)-scaled rows, accumulated in f64
         G = torch.zeros((P, P), dtype=torch.float64, device=X.device)
