@@ -326,24 +326,30 @@ def wide_fused_enabled():
 
 def _wide_gram_assemble(part, S, NB, P, T=128):
     """Sum the slices' f64 tile partials and mirror the upper-triangle tiles
-    into the full (P + 2)^2 Gram (the z column left 0).  T = 256 tiles: the
-    kernel skipped the lower-left quarter of diagonal tiles (taken here from
-    the upper-right one)."""
+    into the (P + 2)^2 Gram (the z column left 0).  T = 256 tiles: the kernel
+    skipped the lower-left quarter of diagonal tiles (taken here from the
+    upper-right one).  Plain block copies (advanced-index assignment into a
+    permuted view was ~10 ms at P = 1000)."""
     Tt = part.view(S, -1, T, T).sum(0)
-    npairs = Tt.shape[0]
-    bi = torch.tensor([i for i in range(NB) for _ in range(i, NB)], device=part.device)
-    bj = torch.tensor([j for i in range(NB) for j in range(i, NB)], device=part.device)
-    assert bi.numel() == npairs
-    dg = bi == bj                        # diagonal tiles: symmetrize
-    D = Tt[dg]
-    if T == 256:
-        D[:, 128:, :128] = D[:, :128, 128:].transpose(1, 2)
-    Tt[dg] = 0.5 * (D + D.transpose(1, 2))
-    G = torch.zeros((NB * T, NB * T), dtype=torch.float64, device=part.device)
-    Gt = G.view(NB, T, NB, T).permute(0, 2, 1, 3)
-    Gt[bj, bi] = Tt.transpose(1, 2)
-    Gt[bi, bj] = Tt
-    out = torch.zeros((P + 2, P + 2), dtype=torch.float64, device=part.device)
+    pairs = [(i, j) for i in range(NB) for j in range(i, NB)]
+    assert len(pairs) == Tt.shape[0]
+    n = NB * T
+    G = torch.empty((n, n), dtype=torch.float64, device=part.device)
+    for p, (i, j) in enumerate(pairs):
+        blk = Tt[p]
+        if i == j:
+            if T == 256:
+                blk[128:, :128] = blk[:128, 128:].T
+            blk = 0.5 * (blk + blk.T)
+        G[i * T:(i + 1) * T, j * T:(j + 1) * T] = blk
+        if i != j:
+            G[j * T:(j + 1) * T, i * T:(i + 1) * T] = blk.T
+    m = P + 2
+    if n >= m:
+        G[:, P + 1:] = 0.0          # columns past the intercept: the z slot (and padding) stay 0
+        G[P + 1:, :] = 0.0
+        return G[:m, :m]
+    out = torch.zeros((m, m), dtype=torch.float64, device=part.device)
     out[:P + 1, :P + 1] = G[:P + 1, :P + 1]
     return out
 

@@ -8,7 +8,12 @@ RACE.R3 are our RACE.1 / RACE.2); the reference model converges in 5
 iterations, and capped at 4 its coefficients match R's to 1e-4, null
 deviance 512.3, residual deviance 378.3, residual DOF 371, AIC 396.3.
 GLMBasicTestBinomial.java:295-299 trains on prostate_cat_train.csv, which
-does not ship: parity unpinned.
+does not ship: parity unpinned.  GBM / DRF: hex/tree/gbm/GBMTest.java and
+hex/tree/drf/DRFTest.java hard-code no training numbers on the shipped files
+(their prostate cases assert MOJO / POJO agreement and staged predictions
+only; the numeric expectations use smalldata files that do not ship):
+parity unpinned -- the tree engine is pinned against the reference's MOJO
+fixtures instead (tests/test_mojo_reference.py).
 """
 import os
 
