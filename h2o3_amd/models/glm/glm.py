@@ -730,8 +730,10 @@ class GLMDriver:
         parts = [G.reshape(-1), xz, xw, sw, swz, dev] + ([gx] if gx is not None else [])
         stats = torch.cat([t.reshape(-1).to(torch.float64) for t in parts])
         coll.allreduce_(stats)
-        host = stats.cpu().numpy()               # one device -> host copy
         P = self.P
+        if stats.is_cuda:
+            return self._finish_stats_dev(stats, gx is not None)
+        host = stats.cpu().numpy()               # one device -> host copy
         o = 0
         G = host[o:o + P * P].reshape(P, P); o += P * P
         xz = host[o:o + P]; o += P
@@ -747,6 +749,42 @@ class GLMDriver:
         else:
             b = np.concatenate([xz, [swz]])
         return Ga, b, dev
+
+    def _finish_stats_dev(self, stats, exact):
+        """_finish_stats for device statistics: the (P+1)^2 system and its
+        right-hand side are assembled on the device and reach the host in ONE
+        copy into a pinned buffer (two alternating buffers: a tier
+        escalation recomputes the statistics while the first Ga is still
+        referenced)."""
+        P = self.P
+        dev_ = stats.device
+        o = 0
+        G = stats[o:o + P * P].view(P, P); o += P * P
+        xz = stats[o:o + P]; o += P
+        xw = stats[o:o + P]; o += P
+        sw, swz, devv = stats[o], stats[o + 1], stats[o + 2]; o += 3
+        Ga = torch.empty((P + 1, P + 1), dtype=torch.float64, device=dev_)
+        Ga[:P, :P] = G
+        Ga[:P, P] = xw
+        Ga[P, :P] = xw
+        Ga[P, P] = sw
+        if exact:
+            gb = torch.as_tensor(self._gbeta, dtype=torch.float64).to(dev_, non_blocking=True)
+            b = Ga @ gb + stats[o:o + P + 1]
+        else:
+            b = torch.cat([xz, swz.view(1)])
+        out = torch.cat([Ga.reshape(-1), b, devv.view(1)])
+        n = out.numel()
+        bufs = getattr(self, "_pin_bufs", None)
+        if bufs is None or bufs[0].numel() < n:
+            bufs = self._pin_bufs = [torch.empty(n, dtype=torch.float64, pin_memory=True) for _ in range(2)]
+            self._pin_i = 0
+        self._pin_i = getattr(self, "_pin_i", 0) ^ 1
+        host_t = bufs[self._pin_i][:n]
+        host_t.copy_(out)                        # synchronous D2H into pinned memory
+        host = host_t.numpy()
+        m = (P + 1) * (P + 1)
+        return host[:m].reshape(P + 1, P + 1), host[m:m + P + 1], float(host[m + P + 1])
 
     def _system(self, Ga, b):
         """The penalized quadratic the IRLS step solves: (Gn, bn, l1, l2)."""
