@@ -854,7 +854,8 @@ class GLMDriver:
             Ga, b = self._check_tier(Ga, b)
         dev = self._stats_dev
         r = self.obj_reg
-        Gn, bn, l1, l2 = self._system(Ga, b)
+        with phase("glm.system"):
+            Gn, bn, l1, l2 = self._system(Ga, b)
         if self.est._parms.get("remove_collinear_columns") and self.active is None:
             self.active = self._find_collinear(Gn)
             self.removed_cols = [self.dinfo.coef_names[i] for i in range(self.P) if not self.active[i]]
