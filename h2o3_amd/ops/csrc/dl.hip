@@ -322,6 +322,13 @@ __global__ __launch_bounds__(256) void dl_softmax_kernel(float* __restrict__ Z, 
 // ---------------------------------------------------------------------------
 #define DL_MAXL 8
 #define DL_ROWS 16
+// forward/backward kernel: 8 waves, each a chunk of DL_TPW output tiles per
+// pass (tiles wave, wave + 8, ...): a 200-unit layer is 13 tiles, two per
+// wave, so the serial MFMA + load chain of each wave is half as long as
+// with 4 waves of 4 tiles
+#define DL_FB_WAVES 8
+#define DL_FB_THREADS (64 * DL_FB_WAVES)
+#define DL_TPW 2
 typedef float dl_f32x4 __attribute__((ext_vector_type(4)));
 
 struct DLNet {
@@ -352,7 +359,7 @@ __device__ __forceinline__ unsigned long long dl_lcg(unsigned long long s) {
   return s * 6364136223846793005ull + 1442695040888963407ull;
 }
 
-__global__ __launch_bounds__(256) void dl_mlp_fb_kernel(const DLNet net, const float* __restrict__ X,
+__global__ __launch_bounds__(DL_FB_THREADS) void dl_mlp_fb_kernel(const DLNet net, const float* __restrict__ X,
                                                         const long long* __restrict__ idx,
                                                         const long long* __restrict__ ycls,
                                                         const float* __restrict__ yreg,
@@ -368,7 +375,7 @@ __global__ __launch_bounds__(256) void dl_mlp_fb_kernel(const DLNet net, const f
   {
     const int P = net.width[0], S = net.stride[0];
     float* a0 = lds + net.lds_a[0];
-    for (int e = tid; e < DL_ROWS * S; e += 256) {
+    for (int e = tid; e < DL_ROWS * S; e += DL_FB_THREADS) {
       const int r = e / S, c = e - r * S;
       const int rg = r0 + r;
       float v = 0.f;
@@ -413,17 +420,17 @@ __global__ __launch_bounds__(256) void dl_mlp_fb_kernel(const DLNet net, const f
       }
       return w;
     };
-    for (int t0 = wave; t0 < NT; t0 += 16) {
-      dl_f32x4 acc[4];
+    for (int t0 = wave; t0 < NT; t0 += DL_FB_WAVES * DL_TPW) {
+      dl_f32x4 acc[DL_TPW];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[j] = (dl_f32x4){0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < DL_TPW; ++j) acc[j] = (dl_f32x4){0.f, 0.f, 0.f, 0.f};
       // 4-deep register ring of weight loads: the L2 latency of step ks + 4
       // hides behind the MFMAs of steps ks .. ks + 3
-      float4 wq[4][4];
+      float4 wq[4][DL_TPW];
 #pragma unroll
       for (int d = 0; d < 4; ++d)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) wq[d][j] = d < nk ? wload(t0 + 4 * j, d) : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int j = 0; j < DL_TPW; ++j) wq[d][j] = d < nk ? wload(t0 + DL_FB_WAVES * j, d) : make_float4(0.f, 0.f, 0.f, 0.f);
       for (int kb = 0; kb < nk; kb += 4) {
 #pragma unroll
         for (int d = 0; d < 4; ++d) {
@@ -431,18 +438,18 @@ __global__ __launch_bounds__(256) void dl_mlp_fb_kernel(const DLNet net, const f
           if (ks < nk) {
             const float4 a = *reinterpret_cast<const float4*>(ain + c16 * Si + ks * 16 + g4);
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-              if (t0 + 4 * j < NT) acc[j] = dl_mfma4(a, wq[d][j], acc[j]);
+            for (int j = 0; j < DL_TPW; ++j)
+              if (t0 + DL_FB_WAVES * j < NT) acc[j] = dl_mfma4(a, wq[d][j], acc[j]);
             if (ks + 4 < nk) {
 #pragma unroll
-              for (int j = 0; j < 4; ++j) wq[d][j] = wload(t0 + 4 * j, ks + 4);
+              for (int j = 0; j < DL_TPW; ++j) wq[d][j] = wload(t0 + DL_FB_WAVES * j, ks + 4);
             }
           }
         }
       }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int t = t0 + 4 * j;
+      for (int j = 0; j < DL_TPW; ++j) {
+        const int t = t0 + DL_FB_WAVES * j;
         if (t < NT) {
           const int u = t * 16 + c16;
           const float bu = u < U ? net.b[l][u] : 0.f;
@@ -533,15 +540,15 @@ __global__ __launch_bounds__(256) void dl_mlp_fb_kernel(const DLNet net, const f
       }
       return w;
     };
-    for (int t0 = wave; t0 < NT; t0 += 16) {
-      dl_f32x4 acc[4];
+    for (int t0 = wave; t0 < NT; t0 += DL_FB_WAVES * DL_TPW) {
+      dl_f32x4 acc[DL_TPW];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[j] = (dl_f32x4){0.f, 0.f, 0.f, 0.f};
-      float4 wq[4][4];
+      for (int j = 0; j < DL_TPW; ++j) acc[j] = (dl_f32x4){0.f, 0.f, 0.f, 0.f};
+      float4 wq[4][DL_TPW];
 #pragma unroll
       for (int d = 0; d < 4; ++d)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) wq[d][j] = d < nk ? wload(t0 + 4 * j, d) : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int j = 0; j < DL_TPW; ++j) wq[d][j] = d < nk ? wload(t0 + DL_FB_WAVES * j, d) : make_float4(0.f, 0.f, 0.f, 0.f);
       for (int kb = 0; kb < nk; kb += 4) {
 #pragma unroll
         for (int d = 0; d < 4; ++d) {
@@ -549,18 +556,18 @@ __global__ __launch_bounds__(256) void dl_mlp_fb_kernel(const DLNet net, const f
           if (ks < nk) {
             const float4 dv = *reinterpret_cast<const float4*>(dcur + c16 * net.ldsw + ks * 16 + g4);
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-              if (t0 + 4 * j < NT) acc[j] = dl_mfma4(dv, wq[d][j], acc[j]);
+            for (int j = 0; j < DL_TPW; ++j)
+              if (t0 + DL_FB_WAVES * j < NT) acc[j] = dl_mfma4(dv, wq[d][j], acc[j]);
             if (ks + 4 < nk) {
 #pragma unroll
-              for (int j = 0; j < 4; ++j) wq[d][j] = wload(t0 + 4 * j, ks + 4);
+              for (int j = 0; j < DL_TPW; ++j) wq[d][j] = wload(t0 + DL_FB_WAVES * j, ks + 4);
             }
           }
         }
       }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int t = t0 + 4 * j;
+      for (int j = 0; j < DL_TPW; ++j) {
+        const int t = t0 + DL_FB_WAVES * j;
         if (t < NT) {
           const int i = t * 16 + c16;
 #pragma unroll
@@ -828,7 +835,7 @@ int h2o_dl_mlp_step(int nl, const int* width, const int* act, const float* drop,
     (void)hipFuncSetAttribute((const void*)dl_mlp_fb_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
-  hipLaunchKernelGGL(dl_mlp_fb_kernel, dim3((B + DL_ROWS - 1) / DL_ROWS), dim3(256), lds_bytes, s, net, X, idx, ycls,
+  hipLaunchKernelGGL(dl_mlp_fb_kernel, dim3((B + DL_ROWS - 1) / DL_ROWS), dim3(DL_FB_THREADS), lds_bytes, s, net, X, idx, ycls,
                      yreg, wts, seed, seed_dev, advance);
   DLGrad g{};
   g.nl = nl;
