@@ -213,7 +213,11 @@ def _solve_quadratic(G, b, l1, l2, intercept, beta0=None, non_negative=False, ma
     boxed = bool(np.isfinite(lo).any() or np.isfinite(hi).any())
     if l1 == 0 and not boxed:
         import scipy.linalg as sla
-        A = G + np.diag(l2 * pen)
+        if l2 != 0:
+            A = G.copy()
+            A[np.diag_indices(P)] += l2 * pen
+        else:
+            A = G                                # cho_factor copies it (no extra diag matrix)
         # a ridge only when the plain factorization fails, and then relative to
         # each diagonal entry: an absolute ridge eps * max(diag) biases the
         # Newton fixed point (g = eps beta) of unstandardized designs by ~1e-5
