@@ -124,3 +124,53 @@ def test_learn_rate_annealing_stops_below_1e6():
                                      min_rows=10)
     m.train(x=["x"], y="y", training_frame=h2o.H2OFrame(df))
     assert m.ntrees_built == 18
+
+
+def test_sampling_factors_rule():
+    """MRUtils.sampleFrameStratified factors: default = every class up to the
+    majority count; user factors taken as given; both scaled down so the
+    balanced size stays <= max_after_balance_size x the original."""
+    from h2o3_amd.models.balance import sampling_factors
+    c = np.array([900.0, 100.0])
+    assert sampling_factors(c, None, 5.0) == pytest.approx([1.0, 9.0])
+    assert sampling_factors(c, None, 1.5) == pytest.approx(np.array([1.0, 9.0]) * 1500 / 1800)
+    assert sampling_factors(c, [1, 4], 5.0) == pytest.approx([1.0, 4.0])
+    assert sampling_factors(c, [2, 4], 1.0) == pytest.approx(np.array([2.0, 4.0]) * 1000 / 2200)
+    with pytest.raises(ValueError):
+        sampling_factors(c, [1, 2, 3], 5.0)
+
+
+def test_balance_classes_distributions_and_correction():
+    """balance_classes + class_sampling_factors=[1, 4] on a 9:1 frame: the
+    balanced frame holds exactly n0 + 4 n1 rows (integer factors), the model
+    records prior [0.9, 0.1] and model distribution [0.9, 0.4] / 1.3, and
+    predictions are corrected back so the mean P(minority) tracks the prior
+    (not the balanced 0.31)."""
+    from h2o3_amd.models.balance import balance_frame, class_counts
+    rng = np.random.default_rng(7)
+    n = 2000
+    x = rng.normal(size=n)
+    y = np.where(np.arange(n) < n // 10, "min", "maj")
+    x = x + np.where(y == "min", 0.8, 0.0)
+    df = pd.DataFrame({"x": x, "y": y})
+    fr = h2o.H2OFrame(df)
+    fr["y"] = fr["y"].asfactor()
+    dom = fr.vec("y").domain
+    imin = dom.index("min")
+    f = [1.0, 1.0]
+    f[imin] = 4.0
+    bal = balance_frame(fr, "y", f, seed=3)
+    cb = class_counts(bal, "y")
+    assert cb[imin] == 4 * (n // 10) and cb[1 - imin] == n - n // 10
+    m = H2OGradientBoostingEstimator(ntrees=20, max_depth=3, seed=1, balance_classes=True,
+                                     class_sampling_factors=f)
+    m.train(x=["x"], y="y", training_frame=fr)
+    prior = np.array(m._output["prior_class_distribution"])
+    model = np.array(m._output["model_class_distribution"])
+    assert prior[imin] == pytest.approx(0.1) and model[imin] == pytest.approx(0.4 / 1.3)
+    p = m.predict(fr).as_data_frame()["min"].values
+    assert abs(p.mean() - 0.1) < 0.03, p.mean()
+    mu = H2OGradientBoostingEstimator(ntrees=20, max_depth=3, seed=1)
+    mu.train(x=["x"], y="y", training_frame=fr)
+    pu = mu.predict(fr).as_data_frame()["min"].values
+    assert np.corrcoef(p, pu)[0, 1] > 0.9
