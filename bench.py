@@ -27,10 +27,23 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 
-_GLM_PRECISION = ("Hessian X'WX: bf16x3 split operands (hi*hi + hi*lo + lo*hi) on MFMA, f32 accumulate, f64 across "
-                  "row blocks; gradient X'(w (y - mu)): f32 VALU products, f64 sums, in the same pass; Newton step "
-                  "beta + H^-1 g, so the converged coefficients are those of the exact gradient "
-                  "(scripts/glm_precision.py)")
+_HESSIAN = {
+    "bf16": "one bf16 MFMA per product (hi*hi), f32 accumulate, f64 across row slices (kappa < 32 tier)",
+    "bf3": "bf16x3 split operands (hi*hi + hi*lo + lo*hi) on MFMA, f32 accumulate, f64 across row blocks",
+    "f32": "f32 MFMA products, f64 across row blocks",
+    "f64": "fp64 GEMMs",
+}
+
+
+def _glm_precision(tier):
+    """The config's precision statement for the Hessian tier the run ended on
+    (glm.py _TIER_LIMITS: chosen from the scaled condition number)."""
+    return (f"Hessian X'WX: {_HESSIAN.get(tier or 'bf3', tier)}; gradient X'(w (y - mu)): f32 VALU products, f64 "
+            "sums, in the same pass; Newton step beta + H^-1 g, so the converged coefficients are those of the "
+            "exact gradient whatever the Hessian tier (scripts/glm_precision.py)")
+
+
+_GLM_PRECISION = _glm_precision("bf3")
 
 
 def make_frame(args, dev, rank, rows_local):
@@ -257,7 +270,8 @@ def main():
         # final coefficient step
         extra["train_deviance_per_row"] = round(float(drv.last_dev) / float(drv.wsum), 6)
         extra["iters"] = int(drv.iter)
-        extra["hessian_tier"] = getattr(drv, "_hprec", None)
+        extra["hessian_tier"] = getattr(drv, "_hprec", None) or ("f64" if dev.type == "cpu" else None)
+        extra_cfg["gram_precision"] = _glm_precision(extra["hessian_tier"])
         k_ = getattr(drv, "hessian_kappa", None)
         extra["hessian_kappa"] = None if k_ is None else round(float(k_), 3)
     if args.algo == "gbm" and not args.no_glm:
@@ -284,7 +298,8 @@ def main():
         extra["glm_iters_per_sec"] = round(args.steps / gel, 4)
         extra["glm_ms_per_iter"] = round(1000 * gel / args.steps, 3)
         extra["glm_model"] = f"GLM binomial IRLSM {args.rows / 1e6:g}Mx{F} (same frame, {args.steps} timed iterations)"
-        extra["glm_precision"] = _GLM_PRECISION
+        extra["glm_hessian_tier"] = getattr(gdrv, "_hprec", None) or ("f64" if dev.type == "cpu" else None)
+        extra["glm_precision"] = _glm_precision(extra["glm_hessian_tier"])
     from h2o3_amd.utils import timer
     if timer.ENABLED and rank == 0:
         print("phases(ms,count):", timer.report(), file=sys.stderr)

@@ -1113,8 +1113,9 @@ extern "C" int h2o_gram_split(const float* X, int ldx, int P, int Pa, const floa
 // the [hi | lo] split of sqrt(W) [x | 1 | z] -- X is read from HBM once per
 // IRLS iteration; the library GEMM that follows reads only the bf16 halves.
 // Deviance: one f64 partial per block (deterministic; the host sums).
-template <int NQ>
-__global__ __launch_bounds__(256) void glm_wide_split_kernel(
+#define WIDE_GFOLD 64
+template <int NQ, int RW, bool HASHL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RW == 1 ? 4 : 1))) void glm_wide_split_kernel(
     const float* __restrict__ X, int ldx, int P, int Pa, long long rows, const float* __restrict__ beta, float b0,
     const float* __restrict__ y, const float* __restrict__ wprior, const float* __restrict__ offset,
     GlmFamArgs fam, __bf16* __restrict__ HL, double* __restrict__ dev_out, double* __restrict__ grad_out,
@@ -1123,11 +1124,20 @@ __global__ __launch_bounds__(256) void glm_wide_split_kernel(
   // fused wide Gram kernel below reads X and these weights).
   // grad_out (optional): [gridDim.x][Pa] f64, this block's slot += X' r over
   // its rows of the chunk (r = w (y - mu) dmu/deta / var: the exact-gradient
-  // channel, see glm_irls_ws_kernel); column P holds sum r
+  // channel, see glm_irls_ws_kernel); column P holds sum r.  Each lane's f32
+  // products are folded into its own f64 LDS slots every WIDE_GFOLD rows, so
+  // one launch can sweep any number of rows at the stated precision.
   __shared__ double dsum[4];
-  __shared__ float gsh[4][NQ * 256];
+  __shared__ double gsh[4][NQ * 256];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
+  if (grad_out) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) gsh[wv][4 * (lane + 64 * q) + e] = 0.0;
+  }
+  int since = 0;
   f32x4 b[NQ];
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
@@ -1140,68 +1150,98 @@ __global__ __launch_bounds__(256) void glm_wide_split_kernel(
 #pragma unroll
   for (int q = 0; q < NQ; ++q) ga[q] = f32x4{0.f, 0.f, 0.f, 0.f};
   float gi = 0.f;
-  const long long nw = (long long)gridDim.x * 4;
-  for (long long r = (long long)blockIdx.x * 4 + wv; r < rows; r += nw) {
-    f32x4 v[NQ];
-    float dot = 0.f;
+  // RW consecutive rows per wave per step: their loads are all issued before
+  // the first dot-product reduction (RW x 4 KB in flight per wave instead of
+  // one row, whose reduction and family math stalled the next row's loads)
+  const long long nw = (long long)gridDim.x * 4 * RW;
+  for (long long r0 = ((long long)blockIdx.x * 4 + wv) * RW; r0 < rows; r0 += nw) {
+    f32x4 v[RW][NQ];
+    float dot[RW];
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const int c = 4 * (lane + 64 * q);
-      if (c + 3 < P) {
-        v[q] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(X + r * ldx + c));
+    for (int j = 0; j < RW; ++j) {
+      const long long r = r0 + j < rows ? r0 + j : rows - 1;
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const int c = 4 * (lane + 64 * q);
+        if (c + 3 < P) {
+          v[j][q] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(X + r * ldx + c));
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[j][q][e] = c + e < P ? X[r * ldx + c + e] : 0.f;
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < RW; ++j) {
+      dot[j] = 0.f;
+#pragma unroll
+      for (int q = 0; q < NQ; ++q)
+        dot[j] += v[j][q].x * b[q].x + v[j][q].y * b[q].y + v[j][q].z * b[q].z + v[j][q].w * b[q].w;
+    }
+#pragma unroll
+    for (int j = 0; j < RW; ++j) dot[j] = wave_sum(dot[j]);
+#pragma unroll
+    for (int j = 0; j < RW; ++j) {
+      const long long r = r0 + j;
+      if (r >= rows) break;
+      const float sy = y[r], sw = wprior ? wprior[r] : 1.f, so = offset ? offset[r] : 0.f;
+      const float eta = dot[j] + b0 + so;
+      const float mu = gi_linkinv(fam.link, eta);
+      float W, z, rres;
+      if (fam.link == 0 && fam.var == 0) {
+        W = sw;
+        z = sy - so;
+        rres = sw * (sy - eta);
       } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[q][e] = c + e < P ? X[r * ldx + c + e] : 0.f;
+        const float d = gi_dmu(fam.link, mu);
+        const float wd = sw * d / gi_var(fam, mu);
+        W = wd * d;
+        z = (eta - so) + (sy - mu) / d;
+        rres = wd * (sy - mu);
       }
-      dot += v[q].x * b[q].x + v[q].y * b[q].y + v[q].z * b[q].z + v[q].w * b[q].w;
-    }
-    dot = wave_sum(dot);
-    const float sy = y[r], sw = wprior ? wprior[r] : 1.f, so = offset ? offset[r] : 0.f;
-    const float eta = dot + b0 + so;
-    const float mu = gi_linkinv(fam.link, eta);
-    float W, z, rres;
-    if (fam.link == 0 && fam.var == 0) {
-      W = sw;
-      z = sy - so;
-      rres = sw * (sy - eta);
-    } else {
-      const float d = gi_dmu(fam.link, mu);
-      const float wd = sw * d / gi_var(fam, mu);
-      W = wd * d;
-      z = (eta - so) + (sy - mu) / d;
-      rres = wd * (sy - mu);
-    }
-    if (lane == 0 && sw != 0.f) dev += (double)(sw * gi_dev(fam, sy, mu));
-    if (grad_out) {
+      if (lane == 0 && sw != 0.f) dev += (double)(sw * gi_dev(fam, sy, mu));
+      if (grad_out) {
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) ga[q] += v[q] * rres;
-      gi += rres;
-    }
-    if (!HL) {
-      if (lane == 0) wout[r] = fmaxf(W, 0.f);
-      continue;
-    }
-    const float s = sqrtf(fmaxf(W, 0.f));
-    __bf16* o = HL + r * (2LL * Pa);
+        for (int q = 0; q < NQ; ++q) ga[q] += v[j][q] * rres;
+        gi += rres;
+        if (++since == WIDE_GFOLD) {
+          since = 0;
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const int c = 4 * (lane + 64 * q);
-      if (c >= Pa) break;
-      f32x4 a = v[q];
+          for (int q = 0; q < NQ; ++q) {
+            const int c = 4 * (lane + 64 * q);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        if (c + e == P) a[e] = 1.f;
-        if (c + e == P + 1) a[e] = z;
+            for (int e = 0; e < 4; ++e) gsh[wv][c + e] += (double)(c + e == P ? gi : ga[q][e]);
+            ga[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+          }
+          gi = 0.f;
+        }
       }
-      bf16x4 h, l;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float t = a[e] * s;
-        h[e] = (__bf16)t;
-        l[e] = (__bf16)(t - (float)h[e]);
+      if constexpr (!HASHL) {
+        if (lane == 0) wout[r] = fmaxf(W, 0.f);
+        continue;
       }
-      *reinterpret_cast<bf16x4*>(o + c) = h;
-      *reinterpret_cast<bf16x4*>(o + Pa + c) = l;
+      const float s = sqrtf(fmaxf(W, 0.f));
+      __bf16* o = HL + r * (2LL * Pa);
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const int c = 4 * (lane + 64 * q);
+        if (c >= Pa) break;
+        f32x4 a = v[j][q];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (c + e == P) a[e] = 1.f;
+          if (c + e == P + 1) a[e] = z;
+        }
+        bf16x4 h, l;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float t = a[e] * s;
+          h[e] = (__bf16)t;
+          l[e] = (__bf16)(t - (float)h[e]);
+        }
+        *reinterpret_cast<bf16x4*>(o + c) = h;
+        *reinterpret_cast<bf16x4*>(o + Pa + c) = l;
+      }
     }
   }
   dev = wave_sum(dev);
@@ -1211,7 +1251,7 @@ __global__ __launch_bounds__(256) void glm_wide_split_kernel(
     for (int q = 0; q < NQ; ++q) {
       const int c = 4 * (lane + 64 * q);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) gsh[wv][c + e] = c + e == P ? gi : ga[q][e];
+      for (int e = 0; e < 4; ++e) gsh[wv][c + e] += (double)(c + e == P ? gi : ga[q][e]);
     }
   }
   __syncthreads();
@@ -1219,11 +1259,27 @@ __global__ __launch_bounds__(256) void glm_wide_split_kernel(
   if (grad_out) {
     for (int c = threadIdx.x; c < Pa; c += 256)
       grad_out[(size_t)blockIdx.x * Pa + c] +=
-          ((double)gsh[0][c] + (double)gsh[1][c]) + ((double)gsh[2][c] + (double)gsh[3][c]);
+          (gsh[0][c] + gsh[1][c]) + (gsh[2][c] + gsh[3][c]);
   }
 }
 
+// Workgroups that fill the chip once for the weight-only pass (resident
+// blocks per CU x CUs): a grid of whole rounds, no partial last round.
+extern "C" int h2o_glm_wide_split_grid(int Pa) {
+  int dev = 0, cus = 0, per_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+  const void* k = Pa <= 256 ? (const void*)glm_wide_split_kernel<1, 1, false>
+                  : Pa <= 512 ? (const void*)glm_wide_split_kernel<2, 1, false>
+                              : (const void*)glm_wide_split_kernel<4, 1, false>;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, 0) != hipSuccess) return 0;
+  return per_cu * cus;
+}
+
 // Pa <= 1024 (P <= 1022), Pa % 4 == 0; dev_out holds `blocks` doubles.
+#ifndef WIDE_RW
+#define WIDE_RW 1
+#endif
 extern "C" int h2o_glm_wide_split(const float* X, int ldx, int P, int Pa, long long rows, const float* beta, float b0,
                                   const float* y, const float* wprior, const float* offset, int link, int var,
                                   float tvp, float theta, void* HL, double* dev_out, int blocks, double* grad_out,
@@ -1231,17 +1287,28 @@ extern "C" int h2o_glm_wide_split(const float* X, int ldx, int P, int Pa, long l
   if (rows <= 0) return 0;
   if (Pa % 4 != 0 || Pa < P + 2 || ldx < P || blocks <= 0 || (!HL && !wout)) return -1;
   GlmFamArgs fam{link, var, tvp, theta, 0, 0, 0, 0};
-  if (Pa <= 256)
-    hipLaunchKernelGGL(glm_wide_split_kernel<1>, dim3(blocks), dim3(256), 0, s, X, ldx, P, Pa, rows, beta, b0, y,
-                       wprior, offset, fam, (__bf16*)HL, dev_out, grad_out, wout);
-  else if (Pa <= 512)
-    hipLaunchKernelGGL(glm_wide_split_kernel<2>, dim3(blocks), dim3(256), 0, s, X, ldx, P, Pa, rows, beta, b0, y,
-                       wprior, offset, fam, (__bf16*)HL, dev_out, grad_out, wout);
-  else if (Pa <= 1024)
-    hipLaunchKernelGGL(glm_wide_split_kernel<4>, dim3(blocks), dim3(256), 0, s, X, ldx, P, Pa, rows, beta, b0, y,
-                       wprior, offset, fam, (__bf16*)HL, dev_out, grad_out, wout);
-  else
-    return -2;
+#define WIDE_SPLIT(NQ, RW, H)                                                                                    \
+  hipLaunchKernelGGL((glm_wide_split_kernel<NQ, RW, H>), dim3(blocks), dim3(256), 0, s, X, ldx, P, Pa, rows, beta, \
+                     b0, y, wprior, offset, fam, (__bf16*)HL, dev_out, grad_out, wout)
+  if (HL) {
+    if (Pa <= 256) WIDE_SPLIT(1, 2, true);
+    else if (Pa <= 512) WIDE_SPLIT(2, 2, true);
+    else if (Pa <= 1024) WIDE_SPLIT(4, 2, true);
+    else return -2;
+  } else {
+    // weight-only pass of the fused wide IRLS: rows in flight per wave
+    // (H2O3_WIDE_RW = 1 / 2 / 4, default WIDE_RW; at 12.5M x 1000 the pass
+    // takes 10.5 / 12.5 / 12.4 ms: more rows per wave lowers occupancy
+    // (129 -> 155 -> 195 VGPRs) and does not raise the read rate)
+    static const int rw = getenv("H2O3_WIDE_RW") ? atoi(getenv("H2O3_WIDE_RW")) : WIDE_RW;
+    if (Pa <= 256) WIDE_SPLIT(1, 1, false);
+    else if (Pa <= 512) WIDE_SPLIT(2, 1, false);
+    else if (Pa > 1024) return -2;
+    else if (rw == 1) WIDE_SPLIT(4, 1, false);
+    else if (rw == 4) WIDE_SPLIT(4, 4, false);
+    else WIDE_SPLIT(4, 2, false);
+  }
+#undef WIDE_SPLIT
   return (int)hipGetLastError();
 }
 
@@ -1449,18 +1516,29 @@ extern "C" int h2o_glm_wide_gram(const float* X, int ldx, int P, long long N, co
 // upper-right one).
 // ---------------------------------------------------------------------------
 #define WG2_T 256
-#define WG2_KR 32
-#define WG2_BUF (4 * WG2_T * WG2_KR)   // bf16 per chunk buffer (A hi, A lo, B hi, B lo)
+// KR rows per chunk: 32 for bf16x3 (4 planes per buffer), 32 or 64 for the
+// one-MFMA bf16 tier (2 planes; 64 halves the barriers and weight loads per
+// row).  k-blocks of 8 are XOR-swizzled so that the 8 lanes of a b128 access
+// (8 consecutive columns, one k-block) land in 8 different 16-B bank groups
+// of the 256-B bank row: pitch 64 B -> swizzle by column >> 2, pitch 128 B
+// -> by column >> 1.
+template <int KR>
+__device__ __forceinline__ int wg2_off(int col, int kb) {
+  return col * KR + ((kb ^ ((col >> (KR == 32 ? 2 : 1)) & (KR / 8 - 1))) << 3);
+}
 
-__device__ __forceinline__ int wg2_off(int col, int kb) { return col * WG2_KR + ((kb ^ ((col >> 2) & 3)) << 3); }
-
-template <bool BF3>
+template <bool BF3, int KR>
 __global__ __launch_bounds__(512, 1) void glm_wide_gram256_kernel(const float* __restrict__ X, int ldx, int P,
                                                                   long long N, const float* __restrict__ Wr, int NB,
                                                                   int npairs, int S, int fold,
                                                                   double* __restrict__ part, int dbg) {
+  constexpr int NPL = BF3 ? 4 : 2;                 // planes: A hi, (A lo), B hi, (B lo)
+  constexpr int BUF = NPL * WG2_T * KR;            // bf16 per chunk buffer
+  constexpr int PBH = BF3 ? 2 : 1;                 // plane index of B hi
+  constexpr int NRG = KR / 8;                      // 8-row groups per chunk
+  constexpr int NQ = NRG;                          // (panel, row group) slices per thread: 2 panels x NRG / 2
   extern __shared__ __bf16 wg2_lds[];
-  float* sW = reinterpret_cast<float*>(wg2_lds + 2 * WG2_BUF);   // [2][32] row weights
+  float* sW = reinterpret_cast<float*>(wg2_lds + 2 * BUF);   // [2][KR] row weights
   const int nblk = npairs * S;
   const int L = xcd_remap(blockIdx.x, nblk);
   const int sl = L / npairs, pr = L - sl * npairs;
@@ -1469,43 +1547,43 @@ __global__ __launch_bounds__(512, 1) void glm_wide_gram256_kernel(const float* _
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int mi = wv >> 2, nq = wv & 3;      // rows 128 mi .., columns 64 nq ..
   const bool skip = bi == bj && mi == 1 && nq < 2;  // lower-left quarter of a diagonal tile
-  const long long nchunk = (N + WG2_KR - 1) / WG2_KR;
+  const long long nchunk = (N + KR - 1) / KR;
   // chunks of this slice: c = sl + t S, t = 0 .. nt - 1
   const long long nt = sl < nchunk ? (nchunk - 1 - sl) / S + 1 : 0;
-  // loader: thread = column tid & 255 of panel (q >> 1), row groups
-  // ((tid >> 8) + 2 q) & 3 -- wave-uniform
+  // loader: thread = column tid & 255 of panel q / (NQ / 2), row group
+  // (tid >> 8) + 2 (q % (NQ / 2)) -- wave-uniform
   const int t8 = __builtin_amdgcn_readfirstlane(tid >> 8);
   const int colb = tid & 255;
   const int gcA = bi * WG2_T + colb, gcB = bj * WG2_T + colb;
   const float fillA = gcA == P ? 1.f : 0.f, fillB = gcB == P ? 1.f : 0.f;
   const bool inA = gcA < P, inB = gcB < P;
-  float xr[4][8];
+  float xr[NQ][8];
   float wpre = 0.f;
   auto load_x = [&](long long t) {
-    const long long row0 = (sl + t * S) * WG2_KR;
+    const long long row0 = (sl + t * S) * KR;
     const long long left = N - row0;
-    const int nr = (int)(left < WG2_KR ? (left > 0 ? left : 0) : WG2_KR);   // past N: every load reads 0
+    const int nr = (int)(left < KR ? (left > 0 ? left : 0) : KR);   // past N: every load reads 0
     const __amdgpu_buffer_rsrc_t rx =
         __builtin_amdgcn_make_buffer_rsrc((void*)(X + row0 * ldx), (short)0, (dbg & 1) ? 0 : nr * ldx * 4, 0x00020000);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int pan = q >> 1, rg = (t8 + 2 * q) & 3;
+    for (int q = 0; q < NQ; ++q) {
+      const int pan = q / (NQ / 2), rg = t8 + 2 * (q % (NQ / 2));
 #pragma unroll
       for (int e = 0; e < 8; ++e)
         xr[q][e] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rx, (pan ? gcB : gcA) * 4, (rg * 8 + e) * ldx * 4, 0));
     }
   };
   auto load_w = [&](long long t) -> float {   // threads < 32: the chunk's row weight (0 past N)
-    const long long row0 = (sl + t * S) * WG2_KR;
+    const long long row0 = (sl + t * S) * KR;
     const long long left = N - row0;
-    const int nr = (int)(left < WG2_KR ? (left > 0 ? left : 0) : WG2_KR);
+    const int nr = (int)(left < KR ? (left > 0 ? left : 0) : KR);
     const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)(Wr + row0), (short)0, nr * 4, 0x00020000);
     return __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rw, tid * 4, 0, 0));
   };
   auto store_q = [&](int buf, int q) {
-    __bf16* base = wg2_lds + buf * WG2_BUF;
-    const float* w = sW + buf * WG2_KR;
-    const int pan = q >> 1, rg = (t8 + 2 * q) & 3;
+    __bf16* base = wg2_lds + buf * BUF;
+    const float* w = sW + buf * KR;
+    const int pan = q / (NQ / 2), rg = t8 + 2 * (q % (NQ / 2));
     bf16x8 h, l;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -1514,13 +1592,13 @@ __global__ __launch_bounds__(512, 1) void glm_wide_gram256_kernel(const float* _
       h[e] = (__bf16)x;
       if constexpr (BF3) l[e] = (__bf16)(x - (float)h[e]);
     }
-    const int off = wg2_off(colb, rg);
-    *reinterpret_cast<bf16x8*>(base + (pan ? 2 : 0) * WG2_T * WG2_KR + off) = h;
-    if constexpr (BF3) *reinterpret_cast<bf16x8*>(base + (pan ? 3 : 1) * WG2_T * WG2_KR + off) = l;
+    const int off = wg2_off<KR>(colb, rg);
+    *reinterpret_cast<bf16x8*>(base + (pan ? PBH : 0) * WG2_T * KR + off) = h;
+    if constexpr (BF3) *reinterpret_cast<bf16x8*>(base + (pan ? 3 : 1) * WG2_T * KR + off) = l;
   };
   auto store = [&](int buf) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) store_q(buf, q);
+    for (int q = 0; q < NQ; ++q) store_q(buf, q);
   };
   f32x16 acc[4][2];
 #pragma unroll
@@ -1554,23 +1632,23 @@ __global__ __launch_bounds__(512, 1) void glm_wide_gram256_kernel(const float* _
   // next chunk's q-th slice into buffer `nbuf` after each (ks, b) sub-step:
   // straight-line code, so the scheduler interleaves VALU with the MFMAs
   auto compute_store = [&](int buf, int nbuf) {
-    const __bf16* sAh = wg2_lds + buf * WG2_BUF;
-    const __bf16* sAl = sAh + WG2_T * WG2_KR;
-    const __bf16* sBh = sAl + WG2_T * WG2_KR;
-    const __bf16* sBl = sBh + WG2_T * WG2_KR;
+    const __bf16* sAh = wg2_lds + buf * BUF;
+    const __bf16* sAl = sAh + WG2_T * KR;
+    const __bf16* sBh = sAh + PBH * WG2_T * KR;
+    const __bf16* sBl = sAh + 3 * WG2_T * KR;
 #pragma unroll
-    for (int ks = 0; ks < WG2_KR / 16; ++ks) {
+    for (int ks = 0; ks < KR / 16; ++ks) {
       const int kb = 2 * ks + (lane >> 5);
       bf16x8 ah[4], al[4];
 #pragma unroll
       for (int a = 0; a < 4; ++a) {
-        const int off = wg2_off(128 * mi + 32 * a + (lane & 31), kb);
+        const int off = wg2_off<KR>(128 * mi + 32 * a + (lane & 31), kb);
         ah[a] = *reinterpret_cast<const bf16x8*>(sAh + off);
         if constexpr (BF3) al[a] = *reinterpret_cast<const bf16x8*>(sAl + off);
       }
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
-        const int off = wg2_off(64 * nq + 32 * b + (lane & 31), kb);
+        const int off = wg2_off<KR>(64 * nq + 32 * b + (lane & 31), kb);
         const bf16x8 bh = *reinterpret_cast<const bf16x8*>(sBh + off);
 #pragma unroll
         for (int a = 0; a < 4; ++a) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bh, acc[a][b], 0, 0, 0);
@@ -1587,14 +1665,14 @@ __global__ __launch_bounds__(512, 1) void glm_wide_gram256_kernel(const float* _
   };
   if (nt == 0) return;
   // prologue: chunk 0 in buffer 0, chunk 1's values in flight
-  if (tid < WG2_KR) sW[tid] = load_w(0);
+  if (tid < KR) sW[tid] = load_w(0);
   load_x(0);
   __syncthreads();
   store(0);
-  if (tid < WG2_KR) sW[WG2_KR + tid] = nt > 1 ? load_w(1) : 0.f;
+  if (tid < KR) sW[KR + tid] = nt > 1 ? load_w(1) : 0.f;
   __syncthreads();
   if (nt > 1) load_x(1);
-  if (tid < WG2_KR && nt > 2) wpre = load_w(2);
+  if (tid < KR && nt > 2) wpre = load_w(2);
   // chunk groups of `fold` with the fold between them; every chunk runs
   // the same straight-line body (a diagonal tile's skipped quarter computes
   // and is never folded; the store past the last chunk writes the unused
@@ -1604,10 +1682,10 @@ __global__ __launch_bounds__(512, 1) void glm_wide_gram256_kernel(const float* _
     for (long long t = t0; t < t1; ++t) {
       const int cur = (int)(t & 1);
       compute_store(cur, cur ^ 1);
-      if (tid < WG2_KR) sW[cur * WG2_KR + tid] = wpre;   // weights of chunk t + 2 (buffer cur is free after the barrier)
+      if (tid < KR) sW[cur * KR + tid] = wpre;   // weights of chunk t + 2 (buffer cur is free after the barrier)
       __syncthreads();
       load_x(t + 2);
-      if (tid < WG2_KR) wpre = load_w(t + 3);
+      if (tid < KR) wpre = load_w(t + 3);
     }
     if (!skip) fold_out();
   }
@@ -1622,20 +1700,31 @@ extern "C" int h2o_glm_wide_gram256(const float* X, int ldx, int P, long long N,
   if (ldx < P || S <= 0 || fold <= 0) return -1;
   const int NB = (P + 1 + WG2_T - 1) / WG2_T;
   const int npairs = NB * (NB + 1) / 2;
-  const size_t lds = 2 * WG2_BUF * sizeof(__bf16) + 2 * WG2_KR * sizeof(float);
+  // bf16 tier chunk rows (H2O3_WIDE_KR = 32 / 64, default 64)
+  static const int kr16 = getenv("H2O3_WIDE_KR") && atoi(getenv("H2O3_WIDE_KR")) == 32 ? 32 : 64;
+  const int KR = bf3 ? 32 : kr16;
+  const size_t lds = 2 * (size_t)(bf3 ? 4 : 2) * WG2_T * KR * sizeof(__bf16) + 2 * KR * sizeof(float);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)glm_wide_gram256_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
-    (void)hipFuncSetAttribute((const void*)glm_wide_gram256_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
+    const size_t l3 = 2 * 4 * WG2_T * 32 * sizeof(__bf16) + 2 * 32 * sizeof(float);
+    const size_t l32 = 2 * 2 * WG2_T * 32 * sizeof(__bf16) + 2 * 32 * sizeof(float);
+    const size_t l64 = 2 * 2 * WG2_T * 64 * sizeof(__bf16) + 2 * 64 * sizeof(float);
+    (void)hipFuncSetAttribute((const void*)glm_wide_gram256_kernel<true, 32>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)l3);
+    (void)hipFuncSetAttribute((const void*)glm_wide_gram256_kernel<false, 32>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)l32);
+    (void)hipFuncSetAttribute((const void*)glm_wide_gram256_kernel<false, 64>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)l64);
     attr = true;
   }
   if (bf3)
-    hipLaunchKernelGGL(glm_wide_gram256_kernel<true>, dim3(npairs * S), dim3(512), lds, s, X, ldx, P, N, Wr, NB,
+    hipLaunchKernelGGL((glm_wide_gram256_kernel<true, 32>), dim3(npairs * S), dim3(512), lds, s, X, ldx, P, N, Wr, NB,
                        npairs, S, fold, part, dbg);
+  else if (KR == 32)
+    hipLaunchKernelGGL((glm_wide_gram256_kernel<false, 32>), dim3(npairs * S), dim3(512), lds, s, X, ldx, P, N, Wr,
+                       NB, npairs, S, fold, part, dbg);
   else
-    hipLaunchKernelGGL(glm_wide_gram256_kernel<false>, dim3(npairs * S), dim3(512), lds, s, X, ldx, P, N, Wr, NB,
-                       npairs, S, fold, part, dbg);
+    hipLaunchKernelGGL((glm_wide_gram256_kernel<false, 64>), dim3(npairs * S), dim3(512), lds, s, X, ldx, P, N, Wr,
+                       NB, npairs, S, fold, part, dbg);
   return (int)hipGetLastError();
 }

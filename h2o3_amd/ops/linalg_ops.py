@@ -26,6 +26,7 @@ def _lib():
         lib.h2o_gram_split.argtypes = [P, I, I, I, P, P, LL, P, P]
         lib.h2o_glm_wide_split.argtypes = [P, I, I, I, LL, P, F, P, P, P, I, I, F, F, P, P, I, P, P, P]
         lib.h2o_glm_wide_gram.argtypes = [P, I, I, LL, P, I, I, P, I, P]
+        lib.h2o_glm_wide_split_grid.argtypes = [I]
         lib.h2o_glm_wide_gram256.argtypes = [P, I, I, LL, P, I, I, P, I, I, P]
         lib._typed = True
     return lib
@@ -387,6 +388,17 @@ def wide_gram(X, P, wr, stream=None, bf3=True):
         return _wide_gram_assemble(part, S, NB, P, T)
 
 
+_SPLIT_GRID = {}
+
+
+def _wide_split_grid(lib, Pa):
+    key = (torch.cuda.current_device(), Pa)
+    if key not in _SPLIT_GRID:
+        g = int(lib.h2o_glm_wide_split_grid(Pa))
+        _SPLIT_GRID[key] = g if g > 0 else 2048
+    return _SPLIT_GRID[key]
+
+
 def glm_wide_irls(X, P, beta, b0, y, wprior=None, offset=None, codes=(1, 1), tvp=0.0, theta=1e-10, step=1 << 19,
                   fused=False, bf3=True):
     """Fused IRLS pass for wide GLMs (P + 2 <= 1024).
@@ -417,7 +429,12 @@ def glm_wide_irls(X, P, beta, b0, y, wprior=None, offset=None, codes=(1, 1), tvp
     nch = -(-N // st)
     if fused:
         from ..utils.timer import phase
-        blocks = 2048
+        # one launch over every row (the kernel folds its f32 gradient
+        # products into f64 every 64 rows), on a grid of whole resident
+        # rounds: 24 launches of 2048 workgroups took 10.5 ms at 12.5M x 1000,
+        # one launch of 768 takes 8.1 ms (scripts/wide_eta_mb.py)
+        st, nch = max(N, 1), 1
+        blocks = int(os.environ.get("H2O3_WIDE_ETA_BLOCKS", "0")) or _wide_split_grid(lib, Pa)
         dev = torch.zeros((nch, blocks), dtype=torch.float64, device=X.device)
         gbuf = torch.zeros((blocks, Pa), dtype=torch.float64, device=X.device)
         wr = torch.empty(N, dtype=torch.float32, device=X.device)

@@ -18,7 +18,10 @@ lib = linalg_ops._lib()
 X = torch.randn(N, P, device="cuda")
 w = torch.rand(N, device="cuda")
 stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-for T, S, dbg, bf3 in ((256, 25, 0, 1), (256, 25, 1, 1), (256, 25, 0, 0), (256, 25, 1, 0), (128, 14, 0, 1)):
+arms = ((256, 25, 0, 1), (256, 25, 1, 1), (256, 25, 0, 0), (256, 25, 1, 0), (128, 14, 0, 1))
+if os.environ.get("MB_ARMS") == "bf16":
+    arms = ((256, 25, 0, 0), (256, 25, 1, 0))
+for T, S, dbg, bf3 in arms:
     NB = -(-(P + 1) // T)
     npairs = NB * (NB + 1) // 2
     part = torch.zeros((npairs * S, T, T), dtype=torch.float64, device="cuda")
@@ -35,4 +38,5 @@ for T, S, dbg, bf3 in ((256, 25, 0, 1), (256, 25, 1, 1), (256, 25, 0, 0), (256, 
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / 3
-    print(f"T={T} S={S:3d} dbg={dbg} bf3={bf3}: {ms:7.2f} ms/launch", flush=True)
+    kr = 32 if bf3 or os.environ.get("H2O3_WIDE_KR") == "32" else 64
+    print(f"T={T} S={S:3d} dbg={dbg} bf3={bf3} KR={kr}: {ms:7.2f} ms/launch", flush=True)

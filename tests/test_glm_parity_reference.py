@@ -53,3 +53,24 @@ def test_glm_prostate_binomial_matches_reference(prostate, max_iterations):
     assert m.aic() == pytest.approx(396.3, abs=0.1)
     # GLMTest.java:1721, :1726: bestSubmodel().iteration == 5 (converged) / == 4 (capped)
     assert m._output["model_summary"]["number_of_iterations"] == (5 if max_iterations is None else 4)
+
+
+def test_scaled_cond_device_estimator_matches_lapack():
+    """GLMDriver._scaled_cond_dev (Hager's estimate on a torch Cholesky, the
+    device path of the wide IRLS system) equals LAPACK dpocon's estimate
+    (_scaled_cond), including a zero-variance column left out of both."""
+    import numpy as np
+    import torch
+    from h2o3_amd.models.glm.glm import GLMDriver
+    g = np.random.default_rng(3)
+    for n, P in ((2000, 50), (5000, 300)):
+        X = g.standard_normal((n, P)) * np.exp(g.uniform(-2, 2, P))
+        X[:, 1] = X[:, 0] + 0.05 * g.standard_normal(n)
+        X[:, 7] = 0.0
+        A = X.T @ X
+        want = GLMDriver._scaled_cond(A)
+        got = GLMDriver._scaled_cond_dev(torch.from_numpy(A))
+        assert got == pytest.approx(want, rel=1e-8)
+    assert GLMDriver._scaled_cond_dev(torch.from_numpy(-np.eye(4))) == 1.0
+    bad = np.ones((3, 3))
+    assert GLMDriver._scaled_cond_dev(torch.from_numpy(bad)) == float("inf")
