@@ -634,6 +634,12 @@ class GLMDriver:
         s = d.rsqrt()
         S = A * s.view(-1, 1) * s.view(1, -1)
         L, info = torch.linalg.cholesky_ex(S)
+        return GLMDriver._hager_kappa(S, L, info)
+
+    @staticmethod
+    def _hager_kappa(S, L, info):
+        """||S||_1 * est(||S^-1||_1) from the Cholesky factor L of S (Hager /
+        Higham: at most 5 steps of two triangular solve pairs)."""
         anorm = S.abs().sum(0).max()
         n = S.shape[0]
         x = torch.full((n, 1), 1.0 / n, dtype=S.dtype, device=S.device)
@@ -656,6 +662,17 @@ class GLMDriver:
         kappa = est * float(h[5])
         return kappa if np.isfinite(kappa) and kappa > 0 else float("inf")
 
+    @staticmethod
+    def _kappa_from_factor(A, L, info):
+        """Scaled condition estimate of A reusing its Cholesky factor: the
+        factor of S = D A D (D = diag(A)^-1/2) is D L, so the tier check costs
+        no second factorization.  A failed factor (a zero-variance column,
+        or indefinite) goes through _scaled_cond_dev's column filter."""
+        if int(info) != 0:
+            return GLMDriver._scaled_cond_dev(A)
+        s = A.diagonal().rsqrt()
+        return GLMDriver._hager_kappa(A * s.view(-1, 1) * s.view(1, -1), L * s.view(-1, 1), info)
+
     def _dev_system_ok(self):
         """The IRLS system of this step can be built, conditioned and solved
         on the device: wide designs (the host f64 Cholesky of a 1001^2
@@ -670,23 +687,14 @@ class GLMDriver:
                 and not p.get("remove_collinear_columns") and not p.get("non_negative")
                 and not p.get("_nonneg_names"))
 
-    def _step_solve_dev(self, Gn, bn, l2):
-        """Ridge Newton step on the device: (max |gradient|, new beta) with
-        one host read; None when the Cholesky fails (the host solver's
-        relative-ridge retries take over)."""
-        k = Gn.shape[0]
+    def _step_solve_dev(self, Gn, bn, l2, L, info):
+        """Ridge Newton step on the device from the factor L of Gn + ridge:
+        (max |gradient|, new beta) with one host read; new is None when the
+        Cholesky failed (the host solver's relative-ridge retries take over)."""
         bcur = self.beta if self.intercept else self.beta[:-1]
         bt = torch.as_tensor(bcur, dtype=torch.float64).to(Gn.device, non_blocking=True)
         gq = Gn @ bt - bn
         gq[:self.P] += l2 * bt[:self.P]
-        A = Gn
-        if l2 != 0:
-            A = Gn.clone()
-            pen = torch.full((k,), l2, dtype=A.dtype, device=A.device)
-            if self.intercept:
-                pen[-1] = 0.0
-            A.diagonal().add_(pen)
-        L, info = torch.linalg.cholesky_ex(A)
         new = torch.cholesky_solve(bn.view(-1, 1), L).view(-1)
         h = torch.cat([info.to(torch.float64).view(1), gq.abs().max().view(1), new]).cpu().numpy()
         if h[0] != 0 or not np.all(np.isfinite(h[2:])):
@@ -893,26 +901,17 @@ class GLMDriver:
             bn += (self.rho * self.beta_given)[:k]
         return Gn, bn, l1, l2
 
-    def _check_tier(self, Ga, b):
-        """Hessian precision tier from the scaled condition number of this
-        iteration's system (checked at iterations 1, 2, 4, 8, ...); when the
-        tier must rise, the statistics are recomputed at the new tier."""
+    def _tiers_due(self):
+        """The tier is (re)checked at iterations 1, 2, 4, 8, ... on the GPU."""
         if self.X.device.type != "cuda" or os.environ.get("H2O3_GLM_TIERS", "1") == "0":
-            return Ga, b
+            return False
         it = self.iter + 1
-        if it & (it - 1):
-            return Ga, b
-        Gn, _, _, l2 = self._system(Ga, b)
-        if torch.is_tensor(Gn):
-            if l2 > 0:
-                Gn = Gn.clone()
-                Gn.diagonal()[:self.P] += l2
-            kappa = self._scaled_cond_dev(Gn)
-        else:
-            if l2 > 0:
-                Gn = Gn.copy()
-                Gn[np.arange(self.P), np.arange(self.P)] += l2
-            kappa = self._scaled_cond(Gn, self.active)
+        return not (it & (it - 1))
+
+    def _tier_raise(self, kappa):
+        """Records kappa; returns the tier the statistics must be recomputed
+        at when this one is too low for kappa (and switches to it), else
+        None."""
         self.hessian_kappa = kappa
         order = [t for t, _ in self._TIER_LIMITS]
         wide = not self._native()
@@ -929,12 +928,66 @@ class GLMDriver:
             want = "f64"
         if order.index(want) > order.index(cur):
             self._hprec = want
+            return want
+        if self._hprec is None:
+            self._hprec = cur
+        return None
+
+    def _check_tier(self, Ga, b):
+        """Hessian precision tier from the scaled condition number of this
+        iteration's system (checked at iterations 1, 2, 4, 8, ...); when the
+        tier must rise, the statistics are recomputed at the new tier."""
+        if not self._tiers_due():
+            return Ga, b
+        Gn, _, _, l2 = self._system(Ga, b)
+        if l2 > 0:
+            Gn = Gn.copy()
+            Gn[np.arange(self.P), np.arange(self.P)] += l2
+        want = self._tier_raise(self._scaled_cond(Gn, self.active))
+        if want is not None:
             Ga, b, dev = self._irls_stats()
             self._stats_dev = dev
             return self._check_tier(Ga, b) if want != "f64" else (Ga, b)
-        if self._hprec is None:
-            self._hprec = cur
         return Ga, b
+
+    def _ridge_system_dev(self, Ga, b):
+        """Device system (Gn, bn, l1, l2), A = Gn + the ridge on the
+        penalized diagonal, and A's Cholesky factor."""
+        Gn, bn, l1, l2 = self._system(Ga, b)
+        A = Gn
+        if l2 != 0:
+            A = Gn.clone()
+            pen = torch.full((A.shape[0],), l2, dtype=A.dtype, device=A.device)
+            if self.intercept:
+                pen[-1] = 0.0
+            A.diagonal().add_(pen)
+        L, info = torch.linalg.cholesky_ex(A)
+        return Gn, bn, l1, l2, A, L, info
+
+    def _step_dev(self, Ga, b):
+        """Device-resident step: ONE f64 Cholesky per system serves both the
+        tier check (scaled-condition estimate from the same factor) and the
+        Newton solve; the statistics are recomputed only when the tier rises."""
+        check = True
+        while True:
+            with phase("glm.system"):
+                Gn, bn, l1, l2, A, L, info = self._ridge_system_dev(Ga, b)
+            if not (check and self._tiers_due()):
+                break
+            with phase("glm.tier"):
+                want = self._tier_raise(self._kappa_from_factor(A, L, info))
+            if want is None:
+                break
+            self._sys_on_dev = True
+            try:
+                Ga, b, dev = self._irls_stats()
+            finally:
+                self._sys_on_dev = False
+            self._stats_dev = dev
+            check = want != "f64"
+        with phase("glm.solve"):
+            gmax, new = self._step_solve_dev(Gn, bn, l2, L, info)
+        return Gn, bn, l1, l2, gmax, new
 
     def step(self):
         """One IRLS iteration (Gram on the matrix cores + host solve; wide
@@ -942,20 +995,21 @@ class GLMDriver:
         self._sys_on_dev = self._dev_system_ok()
         try:
             Ga, b, dev = self._irls_stats()
-            self._stats_dev = dev
-            with phase("glm.tier"):
-                Ga, b = self._check_tier(Ga, b)
         finally:
             self._sys_on_dev = False
-        dev = self._stats_dev
-        with phase("glm.system"):
-            Gn, bn, l1, l2 = self._system(Ga, b)
-        if torch.is_tensor(Gn):
-            with phase("glm.solve"):
-                gmax, new = self._step_solve_dev(Gn, bn, l2)
+        self._stats_dev = dev
+        if torch.is_tensor(Ga):
+            Gn, bn, l1, l2, gmax, new = self._step_dev(Ga, b)
             if new is not None:
-                return self._finish_step(new, gmax, dev, l1, l2)
+                return self._finish_step(new, gmax, self._stats_dev, l1, l2)
             Gn, bn = Gn.cpu().numpy(), bn.cpu().numpy()
+            dev = self._stats_dev
+        else:
+            with phase("glm.tier"):
+                Ga, b = self._check_tier(Ga, b)
+            dev = self._stats_dev
+            with phase("glm.system"):
+                Gn, bn, l1, l2 = self._system(Ga, b)
         if self.est._parms.get("remove_collinear_columns") and self.active is None:
             self.active = self._find_collinear(Gn)
             self.removed_cols = [self.dinfo.coef_names[i] for i in range(self.P) if not self.active[i]]

@@ -74,3 +74,24 @@ def test_scaled_cond_device_estimator_matches_lapack():
     assert GLMDriver._scaled_cond_dev(torch.from_numpy(-np.eye(4))) == 1.0
     bad = np.ones((3, 3))
     assert GLMDriver._scaled_cond_dev(torch.from_numpy(bad)) == float("inf")
+
+
+def test_kappa_from_shared_factor_matches_lapack():
+    """The device step's tier check reuses the solve's Cholesky factor
+    (factor of D A D = D L): same estimate as LAPACK on the scaled matrix;
+    a failed factor falls back to the filtered estimate."""
+    import numpy as np
+    import torch
+    from h2o3_amd.models.glm.glm import GLMDriver
+    g = np.random.default_rng(5)
+    X = g.standard_normal((3000, 200)) * np.exp(g.uniform(-3, 3, 200))
+    X[:, 5] = X[:, 4] + 0.01 * g.standard_normal(3000)
+    A = X.T @ X
+    At = torch.from_numpy(A)
+    L, info = torch.linalg.cholesky_ex(At)
+    assert GLMDriver._kappa_from_factor(At, L, info) == pytest.approx(GLMDriver._scaled_cond(A), rel=1e-8)
+    A[:, 9] = A[9, :] = 0.0
+    At = torch.from_numpy(A)
+    L, info = torch.linalg.cholesky_ex(At)
+    assert int(info) != 0
+    assert GLMDriver._kappa_from_factor(At, L, info) == pytest.approx(GLMDriver._scaled_cond(A), rel=1e-8)
