@@ -1538,7 +1538,6 @@ __global__ __launch_bounds__(512, 1) void glm_wide_gram256_kernel(const float* _
   constexpr int NRG = KR / 8;                      // 8-row groups per chunk
   constexpr int NQ = NRG;                          // (panel, row group) slices per thread: 2 panels x NRG / 2
   extern __shared__ __bf16 wg2_lds[];
-  float* sW = reinterpret_cast<float*>(wg2_lds + 2 * BUF);   // [2][KR] row weights
   const int nblk = npairs * S;
   const int L = xcd_remap(blockIdx.x, nblk);
   const int sl = L / npairs, pr = L - sl * npairs;
@@ -1558,8 +1557,20 @@ __global__ __launch_bounds__(512, 1) void glm_wide_gram256_kernel(const float* _
   const float fillA = gcA == P ? 1.f : 0.f, fillB = gcB == P ? 1.f : 0.f;
   const bool inA = gcA < P, inB = gcB < P;
   float xr[NQ][8];
-  float wpre = 0.f;
-  auto load_x = [&](long long t) {
+  // row weights of the panel-A row groups of the chunk being converted next:
+  // wave-uniform, so they come in by scalar loads (no LDS staging, no LDS
+  // wait inside the MFMA stream).  Wr holds N rounded up to KR, zero past N.
+  typedef float f32x8 __attribute__((ext_vector_type(8)));
+  f32x8 wq[NQ / 2];
+  const long long npad = (N + KR - 1) / KR * KR;
+  auto load_wq = [&](long long t) __attribute__((always_inline)) {
+    long long row0 = (sl + t * S) * KR;
+    row0 = row0 < npad ? row0 : 0;                 // prefetch past the last chunk: any in-bounds rows
+#pragma unroll
+    for (int q = 0; q < NQ / 2; ++q)
+      wq[q] = *reinterpret_cast<const f32x8*>(Wr + row0 + (t8 + 2 * q) * 8);
+  };
+  auto load_x = [&](long long t) __attribute__((always_inline)) {
     const long long row0 = (sl + t * S) * KR;
     const long long left = N - row0;
     const int nr = (int)(left < KR ? (left > 0 ? left : 0) : KR);   // past N: every load reads 0
@@ -1573,22 +1584,18 @@ __global__ __launch_bounds__(512, 1) void glm_wide_gram256_kernel(const float* _
         xr[q][e] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rx, (pan ? gcB : gcA) * 4, (rg * 8 + e) * ldx * 4, 0));
     }
   };
-  auto load_w = [&](long long t) -> float {   // threads < 32: the chunk's row weight (0 past N)
-    const long long row0 = (sl + t * S) * KR;
-    const long long left = N - row0;
-    const int nr = (int)(left < KR ? (left > 0 ? left : 0) : KR);
-    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)(Wr + row0), (short)0, nr * 4, 0x00020000);
-    return __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rw, tid * 4, 0, 0));
-  };
-  auto store_q = [&](int buf, int q) {
+  // FULL (wave-uniform): every column of this wave's loader slice is < P in
+  // both panels, so the conversion needs no per-element fill select
+  auto store_q = [&](int buf, int q, auto fullc) __attribute__((always_inline)) {
     __bf16* base = wg2_lds + buf * BUF;
-    const float* w = sW + buf * KR;
     const int pan = q / (NQ / 2), rg = t8 + 2 * (q % (NQ / 2));
     bf16x8 h, l;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      float x = (pan ? inB : inA) ? xr[q][e] : (pan ? fillB : fillA);
-      if (!pan) x *= w[rg * 8 + e];
+      float x;
+      if constexpr (decltype(fullc)::value) x = xr[q][e];
+      else x = (pan ? inB : inA) ? xr[q][e] : (pan ? fillB : fillA);
+      if (!pan) x *= wq[q][e];
       h[e] = (__bf16)x;
       if constexpr (BF3) l[e] = (__bf16)(x - (float)h[e]);
     }
@@ -1596,9 +1603,9 @@ __global__ __launch_bounds__(512, 1) void glm_wide_gram256_kernel(const float* _
     *reinterpret_cast<bf16x8*>(base + (pan ? PBH : 0) * WG2_T * KR + off) = h;
     if constexpr (BF3) *reinterpret_cast<bf16x8*>(base + (pan ? 3 : 1) * WG2_T * KR + off) = l;
   };
-  auto store = [&](int buf) {
+  auto store = [&](int buf, auto fullc) __attribute__((always_inline)) {
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) store_q(buf, q);
+    for (int q = 0; q < NQ; ++q) store_q(buf, q, fullc);
   };
   f32x16 acc[4][2];
 #pragma unroll
@@ -1608,10 +1615,12 @@ __global__ __launch_bounds__(512, 1) void glm_wide_gram256_kernel(const float* _
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
   double* my = part + (size_t)L * (WG2_T * WG2_T);
-  auto fold_out = [&]() {
+  auto fold_out = [&]() __attribute__((always_inline)) {
     // opaque copies: the 128 fold addresses are not loop-invariant for the
     // compiler, so they are not hoisted out of the chunk loop into registers
-    double* mb = my;
+    const unsigned long long mu = (unsigned long long)my;
+    double* mb = (double*)(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(mu >> 32)) << 32) |
+                           (unsigned)__builtin_amdgcn_readfirstlane((unsigned)mu));
     int ln = lane;
     asm volatile("" : "+s"(mb), "+v"(ln));
 #pragma unroll
@@ -1631,7 +1640,7 @@ __global__ __launch_bounds__(512, 1) void glm_wide_gram256_kernel(const float* _
   // one chunk's MFMAs on buffer `buf`, with the conversion + store of the
   // next chunk's q-th slice into buffer `nbuf` after each (ks, b) sub-step:
   // straight-line code, so the scheduler interleaves VALU with the MFMAs
-  auto compute_store = [&](int buf, int nbuf) {
+  auto compute_store = [&](int buf, int nbuf, auto fullc) __attribute__((always_inline)) {
     const __bf16* sAh = wg2_lds + buf * BUF;
     const __bf16* sAl = sAh + WG2_T * KR;
     const __bf16* sBh = sAh + PBH * WG2_T * KR;
@@ -1659,36 +1668,39 @@ __global__ __launch_bounds__(512, 1) void glm_wide_gram256_kernel(const float* _
 #pragma unroll
           for (int a = 0; a < 4; ++a) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[a], bh, acc[a][b], 0, 0, 0);
         }
-        store_q(nbuf, 2 * ks + b);
+        store_q(nbuf, 2 * ks + b, fullc);
       }
     }
   };
   if (nt == 0) return;
-  // prologue: chunk 0 in buffer 0, chunk 1's values in flight
-  if (tid < KR) sW[tid] = load_w(0);
-  load_x(0);
-  __syncthreads();
-  store(0);
-  if (tid < KR) sW[KR + tid] = nt > 1 ? load_w(1) : 0.f;
-  __syncthreads();
-  if (nt > 1) load_x(1);
-  if (tid < KR && nt > 2) wpre = load_w(2);
-  // chunk groups of `fold` with the fold between them; every chunk runs
-  // the same straight-line body (a diagonal tile's skipped quarter computes
-  // and is never folded; the store past the last chunk writes the unused
-  // buffer), so MFMA and conversion interleave within one basic block
-  for (long long t0 = 0; t0 < nt; t0 += fold) {
-    const long long t1 = t0 + fold < nt ? t0 + fold : nt;
-    for (long long t = t0; t < t1; ++t) {
-      const int cur = (int)(t & 1);
-      compute_store(cur, cur ^ 1);
-      if (tid < KR) sW[cur * KR + tid] = wpre;   // weights of chunk t + 2 (buffer cur is free after the barrier)
-      __syncthreads();
-      load_x(t + 2);
-      if (tid < KR) wpre = load_w(t + 3);
+  const int wbase = (tid & 255) & ~63;              // this wave's first loader column
+  const bool full = bi * WG2_T + wbase + 63 < P && bj * WG2_T + wbase + 63 < P;
+  auto run = [&](auto fullc) __attribute__((always_inline)) {
+    // prologue: chunk 0 in buffer 0, chunk 1's values and weights in flight
+    load_wq(0);
+    load_x(0);
+    store(0, fullc);
+    __syncthreads();
+    if (nt > 1) load_x(1);
+    load_wq(1);
+    // chunk groups of `fold` with the fold between them; every chunk runs
+    // the same straight-line body (a diagonal tile's skipped quarter computes
+    // and is never folded; the store past the last chunk writes the unused
+    // buffer), so MFMA and conversion interleave within one basic block
+    for (long long t0 = 0; t0 < nt; t0 += fold) {
+      const long long t1 = t0 + fold < nt ? t0 + fold : nt;
+      for (long long t = t0; t < t1; ++t) {
+        const int cur = (int)(t & 1);
+        compute_store(cur, cur ^ 1, fullc);
+        __syncthreads();
+        load_x(t + 2);
+        load_wq(t + 2);
+      }
+      if (!skip) fold_out();
     }
-    if (!skip) fold_out();
-  }
+  };
+  if (__builtin_amdgcn_readfirstlane(full ? 1 : 0)) run(std::true_type{});
+  else run(std::false_type{});
 }
 
 // bf3 = 0: one bf16 MFMA per product (hi * hi, ~2^-9 relative): the
@@ -1703,12 +1715,12 @@ extern "C" int h2o_glm_wide_gram256(const float* X, int ldx, int P, long long N,
   // bf16 tier chunk rows (H2O3_WIDE_KR = 32 / 64, default 64)
   static const int kr16 = getenv("H2O3_WIDE_KR") && atoi(getenv("H2O3_WIDE_KR")) == 32 ? 32 : 64;
   const int KR = bf3 ? 32 : kr16;
-  const size_t lds = 2 * (size_t)(bf3 ? 4 : 2) * WG2_T * KR * sizeof(__bf16) + 2 * KR * sizeof(float);
+  const size_t lds = 2 * (size_t)(bf3 ? 4 : 2) * WG2_T * KR * sizeof(__bf16);
   static bool attr = false;
   if (!attr) {
-    const size_t l3 = 2 * 4 * WG2_T * 32 * sizeof(__bf16) + 2 * 32 * sizeof(float);
-    const size_t l32 = 2 * 2 * WG2_T * 32 * sizeof(__bf16) + 2 * 32 * sizeof(float);
-    const size_t l64 = 2 * 2 * WG2_T * 64 * sizeof(__bf16) + 2 * 64 * sizeof(float);
+    const size_t l3 = 2 * 4 * WG2_T * 32 * sizeof(__bf16);
+    const size_t l32 = 2 * 2 * WG2_T * 32 * sizeof(__bf16);
+    const size_t l64 = 2 * 2 * WG2_T * 64 * sizeof(__bf16);
     (void)hipFuncSetAttribute((const void*)glm_wide_gram256_kernel<true, 32>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)l3);
     (void)hipFuncSetAttribute((const void*)glm_wide_gram256_kernel<false, 32>,

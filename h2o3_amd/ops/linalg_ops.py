@@ -363,6 +363,12 @@ def wide_gram(X, P, wr, stream=None, bf3=True):
     lib = _lib()
     N, ldx = X.shape
     T = int(os.environ.get("H2O3_WIDE_TILE", 256))
+    npad = -(-N // 64) * 64
+    if wr.numel() < npad or wr.data_ptr() % 32:
+        # the 256-tile kernel reads whole 64-row chunks of weights (zero past N)
+        w2 = torch.zeros(npad, dtype=torch.float32, device=wr.device)
+        w2[:N] = wr[:N]
+        wr = w2
     NB = -(-(P + 1) // T)
     npairs = NB * (NB + 1) // 2
     from ..utils.timer import phase
@@ -437,7 +443,10 @@ def glm_wide_irls(X, P, beta, b0, y, wprior=None, offset=None, codes=(1, 1), tvp
         blocks = int(os.environ.get("H2O3_WIDE_ETA_BLOCKS", "0")) or _wide_split_grid(lib, Pa)
         dev = torch.zeros((nch, blocks), dtype=torch.float64, device=X.device)
         gbuf = torch.zeros((blocks, Pa), dtype=torch.float64, device=X.device)
-        wr = torch.empty(N, dtype=torch.float32, device=X.device)
+        # row weights, zero-padded to whole 64-row chunks (the Gram kernel
+        # reads each chunk's weights with scalar vector loads)
+        wr = torch.empty(-(-N // 64) * 64, dtype=torch.float32, device=X.device)
+        wr[N:].zero_()
         stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
         offp = lambda t, a: ctypes.c_void_p(0 if t is None else t.data_ptr() + a * 4)
         with phase("glm.wide_eta"):

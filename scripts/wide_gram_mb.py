@@ -16,7 +16,8 @@ N = int(sys.argv[1]) if len(sys.argv) > 1 else 12_500_000
 P = 1000
 lib = linalg_ops._lib()
 X = torch.randn(N, P, device="cuda")
-w = torch.rand(N, device="cuda")
+w = torch.zeros(-(-N // 64) * 64, device="cuda")   # weights zero-padded to whole 64-row chunks
+w[:N] = torch.rand(N, device="cuda")
 stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 arms = ((256, 25, 0, 1), (256, 25, 1, 1), (256, 25, 0, 0), (256, 25, 1, 0), (128, 14, 0, 1))
 if os.environ.get("MB_ARMS") == "bf16":
