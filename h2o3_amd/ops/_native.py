@@ -56,6 +56,18 @@ def _needs_build(src: str, out: str, deps=()) -> bool:
     return False
 
 
+def _source_flags(src: str) -> list[str]:
+    """Extra compiler flags a source asks for on a `// hipcc-flags: ...` line
+    among its first 40 lines."""
+    with open(src) as f:
+        for i, line in enumerate(f):
+            if i >= 40:
+                break
+            if line.startswith("// hipcc-flags:"):
+                return line.split(":", 1)[1].split()
+    return []
+
+
 def build_one_hip(fname: str, force: bool = False, verbose: bool = False) -> str:
     src = os.path.join(CSRC, fname)
     name = os.path.splitext(fname)[0]
@@ -64,7 +76,8 @@ def build_one_hip(fname: str, force: bool = False, verbose: bool = False) -> str
     if force or _needs_build(src, out, headers):
         os.makedirs(LIBDIR, exist_ok=True)
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC",
-               "-ffp-contract=fast", "-I", CSRC, "-o", out + ".tmp", src]
+               "-ffp-contract=fast", *_source_flags(src), *os.environ.get("H2O3_HIPCC_EXTRA", "").split(),
+               "-I", CSRC, "-o", out + ".tmp", src]
         if verbose:
             print(" ".join(cmd))
         subprocess.run(cmd, check=True)
