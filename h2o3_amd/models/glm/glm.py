@@ -539,7 +539,8 @@ class GLMDriver:
             self._w32 = None if bool((self.w == 1).all()) else self.w.to(torch.float32)
             self._off32 = None if self.offset is None else self.offset.to(torch.float32)
         self._gexact = None
-        bf3 = None if self._hprec is None else self._hprec == "bf3"
+        hp = self._hprec or ("bf16" if codes is not None and self._narrow_bf16_ok() else None)
+        bf3 = None if hp is None else ("bf16" if hp == "bf16" else hp == "bf3")
         with phase("glm.irls_pass"):
             if codes is not None:
                 bt = torch.zeros(self.Pp, dtype=torch.float32, device=self.X.device)
@@ -551,7 +552,7 @@ class GLMDriver:
                                                       y=self._y32, wprior=self._w32, offset=self._off32,
                                                       codes=codes, tvp=self.fam.tvp, theta=self.fam.theta,
                                                       width=self.Pp, grad=True, bf3=bf3,
-                                                      grad_f64=self._hprec not in (None, "bf3"))
+                                                      grad_f64=self._hprec not in (None, "bf3", "bf16"))
                     self._gexact = torch.cat([gx[:P], gx[self.Pp:self.Pp + 1]])
                     self._gbeta = np.concatenate([self.beta[:P].astype(np.float32).astype(np.float64),
                                                   [float(np.float32(self.beta[-1]))]])
@@ -575,11 +576,19 @@ class GLMDriver:
     # Hessian precision tiers of the Newton step beta + H^-1 g (g from the exact
     # gradient channel): the iteration contracts at rate ~ kappa * eps(H), so the
     # tier is picked from the Jacobi-scaled condition number kappa of the system
-    # matrix.  Plain bf16 MFMA (eps ~ 4e-3, the fused wide Gram only) while
+    # matrix.  Plain bf16 MFMA (eps ~ 4e-3; the fused wide Gram and the P + 2 <= 128
+    # fused pass, both beside the exact gradient) while
     # kappa < 32, bf16x3 MFMA (eps ~ 2e-5) while kappa < 2e3, f32 MFMA
     # (eps ~ 1e-7) while kappa < 5e5, beyond that fp64 (the reference's Gram
     # precision, hex/gram/Gram.java:17) on the device's f64 GEMMs.
     _TIER_LIMITS = (("bf16", 32.0), ("bf3", 2e3), ("f32", 5e5), ("f64", float("inf")))
+
+    def _narrow_bf16_ok(self):
+        """The plain-bf16 Hessian tier of the P + 2 <= 128 fused kernel
+        (glm_irls_ws_kernel LO = false): needs the exact-gradient channel and
+        the bf16 MFMA path (H2O3_GLM_BF16=0 or H2O3_GLM_BF3=0 disable it)."""
+        return self.Pp == 128 and linalg_ops.glm_grad_supported(self.Pp) and \
+            os.environ.get("H2O3_GLM_BF16", "1") != "0" and os.environ.get("H2O3_GLM_BF3", "1") != "0"
 
     def _wide_bf16_ok(self):
         """The plain-bf16 Hessian tier exists for the fused wide Gram only
@@ -916,7 +925,7 @@ class GLMDriver:
         order = [t for t, _ in self._TIER_LIMITS]
         wide = not self._native()
         cur = self._hprec
-        bf16_ok = wide and self._gexact is not None and self._wide_bf16_ok()
+        bf16_ok = self._gexact is not None and (self._wide_bf16_ok() if wide else self._narrow_bf16_ok())
         if cur is None:
             ws_bf3 = self.Pp == 128 and os.environ.get("H2O3_GLM_BF3", "1") != "0"
             cur = ("bf16" if bf16_ok else "bf3") if (ws_bf3 if not wide else self._gexact is not None) else "f32"

@@ -119,7 +119,7 @@ struct GlmFamArgs {
                 // bit2 skip y/w/offset loads, bit3 skip the eta dot products, bit4 eta and
                 // sqrt(W) by ds_bpermute instead of DPP + LDS (ws kernel)
   int signed_w; // external weights may be negative (no sqrt(W) pre-scaling)
-  int bf3;      // P = 128 ws path: bf16x3 MFMA operands instead of f32
+  int bf3;      // P = 128 ws path: 1 bf16x3 MFMA operands instead of f32, 2 one-MFMA bf16 (fused + gradient)
   int grad_f64; // exact-gradient channel: f64 products (1) or f32 products summed per chunk, f64 beyond (0)
 };
 
@@ -232,6 +232,11 @@ __device__ __forceinline__ void gi_mfma3_q(const bf16x8* ah, const bf16x8* al, f
     if constexpr (M == 1) acc[Q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[ti], al[tj], acc[Q], 0, 0, 0);
     if constexpr (M == 2) acc[Q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[ti], ah[tj], acc[Q], 0, 0, 0);
   }
+}
+// one-MFMA bf16 tier (hi*hi only, ~2^-9 relative per product)
+template <int T, int SL, int... Q>
+__device__ __forceinline__ void gi_mfma1_all(std::integer_sequence<int, Q...>, const bf16x8* ah, f32x4* acc) {
+  (gi_mfma3_q<T, SL, Q, 0>(ah, ah, acc), ...);
 }
 // all hi*hi first, then the two cross terms: consecutive MFMAs hit different
 // accumulators
@@ -498,7 +503,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 // of the bf16x3 Hessian G: its precision only sets the convergence rate.
 // Reference: hex/glm/GLMTask.java:1507 (GLMIterationTask, double _xy) and
 // hex/gram/Gram.java:17 (double _xx).
-template <int PP, bool FUSED, bool SQW, bool BF3>
+// LO = false (with BF3): the one-MFMA bf16 Hessian tier -- no lo plane, one
+// 16x16x32 MFMA per product instead of three (Newton on the exact gradient
+// still converges to the exact-gradient fixed point; the tier is chosen from
+// the condition number, glm.py _TIER_LIMITS)
+template <int PP, bool FUSED, bool SQW, bool BF3, bool LO = true>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) void glm_irls_ws_kernel(
     const float* __restrict__ X, long long N, int ldx, int n_pairs, int rows_per_block,
     const float* __restrict__ beta, float b0, const float* __restrict__ y, const float* __restrict__ wprior,
@@ -527,7 +536,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   constexpr int KS = 64;
   static_assert(!BF3 || (PP == 128 && SQW), "bf16x3 path: P = 128, sqrt(W)-scaled rows");
   __shared__ float L[2][BF3 ? 4 : RC * S];
-  __shared__ __attribute__((aligned(16))) __bf16 LB[2][2][BF3 ? PP * KS : 8];
+  __shared__ __attribute__((aligned(16))) __bf16 LB[2][LO ? 2 : 1][BF3 ? PP * KS : 8];
   __shared__ float wr[2][RC];
   __shared__ double dsum[4];
   // P = 128 producer scratch: eta partials [wave][row 16][quad 8] and the
@@ -746,7 +755,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       const float sq = SQW ? sqrtf(fmaxf(W, 0.f)) : 1.f;
       if constexpr (BF3) {
         __bf16* Hb = LB[c & 1][0];
-        __bf16* Lb2 = LB[c & 1][1];
+        __bf16* Lb2 = LB[c & 1][LO ? 1 : 0];
         const int par = lane / P4;
         // row j = 2 v + par: lanes < 16 publish sqrt(W) as [par][v], every
         // lane reads its 8 rows' factors as two broadcast b128
@@ -770,12 +779,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             const float x = V[v][e] * sv[v];
             const __bf16 hb = (__bf16)x;
             h[v] = hb;
-            l[v] = (__bf16)(x - (float)hb);
+            if constexpr (LO) l[v] = (__bf16)(x - (float)hb);
           }
           const int f = 4 * cq + e;
           const int off = f * KS + (((2 * pw + par) ^ gi_swz(f)) << 3);
           *reinterpret_cast<bf16x8*>(Hb + off) = h;
-          *reinterpret_cast<bf16x8*>(Lb2 + off) = l;
+          if constexpr (LO) *reinterpret_cast<bf16x8*>(Lb2 + off) = l;
         }
         if constexpr (GRAD) {
           if (want_grad) grad_acc(V, rres, qred);   // after the bf16 stores: the sqrt(W) factors are dead
@@ -787,9 +796,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
           const int k0 = aug * KS + ((((k >> 3) ^ gi_swz(aug)) << 3) | (k & 7));
           const int k1 = (aug + 1) * KS + ((((k >> 3) ^ gi_swz(aug + 1)) << 3) | (k & 7));
           Hb[k0] = h0;
-          Lb2[k0] = (__bf16)(a0 - (float)h0);
           Hb[k1] = h1;
-          Lb2[k1] = (__bf16)(a1 - (float)h1);
+          if constexpr (LO) {
+            Lb2[k0] = (__bf16)(a0 - (float)h0);
+            Lb2[k1] = (__bf16)(a1 - (float)h1);
+          }
         }
         return;
       }
@@ -897,7 +908,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         if constexpr (BF3) {
           if (!(fam.dbg & 1)) {
             const __bf16* Hb = LB[i & 1][0];
-            const __bf16* Lo = LB[i & 1][1];
+            const __bf16* Lo = LB[i & 1][LO ? 1 : 0];
             // feature f = 16 t + cc, k-block kr + 4 ks: gi_swz(f) = s0 ^ 4 (t & 1)
             // with s0 = gi_swz(cc), so the swizzled offset is one of two
             // per-lane bases (k-block bit 2 flipped by ks ^ t) + 16 t KS
@@ -912,9 +923,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
               for (int t = 0; t < T; ++t) {
                 const int off = 16 * t * KS + ((t & 1) ? Bo : Be);
                 ah[t] = *reinterpret_cast<const bf16x8*>(Hb + off);
-                al[t] = *reinterpret_cast<const bf16x8*>(Lo + off);
+                if constexpr (LO) al[t] = *reinterpret_cast<const bf16x8*>(Lo + off);
               }
-              gi_mfma3_all<T, SL>(std::make_integer_sequence<int, GI_PPW>{}, ah, al, acc);
+              if constexpr (LO) gi_mfma3_all<T, SL>(std::make_integer_sequence<int, GI_PPW>{}, ah, al, acc);
+              else gi_mfma1_all<T, SL>(std::make_integer_sequence<int, GI_PPW>{}, ah, acc);
             }
           }
         } else if (!(fam.dbg & 1)) {
@@ -963,6 +975,13 @@ static void gi_launch(bool fused, dim3 grid, hipStream_t s, const float* X, long
     // IRLS weights are >= 0 -> sqrt(W) pre-scaling; caller-signed weights
     // (e.g. X'r for lambda_max) take the explicit-multiply path
     if constexpr (PP == 128) {
+      if (fam.bf3 == 2 && !fam.signed_w && fused) {
+        // plain-bf16 Hessian tier (needs the exact gradient channel)
+        hipLaunchKernelGGL((glm_irls_ws_kernel<PP, true, true, true, false>), dim3(grid.x), dim3(512), 0, s, X, N,
+                           ldx, n_pairs, rpb, beta, b0, y, wprior, offset, fam, Wext, zext, aug, out, dev_out,
+                           grad_out);
+        return;
+      }
       if (fam.bf3 && !fam.signed_w) {
         if (fused)
           hipLaunchKernelGGL((glm_irls_ws_kernel<PP, true, true, true>), dim3(grid.x), dim3(512), 0, s, X, N, ldx,
@@ -1032,6 +1051,7 @@ extern "C" int h2o_glm_irls(const float* X, long long N, int P, int ldx, const i
   const int groups = (n_pairs + 4 * GI_PPW - 1) / (4 * GI_PPW);
   dim3 grid(n_splits, groups);
   GlmFamArgs fam{link, var, tvp, theta, gi_dbg(), signed_w, bf3 < 0 ? gi_bf3() : bf3, grad_f64};
+  if (fam.bf3 == 2 && !grad_out) fam.bf3 = 1;   // the plain-bf16 Hessian only beside the exact gradient
   const bool fused = beta != nullptr;
   // the exact-gradient channel rides the fused ws kernel (P <= 128, power of
   // two) only (grad_out: [n_splits][P + 1] doubles)

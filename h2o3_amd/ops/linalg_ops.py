@@ -88,7 +88,8 @@ def glm_irls(X, aug=-1, beta=None, b0=0.0, y=None, wprior=None, offset=None, cod
     (exact f64 products of the f32 values, f64 sums -- or, grad_f64=False,
     f32 products summed over a lane's rows of a chunk, f64 beyond; g[Pp] =
     sum r) as a third element.
-    `bf3`: override H2O3_GLM_BF3 for this call (False: f32 MFMA Gram).
+    `bf3`: override H2O3_GLM_BF3 for this call (False: f32 MFMA Gram;
+    "bf16": one bf16 MFMA per product, fused passes with grad=True only).
     """
     N, ldx = X.shape
     P = int(width) if width else ldx
@@ -115,7 +116,8 @@ def glm_irls(X, aug=-1, beta=None, b0=0.0, y=None, wprior=None, offset=None, cod
     rc = lib.h2o_glm_irls(_ptr(X), N, P, ldx, _ptr(pairs_t), npairs, splits, rpb, _ptr(bt), float(b0),
                           _ptr(keep[0]), _ptr(keep[1]), _ptr(keep[2]), int(codes[0]), int(codes[1]), float(tvp),
                           float(theta), _ptr(keep[3]), _ptr(keep[4]), int(aug), int(bool(signed)), _ptr(out),
-                          _ptr(dev), _ptr(gout), -1 if bf3 is None else int(bool(bf3)), int(bool(grad_f64)),
+                          _ptr(dev), _ptr(gout), -1 if bf3 is None else (2 if bf3 == "bf16" else int(bool(bf3))),
+                          int(bool(grad_f64)),
                           ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
     if rc != 0:
         raise RuntimeError(f"h2o_glm_irls failed: {rc}")

@@ -46,10 +46,15 @@ def main():
     est._spec = spec
     res = {"rows": a.rows, "cols": a.cols, "model": "GLM binomial IRLSM, lambda=0, standardized design"}
     drv = None
-    modes = {"bf16x3_exact_grad": ("1", "1"), "bf16x3_gram_rhs": ("1", "0"), "f32": ("0", "1")}
-    for name, (bf3, exact) in modes.items():
+    # (H2O3_GLM_BF3, H2O3_GLM_EXACT_GRAD, H2O3_GLM_BF16): the default tier ladder
+    # (one-MFMA bf16 Hessian while kappa < 32), bf16x3 pinned, the round-4
+    # Gram right-hand side, f32 MFMA
+    modes = {"default_tiers": ("1", "1", "1"), "bf16x3_exact_grad": ("1", "1", "0"),
+             "bf16x3_gram_rhs": ("1", "0", "0"), "f32": ("0", "1", "0")}
+    for name, (bf3, exact, bf16) in modes.items():
         os.environ["H2O3_GLM_BF3"] = bf3
         os.environ["H2O3_GLM_EXACT_GRAD"] = exact
+        os.environ["H2O3_GLM_BF16"] = bf16
         drv = GLMDriver(est, spec)
         times = []
         while not drv.converged and drv.iter < 25:
@@ -60,7 +65,8 @@ def main():
             times.append(time.time() - t0)
         res[name] = {
             "iterations": drv.iter, "ms_per_iter_median": 1000 * statistics.median(times),
-            "ms_per_iter_all": [round(1000 * t, 3) for t in times], "beta_std": drv.beta.tolist()}
+            "ms_per_iter_all": [round(1000 * t, 3) for t in times], "beta_std": drv.beta.tolist(),
+            "hessian_tier": getattr(drv, "_hprec", None), "hessian_kappa": getattr(drv, "hessian_kappa", None)}
         print(name, drv.iter, 1000 * statistics.median(times), flush=True)
     # independent fp64 IRLS on the same design (drv.X holds the standardized f32 rows)
     X, y, w = drv.X, drv.y, drv.w

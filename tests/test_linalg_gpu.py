@@ -298,11 +298,12 @@ _LEGACY_F32 = {"H2O3_GLM_BF3": "0", "H2O3_GLM_EXACT_GRAD": "0", "H2O3_GLM_TIERS"
 _LEGACY_BF3 = {"H2O3_GLM_BF3": "1", "H2O3_GLM_EXACT_GRAD": "0", "H2O3_GLM_TIERS": "0"}
 
 
-@pytest.mark.parametrize("noise,tier", [(1e-3, "f64"), (2e-2, "f32"), (None, "bf3")])
+@pytest.mark.parametrize("noise,tier", [(1e-3, "f64"), (2e-2, "f32"), (0.1, "bf3"), (None, "bf16")])
 def test_glm_conditioning_tiers_match_fp64(monkeypatch, noise, tier):
     """Newton on the exact gradient channel with the Hessian precision tier
-    picked from the scaled condition number: a well-conditioned design stays
-    on bf16x3, two columns at correlation 1 - 2e-4 (kappa ~ 1e4) move to the
+    picked from the scaled condition number: a well-conditioned design runs
+    on the one-MFMA bf16 Hessian (kappa < 32), two columns at correlation
+    ~0.995 (kappa ~ 400) on bf16x3, at 1 - 2e-4 (kappa ~ 1e4) move to the
     f32 Hessian, correlation 1 - 5e-7 (kappa >= 1e6) to fp64.  Every tier
     lands on the fp64 IRLS solution; at kappa >= 1e6 the legacy paths (Gram
     right-hand side, no tiers) are off by orders of magnitude more."""
