@@ -75,6 +75,7 @@ class BinnedData:
         self.nbins_node = 20         # nbins: floor of the per-node adaptive bin count
         self.nbins_top = 1024        # nbins_top_level
         self.qbounds = None          # RoundRobin: per-feature quantile boundary codes
+        self.has_na = None           # per feature: any NA in the training rows (every rank)
 
     @property
     def dtype(self):
@@ -268,6 +269,7 @@ def bin_frame_tensors(features, is_cat, cat_cards, names, hist_type="AUTO", nbin
     col = torch.empty((max(Fp, 1), N), dtype=dt, device=dev)
     if Fp > F:
         col[F:] = na if code_bytes == 1 else (na if na < 32768 else na - 65536)
+    has_na = torch.zeros(max(F, 1), dtype=torch.float32, device=dev)
     for j in range(F):
         x = features[j]
         if is_cat[j]:
@@ -285,7 +287,12 @@ def bin_frame_tensors(features, is_cat, cat_cards, names, hist_type="AUTO", nbin
                 cu = cu.to(torch.float32)
             c = torch.searchsorted(cu, xf.contiguous(), right=True) if cu.numel() else torch.zeros(N, dtype=torch.int64, device=dev)
             c = torch.where(torch.isnan(xf), torch.full_like(c, na), c)
+        has_na[j] = (c == na).any().to(torch.float32)
         col[j] = c.to(dt) if code_bytes == 1 else c.to(torch.int32).to(torch.int16)
+    # features with NAs anywhere in the training rows (every rank); a split on a
+    # feature without any sends NAs of later data to the heavier child, as the
+    # reference does when a node saw no NAs (DTree.java:1475-1478)
+    coll.allreduce_(has_na, "max")
     bd = BinnedData()
     bd.F, bd.Fp, bd.Bs, bd.na_code = F, Fp, Bs, na
     bd.nbins = list(nb_list)
@@ -295,6 +302,7 @@ def bin_frame_tensors(features, is_cat, cat_cards, names, hist_type="AUTO", nbin
     for j in range(F):
         if not is_cat[j] and features[j].dtype == torch.float32:
             bd.cuts[j] = bd.cuts[j].astype(np.float32).astype(np.float64)
+    bd.has_na = [bool(v) for v in has_na[:F].tolist()]
     bd.cat_card = list(cat_cards)
     bd.cat_group = list(groups)
     bd.names = list(names)

@@ -1845,7 +1845,14 @@ class TreeGrower:
             lid = first + 2 * np.arange(k, dtype=np.int64)
             tb.feat[nid_s] = f_s
             tb.gain[nid_s] = gains[sids]
-            tb.na_left[nid_s] = opt_s == 1
+            na_s = opt_s == 1
+            hn = getattr(self.bd, "has_na", None)
+            if hn is not None and len(hn) == self.bd.F and p.criterion != "xgb":
+                # no NA of this feature in training: NAs of later data go to the
+                # heavier child (DTree.java:1475-1478), numeric splits
+                free = ~np.asarray(hn, dtype=bool)[f_s] & (opt_s != 2) & ~is_cat_np[f_s]
+                na_s = np.where(free, wl_a > wr_a, na_s)
+            tb.na_left[nid_s] = na_s
             tb.left[nid_s] = lid
             tb.right[nid_s] = lid + 1
             cat_s = is_cat_np[f_s]

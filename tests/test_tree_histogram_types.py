@@ -136,3 +136,49 @@ def test_monotone_bounds_in_split_search():
     assert float(free["gain"][0]) == pytest.approx(400.0)
     assert float(res[True]["gain"][0]) == pytest.approx(400.0 - 64.0)
     assert not np.isfinite(float(res[False]["gain"][0]))
+
+
+def test_uniform_adaptive_gbm_matches_reference_mojo_top_splits():
+    """Pinned against the reference's own GBM MOJO fixture
+    (h2o-genmodel/src/test/resources/hex/genmodel/algos/gbm/
+    gbm_variable_importance.zip: prostate, CAPSULE ~ AGE..GLEASON, 50 trees,
+    reference defaults -- deterministic: sample_rate 1, col_sample_rate 1).
+    With histogram_type UniformAdaptive (the reference AUTO) our first two
+    trees split the root exactly as the reference (GLEASON < 6.5, NA left)
+    and its left child exactly (DPROS < 2.5); the right child picks the same
+    feature (PSA) with a threshold inside the same 20-bin cell of the node's
+    range (ours snaps node ranges to the 1024-bin top-level grid, the
+    reference uses the node's exact float min / max -- DHistogram.java:366),
+    and tree 0 has the reference's 23 internal nodes."""
+    import os
+    R = "/root/reference/h2o-genmodel/src/test/resources/hex/genmodel/algos/gbm/gbm_variable_importance.zip"
+    D = "/root/reference/h2o-core/src/main/resources/extdata/prostate.csv"
+    if not (os.path.exists(R) and os.path.exists(D)):
+        pytest.skip("reference fixture not present")
+    import pandas as pd
+    from h2o3_amd.estimators import H2OGradientBoostingEstimator
+    from h2o3_amd.mojo import h2o_mojo
+    from h2o3_amd.tree import H2OTree
+    cols = ["AGE", "RACE", "DPROS", "DCAPS", "PSA", "VOL", "GLEASON"]
+    ref = h2o_mojo.load(R)
+    df = pd.read_csv(D)
+    fr = h2o.H2OFrame(df)
+    fr["CAPSULE"] = fr["CAPSULE"].asfactor()
+    g = H2OGradientBoostingEstimator(ntrees=2, seed=1, histogram_type="UniformAdaptive")
+    g.train(x=cols, y="CAPSULE", training_frame=fr)
+    psa = df.loc[df.GLEASON >= 6.5, "PSA"]
+    cell = (psa.max() - psa.min()) / 20
+    for t in range(2):
+        rt = ref.trees[0][t]
+        ot = H2OTree(g, t)
+        assert ot.features[0] == cols[rt.col[0]] == "GLEASON"
+        assert ot.thresholds[0] == pytest.approx(rt.split[0]) == 6.5
+        assert (ot.nas[0] == "LEFT") == bool(rt.na_left[0])
+        lo, ro = ot.left_children[0], ot.right_children[0]
+        lr, rr = rt.left[0], rt.right[0]
+        assert ot.features[lo] == cols[rt.col[lr]] == "DPROS"
+        assert ot.thresholds[lo] == pytest.approx(rt.split[lr])
+        assert ot.features[ro] == cols[rt.col[rr]] == "PSA"
+        assert abs(ot.thresholds[ro] - rt.split[rr]) < cell
+    n_internal = sum(1 for f in H2OTree(g, 0).features if f is not None)
+    assert n_internal == len(ref.trees[0][0].col) == 23
