@@ -521,8 +521,8 @@ class TreeGrower:
         UniformAdaptive / Random, DHistogram.java:366-386, DTree.java:337).  The
         level histogram is on the fixed fine grid of nbins_top_level cells; the
         reference re-bins each (node, column) into
-        nb = max(nbins_top_level >> depth, nbins) uniform bins over the node's
-        observed range.  Here each run of fine bins that falls into one coarse
+        nb = max(nbins_top_level >> (depth - 1), nbins) uniform bins over the
+        parent's observed range (_adapt_range).  Here each run of fine bins that falls into one coarse
         bin is folded into the run's LAST fine bin: every cumulative sum at an
         allowed boundary is unchanged and every other boundary repeats the sums
         of the previous allowed one, so any split search on the folded
@@ -537,7 +537,10 @@ class TreeGrower:
         Fl, n, Bs, C = H.shape
         B = Bs - 1
         depth = getattr(self, "_depth", 0)
-        nb = max(self.bd.nbins_top >> depth, self.bd.nbins_node)
+        # bins per node: nbins_top_level at the root AND its children, halved per
+        # level below (the reference fixture's splits, gbm_variable_importance.zip,
+        # sit on 1024 / 512 / 256 / 128 cells of the parent's range at depths 1-4)
+        nb = max(self.bd.nbins_top >> max(depth - 1, 0), self.bd.nbins_node)
         f0 = self.f0
         isnum = ~self.is_cat_t[f0:f0 + Fl]
         if ht == "uniformadaptive" and nb >= B:
@@ -548,6 +551,7 @@ class TreeGrower:
         idx = torch.arange(B, device=dev)
         first = torch.where(occ, idx, B).amin(-1, keepdim=True)
         last = torch.where(occ, idx, -1).amax(-1, keepdim=True)
+        first, last = self._adapt_range(first, last, n, Fl, depth)
         L = (last - first + 1).clamp(min=1)
         inr = (idx >= first) & (idx <= last)
         if ht == "uniformadaptive":
@@ -584,6 +588,53 @@ class TreeGrower:
         Hf = torch.where(is_end.unsqueeze(-1), cs - base, torch.zeros_like(cs)).to(H.dtype)
         Hf = torch.where(isnum.view(Fl, 1, 1, 1), Hf, Hn)
         return torch.cat([Hf, H[:, :, B:]], 2).contiguous()
+
+    def _adapt_range(self, first, last, n, Fl, depth):
+        """Code range [first, last] ([Fl, n, 1]) each node's coarse bins span.
+        The reference bins a child over its PARENT's observed range of each
+        column, and the split column over the parent's range cut at the split
+        (DTree.java:337-372, nextLevelHistos); at depth 1 the coarse grid is
+        then exactly every (1024 >> 1)-th top-level cell.  The node's own
+        occupied range is recorded for its children; without a parent record
+        (root, chunk / frontier shapes that do not line up) the node's own
+        range is used."""
+        off = getattr(self, "_bnd_off", 0)
+        cur = self.__dict__.get("_rng_cur")
+        n_level = off + n if cur is None or off == 0 else max(cur[0].shape[1], off + n)
+        if cur is None or off == 0 or cur[0].shape[1] < n_level:
+            nf = torch.zeros((Fl, n_level, 1), dtype=first.dtype, device=first.device)
+            nl = torch.zeros_like(nf)
+            if cur is not None and off > 0:
+                k = min(cur[0].shape[1], n_level)
+                nf[:, :k], nl[:, :k] = cur[0][:, :k], cur[1][:, :k]
+            cur = self._rng_cur = (nf, nl)
+        cur[0][:, off:off + n], cur[1][:, off:off + n] = first, last
+        par = self.__dict__.get("_adapt_par")
+        rp = self.__dict__.get("_rng_par")
+        if depth == 0 or par is None or rp is None or rp[0].shape[0] != Fl:
+            return first, last
+        sids, fs, ts, opts, n_front = par
+        if 2 * len(sids) != n_front or off + n > n_front:
+            return first, last
+        j = np.arange(off, off + n)
+        pi = torch.as_tensor(sids[j // 2], device=first.device)
+        pf, pl = rp[0][:, pi].clone(), rp[1][:, pi].clone()       # [Fl, n, 1]
+        # the split column: left child codes <= t, right child codes > t
+        fl = fs[j // 2] - self.f0
+        ok = (fl >= 0) & (fl < Fl) & (opts[j // 2] != 2)
+        if ok.any():
+            jj = np.nonzero(ok)[0]
+            side = (j[jj] % 2).astype(bool)
+            t = torch.as_tensor(ts[j // 2][jj], device=first.device, dtype=first.dtype)
+            fi = torch.as_tensor(fl[jj], device=first.device)
+            ji = torch.as_tensor(jj, device=first.device)
+            sd = torch.as_tensor(side, device=first.device)
+            cf, cl = pf[fi, ji, 0], pl[fi, ji, 0]
+            pf[fi, ji, 0] = torch.where(sd, torch.maximum(cf, t + 1), cf)
+            pl[fi, ji, 0] = torch.where(sd, cl, torch.minimum(cl, t))
+        # empty nodes / columns keep their own (empty) range
+        use = (pf <= pl) & (first <= last)
+        return torch.where(use, pf, first), torch.where(use, pl, last)
 
     def _find_splits(self, H, col_mask, node_wyy=None, want_pk=False):
         """Dispatch: fused HIP kernel for numeric features on GPU (categorical
@@ -1644,6 +1695,12 @@ class TreeGrower:
             prev_bytes = 0 if H_prev is None else H_prev.numel() * 8
             chunked = can_split and (level_bytes + prev_bytes) > p.hist_mem_budget and n_front > 1
             self._depth = depth
+            # parent records for the per-node adaptive ranges (_adapt_range)
+            nxt = self.__dict__.get("_adapt_next")
+            self._adapt_par = None if (depth == 0 or nxt is None) else nxt + (n_front,)
+            self._rng_par = None if depth == 0 else self.__dict__.get("_rng_cur")
+            self._rng_cur = None
+            self._adapt_next = None
             direct = can_split and f_allow is None and not self._adaptive and not mono_b and \
                 self._direct_level(mode, depth, chunked)
             if mono_b and bool(np.isfinite(f_lo).any() | np.isfinite(f_hi).any()):
@@ -1853,6 +1910,9 @@ class TreeGrower:
                 free = ~np.asarray(hn, dtype=bool)[f_s] & (opt_s != 2) & ~is_cat_np[f_s]
                 na_s = np.where(free, wl_a > wr_a, na_s)
             tb.na_left[nid_s] = na_s
+            if self._adaptive:
+                self._adapt_next = (sids.copy(), np.asarray(f_s).copy(), np.asarray(t_s).copy(),
+                                    np.asarray(opt_s).copy())
             tb.left[nid_s] = lid
             tb.right[nid_s] = lid + 1
             cat_s = is_cat_np[f_s]

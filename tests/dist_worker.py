@@ -36,6 +36,11 @@ def run(out_path):
     gbm.train(x=x, y="y", training_frame=fr)
     res["gbm_auc"] = gbm.auc()
     res["gbm_logloss"] = gbm.logloss()
+    # reference UniformAdaptive: per-node bins over the parent's range (feature slices per rank)
+    gua = H2OGradientBoostingEstimator(ntrees=5, max_depth=5, seed=1, min_rows=5, histogram_type="UniformAdaptive",
+                                       nbins_top_level=256)
+    gua.train(x=x, y="y", training_frame=fr)
+    res["gbm_ua_logloss"] = gua.logloss()
     glm = H2OGeneralizedLinearEstimator(family="binomial", lambda_=0.0)
     glm.train(x=x, y="y", training_frame=fr)
     res["glm_coef"] = glm.coef()

@@ -98,6 +98,7 @@ def test_gbm_matches_single_process(results):
     one, two = results
     assert abs(one["gbm_auc"] - two["gbm_auc"]) < 1e-5
     assert abs(one["gbm_logloss"] - two["gbm_logloss"]) < 1e-5
+    assert abs(one["gbm_ua_logloss"] - two["gbm_ua_logloss"]) < 1e-5
 
 
 def test_metrics_from_merged_sketches_match_single_process(results):

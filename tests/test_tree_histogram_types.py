@@ -25,13 +25,13 @@ def _init():
 def _step_frame(n=20000, seed=0):
     rng = np.random.default_rng(seed)
     x = rng.random(n)
-    y = 3.0 * (x > 0.1) + 1.0 * (x > 0.5317) + 0.01 * rng.normal(size=n)
+    y = 3.0 * (x > 0.1) + 2.0 * (x > 0.95) + 0.5 * (x > 0.5317) + 0.01 * rng.normal(size=n)
     return pd.DataFrame({"x": x, "y": y})
 
 
-def _allowed_right_child(codes, lo_code, nb):
-    """Coarse boundaries of a node whose rows have fine codes `codes`."""
-    first, last = int(codes.min()), int(codes.max())
+def _coarse_ends(first, last, nb):
+    """Allowed split codes: the coarse boundaries of nb uniform bins over the
+    fine-code range [first, last] (every code when the range is narrower)."""
     L = last - first + 1
     b = np.arange(first, last + 1)
     coarse = np.floor((b - first) * nb / L)
@@ -40,29 +40,34 @@ def _allowed_right_child(codes, lo_code, nb):
 
 
 def test_uniform_adaptive_child_splits_on_its_coarse_grid():
+    """Reference UniformAdaptive schedule (DTree.java:337-372, with the bin
+    counts the reference fixture's splits show): the root and its children
+    use the nbins_top_level grid, a depth-2 node max(nbins_top_level >> 1,
+    nbins) uniform bins over its PARENT's range of the column, cut at the
+    parent's split."""
     df = _step_frame()
     fr = h2o.H2OFrame(df)
-    kw = dict(ntrees=1, max_depth=2, learn_rate=1.0, min_rows=1, seed=1, nbins=20, nbins_top_level=128,
+    kw = dict(ntrees=1, max_depth=3, learn_rate=1.0, min_rows=1, seed=1, nbins=20, nbins_top_level=128,
               distribution="gaussian")
     m = H2OGradientBoostingEstimator(histogram_type="UniformAdaptive", **kw)
     m.train(x=["x"], y="y", training_frame=fr)
     t = m._forest.trees[0]
-    root_thr = t.thr[0]
-    assert abs(root_thr - 0.1) < 1.5 / 128                     # root: the 128-cell top-level grid
+    assert abs(t.thr[0] - 0.1) < 1.5 / 128                      # root: the 128-cell top-level grid
     r = t.right[0]
-    assert t.left[r] >= 0, "right child must split"
-    # fine codes of the right child's rows on the 128-cell uniform grid
-    lo, hi = df.x.min(), df.x.max()
-    cuts = np.unique(np.linspace(lo, hi, 129)[1:-1])
-    codes = np.searchsorted(cuts, df.x.values[df.x.values >= root_thr], side="right")
-    allowed = _allowed_right_child(codes, 0, max(128 >> 1, 20))
-    assert len(allowed) < codes.max() - codes.min() + 1          # the grid really is coarser here
-    assert int(t.split_code[r]) in allowed
+    assert abs(t.thr[r] - 0.95) < 1.5 / 128                     # depth 1: still the full grid
+    rl = t.left[r]
+    assert t.left[rl] >= 0, "the depth-2 node [0.1, 0.95) must split"
+    # its range: the parent's fine codes (root split + 1 .. last) cut at the parent's split
+    first, last = int(t.split_code[0]) + 1, int(t.split_code[r])
+    allowed = _coarse_ends(first, last, max(128 >> 1, 20))
+    assert len(allowed) < last - first + 1                       # the grid really is coarser here
+    assert int(t.split_code[rl]) in allowed
+    assert abs(t.thr[rl] - 0.5317) < 2.5 / 128
     # the same data with the global quantile grid is not restricted this way
     q = H2OGradientBoostingEstimator(histogram_type="QuantilesGlobal", **dict(kw, nbins=1000))
     q.train(x=["x"], y="y", training_frame=fr)
     qt = q._forest.trees[0]
-    assert abs(qt.thr[qt.right[0]] - 0.5317) < 0.003
+    assert abs(qt.thr[qt.left[qt.right[0]]] - 0.5317) < 0.003
 
 
 def test_quantiles_global_cuts_are_exact_order_statistics():
@@ -102,7 +107,7 @@ def test_round_robin_cycles_tree_types_and_random_redraws():
     bd = bin_frame_tensors([torch.tensor(df.x.values.astype(np.float32))], [False], [0], ["x"],
                            hist_type="Random", nbins=20, nbins_top_level=1024)
     g = TreeGrower(bd, GrowParams(seed=7))
-    g._tree_no, g._depth = 0, 3                                   # nb = max(1024 >> 3, 20) = 128
+    g._tree_no, g._depth = 0, 4                                   # nb = max(1024 >> (4 - 1), 20) = 128
     H = torch.zeros((1, 2, bd.Bs, 2), dtype=torch.float64)
     H[0, :, : bd.nbins[0], 0] = 1.0
     H[0, :, : bd.nbins[0], 1] = torch.arange(bd.nbins[0], dtype=torch.float64)
@@ -144,12 +149,13 @@ def test_uniform_adaptive_gbm_matches_reference_mojo_top_splits():
     gbm_variable_importance.zip: prostate, CAPSULE ~ AGE..GLEASON, 50 trees,
     reference defaults -- deterministic: sample_rate 1, col_sample_rate 1).
     With histogram_type UniformAdaptive (the reference AUTO) our first two
-    trees split the root exactly as the reference (GLEASON < 6.5, NA left)
-    and its left child exactly (DPROS < 2.5); the right child picks the same
-    feature (PSA) with a threshold inside the same 20-bin cell of the node's
-    range (ours snaps node ranges to the 1024-bin top-level grid, the
-    reference uses the node's exact float min / max -- DHistogram.java:366),
-    and tree 0 has the reference's 23 internal nodes."""
+    trees split the root and both depth-1 children exactly as the reference
+    (GLEASON < 6.5 with NAs left, DPROS < 2.5, PSA < 14.7301: the depth-1
+    node bins its parent's PSA range on the top-level grid), and tree 0 has
+    the reference's 23 internal nodes.  Deeper thresholds differ slightly:
+    the reference re-bins each node over the parent's exact float min / max
+    (DTree.java:337-351), ours folds the fixed top-level grid over the
+    parent's occupied code range, so its cut points stay on that grid."""
     import os
     R = "/root/reference/h2o-genmodel/src/test/resources/hex/genmodel/algos/gbm/gbm_variable_importance.zip"
     D = "/root/reference/h2o-core/src/main/resources/extdata/prostate.csv"
@@ -179,6 +185,7 @@ def test_uniform_adaptive_gbm_matches_reference_mojo_top_splits():
         assert ot.features[lo] == cols[rt.col[lr]] == "DPROS"
         assert ot.thresholds[lo] == pytest.approx(rt.split[lr])
         assert ot.features[ro] == cols[rt.col[rr]] == "PSA"
+        assert ot.thresholds[ro] == pytest.approx(rt.split[rr], abs=1e-4)
         assert abs(ot.thresholds[ro] - rt.split[rr]) < cell
     n_internal = sum(1 for f in H2OTree(g, 0).features if f is not None)
     assert n_internal == len(ref.trees[0][0].col) == 23
