@@ -137,7 +137,16 @@ class Forest:
         def cat(parts, dt):
             return np.concatenate(parts).astype(dt) if parts else np.zeros(0, dtype=dt)
         d = device
-        P = {"feat": torch.as_tensor(cat(feat, np.int32), device=d),
+        # packed 16-byte nodes for the HIP kernel: feature | NA-left << 30 |
+        # categorical << 31, threshold bits, left, right
+        f32 = cat(thr, np.float32)
+        cof = cat(coff, np.int32)
+        node = np.stack([(cat(feat, np.int64) & 0x3FFFFFFF) | (cat(nal, np.int64) << 30) |
+                         ((cof >= 0).astype(np.int64) << 31),
+                         f32.view(np.int32).astype(np.int64), cat(left, np.int64), cat(right, np.int64)], 1)
+        node = node.astype(np.uint32).view(np.int32) if node.size else np.zeros((0, 4), dtype=np.int32)
+        P = {"node": torch.as_tensor(np.ascontiguousarray(node), device=d),
+             "feat": torch.as_tensor(cat(feat, np.int32), device=d),
              "thr": torch.as_tensor(cat(thr, np.float32), device=d),
              "left": torch.as_tensor(cat(left, np.int32), device=d),
              "right": torch.as_tensor(cat(right, np.int32), device=d),
@@ -163,13 +172,12 @@ class Forest:
             return leaf_out if leaf else out
         if X.device.type == "cuda":
             lib = _native.get_lib("tree_predict")
-            if not getattr(lib, "_typed", False):
-                lib.h2o_forest_predict.argtypes = [_c_void, ctypes.c_longlong] + [_c_void] * 11 + \
+            if not getattr(lib, "_typed2", False):
+                lib.h2o_forest_predict.argtypes = [_c_void, ctypes.c_longlong] + [_c_void] * 7 + \
                     [ctypes.c_int, ctypes.c_int, _c_void, _c_void, _c_void]
-                lib._typed = True
+                lib._typed2 = True
             X = X.contiguous().to(torch.float32)
-            rc = lib.h2o_forest_predict(_ptr(X), N, _ptr(P["feat"]), _ptr(P["thr"]), _ptr(P["left"]),
-                                        _ptr(P["right"]), _ptr(P["na_left"]), _ptr(P["cat_off"]),
+            rc = lib.h2o_forest_predict(_ptr(X), N, _ptr(P["node"]), _ptr(P["cat_off"]),
                                         _ptr(P["cat_len"]), _ptr(P["cat_bits"]), _ptr(P["value"]),
                                         _ptr(P["roots"]), _ptr(P["tclass"]), T, K,
                                         _ptr(out) if not leaf else ctypes.c_void_p(0),
