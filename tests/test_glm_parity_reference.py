@@ -95,3 +95,37 @@ def test_kappa_from_shared_factor_matches_lapack():
     L, info = torch.linalg.cholesky_ex(At)
     assert int(info) != 0
     assert GLMDriver._kappa_from_factor(At, L, info) == pytest.approx(GLMDriver._scaled_cond(A), rel=1e-8)
+
+
+@pytest.mark.parametrize("intercept,l2", [(True, 0.0), (True, 0.3), (False, 0.3)])
+def test_device_ridge_step_matches_host_solver(intercept, l2):
+    """GLMDriver._step_solve_dev (the device Newton step of wide ridge-only
+    systems; run here on CPU tensors) equals the host _solve_quadratic on
+    the same system, penalty off the intercept, and reports the same
+    max |gradient|."""
+    from types import SimpleNamespace
+    import numpy as np
+    import torch
+    from h2o3_amd.models.glm.glm import GLMDriver, _solve_quadratic
+    g = np.random.default_rng(11)
+    P = 40
+    k = P + 1 if intercept else P
+    A = g.standard_normal((500, k))
+    Gn = A.T @ A / 500
+    bn = g.standard_normal(k)
+    beta = g.standard_normal(P + 1) * 0.1
+    drv = SimpleNamespace(beta=beta, intercept=intercept, P=P)
+    Gt, bt = torch.from_numpy(Gn), torch.from_numpy(bn)
+    At = Gt.clone()
+    pen = torch.full((k,), l2, dtype=torch.float64)
+    if intercept:
+        pen[-1] = 0.0
+    At.diagonal().add_(pen)
+    L, info = torch.linalg.cholesky_ex(At)
+    gmax, new = GLMDriver._step_solve_dev(drv, Gt, bt, l2, L, info)
+    want = _solve_quadratic(Gn, bn, 0.0, l2, intercept)
+    np.testing.assert_allclose(new, want, rtol=1e-10, atol=1e-12)
+    bcur = beta if intercept else beta[:-1]
+    gq = Gn @ bcur - bn
+    gq[:P] += l2 * bcur[:P]
+    assert gmax == pytest.approx(float(np.abs(gq).max()), rel=1e-12)
