@@ -696,6 +696,37 @@ class GLMDriver:
                 and not p.get("remove_collinear_columns") and not p.get("non_negative")
                 and not p.get("_nonneg_names"))
 
+    def _dev_tier_ok(self):
+        """Wide systems whose solve needs the host (l1 / bounds / non-negative
+        coefficients) still get their condition estimate on the device: the
+        (P+1)^2 statistics cross to the host once, after the tier check."""
+        return (self.X.device.type == "cuda" and self.P + 1 >= 256
+                and os.environ.get("H2O3_GLM_DEV_SOLVE", "1") != "0"
+                and self.rho is None and self.active is None and self._penalty_matrix() is None
+                and not self.est._parms.get("remove_collinear_columns"))
+
+    def _check_tier_dev(self, Ga, b):
+        """_check_tier on device statistics (scaled-condition estimate on a
+        device Cholesky); recomputes the statistics on the device when the
+        tier must rise."""
+        while self._tiers_due():
+            Gn, _, _, l2 = self._system(Ga, b)
+            if l2 > 0:
+                Gn = Gn.clone()
+                Gn.diagonal()[:self.P] += l2
+            want = self._tier_raise(self._scaled_cond_dev(Gn))
+            if want is None:
+                break
+            self._sys_on_dev = True
+            try:
+                Ga, b, dev = self._irls_stats()
+            finally:
+                self._sys_on_dev = False
+            self._stats_dev = dev
+            if want == "f64":
+                break
+        return Ga, b
+
     def _step_solve_dev(self, Gn, bn, l2, L, info):
         """Ridge Newton step on the device from the factor L of Gn + ridge:
         (max |gradient|, new beta) with one host read; new is None when the
@@ -1001,18 +1032,27 @@ class GLMDriver:
     def step(self):
         """One IRLS iteration (Gram on the matrix cores + host solve; wide
         ridge-only systems are conditioned and solved on the device)."""
-        self._sys_on_dev = self._dev_system_ok()
+        dev_solve = self._dev_system_ok()
+        self._sys_on_dev = dev_solve or self._dev_tier_ok()
         try:
             Ga, b, dev = self._irls_stats()
         finally:
             self._sys_on_dev = False
         self._stats_dev = dev
-        if torch.is_tensor(Ga):
+        if torch.is_tensor(Ga) and dev_solve:
             Gn, bn, l1, l2, gmax, new = self._step_dev(Ga, b)
             if new is not None:
                 return self._finish_step(new, gmax, self._stats_dev, l1, l2)
             Gn, bn = Gn.cpu().numpy(), bn.cpu().numpy()
             dev = self._stats_dev
+        elif torch.is_tensor(Ga):
+            # l1 / bounds: condition estimate on the device, solve on the host
+            with phase("glm.tier"):
+                Ga, b = self._check_tier_dev(Ga, b)
+            Ga, b = Ga.cpu().numpy(), b.cpu().numpy()
+            dev = self._stats_dev
+            with phase("glm.system"):
+                Gn, bn, l1, l2 = self._system(Ga, b)
         else:
             with phase("glm.tier"):
                 Ga, b = self._check_tier(Ga, b)

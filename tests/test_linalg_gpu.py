@@ -268,7 +268,7 @@ def _fp64_irls(X, y, beta0, iters=30):
     return b, G
 
 
-def _glm_fit_modes(Xh, y, modes, monkeypatch, iters=30):
+def _glm_fit_modes(Xh, y, modes, monkeypatch, iters=30, est_kw=None):
     import numpy as np
     from h2o3_amd.models.base import TrainSpec
     from h2o3_amd.core.frame import H2OFrame
@@ -282,7 +282,7 @@ def _glm_fit_modes(Xh, y, modes, monkeypatch, iters=30):
     for name, env in modes.items():
         for k, v in env.items():
             monkeypatch.setenv(k, v)
-        est = H2OGeneralizedLinearEstimator(family="binomial", solver="IRLSM", lambda_=0.0)
+        est = H2OGeneralizedLinearEstimator(**(est_kw or dict(family="binomial", solver="IRLSM", lambda_=0.0)))
         spec = TrainSpec(fr, [f"x{j}" for j in range(P)], "y")
         est._spec = spec
         drv = GLMDriver(est, spec)
@@ -469,3 +469,28 @@ def test_glm_wide_device_solve_matches_host(monkeypatch, noise):
     assert drvs["dev"].hessian_kappa == pytest.approx(drvs["host"].hessian_kappa, rel=1e-6)
     err = np.abs(res["dev"] - res["host"]).max() / np.abs(res["host"]).max()
     assert err < 1e-9, err
+
+
+def test_glm_wide_l1_device_tier_check_matches_host(monkeypatch):
+    """P = 600, elastic net (alpha 0.5, lambda > 0: the host coordinate-descent
+    solve): the condition estimate runs on the device statistics before they
+    cross to the host; same tier, kappa and coefficients as the all-host
+    path (H2O3_GLM_DEV_SOLVE=0)."""
+    import numpy as np
+    g = np.random.default_rng(12)
+    n, P = 60_000, 600
+    Xh = g.standard_normal((n, P)).astype(np.float32)
+    b = np.zeros(P)
+    b[:10] = 0.5 * g.standard_normal(10)
+    y = (g.random(n) < 1 / (1 + np.exp(-(Xh.astype(np.float64) @ b)))).astype(int)
+    kw = dict(family="binomial", solver="IRLSM", alpha=0.5, lambda_=1e-3)
+    res, drvs = _glm_fit_modes(Xh, y, {"host": dict(_DEFAULT, H2O3_GLM_DEV_SOLVE="0"),
+                                       "dev": dict(_DEFAULT, H2O3_GLM_DEV_SOLVE="1")}, monkeypatch, iters=8,
+                               est_kw=kw)
+    d = drvs["dev"]
+    assert d._dev_tier_ok() and not d._dev_system_ok()
+    assert d._hprec == drvs["host"]._hprec
+    assert d.hessian_kappa == pytest.approx(drvs["host"].hessian_kappa, rel=1e-6)
+    err = np.abs(res["dev"] - res["host"]).max() / np.abs(res["host"]).max()
+    assert err < 1e-9, err
+    assert np.count_nonzero(res["dev"][:P]) < P                  # the l1 penalty is active
