@@ -341,6 +341,8 @@ class H2OEstimator:
             x = [names[i] if isinstance(i, int) else i for i in (x if isinstance(x, (list, tuple)) else [x])]
             x = [n for n in x if n not in special]
         if p.get("ignore_const_cols", True):
+            from ..ops import frame_ops
+            frame_ops.rollups_many([training_frame.vec(n) for n in x])   # one batched pass on the GPU
             x = [n for n in x if not training_frame.vec(n).is_const()]
         # drop string/uuid columns (reference ignores them for most algos)
         x = [n for n in x if not training_frame.vec(n).on_host]

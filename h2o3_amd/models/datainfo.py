@@ -53,6 +53,8 @@ class DataInfo:
             if len(pdf) != 1:
                 raise ValueError("ERRR on field: _plug_values: Plug values frame needs to have exactly 1 row.")
             plug = {c: float(pdf[c].iloc[0]) for c in pdf.columns if pdf[c].dtype.kind in "fiub"}
+        from ..ops import frame_ops
+        frame_ops.rollups_many([frame.vec(c) for c in self.num_cols])
         for c in self.num_cols:
             v = frame.vec(c)
             r = v.rollups()
@@ -103,7 +105,10 @@ class DataInfo:
             rows = torch.nonzero(m).flatten()
             X[rows, self.cat_offsets[c] + codes[rows]] = 1.0
         base = self.n_cat_expanded
+        fast = self._expand_numeric_fast(frame, X, base, n)
         for j, c in enumerate(self.num_cols):
+            if fast and self.mvh != "skip":
+                break
             if c in frame.names:
                 x = frame.vec(c).as_float(torch.float64)
             else:
@@ -111,11 +116,27 @@ class DataInfo:
             na = torch.isnan(x)
             if self.mvh == "skip":
                 ok &= ~na
+            if fast:
+                continue             # the kernel filled the column; only the skip mask is needed
             x = torch.where(na, torch.full_like(x, self.plug[j]), x)
             if self.standardize:
                 x = (x - self.means[j]) / self.sigmas[j]
             X[:, base + j] = x.to(dtype)
         return X, ok
+
+    def _expand_numeric_fast(self, frame, X, base, n):
+        """The numeric block by the tiled HIP kernel (ops/csrc/frame.hip):
+        every numeric column present, float32 / float64 on the device."""
+        if not self.num_cols or not X.is_cuda or any(c not in frame.names for c in self.num_cols):
+            return False
+        from ..ops import frame_ops
+        vs = [frame.vec(c) for c in self.num_cols]
+        if not all(frame_ops.batchable(v) and v.data.numel() == n for v in vs):
+            return False
+        k = len(vs)
+        mean = self.means if self.standardize else [0.0] * k
+        sd = self.sigmas if self.standardize else [1.0] * k
+        return frame_ops.expand_numeric([v.data for v in vs], self.plug, mean, sd, X, base)
 
     def destandardize(self, beta_std, icpt_std):
         """Convert standardized-space coefficients to original scale."""

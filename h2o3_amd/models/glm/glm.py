@@ -503,12 +503,42 @@ class GLMDriver:
             eta = eta + self.offset
         return eta
 
+    def _wide_eta_codes(self):
+        """Family codes when the wide fused eta kernel applies (the wide IRLS
+        path of _irls_stats), else None."""
+        codes = linalg_ops.glm_fused_codes(self.fam.family, self.fam.link, self.fam.tlp)
+        if self.X.device.type == "cuda" and self.Pp > 512 and self.P + 2 <= 1024 and codes is not None and \
+                linalg_ops._wide_mode() == "bf3" and linalg_ops.wide_fused_enabled():
+            if not hasattr(self, "_y32"):
+                self._y32 = self.y.to(torch.float32)
+                self._w32 = self.w.to(torch.float32)
+                self._off32 = None if self.offset is None else self.offset.to(torch.float32)
+            return codes
+        return None
+
+    def _wide_eta_pass(self, codes, beta, b0):
+        """(deviance, X'r) of the wide eta kernel at (beta[:P], b0): one pass
+        over X instead of a GEMV plus torch elementwise passes."""
+        bt = torch.as_tensor(np.asarray(beta[:self.P], dtype=np.float64), dtype=torch.float32, device=self.X.device)
+        _, dev, gx = linalg_ops.glm_wide_irls(self.X, self.P, bt, float(b0), self._y32, self._w32, self._off32,
+                                              codes, self.fam.tvp, self.fam.theta, fused=True, eta_only=True)
+        return dev, gx
+
     def _lambda_max(self):
         # gradient of the mean log-likelihood at the intercept-only model
-        eta0 = torch.full_like(self.y, self.fam.link_fn(min(max(self.ymu, 1e-10), 1 - 1e-10))
-                               if self.fam.link == "logit" else
-                               (self.fam.link_fn(max(self.ymu, 1e-10)) if self.fam.link in ("log", "inverse")
-                                else self.ymu))
+        e0 = self.fam.link_fn(min(max(self.ymu, 1e-10), 1 - 1e-10)) if self.fam.link == "logit" else \
+            (self.fam.link_fn(max(self.ymu, 1e-10)) if self.fam.link in ("log", "inverse") else self.ymu)
+        codes = self._wide_eta_codes()
+        if codes is not None:
+            # the wide eta kernel at beta = 0, intercept eta0: its gradient
+            # channel is exactly X'r with r = w (y - mu) dmu/deta / var
+            _, gx = self._wide_eta_pass(codes, np.zeros(self.P), float(e0))
+            g = gx[:self.P].contiguous()
+            coll.allreduce_(g)
+            g = g * self.obj_reg
+            amax = float(g.abs().max()) if g.numel() else 0.0
+            return amax / max(1e-2, self.alpha)
+        eta0 = torch.full_like(self.y, e0)
         if self.offset is not None:
             eta0 = eta0 + self.offset
         mu = self.fam.linkinv(eta0)
@@ -1124,6 +1154,11 @@ class GLMDriver:
         return pen
 
     def deviance(self, beta=None):
+        codes = self._wide_eta_codes()
+        if codes is not None:
+            b = self.beta if beta is None else beta
+            dev, _ = self._wide_eta_pass(codes, b, float(b[-1]))
+            return coll.allreduce_scalar(float(dev))
         eta = self._eta(beta)
         mu = self.fam.linkinv(eta)
         return coll.allreduce_scalar(float((self.w * self.fam.deviance(self.y, mu)).sum()))

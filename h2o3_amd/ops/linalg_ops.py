@@ -408,7 +408,7 @@ def _wide_split_grid(lib, Pa):
 
 
 def glm_wide_irls(X, P, beta, b0, y, wprior=None, offset=None, codes=(1, 1), tvp=0.0, theta=1e-10, step=1 << 19,
-                  fused=False, bf3=True):
+                  fused=False, bf3=True, eta_only=False):
     """Fused IRLS pass for wide GLMs (P + 2 <= 1024).
 
     fused=True (needs the exact-gradient channel: the Gram carries no z
@@ -422,7 +422,9 @@ def glm_wide_irls(X, P, beta, b0, y, wprior=None, offset=None, codes=(1, 1), tvp
 
     Returns (G [Pa, Pa] f64 augmented Gram, deviance f64, g [Pa] f64
     exact-gradient channel X'r with g[P] = sum r, r = w (y - mu) dmu/deta /
-    var: f32 VALU products over <= 64 rows per lane, f64 beyond)."""
+    var: f32 VALU products over <= 64 rows per lane, f64 beyond).
+    eta_only (fused): the eta / deviance / gradient pass alone, G is None --
+    the deviance at a coefficient vector and X'r for lambda_max."""
     lib = _lib()
     if lib is None:
         raise RuntimeError("gram extension not built (run __graft_entry__.build())")
@@ -460,6 +462,8 @@ def glm_wide_irls(X, P, beta, b0, y, wprior=None, offset=None, codes=(1, 1), tvp
                                             _ptr(dev[i]), blocks, _ptr(gbuf), offp(wr, a), stream)
                 if rc != 0:
                     raise RuntimeError(f"h2o_glm_wide_split failed: {rc}")
+        if eta_only:
+            return None, dev.sum(), gbuf.sum(0)
         with phase("glm.wide_gram"):
             G = wide_gram(X, P, wr, stream, bf3=bf3)
         return G, dev.sum(), gbuf.sum(0)

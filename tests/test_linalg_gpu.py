@@ -494,3 +494,40 @@ def test_glm_wide_l1_device_tier_check_matches_host(monkeypatch):
     err = np.abs(res["dev"] - res["host"]).max() / np.abs(res["host"]).max()
     assert err < 1e-9, err
     assert np.count_nonzero(res["dev"][:P]) < P                  # the l1 penalty is active
+
+
+@pytest.mark.parametrize("family", ["binomial", "poisson", "gaussian"])
+def test_glm_wide_lambda_max_and_deviance_kernel_match_torch(family, monkeypatch):
+    """P = 600: lambda_max (X'r at the intercept-only model) and the
+    deviance at a coefficient vector from the wide eta kernel agree with the
+    torch f64 paths (f32 products inside the kernel)."""
+    import numpy as np
+    from h2o3_amd.models.base import TrainSpec
+    from h2o3_amd.core.frame import H2OFrame
+    from h2o3_amd.models.glm.glm import GLMDriver, H2OGeneralizedLinearEstimator
+    g = np.random.default_rng(21)
+    n, P = 40_000, 600
+    Xh = g.standard_normal((n, P)).astype(np.float32)
+    eta = Xh[:, :5].astype(np.float64) @ (0.3 * g.standard_normal(5))
+    if family == "binomial":
+        y = (g.random(n) < 1 / (1 + np.exp(-eta))).astype(int)
+    elif family == "poisson":
+        y = g.poisson(np.exp(0.5 * eta)).astype(float)
+    else:
+        y = eta + g.standard_normal(n)
+    cols = {f"x{j}": Xh[:, j] for j in range(P)}
+    cols["y"] = y
+    fr = H2OFrame(cols)
+    if family == "binomial":
+        fr["y"] = fr["y"].asfactor()
+    est = H2OGeneralizedLinearEstimator(family=family, solver="IRLSM", alpha=0.5, lambda_search=True)
+    spec = TrainSpec(fr, [f"x{j}" for j in range(P)], "y")
+    est._spec = spec
+    drv = GLMDriver(est, spec)
+    assert drv._wide_eta_codes() is not None
+    beta = np.concatenate([0.01 * g.standard_normal(P), [0.1]])
+    lm_k, dv_k = drv._lambda_max(), drv.deviance(beta)
+    monkeypatch.setattr(GLMDriver, "_wide_eta_codes", lambda self: None)
+    lm_t, dv_t = drv._lambda_max(), drv.deviance(beta)
+    assert lm_k == pytest.approx(lm_t, rel=1e-5)
+    assert dv_k == pytest.approx(dv_t, rel=1e-5)
