@@ -417,6 +417,8 @@ class H2OFrame:
 
     def summary(self, return_data=False):
         out = {}
+        from ..ops import frame_ops
+        frame_ops.rollups_many(self._vecs)          # every numeric device column in one batched pass
         for n, v in zip(self._names, self._vecs):
             r = v.rollups()
             out[n] = {"type": v.type, "mins": r["min"], "maxs": r["max"], "mean": r["mean"], "sigma": r["sigma"],
@@ -817,6 +819,8 @@ class H2OFrame:
             r = torch.nanmean(x, 1) if skipna else x.mean(1)
             return H2OFrame.from_vecs([Vec(r, T_REAL)], ["mean"])
         res = []
+        from ..ops import frame_ops
+        frame_ops.rollups_many(self._vecs)
         for v in self._vecs:
             r = v.rollups()
             if not skipna and r["nacnt"] > 0:
