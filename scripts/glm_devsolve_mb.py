@@ -57,6 +57,11 @@ print(f"P={P}")
 print(f"dev cholesky        {tdev(lambda: torch.linalg.cholesky(G)):8.3f} ms")
 print(f"dev cholesky_ex     {tdev(lambda: torch.linalg.cholesky_ex(G)):8.3f} ms")
 print(f"dev cholesky_solve  {tdev(lambda: torch.cholesky_solve(b.view(-1, 1), L)):8.3f} ms")
+G32 = G.float()
+print(f"dev cholesky f32    {tdev(lambda: torch.linalg.cholesky_ex(G32)):8.3f} ms")
+L32 = torch.linalg.cholesky(G32)
+print(f"dev chol_solve f32  {tdev(lambda: torch.cholesky_solve(b.float().view(-1, 1), L32)):8.3f} ms")
+print(f"dev inverse f64     {tdev(lambda: torch.cholesky_inverse(L)):8.3f} ms")
 print(f"dev hager estimate  {tdev(lambda: hager(L, P)):8.3f} ms")
 print(f"dev gemv            {tdev(lambda: G @ b):8.3f} ms")
 print(f"dev->host copy      {tdev(lambda: G.cpu()):8.3f} ms")
