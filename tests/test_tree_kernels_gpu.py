@@ -176,6 +176,34 @@ def test_forest_predict_matches_host():
     torch.testing.assert_close(f_train, f_score, rtol=1e-4, atol=1e-4)
 
 
+def test_forest_predict_multiclass_and_leaf_ids_match_host():
+    """Packed-node scoring kernel, K > 1 (per-class sums into out[r, k]) and
+    the leaf-id output, against the torch walk; categorical + NA splits."""
+    _need_gpu()
+    import pandas as pd
+    import h2o3_amd
+    from h2o3_amd.estimators import H2OGradientBoostingEstimator
+    from h2o3_amd.models.tree.shared import Forest
+    rng = np.random.RandomState(1)
+    n = 4000
+    X = rng.randn(n, 4)
+    X[rng.rand(n) < 0.1, 2] = np.nan
+    cat = rng.choice(list("abcdefg"), n)
+    yk = np.where(X[:, 0] + (cat == "b") > 0.5, "u", np.where(np.nan_to_num(X[:, 2]) > 0, "v", "w"))
+    df = pd.DataFrame(X, columns=list("pqrs"))
+    df["cat"] = cat
+    df["y"] = yk
+    fr = h2o3_amd.H2OFrame(df)
+    m = H2OGradientBoostingEstimator(ntrees=4, max_depth=5, seed=3)
+    m.train(y="y", training_frame=fr)
+    Xs = m._score_matrix(fr)
+    K = m._n_tree_classes()
+    assert K == 3
+    P = m._forest.pack(Xs.device)
+    torch.testing.assert_close(m._forest.predict(Xs, K), Forest._predict_torch(Xs, K, P), rtol=1e-5, atol=1e-5)
+    assert torch.equal(m._forest.predict(Xs, K, leaf=True), Forest._predict_torch(Xs, K, P, leaf=True))
+
+
 def test_gbm_gpu_end_to_end_quality():
     _need_gpu()
     import pandas as pd
