@@ -43,20 +43,27 @@ __global__ __launch_bounds__(256) void rollup_multi_kernel(const FrCol* __restri
   double mn = 1.7976931348623157e308, mx = -1.7976931348623157e308;
   const double mu = pass ? mean[blockIdx.y] : 0.0;
   const long long stride = (long long)gridDim.x * blockDim.x;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const double x = fr_load(c, i);
-    if (x != x) { nan += 1.0; continue; }
-    if (isinf(x)) { if (x > 0) pin += 1.0; else nin += 1.0; continue; }
+  auto acc = [&](double x) {
+    if (x != x) { nan += 1.0; return; }
+    if (isinf(x)) { if (x > 0) pin += 1.0; else nin += 1.0; return; }
     if (pass) {
       const double d = x - mu;
       s1 += d * d;
-      continue;
+      return;
     }
     cnt += 1.0; s1 += x;
     zer += x == 0.0 ? 1.0 : 0.0;
     nint += x != rint(x) ? 1.0 : 0.0;
     mn = fmin(mn, x); mx = fmax(mx, x);
+  };
+  // 4 independent loads in flight per thread
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + 3 * stride < n; i += 4 * stride) {
+    const double x0 = fr_load(c, i), x1 = fr_load(c, i + stride), x2 = fr_load(c, i + 2 * stride),
+                 x3 = fr_load(c, i + 3 * stride);
+    acc(x0); acc(x1); acc(x2); acc(x3);
   }
+  for (; i < n; i += stride) acc(fr_load(c, i));
   __shared__ double red[256][10];
   double* r = red[threadIdx.x];
   r[0] = pass ? s1 : cnt; r[1] = s1; r[2] = 0.0; r[3] = nan; r[4] = zer; r[5] = pin; r[6] = nin; r[7] = nint;
@@ -86,20 +93,35 @@ __global__ __launch_bounds__(256) void expand_numeric_kernel(const FrCol* __rest
                                                              const double* __restrict__ sd, OT* __restrict__ X,
                                                              int ldx, int base) {
   __shared__ OT tile[64][65];
+  __shared__ FrCol ct[64];
+  __shared__ double cp[3][64];
   const long long r0 = (long long)blockIdx.x * 64;
   const int j0 = blockIdx.y * 64;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;   // 64 x 4
-  // read: thread (tx = row, ty + 4k = column)
-  for (int k = ty; k < 64; k += 4) {
-    const int j = j0 + k;
-    const long long r = r0 + tx;
-    OT v = (OT)0;
-    if (j < ncols && r < n) {
-      double x = fr_load(cols[j], r);
-      if (x != x) x = plug[j];
-      v = (OT)((x - mean[j]) / sd[j]);
-    }
-    tile[k][tx] = v;
+  // the tile's column table and constants once per block (no dependent
+  // table -> pointer -> data chain per element)
+  if (threadIdx.x < 64) {
+    const int j = j0 + threadIdx.x;
+    ct[threadIdx.x] = j < ncols ? cols[j] : FrCol{nullptr, 0, 0};
+    cp[0][threadIdx.x] = j < ncols ? plug[j] : 0.0;
+    cp[1][threadIdx.x] = j < ncols ? mean[j] : 0.0;
+    cp[2][threadIdx.x] = j < ncols ? sd[j] : 1.0;
+  }
+  __syncthreads();
+  // read: thread (tx = row, ty + 4k = column), all 16 loads issued first
+  const long long rr = r0 + tx;
+  double xv[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int k = ty + 4 * i;
+    xv[i] = (j0 + k < ncols && rr < n) ? fr_load(ct[k], rr) : 0.0;
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int k = ty + 4 * i;
+    double x = xv[i];
+    if (x != x) x = cp[0][k];
+    tile[k][tx] = (OT)((x - cp[1][k]) / cp[2][k]);
   }
   __syncthreads();
   // write: thread (tx = column, ty + 4k = row)
