@@ -100,6 +100,7 @@ def glm_irls(X, aug=-1, beta=None, b0=0.0, y=None, wprior=None, offset=None, cod
     pairs_t, pr = _pairs(T, X.device)
     npairs = len(pr)
     groups = -(-npairs // 36)
+    target_blocks = int(os.environ.get("H2O3_GI_BLOCKS", target_blocks))   # A/B knob
     splits = max(1, min(max(1, target_blocks // groups), N // 4096))
     rpb = -(-N // splits)
     rc = lib.h2o_glm_irls_chunk(P)
