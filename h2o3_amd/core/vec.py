@@ -154,6 +154,11 @@ class Vec:
     def rollups(self) -> dict:
         if self._rollups is not None:
             return self._rollups
+        if not self.on_host and self.data.is_cuda and self.type in NUMERIC_TYPES:
+            # the frame kernel (ops/csrc/frame.hip): one launch per pass, one host read
+            from ..ops import frame_ops
+            if frame_ops.batchable(self) and frame_ops.rollups_many([self]) and self._rollups is not None:
+                return self._rollups
         n = self.nrow()
         red = (lambda t, op="sum": t) if self.replicated else coll.allreduce_
         if self.on_host:

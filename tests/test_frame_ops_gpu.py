@@ -40,9 +40,12 @@ def test_rollups_many_matches_vec_rollups():
     cols = ["a", "b", "c", "d", "e", "f"]
     assert all(frame_ops.batchable(fr1.vec(c)) for c in cols)
     assert frame_ops.rollups_many([fr1.vec(c) for c in cols + ["k"]]) == len(cols)
+    from h2o3_amd.core.vec import Vec
     for c in cols:
         got = fr1.vec(c)._rollups
-        want = fr2.vec(c).rollups()
+        v2 = fr2.vec(c)
+        want = Vec(v2.data.cpu(), v2.type).rollups()            # the torch path (host tensors)
+        assert fr2.vec(c).rollups()["nacnt"] == want["nacnt"]    # Vec.rollups on the device: the kernel
         for k in ("nacnt", "zeros", "isInt", "nrow", "pinfs", "ninfs"):
             assert got[k] == want[k], (c, k, got[k], want[k])
         for k in ("min", "max", "mean", "sigma"):
