@@ -1542,12 +1542,15 @@ extern "C" int h2o_glm_wide_gram(const float* X, int ldx, int P, long long N, co
 // (8 consecutive columns, one k-block) land in 8 different 16-B bank groups
 // of the 256-B bank row: pitch 64 B -> swizzle by column >> 2, pitch 128 B
 // -> by column >> 1.
-template <int KR>
+template <int KR, int SWZ = 0>
 __device__ __forceinline__ int wg2_off(int col, int kb) {
-  return col * KR + ((kb ^ ((col >> (KR == 32 ? 2 : 1)) & (KR / 8 - 1))) << 3);
+  // SWZ (KR = 64 A/B only): 0 (col >> 1) & 7, 1 ((col >> 1) ^ (col >> 4)) & 7, 2 (col >> 2) & 7
+  const int x = KR == 32 ? (col >> 2) & 3
+                         : (SWZ == 1 ? ((col >> 1) ^ (col >> 4)) & 7 : SWZ == 2 ? (col >> 2) & 7 : (col >> 1) & 7);
+  return col * KR + ((kb ^ x) << 3);
 }
 
-template <bool BF3, int KR>
+template <bool BF3, int KR, int SWZ = 0>
 __global__ __launch_bounds__(512, 1) void glm_wide_gram256_kernel(const float* __restrict__ X, int ldx, int P,
                                                                   long long N, const float* __restrict__ Wr, int NB,
                                                                   int npairs, int S, int fold,
@@ -1619,7 +1622,7 @@ __global__ __launch_bounds__(512, 1) void glm_wide_gram256_kernel(const float* _
       h[e] = (__bf16)x;
       if constexpr (BF3) l[e] = (__bf16)(x - (float)h[e]);
     }
-    const int off = wg2_off<KR>(colb, rg);
+    const int off = wg2_off<KR, SWZ>(colb, rg);
     *reinterpret_cast<bf16x8*>(base + (pan ? PBH : 0) * WG2_T * KR + off) = h;
     if constexpr (BF3) *reinterpret_cast<bf16x8*>(base + (pan ? 3 : 1) * WG2_T * KR + off) = l;
   };
@@ -1671,13 +1674,13 @@ __global__ __launch_bounds__(512, 1) void glm_wide_gram256_kernel(const float* _
       bf16x8 ah[4], al[4];
 #pragma unroll
       for (int a = 0; a < 4; ++a) {
-        const int off = wg2_off<KR>(128 * mi + 32 * a + (lane & 31), kb);
+        const int off = wg2_off<KR, SWZ>(128 * mi + 32 * a + (lane & 31), kb);
         ah[a] = *reinterpret_cast<const bf16x8*>(sAh + off);
         if constexpr (BF3) al[a] = *reinterpret_cast<const bf16x8*>(sAl + off);
       }
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
-        const int off = wg2_off<KR>(64 * nq + 32 * b + (lane & 31), kb);
+        const int off = wg2_off<KR, SWZ>(64 * nq + 32 * b + (lane & 31), kb);
         const bf16x8 bh = *reinterpret_cast<const bf16x8*>(sBh + off);
 #pragma unroll
         for (int a = 0; a < 4; ++a) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bh, acc[a][b], 0, 0, 0);
@@ -1755,8 +1758,22 @@ extern "C" int h2o_glm_wide_gram256(const float* X, int ldx, int P, long long N,
   else if (KR == 32)
     hipLaunchKernelGGL((glm_wide_gram256_kernel<false, 32>), dim3(npairs * S), dim3(512), lds, s, X, ldx, P, N, Wr,
                        NB, npairs, S, fold, part, dbg);
-  else
-    hipLaunchKernelGGL((glm_wide_gram256_kernel<false, 64>), dim3(npairs * S), dim3(512), lds, s, X, ldx, P, N, Wr,
-                       NB, npairs, S, fold, part, dbg);
+  else {
+    static const int swz = getenv("H2O3_WG2_SWZ") ? atoi(getenv("H2O3_WG2_SWZ")) : 0;   // A/B knob
+    if (swz == 1) {
+      (void)hipFuncSetAttribute((const void*)glm_wide_gram256_kernel<false, 64, 1>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL((glm_wide_gram256_kernel<false, 64, 1>), dim3(npairs * S), dim3(512), lds, s, X, ldx, P, N,
+                         Wr, NB, npairs, S, fold, part, dbg);
+    } else if (swz == 2) {
+      (void)hipFuncSetAttribute((const void*)glm_wide_gram256_kernel<false, 64, 2>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL((glm_wide_gram256_kernel<false, 64, 2>), dim3(npairs * S), dim3(512), lds, s, X, ldx, P, N,
+                         Wr, NB, npairs, S, fold, part, dbg);
+    } else {
+      hipLaunchKernelGGL((glm_wide_gram256_kernel<false, 64>), dim3(npairs * S), dim3(512), lds, s, X, ldx, P, N, Wr,
+                         NB, npairs, S, fold, part, dbg);
+    }
+  }
   return (int)hipGetLastError();
 }
