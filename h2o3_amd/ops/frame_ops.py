@@ -73,8 +73,9 @@ def rollups_many(vecs) -> int:
     groups += [(True, n, vs) for n, vs in sorted(rep.items())]
     sh = [v for v in todo if not v.replicated]
     uniform = len({int(v.data.numel()) for v in sh}) <= 1
-    if cloud.world() > 1:
-        # every rank must take the same branch (the batch issues collectives)
+    if sh and cloud.world() > 1:
+        # every rank must take the same branch (the batch issues collectives);
+        # replicated-only calls (possibly on one rank) issue none
         uniform = coll.allreduce_scalar(1.0 if uniform else 0.0, "min") > 0
     if sh:
         lens = {int(v.data.numel()) for v in sh}
