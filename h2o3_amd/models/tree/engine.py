@@ -1618,7 +1618,8 @@ class TreeGrower:
         self._tree_no = getattr(self, "_tree_no", -1) + 1
         self._adaptive = getattr(bd, "hist_type", "auto") in ("uniformadaptive", "random", "roundrobin")
         self._stream_obj = torch.cuda.current_stream() if self.dev.type == "cuda" else None
-        torch.arange(N, dtype=torch.int32, device=self.dev, out=self.ridx)
+        if not (self.dev.type == "cuda" and tree_ops.iota_i32(self.ridx)):
+            torch.arange(N, dtype=torch.int32, device=self.dev, out=self.ridx)
         if self.dev.type != "cuda":
             self._vmax = None
         else:

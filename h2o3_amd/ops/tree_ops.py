@@ -768,6 +768,18 @@ def _part_chunk(total):
     return int(max(4096, min(16384, -(-int(total) // 2048 // 64) * 64)))
 
 
+def iota_i32(out) -> bool:
+    """out[:] = 0..n-1 (int32, device) by the 16-byte-store kernel; False when
+    it does not apply (the caller then uses torch.arange)."""
+    lib = _lib()
+    if lib is None or out.dtype != torch.int32 or not out.is_cuda or out.data_ptr() % 16:
+        return False
+    if not getattr(lib, "_typed_iota", False):
+        lib.h2o_iota_i32.argtypes = [_c_void, ctypes.c_longlong, _c_void]
+        lib._typed_iota = True
+    return lib.h2o_iota_i32(_ptr(out), out.numel(), _stream()) == 0
+
+
 def partition_async(bd, ridx, ridx_out, feat_d, masks, starts, counts, chunk=None, payload=None, pk=None,
                     pk_col=0):
     """Sync-free ballot partition of EVERY segment i by masks[i][code(row,
