@@ -19,7 +19,7 @@ def _install_module_aliases():
     from ._modules import MODULES
     _STAR = {"h2o.sklearn": "h2o3_amd.sklearn", "h2o.sklearn.wrapper": "h2o3_amd.sklearn",
              "h2o.tree": "h2o3_amd.tree", "h2o.tree.tree": "h2o3_amd.tree",
-             "h2o.transforms": "h2o3_amd.transforms", "h2o.explanation": "h2o3_amd.models.explain",
+             "h2o.transforms": "h2o3_amd.transforms", "h2o.explanation": "h2o3_amd.explanation",
              "h2o.information_retrieval": "h2o3_amd.information_retrieval"}
     packages = {m.rsplit(".", k)[0] for m in MODULES for k in range(1, m.count("."))}
 

@@ -579,6 +579,70 @@ class H2OAutoML:
     def get_leaderboard(self, extra_columns=None):
         return self._leaderboard.as_frame(extra_columns=extra_columns)
 
+    # ---- reference H2OAutoMLBaseMixin / H2OAutoML object API
+    # (h2o-py/h2o/automl/_base.py:41-237, _estimator.py)
+    @property
+    def key(self):
+        return self.project_name
+
+    def detach(self):
+        dkv.remove(self.project_name)
+
+    def download_pojo(self, path="", get_genmodel_jar=False, genmodel_name=""):
+        """POJO of the leader (_base.py:41)."""
+        return self.leader.download_pojo(path, get_genmodel_jar=get_genmodel_jar, genmodel_name=genmodel_name)
+
+    def download_mojo(self, path=".", get_genmodel_jar=False, genmodel_name="", **kw):
+        """MOJO of the leader (_base.py:54); format="h2o" writes the reference
+        h2o-genmodel layout."""
+        return self.leader.download_mojo(path, get_genmodel_jar=get_genmodel_jar, genmodel_name=genmodel_name, **kw)
+
+    def pareto_front(self, test_frame=None, x_metric=None, y_metric=None, **kwargs):
+        """Pareto front of the leaderboard (_base.py:237): prediction time per
+        row vs the sort metric by default, optimum from the metric directions."""
+        from ..explanation import pareto_front
+        from .leaderboard import make_leaderboard
+        lb = self.get_leaderboard("ALL") if test_frame is None else \
+            make_leaderboard(self, test_frame, extra_columns="ALL")
+        x_metric = x_metric or "predict_time_per_row_ms"
+        y_metric = y_metric or lb.columns[1]
+        hib = ("auc", "aucpr")
+        optimum = "{} {}".format("top" if y_metric.lower() in hib else "bottom",
+                                 "right" if x_metric.lower() in hib else "left")
+        kwargs.setdefault("title", f"Pareto Front for {self.project_name}")
+        return pareto_front(lb, x_metric, y_metric, optimum=optimum, **kwargs)
+
+    def _lb_models(self):
+        return list(self._leaderboard.models) if self._leaderboard else []
+
+    def explain(self, frame, **kw):
+        from ..explanation import explain
+        return explain(self._lb_models(), frame, **kw)
+
+    def explain_row(self, frame, row_index, **kw):
+        from ..explanation import explain_row
+        return explain_row([self.leader], frame, row_index, **kw)
+
+    def varimp(self, use_pandas=True, **kw):
+        from ..explanation import varimp
+        return varimp(self._lb_models(), use_pandas=use_pandas, **kw)
+
+    def varimp_heatmap(self, **kw):
+        from ..explanation import varimp_heatmap
+        return varimp_heatmap(self._lb_models(), **kw)
+
+    def model_correlation(self, frame, **kw):
+        from ..explanation import model_correlation
+        return model_correlation(self._lb_models(), frame, **kw)
+
+    def model_correlation_heatmap(self, frame, **kw):
+        from ..explanation import model_correlation_heatmap
+        return model_correlation_heatmap(self._lb_models(), frame, **kw)
+
+    def pd_multi_plot(self, frame, column, **kw):
+        from ..explanation import pd_multi_plot
+        return pd_multi_plot(self._lb_models(), frame, column, **kw)
+
     @property
     def modeling_steps(self):
         return [{"name": a, "steps": [{"id": s}]} for a, s in (t.split(":") for t in self._done_steps)]

@@ -33,6 +33,7 @@ class Leaderboard:
             sm = {"binomial": "auc", "multinomial": "mean_per_class_error", "regression": "mean_residual_deviance"}[self.kind]
         self.sort_metric = sm
         self._cache = {}
+        self._ptime = {}
         dec = sm in ("auc", "aucpr")
         self.models = sorted(models, key=lambda m: self._score(m, sm), reverse=dec)
 
@@ -40,7 +41,9 @@ class Leaderboard:
         if m.model_id in self._cache:
             return self._cache[m.model_id]
         if self.frame is not None:
+            t0 = time.perf_counter()
             mt = m.model_performance(self.frame)
+            self._ptime[m.model_id] = 1000.0 * (time.perf_counter() - t0) / max(int(self.frame.nrows), 1)
         else:
             mt = m._cross_validation_metrics or m._validation_metrics or m._training_metrics
         self._cache[m.model_id] = mt
@@ -52,6 +55,21 @@ class Leaderboard:
         if v is None or (isinstance(v, float) and math.isnan(v)):
             return -math.inf if metric in ("auc", "aucpr") else math.inf
         return v
+
+    def _predict_time(self, m):
+        """Per-row scoring time in ms (LeaderboardExtensionsProvider's
+        predict_time_per_row_ms): timed on the leaderboard frame when the board
+        was scored on one, else on up to 10k rows of the model's training frame."""
+        if m.model_id not in self._ptime:
+            fr = getattr(getattr(m, "_spec", None), "frame", None)
+            if fr is None:
+                return float("nan")
+            n = min(int(fr.nrows), 10000)
+            sub = fr[:n, :] if n < int(fr.nrows) else fr
+            t0 = time.perf_counter()
+            m.predict(sub)
+            self._ptime[m.model_id] = 1000.0 * (time.perf_counter() - t0) / max(n, 1)
+        return self._ptime[m.model_id]
 
     def as_frame(self, extra_columns=None):
         from ..core.frame import H2OFrame
@@ -69,6 +87,8 @@ class Leaderboard:
                 r[c] = v if math.isfinite(v) else float("nan")
             if extra_columns in ("ALL", "training_time_ms") or (isinstance(extra_columns, list) and "training_time_ms" in extra_columns):
                 r["training_time_ms"] = int(m._run_time * 1000)
+            if extra_columns == "ALL" or (isinstance(extra_columns, list) and "predict_time_per_row_ms" in extra_columns):
+                r["predict_time_per_row_ms"] = self._predict_time(m)
             if extra_columns == "ALL" or (isinstance(extra_columns, list) and "algo" in extra_columns):
                 r["algo"] = m.algo
             rows.append(r)
@@ -99,4 +119,5 @@ def make_leaderboard(object, leaderboard_frame=None, sort_metric="AUTO", extra_c
                            reverse=lb.sort_metric in ("auc", "aucpr"))
     else:
         lb = Leaderboard(models, sort_metric, leaderboard_frame)
-    return lb.as_frame(list(extra_columns) if extra_columns else None)
+    ec = extra_columns if isinstance(extra_columns, str) else (list(extra_columns) if extra_columns else None)
+    return lb.as_frame(ec)

@@ -66,13 +66,11 @@ class Job:
             self.progress_msg = msg
         vals = [1.0 if self.cancel_requested else 0.0] + [float(e) for e in extra]
         self._nticks = getattr(self, "_nticks", 0) + 1
-        # cancel-only ticks agree every 4th iteration (a count, so every rank
-        # picks the same ticks): one control-plane broadcast per 4 trees
-        # instead of per tree; decisions in `extra` are agreed every tick
-        if (extra or (self._spmd_any() and self._nticks % 4 == 1)) and cloud.is_distributed():
+        # SPMD builds agree on the cancel flag at EVERY tick (rank 0's REST
+        # thread sets it; the reference checks stop_requested per tree), so a
+        # cancel is never delayed by more than one iteration nor dropped
+        if (extra or self._spmd_any()) and cloud.is_distributed():
             vals = cloud.agree(vals)
-        elif cloud.is_distributed() and self._spmd_any():
-            vals[0] = 0.0
         if vals[0]:
             self._cancel = True
             raise JobCancelled(self.key)

@@ -28,10 +28,15 @@ class H2OGridSearch:
         self.grid_id = grid_id or dkv.make_key("Grid")
         self.search_criteria = dict(search_criteria or {"strategy": "Cartesian"})
         self.models = []
-        self.failed_params = []
+        self._failures = []          # (combo, message, stack trace) per failed build
         self._sort_metric = None
         self.export_checkpoints_dir = export_checkpoints_dir
         self.recovery_dir = recovery_dir
+        self.parallelism = parallelism
+        self._job = None
+        self._thread = None
+        self._error = None
+        self._train_args = None
 
     def _estimator_factory(self):
         m = self.model
@@ -60,7 +65,12 @@ class H2OGridSearch:
         t0 = time.time()
         make = self._estimator_factory()
         history = []
+        self._train_args = dict(x=x, y=y, training_frame=training_frame, offset_column=offset_column,
+                                fold_column=fold_column, weights_column=weights_column,
+                                validation_frame=validation_frame, **params)
         done = self._recover()
+        # combinations already built (a resumed / restarted grid) are skipped
+        done |= {repr(sorted(m._grid_params.items())) for m in self.models if getattr(m, "_grid_params", None)}
         if self.recovery_dir:
             self._save_train_inputs(x, y, training_frame, validation_frame, weights_column, offset_column,
                                     fold_column, params)
@@ -98,7 +108,8 @@ class H2OGridSearch:
             except Exception as e:  # reference keeps failures in the grid's failure list
                 if isinstance(e, jobmod.JobCancelled):
                     raise
-                self.failed_params.append((combo, repr(e)))
+                import traceback
+                self._failures.append((combo, repr(e), traceback.format_exc()[-4000:]))
         dkv.put(self.grid_id, self)
         return self
 
@@ -216,7 +227,8 @@ class H2OGridSearch:
         g = H2OGridSearch(self.model, self.hyper_params, self.grid_id, self.search_criteria)
         g.models = sorted(self.models, key=lambda m: self._metric_of(m, metric), reverse=decreasing)
         g._sort_metric = metric
-        g.failed_params = self.failed_params
+        g._failures = self._failures
+        g._train_args = self._train_args
         return g
 
     def sorted_metric_table(self):
@@ -230,18 +242,294 @@ class H2OGridSearch:
             rows.append(r)
         return pd.DataFrame(rows)
 
-    summary = sorted_metric_table
-
     @property
     def model_ids(self):
         return [m.model_id for m in self.models]
 
+    # ------------------------------------------------------------ grid state
+    # reference: h2o-py/h2o/grid/grid_search.py:110-206 (properties read from the
+    # grid's JSON); here they read the in-process grid
+    @property
+    def key(self):
+        return self.grid_id
+
+    @property
+    def hyper_names(self):
+        return list(self.hyper_params)
+
+    @property
+    def failed_params(self):
+        return [dict(c) for c, _, _ in self._failures]
+
+    @property
+    def failure_details(self):
+        return [m for _, m, _ in self._failures]
+
+    @property
+    def failure_stack_traces(self):
+        return [t for _, _, t in self._failures]
+
+    @property
+    def failed_raw_params(self):
+        return [[str(c.get(k)) for k in self.hyper_params] for c, _, _ in self._failures]
+
+    def detach(self):
+        self.grid_id = None
+
+    # ------------------------------------------------------------ async build
+    def start(self, x, y=None, training_frame=None, offset_column=None, fold_column=None, weights_column=None,
+              validation_frame=None, **params):
+        """Asynchronous grid build (grid_search.py:209): the models are built on a
+        background thread under a Job; join() waits, cancel() stops it after the
+        model in progress (the grid job's cancel reaches each build's tick)."""
+        import threading
+        job = jobmod.Job(f"Grid search {self.grid_id}", dest=self.grid_id, dest_kind="Grid")
+        self._job, self._error = job, None
+
+        def run():
+            job.start()
+            jobmod.push(job)
+            try:
+                self.train(x=x, y=y, training_frame=training_frame, offset_column=offset_column,
+                           fold_column=fold_column, weights_column=weights_column,
+                           validation_frame=validation_frame, **params)
+                job.done()
+            except BaseException as e:    # surfaced by join()
+                job.fail(e)
+                self._error = e
+            finally:
+                jobmod.pop(job)
+                dkv.put(self.grid_id, self)
+
+        self._thread = threading.Thread(target=run, name=f"grid-{self.grid_id}", daemon=True)
+        self._thread.start()
+        return self
+
+    def join(self):
+        """Wait until the grid finishes (grid_search.py:252)."""
+        if self._thread is not None:
+            self._thread.join()
+            self._thread = None
+        job, self._job = self._job, None
+        err, self._error = self._error, None
+        if err is not None and not isinstance(err, jobmod.JobCancelled) and not (job and job.cancel_requested):
+            raise err
+        return self
+
+    def cancel(self):
+        """Cancel a running grid (grid_search.py:274)."""
+        if self._job is None:
+            raise ValueError("Grid is not running.")
+        self._job.cancel()
+
+    def resume(self, recovery_dir=None, **kwargs):
+        """Continue a stopped grid (grid_search.py:358): the combinations not yet
+        built are trained with the arguments of the last train() / start() (or
+        the recovery state in recovery_dir); kwargs override search criteria."""
+        detach = kwargs.pop("detach", False)
+        if recovery_dir is not None:
+            self.recovery_dir = recovery_dir
+        for k in ("max_models", "max_runtime_secs", "stopping_rounds", "stopping_metric", "stopping_tolerance"):
+            if k in kwargs:
+                self.search_criteria[k] = kwargs.pop(k)
+        args = dict(self._train_args or {})
+        if not args and self.recovery_dir:
+            import json
+            import os
+            from ..core.frame_io import load_frame
+            st = json.load(open(self._state_path()))
+            tr = st["train"]
+            args = dict(x=tr.get("x"), y=tr.get("y"),
+                        training_frame=load_frame(None, os.path.join(self.recovery_dir, tr["frame_dir"])),
+                        validation_frame=load_frame(None, os.path.join(self.recovery_dir, tr["valid_dir"]))
+                        if tr.get("valid_dir") else None, weights_column=tr.get("weights_column"),
+                        offset_column=tr.get("offset_column"), fold_column=tr.get("fold_column"),
+                        **tr.get("params", {}))
+        if not args:
+            raise ValueError("resume: this grid was never trained (no training arguments to resume with)")
+        args.update(kwargs)
+        return self.start(**args) if detach else self.train(**args)
+
+    def build_model(self, algo_params):
+        """(internal, grid_search.py:373) train with a parameter dict."""
+        p = dict(algo_params)
+        keys = ("x", "y", "training_frame", "offset_column", "fold_column", "weights_column", "validation_frame")
+        return self.train(**{k: p.pop(k, None) for k in keys}, **p)
+
+    # ------------------------------------------------------------ per-model passthroughs
+    # every one returns {model_id: value} over the grid's models, as the
+    # reference client does (grid_search.py:485-1353)
+    def _each(self, fn):
+        return {m.model_id: fn(m) for m in self.models}
+
+    def predict(self, test_data):
+        return self._each(lambda m: m.predict(test_data))
+
+    def is_cross_validated(self):
+        return self._each(lambda m: m.is_cross_validated())
+
+    def xval_keys(self):
+        return self._each(lambda m: m.xval_keys())
+
+    def get_xval_models(self, key=None):
+        def one(m):
+            xs = m.get_xval_models()
+            if key is None:
+                return xs
+            return next((x for x in (xs or []) if x.model_id == key), None)
+        return self._each(one)
+
+    def xvals(self):
+        return self._each(lambda m: m.xvals)
+
+    def deepfeatures(self, test_data, layer):
+        return self._each(lambda m: m.deepfeatures(test_data, layer))
+
+    def weights(self, matrix_id=0):
+        return self._each(lambda m: m.weights(matrix_id))
+
+    def biases(self, vector_id=0):
+        return self._each(lambda m: m.biases(vector_id))
+
+    def normmul(self):
+        return self._each(lambda m: m.normmul())
+
+    def normsub(self):
+        return self._each(lambda m: m.normsub())
+
+    def respmul(self):
+        return self._each(lambda m: m.respmul())
+
+    def respsub(self):
+        return self._each(lambda m: m.respsub())
+
+    def catoffsets(self):
+        return self._each(lambda m: m.catoffsets())
+
+    def model_performance(self, test_data=None, train=False, valid=False, xval=False):
+        return self._each(lambda m: m.model_performance(test_data, train, valid, xval))
+
+    def scoring_history(self):
+        return self._each(lambda m: m.scoring_history())
+
+    def varimp(self, use_pandas=False):
+        return self._each(lambda m: m.varimp(use_pandas))
+
+    def residual_deviance(self, train=False, valid=False, xval=False):
+        return self._each(lambda m: m.residual_deviance(train, valid, xval))
+
+    def residual_degrees_of_freedom(self, train=False, valid=False, xval=False):
+        return self._each(lambda m: m.residual_degrees_of_freedom(train, valid, xval))
+
+    def null_deviance(self, train=False, valid=False, xval=False):
+        return self._each(lambda m: m.null_deviance(train, valid, xval))
+
+    def null_degrees_of_freedom(self, train=False, valid=False, xval=False):
+        return self._each(lambda m: m.null_degrees_of_freedom(train, valid, xval))
+
+    def pprint_coef(self):
+        for i, m in enumerate(self.models):
+            print("Model", i)
+            m.pprint_coef()
+            print()
+
+    def coef(self):
+        return self._each(lambda m: m.coef())
+
+    def coef_norm(self):
+        return self._each(lambda m: m.coef_norm())
+
+    def r2(self, train=False, valid=False, xval=False):
+        return self._each(lambda m: m.r2(train, valid, xval))
+
+    def mse(self, train=False, valid=False, xval=False):
+        return self._each(lambda m: m.mse(train, valid, xval))
+
+    def rmse(self, train=False, valid=False, xval=False):
+        return self._each(lambda m: m.rmse(train, valid, xval))
+
+    def mae(self, train=False, valid=False, xval=False):
+        return self._each(lambda m: m.mae(train, valid, xval))
+
+    def rmsle(self, train=False, valid=False, xval=False):
+        return self._each(lambda m: m.rmsle(train, valid, xval))
+
+    def logloss(self, train=False, valid=False, xval=False):
+        return self._each(lambda m: m.logloss(train, valid, xval))
+
+    def mean_residual_deviance(self, train=False, valid=False, xval=False):
+        return self._each(lambda m: m.mean_residual_deviance(train, valid, xval))
+
+    def auc(self, train=False, valid=False, xval=False):
+        return self._each(lambda m: m.auc(train, valid, xval))
+
+    def aic(self, train=False, valid=False, xval=False):
+        return self._each(lambda m: m.aic(train, valid, xval))
+
+    def gini(self, train=False, valid=False, xval=False):
+        return self._each(lambda m: m.gini(train, valid, xval))
+
+    def aucpr(self, train=False, valid=False, xval=False):
+        return self._each(lambda m: m.aucpr(train, valid, xval))
+
+    pr_auc = aucpr
+
+    # ------------------------------------------------------------ summaries
+    def get_summary(self):
+        """One row per model: its model summary with the model id first
+        (grid_search.py:852)."""
+        import pandas as pd
+        rows = []
+        for m in self.models:
+            s = m.get_summary() if hasattr(m, "get_summary") else None
+            if s is None:
+                r = {}
+            elif isinstance(s, pd.DataFrame):
+                r = s.iloc[0].to_dict() if len(s) else {}
+            elif isinstance(s, dict):
+                r = dict(s)
+            else:
+                r = {"summary": str(s)}
+            r.pop("", None)
+            rows.append({"Model Id": m.model_id, **r})
+        return pd.DataFrame(rows)
+
+    def show_summary(self):
+        print(self.get_summary().to_string())
+
+    def summary(self):
+        """Deprecated alias of show_summary (grid_search.py:886)."""
+        self.show_summary()
+
+    def sort_by(self, metric, increasing=True):
+        """Deprecated (grid_search.py:1540): the sorted metric table by `metric`."""
+        return self.get_grid(sort_by=metric.split("(")[0], decreasing=not increasing).sorted_metric_table()
+
+    def pareto_front(self, test_frame, x_metric=None, y_metric=None, **kwargs):
+        """Pareto front of the grid's models on test_frame (grid_search.py:1554):
+        leaderboard with every extra column, optimum corner from the metrics'
+        directions, then h2o.explanation.pareto_front."""
+        from ..automl.leaderboard import make_leaderboard
+        from ..explanation import pareto_front
+        lb = make_leaderboard(self, test_frame, extra_columns="ALL")
+        x_metric = x_metric or "predict_time_per_row_ms"
+        y_metric = y_metric or lb.columns[1]
+        hib = ("auc", "aucpr")
+        optimum = "{} {}".format("top" if y_metric.lower() in hib else "bottom",
+                                 "right" if x_metric.lower() in hib else "left")
+        kwargs.setdefault("title", f"Pareto Front for {self.grid_id}")
+        return pareto_front(lb, x_metric, y_metric, optimum=optimum, **kwargs)
+
     def get_hyperparams(self, id, display=True):
         m = self.models[id] if isinstance(id, int) else next(mm for mm in self.models if mm.model_id == id)
+        if display:
+            print("Hyperparameters: [" + ", ".join(self.hyper_params) + "]")
         return [m._grid_params[k] for k in self.hyper_params]
 
     def get_hyperparams_dict(self, id, display=True):
         m = self.models[id] if isinstance(id, int) else next(mm for mm in self.models if mm.model_id == id)
+        if display:
+            print("Hyperparameters: [" + ", ".join(self.hyper_params) + "]")
         return dict(m._grid_params)
 
     def __getitem__(self, i):
@@ -253,20 +541,8 @@ class H2OGridSearch:
     def __iter__(self):
         return iter(self.models)
 
-    def show(self):
+    def show(self, verbosity=None, fmt=None):
         print(self.sorted_metric_table())
-
-    # metric passthroughs (return dict model_id -> value like h2o-py)
-    def _all(self, name, **kw):
-        return {m.model_id: getattr(m, name)(**kw) for m in self.models}
-
-    def auc(self, train=False, valid=False, xval=False): return self._all("auc", train=train, valid=valid, xval=xval)
-    def logloss(self, train=False, valid=False, xval=False): return self._all("logloss", train=train, valid=valid, xval=xval)
-    def rmse(self, train=False, valid=False, xval=False): return self._all("rmse", train=train, valid=valid, xval=xval)
-    def mse(self, train=False, valid=False, xval=False): return self._all("mse", train=train, valid=valid, xval=xval)
-
-    def predict(self, test_data):
-        return {m.model_id: m.predict(test_data) for m in self.models}
 
 
 # ---------------------------------------------------------------- save / load / resume
@@ -294,7 +570,7 @@ def save_grid(grid_directory, grid_id):
           "hyper_params": _json_safe(g.hyper_params), "search_criteria": _json_safe(g.search_criteria),
           "models": [{"model_id": m.model_id, "params": _json_safe(getattr(m, "_grid_params", {}))}
                      for m in g.models],
-          "failed": [[_json_safe(c), e] for c, e in g.failed_params]}
+          "failed": [[_json_safe(c), e] for c, e, _ in g._failures]}
     path = os.path.join(grid_directory, g.grid_id)
     with open(path, "w") as f:
         json.dump(st, f, default=str)
@@ -327,7 +603,7 @@ def load_grid(grid_file_path):
         m = load_model(os.path.join(d, rec["model_id"]))
         m._grid_params = rec["params"]
         g.models.append(m)
-    g.failed_params = [tuple(x) for x in st.get("failed", [])]
+    g._failures = [(x[0], x[1], "") for x in st.get("failed", [])]
     dkv.put(g.grid_id, g)
     return g
 

@@ -728,6 +728,126 @@ class H2OEstimator:
     def gini(self, train=False, valid=False, xval=False): return self._pick("gini", train, valid, xval)
     def mean_per_class_error(self, train=False, valid=False, xval=False): return self._pick("mean_per_class_error", train, valid, xval)
     def mean_residual_deviance(self, train=False, valid=False, xval=False): return self._pick("mean_residual_deviance", train, valid, xval)
+
+    # ---- ModelBase methods that only some algorithms answer (reference
+    # h2o-py/h2o/model/model_base.py): the generic answer of the reference
+    # client for the others -- None, a message, or the server's refusal
+    def _dev_pick(self, key, train, valid, xval):
+        if xval:
+            raise ValueError("Cross-validation metrics are not available.")
+        m = self._validation_metrics if (valid and not train) else self._training_metrics
+        if m is None:
+            return None
+        f = getattr(m, key, None)
+        return f() if callable(f) else (m.get(key) if hasattr(m, "get") else None)
+
+    def residual_deviance(self, train=False, valid=False, xval=False):
+        return self._dev_pick("residual_deviance", train, valid, xval)
+
+    def residual_degrees_of_freedom(self, train=False, valid=False, xval=False):
+        return self._dev_pick("residual_degrees_of_freedom", train, valid, xval)
+
+    def null_deviance(self, train=False, valid=False, xval=False):
+        return self._dev_pick("null_deviance", train, valid, xval)
+
+    def null_degrees_of_freedom(self, train=False, valid=False, xval=False):
+        return self._dev_pick("null_degrees_of_freedom", train, valid, xval)
+
+    def aic(self, train=False, valid=False, xval=False):
+        return self._pick("aic", train, valid, xval)
+
+    def coef(self):
+        """Coefficients (GLM family); None for models without a coefficients table."""
+        return None
+
+    def coef_norm(self):
+        return None
+
+    def coef_with_p_values(self):
+        raise ValueError("p-values, z-values and std_error are only found in GLM.")
+
+    def rotation(self):
+        raise ValueError("This function is available for PCA models only")
+
+    def deepfeatures(self, test_data, layer):
+        raise ValueError(f"{self.algo}: deep features are only available for Deep Learning models")
+
+    def weights(self, matrix_id=0):
+        raise ValueError(f"{self.algo}: weight matrices are only available for Deep Learning models")
+
+    def biases(self, vector_id=0):
+        raise ValueError(f"{self.algo}: bias vectors are only available for Deep Learning models")
+
+    def staged_predict_proba(self, test_data):
+        raise ValueError(f"{self.algo}: staged predictions are only available for tree models")
+
+    def predict_contributions(self, test_data, output_format="Original", top_n=None, bottom_n=None,
+                              compare_abs=False, **kw):
+        raise ValueError(f"{self.algo}: contributions (SHAP) are only available for tree models")
+
+    def feature_frequencies(self, test_data):
+        raise ValueError(f"{self.algo}: feature frequencies are only available for tree models")
+
+    def ntrees_actual(self):
+        print("No actual number of trees for this model")
+
+    def feature_interaction(self, max_interaction_depth=100, max_tree_depth=100, max_deepening=-1, path=None):
+        print("No calculation available for this model")
+
+    def update_tree_weights(self, frame, weights_column):
+        print("Only supervised tree-based models support tree-reweighting")
+
+    def plot(self, timestep="AUTO", metric="AUTO", server=False, save_plot_path=None, **kwargs):
+        """Scoring-history plot (binomial: the ROC curve with metric="roc"),
+        model_base.py / models/binomial.py plot."""
+        from .explain_plots import _plt
+        plt = _plt()
+        fig = plt.figure(figsize=(7, 5))
+        if str(metric).lower() == "roc":
+            roc = self.roc()
+            fpr, tpr = (roc if isinstance(roc, (tuple, list)) and len(roc) == 2 else ([0, 1], [0, 1]))
+            plt.plot(fpr, tpr)
+            plt.xlabel("False Positive Rate")
+            plt.ylabel("True Positive Rate")
+            plt.title(f"ROC curve for {self.model_id}")
+        else:
+            sh = self.scoring_history()
+            if sh is not None and len(sh):
+                num = [c for c in sh.columns if c.startswith("training_") or c.startswith("validation_")]
+                want = str(metric).lower()
+                cols = [c for c in num if want == "auto" or want in c.lower()][:4]
+                xcol = next((c for c in ("number_of_trees", "iterations", "epochs", "iteration") if c in sh.columns),
+                            None)
+                xs = sh[xcol] if xcol else range(len(sh))
+                for c in cols:
+                    plt.plot(xs, sh[c], label=c)
+                plt.legend()
+                plt.xlabel(xcol or "scoring event")
+            plt.title(f"Scoring History for {self.model_id}")
+        if save_plot_path is not None:
+            fig.savefig(save_plot_path)
+        return fig
+
+    def gains_lift_plot(self, type="both", server=False, save_plot_path=None, **kwargs):
+        """Cumulative gains / lift of a binomial model (models/binomial.py)."""
+        from .explain_plots import _plt
+        plt = _plt()
+        gl = self.gains_lift()
+        fig = plt.figure(figsize=(7, 5))
+        if gl is not None:
+            import pandas as pd
+            t = gl if isinstance(gl, pd.DataFrame) else pd.DataFrame(gl)
+            x = t["cumulative_data_fraction"] if "cumulative_data_fraction" in t else range(len(t))
+            if type in ("both", "gains") and "cumulative_capture_rate" in t:
+                plt.plot(x, t["cumulative_capture_rate"], label="cumulative gains")
+            if type in ("both", "lift") and "cumulative_lift" in t:
+                plt.plot(x, t["cumulative_lift"], label="cumulative lift")
+            plt.legend()
+            plt.xlabel("cumulative data fraction")
+        plt.title(f"Gains / Lift for {self.model_id}")
+        if save_plot_path is not None:
+            fig.savefig(save_plot_path)
+        return fig
     def confusion_matrix(self, train=False, valid=False, xval=False, **kw): return self._pick("confusion_matrix", train, valid, xval)
 
     # ---- threshold metrics of binomial models (h2o-py model/models/binomial.py);

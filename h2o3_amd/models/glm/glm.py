@@ -1129,8 +1129,13 @@ class GLMDriver:
         self.iter += 1
         obj = dev * r / 2 + l1 * np.abs(new[:-1]).sum() + l2 / 2 * (new[:-1] ** 2).sum()
         self.last_grad = gmax
+        # gaussian/identity is solved exactly by one Newton step only when the
+        # Hessian is exact (fp64 tier / host path); on a reduced-precision tier
+        # the step carries ~kappa * eps(tier) relative error, removed by further
+        # steps on the exact-gradient channel (iterative refinement)
+        one_step = self.fam.family == "gaussian" and self.fam.link == "identity" and self._hprec in (None, "f64")
         self.converged = diff < self.beta_eps or abs(self.last_obj - obj) < self.obj_eps * max(abs(obj), 1e-12) or \
-            (self.fam.family == "gaussian" and self.fam.link == "identity") or (self.iter > 1 and gmax < self.grad_eps)
+            one_step or (self.iter > 1 and gmax < self.grad_eps)
         if self.early_stop_enabled and not (self.fam.family == "gaussian" and self.fam.link == "identity"):
             self.converged = False
         self.last_obj = obj

@@ -465,6 +465,28 @@ class H2OKMeansEstimator(H2OEstimator):
     def withinss(self, train=False, valid=False, xval=False):
         return self._training_metrics.withinss()
 
+    def centroid_stats(self, train=False, valid=False):
+        """Per-cluster (centroid, size, within_cluster_sum_of_squares) table of
+        the training (or validation) metrics (ModelMetricsClustering
+        centroid_stats; h2o-py model/models/clustering.py:189)."""
+        import pandas as pd
+
+        def one(mt):
+            if mt is None:
+                return None
+            size = mt.get("size") if hasattr(mt, "get") else None
+            wss = mt.withinss() if hasattr(mt, "withinss") else None
+            if size is None or wss is None:
+                return None
+            return pd.DataFrame({"centroid": list(range(1, len(size) + 1)), "size": [float(v) for v in size],
+                                 "within_cluster_sum_of_squares": [float(v) for v in wss]})
+        res = {}
+        if train or not valid:
+            res["train"] = one(self._training_metrics)
+        if valid:
+            res["valid"] = one(self._validation_metrics)
+        return list(res.values())[0] if len(res) == 1 else res
+
     def num_iterations(self):
         return self._iterations
 

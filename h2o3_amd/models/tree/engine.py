@@ -737,13 +737,14 @@ class TreeGrower:
                 lib.h2o_split_select2.argtypes = [cv, cv, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                   ctypes.c_double, ctypes.c_int, cv, cv, cv, cv]
                 lib._typed_sel2 = True
-            pk = torch.empty((n, 12), dtype=torch.float64, device=self.dev)
+            # 13 fields: split_select2's 12 + the node's NA weight on the chosen column
+            pk = torch.empty((n, 13), dtype=torch.float64, device=self.dev)
             mask = torch.empty((n, Bs), dtype=torch.uint8, device=self.dev)
             feat_i = torch.empty(n, dtype=torch.int32, device=self.dev)
             if self.f0 < self.bd.F:
                 min_w2 = -1.0 if p.criterion == "xgb" else 2.0 * float(p.min_rows)
                 rc = lib.h2o_split_select2(ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(H.data_ptr()), Fl, n,
-                                           Bs, self.f0, min_w2, 12, ctypes.c_void_p(pk.data_ptr()),
+                                           Bs, self.f0, min_w2, 13, ctypes.c_void_p(pk.data_ptr()),
                                            ctypes.c_void_p(mask.data_ptr()), ctypes.c_void_p(feat_i.data_ptr()),
                                            tree_ops._stream())
                 if rc != 0:
@@ -971,7 +972,7 @@ class TreeGrower:
         st = np.asarray(f_st, dtype=np.int64)
         ct = np.asarray(f_ct, dtype=np.int64)
         per = max(1, int(p.hist_mem_budget // (k * Bs * 2 * 8)))
-        pk = torch.empty((n, 12), dtype=torch.float64, device=dev)
+        pk = torch.empty((n, 13), dtype=torch.float64, device=dev)
         mask = torch.empty((n, Bs), dtype=torch.uint8, device=dev)
         feat_i = torch.empty(n, dtype=torch.int32, device=dev)
         min_w2 = -1.0 if p.criterion == "xgb" else 2.0 * float(p.min_rows)
@@ -1002,7 +1003,7 @@ class TreeGrower:
                 Hl[:Hmine.shape[0]] = Hmine
                 wl = coll.reduce_scatter_dim0(wv.contiguous()) if wyy_n is not None else None
                 del Hp, Hmine
-                pk_l = torch.empty((nl, 12), dtype=torch.float64, device=dev)
+                pk_l = torch.empty((nl, 13), dtype=torch.float64, device=dev)
                 mask_l = torch.empty((nl, Bs), dtype=torch.uint8, device=dev)
                 feat_l = torch.empty(nl, dtype=torch.int32, device=dev)
                 self._pair_score_select(lib, Hl, nl, k, pfeat[lo * k:(lo + nl) * k].contiguous(), wl, min_w2,
@@ -1014,7 +1015,8 @@ class TreeGrower:
             self._pair_score_select(lib, Hp, nb, k, pfeat, wyy_n, min_w2, pk[a:b], mask[a:b], feat_i[a:b])
             del Hp
         return {"pk": pk, "feat_i32": feat_i, "mask": mask, "gain": pk[:, 0], "feat": pk[:, 1].long(),
-                "t": pk[:, 2].long(), "opt": pk[:, 3].long(), "L": pk[:, 4:6], "R": pk[:, 6:8], "tot": pk[:, 8:10]}
+                "t": pk[:, 2].long(), "opt": pk[:, 3].long(), "L": pk[:, 4:6], "R": pk[:, 6:8], "tot": pk[:, 8:10],
+                "naw": pk[:, 12]}
 
     # ------------------------------------------------------------------ multi-GPU pair exchange
     def _pair_exchange(self, Hp, pf, pn, n, full):
@@ -1133,13 +1135,13 @@ class TreeGrower:
                 lib._typed_psel2 = True
             rc = lib.h2o_pair_select2(ctypes.c_void_p(Hp.data_ptr()), n, Bs, k, ctypes.c_void_p(best_k.data_ptr()),
                                       ctypes.c_void_p(pfeat.data_ptr()), ctypes.c_void_p(self._fcat_u8.data_ptr()),
-                                      1 if p.criterion == "xgb" else 0, min_w2, 12, ctypes.c_void_p(pk.data_ptr()),
+                                      1 if p.criterion == "xgb" else 0, min_w2, pk.stride(0), ctypes.c_void_p(pk.data_ptr()),
                                       ctypes.c_void_p(mask.data_ptr()), ctypes.c_void_p(feat_i.data_ptr()),
                                       ctypes.c_void_p(nb_t.data_ptr()), tree_ops._stream())
         else:
             rc = lib.h2o_pair_select(ctypes.c_void_p(Hp.data_ptr()), n, Bs, k, ctypes.c_void_p(best_k.data_ptr()),
                                      ctypes.c_void_p(pfeat.data_ptr()), ctypes.c_void_p(self._fcat_u8.data_ptr()),
-                                     1 if p.criterion == "xgb" else 0, min_w2, 12, ctypes.c_void_p(pk.data_ptr()),
+                                     1 if p.criterion == "xgb" else 0, min_w2, pk.stride(0), ctypes.c_void_p(pk.data_ptr()),
                                      ctypes.c_void_p(mask.data_ptr()), ctypes.c_void_p(feat_i.data_ptr()),
                                      tree_ops._stream())
         if rc != 0:
@@ -1157,7 +1159,8 @@ class TreeGrower:
                "mask": torch.zeros((n, Bs), dtype=torch.uint8, device=dev),
                "L": torch.zeros((n, C), dtype=torch.float64, device=dev),
                "R": torch.zeros((n, C), dtype=torch.float64, device=dev),
-               "tot": torch.zeros((n, C), dtype=torch.float64, device=dev)}
+               "tot": torch.zeros((n, C), dtype=torch.float64, device=dev),
+               "naw": torch.zeros(n, dtype=torch.float64, device=dev)}
         with phase("tree.hist"), phase("tree.hist.pairs"):
             Hp, wyy_n = tree_ops.pair_hist(self.bd, ridx, va, vb, mode, st, ct, pn, pf, vmax=self._vmax, posv=posv,
                                            want_wyy=mode == 0)
@@ -1240,6 +1243,8 @@ class TreeGrower:
         out["mask"] = out["mask"].index_put((nodes,), mask)
         out["L"] = out["L"].index_put((nodes,), Lw)
         out["R"] = out["R"].index_put((nodes,), T - Lw)
+        if "naw" in out:
+            out["naw"] = out["naw"].index_put((nodes,), na[:, 0].to(out["naw"].dtype))
         return out
 
     def _pair_stats(self, h, pcat):
@@ -1760,6 +1765,7 @@ class TreeGrower:
                 del Hb
             nleft_pre = None
             ok_h = None
+            naw_h = None
             if can_split:
                 sel = self._col_sel(n_front, depth) if direct else None
                 cm = None if (direct and self.dev.type == "cuda") else self._col_mask(n_front, depth, sel=sel,
@@ -1806,10 +1812,16 @@ class TreeGrower:
                     self._flush_masks(tb)
                     ok_h = pk[:, 10] > 0
                     nleft_pre = pk[:, 11].astype(np.int64)
+                    naw_h = pk[:, 12] if pk.shape[1] > 12 else None
                 cols = [] if nleft_pre is not None else [
                     sp["gain"].view(nn_, 1).to(torch.float64), sp["feat"].view(nn_, 1).to(torch.float64),
                     sp["t"].view(nn_, 1).to(torch.float64), sp["opt"].view(nn_, 1).to(torch.float64),
                     sp["L"].to(torch.float64), sp["R"].to(torch.float64), sp["tot"].to(torch.float64)]
+                naw_d = sp["naw"].to(torch.float64) if (cols and sp.get("naw") is not None) else None
+                if naw_d is None and cols and H is not None and self.W == 1 and mode == 0 and H.shape[1] == nn_:
+                    # the winner's NA-bin weight per node (per-node NA direction rule below)
+                    fi = sp["feat"].to(torch.int64).clamp(0, H.shape[0] - 1)
+                    naw_d = H[fi, torch.arange(nn_, device=H.device), H.shape[2] - 1, 0].to(torch.float64)
                 if async_part and nleft_pre is None:
                     # split decision + partition of the whole frontier on the device: no
                     # host round trip between the split search and the row partition
@@ -1829,6 +1841,8 @@ class TreeGrower:
                     cols += [ok_d.view(nn_, 1).to(torch.float64), nleft_d.view(nn_, 1).to(torch.float64)]
                 # ONE device->host transfer of every per-node scalar of the level
                 if cols:
+                    if naw_d is not None:
+                        cols.append(naw_d.view(nn_, 1))      # last column
                     rec = torch.cat(cols, 1)
                     pk_h = self._d2h_async(rec)
                     if async_part:
@@ -1840,6 +1854,7 @@ class TreeGrower:
                     if async_part:
                         ok_h = pk[:, 4 + 3 * C] > 0
                         nleft_pre = pk[:, 5 + 3 * C].astype(np.int64)
+                    naw_h = pk[:, -1] if naw_d is not None else None
                 gains = pk[:, 0]
                 feats = pk[:, 1].astype(np.int64)
                 t_a = pk[:, 2].astype(np.int64)
@@ -1905,10 +1920,13 @@ class TreeGrower:
             tb.gain[nid_s] = gains[sids]
             na_s = opt_s == 1
             hn = getattr(self.bd, "has_na", None)
-            if hn is not None and len(hn) == self.bd.F and p.criterion != "xgb":
-                # no NA of this feature in training: NAs of later data go to the
-                # heavier child (DTree.java:1475-1478), numeric splits
-                free = ~np.asarray(hn, dtype=bool)[f_s] & (opt_s != 2) & ~is_cat_np[f_s]
+            if p.criterion != "xgb" and (naw_h is not None or (hn is not None and len(hn) == self.bd.F)):
+                # no NA weight reached THIS node on the split column: NAs of later
+                # data go to the heavier child (DTree.java:1475-1478 decides per
+                # node, nasplit == None); without the node's NA weight (chunked /
+                # pair / multi-rank torch paths) the training-wide flag stands in
+                no_na = (np.asarray(naw_h)[sids] == 0) if naw_h is not None else ~np.asarray(hn, dtype=bool)[f_s]
+                free = no_na & (opt_s != 2) & ~is_cat_np[f_s]
                 na_s = np.where(free, wl_a > wr_a, na_s)
             tb.na_left[nid_s] = na_s
             if self._adaptive:

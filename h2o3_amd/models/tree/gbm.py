@@ -188,6 +188,12 @@ class GBMDriver:
         if pend is None:
             return
         self._pending = None
+        if pend[0] == "dev":
+            # device-resident tree: the whole tree arrives as one heap record
+            _, hrec, ev = pend
+            ev.synchronize()
+            self._forest_obj.add(self._devtree.decode(hrec.numpy()), 0)
+            return
         tree, leaves, hv, ev = pend
         ev.synchronize()
         v = hv.numpy().tolist()
@@ -265,6 +271,9 @@ class GBMDriver:
         # are fitted -- the first tree uses learn_rate / annealing
         lr = self.lr * (float(p.get("learn_rate_annealing", 1.0)) ** (self.iter - 1))
         maxabs = float(p.get("max_abs_leafnode_pred", 1.79e308))
+        if self.K == 1 and self._devtree_ok():
+            self._step_devtree(lr)
+            return
         if self.K == 1:
             dpend = self.__dict__.get("_dpend")
             self._dpend = None
@@ -412,6 +421,40 @@ class GBMDriver:
                 self.forest.add(tree, k)
             for k in range(self.K):
                 self.f[:, k] += new[k]
+        self.iter += 1
+
+    def _devtree_ok(self):
+        """The device-resident tree (devtree.py) serves this configuration."""
+        dt = self.__dict__.get("_devtree")
+        if dt is not None:
+            return True
+        if self.__dict__.get("_devtree_why") is not None:
+            return False
+        if getattr(self, "_base_unit", None) is None:
+            bw = self.base_w
+            self._base_unit = bool(((bw == 0) | (bw == 1)).all())
+        from . import devtree
+        why = devtree.supported(self)
+        if why is None:
+            self._devtree = devtree.DevTreeGBM(self)
+            return True
+        self._devtree_why = why
+        return False
+
+    def _step_devtree(self, lr):
+        """One boosting iteration as one device-resident tree (graph replay on
+        one rank): residual, every level, leaf values and the per-row leaf
+        scatter without a host round trip; the tree's record is decoded on the
+        host while the GPU grows the next one."""
+        dt = self._devtree
+        dt.set_tree_cols(self.gp.tree_col_mask)
+        pending = self.__dict__.get("_dpend") is not None
+        self._dpend = None
+        with phase("gbm.devtree"):
+            hrec, ev = dt.run(lr, pending)
+        self._dpend = dt.dbuf
+        self._resolve_pending()
+        self._pending = ("dev", hrec, ev)
         self.iter += 1
 
     def _step_multi_dev(self, P, w, lr, maxabs):

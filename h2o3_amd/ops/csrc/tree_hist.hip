@@ -959,9 +959,11 @@ template <typename CodeT>
 __global__ __launch_bounds__(256) void part_flags_kernel(
     const CodeT* __restrict__ codes, long long rs, long long fs, const int* __restrict__ ridx,
     const int4* __restrict__ work, const int* __restrict__ fbase, const int* __restrict__ feat,
-    const uint8_t* __restrict__ masks, int Bs, unsigned long long* __restrict__ flags, int* __restrict__ cnt) {
+    const uint8_t* __restrict__ masks, int Bs, unsigned long long* __restrict__ flags, int* __restrict__ cnt,
+    const int* __restrict__ nw_dev) {
   __shared__ uint8_t m[4096];
   __shared__ int red[4];
+  if (nw_dev != nullptr && (int)blockIdx.x >= nw_dev[1]) return;   // device-built work list: grid = capacity
   const int4 wk = work[blockIdx.x];
   const int f = feat[wk.x];
   for (int i = threadIdx.x; i < Bs; i += blockDim.x) m[i] = masks[(size_t)wk.x * Bs + i];
@@ -1003,8 +1005,9 @@ template <int U>
 __global__ __launch_bounds__(256) void part_compact_kernel(
     const int* __restrict__ ridx, const int4* __restrict__ work, const int* __restrict__ fbase,
     const unsigned long long* __restrict__ flags, const int* __restrict__ loff, const int* __restrict__ roff,
-    int* __restrict__ out, const float* __restrict__ pa, float* __restrict__ pa_out) {
+    int* __restrict__ out, const float* __restrict__ pa, float* __restrict__ pa_out, const int* __restrict__ nw_dev) {
   __shared__ int wl[U][4], wr_[U][4];
+  if (nw_dev != nullptr && (int)blockIdx.x >= nw_dev[1]) return;
   const int4 wk = work[blockIdx.x];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int end = wk.y + wk.z;
@@ -1167,7 +1170,9 @@ __global__ __launch_bounds__(1024) void part_offsets_kernel(const int* __restric
 // NaN = zero-weight row.  mode 0: (sum z, count), mode 1 (bernoulli): (sum z,
 // sum |z|(1-|z|)).  work[i] = (leaf, start, count, -).
 __global__ __launch_bounds__(256) void leaf_pos_kernel(const float* __restrict__ zp, const int4* __restrict__ work,
-                                                       int mode, double* __restrict__ out) {
+                                                       int mode, double* __restrict__ out,
+                                                       const int* __restrict__ nw_dev) {
+  if (nw_dev != nullptr && (int)blockIdx.x >= nw_dev[1]) return;
   const int4 wk = work[blockIdx.x];
   double sa = 0.0, sb = 0.0;
   const int end = wk.y + wk.z;
@@ -1207,7 +1212,9 @@ __global__ __launch_bounds__(256) void leaf_update_kernel(const int* __restrict_
 // per-row leaf value (no read of f), folded into f by the next tree's
 // residual pass (gbm_grad_kernel with d) or an explicit contiguous add.
 __global__ __launch_bounds__(256) void leaf_scatter_kernel(const int* __restrict__ ridx, const int4* __restrict__ work,
-                                                           const float* __restrict__ val, float* __restrict__ d) {
+                                                           const float* __restrict__ val, float* __restrict__ d,
+                                                           const int* __restrict__ nw_dev) {
+  if (nw_dev != nullptr && (int)blockIdx.x >= nw_dev[1]) return;
   const int4 wk = work[blockIdx.x];
   const float v = val[wk.x];
   const int end = wk.y + wk.z;
@@ -1293,10 +1300,10 @@ int h2o_part_flags(const void* codes, int code_bytes, long long rs, long long fs
   if (n_work <= 0) return 0;
   if (code_bytes == 1)
     hipLaunchKernelGGL(part_flags_kernel<uint8_t>, dim3(n_work), dim3(256), 0, s, (const uint8_t*)codes, rs, fs,
-                       ridx, (const int4*)work, fbase, feat, masks, Bs, flags, cnt);
+                       ridx, (const int4*)work, fbase, feat, masks, Bs, flags, cnt, nullptr);
   else
     hipLaunchKernelGGL(part_flags_kernel<uint16_t>, dim3(n_work), dim3(256), 0, s, (const uint16_t*)codes, rs, fs,
-                       ridx, (const int4*)work, fbase, feat, masks, Bs, flags, cnt);
+                       ridx, (const int4*)work, fbase, feat, masks, Bs, flags, cnt, nullptr);
   return (int)hipGetLastError();
 }
 
@@ -1415,10 +1422,10 @@ int h2o_part_compact(const int* ridx, const int* work, const int* fbase, int n_w
   static const int cu = [] { const char* e = getenv("H2O3_PART_U"); return e ? atoi(e) : 4; }();
   if (cu == 1)
     hipLaunchKernelGGL(part_compact_kernel<1>, dim3(n_work), dim3(256), 0, s, ridx, (const int4*)work, fbase, flags,
-                       loff, roff, out, pa, pa_out);
+                       loff, roff, out, pa, pa_out, nullptr);
   else
     hipLaunchKernelGGL(part_compact_kernel<4>, dim3(n_work), dim3(256), 0, s, ridx, (const int4*)work, fbase, flags,
-                       loff, roff, out, pa, pa_out);
+                       loff, roff, out, pa, pa_out, nullptr);
   return (int)hipGetLastError();
 }
 
@@ -1546,7 +1553,7 @@ extern "C" int h2o_seg_sum2(const int* ridx, const float* a, const float* b, con
 
 extern "C" int h2o_leaf_pos(const float* zp, const int* work, int n_work, int mode, double* out, hipStream_t s) {
   if (n_work <= 0) return 0;
-  hipLaunchKernelGGL(leaf_pos_kernel, dim3(n_work), dim3(256), 0, s, zp, (const int4*)work, mode, out);
+  hipLaunchKernelGGL(leaf_pos_kernel, dim3(n_work), dim3(256), 0, s, zp, (const int4*)work, mode, out, nullptr);
   return (int)hipGetLastError();
 }
 
@@ -1561,7 +1568,7 @@ extern "C" int h2o_col_sample(int n, int m, const long long* elig, int k, unsign
 extern "C" int h2o_leaf_scatter(const int* ridx, const int* work, int n_work, const float* val, float* d,
                                 hipStream_t s) {
   if (n_work <= 0) return 0;
-  hipLaunchKernelGGL(leaf_scatter_kernel, dim3(n_work), dim3(256), 0, s, ridx, (const int4*)work, val, d);
+  hipLaunchKernelGGL(leaf_scatter_kernel, dim3(n_work), dim3(256), 0, s, ridx, (const int4*)work, val, d, nullptr);
   return (int)hipGetLastError();
 }
 
@@ -1956,3 +1963,332 @@ extern "C" int h2o_part_items(const long long* seg, int n, int chunk, int nw, in
   hipLaunchKernelGGL(part_items_kernel, dim3(blocks), dim3(256), 0, s, seg, n, chunk, nw, (int4*)work, meta, fbase);
   return (int)hipGetLastError();
 }
+
+// ===========================================================================
+// Device-resident tree level loop (models/tree/devtree.py).
+//
+// Reference: hex/tree/SharedTree.java:481-516 (scoreAndBuildTrees: one
+// buildLayer per level, DTree.DecidedNode per split node), GBM.java:464.
+//
+// A whole tree runs as a fixed kernel sequence with NO host round trip: the
+// frontier of level d is a heap of 2^d slots (slot i's children are slots 2i
+// and 2i+1 of level d+1; absent nodes have count 0), and every per-level work
+// list (histogram chunks of the lighter children, partition chunks, leaf
+// chunks) is built on the device by dt_items_kernel from the level's split
+// records, with launch grids sized to fixed capacities and early-exiting
+// workgroups.  The sequence is therefore static -- the host captures it once
+// as a hipGraph and replays it per tree -- and the tree comes back as ONE
+// [2^(D+1)-1][DT_RS] f64 record read once per tree.
+// ===========================================================================
+#define DT_RS 16
+enum {
+  DT_GAIN = 0, DT_FEAT = 1, DT_T = 2, DT_OPT = 3, DT_L0 = 4, DT_L1 = 5, DT_R0 = 6, DT_R1 = 7, DT_T0 = 8, DT_T1 = 9,
+  DT_OK = 10, DT_NL = 11, DT_NAW = 12, DT_ST = 13, DT_CT = 14, DT_VAL = 15
+};
+#define DT_MAXN 4096
+
+// Segment of slot i for the three work-list kinds:
+//   kind 0 (level): the slot's own rows (partition, root histogram);
+//   kind 1 (child): the lighter child of a splitting parent slot (by the
+//                   weight channel wch of the record's L / R sums; ties left);
+//   kind 2 (leaf) : heap node i when it is a leaf (count > 0 and level == D or
+//                   no split); i is a heap index into the whole record.
+__device__ __forceinline__ void dt_seg(int kind, const double* __restrict__ rec, int i, int D, int wch,
+                                       long long& start, long long& cnt) {
+  const double* r = rec + (size_t)i * DT_RS;
+  start = 0;
+  cnt = 0;
+  const long long st = (long long)r[DT_ST], ct = (long long)r[DT_CT];
+  if (kind == 0) {
+    start = st; cnt = ct;
+  } else if (kind == 1) {
+    if (r[DT_OK] > 0.0) {
+      const long long nl = (long long)r[DT_NL];
+      const bool bl = r[DT_L0 + wch] <= r[DT_R0 + wch];
+      cnt = bl ? nl : ct - nl;
+      start = bl ? st : st + nl;
+    }
+  } else {
+    const int lv = 31 - __clz(i + 1);
+    if (ct > 0 && (lv == D || !(r[DT_OK] > 0.0))) { start = st; cnt = ct; }
+  }
+}
+
+// One workgroup: per-slot chunk counts scanned into item bases (LDS), then all
+// threads write the items (slot found by binary search over the bases).
+// work[it] = (slot, start, count, k); fbase[it] (optional) = the item's first
+// ballot word (partition flags: the slot's words are contiguous, chunk % 64 == 0).
+// counts[1] = #items (<= cap).
+__global__ __launch_bounds__(1024) void dt_items_kernel(int kind, const double* __restrict__ rec, int n, int D,
+                                                        int wch, int chunk, int cap, int4* __restrict__ work,
+                                                        int* __restrict__ fbase, int* __restrict__ counts) {
+  __shared__ int sb[DT_MAXN + 1];
+  __shared__ int wb[DT_MAXN + 1];
+  __shared__ long long wtot[2][16];
+  __shared__ long long carry[2];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+  if (threadIdx.x == 0) carry[0] = carry[1] = 0;
+  __syncthreads();
+  for (int base = 0; base < n; base += blockDim.x) {
+    const int i = base + threadIdx.x;
+    long long start = 0, cnt = 0;
+    if (i < n) dt_seg(kind, rec, i, D, wch, start, cnt);
+    const long long nch = cnt > 0 ? (cnt + chunk - 1) / chunk : 0;
+    const long long nwd = cnt > 0 ? (cnt + 63) / 64 : 0;
+    long long a = nch, b = nwd;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const long long ta = __shfl_up(a, o, 64), tb = __shfl_up(b, o, 64);
+      if (lane >= o) { a += ta; b += tb; }
+    }
+    if (lane == 63) { wtot[0][wv] = a; wtot[1][wv] = b; }
+    __syncthreads();
+    if (wv == 0) {
+      long long x = lane < nwv ? wtot[0][lane] : 0, y = lane < nwv ? wtot[1][lane] : 0;
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        const long long tx = __shfl_up(x, o, 64), ty = __shfl_up(y, o, 64);
+        if (lane >= o) { x += tx; y += ty; }
+      }
+      if (lane < nwv) { wtot[0][lane] = x; wtot[1][lane] = y; }
+    }
+    __syncthreads();
+    if (i < n) {
+      sb[i] = (int)(carry[0] + (wv > 0 ? wtot[0][wv - 1] : 0) + a - nch);
+      wb[i] = (int)(carry[1] + (wv > 0 ? wtot[1][wv - 1] : 0) + b - nwd);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) { carry[0] += wtot[0][nwv - 1]; carry[1] += wtot[1][nwv - 1]; }
+    __syncthreads();
+  }
+  const int total = (int)min(carry[0], (long long)cap);
+  for (int it = threadIdx.x; it < total; it += blockDim.x) {
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {                       // last slot whose base is <= it (empty slots precede it)
+      const int mid = (lo + hi + 1) >> 1;
+      if (sb[mid] <= it) lo = mid; else hi = mid - 1;
+    }
+    long long start, cnt;
+    dt_seg(kind, rec, lo, D, wch, start, cnt);
+    const int k = it - sb[lo];
+    const long long p = start + (long long)k * chunk;
+    work[it] = make_int4(lo, (int)p, (int)min((long long)chunk, cnt - (long long)k * chunk), k);
+    if (fbase != nullptr) fbase[it] = wb[lo] + k * (chunk / 64);
+  }
+  if (threadIdx.x == 0) { counts[0] = n; counts[1] = total; }
+}
+
+// Compaction offsets of the level partition (one workgroup; items of a slot
+// are consecutive, item k of a slot starts k * chunk rows into it): global
+// exclusive scan of the per-item left counts, per-slot left totals into the
+// record (DT_NL), loff / roff per item, and the NEXT level's segments
+// (children 2i, 2i+1 of a splitting slot; count 0 otherwise) into rec_next.
+__global__ __launch_bounds__(1024) void dt_offsets_kernel(const int* __restrict__ cnt, const int4* __restrict__ work,
+                                                          const int* __restrict__ counts, double* __restrict__ rec,
+                                                          int n, double* __restrict__ rec_next,
+                                                          int* __restrict__ loff, int* __restrict__ roff) {
+  __shared__ long long nl_s[DT_MAXN];
+  __shared__ long long wtot[16];
+  __shared__ long long carry;
+  const int nw = counts[1];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+  for (int s = threadIdx.x; s < n; s += blockDim.x) nl_s[s] = 0;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (int base = 0; base < nw; base += blockDim.x) {
+    const int i = base + threadIdx.x;
+    const long long v = i < nw ? (long long)cnt[i] : 0;
+    long long x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const long long t = __shfl_up(x, o, 64);
+      if (lane >= o) x += t;
+    }
+    if (lane == 63) wtot[wv] = x;
+    __syncthreads();
+    if (wv == 0) {
+      long long w = lane < nwv ? wtot[lane] : 0;
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        const long long t = __shfl_up(w, o, 64);
+        if (lane >= o) w += t;
+      }
+      if (lane < nwv) wtot[lane] = w;
+    }
+    __syncthreads();
+    if (i < nw) loff[i] = (int)(carry + (wv > 0 ? wtot[wv - 1] : 0) + x - v);
+    __syncthreads();
+    if (threadIdx.x == 0) carry += wtot[nwv - 1];
+    __syncthreads();
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < nw; i += blockDim.x) {
+    const int4 wk = work[i];
+    if (i == nw - 1 || work[i + 1].x != wk.x) nl_s[wk.x] = (long long)loff[i] + cnt[i] - (long long)loff[i - wk.w];
+  }
+  for (int i = threadIdx.x; i < nw; i += blockDim.x) roff[i] = loff[i - work[i].w];
+  __syncthreads();
+  for (int i = threadIdx.x; i < nw; i += blockDim.x) {
+    const int4 wk = work[i];
+    const long long st = (long long)rec[(size_t)wk.x * DT_RS + DT_ST];
+    const long long lpre = (long long)loff[i] - (long long)roff[i];
+    loff[i] = (int)(st + lpre);
+    roff[i] = (int)(st + nl_s[wk.x] + ((long long)wk.y - st) - lpre);
+  }
+  for (int s = threadIdx.x; s < n; s += blockDim.x) {
+    double* r = rec + (size_t)s * DT_RS;
+    const long long nl = nl_s[s];
+    r[DT_NL] = (double)nl;
+    if (rec_next != nullptr) {
+      double* c = rec_next + (size_t)(2 * s) * DT_RS;
+      const bool ok = r[DT_OK] > 0.0;
+      const double st = r[DT_ST], ct = r[DT_CT];
+      c[DT_ST] = ok ? st : 0.0;
+      c[DT_CT] = ok ? (double)nl : 0.0;
+      c[DT_RS + DT_ST] = ok ? st + (double)nl : 0.0;
+      c[DT_RS + DT_CT] = ok ? ct - (double)nl : 0.0;
+    }
+  }
+}
+
+// Level histograms by subtraction in heap layout: parent slot i's built
+// (lighter) child histogram Hb[f][i] goes to slot 2i + !left, the sibling
+// Hp[f][i] - Hb[f][i] to the other; a non-splitting parent writes zeros to
+// both (absent nodes).  grid (np, Fl), one block per (parent, feature).
+__global__ __launch_bounds__(256) void dt_sibling_kernel(const double* __restrict__ Hb, const double* __restrict__ Hp,
+                                                         const double* __restrict__ rec_par, int np, int BsC, int C,
+                                                         int clamp_mask, int wch, double* __restrict__ H,
+                                                         const double* __restrict__ wyy_b,
+                                                         const double* __restrict__ wyy_p,
+                                                         double* __restrict__ wyy_out) {
+  const int i = blockIdx.x, f = blockIdx.y;
+  const double* r = rec_par + (size_t)i * DT_RS;
+  const bool ok = r[DT_OK] > 0.0;
+  const bool bl = r[DT_L0 + wch] <= r[DT_R0 + wch];
+  const int bs = 2 * i + (bl ? 0 : 1), ds = 2 * i + (bl ? 1 : 0);
+  const double* hb = Hb + ((size_t)f * np + i) * BsC;
+  const double* hp = Hp + ((size_t)f * np + i) * BsC;
+  double* ob = H + ((size_t)f * 2 * np + bs) * BsC;
+  double* od = H + ((size_t)f * 2 * np + ds) * BsC;
+  for (int k = threadIdx.x; k < BsC; k += blockDim.x) {
+    double b = 0.0, d = 0.0;
+    if (ok) {
+      b = hb[k];
+      d = hp[k] - b;
+      if ((clamp_mask >> (k % C)) & 1) d = fmax(d, 0.0);
+    }
+    ob[k] = b;
+    od[k] = d;
+  }
+  if (wyy_out != nullptr && f == 0 && threadIdx.x == 0) {
+    wyy_out[bs] = ok ? wyy_b[i] : 0.0;
+    wyy_out[ds] = ok ? wyy_p[i] - wyy_b[i] : 0.0;
+  }
+}
+
+// Leaf values from the (all-reduced) leaf sums: v = s0 / s1 (0 if s1 == 0),
+// clamped to +-maxabs, times the learning rate (device scalar, so a captured
+// graph serves every tree).  Existence is global: a node exists when its
+// parent split (the record's ok is merged across ranks), so every rank writes
+// every leaf's value even when it holds none of the leaf's rows.
+__global__ __launch_bounds__(256) void dt_leaf_vals_kernel(double* __restrict__ rec, const double* __restrict__ sums,
+                                                           int nh, int D, const float* __restrict__ lr, double maxabs,
+                                                           float* __restrict__ vals) {
+  const int h = blockIdx.x * blockDim.x + threadIdx.x;
+  if (h >= nh) return;
+  const int lv = 31 - __clz(h + 1);
+  const bool exists = h == 0 || rec[(size_t)((h - 1) >> 1) * DT_RS + DT_OK] > 0.0;
+  const bool leaf = exists && (lv == D || !(rec[(size_t)h * DT_RS + DT_OK] > 0.0));
+  double v = 0.0;
+  if (leaf) {
+    const double den = sums[2 * h + 1];
+    v = den != 0.0 ? sums[2 * h] / den : 0.0;
+    v = fmin(fmax(v, -maxabs), maxabs) * (double)lr[0];
+  }
+  vals[h] = (float)v;
+  rec[(size_t)h * DT_RS + DT_VAL] = v;
+}
+
+// Root record: segment [0, N), everything else zero (the record is re-zeroed
+// per tree by the caller's memset).
+__global__ void dt_root_kernel(double* __restrict__ rec, long long N) {
+  if (threadIdx.x == 0) { rec[DT_ST] = 0.0; rec[DT_CT] = (double)N; }
+}
+
+extern "C" {
+
+int h2o_dt_items(int kind, const double* rec, int n, int D, int wch, int chunk, int cap, int* work, int* fbase,
+                 int* counts, hipStream_t s) {
+  if (n <= 0 || n > DT_MAXN || chunk <= 0 || (fbase != nullptr && chunk % 64 != 0)) return -1;
+  hipLaunchKernelGGL(dt_items_kernel, dim3(1), dim3(1024), 0, s, kind, rec, n, D, wch, chunk, cap, (int4*)work, fbase,
+                     counts);
+  return (int)hipGetLastError();
+}
+
+int h2o_dt_offsets(const int* cnt, const int* work, const int* counts, double* rec, int n, double* rec_next, int* loff,
+                   int* roff, hipStream_t s) {
+  if (n <= 0 || n > DT_MAXN) return -1;
+  hipLaunchKernelGGL(dt_offsets_kernel, dim3(1), dim3(1024), 0, s, cnt, (const int4*)work, counts, rec, n, rec_next,
+                     loff, roff);
+  return (int)hipGetLastError();
+}
+
+int h2o_dt_sibling(const double* Hb, const double* Hp, const double* rec_par, int np, int F, int BsC, int C,
+                   int clamp_mask, int wch, double* H, const double* wyy_b, const double* wyy_p, double* wyy_out,
+                   hipStream_t s) {
+  if (np <= 0 || F <= 0) return 0;
+  hipLaunchKernelGGL(dt_sibling_kernel, dim3(np, F), dim3(256), 0, s, Hb, Hp, rec_par, np, BsC, C, clamp_mask, wch, H,
+                     wyy_b, wyy_p, wyy_out);
+  return (int)hipGetLastError();
+}
+
+int h2o_dt_leaf_vals(double* rec, const double* sums, int nh, int D, const float* lr, double maxabs, float* vals,
+                     hipStream_t s) {
+  hipLaunchKernelGGL(dt_leaf_vals_kernel, dim3((nh + 255) / 256), dim3(256), 0, s, rec, sums, nh, D, lr, maxabs, vals);
+  return (int)hipGetLastError();
+}
+
+int h2o_dt_root(double* rec, long long N, hipStream_t s) {
+  hipLaunchKernelGGL(dt_root_kernel, dim3(1), dim3(64), 0, s, rec, N);
+  return (int)hipGetLastError();
+}
+
+// The partition / leaf kernels with the item count read on the device
+// (counts[1]); n_cap = launch capacity.
+int h2o_part_flags_dev(const void* codes, int code_bytes, long long rs, long long fs, const int* ridx, const int* work,
+                       const int* fbase, int n_cap, const int* feat, const uint8_t* masks, int Bs,
+                       unsigned long long* flags, int* cnt, const int* counts, hipStream_t s) {
+  if (n_cap <= 0) return 0;
+  if (code_bytes == 1)
+    hipLaunchKernelGGL(part_flags_kernel<uint8_t>, dim3(n_cap), dim3(256), 0, s, (const uint8_t*)codes, rs, fs, ridx,
+                       (const int4*)work, fbase, feat, masks, Bs, flags, cnt, counts);
+  else
+    hipLaunchKernelGGL(part_flags_kernel<uint16_t>, dim3(n_cap), dim3(256), 0, s, (const uint16_t*)codes, rs, fs,
+                       ridx, (const int4*)work, fbase, feat, masks, Bs, flags, cnt, counts);
+  return (int)hipGetLastError();
+}
+
+int h2o_part_compact_dev(const int* ridx, const int* work, const int* fbase, int n_cap,
+                         const unsigned long long* flags, const int* loff, const int* roff, int* out, const float* pa,
+                         float* pa_out, const int* counts, hipStream_t s) {
+  if (n_cap <= 0) return 0;
+  hipLaunchKernelGGL(part_compact_kernel<4>, dim3(n_cap), dim3(256), 0, s, ridx, (const int4*)work, fbase, flags, loff,
+                     roff, out, pa, pa_out, counts);
+  return (int)hipGetLastError();
+}
+
+int h2o_leaf_pos_dev(const float* zp, const int* work, int n_cap, int mode, double* out, const int* counts,
+                     hipStream_t s) {
+  if (n_cap <= 0) return 0;
+  hipLaunchKernelGGL(leaf_pos_kernel, dim3(n_cap), dim3(256), 0, s, zp, (const int4*)work, mode, out, counts);
+  return (int)hipGetLastError();
+}
+
+int h2o_leaf_scatter_dev(const int* ridx, const int* work, int n_cap, const float* val, float* d, const int* counts,
+                         hipStream_t s) {
+  if (n_cap <= 0) return 0;
+  hipLaunchKernelGGL(leaf_scatter_kernel, dim3(n_cap), dim3(256), 0, s, ridx, (const int4*)work, val, d, counts);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -301,6 +301,10 @@ __global__ __launch_bounds__(64) void split_select2_kernel(const SplitRec* __res
     o[0] = best; o[1] = (double)(bf + f0); o[2] = (double)r.t; o[3] = (double)r.opt;
     o[4] = r.lw; o[5] = r.ly; o[6] = t0 - r.lw; o[7] = t1 - r.ly; o[8] = t0; o[9] = t1;
     o[10] = ok ? 1.0 : 0.0;
+    // field 12 (stride > 12): the node's NA weight on the chosen feature; 0 =
+    // no NA reached this node, so NAs of later data follow the heavier child
+    // (DTree.java:1475-1478 decides this per node)
+    if (stride > 12) o[12] = H[(((size_t)bf * n + node) * Bs + (Bs - 1)) * 2];
     feat_out[node] = ok ? bf + f0 : 0;
   }
   const int B = Bs - 1;
@@ -766,6 +770,7 @@ __global__ __launch_bounds__(256) void pair_select_kernel(const double* __restri
     o[0] = bg; o[1] = (double)f; o[2] = (double)t; o[3] = (double)opt;
     o[4] = L0; o[5] = L1; o[6] = v[2] - L0; o[7] = v[3] - L1; o[8] = v[2]; o[9] = v[3];
     o[10] = ok ? 1.0 : 0.0;
+    if (stride > 12) o[12] = na0;   // the node's NA weight on the winner (per-node NA direction)
     feat_out[node] = ok ? f : 0;
   }
   if (!ok) {

@@ -51,8 +51,20 @@ from . import spmd
 # cloud status while a build holds the executor
 # GETs served on the HTTP thread while a build runs (collectives refused:
 # collectives.forbid; a read that needs one is queued as usual)
-_READ_PREFIXES = ("/3/Frames", "/3/Models", "/99/Models", "/99/Leaderboards", "/99/AutoML", "/3/ModelBuilders",
-                  "/99/Grids", "/3/Grids", "/3/ModelMetrics", "/3/DKV", "/99/Rapids/help")
+# GET routes served on the HTTP thread while a build runs (exact route
+# templates, no prefixes): pure reads of finished DKV objects and listings.
+# Export / download / binary-model / scoring routes are NOT here -- they write
+# files, serialise whole models or score, so they queue behind the build.
+_READ_ROUTES = frozenset((
+    "/3/Frames", "/3/Frames/{fid}", "/3/Frames/{fid}/light", "/3/Frames/{fid}/summary",
+    "/3/Frames/{fid}/columns", "/3/Frames/{fid}/columns/{col}", "/3/Frames/{fid}/columns/{col}/domain",
+    "/3/Frames/{fid}/columns/{col}/summary",
+    "/3/Models", "/3/Models/{mid}", "/99/Models/{mid}", "/99/Models/{mid}/json",
+    "/3/ModelBuilders", "/3/ModelBuilders/{algo}",
+    "/99/Leaderboards", "/99/Leaderboards/{project}", "/99/AutoML/{project}",
+    "/99/Grids", "/99/Grids/{gid}",
+    "/3/ModelMetrics", "/3/ModelMetrics/models/{mid}", "/3/ModelMetrics/frames/{fid}",
+    "/99/Rapids/help"))
 # builds accepted while another build runs: CREATED job at once, run later
 _BUILD_ROUTES = {"/3/ModelBuilders/{algo}": "model", "/99/Grid/{algo}": "grid", "/99/AutoMLBuilder": "automl"}
 
@@ -368,7 +380,7 @@ def create_app(flow_dir: str | None = None, serve: bool = True) -> FastAPI:
                             NotImplementedError) as e:
                         raise _HTTPError(400 if not isinstance(e, KeyError) else 404, str(e), e)
                     return _to_response(out)
-                if method == "GET" and path.startswith(_READ_PREFIXES) and executor is not None and \
+                if method == "GET" and path in _READ_ROUTES and executor is not None and \
                         cloud.is_distributed() and executor.busy():
                     # a read while a build runs: on this thread, no collectives
                     from ..parallel import collectives as _coll
@@ -1253,7 +1265,7 @@ def create_app(flow_dir: str | None = None, serve: bool = True) -> FastAPI:
             ids.sort(key=lambda k: (math.isnan(vals[k]), -vals[k] if dec else vals[k]))
         return {"__meta": S.meta("GridSchemaV99", "Grid", 99), "grid_id": S.key(gid, "Grid"),
                 "model_ids": [S.key(m, "Model") for m in ids],
-                "failed_params": [], "failure_details": [e for _, e in g.failed_params],
+                "failed_params": [], "failure_details": list(g.failure_details),
                 "failure_stack_traces": [], "failed_raw_params": [],
                 "hyper_names": list(getattr(g, "hyper_params", {}) or {}),
                 "summary_table": S.twodim_from_df("Hyper-Parameter Search Summary", tab),

@@ -337,6 +337,44 @@ def test_glm_conditioning_tiers_match_fp64(monkeypatch, noise, tier):
         assert err["f32"] > 100 * err["default"] and err["bf3_rhs"] > 100 * err["default"], err
 
 
+def test_glm_gaussian_reduced_tier_refines_to_fp64(monkeypatch):
+    """Gaussian / identity on the one-MFMA bf16 Hessian tier: the one-step
+    convergence shortcut only holds for an exact Hessian, so the driver keeps
+    stepping on the exact-gradient channel until the coefficients are those of
+    the fp64 least-squares solution (the bf16 step alone is ~kappa * 2^-8 off)."""
+    import numpy as np
+    from h2o3_amd.models.base import TrainSpec
+    from h2o3_amd.core.frame import H2OFrame
+    from h2o3_amd.models.glm.glm import GLMDriver, H2OGeneralizedLinearEstimator
+    for k, v in _DEFAULT.items():
+        monkeypatch.setenv(k, v)
+    g = np.random.default_rng(11)
+    n, P = 300_000, 100
+    Xh = g.standard_normal((n, P)).astype(np.float32)
+    b = g.standard_normal(P)
+    y = Xh.astype(np.float64) @ b + 0.3 * g.standard_normal(n)
+    cols = {f"x{j}": Xh[:, j] for j in range(P)}
+    cols["y"] = y
+    fr = H2OFrame(cols)
+    est = H2OGeneralizedLinearEstimator(family="gaussian", solver="IRLSM", lambda_=0.0)
+    spec = TrainSpec(fr, [f"x{j}" for j in range(P)], "y")
+    est._spec = spec
+    drv = GLMDriver(est, spec)
+    assert drv.X.is_cuda
+    for _ in range(30):
+        drv.step()
+        if drv.converged:
+            break
+    assert drv.converged
+    assert drv._hprec == "bf16", drv._hprec
+    assert drv.iter > 1
+    Xa = torch.cat([drv.X[:, :P].double(), torch.ones(n, 1, dtype=torch.float64, device=drv.X.device)], 1)
+    yd = drv.y.double().view(-1, 1)
+    ref = torch.linalg.lstsq(Xa.cpu(), yd.cpu()).solution.view(-1).numpy()
+    err = np.abs(drv.beta - ref).max() / np.abs(ref).max()
+    assert err < 1e-6, err
+
+
 @pytest.mark.parametrize("noise,tier", [(None, "bf16"), (0.1, "bf3"), (2e-2, "f64")])
 def test_glm_wide_tiers_match_fp64(monkeypatch, noise, tier):
     """Wide design (P = 600: the fused wide pass -- eta kernel + hand-written
