@@ -144,6 +144,13 @@ def tree_contributions(model, frame, top_n=None, bottom_n=None, compare_abs=Fals
     trees = [t for t, k in zip(model._forest.trees, model._forest.tclass) if k == 0]
     if model.algo == "drf":
         phi = forest_contributions(trees, X, len(names), scale=1.0 / max(1, len(trees)))
+        if spec.nclasses == 2:
+            # the reference's binomial DRF form (ScoreContributionsTaskDRF,
+            # DRFModel.java:97-106: its trees score P(class 0)): 1/(F+1) -
+            # contribution to P0 per column, which still sums to P(class 1)
+            r = 1.0 / (len(names) + 1)
+            phi[:, :-1] += r
+            phi[:, -1] += r - 1.0
     else:
         phi = forest_contributions(trees, X, len(names))
         phi[:, -1] += float(model._init_f[0])

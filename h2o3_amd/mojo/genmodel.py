@@ -77,6 +77,8 @@ class MojoModel:
                 k, v = line.split("=", 1)
                 self.info[k.strip()] = v.strip()
         self.algo = self.meta["algo"]
+        self.details = json.loads(self._z.read("experimental/modelDetails.json")) \
+            if "experimental/modelDetails.json" in self._z.namelist() else None
         self._arr = {}
         for n in self._z.namelist():
             if n.startswith("arrays/") and n.endswith(".npy"):
@@ -262,6 +264,59 @@ class MojoModel:
                 nd = np.where(act, np.where(go, l, right[nd]), nd)
             out[ar, tcls[t]] += val[nd]
         return out
+
+    # ------------------------------------------------------------ contributions
+    def _node_left(self, j, X):
+        """Split decision of packed node j for every row of X (the scoring
+        walk's rule: f32 thresholds, categorical level bitsets, NA direction)."""
+        A = self._arr
+        x = X[:, int(A["forest_feat"][j])]
+        isn = np.isnan(x)
+        nal = A["forest_na_left"][j] != 0
+        co = int(A["forest_cat_off"][j])
+        if co >= 0:
+            code = np.where(isn, -1, np.nan_to_num(x, nan=-1)).astype(np.int64)
+            inr = (code >= 0) & (code < A["forest_cat_len"][j])
+            bits = A["forest_cat_bits"]
+            bit = bits[np.clip(co + np.maximum(code, 0), 0, len(bits) - 1)] != 0
+            return np.where(isn | ~inr, nal, bit)
+        return np.where(isn, nal, x.astype(np.float32) < np.float32(A["forest_thr"][j]))
+
+    def predict_contributions(self, df, output_format="Original", top_n=None, bottom_n=None, compare_abs=False):
+        """TreeSHAP feature contributions of a GBM / DRF / XGBoost MOJO (the
+        reference's EasyPredictModelWrapper.predictContributions /
+        PredictContributions): one column per feature plus BiasTerm, in link
+        space (GBM / XGBoost: the row sum is the raw margin incl. init_f; DRF
+        binomial: the reference's 1/(F+1) - contribution(P(class 0)) form,
+        summing to P(class 1))."""
+        from .treeshap_np import contributions_frame, tree_shap
+        m = self.meta
+        if self.algo not in ("gbm", "drf", "xgboost"):
+            raise ValueError(f"contributions are not available for a {self.algo} MOJO")
+        if self.nclasses > 2:
+            raise ValueError("Calculating contributions is currently not supported for multinomial models.")
+        A = self._arr
+        if "forest_weight" not in A:
+            raise ValueError("this MOJO carries no node weights (written before contributions were supported)")
+        if m.get("catenc") and not getattr(df, "_catenc_done", False):
+            df = encode_df(df, m["catenc"])
+        X = self._tree_matrix(df)
+        n, F = X.shape
+        roots, tcls = A["forest_roots"], A["forest_tclass"]
+        left, right, val, cov, feat = A["forest_left"], A["forest_right"], A["forest_value"], \
+            A["forest_weight"], A["forest_feat"]
+        phi = np.zeros((n, F + 1))
+        trees = [t for t in range(len(roots)) if tcls[t] == 0]
+        scale = 1.0 / max(1, len(trees)) if self.algo == "drf" else 1.0
+        for t in trees:
+            tree_shap(left, right, cov, val, feat, lambda j: self._node_left(j, X), n, phi, scale=scale,
+                      root=int(roots[t]))
+        if self.algo in ("gbm", "xgboost"):
+            phi[:, -1] += float(np.asarray(m["init_f"]).reshape(-1)[0])
+        elif self.nclasses == 2:
+            phi[:, :-1] += 1.0 / (F + 1)
+            phi[:, -1] += 1.0 / (F + 1) - 1.0
+        return contributions_frame(phi, list(m["x"]), top_n=top_n, bottom_n=bottom_n, compare_abs=compare_abs)
 
     def predict_raw(self, df):
         m = self.meta
@@ -716,13 +771,26 @@ class MojoModel:
 
 
 class EasyPredictModelWrapper:
-    """h2o-genmodel's convenience wrapper (predictBinomial / predictRegression...)."""
+    """h2o-genmodel's convenience wrapper (predictBinomial / predictRegression...).
+    enable_contributions=True adds the row's TreeSHAP contributions to each
+    prediction (EasyPredictModelWrapper.Config.setEnableContributions,
+    EasyPredictModelWrapper.java:196); works with either MOJO layout."""
 
-    def __init__(self, model: MojoModel):
+    def __init__(self, model, enable_contributions=False):
         self.m = model
+        self.enable_contributions = bool(enable_contributions)
 
     def predict(self, row: dict):
-        return self.m.predict_row(row)
+        out = self.m.predict_row(row)
+        if self.enable_contributions:
+            out["contributions"] = self.predict_contributions(row)
+        return out
+
+    def predict_contributions(self, row: dict):
+        """{feature: contribution, ..., "BiasTerm": bias} of one row."""
+        import pandas as pd
+        df = self.m.predict_contributions(pd.DataFrame([row]))
+        return {k: float(v) for k, v in df.iloc[0].items()}
 
 
 def load(path):

@@ -143,12 +143,17 @@ def is_h2o_layout(src) -> bool:
 
 
 # --------------------------------------------------------------- tree decode
+# AuxInfo record of trees/tXX_YYY_aux.bin (SharedTreeMojoModel.AuxInfo: 10 x 4 bytes)
+_AUX_DT = np.dtype([("nid", "<i4"), ("res", "<i4"), ("wl", "<f4"), ("wr", "<f4"), ("pl", "<f4"), ("pr", "<f4"),
+                    ("sel", "<f4"), ("ser", "<f4"), ("l", "<i4"), ("r", "<i4")])
+
+
 class _Tree:
     """One compressed tree decoded into flat node arrays.  Children are node
     indices (>= 0) or leaves encoded as -(leaf_index + 1)."""
 
     __slots__ = ("col", "kind", "split", "na_left", "bs_off", "bs_n", "bs_pos", "left", "right", "leaf", "raw",
-                 "root_leaf")
+                 "root_leaf", "_nid")
 
     def __init__(self, buf: bytes, version: float):
         self.raw = np.frombuffer(buf, dtype=np.uint8)
@@ -241,6 +246,66 @@ class _Tree:
         self.right = np.asarray(right, dtype=np.int64)
         self.leaf = np.asarray(leaf, dtype=np.float32).astype(np.float64)
 
+    def node_right(self, j, X, dom_len, version):
+        """The scoring rule of score() for one split node j over every row."""
+        c = self.col[j]
+        d = X[:, c]
+        nan = np.isnan(d)
+        di = np.where(nan, 0, d).astype(np.int64)
+        kind = self.kind[j]
+        right = np.zeros(d.shape[0], dtype=bool)
+        if kind == 0:
+            right = d >= self.split[j]
+        elif kind == 1:
+            rel = di - self.bs_off[j]
+            inr = (rel >= 0) & (rel < self.bs_n[j])
+            relc = np.clip(rel, 0, None)
+            byte = self.raw[np.minimum(self.bs_pos[j] + (relc >> 3), self.raw.size - 1)]
+            right = ((byte >> (relc & 7)) & 1).astype(bool) & inr
+            if version >= 1.1:
+                nan = nan | ~inr
+        if version >= 1.2 and dom_len is not None:
+            dl = dom_len[c]
+            nan = nan | ((dl > 0) & (di >= dl) & ~np.isnan(d))
+        return np.where(nan, ~self.na_left[j], right)
+
+    def shap_graph(self, aux: bytes):
+        """Flat node arrays for TreeSHAP: split nodes keep their ids, leaf i
+        becomes node I + i; covers from the tree's _aux.bin records (AuxInfo:
+        nid, child weights, child node ids -- SharedTreeMojoModel.AuxInfo;
+        the root is node id 0, children are found by the records' nidL / nidR
+        as SharedTreeMojoModel.computeTreeGraph does)."""
+        I, L = len(self.col), len(self.leaf)
+        lt = lambda a: np.where(a >= 0, a, I + (-a - 1))   # noqa: E731
+        left = np.full(I + L, -1, dtype=np.int64)
+        right = np.full(I + L, -1, dtype=np.int64)
+        left[:I], right[:I] = lt(self.left), lt(self.right)
+        value = np.zeros(I + L)
+        value[I:] = self.leaf
+        feat = np.zeros(I + L, dtype=np.int64)
+        feat[:I] = self.col
+        cover = np.zeros(I + L)
+        nid = np.zeros(I + L, dtype=np.int64)
+        rec = np.frombuffer(aux, dtype=_AUX_DT) if aux else np.zeros(0, dtype=_AUX_DT)
+        by_nid = {int(r["nid"]): r for r in rec}
+        if I:
+            r0 = by_nid[0]
+            cover[0] = float(r0["wl"]) + float(r0["wr"])
+            stack = [(0, 0)]
+            while stack:
+                j, nd = stack.pop()
+                nid[j] = nd
+                r = by_nid[nd]
+                cover[left[j]] = float(r["wl"])
+                cover[right[j]] = float(r["wr"])
+                nid[left[j]], nid[right[j]] = int(r["l"]), int(r["r"])
+                if self.left[j] >= 0:
+                    stack.append((int(self.left[j]), int(r["l"])))
+                if self.right[j] >= 0:
+                    stack.append((int(self.right[j]), int(r["r"])))
+        self._nid = nid
+        return left, right, cover, value, feat
+
     def score(self, X: np.ndarray, dom_len: np.ndarray | None, version: float, paths: list | None = None) -> np.ndarray:
         """Leaf value per row of X [n, ncols] (category indices for enums).
         paths: optional list of n strings, extended in place with the row's
@@ -327,6 +392,12 @@ class H2OMojoModel:
         if loader is None:
             raise NotImplementedError(f"reference MOJO algo '{self.algo}' is not supported by this reader")
         loader()
+        # the original model's ModelSchemaV3 JSON (ModelMojoWriter.writeModelDetails;
+        # read by hex.genmodel.attributes.ModelJsonReader)
+        self.details = None
+        if self.be.exists("experimental/modelDetails.json"):
+            import json
+            self.details = json.loads(self.be.read("experimental/modelDetails.json").decode("utf-8"))
 
     # ------------------------------------------------------------ ini parse
     def _parse_ini(self):
@@ -1663,6 +1734,44 @@ class H2OMojoModel:
         return [list(r) for r in zip(*out)]
 
     # ------------------------------------------------------------- outputs
+    def predict_contributions(self, df, output_format="Original", top_n=None, bottom_n=None, compare_abs=False):
+        """TreeSHAP contributions of a reference-layout GBM / DRF MOJO
+        (h2o-genmodel TreeSHAP.java over the trees + _aux.bin node weights;
+        GbmMojoModel adds init_f to the bias, DrfMojoModel's
+        ContributionsPredictorDRF divides by the number of trees -- binomial:
+        1/(F+1) - contribution to the P(class 0) trees)."""
+        from .treeshap_np import contributions_frame, tree_shap
+        if self.algo not in ("gbm", "drf"):
+            raise ValueError(f"contributions are not available for a {self.algo} MOJO")
+        if self.nclasses > 2:
+            raise ValueError("Calculating contributions is currently not supported for multinomial models.")
+        X = self.row_matrix(df)
+        n, F = X.shape[0], self.nfeatures
+        phi = np.zeros((n, F + 1))
+        dl = self.dom_len if self.version >= 1.2 else None
+        for g, t in enumerate(self.trees[0]):
+            if t is None:
+                continue
+            if t.root_leaf is not None:
+                phi[:, -1] += t.root_leaf
+                continue
+            name = "trees/t%02d_%03d_aux.bin" % (0, g)
+            if not self.be.exists(name):
+                raise ValueError("this MOJO has no auxiliary tree info (node weights) for contributions")
+            left, right, cover, value, feat = t.shap_graph(self.be.read(name))
+            I = len(t.col)
+            tree_shap(left, right, cover, value, feat, lambda j, t=t, I=I: ~t.node_right(j, X, dl, self.version) if
+                      j < I else np.ones(n, dtype=bool), n, phi)
+        if self.algo == "gbm":
+            phi[:, -1] += self.init_f
+        else:
+            ng = max(1, sum(1 for t in self.trees[0] if t is not None))
+            if self.nclasses == 2 and not self.binomial_double_trees:
+                phi = 1.0 / (F + 1) - phi / ng
+            else:
+                phi = phi / ng
+        return contributions_frame(phi, list(self.features), top_n=top_n, bottom_n=bottom_n, compare_abs=compare_abs)
+
     def predict_raw(self, df) -> np.ndarray:
         """[n, K] class probabilities (classification) or [n, 1] values /
         cluster ids (Generic model metrics)."""

@@ -1241,7 +1241,29 @@ def build_h2o_mojo(model) -> bytes:
     Word2Vec, Stacked Ensemble, PCA)."""
     z = _Zip()
     _write_algo(model, z)
+    write_model_details(model, z)
     return z.close()
+
+
+def model_details_json(model) -> str:
+    """The model's ModelSchemaV3 JSON (output: metrics, variable importances,
+    model summary, scoring history; parameters) as the reference writes it to
+    experimental/modelDetails.json (ModelMojoWriter.writeModelDetails,
+    hex/ModelMojoWriter.java:96) and ModelJsonReader reads it back."""
+    import json
+    from ..server import schemas as S
+    try:
+        d = S.model_v3(model.model_id, model)
+    except Exception as e:  # noqa: BLE001 - details are informational; the MOJO stays valid
+        d = {"model_id": S.key(model.model_id, "Model"), "algo": model.algo, "output": None,
+             "details_error": repr(e)}
+    return json.dumps(S.jsonable(d))
+
+
+def write_model_details(model, z):
+    z.write("experimental/modelDetails.json", model_details_json(model))
+    z.write("experimental/README.md", "Outputting model information in JSON is an experimental feature and we "
+            "appreciate any feedback.\nThe contents of this folder may change with another version of H2O.\n")
 
 
 def build_mojo_pipeline(models, mapping, main_alias) -> bytes:

@@ -105,6 +105,10 @@ def _forest_arrays(w, forest, names):
     P = forest.pack(torch.device("cpu"))
     for k in ("feat", "thr", "left", "right", "na_left", "cat_off", "cat_len", "cat_bits", "value", "roots", "tclass"):
         w.add_array(f"forest_{k}", P[k].cpu().numpy())
+    # node training weights (covers), in the packed node order: the standalone
+    # scorer's TreeSHAP background distribution (predict_contributions)
+    w.add_array("forest_weight", np.concatenate([np.asarray(t.weight, dtype=np.float64) for t in forest.trees])
+                if forest.trees else np.zeros(0))
 
 
 def build_mojo(model) -> bytes:
@@ -297,6 +301,11 @@ def build_mojo(model) -> bytes:
             "n_features": len(spec.x) if spec else 0, "n_classes": spec.nclasses if spec else 1,
             "supervised": str(model.supervised_learning).lower(), "uuid": model.model_id,
             "h2o_version": "h2o3_amd-0.1.0"}
+    try:
+        from .h2o_writer import model_details_json
+        w.files["experimental/modelDetails.json"] = model_details_json(model)
+    except Exception:  # noqa: BLE001 - informational only
+        pass
     return w.to_zip_bytes(info, cols, domains)
 
 
