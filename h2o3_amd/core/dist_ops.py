@@ -280,7 +280,7 @@ def quantile_values(v: Vec, probs, method="interpolate", weights=None):
 
 
 # ------------------------------------------------------------------ group-wise median / mode
-def segment_median_mode(gid: torch.Tensor, x: torch.Tensor, G: int, op: str) -> torch.Tensor:
+def segment_median_mode(gid: torch.Tensor, x: torch.Tensor, G: int, op: str, combine: str = "interpolate") -> torch.Tensor:
     """Per-group median (torch.quantile 0.5 rule) or mode (most frequent value,
     ties -> smallest) of x over groups gid in [0, G), NaN ignored; one sort,
     no per-group loop."""
@@ -300,7 +300,10 @@ def segment_median_mode(gid: torch.Tensor, x: torch.Tensor, G: int, op: str) -> 
         hi = start + cnt // 2
         lo, hi = lo[has], hi[has]
         a, b = v[lo], v[hi]
-        res[has] = torch.where(lo == hi, a, a + 0.5 * (b - a))
+        cm = str(combine).lower()
+        # even counts: the two middle values combined like Quantile's
+        # combine_method (lo / hi / the average)
+        res[has] = a if cm in ("lo", "low") else b if cm in ("hi", "high") else torch.where(lo == hi, a, a + 0.5 * (b - a))
         return res
     # mode: runs of equal (group, value); per group the longest run, ties -> smallest value
     new = torch.ones(v.numel(), dtype=torch.bool, device=dev)
@@ -316,12 +319,12 @@ def segment_median_mode(gid: torch.Tensor, x: torch.Tensor, G: int, op: str) -> 
     return res
 
 
-def group_median_mode(gid: torch.Tensor, x: torch.Tensor, G: int, op: str) -> torch.Tensor:
+def group_median_mode(gid: torch.Tensor, x: torch.Tensor, G: int, op: str, combine: str = "interpolate") -> torch.Tensor:
     """segment_median_mode over row-sharded (gid, x): each group's rows are
     routed once (all_to_all) to the rank owning a contiguous range of group
     ids, which computes its groups; the G-sized results are all-gathered."""
     if not _dist():
-        return segment_median_mode(gid, x, G, op)
+        return segment_median_mode(gid, x, G, op, combine)
     from .dist_munge import exchange
     W = cloud.world()
     dest = (gid * W) // max(G, 1)
@@ -329,7 +332,7 @@ def group_median_mode(gid: torch.Tensor, x: torch.Tensor, G: int, op: str) -> to
     r = cloud.rank()
     g0 = (r * G + W - 1) // W            # first gid with gid * W // G == r
     g1 = ((r + 1) * G + W - 1) // W
-    loc = segment_median_mode(got[0].data - g0, got[1].data, max(g1 - g0, 0), op)
+    loc = segment_median_mode(got[0].data - g0, got[1].data, max(g1 - g0, 0), op, combine)
     return _gather(loc)
 
 

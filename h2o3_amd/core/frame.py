@@ -987,7 +987,8 @@ class H2OFrame:
         from .munging import rank_within_group_by
         return rank_within_group_by(self, group_by_cols, sort_cols, ascending, new_col_name, sort_cols_sorted)
 
-    def topN(self, column=0, nPercent=10, grabTopN=-1):
+    def topN(self, column=0, nPercent=10, grabTopN=1):
+        """Top nPercent% of a numeric column (h2o-py frame.py:4022 -> topn, grabTopN = 1)."""
         from .munging import topn
         return topn(self, column, nPercent, grabTopN)
 

@@ -94,8 +94,10 @@ def cov(x, y=None):
 
 
 def distance(x, y, measure="l2"):
-    a = _num_matrix(x.gather())
-    b = _num_matrix(y.gather())
+    """AstDistance: rows of x (this rank's shard, the result stays sharded)
+    against every row of y (the reference's MRTask over x broadcasts y)."""
+    a = _num_matrix(x)
+    b = _num_matrix(y.gather() if cloud.is_distributed() else y)
     m = measure.lower()
     if m == "l1":
         d = torch.cdist(a, b, p=1)
@@ -107,7 +109,7 @@ def distance(x, y, measure="l2"):
         d = ((a @ b.T) / torch.outer(a.norm(dim=1), b.norm(dim=1))) ** 2
     else:
         raise ValueError(measure)
-    return _reshard(H2OFrame.from_tensor(d))
+    return H2OFrame.from_tensor(d)
 
 
 # ---------------------------------------------------------------- random / split
@@ -624,53 +626,53 @@ def impute(fr, column=-1, method="mean", combine_method="interpolate", by=None, 
 
 
 def _impute_by_group(fr, j, method, combine_method, by):
-    """AstImpute with group-by columns: each NA of column j takes its group's
-    mean / median / mode (hex.rapids AstImpute + AstGroup); groups whose
-    column is all NA stay NA.  Group ids come from the gathered key columns
-    (every rank the same), the fills of this rank's rows are sliced out.
+    """AstImpute with group-by columns (advmath/AstImpute.java:72): each NA
+    of column j takes its group's mean / median / mode; groups whose column is
+    all NA stay NA.  Distributed like the reference's MRTask: group ids are
+    mixed-radix codes over the GLOBAL per-column key dictionaries, means are
+    one all-reduce of per-group (sum, count), medians / modes route each
+    group's values to one owner rank (dist_ops.group_median_mode); only the
+    G-sized group results cross ranks, never the frame.
     -> frame of the group keys and their fill value."""
     import pandas as pd
-    g = fr.gather() if cloud.is_distributed() else fr
+    from .dist_ops import global_key, group_median_mode
     by = list(by) if isinstance(by, (list, tuple)) else [by]
-    bycols = [g.names[b] if isinstance(b, (int, float)) else b for b in (int(b) if isinstance(b, float) else b
-                                                                          for b in by)]
-    uniq, gid = _group_ids(g, bycols)
-    G = int(uniq.shape[0])
-    v = g._vecs[j]
+    bycols = [fr.names[b] if isinstance(b, (int, float)) else b for b in (int(b) if isinstance(b, float) else b
+                                                                           for b in by)]
+    dist = cloud.is_distributed()
+    keys = [global_key(fr.vec(c)) for c in bycols]
+    keys = [torch.where(torch.isnan(k), torch.full_like(k, -1e300), k) for k in keys]
+    vals = [torch.unique(coll.all_gather_var(torch.unique(k).contiguous())) if dist else torch.unique(k)
+            for k in keys]
+    cards = [max(int(u.numel()), 1) for u in vals]
+    if math.prod(cards) >= (1 << 62):
+        raise ValueError("impute: too many distinct group-by key combinations")
+    code = torch.zeros(fr.nlocal, dtype=torch.int64, device=_dev())
+    for k, u, c in zip(keys, vals, cards):
+        code = code * c + torch.searchsorted(u, k)
+    uc = torch.unique(code)
+    ucode = torch.unique(coll.all_gather_var(uc.contiguous())) if dist else uc
+    G = int(ucode.numel())
+    gid = torch.searchsorted(ucode, code)
+    v = fr._vecs[j]
     enum = v.type == T_ENUM
     x = v.data.to(torch.float64) if enum else v.as_float(torch.float64)
-    ok = (x >= 0) if enum else ~torch.isnan(x)
-    gv, xv = gid[ok], x[ok]
+    if enum:
+        x = torch.where(v.data < 0, torch.full_like(x, math.nan), x)
     if enum or method == "mode":
-        codes = xv.to(torch.int64)
-        L = int(codes.max()) + 1 if codes.numel() else 1
-        cnt = torch.bincount(gv * L + codes, minlength=G * L).view(G, L)
-        fill = torch.argmax(cnt, 1).to(torch.float64)
-        fill = torch.where(cnt.sum(1) > 0, fill, torch.full_like(fill, float("nan")))
+        fill = group_median_mode(gid, x, G, "mode")
     elif method == "median":
-        order = torch.argsort(xv, stable=True)
-        order = order[torch.argsort(gv[order], stable=True)]
-        xs = xv[order]
-        n = torch.bincount(gv, minlength=G)
-        start = torch.cumsum(n, 0) - n
-        lo = (start + (n - 1).clamp_min(0) // 2).clamp_max(max(xs.numel() - 1, 0))
-        hi = (start + n // 2).clamp_max(max(xs.numel() - 1, 0))
-        cm = str(combine_method).lower()
-        if xs.numel() == 0:
-            fill = torch.full((G,), float("nan"), dtype=torch.float64, device=x.device)
-        else:
-            a, b = xs[lo], xs[hi]
-            fill = a if cm in ("lo", "low") else b if cm in ("hi", "high") else (a + b) / 2
-            fill = torch.where(n > 0, fill, torch.full_like(fill, float("nan")))
+        fill = group_median_mode(gid, x, G, "median", combine=str(combine_method))
     else:
-        s = torch.zeros(G, dtype=torch.float64, device=x.device).index_add_(0, gv, xv)
-        n = torch.bincount(gv, minlength=G).to(torch.float64)
-        fill = s / n
+        ok = ~torch.isnan(x)
+        S = torch.zeros((2, G), dtype=torch.float64, device=x.device)
+        S[0].index_add_(0, gid[ok], x[ok])
+        S[1].index_add_(0, gid[ok], torch.ones_like(x[ok]))
+        if dist:
+            coll.allreduce_(S)
+        fill = torch.where(S[1] > 0, S[0] / S[1].clamp(min=1), torch.full_like(S[0], math.nan))
     row_fill = fill[gid]
     lv = fr._vecs[j]
-    if cloud.is_distributed():
-        off = fr.row_offset()
-        row_fill = row_fill[off:off + lv.data.shape[0]]
     if lv.type == T_ENUM:
         miss = (lv.data < 0) & ~torch.isnan(row_fill)
         fr._vecs[j] = Vec(torch.where(miss, torch.nan_to_num(row_fill, nan=-1).to(lv.data.dtype), lv.data),
@@ -678,17 +680,28 @@ def _impute_by_group(fr, j, method, combine_method, by):
     else:
         lx = lv.data
         fr._vecs[j] = Vec(torch.where(torch.isnan(lx), row_fill.to(lx.dtype), lx), lv.type)
-    keys = {}
-    for k, c in enumerate(bycols):
-        kv = g.vec(c)
-        col = uniq[:, k].cpu().numpy()
+    # the group keys, decoded from the codes (every rank the same)
+    out = {}
+    rem = ucode
+    cols_u = []
+    for u, c in zip(reversed(vals), reversed(cards)):
+        cols_u.append(u[rem % c] if u.numel() else torch.full_like(rem, -1e300, dtype=torch.float64))
+        rem = rem // c
+    cols_u = list(reversed(cols_u))
+    for c, col in zip(bycols, cols_u):
+        kv = fr.vec(c)
+        colh = col.cpu().numpy()
         if kv.type == T_ENUM:
-            keys[c] = [kv.domain[int(t)] if t >= 0 else None for t in col]
+            out[c] = [kv.domain[int(t)] if t >= 0 and t != -1e300 else None for t in colh]
+        elif kv.on_host:
+            loc = sorted(set(z for z in kv.to_numpy() if z is not None))
+            allv = sorted(set().union(*coll.all_gather_object(loc))) if dist else loc
+            out[c] = [allv[int(t)] if t != -1e300 else None for t in colh]
         else:
-            keys[c] = [None if t == -1e300 else t for t in col]
+            out[c] = [None if t == -1e300 else t for t in colh]
     fv = fill.cpu().numpy()
-    keys[g.names[j]] = [v.domain[int(t)] if t == t else None for t in fv] if enum else fv.tolist()
-    return H2OFrame(pd.DataFrame(keys), _local=not cloud.is_distributed())
+    out[fr.names[j]] = [v.domain[int(t)] if t == t else None for t in fv] if enum else fv.tolist()
+    return H2OFrame(pd.DataFrame(out), _local=not dist)
 
 
 def _ffill(x, maxlen, dim):
@@ -707,21 +720,30 @@ def _ffill(x, maxlen, dim):
 def fillna(fr, method="forward", axis=0, maxlen=1):
     """AstFillNA: fill up to maxlen consecutive NAs with the previous
     (forward) or next (backward) value, down each column (axis 0) or along
-    each row (axis 1); vectorized scans, no per-element loop."""
+    each row (axis 1); vectorized scans, no per-element loop.  Down columns
+    of a row-sharded frame each rank fills its own shard and the runs that
+    cross a shard boundary take the neighbouring ranks' carry (last / first
+    valid value and its distance): one small all-gather, no frame gather."""
     if method not in ("forward", "backward"):
         raise ValueError("method must be 'forward' or 'backward'")
-    g = fr.gather() if axis == 0 else fr
+    g = fr
     num = [j for j, v in enumerate(g._vecs) if not v.on_host]
     out = list(g._vecs)
     back = method == "backward"
     if axis == 0:
+        xs = {}
         for j in num:
             v = g._vecs[j]
             x = v.as_float(torch.float64)
             if v.type == T_ENUM:
                 x = torch.where(v.data < 0, torch.full_like(x, float("nan")), x)
+            xs[j] = x
             y = _ffill(x.flip(0) if back else x, maxlen, 0)
-            out[j] = _fill_vec(v, y.flip(0) if back else y)
+            out[j] = y.flip(0) if back else y
+        if cloud.is_distributed() and num:
+            out = _fill_across_shards(xs, out, num, back, int(maxlen))
+        for j in num:
+            out[j] = _fill_vec(g._vecs[j], out[j])
     elif num:
         X = torch.stack([(lambda v: torch.where(v.data < 0, torch.full_like(v.as_float(torch.float64), float("nan")),
                                                  v.as_float(torch.float64)) if v.type == T_ENUM
@@ -730,8 +752,53 @@ def fillna(fr, method="forward", axis=0, maxlen=1):
         Y = Y.flip(1) if back else Y
         for q, j in enumerate(num):
             out[j] = _fill_vec(g._vecs[j], Y[:, q].contiguous())
-    res = H2OFrame.from_vecs(out, g.names)
-    return _reshard(res) if (axis == 0 and cloud.is_distributed()) else res
+    return H2OFrame.from_vecs(out, g.names)
+
+
+def _fill_across_shards(xs, out, num, back, maxlen):
+    """Shard-boundary part of fillna down columns: per rank and column the
+    (row count, last / first valid position, its value) are all-gathered;
+    each rank's leading (forward) / trailing (backward) NA run then takes the
+    nearest valid value of the preceding / following ranks within maxlen."""
+    W, r = cloud.world(), cloud.rank()
+    dev = _dev()
+    info = []
+    for j in num:
+        x = xs[j]
+        n = x.numel()
+        valid = torch.nonzero(~torch.isnan(x)).view(-1)
+        if valid.numel():
+            p = int(valid[0]) if back else int(valid[-1])
+            info.append([float(n), float(p), float(x[p])])
+        else:
+            info.append([float(n), -1.0, 0.0])
+    t = torch.tensor(info, dtype=torch.float64, device=dev).view(1, -1)
+    allinfo = coll.all_gather_dim0(t.contiguous()).view(W, len(num), 3).cpu().numpy()
+    for c, j in enumerate(num):
+        x = xs[j]
+        n = x.numel()
+        valid = torch.nonzero(~torch.isnan(x)).view(-1)
+        gap, val, found = 0, 0.0, False
+        ranks = range(r + 1, W) if back else range(r - 1, -1, -1)
+        for q in ranks:
+            nq, pq, vq = allinfo[q, c]
+            if pq >= 0:
+                gap += int(pq) if back else int(nq) - 1 - int(pq)
+                val, found = vq, True
+                break
+            gap += int(nq)
+        if not found or n == 0:
+            continue
+        pos = torch.arange(n, device=x.device)
+        if back:
+            run = pos > (int(valid[-1]) if valid.numel() else -1)     # trailing NAs
+            dist = (n - 1 - pos) + gap + 1
+        else:
+            run = pos < (int(valid[0]) if valid.numel() else n)       # leading NAs
+            dist = pos + gap + 1
+        fill = run & (dist <= maxlen)
+        out[j] = torch.where(fill, torch.full_like(out[j], float(val)), out[j])
+    return out
 
 
 def _fill_vec(v, y):
@@ -784,10 +851,25 @@ def apply(fr, fun, axis=0):
         vals = {n: [x[0] if not isinstance(x[0], H2OFrame) else x[0].flatten()] for n, x in res.items()}
         import pandas as pd
         return H2OFrame(pd.DataFrame(vals))
-    df = fr.as_data_frame()
-    out = df.apply(lambda row: fun(row), axis=1)
+    # axis=1 (AstApply over rows): each rank applies `fun` to its own row shard
+    # (the MRTask map); numeric results stay row-sharded, string results become
+    # an enum column over the GLOBAL sorted set of levels -- no frame gather
     import pandas as pd
-    return H2OFrame(pd.DataFrame({"C1": out.values}))
+    df = fr.as_data_frame(local=True)
+    out = df.apply(lambda row: fun(row), axis=1) if len(df) else pd.Series([], dtype=np.float64)
+    numeric = bool(len(out) == 0 or pd.api.types.is_numeric_dtype(out) or pd.api.types.is_bool_dtype(out))
+    if cloud.is_distributed():
+        numeric = all(coll.all_gather_object(numeric))
+    if numeric:
+        t = torch.as_tensor(np.asarray(out.values, dtype=np.float64), device=_dev())
+        return H2OFrame.from_vecs([Vec(t, T_REAL)], ["C1"])
+    vals = [None if (x is None or (isinstance(x, float) and math.isnan(x))) else str(x) for x in out.values]
+    levels = sorted(set(x for x in vals if x is not None))
+    if cloud.is_distributed():
+        levels = sorted(set().union(*coll.all_gather_object(levels)))
+    pos = {lv: i for i, lv in enumerate(levels)}
+    codes = torch.tensor([pos[x] if x is not None else -1 for x in vals], dtype=torch.int32, device=_dev())
+    return H2OFrame.from_vecs([Vec(codes, T_ENUM, levels)], ["C1"])
 
 
 def drop_duplicates(fr, columns=None, keep="first"):
@@ -812,13 +894,47 @@ def rank_within_group_by(fr, group_by_cols, sort_cols, ascending=None, new_col_n
 
 
 def topn(fr, column=0, nPercent=10, grabTopN=-1):
-    v = fr.vec(column)
+    """AstTopN (GrabTopNPQ, reducers/AstTopN.java:16): the top (grabTopN = 1)
+    or bottom (-1) round(nPercent% of the rows) non-NA values of a column with
+    their ORIGINAL global row indices.  Each rank keeps its own top-k of (value,
+    global row) -- the MRTask map's priority queue --, the k-sized candidate
+    lists are all-gathered (the reduce) and every rank selects the same final k,
+    which come back row-sharded.  Ties keep the lower row index."""
+    from .dist_ops import _sharded_from_replicated
+    j = fr._col_index(column)
+    v = fr._vecs[j]
     x = v.as_float(torch.float64)
-    n = x.numel()
-    k = max(1, int(math.ceil(n * nPercent / 100.0)))
-    vals, idx = torch.topk(torch.nan_to_num(x, nan=-math.inf) if grabTopN > 0 else -torch.nan_to_num(x, nan=math.inf), k)
-    import pandas as pd
-    return H2OFrame(pd.DataFrame({"Row Indices": idx.cpu().numpy().astype(float), fr.names[fr._col_index(column)]: x[idx].cpu().numpy()}))
+    if v.type == T_ENUM:
+        x = torch.where(v.data < 0, torch.full_like(x, math.nan), x)
+    k = int(math.floor(nPercent * 0.01 * fr.nrows + 0.5))    # Java Math.round
+    flip = 1.0 if grabTopN > 0 else -1.0
+    ok = ~torch.isnan(x)
+    key = torch.where(ok, x * flip, torch.full_like(x, -math.inf))
+    kl = min(k, int(ok.sum()))
+    rows = torch.arange(x.numel(), device=x.device, dtype=torch.int64) + fr.row_offset()
+    if kl > 0:
+        o = lexsort_desc_rows(key, rows)[:kl]
+        cand_v, cand_r = x[o], rows[o]
+    else:
+        cand_v = torch.zeros(0, dtype=torch.float64, device=x.device)
+        cand_r = torch.zeros(0, dtype=torch.int64, device=x.device)
+    if cloud.is_distributed():
+        cand_v = coll.all_gather_var(cand_v.contiguous())
+        cand_r = coll.all_gather_var(cand_r.contiguous())
+    o = lexsort_desc_rows(cand_v * flip, cand_r)[:k]
+    vals, ridx = cand_v[o], cand_r[o]
+    name = fr.names[j]
+    is_int = v.type in (T_INT, T_ENUM) or (vals.numel() > 0 and bool((vals == torch.round(vals)).all()))
+    vecs = [Vec(ridx.to(torch.float64), T_INT), Vec(vals, T_INT if is_int else T_REAL)]
+    for q in vecs:
+        q.replicated = True
+    return _sharded_from_replicated(vecs, ["Original_Row_Indices", name])
+
+
+def lexsort_desc_rows(key, rows):
+    """Order by key descending, then row index ascending."""
+    o = torch.argsort(rows, stable=True)
+    return o[torch.argsort(-key[o], stable=True)]
 
 
 def interaction(data, factors, pairwise, max_factors, min_occurrence):

@@ -186,6 +186,25 @@ def _dist_ops(h2o):
     gb = fr.group_by(["b"]).median("v", na="rm").mode("t").get_frame()
     out["gb_med_mode"] = rows(gb)
     out["sort_dups"] = rows(fr.sort(["c", "t"], ascending=[False, True]))
+    # AstTopN / AstImpute-by-group / AstApply / AstFillNA / AstDistance without frame gathers
+    out["topn"] = rows(fr.topN("v", 3))
+    out["bottomn"] = rows(fr.bottomN("t", 2))
+    for meth in ("mean", "median", "mode"):
+        f2 = h2o.H2OFrame(df)
+        f2["b"] = f2["b"].asfactor()
+        col = "b" if meth == "mode" else "v"
+        if meth == "mode":
+            f2[::11, "b"] = None
+        keys = f2.impute(col, method=meth, by=["a"])
+        out[f"impute_{meth}"] = rows(f2[[col, "a"]]) + [["keys"]] + rows(keys[0] if isinstance(keys, list) else keys)
+    out["apply_num"] = rows(fr[["v", "t"]].apply(lambda r: (0.0 if r["v"] != r["v"] else r["v"]) + 2 * r["t"], axis=1))
+    out["apply_str"] = rows(fr[["t"]].apply(lambda r: "hi" if r["t"] > 20 else "lo", axis=1))
+    fz = h2o.H2OFrame(pd.DataFrame({"x": [np.nan if (i % 600) < 7 or 2490 <= i < 2510 else float(i)
+                                          for i in range(n)]}))
+    out["fill_fwd"] = rows(fz.fillna("forward", maxlen=5))
+    out["fill_bwd"] = rows(fz.fillna("backward", maxlen=12))
+    out["distance"] = rows(fr[["v", "t"]][:50, :].fillna("forward", maxlen=100).distance(
+        h2o.H2OFrame(pd.DataFrame({"v": [0.5, -1.0, 2.0], "t": [3.0, 10.0, 30.0]}))))
     return out
 
 

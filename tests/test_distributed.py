@@ -55,7 +55,9 @@ def results(tmp_path_factory):
 
 
 @pytest.mark.parametrize("op", ["quantile", "quantile_w", "table1", "table2", "table_sparse", "unique", "hist", "cor",
-                                "spearman", "dedup", "pivot", "melt", "rank", "inter", "gb_med_mode", "sort_dups"])
+                                "spearman", "dedup", "pivot", "melt", "rank", "inter", "gb_med_mode", "sort_dups",
+                                "topn", "bottomn", "impute_mean", "impute_median", "impute_mode", "apply_num",
+                                "apply_str", "fill_fwd", "fill_bwd", "distance"])
 def test_dist_ops_match_one_rank(results, op):
     """Quantile / table / unique / hist / cor / pivot / melt / rank-within-group /
     interaction / drop_duplicates / median-mode / sort computed shard-locally
