@@ -107,7 +107,7 @@ def main():
     ap.add_argument("--rows", type=int, default=100_000_000)
     ap.add_argument("--cols", type=int, default=100)
     ap.add_argument("--max-depth", type=int, default=8)
-    ap.add_argument("--algo", default="gbm", choices=["gbm", "glm", "drf", "kmeans", "dl"])
+    ap.add_argument("--algo", default="gbm", choices=["gbm", "glm", "drf", "kmeans", "dl", "pca"])
     ap.add_argument("--hidden", default="200,200", help="DL hidden layers (--algo dl)")
     ap.add_argument("--batch", type=int, default=1024, help="DL mini-batch rows (--algo dl)")
     ap.add_argument("--k", type=int, default=16, help="K-Means clusters (--algo kmeans)")
@@ -193,6 +193,37 @@ def main():
         unit = "iters/s"
         model = f"KMeans k={args.k} {args.rows / 1e6:g}Mx{F}"
         extra_cfg = {"distance_precision": "f32 MFMA (v_mfma_f32_16x16x4_f32), f64 cross-workgroup sums"}
+    elif args.algo == "pca":
+        # one step = one PCA fit of rank k (pca_method="Randomized") + the
+        # projection of every row: the MFMA Gram pass (gram.hip) and the
+        # covariance, the subspace iterations on the P x P covariance, then
+        # X V on the skinny MFMA kernel (kmeans.hip, cluster_ops.xv)
+        from h2o3_amd.models.datainfo import DataInfo
+        from h2o3_amd.models.clustering import _top_eig
+        from h2o3_amd.ops import cluster_ops, linalg_ops
+        from h2o3_amd.parallel import collectives as coll
+        di = DataInfo(fr, names, standardize=False, use_all_factor_levels=True, pad_to=4)
+        Xp, _ = di.expand(fr)
+        del fr
+        P = di.P
+        nrow = coll.allreduce_scalar(float(Xp.shape[0]))
+        kk = args.k
+
+        def step():
+            G = linalg_ops.weighted_gram(Xp)[:P, :P]
+            coll.allreduce_(G)
+            mu = Xp[:, :P].to(torch.float64).sum(0)
+            coll.allreduce_(mu)
+            mu = mu / nrow
+            cov = (G - nrow * torch.outer(mu, mu)) / max(nrow - 1, 1)
+            ev, V = _top_eig(cov, kk, "randomized", 30, 1)
+            Vp = torch.zeros((Xp.shape[1], V.shape[1]), dtype=torch.float64)
+            Vp[:P] = V
+            cluster_ops.xv(Xp, Vp, min_rows=0)
+        metric = "pca_fits_per_sec"
+        unit = "fits/s"
+        model = f"PCA Randomized k={args.k} {args.rows / 1e6:g}Mx{F} (Gram pass + subspace iterations + projections)"
+        extra_cfg = {"gram": "gram.hip MFMA, f64 across row blocks", "projection": "kmeans.hip skinny MFMA (f32)"}
     elif args.algo == "dl":
         # one step = one mini-batch training step of the MLP (forward, backward,
         # per-row ADADELTA update); value = training samples / s
@@ -309,7 +340,7 @@ def main():
                "scaling": "strong", "vs_baseline": None, "dtype": "fp32",
                "data": "synthetic (random normal features, logistic label), generated on device",
                "config": {"model": model, "rows": args.rows, "cols": F,
-                          **({} if args.algo in ("glm", "kmeans", "dl") else {"max_depth": est._parms.get("max_depth"),
+                          **({} if args.algo in ("glm", "kmeans", "dl", "pca") else {"max_depth": est._parms.get("max_depth"),
                                                             "histogram_type": args.histogram_type,
                                                             "nbins": args.nbins}),
                           "global_batch": args.rows, "seq_len": None, "parallelism": f"dp{world}", **extra_cfg},

@@ -20,7 +20,7 @@ import torch
 
 from ..core.frame import H2OFrame
 from ..core.vec import T_ENUM, T_INT, T_REAL, Vec
-from ..ops import linalg_ops
+from ..ops import cluster_ops, linalg_ops
 from ..parallel import cloud
 from ..parallel import collectives as coll
 from ..core.groupsum import group_sum
@@ -142,25 +142,21 @@ class H2OPrincipalComponentAnalysisEstimator(H2OEstimator):
                 evals, evecs = torch.linalg.eigh(cov.cpu())
                 order = torch.argsort(evals, descending=True)
                 evals, evecs = evals[order], evecs[:, order]
-        else:  # Power / Randomized: subspace iteration on X (GEMMs on device)
-            gen = torch.Generator(device="cpu").manual_seed(_seed(p))
-            Q = torch.randn((P, k + 5), generator=gen, dtype=torch.float64).to(X.device)
-            Xd = X[:, :P].to(torch.float64)
-            mean = Xd.sum(0)
+        else:  # Power / Randomized (hex/svd/SVD.java): iterations on the covariance
+            # X'X comes from ONE pass of the hand-written MFMA Gram (gram.hip via
+            # weighted_gram, f64 across row blocks); the centred cross-product
+            # Xc'(Xc Q) of every subspace / power iteration is (G - n mu mu') Q,
+            # so the iterations run on the P x P matrix and never re-read X
+            G = linalg_ops.weighted_gram(X)[:P, :P]
+            coll.allreduce_(G)
+            mean = X[:, :P].to(torch.float64).sum(0)
             coll.allreduce_(mean)
             mean = mean / n
-            Xc = Xd - mean if not di.standardize else Xd
-            for _ in range(min(int(p.get("max_iterations", 1000)), 30)):
-                Z = Xc.T @ (Xc @ Q)
-                coll.allreduce_(Z)
-                Q, _ = torch.linalg.qr(Z)
-            B = Xc @ Q
-            S = B.T @ B
-            coll.allreduce_(S)
-            ev, U = torch.linalg.eigh(S.cpu())
-            order = torch.argsort(ev, descending=True)
-            evals = ev[order] / max(n - 1, 1)
-            evecs = (Q.cpu() @ U[:, order])
+            if not di.standardize:
+                G = G - n * torch.outer(mean, mean)
+            cov = G / max(n - 1, 1)
+            iters = min(int(p.get("max_iterations", 1000)), 1000)
+            evals, evecs = _top_eig(cov, k, method, iters, _seed(p))
         k = min(k, evecs.shape[1])
         sd = torch.sqrt(evals.clamp_min(0))
         tot = float(evals.clamp_min(0).sum())
@@ -178,8 +174,13 @@ class H2OPrincipalComponentAnalysisEstimator(H2OEstimator):
 
     def _predict_raw(self, frame):
         X, _ = self._dinfo.expand(frame)
-        Xd = X[:, : self._dinfo.P].to(torch.float64) - self._mean.to(X.device)
-        return Xd @ self._evecs.to(X.device)
+        P = self._dinfo.P
+        # projections X v_j on the MFMA skinny-GEMM kernel for large frames
+        # (cluster_ops.xv; columns past P are padding), minus the mean's
+        V = torch.zeros((X.shape[1], self._evecs.shape[1]), dtype=torch.float64)
+        V[:P] = self._evecs
+        Z = cluster_ops.xv(X, V).to(torch.float64)
+        return Z - (self._mean.to(torch.float64) @ self._evecs).to(X.device).view(1, -1)
 
     def predict(self, test_data, **kw):
         Z = self._predict_raw(test_data)
@@ -227,7 +228,10 @@ class H2OSingularValueDecompositionEstimator(H2OEstimator):
         self._output["d"] = d.tolist()
         self._output["v"] = V.numpy()
         if p.get("keep_u", True):
-            U = (X[:, :P].to(torch.float64) @ V.to(X.device)) / d.to(X.device).clamp_min(1e-300)
+            # U = X V / d: the skinny MFMA projection kernel for large frames
+            Vp = torch.zeros((X.shape[1], V.shape[1]), dtype=torch.float64)
+            Vp[:P] = V
+            U = cluster_ops.xv(X, Vp).to(torch.float64) / d.to(X.device).clamp_min(1e-300)
             self._u = H2OFrame.from_vecs([Vec(U[:, j].contiguous(), T_REAL) for j in range(U.shape[1])],
                                          [f"u{j + 1}" for j in range(U.shape[1])])
             # u_name / v_name: DKV keys of the U and V frames (SVDModel._u_key / _v_key)

@@ -30,6 +30,10 @@ def _lib():
         lib.h2o_kmeans_resident_per_cu.argtypes = [_ci, _ci, _ci, _cf]
         lib.h2o_kmeans_sums.argtypes = [_cv, _cv, _cll, _ci, _ci, _cv, _cv, _cv, _cv, _ci, _cf, _cv]
         lib.h2o_kmeans_sums_resident_per_cu.argtypes = [_ci, _ci]
+        lib.h2o_kmeans_assign.argtypes = [_cv, _cll, _ci, _cv, _cv, _ci, _cv, _cv, _ci, _cv]
+        lib.h2o_kmeans_assign_resident_per_cu.argtypes = [_ci, _ci]
+        lib.h2o_xv.argtypes = [_cv, _cll, _ci, _cv, _ci, _cv, _ci, _cv]
+        lib.h2o_xv_resident_per_cu.argtypes = [_ci, _ci]
         lib._typed = True
     return lib
 
@@ -166,12 +170,22 @@ def _lloyd_split(lib, X, C32, cn, wt, k, P, ntiles, assign, dmin, xabs_max, stri
     asg_new = torch.empty(N, dtype=torch.int32, device=dev)
     d2 = dmin if (dmin is not None and dmin.dtype == torch.float32 and dmin.is_contiguous()) else \
         torch.empty(N, dtype=torch.float32, device=dev)
-    per_cu = int(lib.h2o_kmeans_resident_per_cu(k, P, 0, 0.0))
-    g1 = max(1, min(ntiles, max(per_cu, 1) * cus))
-    rc = lib.h2o_kmeans_lloyd(_ptr(X), _ptr(wt), N, P, _ptr(C32), _ptr(cn), k, _ptr(asg_new), None, _ptr(d2),
-                              None, g1, 0, 0.0, stream)
-    if rc != 0:
-        raise RuntimeError(f"h2o_kmeans_lloyd (assignment pass) failed: {rc}")
+    import os
+    per_cu = int(lib.h2o_kmeans_assign_resident_per_cu(k, P))
+    if per_cu > 0 and os.environ.get("H2O3_KM_ASSIGN", "wave") == "wave":
+        # wave-persistent assignment kernel: X rows in registers, only the
+        # centers in LDS (kmeans_assign_kernel)
+        g1 = max(1, min(-(-N // 64), per_cu * cus))
+        rc = lib.h2o_kmeans_assign(_ptr(X), N, P, _ptr(C32), _ptr(cn), k, _ptr(asg_new), _ptr(d2), g1, stream)
+        if rc != 0:
+            raise RuntimeError(f"h2o_kmeans_assign failed: {rc}")
+    else:
+        per_cu = int(lib.h2o_kmeans_resident_per_cu(k, P, 0, 0.0))
+        g1 = max(1, min(ntiles, max(per_cu, 1) * cus))
+        rc = lib.h2o_kmeans_lloyd(_ptr(X), _ptr(wt), N, P, _ptr(C32), _ptr(cn), k, _ptr(asg_new), None, _ptr(d2),
+                                  None, g1, 0, 0.0, stream)
+        if rc != 0:
+            raise RuntimeError(f"h2o_kmeans_lloyd (assignment pass) failed: {rc}")
     g2 = max(1, min(ntiles, max(int(lib.h2o_kmeans_sums_resident_per_cu(k, P)), 1) * cus))
     rows_wg = 64 * (-(-ntiles // g2))
     fx = float(2.0 ** 62 / (max(xabs_max, 1e-30) * rows_wg)) if xabs_max > 0 else 1.0
@@ -220,3 +234,33 @@ def _lloyd_torch(X, C, w, assign, accumulate, dmin, chunk=1 << 20):
             wsum.index_add_(0, idx, wc)
             wss.index_add_(0, idx, wc * d2)
     return st if accumulate else None
+
+
+# rows below which projections stay on the f64 torch path (small frames keep
+# f64 parity with the CPU reference; large ones take the MFMA kernel)
+XV_MIN_ROWS = 65536
+
+
+def xv(X, V, min_rows=None):
+    """X [N, W] @ V [W, k] -> [N, k] (f32 on the GPU kernel, else f64): the
+    PCA / SVD projections.  On the GPU (W % 4 == 0, W, k <= 256, N >=
+    min_rows) one pass of kmeans.hip's MFMA tile kernel in skinny-GEMM mode
+    (exact f32 products, f32 sums over the W columns; X read once, no
+    library GEMM); otherwise an f64 GEMM."""
+    N, W = X.shape
+    k = V.shape[1]
+    lim = XV_MIN_ROWS if min_rows is None else min_rows
+    lib = _lib() if X.is_cuda else None
+    if (lib is None or X.dtype != torch.float32 or W % 4 or W > 256 or k > 256 or k < 1 or N < lim):
+        return X.to(torch.float64) @ V.to(device=X.device, dtype=torch.float64)
+    Xc = X.contiguous()
+    Vt = V.to(device=X.device, dtype=torch.float32).t().contiguous()      # [k, W]
+    out = torch.empty((N, k), dtype=torch.float32, device=X.device)
+    per_cu = int(lib.h2o_xv_resident_per_cu(k, W))
+    if per_cu < 1:
+        return X.to(torch.float64) @ V.to(device=X.device, dtype=torch.float64)
+    G = max(1, min(-(-N // 64), per_cu * _cu_count(X.device)))
+    rc = lib.h2o_xv(_ptr(Xc), N, W, _ptr(Vt), k, _ptr(out), G, _cv(torch.cuda.current_stream().cuda_stream))
+    if rc != 0:
+        raise RuntimeError(f"h2o_xv failed: {rc}")
+    return out

@@ -317,6 +317,206 @@ __global__ __launch_bounds__(KM_THREADS) void kmeans_lloyd_kernel(
   }
 }
 
+// Large-k assignment pass (split path, first half): WAVE-persistent, X in
+// registers, only the centers in LDS.
+//
+// The fused / acc=0 Lloyd kernel stages a 64-row X tile in LDS next to the
+// centers; at k >= 64 that is 89 KB at P = 100, one 4-wave workgroup per CU,
+// i.e. one wave per SIMD feeding dependent MFMA chains.  Here each wave owns
+// 16-row tiles on its own (no barriers in the loop): lane (row li, k-group
+// g) loads its row's k-range [g*Pq, (g+1)*Pq) straight from HBM as float4
+// (the next tile is prefetched into a second register set), the centers sit
+// in LDS for the whole pass (KP x (P16 + 4) floats: 59 KB at k = 128,
+// P = 100), so 2 workgroups = 8 waves share a CU.  The MFMA loop interleaves
+// the KT independent 16-center accumulators (the four k-slices of a float4
+// outermost) so consecutive v_mfma never depend on each other.  Distances,
+// arg-min (ties to the lowest index) and d2 = |x|^2 + min_j(|c_j|^2 - 2 x.c_j)
+// as in the fused kernel; writes assign[N] and d2[N].
+// MODE 1 (skinny GEMM, PCA / SVD projections): the same MFMA tiles write the
+// dot products out[row][j] = x_row . c_j (f32, row-major [N][k]) instead of
+// the arg-min -- X read once, no library GEMM.
+template <int KT, int MAXNV, int MODE = 0>
+__global__ __launch_bounds__(256) void kmeans_assign_kernel(const float* __restrict__ X, long long N, int P,
+                                                            const float* __restrict__ Cin,
+                                                            const float* __restrict__ cn, int k,
+                                                            int* __restrict__ assign, float* __restrict__ d2out) {
+  extern __shared__ __align__(16) float ldsa[];
+  const int P16 = (P + 15) & ~15;
+  const int S = P16 + 4;
+  const int nq = (k + 15) >> 4;
+  const int KP = nq * 16;
+  float* Cs = ldsa;                          // [KP][S]
+  float* cns = Cs + KP * S;                  // [KP]
+  const int tid = threadIdx.x;
+  for (int e = tid; e < KP * S; e += 256) {
+    const int j = e / S, c = e - j * S;
+    Cs[e] = (j < k && c < P) ? Cin[(long long)j * P + c] : 0.f;
+  }
+  for (int j = tid; j < KP; j += 256) cns[j] = (j < k && cn != nullptr) ? cn[j] : INFINITY;
+  __syncthreads();
+  const int lane = tid & 63, wv = tid >> 6;
+  const int li = lane & 15, g = lane >> 4;
+  const int Pq = P16 >> 2;                   // k-range per lane group (multiple of 4)
+  const int nv = Pq >> 2;                    // float4 per lane
+  const long long ntiles = (N + 15) >> 4;
+  const long long nwaves = (long long)gridDim.x * 4;
+  long long t = (long long)xcd_remap(blockIdx.x, gridDim.x) * 4 + wv;
+  const float* cb = Cs + li * S + g * Pq;
+  f32x4 A[MAXNV], B[MAXNV];
+  auto load = [&](long long tt, f32x4 (&R)[MAXNV]) {
+    const long long row = tt * 16 + li;
+    const bool okr = row < N;
+    const float* src = X + row * (long long)P + g * Pq;
+#pragma unroll
+    for (int v = 0; v < MAXNV; ++v) {
+      f32x4 q = {0.f, 0.f, 0.f, 0.f};
+      if (v < nv && okr && g * Pq + 4 * v < P) q = *(const f32x4*)(src + 4 * v);
+      R[v] = q;
+    }
+  };
+  if (t < ntiles) load(t, A);
+  for (; t < ntiles; t += nwaves) {
+    const bool more = t + nwaves < ntiles;
+    if (more) load(t + nwaves, B);           // next tile in flight during the MFMAs
+    f32x4 acc[KT];
+#pragma unroll
+    for (int q = 0; q < KT; ++q) acc[q] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    float sq = 0.f;
+#pragma unroll
+    for (int v = 0; v < MAXNV; ++v) {
+      if (v < nv) {
+        const f32x4 a4 = A[v];
+        sq += a4[0] * a4[0] + a4[1] * a4[1] + a4[2] * a4[2] + a4[3] * a4[3];
+        f32x4 b4[KT];
+#pragma unroll
+        for (int q = 0; q < KT; ++q)
+          b4[q] = q < nq ? *(const f32x4*)(cb + q * 16 * S + 4 * v) : (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int q = 0; q < KT; ++q)
+            if (q < nq) acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[j], b4[q][j], acc[q], 0, 0, 0);
+      }
+    }
+    sq += __shfl_xor(sq, 16, 64);
+    sq += __shfl_xor(sq, 32, 64);            // |x|^2 of row li on every lane group
+    const long long r0 = t * 16;
+    if (MODE == 1) {
+      // lane holds rows 4g + r, column q*16 + li of every 16-column block
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const long long row = r0 + 4 * g + r;
+        if (row < N) {
+#pragma unroll
+          for (int q = 0; q < KT; ++q) {
+            const int j = q * 16 + li;
+            if (q < nq && j < k) d2out[row * k + j] = acc[q][r];
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < (MODE == 0 ? 4 : 0); ++r) {
+      float best = INFINITY;
+      int bi = 0x7fffffff;
+#pragma unroll
+      for (int q = 0; q < KT; ++q) {
+        const int j = q * 16 + li;
+        const float d = q < nq ? cns[j] - 2.f * acc[q][r] : INFINITY;
+        if (d < best) { best = d; bi = j; }
+      }
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        const float ob = __shfl_xor(best, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        if (ob < best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+      }
+      const float xs = __shfl(sq, 4 * g + r, 64);   // |x|^2 of row 4g + r
+      const long long row = r0 + 4 * g + r;
+      if (li == 0 && row < N) {
+        assign[row] = bi < k ? bi : 0;
+        d2out[row] = fmaxf(xs + best, 0.f);
+      }
+    }
+    if (more) {
+#pragma unroll
+      for (int v = 0; v < MAXNV; ++v) A[v] = B[v];
+    }
+  }
+}
+
+template <int KT, int MAXNV, int MODE = 0>
+static int ka_launch2(const float* X, long long N, int P, const float* C, const float* cn, int k, int* assign,
+                      float* d2, int G, hipStream_t s, int* per_cu_out) {
+  const int P16 = (P + 15) & ~15, KP = ((k + 15) >> 4) * 16;
+  const size_t lds = ((size_t)KP * (P16 + 4) + KP) * sizeof(float);
+  auto kern = kmeans_assign_kernel<KT, MAXNV, MODE>;
+  hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return (int)e;
+  if (per_cu_out) {
+    int pc = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, kern, 256, lds) != hipSuccess) return -1;
+    *per_cu_out = pc;
+    return 0;
+  }
+  hipLaunchKernelGGL(kern, dim3(G), dim3(256), lds, s, X, N, P, C, cn, k, assign, d2);
+  H2O_CHECK_LAUNCH();
+}
+
+template <int KT, int MODE>
+static int ka_launch(const float* X, long long N, int P, const float* C, const float* cn, int k, int* assign,
+                     float* d2, int G, hipStream_t s, int* per_cu_out) {
+  const int nv = ((P + 15) & ~15) >> 4;      // float4 per lane = P16 / 16
+  if (nv <= 2) return ka_launch2<KT, 2, MODE>(X, N, P, C, cn, k, assign, d2, G, s, per_cu_out);
+  if (nv <= 4) return ka_launch2<KT, 4, MODE>(X, N, P, C, cn, k, assign, d2, G, s, per_cu_out);
+  if (nv <= 8) return ka_launch2<KT, 8, MODE>(X, N, P, C, cn, k, assign, d2, G, s, per_cu_out);
+  return ka_launch2<KT, 16, MODE>(X, N, P, C, cn, k, assign, d2, G, s, per_cu_out);
+}
+
+template <int MODE = 0>
+static int ka_dispatch(const float* X, long long N, int P, const float* C, const float* cn, int k, int* assign,
+                       float* d2, int G, hipStream_t s, int* per_cu_out) {
+  if (P <= 0 || P > 256 || (P & 3) || k <= 0 || k > 256) return (int)hipErrorInvalidValue;
+  const int P16 = (P + 15) & ~15, KP = ((k + 15) >> 4) * 16;
+  if (((size_t)KP * (P16 + 4) + KP) * sizeof(float) > 160 * 1024) return (int)hipErrorInvalidValue;
+  const int kt = (k + 15) >> 4;
+  if (kt <= 1 && MODE == 1) return ka_launch<1, MODE>(X, N, P, C, cn, k, assign, d2, G, s, per_cu_out);
+  if (kt <= 2) return ka_launch<2, MODE>(X, N, P, C, cn, k, assign, d2, G, s, per_cu_out);
+  if (kt <= 4) return ka_launch<4, MODE>(X, N, P, C, cn, k, assign, d2, G, s, per_cu_out);
+  if (kt <= 8) return ka_launch<8, MODE>(X, N, P, C, cn, k, assign, d2, G, s, per_cu_out);
+  return ka_launch<16, MODE>(X, N, P, C, cn, k, assign, d2, G, s, per_cu_out);
+}
+
+extern "C" int h2o_kmeans_assign_resident_per_cu(int k, int P) {
+  int pc = 0;
+  if (ka_dispatch(nullptr, 0, P, nullptr, nullptr, k, nullptr, nullptr, 0, nullptr, &pc) != 0) return 0;
+  return pc;
+}
+
+// Assignment pass of the split path: assign[N] (int32) and d2[N] (f32,
+// squared distance to the chosen center).  G workgroups of 4 waves.
+extern "C" int h2o_kmeans_assign(const float* X, long long N, int P, const float* C, const float* cn, int k,
+                                 int* assign, float* d2, int G, hipStream_t s) {
+  if (N <= 0) return 0;
+  if (G <= 0 || !assign || !d2) return (int)hipErrorInvalidValue;
+  return ka_dispatch<0>(X, N, P, C, cn, k, assign, d2, G, s, nullptr);
+}
+
+// out [N][k] f32 = X [N][P] . V^T with V given as [k][P] rows (k <= 256,
+// P % 4 == 0): the projections of PCA / SVD (X v_j) on the f32 matrix cores,
+// X read once.  G workgroups of 4 waves (h2o_xv_resident_per_cu per CU).
+extern "C" int h2o_xv_resident_per_cu(int k, int P) {
+  int pc = 0;
+  if (ka_dispatch<1>(nullptr, 0, P, nullptr, nullptr, k, nullptr, nullptr, 0, nullptr, &pc) != 0) return 0;
+  return pc;
+}
+
+extern "C" int h2o_xv(const float* X, long long N, int P, const float* V, int k, float* out, int G, hipStream_t s) {
+  if (N <= 0) return 0;
+  if (G <= 0 || !out) return (int)hipErrorInvalidValue;
+  return ka_dispatch<1>(X, N, P, V, nullptr, k, nullptr, out, G, s, nullptr);
+}
+
 // out[e] = sum_g part[g][e] in f64 (e over the whole partial record)
 __global__ __launch_bounds__(256) void kmeans_reduce_kernel(const double* __restrict__ part, int G, long long stride,
                                                             double* __restrict__ out) {

@@ -236,6 +236,40 @@ def test_lloyd_kernel_matches_f64_reference(N, P, k, fx):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("N,P,k", [(200_003, 100, 128), (100_001, 100, 64), (50_000, 36, 200), (9_999, 8, 17)])
+def test_split_path_wave_assign_kernel(monkeypatch, N, P, k):
+    """Large-k split path with the wave-persistent assignment kernel
+    (kmeans_assign_kernel: X rows in registers, centers in LDS): the same
+    per-accumulator MFMA order as the Lloyd kernel, so the assignment equals
+    the Lloyd kernel's bit for bit and the f64 reference wherever the two
+    closest centers are not within rounding; the sums pass statistics match f64."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    g = torch.Generator(device="cuda").manual_seed(N + k)
+    X = torch.randn((N, P), generator=g, device="cuda")
+    C = X[torch.randperm(N, generator=g, device="cuda")[:k]].double() + 0.01
+    xa = cluster_ops.abs_bound(X)
+    monkeypatch.setenv("H2O3_KM_SPLIT", "1")
+    a = torch.full((N,), -1, dtype=torch.int32, device="cuda")
+    st = cluster_ops.lloyd_pass(X, C, None, a, xabs_max=xa)
+    monkeypatch.setenv("H2O3_KM_ASSIGN", "lloyd")
+    a_ref = torch.full((N,), -1, dtype=torch.int32, device="cuda")
+    cluster_ops.lloyd_pass(X, C, None, a_ref, xabs_max=xa)
+    torch.cuda.synchronize()
+    assert bool((a == a_ref).all())
+    Xd = X.double()
+    D = (Xd * Xd).sum(1, keepdim=True) - 2 * Xd @ C.T + (C * C).sum(1).view(1, -1)
+    gap = D.topk(2, dim=1, largest=False).values
+    clear = (gap[:, 1] - gap[:, 0]) > 1e-3 * (1 + gap[:, 0].abs())
+    assert bool((a.long()[clear] == D.argmin(1)[clear]).all())
+    oh = torch.zeros((N, k), dtype=torch.float64, device="cuda")
+    oh[torch.arange(N, device="cuda"), a.long()] = 1.0
+    torch.testing.assert_close(st.sums, oh.T @ Xd, rtol=2e-5, atol=2e-3)
+    torch.testing.assert_close(st.weights, oh.sum(0), rtol=0, atol=0)
+    assert float(st.changed) == N
+
+
+@pytest.mark.gpu
 def test_kmeans_estimator_gpu_uses_kernel():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")

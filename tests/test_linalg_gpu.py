@@ -569,3 +569,53 @@ def test_glm_wide_lambda_max_and_deviance_kernel_match_torch(family, monkeypatch
     lm_t, dv_t = drv._lambda_max(), drv.deviance(beta)
     assert lm_k == pytest.approx(lm_t, rel=1e-5)
     assert dv_k == pytest.approx(dv_t, rel=1e-5)
+
+
+@pytest.mark.parametrize("method", ["Randomized", "Power", "GramSVD"])
+def test_pca_methods_on_gram_kernel_match_fp64(method):
+    """PCA Power / Randomized iterate on the covariance from ONE pass of the
+    hand-written Gram kernel (no per-iteration pass over X, no library GEMM),
+    and the projections run on the skinny MFMA kernel (cluster_ops.xv): the
+    eigenvalues / eigenvectors match an fp64 eigendecomposition and the
+    projections an fp64 product."""
+    import numpy as np
+    import h2o3_amd
+    from h2o3_amd.core.frame import H2OFrame
+    from h2o3_amd.models.clustering import H2OPrincipalComponentAnalysisEstimator
+    from h2o3_amd.ops import _native, cluster_ops
+    h2o3_amd.init(verbose=False)
+    g = np.random.default_rng(3)
+    n, P, k = 300_000, 100, 10
+    scales = np.linspace(3.0, 0.5, P)
+    Xh = (g.standard_normal((n, P)) * scales).astype(np.float32)
+    fr = H2OFrame({f"x{j}": Xh[:, j] for j in range(P)})
+    m = H2OPrincipalComponentAnalysisEstimator(k=k, pca_method=method, transform="NONE", max_iterations=300, seed=1)
+    m.train(training_frame=fr)
+    Xd = torch.as_tensor(Xh, dtype=torch.float64)
+    mu = Xd.mean(0)
+    cov = (Xd - mu).T @ (Xd - mu) / (n - 1)
+    ev, V = torch.linalg.eigh(cov)
+    order = torch.argsort(ev, descending=True)[:k]
+    ev, V = ev[order], V[:, order]
+    sd = np.asarray(m._output["std_deviation"])
+    np.testing.assert_allclose(sd, np.sqrt(ev.numpy()), rtol=1e-6)
+    E = np.asarray(m._output["eigenvectors"])
+    # eigenvectors up to sign
+    cosv = np.abs((E * V.numpy()).sum(0))
+    assert cosv.min() > 1 - 1e-6, cosv
+    Z = m.predict(fr).as_data_frame().values
+    Zref = ((Xd - mu) @ torch.as_tensor(E)).numpy()
+    np.testing.assert_allclose(Z, Zref, rtol=1e-4, atol=1e-4 * np.abs(Zref).max())
+    assert "libkmeans.so" in " ".join(_native.loaded_libs()) and "libgram.so" in " ".join(_native.loaded_libs())
+
+
+def test_xv_kernel_matches_fp64():
+    from h2o3_amd.ops import cluster_ops
+    g = torch.Generator(device="cuda").manual_seed(4)
+    for N, W, k in ((100_003, 100, 10), (70_000, 36, 40), (65_536, 256, 3), (80_000, 8, 17)):
+        X = torch.randn((N, W), generator=g, device="cuda")
+        V = torch.randn((W, k), generator=g, device="cuda", dtype=torch.float64)
+        out = cluster_ops.xv(X, V)
+        assert out.dtype == torch.float32 and out.shape == (N, k)
+        ref = X.double() @ V
+        torch.testing.assert_close(out.double(), ref, rtol=1e-4, atol=1e-4 * float(ref.abs().max()))
