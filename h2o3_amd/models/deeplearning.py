@@ -203,14 +203,14 @@ class H2ODeepLearningEstimator(H2OEstimator):
                            seed_dev=seed_dev)
         acts, zs = [A], []
         for li, L in enumerate(self._layers[:-1]):
-            Z = A @ L.W.t()
+            Z = dl_ops.gemm(A, L.W.t())
             Ah = dl_ops.fwd(Z, L.b, L.act, L.drop, seed=seed + 7919 * (li + 1), train=train,
                             test_scale=1.0 - L.drop, seed_dev=seed_dev)
             zs.append(Z)
             acts.append(Ah)
             A = Ah
         Lo = self._layers[-1]
-        Zo = A @ Lo.W.t()
+        Zo = dl_ops.gemm(A, Lo.W.t())
         zs.append(Zo)
         return acts, zs
 
@@ -650,10 +650,10 @@ class H2ODeepLearningEstimator(H2OEstimator):
             L = self._layers[li]
             if li == len(self._layers) - 1:
                 db = dZ.sum(0)
-            dW = dZ.t() @ acts[li]
+            dW = dl_ops.gemm(dZ.t(), acts[li])
             grads.append((li, dW, db))
             if li > 0:
-                dA = dZ @ L.W
+                dA = dl_ops.gemm(dZ, L.W)
                 Lp = self._layers[li - 1]
                 dZ, db = dl_ops.bwd(dA, acts[li], zs[li - 1], Lp.act, Lp.drop, seed=step_seed + 7919 * li,
                                     seed_dev=seed_dev)

@@ -879,3 +879,106 @@ int h2o_dl_mlp_step(int nl, const int* width, const int* act, const float* drop,
 
 }  // extern "C"
 
+
+// ---------------------------------------------------------------------------
+// Tiled f32-MFMA GEMM for the layers the LDS-resident fused step does not
+// cover (wide hidden layers, maxout, autoencoders): C[M][N] = opA . opB with
+// opA(m, k) = A[m * sam + k * sak] and opB(k, n) = B[k * sbk + n * sbn], so
+// the three products of a training step -- Z = A W^T, dA = dZ W, dW = dZ^T A
+// -- are one kernel with different strides (no library GEMM).  A 256-thread
+// workgroup owns a 64 x 64 tile of C; each of its 4 waves a 32 x 32 quarter
+// (2 x 2 blocks of v_mfma_f32_16x16x4f32: exact f32 products, f32
+// accumulation like an f32 BLAS GEMM).  K advances in 32-wide slabs staged
+// through LDS (double buffered: the next slab's global loads are in flight
+// during the current slab's MFMAs); the loader walks the contiguous
+// dimension of each operand so the global loads coalesce for every
+// transpose.  Blocks are mapped XCD-aware.
+// ---------------------------------------------------------------------------
+#define DLG_TM 64
+#define DLG_TN 64
+#define DLG_TK 32
+__global__ __launch_bounds__(256) void dl_gemm_kernel(int M, int N, int K, const float* __restrict__ A, long long sam,
+                                                      long long sak, const float* __restrict__ B, long long sbk,
+                                                      long long sbn, float* __restrict__ C, int ntn) {
+  __shared__ float As[2][DLG_TM][DLG_TK + 1];   // [m][k]
+  __shared__ float Bs[2][DLG_TK][DLG_TN + 1];   // [k][n]
+  const int nwg = gridDim.x;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int tm = bid / ntn, tn = bid - (bid / ntn) * ntn;
+  const int m0 = tm * DLG_TM, n0 = tn * DLG_TN;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wm = (wv >> 1) * 32, wn = (wv & 1) * 32;
+  const bool a_kfast = sak == 1, b_nfast = sbn == 1;
+  // each thread stages 8 elements of each operand per slab (64 x 32 = 2048)
+  float ra[8], rb[8];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = tid + u * 256;
+      int m, k;
+      if (a_kfast) { m = e >> 5; k = e & 31; } else { k = e >> 6; m = e & 63; }
+      const int gm = m0 + m, gk = k0 + k;
+      ra[u] = (gm < M && gk < K) ? A[(long long)gm * sam + (long long)gk * sak] : 0.f;
+      int kb, n;
+      if (b_nfast) { kb = e >> 6; n = e & 63; } else { n = e >> 5; kb = e & 31; }
+      const int gk2 = k0 + kb, gn = n0 + n;
+      rb[u] = (gk2 < K && gn < N) ? B[(long long)gk2 * sbk + (long long)gn * sbn] : 0.f;
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = tid + u * 256;
+      if (a_kfast) As[buf][e >> 5][e & 31] = ra[u];
+      else As[buf][e & 63][e >> 6] = ra[u];
+      if (b_nfast) Bs[buf][e >> 6][e & 63] = rb[u];
+      else Bs[buf][e & 31][e >> 5] = rb[u];
+    }
+  };
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  f4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = (f4){0.f, 0.f, 0.f, 0.f};
+  const int nslab = (K + DLG_TK - 1) / DLG_TK;
+  if (nslab > 0) {
+    load(0);
+    store(0);
+  }
+  __syncthreads();
+  const int li = lane & 15, lg = lane >> 4;
+  for (int s = 0; s < nslab; ++s) {
+    const int cur = s & 1;
+    if (s + 1 < nslab) load((s + 1) * DLG_TK);
+#pragma unroll
+    for (int kk = 0; kk < DLG_TK; kk += 4) {
+      float a0 = As[cur][wm + li][kk + lg], a1 = As[cur][wm + 16 + li][kk + lg];
+      float b0 = Bs[cur][kk + lg][wn + li], b1 = Bs[cur][kk + lg][wn + 16 + li];
+      acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, acc[1][1], 0, 0, 0);
+    }
+    if (s + 1 < nslab) store(cur ^ 1);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int gm = m0 + wm + 16 * i + 4 * lg + r, gn = n0 + wn + 16 * j + li;
+        if (gm < M && gn < N) C[(long long)gm * N + gn] = acc[i][j][r];
+      }
+}
+
+extern "C" int h2o_dl_gemm(int M, int N, int K, const float* A, long long sam, long long sak, const float* B,
+                           long long sbk, long long sbn, float* C, hipStream_t s) {
+  if (M <= 0 || N <= 0) return 0;
+  if (K < 0 || !A || !B || !C) return (int)hipErrorInvalidValue;
+  const int ntm = (M + DLG_TM - 1) / DLG_TM, ntn = (N + DLG_TN - 1) / DLG_TN;
+  hipLaunchKernelGGL(dl_gemm_kernel, dim3(ntm * ntn), dim3(256), 0, s, M, N, K, A, sam, sak, B, sbk, sbn, C, ntn);
+  H2O_CHECK_LAUNCH();
+}

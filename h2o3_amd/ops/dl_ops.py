@@ -34,6 +34,8 @@ def _lib():
         lib.h2o_dl_softmax.argtypes = [_cv] * 7 + [_ci, _ci, _cf, _ci, _cv]
         lib.h2o_dl_mlp_step.argtypes = [_ci] + [_cv] * 15 + [_ci] + [_cv] * 4 + [_ci, _ci, _cf, _cull, _cv, _ci,
                                                                             _cv]
+        lib.h2o_dl_gemm.argtypes = [_ci, _ci, _ci, _cv, ctypes.c_longlong, ctypes.c_longlong, _cv,
+                                    ctypes.c_longlong, ctypes.c_longlong, _cv, _cv]
         lib._typed = True
     return lib
 
@@ -342,3 +344,24 @@ def mlp_step(X, idx, y, w, layers, acts, drops, in_drop, out_kind, inv_n, ups, s
                              upc, _p(Xc), int(Xc.shape[1]), _p(idx), _p(ycls), _p(yreg), _p(w), B, int(out_kind),
                              float(inv_n), seed & _M, _p(seed_dev), int(bool(advance)), _s())
     _check(rc, "h2o_dl_mlp_step")
+
+
+# ---------------------------------------------------------------- GEMM
+def gemm(A, B, out=None):
+    """A @ B for 2-D f32 tensors (any strides: transposed views included) on
+    the hand-written MFMA tile kernel (dl.hip dl_gemm_kernel) on the GPU, a
+    torch matmul on the CPU.  The DL layers the fused step does not cover
+    (wide hidden layers, maxout, autoencoders) run their three products per
+    step -- Z = A W^T, dA = dZ W, dW = dZ^T A -- through it."""
+    import os
+    if A.device.type != "cuda" or A.dtype != torch.float32 or B.dtype != torch.float32 or \
+            os.environ.get("H2O3_DL_GEMM", "mfma") != "mfma":
+        return A @ B
+    M, K = A.shape
+    K2, N = B.shape
+    assert K == K2, (A.shape, B.shape)
+    C = out if out is not None else torch.empty((M, N), dtype=torch.float32, device=A.device)
+    lib = _lib()
+    _check(lib.h2o_dl_gemm(M, N, K, _p(A), A.stride(0), A.stride(1), _p(B), B.stride(0), B.stride(1), _p(C), _s()),
+           "h2o_dl_gemm")
+    return C

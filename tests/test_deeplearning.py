@@ -469,3 +469,72 @@ def test_dl_fused_step_matches_unfused(case):
     if not hp["ada"]:
         for x, y in zip(La, Lb):
             torch.testing.assert_close(x.state["mom"], y.state["mom"], rtol=2e-4, atol=2e-5)
+
+
+@pytest.mark.gpu
+def test_dl_gemm_kernel_matches_fp64():
+    """dl.hip dl_gemm_kernel (f32 MFMA tiles, any strides) against an fp64
+    product, for the three per-step products and ragged shapes."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from h2o3_amd.ops import dl_ops
+    g = torch.Generator(device="cuda").manual_seed(3)
+    for M, K, N in ((1024, 1024, 1024), (333, 37, 19), (1, 5, 7), (1000, 100, 200), (64, 2000, 3)):
+        A = torch.randn((M, K), generator=g, device="cuda")
+        W = torch.randn((N, K), generator=g, device="cuda")
+        C = dl_ops.gemm(A, W.t())                       # Z = A W^T
+        torch.testing.assert_close(C.double(), A.double() @ W.double().t(), rtol=1e-4, atol=1e-4 * K ** 0.5)
+        dZ = torch.randn((M, N), generator=g, device="cuda")
+        dA = dl_ops.gemm(dZ, W)                          # dA = dZ W
+        torch.testing.assert_close(dA.double(), dZ.double() @ W.double(), rtol=1e-4, atol=1e-4 * N ** 0.5)
+        dW = dl_ops.gemm(dZ.t(), A)                      # dW = dZ^T A
+        torch.testing.assert_close(dW.double(), dZ.double().t() @ A.double(), rtol=1e-4, atol=1e-4 * M ** 0.5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["wide1024", "maxout", "autoencoder"])
+def test_dl_wide_layers_on_mfma_gemm(monkeypatch, case):
+    """Networks beyond the LDS-resident fused step (hidden=[1024, 1024],
+    maxout, autoencoders) train through dl_gemm_kernel: the same weights /
+    ADADELTA state as the same steps with torch (library) matmuls."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import copy
+    from h2o3_amd.ops import dl_ops
+    g = torch.Generator(device="cuda").manual_seed(21)
+    P, B = 100, 512
+    X = torch.randn((3000, P), generator=g, device="cuda")
+    if case == "wide1024":
+        mk = lambda: H2ODeepLearningEstimator(hidden=[1024, 1024], activation="RectifierWithDropout", seed=1)
+        K, ae = 2, False
+    elif case == "maxout":
+        mk = lambda: H2ODeepLearningEstimator(hidden=[200, 100], activation="Maxout", seed=2)
+        K, ae = 3, False
+    else:
+        mk = lambda: H2ODeepLearningEstimator(hidden=[300, 20, 300], activation="Tanh", seed=3, autoencoder=True)
+        K, ae = P, True
+    Y = torch.randint(0, max(K, 2), (3000,), generator=g, device="cuda") if not ae else None
+    hp = dict(K=K if not ae else P, ae=ae, bs=B, ada=True, rate0=0.005, anneal=1e-6, decay=1.0, mom_start=0.0,
+              mom_ramp=1e6, mom_stable=0.0, has_mom=False, l1=0.0, l2=0.0, max_w2=3.4e38, sparsity=0.0)
+    from h2o3_amd.models.distributions import get_distribution
+    nets = []
+    for mode in ("mfma", "torch"):
+        monkeypatch.setenv("H2O3_DL_GEMM", mode)
+        m = mk()
+        m._layers = m._build(P, hp["K"], (K > 1) and not ae)
+        m._processed = 0.0
+        m._dist = get_distribution("AUTO" if (K > 1 and not ae) else "gaussian", K)
+        assert m._fused_kind(hp, None) is None
+        gg = torch.Generator(device="cuda").manual_seed(5)
+        for t in range(3):
+            idx = torch.randint(0, 3000, (B,), generator=gg, device="cuda")
+            m._train_step(X.index_select(0, idx), X.index_select(0, idx) if ae else Y.index_select(0, idx), None,
+                          500 + t, hp)
+        nets.append(m._layers)
+    for x, y in zip(nets[0], nets[1]):
+        for ta, tb in ((x.W, y.W), (x.b, y.b), (x.state["ada"], y.state["ada"])):
+            # f32 sums in another order; the first ADADELTA steps move a weight by
+            # ~sign(g) sqrt(eps / (1 - rho)), so gradients within rounding of 0 may
+            # flip: allow a few per million
+            bad = ((ta - tb).abs() > 2e-5 + 2e-4 * tb.abs()).sum().item()
+            assert bad <= max(2, int(2e-5 * ta.numel())), (bad, ta.numel(), (ta - tb).abs().max().item())
