@@ -110,6 +110,9 @@ def main():
     ap.add_argument("--algo", default="gbm", choices=["gbm", "glm", "drf", "kmeans", "dl", "pca"])
     ap.add_argument("--hidden", default="200,200", help="DL hidden layers (--algo dl)")
     ap.add_argument("--batch", type=int, default=1024, help="DL mini-batch rows (--algo dl)")
+    ap.add_argument("--glm-lambda", type=float, default=0.0,
+                    help="GLM lambda (--algo glm); > 0 with --glm-alpha > 0 measures the l1 (COD) path")
+    ap.add_argument("--glm-alpha", type=float, default=0.5, help="GLM elastic-net alpha (used when lambda > 0)")
     ap.add_argument("--k", type=int, default=16, help="K-Means clusters (--algo kmeans)")
     ap.add_argument("--cat-cols", type=int, default=0,
                     help="replace this many of the --cols columns by categoricals (DRF config: mixed num/cat)")
@@ -202,19 +205,17 @@ def main():
         from h2o3_amd.models.clustering import _top_eig
         from h2o3_amd.ops import cluster_ops, linalg_ops
         from h2o3_amd.parallel import collectives as coll
-        di = DataInfo(fr, names, standardize=False, use_all_factor_levels=True, pad_to=4)
+        from h2o3_amd.models.clustering import gram_and_mean
+        # pad_to=32 as the PCA model's expansion (clustering._transform_info):
+        # the Gram kernel's column tiling; one padding column carries the 1s
+        di = DataInfo(fr, names, standardize=False, use_all_factor_levels=True, pad_to=32)
         Xp, _ = di.expand(fr)
         del fr
         P = di.P
-        nrow = coll.allreduce_scalar(float(Xp.shape[0]))
         kk = args.k
 
         def step():
-            G = linalg_ops.weighted_gram(Xp)[:P, :P]
-            coll.allreduce_(G)
-            mu = Xp[:, :P].to(torch.float64).sum(0)
-            coll.allreduce_(mu)
-            mu = mu / nrow
+            G, mu, nrow = gram_and_mean(Xp, P)
             cov = (G - nrow * torch.outer(mu, mu)) / max(nrow - 1, 1)
             ev, V = _top_eig(cov, kk, "randomized", 30, 1)
             Vp = torch.zeros((Xp.shape[1], V.shape[1]), dtype=torch.float64)
@@ -257,15 +258,20 @@ def main():
         extra_cfg = {"hidden": hidden, "batch": args.batch, "hip_graph": gstep is not None}
     else:
         from h2o3_amd.models.glm.glm import GLMDriver, H2OGeneralizedLinearEstimator
-        est = H2OGeneralizedLinearEstimator(family="binomial", solver="IRLSM", lambda_=0.0)
+        kw = {"lambda_": args.glm_lambda}
+        if args.glm_lambda > 0:
+            kw["alpha"] = args.glm_alpha
+        est = H2OGeneralizedLinearEstimator(family="binomial", solver="IRLSM", **kw)
         spec = TrainSpec(fr, names, "y")
         est._spec = spec
         drv = GLMDriver(est, spec)
         step = drv.step
         metric = "glm_iters_per_sec"
         unit = "iters/s"
-        model = f"GLM binomial IRLSM {args.rows / 1e6:g}Mx{F}"
-        extra_cfg = {"gram_precision": _GLM_PRECISION}
+        model = f"GLM binomial IRLSM {args.rows / 1e6:g}Mx{F}" + \
+            (f" lambda={args.glm_lambda:g} alpha={args.glm_alpha:g}" if args.glm_lambda > 0 else "")
+        extra_cfg = {"gram_precision": _GLM_PRECISION, "lambda": args.glm_lambda,
+                     "alpha": args.glm_alpha if args.glm_lambda > 0 else None}
 
     def sync():
         torch.cuda.synchronize() if dev.type == "cuda" else None

@@ -422,8 +422,12 @@ class H2OEstimator:
         max_rt = float(p.get("max_runtime_secs") or 0)
         self._deadline = t0 + max_rt if max_rt > 0 else None
         try:
-            if self.supervised_learning and (nfolds > 1 or p.get("fold_column")):
-                self._cross_validate(spec)
+            if nfolds > 1 or p.get("fold_column"):
+                if self.supervised_learning:
+                    self._cross_validate(spec)
+                elif hasattr(self, "_cross_validate_unsup"):
+                    # clustering CV (KMeans): holdout metrics without labels
+                    self._cross_validate_unsup(spec)
             if self._deadline is not None:
                 p["max_runtime_secs"] = max(1e-3, self._deadline - time.time())
             try:
@@ -541,19 +545,7 @@ class H2OEstimator:
         for i in range(k):
             tr_mask = folds != i
             te_mask = folds == i
-            sub = copy.copy(self)
-            sub.__dict__ = dict(self.__dict__)
-            sub._parms = dict(self._parms)
-            sub._parms["nfolds"] = 0
-            sub._parms["fold_column"] = None
-            dl = getattr(self, "_deadline", None)
-            if dl is not None:
-                # fold i gets an equal share of what is left for the k - i folds and the main model
-                sub._parms["max_runtime_secs"] = max(1e-3, (dl - time.time()) / (k - i + 1))
-            sub._id = f"{self._id}_cv_{i + 1}"
-            sub._cv_models = []
-            sub._scoring_history = []
-            sub._output = {}
+            sub = self._cv_sub(i, k)
             tr = fr[tr_mask]
             te = fr[te_mask]
             sspec = TrainSpec(tr, spec.x, spec.y, spec.weights_column, spec.offset_column, None, te)
@@ -584,6 +576,24 @@ class H2OEstimator:
         self._output["cross_validation_metrics_summary"] = {
             kk: {"mean": float(np.mean(v)), "sd": float(np.std(v, ddof=1)) if len(v) > 1 else 0.0, "values": v}
             for kk, v in rows.items()}
+
+    def _cv_sub(self, i, k):
+        """Fold model i of k: a copy of this builder with its own id, output
+        and scoring history, nfolds off, and an equal share of what is left of
+        max_runtime_secs for the k - i folds and the main model."""
+        sub = copy.copy(self)
+        sub.__dict__ = dict(self.__dict__)
+        sub._parms = dict(self._parms)
+        sub._parms["nfolds"] = 0
+        sub._parms["fold_column"] = None
+        dl = getattr(self, "_deadline", None)
+        if dl is not None:
+            sub._parms["max_runtime_secs"] = max(1e-3, (dl - time.time()) / (k - i + 1))
+        sub._id = f"{self._id}_cv_{i + 1}"
+        sub._cv_models = []
+        sub._scoring_history = []
+        sub._output = {}
+        return sub
 
     def _cv_optimal_params(self, cv_models):
         """Hook: adopt CV-derived parameters for the main model

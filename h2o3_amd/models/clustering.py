@@ -101,6 +101,27 @@ def _top_eig(G, k, method, iters, seed):
     return lam[order], V[:, order]
 
 
+def gram_and_mean(X, P):
+    """(X'X [P,P], column means [P], row count) of the model matrix, all-reduced,
+    from ONE pass of the Gram kernel: when the expansion left a padding column
+    (pad_to=32), it is set to 1 so that the same pass yields the column sums
+    (G[P, :P]) and the row count (G[P, P]) -- no f64 copy of X for the mean.
+    X's padding columns carry no model weight (every projection zeroes rows >=
+    P of V), so the 1s stay."""
+    if X.shape[1] > P and X.device.type == "cuda":
+        X[:, P] = 1.0
+        G = linalg_ops.weighted_gram(X)[:P + 1, :P + 1]
+        coll.allreduce_(G)
+        n = float(G[P, P])
+        return G[:P, :P].contiguous(), G[P, :P] / max(n, 1.0), n
+    G = linalg_ops.weighted_gram(X)[:P, :P]
+    coll.allreduce_(G)
+    s = X[:, :P].sum(0, dtype=torch.float64)
+    coll.allreduce_(s)
+    n = coll.allreduce_scalar(float(X.shape[0]))
+    return G, s / max(n, 1.0), n
+
+
 PCA_DEFAULTS = dict(transform="none", k=1, max_iterations=1000, seed=-1, use_all_factor_levels=False,
                     compute_metrics=True, impute_missing=False, pca_method="GramSVD", pca_impl="mtj_evd_symmmatrix",
                     max_runtime_secs=0.0, export_checkpoints_dir=None)
@@ -117,17 +138,13 @@ class H2OPrincipalComponentAnalysisEstimator(H2OEstimator):
                              mvh="MeanImputation" if p.get("impute_missing") else "Skip")
         self._dinfo = di
         X, ok = di.expand(spec.frame)
-        X = X[ok]          # impute_missing=False: rows with an NA are skipped (PCA.java)
-        n = coll.allreduce_scalar(float(X.shape[0]))
+        if not bool(ok.all()):
+            X = X[ok]      # impute_missing=False: rows with an NA are skipped (PCA.java)
         k = int(p.get("k", 1))
         method = (p.get("pca_method") or "GramSVD").lower()
         P = di.P
+        G, mean, n = gram_and_mean(X, P)
         if method in ("gramsvd", "glrm"):
-            G = linalg_ops.weighted_gram(X)[:P, :P]
-            coll.allreduce_(G)
-            mean = X[:, :P].to(torch.float64).sum(0)
-            coll.allreduce_(mean)
-            mean = mean / n
             if not di.standardize:
                 # covariance about the mean (reference demeans via the Gram's intercept row)
                 G = G - n * torch.outer(mean, mean)
@@ -147,11 +164,6 @@ class H2OPrincipalComponentAnalysisEstimator(H2OEstimator):
             # weighted_gram, f64 across row blocks); the centred cross-product
             # Xc'(Xc Q) of every subspace / power iteration is (G - n mu mu') Q,
             # so the iterations run on the P x P matrix and never re-read X
-            G = linalg_ops.weighted_gram(X)[:P, :P]
-            coll.allreduce_(G)
-            mean = X[:, :P].to(torch.float64).sum(0)
-            coll.allreduce_(mean)
-            mean = mean / n
             if not di.standardize:
                 G = G - n * torch.outer(mean, mean)
             cov = G / max(n - 1, 1)

@@ -277,6 +277,12 @@ class H2OKMeansEstimator(H2OEstimator):
         if not bool(ok.all()):
             X = X[ok]
         w = spec.w_tensor()
+        fw = self.__dict__.get("_fold_w")
+        if fw is not None:
+            # CV fold model: holdout rows carry weight 0 (the reference trains
+            # fold models on the whole frame with a fold-weight column, so the
+            # standardization is the full frame's)
+            w = fw.to(torch.float32) if w is None else w * fw.to(w.dtype)
         w = None if w is None else w[ok]
         _, nrows_tot = self._offsets(X.shape[0])
         rng = np.random.RandomState(_seed(p))
@@ -437,6 +443,71 @@ class H2OKMeansEstimator(H2OEstimator):
         if spec.valid is not None:
             self._validation_metrics = self._unsupervised_perf(spec.valid)
 
+    def _cross_validate_unsup(self, spec):
+        """N-fold CV of a clustering model (ModelBuilder CV +
+        ModelMetricsClustering.MetricBuilderClustering.reduceForCV): fold model
+        i trains on the whole frame with fold i's rows at weight 0, scores
+        its holdout rows; the CV metrics pool the holdout rows' within-cluster
+        squared distances (tot_withinss) and their per-column sums / sums of
+        squares (totss about the pooled mean, x != mode counts for the
+        categorical columns); no per-cluster size / withinss (cluster ids of
+        different fold models do not line up)."""
+        folds, k = self._fold_ids(spec)
+        self._cv_fold_assignment = folds
+        fr = spec.frame
+        cv_models = []
+        acc = None
+        for i in range(k):
+            sub = self._cv_sub(i, k)
+            sub._fold_w = folds != i
+            sub._fit(spec)
+            sub._score_all(spec)
+            sub._fold_w = None
+            te_mask = folds == i
+            X, ok = sub._design(fr[te_mask])
+            if not bool(ok.all()):
+                X = X[ok]
+            sub._validation_metrics = sub._cluster_metrics(X, None)
+            di = sub._dinfo
+            nc = di.n_cat_expanded
+            Xn = X[:, nc:di.P].to(torch.float64)
+            mis = torch.zeros(1, dtype=torch.float64, device=X.device)
+            for c in di.cat_cols:
+                mis += (X[:, di.cat_offsets[c] + di.cat_modes[c]] == 0).sum().to(torch.float64)
+            v = torch.cat([Xn.sum(0), (Xn * Xn).sum(0), mis,
+                           torch.tensor([float(X.shape[0])], dtype=torch.float64, device=X.device)])
+            coll.allreduce_(v)
+            acc = v if acc is None else acc + v
+            acc_tw = float(sub._validation_metrics.tot_withinss())
+            sub._cv_tw = acc_tw
+            cv_models.append(sub)
+        tw = float(sum(m._cv_tw for m in cv_models))
+        nn = (acc.numel() - 2) // 2
+        cs, css, mis, cnt = acc[:nn], acc[nn:2 * nn], float(acc[2 * nn]), float(acc[2 * nn + 1])
+        nrows = float(fr.nrows) if spec.weights_column is None else cnt
+        if int(self._parms.get("k", 1)) == 1:
+            totss = tw
+        else:
+            totss = float((css - cs * cs / max(nrows, 1.0)).sum()) + mis
+        self._cross_validation_metrics = mm.ModelMetricsClustering(tot_withinss=tw, totss=totss,
+                                                                   betweenss=totss - tw, nobs=int(cnt))
+        self._cv_models = cv_models if self._parms.get("keep_cross_validation_models", True) else []
+        rows = {}
+        for m in cv_models:
+            for kk, vv in m._validation_metrics._m.items():
+                if isinstance(vv, (int, float)) and not isinstance(vv, bool):
+                    rows.setdefault(kk, []).append(vv)
+        self._output["cross_validation_metrics_summary"] = {
+            kk: {"mean": float(np.mean(v)), "sd": float(np.std(v, ddof=1)) if len(v) > 1 else 0.0, "values": v}
+            for kk, v in rows.items()}
+
+    def _mt(self, train=False, valid=False, xval=False):
+        if xval:
+            return self._cross_validation_metrics
+        if valid:
+            return self._validation_metrics
+        return self._training_metrics
+
     def _unsupervised_perf(self, frame):
         X, ok = self._design(frame)
         if not bool(ok.all()):
@@ -454,16 +525,16 @@ class H2OKMeansEstimator(H2OEstimator):
         return self._training_metrics.get("size")
 
     def tot_withinss(self, train=False, valid=False, xval=False):
-        return self._training_metrics.tot_withinss()
+        return self._mt(train, valid, xval).tot_withinss()
 
     def betweenss(self, train=False, valid=False, xval=False):
-        return self._training_metrics.betweenss()
+        return self._mt(train, valid, xval).betweenss()
 
     def totss(self, train=False, valid=False, xval=False):
-        return self._training_metrics.totss()
+        return self._mt(train, valid, xval).totss()
 
     def withinss(self, train=False, valid=False, xval=False):
-        return self._training_metrics.withinss()
+        return self._mt(train, valid, xval).withinss()
 
     def centroid_stats(self, train=False, valid=False):
         """Per-cluster (centroid, size, within_cluster_sum_of_squares) table of

@@ -546,6 +546,8 @@ class TreeGrower:
         if ht == "uniformadaptive" and nb >= B:
             return H
         dev = H.device
+        if ht == "uniformadaptive" and dev.type == "cuda" and C <= 4 and tree_ops.env("H2O3_UA_FOLD") != "torch":
+            return self._adapt_hist_dev(H, Fl, n, Bs, C, nb, isnum, depth)
         Hn = H[:, :, :B]
         occ = (Hn != 0).any(-1)                                   # [Fl, n, B]
         idx = torch.arange(B, device=dev)
@@ -588,6 +590,42 @@ class TreeGrower:
         Hf = torch.where(is_end.unsqueeze(-1), cs - base, torch.zeros_like(cs)).to(H.dtype)
         Hf = torch.where(isnum.view(Fl, 1, 1, 1), Hf, Hn)
         return torch.cat([Hf, H[:, :, B:]], 2).contiguous()
+
+    def _adapt_hist_dev(self, H, Fl, n, Bs, C, nb, isnum, depth):
+        """UniformAdaptive fold on the device (tree_split.hip ua_range_kernel /
+        ua_fold_kernel): the same first / last, parent-range rule and run-end
+        folding as the torch chain of _adapt_hist, one wave per (feature,
+        node) row, H read twice and written once."""
+        import ctypes
+        from ...ops import _native
+        lib = _native.get_lib("tree_split")
+        if lib is None:
+            raise RuntimeError("tree_split native library missing (UniformAdaptive fold)")
+        if not getattr(lib, "_typed_ua", False):
+            cv, ci = ctypes.c_void_p, ctypes.c_int
+            lib.h2o_ua_range.argtypes = [cv, ci, ci, ci, cv, cv, cv]
+            lib.h2o_ua_fold.argtypes = [cv, ci, ci, ci, ci, cv, cv, ci, cv, cv, cv]
+            lib._typed_ua = True
+        H = H.contiguous()
+        rows = Fl * n
+        fl = torch.empty(2 * rows, dtype=torch.int32, device=H.device)
+        s = tree_ops._stream()
+        rc = lib.h2o_ua_range(ctypes.c_void_p(H.data_ptr()), rows, Bs, C, ctypes.c_void_p(fl.data_ptr()),
+                              ctypes.c_void_p(fl.data_ptr() + 4 * rows), s)
+        if rc != 0:
+            raise RuntimeError(f"h2o_ua_range failed: {rc}")
+        first, last = fl[:rows].view(Fl, n, 1).long(), fl[rows:].view(Fl, n, 1).long()
+        first, last = self._adapt_range(first, last, n, Fl, depth)
+        fr_ = first.to(torch.int32).contiguous()
+        la_ = last.to(torch.int32).contiguous()
+        isn = isnum.to(torch.uint8).contiguous()
+        out = torch.empty_like(H)
+        rc = lib.h2o_ua_fold(ctypes.c_void_p(H.data_ptr()), Fl, n, Bs, C, ctypes.c_void_p(fr_.data_ptr()),
+                             ctypes.c_void_p(la_.data_ptr()), int(nb), ctypes.c_void_p(isn.data_ptr()),
+                             ctypes.c_void_p(out.data_ptr()), s)
+        if rc != 0:
+            raise RuntimeError(f"h2o_ua_fold failed: {rc}")
+        return out
 
     def _adapt_range(self, first, last, n, Fl, depth):
         """Code range [first, last] ([Fl, n, 1]) each node's coarse bins span.

@@ -382,21 +382,27 @@ __global__ __launch_bounds__(256) void kmeans_assign_kernel(const float* __restr
 #pragma unroll
     for (int q = 0; q < KT; ++q) acc[q] = (f32x4){0.f, 0.f, 0.f, 0.f};
     float sq = 0.f;
+    // Branch-free step loop: steps v >= nv and tiles q >= nq multiply zeros
+    // (a4 is zero-filled by load(), b4 by the select), so the accumulators
+    // never flow through control-flow joins -- with per-step `if`s the
+    // compiler shuffles the KT accumulators between AGPRs and VGPRs at every
+    // join (30k v_accvgpr moves, 412-444 VGPRs at KT = 8).  The dispatcher
+    // picks KT / MAXNV close to nq / nv, so the padding MFMAs are few.
 #pragma unroll
     for (int v = 0; v < MAXNV; ++v) {
-      if (v < nv) {
-        const f32x4 a4 = A[v];
-        sq += a4[0] * a4[0] + a4[1] * a4[1] + a4[2] * a4[2] + a4[3] * a4[3];
-        f32x4 b4[KT];
+      const f32x4 a4 = A[v];
+      sq += a4[0] * a4[0] + a4[1] * a4[1] + a4[2] * a4[2] + a4[3] * a4[3];
+      const bool vin = v < nv;
+      f32x4 b4[KT];
 #pragma unroll
-        for (int q = 0; q < KT; ++q)
-          b4[q] = q < nq ? *(const f32x4*)(cb + q * 16 * S + 4 * v) : (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int q = 0; q < KT; ++q)
-            if (q < nq) acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[j], b4[q][j], acc[q], 0, 0, 0);
+      for (int q = 0; q < KT; ++q) {
+        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+        b4[q] = (vin && q < nq) ? *(const f32x4*)(cb + q * 16 * S + 4 * v) : z;
       }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int q = 0; q < KT; ++q) acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[j], b4[q][j], acc[q], 0, 0, 0);
     }
     sq += __shfl_xor(sq, 16, 64);
     sq += __shfl_xor(sq, 32, 64);            // |x|^2 of row li on every lane group
@@ -469,7 +475,9 @@ static int ka_launch(const float* X, long long N, int P, const float* C, const f
   const int nv = ((P + 15) & ~15) >> 4;      // float4 per lane = P16 / 16
   if (nv <= 2) return ka_launch2<KT, 2, MODE>(X, N, P, C, cn, k, assign, d2, G, s, per_cu_out);
   if (nv <= 4) return ka_launch2<KT, 4, MODE>(X, N, P, C, cn, k, assign, d2, G, s, per_cu_out);
+  if (nv <= 6) return ka_launch2<KT, 6, MODE>(X, N, P, C, cn, k, assign, d2, G, s, per_cu_out);
   if (nv <= 8) return ka_launch2<KT, 8, MODE>(X, N, P, C, cn, k, assign, d2, G, s, per_cu_out);
+  if (nv <= 12) return ka_launch2<KT, 12, MODE>(X, N, P, C, cn, k, assign, d2, G, s, per_cu_out);
   return ka_launch2<KT, 16, MODE>(X, N, P, C, cn, k, assign, d2, G, s, per_cu_out);
 }
 
@@ -483,7 +491,9 @@ static int ka_dispatch(const float* X, long long N, int P, const float* C, const
   if (kt <= 1 && MODE == 1) return ka_launch<1, MODE>(X, N, P, C, cn, k, assign, d2, G, s, per_cu_out);
   if (kt <= 2) return ka_launch<2, MODE>(X, N, P, C, cn, k, assign, d2, G, s, per_cu_out);
   if (kt <= 4) return ka_launch<4, MODE>(X, N, P, C, cn, k, assign, d2, G, s, per_cu_out);
+  if (kt <= 6) return ka_launch<6, MODE>(X, N, P, C, cn, k, assign, d2, G, s, per_cu_out);
   if (kt <= 8) return ka_launch<8, MODE>(X, N, P, C, cn, k, assign, d2, G, s, per_cu_out);
+  if (kt <= 12) return ka_launch<12, MODE>(X, N, P, C, cn, k, assign, d2, G, s, per_cu_out);
   return ka_launch<16, MODE>(X, N, P, C, cn, k, assign, d2, G, s, per_cu_out);
 }
 

@@ -830,3 +830,131 @@ extern "C" int h2o_pair_select2(const double* Hp, int n, int Bs, int kp, const d
   if (rc) return rc;
   return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------
+// UniformAdaptive per-node re-binning on the device (reference
+// DHistogram.java:366-386 / DTree.java:337: each (node, column) histogram is
+// re-binned into nb uniform bins over the column's range in that node).  The
+// level histogram H [Fl][n][Bs][C] (f64, Bs = B fine cells + the NA bin) is on
+// the fixed grid of nbins_top_level cells; a node's coarse bin is a run of
+// fine cells, and folding each run into its LAST cell keeps every cumulative
+// sum at an allowed boundary (any split search then only sees coarse
+// boundaries).  Two kernels, one 64-lane wave per (feature, node) row:
+//   ua_range: first / last occupied fine cell (any channel != 0), or (B, -1);
+//   ua_fold:  out[b] = sum of H over (previous end, b] at every run end b,
+//             0 elsewhere; categorical rows and the NA bin copied unchanged.
+// Lane l owns cells [l*cpl, (l+1)*cpl); the carry into a lane (the sum since
+// the last end before its first cell) is a segmented wave scan of the lanes'
+// tails.  Replaces the torch chain (occupancy, amin/amax, cumsum, cummax,
+// gather, where) on [Fl, n, B, C] f64 tensors of models/tree/engine.py.
+constexpr int UA_MAXC = 4;
+
+__global__ __launch_bounds__(256) void ua_range_kernel(const double* __restrict__ H, int rows, int Bs, int C,
+                                                       int* __restrict__ first, int* __restrict__ last) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const int B = Bs - 1;
+  const double* h = H + (long long)row * Bs * C;
+  int lo = B, hi = -1;
+  for (int b = lane; b < B; b += 64) {
+    bool occ = false;
+    for (int c = 0; c < C; ++c) occ |= h[(long long)b * C + c] != 0.0;
+    if (occ) { lo = min(lo, b); hi = max(hi, b); }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    lo = min(lo, __shfl_xor(lo, o, 64));
+    hi = max(hi, __shfl_xor(hi, o, 64));
+  }
+  if (lane == 0) { first[row] = lo; last[row] = hi; }
+}
+
+__global__ __launch_bounds__(256) void ua_fold_kernel(const double* __restrict__ H, int Fl, int n, int Bs, int C,
+                                                      const int* __restrict__ first, const int* __restrict__ last,
+                                                      int nb, const unsigned char* __restrict__ isnum,
+                                                      double* __restrict__ out) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= Fl * n) return;
+  const int f = row / n;
+  const int B = Bs - 1;
+  const double* h = H + (long long)row * Bs * C;
+  double* o = out + (long long)row * Bs * C;
+  if (!isnum[f]) {
+    for (int e = lane; e < Bs * C; e += 64) o[e] = h[e];
+    return;
+  }
+  for (int c = lane; c < C; c += 64) o[(long long)B * C + c] = h[(long long)B * C + c];   // NA bin
+  const long long fi = first[row], la = last[row];
+  const long long L = max(la - fi + 1, 1LL);
+  const bool narrow = L <= nb;
+  const int cpl = (B + 63) / 64;
+  const int b0 = lane * cpl, b1 = min(B, b0 + cpl);
+  auto is_end = [&](long long b) -> bool {
+    if (b < fi || b > la) return false;
+    if (narrow || b == la) return true;
+    const long long cur = ((b - fi) * nb) / L;
+    const long long nxt = ((b + 1 - fi) * nb) / L;
+    return cur != nxt;
+  };
+  // pass 1: this lane's tail (sum after its last end) and whether it has an end
+  double tail[UA_MAXC];
+  for (int c = 0; c < UA_MAXC; ++c) tail[c] = 0.0;
+  int has_end = 0;
+  for (int b = b0; b < b1; ++b) {
+    for (int c = 0; c < UA_MAXC; ++c)
+      if (c < C) tail[c] += h[(long long)b * C + c];
+    if (is_end(b)) {
+      has_end = 1;
+      for (int c = 0; c < UA_MAXC; ++c) tail[c] = 0.0;
+    }
+  }
+  // segmented inclusive scan over lanes: (f1, v1) + (f2, v2) = (f1 | f2, f2 ? v2 : v1 + v2)
+  int fl = has_end;
+  double v[UA_MAXC];
+  for (int c = 0; c < UA_MAXC; ++c) v[c] = tail[c];
+  for (int o = 1; o < 64; o <<= 1) {
+    const int pf = __shfl_up(fl, o, 64);
+    double pv[UA_MAXC];
+    for (int c = 0; c < UA_MAXC; ++c) pv[c] = __shfl_up(v[c], o, 64);
+    if (lane >= o) {
+      if (!fl)
+        for (int c = 0; c < UA_MAXC; ++c) v[c] += pv[c];
+      fl |= pf;
+    }
+  }
+  // carry into this lane = the previous lane's inclusive value
+  double run[UA_MAXC];
+  for (int c = 0; c < UA_MAXC; ++c) {
+    const double pv = __shfl_up(v[c], 1, 64);
+    run[c] = lane > 0 ? pv : 0.0;
+  }
+  // pass 2: write the folded cells
+  for (int b = b0; b < b1; ++b) {
+    const bool e = is_end(b);
+    for (int c = 0; c < UA_MAXC; ++c) {
+      if (c < C) {
+        run[c] += h[(long long)b * C + c];
+        o[(long long)b * C + c] = e ? run[c] : 0.0;
+        if (e) run[c] = 0.0;
+      }
+    }
+  }
+}
+
+extern "C" int h2o_ua_range(const double* H, int rows, int Bs, int C, int* first, int* last, hipStream_t s) {
+  if (rows <= 0) return 0;
+  if (Bs < 2 || C < 1) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(ua_range_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, H, rows, Bs, C, first, last);
+  return (int)hipGetLastError();
+}
+
+extern "C" int h2o_ua_fold(const double* H, int Fl, int n, int Bs, int C, const int* first, const int* last, int nb,
+                           const unsigned char* isnum, double* out, hipStream_t s) {
+  const int rows = Fl * n;
+  if (rows <= 0) return 0;
+  if (Bs < 2 || C < 1 || C > UA_MAXC || nb < 1) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(ua_fold_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, H, Fl, n, Bs, C, first, last, nb, isnum,
+                     out);
+  return (int)hipGetLastError();
+}

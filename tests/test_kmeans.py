@@ -2,6 +2,7 @@
 HIP Lloyd kernel (ops/csrc/kmeans.hip) against a float64 torch reference on
 the GPU."""
 import math
+import os
 
 import numpy as np
 import pandas as pd
@@ -340,7 +341,9 @@ def test_lloyd_split_path_matches_fused(N, P, k, monkeypatch):
         torch.cuda.synchronize()
         out[mode] = (a.clone(), dmin.clone(), st.vec.clone())
     assert bool((out["0"][0] == out["1"][0]).all())
-    assert bool((out["0"][1] == out["1"][1]).all())
+    # distances: same f32 terms, the wave kernel's interleaved MFMA chains may
+    # sum them in another order (last-ulp differences at small k)
+    torch.testing.assert_close(out["0"][1], out["1"][1], rtol=2e-6, atol=2e-6)
     assert float(out["1"][2][-1]) == float(out["0"][2][-1]) > 0
     # f64 statistics of the common assignment: the split path's fixed-point sums
     # are exact up to the f32 product w*x; the fused kernel at this k may hold
@@ -352,3 +355,32 @@ def test_lloyd_split_path_matches_fused(N, P, k, monkeypatch):
     torch.testing.assert_close(out["1"][2][:k * P], ref[:k * P], rtol=1e-6, atol=1e-4)
     torch.testing.assert_close(out["1"][2][k * P:m], ref[k * P:], rtol=1e-5, atol=1e-3)
     torch.testing.assert_close(out["0"][2][:k * P], ref[:k * P], rtol=2e-5, atol=2e-3)
+
+
+IRIS = "/root/reference/h2o-core/src/main/resources/extdata/iris.csv"
+
+
+@pytest.mark.skipif(not os.path.exists(IRIS), reason="reference extdata not present")
+def test_kmeans_nfolds_cv_metrics_iris():
+    """KMeans N-fold CV (hex/kmeans/KMeansTest.java:576-606 testNfolds): fold
+    models train on the whole frame with the holdout at weight 0 (full-frame
+    standardization), the CV metrics pool the holdout rows.  The reference's
+    CV totss 695.9999869341457 is pinned to its own tolerance (1e-4); its
+    tot_withinss / betweenss depend on the Java RNG's initial centers (its
+    main model lands on a worse optimum, 240.8 vs 158.8 here), so only the
+    identity betweenss = totss - tot_withinss and tot_withinss >= the main
+    model's training optimum's order are checked -- parity unpinned there."""
+    h2o3_amd.init(verbose=False)
+    fr = h2o3_amd.import_file(IRIS)
+    m = H2OKMeansEstimator(k=3, seed=0xdecaf, nfolds=3)
+    m.train(training_frame=fr)
+    assert m.totss(xval=True) == pytest.approx(695.9999869341457, abs=1e-4)
+    assert m.totss() == pytest.approx(695.9999869341457, abs=1e-4)
+    cv = m.model_performance(xval=True)
+    assert cv.betweenss() == pytest.approx(cv.totss() - cv.tot_withinss(), abs=1e-9)
+    assert 100 < cv.tot_withinss() < 400
+    assert len(m.cross_validation_models()) == 3
+    assert m._output["cross_validation_metrics_summary"]["tot_withinss"]["values"].__len__() == 3
+    # holdout within-SS of the folds add up to the CV tot_withinss
+    s = sum(cm._validation_metrics.tot_withinss() for cm in m.cross_validation_models())
+    assert cv.tot_withinss() == pytest.approx(s, rel=1e-12)

@@ -586,7 +586,10 @@ def test_pca_methods_on_gram_kernel_match_fp64(method):
     h2o3_amd.init(verbose=False)
     g = np.random.default_rng(3)
     n, P, k = 300_000, 100, 10
-    scales = np.linspace(3.0, 0.5, P)
+    # well-separated top-k spectrum (variance ratio 0.72 between neighbours and
+    # between the k-th and the bulk) so Power's per-vector iterations converge
+    # within max_iterations, as they would for the reference's PowerSVD
+    scales = np.concatenate([3.0 * 0.85 ** np.arange(k + 1), np.linspace(0.5, 0.2, P - k - 1)])
     Xh = (g.standard_normal((n, P)) * scales).astype(np.float32)
     fr = H2OFrame({f"x{j}": Xh[:, j] for j in range(P)})
     m = H2OPrincipalComponentAnalysisEstimator(k=k, pca_method=method, transform="NONE", max_iterations=300, seed=1)
