@@ -659,17 +659,24 @@ class H2OEstimator:
     def _score_unsupervised(self, spec):
         pass
 
+    def _label_threshold(self):
+        """Binomial labelling threshold (Model.defaultThreshold): max-F1 of the
+        validation metrics, else of the training metrics, else the output's
+        default_threshold (0.5)."""
+        vm, tm = self._validation_metrics, self._training_metrics
+        if vm is not None and vm.get("max_f1_threshold") is not None:
+            return float(vm["max_f1_threshold"])
+        if tm is not None and tm.get("max_f1_threshold") is not None:
+            return float(tm["max_f1_threshold"])
+        return float(self._output.get("default_threshold", 0.5))
+
     def _pred_frame_from_raw(self, raw, spec=None, threshold=None):
         spec = spec or self._spec
         if spec.nclasses == 2:
             p1 = raw[:, -1]
             thr = threshold if threshold is not None else getattr(self, "_threshold_override", None)
             if thr is None:
-                tm = self._training_metrics
-                thr = tm["max_f1_threshold"] if tm is not None and tm.get("max_f1_threshold") is not None else \
-                    float(self._output.get("default_threshold", 0.5))
-                if self._validation_metrics is not None and self._validation_metrics.get("max_f1_threshold") is not None:
-                    thr = self._validation_metrics["max_f1_threshold"]
+                thr = self._label_threshold()
             lab = (p1 >= thr).to(torch.int32)
             lab = torch.where(torch.isnan(p1), torch.full_like(lab, -1), lab)
             vecs = [Vec(lab, T_ENUM, spec.response_domain), Vec((1 - p1).to(torch.float32), T_REAL),

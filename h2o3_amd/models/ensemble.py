@@ -157,6 +157,14 @@ class H2OStackedEnsembleEstimator(H2OEstimator):
     def metalearner(self):
         return self._meta
 
+    def _label_threshold(self):
+        """Labels come from the metalearner's scoring of the level-one frame
+        (StackedEnsembleModel.java:251-258 metalearner.score), i.e. the
+        metalearner's default threshold -- as the MOJO's metalearner does."""
+        if getattr(self, "_meta", None) is not None and hasattr(self._meta, "_label_threshold"):
+            return self._meta._label_threshold()
+        return super()._label_threshold()
+
     def _predict_raw(self, frame):
         vecs, names = self._level_one(self._base, frame, use_cv=False)
         lvl1 = H2OFrame.from_vecs(vecs, names)

@@ -89,6 +89,8 @@ class _Prefixed:
 def _threshold(model):
     """The labelling threshold predict() uses: max-F1 of the validation (else
     training) metrics, 0.5 without metrics (base.py _pred_frame_from_raw)."""
+    if hasattr(model, "_label_threshold"):
+        return float(model._label_threshold())
     thr = 0.5
     for m in (getattr(model, "_training_metrics", None), getattr(model, "_validation_metrics", None)):
         if m is not None and m.get("max_f1_threshold") is not None:

@@ -39,11 +39,12 @@ def _beat():
 
 
 threading.Thread(target=_beat, daemon=True).start()
-g = torch.Generator(device="cuda").manual_seed(7)
-X = torch.randn((N, P), generator=g, device="cuda")
-beta = torch.randn(P, generator=g, device="cuda") / P ** 0.5
+DEV = "cuda" if torch.cuda.is_available() else "cpu"
+g = torch.Generator(device=DEV).manual_seed(7)
+X = torch.randn((N, P), generator=g, device=DEV)
+beta = torch.randn(P, generator=g, device=DEV) / P ** 0.5
 logit = X @ beta + 0.5 * X[:, 0] * X[:, 1] - 0.3 * X[:, 2].abs()
-y = (torch.rand(N, generator=g, device="cuda") < torch.sigmoid(logit)).to(torch.int32)
+y = (torch.rand(N, generator=g, device=DEV) < torch.sigmoid(logit)).to(torch.int32)
 vecs = [Vec(X[:, j].contiguous(), T_REAL) for j in range(P)] + [Vec(y, T_ENUM, ["0", "1"])]
 names = [f"x{j}" for j in range(P)] + ["y"]
 del X, logit

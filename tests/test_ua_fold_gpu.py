@@ -110,13 +110,13 @@ def test_uniform_adaptive_gbm_kernel_vs_torch_fold(monkeypatch):
     X[:, 2] = np.round(X[:, 2] * 3)         # few distinct values: narrow ranges
     df = pd.DataFrame(X, columns=[f"x{i}" for i in range(6)])
     df["c"] = rng.choice(list("abcde"), n)
-    df["y"] = np.where(X[:, 0] + np.sin(3 * X[:, 1]) + 0.3 * rng.randn(n) > 0, "1", "0")
+    df["y"] = np.where(X[:, 0] + np.sin(3 * X[:, 1]) + 0.3 * rng.randn(n) > 0, "yes", "no")
     fr = h2o3_amd.H2OFrame(df)
     preds = {}
     for mode in ("torch", "hip"):
         monkeypatch.setenv("H2O3_UA_FOLD", mode)
         m = H2OGradientBoostingEstimator(ntrees=5, max_depth=6, seed=3, histogram_type="UniformAdaptive")
         m.train(y="y", training_frame=fr)
-        preds[mode] = m.predict(fr).as_data_frame()["1"].values
+        preds[mode] = m.predict(fr).as_data_frame()["yes"].values
     np.testing.assert_allclose(preds["hip"], preds["torch"], rtol=1e-6, atol=1e-7)
     assert "libtree_split.so" in " ".join(_native.loaded_libs())
