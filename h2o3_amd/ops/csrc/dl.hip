@@ -899,12 +899,15 @@ int h2o_dl_mlp_step(int nl, const int* width, const int* act, const float* drop,
 #define DLG_TK 32
 __global__ __launch_bounds__(256) void dl_gemm_kernel(int M, int N, int K, const float* __restrict__ A, long long sam,
                                                       long long sak, const float* __restrict__ B, long long sbk,
-                                                      long long sbn, float* __restrict__ C, int ntn) {
+                                                      long long sbn, float* __restrict__ C, int ntn, int ntiles,
+                                                      int kchunk, float* __restrict__ Cw) {
   __shared__ float As[2][DLG_TM][DLG_TK + 1];   // [m][k]
   __shared__ float Bs[2][DLG_TK][DLG_TN + 1];   // [k][n]
   const int nwg = gridDim.x;
-  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int bid0 = xcd_remap(blockIdx.x, nwg);
+  const int ks = bid0 / ntiles, bid = bid0 - ks * ntiles;   // split-K slice, output tile
   const int tm = bid / ntn, tn = bid - (bid / ntn) * ntn;
+  const int kbeg = ks * kchunk, kend = min(K, kbeg + kchunk);
   const int m0 = tm * DLG_TM, n0 = tn * DLG_TN;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wm = (wv >> 1) * 32, wn = (wv & 1) * 32;
@@ -918,11 +921,11 @@ __global__ __launch_bounds__(256) void dl_gemm_kernel(int M, int N, int K, const
       int m, k;
       if (a_kfast) { m = e >> 5; k = e & 31; } else { k = e >> 6; m = e & 63; }
       const int gm = m0 + m, gk = k0 + k;
-      ra[u] = (gm < M && gk < K) ? A[(long long)gm * sam + (long long)gk * sak] : 0.f;
+      ra[u] = (gm < M && gk < kend) ? A[(long long)gm * sam + (long long)gk * sak] : 0.f;
       int kb, n;
       if (b_nfast) { kb = e >> 6; n = e & 63; } else { n = e >> 5; kb = e & 31; }
       const int gk2 = k0 + kb, gn = n0 + n;
-      rb[u] = (gk2 < K && gn < N) ? B[(long long)gk2 * sbk + (long long)gn * sbn] : 0.f;
+      rb[u] = (gk2 < kend && gn < N) ? B[(long long)gk2 * sbk + (long long)gn * sbn] : 0.f;
     }
   };
   auto store = [&](int buf) {
@@ -941,16 +944,16 @@ __global__ __launch_bounds__(256) void dl_gemm_kernel(int M, int N, int K, const
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = (f4){0.f, 0.f, 0.f, 0.f};
-  const int nslab = (K + DLG_TK - 1) / DLG_TK;
+  const int nslab = kend > kbeg ? (kend - kbeg + DLG_TK - 1) / DLG_TK : 0;
   if (nslab > 0) {
-    load(0);
+    load(kbeg);
     store(0);
   }
   __syncthreads();
   const int li = lane & 15, lg = lane >> 4;
   for (int s = 0; s < nslab; ++s) {
     const int cur = s & 1;
-    if (s + 1 < nslab) load((s + 1) * DLG_TK);
+    if (s + 1 < nslab) load(kbeg + (s + 1) * DLG_TK);
 #pragma unroll
     for (int kk = 0; kk < DLG_TK; kk += 4) {
       float a0 = As[cur][wm + li][kk + lg], a1 = As[cur][wm + 16 + li][kk + lg];
@@ -970,15 +973,66 @@ __global__ __launch_bounds__(256) void dl_gemm_kernel(int M, int N, int K, const
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int gm = m0 + wm + 16 * i + 4 * lg + r, gn = n0 + wn + 16 * j + li;
-        if (gm < M && gn < N) C[(long long)gm * N + gn] = acc[i][j][r];
+        if (gm < M && gn < N) {
+          if (Cw != nullptr) Cw[((long long)ks * M + gm) * N + gn] = acc[i][j][r];
+          else C[(long long)gm * N + gn] = acc[i][j][r];
+        }
       }
 }
 
+// Split-K partials [ks][M*N] summed in slice order (deterministic).
+__global__ __launch_bounds__(256) void dl_gemm_reduce_kernel(const float* __restrict__ Cw, int ksplit, long long mn,
+                                                             float* __restrict__ C) {
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < mn; i += (long long)gridDim.x * 256) {
+    float v = 0.f;
+    for (int k = 0; k < ksplit; ++k) v += Cw[(long long)k * mn + i];
+    C[i] = v;
+  }
+}
+
+// Split-K plan: slices of K (multiples of the 32-deep slab) until the grid has
+// ~4 workgroups per CU -- the thin products of a step (the 2-unit output
+// layer, the input layer's dW) have few output tiles but K = batch or width.
+static void dl_gemm_plan(int M, int N, int K, int& ksplit, int& kchunk) {
+  const int tiles = ((M + DLG_TM - 1) / DLG_TM) * ((N + DLG_TN - 1) / DLG_TN);
+  const int nslab = (K + DLG_TK - 1) / DLG_TK;
+  if (tiles <= 0 || nslab <= 0) {
+    ksplit = 1;
+    kchunk = max(K, 1);
+    return;
+  }
+  int want = (1024 + tiles - 1) / tiles;
+  want = min(want, max(1, nslab / 4));        // at least 4 slabs (128 deep) per slice
+  want = min(want, 32);
+  const int spk = (nslab + want - 1) / max(want, 1);
+  kchunk = spk * DLG_TK;
+  ksplit = K > 0 ? (K + kchunk - 1) / kchunk : 1;
+}
+
+extern "C" long long h2o_dl_gemm_ws(int M, int N, int K) {
+  int ks, kc;
+  dl_gemm_plan(M, N, K, ks, kc);
+  return ks > 1 ? (long long)ks * M * N : 0;
+}
+
 extern "C" int h2o_dl_gemm(int M, int N, int K, const float* A, long long sam, long long sak, const float* B,
-                           long long sbk, long long sbn, float* C, hipStream_t s) {
+                           long long sbk, long long sbn, float* C, float* ws, long long ws_elems, hipStream_t s) {
   if (M <= 0 || N <= 0) return 0;
   if (K < 0 || !A || !B || !C) return (int)hipErrorInvalidValue;
   const int ntm = (M + DLG_TM - 1) / DLG_TM, ntn = (N + DLG_TN - 1) / DLG_TN;
-  hipLaunchKernelGGL(dl_gemm_kernel, dim3(ntm * ntn), dim3(256), 0, s, M, N, K, A, sam, sak, B, sbk, sbn, C, ntn);
+  int ksplit, kchunk;
+  dl_gemm_plan(M, N, K, ksplit, kchunk);
+  if (ksplit > 1 && (ws == nullptr || ws_elems < (long long)ksplit * M * N)) {
+    ksplit = 1;                               // no workspace: one slice
+    kchunk = max(K, 1);
+  }
+  const int ntiles = ntm * ntn;
+  hipLaunchKernelGGL(dl_gemm_kernel, dim3(ntiles * ksplit), dim3(256), 0, s, M, N, K, A, sam, sak, B, sbk, sbn, C,
+                     ntn, ntiles, kchunk, ksplit > 1 ? ws : (float*)nullptr);
+  if (ksplit > 1) {
+    const long long mn = (long long)M * N;
+    const int g = (int)min((mn + 255) / 256, 4096LL);
+    hipLaunchKernelGGL(dl_gemm_reduce_kernel, dim3(g), dim3(256), 0, s, ws, ksplit, mn, C);
+  }
   H2O_CHECK_LAUNCH();
 }

@@ -473,9 +473,14 @@ template <int KT, int MODE>
 static int ka_launch(const float* X, long long N, int P, const float* C, const float* cn, int k, int* assign,
                      float* d2, int G, hipStream_t s, int* per_cu_out) {
   const int nv = ((P + 15) & ~15) >> 4;      // float4 per lane = P16 / 16
+  // exact step counts up to 8 float4 (P <= 128): the padding steps of a
+  // larger MAXNV would be MFMAs on zeros (the loop is branch-free)
   if (nv <= 2) return ka_launch2<KT, 2, MODE>(X, N, P, C, cn, k, assign, d2, G, s, per_cu_out);
+  if (nv <= 3) return ka_launch2<KT, 3, MODE>(X, N, P, C, cn, k, assign, d2, G, s, per_cu_out);
   if (nv <= 4) return ka_launch2<KT, 4, MODE>(X, N, P, C, cn, k, assign, d2, G, s, per_cu_out);
+  if (nv <= 5) return ka_launch2<KT, 5, MODE>(X, N, P, C, cn, k, assign, d2, G, s, per_cu_out);
   if (nv <= 6) return ka_launch2<KT, 6, MODE>(X, N, P, C, cn, k, assign, d2, G, s, per_cu_out);
+  if (nv <= 7) return ka_launch2<KT, 7, MODE>(X, N, P, C, cn, k, assign, d2, G, s, per_cu_out);
   if (nv <= 8) return ka_launch2<KT, 8, MODE>(X, N, P, C, cn, k, assign, d2, G, s, per_cu_out);
   if (nv <= 12) return ka_launch2<KT, 12, MODE>(X, N, P, C, cn, k, assign, d2, G, s, per_cu_out);
   return ka_launch2<KT, 16, MODE>(X, N, P, C, cn, k, assign, d2, G, s, per_cu_out);
@@ -548,85 +553,106 @@ __global__ __launch_bounds__(256) void kmeans_reduce_kernel(const double* __rest
 // pair, no same-address collisions within a wave-instruction), one
 // returnless ds_add_u64 per (row, column).  Row weights / within-SS / changed
 // assignments as in the fused kernel; one f64 partial per workgroup.
-#define KMS_THREADS 1024   // sums pass: 16 waves per workgroup hide the X loads at one workgroup per CU
+#define KMS_THREADS 1024   // sums pass: 16 waves per workgroup at one workgroup per CU
+#define KMS_MAXJ 16        // X elements per thread per 64-row tile (64 * 256 / 1024)
+// Software-pipelined: while the u64 atomics of tile t run, the X elements
+// (and row assignment / weight / d2) of tile t + 1 are already in flight in
+// registers, so each tile costs one HBM latency overlapped with LDS work
+// instead of ~7 dependent load -> atomic round trips (the round-5 loop ran
+// 29 ms at 100M x 100, k = 128, against ~7 ms of loads).  The per-row
+// weight / within-SS go to f64 LDS sums (ds_add_f64, no per-tile f32 fold),
+// and the tile's assignment / weight arrays are double-buffered: ONE barrier
+// per tile.
 __global__ __launch_bounds__(KMS_THREADS) void kmeans_sums_kernel(
     const float* __restrict__ X, const float* __restrict__ w, long long N, int P, int k,
     const int* __restrict__ asg, const int* __restrict__ asg_old, const float* __restrict__ d2,
     double* __restrict__ part, float fx_scale) {
   extern __shared__ __align__(16) unsigned long long S64[];   // [k][P]
-  float* Swt = (float*)(S64 + (size_t)k * P);                   // [k]
-  float* Sss = Swt + k;                                          // [k]
-  int* tasg = (int*)(Sss + k);                                   // [64]
-  float* tw = (float*)(tasg + KM_ROWS);                          // [64]
+  double* Swt = (double*)(S64 + (size_t)k * P);                 // [k]
+  double* Sss = Swt + k;                                         // [k]
+  int* tasg = (int*)(Sss + k);                                   // [2][64]
+  float* tw = (float*)(tasg + 2 * KM_ROWS);                      // [2][64]
   __shared__ int changed_s;
   const int tid = threadIdx.x;
   for (int e = tid; e < k * P; e += KMS_THREADS) S64[e] = 0ull;
-  for (int e = tid; e < 2 * k; e += KMS_THREADS) Swt[e] = 0.f;
+  for (int e = tid; e < 2 * k; e += KMS_THREADS) Swt[e] = 0.0;
   if (tid == 0) changed_s = 0;
-  double wacc[2] = {0.0, 0.0};
   const long long ntiles = (N + KM_ROWS - 1) / KM_ROWS;
   const int G = gridDim.x;
   const int bid = xcd_remap(blockIdx.x, G);
-  const int dr = KMS_THREADS / P, dc = KMS_THREADS - (KMS_THREADS / P) * P;
-  const int r_init = tid / P, c_init = tid - (tid / P) * P;
-  __syncthreads();
-  for (long long t = bid; t < ntiles; t += G) {
-    const long long r0 = t * KM_ROWS;
-    const long long nrow = min((long long)KM_ROWS, N - r0);
-    if (tid < KM_ROWS) {
-      int a = 0;
-      float wr = 0.f;
-      if (tid < nrow) {
-        const long long r = r0 + tid;
-        a = asg[r];
-        wr = w ? w[r] : 1.f;
-        if (asg_old && asg_old[r] != a) atomicAdd(&changed_s, 1);
-        if (wr != 0.f) {
-          lds_add(Swt + a, wr);
-          lds_add(Sss + a, wr * d2[r]);
-        }
-      }
-      tasg[tid] = a;
-      tw[tid] = wr;
-    }
-    __syncthreads();
-    const float* src = X + r0 * P;
-    const int tot = (int)nrow * P;
-    int r = r_init, c = c_init;
-    for (int e = tid; e < tot; e += KMS_THREADS) {
-      const float wr = tw[r];
-      const float v = wr * src[e];
-      if (v != 0.f)
-        __hip_atomic_fetch_add(S64 + tasg[r] * P + c, (unsigned long long)__float2ll_rn(v * fx_scale),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      r += dr; c += dc;
-      if (c >= P) { c -= P; ++r; }
-    }
-    __syncthreads();
-    // weights / within-SS of this tile: f32 LDS -> f64 registers, LDS re-zeroed
+  // this thread's fixed (row, column) slots of a tile
+  int rj[KMS_MAXJ], cj[KMS_MAXJ];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int e = tid + h * KMS_THREADS;
-      if (e < 2 * k) { wacc[h] += (double)Swt[e]; Swt[e] = 0.f; }
+  for (int j = 0; j < KMS_MAXJ; ++j) {
+    const int e = tid + j * KMS_THREADS;
+    rj[j] = e / P;
+    cj[j] = e - (e / P) * P;
+  }
+  float xv[KMS_MAXJ];
+  int ra = 0, rold = 0;
+  float rw = 0.f, rd = 0.f;
+  auto fetch = [&](long long t) {
+    const long long r0 = t * KM_ROWS;
+    const int tot = (int)min((long long)KM_ROWS, N - r0) * P;
+    const float* src = X + r0 * P;
+#pragma unroll
+    for (int j = 0; j < KMS_MAXJ; ++j) {
+      const int e = tid + j * KMS_THREADS;
+      xv[j] = e < tot ? src[e] : 0.f;
     }
-    // Swt/Sss entries are owned by every wave (2k may exceed 64): wave 0 must
-    // not lds_add the next tile's row stats before all waves folded + zeroed
+    if (tid < KM_ROWS) {
+      const long long r = r0 + tid;
+      if (r < N) {
+        ra = asg[r];
+        rw = w ? w[r] : 1.f;
+        rd = d2[r];
+        rold = asg_old ? asg_old[r] : ra;
+      } else {
+        ra = 0; rw = 0.f; rd = 0.f; rold = 0;
+      }
+    }
+  };
+  __syncthreads();
+  long long t = bid;
+  if (t < ntiles) fetch(t);
+  for (int it = 0; t < ntiles; t += G, ++it) {
+    const int b = it & 1;
+    if (tid < KM_ROWS) {
+      if (rold != ra) atomicAdd(&changed_s, 1);
+      if (rw != 0.f) {
+        atomicAdd(Swt + ra, (double)rw);
+        atomicAdd(Sss + ra, (double)rw * (double)rd);
+      }
+      tasg[b * KM_ROWS + tid] = ra;
+      tw[b * KM_ROWS + tid] = rw;
+    }
     __syncthreads();
+    float cur[KMS_MAXJ];
+#pragma unroll
+    for (int j = 0; j < KMS_MAXJ; ++j) cur[j] = xv[j];
+    if (t + G < ntiles) fetch(t + G);        // next tile in flight during this tile's atomics
+    const int* ta = tasg + b * KM_ROWS;
+    const float* twb = tw + b * KM_ROWS;
+#pragma unroll
+    for (int j = 0; j < KMS_MAXJ; ++j) {
+      if (rj[j] < KM_ROWS) {
+        const float v = twb[rj[j]] * cur[j];
+        if (v != 0.f)
+          __hip_atomic_fetch_add(S64 + ta[rj[j]] * P + cj[j], (unsigned long long)__float2ll_rn(v * fx_scale),
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
   }
   __syncthreads();
   double* o = part + (long long)blockIdx.x * km_part_stride(k, P);
   const double inv = 1.0 / (double)fx_scale;
   for (int e = tid; e < k * P; e += KMS_THREADS) o[e] = (double)(long long)S64[e] * inv;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int e = tid + h * KMS_THREADS;
-    if (e < 2 * k) o[(long long)k * P + e] = wacc[h];
-  }
+  for (int e = tid; e < 2 * k; e += KMS_THREADS) o[(long long)k * P + e] = Swt[e];
   if (tid == 0) o[(long long)k * P + 2 * k] = (double)changed_s;
 }
 
 static size_t km_sums_lds_bytes(int k, int P) {
-  return (size_t)k * P * 8 + (size_t)2 * k * 4 + 2 * KM_ROWS * 4;
+  return (size_t)k * P * 8 + (size_t)2 * k * 8 + 2 * 2 * KM_ROWS * 4;
 }
 
 static int km_kt(int k) {   // the template instance a given k runs on

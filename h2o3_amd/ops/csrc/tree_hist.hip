@@ -33,13 +33,21 @@
 template <int MODE> struct Chan { static constexpr int C = MODE == 2 ? 1 : 2; };
 
 // work[i] = (slot, pos_start, pos_count, unused);  grid = (n_work, n_feature_groups)
-template <typename CodeT, int MODE, bool HAS_VB, bool POSV>
+// PACK (MODE 0, 0/1 weights; the wide-code UniformAdaptive histograms): one
+// 64-bit LDS atomic per (row, feature) as in hist_quad_kernel (count in bits
+// 63..40, biased fixed-point response below), so a 1025-bin feature takes
+// 8.2 KB of LDS instead of 16.4 KB and a workgroup covers twice the features
+// -- every feature group re-reads the rows' indices, responses and code
+// sectors, which is what the 1024-cell level histograms pay for.
+template <typename CodeT, int MODE, bool HAS_VB, bool POSV, bool PACK = false>
 __global__ __launch_bounds__(512) void hist_build_kernel(
     const CodeT* __restrict__ codes, int Fp, const int* __restrict__ ridx,
     const float* __restrict__ va, const float* __restrict__ vb,
     const int4* __restrict__ work, int F, int Bs, int FGL, float s0, float s1,
-    double* __restrict__ hist, int n_slots, double* __restrict__ wyy_out, const uint8_t* __restrict__ need) {
+    double* __restrict__ hist, int n_slots, double* __restrict__ wyy_out, const uint8_t* __restrict__ need,
+    long long bq = 0) {
   constexpr int C = Chan<MODE>::C;
+  constexpr int CL = PACK ? 1 : C;                // u64 LDS words per bin
   const int RPW = 64 / FGL;                     // rows per wave instruction
   extern __shared__ __attribute__((aligned(16))) unsigned long long ldsq[];
   const int4 wk = work[blockIdx.x];
@@ -48,10 +56,11 @@ __global__ __launch_bounds__(512) void hist_build_kernel(
   if (need != nullptr && need[(size_t)wk.x * gridDim.y + blockIdx.y] == 0) return;
   const int fg0 = blockIdx.y * FGL;
   const int nf = min(FGL, F - fg0);
-  const int stride_f = Bs * C;
+  const int stride_f = Bs * CL;
   const int total = FGL * stride_f;
   for (int i = threadIdx.x; i < total; i += blockDim.x) ldsq[i] = 0ull;
   __syncthreads();
+  const unsigned long long pk_off = (1ull << 40) + (unsigned long long)bq;
 
   const int lane = threadIdx.x & 63;
   const int fl = lane % FGL;                    // feature within group
@@ -105,6 +114,13 @@ __global__ __launch_bounds__(512) void hist_build_kernel(
     for (int u = 0; u < U; ++u) {
       const bool inr = p0 + u * step < pend;
       if (MODE == 0 && do_wyy && inr) wyy += (double)c1[u] * (double)yv[u];
+      if (PACK) {
+        // 0/1 weights: a row of weight 0 adds nothing
+        if (fok && inr && c0[u] != 0.f)
+          __hip_atomic_fetch_add(hbase + code[u], pk_off + (unsigned long long)__float2ll_rn(c1[u] * s1),
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        continue;
+      }
       const bool ok = fok && inr && (c0[u] != 0.f || c1[u] != 0.f);
       if (ok) {
         unsigned long long* h = hbase + code[u] * C;
@@ -122,6 +138,21 @@ __global__ __launch_bounds__(512) void hist_build_kernel(
     if (lane == 0) gbl_add(wyy_out + wk.x, wyy);
   }
   const double inv0 = 1.0 / (double)s0, inv1 = 1.0 / (double)s1;
+  if (PACK) {
+    const int tot = nf * Bs;
+    for (int i = threadIdx.x; i < tot; i += blockDim.x) {
+      const unsigned long long v = ldsq[i];
+      if (v != 0) {
+        const int j = i / Bs, b = i - (i / Bs) * Bs;
+        const long long cnt = (long long)(v >> 40);
+        const long long low = (long long)(v & ((1ull << 40) - 1));
+        double* o = hist + ((size_t)(fg0 + j) * n_slots + wk.x) * (Bs * 2) + 2 * b;
+        gbl_add(o, (double)cnt);
+        gbl_add(o + 1, (double)(low - cnt * bq) * inv1);
+      }
+    }
+    return;
+  }
   const int tot_real = nf * stride_f;
   for (int i = threadIdx.x; i < tot_real; i += blockDim.x) {
     const long long q = (long long)ldsq[i];
@@ -800,12 +831,32 @@ template <typename CodeT>
 static int launch_hist(const void* codes, int Fp, const int* ridx, const float* va, const float* vb,
                        const int4* work, int n_work, int F, int FG, int Bs, float s0, float s1, double* hist,
                        int n_slots, int mode, int threads, double* wyy, int posv, const uint8_t* need,
-                       hipStream_t s) {
+                       hipStream_t s, long long pack_bq = -1) {
   const int n_fg = (F + FG - 1) / FG;
   dim3 grid(n_work, n_fg);
   const int C = mode == 2 ? 1 : 2;
-  size_t lds = (size_t)FG * Bs * C * sizeof(unsigned long long);
   const CodeT* cc = (const CodeT*)codes;
+  if (pack_bq >= 0 && mode == 0) {
+    const size_t lds = (size_t)FG * Bs * sizeof(unsigned long long);
+    if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
+#define H2O_PK(V, PV)                                                                                        \
+  {                                                                                                          \
+    auto kern = hist_build_kernel<CodeT, 0, V, PV, true>;                                                    \
+    if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=      \
+        hipSuccess)                                                                                          \
+      return (int)hipErrorInvalidValue;                                                                      \
+    hipLaunchKernelGGL(kern, grid, dim3(threads), lds, s, cc, Fp, ridx, va, vb, work, F, Bs, FG, s0, s1,     \
+                       hist, n_slots, wyy, need, pack_bq);                                                   \
+  }
+    if (vb) {
+      if (posv) H2O_PK(true, true) else H2O_PK(true, false)
+    } else {
+      if (posv) H2O_PK(false, true) else H2O_PK(false, false)
+    }
+#undef H2O_PK
+    return (int)hipGetLastError();
+  }
+  size_t lds = (size_t)FG * Bs * C * sizeof(unsigned long long);
   switch (mode) {
 #define H2O_LH(M, V) if (posv) H2O_LH2(M, V, true); else H2O_LH2(M, V, false)
 #define H2O_LH2(M, V, PV) hipLaunchKernelGGL((hist_build_kernel<CodeT, M, V, PV>), grid, dim3(threads), lds, s, cc, Fp, ridx, va, vb, work, F, Bs, FG, s0, s1, hist, n_slots, wyy, need)
@@ -1292,6 +1343,20 @@ int h2o_hist_build(const void* codes, int code_bytes, int Fp, const int* ridx, c
   if (code_bytes == 1)
     return launch_hist<uint8_t>(codes, Fp, ridx, va, vb, (const int4*)work, n_work, F, FG, Bs, s0, s1, hist, n_slots, mode, threads, wyy, posv, need, s);
   return launch_hist<uint16_t>(codes, Fp, ridx, va, vb, (const int4*)work, n_work, F, FG, Bs, s0, s1, hist, n_slots, mode, threads, wyy, posv, need, s);
+}
+
+// Packed single-atomic histogram (MODE 0, 0/1 weights), any code width.
+int h2o_hist_build_pk(const void* codes, int code_bytes, int Fp, const int* ridx, const float* va,
+                      const float* vb, const int* work, int n_work, int F, int FG, int Bs, float s1, long long bq,
+                      double* hist, int n_slots, int threads, double* wyy, int posv, const uint8_t* need,
+                      hipStream_t s) {
+  if (n_work <= 0) return 0;
+  if (bq < 0) return (int)hipErrorInvalidValue;
+  if (code_bytes == 1)
+    return launch_hist<uint8_t>(codes, Fp, ridx, va, vb, (const int4*)work, n_work, F, FG, Bs, 1.f, s1, hist, n_slots,
+                                0, threads, wyy, posv, need, s, bq);
+  return launch_hist<uint16_t>(codes, Fp, ridx, va, vb, (const int4*)work, n_work, F, FG, Bs, 1.f, s1, hist, n_slots,
+                               0, threads, wyy, posv, need, s, bq);
 }
 
 int h2o_part_flags(const void* codes, int code_bytes, long long rs, long long fs, const int* ridx,

@@ -35,7 +35,9 @@ def _lib():
         lib.h2o_dl_mlp_step.argtypes = [_ci] + [_cv] * 15 + [_ci] + [_cv] * 4 + [_ci, _ci, _cf, _cull, _cv, _ci,
                                                                             _cv]
         lib.h2o_dl_gemm.argtypes = [_ci, _ci, _ci, _cv, ctypes.c_longlong, ctypes.c_longlong, _cv,
-                                    ctypes.c_longlong, ctypes.c_longlong, _cv, _cv]
+                                    ctypes.c_longlong, ctypes.c_longlong, _cv, _cv, ctypes.c_longlong, _cv]
+        lib.h2o_dl_gemm_ws.argtypes = [_ci, _ci, _ci]
+        lib.h2o_dl_gemm_ws.restype = ctypes.c_longlong
         lib._typed = True
     return lib
 
@@ -361,7 +363,15 @@ def gemm(A, B, out=None):
     K2, N = B.shape
     assert K == K2, (A.shape, B.shape)
     C = out if out is not None else torch.empty((M, N), dtype=torch.float32, device=A.device)
+    if M == 0 or N == 0:
+        return C
+    if K == 0:
+        return C.zero_()
     lib = _lib()
-    _check(lib.h2o_dl_gemm(M, N, K, _p(A), A.stride(0), A.stride(1), _p(B), B.stride(0), B.stride(1), _p(C), _s()),
-           "h2o_dl_gemm")
+    # split-K workspace (thin products: few output tiles, long K), summed in
+    # slice order by a second kernel -- deterministic, no float atomics
+    nws = int(lib.h2o_dl_gemm_ws(M, N, K))
+    ws = torch.empty(nws, dtype=torch.float32, device=A.device) if nws > 0 else None
+    _check(lib.h2o_dl_gemm(M, N, K, _p(A), A.stride(0), A.stride(1), _p(B), B.stride(0), B.stride(1), _p(C),
+                           _p(ws), nws, _s()), "h2o_dl_gemm")
     return C

@@ -168,6 +168,9 @@ def _lib():
         lib.h2o_hist_bm.argtypes = [_c_void, _c_int, _c_void, _c_void, _c_void, _c_void, _c_int, _c_int, _c_int,
                                     _c_int, ctypes.c_float, ctypes.c_float, _c_void, _c_int, _c_int, _c_void, _c_int,
                                     _c_ll, _c_int, _c_void, _c_void, _c_void, _c_void]
+        lib.h2o_hist_build_pk.argtypes = [_c_void, _c_int, _c_int, _c_void, _c_void, _c_void, _c_void, _c_int,
+                                          _c_int, _c_int, _c_int, ctypes.c_float, _c_ll, _c_void, _c_int, _c_int,
+                                          _c_void, _c_int, _c_void, _c_void]
         lib.h2o_part_flags.argtypes = [_c_void, _c_int, _c_ll, _c_ll, _c_void, _c_void, _c_void, _c_int, _c_void,
                                        _c_void, _c_int, _c_void, _c_void, _c_void]
         lib.h2o_part_compact.argtypes = [_c_void, _c_void, _c_void, _c_int, _c_void, _c_void, _c_void, _c_void,
@@ -322,6 +325,7 @@ def _pack_scale(vmax, chunk):
 # keeping >= 512 workgroups to fill the chip (scripts/hist_bm_mb.py with the
 # two-pass flush of the bin-major kernel: 100M-row root 3.69 -> 3.35 ms,
 # 12.5M-row root 0.59 -> 0.47 ms vs 64K rows, deeper levels unchanged).
+_PK_BUDGET = 152 * 1024     # packed wide-code histogram: one 512-thread workgroup per CU
 _HIST_CHUNK_ROWS = 131072
 _HIST_MIN_BLOCKS = 512
 
@@ -374,10 +378,19 @@ def hist_build(bd, ridx, va, vb, mode, starts, counts, n_slots, use_native=None,
         if quad:
             bm = bm_groups(bd.F, bd.Fp, bd.Bs, pack or mode == 2)
             n_fg, fgw = bm if bm is not None else quad_groups(bd.F, bd.Fp, bd.Bs, pack, qbudget)
-        else:
-            FG = feature_group(bd.F, bd.Bs, mode)
+        pkw = False
+        if not quad:
+            # wide (2-byte) codes, 0/1 weights: one packed u64 LDS atomic per
+            # (row, feature) -- half the LDS per feature, so ~2x the features
+            # per workgroup and half the re-reads of the rows per level
+            pkw = mode == 0 and unit_w and bd.code_bytes == 2 and env("H2O3_HIST_PACK", "1") == "1"
+            FG = feature_group(bd.F, bd.Bs, 2 if pkw else mode, budget=_PK_BUDGET if pkw else _LDS_BUDGET)
             n_fg = (bd.F + FG - 1) // FG
         chunk = hist_chunk(total, n_fg, target_blocks)
+        if pkw and chunk >= (1 << 23):
+            pkw = False
+            FG = feature_group(bd.F, bd.Bs, mode)
+            n_fg = (bd.F + FG - 1) // FG
         if pack and chunk >= (1 << 23):
             pack = False
             bm = bm_groups(bd.F, bd.Fp, bd.Bs, mode == 2)
@@ -419,6 +432,14 @@ def hist_build(bd, ridx, va, vb, mode, starts, counts, n_slots, use_native=None,
                 raise RuntimeError(f"h2o_hist_quad3 failed: error {rc} (F={bd.F}, Fp={bd.Fp}, fgw={fgw})")
             return ret()
         need = _need(FG)
+        if pkw:
+            s1p, bqp = _pack_scale(vmax[1] if vb is None else max(vmax[1], 0.0), chunk)
+            rc = lib.h2o_hist_build_pk(_ptr(bd.codes), bd.code_bytes, bd.Fp, _ptr(ridx), _ptr(va), _ptr(vb),
+                                       _ptr(work), len(items), bd.F, FG, bd.Bs, s1p, bqp, _ptr(hist), n_slots,
+                                       threads, _ptr(wyy), 1 if posv else 0, _ptr(need), _stream())
+            if rc != 0:
+                raise RuntimeError(f"h2o_hist_build_pk failed: hip error {rc}")
+            return ret()
         rc = lib.h2o_hist_build(_ptr(bd.codes), bd.code_bytes, bd.Fp, _ptr(ridx), _ptr(va), _ptr(vb), _ptr(work),
                                 len(items), bd.F, FG, bd.Bs, s0, s1, _ptr(hist), n_slots, mode, threads, _ptr(wyy),
                                 1 if posv else 0, _ptr(need), _stream())

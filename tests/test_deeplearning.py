@@ -479,7 +479,8 @@ def test_dl_gemm_kernel_matches_fp64():
         pytest.skip("no GPU")
     from h2o3_amd.ops import dl_ops
     g = torch.Generator(device="cuda").manual_seed(3)
-    for M, K, N in ((1024, 1024, 1024), (333, 37, 19), (1, 5, 7), (1000, 100, 200), (64, 2000, 3)):
+    for M, K, N in ((1024, 1024, 1024), (333, 37, 19), (1, 5, 7), (1000, 100, 200), (64, 2000, 3), (1024, 1000, 2),
+                    (1024, 0, 5)):
         A = torch.randn((M, K), generator=g, device="cuda")
         W = torch.randn((N, K), generator=g, device="cuda")
         C = dl_ops.gemm(A, W.t())                       # Z = A W^T

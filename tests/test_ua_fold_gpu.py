@@ -120,3 +120,27 @@ def test_uniform_adaptive_gbm_kernel_vs_torch_fold(monkeypatch):
         preds[mode] = m.predict(fr).as_data_frame()["yes"].values
     np.testing.assert_allclose(preds["hip"], preds["torch"], rtol=1e-6, atol=1e-7)
     assert "libtree_split.so" in " ".join(_native.loaded_libs())
+
+
+def test_uniform_adaptive_packed_wide_histogram(monkeypatch):
+    """1024-cell (2-byte code) histograms with the packed single-atomic kernel
+    (h2o_hist_build_pk) grow the same model as the two-channel kernel."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import pandas as pd
+    import h2o3_amd
+    from h2o3_amd.estimators import H2OGradientBoostingEstimator
+    h2o3_amd.init(verbose=False)
+    rng = np.random.RandomState(9)
+    n = 30000
+    X = rng.randn(n, 40).astype(np.float32)
+    df = pd.DataFrame(X, columns=[f"x{i}" for i in range(40)])
+    df["y"] = np.where(X[:, 0] - X[:, 3] * X[:, 5] + 0.3 * rng.randn(n) > 0, "yes", "no")
+    fr = h2o3_amd.H2OFrame(df)
+    preds = {}
+    for pk in ("0", "1"):
+        monkeypatch.setenv("H2O3_HIST_PACK", pk)
+        m = H2OGradientBoostingEstimator(ntrees=4, max_depth=5, seed=3, histogram_type="UniformAdaptive")
+        m.train(y="y", training_frame=fr)
+        preds[pk] = m.predict(fr).as_data_frame()["yes"].values
+    np.testing.assert_allclose(preds["1"], preds["0"], rtol=1e-5, atol=1e-6)
