@@ -897,12 +897,15 @@ int h2o_dl_mlp_step(int nl, const int* width, const int* act, const float* drop,
 #define DLG_TM 64
 #define DLG_TN 64
 #define DLG_TK 32
-__global__ __launch_bounds__(256) void dl_gemm_kernel(int M, int N, int K, const float* __restrict__ A, long long sam,
+__global__ __launch_bounds__(256, 4) void dl_gemm_kernel(int M, int N, int K, const float* __restrict__ A, long long sam,
                                                       long long sak, const float* __restrict__ B, long long sbk,
                                                       long long sbn, float* __restrict__ C, int ntn, int ntiles,
                                                       int kchunk, float* __restrict__ Cw) {
-  __shared__ float As[2][DLG_TM][DLG_TK + 1];   // [m][k]
-  __shared__ float Bs[2][DLG_TK][DLG_TN + 1];   // [k][n]
+  // both operands k-inner in LDS (B transposed to [n][k]), rows padded to
+  // 36 floats: one ds_read_b128 gives a lane 4 consecutive k of its row, and
+  // the 16 rows of a 16-lane group hit distinct 4-bank groups
+  __shared__ __align__(16) float As[2][DLG_TM][DLG_TK + 4];   // [m][k]
+  __shared__ __align__(16) float Bs[2][DLG_TN][DLG_TK + 4];   // [n][k]
   const int nwg = gridDim.x;
   const int bid0 = xcd_remap(blockIdx.x, nwg);
   const int ks = bid0 / ntiles, bid = bid0 - ks * ntiles;   // split-K slice, output tile
@@ -934,8 +937,8 @@ __global__ __launch_bounds__(256) void dl_gemm_kernel(int M, int N, int K, const
       const int e = tid + u * 256;
       if (a_kfast) As[buf][e >> 5][e & 31] = ra[u];
       else As[buf][e & 63][e >> 6] = ra[u];
-      if (b_nfast) Bs[buf][e >> 6][e & 63] = rb[u];
-      else Bs[buf][e & 31][e >> 5] = rb[u];
+      if (b_nfast) Bs[buf][e & 63][e >> 6] = rb[u];
+      else Bs[buf][e >> 5][e & 31] = rb[u];
     }
   };
   typedef float f4 __attribute__((ext_vector_type(4)));
@@ -954,14 +957,21 @@ __global__ __launch_bounds__(256) void dl_gemm_kernel(int M, int N, int K, const
   for (int s = 0; s < nslab; ++s) {
     const int cur = s & 1;
     if (s + 1 < nslab) load(kbeg + (s + 1) * DLG_TK);
+    // MFMA j of a 16-deep chunk covers k = c + 4 * lg + j across the lane
+    // groups (same permutation on both operands: the sum over k is unchanged)
 #pragma unroll
-    for (int kk = 0; kk < DLG_TK; kk += 4) {
-      float a0 = As[cur][wm + li][kk + lg], a1 = As[cur][wm + 16 + li][kk + lg];
-      float b0 = Bs[cur][kk + lg][wn + li], b1 = Bs[cur][kk + lg][wn + 16 + li];
-      acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, acc[1][1], 0, 0, 0);
+    for (int c = 0; c < DLG_TK; c += 16) {
+      const f4 a0 = *(const f4*)&As[cur][wm + li][c + 4 * lg];
+      const f4 a1 = *(const f4*)&As[cur][wm + 16 + li][c + 4 * lg];
+      const f4 b0 = *(const f4*)&Bs[cur][wn + li][c + 4 * lg];
+      const f4 b1 = *(const f4*)&Bs[cur][wn + 16 + li][c + 4 * lg];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[j], b0[j], acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[j], b1[j], acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[j], b0[j], acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[j], b1[j], acc[1][1], 0, 0, 0);
+      }
     }
     if (s + 1 < nslab) store(cur ^ 1);
     __syncthreads();

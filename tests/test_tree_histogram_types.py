@@ -189,3 +189,35 @@ def test_uniform_adaptive_gbm_matches_reference_mojo_top_splits():
         assert abs(ot.thresholds[ro] - rt.split[rr]) < cell
     n_internal = sum(1 for f in H2OTree(g, 0).features if f is not None)
     assert n_internal == len(ref.trees[0][0].col) == 23
+
+
+def test_uniform_adaptive_50_tree_fixture_parity_numbers():
+    """The whole 50-tree reference fixture (gbm_variable_importance.zip, the
+    reference AUTO = UniformAdaptive, defaults) against our UniformAdaptive
+    GBM on the same prostate frame.  Splits are pinned exactly down to depth
+    1 (test above); deeper, our fold snaps cut points to the top-level grid
+    while the reference re-bins over each parent's exact float range, so
+    parity is UNPINNED beyond depth 1 and the whole-model distance is stated
+    instead (measured: max |p - p_ref| 0.124, mean 0.026 over the 380 rows;
+    training AUC 0.97986 vs the fixture's 0.98016, logloss 0.2718 vs
+    0.2676)."""
+    import os
+    R = "/root/reference/h2o-genmodel/src/test/resources/hex/genmodel/algos/gbm/gbm_variable_importance.zip"
+    D = "/root/reference/h2o-core/src/main/resources/extdata/prostate.csv"
+    if not (os.path.exists(R) and os.path.exists(D)):
+        pytest.skip("reference fixture not present")
+    import pandas as pd
+    from h2o3_amd.estimators import H2OGradientBoostingEstimator
+    from h2o3_amd.mojo.genmodel import MojoModel
+    cols = ["AGE", "RACE", "DPROS", "DCAPS", "PSA", "VOL", "GLEASON"]
+    df = pd.read_csv(D)
+    fr = h2o.H2OFrame(df)
+    fr["CAPSULE"] = fr["CAPSULE"].asfactor()
+    p_ref = MojoModel.load(R).predict(df[cols])["p1"].values
+    g = H2OGradientBoostingEstimator(ntrees=50, seed=1, histogram_type="UniformAdaptive")
+    g.train(x=cols, y="CAPSULE", training_frame=fr)
+    p = g.predict(fr).as_data_frame()["p1"].values
+    d = np.abs(p - p_ref)
+    assert d.max() < 0.13 and d.mean() < 0.03, (d.max(), d.mean())
+    assert g.auc() == pytest.approx(0.9801618150931445, abs=1e-3)
+    assert g.logloss() == pytest.approx(0.2675723908575812, rel=0.03)
