@@ -353,6 +353,76 @@ class _Tree:
         return out
 
 
+# ------------------------------------------------------------- native walk
+_FOREST = [False, None]
+
+
+def _forest_lib():
+    """libmojo_forest.so (h2o3_amd/native/mojo_forest.cpp, built with the
+    other native libraries) via ctypes, or None (numpy walk)."""
+    if _FOREST[0]:
+        return _FOREST[1]
+    _FOREST[0] = True
+    if os.environ.get("H2O3_MOJO_NATIVE", "1") != "1":
+        return None
+    import ctypes
+    p = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ops", "lib", "libmojo_forest.so")
+    if not os.path.exists(p):
+        return None
+    try:
+        lib = ctypes.CDLL(p)
+    except OSError:
+        return None
+    cv = ctypes.c_void_p
+    lib.h2o_mojo_forest_score.argtypes = [ctypes.c_longlong, ctypes.c_int, cv, ctypes.c_int] + [cv] * 18 + \
+        [ctypes.c_int, cv, ctypes.c_double, cv, ctypes.c_int]
+    _FOREST[1] = lib
+    return lib
+
+
+def _pack_forest(trees):
+    """[(output column, _Tree)] -> contiguous arrays of the native walk."""
+    cat = lambda xs, dt: np.ascontiguousarray(np.concatenate(xs) if xs else np.zeros(0), dtype=dt)  # noqa: E731
+    ts = [t for _, t in trees]
+    nn = [0 if t.root_leaf is not None else len(t.col) for t in ts]
+    nl = [0 if t.root_leaf is not None else len(t.leaf) for t in ts]
+    nr = [t.raw.size for t in ts]
+    off = lambda v: np.ascontiguousarray(np.concatenate([[0], np.cumsum(v)]), dtype=np.int64)  # noqa: E731
+    live = [t for t in ts if t.root_leaf is None]
+    pk = {
+        "ntrees": len(ts),
+        "node_off": off(nn), "leaf_off": off(nl), "raw_off": off(nr),
+        "raw_len": np.ascontiguousarray(nr, dtype=np.int64),
+        "col": cat([t.col for t in live], np.int32), "kind": cat([t.kind for t in live], np.int8),
+        "split": cat([t.split for t in live], np.float64), "na_left": cat([t.na_left for t in live], np.uint8),
+        "bs_off": cat([t.bs_off for t in live], np.int64), "bs_n": cat([t.bs_n for t in live], np.int64),
+        "bs_pos": cat([t.bs_pos for t in live], np.int64), "left": cat([t.left for t in live], np.int64),
+        "right": cat([t.right for t in live], np.int64), "leaf": cat([t.leaf for t in live], np.float64),
+        "raw": cat([t.raw for t in ts], np.uint8),
+        "root_leaf": np.ascontiguousarray([t.root_leaf if t.root_leaf is not None else 0.0 for t in ts],
+                                          dtype=np.float64),
+        "has_root": np.ascontiguousarray([t.root_leaf is not None for t in ts], dtype=np.uint8),
+        "tree_out": np.ascontiguousarray([o for o, _ in trees], dtype=np.int32),
+    }
+    return pk
+
+
+def _forest_score(lib, pk, X, preds, version, dom_len):
+    import ctypes
+    Xc = np.ascontiguousarray(X, dtype=np.float64)
+    dl = None if dom_len is None else np.ascontiguousarray(dom_len, dtype=np.int32)
+    P = lambda a: None if a is None else a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    assert preds.flags.c_contiguous and preds.dtype == np.float64
+    rc = lib.h2o_mojo_forest_score(
+        Xc.shape[0], Xc.shape[1], P(Xc), pk["ntrees"], P(pk["node_off"]), P(pk["leaf_off"]), P(pk["raw_off"]),
+        P(pk["raw_len"]), P(pk["col"]), P(pk["kind"]), P(pk["split"]), P(pk["na_left"]), P(pk["bs_off"]),
+        P(pk["bs_n"]), P(pk["bs_pos"]), P(pk["left"]), P(pk["right"]), P(pk["leaf"]), P(pk["raw"]),
+        P(pk["root_leaf"]), P(pk["has_root"]), P(pk["tree_out"]), preds.shape[1], P(preds), float(version), P(dl),
+        int(os.environ.get("H2O3_MOJO_THREADS", "0")))
+    if rc != 0:
+        raise RuntimeError(f"h2o_mojo_forest_score failed: {rc}")
+
+
 # ------------------------------------------------------------------- models
 class H2OMojoModel:
     """A reference-layout MOJO.  predict(df) returns the reference's output
@@ -1297,6 +1367,16 @@ class H2OMojoModel:
         preds = np.zeros((X.shape[0], 1 + K if K > 1 else 1))
         off = 0 if K == 1 else 1
         dl = self.dom_len if self.version >= 1.2 else None
+        lib = _forest_lib()
+        if lib is not None and X.shape[0] >= 64:
+            # native per-row walk of every tree (native/mojo_forest.cpp); the
+            # numpy level-by-level walk below is the fallback and the spec
+            pk = self.__dict__.get("_forest_pack")
+            if pk is None:
+                pk = self._forest_pack = _pack_forest(
+                    [(off + ci, t) for ci in range(self.ntrees_per_group) for t in self.trees[ci] if t is not None])
+            _forest_score(lib, pk, X, preds, self.version, dl)
+            return preds
         for ci in range(self.ntrees_per_group):
             acc = preds[:, off + ci]
             for t in self.trees[ci]:
