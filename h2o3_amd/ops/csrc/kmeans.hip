@@ -335,8 +335,11 @@ __global__ __launch_bounds__(KM_THREADS) void kmeans_lloyd_kernel(
 // MODE 1 (skinny GEMM, PCA / SVD projections): the same MFMA tiles write the
 // dot products out[row][j] = x_row . c_j (f32, row-major [N][k]) instead of
 // the arg-min -- X read once, no library GEMM.
-template <int KT, int MAXNV, int MODE = 0>
-__global__ __launch_bounds__(256) void kmeans_assign_kernel(const float* __restrict__ X, long long N, int P,
+// NW waves per workgroup; PF (NW == 4): the next tile is prefetched into a
+// second register set, else (NW == 6, 3 waves per SIMD) occupancy hides the
+// loads and the register set is dropped.
+template <int KT, int MAXNV, int MODE = 0, int NW = 4>
+__global__ __launch_bounds__(64 * NW) void kmeans_assign_kernel(const float* __restrict__ X, long long N, int P,
                                                             const float* __restrict__ Cin,
                                                             const float* __restrict__ cn, int k,
                                                             int* __restrict__ assign, float* __restrict__ d2out) {
@@ -348,22 +351,23 @@ __global__ __launch_bounds__(256) void kmeans_assign_kernel(const float* __restr
   float* Cs = ldsa;                          // [KP][S]
   float* cns = Cs + KP * S;                  // [KP]
   const int tid = threadIdx.x;
-  for (int e = tid; e < KP * S; e += 256) {
+  constexpr bool PF = NW == 4;
+  for (int e = tid; e < KP * S; e += 64 * NW) {
     const int j = e / S, c = e - j * S;
     Cs[e] = (j < k && c < P) ? Cin[(long long)j * P + c] : 0.f;
   }
-  for (int j = tid; j < KP; j += 256) cns[j] = (j < k && cn != nullptr) ? cn[j] : INFINITY;
+  for (int j = tid; j < KP; j += 64 * NW) cns[j] = (j < k && cn != nullptr) ? cn[j] : INFINITY;
   __syncthreads();
   const int lane = tid & 63, wv = tid >> 6;
   const int li = lane & 15, g = lane >> 4;
   const int Pq = P16 >> 2;                   // k-range per lane group (multiple of 4)
   const int nv = Pq >> 2;                    // float4 per lane
   const long long ntiles = (N + 15) >> 4;
-  const long long nwaves = (long long)gridDim.x * 4;
-  long long t = (long long)xcd_remap(blockIdx.x, gridDim.x) * 4 + wv;
+  const long long nwaves = (long long)gridDim.x * NW;
+  long long t = (long long)xcd_remap(blockIdx.x, gridDim.x) * NW + wv;
   const float* cb = Cs + li * S + g * Pq;
-  f32x4 A[MAXNV], B[MAXNV];
-  auto load = [&](long long tt, f32x4 (&R)[MAXNV]) {
+  f32x4 A[MAXNV], B[PF ? MAXNV : 1];
+  auto load = [&](long long tt, f32x4* R) {
     const long long row = tt * 16 + li;
     const bool okr = row < N;
     const float* src = X + row * (long long)P + g * Pq;
@@ -374,10 +378,14 @@ __global__ __launch_bounds__(256) void kmeans_assign_kernel(const float* __restr
       R[v] = q;
     }
   };
-  if (t < ntiles) load(t, A);
+  if (PF && t < ntiles) load(t, A);
   for (; t < ntiles; t += nwaves) {
     const bool more = t + nwaves < ntiles;
-    if (more) load(t + nwaves, B);           // next tile in flight during the MFMAs
+    if constexpr (PF) {
+      if (more) load(t + nwaves, B);         // next tile in flight during the MFMAs
+    } else {
+      load(t, A);
+    }
     f32x4 acc[KT];
 #pragma unroll
     for (int q = 0; q < KT; ++q) acc[q] = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -444,29 +452,39 @@ __global__ __launch_bounds__(256) void kmeans_assign_kernel(const float* __restr
         d2out[row] = fmaxf(xs + best, 0.f);
       }
     }
-    if (more) {
+    if constexpr (PF) {
+      if (more) {
 #pragma unroll
-      for (int v = 0; v < MAXNV; ++v) A[v] = B[v];
+        for (int v = 0; v < MAXNV; ++v) A[v] = B[v];
+      }
     }
   }
+}
+
+template <int KT, int MAXNV, int MODE, int NW>
+static int ka_launch3(const float* X, long long N, int P, const float* C, const float* cn, int k, int* assign,
+                      float* d2, int G, hipStream_t s, int* per_cu_out) {
+  const int P16 = (P + 15) & ~15, KP = ((k + 15) >> 4) * 16;
+  const size_t lds = ((size_t)KP * (P16 + 4) + KP) * sizeof(float);
+  auto kern = kmeans_assign_kernel<KT, MAXNV, MODE, NW>;
+  hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return (int)e;
+  if (per_cu_out) {
+    int pc = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, kern, 64 * NW, lds) != hipSuccess) return -1;
+    *per_cu_out = pc;
+    return 0;
+  }
+  hipLaunchKernelGGL(kern, dim3(G), dim3(64 * NW), lds, s, X, N, P, C, cn, k, assign, d2);
+  H2O_CHECK_LAUNCH();
 }
 
 template <int KT, int MAXNV, int MODE = 0>
 static int ka_launch2(const float* X, long long N, int P, const float* C, const float* cn, int k, int* assign,
                       float* d2, int G, hipStream_t s, int* per_cu_out) {
-  const int P16 = (P + 15) & ~15, KP = ((k + 15) >> 4) * 16;
-  const size_t lds = ((size_t)KP * (P16 + 4) + KP) * sizeof(float);
-  auto kern = kmeans_assign_kernel<KT, MAXNV, MODE>;
-  hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  if (e != hipSuccess) return (int)e;
-  if (per_cu_out) {
-    int pc = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, kern, 256, lds) != hipSuccess) return -1;
-    *per_cu_out = pc;
-    return 0;
-  }
-  hipLaunchKernelGGL(kern, dim3(G), dim3(256), lds, s, X, N, P, C, cn, k, assign, d2);
-  H2O_CHECK_LAUNCH();
+  // NW = 6 (3 waves per SIMD, no register prefetch) measured slower at
+  // k = 128: 56.9 vs 47.0 ms per Lloyd iteration (profiles/README.md round 6)
+  return ka_launch3<KT, MAXNV, MODE, 4>(X, N, P, C, cn, k, assign, d2, G, s, per_cu_out);
 }
 
 template <int KT, int MODE>
