@@ -26,10 +26,18 @@ them.  Here nothing crosses to the host inside a tree:
   asynchronously to pinned memory and decoded on the host when the forest is
   next read.
 
+Row sampling (sample_rate, sample_rate_per_class) enters as the residual
+pass's 0/1 weight buffer (NaN residual = out-of-sample row, as in the level
+loop); per-node column sampling (col_sample_rate, its change per level) as
+a device kernel that builds each level's eligibility mask from the parent
+records with the level loop's per-node samples (dt_colmask_kernel), seeds
+drawn per tree from the grower's generator exactly as the level loop draws
+them.
+
 Scope (everything else takes the level loop of engine.py): bernoulli /
 gaussian GBM, K = 1, 0/1 row weights, numeric features with one-byte codes
-on the bin-major histogram kernel, no per-node column sampling, monotone or
-interaction constraints, adaptive histogram types, max_depth <= 11.
+on the bin-major histogram kernel, no monotone or interaction constraints,
+no adaptive histogram types, max_depth <= 11.
 """
 from __future__ import annotations
 
@@ -69,6 +77,7 @@ def _libs():
                                    _ci, _cll, _ci, _cv, _cv, _cv, _cv]
         lh.h2o_gbm_grad.argtypes = [_cv, _cv, _cv, _ci, _cll, _cv, _cv, _cv]
         lh.h2o_iota_i32.argtypes = [_cv, _cll, _cv]
+        lh.h2o_dt_colmask.argtypes = [_ci, _cv, _cv, _cv, _cv, _cv, _ci, _ci, _cv, _cv]
         lh._typed_dt = True
     if not getattr(ls, "_typed_dt", False):
         ls.h2o_split_find_b.argtypes = [_cv, _ci, _ci, _ci, _cv, _cv, _cv] + [_cd] * 5 + [_ci, _cv, _cv, _ci, _cv]
@@ -94,16 +103,16 @@ def supported(drv) -> str | None:
         return "distribution"
     if drv.mono_on or drv.noise_bw != 0 or gp.interaction_sets:
         return "constraints / prediction noise"
-    if not (drv._unit_weights and drv._base_unit):
-        return "row weights / row sampling"
+    if not drv._base_unit:
+        return "row weights other than 0/1"
     if any(bd.is_cat) or bd.code_bytes != 1 or bd.Bs > 256 or bd.Bs % 4 or bd.Fp % 16:
         return "categorical features / wide codes"
     if getattr(bd, "hist_type", "auto") in ("uniformadaptive", "random", "roundrobin"):
         return "adaptive histogram type"
     if gp.max_depth > MAX_DEPTH or gp.max_depth < 1:
         return "max_depth"
-    if gp.col_sample_rate < 1.0 or gp.col_sample_rate_change_per_level != 1.0 or (gp.mtries or -1) > 0:
-        return "per-node column sampling"
+    if (gp.mtries or -1) > 0:
+        return "mtries"
     if gp.max_leaves:
         return "max_leaves"
     if tree_ops.bm_groups(bd.F, bd.Fp, bd.Bs, True) is None:
@@ -195,6 +204,17 @@ class DevTreeGBM:
         else:
             self.pcodes, self.prs, self.pfs = bd.codes, bd.Fp, 1
         self.cutmat = g._cut_matrix()
+        # row sampling: the residual pass reads a static 0/1 weight buffer
+        self.sampled = not drv._unit_weights
+        self.wbuf = torch.ones(N, dtype=torch.float32, device=dev) if self.sampled else None
+        # per-node column sampling: per-tree eligible ids / count and per-level
+        # (k, seed) in device buffers read by dt_colmask_kernel
+        self.colsamp = gp.col_sample_rate < 1.0 or gp.col_sample_rate_change_per_level != 1.0
+        if self.colsamp:
+            self.cs_elig = torch.zeros(max(self.F, 1), dtype=torch.int64, device=dev)
+            self.cs_m = torch.zeros(1, dtype=torch.int32, device=dev)
+            self.cs_k = torch.zeros(max(D, 1), dtype=torch.int32, device=dev)
+            self.cs_seed = torch.zeros(max(D, 1), dtype=torch.int64, device=dev)
         self.graph = None
         self._hv = [None, None]
         self._k = 0
@@ -298,6 +318,10 @@ class DevTreeGBM:
         H, wyy = self._hist(d, cur)
         recl = self._rec_lvl(d)
         s = _stream()
+        if self.colsamp:
+            rp = self._rec_lvl(d - 1) if d > 0 else None
+            _ck(lh.h2o_dt_colmask(d, _ptr(rp), _ptr(self.cs_elig), _ptr(self.cs_m), _ptr(self.cs_k),
+                                  _ptr(self.cs_seed), self.f0, self.Fl, _ptr(self.okm), s), "dt_colmask")
         _ck(ls.h2o_split_find_b(_ptr(H), self.Fl, n, Bs, _ptr(wyy), _ptr(self.okm), _ptr(self.mono),
                                 float(gp.min_rows), float(gp.min_split_improvement), float(gp.reg_lambda),
                                 float(gp.reg_alpha), float(gp.gamma), 0, _ptr(self.split_out), None, 0, s),
@@ -329,8 +353,8 @@ class DevTreeGBM:
         if not hasattr(self, "_y"):
             self._y = y.contiguous().to(torch.float32)
         f = drv._f[:, 0]
-        _ck(lh.h2o_gbm_grad(_ptr(self._y), _ptr(f), None, 1 if self.bern else 0, self.N, _ptr(self.pos[0]),
-                            _ptr(self.dbuf), s), "gbm_grad")
+        _ck(lh.h2o_gbm_grad(_ptr(self._y), _ptr(f), _ptr(self.wbuf) if self.sampled else None,
+                            1 if self.bern else 0, self.N, _ptr(self.pos[0]), _ptr(self.dbuf), s), "gbm_grad")
         _ck(lh.h2o_iota_i32(_ptr(self.ridx[0]), self.N, s), "iota")
         self.rec.zero_()
         self.sums.zero_()
@@ -352,11 +376,42 @@ class DevTreeGBM:
                                     _ptr(self.dbuf), _ptr(self.counts), s), "leaf_scatter_dev")
         self.cur = cur
 
-    def run(self, lr, pending):
+    def set_col_sampling(self, tree_mask):
+        """Per-tree inputs of dt_colmask_kernel: the eligible features (the
+        per-tree column sample) and, per level, k and the seed -- drawn from
+        the grower's generator in the level loop's order (engine._col_sel:
+        one draw per splitting level that samples)."""
+        if not self.colsamp:
+            return
+        g, gp, F, D = self.drv.grower, self.gp, self.F, self.D
+        base = np.ones(F, dtype=bool) if tree_mask is None else np.asarray(tree_mask, dtype=bool)
+        elig = np.nonzero(base)[0]
+        m = int(elig.size)
+        ks = np.zeros(D, dtype=np.int32)
+        seeds = np.zeros(D, dtype=np.int64)
+        for d in range(D):
+            rate = gp.col_sample_rate * (gp.col_sample_rate_change_per_level ** d)
+            k = max(1, int(np.floor(rate * m + 0.5))) if rate < 1.0 else m
+            if k >= m:
+                ks[d] = m
+            else:
+                ks[d] = k
+                seeds[d] = int(g.rng.randint(0, 2 ** 31 - 1))
+        e = np.zeros(max(F, 1), dtype=np.int64)
+        e[:m] = elig
+        self.cs_elig.copy_(torch.from_numpy(e))
+        self.cs_m.fill_(m)
+        self.cs_k.copy_(torch.from_numpy(ks))
+        self.cs_seed.copy_(torch.from_numpy(seeds))
+
+    def run(self, lr, pending, w=None):
         """Grow one tree; `pending`: the previous tree's scatter (dbuf) has not
-        been folded into f yet.  Returns (host record view, event)."""
+        been folded into f yet; `w`: this tree's 0/1 row weights (row
+        sampling).  Returns (host record view, event)."""
         if not pending:
             self.dbuf.zero_()
+        if self.sampled:
+            self.wbuf.copy_(w)
         self.lr_t.fill_(float(lr))
         if not self.bern:
             # gaussian: per-tree residual bound for the fixed-point scales (the

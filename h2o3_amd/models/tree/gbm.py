@@ -272,7 +272,7 @@ class GBMDriver:
         lr = self.lr * (float(p.get("learn_rate_annealing", 1.0)) ** (self.iter - 1))
         maxabs = float(p.get("max_abs_leafnode_pred", 1.79e308))
         if self.K == 1 and self._devtree_ok():
-            self._step_devtree(lr)
+            self._step_devtree(lr, w)
             return
         if self.K == 1:
             dpend = self.__dict__.get("_dpend")
@@ -441,17 +441,18 @@ class GBMDriver:
         self._devtree_why = why
         return False
 
-    def _step_devtree(self, lr):
+    def _step_devtree(self, lr, w=None):
         """One boosting iteration as one device-resident tree (graph replay on
         one rank): residual, every level, leaf values and the per-row leaf
         scatter without a host round trip; the tree's record is decoded on the
         host while the GPU grows the next one."""
         dt = self._devtree
         dt.set_tree_cols(self.gp.tree_col_mask)
+        dt.set_col_sampling(self.gp.tree_col_mask)
         pending = self.__dict__.get("_dpend") is not None
         self._dpend = None
         with phase("gbm.devtree"):
-            hrec, ev = dt.run(lr, pending)
+            hrec, ev = dt.run(lr, pending, w)
         self._dpend = dt.dbuf
         self._resolve_pending()
         self._pending = ("dev", hrec, ev)

@@ -2357,3 +2357,80 @@ int h2o_leaf_scatter_dev(const int* ridx, const int* work, int n_cap, const floa
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Device-resident tree, per-node column sampling (GBM col_sample_rate /
+// col_sample_rate_change_per_level): the level's [2^d][Fl] split-eligibility
+// mask built on the device from the parent records.  Heap slot i of level d
+// exists when its parent split; the existing slots are ranked in heap order
+// (the level loop's frontier order), and node r draws exactly the sample
+// col_sample_kernel draws for frontier node r with the same seed: selection
+// sampling of k of the m eligible features (the per-tree column sample) from
+// a splitmix64 hash of (seed, r, j).  seed / k / m come from device buffers
+// the host refreshes per tree, so the launch stays inside the captured graph.
+extern "C" __global__ __launch_bounds__(1024) void dt_colmask_kernel(
+    int d, const double* __restrict__ rec_par, const long long* __restrict__ elig, const int* __restrict__ m_dev,
+    const int* __restrict__ k_dev, const unsigned long long* __restrict__ seed_dev, int f0, int Fl,
+    unsigned char* __restrict__ okm) {
+  __shared__ int wsum[16];
+  __shared__ int carry;
+  const int n = 1 << d;
+  const int m = m_dev[0], k = k_dev[d];
+  const unsigned long long seed = seed_dev[d];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (int base = 0; base < n; base += blockDim.x) {
+    const int i = base + threadIdx.x;
+    int ex = 0;
+    if (i < n) ex = d == 0 ? 1 : (rec_par[(size_t)(i >> 1) * DT_RS + DT_OK] > 0.0 ? 1 : 0);
+    int a = ex;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int t = __shfl_up(a, o, 64);
+      if (lane >= o) a += t;
+    }
+    if (lane == 63) wsum[wv] = a;
+    __syncthreads();
+    if (wv == 0) {
+      int x = lane < nwv ? wsum[lane] : 0;
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        const int t = __shfl_up(x, o, 64);
+        if (lane >= o) x += t;
+      }
+      if (lane < nwv) wsum[lane] = x;
+    }
+    __syncthreads();
+    const int rank = carry + (wv > 0 ? wsum[wv - 1] : 0) + a - ex;
+    if (i < n) {
+      unsigned char* row = okm + (size_t)i * Fl;
+      for (int f = 0; f < Fl; ++f) row[f] = 0;
+      if (ex) {
+        const unsigned long long b0 = smix64(seed ^ ((unsigned long long)rank * 0xD1B54A32D192ED03ull));
+        int taken = 0;
+        for (int j = 0; j < m && taken < k; ++j) {
+          const double u = (double)(smix64(b0 + (unsigned long long)j) >> 11) * (1.0 / 9007199254740992.0);
+          if (u * (double)(m - j) < (double)(k - taken)) {
+            ++taken;
+            const long long f = elig[j] - f0;
+            if (f >= 0 && f < Fl) row[f] = 1;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) carry += wsum[nwv - 1];
+    __syncthreads();
+  }
+}
+
+extern "C" int h2o_dt_colmask(int d, const double* rec_par, const long long* elig, const int* m_dev,
+                              const int* k_dev, const unsigned long long* seed_dev, int f0, int Fl,
+                              unsigned char* okm, hipStream_t s) {
+  if (d < 0 || d > 12 || Fl <= 0) return (int)hipErrorInvalidValue;
+  if (d > 0 && rec_par == nullptr) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(dt_colmask_kernel, dim3(1), dim3(1024), 0, s, d, rec_par, elig, m_dev, k_dev, seed_dev, f0,
+                     Fl, okm);
+  return (int)hipGetLastError();
+}

@@ -112,3 +112,25 @@ def test_devtree_model_predicts_like_training_state(monkeypatch):
     p = m.predict(fr).as_data_frame()["p1"].values
     assert m.auc() > 0.7
     assert np.isfinite(p).all() and p.min() >= 0 and p.max() <= 1
+
+
+@pytest.mark.parametrize("kw", [dict(sample_rate=0.7), dict(col_sample_rate=0.6),
+                                dict(sample_rate=0.8, col_sample_rate=0.8, col_sample_rate_per_tree=0.8,
+                                     col_sample_rate_change_per_level=0.9)])
+def test_devtree_row_and_column_sampling(monkeypatch, kw):
+    """AutoML's GBM sampling settings on the device-resident tree: row sampling
+    as the residual pass's 0/1 weights (NaN = out of sample), per-node column
+    samples built on the device with the level loop's per-node draws -- the
+    same trees as the level loop."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    fr, names = _frame(200_000, 32, "bernoulli", seed=11)
+    d1, f1, p1 = _fit(monkeypatch, fr, names, True, ntrees=5, max_depth=6, **kw)
+    assert getattr(d1, "_devtree", None) is not None, getattr(d1, "_devtree_why", None)
+    d0, f0, p0 = _fit(monkeypatch, fr, names, False, ntrees=5, max_depth=6, **kw)
+    for ta, tb in zip(f1.trees, f0.trees):
+        np.testing.assert_array_equal(np.asarray(ta.feat), np.asarray(tb.feat))
+        np.testing.assert_array_equal(np.asarray(ta.left), np.asarray(tb.left))
+        np.testing.assert_allclose(np.asarray(ta.thr), np.asarray(tb.thr))
+        np.testing.assert_allclose(np.asarray(ta.value), np.asarray(tb.value), rtol=1e-5, atol=1e-8)
+    np.testing.assert_allclose(p1, p0, rtol=1e-5, atol=1e-6)
