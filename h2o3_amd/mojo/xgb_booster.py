@@ -168,11 +168,54 @@ class Booster:
             active[r] = cleft[cur[r]] != -1
         return cur
 
+    def _native_acc(self, F, K):
+        """f32 tree sums from the native walk (native/mojo_forest.cpp
+        h2o_xgb_forest_score: the numpy loop's f32 adds in the same order),
+        or None without the library."""
+        from .h2o_mojo import _forest_lib
+        lib = _forest_lib()
+        if lib is None or F.shape[0] < 64 or not self.trees:
+            return None
+        import ctypes
+        if not getattr(lib, "_typed_xgb", False):
+            cv = ctypes.c_void_p
+            lib.h2o_xgb_forest_score.argtypes = [ctypes.c_longlong, ctypes.c_int, cv, ctypes.c_int] + [cv] * 8 + \
+                [ctypes.c_int, cv, ctypes.c_int]
+            lib._typed_xgb = True
+        pk = self.__dict__.get("_xpack")
+        if pk is None:
+            nodes = [nd for nd, _ in self.trees]
+            sizes = [len(nd) for nd in nodes]
+            cat = np.concatenate(nodes) if nodes else np.zeros(0, dtype=_NODE_DT)
+            pk = self._xpack = {
+                "off": np.ascontiguousarray(np.concatenate([[0], np.cumsum(sizes)]), dtype=np.int64),
+                "cleft": np.ascontiguousarray(cat["cleft"], dtype=np.int32),
+                "cright": np.ascontiguousarray(cat["cright"], dtype=np.int32),
+                "feat": np.ascontiguousarray(cat["sindex"] & 0x7FFFFFFF, dtype=np.int32),
+                "dleft": np.ascontiguousarray(cat["sindex"] >> 31, dtype=np.uint8),
+                "info": np.ascontiguousarray(cat["info"], dtype=np.float32),
+                "group": np.ascontiguousarray(self.tree_info[:len(nodes)], dtype=np.int32),
+                "wdrop": None if self.weight_drop is None else
+                np.ascontiguousarray(self.weight_drop[:len(nodes)], dtype=np.float32),
+            }
+        Fc = np.ascontiguousarray(F, dtype=np.float32)
+        acc = np.zeros((F.shape[0], K), dtype=np.float32)
+        P = lambda a: None if a is None else a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+        rc = lib.h2o_xgb_forest_score(Fc.shape[0], Fc.shape[1], P(Fc), len(self.trees), P(pk["off"]), P(pk["cleft"]),
+                                      P(pk["cright"]), P(pk["feat"]), P(pk["dleft"]), P(pk["info"]), P(pk["group"]),
+                                      P(pk["wdrop"]), K, P(acc), 0)
+        if rc != 0:
+            raise RuntimeError(f"h2o_xgb_forest_score failed: {rc}")
+        return acc
+
     def margins(self, F: np.ndarray) -> np.ndarray:
         """[n, num_output_group] raw margins (base margin + tree sums)."""
         F = np.asarray(F, dtype=np.float32)
         K = max(1, int(self.num_output_group))
         out = np.full((F.shape[0], K), self.base_margin, dtype=np.float64)
+        nacc = self._native_acc(F, K)
+        if nacc is not None:
+            return out + nacc
         acc = np.zeros((F.shape[0], K), dtype=np.float32)
         for t, (nodes, _) in enumerate(self.trees):
             leaf = self.tree_leaves(nodes, F)

@@ -120,3 +120,70 @@ extern "C" int h2o_mojo_forest_score(long long n, int ncols, const double* X, in
   for (auto& t : th) t.join();
   return 0;
 }
+
+// XGBoost booster trees (mojo/xgb_booster.py, the legacy binary layout): per
+// row, trees in booster order, f32 "v < cond goes left", missing to the
+// node's default direction, leaf value (x the DART weight) added in f32 into
+// the tree's output group -- the same f32 sums, in the same order, as the
+// numpy walk (XGBoostJavaMojoModel / Predictor.predict semantics).
+namespace {
+struct XgbForest {
+  long long n;
+  int nfeat;
+  const float* F;
+  int ntrees;
+  const long long* node_off;
+  const int32_t* cleft;
+  const int32_t* cright;
+  const int32_t* feat;
+  const uint8_t* dleft;
+  const float* info;
+  const int32_t* group;
+  const float* wdrop;
+  int ngroups;
+  float* acc;
+};
+
+void xgb_rows(const XgbForest& X, long long r0, long long r1) {
+  for (long long r = r0; r < r1; ++r) {
+    const float* row = X.F + r * X.nfeat;
+    float* a = X.acc + r * X.ngroups;
+    for (int t = 0; t < X.ntrees; ++t) {
+      const long long o = X.node_off[t];
+      int c = 0;
+      while (X.cleft[o + c] != -1) {
+        const float v = row[X.feat[o + c]];
+        const bool left = std::isnan(v) ? X.dleft[o + c] != 0 : v < X.info[o + c];
+        c = left ? X.cleft[o + c] : X.cright[o + c];
+      }
+      float lv = X.info[o + c];
+      if (X.wdrop != nullptr) lv = lv * X.wdrop[t];
+      a[X.group[t]] += lv;
+    }
+  }
+}
+}  // namespace
+
+extern "C" int h2o_xgb_forest_score(long long n, int nfeat, const float* F, int ntrees, const long long* node_off,
+                                    const int32_t* cleft, const int32_t* cright, const int32_t* feat,
+                                    const uint8_t* dleft, const float* info, const int32_t* group,
+                                    const float* wdrop, int ngroups, float* acc, int nthreads) {
+  if (n <= 0 || ntrees <= 0) return 0;
+  if (!F || !acc || nfeat <= 0 || ngroups <= 0) return 1;
+  XgbForest X{n, nfeat, F, ntrees, node_off, cleft, cright, feat, dleft, info, group, wdrop, ngroups, acc};
+  int nt = nthreads > 0 ? nthreads : (int)std::max(1u, std::thread::hardware_concurrency());
+  nt = (int)std::min<long long>(nt, std::max<long long>(1, n / 256));
+  if (nt <= 1) {
+    xgb_rows(X, 0, n);
+    return 0;
+  }
+  std::vector<std::thread> th;
+  const long long per = (n + nt - 1) / nt;
+  for (int i = 0; i < nt; ++i) {
+    const long long a = i * per, b = std::min(n, a + per);
+    if (a >= b) break;
+    th.emplace_back(xgb_rows, std::cref(X), a, b);
+  }
+  for (auto& t : th) t.join();
+  return 0;
+}
