@@ -29,6 +29,8 @@
 //     (CrossEntropy) or the Quadratic softmax gradient, one wave per row.
 #include "common.h"
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 
 enum { ACT_LINEAR = 0, ACT_TANH = 1, ACT_RELU = 2, ACT_ELU = 3, ACT_MAXOUT = 4 };
 
@@ -894,59 +896,70 @@ int h2o_dl_mlp_step(int nl, const int* width, const int* act, const float* drop,
 // dimension of each operand so the global loads coalesce for every
 // transpose.  Blocks are mapped XCD-aware.
 // ---------------------------------------------------------------------------
-#define DLG_TM 64
-#define DLG_TN 64
 #define DLG_TK 32
-__global__ __launch_bounds__(256, 4) void dl_gemm_kernel(int M, int N, int K, const float* __restrict__ A, long long sam,
-                                                      long long sak, const float* __restrict__ B, long long sbk,
-                                                      long long sbn, float* __restrict__ C, int ntn, int ntiles,
-                                                      int kchunk, float* __restrict__ Cw) {
+// BM x BN blocks of 16 x 16 per wave, 2 x 2 waves per workgroup: the
+// workgroup tile is (32 BM) x (32 BN).  BM = BN = 2 (64 x 64) is the default;
+// (2, 4) and (4, 4) trade grid size for operand reuse (H2O3_DL_GEMM_TILE).
+template <int BM, int BN>
+__global__ __launch_bounds__(256, 2) void dl_gemm_kernel(int M, int N, int K, const float* __restrict__ A, long long sam,
+                                                         long long sak, const float* __restrict__ B, long long sbk,
+                                                         long long sbn, float* __restrict__ C, int ntn, int ntiles,
+                                                         int kchunk, float* __restrict__ Cw) {
+  constexpr int TM = 32 * BM, TN = 32 * BN;
+  constexpr int LA = TM * DLG_TK / 256, LB = TN * DLG_TK / 256;   // staged elements per thread
   // both operands k-inner in LDS (B transposed to [n][k]), rows padded to
   // 36 floats: one ds_read_b128 gives a lane 4 consecutive k of its row, and
   // the 16 rows of a 16-lane group hit distinct 4-bank groups
-  __shared__ __align__(16) float As[2][DLG_TM][DLG_TK + 4];   // [m][k]
-  __shared__ __align__(16) float Bs[2][DLG_TN][DLG_TK + 4];   // [n][k]
+  __shared__ __align__(16) float As[2][TM][DLG_TK + 4];   // [m][k]
+  __shared__ __align__(16) float Bs[2][TN][DLG_TK + 4];   // [n][k]
   const int nwg = gridDim.x;
   const int bid0 = xcd_remap(blockIdx.x, nwg);
   const int ks = bid0 / ntiles, bid = bid0 - ks * ntiles;   // split-K slice, output tile
   const int tm = bid / ntn, tn = bid - (bid / ntn) * ntn;
   const int kbeg = ks * kchunk, kend = min(K, kbeg + kchunk);
-  const int m0 = tm * DLG_TM, n0 = tn * DLG_TN;
+  const int m0 = tm * TM, n0 = tn * TN;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int wm = (wv >> 1) * 32, wn = (wv & 1) * 32;
+  const int wm = (wv >> 1) * (16 * BM), wn = (wv & 1) * (16 * BN);
   const bool a_kfast = sak == 1, b_nfast = sbn == 1;
-  // each thread stages 8 elements of each operand per slab (64 x 32 = 2048)
-  float ra[8], rb[8];
+  float ra[LA], rb[LB];
   auto load = [&](int k0) {
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < LA; ++u) {
       const int e = tid + u * 256;
       int m, k;
-      if (a_kfast) { m = e >> 5; k = e & 31; } else { k = e >> 6; m = e & 63; }
+      if (a_kfast) { m = e >> 5; k = e & 31; } else { k = e / TM; m = e - (e / TM) * TM; }
       const int gm = m0 + m, gk = k0 + k;
       ra[u] = (gm < M && gk < kend) ? A[(long long)gm * sam + (long long)gk * sak] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < LB; ++u) {
+      const int e = tid + u * 256;
       int kb, n;
-      if (b_nfast) { kb = e >> 6; n = e & 63; } else { n = e >> 5; kb = e & 31; }
+      if (b_nfast) { kb = e / TN; n = e - (e / TN) * TN; } else { n = e >> 5; kb = e & 31; }
       const int gk2 = k0 + kb, gn = n0 + n;
       rb[u] = (gk2 < kend && gn < N) ? B[(long long)gk2 * sbk + (long long)gn * sbn] : 0.f;
     }
   };
   auto store = [&](int buf) {
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < LA; ++u) {
       const int e = tid + u * 256;
       if (a_kfast) As[buf][e >> 5][e & 31] = ra[u];
-      else As[buf][e & 63][e >> 6] = ra[u];
-      if (b_nfast) Bs[buf][e & 63][e >> 6] = rb[u];
+      else As[buf][e - (e / TM) * TM][e / TM] = ra[u];
+    }
+#pragma unroll
+    for (int u = 0; u < LB; ++u) {
+      const int e = tid + u * 256;
+      if (b_nfast) Bs[buf][e - (e / TN) * TN][e / TN] = rb[u];
       else Bs[buf][e >> 5][e & 31] = rb[u];
     }
   };
   typedef float f4 __attribute__((ext_vector_type(4)));
-  f4 acc[2][2];
+  f4 acc[BM][BN];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < BM; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = (f4){0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < BN; ++j) acc[i][j] = (f4){0.f, 0.f, 0.f, 0.f};
   const int nslab = kend > kbeg ? (kend - kbeg + DLG_TK - 1) / DLG_TK : 0;
   if (nslab > 0) {
     load(kbeg);
@@ -961,25 +974,26 @@ __global__ __launch_bounds__(256, 4) void dl_gemm_kernel(int M, int N, int K, co
     // groups (same permutation on both operands: the sum over k is unchanged)
 #pragma unroll
     for (int c = 0; c < DLG_TK; c += 16) {
-      const f4 a0 = *(const f4*)&As[cur][wm + li][c + 4 * lg];
-      const f4 a1 = *(const f4*)&As[cur][wm + 16 + li][c + 4 * lg];
-      const f4 b0 = *(const f4*)&Bs[cur][wn + li][c + 4 * lg];
-      const f4 b1 = *(const f4*)&Bs[cur][wn + 16 + li][c + 4 * lg];
+      f4 av[BM], bv[BN];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[j], b0[j], acc[0][0], 0, 0, 0);
-        acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[j], b1[j], acc[0][1], 0, 0, 0);
-        acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[j], b0[j], acc[1][0], 0, 0, 0);
-        acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[j], b1[j], acc[1][1], 0, 0, 0);
-      }
+      for (int i = 0; i < BM; ++i) av[i] = *(const f4*)&As[cur][wm + 16 * i + li][c + 4 * lg];
+#pragma unroll
+      for (int j = 0; j < BN; ++j) bv[j] = *(const f4*)&Bs[cur][wn + 16 * j + li][c + 4 * lg];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int i = 0; i < BM; ++i)
+#pragma unroll
+          for (int j = 0; j < BN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i][q], bv[j][q], acc[i][j], 0, 0, 0);
     }
     if (s + 1 < nslab) store(cur ^ 1);
     __syncthreads();
   }
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < BM; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < BN; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int gm = m0 + wm + 16 * i + 4 * lg + r, gn = n0 + wn + 16 * j + li;
@@ -1000,11 +1014,20 @@ __global__ __launch_bounds__(256) void dl_gemm_reduce_kernel(const float* __rest
   }
 }
 
+static int dl_gemm_tile() {   // 0: 64 x 64, 1: 64 x 128, 2: 128 x 128 workgroup tiles (H2O3_DL_GEMM_TILE)
+  static int t = -1;
+  if (t < 0) {
+    const char* e = getenv("H2O3_DL_GEMM_TILE");
+    t = e == nullptr ? 0 : (strcmp(e, "64x128") == 0 ? 1 : (strcmp(e, "128x128") == 0 ? 2 : 0));
+  }
+  return t;
+}
+
 // Split-K plan: slices of K (multiples of the 32-deep slab) until the grid has
 // ~4 workgroups per CU -- the thin products of a step (the 2-unit output
 // layer, the input layer's dW) have few output tiles but K = batch or width.
-static void dl_gemm_plan(int M, int N, int K, int& ksplit, int& kchunk) {
-  const int tiles = ((M + DLG_TM - 1) / DLG_TM) * ((N + DLG_TN - 1) / DLG_TN);
+static void dl_gemm_plan(int M, int N, int K, int TM, int TN, int& ksplit, int& kchunk) {
+  const int tiles = ((M + TM - 1) / TM) * ((N + TN - 1) / TN);
   const int nslab = (K + DLG_TK - 1) / DLG_TK;
   if (tiles <= 0 || nslab <= 0) {
     ksplit = 1;
@@ -1019,9 +1042,16 @@ static void dl_gemm_plan(int M, int N, int K, int& ksplit, int& kchunk) {
   ksplit = K > 0 ? (K + kchunk - 1) / kchunk : 1;
 }
 
+static void dl_gemm_dims(int& TM, int& TN) {
+  const int t = dl_gemm_tile();
+  TM = t == 2 ? 128 : 64;
+  TN = t == 0 ? 64 : 128;
+}
+
 extern "C" long long h2o_dl_gemm_ws(int M, int N, int K) {
-  int ks, kc;
-  dl_gemm_plan(M, N, K, ks, kc);
+  int ks, kc, TM, TN;
+  dl_gemm_dims(TM, TN);
+  dl_gemm_plan(M, N, K, TM, TN, ks, kc);
   return ks > 1 ? (long long)ks * M * N : 0;
 }
 
@@ -1029,16 +1059,28 @@ extern "C" int h2o_dl_gemm(int M, int N, int K, const float* A, long long sam, l
                            long long sbk, long long sbn, float* C, float* ws, long long ws_elems, hipStream_t s) {
   if (M <= 0 || N <= 0) return 0;
   if (K < 0 || !A || !B || !C) return (int)hipErrorInvalidValue;
-  const int ntm = (M + DLG_TM - 1) / DLG_TM, ntn = (N + DLG_TN - 1) / DLG_TN;
+  int TM, TN;
+  dl_gemm_dims(TM, TN);
+  const int ntm = (M + TM - 1) / TM, ntn = (N + TN - 1) / TN;
   int ksplit, kchunk;
-  dl_gemm_plan(M, N, K, ksplit, kchunk);
+  dl_gemm_plan(M, N, K, TM, TN, ksplit, kchunk);
   if (ksplit > 1 && (ws == nullptr || ws_elems < (long long)ksplit * M * N)) {
     ksplit = 1;                               // no workspace: one slice
     kchunk = max(K, 1);
   }
   const int ntiles = ntm * ntn;
-  hipLaunchKernelGGL(dl_gemm_kernel, dim3(ntiles * ksplit), dim3(256), 0, s, M, N, K, A, sam, sak, B, sbk, sbn, C,
-                     ntn, ntiles, kchunk, ksplit > 1 ? ws : (float*)nullptr);
+  float* cw = ksplit > 1 ? ws : (float*)nullptr;
+  const dim3 grid(ntiles * ksplit);
+  const int t = dl_gemm_tile();
+  if (t == 2)
+    hipLaunchKernelGGL((dl_gemm_kernel<4, 4>), grid, dim3(256), 0, s, M, N, K, A, sam, sak, B, sbk, sbn, C, ntn,
+                       ntiles, kchunk, cw);
+  else if (t == 1)
+    hipLaunchKernelGGL((dl_gemm_kernel<2, 4>), grid, dim3(256), 0, s, M, N, K, A, sam, sak, B, sbk, sbn, C, ntn,
+                       ntiles, kchunk, cw);
+  else
+    hipLaunchKernelGGL((dl_gemm_kernel<2, 2>), grid, dim3(256), 0, s, M, N, K, A, sam, sak, B, sbk, sbn, C, ntn,
+                       ntiles, kchunk, cw);
   if (ksplit > 1) {
     const long long mn = (long long)M * N;
     const int g = (int)min((mn + 255) / 256, 4096LL);
