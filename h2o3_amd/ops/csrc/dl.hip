@@ -901,7 +901,7 @@ int h2o_dl_mlp_step(int nl, const int* width, const int* act, const float* drop,
 // workgroup tile is (32 BM) x (32 BN).  BM = BN = 2 (64 x 64) is the default;
 // (2, 4) and (4, 4) trade grid size for operand reuse (H2O3_DL_GEMM_TILE).
 template <int BM, int BN>
-__global__ __launch_bounds__(256, 2) void dl_gemm_kernel(int M, int N, int K, const float* __restrict__ A, long long sam,
+__global__ __launch_bounds__(256, BM * BN <= 4 ? 4 : 2) void dl_gemm_kernel(int M, int N, int K, const float* __restrict__ A, long long sam,
                                                          long long sak, const float* __restrict__ B, long long sbk,
                                                          long long sbn, float* __restrict__ C, int ntn, int ntiles,
                                                          int kchunk, float* __restrict__ Cw) {
