@@ -461,12 +461,126 @@ __global__ __launch_bounds__(64 * NW) void kmeans_assign_kernel(const float* __r
   }
 }
 
+// Two 16-row tiles per wave (the default at KT >= 4; H2O3_KM_RT=1 selects the
+// one-tile kernel above): every center
+// float4 read from LDS feeds the MFMAs of both tiles, so the LDS traffic per
+// MFMA halves and each step has 2 x KT independent accumulators in flight;
+// no register prefetch (the second tile's registers take its place).
+// 100M x 100: k = 128 44.1 ms per Lloyd iteration (46.9 one-tile), k = 64 29.0 (29.9).
+template <int KT, int MAXNV>
+__global__ __launch_bounds__(256) void kmeans_assign2_kernel(const float* __restrict__ X, long long N, int P,
+                                                             const float* __restrict__ Cin,
+                                                             const float* __restrict__ cn, int k,
+                                                             int* __restrict__ assign, float* __restrict__ d2out) {
+  extern __shared__ __align__(16) float ldsa[];
+  const int P16 = (P + 15) & ~15;
+  const int S = P16 + 4;
+  const int nq = (k + 15) >> 4;
+  const int KP = nq * 16;
+  float* Cs = ldsa;
+  float* cns = Cs + KP * S;
+  const int tid = threadIdx.x;
+  for (int e = tid; e < KP * S; e += 256) {
+    const int j = e / S, c = e - j * S;
+    Cs[e] = (j < k && c < P) ? Cin[(long long)j * P + c] : 0.f;
+  }
+  for (int j = tid; j < KP; j += 256) cns[j] = (j < k && cn != nullptr) ? cn[j] : INFINITY;
+  __syncthreads();
+  const int lane = tid & 63, wv = tid >> 6;
+  const int li = lane & 15, g = lane >> 4;
+  const int Pq = P16 >> 2;
+  const int nv = Pq >> 2;
+  const long long ntiles = (N + 15) >> 4;
+  const long long npairs = (ntiles + 1) >> 1;
+  const long long nwaves = (long long)gridDim.x * 4;
+  const float* cb = Cs + li * S + g * Pq;
+  auto load = [&](long long tt, f32x4* R) {
+    const long long row = tt * 16 + li;
+    const bool okr = row < N;
+    const float* src = X + row * (long long)P + g * Pq;
+#pragma unroll
+    for (int v = 0; v < MAXNV; ++v) {
+      f32x4 q = {0.f, 0.f, 0.f, 0.f};
+      if (v < nv && okr && g * Pq + 4 * v < P) q = *(const f32x4*)(src + 4 * v);
+      R[v] = q;
+    }
+  };
+  auto finish = [&](const f32x4* acc, float sq, long long r0) {
+    sq += __shfl_xor(sq, 16, 64);
+    sq += __shfl_xor(sq, 32, 64);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float best = INFINITY;
+      int bi = 0x7fffffff;
+#pragma unroll
+      for (int q = 0; q < KT; ++q) {
+        const int j = q * 16 + li;
+        const float d = q < nq ? cns[j] - 2.f * acc[q][r] : INFINITY;
+        if (d < best) { best = d; bi = j; }
+      }
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        const float ob = __shfl_xor(best, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        if (ob < best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+      }
+      const float xs = __shfl(sq, 4 * g + r, 64);
+      const long long row = r0 + 4 * g + r;
+      if (li == 0 && row < N) {
+        assign[row] = bi < k ? bi : 0;
+        d2out[row] = fmaxf(xs + best, 0.f);
+      }
+    }
+  };
+  for (long long tp = (long long)xcd_remap(blockIdx.x, gridDim.x) * 4 + wv; tp < npairs; tp += nwaves) {
+    f32x4 A0[MAXNV], A1[MAXNV];
+    load(2 * tp, A0);
+    load(2 * tp + 1, A1);
+    f32x4 acc0[KT], acc1[KT];
+#pragma unroll
+    for (int q = 0; q < KT; ++q) { acc0[q] = (f32x4){0.f, 0.f, 0.f, 0.f}; acc1[q] = acc0[q]; }
+    float sq0 = 0.f, sq1 = 0.f;
+#pragma unroll
+    for (int v = 0; v < MAXNV; ++v) {
+      const f32x4 a = A0[v], b = A1[v];
+      sq0 += a[0] * a[0] + a[1] * a[1] + a[2] * a[2] + a[3] * a[3];
+      sq1 += b[0] * b[0] + b[1] * b[1] + b[2] * b[2] + b[3] * b[3];
+      const bool vin = v < nv;
+      f32x4 b4[KT];
+#pragma unroll
+      for (int q = 0; q < KT; ++q) {
+        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+        b4[q] = (vin && q < nq) ? *(const f32x4*)(cb + q * 16 * S + 4 * v) : z;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int q = 0; q < KT; ++q) {
+          acc0[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], b4[q][j], acc0[q], 0, 0, 0);
+          acc1[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(b[j], b4[q][j], acc1[q], 0, 0, 0);
+        }
+    }
+    finish(acc0, sq0, 2 * tp * 16);
+    finish(acc1, sq1, (2 * tp + 1) * 16);
+  }
+}
+
+static int km_assign_rt() {   // row tiles per wave: 2 (default), H2O3_KM_RT=1 for the one-tile kernel
+  static int rt = -1;
+  if (rt < 0) {
+    const char* e = getenv("H2O3_KM_RT");
+    rt = (e != nullptr && atoi(e) == 1) ? 1 : 2;
+  }
+  return rt;
+}
+
 template <int KT, int MAXNV, int MODE, int NW>
 static int ka_launch3(const float* X, long long N, int P, const float* C, const float* cn, int k, int* assign,
                       float* d2, int G, hipStream_t s, int* per_cu_out) {
   const int P16 = (P + 15) & ~15, KP = ((k + 15) >> 4) * 16;
   const size_t lds = ((size_t)KP * (P16 + 4) + KP) * sizeof(float);
-  auto kern = kmeans_assign_kernel<KT, MAXNV, MODE, NW>;
+  auto kern = (MODE == 0 && KT >= 4 && km_assign_rt() == 2) ? kmeans_assign2_kernel<KT, MAXNV>
+                                                             : kmeans_assign_kernel<KT, MAXNV, MODE, NW>;
   hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return (int)e;
   if (per_cu_out) {
