@@ -577,6 +577,7 @@ class H2OGradientBoostingEstimator(SharedTreeEstimator):
         drv = GBMDriver(self, spec)
         self._K = drv.K
         self._driver = drv
+        self._vinc = None          # incremental validation link (_valid_raw_incremental)
         ntrees = int(p["ntrees"])
         if p.get("checkpoint") is not None:
             self._resume_from(drv, p["checkpoint"])
@@ -624,6 +625,7 @@ class H2OGradientBoostingEstimator(SharedTreeEstimator):
                                          if len(drv.forest) else 0.0}
         self._output["init_f"] = drv.init_f
         self._train_f = drv.f
+        self._vinc = None
         del drv.grower
         self._driver = None
         if p.get("calibrate_model") and p.get("calibration_frame") is not None:
@@ -677,9 +679,36 @@ class H2OGradientBoostingEstimator(SharedTreeEstimator):
         if spec.valid is not None:
             self._forest = drv.forest
             self._init_f = drv.init_f
-            vm = self._metrics_from_raw(spec, spec.valid, self._predict_raw(spec.valid))
+            vm = self._metrics_from_raw(spec, spec.valid, self._valid_raw_incremental(spec.valid))
             self._add_metrics(entry, "validation", vm)
         return entry
+
+    def _valid_raw_incremental(self, frame):
+        """Validation predictions at a scoring round from the running link of
+        the trees already scored plus the trees grown since (the forest kernel
+        over the new trees only): scoring every score_tree_interval trees
+        costs O(new trees), not O(all trees) per round."""
+        fo = self._forest
+        T = len(fo)
+        st = self.__dict__.get("_vinc")
+        if st is None or st[0] is not frame or st[1] > T:
+            X = self._score_matrix(frame)
+            f = torch.zeros((X.shape[1], self._K), dtype=torch.float32, device=X.device)
+            st = self._vinc = [frame, 0, f, X]
+        _, t0, f, X = st
+        if T > t0:
+            f += fo.predict_range(X, self._K, t0, T)
+            st[1] = T
+        link = f + torch.tensor(self._init_f, dtype=torch.float32, device=f.device).view(1, -1)
+        off = self._spec.offset_column
+        if off and off in frame.names:
+            link = link + torch.nan_to_num(frame.vec(off).as_float()).view(-1, 1)
+        if self._K > 1:
+            return torch.softmax(link, 1)
+        mu = self._dist.linkinv(link[:, 0])
+        if self._spec.nclasses == 2:
+            return torch.stack([1 - mu, mu], 1)
+        return mu.view(-1, 1)
 
     @staticmethod
     def _add_metrics(entry, prefix, m):
