@@ -129,6 +129,7 @@ class H2OXGBoostEstimator(SharedTreeEstimator):
                 gp.max_depth = 64
         grower = TreeGrower(bd, gp)
         forest = Forest()
+        self._vinc = None          # incremental validation link (gbm._valid_raw_incremental)
         eta = float(p["learn_rate"])
         mds = float(p.get("max_delta_step") or 0.0)
         mabs = float(p.get("max_abs_leafnode_pred") or 0.0)
@@ -256,6 +257,7 @@ class H2OXGBoostEstimator(SharedTreeEstimator):
                         tt.value[i] *= wgt
         self._forest = forest
         self._train_f = f
+        self._vinc = None
         from .shared import forest_varimp
         self._output["variable_importances"] = forest_varimp(forest, spec.x)
         self._output["model_summary"] = {"number_of_trees": len(forest) // K, "booster": booster}
@@ -355,8 +357,11 @@ class H2OXGBoostEstimator(SharedTreeEstimator):
         from .gbm import H2OGradientBoostingEstimator as _G
         _G._add_metrics(entry, "training", self._metrics_from_raw(spec, spec.frame, self._raw_from_f(f)))
         if spec.valid is not None:
-            _G._add_metrics(entry, "validation", self._metrics_from_raw(spec, spec.valid,
-                                                                        self._predict_raw(spec.valid)))
+            # gbtree: the validation link grows by the new trees only (DART
+            # rescales earlier trees, so it re-predicts the forest)
+            dart = (self._parms.get("booster") or "gbtree").lower() == "dart"
+            vr = self._predict_raw(spec.valid) if dart else _G._valid_raw_incremental(self, spec.valid)
+            _G._add_metrics(entry, "validation", self._metrics_from_raw(spec, spec.valid, vr))
 
     def _contrib(self, forest, tree_w, dropped, K, bd, N):
         X = self._score_matrix(self._spec.frame)
