@@ -240,8 +240,44 @@ class DevTreeGBM:
         if mask is not None:
             m[:self.F] = np.asarray(mask, dtype=np.uint8)
         m[self.F:] = 0
-        row = torch.as_tensor(m[self.f0:self.f0 + self.Fl].copy(), device=self.dev)
+        row = self._upload([m[self.f0:self.f0 + self.Fl].copy()])[0]
         self.okm.copy_(row.view(1, -1).expand_as(self.okm))
+
+    def _upload(self, arrays):
+        """Per-tree host inputs to the device without a host/GPU sync: packed
+        into a pinned staging slot (two slots, each reused only after its
+        previous copy completed), ONE non-blocking copy into a device staging
+        buffer, returned as device views (8-byte aligned) for stream-ordered
+        device copies.  A pageable torch.as_tensor here waited for the GPU
+        every tree (1.8 ms per tree in an AutoML GBM step)."""
+        offs, n = [], 0
+        for a in arrays:
+            offs.append(n)
+            n += (a.nbytes + 7) & ~7
+        n = max(n, 8)
+        if getattr(self, "_stg", None) is None or self._stg[0].numel() < n:
+            self._stg = [torch.empty(n, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+            self._stg_ev = [None, None]
+            self._dstg = torch.empty(n, dtype=torch.uint8, device=self.dev)
+            self._stg_i = 0
+        i = self._stg_i
+        self._stg_i ^= 1
+        if self._stg_ev[i] is not None:
+            self._stg_ev[i].synchronize()
+        buf = self._stg[i].numpy()
+        for a, o in zip(arrays, offs):
+            buf[o:o + a.nbytes] = np.ascontiguousarray(a).view(np.uint8).reshape(-1)
+        # the device staging buffer is consumed by the copies below in stream
+        # order before the next upload overwrites it
+        self._dstg[:n].copy_(self._stg[i][:n], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._stg_ev[i] = ev
+        out = []
+        for a, o in zip(arrays, offs):
+            out.append(self._dstg[o:o + a.nbytes].view(torch.from_numpy(a[:0]).dtype)
+                       if a.nbytes else torch.empty(0, dtype=torch.from_numpy(a[:0]).dtype, device=self.dev))
+        return out
 
     # ---------------------------------------------------------------- sequence
     def _rec_lvl(self, d):
@@ -399,10 +435,11 @@ class DevTreeGBM:
                 seeds[d] = int(g.rng.randint(0, 2 ** 31 - 1))
         e = np.zeros(max(F, 1), dtype=np.int64)
         e[:m] = elig
-        self.cs_elig.copy_(torch.from_numpy(e))
-        self.cs_m.fill_(m)
-        self.cs_k.copy_(torch.from_numpy(ks))
-        self.cs_seed.copy_(torch.from_numpy(seeds))
+        de, dm, dk, dsd = self._upload([e, np.array([m], dtype=np.int32), ks, seeds])
+        self.cs_elig.copy_(de)
+        self.cs_m.copy_(dm)
+        self.cs_k.copy_(dk)
+        self.cs_seed.copy_(dsd)
 
     def run(self, lr, pending, w=None):
         """Grow one tree; `pending`: the previous tree's scatter (dbuf) has not

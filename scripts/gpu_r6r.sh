@@ -6,3 +6,5 @@ timeout -k 10 400 python -u -m pytest -x -q --timeout 150 --timeout-method threa
 tail -1 gpurun_out/r6r/tests.log
 H2O3_PROFILE=0 timeout -k 10 400 python -u scripts/gbm_automl_prof.py > gpurun_out/r6r/gbm_automl_prof.txt 2>&1 || { echo "prof failed"; tail -20 gpurun_out/r6r/gbm_automl_prof.txt; exit 1; }
 head -4 gpurun_out/r6r/gbm_automl_prof.txt
+H2O3_PROFILE=0 timeout -k 10 400 python -u scripts/xgb_automl_prof.py > gpurun_out/r6r/xgb_automl_prof.txt 2>&1 || { echo "xgb prof failed"; tail -20 gpurun_out/r6r/xgb_automl_prof.txt; exit 1; }
+head -4 gpurun_out/r6r/xgb_automl_prof.txt

@@ -1,5 +1,5 @@
-"""Where an AutoML GBM step's time goes at 10M x 200: GBM_1's parameters
-(depth 6, min_rows 1, sample / column rates 0.8, score_tree_interval 5,
+"""Where an AutoML XGBoost step's time goes at 10M x 200: XGBoost_1's parameters
+(depth 10, min_rows 5, sample rate 0.6, column rates 0.8, score_tree_interval 5,
 stopping_rounds 3), nfolds 3, phase timers + cProfile top entries."""
 import cProfile
 import os
@@ -14,7 +14,7 @@ os.environ.setdefault("H2O3_PROFILE", "0")
 import h2o3_amd as h2o  # noqa: E402
 from h2o3_amd.core.frame import H2OFrame  # noqa: E402
 from h2o3_amd.core.vec import T_ENUM, T_REAL, Vec  # noqa: E402
-from h2o3_amd.estimators import H2OGradientBoostingEstimator  # noqa: E402
+from h2o3_amd.estimators import H2OXGBoostEstimator  # noqa: E402
 
 N = int(os.environ.get("ROWS", 10_000_000))
 P = int(os.environ.get("COLS", 200))
@@ -27,7 +27,7 @@ y = (torch.rand(N, generator=g, device="cuda") < torch.sigmoid(logit)).to(torch.
 fr = H2OFrame.from_vecs([Vec(X[:, j].contiguous(), T_REAL) for j in range(P)] + [Vec(y, T_ENUM, ["0", "1"])],
                         [f"x{j}" for j in range(P)] + ["y"])
 del X, logit
-m = H2OGradientBoostingEstimator(ntrees=10000, score_tree_interval=5, max_depth=6, min_rows=1, sample_rate=0.8,
+m = H2OXGBoostEstimator(ntrees=10000, score_tree_interval=5, max_depth=10, min_rows=5, sample_rate=0.6,
                                  col_sample_rate=0.8, col_sample_rate_per_tree=0.8, stopping_rounds=3,
                                  stopping_tolerance=0.001, nfolds=int(os.environ.get("NFOLDS", 3)), seed=1,
                                  keep_cross_validation_predictions=True)
