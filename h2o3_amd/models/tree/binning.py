@@ -161,6 +161,12 @@ def _exact_quantile_cuts(xs, n, lo, B, seed):
             return (uu[:-1] + uu[1:]) / 2.0 if len(uu) > 1 else np.zeros(0)
     q = np.linspace(0, 1, B + 1)[1:-1]
     ks = np.round(q * (n - 1)).astype(np.int64)
+    if not cloud.is_distributed():
+        # one rank holds every value: the order statistics of one device sort
+        # (the distributed refinement below costs several passes + host loops)
+        srt = torch.sort(xs).values
+        c = np.unique(srt[torch.as_tensor(ks, device=srt.device)].cpu().numpy().astype(np.float64))
+        return c[c > lo]
     vals = kth_smallest_many(xs, ks.tolist())
     c = np.unique(np.array([vals[int(k)] for k in ks], dtype=np.float64))
     return c[c > lo]
