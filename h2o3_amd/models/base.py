@@ -612,8 +612,11 @@ class H2OEstimator:
         if spec.nclasses == 2:
             yy = y.to(torch.float64)
             ok = yy >= 0
+            # scoring rounds (scoring history / early stopping) skip the
+            # gains/lift table: only the final metrics carry it
             res = mm.binomial_metrics(yy[ok], raw[ok][:, -1], None if w is None else w[ok], spec.response_domain,
-                                      gainslift_bins=self._parms.get("gainslift_bins", -1))
+                                      gainslift_bins=self._parms.get("gainslift_bins", -1),
+                                      gainslift=not self.__dict__.get("_lite_metrics", False))
         elif spec.nclasses > 2:
             res = mm.multinomial_metrics(y, raw, w, spec.response_domain,
                                          auc_type=auc_type or self._parms.get("auc_type") or "AUTO",

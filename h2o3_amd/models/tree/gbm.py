@@ -669,6 +669,13 @@ class H2OGradientBoostingEstimator(SharedTreeEstimator):
         return m
 
     def _score_iteration(self, drv, spec):
+        self._lite_metrics = True
+        try:
+            return self._score_iteration_inner(drv, spec)
+        finally:
+            self._lite_metrics = False
+
+    def _score_iteration_inner(self, drv, spec):
         entry = {"number_of_trees": drv.iter}
         pred = drv.predictions()
         raw = pred.view(-1, 1) if pred.dim() == 1 else pred

@@ -354,6 +354,13 @@ class H2OXGBoostEstimator(SharedTreeEstimator):
         return mu.view(-1, 1)
 
     def _score_entry(self, entry, spec, f):
+        self._lite_metrics = True
+        try:
+            self._score_entry_inner(entry, spec, f)
+        finally:
+            self._lite_metrics = False
+
+    def _score_entry_inner(self, entry, spec, f):
         from .gbm import H2OGradientBoostingEstimator as _G
         _G._add_metrics(entry, "training", self._metrics_from_raw(spec, spec.frame, self._raw_from_f(f)))
         if spec.valid is not None:
