@@ -268,7 +268,9 @@ class H2OSingularValueDecompositionEstimator(H2OEstimator):
 
     def _predict_raw(self, frame):
         X, _ = self._dinfo.expand(frame)
-        return X[:, : self._dinfo.P].to(torch.float64) @ self._V.to(X.device)
+        Vp = torch.zeros((X.shape[1], self._V.shape[1]), dtype=torch.float64)
+        Vp[: self._dinfo.P] = self._V
+        return cluster_ops.xv(X, Vp).to(torch.float64)
 
     def predict(self, test_data, **kw):
         Z = self._predict_raw(test_data)
