@@ -38,6 +38,7 @@ import torch
 from ..parallel import cloud
 from ..parallel import collectives as coll
 from .vec import T_ENUM, T_INT, T_REAL, T_TIME, Vec
+from .groupsum import index_add as _ia
 
 _BINS = 1024          # histogram bins per refinement pass (Quantile.java's nbins)
 _GATHER_AT = 4096     # candidate values gathered and sorted exactly below this count
@@ -234,7 +235,7 @@ def weighted_lower(x: torch.Tensor, w: torch.Tensor, t: float) -> float:
         if a == b:
             return a
         bins = ((cand - a) * (_BINS / (b - a))).floor().clamp_(0, _BINS - 1).long()
-        ws = _ar(torch.zeros(_BINS, dtype=torch.float64, device=cand.device).index_add_(0, bins, cw))
+        ws = _ar(_ia(torch.zeros(_BINS, dtype=torch.float64, device=cand.device), bins, cw))
         cum = torch.cumsum(ws, 0) + off
         j = int(torch.searchsorted(cum, torch.tensor([t], dtype=cum.dtype, device=cum.device)).clamp(max=_BINS - 1))
         off = float(cum[j - 1]) if j > 0 else off
@@ -371,7 +372,7 @@ def _key_counts(keys):
     if _dist():
         u, c = _gather(u), _gather(c)
         u, inv = torch.unique(u, dim=0, return_inverse=True)
-        c = torch.zeros(u.shape[0], dtype=torch.int64, device=u.device).index_add_(0, inv, c)
+        c = _ia(torch.zeros(u.shape[0], dtype=torch.int64, device=u.device), inv, c)
     return u, c
 
 
@@ -652,9 +653,8 @@ def pivot(fr, index, column, value):
     first = torch.full((R * C,), big, dtype=torch.int64, device=_dev()).scatter_reduce(0, cell, gidx, "amin")
     first = _ar(first, "min")
     win = gidx == first[cell]
-    val = torch.zeros(R * C, dtype=torch.float64, device=_dev()).index_add_(0, cell[win], x[ok][win])
-    has = torch.zeros(R * C, dtype=torch.float64, device=_dev()).index_add_(
-        0, cell[win], torch.ones_like(x[ok][win]))
+    val = _ia(torch.zeros(R * C, dtype=torch.float64, device=_dev()), cell[win], x[ok][win])
+    has = _ia(torch.zeros(R * C, dtype=torch.float64, device=_dev()), cell[win], torch.ones_like(x[ok][win]))
     red = _ar(torch.stack([val, has]))
     M = torch.where(red[1] > 0, red[0], torch.full_like(red[0], math.nan)).view(R, C)
     out = [_key_vec(rows, iv)] + [Vec(M[:, j].contiguous(), T_REAL) for j in range(C)]
@@ -769,7 +769,7 @@ def _interact(a_codes, a_dom, b_codes, b_dom, same, max_factors, min_occurrence)
     if _dist():
         u, c = _gather(u), _gather(c)
         u, inv = torch.unique(u, return_inverse=True)
-        c = torch.zeros(u.numel(), dtype=torch.int64, device=dev).index_add_(0, inv, c)
+        c = _ia(torch.zeros(u.numel(), dtype=torch.int64, device=dev), inv, c)
     # descending count, ties by key (the reference's hash order is unspecified)
     o = lexsort([-c.to(torch.float64), u.to(torch.float64)])
     u, c = u[o], c[o]

@@ -33,6 +33,7 @@ _TYPE_ALIASES = {"numeric": T_REAL, "real": T_REAL, "float": T_REAL, "double": T
 
 def _dev():
     return cloud.device()
+from .groupsum import index_add as _ia
 
 
 def _local_slice(n_global: int):
@@ -1081,7 +1082,7 @@ class H2OFrame:
             ok = v.data >= 0
             ww = torch.ones_like(v.data, dtype=torch.float64) if w is None else torch.nan_to_num(w)
             lw = torch.zeros(k, dtype=torch.float64, device=v.data.device)
-            lw.index_add_(0, v.data[ok].long(), ww[ok])
+            _ia(lw, v.data[ok].long(), ww[ok])
             lw = coll.allreduce_(lw).cpu().numpy()
             order = list(np.argsort(lw, kind="stable"))
             if top_n != -1 and top_n < k - 1:

@@ -7,6 +7,10 @@ addresses: measured on MI355X, one f64 index_add_ of 2M rows into 2 bins took
 the sums are a one-hot GEMM on the matrix cores instead (f64 in, f64
 accumulate; rows processed in chunks so the one-hot block stays ~256 MB);
 large bin counts keep index_add_ (the atomics spread over many addresses).
+On a GPU with the native library, f64 sums go to ops/csrc/metrics.hip's
+group_sum kernel instead (wave-merged atomics, LDS-privatised for small
+nbins * C): one pass for any bin count.  Rows whose idx is outside
+[0, nbins) are skipped there; callers pass in-range indices.
 """
 from __future__ import annotations
 
@@ -23,6 +27,11 @@ def group_sum(idx: torch.Tensor, vals: torch.Tensor, nbins: int, dtype=torch.flo
     v = (vals.view(-1, 1) if one_d else vals).to(dtype)
     idx = idx.reshape(-1).to(torch.int64)
     C = v.shape[1]
+    if idx.device.type == "cuda" and dtype == torch.float64 and nbins * C < (1 << 31):
+        from ..ops import metrics_ops
+        if metrics_ops.available(idx):
+            out = metrics_ops.group_sum(idx, v, nbins)
+            return out[:, 0] if one_d else out
     if idx.device.type != "cuda" or nbins > _ONEHOT_MAX_BINS or idx.numel() == 0:
         out = torch.zeros((nbins, C), dtype=dtype, device=v.device).index_add_(0, idx, v)
         return out[:, 0] if one_d else out
@@ -33,3 +42,19 @@ def group_sum(idx: torch.Tensor, vals: torch.Tensor, nbins: int, dtype=torch.flo
         oh = (idx[a:a + chunk].view(-1, 1) == ar).to(dtype)      # [c, nbins]
         out.addmm_(oh.T, v[a:a + chunk])
     return out[:, 0] if one_d else out
+
+
+def index_add(out: torch.Tensor, idx: torch.Tensor, vals: torch.Tensor) -> torch.Tensor:
+    """`out.index_add_(0, idx, vals)` that stays fast when millions of rows
+    share a few indices: f64 GPU tensors go through the wave-merged
+    group_sum kernel (torch's f64 index_add_ on this stack retries a
+    compare-and-swap per row and serialises on a hot address: 56 s for 670k
+    rows into one bin, measured); everything else is index_add_ itself."""
+    if out.is_cuda and out.dtype == torch.float64 and out.is_contiguous() and out.shape[0] > 0:
+        from ..ops import metrics_ops
+        if metrics_ops.available(out):
+            n = idx.numel()
+            C = out[0].numel()
+            out.view(out.shape[0], C).add_(metrics_ops.group_sum(idx, vals.reshape(n, C), out.shape[0]))
+            return out
+    return out.index_add_(0, idx, vals)

@@ -24,6 +24,7 @@ from ..parallel import cloud
 from ..parallel import collectives as coll
 from .frame import H2OFrame, _fmt_level, _local_slice, _reshard, _take, _to_enum, _vec_from_array
 from .vec import NUMERIC_TYPES, T_ENUM, T_INT, T_REAL, T_STR, T_TIME, Vec, make_enum, make_numeric, make_string
+from .groupsum import index_add as _ia
 
 
 def _dev():
@@ -342,8 +343,8 @@ class GroupBy:
                 ok = (~nan).to(torch.float64)
             else:
                 xz, ok = x, torch.ones_like(x)
-            s = torch.zeros(G, dtype=torch.float64, device=x.device).index_add_(0, inv, xz)
-            n = torch.zeros(G, dtype=torch.float64, device=x.device).index_add_(0, inv, ok)
+            s = _ia(torch.zeros(G, dtype=torch.float64, device=x.device), inv, xz)
+            n = _ia(torch.zeros(G, dtype=torch.float64, device=x.device), inv, ok)
             if op == "sum":
                 r = s
             elif op == "mean":
@@ -355,7 +356,7 @@ class GroupBy:
             elif op in ("sd", "var", "ss"):
                 mean = s / n
                 d = xz - mean[inv]
-                ss = torch.zeros(G, dtype=torch.float64, device=x.device).index_add_(0, inv, torch.where(ok > 0, d * d, torch.zeros_like(d)))
+                ss = _ia(torch.zeros(G, dtype=torch.float64, device=x.device), inv, torch.where(ok > 0, d * d, torch.zeros_like(d)))
                 r = ss if op == "ss" else (ss / (n - 1) if op == "var" else torch.sqrt(ss / (n - 1)))
             elif op in ("median", "mode"):
                 from .dist_ops import segment_median_mode
@@ -666,8 +667,8 @@ def _impute_by_group(fr, j, method, combine_method, by):
     else:
         ok = ~torch.isnan(x)
         S = torch.zeros((2, G), dtype=torch.float64, device=x.device)
-        S[0].index_add_(0, gid[ok], x[ok])
-        S[1].index_add_(0, gid[ok], torch.ones_like(x[ok]))
+        _ia(S[0], gid[ok], x[ok])
+        _ia(S[1], gid[ok], torch.ones_like(x[ok]))
         if dist:
             coll.allreduce_(S)
         fill = torch.where(S[1] > 0, S[0] / S[1].clamp(min=1), torch.full_like(S[0], math.nan))

@@ -21,6 +21,7 @@ from ..core.frame import H2OFrame, _take
 from ..core.vec import T_ENUM
 from ..parallel import cloud
 from ..parallel import collectives as coll
+from ..core.groupsum import index_add as _ia
 
 
 def class_counts(frame, y, w=None):
@@ -31,7 +32,7 @@ def class_counts(frame, y, w=None):
     wt = torch.ones_like(codes, dtype=torch.float64) if w is None else \
         torch.nan_to_num(frame.vec(w).as_float(torch.float64))
     c = torch.zeros(K, dtype=torch.float64, device=codes.device)
-    c.index_add_(0, codes[ok], wt[ok])
+    _ia(c, codes[ok], wt[ok])
     coll.allreduce_(c)
     return c.cpu().numpy()
 

@@ -611,10 +611,13 @@ class H2OEstimator:
         dist = getattr(self, "_dist", None)
         if spec.nclasses == 2:
             yy = y.to(torch.float64)
-            ok = yy >= 0
+            # NA responses (code -1) become NaN: binomial_metrics drops rows
+            # with a NaN response or score itself (no boolean-mask compaction
+            # and host sync per call)
+            yy = torch.where(yy >= 0, yy, torch.full_like(yy, float("nan")))
             # scoring rounds (scoring history / early stopping) skip the
             # gains/lift table: only the final metrics carry it
-            res = mm.binomial_metrics(yy[ok], raw[ok][:, -1], None if w is None else w[ok], spec.response_domain,
+            res = mm.binomial_metrics(yy, raw[:, -1], w, spec.response_domain,
                                       gainslift_bins=self._parms.get("gainslift_bins", -1),
                                       gainslift=not self.__dict__.get("_lite_metrics", False))
         elif spec.nclasses > 2:

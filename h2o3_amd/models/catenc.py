@@ -42,6 +42,7 @@ import torch
 
 from ..core.vec import T_ENUM, T_REAL, Vec
 from ..parallel import collectives as coll
+from ..core.groupsum import index_add as _ia
 
 _CANON = {"auto": "AUTO", "enum": "Enum", "onehotinternal": "OneHotInternal", "onehotexplicit": "OneHotExplicit",
           "binary": "Binary", "eigen": "Eigen", "labelencoder": "LabelEncoder", "sortbyresponse": "SortByResponse",
@@ -91,7 +92,7 @@ class CategoricalEncoder:
             if self.scheme in ("EnumLimited", "Eigen", "SortByResponse"):
                 wt = None if w is None else frame.vec(w).as_float(torch.float64)
                 cnt = torch.zeros(L + 1, dtype=torch.float64, device=codes.device)
-                cnt.index_add_(0, torch.where(codes < 0, torch.full_like(codes, L), codes),
+                _ia(cnt, torch.where(codes < 0, torch.full_like(codes, L), codes),
                                torch.ones_like(codes, dtype=torch.float64) if wt is None else torch.nan_to_num(wt))
                 coll.allreduce_(cnt)
                 counts = cnt.cpu().numpy()
@@ -160,8 +161,8 @@ class CategoricalEncoder:
             yy = torch.where(yv.data < 0, torch.full_like(yy, float("nan")), yy)
         ok = (codes >= 0) & ~torch.isnan(yy)
         s = torch.zeros(2 * L, dtype=torch.float64, device=codes.device)
-        s[:L].index_add_(0, codes[ok], yy[ok])
-        s[L:].index_add_(0, codes[ok], torch.ones_like(yy[ok]))
+        _ia(s[:L], codes[ok], yy[ok])
+        _ia(s[L:], codes[ok], torch.ones_like(yy[ok]))
         coll.allreduce_(s)
         sh = s.cpu().numpy()
         mean = np.where(sh[L:] > 0, sh[:L] / np.maximum(sh[L:], 1), np.inf)

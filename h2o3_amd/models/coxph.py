@@ -29,6 +29,7 @@ from ..parallel import cloud
 from ..parallel import collectives as coll
 from .base import H2OEstimator
 from .datainfo import DataInfo
+from ..core.groupsum import index_add as _ia
 
 COX_DEFAULTS = dict(start_column=None, stop_column=None, stratify_by=None, ties="efron", init=0.0, lre_min=9.0,
                     max_iterations=20, use_all_factor_levels=False, interactions=None, interactions_only=None,
@@ -290,12 +291,12 @@ class H2OCoxProportionalHazardsEstimator(H2OEstimator):
         flat = sidx * T + tix
         def seg(v):
             out = torch.zeros(S * T, dtype=torch.float64, device=X.device)
-            out.index_add_(0, flat, v)
+            _ia(out, flat, v)
             return out.view(S, T)
         size_ev = seg(w * ev)
         risk_all = seg(risk)
         total = torch.zeros(S, dtype=torch.float64, device=X.device)
-        total.index_add_(0, sidx, risk)
+        _ia(total, sidx, risk)
         # risk still at stake before time t: total minus the rows that left earlier
         at_risk = total.view(-1, 1) - (torch.cumsum(risk_all, 1) - risk_all)
         haz = torch.where(size_ev > 0, size_ev / at_risk.clamp_min(1e-300), torch.zeros_like(size_ev))
@@ -320,12 +321,12 @@ class H2OCoxProportionalHazardsEstimator(H2OEstimator):
         rs_all = risk_all.sum(0)
         rcum = torch.flip(torch.cumsum(torch.flip(rs_all, [0]), 0), [0])      # risk of stop >= t
         xr = torch.zeros((T, X.shape[1]), dtype=torch.float64, device=X.device)
-        xr.index_add_(0, tix, xc * risk.view(-1, 1))
+        _ia(xr, tix, xc * risk.view(-1, 1))
         rcum_x = torch.flip(torch.cumsum(torch.flip(xr, [0]), 0), [0])
         rev = torch.zeros(T, dtype=torch.float64, device=X.device)
-        rev.index_add_(0, tix, risk * ev)
+        _ia(rev, tix, risk * ev)
         xrev = torch.zeros_like(xr)
-        xrev.index_add_(0, tix, xc * (risk * ev).view(-1, 1))
+        _ia(xrev, tix, xc * (risk * ev).view(-1, 1))
         present = torch.zeros(T, dtype=torch.bool, device=X.device)
         present[tix] = True
         ch = torch.zeros(T, dtype=torch.float64, device=X.device)

@@ -27,6 +27,7 @@ import torch
 
 from ...parallel import collectives as coll
 from ..datainfo import DataInfo
+from ...core.groupsum import index_add as _ia
 
 
 def fit_hglm(est, spec):
@@ -78,15 +79,15 @@ def fit_hglm(est, spec):
         cc = codes.clamp(min=0)
         o = q_off[bi]
         wz = torch.where(okc, w, torch.zeros_like(w))
-        XtZ[:, o:o + L] = torch.zeros((L, P), dtype=torch.float64, device=X.device).index_add_(
-            0, cc, X1 * wz.view(-1, 1)).T
-        Zty[o:o + L] = torch.zeros(L, dtype=torch.float64, device=X.device).index_add_(0, cc, wz * y)
+        XtZ[:, o:o + L] = _ia(torch.zeros((L, P), dtype=torch.float64, device=X.device),
+                              cc, X1 * wz.view(-1, 1)).T
+        Zty[o:o + L] = _ia(torch.zeros(L, dtype=torch.float64, device=X.device), cc, wz * y)
         for bj, (codes2, L2) in enumerate(blocks):
             o2 = q_off[bj]
             ok2 = okc & (codes2 >= 0)
             key = cc * L2 + codes2.clamp(min=0)
-            cnt = torch.zeros(L * L2, dtype=torch.float64, device=X.device).index_add_(
-                0, key, torch.where(ok2, w, torch.zeros_like(w)))
+            cnt = _ia(torch.zeros(L * L2, dtype=torch.float64, device=X.device),
+                      key, torch.where(ok2, w, torch.zeros_like(w)))
             ZtZ[o:o + L, o2:o2 + L2] = cnt.view(L, L2)
     yty = (w * y * y).sum().view(1)
     stats = torch.cat([XtX.reshape(-1), Xty, XtZ.reshape(-1), ZtZ.reshape(-1), Zty, yty, w.sum().view(1)])

@@ -16,6 +16,7 @@ import torch
 
 from ..parallel import collectives as coll
 from .base import H2OEstimator
+from ..core.groupsum import index_add as _ia
 
 ISO_DEFAULTS = dict(out_of_bounds="NA", custom_metric_func=None)
 
@@ -52,8 +53,8 @@ class H2OIsotonicRegressionEstimator(H2OEstimator):
         o = torch.argsort(x)
         x, y, w = x[o], y[o], w[o]
         ux, inv = torch.unique_consecutive(x, return_inverse=True)
-        sw = torch.zeros(ux.numel(), dtype=torch.float64, device=x.device).index_add_(0, inv, w)
-        swy = torch.zeros(ux.numel(), dtype=torch.float64, device=x.device).index_add_(0, inv, w * y)
+        sw = _ia(torch.zeros(ux.numel(), dtype=torch.float64, device=x.device), inv, w)
+        swy = _ia(torch.zeros(ux.numel(), dtype=torch.float64, device=x.device), inv, w * y)
         uxh, yh, wh = ux.cpu().numpy(), (swy / sw).cpu().numpy(), sw.cpu().numpy()
         starts, by, _ = pava(yh, wh)
         ends = np.concatenate([starts[1:], [len(uxh)]]) - 1

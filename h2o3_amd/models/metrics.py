@@ -18,6 +18,7 @@ import torch
 
 from ..parallel import cloud
 from ..parallel import collectives as coll
+from ..core.groupsum import index_add as _ia
 
 _MAX_THRESHOLDS = 400
 
@@ -459,29 +460,47 @@ def binomial_metrics(y, p1, w=None, domain=None, threshold=None, auc_type="AUTO"
     """y in {0,1} (float), p1 = P(class 1).  AUC / PR-AUC / thresholds /
     gains-lift from the merged logit-histogram sketch (no gather of rows; a
     2^18-bin logit grid keeps the AUC within ~1e-5 of the exact sort)."""
-    ok = ~torch.isnan(y) & ~torch.isnan(p1)
-    y, p1 = y[ok].to(torch.float64), p1[ok].to(torch.float64)
-    w = torch.ones_like(y) if w is None else w[ok].to(torch.float64)
-    pc = torch.clamp(p1, 1e-15, 1 - 1e-15)
-    sums = torch.stack([w.sum(), -(w * (y * torch.log(pc) + (1 - y) * torch.log(1 - pc))).sum(),
-                        (w * (y - p1) ** 2).sum(), (w * y).sum(),
-                        torch.tensor(float(y.numel()), dtype=torch.float64, device=y.device)])
-    coll.allreduce_(sums)
-    sw, ll_s, se_s, wy_s, nobs = (float(v) for v in sums.cpu().tolist())
+    import os
+    exact = os.environ.get("H2O3_EXACT_AUC") == "1" and not cloud.is_distributed()
+    from ..ops import metrics_ops
+    if not exact and metrics_ops.available(p1):
+        # one HIP pass: NaN filter, logit sketch and the loss sums, one
+        # all-reduce and one host read (ops/csrc/metrics.hip)
+        buf = metrics_ops.logit_hist(y, p1, w, _NB_BIN)
+        coll.allreduce_(buf)
+        pos, neg = buf[:_NB_BIN], buf[_NB_BIN:2 * _NB_BIN]
+        sw, ll_s, se_s, wy_s, nobs = (float(v) for v in buf[2 * _NB_BIN:].cpu().tolist())
+    else:
+        ok = ~torch.isnan(y) & ~torch.isnan(p1)
+        y, p1 = y[ok].to(torch.float64), p1[ok].to(torch.float64)
+        w = torch.ones_like(y) if w is None else w[ok].to(torch.float64)
+        pc = torch.clamp(p1, 1e-15, 1 - 1e-15)
+        sums = torch.stack([w.sum(), -(w * (y * torch.log(pc) + (1 - y) * torch.log(1 - pc))).sum(),
+                            (w * (y - p1) ** 2).sum(), (w * y).sum(),
+                            torch.tensor(float(y.numel()), dtype=torch.float64, device=y.device)])
+        coll.allreduce_(sums)
+        sw, ll_s, se_s, wy_s, nobs = (float(v) for v in sums.cpu().tolist())
+        pos = neg = None
     logloss = ll_s / sw if sw > 0 else float("nan")
     mse = se_s / sw if sw > 0 else float("nan")
     groups = 16 if gainslift_bins is None or int(gainslift_bins) < 0 else int(gainslift_bins)
     # the same merged sketch at every cloud size: metrics do not depend on
     # how many GPUs hold the rows (exact sort: H2O3_EXACT_AUC=1, one rank)
-    import os
-    if os.environ.get("H2O3_EXACT_AUC") == "1" and not cloud.is_distributed():
+    if exact:
         auc, prauc = _auc_exact(p1, y, w)
         tab = _threshold_table(p1, y, w)
         gl = (lambda: _gains_lift(p1, y, w, groups)) if groups > 0 else None
     else:
-        pos, neg = _binomial_sketch(y, p1, w)
-        auc, prauc = _hist_auc(pos, neg)
+        if pos is None:
+            pos, neg = _binomial_sketch(y, p1, w)
         lower = _bin_lower_prob(_NB_BIN, pos.device)
+        # only the occupied bins matter (cumulative sums, thresholds and
+        # gains/lift groups are unchanged by empty bins): ONE device->host
+        # copy of those, then the tables are built on the host
+        nz = torch.nonzero((pos + neg) > 0).flatten()
+        c = torch.stack([pos[nz], neg[nz], lower[nz]]).cpu()
+        pos, neg, lower = c[0], c[1], c[2]
+        auc, prauc = _hist_auc(pos, neg)
         tab = _threshold_table_hist(pos, neg, lower)
         gl = (lambda: _gains_lift_hist(pos, neg, lower, groups)) if groups > 0 else None
     i = int(np.argmax(tab["f1"])) if len(tab["f1"]) else 0
@@ -537,7 +556,7 @@ def multinomial_auc(y, P, w, domain, auc_type):
     s_idx = torch.arange(K, device=P.device).view(1, K)
     idx = (s_idx * K + y.view(-1, 1)) * B + b
     H = torch.zeros(K * K * B, dtype=torch.float64, device=P.device)
-    H.index_add_(0, idx.reshape(-1), w.view(-1, 1).expand(-1, K).reshape(-1))
+    _ia(H, idx.reshape(-1), w.view(-1, 1).expand(-1, K).reshape(-1))
     coll.allreduce_(H)
     H = H.view(K, K, B)                                       # [score class, true class, bin]
     cls_w = H[0].sum(1).cpu().numpy()                         # weight of each true class
@@ -600,7 +619,7 @@ def multinomial_metrics(y_codes, probs, w=None, domain=None, hit_k=10, auc_type=
     onehot = torch.nn.functional.one_hot(y, K).to(torch.float64)
     pred = torch.argmax(P, 1)
     cmat = torch.zeros((K, K), dtype=torch.float64, device=y.device)
-    cmat.index_put_((y, pred), w, accumulate=True)
+    _ia(cmat.view(-1), y * K + pred, w)
     kk = min(hit_k, K)
     topk = torch.topk(P, kk, dim=1).indices
     hits = (topk == y.view(-1, 1)).to(torch.float64)

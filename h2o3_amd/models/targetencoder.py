@@ -26,6 +26,7 @@ from ..core.vec import T_ENUM, T_REAL, Vec
 from ..parallel import cloud
 from ..parallel import collectives as coll
 from .base import H2OEstimator
+from ..core.groupsum import index_add as _ia
 
 TE_DEFAULTS = dict(columns_to_encode=None, keep_original_categorical_columns=True, blending=False,
                    inflection_point=10.0, smoothing=20.0, data_leakage_handling="None", noise=0.01, seed=-1,
@@ -90,9 +91,9 @@ class H2OTargetEncoderEstimator(H2OEstimator):
             codes = torch.where(v.data >= 0, v.data.long(), torch.full_like(v.data.long(), L - 1))
             per = []
             for t in chans:
-                num = torch.zeros(L, dtype=torch.float64, device=t.device).index_add_(0, codes[ok], t[ok])
-                den = torch.zeros(L, dtype=torch.float64, device=t.device).index_add_(
-                    0, codes[ok], torch.ones_like(t[ok]))
+                num = _ia(torch.zeros(L, dtype=torch.float64, device=t.device), codes[ok], t[ok])
+                den = _ia(torch.zeros(L, dtype=torch.float64, device=t.device),
+                          codes[ok], torch.ones_like(t[ok]))
                 st = torch.stack([num, den])
                 coll.allreduce_(st)
                 per.append(st)
@@ -101,9 +102,9 @@ class H2OTargetEncoderEstimator(H2OEstimator):
                 fper = []
                 for t in chans:
                     key = folds[ok] * L + codes[ok]
-                    num = torch.zeros(nf * L, dtype=torch.float64, device=t.device).index_add_(0, key, t[ok])
-                    den = torch.zeros(nf * L, dtype=torch.float64, device=t.device).index_add_(
-                        0, key, torch.ones_like(t[ok]))
+                    num = _ia(torch.zeros(nf * L, dtype=torch.float64, device=t.device), key, t[ok])
+                    den = _ia(torch.zeros(nf * L, dtype=torch.float64, device=t.device),
+                              key, torch.ones_like(t[ok]))
                     st = torch.stack([num.view(nf, L), den.view(nf, L)])
                     coll.allreduce_(st)
                     fper.append(st)

@@ -31,6 +31,7 @@ from .engine import GrowParams, TreeGrower
 from ...ops import tree_ops
 from ...utils.timer import phase
 from .shared import Forest, SharedTreeEstimator
+from ...core.groupsum import index_add as _ia
 
 GBM_DEFAULTS = dict(ntrees=50, max_depth=5, min_rows=10.0, nbins=20, nbins_top_level=1024, nbins_cats=1024,
                     r2_stopping=1.79e308, stopping_rounds=0, stopping_metric="auto", stopping_tolerance=0.001,
@@ -530,8 +531,8 @@ class GBMDriver:
             d = res - mt[idx]
             delta = self.dist.huber_delta
             corr = torch.sign(d) * torch.minimum(d.abs(), torch.full_like(d, delta))
-            num = torch.zeros(L, dtype=torch.float64, device=self.dev).index_add_(0, idx, w.to(torch.float64) * corr)
-            den = torch.zeros(L, dtype=torch.float64, device=self.dev).index_add_(0, idx, w.to(torch.float64))
+            num = _ia(torch.zeros(L, dtype=torch.float64, device=self.dev), idx, w.to(torch.float64) * corr)
+            den = _ia(torch.zeros(L, dtype=torch.float64, device=self.dev), idx, w.to(torch.float64))
             s = torch.cat([num, den])
             coll.allreduce_(s)
             num, den = s[:L], s[L:]

@@ -25,6 +25,7 @@ from __future__ import annotations
 import numpy as np
 import pandas as pd
 import torch
+from ...core.groupsum import index_add as _ia
 
 
 class _FI:
@@ -192,7 +193,7 @@ def update_tree_weights(forest, leaf_ids: torch.Tensor, w: torch.Tensor):
     """Node covers = sum of the row weights reaching each node."""
     for t, tree in enumerate(forest.trees):
         leaf_w = torch.zeros(tree.n_nodes, dtype=torch.float64, device=leaf_ids.device)
-        leaf_w.index_add_(0, leaf_ids[:, t].long(), w.to(torch.float64))
+        _ia(leaf_w, leaf_ids[:, t].long(), w.to(torch.float64))
         from ...parallel import collectives as coll
         coll.allreduce_(leaf_w)
         wt = leaf_w.cpu().numpy()

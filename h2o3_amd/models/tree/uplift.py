@@ -30,6 +30,7 @@ from ...parallel import collectives as coll
 from .. import metrics as mm
 from .engine import GrowParams, TreeGrower
 from .shared import Forest, SharedTreeEstimator
+from ...core.groupsum import index_add as _ia
 
 UPLIFT_DEFAULTS = dict(ntrees=50, max_depth=20, min_rows=1.0, nbins=20, nbins_top_level=1024, nbins_cats=1024,
                        seed=-1, mtries=-2, sample_rate=0.632, col_sample_rate_per_tree=1.0,
@@ -52,7 +53,7 @@ def auuc_metrics(uplift: torch.Tensor, y: torch.Tensor, treat: torch.Tensor, nbi
     # bin = first (largest) threshold <= prediction
     idx = torch.searchsorted(-ths, -u, right=False).clamp(max=nb - 1)
     def cnt(v):
-        return torch.zeros(nb, dtype=torch.float64, device=u.device).index_add_(0, idx, v)
+        return _ia(torch.zeros(nb, dtype=torch.float64, device=u.device), idx, v)
     T = torch.cumsum(cnt(tt), 0)
     C = torch.cumsum(cnt(1 - tt), 0)
     YT = torch.cumsum(cnt(tt * yy), 0)
