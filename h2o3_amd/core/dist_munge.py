@@ -30,6 +30,8 @@ import torch
 from ..parallel import cloud
 from ..parallel import collectives as coll
 from .vec import T_ENUM, T_INT, T_REAL, Vec
+from .groupsum import group_extreme
+from .groupsum import index_add as _ia
 
 
 def eligible(*frames):
@@ -219,15 +221,14 @@ def group_by(fr, by, aggs):
         rm = na in ("rm", "ignore")
         xz = torch.where(nan, torch.zeros_like(x), x) if rm else x
         ok = (~nan).to(torch.float64) if rm else torch.ones_like(x)
-        s = torch.zeros(G, dtype=torch.float64, device=dev).index_add_(0, gid, xz)
-        nn = torch.zeros(G, dtype=torch.float64, device=dev).index_add_(0, gid, ok)
+        s = _ia(torch.zeros(G, dtype=torch.float64, device=dev), gid, xz)
+        nn = _ia(torch.zeros(G, dtype=torch.float64, device=dev), gid, ok)
         sums += [s, nn]
         mi = ma = None
         if op in ("min", "max"):
             fill = math.inf if op == "min" else -math.inf
             # NAs never win an extremum (the one-rank GroupBy semantics)
-            t = torch.full((G,), fill, dtype=torch.float64, device=dev).scatter_reduce(
-                0, gid, torch.where(nan, torch.full_like(x, fill), x), reduce="amin" if op == "min" else "amax")
+            t = group_extreme(gid, torch.where(nan, torch.full_like(x, fill), x).to(torch.float64), G, op)
             (mins if op == "min" else maxs).append(t)
             mi = len(mins) - 1 if op == "min" else None
             ma = len(maxs) - 1 if op == "max" else None
@@ -252,8 +253,7 @@ def group_by(fr, by, aggs):
             d = xz - mean[gid]
             okm = (~nan) if rm else torch.ones_like(nan)
             sq_idx[(op, c, na)] = len(sq)
-            sq.append(torch.zeros(G, dtype=torch.float64, device=dev).index_add_(
-                0, gid, torch.where(okm, d * d, torch.zeros_like(d))))
+            sq.append(_ia(torch.zeros(G, dtype=torch.float64, device=dev), gid, torch.where(okm, d * d, torch.zeros_like(d))))
     if sq:
         SQ = torch.stack(sq)
         coll.allreduce_(SQ)

@@ -58,3 +58,23 @@ def index_add(out: torch.Tensor, idx: torch.Tensor, vals: torch.Tensor) -> torch
             out.view(out.shape[0], C).add_(metrics_ops.group_sum(idx, vals.reshape(n, C), out.shape[0]))
             return out
     return out.index_add_(0, idx, vals)
+
+
+def group_extreme(idx: torch.Tensor, vals: torch.Tensor, nbins: int, op: str) -> torch.Tensor:
+    """Per-group minimum (op "min") or maximum ("max") of vals ([N] or [N, C])
+    by idx in [0, nbins), f64, +inf / -inf for empty groups.  f64 GPU input
+    goes to the wave-merged HIP kernel (torch's float scatter_reduce amin /
+    amax retries a compare-and-swap per row on a hot address)."""
+    one_d = vals.dim() == 1
+    v = vals.view(-1, 1) if one_d else vals
+    idx = idx.reshape(-1).to(torch.int64)
+    if v.is_cuda:
+        from ..ops import metrics_ops
+        if metrics_ops.available(v):
+            out = metrics_ops.group_reduce(idx, v, nbins, op)
+            return out[:, 0] if one_d else out
+    fill = float("inf") if op == "min" else float("-inf")
+    out = torch.full((nbins, v.shape[1]), fill, dtype=torch.float64, device=v.device)
+    out.scatter_reduce_(0, idx.view(-1, 1).expand(-1, v.shape[1]), v.to(torch.float64),
+                        reduce="amin" if op == "min" else "amax")
+    return out[:, 0] if one_d else out

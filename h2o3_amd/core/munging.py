@@ -24,7 +24,7 @@ from ..parallel import cloud
 from ..parallel import collectives as coll
 from .frame import H2OFrame, _fmt_level, _local_slice, _reshard, _take, _to_enum, _vec_from_array
 from .vec import NUMERIC_TYPES, T_ENUM, T_INT, T_REAL, T_STR, T_TIME, Vec, make_enum, make_numeric, make_string
-from .groupsum import index_add as _ia
+from .groupsum import group_extreme, index_add as _ia
 
 
 def _dev():
@@ -351,8 +351,7 @@ class GroupBy:
                 r = s / n
             elif op in ("min", "max"):
                 fill = math.inf if op == "min" else -math.inf
-                r = torch.full((G,), fill, dtype=torch.float64, device=x.device)
-                r = r.scatter_reduce(0, inv, torch.where(nan, torch.full_like(x, fill), x), reduce="amin" if op == "min" else "amax")
+                r = group_extreme(inv, torch.where(nan, torch.full_like(x, fill), x).to(torch.float64), G, op)
             elif op in ("sd", "var", "ss"):
                 mean = s / n
                 d = xz - mean[inv]

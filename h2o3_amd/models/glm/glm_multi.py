@@ -18,6 +18,7 @@ import torch
 
 from ...parallel import collectives as coll
 from ..datainfo import DataInfo
+from ...core.groupsum import group_sum
 
 
 def _loss_grad_multinomial(X, Y, w, B, b0, wsum):
@@ -207,7 +208,7 @@ def fit_multinomial(est, spec, fam):
             if _path_should_stop(est, path, null_dev, valid, dev_of, lmax):
                 break
     else:  # ordinal
-        cnt = torch.bincount(y.clamp(min=0), weights=w, minlength=K).to(torch.float64)
+        cnt = group_sum(y.clamp(min=0), torch.ones_like(y, dtype=torch.float64) if w is None else w, K)
         coll.allreduce_(cnt)
         sqerr = solver == "GRADIENT_DESCENT_SQERR"
         null_beta = torch.zeros(Pp, dtype=torch.float64, device=dev)

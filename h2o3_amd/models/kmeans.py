@@ -41,6 +41,7 @@ from ..parallel import collectives as coll
 from . import metrics as mm
 from .base import H2OEstimator
 from .datainfo import DataInfo
+from ..core.groupsum import group_extreme
 
 KMEANS_DEFAULTS = dict(k=1, estimate_k=False, user_points=None, max_iterations=10, standardize=True, seed=-1,
                        init="Furthest", categorical_encoding="auto", max_runtime_secs=0.0,
@@ -229,9 +230,9 @@ class H2OKMeansEstimator(H2OEstimator):
         hi = torch.full((k, P), float("-inf"), dtype=torch.float64, device=X.device)
         for a in range(0, X.shape[0], chunk):
             xc = X[a:a + chunk].to(torch.float64)
-            idx = assign[a:a + chunk].long().view(-1, 1).expand(-1, P)
-            lo.scatter_reduce_(0, idx, xc, reduce="amin")
-            hi.scatter_reduce_(0, idx, xc, reduce="amax")
+            ac = assign[a:a + chunk]
+            lo = torch.minimum(lo, group_extreme(ac, xc, k, "min"))
+            hi = torch.maximum(hi, group_extreme(ac, xc, k, "max"))
         coll.allreduce_(lo, "min")
         coll.allreduce_(hi, "max")
         return lo, hi

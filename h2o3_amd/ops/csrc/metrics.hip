@@ -91,27 +91,54 @@ __global__ __launch_bounds__(256) void logit_hist_kernel(const double* __restric
   }
 }
 
-// Grouped sums out[g, c] += v[i, c] over rows i with idx[i] == g (rows with
-// idx outside [0, nbins) are skipped): the group-by / class-count / leaf-sum
+// Grouped sums / minima / maxima out[g, c] (+)= v[i, c] over rows i with
+// idx[i] == g (rows with idx outside [0, nbins) are skipped): the group-by / class-count / leaf-sum
 // primitive (water/rapids/ast/prims/mungers/AstGroup.java's per-group
 // accumulators, hex/ModelMetrics* class tallies).  The same contention
 // problem as the sketch above: few groups, millions of rows.  Each wave
 // first merges lanes that share a group (up to PEEL rounds, which covers the
 // few-group case completely), then lanes still pending add directly.  With
 // nbins * C <= LDS_MAX the block accumulates in LDS (ds_add_f64) and flushes
-// once; otherwise the adds go to global memory (global_atomic_add_f64).
+// once; otherwise the atomics go to global memory (global_atomic_add_f64,
+// global_atomic_min_f64 / max_f64).
 #define GS_LDS_MAX 8192
 #define GS_PEEL 8
 
-template <bool LDS>
-__global__ __launch_bounds__(256) void group_sum_kernel(const long long* __restrict__ idx,
-                                                        const double* __restrict__ v, long long n, int C, int nbins,
-                                                        double* __restrict__ out) {
+// OP 0: sum, 1: min, 2: max (the caller fills out with 0 / +inf / -inf).
+template <int OP>
+__device__ __forceinline__ double gs_ident() {
+  return OP == 0 ? 0.0 : (OP == 1 ? __builtin_inf() : -__builtin_inf());
+}
+template <int OP>
+__device__ __forceinline__ double gs_comb(double a, double b) {
+  return OP == 0 ? a + b : (OP == 1 ? fmin(a, b) : fmax(a, b));
+}
+template <int OP>
+__device__ __forceinline__ double gs_wave(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = gs_comb<OP>(v, __shfl_xor(v, o, H2O_WAVE));
+  return v;
+}
+template <int OP, bool LDS>
+__device__ __forceinline__ void gs_atomic(double* p, double v) {
+  constexpr int scope = LDS ? __HIP_MEMORY_SCOPE_WORKGROUP : __HIP_MEMORY_SCOPE_AGENT;
+  if (OP == 0)
+    __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, scope);
+  else if (OP == 1)
+    __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, scope);
+  else
+    __hip_atomic_fetch_max(p, v, __ATOMIC_RELAXED, scope);
+}
+
+template <int OP, bool LDS>
+__global__ __launch_bounds__(256) void group_reduce_kernel(const long long* __restrict__ idx,
+                                                           const double* __restrict__ v, long long n, int C,
+                                                           int nbins, double* __restrict__ out) {
   __shared__ double acc[LDS ? GS_LDS_MAX : 1];
   const int lane = lane_id();
   const int tot = nbins * C;
   if (LDS) {
-    for (int j = threadIdx.x; j < tot; j += blockDim.x) acc[j] = 0.0;
+    for (int j = threadIdx.x; j < tot; j += blockDim.x) acc[j] = gs_ident<OP>();
     __syncthreads();
   }
   double* dst = LDS ? acc : out;
@@ -129,44 +156,42 @@ __global__ __launch_bounds__(256) void group_sum_kernel(const long long* __restr
       const unsigned long long mm = __ballot(m);
       if (__popcll(mm) == 1) {
         // a singleton group: no merge to gain, the lane adds on its own
-        if (m) {
-          for (int c = 0; c < C; ++c) {
-            if (LDS)
-              __hip_atomic_fetch_add(&dst[(size_t)lk * C + c], v[(size_t)i * C + c], __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_WORKGROUP);
-            else
-              gbl_add(&dst[(size_t)lk * C + c], v[(size_t)i * C + c]);
-          }
-        }
+        if (m)
+          for (int c = 0; c < C; ++c) gs_atomic<OP, LDS>(&dst[(size_t)lk * C + c], v[(size_t)i * C + c]);
       } else {
         for (int c = 0; c < C; ++c) {
-          const double t = wave_sum(m ? v[(size_t)i * C + c] : 0.0);
-          if (lane == leader) {
-            if (LDS)
-              __hip_atomic_fetch_add(&dst[(size_t)lk * C + c], t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            else
-              gbl_add(&dst[(size_t)lk * C + c], t);
-          }
+          const double t = gs_wave<OP>(m ? v[(size_t)i * C + c] : gs_ident<OP>());
+          if (lane == leader) gs_atomic<OP, LDS>(&dst[(size_t)lk * C + c], t);
         }
       }
       if (m) pend = false;
       act &= ~mm;
     }
-    if (pend) {
-      for (int c = 0; c < C; ++c) {
-        if (LDS)
-          __hip_atomic_fetch_add(&dst[(size_t)key * C + c], v[(size_t)i * C + c], __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_WORKGROUP);
-        else
-          gbl_add(&dst[(size_t)key * C + c], v[(size_t)i * C + c]);
-      }
-    }
+    if (pend)
+      for (int c = 0; c < C; ++c) gs_atomic<OP, LDS>(&dst[(size_t)key * C + c], v[(size_t)i * C + c]);
   }
   if (LDS) {
     __syncthreads();
     for (int j = threadIdx.x; j < tot; j += blockDim.x)
-      if (acc[j] != 0.0) gbl_add(&out[j], acc[j]);
+      if (acc[j] != gs_ident<OP>()) gs_atomic<OP, false>(&out[j], acc[j]);
   }
+}
+
+template <int OP>
+static int gs_launch(const long long* idx, const double* v, long long n, int C, int nbins, double* out,
+                     hipStream_t s) {
+  const bool lds = (long long)nbins * C <= GS_LDS_MAX;
+  long long blocks = (n + 255) / 256;
+  // LDS mode flushes nbins * C atomics per block: fewer, fuller blocks
+  const long long cap = lds ? 1024 : 4096;
+  if (blocks > cap) blocks = cap;
+  if (lds)
+    hipLaunchKernelGGL((group_reduce_kernel<OP, true>), dim3((unsigned)blocks), dim3(256), 0, s, idx, v, n, C, nbins,
+                       out);
+  else
+    hipLaunchKernelGGL((group_reduce_kernel<OP, false>), dim3((unsigned)blocks), dim3(256), 0, s, idx, v, n, C,
+                       nbins, out);
+  return (int)hipGetLastError();
 }
 
 extern "C" {
@@ -183,21 +208,17 @@ int h2o_logit_hist(const double* p, const double* y, const double* w, long long 
   return (int)hipGetLastError();
 }
 
-// idx: i64 [n]; v: f64 [n, C] row-major; out: f64 [nbins, C], zeroed by the
-// caller (it accumulates).
-int h2o_group_sum(const long long* idx, const double* v, long long n, int C, int nbins, double* out, hipStream_t s) {
+// idx: i64 [n]; v: f64 [n, C] row-major; out: f64 [nbins, C], filled by the
+// caller with the op's identity (0 / +inf / -inf): it accumulates.
+// op 0 sum, 1 min, 2 max.
+int h2o_group_reduce(const long long* idx, const double* v, long long n, int C, int nbins, int op, double* out,
+                     hipStream_t s) {
   if (n <= 0 || C <= 0 || nbins <= 0) return 0;
   if ((long long)nbins * C > 0x7fffffffLL) return -1;
-  const bool lds = (long long)nbins * C <= GS_LDS_MAX;
-  long long blocks = (n + 255) / 256;
-  // LDS mode flushes nbins * C adds per block: fewer, fuller blocks
-  const long long cap = lds ? 1024 : 4096;
-  if (blocks > cap) blocks = cap;
-  if (lds)
-    hipLaunchKernelGGL(group_sum_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, s, idx, v, n, C, nbins, out);
-  else
-    hipLaunchKernelGGL(group_sum_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, s, idx, v, n, C, nbins, out);
-  return (int)hipGetLastError();
+  if (op == 0) return gs_launch<0>(idx, v, n, C, nbins, out, s);
+  if (op == 1) return gs_launch<1>(idx, v, n, C, nbins, out, s);
+  if (op == 2) return gs_launch<2>(idx, v, n, C, nbins, out, s);
+  return -2;
 }
 
 }  // extern "C"

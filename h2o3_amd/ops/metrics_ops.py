@@ -16,7 +16,7 @@ def _lib():
     if lib is not None and not getattr(lib, "_typed", False):
         P = ctypes.c_void_p
         lib.h2o_logit_hist.argtypes = [P, P, P, ctypes.c_longlong, ctypes.c_int, P, P, P]
-        lib.h2o_group_sum.argtypes = [P, P, ctypes.c_longlong, ctypes.c_int, ctypes.c_int, P, P]
+        lib.h2o_group_reduce.argtypes = [P, P, ctypes.c_longlong, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P]
         lib._typed = True
     return lib
 
@@ -49,22 +49,32 @@ def logit_hist(y, p1, w, nb):
     return buf
 
 
-def group_sum(idx, vals, nbins):
-    """f64 [nbins, C] sums of vals [n, C] by idx (rows outside [0, nbins)
-    skipped), on the device."""
+_OPS = {"sum": (0, 0.0), "min": (1, float("inf")), "max": (2, float("-inf"))}
+
+
+def group_reduce(idx, vals, nbins, op="sum"):
+    """f64 [nbins, C] sums / minima / maxima of vals [n, C] by idx (rows
+    outside [0, nbins) skipped; empty groups hold 0 / +inf / -inf), on the
+    device."""
     lib = _lib()
     if lib is None:
         raise RuntimeError("metrics HIP library missing")
+    code, fill = _OPS[op]
     v = vals.to(torch.float64).contiguous()
     idx = idx.reshape(-1).to(device=v.device, dtype=torch.int64).contiguous()
     n, C = v.shape
     if idx.numel() != n:
-        raise ValueError("group_sum: idx / vals lengths differ")
-    out = torch.zeros((nbins, C), dtype=torch.float64, device=v.device)
+        raise ValueError("group_reduce: idx / vals lengths differ")
+    out = torch.full((nbins, C), fill, dtype=torch.float64, device=v.device)
     if n == 0 or nbins == 0 or C == 0:
         return out
-    rc = lib.h2o_group_sum(ctypes.c_void_p(idx.data_ptr()), ctypes.c_void_p(v.data_ptr()), n, C, nbins,
-                           ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    rc = lib.h2o_group_reduce(ctypes.c_void_p(idx.data_ptr()), ctypes.c_void_p(v.data_ptr()), n, C, nbins, code,
+                              ctypes.c_void_p(out.data_ptr()),
+                              ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
     if rc != 0:
-        raise RuntimeError(f"h2o_group_sum failed ({rc})")
+        raise RuntimeError(f"h2o_group_reduce failed ({rc})")
     return out
+
+
+def group_sum(idx, vals, nbins):
+    return group_reduce(idx, vals, nbins, "sum")

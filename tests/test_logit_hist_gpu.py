@@ -90,3 +90,17 @@ def test_group_sum_matches_index_add(n, nbins, C, kind):
         index_add(out, idx, v if C > 1 else v.view(-1))
         torch.testing.assert_close(out, ref + 1, rtol=1e-9, atol=1e-8)
     torch.testing.assert_close(got, ref, rtol=1e-9, atol=1e-8)
+
+
+@pytest.mark.parametrize("n,nbins,C", [(400_000, 1, 1), (400_000, 5, 3), (200_000, 30_000, 2)])
+@pytest.mark.parametrize("op", ["min", "max"])
+def test_group_extreme_matches_host(n, nbins, C, op):
+    from h2o3_amd.core.groupsum import group_extreme
+    g = torch.Generator(device="cuda").manual_seed(13)
+    idx = torch.randint(0, nbins, (n,), generator=g, device="cuda")
+    v = torch.randn((n, C), generator=g, device="cuda", dtype=torch.float64)
+    fill = float("inf") if op == "min" else float("-inf")
+    ref = torch.full((nbins, C), fill, dtype=torch.float64).scatter_reduce_(
+        0, idx.cpu().view(-1, 1).expand(-1, C), v.cpu(), reduce="amin" if op == "min" else "amax")
+    got = group_extreme(idx, v, nbins, op)
+    assert torch.equal(got.cpu(), ref)
