@@ -365,8 +365,11 @@ class H2OAutoML:
             return
         lb = Leaderboard(fam, sort_metric=self.sort_metric)
         best = lb.models[0]
-        base = {k: v for k, v in best._parms.items() if k not in ("model_id", "training_frame", "validation_frame",
-                                                                  "response_column", "checkpoint")}
+        # only the names this estimator takes (its _parms also carry the
+        # shared defaults every estimator holds)
+        base = {k: v for k, v in best._user_parms().items() if k not in ("model_id", "training_frame",
+                                                                          "validation_frame", "response_column",
+                                                                          "checkpoint")}
         if step == "lr_annealing":
             cands = [dict(learn_rate=0.05 if algo == "GBM" else 0.1, learn_rate_annealing=0.99)]
         else:
