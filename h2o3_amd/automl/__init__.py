@@ -26,6 +26,7 @@ import json
 import math
 import os
 import time
+import zlib
 
 import numpy as np
 
@@ -344,7 +345,9 @@ class H2OAutoML:
             self._build(cls, algo, name, _step_params(algo, step), data)
         elif step.startswith("grid_"):
             g = _grid_space(algo, step, classification)
-            rng = np.random.RandomState(self._seed() + hash((algo, step)) % 1000)
+            # a stable per-step offset (str hash() is salted per process, which
+            # made seeded AutoML grids draw different models on every run)
+            rng = np.random.RandomState(self._seed() + zlib.crc32(f"{algo}:{step}".encode()) % 1000)
             nmax = self.grid_models_per_step or 10 ** 6
             for i in range(nmax):
                 if not self._budget_left():

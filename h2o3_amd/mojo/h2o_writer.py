@@ -27,6 +27,7 @@ from __future__ import annotations
 import io
 import struct
 import time
+import zlib
 import zipfile
 
 import numpy as np
@@ -103,7 +104,7 @@ def _header(model, algo_short, algo_full, category, columns, nfeatures, nclasses
     info = {
         "h2o_version": "3.46.0.99999", "mojo_version": mojo_version, "license": "Apache License Version 2.0",
         "algo": algo_short, "algorithm": algo_full, "endianness": "LITTLE_ENDIAN", "category": category,
-        "uuid": str(abs(hash(model.model_id)) % (1 << 62)), "supervised": supervised, "n_features": nfeatures,
+        "uuid": str(zlib.crc32(str(model.model_id).encode()) * 2654435761 % (1 << 62)), "supervised": supervised, "n_features": nfeatures,
         "n_classes": nclasses, "n_columns": len(columns), "n_domains": sum(d is not None for d in domains),
         "balance_classes": False, "default_threshold": _threshold(model),
         "prior_class_distrib": None, "model_class_distrib": None,

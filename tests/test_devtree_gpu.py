@@ -134,3 +134,45 @@ def test_devtree_row_and_column_sampling(monkeypatch, kw):
         np.testing.assert_allclose(np.asarray(ta.thr), np.asarray(tb.thr))
         np.testing.assert_allclose(np.asarray(ta.value), np.asarray(tb.value), rtol=1e-5, atol=1e-8)
     np.testing.assert_allclose(p1, p0, rtol=1e-5, atol=1e-6)
+
+
+# draws from AutoML's GBM grid space (automl/_grid_space) with max_depth in
+# the device tree's range: the device tree must grow the level loop's trees
+# for every sampling / min_rows / min_split_improvement combination it takes
+_GRID_DRAWS = [dict(max_depth=3, min_rows=100, sample_rate=0.5, col_sample_rate=0.4, col_sample_rate_per_tree=0.4,
+                    min_split_improvement=1e-4),
+               dict(max_depth=7, min_rows=30, sample_rate=1.0, col_sample_rate=1.0, col_sample_rate_per_tree=0.4,
+                    min_split_improvement=1e-5),
+               dict(max_depth=11, min_rows=1, sample_rate=0.9, col_sample_rate=0.7, col_sample_rate_per_tree=1.0,
+                    min_split_improvement=1e-4),
+               dict(max_depth=5, min_rows=15, sample_rate=0.6, col_sample_rate=0.4, col_sample_rate_per_tree=0.7,
+                    min_split_improvement=1e-5)]
+
+
+@pytest.mark.parametrize("hp", _GRID_DRAWS, ids=[f"d{h['max_depth']}" for h in _GRID_DRAWS])
+def test_devtree_matches_level_loop_on_automl_grid_draws(monkeypatch, hp):
+    fr, names = _frame(300_000, 48, "bernoulli", seed=4)
+    d1, f1, p1 = _fit(monkeypatch, fr, names, True, **hp)
+    assert getattr(d1, "_devtree", None) is not None, getattr(d1, "_devtree_why", None)
+    d0, f0, p0 = _fit(monkeypatch, fr, names, False, **hp)
+    _same_trees(f1, f0)
+    np.testing.assert_allclose(p1, p0, rtol=1e-5, atol=1e-6)
+
+
+def test_devtree_full_train_with_early_stopping(monkeypatch):
+    """The estimator path (scoring every 5 trees, early stopping, validation
+    scoring) gives the level loop's model and a sound AUC."""
+    from h2o3_amd.estimators import H2OGradientBoostingEstimator
+    fr, names = _frame(200_000, 48, "bernoulli", seed=5)
+    va, _ = _frame(50_000, 48, "bernoulli", seed=6)
+    out = {}
+    for dev in (True, False):
+        monkeypatch.setenv("H2O3_DEV_TREE", "1" if dev else "0")
+        m = H2OGradientBoostingEstimator(ntrees=60, score_tree_interval=5, stopping_rounds=3, seed=3,
+                                         **_GRID_DRAWS[0])
+        m.train(x=names, y="y", training_frame=fr, validation_frame=va)
+        out[dev] = (len(m._forest), m.auc(valid=True),
+                    m.predict(va).as_data_frame()["1"].to_numpy())
+    assert out[True][0] == out[False][0]
+    assert out[True][1] > 0.7, out[True][1]
+    np.testing.assert_allclose(out[True][2], out[False][2], rtol=1e-5, atol=1e-6)
