@@ -172,7 +172,7 @@ def test_devtree_full_train_with_early_stopping(monkeypatch):
                                          **_GRID_DRAWS[0])
         m.train(x=names, y="y", training_frame=fr, validation_frame=va)
         out[dev] = (len(m._forest), m.auc(valid=True),
-                    m.predict(va).as_data_frame()["1"].to_numpy())
+                    m.predict(va).as_data_frame().iloc[:, -1].to_numpy())
     assert out[True][0] == out[False][0]
     assert out[True][1] > 0.7, out[True][1]
     np.testing.assert_allclose(out[True][2], out[False][2], rtol=1e-5, atol=1e-6)
