@@ -850,6 +850,8 @@ class GLMDriver:
         g = torch.zeros(P + 1, dtype=torch.float64, device=dv)
         dev = torch.zeros(1, dtype=torch.float64, device=dv)
         ident = self.fam.family == "gaussian" and self.fam.link == "identity"
+        native = (X.is_cuda and X.dtype == torch.float32 and X.stride(1) == 1
+                  and os.environ.get("H2O3_GLM_F64_MFMA", "1") == "1")
         with phase("glm.irls_f64"):
             for a in range(0, X.shape[0], step):
                 Xc = X[a:a + step, :P].to(torch.float64)
@@ -864,10 +866,18 @@ class GLMDriver:
                     d = self.fam.dmu_deta(eta, mu)
                     wd = w * d / self.fam.variance(mu)
                     W, r = wd * d, wd * (y - mu)
-                Xa = torch.cat([Xc, torch.ones((Xc.shape[0], 1), dtype=torch.float64, device=dv)], 1)
-                del Xc
-                Ga += (Xa * W.view(-1, 1)).T @ Xa
-                g += Xa.T @ r
+                if native:
+                    # exact f64 products on the f64 matrix cores, straight
+                    # from the f32 rows (no f64 copy of X in the Gram)
+                    Ga += linalg_ops.gram_f64_aug(X[a:a + step], P, W)
+                    g[:P] += Xc.T @ r
+                    g[P] += r.sum()
+                    del Xc
+                else:
+                    Xa = torch.cat([Xc, torch.ones((Xc.shape[0], 1), dtype=torch.float64, device=dv)], 1)
+                    del Xc
+                    Ga += (Xa * W.view(-1, 1)).T @ Xa
+                    g += Xa.T @ r
                 dev += (w * self.fam.deviance(y, mu)).sum()
         self._gexact = g
         self._gbeta = self.beta.copy()

@@ -1777,3 +1777,117 @@ extern "C" int h2o_glm_wide_gram256(const float* X, int ldx, int P, long long N,
   }
   return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------
+// Exact f64 weighted Gram on the f64 matrix cores: G = Xa' diag(W) Xa with
+// Xa = [X[:, :P] | 1] (the intercept column implicit), f32 storage widened
+// exactly, f64 products and f64 accumulation -- the top GLM precision tier
+// (ill-conditioned designs: RuleFit's 0/1 rule matrices, near-collinear
+// columns), which ran as chunked f64 torch GEMMs over an f64 copy of X.
+//
+// Reference: hex/gram/Gram.java (GramTask: X'WX accumulated in double per
+// chunk, reduced across nodes).
+//
+// Layout.  One workgroup = one 64 x 64 tile pair (I <= J) of the augmented
+// Gram over one slab of rows; 4 waves, each a 32 x 32 quarter = 2 x 2
+// v_mfma_f64_16x16x4_f64 blocks (A lane l: A[l&15][k=l>>4]; C/D: col=l&15,
+// row=(l>>4)+4*reg).  Rows are staged 16 at a time through LDS as f64
+// (A side pre-multiplied by W), the next 16 rows prefetched into registers
+// while the MFMAs run.  Slab partials [S][npairs][64][64] are summed in a
+// fixed order by the caller (deterministic).
+#define GF_T 64
+#define GF_KR 16
+
+__device__ __forceinline__ double gf_load(const float* __restrict__ X, int ldx, int P, long long N, long long r,
+                                          int c) {
+  if (r >= N) return 0.0;
+  if (c < P) return (double)X[(size_t)r * ldx + c];
+  return c == P ? 1.0 : 0.0;
+}
+
+__global__ __launch_bounds__(256) void gram_f64_kernel(const float* __restrict__ X, int ldx, int P, long long N,
+                                                       const double* __restrict__ W, const int2* __restrict__ pairs,
+                                                       int npairs, long long rows_per_slab,
+                                                       double* __restrict__ part) {
+  __shared__ double As[GF_KR][GF_T + 1];
+  __shared__ double Bs[GF_KR][GF_T + 1];
+  // blocks of one slab are consecutive: the tile pairs of a slab run
+  // together and share its rows in L2
+  const int p = blockIdx.x % npairs;
+  const long long s = blockIdx.x / npairs;
+  const int I0 = pairs[p].x * GF_T, J0 = pairs[p].y * GF_T;
+  const long long r0 = s * rows_per_slab;
+  long long r1 = r0 + rows_per_slab;
+  if (r1 > N) r1 = N;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int wi = wv >> 1, wj = wv & 1;
+  typedef double d4 __attribute__((ext_vector_type(4)));
+  d4 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+  // staging map: element e of thread t is (row (t + 256 e) / 64, col (t + 256 e) % 64)
+  double ra[4], rb[4];
+  auto fetch = [&](long long base) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int idx = t + 256 * e;
+      const int rr = idx >> 6, cc = idx & 63;
+      const long long r = base + rr;
+      const bool in = r < r1;
+      const double w = in ? W[r] : 0.0;
+      ra[e] = in ? gf_load(X, ldx, P, N, r, I0 + cc) * w : 0.0;
+      rb[e] = in ? gf_load(X, ldx, P, N, r, J0 + cc) : 0.0;
+    }
+  };
+  if (r0 < r1) fetch(r0);
+  for (long long base = r0; base < r1; base += GF_KR) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int idx = t + 256 * e;
+      As[idx >> 6][idx & 63] = ra[e];
+      Bs[idx >> 6][idx & 63] = rb[e];
+    }
+    __syncthreads();
+    if (base + GF_KR < r1) fetch(base + GF_KR);   // overlaps the MFMAs below
+#pragma unroll
+    for (int ks = 0; ks < GF_KR / 4; ++ks) {
+      const int k = 4 * ks + (lane >> 4);
+      double a0 = As[k][wi * 32 + (lane & 15)];
+      double a1 = As[k][wi * 32 + 16 + (lane & 15)];
+      double b0 = Bs[k][wj * 32 + (lane & 15)];
+      double b1 = Bs[k][wj * 32 + 16 + (lane & 15)];
+      acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  double* out = part + ((size_t)s * npairs + p) * (GF_T * GF_T);
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        const int row = wi * 32 + a * 16 + (lane >> 4) + 4 * reg;
+        const int col = wj * 32 + b * 16 + (lane & 15);
+        out[row * GF_T + col] = acc[a][b][reg];
+      }
+}
+
+// X: f32 [N, ldx] (first P columns used), W: f64 [N]; pairs: int2 [npairs]
+// tile pairs (I <= J) of the augmented Gram (P + 1 columns, 64-wide tiles);
+// part: f64 [slabs, npairs, 64, 64].
+extern "C" int h2o_gram_f64(const float* X, int ldx, int P, long long N, const double* W, const int* pairs,
+                            int npairs, int slabs, long long rows_per_slab, double* part, hipStream_t s) {
+  if (npairs <= 0 || slabs <= 0) return 0;
+  if (P < 0 || ldx < P || rows_per_slab <= 0 || (long long)slabs * rows_per_slab < N) return -1;
+  const long long blocks = (long long)slabs * npairs;
+  if (blocks > 0x7fffffffLL) return -2;
+  hipLaunchKernelGGL(gram_f64_kernel, dim3((unsigned)blocks), dim3(256), 0, s, X, ldx, P, N, W,
+                     (const int2*)pairs, npairs, rows_per_slab, part);
+  return (int)hipGetLastError();
+}

@@ -28,6 +28,7 @@ def _lib():
         lib.h2o_glm_wide_gram.argtypes = [P, I, I, LL, P, I, I, P, I, P]
         lib.h2o_glm_wide_split_grid.argtypes = [I]
         lib.h2o_glm_wide_gram256.argtypes = [P, I, I, LL, P, I, I, P, I, I, P]
+        lib.h2o_gram_f64.argtypes = [P, I, I, LL, P, P, I, I, LL, P, P]
         lib._typed = True
     return lib
 
@@ -205,6 +206,38 @@ def weighted_gram(X: torch.Tensor, w: torch.Tensor | None = None, use_native=Non
     if rc != 0:
         raise RuntimeError(f"h2o_gram failed: {rc}")
     return _assemble(out.sum(0), pairs_t, T)
+
+
+def gram_f64_aug(X: torch.Tensor, P: int, W: torch.Tensor, part_budget: int = 1 << 28) -> torch.Tensor:
+    """[P+1, P+1] f64 Gram of [X[:, :P] | 1] weighted by W (f64 [N]), exact
+    f64 products on the f64 matrix cores (ops/csrc/gram.hip gram_f64_kernel):
+    the GLM top precision tier without an f64 copy of X.  X: f32 [N, ldx]
+    with unit column stride."""
+    N = X.shape[0]
+    Pa = P + 1
+    T = -(-Pa // 64)
+    if N == 0:
+        return torch.zeros((Pa, Pa), dtype=torch.float64, device=X.device)
+    if X.dtype != torch.float32 or X.stride(1) != 1:
+        raise ValueError("gram_f64_aug: X must be f32 with unit column stride")
+    lib = _lib()
+    pairs_t, pr = _pairs(T, X.device)
+    npairs = len(pr)
+    # enough slabs for ~2048 workgroups, partials within the budget
+    slabs = max(1, min(-(-2048 // npairs), N // 256, part_budget // (npairs * 64 * 64 * 8)))
+    rps = -(-N // slabs)
+    rps = ((rps + 15) // 16) * 16
+    slabs = -(-N // rps)
+    part = torch.empty((slabs, npairs, 64, 64), dtype=torch.float64, device=X.device)
+    Wd = W.to(torch.float64).contiguous()
+    if Wd.numel() != N:
+        raise ValueError("gram_f64_aug: W length differs from X rows")
+    rc = lib.h2o_gram_f64(ctypes.c_void_p(X.data_ptr()), X.stride(0), P, N, ctypes.c_void_p(Wd.data_ptr()),
+                          ctypes.c_void_p(pairs_t.data_ptr()), npairs, slabs, rps, ctypes.c_void_p(part.data_ptr()),
+                          ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    if rc != 0:
+        raise RuntimeError(f"h2o_gram_f64 failed: {rc}")
+    return _assemble(part.sum(0), pairs_t, T)[:Pa, :Pa]
 
 
 # Row chunks per batched Gram GEMM: C_b = hi_b^T [hi_b | lo_b] for g chunks of

@@ -622,3 +622,24 @@ def test_xv_kernel_matches_fp64():
         assert out.dtype == torch.float32 and out.shape == (N, k)
         ref = X.double() @ V
         torch.testing.assert_close(out.double(), ref, rtol=1e-4, atol=1e-4 * float(ref.abs().max()))
+
+
+@pytest.mark.parametrize("N,P,ldx", [(100_003, 5, 8), (65_536, 63, 64), (50_000, 64, 96), (40_000, 130, 130),
+                                     (10, 3, 3)])
+def test_gram_f64_aug_matches_fp64(N, P, ldx):
+    """gram_f64_kernel (f64 MFMA) against torch fp64 on [X | 1]: exact f64
+    products, so only summation order differs."""
+    from h2o3_amd.ops import linalg_ops
+    g = torch.Generator(device="cuda").manual_seed(P)
+    Xs = torch.randn((N, ldx), generator=g, device="cuda")
+    Xs[:, :P:3] = (Xs[:, :P:3] > 0.3).float()          # 0/1 rule-like columns
+    W = torch.rand(N, generator=g, device="cuda", dtype=torch.float64)
+    W[::11] = 0.0
+    G = linalg_ops.gram_f64_aug(Xs, P, W)
+    Xa = torch.cat([Xs[:, :P].double(), torch.ones((N, 1), dtype=torch.float64, device="cuda")], 1)
+    ref = (Xa * W.view(-1, 1)).T @ Xa
+    torch.testing.assert_close(G, ref, rtol=1e-12, atol=1e-9)
+    # a row slice (the GLM passes chunks of a larger matrix)
+    G2 = linalg_ops.gram_f64_aug(Xs[7:N // 2], P, W[7:N // 2])
+    ref2 = (Xa[7:N // 2] * W[7:N // 2].view(-1, 1)).T @ Xa[7:N // 2]
+    torch.testing.assert_close(G2, ref2, rtol=1e-12, atol=1e-9)
