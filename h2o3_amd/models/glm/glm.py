@@ -854,8 +854,12 @@ class GLMDriver:
                   and os.environ.get("H2O3_GLM_F64_MFMA", "1") == "1")
         with phase("glm.irls_f64"):
             for a in range(0, X.shape[0], step):
-                Xc = X[a:a + step, :P].to(torch.float64)
-                eta = Xc @ bt + float(self.beta[-1])
+                if native:
+                    Xc = None
+                    eta = linalg_ops.xv_f64(X[a:a + step], P, bt, float(self.beta[-1]))
+                else:
+                    Xc = X[a:a + step, :P].to(torch.float64)
+                    eta = Xc @ bt + float(self.beta[-1])
                 if self.offset is not None:
                     eta = eta + self.offset[a:a + step]
                 w, y = self.w[a:a + step], self.y[a:a + step]
@@ -870,9 +874,8 @@ class GLMDriver:
                     # exact f64 products on the f64 matrix cores, straight
                     # from the f32 rows (no f64 copy of X in the Gram)
                     Ga += linalg_ops.gram_f64_aug(X[a:a + step], P, W)
-                    g[:P] += Xc.T @ r
+                    g[:P] += linalg_ops.xtr_f64(X[a:a + step], P, r)
                     g[P] += r.sum()
-                    del Xc
                 else:
                     Xa = torch.cat([Xc, torch.ones((Xc.shape[0], 1), dtype=torch.float64, device=dv)], 1)
                     del Xc

@@ -1891,3 +1891,53 @@ extern "C" int h2o_gram_f64(const float* X, int ldx, int P, long long N, const d
                      (const int2*)pairs, npairs, rows_per_slab, part);
   return (int)hipGetLastError();
 }
+
+// The two f64 matrix-vector products of the same tier, straight from the f32
+// rows: eta = X[:, :P] beta + b0 (one wave per row, coalesced along the row,
+// f64 FMAs, wave sum) and the gradient partials X[:, :P]' r per row slab
+// (thread per column, coalesced row reads, f64 register sums; slabs summed by
+// the caller in a fixed order).
+__global__ __launch_bounds__(256) void xv_f64_kernel(const float* __restrict__ X, int ldx, int P, long long N,
+                                                     const double* __restrict__ beta, double b0,
+                                                     double* __restrict__ eta) {
+  const int lane = threadIdx.x & 63;
+  const long long r = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= N) return;   // wave-uniform
+  const float* xr = X + (size_t)r * ldx;
+  double acc = 0.0;
+  for (int c = lane; c < P; c += 64) acc += (double)xr[c] * beta[c];
+  acc = wave_sum(acc);
+  if (lane == 0) eta[r] = acc + b0;
+}
+
+__global__ __launch_bounds__(256) void xtr_f64_kernel(const float* __restrict__ X, int ldx, int P, long long N,
+                                                      const double* __restrict__ rv, long long rows_per_slab,
+                                                      double* __restrict__ part) {
+  const long long r0 = (long long)blockIdx.y * rows_per_slab;
+  long long r1 = r0 + rows_per_slab;
+  if (r1 > N) r1 = N;
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= P) return;
+  double acc = 0.0;
+  for (long long r = r0; r < r1; ++r) acc += (double)X[(size_t)r * ldx + c] * rv[r];
+  part[(size_t)blockIdx.y * P + c] = acc;
+}
+
+extern "C" int h2o_xv_f64(const float* X, int ldx, int P, long long N, const double* beta, double b0, double* eta,
+                          hipStream_t s) {
+  if (N <= 0) return 0;
+  if (P < 0 || ldx < P) return -1;
+  const long long blocks = (N + 3) / 4;
+  if (blocks > 0x7fffffffLL) return -2;
+  hipLaunchKernelGGL(xv_f64_kernel, dim3((unsigned)blocks), dim3(256), 0, s, X, ldx, P, N, beta, b0, eta);
+  return (int)hipGetLastError();
+}
+
+extern "C" int h2o_xtr_f64(const float* X, int ldx, int P, long long N, const double* r, int slabs,
+                           long long rows_per_slab, double* part, hipStream_t s) {
+  if (N <= 0 || P <= 0) return 0;
+  if (ldx < P || slabs <= 0 || slabs > 65535 || (long long)slabs * rows_per_slab < N) return -1;
+  hipLaunchKernelGGL(xtr_f64_kernel, dim3((unsigned)((P + 255) / 256), (unsigned)slabs), dim3(256), 0, s, X, ldx, P,
+                     N, r, rows_per_slab, part);
+  return (int)hipGetLastError();
+}

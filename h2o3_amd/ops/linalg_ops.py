@@ -29,6 +29,8 @@ def _lib():
         lib.h2o_glm_wide_split_grid.argtypes = [I]
         lib.h2o_glm_wide_gram256.argtypes = [P, I, I, LL, P, I, I, P, I, I, P]
         lib.h2o_gram_f64.argtypes = [P, I, I, LL, P, P, I, I, LL, P, P]
+        lib.h2o_xv_f64.argtypes = [P, I, I, LL, P, ctypes.c_double, P, P]
+        lib.h2o_xtr_f64.argtypes = [P, I, I, LL, P, I, LL, P, P]
         lib._typed = True
     return lib
 
@@ -238,6 +240,49 @@ def gram_f64_aug(X: torch.Tensor, P: int, W: torch.Tensor, part_budget: int = 1 
     if rc != 0:
         raise RuntimeError(f"h2o_gram_f64 failed: {rc}")
     return _assemble(part.sum(0), pairs_t, T)[:Pa, :Pa]
+
+
+def xv_f64(X: torch.Tensor, P: int, beta: torch.Tensor, b0: float = 0.0) -> torch.Tensor:
+    """f64 [N] = X[:, :P] beta + b0 with f64 products from the f32 rows."""
+    N = X.shape[0]
+    out = torch.empty(N, dtype=torch.float64, device=X.device)
+    if N == 0:
+        return out
+    if X.dtype != torch.float32 or X.stride(1) != 1:
+        raise ValueError("xv_f64: X must be f32 with unit column stride")
+    bt = beta.to(device=X.device, dtype=torch.float64).contiguous()
+    if bt.numel() < P:
+        raise ValueError("xv_f64: beta shorter than P")
+    rc = _lib().h2o_xv_f64(ctypes.c_void_p(X.data_ptr()), X.stride(0), P, N, ctypes.c_void_p(bt.data_ptr()),
+                           float(b0), ctypes.c_void_p(out.data_ptr()),
+                           ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    if rc != 0:
+        raise RuntimeError(f"h2o_xv_f64 failed: {rc}")
+    return out
+
+
+def xtr_f64(X: torch.Tensor, P: int, r: torch.Tensor) -> torch.Tensor:
+    """f64 [P] = X[:, :P]' r (r f64 [N]) with f64 products, slab partials
+    summed in a fixed order."""
+    N = X.shape[0]
+    if N == 0 or P == 0:
+        return torch.zeros(P, dtype=torch.float64, device=X.device)
+    if X.dtype != torch.float32 or X.stride(1) != 1:
+        raise ValueError("xtr_f64: X must be f32 with unit column stride")
+    rv = r.to(torch.float64).contiguous()
+    if rv.numel() != N:
+        raise ValueError("xtr_f64: r length differs from X rows")
+    cb = -(-P // 256)
+    slabs = max(1, min(65535, N // 512, -(-4096 // cb)))
+    rps = -(-N // slabs)
+    slabs = -(-N // rps)
+    part = torch.empty((slabs, P), dtype=torch.float64, device=X.device)
+    rc = _lib().h2o_xtr_f64(ctypes.c_void_p(X.data_ptr()), X.stride(0), P, N, ctypes.c_void_p(rv.data_ptr()), slabs,
+                            rps, ctypes.c_void_p(part.data_ptr()),
+                            ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    if rc != 0:
+        raise RuntimeError(f"h2o_xtr_f64 failed: {rc}")
+    return part.sum(0)
 
 
 # Row chunks per batched Gram GEMM: C_b = hi_b^T [hi_b | lo_b] for g chunks of

@@ -643,3 +643,15 @@ def test_gram_f64_aug_matches_fp64(N, P, ldx):
     G2 = linalg_ops.gram_f64_aug(Xs[7:N // 2], P, W[7:N // 2])
     ref2 = (Xa[7:N // 2] * W[7:N // 2].view(-1, 1)).T @ Xa[7:N // 2]
     torch.testing.assert_close(G2, ref2, rtol=1e-12, atol=1e-9)
+
+
+@pytest.mark.parametrize("N,P,ldx", [(100_003, 5, 8), (70_000, 300, 320), (3, 2, 2)])
+def test_xv_xtr_f64_match_fp64(N, P, ldx):
+    from h2o3_amd.ops import linalg_ops
+    g = torch.Generator(device="cuda").manual_seed(N % 97)
+    X = torch.randn((N, ldx), generator=g, device="cuda")
+    b = torch.randn(P, generator=g, device="cuda", dtype=torch.float64)
+    r = torch.randn(N, generator=g, device="cuda", dtype=torch.float64)
+    Xd = X[:, :P].double()
+    torch.testing.assert_close(linalg_ops.xv_f64(X, P, b, 0.25), Xd @ b + 0.25, rtol=1e-12, atol=1e-12)
+    torch.testing.assert_close(linalg_ops.xtr_f64(X, P, r), Xd.T @ r, rtol=1e-12, atol=1e-9)
