@@ -627,6 +627,7 @@ class H2OGradientBoostingEstimator(SharedTreeEstimator):
         self._output["init_f"] = drv.init_f
         self._train_f = drv.f
         self._vinc = None
+        self._used_devtree = drv.__dict__.get("_devtree") is not None
         del drv.grower
         self._driver = None
         if p.get("calibrate_model") and p.get("calibration_frame") is not None:

@@ -80,6 +80,15 @@ def run(out_path):
     gbm2.train(x=xn, y="y", training_frame=fr)
     res["gbm2_trees"] = _trees(gbm2)
     res["gbm2_logloss"] = gbm2.logloss()
+    # numeric-only, 32 features, row and per-node column sampling: the
+    # device-resident tree (devtree.py) with its stream-ordered collectives
+    xd = [f"x{i}" for i in range(32)]
+    gbm3 = H2OGradientBoostingEstimator(ntrees=4, max_depth=6, seed=1, min_rows=20, sample_rate=0.8,
+                                        col_sample_rate=0.7, histogram_type="QuantilesGlobal", nbins=255)
+    gbm3.train(x=xd, y="y", training_frame=fr)
+    res["gbm3_trees"] = _trees(gbm3)
+    res["gbm3_logloss"] = gbm3.logloss()
+    res["gbm3_devtree"] = bool(getattr(gbm3, "_used_devtree", False))
     from h2o3_amd.ops import _native
     res["native"] = _native.loaded_libs()
     if cloud.rank() == 0:

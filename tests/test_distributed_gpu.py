@@ -59,7 +59,10 @@ def test_two_ranks_one_gpu_grow_same_trees(tmp_path):
     two = _run(2, str(tmp_path / "w2.json"))
     assert one["world"] == 1 and two["world"] == 2 and two["backend"] == "gloo"
     assert any("libtree_hist.so" in s for s in two["native"]) and any("libtree_split.so" in s for s in two["native"])
-    for key in ("drf_trees", "drf2_trees", "gbm_trees", "gbm2_trees"):
+    # the device-resident tree ran in both clouds (stream-ordered collectives at W = 2)
+    assert one["gbm3_devtree"] and two["gbm3_devtree"]
+    assert abs(one["gbm3_logloss"] - two["gbm3_logloss"]) < 1e-5
+    for key in ("drf_trees", "drf2_trees", "gbm_trees", "gbm2_trees", "gbm3_trees"):
         assert len(one[key]) == len(two[key])
         for t1, t2 in zip(one[key], two[key]):
             assert t1["feat"] == t2["feat"], key
