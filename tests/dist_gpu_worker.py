@@ -80,15 +80,28 @@ def run(out_path):
     gbm2.train(x=xn, y="y", training_frame=fr)
     res["gbm2_trees"] = _trees(gbm2)
     res["gbm2_logloss"] = gbm2.logloss()
-    # numeric-only, 32 features, row and per-node column sampling: the
-    # device-resident tree (devtree.py) with its stream-ordered collectives
+    # numeric-only, 32 features: the device-resident tree (devtree.py) with
+    # its stream-ordered collectives -- without sampling (gbm3), with row and
+    # per-node column sampling (gbm4), and gbm4's configuration on the level
+    # loop (gbm5)
     xd = [f"x{i}" for i in range(32)]
-    gbm3 = H2OGradientBoostingEstimator(ntrees=4, max_depth=6, seed=1, min_rows=20, sample_rate=0.8,
-                                        col_sample_rate=0.7, histogram_type="QuantilesGlobal", nbins=255)
-    gbm3.train(x=xd, y="y", training_frame=fr)
-    res["gbm3_trees"] = _trees(gbm3)
-    res["gbm3_logloss"] = gbm3.logloss()
-    res["gbm3_devtree"] = bool(getattr(gbm3, "_used_devtree", False))
+    qg = dict(ntrees=4, max_depth=6, seed=1, min_rows=20, histogram_type="QuantilesGlobal", nbins=255)
+    smp = dict(sample_rate=0.8, col_sample_rate=0.7)
+    for key, kw, lvl in (("gbm3", {}, False), ("gbm4", smp, False), ("gbm5", smp, True)):
+        old_env = os.environ.get("H2O3_DEV_TREE")
+        if lvl:
+            os.environ["H2O3_DEV_TREE"] = "0"
+        try:
+            m = H2OGradientBoostingEstimator(**qg, **kw)
+            m.train(x=xd, y="y", training_frame=fr)
+        finally:
+            if old_env is None:
+                os.environ.pop("H2O3_DEV_TREE", None)
+            else:
+                os.environ["H2O3_DEV_TREE"] = old_env
+        res[key + "_trees"] = _trees(m)
+        res[key + "_logloss"] = m.logloss()
+        res[key + "_devtree"] = bool(getattr(m, "_used_devtree", False))
     from h2o3_amd.ops import _native
     res["native"] = _native.loaded_libs()
     if cloud.rank() == 0:

@@ -59,9 +59,22 @@ def test_two_ranks_one_gpu_grow_same_trees(tmp_path):
     two = _run(2, str(tmp_path / "w2.json"))
     assert one["world"] == 1 and two["world"] == 2 and two["backend"] == "gloo"
     assert any("libtree_hist.so" in s for s in two["native"]) and any("libtree_split.so" in s for s in two["native"])
-    # the device-resident tree ran in both clouds (stream-ordered collectives at W = 2)
-    assert one["gbm3_devtree"] and two["gbm3_devtree"]
-    assert abs(one["gbm3_logloss"] - two["gbm3_logloss"]) < 1e-5
+    # the device-resident tree ran in both clouds (stream-ordered collectives
+    # at W = 2), the level loop where forced
+    for w in (one, two):
+        assert w["gbm3_devtree"] and w["gbm4_devtree"] and not w["gbm5_devtree"]
+    ll = {k: (one[k + "_logloss"], two[k + "_logloss"]) for k in ("gbm3", "gbm4", "gbm5")}
+    print("logloss (1 rank, 2 ranks):", ll)
+    # without sampling the cloud size does not change the model
+    assert abs(ll["gbm3"][0] - ll["gbm3"][1]) < 1e-5, ll
+    # row sampling draws from a per-rank stream (like the reference's
+    # per-chunk seeds, the sample depends on the row layout), so at each
+    # cloud size the device tree must grow the level loop's trees
+    for w in (one, two):
+        assert abs(w["gbm4_logloss"] - w["gbm5_logloss"]) < 1e-6, ll
+        for t4, t5 in zip(w["gbm4_trees"], w["gbm5_trees"]):
+            assert t4["feat"] == t5["feat"] and t4["left"] == t5["left"]
+            np.testing.assert_allclose(t4["thr"], t5["thr"], rtol=1e-6, atol=1e-9)
     for key in ("drf_trees", "drf2_trees", "gbm_trees", "gbm2_trees", "gbm3_trees"):
         assert len(one[key]) == len(two[key])
         for t1, t2 in zip(one[key], two[key]):
