@@ -1791,20 +1791,37 @@ extern "C" int h2o_glm_wide_gram256(const float* X, int ldx, int P, long long N,
 // Layout.  One workgroup = one 64 x 64 tile pair (I <= J) of the augmented
 // Gram over one slab of rows; 4 waves, each a 32 x 32 quarter = 2 x 2
 // v_mfma_f64_16x16x4_f64 blocks (A lane l: A[l&15][k=l>>4]; C/D: col=l&15,
-// row=(l>>4)+4*reg).  Rows are staged 16 at a time through LDS as f64
+// row=(l>>4)+4*reg).  Rows are staged 32 at a time through LDS as f64
 // (A side pre-multiplied by W), the next 16 rows prefetched into registers
-// while the MFMAs run.  Slab partials [S][npairs][64][64] are summed in a
+// while the MFMAs run (16-byte row loads when aligned).  Slab partials [S][npairs][64][64] are summed in a
 // fixed order by the caller (deterministic).
 #define GF_T 64
-#define GF_KR 16
+#define GF_KR 32
 
-__device__ __forceinline__ double gf_load(const float* __restrict__ X, int ldx, int P, long long N, long long r,
-                                          int c) {
-  if (r >= N) return 0.0;
+__device__ __forceinline__ double gf_load(const float* __restrict__ X, int ldx, int P, long long r, int c) {
   if (c < P) return (double)X[(size_t)r * ldx + c];
   return c == P ? 1.0 : 0.0;
 }
 
+// 4 consecutive columns c .. c+3 of row r of [X | 1 | 0...] as f64; VEC: one
+// 16-byte load when all four are columns of X (rows 16-byte aligned).
+typedef double gf_d4 __attribute__((ext_vector_type(4)));
+
+template <bool VEC>
+__device__ __forceinline__ gf_d4 gf_load4(const float* __restrict__ X, int ldx, int P, long long r, int c) {
+  if (VEC && c + 3 < P) {
+    const float4 q = *reinterpret_cast<const float4*>(X + (size_t)r * ldx + c);
+    return gf_d4{(double)q.x, (double)q.y, (double)q.z, (double)q.w};
+  }
+  if (c + 3 < P) {
+    const float* x = X + (size_t)r * ldx + c;
+    return gf_d4{(double)x[0], (double)x[1], (double)x[2], (double)x[3]};
+  }
+  return gf_d4{gf_load(X, ldx, P, r, c), gf_load(X, ldx, P, r, c + 1), gf_load(X, ldx, P, r, c + 2),
+               gf_load(X, ldx, P, r, c + 3)};
+}
+
+template <bool VEC>
 __global__ __launch_bounds__(256) void gram_f64_kernel(const float* __restrict__ X, int ldx, int P, long long N,
                                                        const double* __restrict__ W, const int2* __restrict__ pairs,
                                                        int npairs, long long rows_per_slab,
@@ -1816,6 +1833,7 @@ __global__ __launch_bounds__(256) void gram_f64_kernel(const float* __restrict__
   const int p = blockIdx.x % npairs;
   const long long s = blockIdx.x / npairs;
   const int I0 = pairs[p].x * GF_T, J0 = pairs[p].y * GF_T;
+  const bool diag = I0 == J0;
   const long long r0 = s * rows_per_slab;
   long long r1 = r0 + rows_per_slab;
   if (r1 > N) r1 = N;
@@ -1827,37 +1845,49 @@ __global__ __launch_bounds__(256) void gram_f64_kernel(const float* __restrict__
   for (int a = 0; a < 2; ++a)
 #pragma unroll
     for (int b = 0; b < 2; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
-  // staging map: element e of thread t is (row (t + 256 e) / 64, col (t + 256 e) % 64)
-  double ra[4], rb[4];
+  // staging map: quad e of thread t is row (t + 256 e) / 16, columns
+  // 4 ((t + 256 e) % 16) .. +3 (16 threads cover one 64-column row)
+  gf_d4 ra[2], rb[2];
+  double wr[2];
   auto fetch = [&](long long base) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int idx = t + 256 * e;
-      const int rr = idx >> 6, cc = idx & 63;
+    for (int e = 0; e < 2; ++e) {
+      const int q = t + 256 * e;
+      const int rr = q >> 4, cc = (q & 15) * 4;
       const long long r = base + rr;
-      const bool in = r < r1;
-      const double w = in ? W[r] : 0.0;
-      ra[e] = in ? gf_load(X, ldx, P, N, r, I0 + cc) * w : 0.0;
-      rb[e] = in ? gf_load(X, ldx, P, N, r, J0 + cc) : 0.0;
+      const gf_d4 z = {0.0, 0.0, 0.0, 0.0};
+      if (r < r1) {
+        wr[e] = W[r];
+        ra[e] = gf_load4<VEC>(X, ldx, P, r, I0 + cc);
+        rb[e] = diag ? z : gf_load4<VEC>(X, ldx, P, r, J0 + cc);
+      } else {
+        wr[e] = 0.0;
+        ra[e] = z;
+        rb[e] = z;
+      }
     }
   };
   if (r0 < r1) fetch(r0);
   for (long long base = r0; base < r1; base += GF_KR) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int idx = t + 256 * e;
-      As[idx >> 6][idx & 63] = ra[e];
-      Bs[idx >> 6][idx & 63] = rb[e];
+    for (int e = 0; e < 2; ++e) {
+      const int q = t + 256 * e;
+      const int rr = q >> 4, cc = (q & 15) * 4;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        As[rr][cc + u] = ra[e][u] * wr[e];
+        Bs[rr][cc + u] = diag ? ra[e][u] : rb[e][u];
+      }
     }
     __syncthreads();
     if (base + GF_KR < r1) fetch(base + GF_KR);   // overlaps the MFMAs below
 #pragma unroll
     for (int ks = 0; ks < GF_KR / 4; ++ks) {
       const int k = 4 * ks + (lane >> 4);
-      double a0 = As[k][wi * 32 + (lane & 15)];
-      double a1 = As[k][wi * 32 + 16 + (lane & 15)];
-      double b0 = Bs[k][wj * 32 + (lane & 15)];
-      double b1 = Bs[k][wj * 32 + 16 + (lane & 15)];
+      const double a0 = As[k][wi * 32 + (lane & 15)];
+      const double a1 = As[k][wi * 32 + 16 + (lane & 15)];
+      const double b0 = Bs[k][wj * 32 + (lane & 15)];
+      const double b1 = Bs[k][wj * 32 + 16 + (lane & 15)];
       acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
       acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
       acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
@@ -1887,8 +1917,13 @@ extern "C" int h2o_gram_f64(const float* X, int ldx, int P, long long N, const d
   if (P < 0 || ldx < P || rows_per_slab <= 0 || (long long)slabs * rows_per_slab < N) return -1;
   const long long blocks = (long long)slabs * npairs;
   if (blocks > 0x7fffffffLL) return -2;
-  hipLaunchKernelGGL(gram_f64_kernel, dim3((unsigned)blocks), dim3(256), 0, s, X, ldx, P, N, W,
-                     (const int2*)pairs, npairs, rows_per_slab, part);
+  const bool vec = (ldx % 4 == 0) && ((uintptr_t)X % 16 == 0);
+  if (vec)
+    hipLaunchKernelGGL(gram_f64_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, s, X, ldx, P, N, W,
+                       (const int2*)pairs, npairs, rows_per_slab, part);
+  else
+    hipLaunchKernelGGL(gram_f64_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, s, X, ldx, P, N, W,
+                       (const int2*)pairs, npairs, rows_per_slab, part);
   return (int)hipGetLastError();
 }
 

@@ -11,8 +11,11 @@ from h2o3_amd.ops import linalg_ops  # noqa: E402
 
 N, P = int(os.environ.get("ROWS", 1_000_000)), int(os.environ.get("COLS", 711))
 g = torch.Generator(device="cuda").manual_seed(0)
-X = (torch.rand((N, P), generator=g, device="cuda") > 0.7).float()
+LD = int(os.environ.get("LDX", -(-P // 4) * 4))       # row pitch (16-byte rows: vector loads)
+Xs = (torch.rand((N, LD), generator=g, device="cuda") > 0.7).float()
+X = Xs[:, :P]
 W = torch.rand(N, generator=g, device="cuda", dtype=torch.float64)
+print(f"N={N} P={P} ldx={LD}")
 
 
 def torch_path():
