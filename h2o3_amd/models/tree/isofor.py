@@ -45,13 +45,24 @@ IF_DEFAULTS = dict(ntrees=50, max_depth=8, min_rows=1.0, max_runtime_secs=0.0, s
                    score_tree_interval=0)
 
 
+def _floyd_sample(n, k, rng):
+    """k distinct sorted indices of range(n) in O(k) draws (Floyd's
+    algorithm): RandomState.choice(replace=False) permutes all n rows per
+    tree (7 ms per tree at 1M rows)."""
+    chosen = set()
+    for j in range(n - k, n):
+        t = int(rng.randint(0, j + 1))
+        chosen.add(j if t in chosen else t)
+    return np.fromiter(sorted(chosen), dtype=np.int64, count=len(chosen))
+
+
 def _sample_rows(X, n, k, rng):
     """Gather k random rows (global) of X [F, n_local] to the host."""
     if cloud.is_distributed():
         ntot = int(coll.allreduce_scalar(n))
     else:
         ntot = n
-    idx = np.sort(rng.choice(ntot, size=min(k, ntot), replace=False))
+    idx = _floyd_sample(ntot, min(k, ntot), rng)
     if cloud.is_distributed():
         off = int(coll.all_gather_dim0(torch.tensor([n], device=X.device)).cumsum(0)[cloud.rank()].item()) - n
         loc = idx[(idx >= off) & (idx < off + n)] - off
