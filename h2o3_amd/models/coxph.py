@@ -74,21 +74,6 @@ def _cumsum0(x):
     return torch.cumsum(x, 0)
 
 
-def _tmm(A, B, chunk=4096):
-    """A.T @ B for tall [n, p], [n, q] with small p, q: the long inner
-    dimension split into chunks of one batched GEMM (a single [p, n] x [n, q]
-    GEMM with a 10 x 10 output runs on one workgroup: 40 ms at n = 500k)."""
-    n = A.shape[0]
-    if not A.is_cuda or n < 4 * chunk:
-        return A.T @ B
-    S = -(-n // chunk)
-    pad = S * chunk - n
-    if pad:
-        A = torch.cat([A, A.new_zeros((pad, A.shape[1]))])
-        B = torch.cat([B, B.new_zeros((pad, B.shape[1]))])
-    return torch.bmm(A.view(S, chunk, -1).transpose(1, 2), B.view(S, chunk, -1)).sum(0)
-
-
 class _Stratum:
     """Risk-set structure of one stratum, independent of beta: event times,
     each row's risk interval (jstart, jstop] in event-time indices, the
@@ -151,8 +136,8 @@ class _Stratum:
         a_ev[self.evm] = Cf[self.je]
         a = r * (a - a_ev)
         H1 = linalg_ops.weighted_gram(X.to(torch.float32), a.to(torch.float32)) if (
-            X.device.type == "cuda" and P % 32 == 0) else _tmm(X, X * a.view(-1, 1))
-        H2 = _tmm(R1l, R1l * (wl / (R0l * R0l)).view(-1, 1))
+            X.device.type == "cuda" and P % 32 == 0) else linalg_ops.tmm(X, X * a.view(-1, 1))
+        H2 = linalg_ops.tmm(R1l, R1l * (wl / (R0l * R0l)).view(-1, 1))
         return ll, grad, H1.to(X.dtype) - H2
 
 

@@ -19,6 +19,7 @@ import torch
 from ...parallel import collectives as coll
 from ..datainfo import DataInfo
 from ...core.groupsum import group_sum
+from ...ops import linalg_ops
 
 
 def _loss_grad_multinomial(X, Y, w, B, b0, wsum):
@@ -28,7 +29,7 @@ def _loss_grad_multinomial(X, Y, w, B, b0, wsum):
     ll = (w * (lse - (eta * Y).sum(1))).sum()
     P = torch.softmax(eta, 1)
     R = (P - Y) * w.view(-1, 1)
-    gB = (X.T @ R.to(X.dtype)).to(torch.float64)
+    gB = linalg_ops.tmm(X, R.to(X.dtype)).to(torch.float64)
     gb = R.sum(0)
     s = torch.cat([ll.view(1), gB.reshape(-1), gb])
     coll.allreduce_(s)

@@ -28,6 +28,7 @@ import torch
 from ...parallel import collectives as coll
 from ..datainfo import DataInfo
 from ...core.groupsum import index_add as _ia
+from ...ops import linalg_ops
 
 
 def fit_hglm(est, spec):
@@ -69,8 +70,8 @@ def fit_hglm(est, spec):
         off += L
     Q = off
     # sufficient statistics: X'WX, X'Wy, X'WZ, Z'WZ (diag + cross blocks), Z'Wy
-    XtX = X1.T @ (X1 * w.view(-1, 1))
-    Xty = X1.T @ (w * y)
+    XtX = linalg_ops.tmm(X1, X1 * w.view(-1, 1))
+    Xty = linalg_ops.tmm(X1, w * y)
     XtZ = torch.zeros((P, Q), dtype=torch.float64, device=X.device)
     ZtZ = torch.zeros((Q, Q), dtype=torch.float64, device=X.device)
     Zty = torch.zeros(Q, dtype=torch.float64, device=X.device)

@@ -30,6 +30,7 @@ from ..core.vec import T_ENUM, T_REAL, Vec
 from ..parallel import cloud
 from ..parallel import collectives as coll
 from .base import H2OEstimator
+from ..ops import linalg_ops
 
 GLRM_DEFAULTS = dict(k=1, loss="Quadratic", loss_by_col=None, loss_by_col_idx=None, multi_loss="Categorical",
                      period=1, regularization_x="None", regularization_y="None", gamma_x=0.0, gamma_y=0.0,
@@ -348,7 +349,7 @@ class H2OGeneralizedLowRankEstimator(H2OEstimator):
             gX = self._grad_u(A, M, X @ Y, blocks) @ Y.T
             Xn = _prox(rx, X - step * scale * gX, step * scale * gx)
             # Y update
-            gY = Xn.T @ self._grad_u(A, M, Xn @ Y, blocks)
+            gY = linalg_ops.tmm(Xn, self._grad_u(A, M, Xn @ Y, blocks))
             coll.allreduce_(gY)
             Yn = _prox(ry, Y - step * scale * gY, step * scale * gy)
             on = objective(Xn, Yn)

@@ -27,6 +27,7 @@ from ..parallel import cloud
 from ..parallel import collectives as coll
 from .base import H2OEstimator
 from .datainfo import DataInfo
+from ..ops import linalg_ops
 
 PSVM_DEFAULTS = dict(hyper_param=1.0, kernel_type="gaussian", gamma=-1.0, rank_ratio=-1.0, positive_weight=1.0,
                      negative_weight=1.0, disable_training_metrics=True, sv_threshold=1e-4, fact_threshold=1e-5,
@@ -81,7 +82,7 @@ def ipm(H, y, Cvec, mu_factor, feas_tol, gap_tol, max_iter):
         z = -rd + (mu / a - lam) - (mu / (Cvec - a) - xi)
         # M = Ht Ht' + diag(sig): SMW with p x p Cholesky
         Di = 1.0 / sig
-        Sm = eye + Ht.T @ (Ht * Di.view(-1, 1))
+        Sm = eye + linalg_ops.tmm(Ht, Ht * Di.view(-1, 1))
         Lc = torch.linalg.cholesky(Sm)
 
         def Minv(v):

@@ -655,3 +655,13 @@ def test_xv_xtr_f64_match_fp64(N, P, ldx):
     Xd = X[:, :P].double()
     torch.testing.assert_close(linalg_ops.xv_f64(X, P, b, 0.25), Xd @ b + 0.25, rtol=1e-12, atol=1e-12)
     torch.testing.assert_close(linalg_ops.xtr_f64(X, P, r), Xd.T @ r, rtol=1e-12, atol=1e-9)
+
+
+@pytest.mark.parametrize("n,p,q", [(100_003, 10, 3), (50_000, 7, 0), (30_000, 300, 2), (1000, 4, 4)])
+def test_tmm_matches_matmul(n, p, q):
+    from h2o3_amd.ops import linalg_ops
+    g = torch.Generator(device="cuda").manual_seed(n % 13)
+    A = torch.randn((n, p), generator=g, device="cuda", dtype=torch.float64)
+    B = torch.randn((n, q), generator=g, device="cuda", dtype=torch.float64) if q else \
+        torch.randn(n, generator=g, device="cuda", dtype=torch.float64)
+    torch.testing.assert_close(linalg_ops.tmm(A, B), A.T @ B, rtol=1e-10, atol=1e-9)
