@@ -362,11 +362,31 @@ class TreeGrower:
             key = elig.tobytes()
             if key not in el:
                 el.clear()
-                el[key] = torch.as_tensor(elig.astype(np.int64), device=self.dev)
+                el[key] = self._upload_elig(elig)
             return tree_ops.col_sample(n_nodes, el[key], k, seed)
         keys = self.rng.random_sample((n_nodes, len(elig)))
         sel = np.argpartition(keys, k - 1, axis=1)[:, :k]
         return torch.from_numpy(np.sort(elig[sel], axis=1))
+
+    def _upload_elig(self, elig):
+        """The eligible feature ids on the device without a host wait: a
+        pageable H2D copy waits for the queued kernels (the look-ahead
+        pipeline stalled once per tree, ~1 ms), so the ids go through a
+        persistent pinned buffer and a non-blocking copy; the buffer is reused
+        once the previous copy's event has completed."""
+        n = elig.size
+        pin = self.__dict__.get("_elig_pin")
+        if pin is None or pin.numel() < max(n, 1):
+            pin = self._elig_pin = torch.empty(max(n, 1, self.bd.F), dtype=torch.int64).pin_memory()
+            self._elig_evt = None
+        if self.__dict__.get("_elig_evt") is not None:
+            self._elig_evt.synchronize()
+        pin[:n].copy_(torch.from_numpy(elig.astype(np.int64)))
+        out = torch.empty(n, dtype=torch.int64, device=self.dev)
+        out.copy_(pin[:n], non_blocking=True)
+        ev = self._elig_evt = torch.cuda.Event()
+        ev.record()
+        return out
 
     def _col_mask_allowed(self, allow, depth):
         """Per-node mask under interaction constraints, on the device: the

@@ -39,4 +39,4 @@ pr.disable()
 print(f"train {time.time() - t0:.2f} s, trees {len(m._forest)}", flush=True)
 from h2o3_amd.utils import timer  # noqa: E402
 print("phases:", timer.report(), flush=True)
-pstats.Stats(pr).sort_stats("cumulative").print_stats(45)
+st = pstats.Stats(pr); st.sort_stats("cumulative").print_stats(45); st.print_callers("as_tensor|Event.synchronize|method .cpu.|method .item.")
