@@ -42,6 +42,7 @@ from __future__ import annotations
 
 import copy
 import math
+import os
 import time
 
 import numpy as np
@@ -492,23 +493,40 @@ class H2ODeepLearningEstimator(H2OEstimator):
                     perm = torch.randperm(n, generator=gen, device=X.device) if shuffle else \
                         torch.arange(n, device=X.device)
                     pos = 0
-                idx = perm[pos:pos + bs]
-                pos += bs
-                if graph is not None:
-                    # ONE graph launch per step: the batch gather, forward, backward,
-                    # updates and the dropout-seed advance were captured once
-                    graph["idx"].copy_(idx)
-                    graph["g"].replay()
+                S = graph.get("S", 1) if graph is not None else 1
+                nstep0 = nstep
+                if S > 1 and W_ == 1 and pos + S * bs <= n and \
+                        samples_done + (S - 1) * bs * contrib < min(next_iter, total_samples):
+                    # S steps in one replay (one GPU: no collective is paced by
+                    # the step count); no iteration boundary inside the group
+                    # -- its last step may end one, handled below as usual
+                    graph["idxm"].copy_(perm[pos:pos + S * bs].view(S, bs))
+                    graph["gm"].replay()
+                    pos += S * bs
+                    self._processed += S * bs * contrib
+                    samples_done += S * bs * contrib
+                    nstep += S
+                    final = samples_done >= total_samples
+                    idx = None
                 else:
-                    xb = X.index_select(0, idx)
-                    yb = None if Y is None else Y.index_select(0, idx)
-                    wb = None if w is None else w.index_select(0, idx)
-                    step_seed = (step_seed * 6364136223846793005 + 1442695040888963407) & ((1 << 63) - 1)
-                    self._train_step(xb, yb, wb, step_seed, hp, avg_act)
-                self._processed += bs * contrib
-                samples_done += bs * contrib
-                nstep += 1
-                final = samples_done >= total_samples
+                    idx = perm[pos:pos + bs]
+                    pos += bs
+                if idx is not None:
+                    if graph is not None:
+                        # ONE graph launch per step: the batch gather, forward, backward,
+                        # updates and the dropout-seed advance were captured once
+                        graph["idx"].copy_(idx)
+                        graph["g"].replay()
+                    else:
+                        xb = X.index_select(0, idx)
+                        yb = None if Y is None else Y.index_select(0, idx)
+                        wb = None if w is None else w.index_select(0, idx)
+                        step_seed = (step_seed * 6364136223846793005 + 1442695040888963407) & ((1 << 63) - 1)
+                        self._train_step(xb, yb, wb, step_seed, hp, avg_act)
+                    self._processed += bs * contrib
+                    samples_done += bs * contrib
+                    nstep += 1
+                    final = samples_done >= total_samples
                 if samples_done >= next_iter or final:
                     it += 1
                     t_comp = time.time() - iter_t0
@@ -562,7 +580,7 @@ class H2ODeepLearningEstimator(H2OEstimator):
                     iter_t0 = time.time()
                 # job progress / cancel and the max_runtime_secs clock, agreed across
                 # ranks every 64 mini-batches (not per step: a 0.14 ms step)
-                if nstep % 64 == 0 or final:
+                if nstep // 64 != nstep0 // 64 or final:
                     _, timed_out = self._tick(samples_done, total_samples, None, False, t0, max_rt)
                     if timed_out:
                         if contrib > 1 or single:
@@ -741,15 +759,16 @@ class H2ODeepLearningEstimator(H2OEstimator):
 
         kind = self._fused_kind(hp, avg_act)
 
-        def body():
+        def body(idx=None):
+            idx = gs["idx"] if idx is None else idx
             if kind is not None:
                 # the whole step in three kernels: gather + forward + backward,
                 # weight gradients, updates + seed advance
-                self._fused_step(X, gs["idx"], Y, w, 0, hp, kind, gs["seed"], True)
+                self._fused_step(X, idx, Y, w, 0, hp, kind, gs["seed"], True)
                 return
-            xb = X.index_select(0, gs["idx"])
-            yb = None if Y is None else Y.index_select(0, gs["idx"])
-            wb = None if w is None else w.index_select(0, gs["idx"])
+            xb = X.index_select(0, idx)
+            yb = None if Y is None else Y.index_select(0, idx)
+            wb = None if w is None else w.index_select(0, idx)
             dl_ops.seed_advance(gs["seed"])
             self._train_step(xb, yb, wb, 0, hp, avg_act, seed_dev=gs["seed"])
         cur = torch.cuda.current_stream()
@@ -771,6 +790,17 @@ class H2ODeepLearningEstimator(H2OEstimator):
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             body()
+        # S consecutive steps in one graph (their batches in one [S, bs] index
+        # buffer): a small net's step is ~10 us of GPU work and ~37 us of host
+        # time per replay + index copy, so single-step replays are launch bound
+        S = int(os.environ.get("H2O3_DL_GRAPH_STEPS", "8"))
+        if S > 1:
+            gs["idxm"] = torch.zeros((S, bs), dtype=torch.int64, device=dev)
+            gm = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gm):
+                for k in range(S):
+                    body(gs["idxm"][k])
+            gs["gm"], gs["S"] = gm, S
         for L, (Wb, bb, st) in zip(self._layers, saved):
             L.W.copy_(Wb)
             L.b.copy_(bb)

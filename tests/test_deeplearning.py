@@ -539,3 +539,23 @@ def test_dl_wide_layers_on_mfma_gemm(monkeypatch, case):
             # flip: allow a few per million
             bad = ((ta - tb).abs() > 2e-5 + 2e-4 * tb.abs()).sum().item()
             assert bad <= max(2, int(2e-5 * ta.numel())), (bad, ta.numel(), (ta - tb).abs().max().item())
+
+
+@pytest.mark.gpu
+def test_dl_multi_step_graph_matches_single_steps(monkeypatch):
+    """S steps captured in one graph (H2O3_DL_GRAPH_STEPS) train the model
+    that S single-step replays train: same batches, same dropout seeds."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    fr, x = _frame_cls(n=60000)
+    out = []
+    for S in ("1", "8"):
+        monkeypatch.setenv("H2O3_DL_GRAPH_STEPS", S)
+        m = H2ODeepLearningEstimator(hidden=[50], epochs=3, seed=1, activation="RectifierWithDropout",
+                                     hidden_dropout_ratios=[0.1], input_dropout_ratio=0.05)
+        m.train(x=x, y="y", training_frame=fr)
+        out.append(([L.W.detach().clone() for L in m._layers], m.logloss()))
+    for Wa, Wb in zip(out[0][0], out[1][0]):
+        torch.testing.assert_close(Wa, Wb, rtol=1e-5, atol=1e-6)
+    assert abs(out[0][1] - out[1][1]) < 1e-6
