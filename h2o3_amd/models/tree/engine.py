@@ -371,22 +371,10 @@ class TreeGrower:
     def _upload_elig(self, elig):
         """The eligible feature ids on the device without a host wait: a
         pageable H2D copy waits for the queued kernels (the look-ahead
-        pipeline stalled once per tree, ~1 ms), so the ids go through a
-        persistent pinned buffer and a non-blocking copy; the buffer is reused
-        once the previous copy's event has completed."""
-        n = elig.size
-        pin = self.__dict__.get("_elig_pin")
-        if pin is None or pin.numel() < max(n, 1):
-            pin = self._elig_pin = torch.empty(max(n, 1, self.bd.F), dtype=torch.int64).pin_memory()
-            self._elig_evt = None
-        if self.__dict__.get("_elig_evt") is not None:
-            self._elig_evt.synchronize()
-        pin[:n].copy_(torch.from_numpy(elig.astype(np.int64)))
-        out = torch.empty(n, dtype=torch.int64, device=self.dev)
-        out.copy_(pin[:n], non_blocking=True)
-        ev = self._elig_evt = torch.cuda.Event()
-        ev.record()
-        return out
+        pipeline stalled once per tree, ~1 ms), so the ids go through the
+        pinned upload ring (non-blocking) and a stream-ordered device copy
+        that outlives the ring slot (the ids are cached for the tree)."""
+        return tree_ops._h2d(elig.astype(np.int64), self.dev).clone()
 
     def _col_mask_allowed(self, allow, depth):
         """Per-node mask under interaction constraints, on the device: the

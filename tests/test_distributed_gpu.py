@@ -45,7 +45,8 @@ def _run(world, out):
             o, _ = p.communicate()
         outs.append(o.decode(errors="replace"))
     for p, o in zip(procs, outs):
-        assert p.returncode == 0, o[-3000:]
+        # the head holds the Python traceback / error line, the tail the exit
+        assert p.returncode == 0, o[:6000] + "\n...\n" + o[-2000:]
     with open(out) as f:
         return json.load(f)
 
