@@ -53,6 +53,7 @@ from ..core.vec import T_REAL, Vec
 from ..ops import dl_ops
 from ..parallel import cloud
 from ..parallel import collectives as coll
+from ..utils import graphs
 from . import metrics as mm
 from .base import H2OEstimator, ScoreKeeper, _LESS_IS_BETTER
 from .datainfo import DataInfo
@@ -788,7 +789,7 @@ class H2ODeepLearningEstimator(H2OEstimator):
                 body()
         cur.wait_stream(side)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with graphs.capture(g):
             body()
         # S consecutive steps in one graph (their batches in one [S, bs] index
         # buffer): a small net's step is ~10 us of GPU work and ~37 us of host
@@ -797,7 +798,7 @@ class H2ODeepLearningEstimator(H2OEstimator):
         if S > 1:
             gs["idxm"] = torch.zeros((S, bs), dtype=torch.int64, device=dev)
             gm = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(gm):
+            with graphs.capture(gm):
                 for k in range(S):
                     body(gs["idxm"][k])
             gs["gm"], gs["S"] = gm, S

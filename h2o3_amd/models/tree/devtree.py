@@ -51,6 +51,7 @@ from ...ops import tree_ops
 from ...ops.tree_ops import _ptr, _stream
 from ...parallel import cloud
 from ...parallel import collectives as coll
+from ...utils import graphs
 from .engine import _TreeBuf
 
 RS = 16
@@ -466,7 +467,7 @@ class DevTreeGBM:
                 self._sequence()
                 torch.cuda.synchronize()
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
+                with graphs.capture(g):
                     self._sequence()
                 self.graph = g
             else:
