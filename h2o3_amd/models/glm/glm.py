@@ -1349,18 +1349,28 @@ class H2OGeneralizedLinearEstimator(H2OEstimator):
         self._dinfo = drv.dinfo
         self._fam = drv.fam
         self._finalize_outputs(drv, sm)
+        self._dev_x_cache = {}
         drv.X = None
 
     def _dev_on(self, frame, sm, drv):
-        X, ok = drv.dinfo.expand(frame)
+        # the frame's model matrix, response and row mask are built once per
+        # fit (a lambda search evaluates every submodel on the validation
+        # frame: re-expanding it per lambda was most of an AutoML GLM step)
+        cache = self.__dict__.setdefault("_dev_x_cache", {})
+        ent = cache.get(id(frame))
+        if ent is None or ent[0] is not frame or ent[1] is not drv:
+            cache.clear()
+            X, ok = drv.dinfo.expand(frame)
+            y = self._spec.y_tensor(frame)
+            yy = (y == 1).to(torch.float64) if self._spec.is_classification else y.to(torch.float64)
+            m = ok & (~torch.isnan(yy) if not self._spec.is_classification else (y >= 0))
+            ent = cache[id(frame)] = (frame, drv, X, yy[m], m)
+        _, _, X, ym, m = ent
         bt = torch.zeros(drv.Pp, dtype=torch.float32, device=X.device)
         bt[: drv.P] = torch.as_tensor(sm["beta_std"][: drv.P], dtype=torch.float32)
         eta = (X @ bt).to(torch.float64) + sm["beta_std"][-1]
         mu = drv.fam.linkinv(eta)
-        y = self._spec.y_tensor(frame)
-        yy = (y == 1).to(torch.float64) if self._spec.is_classification else y.to(torch.float64)
-        m = ok & (~torch.isnan(yy) if not self._spec.is_classification else (y >= 0))
-        return coll.allreduce_scalar(float(drv.fam.deviance(yy[m], mu[m]).sum()))
+        return coll.allreduce_scalar(float(drv.fam.deviance(ym, mu[m]).sum()))
 
     def _null_deviance_on(self, frame, drv):
         """Deviance of the intercept-only (training mean) model on `frame`."""
