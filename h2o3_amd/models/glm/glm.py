@@ -165,6 +165,13 @@ def _soft(x, t):
 _CD = []
 
 
+def _narrow_max():
+    """Widest padded design on the narrow fused IRLS kernel (32-wide tile
+    pairs, one pass); wider designs take the wide path (eta pass + 256-tile
+    MFMA Gram)."""
+    return int(os.environ.get("H2O3_GLM_NARROW_MAX", "512"))
+
+
 def _native_cd():
     """C++ coordinate descent (h2o3_amd/native/glm_solver.cpp), None if unbuilt."""
     if not _CD:
@@ -507,7 +514,7 @@ class GLMDriver:
         """Family codes when the wide fused eta kernel applies (the wide IRLS
         path of _irls_stats), else None."""
         codes = linalg_ops.glm_fused_codes(self.fam.family, self.fam.link, self.fam.tlp)
-        if self.X.device.type == "cuda" and self.Pp > 512 and self.P + 2 <= 1024 and codes is not None and \
+        if self.X.device.type == "cuda" and self.Pp > _narrow_max() and self.P + 2 <= 1024 and codes is not None and \
                 linalg_ops._wide_mode() == "bf3" and linalg_ops.wide_fused_enabled():
             if not hasattr(self, "_y32"):
                 self._y32 = self.y.to(torch.float32)
@@ -556,7 +563,7 @@ class GLMDriver:
 
     def _native(self):
         return self.X.device.type == "cuda" and self.X.dtype == torch.float32 and self.Pp % 32 == 0 and \
-            self.Pp <= 512 and self.Pp >= self.P + 2
+            self.Pp <= _narrow_max() and self.Pp >= self.P + 2
 
     def _irls_stats_native(self):
         """One fused kernel pass: eta, IRLS weights, deviance, augmented Gram."""
@@ -781,7 +788,7 @@ class GLMDriver:
             G, xz, xw, sw, swz, dev = self._irls_stats_native()
             return self._finish_stats(G, xz, xw, sw, swz, dev)
         codes = linalg_ops.glm_fused_codes(self.fam.family, self.fam.link, self.fam.tlp)
-        if self.X.device.type == "cuda" and self.Pp > 512 and self.P + 2 <= 1024 and codes is not None and \
+        if self.X.device.type == "cuda" and self.Pp > _narrow_max() and self.P + 2 <= 1024 and codes is not None and \
                 linalg_ops._wide_mode() == "bf3":
             # one fused pass: eta + family + bf16 hi/lo split, then one bf16 GEMM
             with phase("glm.wide_pass"):
@@ -821,7 +828,7 @@ class GLMDriver:
                 W = self.w
                 z = self.y - off
             Wf = W.to(torch.float32)
-        if self.X.device.type == "cuda" and self.Pp > 512 and bool((W >= 0).all()):
+        if self.X.device.type == "cuda" and self.Pp > _narrow_max() and bool((W >= 0).all()):
             with phase("glm.gram"):
                 G, xw, xz, sw, swz = linalg_ops.weighted_gram_aug(self.X, W, z, self.P)
                 dev = (self.w * self.fam.deviance(self.y, mu)).sum().view(1)

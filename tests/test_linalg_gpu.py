@@ -375,8 +375,9 @@ def test_glm_gaussian_reduced_tier_refines_to_fp64(monkeypatch):
     assert err < 1e-6, err
 
 
-@pytest.mark.parametrize("noise,tier", [(None, "bf16"), (0.1, "bf3"), (2e-2, "f64")])
-def test_glm_wide_tiers_match_fp64(monkeypatch, noise, tier):
+@pytest.mark.parametrize("noise,tier,P", [(None, "bf16", 600), (0.1, "bf3", 600), (2e-2, "f64", 600),
+                                          (None, "bf16", 200), (0.1, "bf3", 200)])
+def test_glm_wide_tiers_match_fp64(monkeypatch, noise, tier, P):
     """Wide design (P = 600: the fused wide pass -- eta kernel + hand-written
     Gram): a well-conditioned design runs on the one-MFMA bf16 Hessian
     (kappa < 32), a correlated pair (kappa ~ 400) on bf16x3, a
@@ -384,7 +385,10 @@ def test_glm_wide_tiers_match_fp64(monkeypatch, noise, tier):
     tier).  Every tier lands on the fp64 IRLS solution."""
     import numpy as np
     g = np.random.default_rng(8)
-    n, P = 120_000, 600
+    n = 120_000
+    if P < 512:
+        # a mid-width design forced onto the wide path
+        monkeypatch.setenv("H2O3_GLM_NARROW_MAX", "128")
     Xh = g.standard_normal((n, P)).astype(np.float32)
     if noise is not None:
         Xh[:, 1] = Xh[:, 0] + noise * g.standard_normal(n).astype(np.float32)
