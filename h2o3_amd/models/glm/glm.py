@@ -168,8 +168,10 @@ _CD = []
 def _narrow_max():
     """Widest padded design on the narrow fused IRLS kernel (32-wide tile
     pairs, one pass); wider designs take the wide path (eta pass + 256-tile
-    MFMA Gram)."""
-    return int(os.environ.get("H2O3_GLM_NARROW_MAX", "512"))
+    bf16 MFMA Gram).  128: at 10M x 200 (AutoML's GLM step without CV) the
+    wide path trains in 2.1 s against 11.4 s on the 32-wide tile pairs, with
+    the same tiers and fp64-level coefficients (profiles/glm_f64_r6/)."""
+    return int(os.environ.get("H2O3_GLM_NARROW_MAX", "128"))
 
 
 def _native_cd():
